@@ -1,0 +1,102 @@
+"""ctypes binding of liborbslam_gpu.so (the C ABI in include/orbslam_gpu.h).
+
+The product path is the HIP library: if it is missing or no GPU is usable the
+calls fail loudly (ORB_E_NODEVICE / ImportError) -- there is no CPU fallback.
+"""
+import ctypes as C
+import os
+import re
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+LIB_PATH = PKG / "liborbslam_gpu.so"
+HEADER = ROOT / "include" / "orbslam_gpu.h"
+
+ORB_OK, ORB_E_INVALID, ORB_E_HIP, ORB_E_CAPACITY, ORB_E_NODEVICE = 0, -1, -2, -3, -4
+_ERR = {ORB_E_INVALID: "ORB_E_INVALID", ORB_E_HIP: "ORB_E_HIP", ORB_E_CAPACITY: "ORB_E_CAPACITY",
+        ORB_E_NODEVICE: "ORB_E_NODEVICE"}
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KP_DTYPE.itemsize == 28
+
+
+class OrbGpuError(RuntimeError):
+    def __init__(self, code, what=""):
+        super().__init__(f"{what}: {_ERR.get(code, code)}")
+        self.code = code
+
+
+def check(rc, what=""):
+    if rc != ORB_OK:
+        raise OrbGpuError(rc, what)
+    return rc
+
+
+class orb_frame(C.Structure):
+    _fields_ = [("N", C.c_int), ("keysUn", C.c_void_p), ("desc", C.c_void_p), ("uRight", C.c_void_p),
+                ("minX", C.c_float), ("maxX", C.c_float), ("minY", C.c_float), ("maxY", C.c_float),
+                ("gridWInv", C.c_float), ("gridHInv", C.c_float), ("scaleFactors", C.c_void_p),
+                ("nlevels", C.c_int), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float),
+                ("cy", C.c_float), ("bf", C.c_float), ("b", C.c_float), ("Tcw", C.c_void_p)]
+
+
+class orb_mappoints(C.Structure):
+    _fields_ = [("n", C.c_int), ("pos", C.c_void_p), ("desc", C.c_void_p), ("observations", C.c_void_p)]
+
+
+def header_functions(path=HEADER):
+    """Names of every function the public header declares."""
+    txt = re.sub(r"/\*.*?\*/", "", Path(path).read_text(), flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\(", txt, flags=re.M))
+                  - {"if", "while", "for", "return", "sizeof"})
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(str(LIB_PATH))
+    vp, i32, f32, sz = C.c_void_p, C.c_int, C.c_float, C.c_size_t
+    P = C.POINTER
+    L.orbgpu_version.restype = C.c_char_p
+    L.ORBextractor_create.argtypes = [i32, f32, i32, i32, i32, i32, i32, i32, P(vp)]
+    L.ORBextractor_destroy.argtypes = [vp]
+    L.ORBextractor_extract.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, P(i32)]
+    L.ORBextractor_extract_batch.argtypes = [vp, vp, i32, i32, i32, i32, sz, i32, vp, vp, i32, i32, vp]
+    L.ORBextractor_get_level.argtypes = [vp, i32, i32, vp, i32, P(i32), P(i32)]
+    L.ORBextractor_get_levels.argtypes = [vp, P(i32), P(f32)]
+    L.ORBextractor_get_scale_tables.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.ORBextractor_stream.restype = vp
+    L.ORBextractor_stream.argtypes = [vp]
+    L.ORBextractor_last_timings.argtypes = [vp, vp]
+    L.ORBmatcher_create.argtypes = [f32, i32, P(vp)]
+    L.ORBmatcher_destroy.argtypes = [vp]
+    L.ORBmatcher_set_device_pointers.argtypes = [vp, i32]
+    L.ORBmatcher_stream.restype = vp
+    L.ORBmatcher_stream.argtypes = [vp]
+    L.ORBmatcher_DescriptorDistance.argtypes = [vp, vp]
+    L.ORBmatcher_SearchByProjection_LastFrame.argtypes = [vp, P(orb_frame), vp, P(orb_frame), vp, vp, vp,
+                                                          P(orb_mappoints), f32, i32, P(i32)]
+    L.ORBmatcher_SearchByProjection_LastFrame_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, f32, i32, vp]
+    L.ORBmatcher_SearchByProjection_MapPoints.argtypes = [vp, P(orb_frame), vp, i32, vp, vp, vp, vp, vp, vp, vp,
+                                                          P(orb_mappoints), f32, P(i32)]
+    L.ORBmatcher_SearchCandidates.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp]
+    _lib = L
+    return L
+
+
+def ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def device_available():
+    return bool(lib().orbgpu_device_available())

@@ -1,0 +1,126 @@
+// orb_common.hpp -- shared HIP helpers for the gfx950 ORB-SLAM2 hot path.
+//
+// Every kernel is compiled with -ffp-contract=off and correctly rounded f32
+// division so float expressions evaluate exactly as the reference's scalar C++
+// (SURVEY.md F8).  Device math that must match host libm/OpenCV bit-for-bit
+// (cvRound, fastAtan2, glibc sinf/cosf) is restated here explicitly.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+
+#define ORB_HIP_CHECK(expr)                                                            \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess) {                                                        \
+            fprintf(stderr, "[orbslam_gpu] HIP error %s at %s:%d: %s\n",               \
+                    hipGetErrorName(_e), __FILE__, __LINE__, #expr);                   \
+            return -2;                                                                 \
+        }                                                                              \
+    } while (0)
+
+namespace orbgpu {
+
+constexpr int kEdge = 19;          // EDGE_THRESHOLD, ORBextractor.cc:67
+constexpr int kPatch = 31;         // PATCH_SIZE, ORBextractor.cc:65
+constexpr int kHalfPatch = 15;     // HALF_PATCH_SIZE, ORBextractor.cc:66
+
+// cvRound(float) == lrintf: round half to even.
+__device__ __forceinline__ int cv_round(float v) { return __float2int_rn(v); }
+
+// OpenCV 3.2 fastAtan2 (core/mathfuncs.cpp), degrees in [0, 360).
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float k180 = (float)(180.0 / 3.14159265358979323846);
+    const float p1 = 0.9997878412794807f * k180;
+    const float p3 = -0.3258083974640975f * k180;
+    const float p5 = 0.1555786518463281f * k180;
+    const float p7 = -0.04432655554792128f * k180;
+    const float eps = (float)2.220446049250313e-16;
+    float ax = fabsf(x), ay = fabsf(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// glibc 2.35 sinf/cosf restated in f64 (|x| < 120).  The reference computes
+// `(float)cos(angle)` with std::cos(float) == glibc cosf (ORBextractor.cc:112);
+// the restatement is exhaustively equal to host libm on [0, 2*pi].
+struct SinCosTab {
+    double sign[4], hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
+};
+__device__ __forceinline__ const SinCosTab& sincos_tab(int i) {
+    static constexpr SinCosTab T[2] = {
+        {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0,
+         -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16,
+         -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
+        {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0,
+         0x1.ffffffd0c621cp-2, -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16,
+         -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13}};
+    return T[i];
+}
+
+__device__ __forceinline__ float sincos_poly(double x, double x2, const SinCosTab& p, int n) {
+    if ((n & 1) == 0) {
+        double x3 = x * x2;
+        double s1 = p.s2 + x2 * p.s3;
+        double x7 = x3 * x2;
+        double s = x + x3 * p.s1;
+        return (float)(s + x7 * s1);
+    }
+    double x4 = x2 * x2;
+    double c2 = p.c3 + x2 * p.c4;
+    double c1 = p.c0 + x2 * p.c1;
+    double x6 = x4 * x2;
+    double c = c1 + x4 * p.c2;
+    return (float)(c + x6 * c2);
+}
+
+__device__ __forceinline__ uint32_t top12(float f) { return (__float_as_uint(f) >> 20) & 0x7ff; }
+
+// Returns (sin, cos) of y exactly as glibc sinf(y), cosf(y).
+__device__ __forceinline__ void glibc_sincosf(float y, float* s_out, float* c_out) {
+    const uint32_t t = top12(y);
+    if (t < top12(0x1.921FB6p-1f)) {
+        double x = y, x2 = x * x;
+        if (t < top12(0x1p-12f)) {
+            *s_out = y;
+            *c_out = 1.0f;
+            return;
+        }
+        *s_out = sincos_poly(x, x2, sincos_tab(0), 0);
+        *c_out = sincos_poly(x, x2, sincos_tab(0), 1);
+        return;
+    }
+    double x = y;
+    const SinCosTab& p0 = sincos_tab(0);
+    double r = x * p0.hpi_inv;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    x = x - n * p0.hpi;
+    double s = p0.sign[n & 3];
+    const SinCosTab& p = (n & 2) ? sincos_tab(1) : p0;
+    *s_out = sincos_poly(x * s, x * x, p, n);
+    *c_out = sincos_poly(x * s, x * x, p, n ^ 1);
+}
+
+__device__ __forceinline__ int refl101(int p, int len) {
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
+    return p;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace orbgpu

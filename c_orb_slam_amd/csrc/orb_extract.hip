@@ -1,0 +1,895 @@
+// orb_extract.hip -- MI355X (gfx950) ORB extraction: the device side of
+// ORBextractor::operator() (reference src/ORBextractor.cc:1043-1105).
+//
+// Pipeline per batch of B equal-size u8 images (all device-resident):
+//   k_pyr_level0   copyMakeBorder(REFLECT_101, 19 px)            ORBextractor.cc:1126-1128
+//   k_pyr_resize   resize(INTER_LINEAR, 8U fixed point) + border  ORBextractor.cc:1118-1123
+//   k_blur7        GaussianBlur 7x7 sigma 2 (8-bit fixed point)    ORBextractor.cc:1085-1086
+//   k_fast_cells   per-cell FAST(th=20) / FAST(th=7) + NMS, LDS-staged ROI,
+//                  raster-order compaction                        ORBextractor.cc:776-829
+//   k_compact      per-image, per-level candidate lists (cell order)
+//   host           DistributeOctTree (order-defining)             ORBextractor.cc:539-763
+//   k_orient_desc  IC_Angle + rotated BRIEF, one wave per keypoint ORBextractor.cc:77-147
+//
+// HBM layout: per image, the padded levels (pitch = align16(w+38)) are
+// concatenated; the blurred levels use the identical geometry in a second
+// buffer.  Cells of all levels are one flat launch (grid = cells x images).
+#include "orb_extract.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+namespace orbgpu {
+
+// ---------------------------------------------------------------- constants
+__constant__ int8_t c_pattern[256 * 4];     // rBRIEF pairs (x0,y0,x1,y1)
+__constant__ int8_t c_disc[2 * 1024];       // IC_Angle disc offsets (u, v)
+__constant__ int c_ndisc;
+__constant__ int c_gauss[7];
+
+static const int8_t kPattern[256 * 4] = {
+#include "brief_pattern.inc"
+};
+
+// ------------------------------------------------------------------ kernels
+// copyMakeBorder(image, temp, 19,19,19,19, BORDER_REFLECT_101), 4 bytes/thread.
+__global__ void k_pyr_level0(const uint8_t* __restrict__ src, size_t src_stride, int step, int W,
+                             int H, uint8_t* __restrict__ pyr, size_t img_bytes, int pitch, int ph) {
+    const int b = blockIdx.y;
+    const int quads = pitch >> 2;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= quads * ph) return;
+    const int py = t / quads, px4 = (t - py * quads) * 4;
+    const int sy = refl101(py - kEdge, H);
+    const uint8_t* srow = src + (size_t)b * src_stride + (size_t)sy * step;
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int px = px4 + k;
+        const int sx = refl101(px - kEdge, W);
+        v |= (uint32_t)srow[sx] << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(pyr + (size_t)b * img_bytes + (size_t)py * pitch + px4) = v;
+}
+
+// resize(prev level, INTER_LINEAR) for CV_8U (OpenCV 3.2 imgwarp.cpp fixed
+// point: 11-bit coefficients, VResizeLinear<uchar,int,short,FixedPtCast>),
+// written straight into the padded level through the REFLECT_101 map.
+__global__ void k_pyr_resize(uint8_t* __restrict__ pyr, size_t img_bytes, size_t src_off,
+                             int src_pitch, size_t dst_off, int dst_pitch, int dst_ph, int w, int h,
+                             const int* __restrict__ xofs, const short2* __restrict__ xalpha,
+                             const int2* __restrict__ yrows, const short2* __restrict__ ybeta) {
+    const int b = blockIdx.y;
+    const int quads = dst_pitch >> 2;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= quads * dst_ph) return;
+    const int py = t / quads, px4 = (t - py * quads) * 4;
+    uint8_t* base = pyr + (size_t)b * img_bytes;
+    const uint8_t* S = base + src_off + (size_t)kEdge * src_pitch + kEdge;  // prev interior
+    const int y = refl101(py - kEdge, h);
+    const int2 rr = yrows[y];
+    const short2 bb = ybeta[y];
+    const uint8_t* S0 = S + (size_t)rr.x * src_pitch;
+    const uint8_t* S1 = S + (size_t)rr.y * src_pitch;
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int x = refl101(px4 + k - kEdge, w);
+        const int sx = xofs[x];
+        const short2 a = xalpha[x];
+        const int D0 = S0[sx] * a.x + S0[sx + (a.y != 0)] * a.y;
+        const int D1 = S1[sx] * a.x + S1[sx + (a.y != 0)] * a.y;
+        const int o = (((bb.x * (D0 >> 4)) >> 16) + ((bb.y * (D1 >> 4)) >> 16) + 2) >> 2;
+        v |= (uint32_t)(uint8_t)o << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(base + dst_off + (size_t)py * dst_pitch + px4) = v;
+}
+
+// GaussianBlur(7x7, sigma 2, REFLECT_101) on CV_8U: int taps (round(k*256)),
+// int row pass, int column pass, (v + 2^15) >> 16, saturate.  The padded
+// level's 19-px REFLECT_101 border supplies the filter border.  Tile 64x16.
+constexpr int BT_W = 64, BT_H = 16;
+__global__ void __launch_bounds__(256) k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                               size_t img_bytes, const BlurTile* __restrict__ tiles) {
+    __shared__ uint8_t s_src[BT_H + 6][BT_W + 8];
+    __shared__ int s_row[BT_H + 6][BT_W + 1];
+    const BlurTile tl = tiles[blockIdx.x];
+    const int b = blockIdx.y;
+    const uint8_t* P = pyr + (size_t)b * img_bytes + tl.off + (size_t)kEdge * tl.pitch + kEdge;
+    uint8_t* O = blur + (size_t)b * img_bytes + tl.off + (size_t)kEdge * tl.pitch + kEdge;
+    const int x0 = tl.tx * BT_W, y0 = tl.ty * BT_H;
+    for (int i = threadIdx.x; i < (BT_H + 6) * (BT_W + 6); i += 256) {
+        const int r = i / (BT_W + 6), c = i - r * (BT_W + 6);
+        int yy = y0 + r - 3, xx = x0 + c - 3;
+        // clamp into the padded area; such pixels only feed outputs outside the level
+        yy = min(yy, tl.h + 2);
+        xx = min(xx, tl.w + 2);
+        s_src[r][c] = P[(ptrdiff_t)yy * tl.pitch + xx];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (BT_H + 6) * BT_W; i += 256) {
+        const int r = i / BT_W, c = i - r * BT_W;
+        int s = 0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) s += c_gauss[k] * s_src[r][c + k];
+        s_row[r][c] = s;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < BT_H * BT_W; i += 256) {
+        const int r = i / BT_W, c = i - r * BT_W;
+        const int y = y0 + r, x = x0 + c;
+        if (y >= tl.h || x >= tl.w) continue;
+        int s = 0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) s += c_gauss[k] * s_row[r + k][c];
+        const int v = (s + (1 << 15)) >> 16;
+        O[(size_t)y * tl.pitch + x] = (uint8_t)min(max(v, 0), 255);
+    }
+}
+
+// FAST-9/16 score S = max(A,B)-1 (OpenCV cornerScore<16>): A/B = best
+// contiguous-9 dark/bright contrast.  A pixel is a corner at threshold t
+// iff S >= t, and its stored score is then S (see oracle/ocv_semantics.c).
+__device__ __forceinline__ int fast_score_lds(const uint8_t* p, int ld) {
+    const int v = p[0];
+    int d[16];
+    d[0] = v - p[3 * ld];       d[1] = v - p[3 * ld + 1];   d[2] = v - p[2 * ld + 2];
+    d[3] = v - p[ld + 3];       d[4] = v - p[3];            d[5] = v - p[-ld + 3];
+    d[6] = v - p[-2 * ld + 2];  d[7] = v - p[-3 * ld + 1];  d[8] = v - p[-3 * ld];
+    d[9] = v - p[-3 * ld - 1];  d[10] = v - p[-2 * ld - 2]; d[11] = v - p[-ld - 3];
+    d[12] = v - p[-3];          d[13] = v - p[ld - 3];      d[14] = v - p[2 * ld - 2];
+    d[15] = v - p[3 * ld - 1];
+    int mn2[16], mx2[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn2[k] = min(d[k], d[(k + 1) & 15]);
+        mx2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int A = -1000, B = -1000;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        // arc k..k+8 = pairs (k,k+1),(k+2,k+3),(k+4,k+5),(k+6,k+7) + element k+8
+        const int mn = min(min(min(mn2[k], mn2[(k + 2) & 15]), min(mn2[(k + 4) & 15], mn2[(k + 6) & 15])), d[(k + 8) & 15]);
+        const int mx = max(max(max(mx2[k], mx2[(k + 2) & 15]), max(mx2[(k + 4) & 15], mx2[(k + 6) & 15])), d[(k + 8) & 15]);
+        A = max(A, mn);
+        B = max(B, -mx);
+    }
+    return max(A, B) - 1;
+}
+
+constexpr int FC_LD = 72;      // LDS row pitch of the cell ROI
+constexpr int FC_MAXR = 70;    // max ROI rows/cols supported (wCell/hCell <= 64)
+
+__global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ pyr, size_t img_bytes,
+                                                    const CellDesc* __restrict__ cells, int iniTh, int minTh,
+                                                    uint32_t* __restrict__ slots, size_t slots_per_image,
+                                                    int* __restrict__ counts, int ncells) {
+    __shared__ uint8_t s_img[FC_MAXR * FC_LD];
+    __shared__ uint8_t s_sc[FC_MAXR * FC_LD];
+    __shared__ int s_wave[4];
+    const CellDesc cd = cells[blockIdx.x];
+    const int b = blockIdx.y;
+    const int rows = cd.r1 - cd.r0, cols = cd.c1 - cd.c0;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    int* cnt_out = counts + (size_t)b * ncells + blockIdx.x;
+    if (rows < 7 || cols < 7) {
+        if (tid == 0) *cnt_out = 0;
+        return;
+    }
+    const uint8_t* P = pyr + (size_t)b * img_bytes + cd.lvl_off + (size_t)(kEdge + cd.r0) * cd.pitch + kEdge + cd.c0;
+    for (int i = tid; i < rows * cols; i += 256) {
+        const int r = i / cols, c = i - r * cols;
+        s_img[r * FC_LD + c] = P[(size_t)r * cd.pitch + c];
+        s_sc[r * FC_LD + c] = 0;
+    }
+    __syncthreads();
+    const int dr = rows - 6, dc = cols - 6, nd = dr * dc;
+    for (int i = tid; i < nd; i += 256) {
+        const int r = 3 + i / dc, c = 3 + i % dc;
+        const int s = fast_score_lds(&s_img[r * FC_LD + c], FC_LD);
+        s_sc[r * FC_LD + c] = (uint8_t)max(s, 0);
+    }
+    __syncthreads();
+    uint32_t* out = slots + (size_t)b * slots_per_image + cd.slot_off;
+    int th = iniTh;
+    for (int pass = 0; pass < 2; pass++) {
+        int base = 0;
+        for (int c0 = 0; c0 < nd; c0 += 256) {
+            const int i = c0 + tid;
+            bool keep = false;
+            int s = 0, r = 0, c = 0;
+            if (i < nd) {
+                r = 3 + i / dc;
+                c = 3 + i % dc;
+                s = s_sc[r * FC_LD + c];
+                if (s >= th) {
+                    keep = true;
+#pragma unroll
+                    for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; dx++) {
+                            if (!dx && !dy) continue;
+                            int n = s_sc[(r + dy) * FC_LD + c + dx];
+                            n = n >= th ? n : 0;
+                            keep = keep && (s > n);
+                        }
+                }
+            }
+            const uint64_t m = __ballot(keep);
+            const int wcount = __popcll(m);
+            if (lane == 0) s_wave[wid] = wcount;
+            __syncthreads();
+            int woff = 0;
+            for (int w = 0; w < wid; w++) woff += s_wave[w];
+            const int total = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+            if (keep) {
+                const int rank = __popcll(m & ((1ull << lane) - 1ull));
+                const int pos = base + woff + rank;
+                if (pos < cd.cap) {
+                    const uint32_t xr = (uint32_t)(c + cd.offx), yr = (uint32_t)(r + cd.offy);
+                    out[pos] = ((uint32_t)s << 24) | (yr << 12) | xr;
+                }
+            }
+            base += total;
+            __syncthreads();
+        }
+        if (base > 0 || pass == 1) {
+            if (tid == 0) *cnt_out = min(base, cd.cap);
+            break;
+        }
+        th = minTh;
+    }
+}
+
+// Per image: concatenate the cell outputs of every level in cell order
+// (= the reference's vToDistributeKeys order) into one packed list.
+// Header per image: [total][cnt_l0..cnt_lL-1][base] in hdr.
+__global__ void __launch_bounds__(1024) k_compact(const uint32_t* __restrict__ slots, size_t slots_per_image,
+                                                  const int* __restrict__ counts, const CellDesc* __restrict__ cells,
+                                                  int ncells, const int* __restrict__ level_cell_begin, int nlevels,
+                                                  uint32_t* __restrict__ packed, int* __restrict__ hdr,
+                                                  int* __restrict__ g_total, int packed_cap) {
+    __shared__ int s_off[4096 + 1];
+    __shared__ int s_base;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int* cnt = counts + (size_t)b * ncells;
+    // exclusive scan of counts over cells (ncells <= 4096): 4 per thread + wave scans
+    __shared__ int s_wsum[16];
+    int v[4], loc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int i = tid * 4 + k;
+        v[k] = i < ncells ? cnt[i] : 0;
+        loc += v[k];
+    }
+    const int lane0 = tid & 63, w0 = tid >> 6;
+    int incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane0 >= o) incl += y;
+    }
+    if (lane0 == 63) s_wsum[w0] = incl;
+    __syncthreads();
+    int wpre = 0;
+    for (int w = 0; w < w0; w++) wpre += s_wsum[w];
+    int run = wpre + incl - loc;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int i = tid * 4 + k;
+        if (i < ncells) s_off[i] = run;
+        run += v[k];
+    }
+    if (tid == 1023) s_off[ncells] = run;  // total (tid 1023 holds the block total)
+    __syncthreads();
+    if (tid == 0) {
+        const int total = s_off[ncells];
+        int base = atomicAdd(g_total, total);
+        if (base + total > packed_cap) base = -1;
+        s_base = base;
+        int* H = hdr + (size_t)b * (nlevels + 2);
+        H[0] = total;
+        for (int l = 0; l < nlevels; l++) H[1 + l] = s_off[level_cell_begin[l + 1]] - s_off[level_cell_begin[l]];
+        H[nlevels + 1] = base;
+    }
+    __syncthreads();
+    const int base = s_base;
+    if (base < 0) return;
+    const uint32_t* S = slots + (size_t)b * slots_per_image;
+    // one wave per cell
+    const int lane = tid & 63, wid = tid >> 6;
+    for (int c = wid; c < ncells; c += 16) {
+        const int n = s_off[c + 1] - s_off[c];
+        const uint32_t* src = S + cells[c].slot_off;
+        uint32_t* dst = packed + base + s_off[c];
+        for (int k = lane; k < n; k += 64) dst[k] = src[k];
+    }
+}
+
+// IC_Angle (unblurred level) + rotated BRIEF (blurred level), one wave per
+// keypoint.  Moments are exact integer sums (order-free); the 256 tests of
+// lane l are pairs l, l+64, l+128, l+192, so the four wave ballots ARE the
+// 32 descriptor bytes (byte i bit k = pair 8i+k, little endian).
+__global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+                                                     size_t img_bytes, const int2* __restrict__ sel, int nsel,
+                                                     const LevelDev* __restrict__ lv, orb_kp_dev* __restrict__ kps,
+                                                     uint8_t* __restrict__ desc, int cap_per_image) {
+    const int lane = threadIdx.x & 63;
+    const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= nsel) return;
+    const int2 s = sel[k];
+    const uint32_t pk = (uint32_t)s.x;
+    const int meta = s.y;
+    const int b = meta >> 20, l = (meta >> 16) & 15, idx = meta & 0xffff;
+    const int x = (int)(pk & 0xfff) + (kEdge - 3), y = (int)((pk >> 12) & 0xfff) + (kEdge - 3);
+    const int score = (int)(pk >> 24);
+    const LevelDev L = lv[l];
+    const uint8_t* cimg = pyr + (size_t)b * img_bytes + L.off + (size_t)(kEdge + y) * L.pitch + kEdge + x;
+    int m01 = 0, m10 = 0;
+    for (int i = lane; i < c_ndisc; i += 64) {
+        const int u = c_disc[2 * i], v = c_disc[2 * i + 1];
+        const int val = cimg[v * L.pitch + u];
+        m10 += u * val;
+        m01 += v * val;
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = fast_atan2((float)m01, (float)m10);
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    float sa, ca;
+    glibc_sincosf(angle * factorPI, &sa, &ca);
+    const float a = ca, bb = sa;
+    const uint8_t* cb = blur + (size_t)b * img_bytes + L.off + (size_t)(kEdge + y) * L.pitch + kEdge + x;
+    uint64_t words[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int p = lane + 64 * q;
+        const float x0 = (float)c_pattern[4 * p], y0 = (float)c_pattern[4 * p + 1];
+        const float x1 = (float)c_pattern[4 * p + 2], y1 = (float)c_pattern[4 * p + 3];
+        const int t0 = cb[cv_round(x0 * bb + y0 * a) * L.pitch + cv_round(x0 * a - y0 * bb)];
+        const int t1 = cb[cv_round(x1 * bb + y1 * a) * L.pitch + cv_round(x1 * a - y1 * bb)];
+        words[q] = __ballot(t0 < t1);
+    }
+    const size_t o = (size_t)b * cap_per_image + idx;
+    if (lane < 4) reinterpret_cast<uint64_t*>(desc + o * 32)[lane] = words[lane];
+    if (lane == 0) {
+        orb_kp_dev kp;
+        float fx = (float)x, fy = (float)y;
+        if (l != 0) {
+            fx = fx * L.scale;
+            fy = fy * L.scale;
+        }
+        kp.x = fx;
+        kp.y = fy;
+        kp.size = L.kp_size;
+        kp.angle = angle;
+        kp.response = (float)score;
+        kp.octave = l;
+        kp.class_id = -1;
+        kps[o] = kp;
+    }
+}
+
+// ------------------------------------------------------------- host driver
+static inline int align_up(int v, int a) { return (v + a - 1) / a * a; }
+
+static float cvRoundf_host(float v) { return (float)std::lrint(v); }
+
+Extractor::Extractor(int nfeatures, float scaleFactor, int nlevels, int iniTh, int minTh)
+    : nfeatures_(nfeatures), scaleFactorD_((double)scaleFactor), scaleFactor_(scaleFactor),
+      nlevels_(nlevels), iniTh_(iniTh), minTh_(minTh) {
+    // ORBextractor ctor, ORBextractor.cc:410-452 (float/double promotion kept)
+    scale_.resize(nlevels);
+    sigma2_.resize(nlevels);
+    invScale_.resize(nlevels);
+    invSigma2_.resize(nlevels);
+    nPerLevel_.resize(nlevels);
+    scale_[0] = 1.0f;
+    sigma2_[0] = 1.0f;
+    for (int i = 1; i < nlevels; i++) {
+        scale_[i] = (float)(scale_[i - 1] * scaleFactorD_);
+        sigma2_[i] = scale_[i] * scale_[i];
+    }
+    for (int i = 0; i < nlevels; i++) {
+        invScale_[i] = 1.0f / scale_[i];
+        invSigma2_[i] = 1.0f / sigma2_[i];
+    }
+    const float factor = (float)(1.0f / scaleFactorD_);
+    float nDesired = nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; l++) {
+        nPerLevel_[l] = (int)cvRoundf_host(nDesired);
+        sum += nPerLevel_[l];
+        nDesired *= factor;
+    }
+    nPerLevel_[nlevels - 1] = std::max(nfeatures - sum, 0);
+    // umax, ORBextractor.cc:454-469
+    umax_.assign(kHalfPatch + 1, 0);
+    const int vmax = (int)std::floor(kHalfPatch * std::sqrt(2.f) / 2 + 1);
+    const int vmin = (int)std::ceil(kHalfPatch * std::sqrt(2.f) / 2);
+    const double hp2 = kHalfPatch * kHalfPatch;
+    for (int v = 0; v <= vmax; ++v) umax_[v] = (int)std::lrint(std::sqrt(hp2 - v * v));
+    for (int v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+        while (umax_[v0] == umax_[v0 + 1]) ++v0;
+        umax_[v] = v0;
+        ++v0;
+    }
+}
+
+Extractor::~Extractor() { release(); }
+
+void Extractor::release() {
+    if (workers_started_) {
+        {
+            std::lock_guard<std::mutex> g(pool_mu_);
+            pool_stop_ = true;
+        }
+        pool_cv_.notify_all();
+        for (auto& t : pool_) t.join();
+        pool_.clear();
+        workers_started_ = false;
+    }
+    auto F = [](void* p) { if (p) (void)hipFree(p); };
+    F(d_in_); F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_);
+    F(d_lcb_); F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_);
+    F(d_kps_); F(d_desc_);
+    d_in_ = d_pyr_ = d_blur_ = nullptr;
+    d_slots_ = nullptr; d_counts_ = nullptr; d_cells_ = nullptr; d_tiles_ = nullptr;
+    d_lcb_ = nullptr; d_packed_ = nullptr; d_hdr_ = nullptr; d_gtotal_ = nullptr; d_sel_ = nullptr;
+    d_levels_ = nullptr; d_tabs_ = nullptr; d_kps_ = nullptr; d_desc_ = nullptr;
+    if (h_hdr_) (void)hipHostFree(h_hdr_);
+    if (h_packed_) (void)hipHostFree(h_packed_);
+    if (h_sel_) (void)hipHostFree(h_sel_);
+    h_hdr_ = nullptr; h_packed_ = nullptr; h_sel_ = nullptr;
+    for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
+    for (auto& e : ev_) e = nullptr;
+    if (stream_) (void)hipStreamDestroy(stream_);
+    stream_ = nullptr;
+}
+
+int Extractor::init_device(int maxW, int maxH, int maxBatch) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -4;
+    ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    for (auto& e : ev_) ORB_HIP_CHECK(hipEventCreate(&e));
+    static bool consts_done = false;  // per process; guarded by first-use in create
+    if (!consts_done) {
+        ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kPattern, sizeof(kPattern)));
+        int taps[7];
+        gaussian_taps(taps);
+        ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_gauss), taps, sizeof(taps)));
+        consts_done = true;
+    }
+    // disc offsets for IC_Angle: row v uses |u| <= umax[|v|]
+    std::vector<int8_t> disc;
+    for (int v = -kHalfPatch; v <= kHalfPatch; v++) {
+        const int d = v == 0 ? kHalfPatch : umax_[std::abs(v)];
+        for (int u = -d; u <= d; u++) { disc.push_back((int8_t)u); disc.push_back((int8_t)v); }
+    }
+    const int nd = (int)disc.size() / 2;
+    ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_disc), disc.data(), disc.size()));
+    ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_ndisc), &nd, sizeof(int)));
+    maxW_ = maxW; maxH_ = maxH; maxB_ = maxBatch;
+    return 0;
+}
+
+void Extractor::gaussian_taps(int taps[7]) {
+    // getGaussianKernel(7, 2, CV_32F) then *256 -> int (createSeparableLinearFilter)
+    float cf[7];
+    double sum = 0, scale2X = -0.5 / (2.0 * 2.0);
+    for (int i = 0; i < 7; i++) {
+        double x = i - 3.0;
+        cf[i] = (float)std::exp(scale2X * x * x);
+        sum += cf[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < 7; i++) {
+        cf[i] = (float)(cf[i] * sum);
+        taps[i] = (int)std::lrint(cf[i] * 256.0f);
+    }
+}
+
+// Geometry of the pyramid / cells / resize tables for an image size.
+int Extractor::setup_geometry(int W, int H) {
+    if (W == geomW_ && H == geomH_) return 0;
+    if (W > 4000 || H > 4000) return -1;
+    levels_.assign(nlevels_, LevelHost{});
+    size_t off = 0;
+    for (int l = 0; l < nlevels_; l++) {
+        LevelHost& L = levels_[l];
+        L.w = (int)std::lrint((float)W * invScale_[l]);
+        L.h = (int)std::lrint((float)H * invScale_[l]);
+        if (L.w < 1 || L.h < 1) return -1;
+        L.pw = L.w + 2 * kEdge;
+        L.ph = L.h + 2 * kEdge;
+        L.pitch = align_up(L.pw, 16);
+        L.off = off;
+        off += (size_t)L.pitch * L.ph;
+        off = (off + 255) & ~(size_t)255;
+    }
+    img_bytes_ = off;
+    // cells, ORBextractor.cc:776-829
+    cells_.clear();
+    level_cell_begin_.assign(nlevels_ + 1, 0);
+    size_t slot = 0;
+    for (int l = 0; l < nlevels_; l++) {
+        const LevelHost& L = levels_[l];
+        level_cell_begin_[l] = (int)cells_.size();
+        const float Wc = 30;
+        const int minBorderX = kEdge - 3, minBorderY = minBorderX;
+        const int maxBorderX = L.w - kEdge + 3, maxBorderY = L.h - kEdge + 3;
+        const float width = (float)(maxBorderX - minBorderX), height = (float)(maxBorderY - minBorderY);
+        const int nCols = (int)(width / Wc), nRows = (int)(height / Wc);
+        if (nCols <= 0 || nRows <= 0) return -1;  // reference divides by zero
+        const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+        if (wCell + 6 > FC_MAXR || hCell + 6 > FC_MAXR) return -1;
+        for (int i = 0; i < nRows; i++) {
+            const float iniY = (float)(minBorderY + i * hCell);
+            float maxY = iniY + hCell + 6;
+            if (iniY >= maxBorderY - 3) continue;
+            if (maxY > maxBorderY) maxY = (float)maxBorderY;
+            for (int j = 0; j < nCols; j++) {
+                const float iniX = (float)(minBorderX + j * wCell);
+                float maxX = iniX + wCell + 6;
+                if (iniX >= maxBorderX - 6) continue;
+                if (maxX > maxBorderX) maxX = (float)maxBorderX;
+                CellDesc c;
+                c.r0 = (int)iniY; c.r1 = (int)maxY; c.c0 = (int)iniX; c.c1 = (int)maxX;
+                c.offx = j * wCell; c.offy = i * hCell;
+                c.pitch = L.pitch;
+                c.lvl_off = L.off;
+                const int dr = c.r1 - c.r0 - 6, dc = c.c1 - c.c0 - 6;
+                c.cap = (dr > 0 && dc > 0) ? ((dr + 1) / 2) * ((dc + 1) / 2) : 0;
+                c.slot_off = (int)slot;
+                slot += c.cap;
+                c.level = l;
+                cells_.push_back(c);
+            }
+        }
+    }
+    level_cell_begin_[nlevels_] = (int)cells_.size();
+    slots_per_image_ = (slot + 63) & ~(size_t)63;
+    if (cells_.size() > 4096) return -1;
+    // blur tiles
+    tiles_.clear();
+    for (int l = 0; l < nlevels_; l++) {
+        const LevelHost& L = levels_[l];
+        for (int ty = 0; ty < (L.h + BT_H - 1) / BT_H; ty++)
+            for (int tx = 0; tx < (L.w + BT_W - 1) / BT_W; tx++) {
+                BlurTile t;
+                t.off = L.off; t.pitch = L.pitch; t.w = L.w; t.h = L.h; t.tx = tx; t.ty = ty;
+                tiles_.push_back(t);
+            }
+    }
+    // resize tables (OpenCV 3.2 resize(), INTER_LINEAR, fixpt)
+    std::vector<uint8_t> tabs;
+    auto push = [&tabs](const void* p, size_t n) -> size_t {
+        size_t o = (tabs.size() + 15) & ~(size_t)15;
+        tabs.resize(o + n);
+        memcpy(tabs.data() + o, p, n);
+        return o;
+    };
+    tab_off_.assign(nlevels_, {0, 0, 0, 0});
+    for (int l = 1; l < nlevels_; l++) {
+        const int sw = levels_[l - 1].w, sh = levels_[l - 1].h, dw = levels_[l].w, dh = levels_[l].h;
+        const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+        std::vector<int> xofs(dw);
+        std::vector<short> xal(2 * dw);
+        int xmax = dw;
+        auto sat_s = [](float v) { long i = std::lrint(v); return (short)std::min(32767L, std::max(-32768L, i)); };
+        for (int dx = 0; dx < dw; dx++) {
+            float fx = (float)((dx + 0.5) * scale_x - 0.5);
+            int sx = (int)std::floor(fx);
+            fx -= sx;
+            if (sx < 0) { fx = 0; sx = 0; }
+            if (sx + 1 >= sw) {
+                xmax = std::min(xmax, dx);
+                if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+            }
+            xofs[dx] = sx;
+            xal[2 * dx] = sat_s((1.f - fx) * 2048);
+            xal[2 * dx + 1] = sat_s(fx * 2048);
+        }
+        for (int dx = xmax; dx < dw; dx++) { xal[2 * dx] = 2048; xal[2 * dx + 1] = 0; }
+        std::vector<int> yr(2 * dh);
+        std::vector<short> yb(2 * dh);
+        for (int dy = 0; dy < dh; dy++) {
+            float fy = (float)((dy + 0.5) * scale_y - 0.5);
+            int sy = (int)std::floor(fy);
+            fy -= sy;
+            yr[2 * dy] = std::min(std::max(sy, 0), sh - 1);
+            yr[2 * dy + 1] = std::min(std::max(sy + 1, 0), sh - 1);
+            yb[2 * dy] = sat_s((1.f - fy) * 2048);
+            yb[2 * dy + 1] = sat_s(fy * 2048);
+        }
+        tab_off_[l][0] = push(xofs.data(), xofs.size() * 4);
+        tab_off_[l][1] = push(xal.data(), xal.size() * 2);
+        tab_off_[l][2] = push(yr.data(), yr.size() * 4);
+        tab_off_[l][3] = push(yb.data(), yb.size() * 2);
+    }
+    // (re)allocate device buffers for maxB_
+    auto F = [](void*& p) { if (p) (void)hipFree(p); p = nullptr; };
+    F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_lcb_);
+    F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_);
+    const int B = maxB_;
+    ORB_HIP_CHECK(hipMalloc(&d_pyr_, img_bytes_ * B));
+    ORB_HIP_CHECK(hipMalloc(&d_blur_, img_bytes_ * B));
+    ORB_HIP_CHECK(hipMemset(d_blur_, 0, img_bytes_ * B));
+    ORB_HIP_CHECK(hipMalloc(&d_slots_, slots_per_image_ * 4 * B));
+    ORB_HIP_CHECK(hipMalloc(&d_counts_, cells_.size() * 4 * B));
+    ORB_HIP_CHECK(hipMalloc(&d_cells_, cells_.size() * sizeof(CellDesc)));
+    ORB_HIP_CHECK(hipMemcpy(d_cells_, cells_.data(), cells_.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
+    ORB_HIP_CHECK(hipMalloc(&d_tiles_, tiles_.size() * sizeof(BlurTile)));
+    ORB_HIP_CHECK(hipMemcpy(d_tiles_, tiles_.data(), tiles_.size() * sizeof(BlurTile), hipMemcpyHostToDevice));
+    ORB_HIP_CHECK(hipMalloc(&d_lcb_, level_cell_begin_.size() * 4));
+    ORB_HIP_CHECK(hipMemcpy(d_lcb_, level_cell_begin_.data(), level_cell_begin_.size() * 4, hipMemcpyHostToDevice));
+    packed_cap_ = (int)std::min<size_t>(slots_per_image_ * B, (size_t)1 << 30);
+    ORB_HIP_CHECK(hipMalloc(&d_packed_, (size_t)packed_cap_ * 4));
+    ORB_HIP_CHECK(hipMalloc(&d_hdr_, (size_t)B * (nlevels_ + 2) * 4 + 64));
+    d_gtotal_ = (int*)((char*)d_hdr_ + (size_t)B * (nlevels_ + 2) * 4);
+    d_gtotal_alias_ = true;
+    sel_cap_ = B * std::max(nfeatures_ * 2 + 64, 256);
+    ORB_HIP_CHECK(hipMalloc(&d_sel_, (size_t)sel_cap_ * sizeof(int2)));
+    std::vector<LevelDev> ld(nlevels_);
+    for (int l = 0; l < nlevels_; l++) {
+        ld[l].off = levels_[l].off;
+        ld[l].pitch = levels_[l].pitch;
+        ld[l].scale = scale_[l];
+        ld[l].kp_size = (float)(int)(kPatch * scale_[l]);
+    }
+    ORB_HIP_CHECK(hipMalloc(&d_levels_, ld.size() * sizeof(LevelDev)));
+    ORB_HIP_CHECK(hipMemcpy(d_levels_, ld.data(), ld.size() * sizeof(LevelDev), hipMemcpyHostToDevice));
+    ORB_HIP_CHECK(hipMalloc(&d_tabs_, std::max<size_t>(tabs.size(), 16)));
+    if (!tabs.empty()) ORB_HIP_CHECK(hipMemcpy(d_tabs_, tabs.data(), tabs.size(), hipMemcpyHostToDevice));
+    if (h_hdr_) (void)hipHostFree(h_hdr_);
+    if (h_packed_) (void)hipHostFree(h_packed_);
+    if (h_sel_) (void)hipHostFree(h_sel_);
+    ORB_HIP_CHECK(hipHostMalloc((void**)&h_hdr_, (size_t)B * (nlevels_ + 2) * 4 + 64));
+    ORB_HIP_CHECK(hipHostMalloc((void**)&h_packed_, (size_t)packed_cap_ * 4));
+    ORB_HIP_CHECK(hipHostMalloc((void**)&h_sel_, (size_t)sel_cap_ * sizeof(int2)));
+    geomW_ = W;
+    geomH_ = H;
+    return 0;
+}
+
+void Extractor::start_workers() {
+    if (workers_started_) return;
+    unsigned n = std::thread::hardware_concurrency();
+    const char* env = getenv("ORBGPU_HOST_THREADS");
+    if (env) n = (unsigned)atoi(env);
+    n = std::max(1u, std::min(n, 16u));
+    pool_stop_ = false;
+    workers_.resize(n + 1);
+    for (unsigned i = 0; i < n; i++) pool_.emplace_back([this] { worker_loop(); });
+    workers_started_ = true;
+}
+
+void Extractor::worker_loop() {
+    // each worker has an id from the order it grabs it
+    int wid;
+    {
+        std::lock_guard<std::mutex> g(pool_mu_);
+        wid = worker_ids_++;
+    }
+    uint64_t seen = 0;
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> g(pool_mu_);
+            pool_cv_.wait(g, [&] { return pool_stop_ || pool_gen_ != seen; });
+            if (pool_stop_) return;
+            seen = pool_gen_;
+        }
+        run_octree_jobs(wid + 1);
+        if (pool_pending_.fetch_sub(1) == 1) {
+            std::lock_guard<std::mutex> g(pool_mu_);
+            pool_done_cv_.notify_all();
+        }
+    }
+}
+
+void Extractor::run_octree_jobs(int wid) {
+    OctreeWorker& W = workers_[wid].oct;
+    std::vector<OctKey>& keys = workers_[wid].keys;
+    std::vector<uint32_t>& out = workers_[wid].out;
+    for (;;) {
+        const int job = next_job_.fetch_add(1);
+        if (job >= njobs_) break;
+        const int b = job / nlevels_, l = job % nlevels_;
+        const int* H = h_hdr_ + (size_t)b * (nlevels_ + 2);
+        const int base = H[nlevels_ + 1];
+        int loff = 0;
+        for (int k = 0; k < l; k++) loff += H[1 + k];
+        const int n = H[1 + l];
+        const uint32_t* src = h_packed_ + base + loff;
+        keys.resize(n);
+        for (int i = 0; i < n; i++) {
+            const uint32_t p = src[i];
+            keys[i].x = (float)(p & 0xfff);
+            keys[i].y = (float)((p >> 12) & 0xfff);
+            keys[i].response = (float)(p >> 24);
+            keys[i].packed = p;
+        }
+        const LevelHost& L = levels_[l];
+        const int minB = kEdge - 3;
+        const int r = W.distribute(keys.data(), n, minB, L.w - kEdge + 3, minB, L.h - kEdge + 3, nPerLevel_[l], out);
+        job_res_[job].assign(out.begin(), out.begin() + std::max(r, 0));
+        job_ok_[job] = r >= 0;
+    }
+}
+
+int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_t img_stride,
+                       bool imgs_on_device, orb_kp* kps, uint8_t* desc, int cap, bool out_on_device,
+                       int* n_out) {
+    if (B <= 0 || B > maxB_ || W <= 0 || H <= 0) return -1;
+    if (W > maxW_ || H > maxH_) return -1;
+    if (int e = setup_geometry(W, H)) return e;
+    start_workers();
+    hipStream_t s = stream_;
+    const uint8_t* src = imgs;
+    if (!imgs_on_device) {
+        const size_t need = img_stride * (B - 1) + (size_t)step * (H - 1) + W;
+        if (need > in_cap_) {
+            if (d_in_) (void)hipFree(d_in_);
+            ORB_HIP_CHECK(hipMalloc(&d_in_, need));
+            in_cap_ = need;
+        }
+        ORB_HIP_CHECK(hipMemcpyAsync(d_in_, imgs, need, hipMemcpyHostToDevice, s));
+        src = (const uint8_t*)d_in_;
+    }
+    ORB_HIP_CHECK(hipEventRecord(ev_[0], s));
+    // 1. pyramid
+    {
+        const LevelHost& L0 = levels_[0];
+        const int n = (L0.pitch / 4) * L0.ph;
+        hipLaunchKernelGGL(k_pyr_level0, dim3((n + 255) / 256, B), dim3(256), 0, s, src, img_stride, step, W, H,
+                           (uint8_t*)d_pyr_, img_bytes_, L0.pitch, L0.ph);
+        for (int l = 1; l < nlevels_; l++) {
+            const LevelHost& L = levels_[l];
+            const LevelHost& P = levels_[l - 1];
+            const int nq = (L.pitch / 4) * L.ph;
+            const uint8_t* T = (const uint8_t*)d_tabs_;
+            hipLaunchKernelGGL(k_pyr_resize, dim3((nq + 255) / 256, B), dim3(256), 0, s, (uint8_t*)d_pyr_, img_bytes_,
+                               P.off, P.pitch, L.off, L.pitch, L.ph, L.w, L.h,
+                               (const int*)(T + tab_off_[l][0]), (const short2*)(T + tab_off_[l][1]),
+                               (const int2*)(T + tab_off_[l][2]), (const short2*)(T + tab_off_[l][3]));
+        }
+    }
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
+    // 2. blur (independent of keypoints; overlaps nothing yet, kept on the stream)
+    hipLaunchKernelGGL(k_blur7, dim3((unsigned)tiles_.size(), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
+                       (uint8_t*)d_blur_, img_bytes_, (const BlurTile*)d_tiles_);
+    ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
+    // 3. FAST per cell
+    const int ncells = (int)cells_.size();
+    hipLaunchKernelGGL(k_fast_cells, dim3(ncells, B), dim3(256), 0, s, (const uint8_t*)d_pyr_, img_bytes_,
+                       (const CellDesc*)d_cells_, iniTh_, minTh_, (uint32_t*)d_slots_, slots_per_image_,
+                       (int*)d_counts_, ncells);
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipEventRecord(ev_[3], s));
+    // 4. compaction
+    ORB_HIP_CHECK(hipMemsetAsync(d_gtotal_, 0, 4, s));
+    hipLaunchKernelGGL(k_compact, dim3(B), dim3(1024), 0, s, (const uint32_t*)d_slots_, slots_per_image_,
+                       (const int*)d_counts_, (const CellDesc*)d_cells_, ncells, (const int*)d_lcb_, nlevels_,
+                       (uint32_t*)d_packed_, (int*)d_hdr_, d_gtotal_, packed_cap_);
+    ORB_HIP_CHECK(hipGetLastError());
+    const size_t hdr_bytes = (size_t)maxB_ * (nlevels_ + 2) * 4;  // d_gtotal_ sits right after
+    ORB_HIP_CHECK(hipMemcpyAsync(h_hdr_, d_hdr_, hdr_bytes + 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_CHECK(hipEventRecord(ev_[4], s));
+    ORB_HIP_CHECK(hipStreamSynchronize(s));
+    const int gtotal = *(int*)((char*)h_hdr_ + hdr_bytes);
+    for (int b = 0; b < B; b++)
+        if (h_hdr_[(size_t)b * (nlevels_ + 2) + nlevels_ + 1] < 0) return -3;  // packed capacity
+    if (gtotal > 0)
+        ORB_HIP_CHECK(hipMemcpyAsync(h_packed_, d_packed_, (size_t)gtotal * 4, hipMemcpyDeviceToHost, s));
+    ORB_HIP_CHECK(hipStreamSynchronize(s));
+    // 5. host octree, (image, level) jobs over the worker pool
+    auto t_oct0 = std::chrono::steady_clock::now();
+    njobs_ = B * nlevels_;
+    job_res_.resize(njobs_);
+    job_ok_.assign(njobs_, 0);
+    next_job_ = 0;
+    {
+        std::lock_guard<std::mutex> g(pool_mu_);
+        pool_pending_ = (int)pool_.size();
+        pool_gen_++;
+    }
+    pool_cv_.notify_all();
+    run_octree_jobs(0);
+    {
+        std::unique_lock<std::mutex> g(pool_mu_);
+        pool_done_cv_.wait(g, [&] { return pool_pending_.load() == 0; });
+    }
+    for (int j = 0; j < njobs_; j++)
+        if (!job_ok_[j]) return -1;
+    // selected list: image-major, level-major, octree order
+    int nsel = 0;
+    for (int b = 0; b < B; b++) {
+        int k = 0;
+        for (int l = 0; l < nlevels_; l++) k += (int)job_res_[b * nlevels_ + l].size();
+        n_out[b] = k;
+        if (k > cap) return -3;
+        nsel += k;
+    }
+    if (nsel > sel_cap_) return -3;
+    {
+        int o = 0;
+        for (int b = 0; b < B; b++) {
+            int k = 0;
+            for (int l = 0; l < nlevels_; l++)
+                for (uint32_t p : job_res_[b * nlevels_ + l]) {
+                    h_sel_[o].x = (int)p;
+                    h_sel_[o].y = (b << 20) | (l << 16) | k;
+                    o++;
+                    k++;
+                }
+        }
+    }
+    octree_ms_ = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_oct0).count();
+    ORB_HIP_CHECK(hipEventRecord(ev_[5], s));
+    // 6. orientation + descriptors
+    orb_kp_dev* okps = (orb_kp_dev*)kps;
+    uint8_t* odesc = desc;
+    if (!out_on_device) {
+        const size_t nk = (size_t)B * cap;
+        if (nk > out_cap_) {
+            if (d_kps_) (void)hipFree(d_kps_);
+            if (d_desc_) (void)hipFree(d_desc_);
+            ORB_HIP_CHECK(hipMalloc(&d_kps_, nk * sizeof(orb_kp_dev)));
+            ORB_HIP_CHECK(hipMalloc(&d_desc_, nk * 32));
+            out_cap_ = nk;
+        }
+        okps = (orb_kp_dev*)d_kps_;
+        odesc = (uint8_t*)d_desc_;
+    }
+    if (nsel > 0) {
+        ORB_HIP_CHECK(hipMemcpyAsync(d_sel_, h_sel_, (size_t)nsel * sizeof(int2), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_orient_desc, dim3((nsel + 3) / 4), dim3(256), 0, s, (const uint8_t*)d_pyr_,
+                           (const uint8_t*)d_blur_, img_bytes_, (const int2*)d_sel_, nsel,
+                           (const LevelDev*)d_levels_, okps, odesc, cap);
+        ORB_HIP_CHECK(hipGetLastError());
+    }
+    ORB_HIP_CHECK(hipEventRecord(ev_[6], s));
+    if (!out_on_device) {
+        for (int b = 0; b < B; b++) {
+            if (n_out[b] == 0) continue;
+            ORB_HIP_CHECK(hipMemcpyAsync(kps + (size_t)b * cap, okps + (size_t)b * cap, (size_t)n_out[b] * sizeof(orb_kp_dev),
+                                         hipMemcpyDeviceToHost, s));
+            ORB_HIP_CHECK(hipMemcpyAsync(desc + (size_t)b * cap * 32, odesc + (size_t)b * cap * 32, (size_t)n_out[b] * 32,
+                                         hipMemcpyDeviceToHost, s));
+        }
+    }
+    ORB_HIP_CHECK(hipStreamSynchronize(s));
+    last_B_ = B;
+    return 0;
+}
+
+int Extractor::timings(float* ms6) {
+    float t[6] = {0};
+    (void)hipEventElapsedTime(&t[0], ev_[0], ev_[1]);
+    (void)hipEventElapsedTime(&t[1], ev_[1], ev_[2]);
+    (void)hipEventElapsedTime(&t[2], ev_[2], ev_[3]);
+    (void)hipEventElapsedTime(&t[3], ev_[3], ev_[4]);
+    t[4] = octree_ms_;
+    (void)hipEventElapsedTime(&t[5], ev_[5], ev_[6]);
+    for (int i = 0; i < 6; i++) ms6[i] = t[i];
+    return 0;
+}
+
+int Extractor::get_level(int index, int level, uint8_t* dst, int dst_step, int* w, int* h) {
+    if (level < 0 || level >= nlevels_ || index < 0 || index >= last_B_ || !d_pyr_) return -1;
+    const LevelHost& L = levels_[level];
+    *w = L.w;
+    *h = L.h;
+    if (!dst) return 0;
+    ORB_HIP_CHECK(hipMemcpy2D(dst, dst_step, (const uint8_t*)d_pyr_ + (size_t)index * img_bytes_ + L.off, L.pitch,
+                              L.pw, L.ph, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+}  // namespace orbgpu

@@ -1,0 +1,125 @@
+// orb_extract.hpp -- host driver of the gfx950 ORB extractor (see orb_extract.hip).
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <mutex>
+#include <thread>
+#include <vector>
+#include <array>
+
+#include "orb_common.hpp"
+#include "octree.hpp"
+#include "../../include/orbslam_gpu.h"
+
+namespace orbgpu {
+
+struct orb_kp_dev {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+};
+static_assert(sizeof(orb_kp_dev) == 28, "cv::KeyPoint layout");
+
+struct CellDesc {          // one FAST cell ROI, ORBextractor.cc:794-829
+    int r0, r1, c0, c1;    // ROI rows/cols in level interior coords
+    int offx, offy;        // j*wCell, i*hCell (pt offset relative to minBorder)
+    int pitch, cap, slot_off, level;
+    long long lvl_off;     // byte offset of the padded level in an image slab
+};
+
+struct BlurTile {
+    long long off;
+    int pitch, w, h, tx, ty;
+};
+
+struct LevelDev {
+    long long off;
+    int pitch;
+    float scale, kp_size;
+};
+
+struct LevelHost {
+    int w, h, pw, ph, pitch;
+    size_t off;
+};
+
+class Extractor {
+public:
+    Extractor(int nfeatures, float scaleFactor, int nlevels, int iniTh, int minTh);
+    ~Extractor();
+    int init_device(int maxW, int maxH, int maxBatch);
+    int extract(const uint8_t* imgs, int B, int W, int H, int step, size_t img_stride, bool imgs_on_device,
+                orb_kp* kps, uint8_t* desc, int cap, bool out_on_device, int* n_out);
+    int get_level(int index, int level, uint8_t* dst, int dst_step, int* w, int* h);
+    int timings(float* ms6);
+    hipStream_t stream() const { return stream_; }
+
+    int nlevels() const { return nlevels_; }
+    float scale_factor() const { return scaleFactor_; }
+    const std::vector<float>& scale() const { return scale_; }
+    const std::vector<float>& inv_scale() const { return invScale_; }
+    const std::vector<float>& sigma2() const { return sigma2_; }
+    const std::vector<float>& inv_sigma2() const { return invSigma2_; }
+    const std::vector<int>& n_per_level() const { return nPerLevel_; }
+
+private:
+    static void gaussian_taps(int taps[7]);
+    int setup_geometry(int W, int H);
+    void release();
+    void start_workers();
+    void worker_loop();
+    void run_octree_jobs(int wid);
+
+    int nfeatures_;
+    double scaleFactorD_;
+    float scaleFactor_;
+    int nlevels_, iniTh_, minTh_;
+    std::vector<float> scale_, invScale_, sigma2_, invSigma2_;
+    std::vector<int> nPerLevel_, umax_;
+
+    int maxW_ = 0, maxH_ = 0, maxB_ = 0;
+    int geomW_ = -1, geomH_ = -1;
+    std::vector<LevelHost> levels_;
+    std::vector<CellDesc> cells_;
+    std::vector<int> level_cell_begin_;
+    std::vector<BlurTile> tiles_;
+    std::vector<std::array<size_t, 4>> tab_off_;
+    size_t img_bytes_ = 0, slots_per_image_ = 0;
+    int packed_cap_ = 0, sel_cap_ = 0;
+    int last_B_ = 0;
+
+    hipStream_t stream_ = nullptr;
+    hipEvent_t ev_[7] = {};
+    void *d_in_ = nullptr, *d_pyr_ = nullptr, *d_blur_ = nullptr, *d_slots_ = nullptr, *d_counts_ = nullptr;
+    void *d_cells_ = nullptr, *d_tiles_ = nullptr, *d_lcb_ = nullptr, *d_packed_ = nullptr, *d_hdr_ = nullptr;
+    void *d_sel_ = nullptr, *d_levels_ = nullptr, *d_tabs_ = nullptr, *d_kps_ = nullptr, *d_desc_ = nullptr;
+    int* d_gtotal_ = nullptr;
+    bool d_gtotal_alias_ = false;
+    size_t in_cap_ = 0, out_cap_ = 0;
+    int* h_hdr_ = nullptr;
+    uint32_t* h_packed_ = nullptr;
+    int2* h_sel_ = nullptr;
+    float octree_ms_ = 0;
+
+    // host octree worker pool
+    struct WorkerScratch {
+        OctreeWorker oct;
+        std::vector<OctKey> keys;
+        std::vector<uint32_t> out;
+    };
+    std::vector<WorkerScratch> workers_;
+    std::vector<std::thread> pool_;
+    std::mutex pool_mu_;
+    std::condition_variable pool_cv_, pool_done_cv_;
+    bool pool_stop_ = false, workers_started_ = false;
+    uint64_t pool_gen_ = 0;
+    std::atomic<int> pool_pending_{0};
+    int worker_ids_ = 0;
+    std::atomic<int> next_job_{0};
+    int njobs_ = 0;
+    std::vector<std::vector<uint32_t>> job_res_;
+    std::vector<char> job_ok_;
+};
+
+}  // namespace orbgpu

@@ -1,0 +1,536 @@
+// orb_match.hip -- gfx950 guided 256-bit Hamming matching (reference src/ORBmatcher.cc).
+//
+// The reference matchers are greedy: a query may not take a candidate that an
+// earlier query already took (`if(F.mvpMapPoints[idx]) ... continue`,
+// ORBmatcher.cc:87-89, 1403-1405).  So the work is split in two launches:
+//   k_candidates  (one thread per query, all queries of all problems in
+//                 parallel): projection, Frame::GetFeaturesInArea window over
+//                 the device grid, static filters, popcount distances, and the
+//                 kTopK smallest (dist, enumeration order) candidates;
+//   k_select      (one wave per problem): the sequential greedy replay over the
+//                 queries against the occupancy array held in LDS, with a full
+//                 rescan only when every kept candidate is already taken, then
+//                 the rotation-consistency histogram (ORBmatcher.cc:1447-1467).
+// k_build_grid rebuilds Frame::mGrid (AssignFeaturesToGrid, Frame.cc:230-245)
+// as a CSR in cell order (ix-major) with keypoint order kept inside a cell.
+#include "orb_match.hpp"
+
+#include <cstring>
+
+namespace orbgpu {
+
+constexpr int TH_HIGH = 100;  // ORBmatcher.cc:37
+constexpr int HISTO_LENGTH = 30;
+
+__device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
+    const uint4* pa = reinterpret_cast<const uint4*>(a);
+    const uint4* pb = reinterpret_cast<const uint4*>(b);
+    const uint4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// Rcw*X + tcw as one cv::gemm (GEMMSingleMul<float,double>): f64 accumulate, one rounding.
+__device__ __forceinline__ float gemm_row(const float* T, int r, float X0, float X1, float X2) {
+    double s = (double)T[r * 4 + 0] * X0 + (double)T[r * 4 + 1] * X1 + (double)T[r * 4 + 2] * X2;
+    return (float)(s + (double)T[r * 4 + 3]);
+}
+
+// ---------------------------------------------------------------- grid build
+__global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs) {
+    __shared__ uint32_t s_key[kMaxFrameKeys];
+    SearchDev& P = probs[blockIdx.x];
+    const FrameDev& F = P.cur;
+    const int N = F.N;
+    int Pn = 1;
+    while (Pn < N) Pn <<= 1;
+    for (int i = threadIdx.x; i < Pn; i += 256) {
+        uint32_t key = 0xffffffffu;
+        if (i < N) {
+            const orb_kp_dev kp = F.keysUn[i];
+            const int px = (int)roundf((kp.x - F.minX) * F.gridWInv);
+            const int py = (int)roundf((kp.y - F.minY) * F.gridHInv);
+            if (!(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows))
+                key = ((uint32_t)(px * kGridRows + py) << 12) | (uint32_t)i;
+        }
+        s_key[i] = key;
+    }
+    __syncthreads();
+    for (int k = 2; k <= Pn; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < Pn; i += 256) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t a = s_key[i], b = s_key[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) { s_key[i] = b; s_key[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = threadIdx.x; i < N; i += 256) P.gridIdx[i] = (int)(s_key[i] & 0xfff);
+    for (int c = threadIdx.x; c <= kGridCells; c += 256) {
+        const uint32_t target = (uint32_t)c << 12;
+        int lo = 0, hi = N;  // first position with key >= target
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_key[mid] < target) lo = mid + 1; else hi = mid;
+        }
+        P.gridStart[c] = lo;
+    }
+}
+
+// ------------------------------------------------------- candidate enumeration
+struct QueryWin {
+    float x, y, r;
+    int minLevel, maxLevel;
+};
+
+// Frame::GetFeaturesInArea (Frame.cc:327-380) over the CSR grid, calling
+// visit(idx) in the reference's enumeration order.
+template <class Visit>
+__device__ __forceinline__ void for_features_in_area(const SearchDev& P, const QueryWin& w, Visit visit) {
+    const FrameDev& F = P.cur;
+    const int nMinCellX = max(0, (int)floorf((w.x - F.minX - w.r) * F.gridWInv));
+    if (nMinCellX >= kGridCols) return;
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((w.x - F.minX + w.r) * F.gridWInv));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = max(0, (int)floorf((w.y - F.minY - w.r) * F.gridHInv));
+    if (nMinCellY >= kGridRows) return;
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((w.y - F.minY + w.r) * F.gridHInv));
+    if (nMaxCellY < 0) return;
+    const bool bCheckLevels = (w.minLevel > 0) || (w.maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+            const int c = ix * kGridRows + iy;
+            const int e = P.gridStart[c + 1];
+            for (int j = P.gridStart[c]; j < e; j++) {
+                const int idx = P.gridIdx[j];
+                const orb_kp_dev kp = F.keysUn[idx];
+                if (bCheckLevels) {
+                    if (kp.octave < w.minLevel) continue;
+                    if (w.maxLevel >= 0 && kp.octave > w.maxLevel) continue;
+                }
+                const float distx = kp.x - w.x, disty = kp.y - w.y;
+                if (fabsf(distx) < w.r && fabsf(disty) < w.r) visit(idx);
+            }
+        }
+}
+
+// Sorted insertion by (dist, order): later equal distances go after earlier ones.
+__device__ __forceinline__ void topk_insert(int2* top, int& n, int K, int dist, int idx) {
+    if (n == K && dist >= top[K - 1].x) return;
+    int p = n < K ? n : K - 1;
+    while (p > 0 && top[p - 1].x > dist) {
+        top[p] = top[p - 1];
+        p--;
+    }
+    top[p] = make_int2(dist, idx);
+    if (n < K) n++;
+}
+
+struct LastQuery {
+    bool valid;
+    QueryWin w;
+    float u, invzc, radius;
+    int mp;
+};
+
+// Projection part of SearchByProjection(Cur, Last), ORBmatcher.cc:1358-1395
+__device__ __forceinline__ LastQuery last_query(const SearchDev& P, int i, float th, bool bFwd, bool bBwd) {
+    LastQuery q;
+    q.valid = false;
+    const int mp = P.lastMP[i];
+    if (mp < 0 || P.lastOutlier[i]) return q;
+    const float* X = P.mpPos + 3 * (size_t)mp;
+    const float* T = P.cur.Tcw;
+    const float xc = gemm_row(T, 0, X[0], X[1], X[2]);
+    const float yc = gemm_row(T, 1, X[0], X[1], X[2]);
+    const float zc = gemm_row(T, 2, X[0], X[1], X[2]);
+    const float invzc = (float)(1.0 / (double)zc);
+    if (invzc < 0) return q;
+    const float u = P.cur.fx * xc * invzc + P.cur.cx;
+    const float v = P.cur.fy * yc * invzc + P.cur.cy;
+    if (u < P.cur.minX || u > P.cur.maxX) return q;
+    if (v < P.cur.minY || v > P.cur.maxY) return q;
+    const int nLastOctave = P.lastKeys[i].octave;
+    const float radius = th * P.cur.scale[nLastOctave];
+    q.w.x = u;
+    q.w.y = v;
+    q.w.r = radius;
+    if (bFwd) { q.w.minLevel = nLastOctave; q.w.maxLevel = -1; }
+    else if (bBwd) { q.w.minLevel = 0; q.w.maxLevel = nLastOctave; }
+    else { q.w.minLevel = nLastOctave - 1; q.w.maxLevel = nLastOctave + 1; }
+    q.u = u;
+    q.invzc = invzc;
+    q.radius = radius;
+    q.mp = mp;
+    q.valid = true;
+    return q;
+}
+
+__device__ __forceinline__ void fwd_bwd(const SearchDev& P, bool bMono, bool& bFwd, bool& bBwd) {
+    const float* Tc = P.cur.Tcw;
+    const float* Tl = P.last.Tcw;
+    float twc[3];
+    for (int i = 0; i < 3; i++) {
+        double s = (double)Tc[0 * 4 + i] * Tc[3] + (double)Tc[1 * 4 + i] * Tc[7] + (double)Tc[2 * 4 + i] * Tc[11];
+        twc[i] = (float)(s * -1.0);
+    }
+    const float tlc2 = gemm_row(Tl, 2, twc[0], twc[1], twc[2]);
+    bFwd = tlc2 > P.cur.b && !bMono;
+    bBwd = -tlc2 > P.cur.b && !bMono;
+}
+
+// Enumerate a LastFrame query's passing candidates; `blocked(i2)` models occupancy.
+template <class Blocked>
+__device__ int scan_last(const SearchDev& P, const LastQuery& q, Blocked blocked, int2* top, int K) {
+    int n = 0, cnt = 0;
+    const uint8_t* dMP = P.mpDesc + 32 * (size_t)q.mp;
+    for_features_in_area(P, q.w, [&](int i2) {
+        if (blocked(i2)) return;
+        if (P.cur.uRight && P.cur.uRight[i2] > 0) {
+            const float ur = q.u - P.cur.bf * q.invzc;
+            const float er = fabsf(ur - P.cur.uRight[i2]);
+            if (er > q.radius) return;
+        }
+        const int dist = hamming32(dMP, P.cur.desc + 32 * (size_t)i2);
+        topk_insert(top, n, K, dist, i2);
+        cnt++;
+    });
+    return cnt;
+}
+
+struct LocalQuery {
+    bool valid;
+    QueryWin w;
+    float r, projXR;
+    int level, mp;
+};
+
+// SearchByProjection(F, vpMapPoints, th) window, ORBmatcher.cc:51-71
+__device__ __forceinline__ LocalQuery local_query(const SearchDev& P, int j, float th) {
+    LocalQuery q;
+    q.valid = false;
+    if (!P.inView[j]) return q;
+    const int lvl = P.level[j];
+    float r = P.viewCos[j] > 0.998f ? 2.5f : 4.0f;  // RadiusByViewingCos, 131-137
+    if (th != 1.0f) r *= th;
+    q.w.x = P.projX[j];
+    q.w.y = P.projY[j];
+    q.w.r = r * P.cur.scale[lvl];
+    q.w.minLevel = lvl - 1;
+    q.w.maxLevel = lvl;
+    q.r = r;
+    q.projXR = P.projXR[j];
+    q.level = lvl;
+    q.mp = P.mpIndex[j];
+    q.valid = true;
+    return q;
+}
+
+template <class Blocked>
+__device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked blocked, int2* top, int K) {
+    int n = 0, cnt = 0;
+    const uint8_t* d0 = P.mpDesc + 32 * (size_t)q.mp;
+    for_features_in_area(P, q.w, [&](int idx) {
+        if (blocked(idx)) return;
+        if (P.cur.uRight && P.cur.uRight[idx] > 0) {
+            const float er = fabsf(q.projXR - P.cur.uRight[idx]);
+            if (er > q.r * P.cur.scale[q.level]) return;
+        }
+        const int dist = hamming32(d0, P.cur.desc + 32 * (size_t)idx);
+        topk_insert(top, n, K, dist, idx);
+        cnt++;
+    });
+    return cnt;
+}
+
+// Parallel phase: one thread per query.
+template <bool LAST>
+__global__ void __launch_bounds__(256) k_candidates(SearchDev* probs, float th, int bMono) {
+    const SearchDev& P = probs[blockIdx.y];
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= P.nq) return;
+    int2 top[kTopK];
+    int cnt = -1;
+    auto never = [](int) { return false; };
+    if (LAST) {
+        bool bF, bB;
+        fwd_bwd(P, bMono != 0, bF, bB);
+        const LastQuery lq = last_query(P, q, th, bF, bB);
+        if (lq.valid) cnt = scan_last(P, lq, never, top, kTopK);
+    } else {
+        const LocalQuery lq = local_query(P, q, th);
+        if (lq.valid) cnt = scan_local(P, lq, never, top, kTopK);
+    }
+    P.qinfo[q] = make_int4(cnt, 0, 0, 0);
+    const int kk = cnt < kTopK ? cnt : kTopK;
+    for (int k = 0; k < kk; k++) P.topk[(size_t)q * kTopK + k] = top[k];
+}
+
+// Sequential greedy replay: one wave per problem.
+template <bool LAST>
+__global__ void __launch_bounds__(64) k_select(SearchDev* probs, float th, int bMono, float nnratio, int checkOri) {
+    __shared__ int s_cur[kMaxFrameKeys];
+    __shared__ int s_nh;
+    SearchDev& P = probs[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int N = P.cur.N;
+    for (int i = lane; i < N; i += 64) s_cur[i] = P.curMP[i];
+    if (lane == 0) s_nh = 0;
+    __syncthreads();
+    bool bF = false, bB = false;
+    if (LAST) fwd_bwd(P, bMono != 0, bF, bB);
+    int nmatches = 0;
+    auto occupied = [&](int idx) {
+        const int m = s_cur[idx];
+        return m >= 0 && P.mpObs[m] > 0;
+    };
+    for (int q = 0; q < P.nq; q++) {
+        const int cnt = P.qinfo[q].x;
+        if (cnt <= 0) continue;
+        const int kk = cnt < kTopK ? cnt : kTopK;
+        int2 e = make_int2(256, -1);
+        bool free_ = false;
+        if (lane < kk) {
+            e = P.topk[(size_t)q * kTopK + lane];
+            free_ = !occupied(e.y);
+        }
+        uint64_t m = __ballot(free_);
+        int bestDist = 256, bestIdx = -1, bestDist2 = 256, bestLevel = -1, bestLevel2 = -1;
+        bool resolved = true;
+        if (LAST) {
+            if (m) {
+                const int f = __ffsll((long long)m) - 1;
+                bestDist = __shfl(e.x, f, 64);
+                bestIdx = __shfl(e.y, f, 64);
+            } else if (cnt > kTopK) {
+                resolved = false;
+            }
+        } else {
+            const int nfree = __popcll(m);
+            if (nfree >= 2 || (nfree == 1 && cnt <= kTopK) || (nfree == 0 && cnt <= kTopK)) {
+                if (nfree >= 1) {
+                    const int f = __ffsll((long long)m) - 1;
+                    bestDist = __shfl(e.x, f, 64);
+                    bestIdx = __shfl(e.y, f, 64);
+                    const uint64_t m2 = m & (m - 1);
+                    if (m2) {
+                        const int f2 = __ffsll((long long)m2) - 1;
+                        bestDist2 = __shfl(e.x, f2, 64);
+                        const int i2 = __shfl(e.y, f2, 64);
+                        bestLevel2 = P.cur.keysUn[i2].octave;
+                    }
+                    bestLevel = P.cur.keysUn[bestIdx].octave;
+                }
+            } else {
+                resolved = false;
+            }
+        }
+        if (!resolved) {
+            // every kept candidate is taken: rescan this query with occupancy (rare)
+            if (lane == 0) {
+                int2 top2[2];
+                int c2;
+                if (LAST) {
+                    const LastQuery lq = last_query(P, q, th, bF, bB);
+                    c2 = scan_last(P, lq, occupied, top2, 1);
+                    if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
+                } else {
+                    const LocalQuery lq = local_query(P, q, th);
+                    c2 = scan_local(P, lq, occupied, top2, 2);
+                    if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; bestLevel = P.cur.keysUn[bestIdx].octave; }
+                    if (c2 > 1) { bestDist2 = top2[1].x; bestLevel2 = P.cur.keysUn[top2[1].y].octave; }
+                }
+            }
+            bestDist = __shfl(bestDist, 0, 64);
+            bestIdx = __shfl(bestIdx, 0, 64);
+            bestDist2 = __shfl(bestDist2, 0, 64);
+            bestLevel = __shfl(bestLevel, 0, 64);
+            bestLevel2 = __shfl(bestLevel2, 0, 64);
+        }
+        if (bestDist <= TH_HIGH) {
+            if (LAST) {
+                if (lane == 0) {
+                    s_cur[bestIdx] = P.lastMP[q];
+                    if (checkOri) {
+                        float rot = P.last.keysUn[q].angle - P.cur.keysUn[bestIdx].angle;
+                        if (rot < 0.0f) rot += 360.0f;
+                        int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
+                        if (bin == HISTO_LENGTH) bin = 0;
+                        P.hist[s_nh] = make_int2(bin, bestIdx);
+                        s_nh++;
+                    }
+                }
+                nmatches++;
+            } else {
+                if (!(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2)) {
+                    if (lane == 0) s_cur[bestIdx] = P.mpIndex[q];
+                    nmatches++;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (LAST && checkOri) {
+        __syncthreads();
+        if (lane == 0) {
+            const int nh = s_nh;
+            int sizes[HISTO_LENGTH];
+            for (int b = 0; b < HISTO_LENGTH; b++) sizes[b] = 0;
+            for (int k = 0; k < nh; k++) sizes[P.hist[k].x]++;
+            // ComputeThreeMaxima, ORBmatcher.cc:1601-1642
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < HISTO_LENGTH; i++) {
+                const int s = sizes[i];
+                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+                else if (s > max3) { max3 = s; ind3 = i; }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+            for (int b = 0; b < HISTO_LENGTH; b++) {
+                if (b == ind1 || b == ind2 || b == ind3) continue;
+                for (int k = 0; k < nh; k++)
+                    if (P.hist[k].x == b) { s_cur[P.hist[k].y] = -1; nmatches--; }
+            }
+        }
+        nmatches = __shfl(nmatches, 0, 64);
+    }
+    __syncthreads();
+    for (int i = lane; i < N; i += 64) P.curMP[i] = s_cur[i];
+    if (lane == 0) *P.nmatches = nmatches;
+}
+
+// CSR candidate mode: one wave per query, lanes over candidates; (dist<<20 | k)
+// keys make the wave min pick the earliest candidate among equal distances.
+__global__ void __launch_bounds__(256) k_csr_hamming(const uint8_t* __restrict__ q, int nq, const uint8_t* __restrict__ t,
+                                                     const int* __restrict__ off, const int* __restrict__ cand,
+                                                     int* __restrict__ dist, int* __restrict__ best_idx,
+                                                     int* __restrict__ best_dist, int* __restrict__ second_dist) {
+    const int lane = threadIdx.x & 63;
+    const int qi = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (qi >= nq) return;
+    const int b = off[qi], e = off[qi + 1];
+    const uint8_t* qd = q + 32 * (size_t)qi;
+    unsigned long long k1 = ~0ull, k2 = ~0ull;
+    for (int k = b + lane; k < e; k += 64) {
+        const int d = hamming32(qd, t + 32 * (size_t)cand[k]);
+        dist[k] = d;
+        const unsigned long long key = ((unsigned long long)d << 32) | (unsigned)(k - b);
+        if (key < k1) { k2 = k1; k1 = key; }
+        else if (key < k2) k2 = key;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long o1 = __shfl_xor(k1, o, 64), o2 = __shfl_xor(k2, o, 64);
+        const unsigned long long n1 = o1 < k1 ? o1 : k1;
+        const unsigned long long hi = o1 < k1 ? k1 : o1;
+        unsigned long long n2 = o2 < k2 ? o2 : k2;
+        n2 = hi < n2 ? hi : n2;
+        k1 = n1;
+        k2 = n2;
+    }
+    if (lane == 0) {
+        best_idx[qi] = k1 == ~0ull ? -1 : cand[b + (int)(k1 & 0xffffffffu)];
+        best_dist[qi] = k1 == ~0ull ? 256 : (int)(k1 >> 32);
+        second_dist[qi] = k2 == ~0ull ? 256 : (int)(k2 >> 32);
+    }
+}
+
+// --------------------------------------------------------------------- host
+Matcher::~Matcher() {
+    if (d_scratch_) (void)hipFree(d_scratch_);
+    if (d_probs_) (void)hipFree(d_probs_);
+    if (d_arena_) (void)hipFree(d_arena_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+int Matcher::init_device() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
+    ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    return 0;
+}
+
+int Matcher::arena_reserve(size_t bytes) {
+    arena_used_ = 0;
+    if (bytes <= arena_cap_) return 0;
+    if (d_arena_) (void)hipFree(d_arena_);
+    d_arena_ = nullptr;
+    arena_cap_ = 0;
+    ORB_HIP_CHECK(hipMalloc(&d_arena_, bytes));
+    arena_cap_ = bytes;
+    return 0;
+}
+
+void* Matcher::arena_alloc(size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    if (arena_used_ + bytes > arena_cap_) return nullptr;
+    void* p = (char*)d_arena_ + arena_used_;
+    arena_used_ += bytes;
+    return p;
+}
+
+int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastMode) {
+    const int np = (int)probs.size();
+    if (np == 0) return 0;
+    size_t need = 0;
+    int maxq = 0;
+    for (auto& p : probs) {
+        if (p.cur.N > kMaxFrameKeys || p.cur.N < 0 || p.nq < 0) return -1;
+        need += ((size_t)(kGridCells + 1 + p.cur.N) * 4 + 255) & ~(size_t)255;
+        need += ((size_t)p.nq * (kTopK * 8 + 16 + 8) + 255) & ~(size_t)255;
+        maxq = std::max(maxq, p.nq);
+    }
+    if (need > scratch_cap_) {
+        if (d_scratch_) (void)hipFree(d_scratch_);
+        scratch_cap_ = need * 2;
+        ORB_HIP_CHECK(hipMalloc(&d_scratch_, scratch_cap_));
+    }
+    char* s = (char*)d_scratch_;
+    for (auto& p : probs) {
+        p.gridStart = (int*)s;
+        p.gridIdx = p.gridStart + kGridCells + 1;
+        s += ((size_t)(kGridCells + 1 + p.cur.N) * 4 + 255) & ~(size_t)255;
+        p.topk = (int2*)s;
+        p.qinfo = (int4*)(p.topk + (size_t)p.nq * kTopK);
+        p.hist = (int2*)(p.qinfo + p.nq);
+        s += ((size_t)p.nq * (kTopK * 8 + 16 + 8) + 255) & ~(size_t)255;
+    }
+    const size_t pb = sizeof(SearchDev) * np;
+    if (pb > probs_cap_) {
+        if (d_probs_) (void)hipFree(d_probs_);
+        probs_cap_ = pb * 2;
+        ORB_HIP_CHECK(hipMalloc(&d_probs_, probs_cap_));
+    }
+    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, probs.data(), pb, hipMemcpyHostToDevice, stream_));
+    SearchDev* dp = (SearchDev*)d_probs_;
+    hipLaunchKernelGGL(k_build_grid, dim3(np), dim3(256), 0, stream_, dp);
+    if (maxq > 0) {
+        if (lastMode) {
+            hipLaunchKernelGGL(k_candidates<true>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, (int)bMono);
+            hipLaunchKernelGGL(k_select<true>, dim3(np), dim3(64), 0, stream_, dp, th, (int)bMono, nnratio_, (int)checkOri_);
+        } else {
+            hipLaunchKernelGGL(k_candidates<false>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0);
+            hipLaunchKernelGGL(k_select<false>, dim3(np), dim3(64), 0, stream_, dp, th, 0, nnratio_, 0);
+        }
+    }
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int Matcher::search_last(std::vector<SearchDev>& probs, float th, bool bMono) { return run(probs, th, bMono, true); }
+int Matcher::search_local(std::vector<SearchDev>& probs, float th) { return run(probs, th, false, false); }
+
+int Matcher::candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, const int* off, const int* cand, int* dist,
+                        int* best_idx, int* best_dist, int* second_dist) {
+    (void)nt;
+    if (nq <= 0) return 0;
+    hipLaunchKernelGGL(k_csr_hamming, dim3((nq + 3) / 4), dim3(256), 0, stream_, q, nq, t, off, cand, dist, best_idx,
+                       best_dist, second_dist);
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace orbgpu

@@ -1,0 +1,95 @@
+// orb_match.hpp -- gfx950 guided Hamming matching (see orb_match.hip).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "orb_common.hpp"
+#include "orb_extract.hpp"
+
+namespace orbgpu {
+
+constexpr int kGridCols = 64;   // FRAME_GRID_COLS, Frame.h:37
+constexpr int kGridRows = 48;   // FRAME_GRID_ROWS, Frame.h:38
+constexpr int kGridCells = kGridCols * kGridRows;
+constexpr int kTopK = 8;        // candidates kept per query for the greedy replay
+constexpr int kMaxFrameKeys = 4096;
+
+struct FrameDev {
+    int N;
+    const orb_kp_dev* keysUn;
+    const uint8_t* desc;
+    const float* uRight;  // may be null
+    float minX, maxX, minY, maxY, gridWInv, gridHInv;
+    const float* scale;
+    int nlevels;
+    float fx, fy, cx, cy, bf, b;
+    const float* Tcw;
+};
+
+// One SearchByProjection problem (one (cur, last) pair, or one (F, map points) set).
+struct SearchDev {
+    FrameDev cur;
+    // LastFrame mode
+    FrameDev last;
+    const orb_kp_dev* lastKeys;
+    const int* lastMP;
+    const uint8_t* lastOutlier;
+    // MapPoints mode (per query arrays)
+    const uint8_t* inView;
+    const float* projX;
+    const float* projXR;
+    const float* projY;
+    const int* level;
+    const float* viewCos;
+    const int* mpIndex;
+    int nq;
+    // map point table
+    const float* mpPos;
+    const uint8_t* mpDesc;
+    const int* mpObs;
+    // in/out
+    int* curMP;
+    int* nmatches;
+    // scratch (device)
+    int* gridStart;   // kGridCells+1
+    int* gridIdx;     // cur.N
+    int2* topk;       // nq * kTopK  (x = dist, y = candidate index)
+    int4* qinfo;      // nq: x = ncand (-1 skip), y = bits(u), z = bits(v), w = bits(radius/r)
+    int2* hist;       // nq (bin, idx)
+};
+
+class Matcher {
+public:
+    Matcher(float nnratio, bool checkOri) : nnratio_(nnratio), checkOri_(checkOri) {}
+    ~Matcher();
+    int init_device();
+    void set_device_pointers(bool on) { device_ptrs_ = on; }
+    bool device_pointers() const { return device_ptrs_; }
+    // Runs `n` SearchByProjection(Cur, Last) problems in one set of launches.
+    int search_last(std::vector<SearchDev>& probs, float th, bool bMono);
+    int search_local(std::vector<SearchDev>& probs, float th);
+    int candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, const int* off, const int* cand, int* dist,
+                   int* best_idx, int* best_dist, int* second_dist);
+    hipStream_t stream() const { return stream_; }
+    float nnratio() const { return nnratio_; }
+    bool check_ori() const { return checkOri_; }
+
+    // device arena for host-pointer mode: reserve() resets it, alloc() carves it
+    int arena_reserve(size_t bytes);
+    void* arena_alloc(size_t bytes);
+
+private:
+    int run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastMode);
+    float nnratio_;
+    bool checkOri_;
+    bool device_ptrs_ = false;
+    hipStream_t stream_ = nullptr;
+    void* d_scratch_ = nullptr;
+    size_t scratch_cap_ = 0;
+    void* d_probs_ = nullptr;
+    size_t probs_cap_ = 0;
+    void* d_arena_ = nullptr;
+    size_t arena_cap_ = 0, arena_used_ = 0;
+};
+
+}  // namespace orbgpu

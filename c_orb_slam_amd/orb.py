@@ -1,0 +1,247 @@
+"""Host-side mirror of the reference ORBextractor / ORBmatcher interface.
+
+Same names, argument meaning and error behaviour as the reference classes
+(include/ORBextractor.h, include/ORBmatcher.h); every call goes through the
+C ABI of include/orbslam_gpu.h into the HIP library.  cv::Mat / vector<KeyPoint>
+become numpy arrays: keypoints are KP_DTYPE records (cv::KeyPoint layout),
+descriptors (N, 32) uint8, map-point pointers int32 indices (-1 = NULL).
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import (KP_DTYPE, ORB_E_CAPACITY, OrbGpuError, check, lib, orb_frame, orb_mappoints, ptr)
+
+FRAME_GRID_COLS, FRAME_GRID_ROWS = 64, 48   # Frame.h:37-38
+
+
+class ORBextractor:
+    """ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)  (ORBextractor.cc:410)."""
+
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST,
+                 max_width=2048, max_height=2048, max_batch=1):
+        self._L = lib()
+        h = C.c_void_p()
+        check(self._L.ORBextractor_create(int(nfeatures), float(scaleFactor), int(nlevels), int(iniThFAST),
+                                          int(minThFAST), int(max_width), int(max_height), int(max_batch),
+                                          C.byref(h)), "ORBextractor_create")
+        self._h = h
+        self.nfeatures, self.nlevels = int(nfeatures), int(nlevels)
+        self.max_batch = int(max_batch)
+        self._cap = max(64, 2 * int(nfeatures) + 64)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ORBextractor_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    # operator()(image, mask, keypoints, descriptors) -- ORBextractor.cc:1043
+    def __call__(self, image, mask=None):
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        if img.size == 0:
+            return np.zeros(0, KP_DTYPE), None
+        while True:
+            kps = np.zeros(self._cap, KP_DTYPE)
+            desc = np.zeros((self._cap, 32), np.uint8)
+            n = C.c_int()
+            rc = self._L.ORBextractor_extract(self._h, ptr(img), img.shape[1], img.shape[0], img.strides[0],
+                                              ptr(kps), ptr(desc), self._cap, C.byref(n))
+            if rc == ORB_E_CAPACITY:
+                self._cap *= 2
+                continue
+            check(rc, "ORBextractor_extract")
+            n = n.value
+            return kps[:n].copy(), (desc[:n].copy() if n else None)
+
+    def extract_batch(self, images):
+        imgs = np.ascontiguousarray(images, dtype=np.uint8)
+        B, H, W = imgs.shape
+        while True:
+            kps = np.zeros((B, self._cap), KP_DTYPE)
+            desc = np.zeros((B, self._cap, 32), np.uint8)
+            n = np.zeros(B, np.int32)
+            rc = self._L.ORBextractor_extract_batch(self._h, ptr(imgs), B, W, H, imgs.strides[1], imgs.strides[0],
+                                                    0, ptr(kps), ptr(desc), self._cap, 0, ptr(n))
+            if rc == ORB_E_CAPACITY:
+                self._cap *= 2
+                continue
+            check(rc, "ORBextractor_extract_batch")
+            return [(kps[b, :n[b]].copy(), desc[b, :n[b]].copy()) for b in range(B)]
+
+    def extract_device(self, d_imgs_ptr, B, W, H, step, img_stride, d_kps_ptr, d_desc_ptr, cap):
+        """HBM-resident form: all pointers are device addresses; returns per-image counts."""
+        n = np.zeros(B, np.int32)
+        check(self._L.ORBextractor_extract_batch(self._h, C.c_void_p(d_imgs_ptr), B, W, H, step, img_stride, 1,
+                                                 C.c_void_p(d_kps_ptr), C.c_void_p(d_desc_ptr), cap, 1, ptr(n)),
+              "ORBextractor_extract_batch(device)")
+        return n
+
+    def image_pyramid_level(self, level, index=0):
+        """mvImagePyramid[level] WITH its 19-px border (ORBextractor.h:85)."""
+        w, h = C.c_int(), C.c_int()
+        check(self._L.ORBextractor_get_level(self._h, index, level, None, 0, C.byref(w), C.byref(h)), "get_level")
+        out = np.zeros((h.value + 38, w.value + 38), np.uint8)
+        check(self._L.ORBextractor_get_level(self._h, index, level, ptr(out), out.strides[0], C.byref(w),
+                                             C.byref(h)), "get_level")
+        return out
+
+    def _tables(self):
+        nl = self.nlevels
+        t = [np.zeros(nl, np.float32) for _ in range(4)] + [np.zeros(nl, np.int32)]
+        check(self._L.ORBextractor_get_scale_tables(self._h, *[ptr(a) for a in t]), "get_scale_tables")
+        return t
+
+    def GetLevels(self):
+        return self.nlevels
+
+    def GetScaleFactor(self):
+        n, s = C.c_int(), C.c_float()
+        check(self._L.ORBextractor_get_levels(self._h, C.byref(n), C.byref(s)))
+        return s.value
+
+    def GetScaleFactors(self):
+        return self._tables()[0]
+
+    def GetInverseScaleFactors(self):
+        return self._tables()[1]
+
+    def GetScaleSigmaSquares(self):
+        return self._tables()[2]
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._tables()[3]
+
+    def features_per_level(self):
+        return self._tables()[4]
+
+    @property
+    def stream(self):
+        return self._L.ORBextractor_stream(self._h)
+
+    def last_timings(self):
+        t = np.zeros(6, np.float32)
+        check(self._L.ORBextractor_last_timings(self._h, ptr(t)))
+        return dict(zip(["pyramid", "blur", "fast_cells", "compact", "octree_host", "orient_desc"], t.tolist()))
+
+
+class Frame:
+    """The Frame fields the matcher reads (Frame.h).  Arrays are host numpy."""
+
+    def __init__(self, keysUn, desc, scale_factors, Tcw, fx, fy, cx, cy, bf=0.0, width=None, height=None,
+                 uRight=None, minX=0.0, maxX=None, minY=0.0, maxY=None):
+        self.keysUn = np.ascontiguousarray(keysUn, KP_DTYPE)
+        self.N = len(self.keysUn)
+        self.desc = np.ascontiguousarray(desc if desc is not None else np.zeros((0, 32), np.uint8), np.uint8)
+        self.uRight = None if uRight is None else np.ascontiguousarray(uRight, np.float32)
+        self.scale = np.ascontiguousarray(scale_factors, np.float32)
+        self.Tcw = np.ascontiguousarray(Tcw, np.float32).reshape(4, 4)
+        self.fx, self.fy, self.cx, self.cy = (np.float32(v) for v in (fx, fy, cx, cy))
+        self.bf = np.float32(bf)
+        self.b = np.float32(np.float32(bf) / np.float32(fx))   # mb = mbf/fx (Frame.cc:114)
+        # ComputeImageBounds (no distortion), Frame.cc:464-469
+        self.minX, self.minY = np.float32(minX), np.float32(minY)
+        self.maxX = np.float32(width if maxX is None else maxX)
+        self.maxY = np.float32(height if maxY is None else maxY)
+        self.gridWInv = np.float32(np.float32(FRAME_GRID_COLS) / (self.maxX - self.minX))
+        self.gridHInv = np.float32(np.float32(FRAME_GRID_ROWS) / (self.maxY - self.minY))
+
+    def cstruct(self):
+        f = orb_frame()
+        f.N = self.N
+        f.keysUn = self.keysUn.ctypes.data if self.N else None
+        f.desc = self.desc.ctypes.data if self.N else None
+        f.uRight = None if self.uRight is None else self.uRight.ctypes.data
+        f.minX, f.maxX, f.minY, f.maxY = self.minX, self.maxX, self.minY, self.maxY
+        f.gridWInv, f.gridHInv = self.gridWInv, self.gridHInv
+        f.scaleFactors = self.scale.ctypes.data
+        f.nlevels = len(self.scale)
+        f.fx, f.fy, f.cx, f.cy, f.bf, f.b = self.fx, self.fy, self.cx, self.cy, self.bf, self.b
+        f.Tcw = self.Tcw.ctypes.data
+        return f
+
+
+class MapPoints:
+    def __init__(self, pos, desc, observations):
+        self.pos = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+        self.desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        self.obs = np.ascontiguousarray(observations, np.int32)
+        self.n = len(self.pos)
+
+    def cstruct(self):
+        m = orb_mappoints()
+        m.n = self.n
+        m.pos = self.pos.ctypes.data if self.n else None
+        m.desc = self.desc.ctypes.data if self.n else None
+        m.observations = self.obs.ctypes.data if self.n else None
+        return m
+
+
+class ORBmatcher:
+    """ORBmatcher(nnratio=0.6, checkOri=True)  (ORBmatcher.cc:41-43)."""
+
+    TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30
+
+    def __init__(self, nnratio=0.6, checkOri=True):
+        self._L = lib()
+        h = C.c_void_p()
+        check(self._L.ORBmatcher_create(float(nnratio), int(bool(checkOri)), C.byref(h)), "ORBmatcher_create")
+        self._h = h
+        self.mfNNratio, self.mbCheckOrientation = float(nnratio), bool(checkOri)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ORBmatcher_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @staticmethod
+    def DescriptorDistance(a, b):
+        a = np.ascontiguousarray(a, np.uint8)
+        b = np.ascontiguousarray(b, np.uint8)
+        return lib().ORBmatcher_DescriptorDistance(ptr(a), ptr(b))
+
+    def SearchByProjection_LastFrame(self, cur: Frame, cur_mp, last: Frame, last_keys, last_mp, last_outlier,
+                                     mps: MapPoints, th, bMono):
+        """SearchByProjection(CurrentFrame, LastFrame, th, bMono) (ORBmatcher.cc:1328).
+        cur_mp is updated in place (CurrentFrame.mvpMapPoints); returns nmatches."""
+        assert cur_mp.dtype == np.int32 and cur_mp.flags.c_contiguous and len(cur_mp) == cur.N
+        lk = np.ascontiguousarray(last_keys, KP_DTYPE)
+        lm = np.ascontiguousarray(last_mp, np.int32)
+        lo = np.ascontiguousarray(last_outlier, np.uint8)
+        cf, lf, mp = cur.cstruct(), last.cstruct(), mps.cstruct()
+        n = C.c_int()
+        check(self._L.ORBmatcher_SearchByProjection_LastFrame(self._h, C.byref(cf), ptr(cur_mp), C.byref(lf),
+                                                              ptr(lk), ptr(lm), ptr(lo), C.byref(mp),
+                                                              float(th), int(bool(bMono)), C.byref(n)),
+              "SearchByProjection(LastFrame)")
+        return n.value
+
+    def SearchByProjection_MapPoints(self, F: Frame, cur_mp, track_in_view, proj_x, proj_xr, proj_y, level,
+                                     view_cos, mp_index, mps: MapPoints, th=1.0):
+        """SearchByProjection(F, vpMapPoints, th) (ORBmatcher.cc:45); cur_mp updated in place."""
+        assert cur_mp.dtype == np.int32 and len(cur_mp) == F.N
+        a = [np.ascontiguousarray(track_in_view, np.uint8), np.ascontiguousarray(proj_x, np.float32),
+             np.ascontiguousarray(proj_xr, np.float32), np.ascontiguousarray(proj_y, np.float32),
+             np.ascontiguousarray(level, np.int32), np.ascontiguousarray(view_cos, np.float32),
+             np.ascontiguousarray(mp_index, np.int32)]
+        f, mp = F.cstruct(), mps.cstruct()
+        n = C.c_int()
+        check(self._L.ORBmatcher_SearchByProjection_MapPoints(self._h, C.byref(f), ptr(cur_mp), len(a[0]),
+                                                              *[ptr(x) for x in a], C.byref(mp), float(th),
+                                                              C.byref(n)), "SearchByProjection(MapPoints)")
+        return n.value
+
+    def SearchCandidates(self, qdesc, tdesc, offsets, cand):
+        q = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
+        t = np.ascontiguousarray(tdesc, np.uint8).reshape(-1, 32)
+        off = np.ascontiguousarray(offsets, np.int32)
+        c = np.ascontiguousarray(cand, np.int32)
+        nq = len(q)
+        dist = np.zeros(max(len(c), 1), np.int32)
+        bi, bd, sd = (np.zeros(max(nq, 1), np.int32) for _ in range(3))
+        check(self._L.ORBmatcher_SearchCandidates(self._h, ptr(q), nq, ptr(t), len(t), ptr(off), ptr(c), ptr(dist),
+                                                  ptr(bi), ptr(bd), ptr(sd)), "SearchCandidates")
+        return dist[:len(c)], bi[:nq], bd[:nq], sd[:nq]

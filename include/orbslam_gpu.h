@@ -1,0 +1,178 @@
+/*
+ * orbslam_gpu.h -- C ABI of the MI355X-native ORB-SLAM2 per-frame hot path.
+ *
+ * Drop-in boundary for junejunejune/c_orb_slam (ORB-SLAM2, C++11).  The
+ * reference exposes these operations as C++ class methods taking cv::Mat /
+ * std::vector; each entry point below replaces one of them with plain
+ * pointers + sizes.  The C++ adapter in
+ * c_orb_slam_amd/adapter/ re-exposes the reference class signatures on top
+ * of this header; INTEGRATION.md shows the binding a maintainer adds.
+ *
+ * Conventions
+ *   - every call returns int status: ORB_OK (0) or a negative ORB_E_*;
+ *   - the caller owns all host buffers (pointer + capacity; counts are
+ *     written to *n_out; ORB_E_CAPACITY if a buffer is too small);
+ *   - each handle owns its device workspace and one HIP stream; handles are
+ *     not shared between threads (the reference calls the extractor from two
+ *     threads per stereo frame, Frame.cc:78-81: create one handle per thread);
+ *   - there is no CPU fallback: without a usable gfx950 device, create()
+ *     returns ORB_E_NODEVICE.
+ */
+#ifndef ORBSLAM_GPU_H
+#define ORBSLAM_GPU_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORB_OK 0
+#define ORB_E_INVALID -1
+#define ORB_E_HIP -2
+#define ORB_E_CAPACITY -3
+#define ORB_E_NODEVICE -4
+
+/* cv::KeyPoint memory layout (28 B): pt.x, pt.y, size, angle, response, octave, class_id */
+typedef struct orb_kp {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orb_kp;
+
+/* Library info: 1 if a HIP device is usable, else 0 (never aborts). */
+int orbgpu_device_available(void);
+const char* orbgpu_version(void);
+
+/* ======================================================================
+ * ORBextractor  (reference include/ORBextractor.h:51-113, src/ORBextractor.cc)
+ * ====================================================================== */
+typedef struct ORBextractor_t* ORBextractor_h;
+
+/* ORBextractor::ORBextractor(int nfeatures, float scaleFactor, int nlevels,
+ *                            int iniThFAST, int minThFAST)   ORBextractor.cc:410-470
+ * max_width/max_height size the device pyramid (images up to that size). */
+int ORBextractor_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST,
+                        int minThFAST, int max_width, int max_height, int max_batch,
+                        ORBextractor_h* out);
+int ORBextractor_destroy(ORBextractor_h h);
+
+/* ORBextractor::operator()(image, mask(ignored), keypoints, descriptors)
+ *                                                          ORBextractor.cc:1043-1105
+ * img: u8 grey, row stride `step`.  kps: capacity entries; desc: capacity x 32.
+ * Empty image (w or h == 0) returns ORB_OK with *n_out = 0 (1046-1047). */
+int ORBextractor_extract(ORBextractor_h h, const uint8_t* img, int width, int height, int step,
+                         orb_kp* kps, uint8_t* desc, int capacity, int* n_out);
+
+/* Batched form: `batch` images of equal size; image b at imgs + b*img_stride.
+ * imgs_on_device != 0: imgs is a device pointer (HBM-resident input).
+ * Outputs for image b at kps + b*cap_per_image, desc + b*cap_per_image*32;
+ * outputs_on_device != 0: kps/desc are device pointers.  n_out[b] host. */
+int ORBextractor_extract_batch(ORBextractor_h h, const uint8_t* imgs, int batch, int width,
+                               int height, int step, size_t img_stride, int imgs_on_device,
+                               orb_kp* kps, uint8_t* desc, int cap_per_image,
+                               int outputs_on_device, int* n_out);
+
+/* mvImagePyramid[level] (ORBextractor.h:85) of image `index` of the last call,
+ * copied to host WITH its 19-px REFLECT_101 border (Frame.cc:573-580 reads it).
+ * dst must hold (w+38)*(h+38) bytes at stride dst_step; *w,*h = unpadded dims. */
+int ORBextractor_get_level(ORBextractor_h h, int index, int level, uint8_t* dst, int dst_step,
+                           int* w, int* h_);
+/* GetLevels/GetScaleFactor/GetScaleFactors/GetInverseScaleFactors/
+ * GetScaleSigmaSquares/GetInverseScaleSigmaSquares   ORBextractor.h:63-85 */
+int ORBextractor_get_levels(ORBextractor_h h, int* nlevels, float* scaleFactor);
+int ORBextractor_get_scale_tables(ORBextractor_h h, float* scale, float* invScale,
+                                  float* sigma2, float* invSigma2, int* nFeaturesPerLevel);
+/* HIP stream (hipStream_t) the extractor launches on; for event timing. */
+void* ORBextractor_stream(ORBextractor_h h);
+/* Per-stage device time of the last call (ms), from HIP events:
+ * [0]=pyramid [1]=blur [2]=FAST cells [3]=compaction [4]=octree(host) [5]=orientation+rBRIEF */
+int ORBextractor_last_timings(ORBextractor_h h, float* ms6);
+
+/* ======================================================================
+ * ORBmatcher  (reference include/ORBmatcher.h:41-103, src/ORBmatcher.cc)
+ * ====================================================================== */
+typedef struct ORBmatcher_t* ORBmatcher_h;
+
+/* ORBmatcher::ORBmatcher(float nnratio=0.6, bool checkOri=true)  ORBmatcher.cc:41-43 */
+int ORBmatcher_create(float nnratio, int checkOri, ORBmatcher_h* out);
+int ORBmatcher_destroy(ORBmatcher_h h);
+/* Pointer space of every array argument below (and inside orb_frame /
+ * orb_mappoints): 0 = host memory (default, copied per call), 1 = device
+ * (HBM-resident, e.g. ORBextractor_extract_batch outputs); counts stay host. */
+int ORBmatcher_set_device_pointers(ORBmatcher_h h, int on);
+void* ORBmatcher_stream(ORBmatcher_h h);
+
+/* static int ORBmatcher::DescriptorDistance(a, b)   ORBmatcher.cc:1647-1663 (host) */
+int ORBmatcher_DescriptorDistance(const uint8_t* a, const uint8_t* b);
+
+/* Frame view used for guided search (Frame.h fields the matcher reads).
+ * Grid: Frame::mGrid (64 x 48, Frame.h:37-38) is rebuilt on device from
+ * kpsUn (AssignFeaturesToGrid, Frame.cc:230-245). */
+typedef struct orb_frame {
+    int N;
+    const orb_kp* keysUn;        /* mvKeysUn (N) */
+    const uint8_t* desc;         /* mDescriptors (N x 32) */
+    const float* uRight;         /* mvuRight (N) or NULL (monocular) */
+    float minX, maxX, minY, maxY;/* mnMinX.. (Frame.cc:442-470) */
+    float gridWInv, gridHInv;    /* mfGridElementWidthInv/HeightInv */
+    const float* scaleFactors;   /* mvScaleFactors */
+    int nlevels;
+    float fx, fy, cx, cy, bf, b; /* intrinsics, mbf, mb */
+    const float* Tcw;            /* 4x4 row-major float (mTcw) */
+} orb_frame;
+
+/* Map point table shared by the search calls (MapPoint fields read by the matcher). */
+typedef struct orb_mappoints {
+    int n;
+    const float* pos;            /* GetWorldPos (n x 3) */
+    const uint8_t* desc;         /* GetDescriptor (n x 32) */
+    const int* observations;     /* Observations() (n) */
+} orb_mappoints;
+
+/* int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, float th, bool bMono)
+ *                                                          ORBmatcher.cc:1328-1470
+ * last_mp[i]: map point index of LastFrame.mvpMapPoints[i] (-1 = NULL);
+ * last_outlier[i]: LastFrame.mvbOutlier; last_keys: LastFrame.mvKeys (octave),
+ * last_keysUn: LastFrame.mvKeysUn (angle).
+ * cur_mp (in/out, N of current): CurrentFrame.mvpMapPoints as indices (-1 = NULL).
+ * *nmatches = return value of the reference. */
+int ORBmatcher_SearchByProjection_LastFrame(ORBmatcher_h h, const orb_frame* cur, int32_t* cur_mp,
+                                            const orb_frame* last, const orb_kp* last_keys,
+                                            const int32_t* last_mp, const uint8_t* last_outlier,
+                                            const orb_mappoints* mps, float th, int bMono,
+                                            int* nmatches);
+
+/* Batched form of the above over `npairs` independent (cur, last) pairs in ONE launch. */
+int ORBmatcher_SearchByProjection_LastFrame_batch(ORBmatcher_h h, int npairs, const orb_frame* cur,
+                                                  int32_t* const* cur_mp, const orb_frame* last,
+                                                  const orb_kp* const* last_keys,
+                                                  const int32_t* const* last_mp,
+                                                  const uint8_t* const* last_outlier,
+                                                  const orb_mappoints* mps, float th, int bMono,
+                                                  int* nmatches);
+
+/* int SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, float th)
+ *                                                          ORBmatcher.cc:45-129
+ * Per map point j (order = vpMapPoints order): track_in_view (mbTrackInView),
+ * proj_x/proj_xr/proj_y (mTrackProjX/XR/Y), level (mnTrackScaleLevel),
+ * view_cos (mTrackViewCos), mp_index (index into mps, written to cur_mp). */
+int ORBmatcher_SearchByProjection_MapPoints(ORBmatcher_h h, const orb_frame* F, int32_t* cur_mp,
+                                            int n, const uint8_t* track_in_view,
+                                            const float* proj_x, const float* proj_xr,
+                                            const float* proj_y, const int32_t* level,
+                                            const float* view_cos, const int32_t* mp_index,
+                                            const orb_mappoints* mps, float th, int* nmatches);
+
+/* Hamming distances for CSR candidate lists (the inner loop of every Search*):
+ * query q (descriptor qdesc[q]) against train rows cand[off[q] .. off[q+1]).
+ * Writes dist[k] for every candidate k and best/second per query
+ * (strict '<', earliest candidate wins ties, like the reference loops). */
+int ORBmatcher_SearchCandidates(ORBmatcher_h h, const uint8_t* qdesc, int nq,
+                                const uint8_t* tdesc, int nt, const int32_t* off,
+                                const int32_t* cand, int32_t* dist, int32_t* best_idx,
+                                int32_t* best_dist, int32_t* second_dist);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

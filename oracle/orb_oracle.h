@@ -1,0 +1,146 @@
+/*
+ * orb_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C11, built with -ffp-contract=off) of the reference
+ * junejunejune/c_orb_slam per-frame hot path.  It is the parity CHECKER for the
+ * HIP product in c_orb_slam_amd/: only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load it.  The product never links it.
+ *
+ * Parity status (see DESIGN.md "Oracle"): the reference cannot be compiled in
+ * this image (needs OpenCV/Eigen, absent) and ships no tests or golden
+ * vectors, so the OpenCV call sites are restated from OpenCV 3.2's scalar
+ * code paths ("parity unpinned" at that boundary).  What IS pinned:
+ *   - glibc sinf/cosf restatement: exhaustively equal to the host libm over
+ *     every float in [0, 2*pi] (tests/test_oracle_kat.py);
+ *   - glibc rand() (TYPE_3 additive feedback) against the host libc;
+ *   - the BRIEF pattern table parsed from the reference source.
+ * Every function cites the reference file:line it follows.
+ */
+#ifndef ORB_ORACLE_H
+#define ORB_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* cv::KeyPoint layout (28 bytes): pt.x, pt.y, size, angle, response, octave, class_id */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} ora_kp;
+
+/* ---- OpenCV-semantic primitives (ocv_semantics.c) ---------------------- */
+int   ora_cvRound_f(float v);
+int   ora_cvRound_d(double v);
+float ora_fastAtan2(float y, float x);
+float ora_sinf(float x);           /* glibc 2.35 sinf restatement, |x| < 120 */
+float ora_cosf(float x);           /* glibc 2.35 cosf restatement, |x| < 120 */
+/* FAST-9/16 score S = max(A,B)-1 (A,B = best dark/bright 9-arc contrast). */
+int   ora_fast_score(const uint8_t* p, int step);
+/* cv::FAST(roi, kps, th, nonmax=true) on a ROI view; returns count (raster order). */
+int   ora_fast_roi(const uint8_t* roi, int step, int cols, int rows, int th,
+                   int* xs, int* ys, int* scores, int cap);
+/* resize(INTER_LINEAR, 8U fixed point) dst (dw x dh) from src (sw x sh) */
+void  ora_resize_linear_u8(const uint8_t* src, int sstep, int sw, int sh,
+                           uint8_t* dst, int dstep, int dw, int dh);
+/* GaussianBlur 7x7 sigma 2, 8U fixed-point separable, REFLECT_101, into contiguous dst */
+void  ora_gaussian7_u8(const uint8_t* src, int sstep, int w, int h, uint8_t* dst, int dstep);
+void  ora_gaussian7_taps(int taps[7]);
+
+/* ---- ORBextractor (orb_extract.c) ---------------------------------------- */
+typedef struct ora_extractor ora_extractor;
+ora_extractor* ora_extractor_new(int nfeatures, float scaleFactor, int nlevels,
+                                 int iniThFAST, int minThFAST);
+void  ora_extractor_free(ora_extractor* e);
+/* operator()(image) -> keypoints+descriptors. Returns number of keypoints, or
+ * -(needed) if cap is too small (nothing written then). */
+int   ora_extract(ora_extractor* e, const uint8_t* img, int w, int h, int step,
+                  ora_kp* kps, uint8_t* desc, int cap);
+/* Padded pyramid level (after the last ora_extract): returns pointer to the
+ * top-left of the 19-px bordered image, its padded dims and step. */
+int   ora_extractor_level(const ora_extractor* e, int level, const uint8_t** data,
+                          int* pw, int* ph, int* step);
+int   ora_extractor_nlevels(const ora_extractor* e);
+void  ora_extractor_tables(const ora_extractor* e, float* scale, float* invScale,
+                           float* sigma2, float* invSigma2, int* nPerLevel, int* umax16);
+/* Debug taps for stage tests: candidates (pre-octree) per level, in reference order */
+int   ora_extractor_candidates(const ora_extractor* e, int level, ora_kp* out, int cap);
+/* Blurred level (contiguous w x h), valid after ora_extract */
+int   ora_extractor_blurred(const ora_extractor* e, int level, const uint8_t** data, int* w, int* h);
+
+/* ---- ORBmatcher (orb_match.c) -------------------------------------------- */
+int   ora_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Frame-side data for guided matching (Frame.h:37-38, Frame.cc:230-392) */
+#define ORA_GRID_COLS 64
+#define ORA_GRID_ROWS 48
+typedef struct {
+    int N;
+    const ora_kp* kpsUn;       /* undistorted keypoints (mvKeysUn) */
+    const uint8_t* desc;       /* N x 32 */
+    const float* uRight;       /* mvuRight (N), <0 = none; may be NULL */
+    float minX, maxX, minY, maxY;
+    float gridWInv, gridHInv;
+    const float* scaleFactors; /* per level */
+    int nlevels;
+    /* grid (built by ora_frame_build_grid): CSR over 64*48 cells, cell = ix*48+iy */
+    int* cellStart;            /* 64*48+1 */
+    int* cellIdx;              /* N */
+} ora_frame;
+void  ora_frame_build_grid(ora_frame* f);
+/* Frame::GetFeaturesInArea -> writes indices, returns count */
+int   ora_frame_features_in_area(const ora_frame* f, float x, float y, float r,
+                                 int minLevel, int maxLevel, int* out, int cap);
+
+/* SearchByProjection(Frame& Cur, const Frame& Last, th, bMono), ORBmatcher.cc:1328-1470.
+ * Last-frame map points: per last keypoint i, lastMP[i] = map point id or -1,
+ * lastOutlier[i], mpPos[id*3] world position, mpDesc[id*32] descriptor.
+ * Current frame occupancy: curMP[i2] (in/out) map point id or -1;
+ * mpObs[id] = observations of that map point.  Poses: Tcw row-major 4x4 float. */
+typedef struct {
+    const float* Tcw_cur;    /* 16 */
+    const float* Tcw_last;   /* 16 */
+    float fx, fy, cx, cy, mbf, mb;
+    const ora_kp* lastKeys;  /* mvKeys of last (octave) */
+    const ora_kp* lastKeysUn;/* mvKeysUn of last (angle) */
+    const int* lastMP;
+    const uint8_t* lastOutlier;
+    int lastN;
+    const float* mpPos;
+    const uint8_t* mpDesc;
+    const int* mpObs;
+} ora_lastframe;
+int   ora_search_by_projection_last(const ora_frame* cur, int* curMP,
+                                    const ora_lastframe* last, float th, int bMono,
+                                    float nnratio, int checkOri);
+
+/* SearchByProjection(Frame& F, const vector<MapPoint*>&, th), ORBmatcher.cc:45-129.
+ * Per map point: trackInView, projX, projXR, projY, predictedLevel, viewCos, desc. */
+typedef struct {
+    int n;
+    const uint8_t* inView;
+    const float* projX;
+    const float* projXR;
+    const float* projY;
+    const int* level;
+    const float* viewCos;
+    const uint8_t* desc;   /* n x 32 */
+    const int* mpId;       /* id written into curMP */
+} ora_localmaps;
+int   ora_search_by_projection_local(const ora_frame* f, int* curMP, const int* mpObs,
+                                     const ora_localmaps* m, float th, float nnratio);
+
+void  ora_compute_three_maxima(const int* histSizes, int L, int* ind1, int* ind2, int* ind3);
+
+/* ---- glibc rand() restatement (rng.c) ------------------------------------- */
+typedef struct { int32_t tbl[31]; int f, r; } ora_rng;
+void  ora_rng_seed(ora_rng* g, unsigned int seed);
+int   ora_rng_rand(ora_rng* g);
+int   ora_rng_random_int(ora_rng* g, int min, int max);  /* DUtils::Random::RandomInt */
+
+#ifdef __cplusplus
+}
+#endif
+#endif
