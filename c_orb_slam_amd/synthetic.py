@@ -28,16 +28,35 @@ def textured_image(rng, w=KITTI_W, h=KITTI_H, n_rects=None):
     return np.clip(np.rint(img), 0, 255).astype(np.uint8)
 
 
-def small_homography(rng, w=KITTI_W, h=KITTI_H, max_shift=3.0, max_rot_deg=1.0):
-    th = np.deg2rad(rng.uniform(-max_rot_deg, max_rot_deg))
-    tx, ty = rng.uniform(-max_shift, max_shift, size=2)
-    c, s = np.cos(th), np.sin(th)
-    cx, cy = w / 2.0, h / 2.0
-    # rotate about the image centre, then translate
-    H = np.array([[c, -s, cx - c * cx + s * cy + tx],
-                  [s, c, cy - s * cx - c * cy + ty],
-                  [0, 0, 1.0]])
-    return H
+# KITTI-00 intrinsics (Examples/Stereo/KITTI00-02.yaml:8-25); other sizes scale them.
+KITTI_K = (718.856, 718.856, 607.1928, 185.2157)
+KITTI_BF = 386.1448
+
+
+def intrinsics(w, h):
+    if (w, h) == (KITTI_W, KITTI_H):
+        return KITTI_K
+    s = w / KITTI_W
+    return (KITTI_K[0] * s, KITTI_K[1] * s, w / 2.0, h / 2.0)
+
+
+def small_rotation(rng, fx, max_shift=3.0, max_rot_deg=1.0):
+    """Camera rotation: roll <= 1 deg, pan/tilt shifting the image <= 3 px."""
+    roll = np.deg2rad(rng.uniform(-max_rot_deg, max_rot_deg))
+    yaw, pitch = rng.uniform(-max_shift, max_shift, size=2) / fx
+    cz, sz = np.cos(roll), np.sin(roll)
+    cy_, sy_ = np.cos(yaw), np.sin(yaw)
+    cp, sp = np.cos(pitch), np.sin(pitch)
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1.0]])
+    Ry = np.array([[cy_, 0, sy_], [0, 1.0, 0], [-sy_, 0, cy_]])
+    Rx = np.array([[1.0, 0, 0], [0, cp, -sp], [0, sp, cp]])
+    return Rz @ Ry @ Rx
+
+
+def rotation_homography(K4, R):
+    fx, fy, cx, cy = K4
+    K = np.array([[fx, 0, cx], [0, fy, cy], [0, 0, 1.0]])
+    return K @ R @ np.linalg.inv(K)
 
 
 def warp(img, H):
@@ -58,15 +77,37 @@ def warp(img, H):
     return np.clip(np.rint(v), 0, 255).astype(np.uint8)
 
 
-def sequence(seed, n_frames, w=KITTI_W, h=KITTI_H):
-    """n_frames u8 images (n, h, w) and the n-1 homographies frame t -> t+1."""
+def sequence(seed, n_frames, w=KITTI_W, h=KITTI_H, return_rotations=False):
+    """n_frames u8 images (n, h, w); frame t+1 is frame t seen by the camera
+    rotated by R_t (homography K R K^-1) plus +-2 grey levels of noise.
+    Returns (frames, Hs) or (frames, Hs, Rs)."""
     rng = np.random.default_rng(seed)
+    K4 = intrinsics(w, h)
     frames = [textured_image(rng, w, h)]
-    Hs = []
+    Hs, Rs = [], []
     for _ in range(n_frames - 1):
-        H = small_homography(rng, w, h)
+        R = small_rotation(rng, K4[0])
+        H = rotation_homography(K4, R)
         nxt = warp(frames[-1], H)
         nxt = np.clip(nxt.astype(np.int16) + rng.integers(-2, 3, size=nxt.shape), 0, 255).astype(np.uint8)
         frames.append(nxt)
         Hs.append(H)
+        Rs.append(R)
+    if return_rotations:
+        return np.stack(frames), Hs, Rs
     return np.stack(frames), Hs
+
+
+def lift_map_points(rng, kps, K4, depth_range=(5.0, 50.0)):
+    """World points (camera frame of the last frame = world) for keypoints: X = d K^-1 [u v 1]."""
+    fx, fy, cx, cy = K4
+    d = rng.uniform(*depth_range, size=len(kps))
+    X = np.stack([(kps["x"] - cx) / fx * d, (kps["y"] - cy) / fy * d, d], axis=1)
+    return X.astype(np.float32)
+
+
+def pose_from_rotation(R, t=(0.0, 0.0, 0.0)):
+    T = np.eye(4, dtype=np.float32)
+    T[:3, :3] = R
+    T[:3, 3] = t
+    return T

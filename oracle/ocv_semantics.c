@@ -335,3 +335,22 @@ void ora_gaussian7_u8(const uint8_t* src, int sstep, int w, int h, uint8_t* dst,
         }
     free(tmp);
 }
+
+/* Test helper: count floats in [lo, hi] where the sinf/cosf restatement and
+ * the host libm differ (pins the restatement; tests/test_oracle_kat.py). */
+long ora_check_sincos_vs_libm(float lo, float hi, long stride)
+{
+    long bad = 0;
+    uint32_t u = f2u(lo);
+    const uint32_t uhi = f2u(hi);
+    if (stride < 1) stride = 1;
+    for (; u <= uhi; u += (uint32_t)stride) {
+        float f;
+        memcpy(&f, &u, 4);
+        volatile float vf = f;
+        float c = cosf(vf), s = sinf(vf);
+        if (f2u(c) != f2u(ora_cosf(f)) || f2u(s) != f2u(ora_sinf(f))) bad++;
+        if (uhi - u < (uint32_t)stride) break;
+    }
+    return bad;
+}

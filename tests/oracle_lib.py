@@ -117,3 +117,99 @@ class OracleExtractor:
         umax = np.zeros(16, np.int32)
         self.L.ora_extractor_tables(self.h, ptr(sc), ptr(isc), ptr(s2), ptr(is2), ptr(npl), ptr(umax))
         return dict(scale=sc, inv_scale=isc, sigma2=s2, inv_sigma2=is2, n_per_level=npl, umax=umax)
+
+
+# ---------------------------------------------------------------- matcher oracle
+class ora_frame(C.Structure):
+    _fields_ = [("N", C.c_int), ("kpsUn", C.c_void_p), ("desc", C.c_void_p), ("uRight", C.c_void_p),
+                ("minX", C.c_float), ("maxX", C.c_float), ("minY", C.c_float), ("maxY", C.c_float),
+                ("gridWInv", C.c_float), ("gridHInv", C.c_float), ("scaleFactors", C.c_void_p),
+                ("nlevels", C.c_int), ("cellStart", C.c_void_p), ("cellIdx", C.c_void_p)]
+
+
+class ora_lastframe(C.Structure):
+    _fields_ = [("Tcw_cur", C.c_void_p), ("Tcw_last", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("mbf", C.c_float), ("mb", C.c_float),
+                ("lastKeys", C.c_void_p), ("lastKeysUn", C.c_void_p), ("lastMP", C.c_void_p),
+                ("lastOutlier", C.c_void_p), ("lastN", C.c_int), ("mpPos", C.c_void_p), ("mpDesc", C.c_void_p),
+                ("mpObs", C.c_void_p)]
+
+
+class ora_localmaps(C.Structure):
+    _fields_ = [("n", C.c_int), ("inView", C.c_void_p), ("projX", C.c_void_p), ("projXR", C.c_void_p),
+                ("projY", C.c_void_p), ("level", C.c_void_p), ("viewCos", C.c_void_p), ("desc", C.c_void_p),
+                ("mpId", C.c_void_p)]
+
+
+def _addr(a):
+    return None if a is None else a.ctypes.data
+
+
+class OracleFrame:
+    """Frame grid (Frame.cc:230-245) over host arrays; mirrors c_orb_slam_amd.Frame fields."""
+
+    def __init__(self, F):
+        self.F = F
+        self.cellStart = np.zeros(64 * 48 + 1, np.int32)
+        self.cellIdx = np.zeros(max(F.N, 1), np.int32)
+        s = ora_frame()
+        s.N = F.N
+        s.kpsUn = _addr(F.keysUn)
+        s.desc = _addr(F.desc)
+        s.uRight = _addr(F.uRight)
+        s.minX, s.maxX, s.minY, s.maxY = F.minX, F.maxX, F.minY, F.maxY
+        s.gridWInv, s.gridHInv = F.gridWInv, F.gridHInv
+        s.scaleFactors = _addr(F.scale)
+        s.nlevels = len(F.scale)
+        s.cellStart = _addr(self.cellStart)
+        s.cellIdx = _addr(self.cellIdx)
+        self.s = s
+        L = lib()
+        L.ora_frame_build_grid.argtypes = [C.c_void_p]
+        L.ora_frame_build_grid(C.byref(s))
+
+    def features_in_area(self, x, y, r, minLevel=-1, maxLevel=-1):
+        L = lib()
+        L.ora_frame_features_in_area.argtypes = [C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int,
+                                                 C.c_void_p, C.c_int]
+        out = np.zeros(max(self.F.N, 1), np.int32)
+        n = L.ora_frame_features_in_area(C.byref(self.s), x, y, r, minLevel, maxLevel, ptr(out), self.F.N)
+        return out[:n]
+
+
+def oracle_search_last(cur, cur_mp, last, last_keys, last_mp, last_outlier, mps, th, bMono, nnratio=0.9,
+                       checkOri=True):
+    """SearchByProjection(Cur, Last, th, bMono) on the CPU oracle; updates cur_mp in place."""
+    of = OracleFrame(cur)
+    lf = ora_lastframe()
+    lk = np.ascontiguousarray(last_keys, KP_DTYPE)
+    lm = np.ascontiguousarray(last_mp, np.int32)
+    lo = np.ascontiguousarray(last_outlier, np.uint8)
+    lf.Tcw_cur, lf.Tcw_last = _addr(cur.Tcw), _addr(last.Tcw)
+    lf.fx, lf.fy, lf.cx, lf.cy = cur.fx, cur.fy, cur.cx, cur.cy
+    lf.mbf, lf.mb = cur.bf, cur.b
+    lf.lastKeys, lf.lastKeysUn = _addr(lk), _addr(last.keysUn)
+    lf.lastMP, lf.lastOutlier, lf.lastN = _addr(lm), _addr(lo), len(lm)
+    lf.mpPos, lf.mpDesc, lf.mpObs = _addr(mps.pos), _addr(mps.desc), _addr(mps.obs)
+    L = lib()
+    L.ora_search_by_projection_last.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_int, C.c_float,
+                                                C.c_int]
+    return L.ora_search_by_projection_last(C.byref(of.s), ptr(cur_mp), C.byref(lf), th, int(bMono), nnratio,
+                                           int(checkOri))
+
+
+def oracle_search_local(F, cur_mp, mp_obs, in_view, proj_x, proj_xr, proj_y, level, view_cos, qdesc, mp_id, th,
+                        nnratio):
+    of = OracleFrame(F)
+    a = [np.ascontiguousarray(in_view, np.uint8), np.ascontiguousarray(proj_x, np.float32),
+         np.ascontiguousarray(proj_xr, np.float32), np.ascontiguousarray(proj_y, np.float32),
+         np.ascontiguousarray(level, np.int32), np.ascontiguousarray(view_cos, np.float32),
+         np.ascontiguousarray(qdesc, np.uint8), np.ascontiguousarray(mp_id, np.int32)]
+    m = ora_localmaps()
+    m.n = len(a[0])
+    m.inView, m.projX, m.projXR, m.projY, m.level, m.viewCos, m.desc, m.mpId = [_addr(x) for x in a]
+    obs = np.ascontiguousarray(mp_obs, np.int32)
+    L = lib()
+    L.ora_search_by_projection_local.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float,
+                                                 C.c_float]
+    return L.ora_search_by_projection_local(C.byref(of.s), ptr(cur_mp), ptr(obs), C.byref(m), th, nnratio)

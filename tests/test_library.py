@@ -1,0 +1,49 @@
+"""CPU: the C-ABI library loads, exports every symbol include/orbslam_gpu.h declares,
+validates arguments before touching the device, and reports ORB_E_NODEVICE
+(never a silent CPU fallback) when no GPU is visible."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import c_orb_slam_amd as orb
+from c_orb_slam_amd._lib import (ORB_E_INVALID, ORB_E_NODEVICE, header_functions, lib, ptr)
+
+
+def test_all_header_symbols_exported():
+    L = lib()
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_version_and_device_probe():
+    assert b"gfx950" in lib().orbgpu_version()
+    assert orb.device_available() in (True, False)
+
+
+def test_invalid_arguments_rejected_without_device():
+    L = lib()
+    h = C.c_void_p()
+    assert L.ORBextractor_create(1200, 1.2, 0, 20, 7, 640, 480, 1, C.byref(h)) == ORB_E_INVALID
+    assert L.ORBextractor_create(1200, 1.0, 8, 20, 7, 640, 480, 1, C.byref(h)) == ORB_E_INVALID
+    assert L.ORBextractor_create(1200, 1.2, 8, 20, 7, 0, 480, 1, C.byref(h)) == ORB_E_INVALID
+    assert L.ORBextractor_destroy(None) == ORB_E_INVALID
+    assert L.ORBmatcher_destroy(None) == ORB_E_INVALID
+    assert L.ORBmatcher_create(0.6, 1, None) == ORB_E_INVALID
+
+
+def test_descriptor_distance_host_entry():
+    a = np.arange(32, dtype=np.uint8)
+    b = a[::-1].copy()
+    assert orb.ORBmatcher.DescriptorDistance(a, b) == int(np.unpackbits(a ^ b).sum())
+
+
+@pytest.mark.skipif(orb.device_available(), reason="a GPU is visible here")
+def test_no_silent_cpu_fallback():
+    with pytest.raises(orb.OrbGpuError) as ei:
+        orb.ORBextractor(1200, 1.2, 8, 20, 7)
+    assert ei.value.code == ORB_E_NODEVICE
+    with pytest.raises(orb.OrbGpuError):
+        orb.ORBmatcher(0.9, True)

