@@ -143,8 +143,9 @@ int ORBmatcher_SearchByProjection_LastFrame_batch(ORBmatcher_h h, int npairs, co
                     al((size_t)mps[p].n * 12) + al((size_t)mps[p].n * 32) + al((size_t)mps[p].n * 4) +
                     al((size_t)cur[p].N * 4) + al(4);
         }
-        if (m->arena_reserve(need + 4096)) return ORB_E_HIP;
+        if (m->arena_reserve(need + (size_t)npairs * 4 + 4096)) return ORB_E_HIP;
     }
+    if (dev && m->arena_reserve((size_t)npairs * 4 + 256)) return ORB_E_HIP;
     int* d_nm = nullptr;
     std::vector<int*> nm_dev(npairs, nullptr);
     for (int p = 0; p < npairs; p++) {
@@ -183,11 +184,7 @@ int ORBmatcher_SearchByProjection_LastFrame_batch(ORBmatcher_h h, int npairs, co
     // nmatches: small device array
     {
         void* d = m->arena_alloc((size_t)npairs * 4 + 4);
-        if (!d && !dev) return ORB_E_HIP;
-        if (!d) {  // device mode: separate allocation held by arena (reserve small)
-            if (m->arena_reserve((size_t)npairs * 4 + 256)) return ORB_E_HIP;
-            d = m->arena_alloc((size_t)npairs * 4 + 4);
-        }
+        if (!d) return ORB_E_HIP;
         d_nm = (int*)d;
         for (int p = 0; p < npairs; p++) probs[p].nmatches = d_nm + p;
     }
