@@ -113,6 +113,21 @@ def main():
     stage_acc = {}
     kernel_ms = []   # k_fast_cells duration per step (HIP events on the extractor stream)
 
+    # ctypes views of the batch, built once (device pointers do not move; only counts change)
+    curs = (orb_frame * P)(*[frame_struct(b, 0, poses[b - 1].data_ptr()) for b in range(1, B)])
+    lasts = (orb_frame * P)(*[frame_struct(b, 0, eye.data_ptr()) for b in range(0, B - 1)])
+    mps = (orb_mappoints * P)()
+    for p in range(P):
+        mps[p].pos = d_mp_pos[p].data_ptr()
+        mps[p].desc = d_desc[p].data_ptr()
+        mps[p].observations = d_obs.data_ptr()
+    arr = lambda xs: (C.c_void_p * P)(*xs)
+    a_cur_mp = arr([d_cur_mp[b].data_ptr() for b in range(1, B)])
+    a_last_kps = arr([d_kps[b].data_ptr() for b in range(P)])
+    a_last_mp = arr([d_arange.data_ptr()] * P)
+    a_last_out = arr([d_outlier.data_ptr()] * P)
+    nm = np.zeros(P, np.int32)
+
     def step():
         n = ex.extract_device(d_imgs.data_ptr(), B, W, H, W, W * H, d_kps.data_ptr(), d_desc.data_ptr(), cap)
         # last-frame map points: X = d K^-1 [u v 1] (UpdateLastFrame-style lift), on device
@@ -121,21 +136,14 @@ def main():
         d_mp_pos[..., 1] = (y - float(cy)) / float(fy) * d_depth
         d_mp_pos[..., 2] = d_depth
         d_cur_mp.fill_(-1)
-        torch.cuda.current_stream().synchronize()
-        curs = (orb_frame * P)(*[frame_struct(b, n[b], poses[b - 1].data_ptr()) for b in range(1, B)])
-        lasts = (orb_frame * P)(*[frame_struct(b, n[b], eye.data_ptr()) for b in range(0, B - 1)])
-        mps = (orb_mappoints * P)()
         for p in range(P):
+            curs[p].N = int(n[p + 1])
+            lasts[p].N = int(n[p])
             mps[p].n = int(n[p])
-            mps[p].pos = d_mp_pos[p].data_ptr()
-            mps[p].desc = d_desc[p].data_ptr()
-            mps[p].observations = d_obs.data_ptr()
-        arr = lambda xs: (C.c_void_p * P)(*xs)
-        nm = np.zeros(P, np.int32)
-        check(L.ORBmatcher_SearchByProjection_LastFrame_batch(
-            m._h, P, curs, arr([d_cur_mp[b].data_ptr() for b in range(1, B)]), lasts,
-            arr([d_kps[b].data_ptr() for b in range(P)]), arr([d_arange.data_ptr()] * P),
-            arr([d_outlier.data_ptr()] * P), mps, 15.0, 1, ptr(nm)), "SearchByProjection batch")
+        torch.cuda.current_stream().synchronize()
+        check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, P, curs, a_cur_mp, lasts, a_last_kps, a_last_mp,
+                                                              a_last_out, mps, 15.0, 1, ptr(nm)),
+              "SearchByProjection batch")
         t = ex.last_timings()
         for k, v in t.items():
             stage_acc[k] = stage_acc.get(k, 0.0) + v

@@ -91,43 +91,59 @@ __global__ void k_pyr_resize(uint8_t* __restrict__ pyr, size_t img_bytes, size_t
 
 // GaussianBlur(7x7, sigma 2, REFLECT_101) on CV_8U: int taps (round(k*256)),
 // int row pass, int column pass, (v + 2^15) >> 16, saturate.  The padded
-// level's 19-px REFLECT_101 border supplies the filter border.  Tile 64x16.
-constexpr int BT_W = 64, BT_H = 16;
+// level's 19-px REFLECT_101 border supplies the filter border.  Tile 128x32,
+// dword LDS staging (the padded row is dword-aligned at interior x0-3), four
+// outputs per thread per pass, dword stores into the unpadded blurred level.
+constexpr int BT_W = 128, BT_H = 32, BT_LW = BT_W + 8;  // staged cols: interior [x0-3, x0+133)
 __global__ void __launch_bounds__(256) k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                               size_t img_bytes, const BlurTile* __restrict__ tiles) {
-    __shared__ uint8_t s_src[BT_H + 6][BT_W + 8];
-    __shared__ int s_row[BT_H + 6][BT_W + 1];
+                                               size_t img_bytes, size_t blur_bytes,
+                                               const BlurTile* __restrict__ tiles) {
+    __shared__ uint32_t s_src[(BT_H + 6) * (BT_LW / 4)];
+    __shared__ int4 s_row[(BT_H + 6) * (BT_W / 4)];
     const BlurTile tl = tiles[blockIdx.x];
     const int b = blockIdx.y;
-    const uint8_t* P = pyr + (size_t)b * img_bytes + tl.off + (size_t)kEdge * tl.pitch + kEdge;
-    uint8_t* O = blur + (size_t)b * img_bytes + tl.off + (size_t)kEdge * tl.pitch + kEdge;
+    const uint8_t* P = pyr + (size_t)b * img_bytes + tl.off;           // padded level base
+    uint8_t* O = blur + (size_t)b * blur_bytes + tl.boff;               // unpadded blurred level
     const int x0 = tl.tx * BT_W, y0 = tl.ty * BT_H;
-    for (int i = threadIdx.x; i < (BT_H + 6) * (BT_W + 6); i += 256) {
-        const int r = i / (BT_W + 6), c = i - r * (BT_W + 6);
-        int yy = y0 + r - 3, xx = x0 + c - 3;
-        // clamp into the padded area; such pixels only feed outputs outside the level
-        yy = min(yy, tl.h + 2);
-        xx = min(xx, tl.w + 2);
-        s_src[r][c] = P[(ptrdiff_t)yy * tl.pitch + xx];
+    constexpr int WPR = BT_LW / 4;  // words per staged row
+    for (int i = threadIdx.x; i < (BT_H + 6) * WPR; i += 256) {
+        const int r = i / WPR, wq = i - r * WPR;
+        const int yy = min(y0 + r - 3, tl.h + 2) + kEdge;                 // padded row
+        const int c = min(kEdge - 3 + x0 + 4 * wq, tl.pitch - 4);           // padded col (dword aligned)
+        s_src[i] = *reinterpret_cast<const uint32_t*>(P + (size_t)yy * tl.pitch + c);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < (BT_H + 6) * BT_W; i += 256) {
-        const int r = i / BT_W, c = i - r * BT_W;
-        int s = 0;
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(s_src);
+    for (int i = threadIdx.x; i < (BT_H + 6) * (BT_W / 4); i += 256) {
+        const int r = i / (BT_W / 4), q = i - r * (BT_W / 4);
+        const uint8_t* src = sb + r * BT_LW + 4 * q;
+        int v[10];
 #pragma unroll
-        for (int k = 0; k < 7; k++) s += c_gauss[k] * s_src[r][c + k];
-        s_row[r][c] = s;
+        for (int k = 0; k < 10; k++) v[k] = src[k];
+        int4 o;
+        o.x = c_gauss[0] * v[0] + c_gauss[1] * v[1] + c_gauss[2] * v[2] + c_gauss[3] * v[3] + c_gauss[4] * v[4] + c_gauss[5] * v[5] + c_gauss[6] * v[6];
+        o.y = c_gauss[0] * v[1] + c_gauss[1] * v[2] + c_gauss[2] * v[3] + c_gauss[3] * v[4] + c_gauss[4] * v[5] + c_gauss[5] * v[6] + c_gauss[6] * v[7];
+        o.z = c_gauss[0] * v[2] + c_gauss[1] * v[3] + c_gauss[2] * v[4] + c_gauss[3] * v[5] + c_gauss[4] * v[6] + c_gauss[5] * v[7] + c_gauss[6] * v[8];
+        o.w = c_gauss[0] * v[3] + c_gauss[1] * v[4] + c_gauss[2] * v[5] + c_gauss[3] * v[6] + c_gauss[4] * v[7] + c_gauss[5] * v[8] + c_gauss[6] * v[9];
+        s_row[i] = o;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < BT_H * BT_W; i += 256) {
-        const int r = i / BT_W, c = i - r * BT_W;
-        const int y = y0 + r, x = x0 + c;
+    for (int i = threadIdx.x; i < BT_H * (BT_W / 4); i += 256) {
+        const int r = i / (BT_W / 4), q = i - r * (BT_W / 4);
+        const int y = y0 + r, x = x0 + 4 * q;
         if (y >= tl.h || x >= tl.w) continue;
-        int s = 0;
+        int4 acc = make_int4(0, 0, 0, 0);
 #pragma unroll
-        for (int k = 0; k < 7; k++) s += c_gauss[k] * s_row[r + k][c];
-        const int v = (s + (1 << 15)) >> 16;
-        O[(size_t)y * tl.pitch + x] = (uint8_t)min(max(v, 0), 255);
+        for (int k = 0; k < 7; k++) {
+            const int4 t = s_row[(r + k) * (BT_W / 4) + q];
+            acc.x += c_gauss[k] * t.x; acc.y += c_gauss[k] * t.y;
+            acc.z += c_gauss[k] * t.z; acc.w += c_gauss[k] * t.w;
+        }
+        const uint32_t px = (uint32_t)min(max((acc.x + (1 << 15)) >> 16, 0), 255) |
+                            ((uint32_t)min(max((acc.y + (1 << 15)) >> 16, 0), 255) << 8) |
+                            ((uint32_t)min(max((acc.z + (1 << 15)) >> 16, 0), 255) << 16) |
+                            ((uint32_t)min(max((acc.w + (1 << 15)) >> 16, 0), 255) << 24);
+        *reinterpret_cast<uint32_t*>(O + (size_t)y * tl.bpitch + x) = px;
     }
 }
 
@@ -316,7 +332,7 @@ __global__ void __launch_bounds__(1024) k_compact(const uint32_t* __restrict__ s
 // lane l are pairs l, l+64, l+128, l+192, so the four wave ballots ARE the
 // 32 descriptor bytes (byte i bit k = pair 8i+k, little endian).
 __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
-                                                     size_t img_bytes, const int2* __restrict__ sel, int nsel,
+                                                     size_t img_bytes, size_t blur_bytes, const int2* __restrict__ sel, int nsel,
                                                      const LevelDev* __restrict__ lv, orb_kp_dev* __restrict__ kps,
                                                      uint8_t* __restrict__ desc, int cap_per_image) {
     const int lane = threadIdx.x & 63;
@@ -344,15 +360,15 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     float sa, ca;
     glibc_sincosf(angle * factorPI, &sa, &ca);
     const float a = ca, bb = sa;
-    const uint8_t* cb = blur + (size_t)b * img_bytes + L.off + (size_t)(kEdge + y) * L.pitch + kEdge + x;
+    const uint8_t* cb = blur + (size_t)b * blur_bytes + L.boff + (size_t)y * L.bpitch + x;
     uint64_t words[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int p = lane + 64 * q;
         const float x0 = (float)c_pattern[4 * p], y0 = (float)c_pattern[4 * p + 1];
         const float x1 = (float)c_pattern[4 * p + 2], y1 = (float)c_pattern[4 * p + 3];
-        const int t0 = cb[cv_round(x0 * bb + y0 * a) * L.pitch + cv_round(x0 * a - y0 * bb)];
-        const int t1 = cb[cv_round(x1 * bb + y1 * a) * L.pitch + cv_round(x1 * a - y1 * bb)];
+        const int t0 = cb[cv_round(x0 * bb + y0 * a) * L.bpitch + cv_round(x0 * a - y0 * bb)];
+        const int t1 = cb[cv_round(x1 * bb + y1 * a) * L.bpitch + cv_round(x1 * a - y1 * bb)];
         words[q] = __ballot(t0 < t1);
     }
     const size_t o = (size_t)b * cap_per_image + idx;
@@ -513,6 +529,15 @@ int Extractor::setup_geometry(int W, int H) {
         off = (off + 255) & ~(size_t)255;
     }
     img_bytes_ = off;
+    size_t boff = 0;
+    for (int l = 0; l < nlevels_; l++) {
+        LevelHost& L = levels_[l];
+        L.bpitch = align_up(L.w, 16);
+        L.boff = boff;
+        boff += (size_t)L.bpitch * L.h;
+        boff = (boff + 255) & ~(size_t)255;
+    }
+    blur_bytes_ = boff;
     // cells, ORBextractor.cc:776-829
     cells_.clear();
     level_cell_begin_.assign(nlevels_ + 1, 0);
@@ -563,6 +588,7 @@ int Extractor::setup_geometry(int W, int H) {
             for (int tx = 0; tx < (L.w + BT_W - 1) / BT_W; tx++) {
                 BlurTile t;
                 t.off = L.off; t.pitch = L.pitch; t.w = L.w; t.h = L.h; t.tx = tx; t.ty = ty;
+                t.boff = L.boff; t.bpitch = L.bpitch;
                 tiles_.push_back(t);
             }
     }
@@ -618,8 +644,8 @@ int Extractor::setup_geometry(int W, int H) {
     F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_);
     const int B = maxB_;
     ORB_HIP_CHECK(hipMalloc(&d_pyr_, img_bytes_ * B));
-    ORB_HIP_CHECK(hipMalloc(&d_blur_, img_bytes_ * B));
-    ORB_HIP_CHECK(hipMemset(d_blur_, 0, img_bytes_ * B));
+    ORB_HIP_CHECK(hipMalloc(&d_blur_, blur_bytes_ * B));
+    ORB_HIP_CHECK(hipMemset(d_blur_, 0, blur_bytes_ * B));
     ORB_HIP_CHECK(hipMalloc(&d_slots_, slots_per_image_ * 4 * B));
     ORB_HIP_CHECK(hipMalloc(&d_counts_, cells_.size() * 4 * B));
     ORB_HIP_CHECK(hipMalloc(&d_cells_, cells_.size() * sizeof(CellDesc)));
@@ -640,6 +666,8 @@ int Extractor::setup_geometry(int W, int H) {
         ld[l].off = levels_[l].off;
         ld[l].pitch = levels_[l].pitch;
         ld[l].scale = scale_[l];
+        ld[l].boff = levels_[l].boff;
+        ld[l].bpitch = levels_[l].bpitch;
         ld[l].kp_size = (float)(int)(kPatch * scale_[l]);
     }
     ORB_HIP_CHECK(hipMalloc(&d_levels_, ld.size() * sizeof(LevelDev)));
@@ -763,7 +791,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
     // 2. blur (independent of keypoints; overlaps nothing yet, kept on the stream)
     hipLaunchKernelGGL(k_blur7, dim3((unsigned)tiles_.size(), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
-                       (uint8_t*)d_blur_, img_bytes_, (const BlurTile*)d_tiles_);
+                       (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_);
     ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
     // 3. FAST per cell
     const int ncells = (int)cells_.size();
@@ -850,7 +878,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     if (nsel > 0) {
         ORB_HIP_CHECK(hipMemcpyAsync(d_sel_, h_sel_, (size_t)nsel * sizeof(int2), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_orient_desc, dim3((nsel + 3) / 4), dim3(256), 0, s, (const uint8_t*)d_pyr_,
-                           (const uint8_t*)d_blur_, img_bytes_, (const int2*)d_sel_, nsel,
+                           (const uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const int2*)d_sel_, nsel,
                            (const LevelDev*)d_levels_, okps, odesc, cap);
         ORB_HIP_CHECK(hipGetLastError());
     }

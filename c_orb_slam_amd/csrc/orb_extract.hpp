@@ -29,19 +29,19 @@ struct CellDesc {          // one FAST cell ROI, ORBextractor.cc:794-829
 };
 
 struct BlurTile {
-    long long off;
-    int pitch, w, h, tx, ty;
+    long long off, boff;
+    int pitch, bpitch, w, h, tx, ty;
 };
 
 struct LevelDev {
-    long long off;
-    int pitch;
+    long long off, boff;
+    int pitch, bpitch;
     float scale, kp_size;
 };
 
 struct LevelHost {
-    int w, h, pw, ph, pitch;
-    size_t off;
+    int w, h, pw, ph, pitch, bpitch;
+    size_t off, boff;
 };
 
 class Extractor {
@@ -85,7 +85,7 @@ private:
     std::vector<int> level_cell_begin_;
     std::vector<BlurTile> tiles_;
     std::vector<std::array<size_t, 4>> tab_off_;
-    size_t img_bytes_ = 0, slots_per_image_ = 0;
+    size_t img_bytes_ = 0, blur_bytes_ = 0, slots_per_image_ = 0;
     int packed_cap_ = 0, sel_cap_ = 0;
     int last_B_ = 0;
 

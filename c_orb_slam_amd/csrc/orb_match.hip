@@ -248,8 +248,8 @@ __device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked block
 
 // Parallel phase: one thread per query.
 template <bool LAST>
-__global__ void __launch_bounds__(256) k_candidates(SearchDev* probs, float th, int bMono) {
-    const SearchDev& P = probs[blockIdx.y];
+__global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict__ probs, float th, int bMono) {
+    const SearchDev P = probs[blockIdx.y];
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= P.nq) return;
     int2 top[kTopK];
@@ -269,112 +269,139 @@ __global__ void __launch_bounds__(256) k_candidates(SearchDev* probs, float th, 
     for (int k = 0; k < kk; k++) P.topk[(size_t)q * kTopK + k] = top[k];
 }
 
-// Sequential greedy replay: one wave per problem.
+// Sequential greedy replay: one wave per problem.  Per-query inputs are
+// staged into LDS in chunks (coalesced), occupancy is an LDS flag array
+// (occ[i] = mvpMapPoints[i] && Observations()>0), so the per-query critical
+// path is a handful of LDS ops + one ballot.
+constexpr int SEL_CHUNK = 256;
 template <bool LAST>
-__global__ void __launch_bounds__(64) k_select(SearchDev* probs, float th, int bMono, float nnratio, int checkOri) {
+__global__ void __launch_bounds__(64) k_select(const SearchDev* __restrict__ probs, float th, int bMono,
+                                               float nnratio, int checkOri) {
     __shared__ int s_cur[kMaxFrameKeys];
+    __shared__ uint8_t s_occ[kMaxFrameKeys];
+    __shared__ int2 s_top[SEL_CHUNK * kTopK];
+    __shared__ int s_cnt[SEL_CHUNK];
+    __shared__ int s_qmp[SEL_CHUNK];     // map point written by the query
+    __shared__ uint8_t s_qobs[SEL_CHUNK];
     __shared__ int s_nh;
-    SearchDev& P = probs[blockIdx.x];
+    const SearchDev P = probs[blockIdx.x];
     const int lane = threadIdx.x;
     const int N = P.cur.N;
-    for (int i = lane; i < N; i += 64) s_cur[i] = P.curMP[i];
+    for (int i = lane; i < N; i += 64) {
+        const int m = P.curMP[i];
+        s_cur[i] = m;
+        s_occ[i] = (m >= 0 && P.mpObs[m] > 0) ? 1 : 0;
+    }
     if (lane == 0) s_nh = 0;
-    __syncthreads();
     bool bF = false, bB = false;
     if (LAST) fwd_bwd(P, bMono != 0, bF, bB);
     int nmatches = 0;
-    auto occupied = [&](int idx) {
-        const int m = s_cur[idx];
-        return m >= 0 && P.mpObs[m] > 0;
-    };
-    for (int q = 0; q < P.nq; q++) {
-        const int cnt = P.qinfo[q].x;
-        if (cnt <= 0) continue;
-        const int kk = cnt < kTopK ? cnt : kTopK;
-        int2 e = make_int2(256, -1);
-        bool free_ = false;
-        if (lane < kk) {
-            e = P.topk[(size_t)q * kTopK + lane];
-            free_ = !occupied(e.y);
+    auto occupied = [&](int idx) { return s_occ[idx] != 0; };
+    for (int q0 = 0; q0 < P.nq; q0 += SEL_CHUNK) {
+        const int nc = min(SEL_CHUNK, P.nq - q0);
+        __syncthreads();
+        for (int i = lane; i < nc; i += 64) {
+            const int c = P.qinfo[q0 + i].x;
+            s_cnt[i] = c;
+            const int mp = LAST ? P.lastMP[q0 + i] : P.mpIndex[q0 + i];
+            s_qmp[i] = mp;
+            s_qobs[i] = (c > 0 && mp >= 0 && P.mpObs[mp] > 0) ? 1 : 0;
         }
-        uint64_t m = __ballot(free_);
-        int bestDist = 256, bestIdx = -1, bestDist2 = 256, bestLevel = -1, bestLevel2 = -1;
-        bool resolved = true;
-        if (LAST) {
-            if (m) {
-                const int f = __ffsll((long long)m) - 1;
-                bestDist = __shfl(e.x, f, 64);
-                bestIdx = __shfl(e.y, f, 64);
-            } else if (cnt > kTopK) {
-                resolved = false;
+        for (int i = lane; i < nc * kTopK; i += 64) {
+            const int qq = i / kTopK, k = i - qq * kTopK;
+            const int c = P.qinfo[q0 + qq].x;
+            if (k < c) s_top[i] = P.topk[(size_t)q0 * kTopK + i];
+        }
+        __syncthreads();
+        for (int qi = 0; qi < nc; qi++) {
+            const int q = q0 + qi;
+            const int cnt = s_cnt[qi];
+            if (cnt <= 0) continue;
+            const int kk = cnt < kTopK ? cnt : kTopK;
+            int2 e = make_int2(256, -1);
+            bool free_ = false;
+            if (lane < kk) {
+                e = s_top[qi * kTopK + lane];
+                free_ = !occupied(e.y);
             }
-        } else {
-            const int nfree = __popcll(m);
-            if (nfree >= 2 || (nfree == 1 && cnt <= kTopK) || (nfree == 0 && cnt <= kTopK)) {
-                if (nfree >= 1) {
+            uint64_t m = __ballot(free_);
+            int bestDist = 256, bestIdx = -1, bestDist2 = 256, bestLevel = -1, bestLevel2 = -1;
+            bool resolved = true;
+            if (LAST) {
+                if (m) {
                     const int f = __ffsll((long long)m) - 1;
                     bestDist = __shfl(e.x, f, 64);
                     bestIdx = __shfl(e.y, f, 64);
-                    const uint64_t m2 = m & (m - 1);
-                    if (m2) {
-                        const int f2 = __ffsll((long long)m2) - 1;
-                        bestDist2 = __shfl(e.x, f2, 64);
-                        const int i2 = __shfl(e.y, f2, 64);
-                        bestLevel2 = P.cur.keysUn[i2].octave;
-                    }
-                    bestLevel = P.cur.keysUn[bestIdx].octave;
+                } else if (cnt > kTopK) {
+                    resolved = false;
                 }
             } else {
-                resolved = false;
-            }
-        }
-        if (!resolved) {
-            // every kept candidate is taken: rescan this query with occupancy (rare)
-            if (lane == 0) {
-                int2 top2[2];
-                int c2;
-                if (LAST) {
-                    const LastQuery lq = last_query(P, q, th, bF, bB);
-                    c2 = scan_last(P, lq, occupied, top2, 1);
-                    if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
+                const int nfree = __popcll(m);
+                if (nfree >= 2 || cnt <= kTopK) {
+                    if (nfree >= 1) {
+                        const int f = __ffsll((long long)m) - 1;
+                        bestDist = __shfl(e.x, f, 64);
+                        bestIdx = __shfl(e.y, f, 64);
+                        const uint64_t m2 = m & (m - 1);
+                        if (m2) {
+                            const int f2 = __ffsll((long long)m2) - 1;
+                            bestDist2 = __shfl(e.x, f2, 64);
+                            const int i2 = __shfl(e.y, f2, 64);
+                            bestLevel2 = P.cur.keysUn[i2].octave;
+                        }
+                        bestLevel = P.cur.keysUn[bestIdx].octave;
+                    }
                 } else {
-                    const LocalQuery lq = local_query(P, q, th);
-                    c2 = scan_local(P, lq, occupied, top2, 2);
-                    if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; bestLevel = P.cur.keysUn[bestIdx].octave; }
-                    if (c2 > 1) { bestDist2 = top2[1].x; bestLevel2 = P.cur.keysUn[top2[1].y].octave; }
+                    resolved = false;
                 }
             }
-            bestDist = __shfl(bestDist, 0, 64);
-            bestIdx = __shfl(bestIdx, 0, 64);
-            bestDist2 = __shfl(bestDist2, 0, 64);
-            bestLevel = __shfl(bestLevel, 0, 64);
-            bestLevel2 = __shfl(bestLevel2, 0, 64);
-        }
-        if (bestDist <= TH_HIGH) {
-            if (LAST) {
+            if (!resolved) {
+                // every kept candidate is taken: rescan this query with occupancy (rare)
                 if (lane == 0) {
-                    s_cur[bestIdx] = P.lastMP[q];
-                    if (checkOri) {
-                        float rot = P.last.keysUn[q].angle - P.cur.keysUn[bestIdx].angle;
-                        if (rot < 0.0f) rot += 360.0f;
-                        int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
-                        if (bin == HISTO_LENGTH) bin = 0;
-                        P.hist[s_nh] = make_int2(bin, bestIdx);
-                        s_nh++;
+                    int2 top2[2];
+                    int c2;
+                    if (LAST) {
+                        const LastQuery lq = last_query(P, q, th, bF, bB);
+                        c2 = scan_last(P, lq, occupied, top2, 1);
+                        if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
+                    } else {
+                        const LocalQuery lq = local_query(P, q, th);
+                        c2 = scan_local(P, lq, occupied, top2, 2);
+                        if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; bestLevel = P.cur.keysUn[bestIdx].octave; }
+                        if (c2 > 1) { bestDist2 = top2[1].x; bestLevel2 = P.cur.keysUn[top2[1].y].octave; }
                     }
                 }
-                nmatches++;
-            } else {
-                if (!(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2)) {
-                    if (lane == 0) s_cur[bestIdx] = P.mpIndex[q];
+                bestDist = __shfl(bestDist, 0, 64);
+                bestIdx = __shfl(bestIdx, 0, 64);
+                bestDist2 = __shfl(bestDist2, 0, 64);
+                bestLevel = __shfl(bestLevel, 0, 64);
+                bestLevel2 = __shfl(bestLevel2, 0, 64);
+            }
+            if (bestDist <= TH_HIGH) {
+                bool take = true;
+                if (!LAST) take = !(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2);
+                if (take) {
+                    if (lane == 0) {
+                        s_cur[bestIdx] = s_qmp[qi];
+                        s_occ[bestIdx] = s_qobs[qi];
+                        if (LAST && checkOri) {
+                            float rot = P.last.keysUn[q].angle - P.cur.keysUn[bestIdx].angle;
+                            if (rot < 0.0f) rot += 360.0f;
+                            int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
+                            if (bin == HISTO_LENGTH) bin = 0;
+                            P.hist[s_nh] = make_int2(bin, bestIdx);
+                            s_nh++;
+                        }
+                    }
                     nmatches++;
                 }
             }
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): lane 0's LDS writes land before the next query
+            __builtin_amdgcn_wave_barrier();
         }
-        __syncthreads();
     }
+    __syncthreads();
     if (LAST && checkOri) {
-        __syncthreads();
         if (lane == 0) {
             const int nh = s_nh;
             int sizes[HISTO_LENGTH];
@@ -383,17 +410,16 @@ __global__ void __launch_bounds__(64) k_select(SearchDev* probs, float th, int b
             // ComputeThreeMaxima, ORBmatcher.cc:1601-1642
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < HISTO_LENGTH; i++) {
-                const int s = sizes[i];
-                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
-                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
-                else if (s > max3) { max3 = s; ind3 = i; }
+                const int sz = sizes[i];
+                if (sz > max1) { max3 = max2; max2 = max1; max1 = sz; ind3 = ind2; ind2 = ind1; ind1 = i; }
+                else if (sz > max2) { max3 = max2; max2 = sz; ind3 = ind2; ind2 = i; }
+                else if (sz > max3) { max3 = sz; ind3 = i; }
             }
             if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
             else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-            for (int b = 0; b < HISTO_LENGTH; b++) {
-                if (b == ind1 || b == ind2 || b == ind3) continue;
-                for (int k = 0; k < nh; k++)
-                    if (P.hist[k].x == b) { s_cur[P.hist[k].y] = -1; nmatches--; }
+            for (int k = 0; k < nh; k++) {
+                const int2 h = P.hist[k];
+                if (h.x != ind1 && h.x != ind2 && h.x != ind3) { s_cur[h.y] = -1; nmatches--; }
             }
         }
         nmatches = __shfl(nmatches, 0, 64);
