@@ -72,6 +72,13 @@ int ORBextractor_get_level(ORBextractor_h h, int index, int level, uint8_t* dst,
     return rc == 0 ? ORB_OK : (rc == -2 ? ORB_E_HIP : ORB_E_INVALID);
 }
 
+int ORBextractor_get_blurred_level(ORBextractor_h h, int index, int level, uint8_t* dst, int dst_step, int* w,
+                                   int* h_) {
+    if (!h || !w || !h_) return ORB_E_INVALID;
+    int rc = h->ex->get_blurred(index, level, dst, dst_step, w, h_);
+    return rc == 0 ? ORB_OK : (rc == -2 ? ORB_E_HIP : ORB_E_INVALID);
+}
+
 int ORBextractor_get_levels(ORBextractor_h h, int* nlevels, float* scaleFactor) {
     if (!h) return ORB_E_INVALID;
     if (nlevels) *nlevels = h->ex->nlevels();

@@ -113,13 +113,19 @@ __global__ void __launch_bounds__(256) k_blur7(const uint8_t* __restrict__ pyr, 
         s_src[i] = *reinterpret_cast<const uint32_t*>(P + (size_t)yy * tl.pitch + c);
     }
     __syncthreads();
-    const uint8_t* sb = reinterpret_cast<const uint8_t*>(s_src);
+    // NB: read aligned dwords and split them; byte-indexed LDS reads get merged by
+    // hipcc into ds_read_u16 at odd offsets, which gfx950 serves misaligned.
     for (int i = threadIdx.x; i < (BT_H + 6) * (BT_W / 4); i += 256) {
         const int r = i / (BT_W / 4), q = i - r * (BT_W / 4);
-        const uint8_t* src = sb + r * BT_LW + 4 * q;
+        const uint32_t w0 = s_src[r * WPR + q], w1 = s_src[r * WPR + q + 1], w2 = s_src[r * WPR + q + 2];
         int v[10];
 #pragma unroll
-        for (int k = 0; k < 10; k++) v[k] = src[k];
+        for (int k = 0; k < 4; k++) {
+            v[k] = (w0 >> (8 * k)) & 0xff;
+            v[4 + k] = (w1 >> (8 * k)) & 0xff;
+        }
+        v[8] = w2 & 0xff;
+        v[9] = (w2 >> 8) & 0xff;
         int4 o;
         o.x = c_gauss[0] * v[0] + c_gauss[1] * v[1] + c_gauss[2] * v[2] + c_gauss[3] * v[3] + c_gauss[4] * v[4] + c_gauss[5] * v[5] + c_gauss[6] * v[6];
         o.y = c_gauss[0] * v[1] + c_gauss[1] * v[2] + c_gauss[2] * v[3] + c_gauss[3] * v[4] + c_gauss[4] * v[5] + c_gauss[5] * v[6] + c_gauss[6] * v[7];
@@ -894,6 +900,17 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     }
     ORB_HIP_CHECK(hipStreamSynchronize(s));
     last_B_ = B;
+    return 0;
+}
+
+int Extractor::get_blurred(int index, int level, uint8_t* dst, int dst_step, int* w, int* h) {
+    if (level < 0 || level >= nlevels_ || index < 0 || index >= last_B_ || !d_blur_) return -1;
+    const LevelHost& L = levels_[level];
+    *w = L.w;
+    *h = L.h;
+    if (!dst) return 0;
+    ORB_HIP_CHECK(hipMemcpy2D(dst, dst_step, (const uint8_t*)d_blur_ + (size_t)index * blur_bytes_ + L.boff, L.bpitch,
+                              L.w, L.h, hipMemcpyDeviceToHost));
     return 0;
 }
 

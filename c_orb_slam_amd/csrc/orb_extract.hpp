@@ -52,6 +52,7 @@ public:
     int extract(const uint8_t* imgs, int B, int W, int H, int step, size_t img_stride, bool imgs_on_device,
                 orb_kp* kps, uint8_t* desc, int cap, bool out_on_device, int* n_out);
     int get_level(int index, int level, uint8_t* dst, int dst_step, int* w, int* h);
+    int get_blurred(int index, int level, uint8_t* dst, int dst_step, int* w, int* h);
     int timings(float* ms6);
     hipStream_t stream() const { return stream_; }
 

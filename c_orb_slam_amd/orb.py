@@ -87,6 +87,15 @@ class ORBextractor:
                                              C.byref(h)), "get_level")
         return out
 
+    def blurred_level(self, level, index=0):
+        """GaussianBlur working image of `level` (diagnostic; ORBextractor.cc:1085-1086)."""
+        w, h = C.c_int(), C.c_int()
+        check(self._L.ORBextractor_get_blurred_level(self._h, index, level, None, 0, C.byref(w), C.byref(h)))
+        out = np.zeros((h.value, w.value), np.uint8)
+        check(self._L.ORBextractor_get_blurred_level(self._h, index, level, ptr(out), out.strides[0], C.byref(w),
+                                                     C.byref(h)))
+        return out
+
     def _tables(self):
         nl = self.nlevels
         t = [np.zeros(nl, np.float32) for _ in range(4)] + [np.zeros(nl, np.int32)]

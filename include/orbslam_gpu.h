@@ -77,6 +77,10 @@ int ORBextractor_extract_batch(ORBextractor_h h, const uint8_t* imgs, int batch,
  * dst must hold (w+38)*(h+38) bytes at stride dst_step; *w,*h = unpadded dims. */
 int ORBextractor_get_level(ORBextractor_h h, int index, int level, uint8_t* dst, int dst_step,
                            int* w, int* h_);
+/* Diagnostic: the GaussianBlur(7x7, 2) working image of `level` (ORBextractor.cc:1085-1086,
+ * no border) of image `index` of the last call; dst holds w*h bytes at dst_step. */
+int ORBextractor_get_blurred_level(ORBextractor_h h, int index, int level, uint8_t* dst,
+                                   int dst_step, int* w, int* h_);
 /* GetLevels/GetScaleFactor/GetScaleFactors/GetInverseScaleFactors/
  * GetScaleSigmaSquares/GetInverseScaleSigmaSquares   ORBextractor.h:63-85 */
 int ORBextractor_get_levels(ORBextractor_h h, int* nlevels, float* scaleFactor);

@@ -51,6 +51,9 @@ def test_extract_bit_exact(gpu, w, h, nf, seed):
         ol = orc.level(l)
         assert gl.shape == ol.shape
         assert np.array_equal(gl, ol), f"pyramid level {l} differs at {np.argwhere(gl != ol)[:5]}"
+    for l in range(8):
+        gb, ob = ex.blurred_level(l), orc.blurred(l)
+        assert np.array_equal(gb, ob), f"blurred level {l} differs at {np.argwhere(gb != ob)[:5]}"
     assert len(gk) == len(ok) and np.array_equal(gk.view(np.uint8), ok.view(np.uint8)), _diag(gk, gd, ok, od)
     assert np.array_equal(gd, od)
 
