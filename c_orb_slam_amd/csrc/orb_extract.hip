@@ -145,10 +145,13 @@ __global__ void __launch_bounds__(256) k_blur7(const uint8_t* __restrict__ pyr, 
             acc.x += c_gauss[k] * t.x; acc.y += c_gauss[k] * t.y;
             acc.z += c_gauss[k] * t.z; acc.w += c_gauss[k] * t.w;
         }
-        const uint32_t px = (uint32_t)min(max((acc.x + (1 << 15)) >> 16, 0), 255) |
-                            ((uint32_t)min(max((acc.y + (1 << 15)) >> 16, 0), 255) << 8) |
-                            ((uint32_t)min(max((acc.z + (1 << 15)) >> 16, 0), 255) << 16) |
-                            ((uint32_t)min(max((acc.w + (1 << 15)) >> 16, 0), 255) << 24);
+        // every term is >= 0, so saturate_cast<uchar> is an unsigned min.  (The signed
+        // min(max(.,0),255) form is lowered by hipcc to v_ashr_pk_u8_i32 pairs whose
+        // destination high half is not cleared before the following v_or3_b32.)
+        const uint32_t px = min((uint32_t)(acc.x + (1 << 15)) >> 16, 255u) |
+                            (min((uint32_t)(acc.y + (1 << 15)) >> 16, 255u) << 8) |
+                            (min((uint32_t)(acc.z + (1 << 15)) >> 16, 255u) << 16) |
+                            (min((uint32_t)(acc.w + (1 << 15)) >> 16, 255u) << 24);
         *reinterpret_cast<uint32_t*>(O + (size_t)y * tl.bpitch + x) = px;
     }
 }
