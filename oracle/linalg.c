@@ -143,11 +143,13 @@ static void jacobi_svd(double* At, int astep, double* W_out, double* Vt, int vst
  * transposed left vectors, Vt (n x n). */
 void ora_svd(const double* A, int m, int n, double* w, double* Ut, double* Vt)
 {
-    double At[32 * 32];
+    double At[32 * 32], Vtmp[32 * 32];
+    const int uv = (Ut || Vt) != 0;  /* SVD::compute allocates temp_v whenever u or vt is wanted */
     for (int i = 0; i < n; i++)
         for (int k = 0; k < m; k++) At[i * m + k] = A[k * n + i];
-    jacobi_svd(At, m, w, Vt, n, m, n, (Ut || Vt) ? n : 0);
+    jacobi_svd(At, m, w, uv ? Vtmp : NULL, n, m, n, uv ? n : 0);
     if (Ut) memcpy(Ut, At, sizeof(double) * n * m);
+    if (Vt) memcpy(Vt, Vtmp, sizeof(double) * n * n);
 }
 
 /* SVBkSb: x (n) = V diag(1/w) U^T b, skipping w <= 2*DBL_EPSILON * sum(w). */

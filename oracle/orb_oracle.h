@@ -140,6 +140,27 @@ void  ora_rng_seed(ora_rng* g, unsigned int seed);
 int   ora_rng_rand(ora_rng* g);
 int   ora_rng_random_int(ora_rng* g, int min, int max);  /* DUtils::Random::RandomInt */
 
+/* ---- OpenCV C-API linear algebra restated (linalg.c) --------------------- */
+void  ora_svd(const double* A, int m, int n, double* w, double* Ut, double* Vt);
+void  ora_svd_solve(const double* A, int m, int n, const double* b, double* x);
+void  ora_svd_invert(const double* A, int n, double* X);
+void  ora_mul_transposed_ata(const double* src, int rows, int cols, double* dst);
+
+/* ---- PnPsolver (pnp.c), reference src/PnPsolver.cc ------------------------ */
+typedef struct ora_pnp ora_pnp;
+double ora_epnp_compute_pose(const double* pws, const double* us, int n, double fu, double fv, double uc,
+                             double vc, double R[3][3], double t[3]);
+ora_pnp* ora_pnp_new(int N, const float* p3d, const float* p2d, const float* sigma2, const int* kpIdx,
+                     int nMatches, float fx, float fy, float cx, float cy);
+void  ora_pnp_free(ora_pnp* P);
+void  ora_pnp_set_ransac(ora_pnp* P, double probability, int minInliers, int maxIterations, int minSet,
+                         float epsilon, float th2);
+int   ora_pnp_iterate(ora_pnp* P, int nIterations, ora_rng* rng, int* bNoMore, uint8_t* inliers_out,
+                      int* nInliers, float* Tcw);
+int   ora_pnp_iterations(const ora_pnp* P);
+int   ora_pnp_max_its(const ora_pnp* P);
+int   ora_pnp_min_inliers(const ora_pnp* P);
+
 #ifdef __cplusplus
 }
 #endif

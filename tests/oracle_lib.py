@@ -213,3 +213,53 @@ def oracle_search_local(F, cur_mp, mp_obs, in_view, proj_x, proj_xr, proj_y, lev
     L.ora_search_by_projection_local.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float,
                                                  C.c_float]
     return L.ora_search_by_projection_local(C.byref(of.s), ptr(cur_mp), ptr(obs), C.byref(m), th, nnratio)
+
+
+# ---------------------------------------------------------------- PnP oracle
+class OraclePnP:
+    """PnPsolver(F, vpMapPointMatches) restated on CPU (reference src/PnPsolver.cc)."""
+
+    def __init__(self, p3d, p2d, sigma2, kp_idx, n_matches, fx, fy, cx, cy):
+        L = lib()
+        L.ora_pnp_new.restype = C.c_void_p
+        L.ora_pnp_new.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float,
+                                  C.c_float, C.c_float, C.c_float]
+        L.ora_pnp_free.argtypes = [C.c_void_p]
+        L.ora_pnp_set_ransac.argtypes = [C.c_void_p, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
+        L.ora_pnp_iterate.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p]
+        for f in ("ora_pnp_iterations", "ora_pnp_max_its", "ora_pnp_min_inliers"):
+            getattr(L, f).argtypes = [C.c_void_p]
+        self.L = L
+        self.p3d = np.ascontiguousarray(p3d, np.float32)
+        self.p2d = np.ascontiguousarray(p2d, np.float32)
+        self.s2 = np.ascontiguousarray(sigma2, np.float32)
+        self.kp = np.ascontiguousarray(kp_idx, np.int32)
+        self.n_matches = n_matches
+        self.h = L.ora_pnp_new(len(self.p3d), ptr(self.p3d), ptr(self.p2d), ptr(self.s2), ptr(self.kp), n_matches,
+                               fx, fy, cx, cy)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.ora_pnp_free(self.h)
+
+    def set_ransac(self, probability=0.99, minInliers=8, maxIterations=300, minSet=4, epsilon=0.4, th2=5.991):
+        self.L.ora_pnp_set_ransac(self.h, probability, minInliers, maxIterations, minSet, epsilon, th2)
+
+    def iterate(self, n_iterations, rng):
+        no_more = C.c_int()
+        nin = C.c_int()
+        inl = np.zeros(max(self.n_matches, 1), np.uint8)
+        T = np.zeros(16, np.float32)
+        ok = self.L.ora_pnp_iterate(self.h, n_iterations, rng, C.byref(no_more), ptr(inl), C.byref(nin), ptr(T))
+        return bool(ok), T.reshape(4, 4), inl[:self.n_matches].astype(bool), nin.value, bool(no_more.value)
+
+    @property
+    def iterations(self):
+        return self.L.ora_pnp_iterations(self.h)
+
+
+def new_rng(seed=1):
+    g = (C.c_int32 * 40)()
+    lib().ora_rng_seed(g, seed)
+    return g
