@@ -91,8 +91,20 @@ def lib():
     L.ORBmatcher_SearchByProjection_MapPoints.argtypes = [vp, P(orb_frame), vp, i32, vp, vp, vp, vp, vp, vp, vp,
                                                           P(orb_mappoints), f32, P(i32)]
     L.ORBmatcher_SearchCandidates.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp]
+    L.orb_rng_seed.argtypes = [vp, C.c_uint]
+    L.orb_rng_rand.argtypes = [vp]
+    L.PnPsolver_create.argtypes = [i32, vp, vp, vp, vp, i32, f32, f32, f32, f32, P(vp)]
+    L.PnPsolver_destroy.argtypes = [vp]
+    L.PnPsolver_set_ransac.argtypes = [vp, C.c_double, i32, i32, i32, f32, f32]
+    L.PnPsolver_iterate.argtypes = [vp, i32, vp, P(i32), vp, P(i32), vp, P(i32)]
+    L.PnPsolver_iterate_batch.argtypes = [i32, vp, i32, vp, vp, vp, vp, vp, vp]
+    L.PnPsolver_get_state.argtypes = [vp, P(i32), P(i32), P(i32)]
     _lib = L
     return L
+
+
+class orb_rng(C.Structure):
+    _fields_ = [("tbl", C.c_int32 * 31), ("f", C.c_int32), ("r", C.c_int32)]
 
 
 def ptr(a):

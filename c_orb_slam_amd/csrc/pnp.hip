@@ -1,0 +1,453 @@
+// pnp.hip -- gfx950 EPnP RANSAC: the device side of PnPsolver::iterate
+// (reference src/PnPsolver.cc:165-339).
+//
+// The reference loop draws a minimal set with the process rand(), solves
+// EPnP, scores every correspondence, and returns as soon as Refine() on the
+// best-so-far inliers succeeds.  The draws do not depend on the results, so a
+// call's hypotheses are generated up front from a snapshot of the caller's
+// glibc-rand state and scored in ONE launch for every solver of the batch
+// (k_pnp_hypotheses: a thread per hypothesis, EPnP in FP64 + CheckInliers over
+// all N correspondences, inlier bitmask out).  The host then replays the
+// sequential accept/Refine logic; each Refine it reaches is one more launch
+// (k_pnp_refine), and the RNG is re-advanced by exactly the draws the
+// reference would have consumed.
+#include "pnp.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "epnp.hpp"
+
+namespace orbgpu {
+
+struct IdxPts {
+    const float* p3d;
+    const float* p2d;
+    const int* idx;
+    __device__ void pw(int k, double out[3]) const {
+        const int i = idx[k];
+        out[0] = p3d[3 * i];
+        out[1] = p3d[3 * i + 1];
+        out[2] = p3d[3 * i + 2];
+    }
+    __device__ void uv(int k, double& u, double& v) const {
+        const int i = idx[k];
+        u = p2d[2 * i];
+        v = p2d[2 * i + 1];
+    }
+};
+
+// PnPsolver::CheckInliers (308-339): float/double mix kept expression by expression.
+__device__ inline int check_inliers(const PnPProbDev& P, const double R[3][3], const double t[3], uint32_t* mask) {
+    int n = 0;
+    const int words = (P.N + 31) >> 5;
+    for (int w = 0; w < words; w++) {
+        uint32_t bits = 0;
+        for (int b = 0; b < 32; b++) {
+            const int i = w * 32 + b;
+            if (i >= P.N) break;
+            const float X = P.p3d[3 * i], Y = P.p3d[3 * i + 1], Z = P.p3d[3 * i + 2];
+            const float Xc = (float)(R[0][0] * X + R[0][1] * Y + R[0][2] * Z + t[0]);
+            const float Yc = (float)(R[1][0] * X + R[1][1] * Y + R[1][2] * Z + t[1]);
+            const float invZc = (float)(1 / (R[2][0] * X + R[2][1] * Y + R[2][2] * Z + t[2]));
+            const double ue = P.uc + P.fu * Xc * invZc;
+            const double ve = P.vc + P.fv * Yc * invZc;
+            const float distX = (float)(P.p2d[2 * i] - ue);
+            const float distY = (float)(P.p2d[2 * i + 1] - ve);
+            const float error2 = distX * distX + distY * distY;
+            if (error2 < P.maxErr[i]) {
+                bits |= 1u << b;
+                n++;
+            }
+        }
+        mask[w] = bits;
+    }
+    return n;
+}
+
+__device__ inline void store_rt(double* out, const double R[3][3], const double t[3]) {
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) out[3 * i + j] = R[i][j];
+        out[9 + i] = t[i];
+    }
+}
+
+__global__ void __launch_bounds__(64) k_pnp_hypotheses(const PnPProbDev* __restrict__ probs) {
+    const PnPProbDev P = probs[blockIdx.y];
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= P.nhyp) return;
+    IdxPts pts{P.p3d, P.p2d, P.hyp_idx + (size_t)h * P.minSet};
+    epnp::Solver<IdxPts> S(pts, P.minSet, P.fu, P.fv, P.uc, P.vc);
+    double R[3][3], t[3];
+    S.compute_pose(R, t);
+    const int words = (P.N + 31) >> 5;
+    P.counts[h] = check_inliers(P, R, t, P.masks + (size_t)h * words);
+    store_rt(P.rt + (size_t)h * 12, R, t);
+}
+
+// Refine (260-305): EPnP on the best-so-far inliers, then CheckInliers.
+__global__ void __launch_bounds__(64) k_pnp_refine(const PnPProbDev* __restrict__ probs, int nprob) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= nprob) return;
+    const PnPProbDev P = probs[p];
+    IdxPts pts{P.p3d, P.p2d, P.ref_idx};
+    epnp::Solver<IdxPts> S(pts, P.ref_n, P.fu, P.fv, P.uc, P.vc);
+    double R[3][3], t[3];
+    S.compute_pose(R, t);
+    P.ref_out[0] = check_inliers(P, R, t, P.ref_mask);
+    store_rt(P.ref_rt, R, t);
+}
+
+// ------------------------------------------------------------------- host
+// glibc random_r TYPE_3 (degree 31, separation 3, 310 warm-up draws)
+void rng_seed(orb_rng* g, unsigned seed) {
+    if (seed == 0) seed = 1;
+    int32_t word = (int32_t)seed;
+    g->tbl[0] = word;
+    for (int i = 1; i < 31; i++) {
+        const long hi = word / 127773, lo = word % 127773;
+        word = (int32_t)(16807 * lo - 2836 * hi);
+        if (word < 0) word += 2147483647;
+        g->tbl[i] = word;
+    }
+    g->f = 3;
+    g->r = 0;
+    for (int i = 0; i < 310; i++) (void)rng_rand(g);
+}
+
+int rng_rand(orb_rng* g) {
+    const uint32_t val = (uint32_t)g->tbl[g->f] + (uint32_t)g->tbl[g->r];
+    g->tbl[g->f] = (int32_t)val;
+    const int result = (int)(val >> 1);
+    if (++g->f >= 31) {
+        g->f = 0;
+        ++g->r;
+    } else if (++g->r >= 31) {
+        g->r = 0;
+    }
+    return result;
+}
+
+// DUtils::Random::RandomInt (Random.cpp:47-50)
+static int random_int(orb_rng* g, int min, int max) {
+    const int d = max - min + 1;
+    return int(((double)rng_rand(g) / ((double)2147483647 + 1.0)) * d) + min;
+}
+
+PnPSolver::PnPSolver(int N, const float* p3d, const float* p2d, const float* sigma2, const int* kpIdx, int nMatches,
+                     float fx, float fy, float cx, float cy)
+    : N_(N), nMatches_(nMatches), fu_(fx), fv_(fy), uc_(cx), vc_(cy) {
+    p3d_.assign(p3d, p3d + 3 * (size_t)N);
+    p2d_.assign(p2d, p2d + 2 * (size_t)N);
+    sigma2_.assign(sigma2, sigma2 + N);
+    kpIdx_.assign(kpIdx, kpIdx + N);
+    maxErr_.assign(N, 0.f);
+    bestInliers_.assign(N, 0);
+    set_ransac(0.99, 8, 300, 4, 0.4f, 5.991f);  // PnPsolver.h:67 defaults (ctor calls SetRansacParameters())
+}
+
+PnPSolver::~PnPSolver() {
+    if (d_pts_) (void)hipFree(d_pts_);
+}
+
+// SetRansacParameters, PnPsolver.cc:121-157
+void PnPSolver::set_ransac(double probability, int minInliers, int maxIterations, int minSet, float epsilon, float th2) {
+    prob_ = probability;
+    minInliers_ = minInliers;
+    maxIts_ = maxIterations;
+    epsilon_ = epsilon;
+    minSet_ = minSet;
+    int nMinInliers = (int)(N_ * epsilon_);
+    if (nMinInliers < minInliers_) nMinInliers = minInliers_;
+    if (nMinInliers < minSet) nMinInliers = minSet;
+    minInliers_ = nMinInliers;
+    if (epsilon_ < (float)minInliers_ / N_) epsilon_ = (float)minInliers_ / N_;
+    int nIterations;
+    if (minInliers_ == N_) nIterations = 1;
+    else nIterations = (int)std::ceil(std::log(1 - prob_) / std::log(1 - std::pow(epsilon_, 3)));
+    maxIts_ = std::max(1, std::min(nIterations, maxIts_));
+    for (int i = 0; i < N_; i++) maxErr_[i] = sigma2_[i] * th2;
+    dev_dirty_ = true;
+}
+
+int PnPSolver::upload(hipStream_t s) {
+    if (!dev_dirty_) return 0;
+    const size_t bytes = (size_t)N_ * (3 + 2 + 1) * 4 + 64;
+    if (bytes > d_pts_cap_) {
+        if (d_pts_) (void)hipFree(d_pts_);
+        ORB_HIP_CHECK(hipMalloc(&d_pts_, bytes));
+        d_pts_cap_ = bytes;
+    }
+    float* d = (float*)d_pts_;
+    ORB_HIP_CHECK(hipMemcpyAsync(d, p3d_.data(), (size_t)N_ * 12, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(d + 3 * N_, p2d_.data(), (size_t)N_ * 8, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(d + 5 * N_, maxErr_.data(), (size_t)N_ * 4, hipMemcpyHostToDevice, s));
+    dev_dirty_ = false;
+    return 0;
+}
+
+static void rt_to_tcw(const double* rt, float* T) {
+    // cv::Mat(3,3,CV_64F,mRi).convertTo(CV_32F) into eye(4) (PnPsolver.cc:217-224)
+    for (int i = 0; i < 16; i++) T[i] = 0.f;
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) T[4 * i + j] = (float)rt[3 * i + j];
+        T[4 * i + 3] = (float)rt[9 + i];
+    }
+    T[15] = 1.f;
+}
+
+PnPBatch::~PnPBatch() {
+    if (d_work_) (void)hipFree(d_work_);
+    if (d_probs_) (void)hipFree(d_probs_);
+    if (h_work_) (void)hipHostFree(h_work_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+int PnPBatch::init() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
+    ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    return 0;
+}
+
+int PnPBatch::ensure(size_t dev_bytes, size_t host_bytes, size_t probs) {
+    if (dev_bytes > work_cap_) {
+        if (d_work_) (void)hipFree(d_work_);
+        ORB_HIP_CHECK(hipMalloc(&d_work_, dev_bytes));
+        work_cap_ = dev_bytes;
+    }
+    if (host_bytes > hwork_cap_) {
+        if (h_work_) (void)hipHostFree(h_work_);
+        ORB_HIP_CHECK(hipHostMalloc(&h_work_, host_bytes));
+        hwork_cap_ = host_bytes;
+    }
+    if (probs * sizeof(PnPProbDev) > probs_cap_) {
+        if (d_probs_) (void)hipFree(d_probs_);
+        ORB_HIP_CHECK(hipMalloc(&d_probs_, probs * sizeof(PnPProbDev)));
+        probs_cap_ = probs * sizeof(PnPProbDev);
+    }
+    return 0;
+}
+
+// PnPsolver::iterate for `n` solvers; solver k draws from rngs[k] (may alias).
+int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnPResult* res) {
+    hipStream_t s = stream_;
+    struct Job {
+        int K = 0;            // hypotheses generated for this call
+        orb_rng snap;         // RNG state before the call
+        size_t hyp_off = 0, mask_off = 0, cnt_off = 0, rt_off = 0;
+        bool active = false;
+        int next = 0;         // next hypothesis to replay
+    };
+    std::vector<Job> jobs(n);
+    size_t dev = 0, host = 0;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    for (int k = 0; k < n; k++) {
+        PnPSolver& P = *S[k];
+        PnPResult& r = res[k];
+        r.has_pose = 0;
+        r.bNoMore = 0;
+        r.nInliers = 0;
+        if (r.inliers) std::fill(r.inliers, r.inliers + P.nMatches_, 0);  // vbInliers.clear()
+        if (P.N_ < P.minInliers_) {  // 176-180
+            r.bNoMore = 1;
+            continue;
+        }
+        Job& J = jobs[k];
+        J.K = std::max(P.maxIts_ - P.nIterations_, nIterations);  // `while (it < max || cur < nIt)`
+        if (J.K <= 0) J.K = 0;
+        J.active = J.K > 0;
+        J.snap = *rngs[k];
+        const int words = (P.N_ + 31) >> 5;
+        J.hyp_off = dev; dev += al((size_t)J.K * P.minSet_ * 4);
+        J.mask_off = dev; dev += al((size_t)J.K * words * 4);
+        J.cnt_off = dev; dev += al((size_t)J.K * 4);
+        J.rt_off = dev; dev += al((size_t)J.K * 12 * 8);
+        host = std::max(host, (size_t)J.K * (P.minSet_ * 4 + words * 4 + 4 + 96));
+        if (int e = P.upload(s)) return e;
+    }
+    // refine scratch (per solver): idx list N + mask + rt + count
+    size_t ref_base = dev;
+    for (int k = 0; k < n; k++) dev += al((size_t)S[k]->N_ * 4 + ((S[k]->N_ + 31) / 32) * 4 + 12 * 8 + 16);
+    if (int e = ensure(dev + 256, (host + 256) * n + 1024, (size_t)n)) return e;
+    char* D = (char*)d_work_;
+    char* Hh = (char*)h_work_;
+    // 1. generate all hypotheses (draws as the reference would make them)
+    std::vector<int> hyp;
+    std::vector<PnPProbDev> pd(n);
+    int maxK = 0;
+    for (int k = 0; k < n; k++) {
+        Job& J = jobs[k];
+        PnPSolver& P = *S[k];
+        std::memset(&pd[k], 0, sizeof(PnPProbDev));
+        if (!J.active) continue;
+        orb_rng g = J.snap;
+        hyp.assign((size_t)J.K * P.minSet_, 0);
+        std::vector<int> avail(P.N_);
+        for (int h = 0; h < J.K; h++) {
+            for (int i = 0; i < P.N_; i++) avail[i] = i;
+            int navail = P.N_;
+            for (int i = 0; i < P.minSet_; ++i) {
+                const int randi = random_int(&g, 0, navail - 1);
+                hyp[(size_t)h * P.minSet_ + i] = avail[randi];
+                avail[randi] = avail[navail - 1];
+                navail--;
+            }
+        }
+        ORB_HIP_CHECK(hipMemcpyAsync(D + J.hyp_off, hyp.data(), hyp.size() * 4, hipMemcpyHostToDevice, s));
+        const float* dp = (const float*)P.d_pts_;
+        PnPProbDev& q = pd[k];
+        q.p3d = dp;
+        q.p2d = dp + 3 * P.N_;
+        q.maxErr = dp + 5 * P.N_;
+        q.N = P.N_;
+        q.fu = P.fu_; q.fv = P.fv_; q.uc = P.uc_; q.vc = P.vc_;
+        q.hyp_idx = (const int*)(D + J.hyp_off);
+        q.nhyp = J.K;
+        q.minSet = P.minSet_;
+        q.counts = (int*)(D + J.cnt_off);
+        q.masks = (uint32_t*)(D + J.mask_off);
+        q.rt = (double*)(D + J.rt_off);
+        maxK = std::max(maxK, J.K);
+    }
+    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(PnPProbDev) * n, hipMemcpyHostToDevice, s));
+    if (maxK > 0)
+        hipLaunchKernelGGL(k_pnp_hypotheses, dim3((maxK + 63) / 64, n), dim3(64), 0, s, (const PnPProbDev*)d_probs_);
+    ORB_HIP_CHECK(hipGetLastError());
+    // 2. results back (counts, masks, poses) in one pinned region per solver
+    std::vector<size_t> hoff(n, 0);
+    size_t ho = 0;
+    for (int k = 0; k < n; k++) {
+        Job& J = jobs[k];
+        if (!J.active) continue;
+        PnPSolver& P = *S[k];
+        const int words = (P.N_ + 31) >> 5;
+        hoff[k] = ho;
+        ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho, D + J.cnt_off, (size_t)J.K * 4, hipMemcpyDeviceToHost, s));
+        ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho + al((size_t)J.K * 4), D + J.mask_off, (size_t)J.K * words * 4,
+                                     hipMemcpyDeviceToHost, s));
+        ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho + al((size_t)J.K * 4) + al((size_t)J.K * words * 4), D + J.rt_off,
+                                     (size_t)J.K * 96, hipMemcpyDeviceToHost, s));
+        ho += al((size_t)J.K * 4) + al((size_t)J.K * words * 4) + al((size_t)J.K * 96);
+    }
+    ORB_HIP_CHECK(hipStreamSynchronize(s));
+    // 3. sequential replay; Refine requests batched across solvers
+    std::vector<char> done(n, 0);
+    std::vector<int> ref_n(n, 0);
+    for (int k = 0; k < n; k++) done[k] = !jobs[k].active;
+    for (;;) {
+        std::vector<int> need;  // solvers waiting for a Refine
+        for (int k = 0; k < n; k++) {
+            if (done[k]) continue;
+            Job& J = jobs[k];
+            PnPSolver& P = *S[k];
+            const int words = (P.N_ + 31) >> 5;
+            const int* cnt = (const int*)(Hh + hoff[k]);
+            const uint32_t* masks = (const uint32_t*)(Hh + hoff[k] + al((size_t)J.K * 4));
+            const double* rts = (const double*)(Hh + hoff[k] + al((size_t)J.K * 4) + al((size_t)J.K * words * 4));
+            bool wait = false;
+            while (J.next < J.K) {
+                const int h = J.next;
+                if (P.refine_pending_ < 0) {  // iteration h not yet counted
+                    P.nIterations_++;
+                    const int c = cnt[h];
+                    if (c >= P.minInliers_) {
+                        if (c > P.nBestInliers_) {
+                            for (int i = 0; i < P.N_; i++)
+                                P.bestInliers_[i] = (masks[(size_t)h * words + (i >> 5)] >> (i & 31)) & 1;
+                            P.nBestInliers_ = c;
+                            rt_to_tcw(rts + (size_t)h * 12, P.bestTcw_);
+                            P.refine_valid_ = false;
+                        }
+                        P.refine_pending_ = h;
+                        if (!P.refine_valid_) {  // Refine(best) not computed for this best set yet
+                            wait = true;
+                            break;
+                        }
+                    } else {
+                        J.next++;
+                        continue;
+                    }
+                }
+                // Refine result for the current best set is available
+                P.refine_pending_ = -1;
+                if (P.refNin_ > P.minInliers_) {
+                    PnPResult& r = res[k];
+                    r.has_pose = 1;
+                    r.nInliers = P.refNin_;
+                    std::fill(r.inliers, r.inliers + P.nMatches_, 0);
+                    for (int i = 0; i < P.N_; i++)
+                        if (P.refMask_[i >> 5] >> (i & 31) & 1) r.inliers[P.kpIdx_[i]] = 1;
+                    rt_to_tcw(P.refRt_, r.Tcw);
+                    // consumed draws: hypotheses 0..h
+                    *rngs[k] = J.snap;
+                    for (int d = 0; d < (h + 1) * P.minSet_; d++) (void)rng_rand(rngs[k]);
+                    done[k] = 1;
+                    break;
+                }
+                J.next++;
+            }
+            if (done[k]) continue;
+            if (wait) {
+                need.push_back(k);
+                continue;
+            }
+            // loop exhausted (PnPsolver.cc:241-257)
+            *rngs[k] = J.snap;
+            for (int d = 0; d < J.K * P.minSet_; d++) (void)rng_rand(rngs[k]);
+            PnPResult& r = res[k];
+            if (P.nIterations_ >= P.maxIts_) {
+                r.bNoMore = 1;
+                if (P.nBestInliers_ >= P.minInliers_) {
+                    r.has_pose = 1;
+                    r.nInliers = P.nBestInliers_;
+                    std::fill(r.inliers, r.inliers + P.nMatches_, 0);
+                    for (int i = 0; i < P.N_; i++)
+                        if (P.bestInliers_[i]) r.inliers[P.kpIdx_[i]] = 1;
+                    std::memcpy(r.Tcw, P.bestTcw_, sizeof(float) * 16);
+                }
+            }
+            done[k] = 1;
+        }
+        if (need.empty()) break;
+        // Refine launch for every waiting solver
+        std::vector<PnPProbDev> rq(need.size());
+        size_t ro = ref_base;
+        std::vector<size_t> roff(need.size());
+        for (size_t q = 0; q < need.size(); q++) {
+            PnPSolver& P = *S[need[q]];
+            std::vector<int> idx;
+            for (int i = 0; i < P.N_; i++)
+                if (P.bestInliers_[i]) idx.push_back(i);
+            roff[q] = ro;
+            const int words = (P.N_ + 31) >> 5;
+            ORB_HIP_CHECK(hipMemcpyAsync(D + ro, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, s));
+            PnPProbDev r = pd[need[q]];
+            r.ref_idx = (const int*)(D + ro);
+            r.ref_n = (int)idx.size();
+            r.ref_mask = (uint32_t*)(D + ro + al((size_t)P.N_ * 4));
+            r.ref_rt = (double*)(D + ro + al((size_t)P.N_ * 4) + al((size_t)words * 4));
+            r.ref_out = (int*)(D + ro + al((size_t)P.N_ * 4) + al((size_t)words * 4) + 96);
+            rq[q] = r;
+            ro += al((size_t)P.N_ * 4) + al((size_t)words * 4) + 96 + 256;
+        }
+        ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, rq.data(), sizeof(PnPProbDev) * rq.size(), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_pnp_refine, dim3((unsigned)(need.size() + 63) / 64), dim3(64), 0, s,
+                           (const PnPProbDev*)d_probs_, (int)need.size());
+        ORB_HIP_CHECK(hipGetLastError());
+        for (size_t q = 0; q < need.size(); q++) {
+            PnPSolver& P = *S[need[q]];
+            const int words = (P.N_ + 31) >> 5;
+            P.refMask_.resize(words);
+            ORB_HIP_CHECK(hipMemcpyAsync(P.refMask_.data(), rq[q].ref_mask, (size_t)words * 4, hipMemcpyDeviceToHost, s));
+            ORB_HIP_CHECK(hipMemcpyAsync(P.refRt_, rq[q].ref_rt, 96, hipMemcpyDeviceToHost, s));
+            ORB_HIP_CHECK(hipMemcpyAsync(&P.refNin_, rq[q].ref_out, 4, hipMemcpyDeviceToHost, s));
+        }
+        ORB_HIP_CHECK(hipStreamSynchronize(s));
+        for (int k : need) S[k]->refine_valid_ = true;
+    }
+    return 0;
+}
+
+}  // namespace orbgpu

@@ -1,0 +1,80 @@
+"""Host mirror of ORB_SLAM2::PnPsolver and DUtils::Random over the C ABI.
+
+PnPsolver(...) takes the packed correspondences the reference constructor
+builds from a Frame and its map-point matches (PnPsolver.cc:67-110).
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import check, lib, orb_rng, ptr
+
+
+class Rng:
+    """glibc rand() stream (srand(seed)); the reference's process RNG, made explicit."""
+
+    def __init__(self, seed=1):
+        self.s = orb_rng()
+        lib().orb_rng_seed(C.byref(self.s), seed)
+
+    def rand(self):
+        return lib().orb_rng_rand(C.byref(self.s))
+
+    def state(self):
+        return (tuple(self.s.tbl), self.s.f, self.s.r)
+
+
+class PnPsolver:
+    def __init__(self, p3d, p2d, sigma2, kp_index, n_matches, fx, fy, cx, cy):
+        self._L = lib()
+        self.p3d = np.ascontiguousarray(p3d, np.float32).reshape(-1, 3)
+        self.p2d = np.ascontiguousarray(p2d, np.float32).reshape(-1, 2)
+        self.sigma2 = np.ascontiguousarray(sigma2, np.float32)
+        self.kp = np.ascontiguousarray(kp_index, np.int32)
+        self.n_matches = int(n_matches)
+        h = C.c_void_p()
+        check(self._L.PnPsolver_create(len(self.p3d), ptr(self.p3d), ptr(self.p2d), ptr(self.sigma2), ptr(self.kp),
+                                       self.n_matches, fx, fy, cx, cy, C.byref(h)), "PnPsolver_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.PnPsolver_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def SetRansacParameters(self, probability=0.99, minInliers=8, maxIterations=300, minSet=4, epsilon=0.4,
+                            th2=5.991):
+        check(self._L.PnPsolver_set_ransac(self._h, probability, minInliers, maxIterations, minSet, epsilon, th2))
+
+    def iterate(self, nIterations, rng: Rng):
+        """-> (Tcw or None, bNoMore, vbInliers, nInliers)"""
+        no_more, nin, has = C.c_int(), C.c_int(), C.c_int()
+        inl = np.zeros(max(self.n_matches, 1), np.uint8)
+        T = np.zeros(16, np.float32)
+        check(self._L.PnPsolver_iterate(self._h, nIterations, C.byref(rng.s), C.byref(no_more), ptr(inl),
+                                        C.byref(nin), ptr(T), C.byref(has)), "PnPsolver_iterate")
+        return (T.reshape(4, 4) if has.value else None), bool(no_more.value), inl[:self.n_matches].astype(bool), \
+            nin.value
+
+    def state(self):
+        a, b, c = C.c_int(), C.c_int(), C.c_int()
+        check(self._L.PnPsolver_get_state(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
+
+
+def iterate_batch(solvers, nIterations, rngs):
+    """PnPsolver_iterate_batch: one hypothesis launch for all solvers."""
+    L = lib()
+    n = len(solvers)
+    hs = (C.c_void_p * n)(*[s._h.value for s in solvers])
+    rp = (C.c_void_p * n)(*[C.cast(C.byref(r.s), C.c_void_p).value for r in rngs])
+    bufs = [np.zeros(max(s.n_matches, 1), np.uint8) for s in solvers]
+    ip = (C.c_void_p * n)(*[b.ctypes.data for b in bufs])
+    nm, nin, has = (np.zeros(n, np.int32) for _ in range(3))
+    T = np.zeros((n, 16), np.float32)
+    check(L.PnPsolver_iterate_batch(n, hs, nIterations, rp, ptr(nm), ip, ptr(nin), ptr(T), ptr(has)),
+          "PnPsolver_iterate_batch")
+    return [((T[k].reshape(4, 4) if has[k] else None), bool(nm[k]), bufs[k][:solvers[k].n_matches].astype(bool),
+             int(nin[k])) for k in range(n)]

@@ -176,6 +176,53 @@ int ORBmatcher_SearchCandidates(ORBmatcher_h h, const uint8_t* qdesc, int nq,
                                 const int32_t* cand, int32_t* dist, int32_t* best_idx,
                                 int32_t* best_dist, int32_t* second_dist);
 
+/* ======================================================================
+ * RANSAC random stream  (DUtils::Random::RandomInt over glibc rand(),
+ * Thirdparty/DBoW2/DUtils/Random.cpp:47-50)
+ * The reference draws from the process-global rand() (never seeded on the
+ * stereo path => seed 1).  The boundary takes the stream explicitly: an
+ * orb_rng is the glibc TYPE_3 additive-feedback state, bit-identical to
+ * rand() after srand(seed); the solvers advance it by exactly the draws the
+ * reference's loops consume (early returns included).
+ * ====================================================================== */
+typedef struct orb_rng {
+    int32_t tbl[31];
+    int32_t f, r;
+} orb_rng;
+void orb_rng_seed(orb_rng* g, unsigned seed);   /* srand(seed) */
+int orb_rng_rand(orb_rng* g);                    /* rand() */
+
+/* ======================================================================
+ * PnPsolver  (reference include/PnPsolver.h:59-196, src/PnPsolver.cc)
+ * ====================================================================== */
+typedef struct PnPsolver_t* PnPsolver_h;
+
+/* PnPsolver(const Frame& F, const vector<MapPoint*>& vpMapPointMatches)  PnPsolver.cc:67-110
+ * The adapter packs the N matched, non-bad map points: p3d (N x 3, GetWorldPos),
+ * p2d (N x 2, F.mvKeysUn[i].pt), sigma2 (N, F.mvLevelSigma2[octave]),
+ * kp_index (N, mvKeyPointIndices) into vpMapPointMatches of size n_matches.
+ * SetRansacParameters() defaults are applied as in the reference ctor. */
+int PnPsolver_create(int N, const float* p3d, const float* p2d, const float* sigma2,
+                     const int32_t* kp_index, int n_matches, float fx, float fy, float cx,
+                     float cy, PnPsolver_h* out);
+int PnPsolver_destroy(PnPsolver_h h);
+/* SetRansacParameters(probability, minInliers, maxIterations, minSet, epsilon, th2)  121-157 */
+int PnPsolver_set_ransac(PnPsolver_h h, double probability, int minInliers, int maxIterations,
+                         int minSet, float epsilon, float th2);
+/* cv::Mat iterate(int nIterations, bool& bNoMore, vector<bool>& vbInliers, int& nInliers) 165-258
+ * inliers: n_matches bytes (vbInliers); Tcw: 16 floats (row-major CV_32F 4x4);
+ * *has_pose = 0 where the reference returns an empty cv::Mat. */
+int PnPsolver_iterate(PnPsolver_h h, int nIterations, orb_rng* rng, int* bNoMore,
+                      uint8_t* inliers, int* nInliers, float* Tcw, int* has_pose);
+/* `count` independent solvers in one hypothesis launch; solver k draws from rngs[k]
+ * (pass the same pointer for all to share one stream in solver order). Per-solver
+ * outputs at inliers[k] / Tcw + 16k / bNoMore[k] / nInliers[k] / has_pose[k]. */
+int PnPsolver_iterate_batch(int count, PnPsolver_h* hs, int nIterations, orb_rng** rngs,
+                            int* bNoMore, uint8_t** inliers, int* nInliers, float* Tcw,
+                            int* has_pose);
+/* RANSAC bookkeeping (mnIterations, mRansacMaxIts, mRansacMinInliers) */
+int PnPsolver_get_state(PnPsolver_h h, int* iterations, int* max_its, int* min_inliers);
+
 #ifdef __cplusplus
 }
 #endif

@@ -169,3 +169,41 @@ def test_oracle_keypoint_invariants():
         lvl = e.level(l)
         assert (lx >= 19 - 1e-3).all() and (lx <= lvl.shape[1] - 38 - 20 + 1e-3).all()
         assert (ly >= 19 - 1e-3).all()
+
+
+def test_oracle_svd_and_epnp():
+    """OpenCV-semantics SVD restatement reconstructs; EPnP is exact on noise-free 6+ points."""
+    import sys
+    from pnp_cases import rot
+    L = lib()
+    L.ora_svd.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ora_epnp_compute_pose.restype = C.c_double
+    L.ora_epnp_compute_pose.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_double,
+                                        C.c_double, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(0)
+    for m, n in [(3, 3), (6, 4), (12, 12), (6, 5)]:
+        A = rng.normal(size=(m, n))
+        w, Ut, Vt = np.zeros(n), np.zeros((n, m)), np.zeros((n, n))
+        L.ora_svd(ptr(A), m, n, ptr(w), ptr(Ut), ptr(Vt))
+        assert np.abs(Ut.T @ np.diag(w) @ Vt - A).max() < 1e-12
+        assert (np.diff(w) <= 0).all()
+    fx, fy, cx, cy = 718.856, 718.856, 607.1928, 185.2157
+    for trial in range(20):
+        R = rot(rng)
+        t = rng.uniform(-2, 2, 3)
+        n = 8
+        u, v, d = rng.uniform(20, 1220, n), rng.uniform(20, 356, n), rng.uniform(5, 50, n)
+        Xw = (np.stack([(u - cx) / fx * d, (v - cy) / fy * d, d], 1) - t) @ R
+        pws, us = np.ascontiguousarray(Xw), np.ascontiguousarray(np.stack([u, v], 1))
+        Ro, to = np.zeros((3, 3)), np.zeros(3)
+        L.ora_epnp_compute_pose(ptr(pws), ptr(us), n, fx, fy, cx, cy, ptr(Ro), ptr(to))
+        assert np.abs(Ro - R).max() < 1e-6 and np.abs(to - t).max() < 1e-5
+
+
+def test_oracle_pnp_ransac_recovers_pose():
+    from pnp_cases import pnp_problem
+    pr = pnp_problem(3, 500)
+    P = oracle_lib.OraclePnP(pr["p3d"], pr["p2d"], pr["sigma2"], pr["kp_idx"], pr["n_matches"], *pr["K"])
+    P.set_ransac(0.99, 10, 300, 4, 0.5, 5.991)
+    ok, T, inl, n, no_more = P.iterate(5, oracle_lib.new_rng(1))
+    assert ok and n > 250 and np.abs(T - pr["Tcw"]).max() < 0.1
