@@ -18,7 +18,7 @@ constexpr double kDblEps = 2.220446049250313e-16;
 constexpr double kDblMin = 2.2250738585072014e-308;
 
 // JacobiSVDImpl_<double> (OpenCV 3.2 lapack.cpp): At n x m (stride astep).
-__device__ inline void jacobi_svd(double* At, int astep, double* W_out, double* Vt, int vstep, int m, int n, int n1) {
+__device__ __forceinline__ void jacobi_svd(double* At, int astep, double* W_out, double* Vt, int vstep, int m, int n, int n1) {
     const double eps = kDblEps * 10;
     double W[12];
     const int max_iter = m > 30 ? m : 30;
@@ -129,13 +129,13 @@ __device__ inline void jacobi_svd(double* At, int astep, double* W_out, double* 
 }
 
 // SVD::compute(A m x n, m >= n): w, Ut (n x m), Vt (n x n).  A is consumed as At scratch.
-__device__ inline void svd(const double* A, int m, int n, double* w, double* Ut, double* Vt) {
+__device__ __forceinline__ void svd(const double* A, int m, int n, double* w, double* Ut, double* Vt) {
     for (int i = 0; i < n; i++)
         for (int k = 0; k < m; k++) Ut[i * m + k] = A[k * n + i];
     jacobi_svd(Ut, m, w, Vt, n, m, n, n);
 }
 
-__device__ inline void svd_solve(const double* A, int m, int n, const double* b, double* x) {
+__device__ __forceinline__ void svd_solve(const double* A, int m, int n, const double* b, double* x) {
     double w[6], Ut[36], Vt[36];
     svd(A, m, n, w, Ut, Vt);
     const int nm = m < n ? m : n;
@@ -154,7 +154,7 @@ __device__ inline void svd_solve(const double* A, int m, int n, const double* b,
     }
 }
 
-__device__ inline void svd_invert3(const double* A, double* X) {
+__device__ __forceinline__ void svd_invert3(const double* A, double* X) {
     double w[3], Ut[9], Vt[9], buf[3];
     svd(A, 3, 3, w, Ut, Vt);
     double threshold = 0;
@@ -171,13 +171,13 @@ __device__ inline void svd_invert3(const double* A, double* X) {
     }
 }
 
-__device__ inline double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-__device__ inline double dist2(const double* p1, const double* p2) {
+__device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ double dist2(const double* p1, const double* p2) {
     return (p1[0] - p2[0]) * (p1[0] - p2[0]) + (p1[1] - p2[1]) * (p1[1] - p2[1]) + (p1[2] - p2[2]) * (p1[2] - p2[2]);
 }
 
 // Householder QR solve (PnPsolver.cc:860-950, incl. its row-scan quirk); false if singular.
-__device__ inline bool qr_solve(double* A, int nr, int nc, double* b, double* X) {
+__device__ __forceinline__ bool qr_solve(double* A, int nr, int nc, double* b, double* X) {
     double A1[4], A2[4];
     double* pA = A;
     double* ppAkk = pA;
@@ -247,7 +247,7 @@ __device__ inline bool qr_solve(double* A, int nr, int nc, double* b, double* X)
     return true;
 }
 
-__device__ inline void gauss_newton(const double* L, const double* rho, double betas[4]) {
+__device__ __forceinline__ void gauss_newton(const double* L, const double* rho, double betas[4]) {
     double A[24], b[6], x[4] = {0, 0, 0, 0};
     for (int k = 0; k < 5; k++) {
         for (int i = 0; i < 6; i++) {
@@ -275,23 +275,23 @@ struct Solver {
     double fu, fv, uc, vc;
     double cws[4][3], ccs[4][3], ci[9];
 
-    __device__ Solver(const Pts& p, int n_, double fu_, double fv_, double uc_, double vc_)
+    __device__ __forceinline__ Solver(const Pts& p, int n_, double fu_, double fv_, double uc_, double vc_)
         : P(p), n(n_), fu(fu_), fv(fv_), uc(uc_), vc(vc_) {}
 
-    __device__ void alphas(int i, double a[4]) const {
+    __device__ __forceinline__ void alphas(int i, double a[4]) const {
         double pi[3];
         P.pw(i, pi);
         for (int j = 0; j < 3; j++)
             a[1 + j] = ci[3 * j] * (pi[0] - cws[0][0]) + ci[3 * j + 1] * (pi[1] - cws[0][1]) + ci[3 * j + 2] * (pi[2] - cws[0][2]);
         a[0] = 1.0f - a[1] - a[2] - a[3];
     }
-    __device__ void pc(int i, double out[3]) const {
+    __device__ __forceinline__ void pc(int i, double out[3]) const {
         double a[4];
         alphas(i, a);
         for (int j = 0; j < 3; j++) out[j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
     }
 
-    __device__ void choose_control_points() {
+    __device__ __forceinline__ void choose_control_points() {
         cws[0][0] = cws[0][1] = cws[0][2] = 0;
         for (int i = 0; i < n; i++) {
             double p[3];
@@ -318,7 +318,7 @@ struct Solver {
         }
     }
 
-    __device__ void barycentric() {
+    __device__ __forceinline__ void barycentric() {
         double cc[9];
         for (int i = 0; i < 3; i++)
             for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = cws[j][i] - cws[0][i];
@@ -326,7 +326,7 @@ struct Solver {
     }
 
     // cvMulTransposed(M, MtM, 1): rows of M in order 2i, 2i+1, accumulated in place.
-    __device__ void mtm(double* out) const {
+    __device__ __forceinline__ void mtm(double* out) const {
         for (int i = 0; i < 144; i++) out[i] = 0;
         for (int i = 0; i < n; i++) {
             double a[4], u, v;
@@ -350,7 +350,7 @@ struct Solver {
             for (int c = 0; c < r; c++) out[r * 12 + c] = out[c * 12 + r];
     }
 
-    __device__ double reprojection_error(const double R[3][3], const double t[3]) const {
+    __device__ __forceinline__ double reprojection_error(const double R[3][3], const double t[3]) const {
         double sum2 = 0.0;
         for (int i = 0; i < n; i++) {
             double pw[3], u, v;
@@ -366,7 +366,7 @@ struct Solver {
         return sum2 / n;
     }
 
-    __device__ void estimate_R_and_t(double R[3][3], double t[3]) const {
+    __device__ __forceinline__ void estimate_R_and_t(double R[3][3], double t[3]) const {
         double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
         for (int i = 0; i < n; i++) {
             double pcv[3], pw[3];
@@ -413,7 +413,7 @@ struct Solver {
         t[2] = pc0[2] - dot3(R[2], pw0);
     }
 
-    __device__ double compute_R_and_t(const double* ut, const double* betas, double R[3][3], double t[3]) {
+    __device__ __forceinline__ double compute_R_and_t(const double* ut, const double* betas, double R[3][3], double t[3]) {
         for (int i = 0; i < 4; i++) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
         for (int i = 0; i < 4; i++) {
             const double* v = ut + 12 * (11 - i);
@@ -431,7 +431,7 @@ struct Solver {
     }
 
     // compute_pose, PnPsolver.cc:477-525
-    __device__ double compute_pose(double R[3][3], double t[3]) {
+    __device__ __forceinline__ double compute_pose(double R[3][3], double t[3]) {
         choose_control_points();
         barycentric();
         double m[144], d[12], ut[144], vt[144];

@@ -15,6 +15,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "epnp.hpp"
@@ -25,13 +27,13 @@ struct IdxPts {
     const float* p3d;
     const float* p2d;
     const int* idx;
-    __device__ void pw(int k, double out[3]) const {
+    __device__ __forceinline__ void pw(int k, double out[3]) const {
         const int i = idx[k];
         out[0] = p3d[3 * i];
         out[1] = p3d[3 * i + 1];
         out[2] = p3d[3 * i + 2];
     }
-    __device__ void uv(int k, double& u, double& v) const {
+    __device__ __forceinline__ void uv(int k, double& u, double& v) const {
         const int i = idx[k];
         u = p2d[2 * i];
         v = p2d[2 * i + 1];
@@ -39,7 +41,7 @@ struct IdxPts {
 };
 
 // PnPsolver::CheckInliers (308-339): float/double mix kept expression by expression.
-__device__ inline int check_inliers(const PnPProbDev& P, const double R[3][3], const double t[3], uint32_t* mask) {
+__device__ __forceinline__ int check_inliers(const PnPProbDev& P, const double R[3][3], const double t[3], uint32_t* mask) {
     int n = 0;
     const int words = (P.N + 31) >> 5;
     for (int w = 0; w < words; w++) {
@@ -66,7 +68,7 @@ __device__ inline int check_inliers(const PnPProbDev& P, const double R[3][3], c
     return n;
 }
 
-__device__ inline void store_rt(double* out, const double R[3][3], const double t[3]) {
+__device__ __forceinline__ void store_rt(double* out, const double R[3][3], const double t[3]) {
     for (int i = 0; i < 3; i++) {
         for (int j = 0; j < 3; j++) out[3 * i + j] = R[i][j];
         out[9 + i] = t[i];
@@ -77,6 +79,13 @@ __global__ void __launch_bounds__(64) k_pnp_hypotheses(const PnPProbDev* __restr
     const PnPProbDev P = probs[blockIdx.y];
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= P.nhyp) return;
+    for (int k = 0; k < P.minSet; k++) {
+        const int i = P.hyp_idx[(size_t)h * P.minSet + k];
+        if (i < 0 || i >= P.N) {  // never expected: host draws from [0, N)
+            P.counts[h] = -1;
+            return;
+        }
+    }
     IdxPts pts{P.p3d, P.p2d, P.hyp_idx + (size_t)h * P.minSet};
     epnp::Solver<IdxPts> S(pts, P.minSet, P.fu, P.fv, P.uc, P.vc);
     double R[3][3], t[3];
@@ -264,12 +273,12 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
         J.mask_off = dev; dev += al((size_t)J.K * words * 4);
         J.cnt_off = dev; dev += al((size_t)J.K * 4);
         J.rt_off = dev; dev += al((size_t)J.K * 12 * 8);
-        host = std::max(host, (size_t)J.K * (P.minSet_ * 4 + words * 4 + 4 + 96));
+        host = std::max(host, al((size_t)J.K * 4) + al((size_t)J.K * words * 4) + al((size_t)J.K * 96));
         if (int e = P.upload(s)) return e;
     }
     // refine scratch (per solver): idx list N + mask + rt + count
     size_t ref_base = dev;
-    for (int k = 0; k < n; k++) dev += al((size_t)S[k]->N_ * 4 + ((S[k]->N_ + 31) / 32) * 4 + 12 * 8 + 16);
+    for (int k = 0; k < n; k++) dev += al((size_t)S[k]->N_ * 4) + al((size_t)((S[k]->N_ + 31) / 32) * 4) + 96 + 256;
     if (int e = ensure(dev + 256, (host + 256) * n + 1024, (size_t)n)) return e;
     char* D = (char*)d_work_;
     char* Hh = (char*)h_work_;
@@ -310,6 +319,26 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
         q.masks = (uint32_t*)(D + J.mask_off);
         q.rt = (double*)(D + J.rt_off);
         maxK = std::max(maxK, J.K);
+    }
+    if (getenv("ORBGPU_CHECK_PTRS")) {
+        auto in = [](const void* p, size_t bytes) {
+            void* base = nullptr;
+            size_t size = 0;
+            if (hipMemGetAddressRange((hipDeviceptr_t*)&base, &size, (hipDeviceptr_t)p) != hipSuccess) return false;
+            return (const char*)p >= (const char*)base && (const char*)p + bytes <= (const char*)base + size;
+        };
+        for (int k = 0; k < n; k++) {
+            const PnPProbDev& q = pd[k];
+            if (!jobs[k].active) continue;
+            const int words = (q.N + 31) >> 5;
+            const bool ok = in(q.p3d, q.N * 12) && in(q.p2d, q.N * 8) && in(q.maxErr, q.N * 4) &&
+                            in(q.hyp_idx, (size_t)q.nhyp * q.minSet * 4) && in(q.counts, (size_t)q.nhyp * 4) &&
+                            in(q.masks, (size_t)q.nhyp * words * 4) && in(q.rt, (size_t)q.nhyp * 96) &&
+                            in(d_probs_, sizeof(PnPProbDev) * n);
+            fprintf(stderr, "[pnp] k=%d N=%d nhyp=%d minSet=%d ptrs %s p3d=%p hyp=%p work=%p cap=%zu\n", k, q.N, q.nhyp,
+                    q.minSet, ok ? "ok" : "BAD", (const void*)q.p3d, (const void*)q.hyp_idx, d_work_, work_cap_);
+            if (!ok) return -1;
+        }
     }
     ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(PnPProbDev) * n, hipMemcpyHostToDevice, s));
     if (maxK > 0)
