@@ -99,6 +99,13 @@ def lib():
     L.PnPsolver_iterate.argtypes = [vp, i32, vp, P(i32), vp, P(i32), vp, P(i32)]
     L.PnPsolver_iterate_batch.argtypes = [i32, vp, i32, vp, vp, vp, vp, vp, vp]
     L.PnPsolver_get_state.argtypes = [vp, P(i32), P(i32), P(i32)]
+    L.Sim3Solver_create.argtypes = [i32, vp, vp, vp, vp, vp, i32, vp, vp, i32, P(vp)]
+    L.Sim3Solver_destroy.argtypes = [vp]
+    L.Sim3Solver_set_ransac.argtypes = [vp, C.c_double, i32, i32]
+    L.Sim3Solver_iterate.argtypes = [vp, i32, vp, P(i32), vp, P(i32), vp, P(i32)]
+    L.Sim3Solver_iterate_batch.argtypes = [i32, vp, i32, vp, vp, vp, vp, vp, vp]
+    L.Sim3Solver_get_estimate.argtypes = [vp, vp, vp, vp]
+    L.Sim3Solver_get_state.argtypes = [vp, P(i32), P(i32), P(i32)]
     _lib = L
     return L
 

@@ -1,0 +1,479 @@
+// sim3.hip -- gfx950 Sim3 RANSAC: the device side of Sim3Solver::iterate
+// (reference src/Sim3Solver.cc:140-403).
+//
+// Each hypothesis (3 pairs drawn with rand(), Sim3Solver.cc:165-177) runs
+// Horn's closed form (centroids, M, N, Jacobi eigenvector of the 4x4 N,
+// angle-axis, Rodrigues, scale, t, T12/T21) and the bidirectional reprojection
+// test over all N pairs in one thread; every hypothesis of every solver of the
+// batch is one launch.  The draws do not depend on results, so the host
+// replays the `>=` best update and the `> minInliers` early return and
+// advances the RNG by exactly 3 draws per consumed iteration.
+#include "sim3.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "detmath.hpp"
+
+namespace orbgpu {
+
+// cv::eigen for a symmetric 4x4 CV_32F matrix: OpenCV 3.2 JacobiImpl_<float> (hypot as sqrtf).
+__device__ __forceinline__ void jacobi_eigen4(float* A, float* W, float* V) {
+    const int n = 4;
+    const float eps = 1.1920928955078125e-07f;
+    int i, j, k, m;
+    int indR[4], indC[4];
+    float mv = 0;
+    for (i = 0; i < n; i++) {
+        for (j = 0; j < n; j++) V[i * n + j] = 0;
+        V[i * n + i] = 1;
+    }
+    for (k = 0; k < n; k++) {
+        W[k] = A[(n + 1) * k];
+        if (k < n - 1) {
+            for (m = k + 1, mv = fabsf(A[n * k + m]), i = k + 2; i < n; i++) {
+                const float val = fabsf(A[n * k + i]);
+                if (mv < val) mv = val, m = i;
+            }
+            indR[k] = m;
+        }
+        if (k > 0) {
+            for (m = 0, mv = fabsf(A[k]), i = 1; i < k; i++) {
+                const float val = fabsf(A[n * i + k]);
+                if (mv < val) mv = val, m = i;
+            }
+            indC[k] = m;
+        }
+    }
+    for (int iters = 0; iters < n * n * 30; iters++) {
+        for (k = 0, mv = fabsf(A[indR[0]]), i = 1; i < n - 1; i++) {
+            const float val = fabsf(A[n * i + indR[i]]);
+            if (mv < val) mv = val, k = i;
+        }
+        int l = indR[k];
+        for (i = 1; i < n; i++) {
+            const float val = fabsf(A[n * indC[i] + i]);
+            if (mv < val) mv = val, k = indC[i], l = i;
+        }
+        const float p = A[n * k + l];
+        if (fabsf(p) <= eps) break;
+        const float y = (float)((W[l] - W[k]) * 0.5);
+        float t = fabsf(y) + sqrtf(p * p + y * y);
+        float s = sqrtf(p * p + t * t);
+        const float c = t / s;
+        s = p / s;
+        t = (p / t) * p;
+        if (y < 0) s = -s, t = -t;
+        A[n * k + l] = 0;
+        W[k] -= t;
+        W[l] += t;
+        float a0, b0;
+#define ROT(v0, v1) a0 = v0, b0 = v1, v0 = a0 * c - b0 * s, v1 = a0 * s + b0 * c
+        for (i = 0; i < k; i++) ROT(A[n * i + k], A[n * i + l]);
+        for (i = k + 1; i < l; i++) ROT(A[n * k + i], A[n * i + l]);
+        for (i = l + 1; i < n; i++) ROT(A[n * k + i], A[n * l + i]);
+        for (i = 0; i < n; i++) ROT(V[n * k + i], V[n * l + i]);
+#undef ROT
+        for (j = 0; j < 2; j++) {
+            const int idx = j == 0 ? k : l;
+            if (idx < n - 1) {
+                for (m = idx + 1, mv = fabsf(A[n * idx + m]), i = idx + 2; i < n; i++) {
+                    const float val = fabsf(A[n * idx + i]);
+                    if (mv < val) mv = val, m = i;
+                }
+                indR[idx] = m;
+            }
+            if (idx > 0) {
+                for (m = 0, mv = fabsf(A[idx]), i = 1; i < idx; i++) {
+                    const float val = fabsf(A[n * i + idx]);
+                    if (mv < val) mv = val, m = i;
+                }
+                indC[idx] = m;
+            }
+        }
+    }
+    for (k = 0; k < n - 1; k++) {
+        m = k;
+        for (i = k + 1; i < n; i++)
+            if (W[m] < W[i]) m = i;
+        if (k != m) {
+            const float tw = W[m]; W[m] = W[k]; W[k] = tw;
+            for (i = 0; i < n; i++) { const float tv = V[n * m + i]; V[n * m + i] = V[n * k + i]; V[n * k + i] = tv; }
+        }
+    }
+}
+
+// ComputeSim3 (226-337); P1/P2 [row][col], column i = point i.  est: R9 t3 s T12[16] T21[16]
+__device__ __forceinline__ void compute_sim3(const float P1[3][3], const float P2[3][3], int bFixScale, float* R,
+                                             float* t, float* s_out, float* T12, float* T21) {
+    float O1[3], O2[3], Pr1[3][3], Pr2[3][3];
+    for (int r = 0; r < 3; r++) {
+        O1[r] = (P1[r][0] + P1[r][1]) + P1[r][2];
+        O2[r] = (P2[r][0] + P2[r][1]) + P2[r][2];
+        O1[r] = O1[r] * (float)(1.0 / 3);
+        O2[r] = O2[r] * (float)(1.0 / 3);
+        for (int c = 0; c < 3; c++) {
+            Pr1[r][c] = P1[r][c] - O1[r];
+            Pr2[r][c] = P2[r][c] - O2[r];
+        }
+    }
+    float M[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            M[i][j] = (float)((double)Pr2[i][0] * Pr1[j][0] + (double)Pr2[i][1] * Pr1[j][1] + (double)Pr2[i][2] * Pr1[j][2]);
+    const double N11 = M[0][0] + M[1][1] + M[2][2];
+    const double N12 = M[1][2] - M[2][1];
+    const double N13 = M[2][0] - M[0][2];
+    const double N14 = M[0][1] - M[1][0];
+    const double N22 = M[0][0] - M[1][1] - M[2][2];
+    const double N23 = M[0][1] + M[1][0];
+    const double N24 = M[2][0] + M[0][2];
+    const double N33 = -M[0][0] + M[1][1] - M[2][2];
+    const double N34 = M[1][2] + M[2][1];
+    const double N44 = -M[0][0] - M[1][1] + M[2][2];
+    float N[16] = {(float)N11, (float)N12, (float)N13, (float)N14, (float)N12, (float)N22, (float)N23, (float)N24,
+                   (float)N13, (float)N23, (float)N33, (float)N34, (float)N14, (float)N24, (float)N34, (float)N44};
+    float eval[4], evec[16];
+    jacobi_eigen4(N, eval, evec);
+    float vec[3] = {evec[1], evec[2], evec[3]};
+    const double nv = sqrt((double)vec[0] * vec[0] + (double)vec[1] * vec[1] + (double)vec[2] * vec[2]);
+    const double ang = detmath::atan2_d(nv, evec[0]);
+    const double f = 2 * ang / nv;
+    for (int i = 0; i < 3; i++) vec[i] = (float)(vec[i] * f);
+    {  // cv::Rodrigues
+        double rx = vec[0], ry = vec[1], rz = vec[2];
+        const double theta = sqrt(rx * rx + ry * ry + rz * rz);
+        if (theta < 2.220446049250313e-16) {
+            for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.f : 0.f;
+        } else {
+            double sn, cs;
+            detmath::sincos_d(theta, &sn, &cs);
+            const double c1 = 1. - cs;
+            const double itheta = theta ? 1. / theta : 0.;
+            rx *= itheta; ry *= itheta; rz *= itheta;
+            const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+            const double r_x[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+            for (int i = 0; i < 9; i++) R[i] = (float)(cs * ((i % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[i] + sn * r_x[i]);
+        }
+    }
+    float P3[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            P3[i][j] = (float)((double)R[3 * i] * Pr2[0][j] + (double)R[3 * i + 1] * Pr2[1][j] + (double)R[3 * i + 2] * Pr2[2][j]);
+    float s;
+    if (!bFixScale) {
+        double nom = 0, den = 0;
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                nom += (double)Pr1[i][j] * P3[i][j];
+                den += (float)(P3[i][j] * P3[i][j]);
+            }
+        s = (float)(nom / den);
+    } else {
+        s = 1.0f;
+    }
+    *s_out = s;
+    for (int i = 0; i < 3; i++) {
+        const double rO2 = (double)R[3 * i] * O2[0] + (double)R[3 * i + 1] * O2[1] + (double)R[3 * i + 2] * O2[2];
+        t[i] = O1[i] - (float)(s * rO2);
+    }
+    for (int i = 0; i < 16; i++) T12[i] = T21[i] = 0.f;
+    T12[15] = T21[15] = 1.f;
+    float sRinv[9];
+    const double is = 1.0 / s;
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) {
+            T12[4 * i + j] = (float)(s * (double)R[3 * i + j]);
+            sRinv[3 * i + j] = (float)(is * (double)R[3 * j + i]);
+            T21[4 * i + j] = sRinv[3 * i + j];
+        }
+        T12[4 * i + 3] = t[i];
+    }
+    for (int i = 0; i < 3; i++) {
+        const double v = (double)sRinv[3 * i] * t[0] + (double)sRinv[3 * i + 1] * t[1] + (double)sRinv[3 * i + 2] * t[2];
+        T21[4 * i + 3] = (float)(-v);
+    }
+}
+
+__device__ __forceinline__ void project(const float* X, const float* T, const float* K, float* uv) {
+    float p[3];
+    for (int r = 0; r < 3; r++)
+        p[r] = (float)((double)T[4 * r] * X[0] + (double)T[4 * r + 1] * X[1] + (double)T[4 * r + 2] * X[2] + (double)T[4 * r + 3]);
+    const float invz = 1 / p[2];
+    const float x = p[0] * invz, y = p[1] * invz;
+    uv[0] = K[0] * x + K[2];
+    uv[1] = K[1] * y + K[3];
+}
+
+__global__ void __launch_bounds__(64) k_sim3_hypotheses(const Sim3ProbDev* __restrict__ probs) {
+    const Sim3ProbDev P = probs[blockIdx.y];
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= P.nhyp) return;
+    float P1[3][3], P2[3][3];
+    for (int i = 0; i < 3; i++) {
+        const int idx = P.hyp_idx[3 * h + i];
+        for (int r = 0; r < 3; r++) {
+            P1[r][i] = P.X1[3 * idx + r];
+            P2[r][i] = P.X2[3 * idx + r];
+        }
+    }
+    float R[9], t[3], s, T12[16], T21[16];
+    compute_sim3(P1, P2, P.bFixScale, R, t, &s, T12, T21);
+    // CheckInliers (340-364)
+    const int words = (P.N + 31) >> 5;
+    uint32_t* mask = P.masks + (size_t)h * words;
+    int n = 0;
+    for (int w = 0; w < words; w++) {
+        uint32_t bits = 0;
+        for (int b = 0; b < 32; b++) {
+            const int i = w * 32 + b;
+            if (i >= P.N) break;
+            float p2im1[2], p1im2[2];
+            project(P.X2 + 3 * i, T12, P.K1, p2im1);
+            project(P.X1 + 3 * i, T21, P.K2, p1im2);
+            const float d1x = P.p1[2 * i] - p2im1[0], d1y = P.p1[2 * i + 1] - p2im1[1];
+            const float d2x = p1im2[0] - P.p2[2 * i], d2y = p1im2[1] - P.p2[2 * i + 1];
+            const float err1 = (float)((double)d1x * d1x + (double)d1y * d1y);
+            const float err2 = (float)((double)d2x * d2x + (double)d2y * d2y);
+            if (err1 < P.maxErr1[i] && err2 < P.maxErr2[i]) {
+                bits |= 1u << b;
+                n++;
+            }
+        }
+        mask[w] = bits;
+    }
+    P.counts[h] = n;
+    float* e = P.est + (size_t)h * 32;
+    for (int i = 0; i < 9; i++) e[i] = R[i];
+    for (int i = 0; i < 3; i++) e[9 + i] = t[i];
+    e[12] = s;
+    for (int i = 0; i < 16; i++) e[16 + i] = T12[i];
+}
+
+// ----------------------------------------------------------------------- host
+static int random_int3(orb_rng* g, int min, int max) {
+    const int d = max - min + 1;
+    return int(((double)rng_rand(g) / ((double)2147483647 + 1.0)) * d) + min;
+}
+
+Sim3Solver::Sim3Solver(int N, const float* X1c, const float* X2c, const float* s1, const float* s2, const int* idx1,
+                       int N1, const float* K1, const float* K2, bool bFixScale)
+    : N_(N), N1_(N1), bFixScale_(bFixScale) {
+    X1_.assign(X1c, X1c + 3 * (size_t)N);
+    X2_.assign(X2c, X2c + 3 * (size_t)N);
+    idx1_.assign(idx1, idx1 + N);
+    std::memcpy(K1_, K1, 16);
+    std::memcpy(K2_, K2, 16);
+    p1_.resize(2 * (size_t)N);
+    p2_.resize(2 * (size_t)N);
+    maxErr1_.resize(N);
+    maxErr2_.resize(N);
+    for (int i = 0; i < N; i++) {
+        // mvnMaxError are vector<size_t> (Sim3Solver.h:78-79): truncated, compared as float
+        maxErr1_[i] = (float)(size_t)(9.210 * s1[i]);
+        maxErr2_[i] = (float)(size_t)(9.210 * s2[i]);
+        for (int k = 0; k < 2; k++) {  // FromCameraToImage (405-423)
+            const float* X = k ? &X2_[3 * i] : &X1_[3 * i];
+            const float* K = k ? K2_ : K1_;
+            float* out = k ? &p2_[2 * i] : &p1_[2 * i];
+            const float invz = 1 / X[2];
+            const float x = X[0] * invz, y = X[1] * invz;
+            out[0] = K[0] * x + K[2];
+            out[1] = K[1] * y + K[3];
+        }
+    }
+    bestInliers_.assign(N, 0);
+    set_ransac(0.99, 6, 300);  // Sim3Solver.h:45 defaults, called by the ctor
+}
+
+Sim3Solver::~Sim3Solver() {
+    if (d_pts_) (void)hipFree(d_pts_);
+}
+
+// SetRansacParameters (114-138)
+void Sim3Solver::set_ransac(double probability, int minInliers, int maxIterations) {
+    prob_ = probability;
+    minInliers_ = minInliers;
+    maxIts_ = maxIterations;
+    const float epsilon = (float)minInliers_ / N_;
+    int nIterations;
+    if (minInliers_ == N_) nIterations = 1;
+    else nIterations = (int)std::ceil(std::log(1 - prob_) / std::log(1 - std::pow(epsilon, 3)));
+    maxIts_ = std::max(1, std::min(nIterations, maxIts_));
+    nIterations_ = 0;
+}
+
+int Sim3Solver::upload(hipStream_t s) {
+    if (!dirty_) return 0;
+    const size_t bytes = (size_t)N_ * 12 * 4 + 64;
+    if (bytes > d_cap_) {
+        if (d_pts_) (void)hipFree(d_pts_);
+        ORB_HIP_CHECK(hipMalloc(&d_pts_, bytes));
+        d_cap_ = bytes;
+    }
+    float* d = (float*)d_pts_;
+    ORB_HIP_CHECK(hipMemcpyAsync(d, X1_.data(), (size_t)N_ * 12, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(d + 3 * N_, X2_.data(), (size_t)N_ * 12, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(d + 6 * N_, p1_.data(), (size_t)N_ * 8, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(d + 8 * N_, p2_.data(), (size_t)N_ * 8, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(d + 10 * N_, maxErr1_.data(), (size_t)N_ * 4, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(d + 11 * N_, maxErr2_.data(), (size_t)N_ * 4, hipMemcpyHostToDevice, s));
+    dirty_ = false;
+    return 0;
+}
+
+Sim3Batch::~Sim3Batch() {
+    if (d_work_) (void)hipFree(d_work_);
+    if (d_probs_) (void)hipFree(d_probs_);
+    if (h_work_) (void)hipHostFree(h_work_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+int Sim3Batch::init() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
+    ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    return 0;
+}
+
+int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, Sim3Result* res) {
+    hipStream_t s = stream_;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    std::vector<int> K(n, 0);
+    std::vector<size_t> hyp_off(n), cnt_off(n), mask_off(n), est_off(n), hoff(n);
+    std::vector<orb_rng> snap(n);
+    size_t dev = 0, host = 0;
+    for (int k = 0; k < n; k++) {
+        Sim3Solver& P = *S[k];
+        Sim3Result& r = res[k];
+        r.has_pose = 0;
+        r.bNoMore = 0;
+        r.nInliers = 0;
+        if (r.inliers) std::fill(r.inliers, r.inliers + P.N1_, 0);  // vbInliers = vector<bool>(mN1,false)
+        if (P.N_ < P.minInliers_) {
+            r.bNoMore = 1;
+            continue;
+        }
+        // `while (mnIterations < max && nCurrent < nIterations)`
+        K[k] = std::max(0, std::min(P.maxIts_ - P.nIterations_, nIterations));
+        snap[k] = *rngs[k];
+        const int words = (P.N_ + 31) >> 5;
+        hyp_off[k] = dev; dev += al((size_t)K[k] * 12);
+        cnt_off[k] = dev; dev += al((size_t)K[k] * 4);
+        mask_off[k] = dev; dev += al((size_t)K[k] * words * 4);
+        est_off[k] = dev; dev += al((size_t)K[k] * 128);
+        hoff[k] = host;
+        host += al((size_t)K[k] * 4) + al((size_t)K[k] * words * 4) + al((size_t)K[k] * 128);
+        if (int e = P.upload(s)) return e;
+    }
+    if (dev + 256 > work_cap_) {
+        if (d_work_) (void)hipFree(d_work_);
+        ORB_HIP_CHECK(hipMalloc(&d_work_, dev + 256));
+        work_cap_ = dev + 256;
+    }
+    if (host + 256 > hwork_cap_) {
+        if (h_work_) (void)hipHostFree(h_work_);
+        ORB_HIP_CHECK(hipHostMalloc(&h_work_, host + 256));
+        hwork_cap_ = host + 256;
+    }
+    if (sizeof(Sim3ProbDev) * n > probs_cap_) {
+        if (d_probs_) (void)hipFree(d_probs_);
+        ORB_HIP_CHECK(hipMalloc(&d_probs_, sizeof(Sim3ProbDev) * n + 16));
+        probs_cap_ = sizeof(Sim3ProbDev) * n;
+    }
+    char* D = (char*)d_work_;
+    char* Hh = (char*)h_work_;
+    std::vector<Sim3ProbDev> pd(n);
+    std::vector<std::vector<int>> hyps(n);
+    int maxK = 0;
+    for (int k = 0; k < n; k++) {
+        std::memset(&pd[k], 0, sizeof(Sim3ProbDev));
+        if (K[k] <= 0) continue;
+        Sim3Solver& P = *S[k];
+        orb_rng g = snap[k];
+        std::vector<int>& hyp = hyps[k];
+        hyp.assign((size_t)K[k] * 3, 0);
+        std::vector<int> avail(P.N_);
+        for (int h = 0; h < K[k]; h++) {
+            for (int i = 0; i < P.N_; i++) avail[i] = i;
+            int navail = P.N_;
+            for (int i = 0; i < 3; ++i) {
+                const int randi = random_int3(&g, 0, navail - 1);
+                hyp[3 * h + i] = avail[randi];
+                avail[randi] = avail[navail - 1];
+                navail--;
+            }
+        }
+        ORB_HIP_CHECK(hipMemcpyAsync(D + hyp_off[k], hyp.data(), hyp.size() * 4, hipMemcpyHostToDevice, s));
+        const float* d = (const float*)P.d_pts_;
+        Sim3ProbDev& q = pd[k];
+        q.X1 = d; q.X2 = d + 3 * P.N_; q.p1 = d + 6 * P.N_; q.p2 = d + 8 * P.N_;
+        q.maxErr1 = d + 10 * P.N_; q.maxErr2 = d + 11 * P.N_;
+        q.N = P.N_;
+        q.bFixScale = P.bFixScale_ ? 1 : 0;
+        std::memcpy(q.K1, P.K1_, 16);
+        std::memcpy(q.K2, P.K2_, 16);
+        q.hyp_idx = (const int*)(D + hyp_off[k]);
+        q.nhyp = K[k];
+        q.counts = (int*)(D + cnt_off[k]);
+        q.masks = (uint32_t*)(D + mask_off[k]);
+        q.est = (float*)(D + est_off[k]);
+        maxK = std::max(maxK, K[k]);
+    }
+    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(Sim3ProbDev) * n, hipMemcpyHostToDevice, s));
+    if (maxK > 0)
+        hipLaunchKernelGGL(k_sim3_hypotheses, dim3((maxK + 63) / 64, n), dim3(64), 0, s, (const Sim3ProbDev*)d_probs_);
+    ORB_HIP_CHECK(hipGetLastError());
+    for (int k = 0; k < n; k++) {
+        if (K[k] <= 0) continue;
+        const int words = (S[k]->N_ + 31) >> 5;
+        char* h = Hh + hoff[k];
+        ORB_HIP_CHECK(hipMemcpyAsync(h, D + cnt_off[k], (size_t)K[k] * 4, hipMemcpyDeviceToHost, s));
+        ORB_HIP_CHECK(hipMemcpyAsync(h + al((size_t)K[k] * 4), D + mask_off[k], (size_t)K[k] * words * 4,
+                                     hipMemcpyDeviceToHost, s));
+        ORB_HIP_CHECK(hipMemcpyAsync(h + al((size_t)K[k] * 4) + al((size_t)K[k] * words * 4), D + est_off[k],
+                                     (size_t)K[k] * 128, hipMemcpyDeviceToHost, s));
+    }
+    ORB_HIP_CHECK(hipStreamSynchronize(s));
+    // sequential replay (Sim3Solver.cc:158-206)
+    for (int k = 0; k < n; k++) {
+        Sim3Solver& P = *S[k];
+        Sim3Result& r = res[k];
+        if (P.N_ < P.minInliers_) continue;
+        const int words = (P.N_ + 31) >> 5;
+        const char* h = Hh + hoff[k];
+        const int* cnt = (const int*)h;
+        const uint32_t* masks = (const uint32_t*)(h + al((size_t)K[k] * 4));
+        const float* est = (const float*)(h + al((size_t)K[k] * 4) + al((size_t)K[k] * words * 4));
+        int consumed = K[k];
+        for (int hh = 0; hh < K[k]; hh++) {
+            P.nIterations_++;
+            const int c = cnt[hh];
+            if (c >= P.nBestInliers_) {
+                for (int i = 0; i < P.N_; i++) P.bestInliers_[i] = (masks[(size_t)hh * words + (i >> 5)] >> (i & 31)) & 1;
+                P.nBestInliers_ = c;
+                const float* e = est + (size_t)hh * 32;
+                std::memcpy(P.bestR_, e, 36);
+                std::memcpy(P.bestT_, e + 9, 12);
+                P.bestS_ = e[12];
+                std::memcpy(P.bestT12_, e + 16, 64);
+                if (c > P.minInliers_) {
+                    r.has_pose = 1;
+                    r.nInliers = c;
+                    for (int i = 0; i < P.N_; i++)
+                        if (P.bestInliers_[i]) r.inliers[P.idx1_[i]] = 1;
+                    std::memcpy(r.T12, P.bestT12_, 64);
+                    consumed = hh + 1;
+                    break;
+                }
+            }
+        }
+        *rngs[k] = snap[k];
+        for (int d = 0; d < consumed * 3; d++) (void)rng_rand(rngs[k]);
+        if (!r.has_pose && P.nIterations_ >= P.maxIts_) r.bNoMore = 1;
+    }
+    return 0;
+}
+
+}  // namespace orbgpu

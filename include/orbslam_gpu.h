@@ -223,6 +223,39 @@ int PnPsolver_iterate_batch(int count, PnPsolver_h* hs, int nIterations, orb_rng
 /* RANSAC bookkeeping (mnIterations, mRansacMaxIts, mRansacMinInliers) */
 int PnPsolver_get_state(PnPsolver_h h, int* iterations, int* max_its, int* min_inliers);
 
+/* ======================================================================
+ * Sim3Solver  (reference include/Sim3Solver.h:39-137, src/Sim3Solver.cc)
+ * ====================================================================== */
+typedef struct Sim3Solver_t* Sim3Solver_h;
+
+/* Sim3Solver(pKF1, pKF2, vpMatched12, bFixScale)  Sim3Solver.cc:37-112
+ * The adapter packs the N valid pairs in vpMatched12 order: X1c/X2c (N x 3,
+ * Rcw*Xw+tcw of each keyframe = mvX3Dc1/2), sigma2_1/2 (N, mvLevelSigma2[octave]),
+ * idx1 (N, mvnIndices1) into vpMatched12 of size N1; K1/K2 = {fx, fy, cx, cy}.
+ * SetRansacParameters() defaults (0.99, 6, 300) are applied as in the reference
+ * ctor. N must be >= 3 (the reference's loop-closing caller guarantees >= 20). */
+int Sim3Solver_create(int N, const float* X1c, const float* X2c, const float* sigma2_1,
+                      const float* sigma2_2, const int32_t* idx1, int N1, const float* K1,
+                      const float* K2, int bFixScale, Sim3Solver_h* out);
+int Sim3Solver_destroy(Sim3Solver_h h);
+/* SetRansacParameters(probability, minInliers, maxIterations)  114-138 */
+int Sim3Solver_set_ransac(Sim3Solver_h h, double probability, int minInliers, int maxIterations);
+/* cv::Mat iterate(nIterations, bNoMore, vbInliers, nInliers)  140-207
+ * inliers: N1 bytes; T12: 16 floats (row-major 4x4 sim3 [sR t; 0 1]);
+ * *has_pose = 0 where the reference returns an empty cv::Mat. */
+int Sim3Solver_iterate(Sim3Solver_h h, int nIterations, orb_rng* rng, int* bNoMore,
+                       uint8_t* inliers, int* nInliers, float* T12, int* has_pose);
+/* `count` independent solvers in one hypothesis launch (LoopClosing::ComputeSim3
+ * runs one per loop candidate); same conventions as PnPsolver_iterate_batch. */
+int Sim3Solver_iterate_batch(int count, Sim3Solver_h* hs, int nIterations, orb_rng** rngs,
+                             int* bNoMore, uint8_t** inliers, int* nInliers, float* T12,
+                             int* has_pose);
+/* GetEstimatedRotation / GetEstimatedTranslation / GetEstimatedScale  366-379:
+ * R (9, row-major), t (3), s of the best hypothesis so far. */
+int Sim3Solver_get_estimate(Sim3Solver_h h, float* R, float* t, float* s);
+/* (mnIterations, mRansacMaxIts, mRansacMinInliers) */
+int Sim3Solver_get_state(Sim3Solver_h h, int* iterations, int* max_its, int* min_inliers);
+
 #ifdef __cplusplus
 }
 #endif

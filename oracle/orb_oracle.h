@@ -161,6 +161,21 @@ int   ora_pnp_iterations(const ora_pnp* P);
 int   ora_pnp_max_its(const ora_pnp* P);
 int   ora_pnp_min_inliers(const ora_pnp* P);
 
+
+/* ---- Sim3Solver (sim3.c), reference src/Sim3Solver.cc --------------------- */
+typedef struct ora_sim3 ora_sim3;
+void  ora_det_sincos(double x, double* s, double* c);
+double ora_det_atan2(double y, double x);
+void  ora_jacobi_eigen_f(float* A, int n, float* W, float* V);
+ora_sim3* ora_sim3_new(int N, const float* X1c, const float* X2c, const float* sigma2_1, const float* sigma2_2,
+                       const int* idx1, int N1, const float* K1, const float* K2, int bFixScale);
+void  ora_sim3_free(ora_sim3* S);
+void  ora_sim3_set_ransac(ora_sim3* S, double probability, int minInliers, int maxIterations);
+int   ora_sim3_iterate(ora_sim3* S, int nIterations, ora_rng* rng, int* bNoMore, uint8_t* inliers, int* nInliers,
+                       float* T12);
+void  ora_sim3_estimate(const ora_sim3* S, float* R, float* t, float* s);
+int   ora_sim3_iterations(const ora_sim3* S);
+
 #ifdef __cplusplus
 }
 #endif

@@ -259,6 +259,53 @@ class OraclePnP:
         return self.L.ora_pnp_iterations(self.h)
 
 
+class OracleSim3:
+    """Sim3Solver(pKF1, pKF2, vpMatched12, bFixScale) restated on CPU (reference src/Sim3Solver.cc)."""
+
+    def __init__(self, X1c, X2c, s1, s2, idx1, N1, K1, K2, bFixScale=True):
+        L = lib()
+        L.ora_sim3_new.restype = C.c_void_p
+        L.ora_sim3_new.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                   C.c_void_p, C.c_void_p, C.c_int]
+        L.ora_sim3_free.argtypes = [C.c_void_p]
+        L.ora_sim3_set_ransac.argtypes = [C.c_void_p, C.c_double, C.c_int, C.c_int]
+        L.ora_sim3_iterate.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p]
+        L.ora_sim3_estimate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.ora_sim3_iterations.argtypes = [C.c_void_p]
+        self.L = L
+        self.arrs = [np.ascontiguousarray(a, t) for a, t in
+                     ((X1c, np.float32), (X2c, np.float32), (s1, np.float32), (s2, np.float32), (idx1, np.int32),
+                      (K1, np.float32), (K2, np.float32))]
+        X1, X2, a1, a2, ix, k1, k2 = self.arrs
+        self.n_matches = N1
+        self.h = L.ora_sim3_new(len(ix), ptr(X1), ptr(X2), ptr(a1), ptr(a2), ptr(ix), N1, ptr(k1), ptr(k2),
+                                int(bFixScale))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.ora_sim3_free(self.h)
+
+    def set_ransac(self, probability=0.99, minInliers=6, maxIterations=300):
+        self.L.ora_sim3_set_ransac(self.h, probability, minInliers, maxIterations)
+
+    def iterate(self, n_iterations, rng):
+        no_more, nin = C.c_int(), C.c_int()
+        inl = np.zeros(max(self.n_matches, 1), np.uint8)
+        T = np.zeros(16, np.float32)
+        ok = self.L.ora_sim3_iterate(self.h, n_iterations, rng, C.byref(no_more), ptr(inl), C.byref(nin), ptr(T))
+        return bool(ok), T.reshape(4, 4), inl[:self.n_matches].astype(bool), nin.value, bool(no_more.value)
+
+    def estimate(self):
+        R, t, s = np.zeros(9, np.float32), np.zeros(3, np.float32), np.zeros(1, np.float32)
+        self.L.ora_sim3_estimate(self.h, ptr(R), ptr(t), ptr(s))
+        return R.reshape(3, 3), t, float(s[0])
+
+    @property
+    def iterations(self):
+        return self.L.ora_sim3_iterations(self.h)
+
+
 def new_rng(seed=1):
     g = (C.c_int32 * 40)()
     lib().ora_rng_seed(g, seed)

@@ -47,3 +47,23 @@ def test_no_silent_cpu_fallback():
     assert ei.value.code == ORB_E_NODEVICE
     with pytest.raises(orb.OrbGpuError):
         orb.ORBmatcher(0.9, True)
+
+
+def test_ransac_solvers_validate_and_refuse_without_device():
+    L = lib()
+    h = C.c_void_p()
+    X = np.zeros((4, 3), np.float32)
+    s = np.ones(4, np.float32)
+    K = np.array([700, 700, 600, 180], np.float32)
+    idx = np.arange(4, dtype=np.int32)
+    # N < 3 and out-of-range idx1 are argument errors, checked before the device
+    assert L.Sim3Solver_create(2, ptr(X), ptr(X), ptr(s), ptr(s), ptr(idx), 4, ptr(K), ptr(K), 1,
+                               C.byref(h)) == ORB_E_INVALID
+    bad = np.array([0, 1, 2, 9], np.int32)
+    assert L.Sim3Solver_create(4, ptr(X), ptr(X), ptr(s), ptr(s), ptr(bad), 4, ptr(K), ptr(K), 1,
+                               C.byref(h)) == ORB_E_INVALID
+    assert L.Sim3Solver_destroy(None) == ORB_E_INVALID
+    assert L.PnPsolver_destroy(None) == ORB_E_INVALID
+    if not orb.device_available():
+        assert L.Sim3Solver_create(4, ptr(X), ptr(X), ptr(s), ptr(s), ptr(idx), 4, ptr(K), ptr(K), 1,
+                                   C.byref(h)) == ORB_E_NODEVICE

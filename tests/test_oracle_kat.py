@@ -207,3 +207,60 @@ def test_oracle_pnp_ransac_recovers_pose():
     P.set_ransac(0.99, 10, 300, 4, 0.5, 5.991)
     ok, T, inl, n, no_more = P.iterate(5, oracle_lib.new_rng(1))
     assert ok and n > 250 and np.abs(T - pr["Tcw"]).max() < 0.1
+
+
+# ---- Sim3 (oracle/sim3.c) ---------------------------------------------------
+def test_det_trig_close_to_libm():
+    """det_sincos/det_atan2 (shared bit-for-bit with the GPU) stay within 4 ulp of libm."""
+    import math
+    L = oracle_lib.lib()
+    L.ora_det_sincos.argtypes = [ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]
+    L.ora_det_atan2.argtypes = [ctypes.c_double, ctypes.c_double]
+    L.ora_det_atan2.restype = ctypes.c_double
+    rng = np.random.default_rng(0)
+    s, c = ctypes.c_double(), ctypes.c_double()
+    for x in np.concatenate([rng.uniform(0, 4 * np.pi, 2000), [0.0, 1e-9, np.pi / 4, np.pi / 2, np.pi]]):
+        L.ora_det_sincos(float(x), ctypes.byref(s), ctypes.byref(c))
+        assert abs(s.value - math.sin(x)) <= 2 * math.ulp(max(abs(math.sin(x)), 1e-300)) + 1e-17
+        assert abs(c.value - math.cos(x)) <= 2 * math.ulp(max(abs(math.cos(x)), 1e-300)) + 1e-17
+    for y, x in rng.normal(0, 3, (2000, 2)).tolist() + [(0.0, 1.0), (1.0, 0.0), (0.0, -1.0), (-1.0, -1.0)]:
+        a = math.atan2(y, x)
+        assert abs(L.ora_det_atan2(y, x) - a) <= 4 * math.ulp(abs(a)) + 1e-300
+
+
+def test_jacobi_eigen_symmetric():
+    L = oracle_lib.lib()
+    L.ora_jacobi_eigen_f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    rng = np.random.default_rng(1)
+    for _ in range(50):
+        B = rng.normal(size=(4, 4)).astype(np.float32)
+        A = (B + B.T).astype(np.float32)
+        W, V, A2 = np.zeros(4, np.float32), np.zeros(16, np.float32), A.copy()
+        L.ora_jacobi_eigen_f(A2.ctypes.data, 4, W.ctypes.data, V.ctypes.data)
+        w_ref = np.sort(np.linalg.eigvalsh(A.astype(np.float64)))[::-1]
+        np.testing.assert_allclose(W, w_ref, rtol=1e-4, atol=1e-4)
+        V = V.reshape(4, 4)
+        for i in range(4):   # rows are eigenvectors
+            np.testing.assert_allclose(A @ V[i], W[i] * V[i], atol=2e-4)
+
+
+@pytest.mark.parametrize("fix", [True, False])
+def test_sim3_oracle_recovers_similarity(fix):
+    from sim3_cases import sim3_problem
+    pr = sim3_problem(11, 120, fix_scale=fix)
+    o = oracle_lib.OracleSim3(pr["X1"], pr["X2"], pr["s1"], pr["s2"], pr["idx1"], pr["N1"], pr["K1"], pr["K2"],
+                              pr["fix"])
+    o.set_ransac(0.99, 20, 300)
+    rng = oracle_lib.new_rng(1)
+    for _ in range(60):
+        ok, T, inl, nin, nm = o.iterate(5, rng)
+        if ok or nm:
+            break
+    assert ok and nin > 20
+    np.testing.assert_allclose(T[:3, :3], pr["T12"][:3, :3], atol=0.05)
+    _, _, s = o.estimate()
+    assert abs(s - pr["s"]) < 0.05 * pr["s"]
+    mask = np.zeros(len(pr["X1"]), bool)
+    mask[pr["outliers"]] = True
+    flagged = inl[pr["idx1"]]
+    assert not np.any(flagged & mask), "an outlier accepted as inlier"
