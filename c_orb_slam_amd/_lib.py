@@ -99,6 +99,9 @@ def lib():
     L.PnPsolver_iterate.argtypes = [vp, i32, vp, P(i32), vp, P(i32), vp, P(i32)]
     L.PnPsolver_iterate_batch.argtypes = [i32, vp, i32, vp, vp, vp, vp, vp, vp]
     L.PnPsolver_get_state.argtypes = [vp, P(i32), P(i32), P(i32)]
+    L.Optimizer_LocalBundleAdjustment.argtypes = [vp, vp, vp]
+    L.Optimizer_last_trace.argtypes = [vp, vp, i32, P(i32), vp, vp, i32, P(i32)]
+    L.Optimizer_last_timings.argtypes = [vp]
     L.Sim3Solver_create.argtypes = [i32, vp, vp, vp, vp, vp, i32, vp, vp, i32, P(vp)]
     L.Sim3Solver_destroy.argtypes = [vp]
     L.Sim3Solver_set_ransac.argtypes = [vp, C.c_double, i32, i32]
@@ -120,3 +123,15 @@ def ptr(a):
 
 def device_available():
     return bool(lib().orbgpu_device_available())
+
+
+class ba_problem(C.Structure):
+    _fields_ = [("n_kf", C.c_int), ("kf_id", C.c_void_p), ("kf_Tcw", C.c_void_p), ("kf_local", C.c_void_p),
+                ("kf_cam", C.c_void_p), ("n_pt", C.c_int), ("pt_id", C.c_void_p), ("pt_pos", C.c_void_p),
+                ("n_edge", C.c_int), ("edge_pt", C.c_void_p), ("edge_kf", C.c_void_p), ("edge_obs", C.c_void_p),
+                ("edge_inv_sigma2", C.c_void_p)]
+
+
+class ba_result(C.Structure):
+    _fields_ = [("kf_Tcw", C.c_void_p), ("pt_pos", C.c_void_p), ("edge_erase", C.c_void_p),
+                ("iterations", C.c_int32 * 2), ("n_erased", C.c_int32), ("aborted", C.c_int32)]

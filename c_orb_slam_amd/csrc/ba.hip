@@ -1,0 +1,1125 @@
+// ba.hip -- gfx950 local bundle adjustment: Optimizer::LocalBundleAdjustment
+// (reference src/Optimizer.cc:453-778) on g2o's BlockSolver<6,3> +
+// OptimizationAlgorithmLevenberg (Thirdparty/g2o/g2o/core/*.cpp|hpp).
+//
+// Layout in HBM (FP64 inside, FP32 I/O like the reference):
+//   poses  Se3[n_kf] (q xyzw, t) + backup; points double[3][n_pt] + backup;
+//   edges  EdgeDev[n_edge] (static) + level/robust flags + last _error[3];
+//   per active edge: quadratic-form terms SoA (Hpp 21 | bp 6 | Hll 9 | bl 3),
+//   Hpl 6x3 AoS, BDinv 6x3 AoS, B*db 6; per pose Hpp/bp; per landmark Hll/bl/Dinv/db;
+//   dense Schur system S (6 nP)^2 (upper triangle used).
+// Kernels per LM solve():  k_linearize (edge ||) -> k_pose_reduce (workgroup per pose)
+//   + k_land_reduce (wave per landmark) -> [k_lambda_init] ; per trial:
+//   k_point_prep (thread per landmark) -> k_schur (workgroup per pose block)
+//   -> k_ldlt (one workgroup) -> k_update (thread per vertex) -> k_errors (edge ||)
+//   -> k_csum2 (canonical chi2 and computeScale) ; host reads 4 scalars, decides.
+// Every accumulation uses the canonical 64-wide tree order (oracle/ba.c ora_csum),
+// so results are bit-identical to the CPU restatement.
+#include "ba.hpp"
+
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+
+#include "detmath.hpp"
+#include "orb_common.hpp"
+
+namespace orbgpu {
+
+// ---------------------------------------------------------------- math (host + device)
+#define HD __host__ __device__ __forceinline__
+
+HD void quat_normalize(double* q) {
+    const double z = ((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3];
+    if (z > 0) {
+        const double n = sqrt(z);
+        for (int i = 0; i < 4; i++) q[i] = q[i] / n;
+    }
+}
+
+HD void se3_normalize(Se3& T) {
+    if (T.q[3] < 0)
+        for (int i = 0; i < 4; i++) T.q[i] *= -1;
+    quat_normalize(T.q);
+}
+
+HD void quat_from_R(const double* m, double* q) {
+    double t = (m[0] + m[4]) + m[8];
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[7] - m[5]) * t;
+        q[1] = (m[2] - m[6]) * t;
+        q[2] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[i * 4]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(((m[i * 4] - m[j * 4]) - m[k * 4]) + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * t;
+        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
+        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
+    }
+}
+
+HD void quat_to_R(const double* q, double* R) {
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;         R[2] = txz + twy;
+    R[3] = txy + twz;         R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.0 - (txx + tyy);
+}
+
+HD void cross3(const double* a, const double* b, double* c) {
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+HD void quat_rotate(const double* q, const double* v, double* out) {
+    double uv[3], c[3];
+    cross3(q, v, uv);
+    for (int i = 0; i < 3; i++) uv[i] += uv[i];
+    cross3(q, uv, c);
+    for (int i = 0; i < 3; i++) out[i] = (v[i] + q[3] * uv[i]) + c[i];
+}
+
+HD void se3_map(const Se3& T, const double* X, double* out) {
+    double r[3];
+    quat_rotate(T.q, X, r);
+    for (int i = 0; i < 3; i++) out[i] = r[i] + T.t[i];
+}
+
+HD void se3_mul(const Se3& a, const Se3& b, Se3& o) {
+    Se3 r{};
+    double rt[3];
+    quat_rotate(a.q, b.t, rt);
+    for (int i = 0; i < 3; i++) r.t[i] = a.t[i] + rt[i];
+    r.q[3] = ((a.q[3] * b.q[3] - a.q[0] * b.q[0]) - a.q[1] * b.q[1]) - a.q[2] * b.q[2];
+    r.q[0] = ((a.q[3] * b.q[0] + a.q[0] * b.q[3]) + a.q[1] * b.q[2]) - a.q[2] * b.q[1];
+    r.q[1] = ((a.q[3] * b.q[1] + a.q[1] * b.q[3]) + a.q[2] * b.q[0]) - a.q[0] * b.q[2];
+    r.q[2] = ((a.q[3] * b.q[2] + a.q[2] * b.q[3]) + a.q[0] * b.q[1]) - a.q[1] * b.q[0];
+    se3_normalize(r);
+    o = r;
+}
+
+__device__ __forceinline__ void se3_exp(const double* upd, Se3& out) {
+    const double* w = upd;
+    const double* u = upd + 3;
+    const double theta = sqrt((w[0] * w[0] + w[1] * w[1]) + w[2] * w[2]);
+    const double Om[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+    double Om2[9], R[9], V[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            Om2[i * 3 + j] = (Om[i * 3] * Om[j] + Om[i * 3 + 1] * Om[3 + j]) + Om[i * 3 + 2] * Om[6 + j];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) {
+            R[i] = (((i % 4) == 0 ? 1.0 : 0.0) + Om[i]) + Om2[i];
+            V[i] = R[i];
+        }
+    } else {
+        double s, c;
+        detmath::sincos_d(theta, &s, &c);
+        const double a = s / theta, b = (1 - c) / (theta * theta);
+        const double cc = (theta - s) / ((theta * theta) * theta);
+        for (int i = 0; i < 9; i++) {
+            const double I = (i % 4) == 0 ? 1.0 : 0.0;
+            R[i] = (I + a * Om[i]) + b * Om2[i];
+            V[i] = (I + b * Om[i]) + cc * Om2[i];
+        }
+    }
+    quat_from_R(R, out.q);
+    for (int i = 0; i < 3; i++) out.t[i] = (V[i * 3] * u[0] + V[i * 3 + 1] * u[1]) + V[i * 3 + 2] * u[2];
+    out.pad = 0;
+    se3_normalize(out);
+}
+
+// computeError (types_six_dof_expmap.h:94-99, 126-131; .cpp:141-157)
+__device__ __forceinline__ void edge_error(const EdgeDev& e, const Se3& T, const double* X, double* err) {
+    double p[3];
+    se3_map(T, X, p);
+    if (!e.stereo) {
+        const double px = p[0] / p[2], py = p[1] / p[2];
+        err[0] = e.obs[0] - (px * e.fx + e.cx);
+        err[1] = e.obs[1] - (py * e.fy + e.cy);
+        err[2] = 0;
+    } else {
+        const float invz = (float)(1.0 / p[2]);
+        const float bf = (float)e.bf;
+        const double u = (p[0] * (double)invz) * e.fx + e.cx;
+        const double v = (p[1] * (double)invz) * e.fy + e.cy;
+        err[0] = e.obs[0] - u;
+        err[1] = e.obs[1] - v;
+        err[2] = e.obs[2] - (u - (double)(bf * invz));
+    }
+}
+
+__device__ __forceinline__ double edge_chi2(const EdgeDev& e, const double* err) {
+    double s = 0;
+    const int D = e.stereo ? 3 : 2;
+    for (int j = 0; j < D; j++) s += err[j] * (e.info * err[j]);
+    return s;
+}
+
+__device__ __forceinline__ void huber(const EdgeDev& e, double chi, double* rho0, double* rho1) {
+    if (chi <= e.dsqr) {
+        *rho0 = chi;
+        *rho1 = 1.;
+    } else {
+        const double sq = sqrt(chi);
+        *rho0 = (2 * sq) * e.delta - e.dsqr;
+        *rho1 = e.delta / sq;
+    }
+}
+
+// ---------------------------------------------------------------- canonical reductions
+__device__ __forceinline__ double wave_tree(double v) {
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;
+}
+
+// Canonical sum (oracle ora_csum) of f(0..n) by one wave; sc: this wave's LDS scratch
+// (>= ceil(n/64) doubles).  Result broadcast to all lanes.
+template <class F>
+__device__ __forceinline__ double wave_csum(F f, int n, double* sc) {
+    const int lane = threadIdx.x & 63;
+    if (n <= 0) return 0.0;
+    if (n == 1) return f(0);  // ora_csum returns a single term untouched
+    int m = (n + 63) >> 6;
+    double v = 0;
+    for (int c = 0; c < m; c++) {
+        v = (c * 64 + lane < n) ? f(c * 64 + lane) : 0.0;
+        v = wave_tree(v);
+        if (m > 1 && lane == 0) sc[c] = v;
+    }
+    while (m > 1) {
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        const int m2 = (m + 63) >> 6;
+        for (int c = 0; c < m2; c++) {
+            double u = (c * 64 + lane < m) ? sc[c * 64 + lane] : 0.0;
+            u = wave_tree(u);
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) sc[c] = u;
+            v = u;
+        }
+        m = m2;
+    }
+    return __shfl(v, 0, 64);
+}
+
+constexpr int kWaveScratch = 512;  // per-wave LDS scratch: lists up to 32768 terms
+constexpr int DIAG21[6] = {0, 6, 11, 15, 18, 20};
+
+// term layout (SoA, stride nE): Hpp 0..20 | bp 21..26 | Hll 27..35 | bl 36..38
+constexpr int T_HPP = 0, T_BP = 21, T_HLL = 27, T_BL = 36, T_N = 39;
+
+// ---------------------------------------------------------------- kernels
+struct LinArgs {
+    BaStructDev s;
+    const EdgeDev* E;
+    const Se3* T;
+    const double* X;
+    const uint8_t* robust;
+    double* err;      // ne x 3
+    double* rc;       // nE robust chi2 terms
+    double* terms;    // T_N x nE
+    double* Hpl;      // nE x 18
+    int linearize;
+};
+
+// computeActiveErrors + activeRobustChi2 terms (+ linearizeOplus + constructQuadraticForm)
+__global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.s.nE) return;
+    const int ei = a.s.aE[i];
+    const EdgeDev e = a.E[ei];
+    const Se3 T = a.T[e.kf];
+    const double X[3] = {a.X[3 * e.pt], a.X[3 * e.pt + 1], a.X[3 * e.pt + 2]};
+    double err[3];
+    edge_error(e, T, X, err);
+    for (int k = 0; k < 3; k++) a.err[3 * ei + k] = err[k];
+    const double chi = edge_chi2(e, err);
+    const int robust = a.robust[ei];
+    double r0 = chi, rho1 = 1.0;
+    if (robust) huber(e, chi, &r0, &rho1);
+    a.rc[i] = r0;
+    if (!a.linearize) return;
+    // linearizeOplus (.cpp:103-147 mono, 188-234 stereo)
+    double p[3], R[9], A[9], B[18];
+    se3_map(T, X, p);
+    quat_to_R(T.q, R);
+    const double x = p[0], y = p[1], z = p[2], z_2 = z * z;
+    const double fx = e.fx, fy = e.fy;
+    const int D = e.stereo ? 3 : 2;
+    if (!e.stereo) {
+        const double tmp[6] = {fx, 0, ((-x) / z) * fx, 0, fy, ((-y) / z) * fy};
+        const double s = -1. / z;
+        double st[6];
+        for (int k = 0; k < 6; k++) st[k] = s * tmp[k];
+        for (int r = 0; r < 2; r++)
+            for (int c = 0; c < 3; c++) A[r * 3 + c] = (st[r * 3] * R[c] + st[r * 3 + 1] * R[3 + c]) + st[r * 3 + 2] * R[6 + c];
+    } else {
+        const double bf = e.bf;
+        for (int c = 0; c < 3; c++) {
+            A[0 * 3 + c] = ((-fx) * R[0 * 3 + c]) / z + ((fx * x) * R[2 * 3 + c]) / z_2;
+            A[1 * 3 + c] = ((-fy) * R[1 * 3 + c]) / z + ((fy * y) * R[2 * 3 + c]) / z_2;
+            A[2 * 3 + c] = A[0 * 3 + c] - (bf * R[2 * 3 + c]) / z_2;
+        }
+    }
+    B[0] = ((x * y) / z_2) * fx;
+    B[1] = (-(1 + ((x * x) / z_2))) * fx;
+    B[2] = (y / z) * fx;
+    B[3] = (-1. / z) * fx;
+    B[4] = 0;
+    B[5] = (x / z_2) * fx;
+    B[6] = (1 + ((y * y) / z_2)) * fy;
+    B[7] = (((-x) * y) / z_2) * fy;
+    B[8] = ((-x) / z) * fy;
+    B[9] = 0;
+    B[10] = (-1. / z) * fy;
+    B[11] = (y / z_2) * fy;
+    if (e.stereo) {
+        const double bf = e.bf;
+        B[12] = B[0] - (bf * y) / z_2;
+        B[13] = B[1] + (bf * x) / z_2;
+        B[14] = B[2];
+        B[15] = B[3];
+        B[16] = 0;
+        B[17] = B[5] - bf / z_2;
+    } else {
+        for (int k = 12; k < 18; k++) B[k] = 0;
+    }
+    // constructQuadraticForm (base_binary_edge.hpp:55-120)
+    const double w = robust ? rho1 * e.info : e.info;
+    double omr[3] = {0, 0, 0};
+    for (int k = 0; k < D; k++) {
+        omr[k] = -(e.info * err[k]);
+        if (robust) omr[k] *= rho1;
+    }
+    const int nE = a.s.nE;
+    double* t = a.terms;
+    for (int r = 0; r < 3; r++) {
+        double s = 0;
+        for (int k = 0; k < D; k++) s += A[k * 3 + r] * omr[k];
+        t[(T_BL + r) * nE + i] = s;
+        for (int c = 0; c < 3; c++) {
+            double h = 0;
+            for (int k = 0; k < D; k++) h += (A[k * 3 + r] * w) * A[k * 3 + c];
+            t[(T_HLL + r * 3 + c) * nE + i] = h;
+        }
+    }
+    if (a.s.ePose[i] < 0) return;
+    int q = 0;
+    for (int r = 0; r < 6; r++) {
+        double s = 0;
+        for (int k = 0; k < D; k++) s += B[k * 6 + r] * omr[k];
+        t[(T_BP + r) * nE + i] = s;
+        for (int c = r; c < 6; c++) {
+            double h = 0;
+            for (int k = 0; k < D; k++) h += (B[k * 6 + r] * w) * B[k * 6 + c];
+            t[(T_HPP + q) * nE + i] = h;
+            q++;
+        }
+        for (int c = 0; c < 3; c++) {
+            double h = 0;
+            if (robust)
+                for (int k = 0; k < D; k++) h += (B[k * 6 + r] * w) * A[k * 3 + c];
+            else
+                for (int k = 0; k < D; k++) h += B[k * 6 + r] * (A[k * 3 + c] * e.info);
+            a.Hpl[18 * (size_t)i + r * 3 + c] = h;
+        }
+    }
+}
+
+// per free pose: Hpp (upper 21) and b_p as canonical sums over its active edges (edge order)
+__global__ void __launch_bounds__(256) k_pose_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
+                                                     double* bp) {
+    __shared__ double sc[4][kWaveScratch];
+    const int i = blockIdx.x;
+    const int w = threadIdx.x >> 6;
+    const int s0 = s.peStart[i], n = s.peStart[i + 1] - s0;
+    const int nE = s.nE;
+    for (int q = w; q < 27; q += 4) {
+        const double* col = terms + (size_t)(q < 21 ? T_HPP + q : T_BP + (q - 21)) * nE;
+        const double v = wave_csum([&](int j) { return col[s.peList[s0 + j]]; }, n, sc[w]);
+        if ((threadIdx.x & 63) == 0) {
+            if (q < 21) Hpp[21 * i + q] = v;
+            else bp[6 * i + (q - 21)] = v;
+        }
+    }
+}
+
+// per landmark (one wave): Hll (full 3x3) and b_l over its active edges (edge order)
+__global__ void __launch_bounds__(256) k_land_reduce(BaStructDev s, const double* __restrict__ terms, double* Hll,
+                                                     double* bl) {
+    __shared__ double sc[4][kWaveScratch];
+    const int w = threadIdx.x >> 6;
+    const int l = blockIdx.x * 4 + w;
+    if (l >= s.nL) return;
+    const int s0 = s.leStart[l], n = s.leStart[l + 1] - s0;
+    const int nE = s.nE;
+    for (int q = 0; q < 12; q++) {
+        const double* col = terms + (size_t)(q < 9 ? T_HLL + q : T_BL + (q - 9)) * nE;
+        const double v = wave_csum([&](int j) { return col[s.leList[s0 + j]]; }, n, sc[w]);
+        if ((threadIdx.x & 63) == 0) {
+            if (q < 9) Hll[9 * l + q] = v;
+            else bl[3 * l + (q - 9)] = v;
+        }
+    }
+}
+
+// computeLambdaInit: tau * max |diag| over poses and landmarks (order-free max)
+__global__ void __launch_bounds__(1024) k_lambda_init(int nP, int nL, const double* Hpp, const double* Hll,
+                                                      double* scal) {
+    __shared__ double red[1024];
+    double m = 0.;
+    for (int j = threadIdx.x; j < 6 * nP + 3 * nL; j += blockDim.x) {
+        const double d = j < 6 * nP ? Hpp[21 * (j / 6) + DIAG21[j % 6]] : Hll[9 * ((j - 6 * nP) / 3) + 4 * ((j - 6 * nP) % 3)];
+        m = fmax(fabs(d), m);
+    }
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 512; o >= 1; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        scal[4] = red[0];
+        scal[5] = 1e-5 * red[0];
+    }
+}
+
+__device__ __forceinline__ double lam_of(double lam_host, int use_dev, const double* scal) {
+    return use_dev ? scal[5] : lam_host;
+}
+
+// Eigen 3x3 inverse (compute_inverse_size3)
+__device__ __forceinline__ void inv3(const double* m, double* r) {
+#define M(i, j) m[(i) * 3 + (j)]
+#define COF(i, j) (M(((i) + 1) % 3, ((j) + 1) % 3) * M(((i) + 2) % 3, ((j) + 2) % 3) - \
+                   M(((i) + 1) % 3, ((j) + 2) % 3) * M(((i) + 2) % 3, ((j) + 1) % 3))
+    const double c0 = COF(0, 0), c1 = COF(1, 0), c2 = COF(2, 0);
+    const double det = (c0 * M(0, 0) + c1 * M(1, 0)) + c2 * M(2, 0);
+    const double invdet = 1.0 / det;
+    r[0] = c0 * invdet; r[1] = c1 * invdet; r[2] = c2 * invdet;
+    r[3] = COF(0, 1) * invdet; r[4] = COF(1, 1) * invdet; r[5] = COF(2, 1) * invdet;
+    r[6] = COF(0, 2) * invdet; r[7] = COF(1, 2) * invdet; r[8] = COF(2, 2) * invdet;
+#undef COF
+#undef M
+}
+
+// per landmark: Dinv = (Hll + lambda I)^-1, db = Dinv b_l, and per free-pose edge
+// BDinv = Hpl Dinv and B db (block_solver.hpp:376-404)
+__global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double* Hll, const double* bl,
+                                                    const double* __restrict__ Hpl, double lam_host, int use_dev,
+                                                    const double* scal, double* Dinv, double* db, double* Emat,
+                                                    double* cb) {
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= s.nL) return;
+    const double lambda = lam_of(lam_host, use_dev, scal);
+    double D[9], Di[9], b[3], d[3];
+    for (int q = 0; q < 9; q++) D[q] = Hll[9 * l + q];
+    for (int j = 0; j < 3; j++) D[4 * j] += lambda;
+    inv3(D, Di);
+    for (int q = 0; q < 3; q++) b[q] = bl[3 * l + q];
+    for (int r = 0; r < 3; r++) d[r] = (Di[r * 3] * b[0] + Di[r * 3 + 1] * b[1]) + Di[r * 3 + 2] * b[2];
+    for (int q = 0; q < 9; q++) Dinv[9 * l + q] = Di[q];
+    for (int q = 0; q < 3; q++) db[3 * l + q] = d[q];
+    for (int j = s.lpStart[l]; j < s.lpStart[l + 1]; j++) {
+        const int a = s.lpList[j];
+        const double* Bi = Hpl + 18 * (size_t)a;
+        for (int r = 0; r < 6; r++) {
+            const double b0 = Bi[r * 3], b1 = Bi[r * 3 + 1], b2 = Bi[r * 3 + 2];
+            for (int k = 0; k < 3; k++) Emat[18 * (size_t)a + r * 3 + k] = (b0 * Di[k] + b1 * Di[3 + k]) + b2 * Di[6 + k];
+            cb[6 * (size_t)a + r] = (b0 * d[0] + b1 * d[1]) + b2 * d[2];
+        }
+    }
+}
+
+// Schur complement block (i1, i2): S = [Hpp + lambda I] - csum_l BDinv_l,i1 B_l,i2^T
+// (upper triangle of the diagonal blocks), and b_s = b_p - csum_l B db.
+__global__ void __launch_bounds__(256) k_schur(BaStructDev s, const double* __restrict__ Emat,
+                                               const double* __restrict__ Hpl, const double* __restrict__ cb,
+                                               const double* Hpp, const double* bp, double lam_host, int use_dev,
+                                               const double* scal, double* S, double* bs) {
+    __shared__ double sc[4][kWaveScratch];
+    const int blk = blockIdx.x;
+    const int i1 = s.blkI[blk], i2 = s.blkJ[blk];
+    const int w = threadIdx.x >> 6;
+    const int s0 = s.blkStart[blk], n = s.blkStart[blk + 1] - s0;
+    const int nn = 6 * s.nP;
+    const bool diag = i1 == i2;
+    const double lambda = lam_of(lam_host, use_dev, scal);
+    const int nent = diag ? 27 : 36;
+    for (int q = w; q < nent; q += 4) {
+        if (diag && q >= 21) {  // b_schur row r of pose i1
+            const int r = q - 21;
+            const double v = wave_csum([&](int j) { return cb[6 * (size_t)s.pairA[s0 + j] + r]; }, n, sc[w]);
+            if ((threadIdx.x & 63) == 0) bs[6 * i1 + r] = bp[6 * i1 + r] - v;
+            continue;
+        }
+        int r, c;
+        if (diag) {  // q -> (r, c) with c >= r, packed like DIAG21
+            r = 0;
+            while (r < 5 && q >= DIAG21[r + 1]) r++;
+            c = r + (q - DIAG21[r]);
+        } else {
+            r = q / 6;
+            c = q % 6;
+        }
+        const double v = wave_csum(
+            [&](int j) {
+                const double* Ei = Emat + 18 * (size_t)s.pairA[s0 + j] + r * 3;
+                const double* Bj = Hpl + 18 * (size_t)s.pairB[s0 + j] + c * 3;
+                return (Ei[0] * Bj[0] + Ei[1] * Bj[1]) + Ei[2] * Bj[2];
+            },
+            n, sc[w]);
+        if ((threadIdx.x & 63) == 0) {
+            double h = 0;
+            if (diag) {
+                h = Hpp[21 * i1 + q];
+                if (c == r) h += lambda;
+            }
+            S[(size_t)(6 * i1 + r) * nn + 6 * i2 + c] = h - v;
+        }
+    }
+}
+
+// Dense LDL^T of the upper triangle + solve (oracle ora_ldlt_solve), one workgroup.
+// S is staged in LDS when it fits.  x_p -> x[0..n), ok flag -> scal[3].
+__global__ void __launch_bounds__(256) k_ldlt(int n, double* Sg, const double* bs, double* x, double* scal, int in_lds) {
+    extern __shared__ double lds[];
+    double* l = lds;            // n
+    double* y = lds + n;        // n
+    double* A = in_lds ? lds + 2 * n : Sg;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (in_lds)
+        for (int q = tid; q < n * n; q += nt) A[q] = Sg[q];
+    for (int q = tid; q < n; q += nt) y[q] = bs[q];
+    __syncthreads();
+    __shared__ int ok;
+    if (tid == 0) ok = 1;
+    __syncthreads();
+    for (int k = 0; k < n; k++) {
+        const double d = A[(size_t)k * n + k];
+        if (d == 0.0) {
+            if (tid == 0) ok = 0;
+            break;
+        }
+        for (int i = k + 1 + tid; i < n; i += nt) l[i] = A[(size_t)k * n + i] / d;
+        __syncthreads();
+        const int m = n - k - 1;
+        for (int q = tid; q < m * m; q += nt) {
+            const int i = k + 1 + q / m, j = k + 1 + q % m;
+            if (j >= i) A[(size_t)i * n + j] -= l[i] * A[(size_t)k * n + j];
+        }
+        __syncthreads();
+        for (int i = k + 1 + tid; i < n; i += nt) A[(size_t)k * n + i] = l[i];
+        __syncthreads();
+    }
+    __syncthreads();
+    if (!ok) {
+        if (tid == 0) scal[3] = 0.0;
+        return;
+    }
+    for (int k = 0; k < n; k++) {
+        const double yk = y[k];
+        for (int i = k + 1 + tid; i < n; i += nt) y[i] -= A[(size_t)k * n + i] * yk;
+        __syncthreads();
+    }
+    for (int k = tid; k < n; k += nt) y[k] = y[k] / A[(size_t)k * n + k];
+    __syncthreads();
+    for (int k = n - 1; k >= 0; k--) {
+        const double yk = y[k];
+        for (int i = tid; i < k; i += nt) y[i] -= A[(size_t)i * n + k] * yk;
+        __syncthreads();
+    }
+    for (int k = tid; k < n; k += nt) x[k] = y[k];
+    if (tid == 0) scal[3] = 1.0;
+}
+
+// push + back-substitution (block_solver.hpp:457-484) + SparseOptimizer::update (oplus)
+__global__ void __launch_bounds__(256) k_update(BaStructDev s, Se3* T, Se3* Tbak, double* X, double* Xbak,
+                                                double* x, const double* __restrict__ Hpl, const double* Dinv,
+                                                const double* bl, const double* scal) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nP = s.nP;
+    if (g < nP) {
+        const int kf = s.poseKf[g];
+        const Se3 t0 = T[kf];
+        Tbak[kf] = t0;
+        double upd[6];
+        for (int k = 0; k < 6; k++) upd[k] = x[6 * g + k];
+        Se3 d, r;
+        se3_exp(upd, d);
+        se3_mul(d, t0, r);
+        T[kf] = r;
+        return;
+    }
+    const int l = g - nP;
+    if (l >= s.nL) return;
+    const int pt = s.landPt[l];
+    double* xl = x + 6 * nP + 3 * l;
+    if (scal[3] != 0.0) {  // solver succeeded: xl = Dinv (b_l - sum_i B_i^T xp_i), blocks in pose order
+        double cl[3] = {bl[3 * l], bl[3 * l + 1], bl[3 * l + 2]};
+        for (int j = s.lpStart[l]; j < s.lpStart[l + 1]; j++) {
+            const int a = s.lpList[j];
+            const double* B = Hpl + 18 * (size_t)a;
+            const double* cp = x + 6 * s.ePose[a];
+            for (int k = 0; k < 3; k++) {
+                double acc = 0;
+                for (int r = 0; r < 6; r++) acc += B[r * 3 + k] * (-cp[r]);
+                cl[k] += acc;
+            }
+        }
+        const double* Di = Dinv + 9 * l;
+        for (int r = 0; r < 3; r++) xl[r] = (Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1]) + Di[r * 3 + 2] * cl[2];
+    }
+    for (int k = 0; k < 3; k++) {
+        const double v = X[3 * pt + k];
+        Xbak[3 * pt + k] = v;
+        X[3 * pt + k] = v + xl[k];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pop(BaStructDev s, Se3* T, const Se3* Tbak, double* X, const double* Xbak) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < s.nP) {
+        const int kf = s.poseKf[g];
+        T[kf] = Tbak[kf];
+        return;
+    }
+    const int l = g - s.nP;
+    if (l >= s.nL) return;
+    const int pt = s.landPt[l];
+    for (int k = 0; k < 3; k++) X[3 * pt + k] = Xbak[3 * pt + k];
+}
+
+// computeScale terms: x_j (lambda x_j + b_j)
+__global__ void __launch_bounds__(256) k_scale_terms(int n, const double* x, const double* b, double lam_host,
+                                                     int use_dev, const double* scal, double* out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const double lambda = lam_of(lam_host, use_dev, scal);
+    out[j] = x[j] * (lambda * x[j] + b[j]);
+}
+
+// b vector (poses then landmarks) for computeScale
+__global__ void __launch_bounds__(256) k_copy_b(int nP, int nL, const double* bp, const double* bl, double* b) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < 6 * nP) b[j] = bp[j];
+    else if (j < 6 * nP + 3 * nL) b[j] = bl[j - 6 * nP];
+}
+
+// canonical sum of one list per workgroup (blockIdx.x selects the list), 1024 threads,
+// level buffers ping-pong in global scratch.
+struct CsumList {
+    const double* v;
+    int n;
+    double* tmp0;
+    double* tmp1;
+    double* out;
+};
+__global__ void __launch_bounds__(1024) k_csum(CsumList L0, CsumList L1) {
+    const CsumList L = blockIdx.x == 0 ? L0 : L1;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (L.n <= 1) {
+        if (threadIdx.x == 0) *L.out = L.n == 1 ? L.v[0] : 0.0;
+        return;
+    }
+    const double* src = L.v;
+    double* dst = L.tmp0;
+    int m = L.n;
+    while (true) {
+        const int m2 = (m + 63) >> 6;
+        for (int c = w; c < m2; c += nw) {
+            double v = (c * 64 + lane < m) ? src[c * 64 + lane] : 0.0;
+            v = wave_tree(v);
+            if (lane == 0) dst[c] = v;
+        }
+        __threadfence_block();
+        __syncthreads();
+        if (m2 == 1) break;
+        src = dst;
+        dst = (dst == L.tmp0) ? L.tmp1 : L.tmp0;
+        m = m2;
+    }
+    if (threadIdx.x == 0) *L.out = dst[0];
+}
+
+// outlier gating / final check over all edges (Optimizer.cc:674-706, 714-746):
+// flag = chi2(last _error) > th || !isDepthPositive()
+__global__ void __launch_bounds__(256) k_gate(int ne, const EdgeDev* E, const Se3* T, const double* X,
+                                              const double* err, uint8_t* flag, uint8_t* level, uint8_t* robust,
+                                              int set_level) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ne) return;
+    const EdgeDev e = E[i];
+    const double chi = edge_chi2(e, err + 3 * i);
+    double p[3];
+    const double Xp[3] = {X[3 * e.pt], X[3 * e.pt + 1], X[3 * e.pt + 2]};
+    se3_map(T[e.kf], Xp, p);
+    const double th = e.stereo ? 7.815 : 5.991;
+    const uint8_t bad = (chi > th || !(p[2] > 0.0)) ? 1 : 0;
+    flag[i] = bad;
+    if (set_level) {
+        if (bad) level[i] = 1;
+        robust[i] = 0;
+    }
+}
+
+// ---------------------------------------------------------------- host
+static void host_se3_from_Tcw(const float* T, Se3& o) {
+    double R[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) R[r * 3 + c] = (double)T[r * 4 + c];
+    quat_from_R(R, o.q);
+    for (int r = 0; r < 3; r++) o.t[r] = (double)T[r * 4 + 3];
+    o.pad = 0;
+    se3_normalize(o);
+}
+
+static void host_se3_to_Tcw(const Se3& s, float* T) {
+    double R[9];
+    quat_to_R(s.q, R);
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) T[r * 4 + c] = (float)R[r * 3 + c];
+        T[r * 4 + 3] = (float)s.t[r];
+    }
+    T[12] = T[13] = T[14] = 0.f;
+    T[15] = 1.f;
+}
+
+BaEngine::~BaEngine() {
+    if (arena_) (void)hipFree(arena_);
+    if (dStruct_) (void)hipFree(dStruct_);
+    if (hScal_) (void)hipHostFree(hScal_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+int BaEngine::init() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
+    ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    ORB_HIP_CHECK(hipHostMalloc((void**)&hScal_, 64 * sizeof(double)));
+    ORB_HIP_CHECK(hipFuncSetAttribute((const void*)k_ldlt, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    return 0;
+}
+
+// Carve every device buffer of the problem out of one grow-only arena.
+int BaEngine::carve(bool commit, size_t* total) {
+    const size_t ne = (size_t)std::max(ne_, 1), nkf = (size_t)std::max(nkf_, 1), npt = (size_t)std::max(npt_, 1);
+    scratchN_ = 6 * nkf + 3 * npt + ne + 64;
+    const size_t tmpN = scratchN_ / 64 + 64;
+    size_t off = 0;
+    char* base = (char*)arena_;
+    auto take = [&](size_t bytes) -> void* {
+        void* p = commit ? (void*)(base + off) : nullptr;
+        off += (bytes + 255) & ~(size_t)255;
+        return p;
+    };
+    dT_ = (Se3*)take(sizeof(Se3) * nkf);
+    dTbak_ = (Se3*)take(sizeof(Se3) * nkf);
+    dX_ = (double*)take(sizeof(double) * 3 * npt);
+    dXbak_ = (double*)take(sizeof(double) * 3 * npt);
+    dE_ = (EdgeDev*)take(sizeof(EdgeDev) * ne);
+    dLevel_ = (uint8_t*)take(ne);
+    dRobust_ = (uint8_t*)take(ne);
+    dErr_ = (double*)take(sizeof(double) * 3 * ne);
+    dTerms_ = (double*)take(sizeof(double) * T_N * ne);
+    dRc_ = (double*)take(sizeof(double) * ne);
+    dHpp_ = (double*)take(sizeof(double) * 21 * nkf);
+    dBp_ = (double*)take(sizeof(double) * 6 * nkf);
+    dHll_ = (double*)take(sizeof(double) * 9 * npt);
+    dBl_ = (double*)take(sizeof(double) * 3 * npt);
+    dB_ = (double*)take(sizeof(double) * (6 * nkf + 3 * npt));
+    dX2_ = (double*)take(sizeof(double) * (6 * nkf + 3 * npt));
+    dS_ = (double*)take(sizeof(double) * 36 * nkf * nkf);
+    dBs_ = (double*)take(sizeof(double) * 6 * nkf);
+    dDinv_ = (double*)take(sizeof(double) * 9 * npt);
+    dDb_ = (double*)take(sizeof(double) * 3 * npt);
+    dEmat_ = (double*)take(sizeof(double) * 18 * ne);
+    dCb_ = (double*)take(sizeof(double) * 6 * ne);
+    dHplA_ = (double*)take(sizeof(double) * 18 * ne);
+    dScal_ = (double*)take(sizeof(double) * 16);
+    dScratch_ = (double*)take(sizeof(double) * scratchN_);
+    tmpA0_ = (double*)take(sizeof(double) * tmpN);
+    tmpA1_ = (double*)take(sizeof(double) * tmpN);
+    tmpB0_ = (double*)take(sizeof(double) * tmpN);
+    tmpB1_ = (double*)take(sizeof(double) * tmpN);
+    *total = off;
+    return 0;
+}
+
+int BaEngine::upload_problem(const ba_problem* P) {
+    nkf_ = P->n_kf;
+    npt_ = P->n_pt;
+    ne_ = P->n_edge;
+    size_t need = 0;
+    carve(false, &need);
+    if (need > arenaCap_) {
+        if (arena_) (void)hipFree(arena_);
+        arena_ = nullptr;
+        arenaCap_ = 0;
+        ORB_HIP_CHECK(hipMalloc(&arena_, need + need / 4));
+        arenaCap_ = need + need / 4;
+    }
+    carve(true, &need);
+
+    kfId_.assign(P->kf_id, P->kf_id + nkf_);
+    ptId_.assign(P->pt_id, P->pt_id + npt_);
+    ePt_.assign(P->edge_pt, P->edge_pt + ne_);
+    eKf_.assign(P->edge_kf, P->edge_kf + ne_);
+    kfLocal_.assign(P->kf_local, P->kf_local + nkf_);
+    kfFixed_.resize(nkf_);
+    for (int k = 0; k < nkf_; k++) kfFixed_[k] = (!P->kf_local[k] || P->kf_id[k] == 0) ? 1 : 0;
+    std::vector<Se3> T(nkf_);
+    for (int k = 0; k < nkf_; k++) host_se3_from_Tcw(P->kf_Tcw + 16 * k, T[k]);
+    std::vector<double> X(3 * (size_t)npt_);
+    for (size_t q = 0; q < X.size(); q++) X[q] = (double)P->pt_pos[q];
+    const float thMono = (float)std::sqrt(5.991), thStereo = (float)std::sqrt(7.815);
+    std::vector<EdgeDev> E(ne_);
+    for (int i = 0; i < ne_; i++) {
+        EdgeDev& e = E[i];
+        std::memset(&e, 0, sizeof(e));
+        e.pt = P->edge_pt[i];
+        e.kf = P->edge_kf[i];
+        e.stereo = !(P->edge_obs[3 * i + 2] < 0);
+        for (int j = 0; j < 3; j++) e.obs[j] = (double)P->edge_obs[3 * i + j];
+        e.info = (double)P->edge_inv_sigma2[i];
+        const float* cam = P->kf_cam + 5 * e.kf;
+        e.fx = cam[0]; e.fy = cam[1]; e.cx = cam[2]; e.cy = cam[3]; e.bf = cam[4];
+        e.delta = (double)(e.stereo ? thStereo : thMono);
+        e.dsqr = e.delta * e.delta;
+    }
+    level_.assign(ne_, 0);
+    hipStream_t s = stream_;
+    if (nkf_) ORB_HIP_CHECK(hipMemcpyAsync(dT_, T.data(), sizeof(Se3) * nkf_, hipMemcpyHostToDevice, s));
+    if (npt_) ORB_HIP_CHECK(hipMemcpyAsync(dX_, X.data(), sizeof(double) * X.size(), hipMemcpyHostToDevice, s));
+    if (ne_) {
+        ORB_HIP_CHECK(hipMemcpyAsync(dE_, E.data(), sizeof(EdgeDev) * ne_, hipMemcpyHostToDevice, s));
+        ORB_HIP_CHECK(hipMemsetAsync(dLevel_, 0, ne_, s));
+        ORB_HIP_CHECK(hipMemsetAsync(dRobust_, 1, ne_, s));
+        ORB_HIP_CHECK(hipMemsetAsync(dErr_, 0, sizeof(double) * 3 * ne_, s));
+    }
+    ORB_HIP_CHECK(hipStreamSynchronize(s));  // host vectors above are pageable temporaries
+    return 0;
+}
+
+// initializeOptimization(level) + buildIndexMapping + BlockSolver::buildStructure
+int BaEngine::build_structure(int level) {
+    std::vector<int32_t> aE;
+    aE.reserve(ne_);
+    std::vector<uint8_t> kfAct(nkf_, 0), ptAct(npt_, 0);
+    for (int i = 0; i < ne_; i++)
+        if (level_[i] == level) {
+            aE.push_back(i);
+            kfAct[eKf_[i]] = 1;
+            ptAct[ePt_[i]] = 1;
+        }
+    std::vector<int32_t> poseKf, landPt;
+    for (int k = 0; k < nkf_; k++)
+        if (kfAct[k] && !kfFixed_[k]) poseKf.push_back(k);
+    std::sort(poseKf.begin(), poseKf.end(), [&](int a, int b) { return kfId_[a] < kfId_[b]; });
+    for (int p = 0; p < npt_; p++)
+        if (ptAct[p]) landPt.push_back(p);
+    std::sort(landPt.begin(), landPt.end(), [&](int a, int b) { return ptId_[a] < ptId_[b]; });
+    const int nE = (int)aE.size(), nP = (int)poseKf.size(), nL = (int)landPt.size();
+    std::vector<int32_t> poseIdx(nkf_, -1), landIdx(npt_, -1);
+    for (int i = 0; i < nP; i++) poseIdx[poseKf[i]] = i;
+    for (int i = 0; i < nL; i++) landIdx[landPt[i]] = i;
+    std::vector<int32_t> ePose(nE), eLand(nE);
+    std::vector<int32_t> peStart(nP + 1, 0), leStart(nL + 1, 0), lpStart(nL + 1, 0);
+    for (int a = 0; a < nE; a++) {
+        ePose[a] = poseIdx[eKf_[aE[a]]];
+        eLand[a] = landIdx[ePt_[aE[a]]];
+        if (ePose[a] >= 0) {
+            peStart[ePose[a] + 1]++;
+            lpStart[eLand[a] + 1]++;
+        }
+        leStart[eLand[a] + 1]++;
+    }
+    for (int i = 0; i < nP; i++) peStart[i + 1] += peStart[i];
+    for (int i = 0; i < nL; i++) {
+        leStart[i + 1] += leStart[i];
+        lpStart[i + 1] += lpStart[i];
+    }
+    std::vector<int32_t> peList(std::max(peStart[nP], 1)), leList(std::max(leStart[nL], 1)), lpList(std::max(lpStart[nL], 1));
+    {
+        std::vector<int32_t> fp(peStart.begin(), peStart.end() - 1), fl(leStart.begin(), leStart.end() - 1),
+            fq(lpStart.begin(), lpStart.end() - 1);
+        for (int a = 0; a < nE; a++) {
+            if (ePose[a] >= 0) {
+                peList[fp[ePose[a]]++] = a;
+                lpList[fq[eLand[a]]++] = a;
+            }
+            leList[fl[eLand[a]]++] = a;
+        }
+    }
+    // landmark blocks in pose order; enforce one edge per (pose, landmark)
+    for (int l = 0; l < nL; l++) {
+        std::sort(lpList.begin() + lpStart[l], lpList.begin() + lpStart[l + 1],
+                  [&](int a, int b) { return ePose[a] < ePose[b]; });
+        for (int j = lpStart[l] + 1; j < lpStart[l + 1]; j++)
+            if (ePose[lpList[j]] == ePose[lpList[j - 1]]) return -1;
+    }
+    // Schur pattern: blocks (i1 <= i2), diagonal always; terms in landmark order
+    std::vector<int64_t> cnt;
+    std::vector<int32_t> blkOf((size_t)nP * nP, -1), blkI, blkJ;
+    for (int i = 0; i < nP; i++) {
+        blkOf[(size_t)i * nP + i] = (int)blkI.size();
+        blkI.push_back(i);
+        blkJ.push_back(i);
+    }
+    std::vector<int32_t> bcount(nP, 0);
+    for (int l = 0; l < nL; l++)
+        for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
+            for (int v = u; v < lpStart[l + 1]; v++) {
+                const int i1 = ePose[lpList[u]], i2 = ePose[lpList[v]];
+                int32_t& b = blkOf[(size_t)i1 * nP + i2];
+                if (b < 0) {
+                    b = (int)blkI.size();
+                    blkI.push_back(i1);
+                    blkJ.push_back(i2);
+                }
+            }
+    const int nBlk = (int)blkI.size();
+    std::vector<int32_t> blkStart(nBlk + 1, 0);
+    for (int l = 0; l < nL; l++)
+        for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
+            for (int v = u; v < lpStart[l + 1]; v++)
+                blkStart[blkOf[(size_t)ePose[lpList[u]] * nP + ePose[lpList[v]]] + 1]++;
+    for (int b = 0; b < nBlk; b++) blkStart[b + 1] += blkStart[b];
+    const int nPair = blkStart[nBlk];
+    std::vector<int32_t> pairA(std::max(nPair, 1)), pairB(std::max(nPair, 1));
+    {
+        std::vector<int32_t> fb(blkStart.begin(), blkStart.end() - 1);
+        for (int l = 0; l < nL; l++)
+            for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
+                for (int v = u; v < lpStart[l + 1]; v++) {
+                    const int b = blkOf[(size_t)ePose[lpList[u]] * nP + ePose[lpList[v]]];
+                    pairA[fb[b]] = lpList[u];
+                    pairB[fb[b]++] = lpList[v];
+                }
+    }
+    for (int i = 0; i < nP; i++)
+        if (peStart[i + 1] - peStart[i] > 64 * kWaveScratch) return -3;
+    for (int l = 0; l < nL; l++)
+        if (leStart[l + 1] - leStart[l] > 64 * kWaveScratch) return -3;
+    for (int b = 0; b < nBlk; b++)
+        if (blkStart[b + 1] - blkStart[b] > 64 * kWaveScratch) return -3;
+    // pack and upload
+    std::vector<const std::vector<int32_t>*> parts = {&aE,      &ePose,   &eLand,  &poseKf, &landPt, &peStart,
+                                                      &peList,  &leStart, &leList, &lpStart, &lpList, &blkI,
+                                                      &blkJ,    &blkStart, &pairA, &pairB};
+    size_t tot = 0;
+    for (auto* p : parts) tot += (p->size() + 63) & ~(size_t)63;
+    hStruct_.assign(tot, 0);
+    std::vector<size_t> off;
+    size_t o = 0;
+    for (auto* p : parts) {
+        off.push_back(o);
+        std::copy(p->begin(), p->end(), hStruct_.begin() + o);
+        o += (p->size() + 63) & ~(size_t)63;
+    }
+    if (tot * 4 > dStructCap_) {
+        if (dStruct_) (void)hipFree(dStruct_);
+        ORB_HIP_CHECK(hipMalloc(&dStruct_, tot * 4 * 2));
+        dStructCap_ = tot * 4 * 2;
+    }
+    ORB_HIP_CHECK(hipMemcpyAsync(dStruct_, hStruct_.data(), tot * 4, hipMemcpyHostToDevice, stream_));
+    const int32_t* d = dStruct_;
+    st_.nE = nE; st_.nP = nP; st_.nL = nL; st_.nBlk = nBlk;
+    st_.aE = d + off[0]; st_.ePose = d + off[1]; st_.eLand = d + off[2]; st_.poseKf = d + off[3];
+    st_.landPt = d + off[4]; st_.peStart = d + off[5]; st_.peList = d + off[6]; st_.leStart = d + off[7];
+    st_.leList = d + off[8]; st_.lpStart = d + off[9]; st_.lpList = d + off[10]; st_.blkI = d + off[11];
+    st_.blkJ = d + off[12]; st_.blkStart = d + off[13]; st_.pairA = d + off[14]; st_.pairB = d + off[15];
+    ORB_HIP_CHECK(hipMemsetAsync(dX2_, 0, sizeof(double) * (6 * (size_t)nP + 3 * (size_t)nL + 1), stream_));
+    ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * 36 * (size_t)nP * nP + 8, stream_));
+    // the pageable hStruct_ copy must finish before the host vector is reused
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    return 0;
+}
+
+static inline int nblk(int n, int b) { return (n + b - 1) / b; }
+
+// OptimizationAlgorithmLevenberg::solve (optimization_algorithm_levenberg.cpp:59-164)
+int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate) {
+    hipStream_t s = stream_;
+    const BaStructDev& S = st_;
+    const int nE = S.nE, nP = S.nP, nL = S.nL, nv = 6 * nP + 3 * nL;
+    LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1};
+    if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+    CsumList c0{dRc_, nE, tmpA0_, tmpA1_, dScal_ + 0};
+    hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, c0, c0);
+    if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(256), 0, s, S, dTerms_, dHpp_, dBp_);
+    if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(nL, 4)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_);
+    if (nv) hipLaunchKernelGGL(k_copy_b, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dBp_, dBl_, dB_);
+    int use_dev = 0;
+    if (iteration == 0) {
+        hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, nP, nL, dHpp_, dHll_, dScal_);
+        use_dev = 1;  // lambda known on the device only until the first readback
+        ni_ = 2;
+        nBad_ = 0;
+    }
+    ORB_HIP_CHECK(hipGetLastError());
+    double currentChi = 0, iniChi = 0;
+    bool haveChi = false;
+    double rho = 0;
+    int qmax = 0;
+    const int n = 6 * nP;
+    const size_t ldsBytes = sizeof(double) * (2 * (size_t)n + (size_t)n * n);
+    const int in_lds = ldsBytes <= 150 * 1024 ? 1 : 0;
+    const size_t shm = in_lds ? ldsBytes : sizeof(double) * 2 * (size_t)n;
+    if (shm > 160 * 1024) return -3;
+    do {
+        // setLambda + BlockSolver::solve
+        if (nL) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nL, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
+                                   lambda_, use_dev, dScal_, dDinv_, dDb_, dEmat_, dCb_);
+        if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(256), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
+                                       lambda_, use_dev, dScal_, dS_, dBs_);
+        hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds);
+        // push + update
+        if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_,
+                                        dXbak_, dX2_, dHplA_, dDinv_, dBl_, dScal_);
+        // computeActiveErrors + activeRobustChi2 ; computeScale
+        la.linearize = 0;
+        if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+        if (nv) hipLaunchKernelGGL(k_scale_terms, dim3(nblk(nv, 256)), dim3(256), 0, s, nv, dX2_, dB_, lambda_,
+                                   use_dev, dScal_, dScratch_);
+        CsumList c1{dRc_, nE, tmpA0_, tmpA1_, dScal_ + 1};
+        CsumList c2{dScratch_, nv, tmpB0_, tmpB1_, dScal_ + 2};
+        hipLaunchKernelGGL(k_csum, dim3(2), dim3(1024), 0, s, c1, c2);
+        ORB_HIP_CHECK(hipGetLastError());
+        ORB_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
+        ORB_HIP_CHECK(hipStreamSynchronize(s));
+        if (!haveChi) {
+            currentChi = iniChi = hScal_[0];
+            haveChi = true;
+        }
+        if (use_dev) {
+            lambda_ = hScal_[5];
+            use_dev = 0;
+        }
+        const bool ok2 = hScal_[3] != 0.0;
+        double tempChi = hScal_[1];
+        if (!ok2) tempChi = DBL_MAX;
+        rho = currentChi - tempChi;
+        double scale = hScal_[2];
+        scale += 1e-3;
+        rho /= scale;
+        if (rho > 0 && std::isfinite(tempChi)) {
+            const double a3 = 2 * rho - 1;
+            double alpha = 1. - (a3 * a3) * a3;
+            alpha = std::fmin(alpha, 2. / 3.);
+            const double scaleFactor = std::fmax(1. / 3., alpha);
+            lambda_ *= scaleFactor;
+            ni_ = 2;
+            currentChi = tempChi;
+        } else {
+            lambda_ *= ni_;
+            ni_ *= 2;
+            if (nP + nL) hipLaunchKernelGGL(k_pop, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_,
+                                            dXbak_);
+        }
+        qmax++;
+        trace_.trial_chi2.push_back(tempChi);
+        trace_.trial_lambda.push_back(lambda_);
+    } while (rho < 0 && qmax < 10 && !(stop && *stop));
+    trace_.solve_ini_chi2.push_back(iniChi);
+    trace_.solve_chi2.push_back(currentChi);
+    *terminate = false;
+    if (qmax == 10 || rho == 0) {
+        *terminate = true;
+        return 0;
+    }
+    if ((iniChi - currentChi) * 1e3 < iniChi) nBad_++;
+    else nBad_ = 0;
+    if (nBad_ >= 3) *terminate = true;
+    return 0;
+}
+
+// SparseOptimizer::optimize (sparse_optimizer.cpp:354-418)
+int BaEngine::optimize(int iterations, const volatile bool* stop, int* its) {
+    *its = 0;
+    bool ok = true;
+    for (int i = 0; i < iterations && !(stop && *stop) && ok; i++) {
+        bool term = false;
+        if (int e = lm_solve(i, stop, &term)) return e;
+        ok = !term;
+        (*its)++;
+    }
+    return 0;
+}
+
+int BaEngine::gate_edges(int final_check, uint8_t* erase) {
+    if (!ne_) return 0;
+    uint8_t* dFlag = (uint8_t*)(dScratch_);  // reuse scratch (ne bytes)
+    hipLaunchKernelGGL(k_gate, dim3(nblk(ne_, 256)), dim3(256), 0, stream_, ne_, dE_, dT_, dX_, dErr_, dFlag, dLevel_,
+                       dRobust_, final_check ? 0 : 1);
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipMemcpyAsync(erase, dFlag, ne_, hipMemcpyDeviceToHost, stream_));
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    return 0;
+}
+
+int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    trace_ = BaTrace{};
+    std::memcpy(R->kf_Tcw, P->kf_Tcw, sizeof(float) * 16 * P->n_kf);
+    std::memcpy(R->pt_pos, P->pt_pos, sizeof(float) * 3 * P->n_pt);
+    if (P->n_edge) std::memset(R->edge_erase, 0, P->n_edge);
+    R->aborted = 0;
+    R->iterations[0] = R->iterations[1] = 0;
+    R->n_erased = 0;
+    if ((stop && *stop) || P->n_edge == 0) {
+        R->aborted = 1;
+        return 0;
+    }
+    if (int e = upload_problem(P)) return e;
+    double t_struct = 0;
+    auto ts = clk::now();
+    if (int e = build_structure(0)) return e;
+    t_struct += std::chrono::duration<double, std::milli>(clk::now() - ts).count();
+    if (st_.nP + st_.nL > 0)
+        if (int e = optimize(5, stop, &R->iterations[0])) return e;
+    if (!(stop && *stop)) {
+        std::vector<uint8_t> flag(ne_);
+        if (int e = gate_edges(0, flag.data())) return e;
+        for (int i = 0; i < ne_; i++)
+            if (flag[i]) level_[i] = 1;
+        ts = clk::now();
+        if (int e = build_structure(0)) return e;
+        t_struct += std::chrono::duration<double, std::milli>(clk::now() - ts).count();
+        if (st_.nE > 0 && st_.nP + st_.nL > 0)
+            if (int e = optimize(10, stop, &R->iterations[1])) return e;
+    }
+    if (int e = gate_edges(1, R->edge_erase)) return e;
+    for (int i = 0; i < ne_; i++) R->n_erased += R->edge_erase[i];
+    std::vector<Se3> T(nkf_);
+    std::vector<double> X(3 * (size_t)npt_);
+    if (nkf_) ORB_HIP_CHECK(hipMemcpyAsync(T.data(), dT_, sizeof(Se3) * nkf_, hipMemcpyDeviceToHost, stream_));
+    if (npt_) ORB_HIP_CHECK(hipMemcpyAsync(X.data(), dX_, sizeof(double) * X.size(), hipMemcpyDeviceToHost, stream_));
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int k = 0; k < nkf_; k++)
+        if (kfLocal_[k]) host_se3_to_Tcw(T[k], R->kf_Tcw + 16 * k);
+    for (size_t q = 0; q < X.size(); q++) R->pt_pos[q] = (float)X[q];
+    last_ms[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    last_ms[1] = t_struct;
+    return 0;
+}
+
+}  // namespace orbgpu

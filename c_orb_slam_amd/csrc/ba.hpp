@@ -1,0 +1,100 @@
+// ba.hpp -- gfx950 local bundle adjustment (Optimizer::LocalBundleAdjustment,
+// reference src/Optimizer.cc:453-778, g2o BlockSolver<6,3> + Levenberg).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/orbslam_gpu.h"
+
+namespace orbgpu {
+
+struct Se3 {  // g2o::SE3Quat: q = (x, y, z, w) like Eigen coeffs(), t
+    double q[4];
+    double t[3];
+    double pad;
+};
+
+struct EdgeDev {  // one g2o edge (vertex 0 = point, vertex 1 = keyframe pose)
+    double obs[3];
+    double info;            // invSigma2 (float -> double)
+    double fx, fy, cx, cy, bf;
+    double delta, dsqr;     // RobustKernelHuber: delta = (double)(float)sqrt(th)
+    int32_t pt, kf;
+    int32_t stereo, pad;
+};
+
+// per-phase active structure (initializeOptimization + buildIndexMapping + buildStructure)
+struct BaStructDev {
+    int nE, nP, nL, nBlk;
+    const int32_t* aE;        // active edge -> edge
+    const int32_t* ePose;     // active edge -> pose index or -1 (fixed keyframe)
+    const int32_t* eLand;     // active edge -> landmark index
+    const int32_t* poseKf;    // pose index -> keyframe
+    const int32_t* landPt;    // landmark index -> point
+    const int32_t* peStart;   // pose -> active edges (edge order)
+    const int32_t* peList;
+    const int32_t* leStart;   // landmark -> active edges (edge order)
+    const int32_t* leList;
+    const int32_t* lpStart;   // landmark -> active edges with a free pose (pose order)
+    const int32_t* lpList;
+    const int32_t* blkI;      // Schur blocks (i1 <= i2), diagonal blocks always present
+    const int32_t* blkJ;
+    const int32_t* blkStart;  // block -> pair terms (landmark order)
+    const int32_t* pairA;     // active edge of the landmark to pose i1
+    const int32_t* pairB;     // active edge of the landmark to pose i2
+};
+
+struct BaTrace {
+    std::vector<double> solve_ini_chi2, solve_chi2, trial_chi2, trial_lambda;
+};
+
+class BaEngine {
+public:
+    ~BaEngine();
+    int init();
+    int run(const ba_problem* P, const volatile bool* stop, ba_result* R);
+    const BaTrace& trace() const { return trace_; }
+    double last_ms[4] = {0, 0, 0, 0};  // total, structure (host), solves (device+control), io
+
+private:
+    int upload_problem(const ba_problem* P);
+    int build_structure(int level);
+    int optimize(int iterations, const volatile bool* stop, int* its);
+    int lm_solve(int iteration, const volatile bool* stop, bool* terminate);
+    int gate_edges(int final_check, uint8_t* erase);
+    int carve(bool commit, size_t* total);
+
+    hipStream_t stream_ = nullptr;
+    // problem (device)
+    int nkf_ = 0, npt_ = 0, ne_ = 0;
+    Se3 *dT_ = nullptr, *dTbak_ = nullptr;
+    double *dX_ = nullptr, *dXbak_ = nullptr;
+    EdgeDev* dE_ = nullptr;
+    uint8_t *dLevel_ = nullptr, *dRobust_ = nullptr;
+    double* dErr_ = nullptr;       // ne x 3, last computed _error
+    // host mirror of the static problem
+    std::vector<int32_t> kfId_, ptId_, ePt_, eKf_;
+    std::vector<uint8_t> kfFixed_, kfLocal_, level_;
+    // structure
+    BaStructDev st_{};
+    std::vector<int32_t> hStruct_;
+    int32_t* dStruct_ = nullptr;
+    size_t dStructCap_ = 0;
+    // system / workspace
+    double *dTerms_ = nullptr, *dRc_ = nullptr, *dHpp_ = nullptr, *dBp_ = nullptr, *dHll_ = nullptr, *dBl_ = nullptr;
+    double *dB_ = nullptr, *dX2_ = nullptr, *dS_ = nullptr, *dBs_ = nullptr, *dDinv_ = nullptr, *dDb_ = nullptr;
+    double *dEmat_ = nullptr, *dCb_ = nullptr, *dScal_ = nullptr, *dScratch_ = nullptr, *dHplA_ = nullptr;
+    double *tmpA0_ = nullptr, *tmpA1_ = nullptr, *tmpB0_ = nullptr, *tmpB1_ = nullptr;
+    void* arena_ = nullptr;
+    size_t arenaCap_ = 0;
+    double* hScal_ = nullptr;      // pinned
+    size_t scratchN_ = 0;
+    // LM state (g2o OptimizationAlgorithmLevenberg)
+    double lambda_ = 0, ni_ = 2;
+    int nBad_ = 0;
+    BaTrace trace_;
+};
+
+}  // namespace orbgpu

@@ -20,6 +20,7 @@
  */
 #ifndef ORBSLAM_GPU_H
 #define ORBSLAM_GPU_H
+#include <stdbool.h>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -255,6 +256,52 @@ int Sim3Solver_iterate_batch(int count, Sim3Solver_h* hs, int nIterations, orb_r
 int Sim3Solver_get_estimate(Sim3Solver_h h, float* R, float* t, float* s);
 /* (mnIterations, mRansacMaxIts, mRansacMinInliers) */
 int Sim3Solver_get_state(Sim3Solver_h h, int* iterations, int* max_its, int* min_inliers);
+
+/* ======================================================================
+ * Local bundle adjustment  (reference Optimizer::LocalBundleAdjustment,
+ * src/Optimizer.cc:453-778; include/Optimizer.h:45)
+ * The adapter gathers lLocalKeyFrames / lLocalMapPoints / lFixedCameras
+ * (Optimizer.cc:456-504) and the observations in the order the reference
+ * creates its g2o edges (map points in list order, then each point's
+ * observation map order, 572-653), and applies the results (Converter
+ * round trip, EraseMapPointMatch / EraseObservation, 711-777).
+ * Requirements: unique kf_id / pt_id; at most one edge per (keyframe, point).
+ * ====================================================================== */
+typedef struct ba_problem {
+    int n_kf;
+    const int32_t* kf_id;      /* KeyFrame::mnId (g2o vertex id) */
+    const float* kf_Tcw;       /* n_kf x 16 row-major CV_32F pose */
+    const uint8_t* kf_local;   /* 1 = local keyframe (written back; fixed iff mnId == 0), 0 = fixed camera */
+    const float* kf_cam;       /* n_kf x 5: fx fy cx cy mbf */
+    int n_pt;
+    const int32_t* pt_id;      /* MapPoint::mnId */
+    const float* pt_pos;       /* n_pt x 3 GetWorldPos() */
+    int n_edge;
+    const int32_t* edge_pt;    /* index into the points */
+    const int32_t* edge_kf;    /* index into the keyframes */
+    const float* edge_obs;     /* n_edge x 3: kpUn.pt.x, kpUn.pt.y, mvuRight (< 0 = monocular edge) */
+    const float* edge_inv_sigma2;  /* mvInvLevelSigma2[kpUn.octave] */
+} ba_problem;
+
+typedef struct ba_result {
+    float* kf_Tcw;             /* n_kf x 16 (local keyframes updated, fixed cameras copied) */
+    float* pt_pos;             /* n_pt x 3 */
+    uint8_t* edge_erase;       /* n_edge: 1 = (pKFi, pMP) pushed to vToErase */
+    int32_t iterations[2];     /* optimize(5) / optimize(10) return values */
+    int32_t n_erased;
+    int32_t aborted;           /* *pbStopFlag was set before optimising: nothing written back */
+} ba_result;
+
+/* static void Optimizer::LocalBundleAdjustment(KeyFrame*, bool* pbStopFlag, Map*)
+ * stop may be NULL; it is read between LM iterations and trials like g2o's
+ * force-stop flag. */
+int Optimizer_LocalBundleAdjustment(const ba_problem* P, const volatile bool* stop, ba_result* R);
+/* LM trace of the calling thread's last run (for diagnostics / parity tests):
+ * per solve() the initial and final robust chi2, per trial the chi2 and lambda. */
+int Optimizer_last_trace(double* solve_ini_chi2, double* solve_chi2, int solve_cap, int* n_solves,
+                         double* trial_chi2, double* trial_lambda, int trial_cap, int* n_trials);
+/* host milliseconds of the calling thread's last run: [total, structure build] */
+int Optimizer_last_timings(double* ms2);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,894 @@
+/*
+ * ba.c -- TEST INFRASTRUCTURE ONLY (parity oracle).
+ *
+ * Restatement of ORB_SLAM2::Optimizer::LocalBundleAdjustment (reference
+ * src/Optimizer.cc:453-778) and the g2o pieces it runs on:
+ *   SE3Quat (Thirdparty/g2o/g2o/types/se3quat.h: ctor 58-60, operator* 92-98,
+ *     map 217-220, exp 223-257, normalizeRotation 280-285) with Eigen 3
+ *     Quaterniond semantics (from-matrix, toRotationMatrix, _transformVector,
+ *     scalar quaternion product);
+ *   EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ (types_six_dof_expmap.h:80-141,
+ *     .cpp:103-234; the stereo cam_project's float invz and float bf*invz);
+ *   BaseBinaryEdge::constructQuadraticForm (base_binary_edge.hpp:55-120),
+ *     BaseEdge::chi2 / robustInformation (base_edge.h:58-61, 96-102),
+ *     RobustKernelHuber::robustify (robust_kernel_impl.cpp:78-91);
+ *   BlockSolver<6,3> buildStructure/buildSystem/setLambda/solve
+ *     (block_solver.hpp:142-604), SparseOptimizer active set / index map /
+ *     update / push-pop (sparse_optimizer.cpp:61-114, 166-267, 354-435),
+ *     OptimizationAlgorithmLevenberg::solve / computeLambdaInit / computeScale
+ *     (optimization_algorithm_levenberg.cpp:59-189);
+ *   Converter::toSE3Quat / toCvMat (Converter.cc:37-68).
+ *
+ * Choices where the reference's arithmetic is unpinned (Eigen):
+ *   - every accumulation that g2o/Eigen performs as a running "+=" over edges,
+ *     landmarks or vector entries is evaluated in the CANONICAL order below
+ *     (ora_csum: 64-wide pairwise tree, recursively), identically on the GPU;
+ *   - the pose system is factorised by a dense right-looking LDL^T on the
+ *     upper triangle in natural pose order (SimplicialLDLT+AMD in the
+ *     reference); failure = an exactly zero pivot, like Eigen's LDLT;
+ *   - sin/cos in SE3Quat::exp use ora_det_sincos (sim3.c); pow(theta,3) in
+ *     exp and pow(2*rho-1,3) in the LM step are (a*a)*a;
+ *   - small fixed-size products sum their terms left to right.
+ * Map points are never isBad() inside the call (the adapter's view).
+ */
+#include "orb_oracle.h"
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---- canonical reduction ---------------------------------------------- */
+/* Sum of v[0..n) (destroys v): split into chunks of 64, reduce each chunk by
+ * the tree a[i] += a[i+off] for off = 32,16,..,1 (zero padded), recurse on the
+ * chunk sums.  This is exactly a wave64 shuffle-down reduction per level. */
+double ora_csum(double* v, int n)
+{
+    if (n <= 0) return 0.0;
+    while (n > 1) {
+        int m = (n + 63) / 64;
+        for (int c = 0; c < m; c++) {
+            double a[64];
+            for (int i = 0; i < 64; i++) a[i] = (c * 64 + i < n) ? v[c * 64 + i] : 0.0;
+            for (int off = 32; off >= 1; off >>= 1)
+                for (int i = 0; i < off; i++) a[i] += a[i + off];
+            v[c] = a[0];
+        }
+        n = m;
+    }
+    return v[0];
+}
+
+/* ---- SE3Quat ------------------------------------------------------------ */
+typedef struct { double q[4]; double t[3]; } se3q; /* q = (x, y, z, w) like Eigen coeffs() */
+
+static void quat_normalize(double* q)
+{
+    double z = ((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3];
+    if (z > 0) {
+        double n = sqrt(z);
+        for (int i = 0; i < 4; i++) q[i] = q[i] / n;
+    }
+}
+
+static void se3_normalize(se3q* T) /* normalizeRotation */
+{
+    if (T->q[3] < 0)
+        for (int i = 0; i < 4; i++) T->q[i] *= -1;
+    quat_normalize(T->q);
+}
+
+static void quat_from_R(const double* m, double* q) /* Quaterniond(const Matrix3d&) */
+{
+    double t = (m[0] + m[4]) + m[8];
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (m[7] - m[5]) * t;
+        q[1] = (m[2] - m[6]) * t;
+        q[2] = (m[3] - m[1]) * t;
+    } else {
+        int i = 0;
+        if (m[4] > m[0]) i = 1;
+        if (m[8] > m[i * 4]) i = 2;
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(((m[i * 4] - m[j * 4]) - m[k * 4]) + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * t;
+        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
+        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
+    }
+}
+
+static void quat_to_R(const double* q, double* R) /* toRotationMatrix */
+{
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;         R[2] = txz + twy;
+    R[3] = txy + twz;         R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.0 - (txx + tyy);
+}
+
+static void cross3(const double* a, const double* b, double* c)
+{
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+static void quat_rotate(const double* q, const double* v, double* out) /* _transformVector */
+{
+    double uv[3], c[3];
+    cross3(q, v, uv);
+    for (int i = 0; i < 3; i++) uv[i] += uv[i];
+    cross3(q, uv, c);
+    for (int i = 0; i < 3; i++) out[i] = (v[i] + q[3] * uv[i]) + c[i];
+}
+
+static void quat_mul(const double* a, const double* b, double* o) /* quat_product (scalar path) */
+{
+    double r[4];
+    r[3] = ((a[3] * b[3] - a[0] * b[0]) - a[1] * b[1]) - a[2] * b[2];
+    r[0] = ((a[3] * b[0] + a[0] * b[3]) + a[1] * b[2]) - a[2] * b[1];
+    r[1] = ((a[3] * b[1] + a[1] * b[3]) + a[2] * b[0]) - a[0] * b[2];
+    r[2] = ((a[3] * b[2] + a[2] * b[3]) + a[0] * b[1]) - a[1] * b[0];
+    memcpy(o, r, sizeof(r));
+}
+
+static void se3_map(const se3q* T, const double* X, double* out) /* map */
+{
+    double r[3];
+    quat_rotate(T->q, X, r);
+    for (int i = 0; i < 3; i++) out[i] = r[i] + T->t[i];
+}
+
+static void se3_mul(const se3q* a, const se3q* b, se3q* o) /* operator* */
+{
+    se3q r;
+    double rt[3];
+    quat_rotate(a->q, b->t, rt);
+    for (int i = 0; i < 3; i++) r.t[i] = a->t[i] + rt[i];
+    quat_mul(a->q, b->q, r.q);
+    se3_normalize(&r);
+    *o = r;
+}
+
+static void mat3_mul(const double* A, const double* B, double* C)
+{
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            C[i * 3 + j] = (A[i * 3] * B[j] + A[i * 3 + 1] * B[3 + j]) + A[i * 3 + 2] * B[6 + j];
+}
+
+static void se3_exp(const double* upd, se3q* out) /* SE3Quat::exp */
+{
+    const double* w = upd;
+    const double* u = upd + 3;
+    double theta = sqrt((w[0] * w[0] + w[1] * w[1]) + w[2] * w[2]);
+    double Om[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+    double Om2[9], R[9], V[9];
+    mat3_mul(Om, Om, Om2);
+    if (theta < 0.00001) {
+        for (int i = 0; i < 9; i++) R[i] = (((i % 4) == 0 ? 1.0 : 0.0) + Om[i]) + Om2[i];
+        memcpy(V, R, sizeof(R));
+    } else {
+        double s, c;
+        ora_det_sincos(theta, &s, &c);
+        const double a = s / theta, b = (1 - c) / (theta * theta);
+        const double cc = (theta - s) / ((theta * theta) * theta);
+        for (int i = 0; i < 9; i++) {
+            const double I = (i % 4) == 0 ? 1.0 : 0.0;
+            R[i] = (I + a * Om[i]) + b * Om2[i];
+            V[i] = (I + b * Om[i]) + cc * Om2[i];
+        }
+    }
+    quat_from_R(R, out->q);
+    for (int i = 0; i < 3; i++) out->t[i] = (V[i * 3] * u[0] + V[i * 3 + 1] * u[1]) + V[i * 3 + 2] * u[2];
+    se3_normalize(out);
+}
+
+static void se3_from_Tcw(const float* T, se3q* o) /* Converter::toSE3Quat */
+{
+    double R[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) R[r * 3 + c] = (double)T[r * 4 + c];
+    quat_from_R(R, o->q);
+    for (int r = 0; r < 3; r++) o->t[r] = (double)T[r * 4 + 3];
+    se3_normalize(o);
+}
+
+static void se3_to_Tcw(const se3q* s, float* T) /* Converter::toCvMat(SE3Quat) */
+{
+    double R[9];
+    quat_to_R(s->q, R);
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) T[r * 4 + c] = (float)R[r * 3 + c];
+        T[r * 4 + 3] = (float)s->t[r];
+    }
+    T[12] = T[13] = T[14] = 0.f;
+    T[15] = 1.f;
+}
+
+/* ---- edges ---------------------------------------------------------------- */
+typedef struct {
+    int pt, kf, stereo;
+    double obs[3], info, fx, fy, cx, cy, bf;
+    double delta, dsqr;   /* Huber, delta = (double)(float)sqrt(th) */
+    int robust, level;
+    double err[3];        /* _error as last computed */
+} ba_edge;
+
+/* computeError: EdgeSE3ProjectXYZ (h:94-99) / EdgeStereoSE3ProjectXYZ (h:126-131) */
+static void edge_error(ba_edge* e, const se3q* T, const double* X)
+{
+    double p[3];
+    se3_map(T, X, p);
+    if (!e->stereo) {
+        const double px = p[0] / p[2], py = p[1] / p[2];
+        e->err[0] = e->obs[0] - (px * e->fx + e->cx);
+        e->err[1] = e->obs[1] - (py * e->fy + e->cy);
+        e->err[2] = 0;
+    } else {
+        const float invz = (float)(1.0 / p[2]);
+        const float bf = (float)e->bf;
+        const double u = (p[0] * (double)invz) * e->fx + e->cx;
+        const double v = (p[1] * (double)invz) * e->fy + e->cy;
+        e->err[0] = e->obs[0] - u;
+        e->err[1] = e->obs[1] - v;
+        e->err[2] = e->obs[2] - (u - (double)(bf * invz));
+    }
+}
+
+static double edge_chi2(const ba_edge* e)
+{
+    const int D = e->stereo ? 3 : 2;
+    double s = 0;
+    for (int j = 0; j < D; j++) s += e->err[j] * (e->info * e->err[j]);
+    return s;
+}
+
+static void huber(const ba_edge* e, double chi, double* rho0, double* rho1)
+{
+    if (chi <= e->dsqr) {
+        *rho0 = chi;
+        *rho1 = 1.;
+    } else {
+        const double sq = sqrt(chi);
+        *rho0 = (2 * sq) * e->delta - e->dsqr;
+        *rho1 = e->delta / sq;
+    }
+}
+
+static double edge_robust_chi2(const ba_edge* e)
+{
+    double c = edge_chi2(e), r0, r1;
+    if (!e->robust) return c;
+    huber(e, c, &r0, &r1);
+    return r0;
+}
+
+static int edge_depth_positive(const ba_edge* e, const se3q* T, const double* X)
+{
+    double p[3];
+    se3_map(T, X, p);
+    return p[2] > 0.0;
+}
+
+/* linearizeOplus (.cpp:103-147 mono, 188-234 stereo): A = d e / d point (Dx3), B = d e / d pose (Dx6) */
+static void edge_jacobians(const ba_edge* e, const se3q* T, const double* X, double* A, double* B)
+{
+    double p[3], R[9];
+    se3_map(T, X, p);
+    quat_to_R(T->q, R);
+    const double x = p[0], y = p[1], z = p[2], z_2 = z * z;
+    const double fx = e->fx, fy = e->fy;
+    if (!e->stereo) {
+        double tmp[6] = {fx, 0, ((-x) / z) * fx, 0, fy, ((-y) / z) * fy};
+        const double s = -1. / z;
+        double st[6];
+        for (int i = 0; i < 6; i++) st[i] = s * tmp[i];
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++)
+                A[i * 3 + j] = (st[i * 3] * R[j] + st[i * 3 + 1] * R[3 + j]) + st[i * 3 + 2] * R[6 + j];
+    } else {
+        const double bf = e->bf;
+        for (int j = 0; j < 3; j++) {
+            A[0 * 3 + j] = ((-fx) * R[0 * 3 + j]) / z + ((fx * x) * R[2 * 3 + j]) / z_2;
+            A[1 * 3 + j] = ((-fy) * R[1 * 3 + j]) / z + ((fy * y) * R[2 * 3 + j]) / z_2;
+            A[2 * 3 + j] = A[0 * 3 + j] - (bf * R[2 * 3 + j]) / z_2;
+        }
+    }
+    B[0] = ((x * y) / z_2) * fx;
+    B[1] = (-(1 + ((x * x) / z_2))) * fx;
+    B[2] = (y / z) * fx;
+    B[3] = (-1. / z) * fx;
+    B[4] = 0;
+    B[5] = (x / z_2) * fx;
+    B[6] = (1 + ((y * y) / z_2)) * fy;
+    B[7] = ((-x) * y / z_2) * fy;
+    B[8] = ((-x) / z) * fy;
+    B[9] = 0;
+    B[10] = (-1. / z) * fy;
+    B[11] = (y / z_2) * fy;
+    if (e->stereo) {
+        const double bf = e->bf;
+        B[12] = B[0] - (bf * y) / z_2;
+        B[13] = B[1] + (bf * x) / z_2;
+        B[14] = B[2];
+        B[15] = B[3];
+        B[16] = 0;
+        B[17] = B[5] - bf / z_2;
+    }
+}
+
+/* per-edge quadratic-form terms (constructQuadraticForm), summed canonically by vertex */
+typedef struct {
+    double Hpp[21];  /* upper triangle r<=c of B^T W B, row-major packed */
+    double bp[6];
+    double Hpl[18];  /* 6x3 */
+    double Hll[9];   /* full 3x3 */
+    double bl[3];
+} edge_terms;
+
+static void edge_quadratic(const ba_edge* e, const double* A, const double* B, int poseFree, edge_terms* o)
+{
+    const int D = e->stereo ? 3 : 2;
+    const double chi = edge_chi2(e);
+    double rho1 = 1.0, r0;
+    if (e->robust) huber(e, chi, &r0, &rho1);
+    const double w = e->robust ? rho1 * e->info : e->info;
+    double omr[3];
+    for (int k = 0; k < D; k++) {
+        omr[k] = -(e->info * e->err[k]);
+        if (e->robust) omr[k] *= rho1;
+    }
+    /* point (from) */
+    for (int r = 0; r < 3; r++) {
+        double s = 0;
+        for (int k = 0; k < D; k++) s += A[k * 3 + r] * omr[k];
+        o->bl[r] = s;
+        for (int c = 0; c < 3; c++) {
+            double h = 0;
+            for (int k = 0; k < D; k++) h += (A[k * 3 + r] * w) * A[k * 3 + c];
+            o->Hll[r * 3 + c] = h;
+        }
+    }
+    if (!poseFree) return;
+    int idx = 0;
+    for (int r = 0; r < 6; r++) {
+        double s = 0;
+        for (int k = 0; k < D; k++) s += B[k * 6 + r] * omr[k];
+        o->bp[r] = s;
+        for (int c = r; c < 6; c++) {
+            double h = 0;
+            for (int k = 0; k < D; k++) h += (B[k * 6 + r] * w) * B[k * 6 + c];
+            o->Hpp[idx++] = h;
+        }
+        for (int c = 0; c < 3; c++) {
+            double h = 0;
+            if (e->robust)   /* B^T * weightedOmega * A */
+                for (int k = 0; k < D; k++) h += (B[k * 6 + r] * w) * A[k * 3 + c];
+            else             /* B^T * AtO^T */
+                for (int k = 0; k < D; k++) h += B[k * 6 + r] * (A[k * 3 + c] * e->info);
+            o->Hpl[r * 3 + c] = h;
+        }
+    }
+}
+
+/* Eigen 3x3 inverse (cofactors, InverseImpl.h compute_inverse_size3) */
+static void inv3(const double* m, double* r)
+{
+#define M(i, j) m[(i) * 3 + (j)]
+#define COF(i, j) (M(((i) + 1) % 3, ((j) + 1) % 3) * M(((i) + 2) % 3, ((j) + 2) % 3) - \
+                   M(((i) + 1) % 3, ((j) + 2) % 3) * M(((i) + 2) % 3, ((j) + 1) % 3))
+    const double c0 = COF(0, 0), c1 = COF(1, 0), c2 = COF(2, 0);
+    const double det = (c0 * M(0, 0) + c1 * M(1, 0)) + c2 * M(2, 0);
+    const double invdet = 1.0 / det;
+    r[0] = c0 * invdet; r[1] = c1 * invdet; r[2] = c2 * invdet;
+    r[3] = COF(0, 1) * invdet; r[4] = COF(1, 1) * invdet; r[5] = COF(2, 1) * invdet;
+    r[6] = COF(0, 2) * invdet; r[7] = COF(1, 2) * invdet; r[8] = COF(2, 2) * invdet;
+#undef COF
+#undef M
+}
+
+/* Dense LDL^T on the upper triangle (row-major n x n, only r<=c read), in place.
+ * Returns 0 on an exactly zero pivot. */
+int ora_ldlt_solve(double* S, int n, const double* b, double* x)
+{
+    double* l = (double*)malloc(sizeof(double) * (n + 1));
+    for (int k = 0; k < n; k++) {
+        const double d = S[k * n + k];
+        if (d == 0.0) { free(l); return 0; }
+        for (int i = k + 1; i < n; i++) l[i] = S[k * n + i] / d;
+        for (int i = k + 1; i < n; i++)
+            for (int j = i; j < n; j++) S[i * n + j] -= l[i] * S[k * n + j];
+        for (int i = k + 1; i < n; i++) S[k * n + i] = l[i];   /* row k now holds L^T */
+    }
+    double* y = (double*)malloc(sizeof(double) * (n + 1));
+    memcpy(y, b, sizeof(double) * n);
+    for (int k = 0; k < n; k++)          /* L y = b (column sweep) */
+        for (int i = k + 1; i < n; i++) y[i] -= S[k * n + i] * y[k];
+    for (int k = 0; k < n; k++) y[k] = y[k] / S[k * n + k];
+    for (int k = n - 1; k >= 0; k--)     /* L^T x = z (column sweep) */
+        for (int i = 0; i < k; i++) y[i] -= S[i * n + k] * y[k];
+    memcpy(x, y, sizeof(double) * n);
+    free(y);
+    free(l);
+    return 1;
+}
+
+/* ---- the optimizer -------------------------------------------------------- */
+typedef struct {
+    int nkf, npt, ne;
+    se3q *T, *Tbak;
+    double *X, *Xbak;
+    int *kfFixed, *kfId, *ptId;
+    ba_edge* E;
+    /* active structure */
+    int nE, nP, nL;          /* active edges, free poses, active points */
+    int *aE;                 /* active edge list (edge order) */
+    int *poseIdx, *ptIdx;    /* kf -> pose index or -1; pt -> landmark index or -1 */
+    int *poseOf, *ptOf;      /* pose index -> kf; landmark -> pt */
+    int *peStart, *peList;   /* per pose: active edges (edge order) */
+    int *leStart, *leList;   /* per landmark: active edges (edge order) */
+    /* system */
+    edge_terms* terms;       /* per active edge */
+    double *Hpp, *bp, *Hll, *bl;   /* Hpp 21 per pose, Hll 9 per landmark */
+    double *x, *b;           /* vector: poses (6 nP) then landmarks (3 nL) */
+    double lambda, ni;
+    int nBad;
+    double* scratch;
+    int scratchN;
+    ora_ba_trace* trace;
+} ba_ctx;
+
+static double* scratch(ba_ctx* c, int n)
+{
+    if (n > c->scratchN) {
+        free(c->scratch);
+        c->scratch = (double*)malloc(sizeof(double) * (n + 64));
+        c->scratchN = n;
+    }
+    return c->scratch;
+}
+
+static const int* g_keys;
+static int cmp_idx(const void* a, const void* b)
+{
+    int ka = g_keys[*(const int*)a], kb = g_keys[*(const int*)b];
+    return ka < kb ? -1 : ka > kb;
+}
+
+/* initializeOptimization(level) + buildIndexMapping + BlockSolver::buildStructure */
+static void build_structure(ba_ctx* c, int level)
+{
+    int* kfAct = (int*)calloc(c->nkf, sizeof(int));
+    int* ptAct = (int*)calloc(c->npt, sizeof(int));
+    c->nE = 0;
+    for (int i = 0; i < c->ne; i++)
+        if (c->E[i].level == level) {   /* allVerticesFixed never holds: points are free */
+            c->aE[c->nE++] = i;
+            kfAct[c->E[i].kf] = 1;
+            ptAct[c->E[i].pt] = 1;
+        }
+    /* poses: active, not fixed, sorted by id; landmarks: active, sorted by id */
+    int* ord = (int*)malloc(sizeof(int) * (c->nkf + c->npt + 1));
+    int n = 0;
+    for (int k = 0; k < c->nkf; k++)
+        if (kfAct[k] && !c->kfFixed[k]) ord[n++] = k;
+    g_keys = c->kfId;
+    qsort(ord, n, sizeof(int), cmp_idx);
+    c->nP = n;
+    for (int k = 0; k < c->nkf; k++) c->poseIdx[k] = -1;
+    for (int i = 0; i < n; i++) { c->poseOf[i] = ord[i]; c->poseIdx[ord[i]] = i; }
+    n = 0;
+    for (int p = 0; p < c->npt; p++)
+        if (ptAct[p]) ord[n++] = p;
+    g_keys = c->ptId;
+    qsort(ord, n, sizeof(int), cmp_idx);
+    c->nL = n;
+    for (int p = 0; p < c->npt; p++) c->ptIdx[p] = -1;
+    for (int i = 0; i < n; i++) { c->ptOf[i] = ord[i]; c->ptIdx[ord[i]] = i; }
+    free(ord);
+    /* CSR edge lists in active-edge order */
+    memset(c->peStart, 0, sizeof(int) * (c->nP + 1));
+    memset(c->leStart, 0, sizeof(int) * (c->nL + 1));
+    for (int a = 0; a < c->nE; a++) {
+        const ba_edge* e = &c->E[c->aE[a]];
+        if (c->poseIdx[e->kf] >= 0) c->peStart[c->poseIdx[e->kf] + 1]++;
+        c->leStart[c->ptIdx[e->pt] + 1]++;
+    }
+    for (int i = 0; i < c->nP; i++) c->peStart[i + 1] += c->peStart[i];
+    for (int i = 0; i < c->nL; i++) c->leStart[i + 1] += c->leStart[i];
+    int* fp = (int*)malloc(sizeof(int) * (c->nP + 1));
+    int* fl = (int*)malloc(sizeof(int) * (c->nL + 1));
+    memcpy(fp, c->peStart, sizeof(int) * (c->nP + 1));
+    memcpy(fl, c->leStart, sizeof(int) * (c->nL + 1));
+    for (int a = 0; a < c->nE; a++) {
+        const ba_edge* e = &c->E[c->aE[a]];
+        if (c->poseIdx[e->kf] >= 0) c->peList[fp[c->poseIdx[e->kf]]++] = a;
+        c->leList[fl[c->ptIdx[e->pt]]++] = a;
+    }
+    free(fp);
+    free(fl);
+    free(kfAct);
+    free(ptAct);
+    memset(c->x, 0, sizeof(double) * (6 * c->nP + 3 * c->nL + 1));
+}
+
+static void compute_active_errors(ba_ctx* c)
+{
+    for (int a = 0; a < c->nE; a++) {
+        ba_edge* e = &c->E[c->aE[a]];
+        edge_error(e, &c->T[e->kf], &c->X[3 * e->pt]);
+    }
+}
+
+static double active_robust_chi2(ba_ctx* c)
+{
+    double* v = scratch(c, c->nE);
+    for (int a = 0; a < c->nE; a++) v[a] = edge_robust_chi2(&c->E[c->aE[a]]);
+    return ora_csum(v, c->nE);
+}
+
+/* BlockSolver::buildSystem */
+static void build_system(ba_ctx* c)
+{
+    for (int a = 0; a < c->nE; a++) {
+        const ba_edge* e = &c->E[c->aE[a]];
+        double A[9], B[18];
+        edge_jacobians(e, &c->T[e->kf], &c->X[3 * e->pt], A, B);
+        edge_quadratic(e, A, B, c->poseIdx[e->kf] >= 0, &c->terms[a]);
+    }
+    int maxn = 1;
+    for (int i = 0; i < c->nP; i++) if (c->peStart[i + 1] - c->peStart[i] > maxn) maxn = c->peStart[i + 1] - c->peStart[i];
+    double* v = scratch(c, maxn);
+    for (int i = 0; i < c->nP; i++) {
+        const int s = c->peStart[i], n = c->peStart[i + 1] - s;
+        for (int q = 0; q < 21; q++) {
+            for (int j = 0; j < n; j++) v[j] = c->terms[c->peList[s + j]].Hpp[q];
+            c->Hpp[21 * i + q] = ora_csum(v, n);
+        }
+        for (int q = 0; q < 6; q++) {
+            for (int j = 0; j < n; j++) v[j] = c->terms[c->peList[s + j]].bp[q];
+            c->bp[6 * i + q] = ora_csum(v, n);
+        }
+    }
+    for (int i = 0; i < c->nL; i++) {
+        const int s = c->leStart[i], n = c->leStart[i + 1] - s;
+        double w[64];
+        double* vv = n <= 64 ? w : scratch(c, n);
+        for (int q = 0; q < 9; q++) {
+            for (int j = 0; j < n; j++) vv[j] = c->terms[c->leList[s + j]].Hll[q];
+            c->Hll[9 * i + q] = ora_csum(vv, n);
+        }
+        for (int q = 0; q < 3; q++) {
+            for (int j = 0; j < n; j++) vv[j] = c->terms[c->leList[s + j]].bl[q];
+            c->bl[3 * i + q] = ora_csum(vv, n);
+        }
+    }
+    for (int i = 0; i < c->nP; i++)
+        for (int q = 0; q < 6; q++) c->b[6 * i + q] = c->bp[6 * i + q];
+    for (int i = 0; i < c->nL; i++)
+        for (int q = 0; q < 3; q++) c->b[6 * c->nP + 3 * i + q] = c->bl[3 * i + q];
+}
+
+static const int DIAG21[6] = {0, 6, 11, 15, 18, 20};
+
+static double lambda_init(ba_ctx* c)
+{
+    double m = 0.;
+    for (int i = 0; i < c->nP; i++)
+        for (int j = 0; j < 6; j++) m = fmax(fabs(c->Hpp[21 * i + DIAG21[j]]), m);
+    for (int i = 0; i < c->nL; i++)
+        for (int j = 0; j < 3; j++) m = fmax(fabs(c->Hll[9 * i + 4 * j]), m);
+    return 1e-5 * m;
+}
+
+/* BlockSolver::solve with lambda on the diagonals (setLambda .. restoreDiagonal) */
+static int schur_solve(ba_ctx* c, double lambda)
+{
+    const int nP = c->nP, nL = c->nL, n = 6 * nP;
+    double* Dinv = (double*)malloc(sizeof(double) * 9 * (nL + 1));
+    double* db = (double*)malloc(sizeof(double) * 3 * (nL + 1));
+    /* per active edge with a free pose: BDinv (6x3) and B*db (6) */
+    double* E = (double*)malloc(sizeof(double) * 18 * (c->nE + 1));
+    double* cb = (double*)malloc(sizeof(double) * 6 * (c->nE + 1));
+    for (int l = 0; l < nL; l++) {
+        double D[9];
+        memcpy(D, &c->Hll[9 * l], sizeof(D));
+        for (int j = 0; j < 3; j++) D[4 * j] += lambda;
+        inv3(D, &Dinv[9 * l]);
+        const double* Di = &Dinv[9 * l];
+        const double* bl = &c->bl[3 * l];
+        for (int r = 0; r < 3; r++) db[3 * l + r] = (Di[r * 3] * bl[0] + Di[r * 3 + 1] * bl[1]) + Di[r * 3 + 2] * bl[2];
+        for (int j = c->leStart[l]; j < c->leStart[l + 1]; j++) {
+            const int a = c->leList[j];
+            if (c->poseIdx[c->E[c->aE[a]].kf] < 0) continue;
+            const double* Bi = c->terms[a].Hpl;
+            for (int r = 0; r < 6; r++) {
+                for (int k = 0; k < 3; k++)
+                    E[18 * a + r * 3 + k] = (Bi[r * 3] * Di[k] + Bi[r * 3 + 1] * Di[3 + k]) + Bi[r * 3 + 2] * Di[6 + k];
+                cb[6 * a + r] = (Bi[r * 3] * db[3 * l] + Bi[r * 3 + 1] * db[3 * l + 1]) + Bi[r * 3 + 2] * db[3 * l + 2];
+            }
+        }
+    }
+    /* S (upper) and b_schur: terms in landmark order */
+    double* S = (double*)calloc((size_t)n * n + 1, sizeof(double));
+    double* bs = (double*)malloc(sizeof(double) * (n + 1));
+    /* edge of landmark l to pose i (at most one: keyframes observe a point once) */
+    int maxT = 1;
+    double* v = (double*)malloc(sizeof(double) * (nL + 1));
+    (void)maxT;
+    int* ePL = (int*)malloc(sizeof(int) * ((size_t)nP * nL + 1));
+    for (size_t q = 0; q < (size_t)nP * nL; q++) ePL[q] = -1;
+    for (int l = 0; l < nL; l++)
+        for (int j = c->leStart[l]; j < c->leStart[l + 1]; j++) {
+            const int a = c->leList[j];
+            const int pi = c->poseIdx[c->E[c->aE[a]].kf];
+            if (pi >= 0) ePL[(size_t)pi * nL + l] = a;
+        }
+    for (int i1 = 0; i1 < nP; i1++)
+        for (int i2 = i1; i2 < nP; i2++)
+            for (int r = 0; r < 6; r++)
+                for (int cc = (i1 == i2 ? r : 0); cc < 6; cc++) {
+                    int m = 0;
+                    for (int l = 0; l < nL; l++) {
+                        const int a1 = ePL[(size_t)i1 * nL + l], a2 = ePL[(size_t)i2 * nL + l];
+                        if (a1 < 0 || a2 < 0) continue;
+                        const double* Ei = &E[18 * a1 + r * 3];
+                        const double* Bj = &c->terms[a2].Hpl[cc * 3];
+                        v[m++] = (Ei[0] * Bj[0] + Ei[1] * Bj[1]) + Ei[2] * Bj[2];
+                    }
+                    double h = 0;
+                    if (i1 == i2) {
+                        h = c->Hpp[21 * i1 + DIAG21[r] + (cc - r)];
+                        if (cc == r) h += lambda;
+                    }
+                    S[(size_t)(6 * i1 + r) * n + 6 * i2 + cc] = h - ora_csum(v, m);
+                }
+    for (int i = 0; i < nP; i++)
+        for (int r = 0; r < 6; r++) {
+            int m = 0;
+            for (int l = 0; l < nL; l++) {
+                const int a = ePL[(size_t)i * nL + l];
+                if (a >= 0) v[m++] = cb[6 * a + r];
+            }
+            bs[6 * i + r] = c->bp[6 * i + r] - ora_csum(v, m);
+        }
+    double* xp = (double*)malloc(sizeof(double) * (n + 1));
+    int ok = n == 0 ? 1 : ora_ldlt_solve(S, n, bs, xp);
+    if (ok) {
+        memcpy(c->x, xp, sizeof(double) * n);
+        /* xl = Dinv (bl - sum_i B_i^T xp_i); rightMultiply over the landmark's blocks in pose order */
+        for (int l = 0; l < nL; l++) {
+            double cl[3] = {c->bl[3 * l], c->bl[3 * l + 1], c->bl[3 * l + 2]};
+            for (int i = 0; i < nP; i++) {
+                const int a = ePL[(size_t)i * nL + l];
+                if (a < 0) continue;
+                const double* B = c->terms[a].Hpl;
+                const double* cp = &xp[6 * i];
+                for (int k = 0; k < 3; k++) {
+                    double s = 0;
+                    for (int r = 0; r < 6; r++) s += B[r * 3 + k] * (-cp[r]);
+                    cl[k] += s;
+                }
+            }
+            const double* Di = &Dinv[9 * l];
+            for (int r = 0; r < 3; r++)
+                c->x[6 * nP + 3 * l + r] = (Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1]) + Di[r * 3 + 2] * cl[2];
+        }
+    }
+    free(xp); free(ePL); free(v); free(S); free(bs); free(E); free(cb); free(Dinv); free(db);
+    return ok;
+}
+
+static void push_state(ba_ctx* c)
+{
+    memcpy(c->Tbak, c->T, sizeof(se3q) * c->nkf);
+    memcpy(c->Xbak, c->X, sizeof(double) * 3 * c->npt);
+}
+
+static void pop_state(ba_ctx* c)
+{
+    memcpy(c->T, c->Tbak, sizeof(se3q) * c->nkf);
+    memcpy(c->X, c->Xbak, sizeof(double) * 3 * c->npt);
+}
+
+static void apply_update(ba_ctx* c) /* SparseOptimizer::update in _ivMap order */
+{
+    for (int i = 0; i < c->nP; i++) {
+        se3q d, r;
+        se3_exp(&c->x[6 * i], &d);
+        se3_mul(&d, &c->T[c->poseOf[i]], &r);
+        c->T[c->poseOf[i]] = r;
+    }
+    for (int l = 0; l < c->nL; l++)
+        for (int k = 0; k < 3; k++) c->X[3 * c->ptOf[l] + k] += c->x[6 * c->nP + 3 * l + k];
+}
+
+static double compute_scale(ba_ctx* c)
+{
+    const int n = 6 * c->nP + 3 * c->nL;
+    double* v = scratch(c, n);
+    for (int j = 0; j < n; j++) v[j] = c->x[j] * (c->lambda * c->x[j] + c->b[j]);
+    return ora_csum(v, n);
+}
+
+static int stop_set(const volatile int* stop) { return stop && *stop; }
+
+enum { SOLVE_OK = 0, SOLVE_TERMINATE = 1 };
+
+/* OptimizationAlgorithmLevenberg::solve */
+static int lm_solve(ba_ctx* c, int iteration, const volatile int* stop)
+{
+    compute_active_errors(c);
+    double currentChi = active_robust_chi2(c);
+    const double iniChi = currentChi;
+    build_system(c);
+    if (iteration == 0) {
+        c->lambda = lambda_init(c);
+        c->ni = 2;
+        c->nBad = 0;
+    }
+    double rho = 0;
+    int qmax = 0;
+    do {
+        push_state(c);
+        const int ok2 = schur_solve(c, c->lambda);
+        apply_update(c);
+        compute_active_errors(c);
+        double tempChi = active_robust_chi2(c);
+        if (!ok2) tempChi = DBL_MAX;
+        rho = currentChi - tempChi;
+        double scale = compute_scale(c);
+        scale += 1e-3;
+        rho /= scale;
+        if (rho > 0 && isfinite(tempChi)) {
+            const double a3 = 2 * rho - 1;
+            double alpha = 1. - (a3 * a3) * a3;
+            alpha = fmin(alpha, 2. / 3.);
+            const double scaleFactor = fmax(1. / 3., alpha);
+            c->lambda *= scaleFactor;
+            c->ni = 2;
+            currentChi = tempChi;
+        } else {
+            c->lambda *= c->ni;
+            c->ni *= 2;
+            pop_state(c);
+        }
+        qmax++;
+        if (c->trace && c->trace->n_trials < ORA_BA_TRACE_MAX) {
+            ora_ba_trace* t = c->trace;
+            t->trial_chi2[t->n_trials] = tempChi;
+            t->trial_lambda[t->n_trials] = c->lambda;
+            t->n_trials++;
+        }
+    } while (rho < 0 && qmax < 10 && !stop_set(stop));
+    if (c->trace && c->trace->n_solves < ORA_BA_TRACE_MAX) {
+        c->trace->solve_ini_chi2[c->trace->n_solves] = iniChi;
+        c->trace->solve_chi2[c->trace->n_solves] = currentChi;
+        c->trace->n_solves++;
+    }
+    if (qmax == 10 || rho == 0) return SOLVE_TERMINATE;
+    if ((iniChi - currentChi) * 1e3 < iniChi) c->nBad++;
+    else c->nBad = 0;
+    if (c->nBad >= 3) return SOLVE_TERMINATE;
+    return SOLVE_OK;
+}
+
+/* SparseOptimizer::optimize(iterations) */
+static int optimize(ba_ctx* c, int iterations, const volatile int* stop)
+{
+    int it = 0, ok = 1;
+    for (int i = 0; i < iterations && !stop_set(stop) && ok; i++) {
+        ok = lm_solve(c, i, stop) == SOLVE_OK;
+        it++;
+    }
+    return it;
+}
+
+int ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_result* R, ora_ba_trace* trace)
+{
+    ba_ctx C;
+    memset(&C, 0, sizeof(C));
+    ba_ctx* c = &C;
+    c->nkf = P->n_kf; c->npt = P->n_pt; c->ne = P->n_edge;
+    c->trace = trace;
+    if (trace) memset(trace, 0, sizeof(*trace));
+    c->T = (se3q*)malloc(sizeof(se3q) * (c->nkf + 1));
+    c->Tbak = (se3q*)malloc(sizeof(se3q) * (c->nkf + 1));
+    c->X = (double*)malloc(sizeof(double) * 3 * (c->npt + 1));
+    c->Xbak = (double*)malloc(sizeof(double) * 3 * (c->npt + 1));
+    c->kfFixed = (int*)malloc(sizeof(int) * (c->nkf + 1));
+    c->kfId = (int*)malloc(sizeof(int) * (c->nkf + 1));
+    c->ptId = (int*)malloc(sizeof(int) * (c->npt + 1));
+    c->E = (ba_edge*)calloc(c->ne + 1, sizeof(ba_edge));
+    c->aE = (int*)malloc(sizeof(int) * (c->ne + 1));
+    c->poseIdx = (int*)malloc(sizeof(int) * (c->nkf + 1));
+    c->poseOf = (int*)malloc(sizeof(int) * (c->nkf + 1));
+    c->ptIdx = (int*)malloc(sizeof(int) * (c->npt + 1));
+    c->ptOf = (int*)malloc(sizeof(int) * (c->npt + 1));
+    c->peStart = (int*)malloc(sizeof(int) * (c->nkf + 2));
+    c->leStart = (int*)malloc(sizeof(int) * (c->npt + 2));
+    c->peList = (int*)malloc(sizeof(int) * (c->ne + 1));
+    c->leList = (int*)malloc(sizeof(int) * (c->ne + 1));
+    c->terms = (edge_terms*)calloc(c->ne + 1, sizeof(edge_terms));
+    c->Hpp = (double*)malloc(sizeof(double) * 21 * (c->nkf + 1));
+    c->bp = (double*)malloc(sizeof(double) * 6 * (c->nkf + 1));
+    c->Hll = (double*)malloc(sizeof(double) * 9 * (c->npt + 1));
+    c->bl = (double*)malloc(sizeof(double) * 3 * (c->npt + 1));
+    c->x = (double*)calloc(6 * c->nkf + 3 * c->npt + 1, sizeof(double));
+    c->b = (double*)calloc(6 * c->nkf + 3 * c->npt + 1, sizeof(double));
+
+    for (int k = 0; k < c->nkf; k++) {
+        se3_from_Tcw(&P->kf_Tcw[16 * k], &c->T[k]);
+        c->kfId[k] = P->kf_id[k];
+        c->kfFixed[k] = !P->kf_local[k] || P->kf_id[k] == 0;
+    }
+    for (int p = 0; p < c->npt; p++) {
+        c->ptId[p] = P->pt_id[p];
+        for (int j = 0; j < 3; j++) c->X[3 * p + j] = (double)P->pt_pos[3 * p + j];
+    }
+    const float thMono = (float)sqrt(5.991), thStereo = (float)sqrt(7.815);
+    for (int i = 0; i < c->ne; i++) {
+        ba_edge* e = &c->E[i];
+        e->pt = P->edge_pt[i];
+        e->kf = P->edge_kf[i];
+        e->stereo = !(P->edge_obs[3 * i + 2] < 0);
+        for (int j = 0; j < 3; j++) e->obs[j] = (double)P->edge_obs[3 * i + j];
+        e->info = (double)P->edge_inv_sigma2[i];
+        const float* cam = &P->kf_cam[5 * e->kf];
+        e->fx = cam[0]; e->fy = cam[1]; e->cx = cam[2]; e->cy = cam[3]; e->bf = cam[4];
+        e->delta = (double)(e->stereo ? thStereo : thMono);
+        e->dsqr = e->delta * e->delta;
+        e->robust = 1;
+        e->level = 0;
+    }
+    /* outputs default to the inputs (early abort writes nothing back) */
+    memcpy(R->kf_Tcw, P->kf_Tcw, sizeof(float) * 16 * c->nkf);
+    memcpy(R->pt_pos, P->pt_pos, sizeof(float) * 3 * c->npt);
+    memset(R->edge_erase, 0, c->ne);
+    R->aborted = 0;
+    R->iterations[0] = R->iterations[1] = 0;
+    R->n_erased = 0;
+    if (stop_set(stop) || c->ne == 0) {
+        R->aborted = 1;
+        goto done;
+    }
+
+    build_structure(c, 0);
+    if (c->nP + c->nL > 0) R->iterations[0] = optimize(c, 5, stop);
+    if (!stop_set(stop)) {
+        for (int i = 0; i < c->ne; i++) {   /* Optimizer.cc:674-706 */
+            ba_edge* e = &c->E[i];
+            const double th = e->stereo ? 7.815 : 5.991;
+            if (edge_chi2(e) > th || !edge_depth_positive(e, &c->T[e->kf], &c->X[3 * e->pt])) e->level = 1;
+            e->robust = 0;
+        }
+        build_structure(c, 0);
+        if (c->nE > 0 && c->nP + c->nL > 0) R->iterations[1] = optimize(c, 10, stop);
+    }
+    for (int i = 0; i < c->ne; i++) {       /* Optimizer.cc:714-746 */
+        const ba_edge* e = &c->E[i];
+        const double th = e->stereo ? 7.815 : 5.991;
+        if (edge_chi2(e) > th || !edge_depth_positive(e, &c->T[e->kf], &c->X[3 * e->pt])) {
+            R->edge_erase[i] = 1;
+            R->n_erased++;
+        }
+    }
+    for (int k = 0; k < c->nkf; k++)
+        if (P->kf_local[k]) se3_to_Tcw(&c->T[k], &R->kf_Tcw[16 * k]);
+    for (int p = 0; p < c->npt; p++)
+        for (int j = 0; j < 3; j++) R->pt_pos[3 * p + j] = (float)c->X[3 * p + j];
+done:
+    free(c->T); free(c->Tbak); free(c->X); free(c->Xbak); free(c->kfFixed); free(c->kfId); free(c->ptId);
+    free(c->E); free(c->aE); free(c->poseIdx); free(c->poseOf); free(c->ptIdx); free(c->ptOf);
+    free(c->peStart); free(c->leStart); free(c->peList); free(c->leList); free(c->terms);
+    free(c->Hpp); free(c->bp); free(c->Hll); free(c->bl); free(c->x); free(c->b); free(c->scratch);
+    return 0;
+}

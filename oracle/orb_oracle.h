@@ -176,6 +176,40 @@ int   ora_sim3_iterate(ora_sim3* S, int nIterations, ora_rng* rng, int* bNoMore,
 void  ora_sim3_estimate(const ora_sim3* S, float* R, float* t, float* s);
 int   ora_sim3_iterations(const ora_sim3* S);
 
+
+/* ---- Local bundle adjustment (ba.c), reference Optimizer.cc:453-778 + g2o --- */
+typedef struct {
+    int n_kf;
+    const int32_t* kf_id;      /* KeyFrame::mnId (vertex id) */
+    const float* kf_Tcw;       /* n_kf x 16 row-major */
+    const uint8_t* kf_local;   /* 1 = lLocalKeyFrames (written back; fixed iff id 0), 0 = lFixedCameras */
+    const float* kf_cam;       /* n_kf x 5: fx fy cx cy bf */
+    int n_pt;
+    const int32_t* pt_id;      /* MapPoint::mnId */
+    const float* pt_pos;       /* n_pt x 3 */
+    int n_edge;                /* in the reference's creation order (map point, then observation order) */
+    const int32_t* edge_pt;
+    const int32_t* edge_kf;
+    const float* edge_obs;     /* n_edge x 3: u, v, uRight (uRight < 0 = monocular edge) */
+    const float* edge_inv_sigma2;
+} ora_ba_problem;
+typedef struct {
+    float* kf_Tcw;             /* n_kf x 16 (local keyframes updated) */
+    float* pt_pos;             /* n_pt x 3 */
+    uint8_t* edge_erase;       /* n_edge: vToErase membership */
+    int iterations[2];         /* optimize(5) / optimize(10) return values */
+    int n_erased, aborted;
+} ora_ba_result;
+#define ORA_BA_TRACE_MAX 256
+typedef struct {
+    int n_solves, n_trials;
+    double solve_ini_chi2[ORA_BA_TRACE_MAX], solve_chi2[ORA_BA_TRACE_MAX];
+    double trial_chi2[ORA_BA_TRACE_MAX], trial_lambda[ORA_BA_TRACE_MAX];
+} ora_ba_trace;
+double ora_csum(double* v, int n);
+int   ora_ldlt_solve(double* S, int n, const double* b, double* x);
+int   ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_result* R, ora_ba_trace* trace);
+
 #ifdef __cplusplus
 }
 #endif

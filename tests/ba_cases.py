@@ -1,0 +1,108 @@
+"""Local-BA-shaped problems (EuRoC MH_05 stereo).
+
+n_local local keyframes (the one with mnId 0 is fixed) + n_fixed fixed
+keyframes; n_pt map points, each observed by U{2..8} keyframes (at least one
+local); `stereo_frac` of the observations carry uRight; EuRoC intrinsics
+(fx=fy=435.2047, cx=367.4517, cy=252.2009, bf=47.9064).  Noise: poses 1 cm /
+0.5 deg, points 5 cm, pixels sigma = 1 x 1.2^octave, `outlier_frac` gross
+outliers (20 px).  Edge order mimics the reference: map points in list order,
+each point's observations in a per-point shuffled (pointer-map) order.
+"""
+import numpy as np
+
+EUROC = (435.2047, 435.2047, 367.4517, 252.2009, 47.9064)
+
+
+def _rot(rng, deg):
+    a = np.deg2rad(rng.normal(0, deg, 3))
+    th = np.linalg.norm(a)
+    if th < 1e-12:
+        return np.eye(3)
+    k = a / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def ba_problem(seed=0, n_local=15, n_fixed=15, n_pt=3000, stereo_frac=0.7, outlier_frac=0.05, obs_range=(2, 8),
+               cam=EUROC):
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = cam
+    nkf = n_local + n_fixed
+    # keyframes along a gently curving path, all looking roughly +z
+    Rwc, twc = [], []
+    for k in range(nkf):
+        Rwc.append(_rot(rng, 2.0))
+        twc.append(np.array([0.15 * k, 0.02 * np.sin(k), 0.05 * k]) + rng.normal(0, 0.02, 3))
+    Tcw_true = []
+    for R, t in zip(Rwc, twc):
+        T = np.eye(4)
+        T[:3, :3] = R.T
+        T[:3, 3] = -R.T @ t
+        Tcw_true.append(T)
+    # points in front of the middle of the path
+    Xw = np.stack([rng.uniform(-4, 9, n_pt), rng.uniform(-2.5, 2.5, n_pt), rng.uniform(3, 12, n_pt)], 1)
+    ids = rng.permutation(np.arange(1, nkf + 200))[:nkf]
+    local = np.zeros(nkf, np.uint8)
+    local[:n_local] = 1
+    ids[0] = 0                                   # the first local keyframe is the map origin (fixed)
+    edges_pt, edges_kf, obs, isig = [], [], [], []
+    lo, hi = obs_range
+    W, H = 2 * cx, 2 * cy
+
+    def visible(p, kf):
+        T = Tcw_true[kf]
+        Xc = T[:3, :3] @ Xw[p] + T[:3, 3]
+        if Xc[2] < 1.0:
+            return False
+        u, v = fx * Xc[0] / Xc[2] + cx, fy * Xc[1] / Xc[2] + cy
+        return 10 <= u < W - 10 and 10 <= v < H - 10
+
+    for p in range(n_pt):
+        while True:
+            vis = [kf for kf in range(nkf) if visible(p, kf)]
+            if len(vis) >= lo and any(local[kf] for kf in vis):
+                break
+            Xw[p] = [rng.uniform(-4, 9), rng.uniform(-2.5, 2.5), rng.uniform(3, 12)]
+        k = min(int(rng.integers(lo, hi + 1)), len(vis))
+        kfs = rng.choice(vis, k, replace=False)
+        if not local[kfs].any():
+            kfs[0] = rng.choice([kf for kf in vis if local[kf]])
+            kfs = np.unique(kfs)
+        rng.shuffle(kfs)
+        for kf in kfs:
+            T = Tcw_true[kf]
+            Xc = T[:3, :3] @ Xw[p] + T[:3, 3]
+            octv = int(rng.integers(0, 8))
+            s = 1.2 ** octv
+            u = fx * Xc[0] / Xc[2] + cx + rng.normal(0, s)
+            v = fy * Xc[1] / Xc[2] + cy + rng.normal(0, s)
+            ur = -1.0
+            if rng.random() < stereo_frac:
+                ur = u - bf / Xc[2] + rng.normal(0, s)
+            if rng.random() < outlier_frac:
+                a = rng.uniform(0, 2 * np.pi)
+                u += 20 * np.cos(a)
+                v += 20 * np.sin(a)
+                if ur >= 0:
+                    ur += 20 * np.cos(a)
+            if ur < 0 and ur != -1.0:
+                ur = 0.0
+            edges_pt.append(p)
+            edges_kf.append(kf)
+            obs.append((u, v, ur))
+            isig.append(np.float32(1.0) / np.float32(1.2) ** (2 * octv))
+    # noisy initial estimates (the fixed keyframes and the origin keep their true pose)
+    Tcw0 = np.zeros((nkf, 16), np.float32)
+    for k in range(nkf):
+        T = Tcw_true[k].copy()
+        if local[k] and ids[k] != 0:
+            T[:3, :3] = _rot(rng, 0.5) @ T[:3, :3]
+            T[:3, 3] += rng.normal(0, 0.01, 3)
+        Tcw0[k] = T.astype(np.float32).ravel()
+    X0 = (Xw + rng.normal(0, 0.05, Xw.shape)).astype(np.float32)
+    kcam = np.tile(np.array(cam, np.float32), (nkf, 1))
+    pt_ids = rng.permutation(np.arange(10, 10 + 4 * n_pt))[:n_pt].astype(np.int32)
+    return dict(kf_id=ids.astype(np.int32), kf_Tcw=Tcw0, kf_local=local, kf_cam=kcam, pt_id=pt_ids, pt_pos=X0,
+                edge_pt=np.array(edges_pt, np.int32), edge_kf=np.array(edges_kf, np.int32),
+                edge_obs=np.array(obs, np.float32), edge_inv_sigma2=np.array(isig, np.float32),
+                Tcw_true=np.array(Tcw_true), Xw_true=Xw)

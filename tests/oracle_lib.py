@@ -310,3 +310,44 @@ def new_rng(seed=1):
     g = (C.c_int32 * 40)()
     lib().ora_rng_seed(g, seed)
     return g
+
+
+class _BAProblem(C.Structure):
+    _fields_ = [("n_kf", C.c_int), ("kf_id", C.c_void_p), ("kf_Tcw", C.c_void_p), ("kf_local", C.c_void_p),
+                ("kf_cam", C.c_void_p), ("n_pt", C.c_int), ("pt_id", C.c_void_p), ("pt_pos", C.c_void_p),
+                ("n_edge", C.c_int), ("edge_pt", C.c_void_p), ("edge_kf", C.c_void_p), ("edge_obs", C.c_void_p),
+                ("edge_inv_sigma2", C.c_void_p)]
+
+
+class _BAResult(C.Structure):
+    _fields_ = [("kf_Tcw", C.c_void_p), ("pt_pos", C.c_void_p), ("edge_erase", C.c_void_p),
+                ("iterations", C.c_int * 2), ("n_erased", C.c_int), ("aborted", C.c_int)]
+
+
+class _BATrace(C.Structure):
+    _fields_ = [("n_solves", C.c_int), ("n_trials", C.c_int), ("solve_ini_chi2", C.c_double * 256),
+                ("solve_chi2", C.c_double * 256), ("trial_chi2", C.c_double * 256),
+                ("trial_lambda", C.c_double * 256)]
+
+
+def oracle_local_ba(pr, stop=False):
+    """Optimizer::LocalBundleAdjustment restated on CPU -> dict of outputs + LM trace."""
+    L = lib()
+    L.ora_local_ba.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    keep = {k: np.ascontiguousarray(pr[k]) for k in ("kf_id", "kf_Tcw", "kf_local", "kf_cam", "pt_id", "pt_pos",
+                                                     "edge_pt", "edge_kf", "edge_obs", "edge_inv_sigma2")}
+    P = _BAProblem(len(keep["kf_id"]), ptr(keep["kf_id"]), ptr(keep["kf_Tcw"]), ptr(keep["kf_local"]),
+                   ptr(keep["kf_cam"]), len(keep["pt_id"]), ptr(keep["pt_id"]), ptr(keep["pt_pos"]),
+                   len(keep["edge_pt"]), ptr(keep["edge_pt"]), ptr(keep["edge_kf"]), ptr(keep["edge_obs"]),
+                   ptr(keep["edge_inv_sigma2"]))
+    T = np.zeros_like(keep["kf_Tcw"])
+    X = np.zeros_like(keep["pt_pos"])
+    er = np.zeros(len(keep["edge_pt"]), np.uint8)
+    R = _BAResult(ptr(T), ptr(X), ptr(er))
+    tr = _BATrace()
+    st = C.c_int(1 if stop else 0)
+    L.ora_local_ba(C.byref(P), C.byref(st), C.byref(R), C.byref(tr))
+    return dict(kf_Tcw=T, pt_pos=X, edge_erase=er.astype(bool), iterations=tuple(R.iterations),
+                n_erased=R.n_erased, aborted=bool(R.aborted),
+                solve_chi2=np.array(tr.solve_chi2[:tr.n_solves]), solve_ini_chi2=np.array(tr.solve_ini_chi2[:tr.n_solves]),
+                trial_chi2=np.array(tr.trial_chi2[:tr.n_trials]), trial_lambda=np.array(tr.trial_lambda[:tr.n_trials]))

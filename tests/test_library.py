@@ -67,3 +67,29 @@ def test_ransac_solvers_validate_and_refuse_without_device():
     if not orb.device_available():
         assert L.Sim3Solver_create(4, ptr(X), ptr(X), ptr(s), ptr(s), ptr(idx), 4, ptr(K), ptr(K), 1,
                                    C.byref(h)) == ORB_E_NODEVICE
+
+
+def test_ba_validates_without_device():
+    from c_orb_slam_amd._lib import ba_problem, ba_result
+    L = lib()
+    kid = np.array([0, 1], np.int32)
+    T = np.tile(np.eye(4, dtype=np.float32).ravel(), (2, 1))
+    loc = np.array([1, 1], np.uint8)
+    cam = np.tile(np.array([435, 435, 367, 252, 47.9], np.float32), (2, 1))
+    pid = np.array([5], np.int32)
+    X = np.array([[0, 0, 5]], np.float32)
+    ept = np.array([0, 0], np.int32)
+    ekf = np.array([1, 1], np.int32)          # duplicate (keyframe, point) edge
+    obs = np.zeros((2, 3), np.float32)
+    isg = np.ones(2, np.float32)
+    P = ba_problem(2, ptr(kid), ptr(T), ptr(loc), ptr(cam), 1, ptr(pid), ptr(X), 2, ptr(ept), ptr(ekf), ptr(obs),
+                   ptr(isg))
+    To, Xo, er = np.zeros_like(T), np.zeros_like(X), np.zeros(2, np.uint8)
+    R = ba_result(ptr(To), ptr(Xo), ptr(er))
+    assert L.Optimizer_LocalBundleAdjustment(C.byref(P), None, C.byref(R)) == ORB_E_INVALID
+    ekf[1] = 0
+    kid[1] = 0                                 # duplicate keyframe id
+    assert L.Optimizer_LocalBundleAdjustment(C.byref(P), None, C.byref(R)) == ORB_E_INVALID
+    kid[1] = 1
+    if not orb.device_available():
+        assert L.Optimizer_LocalBundleAdjustment(C.byref(P), None, C.byref(R)) == ORB_E_NODEVICE
