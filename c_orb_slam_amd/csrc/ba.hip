@@ -714,7 +714,11 @@ int BaEngine::init() {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     ORB_HIP_CHECK(hipHostMalloc((void**)&hScal_, 64 * sizeof(double)));
-    ORB_HIP_CHECK(hipFuncSetAttribute((const void*)k_ldlt, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    int dev = 0;
+    ORB_HIP_CHECK(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    ORB_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+    ldsMax_ = prop.sharedMemPerBlock > 2048 ? prop.sharedMemPerBlock - 1024 : 0;
     return 0;
 }
 
@@ -981,9 +985,9 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     int qmax = 0;
     const int n = 6 * nP;
     const size_t ldsBytes = sizeof(double) * (2 * (size_t)n + (size_t)n * n);
-    const int in_lds = ldsBytes <= 150 * 1024 ? 1 : 0;
+    const int in_lds = ldsBytes <= ldsMax_ ? 1 : 0;
     const size_t shm = in_lds ? ldsBytes : sizeof(double) * 2 * (size_t)n;
-    if (shm > 160 * 1024) return -3;
+    if (shm > ldsMax_) return -3;
     do {
         // setLambda + BlockSolver::solve
         if (nL) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nL, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,

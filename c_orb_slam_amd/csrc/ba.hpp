@@ -91,6 +91,7 @@ private:
     size_t arenaCap_ = 0;
     double* hScal_ = nullptr;      // pinned
     size_t scratchN_ = 0;
+    size_t ldsMax_ = 0;
     // LM state (g2o OptimizationAlgorithmLevenberg)
     double lambda_ = 0, ni_ = 2;
     int nBad_ = 0;
