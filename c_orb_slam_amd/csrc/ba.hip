@@ -343,41 +343,170 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
     }
 }
 
-// per free pose: Hpp (upper 21) and b_p as canonical sums over its active edges (edge order)
+// Reduce chunk sums arr[0..m) (already level-1 trees) to the canonical total, one wave.
+__device__ __forceinline__ double wave_lds_csum(double* arr, int m) {
+    const int lane = threadIdx.x & 63;
+    while (m > 1) {
+        const int m2 = (m + 63) >> 6;
+        for (int c = 0; c < m2; c++) {
+            double u = (c * 64 + lane < m) ? arr[c * 64 + lane] : 0.0;
+            u = wave_tree(u);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) arr[c] = u;
+            __builtin_amdgcn_wave_barrier();
+        }
+        m = m2;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return arr[0];
+}
+
+
+// ---- exact thread-local emulation of the canonical 64-tree ------------------------
+// tree64_local(get, cnt): a[i] = i < cnt ? get(i) : 0 (i < 64), then a[i] += a[i+off]
+// for off = 32..1 -- the same pairing as wave_tree, evaluated in one thread.
+template <class G>
+__device__ __forceinline__ double tree64_local(G get, int cnt) {
+    double a[32];
+#pragma unroll
+    for (int i = 0; i < 32; i++) a[i] = (i < cnt ? get(i) : 0.0) + (i + 32 < cnt ? get(i + 32) : 0.0);
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1)
+#pragma unroll
+        for (int i = 0; i < off; i++) a[i] = a[i] + a[i + off];
+    return a[0];
+}
+
+// Canonical total (ora_csum) of arr[0..m) by ONE thread, in place (arr is private to it).
+__device__ __forceinline__ double local_csum_inplace(double* arr, int m) {
+    if (m <= 0) return 0.0;
+    while (m > 1) {
+        const int m2 = (m + 63) >> 6;
+        for (int c = 0; c < m2; c++) {
+            const int cnt = min(64, m - c * 64);
+            const double t = tree64_local([&](int i) { return arr[c * 64 + i]; }, cnt);
+            arr[c] = t;
+        }
+        m = m2;
+    }
+    return arr[0];
+}
+
+// K canonical 64-trees at once: lane holds v[0..K); lane q < K receives the tree of entry q.
+// Transpose through this wave's LDS buffer (K x 65 doubles), then per-lane register trees.
+template <int K>
+__device__ __forceinline__ double wave_trees(const double* v, double* buf) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < K; q++) buf[q * 65 + lane] = v[q];
+    __builtin_amdgcn_wave_barrier();
+    double r = 0.0;
+    if (lane < K) {
+        const double* row = buf + lane * 65;
+        r = tree64_local([&](int i) { return row[i]; }, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return r;
+}
+
+constexpr int kChunks = 128;  // per-list LDS chunk sums: lists up to 8192 terms
+
+// per free pose: Hpp (upper 21) and b_p as canonical sums over its active edges (edge order).
+// Each lane loads the 27 terms of one edge; chunk trees via wave_trees; chunk sums reduced
+// per entry by one thread.
 __global__ void __launch_bounds__(256) k_pose_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
                                                      double* bp) {
-    __shared__ double sc[4][kWaveScratch];
+    __shared__ double cs[27][kChunks];
+    __shared__ double tb[4][27 * 65];
     const int i = blockIdx.x;
-    const int w = threadIdx.x >> 6;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int s0 = s.peStart[i], n = s.peStart[i + 1] - s0;
+    const int m = (n + 63) >> 6;
     const int nE = s.nE;
-    for (int q = w; q < 27; q += 4) {
-        const double* col = terms + (size_t)(q < 21 ? T_HPP + q : T_BP + (q - 21)) * nE;
-        const double v = wave_csum([&](int j) { return col[s.peList[s0 + j]]; }, n, sc[w]);
-        if ((threadIdx.x & 63) == 0) {
-            if (q < 21) Hpp[21 * i + q] = v;
-            else bp[6 * i + (q - 21)] = v;
+    for (int c = w; c < m; c += 4) {
+        const int j = c * 64 + lane;
+        const bool valid = j < n;
+        const int a = valid ? s.peList[s0 + j] : 0;
+        double v[27];
+#pragma unroll
+        for (int q = 0; q < 27; q++) {
+            const int col = q < 21 ? T_HPP + q : T_BP + (q - 21);
+            v[q] = valid ? terms[(size_t)col * nE + a] : 0.0;
         }
+        if (n == 1) {  // ora_csum returns a single term untouched
+            if (lane == 0)
+                for (int q = 0; q < 27; q++) cs[q][0] = v[q];
+        } else {
+            const double t = wave_trees<27>(v, tb[w]);
+            if (lane < 27) cs[lane][c] = t;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 27) {
+        const int q = threadIdx.x;
+        const double v = n > 0 ? local_csum_inplace(cs[q], m) : 0.0;
+        if (q < 21) Hpp[21 * i + q] = v;
+        else bp[6 * i + (q - 21)] = v;
     }
 }
 
-// per landmark (one wave): Hll (full 3x3) and b_l over its active edges (edge order)
+// per landmark (one thread): Hll (full 3x3) and b_l over its active edges (edge order);
+// typical tracks are short, so the 64-tree is emulated on the few live terms.
 __global__ void __launch_bounds__(256) k_land_reduce(BaStructDev s, const double* __restrict__ terms, double* Hll,
                                                      double* bl) {
-    __shared__ double sc[4][kWaveScratch];
-    const int w = threadIdx.x >> 6;
-    const int l = blockIdx.x * 4 + w;
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= s.nL) return;
     const int s0 = s.leStart[l], n = s.leStart[l + 1] - s0;
     const int nE = s.nE;
-    for (int q = 0; q < 12; q++) {
-        const double* col = terms + (size_t)(q < 9 ? T_HLL + q : T_BL + (q - 9)) * nE;
-        const double v = wave_csum([&](int j) { return col[s.leList[s0 + j]]; }, n, sc[w]);
-        if ((threadIdx.x & 63) == 0) {
-            if (q < 9) Hll[9 * l + q] = v;
-            else bl[3 * l + (q - 9)] = v;
+    double res[12];
+    if (n <= 8) {
+        int ed[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) ed[j] = j < n ? s.leList[s0 + j] : 0;
+#pragma unroll
+        for (int q = 0; q < 12; q++) {
+            const int col = q < 9 ? T_HLL + q : T_BL + (q - 9);
+            double a[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) a[j] = j < n ? terms[(size_t)col * nE + ed[j]] : 0.0;
+            if (n == 1) {
+                res[q] = a[0];
+                continue;
+            }
+            // levels 32, 16, 8 only add the zero padding
+#pragma unroll
+            for (int j = 0; j < 8; j++) a[j] = ((a[j] + 0.0) + 0.0) + 0.0;
+#pragma unroll
+            for (int off = 4; off >= 1; off >>= 1)
+#pragma unroll
+                for (int j = 0; j < off; j++) a[j] = a[j] + a[j + off];
+            res[q] = a[0];
+        }
+    } else {
+        for (int q = 0; q < 12; q++) {
+            const int col = q < 9 ? T_HLL + q : T_BL + (q - 9);
+            const double* cp = terms + (size_t)col * nE;
+            const int m = (n + 63) >> 6;
+            double c0 = 0, c1 = 0, tot = 0;
+            // n <= 4096 (validated): level 1 chunk sums are consumed by a second 64-tree
+            double chunk[2];
+            if (m <= 2) {
+                for (int c = 0; c < m; c++)
+                    chunk[c] = tree64_local([&](int i) { return cp[s.leList[s0 + c * 64 + i]]; }, min(64, n - c * 64));
+                c0 = chunk[0];
+                c1 = m > 1 ? chunk[1] : 0.0;
+                tot = m == 1 ? c0 : tree64_local([&](int i) { return i == 0 ? c0 : c1; }, 2);
+            } else {
+                double lv[64];
+                for (int c = 0; c < m; c++)
+                    lv[c] = tree64_local([&](int i) { return cp[s.leList[s0 + c * 64 + i]]; }, min(64, n - c * 64));
+                tot = tree64_local([&](int i) { return lv[i]; }, m);
+            }
+            res[q] = tot;
         }
     }
+    for (int q = 0; q < 9; q++) Hll[9 * l + q] = res[q];
+    for (int q = 0; q < 3; q++) bl[3 * l + q] = res[9 + q];
 }
 
 // computeLambdaInit: tau * max |diag| over poses and landmarks (order-free max)
@@ -420,140 +549,357 @@ __device__ __forceinline__ void inv3(const double* m, double* r) {
 #undef M
 }
 
-// per landmark: Dinv = (Hll + lambda I)^-1, db = Dinv b_l, and per free-pose edge
-// BDinv = Hpl Dinv and B db (block_solver.hpp:376-404)
-__global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double* Hll, const double* bl,
-                                                    const double* __restrict__ Hpl, double lam_host, int use_dev,
-                                                    const double* scal, double* Dinv, double* db, double* Emat,
-                                                    double* cb) {
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= s.nL) return;
-    const double lambda = lam_of(lam_host, use_dev, scal);
-    double D[9], Di[9], b[3], d[3];
+// Dinv = (Hll + lambda I)^-1 of landmark l (setLambda + D->inverse(), block_solver.hpp:383-389)
+__device__ __forceinline__ void land_dinv(const double* Hll, int l, double lambda, double* Di) {
+    double D[9];
     for (int q = 0; q < 9; q++) D[q] = Hll[9 * l + q];
     for (int j = 0; j < 3; j++) D[4 * j] += lambda;
     inv3(D, Di);
-    for (int q = 0; q < 3; q++) b[q] = bl[3 * l + q];
+}
+
+// per active edge with a free pose: BDinv = Hpl Dinv and B (Dinv b_l)  (block_solver.hpp:376-404)
+__global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double* Hll, const double* bl,
+                                                    const double* __restrict__ Hpl, double lam_host, int use_dev,
+                                                    const double* scal, double* Emat, double* cb) {
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= s.nE || s.ePose[a] < 0) return;
+    const int l = s.eLand[a];
+    const double lambda = lam_of(lam_host, use_dev, scal);
+    double Di[9], d[3];
+    land_dinv(Hll, l, lambda, Di);
+    const double b[3] = {bl[3 * l], bl[3 * l + 1], bl[3 * l + 2]};
     for (int r = 0; r < 3; r++) d[r] = (Di[r * 3] * b[0] + Di[r * 3 + 1] * b[1]) + Di[r * 3 + 2] * b[2];
-    for (int q = 0; q < 9; q++) Dinv[9 * l + q] = Di[q];
-    for (int q = 0; q < 3; q++) db[3 * l + q] = d[q];
-    for (int j = s.lpStart[l]; j < s.lpStart[l + 1]; j++) {
-        const int a = s.lpList[j];
-        const double* Bi = Hpl + 18 * (size_t)a;
-        for (int r = 0; r < 6; r++) {
-            const double b0 = Bi[r * 3], b1 = Bi[r * 3 + 1], b2 = Bi[r * 3 + 2];
-            for (int k = 0; k < 3; k++) Emat[18 * (size_t)a + r * 3 + k] = (b0 * Di[k] + b1 * Di[3 + k]) + b2 * Di[6 + k];
-            cb[6 * (size_t)a + r] = (b0 * d[0] + b1 * d[1]) + b2 * d[2];
-        }
+    const double* Bi = Hpl + 18 * (size_t)a;
+    for (int r = 0; r < 6; r++) {
+        const double b0 = Bi[r * 3], b1 = Bi[r * 3 + 1], b2 = Bi[r * 3 + 2];
+        for (int k = 0; k < 3; k++) Emat[18 * (size_t)a + r * 3 + k] = (b0 * Di[k] + b1 * Di[3 + k]) + b2 * Di[6 + k];
+        cb[6 * (size_t)a + r] = (b0 * d[0] + b1 * d[1]) + b2 * d[2];
     }
 }
 
 // Schur complement block (i1, i2): S = [Hpp + lambda I] - csum_l BDinv_l,i1 B_l,i2^T
 // (upper triangle of the diagonal blocks), and b_s = b_p - csum_l B db.
+// Each lane loads the two 6x3 blocks of one landmark term once and feeds all entries.
 __global__ void __launch_bounds__(256) k_schur(BaStructDev s, const double* __restrict__ Emat,
                                                const double* __restrict__ Hpl, const double* __restrict__ cb,
                                                const double* Hpp, const double* bp, double lam_host, int use_dev,
                                                const double* scal, double* S, double* bs) {
-    __shared__ double sc[4][kWaveScratch];
+    __shared__ double cs[36][kChunks];
+    __shared__ double tb[4][36 * 65];
     const int blk = blockIdx.x;
     const int i1 = s.blkI[blk], i2 = s.blkJ[blk];
-    const int w = threadIdx.x >> 6;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int s0 = s.blkStart[blk], n = s.blkStart[blk + 1] - s0;
+    const int m = (n + 63) >> 6;
     const int nn = 6 * s.nP;
     const bool diag = i1 == i2;
-    const double lambda = lam_of(lam_host, use_dev, scal);
     const int nent = diag ? 27 : 36;
-    for (int q = w; q < nent; q += 4) {
-        if (diag && q >= 21) {  // b_schur row r of pose i1
-            const int r = q - 21;
-            const double v = wave_csum([&](int j) { return cb[6 * (size_t)s.pairA[s0 + j] + r]; }, n, sc[w]);
-            if ((threadIdx.x & 63) == 0) bs[6 * i1 + r] = bp[6 * i1 + r] - v;
-            continue;
+    for (int c = w; c < m; c += 4) {
+        const int j = c * 64 + lane;
+        const bool valid = j < n;
+        const int a1 = valid ? s.pairA[s0 + j] : 0, a2 = valid ? s.pairB[s0 + j] : 0;
+        double E[18], B[18], v[36];
+#pragma unroll
+        for (int q = 0; q < 18; q++) {
+            E[q] = valid ? Emat[18 * (size_t)a1 + q] : 0.0;
+            B[q] = valid ? Hpl[18 * (size_t)a2 + q] : 0.0;
         }
-        int r, c;
-        if (diag) {  // q -> (r, c) with c >= r, packed like DIAG21
-            r = 0;
-            while (r < 5 && q >= DIAG21[r + 1]) r++;
-            c = r + (q - DIAG21[r]);
+        if (diag) {
+            int q = 0;
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int cc = r; cc < 6; cc++, q++)
+                    v[q] = valid ? (E[r * 3] * B[cc * 3] + E[r * 3 + 1] * B[cc * 3 + 1]) + E[r * 3 + 2] * B[cc * 3 + 2] : 0.0;
+#pragma unroll
+            for (int r = 0; r < 6; r++) v[21 + r] = valid ? cb[6 * (size_t)a1 + r] : 0.0;
+#pragma unroll
+            for (int q2 = 27; q2 < 36; q2++) v[q2] = 0.0;
         } else {
-            r = q / 6;
-            c = q % 6;
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int cc = 0; cc < 6; cc++)
+                    v[r * 6 + cc] = valid ? (E[r * 3] * B[cc * 3] + E[r * 3 + 1] * B[cc * 3 + 1]) + E[r * 3 + 2] * B[cc * 3 + 2] : 0.0;
         }
-        const double v = wave_csum(
-            [&](int j) {
-                const double* Ei = Emat + 18 * (size_t)s.pairA[s0 + j] + r * 3;
-                const double* Bj = Hpl + 18 * (size_t)s.pairB[s0 + j] + c * 3;
-                return (Ei[0] * Bj[0] + Ei[1] * Bj[1]) + Ei[2] * Bj[2];
-            },
-            n, sc[w]);
-        if ((threadIdx.x & 63) == 0) {
-            double h = 0;
-            if (diag) {
-                h = Hpp[21 * i1 + q];
-                if (c == r) h += lambda;
-            }
-            S[(size_t)(6 * i1 + r) * nn + 6 * i2 + c] = h - v;
+        if (n == 1) {
+            if (lane == 0)
+                for (int q = 0; q < 36; q++) cs[q][0] = v[q];
+        } else {
+            const double t = wave_trees<36>(v, tb[w]);
+            if (lane < 36) cs[lane][c] = t;
         }
     }
+    __syncthreads();
+    if (threadIdx.x >= nent) return;
+    const int q = threadIdx.x;
+    const double v = local_csum_inplace(cs[q], m);
+    const double lambda = lam_of(lam_host, use_dev, scal);
+    if (diag && q >= 21) {
+        bs[6 * i1 + (q - 21)] = bp[6 * i1 + (q - 21)] - v;
+        return;
+    }
+    int r, c;
+    if (diag) {
+        r = 0;
+        while (r < 5 && q >= DIAG21[r + 1]) r++;
+        c = r + (q - DIAG21[r]);
+    } else {
+        r = q / 6;
+        c = q % 6;
+    }
+    double h = 0;
+    if (diag) {
+        h = Hpp[21 * i1 + q];
+        if (c == r) h += lambda;
+    }
+    S[(size_t)(6 * i1 + r) * nn + 6 * i2 + c] = h - v;
 }
 
-// Dense LDL^T of the upper triangle + solve (oracle ora_ldlt_solve), one workgroup.
-// S is staged in LDS when it fits.  x_p -> x[0..n), ok flag -> scal[3].
+// Dense LDL^T of the upper triangle + solve, one workgroup (256 threads).
+// Same per-element operation sequence as oracle ora_ldlt_solve, blocked by 6-column panels:
+// wave 0 factorises the panel rows and writes L (lower triangle), then every wave
+// applies the panel's rank-1 updates, in k order, to its trailing rows.
 __global__ void __launch_bounds__(256) k_ldlt(int n, double* Sg, const double* bs, double* x, double* scal, int in_lds) {
     extern __shared__ double lds[];
-    double* l = lds;            // n
-    double* y = lds + n;        // n
-    double* A = in_lds ? lds + 2 * n : Sg;
-    const int tid = threadIdx.x, nt = blockDim.x;
-    if (in_lds)
-        for (int q = tid; q < n * n; q += nt) A[q] = Sg[q];
-    for (int q = tid; q < n; q += nt) y[q] = bs[q];
-    __syncthreads();
+    double* y = lds;            // n
+    double* A = in_lds ? lds + n : Sg;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     __shared__ int ok;
+    if (in_lds)
+        for (int q = tid; q < n * n; q += blockDim.x) A[q] = Sg[q];
+    for (int q = tid; q < n; q += blockDim.x) y[q] = bs[q];
     if (tid == 0) ok = 1;
     __syncthreads();
-    for (int k = 0; k < n; k++) {
-        const double d = A[(size_t)k * n + k];
-        if (d == 0.0) {
-            if (tid == 0) ok = 0;
-            break;
+    for (int p0 = 0; p0 < n; p0 += 6) {
+        const int p1 = min(p0 + 6, n);
+        if (w == 0) {
+            for (int k = p0; k < p1; k++) {
+                const double d = A[(size_t)k * n + k];
+                if (d == 0.0) {
+                    if (lane == 0) ok = 0;
+                    break;
+                }
+                for (int i = k + 1 + lane; i < n; i += 64) A[(size_t)i * n + k] = A[(size_t)k * n + i] / d;
+                __builtin_amdgcn_wave_barrier();
+                for (int i = k + 1; i < p1; i++) {
+                    const double li = A[(size_t)i * n + k];
+                    for (int j = i + lane; j < n; j += 64) A[(size_t)i * n + j] -= li * A[(size_t)k * n + j];
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
         }
-        for (int i = k + 1 + tid; i < n; i += nt) l[i] = A[(size_t)k * n + i] / d;
         __syncthreads();
-        const int m = n - k - 1;
-        for (int q = tid; q < m * m; q += nt) {
-            const int i = k + 1 + q / m, j = k + 1 + q % m;
-            if (j >= i) A[(size_t)i * n + j] -= l[i] * A[(size_t)k * n + j];
+        if (!ok) break;
+        for (int i = p1 + w; i < n; i += 4) {
+            double L[6];
+            for (int k = p0; k < p1; k++) L[k - p0] = A[(size_t)i * n + k];
+            for (int j = i + lane; j < n; j += 64) {
+                double v = A[(size_t)i * n + j];
+                for (int k = p0; k < p1; k++) v -= L[k - p0] * A[(size_t)k * n + j];
+                A[(size_t)i * n + j] = v;
+            }
         }
-        __syncthreads();
-        for (int i = k + 1 + tid; i < n; i += nt) A[(size_t)k * n + i] = l[i];
         __syncthreads();
     }
-    __syncthreads();
     if (!ok) {
         if (tid == 0) scal[3] = 0.0;
         return;
     }
-    for (int k = 0; k < n; k++) {
-        const double yk = y[k];
-        for (int i = k + 1 + tid; i < n; i += nt) y[i] -= A[(size_t)k * n + i] * yk;
-        __syncthreads();
+    if (w == 0) {
+        // L y = b: per row, subtractions in k order (column-sweep order of the oracle)
+        for (int r0 = 0; r0 < n; r0 += 64) {
+            const int i = r0 + lane;
+            double acc = i < n ? y[i] : 0.0;
+            for (int k = 0; k < r0; k++)
+                if (i < n) acc -= A[(size_t)i * n + k] * y[k];
+            for (int k = r0; k < min(r0 + 64, n); k++) {
+                const double yk = __shfl(acc, k - r0, 64);
+                if (i > k && i < n) acc -= A[(size_t)i * n + k] * yk;
+            }
+            if (i < n) y[i] = acc;
+            __builtin_amdgcn_wave_barrier();
+        }
+        for (int k = lane; k < n; k += 64) y[k] = y[k] / A[(size_t)k * n + k];
+        __builtin_amdgcn_wave_barrier();
+        // L^T x = z: per row, subtractions in descending k order
+        for (int r1 = n; r1 > 0; r1 -= 64) {
+            const int r0 = max(r1 - 64, 0);
+            const int i = r0 + lane;
+            double acc = i < r1 ? y[i] : 0.0;
+            for (int k = n - 1; k >= r1; k--)
+                if (i < r1) acc -= A[(size_t)k * n + i] * y[k];
+            for (int k = r1 - 1; k >= r0; k--) {
+                const double yk = __shfl(acc, k - r0, 64);
+                if (i < k) acc -= A[(size_t)k * n + i] * yk;
+            }
+            if (i < r1) y[i] = acc;
+            __builtin_amdgcn_wave_barrier();
+        }
+        for (int k = lane; k < n; k += 64) x[k] = y[k];
+        if (lane == 0) scal[3] = 1.0;
     }
-    for (int k = tid; k < n; k += nt) y[k] = y[k] / A[(size_t)k * n + k];
+}
+
+// Register-resident LDL^T + solve for n <= 128 (<= 21 free keyframes), 256 threads.
+// Thread (wave w, lane) owns rows i = 4r + w (r < 32) of columns j = lane and lane + 64.
+// Per 6-column panel: owners publish the panel rows to LDS (U), wave 0 factorises them
+// in registers and writes L (Lall[k][i] = L[i][k], Lpan[i][k - p0]) and d_k, then every
+// thread applies the panel's updates to its rows in k order.  Per-element operation
+// sequence identical to oracle ora_ldlt_solve.
+constexpr int kLdltMax = 128;
+__global__ void __launch_bounds__(256) k_ldlt_reg(int n, const double* __restrict__ Sg, const double* bs, double* x,
+                                                  double* scal) {
+    extern __shared__ double lds[];
+    double* Lall = lds;                    // n x n, Lall[k * n + i] = L[i][k]
+    double* U = Lall + (size_t)n * n;      // 6 x kLdltMax panel rows
+    double* Lpan = U + 6 * kLdltMax;       // kLdltMax x 6
+    double* dvec = Lpan + 6 * kLdltMax;    // n
+    double* y = dvec + kLdltMax;           // n
+    __shared__ int ok;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    double R[2][32];
+#pragma unroll
+    for (int c = 0; c < 2; c++)
+#pragma unroll
+        for (int r = 0; r < 32; r++) {
+            const int i = 4 * r + w, j = lane + 64 * c;
+            R[c][r] = (i < n && j < n && i <= j) ? Sg[(size_t)i * n + j] : 0.0;
+        }
+    for (int q = tid; q < n; q += 256) y[q] = bs[q];
+    if (tid == 0) ok = 1;
     __syncthreads();
-    for (int k = n - 1; k >= 0; k--) {
-        const double yk = y[k];
-        for (int i = tid; i < k; i += nt) y[i] -= A[(size_t)i * n + k] * yk;
+    for (int p0 = 0; p0 < n; p0 += 6) {
+        const int p1 = min(p0 + 6, n), pw = p1 - p0;
+        // publish panel rows (all columns)
+#pragma unroll
+        for (int r = 0; r < 32; r++) {
+            const int i = 4 * r + w;
+            if (i >= p0 && i < p1) {
+                U[(i - p0) * kLdltMax + lane] = R[0][r];
+                U[(i - p0) * kLdltMax + lane + 64] = R[1][r];
+            }
+        }
+        __syncthreads();
+        if (w == 0) {
+            double u0[6], u1[6];
+#pragma unroll
+            for (int t = 0; t < 6; t++) {
+                u0[t] = t < pw ? U[t * kLdltMax + lane] : 0.0;
+                u1[t] = t < pw ? U[t * kLdltMax + lane + 64] : 0.0;
+            }
+            bool bad = false;
+#pragma unroll
+            for (int t = 0; t < 6; t++) {
+                if (t >= pw || bad) break;
+                const int k = p0 + t;
+                const double d = __shfl(k < 64 ? u0[t] : u1[t], k & 63, 64);
+                if (d == 0.0) {
+                    bad = true;
+                    break;
+                }
+                // l_i = A[k][i] / d for every column i > k (lane-local)
+                const double l0 = (lane > k && lane < n) ? u0[t] / d : 0.0;
+                const double l1 = (lane + 64 > k && lane + 64 < n) ? u1[t] / d : 0.0;
+                if (lane > k && lane < n) {
+                    Lall[(size_t)k * n + lane] = l0;
+                    Lpan[lane * 6 + t] = l0;
+                }
+                if (lane + 64 > k && lane + 64 < n) {
+                    Lall[(size_t)k * n + lane + 64] = l1;
+                    Lpan[(lane + 64) * 6 + t] = l1;
+                }
+                if (lane == 0) dvec[k] = d;
+                // remaining panel rows i = p0 + t2 (t2 > t): A[i][j] -= l_i * A[k][j], j >= i
+#pragma unroll
+                for (int t2 = t + 1; t2 < 6; t2++) {
+                    if (t2 >= pw) break;
+                    const int i = p0 + t2;
+                    const double li = __shfl(i < 64 ? l0 : l1, i & 63, 64);
+                    if (lane >= i) u0[t2] -= li * u0[t];
+                    if (lane + 64 >= i) u1[t2] -= li * u1[t];
+                }
+            }
+            if (bad && lane == 0) ok = 0;
+            // the panel rows after their in-panel updates are the U rows of the trailing update
+#pragma unroll
+            for (int t = 0; t < 6; t++)
+                if (t < pw) {
+                    U[t * kLdltMax + lane] = u0[t];
+                    U[t * kLdltMax + lane + 64] = u1[t];
+                }
+        }
+        __syncthreads();
+        if (!ok) break;
+        // trailing rows i >= p1: v -= L[i][k] * A[k][j] for k = p0..p1-1 in order
+        double u0[6], u1[6];
+#pragma unroll
+        for (int t = 0; t < 6; t++) {
+            u0[t] = t < pw ? U[t * kLdltMax + lane] : 0.0;
+            u1[t] = t < pw ? U[t * kLdltMax + lane + 64] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 32; r++) {
+            const int i = 4 * r + w;
+            if (i >= p1 && i < n) {
+                double L[6];
+#pragma unroll
+                for (int t = 0; t < 6; t++) L[t] = t < pw ? Lpan[i * 6 + t] : 0.0;
+                double v0 = R[0][r], v1 = R[1][r];
+#pragma unroll
+                for (int t = 0; t < 6; t++) {
+                    if (t >= pw) break;
+                    v0 -= L[t] * u0[t];
+                    v1 -= L[t] * u1[t];
+                }
+                if (lane >= i) R[0][r] = v0;
+                if (lane + 64 >= i) R[1][r] = v1;
+            }
+        }
         __syncthreads();
     }
-    for (int k = tid; k < n; k += nt) x[k] = y[k];
-    if (tid == 0) scal[3] = 1.0;
+    if (!ok) {
+        if (tid == 0) scal[3] = 0.0;
+        return;
+    }
+    if (w != 0) return;
+    // L y = b: per row, subtractions in k order
+    for (int r0 = 0; r0 < n; r0 += 64) {
+        const int i = r0 + lane;
+        double acc = i < n ? y[i] : 0.0;
+        for (int k = 0; k < r0; k++)
+            if (i < n) acc -= Lall[(size_t)k * n + i] * y[k];
+        for (int k = r0; k < min(r0 + 64, n); k++) {
+            const double yk = __shfl(acc, k - r0, 64);
+            if (i > k && i < n) acc -= Lall[(size_t)k * n + i] * yk;
+        }
+        if (i < n) y[i] = acc;
+        __builtin_amdgcn_wave_barrier();
+    }
+    for (int k = lane; k < n; k += 64) y[k] = y[k] / dvec[k];
+    __builtin_amdgcn_wave_barrier();
+    // L^T x = z: per row, subtractions in descending k order (L[k][i] = Lall[i * n + k])
+    for (int r1 = n; r1 > 0; r1 -= 64) {
+        const int r0 = max(r1 - 64, 0);
+        const int i = r0 + lane;
+        double acc = i < r1 ? y[i] : 0.0;
+        for (int k = n - 1; k >= r1; k--)
+            if (i < r1) acc -= Lall[(size_t)i * n + k] * y[k];
+        for (int k = r1 - 1; k >= r0; k--) {
+            const double yk = __shfl(acc, k - r0, 64);
+            if (i < k) acc -= Lall[(size_t)i * n + k] * yk;
+        }
+        if (i < r1) y[i] = acc;
+        __builtin_amdgcn_wave_barrier();
+    }
+    for (int k = lane; k < n; k += 64) x[k] = y[k];
+    if (lane == 0) scal[3] = 1.0;
 }
 
 // push + back-substitution (block_solver.hpp:457-484) + SparseOptimizer::update (oplus)
 __global__ void __launch_bounds__(256) k_update(BaStructDev s, Se3* T, Se3* Tbak, double* X, double* Xbak,
-                                                double* x, const double* __restrict__ Hpl, const double* Dinv,
-                                                const double* bl, const double* scal) {
+                                                double* x, const double* __restrict__ Hpl, const double* Hll,
+                                                const double* bl, double lam_host, int use_dev, const double* scal) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     const int nP = s.nP;
     if (g < nP) {
@@ -584,7 +930,8 @@ __global__ void __launch_bounds__(256) k_update(BaStructDev s, Se3* T, Se3* Tbak
                 cl[k] += acc;
             }
         }
-        const double* Di = Dinv + 9 * l;
+        double Di[9];
+        land_dinv(Hll, l, lam_of(lam_host, use_dev, scal), Di);
         for (int r = 0; r < 3; r++) xl[r] = (Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1]) + Di[r * 3 + 2] * cl[2];
     }
     for (int k = 0; k < 3; k++) {
@@ -634,7 +981,6 @@ struct CsumList {
 };
 __global__ void __launch_bounds__(1024) k_csum(CsumList L0, CsumList L1) {
     const CsumList L = blockIdx.x == 0 ? L0 : L1;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     if (L.n <= 1) {
         if (threadIdx.x == 0) *L.out = L.n == 1 ? L.v[0] : 0.0;
         return;
@@ -644,10 +990,9 @@ __global__ void __launch_bounds__(1024) k_csum(CsumList L0, CsumList L1) {
     int m = L.n;
     while (true) {
         const int m2 = (m + 63) >> 6;
-        for (int c = w; c < m2; c += nw) {
-            double v = (c * 64 + lane < m) ? src[c * 64 + lane] : 0.0;
-            v = wave_tree(v);
-            if (lane == 0) dst[c] = v;
+        for (int c = threadIdx.x; c < m2; c += blockDim.x) {
+            const double* p = src + c * 64;
+            dst[c] = tree64_local([&](int i) { return p[i]; }, min(64, m - c * 64));
         }
         __threadfence_block();
         __syncthreads();
@@ -919,11 +1264,11 @@ int BaEngine::build_structure(int level) {
                 }
     }
     for (int i = 0; i < nP; i++)
-        if (peStart[i + 1] - peStart[i] > 64 * kWaveScratch) return -3;
+        if (peStart[i + 1] - peStart[i] > 64 * kChunks) return -3;
     for (int l = 0; l < nL; l++)
-        if (leStart[l + 1] - leStart[l] > 64 * kWaveScratch) return -3;
+        if (leStart[l + 1] - leStart[l] > 64 * 64) return -3;
     for (int b = 0; b < nBlk; b++)
-        if (blkStart[b + 1] - blkStart[b] > 64 * kWaveScratch) return -3;
+        if (blkStart[b + 1] - blkStart[b] > 64 * kChunks) return -3;
     // pack and upload
     std::vector<const std::vector<int32_t>*> parts = {&aE,      &ePose,   &eLand,  &poseKf, &landPt, &peStart,
                                                       &peList,  &leStart, &leList, &lpStart, &lpList, &blkI,
@@ -969,7 +1314,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     CsumList c0{dRc_, nE, tmpA0_, tmpA1_, dScal_ + 0};
     hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, c0, c0);
     if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(256), 0, s, S, dTerms_, dHpp_, dBp_);
-    if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(nL, 4)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_);
+    if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(nL, 256)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_);
     if (nv) hipLaunchKernelGGL(k_copy_b, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dBp_, dBl_, dB_);
     int use_dev = 0;
     if (iteration == 0) {
@@ -984,20 +1329,25 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     double rho = 0;
     int qmax = 0;
     const int n = 6 * nP;
-    const size_t ldsBytes = sizeof(double) * (2 * (size_t)n + (size_t)n * n);
+    const size_t ldsBytes = sizeof(double) * ((size_t)n + (size_t)n * n);
     const int in_lds = ldsBytes <= ldsMax_ ? 1 : 0;
-    const size_t shm = in_lds ? ldsBytes : sizeof(double) * 2 * (size_t)n;
-    if (shm > ldsMax_) return -3;
+    const size_t shm = in_lds ? ldsBytes : sizeof(double) * (size_t)n;
+    const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
+    const bool use_reg = n <= kLdltMax && regShm <= ldsMax_;
+    if (!use_reg && shm > ldsMax_) return -3;
     do {
         // setLambda + BlockSolver::solve
-        if (nL) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nL, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
-                                   lambda_, use_dev, dScal_, dDinv_, dDb_, dEmat_, dCb_);
+        if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
+                                   lambda_, use_dev, dScal_, dEmat_, dCb_);
         if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(256), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
                                        lambda_, use_dev, dScal_, dS_, dBs_);
-        hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds);
+        if (use_reg)
+            hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(256), regShm, s, n, dS_, dBs_, dX2_, dScal_);
+        else
+            hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds);
         // push + update
         if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_,
-                                        dXbak_, dX2_, dHplA_, dDinv_, dBl_, dScal_);
+                                        dXbak_, dX2_, dHplA_, dHll_, dBl_, lambda_, use_dev, dScal_);
         // computeActiveErrors + activeRobustChi2 ; computeScale
         la.linearize = 0;
         if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
@@ -1126,4 +1476,47 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R) 
     return 0;
 }
 
+}  // namespace orbgpu
+
+// ---------------------------------------------------------------- unit entry points
+namespace orbgpu {
+int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) {
+    double *dS = nullptr, *dB = nullptr, *dX = nullptr, *dScal = nullptr;
+    const size_t nn = (size_t)std::max(n, 1);
+    ORB_HIP_CHECK(hipMalloc(&dS, sizeof(double) * nn * nn));
+    ORB_HIP_CHECK(hipMalloc(&dB, sizeof(double) * nn));
+    ORB_HIP_CHECK(hipMalloc(&dX, sizeof(double) * nn));
+    ORB_HIP_CHECK(hipMalloc(&dScal, sizeof(double) * 16));
+    ORB_HIP_CHECK(hipMemcpy(dS, S, sizeof(double) * n * n, hipMemcpyHostToDevice));
+    ORB_HIP_CHECK(hipMemcpy(dB, b, sizeof(double) * n, hipMemcpyHostToDevice));
+    ORB_HIP_CHECK(hipMemset(dX, 0, sizeof(double) * nn));
+    if (variant == 0) {
+        const size_t shm = sizeof(double) * ((size_t)n * n + 14 * kLdltMax);
+        if (n > kLdltMax) return -3;
+        hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(256), shm, 0, n, dS, dB, dX, dScal);
+    } else {
+        hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), sizeof(double) * n + 16, 0, n, dS, dB, dX, dScal, 0);
+    }
+    ORB_HIP_CHECK(hipGetLastError());
+    double sc[16];
+    ORB_HIP_CHECK(hipMemcpy(sc, dScal, sizeof(sc), hipMemcpyDeviceToHost));
+    ORB_HIP_CHECK(hipMemcpy(x, dX, sizeof(double) * n, hipMemcpyDeviceToHost));
+    (void)hipFree(dS); (void)hipFree(dB); (void)hipFree(dX); (void)hipFree(dScal);
+    return sc[3] != 0.0 ? 1 : 0;
+}
+
+int debug_csum(const double* v, int n, double* out) {
+    double *dV = nullptr, *dT = nullptr;
+    const size_t nn = (size_t)std::max(n, 1);
+    ORB_HIP_CHECK(hipMalloc(&dV, sizeof(double) * (nn + 16)));
+    ORB_HIP_CHECK(hipMalloc(&dT, sizeof(double) * (2 * (nn / 64 + 64) + 16)));
+    ORB_HIP_CHECK(hipMemcpy(dV, v, sizeof(double) * n, hipMemcpyHostToDevice));
+    double* o = dT + 2 * (nn / 64 + 64);
+    CsumList L{dV, n, dT, dT + nn / 64 + 64, o};
+    hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, 0, L, L);
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipMemcpy(out, o, sizeof(double), hipMemcpyDeviceToHost));
+    (void)hipFree(dV); (void)hipFree(dT);
+    return 0;
+}
 }  // namespace orbgpu

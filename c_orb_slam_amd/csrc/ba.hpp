@@ -98,4 +98,7 @@ private:
     BaTrace trace_;
 };
 
+int debug_ldlt(int n, const double* S, const double* b, double* x, int variant);
+int debug_csum(const double* v, int n, double* out);
+
 }  // namespace orbgpu

@@ -85,4 +85,23 @@ int Optimizer_last_timings(double* ms2) {
     return ORB_OK;
 }
 
+int orbgpu_unit_ldlt_solve(int n, const double* S, const double* b, double* x, int variant, int* ok) {
+    if (n < 0 || (n > 0 && (!S || !b || !x)) || !ok) return ORB_E_INVALID;
+    int rc = 0;
+    engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    const int r = orbgpu::debug_ldlt(n, S, b, x, variant);
+    if (r < 0) return r == -3 ? ORB_E_CAPACITY : ORB_E_HIP;
+    *ok = r;
+    return ORB_OK;
+}
+
+int orbgpu_unit_csum(const double* v, int n, double* out) {
+    if (n < 0 || (n > 0 && !v) || !out) return ORB_E_INVALID;
+    int rc = 0;
+    engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    return orbgpu::debug_csum(v, n, out) ? ORB_E_HIP : ORB_OK;
+}
+
 }  // extern "C"

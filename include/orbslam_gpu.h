@@ -303,6 +303,12 @@ int Optimizer_last_trace(double* solve_ini_chi2, double* solve_chi2, int solve_c
 /* host milliseconds of the calling thread's last run: [total, structure build] */
 int Optimizer_last_timings(double* ms2);
 
+/* Unit entry points of the BA building blocks (parity tests): the dense LDL^T
+ * solve of the reduced pose system (variant 0 = register-resident kernel,
+ * n <= 128; 1 = generic kernel) and the canonical FP64 sum. */
+int orbgpu_unit_ldlt_solve(int n, const double* S, const double* b, double* x, int variant, int* ok);
+int orbgpu_unit_csum(const double* v, int n, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,78 @@
+"""GPU BA building blocks vs the oracle: canonical FP64 sum (ora_csum) and the dense
+LDL^T pose-system solve (ora_ldlt_solve), bit-identical by construction."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from oracle_lib import ptr
+
+pytestmark = pytest.mark.gpu
+
+
+def _ora_csum(v):
+    L = oracle_lib.lib()
+    L.ora_csum.restype = C.c_double
+    L.ora_csum.argtypes = [C.c_void_p, C.c_int]
+    w = np.array(v, np.float64)
+    return L.ora_csum(ptr(w), len(w))
+
+
+def _ora_ldlt(S, b):
+    L = oracle_lib.lib()
+    L.ora_ldlt_solve.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    A = np.array(S, np.float64)
+    x = np.zeros(len(b))
+    ok = L.ora_ldlt_solve(ptr(A), len(b), ptr(np.array(b, np.float64)), ptr(x))
+    return ok, x
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 65, 127, 128, 129, 4095, 4096, 4097, 15000, 300000])
+def test_csum_matches_oracle(gpu, n):
+    from c_orb_slam_amd._lib import lib
+    rng = np.random.default_rng(n)
+    v = rng.normal(0, 1, n) * 10.0 ** rng.integers(-8, 8, n)
+    if n:
+        v[0] = -0.0 if n == 1 else v[0]
+    out = C.c_double()
+    assert lib().orbgpu_unit_csum(ptr(np.ascontiguousarray(v)), n, C.byref(out)) == 0
+    ref = _ora_csum(v)
+    assert out.value == ref or (np.isnan(out.value) and np.isnan(ref))
+    assert np.signbit(out.value) == np.signbit(ref)
+
+
+def _spd(rng, n):
+    A = rng.normal(size=(n, n))
+    S = A @ A.T + n * np.eye(n)
+    return S
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("n", [1, 6, 12, 60, 64, 66, 84, 126, 128])
+def test_ldlt_matches_oracle(gpu, n, variant):
+    from c_orb_slam_amd._lib import lib
+    rng = np.random.default_rng(100 + n)
+    S = _spd(rng, n)
+    # only the upper triangle is read: poison the lower one
+    S_in = S.copy()
+    S_in[np.tril_indices(n, -1)] = np.nan
+    b = rng.normal(size=n)
+    x = np.zeros(n)
+    ok = C.c_int()
+    assert lib().orbgpu_unit_ldlt_solve(n, ptr(np.ascontiguousarray(S_in)), ptr(b), ptr(x), variant, C.byref(ok)) == 0
+    oko, xo = _ora_ldlt(S_in, b)
+    assert ok.value == oko == 1
+    assert np.array_equal(x, xo), np.abs(x - xo).max()
+    np.testing.assert_allclose(S @ x, b, rtol=1e-8, atol=1e-8)
+
+
+def test_ldlt_zero_pivot_fails(gpu):
+    from c_orb_slam_amd._lib import lib
+    S = np.eye(12)
+    S[7, 7] = 0.0
+    x = np.zeros(12)
+    ok = C.c_int(5)
+    for variant in (0, 1):
+        assert lib().orbgpu_unit_ldlt_solve(12, ptr(S), ptr(np.ones(12)), ptr(x), variant, C.byref(ok)) == 0
+        assert ok.value == 0
