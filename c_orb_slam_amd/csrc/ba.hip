@@ -183,8 +183,28 @@ __device__ __forceinline__ void huber(const EdgeDev& e, double chi, double* rho0
 }
 
 // ---------------------------------------------------------------- canonical reductions
+// Canonical 64-tree across a wave: lane i (< off) += lane i + off for off = 32..1, result in
+// lane 0.  gfx950 cross-lane moves instead of LDS: v_permlane32_swap (off 32),
+// v_permlane16_swap (off 16), DPP row_shl (off 8..1, within the first row).
+__device__ __forceinline__ unsigned xl_down(unsigned v, int off) {
+    switch (off) {
+        case 32: return __builtin_amdgcn_permlane32_swap(v, v, false, false)[1];
+        case 16: return __builtin_amdgcn_permlane16_swap(v, v, false, false)[1];
+        case 8: return __builtin_amdgcn_update_dpp(0u, v, 0x108, 0xf, 0xf, false);
+        case 4: return __builtin_amdgcn_update_dpp(0u, v, 0x104, 0xf, 0xf, false);
+        case 2: return __builtin_amdgcn_update_dpp(0u, v, 0x102, 0xf, 0xf, false);
+        default: return __builtin_amdgcn_update_dpp(0u, v, 0x101, 0xf, 0xf, false);
+    }
+}
+__device__ __forceinline__ double wave_down(double v, int off) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = xl_down((unsigned)(u & 0xffffffffu), off);
+    const unsigned hi = xl_down((unsigned)(u >> 32), off);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
 __device__ __forceinline__ double wave_tree(double v) {
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += wave_down(v, off);
     return v;
 }
 
@@ -219,6 +239,54 @@ __device__ __forceinline__ double wave_csum(F f, int n, double* sc) {
     return __shfl(v, 0, 64);
 }
 
+// ---- exact thread-local emulation of the canonical 64-tree ------------------------
+// tree64_local(get, cnt): a[i] = i < cnt ? get(i) : 0 (i < 64), then a[i] += a[i+off]
+// for off = 32..1 -- the same pairing as wave_tree, evaluated in one thread.
+template <class G>
+__device__ __forceinline__ double tree64_local(G get, int cnt) {
+    double a[32];
+#pragma unroll
+    for (int i = 0; i < 32; i++) a[i] = (i < cnt ? get(i) : 0.0) + (i + 32 < cnt ? get(i + 32) : 0.0);
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1)
+#pragma unroll
+        for (int i = 0; i < off; i++) a[i] = a[i] + a[i + off];
+    return a[0];
+}
+
+// Canonical total (ora_csum) of arr[0..m) by ONE thread, in place (arr is private to it).
+__device__ __forceinline__ double local_csum_inplace(double* arr, int m) {
+    if (m <= 0) return 0.0;
+    while (m > 1) {
+        const int m2 = (m + 63) >> 6;
+        for (int c = 0; c < m2; c++) {
+            const int cnt = min(64, m - c * 64);
+            const double t = tree64_local([&](int i) { return arr[c * 64 + i]; }, cnt);
+            arr[c] = t;
+        }
+        m = m2;
+    }
+    return arr[0];
+}
+
+// K canonical 64-trees at once: lane holds v[0..K); lane q < K receives the tree of entry q.
+// Transpose through this wave's LDS buffer (K x 65 doubles), then per-lane register trees.
+template <int K>
+__device__ __forceinline__ double wave_trees(const double* v, double* buf) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < K; q++) buf[q * 65 + lane] = v[q];
+    __builtin_amdgcn_wave_barrier();
+    double r = 0.0;
+    if (lane < K) {
+        const double* row = buf + lane * 65;
+        r = tree64_local([&](int i) { return row[i]; }, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return r;
+}
+
+
 constexpr int kWaveScratch = 512;  // per-wave LDS scratch: lists up to 32768 terms
 constexpr int DIAG21[6] = {0, 6, 11, 15, 18, 20};
 
@@ -237,25 +305,69 @@ struct LinArgs {
     double* terms;    // T_N x nE
     double* Hpl;      // nE x 18
     int linearize;
+    double* chunks;   // per-wave chunk trees of rc (ceil(nE/64))
+    unsigned* counter;
+    double* out;      // canonical sum of rc
 };
 
 // computeActiveErrors + activeRobustChi2 terms (+ linearizeOplus + constructQuadraticForm)
+// canonical total of chunk sums c[0..m) with 256 threads (LDS level buffer), into *out
+__device__ __forceinline__ void block_finish_csum(const double* c, int m, int nterms, const double* single, double* out) {
+    __shared__ double lv[1024];
+    if (nterms <= 1) {
+        if (threadIdx.x == 0) *out = nterms == 1 ? *single : 0.0;
+        return;
+    }
+    if (m == 1) {
+        if (threadIdx.x == 0) *out = c[0];
+        return;
+    }
+    int m2 = (m + 63) >> 6;
+    for (int t = threadIdx.x; t < m2; t += blockDim.x)
+        lv[t] = tree64_local([&](int k) { return c[t * 64 + k]; }, min(64, m - t * 64));
+    __syncthreads();
+    if (threadIdx.x == 0) *out = local_csum_inplace(lv, m2);
+}
+
 __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.s.nE) return;
-    const int ei = a.s.aE[i];
-    const EdgeDev e = a.E[ei];
-    const Se3 T = a.T[e.kf];
-    const double X[3] = {a.X[3 * e.pt], a.X[3 * e.pt + 1], a.X[3 * e.pt + 2]};
-    double err[3];
-    edge_error(e, T, X, err);
-    for (int k = 0; k < 3; k++) a.err[3 * ei + k] = err[k];
-    const double chi = edge_chi2(e, err);
-    const int robust = a.robust[ei];
-    double r0 = chi, rho1 = 1.0;
-    if (robust) huber(e, chi, &r0, &rho1);
-    a.rc[i] = r0;
-    if (!a.linearize) return;
+    const bool valid = i < a.s.nE;
+    double r0 = 0.0, rho1 = 1.0;
+    double err[3] = {0, 0, 0};
+    EdgeDev e;
+    Se3 T;
+    double X[3] = {0, 0, 0};
+    int robust = 0;
+    if (valid) {
+        const int ei = a.s.aE[i];
+        e = a.E[ei];
+        T = a.T[e.kf];
+        X[0] = a.X[3 * e.pt]; X[1] = a.X[3 * e.pt + 1]; X[2] = a.X[3 * e.pt + 2];
+        edge_error(e, T, X, err);
+        for (int k = 0; k < 3; k++) a.err[3 * ei + k] = err[k];
+        const double chi = edge_chi2(e, err);
+        robust = a.robust[ei];
+        r0 = chi;
+        if (robust) huber(e, chi, &r0, &rho1);
+        a.rc[i] = r0;
+    }
+    // activeRobustChi2: chunk tree per wave (64 consecutive active edges), last block finishes
+    {
+        const double t = wave_tree(r0);
+        if ((threadIdx.x & 63) == 0) a.chunks[i >> 6] = t;
+        __threadfence();
+        __syncthreads();
+        __shared__ bool last;
+        if (threadIdx.x == 0) last = atomicAdd(a.counter, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (last) {
+            __threadfence();
+            block_finish_csum(a.chunks, (a.s.nE + 63) >> 6, a.s.nE, a.rc, a.out);
+            if (threadIdx.x == 0) *a.counter = 0;
+        }
+    }
+    if (!valid || !a.linearize) return;
+    {
     // linearizeOplus (.cpp:103-147 mono, 188-234 stereo)
     double p[3], R[9], A[9], B[18];
     se3_map(T, X, p);
@@ -341,6 +453,7 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
             a.Hpl[18 * (size_t)i + r * 3 + c] = h;
         }
     }
+    }
 }
 
 // Reduce chunk sums arr[0..m) (already level-1 trees) to the canonical total, one wave.
@@ -362,68 +475,20 @@ __device__ __forceinline__ double wave_lds_csum(double* arr, int m) {
 }
 
 
-// ---- exact thread-local emulation of the canonical 64-tree ------------------------
-// tree64_local(get, cnt): a[i] = i < cnt ? get(i) : 0 (i < 64), then a[i] += a[i+off]
-// for off = 32..1 -- the same pairing as wave_tree, evaluated in one thread.
-template <class G>
-__device__ __forceinline__ double tree64_local(G get, int cnt) {
-    double a[32];
-#pragma unroll
-    for (int i = 0; i < 32; i++) a[i] = (i < cnt ? get(i) : 0.0) + (i + 32 < cnt ? get(i + 32) : 0.0);
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1)
-#pragma unroll
-        for (int i = 0; i < off; i++) a[i] = a[i] + a[i + off];
-    return a[0];
-}
-
-// Canonical total (ora_csum) of arr[0..m) by ONE thread, in place (arr is private to it).
-__device__ __forceinline__ double local_csum_inplace(double* arr, int m) {
-    if (m <= 0) return 0.0;
-    while (m > 1) {
-        const int m2 = (m + 63) >> 6;
-        for (int c = 0; c < m2; c++) {
-            const int cnt = min(64, m - c * 64);
-            const double t = tree64_local([&](int i) { return arr[c * 64 + i]; }, cnt);
-            arr[c] = t;
-        }
-        m = m2;
-    }
-    return arr[0];
-}
-
-// K canonical 64-trees at once: lane holds v[0..K); lane q < K receives the tree of entry q.
-// Transpose through this wave's LDS buffer (K x 65 doubles), then per-lane register trees.
-template <int K>
-__device__ __forceinline__ double wave_trees(const double* v, double* buf) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int q = 0; q < K; q++) buf[q * 65 + lane] = v[q];
-    __builtin_amdgcn_wave_barrier();
-    double r = 0.0;
-    if (lane < K) {
-        const double* row = buf + lane * 65;
-        r = tree64_local([&](int i) { return row[i]; }, 64);
-    }
-    __builtin_amdgcn_wave_barrier();
-    return r;
-}
-
 constexpr int kChunks = 128;  // per-list LDS chunk sums: lists up to 8192 terms
 
 // per free pose: Hpp (upper 21) and b_p as canonical sums over its active edges (edge order).
-// Each lane loads the 27 terms of one edge; chunk trees via wave_trees; chunk sums reduced
-// per entry by one thread.
-__global__ void __launch_bounds__(256) k_pose_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
-                                                     double* bp) {
+// Each lane loads the 27 terms of one edge; one wave tree per entry and chunk; chunk sums
+// reduced per entry by one thread.
+__global__ void __launch_bounds__(1024) k_pose_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
+                                                      double* bp) {
     __shared__ double cs[27][kChunks];
-    __shared__ double tb[4][27 * 65];
     const int i = blockIdx.x;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int s0 = s.peStart[i], n = s.peStart[i + 1] - s0;
     const int m = (n + 63) >> 6;
     const int nE = s.nE;
-    for (int c = w; c < m; c += 4) {
+    for (int c = w; c < m; c += nw) {
         const int j = c * 64 + lane;
         const bool valid = j < n;
         const int a = valid ? s.peList[s0 + j] : 0;
@@ -433,12 +498,10 @@ __global__ void __launch_bounds__(256) k_pose_reduce(BaStructDev s, const double
             const int col = q < 21 ? T_HPP + q : T_BP + (q - 21);
             v[q] = valid ? terms[(size_t)col * nE + a] : 0.0;
         }
-        if (n == 1) {  // ora_csum returns a single term untouched
-            if (lane == 0)
-                for (int q = 0; q < 27; q++) cs[q][0] = v[q];
-        } else {
-            const double t = wave_trees<27>(v, tb[w]);
-            if (lane < 27) cs[lane][c] = t;
+#pragma unroll
+        for (int q = 0; q < 27; q++) {
+            const double t = n == 1 ? v[q] : wave_tree(v[q]);  // ora_csum keeps a single term untouched
+            if (lane == 0) cs[q][c] = t;
         }
     }
     __syncthreads();
@@ -450,63 +513,29 @@ __global__ void __launch_bounds__(256) k_pose_reduce(BaStructDev s, const double
     }
 }
 
-// per landmark (one thread): Hll (full 3x3) and b_l over its active edges (edge order);
-// typical tracks are short, so the 64-tree is emulated on the few live terms.
+// per (landmark, entry): Hll (full 3x3) and b_l over the landmark's active edges (edge order)
 __global__ void __launch_bounds__(256) k_land_reduce(BaStructDev s, const double* __restrict__ terms, double* Hll,
                                                      double* bl) {
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= s.nL) return;
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= 12 * s.nL) return;
+    const int l = g / 12, q = g % 12;
     const int s0 = s.leStart[l], n = s.leStart[l + 1] - s0;
-    const int nE = s.nE;
-    double res[12];
-    if (n <= 8) {
-        int ed[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) ed[j] = j < n ? s.leList[s0 + j] : 0;
-#pragma unroll
-        for (int q = 0; q < 12; q++) {
-            const int col = q < 9 ? T_HLL + q : T_BL + (q - 9);
-            double a[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) a[j] = j < n ? terms[(size_t)col * nE + ed[j]] : 0.0;
-            if (n == 1) {
-                res[q] = a[0];
-                continue;
-            }
-            // levels 32, 16, 8 only add the zero padding
-#pragma unroll
-            for (int j = 0; j < 8; j++) a[j] = ((a[j] + 0.0) + 0.0) + 0.0;
-#pragma unroll
-            for (int off = 4; off >= 1; off >>= 1)
-#pragma unroll
-                for (int j = 0; j < off; j++) a[j] = a[j] + a[j + off];
-            res[q] = a[0];
-        }
-    } else {
-        for (int q = 0; q < 12; q++) {
-            const int col = q < 9 ? T_HLL + q : T_BL + (q - 9);
-            const double* cp = terms + (size_t)col * nE;
-            const int m = (n + 63) >> 6;
-            double c0 = 0, c1 = 0, tot = 0;
-            // n <= 4096 (validated): level 1 chunk sums are consumed by a second 64-tree
-            double chunk[2];
-            if (m <= 2) {
-                for (int c = 0; c < m; c++)
-                    chunk[c] = tree64_local([&](int i) { return cp[s.leList[s0 + c * 64 + i]]; }, min(64, n - c * 64));
-                c0 = chunk[0];
-                c1 = m > 1 ? chunk[1] : 0.0;
-                tot = m == 1 ? c0 : tree64_local([&](int i) { return i == 0 ? c0 : c1; }, 2);
-            } else {
-                double lv[64];
-                for (int c = 0; c < m; c++)
-                    lv[c] = tree64_local([&](int i) { return cp[s.leList[s0 + c * 64 + i]]; }, min(64, n - c * 64));
-                tot = tree64_local([&](int i) { return lv[i]; }, m);
-            }
-            res[q] = tot;
-        }
+    const int col = q < 9 ? T_HLL + q : T_BL + (q - 9);
+    const double* cp = terms + (size_t)col * s.nE;
+    const int* li = s.leList + s0;
+    double v;
+    if (n == 1) {
+        v = cp[li[0]];
+    } else if (n <= 64) {
+        v = tree64_local([&](int k) { return cp[li[k]]; }, n);
+    } else {  // long tracks (<= 4096 edges, validated): chunk trees, then one more level
+        const int m = (n + 63) >> 6;
+        double c[64];
+        for (int t = 0; t < m; t++) c[t] = tree64_local([&](int k) { return cp[li[t * 64 + k]]; }, min(64, n - t * 64));
+        v = tree64_local([&](int k) { return c[k]; }, m);
     }
-    for (int q = 0; q < 9; q++) Hll[9 * l + q] = res[q];
-    for (int q = 0; q < 3; q++) bl[3 * l + q] = res[9 + q];
+    if (q < 9) Hll[9 * l + q] = v;
+    else bl[3 * l + (q - 9)] = v;
 }
 
 // computeLambdaInit: tau * max |diag| over poses and landmarks (order-free max)
@@ -580,25 +609,24 @@ __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double*
 // Schur complement block (i1, i2): S = [Hpp + lambda I] - csum_l BDinv_l,i1 B_l,i2^T
 // (upper triangle of the diagonal blocks), and b_s = b_p - csum_l B db.
 // Each lane loads the two 6x3 blocks of one landmark term once and feeds all entries.
-__global__ void __launch_bounds__(256) k_schur(BaStructDev s, const double* __restrict__ Emat,
-                                               const double* __restrict__ Hpl, const double* __restrict__ cb,
-                                               const double* Hpp, const double* bp, double lam_host, int use_dev,
-                                               const double* scal, double* S, double* bs) {
+__global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __restrict__ Emat,
+                                                const double* __restrict__ Hpl, const double* __restrict__ cb,
+                                                const double* Hpp, const double* bp, double lam_host, int use_dev,
+                                                const double* scal, double* S, double* bs) {
     __shared__ double cs[36][kChunks];
-    __shared__ double tb[4][36 * 65];
     const int blk = blockIdx.x;
     const int i1 = s.blkI[blk], i2 = s.blkJ[blk];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int s0 = s.blkStart[blk], n = s.blkStart[blk + 1] - s0;
     const int m = (n + 63) >> 6;
     const int nn = 6 * s.nP;
     const bool diag = i1 == i2;
     const int nent = diag ? 27 : 36;
-    for (int c = w; c < m; c += 4) {
+    for (int c = w; c < m; c += nw) {
         const int j = c * 64 + lane;
         const bool valid = j < n;
         const int a1 = valid ? s.pairA[s0 + j] : 0, a2 = valid ? s.pairB[s0 + j] : 0;
-        double E[18], B[18], v[36];
+        double E[18], B[18];
 #pragma unroll
         for (int q = 0; q < 18; q++) {
             E[q] = valid ? Emat[18 * (size_t)a1 + q] : 0.0;
@@ -609,29 +637,30 @@ __global__ void __launch_bounds__(256) k_schur(BaStructDev s, const double* __re
 #pragma unroll
             for (int r = 0; r < 6; r++)
 #pragma unroll
-                for (int cc = r; cc < 6; cc++, q++)
-                    v[q] = valid ? (E[r * 3] * B[cc * 3] + E[r * 3 + 1] * B[cc * 3 + 1]) + E[r * 3 + 2] * B[cc * 3 + 2] : 0.0;
+                for (int cc = r; cc < 6; cc++, q++) {
+                    const double v = valid ? (E[r * 3] * B[cc * 3] + E[r * 3 + 1] * B[cc * 3 + 1]) + E[r * 3 + 2] * B[cc * 3 + 2] : 0.0;
+                    const double t = n == 1 ? v : wave_tree(v);
+                    if (lane == 0) cs[q][c] = t;
+                }
 #pragma unroll
-            for (int r = 0; r < 6; r++) v[21 + r] = valid ? cb[6 * (size_t)a1 + r] : 0.0;
-#pragma unroll
-            for (int q2 = 27; q2 < 36; q2++) v[q2] = 0.0;
+            for (int r = 0; r < 6; r++) {
+                const double v = valid ? cb[6 * (size_t)a1 + r] : 0.0;
+                const double t = n == 1 ? v : wave_tree(v);
+                if (lane == 0) cs[21 + r][c] = t;
+            }
         } else {
 #pragma unroll
             for (int r = 0; r < 6; r++)
 #pragma unroll
-                for (int cc = 0; cc < 6; cc++)
-                    v[r * 6 + cc] = valid ? (E[r * 3] * B[cc * 3] + E[r * 3 + 1] * B[cc * 3 + 1]) + E[r * 3 + 2] * B[cc * 3 + 2] : 0.0;
-        }
-        if (n == 1) {
-            if (lane == 0)
-                for (int q = 0; q < 36; q++) cs[q][0] = v[q];
-        } else {
-            const double t = wave_trees<36>(v, tb[w]);
-            if (lane < 36) cs[lane][c] = t;
+                for (int cc = 0; cc < 6; cc++) {
+                    const double v = valid ? (E[r * 3] * B[cc * 3] + E[r * 3 + 1] * B[cc * 3 + 1]) + E[r * 3 + 2] * B[cc * 3 + 2] : 0.0;
+                    const double t = n == 1 ? v : wave_tree(v);
+                    if (lane == 0) cs[r * 6 + cc][c] = t;
+                }
         }
     }
     __syncthreads();
-    if (threadIdx.x >= nent) return;
+    if ((int)threadIdx.x >= nent) return;
     const int q = threadIdx.x;
     const double v = local_csum_inplace(cs[q], m);
     const double lambda = lam_of(lam_host, use_dev, scal);
@@ -741,15 +770,35 @@ __global__ void __launch_bounds__(256) k_ldlt(int n, double* Sg, const double* b
     }
 }
 
-// Register-resident LDL^T + solve for n <= 128 (<= 21 free keyframes), 256 threads.
-// Thread (wave w, lane) owns rows i = 4r + w (r < 32) of columns j = lane and lane + 64.
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), l);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// Register-resident LDL^T + solve for n <= 128 (<= 21 free keyframes), 1024 threads.
+// Thread (wave w < 16, lane) owns rows i = 16 r + w (r < 8) of columns j = lane, lane + 64.
 // Per 6-column panel: owners publish the panel rows to LDS (U), wave 0 factorises them
 // in registers and writes L (Lall[k][i] = L[i][k], Lpan[i][k - p0]) and d_k, then every
 // thread applies the panel's updates to its rows in k order.  Per-element operation
 // sequence identical to oracle ora_ldlt_solve.
+#ifdef ORB_LDLT_PROBE
+__device__ long long g_ldlt_probe[256];
+#define LDLT_PROBE(slot) \
+    do {                                                  \
+        if (threadIdx.x == 0) g_ldlt_probe[slot] = clock64(); \
+    } while (0)
+#else
+#define LDLT_PROBE(slot) \
+    do {                 \
+    } while (0)
+#endif
 constexpr int kLdltMax = 128;
-__global__ void __launch_bounds__(256) k_ldlt_reg(int n, const double* __restrict__ Sg, const double* bs, double* x,
-                                                  double* scal) {
+constexpr int kLdltWaves = 16;
+constexpr int kLdltRows = kLdltMax / kLdltWaves;
+__global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restrict__ Sg, const double* bs, double* x,
+                                                   double* scal) {
     extern __shared__ double lds[];
     double* Lall = lds;                    // n x n, Lall[k * n + i] = L[i][k]
     double* U = Lall + (size_t)n * n;      // 6 x kLdltMax panel rows
@@ -758,29 +807,32 @@ __global__ void __launch_bounds__(256) k_ldlt_reg(int n, const double* __restric
     double* y = dvec + kLdltMax;           // n
     __shared__ int ok;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    double R[2][32];
+    double R[2][kLdltRows];
 #pragma unroll
     for (int c = 0; c < 2; c++)
 #pragma unroll
-        for (int r = 0; r < 32; r++) {
-            const int i = 4 * r + w, j = lane + 64 * c;
+        for (int r = 0; r < kLdltRows; r++) {
+            const int i = kLdltWaves * r + w, j = lane + 64 * c;
             R[c][r] = (i < n && j < n && i <= j) ? Sg[(size_t)i * n + j] : 0.0;
         }
-    for (int q = tid; q < n; q += 256) y[q] = bs[q];
+    LDLT_PROBE(0);
+    for (int q = tid; q < n; q += blockDim.x) y[q] = bs[q];
     if (tid == 0) ok = 1;
     __syncthreads();
+    LDLT_PROBE(1);
     for (int p0 = 0; p0 < n; p0 += 6) {
         const int p1 = min(p0 + 6, n), pw = p1 - p0;
-        // publish panel rows (all columns)
+        LDLT_PROBE(10 + 4 * (p0 / 6));
 #pragma unroll
-        for (int r = 0; r < 32; r++) {
-            const int i = 4 * r + w;
+        for (int r = 0; r < kLdltRows; r++) {
+            const int i = kLdltWaves * r + w;
             if (i >= p0 && i < p1) {
                 U[(i - p0) * kLdltMax + lane] = R[0][r];
                 U[(i - p0) * kLdltMax + lane + 64] = R[1][r];
             }
         }
         __syncthreads();
+        LDLT_PROBE(11 + 4 * (p0 / 6));
         if (w == 0) {
             double u0[6], u1[6];
 #pragma unroll
@@ -793,35 +845,33 @@ __global__ void __launch_bounds__(256) k_ldlt_reg(int n, const double* __restric
             for (int t = 0; t < 6; t++) {
                 if (t >= pw || bad) break;
                 const int k = p0 + t;
-                const double d = __shfl(k < 64 ? u0[t] : u1[t], k & 63, 64);
+                const double d = readlane_d(k < 64 ? u0[t] : u1[t], k & 63);
                 if (d == 0.0) {
                     bad = true;
                     break;
                 }
-                // l_i = A[k][i] / d for every column i > k (lane-local)
-                const double l0 = (lane > k && lane < n) ? u0[t] / d : 0.0;
-                const double l1 = (lane + 64 > k && lane + 64 < n) ? u1[t] / d : 0.0;
-                if (lane > k && lane < n) {
-                    Lall[(size_t)k * n + lane] = l0;
-                    Lpan[lane * 6 + t] = l0;
-                }
-                if (lane + 64 > k && lane + 64 < n) {
-                    Lall[(size_t)k * n + lane + 64] = l1;
-                    Lpan[(lane + 64) * 6 + t] = l1;
-                }
-                if (lane == 0) dvec[k] = d;
-                // remaining panel rows i = p0 + t2 (t2 > t): A[i][j] -= l_i * A[k][j], j >= i
+                const bool a0 = lane > k && lane < n, a1 = lane + 64 > k && lane + 64 < n;
+                const double l0 = a0 ? u0[t] / d : 0.0;
+                const double l1 = a1 ? u1[t] / d : 0.0;
 #pragma unroll
                 for (int t2 = t + 1; t2 < 6; t2++) {
                     if (t2 >= pw) break;
                     const int i = p0 + t2;
-                    const double li = __shfl(i < 64 ? l0 : l1, i & 63, 64);
+                    const double li = readlane_d(i < 64 ? l0 : l1, i & 63);
                     if (lane >= i) u0[t2] -= li * u0[t];
                     if (lane + 64 >= i) u1[t2] -= li * u1[t];
                 }
+                if (a0) {
+                    Lall[(size_t)k * n + lane] = l0;
+                    Lpan[lane * 6 + t] = l0;
+                }
+                if (a1) {
+                    Lall[(size_t)k * n + lane + 64] = l1;
+                    Lpan[(lane + 64) * 6 + t] = l1;
+                }
+                if (lane == 0) dvec[k] = d;
             }
             if (bad && lane == 0) ok = 0;
-            // the panel rows after their in-panel updates are the U rows of the trailing update
 #pragma unroll
             for (int t = 0; t < 6; t++)
                 if (t < pw) {
@@ -830,8 +880,8 @@ __global__ void __launch_bounds__(256) k_ldlt_reg(int n, const double* __restric
                 }
         }
         __syncthreads();
+        LDLT_PROBE(12 + 4 * (p0 / 6));
         if (!ok) break;
-        // trailing rows i >= p1: v -= L[i][k] * A[k][j] for k = p0..p1-1 in order
         double u0[6], u1[6];
 #pragma unroll
         for (int t = 0; t < 6; t++) {
@@ -839,8 +889,8 @@ __global__ void __launch_bounds__(256) k_ldlt_reg(int n, const double* __restric
             u1[t] = t < pw ? U[t * kLdltMax + lane + 64] : 0.0;
         }
 #pragma unroll
-        for (int r = 0; r < 32; r++) {
-            const int i = 4 * r + w;
+        for (int r = 0; r < kLdltRows; r++) {
+            const int i = kLdltWaves * r + w;
             if (i >= p1 && i < n) {
                 double L[6];
 #pragma unroll
@@ -857,43 +907,95 @@ __global__ void __launch_bounds__(256) k_ldlt_reg(int n, const double* __restric
             }
         }
         __syncthreads();
+        LDLT_PROBE(13 + 4 * (p0 / 6));
     }
+    LDLT_PROBE(2);
     if (!ok) {
         if (tid == 0) scal[3] = 0.0;
         return;
     }
     if (w != 0) return;
-    // L y = b: per row, subtractions in k order
+    // L y = b: per row, subtractions in k order.  Operands of 8 steps are loaded ahead of
+    // the dependent chain (loads do not depend on acc).
     for (int r0 = 0; r0 < n; r0 += 64) {
         const int i = r0 + lane;
-        double acc = i < n ? y[i] : 0.0;
-        for (int k = 0; k < r0; k++)
-            if (i < n) acc -= Lall[(size_t)k * n + i] * y[k];
-        for (int k = r0; k < min(r0 + 64, n); k++) {
-            const double yk = __shfl(acc, k - r0, 64);
-            if (i > k && i < n) acc -= Lall[(size_t)k * n + i] * yk;
+        const bool on = i < n;
+        const int ic = on ? i : 0;
+        double acc = on ? y[i] : 0.0;
+        int k = 0;
+        for (; k + 8 <= r0; k += 8) {
+            double L8[8], Y8[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                L8[u] = Lall[(size_t)(k + u) * n + ic];
+                Y8[u] = y[k + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc -= L8[u] * Y8[u];
         }
-        if (i < n) y[i] = acc;
+        for (; k < r0; k++) acc -= Lall[(size_t)k * n + ic] * y[k];
+        const int kend = min(r0 + 64, n);
+        k = r0;
+        for (; k + 8 <= kend; k += 8) {
+            double L8[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) L8[u] = Lall[(size_t)(k + u) * n + ic];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const double yk = readlane_d(acc, k + u - r0);
+                if (i > k + u) acc -= L8[u] * yk;
+            }
+        }
+        for (; k < kend; k++) {
+            const double yk = readlane_d(acc, k - r0);
+            if (i > k) acc -= Lall[(size_t)k * n + ic] * yk;
+        }
+        if (on) y[i] = acc;
         __builtin_amdgcn_wave_barrier();
     }
+    LDLT_PROBE(3);
     for (int k = lane; k < n; k += 64) y[k] = y[k] / dvec[k];
     __builtin_amdgcn_wave_barrier();
     // L^T x = z: per row, subtractions in descending k order (L[k][i] = Lall[i * n + k])
     for (int r1 = n; r1 > 0; r1 -= 64) {
         const int r0 = max(r1 - 64, 0);
         const int i = r0 + lane;
-        double acc = i < r1 ? y[i] : 0.0;
-        for (int k = n - 1; k >= r1; k--)
-            if (i < r1) acc -= Lall[(size_t)i * n + k] * y[k];
-        for (int k = r1 - 1; k >= r0; k--) {
-            const double yk = __shfl(acc, k - r0, 64);
-            if (i < k) acc -= Lall[(size_t)i * n + k] * yk;
+        const bool on = i < r1;
+        const int ic = on ? i : r0;
+        double acc = on ? y[i] : 0.0;
+        int k = n - 1;
+        for (; k - 8 >= r1 - 1; k -= 8) {
+            double L8[8], Y8[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                L8[u] = Lall[(size_t)ic * n + (k - u)];
+                Y8[u] = y[k - u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc -= L8[u] * Y8[u];
         }
-        if (i < r1) y[i] = acc;
+        for (; k >= r1; k--) acc -= Lall[(size_t)ic * n + k] * y[k];
+        k = r1 - 1;
+        for (; k - 8 >= r0 - 1; k -= 8) {
+            double L8[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) L8[u] = Lall[(size_t)ic * n + (k - u)];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const double yk = readlane_d(acc, k - u - r0);
+                if (i < k - u) acc -= L8[u] * yk;
+            }
+        }
+        for (; k >= r0; k--) {
+            const double yk = readlane_d(acc, k - r0);
+            if (i < k) acc -= Lall[(size_t)ic * n + k] * yk;
+        }
+        if (on) y[i] = acc;
         __builtin_amdgcn_wave_barrier();
     }
     for (int k = lane; k < n; k += 64) x[k] = y[k];
     if (lane == 0) scal[3] = 1.0;
+    LDLT_PROBE(4);
 }
 
 // push + back-substitution (block_solver.hpp:457-484) + SparseOptimizer::update (oplus)
@@ -954,20 +1056,30 @@ __global__ void __launch_bounds__(256) k_pop(BaStructDev s, Se3* T, const Se3* T
     for (int k = 0; k < 3; k++) X[3 * pt + k] = Xbak[3 * pt + k];
 }
 
-// computeScale terms: x_j (lambda x_j + b_j)
-__global__ void __launch_bounds__(256) k_scale_terms(int n, const double* x, const double* b, double lam_host,
-                                                     int use_dev, const double* scal, double* out) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+// computeScale: csum_j x_j (lambda x_j + b_j) over poses then landmarks, one workgroup:
+// wave trees of 64 consecutive terms (coalesced), chunk sums reduced by one thread.
+__global__ void __launch_bounds__(1024) k_scale(int nP, int nL, const double* x, const double* bp, const double* bl,
+                                                double lam_host, int use_dev, const double* scal, double* out) {
+    __shared__ double lv[2048];
+    const int n = 6 * nP + 3 * nL;
     const double lambda = lam_of(lam_host, use_dev, scal);
-    out[j] = x[j] * (lambda * x[j] + b[j]);
-}
-
-// b vector (poses then landmarks) for computeScale
-__global__ void __launch_bounds__(256) k_copy_b(int nP, int nL, const double* bp, const double* bl, double* b) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < 6 * nP) b[j] = bp[j];
-    else if (j < 6 * nP + 3 * nL) b[j] = bl[j - 6 * nP];
+    auto term = [&](int j) {
+        const double b = j < 6 * nP ? bp[j] : bl[j - 6 * nP];
+        return x[j] * (lambda * x[j] + b);
+    };
+    if (n <= 1) {
+        if (threadIdx.x == 0) *out = n == 1 ? term(0) : 0.0;
+        return;
+    }
+    const int m = (n + 63) >> 6;   // <= 2048 (validated)
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int c = w; c < m; c += 16) {
+        const int j = c * 64 + lane;
+        const double t = wave_tree(j < n ? term(j) : 0.0);
+        if (lane == 0) lv[c] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *out = local_csum_inplace(lv, m);
 }
 
 // canonical sum of one list per workgroup (blockIdx.x selects the list), 1024 threads,
@@ -1103,6 +1215,7 @@ int BaEngine::carve(bool commit, size_t* total) {
     dCb_ = (double*)take(sizeof(double) * 6 * ne);
     dHplA_ = (double*)take(sizeof(double) * 18 * ne);
     dScal_ = (double*)take(sizeof(double) * 16);
+    dCounter_ = (unsigned*)take(sizeof(unsigned) * 16);
     dScratch_ = (double*)take(sizeof(double) * scratchN_);
     tmpA0_ = (double*)take(sizeof(double) * tmpN);
     tmpA1_ = (double*)take(sizeof(double) * tmpN);
@@ -1163,6 +1276,7 @@ int BaEngine::upload_problem(const ba_problem* P) {
         ORB_HIP_CHECK(hipMemsetAsync(dRobust_, 1, ne_, s));
         ORB_HIP_CHECK(hipMemsetAsync(dErr_, 0, sizeof(double) * 3 * ne_, s));
     }
+    ORB_HIP_CHECK(hipMemsetAsync(dCounter_, 0, sizeof(unsigned) * 16, s));
     ORB_HIP_CHECK(hipStreamSynchronize(s));  // host vectors above are pageable temporaries
     return 0;
 }
@@ -1267,6 +1381,7 @@ int BaEngine::build_structure(int level) {
         if (peStart[i + 1] - peStart[i] > 64 * kChunks) return -3;
     for (int l = 0; l < nL; l++)
         if (leStart[l + 1] - leStart[l] > 64 * 64) return -3;
+    if (6 * nP + 3 * nL > 2048 * 64 || nE > 1024 * 64 * 64) return -3;
     for (int b = 0; b < nBlk; b++)
         if (blkStart[b + 1] - blkStart[b] > 64 * kChunks) return -3;
     // pack and upload
@@ -1308,14 +1423,11 @@ static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate) {
     hipStream_t s = stream_;
     const BaStructDev& S = st_;
-    const int nE = S.nE, nP = S.nP, nL = S.nL, nv = 6 * nP + 3 * nL;
-    LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1};
+    const int nE = S.nE, nP = S.nP, nL = S.nL;
+    LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1, tmpA0_, dCounter_, dScal_ + 0};
     if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
-    CsumList c0{dRc_, nE, tmpA0_, tmpA1_, dScal_ + 0};
-    hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, c0, c0);
-    if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(256), 0, s, S, dTerms_, dHpp_, dBp_);
-    if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(nL, 256)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_);
-    if (nv) hipLaunchKernelGGL(k_copy_b, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dBp_, dBl_, dB_);
+    if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(1024), 0, s, S, dTerms_, dHpp_, dBp_);
+    if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(12 * nL, 256)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_);
     int use_dev = 0;
     if (iteration == 0) {
         hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, nP, nL, dHpp_, dHll_, dScal_);
@@ -1339,10 +1451,10 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         // setLambda + BlockSolver::solve
         if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
                                    lambda_, use_dev, dScal_, dEmat_, dCb_);
-        if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(256), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
+        if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(1024), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
                                        lambda_, use_dev, dScal_, dS_, dBs_);
         if (use_reg)
-            hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(256), regShm, s, n, dS_, dBs_, dX2_, dScal_);
+            hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_);
         else
             hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds);
         // push + update
@@ -1350,12 +1462,10 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
                                         dXbak_, dX2_, dHplA_, dHll_, dBl_, lambda_, use_dev, dScal_);
         // computeActiveErrors + activeRobustChi2 ; computeScale
         la.linearize = 0;
+        la.out = dScal_ + 1;
         if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
-        if (nv) hipLaunchKernelGGL(k_scale_terms, dim3(nblk(nv, 256)), dim3(256), 0, s, nv, dX2_, dB_, lambda_,
-                                   use_dev, dScal_, dScratch_);
-        CsumList c1{dRc_, nE, tmpA0_, tmpA1_, dScal_ + 1};
-        CsumList c2{dScratch_, nv, tmpB0_, tmpB1_, dScal_ + 2};
-        hipLaunchKernelGGL(k_csum, dim3(2), dim3(1024), 0, s, c1, c2);
+        hipLaunchKernelGGL(k_scale, dim3(1), dim3(1024), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_, use_dev, dScal_,
+                           dScal_ + 2);
         ORB_HIP_CHECK(hipGetLastError());
         ORB_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
         ORB_HIP_CHECK(hipStreamSynchronize(s));
@@ -1493,7 +1603,7 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     if (variant == 0) {
         const size_t shm = sizeof(double) * ((size_t)n * n + 14 * kLdltMax);
         if (n > kLdltMax) return -3;
-        hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(256), shm, 0, n, dS, dB, dX, dScal);
+        hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal);
     } else {
         hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), sizeof(double) * n + 16, 0, n, dS, dB, dX, dScal, 0);
     }
@@ -1503,6 +1613,22 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     ORB_HIP_CHECK(hipMemcpy(x, dX, sizeof(double) * n, hipMemcpyDeviceToHost));
     (void)hipFree(dS); (void)hipFree(dB); (void)hipFree(dX); (void)hipFree(dScal);
     return sc[3] != 0.0 ? 1 : 0;
+}
+
+__global__ void k_unit_wave_tree(const double* v, double* out) {
+    const double t = wave_tree(v[threadIdx.x]);
+    if (threadIdx.x == 0) *out = t;
+}
+
+int debug_wave_tree(const double* v64, double* out) {
+    double* d = nullptr;
+    ORB_HIP_CHECK(hipMalloc(&d, sizeof(double) * 65));
+    ORB_HIP_CHECK(hipMemcpy(d, v64, sizeof(double) * 64, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_unit_wave_tree, dim3(1), dim3(64), 0, 0, d, d + 64);
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipMemcpy(out, d + 64, sizeof(double), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return 0;
 }
 
 int debug_csum(const double* v, int n, double* out) {

@@ -87,6 +87,7 @@ private:
     double *dB_ = nullptr, *dX2_ = nullptr, *dS_ = nullptr, *dBs_ = nullptr, *dDinv_ = nullptr, *dDb_ = nullptr;
     double *dEmat_ = nullptr, *dCb_ = nullptr, *dScal_ = nullptr, *dScratch_ = nullptr, *dHplA_ = nullptr;
     double *tmpA0_ = nullptr, *tmpA1_ = nullptr, *tmpB0_ = nullptr, *tmpB1_ = nullptr;
+    unsigned* dCounter_ = nullptr;
     void* arena_ = nullptr;
     size_t arenaCap_ = 0;
     double* hScal_ = nullptr;      // pinned
@@ -100,5 +101,6 @@ private:
 
 int debug_ldlt(int n, const double* S, const double* b, double* x, int variant);
 int debug_csum(const double* v, int n, double* out);
+int debug_wave_tree(const double* v64, double* out);
 
 }  // namespace orbgpu

@@ -76,3 +76,13 @@ def test_ldlt_zero_pivot_fails(gpu):
     for variant in (0, 1):
         assert lib().orbgpu_unit_ldlt_solve(12, ptr(S), ptr(np.ones(12)), ptr(x), variant, C.byref(ok)) == 0
         assert ok.value == 0
+
+
+def test_wave_tree_matches_canonical_tree(gpu):
+    from c_orb_slam_amd._lib import lib
+    rng = np.random.default_rng(7)
+    for trial in range(20):
+        v = rng.normal(0, 1, 64) * 10.0 ** rng.integers(-10, 10, 64)
+        out = C.c_double()
+        assert lib().orbgpu_unit_wave_tree(ptr(np.ascontiguousarray(v)), C.byref(out)) == 0
+        assert out.value == _ora_csum(v), trial

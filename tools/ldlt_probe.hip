@@ -1,0 +1,41 @@
+// ldlt_probe.hip -- phase timing (shader cycles) of k_ldlt_reg on an n=84 SPD system.
+#define ORB_LDLT_PROBE 1
+#include "../c_orb_slam_amd/csrc/ba.hip"
+#include <cstdio>
+#include <vector>
+#include <random>
+
+int main() {
+    const int n = 84;
+    std::mt19937 g(1);
+    std::normal_distribution<double> N(0, 1);
+    std::vector<double> A(n * n), S(n * n, 0), b(n);
+    for (auto& v : A) v = N(g);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            double t = 0;
+            for (int k = 0; k < n; k++) t += A[i * n + k] * A[j * n + k];
+            S[i * n + j] = t + (i == j ? n : 0);
+        }
+    for (auto& v : b) v = N(g);
+    double *dS, *dB, *dX, *dScal;
+    hipMalloc(&dS, 8 * n * n); hipMalloc(&dB, 8 * n); hipMalloc(&dX, 8 * n); hipMalloc(&dScal, 128);
+    hipMemcpy(dS, S.data(), 8 * n * n, hipMemcpyHostToDevice);
+    hipMemcpy(dB, b.data(), 8 * n, hipMemcpyHostToDevice);
+    const size_t shm = sizeof(double) * ((size_t)n * n + 14 * orbgpu::kLdltMax);
+    for (int rep = 0; rep < 3; rep++) {
+        hipLaunchKernelGGL(orbgpu::k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal);
+        hipDeviceSynchronize();
+    }
+    long long p[256];
+    hipMemcpyFromSymbol(p, HIP_SYMBOL(orbgpu::g_ldlt_probe), sizeof(p));
+    printf("load %lld | panels %lld | fwd %lld | bwd %lld  (cycles)\n", p[1] - p[0], p[2] - p[1], p[3] - p[2], p[4] - p[3]);
+    long long pub = 0, ph1 = 0, tr = 0;
+    for (int k = 0; k < 14; k++) {
+        pub += p[11 + 4 * k] - p[10 + 4 * k];
+        ph1 += p[12 + 4 * k] - p[11 + 4 * k];
+        tr += p[13 + 4 * k] - p[12 + 4 * k];
+    }
+    printf("publish %lld | phase1 %lld | trailing %lld  (cycles, 14 panels)\n", pub, ph1, tr);
+    return 0;
+}
