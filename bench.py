@@ -200,6 +200,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(frames, Rs, args.cpu_seconds)
 
+    # local BA (BASELINE metric part 3): SURVEY config 4 on every rank (replicas), own timed region
+    ba = bench_local_ba(args, world, rank, dist if world > 1 else None, dev)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ba["cpu_baseline"] = ba_cpu_baseline(args.cpu_seconds / 4)
+
     if rank == 0:
         stage_ms = {k: round(v / args.steps, 4) for k, v in stage_acc.items()}
         out = {
@@ -211,11 +216,70 @@ def main():
                        "nfeatures": NFEAT, "nlevels": 8, "scale_factor": 1.2, "fast_th": [20, 7],
                        "frames_per_step": B, "parallelism": f"replicas{world}"},
             "matches_per_s": round(tot_match / dt, 1), "keypoints_per_frame": round(tot_kp / frames_total, 1),
-            "stage_ms_per_step": stage_ms, "roofline": roof, "cpu_baseline": cpu,
+            "stage_ms_per_step": stage_ms, "roofline": roof, "cpu_baseline": cpu, "local_ba": ba,
         }
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+BA_KEYS = ("kf_id", "kf_Tcw", "kf_local", "kf_cam", "pt_id", "pt_pos", "edge_pt", "edge_kf", "edge_obs",
+           "edge_inv_sigma2")
+
+
+def bench_local_ba(args, world, rank, dist, dev):
+    """Optimizer::LocalBundleAdjustment on SURVEY config 4 (EuRoC-shaped: 15 local + 15 fixed
+    keyframes, 3000 points, ~15k edges, 70% stereo, 5% outliers); one iter = one LM solve()."""
+    import torch
+    sys.path.insert(0, str(ROOT / "tests"))
+    from ba_cases import ba_problem
+    from c_orb_slam_amd.optimizer import LocalBundleAdjustment
+    pr = ba_problem(0)
+    a = [pr[k] for k in BA_KEYS]
+    for _ in range(3):
+        LocalBundleAdjustment(*a)
+    reps = max(5, args.steps * 2)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    its = 0
+    for _ in range(reps):
+        r = LocalBundleAdjustment(*a)
+        its += sum(r["iterations"])
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt, its], dtype=torch.float64, device=dev)
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:])
+        dt, its = float(t[0].item()), int(t[1].item())
+    ne = len(pr["edge_pt"])
+    return {"metric": "local-BA iter/s", "value": round(its / dt, 1), "unit": "iter/s",
+            "ms_per_call": round(dt / (reps * max(world, 1)) * 1e3 * max(world, 1), 3),
+            "edges_per_s": round(its * ne / dt, 1), "calls": reps * world,
+            "config": {"workload": "euroc_mh05_stereo_local_ba (SURVEY config 4)", "local_kfs": 15, "fixed_kfs": 15,
+                       "points": len(pr["pt_id"]), "edges": ne,
+                       "stereo_edges": int((pr["edge_obs"][:, 2] >= 0).sum()),
+                       "lm": "optimize(5) + gating + optimize(10)", "parallelism": f"replicas{world}"},
+            "dtype": "f64 (f32 I/O)"}
+
+
+def ba_cpu_baseline(budget_s):
+    """Oracle LocalBundleAdjustment (C restatement of the g2o path, 1 thread) on the same problem."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    from ba_cases import ba_problem
+    pr = ba_problem(0)
+    t0 = time.perf_counter()
+    its = calls = 0
+    while True:
+        o = oracle_lib.oracle_local_ba(pr)
+        its += sum(o["iterations"])
+        calls += 1
+        if time.perf_counter() - t0 > budget_s and calls >= 2:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(its / dt, 2), "unit": "iter/s", "cores": 1, "kind": "port",
+            "sample": f"{calls} LocalBundleAdjustment calls on config 4 ({its} LM solves), oracle/ba.c -O2, 1 thread"}
 
 
 def cpu_baseline(frames, Rs, budget_s):
