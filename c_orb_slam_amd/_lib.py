@@ -100,6 +100,15 @@ def lib():
     L.PnPsolver_iterate_batch.argtypes = [i32, vp, i32, vp, vp, vp, vp, vp, vp]
     L.PnPsolver_get_state.argtypes = [vp, P(i32), P(i32), P(i32)]
     L.Optimizer_LocalBundleAdjustment.argtypes = [vp, vp, vp]
+    L.Optimizer_BundleAdjustment.argtypes = [vp, i32, i32, vp, vp]
+    L.Optimizer_LocalBundleAdjustment_sharded.argtypes = [vp, vp, vp, vp]
+    L.Optimizer_BundleAdjustment_sharded.argtypes = [vp, vp, i32, i32, vp, vp]
+    L.Optimizer_partition_points.argtypes = [vp, i32, vp]
+    L.orbgpu_comm_unique_id.argtypes = [vp]
+    L.orbgpu_comm_init_rccl.argtypes = [i32, i32, vp, P(vp)]
+    L.orbgpu_comm_init_local.argtypes = [i32, vp]
+    L.orbgpu_comm_rank.argtypes = [vp, P(i32), P(i32)]
+    L.orbgpu_comm_destroy.argtypes = [vp]
     L.Optimizer_last_trace.argtypes = [vp, vp, i32, P(i32), vp, vp, i32, P(i32)]
     L.Optimizer_last_timings.argtypes = [vp]
     L.orbgpu_unit_ldlt_solve.argtypes = [i32, vp, vp, vp, i32, P(i32)]

@@ -612,7 +612,7 @@ __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double*
 __global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __restrict__ Emat,
                                                 const double* __restrict__ Hpl, const double* __restrict__ cb,
                                                 const double* Hpp, const double* bp, double lam_host, int use_dev,
-                                                const double* scal, double* S, double* bs) {
+                                                const double* scal, double* S, double* bs, int own) {
     __shared__ double cs[36][kChunks];
     const int blk = blockIdx.x;
     const int i1 = s.blkI[blk], i2 = s.blkJ[blk];
@@ -664,8 +664,8 @@ __global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __r
     const int q = threadIdx.x;
     const double v = local_csum_inplace(cs[q], m);
     const double lambda = lam_of(lam_host, use_dev, scal);
-    if (diag && q >= 21) {
-        bs[6 * i1 + (q - 21)] = bp[6 * i1 + (q - 21)] - v;
+    if (diag && q >= 21) {  // a shard that does not own the pose terms contributes -sum only
+        bs[6 * i1 + (q - 21)] = (own ? bp[6 * i1 + (q - 21)] : 0.0) - v;
         return;
     }
     int r, c;
@@ -678,7 +678,7 @@ __global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __r
         c = q % 6;
     }
     double h = 0;
-    if (diag) {
+    if (diag && own) {
         h = Hpp[21 * i1 + q];
         if (c == r) h += lambda;
     }
@@ -1059,11 +1059,13 @@ __global__ void __launch_bounds__(256) k_pop(BaStructDev s, Se3* T, const Se3* T
 // computeScale: csum_j x_j (lambda x_j + b_j) over poses then landmarks, one workgroup:
 // wave trees of 64 consecutive terms (coalesced), chunk sums reduced by one thread.
 __global__ void __launch_bounds__(1024) k_scale(int nP, int nL, const double* x, const double* bp, const double* bl,
-                                                double lam_host, int use_dev, const double* scal, double* out) {
+                                                double lam_host, int use_dev, const double* scal, double* out,
+                                                int poses) {
     __shared__ double lv[2048];
     const int n = 6 * nP + 3 * nL;
     const double lambda = lam_of(lam_host, use_dev, scal);
-    auto term = [&](int j) {
+    auto term = [&](int j) {  // poses == 0: a shard that does not own the (replicated) pose terms
+        if (j < 6 * nP && !poses) return 0.0;
         const double b = j < 6 * nP ? bp[j] : bl[j - 6 * nP];
         return x[j] * (lambda * x[j] + b);
     };
@@ -1246,12 +1248,17 @@ int BaEngine::upload_problem(const ba_problem* P) {
     eKf_.assign(P->edge_kf, P->edge_kf + ne_);
     kfLocal_.assign(P->kf_local, P->kf_local + nkf_);
     kfFixed_.resize(nkf_);
-    for (int k = 0; k < nkf_; k++) kfFixed_[k] = (!P->kf_local[k] || P->kf_id[k] == 0) ? 1 : 0;
+    for (int k = 0; k < nkf_; k++)  // BundleAdjustment: every keyframe is a vertex, fixed iff mnId == 0 (Optimizer.cc:79)
+        kfFixed_[k] = ((!mode_.global && !P->kf_local[k]) || P->kf_id[k] == 0) ? 1 : 0;
+    if (mode_.global) kfLocal_.assign(nkf_, 1);
+    ptHasEdge_.assign(npt_, 0);
+    for (int i = 0; i < ne_; i++) ptHasEdge_[P->edge_pt[i]] = 1;
     std::vector<Se3> T(nkf_);
     for (int k = 0; k < nkf_; k++) host_se3_from_Tcw(P->kf_Tcw + 16 * k, T[k]);
     std::vector<double> X(3 * (size_t)npt_);
     for (size_t q = 0; q < X.size(); q++) X[q] = (double)P->pt_pos[q];
-    const float thMono = (float)std::sqrt(5.991), thStereo = (float)std::sqrt(7.815);
+    // Huber deltas: LocalBundleAdjustment sqrt(5.991) (Optimizer.cc:585), BundleAdjustment sqrt(5.99) (:87)
+    const float thMono = (float)std::sqrt(mode_.global ? 5.99 : 5.991), thStereo = (float)std::sqrt(7.815);
     std::vector<EdgeDev> E(ne_);
     for (int i = 0; i < ne_; i++) {
         EdgeDev& e = E[i];
@@ -1273,7 +1280,7 @@ int BaEngine::upload_problem(const ba_problem* P) {
     if (ne_) {
         ORB_HIP_CHECK(hipMemcpyAsync(dE_, E.data(), sizeof(EdgeDev) * ne_, hipMemcpyHostToDevice, s));
         ORB_HIP_CHECK(hipMemsetAsync(dLevel_, 0, ne_, s));
-        ORB_HIP_CHECK(hipMemsetAsync(dRobust_, 1, ne_, s));
+        ORB_HIP_CHECK(hipMemsetAsync(dRobust_, (mode_.global && !mode_.robust) ? 0 : 1, ne_, s));
         ORB_HIP_CHECK(hipMemsetAsync(dErr_, 0, sizeof(double) * 3 * ne_, s));
     }
     ORB_HIP_CHECK(hipMemsetAsync(dCounter_, 0, sizeof(unsigned) * 16, s));
@@ -1292,6 +1299,23 @@ int BaEngine::build_structure(int level) {
             kfAct[eKf_[i]] = 1;
             ptAct[ePt_[i]] = 1;
         }
+    if (comm_) {
+        // shards agree on the pose set: a keyframe is active if any shard has an active edge
+        // on it (its pose index must be the same everywhere); also the global edge/landmark counts
+        int nLloc = 0;
+        for (int p = 0; p < npt_; p++) nLloc += ptAct[p];
+        std::vector<double> red(nkf_ + 2);
+        for (int k = 0; k < nkf_; k++) red[k] = kfAct[k];
+        red[nkf_] = (double)aE.size();
+        red[nkf_ + 1] = (double)nLloc;
+        ORB_HIP_CHECK(hipMemcpyAsync(dScratch_, red.data(), sizeof(double) * red.size(), hipMemcpyHostToDevice, stream_));
+        if (int e = comm_->allreduce(dScratch_, red.size(), RedOp::Sum, stream_)) return e;
+        ORB_HIP_CHECK(hipMemcpyAsync(red.data(), dScratch_, sizeof(double) * red.size(), hipMemcpyDeviceToHost, stream_));
+        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        for (int k = 0; k < nkf_; k++) kfAct[k] = red[k] > 0 ? 1 : 0;
+        nEglob_ = (int)red[nkf_];
+        nLglob_ = (int)red[nkf_ + 1];
+    }
     std::vector<int32_t> poseKf, landPt;
     for (int k = 0; k < nkf_; k++)
         if (kfAct[k] && !kfFixed_[k]) poseKf.push_back(k);
@@ -1300,6 +1324,10 @@ int BaEngine::build_structure(int level) {
         if (ptAct[p]) landPt.push_back(p);
     std::sort(landPt.begin(), landPt.end(), [&](int a, int b) { return ptId_[a] < ptId_[b]; });
     const int nE = (int)aE.size(), nP = (int)poseKf.size(), nL = (int)landPt.size();
+    if (!comm_) {
+        nEglob_ = nE;
+        nLglob_ = nL;
+    }
     std::vector<int32_t> poseIdx(nkf_, -1), landIdx(npt_, -1);
     for (int i = 0; i < nP; i++) poseIdx[poseKf[i]] = i;
     for (int i = 0; i < nL; i++) landIdx[landPt[i]] = i;
@@ -1420,17 +1448,35 @@ int BaEngine::build_structure(int level) {
 static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 
 // OptimizationAlgorithmLevenberg::solve (optimization_algorithm_levenberg.cpp:59-164)
+// Sharded (comm_ set): the pose rows of H and the Schur complement are sums over the shards'
+// points, so each shard reduces its own edges and the exchange steps are
+//   after buildSystem:  all-reduce(sum) {Hpp, b_p, chi2}           -> identical pose system
+//   lambda init:        all-reduce(max) {max|diag|, lambda0}
+//   per trial:          all-reduce(sum) {S, b_s} (own pose terms and lambda added by rank 0),
+//                       replicated LDL^T, local back-substitution,
+//                       all-reduce(sum) {chi2_new, scale (rank 0 owns the pose terms), stop}
 int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate) {
     hipStream_t s = stream_;
     const BaStructDev& S = st_;
     const int nE = S.nE, nP = S.nP, nL = S.nL;
+    const bool own = !comm_ || comm_->rank() == 0;
     LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1, tmpA0_, dCounter_, dScal_ + 0};
+    if (comm_ && !nE) ORB_HIP_CHECK(hipMemsetAsync(dScal_, 0, 2 * sizeof(double), s));
     if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
     if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(1024), 0, s, S, dTerms_, dHpp_, dBp_);
     if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(12 * nL, 256)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_);
+    if (comm_) {
+        const RedBuf rb[3] = {{dHpp_, 21 * (size_t)nP}, {dBp_, 6 * (size_t)nP}, {dScal_, 1}};
+        ORB_HIP_CHECK(hipGetLastError());
+        if (int e = comm_->allreduce(rb, 3, RedOp::Sum, s)) return e;
+    }
     int use_dev = 0;
     if (iteration == 0) {
         hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, nP, nL, dHpp_, dHll_, dScal_);
+        if (comm_) {
+            ORB_HIP_CHECK(hipGetLastError());
+            if (int e = comm_->allreduce(dScal_ + 4, 2, RedOp::Max, s)) return e;
+        }
         use_dev = 1;  // lambda known on the device only until the first readback
         ni_ = 2;
         nBad_ = 0;
@@ -1447,12 +1493,20 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
     const bool use_reg = n <= kLdltMax && regShm <= ldsMax_;
     if (!use_reg && shm > ldsMax_) return -3;
+    // the in-place (global memory) LDL^T leaves fill-in outside the Schur pattern: clear S
+    const bool clearS = !use_reg && !in_lds;
     do {
         // setLambda + BlockSolver::solve
         if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
                                    lambda_, use_dev, dScal_, dEmat_, dCb_);
+        if (clearS && n) ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * (size_t)n * n, s));
         if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(1024), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
-                                       lambda_, use_dev, dScal_, dS_, dBs_);
+                                       lambda_, use_dev, dScal_, dS_, dBs_, own ? 1 : 0);
+        if (comm_) {
+            const RedBuf rb[2] = {{dS_, (size_t)n * n}, {dBs_, (size_t)n}};
+            ORB_HIP_CHECK(hipGetLastError());
+            if (int e = comm_->allreduce(rb, 2, RedOp::Sum, s)) return e;
+        }
         if (use_reg)
             hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_);
         else
@@ -1465,10 +1519,17 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         la.out = dScal_ + 1;
         if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
         hipLaunchKernelGGL(k_scale, dim3(1), dim3(1024), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_, use_dev, dScal_,
-                           dScal_ + 2);
+                           dScal_ + 2, own ? 1 : 0);
         ORB_HIP_CHECK(hipGetLastError());
+        if (comm_) {
+            hScal_[32] = (stop && *stop) ? 1.0 : 0.0;
+            ORB_HIP_CHECK(hipMemcpyAsync(dScal_ + 6, hScal_ + 32, sizeof(double), hipMemcpyHostToDevice, s));
+            const RedBuf rb[2] = {{dScal_ + 1, 2}, {dScal_ + 6, 1}};
+            if (int e = comm_->allreduce(rb, 2, RedOp::Sum, s)) return e;
+        }
         ORB_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
         ORB_HIP_CHECK(hipStreamSynchronize(s));
+        if (comm_) stopRed_ = hScal_[6] != 0.0;
         if (!haveChi) {
             currentChi = iniChi = hScal_[0];
             haveChi = true;
@@ -1501,7 +1562,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         qmax++;
         trace_.trial_chi2.push_back(tempChi);
         trace_.trial_lambda.push_back(lambda_);
-    } while (rho < 0 && qmax < 10 && !(stop && *stop));
+    } while (rho < 0 && qmax < 10 && !stopped(stop));
     trace_.solve_ini_chi2.push_back(iniChi);
     trace_.solve_chi2.push_back(currentChi);
     *terminate = false;
@@ -1519,12 +1580,24 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
 int BaEngine::optimize(int iterations, const volatile bool* stop, int* its) {
     *its = 0;
     bool ok = true;
-    for (int i = 0; i < iterations && !(stop && *stop) && ok; i++) {
+    for (int i = 0; i < iterations && !stopped(stop) && ok; i++) {
         bool term = false;
         if (int e = lm_solve(i, stop, &term)) return e;
         ok = !term;
         (*its)++;
     }
+    return 0;
+}
+
+// sharded: every rank sees the same stop decision (any rank's flag stops all)
+int BaEngine::reduce_stop(const volatile bool* stop) {
+    if (!comm_) return 0;
+    hScal_[32] = (stop && *stop) ? 1.0 : 0.0;
+    ORB_HIP_CHECK(hipMemcpyAsync(dScal_ + 6, hScal_ + 32, sizeof(double), hipMemcpyHostToDevice, stream_));
+    if (int e = comm_->allreduce(dScal_ + 6, 1, RedOp::Sum, stream_)) return e;
+    ORB_HIP_CHECK(hipMemcpyAsync(hScal_ + 33, dScal_ + 6, sizeof(double), hipMemcpyDeviceToHost, stream_));
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    stopRed_ = hScal_[33] != 0.0;
     return 0;
 }
 
@@ -1539,40 +1612,59 @@ int BaEngine::gate_edges(int final_check, uint8_t* erase) {
     return 0;
 }
 
-int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R) {
+int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, Comm* comm, const BaMode* mode) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     trace_ = BaTrace{};
+    comm_ = comm;
+    mode_ = mode ? *mode : BaMode{};
+    stopRed_ = false;
     std::memcpy(R->kf_Tcw, P->kf_Tcw, sizeof(float) * 16 * P->n_kf);
     std::memcpy(R->pt_pos, P->pt_pos, sizeof(float) * 3 * P->n_pt);
     if (P->n_edge) std::memset(R->edge_erase, 0, P->n_edge);
     R->aborted = 0;
     R->iterations[0] = R->iterations[1] = 0;
     R->n_erased = 0;
-    if ((stop && *stop) || P->n_edge == 0) {
+    if (!comm_ && ((stop && *stop) || P->n_edge == 0)) {
         R->aborted = 1;
         return 0;
     }
     if (int e = upload_problem(P)) return e;
+    if (comm_) {  // every shard takes the same early-return decision
+        if (int e = reduce_stop(stop)) return e;
+    }
     double t_struct = 0;
     auto ts = clk::now();
     if (int e = build_structure(0)) return e;
     t_struct += std::chrono::duration<double, std::milli>(clk::now() - ts).count();
-    if (st_.nP + st_.nL > 0)
-        if (int e = optimize(5, stop, &R->iterations[0])) return e;
-    if (!(stop && *stop)) {
-        std::vector<uint8_t> flag(ne_);
-        if (int e = gate_edges(0, flag.data())) return e;
-        for (int i = 0; i < ne_; i++)
-            if (flag[i]) level_[i] = 1;
-        ts = clk::now();
-        if (int e = build_structure(0)) return e;
-        t_struct += std::chrono::duration<double, std::milli>(clk::now() - ts).count();
-        if (st_.nE > 0 && st_.nP + st_.nL > 0)
-            if (int e = optimize(10, stop, &R->iterations[1])) return e;
+    if (comm_ && (stopRed_ || nEglob_ == 0)) {  // Optimizer.cc:655-657 (and no edges at all)
+        R->aborted = 1;
+        return 0;
     }
-    if (int e = gate_edges(1, R->edge_erase)) return e;
-    for (int i = 0; i < ne_; i++) R->n_erased += R->edge_erase[i];
+    if (mode_.global) {
+        // Optimizer::BundleAdjustment: initializeOptimization(); optimize(nIterations) (Optimizer.cc:190-191)
+        if (st_.nP + nLglob_ > 0)
+            if (int e = optimize(mode_.iterations, stop, &R->iterations[0])) return e;
+    } else {
+        if (st_.nP + nLglob_ > 0)
+            if (int e = optimize(5, stop, &R->iterations[0])) return e;
+        if (comm_) {
+            if (int e = reduce_stop(stop)) return e;
+        }
+        if (!stopped(stop)) {
+            std::vector<uint8_t> flag(ne_);
+            if (int e = gate_edges(0, flag.data())) return e;
+            for (int i = 0; i < ne_; i++)
+                if (flag[i]) level_[i] = 1;
+            ts = clk::now();
+            if (int e = build_structure(0)) return e;
+            t_struct += std::chrono::duration<double, std::milli>(clk::now() - ts).count();
+            if (nEglob_ > 0 && st_.nP + nLglob_ > 0)
+                if (int e = optimize(10, stop, &R->iterations[1])) return e;
+        }
+        if (int e = gate_edges(1, R->edge_erase)) return e;
+        for (int i = 0; i < ne_; i++) R->n_erased += R->edge_erase[i];
+    }
     std::vector<Se3> T(nkf_);
     std::vector<double> X(3 * (size_t)npt_);
     if (nkf_) ORB_HIP_CHECK(hipMemcpyAsync(T.data(), dT_, sizeof(Se3) * nkf_, hipMemcpyDeviceToHost, stream_));
@@ -1580,9 +1672,14 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R) 
     ORB_HIP_CHECK(hipStreamSynchronize(stream_));
     for (int k = 0; k < nkf_; k++)
         if (kfLocal_[k]) host_se3_to_Tcw(T[k], R->kf_Tcw + 16 * k);
-    for (size_t q = 0; q < X.size(); q++) R->pt_pos[q] = (float)X[q];
+    // BundleAdjustment writes back only the points that got a vertex (vbNotIncludedMP, Optimizer.cc:217-219);
+    // LocalBundleAdjustment writes back every local map point (Optimizer.cc:771-777)
+    for (int p = 0; p < npt_; p++)
+        if (!mode_.global || ptHasEdge_[p])
+            for (int k = 0; k < 3; k++) R->pt_pos[3 * p + k] = (float)X[3 * p + k];
     last_ms[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     last_ms[1] = t_struct;
+    comm_ = nullptr;
     return 0;
 }
 

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "../../include/orbslam_gpu.h"
+#include "comm.hpp"
 
 namespace orbgpu {
 
@@ -50,11 +51,23 @@ struct BaTrace {
     std::vector<double> solve_ini_chi2, solve_chi2, trial_chi2, trial_lambda;
 };
 
+// Which reference optimisation a run restates.
+struct BaMode {
+    bool global = false;   // false: Optimizer::LocalBundleAdjustment (Optimizer.cc:453-778)
+                           // true:  Optimizer::BundleAdjustment (Optimizer.cc:49-237)
+    int iterations = 10;   // global: optimize(nIterations)
+    bool robust = true;    // global: bRobust
+};
+
 class BaEngine {
 public:
     ~BaEngine();
     int init();
-    int run(const ba_problem* P, const volatile bool* stop, ba_result* R);
+    // comm == nullptr: the whole problem on this device.  Otherwise P is this rank's
+    // shard (every keyframe, the rank's own map points and all of their edges) and
+    // every rank of comm calls run() with the same keyframes and mode.
+    int run(const ba_problem* P, const volatile bool* stop, ba_result* R, Comm* comm = nullptr,
+            const BaMode* mode = nullptr);
     const BaTrace& trace() const { return trace_; }
     double last_ms[4] = {0, 0, 0, 0};  // total, structure (host), solves (device+control), io
 
@@ -65,6 +78,9 @@ private:
     int lm_solve(int iteration, const volatile bool* stop, bool* terminate);
     int gate_edges(int final_check, uint8_t* erase);
     int carve(bool commit, size_t* total);
+    bool stopped(const volatile bool* stop) const { return comm_ ? stopRed_ : (stop && *stop); }
+    int reduce_stop(const volatile bool* stop);
+    bool sharded() const { return comm_ && comm_->size() > 1; }
 
     hipStream_t stream_ = nullptr;
     // problem (device)
@@ -76,7 +92,7 @@ private:
     double* dErr_ = nullptr;       // ne x 3, last computed _error
     // host mirror of the static problem
     std::vector<int32_t> kfId_, ptId_, ePt_, eKf_;
-    std::vector<uint8_t> kfFixed_, kfLocal_, level_;
+    std::vector<uint8_t> kfFixed_, kfLocal_, level_, ptHasEdge_;
     // structure
     BaStructDev st_{};
     std::vector<int32_t> hStruct_;
@@ -93,6 +109,11 @@ private:
     double* hScal_ = nullptr;      // pinned
     size_t scratchN_ = 0;
     size_t ldsMax_ = 0;
+    // sharding
+    Comm* comm_ = nullptr;
+    bool stopRed_ = false;
+    int nEglob_ = 0, nLglob_ = 0;
+    BaMode mode_{};
     // LM state (g2o OptimizationAlgorithmLevenberg)
     double lambda_ = 0, ni_ = 2;
     int nBad_ = 0;

@@ -4,6 +4,7 @@
 #include <cstring>
 #include <new>
 #include <unordered_set>
+#include <vector>
 
 #include "ba.hpp"
 
@@ -40,19 +41,125 @@ int validate(const ba_problem* P, const ba_result* R) {
     if (6LL * P->n_kf > 6LL * 4096) return ORB_E_CAPACITY;
     return ORB_OK;
 }
-}  // namespace
 
-extern "C" {
-
-int Optimizer_LocalBundleAdjustment(const ba_problem* P, const volatile bool* stop, ba_result* R) {
+int run_ba(const ba_problem* P, const volatile bool* stop, ba_result* R, orbgpu::Comm* comm,
+           const orbgpu::BaMode* mode) {
     if (int v = validate(P, R)) return v;
     int rc = 0;
     orbgpu::BaEngine* e = engine(&rc);
     if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
-    const int r = e->run(P, stop, R);
+    const int r = e->run(P, stop, R, comm, mode);
     if (r == -1) return ORB_E_INVALID;
     if (r == -3) return ORB_E_CAPACITY;
+    if (r == ORB_E_NODEVICE || r == ORB_E_HIP) return r;
     return r ? ORB_E_HIP : ORB_OK;
+}
+}  // namespace
+
+struct orbgpu_comm_t {};  // opaque: a handle is an orbgpu::Comm*
+
+static orbgpu::Comm* as_comm(orbgpu_comm_h h) { return reinterpret_cast<orbgpu::Comm*>(h); }
+
+extern "C" {
+
+int Optimizer_LocalBundleAdjustment(const ba_problem* P, const volatile bool* stop, ba_result* R) {
+    return run_ba(P, stop, R, nullptr, nullptr);
+}
+
+int Optimizer_BundleAdjustment(const ba_problem* P, int nIterations, int bRobust, const volatile bool* stop,
+                               ba_result* R) {
+    if (nIterations < 0) return ORB_E_INVALID;
+    orbgpu::BaMode m;
+    m.global = true;
+    m.iterations = nIterations;
+    m.robust = bRobust != 0;
+    return run_ba(P, stop, R, nullptr, &m);
+}
+
+int Optimizer_LocalBundleAdjustment_sharded(const ba_problem* shard, orbgpu_comm_h comm, const volatile bool* stop,
+                                            ba_result* R) {
+    if (!comm) return ORB_E_INVALID;
+    return run_ba(shard, stop, R, as_comm(comm), nullptr);
+}
+
+int Optimizer_BundleAdjustment_sharded(const ba_problem* shard, orbgpu_comm_h comm, int nIterations, int bRobust,
+                                       const volatile bool* stop, ba_result* R) {
+    if (!comm || nIterations < 0) return ORB_E_INVALID;
+    orbgpu::BaMode m;
+    m.global = true;
+    m.iterations = nIterations;
+    m.robust = bRobust != 0;
+    return run_ba(shard, stop, R, as_comm(comm), &m);
+}
+
+int Optimizer_partition_points(const ba_problem* P, int nranks, int32_t* pt_rank) {
+    if (!P || nranks < 1 || P->n_kf < 0 || P->n_pt < 0 || P->n_edge < 0) return ORB_E_INVALID;
+    if (P->n_pt && !pt_rank) return ORB_E_INVALID;
+    if (P->n_edge && (!P->edge_pt || !P->edge_kf)) return ORB_E_INVALID;
+    if (P->n_kf && !P->kf_id) return ORB_E_INVALID;
+    // reference keyframe of a point = keyframe of its first observation (edge order);
+    // keyframe weight = edges of the points it references
+    std::vector<int32_t> ref(P->n_pt, -1), nedge(P->n_pt, 0);
+    for (int i = 0; i < P->n_edge; i++) {
+        const int pt = P->edge_pt[i], kf = P->edge_kf[i];
+        if (pt < 0 || pt >= P->n_pt || kf < 0 || kf >= P->n_kf) return ORB_E_INVALID;
+        if (ref[pt] < 0) ref[pt] = kf;
+        nedge[pt]++;
+    }
+    std::vector<int64_t> w(P->n_kf, 0);
+    int64_t W = 0;
+    for (int p = 0; p < P->n_pt; p++)
+        if (ref[p] >= 0) {
+            w[ref[p]] += nedge[p];
+            W += nedge[p];
+        }
+    // contiguous keyframe blocks in mnId order with ~equal edge weight
+    std::vector<int32_t> order(P->n_kf);
+    for (int k = 0; k < P->n_kf; k++) order[k] = k;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return P->kf_id[a] < P->kf_id[b]; });
+    std::vector<int32_t> kfRank(P->n_kf, 0);
+    int64_t acc = 0;
+    for (int32_t k : order) {
+        // block of the keyframe = where the middle of its weight falls
+        const int64_t mid2 = 2 * acc + w[k];
+        int r = W > 0 ? (int)((mid2 * nranks) / (2 * W)) : 0;
+        kfRank[k] = std::min(std::max(r, 0), nranks - 1);
+        acc += w[k];
+    }
+    for (int p = 0; p < P->n_pt; p++) pt_rank[p] = ref[p] >= 0 ? kfRank[ref[p]] : 0;
+    return ORB_OK;
+}
+
+int orbgpu_comm_unique_id(uint8_t* id) {
+    if (!id) return ORB_E_INVALID;
+    return orbgpu::rccl_unique_id(id);
+}
+
+int orbgpu_comm_init_rccl(int nranks, int rank, const uint8_t* id, orbgpu_comm_h* out) {
+    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) return ORB_E_INVALID;
+    int rc = 0;
+    orbgpu::Comm* c = orbgpu::rccl_comm_create(nranks, rank, id, &rc);
+    *out = reinterpret_cast<orbgpu_comm_h>(c);
+    return rc;
+}
+
+int orbgpu_comm_init_local(int nranks, orbgpu_comm_h* out) {
+    if (!out || nranks < 1 || nranks > 64) return ORB_E_INVALID;
+    std::vector<orbgpu::Comm*> v = orbgpu::local_comm_group(nranks);
+    for (int r = 0; r < nranks; r++) out[r] = reinterpret_cast<orbgpu_comm_h>(v[r]);
+    return ORB_OK;
+}
+
+int orbgpu_comm_rank(orbgpu_comm_h h, int* rank, int* size) {
+    if (!h) return ORB_E_INVALID;
+    if (rank) *rank = as_comm(h)->rank();
+    if (size) *size = as_comm(h)->size();
+    return ORB_OK;
+}
+
+int orbgpu_comm_destroy(orbgpu_comm_h h) {
+    delete as_comm(h);
+    return ORB_OK;
 }
 
 int Optimizer_last_trace(double* solve_ini_chi2, double* solve_chi2, int solve_cap, int* n_solves,

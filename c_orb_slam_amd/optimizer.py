@@ -1,11 +1,20 @@
-"""Host mirror of ORB_SLAM2::Optimizer::LocalBundleAdjustment over the C ABI.
+"""Host mirror of ORB_SLAM2::Optimizer (LocalBundleAdjustment, BundleAdjustment) over the C ABI.
 
 LocalBundleAdjustment(...) takes the arrays the reference gathers from the
 covisibility graph (Optimizer.cc:456-653, see include/orbslam_gpu.h ba_problem)
 and returns what it writes back: keyframe poses, map point positions and the
-(keyframe, map point) observations to erase.
+(keyframe, map point) observations to erase.  BundleAdjustment(...) is
+Optimizer::BundleAdjustment (Optimizer.cc:49-237, GlobalBundleAdjustemnt's body).
+
+Keyframe-block sharding across GPUs: partition_points() assigns
+every map point to the rank owning its reference keyframe's block,
+shard_problem() cuts a rank's shard (all keyframes, own points and their
+edges), the *_sharded calls run the LM with one all-reduce of the partial
+Schur complement per trial (RCCL across processes, or an in-process group of
+threads on one device), and merge_shards() reassembles the full result.
 """
 import ctypes as C
+import threading
 
 import numpy as np
 
@@ -14,6 +23,51 @@ from ._lib import ba_problem, ba_result, check, lib, ptr
 _FIELDS = (("kf_id", np.int32), ("kf_Tcw", np.float32), ("kf_local", np.uint8), ("kf_cam", np.float32),
            ("pt_id", np.int32), ("pt_pos", np.float32), ("edge_pt", np.int32), ("edge_kf", np.int32),
            ("edge_obs", np.float32), ("edge_inv_sigma2", np.float32))
+FIELDS = tuple(n for n, _ in _FIELDS)
+
+
+class _Packed:
+    """Contiguous copies of a problem + its ba_problem/ba_result structs (kept alive together)."""
+
+    def __init__(self, arrays):
+        a = {}
+        for (name, dt), v in zip(_FIELDS, arrays):
+            a[name] = np.ascontiguousarray(v, dt)
+        self.a = a
+        self.nkf, self.npt, self.ne = len(a["kf_id"]), len(a["pt_id"]), len(a["edge_pt"])
+        self.P = ba_problem(self.nkf, ptr(a["kf_id"]), ptr(a["kf_Tcw"]), ptr(a["kf_local"]), ptr(a["kf_cam"]),
+                            self.npt, ptr(a["pt_id"]), ptr(a["pt_pos"]), self.ne, ptr(a["edge_pt"]),
+                            ptr(a["edge_kf"]), ptr(a["edge_obs"]), ptr(a["edge_inv_sigma2"]))
+        self.T = np.zeros((self.nkf, 16), np.float32)
+        self.X = np.zeros((self.npt, 3), np.float32)
+        self.er = np.zeros(max(self.ne, 1), np.uint8)
+        self.R = ba_result(ptr(self.T), ptr(self.X), ptr(self.er))
+
+    def result(self, trace):
+        R = self.R
+        out = dict(kf_Tcw=self.T, pt_pos=self.X, edge_erase=self.er[:self.ne].astype(bool),
+                   iterations=tuple(R.iterations), n_erased=R.n_erased, aborted=bool(R.aborted))
+        if trace:
+            out.update(last_trace())
+        return out
+
+
+def _args(problem):
+    return [problem[k] for k in FIELDS]
+
+
+def last_trace():
+    """LM trace of the calling thread's last run (per solve: initial/final chi2; per trial: chi2, lambda)."""
+    cap = 4096
+    si, sc, tc, tl = (np.zeros(cap) for _ in range(4))
+    ns, nt = C.c_int(), C.c_int()
+    check(lib().Optimizer_last_trace(ptr(si), ptr(sc), cap, C.byref(ns), ptr(tc), ptr(tl), cap, C.byref(nt)))
+    return dict(solve_ini_chi2=si[:ns.value], solve_chi2=sc[:ns.value], trial_chi2=tc[:nt.value],
+                trial_lambda=tl[:nt.value])
+
+
+def _stop_ref(stop):
+    return C.byref(stop) if stop is not None else None
 
 
 def LocalBundleAdjustment(kf_id, kf_Tcw, kf_local, kf_cam, pt_id, pt_pos, edge_pt, edge_kf, edge_obs, edge_inv_sigma2,
@@ -21,34 +75,155 @@ def LocalBundleAdjustment(kf_id, kf_Tcw, kf_local, kf_cam, pt_id, pt_pos, edge_p
     """-> dict(kf_Tcw, pt_pos, edge_erase, iterations, n_erased, aborted[, trace])
 
     stop: optional ctypes.c_bool shared with another thread (pbStopFlag)."""
-    L = lib()
-    a = {}
-    for (name, dt), v in zip(_FIELDS, (kf_id, kf_Tcw, kf_local, kf_cam, pt_id, pt_pos, edge_pt, edge_kf, edge_obs,
-                                       edge_inv_sigma2)):
-        a[name] = np.ascontiguousarray(v, dt)
-    nkf, npt, ne = len(a["kf_id"]), len(a["pt_id"]), len(a["edge_pt"])
-    P = ba_problem(nkf, ptr(a["kf_id"]), ptr(a["kf_Tcw"]), ptr(a["kf_local"]), ptr(a["kf_cam"]), npt, ptr(a["pt_id"]),
-                   ptr(a["pt_pos"]), ne, ptr(a["edge_pt"]), ptr(a["edge_kf"]), ptr(a["edge_obs"]),
-                   ptr(a["edge_inv_sigma2"]))
-    T = np.zeros((nkf, 16), np.float32)
-    X = np.zeros((npt, 3), np.float32)
-    er = np.zeros(max(ne, 1), np.uint8)
-    R = ba_result(ptr(T), ptr(X), ptr(er))
-    check(L.Optimizer_LocalBundleAdjustment(C.byref(P), C.byref(stop) if stop is not None else None, C.byref(R)),
+    k = _Packed((kf_id, kf_Tcw, kf_local, kf_cam, pt_id, pt_pos, edge_pt, edge_kf, edge_obs, edge_inv_sigma2))
+    check(lib().Optimizer_LocalBundleAdjustment(C.byref(k.P), _stop_ref(stop), C.byref(k.R)),
           "Optimizer_LocalBundleAdjustment")
-    out = dict(kf_Tcw=T, pt_pos=X, edge_erase=er[:ne].astype(bool), iterations=tuple(R.iterations),
-               n_erased=R.n_erased, aborted=bool(R.aborted))
-    if trace:
-        cap = 4096
-        si, sc, tc, tl = (np.zeros(cap) for _ in range(4))
-        ns, nt = C.c_int(), C.c_int()
-        check(L.Optimizer_last_trace(ptr(si), ptr(sc), cap, C.byref(ns), ptr(tc), ptr(tl), cap, C.byref(nt)))
-        out.update(solve_ini_chi2=si[:ns.value], solve_chi2=sc[:ns.value], trial_chi2=tc[:nt.value],
-                   trial_lambda=tl[:nt.value])
-    return out
+    return k.result(trace)
+
+
+def BundleAdjustment(problem, nIterations=10, bRobust=False, stop=None, trace=False):
+    """Optimizer::BundleAdjustment(vpKFs, vpMP, nIterations, pbStopFlag, nLoopKF, bRobust) (Optimizer.cc:49).
+    LoopClosing runs it with nIterations=10, bRobust=false (LoopClosing.cc:650)."""
+    k = _Packed(_args(problem))
+    check(lib().Optimizer_BundleAdjustment(C.byref(k.P), int(nIterations), int(bool(bRobust)), _stop_ref(stop),
+                                           C.byref(k.R)), "Optimizer_BundleAdjustment")
+    return k.result(trace)
 
 
 def last_timings():
     ms = np.zeros(2)
     check(lib().Optimizer_last_timings(ptr(ms)))
     return ms
+
+
+# ------------------------------------------------------------------ sharding
+def partition_points(problem, nranks):
+    """pt_rank[p]: keyframe-block owner of every map point (Optimizer_partition_points, host only)."""
+    k = _Packed(_args(problem))
+    out = np.zeros(max(k.npt, 1), np.int32)
+    check(lib().Optimizer_partition_points(C.byref(k.P), int(nranks), ptr(out)), "Optimizer_partition_points")
+    return out[:k.npt]
+
+
+def shard_problem(problem, pt_rank, rank):
+    """Rank `rank`'s shard: every keyframe, its own points and all of their edges, in the original
+    (reference creation) order.  Adds pt_index / edge_index: positions in the full problem."""
+    pts = np.flatnonzero(np.asarray(pt_rank) == rank).astype(np.int64)
+    remap = np.full(len(problem["pt_id"]), -1, np.int64)
+    remap[pts] = np.arange(len(pts))
+    ep = np.asarray(problem["edge_pt"])
+    edges = np.flatnonzero(remap[ep] >= 0)
+    sh = {k: problem[k] for k in ("kf_id", "kf_Tcw", "kf_local", "kf_cam")}
+    sh["pt_id"] = np.asarray(problem["pt_id"])[pts]
+    sh["pt_pos"] = np.asarray(problem["pt_pos"])[pts]
+    sh["edge_pt"] = remap[ep[edges]].astype(np.int32)
+    sh["edge_kf"] = np.asarray(problem["edge_kf"])[edges]
+    sh["edge_obs"] = np.asarray(problem["edge_obs"])[edges]
+    sh["edge_inv_sigma2"] = np.asarray(problem["edge_inv_sigma2"])[edges]
+    sh["pt_index"] = pts
+    sh["edge_index"] = edges
+    return sh
+
+
+def merge_shards(problem, shards, results):
+    """Full-problem outputs from per-rank results (poses are identical on every rank: take rank 0's)."""
+    npt, ne = len(problem["pt_id"]), len(problem["edge_pt"])
+    X = np.zeros((npt, 3), np.float32)
+    er = np.zeros(ne, bool)
+    for sh, r in zip(shards, results):
+        X[sh["pt_index"]] = r["pt_pos"]
+        er[sh["edge_index"]] = r["edge_erase"]
+    r0 = results[0]
+    out = dict(kf_Tcw=r0["kf_Tcw"], pt_pos=X, edge_erase=er, iterations=r0["iterations"],
+               n_erased=int(er.sum()), aborted=r0["aborted"])
+    for k in ("solve_ini_chi2", "solve_chi2", "trial_chi2", "trial_lambda"):
+        if k in r0:
+            out[k] = r0[k]
+    return out
+
+
+class Comm:
+    """Exchange handle of a sharded BA rank (orbgpu_comm_h)."""
+
+    def __init__(self, h):
+        self._h = h
+
+    @staticmethod
+    def unique_id():
+        """RCCL unique id (rank 0); distribute the 128 bytes to every rank."""
+        buf = (C.c_uint8 * 128)()
+        check(lib().orbgpu_comm_unique_id(buf), "orbgpu_comm_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, nranks, rank, uid):
+        h = C.c_void_p()
+        check(lib().orbgpu_comm_init_rccl(int(nranks), int(rank), (C.c_uint8 * 128)(*uid), C.byref(h)),
+              "orbgpu_comm_init_rccl")
+        return cls(h)
+
+    @classmethod
+    def local_group(cls, nranks):
+        hs = (C.c_void_p * nranks)()
+        check(lib().orbgpu_comm_init_local(int(nranks), hs), "orbgpu_comm_init_local")
+        return [cls(C.c_void_p(h)) for h in hs]
+
+    @property
+    def rank_size(self):
+        r, s = C.c_int(), C.c_int()
+        check(lib().orbgpu_comm_rank(self._h, C.byref(r), C.byref(s)))
+        return r.value, s.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbgpu_comm_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+
+def LocalBundleAdjustmentSharded(shard, comm, stop=None, trace=False):
+    k = _Packed(_args(shard))
+    check(lib().Optimizer_LocalBundleAdjustment_sharded(C.byref(k.P), comm._h, _stop_ref(stop), C.byref(k.R)),
+          "Optimizer_LocalBundleAdjustment_sharded")
+    return k.result(trace)
+
+
+def BundleAdjustmentSharded(shard, comm, nIterations=10, bRobust=False, stop=None, trace=False):
+    k = _Packed(_args(shard))
+    check(lib().Optimizer_BundleAdjustment_sharded(C.byref(k.P), comm._h, int(nIterations), int(bool(bRobust)),
+                                                   _stop_ref(stop), C.byref(k.R)),
+          "Optimizer_BundleAdjustment_sharded")
+    return k.result(trace)
+
+
+def run_sharded_local(problem, nranks, mode="local", nIterations=10, bRobust=False, trace=False, pt_rank=None):
+    """Run the sharded protocol with `nranks` in-process ranks (threads) on the current device;
+    returns (merged result, per-rank results).  mode: "local" or "global"."""
+    if pt_rank is None:
+        pt_rank = partition_points(problem, nranks)
+    shards = [shard_problem(problem, pt_rank, r) for r in range(nranks)]
+    comms = Comm.local_group(nranks)
+    results = [None] * nranks
+    errors = [None] * nranks
+
+    def work(r):
+        try:
+            if mode == "local":
+                results[r] = LocalBundleAdjustmentSharded(shards[r], comms[r], trace=trace)
+            else:
+                results[r] = BundleAdjustmentSharded(shards[r], comms[r], nIterations, bRobust, trace=trace)
+        except Exception as e:  # noqa: BLE001 -- re-raised below
+            errors[r] = e
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(nranks)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for c in comms:
+        c.close()
+    for e in errors:
+        if e is not None:
+            raise e
+    return merge_shards(problem, shards, results), results

@@ -296,6 +296,44 @@ typedef struct ba_result {
  * stop may be NULL; it is read between LM iterations and trials like g2o's
  * force-stop flag. */
 int Optimizer_LocalBundleAdjustment(const ba_problem* P, const volatile bool* stop, ba_result* R);
+/* static void Optimizer::BundleAdjustment(vpKFs, vpMP, nIterations, pbStopFlag, nLoopKF, bRobust)
+ *                                                          Optimizer.cc:49-237
+ * (GlobalBundleAdjustemnt, Optimizer.cc:41-47, passes every keyframe and map point.)
+ * Every keyframe is a vertex, fixed iff kf_id == 0 (kf_local is ignored); one
+ * optimize(nIterations); Huber deltas sqrt(5.99)/sqrt(7.815) when bRobust; no outlier
+ * gating.  R->kf_Tcw: every keyframe; R->pt_pos: points with >= 1 edge updated
+ * (vbNotIncludedMP points copied); R->iterations[0] = optimize() iterations. */
+int Optimizer_BundleAdjustment(const ba_problem* P, int nIterations, int bRobust, const volatile bool* stop,
+                               ba_result* R);
+
+/* ----------------------------------------------------------------------
+ * Keyframe-block sharded BA across GPUs: one process (or
+ * thread) per rank, map points partitioned by the block of their reference
+ * keyframe, poses replicated.  Per LM trial the ranks all-reduce the partial
+ * Schur complement {S, b_s} and the scalars {chi2, scale, stop}; every rank
+ * solves the identical reduced system.  Pass each rank the SAME keyframes and
+ * its own points + all of their edges (edge order preserved); the results are
+ * the rank's points / edges and the (identical) poses.
+ * ---------------------------------------------------------------------- */
+typedef struct orbgpu_comm_t* orbgpu_comm_h;
+/* RCCL over xGMI: rank 0 calls orbgpu_comm_unique_id, the caller distributes the
+ * 128 bytes (e.g. MPI / torch.distributed), every rank calls init_rccl with the
+ * HIP device it runs on already current.  ORB_E_NODEVICE if librccl is absent. */
+int orbgpu_comm_unique_id(uint8_t* id128);
+int orbgpu_comm_init_rccl(int nranks, int rank, const uint8_t* id128, orbgpu_comm_h* out);
+/* `nranks` in-process ranks (one host thread each, one device): out[0..nranks). */
+int orbgpu_comm_init_local(int nranks, orbgpu_comm_h* out);
+int orbgpu_comm_rank(orbgpu_comm_h h, int* rank, int* size);
+int orbgpu_comm_destroy(orbgpu_comm_h h);
+/* Keyframe-block partition: pt_rank[p] = rank owning point p.  Reference keyframe
+ * of a point = keyframe of its first edge; keyframes in mnId order are cut into
+ * nranks contiguous blocks of ~equal edge weight.  Host only (no device needed). */
+int Optimizer_partition_points(const ba_problem* P, int nranks, int32_t* pt_rank);
+int Optimizer_LocalBundleAdjustment_sharded(const ba_problem* shard, orbgpu_comm_h comm,
+                                            const volatile bool* stop, ba_result* R);
+int Optimizer_BundleAdjustment_sharded(const ba_problem* shard, orbgpu_comm_h comm, int nIterations,
+                                       int bRobust, const volatile bool* stop, ba_result* R);
+
 /* LM trace of the calling thread's last run (for diagnostics / parity tests):
  * per solve() the initial and final robust chi2, per trial the chi2 and lambda. */
 int Optimizer_last_trace(double* solve_ini_chi2, double* solve_chi2, int solve_cap, int* n_solves,

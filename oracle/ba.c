@@ -792,7 +792,10 @@ static int optimize(ba_ctx* c, int iterations, const volatile int* stop)
     return it;
 }
 
-int ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_result* R, ora_ba_trace* trace)
+/* global = 0: Optimizer::LocalBundleAdjustment (Optimizer.cc:453-778);
+ * global = 1: Optimizer::BundleAdjustment (Optimizer.cc:49-237) with nIterations / bRobust. */
+static int ba_run(const ora_ba_problem* P, int global, int nIterations, int bRobust, const volatile int* stop,
+                  ora_ba_result* R, ora_ba_trace* trace)
 {
     ba_ctx C;
     memset(&C, 0, sizeof(C));
@@ -828,13 +831,14 @@ int ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_resul
     for (int k = 0; k < c->nkf; k++) {
         se3_from_Tcw(&P->kf_Tcw[16 * k], &c->T[k]);
         c->kfId[k] = P->kf_id[k];
-        c->kfFixed[k] = !P->kf_local[k] || P->kf_id[k] == 0;
+        c->kfFixed[k] = (!global && !P->kf_local[k]) || P->kf_id[k] == 0;   /* Optimizer.cc:79 / 524, 547 */
     }
     for (int p = 0; p < c->npt; p++) {
         c->ptId[p] = P->pt_id[p];
         for (int j = 0; j < 3; j++) c->X[3 * p + j] = (double)P->pt_pos[3 * p + j];
     }
-    const float thMono = (float)sqrt(5.991), thStereo = (float)sqrt(7.815);
+    /* Huber deltas: sqrt(5.991) in LocalBundleAdjustment (585), sqrt(5.99) in BundleAdjustment (87) */
+    const float thMono = (float)sqrt(global ? 5.99 : 5.991), thStereo = (float)sqrt(7.815);
     for (int i = 0; i < c->ne; i++) {
         ba_edge* e = &c->E[i];
         e->pt = P->edge_pt[i];
@@ -846,7 +850,7 @@ int ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_resul
         e->fx = cam[0]; e->fy = cam[1]; e->cx = cam[2]; e->cy = cam[3]; e->bf = cam[4];
         e->delta = (double)(e->stereo ? thStereo : thMono);
         e->dsqr = e->delta * e->delta;
-        e->robust = 1;
+        e->robust = global ? (bRobust != 0) : 1;
         e->level = 0;
     }
     /* outputs default to the inputs (early abort writes nothing back) */
@@ -862,6 +866,14 @@ int ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_resul
     }
 
     build_structure(c, 0);
+    if (global) {   /* initializeOptimization(); optimize(nIterations); no gating (Optimizer.cc:190-191) */
+        if (c->nP + c->nL > 0) R->iterations[0] = optimize(c, nIterations, stop);
+        for (int k = 0; k < c->nkf; k++) se3_to_Tcw(&c->T[k], &R->kf_Tcw[16 * k]);
+        for (int p = 0; p < c->npt; p++)
+            if (c->ptIdx[p] >= 0)   /* vbNotIncludedMP points keep their position (217-219) */
+                for (int j = 0; j < 3; j++) R->pt_pos[3 * p + j] = (float)c->X[3 * p + j];
+        goto done;
+    }
     if (c->nP + c->nL > 0) R->iterations[0] = optimize(c, 5, stop);
     if (!stop_set(stop)) {
         for (int i = 0; i < c->ne; i++) {   /* Optimizer.cc:674-706 */
@@ -891,4 +903,15 @@ done:
     free(c->peStart); free(c->leStart); free(c->peList); free(c->leList); free(c->terms);
     free(c->Hpp); free(c->bp); free(c->Hll); free(c->bl); free(c->x); free(c->b); free(c->scratch);
     return 0;
+}
+
+int ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_result* R, ora_ba_trace* trace)
+{
+    return ba_run(P, 0, 0, 1, stop, R, trace);
+}
+
+int ora_global_ba(const ora_ba_problem* P, int nIterations, int bRobust, const volatile int* stop, ora_ba_result* R,
+                  ora_ba_trace* trace)
+{
+    return ba_run(P, 1, nIterations, bRobust, stop, R, trace);
 }

@@ -209,6 +209,10 @@ typedef struct {
 double ora_csum(double* v, int n);
 int   ora_ldlt_solve(double* S, int n, const double* b, double* x);
 int   ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_result* R, ora_ba_trace* trace);
+/* Optimizer::BundleAdjustment (Optimizer.cc:49-237): all keyframes vertices (fixed iff id 0),
+ * one optimize(nIterations), Huber sqrt(5.99)/sqrt(7.815) iff bRobust, no gating. */
+int   ora_global_ba(const ora_ba_problem* P, int nIterations, int bRobust, const volatile int* stop,
+                    ora_ba_result* R, ora_ba_trace* trace);
 
 #ifdef __cplusplus
 }

@@ -106,3 +106,93 @@ def ba_problem(seed=0, n_local=15, n_fixed=15, n_pt=3000, stereo_frac=0.7, outli
                 edge_pt=np.array(edges_pt, np.int32), edge_kf=np.array(edges_kf, np.int32),
                 edge_obs=np.array(obs, np.float32), edge_inv_sigma2=np.array(isig, np.float32),
                 Tcw_true=np.array(Tcw_true), Xw_true=Xw)
+
+
+KITTI = (718.856, 718.856, 607.1928, 185.2157, 386.1448)   # Stereo/KITTI00-02.yaml:8-25
+KITTI_WH = (1241, 376)
+
+
+def _rot_y(a):
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+
+
+def global_ba_problem(seed=0, n_kf=64, pts_per_kf=150, obs_range=(3, 10), stereo_frac=0.5, cam=KITTI,
+                      pose_noise=(0.02, 0.2), point_noise=0.1):
+    """Merged-map global-BA-shaped problem (KITTI intrinsics).
+
+    Keyframes ~1 m apart along a gently turning drive; each keyframe creates `pts_per_kf`
+    points 5-40 m ahead, each observed by U{obs_range} consecutive keyframes starting at
+    its creator (visibility-checked, >= 2 observations).  No gross outliers: LoopClosing
+    runs BundleAdjustment with bRobust=false (LoopClosing.cc:650).  Keyframe mnId = index
+    (id 0 fixed); edges in map-point order, each point's observations in shuffled order.
+    Vectorised numpy (10^5-10^6 edges in seconds)."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = cam
+    W, H = KITTI_WH
+    yaw = np.cumsum(rng.normal(0, 0.02, n_kf))
+    Rwc = np.stack([_rot_y(a) for a in yaw])
+    step = np.stack([np.sin(yaw), np.zeros(n_kf), np.cos(yaw)], 1)
+    twc = np.cumsum(step, 0) - step[0]
+    Rcw = np.transpose(Rwc, (0, 2, 1))
+    tcw = -np.einsum("kij,kj->ki", Rcw, twc)
+    # candidate points in each creator keyframe's frame
+    n = n_kf * pts_per_kf
+    creator = np.repeat(np.arange(n_kf), pts_per_kf)
+    z = rng.uniform(5, 40, n)
+    u = rng.uniform(20, W - 20, n)
+    v = rng.uniform(20, H - 20, n)
+    Xc = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    Xw = np.einsum("nij,nj->ni", Rwc[creator], Xc) + twc[creator]
+    lo, hi = obs_range
+    k = rng.integers(lo, hi + 1, n)
+    pe, ke = [], []
+    for j in range(hi):                               # j-th observer = creator + j
+        kf = creator + j
+        ok = (j < k) & (kf < n_kf)
+        kfc = np.minimum(kf, n_kf - 1)
+        Xcj = np.einsum("nij,nj->ni", Rcw[kfc], Xw) + tcw[kfc]
+        zz = Xcj[:, 2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            uu, vv = fx * Xcj[:, 0] / zz + cx, fy * Xcj[:, 1] / zz + cy
+        ok &= (zz > 1.0) & (uu >= 10) & (uu < W - 10) & (vv >= 10) & (vv < H - 10)
+        pe.append(np.flatnonzero(ok))
+        ke.append(kf[ok])
+    pe, ke = np.concatenate(pe), np.concatenate(ke)
+    cnt = np.bincount(pe, minlength=n)
+    keep = cnt >= 2
+    newid = np.cumsum(keep) - 1
+    m = keep[pe]
+    pe, ke = newid[pe[m]], ke[m]
+    Xw = Xw[keep]
+    npt = len(Xw)
+    # edge order: by point, then a per-point shuffle (observation map order)
+    order = np.lexsort((rng.random(len(pe)), pe))
+    pe, ke = pe[order], ke[order]
+    Xc = np.einsum("nij,nj->ni", Rcw[ke], Xw[pe]) + tcw[ke]
+    octv = rng.integers(0, 8, len(pe))
+    s = 1.2 ** octv
+    uu = fx * Xc[:, 0] / Xc[:, 2] + cx + rng.normal(0, 1, len(pe)) * s
+    vv = fy * Xc[:, 1] / Xc[:, 2] + cy + rng.normal(0, 1, len(pe)) * s
+    ur = np.where(rng.random(len(pe)) < stereo_frac, uu - bf / Xc[:, 2] + rng.normal(0, 1, len(pe)) * s, -1.0)
+    ur = np.where((ur < 0) & (ur != -1.0), 0.0, ur)
+    isig = (np.float32(1.0) / np.float32(1.2) ** (2 * octv)).astype(np.float32)
+    Tcw0 = np.zeros((n_kf, 16), np.float32)
+    Tcw_true = np.zeros((n_kf, 4, 4))
+    for kk in range(n_kf):
+        T = np.eye(4)
+        T[:3, :3] = Rcw[kk]
+        T[:3, 3] = tcw[kk]
+        Tcw_true[kk] = T
+        if kk:
+            T = T.copy()
+            T[:3, :3] = _rot(rng, pose_noise[1]) @ T[:3, :3]
+            T[:3, 3] += rng.normal(0, pose_noise[0], 3)
+        Tcw0[kk] = T.astype(np.float32).ravel()
+    X0 = (Xw + rng.normal(0, point_noise, Xw.shape)).astype(np.float32)
+    return dict(kf_id=np.arange(n_kf, dtype=np.int32), kf_Tcw=Tcw0, kf_local=np.ones(n_kf, np.uint8),
+                kf_cam=np.tile(np.array(cam, np.float32), (n_kf, 1)),
+                pt_id=np.arange(npt, dtype=np.int32) + 1, pt_pos=X0,
+                edge_pt=pe.astype(np.int32), edge_kf=ke.astype(np.int32),
+                edge_obs=np.stack([uu, vv, ur], 1).astype(np.float32), edge_inv_sigma2=isig,
+                Tcw_true=Tcw_true, Xw_true=Xw)

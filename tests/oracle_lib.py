@@ -332,8 +332,18 @@ class _BATrace(C.Structure):
 
 def oracle_local_ba(pr, stop=False):
     """Optimizer::LocalBundleAdjustment restated on CPU -> dict of outputs + LM trace."""
+    return _oracle_ba(pr, stop, None)
+
+
+def oracle_global_ba(pr, nIterations=10, bRobust=False, stop=False):
+    """Optimizer::BundleAdjustment restated on CPU -> dict of outputs + LM trace."""
+    return _oracle_ba(pr, stop, (nIterations, bRobust))
+
+
+def _oracle_ba(pr, stop, glob):
     L = lib()
     L.ora_local_ba.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ora_global_ba.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
     keep = {k: np.ascontiguousarray(pr[k]) for k in ("kf_id", "kf_Tcw", "kf_local", "kf_cam", "pt_id", "pt_pos",
                                                      "edge_pt", "edge_kf", "edge_obs", "edge_inv_sigma2")}
     P = _BAProblem(len(keep["kf_id"]), ptr(keep["kf_id"]), ptr(keep["kf_Tcw"]), ptr(keep["kf_local"]),
@@ -346,7 +356,10 @@ def oracle_local_ba(pr, stop=False):
     R = _BAResult(ptr(T), ptr(X), ptr(er))
     tr = _BATrace()
     st = C.c_int(1 if stop else 0)
-    L.ora_local_ba(C.byref(P), C.byref(st), C.byref(R), C.byref(tr))
+    if glob is None:
+        L.ora_local_ba(C.byref(P), C.byref(st), C.byref(R), C.byref(tr))
+    else:
+        L.ora_global_ba(C.byref(P), int(glob[0]), int(bool(glob[1])), C.byref(st), C.byref(R), C.byref(tr))
     return dict(kf_Tcw=T, pt_pos=X, edge_erase=er.astype(bool), iterations=tuple(R.iterations),
                 n_erased=R.n_erased, aborted=bool(R.aborted),
                 solve_chi2=np.array(tr.solve_chi2[:tr.n_solves]), solve_ini_chi2=np.array(tr.solve_ini_chi2[:tr.n_solves]),
