@@ -287,7 +287,6 @@ __device__ __forceinline__ double wave_trees(const double* v, double* buf) {
 }
 
 
-constexpr int kWaveScratch = 512;  // per-wave LDS scratch: lists up to 32768 terms
 constexpr int DIAG21[6] = {0, 6, 11, 15, 18, 20};
 
 // term layout (SoA, stride nE): Hpp 0..20 | bp 21..26 | Hll 27..35 | bl 36..38
@@ -1493,8 +1492,9 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
     const bool use_reg = n <= kLdltMax && regShm <= ldsMax_;
     if (!use_reg && shm > ldsMax_) return -3;
-    // the in-place (global memory) LDL^T leaves fill-in outside the Schur pattern: clear S
-    const bool clearS = !use_reg && !in_lds;
+    // the in-place (global memory) LDL^T leaves fill-in outside the Schur pattern, and a shard's
+    // S holds the previous trial's all-reduced blocks outside its own pattern: clear S
+    const bool clearS = (!use_reg && !in_lds) || comm_ != nullptr;
     do {
         // setLambda + BlockSolver::solve
         if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
