@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=64, help="frames per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gba-kf", type=int, default=128, help="keyframes of the sharded global-BA problem")
+    ap.add_argument("--gba-reps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -204,6 +206,10 @@ def main():
     ba = bench_local_ba(args, world, rank, dist if world > 1 else None, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ba["cpu_baseline"] = ba_cpu_baseline(args.cpu_seconds / 4)
+    # global BA (SURVEY config 5): ONE problem keyframe-block sharded over the ranks, RCCL exchange
+    gba = bench_global_ba(args, world, rank, dist if world > 1 else None, dev)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        gba["cpu_baseline"] = gba_cpu_baseline(args.gba_kf)
 
     if rank == 0:
         stage_ms = {k: round(v / args.steps, 4) for k, v in stage_acc.items()}
@@ -217,6 +223,7 @@ def main():
                        "frames_per_step": B, "parallelism": f"replicas{world}"},
             "matches_per_s": round(tot_match / dt, 1), "keypoints_per_frame": round(tot_kp / frames_total, 1),
             "stage_ms_per_step": stage_ms, "roofline": roof, "cpu_baseline": cpu, "local_ba": ba,
+            "global_ba": gba,
         }
         print(json.dumps(out))
     if world > 1:
@@ -261,6 +268,60 @@ def bench_local_ba(args, world, rank, dist, dev):
                        "stereo_edges": int((pr["edge_obs"][:, 2] >= 0).sum()),
                        "lm": "optimize(5) + gating + optimize(10)", "parallelism": f"replicas{world}"},
             "dtype": "f64 (f32 I/O)"}
+
+
+def bench_global_ba(args, world, rank, dist, dev):
+    """Optimizer::BundleAdjustment (nIterations=10, bRobust=false, LoopClosing.cc:650) on one
+    merged-map-shaped problem (SURVEY config 5, KITTI intrinsics), keyframe-block sharded over
+    the N ranks: per LM trial one RCCL all-reduce of the partial Schur complement over xGMI.
+    Strong scaling: the problem is fixed, N ranks share it; iter = one LM solve()."""
+    import torch
+    sys.path.insert(0, str(ROOT / "tests"))
+    from ba_cases import global_ba_problem
+    from c_orb_slam_amd.optimizer import BundleAdjustmentSharded, Comm, partition_points, shard_problem
+    pr = global_ba_problem(0, n_kf=args.gba_kf, pts_per_kf=150)
+    shard = shard_problem(pr, partition_points(pr, world), rank)
+    uid = [Comm.unique_id() if rank == 0 else None]
+    if dist is not None:
+        dist.broadcast_object_list(uid, src=0)
+    comm = Comm.rccl(world, rank, uid[0])
+    BundleAdjustmentSharded(shard, comm, 10, False)          # warm-up (allocations, structure)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    its = 0
+    for _ in range(args.gba_reps):
+        r = BundleAdjustmentSharded(shard, comm, 10, False)
+        its += r["iterations"][0]
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    comm.close()
+    ne = len(pr["edge_pt"])
+    return {"metric": "global-BA iter/s", "value": round(its / dt, 2), "unit": "iter/s",
+            "ms_per_call": round(dt / args.gba_reps * 1e3, 3), "edges_per_s": round(its * ne / dt, 1),
+            "scaling": "strong", "calls": args.gba_reps,
+            "config": {"workload": "kitti_merged_map_global_ba (SURVEY config 5)", "keyframes": args.gba_kf,
+                       "points": len(pr["pt_id"]), "edges": ne, "edges_per_rank": len(shard["edge_pt"]),
+                       "lm": "optimize(10), bRobust=false", "parallelism": f"keyframe-block shards x{world} (RCCL)"},
+            "dtype": "f64 (f32 I/O)"}
+
+
+def gba_cpu_baseline(n_kf):
+    """Oracle BundleAdjustment (C restatement of the g2o path, 1 thread) on the same problem, one call."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    from ba_cases import global_ba_problem
+    pr = global_ba_problem(0, n_kf=n_kf, pts_per_kf=150)
+    t0 = time.perf_counter()
+    o = oracle_lib.oracle_global_ba(pr, 10, False)
+    dt = time.perf_counter() - t0
+    return {"value": round(o["iterations"][0] / dt, 3), "unit": "iter/s", "cores": 1, "kind": "port",
+            "sample": f"1 BundleAdjustment call on config 5 ({n_kf} KFs, {o['iterations'][0]} LM solves), "
+                      f"oracle/ba.c -O2 dense LDL^T, 1 thread"}
 
 
 def ba_cpu_baseline(budget_s):

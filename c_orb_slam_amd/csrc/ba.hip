@@ -25,6 +25,7 @@
 #include <numeric>
 
 #include "detmath.hpp"
+#include "ldlt.hpp"
 #include "orb_common.hpp"
 
 namespace orbgpu {
@@ -1222,6 +1223,7 @@ int BaEngine::carve(bool commit, size_t* total) {
     tmpA1_ = (double*)take(sizeof(double) * tmpN);
     tmpB0_ = (double*)take(sizeof(double) * tmpN);
     tmpB1_ = (double*)take(sizeof(double) * tmpN);
+    dLdltWs_ = take(ldlt_tiled_workspace((int)(6 * nkf)));
     *total = off;
     return 0;
 }
@@ -1491,10 +1493,12 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const size_t shm = in_lds ? ldsBytes : sizeof(double) * (size_t)n;
     const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
     const bool use_reg = n <= kLdltMax && regShm <= ldsMax_;
-    if (!use_reg && shm > ldsMax_) return -3;
-    // the in-place (global memory) LDL^T leaves fill-in outside the Schur pattern, and a shard's
+    // n <= 128: register-resident single-workgroup LDL^T; S fits LDS: single-workgroup in LDS;
+    // larger: tiled multi-workgroup LDL^T in HBM (ldlt.hip)
+    const bool use_tiled = !use_reg && !in_lds;
+    // the in-place (HBM) LDL^T overwrites S (fill-in, L in the lower triangle), and a shard's
     // S holds the previous trial's all-reduced blocks outside its own pattern: clear S
-    const bool clearS = (!use_reg && !in_lds) || comm_ != nullptr;
+    const bool clearS = use_tiled || comm_ != nullptr;
     do {
         // setLambda + BlockSolver::solve
         if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
@@ -1509,8 +1513,10 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         }
         if (use_reg)
             hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_);
-        else
+        else if (in_lds)
             hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds);
+        else if (int e = ldlt_tiled_solve(n, dS_, dBs_, dX2_, dScal_, dLdltWs_, s))
+            return e;
         // push + update
         if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_,
                                         dXbak_, dX2_, dHplA_, dHll_, dBl_, lambda_, use_dev, dScal_);
@@ -1697,10 +1703,19 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     ORB_HIP_CHECK(hipMemcpy(dS, S, sizeof(double) * n * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemcpy(dB, b, sizeof(double) * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemset(dX, 0, sizeof(double) * nn));
+    void* ws = nullptr;
     if (variant == 0) {
         const size_t shm = sizeof(double) * ((size_t)n * n + 14 * kLdltMax);
         if (n > kLdltMax) return -3;
         hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal);
+    } else if (variant == 2) {  // tiled: strict lower triangle must start at zero
+        std::vector<double> U((size_t)n * n, 0.0);
+        for (int i = 0; i < n; i++)
+            for (int j = i; j < n; j++) U[(size_t)i * n + j] = S[(size_t)i * n + j];
+        ORB_HIP_CHECK(hipMemcpy(dS, U.data(), sizeof(double) * U.size(), hipMemcpyHostToDevice));
+        ORB_HIP_CHECK(hipMalloc(&ws, ldlt_tiled_workspace(n)));
+        if (int e = ldlt_tiled_solve(n, dS, dB, dX, dScal, ws, 0)) return e;
+        ORB_HIP_CHECK(hipDeviceSynchronize());
     } else {
         hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), sizeof(double) * n + 16, 0, n, dS, dB, dX, dScal, 0);
     }
@@ -1709,6 +1724,7 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     ORB_HIP_CHECK(hipMemcpy(sc, dScal, sizeof(sc), hipMemcpyDeviceToHost));
     ORB_HIP_CHECK(hipMemcpy(x, dX, sizeof(double) * n, hipMemcpyDeviceToHost));
     (void)hipFree(dS); (void)hipFree(dB); (void)hipFree(dX); (void)hipFree(dScal);
+    if (ws) (void)hipFree(ws);
     return sc[3] != 0.0 ? 1 : 0;
 }
 

@@ -104,6 +104,7 @@ private:
     double *dEmat_ = nullptr, *dCb_ = nullptr, *dScal_ = nullptr, *dScratch_ = nullptr, *dHplA_ = nullptr;
     double *tmpA0_ = nullptr, *tmpA1_ = nullptr, *tmpB0_ = nullptr, *tmpB1_ = nullptr;
     unsigned* dCounter_ = nullptr;
+    void* dLdltWs_ = nullptr;
     void* arena_ = nullptr;
     size_t arenaCap_ = 0;
     double* hScal_ = nullptr;      // pinned

@@ -401,20 +401,22 @@ int ora_ldlt_solve(double* S, int n, const double* b, double* x)
 {
     double* l = (double*)malloc(sizeof(double) * (n + 1));
     for (int k = 0; k < n; k++) {
-        const double d = S[k * n + k];
+        const double d = S[(size_t)k * n + k];
         if (d == 0.0) { free(l); return 0; }
-        for (int i = k + 1; i < n; i++) l[i] = S[k * n + i] / d;
-        for (int i = k + 1; i < n; i++)
-            for (int j = i; j < n; j++) S[i * n + j] -= l[i] * S[k * n + j];
-        for (int i = k + 1; i < n; i++) S[k * n + i] = l[i];   /* row k now holds L^T */
+        for (int i = k + 1; i < n; i++) l[i] = S[(size_t)k * n + i] / d;
+        for (int i = k + 1; i < n; i++) {
+            if (l[i] == 0.0) continue;   /* envelope skip: S[i][j] - 0*S[k][j] == S[i][j] (up to the sign of 0) */
+            for (int j = i; j < n; j++) S[(size_t)i * n + j] -= l[i] * S[(size_t)k * n + j];
+        }
+        for (int i = k + 1; i < n; i++) S[(size_t)k * n + i] = l[i];   /* row k now holds L^T */
     }
     double* y = (double*)malloc(sizeof(double) * (n + 1));
     memcpy(y, b, sizeof(double) * n);
     for (int k = 0; k < n; k++)          /* L y = b (column sweep) */
-        for (int i = k + 1; i < n; i++) y[i] -= S[k * n + i] * y[k];
-    for (int k = 0; k < n; k++) y[k] = y[k] / S[k * n + k];
+        for (int i = k + 1; i < n; i++) y[i] -= S[(size_t)k * n + i] * y[k];
+    for (int k = 0; k < n; k++) y[k] = y[k] / S[(size_t)k * n + k];
     for (int k = n - 1; k >= 0; k--)     /* L^T x = z (column sweep) */
-        for (int i = 0; i < k; i++) y[i] -= S[i * n + k] * y[k];
+        for (int i = 0; i < k; i++) y[i] -= S[(size_t)i * n + k] * y[k];
     memcpy(x, y, sizeof(double) * n);
     free(y);
     free(l);
@@ -617,32 +619,69 @@ static int schur_solve(ba_ctx* c, double lambda)
             }
         }
     }
-    /* S (upper) and b_schur: terms in landmark order */
+    /* S (upper) and b_schur: terms in landmark order.  Per landmark its pose edges sorted by
+     * pose (g2o's per-landmark block list); Schur block (i1 <= i2) -> its (a1, a2) pairs in
+     * landmark order, so the cost is sum_l k_l^2 like the reference's BlockSolver::solve. */
     double* S = (double*)calloc((size_t)n * n + 1, sizeof(double));
     double* bs = (double*)malloc(sizeof(double) * (n + 1));
-    /* edge of landmark l to pose i (at most one: keyframes observe a point once) */
-    int maxT = 1;
-    double* v = (double*)malloc(sizeof(double) * (nL + 1));
-    (void)maxT;
-    int* ePL = (int*)malloc(sizeof(int) * ((size_t)nP * nL + 1));
-    for (size_t q = 0; q < (size_t)nP * nL; q++) ePL[q] = -1;
-    for (int l = 0; l < nL; l++)
+    int* lpStart = (int*)calloc(nL + 2, sizeof(int));
+    int* lpList = (int*)malloc(sizeof(int) * (c->nE + 1));
+    for (int l = 0; l < nL; l++) {
+        lpStart[l + 1] = lpStart[l];
         for (int j = c->leStart[l]; j < c->leStart[l + 1]; j++) {
             const int a = c->leList[j];
             const int pi = c->poseIdx[c->E[c->aE[a]].kf];
-            if (pi >= 0) ePL[(size_t)pi * nL + l] = a;
+            if (pi < 0) continue;
+            int q = lpStart[l + 1]++;   /* insertion sort by pose index (k_l is small) */
+            while (q > lpStart[l] && c->poseIdx[c->E[c->aE[lpList[q - 1]]].kf] > pi) {
+                lpList[q] = lpList[q - 1];
+                q--;
+            }
+            lpList[q] = a;
         }
+    }
+#define POSE_OF(a) (c->poseIdx[c->E[c->aE[(a)]].kf])
+    int* blkOf = (int*)malloc(sizeof(int) * ((size_t)nP * nP + 1));
+    for (size_t q = 0; q < (size_t)nP * nP; q++) blkOf[q] = -1;
+    int nBlk = 0;
+    for (int l = 0; l < nL; l++)
+        for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
+            for (int w = u; w < lpStart[l + 1]; w++) {
+                int* bo = &blkOf[(size_t)POSE_OF(lpList[u]) * nP + POSE_OF(lpList[w])];
+                if (*bo < 0) *bo = nBlk++;
+            }
+    int* bStart = (int*)calloc(nBlk + 2, sizeof(int));
+    for (int l = 0; l < nL; l++)
+        for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
+            for (int w = u; w < lpStart[l + 1]; w++)
+                bStart[blkOf[(size_t)POSE_OF(lpList[u]) * nP + POSE_OF(lpList[w])] + 1]++;
+    for (int q = 0; q < nBlk; q++) bStart[q + 1] += bStart[q];
+    const int nPair = bStart[nBlk];
+    int* pA = (int*)malloc(sizeof(int) * (nPair + 1));
+    int* pB = (int*)malloc(sizeof(int) * (nPair + 1));
+    int* fill = (int*)malloc(sizeof(int) * (nBlk + 1));
+    memcpy(fill, bStart, sizeof(int) * (nBlk + 1));
+    for (int l = 0; l < nL; l++)
+        for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
+            for (int w = u; w < lpStart[l + 1]; w++) {
+                const int q = fill[blkOf[(size_t)POSE_OF(lpList[u]) * nP + POSE_OF(lpList[w])]]++;
+                pA[q] = lpList[u];
+                pB[q] = lpList[w];
+            }
+    int maxM = 1;
+    for (int q = 0; q < nBlk; q++) if (bStart[q + 1] - bStart[q] > maxM) maxM = bStart[q + 1] - bStart[q];
+    double* v = (double*)malloc(sizeof(double) * (maxM + nL + 1));
     for (int i1 = 0; i1 < nP; i1++)
-        for (int i2 = i1; i2 < nP; i2++)
+        for (int i2 = i1; i2 < nP; i2++) {
+            const int bq = blkOf[(size_t)i1 * nP + i2];
+            const int s0 = bq < 0 ? 0 : bStart[bq], m = bq < 0 ? 0 : bStart[bq + 1] - s0;
+            if (bq < 0 && i1 != i2) continue;   /* structurally zero block (calloc) */
             for (int r = 0; r < 6; r++)
                 for (int cc = (i1 == i2 ? r : 0); cc < 6; cc++) {
-                    int m = 0;
-                    for (int l = 0; l < nL; l++) {
-                        const int a1 = ePL[(size_t)i1 * nL + l], a2 = ePL[(size_t)i2 * nL + l];
-                        if (a1 < 0 || a2 < 0) continue;
-                        const double* Ei = &E[18 * a1 + r * 3];
-                        const double* Bj = &c->terms[a2].Hpl[cc * 3];
-                        v[m++] = (Ei[0] * Bj[0] + Ei[1] * Bj[1]) + Ei[2] * Bj[2];
+                    for (int t = 0; t < m; t++) {
+                        const double* Ei = &E[18 * pA[s0 + t] + r * 3];
+                        const double* Bj = &c->terms[pB[s0 + t]].Hpl[cc * 3];
+                        v[t] = (Ei[0] * Bj[0] + Ei[1] * Bj[1]) + Ei[2] * Bj[2];
                     }
                     double h = 0;
                     if (i1 == i2) {
@@ -651,15 +690,26 @@ static int schur_solve(ba_ctx* c, double lambda)
                     }
                     S[(size_t)(6 * i1 + r) * n + 6 * i2 + cc] = h - ora_csum(v, m);
                 }
-    for (int i = 0; i < nP; i++)
-        for (int r = 0; r < 6; r++) {
-            int m = 0;
-            for (int l = 0; l < nL; l++) {
-                const int a = ePL[(size_t)i * nL + l];
-                if (a >= 0) v[m++] = cb[6 * a + r];
-            }
-            bs[6 * i + r] = c->bp[6 * i + r] - ora_csum(v, m);
         }
+    /* b_schur: per pose, its landmarks' terms in landmark order */
+    {
+        int* psStart = (int*)calloc(nP + 2, sizeof(int));
+        int* psList = (int*)malloc(sizeof(int) * (c->nE + 1));
+        for (int l = 0; l < nL; l++)
+            for (int u = lpStart[l]; u < lpStart[l + 1]; u++) psStart[POSE_OF(lpList[u]) + 1]++;
+        for (int i = 0; i < nP; i++) psStart[i + 1] += psStart[i];
+        int* pf = (int*)malloc(sizeof(int) * (nP + 1));
+        memcpy(pf, psStart, sizeof(int) * (nP + 1));
+        for (int l = 0; l < nL; l++)
+            for (int u = lpStart[l]; u < lpStart[l + 1]; u++) psList[pf[POSE_OF(lpList[u])]++] = lpList[u];
+        for (int i = 0; i < nP; i++)
+            for (int r = 0; r < 6; r++) {
+                const int m = psStart[i + 1] - psStart[i];
+                for (int t = 0; t < m; t++) v[t] = cb[6 * psList[psStart[i] + t] + r];
+                bs[6 * i + r] = c->bp[6 * i + r] - ora_csum(v, m);
+            }
+        free(psStart); free(psList); free(pf);
+    }
     double* xp = (double*)malloc(sizeof(double) * (n + 1));
     int ok = n == 0 ? 1 : ora_ldlt_solve(S, n, bs, xp);
     if (ok) {
@@ -667,11 +717,10 @@ static int schur_solve(ba_ctx* c, double lambda)
         /* xl = Dinv (bl - sum_i B_i^T xp_i); rightMultiply over the landmark's blocks in pose order */
         for (int l = 0; l < nL; l++) {
             double cl[3] = {c->bl[3 * l], c->bl[3 * l + 1], c->bl[3 * l + 2]};
-            for (int i = 0; i < nP; i++) {
-                const int a = ePL[(size_t)i * nL + l];
-                if (a < 0) continue;
+            for (int u = lpStart[l]; u < lpStart[l + 1]; u++) {
+                const int a = lpList[u];
                 const double* B = c->terms[a].Hpl;
-                const double* cp = &xp[6 * i];
+                const double* cp = &xp[6 * POSE_OF(a)];
                 for (int k = 0; k < 3; k++) {
                     double s = 0;
                     for (int r = 0; r < 6; r++) s += B[r * 3 + k] * (-cp[r]);
@@ -683,7 +732,9 @@ static int schur_solve(ba_ctx* c, double lambda)
                 c->x[6 * nP + 3 * l + r] = (Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1]) + Di[r * 3 + 2] * cl[2];
         }
     }
-    free(xp); free(ePL); free(v); free(S); free(bs); free(E); free(cb); free(Dinv); free(db);
+#undef POSE_OF
+    free(lpStart); free(lpList); free(blkOf); free(bStart); free(pA); free(pB); free(fill);
+    free(xp); free(v); free(S); free(bs); free(E); free(cb); free(Dinv); free(db);
     return ok;
 }
 

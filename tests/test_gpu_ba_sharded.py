@@ -27,7 +27,7 @@ def _exact(g, o):
     assert np.array_equal(g["pt_pos"], o["pt_pos"].reshape(g["pt_pos"].shape))
 
 
-@pytest.mark.parametrize("n_kf,robust", [(12, False), (24, True), (40, False)])
+@pytest.mark.parametrize("n_kf,robust", [(12, False), (24, True), (40, False), (128, False)])
 def test_global_ba_matches_oracle(gpu, n_kf, robust):
     from c_orb_slam_amd.optimizer import BundleAdjustment
     pr = global_ba_problem(n_kf, n_kf=n_kf, pts_per_kf=60)

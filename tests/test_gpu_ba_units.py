@@ -67,6 +67,55 @@ def test_ldlt_matches_oracle(gpu, n, variant):
     np.testing.assert_allclose(S @ x, b, rtol=1e-8, atol=1e-8)
 
 
+def _banded_spd(rng, nblk, bw, loops=()):
+    """Schur-complement-shaped SPD matrix: 6x6 blocks, block bandwidth bw, plus loop-closure blocks."""
+    n = 6 * nblk
+    S = np.zeros((n, n))
+    for i in range(nblk):
+        for j in range(i, min(nblk, i + bw + 1)):
+            S[6 * i:6 * i + 6, 6 * j:6 * j + 6] = rng.normal(size=(6, 6))
+    for i, j in loops:
+        S[6 * i:6 * i + 6, 6 * j:6 * j + 6] = rng.normal(size=(6, 6))
+    S = np.triu(S) + np.triu(S, 1).T
+    S += np.diag(np.abs(S).sum(1) + 1.0)
+    return S
+
+
+@pytest.mark.parametrize("n,kind", [(1, "dense"), (63, "dense"), (64, "dense"), (65, "dense"), (130, "dense"),
+                                    (200, "dense"), (511, "dense"), (600, "banded"), (1200, "banded"),
+                                    (1200, "loops"), (1998, "banded")])
+def test_ldlt_tiled_matches_oracle(gpu, n, kind):
+    from c_orb_slam_amd._lib import lib
+    rng = np.random.default_rng(7 + n)
+    if kind == "dense":
+        S = _spd(rng, n)
+    else:
+        nb = n // 6
+        S = _banded_spd(rng, nb, 8, loops=[(1, nb - 2), (3, nb // 2)] if kind == "loops" else ())
+        n = 6 * nb
+    S_in = S.copy()
+    S_in[np.tril_indices(n, -1)] = np.nan   # only the upper triangle is read
+    b = rng.normal(size=n)
+    x = np.zeros(n)
+    ok = C.c_int()
+    assert lib().orbgpu_unit_ldlt_solve(n, ptr(np.ascontiguousarray(S_in)), ptr(b), ptr(x), 2, C.byref(ok)) == 0
+    oko, xo = _ora_ldlt(S_in, b)
+    assert ok.value == oko == 1
+    assert np.array_equal(x, xo), np.abs(x - xo).max()
+    np.testing.assert_allclose(S @ x, b, rtol=1e-8, atol=1e-8)
+
+
+def test_ldlt_tiled_zero_pivot_fails(gpu):
+    from c_orb_slam_amd._lib import lib
+    n = 300
+    S = np.eye(n) * 2.0
+    S[150, 150] = 0.0
+    x = np.full(n, 7.0)
+    ok = C.c_int(5)
+    assert lib().orbgpu_unit_ldlt_solve(n, ptr(S), ptr(np.ones(n)), ptr(x), 2, C.byref(ok)) == 0
+    assert ok.value == 0
+
+
 def test_ldlt_zero_pivot_fails(gpu):
     from c_orb_slam_amd._lib import lib
     S = np.eye(12)
