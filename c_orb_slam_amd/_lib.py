@@ -113,6 +113,7 @@ def lib():
     L.Optimizer_last_timings.argtypes = [vp]
     L.orbgpu_unit_ldlt_solve.argtypes = [i32, vp, vp, vp, i32, P(i32)]
     L.orbgpu_unit_csum.argtypes = [vp, i32, vp]
+    L.orbgpu_unit_ldlt_factor.argtypes = [i32, vp, vp]
     L.orbgpu_unit_wave_tree.argtypes = [vp, vp]
     L.Sim3Solver_create.argtypes = [i32, vp, vp, vp, vp, vp, i32, vp, vp, i32, P(vp)]
     L.Sim3Solver_destroy.argtypes = [vp]

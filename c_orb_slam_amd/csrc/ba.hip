@@ -1084,6 +1084,21 @@ __global__ void __launch_bounds__(1024) k_scale(int nP, int nL, const double* x,
     if (threadIdx.x == 0) *out = local_csum_inplace(lv, m);
 }
 
+// computeScale terms for large problems (6 nP + 3 nL > 2048 * 64): written out, then k_csum
+__global__ void __launch_bounds__(256) k_scale_terms(int nP, int nL, const double* x, const double* bp,
+                                                     const double* bl, double lam_host, int use_dev,
+                                                     const double* scal, double* v, int poses) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= 6 * nP + 3 * nL) return;
+    const double lambda = lam_of(lam_host, use_dev, scal);
+    if (j < 6 * nP && !poses) {
+        v[j] = 0.0;
+        return;
+    }
+    const double b = j < 6 * nP ? bp[j] : bl[j - 6 * nP];
+    v[j] = x[j] * (lambda * x[j] + b);
+}
+
 // canonical sum of one list per workgroup (blockIdx.x selects the list), 1024 threads,
 // level buffers ping-pong in global scratch.
 struct CsumList {
@@ -1410,7 +1425,7 @@ int BaEngine::build_structure(int level) {
         if (peStart[i + 1] - peStart[i] > 64 * kChunks) return -3;
     for (int l = 0; l < nL; l++)
         if (leStart[l + 1] - leStart[l] > 64 * 64) return -3;
-    if (6 * nP + 3 * nL > 2048 * 64 || nE > 1024 * 64 * 64) return -3;
+    if (nE > 1024 * 64 * 64 || 6LL * nP + 3LL * nL > (long long)scratchN_) return -3;
     for (int b = 0; b < nBlk; b++)
         if (blkStart[b + 1] - blkStart[b] > 64 * kChunks) return -3;
     // pack and upload
@@ -1524,8 +1539,16 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         la.linearize = 0;
         la.out = dScal_ + 1;
         if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
-        hipLaunchKernelGGL(k_scale, dim3(1), dim3(1024), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_, use_dev, dScal_,
-                           dScal_ + 2, own ? 1 : 0);
+        if (6 * nP + 3 * nL <= 2048 * 64) {
+            hipLaunchKernelGGL(k_scale, dim3(1), dim3(1024), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_, use_dev, dScal_,
+                               dScal_ + 2, own ? 1 : 0);
+        } else {
+            const int nv = 6 * nP + 3 * nL;
+            hipLaunchKernelGGL(k_scale_terms, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_,
+                               use_dev, dScal_, dScratch_, own ? 1 : 0);
+            CsumList L0{dScratch_, nv, tmpA0_, tmpA1_, dScal_ + 2};
+            hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, L0, L0);
+        }
         ORB_HIP_CHECK(hipGetLastError());
         if (comm_) {
             hScal_[32] = (stop && *stop) ? 1.0 : 0.0;
@@ -1726,6 +1749,28 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     (void)hipFree(dS); (void)hipFree(dB); (void)hipFree(dX); (void)hipFree(dScal);
     if (ws) (void)hipFree(ws);
     return sc[3] != 0.0 ? 1 : 0;
+}
+
+// tiled factorisation only: A (n x n, upper = S) -> d on the diagonal, L in the strict lower triangle
+int debug_ldlt_factor(int n, const double* S, double* out) {
+    if (n <= 0) return 0;
+    double *dS = nullptr, *dB = nullptr, *dX = nullptr, *dScal = nullptr;
+    void* ws = nullptr;
+    std::vector<double> U((size_t)n * n, 0.0);
+    for (int i = 0; i < n; i++)
+        for (int j = i; j < n; j++) U[(size_t)i * n + j] = S[(size_t)i * n + j];
+    ORB_HIP_CHECK(hipMalloc(&dS, sizeof(double) * U.size()));
+    ORB_HIP_CHECK(hipMalloc(&dB, sizeof(double) * n));
+    ORB_HIP_CHECK(hipMalloc(&dX, sizeof(double) * n));
+    ORB_HIP_CHECK(hipMalloc(&dScal, sizeof(double) * 16));
+    ORB_HIP_CHECK(hipMalloc(&ws, ldlt_tiled_workspace(n)));
+    ORB_HIP_CHECK(hipMemcpy(dS, U.data(), sizeof(double) * U.size(), hipMemcpyHostToDevice));
+    ORB_HIP_CHECK(hipMemset(dB, 0, sizeof(double) * n));
+    if (int e = ldlt_tiled_solve(n, dS, dB, dX, dScal, ws, 0)) return e;
+    ORB_HIP_CHECK(hipDeviceSynchronize());
+    ORB_HIP_CHECK(hipMemcpy(out, dS, sizeof(double) * U.size(), hipMemcpyDeviceToHost));
+    (void)hipFree(dS); (void)hipFree(dB); (void)hipFree(dX); (void)hipFree(dScal); (void)hipFree(ws);
+    return 0;
 }
 
 __global__ void k_unit_wave_tree(const double* v, double* out) {

@@ -123,6 +123,7 @@ private:
 
 int debug_ldlt(int n, const double* S, const double* b, double* x, int variant);
 int debug_csum(const double* v, int n, double* out);
+int debug_ldlt_factor(int n, const double* S, double* out);
 int debug_wave_tree(const double* v64, double* out);
 
 }  // namespace orbgpu

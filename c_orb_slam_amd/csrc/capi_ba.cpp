@@ -203,6 +203,14 @@ int orbgpu_unit_ldlt_solve(int n, const double* S, const double* b, double* x, i
     return ORB_OK;
 }
 
+int orbgpu_unit_ldlt_factor(int n, const double* S, double* out) {
+    if (n < 0 || (n > 0 && (!S || !out))) return ORB_E_INVALID;
+    int rc = 0;
+    engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    return orbgpu::debug_ldlt_factor(n, S, out) ? ORB_E_HIP : ORB_OK;
+}
+
 int orbgpu_unit_wave_tree(const double* v64, double* out) {
     if (!v64 || !out) return ORB_E_INVALID;
     int rc = 0;

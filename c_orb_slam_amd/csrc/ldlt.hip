@@ -33,100 +33,106 @@ namespace orbgpu {
 constexpr int LT = 64;          // tile edge
 constexpr int LP = LT + 1;      // LDS row pitch (doubles)
 
-__global__ void __launch_bounds__(256) k_ldlt_panel(int n, int p, double* __restrict__ A, uint8_t* nz, int nt,
-                                                    int* fail, double* dstage) {
-    __shared__ double D[LT * LP];   // diagonal block: upper = eliminated rows, lower = L
-    __shared__ double Cc[LT * LP];  // this workgroup's chunk of the panel rows
-    __shared__ double dv[LT];
-    __shared__ int anyNz;
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), l);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// One wave per workgroup; lane j owns column j of a 64-row block in registers.
+// Phase 1 (every workgroup, redundantly): factorise the diagonal block -- at pivot k lane i
+// forms l_ik = D[k][i] / d_k from its own column, and lane j applies D[i][j] -= l_i D[k][j]
+// to its column (rows k < i <= j) with l_i broadcast by readlane.  Phase 2 (J > p): the
+// same pivots on the chunk columns, l_ik broadcast from LDS (uniform `l != 0` skip).
+__global__ void __launch_bounds__(64) k_ldlt_panel(int n, int p, double* __restrict__ A, uint8_t* nz, int nt,
+                                                   int* fail, double* dstage) {
+    __shared__ double Ls[LT * LP];   // Ls[k * LP + i] = l_ik ; reused as the L transpose buffer
+    __shared__ double dvs[LT];
     if (*fail) return;
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
     const int p0 = p * LT, pw = min(LT, n - p0);
     const int J = p + blockIdx.x, J0 = J * LT, cw = min(LT, n - J0);
     const bool diag = J == p;
-    // load the diagonal block (upper triangle) and, off the diagonal, the chunk
-    for (int q = tid; q < LT * LT; q += 256) {
-        const int i = q >> 6, j = q & 63;
-        D[i * LP + j] = (i < pw && j < pw && i <= j) ? A[(size_t)(p0 + i) * n + p0 + j] : 0.0;
-    }
-    if (!diag) {
+    double* Ap = A + (size_t)p0 * n;   // panel rows
+    if (!diag) {   // an all-zero chunk stays zero and its L stays zero (A is pre-cleared)
         bool nzc = false;
-        for (int q = tid; q < LT * LT; q += 256) {
-            const int i = q >> 6, j = q & 63;
-            const double v = (i < pw && j < cw) ? A[(size_t)(p0 + i) * n + J0 + j] : 0.0;
-            Cc[i * LP + j] = v;
-            nzc |= v != 0.0;
+        for (int r0 = 0; r0 < pw; r0 += 16) {
+            double v[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) v[u] = (r0 + u < pw && lane < cw) ? Ap[(size_t)(r0 + u) * n + J0 + lane] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; u++) nzc |= v[u] != 0.0;
         }
-        if (tid == 0) anyNz = 0;
-        __syncthreads();
-        if (nzc) anyNz = 1;
+        if (!__any(nzc)) {
+            if (lane == 0) nz[(size_t)J * nt + p] = 0;
+            return;
+        }
     }
-    __syncthreads();
-    if (!diag && !anyNz) {   // an all-zero chunk stays zero and its L stays zero (A is pre-cleared)
-        if (tid == 0) nz[(size_t)J * nt + p] = 0;
-        return;
-    }
-    // redundant factorisation of the diagonal block (oracle order)
+    double col[LT];
+#pragma unroll
+    for (int r = 0; r < LT; r++)
+        col[r] = (r < pw && lane < pw && r <= lane) ? Ap[(size_t)r * n + p0 + lane] : 0.0;
     bool bad = false;
-    for (int k = 0; k < pw; k++) {
-        const double d = D[k * LP + k];
-        if (d == 0.0) {   // every thread sees the same pivot: uniform exit
-            bad = true;
-            break;
-        }
-        if (tid < LT && tid > k && tid < pw) D[tid * LP + k] = D[k * LP + tid] / d;
-        __syncthreads();
-        for (int q = tid; q < LT * LT; q += 256) {
-            const int i = q >> 6, j = q & 63;
-            if (i > k && i <= j && j < pw) {
-                const double l = D[i * LP + k];
-                if (l != 0.0) D[i * LP + j] -= l * D[k * LP + j];
+#pragma unroll
+    for (int k = 0; k < LT; k++) {
+        if (k < pw && !bad) {
+            const double d = rdlane(col[k], k);
+            if (d == 0.0) {
+                bad = true;
+            } else {
+                const double li = (lane > k && lane < pw) ? col[k] / d : 0.0;
+                Ls[k * LP + lane] = li;
+                if (lane == k) dvs[k] = d;
+                const double dkj = col[k];
+#pragma unroll
+                for (int i = k + 1; i < LT; i++) {
+                    const double l = rdlane(li, i);
+                    if (i < pw && i <= lane && l != 0.0) col[i] -= l * dkj;
+                }
             }
         }
-        __syncthreads();
     }
     if (bad) {
-        if (tid == 0) atomicExch(fail, 1);
+        if (lane == 0) atomicExch(fail, 1);
         return;
     }
     __syncthreads();
-    if (tid < pw) dv[tid] = D[tid * LP + tid];
     if (diag) {   // the other workgroups of this launch still read A's diagonal block: stage it
-        __syncthreads();
-        for (int q = tid; q < LT * LT; q += 256) dstage[q] = D[(q >> 6) * LP + (q & 63)];
-        if (tid == 0) nz[(size_t)p * nt + p] = 1;
+#pragma unroll
+        for (int r = 0; r < LT; r++) dstage[r * LT + lane] = lane >= r ? col[r] : Ls[lane * LP + r];
+        if (lane == 0) nz[(size_t)p * nt + p] = 1;
         return;
     }
-    // apply the panel pivots to the chunk: row k is final when pivot k starts
-    const int j = tid & 63, g = tid >> 6;
-    for (int k = 0; k < pw; k++) {
-        const double u = Cc[k * LP + j];
-        for (int i = k + 1 + ((g - (k + 1)) & 3); i < pw; i += 4) {
-            const double l = D[i * LP + k];
-            if (l != 0.0) Cc[i * LP + j] -= l * u;
+    // phase 2: this workgroup's chunk of the panel rows
+#pragma unroll
+    for (int r = 0; r < LT; r++) col[r] = (r < pw && lane < cw) ? Ap[(size_t)r * n + J0 + lane] : 0.0;
+#pragma unroll
+    for (int k = 0; k < LT; k++) {
+        if (k < pw) {
+            const double ckj = col[k];
+#pragma unroll
+            for (int i = k + 1; i < LT; i++) {
+                const double l = Ls[k * LP + i];   // uniform
+                if (i < pw && l != 0.0) col[i] -= l * ckj;
+            }
         }
-        __syncthreads();
     }
-    // write back the eliminated chunk rows and L[J block][panel] = U[k][j] / d_k.  The tile
-    // flag is "some eliminated U[k][j] != 0", a superset of "some l != 0": skipping on it is exact.
     bool nzl = false;
-    for (int q = tid; q < LT * LT; q += 256) {
-        const int i = q >> 6, jj = q & 63;
-        if (i < pw && jj < cw) {
-            const double v = Cc[i * LP + jj];
-            A[(size_t)(p0 + i) * n + J0 + jj] = v;
-            nzl |= v != 0.0;
-        }
+#pragma unroll
+    for (int r = 0; r < LT; r++) {
+        if (r < pw && lane < cw) Ap[(size_t)r * n + J0 + lane] = col[r];
+        nzl |= col[r] != 0.0;
     }
-    for (int q = tid; q < LT * LT; q += 256) {
-        const int jj = q >> 6, k = q & 63;   // row J0+jj of L, column p0+k (coalesced over k)
-        if (jj < cw && k < pw) A[(size_t)(J0 + jj) * n + p0 + k] = Cc[k * LP + jj] / dv[k];
-    }
-    if (tid == 0) anyNz = 0;
+    // flag = some eliminated U[k][j] != 0, a superset of "some l != 0": skipping on it is exact
+    __syncthreads();   // everyone is done reading Ls
+#pragma unroll
+    for (int k = 0; k < LT; k++) Ls[lane * LP + k] = k < pw ? col[k] / dvs[k] : 0.0;   // row J0+lane of L
     __syncthreads();
-    if (nzl) anyNz = 1;
-    __syncthreads();
-    if (tid == 0) nz[(size_t)J * nt + p] = anyNz ? 1 : 0;
+    for (int jj = 0; jj < cw; jj++)
+        if (lane < pw) A[(size_t)(J0 + jj) * n + p0 + lane] = Ls[jj * LP + lane];
+    const bool anyl = __any(nzl);   // wave-wide vote outside the lane-0 branch
+    if (lane == 0) nz[(size_t)J * nt + p] = anyl ? 1 : 0;
 }
 
 // grid = m*m + 1 (m = trailing tiles): block m*m stores the staged diagonal block of panel p.
@@ -185,19 +191,26 @@ __global__ void __launch_bounds__(256) k_ldlt_trail(int n, int p, double* __rest
         }
 }
 
-__device__ __forceinline__ double rdlane(double v, int l) {
-    const unsigned long long u = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), l);
-    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
-    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-
 __device__ __forceinline__ void wait_flag(const int* f) {
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(1);
 }
 
 __device__ __forceinline__ void set_flag(int* f) {
     __hip_atomic_store(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Stage rows [0, rows) of a 64-column tile (row r at src + r * n, column = lane) into
+// Lt[r * LP + lane], 16 independent loads in flight per batch.
+__device__ __forceinline__ void stage_rows(double* Lt, const double* __restrict__ src, size_t n, int rows, int lane,
+                                           bool col_ok) {
+    for (int r0 = 0; r0 < rows; r0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = (r0 + u < rows && col_ok) ? src[(size_t)(r0 + u) * n + lane] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (r0 + u < rows) Lt[(r0 + u) * LP + lane] = v[u];
+    }
 }
 
 // L y = b (column-sweep order per element): block I = blockIdx.x, one wave.
@@ -214,7 +227,7 @@ __global__ void __launch_bounds__(64) k_ldlt_fwd(int n, const double* __restrict
     for (int K = 0; K < I; K++) {
         if (!nz[(size_t)I * nt + K]) continue;
         const int K0 = K * LT;
-        for (int r = 0; r < ih; r++) Lt[r * LP + lane] = A[(size_t)(I0 + r) * n + K0 + lane];
+        stage_rows(Lt, A + (size_t)I0 * n + K0, n, ih, lane, true);
         if (lane == 0) wait_flag(done + K);
         __syncthreads();
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
@@ -225,7 +238,7 @@ __global__ void __launch_bounds__(64) k_ldlt_fwd(int n, const double* __restrict
         }
     }
     // diagonal block: y_k final when all k' < k applied
-    for (int r = 0; r < ih; r++) Lt[r * LP + lane] = lane < ih ? A[(size_t)(I0 + r) * n + I0 + lane] : 0.0;
+    stage_rows(Lt, A + (size_t)I0 * n + I0, n, ih, lane, lane < ih);
     __syncthreads();
     for (int k = 0; k < ih; k++) {
         const double yk = rdlane(acc, k);
@@ -250,7 +263,7 @@ __global__ void __launch_bounds__(64) k_ldlt_bwd(int n, const double* __restrict
         if (!nz[(size_t)K * nt + I]) continue;   // L[K block][I block] == 0
         const int K0 = K * LT, kh = min(LT, n - K0);
         // Lt[k][i] = L[K0+k][I0+i] = A[(K0+k) n + I0+i] (coalesced over i)
-        for (int k = 0; k < kh; k++) Lt[k * LP + lane] = on ? A[(size_t)(K0 + k) * n + I0 + lane] : 0.0;
+        stage_rows(Lt, A + (size_t)K0 * n + I0, n, kh, lane, on);
         if (lane == 0) wait_flag(done + K);
         __syncthreads();
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
@@ -260,7 +273,7 @@ __global__ void __launch_bounds__(64) k_ldlt_bwd(int n, const double* __restrict
             if (on) acc -= Lt[k * LP + lane] * xk;
         }
     }
-    for (int k = 0; k < ih; k++) Lt[k * LP + lane] = on ? A[(size_t)(I0 + k) * n + I0 + lane] : 0.0;
+    stage_rows(Lt, A + (size_t)I0 * n + I0, n, ih, lane, on);
     __syncthreads();
     for (int k = ih - 1; k >= 0; k--) {
         const double xk = rdlane(acc, k);
@@ -295,7 +308,7 @@ int ldlt_tiled_solve(int n, double* A, const double* b, double* x, double* scal,
     ORB_HIP_CHECK(hipMemsetAsync(flags, 0, sizeof(int) * (64 + 2 * nt), s));
     for (int p = 0; p < nt; p++) {
         const int m = nt - p - 1;
-        hipLaunchKernelGGL(k_ldlt_panel, dim3(nt - p), dim3(256), 0, s, n, p, A, nz, nt, fail, dstage);
+        hipLaunchKernelGGL(k_ldlt_panel, dim3(nt - p), dim3(64), 0, s, n, p, A, nz, nt, fail, dstage);
         hipLaunchKernelGGL(k_ldlt_trail, dim3(m * m + 1), dim3(256), 0, s, n, p, A, nz, nt, fail, dstage);
     }
     hipLaunchKernelGGL(k_ldlt_fwd, dim3(nt), dim3(64), 0, s, n, A, b, y, nz, nt, fail, done, scal);

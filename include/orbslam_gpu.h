@@ -346,6 +346,9 @@ int Optimizer_last_timings(double* ms2);
  * n <= 128; 1 = generic kernel) and the canonical FP64 sum. */
 int orbgpu_unit_ldlt_solve(int n, const double* S, const double* b, double* x, int variant, int* ok);
 int orbgpu_unit_csum(const double* v, int n, double* out);
+/* tiled LDL^T factorisation only (n x n row-major, upper triangle read): out = d on the
+ * diagonal, L in the strict lower triangle, eliminated rows in the strict upper. */
+int orbgpu_unit_ldlt_factor(int n, const double* S, double* out);
 /* one wave's canonical 64-tree of v64[0..64) (cross-lane permlane/DPP path) */
 int orbgpu_unit_wave_tree(const double* v64, double* out);
 
