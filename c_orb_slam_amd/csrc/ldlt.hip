@@ -87,12 +87,13 @@ __global__ void __launch_bounds__(64) k_ldlt_diag(int n, int p, double* __restri
             } else {
                 const double li = (lane > k && lane < pw) ? col[k] / d : 0.0;
                 Ls[k * LP + lane] = li;
+                // lanes j < i update their (never stored) lower-triangle slot too: no per-lane
+                // predicate, and the oracle's `l == 0` row skip is a wave-uniform branch
                 const double dkj = col[k];
 #pragma unroll
                 for (int i = k + 1; i < LT; i++) {
                     const double l = rdlane(li, i);
-                    const double v = col[i] - l * dkj;
-                    col[i] = (i <= lane && l != 0.0) ? v : col[i];
+                    if (l != 0.0) col[i] -= l * dkj;
                 }
             }
         }
@@ -143,8 +144,7 @@ __global__ void __launch_bounds__(64) k_ldlt_chunks(int n, int p, double* __rest
 #pragma unroll
                 for (int k = 0; k < i; k++) {
                     const double l = Ld[(size_t)i * n + k];   // wave-uniform
-                    const double v = c[i] - l * c[k];
-                    c[i] = l != 0.0 ? v : c[i];
+                    if (l != 0.0) c[i] -= l * c[k];
                 }
             }
         }
