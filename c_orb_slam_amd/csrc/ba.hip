@@ -1154,6 +1154,28 @@ __global__ void __launch_bounds__(256) k_gate(int ne, const EdgeDev* E, const Se
     }
 }
 
+// Sharded exchange of S: only the 64x64 tiles of the union Schur pattern travel.
+// tiles[t] = (I, J) with I <= J; buf = T * 4096 doubles (row-major tile, zero padded).
+__global__ void __launch_bounds__(256) k_tile_pack(int n, const double* __restrict__ S, const int2* tiles,
+                                                   double* buf) {
+    const int2 tj = tiles[blockIdx.x];
+    double* o = buf + (size_t)blockIdx.x * 4096;
+    for (int q = threadIdx.x; q < 4096; q += 256) {
+        const int r = tj.x * 64 + (q >> 6), c = tj.y * 64 + (q & 63);
+        o[q] = (r < n && c < n) ? S[(size_t)r * n + c] : 0.0;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_tile_unpack(int n, double* __restrict__ S, const int2* tiles,
+                                                     const double* buf) {
+    const int2 tj = tiles[blockIdx.x];
+    const double* o = buf + (size_t)blockIdx.x * 4096;
+    for (int q = threadIdx.x; q < 4096; q += 256) {
+        const int r = tj.x * 64 + (q >> 6), c = tj.y * 64 + (q & 63);
+        if (r < n && c < n) S[(size_t)r * n + c] = o[q];
+    }
+}
+
 // ---------------------------------------------------------------- host
 static void host_se3_from_Tcw(const float* T, Se3& o) {
     double R[9];
@@ -1177,6 +1199,7 @@ static void host_se3_to_Tcw(const Se3& s, float* T) {
 }
 
 BaEngine::~BaEngine() {
+    if (dPack_) (void)hipFree(dPack_);
     if (arena_) (void)hipFree(arena_);
     if (dStruct_) (void)hipFree(dStruct_);
     if (hScal_) (void)hipHostFree(hScal_);
@@ -1454,6 +1477,40 @@ int BaEngine::build_structure(int level) {
     st_.landPt = d + off[4]; st_.peStart = d + off[5]; st_.peList = d + off[6]; st_.leStart = d + off[7];
     st_.leList = d + off[8]; st_.lpStart = d + off[9]; st_.lpList = d + off[10]; st_.blkI = d + off[11];
     st_.blkJ = d + off[12]; st_.blkStart = d + off[13]; st_.pairA = d + off[14]; st_.pairB = d + off[15];
+    nTiles_ = 0;
+    if (comm_ && nP > 0) {
+        // union (over the shards) of the 64x64 tiles the Schur blocks touch; S travels as those tiles
+        const int n = 6 * nP, nt = (n + 63) / 64;
+        std::vector<double> tm((size_t)nt * nt, 0.0);
+        for (int b = 0; b < nBlk; b++) {
+            const int i1 = blkI[b], i2 = blkJ[b];
+            for (int I = (6 * i1) / 64; I <= (6 * i1 + 5) / 64; I++)
+                for (int J = (6 * i2) / 64; J <= (6 * i2 + 5) / 64; J++)
+                    if (I <= J) tm[(size_t)I * nt + J] = 1.0;
+        }
+        if (tm.size() > scratchN_) return -3;
+        ORB_HIP_CHECK(hipMemcpyAsync(dScratch_, tm.data(), sizeof(double) * tm.size(), hipMemcpyHostToDevice, stream_));
+        if (int e = comm_->allreduce(dScratch_, tm.size(), RedOp::Max, stream_)) return e;
+        ORB_HIP_CHECK(hipMemcpyAsync(tm.data(), dScratch_, sizeof(double) * tm.size(), hipMemcpyDeviceToHost, stream_));
+        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        std::vector<int2> tl;
+        for (int I = 0; I < nt; I++)
+            for (int J = I; J < nt; J++)
+                if (tm[(size_t)I * nt + J] != 0.0) tl.push_back(make_int2(I, J));
+        nTiles_ = (int)tl.size();
+        const size_t need = sizeof(int2) * tl.size() + 256 + sizeof(double) * ((size_t)nTiles_ * 4096 + n);
+        if (need > packCap_) {
+            if (dPack_) (void)hipFree(dPack_);
+            dPack_ = nullptr;
+            packCap_ = 0;
+            ORB_HIP_CHECK(hipMalloc(&dPack_, need));
+            packCap_ = need;
+        }
+        dTiles_ = (int2*)dPack_;
+        dPackBuf_ = (double*)((char*)dPack_ + ((sizeof(int2) * tl.size() + 255) & ~(size_t)255));
+        ORB_HIP_CHECK(hipMemcpyAsync(dTiles_, tl.data(), sizeof(int2) * tl.size(), hipMemcpyHostToDevice, stream_));
+        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
     ORB_HIP_CHECK(hipMemsetAsync(dX2_, 0, sizeof(double) * (6 * (size_t)nP + 3 * (size_t)nL + 1), stream_));
     ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * 36 * (size_t)nP * nP + 8, stream_));
     // the pageable hStruct_ copy must finish before the host vector is reused
@@ -1521,10 +1578,14 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         if (clearS && n) ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * (size_t)n * n, s));
         if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(1024), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
                                        lambda_, use_dev, dScal_, dS_, dBs_, own ? 1 : 0);
-        if (comm_) {
-            const RedBuf rb[2] = {{dS_, (size_t)n * n}, {dBs_, (size_t)n}};
+        if (comm_ && nTiles_) {   // all-reduce the union-pattern tiles of S and b_s (packed)
+            hipLaunchKernelGGL(k_tile_pack, dim3(nTiles_), dim3(256), 0, s, n, dS_, dTiles_, dPackBuf_);
+            double* pb = dPackBuf_ + (size_t)nTiles_ * 4096;
+            ORB_HIP_CHECK(hipMemcpyAsync(pb, dBs_, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
             ORB_HIP_CHECK(hipGetLastError());
-            if (int e = comm_->allreduce(rb, 2, RedOp::Sum, s)) return e;
+            if (int e = comm_->allreduce(dPackBuf_, (size_t)nTiles_ * 4096 + n, RedOp::Sum, s)) return e;
+            hipLaunchKernelGGL(k_tile_unpack, dim3(nTiles_), dim3(256), 0, s, n, dS_, dTiles_, dPackBuf_);
+            ORB_HIP_CHECK(hipMemcpyAsync(dBs_, pb, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
         }
         if (use_reg)
             hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_);

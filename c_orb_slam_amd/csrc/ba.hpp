@@ -114,6 +114,11 @@ private:
     Comm* comm_ = nullptr;
     bool stopRed_ = false;
     int nEglob_ = 0, nLglob_ = 0;
+    int nTiles_ = 0;               // union Schur tiles exchanged per trial
+    void* dPack_ = nullptr;
+    size_t packCap_ = 0;
+    int2* dTiles_ = nullptr;
+    double* dPackBuf_ = nullptr;
     BaMode mode_{};
     // LM state (g2o OptimizationAlgorithmLevenberg)
     double lambda_ = 0, ni_ = 2;
