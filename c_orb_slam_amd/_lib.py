@@ -90,6 +90,10 @@ def lib():
     L.ORBmatcher_SearchByProjection_LastFrame_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, f32, i32, vp]
     L.ORBmatcher_SearchByProjection_MapPoints.argtypes = [vp, P(orb_frame), vp, i32, vp, vp, vp, vp, vp, vp, vp,
                                                           P(orb_mappoints), f32, P(i32)]
+    L.ORBmatcher_ComputeStereoMatches.argtypes = [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp, f32, f32, vp, vp,
+                                                  P(i32)]
+    L.ORBmatcher_ComputeStereoMatches_batch.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, f32, vp, vp,
+                                                        vp]
     L.ORBmatcher_SearchCandidates.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp]
     L.orb_rng_seed.argtypes = [vp, C.c_uint]
     L.orb_rng_rand.argtypes = [vp]

@@ -2,11 +2,7 @@
 // Each replaces a member of ORB_SLAM2::ORBextractor (reference include/ORBextractor.h).
 #include <new>
 
-#include "orb_extract.hpp"
-
-struct ORBextractor_t {
-    orbgpu::Extractor* ex;
-};
+#include "capi_handles.hpp"
 
 extern "C" {
 

@@ -4,15 +4,12 @@
 #include <new>
 #include <vector>
 
-#include "orb_match.hpp"
+#include "capi_handles.hpp"
 
 using orbgpu::FrameDev;
 using orbgpu::Matcher;
 using orbgpu::SearchDev;
 
-struct ORBmatcher_t {
-    Matcher* m;
-};
 
 namespace {
 

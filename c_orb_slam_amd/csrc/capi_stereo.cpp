@@ -1,0 +1,136 @@
+// capi_stereo.cpp -- extern "C" ORBmatcher_ComputeStereoMatches[_batch] (include/orbslam_gpu.h).
+// Replaces ORB_SLAM2::Frame::ComputeStereoMatches (reference src/Frame.cc:466-640).
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "capi_handles.hpp"
+#include "stereo.hpp"
+
+namespace {
+size_t al(size_t n) { return (n + 255) & ~(size_t)255; }
+
+template <class T>
+T* up(orbgpu::Matcher* m, const T* src, size_t count, hipStream_t s, int* err) {
+    if (!src || count == 0) return nullptr;
+    void* d = m->arena_alloc(count * sizeof(T));
+    if (!d || hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, s) != hipSuccess) {
+        *err = ORB_E_HIP;
+        return nullptr;
+    }
+    return (T*)d;
+}
+}  // namespace
+
+extern "C" {
+
+int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, ORBextractor_h right, int npairs,
+                                          const int* NL, const orb_kp* const* keysL, const uint8_t* const* descL,
+                                          const int* NR, const orb_kp* const* keysR,
+                                          const uint8_t* const* descR, float mbf, float mb,
+                                          float* const* uRight, float* const* depth, int* nmatches) {
+    if (!h || !left || !right || npairs < 0 || !NL || !keysL || !descL || !NR || !keysR || !descR || !uRight ||
+        !depth || !nmatches)
+        return ORB_E_INVALID;
+    if (npairs == 0) return ORB_OK;
+    const orbgpu::Extractor* EL = left->ex;
+    const orbgpu::Extractor* ER = right->ex;
+    if (!EL->pyramid_base() || !ER->pyramid_base() || npairs > EL->last_batch() || npairs > ER->last_batch())
+        return ORB_E_INVALID;   // image p of the last extract() of both extractors
+    const auto& LL = EL->levels();
+    const auto& LR = ER->levels();
+    if (LL.size() != LR.size() || (int)LL.size() > orbgpu::kStereoMaxLevels) return ORB_E_INVALID;
+    for (size_t l = 0; l < LL.size(); l++)
+        if (LL[l].w != LR[l].w || LL[l].h != LR[l].h || LL[l].pitch != LR[l].pitch || LL[l].off != LR[l].off)
+            return ORB_E_INVALID;   // a rectified pair: equal image geometry
+    if (!(mb > 0.0f)) return ORB_E_INVALID;
+    for (int p = 0; p < npairs; p++) {
+        if (NL[p] < 0 || NR[p] < 0 || NL[p] > orbgpu::kStereoMaxKeys || NR[p] > 65535) return ORB_E_INVALID;
+        if ((NL[p] && (!keysL[p] || !descL[p] || !uRight[p] || !depth[p])) || (NR[p] && (!keysR[p] || !descR[p])))
+            return ORB_E_INVALID;
+    }
+    orbgpu::Matcher* m = h->m;
+    const bool dev = m->device_pointers();
+    hipStream_t s = m->stream();
+    // the pyramids are produced on the extractors' streams
+    if (hipStreamSynchronize(EL->stream()) != hipSuccess || hipStreamSynchronize(ER->stream()) != hipSuccess)
+        return ORB_E_HIP;
+    orbgpu::StereoParams P;
+    std::memset(&P, 0, sizeof(P));
+    for (size_t l = 0; l < LL.size(); l++) {
+        P.lv[l].off = (long long)LL[l].off;
+        P.lv[l].pitch = LL[l].pitch;
+        P.lv[l].w = LL[l].w;
+        P.lv[l].h = LL[l].h;
+        P.scale[l] = EL->scale()[l];
+        P.invScale[l] = EL->inv_scale()[l];
+    }
+    P.mbf = mbf;
+    P.mb = mb;
+    P.rows0 = LL[0].h;
+    size_t need = al(sizeof(orbgpu::StereoDev) * npairs) + al(4 * (size_t)npairs);
+    int maxNL = 0;
+    for (int p = 0; p < npairs; p++) {
+        need += al(4 * (size_t)NL[p]);
+        if (!dev) need += al(28 * (size_t)NL[p]) + al(32 * (size_t)NL[p]) + al(28 * (size_t)NR[p]) +
+                          al(32 * (size_t)NR[p]) + 2 * al(4 * (size_t)NL[p]);
+        maxNL = std::max(maxNL, NL[p]);
+    }
+    if (m->arena_reserve(need + 4096)) return ORB_E_HIP;
+    int err = 0;
+    std::vector<orbgpu::StereoDev> probs(npairs);
+    int* d_kept = (int*)m->arena_alloc(4 * (size_t)npairs);
+    for (int p = 0; p < npairs; p++) {
+        orbgpu::StereoDev& S = probs[p];
+        S.NL = NL[p];
+        S.NR = NR[p];
+        S.pyrL = EL->pyramid_base() + (size_t)p * EL->pyramid_image_bytes();
+        S.pyrR = ER->pyramid_base() + (size_t)p * ER->pyramid_image_bytes();
+        S.sad = (int*)m->arena_alloc(4 * (size_t)NL[p] + 4);
+        S.kept = d_kept + p;
+        if (dev) {
+            S.kL = (const orbgpu::orb_kp_dev*)keysL[p];
+            S.dL = descL[p];
+            S.kR = (const orbgpu::orb_kp_dev*)keysR[p];
+            S.dR = descR[p];
+            S.uRight = uRight[p];
+            S.depth = depth[p];
+        } else {
+            S.kL = (const orbgpu::orb_kp_dev*)up(m, keysL[p], (size_t)NL[p], s, &err);
+            S.dL = up(m, descL[p], 32 * (size_t)NL[p], s, &err);
+            S.kR = (const orbgpu::orb_kp_dev*)up(m, keysR[p], (size_t)NR[p], s, &err);
+            S.dR = up(m, descR[p], 32 * (size_t)NR[p], s, &err);
+            S.uRight = (float*)m->arena_alloc(4 * (size_t)NL[p] + 4);
+            S.depth = (float*)m->arena_alloc(4 * (size_t)NL[p] + 4);
+        }
+    }
+    if (err || !d_kept) return ORB_E_HIP;
+    auto* d_probs = (orbgpu::StereoDev*)m->arena_alloc(sizeof(orbgpu::StereoDev) * npairs);
+    if (!d_probs) return ORB_E_HIP;
+    if (hipMemcpyAsync(d_probs, probs.data(), sizeof(orbgpu::StereoDev) * npairs, hipMemcpyHostToDevice, s) !=
+        hipSuccess)
+        return ORB_E_HIP;
+    if (orbgpu::stereo_launch(d_probs, npairs, maxNL, P, s)) return ORB_E_HIP;
+    if (hipMemcpyAsync(nmatches, d_kept, 4 * (size_t)npairs, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return ORB_E_HIP;
+    if (!dev)
+        for (int p = 0; p < npairs; p++)
+            if (NL[p] && (hipMemcpyAsync(uRight[p], probs[p].uRight, 4 * (size_t)NL[p], hipMemcpyDeviceToHost, s) !=
+                              hipSuccess ||
+                          hipMemcpyAsync(depth[p], probs[p].depth, 4 * (size_t)NL[p], hipMemcpyDeviceToHost, s) !=
+                              hipSuccess))
+                return ORB_E_HIP;
+    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+}
+
+int ORBmatcher_ComputeStereoMatches(ORBmatcher_h h, ORBextractor_h left, ORBextractor_h right, int index, int NL,
+                                    const orb_kp* keysL, const uint8_t* descL, int NR, const orb_kp* keysR,
+                                    const uint8_t* descR, float mbf, float mb, float* uRight, float* depth,
+                                    int* nmatches) {
+    if (!h || !left || !right || index < 0) return ORB_E_INVALID;
+    if (index != 0) return ORB_E_INVALID;   // single form: image 0 of the last extract() call
+    return ORBmatcher_ComputeStereoMatches_batch(h, left, right, 1, &NL, &keysL, &descL, &NR, &keysR, &descR, mbf,
+                                                 mb, &uRight, &depth, nmatches);
+}
+
+}  // extern "C"

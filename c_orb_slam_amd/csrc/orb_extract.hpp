@@ -55,6 +55,12 @@ public:
     int get_blurred(int index, int level, uint8_t* dst, int dst_step, int* w, int* h);
     int timings(float* ms6);
     hipStream_t stream() const { return stream_; }
+    // Device pyramid of the last extract() (mvImagePyramid with its 19-px border): image b's
+    // padded level l starts at pyramid_base() + b * pyramid_image_bytes() + levels()[l].off.
+    const uint8_t* pyramid_base() const { return (const uint8_t*)d_pyr_; }
+    size_t pyramid_image_bytes() const { return img_bytes_; }
+    const std::vector<LevelHost>& levels() const { return levels_; }
+    int last_batch() const { return last_B_; }
 
     int nlevels() const { return nlevels_; }
     float scale_factor() const { return scaleFactor_; }

@@ -1,0 +1,208 @@
+// stereo.hip -- gfx950 Frame::ComputeStereoMatches (reference src/Frame.cc:466-640).
+//
+// Rectified stereo: for every left keypoint the best right keypoint (256-bit Hamming) among
+// those whose row band (y +- 2 * scale) covers the left row, octave within +-1 and u_R in
+// [u_L - bf/b, u_L]; then an 11x11 SAD over +-5 pixel shifts on the padded pyramid level of
+// the left octave, a parabola through the best three SADs, depth = bf / disparity, and the
+// 2.1 x median SAD outlier filter.  No occupancy: every left keypoint is independent.
+//
+//   k_stereo_match   one wave per left keypoint (4 per workgroup), all pairs of the batch in
+//                    one launch (grid.y = pair): lanes sweep the right keypoints in index
+//                    order with popcount distances, a wave min over (dist, iR) picks the
+//                    reference's first strict minimum; the 11 SADs are integer wave sums
+//                    (cv::norm of centred integer windows is exact), the parabola and the
+//                    disparity follow the reference's float expression order.
+//   k_stereo_filter  one workgroup per pair: bitonic sort of the kept SADs in LDS, median,
+//                    thDist = 1.5f*1.4f*median, invalidation of SAD >= thDist.
+#include "stereo.hpp"
+
+#include <climits>
+
+namespace orbgpu {
+
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ unsigned wave_min_u(unsigned v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
+__global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restrict__ probs, StereoParams P) {
+    const StereoDev& S = probs[blockIdx.y];
+    const int lane = threadIdx.x & 63;
+    const int iL = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (iL >= S.NL) return;
+    const orb_kp_dev kpL = S.kL[iL];
+    float uR_out = -1.0f, depth_out = -1.0f;
+    int sad_out = -1;
+    const int levelL = kpL.octave;
+    const float vL = kpL.y, uL = kpL.x;
+    const int row = (int)vL;                                  // vRowIndices[vL]
+    const float minZ = P.mb, minD = 0.0f, maxD = P.mbf / minZ;
+    const float minU = uL - maxD, maxU = uL - minD;
+    if (row >= 0 && row < P.rows0 && !(maxU < 0)) {
+        // best right keypoint: first strict minimum below TH_HIGH in iR order
+        const uint32_t* dl = (const uint32_t*)(S.dL + 32 * (size_t)iL);   // descriptors: 4-B aligned rows
+        uint32_t q[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) q[k] = dl[k];
+        unsigned best = 0xffffffffu;
+        for (int iR = lane; iR < S.NR; iR += 64) {
+            const orb_kp_dev kpR = S.kR[iR];
+            const float r = 2.0f * P.scale[kpR.octave];
+            const int maxr = (int)ceilf(kpR.y + r), minr = (int)floorf(kpR.y - r);
+            if (row < minr || row > maxr) continue;
+            if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+            const float uR = kpR.x;
+            if (!(uR >= minU && uR <= maxU)) continue;
+            const uint32_t* dr = (const uint32_t*)(S.dR + 32 * (size_t)iR);
+            int dist = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) dist += __popc(q[k] ^ dr[k]);
+            if (dist < 100) best = min(best, ((unsigned)dist << 16) | (unsigned)iR);
+        }
+        best = wave_min_u(best);
+        const int bestDist = best == 0xffffffffu ? 100 : (int)(best >> 16);
+        const int bestIdxR = (int)(best & 0xffffu);
+        if (bestDist < 75) {   // thOrbDist = (TH_HIGH + TH_LOW) / 2
+            const float uR0 = S.kR[bestIdxR].x;
+            const float scaleFactor = P.invScale[levelL];
+            const float scaleduL = roundf(kpL.x * scaleFactor);
+            const float scaledvL = roundf(kpL.y * scaleFactor);
+            const float scaleduR0 = roundf(uR0 * scaleFactor);
+            const int w = 5, L = 5;
+            const StereoLevel lv = P.lv[levelL];
+            const float iniu = scaleduR0 + L - w, endu = scaleduR0 + L + w + 1;
+            if (!(iniu < 0 || endu >= lv.w)) {
+                const uint8_t* IL = S.pyrL + lv.off + (size_t)kEdge * lv.pitch + kEdge;
+                const uint8_t* IR = S.pyrR + lv.off + (size_t)kEdge * lv.pitch + kEdge;
+                const int yL = (int)scaledvL, xL = (int)scaleduL, xR0 = (int)scaleduR0;
+                const int cL = IL[(ptrdiff_t)yL * lv.pitch + xL];
+                // lane owns window pixels p = lane and lane + 64 (p < 121)
+                int a[2], dyv[2], dxv[2];
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    const int p = lane + 64 * t;
+                    dyv[t] = p / 11 - 5;
+                    dxv[t] = p % 11 - 5;
+                    a[t] = p < 121 ? IL[(ptrdiff_t)(yL + dyv[t]) * lv.pitch + xL + dxv[t]] - cL : 0;
+                }
+                int vD[11];
+#pragma unroll
+                for (int inc = 0; inc < 11; inc++) {
+                    const int xR = xR0 + inc - L;
+                    const int cR = IR[(ptrdiff_t)yL * lv.pitch + xR];
+                    int s = 0;
+#pragma unroll
+                    for (int t = 0; t < 2; t++) {
+                        const int p = lane + 64 * t;
+                        if (p < 121) s += abs(a[t] - (IR[(ptrdiff_t)(yL + dyv[t]) * lv.pitch + xR + dxv[t]] - cR));
+                    }
+                    vD[inc] = wave_sum_i(s);
+                }
+                int bestD = INT_MAX, bestinc = 0;
+#pragma unroll
+                for (int inc = 0; inc < 11; inc++)
+                    if (vD[inc] < bestD) {
+                        bestD = vD[inc];
+                        bestinc = inc - L;
+                    }
+                if (bestinc != -L && bestinc != L) {
+                    const float dist1 = (float)vD[L + bestinc - 1];
+                    const float dist2 = (float)vD[L + bestinc];
+                    const float dist3 = (float)vD[L + bestinc + 1];
+                    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+                    if (!(deltaR < -1 || deltaR > 1)) {
+                        float bestuR = P.scale[levelL] * ((float)scaleduR0 + (float)bestinc + deltaR);
+                        float disparity = (uL - bestuR);
+                        if (disparity >= minD && disparity < maxD) {
+                            if (disparity <= 0) {
+                                disparity = (float)0.01;
+                                bestuR = (float)((double)uL - 0.01);
+                            }
+                            depth_out = P.mbf / disparity;
+                            uR_out = bestuR;
+                            sad_out = bestD;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        S.uRight[iL] = uR_out;
+        S.depth[iL] = depth_out;
+        S.sad[iL] = sad_out;
+    }
+}
+
+// median filter (Frame.cc:624-639): sort the kept SADs, thDist = 1.5f*1.4f*median,
+// invalidate SAD >= thDist (the reference walks the sorted tail from the end).
+__global__ void __launch_bounds__(1024) k_stereo_filter(const StereoDev* __restrict__ probs) {
+    const StereoDev& S = probs[blockIdx.x];
+    __shared__ int v[kStereoMaxKeys];
+    __shared__ int cnt, kept;
+    const int tid = threadIdx.x;
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    for (int i = tid; i < S.NL; i += blockDim.x) {
+        const int d = S.sad[i];
+        if (d >= 0) v[atomicAdd(&cnt, 1)] = d;
+    }
+    __syncthreads();
+    const int n = cnt;
+    if (n == 0) {   // empty vDistIdx is UB in the reference; nothing to filter
+        if (tid == 0) *S.kept = 0;
+        return;
+    }
+    int m = 1;
+    while (m < n) m <<= 1;
+    for (int i = n + tid; i < m; i += blockDim.x) v[i] = INT_MAX;
+    __syncthreads();
+    for (int k = 2; k <= m; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < m; i += blockDim.x) {
+                const int ix = i ^ j;
+                if (ix > i) {
+                    const bool up = (i & k) == 0;
+                    const int a = v[i], b = v[ix];
+                    if ((a > b) == up) {
+                        v[i] = b;
+                        v[ix] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    const float median = (float)v[n / 2];
+    const float thDist = 1.5f * 1.4f * median;
+    if (tid == 0) kept = n;
+    __syncthreads();
+    for (int i = tid; i < S.NL; i += blockDim.x) {
+        const int d = S.sad[i];
+        if (d >= 0 && !((float)d < thDist)) {
+            S.uRight[i] = -1.0f;
+            S.depth[i] = -1.0f;
+            atomicSub(&kept, 1);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) *S.kept = kept;
+}
+
+int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoParams& P, hipStream_t s) {
+    if (nprob <= 0) return 0;
+    if (maxNL > 0)
+        hipLaunchKernelGGL(k_stereo_match, dim3((maxNL + 3) / 4, nprob), dim3(256), 0, s, d_probs, P);
+    hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(1024), 0, s, d_probs);
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace orbgpu

@@ -1,0 +1,44 @@
+// stereo.hpp -- gfx950 Frame::ComputeStereoMatches (see stereo.hip).  Reference src/Frame.cc:466-640.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "orb_common.hpp"
+#include "orb_extract.hpp"
+
+namespace orbgpu {
+
+constexpr int kStereoMaxKeys = 4096;
+constexpr int kStereoMaxLevels = 16;
+
+struct StereoLevel {   // padded level l of one image slab: (0,0) of the unpadded level at +19 rows/cols
+    long long off;
+    int pitch, w, h;
+};
+
+struct StereoParams {
+    StereoLevel lv[kStereoMaxLevels];
+    float scale[kStereoMaxLevels], invScale[kStereoMaxLevels];
+    float mbf, mb;
+    int rows0;         // mvImagePyramid[0].rows
+};
+
+// one stereo pair
+struct StereoDev {
+    int NL, NR;
+    const orb_kp_dev* kL;   // mvKeys (left)
+    const uint8_t* dL;      // mDescriptors
+    const orb_kp_dev* kR;   // mvKeysRight
+    const uint8_t* dR;      // mDescriptorsRight
+    const uint8_t* pyrL;    // left extractor pyramid slab of this image
+    const uint8_t* pyrR;
+    float* uRight;          // out: mvuRight (NL)
+    float* depth;           // out: mvDepth (NL)
+    int* sad;               // scratch (NL): best SAD or -1
+    int* kept;              // out: stereo matches after the median filter
+};
+
+int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoParams& P, hipStream_t s);
+
+}  // namespace orbgpu

@@ -243,6 +243,40 @@ class ORBmatcher:
                                                               C.byref(n)), "SearchByProjection(MapPoints)")
         return n.value
 
+    def ComputeStereoMatches(self, left, right, keysL, descL, keysR, descR, mbf, mb):
+        """Frame::ComputeStereoMatches() (Frame.cc:466-640) for image 0 of the last call of the
+        `left` / `right` ORBextractors (their mvImagePyramid).  -> (mvuRight, mvDepth, nmatches)."""
+        kL = np.ascontiguousarray(keysL, KP_DTYPE)
+        kR = np.ascontiguousarray(keysR, KP_DTYPE)
+        dL = np.ascontiguousarray(descL if descL is not None else np.zeros((0, 32)), np.uint8)
+        dR = np.ascontiguousarray(descR if descR is not None else np.zeros((0, 32)), np.uint8)
+        uR = np.zeros(max(len(kL), 1), np.float32)
+        dep = np.zeros(max(len(kL), 1), np.float32)
+        n = C.c_int()
+        check(self._L.ORBmatcher_ComputeStereoMatches(self._h, left._h, right._h, 0, len(kL), ptr(kL), ptr(dL),
+                                                      len(kR), ptr(kR), ptr(dR), float(mbf), float(mb), ptr(uR),
+                                                      ptr(dep), C.byref(n)), "ORBmatcher_ComputeStereoMatches")
+        return uR[:len(kL)], dep[:len(kL)], n.value
+
+    def ComputeStereoMatches_batch(self, left, right, keysL, descL, keysR, descR, mbf, mb):
+        """Batched form over the images 0..P-1 of the last extract_batch of both extractors."""
+        P = len(keysL)
+        kL = [np.ascontiguousarray(k, KP_DTYPE) for k in keysL]
+        kR = [np.ascontiguousarray(k, KP_DTYPE) for k in keysR]
+        dL = [np.ascontiguousarray(d if d is not None else np.zeros((0, 32)), np.uint8) for d in descL]
+        dR = [np.ascontiguousarray(d if d is not None else np.zeros((0, 32)), np.uint8) for d in descR]
+        uR = [np.zeros(max(len(k), 1), np.float32) for k in kL]
+        dep = [np.zeros(max(len(k), 1), np.float32) for k in kL]
+        arr = lambda xs: (C.c_void_p * P)(*[x.ctypes.data for x in xs])
+        NL = np.array([len(k) for k in kL], np.int32)
+        NR = np.array([len(k) for k in kR], np.int32)
+        n = np.zeros(P, np.int32)
+        check(self._L.ORBmatcher_ComputeStereoMatches_batch(self._h, left._h, right._h, P, ptr(NL), arr(kL), arr(dL),
+                                                            ptr(NR), arr(kR), arr(dR), float(mbf), float(mb),
+                                                            arr(uR), arr(dep), ptr(n)),
+              "ORBmatcher_ComputeStereoMatches_batch")
+        return [u[:len(k)] for u, k in zip(uR, kL)], [d[:len(k)] for d, k in zip(dep, kL)], n
+
     def SearchCandidates(self, qdesc, tdesc, offsets, cand):
         q = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
         t = np.ascontiguousarray(tdesc, np.uint8).reshape(-1, 32)

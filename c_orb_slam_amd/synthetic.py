@@ -111,3 +111,35 @@ def pose_from_rotation(R, t=(0.0, 0.0, 0.0)):
     T[:3, :3] = R
     T[:3, 3] = t
     return T
+
+
+def stereo_pair(rng, w=KITTI_W, h=KITTI_H, n_rects=None, max_disp=64):
+    """Rectified stereo pair: the right image is the left one with every
+    rectangle shifted left by its own integer disparity in [0, max_disp]; independent sensor noise."""
+    if n_rects is None:
+        n_rects = max(40, (w * h) // 400)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    gx, gy = rng.uniform(-0.1, 0.1, size=2)
+    base = 110.0 + gx * (xx - w / 2) + gy * (yy - h / 2)
+    left, right = base.copy(), base.copy()
+    for _ in range(n_rects):
+        big = rng.random() < 0.1
+        rw = rng.integers(6, max(8, w // (6 if big else 40)))
+        rh = rng.integers(6, max(8, h // (4 if big else 20)))
+        x0, y0 = rng.integers(-rw // 2, w), rng.integers(-rh // 2, h)
+        v = rng.uniform(0, 255)
+        d = int(rng.integers(0, max_disp + 1))
+        left[max(0, y0):max(0, y0 + rh), max(0, x0):max(0, x0 + rw)] = v
+        right[max(0, y0):max(0, y0 + rh), max(0, x0 - d):max(0, x0 - d + rw)] = v
+    out = []
+    for img in (left, right):
+        img = img + rng.normal(0.0, 3.0, size=img.shape)
+        out.append(np.clip(np.rint(img), 0, 255).astype(np.uint8))
+    return out[0], out[1]
+
+
+def stereo_batch(seed, n, w=KITTI_W, h=KITTI_H):
+    """n independent stereo pairs: (lefts, rights), each (n, h, w) u8."""
+    rng = np.random.default_rng(seed)
+    pairs = [stereo_pair(rng, w, h) for _ in range(n)]
+    return np.stack([p[0] for p in pairs]), np.stack([p[1] for p in pairs])

@@ -168,6 +168,26 @@ int ORBmatcher_SearchByProjection_MapPoints(ORBmatcher_h h, const orb_frame* F, 
                                             const float* view_cos, const int32_t* mp_index,
                                             const orb_mappoints* mps, float th, int* nmatches);
 
+/* void Frame::ComputeStereoMatches()                            Frame.cc:466-640
+ * Rectified stereo matching of the left keypoints of image `index` (0 only for the single
+ * form; image p of the batch form) of the last ORBextractor_extract[_batch] call of `left`
+ * and `right`: mvImagePyramid (with border) is read from those extractors, the scale
+ * tables from `left`.  keysL/descL: mvKeys/mDescriptors (NL), keysR/descR: mvKeysRight /
+ * mDescriptorsRight (NR).  mbf, mb: Frame::mbf, mb.  Outputs mvuRight / mvDepth (NL
+ * floats, -1 = no stereo) and *nmatches = the stereo matches kept after the median filter.
+ * Pointer space per ORBmatcher_set_device_pointers.  NL <= 4096. */
+int ORBmatcher_ComputeStereoMatches(ORBmatcher_h h, ORBextractor_h left, ORBextractor_h right, int index,
+                                    int NL, const orb_kp* keysL, const uint8_t* descL, int NR,
+                                    const orb_kp* keysR, const uint8_t* descR, float mbf, float mb,
+                                    float* uRight, float* depth, int* nmatches);
+/* `npairs` stereo pairs (images 0..npairs-1 of the last batch calls) in one launch. */
+int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, ORBextractor_h right,
+                                          int npairs, const int* NL, const orb_kp* const* keysL,
+                                          const uint8_t* const* descL, const int* NR,
+                                          const orb_kp* const* keysR, const uint8_t* const* descR,
+                                          float mbf, float mb, float* const* uRight,
+                                          float* const* depth, int* nmatches);
+
 /* Hamming distances for CSR candidate lists (the inner loop of every Search*):
  * query q (descriptor qdesc[q]) against train rows cand[off[q] .. off[q+1]).
  * Writes dist[k] for every candidate k and best/second per query

@@ -177,6 +177,15 @@ void  ora_sim3_estimate(const ora_sim3* S, float* R, float* t, float* s);
 int   ora_sim3_iterations(const ora_sim3* S);
 
 
+/* ---- Frame::ComputeStereoMatches (stereo.c), reference Frame.cc:466-640 ----------
+ * kL/dL: left mvKeys + descriptors (NL), kR/dR: right (NR); exL/exR: the extractors that
+ * produced them (their last pyramids); rows0 = level-0 rows.  Writes mvuRight / mvDepth
+ * (-1 = none) and returns the number of stereo matches kept after the median filter. */
+int   ora_compute_stereo_matches(const ora_kp* kL, const uint8_t* dL, int NL, const ora_kp* kR,
+                                 const uint8_t* dR, int NR, const ora_extractor* exL,
+                                 const ora_extractor* exR, int rows0, float mbf, float mb,
+                                 float* uRight, float* depth);
+
 /* ---- Local bundle adjustment (ba.c), reference Optimizer.cc:453-778 + g2o --- */
 typedef struct {
     int n_kf;

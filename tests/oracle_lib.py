@@ -119,6 +119,24 @@ class OracleExtractor:
         return dict(scale=sc, inv_scale=isc, sigma2=s2, inv_sigma2=is2, n_per_level=npl, umax=umax)
 
 
+def oracle_stereo_matches(exL, exR, kL, dL, kR, dR, rows0, mbf, mb):
+    """Frame::ComputeStereoMatches (Frame.cc:466-640) on the oracle extractors' last pyramids.
+    -> (uRight, depth, kept)."""
+    L = lib()
+    L.ora_compute_stereo_matches.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                             C.c_void_p, C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_void_p,
+                                             C.c_void_p]
+    kL = np.ascontiguousarray(kL, KP_DTYPE)
+    kR = np.ascontiguousarray(kR, KP_DTYPE)
+    dL = np.ascontiguousarray(dL, np.uint8) if len(kL) else np.zeros((1, 32), np.uint8)
+    dR = np.ascontiguousarray(dR, np.uint8) if len(kR) else np.zeros((1, 32), np.uint8)
+    uR = np.zeros(max(len(kL), 1), np.float32)
+    dep = np.zeros(max(len(kL), 1), np.float32)
+    kept = L.ora_compute_stereo_matches(ptr(kL), ptr(dL), len(kL), ptr(kR), ptr(dR), len(kR), C.c_void_p(exL.h),
+                                        C.c_void_p(exR.h), int(rows0), float(mbf), float(mb), ptr(uR), ptr(dep))
+    return uR[:len(kL)], dep[:len(kL)], kept
+
+
 # ---------------------------------------------------------------- matcher oracle
 class ora_frame(C.Structure):
     _fields_ = [("N", C.c_int), ("kpsUn", C.c_void_p), ("desc", C.c_void_p), ("uRight", C.c_void_p),

@@ -264,3 +264,22 @@ def test_sim3_oracle_recovers_similarity(fix):
     mask[pr["outliers"]] = True
     flagged = inl[pr["idx1"]]
     assert not np.any(flagged & mask), "an outlier accepted as inlier"
+
+
+def test_oracle_stereo_recovers_disparity():
+    """Frame::ComputeStereoMatches restatement (oracle/stereo.c) on a synthetic rectified pair:
+    kept matches sit at the rectangles' integer disparities (0..64) within a pixel."""
+    from c_orb_slam_amd import synthetic
+    L, R = synthetic.stereo_batch(0, 1, 1241, 376)
+    exL, exR = oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7), oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7)
+    kL, dL = exL(L[0])
+    kR, dR = exR(R[0])
+    mbf = 386.1448
+    mb = np.float32(np.float32(mbf) / np.float32(718.856))
+    uR, dep, kept = oracle_lib.oracle_stereo_matches(exL, exR, kL, dL, kR, dR, 376, mbf, mb)
+    ok = uR >= 0
+    assert kept == ok.sum() and kept > 50
+    d = kL["x"][ok] - uR[ok]
+    near_int = np.abs(d - np.round(d)) < 0.75
+    assert near_int.mean() > 0.8 and (np.round(d) <= 65).mean() > 0.9
+    np.testing.assert_allclose(dep[ok], mbf / d, rtol=1e-5)
