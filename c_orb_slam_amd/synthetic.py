@@ -143,3 +143,27 @@ def stereo_batch(seed, n, w=KITTI_W, h=KITTI_H):
     rng = np.random.default_rng(seed)
     pairs = [stereo_pair(rng, w, h) for _ in range(n)]
     return np.stack([p[0] for p in pairs]), np.stack([p[1] for p in pairs])
+
+
+def stereo_sequence(seed, n_frames, w=KITTI_W, h=KITTI_H, return_rotations=False):
+    """Left frames as in sequence(); right frame = left resampled with a smooth ground-plane-like
+    disparity field d(x, y) = 4 + 36 * y / h (+-2 px ripple), plus independent noise."""
+    out = sequence(seed, n_frames, w, h, return_rotations=True)
+    lefts = out[0]
+    rng = np.random.default_rng(seed + 7919)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    d = 4.0 + 36.0 * yy / h + 2.0 * np.sin(xx / 37.0)
+    sx = np.clip(xx + d, 0, w - 1.001)
+    x0 = np.floor(sx).astype(np.int64)
+    fx = sx - x0
+    rights = []
+    for L in lefts:
+        f = L.astype(np.float64)
+        yi = yy.astype(np.int64)
+        v = f[yi, x0] * (1 - fx) + f[yi, x0 + 1] * fx
+        v += rng.normal(0.0, 1.0, size=v.shape)
+        rights.append(np.clip(np.rint(v), 0, 255).astype(np.uint8))
+    rights = np.stack(rights)
+    if return_rotations:
+        return lefts, rights, out[1], out[2]
+    return lefts, rights
