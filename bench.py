@@ -151,11 +151,17 @@ def main():
     s_dep = arr([d_depth[b].data_ptr() for b in range(B)])
     nm = np.zeros(P, np.int32)
     nst = np.zeros(B, np.int32)
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(1, initializer=lambda: torch.cuda.set_device(dev))   # HIP device is per thread
 
     def step():
         # Frame(imLeft, imRight): two ORBextractor calls (Frame.cc:78-81), then ComputeStereoMatches
+        # the two extractors run concurrently on their own streams / host octree pools, like the
+        # reference's two extractor threads per stereo frame
+        fR = pool.submit(exR.extract_device, d_R.data_ptr(), B, W, H, W, W * H, d_kpsR.data_ptr(),
+                         d_descR.data_ptr(), cap)
         nL = exL.extract_device(d_L.data_ptr(), B, W, H, W, W * H, d_kps.data_ptr(), d_desc.data_ptr(), cap)
-        nR = exR.extract_device(d_R.data_ptr(), B, W, H, W, W * H, d_kpsR.data_ptr(), d_descR.data_ptr(), cap)
+        nR = fR.result()
         nL = np.ascontiguousarray(nL, np.int32)
         nR = np.ascontiguousarray(nR, np.int32)
         check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, exL._h, exR._h, B, ptr(nL), s_kL, s_dL, ptr(nR), s_kR,
