@@ -5,7 +5,7 @@ junejunejune/c_orb_slam classes on the hot path.  All compute runs in the HIP
 library liborbslam_gpu.so (gfx950); there is no CPU fallback.
 """
 from ._lib import KP_DTYPE, OrbGpuError, device_available, lib  # noqa: F401
-from .orb import Frame, MapPoints, ORBextractor, ORBmatcher  # noqa: F401
+from .orb import FeatureVector, Frame, MapPoints, ORBextractor, ORBmatcher  # noqa: F401
 from .optimizer import BundleAdjustment, LocalBundleAdjustment  # noqa: F401
 
 __all__ = ["ORBextractor", "ORBmatcher", "Frame", "MapPoints", "KP_DTYPE", "OrbGpuError",

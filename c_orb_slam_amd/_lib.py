@@ -44,6 +44,10 @@ class orb_frame(C.Structure):
                 ("cy", C.c_float), ("bf", C.c_float), ("b", C.c_float), ("Tcw", C.c_void_p)]
 
 
+class orb_featvec(C.Structure):
+    _fields_ = [("n_nodes", C.c_int), ("node_id", C.c_void_p), ("start", C.c_void_p), ("feat", C.c_void_p)]
+
+
 class orb_mappoints(C.Structure):
     _fields_ = [("n", C.c_int), ("pos", C.c_void_p), ("desc", C.c_void_p), ("observations", C.c_void_p)]
 
@@ -94,6 +98,15 @@ def lib():
                                                   P(i32)]
     L.ORBmatcher_ComputeStereoMatches_batch.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, f32, vp, vp,
                                                         vp]
+    L.ORBmatcher_SearchByProjection_KeyFrame.argtypes = [vp, P(orb_frame), vp, i32, vp, vp, vp, P(orb_mappoints), vp,
+                                                         vp, f32, f32, i32, P(i32)]
+    L.ORBmatcher_SearchForInitialization.argtypes = [vp, P(orb_frame), P(orb_frame), vp, vp, i32, P(i32)]
+    L.ORBmatcher_SearchByBoW_Frame.argtypes = [vp, i32, vp, vp, vp, vp, P(orb_featvec), i32, vp, vp, P(orb_featvec),
+                                               vp, P(i32)]
+    L.ORBmatcher_SearchByBoW_KeyFrames.argtypes = [vp, i32, vp, vp, vp, vp, P(orb_featvec), i32, vp, vp, vp, vp,
+                                                   P(orb_featvec), vp, P(i32)]
+    L.ORBmatcher_SearchForTriangulation.argtypes = [vp, P(orb_frame), vp, P(orb_featvec), P(orb_frame), vp,
+                                                    P(orb_featvec), vp, vp, i32, vp, i32, P(i32)]
     L.ORBmatcher_SearchCandidates.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp]
     L.orb_rng_seed.argtypes = [vp, C.c_uint]
     L.orb_rng_rand.argtypes = [vp]

@@ -464,8 +464,87 @@ __global__ void __launch_bounds__(256) k_csr_hamming(const uint8_t* __restrict__
     }
 }
 
+// ------------------------------------------------------- area-candidate engine
+// Frame::GetFeaturesInArea windows of arbitrary queries over one frame grid, every candidate
+// with its Hamming distance, in the reference's enumeration order (CSR).  The order-dependent
+// selection of the remaining ORBmatcher searches is replayed on the host from these lists.
+__global__ void __launch_bounds__(256) k_area_count(const SearchDev* __restrict__ probs, const AreaQuery* __restrict__ q,
+                                                    int nq, int* __restrict__ cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const AreaQuery a = q[i];
+    int c = 0;
+    if (a.qd >= 0) {
+        QueryWin w{a.x, a.y, a.r, a.minLevel, a.maxLevel};
+        for_features_in_area(probs[0], w, [&](int) { c++; });
+    }
+    cnt[i] = c;
+}
+
+__global__ void __launch_bounds__(256) k_area_fill(const SearchDev* __restrict__ probs, const AreaQuery* __restrict__ q,
+                                                   int nq, const uint8_t* __restrict__ qdesc, const int* __restrict__ off,
+                                                   int2* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const AreaQuery a = q[i];
+    if (a.qd < 0) return;
+    const SearchDev& P = probs[0];
+    const uint8_t* d0 = qdesc + 32 * (size_t)a.qd;
+    int k = off[i];
+    QueryWin w{a.x, a.y, a.r, a.minLevel, a.maxLevel};
+    for_features_in_area(P, w, [&](int idx) { out[k++] = make_int2(idx, hamming32(d0, P.cur.desc + 32 * (size_t)idx)); });
+}
+
+int Matcher::area_candidates(const SearchDev& frame, const AreaQuery* d_q, int nq, const uint8_t* d_qdesc,
+                             std::vector<int>& off, std::vector<int2>& cand) {
+    off.assign((size_t)nq + 1, 0);
+    cand.clear();
+    if (frame.cur.N > kMaxFrameKeys || frame.cur.N < 0) return -1;
+    const size_t grid = ((size_t)(kGridCells + 1 + frame.cur.N) * 4 + 255) & ~(size_t)255;
+    const size_t need = grid + 2 * (((size_t)nq + 1) * 4 + 256) + sizeof(SearchDev) + 256;
+    if (need > scratch_cap_) {
+        if (d_scratch_) (void)hipFree(d_scratch_);
+        scratch_cap_ = need * 2;
+        ORB_HIP_CHECK(hipMalloc(&d_scratch_, scratch_cap_));
+    }
+    char* s = (char*)d_scratch_;
+    SearchDev P = frame;
+    P.gridStart = (int*)s;
+    P.gridIdx = P.gridStart + kGridCells + 1;
+    s += grid;
+    int* d_cnt = (int*)s;
+    s += (((size_t)nq + 1) * 4 + 255) & ~(size_t)255;
+    int* d_off = (int*)s;
+    s += (((size_t)nq + 1) * 4 + 255) & ~(size_t)255;
+    SearchDev* dp = (SearchDev*)s;
+    ORB_HIP_CHECK(hipMemcpyAsync(dp, &P, sizeof(SearchDev), hipMemcpyHostToDevice, stream_));
+    hipLaunchKernelGGL(k_build_grid, dim3(1), dim3(256), 0, stream_, dp);
+    if (nq == 0) return hipStreamSynchronize(stream_) == hipSuccess ? 0 : -2;
+    hipLaunchKernelGGL(k_area_count, dim3((nq + 255) / 256), dim3(256), 0, stream_, dp, d_q, nq, d_cnt);
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipMemcpyAsync(off.data() + 1, d_cnt, sizeof(int) * nq, hipMemcpyDeviceToHost, stream_));
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int i = 0; i < nq; i++) off[i + 1] += off[i];
+    const int total = off[nq];
+    cand.resize((size_t)std::max(total, 1));
+    if (total == 0) return 0;
+    if ((size_t)total * sizeof(int2) > cand_cap_) {
+        if (d_cand_) (void)hipFree(d_cand_);
+        cand_cap_ = (size_t)total * sizeof(int2) * 2;
+        ORB_HIP_CHECK(hipMalloc(&d_cand_, cand_cap_));
+    }
+    ORB_HIP_CHECK(hipMemcpyAsync(d_off, off.data(), sizeof(int) * ((size_t)nq + 1), hipMemcpyHostToDevice, stream_));
+    hipLaunchKernelGGL(k_area_fill, dim3((nq + 255) / 256), dim3(256), 0, stream_, dp, d_q, nq, d_qdesc, d_off,
+                       (int2*)d_cand_);
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipMemcpyAsync(cand.data(), d_cand_, sizeof(int2) * (size_t)total, hipMemcpyDeviceToHost, stream_));
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    return 0;
+}
+
 // --------------------------------------------------------------------- host
 Matcher::~Matcher() {
+    if (d_cand_) (void)hipFree(d_cand_);
     if (d_scratch_) (void)hipFree(d_scratch_);
     if (d_probs_) (void)hipFree(d_probs_);
     if (d_arena_) (void)hipFree(d_arena_);

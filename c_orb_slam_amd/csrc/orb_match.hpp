@@ -58,6 +58,13 @@ struct SearchDev {
     int2* hist;       // nq (bin, idx)
 };
 
+// one GetFeaturesInArea query of the area-candidate engine; qd = query descriptor row (-1 = none)
+struct AreaQuery {
+    float x, y, r;
+    int minLevel, maxLevel;
+    int qd;
+};
+
 class Matcher {
 public:
     Matcher(float nnratio, bool checkOri) : nnratio_(nnratio), checkOri_(checkOri) {}
@@ -74,6 +81,10 @@ public:
     float nnratio() const { return nnratio_; }
     bool check_ori() const { return checkOri_; }
 
+    // Every GetFeaturesInArea candidate (idx, Hamming distance) of each query over `frame`
+    // (its cur frame: device keysUn/desc + grid geometry), CSR in reference order, to host.
+    int area_candidates(const SearchDev& frame, const AreaQuery* d_q, int nq, const uint8_t* d_qdesc,
+                        std::vector<int>& off, std::vector<int2>& cand);
     // device arena for host-pointer mode: reserve() resets it, alloc() carves it
     int arena_reserve(size_t bytes);
     void* arena_alloc(size_t bytes);
@@ -90,6 +101,8 @@ private:
     size_t probs_cap_ = 0;
     void* d_arena_ = nullptr;
     size_t arena_cap_ = 0, arena_used_ = 0;
+    void* d_cand_ = nullptr;
+    size_t cand_cap_ = 0;
 };
 
 }  // namespace orbgpu

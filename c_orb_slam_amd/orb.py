@@ -10,7 +10,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (KP_DTYPE, ORB_E_CAPACITY, OrbGpuError, check, lib, orb_frame, orb_mappoints, ptr)
+from ._lib import (KP_DTYPE, ORB_E_CAPACITY, OrbGpuError, check, lib, orb_featvec, orb_frame, orb_mappoints, ptr)
 
 FRAME_GRID_COLS, FRAME_GRID_ROWS = 64, 48   # Frame.h:37-38
 
@@ -171,6 +171,26 @@ class Frame:
         return f
 
 
+class FeatureVector:
+    """DBoW2::FeatureVector (map<NodeId, vector<unsigned>>) as CSR; built from per-feature node ids."""
+
+    def __init__(self, node_of_feature):
+        node = np.asarray(node_of_feature, np.int64)
+        order = np.argsort(node, kind="stable")              # feature index order kept inside a node
+        ids, counts = np.unique(node[order], return_counts=True)
+        self.node_id = np.ascontiguousarray(ids, np.uint32)
+        self.start = np.ascontiguousarray(np.concatenate([[0], np.cumsum(counts)]), np.int32)
+        self.feat = np.ascontiguousarray(order, np.int32)
+
+    def cstruct(self):
+        v = orb_featvec()
+        v.n_nodes = len(self.node_id)
+        v.node_id = self.node_id.ctypes.data
+        v.start = self.start.ctypes.data
+        v.feat = self.feat.ctypes.data
+        return v
+
+
 class MapPoints:
     def __init__(self, pos, desc, observations):
         self.pos = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
@@ -276,6 +296,81 @@ class ORBmatcher:
                                                             arr(uR), arr(dep), ptr(n)),
               "ORBmatcher_ComputeStereoMatches_batch")
         return [u[:len(k)] for u, k in zip(uR, kL)], [d[:len(k)] for d, k in zip(dep, kL)], n
+
+    def SearchByProjection_KeyFrame(self, F: Frame, cur_mp, kf_mp, skip, kf_angle, mps: MapPoints, max_dist,
+                                    min_dist, logScaleFactor, th, ORBdist):
+        """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (ORBmatcher.cc:1472).
+        cur_mp is updated in place; returns nmatches."""
+        assert cur_mp.dtype == np.int32 and cur_mp.flags.c_contiguous and len(cur_mp) == F.N
+        kf_mp = np.ascontiguousarray(kf_mp, np.int32)
+        skip = np.ascontiguousarray(skip, np.uint8)
+        kf_angle = np.ascontiguousarray(kf_angle, np.float32)
+        mx = np.ascontiguousarray(max_dist, np.float32)
+        mn = np.ascontiguousarray(min_dist, np.float32)
+        f, m, n = F.cstruct(), mps.cstruct(), C.c_int()
+        check(self._L.ORBmatcher_SearchByProjection_KeyFrame(self._h, C.byref(f), ptr(cur_mp), len(kf_mp), ptr(kf_mp),
+                                                             ptr(skip), ptr(kf_angle), C.byref(m), ptr(mx), ptr(mn),
+                                                             float(logScaleFactor), float(th), int(ORBdist),
+                                                             C.byref(n)), "SearchByProjection_KeyFrame")
+        return n.value
+
+    def SearchForInitialization(self, F1: Frame, F2: Frame, prev_matched, windowSize=10):
+        """SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) (ORBmatcher.cc:405).
+        prev_matched (N1 x 2 float32) is updated in place; returns (nmatches, vnMatches12)."""
+        assert prev_matched.dtype == np.float32 and prev_matched.flags.c_contiguous
+        m12 = np.full(max(F1.N, 1), -1, np.int32)
+        f1, f2, n = F1.cstruct(), F2.cstruct(), C.c_int()
+        check(self._L.ORBmatcher_SearchForInitialization(self._h, C.byref(f1), C.byref(f2), ptr(prev_matched),
+                                                         ptr(m12), int(windowSize), C.byref(n)),
+              "SearchForInitialization")
+        return n.value, m12[:F1.N]
+
+    def SearchByBoW_Frame(self, kf_desc, kf_angle, kf_mp, kf_mp_bad, fvKF: FeatureVector, f_desc, f_angle,
+                          fvF: FeatureVector):
+        """SearchByBoW(pKF, F, vpMapPointMatches) (ORBmatcher.cc:159) -> (nmatches, matches[NF])."""
+        kd = np.ascontiguousarray(kf_desc, np.uint8).reshape(-1, 32)
+        fd = np.ascontiguousarray(f_desc, np.uint8).reshape(-1, 32)
+        ka = np.ascontiguousarray(kf_angle, np.float32)
+        fa = np.ascontiguousarray(f_angle, np.float32)
+        km = np.ascontiguousarray(kf_mp, np.int32)
+        kb = np.ascontiguousarray(kf_mp_bad, np.uint8)
+        out = np.full(max(len(fd), 1), -1, np.int32)
+        v1, v2, n = fvKF.cstruct(), fvF.cstruct(), C.c_int()
+        check(self._L.ORBmatcher_SearchByBoW_Frame(self._h, len(kd), ptr(kd), ptr(ka), ptr(km), ptr(kb), C.byref(v1),
+                                                   len(fd), ptr(fd), ptr(fa), C.byref(v2), ptr(out), C.byref(n)),
+              "SearchByBoW_Frame")
+        return n.value, out[:len(fd)]
+
+    def SearchByBoW_KeyFrames(self, desc1, angle1, mp1, bad1, fv1: FeatureVector, desc2, angle2, mp2, bad2,
+                              fv2: FeatureVector):
+        """SearchByBoW(pKF1, pKF2, vpMatches12) (ORBmatcher.cc:522) -> (nmatches, matches12[n1])."""
+        d1 = np.ascontiguousarray(desc1, np.uint8).reshape(-1, 32)
+        d2 = np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32)
+        a1, a2 = np.ascontiguousarray(angle1, np.float32), np.ascontiguousarray(angle2, np.float32)
+        m1, m2 = np.ascontiguousarray(mp1, np.int32), np.ascontiguousarray(mp2, np.int32)
+        b1, b2 = np.ascontiguousarray(bad1, np.uint8), np.ascontiguousarray(bad2, np.uint8)
+        out = np.full(max(len(d1), 1), -1, np.int32)
+        v1, v2, n = fv1.cstruct(), fv2.cstruct(), C.c_int()
+        check(self._L.ORBmatcher_SearchByBoW_KeyFrames(self._h, len(d1), ptr(d1), ptr(a1), ptr(m1), ptr(b1),
+                                                       C.byref(v1), len(d2), ptr(d2), ptr(a2), ptr(m2), ptr(b2),
+                                                       C.byref(v2), ptr(out), C.byref(n)), "SearchByBoW_KeyFrames")
+        return n.value, out[:len(d1)]
+
+    def SearchForTriangulation(self, KF1: Frame, has_mp1, fv1: FeatureVector, KF2: Frame, has_mp2,
+                               fv2: FeatureVector, levelSigma2_2, F12, bOnlyStereo=False):
+        """SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo) (ORBmatcher.cc:657)
+        -> array (n, 2) of (idx1, idx2)."""
+        h1 = np.ascontiguousarray(has_mp1, np.uint8)
+        h2 = np.ascontiguousarray(has_mp2, np.uint8)
+        s2 = np.ascontiguousarray(levelSigma2_2, np.float32)
+        F = np.ascontiguousarray(F12, np.float32).reshape(3, 3)
+        cap = max(KF1.N, 1)
+        pairs = np.zeros((cap, 2), np.int32)
+        k1, k2, v1, v2, n = KF1.cstruct(), KF2.cstruct(), fv1.cstruct(), fv2.cstruct(), C.c_int()
+        check(self._L.ORBmatcher_SearchForTriangulation(self._h, C.byref(k1), ptr(h1), C.byref(v1), C.byref(k2),
+                                                        ptr(h2), C.byref(v2), ptr(s2), ptr(F), int(bool(bOnlyStereo)),
+                                                        ptr(pairs), cap, C.byref(n)), "SearchForTriangulation")
+        return pairs[:n.value].copy()
 
     def SearchCandidates(self, qdesc, tdesc, offsets, cand):
         q = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)

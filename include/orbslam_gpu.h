@@ -188,6 +188,67 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
                                           float mbf, float mb, float* const* uRight,
                                           float* const* depth, int* nmatches);
 
+/* DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned>>) as CSR: strictly ascending
+ * node ids, the feature indices of node a at feat[start[a] .. start[a+1]) in insertion order.
+ * (Computed by the caller's vocabulary; ORBvoc.txt is not shipped with the reference.) */
+typedef struct orb_featvec {
+    int n_nodes;
+    const uint32_t* node_id;
+    const int32_t* start;
+    const int32_t* feat;
+} orb_featvec;
+
+/* The searches below take host arrays only (ORBmatcher_set_device_pointers(h, 0)).  The
+ * device enumerates every window / vocabulary-node candidate with its Hamming distance; the
+ * order-dependent selection is replayed on the host, in the reference's order. */
+
+/* int SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set<MapPoint*>& sAlreadyFound,
+ *                        const float th, const int ORBdist)          ORBmatcher.cc:1472-1599
+ * F: CurrentFrame (grid over keysUn, Tcw = mTcw); cur_mp in/out (mvpMapPoints as indices).
+ * n = pKF->GetMapPointMatches().size(); kf_mp[i]: map point index or -1; skip[i] = isBad() ||
+ * sAlreadyFound.count(pMP); kf_angle[i] = pKF->mvKeysUn[i].angle.  mp_max_dist / mp_min_dist:
+ * MapPoint::mfMaxDistance / mfMinDistance; logScaleFactor = CurrentFrame.mfLogScaleFactor. */
+int ORBmatcher_SearchByProjection_KeyFrame(ORBmatcher_h h, const orb_frame* F, int32_t* cur_mp, int n,
+                                           const int32_t* kf_mp, const uint8_t* skip,
+                                           const float* kf_angle, const orb_mappoints* mps,
+                                           const float* mp_max_dist, const float* mp_min_dist,
+                                           float logScaleFactor, float th, int ORBdist, int* nmatches);
+
+/* int SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f>& vbPrevMatched,
+ *                             vector<int>& vnMatches12, int windowSize)  ORBmatcher.cc:405-520
+ * prev_matched: F1.N x 2 (in/out); matches12: F1.N (out). */
+int ORBmatcher_SearchForInitialization(ORBmatcher_h h, const orb_frame* F1, const orb_frame* F2,
+                                       float* prev_matched, int32_t* matches12, int windowSize,
+                                       int* nmatches);
+
+/* int SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)  ORBmatcher.cc:159-288
+ * kf_mp[i]: pKF->GetMapPointMatches()[i] index or -1, kf_mp_bad[i]: isBad(); kf_angle =
+ * pKF->mvKeysUn angles, f_angle = F.mvKeys angles; matches[NF] (out): vpMapPointMatches. */
+int ORBmatcher_SearchByBoW_Frame(ORBmatcher_h h, int nKF, const uint8_t* kf_desc, const float* kf_angle,
+                                 const int32_t* kf_mp, const uint8_t* kf_mp_bad, const orb_featvec* fvKF,
+                                 int NF, const uint8_t* f_desc, const float* f_angle,
+                                 const orb_featvec* fvF, int32_t* matches, int* nmatches);
+
+/* int SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)  ORBmatcher.cc:522-655
+ * matches12[n1] (out): the map point of KF2 matched to feature i of KF1, or -1. */
+int ORBmatcher_SearchByBoW_KeyFrames(ORBmatcher_h h, int n1, const uint8_t* desc1, const float* angle1,
+                                     const int32_t* mp1, const uint8_t* bad1, const orb_featvec* fv1,
+                                     int n2, const uint8_t* desc2, const float* angle2,
+                                     const int32_t* mp2, const uint8_t* bad2, const orb_featvec* fv2,
+                                     int32_t* matches12, int* nmatches);
+
+/* int SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, cv::Mat F12,
+ *                            vector<pair<size_t,size_t>>& vMatchedPairs, const bool bOnlyStereo)
+ *                                                                    ORBmatcher.cc:657-823
+ * KF1/KF2: keysUn, desc, uRight (mvuRight, NULL = all monocular), Tcw, intrinsics, scaleFactors;
+ * has_mp[i] = GetMapPoint(i) != NULL; levelSigma2_2 = pKF2->mvLevelSigma2; F12 3x3 row-major.
+ * pairs: cap x 2 (idx1, idx2) in idx1 order; *npairs = count (ORB_E_CAPACITY if > cap). */
+int ORBmatcher_SearchForTriangulation(ORBmatcher_h h, const orb_frame* KF1, const uint8_t* has_mp1,
+                                      const orb_featvec* fv1, const orb_frame* KF2,
+                                      const uint8_t* has_mp2, const orb_featvec* fv2,
+                                      const float* levelSigma2_2, const float* F12, int bOnlyStereo,
+                                      int32_t* pairs, int cap, int* npairs);
+
 /* Hamming distances for CSR candidate lists (the inner loop of every Search*):
  * query q (descriptor qdesc[q]) against train rows cand[off[q] .. off[q+1]).
  * Writes dist[k] for every candidate k and best/second per query

@@ -177,6 +177,44 @@ void  ora_sim3_estimate(const ora_sim3* S, float* R, float* t, float* s);
 int   ora_sim3_iterations(const ora_sim3* S);
 
 
+/* ---- remaining ORBmatcher searches (matchers2.c) ------------------------------
+ * DBoW2::FeatureVector as CSR: ascending node ids, the feature indices of each node. */
+typedef struct {
+    int n_nodes;
+    const uint32_t* node_id;
+    const int32_t* start;      /* n_nodes + 1 */
+    const int32_t* feat;
+} ora_featvec;
+/* SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist), ORBmatcher.cc:1472-1599.
+ * F grid over mvKeysUn (ora_frame_build_grid); Tcw = CurrentFrame.mTcw; K = {fx,fy,cx,cy}; curMP in/out.
+ * KF map points i < n: kfMP[i] (-1 = NULL), skip[i] (isBad || in sAlreadyFound), kfAngle[i].
+ * mpMaxDist/mpMinDist: mfMaxDistance / mfMinDistance per map point. */
+int   ora_search_by_projection_kf(const ora_frame* F, const float* Tcw, const float* K, int* curMP, int n, const int* kfMP,
+                                  const uint8_t* skip, const float* kfAngle, const float* mpPos,
+                                  const uint8_t* mpDesc, const float* mpMaxDist, const float* mpMinDist,
+                                  float logScaleFactor, float th, int ORBdist, int checkOri);
+/* SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches), ORBmatcher.cc:159-288: matchesF[i] = map point or -1 */
+int   ora_search_by_bow_frame(const ora_featvec* fvKF, const int* kfMP, const uint8_t* kfMPbad,
+                              const uint8_t* kfDesc, const float* kfAngle, int nKF, const ora_featvec* fvF,
+                              const uint8_t* fDesc, const float* fAngle, int NF, float nnratio, int checkOri,
+                              int* matchesF);
+/* SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12), ORBmatcher.cc:522-655: matches12[i] = map point or -1 */
+int   ora_search_by_bow_kf(const ora_featvec* fv1, const int* mp1, const uint8_t* bad1, const uint8_t* desc1,
+                           const float* ang1, int n1, const ora_featvec* fv2, const int* mp2, const uint8_t* bad2,
+                           const uint8_t* desc2, const float* ang2, int n2, float nnratio, int checkOri,
+                           int* matches12);
+/* SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize), ORBmatcher.cc:405-520 */
+int   ora_search_for_initialization(const ora_frame* F1, const ora_frame* F2, float* prevMatched, int* matches12,
+                                    int windowSize, float nnratio, int checkOri);
+/* SearchForTriangulation(KF1, KF2, F12, vMatchedPairs, bOnlyStereo), ORBmatcher.cc:657-823.
+ * K2 = {fx, fy, cx, cy} of KF2; writes min(cap, n) pairs (idx1, idx2) in idx1 order, returns n. */
+int   ora_search_for_triangulation(const ora_featvec* fv1, const ora_kp* k1, const uint8_t* d1, const float* uR1,
+                                   const uint8_t* hasMP1, int n1, const float* Tcw1, const ora_featvec* fv2,
+                                   const ora_kp* k2, const uint8_t* d2, const float* uR2, const uint8_t* hasMP2,
+                                   int n2, const float* Tcw2, const float* K2, const float* scale2,
+                                   const float* sigma2_2, const float* F12, int bOnlyStereo, int checkOri,
+                                   int* pairs, int cap);
+
 /* ---- Frame::ComputeStereoMatches (stereo.c), reference Frame.cc:466-640 ----------
  * kL/dL: left mvKeys + descriptors (NL), kR/dR: right (NR); exL/exR: the extractors that
  * produced them (their last pyramids); rows0 = level-0 rows.  Writes mvuRight / mvDepth

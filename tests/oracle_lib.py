@@ -382,3 +382,99 @@ def _oracle_ba(pr, stop, glob):
                 n_erased=R.n_erased, aborted=bool(R.aborted),
                 solve_chi2=np.array(tr.solve_chi2[:tr.n_solves]), solve_ini_chi2=np.array(tr.solve_ini_chi2[:tr.n_solves]),
                 trial_chi2=np.array(tr.trial_chi2[:tr.n_trials]), trial_lambda=np.array(tr.trial_lambda[:tr.n_trials]))
+
+
+# ---------------------------------------------------------------- remaining ORBmatcher searches
+class ora_featvec(C.Structure):
+    _fields_ = [("n_nodes", C.c_int), ("node_id", C.c_void_p), ("start", C.c_void_p), ("feat", C.c_void_p)]
+
+
+def _fv(fv):
+    v = ora_featvec()
+    v.n_nodes = len(fv.node_id)
+    v.node_id, v.start, v.feat = fv.node_id.ctypes.data, fv.start.ctypes.data, fv.feat.ctypes.data
+    return v
+
+
+def _u8(a):
+    return np.ascontiguousarray(a, np.uint8)
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, np.float32)
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, np.int32)
+
+
+def oracle_search_by_projection_kf(F, cur_mp, kf_mp, skip, kf_angle, mps, max_dist, min_dist, logScaleFactor, th,
+                                   ORBdist, checkOri=True):
+    L = lib()
+    vp, i32, f32 = C.c_void_p, C.c_int, C.c_float
+    L.ora_search_by_projection_kf.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, f32, f32, i32, i32]
+    of = OracleFrame(F)
+    K = np.array([F.fx, F.fy, F.cx, F.cy], np.float32)
+    kf_mp, skip, kf_angle, mx, mn = _i32(kf_mp), _u8(skip), _f32(kf_angle), _f32(max_dist), _f32(min_dist)
+    return L.ora_search_by_projection_kf(C.byref(of.s), F.Tcw.ctypes.data, ptr(K), ptr(cur_mp), len(kf_mp), ptr(kf_mp),
+                                         ptr(skip), ptr(kf_angle), ptr(mps.pos), ptr(mps.desc), ptr(mx), ptr(mn),
+                                         float(logScaleFactor), float(th), int(ORBdist), int(bool(checkOri)))
+
+
+def oracle_search_for_initialization(F1, F2, prev_matched, windowSize, nnratio=0.9, checkOri=True):
+    L = lib()
+    vp = C.c_void_p
+    L.ora_search_for_initialization.argtypes = [vp, vp, vp, vp, C.c_int, C.c_float, C.c_int]
+    o1, o2 = OracleFrame(F1), OracleFrame(F2)
+    m12 = np.full(max(F1.N, 1), -1, np.int32)
+    n = L.ora_search_for_initialization(C.byref(o1.s), C.byref(o2.s), ptr(prev_matched), ptr(m12), int(windowSize),
+                                        float(nnratio), int(bool(checkOri)))
+    return n, m12[:F1.N]
+
+
+def oracle_search_by_bow_frame(kf_desc, kf_angle, kf_mp, kf_mp_bad, fvKF, f_desc, f_angle, fvF, nnratio,
+                               checkOri=True):
+    L = lib()
+    vp, i32 = C.c_void_p, C.c_int
+    L.ora_search_by_bow_frame.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp, i32, C.c_float, i32, vp]
+    kd, fd = _u8(kf_desc).reshape(-1, 32), _u8(f_desc).reshape(-1, 32)
+    out = np.full(max(len(fd), 1), -1, np.int32)
+    v1, v2 = _fv(fvKF), _fv(fvF)
+    km, kb, ka, fa = _i32(kf_mp), _u8(kf_mp_bad), _f32(kf_angle), _f32(f_angle)
+    n = L.ora_search_by_bow_frame(C.byref(v1), ptr(km), ptr(kb), ptr(kd), ptr(ka), len(kd), C.byref(v2), ptr(fd),
+                                  ptr(fa), len(fd), float(nnratio), int(bool(checkOri)), ptr(out))
+    return n, out[:len(fd)]
+
+
+def oracle_search_by_bow_kf(desc1, angle1, mp1, bad1, fv1, desc2, angle2, mp2, bad2, fv2, nnratio, checkOri=True):
+    L = lib()
+    vp, i32 = C.c_void_p, C.c_int
+    L.ora_search_by_bow_kf.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, i32, C.c_float, i32, vp]
+    d1, d2 = _u8(desc1).reshape(-1, 32), _u8(desc2).reshape(-1, 32)
+    out = np.full(max(len(d1), 1), -1, np.int32)
+    a1, a2, m1, m2, b1, b2 = _f32(angle1), _f32(angle2), _i32(mp1), _i32(mp2), _u8(bad1), _u8(bad2)
+    v1, v2 = _fv(fv1), _fv(fv2)
+    n = L.ora_search_by_bow_kf(C.byref(v1), ptr(m1), ptr(b1), ptr(d1), ptr(a1), len(d1), C.byref(v2), ptr(m2),
+                               ptr(b2), ptr(d2), ptr(a2), len(d2), float(nnratio), int(bool(checkOri)), ptr(out))
+    return n, out[:len(d1)]
+
+
+def oracle_search_for_triangulation(KF1, has_mp1, fv1, KF2, has_mp2, fv2, levelSigma2_2, F12, bOnlyStereo,
+                                    checkOri=True):
+    L = lib()
+    vp, i32 = C.c_void_p, C.c_int
+    L.ora_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp,
+                                               vp, i32, i32, vp, i32]
+    uR1 = KF1.uRight if KF1.uRight is not None else np.full(KF1.N, -1, np.float32)
+    uR2 = KF2.uRight if KF2.uRight is not None else np.full(KF2.N, -1, np.float32)
+    h1, h2 = _u8(has_mp1), _u8(has_mp2)
+    K2 = np.array([KF2.fx, KF2.fy, KF2.cx, KF2.cy], np.float32)
+    s2, F = _f32(levelSigma2_2), _f32(F12).reshape(3, 3)
+    pairs = np.zeros((max(KF1.N, 1), 2), np.int32)
+    v1, v2 = _fv(fv1), _fv(fv2)
+    n = L.ora_search_for_triangulation(C.byref(v1), ptr(KF1.keysUn), ptr(KF1.desc), ptr(_f32(uR1)), ptr(h1), KF1.N,
+                                       KF1.Tcw.ctypes.data, C.byref(v2), ptr(KF2.keysUn), ptr(KF2.desc),
+                                       ptr(_f32(uR2)), ptr(h2), KF2.N, KF2.Tcw.ctypes.data, ptr(K2), ptr(KF2.scale),
+                                       ptr(s2), ptr(F), int(bool(bOnlyStereo)), int(bool(checkOri)), ptr(pairs),
+                                       len(pairs))
+    return pairs[:n].copy()

@@ -283,3 +283,30 @@ def test_oracle_stereo_recovers_disparity():
     near_int = np.abs(d - np.round(d)) < 0.75
     assert near_int.mean() > 0.8 and (np.round(d) <= 65).mean() > 0.9
     np.testing.assert_allclose(dep[ok], mbf / d, rtol=1e-5)
+
+
+def test_oracle_searches_run_and_agree_with_geometry():
+    """CPU sanity of the restated searches (oracle/matchers2.c): relocalization projection matches
+    land on the keypoint the map point came from (frames related by a known rotation), and the
+    BoW / initialization searches return consistent one-to-one assignments."""
+    import search_cases as sc
+    c = sc.reloc_case(0)
+    cur = c["cur_mp"].copy()
+    n = oracle_lib.oracle_search_by_projection_kf(c["F"], cur, c["kf_mp"], c["skip"], c["kf_angle"], c["mps"],
+                                                  c["max_dist"], c["min_dist"], c["logScaleFactor"], 10, 100)
+    assert n > 100
+    new = (cur >= 0) & (c["cur_mp"] < 0)
+    assert new.sum() == n
+    (k0, d0), (k1, d1) = sc.frames(0)[0]
+    t = sc.frames(0)[3]
+    F1 = sc.make_frame(k0, d0, t, np.eye(4, dtype=np.float32))
+    F2 = sc.make_frame(k1, d1, t, np.eye(4, dtype=np.float32))
+    prev = np.ascontiguousarray(np.stack([k0["x"], k0["y"]], 1), np.float32)
+    n, m12 = oracle_lib.oracle_search_for_initialization(F1, F2, prev, 100)
+    got = m12[m12 >= 0]
+    assert n == len(got) and len(np.unique(got)) == len(got) and n > 50
+    mp = np.arange(len(k0), dtype=np.int32)
+    n, out = oracle_lib.oracle_search_by_bow_frame(d0, k0["angle"], mp, np.zeros(len(k0), np.uint8), sc.featvec(d0),
+                                                   d1, k1["angle"], sc.featvec(d1), 0.7)
+    got = out[out >= 0]
+    assert n == len(got) and len(np.unique(got)) == len(got) and n > 50
