@@ -128,6 +128,8 @@ def lib():
     L.orbgpu_comm_destroy.argtypes = [vp]
     L.Optimizer_last_trace.argtypes = [vp, vp, i32, P(i32), vp, vp, i32, P(i32)]
     L.Optimizer_last_timings.argtypes = [vp]
+    L.Optimizer_PoseOptimization.argtypes = [P(pose_problem), vp, vp, P(i32)]
+    L.Optimizer_PoseOptimization_batch.argtypes = [i32, vp, vp, vp, vp]
     L.orbgpu_unit_ldlt_solve.argtypes = [i32, vp, vp, vp, i32, P(i32)]
     L.orbgpu_unit_csum.argtypes = [vp, i32, vp]
     L.orbgpu_unit_ldlt_factor.argtypes = [i32, vp, vp]
@@ -160,6 +162,12 @@ class ba_problem(C.Structure):
                 ("kf_cam", C.c_void_p), ("n_pt", C.c_int), ("pt_id", C.c_void_p), ("pt_pos", C.c_void_p),
                 ("n_edge", C.c_int), ("edge_pt", C.c_void_p), ("edge_kf", C.c_void_p), ("edge_obs", C.c_void_p),
                 ("edge_inv_sigma2", C.c_void_p)]
+
+
+class pose_problem(C.Structure):
+    _fields_ = [("N", C.c_int), ("Tcw", C.c_void_p), ("has_mp", C.c_void_p), ("Xw", C.c_void_p),
+                ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float)]
 
 
 class ba_result(C.Structure):

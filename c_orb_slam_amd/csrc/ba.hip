@@ -1176,6 +1176,387 @@ __global__ void __launch_bounds__(256) k_tile_unpack(int n, double* __restrict__
     }
 }
 
+// ---------------------------------------------------------------- PoseOptimization
+// Optimizer::PoseOptimization (Optimizer.cc:239-451): one SE3 vertex with unary
+// EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose edges
+// (types_six_dof_expmap.cpp:266-364), solved by LinearSolverDense (Eigen LDLT with diagonal
+// pivoting).  The whole call -- 4 rounds of optimize(10), each restarted from mTcw, with the
+// outlier classification after every round -- is ONE persistent workgroup per frame (a batch
+// of frames is one launch): the per-iteration work (errors, Jacobians, 6x6 system) is spread
+// over 1024 threads with the canonical 64-tree sums of oracle/ba.c, the 6x6 pivoted LDL^T,
+// the SE3 update and the LM control run on thread 0 between barriers.
+struct PoseEdgeDev {
+    double Xw[3], obs[3];
+    double info, delta, dsqr;
+    int stereo, kp;
+};
+
+struct PoseProbDev {
+    int ne, e0;            // edges E[e0 .. e0+ne)
+    int nbad, pad;         // out: nBad of the last round (-1: < 3 correspondences)
+    Se3 T0;                // Converter::toSE3Quat(pFrame->mTcw)
+    Se3 T;                 // out
+    double fx, fy, cx, cy, bf;
+};
+
+__device__ __forceinline__ void pose_err(const PoseEdgeDev& e, const Se3& T, const PoseProbDev& P, double* err) {
+    double p[3];
+    se3_map(T, e.Xw, p);
+    if (!e.stereo) {
+        const double px = p[0] / p[2], py = p[1] / p[2];
+        err[0] = e.obs[0] - (px * P.fx + P.cx);
+        err[1] = e.obs[1] - (py * P.fy + P.cy);
+        err[2] = 0;
+    } else {
+        const float invz = (float)(1.0 / p[2]);
+        const double u = (p[0] * (double)invz) * P.fx + P.cx;
+        const double v = (p[1] * (double)invz) * P.fy + P.cy;
+        err[0] = e.obs[0] - u;
+        err[1] = e.obs[1] - v;
+        err[2] = e.obs[2] - (u - P.bf * (double)invz);
+    }
+}
+
+__device__ __forceinline__ double pose_chi2(const PoseEdgeDev& e, const double* err) {
+    double s = 0;
+    const int D = e.stereo ? 3 : 2;
+    for (int j = 0; j < D; j++) s += err[j] * (e.info * err[j]);
+    return s;
+}
+
+__device__ __forceinline__ double pose_rho0(const PoseEdgeDev& e, double c, bool robust) {
+    if (!robust || c <= e.dsqr) return c;
+    const double sq = sqrt(c);
+    return (2 * sq) * e.delta - e.dsqr;
+}
+
+// Eigen::LDLT<MatrixXd> compute + solve (diagonal pivoting, sequential dot products),
+// identical operation sequence to oracle ora_ldlt_pivot_solve.  H is destroyed.
+// H, tmp, y, tr live in LDS (dynamic indexing stays out of scratch).
+__device__ bool ldlt_pivot6(double* H, const double* b, double* x, double* tmp, double* y, int* tr) {
+    constexpr int n = 6;
+    int sign = 0;
+#define M(i, j) H[(i) * n + (j)]
+    for (int k = 0; k < n; k++) {
+        int idx = k;
+        double big = fabs(M(k, k));
+        for (int i = k + 1; i < n; i++)
+            if (fabs(M(i, i)) > big) {
+                big = fabs(M(i, i));
+                idx = i;
+            }
+        tr[k] = idx;
+        if (idx != k) {
+            for (int j = 0; j < k; j++) { const double t = M(k, j); M(k, j) = M(idx, j); M(idx, j) = t; }
+            for (int i = idx + 1; i < n; i++) { const double t = M(i, k); M(i, k) = M(i, idx); M(i, idx) = t; }
+            { const double t = M(k, k); M(k, k) = M(idx, idx); M(idx, idx) = t; }
+            for (int i = k + 1; i < idx; i++) { const double t = M(i, k); M(i, k) = M(idx, i); M(idx, i) = t; }
+        }
+        if (k > 0) {
+            for (int j = 0; j < k; j++) tmp[j] = M(j, j) * M(k, j);
+            double s = 0;
+            for (int j = 0; j < k; j++) s += M(k, j) * tmp[j];
+            M(k, k) -= s;
+            for (int i = k + 1; i < n; i++) {
+                double t = 0;
+                for (int j = 0; j < k; j++) t += M(i, j) * tmp[j];
+                M(i, k) -= t;
+            }
+        }
+        const double akk = M(k, k);
+        const bool valid = fabs(akk) > 0.0;
+        if (k == 0 && !valid) {
+            for (int j = k; j < n; j++) tr[j] = j;
+            sign = 0;
+            break;
+        }
+        if (valid)
+            for (int i = k + 1; i < n; i++) M(i, k) /= akk;
+        if (sign == 1) { if (akk < 0) sign = 3; }
+        else if (sign == 2) { if (akk > 0) sign = 3; }
+        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+    }
+    if (!(sign == 1 || sign == 0)) return false;
+    for (int i = 0; i < n; i++) y[i] = b[i];
+    for (int k = 0; k < n; k++) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < i; j++) y[i] -= M(i, j) * y[j];
+    for (int i = 0; i < n; i++) y[i] = fabs(M(i, i)) > DBL_MIN ? y[i] / M(i, i) : 0.0;
+    for (int i = n - 1; i >= 0; i--)
+        for (int j = n - 1; j > i; j--) y[i] -= M(j, i) * y[j];
+    for (int k = n - 1; k >= 0; k--) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+    for (int i = 0; i < n; i++) x[i] = y[i];
+#undef M
+    return true;
+}
+
+constexpr int kPoseMaxEdges = 4096;
+constexpr int kPoseThreads = 512;   // 256 VGPRs per lane for the 27-term system build
+constexpr int kPosePer = kPoseMaxEdges / kPoseThreads;
+
+// Block-wide canonical sum (ora_csum) of K per-active-edge values f(a, out[K]), a < nA:
+// 64-edge chunk trees per wave, then one thread per entry over the chunk sums.
+template <int K, class F>
+__device__ __forceinline__ void block_csum(F f, int nA, double (*cs)[64], double* res) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const int m = (nA + 63) >> 6;
+    for (int c = w; c < m; c += nw) {
+        const int a = c * 64 + lane;
+        double v[K];
+        if (a < nA) f(a, v);
+        else
+#pragma unroll
+            for (int q = 0; q < K; q++) v[q] = 0.0;
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            const double t = nA == 1 ? v[q] : wave_tree(v[q]);   // ora_csum keeps a single term untouched
+            if (lane == 0) cs[q][c] = t;
+        }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < K) res[threadIdx.x] = nA > 0 ? local_csum_inplace(cs[threadIdx.x], m) : 0.0;
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, const PoseEdgeDev* __restrict__ Eall,
+                                                   double* errAll, uint8_t* outlAll) {
+    PoseProbDev& P = probs[blockIdx.x];
+    const int ne = P.ne;
+    const PoseEdgeDev* E = Eall + P.e0;
+    double* err = errAll + 3 * (size_t)P.e0;
+    uint8_t* outl = outlAll + P.e0;
+    __shared__ uint8_t level[kPoseMaxEdges], robust[kPoseMaxEdges];
+    __shared__ int aE[kPoseMaxEdges];
+    __shared__ double cs[27][64];
+    __shared__ double red[32];
+    __shared__ Se3 T, Tbak;
+    __shared__ double xs[6], Hs[21], bs[6], Hd[36], xn[6], lt[12];
+    __shared__ int ltr[6];
+    __shared__ double lambda, ni, currentChi, iniChi;
+    __shared__ int nA, nBadLM, qmax, again, term, nBad, okS, wsum[16];
+    const int tid = threadIdx.x;
+    if (ne < 3) {
+        if (tid == 0) {
+            P.T = P.T0;
+            P.nbad = -1;
+        }
+        return;
+    }
+    for (int i = tid; i < ne; i += blockDim.x) {
+        level[i] = 0;
+        robust[i] = 1;
+        outl[i] = 0;
+    }
+    __syncthreads();
+    const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
+    for (int it = 0; it < 4; it++) {
+        if (tid == 0) {
+            T = P.T0;   // vSE3->setEstimate(Converter::toSE3Quat(pFrame->mTcw)) every round
+            for (int j = 0; j < 6; j++) xs[j] = 0.0;
+        }
+        // active edges (level 0) in edge order: block prefix over kPosePer edges per thread
+        {
+            const int base = tid * kPosePer;
+            int c = 0;
+            for (int j = 0; j < kPosePer; j++) c += (base + j < ne && level[base + j] == 0) ? 1 : 0;
+            int incl = c;   // inclusive scan within the wave
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o, 64);
+                if ((tid & 63) >= o) incl += t;
+            }
+            if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+            __syncthreads();
+            int off = 0;
+            for (int w = 0; w < (tid >> 6); w++) off += wsum[w];
+            int pos = off + incl - c;
+            for (int j = 0; j < kPosePer; j++)
+                if (base + j < ne && level[base + j] == 0) aE[pos++] = base + j;
+            if (tid == blockDim.x - 1) nA = off + incl;
+            __syncthreads();
+        }
+        const int na = nA;
+        if (na > 0) {   // optimize(10); without active edges the vertex is not optimised at all
+            for (int k = 0; k < 10; k++) {
+                // computeActiveErrors + activeRobustChi2
+                block_csum<1>([&](int a, double* v) {
+                    const int i = aE[a];
+                    double e3[3];
+                    pose_err(E[i], T, P, e3);
+                    for (int j = 0; j < 3; j++) err[3 * i + j] = e3[j];
+                    v[0] = pose_rho0(E[i], pose_chi2(E[i], e3), robust[i]);
+                }, na, cs, red);
+                if (tid == 0) currentChi = iniChi = red[0];
+                // buildSystem: J^T W J and -J^T W e per active edge, canonical sums
+                block_csum<27>([&](int a, double* v) {
+                    const int i = aE[a];
+                    const PoseEdgeDev e = E[i];
+                    const double e3[3] = {err[3 * i], err[3 * i + 1], err[3 * i + 2]};
+                    double p[3];
+                    se3_map(T, e.Xw, p);
+                    const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
+                    double J[18];
+                    J[0] = ((x * y) * invz_2) * P.fx;
+                    J[1] = (-(1 + ((x * x) * invz_2))) * P.fx;
+                    J[2] = (y * invz) * P.fx;
+                    J[3] = (-invz) * P.fx;
+                    J[4] = 0;
+                    J[5] = (x * invz_2) * P.fx;
+                    J[6] = (1 + ((y * y) * invz_2)) * P.fy;
+                    J[7] = (((-x) * y) * invz_2) * P.fy;
+                    J[8] = ((-x) * invz) * P.fy;
+                    J[9] = 0;
+                    J[10] = (-invz) * P.fy;
+                    J[11] = (y * invz_2) * P.fy;
+                    J[12] = J[0] - ((P.bf * y) * invz_2);
+                    J[13] = J[1] + ((P.bf * x) * invz_2);
+                    J[14] = J[2];
+                    J[15] = J[3];
+                    J[16] = 0;
+                    J[17] = J[5] - (P.bf * invz_2);
+                    const int D = e.stereo ? 3 : 2;
+                    const double c = pose_chi2(e, e3);
+                    const bool rb = robust[i];
+                    double r1 = 1.;
+                    if (rb && !(c <= e.dsqr)) r1 = e.delta / sqrt(c);
+                    const double wgt = rb ? r1 * e.info : e.info;
+                    double omr[3] = {0, 0, 0};
+#pragma unroll
+                    for (int kk = 0; kk < 3; kk++)
+                        if (kk < D) {
+                            omr[kk] = -(e.info * e3[kk]);
+                            if (rb) omr[kk] *= r1;
+                        }
+#pragma unroll
+                    for (int r = 0; r < 6; r++) {
+                        double sb = 0;
+#pragma unroll
+                        for (int kk = 0; kk < 3; kk++)
+                            if (kk < D) sb += J[kk * 6 + r] * omr[kk];
+                        v[21 + r] = sb;
+#pragma unroll
+                        for (int cc = r; cc < 6; cc++) {
+                            double hh = 0;
+#pragma unroll
+                            for (int kk = 0; kk < 3; kk++)
+                                if (kk < D) hh += (J[kk * 6 + r] * wgt) * J[kk * 6 + cc];
+                            v[r * 6 - (r * (r - 1)) / 2 + (cc - r)] = hh;
+                        }
+                    }
+                }, na, cs, red);
+                if (tid < 27) {
+                    if (tid < 21) Hs[tid] = red[tid];
+                    else bs[tid - 21] = red[tid];
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    if (k == 0) {   // computeLambdaInit over the pose diagonal
+                        double mx = 0.;
+                        for (int j = 0; j < 6; j++) mx = fmax(fabs(Hs[DIAG21[j]]), mx);
+                        lambda = 1e-5 * mx;
+                        ni = 2;
+                        nBadLM = 0;
+                    }
+                    qmax = 0;
+                }
+                __syncthreads();
+                do {
+                    if (tid == 0) {
+                        Tbak = T;
+                        for (int r = 0, q = 0; r < 6; r++)
+                            for (int cc = r; cc < 6; cc++, q++) {
+                                double h = Hs[q];
+                                if (cc == r) h += lambda;
+                                Hd[r * 6 + cc] = h;
+                                Hd[cc * 6 + r] = h;
+                            }
+                        const bool ok2 = ldlt_pivot6(Hd, bs, xn, lt, lt + 6, ltr);
+                        if (ok2)
+                            for (int j = 0; j < 6; j++) xs[j] = xn[j];
+                        okS = ok2 ? 1 : 0;
+                        Se3 d, r;
+                        se3_exp(xs, d);
+                        se3_mul(d, T, r);
+                        T = r;
+                    }
+                    __syncthreads();
+                    block_csum<1>([&](int a, double* v) {
+                        const int i = aE[a];
+                        double e3[3];
+                        pose_err(E[i], T, P, e3);
+                        for (int j = 0; j < 3; j++) err[3 * i + j] = e3[j];
+                        v[0] = pose_rho0(E[i], pose_chi2(E[i], e3), robust[i]);
+                    }, na, cs, red);
+                    if (tid == 0) {
+                        double tempChi = red[0];
+                        if (!okS) tempChi = DBL_MAX;
+                        double rho = currentChi - tempChi;
+                        double sv[6];
+                        for (int j = 0; j < 6; j++) sv[j] = xs[j] * (lambda * xs[j] + bs[j]);
+                        double scale = tree64_local([&](int j) { return sv[j]; }, 6);
+                        scale += 1e-3;
+                        rho /= scale;
+                        if (rho > 0 && isfinite(tempChi)) {
+                            const double a3 = 2 * rho - 1;
+                            double alpha = 1. - (a3 * a3) * a3;
+                            alpha = fmin(alpha, 2. / 3.);
+                            const double scaleFactor = fmax(1. / 3., alpha);
+                            lambda *= scaleFactor;
+                            ni = 2;
+                            currentChi = tempChi;
+                        } else {
+                            lambda *= ni;
+                            ni *= 2;
+                            T = Tbak;
+                        }
+                        qmax++;
+                        again = (rho < 0 && qmax < 10) ? 1 : 0;
+                        if (!again) {
+                            if (qmax == 10 || rho == 0) {
+                                term = 1;
+                            } else {
+                                if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
+                                else nBadLM = 0;
+                                term = nBadLM >= 3 ? 1 : 0;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                } while (again);
+                if (term) break;
+            }
+        }
+        // classification (Optimizer.cc:376-426): outliers get their error recomputed
+        if (tid == 0) nBad = 0;
+        __syncthreads();
+        int mybad = 0;
+        for (int i = tid; i < ne; i += blockDim.x) {
+            const PoseEdgeDev& e = E[i];
+            double e3[3] = {err[3 * i], err[3 * i + 1], err[3 * i + 2]};
+            if (outl[i]) {
+                pose_err(e, T, P, e3);
+                for (int j = 0; j < 3; j++) err[3 * i + j] = e3[j];
+            }
+            const float chi2 = (float)pose_chi2(e, e3);
+            if (chi2 > (e.stereo ? chi2Stereo : chi2Mono)) {
+                outl[i] = 1;
+                level[i] = 1;
+                mybad++;
+            } else {
+                outl[i] = 0;
+                level[i] = 0;
+            }
+            if (it == 2) robust[i] = 0;
+        }
+        if (mybad) atomicAdd(&nBad, mybad);
+        __syncthreads();
+        if (ne < 10) break;   // optimizer.edges().size() < 10
+    }
+    if (tid == 0) {
+        P.T = T;
+        P.nbad = nBad;
+    }
+}
+
 // ---------------------------------------------------------------- host
 static void host_se3_from_Tcw(const float* T, Se3& o) {
     double R[9];
@@ -1196,6 +1577,102 @@ static void host_se3_to_Tcw(const Se3& s, float* T) {
     }
     T[12] = T[13] = T[14] = 0.f;
     T[15] = 1.f;
+}
+
+// ---------------------------------------------------------------- PoseEngine
+PoseEngine::~PoseEngine() {
+    if (dArena_) (void)hipFree(dArena_);
+    if (hArena_) (void)hipHostFree(hArena_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+int PoseEngine::init() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
+    ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    return 0;
+}
+
+// Edge creation (Optimizer.cc:268-347): rows with a map point in keypoint order.
+int PoseEngine::run(int count, const pose_problem* P, float* Tcw_out, uint8_t* const* outlier, int* ninliers) {
+    size_t ne = 0;
+    std::vector<int> nE(count);
+    for (int f = 0; f < count; f++) {
+        int c = 0;
+        for (int i = 0; i < P[f].N; i++) c += P[f].has_mp[i] ? 1 : 0;
+        if (c > kPoseMaxEdges) return -3;
+        nE[f] = c;
+        ne += c;
+    }
+    const auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t bProb = al(sizeof(PoseProbDev) * count), bEdge = al(sizeof(PoseEdgeDev) * std::max<size_t>(ne, 1));
+    const size_t bErr = al(sizeof(double) * 3 * std::max<size_t>(ne, 1)), bOut = al(std::max<size_t>(ne, 1));
+    const size_t need = bProb + bEdge + bErr + bOut;
+    if (need > cap_) {
+        if (dArena_) (void)hipFree(dArena_);
+        if (hArena_) (void)hipHostFree(hArena_);
+        dArena_ = hArena_ = nullptr;
+        cap_ = 0;
+        ORB_HIP_CHECK(hipMalloc(&dArena_, need));
+        ORB_HIP_CHECK(hipHostMalloc(&hArena_, need));
+        cap_ = need;
+    }
+    char* h = (char*)hArena_;
+    char* d = (char*)dArena_;
+    PoseProbDev* hp = (PoseProbDev*)h;
+    PoseEdgeDev* he = (PoseEdgeDev*)(h + bProb);
+    uint8_t* hOut = (uint8_t*)(h + bProb + bEdge + bErr);
+    const double deltaMono = (double)(float)sqrt(5.991), deltaStereo = (double)(float)sqrt(7.815);
+    int e0 = 0;
+    for (int f = 0; f < count; f++) {
+        const pose_problem& Q = P[f];
+        PoseProbDev& pp = hp[f];
+        memset(&pp, 0, sizeof(pp));
+        pp.ne = nE[f];
+        pp.e0 = e0;
+        host_se3_from_Tcw(Q.Tcw, pp.T0);
+        pp.fx = Q.fx; pp.fy = Q.fy; pp.cx = Q.cx; pp.cy = Q.cy; pp.bf = Q.bf;
+        for (int i = 0; i < Q.N; i++) {
+            if (!Q.has_mp[i]) continue;
+            PoseEdgeDev& e = he[e0++];
+            for (int j = 0; j < 3; j++) {
+                e.Xw[j] = (double)Q.Xw[3 * i + j];
+                e.obs[j] = (double)Q.obs[3 * i + j];
+            }
+            e.stereo = !(Q.obs[3 * i + 2] < 0) ? 1 : 0;
+            e.info = (double)Q.inv_sigma2[i];
+            e.delta = e.stereo ? deltaStereo : deltaMono;
+            e.dsqr = e.delta * e.delta;
+            e.kp = i;
+        }
+    }
+    PoseProbDev* dp = (PoseProbDev*)d;
+    ORB_HIP_CHECK(hipMemcpyAsync(d, h, bProb + sizeof(PoseEdgeDev) * ne, hipMemcpyHostToDevice, stream_));
+    if (count > 0)
+        hipLaunchKernelGGL(k_pose_opt, dim3(count), dim3(kPoseThreads), 0, stream_, dp, (const PoseEdgeDev*)(d + bProb),
+                           (double*)(d + bProb + bEdge), (uint8_t*)(d + bProb + bEdge + bErr));
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipMemcpyAsync(h, d, bProb, hipMemcpyDeviceToHost, stream_));
+    if (ne) ORB_HIP_CHECK(hipMemcpyAsync(hOut, d + bProb + bEdge + bErr, ne, hipMemcpyDeviceToHost, stream_));
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int f = 0; f < count; f++) {
+        const pose_problem& Q = P[f];
+        const PoseProbDev& pp = hp[f];
+        const uint8_t* o = hOut + pp.e0;
+        for (int i = 0, k = 0; i < Q.N; i++)
+            if (Q.has_mp[i]) {
+                outlier[f][i] = pp.nbad < 0 ? 0 : o[k];
+                k++;
+            }
+        if (pp.nbad < 0) {   // nInitialCorrespondences < 3: return 0, pose untouched
+            memcpy(Tcw_out + 16 * (size_t)f, Q.Tcw, sizeof(float) * 16);
+            ninliers[f] = 0;
+        } else {
+            host_se3_to_Tcw(pp.T, Tcw_out + 16 * (size_t)f);
+            ninliers[f] = pp.ne - pp.nbad;
+        }
+    }
+    return 0;
 }
 
 BaEngine::~BaEngine() {

@@ -126,6 +126,23 @@ private:
     BaTrace trace_;
 };
 
+struct PoseEdgeDev;
+struct PoseProbDev;
+
+// Optimizer::PoseOptimization for a batch of frames: one persistent workgroup per frame.
+class PoseEngine {
+public:
+    ~PoseEngine();
+    int init();
+    int run(int count, const pose_problem* P, float* Tcw_out, uint8_t* const* outlier, int* ninliers);
+
+private:
+    hipStream_t stream_ = nullptr;
+    void* dArena_ = nullptr;
+    void* hArena_ = nullptr;   // pinned staging: problems + edges in, outliers back
+    size_t cap_ = 0;
+};
+
 int debug_ldlt(int n, const double* S, const double* b, double* x, int variant);
 int debug_csum(const double* v, int n, double* out);
 int debug_ldlt_factor(int n, const double* S, double* out);

@@ -54,6 +54,17 @@ int run_ba(const ba_problem* P, const volatile bool* stop, ba_result* R, orbgpu:
     if (r == ORB_E_NODEVICE || r == ORB_E_HIP) return r;
     return r ? ORB_E_HIP : ORB_OK;
 }
+
+orbgpu::PoseEngine* pose_engine(int* rc) {
+    thread_local orbgpu::PoseEngine* e = nullptr;
+    thread_local int erc = 0;
+    if (!e) {
+        e = new orbgpu::PoseEngine();
+        erc = e->init();
+    }
+    *rc = erc;
+    return e;
+}
 }  // namespace
 
 struct orbgpu_comm_t {};  // opaque: a handle is an orbgpu::Comm*
@@ -90,6 +101,29 @@ int Optimizer_BundleAdjustment_sharded(const ba_problem* shard, orbgpu_comm_h co
     m.iterations = nIterations;
     m.robust = bRobust != 0;
     return run_ba(shard, stop, R, as_comm(comm), &m);
+}
+
+int Optimizer_PoseOptimization_batch(int count, const pose_problem* P, float* Tcw_out, uint8_t* const* outlier,
+                                     int* ninliers) {
+    if (count < 0 || (count > 0 && (!P || !Tcw_out || !outlier || !ninliers))) return ORB_E_INVALID;
+    for (int f = 0; f < count; f++) {
+        const pose_problem& Q = P[f];
+        if (Q.N < 0 || !Q.Tcw || (!outlier[f] && Q.N > 0)) return ORB_E_INVALID;
+        if (Q.N > 0 && (!Q.has_mp || !Q.Xw || !Q.obs || !Q.inv_sigma2)) return ORB_E_INVALID;
+    }
+    if (count == 0) return ORB_OK;
+    int rc = 0;
+    orbgpu::PoseEngine* e = pose_engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    const int r = e->run(count, P, Tcw_out, outlier, ninliers);
+    if (r == -3) return ORB_E_CAPACITY;
+    return r ? ORB_E_HIP : ORB_OK;
+}
+
+int Optimizer_PoseOptimization(const pose_problem* P, float* Tcw_out, uint8_t* outlier, int* ninliers) {
+    if (!P || !Tcw_out || !ninliers) return ORB_E_INVALID;
+    uint8_t* const o[1] = {outlier};
+    return Optimizer_PoseOptimization_batch(1, P, Tcw_out, o, ninliers);
 }
 
 int Optimizer_partition_points(const ba_problem* P, int nranks, int32_t* pt_rank) {

@@ -18,7 +18,7 @@ import threading
 
 import numpy as np
 
-from ._lib import ba_problem, ba_result, check, lib, ptr
+from ._lib import ba_problem, ba_result, check, lib, pose_problem, ptr
 
 _FIELDS = (("kf_id", np.int32), ("kf_Tcw", np.float32), ("kf_local", np.uint8), ("kf_cam", np.float32),
            ("pt_id", np.int32), ("pt_pos", np.float32), ("edge_pt", np.int32), ("edge_kf", np.int32),
@@ -94,6 +94,46 @@ def last_timings():
     ms = np.zeros(2)
     check(lib().Optimizer_last_timings(ptr(ms)))
     return ms
+
+
+# ------------------------------------------------------------------ PoseOptimization
+_POSE = (("Tcw", np.float32), ("has_mp", np.uint8), ("Xw", np.float32), ("obs", np.float32),
+         ("inv_sigma2", np.float32))
+
+
+def _pose_struct(frame, keep):
+    a = {k: np.ascontiguousarray(frame[k], dt) for k, dt in _POSE}
+    keep.append(a)
+    N = len(a["has_mp"])
+    if a["Tcw"].size != 16 or a["Xw"].shape != (N, 3) or a["obs"].shape != (N, 3) or a["inv_sigma2"].shape != (N,):
+        raise ValueError("PoseOptimization: inconsistent frame arrays")
+    fx, fy, cx, cy, bf = (float(v) for v in frame["cam"])
+    return pose_problem(N, ptr(a["Tcw"]), ptr(a["has_mp"]), ptr(a["Xw"]), ptr(a["obs"]), ptr(a["inv_sigma2"]),
+                        fx, fy, cx, cy, bf)
+
+
+def PoseOptimization(frame, outlier=None):
+    """Optimizer::PoseOptimization(Frame*) (Optimizer.cc:239-451).
+
+    frame: dict with Tcw (4x4), has_mp (N), Xw (N x 3), obs (N x 3: kpUn.x, kpUn.y, mvuRight),
+    inv_sigma2 (N), cam (fx, fy, cx, cy, mbf).  outlier: mvbOutlier (N, in/out; rows without
+    a map point are left as given).  -> (nInliers, Tcw 4x4, outlier)."""
+    n, T, o = PoseOptimizationBatch([frame], None if outlier is None else [outlier])
+    return int(n[0]), T[0], o[0]
+
+
+def PoseOptimizationBatch(frames, outliers=None):
+    """One launch for many frames (one workgroup per frame) -> (nInliers[F], Tcw[F,4,4], [outlier_f])."""
+    keep = []
+    F = len(frames)
+    probs = (pose_problem * max(F, 1))(*[_pose_struct(f, keep) for f in frames])
+    outs = [np.ascontiguousarray(outliers[i] if outliers is not None else np.zeros(len(keep[i]["has_mp"])),
+                                 np.uint8).copy() for i in range(F)]
+    optr = (C.c_void_p * max(F, 1))(*[o.ctypes.data for o in outs])
+    T = np.zeros((max(F, 1), 16), np.float32)
+    n = np.zeros(max(F, 1), np.int32)
+    check(lib().Optimizer_PoseOptimization_batch(F, probs, ptr(T), optr, ptr(n)), "Optimizer_PoseOptimization")
+    return n[:F], T[:F].reshape(F, 4, 4), outs
 
 
 # ------------------------------------------------------------------ sharding

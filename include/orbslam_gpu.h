@@ -387,6 +387,37 @@ int Optimizer_LocalBundleAdjustment(const ba_problem* P, const volatile bool* st
 int Optimizer_BundleAdjustment(const ba_problem* P, int nIterations, int bRobust, const volatile bool* stop,
                                ba_result* R);
 
+/* ======================================================================
+ * Motion-only pose optimisation  (reference Optimizer::PoseOptimization,
+ * src/Optimizer.cc:239-451; include/Optimizer.h:48)
+ * One SE3 vertex, one unary edge per keypoint with a map point
+ * (EdgeSE3ProjectXYZOnlyPose if mvuRight[i] < 0, else the stereo edge),
+ * Huber sqrt(5.991) / sqrt(7.815), 4 rounds of optimize(10) each restarted
+ * from mTcw, chi2 outlier classification after every round, robust kernel
+ * dropped after round 3, early exit when fewer than 10 edges.
+ * ====================================================================== */
+typedef struct pose_problem {
+    int N;                     /* keypoints (pFrame->N) */
+    const float* Tcw;          /* 16 row-major pFrame->mTcw */
+    const uint8_t* has_mp;     /* N: mvpMapPoints[i] != NULL */
+    const float* Xw;           /* N x 3: pMP->GetWorldPos() (rows with has_mp) */
+    const float* obs;          /* N x 3: mvKeysUn[i].pt.x, .y, mvuRight[i] */
+    const float* inv_sigma2;   /* N: mvInvLevelSigma2[mvKeysUn[i].octave] */
+    float fx, fy, cx, cy, bf;  /* pFrame->fx ... mbf */
+} pose_problem;
+
+/* static int Optimizer::PoseOptimization(Frame* pFrame).
+ * Tcw_out: 16 floats (pFrame->SetPose(toCvMat(SE3quat_recov))); unchanged copy of
+ * Tcw when fewer than 3 correspondences.  outlier: N bytes, in/out like
+ * pFrame->mvbOutlier -- rows with has_mp are written, the others left as they are.
+ * *ninliers = the return value (nInitialCorrespondences - nBad).  At most 4096 map
+ * points per frame (ORB_E_CAPACITY). */
+int Optimizer_PoseOptimization(const pose_problem* P, float* Tcw_out, uint8_t* outlier, int* ninliers);
+/* `count` frames in one launch (one workgroup per frame): Tcw_out count x 16,
+ * outlier[f] N_f bytes, ninliers[count]. */
+int Optimizer_PoseOptimization_batch(int count, const pose_problem* P, float* Tcw_out, uint8_t* const* outlier,
+                                     int* ninliers);
+
 /* ----------------------------------------------------------------------
  * Keyframe-block sharded BA across GPUs: one process (or
  * thread) per rank, map points partitioned by the block of their reference

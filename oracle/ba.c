@@ -966,3 +966,326 @@ int ora_global_ba(const ora_ba_problem* P, int nIterations, int bRobust, const v
 {
     return ba_run(P, 1, nIterations, bRobust, stop, R, trace);
 }
+
+
+/* ======================================================================
+ * Optimizer::PoseOptimization (Optimizer.cc:239-451): one SE3 vertex, unary
+ * EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose edges
+ * (types_six_dof_expmap.cpp:266-364), LinearSolverDense (Eigen LDLT with
+ * diagonal pivoting, linear_solver_dense.h:65-113), 4 rounds of optimize(10)
+ * each restarted from pFrame->mTcw, outlier classification after every round.
+ * ====================================================================== */
+typedef struct {
+    double Xw[3], obs[3], info, delta, dsqr, err[3];
+    int stereo, level, robust, kp;
+} pose_edge;
+
+static void pose_edge_error(pose_edge* e, const se3q* T, const ora_pose_problem* P)
+{
+    double p[3];
+    se3_map(T, e->Xw, p);
+    const double fx = P->fx, fy = P->fy, cx = P->cx, cy = P->cy;
+    if (!e->stereo) {
+        const double px = p[0] / p[2], py = p[1] / p[2];
+        e->err[0] = e->obs[0] - (px * fx + cx);
+        e->err[1] = e->obs[1] - (py * fy + cy);
+        e->err[2] = 0;
+    } else {
+        const float invz = (float)(1.0 / p[2]);
+        const double u = (p[0] * (double)invz) * fx + cx;
+        const double v = (p[1] * (double)invz) * fy + cy;
+        e->err[0] = e->obs[0] - u;
+        e->err[1] = e->obs[1] - v;
+        e->err[2] = e->obs[2] - (u - (double)P->bf * (double)invz);
+    }
+}
+
+static double pose_edge_chi2(const pose_edge* e)
+{
+    const int D = e->stereo ? 3 : 2;
+    double s = 0;
+    for (int j = 0; j < D; j++) s += e->err[j] * (e->info * e->err[j]);
+    return s;
+}
+
+/* Jacobian d e / d pose (D x 6), linearizeOplus of the OnlyPose edges */
+static void pose_edge_jacobian(const pose_edge* e, const se3q* T, const ora_pose_problem* P, double* J)
+{
+    double p[3];
+    se3_map(T, e->Xw, p);
+    const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
+    const double fx = P->fx, fy = P->fy, bf = P->bf;
+    J[0] = ((x * y) * invz_2) * fx;
+    J[1] = (-(1 + ((x * x) * invz_2))) * fx;
+    J[2] = (y * invz) * fx;
+    J[3] = (-invz) * fx;
+    J[4] = 0;
+    J[5] = (x * invz_2) * fx;
+    J[6] = (1 + ((y * y) * invz_2)) * fy;
+    J[7] = (((-x) * y) * invz_2) * fy;
+    J[8] = ((-x) * invz) * fy;
+    J[9] = 0;
+    J[10] = (-invz) * fy;
+    J[11] = (y * invz_2) * fy;
+    if (e->stereo) {
+        J[12] = J[0] - ((bf * y) * invz_2);
+        J[13] = J[1] + ((bf * x) * invz_2);
+        J[14] = J[2];
+        J[15] = J[3];
+        J[16] = 0;
+        J[17] = J[5] - (bf * invz_2);
+    }
+}
+
+/* Eigen::LDLT<MatrixXd> (Lower) compute + solve, diagonal pivoting, sequential dot products.
+ * H: n x n symmetric (both triangles), destroyed.  Returns isPositive(). */
+int ora_ldlt_pivot_solve(double* H, int n, const double* b, double* x)
+{
+    int tr[64];
+    double tmp[64], y[64];
+    int sign = 0;   /* 0 ZeroSign, 1 PositiveSemiDef, 2 NegativeSemiDef, 3 Indefinite */
+    if (n > 64) return 0;
+#define M(i, j) H[(i) * n + (j)]
+    for (int k = 0; k < n; k++) {
+        int idx = k;
+        double big = fabs(M(k, k));
+        for (int i = k + 1; i < n; i++)
+            if (fabs(M(i, i)) > big) { big = fabs(M(i, i)); idx = i; }
+        tr[k] = idx;
+        if (idx != k) {
+            for (int j = 0; j < k; j++) { const double t = M(k, j); M(k, j) = M(idx, j); M(idx, j) = t; }
+            for (int i = idx + 1; i < n; i++) { const double t = M(i, k); M(i, k) = M(i, idx); M(i, idx) = t; }
+            { const double t = M(k, k); M(k, k) = M(idx, idx); M(idx, idx) = t; }
+            for (int i = k + 1; i < idx; i++) { const double t = M(i, k); M(i, k) = M(idx, i); M(idx, i) = t; }
+        }
+        if (k > 0) {
+            for (int j = 0; j < k; j++) tmp[j] = M(j, j) * M(k, j);
+            double s = 0;
+            for (int j = 0; j < k; j++) s += M(k, j) * tmp[j];
+            M(k, k) -= s;
+            for (int i = k + 1; i < n; i++) {
+                double t = 0;
+                for (int j = 0; j < k; j++) t += M(i, j) * tmp[j];
+                M(i, k) -= t;
+            }
+        }
+        const double akk = M(k, k);
+        const int valid = fabs(akk) > 0.0;
+        if (k == 0 && !valid) {   /* the whole diagonal is zero */
+            for (int j = k; j < n; j++) tr[j] = j;
+            sign = 0;
+            break;
+        }
+        if (valid)
+            for (int i = k + 1; i < n; i++) M(i, k) /= akk;
+        if (sign == 1) { if (akk < 0) sign = 3; }
+        else if (sign == 2) { if (akk > 0) sign = 3; }
+        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+    }
+    if (!(sign == 1 || sign == 0)) return 0;
+    for (int i = 0; i < n; i++) y[i] = b[i];
+    for (int k = 0; k < n; k++) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }   /* P b */
+    for (int i = 0; i < n; i++)                                                          /* L y */
+        for (int j = 0; j < i; j++) y[i] -= M(i, j) * y[j];
+    for (int i = 0; i < n; i++)                                                          /* D */
+        y[i] = fabs(M(i, i)) > DBL_MIN ? y[i] / M(i, i) : 0.0;
+    for (int i = n - 1; i >= 0; i--)                                                     /* L^T x */
+        for (int j = n - 1; j > i; j--) y[i] -= M(j, i) * y[j];
+    for (int k = n - 1; k >= 0; k--) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }  /* P^T */
+    for (int i = 0; i < n; i++) x[i] = y[i];
+#undef M
+    return 1;
+}
+
+static const int DIAG21P[6] = {0, 6, 11, 15, 18, 20};
+
+/* one OptimizationAlgorithmLevenberg::solve on the single pose */
+static int pose_lm_solve(pose_edge* E, int ne, se3q* T, const ora_pose_problem* P, int iteration, double* lambda,
+                         double* ni, int* nBadLM, double* scratch, double* xs, ora_ba_trace* tr)
+{
+    int nA = 0;
+    double* v = scratch;
+    for (int i = 0; i < ne; i++)
+        if (E[i].level == 0) {
+            pose_edge_error(&E[i], T, P);
+            const double c = pose_edge_chi2(&E[i]);
+            double r0 = c;
+            if (E[i].robust && !(c <= E[i].dsqr)) { const double sq = sqrt(c); r0 = (2 * sq) * E[i].delta - E[i].dsqr; }
+            v[nA++] = r0;
+        }
+    double currentChi = ora_csum(v, nA);
+    const double iniChi = currentChi;
+    /* buildSystem: terms per active edge, canonical sums in edge order */
+    double H[21], bvec[6];
+    {
+        double* terms = scratch + ne + 64;   /* 27 x nA */
+        int a = 0;
+        for (int i = 0; i < ne; i++) {
+            if (E[i].level != 0) continue;
+            pose_edge* e = &E[i];
+            double J[18];
+            pose_edge_jacobian(e, T, P, J);
+            const int D = e->stereo ? 3 : 2;
+            const double c = pose_edge_chi2(e);
+            double r1 = 1.;
+            if (e->robust && !(c <= e->dsqr)) r1 = e->delta / sqrt(c);
+            const double w = e->robust ? r1 * e->info : e->info;
+            double omr[3] = {0, 0, 0};
+            for (int k = 0; k < D; k++) {
+                omr[k] = -(e->info * e->err[k]);
+                if (e->robust) omr[k] *= r1;
+            }
+            int q = 0;
+            for (int r = 0; r < 6; r++) {
+                double s = 0;
+                for (int k = 0; k < D; k++) s += J[k * 6 + r] * omr[k];
+                terms[(21 + r) * nA + a] = s;
+                for (int cc = r; cc < 6; cc++) {
+                    double h = 0;
+                    for (int k = 0; k < D; k++) h += (J[k * 6 + r] * w) * J[k * 6 + cc];
+                    terms[q * nA + a] = h;
+                    q++;
+                }
+            }
+            a++;
+        }
+        for (int q = 0; q < 27; q++) {
+            for (int j = 0; j < nA; j++) v[j] = terms[q * nA + j];
+            const double s = ora_csum(v, nA);
+            if (q < 21) H[q] = s; else bvec[q - 21] = s;
+        }
+    }
+    if (iteration == 0) {
+        double m = 0.;
+        for (int j = 0; j < 6; j++) m = fmax(fabs(H[DIAG21P[j]]), m);
+        *lambda = 1e-5 * m;
+        *ni = 2;
+        *nBadLM = 0;
+    }
+    double rho = 0;
+    int qmax = 0;
+    do {
+        const se3q Tbak = *T;
+        double Hd[36], x[6];
+        for (int r = 0, q = 0; r < 6; r++)
+            for (int cc = r; cc < 6; cc++, q++) {
+                double h = H[q];
+                if (cc == r) h += *lambda;
+                Hd[r * 6 + cc] = h;
+                Hd[cc * 6 + r] = h;
+            }
+        const int ok2 = ora_ldlt_pivot_solve(Hd, 6, bvec, x);
+        if (ok2) memcpy(xs, x, sizeof(x));   /* a failed solve leaves the solver's _x as it was */
+        {
+            se3q d, r;
+            se3_exp(xs, &d);
+            se3_mul(&d, T, &r);
+            *T = r;
+        }
+        int nB = 0;
+        for (int i = 0; i < ne; i++)
+            if (E[i].level == 0) {
+                pose_edge_error(&E[i], T, P);
+                const double c = pose_edge_chi2(&E[i]);
+                double r0 = c;
+                if (E[i].robust && !(c <= E[i].dsqr)) { const double sq = sqrt(c); r0 = (2 * sq) * E[i].delta - E[i].dsqr; }
+                v[nB++] = r0;
+            }
+        double tempChi = ora_csum(v, nB);
+        if (!ok2) tempChi = DBL_MAX;
+        rho = currentChi - tempChi;
+        for (int j = 0; j < 6; j++) v[j] = xs[j] * (*lambda * xs[j] + bvec[j]);
+        double scale = ora_csum(v, 6);
+        scale += 1e-3;
+        rho /= scale;
+        if (rho > 0 && isfinite(tempChi)) {
+            const double a3 = 2 * rho - 1;
+            double alpha = 1. - (a3 * a3) * a3;
+            alpha = fmin(alpha, 2. / 3.);
+            const double scaleFactor = fmax(1. / 3., alpha);
+            *lambda *= scaleFactor;
+            *ni = 2;
+            currentChi = tempChi;
+        } else {
+            *lambda *= *ni;
+            *ni *= 2;
+            *T = Tbak;
+        }
+        qmax++;
+        if (tr && tr->n_trials < ORA_BA_TRACE_MAX) {
+            tr->trial_chi2[tr->n_trials] = tempChi;
+            tr->trial_lambda[tr->n_trials] = *lambda;
+            tr->n_trials++;
+        }
+    } while (rho < 0 && qmax < 10);
+    if (tr && tr->n_solves < ORA_BA_TRACE_MAX) {
+        tr->solve_ini_chi2[tr->n_solves] = iniChi;
+        tr->solve_chi2[tr->n_solves] = currentChi;
+        tr->n_solves++;
+    }
+    if (qmax == 10 || rho == 0) return 1;
+    if ((iniChi - currentChi) * 1e3 < iniChi) (*nBadLM)++;
+    else *nBadLM = 0;
+    return *nBadLM >= 3;
+}
+
+int ora_pose_optimization(const ora_pose_problem* P, float* Tcw_out, uint8_t* outlier, ora_ba_trace* tr)
+{
+    const int N = P->N;
+    if (tr) memset(tr, 0, sizeof(*tr));
+    memcpy(Tcw_out, P->Tcw, sizeof(float) * 16);
+    pose_edge* E = (pose_edge*)calloc(N + 1, sizeof(pose_edge));
+    const float deltaMono = (float)sqrt(5.991), deltaStereo = (float)sqrt(7.815);
+    int ne = 0;
+    for (int i = 0; i < N; i++) {
+        if (!P->has_mp[i]) continue;
+        outlier[i] = 0;
+        pose_edge* e = &E[ne++];
+        e->kp = i;
+        e->stereo = !(P->obs[3 * i + 2] < 0);
+        for (int j = 0; j < 3; j++) { e->Xw[j] = (double)P->Xw[3 * i + j]; e->obs[j] = (double)P->obs[3 * i + j]; }
+        e->info = (double)P->inv_sigma2[i];
+        e->delta = (double)(e->stereo ? deltaStereo : deltaMono);
+        e->dsqr = e->delta * e->delta;
+        e->robust = 1;
+        e->level = 0;
+    }
+    const int nInitial = ne;
+    if (nInitial < 3) { free(E); return 0; }
+    double* scratch = (double*)malloc(sizeof(double) * (28 * (size_t)ne + 128));
+    const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
+    int nBad = 0;
+    se3q T;
+    for (int it = 0; it < 4; it++) {
+        se3_from_Tcw(P->Tcw, &T);            /* vSE3->setEstimate(toSE3Quat(pFrame->mTcw)) */
+        double xs[6] = {0, 0, 0, 0, 0, 0};   /* BlockSolver::_x, (re)allocated by buildStructure */
+        int nAct = 0;
+        for (int i = 0; i < ne; i++) nAct += E[i].level == 0;
+        if (nAct > 0) {   /* optimize(10): no active edge -> no vertex to optimise (returns -1) */
+            double lambda = 0, ni = 2;
+            int nBadLM = 0;
+            for (int k = 0; k < 10; k++)
+                if (pose_lm_solve(E, ne, &T, P, k, &lambda, &ni, &nBadLM, scratch, xs, tr)) break;
+        }
+        nBad = 0;
+        for (int i = 0; i < ne; i++) {
+            pose_edge* e = &E[i];
+            if (outlier[e->kp]) pose_edge_error(e, &T, P);
+            const float chi2 = (float)pose_edge_chi2(e);
+            if (chi2 > (e->stereo ? chi2Stereo : chi2Mono)) {
+                outlier[e->kp] = 1;
+                e->level = 1;
+                nBad++;
+            } else {
+                outlier[e->kp] = 0;
+                e->level = 0;
+            }
+            if (it == 2) e->robust = 0;
+        }
+        if (ne < 10) break;
+    }
+    se3_to_Tcw(&T, Tcw_out);
+    free(scratch);
+    free(E);
+    return nInitial - nBad;
+}

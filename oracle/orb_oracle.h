@@ -253,6 +253,20 @@ typedef struct {
     double solve_ini_chi2[ORA_BA_TRACE_MAX], solve_chi2[ORA_BA_TRACE_MAX];
     double trial_chi2[ORA_BA_TRACE_MAX], trial_lambda[ORA_BA_TRACE_MAX];
 } ora_ba_trace;
+/* Optimizer::PoseOptimization (Optimizer.cc:239-451).  Per keypoint i < N: has_mp[i]
+ * (mvpMapPoints[i] != NULL), Xw (GetWorldPos), obs = (kpUn.x, kpUn.y, mvuRight),
+ * inv_sigma2 = mvInvLevelSigma2[kpUn.octave]. */
+typedef struct {
+    int N;
+    const float* Tcw;
+    const uint8_t* has_mp;
+    const float* Xw;
+    const float* obs;
+    const float* inv_sigma2;
+    float fx, fy, cx, cy, bf;
+} ora_pose_problem;
+int   ora_pose_optimization(const ora_pose_problem* P, float* Tcw_out, uint8_t* outlier, ora_ba_trace* trace);
+int   ora_ldlt_pivot_solve(double* H, int n, const double* b, double* x);
 double ora_csum(double* v, int n);
 int   ora_ldlt_solve(double* S, int n, const double* b, double* x);
 int   ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_result* R, ora_ba_trace* trace);

@@ -478,3 +478,27 @@ def oracle_search_for_triangulation(KF1, has_mp1, fv1, KF2, has_mp2, fv2, levelS
                                        ptr(s2), ptr(F), int(bool(bOnlyStereo)), int(bool(checkOri)), ptr(pairs),
                                        len(pairs))
     return pairs[:n].copy()
+
+
+class _PoseProblem(C.Structure):
+    _fields_ = [("N", C.c_int), ("Tcw", C.c_void_p), ("has_mp", C.c_void_p), ("Xw", C.c_void_p), ("obs", C.c_void_p),
+                ("inv_sigma2", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float),
+                ("cy", C.c_float), ("bf", C.c_float)]
+
+
+def oracle_pose_optimization(pr):
+    """Optimizer::PoseOptimization restated on CPU -> dict(Tcw, outlier, inliers, trace)."""
+    L = lib()
+    L.ora_pose_optimization.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    a = {k: np.ascontiguousarray(pr[k], dt) for k, dt in (("Tcw", np.float32), ("has_mp", np.uint8),
+                                                           ("Xw", np.float32), ("obs", np.float32),
+                                                           ("inv_sigma2", np.float32))}
+    N = len(a["has_mp"])
+    P = _PoseProblem(N, ptr(a["Tcw"]), ptr(a["has_mp"]), ptr(a["Xw"]), ptr(a["obs"]), ptr(a["inv_sigma2"]),
+                     *[float(v) for v in pr["cam"]])
+    T = np.zeros(16, np.float32)
+    outl = np.ascontiguousarray(pr.get("outlier", np.zeros(N, np.uint8)), np.uint8).copy()
+    tr = _BATrace()
+    n = L.ora_pose_optimization(C.byref(P), ptr(T), ptr(outl), C.byref(tr))
+    return dict(Tcw=T.reshape(4, 4), outlier=outl, inliers=n, solve_chi2=np.array(tr.solve_chi2[:tr.n_solves]),
+                trial_chi2=np.array(tr.trial_chi2[:tr.n_trials]), trial_lambda=np.array(tr.trial_lambda[:tr.n_trials]))

@@ -310,3 +310,35 @@ def test_oracle_searches_run_and_agree_with_geometry():
                                                    d1, k1["angle"], sc.featvec(d1), 0.7)
     got = out[out >= 0]
     assert n == len(got) and len(np.unique(got)) == len(got) and n > 50
+
+
+def test_oracle_pose_optimization_recovers_pose():
+    """ora_pose_optimization (Optimizer.cc:239-451) on a synthetic tracked frame: the
+    motion-model prior is pulled to the true pose and the injected gross outliers are flagged."""
+    from pose_cases import pose_problem
+    pr = pose_problem(0)
+    o = oracle_lib.oracle_pose_optimization(pr)
+    mp = pr["has_mp"].astype(bool)
+    T = o["Tcw"].astype(np.float64)
+    assert np.linalg.norm(T[:3, 3] - pr["T_true"][:3, 3]) < 0.02
+    assert np.abs(T[:3, :3] - pr["T_true"][:3, :3]).max() < 2e-3
+    assert o["outlier"][pr["gross"] & mp].mean() > 0.9
+    assert o["inliers"] == int(mp.sum()) - int(o["outlier"][mp].sum())
+    assert len(o["solve_chi2"]) >= 4
+
+
+def test_oracle_ldlt_pivot_solve():
+    """Eigen LDLT with diagonal pivoting (LinearSolverDense) vs numpy on SPD 6x6 systems."""
+    L = lib()
+    L.ora_ldlt_pivot_solve.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        A = rng.normal(size=(6, 6))
+        H = A @ A.T + np.diag(rng.uniform(0, 5, 6) ** 3)
+        b = rng.normal(size=6)
+        x = np.zeros(6)
+        Hc = np.ascontiguousarray(H).copy()
+        assert L.ora_ldlt_pivot_solve(ptr(Hc), 6, ptr(b), ptr(x)) == 1
+        np.testing.assert_allclose(x, np.linalg.solve(H, b), rtol=1e-9, atol=1e-12)
+    Hn = -np.eye(6)
+    assert L.ora_ldlt_pivot_solve(ptr(Hn), 6, ptr(np.ones(6)), ptr(np.zeros(6))) == 0
