@@ -1290,14 +1290,14 @@ __device__ bool ldlt_pivot6(double* H, const double* b, double* x, double* tmp, 
     return true;
 }
 
-constexpr int kPoseMaxEdges = 4096;
+constexpr int kPoseMaxEdges = 8192;
 constexpr int kPoseThreads = 512;   // 256 VGPRs per lane for the 27-term system build
 constexpr int kPosePer = kPoseMaxEdges / kPoseThreads;
 
 // Block-wide canonical sum (ora_csum) of K per-active-edge values f(a, out[K]), a < nA:
 // 64-edge chunk trees per wave, then one thread per entry over the chunk sums.
 template <int K, class F>
-__device__ __forceinline__ void block_csum(F f, int nA, double (*cs)[64], double* res) {
+__device__ __forceinline__ void block_csum(F f, int nA, double (*cs)[kPoseMaxEdges / 64], double* res) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int m = (nA + 63) >> 6;
     for (int c = w; c < m; c += nw) {
@@ -1327,7 +1327,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     uint8_t* outl = outlAll + P.e0;
     __shared__ uint8_t level[kPoseMaxEdges], robust[kPoseMaxEdges];
     __shared__ int aE[kPoseMaxEdges];
-    __shared__ double cs[27][64];
+    __shared__ double cs[27][kPoseMaxEdges / 64];
     __shared__ double red[32];
     __shared__ Se3 T, Tbak;
     __shared__ double xs[6], Hs[21], bs[6], Hd[36], xn[6], lt[12];

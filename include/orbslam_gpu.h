@@ -410,7 +410,7 @@ typedef struct pose_problem {
  * Tcw_out: 16 floats (pFrame->SetPose(toCvMat(SE3quat_recov))); unchanged copy of
  * Tcw when fewer than 3 correspondences.  outlier: N bytes, in/out like
  * pFrame->mvbOutlier -- rows with has_mp are written, the others left as they are.
- * *ninliers = the return value (nInitialCorrespondences - nBad).  At most 4096 map
+ * *ninliers = the return value (nInitialCorrespondences - nBad).  At most 8192 map
  * points per frame (ORB_E_CAPACITY). */
 int Optimizer_PoseOptimization(const pose_problem* P, float* Tcw_out, uint8_t* outlier, int* ninliers);
 /* `count` frames in one launch (one workgroup per frame): Tcw_out count x 16,

@@ -80,6 +80,6 @@ def test_pose_batch_equals_single(gpu):
 def test_pose_capacity(gpu):
     from c_orb_slam_amd import PoseOptimization
     from c_orb_slam_amd._lib import OrbGpuError
-    pr = pose_problem(1, N=4200, mp_frac=1.0)
+    pr = pose_problem(1, N=8300, mp_frac=1.0)
     with pytest.raises(OrbGpuError):
         PoseOptimization(pr)
