@@ -130,6 +130,7 @@ def lib():
     L.Optimizer_last_timings.argtypes = [vp]
     L.Optimizer_PoseOptimization.argtypes = [P(pose_problem), vp, vp, P(i32)]
     L.Optimizer_PoseOptimization_batch.argtypes = [i32, vp, vp, vp, vp]
+    L.Optimizer_PoseOptimization_batch_device.argtypes = [i32, vp, vp, vp, vp]
     L.orbgpu_unit_ldlt_solve.argtypes = [i32, vp, vp, vp, i32, P(i32)]
     L.orbgpu_unit_csum.argtypes = [vp, i32, vp]
     L.orbgpu_unit_ldlt_factor.argtypes = [i32, vp, vp]

@@ -1193,10 +1193,19 @@ struct PoseEdgeDev {
 
 struct PoseProbDev {
     int ne, e0;            // edges E[e0 .. e0+ne)
-    int nbad, pad;         // out: nBad of the last round (-1: < 3 correspondences)
+    int nbad, N;           // out: nBad of the last round (-1: < 3 correspondences, -2: > capacity)
     Se3 T0;                // Converter::toSE3Quat(pFrame->mTcw)
     Se3 T;                 // out
     double fx, fy, cx, cy, bf;
+    // device mode: the frame's arrays in HBM (edges are built by k_pose_pack, results
+    // written back by k_pose_opt's epilogue); null in host mode
+    const float* Tcw;
+    const uint8_t* has_mp;
+    const float* Xw;
+    const float* obs;
+    const float* inv_sigma2;
+    float* Tcw_out;
+    uint8_t* outlier;
 };
 
 __device__ __forceinline__ void pose_err(const PoseEdgeDev& e, const Se3& T, const PoseProbDev& P, double* err) {
@@ -1335,10 +1344,15 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     __shared__ double lambda, ni, currentChi, iniChi;
     __shared__ int nA, nBadLM, qmax, again, term, nBad, okS, wsum[16];
     const int tid = threadIdx.x;
+    if (ne < 0) return;   // device mode: capacity exceeded (reported by the host)
     if (ne < 3) {
         if (tid == 0) {
             P.T = P.T0;
             P.nbad = -1;
+        }
+        if (P.Tcw_out) {
+            if (tid < 16) P.Tcw_out[tid] = P.Tcw[tid];
+            for (int i = tid; i < ne; i += blockDim.x) P.outlier[E[i].kp] = 0;
         }
         return;
     }
@@ -1555,6 +1569,74 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
         P.T = T;
         P.nbad = nBad;
     }
+    if (P.Tcw_out) {   // pFrame->SetPose(Converter::toCvMat(SE3quat_recov)); mvbOutlier
+        if (tid == 0) {
+            double R[9];
+            quat_to_R(T.q, R);
+            float* o = P.Tcw_out;
+            for (int r = 0; r < 3; r++) {
+                for (int c = 0; c < 3; c++) o[r * 4 + c] = (float)R[r * 3 + c];
+                o[r * 4 + 3] = (float)T.t[r];
+            }
+            o[12] = o[13] = o[14] = 0.f;
+            o[15] = 1.f;
+        }
+        for (int i = tid; i < ne; i += blockDim.x) P.outlier[E[i].kp] = outl[i];
+    }
+}
+
+// Device mode edge creation (Optimizer.cc:268-347): rows with a map point, keypoint order,
+// compacted by a block scan; the initial pose from the frame's Tcw.  One workgroup per frame.
+__global__ void __launch_bounds__(kPoseThreads) k_pose_pack(PoseProbDev* probs, PoseEdgeDev* Eall) {
+    PoseProbDev& P = probs[blockIdx.x];
+    const int N = P.N, tid = threadIdx.x;
+    PoseEdgeDev* E = Eall + P.e0;
+    __shared__ int wsum[kPoseThreads / 64], base;
+    if (tid == 0) {
+        base = 0;
+        double R[9];
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) R[r * 3 + c] = (double)P.Tcw[r * 4 + c];
+        quat_from_R(R, P.T0.q);
+        for (int r = 0; r < 3; r++) P.T0.t[r] = (double)P.Tcw[r * 4 + 3];
+        P.T0.pad = 0;
+        se3_normalize(P.T0);
+    }
+    __syncthreads();
+    const double deltaMono = (double)(float)sqrt(5.991), deltaStereo = (double)(float)sqrt(7.815);
+    for (int c0 = 0; c0 < N; c0 += kPoseThreads) {
+        const int i = c0 + tid;
+        const int f = (i < N && P.has_mp[i]) ? 1 : 0;
+        int incl = f;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if ((tid & 63) >= o) incl += t;
+        }
+        if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+        __syncthreads();
+        int off = base;
+        for (int w = 0; w < (tid >> 6); w++) off += wsum[w];
+        if (f) {
+            const int k = off + incl - 1;
+            if (k < kPoseMaxEdges) {
+                PoseEdgeDev e;
+                for (int j = 0; j < 3; j++) {
+                    e.Xw[j] = (double)P.Xw[3 * i + j];
+                    e.obs[j] = (double)P.obs[3 * i + j];
+                }
+                e.stereo = !(P.obs[3 * i + 2] < 0) ? 1 : 0;
+                e.info = (double)P.inv_sigma2[i];
+                e.delta = e.stereo ? deltaStereo : deltaMono;
+                e.dsqr = e.delta * e.delta;
+                e.kp = i;
+                E[k] = e;
+            }
+        }
+        __syncthreads();
+        if (tid == kPoseThreads - 1) base = off + incl;
+        __syncthreads();
+    }
+    if (tid == 0) P.ne = base > kPoseMaxEdges ? -1 : base;
 }
 
 // ---------------------------------------------------------------- host
@@ -1580,6 +1662,57 @@ static void host_se3_to_Tcw(const Se3& s, float* T) {
 }
 
 // ---------------------------------------------------------------- PoseEngine
+int PoseEngine::run_device(int count, const pose_problem* P, float* const* Tcw_out, uint8_t* const* outlier,
+                           int* ninliers) {
+    size_t nmax = 0;
+    for (int f = 0; f < count; f++) nmax += (size_t)std::min(P[f].N, kPoseMaxEdges + 1);
+    const auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t bProb = al(sizeof(PoseProbDev) * count), bEdge = al(sizeof(PoseEdgeDev) * std::max<size_t>(nmax, 1));
+    const size_t bErr = al(sizeof(double) * 3 * std::max<size_t>(nmax, 1)), bOut = al(std::max<size_t>(nmax, 1));
+    const size_t need = bProb + bEdge + bErr + bOut;
+    if (need > cap_) {
+        if (dArena_) (void)hipFree(dArena_);
+        if (hArena_) (void)hipHostFree(hArena_);
+        dArena_ = hArena_ = nullptr;
+        cap_ = 0;
+        ORB_HIP_CHECK(hipMalloc(&dArena_, need));
+        ORB_HIP_CHECK(hipHostMalloc(&hArena_, need));
+        cap_ = need;
+    }
+    char* h = (char*)hArena_;
+    char* d = (char*)dArena_;
+    PoseProbDev* hp = (PoseProbDev*)h;
+    size_t e0 = 0;
+    for (int f = 0; f < count; f++) {
+        const pose_problem& Q = P[f];
+        PoseProbDev& pp = hp[f];
+        memset(&pp, 0, sizeof(pp));
+        pp.N = Q.N;
+        pp.e0 = (int)e0;
+        e0 += (size_t)std::min(Q.N, kPoseMaxEdges + 1);
+        pp.fx = Q.fx; pp.fy = Q.fy; pp.cx = Q.cx; pp.cy = Q.cy; pp.bf = Q.bf;
+        pp.Tcw = Q.Tcw; pp.has_mp = Q.has_mp; pp.Xw = Q.Xw; pp.obs = Q.obs; pp.inv_sigma2 = Q.inv_sigma2;
+        pp.Tcw_out = Tcw_out[f];
+        pp.outlier = outlier[f];
+    }
+    PoseProbDev* dp = (PoseProbDev*)d;
+    PoseEdgeDev* dE = (PoseEdgeDev*)(d + bProb);
+    ORB_HIP_CHECK(hipMemcpyAsync(d, h, bProb, hipMemcpyHostToDevice, stream_));
+    hipLaunchKernelGGL(k_pose_pack, dim3(count), dim3(kPoseThreads), 0, stream_, dp, dE);
+    hipLaunchKernelGGL(k_pose_opt, dim3(count), dim3(kPoseThreads), 0, stream_, dp, (const PoseEdgeDev*)dE,
+                       (double*)(d + bProb + bEdge), (uint8_t*)(d + bProb + bEdge + bErr));
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipMemcpyAsync(h, d, bProb, hipMemcpyDeviceToHost, stream_));
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    int rc = 0;
+    for (int f = 0; f < count; f++) {
+        const PoseProbDev& pp = hp[f];
+        if (pp.ne < 0) rc = -3;
+        ninliers[f] = pp.ne < 0 || pp.nbad < 0 ? 0 : pp.ne - pp.nbad;
+    }
+    return rc;
+}
+
 PoseEngine::~PoseEngine() {
     if (dArena_) (void)hipFree(dArena_);
     if (hArena_) (void)hipHostFree(hArena_);

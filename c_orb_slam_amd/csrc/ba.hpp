@@ -135,6 +135,9 @@ public:
     ~PoseEngine();
     int init();
     int run(int count, const pose_problem* P, float* Tcw_out, uint8_t* const* outlier, int* ninliers);
+    // P's arrays, Tcw_out[f] (16 floats) and outlier[f] are device pointers
+    int run_device(int count, const pose_problem* P, float* const* Tcw_out, uint8_t* const* outlier, int* ninliers);
+    hipStream_t stream() const { return stream_; }
 
 private:
     hipStream_t stream_ = nullptr;

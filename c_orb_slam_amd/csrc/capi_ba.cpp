@@ -120,6 +120,24 @@ int Optimizer_PoseOptimization_batch(int count, const pose_problem* P, float* Tc
     return r ? ORB_E_HIP : ORB_OK;
 }
 
+int Optimizer_PoseOptimization_batch_device(int count, const pose_problem* P, float* const* Tcw_out,
+                                            uint8_t* const* outlier, int* ninliers) {
+    if (count < 0 || (count > 0 && (!P || !Tcw_out || !outlier || !ninliers))) return ORB_E_INVALID;
+    for (int f = 0; f < count; f++) {
+        const pose_problem& Q = P[f];
+        if (Q.N < 0 || !Q.Tcw || !Tcw_out[f] || (Q.N > 0 && (!outlier[f] || !Q.has_mp || !Q.Xw || !Q.obs ||
+                                                             !Q.inv_sigma2)))
+            return ORB_E_INVALID;
+    }
+    if (count == 0) return ORB_OK;
+    int rc = 0;
+    orbgpu::PoseEngine* e = pose_engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    const int r = e->run_device(count, P, Tcw_out, outlier, ninliers);
+    if (r == -3) return ORB_E_CAPACITY;
+    return r ? ORB_E_HIP : ORB_OK;
+}
+
 int Optimizer_PoseOptimization(const pose_problem* P, float* Tcw_out, uint8_t* outlier, int* ninliers) {
     if (!P || !Tcw_out || !ninliers) return ORB_E_INVALID;
     uint8_t* const o[1] = {outlier};

@@ -136,6 +136,30 @@ def PoseOptimizationBatch(frames, outliers=None):
     return n[:F], T[:F].reshape(F, 4, 4), outs
 
 
+def PoseOptimizationBatchDevice(frames, Tcw_out, outliers):
+    """Device-resident batch: frames[f] holds torch device tensors Tcw (16 f32), has_mp (N u8),
+    Xw (N x 3 f32), obs (N x 3 f32), inv_sigma2 (N f32) and cam (5 floats, host); Tcw_out[f]
+    (16 f32) and outliers[f] (N u8, in/out) are device tensors.  -> nInliers[F] (host)."""
+    F = len(frames)
+    ps = []
+    for f in frames:
+        for k, dt in _POSE:
+            t = f[k]
+            if not t.is_contiguous() or t.element_size() != np.dtype(dt).itemsize:
+                raise ValueError(f"PoseOptimizationBatchDevice: {k} must be contiguous {np.dtype(dt).name}")
+        fx, fy, cx, cy, bf = (float(v) for v in f["cam"])
+        ps.append(pose_problem(int(f["has_mp"].numel()), f["Tcw"].data_ptr(), f["has_mp"].data_ptr(),
+                               f["Xw"].data_ptr(), f["obs"].data_ptr(), f["inv_sigma2"].data_ptr(),
+                               fx, fy, cx, cy, bf))
+    probs = (pose_problem * max(F, 1))(*ps)
+    tptr = (C.c_void_p * max(F, 1))(*[t.data_ptr() for t in Tcw_out])
+    optr = (C.c_void_p * max(F, 1))(*[o.data_ptr() for o in outliers])
+    n = np.zeros(max(F, 1), np.int32)
+    check(lib().Optimizer_PoseOptimization_batch_device(F, probs, tptr, optr, ptr(n)),
+          "Optimizer_PoseOptimization_batch_device")
+    return n[:F]
+
+
 # ------------------------------------------------------------------ sharding
 def partition_points(problem, nranks):
     """pt_rank[p]: keyframe-block owner of every map point (Optimizer_partition_points, host only)."""

@@ -418,6 +418,13 @@ int Optimizer_PoseOptimization(const pose_problem* P, float* Tcw_out, uint8_t* o
 int Optimizer_PoseOptimization_batch(int count, const pose_problem* P, float* Tcw_out, uint8_t* const* outlier,
                                      int* ninliers);
 
+/* Device-resident variant: every array of P[f], Tcw_out[f] (16 floats) and outlier[f]
+ * are HIP device pointers (e.g. the matcher's device-mode outputs gathered in HBM);
+ * the edges are built on the device.  Synchronous; ninliers is host memory.
+ * ORB_E_CAPACITY if a frame has more than 8192 map points (its outputs are not written). */
+int Optimizer_PoseOptimization_batch_device(int count, const pose_problem* P, float* const* Tcw_out,
+                                            uint8_t* const* outlier, int* ninliers);
+
 /* ----------------------------------------------------------------------
  * Keyframe-block sharded BA across GPUs: one process (or
  * thread) per rank, map points partitioned by the block of their reference

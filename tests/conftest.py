@@ -10,6 +10,15 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
 
+# torch (device tensors for the device-pointer entry points) bundles its own HIP runtime
+# under the same soname as /opt/rocm's; load it before liborbslam_gpu.so so that both use
+# torch's copy, as bench.py does (the library only needs the soname).
+try:
+    import torch  # noqa: F401,E402
+except Exception:  # pragma: no cover
+    torch = None
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP library)")
     config.addinivalue_line("markers", "slow: long-running CPU test")

@@ -83,3 +83,28 @@ def test_pose_capacity(gpu):
     pr = pose_problem(1, N=8300, mp_frac=1.0)
     with pytest.raises(OrbGpuError):
         PoseOptimization(pr)
+
+
+def test_pose_device_mode_equals_host(gpu):
+    import torch
+    from c_orb_slam_amd import PoseOptimizationBatch
+    from c_orb_slam_amd.optimizer import PoseOptimizationBatchDevice
+    frames = [pose_problem(20 + s, N=500 + 700 * s) for s in range(4)]
+    frames.append(pose_problem(30, N=20, mp_frac=0.1))           # < 3 correspondences
+    frames[-1]["has_mp"][:] = 0
+    frames[-1]["has_mp"][:2] = 1
+    n_h, T_h, o_h = PoseOptimizationBatch(frames)
+    dev = torch.device("cuda", 0)
+    df = [dict(Tcw=torch.from_numpy(np.ascontiguousarray(f["Tcw"], np.float32).reshape(16)).to(dev),
+               has_mp=torch.from_numpy(f["has_mp"]).to(dev), Xw=torch.from_numpy(f["Xw"]).to(dev),
+               obs=torch.from_numpy(f["obs"]).to(dev), inv_sigma2=torch.from_numpy(f["inv_sigma2"]).to(dev),
+               cam=f["cam"]) for f in frames]
+    T_d = [torch.zeros(16, dtype=torch.float32, device=dev) for _ in frames]
+    o_d = [torch.full((len(f["has_mp"]),), 9, dtype=torch.uint8, device=dev) for f in frames]
+    n_d = PoseOptimizationBatchDevice(df, T_d, o_d)
+    assert np.array_equal(n_d, n_h)
+    for f, fr in enumerate(frames):
+        assert np.array_equal(T_d[f].cpu().numpy().reshape(4, 4), T_h[f])
+        mp = fr["has_mp"].astype(bool)
+        od = o_d[f].cpu().numpy()
+        assert np.array_equal(od[mp], o_h[f][mp]) and (od[~mp] == 9).all()
