@@ -8,7 +8,9 @@ already resident in HBM: Frame(imLeft, imRight) -- ORBextractor::operator() on b
 (Frame.cc:78-81) and ComputeStereoMatches (Frame.cc:466-640) -- then
 TrackWithMotionModel's SearchByProjection(CurrentFrame, LastFrame, th=7, stereo) for the
 B-1 consecutive pairs (Tracking.cc:867-885), the last frame's map points lifted from its
-stereo depth (UpdateLastFrame).  value = stereo frames/s.
+stereo depth (UpdateLastFrame), and Optimizer::PoseOptimization(&mCurrentFrame) on the
+matched map points (Tracking.cc:887, Optimizer.cc:239-451), device-resident end to end.
+value = stereo frames/s.
 
 Extraction + matching do not shard within a sequence (frame t+1 needs frame t), so N GPUs
 run N independent replicas ("replicas only"); value is the frames of all ranks /
@@ -109,9 +111,18 @@ def main():
     eye = torch.eye(4, dtype=torch.float32, device=dev)
     poses = torch.from_numpy(np.stack([synthetic.pose_from_rotation(R) for R in Rs])).to(dev)
     kp_f = d_kps.view(torch.float32)
+    P = B - 1
+    # PoseOptimization inputs gathered in HBM from the matcher's output
+    d_has = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
+    d_Xw = torch.empty((P, cap, 3), dtype=torch.float32, device=dev)
+    d_pobs = torch.empty((P, cap, 3), dtype=torch.float32, device=dev)
+    d_isig = torch.empty((P, cap), dtype=torch.float32, device=dev)
+    d_Tout = torch.empty((P, 16), dtype=torch.float32, device=dev)
+    d_poutl = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
+    isig_tab = torch.from_numpy(exL.GetInverseScaleSigmaSquares()).to(dev)
+    octv = d_kps[1:, :, 5]
     gW = np.float32(np.float32(64) / np.float32(W))
     gH = np.float32(np.float32(48) / np.float32(H))
-    P = B - 1
 
     def frame_struct(b, n, Tptr, stereo):
         f = orb_frame()
@@ -128,6 +139,7 @@ def main():
         return f
 
     stage_acc = {}
+    pose_inl = []
     kernel_ms = []   # k_fast_cells duration per step (HIP events on the extractor streams)
 
     # ctypes views of the batch, built once (device pointers do not move; only counts change)
@@ -149,6 +161,13 @@ def main():
     s_dR = arr([d_descR[b].data_ptr() for b in range(B)])
     s_uR = arr([d_uR[b].data_ptr() for b in range(B)])
     s_dep = arr([d_depth[b].data_ptr() for b in range(B)])
+    from c_orb_slam_amd._lib import pose_problem
+    pprobs = (pose_problem * P)(*[pose_problem(0, poses[p].data_ptr(), d_has[p].data_ptr(), d_Xw[p].data_ptr(),
+                                               d_pobs[p].data_ptr(), d_isig[p].data_ptr(), float(fx), float(fy),
+                                               float(cx), float(cy), float(mbf)) for p in range(P)])
+    a_Tout = arr([d_Tout[p].data_ptr() for p in range(P)])
+    a_poutl = arr([d_poutl[p].data_ptr() for p in range(P)])
+    ninl = np.zeros(P, np.int32)
     nm = np.zeros(P, np.int32)
     nst = np.zeros(B, np.int32)
     from concurrent.futures import ThreadPoolExecutor
@@ -183,17 +202,31 @@ def main():
         check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, P, curs, a_cur_mp, lasts, a_last_kps, a_last_mp,
                                                               a_last_out, mps, 7.0, 0, ptr(nm)),
               "SearchByProjection batch")
+        # Optimizer::PoseOptimization(&mCurrentFrame) (Tracking.cc:887) on the matched map points
+        cm = d_cur_mp[1:]
+        d_has.copy_(cm >= 0)
+        torch.gather(d_mp_pos[:-1], 1, cm.clamp(min=0).long().unsqueeze(-1).expand(-1, -1, 3), out=d_Xw)
+        d_pobs[..., 0:2] = kp_f[1:, :, 0:2]
+        d_pobs[..., 2] = d_uR[1:]
+        torch.index_select(isig_tab, 0, octv.reshape(-1).clamp(0, 7), out=d_isig.view(-1))
+        for p in range(P):
+            pprobs[p].N = int(nL[p + 1])
+        torch.cuda.current_stream().synchronize()
+        check(L.Optimizer_PoseOptimization_batch_device(P, pprobs, a_Tout, a_poutl, ptr(ninl)),
+              "PoseOptimization batch")
         tl, tr = exL.last_timings(), exR.last_timings()
         for k in tl:
             stage_acc[k] = stage_acc.get(k, 0.0) + tl[k] + tr[k]
         kernel_ms.append(tl["fast_cells"])
         kernel_ms.append(tr["fast_cells"])
+        pose_inl.append(int(ninl.sum()))
         return int(nL.sum() + nR.sum()), int(nm.sum()), int(nst.sum())
 
     for _ in range(args.warmup):
         step()
     stage_acc.clear()
     kernel_ms.clear()
+    pose_inl.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -259,11 +292,12 @@ def main():
             "data": "synthetic (seeded KITTI-shaped textured stereo frames: camera-rotation motion, "
                     "ground-plane disparity field 4..40 px)",
             "config": {"workload": "kitti00_stereo: ORB extract L+R, ComputeStereoMatches, "
-                                   "SearchByProjection(Cur,Last,th=7)", "width": W, "height": H,
+                                   "SearchByProjection(Cur,Last,th=7), PoseOptimization", "width": W, "height": H,
                        "nfeatures": NFEAT, "nlevels": 8, "scale_factor": 1.2, "fast_th": [20, 7],
                        "stereo_frames_per_step": B, "parallelism": f"replicas{world}"},
             "matches_per_s": round(tot_match / dt, 1), "stereo_matches_per_s": round(tot_stereo / dt, 1),
             "keypoints_per_image": round(tot_kp / (2 * frames_total), 1),
+            "pose_inliers_per_frame": round(float(np.sum(pose_inl)) / max(len(pose_inl) * P, 1), 1),
             "stage_ms_per_step": stage_ms, "roofline": roof, "cpu_baseline": cpu, "local_ba": ba,
             "global_ba": gba,
         }
@@ -388,7 +422,8 @@ def ba_cpu_baseline(budget_s):
 
 def cpu_baseline(lefts, rights, Rs, budget_s):
     """Oracle (line-faithful C restatement, 1 thread) on a bounded sample of the same workload:
-    per stereo frame extract L and R, ComputeStereoMatches, SearchByProjection(Cur, Last, 7)."""
+    per stereo frame extract L and R, ComputeStereoMatches, SearchByProjection(Cur, Last, 7),
+    PoseOptimization."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
     from c_orb_slam_amd import synthetic
@@ -402,7 +437,8 @@ def cpu_baseline(lefts, rights, Rs, budget_s):
     t0 = time.perf_counter()
     done = 0
     prev = None
-    extract_t = stereo_t = match_t = 0.0
+    extract_t = stereo_t = match_t = pose_t = 0.0
+    isig = eL.tables()["inv_sigma2"]
     while True:
         i = done % len(lefts)
         ta = time.perf_counter()
@@ -424,16 +460,24 @@ def cpu_baseline(lefts, rights, Rs, budget_s):
             td = time.perf_counter()
             oracle_lib.oracle_search_last(cur, cm, last, pk, lm, np.zeros(len(pk), np.uint8), mps, 7.0, False,
                                           0.9, True)
-            match_t += time.perf_counter() - td
+            te = time.perf_counter()
+            match_t += te - td
+            has = (cm >= 0).astype(np.uint8)
+            pr = dict(Tcw=cur.Tcw, has_mp=has, Xw=X[np.maximum(cm, 0)],
+                      obs=np.stack([kL["x"], kL["y"], uR], 1).astype(np.float32),
+                      inv_sigma2=isig[kL["octave"]].astype(np.float32), cam=(fx, fy, cx, cy, mbf))
+            oracle_lib.oracle_pose_optimization(pr)
+            pose_t += time.perf_counter() - te
         prev = (kL, dL, dep)
         done += 1
         if time.perf_counter() - t0 > budget_s and done >= 4:
             break
-    fps = done / (extract_t + stereo_t + match_t)
+    fps = done / (extract_t + stereo_t + match_t + pose_t)
     return {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": f"{done} KITTI-shaped stereo frames: oracle ORBextractor x2 + ComputeStereoMatches + "
-                      f"SearchByProjection(Cur,Last,7) (extract {extract_t / done * 1e3:.1f} ms/frame, stereo "
+                      f"SearchByProjection(Cur,Last,7) + PoseOptimization (extract {extract_t / done * 1e3:.1f} ms/frame, stereo "
                       f"{stereo_t / done * 1e3:.2f} ms, match {match_t / max(done - 1, 1) * 1e3:.2f} ms, "
+                      f"pose {pose_t / max(done - 1, 1) * 1e3:.2f} ms, "
                       f"1 thread, -O2 C restatement)"}
 
 
