@@ -48,6 +48,10 @@ class orb_featvec(C.Structure):
     _fields_ = [("n_nodes", C.c_int), ("node_id", C.c_void_p), ("start", C.c_void_p), ("feat", C.c_void_p)]
 
 
+class orb_mappoint_geo(C.Structure):
+    _fields_ = [("max_dist", C.c_void_p), ("min_dist", C.c_void_p), ("normal", C.c_void_p)]
+
+
 class orb_mappoints(C.Structure):
     _fields_ = [("n", C.c_int), ("pos", C.c_void_p), ("desc", C.c_void_p), ("observations", C.c_void_p)]
 
@@ -107,6 +111,13 @@ def lib():
                                                    P(orb_featvec), vp, P(i32)]
     L.ORBmatcher_SearchForTriangulation.argtypes = [vp, P(orb_frame), vp, P(orb_featvec), P(orb_frame), vp,
                                                     P(orb_featvec), vp, vp, i32, vp, i32, P(i32)]
+    L.ORBmatcher_SearchByProjection_Sim3.argtypes = [vp, P(orb_frame), vp, P(orb_mappoints), P(orb_mappoint_geo), vp,
+                                                     f32, i32, vp, P(i32)]
+    L.ORBmatcher_Fuse.argtypes = [vp, P(orb_frame), P(orb_mappoints), P(orb_mappoint_geo), vp, f32, f32, vp, P(i32)]
+    L.ORBmatcher_Fuse_Sim3.argtypes = [vp, P(orb_frame), vp, P(orb_mappoints), P(orb_mappoint_geo), vp, f32, f32, vp,
+                                       P(i32)]
+    L.ORBmatcher_SearchBySim3.argtypes = [vp, P(orb_frame), vp, P(orb_frame), vp, P(orb_mappoints),
+                                          P(orb_mappoint_geo), vp, f32, vp, vp, f32, f32, vp, P(i32)]
     L.ORBmatcher_SearchCandidates.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp]
     L.orb_rng_seed.argtypes = [vp, C.c_uint]
     L.orb_rng_rand.argtypes = [vp]

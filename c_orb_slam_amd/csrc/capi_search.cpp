@@ -5,6 +5,10 @@
 //   SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches)           159-288
 //   SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12)              522-655
 //   SearchForTriangulation(KF1, KF2, F12, vMatchedPairs, bOnlyStereo)         657-823
+//   SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)  290-403   (loop closing)
+//   Fuse(KeyFrame*, vpMapPoints, th)                             825-975   (local mapping)
+//   Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint)           977-1100  (loop closing)
+//   SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)     1102-1326 (loop detection)
 //
 // Split of the work: the device enumerates every candidate of every query and its 256-bit
 // Hamming distance (the window engine Matcher::area_candidates over the frame grid, or the
@@ -184,6 +188,189 @@ int node_lists(Matcher* m, const orb_featvec* fv1, const uint8_t* ok1, const uin
     if (m->candidates(dq, nq, dt, n2, doff, dc, dd, dbi, dbd, dsd)) return ORB_E_HIP;
     if (hipMemcpyAsync(L.dist.data(), dd, (size_t)nc * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return ORB_E_HIP;
     return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+}
+
+
+// ---- similarity-pose projection searches (ORBmatcher.cc:290-403, 825-1326) -----------------
+struct SimPose {
+    float R[9], t[3], O[3];
+};
+
+inline float gemm3(const float* R, const float* t, int r, const float* X) {
+    const double s = (double)R[r * 3 + 0] * X[0] + (double)R[r * 3 + 1] * X[1] + (double)R[r * 3 + 2] * X[2];
+    return (float)(s + (double)t[r]);
+}
+
+inline void pose_center(SimPose& P) {   // -Rcw.t()*tcw: gemm with alpha -1
+    for (int i = 0; i < 3; i++) {
+        const double s = (double)P.R[i] * P.t[0] + (double)P.R[3 + i] * P.t[1] + (double)P.R[6 + i] * P.t[2];
+        P.O[i] = (float)(s * -1.0);
+    }
+}
+
+inline SimPose pose_T(const float* T) {
+    SimPose P;
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) P.R[r * 3 + c] = T[r * 4 + c];
+        P.t[r] = T[r * 4 + 3];
+    }
+    pose_center(P);
+    return P;
+}
+
+// ORBmatcher.cc:298-303: scw = sqrt(row0.row0); Rcw = sRcw/scw, tcw = t/scw (convertTo: float
+// multiply by (float)(1/scw)); Ow = -Rcw.t()*tcw
+inline SimPose pose_Scw(const float* S) {
+    SimPose P;
+    const double d = (double)S[0] * S[0] + (double)S[1] * S[1] + (double)S[2] * S[2];
+    const float scw = (float)std::sqrt(d);
+    const float a = (float)(1.0 / (double)scw);
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) P.R[r * 3 + c] = S[r * 4 + c] * a + 0.0f;
+        P.t[r] = S[r * 4 + 3] * a + 0.0f;
+    }
+    pose_center(P);
+    return P;
+}
+
+inline int predict_scale(float maxDistance, float dist, float logScaleFactor, int nlevels) {   // MapPoint.cc:385-400
+    const float ratio = maxDistance / dist;
+    int n = (int)std::ceil(std::log(ratio) / logScaleFactor);
+    return n < 0 ? 0 : (n >= nlevels ? nlevels - 1 : n);
+}
+
+inline bool kf_in_image(const orb_frame* F, float u, float v) {   // KeyFrame::IsInImage
+    return u >= F->minX && u < F->maxX && v >= F->minY && v < F->maxY;
+}
+
+inline float norm3f(const float* v) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)v[k] * (double)v[k];
+    return (float)std::sqrt(s);
+}
+
+bool geo_ok(const orb_mappoints* p, const orb_mappoint_geo* g, bool normal) {
+    if (!p || p->n < 0) return false;
+    if (p->n == 0) return true;
+    return p->pos && p->desc && g && g->max_dist && g->min_dist && (!normal || g->normal);
+}
+
+// Queries of one projection pass -> every in-window candidate (KeyFrame::GetFeaturesInArea,
+// octave range [pred-1, pred] applied on device) with its Hamming distance.
+struct ProjPass {
+    std::vector<AreaQuery> q;
+    std::vector<uint8_t> qdesc;
+    std::vector<float> u, v, ur;   // projections for the host gates
+    std::vector<int> off;
+    std::vector<int2> cand;
+    void add(float x, float y, float r, int lvl, const uint8_t* d, float uu, float vv, float uur, size_t i) {
+        AreaQuery& a = q[i];
+        a.x = x;
+        a.y = y;
+        a.r = r;
+        a.minLevel = lvl - 1;
+        a.maxLevel = lvl;
+        a.qd = (int)(qdesc.size() / 32);
+        qdesc.insert(qdesc.end(), d, d + 32);
+        u[i] = uu;
+        v[i] = vv;
+        ur[i] = uur;
+    }
+    void reset(int n) {
+        q.assign((size_t)n, AreaQuery{0, 0, 0, -1, -1, -1});
+        qdesc.clear();
+        u.assign((size_t)n, 0.f);
+        v.assign((size_t)n, 0.f);
+        ur.assign((size_t)n, 0.f);
+    }
+    int run(Matcher* m, const orb_frame* F) {
+        const size_t n = q.size();
+        if (m->arena_reserve(al((size_t)F->N * 28) + al((size_t)F->N * 32) + al(n * sizeof(AreaQuery)) +
+                             al(qdesc.size()) + 4096))
+            return ORB_E_HIP;
+        int err = 0;
+        hipStream_t s = m->stream();
+        SearchDev P = frame_dev(m, F, s, &err);
+        const AreaQuery* dq = up(m, q.data(), n, s, &err);
+        const uint8_t* dd = up(m, qdesc.data(), qdesc.size(), s, &err);
+        if (err) return err;
+        if (n == 0) {
+            off.assign(1, 0);
+            return ORB_OK;
+        }
+        return m->area_candidates(P, dq, (int)n, dd, off, cand) ? ORB_E_HIP : ORB_OK;
+    }
+};
+
+// Projection of map point i for SearchByProjection(KF,Scw) / Fuse / Fuse(Scw) (shared gates):
+// returns the predicted level or -1 when a gate rejects the point.
+int project_point(const orb_frame* KF, const SimPose& P, const float* X, float maxD, float minD, const float* Pn,
+                  float logScaleFactor, int invz_mode, float bf, float* u, float* v, float* ur) {
+    const float xc = gemm3(P.R, P.t, 0, X), yc = gemm3(P.R, P.t, 1, X), zc = gemm3(P.R, P.t, 2, X);
+    if (zc < 0.0f) return -1;
+    const float invz = invz_mode ? (float)(1.0 / (double)zc) : 1 / zc;   // `1.0/z` vs `1/z`
+    const float x = xc * invz, y = yc * invz;
+    *u = KF->fx * x + KF->cx;
+    *v = KF->fy * y + KF->cy;
+    if (!kf_in_image(KF, *u, *v)) return -1;
+    *ur = *u - bf * invz;
+    const float PO[3] = {X[0] - P.O[0], X[1] - P.O[1], X[2] - P.O[2]};
+    const float dist = norm3f(PO);
+    if (dist < 0.8f * minD || dist > 1.2f * maxD) return -1;
+    const double dot = (double)PO[0] * Pn[0] + (double)PO[1] * Pn[1] + (double)PO[2] * Pn[2];
+    if (dot < 0.5 * dist) return -1;
+    return predict_scale(maxD, dist, logScaleFactor, KF->nlevels);
+}
+
+int fuse_common(Matcher* m, const orb_frame* KF, const SimPose& P, bool sim3, const orb_mappoints* pts,
+                const orb_mappoint_geo* geo, const uint8_t* skip, float logScaleFactor, float th, int32_t* best,
+                int* nfused) {
+    const int n = pts->n;
+    ProjPass pp;
+    pp.reset(n);
+    for (int i = 0; i < n; i++) {
+        best[i] = -1;
+        if (skip[i]) continue;
+        float u, v, ur;
+        const int lvl = project_point(KF, P, pts->pos + 3 * (size_t)i, geo->max_dist[i], geo->min_dist[i],
+                                      geo->normal + 3 * (size_t)i, logScaleFactor, sim3 ? 1 : 0, sim3 ? 0.f : KF->bf,
+                                      &u, &v, &ur);
+        if (lvl < 0) continue;
+        pp.add(u, v, th * KF->scaleFactors[lvl], lvl, pts->desc + 32 * (size_t)i, u, v, ur, (size_t)i);
+    }
+    if (int e = pp.run(m, KF)) return e;
+    int nf = 0;
+    for (int i = 0; i < n; i++) {
+        if (pp.q[i].qd < 0) continue;
+        int bestDist = sim3 ? INT_MAX : 256, bestIdx = -1;
+        for (int k = pp.off[i]; k < pp.off[i + 1]; k++) {
+            const int idx = pp.cand[k].x;
+            if (!sim3) {   // reprojection gate (ORBmatcher.cc:914-938)
+                const orb_kp& kp = KF->keysUn[idx];
+                const float s2 = KF->scaleFactors[kp.octave] * KF->scaleFactors[kp.octave];
+                const float invSigma2 = 1.0f / s2;
+                const float ex = pp.u[i] - kp.x, ey = pp.v[i] - kp.y;
+                if (KF->uRight && KF->uRight[idx] >= 0) {
+                    const float er = pp.ur[i] - KF->uRight[idx];
+                    const float e2 = ex * ex + ey * ey + er * er;
+                    if (e2 * invSigma2 > 7.8) continue;
+                } else {
+                    const float e2 = ex * ex + ey * ey;
+                    if (e2 * invSigma2 > 5.99) continue;
+                }
+            }
+            if (pp.cand[k].y < bestDist) {
+                bestDist = pp.cand[k].y;
+                bestIdx = idx;
+            }
+        }
+        if (bestDist <= kThLow) {
+            best[i] = bestIdx;
+            nf++;
+        }
+    }
+    *nfused = nf;
+    return ORB_OK;
 }
 
 }  // namespace
@@ -515,6 +702,150 @@ int ORBmatcher_SearchForTriangulation(ORBmatcher_h h, const orb_frame* KF1, cons
         }
     *npairs = np;
     return np > cap ? ORB_E_CAPACITY : ORB_OK;
+}
+
+int ORBmatcher_SearchByProjection_Sim3(ORBmatcher_h h, const orb_frame* KF, const float* Scw,
+                                       const orb_mappoints* pts, const orb_mappoint_geo* geo, const uint8_t* skip,
+                                       float logScaleFactor, int th, int32_t* matched, int* nmatches) {
+    if (!h || !frame_ok(KF) || !Scw || !geo_ok(pts, geo, true) || (pts->n && !skip) || !nmatches ||
+        (KF->N && !matched))
+        return ORB_E_INVALID;
+    Matcher* m = h->m;
+    if (m->device_pointers()) return ORB_E_INVALID;
+    const SimPose P = pose_Scw(Scw);
+    const int n = pts->n;
+    ProjPass pp;
+    pp.reset(n);
+    for (int i = 0; i < n; i++) {
+        if (skip[i]) continue;
+        float u, v, ur;
+        const int lvl = project_point(KF, P, pts->pos + 3 * (size_t)i, geo->max_dist[i], geo->min_dist[i],
+                                      geo->normal + 3 * (size_t)i, logScaleFactor, 0, 0.f, &u, &v, &ur);
+        if (lvl < 0) continue;
+        pp.add(u, v, th * KF->scaleFactors[lvl], lvl, pts->desc + 32 * (size_t)i, u, v, ur, (size_t)i);
+    }
+    if (int e = pp.run(m, KF)) return e;
+    // greedy replay in vpPoints order: vpMatched occupancy grows as points are matched (375, 396)
+    int nm = 0;
+    for (int i = 0; i < n; i++) {
+        if (pp.q[i].qd < 0) continue;
+        int bestDist = 256, bestIdx = -1;
+        for (int k = pp.off[i]; k < pp.off[i + 1]; k++) {
+            const int idx = pp.cand[k].x;
+            if (matched[idx] >= 0) continue;
+            if (pp.cand[k].y < bestDist) {
+                bestDist = pp.cand[k].y;
+                bestIdx = idx;
+            }
+        }
+        if (bestDist <= kThLow) {
+            matched[bestIdx] = i;
+            nm++;
+        }
+    }
+    *nmatches = nm;
+    return ORB_OK;
+}
+
+int ORBmatcher_Fuse(ORBmatcher_h h, const orb_frame* KF, const orb_mappoints* pts, const orb_mappoint_geo* geo,
+                    const uint8_t* skip, float logScaleFactor, float th, int32_t* best, int* nfused) {
+    if (!h || !frame_ok(KF) || !KF->Tcw || !geo_ok(pts, geo, true) || (pts->n && (!skip || !best)) || !nfused)
+        return ORB_E_INVALID;
+    if (h->m->device_pointers()) return ORB_E_INVALID;
+    return fuse_common(h->m, KF, pose_T(KF->Tcw), false, pts, geo, skip, logScaleFactor, th, best, nfused);
+}
+
+int ORBmatcher_Fuse_Sim3(ORBmatcher_h h, const orb_frame* KF, const float* Scw, const orb_mappoints* pts,
+                         const orb_mappoint_geo* geo, const uint8_t* skip, float logScaleFactor, float th,
+                         int32_t* best, int* nfused) {
+    if (!h || !frame_ok(KF) || !Scw || !geo_ok(pts, geo, true) || (pts->n && (!skip || !best)) || !nfused)
+        return ORB_E_INVALID;
+    if (h->m->device_pointers()) return ORB_E_INVALID;
+    return fuse_common(h->m, KF, pose_Scw(Scw), true, pts, geo, skip, logScaleFactor, th, best, nfused);
+}
+
+int ORBmatcher_SearchBySim3(ORBmatcher_h h, const orb_frame* KF1, const int32_t* mp1, const orb_frame* KF2,
+                            const int32_t* mp2, const orb_mappoints* pts, const orb_mappoint_geo* geo,
+                            const uint8_t* bad, float s12, const float* R12, const float* t12, float logScaleFactor,
+                            float th, int32_t* matches12, int* nfound) {
+    if (!h || !frame_ok(KF1) || !frame_ok(KF2) || !KF1->Tcw || !KF2->Tcw || !geo_ok(pts, geo, false) ||
+        (pts->n && !bad) || !R12 || !t12 || !nfound || (KF1->N && (!mp1 || !matches12)) || (KF2->N && !mp2))
+        return ORB_E_INVALID;
+    Matcher* m = h->m;
+    if (m->device_pointers()) return ORB_E_INVALID;
+    const int N1 = KF1->N, N2 = KF2->N;
+    for (int i = 0; i < N1; i++)
+        if (mp1[i] >= pts->n || matches12[i] < -2 || matches12[i] >= N2) return ORB_E_INVALID;
+    for (int i = 0; i < N2; i++)
+        if (mp2[i] >= pts->n) return ORB_E_INVALID;
+    const SimPose P1 = pose_T(KF1->Tcw), P2 = pose_T(KF2->Tcw);
+    // sR12 = s12*R12, sR21 = (1.0/s12)*R12.t(), t21 = -sR21*t12 (ORBmatcher.cc:1119-1121)
+    float sR12[9], sR21[9], t21[3];
+    const float a21 = (float)(1.0 / (double)s12);
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            sR12[r * 3 + c] = R12[r * 3 + c] * s12 + 0.0f;
+            sR21[r * 3 + c] = R12[c * 3 + r] * a21 + 0.0f;
+        }
+    for (int r = 0; r < 3; r++) {
+        const double sacc = (double)sR21[r * 3] * t12[0] + (double)sR21[r * 3 + 1] * t12[1] + (double)sR21[r * 3 + 2] * t12[2];
+        t21[r] = (float)(sacc * -1.0);
+    }
+    std::vector<uint8_t> am1((size_t)N1), am2((size_t)N2);
+    for (int i = 0; i < N1; i++)
+        if (matches12[i] != -1) {
+            am1[i] = 1;
+            if (matches12[i] >= 0) am2[matches12[i]] = 1;
+        }
+    // one direction: side A's points through A's pose and (sR, t) into side B (1148-1225 / 1228-1305)
+    auto direction = [&](const orb_frame* B, const SimPose& Aw, const float* sR, const float* t, int NA,
+                         const int32_t* mpA, const std::vector<uint8_t>& amA, std::vector<int>& vn) -> int {
+        ProjPass pp;
+        pp.reset(NA);
+        vn.assign((size_t)NA, -1);
+        for (int i = 0; i < NA; i++) {
+            const int mp = mpA[i];
+            if (mp < 0 || amA[i] || bad[mp]) continue;
+            const float* X = pts->pos + 3 * (size_t)mp;
+            float c1[3], c2[3];
+            for (int r = 0; r < 3; r++) c1[r] = gemm3(Aw.R, Aw.t, r, X);
+            for (int r = 0; r < 3; r++) c2[r] = gemm3(sR, t, r, c1);
+            if (c2[2] < 0.0) continue;
+            const float invz = (float)(1.0 / (double)c2[2]);
+            const float x = c2[0] * invz, y = c2[1] * invz;
+            const float u = KF1->fx * x + KF1->cx, v = KF1->fy * y + KF1->cy;   // pKF1's intrinsics
+            if (!kf_in_image(B, u, v)) continue;
+            const float dist3D = norm3f(c2);
+            if (dist3D < 0.8f * geo->min_dist[mp] || dist3D > 1.2f * geo->max_dist[mp]) continue;
+            const int lvl = predict_scale(geo->max_dist[mp], dist3D, logScaleFactor, B->nlevels);
+            pp.add(u, v, th * B->scaleFactors[lvl], lvl, pts->desc + 32 * (size_t)mp, u, v, 0.f, (size_t)i);
+        }
+        if (int e = pp.run(m, B)) return e;
+        for (int i = 0; i < NA; i++) {
+            if (pp.q[i].qd < 0) continue;
+            int bestDist = INT_MAX, bestIdx = -1;
+            for (int k = pp.off[i]; k < pp.off[i + 1]; k++)
+                if (pp.cand[k].y < bestDist) {
+                    bestDist = pp.cand[k].y;
+                    bestIdx = pp.cand[k].x;
+                }
+            if (bestDist <= 100) vn[i] = bestIdx;   // TH_HIGH
+        }
+        return ORB_OK;
+    };
+    std::vector<int> vn1, vn2;
+    if (int e = direction(KF2, P1, sR21, t21, N1, mp1, am1, vn1)) return e;
+    if (int e = direction(KF1, P2, sR12, t12, N2, mp2, am2, vn2)) return e;
+    int nf = 0;
+    for (int i1 = 0; i1 < N1; i1++) {
+        const int idx2 = vn1[i1];
+        if (idx2 >= 0 && vn2[idx2] == i1) {
+            matches12[i1] = idx2;
+            nf++;
+        }
+    }
+    *nfound = nf;
+    return ORB_OK;
 }
 
 }  // extern "C"

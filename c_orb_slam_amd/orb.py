@@ -10,7 +10,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (KP_DTYPE, ORB_E_CAPACITY, OrbGpuError, check, lib, orb_featvec, orb_frame, orb_mappoints, ptr)
+from ._lib import (KP_DTYPE, ORB_E_CAPACITY, OrbGpuError, check, lib, orb_featvec, orb_frame, orb_mappoint_geo, orb_mappoints, ptr)
 
 FRAME_GRID_COLS, FRAME_GRID_ROWS = 64, 48   # Frame.h:37-38
 
@@ -207,6 +207,22 @@ class MapPoints:
         return m
 
 
+class MapPointGeo:
+    """mfMaxDistance, mfMinDistance, GetNormal() of the rows of a MapPoints table."""
+
+    def __init__(self, max_dist, min_dist, normal=None):
+        self.max_dist = np.ascontiguousarray(max_dist, np.float32)
+        self.min_dist = np.ascontiguousarray(min_dist, np.float32)
+        self.normal = None if normal is None else np.ascontiguousarray(normal, np.float32).reshape(-1, 3)
+
+    def cstruct(self):
+        g = orb_mappoint_geo()
+        g.max_dist = self.max_dist.ctypes.data if len(self.max_dist) else None
+        g.min_dist = self.min_dist.ctypes.data if len(self.min_dist) else None
+        g.normal = self.normal.ctypes.data if self.normal is not None and len(self.normal) else None
+        return g
+
+
 class ORBmatcher:
     """ORBmatcher(nnratio=0.6, checkOri=True)  (ORBmatcher.cc:41-43)."""
 
@@ -312,6 +328,53 @@ class ORBmatcher:
                                                              ptr(skip), ptr(kf_angle), C.byref(m), ptr(mx), ptr(mn),
                                                              float(logScaleFactor), float(th), int(ORBdist),
                                                              C.byref(n)), "SearchByProjection_KeyFrame")
+        return n.value
+
+    def SearchByProjection_Sim3(self, KF: Frame, Scw, pts: MapPoints, geo: MapPointGeo, skip, matched,
+                                logScaleFactor, th):
+        """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (ORBmatcher.cc:290-403).
+        matched (KF.N int32, rows of pts or -1) is updated in place; returns nmatches."""
+        assert matched.dtype == np.int32 and matched.flags.c_contiguous and len(matched) == KF.N
+        S = np.ascontiguousarray(Scw, np.float32).reshape(16)
+        skip = np.ascontiguousarray(skip, np.uint8)
+        f, m, g, n = KF.cstruct(), pts.cstruct(), geo.cstruct(), C.c_int()
+        check(self._L.ORBmatcher_SearchByProjection_Sim3(self._h, C.byref(f), ptr(S), C.byref(m), C.byref(g), ptr(skip),
+                                                         float(logScaleFactor), int(th), ptr(matched), C.byref(n)),
+              "SearchByProjection_Sim3")
+        return n.value
+
+    def Fuse(self, KF: Frame, pts: MapPoints, geo: MapPointGeo, skip, logScaleFactor, th=3.0):
+        """Fuse(pKF, vpMapPoints, th) (ORBmatcher.cc:825-975) -> (nFused, best keypoint per point or -1)."""
+        skip = np.ascontiguousarray(skip, np.uint8)
+        best = np.full(max(pts.n, 1), -1, np.int32)
+        f, m, g, n = KF.cstruct(), pts.cstruct(), geo.cstruct(), C.c_int()
+        check(self._L.ORBmatcher_Fuse(self._h, C.byref(f), C.byref(m), C.byref(g), ptr(skip), float(logScaleFactor),
+                                      float(th), ptr(best), C.byref(n)), "Fuse")
+        return n.value, best[:pts.n]
+
+    def Fuse_Sim3(self, KF: Frame, Scw, pts: MapPoints, geo: MapPointGeo, skip, logScaleFactor, th=4.0):
+        """Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (ORBmatcher.cc:977-1100) -> (nFused, best)."""
+        S = np.ascontiguousarray(Scw, np.float32).reshape(16)
+        skip = np.ascontiguousarray(skip, np.uint8)
+        best = np.full(max(pts.n, 1), -1, np.int32)
+        f, m, g, n = KF.cstruct(), pts.cstruct(), geo.cstruct(), C.c_int()
+        check(self._L.ORBmatcher_Fuse_Sim3(self._h, C.byref(f), ptr(S), C.byref(m), C.byref(g), ptr(skip),
+                                           float(logScaleFactor), float(th), ptr(best), C.byref(n)), "Fuse_Sim3")
+        return n.value, best[:pts.n]
+
+    def SearchBySim3(self, KF1: Frame, mp1, KF2: Frame, mp2, pts: MapPoints, geo: MapPointGeo, bad, matches12, s12,
+                     R12, t12, logScaleFactor, th=7.5):
+        """SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (ORBmatcher.cc:1102-1326).
+        matches12 (KF1.N int32: -1 / KF2 keypoint / -2) is updated in place; returns nFound."""
+        assert matches12.dtype == np.int32 and matches12.flags.c_contiguous and len(matches12) == KF1.N
+        mp1, mp2 = np.ascontiguousarray(mp1, np.int32), np.ascontiguousarray(mp2, np.int32)
+        bad = np.ascontiguousarray(bad, np.uint8)
+        R = np.ascontiguousarray(R12, np.float32).reshape(9)
+        t = np.ascontiguousarray(t12, np.float32).reshape(3)
+        f1, f2, m, g, n = KF1.cstruct(), KF2.cstruct(), pts.cstruct(), geo.cstruct(), C.c_int()
+        check(self._L.ORBmatcher_SearchBySim3(self._h, C.byref(f1), ptr(mp1), C.byref(f2), ptr(mp2), C.byref(m),
+                                              C.byref(g), ptr(bad), float(s12), ptr(R), ptr(t), float(logScaleFactor),
+                                              float(th), ptr(matches12), C.byref(n)), "SearchBySim3")
         return n.value
 
     def SearchForInitialization(self, F1: Frame, F2: Frame, prev_matched, windowSize=10):

@@ -249,6 +249,53 @@ int ORBmatcher_SearchForTriangulation(ORBmatcher_h h, const orb_frame* KF1, cons
                                       const float* levelSigma2_2, const float* F12, int bOnlyStereo,
                                       int32_t* pairs, int cap, int* npairs);
 
+/* ---- LocalMapping / LoopClosing projection searches -------------------------------------
+ * Map points are the rows of `pts` (GetWorldPos, GetDescriptor) with their
+ * orb_mappoint_geo (mfMaxDistance, mfMinDistance, GetNormal).  KeyFrame::GetFeaturesInArea
+ * (KeyFrame.cc:569-608, no level filter) and KeyFrame::IsInImage (strict upper bounds)
+ * semantics.  Host pointers only (ORB_E_INVALID in device-pointer mode). */
+typedef struct orb_mappoint_geo {
+    const float* max_dist;     /* MapPoint::mfMaxDistance (n) */
+    const float* min_dist;     /* MapPoint::mfMinDistance (n) */
+    const float* normal;       /* GetNormal() (n x 3) */
+} orb_mappoint_geo;
+
+/* int SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints,
+ *                        vector<MapPoint*>& vpMatched, int th)      ORBmatcher.cc:290-403
+ * pts = vpPoints; skip[i] = isBad() || spAlreadyFound.count(pMP); matched (KF->N, in/out):
+ * vpMatched as row indices of pts (-1 = NULL).  KF: keysUn, desc, grid bounds, intrinsics,
+ * scaleFactors (Tcw unused: the pose is Scw, 4x4 row-major similarity). */
+int ORBmatcher_SearchByProjection_Sim3(ORBmatcher_h h, const orb_frame* KF, const float* Scw,
+                                       const orb_mappoints* pts, const orb_mappoint_geo* geo,
+                                       const uint8_t* skip, float logScaleFactor, int th,
+                                       int32_t* matched, int* nmatches);
+/* int Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th)   825-975
+ * skip[i] = !pMP || isBad() || IsInKeyFrame(pKF).  best[i] (out) = keypoint of pKF the
+ * reference fuses point i with (bestIdx, 951-971) or -1; *nfused = the return value.  The
+ * caller applies 953-969 (Replace / AddObservation) in point order: the selection never
+ * depends on those mutations (no occupancy test in Fuse), so the plan is exact. */
+int ORBmatcher_Fuse(ORBmatcher_h h, const orb_frame* KF, const orb_mappoints* pts,
+                    const orb_mappoint_geo* geo, const uint8_t* skip, float logScaleFactor, float th,
+                    int32_t* best, int* nfused);
+/* int Fuse(KeyFrame* pKF, cv::Mat Scw, const vector<MapPoint*>& vpPoints, float th,
+ *          vector<MapPoint*>& vpReplacePoint)                         977-1100
+ * skip[i] = isBad() || pKF->GetMapPoints().count(pMP); best / nfused as Fuse (the caller
+ * fills vpReplacePoint[i] from pKF->GetMapPoint(best[i]) or adds the observation). */
+int ORBmatcher_Fuse_Sim3(ORBmatcher_h h, const orb_frame* KF, const float* Scw, const orb_mappoints* pts,
+                         const orb_mappoint_geo* geo, const uint8_t* skip, float logScaleFactor, float th,
+                         int32_t* best, int* nfused);
+/* int SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12,
+ *                  const float& s12, const cv::Mat& R12, const cv::Mat& t12, float th)  1102-1326
+ * mp1 (KF1->N) / mp2 (KF2->N): GetMapPointMatches() as rows of pts (-1 = NULL); bad[row] =
+ * isBad().  matches12 (KF1->N, in/out): -1 = NULL, >= 0 = the KF2 keypoint of the matched
+ * point (GetIndexInKeyFrame(pKF2)), -2 = matched to a point not observed in KF2; every new
+ * agreement writes the KF2 keypoint (vpMatches12[i1] = vpMapPoints2[idx2]).  R12: 3x3, t12: 3.
+ * KF1's intrinsics project into both keyframes, as in the reference. */
+int ORBmatcher_SearchBySim3(ORBmatcher_h h, const orb_frame* KF1, const int32_t* mp1, const orb_frame* KF2,
+                            const int32_t* mp2, const orb_mappoints* pts, const orb_mappoint_geo* geo,
+                            const uint8_t* bad, float s12, const float* R12, const float* t12,
+                            float logScaleFactor, float th, int32_t* matches12, int* nfound);
+
 /* Hamming distances for CSR candidate lists (the inner loop of every Search*):
  * query q (descriptor qdesc[q]) against train rows cand[off[q] .. off[q+1]).
  * Writes dist[k] for every candidate k and best/second per query

@@ -265,6 +265,30 @@ typedef struct {
     const float* inv_sigma2;
     float fx, fy, cx, cy, bf;
 } ora_pose_problem;
+/* ---- LocalMapping / LoopClosing projection searches (matchers3.c) ------- */
+/* SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)  ORBmatcher.cc:290-403.
+ * K = fx fy cx cy; skip[i] = isBad || already found; matched: KF->N in/out (point index or -1). */
+int   ora_search_by_projection_sim3(const ora_frame* KF, const float* K, const float* Scw, int np, const float* pos,
+                                    const uint8_t* desc, const float* maxD, const float* minD, const float* normal,
+                                    const uint8_t* skip, float logScaleFactor, int th, int* matched);
+/* Fuse(KeyFrame*, vpMapPoints, th) 825-975: best[i] = KF keypoint to fuse with or -1.
+ * K5 = fx fy cx cy mbf; skip[i] = !pMP || isBad || IsInKeyFrame(pKF). Returns nFused. */
+int   ora_fuse(const ora_frame* KF, const float* Tcw, const float* K5, int np, const float* pos, const uint8_t* desc,
+               const float* maxD, const float* minD, const float* normal, const uint8_t* skip, float logScaleFactor,
+               float th, int* best);
+/* Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint) 977-1100 (skip = isBad || in pKF's map points) */
+int   ora_fuse_sim3(const ora_frame* KF, const float* K4, const float* Scw, int np, const float* pos,
+                    const uint8_t* desc, const float* maxD, const float* minD, const float* normal,
+                    const uint8_t* skip, float logScaleFactor, float th, int* best);
+/* SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) 1102-1326. mp1/mp2: map point of
+ * each keypoint or -1; K = KF1 fx fy cx cy (used for both projections, as the reference);
+ * matches12 (N1 in/out): -1 none, >= 0 KF2 keypoint of the matched point, -2 matched to a
+ * point not in KF2.  Returns nFound (new agreements written as KF2 keypoint indices). */
+int   ora_search_by_sim3(const ora_frame* KF1, const float* T1w, const int* mp1, const ora_frame* KF2,
+                         const float* T2w, const int* mp2, const float* K, const float* pos, const uint8_t* desc,
+                         const float* maxD, const float* minD, const uint8_t* bad, int* matches12, float s12,
+                         const float* R12, const float* t12, float logScaleFactor, float th);
+
 int   ora_pose_optimization(const ora_pose_problem* P, float* Tcw_out, uint8_t* outlier, ora_ba_trace* trace);
 int   ora_ldlt_pivot_solve(double* H, int n, const double* b, double* x);
 double ora_csum(double* v, int n);

@@ -502,3 +502,64 @@ def oracle_pose_optimization(pr):
     n = L.ora_pose_optimization(C.byref(P), ptr(T), ptr(outl), C.byref(tr))
     return dict(Tcw=T.reshape(4, 4), outlier=outl, inliers=n, solve_chi2=np.array(tr.solve_chi2[:tr.n_solves]),
                 trial_chi2=np.array(tr.trial_chi2[:tr.n_trials]), trial_lambda=np.array(tr.trial_lambda[:tr.n_trials]))
+
+
+# ---- LocalMapping / LoopClosing projection searches (oracle/matchers3.c) ----------------
+def _geo_arrays(geo):
+    return _f32(geo.max_dist), _f32(geo.min_dist), _f32(geo.normal if geo.normal is not None else np.zeros((1, 3)))
+
+
+def oracle_search_by_projection_sim3(KF, Scw, pts, geo, skip, matched, logScaleFactor, th):
+    L = lib()
+    vp, i32, f32 = C.c_void_p, C.c_int, C.c_float
+    L.ora_search_by_projection_sim3.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, vp]
+    of = OracleFrame(KF)
+    K = np.array([KF.fx, KF.fy, KF.cx, KF.cy], np.float32)
+    S = _f32(Scw).reshape(16)
+    mx, mn, nrm = _geo_arrays(geo)
+    m = _i32(matched).copy()
+    n = L.ora_search_by_projection_sim3(C.byref(of.s), ptr(K), ptr(S), pts.n, ptr(pts.pos), ptr(pts.desc), ptr(mx),
+                                        ptr(mn), ptr(nrm), ptr(_u8(skip)), float(logScaleFactor), int(th), ptr(m))
+    return n, m
+
+
+def oracle_fuse(KF, pts, geo, skip, logScaleFactor, th):
+    L = lib()
+    vp, i32, f32 = C.c_void_p, C.c_int, C.c_float
+    L.ora_fuse.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, f32, vp]
+    of = OracleFrame(KF)
+    K5 = np.array([KF.fx, KF.fy, KF.cx, KF.cy, KF.bf], np.float32)
+    mx, mn, nrm = _geo_arrays(geo)
+    best = np.full(max(pts.n, 1), -1, np.int32)
+    n = L.ora_fuse(C.byref(of.s), KF.Tcw.ctypes.data, ptr(K5), pts.n, ptr(pts.pos), ptr(pts.desc), ptr(mx), ptr(mn),
+                   ptr(nrm), ptr(_u8(skip)), float(logScaleFactor), float(th), ptr(best))
+    return n, best[:pts.n]
+
+
+def oracle_fuse_sim3(KF, Scw, pts, geo, skip, logScaleFactor, th):
+    L = lib()
+    vp, i32, f32 = C.c_void_p, C.c_int, C.c_float
+    L.ora_fuse_sim3.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, f32, vp]
+    of = OracleFrame(KF)
+    K = np.array([KF.fx, KF.fy, KF.cx, KF.cy], np.float32)
+    S = _f32(Scw).reshape(16)
+    mx, mn, nrm = _geo_arrays(geo)
+    best = np.full(max(pts.n, 1), -1, np.int32)
+    n = L.ora_fuse_sim3(C.byref(of.s), ptr(K), ptr(S), pts.n, ptr(pts.pos), ptr(pts.desc), ptr(mx), ptr(mn), ptr(nrm),
+                        ptr(_u8(skip)), float(logScaleFactor), float(th), ptr(best))
+    return n, best[:pts.n]
+
+
+def oracle_search_by_sim3(KF1, mp1, KF2, mp2, pts, geo, bad, matches12, s12, R12, t12, logScaleFactor, th):
+    L = lib()
+    vp, f32 = C.c_void_p, C.c_float
+    L.ora_search_by_sim3.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, f32, f32]
+    o1, o2 = OracleFrame(KF1), OracleFrame(KF2)
+    K = np.array([KF1.fx, KF1.fy, KF1.cx, KF1.cy], np.float32)
+    mx, mn, _ = _geo_arrays(geo)
+    m12 = _i32(matches12).copy()
+    n = L.ora_search_by_sim3(C.byref(o1.s), KF1.Tcw.ctypes.data, ptr(_i32(mp1)), C.byref(o2.s), KF2.Tcw.ctypes.data,
+                             ptr(_i32(mp2)), ptr(K), ptr(pts.pos), ptr(pts.desc), ptr(mx), ptr(mn), ptr(_u8(bad)),
+                             ptr(m12), float(s12), ptr(_f32(R12).reshape(9)), ptr(_f32(t12).reshape(3)),
+                             float(logScaleFactor), float(th))
+    return n, m12

@@ -116,3 +116,64 @@ def test_searches_refuse_device_pointers(gpu):
     with pytest.raises(OrbGpuError):
         m.SearchByProjection_KeyFrame(c["F"], c["cur_mp"].copy(), c["kf_mp"], c["skip"], c["kf_angle"], c["mps"],
                                       c["max_dist"], c["min_dist"], c["logScaleFactor"], 10, 100)
+
+
+# ---- LocalMapping / LoopClosing projection searches (ORBmatcher.cc:290-403, 825-1326) ----
+@pytest.mark.parametrize("seed,scale,th", [(0, 1.3, 10), (3, 0.7, 10), (5, 1.0, 5)])
+def test_search_by_projection_sim3(gpu, seed, scale, th):
+    c = sc.loop_case(seed, scale=scale)
+    m = gpu.ORBmatcher(0.75, True)
+    matched = c["matched"].copy()
+    n = m.SearchByProjection_Sim3(c["KF"], c["Scw"], c["pts"], c["geo"], c["skip"], matched, c["logScaleFactor"], th)
+    on, om = oracle_lib.oracle_search_by_projection_sim3(c["KF"], c["Scw"], c["pts"], c["geo"], c["skip"],
+                                                         c["matched"], c["logScaleFactor"], th)
+    assert n == on and np.array_equal(matched, om)
+    assert n > 100, n
+
+
+@pytest.mark.parametrize("seed,stereo_frac,th", [(0, 0.5, 3.0), (4, 0.0, 3.0), (6, 1.0, 5.0)])
+def test_fuse(gpu, seed, stereo_frac, th):
+    c = sc.loop_case(seed, stereo_frac=stereo_frac)
+    m = gpu.ORBmatcher(0.6, True)
+    n, best = m.Fuse(c["KF"], c["pts"], c["geo"], c["skip"], c["logScaleFactor"], th)
+    on, ob = oracle_lib.oracle_fuse(c["KF"], c["pts"], c["geo"], c["skip"], c["logScaleFactor"], th)
+    assert n == on and np.array_equal(best, ob)
+    assert n > 50, n
+
+
+@pytest.mark.parametrize("seed,scale", [(1, 1.3), (2, 0.5)])
+def test_fuse_sim3(gpu, seed, scale):
+    c = sc.loop_case(seed, scale=scale)
+    m = gpu.ORBmatcher(0.8, True)
+    n, best = m.Fuse_Sim3(c["KF"], c["Scw"], c["pts"], c["geo"], c["skip"], c["logScaleFactor"], 4.0)
+    on, ob = oracle_lib.oracle_fuse_sim3(c["KF"], c["Scw"], c["pts"], c["geo"], c["skip"], c["logScaleFactor"], 4.0)
+    assert n == on and np.array_equal(best, ob)
+    assert n > 100, n
+
+
+@pytest.mark.parametrize("seed,s12", [(0, 1.02), (7, 0.9), (8, 1.0)])
+def test_search_by_sim3(gpu, seed, s12):
+    s = sc.sim3_case(seed, s12=s12)
+    m = gpu.ORBmatcher(0.75, True)
+    m12 = s["m12"].copy()
+    n = m.SearchBySim3(s["KF1"], s["mp1"], s["KF2"], s["mp2"], s["pts"], s["geo"], s["bad"], m12, s["s12"],
+                       s["R12"], s["t12"], s["logScaleFactor"], 7.5)
+    on, om = oracle_lib.oracle_search_by_sim3(s["KF1"], s["mp1"], s["KF2"], s["mp2"], s["pts"], s["geo"], s["bad"],
+                                              s["m12"], s["s12"], s["R12"], s["t12"], s["logScaleFactor"], 7.5)
+    assert n == on and np.array_equal(m12, om)
+    assert n > 50, n
+
+
+def test_projection_searches_empty_inputs(gpu):
+    from c_orb_slam_amd.orb import MapPointGeo, MapPoints
+    c = sc.loop_case(0)
+    m = gpu.ORBmatcher(0.75, True)
+    empty = MapPoints(np.zeros((0, 3)), np.zeros((0, 32)), np.zeros(0))
+    eg = MapPointGeo(np.zeros(0), np.zeros(0), np.zeros((0, 3)))
+    matched = c["matched"].copy()
+    assert m.SearchByProjection_Sim3(c["KF"], c["Scw"], empty, eg, np.zeros(0), matched, c["logScaleFactor"], 10) == 0
+    assert np.array_equal(matched, c["matched"])
+    assert m.Fuse(c["KF"], empty, eg, np.zeros(0), c["logScaleFactor"], 3.0)[0] == 0
+    allskip = np.ones(c["pts"].n, np.uint8)
+    n, best = m.Fuse_Sim3(c["KF"], c["Scw"], c["pts"], c["geo"], allskip, c["logScaleFactor"], 4.0)
+    assert n == 0 and (best == -1).all()

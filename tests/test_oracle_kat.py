@@ -342,3 +342,23 @@ def test_oracle_ldlt_pivot_solve():
         np.testing.assert_allclose(x, np.linalg.solve(H, b), rtol=1e-9, atol=1e-12)
     Hn = -np.eye(6)
     assert L.ora_ldlt_pivot_solve(ptr(Hn), 6, ptr(np.ones(6)), ptr(np.zeros(6))) == 0
+
+
+def test_oracle_projection_searches_sanity():
+    """matchers3.c on the loop-closing cases: Sim3-projected map points of keyframe 0 land on
+    keyframe 1 keypoints carrying the same descriptor (the rotation-only synthetic motion keeps
+    most of them), and SearchBySim3's two directions agree on a large set."""
+    import search_cases as sc
+    c = sc.loop_case(0)
+    n, m = oracle_lib.oracle_search_by_projection_sim3(c["KF"], c["Scw"], c["pts"], c["geo"], c["skip"],
+                                                       c["matched"], c["logScaleFactor"], 10)
+    new = (m >= 0) & (c["matched"] < 0)
+    assert n == new.sum() and n > 300
+    assert not c["skip"][m[new]].any()
+    nf, best = oracle_lib.oracle_fuse(c["KF"], c["pts"], c["geo"], c["skip"], c["logScaleFactor"], 3.0)
+    assert nf == (best >= 0).sum() and nf > 100
+    s = sc.sim3_case(0)
+    nfound, m12 = oracle_lib.oracle_search_by_sim3(s["KF1"], s["mp1"], s["KF2"], s["mp2"], s["pts"], s["geo"],
+                                                   s["bad"], s["m12"], s["s12"], s["R12"], s["t12"],
+                                                   s["logScaleFactor"], 7.5)
+    assert nfound == ((m12 >= 0) & (s["m12"] == -1)).sum() and nfound > 200
