@@ -139,6 +139,7 @@ def main():
         return f
 
     stage_acc = {}
+    phase_acc = {}
     pose_inl = []
     kernel_ms = []   # k_fast_cells duration per step (HIP events on the extractor streams)
 
@@ -177,15 +178,18 @@ def main():
         # Frame(imLeft, imRight): two ORBextractor calls (Frame.cc:78-81), then ComputeStereoMatches
         # the two extractors run concurrently on their own streams / host octree pools, like the
         # reference's two extractor threads per stereo frame
+        t0 = time.perf_counter()
         fR = pool.submit(exR.extract_device, d_R.data_ptr(), B, W, H, W, W * H, d_kpsR.data_ptr(),
                          d_descR.data_ptr(), cap)
         nL = exL.extract_device(d_L.data_ptr(), B, W, H, W, W * H, d_kps.data_ptr(), d_desc.data_ptr(), cap)
         nR = fR.result()
+        t1 = time.perf_counter()
         nL = np.ascontiguousarray(nL, np.int32)
         nR = np.ascontiguousarray(nR, np.int32)
         check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, exL._h, exR._h, B, ptr(nL), s_kL, s_dL, ptr(nR), s_kR,
                                                       s_dR, float(mbf), float(mb), s_uR, s_dep, ptr(nst)),
               "ComputeStereoMatches batch")
+        t2 = time.perf_counter()
         # UpdateLastFrame-style map points of the last frame from its stereo depth: X = d K^-1 [u v 1]
         x, y = kp_f[..., 0], kp_f[..., 1]
         d_mp_pos[..., 0] = (x - float(cx)) / float(fx) * d_depth
@@ -202,6 +206,7 @@ def main():
         check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, P, curs, a_cur_mp, lasts, a_last_kps, a_last_mp,
                                                               a_last_out, mps, 7.0, 0, ptr(nm)),
               "SearchByProjection batch")
+        t3 = time.perf_counter()
         # Optimizer::PoseOptimization(&mCurrentFrame) (Tracking.cc:887) on the matched map points
         cm = d_cur_mp[1:]
         d_has.copy_(cm >= 0)
@@ -214,6 +219,9 @@ def main():
         torch.cuda.current_stream().synchronize()
         check(L.Optimizer_PoseOptimization_batch_device(P, pprobs, a_Tout, a_poutl, ptr(ninl)),
               "PoseOptimization batch")
+        t4 = time.perf_counter()
+        for k, v in (("extract_LR", t1 - t0), ("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3)):
+            phase_acc[k] = phase_acc.get(k, 0.0) + v * 1e3
         tl, tr = exL.last_timings(), exR.last_timings()
         for k in tl:
             stage_acc[k] = stage_acc.get(k, 0.0) + tl[k] + tr[k]
@@ -225,6 +233,7 @@ def main():
     for _ in range(args.warmup):
         step()
     stage_acc.clear()
+    phase_acc.clear()
     kernel_ms.clear()
     pose_inl.clear()
     if world > 1:
@@ -298,7 +307,8 @@ def main():
             "matches_per_s": round(tot_match / dt, 1), "stereo_matches_per_s": round(tot_stereo / dt, 1),
             "keypoints_per_image": round(tot_kp / (2 * frames_total), 1),
             "pose_inliers_per_frame": round(float(np.sum(pose_inl)) / max(len(pose_inl) * P, 1), 1),
-            "stage_ms_per_step": stage_ms, "roofline": roof, "cpu_baseline": cpu, "local_ba": ba,
+            "stage_ms_per_step": stage_ms,
+            "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}, "roofline": roof, "cpu_baseline": cpu, "local_ba": ba,
             "global_ba": gba,
         }
         json_out.write(json.dumps(out) + "\n")

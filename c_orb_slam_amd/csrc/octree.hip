@@ -1,0 +1,449 @@
+// octree.hip -- gfx950 ORBextractor::DistributeOctTree (reference src/ORBextractor.cc:481-763).
+//
+// One workgroup per (image, level) job, all jobs of a batch in one launch, straight after
+// k_compact: no host round trip between FAST and the descriptor kernel.
+//
+// The std::list algorithm is restated over two observations:
+//  * keys inside a node are always a subsequence of the input order, and the only
+//    order-dependent use of that order is "first key wins response ties" -- so per-node key
+//    sets are kept order-free (node id per key, or an unordered arena slice) and the tie is
+//    resolved as (max response, min input index);
+//  * the phase-1 loop (divide every node with > 1 key, children pushed to the FRONT in
+//    n1..n4 order, parents erased) is a pure function of the list order, so the new list is
+//    [children in reverse push order] ++ [the 1-key nodes in old order], built with block
+//    scans; node id == list position.
+// Phase 2 (size + 3 * nToExpand > N: divide the previous round's nodes largest-first,
+// stop at N) is the reference's sequential loop: an index-linked list, one divide at a time
+// with the workgroup partitioning the node's arena slice.  The reference sorts
+// pair<int, ExtractorNode*> and so breaks size ties by heap address; this (like the host
+// oracle) breaks them by node creation order -- DESIGN.md Appendix, quirk Q1.
+#include "octree.hpp"
+
+namespace orbgpu {
+
+constexpr int OCT_T = 256;
+
+struct OctShared {
+    int16_t x0[2 * kOctNMax], y0[2 * kOctNMax], x1[2 * kOctNMax], y1[2 * kOctNMax];
+    uint16_t cnt[2 * kOctNMax], seq[2 * kOctNMax], kbeg[2 * kOctNMax];
+    int16_t prv[2 * kOctNMax], nxt[2 * kOctNMax];
+    int ia[4 * kOctNMax];          // counters (phase 1 per virtual child, phase 2 per quadrant); best keys
+    uint16_t vpos[4 * kOctNMax];   // virtual child -> push index -> list position
+    uint16_t er[kOctNMax], eidx[kOctNMax];
+    uint16_t vs[kOctNMax], vs2[kOctNMax];
+    uint16_t knode[kOctKMax], arena[kOctKMax], tmp[kOctKMax];
+    int wsum[OCT_T / 64];
+    int head, size, nfree, m, newm, seqctr, flag;
+};
+
+// Block-wide exclusive scan of flag(i) over i < n; put(i, rank) for flagged i.  Returns the
+// total.  Every thread of the block calls it (two barriers).
+template <class Flag, class Put>
+__device__ __forceinline__ int oct_scan(int n, Flag flag, Put put, int* wsum) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int per = (n + OCT_T - 1) / OCT_T;
+    const int a = min(n, t * per), e = min(n, a + per);
+    int local = 0;
+    for (int i = a; i < e; i++) local += flag(i) ? 1 : 0;
+    int incl = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int off = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < OCT_T / 64; w++) {
+        const int s = wsum[w];
+        if (w < wid) off += s;
+        total += s;
+    }
+    int ex = off + incl - local;
+    for (int i = a; i < e; i++)
+        if (flag(i)) put(i, ex++);
+    __syncthreads();
+    return total;
+}
+
+__device__ __forceinline__ void oct_child_rect(const OctShared& S, int p, int q, int& a0, int& b0, int& a1, int& b1) {
+    const int X0 = S.x0[p], Y0 = S.y0[p], X1 = S.x1[p], Y1 = S.y1[p];
+    const int halfX = (int)ceilf((float)(X1 - X0) / 2), halfY = (int)ceilf((float)(Y1 - Y0) / 2);
+    const int mx = X0 + halfX, my = Y0 + halfY;
+    a0 = (q & 1) ? mx : X0;
+    a1 = (q & 1) ? X1 : mx;
+    b0 = (q & 2) ? my : Y0;
+    b1 = (q & 2) ? Y1 : my;
+}
+
+// ExtractorNode::DivideNode child of a key: n1 (0) / n2 (1) / n3 (2) / n4 (3)
+__device__ __forceinline__ int oct_quadrant(const OctShared& S, int p, uint32_t pk) {
+    const int halfX = (int)ceilf((float)(S.x1[p] - S.x0[p]) / 2), halfY = (int)ceilf((float)(S.y1[p] - S.y0[p]) / 2);
+    const int mx = S.x0[p] + halfX, my = S.y0[p] + halfY;
+    const int x = (int)(pk & 0xfff), y = (int)((pk >> 12) & 0xfff);
+    return (x < mx) ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
+}
+
+__device__ __forceinline__ int oct_best_key(uint32_t pk, int k) { return (int)((pk >> 24) << 16) | (0xffff - k); }
+
+__global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ packed, const int* __restrict__ hdr,
+                                                 int nlevels, const OctLevelDev* __restrict__ lv,
+                                                 uint32_t* __restrict__ jobsel, int* __restrict__ jobcnt, int jcap,
+                                                 uint16_t* __restrict__ gscratch, size_t gstride, int* __restrict__ err) {
+    __shared__ OctShared S;
+    const int job = blockIdx.x, b = job / nlevels, l = job - b * nlevels;
+    const int tid = threadIdx.x;
+    const int* H = hdr + (size_t)b * (nlevels + 2);
+    const int base = H[nlevels + 1];
+    int loff = 0;
+    for (int k = 0; k < l; k++) loff += H[1 + k];
+    const int n = H[1 + l];
+    if (base < 0 || n <= 0 || n > 0xffff) {
+        if (tid == 0) {
+            jobcnt[job] = 0;
+            if (base < 0) atomicOr(err, 1);   // k_compact: packed capacity
+            else if (n > 0xffff) atomicOr(err, 2);
+        }
+        return;
+    }
+    const uint32_t* src = packed + base + loff;
+    const OctLevelDev L = lv[l];
+    const int N = L.N;
+    // keys: node / arena / scratch indices in LDS, or in the global scratch for big jobs
+    uint16_t* knode = S.knode;
+    uint16_t* arena = S.arena;
+    uint16_t* tmp = S.tmp;
+    if (n > kOctKMax) {
+        knode = gscratch + (size_t)base + loff;
+        arena = knode + gstride;
+        tmp = arena + gstride;
+    }
+    // ---- initial nodes (ORBextractor.cc:543-585)
+    const int W = L.maxX - L.minX, Hh = L.maxY - L.minY;
+    const int nIni = (int)roundf((float)W / (float)Hh);
+    if (nIni < 1 || nIni > kOctNMax) {
+        if (tid == 0) {
+            jobcnt[job] = 0;
+            atomicOr(err, 4);
+        }
+        return;
+    }
+    const float hX = (float)W / (float)nIni;
+    for (int i = tid; i < nIni; i += OCT_T) S.ia[i] = 0;
+    __syncthreads();
+    for (int k = tid; k < n; k += OCT_T) {
+        const uint32_t pk = src[k];
+        int ib = (int)((float)(pk & 0xfff) / hX);
+        ib = min(ib, nIni - 1);
+        knode[k] = (uint16_t)ib;
+        atomicAdd(&S.ia[ib], 1);
+    }
+    __syncthreads();
+    // list = non-empty initial nodes in order (buffer 0), node id == position
+    int cur = 0;
+    int Sz = oct_scan(
+        nIni, [&](int i) { return S.ia[i] > 0; },
+        [&](int i, int r) {
+            S.x0[r] = (int16_t)(int)(hX * (float)i);
+            S.x1[r] = (int16_t)(int)(hX * (float)(i + 1));
+            S.y0[r] = 0;
+            S.y1[r] = (int16_t)Hh;
+            S.cnt[r] = (uint16_t)S.ia[i];
+            S.seq[r] = (uint16_t)i;
+            S.er[i] = (uint16_t)r;
+        },
+        S.wsum);
+    for (int k = tid; k < n; k += OCT_T) knode[k] = S.er[knode[k]];
+    int seqbase = nIni;
+    int phase2 = 0, m = 0;
+    __syncthreads();
+    // ---- phase 1 (ORBextractor.cc:594-673)
+    for (;;) {
+        const int prevSize = Sz;
+        const int nE = oct_scan(
+            Sz, [&](int i) { return S.cnt[cur + i] > 1; },
+            [&](int i, int r) {
+                S.er[i] = (uint16_t)r;
+                S.eidx[r] = (uint16_t)i;
+            },
+            S.wsum);
+        if (nE == 0) break;   // every node holds one key: size == prevSize
+        for (int v = tid; v < 4 * nE; v += OCT_T) S.ia[v] = 0;
+        __syncthreads();
+        for (int k = tid; k < n; k += OCT_T) {
+            const int p = knode[k];
+            if (S.cnt[cur + p] > 1) {
+                const int v = 4 * S.er[p] + oct_quadrant(S, cur + p, src[k]);
+                tmp[k] = (uint16_t)v;
+                atomicAdd(&S.ia[v], 1);
+            } else {
+                tmp[k] = 0xffff;
+            }
+        }
+        __syncthreads();
+        // push order of the non-empty children: parents in list order, n1..n4
+        const int nC = oct_scan(
+            4 * nE, [&](int v) { return S.ia[v] > 0; }, [&](int v, int r) { S.vpos[v] = (uint16_t)r; }, S.wsum);
+        const int nb = kOctNMax - cur;
+        // 1-key nodes keep their relative order behind the children
+        const int nNM = oct_scan(
+            Sz, [&](int i) { return S.cnt[cur + i] == 1; }, [&](int i, int r) { S.er[i] = (uint16_t)(nC + r); },
+            S.wsum);
+        if (nC + nNM > kOctNMax) {
+            if (tid == 0) {
+                jobcnt[job] = 0;
+                atomicOr(err, 8);
+            }
+            return;
+        }
+        for (int v = tid; v < 4 * nE; v += OCT_T) {
+            const int c = S.ia[v];
+            if (c > 0) {
+                const int t = S.vpos[v], pos = nC - 1 - t, parent = cur + S.eidx[v >> 2];
+                int a0, b0, a1, b1;
+                oct_child_rect(S, parent, v & 3, a0, b0, a1, b1);
+                S.x0[nb + pos] = (int16_t)a0;
+                S.y0[nb + pos] = (int16_t)b0;
+                S.x1[nb + pos] = (int16_t)a1;
+                S.y1[nb + pos] = (int16_t)b1;
+                S.cnt[nb + pos] = (uint16_t)c;
+                S.seq[nb + pos] = (uint16_t)(seqbase + t);
+                S.vpos[v] = (uint16_t)pos;
+            }
+        }
+        for (int i = tid; i < Sz; i += OCT_T)
+            if (S.cnt[cur + i] == 1) {
+                const int pos = S.er[i];
+                S.x0[nb + pos] = S.x0[cur + i];
+                S.y0[nb + pos] = S.y0[cur + i];
+                S.x1[nb + pos] = S.x1[cur + i];
+                S.y1[nb + pos] = S.y1[cur + i];
+                S.cnt[nb + pos] = 1;
+                S.seq[nb + pos] = S.seq[cur + i];
+            }
+        __syncthreads();
+        // vSizeAndPointerToNode: children with > 1 key, push order
+        const int nToExpand = oct_scan(
+            4 * nE, [&](int v) { return S.ia[v] > 1; }, [&](int v, int r) { S.vs[r] = (uint16_t)S.vpos[v]; },
+            S.wsum);
+        for (int k = tid; k < n; k += OCT_T) {
+            const int v = tmp[k];
+            knode[k] = v != 0xffff ? S.vpos[v] : S.er[knode[k]];
+        }
+        seqbase += nC;
+        cur = nb;
+        Sz = nC + nNM;
+        __syncthreads();
+        if (Sz >= N || Sz == prevSize) break;
+        if (Sz + nToExpand * 3 > N) {
+            phase2 = 1;
+            m = nToExpand;
+            break;
+        }
+    }
+    if (phase2) {
+        // ---- phase 2 (ORBextractor.cc:673-738): arena slices, linked list, largest first
+        const int nb = kOctNMax - cur;
+        // kbeg = exclusive scan of cnt in list order
+        {
+            // small serial scan by thread 0 (Sz <= kOctNMax)
+            if (tid == 0) {
+                int acc = 0;
+                for (int i = 0; i < Sz; i++) {
+                    S.kbeg[cur + i] = (uint16_t)acc;
+                    acc += S.cnt[cur + i];
+                    S.ia[i] = 0;
+                    S.prv[cur + i] = (int16_t)(i > 0 ? cur + i - 1 : -1);
+                    S.nxt[cur + i] = (int16_t)(i + 1 < Sz ? cur + i + 1 : -1);
+                }
+                S.head = Sz > 0 ? cur : -1;
+                S.size = Sz;
+                S.nfree = nb;
+                S.seqctr = seqbase;
+                S.m = m;
+                S.flag = 0;
+            }
+            for (int i = tid; i < m; i += OCT_T) S.vs[i] = (uint16_t)(cur + S.vs[i]);
+            __syncthreads();
+            for (int k = tid; k < n; k += OCT_T) {
+                const int p = knode[k];
+                arena[S.kbeg[cur + p] + atomicAdd(&S.ia[p], 1)] = (uint16_t)k;
+            }
+            __syncthreads();
+        }
+        for (;;) {
+            const int prevSize = S.size;
+            const int mm = S.m;
+            // sort ascending by (size, creation order): rank sort, keys unique
+            for (int i = tid; i < mm; i += OCT_T) {
+                const int id = S.vs[i];
+                const uint32_t ki = ((uint32_t)S.cnt[id] << 16) | S.seq[id];
+                int r = 0;
+                for (int j = 0; j < mm; j++) {
+                    const int jd = S.vs[j];
+                    const uint32_t kj = ((uint32_t)S.cnt[jd] << 16) | S.seq[jd];
+                    r += kj < ki ? 1 : 0;
+                }
+                S.vs2[r] = (uint16_t)id;
+            }
+            if (tid == 0) S.newm = 0;
+            if (tid < 12) S.ia[tid] = 0;
+            __syncthreads();
+            for (int j = mm - 1; j >= 0; j--) {
+                const int p = S.vs2[j];
+                const int kb = S.kbeg[p], kc = S.cnt[p];
+                for (int i = tid; i < kc; i += OCT_T) {
+                    const int k = arena[kb + i];
+                    const int q = oct_quadrant(S, p, src[k]);
+                    tmp[kb + i] = (uint16_t)k;
+                    knode[kb + i] = (uint16_t)q;
+                    atomicAdd(&S.ia[q], 1);
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    int start = kb;
+                    for (int q = 0; q < 4; q++) {
+                        const int c = S.ia[q];
+                        S.ia[4 + q] = start;
+                        S.ia[8 + q] = 0;
+                        if (c > 0) {
+                            const int id = S.nfree++;
+                            if (S.nfree > 2 * kOctNMax || id == cur) S.flag = 1;
+                            if (!S.flag) {
+                                int a0, b0, a1, b1;
+                                oct_child_rect(S, p, q, a0, b0, a1, b1);
+                                S.x0[id] = (int16_t)a0;
+                                S.y0[id] = (int16_t)b0;
+                                S.x1[id] = (int16_t)a1;
+                                S.y1[id] = (int16_t)b1;
+                                S.cnt[id] = (uint16_t)c;
+                                S.seq[id] = (uint16_t)(S.seqctr++);
+                                S.kbeg[id] = (uint16_t)start;
+                                // lNodes.push_front
+                                S.prv[id] = -1;
+                                S.nxt[id] = (int16_t)S.head;
+                                if (S.head >= 0) S.prv[S.head] = (int16_t)id;
+                                S.head = id;
+                                S.size++;
+                                if (c > 1) S.vs[S.newm++] = (uint16_t)id;
+                            }
+                        }
+                        start += c;
+                    }
+                    // lNodes.erase(parent)
+                    const int pp = S.prv[p], pn = S.nxt[p];
+                    if (pp >= 0) S.nxt[pp] = (int16_t)pn; else S.head = pn;
+                    if (pn >= 0) S.prv[pn] = (int16_t)pp;
+                    S.size--;
+                    S.ia[0] = S.ia[1] = S.ia[2] = S.ia[3] = 0;
+                }
+                __syncthreads();
+                if (S.flag) {
+                    if (tid == 0) {
+                        jobcnt[job] = 0;
+                        atomicOr(err, 8);
+                    }
+                    return;
+                }
+                for (int i = tid; i < kc; i += OCT_T) {
+                    const int q = knode[kb + i];
+                    arena[S.ia[4 + q] + atomicAdd(&S.ia[8 + q], 1)] = tmp[kb + i];
+                }
+                __syncthreads();
+                if (S.size >= N) break;
+            }
+            if (S.size >= N || S.size == prevSize) break;
+            if (tid == 0) S.m = S.newm;
+            __syncthreads();
+        }
+        // final list order, then the best key of each node over its slice
+        if (tid == 0) {
+            int i = 0;
+            for (int id = S.head; id >= 0 && i < 2 * kOctNMax; id = S.nxt[id]) S.vpos[i++] = (uint16_t)id;
+            S.size = i;
+        }
+        __syncthreads();
+        const int sz = S.size;
+        if (sz > jcap) {
+            if (tid == 0) {
+                jobcnt[job] = 0;
+                atomicOr(err, 16);
+            }
+            return;
+        }
+        for (int i = tid; i < sz; i += OCT_T) {
+            const int id = S.vpos[i];
+            const int kb = S.kbeg[id], kc = S.cnt[id];
+            int best = -1, bk = 0;
+            for (int t = 0; t < kc; t++) {
+                const int k = arena[kb + t];
+                const int v = oct_best_key(src[k], k);
+                if (v > best) {
+                    best = v;
+                    bk = k;
+                }
+            }
+            jobsel[(size_t)job * jcap + i] = src[bk];
+        }
+        if (tid == 0) jobcnt[job] = sz;
+        return;
+    }
+    // ---- phase 1 finished: list = positions 0..Sz-1 of buffer `cur`
+    if (Sz > jcap) {
+        if (tid == 0) {
+            jobcnt[job] = 0;
+            atomicOr(err, 16);
+        }
+        return;
+    }
+    for (int i = tid; i < Sz; i += OCT_T) S.ia[i] = -1;
+    __syncthreads();
+    for (int k = tid; k < n; k += OCT_T) atomicMax(&S.ia[knode[k]], oct_best_key(src[k], k));
+    __syncthreads();
+    for (int i = tid; i < Sz; i += OCT_T) {
+        const int k = 0xffff - (S.ia[i] & 0xffff);
+        jobsel[(size_t)job * jcap + i] = src[k];
+    }
+    if (tid == 0) jobcnt[job] = Sz;
+}
+
+// Per image: level-major concatenation of the job lists -> (packed, b<<20 | l<<16 | k) at
+// sel[b * selcap + k], n_out[b] (the reference's allKeypoints order, ORBextractor.cc:1065-1101).
+__global__ void __launch_bounds__(64) k_sel_build(const uint32_t* __restrict__ jobsel, const int* __restrict__ jobcnt,
+                                                  int nlevels, int jcap, int cap, int2* __restrict__ sel, int selcap,
+                                                  int* __restrict__ nout, int* __restrict__ err) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const int c = lane < nlevels ? jobcnt[b * nlevels + lane] : 0;
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int total = __shfl(incl, 63, 64);
+    if (lane == 0) {
+        nout[b] = total;
+        if (total > cap || total > selcap) atomicOr(err, 1);
+    }
+    if (total > cap || total > selcap) return;
+    for (int l = 0; l < nlevels; l++) {
+        const int cl = __shfl(c, l, 64), off = __shfl(incl - c, l, 64);
+        const uint32_t* js = jobsel + (size_t)(b * nlevels + l) * jcap;
+        for (int i = lane; i < cl; i += 64)
+            sel[(size_t)b * selcap + off + i] = make_int2((int)js[i], (b << 20) | (l << 16) | (off + i));
+    }
+}
+
+int octree_launch(const uint32_t* packed, const int* hdr, int B, int nlevels, const OctLevelDev* lv, uint32_t* jobsel,
+                  int* jobcnt, int jcap, uint16_t* gscratch, size_t gstride, int cap, int2* sel, int selcap, int* nout,
+                  int* err, hipStream_t s) {
+    hipLaunchKernelGGL(k_octree, dim3(B * nlevels), dim3(OCT_T), 0, s, packed, hdr, nlevels, lv, jobsel, jobcnt, jcap,
+                       gscratch, gstride, err);
+    hipLaunchKernelGGL(k_sel_build, dim3(B), dim3(64), 0, s, (const uint32_t*)jobsel, (const int*)jobcnt, nlevels,
+                       jcap, cap, sel, selcap, nout, err);
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace orbgpu

@@ -186,16 +186,52 @@ __device__ __forceinline__ int fast_score_lds(const uint8_t* p, int ld) {
     return max(A, B) - 1;
 }
 
-constexpr int FC_LD = 72;      // LDS row pitch of the cell ROI
+constexpr int FC_LD = 76;      // LDS row pitch of the cell ROI (19 dwords: odd bank stride)
 constexpr int FC_MAXR = 70;    // max ROI rows/cols supported (wCell/hCell <= 64)
 
+// Necessary condition for FAST-9 at threshold t (S >= t): a 9-arc contains two consecutive
+// compass points (0,4), (4,8), (8,12) or (12,0), all brighter than v+t or all darker than v-t.
+__device__ __forceinline__ bool fast_pretest(const uint8_t* p, int ld, int t) {
+    const int v = p[0];
+    const int a = p[3 * ld], b = p[3], c = p[-3 * ld], d = p[-3];
+    const bool da = v - a > t, db = v - b > t, dc = v - c > t, dd = v - d > t;
+    const bool ba = a - v > t, bb = b - v > t, bc = c - v > t, bd = d - v > t;
+    return (da && db) || (db && dc) || (dc && dd) || (dd && da) || (ba && bb) || (bb && bc) || (bc && bd) ||
+           (bd && ba);
+}
+
+// Exclusive scan by wave 0 of the popcounts of masks[0..n) (n <= 64) into off[0..n], off[64] = total.
+__device__ __forceinline__ void mask_scan64(const uint64_t* masks, int n, int* off, int lane) {
+    const int cnt = lane < n ? (int)__popcll(masks[lane]) : 0;
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    off[lane] = incl - cnt;
+    if (lane == 63) off[64] = incl;
+}
+
+// One workgroup (4 waves) per (cell, image); every pixel loop is division-free.
+//   stage    ROI rows as aligned dwords into LDS (3 rows per wave instruction)
+//   pretest  FAST-9 necessary condition at min(iniTh, minTh) per detection pixel, two rows per
+//            wave instruction when the cell is <= 32 columns wide; per-row survivor masks
+//   list     survivors in raster order (row-count scan), ~10 % of the pixels
+//   score    OpenCV cornerScore<16> for the list only (pixels failing the pretest score < th)
+//   NMS      list entries: keep = S >= th && S > every 8-neighbour's (S >= th ? S : 0);
+//            kept entries compacted in list (= raster) order by a chunk-count scan.
 __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ pyr, size_t img_bytes,
                                                     const CellDesc* __restrict__ cells, int iniTh, int minTh,
                                                     uint32_t* __restrict__ slots, size_t slots_per_image,
                                                     int* __restrict__ counts, int ncells) {
-    __shared__ uint8_t s_img[FC_MAXR * FC_LD];
-    __shared__ uint8_t s_sc[FC_MAXR * FC_LD];
-    __shared__ int s_wave[4];
+    __shared__ uint32_t s_img32[FC_MAXR * FC_LD / 4];
+    __shared__ uint32_t s_sc32[FC_MAXR * FC_LD / 4];
+    __shared__ uint16_t s_list[64 * 64];
+    __shared__ uint64_t s_mask[64];
+    __shared__ int s_off[65];
+    uint8_t* s_img = reinterpret_cast<uint8_t*>(s_img32);
+    uint8_t* s_sc = reinterpret_cast<uint8_t*>(s_sc32);
     const CellDesc cd = cells[blockIdx.x];
     const int b = blockIdx.y;
     const int rows = cd.r1 - cd.r0, cols = cd.c1 - cd.c0;
@@ -205,32 +241,69 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
         if (tid == 0) *cnt_out = 0;
         return;
     }
+    // ROI rows staged as aligned dwords: pixel (r, c) sits at LDS byte r*FC_LD + mis + c
     const uint8_t* P = pyr + (size_t)b * img_bytes + cd.lvl_off + (size_t)(kEdge + cd.r0) * cd.pitch + kEdge + cd.c0;
-    for (int i = tid; i < rows * cols; i += 256) {
-        const int r = i / cols, c = i - r * cols;
-        s_img[r * FC_LD + c] = P[(size_t)r * cd.pitch + c];
-        s_sc[r * FC_LD + c] = 0;
+    const int mis = (int)((uintptr_t)P & 3);
+    const uint32_t* P32 = reinterpret_cast<const uint32_t*>(P - mis);
+    constexpr int ldw = FC_LD / 4;
+    const int wpr = (cols + mis + 3) >> 2, pw = cd.pitch >> 2;
+    {
+        const int rr = lane / ldw, w = lane - rr * ldw;   // 3 rows x 19 dwords per wave instruction
+        for (int r0 = wid * 3; r0 < rows; r0 += 12) {
+            const int r = r0 + rr;
+            if (rr < 3 && r < rows && w < wpr) s_img32[r * ldw + w] = P32[(size_t)r * pw + w];
+        }
+    }
+    for (int i = tid; i < rows * ldw; i += 256) s_sc32[i] = 0u;
+    __syncthreads();
+    const int dr = rows - 6, dc = cols - 6;
+    const int tp = min(iniTh, minTh);
+    // lane -> (row slot, column): two rows per instruction for cells <= 32 columns
+    const bool two = dc <= 32;
+    const int sub = two ? (lane >> 5) : 0, col = two ? (lane & 31) : lane, rstep = two ? 2 : 1;
+    const bool col_ok = col < dc;
+    const int c = 3 + col;
+    for (int rb = wid * rstep; rb < dr; rb += 4 * rstep) {
+        const int i = rb + sub;
+        const bool pass = col_ok && i < dr && (tp < 1 || fast_pretest(&s_img[(3 + i) * FC_LD + mis + c], FC_LD, tp));
+        const uint64_t m = __ballot(pass);
+        if (lane == 0) {
+            if (two) {
+                s_mask[rb] = m & 0xffffffffull;
+                if (rb + 1 < dr) s_mask[rb + 1] = m >> 32;
+            } else {
+                s_mask[rb] = m;
+            }
+        }
     }
     __syncthreads();
-    const int dr = rows - 6, dc = cols - 6, nd = dr * dc;
-    for (int i = tid; i < nd; i += 256) {
-        const int r = 3 + i / dc, c = 3 + i % dc;
-        const int s = fast_score_lds(&s_img[r * FC_LD + c], FC_LD);
-        s_sc[r * FC_LD + c] = (uint8_t)max(s, 0);
+    if (wid == 0) mask_scan64(s_mask, dr, s_off, lane);
+    __syncthreads();
+    const int nl = s_off[64];
+    for (int rb = wid * rstep; rb < dr; rb += 4 * rstep) {
+        const int i = rb + sub;
+        if (i < dr && col_ok) {
+            const uint64_t m = s_mask[i];
+            if ((m >> col) & 1ull) s_list[s_off[i] + __popcll(m & ((1ull << col) - 1ull))] = (uint16_t)(((3 + i) << 8) | c);
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < nl; k += 256) {
+        const int rc = s_list[k], r = rc >> 8, cc = rc & 0xff;
+        const int sc = fast_score_lds(&s_img[r * FC_LD + mis + cc], FC_LD);
+        s_sc[r * FC_LD + cc] = (uint8_t)max(sc, 0);
     }
     __syncthreads();
     uint32_t* out = slots + (size_t)b * slots_per_image + cd.slot_off;
+    const int nch = (nl + 63) >> 6;
     int th = iniTh;
     for (int pass = 0; pass < 2; pass++) {
-        int base = 0;
-        for (int c0 = 0; c0 < nd; c0 += 256) {
-            const int i = c0 + tid;
+        for (int ch = wid; ch < nch; ch += 4) {
+            const int k = ch * 64 + lane;
             bool keep = false;
-            int s = 0, r = 0, c = 0;
-            if (i < nd) {
-                r = 3 + i / dc;
-                c = 3 + i % dc;
-                s = s_sc[r * FC_LD + c];
+            if (k < nl) {
+                const int rc = s_list[k], r = rc >> 8, cc = rc & 0xff;
+                const int s = s_sc[r * FC_LD + cc];
                 if (s >= th) {
                     keep = true;
 #pragma unroll
@@ -238,35 +311,37 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
 #pragma unroll
                         for (int dx = -1; dx <= 1; dx++) {
                             if (!dx && !dy) continue;
-                            int n = s_sc[(r + dy) * FC_LD + c + dx];
+                            int n = s_sc[(r + dy) * FC_LD + cc + dx];
                             n = n >= th ? n : 0;
                             keep = keep && (s > n);
                         }
                 }
             }
             const uint64_t m = __ballot(keep);
-            const int wcount = __popcll(m);
-            if (lane == 0) s_wave[wid] = wcount;
-            __syncthreads();
-            int woff = 0;
-            for (int w = 0; w < wid; w++) woff += s_wave[w];
-            const int total = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
-            if (keep) {
-                const int rank = __popcll(m & ((1ull << lane) - 1ull));
-                const int pos = base + woff + rank;
-                if (pos < cd.cap) {
-                    const uint32_t xr = (uint32_t)(c + cd.offx), yr = (uint32_t)(r + cd.offy);
-                    out[pos] = ((uint32_t)s << 24) | (yr << 12) | xr;
+            if (lane == 0) s_mask[ch] = m;
+        }
+        __syncthreads();
+        if (wid == 0) mask_scan64(s_mask, nch, s_off, lane);
+        __syncthreads();
+        const int total = s_off[64];
+        if (total > 0 || pass == 1) {
+            for (int ch = wid; ch < nch; ch += 4) {
+                const uint64_t m = s_mask[ch];
+                if ((m >> lane) & 1ull) {
+                    const int pos = s_off[ch] + __popcll(m & ((1ull << lane) - 1ull));
+                    if (pos < cd.cap) {
+                        const int rc = s_list[ch * 64 + lane], r = rc >> 8, cc = rc & 0xff;
+                        const uint32_t sv = s_sc[r * FC_LD + cc];
+                        const uint32_t xr = (uint32_t)(cc + cd.offx), yr = (uint32_t)(r + cd.offy);
+                        out[pos] = (sv << 24) | (yr << 12) | xr;
+                    }
                 }
             }
-            base += total;
-            __syncthreads();
-        }
-        if (base > 0 || pass == 1) {
-            if (tid == 0) *cnt_out = min(base, cd.cap);
+            if (tid == 0) *cnt_out = min(total, cd.cap);
             break;
         }
         th = minTh;
+        __syncthreads();   // s_mask / s_off are rewritten by the second pass
     }
 }
 
@@ -341,13 +416,14 @@ __global__ void __launch_bounds__(1024) k_compact(const uint32_t* __restrict__ s
 // lane l are pairs l, l+64, l+128, l+192, so the four wave ballots ARE the
 // 32 descriptor bytes (byte i bit k = pair 8i+k, little endian).
 __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
-                                                     size_t img_bytes, size_t blur_bytes, const int2* __restrict__ sel, int nsel,
-                                                     const LevelDev* __restrict__ lv, orb_kp_dev* __restrict__ kps,
-                                                     uint8_t* __restrict__ desc, int cap_per_image) {
+                                                     size_t img_bytes, size_t blur_bytes, const int2* __restrict__ sel, int selcap,
+                                                     const int* __restrict__ nout, const LevelDev* __restrict__ lv,
+                                                     orb_kp_dev* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                     int cap_per_image) {
     const int lane = threadIdx.x & 63;
     const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (k >= nsel) return;
-    const int2 s = sel[k];
+    if (k >= nout[blockIdx.y] || k >= cap_per_image) return;
+    const int2 s = sel[(size_t)blockIdx.y * selcap + k];
     const uint32_t pk = (uint32_t)s.x;
     const int meta = s.y;
     const int b = meta >> 20, l = (meta >> 16) & 15, idx = meta & 0xffff;
@@ -449,28 +525,17 @@ Extractor::Extractor(int nfeatures, float scaleFactor, int nlevels, int iniTh, i
 Extractor::~Extractor() { release(); }
 
 void Extractor::release() {
-    if (workers_started_) {
-        {
-            std::lock_guard<std::mutex> g(pool_mu_);
-            pool_stop_ = true;
-        }
-        pool_cv_.notify_all();
-        for (auto& t : pool_) t.join();
-        pool_.clear();
-        workers_started_ = false;
-    }
     auto F = [](void* p) { if (p) (void)hipFree(p); };
     F(d_in_); F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_);
     F(d_lcb_); F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_);
-    F(d_kps_); F(d_desc_);
+    F(d_kps_); F(d_desc_); F(d_jobsel_); F(d_jobcnt_); F(d_octlv_); F(d_gscr_); F(d_nout_);
+    d_jobsel_ = d_jobcnt_ = d_octlv_ = d_gscr_ = d_nout_ = nullptr;
     d_in_ = d_pyr_ = d_blur_ = nullptr;
     d_slots_ = nullptr; d_counts_ = nullptr; d_cells_ = nullptr; d_tiles_ = nullptr;
     d_lcb_ = nullptr; d_packed_ = nullptr; d_hdr_ = nullptr; d_gtotal_ = nullptr; d_sel_ = nullptr;
     d_levels_ = nullptr; d_tabs_ = nullptr; d_kps_ = nullptr; d_desc_ = nullptr;
-    if (h_hdr_) (void)hipHostFree(h_hdr_);
-    if (h_packed_) (void)hipHostFree(h_packed_);
-    if (h_sel_) (void)hipHostFree(h_sel_);
-    h_hdr_ = nullptr; h_packed_ = nullptr; h_sel_ = nullptr;
+    if (h_nout_) (void)hipHostFree(h_nout_);
+    h_nout_ = nullptr;
     for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
     for (auto& e : ev_) e = nullptr;
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -683,80 +748,35 @@ int Extractor::setup_geometry(int W, int H) {
     ORB_HIP_CHECK(hipMemcpy(d_levels_, ld.data(), ld.size() * sizeof(LevelDev), hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMalloc(&d_tabs_, std::max<size_t>(tabs.size(), 16)));
     if (!tabs.empty()) ORB_HIP_CHECK(hipMemcpy(d_tabs_, tabs.data(), tabs.size(), hipMemcpyHostToDevice));
-    if (h_hdr_) (void)hipHostFree(h_hdr_);
-    if (h_packed_) (void)hipHostFree(h_packed_);
-    if (h_sel_) (void)hipHostFree(h_sel_);
-    ORB_HIP_CHECK(hipHostMalloc((void**)&h_hdr_, (size_t)B * (nlevels_ + 2) * 4 + 64));
-    ORB_HIP_CHECK(hipHostMalloc((void**)&h_packed_, (size_t)packed_cap_ * 4));
-    ORB_HIP_CHECK(hipHostMalloc((void**)&h_sel_, (size_t)sel_cap_ * sizeof(int2)));
+    // device octree: jobs (image, level), per-job capacity N_l + 8 (phase 2 stops within N + 3)
+    F(d_jobsel_); F(d_jobcnt_); F(d_octlv_); F(d_gscr_); F(d_nout_);
+    jcap_ = 0;
+    std::vector<OctLevelDev> ol(nlevels_);
+    for (int l = 0; l < nlevels_; l++) {
+        ol[l].minX = kEdge - 3;
+        ol[l].maxX = levels_[l].w - kEdge + 3;
+        ol[l].minY = kEdge - 3;
+        ol[l].maxY = levels_[l].h - kEdge + 3;
+        ol[l].N = nPerLevel_[l];
+        jcap_ = std::max(jcap_, nPerLevel_[l] + 8);
+    }
+    if (jcap_ > kOctNMax) return -1;   // nFeaturesPerLevel beyond the device octree's node pool
+    selcap_ = jcap_ * nlevels_;
+    ORB_HIP_CHECK(hipMalloc(&d_octlv_, ol.size() * sizeof(OctLevelDev)));
+    ORB_HIP_CHECK(hipMemcpy(d_octlv_, ol.data(), ol.size() * sizeof(OctLevelDev), hipMemcpyHostToDevice));
+    ORB_HIP_CHECK(hipMalloc(&d_jobsel_, (size_t)B * nlevels_ * jcap_ * 4));
+    ORB_HIP_CHECK(hipMalloc(&d_jobcnt_, (size_t)B * nlevels_ * 4));
+    ORB_HIP_CHECK(hipMalloc(&d_gscr_, (size_t)packed_cap_ * 3 * 2));
+    ORB_HIP_CHECK(hipMalloc(&d_nout_, (size_t)(B + 1) * 4));
+    ORB_HIP_CHECK(hipFree(d_sel_));
+    d_sel_ = nullptr;
+    sel_cap_ = selcap_ * B;
+    ORB_HIP_CHECK(hipMalloc(&d_sel_, (size_t)sel_cap_ * sizeof(int2)));
+    if (h_nout_) (void)hipHostFree(h_nout_);
+    ORB_HIP_CHECK(hipHostMalloc((void**)&h_nout_, (size_t)(B + 1) * 4));
     geomW_ = W;
     geomH_ = H;
     return 0;
-}
-
-void Extractor::start_workers() {
-    if (workers_started_) return;
-    unsigned n = std::thread::hardware_concurrency();
-    const char* env = getenv("ORBGPU_HOST_THREADS");
-    if (env) n = (unsigned)atoi(env);
-    n = std::max(1u, std::min(n, 16u));
-    pool_stop_ = false;
-    workers_.resize(n + 1);
-    for (unsigned i = 0; i < n; i++) pool_.emplace_back([this] { worker_loop(); });
-    workers_started_ = true;
-}
-
-void Extractor::worker_loop() {
-    // each worker has an id from the order it grabs it
-    int wid;
-    {
-        std::lock_guard<std::mutex> g(pool_mu_);
-        wid = worker_ids_++;
-    }
-    uint64_t seen = 0;
-    for (;;) {
-        {
-            std::unique_lock<std::mutex> g(pool_mu_);
-            pool_cv_.wait(g, [&] { return pool_stop_ || pool_gen_ != seen; });
-            if (pool_stop_) return;
-            seen = pool_gen_;
-        }
-        run_octree_jobs(wid + 1);
-        if (pool_pending_.fetch_sub(1) == 1) {
-            std::lock_guard<std::mutex> g(pool_mu_);
-            pool_done_cv_.notify_all();
-        }
-    }
-}
-
-void Extractor::run_octree_jobs(int wid) {
-    OctreeWorker& W = workers_[wid].oct;
-    std::vector<OctKey>& keys = workers_[wid].keys;
-    std::vector<uint32_t>& out = workers_[wid].out;
-    for (;;) {
-        const int job = next_job_.fetch_add(1);
-        if (job >= njobs_) break;
-        const int b = job / nlevels_, l = job % nlevels_;
-        const int* H = h_hdr_ + (size_t)b * (nlevels_ + 2);
-        const int base = H[nlevels_ + 1];
-        int loff = 0;
-        for (int k = 0; k < l; k++) loff += H[1 + k];
-        const int n = H[1 + l];
-        const uint32_t* src = h_packed_ + base + loff;
-        keys.resize(n);
-        for (int i = 0; i < n; i++) {
-            const uint32_t p = src[i];
-            keys[i].x = (float)(p & 0xfff);
-            keys[i].y = (float)((p >> 12) & 0xfff);
-            keys[i].response = (float)(p >> 24);
-            keys[i].packed = p;
-        }
-        const LevelHost& L = levels_[l];
-        const int minB = kEdge - 3;
-        const int r = W.distribute(keys.data(), n, minB, L.w - kEdge + 3, minB, L.h - kEdge + 3, nPerLevel_[l], out);
-        job_res_[job].assign(out.begin(), out.begin() + std::max(r, 0));
-        job_ok_[job] = r >= 0;
-    }
 }
 
 int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_t img_stride,
@@ -765,7 +785,6 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     if (B <= 0 || B > maxB_ || W <= 0 || H <= 0) return -1;
     if (W > maxW_ || H > maxH_) return -1;
     if (int e = setup_geometry(W, H)) return e;
-    start_workers();
     hipStream_t s = stream_;
     const uint8_t* src = imgs;
     if (!imgs_on_device) {
@@ -815,59 +834,15 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
                        (const int*)d_counts_, (const CellDesc*)d_cells_, ncells, (const int*)d_lcb_, nlevels_,
                        (uint32_t*)d_packed_, (int*)d_hdr_, d_gtotal_, packed_cap_);
     ORB_HIP_CHECK(hipGetLastError());
-    const size_t hdr_bytes = (size_t)maxB_ * (nlevels_ + 2) * 4;  // d_gtotal_ sits right after
-    ORB_HIP_CHECK(hipMemcpyAsync(h_hdr_, d_hdr_, hdr_bytes + 4, hipMemcpyDeviceToHost, s));
     ORB_HIP_CHECK(hipEventRecord(ev_[4], s));
-    ORB_HIP_CHECK(hipStreamSynchronize(s));
-    const int gtotal = *(int*)((char*)h_hdr_ + hdr_bytes);
-    for (int b = 0; b < B; b++)
-        if (h_hdr_[(size_t)b * (nlevels_ + 2) + nlevels_ + 1] < 0) return -3;  // packed capacity
-    if (gtotal > 0)
-        ORB_HIP_CHECK(hipMemcpyAsync(h_packed_, d_packed_, (size_t)gtotal * 4, hipMemcpyDeviceToHost, s));
-    ORB_HIP_CHECK(hipStreamSynchronize(s));
-    // 5. host octree, (image, level) jobs over the worker pool
-    auto t_oct0 = std::chrono::steady_clock::now();
-    njobs_ = B * nlevels_;
-    job_res_.resize(njobs_);
-    job_ok_.assign(njobs_, 0);
-    next_job_ = 0;
-    {
-        std::lock_guard<std::mutex> g(pool_mu_);
-        pool_pending_ = (int)pool_.size();
-        pool_gen_++;
-    }
-    pool_cv_.notify_all();
-    run_octree_jobs(0);
-    {
-        std::unique_lock<std::mutex> g(pool_mu_);
-        pool_done_cv_.wait(g, [&] { return pool_pending_.load() == 0; });
-    }
-    for (int j = 0; j < njobs_; j++)
-        if (!job_ok_[j]) return -1;
-    // selected list: image-major, level-major, octree order
-    int nsel = 0;
-    for (int b = 0; b < B; b++) {
-        int k = 0;
-        for (int l = 0; l < nlevels_; l++) k += (int)job_res_[b * nlevels_ + l].size();
-        n_out[b] = k;
-        if (k > cap) return -3;
-        nsel += k;
-    }
-    if (nsel > sel_cap_) return -3;
-    {
-        int o = 0;
-        for (int b = 0; b < B; b++) {
-            int k = 0;
-            for (int l = 0; l < nlevels_; l++)
-                for (uint32_t p : job_res_[b * nlevels_ + l]) {
-                    h_sel_[o].x = (int)p;
-                    h_sel_[o].y = (b << 20) | (l << 16) | k;
-                    o++;
-                    k++;
-                }
-        }
-    }
-    octree_ms_ = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_oct0).count();
+    // 5. DistributeOctTree per (image, level) + per-image selected lists, on the device
+    int* d_err = (int*)d_nout_ + B;
+    ORB_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
+    if (int e = octree_launch((const uint32_t*)d_packed_, (const int*)d_hdr_, B, nlevels_,
+                              (const OctLevelDev*)d_octlv_, (uint32_t*)d_jobsel_, (int*)d_jobcnt_, jcap_,
+                              (uint16_t*)d_gscr_, (size_t)packed_cap_, cap, (int2*)d_sel_, selcap_, (int*)d_nout_,
+                              d_err, s))
+        return e;
     ORB_HIP_CHECK(hipEventRecord(ev_[5], s));
     // 6. orientation + descriptors
     orb_kp_dev* okps = (orb_kp_dev*)kps;
@@ -884,14 +859,17 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
         okps = (orb_kp_dev*)d_kps_;
         odesc = (uint8_t*)d_desc_;
     }
-    if (nsel > 0) {
-        ORB_HIP_CHECK(hipMemcpyAsync(d_sel_, h_sel_, (size_t)nsel * sizeof(int2), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_orient_desc, dim3((nsel + 3) / 4), dim3(256), 0, s, (const uint8_t*)d_pyr_,
-                           (const uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const int2*)d_sel_, nsel,
-                           (const LevelDev*)d_levels_, okps, odesc, cap);
-        ORB_HIP_CHECK(hipGetLastError());
-    }
+    hipLaunchKernelGGL(k_orient_desc, dim3((selcap_ + 3) / 4, B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
+                       (const uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const int2*)d_sel_, selcap_,
+                       (const int*)d_nout_, (const LevelDev*)d_levels_, okps, odesc, cap);
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipMemcpyAsync(h_nout_, d_nout_, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, s));
     ORB_HIP_CHECK(hipEventRecord(ev_[6], s));
+    ORB_HIP_CHECK(hipStreamSynchronize(s));
+    const int err = h_nout_[B];
+    for (int b = 0; b < B; b++) n_out[b] = h_nout_[b];
+    if (err & 1) return -3;   // keypoints beyond `cap` (or the selection capacity)
+    if (err) return -1;
     if (!out_on_device) {
         for (int b = 0; b < B; b++) {
             if (n_out[b] == 0) continue;
@@ -900,8 +878,8 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
             ORB_HIP_CHECK(hipMemcpyAsync(desc + (size_t)b * cap * 32, odesc + (size_t)b * cap * 32, (size_t)n_out[b] * 32,
                                          hipMemcpyDeviceToHost, s));
         }
+        ORB_HIP_CHECK(hipStreamSynchronize(s));
     }
-    ORB_HIP_CHECK(hipStreamSynchronize(s));
     last_B_ = B;
     return 0;
 }
@@ -923,7 +901,7 @@ int Extractor::timings(float* ms6) {
     (void)hipEventElapsedTime(&t[1], ev_[1], ev_[2]);
     (void)hipEventElapsedTime(&t[2], ev_[2], ev_[3]);
     (void)hipEventElapsedTime(&t[3], ev_[3], ev_[4]);
-    t[4] = octree_ms_;
+    (void)hipEventElapsedTime(&t[4], ev_[4], ev_[5]);
     (void)hipEventElapsedTime(&t[5], ev_[5], ev_[6]);
     for (int i = 0; i < 6; i++) ms6[i] = t[i];
     return 0;

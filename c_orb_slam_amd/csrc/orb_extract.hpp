@@ -74,9 +74,6 @@ private:
     static void gaussian_taps(int taps[7]);
     int setup_geometry(int W, int H);
     void release();
-    void start_workers();
-    void worker_loop();
-    void run_octree_jobs(int wid);
 
     int nfeatures_;
     double scaleFactorD_;
@@ -104,29 +101,11 @@ private:
     int* d_gtotal_ = nullptr;
     bool d_gtotal_alias_ = false;
     size_t in_cap_ = 0, out_cap_ = 0;
-    int* h_hdr_ = nullptr;
-    uint32_t* h_packed_ = nullptr;
-    int2* h_sel_ = nullptr;
-    float octree_ms_ = 0;
+    // device octree (octree.hip): per-job selections, per-image selected lists
+    void *d_jobsel_ = nullptr, *d_jobcnt_ = nullptr, *d_octlv_ = nullptr, *d_gscr_ = nullptr, *d_nout_ = nullptr;
+    int jcap_ = 0, selcap_ = 0;
+    int* h_nout_ = nullptr;   // pinned: nout[maxB] + err
 
-    // host octree worker pool
-    struct WorkerScratch {
-        OctreeWorker oct;
-        std::vector<OctKey> keys;
-        std::vector<uint32_t> out;
-    };
-    std::vector<WorkerScratch> workers_;
-    std::vector<std::thread> pool_;
-    std::mutex pool_mu_;
-    std::condition_variable pool_cv_, pool_done_cv_;
-    bool pool_stop_ = false, workers_started_ = false;
-    uint64_t pool_gen_ = 0;
-    std::atomic<int> pool_pending_{0};
-    int worker_ids_ = 0;
-    std::atomic<int> next_job_{0};
-    int njobs_ = 0;
-    std::vector<std::vector<uint32_t>> job_res_;
-    std::vector<char> job_ok_;
 };
 
 }  // namespace orbgpu

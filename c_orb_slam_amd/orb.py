@@ -132,7 +132,7 @@ class ORBextractor:
     def last_timings(self):
         t = np.zeros(6, np.float32)
         check(self._L.ORBextractor_last_timings(self._h, ptr(t)))
-        return dict(zip(["pyramid", "blur", "fast_cells", "compact", "octree_host", "orient_desc"], t.tolist()))
+        return dict(zip(["pyramid", "blur", "fast_cells", "compact", "octree", "orient_desc"], t.tolist()))
 
 
 class Frame:

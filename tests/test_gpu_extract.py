@@ -110,3 +110,27 @@ def test_extract_non_contiguous_stride(gpu):
     ok, od = oracle_lib.OracleExtractor(1000, 1.2, 8, 20, 7)(frames[0])
     assert np.array_equal(kps[:n.value].view(np.uint8), ok.view(np.uint8))
     assert np.array_equal(desc[:n.value], od)
+
+
+def _sparse_image(seed, w=1241, h=376, nrect=12):
+    rng = np.random.default_rng(seed)
+    img = np.full((h, w), 90, np.uint8)
+    for _ in range(nrect):
+        x0, y0 = rng.integers(0, w - 60), rng.integers(0, h - 40)
+        img[y0:y0 + rng.integers(10, 40), x0:x0 + rng.integers(10, 60)] = rng.integers(150, 255)
+    return img
+
+
+@pytest.mark.parametrize("kind,nf", [("noise", 1200), ("noise", 2000), ("sparse", 1200), ("sparse", 500)])
+def test_extract_octree_regimes(gpu, kind, nf):
+    """DistributeOctTree regimes on the device octree: pure-noise frames put >40k FAST
+    candidates on level 0 (> the LDS key budget -> global-scratch path, phase 2 from the
+    first round); sparse frames end phase 1 with every node holding one key."""
+    rng = np.random.default_rng(7)
+    img = rng.integers(0, 256, (376, 1241), dtype=np.uint8) if kind == "noise" else _sparse_image(7)
+    ex = gpu.ORBextractor(nf, 1.2, 8, 20, 7, max_width=1241, max_height=376)
+    gk, gd = ex(img)
+    ok, od = oracle_lib.OracleExtractor(nf, 1.2, 8, 20, 7)(img)
+    assert len(gk) == len(ok) and np.array_equal(gk.view(np.uint8), ok.view(np.uint8)), _diag(gk, gd, ok, od)
+    if len(ok):
+        assert np.array_equal(gd, od)

@@ -1,0 +1,30 @@
+"""Stage timings of ONE extractor on a batch of KITTI-shaped images (no concurrent stream)."""
+import sys
+import time
+
+sys.path.insert(0, ".")
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import c_orb_slam_amd as orb  # noqa: E402
+from c_orb_slam_amd import synthetic  # noqa: E402
+
+W, H, B = 1241, 376, int(sys.argv[1]) if len(sys.argv) > 1 else 64
+dev = torch.device("cuda", 0)
+lefts, rights, Hs, Rs = synthetic.stereo_sequence(1000, B, W, H, return_rotations=True)
+ex = orb.ORBextractor(1200, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=B)
+d_L = torch.from_numpy(lefts).to(dev)
+cap = 2 * 1200 + 64
+d_kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
+d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+acc = {}
+for it in range(13):
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    ex.extract_device(d_L.data_ptr(), B, W, H, W, W * H, d_kps.data_ptr(), d_desc.data_ptr(), cap)
+    wall = (time.perf_counter() - t) * 1e3
+    if it >= 3:
+        for k, v in ex.last_timings().items():
+            acc[k] = acc.get(k, 0) + v / 10
+        acc["wall"] = acc.get("wall", 0) + wall / 10
+print({k: round(v, 4) for k, v in acc.items()}, flush=True)
