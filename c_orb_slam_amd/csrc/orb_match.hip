@@ -283,7 +283,9 @@ __global__ void __launch_bounds__(64) k_select(const SearchDev* __restrict__ pro
     __shared__ int s_cnt[SEL_CHUNK];
     __shared__ int s_qmp[SEL_CHUNK];     // map point written by the query
     __shared__ uint8_t s_qobs[SEL_CHUNK];
-    __shared__ int s_nh;
+    __shared__ int16_t s_mbest[kMaxFrameKeys];   // query -> keypoint taken (rotation check deferred)
+    __shared__ int s_hsz[HISTO_LENGTH];
+    __shared__ int s_ind[3];
     const SearchDev P = probs[blockIdx.x];
     const int lane = threadIdx.x;
     const int N = P.cur.N;
@@ -292,7 +294,8 @@ __global__ void __launch_bounds__(64) k_select(const SearchDev* __restrict__ pro
         s_cur[i] = m;
         s_occ[i] = (m >= 0 && P.mpObs[m] > 0) ? 1 : 0;
     }
-    if (lane == 0) s_nh = 0;
+    for (int i = lane; i < P.nq; i += 64) s_mbest[i] = -1;
+    if (lane < HISTO_LENGTH) s_hsz[lane] = 0;
     bool bF = false, bB = false;
     if (LAST) fwd_bwd(P, bMono != 0, bF, bB);
     int nmatches = 0;
@@ -384,14 +387,7 @@ __global__ void __launch_bounds__(64) k_select(const SearchDev* __restrict__ pro
                     if (lane == 0) {
                         s_cur[bestIdx] = s_qmp[qi];
                         s_occ[bestIdx] = s_qobs[qi];
-                        if (LAST && checkOri) {
-                            float rot = P.last.keysUn[q].angle - P.cur.keysUn[bestIdx].angle;
-                            if (rot < 0.0f) rot += 360.0f;
-                            int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
-                            if (bin == HISTO_LENGTH) bin = 0;
-                            P.hist[s_nh] = make_int2(bin, bestIdx);
-                            s_nh++;
-                        }
+                        s_mbest[q] = (int16_t)bestIdx;
                     }
                     nmatches++;
                 }
@@ -402,27 +398,49 @@ __global__ void __launch_bounds__(64) k_select(const SearchDev* __restrict__ pro
     }
     __syncthreads();
     if (LAST && checkOri) {
+        // rotation-consistency histogram over the matches, bins in parallel (ORBmatcher.cc:1422-1467)
+        for (int q = lane; q < P.nq; q += 64) {
+            const int bi = s_mbest[q];
+            if (bi < 0) continue;
+            float rot = P.last.keysUn[q].angle - P.cur.keysUn[bi].angle;
+            if (rot < 0.0f) rot += 360.0f;
+            int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
+            if (bin == HISTO_LENGTH) bin = 0;
+            atomicAdd(&s_hsz[bin], 1);
+        }
+        __syncthreads();
         if (lane == 0) {
-            const int nh = s_nh;
-            int sizes[HISTO_LENGTH];
-            for (int b = 0; b < HISTO_LENGTH; b++) sizes[b] = 0;
-            for (int k = 0; k < nh; k++) sizes[P.hist[k].x]++;
             // ComputeThreeMaxima, ORBmatcher.cc:1601-1642
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < HISTO_LENGTH; i++) {
-                const int sz = sizes[i];
+                const int sz = s_hsz[i];
                 if (sz > max1) { max3 = max2; max2 = max1; max1 = sz; ind3 = ind2; ind2 = ind1; ind1 = i; }
                 else if (sz > max2) { max3 = max2; max2 = sz; ind3 = ind2; ind2 = i; }
                 else if (sz > max3) { max3 = sz; ind3 = i; }
             }
             if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
             else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-            for (int k = 0; k < nh; k++) {
-                const int2 h = P.hist[k];
-                if (h.x != ind1 && h.x != ind2 && h.x != ind3) { s_cur[h.y] = -1; nmatches--; }
+            s_ind[0] = ind1;
+            s_ind[1] = ind2;
+            s_ind[2] = ind3;
+        }
+        __syncthreads();
+        const int ind1 = s_ind[0], ind2 = s_ind[1], ind3 = s_ind[2];
+        int removed = 0;
+        for (int q = lane; q < P.nq; q += 64) {
+            const int bi = s_mbest[q];
+            if (bi < 0) continue;
+            float rot = P.last.keysUn[q].angle - P.cur.keysUn[bi].angle;
+            if (rot < 0.0f) rot += 360.0f;
+            int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
+            if (bin == HISTO_LENGTH) bin = 0;
+            if (bin != ind1 && bin != ind2 && bin != ind3) {
+                s_cur[bi] = -1;
+                removed++;
             }
         }
-        nmatches = __shfl(nmatches, 0, 64);
+        for (int o = 32; o >= 1; o >>= 1) removed += __shfl_xor(removed, o, 64);
+        nmatches -= removed;
     }
     __syncthreads();
     for (int i = lane; i < N; i += 64) P.curMP[i] = s_cur[i];
