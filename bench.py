@@ -87,151 +87,190 @@ def main():
     mb = np.float32(mbf / fx)
     cap = 2 * NFEAT + 64
 
-    exL = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=B)
-    exR = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=B)
     m = orb.ORBmatcher(0.9, True)
     L = lib()
     check(L.ORBmatcher_set_device_pointers(m._h, 1))
-
     d_L = torch.from_numpy(lefts).to(dev)
     d_R = torch.from_numpy(rights).to(dev)
-    d_kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)      # left mvKeys (== mvKeysUn, KITTI k1=0)
-    d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
-    d_kpsR = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
-    d_descR = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
-    d_uR = torch.empty((B, cap), dtype=torch.float32, device=dev)         # mvuRight
-    d_depth = torch.empty((B, cap), dtype=torch.float32, device=dev)      # mvDepth
     d_obs = torch.ones(cap, dtype=torch.int32, device=dev)
     d_arange = torch.arange(cap, dtype=torch.int32, device=dev)
     d_outlier = torch.zeros(cap, dtype=torch.uint8, device=dev)
-    d_mp_pos = torch.empty((B, cap, 3), dtype=torch.float32, device=dev)
-    d_last_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
-    d_cur_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
-    scale = torch.from_numpy(exL.GetScaleFactors()).to(dev)
     eye = torch.eye(4, dtype=torch.float32, device=dev)
     poses = torch.from_numpy(np.stack([synthetic.pose_from_rotation(R) for R in Rs])).to(dev)
-    kp_f = d_kps.view(torch.float32)
-    P = B - 1
-    # PoseOptimization inputs gathered in HBM from the matcher's output
-    d_has = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
-    d_Xw = torch.empty((P, cap, 3), dtype=torch.float32, device=dev)
-    d_pobs = torch.empty((P, cap, 3), dtype=torch.float32, device=dev)
-    d_isig = torch.empty((P, cap), dtype=torch.float32, device=dev)
-    d_Tout = torch.empty((P, 16), dtype=torch.float32, device=dev)
-    d_poutl = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
-    isig_tab = torch.from_numpy(exL.GetInverseScaleSigmaSquares()).to(dev)
-    octv = d_kps[1:, :, 5]
     gW = np.float32(np.float32(64) / np.float32(W))
     gH = np.float32(np.float32(48) / np.float32(H))
+    P = B - 1
+    arr = lambda xs: (C.c_void_p * len(xs))(*xs)
+    from c_orb_slam_amd._lib import pose_problem
+    from concurrent.futures import ThreadPoolExecutor
+    # HIP's current device is per thread: every worker binds it first
+    pool = ThreadPoolExecutor(2, initializer=lambda: torch.cuda.set_device(dev))
+    track_stream = torch.cuda.Stream(device=dev)
 
-    def frame_struct(b, n, Tptr, stereo):
-        f = orb_frame()
-        f.N = int(n)
-        f.keysUn = d_kps[b].data_ptr()
-        f.desc = d_desc[b].data_ptr()
-        f.uRight = d_uR[b].data_ptr() if stereo else None
-        f.minX, f.maxX, f.minY, f.maxY = 0.0, float(W), 0.0, float(H)
-        f.gridWInv, f.gridHInv = gW, gH
-        f.scaleFactors = scale.data_ptr()
-        f.nlevels = 8
-        f.fx, f.fy, f.cx, f.cy, f.bf, f.b = fx, fy, cx, cy, mbf, mb
-        f.Tcw = Tptr
-        return f
+    class Lane:
+        """One batch in flight: its own extractor pair (pyramids, keypoints) and tracking buffers."""
+
+        def __init__(self):
+            self.exL = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=B)
+            self.exR = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=B)
+            self.d_kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)   # mvKeys (== mvKeysUn, KITTI k1=0)
+            self.d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+            self.d_kpsR = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
+            self.d_descR = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+            self.d_uR = torch.empty((B, cap), dtype=torch.float32, device=dev)      # mvuRight
+            self.d_depth = torch.empty((B, cap), dtype=torch.float32, device=dev)   # mvDepth
+            self.d_mp_pos = torch.empty((B, cap, 3), dtype=torch.float32, device=dev)
+            self.d_last_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
+            self.d_cur_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
+            self.scale = torch.from_numpy(self.exL.GetScaleFactors()).to(dev)
+            self.kp_f = self.d_kps.view(torch.float32)
+            # PoseOptimization inputs gathered in HBM from the matcher's output
+            self.d_has = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
+            self.d_Xw = torch.empty((P, cap, 3), dtype=torch.float32, device=dev)
+            self.d_pobs = torch.empty((P, cap, 3), dtype=torch.float32, device=dev)
+            self.d_isig = torch.empty((P, cap), dtype=torch.float32, device=dev)
+            self.d_Tout = torch.empty((P, 16), dtype=torch.float32, device=dev)
+            self.d_poutl = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
+            self.isig_tab = torch.from_numpy(self.exL.GetInverseScaleSigmaSquares()).to(dev)
+            self.octv = self.d_kps[1:, :, 5]
+            # ctypes views of the batch, built once (device pointers do not move; only counts change)
+            self.curs = (orb_frame * P)(*[self.frame_struct(b, poses[b - 1].data_ptr()) for b in range(1, B)])
+            self.lasts = (orb_frame * P)(*[self.frame_struct(b, eye.data_ptr()) for b in range(0, B - 1)])
+            self.mps = (orb_mappoints * P)()
+            for p in range(P):
+                self.mps[p].pos = self.d_mp_pos[p].data_ptr()
+                self.mps[p].desc = self.d_desc[p].data_ptr()
+                self.mps[p].observations = d_obs.data_ptr()
+            self.a_cur_mp = arr([self.d_cur_mp[b].data_ptr() for b in range(1, B)])
+            self.a_last_kps = arr([self.d_kps[b].data_ptr() for b in range(P)])
+            self.a_last_mp = arr([self.d_last_mp[b].data_ptr() for b in range(P)])
+            self.a_last_out = arr([d_outlier.data_ptr()] * P)
+            self.s_kL = arr([self.d_kps[b].data_ptr() for b in range(B)])
+            self.s_dL = arr([self.d_desc[b].data_ptr() for b in range(B)])
+            self.s_kR = arr([self.d_kpsR[b].data_ptr() for b in range(B)])
+            self.s_dR = arr([self.d_descR[b].data_ptr() for b in range(B)])
+            self.s_uR = arr([self.d_uR[b].data_ptr() for b in range(B)])
+            self.s_dep = arr([self.d_depth[b].data_ptr() for b in range(B)])
+            self.pprobs = (pose_problem * P)(*[
+                pose_problem(0, poses[p].data_ptr(), self.d_has[p].data_ptr(), self.d_Xw[p].data_ptr(),
+                             self.d_pobs[p].data_ptr(), self.d_isig[p].data_ptr(), float(fx), float(fy), float(cx),
+                             float(cy), float(mbf)) for p in range(P)])
+            self.a_Tout = arr([self.d_Tout[p].data_ptr() for p in range(P)])
+            self.a_poutl = arr([self.d_poutl[p].data_ptr() for p in range(P)])
+            self.ninl = np.zeros(P, np.int32)
+            self.nm = np.zeros(P, np.int32)
+            self.nst = np.zeros(B, np.int32)
+            self.nL = self.nR = None
+
+        def frame_struct(self, b, Tptr):
+            f = orb_frame()
+            f.N = 0
+            f.keysUn = self.d_kps[b].data_ptr()
+            f.desc = self.d_desc[b].data_ptr()
+            f.uRight = self.d_uR[b].data_ptr()
+            f.minX, f.maxX, f.minY, f.maxY = 0.0, float(W), 0.0, float(H)
+            f.gridWInv, f.gridHInv = gW, gH
+            f.scaleFactors = self.scale.data_ptr()
+            f.nlevels = 8
+            f.fx, f.fy, f.cx, f.cy, f.bf, f.b = fx, fy, cx, cy, mbf, mb
+            f.Tcw = Tptr
+            return f
+
+        def extract(self):
+            # Frame(imLeft, imRight): two ORBextractor calls (Frame.cc:78-81) on two host threads and
+            # two HIP streams, like the reference's two extractor threads per stereo frame
+            fR = pool.submit(self.exR.extract_device, d_R.data_ptr(), B, W, H, W, W * H, self.d_kpsR.data_ptr(),
+                             self.d_descR.data_ptr(), cap)
+            self.nL = np.ascontiguousarray(self.exL.extract_device(d_L.data_ptr(), B, W, H, W, W * H,
+                                                                   self.d_kps.data_ptr(), self.d_desc.data_ptr(), cap),
+                                           np.int32)
+            self.nR = np.ascontiguousarray(fR.result(), np.int32)
+
+        def track(self):
+            """ComputeStereoMatches, UpdateLastFrame, SearchByProjection(Cur, Last, 7), PoseOptimization."""
+            t1 = time.perf_counter()
+            nL, nR = self.nL, self.nR
+            check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, self.exL._h, self.exR._h, B, ptr(nL), self.s_kL,
+                                                          self.s_dL, ptr(nR), self.s_kR, self.s_dR, float(mbf),
+                                                          float(mb), self.s_uR, self.s_dep, ptr(self.nst)),
+                  "ComputeStereoMatches batch")
+            t2 = time.perf_counter()
+            with torch.cuda.stream(track_stream):
+                # UpdateLastFrame-style map points of the last frame from its stereo depth: X = d K^-1 [u v 1]
+                x, y = self.kp_f[..., 0], self.kp_f[..., 1]
+                self.d_mp_pos[..., 0] = (x - float(cx)) / float(fx) * self.d_depth
+                self.d_mp_pos[..., 1] = (y - float(cy)) / float(fy) * self.d_depth
+                self.d_mp_pos[..., 2] = self.d_depth
+                torch.where(self.d_depth > 0, d_arange, torch.full_like(d_arange, -1), out=self.d_last_mp)
+                self.d_cur_mp.fill_(-1)
+            for p in range(P):
+                self.curs[p].N = int(nL[p + 1])
+                self.lasts[p].N = int(nL[p])
+                self.mps[p].n = int(nL[p])
+                self.pprobs[p].N = int(nL[p + 1])
+            track_stream.synchronize()
+            # TrackWithMotionModel: SearchByProjection(CurrentFrame, LastFrame, th=7, stereo) (Tracking.cc:869-885)
+            check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, P, self.curs, self.a_cur_mp, self.lasts,
+                                                                  self.a_last_kps, self.a_last_mp, self.a_last_out,
+                                                                  self.mps, 7.0, 0, ptr(self.nm)),
+                  "SearchByProjection batch")
+            t3 = time.perf_counter()
+            # Optimizer::PoseOptimization(&mCurrentFrame) (Tracking.cc:887) on the matched map points
+            with torch.cuda.stream(track_stream):
+                cm = self.d_cur_mp[1:]
+                self.d_has.copy_(cm >= 0)
+                torch.gather(self.d_mp_pos[:-1], 1, cm.clamp(min=0).long().unsqueeze(-1).expand(-1, -1, 3),
+                             out=self.d_Xw)
+                self.d_pobs[..., 0:2] = self.kp_f[1:, :, 0:2]
+                self.d_pobs[..., 2] = self.d_uR[1:]
+                torch.index_select(self.isig_tab, 0, self.octv.reshape(-1).clamp(0, 7), out=self.d_isig.view(-1))
+            track_stream.synchronize()
+            check(L.Optimizer_PoseOptimization_batch_device(P, self.pprobs, self.a_Tout, self.a_poutl,
+                                                            ptr(self.ninl)), "PoseOptimization batch")
+            t4 = time.perf_counter()
+            for k, v in (("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3)):
+                phase_acc[k] = phase_acc.get(k, 0.0) + v * 1e3
+            tl, tr = self.exL.last_timings(), self.exR.last_timings()
+            for k in tl:
+                stage_acc[k] = stage_acc.get(k, 0.0) + tl[k] + tr[k]
+            kernel_ms.append(tl["fast_cells"])
+            kernel_ms.append(tr["fast_cells"])
+            pose_inl.append(int(self.ninl.sum()))
+            return int(nL.sum() + nR.sum()), int(self.nm.sum()), int(self.nst.sum())
 
     stage_acc = {}
     phase_acc = {}
     pose_inl = []
     kernel_ms = []   # k_fast_cells duration per step (HIP events on the extractor streams)
-
-    # ctypes views of the batch, built once (device pointers do not move; only counts change)
-    curs = (orb_frame * P)(*[frame_struct(b, 0, poses[b - 1].data_ptr(), True) for b in range(1, B)])
-    lasts = (orb_frame * P)(*[frame_struct(b, 0, eye.data_ptr(), True) for b in range(0, B - 1)])
-    mps = (orb_mappoints * P)()
-    for p in range(P):
-        mps[p].pos = d_mp_pos[p].data_ptr()
-        mps[p].desc = d_desc[p].data_ptr()
-        mps[p].observations = d_obs.data_ptr()
-    arr = lambda xs: (C.c_void_p * len(xs))(*xs)
-    a_cur_mp = arr([d_cur_mp[b].data_ptr() for b in range(1, B)])
-    a_last_kps = arr([d_kps[b].data_ptr() for b in range(P)])
-    a_last_mp = arr([d_last_mp[b].data_ptr() for b in range(P)])
-    a_last_out = arr([d_outlier.data_ptr()] * P)
-    s_kL = arr([d_kps[b].data_ptr() for b in range(B)])
-    s_dL = arr([d_desc[b].data_ptr() for b in range(B)])
-    s_kR = arr([d_kpsR[b].data_ptr() for b in range(B)])
-    s_dR = arr([d_descR[b].data_ptr() for b in range(B)])
-    s_uR = arr([d_uR[b].data_ptr() for b in range(B)])
-    s_dep = arr([d_depth[b].data_ptr() for b in range(B)])
-    from c_orb_slam_amd._lib import pose_problem
-    pprobs = (pose_problem * P)(*[pose_problem(0, poses[p].data_ptr(), d_has[p].data_ptr(), d_Xw[p].data_ptr(),
-                                               d_pobs[p].data_ptr(), d_isig[p].data_ptr(), float(fx), float(fy),
-                                               float(cx), float(cy), float(mbf)) for p in range(P)])
-    a_Tout = arr([d_Tout[p].data_ptr() for p in range(P)])
-    a_poutl = arr([d_poutl[p].data_ptr() for p in range(P)])
-    ninl = np.zeros(P, np.int32)
-    nm = np.zeros(P, np.int32)
-    nst = np.zeros(B, np.int32)
-    from concurrent.futures import ThreadPoolExecutor
-    pool = ThreadPoolExecutor(1, initializer=lambda: torch.cuda.set_device(dev))   # HIP device is per thread
+    lanes = [Lane(), Lane()]
+    exL = lanes[0].exL
+    ex_pool = ThreadPoolExecutor(1, initializer=lambda: torch.cuda.set_device(dev))
+    state = {"k": 0, "ready": None}
 
     def step():
-        # Frame(imLeft, imRight): two ORBextractor calls (Frame.cc:78-81), then ComputeStereoMatches
-        # the two extractors run concurrently on their own streams / host octree pools, like the
-        # reference's two extractor threads per stereo frame
-        t0 = time.perf_counter()
-        fR = pool.submit(exR.extract_device, d_R.data_ptr(), B, W, H, W, W * H, d_kpsR.data_ptr(),
-                         d_descR.data_ptr(), cap)
-        nL = exL.extract_device(d_L.data_ptr(), B, W, H, W, W * H, d_kps.data_ptr(), d_desc.data_ptr(), cap)
-        nR = fR.result()
-        t1 = time.perf_counter()
-        nL = np.ascontiguousarray(nL, np.int32)
-        nR = np.ascontiguousarray(nR, np.int32)
-        check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, exL._h, exR._h, B, ptr(nL), s_kL, s_dL, ptr(nR), s_kR,
-                                                      s_dR, float(mbf), float(mb), s_uR, s_dep, ptr(nst)),
-              "ComputeStereoMatches batch")
-        t2 = time.perf_counter()
-        # UpdateLastFrame-style map points of the last frame from its stereo depth: X = d K^-1 [u v 1]
-        x, y = kp_f[..., 0], kp_f[..., 1]
-        d_mp_pos[..., 0] = (x - float(cx)) / float(fx) * d_depth
-        d_mp_pos[..., 1] = (y - float(cy)) / float(fy) * d_depth
-        d_mp_pos[..., 2] = d_depth
-        torch.where(d_depth > 0, d_arange, torch.full_like(d_arange, -1), out=d_last_mp)
-        d_cur_mp.fill_(-1)
-        for p in range(P):
-            curs[p].N = int(nL[p + 1])
-            lasts[p].N = int(nL[p])
-            mps[p].n = int(nL[p])
-        torch.cuda.current_stream().synchronize()
-        # TrackWithMotionModel: SearchByProjection(CurrentFrame, LastFrame, th=7, stereo) (Tracking.cc:869-885)
-        check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, P, curs, a_cur_mp, lasts, a_last_kps, a_last_mp,
-                                                              a_last_out, mps, 7.0, 0, ptr(nm)),
-              "SearchByProjection batch")
-        t3 = time.perf_counter()
-        # Optimizer::PoseOptimization(&mCurrentFrame) (Tracking.cc:887) on the matched map points
-        cm = d_cur_mp[1:]
-        d_has.copy_(cm >= 0)
-        torch.gather(d_mp_pos[:-1], 1, cm.clamp(min=0).long().unsqueeze(-1).expand(-1, -1, 3), out=d_Xw)
-        d_pobs[..., 0:2] = kp_f[1:, :, 0:2]
-        d_pobs[..., 2] = d_uR[1:]
-        torch.index_select(isig_tab, 0, octv.reshape(-1).clamp(0, 7), out=d_isig.view(-1))
-        for p in range(P):
-            pprobs[p].N = int(nL[p + 1])
-        torch.cuda.current_stream().synchronize()
-        check(L.Optimizer_PoseOptimization_batch_device(P, pprobs, a_Tout, a_poutl, ptr(ninl)),
-              "PoseOptimization batch")
-        t4 = time.perf_counter()
-        for k, v in (("extract_LR", t1 - t0), ("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3)):
-            phase_acc[k] = phase_acc.get(k, 0.0) + v * 1e3
-        tl, tr = exL.last_timings(), exR.last_timings()
-        for k in tl:
-            stage_acc[k] = stage_acc.get(k, 0.0) + tl[k] + tr[k]
-        kernel_ms.append(tl["fast_cells"])
-        kernel_ms.append(tr["fast_cells"])
-        pose_inl.append(int(ninl.sum()))
-        return int(nL.sum() + nR.sum()), int(nm.sum()), int(nst.sum())
+        """Software pipeline over two lanes: the extraction of batch k (worker threads, extractor
+        streams) runs while batch k-1 is tracked on this thread (matcher / pose / torch streams)."""
+        lane = lanes[state["k"] % 2]
+        te = time.perf_counter()
+        fut = ex_pool.submit(lane.extract)
+        res = (0, 0, 0)
+        if state["ready"] is not None:
+            res = state["ready"].track()
+        fut.result()
+        phase_acc["step_wall"] = phase_acc.get("step_wall", 0.0) + (time.perf_counter() - te) * 1e3
+        state["ready"] = lane
+        state["k"] += 1
+        return res
+
+    def drain():
+        if state["ready"] is not None:
+            state["ready"].track()
+            state["ready"] = None
 
     for _ in range(args.warmup):
         step()
+    drain()
+    step()   # prime the pipeline: one batch extracted, awaiting tracking
     stage_acc.clear()
     phase_acc.clear()
     kernel_ms.clear()
@@ -250,6 +289,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    drain()   # the batch extracted by the last timed step (outside the timed region)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
