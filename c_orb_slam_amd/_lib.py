@@ -12,7 +12,8 @@ import numpy as np
 
 PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
-LIB_PATH = PKG / "liborbslam_gpu.so"
+# ORBGPU_LIB: an instrumented build (make -C c_orb_slam_amd/csrc prof) for tools/ only
+LIB_PATH = Path(os.environ["ORBGPU_LIB"]) if os.environ.get("ORBGPU_LIB") else PKG / "liborbslam_gpu.so"
 HEADER = ROOT / "include" / "orbslam_gpu.h"
 
 ORB_OK, ORB_E_INVALID, ORB_E_HIP, ORB_E_CAPACITY, ORB_E_NODEVICE = 0, -1, -2, -3, -4
@@ -146,6 +147,7 @@ def lib():
     L.orbgpu_unit_csum.argtypes = [vp, i32, vp]
     L.orbgpu_unit_ldlt_factor.argtypes = [i32, vp, vp]
     L.orbgpu_unit_wave_tree.argtypes = [vp, vp]
+    L.orbgpu_debug_prof.argtypes = [vp]
     L.Sim3Solver_create.argtypes = [i32, vp, vp, vp, vp, vp, i32, vp, vp, i32, P(vp)]
     L.Sim3Solver_destroy.argtypes = [vp]
     L.Sim3Solver_set_ransac.argtypes = [vp, C.c_double, i32, i32]

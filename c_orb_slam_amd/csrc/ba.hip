@@ -47,6 +47,19 @@ HD void se3_normalize(Se3& T) {
     quat_normalize(T.q);
 }
 
+// Eigen Quaternion(Matrix3) branch for a dominant diagonal entry I (static indices keep the
+// matrix in registers on the device)
+template <int I>
+HD void quat_from_R_diag(const double* m, double* q) {
+    constexpr int J = (I + 1) % 3, K = (J + 1) % 3;
+    double t = sqrt(((m[I * 4] - m[J * 4]) - m[K * 4]) + 1.0);
+    q[I] = 0.5 * t;
+    t = 0.5 / t;
+    q[3] = (m[K * 3 + J] - m[J * 3 + K]) * t;
+    q[J] = (m[J * 3 + I] + m[I * 3 + J]) * t;
+    q[K] = (m[K * 3 + I] + m[I * 3 + K]) * t;
+}
+
 HD void quat_from_R(const double* m, double* q) {
     double t = (m[0] + m[4]) + m[8];
     if (t > 0) {
@@ -59,14 +72,10 @@ HD void quat_from_R(const double* m, double* q) {
     } else {
         int i = 0;
         if (m[4] > m[0]) i = 1;
-        if (m[8] > m[i * 4]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(((m[i * 4] - m[j * 4]) - m[k * 4]) + 1.0);
-        q[i] = 0.5 * t;
-        t = 0.5 / t;
-        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * t;
-        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * t;
-        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * t;
+        if (m[8] > (i == 0 ? m[0] : m[4])) i = 2;
+        if (i == 0) quat_from_R_diag<0>(m, q);
+        else if (i == 1) quat_from_R_diag<1>(m, q);
+        else quat_from_R_diag<2>(m, q);
     }
 }
 
@@ -1182,18 +1191,20 @@ __global__ void __launch_bounds__(256) k_tile_unpack(int n, double* __restrict__
 // (types_six_dof_expmap.cpp:266-364), solved by LinearSolverDense (Eigen LDLT with diagonal
 // pivoting).  The whole call -- 4 rounds of optimize(10), each restarted from mTcw, with the
 // outlier classification after every round -- is ONE persistent workgroup per frame (a batch
-// of frames is one launch): the per-iteration work (errors, Jacobians, 6x6 system) is spread
-// over 1024 threads with the canonical 64-tree sums of oracle/ba.c, the 6x6 pivoted LDL^T,
-// the SE3 update and the LM control run on thread 0 between barriers.
+// of frames is one launch).  Per LM iteration: one fused pass over the active edges (errors,
+// robust chi2 and the 27 terms of the 6x6 system, canonical 64-tree sums of oracle/ba.c),
+// then per trial the register-resident pivoted LDL^T + SE3 update on thread 0 and one error
+// pass.  Edges are 32 B (the reference's float inputs; converted to double on load) and each
+// wave prefetches its next chunk's edges while it computes the current one.
 struct PoseEdgeDev {
-    double Xw[3], obs[3];
-    double info, delta, dsqr;
-    int stereo, kp;
+    float Xw[3], obs[3];   // GetWorldPos(); kpUn.pt.x, .y, mvuRight
+    float info;            // mvInvLevelSigma2[octave]
+    int meta;              // bit 31: stereo edge; bits 0-30: keypoint index
 };
 
 struct PoseProbDev {
     int ne, e0;            // edges E[e0 .. e0+ne)
-    int nbad, N;           // out: nBad of the last round (-1: < 3 correspondences, -2: > capacity)
+    int nbad, N;           // out: nBad of the last round (-1: < 3 correspondences)
     Se3 T0;                // Converter::toSE3Quat(pFrame->mTcw)
     Se3 T;                 // out
     double fx, fy, cx, cy, bf;
@@ -1208,9 +1219,32 @@ struct PoseProbDev {
     uint8_t* outlier;
 };
 
-__device__ __forceinline__ void pose_err(const PoseEdgeDev& e, const Se3& T, const PoseProbDev& P, double* err) {
+// one edge in double (the g2o edge's _measurement / information / Huber delta)
+struct PoseEdgeD {
+    double X[3], obs[3], info, delta, dsqr;
+    bool stereo;
+};
+
+__device__ __forceinline__ PoseEdgeD pose_edge_load(const PoseEdgeDev* E, int i, double dM, double dS) {
+    const uint4* p = reinterpret_cast<const uint4*>(E + i);
+    const uint4 a = p[0], b = p[1];
+    PoseEdgeD e;
+    e.X[0] = (double)__uint_as_float(a.x);
+    e.X[1] = (double)__uint_as_float(a.y);
+    e.X[2] = (double)__uint_as_float(a.z);
+    e.obs[0] = (double)__uint_as_float(a.w);
+    e.obs[1] = (double)__uint_as_float(b.x);
+    e.obs[2] = (double)__uint_as_float(b.y);
+    e.info = (double)__uint_as_float(b.z);
+    e.stereo = (b.w >> 31) != 0;
+    e.delta = e.stereo ? dS : dM;   // RobustKernelHuber delta = sqrt(chi2 threshold) as float
+    e.dsqr = e.delta * e.delta;
+    return e;
+}
+
+__device__ __forceinline__ void pose_err(const PoseEdgeD& e, const Se3& T, const PoseProbDev& P, double* err) {
     double p[3];
-    se3_map(T, e.Xw, p);
+    se3_map(T, e.X, p);
     if (!e.stereo) {
         const double px = p[0] / p[2], py = p[1] / p[2];
         err[0] = e.obs[0] - (px * P.fx + P.cx);
@@ -1226,93 +1260,138 @@ __device__ __forceinline__ void pose_err(const PoseEdgeDev& e, const Se3& T, con
     }
 }
 
-__device__ __forceinline__ double pose_chi2(const PoseEdgeDev& e, const double* err) {
-    double s = 0;
-    const int D = e.stereo ? 3 : 2;
-    for (int j = 0; j < D; j++) s += err[j] * (e.info * err[j]);
+__device__ __forceinline__ double pose_chi2(const PoseEdgeD& e, const double* err) {
+    double s = err[0] * (e.info * err[0]);
+    s += err[1] * (e.info * err[1]);
+    if (e.stereo) s += err[2] * (e.info * err[2]);
     return s;
 }
 
-__device__ __forceinline__ double pose_rho0(const PoseEdgeDev& e, double c, bool robust) {
+__device__ __forceinline__ double pose_rho0(const PoseEdgeD& e, double c, bool robust) {
     if (!robust || c <= e.dsqr) return c;
     const double sq = sqrt(c);
     return (2 * sq) * e.delta - e.dsqr;
 }
 
 // Eigen::LDLT<MatrixXd> compute + solve (diagonal pivoting, sequential dot products),
-// identical operation sequence to oracle ora_ldlt_pivot_solve.  H is destroyed.
-// H, tmp, y, tr live in LDS (dynamic indexing stays out of scratch).
-__device__ bool ldlt_pivot6(double* H, const double* b, double* x, double* tmp, double* y, int* tr) {
+// identical operation sequence to oracle ora_ldlt_pivot_solve, fully unrolled so the 6x6
+// stays in registers: the data-dependent pivot swaps are unrolled conditional swaps.
+__device__ __forceinline__ bool ldlt_pivot6(double* M, const double* b, double* x) {
     constexpr int n = 6;
+    int tr[n];
+    double tmp[n];
     int sign = 0;
-#define M(i, j) H[(i) * n + (j)]
+    bool stop = false;
+#pragma unroll
     for (int k = 0; k < n; k++) {
-        int idx = k;
-        double big = fabs(M(k, k));
-        for (int i = k + 1; i < n; i++)
-            if (fabs(M(i, i)) > big) {
-                big = fabs(M(i, i));
-                idx = i;
-            }
-        tr[k] = idx;
-        if (idx != k) {
-            for (int j = 0; j < k; j++) { const double t = M(k, j); M(k, j) = M(idx, j); M(idx, j) = t; }
-            for (int i = idx + 1; i < n; i++) { const double t = M(i, k); M(i, k) = M(i, idx); M(i, idx) = t; }
-            { const double t = M(k, k); M(k, k) = M(idx, idx); M(idx, idx) = t; }
-            for (int i = k + 1; i < idx; i++) { const double t = M(i, k); M(i, k) = M(idx, i); M(idx, i) = t; }
-        }
-        if (k > 0) {
-            for (int j = 0; j < k; j++) tmp[j] = M(j, j) * M(k, j);
-            double s = 0;
-            for (int j = 0; j < k; j++) s += M(k, j) * tmp[j];
-            M(k, k) -= s;
+        if (!stop) {
+            int idx = k;
+            double big = fabs(M[k * n + k]);
+#pragma unroll
             for (int i = k + 1; i < n; i++) {
-                double t = 0;
-                for (int j = 0; j < k; j++) t += M(i, j) * tmp[j];
-                M(i, k) -= t;
+                const double d = fabs(M[i * n + i]);
+                if (d > big) {
+                    big = d;
+                    idx = i;
+                }
+            }
+            tr[k] = idx;
+#pragma unroll
+            for (int i = k + 1; i < n; i++)
+                if (idx == i) {
+#pragma unroll
+                    for (int j = 0; j < k; j++) { const double t = M[k * n + j]; M[k * n + j] = M[i * n + j]; M[i * n + j] = t; }
+#pragma unroll
+                    for (int r = i + 1; r < n; r++) { const double t = M[r * n + k]; M[r * n + k] = M[r * n + i]; M[r * n + i] = t; }
+                    { const double t = M[k * n + k]; M[k * n + k] = M[i * n + i]; M[i * n + i] = t; }
+#pragma unroll
+                    for (int r = k + 1; r < i; r++) { const double t = M[r * n + k]; M[r * n + k] = M[i * n + r]; M[i * n + r] = t; }
+                }
+            if (k > 0) {
+#pragma unroll
+                for (int j = 0; j < k; j++) tmp[j] = M[j * n + j] * M[k * n + j];
+                double s = 0;
+#pragma unroll
+                for (int j = 0; j < k; j++) s += M[k * n + j] * tmp[j];
+                M[k * n + k] -= s;
+#pragma unroll
+                for (int i = k + 1; i < n; i++) {
+                    double t = 0;
+#pragma unroll
+                    for (int j = 0; j < k; j++) t += M[i * n + j] * tmp[j];
+                    M[i * n + k] -= t;
+                }
+            }
+            const double akk = M[k * n + k];
+            const bool valid = fabs(akk) > 0.0;
+            if (k == 0 && !valid) {
+#pragma unroll
+                for (int j = 0; j < n; j++) tr[j] = j;
+                sign = 0;
+                stop = true;
+            } else {
+                if (valid) {
+#pragma unroll
+                    for (int i = k + 1; i < n; i++) M[i * n + k] /= akk;
+                }
+                if (sign == 1) { if (akk < 0) sign = 3; }
+                else if (sign == 2) { if (akk > 0) sign = 3; }
+                else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
             }
         }
-        const double akk = M(k, k);
-        const bool valid = fabs(akk) > 0.0;
-        if (k == 0 && !valid) {
-            for (int j = k; j < n; j++) tr[j] = j;
-            sign = 0;
-            break;
-        }
-        if (valid)
-            for (int i = k + 1; i < n; i++) M(i, k) /= akk;
-        if (sign == 1) { if (akk < 0) sign = 3; }
-        else if (sign == 2) { if (akk > 0) sign = 3; }
-        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
     }
     if (!(sign == 1 || sign == 0)) return false;
+    double y[n];
+#pragma unroll
     for (int i = 0; i < n; i++) y[i] = b[i];
-    for (int k = 0; k < n; k++) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+#pragma unroll
+    for (int k = 0; k < n; k++)
+#pragma unroll
+        for (int i = k + 1; i < n; i++)
+            if (tr[k] == i) { const double t = y[k]; y[k] = y[i]; y[i] = t; }
+#pragma unroll
     for (int i = 0; i < n; i++)
-        for (int j = 0; j < i; j++) y[i] -= M(i, j) * y[j];
-    for (int i = 0; i < n; i++) y[i] = fabs(M(i, i)) > DBL_MIN ? y[i] / M(i, i) : 0.0;
+#pragma unroll
+        for (int j = 0; j < i; j++) y[i] -= M[i * n + j] * y[j];
+#pragma unroll
+    for (int i = 0; i < n; i++) y[i] = fabs(M[i * n + i]) > DBL_MIN ? y[i] / M[i * n + i] : 0.0;
+#pragma unroll
     for (int i = n - 1; i >= 0; i--)
-        for (int j = n - 1; j > i; j--) y[i] -= M(j, i) * y[j];
-    for (int k = n - 1; k >= 0; k--) { const double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+#pragma unroll
+        for (int j = n - 1; j > i; j--) y[i] -= M[j * n + i] * y[j];
+#pragma unroll
+    for (int k = n - 1; k >= 0; k--)
+#pragma unroll
+        for (int i = k + 1; i < n; i++)
+            if (tr[k] == i) { const double t = y[k]; y[k] = y[i]; y[i] = t; }
+#pragma unroll
     for (int i = 0; i < n; i++) x[i] = y[i];
-#undef M
     return true;
 }
 
 constexpr int kPoseMaxEdges = 8192;
-constexpr int kPoseThreads = 512;   // 256 VGPRs per lane for the 27-term system build
+constexpr int kPoseThreads = 512;   // 256 VGPRs per lane for the fused 28-term pass
 constexpr int kPosePer = kPoseMaxEdges / kPoseThreads;
 
-// Block-wide canonical sum (ora_csum) of K per-active-edge values f(a, out[K]), a < nA:
-// 64-edge chunk trees per wave, then one thread per entry over the chunk sums.
+// Block-wide canonical sums (ora_csum) of K per-active-edge values: wave w owns chunks
+// c = w, w + nw, ... of 64 active edges; the edge of chunk c + nw is loaded while chunk c is
+// computed.  f(e, i, out[K]) evaluates active edge i (edge e loaded).  Chunk trees go to
+// cs[q][c]; thread q < K finishes entry q.
 template <int K, class F>
-__device__ __forceinline__ void block_csum(F f, int nA, double (*cs)[kPoseMaxEdges / 64], double* res) {
+__device__ __forceinline__ void pose_pass(F f, int nA, const int* aE, const PoseEdgeDev* E, double dM, double dS,
+                                          double (*cs)[kPoseMaxEdges / 64], double* res) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int m = (nA + 63) >> 6;
-    for (int c = w; c < m; c += nw) {
-        const int a = c * 64 + lane;
+    int c = w;
+    int a = c * 64 + lane;
+    int i = a < nA ? aE[a] : 0;
+    PoseEdgeD e = pose_edge_load(E, i, dM, dS);
+    while (c < m) {
+        const int cn = c + nw, an = cn * 64 + lane;
+        const int in = (cn < m && an < nA) ? aE[an] : 0;
+        const PoseEdgeD en = pose_edge_load(E, in, dM, dS);   // prefetch the next chunk's edge
         double v[K];
-        if (a < nA) f(a, v);
+        if (a < nA) f(e, i, v);
         else
 #pragma unroll
             for (int q = 0; q < K; q++) v[q] = 0.0;
@@ -1321,6 +1400,10 @@ __device__ __forceinline__ void block_csum(F f, int nA, double (*cs)[kPoseMaxEdg
             const double t = nA == 1 ? v[q] : wave_tree(v[q]);   // ora_csum keeps a single term untouched
             if (lane == 0) cs[q][c] = t;
         }
+        c = cn;
+        a = an;
+        i = in;
+        e = en;
     }
     __syncthreads();
     if ((int)threadIdx.x < K) res[threadIdx.x] = nA > 0 ? local_csum_inplace(cs[threadIdx.x], m) : 0.0;
@@ -1336,14 +1419,14 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     uint8_t* outl = outlAll + P.e0;
     __shared__ uint8_t level[kPoseMaxEdges], robust[kPoseMaxEdges];
     __shared__ int aE[kPoseMaxEdges];
-    __shared__ double cs[27][kPoseMaxEdges / 64];
+    __shared__ double cs[28][kPoseMaxEdges / 64];
     __shared__ double red[32];
     __shared__ Se3 T, Tbak;
-    __shared__ double xs[6], Hs[21], bs[6], Hd[36], xn[6], lt[12];
-    __shared__ int ltr[6];
+    __shared__ double xs[6], Hs[21], bs[6];
     __shared__ double lambda, ni, currentChi, iniChi;
     __shared__ int nA, nBadLM, qmax, again, term, nBad, okS, wsum[16];
     const int tid = threadIdx.x;
+    const double dM = (double)(float)sqrt(5.991), dS = (double)(float)sqrt(7.815);
     if (ne < 0) return;   // device mode: capacity exceeded (reported by the host)
     if (ne < 3) {
         if (tid == 0) {
@@ -1352,7 +1435,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
         }
         if (P.Tcw_out) {
             if (tid < 16) P.Tcw_out[tid] = P.Tcw[tid];
-            for (int i = tid; i < ne; i += blockDim.x) P.outlier[E[i].kp] = 0;
+            for (int i = tid; i < ne; i += blockDim.x) P.outlier[E[i].meta & 0x7fffffff] = 0;
         }
         return;
     }
@@ -1363,6 +1446,13 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     }
     __syncthreads();
     const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
+    // computeActiveErrors + activeRobustChi2 term of edge i
+    auto err_term = [&](const PoseEdgeD& e, int i, double* v) {
+        double e3[3];
+        pose_err(e, T, P, e3);
+        for (int j = 0; j < 3; j++) err[3 * i + j] = e3[j];
+        v[0] = pose_rho0(e, pose_chi2(e, e3), robust[i]);
+    };
     for (int it = 0; it < 4; it++) {
         if (tid == 0) {
             T = P.T0;   // vSE3->setEstimate(Converter::toSE3Quat(pFrame->mTcw)) every round
@@ -1390,23 +1480,20 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
         }
         const int na = nA;
         if (na > 0) {   // optimize(10); without active edges the vertex is not optimised at all
+            ORBGPU_PROF_START;
             for (int k = 0; k < 10; k++) {
-                // computeActiveErrors + activeRobustChi2
-                block_csum<1>([&](int a, double* v) {
-                    const int i = aE[a];
+                ORBGPU_PROF_MARK(0);
+                // computeActiveErrors + activeRobustChi2 (entry 0) and buildSystem (entries 1..27:
+                // J^T W J upper triangle, -J^T W e), one pass, canonical sums per entry
+                pose_pass<28>([&](const PoseEdgeD& e, int i, double* v) {
                     double e3[3];
-                    pose_err(E[i], T, P, e3);
+                    pose_err(e, T, P, e3);
                     for (int j = 0; j < 3; j++) err[3 * i + j] = e3[j];
-                    v[0] = pose_rho0(E[i], pose_chi2(E[i], e3), robust[i]);
-                }, na, cs, red);
-                if (tid == 0) currentChi = iniChi = red[0];
-                // buildSystem: J^T W J and -J^T W e per active edge, canonical sums
-                block_csum<27>([&](int a, double* v) {
-                    const int i = aE[a];
-                    const PoseEdgeDev e = E[i];
-                    const double e3[3] = {err[3 * i], err[3 * i + 1], err[3 * i + 2]};
+                    const double c = pose_chi2(e, e3);
+                    const bool rb = robust[i];
+                    v[0] = pose_rho0(e, c, rb);
                     double p[3];
-                    se3_map(T, e.Xw, p);
+                    se3_map(T, e.X, p);
                     const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
                     double J[18];
                     J[0] = ((x * y) * invz_2) * P.fx;
@@ -1428,8 +1515,6 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                     J[16] = 0;
                     J[17] = J[5] - (P.bf * invz_2);
                     const int D = e.stereo ? 3 : 2;
-                    const double c = pose_chi2(e, e3);
-                    const bool rb = robust[i];
                     double r1 = 1.;
                     if (rb && !(c <= e.dsqr)) r1 = e.delta / sqrt(c);
                     const double wgt = rb ? r1 * e.info : e.info;
@@ -1446,20 +1531,22 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
 #pragma unroll
                         for (int kk = 0; kk < 3; kk++)
                             if (kk < D) sb += J[kk * 6 + r] * omr[kk];
-                        v[21 + r] = sb;
+                        v[22 + r] = sb;
 #pragma unroll
                         for (int cc = r; cc < 6; cc++) {
                             double hh = 0;
 #pragma unroll
                             for (int kk = 0; kk < 3; kk++)
                                 if (kk < D) hh += (J[kk * 6 + r] * wgt) * J[kk * 6 + cc];
-                            v[r * 6 - (r * (r - 1)) / 2 + (cc - r)] = hh;
+                            v[1 + r * 6 - (r * (r - 1)) / 2 + (cc - r)] = hh;
                         }
                     }
-                }, na, cs, red);
-                if (tid < 27) {
-                    if (tid < 21) Hs[tid] = red[tid];
-                    else bs[tid - 21] = red[tid];
+                }, na, aE, E, dM, dS, cs, red);
+                ORBGPU_PROF_MARK(1);
+                if (tid < 28) {
+                    if (tid == 0) currentChi = iniChi = red[0];
+                    else if (tid < 22) Hs[tid - 1] = red[tid];
+                    else bs[tid - 22] = red[tid];
                 }
                 __syncthreads();
                 if (tid == 0) {
@@ -1476,14 +1563,19 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                 do {
                     if (tid == 0) {
                         Tbak = T;
+                        double Hd[36], xn[6], bb[6];
+#pragma unroll
                         for (int r = 0, q = 0; r < 6; r++)
+#pragma unroll
                             for (int cc = r; cc < 6; cc++, q++) {
                                 double h = Hs[q];
                                 if (cc == r) h += lambda;
                                 Hd[r * 6 + cc] = h;
                                 Hd[cc * 6 + r] = h;
                             }
-                        const bool ok2 = ldlt_pivot6(Hd, bs, xn, lt, lt + 6, ltr);
+#pragma unroll
+                        for (int j = 0; j < 6; j++) bb[j] = bs[j];
+                        const bool ok2 = ldlt_pivot6(Hd, bb, xn);
                         if (ok2)
                             for (int j = 0; j < 6; j++) xs[j] = xn[j];
                         okS = ok2 ? 1 : 0;
@@ -1493,13 +1585,9 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                         T = r;
                     }
                     __syncthreads();
-                    block_csum<1>([&](int a, double* v) {
-                        const int i = aE[a];
-                        double e3[3];
-                        pose_err(E[i], T, P, e3);
-                        for (int j = 0; j < 3; j++) err[3 * i + j] = e3[j];
-                        v[0] = pose_rho0(E[i], pose_chi2(E[i], e3), robust[i]);
-                    }, na, cs, red);
+                    ORBGPU_PROF_MARK(2);
+                    pose_pass<1>(err_term, na, aE, E, dM, dS, cs, red);
+                    ORBGPU_PROF_MARK(3);
                     if (tid == 0) {
                         double tempChi = red[0];
                         if (!okS) tempChi = DBL_MAX;
@@ -1535,6 +1623,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                         }
                     }
                     __syncthreads();
+                    ORBGPU_PROF_MARK(4);
                 } while (again);
                 if (term) break;
             }
@@ -1544,7 +1633,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
         __syncthreads();
         int mybad = 0;
         for (int i = tid; i < ne; i += blockDim.x) {
-            const PoseEdgeDev& e = E[i];
+            const PoseEdgeD e = pose_edge_load(E, i, dM, dS);
             double e3[3] = {err[3 * i], err[3 * i + 1], err[3 * i + 2]};
             if (outl[i]) {
                 pose_err(e, T, P, e3);
@@ -1581,7 +1670,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
             o[12] = o[13] = o[14] = 0.f;
             o[15] = 1.f;
         }
-        for (int i = tid; i < ne; i += blockDim.x) P.outlier[E[i].kp] = outl[i];
+        for (int i = tid; i < ne; i += blockDim.x) P.outlier[E[i].meta & 0x7fffffff] = outl[i];
     }
 }
 
@@ -1603,7 +1692,6 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_pack(PoseProbDev* probs, 
         se3_normalize(P.T0);
     }
     __syncthreads();
-    const double deltaMono = (double)(float)sqrt(5.991), deltaStereo = (double)(float)sqrt(7.815);
     for (int c0 = 0; c0 < N; c0 += kPoseThreads) {
         const int i = c0 + tid;
         const int f = (i < N && P.has_mp[i]) ? 1 : 0;
@@ -1621,14 +1709,11 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_pack(PoseProbDev* probs, 
             if (k < kPoseMaxEdges) {
                 PoseEdgeDev e;
                 for (int j = 0; j < 3; j++) {
-                    e.Xw[j] = (double)P.Xw[3 * i + j];
-                    e.obs[j] = (double)P.obs[3 * i + j];
+                    e.Xw[j] = P.Xw[3 * i + j];
+                    e.obs[j] = P.obs[3 * i + j];
                 }
-                e.stereo = !(P.obs[3 * i + 2] < 0) ? 1 : 0;
-                e.info = (double)P.inv_sigma2[i];
-                e.delta = e.stereo ? deltaStereo : deltaMono;
-                e.dsqr = e.delta * e.delta;
-                e.kp = i;
+                e.info = P.inv_sigma2[i];
+                e.meta = i | (!(P.obs[3 * i + 2] < 0) ? (int)0x80000000u : 0);
                 E[k] = e;
             }
         }
@@ -1755,7 +1840,6 @@ int PoseEngine::run(int count, const pose_problem* P, float* Tcw_out, uint8_t* c
     PoseProbDev* hp = (PoseProbDev*)h;
     PoseEdgeDev* he = (PoseEdgeDev*)(h + bProb);
     uint8_t* hOut = (uint8_t*)(h + bProb + bEdge + bErr);
-    const double deltaMono = (double)(float)sqrt(5.991), deltaStereo = (double)(float)sqrt(7.815);
     int e0 = 0;
     for (int f = 0; f < count; f++) {
         const pose_problem& Q = P[f];
@@ -1769,14 +1853,11 @@ int PoseEngine::run(int count, const pose_problem* P, float* Tcw_out, uint8_t* c
             if (!Q.has_mp[i]) continue;
             PoseEdgeDev& e = he[e0++];
             for (int j = 0; j < 3; j++) {
-                e.Xw[j] = (double)Q.Xw[3 * i + j];
-                e.obs[j] = (double)Q.obs[3 * i + j];
+                e.Xw[j] = Q.Xw[3 * i + j];
+                e.obs[j] = Q.obs[3 * i + j];
             }
-            e.stereo = !(Q.obs[3 * i + 2] < 0) ? 1 : 0;
-            e.info = (double)Q.inv_sigma2[i];
-            e.delta = e.stereo ? deltaStereo : deltaMono;
-            e.dsqr = e.delta * e.delta;
-            e.kp = i;
+            e.info = Q.inv_sigma2[i];
+            e.meta = i | (!(Q.obs[3 * i + 2] < 0) ? (int)0x80000000u : 0);
         }
     }
     PoseProbDev* dp = (PoseProbDev*)d;
@@ -2447,6 +2528,19 @@ int debug_ldlt_factor(int n, const double* S, double* out) {
 __global__ void k_unit_wave_tree(const double* v, double* out) {
     const double t = wave_tree(v[threadIdx.x]);
     if (threadIdx.x == 0) *out = t;
+}
+
+// instrumented builds only: read and clear this unit's section timers
+int debug_prof(unsigned long long* out32) {
+#ifdef ORBGPU_PROF
+    ORB_HIP_CHECK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_orbgpu_prof), sizeof(unsigned long long) * 32));
+    unsigned long long z[32] = {};
+    ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_orbgpu_prof), z, sizeof(z)));
+    return 0;
+#else
+    (void)out32;
+    return -1;
+#endif
 }
 
 int debug_wave_tree(const double* v64, double* out) {

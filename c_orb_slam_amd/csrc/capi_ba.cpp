@@ -263,6 +263,8 @@ int orbgpu_unit_ldlt_factor(int n, const double* S, double* out) {
     return orbgpu::debug_ldlt_factor(n, S, out) ? ORB_E_HIP : ORB_OK;
 }
 
+int orbgpu_debug_prof(unsigned long long* out32) { return out32 ? orbgpu::debug_prof(out32) : ORB_E_INVALID; }
+
 int orbgpu_unit_wave_tree(const double* v64, double* out) {
     if (!v64 || !out) return ORB_E_INVALID;
     int rc = 0;

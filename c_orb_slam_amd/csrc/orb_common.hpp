@@ -124,3 +124,21 @@ __device__ __forceinline__ int wave_sum(int v) {
 }
 
 }  // namespace orbgpu
+
+// Section timers for instrumented builds (make prof -> -DORBGPU_PROF): clock64() deltas of
+// workgroup 0 / thread 0 accumulated into g_orbgpu_prof[slot]; compiled out otherwise.
+#ifdef ORBGPU_PROF
+static __device__ unsigned long long g_orbgpu_prof[32];   // one copy per translation unit
+#define ORBGPU_PROF_START unsigned long long _orbgpu_pt = clock64()
+#define ORBGPU_PROF_MARK(i)                                                                   \
+    do {                                                                                      \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                                            \
+            const unsigned long long _t = clock64();                                          \
+            atomicAdd(&g_orbgpu_prof[i], _t - _orbgpu_pt);                                    \
+            _orbgpu_pt = _t;                                                                  \
+        }                                                                                     \
+    } while (0)
+#else
+#define ORBGPU_PROF_START
+#define ORBGPU_PROF_MARK(i)
+#endif

@@ -517,6 +517,9 @@ int orbgpu_unit_csum(const double* v, int n, double* out);
 int orbgpu_unit_ldlt_factor(int n, const double* S, double* out);
 /* one wave's canonical 64-tree of v64[0..64) (cross-lane permlane/DPP path) */
 int orbgpu_unit_wave_tree(const double* v64, double* out);
+/* Instrumented builds only (make prof): read and clear the BA/pose section timers (32 x u64
+ * clock64 deltas of workgroup 0); ORB_E_INVALID in normal builds. */
+int orbgpu_debug_prof(unsigned long long* out32);
 
 #ifdef __cplusplus
 }

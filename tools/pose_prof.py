@@ -1,0 +1,22 @@
+"""Section timers of k_pose_opt (workgroup 0) from the instrumented build:
+   make -C c_orb_slam_amd/csrc prof && ORBGPU_LIB=build/liborbslam_gpu_prof.so python tools/pose_prof.py"""
+import ctypes as C
+import sys
+
+sys.path.insert(0, ".")
+sys.path.insert(0, "tests")
+from c_orb_slam_amd import PoseOptimizationBatch  # noqa: E402
+from c_orb_slam_amd._lib import lib  # noqa: E402
+from pose_cases import pose_problem  # noqa: E402
+
+frames = [pose_problem(s, N=1500) for s in range(64)]
+PoseOptimizationBatch(frames)
+out = (C.c_ulonglong * 32)()
+lib().orbgpu_debug_prof(out)
+PoseOptimizationBatch(frames)
+lib().orbgpu_debug_prof(out)
+names = ["iter_top", "fused28", "solve_thread0", "trial_pass", "decide"]
+v = [out[i] for i in range(len(names))]
+tot = sum(v)
+print("cycles (frame 0, one call):", dict(zip(names, v)), "total", tot)
+print({n: round(x / tot, 3) for n, x in zip(names, v)})
