@@ -10,9 +10,9 @@ mkdir -p "$OUT"
 cd "$R" || exit 1
 echo "[gpu_check] pytest -m gpu" && date
 if [ -n "$KEXPR" ]; then
-  timeout -k 10 700 python -m pytest tests -m gpu -x -q -k "$KEXPR" > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+  timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$KEXPR" > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
 else
-  timeout -k 10 700 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+  timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
 fi
 tail -3 "$OUT/pytest_gpu.log"
 echo "[gpu_check] bench" && date
