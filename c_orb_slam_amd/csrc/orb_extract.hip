@@ -36,57 +36,115 @@ static const int8_t kPattern[256 * 4] = {
 };
 
 // ------------------------------------------------------------------ kernels
-// copyMakeBorder(image, temp, 19,19,19,19, BORDER_REFLECT_101), 4 bytes/thread.
-__global__ void k_pyr_level0(const uint8_t* __restrict__ src, size_t src_stride, int step, int W,
-                             int H, uint8_t* __restrict__ pyr, size_t img_bytes, int pitch, int ph) {
+// XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (linear id % 8),
+// so with gridDim.x a multiple of 8 the XCD of block x is x % 8.  Give each XCD a contiguous
+// run of tiles/cells, so the halos that neighbouring tiles share are re-read from that XCD's
+// own L2 instead of being fetched again by a different XCD.
+__device__ __forceinline__ int xcd_tile(int bid, int nb) { return (bid & 7) * (nb >> 3) + (bid >> 3); }
+static inline unsigned grid8(int n) { return (unsigned)((n + 7) & ~7); }
+
+// copyMakeBorder(image, temp, 19,19,19,19, BORDER_REFLECT_101), 16 bytes/thread.
+// Interior chunks: the (arbitrarily aligned) source row is read as aligned dwords and
+// realigned with v_alignbyte; the two border chunks of a row reflect byte by byte.
+__global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ src, size_t src_stride, int step,
+                                                    int W, int H, uint8_t* __restrict__ pyr, size_t img_bytes,
+                                                    int pitch, int ph) {
     const int b = blockIdx.y;
-    const int quads = pitch >> 2;
+    const int chunks = pitch >> 4;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= quads * ph) return;
-    const int py = t / quads, px4 = (t - py * quads) * 4;
+    if (t >= chunks * ph) return;
+    const int py = t / chunks, px0 = (t - py * chunks) * 16;
     const int sy = refl101(py - kEdge, H);
     const uint8_t* srow = src + (size_t)b * src_stride + (size_t)sy * step;
-    uint32_t v = 0;
+    const int x0 = px0 - kEdge;
+    uint4 o;
+    if (x0 >= 0 && x0 + 15 < W) {
+        const uintptr_t a = (uintptr_t)(srow + x0);
+        const uint32_t* a32 = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint32_t w0 = a32[0], w1 = a32[1], w2 = a32[2], w3 = a32[3];
+        const uint32_t w4 = sh ? a32[4] : 0u;   // only when the 16 bytes straddle a 5th dword
+        o.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        o.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        o.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+    } else {
+        uint32_t v[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int px = px4 + k;
-        const int sx = refl101(px - kEdge, W);
-        v |= (uint32_t)srow[sx] << (8 * k);
+        for (int k = 0; k < 16; k++) v[k >> 2] |= (uint32_t)srow[refl101(x0 + k, W)] << (8 * (k & 3));
+        o = make_uint4(v[0], v[1], v[2], v[3]);
     }
-    *reinterpret_cast<uint32_t*>(pyr + (size_t)b * img_bytes + (size_t)py * pitch + px4) = v;
+    *reinterpret_cast<uint4*>(pyr + (size_t)b * img_bytes + (size_t)py * pitch + px0) = o;
 }
 
 // resize(prev level, INTER_LINEAR) for CV_8U (OpenCV 3.2 imgwarp.cpp fixed
 // point: 11-bit coefficients, VResizeLinear<uchar,int,short,FixedPtCast>),
 // written straight into the padded level through the REFLECT_101 map.
-__global__ void k_pyr_resize(uint8_t* __restrict__ pyr, size_t img_bytes, size_t src_off,
-                             int src_pitch, size_t dst_off, int dst_pitch, int dst_ph, int w, int h,
-                             const int* __restrict__ xofs, const short2* __restrict__ xalpha,
-                             const int2* __restrict__ yrows, const short2* __restrict__ ybeta) {
+// One workgroup per PT_W x nrow tile of the padded destination: the source rectangle the
+// tile reads (host-computed, PyrTile) is staged into LDS as aligned dwords, then every
+// thread forms 4 adjacent columns of every 4th row (coefficients of its columns held in
+// registers) and stores dwords, a wave covering 256 contiguous bytes of a row.
+__global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, size_t img_bytes, size_t src_off,
+                                                    int src_pitch, size_t dst_off, int dst_pitch, int dst_ph, int w,
+                                                    int h, const int* __restrict__ xofs,
+                                                    const short2* __restrict__ xalpha, const int2* __restrict__ yrows,
+                                                    const short2* __restrict__ ybeta,
+                                                    const PyrTile* __restrict__ tiles, int ntiles) {
+    extern __shared__ uint32_t s_src[];   // tl.nsr rows x tl.nsw dwords
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    if (tile >= ntiles) return;
+    const PyrTile tl = tiles[tile];
     const int b = blockIdx.y;
-    const int quads = dst_pitch >> 2;
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= quads * dst_ph) return;
-    const int py = t / quads, px4 = (t - py * quads) * 4;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint8_t* base = pyr + (size_t)b * img_bytes;
-    const uint8_t* S = base + src_off + (size_t)kEdge * src_pitch + kEdge;  // prev interior
-    const int y = refl101(py - kEdge, h);
-    const int2 rr = yrows[y];
-    const short2 bb = ybeta[y];
-    const uint8_t* S0 = S + (size_t)rr.x * src_pitch;
-    const uint8_t* S1 = S + (size_t)rr.y * src_pitch;
-    uint32_t v = 0;
+    const uint32_t* S32 = reinterpret_cast<const uint32_t*>(base + src_off + (size_t)(kEdge + tl.sr0) * src_pitch + tl.sc0);
+    const int spw = src_pitch >> 2;
+    for (int r = wid; r < tl.nsr; r += 4)
+        for (int c = lane; c < tl.nsw; c += 64) s_src[r * tl.nsw + c] = S32[(size_t)r * spw + c];
+    const int px = tl.px0 + 4 * lane;
+    const bool col_ok = px < dst_pitch;
+    int lx[4];
+    short2 al[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int x = refl101(px4 + k - kEdge, w);
-        const int sx = xofs[x];
-        const short2 a = xalpha[x];
-        const int D0 = S0[sx] * a.x + S0[sx + (a.y != 0)] * a.y;
-        const int D1 = S1[sx] * a.x + S1[sx + (a.y != 0)] * a.y;
-        const int o = (((bb.x * (D0 >> 4)) >> 16) + ((bb.y * (D1 >> 4)) >> 16) + 2) >> 2;
-        v |= (uint32_t)(uint8_t)o << (8 * k);
+        const int x = refl101(px + k - kEdge, w);
+        lx[k] = col_ok ? xofs[x] + kEdge - tl.sc0 : 0;
+        al[k] = col_ok ? xalpha[x] : make_short2(0, 0);
     }
-    *reinterpret_cast<uint32_t*>(base + dst_off + (size_t)py * dst_pitch + px4) = v;
+    // this thread's rows (j = wid, wid+4, ... < nrow <= PT_H): row taps fetched before the barrier
+    int2 rr[PT_H / 4];
+    short2 bb[PT_H / 4];
+#pragma unroll
+    for (int i = 0; i < PT_H / 4; i++) {
+        const int j = wid + 4 * i;
+        const int y = refl101(tl.py0 + min(j, tl.nrow - 1) - kEdge, h);
+        rr[i] = yrows[y];
+        bb[i] = ybeta[y];
+    }
+    __syncthreads();
+    if (!col_ok) return;
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(s_src);
+    const int rowb = tl.nsw * 4;
+#pragma unroll
+    for (int i = 0; i < PT_H / 4; i++) {
+        const int j = wid + 4 * i;
+        if (j >= tl.nrow) break;
+        const int py = tl.py0 + j;
+        const uint8_t* R0 = sb + (rr[i].x - tl.sr0) * rowb;
+        const uint8_t* R1 = sb + (rr[i].y - tl.sr0) * rowb;
+        const short2 bb_ = bb[i];
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int sx = lx[k];
+            const short2 a = al[k];
+            const int D0 = R0[sx] * a.x + R0[sx + (a.y != 0)] * a.y;
+            const int D1 = R1[sx] * a.x + R1[sx + (a.y != 0)] * a.y;
+            const int o = (((bb_.x * (D0 >> 4)) >> 16) + ((bb_.y * (D1 >> 4)) >> 16) + 2) >> 2;
+            v |= (uint32_t)(uint8_t)o << (8 * k);
+        }
+        *reinterpret_cast<uint32_t*>(base + dst_off + (size_t)py * dst_pitch + px) = v;
+    }
 }
 
 // GaussianBlur(7x7, sigma 2, REFLECT_101) on CV_8U: int taps (round(k*256)),
@@ -97,10 +155,12 @@ __global__ void k_pyr_resize(uint8_t* __restrict__ pyr, size_t img_bytes, size_t
 constexpr int BT_W = 128, BT_H = 32, BT_LW = BT_W + 8;  // staged cols: interior [x0-3, x0+133)
 __global__ void __launch_bounds__(256) k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                size_t img_bytes, size_t blur_bytes,
-                                               const BlurTile* __restrict__ tiles) {
+                                               const BlurTile* __restrict__ tiles, int ntiles) {
     __shared__ uint32_t s_src[(BT_H + 6) * (BT_LW / 4)];
     __shared__ int4 s_row[(BT_H + 6) * (BT_W / 4)];
-    const BlurTile tl = tiles[blockIdx.x];
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    if (tile >= ntiles) return;
+    const BlurTile tl = tiles[tile];
     const int b = blockIdx.y;
     const uint8_t* P = pyr + (size_t)b * img_bytes + tl.off;           // padded level base
     uint8_t* O = blur + (size_t)b * blur_bytes + tl.boff;               // unpadded blurred level
@@ -232,11 +292,14 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     __shared__ int s_off[65];
     uint8_t* s_img = reinterpret_cast<uint8_t*>(s_img32);
     uint8_t* s_sc = reinterpret_cast<uint8_t*>(s_sc32);
-    const CellDesc cd = cells[blockIdx.x];
+    // identity cell order: the XCD-contiguous order (xcd_tile) cut FETCH_SIZE 4.8x here but ran
+    // ~9 % slower -- this kernel is VALU-bound and the contiguous runs unbalance the XCDs
+    const int cell = blockIdx.x;
+    const CellDesc cd = cells[cell];
     const int b = blockIdx.y;
     const int rows = cd.r1 - cd.r0, cols = cd.c1 - cd.c0;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    int* cnt_out = counts + (size_t)b * ncells + blockIdx.x;
+    int* cnt_out = counts + (size_t)b * ncells + cell;
     if (rows < 7 || cols < 7) {
         if (tid == 0) *cnt_out = 0;
         return;
@@ -528,7 +591,8 @@ void Extractor::release() {
     auto F = [](void* p) { if (p) (void)hipFree(p); };
     F(d_in_); F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_);
     F(d_lcb_); F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_);
-    F(d_kps_); F(d_desc_); F(d_jobsel_); F(d_jobcnt_); F(d_octlv_); F(d_gscr_); F(d_nout_);
+    F(d_kps_); F(d_desc_); F(d_jobsel_); F(d_jobcnt_); F(d_octlv_); F(d_gscr_); F(d_nout_); F(d_ptiles_);
+    d_ptiles_ = nullptr;
     d_jobsel_ = d_jobcnt_ = d_octlv_ = d_gscr_ = d_nout_ = nullptr;
     d_in_ = d_pyr_ = d_blur_ = nullptr;
     d_slots_ = nullptr; d_counts_ = nullptr; d_cells_ = nullptr; d_tiles_ = nullptr;
@@ -675,6 +739,9 @@ int Extractor::setup_geometry(int W, int H) {
         return o;
     };
     tab_off_.assign(nlevels_, {0, 0, 0, 0});
+    ptiles_.clear();
+    ptile_begin_.assign(nlevels_ + 1, 0);
+    plds_.assign(nlevels_, 0);
     for (int l = 1; l < nlevels_; l++) {
         const int sw = levels_[l - 1].w, sh = levels_[l - 1].h, dw = levels_[l].w, dh = levels_[l].h;
         const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
@@ -707,16 +774,70 @@ int Extractor::setup_geometry(int W, int H) {
             yb[2 * dy] = sat_s((1.f - fy) * 2048);
             yb[2 * dy + 1] = sat_s(fy * 2048);
         }
+        // k_pyr_resize tiles over the padded destination: the source rectangle each reads
+        {
+            const LevelHost& D = levels_[l];
+            auto refl = [](int p, int len) {
+                if (len == 1) return 0;
+                while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
+                return p;
+            };
+            ptile_begin_[l] = (int)ptiles_.size();
+            // tile height: PT_H rows unless the source rectangle would exceed the LDS budget
+            // (scale factors well above the reference's 1.2)
+            auto make = [&](int py0, int px0, int nrow, PyrTile& t) {
+                int r0 = 1 << 30, r1 = -1, c0 = 1 << 30, c1 = -1;
+                for (int py = py0; py < std::min(py0 + nrow, D.ph); py++) {
+                    const int y = refl(py - kEdge, dh);
+                    r0 = std::min(r0, yr[2 * y]);
+                    r1 = std::max(r1, yr[2 * y + 1]);
+                }
+                for (int px = px0; px < std::min(px0 + PT_W, D.pitch); px++) {
+                    const int x = refl(px - kEdge, dw);
+                    c0 = std::min(c0, xofs[x]);
+                    c1 = std::max(c1, xofs[x] + 1);
+                }
+                t.py0 = py0; t.px0 = px0; t.nrow = std::min(nrow, D.ph - py0);
+                t.sr0 = r0; t.nsr = r1 - r0 + 1;
+                t.sc0 = (c0 + kEdge) & ~3;
+                t.nsw = (c1 + kEdge - t.sc0) / 4 + 1;
+                return (size_t)t.nsr * t.nsw * 4 <= (size_t)kPyrLdsMax;
+            };
+            int nrow = PT_H;
+            for (bool ok = false; !ok;) {
+                ok = true;
+                for (int py0 = 0; py0 < D.ph && ok; py0 += nrow)
+                    for (int px0 = 0; px0 < D.pitch && ok; px0 += PT_W) {
+                        PyrTile t;
+                        ok = make(py0, px0, nrow, t);
+                    }
+                if (!ok && --nrow < 1) return -1;
+            }
+            size_t lds = 0;
+            for (int py0 = 0; py0 < D.ph; py0 += nrow)
+                for (int px0 = 0; px0 < D.pitch; px0 += PT_W) {
+                    PyrTile t;
+                    make(py0, px0, nrow, t);
+                    if ((size_t)(t.sc0 + 4 * t.nsw) > (size_t)levels_[l - 1].pitch) return -1;
+                    lds = std::max(lds, (size_t)t.nsr * t.nsw * 4);
+                    ptiles_.push_back(t);
+                }
+            plds_[l] = (int)lds;
+        }
         tab_off_[l][0] = push(xofs.data(), xofs.size() * 4);
         tab_off_[l][1] = push(xal.data(), xal.size() * 2);
         tab_off_[l][2] = push(yr.data(), yr.size() * 4);
         tab_off_[l][3] = push(yb.data(), yb.size() * 2);
     }
+    ptile_begin_[nlevels_] = (int)ptiles_.size();
     // (re)allocate device buffers for maxB_
     auto F = [](void*& p) { if (p) (void)hipFree(p); p = nullptr; };
     F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_lcb_);
-    F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_);
+    F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_); F(d_ptiles_);
     const int B = maxB_;
+    ORB_HIP_CHECK(hipMalloc(&d_ptiles_, std::max<size_t>(ptiles_.size(), 1) * sizeof(PyrTile)));
+    if (!ptiles_.empty())
+        ORB_HIP_CHECK(hipMemcpy(d_ptiles_, ptiles_.data(), ptiles_.size() * sizeof(PyrTile), hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMalloc(&d_pyr_, img_bytes_ * B));
     ORB_HIP_CHECK(hipMalloc(&d_blur_, blur_bytes_ * B));
     ORB_HIP_CHECK(hipMemset(d_blur_, 0, blur_bytes_ * B));
@@ -801,25 +922,26 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     // 1. pyramid
     {
         const LevelHost& L0 = levels_[0];
-        const int n = (L0.pitch / 4) * L0.ph;
+        const int n = (L0.pitch / 16) * L0.ph;
         hipLaunchKernelGGL(k_pyr_level0, dim3((n + 255) / 256, B), dim3(256), 0, s, src, img_stride, step, W, H,
                            (uint8_t*)d_pyr_, img_bytes_, L0.pitch, L0.ph);
         for (int l = 1; l < nlevels_; l++) {
             const LevelHost& L = levels_[l];
             const LevelHost& P = levels_[l - 1];
-            const int nq = (L.pitch / 4) * L.ph;
             const uint8_t* T = (const uint8_t*)d_tabs_;
-            hipLaunchKernelGGL(k_pyr_resize, dim3((nq + 255) / 256, B), dim3(256), 0, s, (uint8_t*)d_pyr_, img_bytes_,
+            const int nt = ptile_begin_[l + 1] - ptile_begin_[l];
+            hipLaunchKernelGGL(k_pyr_resize, dim3(grid8(nt), B), dim3(256), plds_[l], s, (uint8_t*)d_pyr_, img_bytes_,
                                P.off, P.pitch, L.off, L.pitch, L.ph, L.w, L.h,
                                (const int*)(T + tab_off_[l][0]), (const short2*)(T + tab_off_[l][1]),
-                               (const int2*)(T + tab_off_[l][2]), (const short2*)(T + tab_off_[l][3]));
+                               (const int2*)(T + tab_off_[l][2]), (const short2*)(T + tab_off_[l][3]),
+                               (const PyrTile*)d_ptiles_ + ptile_begin_[l], nt);
         }
     }
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
     // 2. blur (independent of keypoints; overlaps nothing yet, kept on the stream)
-    hipLaunchKernelGGL(k_blur7, dim3((unsigned)tiles_.size(), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
-                       (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_);
+    hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
+                       (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_, (int)tiles_.size());
     ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
     // 3. FAST per cell
     const int ncells = (int)cells_.size();

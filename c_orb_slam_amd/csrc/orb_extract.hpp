@@ -33,6 +33,13 @@ struct BlurTile {
     int pitch, bpitch, w, h, tx, ty;
 };
 
+// One destination tile of k_pyr_resize: padded-destination origin and the source
+// rectangle it reads (interior rows [sr0, sr0+nsr), padded dword columns [sc0, sc0+4*nsw)).
+constexpr int PT_W = 256, PT_H = 16, kPyrLdsMax = 48 * 1024;
+struct PyrTile {
+    int py0, px0, nrow, sr0, nsr, sc0, nsw, pad;
+};
+
 struct LevelDev {
     long long off, boff;
     int pitch, bpitch;
@@ -88,6 +95,8 @@ private:
     std::vector<CellDesc> cells_;
     std::vector<int> level_cell_begin_;
     std::vector<BlurTile> tiles_;
+    std::vector<PyrTile> ptiles_;
+    std::vector<int> ptile_begin_, plds_;
     std::vector<std::array<size_t, 4>> tab_off_;
     size_t img_bytes_ = 0, blur_bytes_ = 0, slots_per_image_ = 0;
     int packed_cap_ = 0, sel_cap_ = 0;
@@ -96,6 +105,7 @@ private:
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[7] = {};
     void *d_in_ = nullptr, *d_pyr_ = nullptr, *d_blur_ = nullptr, *d_slots_ = nullptr, *d_counts_ = nullptr;
+    void *d_ptiles_ = nullptr;
     void *d_cells_ = nullptr, *d_tiles_ = nullptr, *d_lcb_ = nullptr, *d_packed_ = nullptr, *d_hdr_ = nullptr;
     void *d_sel_ = nullptr, *d_levels_ = nullptr, *d_tabs_ = nullptr, *d_kps_ = nullptr, *d_desc_ = nullptr;
     int* d_gtotal_ = nullptr;

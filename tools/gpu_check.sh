@@ -23,4 +23,14 @@ export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o bench -- python3 "$R/bench.py" --no-cpu-baseline \
   > "$OUT/prof_bench.log" 2>&1 || { tail -30 "$OUT/prof_bench.log"; exit 1; }
 find "$OUT/prof" -name '*kernel_stats.csv' | head -5
+python3 tools/prof_csv.py "$(find "$OUT/prof" -name '*kernel_stats.csv' | head -1)" 60 > "$OUT/kernel_stats.txt"
+python3 tools/roofline_check.py "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)" "$OUT/bench.json" | tee "$OUT/roofline_check.json"
+echo "[gpu_check] pmc traffic" && date
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace -f csv -d "$OUT/$c" -o ex -- python3 "$R/tools/extract_timing.py" 64 \
+    > "$OUT/$c.log" 2>&1 || { echo "$c pass failed"; tail -20 "$OUT/$c.log"; exit 1; }
+done
+python3 tools/pmc_traffic.py "$(find "$OUT/FETCH_SIZE" -name '*counter_collection.csv' | head -1)" \
+  "$(find "$OUT/WRITE_SIZE" -name '*counter_collection.csv' | head -1)" "$OUT/traffic.json" \
+  "workload: tools/extract_timing.py 64 = the bench roofline pass (left batch, seed 1000, B=64)"
 echo "[gpu_check] done" && date
