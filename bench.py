@@ -95,7 +95,6 @@ def main():
     d_L = torch.from_numpy(lefts).to(dev)
     d_R = torch.from_numpy(rights).to(dev)
     d_obs = torch.ones(cap, dtype=torch.int32, device=dev)
-    d_arange = torch.arange(cap, dtype=torch.int32, device=dev)
     d_outlier = torch.zeros(cap, dtype=torch.uint8, device=dev)
     eye = torch.eye(4, dtype=torch.float32, device=dev)
     poses = torch.from_numpy(np.stack([synthetic.pose_from_rotation(R) for R in Rs])).to(dev)
@@ -103,11 +102,16 @@ def main():
     gH = np.float32(np.float32(48) / np.float32(H))
     P = B - 1
     arr = lambda xs: (C.c_void_p * len(xs))(*xs)
-    from c_orb_slam_amd._lib import pose_problem
+    from c_orb_slam_amd._lib import orb_unproject, pose_frame
     from concurrent.futures import ThreadPoolExecutor
     # HIP's current device is per thread: every worker binds it first
     pool = ThreadPoolExecutor(2, initializer=lambda: torch.cuda.set_device(dev))
-    track_stream = torch.cuda.Stream(device=dev)
+    match_stream = torch.cuda.ExternalStream(L.ORBmatcher_stream(m._h), device=dev)
+
+    def n_field(arr, cls, count):
+        """int32 view of field 0 (the count N) of every struct of a ctypes struct array."""
+        w = C.sizeof(cls) // 4
+        return np.ctypeslib.as_array((C.c_int32 * (count * w)).from_address(C.addressof(arr))).reshape(count, w)[:, 0]
 
     class Lane:
         """One batch in flight: its own extractor pair (pyramids, keypoints) and tracking buffers."""
@@ -125,16 +129,9 @@ def main():
             self.d_last_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
             self.d_cur_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
             self.scale = torch.from_numpy(self.exL.GetScaleFactors()).to(dev)
-            self.kp_f = self.d_kps.view(torch.float32)
-            # PoseOptimization inputs gathered in HBM from the matcher's output
-            self.d_has = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
-            self.d_Xw = torch.empty((P, cap, 3), dtype=torch.float32, device=dev)
-            self.d_pobs = torch.empty((P, cap, 3), dtype=torch.float32, device=dev)
-            self.d_isig = torch.empty((P, cap), dtype=torch.float32, device=dev)
             self.d_Tout = torch.empty((P, 16), dtype=torch.float32, device=dev)
             self.d_poutl = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
             self.isig_tab = torch.from_numpy(self.exL.GetInverseScaleSigmaSquares()).to(dev)
-            self.octv = self.d_kps[1:, :, 5]
             # ctypes views of the batch, built once (device pointers do not move; only counts change)
             self.curs = (orb_frame * P)(*[self.frame_struct(b, poses[b - 1].data_ptr()) for b in range(1, B)])
             self.lasts = (orb_frame * P)(*[self.frame_struct(b, eye.data_ptr()) for b in range(0, B - 1)])
@@ -153,12 +150,24 @@ def main():
             self.s_dR = arr([self.d_descR[b].data_ptr() for b in range(B)])
             self.s_uR = arr([self.d_uR[b].data_ptr() for b in range(B)])
             self.s_dep = arr([self.d_depth[b].data_ptr() for b in range(B)])
-            self.pprobs = (pose_problem * P)(*[
-                pose_problem(0, poses[p].data_ptr(), self.d_has[p].data_ptr(), self.d_Xw[p].data_ptr(),
-                             self.d_pobs[p].data_ptr(), self.d_isig[p].data_ptr(), float(fx), float(fy), float(cx),
-                             float(cy), float(mbf)) for p in range(P)])
+            # UpdateLastFrame: Frame::UnprojectStereo of frame b's stereo keypoints (Twc = I: the last
+            # frame is the reference) -> the map point table of pair b and LastFrame.mvpMapPoints
+            self.unp = (orb_unproject * B)(*[
+                orb_unproject(0, self.d_kps[b].data_ptr(), self.d_depth[b].data_ptr(), eye.data_ptr(), float(fx),
+                              float(fy), float(cx), float(cy), self.d_mp_pos[b].data_ptr(),
+                              self.d_last_mp[b].data_ptr()) for b in range(B)])
+            # PoseOptimization(&mCurrentFrame): the frame's own arrays, map points by index
+            self.pframes = (pose_frame * P)(*[
+                pose_frame(0, poses[p].data_ptr(), self.d_cur_mp[p + 1].data_ptr(), self.d_mp_pos[p].data_ptr(),
+                           self.d_kps[p + 1].data_ptr(), self.d_uR[p + 1].data_ptr(), self.isig_tab.data_ptr(), 8,
+                           float(fx), float(fy), float(cx), float(cy), float(mbf)) for p in range(P)])
             self.a_Tout = arr([self.d_Tout[p].data_ptr() for p in range(P)])
             self.a_poutl = arr([self.d_poutl[p].data_ptr() for p in range(P)])
+            self.n_unp = n_field(self.unp, orb_unproject, B)
+            self.n_cur = n_field(self.curs, orb_frame, P)
+            self.n_last = n_field(self.lasts, orb_frame, P)
+            self.n_mps = n_field(self.mps, orb_mappoints, P)
+            self.n_pose = n_field(self.pframes, pose_frame, P)
             self.ninl = np.zeros(P, np.int32)
             self.nm = np.zeros(P, np.int32)
             self.nst = np.zeros(B, np.int32)
@@ -197,20 +206,16 @@ def main():
                                                           float(mb), self.s_uR, self.s_dep, ptr(self.nst)),
                   "ComputeStereoMatches batch")
             t2 = time.perf_counter()
-            with torch.cuda.stream(track_stream):
-                # UpdateLastFrame-style map points of the last frame from its stereo depth: X = d K^-1 [u v 1]
-                x, y = self.kp_f[..., 0], self.kp_f[..., 1]
-                self.d_mp_pos[..., 0] = (x - float(cx)) / float(fx) * self.d_depth
-                self.d_mp_pos[..., 1] = (y - float(cy)) / float(fy) * self.d_depth
-                self.d_mp_pos[..., 2] = self.d_depth
-                torch.where(self.d_depth > 0, d_arange, torch.full_like(d_arange, -1), out=self.d_last_mp)
+            # UpdateLastFrame (Frame::UnprojectStereo) and the current frames' empty mvpMapPoints, on
+            # the matcher's stream ahead of the search
+            self.n_unp[:] = nL
+            self.n_cur[:] = nL[1:]
+            self.n_last[:] = nL[:-1]
+            self.n_mps[:] = nL[:-1]
+            self.n_pose[:] = nL[1:]
+            check(L.Frame_UnprojectStereo_batch_device(m._h, B, self.unp), "UnprojectStereo batch")
+            with torch.cuda.stream(match_stream):
                 self.d_cur_mp.fill_(-1)
-            for p in range(P):
-                self.curs[p].N = int(nL[p + 1])
-                self.lasts[p].N = int(nL[p])
-                self.mps[p].n = int(nL[p])
-                self.pprobs[p].N = int(nL[p + 1])
-            track_stream.synchronize()
             # TrackWithMotionModel: SearchByProjection(CurrentFrame, LastFrame, th=7, stereo) (Tracking.cc:869-885)
             check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, P, self.curs, self.a_cur_mp, self.lasts,
                                                                   self.a_last_kps, self.a_last_mp, self.a_last_out,
@@ -218,17 +223,8 @@ def main():
                   "SearchByProjection batch")
             t3 = time.perf_counter()
             # Optimizer::PoseOptimization(&mCurrentFrame) (Tracking.cc:887) on the matched map points
-            with torch.cuda.stream(track_stream):
-                cm = self.d_cur_mp[1:]
-                self.d_has.copy_(cm >= 0)
-                torch.gather(self.d_mp_pos[:-1], 1, cm.clamp(min=0).long().unsqueeze(-1).expand(-1, -1, 3),
-                             out=self.d_Xw)
-                self.d_pobs[..., 0:2] = self.kp_f[1:, :, 0:2]
-                self.d_pobs[..., 2] = self.d_uR[1:]
-                torch.index_select(self.isig_tab, 0, self.octv.reshape(-1).clamp(0, 7), out=self.d_isig.view(-1))
-            track_stream.synchronize()
-            check(L.Optimizer_PoseOptimization_batch_device(P, self.pprobs, self.a_Tout, self.a_poutl,
-                                                            ptr(self.ninl)), "PoseOptimization batch")
+            check(L.Optimizer_PoseOptimization_frames_device(P, self.pframes, self.a_Tout, self.a_poutl,
+                                                             ptr(self.ninl)), "PoseOptimization batch")
             t4 = time.perf_counter()
             for k, v in (("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3)):
                 phase_acc[k] = phase_acc.get(k, 0.0) + v * 1e3
@@ -291,6 +287,10 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if os.environ.get("ORBGPU_PROF_DUMP"):   # instrumented build (make prof): k_select section timers
+        buf = (C.c_ulonglong * 32)()
+        L.orbgpu_debug_prof_match(buf)
+        print("k_select sections (cycles, problem 0, summed over the timed steps):", list(buf)[:8], file=sys.stderr)
     drain()   # the batch extracted by the last timed step (outside the timed region)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -519,9 +519,9 @@ def cpu_baseline(lefts, rights, Rs, budget_s):
             pk, pd, pdep = prev
             last = Frame(pk, pd, scale, np.eye(4, dtype=np.float32), fx, fy, cx, cy, mbf, W, H)
             cur = Frame(kL, dL, scale, synthetic.pose_from_rotation(Rs[i - 1]), fx, fy, cx, cy, mbf, W, H, uRight=uR)
-            X = np.stack([(pk["x"] - cx) / fx * pdep, (pk["y"] - cy) / fy * pdep, pdep], 1).astype(np.float32)
+            X, lm = oracle_lib.oracle_unproject_stereo(pk, pdep, np.eye(4, dtype=np.float32), fx, fy, cx, cy)
+            X = np.nan_to_num(X)
             mps = MapPoints(X, pd, np.ones(len(pk), np.int32))
-            lm = np.where(pdep > 0, np.arange(len(pk)), -1).astype(np.int32)
             cm = np.full(cur.N, -1, np.int32)
             td = time.perf_counter()
             oracle_lib.oracle_search_last(cur, cm, last, pk, lm, np.zeros(len(pk), np.uint8), mps, 7.0, False,

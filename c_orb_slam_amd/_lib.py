@@ -143,11 +143,14 @@ def lib():
     L.Optimizer_PoseOptimization.argtypes = [P(pose_problem), vp, vp, P(i32)]
     L.Optimizer_PoseOptimization_batch.argtypes = [i32, vp, vp, vp, vp]
     L.Optimizer_PoseOptimization_batch_device.argtypes = [i32, vp, vp, vp, vp]
+    L.Optimizer_PoseOptimization_frames_device.argtypes = [i32, vp, vp, vp, vp]
+    L.Frame_UnprojectStereo_batch_device.argtypes = [vp, i32, vp]
     L.orbgpu_unit_ldlt_solve.argtypes = [i32, vp, vp, vp, i32, P(i32)]
     L.orbgpu_unit_csum.argtypes = [vp, i32, vp]
     L.orbgpu_unit_ldlt_factor.argtypes = [i32, vp, vp]
     L.orbgpu_unit_wave_tree.argtypes = [vp, vp]
     L.orbgpu_debug_prof.argtypes = [vp]
+    L.orbgpu_debug_prof_match.argtypes = [vp]
     L.Sim3Solver_create.argtypes = [i32, vp, vp, vp, vp, vp, i32, vp, vp, i32, P(vp)]
     L.Sim3Solver_destroy.argtypes = [vp]
     L.Sim3Solver_set_ransac.argtypes = [vp, C.c_double, i32, i32]
@@ -176,6 +179,19 @@ class ba_problem(C.Structure):
                 ("kf_cam", C.c_void_p), ("n_pt", C.c_int), ("pt_id", C.c_void_p), ("pt_pos", C.c_void_p),
                 ("n_edge", C.c_int), ("edge_pt", C.c_void_p), ("edge_kf", C.c_void_p), ("edge_obs", C.c_void_p),
                 ("edge_inv_sigma2", C.c_void_p)]
+
+
+class orb_unproject(C.Structure):
+    _fields_ = [("N", C.c_int), ("keysUn", C.c_void_p), ("depth", C.c_void_p), ("Twc", C.c_void_p),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("x3D", C.c_void_p), ("mp", C.c_void_p)]
+
+
+class pose_frame(C.Structure):
+    _fields_ = [("N", C.c_int), ("Tcw", C.c_void_p), ("mp", C.c_void_p), ("mp_pos", C.c_void_p),
+                ("keysUn", C.c_void_p), ("uRight", C.c_void_p), ("invLevelSigma2", C.c_void_p),
+                ("nlevels", C.c_int), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float),
+                ("cy", C.c_float), ("bf", C.c_float)]
 
 
 class pose_problem(C.Structure):

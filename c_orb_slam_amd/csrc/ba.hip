@@ -17,6 +17,8 @@
 // so results are bit-identical to the CPU restatement.
 #include "ba.hpp"
 
+#include <functional>
+
 #include <algorithm>
 #include <cfloat>
 #include <chrono>
@@ -1217,6 +1219,13 @@ struct PoseProbDev {
     const float* inv_sigma2;
     float* Tcw_out;
     uint8_t* outlier;
+    // frame mode (pose_frame): gathered by k_pose_pack instead of the packed arrays above
+    const int* mpidx;          // mvpMapPoints as indices (-1 NULL)
+    const float* mp_pos;       // map point rows (GetWorldPos)
+    const float* keys;         // mvKeysUn, 7 words per cv::KeyPoint (x y size angle response octave class_id)
+    const float* uR;           // mvuRight
+    const float* isig_tab;     // mvInvLevelSigma2
+    int nlev;
 };
 
 // one edge in double (the g2o edge's _measurement / information / Huber delta)
@@ -1694,7 +1703,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_pack(PoseProbDev* probs, 
     __syncthreads();
     for (int c0 = 0; c0 < N; c0 += kPoseThreads) {
         const int i = c0 + tid;
-        const int f = (i < N && P.has_mp[i]) ? 1 : 0;
+        const int f = i < N ? (P.mpidx ? (P.mpidx[i] >= 0 ? 1 : 0) : (P.has_mp[i] ? 1 : 0)) : 0;
         int incl = f;
         for (int o = 1; o < 64; o <<= 1) {
             const int t = __shfl_up(incl, o, 64);
@@ -1708,12 +1717,23 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_pack(PoseProbDev* probs, 
             const int k = off + incl - 1;
             if (k < kPoseMaxEdges) {
                 PoseEdgeDev e;
-                for (int j = 0; j < 3; j++) {
-                    e.Xw[j] = P.Xw[3 * i + j];
-                    e.obs[j] = P.obs[3 * i + j];
+                if (P.mpidx) {
+                    // Optimizer.cc:268-347: pMP->GetWorldPos(), kpUn.pt, mvuRight, mvInvLevelSigma2[kpUn.octave]
+                    const size_t m = (size_t)P.mpidx[i];
+                    for (int j = 0; j < 3; j++) e.Xw[j] = P.mp_pos[3 * m + j];
+                    e.obs[0] = P.keys[7 * (size_t)i];
+                    e.obs[1] = P.keys[7 * (size_t)i + 1];
+                    e.obs[2] = P.uR[i];
+                    const int oct = min(max(__float_as_int(P.keys[7 * (size_t)i + 5]), 0), P.nlev - 1);
+                    e.info = P.isig_tab[oct];
+                } else {
+                    for (int j = 0; j < 3; j++) {
+                        e.Xw[j] = P.Xw[3 * i + j];
+                        e.obs[j] = P.obs[3 * i + j];
+                    }
+                    e.info = P.inv_sigma2[i];
                 }
-                e.info = P.inv_sigma2[i];
-                e.meta = i | (!(P.obs[3 * i + 2] < 0) ? (int)0x80000000u : 0);
+                e.meta = i | (!(e.obs[2] < 0) ? (int)0x80000000u : 0);
                 E[k] = e;
             }
         }
@@ -1749,8 +1769,32 @@ static void host_se3_to_Tcw(const Se3& s, float* T) {
 // ---------------------------------------------------------------- PoseEngine
 int PoseEngine::run_device(int count, const pose_problem* P, float* const* Tcw_out, uint8_t* const* outlier,
                            int* ninliers) {
+    std::vector<int> Ns(count);
+    for (int f = 0; f < count; f++) Ns[f] = P[f].N;
+    return launch_device(count, Ns.data(), [&](int f, PoseProbDev& pp) {
+        const pose_problem& Q = P[f];
+        pp.fx = Q.fx; pp.fy = Q.fy; pp.cx = Q.cx; pp.cy = Q.cy; pp.bf = Q.bf;
+        pp.Tcw = Q.Tcw; pp.has_mp = Q.has_mp; pp.Xw = Q.Xw; pp.obs = Q.obs; pp.inv_sigma2 = Q.inv_sigma2;
+    }, Tcw_out, outlier, ninliers);
+}
+
+int PoseEngine::run_frames_device(int count, const pose_frame* F, float* const* Tcw_out, uint8_t* const* outlier,
+                                  int* ninliers) {
+    std::vector<int> Ns(count);
+    for (int f = 0; f < count; f++) Ns[f] = F[f].N;
+    return launch_device(count, Ns.data(), [&](int f, PoseProbDev& pp) {
+        const pose_frame& Q = F[f];
+        pp.fx = Q.fx; pp.fy = Q.fy; pp.cx = Q.cx; pp.cy = Q.cy; pp.bf = Q.bf;
+        pp.Tcw = Q.Tcw;
+        pp.mpidx = Q.mp; pp.mp_pos = Q.mp_pos; pp.keys = (const float*)Q.keysUn; pp.uR = Q.uRight;
+        pp.isig_tab = Q.invLevelSigma2; pp.nlev = Q.nlevels;
+    }, Tcw_out, outlier, ninliers);
+}
+
+int PoseEngine::launch_device(int count, const int* Ns, const std::function<void(int, PoseProbDev&)>& fill,
+                              float* const* Tcw_out, uint8_t* const* outlier, int* ninliers) {
     size_t nmax = 0;
-    for (int f = 0; f < count; f++) nmax += (size_t)std::min(P[f].N, kPoseMaxEdges + 1);
+    for (int f = 0; f < count; f++) nmax += (size_t)std::min(Ns[f], kPoseMaxEdges + 1);
     const auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t bProb = al(sizeof(PoseProbDev) * count), bEdge = al(sizeof(PoseEdgeDev) * std::max<size_t>(nmax, 1));
     const size_t bErr = al(sizeof(double) * 3 * std::max<size_t>(nmax, 1)), bOut = al(std::max<size_t>(nmax, 1));
@@ -1769,14 +1813,12 @@ int PoseEngine::run_device(int count, const pose_problem* P, float* const* Tcw_o
     PoseProbDev* hp = (PoseProbDev*)h;
     size_t e0 = 0;
     for (int f = 0; f < count; f++) {
-        const pose_problem& Q = P[f];
         PoseProbDev& pp = hp[f];
         memset(&pp, 0, sizeof(pp));
-        pp.N = Q.N;
+        pp.N = Ns[f];
         pp.e0 = (int)e0;
-        e0 += (size_t)std::min(Q.N, kPoseMaxEdges + 1);
-        pp.fx = Q.fx; pp.fy = Q.fy; pp.cx = Q.cx; pp.cy = Q.cy; pp.bf = Q.bf;
-        pp.Tcw = Q.Tcw; pp.has_mp = Q.has_mp; pp.Xw = Q.Xw; pp.obs = Q.obs; pp.inv_sigma2 = Q.inv_sigma2;
+        e0 += (size_t)std::min(Ns[f], kPoseMaxEdges + 1);
+        fill(f, pp);
         pp.Tcw_out = Tcw_out[f];
         pp.outlier = outlier[f];
     }

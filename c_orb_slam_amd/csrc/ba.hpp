@@ -1,6 +1,7 @@
 // ba.hpp -- gfx950 local bundle adjustment (Optimizer::LocalBundleAdjustment,
 // reference src/Optimizer.cc:453-778, g2o BlockSolver<6,3> + Levenberg).
 #pragma once
+#include <functional>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -130,6 +131,7 @@ struct PoseEdgeDev;
 struct PoseProbDev;
 
 // Optimizer::PoseOptimization for a batch of frames: one persistent workgroup per frame.
+struct PoseProbDev;
 class PoseEngine {
 public:
     ~PoseEngine();
@@ -137,9 +139,14 @@ public:
     int run(int count, const pose_problem* P, float* Tcw_out, uint8_t* const* outlier, int* ninliers);
     // P's arrays, Tcw_out[f] (16 floats) and outlier[f] are device pointers
     int run_device(int count, const pose_problem* P, float* const* Tcw_out, uint8_t* const* outlier, int* ninliers);
+    // pose_frame form: the edges are gathered from the frame's own arrays on the device
+    int run_frames_device(int count, const pose_frame* F, float* const* Tcw_out, uint8_t* const* outlier,
+                          int* ninliers);
     hipStream_t stream() const { return stream_; }
 
 private:
+    int launch_device(int count, const int* Ns, const std::function<void(int, PoseProbDev&)>& fill,
+                      float* const* Tcw_out, uint8_t* const* outlier, int* ninliers);
     hipStream_t stream_ = nullptr;
     void* dArena_ = nullptr;
     void* hArena_ = nullptr;   // pinned staging: problems + edges in, outliers back

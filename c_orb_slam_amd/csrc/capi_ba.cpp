@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "ba.hpp"
+#include "orb_match.hpp"
 
 namespace {
 orbgpu::BaEngine* engine(int* rc) {
@@ -138,6 +139,25 @@ int Optimizer_PoseOptimization_batch_device(int count, const pose_problem* P, fl
     return r ? ORB_E_HIP : ORB_OK;
 }
 
+int Optimizer_PoseOptimization_frames_device(int count, const pose_frame* F, float* const* Tcw_out,
+                                             uint8_t* const* outlier, int* ninliers) {
+    if (count < 0 || (count > 0 && (!F || !Tcw_out || !outlier || !ninliers))) return ORB_E_INVALID;
+    for (int f = 0; f < count; f++) {
+        const pose_frame& Q = F[f];
+        if (Q.N < 0 || !Q.Tcw || !Tcw_out[f]) return ORB_E_INVALID;
+        if (Q.N > 0 && (!outlier[f] || !Q.mp || !Q.mp_pos || !Q.keysUn || !Q.uRight || !Q.invLevelSigma2 ||
+                        Q.nlevels <= 0))
+            return ORB_E_INVALID;
+    }
+    if (count == 0) return ORB_OK;
+    int rc = 0;
+    orbgpu::PoseEngine* e = pose_engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    const int r = e->run_frames_device(count, F, Tcw_out, outlier, ninliers);
+    if (r == -3) return ORB_E_CAPACITY;
+    return r ? ORB_E_HIP : ORB_OK;
+}
+
 int Optimizer_PoseOptimization(const pose_problem* P, float* Tcw_out, uint8_t* outlier, int* ninliers) {
     if (!P || !Tcw_out || !ninliers) return ORB_E_INVALID;
     uint8_t* const o[1] = {outlier};
@@ -264,6 +284,9 @@ int orbgpu_unit_ldlt_factor(int n, const double* S, double* out) {
 }
 
 int orbgpu_debug_prof(unsigned long long* out32) { return out32 ? orbgpu::debug_prof(out32) : ORB_E_INVALID; }
+int orbgpu_debug_prof_match(unsigned long long* out32) {
+    return out32 ? orbgpu::debug_prof_match(out32) : ORB_E_INVALID;
+}
 
 int orbgpu_unit_wave_tree(const double* v64, double* out) {
     if (!v64 || !out) return ORB_E_INVALID;

@@ -133,4 +133,27 @@ int ORBmatcher_ComputeStereoMatches(ORBmatcher_h h, ORBextractor_h left, ORBextr
                                                  mb, &uRight, &depth, nmatches);
 }
 
+int Frame_UnprojectStereo_batch_device(ORBmatcher_h h, int count, const orb_unproject* U) {
+    if (!h || count < 0 || (count > 0 && !U)) return ORB_E_INVALID;
+    if (count == 0) return ORB_OK;
+    std::vector<orbgpu::UnprojDev> P((size_t)count);
+    int maxN = 0;
+    for (int f = 0; f < count; f++) {
+        const orb_unproject& Q = U[f];
+        if (Q.N < 0 || (Q.N > 0 && (!Q.keysUn || !Q.depth || !Q.Twc || !Q.x3D))) return ORB_E_INVALID;
+        orbgpu::UnprojDev& d = P[f];
+        d.N = Q.N;
+        d.keys = (const orbgpu::orb_kp_dev*)Q.keysUn;
+        d.depth = Q.depth;
+        d.Twc = Q.Twc;
+        d.fx = Q.fx; d.fy = Q.fy; d.cx = Q.cx; d.cy = Q.cy;
+        d.invfx = 1.0f / Q.fx;   // Frame.cc:108-109
+        d.invfy = 1.0f / Q.fy;
+        d.x3D = Q.x3D;
+        d.mp = Q.mp;
+        maxN = std::max(maxN, Q.N);
+    }
+    return orbgpu::unproject_batch(P.data(), count, maxN, h->m->stream()) ? ORB_E_HIP : ORB_OK;
+}
+
 }  // extern "C"

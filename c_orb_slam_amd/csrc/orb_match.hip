@@ -7,10 +7,11 @@
 //                 parallel): projection, Frame::GetFeaturesInArea window over
 //                 the device grid, static filters, popcount distances, and the
 //                 kTopK smallest (dist, enumeration order) candidates;
-//   k_select      (one wave per problem): the sequential greedy replay over the
-//                 queries against the occupancy array held in LDS, with a full
-//                 rescan only when every kept candidate is already taken, then
-//                 the rotation-consistency histogram (ORBmatcher.cc:1447-1467).
+//   k_select      (one workgroup per problem): the sequential greedy replay,
+//                 solved as a parallel fixed-point iteration over the queries
+//                 (occupancy owners in LDS), with a full rescan only when every
+//                 kept candidate is already taken, then the rotation-consistency
+//                 histogram (ORBmatcher.cc:1447-1467).
 // k_build_grid rebuilds Frame::mGrid (AssignFeaturesToGrid, Frame.cc:230-245)
 // as a CSR in cell order (ix-major) with keypoint order kept inside a cell.
 #include "orb_match.hpp"
@@ -269,147 +270,133 @@ __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict_
     for (int k = 0; k < kk; k++) P.topk[(size_t)q * kTopK + k] = top[k];
 }
 
-// Sequential greedy replay: one wave per problem.  Per-query inputs are
-// staged into LDS in chunks (coalesced), occupancy is an LDS flag array
-// (occ[i] = mvpMapPoints[i] && Observations()>0), so the per-query critical
-// path is a handful of LDS ops + one ballot.
-constexpr int SEL_CHUNK = 256;
+// Greedy replay as a fixed-point iteration (one 256-thread workgroup per problem).
+// The reference loop is sequential: query q may not take a keypoint that an earlier
+// query q' < q already took with Observations() > 0 (ORBmatcher.cc:87-89, 1403-1405).
+// Its outcome is the unique solution of
+//     choice(q) = decide(q, occupied = occ0 U { choice(q') : q' < q, take(q'), obs(q') })
+// and since choice(q) depends only on earlier queries, Jacobi iteration over all queries
+// in parallel reaches it: after round r every query whose dependency chain is shorter
+// than r is final, and a round that changes nothing is the fixed point.  Conflicts are
+// rare (a few per frame), so it converges in 2-4 rounds; each round is one owner[]
+// rebuild (atomicMin of the claiming query per keypoint, in LDS) plus one decide() per
+// query against the kTopK list, with a full rescan only when every kept candidate is
+// taken.  Overwrites (a later query re-taking a keypoint whose earlier taker has no
+// observations) keep the latest taker, as the reference's sequential assignment does.
 template <bool LAST>
-__global__ void __launch_bounds__(64) k_select(const SearchDev* __restrict__ probs, float th, int bMono,
-                                               float nnratio, int checkOri) {
-    __shared__ int s_cur[kMaxFrameKeys];
-    __shared__ uint8_t s_occ[kMaxFrameKeys];
-    __shared__ int2 s_top[SEL_CHUNK * kTopK];
-    __shared__ int s_cnt[SEL_CHUNK];
-    __shared__ int s_qmp[SEL_CHUNK];     // map point written by the query
-    __shared__ uint8_t s_qobs[SEL_CHUNK];
-    __shared__ int16_t s_mbest[kMaxFrameKeys];   // query -> keypoint taken (rotation check deferred)
+__global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ probs, float th, int bMono,
+                                                float nnratio, int checkOri) {
+    __shared__ int s_owner[kMaxFrameKeys];    // earliest claiming query with Observations() > 0
+    __shared__ int s_lastq[kMaxFrameKeys];    // latest claiming query (any)
+    __shared__ uint8_t s_occ0[kMaxFrameKeys]; // occupancy before this call
+    __shared__ uint8_t s_rm[kMaxFrameKeys];   // slot cleared by the rotation check
     __shared__ int s_hsz[HISTO_LENGTH];
     __shared__ int s_ind[3];
+    __shared__ int s_changed, s_nm, s_rmcnt;
+    ORBGPU_PROF_START;
     const SearchDev P = probs[blockIdx.x];
-    const int lane = threadIdx.x;
-    const int N = P.cur.N;
-    for (int i = lane; i < N; i += 64) {
+    const int tid = threadIdx.x;
+    const int N = P.cur.N, nq = P.nq;
+    for (int i = tid; i < N; i += 256) {
         const int m = P.curMP[i];
-        s_cur[i] = m;
-        s_occ[i] = (m >= 0 && P.mpObs[m] > 0) ? 1 : 0;
+        s_occ0[i] = (m >= 0 && P.mpObs[m] > 0) ? 1 : 0;
+        s_owner[i] = INT_MAX;
+        s_lastq[i] = -1;
+        s_rm[i] = 0;
     }
-    for (int i = lane; i < P.nq; i += 64) s_mbest[i] = -1;
-    if (lane < HISTO_LENGTH) s_hsz[lane] = 0;
+    if (tid < HISTO_LENGTH) s_hsz[tid] = 0;
+    if (tid == 0) { s_nm = 0; s_rmcnt = 0; }
     bool bF = false, bB = false;
     if (LAST) fwd_bwd(P, bMono != 0, bF, bB);
-    int nmatches = 0;
-    auto occupied = [&](int idx) { return s_occ[idx] != 0; };
-    for (int q0 = 0; q0 < P.nq; q0 += SEL_CHUNK) {
-        const int nc = min(SEL_CHUNK, P.nq - q0);
-        __syncthreads();
-        for (int i = lane; i < nc; i += 64) {
-            const int c = P.qinfo[q0 + i].x;
-            s_cnt[i] = c;
-            const int mp = LAST ? P.lastMP[q0 + i] : P.mpIndex[q0 + i];
-            s_qmp[i] = mp;
-            s_qobs[i] = (c > 0 && mp >= 0 && P.mpObs[mp] > 0) ? 1 : 0;
-        }
-        for (int i = lane; i < nc * kTopK; i += 64) {
-            const int qq = i / kTopK, k = i - qq * kTopK;
-            const int c = P.qinfo[q0 + qq].x;
-            if (k < c) s_top[i] = P.topk[(size_t)q0 * kTopK + i];
-        }
-        __syncthreads();
-        for (int qi = 0; qi < nc; qi++) {
-            const int q = q0 + qi;
-            const int cnt = s_cnt[qi];
-            if (cnt <= 0) continue;
-            const int kk = cnt < kTopK ? cnt : kTopK;
-            int2 e = make_int2(256, -1);
-            bool free_ = false;
-            if (lane < kk) {
-                e = s_top[qi * kTopK + lane];
-                free_ = !occupied(e.y);
-            }
-            uint64_t m = __ballot(free_);
-            int bestDist = 256, bestIdx = -1, bestDist2 = 256, bestLevel = -1, bestLevel2 = -1;
-            bool resolved = true;
-            if (LAST) {
-                if (m) {
-                    const int f = __ffsll((long long)m) - 1;
-                    bestDist = __shfl(e.x, f, 64);
-                    bestIdx = __shfl(e.y, f, 64);
-                } else if (cnt > kTopK) {
-                    resolved = false;
-                }
-            } else {
-                const int nfree = __popcll(m);
-                if (nfree >= 2 || cnt <= kTopK) {
-                    if (nfree >= 1) {
-                        const int f = __ffsll((long long)m) - 1;
-                        bestDist = __shfl(e.x, f, 64);
-                        bestIdx = __shfl(e.y, f, 64);
-                        const uint64_t m2 = m & (m - 1);
-                        if (m2) {
-                            const int f2 = __ffsll((long long)m2) - 1;
-                            bestDist2 = __shfl(e.x, f2, 64);
-                            const int i2 = __shfl(e.y, f2, 64);
-                            bestLevel2 = P.cur.keysUn[i2].octave;
-                        }
-                        bestLevel = P.cur.keysUn[bestIdx].octave;
-                    }
-                } else {
-                    resolved = false;
-                }
-            }
-            if (!resolved) {
-                // every kept candidate is taken: rescan this query with occupancy (rare)
-                if (lane == 0) {
-                    int2 top2[2];
-                    int c2;
-                    if (LAST) {
-                        const LastQuery lq = last_query(P, q, th, bF, bB);
-                        c2 = scan_last(P, lq, occupied, top2, 1);
-                        if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
-                    } else {
-                        const LocalQuery lq = local_query(P, q, th);
-                        c2 = scan_local(P, lq, occupied, top2, 2);
-                        if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; bestLevel = P.cur.keysUn[bestIdx].octave; }
-                        if (c2 > 1) { bestDist2 = top2[1].x; bestLevel2 = P.cur.keysUn[top2[1].y].octave; }
-                    }
-                }
-                bestDist = __shfl(bestDist, 0, 64);
-                bestIdx = __shfl(bestIdx, 0, 64);
-                bestDist2 = __shfl(bestDist2, 0, 64);
-                bestLevel = __shfl(bestLevel, 0, 64);
-                bestLevel2 = __shfl(bestLevel2, 0, 64);
-            }
-            if (bestDist <= TH_HIGH) {
-                bool take = true;
-                if (!LAST) take = !(bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2);
-                if (take) {
-                    if (lane == 0) {
-                        s_cur[bestIdx] = s_qmp[qi];
-                        s_occ[bestIdx] = s_qobs[qi];
-                        s_mbest[q] = (int16_t)bestIdx;
-                    }
-                    nmatches++;
-                }
-            }
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): lane 0's LDS writes land before the next query
-            __builtin_amdgcn_wave_barrier();
-        }
+    // per query: qinfo.x = candidate count (k_candidates), .y = current choice (-1 none), .z = obs flag
+    for (int q = tid; q < nq; q += 256) {
+        const int c = P.qinfo[q].x;
+        const int mp = LAST ? P.lastMP[q] : P.mpIndex[q];
+        P.qinfo[q].z = (c > 0 && mp >= 0 && P.mpObs[mp] > 0) ? 1 : 0;
     }
     __syncthreads();
+    ORBGPU_PROF_MARK(0);
+    // decide(q): the reference's choice for query q given the occupancy by earlier queries
+    auto decide = [&](int q) -> int {
+        const int cnt = P.qinfo[q].x;
+        if (cnt <= 0) return -1;
+        auto occupied = [&](int idx) { return s_occ0[idx] != 0 || s_owner[idx] < q; };
+        const int kk = cnt < kTopK ? cnt : kTopK;
+        const int2* top = P.topk + (size_t)q * kTopK;
+        int bestDist = 256, bestIdx = -1, bestDist2 = 256, idx2 = -1, nfree = 0;
+        for (int k = 0; k < kk && nfree < (LAST ? 1 : 2); k++) {
+            const int2 e = top[k];
+            if (occupied(e.y)) continue;
+            if (nfree == 0) { bestDist = e.x; bestIdx = e.y; }
+            else { bestDist2 = e.x; idx2 = e.y; }
+            nfree++;
+        }
+        if (nfree < (LAST ? 1 : 2) && cnt > kTopK) {
+            // every kept candidate that could decide is taken: rescan with occupancy (rare)
+            int2 top2[2];
+            bestDist = bestDist2 = 256;
+            bestIdx = idx2 = -1;
+            if (LAST) {
+                const LastQuery lq = last_query(P, q, th, bF, bB);
+                if (scan_last(P, lq, occupied, top2, 1) > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
+            } else {
+                const LocalQuery lq = local_query(P, q, th);
+                const int c2 = scan_local(P, lq, occupied, top2, 2);
+                if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
+                if (c2 > 1) { bestDist2 = top2[1].x; idx2 = top2[1].y; }
+            }
+        }
+        if (bestDist > TH_HIGH) return -1;
+        if (!LAST) {
+            const int bestLevel = P.cur.keysUn[bestIdx].octave;
+            const int bestLevel2 = idx2 >= 0 ? P.cur.keysUn[idx2].octave : -1;
+            if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) return -1;
+        }
+        return bestIdx;
+    };
+    for (int q = tid; q < nq; q += 256) P.qinfo[q].y = decide(q);   // round 0: nothing claimed yet
+    for (int round = 0; round <= nq; round++) {
+        __syncthreads();
+        for (int i = tid; i < N; i += 256) s_owner[i] = INT_MAX;
+        if (tid == 0) s_changed = 0;
+        __syncthreads();
+        for (int q = tid; q < nq; q += 256) {
+            const int4 qi = P.qinfo[q];
+            if (qi.y >= 0 && qi.z) atomicMin(&s_owner[qi.y], q);
+        }
+        __syncthreads();
+        bool ch = false;
+        for (int q = tid; q < nq; q += 256) {
+            const int c = decide(q);
+            if (c != P.qinfo[q].y) { P.qinfo[q].y = c; ch = true; }
+        }
+        if (ch) s_changed = 1;
+        __syncthreads();
+        if (!s_changed) break;
+    }
+    ORBGPU_PROF_MARK(1);
+    // the fixed point: takes, latest taker per keypoint, match count
+    int nm = 0;
+    for (int q = tid; q < nq; q += 256) {
+        const int c = P.qinfo[q].y;
+        if (c >= 0) { atomicMax(&s_lastq[c], q); nm++; }
+    }
+    atomicAdd(&s_nm, nm);
+    __syncthreads();
     if (LAST && checkOri) {
-        // rotation-consistency histogram over the matches, bins in parallel (ORBmatcher.cc:1422-1467)
-        for (int q = lane; q < P.nq; q += 64) {
-            const int bi = s_mbest[q];
+        // rotation-consistency histogram over the matches (ORBmatcher.cc:1422-1467)
+        for (int q = tid; q < nq; q += 256) {
+            const int bi = P.qinfo[q].y;
             if (bi < 0) continue;
             float rot = P.last.keysUn[q].angle - P.cur.keysUn[bi].angle;
             if (rot < 0.0f) rot += 360.0f;
             int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
             if (bin == HISTO_LENGTH) bin = 0;
             atomicAdd(&s_hsz[bin], 1);
+            P.hist[q] = make_int2(bin, bi);
         }
         __syncthreads();
-        if (lane == 0) {
+        if (tid == 0) {
             // ComputeThreeMaxima, ORBmatcher.cc:1601-1642
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < HISTO_LENGTH; i++) {
@@ -427,24 +414,25 @@ __global__ void __launch_bounds__(64) k_select(const SearchDev* __restrict__ pro
         __syncthreads();
         const int ind1 = s_ind[0], ind2 = s_ind[1], ind3 = s_ind[2];
         int removed = 0;
-        for (int q = lane; q < P.nq; q += 64) {
-            const int bi = s_mbest[q];
-            if (bi < 0) continue;
-            float rot = P.last.keysUn[q].angle - P.cur.keysUn[bi].angle;
-            if (rot < 0.0f) rot += 360.0f;
-            int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
-            if (bin == HISTO_LENGTH) bin = 0;
-            if (bin != ind1 && bin != ind2 && bin != ind3) {
-                s_cur[bi] = -1;
+        for (int q = tid; q < nq; q += 256) {
+            if (P.qinfo[q].y < 0) continue;
+            const int2 h = P.hist[q];
+            if (h.x != ind1 && h.x != ind2 && h.x != ind3) {
+                s_rm[h.y] = 1;
                 removed++;
             }
         }
-        for (int o = 32; o >= 1; o >>= 1) removed += __shfl_xor(removed, o, 64);
-        nmatches -= removed;
+        atomicAdd(&s_rmcnt, removed);
     }
     __syncthreads();
-    for (int i = lane; i < N; i += 64) P.curMP[i] = s_cur[i];
-    if (lane == 0) *P.nmatches = nmatches;
+    ORBGPU_PROF_MARK(2);
+    for (int i = tid; i < N; i += 256) {
+        const int lq = s_lastq[i];
+        if (s_rm[i]) P.curMP[i] = -1;
+        else if (lq >= 0) P.curMP[i] = LAST ? P.lastMP[lq] : P.mpIndex[lq];
+    }
+    if (tid == 0) *P.nmatches = s_nm - s_rmcnt;
+    ORBGPU_PROF_MARK(3);
 }
 
 // CSR candidate mode: one wave per query, lanes over candidates; (dist<<20 | k)
@@ -633,10 +621,10 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     if (maxq > 0) {
         if (lastMode) {
             hipLaunchKernelGGL(k_candidates<true>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, (int)bMono);
-            hipLaunchKernelGGL(k_select<true>, dim3(np), dim3(64), 0, stream_, dp, th, (int)bMono, nnratio_, (int)checkOri_);
+            hipLaunchKernelGGL(k_select<true>, dim3(np), dim3(256), 0, stream_, dp, th, (int)bMono, nnratio_, (int)checkOri_);
         } else {
             hipLaunchKernelGGL(k_candidates<false>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0);
-            hipLaunchKernelGGL(k_select<false>, dim3(np), dim3(64), 0, stream_, dp, th, 0, nnratio_, 0);
+            hipLaunchKernelGGL(k_select<false>, dim3(np), dim3(256), 0, stream_, dp, th, 0, nnratio_, 0);
         }
     }
     ORB_HIP_CHECK(hipGetLastError());
@@ -654,6 +642,18 @@ int Matcher::candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, cons
                        best_dist, second_dist);
     ORB_HIP_CHECK(hipGetLastError());
     return 0;
+}
+
+int debug_prof_match(unsigned long long* out32) {
+#ifdef ORBGPU_PROF
+    ORB_HIP_CHECK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_orbgpu_prof), sizeof(unsigned long long) * 32));
+    unsigned long long z[32] = {};
+    ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_orbgpu_prof), z, sizeof(z)));
+    return 0;
+#else
+    (void)out32;
+    return -1;
+#endif
 }
 
 }  // namespace orbgpu

@@ -105,4 +105,6 @@ private:
     size_t cand_cap_ = 0;
 };
 
+int debug_prof_match(unsigned long long* out32);   // section timers of k_select (prof builds)
+
 }  // namespace orbgpu

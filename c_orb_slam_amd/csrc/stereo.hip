@@ -205,4 +205,41 @@ int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoPa
     return 0;
 }
 
+// ------------------------------------------------------------ UnprojectStereo
+// x3Dc = ((u-cx)*z*invfx, (v-cy)*z*invfy, z) in float, then mRwc*x3Dc + mOw as one cv::gemm
+// (the matcher's convention: f64 accumulation, one rounding to float).  One thread per keypoint.
+__global__ void __launch_bounds__(256) k_unproject(const UnprojDev* __restrict__ probs) {
+    const UnprojDev P = probs[blockIdx.y];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.N) return;
+    const float z = P.depth[i];
+    if (P.mp) P.mp[i] = z > 0 ? i : -1;
+    if (!(z > 0)) return;
+    const orb_kp_dev kp = P.keys[i];
+    const float x = (kp.x - P.cx) * z * P.invfx;
+    const float y = (kp.y - P.cy) * z * P.invfy;
+    const float* T = P.Twc;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const double acc = (double)T[r * 4 + 0] * x + (double)T[r * 4 + 1] * y + (double)T[r * 4 + 2] * z;
+        P.x3D[3 * i + r] = (float)(acc + (double)T[r * 4 + 3]);
+    }
+}
+
+int unproject_batch(const UnprojDev* probs, int count, int maxN, hipStream_t s) {
+    thread_local void* d_buf = nullptr;   // grow-only, one per calling thread
+    thread_local size_t cap = 0;
+    const size_t need = sizeof(UnprojDev) * (size_t)count;
+    if (need > cap) {
+        if (d_buf) (void)hipFree(d_buf);
+        cap = need * 2;
+        ORB_HIP_CHECK(hipMalloc(&d_buf, cap));
+    }
+    ORB_HIP_CHECK(hipMemcpyAsync(d_buf, probs, need, hipMemcpyHostToDevice, s));
+    if (maxN > 0)
+        hipLaunchKernelGGL(k_unproject, dim3((maxN + 255) / 256, count), dim3(256), 0, s, (const UnprojDev*)d_buf);
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 }  // namespace orbgpu

@@ -41,4 +41,17 @@ struct StereoDev {
 
 int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoParams& P, hipStream_t s);
 
+// Frame::UnprojectStereo over a batch of frames (Frame.cc:666-680)
+struct UnprojDev {
+    int N;
+    const orb_kp_dev* keys;
+    const float* depth;
+    const float* Twc;
+    float fx, fy, cx, cy, invfx, invfy;
+    float* x3D;
+    int* mp;
+};
+// enqueue on `s`; the problem array is copied from host through a per-thread grow-only buffer
+int unproject_batch(const UnprojDev* probs, int count, int maxN, hipStream_t s);
+
 }  // namespace orbgpu

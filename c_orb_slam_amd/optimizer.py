@@ -160,6 +160,31 @@ def PoseOptimizationBatchDevice(frames, Tcw_out, outliers):
     return n[:F]
 
 
+def PoseOptimizationFramesDevice(frames, Tcw_out, outliers):
+    """Optimizer::PoseOptimization(Frame*) on device-resident frames as the reference reads them
+    (Optimizer.cc:255-347): frames[f] holds torch device tensors Tcw (16 f32), mp (N i32 indices
+    into mp_pos, -1 = NULL), mp_pos (M x 3 f32), keysUn (N x 7 words, cv::KeyPoint layout),
+    uRight (N f32), invLevelSigma2 (nlevels f32) and cam (5 floats, host).  -> nInliers[F]."""
+    from ._lib import pose_frame
+    F = len(frames)
+    ps = []
+    for f in frames:
+        for k in ("Tcw", "mp", "mp_pos", "keysUn", "uRight", "invLevelSigma2"):
+            if not f[k].is_contiguous() or f[k].element_size() != 4:
+                raise ValueError(f"PoseOptimizationFramesDevice: {k} must be contiguous 4-byte elements")
+        fx, fy, cx, cy, bf = (float(v) for v in f["cam"])
+        ps.append(pose_frame(int(f["mp"].numel()), f["Tcw"].data_ptr(), f["mp"].data_ptr(), f["mp_pos"].data_ptr(),
+                             f["keysUn"].data_ptr(), f["uRight"].data_ptr(), f["invLevelSigma2"].data_ptr(),
+                             int(f["invLevelSigma2"].numel()), fx, fy, cx, cy, bf))
+    probs = (pose_frame * max(F, 1))(*ps)
+    tptr = (C.c_void_p * max(F, 1))(*[t.data_ptr() for t in Tcw_out])
+    optr = (C.c_void_p * max(F, 1))(*[o.data_ptr() for o in outliers])
+    n = np.zeros(max(F, 1), np.int32)
+    check(lib().Optimizer_PoseOptimization_frames_device(F, probs, tptr, optr, ptr(n)),
+          "Optimizer_PoseOptimization_frames_device")
+    return n[:F]
+
+
 # ------------------------------------------------------------------ sharding
 def partition_points(problem, nranks):
     """pt_rank[p]: keyframe-block owner of every map point (Optimizer_partition_points, host only)."""

@@ -313,6 +313,22 @@ class ORBmatcher:
               "ORBmatcher_ComputeStereoMatches_batch")
         return [u[:len(k)] for u, k in zip(uR, kL)], [d[:len(k)] for d, k in zip(dep, kL)], n
 
+    def UnprojectStereo_device(self, frames):
+        """Frame::UnprojectStereo (Frame.cc:666-680) for every keypoint of device-resident frames,
+        enqueued on this matcher's stream (ORBmatcher_stream): frames[f] is a dict of torch device
+        tensors keysUn (N x 7 words), depth (N f32), Twc (16 f32, [Rwc | Ow]), x3D (N x 3 f32, out),
+        optional mp (N i32, out), and cam = (fx, fy, cx, cy)."""
+        from ._lib import orb_unproject
+        us = []
+        for f in frames:
+            fx, fy, cx, cy = (float(v) for v in f["cam"])
+            mp = f.get("mp")
+            us.append(orb_unproject(int(f["depth"].numel()), f["keysUn"].data_ptr(), f["depth"].data_ptr(),
+                                    f["Twc"].data_ptr(), fx, fy, cx, cy, f["x3D"].data_ptr(),
+                                    mp.data_ptr() if mp is not None else None))
+        arr = (orb_unproject * max(len(us), 1))(*us)
+        check(self._L.Frame_UnprojectStereo_batch_device(self._h, len(us), arr), "Frame_UnprojectStereo_batch_device")
+
     def SearchByProjection_KeyFrame(self, F: Frame, cur_mp, kf_mp, skip, kf_angle, mps: MapPoints, max_dist,
                                     min_dist, logScaleFactor, th, ORBdist):
         """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (ORBmatcher.cc:1472).

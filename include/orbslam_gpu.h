@@ -188,6 +188,25 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
                                           float mbf, float mb, float* const* uRight,
                                           float* const* depth, int* nmatches);
 
+/* cv::Mat Frame::UnprojectStereo(const int& i)                   Frame.cc:666-680
+ * x3D = mRwc * ((u-cx)*z*invfx, (v-cy)*z*invfy, z) + mOw for every keypoint with
+ * mvDepth[i] = z > 0 (invfx = 1.0f/fx, Frame.cc:108); the callers are Tracking's
+ * UpdateLastFrame / CreateNewKeyFrame / StereoInitialization (Tracking.cc:520-840).
+ * Twc: 16 floats row-major, [mRwc | mOw] (the inverse pose).  Rows with z <= 0 are not
+ * written; mp (optional) gets i for z > 0 and -1 otherwise (the frame's new map-point
+ * slots).  Every pointer is device memory; runs asynchronously on the matcher's stream
+ * (ORBmatcher_stream), so a following search on `h` sees the points. */
+typedef struct orb_unproject {
+    int N;
+    const orb_kp* keysUn;        /* mvKeysUn (N) */
+    const float* depth;          /* mvDepth (N) */
+    const float* Twc;            /* 16 floats: [mRwc | mOw] */
+    float fx, fy, cx, cy;
+    float* x3D;                  /* out: N x 3 */
+    int32_t* mp;                 /* out (may be NULL): i if depth > 0, else -1 */
+} orb_unproject;
+int Frame_UnprojectStereo_batch_device(ORBmatcher_h h, int count, const orb_unproject* U);
+
 /* DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned>>) as CSR: strictly ascending
  * node ids, the feature indices of node a at feat[start[a] .. start[a+1]) in insertion order.
  * (Computed by the caller's vocabulary; ORBvoc.txt is not shipped with the reference.) */
@@ -472,6 +491,26 @@ int Optimizer_PoseOptimization_batch(int count, const pose_problem* P, float* Tc
 int Optimizer_PoseOptimization_batch_device(int count, const pose_problem* P, float* const* Tcw_out,
                                             uint8_t* const* outlier, int* ninliers);
 
+/* The frame as PoseOptimization(Frame*) reads it (Optimizer.cc:255-347), every array in
+ * device memory: mvpMapPoints as indices into a map-point table (mp[i] = -1: NULL),
+ * pMP->GetWorldPos() = mp_pos[3*mp[i]..], mvKeysUn, mvuRight (< 0: monocular edge) and
+ * the mvInvLevelSigma2 table indexed by kpUn.octave.  The edges are gathered on the
+ * device, so no per-frame host or framework-side packing is needed. */
+typedef struct pose_frame {
+    int N;
+    const float* Tcw;            /* 16 row-major pFrame->mTcw */
+    const int32_t* mp;           /* N */
+    const float* mp_pos;         /* map point rows, 3 floats each */
+    const orb_kp* keysUn;        /* N */
+    const float* uRight;         /* N */
+    const float* invLevelSigma2; /* nlevels */
+    int nlevels;
+    float fx, fy, cx, cy, bf;
+} pose_frame;
+/* Same outputs and capacity rule as Optimizer_PoseOptimization_batch_device. */
+int Optimizer_PoseOptimization_frames_device(int count, const pose_frame* F, float* const* Tcw_out,
+                                             uint8_t* const* outlier, int* ninliers);
+
 /* ----------------------------------------------------------------------
  * Keyframe-block sharded BA across GPUs: one process (or
  * thread) per rank, map points partitioned by the block of their reference
@@ -520,6 +559,8 @@ int orbgpu_unit_wave_tree(const double* v64, double* out);
 /* Instrumented builds only (make prof): read and clear the BA/pose section timers (32 x u64
  * clock64 deltas of workgroup 0); ORB_E_INVALID in normal builds. */
 int orbgpu_debug_prof(unsigned long long* out32);
+/* Section timers of the matcher's greedy replay kernel (instrumented builds only). */
+int orbgpu_debug_prof_match(unsigned long long* out32);
 
 #ifdef __cplusplus
 }

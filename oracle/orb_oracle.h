@@ -215,6 +215,12 @@ int   ora_search_for_triangulation(const ora_featvec* fv1, const ora_kp* k1, con
                                    const float* sigma2_2, const float* F12, int bOnlyStereo, int checkOri,
                                    int* pairs, int cap);
 
+/* ---- Frame::UnprojectStereo (stereo.c), reference Frame.cc:666-680 ----------------
+ * x3D = Rwc * ((u-cx)*z*invfx, (v-cy)*z*invfy, z) + Ow for depth z > 0 (invfx = 1.0f/fx,
+ * Frame.cc:108); Twc = [Rwc | Ow] row-major 4x4; rows with z <= 0 untouched, mp[i] = i or -1. */
+void  ora_unproject_stereo(const ora_kp* kps, const float* depth, int N, const float* Twc, float fx, float fy,
+                           float cx, float cy, float* x3D, int* mp);
+
 /* ---- Frame::ComputeStereoMatches (stereo.c), reference Frame.cc:466-640 ----------
  * kL/dL: left mvKeys + descriptors (NL), kR/dR: right (NR); exL/exR: the extractors that
  * produced them (their last pyramids); rows0 = level-0 rows.  Writes mvuRight / mvDepth

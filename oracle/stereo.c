@@ -155,3 +155,23 @@ int ora_compute_stereo_matches(const ora_kp* kL, const uint8_t* dL, int NL, cons
     free(rcnt); free(ridx); free(fill); free(vd);
     return kept;
 }
+
+/* Frame::UnprojectStereo, Frame.cc:666-680.  mRwc*x3Dc+mOw is one cv::gemm (3x3 by 3x1 plus
+ * 3x1), evaluated as the rest of this oracle evaluates that product: f64 accumulation of the
+ * f32 products, one rounding to float (matchers2.c gemm_row3). */
+void ora_unproject_stereo(const ora_kp* kps, const float* depth, int N, const float* Twc, float fx, float fy,
+                          float cx, float cy, float* x3D, int* mp) {
+    const float invfx = 1.0f / fx, invfy = 1.0f / fy;
+    for (int i = 0; i < N; i++) {
+        const float z = depth[i];
+        if (mp) mp[i] = z > 0 ? i : -1;
+        if (!(z > 0)) continue;
+        const float u = kps[i].x, v = kps[i].y;
+        const float x = (u - cx) * z * invfx;
+        const float y = (v - cy) * z * invfy;
+        for (int r = 0; r < 3; r++) {
+            const double acc = (double)Twc[r * 4 + 0] * x + (double)Twc[r * 4 + 1] * y + (double)Twc[r * 4 + 2] * z;
+            x3D[3 * i + r] = (float)(acc + (double)Twc[r * 4 + 3]);
+        }
+    }
+}

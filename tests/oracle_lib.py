@@ -137,6 +137,23 @@ def oracle_stereo_matches(exL, exR, kL, dL, kR, dR, rows0, mbf, mb):
     return uR[:len(kL)], dep[:len(kL)], kept
 
 
+def oracle_unproject_stereo(kps, depth, Twc, fx, fy, cx, cy):
+    """Frame::UnprojectStereo (Frame.cc:666-680) for every keypoint -> (x3D N x 3, mp N);
+    rows with depth <= 0 are NaN in x3D (the reference returns an empty Mat)."""
+    L = lib()
+    L.ora_unproject_stereo.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_float, C.c_float,
+                                       C.c_float, C.c_float, C.c_void_p, C.c_void_p]
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    depth = np.ascontiguousarray(depth, np.float32)
+    Twc = np.ascontiguousarray(Twc, np.float32)
+    n = len(kps)
+    x3D = np.full((max(n, 1), 3), np.nan, np.float32)
+    mp = np.zeros(max(n, 1), np.int32)
+    L.ora_unproject_stereo(ptr(kps), ptr(depth), n, ptr(Twc), float(fx), float(fy), float(cx), float(cy), ptr(x3D),
+                           ptr(mp))
+    return x3D[:n], mp[:n]
+
+
 # ---------------------------------------------------------------- matcher oracle
 class ora_frame(C.Structure):
     _fields_ = [("N", C.c_int), ("kpsUn", C.c_void_p), ("desc", C.c_void_p), ("uRight", C.c_void_p),

@@ -1,0 +1,111 @@
+"""Frame-level device ops on the tracking path vs the CPU oracle.
+
+* Frame::UnprojectStereo (reference src/Frame.cc:666-680) -- bit-exact x3D and slot indices
+  over a batch (empty frame, all-negative depths, random Twc), rows with depth <= 0 untouched.
+* Optimizer::PoseOptimization(Frame*) in the frame form (map points as indices into a table,
+  keypoints, mvuRight, the mvInvLevelSigma2 table; Optimizer.cc:255-347) -- identical to the
+  packed device form and to the oracle (Tcw bits, outlier flags, nInliers)."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from pose_cases import pose_problem
+
+pytestmark = pytest.mark.gpu
+
+KITTI = (718.856, 718.856, 607.1928, 185.2157)
+
+
+def _rand_T(rng):
+    a = rng.normal(0, 0.3, 3)
+    th = np.linalg.norm(a)
+    k = a / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    T = np.eye(4)
+    T[:3, :3] = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+    T[:3, 3] = rng.normal(0, 5, 3)
+    return T.astype(np.float32)
+
+
+def _kps(rng, n):
+    k = np.zeros(n, oracle_lib.KP_DTYPE)
+    k["x"] = rng.uniform(0, 1241, n).astype(np.float32)
+    k["y"] = rng.uniform(0, 376, n).astype(np.float32)
+    k["octave"] = rng.integers(0, 8, n)
+    return k
+
+
+def test_unproject_stereo_matches_oracle(gpu):
+    import torch
+    import c_orb_slam_amd as orb
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    sizes = [1500, 0, 7, 300]
+    frames, host = [], []
+    for f, n in enumerate(sizes):
+        k = _kps(rng, n)
+        dep = rng.uniform(-5, 60, n).astype(np.float32)
+        if f == 2:
+            dep[:] = -1.0
+        Twc = _rand_T(rng)
+        x3, mp = oracle_lib.oracle_unproject_stereo(k, dep, Twc, *KITTI)
+        host.append((x3, mp, dep))
+        frames.append(dict(keysUn=torch.from_numpy(k.view(np.int32).reshape(n, 7).copy()).to(dev),
+                           depth=torch.from_numpy(dep).to(dev), Twc=torch.from_numpy(Twc.reshape(16)).to(dev),
+                           x3D=torch.full((n, 3), 7.0, dtype=torch.float32, device=dev),
+                           mp=torch.full((n,), -7, dtype=torch.int32, device=dev), cam=KITTI))
+    m = orb.ORBmatcher(0.9, True)
+    m.UnprojectStereo_device(frames)
+    torch.cuda.synchronize()
+    for (x3, mp, dep), fr in zip(host, frames):
+        gx = fr["x3D"].cpu().numpy()
+        gm = fr["mp"].cpu().numpy()
+        assert np.array_equal(gm, mp)
+        ok = dep > 0
+        assert np.array_equal(gx[ok].view(np.uint32), x3[ok].view(np.uint32))
+        assert (gx[~ok] == 7.0).all()
+
+
+def _octaves(inv_sigma2):
+    tab = (np.float32(1.0) / np.float32(1.2) ** (2 * np.arange(8))).astype(np.float32)
+    return np.array([int(np.flatnonzero(tab == v)[0]) for v in inv_sigma2], np.int32), tab
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_pose_frames_form_equals_packed_and_oracle(gpu, seed):
+    import torch
+    from c_orb_slam_amd.optimizer import PoseOptimizationBatchDevice, PoseOptimizationFramesDevice
+    dev = torch.device("cuda", 0)
+    frames = [pose_problem(100 * seed + s, N=400 + 500 * s) for s in range(3)]
+    packed, framed = [], []
+    for fr in frames:
+        N = len(fr["has_mp"])
+        octv, tab = _octaves(fr["inv_sigma2"])
+        k = np.zeros(N, oracle_lib.KP_DTYPE)
+        k["x"], k["y"], k["octave"] = fr["obs"][:, 0], fr["obs"][:, 1], octv
+        # map point table in a shuffled order: the frame form gathers rows by index
+        perm = np.random.default_rng(seed).permutation(N)
+        table = np.zeros((N, 3), np.float32)
+        table[perm] = fr["Xw"]
+        mp = np.where(fr["has_mp"] > 0, perm, -1).astype(np.int32)
+        T = torch.from_numpy(np.ascontiguousarray(fr["Tcw"], np.float32).reshape(16)).to(dev)
+        packed.append(dict(Tcw=T, has_mp=torch.from_numpy(fr["has_mp"]).to(dev), Xw=torch.from_numpy(fr["Xw"]).to(dev),
+                           obs=torch.from_numpy(fr["obs"]).to(dev), inv_sigma2=torch.from_numpy(fr["inv_sigma2"]).to(dev),
+                           cam=fr["cam"]))
+        framed.append(dict(Tcw=T, mp=torch.from_numpy(mp).to(dev), mp_pos=torch.from_numpy(table).to(dev),
+                           keysUn=torch.from_numpy(k.view(np.int32).reshape(N, 7).copy()).to(dev),
+                           uRight=torch.from_numpy(np.ascontiguousarray(fr["obs"][:, 2])).to(dev),
+                           invLevelSigma2=torch.from_numpy(tab).to(dev), cam=fr["cam"]))
+    Tp = [torch.zeros(16, dtype=torch.float32, device=dev) for _ in frames]
+    Tf = [torch.zeros(16, dtype=torch.float32, device=dev) for _ in frames]
+    op = [torch.full((len(f["has_mp"]),), 9, dtype=torch.uint8, device=dev) for f in frames]
+    of = [torch.full((len(f["has_mp"]),), 9, dtype=torch.uint8, device=dev) for f in frames]
+    n_p = PoseOptimizationBatchDevice(packed, Tp, op)
+    n_f = PoseOptimizationFramesDevice(framed, Tf, of)
+    assert np.array_equal(n_p, n_f)
+    for f, fr in enumerate(frames):
+        assert np.array_equal(Tp[f].cpu().numpy(), Tf[f].cpu().numpy())
+        assert np.array_equal(op[f].cpu().numpy(), of[f].cpu().numpy())
+        o = oracle_lib.oracle_pose_optimization(fr)
+        assert int(n_f[f]) == int(o["inliers"])
+        assert np.array_equal(Tf[f].cpu().numpy().reshape(4, 4), o["Tcw"])
