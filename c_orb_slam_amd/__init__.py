@@ -10,3 +10,4 @@ from .optimizer import BundleAdjustment, LocalBundleAdjustment, PoseOptimization
 
 __all__ = ["ORBextractor", "ORBmatcher", "Frame", "MapPoints", "KP_DTYPE", "OrbGpuError",
            "device_available", "lib"]
+from .vocabulary import BowVector, ORBVocabulary  # noqa: F401

@@ -145,6 +145,14 @@ def lib():
     L.Optimizer_PoseOptimization_batch_device.argtypes = [i32, vp, vp, vp, vp]
     L.Optimizer_PoseOptimization_frames_device.argtypes = [i32, vp, vp, vp, vp]
     L.Frame_UnprojectStereo_batch_device.argtypes = [vp, i32, vp]
+    L.ORBvocabulary_create.argtypes = [P(vp)]
+    L.ORBvocabulary_destroy.argtypes = [vp]
+    L.ORBvocabulary_loadFromTextFile.argtypes = [vp, C.c_char_p]
+    L.ORBvocabulary_info.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+    L.ORBvocabulary_transform.argtypes = [vp, vp, i32, i32, vp]
+    L.ORBvocabulary_transform_batch.argtypes = [vp, i32, vp, vp, i32, vp]
+    L.ORBvocabulary_transform_features.argtypes = [vp, vp, i32, i32, vp, vp, vp]
+    L.ORBvocabulary_score.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp, vp]
     L.orbgpu_unit_ldlt_solve.argtypes = [i32, vp, vp, vp, i32, P(i32)]
     L.orbgpu_unit_csum.argtypes = [vp, i32, vp]
     L.orbgpu_unit_ldlt_factor.argtypes = [i32, vp, vp]
@@ -185,6 +193,11 @@ class orb_unproject(C.Structure):
     _fields_ = [("N", C.c_int), ("keysUn", C.c_void_p), ("depth", C.c_void_p), ("Twc", C.c_void_p),
                 ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
                 ("x3D", C.c_void_p), ("mp", C.c_void_p)]
+
+
+class orb_bow(C.Structure):
+    _fields_ = [("cap", C.c_int), ("word", C.c_void_p), ("value", C.c_void_p), ("n_words", C.c_int),
+                ("fv_node", C.c_void_p), ("fv_start", C.c_void_p), ("fv_feat", C.c_void_p), ("n_nodes", C.c_int)]
 
 
 class pose_frame(C.Structure):

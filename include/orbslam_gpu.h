@@ -207,6 +207,53 @@ typedef struct orb_unproject {
 } orb_unproject;
 int Frame_UnprojectStereo_batch_device(ORBmatcher_h h, int count, const orb_unproject* U);
 
+/* ======================================================================
+ * ORBVocabulary (reference include/ORBVocabulary.h: DBoW2::TemplatedVocabulary<
+ * FORB::TDescriptor, FORB>, Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h)
+ * ====================================================================== */
+typedef struct ORBvocabulary_t* ORBvocabulary_h;
+int ORBvocabulary_create(ORBvocabulary_h* out);
+int ORBvocabulary_destroy(ORBvocabulary_h h);
+/* bool loadFromTextFile(const std::string&)  TemplatedVocabulary.h:1338-1424 (host parse).
+ * ORB_E_INVALID where the reference returns false (unreadable file, header out of range) or
+ * a node names a parent not yet defined.  The trailing line after saveToTextFile's final endl
+ * is the reference's undefined behaviour; DESIGN.md §5 states how it is realised. */
+int ORBvocabulary_loadFromTextFile(ORBvocabulary_h h, const char* path);
+/* m_k, m_L, m_scoring, m_weighting, size of m_nodes (root included), size of m_words */
+int ORBvocabulary_info(ORBvocabulary_h h, int* k, int* L, int* scoring, int* weighting, int* n_nodes,
+                       int* n_words);
+/* One frame's DBoW2::BowVector (std::map<WordId, WordValue>: ascending words) and
+ * DBoW2::FeatureVector (as orb_featvec CSR: fv_node ascending, fv_start[n_nodes + 1],
+ * fv_feat in insertion order).  Host buffers of capacity `cap` >= N (fv_start: cap + 1). */
+typedef struct orb_bow {
+    int cap;
+    uint32_t* word;
+    double* value;
+    int n_words;                 /* out */
+    uint32_t* fv_node;
+    int32_t* fv_start;
+    int32_t* fv_feat;
+    int n_nodes;                 /* out */
+} orb_bow;
+/* void transform(const vector<TDescriptor>& features, BowVector& v, FeatureVector& fv,
+ *                int levelsup) const                       TemplatedVocabulary.h:1126-1197
+ * = Frame::ComputeBoW / KeyFrame::ComputeBoW with levelsup 4 (Frame.cc:395-402).
+ * desc: N x 32 descriptors (host).  N <= 4096 per frame (ORB_E_CAPACITY). */
+int ORBvocabulary_transform(ORBvocabulary_h h, const uint8_t* desc, int N, int levelsup, orb_bow* out);
+/* `count` frames in one launch (one tree walk per descriptor, one assembly per frame). */
+int ORBvocabulary_transform_batch(ORBvocabulary_h h, int count, const uint8_t* const* desc, const int* N,
+                                  int levelsup, orb_bow* out);
+/* void transform(const TDescriptor& feature, WordId& id, WordValue& weight, NodeId* nid,
+ *                int levelsup) const, for each of N descriptors  TemplatedVocabulary.h:1217-1256 */
+int ORBvocabulary_transform_features(ORBvocabulary_h h, const uint8_t* desc, int N, int levelsup,
+                                     uint32_t* word, double* weight, uint32_t* node);
+/* double score(const BowVector& a, const BowVector& b) const  (L1Scoring::score,
+ * ScoringObject.cpp:21-66) of one query BowVector against `count` candidates given as CSR
+ * (candidate c: words/values [cstart[c], cstart[c+1])), as KeyFrameDatabase scores the
+ * keyframes sharing words (KeyFrameDatabase.cc:133, 249).  L1_NORM vocabularies only. */
+int ORBvocabulary_score(ORBvocabulary_h h, const uint32_t* qw, const double* qv, int nq, int count,
+                        const int32_t* cstart, const uint32_t* cw, const double* cv, double* scores);
+
 /* DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned>>) as CSR: strictly ascending
  * node ids, the feature indices of node a at feat[start[a] .. start[a+1]) in insertion order.
  * (Computed by the caller's vocabulary; ORBvoc.txt is not shipped with the reference.) */

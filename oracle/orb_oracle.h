@@ -215,6 +215,17 @@ int   ora_search_for_triangulation(const ora_featvec* fv1, const ora_kp* k1, con
                                    const float* sigma2_2, const float* F12, int bOnlyStereo, int checkOri,
                                    int* pairs, int cap);
 
+/* ---- DBoW2 vocabulary (dbow2.c), reference Thirdparty/DBoW2 ------------------------ */
+typedef struct ora_voc ora_voc;
+ora_voc* ora_voc_load_text(const char* path, int* err);   /* loadFromTextFile, TemplatedVocabulary.h:1338 */
+void  ora_voc_free(ora_voc* v);
+void  ora_voc_info(const ora_voc* v, int* k, int* L, int* scoring, int* weighting, int* nnodes, int* nwords);
+void  ora_voc_transform_feature(const ora_voc* v, const uint8_t* f, int levelsup, uint32_t* word, double* weight,
+                                uint32_t* nid);
+int   ora_voc_transform(const ora_voc* v, const uint8_t* desc, int N, int levelsup, uint32_t* bow_w, double* bow_v,
+                        int* n_bow, uint32_t* fv_node, int* fv_start, int* fv_feat, int* n_fv);
+double ora_voc_score_l1(const uint32_t* w1, const double* v1, int n1, const uint32_t* w2, const double* v2, int n2);
+
 /* ---- Frame::UnprojectStereo (stereo.c), reference Frame.cc:666-680 ----------------
  * x3D = Rwc * ((u-cx)*z*invfx, (v-cy)*z*invfy, z) + Ow for depth z > 0 (invfx = 1.0f/fx,
  * Frame.cc:108); Twc = [Rwc | Ow] row-major 4x4; rows with z <= 0 untouched, mp[i] = i or -1. */

@@ -154,6 +154,61 @@ def oracle_unproject_stereo(kps, depth, Twc, fx, fy, cx, cy):
     return x3D[:n], mp[:n]
 
 
+class OracleVocabulary:
+    """TemplatedVocabulary (Thirdparty/DBoW2) restated on CPU: loadFromTextFile, transform, score."""
+
+    def __init__(self, path):
+        L = lib()
+        L.ora_voc_load_text.restype = C.c_void_p
+        L.ora_voc_load_text.argtypes = [C.c_char_p, C.POINTER(C.c_int)]
+        L.ora_voc_free.argtypes = [C.c_void_p]
+        L.ora_voc_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 6
+        L.ora_voc_transform_feature.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.ora_voc_transform.restype = C.c_int
+        L.ora_voc_transform.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 7
+        L.ora_voc_score_l1.restype = C.c_double
+        L.ora_voc_score_l1.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        self.L = L
+        err = C.c_int()
+        self.h = L.ora_voc_load_text(os.fsencode(str(path)), C.byref(err))
+        self.err = err.value
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.ora_voc_free(self.h)
+
+    def info(self):
+        v = [C.c_int() for _ in range(6)]
+        self.L.ora_voc_info(self.h, *[C.byref(x) for x in v])
+        return dict(zip(["k", "L", "scoring", "weighting", "nodes", "words"], [x.value for x in v]))
+
+    def transform_features(self, desc, levelsup=4):
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(d)
+        w, wt, nd = np.zeros(n, np.uint32), np.zeros(n, np.float64), np.zeros(n, np.uint32)
+        for i in range(n):
+            self.L.ora_voc_transform_feature(self.h, d[i].ctypes.data, int(levelsup), w[i:].ctypes.data,
+                                             wt[i:].ctypes.data, nd[i:].ctypes.data)
+        return w, wt, nd
+
+    def transform(self, desc, levelsup=4):
+        """-> (words, values, fv_node, fv_start, fv_feat)."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = max(len(d), 1)
+        bw, bv = np.zeros(n, np.uint32), np.zeros(n, np.float64)
+        fn, fs, ff = np.zeros(n, np.uint32), np.zeros(n + 1, np.int32), np.zeros(n, np.int32)
+        nb, nf = C.c_int(), C.c_int()
+        self.L.ora_voc_transform(self.h, ptr(d), len(d), int(levelsup), ptr(bw), ptr(bv), C.byref(nb), ptr(fn), ptr(fs),
+                                 ptr(ff), C.byref(nf))
+        m = int(fs[nf.value]) if nf.value else 0
+        return bw[:nb.value], bv[:nb.value], fn[:nf.value], fs[:nf.value + 1], ff[:m]
+
+    def score(self, w1, v1, w2, v2):
+        w1, w2 = np.ascontiguousarray(w1, np.uint32), np.ascontiguousarray(w2, np.uint32)
+        v1, v2 = np.ascontiguousarray(v1, np.float64), np.ascontiguousarray(v2, np.float64)
+        return self.L.ora_voc_score_l1(w1.ctypes.data, v1.ctypes.data, len(w1), w2.ctypes.data, v2.ctypes.data, len(w2))
+
+
 # ---------------------------------------------------------------- matcher oracle
 class ora_frame(C.Structure):
     _fields_ = [("N", C.c_int), ("kpsUn", C.c_void_p), ("desc", C.c_void_p), ("uRight", C.c_void_p),
