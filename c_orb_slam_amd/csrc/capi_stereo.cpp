@@ -1,6 +1,7 @@
 // capi_stereo.cpp -- extern "C" ORBmatcher_ComputeStereoMatches[_batch] (include/orbslam_gpu.h).
 // Replaces ORB_SLAM2::Frame::ComputeStereoMatches (reference src/Frame.cc:466-640).
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -68,10 +69,13 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
     P.mbf = mbf;
     P.mb = mb;
     P.rows0 = LL[0].h;
+    if (P.rows0 > orbgpu::kStereoMaxRows) return ORB_E_INVALID;
+    // rows a right keypoint covers: ceil(y + r) - floor(y - r) + 1 <= 2r + 3, r = 2 * scale
+    const int band = (int)std::ceil(4.0f * EL->scale()[LL.size() - 1]) + 3;
     size_t need = al(sizeof(orbgpu::StereoDev) * npairs) + al(4 * (size_t)npairs);
     int maxNL = 0;
     for (int p = 0; p < npairs; p++) {
-        need += al(4 * (size_t)NL[p]);
+        need += al(4 * (size_t)NL[p]) + al(4 * ((size_t)P.rows0 + 1)) + al(4 * (size_t)NR[p] * band + 4);
         if (!dev) need += al(28 * (size_t)NL[p]) + al(32 * (size_t)NL[p]) + al(28 * (size_t)NR[p]) +
                           al(32 * (size_t)NR[p]) + 2 * al(4 * (size_t)NL[p]);
         maxNL = std::max(maxNL, NL[p]);
@@ -87,6 +91,9 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
         S.pyrL = EL->pyramid_base() + (size_t)p * EL->pyramid_image_bytes();
         S.pyrR = ER->pyramid_base() + (size_t)p * ER->pyramid_image_bytes();
         S.sad = (int*)m->arena_alloc(4 * (size_t)NL[p] + 4);
+        S.rowStart = (int*)m->arena_alloc(4 * ((size_t)P.rows0 + 1));
+        S.rowIdx = (int*)m->arena_alloc(4 * (size_t)NR[p] * band + 4);
+        if (!S.sad || !S.rowStart || !S.rowIdx) return ORB_E_HIP;
         S.kept = d_kept + p;
         if (dev) {
             S.kL = (const orbgpu::orb_kp_dev*)keysL[p];
@@ -153,7 +160,8 @@ int Frame_UnprojectStereo_batch_device(ORBmatcher_h h, int count, const orb_unpr
         d.mp = Q.mp;
         maxN = std::max(maxN, Q.N);
     }
-    return orbgpu::unproject_batch(P.data(), count, maxN, h->m->stream()) ? ORB_E_HIP : ORB_OK;
+    (void)maxN;
+    return orbgpu::unproject_batch(P.data(), count, h->m->stream()) ? ORB_E_HIP : ORB_OK;
 }
 
 }  // extern "C"

@@ -16,7 +16,9 @@
 //                    thDist = 1.5f*1.4f*median, invalidation of SAD >= thDist.
 #include "stereo.hpp"
 
+#include <algorithm>
 #include <climits>
+#include <cstring>
 
 namespace orbgpu {
 
@@ -33,6 +35,62 @@ __device__ __forceinline__ unsigned wave_min_u(unsigned v) {
     return v;
 }
 
+// vRowIndices (Frame.cc:476-493) as a CSR per pair: right keypoint iR is listed on every row
+// yi in [floor(y - r), ceil(y + r)], r = 2 * mvScaleFactors[octave].  The order inside a row
+// does not matter: the match kernel takes the minimum of (dist, iR).
+__global__ void __launch_bounds__(1024) k_stereo_rows(const StereoDev* __restrict__ probs, StereoParams P) {
+    const StereoDev& S = probs[blockIdx.x];
+    __shared__ int s_cnt[kStereoMaxRows];
+    __shared__ int s_w[16];
+    const int tid = threadIdx.x, rows = P.rows0;
+    for (int y = tid; y < rows; y += 1024) s_cnt[y] = 0;
+    __syncthreads();
+    for (int iR = tid; iR < S.NR; iR += 1024) {
+        const orb_kp_dev kp = S.kR[iR];
+        const float r = 2.0f * P.scale[kp.octave];
+        const int maxr = min((int)ceilf(kp.y + r), rows - 1), minr = max((int)floorf(kp.y - r), 0);
+        for (int y = minr; y <= maxr; y++) atomicAdd(&s_cnt[y], 1);
+    }
+    __syncthreads();
+    // exclusive scan of the row counts (rows <= 4096: 4 per thread)
+    const int lane = tid & 63, wid = tid >> 6;
+    int v[4], loc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int y = 4 * tid + k;
+        v[k] = y < rows ? s_cnt[y] : 0;
+        loc += v[k];
+    }
+    int incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    int off = 0;
+    for (int w = 0; w < wid; w++) off += s_w[w];
+    int run = off + incl - loc;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int y = 4 * tid + k;
+        if (y < rows) {
+            S.rowStart[y] = run;
+            s_cnt[y] = run;   // fill cursor
+        }
+        run += v[k];
+    }
+    if (tid == 1023) S.rowStart[rows] = run;
+    __syncthreads();
+    for (int iR = tid; iR < S.NR; iR += 1024) {
+        const orb_kp_dev kp = S.kR[iR];
+        const float r = 2.0f * P.scale[kp.octave];
+        const int maxr = min((int)ceilf(kp.y + r), rows - 1), minr = max((int)floorf(kp.y - r), 0);
+        for (int y = minr; y <= maxr; y++) S.rowIdx[atomicAdd(&s_cnt[y], 1)] = iR;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restrict__ probs, StereoParams P) {
     const StereoDev& S = probs[blockIdx.y];
     const int lane = threadIdx.x & 63;
@@ -47,17 +105,16 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
     const float minZ = P.mb, minD = 0.0f, maxD = P.mbf / minZ;
     const float minU = uL - maxD, maxU = uL - minD;
     if (row >= 0 && row < P.rows0 && !(maxU < 0)) {
-        // best right keypoint: first strict minimum below TH_HIGH in iR order
+        // best right keypoint among the row's candidates: first strict minimum below TH_HIGH in iR order
         const uint32_t* dl = (const uint32_t*)(S.dL + 32 * (size_t)iL);   // descriptors: 4-B aligned rows
         uint32_t q[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) q[k] = dl[k];
         unsigned best = 0xffffffffu;
-        for (int iR = lane; iR < S.NR; iR += 64) {
+        const int c1 = S.rowStart[row + 1];
+        for (int c = S.rowStart[row] + lane; c < c1; c += 64) {
+            const int iR = S.rowIdx[c];
             const orb_kp_dev kpR = S.kR[iR];
-            const float r = 2.0f * P.scale[kpR.octave];
-            const int maxr = (int)ceilf(kpR.y + r), minr = (int)floorf(kpR.y - r);
-            if (row < minr || row > maxr) continue;
             if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
             const float uR = kpR.x;
             if (!(uR >= minU && uR <= maxU)) continue;
@@ -198,6 +255,7 @@ __global__ void __launch_bounds__(1024) k_stereo_filter(const StereoDev* __restr
 
 int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoParams& P, hipStream_t s) {
     if (nprob <= 0) return 0;
+    hipLaunchKernelGGL(k_stereo_rows, dim3(nprob), dim3(1024), 0, s, d_probs, P);
     if (maxNL > 0)
         hipLaunchKernelGGL(k_stereo_match, dim3((maxNL + 3) / 4, nprob), dim3(256), 0, s, d_probs, P);
     hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(1024), 0, s, d_probs);
@@ -208,8 +266,14 @@ int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoPa
 // ------------------------------------------------------------ UnprojectStereo
 // x3Dc = ((u-cx)*z*invfx, (v-cy)*z*invfy, z) in float, then mRwc*x3Dc + mOw as one cv::gemm
 // (the matcher's convention: f64 accumulation, one rounding to float).  One thread per keypoint.
-__global__ void __launch_bounds__(256) k_unproject(const UnprojDev* __restrict__ probs) {
-    const UnprojDev P = probs[blockIdx.y];
+// The frames travel as kernel arguments (kUnprojPerLaunch per launch), so an asynchronous call
+// leaves no host or device staging buffer behind.
+struct UnprojBatch {
+    UnprojDev p[kUnprojPerLaunch];
+};
+
+__global__ void __launch_bounds__(256) k_unproject(UnprojBatch B) {
+    const UnprojDev& P = B.p[blockIdx.y];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.N) return;
     const float z = P.depth[i];
@@ -226,18 +290,18 @@ __global__ void __launch_bounds__(256) k_unproject(const UnprojDev* __restrict__
     }
 }
 
-int unproject_batch(const UnprojDev* probs, int count, int maxN, hipStream_t s) {
-    thread_local void* d_buf = nullptr;   // grow-only, one per calling thread
-    thread_local size_t cap = 0;
-    const size_t need = sizeof(UnprojDev) * (size_t)count;
-    if (need > cap) {
-        if (d_buf) (void)hipFree(d_buf);
-        cap = need * 2;
-        ORB_HIP_CHECK(hipMalloc(&d_buf, cap));
+int unproject_batch(const UnprojDev* probs, int count, hipStream_t s) {
+    for (int f0 = 0; f0 < count; f0 += kUnprojPerLaunch) {
+        const int n = std::min(kUnprojPerLaunch, count - f0);
+        UnprojBatch B;
+        std::memset(&B, 0, sizeof(B));
+        int maxN = 0;
+        for (int f = 0; f < n; f++) {
+            B.p[f] = probs[f0 + f];
+            maxN = std::max(maxN, B.p[f].N);
+        }
+        if (maxN > 0) hipLaunchKernelGGL(k_unproject, dim3((maxN + 255) / 256, n), dim3(256), 0, s, B);
     }
-    ORB_HIP_CHECK(hipMemcpyAsync(d_buf, probs, need, hipMemcpyHostToDevice, s));
-    if (maxN > 0)
-        hipLaunchKernelGGL(k_unproject, dim3((maxN + 255) / 256, count), dim3(256), 0, s, (const UnprojDev*)d_buf);
     ORB_HIP_CHECK(hipGetLastError());
     return 0;
 }

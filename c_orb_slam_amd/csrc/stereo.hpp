@@ -11,6 +11,7 @@ namespace orbgpu {
 
 constexpr int kStereoMaxKeys = 4096;
 constexpr int kStereoMaxLevels = 16;
+constexpr int kStereoMaxRows = 4096;   // mvImagePyramid[0].rows (the row table lives in LDS)
 
 struct StereoLevel {   // padded level l of one image slab: (0,0) of the unpadded level at +19 rows/cols
     long long off;
@@ -37,6 +38,8 @@ struct StereoDev {
     float* depth;           // out: mvDepth (NL)
     int* sad;               // scratch (NL): best SAD or -1
     int* kept;              // out: stereo matches after the median filter
+    int* rowStart;          // scratch (rows0 + 1): vRowIndices as CSR (Frame.cc:476-493)
+    int* rowIdx;            // scratch (NR * band rows)
 };
 
 int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoParams& P, hipStream_t s);
@@ -51,7 +54,8 @@ struct UnprojDev {
     float* x3D;
     int* mp;
 };
-// enqueue on `s`; the problem array is copied from host through a per-thread grow-only buffer
-int unproject_batch(const UnprojDev* probs, int count, int maxN, hipStream_t s);
+constexpr int kUnprojPerLaunch = 56;   // frames per launch, passed by value (kernel-argument space)
+// enqueue on `s` (no staging buffer: the frames are kernel arguments)
+int unproject_batch(const UnprojDev* probs, int count, hipStream_t s);
 
 }  // namespace orbgpu
