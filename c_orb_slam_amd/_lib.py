@@ -159,6 +159,7 @@ def lib():
     L.orbgpu_unit_wave_tree.argtypes = [vp, vp]
     L.orbgpu_debug_prof.argtypes = [vp]
     L.orbgpu_debug_prof_match.argtypes = [vp]
+    L.orbgpu_debug_prof_extract.argtypes = [vp]
     L.Sim3Solver_create.argtypes = [i32, vp, vp, vp, vp, vp, i32, vp, vp, i32, P(vp)]
     L.Sim3Solver_destroy.argtypes = [vp]
     L.Sim3Solver_set_ransac.argtypes = [vp, C.c_double, i32, i32]

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "ba.hpp"
+#include "orb_extract.hpp"
 #include "orb_match.hpp"
 
 namespace {
@@ -284,6 +285,9 @@ int orbgpu_unit_ldlt_factor(int n, const double* S, double* out) {
 }
 
 int orbgpu_debug_prof(unsigned long long* out32) { return out32 ? orbgpu::debug_prof(out32) : ORB_E_INVALID; }
+int orbgpu_debug_prof_extract(unsigned long long* out32) {
+    return out32 ? orbgpu::debug_prof_extract(out32) : ORB_E_INVALID;
+}
 int orbgpu_debug_prof_match(unsigned long long* out32) {
     return out32 ? orbgpu::debug_prof_match(out32) : ORB_E_INVALID;
 }

@@ -294,6 +294,7 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     uint8_t* s_sc = reinterpret_cast<uint8_t*>(s_sc32);
     // identity cell order: the XCD-contiguous order (xcd_tile) cut FETCH_SIZE 4.8x here but ran
     // ~9 % slower -- this kernel is VALU-bound and the contiguous runs unbalance the XCDs
+    ORBGPU_PROF_START;
     const int cell = blockIdx.x;
     const CellDesc cd = cells[cell];
     const int b = blockIdx.y;
@@ -311,14 +312,26 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     constexpr int ldw = FC_LD / 4;
     const int wpr = (cols + mis + 3) >> 2, pw = cd.pitch >> 2;
     {
-        const int rr = lane / ldw, w = lane - rr * ldw;   // 3 rows x 19 dwords per wave instruction
-        for (int r0 = wid * 3; r0 < rows; r0 += 12) {
-            const int r = r0 + rr;
-            if (rr < 3 && r < rows && w < wpr) s_img32[r * ldw + w] = P32[(size_t)r * pw + w];
+        // 3 rows x 19 dwords per wave instruction; rows wid*3 + rr + 12k (k < 6 covers FC_MAXR):
+        // every load of the thread is issued before the first LDS store (one wait, not six)
+        const int rr = lane / ldw, w = lane - rr * ldw;
+        const bool ok = rr < 3 && w < wpr;
+        const uint32_t* g = P32 + (size_t)(wid * 3 + rr) * pw + w;
+        uint32_t v[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int r = wid * 3 + rr + 12 * k;
+            v[k] = (ok && r < rows) ? g[(size_t)12 * k * pw] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int r = wid * 3 + rr + 12 * k;
+            if (ok && r < rows) s_img32[r * ldw + w] = v[k];
         }
     }
     for (int i = tid; i < rows * ldw; i += 256) s_sc32[i] = 0u;
     __syncthreads();
+    ORBGPU_PROF_MARK(0);
     const int dr = rows - 6, dc = cols - 6;
     const int tp = min(iniTh, minTh);
     // lane -> (row slot, column): two rows per instruction for cells <= 32 columns
@@ -340,6 +353,7 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
         }
     }
     __syncthreads();
+    ORBGPU_PROF_MARK(1);
     if (wid == 0) mask_scan64(s_mask, dr, s_off, lane);
     __syncthreads();
     const int nl = s_off[64];
@@ -357,6 +371,7 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
         s_sc[r * FC_LD + cc] = (uint8_t)max(sc, 0);
     }
     __syncthreads();
+    ORBGPU_PROF_MARK(2);
     uint32_t* out = slots + (size_t)b * slots_per_image + cd.slot_off;
     const int nch = (nl + 63) >> 6;
     int th = iniTh;
@@ -401,6 +416,7 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
                 }
             }
             if (tid == 0) *cnt_out = min(total, cd.cap);
+            ORBGPU_PROF_MARK(3);
             break;
         }
         th = minTh;
@@ -1015,6 +1031,18 @@ int Extractor::get_blurred(int index, int level, uint8_t* dst, int dst_step, int
     ORB_HIP_CHECK(hipMemcpy2D(dst, dst_step, (const uint8_t*)d_blur_ + (size_t)index * blur_bytes_ + L.boff, L.bpitch,
                               L.w, L.h, hipMemcpyDeviceToHost));
     return 0;
+}
+
+int debug_prof_extract(unsigned long long* out32) {
+#ifdef ORBGPU_PROF
+    ORB_HIP_CHECK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_orbgpu_prof), sizeof(unsigned long long) * 32));
+    unsigned long long z[32] = {};
+    ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_orbgpu_prof), z, sizeof(z)));
+    return 0;
+#else
+    (void)out32;
+    return -1;
+#endif
 }
 
 int Extractor::timings(float* ms6) {

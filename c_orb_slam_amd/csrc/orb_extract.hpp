@@ -118,4 +118,6 @@ private:
 
 };
 
+int debug_prof_extract(unsigned long long* out32);   // section timers of k_fast_cells (prof builds)
+
 }  // namespace orbgpu

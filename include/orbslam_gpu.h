@@ -608,6 +608,8 @@ int orbgpu_unit_wave_tree(const double* v64, double* out);
 int orbgpu_debug_prof(unsigned long long* out32);
 /* Section timers of the matcher's greedy replay kernel (instrumented builds only). */
 int orbgpu_debug_prof_match(unsigned long long* out32);
+/* Section timers of the FAST cell kernel (instrumented builds only). */
+int orbgpu_debug_prof_extract(unsigned long long* out32);
 
 #ifdef __cplusplus
 }

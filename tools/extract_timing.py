@@ -28,3 +28,10 @@ for it in range(13):
             acc[k] = acc.get(k, 0) + v / 10
         acc["wall"] = acc.get("wall", 0) + wall / 10
 print({k: round(v, 4) for k, v in acc.items()}, flush=True)
+
+if __import__("os").environ.get("ORBGPU_PROF_DUMP"):
+    import ctypes as C
+    from c_orb_slam_amd._lib import lib
+    buf = (C.c_ulonglong * 32)()
+    lib().orbgpu_debug_prof_extract(buf)
+    print("k_fast_cells sections (cycles, cell 0 of image 0, 13 calls):", list(buf)[:6], flush=True)
