@@ -216,6 +216,9 @@ __global__ void __launch_bounds__(256) k_blur7(const uint8_t* __restrict__ pyr, 
     }
 }
 
+__device__ __forceinline__ int min3(int a, int b, int c) { return min(min(a, b), c); }
+__device__ __forceinline__ int max3(int a, int b, int c) { return max(max(a, b), c); }
+
 // FAST-9/16 score S = max(A,B)-1 (OpenCV cornerScore<16>): A/B = best
 // contiguous-9 dark/bright contrast.  A pixel is a corner at threshold t
 // iff S >= t, and its stored score is then S (see oracle/ocv_semantics.c).
@@ -234,15 +237,18 @@ __device__ __forceinline__ int fast_score_lds(const uint8_t* p, int ld) {
         mn2[k] = min(d[k], d[(k + 1) & 15]);
         mx2[k] = max(d[k], d[(k + 1) & 15]);
     }
-    int A = -1000, B = -1000;
+    // arcs k and k+1 (k even) share d[k+1..k+8]: max over the pair of the arc minima is
+    // min(shared minimum, max(d[k], d[k+9])) (and the mirrored form for the maxima), so the
+    // 16 arcs cost 8 shared reductions
+    int A = -1000, M = 1000;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        // arc k..k+8 = pairs (k,k+1),(k+2,k+3),(k+4,k+5),(k+6,k+7) + element k+8
-        const int mn = min(min(min(mn2[k], mn2[(k + 2) & 15]), min(mn2[(k + 4) & 15], mn2[(k + 6) & 15])), d[(k + 8) & 15]);
-        const int mx = max(max(max(mx2[k], mx2[(k + 2) & 15]), max(mx2[(k + 4) & 15], mx2[(k + 6) & 15])), d[(k + 8) & 15]);
-        A = max(A, mn);
-        B = max(B, -mx);
+    for (int k = 0; k < 16; k += 2) {
+        const int smin = min(min3(mn2[(k + 1) & 15], mn2[(k + 3) & 15], mn2[(k + 5) & 15]), mn2[(k + 7) & 15]);
+        const int smax = max(max3(mx2[(k + 1) & 15], mx2[(k + 3) & 15], mx2[(k + 5) & 15]), mx2[(k + 7) & 15]);
+        A = max(A, min(smin, max(d[k], d[(k + 9) & 15])));
+        M = min(M, max(smax, min(d[k], d[(k + 9) & 15])));
     }
+    const int B = -M;
     return max(A, B) - 1;
 }
 
