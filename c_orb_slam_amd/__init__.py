@@ -6,7 +6,8 @@ library liborbslam_gpu.so (gfx950); there is no CPU fallback.
 """
 from ._lib import KP_DTYPE, OrbGpuError, device_available, lib  # noqa: F401
 from .orb import FeatureVector, Frame, MapPoints, ORBextractor, ORBmatcher  # noqa: F401
-from .optimizer import BundleAdjustment, LocalBundleAdjustment, PoseOptimization, PoseOptimizationBatch  # noqa: F401
+from .optimizer import (BundleAdjustment, LocalBundleAdjustment, OptimizeSim3, OptimizeSim3Batch,  # noqa: F401
+                        PoseOptimization, PoseOptimizationBatch)
 
 __all__ = ["ORBextractor", "ORBmatcher", "Frame", "MapPoints", "KP_DTYPE", "OrbGpuError",
            "device_available", "lib"]

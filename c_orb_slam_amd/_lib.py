@@ -143,6 +143,8 @@ def lib():
     L.Optimizer_PoseOptimization.argtypes = [P(pose_problem), vp, vp, P(i32)]
     L.Optimizer_PoseOptimization_batch.argtypes = [i32, vp, vp, vp, vp]
     L.Optimizer_PoseOptimization_batch_device.argtypes = [i32, vp, vp, vp, vp]
+    L.Optimizer_OptimizeSim3.argtypes = [vp, vp, vp, P(i32)]
+    L.Optimizer_OptimizeSim3_batch.argtypes = [i32, vp, vp, vp, vp]
     L.Optimizer_PoseOptimization_frames_device.argtypes = [i32, vp, vp, vp, vp]
     L.Frame_UnprojectStereo_batch_device.argtypes = [vp, i32, vp]
     L.ORBvocabulary_create.argtypes = [P(vp)]
@@ -212,6 +214,13 @@ class pose_problem(C.Structure):
     _fields_ = [("N", C.c_int), ("Tcw", C.c_void_p), ("has_mp", C.c_void_p), ("Xw", C.c_void_p),
                 ("obs", C.c_void_p), ("inv_sigma2", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
                 ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float)]
+
+
+class sim3opt_problem(C.Structure):
+    _fields_ = [("N", C.c_int), ("valid", C.c_void_p), ("X1c", C.c_void_p), ("X2c", C.c_void_p),
+                ("obs1", C.c_void_p), ("obs2", C.c_void_p), ("inv_sigma2_1", C.c_void_p),
+                ("inv_sigma2_2", C.c_void_p), ("K1", C.c_float * 4), ("K2", C.c_float * 4), ("th2", C.c_float),
+                ("bFixScale", C.c_int)]
 
 
 class ba_result(C.Structure):

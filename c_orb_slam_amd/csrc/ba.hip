@@ -26,104 +26,13 @@
 #include <cstring>
 #include <numeric>
 
+#include "ba_math.hpp"
 #include "detmath.hpp"
 #include "ldlt.hpp"
 #include "orb_common.hpp"
 
 namespace orbgpu {
 
-// ---------------------------------------------------------------- math (host + device)
-#define HD __host__ __device__ __forceinline__
-
-HD void quat_normalize(double* q) {
-    const double z = ((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3];
-    if (z > 0) {
-        const double n = sqrt(z);
-        for (int i = 0; i < 4; i++) q[i] = q[i] / n;
-    }
-}
-
-HD void se3_normalize(Se3& T) {
-    if (T.q[3] < 0)
-        for (int i = 0; i < 4; i++) T.q[i] *= -1;
-    quat_normalize(T.q);
-}
-
-// Eigen Quaternion(Matrix3) branch for a dominant diagonal entry I (static indices keep the
-// matrix in registers on the device)
-template <int I>
-HD void quat_from_R_diag(const double* m, double* q) {
-    constexpr int J = (I + 1) % 3, K = (J + 1) % 3;
-    double t = sqrt(((m[I * 4] - m[J * 4]) - m[K * 4]) + 1.0);
-    q[I] = 0.5 * t;
-    t = 0.5 / t;
-    q[3] = (m[K * 3 + J] - m[J * 3 + K]) * t;
-    q[J] = (m[J * 3 + I] + m[I * 3 + J]) * t;
-    q[K] = (m[K * 3 + I] + m[I * 3 + K]) * t;
-}
-
-HD void quat_from_R(const double* m, double* q) {
-    double t = (m[0] + m[4]) + m[8];
-    if (t > 0) {
-        t = sqrt(t + 1.0);
-        q[3] = 0.5 * t;
-        t = 0.5 / t;
-        q[0] = (m[7] - m[5]) * t;
-        q[1] = (m[2] - m[6]) * t;
-        q[2] = (m[3] - m[1]) * t;
-    } else {
-        int i = 0;
-        if (m[4] > m[0]) i = 1;
-        if (m[8] > (i == 0 ? m[0] : m[4])) i = 2;
-        if (i == 0) quat_from_R_diag<0>(m, q);
-        else if (i == 1) quat_from_R_diag<1>(m, q);
-        else quat_from_R_diag<2>(m, q);
-    }
-}
-
-HD void quat_to_R(const double* q, double* R) {
-    const double x = q[0], y = q[1], z = q[2], w = q[3];
-    const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
-    const double twx = tx * w, twy = ty * w, twz = tz * w;
-    const double txx = tx * x, txy = ty * x, txz = tz * x;
-    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
-    R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;         R[2] = txz + twy;
-    R[3] = txy + twz;         R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
-    R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.0 - (txx + tyy);
-}
-
-HD void cross3(const double* a, const double* b, double* c) {
-    c[0] = a[1] * b[2] - a[2] * b[1];
-    c[1] = a[2] * b[0] - a[0] * b[2];
-    c[2] = a[0] * b[1] - a[1] * b[0];
-}
-
-HD void quat_rotate(const double* q, const double* v, double* out) {
-    double uv[3], c[3];
-    cross3(q, v, uv);
-    for (int i = 0; i < 3; i++) uv[i] += uv[i];
-    cross3(q, uv, c);
-    for (int i = 0; i < 3; i++) out[i] = (v[i] + q[3] * uv[i]) + c[i];
-}
-
-HD void se3_map(const Se3& T, const double* X, double* out) {
-    double r[3];
-    quat_rotate(T.q, X, r);
-    for (int i = 0; i < 3; i++) out[i] = r[i] + T.t[i];
-}
-
-HD void se3_mul(const Se3& a, const Se3& b, Se3& o) {
-    Se3 r{};
-    double rt[3];
-    quat_rotate(a.q, b.t, rt);
-    for (int i = 0; i < 3; i++) r.t[i] = a.t[i] + rt[i];
-    r.q[3] = ((a.q[3] * b.q[3] - a.q[0] * b.q[0]) - a.q[1] * b.q[1]) - a.q[2] * b.q[2];
-    r.q[0] = ((a.q[3] * b.q[0] + a.q[0] * b.q[3]) + a.q[1] * b.q[2]) - a.q[2] * b.q[1];
-    r.q[1] = ((a.q[3] * b.q[1] + a.q[1] * b.q[3]) + a.q[2] * b.q[0]) - a.q[0] * b.q[2];
-    r.q[2] = ((a.q[3] * b.q[2] + a.q[2] * b.q[3]) + a.q[0] * b.q[1]) - a.q[1] * b.q[0];
-    se3_normalize(r);
-    o = r;
-}
 
 __device__ __forceinline__ void se3_exp(const double* upd, Se3& out) {
     const double* w = upd;
@@ -194,92 +103,6 @@ __device__ __forceinline__ void huber(const EdgeDev& e, double chi, double* rho0
     }
 }
 
-// ---------------------------------------------------------------- canonical reductions
-// Canonical 64-tree across a wave: lane i (< off) += lane i + off for off = 32..1, result in
-// lane 0.  gfx950 cross-lane moves instead of LDS: v_permlane32_swap (off 32),
-// v_permlane16_swap (off 16), DPP row_shl (off 8..1, within the first row).
-__device__ __forceinline__ unsigned xl_down(unsigned v, int off) {
-    switch (off) {
-        case 32: return __builtin_amdgcn_permlane32_swap(v, v, false, false)[1];
-        case 16: return __builtin_amdgcn_permlane16_swap(v, v, false, false)[1];
-        case 8: return __builtin_amdgcn_update_dpp(0u, v, 0x108, 0xf, 0xf, false);
-        case 4: return __builtin_amdgcn_update_dpp(0u, v, 0x104, 0xf, 0xf, false);
-        case 2: return __builtin_amdgcn_update_dpp(0u, v, 0x102, 0xf, 0xf, false);
-        default: return __builtin_amdgcn_update_dpp(0u, v, 0x101, 0xf, 0xf, false);
-    }
-}
-__device__ __forceinline__ double wave_down(double v, int off) {
-    const unsigned long long u = __double_as_longlong(v);
-    const unsigned lo = xl_down((unsigned)(u & 0xffffffffu), off);
-    const unsigned hi = xl_down((unsigned)(u >> 32), off);
-    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ double wave_tree(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += wave_down(v, off);
-    return v;
-}
-
-// Canonical sum (oracle ora_csum) of f(0..n) by one wave; sc: this wave's LDS scratch
-// (>= ceil(n/64) doubles).  Result broadcast to all lanes.
-template <class F>
-__device__ __forceinline__ double wave_csum(F f, int n, double* sc) {
-    const int lane = threadIdx.x & 63;
-    if (n <= 0) return 0.0;
-    if (n == 1) return f(0);  // ora_csum returns a single term untouched
-    int m = (n + 63) >> 6;
-    double v = 0;
-    for (int c = 0; c < m; c++) {
-        v = (c * 64 + lane < n) ? f(c * 64 + lane) : 0.0;
-        v = wave_tree(v);
-        if (m > 1 && lane == 0) sc[c] = v;
-    }
-    while (m > 1) {
-        __builtin_amdgcn_s_waitcnt(0);
-        __builtin_amdgcn_wave_barrier();
-        const int m2 = (m + 63) >> 6;
-        for (int c = 0; c < m2; c++) {
-            double u = (c * 64 + lane < m) ? sc[c * 64 + lane] : 0.0;
-            u = wave_tree(u);
-            __builtin_amdgcn_s_waitcnt(0);
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) sc[c] = u;
-            v = u;
-        }
-        m = m2;
-    }
-    return __shfl(v, 0, 64);
-}
-
-// ---- exact thread-local emulation of the canonical 64-tree ------------------------
-// tree64_local(get, cnt): a[i] = i < cnt ? get(i) : 0 (i < 64), then a[i] += a[i+off]
-// for off = 32..1 -- the same pairing as wave_tree, evaluated in one thread.
-template <class G>
-__device__ __forceinline__ double tree64_local(G get, int cnt) {
-    double a[32];
-#pragma unroll
-    for (int i = 0; i < 32; i++) a[i] = (i < cnt ? get(i) : 0.0) + (i + 32 < cnt ? get(i + 32) : 0.0);
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1)
-#pragma unroll
-        for (int i = 0; i < off; i++) a[i] = a[i] + a[i + off];
-    return a[0];
-}
-
-// Canonical total (ora_csum) of arr[0..m) by ONE thread, in place (arr is private to it).
-__device__ __forceinline__ double local_csum_inplace(double* arr, int m) {
-    if (m <= 0) return 0.0;
-    while (m > 1) {
-        const int m2 = (m + 63) >> 6;
-        for (int c = 0; c < m2; c++) {
-            const int cnt = min(64, m - c * 64);
-            const double t = tree64_local([&](int i) { return arr[c * 64 + i]; }, cnt);
-            arr[c] = t;
-        }
-        m = m2;
-    }
-    return arr[0];
-}
 
 // K canonical 64-trees at once: lane holds v[0..K); lane q < K receives the tree of entry q.
 // Transpose through this wave's LDS buffer (K x 65 doubles), then per-lane register trees.
@@ -1282,101 +1105,6 @@ __device__ __forceinline__ double pose_rho0(const PoseEdgeD& e, double c, bool r
     return (2 * sq) * e.delta - e.dsqr;
 }
 
-// Eigen::LDLT<MatrixXd> compute + solve (diagonal pivoting, sequential dot products),
-// identical operation sequence to oracle ora_ldlt_pivot_solve, fully unrolled so the 6x6
-// stays in registers: the data-dependent pivot swaps are unrolled conditional swaps.
-__device__ __forceinline__ bool ldlt_pivot6(double* M, const double* b, double* x) {
-    constexpr int n = 6;
-    int tr[n];
-    double tmp[n];
-    int sign = 0;
-    bool stop = false;
-#pragma unroll
-    for (int k = 0; k < n; k++) {
-        if (!stop) {
-            int idx = k;
-            double big = fabs(M[k * n + k]);
-#pragma unroll
-            for (int i = k + 1; i < n; i++) {
-                const double d = fabs(M[i * n + i]);
-                if (d > big) {
-                    big = d;
-                    idx = i;
-                }
-            }
-            tr[k] = idx;
-#pragma unroll
-            for (int i = k + 1; i < n; i++)
-                if (idx == i) {
-#pragma unroll
-                    for (int j = 0; j < k; j++) { const double t = M[k * n + j]; M[k * n + j] = M[i * n + j]; M[i * n + j] = t; }
-#pragma unroll
-                    for (int r = i + 1; r < n; r++) { const double t = M[r * n + k]; M[r * n + k] = M[r * n + i]; M[r * n + i] = t; }
-                    { const double t = M[k * n + k]; M[k * n + k] = M[i * n + i]; M[i * n + i] = t; }
-#pragma unroll
-                    for (int r = k + 1; r < i; r++) { const double t = M[r * n + k]; M[r * n + k] = M[i * n + r]; M[i * n + r] = t; }
-                }
-            if (k > 0) {
-#pragma unroll
-                for (int j = 0; j < k; j++) tmp[j] = M[j * n + j] * M[k * n + j];
-                double s = 0;
-#pragma unroll
-                for (int j = 0; j < k; j++) s += M[k * n + j] * tmp[j];
-                M[k * n + k] -= s;
-#pragma unroll
-                for (int i = k + 1; i < n; i++) {
-                    double t = 0;
-#pragma unroll
-                    for (int j = 0; j < k; j++) t += M[i * n + j] * tmp[j];
-                    M[i * n + k] -= t;
-                }
-            }
-            const double akk = M[k * n + k];
-            const bool valid = fabs(akk) > 0.0;
-            if (k == 0 && !valid) {
-#pragma unroll
-                for (int j = 0; j < n; j++) tr[j] = j;
-                sign = 0;
-                stop = true;
-            } else {
-                if (valid) {
-#pragma unroll
-                    for (int i = k + 1; i < n; i++) M[i * n + k] /= akk;
-                }
-                if (sign == 1) { if (akk < 0) sign = 3; }
-                else if (sign == 2) { if (akk > 0) sign = 3; }
-                else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
-            }
-        }
-    }
-    if (!(sign == 1 || sign == 0)) return false;
-    double y[n];
-#pragma unroll
-    for (int i = 0; i < n; i++) y[i] = b[i];
-#pragma unroll
-    for (int k = 0; k < n; k++)
-#pragma unroll
-        for (int i = k + 1; i < n; i++)
-            if (tr[k] == i) { const double t = y[k]; y[k] = y[i]; y[i] = t; }
-#pragma unroll
-    for (int i = 0; i < n; i++)
-#pragma unroll
-        for (int j = 0; j < i; j++) y[i] -= M[i * n + j] * y[j];
-#pragma unroll
-    for (int i = 0; i < n; i++) y[i] = fabs(M[i * n + i]) > DBL_MIN ? y[i] / M[i * n + i] : 0.0;
-#pragma unroll
-    for (int i = n - 1; i >= 0; i--)
-#pragma unroll
-        for (int j = n - 1; j > i; j--) y[i] -= M[j * n + i] * y[j];
-#pragma unroll
-    for (int k = n - 1; k >= 0; k--)
-#pragma unroll
-        for (int i = k + 1; i < n; i++)
-            if (tr[k] == i) { const double t = y[k]; y[k] = y[i]; y[i] = t; }
-#pragma unroll
-    for (int i = 0; i < n; i++) x[i] = y[i];
-    return true;
-}
 
 constexpr int kPoseMaxEdges = 8192;
 constexpr int kPoseThreads = 512;   // 256 VGPRs per lane for the fused 28-term pass

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "ba.hpp"
+#include "sim3opt.hpp"
 #include "orb_extract.hpp"
 #include "orb_match.hpp"
 
@@ -157,6 +158,28 @@ int Optimizer_PoseOptimization_frames_device(int count, const pose_frame* F, flo
     const int r = e->run_frames_device(count, F, Tcw_out, outlier, ninliers);
     if (r == -3) return ORB_E_CAPACITY;
     return r ? ORB_E_HIP : ORB_OK;
+}
+
+int Optimizer_OptimizeSim3_batch(int count, const sim3opt_problem* P, double* S12, uint8_t* const* erased,
+                                 int* nIn) {
+    if (count < 0 || (count > 0 && (!P || !S12 || !erased || !nIn))) return ORB_E_INVALID;
+    for (int f = 0; f < count; f++) {
+        const sim3opt_problem& Q = P[f];
+        if (Q.N < 0 || (Q.N > 0 && (!erased[f] || !Q.valid || !Q.X1c || !Q.X2c || !Q.obs1 || !Q.obs2 ||
+                                    !Q.inv_sigma2_1 || !Q.inv_sigma2_2)))
+            return ORB_E_INVALID;
+        if (!(Q.th2 >= 0.f)) return ORB_E_INVALID;
+    }
+    if (count == 0) return ORB_OK;
+    const int r = orbgpu::sim3opt_run(count, P, S12, erased, nIn);
+    if (r == -3) return ORB_E_CAPACITY;
+    if (r == -4) return ORB_E_NODEVICE;
+    return r ? ORB_E_HIP : ORB_OK;
+}
+
+int Optimizer_OptimizeSim3(const sim3opt_problem* P, double* S12, uint8_t* erased, int* nIn) {
+    uint8_t* e[1] = {erased};
+    return Optimizer_OptimizeSim3_batch(1, P, S12, e, nIn);
 }
 
 int Optimizer_PoseOptimization(const pose_problem* P, float* Tcw_out, uint8_t* outlier, int* ninliers) {

@@ -55,5 +55,42 @@ __device__ __forceinline__ double atan2_d(double y, double x) {
     return y < 0 ? -a : a;
 }
 
+// fdlibm __ieee754_exp as an IEEE operation sequence (oracle/ba.c ora_det_exp): g2o::Sim3's
+// exp(sigma) (sim3.h:84) in OptimizeSim3's numeric Jacobian and update.
+__device__ __forceinline__ double exp_d(double x) {
+    const double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10;
+    const double invln2 = 1.44269504088896338700e+00;
+    const double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+                 P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+                 P5 = 4.13813679705723846039e-08;
+    if (x != x) return x;
+    if (x > 7.09782712893383973096e+02) return HUGE_VAL;
+    if (x < -7.45133219101941108420e+02) return 0.0;
+    const int xsb = x < 0;
+    const double ax = fabs(x);
+    double hi = 0, lo = 0;
+    int k = 0;
+    if (ax > 0.5 * 6.93147180559945286227e-01) {
+        if (ax < 1.5 * 6.93147180559945286227e-01) {
+            hi = x - (xsb ? -ln2HI : ln2HI);
+            lo = xsb ? -ln2LO : ln2LO;
+            k = 1 - xsb - xsb;
+        } else {
+            k = (int)(invln2 * x + (xsb ? -0.5 : 0.5));
+            const double t = k;
+            hi = x - t * ln2HI;
+            lo = t * ln2LO;
+        }
+        x = hi - lo;
+    } else if (ax < 3.7252902984e-09) {
+        return 1.0 + x;
+    }
+    const double t = x * x;
+    const double c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
+    const double y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
+    return ldexp(y, k);
+}
+
 }  // namespace detmath
 }  // namespace orbgpu

@@ -18,7 +18,7 @@ import threading
 
 import numpy as np
 
-from ._lib import ba_problem, ba_result, check, lib, pose_problem, ptr
+from ._lib import ba_problem, ba_result, check, lib, pose_problem, ptr, sim3opt_problem
 
 _FIELDS = (("kf_id", np.int32), ("kf_Tcw", np.float32), ("kf_local", np.uint8), ("kf_cam", np.float32),
            ("pt_id", np.int32), ("pt_pos", np.float32), ("edge_pt", np.int32), ("edge_kf", np.int32),
@@ -94,6 +94,55 @@ def last_timings():
     ms = np.zeros(2)
     check(lib().Optimizer_last_timings(ptr(ms)))
     return ms
+
+
+# ------------------------------------------------------------------ OptimizeSim3
+_SIM3OPT = (("valid", np.uint8), ("X1c", np.float32), ("X2c", np.float32), ("obs1", np.float32),
+            ("obs2", np.float32), ("inv_sigma2_1", np.float32), ("inv_sigma2_2", np.float32))
+
+
+def _sim3opt_struct(pr, keep):
+    a = {k: np.ascontiguousarray(pr[k], dt) for k, dt in _SIM3OPT}
+    keep.append(a)
+    N = len(a["valid"])
+    if (a["X1c"].shape != (N, 3) or a["X2c"].shape != (N, 3) or a["obs1"].shape != (N, 2)
+            or a["obs2"].shape != (N, 2) or a["inv_sigma2_1"].shape != (N,) or a["inv_sigma2_2"].shape != (N,)):
+        raise ValueError("OptimizeSim3: inconsistent correspondence arrays")
+    P = sim3opt_problem()
+    P.N = N
+    for k, _ in _SIM3OPT:
+        setattr(P, k, ptr(a[k]))
+    P.K1 = (C.c_float * 4)(*[float(v) for v in pr["K1"]])
+    P.K2 = (C.c_float * 4)(*[float(v) for v in pr["K2"]])
+    P.th2 = float(pr.get("th2", 10.0))
+    P.bFixScale = int(bool(pr["bFixScale"]))
+    return P
+
+
+def OptimizeSim3(problem, S12):
+    """Optimizer::OptimizeSim3(pKF1, pKF2, vpMatches1, g2oS12, th2, bFixScale) (Optimizer.cc:1046-1241).
+
+    problem: dict with valid (N), X1c / X2c (N x 3 camera-frame points), obs1 / obs2 (N x 2 undistorted
+    keypoints), inv_sigma2_1 / inv_sigma2_2 (N), K1 / K2 (fx fy cx cy), th2, bFixScale.
+    S12: g2o::Sim3 as 8 doubles (quaternion x y z w, t, s).
+    -> (nIn, S12 out, erased mask: vpMatches1[i] set to NULL)."""
+    n, S, e = OptimizeSim3Batch([problem], [S12])
+    return int(n[0]), S[0], e[0]
+
+
+def OptimizeSim3Batch(problems, S12s):
+    """One launch for many loop candidates (one workgroup each) -> (nIn[C], S12[C, 8], [erased_c])."""
+    keep = []
+    F = len(problems)
+    probs = (sim3opt_problem * max(F, 1))(*[_sim3opt_struct(p, keep) for p in problems])
+    S = np.zeros((max(F, 1), 8), np.float64)
+    for i, s in enumerate(S12s):
+        S[i] = np.asarray(s, np.float64).reshape(8)
+    er = [np.zeros(max(len(k["valid"]), 1), np.uint8) for k in keep]
+    eptr = (C.c_void_p * max(F, 1))(*[e.ctypes.data for e in er])
+    n = np.zeros(max(F, 1), np.int32)
+    check(lib().Optimizer_OptimizeSim3_batch(F, probs, ptr(S), eptr, ptr(n)), "Optimizer_OptimizeSim3")
+    return n[:F], S[:F], [e[:len(k["valid"])].astype(bool) for e, k in zip(er, keep)]
 
 
 # ------------------------------------------------------------------ PoseOptimization

@@ -501,6 +501,38 @@ int Optimizer_BundleAdjustment(const ba_problem* P, int nIterations, int bRobust
                                ba_result* R);
 
 /* ======================================================================
+ * Sim3 refinement of a loop candidate  (reference Optimizer::OptimizeSim3,
+ * src/Optimizer.cc:1046-1241; include/Optimizer.h:56-57; called from
+ * LoopClosing::ComputeSim3, LoopClosing.cc:326)
+ * One VertexSim3Expmap (numeric Jacobians of EdgeSim3ProjectXYZ and
+ * EdgeInverseSim3ProjectXYZ), fixed point vertices, Huber sqrt(th2),
+ * optimize(5), chi2 > th2 gating, optimize(10 | 5) on the inliers.
+ * ====================================================================== */
+typedef struct sim3opt_problem {
+    int N;                       /* vpMatches1.size() (= pKF1->N) */
+    const uint8_t* valid;        /* N: vpMatches1[i] && pMP1 && !pMP1->isBad() && !pMP2->isBad() && i2 >= 0 */
+    const float* X1c;            /* N x 3: R1w*P3D1w + t1w (CV_32F, as Optimizer.cc:1118) */
+    const float* X2c;            /* N x 3: R2w*P3D2w + t2w */
+    const float* obs1;           /* N x 2: pKF1->mvKeysUn[i].pt */
+    const float* obs2;           /* N x 2: pKF2->mvKeysUn[i2].pt */
+    const float* inv_sigma2_1;   /* N: pKF1->mvInvLevelSigma2[kpUn1.octave] */
+    const float* inv_sigma2_2;   /* N: pKF2->mvInvLevelSigma2[kpUn2.octave] */
+    float K1[4], K2[4];          /* fx fy cx cy of pKF1->mK / pKF2->mK */
+    float th2;                   /* chi2 threshold (LoopClosing passes 10) */
+    int bFixScale;
+} sim3opt_problem;
+
+/* static int Optimizer::OptimizeSim3(pKF1, pKF2, vpMatches1, g2oS12, th2, bFixScale).
+ * S12: g2o::Sim3 as 8 doubles (quaternion x y z w = Eigen coeffs(), t, s), in/out; left
+ * unchanged on the reference's early return (fewer than 10 inliers after gating).
+ * erased: N bytes out, 1 where the reference sets vpMatches1[i] = NULL.
+ * *nIn = the return value.  At most 2048 valid correspondences (ORB_E_CAPACITY). */
+int Optimizer_OptimizeSim3(const sim3opt_problem* P, double* S12, uint8_t* erased, int* nIn);
+/* `count` candidates in one launch (one workgroup each): S12 count x 8, erased[c] N_c bytes. */
+int Optimizer_OptimizeSim3_batch(int count, const sim3opt_problem* P, double* S12, uint8_t* const* erased,
+                                 int* nIn);
+
+/* ======================================================================
  * Motion-only pose optimisation  (reference Optimizer::PoseOptimization,
  * src/Optimizer.cc:239-451; include/Optimizer.h:48)
  * One SE3 vertex, one unary edge per keypoint with a map point

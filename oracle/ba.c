@@ -1289,3 +1289,408 @@ int ora_pose_optimization(const ora_pose_problem* P, float* Tcw_out, uint8_t* ou
     free(E);
     return nInitial - nBad;
 }
+
+/* ======================================================================
+ * Optimizer::OptimizeSim3 (reference src/Optimizer.cc:1046-1241).
+ * One VertexSim3Expmap (types_seven_dof_expmap.h:48-94: oplus = Sim3(update)*estimate,
+ * update[6] zeroed IN PLACE when _fix_scale -- it is the solver's _x), fixed point
+ * vertices, EdgeSim3ProjectXYZ / EdgeInverseSim3ProjectXYZ (130-171) with the default
+ * numeric Jacobian of BaseBinaryEdge::linearizeOplus (base_binary_edge.hpp:131-204:
+ * delta 1e-9, central difference, push/oplus/computeError/pop per column), Huber
+ * sqrt(th2) on both edges, BlockSolverX + LinearSolverDense (pivoted LDL^T of the 7x7
+ * block), optimize(5), chi2 gating, optimize(10 | 5) on the inliers.
+ * g2o::Sim3 (sim3.h): ctor from update 64-146, map 148-150, inverse 235-238,
+ * operator* 264-270.  exp uses ora_det_exp / ora_det_sincos; 3x3 products and norms
+ * sum their terms left to right; the canonical sums of the LM are those of the pose
+ * optimisation above.
+ * ====================================================================== */
+
+/* fdlibm __ieee754_exp, as IEEE operation sequence (deterministic on CPU and GPU) */
+double ora_det_exp(double x)
+{
+    const double halF[2] = {0.5, -0.5};
+    const double ln2HI[2] = {6.93147180369123816490e-01, -6.93147180369123816490e-01};
+    const double ln2LO[2] = {1.90821492927058770002e-10, -1.90821492927058770002e-10};
+    const double invln2 = 1.44269504088896338700e+00;
+    const double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+                 P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+                 P5 = 4.13813679705723846039e-08;
+    if (x != x) return x;
+    if (x > 7.09782712893383973096e+02) return HUGE_VAL;
+    if (x < -7.45133219101941108420e+02) return 0.0;
+    const int xsb = x < 0;
+    const double ax = fabs(x);
+    double hi = 0, lo = 0;
+    int k = 0;
+    if (ax > 0.5 * 6.93147180559945286227e-01) {
+        if (ax < 1.5 * 6.93147180559945286227e-01) {
+            hi = x - ln2HI[xsb];
+            lo = ln2LO[xsb];
+            k = 1 - xsb - xsb;
+        } else {
+            k = (int)(invln2 * x + halF[xsb]);
+            const double t = k;
+            hi = x - t * ln2HI[0];
+            lo = t * ln2LO[0];
+        }
+        x = hi - lo;
+    } else if (ax < 3.7252902984e-09) { /* 2^-28 */
+        return 1.0 + x;
+    }
+    const double t = x * x;
+    const double c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
+    const double y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
+    return ldexp(y, k);
+}
+
+typedef struct { double q[4]; double t[3]; double s; } sim3q;
+
+static void sim3_exp(const double* upd, sim3q* o) /* Sim3(const Vector7d&) sim3.h:64-146 */
+{
+    const double w[3] = {upd[0], upd[1], upd[2]};
+    const double u[3] = {upd[3], upd[4], upd[5]};
+    const double sigma = upd[6];
+    const double theta = sqrt((w[0] * w[0] + w[1] * w[1]) + w[2] * w[2]);
+    const double Om[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+    double Om2[9], R[9], W[9];
+    mat3_mul(Om, Om, Om2);
+    const double s = ora_det_exp(sigma);
+    const double eps = 0.00001;
+    double A, B, C;
+    if (fabs(sigma) < eps) {
+        C = 1;
+        if (theta < eps) {
+            A = 1. / 2.;
+            B = 1. / 6.;
+            for (int i = 0; i < 9; i++) R[i] = (((i % 4) == 0 ? 1.0 : 0.0) + Om[i]) + Om2[i];
+        } else {
+            double sn, cs;
+            ora_det_sincos(theta, &sn, &cs);
+            const double theta2 = theta * theta;
+            A = (1 - cs) / theta2;
+            B = (theta - sn) / (theta2 * theta);
+            const double a = sn / theta, b = (1 - cs) / (theta * theta);
+            for (int i = 0; i < 9; i++) R[i] = (((i % 4) == 0 ? 1.0 : 0.0) + a * Om[i]) + b * Om2[i];
+        }
+    } else {
+        C = (s - 1) / sigma;
+        if (theta < eps) {
+            const double sigma2 = sigma * sigma;
+            A = ((sigma - 1) * s + 1) / sigma2;
+            B = ((0.5 * sigma2 - sigma + 1) * s) / (sigma2 * sigma);
+            for (int i = 0; i < 9; i++) R[i] = (((i % 4) == 0 ? 1.0 : 0.0) + Om[i]) + Om2[i];
+        } else {
+            double sn, cs;
+            ora_det_sincos(theta, &sn, &cs);
+            const double ra = sn / theta, rb = (1 - cs) / (theta * theta);
+            for (int i = 0; i < 9; i++) R[i] = (((i % 4) == 0 ? 1.0 : 0.0) + ra * Om[i]) + rb * Om2[i];
+            const double a = s * sn, b = s * cs;
+            const double theta2 = theta * theta, sigma2 = sigma * sigma;
+            const double c = theta2 + sigma2;
+            A = (a * sigma + (1 - b) * theta) / (theta * c);
+            B = (C - ((b - 1) * sigma + a * theta) / c) * 1. / theta2;
+        }
+    }
+    quat_from_R(R, o->q);
+    for (int i = 0; i < 9; i++) W[i] = (A * Om[i] + B * Om2[i]) + C * ((i % 4) == 0 ? 1.0 : 0.0);
+    for (int i = 0; i < 3; i++) o->t[i] = (W[i * 3] * u[0] + W[i * 3 + 1] * u[1]) + W[i * 3 + 2] * u[2];
+    o->s = s;
+}
+
+static void sim3_mul(const sim3q* a, const sim3q* b, sim3q* o) /* operator* sim3.h:264-270 */
+{
+    sim3q r;
+    double rt[3];
+    quat_mul(a->q, b->q, r.q);
+    quat_rotate(a->q, b->t, rt);
+    for (int i = 0; i < 3; i++) r.t[i] = a->s * rt[i] + a->t[i];
+    r.s = a->s * b->s;
+    *o = r;
+}
+
+static void sim3_map(const sim3q* T, const double* X, double* out) /* map sim3.h:148-150 */
+{
+    double r[3];
+    quat_rotate(T->q, X, r);
+    for (int i = 0; i < 3; i++) out[i] = T->s * r[i] + T->t[i];
+}
+
+static void sim3_inverse(const sim3q* T, sim3q* o) /* inverse sim3.h:235-238 */
+{
+    sim3q r;
+    r.q[0] = -T->q[0]; r.q[1] = -T->q[1]; r.q[2] = -T->q[2]; r.q[3] = T->q[3];
+    const double ms = -1. / T->s;
+    const double v[3] = {ms * T->t[0], ms * T->t[1], ms * T->t[2]};
+    quat_rotate(r.q, v, r.t);
+    r.s = 1. / T->s;
+    *o = r;
+}
+
+/* g2o::Sim3(Converter::toMatrix3d(R), toVector3d(t), s) (LoopClosing.cc:317) */
+void ora_sim3_from_Rts(const float* R, const float* t, float s, double* S12)
+{
+    double Rd[9];
+    for (int i = 0; i < 9; i++) Rd[i] = (double)R[i];
+    quat_from_R(Rd, S12);
+    for (int i = 0; i < 3; i++) S12[4 + i] = (double)t[i];
+    S12[7] = (double)s;
+}
+
+typedef struct {
+    double X[3], obs[2], info, err[2];
+    int inv;        /* 0: EdgeSim3ProjectXYZ (X = point 2, camera 1), 1: inverse edge */
+    int level;      /* 0 active, 1 removed */
+} s3_edge;
+
+typedef struct { double f1[2], p1[2], f2[2], p2[2]; } s3_cam;
+
+/* computeError with the Sim3 estimate T and its inverse Ti */
+static void s3_error(const s3_edge* e, const sim3q* T, const sim3q* Ti, const s3_cam* K, double* err)
+{
+    double p[3];
+    if (!e->inv) {
+        sim3_map(T, e->X, p);
+        const double px = p[0] / p[2], py = p[1] / p[2];
+        err[0] = e->obs[0] - (px * K->f1[0] + K->p1[0]);
+        err[1] = e->obs[1] - (py * K->f1[1] + K->p1[1]);
+    } else {
+        sim3_map(Ti, e->X, p);
+        const double px = p[0] / p[2], py = p[1] / p[2];
+        err[0] = e->obs[0] - (px * K->f2[0] + K->p2[0]);
+        err[1] = e->obs[1] - (py * K->f2[1] + K->p2[1]);
+    }
+}
+
+static double s3_chi2(const double* err, double info) { return err[0] * (info * err[0]) + err[1] * (info * err[1]); }
+
+static double s3_rho0(double c, double delta, double dsqr)
+{
+    if (c <= dsqr) return c;
+    const double sq = sqrt(c);
+    return (2 * sq) * delta - dsqr;
+}
+
+static const int DIAG28[7] = {0, 7, 13, 18, 22, 25, 27};
+
+/* the 14 perturbed estimates of linearizeOplus: Sim3(+-delta e_d) * T and their inverses */
+static void s3_perturbed(const sim3q* T, int fixScale, sim3q* Tp, sim3q* Tpi)
+{
+    const double delta = 1e-9;
+    for (int d = 0; d < 7; d++)
+        for (int sgn = 0; sgn < 2; sgn++) {
+            double add[7] = {0, 0, 0, 0, 0, 0, 0};
+            add[d] = sgn ? -delta : delta;
+            if (fixScale) add[6] = 0;
+            sim3q U;
+            sim3_exp(add, &U);
+            sim3_mul(&U, T, &Tp[2 * d + sgn]);
+            sim3_inverse(&Tp[2 * d + sgn], &Tpi[2 * d + sgn]);
+        }
+}
+
+/* one OptimizationAlgorithmLevenberg::solve on the Sim3 vertex */
+static int s3_lm_solve(s3_edge* E, int ne, sim3q* T, const s3_cam* K, int fixScale, double delta, int iteration,
+                       double* lambda, double* ni, int* nBadLM, double* scratch, double* xs, ora_ba_trace* tr)
+{
+    const double dsqr = delta * delta;
+    double* v = scratch;
+    sim3q Ti;
+    sim3_inverse(T, &Ti);
+    int nA = 0;
+    for (int i = 0; i < ne; i++)
+        if (E[i].level == 0) {
+            s3_error(&E[i], T, &Ti, K, E[i].err);
+            v[nA++] = s3_rho0(s3_chi2(E[i].err, E[i].info), delta, dsqr);
+        }
+    double currentChi = ora_csum(v, nA);
+    const double iniChi = currentChi;
+    double H[28], bvec[7];
+    {
+        sim3q Tp[14], Tpi[14];
+        s3_perturbed(T, fixScale, Tp, Tpi);
+        const double scalar = 1.0 / (2 * 1e-9);
+        double* terms = scratch + ne + 64; /* 35 x nA */
+        int a = 0;
+        for (int i = 0; i < ne; i++) {
+            s3_edge* e = &E[i];
+            if (e->level != 0) continue;
+            double J[14]; /* 2 x 7 row-major */
+            for (int d = 0; d < 7; d++) {
+                double ep[2], em[2];
+                s3_error(e, &Tp[2 * d], &Tpi[2 * d], K, ep);
+                s3_error(e, &Tp[2 * d + 1], &Tpi[2 * d + 1], K, em);
+                J[d] = scalar * (ep[0] - em[0]);
+                J[7 + d] = scalar * (ep[1] - em[1]);
+            }
+            const double c = s3_chi2(e->err, e->info);
+            double r1 = 1.;
+            if (!(c <= dsqr)) r1 = delta / sqrt(c);
+            const double w = r1 * e->info;
+            double omr[2];
+            for (int k = 0; k < 2; k++) omr[k] = -(e->info * e->err[k]) * r1;
+            int q = 0;
+            for (int r = 0; r < 7; r++) {
+                terms[(28 + r) * nA + a] = J[r] * omr[0] + J[7 + r] * omr[1];
+                for (int cc = r; cc < 7; cc++) {
+                    terms[q * nA + a] = (J[r] * w) * J[cc] + (J[7 + r] * w) * J[7 + cc];
+                    q++;
+                }
+            }
+            a++;
+        }
+        for (int q = 0; q < 35; q++) {
+            for (int j = 0; j < nA; j++) v[j] = terms[q * nA + j];
+            const double s = ora_csum(v, nA);
+            if (q < 28) H[q] = s; else bvec[q - 28] = s;
+        }
+    }
+    if (iteration == 0) {
+        double m = 0.;
+        for (int j = 0; j < 7; j++) m = fmax(fabs(H[DIAG28[j]]), m);
+        *lambda = 1e-5 * m;
+        *ni = 2;
+        *nBadLM = 0;
+    }
+    double rho = 0;
+    int qmax = 0;
+    do {
+        const sim3q Tbak = *T;
+        double Hd[49], x[7];
+        for (int r = 0, q = 0; r < 7; r++)
+            for (int cc = r; cc < 7; cc++, q++) {
+                double h = H[q];
+                if (cc == r) h += *lambda;
+                Hd[r * 7 + cc] = h;
+                Hd[cc * 7 + r] = h;
+            }
+        const int ok2 = ora_ldlt_pivot_solve(Hd, 7, bvec, x);
+        if (ok2) memcpy(xs, x, sizeof(x));
+        if (fixScale) xs[6] = 0; /* oplusImpl writes through the Map of the solver's _x */
+        {
+            sim3q U, r;
+            sim3_exp(xs, &U);
+            sim3_mul(&U, T, &r);
+            *T = r;
+        }
+        sim3_inverse(T, &Ti);
+        int nB = 0;
+        for (int i = 0; i < ne; i++)
+            if (E[i].level == 0) {
+                s3_error(&E[i], T, &Ti, K, E[i].err);
+                v[nB++] = s3_rho0(s3_chi2(E[i].err, E[i].info), delta, dsqr);
+            }
+        double tempChi = ora_csum(v, nB);
+        if (!ok2) tempChi = DBL_MAX;
+        rho = currentChi - tempChi;
+        for (int j = 0; j < 7; j++) v[j] = xs[j] * (*lambda * xs[j] + bvec[j]);
+        double scale = ora_csum(v, 7);
+        scale += 1e-3;
+        rho /= scale;
+        if (rho > 0 && isfinite(tempChi)) {
+            const double a3 = 2 * rho - 1;
+            double alpha = 1. - (a3 * a3) * a3;
+            alpha = fmin(alpha, 2. / 3.);
+            const double scaleFactor = fmax(1. / 3., alpha);
+            *lambda *= scaleFactor;
+            *ni = 2;
+            currentChi = tempChi;
+        } else {
+            *lambda *= *ni;
+            *ni *= 2;
+            *T = Tbak;
+        }
+        qmax++;
+        if (tr && tr->n_trials < ORA_BA_TRACE_MAX) {
+            tr->trial_chi2[tr->n_trials] = tempChi;
+            tr->trial_lambda[tr->n_trials] = *lambda;
+            tr->n_trials++;
+        }
+    } while (rho < 0 && qmax < 10);
+    if (tr && tr->n_solves < ORA_BA_TRACE_MAX) {
+        tr->solve_ini_chi2[tr->n_solves] = iniChi;
+        tr->solve_chi2[tr->n_solves] = currentChi;
+        tr->n_solves++;
+    }
+    if (qmax == 10 || rho == 0) return 1;
+    if ((iniChi - currentChi) * 1e3 < iniChi) (*nBadLM)++;
+    else *nBadLM = 0;
+    return *nBadLM >= 3;
+}
+
+static void s3_optimize(s3_edge* E, int ne, sim3q* T, const s3_cam* K, int fixScale, double delta, int its,
+                        double* scratch, ora_ba_trace* tr)
+{
+    double xs[7] = {0, 0, 0, 0, 0, 0, 0}; /* BlockSolver::_x after buildStructure */
+    double lambda = 0, ni = 2;
+    int nBadLM = 0;
+    int nAct = 0;
+    for (int i = 0; i < ne; i++) nAct += E[i].level == 0;
+    if (nAct == 0) return; /* no active edge: the Sim3 vertex is not in the index map (optimize returns -1) */
+    for (int k = 0; k < its; k++)
+        if (s3_lm_solve(E, ne, T, K, fixScale, delta, k, &lambda, &ni, &nBadLM, scratch, xs, tr)) break;
+}
+
+int ora_optimize_sim3(const ora_sim3opt_problem* P, double* S12, uint8_t* erased, ora_ba_trace* tr)
+{
+    const int N = P->N;
+    if (tr) memset(tr, 0, sizeof(*tr));
+    for (int i = 0; i < N; i++) erased[i] = 0;
+    s3_cam K;
+    K.f1[0] = P->K1[0]; K.f1[1] = P->K1[1]; K.p1[0] = P->K1[2]; K.p1[1] = P->K1[3];
+    K.f2[0] = P->K2[0]; K.f2[1] = P->K2[1]; K.p2[0] = P->K2[2]; K.p2[1] = P->K2[3];
+    s3_edge* E = (s3_edge*)calloc(2 * (size_t)N + 1, sizeof(s3_edge));
+    int* corr = (int*)malloc(sizeof(int) * ((size_t)N + 1));
+    int nc = 0;
+    for (int i = 0; i < N; i++) {
+        if (!P->valid[i]) continue;
+        s3_edge* e12 = &E[2 * nc];
+        s3_edge* e21 = &E[2 * nc + 1];
+        for (int j = 0; j < 3; j++) { e12->X[j] = (double)P->X2c[3 * i + j]; e21->X[j] = (double)P->X1c[3 * i + j]; }
+        e12->obs[0] = P->obs1[2 * i]; e12->obs[1] = P->obs1[2 * i + 1];
+        e21->obs[0] = P->obs2[2 * i]; e21->obs[1] = P->obs2[2 * i + 1];
+        e12->info = (double)P->inv_sigma2_1[i];
+        e21->info = (double)P->inv_sigma2_2[i];
+        e12->inv = 0; e21->inv = 1;
+        corr[nc++] = i;
+    }
+    const int ne = 2 * nc;
+    const float deltaHuberF = sqrtf(P->th2);
+    const double delta = (double)deltaHuberF;
+    const double th2 = (double)P->th2;
+    double* scratch = (double*)malloc(sizeof(double) * (36 * (size_t)ne + 192));
+    sim3q T;
+    memcpy(T.q, S12, 4 * sizeof(double));
+    memcpy(T.t, S12 + 4, 3 * sizeof(double));
+    T.s = S12[7];
+    s3_optimize(E, ne, &T, &K, P->bFixScale, delta, 5, scratch, tr);
+    int nBad = 0;
+    for (int c = 0; c < nc; c++) {
+        s3_edge* a = &E[2 * c];
+        s3_edge* b = &E[2 * c + 1];
+        if (s3_chi2(a->err, a->info) > th2 || s3_chi2(b->err, b->info) > th2) {
+            erased[corr[c]] = 1;
+            a->level = b->level = 1;
+            nBad++;
+        }
+    }
+    const int nMoreIterations = nBad > 0 ? 10 : 5;
+    int nIn = 0;
+    if (nc - nBad >= 10) {
+        s3_optimize(E, ne, &T, &K, P->bFixScale, delta, nMoreIterations, scratch, tr);
+        for (int c = 0; c < nc; c++) {
+            s3_edge* a = &E[2 * c];
+            s3_edge* b = &E[2 * c + 1];
+            if (a->level) continue;
+            if (s3_chi2(a->err, a->info) > th2 || s3_chi2(b->err, b->info) > th2) erased[corr[c]] = 1;
+            else nIn++;
+        }
+        memcpy(S12, T.q, 4 * sizeof(double));
+        memcpy(S12 + 4, T.t, 3 * sizeof(double));
+        S12[7] = T.s;
+    }
+    free(scratch);
+    free(corr);
+    free(E);
+    return nIn;
+}

@@ -315,6 +315,30 @@ int   ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_res
  * one optimize(nIterations), Huber sqrt(5.99)/sqrt(7.815) iff bRobust, no gating. */
 int   ora_global_ba(const ora_ba_problem* P, int nIterations, int bRobust, const volatile int* stop,
                     ora_ba_result* R, ora_ba_trace* trace);
+/* Optimizer::OptimizeSim3 (Optimizer.cc:1046-1241).  Per index i < N of vpMatches1:
+ * valid[i] (vpMatches1[i] && pMP1 && !isBad both && i2 >= 0), X1c/X2c = R1w*P3D1w+t1w /
+ * R2w*P3D2w+t2w (N x 3, CV_32F), obs1 = pKF1->mvKeysUn[i].pt, obs2 = pKF2->mvKeysUn[i2].pt
+ * (N x 2), inv_sigma2_1/2 = mvInvLevelSigma2[octave]; K = fx fy cx cy. */
+typedef struct {
+    int N;
+    const uint8_t* valid;
+    const float* X1c;
+    const float* X2c;
+    const float* obs1;
+    const float* obs2;
+    const float* inv_sigma2_1;
+    const float* inv_sigma2_2;
+    float K1[4], K2[4];
+    float th2;
+    int bFixScale;
+} ora_sim3opt_problem;
+/* S12 (8 doubles: quaternion x y z w, t, s) in/out (written only when the reference
+ * reaches its second optimize); erased[i] = 1 where vpMatches1[i] is set to NULL.
+ * Returns nIn (0 on the early return). */
+int   ora_optimize_sim3(const ora_sim3opt_problem* P, double* S12, uint8_t* erased, ora_ba_trace* trace);
+/* g2o::Sim3(Converter::toMatrix3d(R), toVector3d(t), s) */
+void  ora_sim3_from_Rts(const float* R, const float* t, float s, double* S12);
+double ora_det_exp(double x);
 
 #ifdef __cplusplus
 }

@@ -635,3 +635,60 @@ def oracle_search_by_sim3(KF1, mp1, KF2, mp2, pts, geo, bad, matches12, s12, R12
                              ptr(m12), float(s12), ptr(_f32(R12).reshape(9)), ptr(_f32(t12).reshape(3)),
                              float(logScaleFactor), float(th))
     return n, m12
+
+
+# ---------------------------------------------------------------- Optimizer::OptimizeSim3
+class ora_sim3opt_problem(C.Structure):
+    _fields_ = [("N", C.c_int), ("valid", C.c_void_p), ("X1c", C.c_void_p), ("X2c", C.c_void_p),
+                ("obs1", C.c_void_p), ("obs2", C.c_void_p), ("inv_sigma2_1", C.c_void_p),
+                ("inv_sigma2_2", C.c_void_p), ("K1", C.c_float * 4), ("K2", C.c_float * 4), ("th2", C.c_float),
+                ("bFixScale", C.c_int)]
+
+
+SIM3OPT_ARRAYS = (("valid", np.uint8), ("X1c", np.float32), ("X2c", np.float32), ("obs1", np.float32),
+                  ("obs2", np.float32), ("inv_sigma2_1", np.float32), ("inv_sigma2_2", np.float32))
+
+
+def sim3opt_struct(pr, cls=ora_sim3opt_problem):
+    """Fill a (layout-identical) problem struct; returns (struct, arrays kept alive)."""
+    keep = {k: np.ascontiguousarray(pr[k], t) for k, t in SIM3OPT_ARRAYS}
+    P = cls()
+    P.N = int(pr["N"])
+    for k, _ in SIM3OPT_ARRAYS:
+        setattr(P, k, ptr(keep[k]))
+    P.K1 = (C.c_float * 4)(*[float(x) for x in pr["K1"]])
+    P.K2 = (C.c_float * 4)(*[float(x) for x in pr["K2"]])
+    P.th2 = float(pr["th2"])
+    P.bFixScale = int(pr["bFixScale"])
+    return P, keep
+
+
+def oracle_sim3_from_Rts(R, t, s):
+    L = lib()
+    L.ora_sim3_from_Rts.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_void_p]
+    Rf, tf = np.ascontiguousarray(R, np.float32), np.ascontiguousarray(t, np.float32)
+    S = np.zeros(8, np.float64)
+    L.ora_sim3_from_Rts(ptr(Rf), ptr(tf), float(s), ptr(S))
+    return S
+
+
+def oracle_optimize_sim3(pr, S12):
+    """Optimizer::OptimizeSim3 restated on CPU -> (nIn, S12 out, erased mask, LM trace)."""
+    L = lib()
+    L.ora_optimize_sim3.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ora_optimize_sim3.restype = C.c_int
+    P, keep = sim3opt_struct(pr)
+    S = np.array(S12, np.float64).copy()
+    er = np.zeros(max(int(pr["N"]), 1), np.uint8)
+    tr = _BATrace()
+    n = L.ora_optimize_sim3(C.byref(P), ptr(S), ptr(er), C.byref(tr))
+    return n, S, er[:int(pr["N"])].astype(bool), dict(
+        solve_chi2=np.array(tr.solve_chi2[:tr.n_solves]), trial_chi2=np.array(tr.trial_chi2[:tr.n_trials]),
+        trial_lambda=np.array(tr.trial_lambda[:tr.n_trials]))
+
+
+def oracle_det_exp(x):
+    L = lib()
+    L.ora_det_exp.argtypes = [C.c_double]
+    L.ora_det_exp.restype = C.c_double
+    return L.ora_det_exp(float(x))

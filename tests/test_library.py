@@ -93,3 +93,26 @@ def test_ba_validates_without_device():
     kid[1] = 1
     if not orb.device_available():
         assert L.Optimizer_LocalBundleAdjustment(C.byref(P), None, C.byref(R)) == ORB_E_NODEVICE
+
+
+def test_optimize_sim3_validates_without_device():
+    from c_orb_slam_amd._lib import sim3opt_problem
+    L = lib()
+    N = 4
+    v = np.ones(N, np.uint8)
+    X = np.ones((N, 3), np.float32)
+    o = np.zeros((N, 2), np.float32)
+    s = np.ones(N, np.float32)
+    P = sim3opt_problem(N, ptr(v), ptr(X), ptr(X), ptr(o), ptr(o), ptr(s), ptr(s))
+    P.th2 = 10.0
+    S = np.array([0, 0, 0, 1, 0, 0, 0, 1], np.float64)
+    er = np.zeros(N, np.uint8)
+    n = C.c_int()
+    assert L.Optimizer_OptimizeSim3(None, ptr(S), ptr(er), C.byref(n)) == ORB_E_INVALID
+    P2 = sim3opt_problem(N, ptr(v), None, ptr(X), ptr(o), ptr(o), ptr(s), ptr(s))
+    assert L.Optimizer_OptimizeSim3(C.byref(P2), ptr(S), ptr(er), C.byref(n)) == ORB_E_INVALID
+    P.th2 = float("nan")
+    assert L.Optimizer_OptimizeSim3(C.byref(P), ptr(S), ptr(er), C.byref(n)) == ORB_E_INVALID
+    P.th2 = 10.0
+    if not orb.device_available():
+        assert L.Optimizer_OptimizeSim3(C.byref(P), ptr(S), ptr(er), C.byref(n)) == ORB_E_NODEVICE

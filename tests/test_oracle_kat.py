@@ -362,3 +362,49 @@ def test_oracle_projection_searches_sanity():
                                                    s["bad"], s["m12"], s["s12"], s["R12"], s["t12"],
                                                    s["logScaleFactor"], 7.5)
     assert nfound == ((m12 >= 0) & (s["m12"] == -1)).sum() and nfound > 200
+
+
+def test_det_exp_close_to_libm():
+    """ora_det_exp (fdlibm __ieee754_exp restated) is within 1 ulp of libm over the ranges
+    g2o::Sim3 uses (sigma = log scale, +-1e-9 numeric steps) and far beyond."""
+    import math
+    xs = np.concatenate([[0.0, 1e-9, -1e-9, 1e-12, 0.3465, 0.3466, 1.0397, 1.0398, -0.3466, -1.0398, 700.0, -700.0],
+                         np.random.default_rng(0).uniform(-30, 30, 2000)])
+    for x in xs:
+        a, b = oracle_lib.oracle_det_exp(x), math.exp(x)
+        assert a == b or abs(a - b) <= abs(b) * 2.3e-16, (x, a, b)
+    assert oracle_lib.oracle_det_exp(0.0) == 1.0
+
+
+@pytest.mark.parametrize("fix", [True, False])
+def test_oracle_optimize_sim3_refines_similarity(fix):
+    """Optimizer::OptimizeSim3 restatement: the refined Sim3 is closer to the truth than the
+    RANSAC-shaped initial guess, the synthetic gross outliers are erased, scale fixed iff bFixScale."""
+    from scipy.spatial.transform import Rotation
+    from sim3opt_cases import sim3opt_problem
+    for seed in range(3):
+        pr = sim3opt_problem(seed=seed, fix_scale=fix)
+        S0 = oracle_lib.oracle_sim3_from_Rts(pr["R0"], pr["t0"], pr["s0"])
+        n, S, er, tr = oracle_lib.oracle_optimize_sim3(pr, S0)
+        valid = pr["valid"].astype(bool)
+        assert n >= 10 and n + er.sum() == valid.sum() and not er[~valid].any()
+        assert er[pr["gross"]].mean() > 0.8
+        Rq = Rotation.from_quat(S[:4] / np.linalg.norm(S[:4])).as_matrix()
+        e0 = np.linalg.norm(Rotation.from_matrix(pr["R0"].astype(np.float64) @ pr["R_true"].T).as_rotvec())
+        e1 = np.linalg.norm(Rotation.from_matrix(Rq @ pr["R_true"].T).as_rotvec())
+        assert e1 < 0.25 * e0
+        assert np.linalg.norm(S[4:7] - pr["t_true"]) < np.linalg.norm(pr["t0"] - pr["t_true"])
+        if fix:
+            assert S[7] == float(pr["s0"])
+        else:
+            assert abs(S[7] - pr["s_true"]) < abs(float(pr["s0"]) - pr["s_true"]) + 1e-3
+        assert np.all(np.diff(tr["solve_chi2"][:5]) <= 1e-9 * tr["solve_chi2"][0])
+
+
+def test_oracle_optimize_sim3_early_return():
+    """Fewer than 10 correspondences left after gating: return 0, g2oS12 untouched."""
+    from sim3opt_cases import sim3opt_problem
+    pr = sim3opt_problem(seed=4, N=40, match_frac=0.25)
+    S0 = oracle_lib.oracle_sim3_from_Rts(pr["R0"], pr["t0"], pr["s0"])
+    n, S, er, _ = oracle_lib.oracle_optimize_sim3(pr, S0)
+    assert pr["valid"].sum() < 10 and n == 0 and np.array_equal(S, S0)
