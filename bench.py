@@ -486,65 +486,110 @@ def ba_cpu_baseline(budget_s):
             "sample": f"{calls} LocalBundleAdjustment calls on config 4 ({its} LM solves), oracle/ba.c -O2, 1 thread"}
 
 
-def cpu_baseline(lefts, rights, Rs, budget_s):
-    """Oracle (line-faithful C restatement, 1 thread) on a bounded sample of the same workload:
+class _CpuStream:
+    """One reference-structured CPU tracking stream on the oracle (line-faithful C restatement):
     per stereo frame extract L and R, ComputeStereoMatches, SearchByProjection(Cur, Last, 7),
-    PoseOptimization."""
-    sys.path.insert(0, str(ROOT / "tests"))
-    import oracle_lib
-    from c_orb_slam_amd import synthetic
-    from c_orb_slam_amd.orb import Frame, MapPoints
-    eL = oracle_lib.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
-    eR = oracle_lib.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
-    scale = eL.tables()["scale"]
-    fx, fy, cx, cy = synthetic.intrinsics(W, H)
-    mbf = np.float32(synthetic.KITTI_BF)
-    mb = np.float32(mbf / np.float32(fx))
-    t0 = time.perf_counter()
-    done = 0
-    prev = None
-    extract_t = stereo_t = match_t = pose_t = 0.0
-    isig = eL.tables()["inv_sigma2"]
-    while True:
-        i = done % len(lefts)
+    PoseOptimization.  The oracle's C calls release the GIL, so streams run on separate cores."""
+
+    def __init__(self, lefts, rights, Rs):
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_lib
+        from c_orb_slam_amd import synthetic
+        self.ol = oracle_lib
+        self.lefts, self.rights, self.Rs = lefts, rights, Rs
+        self.eL = oracle_lib.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
+        self.eR = oracle_lib.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
+        self.scale = self.eL.tables()["scale"]
+        self.isig = self.eL.tables()["inv_sigma2"]
+        self.fx, self.fy, self.cx, self.cy = synthetic.intrinsics(W, H)
+        self.mbf = np.float32(synthetic.KITTI_BF)
+        self.mb = np.float32(self.mbf / np.float32(self.fx))
+        self.synthetic = synthetic
+        self.prev = None
+        self.t = {"extract": 0.0, "stereo": 0.0, "match": 0.0, "pose": 0.0}
+        self.done = 0
+
+    def frame(self, i):
+        from c_orb_slam_amd.orb import Frame, MapPoints
+        ol, fx, fy, cx, cy, mbf = self.ol, self.fx, self.fy, self.cx, self.cy, self.mbf
         ta = time.perf_counter()
-        kL, dL = eL(lefts[i])
-        kR, dR = eR(rights[i])
+        kL, dL = self.eL(self.lefts[i])
+        kR, dR = self.eR(self.rights[i])
         tb = time.perf_counter()
-        uR, dep, _ = oracle_lib.oracle_stereo_matches(eL, eR, kL, dL, kR, dR, H, mbf, mb)
+        uR, dep, _ = ol.oracle_stereo_matches(self.eL, self.eR, kL, dL, kR, dR, H, mbf, self.mb)
         tc = time.perf_counter()
-        extract_t += tb - ta
-        stereo_t += tc - tb
-        if prev is not None and i != 0:
-            pk, pd, pdep = prev
-            last = Frame(pk, pd, scale, np.eye(4, dtype=np.float32), fx, fy, cx, cy, mbf, W, H)
-            cur = Frame(kL, dL, scale, synthetic.pose_from_rotation(Rs[i - 1]), fx, fy, cx, cy, mbf, W, H, uRight=uR)
-            X, lm = oracle_lib.oracle_unproject_stereo(pk, pdep, np.eye(4, dtype=np.float32), fx, fy, cx, cy)
+        self.t["extract"] += tb - ta
+        self.t["stereo"] += tc - tb
+        if self.prev is not None and i != 0:
+            pk, pd, pdep = self.prev
+            last = Frame(pk, pd, self.scale, np.eye(4, dtype=np.float32), fx, fy, cx, cy, mbf, W, H)
+            cur = Frame(kL, dL, self.scale, self.synthetic.pose_from_rotation(self.Rs[i - 1]), fx, fy, cx, cy, mbf,
+                        W, H, uRight=uR)
+            X, lm = ol.oracle_unproject_stereo(pk, pdep, np.eye(4, dtype=np.float32), fx, fy, cx, cy)
             X = np.nan_to_num(X)
             mps = MapPoints(X, pd, np.ones(len(pk), np.int32))
             cm = np.full(cur.N, -1, np.int32)
             td = time.perf_counter()
-            oracle_lib.oracle_search_last(cur, cm, last, pk, lm, np.zeros(len(pk), np.uint8), mps, 7.0, False,
-                                          0.9, True)
+            ol.oracle_search_last(cur, cm, last, pk, lm, np.zeros(len(pk), np.uint8), mps, 7.0, False, 0.9, True)
             te = time.perf_counter()
-            match_t += te - td
+            self.t["match"] += te - td
             has = (cm >= 0).astype(np.uint8)
             pr = dict(Tcw=cur.Tcw, has_mp=has, Xw=X[np.maximum(cm, 0)],
                       obs=np.stack([kL["x"], kL["y"], uR], 1).astype(np.float32),
-                      inv_sigma2=isig[kL["octave"]].astype(np.float32), cam=(fx, fy, cx, cy, mbf))
-            oracle_lib.oracle_pose_optimization(pr)
-            pose_t += time.perf_counter() - te
-        prev = (kL, dL, dep)
-        done += 1
-        if time.perf_counter() - t0 > budget_s and done >= 4:
-            break
-    fps = done / (extract_t + stereo_t + match_t + pose_t)
-    return {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{done} KITTI-shaped stereo frames: oracle ORBextractor x2 + ComputeStereoMatches + "
-                      f"SearchByProjection(Cur,Last,7) + PoseOptimization (extract {extract_t / done * 1e3:.1f} ms/frame, stereo "
-                      f"{stereo_t / done * 1e3:.2f} ms, match {match_t / max(done - 1, 1) * 1e3:.2f} ms, "
-                      f"pose {pose_t / max(done - 1, 1) * 1e3:.2f} ms, "
-                      f"1 thread, -O2 C restatement)"}
+                      inv_sigma2=self.isig[kL["octave"]].astype(np.float32), cam=(fx, fy, cx, cy, mbf))
+            ol.oracle_pose_optimization(pr)
+            self.t["pose"] += time.perf_counter() - te
+        self.prev = (kL, dL, dep)
+        self.done += 1
+
+    def run(self, start, budget_s, min_frames):
+        t0 = time.perf_counter()
+        i = start
+        while True:
+            self.frame(i % len(self.lefts))
+            i += 1
+            if time.perf_counter() - t0 > budget_s and self.done >= min_frames:
+                return time.perf_counter() - t0
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(lefts, rights, Rs, budget_s):
+    """The oracle timed on the host cores on a bounded sample of the same workload:
+    (i) one reference-structured stream on 1 thread; (ii) P independent streams on P threads
+    (P = this box's CPU share, at most 16) -> whole-host frames/s, the figure `value` reports."""
+    from concurrent.futures import ThreadPoolExecutor
+    one = _CpuStream(lefts, rights, Rs)
+    one.run(0, budget_s / 2, 4)
+    fps1 = one.done / sum(one.t.values())
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    P = max(1, min(16, share))
+    streams = [_CpuStream(lefts, rights, Rs) for _ in range(P)]
+    with ThreadPoolExecutor(P) as ex:
+        walls = list(ex.map(lambda a: a[1].run(a[0] * 7, budget_s / 2, 2), enumerate(streams)))
+    framesP = sum(s.done for s in streams)
+    fpsP = framesP / max(walls)
+    t = one.t
+    return {"value": round(fpsP, 3), "unit": "frames/s", "cores": P, "kind": "port",
+            "sample": f"{P} independent reference-structured streams on {P} threads ({_cpu_model()}): oracle "
+                      f"ORBextractor x2 + ComputeStereoMatches + SearchByProjection(Cur,Last,7) + PoseOptimization "
+                      f"per stereo frame, -O2 C restatement; {framesP} frames in {max(walls):.1f} s",
+            "single_thread": {"value": round(fps1, 3), "unit": "frames/s", "cores": 1,
+                              "sample": f"{one.done} frames on 1 thread: extract {t['extract'] / one.done * 1e3:.1f} "
+                                        f"ms/frame, stereo {t['stereo'] / one.done * 1e3:.2f} ms, match "
+                                        f"{t['match'] / max(one.done - 1, 1) * 1e3:.2f} ms, pose "
+                                        f"{t['pose'] / max(one.done - 1, 1) * 1e3:.2f} ms"}}
 
 
 if __name__ == "__main__":
