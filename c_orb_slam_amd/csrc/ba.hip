@@ -1149,6 +1149,7 @@ __device__ __forceinline__ void pose_pass(F f, int nA, const int* aE, const Pose
 
 __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, const PoseEdgeDev* __restrict__ Eall,
                                                    double* errAll, uint8_t* outlAll) {
+    ORBGPU_LATENCY_WAVE();
     PoseProbDev& P = probs[blockIdx.x];
     const int ne = P.ne;
     const PoseEdgeDev* E = Eall + P.e0;
@@ -1414,6 +1415,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
 // Device mode edge creation (Optimizer.cc:268-347): rows with a map point, keypoint order,
 // compacted by a block scan; the initial pose from the frame's Tcw.  One workgroup per frame.
 __global__ void __launch_bounds__(kPoseThreads) k_pose_pack(PoseProbDev* probs, PoseEdgeDev* Eall) {
+    ORBGPU_LATENCY_WAVE();
     PoseProbDev& P = probs[blockIdx.x];
     const int N = P.N, tid = threadIdx.x;
     PoseEdgeDev* E = Eall + P.e0;

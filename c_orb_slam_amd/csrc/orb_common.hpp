@@ -123,6 +123,9 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
+// Issue priority of a latency-critical wave over co-resident bulk waves on its SIMD.
+#define ORBGPU_LATENCY_WAVE() __builtin_amdgcn_s_setprio(3)
+
 }  // namespace orbgpu
 
 // Section timers for instrumented builds (make prof -> -DORBGPU_PROF): clock64() deltas of

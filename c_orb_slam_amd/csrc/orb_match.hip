@@ -39,6 +39,7 @@ __device__ __forceinline__ float gemm_row(const float* T, int r, float X0, float
 
 // ---------------------------------------------------------------- grid build
 __global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs) {
+    ORBGPU_LATENCY_WAVE();
     __shared__ uint32_t s_key[kMaxFrameKeys];
     SearchDev& P = probs[blockIdx.x];
     const FrameDev& F = P.cur;
@@ -250,6 +251,7 @@ __device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked block
 // Parallel phase: one thread per query.
 template <bool LAST>
 __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict__ probs, float th, int bMono) {
+    ORBGPU_LATENCY_WAVE();
     const SearchDev P = probs[blockIdx.y];
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= P.nq) return;
@@ -286,6 +288,7 @@ __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict_
 template <bool LAST>
 __global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ probs, float th, int bMono,
                                                 float nnratio, int checkOri) {
+    ORBGPU_LATENCY_WAVE();
     __shared__ int s_owner[kMaxFrameKeys];    // earliest claiming query with Observations() > 0
     __shared__ int s_lastq[kMaxFrameKeys];    // latest claiming query (any)
     __shared__ uint8_t s_occ0[kMaxFrameKeys]; // occupancy before this call

@@ -39,6 +39,7 @@ __device__ __forceinline__ unsigned wave_min_u(unsigned v) {
 // yi in [floor(y - r), ceil(y + r)], r = 2 * mvScaleFactors[octave].  The order inside a row
 // does not matter: the match kernel takes the minimum of (dist, iR).
 __global__ void __launch_bounds__(1024) k_stereo_rows(const StereoDev* __restrict__ probs, StereoParams P) {
+    ORBGPU_LATENCY_WAVE();
     const StereoDev& S = probs[blockIdx.x];
     __shared__ int s_cnt[kStereoMaxRows];
     __shared__ int s_w[16];
@@ -92,6 +93,7 @@ __global__ void __launch_bounds__(1024) k_stereo_rows(const StereoDev* __restric
 }
 
 __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restrict__ probs, StereoParams P) {
+    ORBGPU_LATENCY_WAVE();
     const StereoDev& S = probs[blockIdx.y];
     const int lane = threadIdx.x & 63;
     const int iL = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -202,6 +204,7 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
 // median filter (Frame.cc:624-639): sort the kept SADs, thDist = 1.5f*1.4f*median,
 // invalidate SAD >= thDist (the reference walks the sorted tail from the end).
 __global__ void __launch_bounds__(1024) k_stereo_filter(const StereoDev* __restrict__ probs) {
+    ORBGPU_LATENCY_WAVE();
     const StereoDev& S = probs[blockIdx.x];
     __shared__ int v[kStereoMaxKeys];
     __shared__ int cnt, kept;
@@ -273,6 +276,7 @@ struct UnprojBatch {
 };
 
 __global__ void __launch_bounds__(256) k_unproject(UnprojBatch B) {
+    ORBGPU_LATENCY_WAVE();
     const UnprojDev& P = B.p[blockIdx.y];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.N) return;
