@@ -1116,9 +1116,30 @@ constexpr int kPosePer = kPoseMaxEdges / kPoseThreads;
 // cs[q][c]; thread q < K finishes entry q.
 template <int K, class F>
 __device__ __forceinline__ void pose_pass(F f, int nA, const int* aE, const PoseEdgeDev* E, double dM, double dS,
-                                          double (*cs)[kPoseMaxEdges / 64], double* res) {
+                                          double (*cs)[kPoseMaxEdges / 64], double* res, const PoseEdgeD& mine,
+                                          int mineIdx) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int m = (nA + 63) >> 6;
+    if (m <= nw) {
+        // one chunk per wave: active edge tid is this thread's for the whole round, kept in
+        // registers (loaded once per round) instead of re-read from HBM/L2 every pass
+        if (w < m) {
+            double v[K];
+            if ((int)threadIdx.x < nA) f(mine, mineIdx, v);
+            else
+#pragma unroll
+                for (int q = 0; q < K; q++) v[q] = 0.0;
+#pragma unroll
+            for (int q = 0; q < K; q++) {
+                const double t = nA == 1 ? v[q] : wave_tree(v[q]);
+                if (lane == 0) cs[q][w] = t;
+            }
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < K) res[threadIdx.x] = nA > 0 ? local_csum_inplace(cs[threadIdx.x], m) : 0.0;
+        __syncthreads();
+        return;
+    }
     int c = w;
     int a = c * 64 + lane;
     int i = a < nA ? aE[a] : 0;
@@ -1217,6 +1238,8 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
             __syncthreads();
         }
         const int na = nA;
+        const int myIdx = tid < na ? aE[tid] : 0;
+        const PoseEdgeD myE = pose_edge_load(E, myIdx, dM, dS);
         if (na > 0) {   // optimize(10); without active edges the vertex is not optimised at all
             ORBGPU_PROF_START;
             for (int k = 0; k < 10; k++) {
@@ -1279,7 +1302,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                             v[1 + r * 6 - (r * (r - 1)) / 2 + (cc - r)] = hh;
                         }
                     }
-                }, na, aE, E, dM, dS, cs, red);
+                }, na, aE, E, dM, dS, cs, red, myE, myIdx);
                 ORBGPU_PROF_MARK(1);
                 if (tid < 28) {
                     if (tid == 0) currentChi = iniChi = red[0];
@@ -1324,7 +1347,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                     }
                     __syncthreads();
                     ORBGPU_PROF_MARK(2);
-                    pose_pass<1>(err_term, na, aE, E, dM, dS, cs, red);
+                    pose_pass<1>(err_term, na, aE, E, dM, dS, cs, red, myE, myIdx);
                     ORBGPU_PROF_MARK(3);
                     if (tid == 0) {
                         double tempChi = red[0];
