@@ -35,6 +35,8 @@ METRIC = "tracking FPS + ORB matches/sec, KITTI-00 stereo; local-BA iter/sec"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md (spec)
 ROOFLINE_REPS = 5
 TRAFFIC_FILE = "traffic_r01.json"   # PMC FETCH_SIZE/WRITE_SIZE per launch (tools/pmc_traffic.py)
+VALU_FILE = "valu_r01.json"   # PMC SQ_INSTS_VALU per launch (tools/pmc_valu.py)
+VALU_PEAK_GINST = 1228.8   # 256 CUs x 2 wave64 VALU issues per cycle x 2.4 GHz (MI355X_MICROARCH.md)
 W, H, NFEAT = 1241, 376, 1200
 
 
@@ -328,12 +330,22 @@ def main():
             traffic_src = f"profiles/{TRAFFIC_FILE}"
         except Exception:
             traffic = None
+    valu = None
+    vf = ROOT / "profiles" / VALU_FILE
+    if vf.exists():
+        try:
+            vi = json.loads(vf.read_text())["k_fast_cells"]["valu_insts_per_launch"]
+            vr = vi / (k_avg_ms * 1e-3) / 1e9
+            valu = {"insts_per_launch": round(vi), "achieved": round(vr, 1), "peak": VALU_PEAK_GINST,
+                    "unit": "G wave-instr/s", "frac": round(vr / VALU_PEAK_GINST, 4), "source": f"profiles/{VALU_FILE}"}
+        except Exception:
+            valu = None
     roof = {"bound": "hbm", "kernel": "k_fast_cells", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_source": traffic_src, "avg_launch_ms": round(k_avg_ms, 4), "launches": ROOFLINE_REPS,
             "alg_bytes_per_launch": alg_bytes,
             "avg_launch_ms_in_pipeline": round(float(np.mean(kernel_ms)), 4),
-            "secondary_bound": "VALU (16-px circle test; DESIGN.md §3)"}
+            "secondary_bound": "VALU (16-px circle test; DESIGN.md §3)", "valu": valu}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
