@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(kS3Threads) k_sim3_opt(S3ProbDev* probs, const
                 if (term) break;
             }
         }
-        // chi2 gating on the last evaluated errors (Optimizer.cc:1171-1188 / 1205-1220)
+        // chi2 gating on the last evaluated errors (Optimizer.cc:1185-1209 / 1219-1234)
         int cnt = 0;
         for (int c = tid; c < nc; c += blockDim.x) {
             if (level[2 * c]) continue;
@@ -468,7 +468,7 @@ private:
     size_t cap_ = 0;
 };
 
-// Edge creation (Optimizer.cc:1097-1165): for each valid correspondence in index order,
+// Edge creation (Optimizer.cc:1099-1178): for each valid correspondence in index order,
 // e12 (point 2 -> camera 1) then e21 (point 1 -> camera 2).
 int Sim3OptEngine::run(int count, const sim3opt_problem* P, double* S12, uint8_t* const* erased, int* nIn) {
     std::vector<int> nc(count);
