@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=64, help="stereo frames per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--reserve-cus", type=int, default=0,
+                    help="extractor streams leave out one CU in N for the tracking lane (0: off)")
     ap.add_argument("--gba-kf", type=int, default=512, help="keyframes of the sharded global-BA problem")
     ap.add_argument("--gba-reps", type=int, default=3)
     return ap.parse_args()
@@ -244,6 +246,12 @@ def main():
     kernel_ms = []   # k_fast_cells duration per step (HIP events on the extractor streams)
     lanes = [Lane(), Lane()]
     exL = lanes[0].exL
+    if args.reserve_cus:
+        # the tracking lane's one-workgroup-per-frame kernels (k_select, k_pose_opt) need free
+        # wave slots while a batch is extracted: the extractor streams leave 1 CU in N out
+        for ln in lanes:
+            for ex in (ln.exL, ln.exR):
+                check(L.ORBextractor_reserve_cus(ex._h, args.reserve_cus), "ORBextractor_reserve_cus")
     ex_pool = ThreadPoolExecutor(1, initializer=lambda: torch.cuda.set_device(dev))
     state = {"k": 0, "ready": None}
 
@@ -313,6 +321,7 @@ def main():
     # Algorithmic bytes per launch = every level pixel read once (sum P_l = 1,444,097 B per
     # KITTI image) + 4 B per corner written + 4 B per cell count, over B images.
     torch.cuda.synchronize()
+    check(L.ORBextractor_reserve_cus(exL._h, 0), "ORBextractor_reserve_cus")   # the whole device
     iso_ms = []
     for _ in range(ROOFLINE_REPS):
         exL.extract_device(d_L.data_ptr(), B, W, H, W, W * H, lanes[0].d_kps.data_ptr(), lanes[0].d_desc.data_ptr(), cap)
@@ -371,7 +380,7 @@ def main():
             "config": {"workload": "kitti00_stereo: ORB extract L+R, ComputeStereoMatches, "
                                    "SearchByProjection(Cur,Last,th=7), PoseOptimization", "width": W, "height": H,
                        "nfeatures": NFEAT, "nlevels": 8, "scale_factor": 1.2, "fast_th": [20, 7],
-                       "stereo_frames_per_step": B, "parallelism": f"replicas{world}"},
+                       "stereo_frames_per_step": B, "parallelism": f"replicas{world}", "extractor_cu_reserve": args.reserve_cus},
             "matches_per_s": round(tot_match / dt, 1), "stereo_matches_per_s": round(tot_stereo / dt, 1),
             "keypoints_per_image": round(tot_kp / (2 * frames_total), 1),
             "pose_inliers_per_frame": round(float(np.sum(pose_inl)) / max(len(pose_inl) * P, 1), 1),

@@ -85,6 +85,7 @@ def lib():
     L.ORBextractor_get_blurred_level.argtypes = [vp, i32, i32, vp, i32, P(i32), P(i32)]
     L.ORBextractor_get_levels.argtypes = [vp, P(i32), P(f32)]
     L.ORBextractor_get_scale_tables.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.ORBextractor_reserve_cus.argtypes = [vp, i32]
     L.ORBextractor_stream.restype = vp
     L.ORBextractor_stream.argtypes = [vp]
     L.ORBextractor_last_timings.argtypes = [vp, vp]

@@ -98,6 +98,12 @@ int ORBextractor_get_scale_tables(ORBextractor_h h, float* scale, float* invScal
 
 void* ORBextractor_stream(ORBextractor_h h) { return h ? (void*)h->ex->stream() : nullptr; }
 
+int ORBextractor_reserve_cus(ORBextractor_h h, int one_in_n) {
+    if (!h || one_in_n < 0 || one_in_n == 1) return ORB_E_INVALID;
+    const int r = h->ex->reserve_cus(one_in_n);
+    return r == -4 ? ORB_E_NODEVICE : (r ? ORB_E_HIP : ORB_OK);
+}
+
 int ORBextractor_last_timings(ORBextractor_h h, float* ms6) {
     if (!h || !ms6) return ORB_E_INVALID;
     return h->ex->timings(ms6);

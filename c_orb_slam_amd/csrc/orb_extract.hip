@@ -654,6 +654,29 @@ int Extractor::init_device(int maxW, int maxH, int maxBatch) {
     return 0;
 }
 
+int Extractor::reserve_cus(int one_in_n) {
+    if (!stream_) return -4;
+    int dev = 0, ncu = 0;
+    ORB_HIP_CHECK(hipGetDevice(&dev));
+    ORB_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    hipStream_t s = nullptr;
+    if (one_in_n <= 0) {
+        ORB_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    } else {
+        // mask bit c is CU c / kXcds of XCD c % kXcds (CUs are enumerated round-robin over the
+        // XCDs): leave out the same CUs of every XCD so that no XCD's share of a grid straggles
+        constexpr int kXcds = 8;
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int c = 0; c < ncu; c++)
+            if ((c / kXcds) % one_in_n != one_in_n - 1) mask[c >> 5] |= 1u << (c & 31);
+        ORB_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    }
+    (void)hipStreamDestroy(stream_);
+    stream_ = s;
+    return 0;
+}
+
 void Extractor::gaussian_taps(int taps[7]) {
     // getGaussianKernel(7, 2, CV_32F) then *256 -> int (createSeparableLinearFilter)
     float cf[7];

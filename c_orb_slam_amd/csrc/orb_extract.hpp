@@ -62,6 +62,8 @@ public:
     int get_blurred(int index, int level, uint8_t* dst, int dst_step, int* w, int* h);
     int timings(float* ms6);
     hipStream_t stream() const { return stream_; }
+    // recreate the stream with a CU mask leaving out one CU in every `one_in_n` (0: all CUs)
+    int reserve_cus(int one_in_n);
     // Device pyramid of the last extract() (mvImagePyramid with its 19-px border): image b's
     // padded level l starts at pyramid_base() + b * pyramid_image_bytes() + levels()[l].off.
     const uint8_t* pyramid_base() const { return (const uint8_t*)d_pyr_; }

@@ -92,6 +92,12 @@ void* ORBextractor_stream(ORBextractor_h h);
 /* Per-stage device time of the last call (ms), from HIP events:
  * [0]=pyramid [1]=blur [2]=FAST cells [3]=compaction [4]=octree(host) [5]=orientation+rBRIEF */
 int ORBextractor_last_timings(ORBextractor_h h, float* ms6);
+/* Scheduling (no reference counterpart): keep one CU in every `one_in_n` of each XCD out of
+ * this extractor's launches (its stream is recreated with a CU mask), so the tracking lane's
+ * one-workgroup-per-frame kernels (matcher greedy replay, PoseOptimization) find free wave
+ * slots while a batch is being extracted.  one_in_n = 0 restores the full device.  Call
+ * between extractions; ORBextractor_stream() changes. */
+int ORBextractor_reserve_cus(ORBextractor_h h, int one_in_n);
 
 /* ======================================================================
  * ORBmatcher  (reference include/ORBmatcher.h:41-103, src/ORBmatcher.cc)
