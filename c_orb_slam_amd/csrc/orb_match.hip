@@ -38,9 +38,19 @@ __device__ __forceinline__ float gemm_row(const float* T, int r, float X0, float
 }
 
 // ---------------------------------------------------------------- grid build
+// LDS is sized at launch for the batch's largest frame (grid_lds_bytes), so the workgroup fits
+// in the slot a retiring extraction workgroup frees while the two lanes share the chip.
+__host__ __device__ inline int pow2_at_least(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+inline size_t grid_lds_bytes(int maxN) { return (size_t)pow2_at_least(std::max(maxN, 1)) * 4; }
+inline size_t select_lds_bytes(int maxN) { return ((size_t)std::max(maxN, 1) * 10 + 15) & ~(size_t)15; }
+
 __global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs) {
     ORBGPU_LATENCY_WAVE();
-    __shared__ uint32_t s_key[kMaxFrameKeys];
+    extern __shared__ uint32_t s_key[];   // pow2_at_least(max N) entries
     SearchDev& P = probs[blockIdx.x];
     const FrameDev& F = P.cur;
     const int N = F.N;
@@ -287,12 +297,14 @@ __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict_
 // observations) keep the latest taker, as the reference's sequential assignment does.
 template <bool LAST>
 __global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ probs, float th, int bMono,
-                                                float nnratio, int checkOri) {
+                                                float nnratio, int checkOri, int Nmax) {
     ORBGPU_LATENCY_WAVE();
-    __shared__ int s_owner[kMaxFrameKeys];    // earliest claiming query with Observations() > 0
-    __shared__ int s_lastq[kMaxFrameKeys];    // latest claiming query (any)
-    __shared__ uint8_t s_occ0[kMaxFrameKeys]; // occupancy before this call
-    __shared__ uint8_t s_rm[kMaxFrameKeys];   // slot cleared by the rotation check
+    // dynamic LDS, max N of the batch entries each (select_lds_bytes)
+    extern __shared__ int s_dyn[];
+    int* s_owner = s_dyn;                                           // earliest claiming query with Observations() > 0
+    int* s_lastq = s_dyn + Nmax;                                    // latest claiming query (any)
+    uint8_t* s_occ0 = reinterpret_cast<uint8_t*>(s_dyn + 2 * Nmax); // occupancy before this call
+    uint8_t* s_rm = s_occ0 + Nmax;                                  // slot cleared by the rotation check
     __shared__ int s_hsz[HISTO_LENGTH];
     __shared__ int s_ind[3];
     __shared__ int s_changed, s_nm, s_rmcnt;
@@ -527,7 +539,7 @@ int Matcher::area_candidates(const SearchDev& frame, const AreaQuery* d_q, int n
     s += (((size_t)nq + 1) * 4 + 255) & ~(size_t)255;
     SearchDev* dp = (SearchDev*)s;
     ORB_HIP_CHECK(hipMemcpyAsync(dp, &P, sizeof(SearchDev), hipMemcpyHostToDevice, stream_));
-    hipLaunchKernelGGL(k_build_grid, dim3(1), dim3(256), 0, stream_, dp);
+    hipLaunchKernelGGL(k_build_grid, dim3(1), dim3(256), grid_lds_bytes(frame.cur.N), stream_, dp);
     if (nq == 0) return hipStreamSynchronize(stream_) == hipSuccess ? 0 : -2;
     hipLaunchKernelGGL(k_area_count, dim3((nq + 255) / 256), dim3(256), 0, stream_, dp, d_q, nq, d_cnt);
     ORB_HIP_CHECK(hipGetLastError());
@@ -590,9 +602,10 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     const int np = (int)probs.size();
     if (np == 0) return 0;
     size_t need = 0;
-    int maxq = 0;
+    int maxq = 0, maxN = 1;
     for (auto& p : probs) {
         if (p.cur.N > kMaxFrameKeys || p.cur.N < 0 || p.nq < 0) return -1;
+        maxN = std::max(maxN, p.cur.N);
         need += ((size_t)(kGridCells + 1 + p.cur.N) * 4 + 255) & ~(size_t)255;
         need += ((size_t)p.nq * (kTopK * 8 + 16 + 8) + 255) & ~(size_t)255;
         maxq = std::max(maxq, p.nq);
@@ -620,14 +633,16 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     }
     ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, probs.data(), pb, hipMemcpyHostToDevice, stream_));
     SearchDev* dp = (SearchDev*)d_probs_;
-    hipLaunchKernelGGL(k_build_grid, dim3(np), dim3(256), 0, stream_, dp);
+    hipLaunchKernelGGL(k_build_grid, dim3(np), dim3(256), grid_lds_bytes(maxN), stream_, dp);
     if (maxq > 0) {
         if (lastMode) {
             hipLaunchKernelGGL(k_candidates<true>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, (int)bMono);
-            hipLaunchKernelGGL(k_select<true>, dim3(np), dim3(256), 0, stream_, dp, th, (int)bMono, nnratio_, (int)checkOri_);
+            hipLaunchKernelGGL(k_select<true>, dim3(np), dim3(256), select_lds_bytes(maxN), stream_, dp, th, (int)bMono,
+                               nnratio_, (int)checkOri_, maxN);
         } else {
             hipLaunchKernelGGL(k_candidates<false>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0);
-            hipLaunchKernelGGL(k_select<false>, dim3(np), dim3(256), 0, stream_, dp, th, 0, nnratio_, 0);
+            hipLaunchKernelGGL(k_select<false>, dim3(np), dim3(256), select_lds_bytes(maxN), stream_, dp, th, 0,
+                               nnratio_, 0, maxN);
         }
     }
     ORB_HIP_CHECK(hipGetLastError());
