@@ -1437,12 +1437,14 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
 
 // Device mode edge creation (Optimizer.cc:268-347): rows with a map point, keypoint order,
 // compacted by a block scan; the initial pose from the frame's Tcw.  One workgroup per frame.
-__global__ void __launch_bounds__(kPoseThreads) k_pose_pack(PoseProbDev* probs, PoseEdgeDev* Eall) {
+// 4 waves: the pack fits in the slot of one retiring extraction workgroup
+constexpr int kPackThreads = 256;
+__global__ void __launch_bounds__(kPackThreads) k_pose_pack(PoseProbDev* probs, PoseEdgeDev* Eall) {
     ORBGPU_LATENCY_WAVE();
     PoseProbDev& P = probs[blockIdx.x];
     const int N = P.N, tid = threadIdx.x;
     PoseEdgeDev* E = Eall + P.e0;
-    __shared__ int wsum[kPoseThreads / 64], base;
+    __shared__ int wsum[kPackThreads / 64], base;
     if (tid == 0) {
         base = 0;
         double R[9];
@@ -1454,7 +1456,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_pack(PoseProbDev* probs, 
         se3_normalize(P.T0);
     }
     __syncthreads();
-    for (int c0 = 0; c0 < N; c0 += kPoseThreads) {
+    for (int c0 = 0; c0 < N; c0 += kPackThreads) {
         const int i = c0 + tid;
         const int f = i < N ? (P.mpidx ? (P.mpidx[i] >= 0 ? 1 : 0) : (P.has_mp[i] ? 1 : 0)) : 0;
         int incl = f;
@@ -1491,7 +1493,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_pack(PoseProbDev* probs, 
             }
         }
         __syncthreads();
-        if (tid == kPoseThreads - 1) base = off + incl;
+        if (tid == kPackThreads - 1) base = off + incl;
         __syncthreads();
     }
     if (tid == 0) P.ne = base > kPoseMaxEdges ? -1 : base;
@@ -1578,7 +1580,7 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
     PoseProbDev* dp = (PoseProbDev*)d;
     PoseEdgeDev* dE = (PoseEdgeDev*)(d + bProb);
     ORB_HIP_CHECK(hipMemcpyAsync(d, h, bProb, hipMemcpyHostToDevice, stream_));
-    hipLaunchKernelGGL(k_pose_pack, dim3(count), dim3(kPoseThreads), 0, stream_, dp, dE);
+    hipLaunchKernelGGL(k_pose_pack, dim3(count), dim3(kPackThreads), 0, stream_, dp, dE);
     hipLaunchKernelGGL(k_pose_opt, dim3(count), dim3(kPoseThreads), 0, stream_, dp, (const PoseEdgeDev*)dE,
                        (double*)(d + bProb + bEdge), (uint8_t*)(d + bProb + bEdge + bErr));
     ORB_HIP_CHECK(hipGetLastError());
