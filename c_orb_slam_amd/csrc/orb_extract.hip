@@ -290,7 +290,8 @@ __device__ __forceinline__ void mask_scan64(const uint64_t* masks, int n, int* o
 __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ pyr, size_t img_bytes,
                                                     const CellDesc* __restrict__ cells, int iniTh, int minTh,
                                                     uint32_t* __restrict__ slots, size_t slots_per_image,
-                                                    int* __restrict__ counts, int ncells) {
+                                                    int* __restrict__ counts, int ncells,
+                                                    const int* __restrict__ work) {
     __shared__ uint32_t s_img32[FC_MAXR * FC_LD / 4];
     __shared__ uint32_t s_sc32[FC_MAXR * FC_LD / 4];
     __shared__ uint16_t s_list[64 * 64];
@@ -298,12 +299,15 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     __shared__ int s_off[65];
     uint8_t* s_img = reinterpret_cast<uint8_t*>(s_img32);
     uint8_t* s_sc = reinterpret_cast<uint8_t*>(s_sc32);
-    // identity cell order: the XCD-contiguous order (xcd_tile) cut FETCH_SIZE 4.8x here but ran
-    // ~9 % slower -- this kernel is VALU-bound and the contiguous runs unbalance the XCDs
+    // work order (Extractor::build_work): workgroup g runs on XCD g % 8; whole cell rows of an
+    // image go to one XCD (rows dealt round-robin), so horizontally adjacent cells -- which
+    // share ROI halo columns and 128-B lines -- hit that XCD's L2 instead of being fetched
+    // once per XCD, while every XCD still gets the same mix of levels
     ORBGPU_PROF_START;
-    const int cell = blockIdx.x;
+    const int wk = work[blockIdx.x];
+    if (wk < 0) return;   // padding of a shorter XCD list
+    const int cell = wk & 0xffff, b = wk >> 16;
     const CellDesc cd = cells[cell];
-    const int b = blockIdx.y;
     const int rows = cd.r1 - cd.r0, cols = cd.c1 - cd.c0;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     int* cnt_out = counts + (size_t)b * ncells + cell;
@@ -611,13 +615,14 @@ Extractor::~Extractor() { release(); }
 
 void Extractor::release() {
     auto F = [](void* p) { if (p) (void)hipFree(p); };
-    F(d_in_); F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_);
+    F(d_in_); F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_work_);
     F(d_lcb_); F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_);
     F(d_kps_); F(d_desc_); F(d_jobsel_); F(d_jobcnt_); F(d_octlv_); F(d_gscr_); F(d_nout_); F(d_ptiles_);
     d_ptiles_ = nullptr;
     d_jobsel_ = d_jobcnt_ = d_octlv_ = d_gscr_ = d_nout_ = nullptr;
     d_in_ = d_pyr_ = d_blur_ = nullptr;
-    d_slots_ = nullptr; d_counts_ = nullptr; d_cells_ = nullptr; d_tiles_ = nullptr;
+    d_slots_ = nullptr; d_counts_ = nullptr; d_cells_ = nullptr; d_tiles_ = nullptr; d_work_ = nullptr;
+    work_B_ = -1;
     d_lcb_ = nullptr; d_packed_ = nullptr; d_hdr_ = nullptr; d_gtotal_ = nullptr; d_sel_ = nullptr;
     d_levels_ = nullptr; d_tabs_ = nullptr; d_kps_ = nullptr; d_desc_ = nullptr;
     if (h_nout_) (void)hipHostFree(h_nout_);
@@ -651,6 +656,36 @@ int Extractor::init_device(int maxW, int maxH, int maxBatch) {
     ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_disc), disc.data(), disc.size()));
     ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_ndisc), &nd, sizeof(int)));
     maxW_ = maxW; maxH_ = maxH; maxB_ = maxBatch;
+    return 0;
+}
+
+// k_fast_cells work order for a batch of B images: the cell rows (cells sharing level and ROI
+// top row, in cell order) of every image are dealt round-robin to the 8 XCDs; entry
+// g = slot * 8 + xcd of the table is the slot-th (b << 16 | cell) of that XCD's list, -1 past
+// its end.
+int Extractor::build_work(int B) {
+    constexpr int kXcds = 8;
+    const int ncells = (int)cells_.size();
+    std::vector<int> unit;
+    for (int c = 0; c < ncells; c++)
+        if (c == 0 || cells_[c].level != cells_[c - 1].level || cells_[c].r0 != cells_[c - 1].r0) unit.push_back(c);
+    unit.push_back(ncells);
+    std::vector<std::vector<int>> lists(kXcds);
+    long u = 0;
+    for (int b = 0; b < B; b++)
+        for (size_t k = 0; k + 1 < unit.size(); k++, u++)
+            for (int c = unit[k]; c < unit[k + 1]; c++) lists[u % kXcds].push_back((b << 16) | c);
+    size_t len = 0;
+    for (auto& l : lists) len = std::max(len, l.size());
+    std::vector<int> work(len * kXcds, -1);
+    for (int x = 0; x < kXcds; x++)
+        for (size_t sl = 0; sl < lists[x].size(); sl++) work[sl * kXcds + x] = lists[x][sl];
+    if (d_work_) (void)hipFree(d_work_);
+    d_work_ = nullptr;
+    ORB_HIP_CHECK(hipMalloc(&d_work_, std::max<size_t>(work.size(), 1) * 4));
+    ORB_HIP_CHECK(hipMemcpy(d_work_, work.data(), work.size() * 4, hipMemcpyHostToDevice));
+    work_n_ = (int)work.size();
+    work_B_ = B;
     return 0;
 }
 
@@ -877,7 +912,8 @@ int Extractor::setup_geometry(int W, int H) {
     ptile_begin_[nlevels_] = (int)ptiles_.size();
     // (re)allocate device buffers for maxB_
     auto F = [](void*& p) { if (p) (void)hipFree(p); p = nullptr; };
-    F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_lcb_);
+    F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_lcb_); F(d_work_);
+    work_B_ = -1;
     F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_); F(d_ptiles_);
     const int B = maxB_;
     ORB_HIP_CHECK(hipMalloc(&d_ptiles_, std::max<size_t>(ptiles_.size(), 1) * sizeof(PyrTile)));
@@ -990,9 +1026,10 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
     // 3. FAST per cell
     const int ncells = (int)cells_.size();
-    hipLaunchKernelGGL(k_fast_cells, dim3(ncells, B), dim3(256), 0, s, (const uint8_t*)d_pyr_, img_bytes_,
+    if (work_B_ != B && build_work(B)) return -2;
+    hipLaunchKernelGGL(k_fast_cells, dim3(work_n_), dim3(256), 0, s, (const uint8_t*)d_pyr_, img_bytes_,
                        (const CellDesc*)d_cells_, iniTh_, minTh_, (uint32_t*)d_slots_, slots_per_image_,
-                       (int*)d_counts_, ncells);
+                       (int*)d_counts_, ncells, (const int*)d_work_);
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[3], s));
     // 4. compaction

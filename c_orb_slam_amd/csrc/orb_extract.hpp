@@ -64,6 +64,7 @@ public:
     hipStream_t stream() const { return stream_; }
     // recreate the stream with a CU mask leaving out one CU in every `one_in_n` (0: all CUs)
     int reserve_cus(int one_in_n);
+    int build_work(int B);
     // Device pyramid of the last extract() (mvImagePyramid with its 19-px border): image b's
     // padded level l starts at pyramid_base() + b * pyramid_image_bytes() + levels()[l].off.
     const uint8_t* pyramid_base() const { return (const uint8_t*)d_pyr_; }
@@ -111,6 +112,8 @@ private:
     void *d_cells_ = nullptr, *d_tiles_ = nullptr, *d_lcb_ = nullptr, *d_packed_ = nullptr, *d_hdr_ = nullptr;
     void *d_sel_ = nullptr, *d_levels_ = nullptr, *d_tabs_ = nullptr, *d_kps_ = nullptr, *d_desc_ = nullptr;
     int* d_gtotal_ = nullptr;
+    void* d_work_ = nullptr;   // k_fast_cells work order (build_work), for work_B_ images
+    int work_B_ = -1, work_n_ = 0;
     bool d_gtotal_alias_ = false;
     size_t in_cap_ = 0, out_cap_ = 0;
     // device octree (octree.hip): per-job selections, per-image selected lists
