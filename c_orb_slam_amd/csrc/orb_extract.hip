@@ -508,11 +508,24 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                                                      size_t img_bytes, size_t blur_bytes, const int2* __restrict__ sel, int selcap,
                                                      const int* __restrict__ nout, const LevelDev* __restrict__ lv,
                                                      orb_kp_dev* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                     int cap_per_image) {
+                                                     int cap_per_image, int gx, int B) {
+    // batches of >= 8 images: workgroup g runs on XCD g % 8, and image b's keypoint groups all
+    // go to XCD b % 8 (images in turn), so the level and blurred-level lines their patches
+    // share stay in that XCD's L2; smaller batches spread every image over all XCDs
     const int lane = threadIdx.x & 63;
-    const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (k >= nout[blockIdx.y] || k >= cap_per_image) return;
-    const int2 s = sel[(size_t)blockIdx.y * selcap + k];
+    int img, grp;
+    if (B >= 8) {
+        const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+        img = xcd + 8 * (slot / gx);
+        grp = slot - (slot / gx) * gx;
+    } else {
+        img = blockIdx.x / gx;
+        grp = blockIdx.x - img * gx;
+    }
+    if (img >= B) return;
+    const int k = grp * 4 + (threadIdx.x >> 6);
+    if (k >= nout[img] || k >= cap_per_image) return;
+    const int2 s = sel[(size_t)img * selcap + k];
     const uint32_t pk = (uint32_t)s.x;
     const int meta = s.y;
     const int b = meta >> 20, l = (meta >> 16) & 15, idx = meta & 0xffff;
@@ -1063,9 +1076,13 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
         okps = (orb_kp_dev*)d_kps_;
         odesc = (uint8_t*)d_desc_;
     }
-    hipLaunchKernelGGL(k_orient_desc, dim3((selcap_ + 3) / 4, B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
-                       (const uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const int2*)d_sel_, selcap_,
-                       (const int*)d_nout_, (const LevelDev*)d_levels_, okps, odesc, cap);
+    {
+        const int gx = (selcap_ + 3) / 4;
+        const int nwg = B >= 8 ? gx * 8 * ((B + 7) / 8) : gx * B;
+        hipLaunchKernelGGL(k_orient_desc, dim3(nwg), dim3(256), 0, s, (const uint8_t*)d_pyr_,
+                           (const uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const int2*)d_sel_, selcap_,
+                           (const int*)d_nout_, (const LevelDev*)d_levels_, okps, odesc, cap, gx, B);
+    }
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipMemcpyAsync(h_nout_, d_nout_, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, s));
     ORB_HIP_CHECK(hipEventRecord(ev_[6], s));
