@@ -344,34 +344,29 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     ORBGPU_PROF_MARK(0);
     const int dr = rows - 6, dc = cols - 6;
     const int tp = min(iniTh, minTh);
-    // lane -> (row slot, column): two rows per instruction for cells <= 32 columns
-    const bool two = dc <= 32;
-    const int sub = two ? (lane >> 5) : 0, col = two ? (lane & 31) : lane, rstep = two ? 2 : 1;
-    const bool col_ok = col < dc;
-    const int c = 3 + col;
-    for (int rb = wid * rstep; rb < dr; rb += 4 * rstep) {
-        const int i = rb + sub;
-        const bool pass = col_ok && i < dr && (tp < 1 || fast_pretest(&s_img[(3 + i) * FC_LD + mis + c], FC_LD, tp));
+    // detection pixels flattened in raster order, 64 per wave instruction (all lanes busy for
+    // any cell width): pixel p = i * dc + j of chunk p >> 6; i = floor((p + 0.5) / dc) is exact
+    // in float for p < 4096, dc <= 64 (the fraction stays >= 1/128 from an integer)
+    const int npx = dr * dc, nchk = (npx + 63) >> 6;
+    const float inv_dc = 1.0f / (float)dc;
+    for (int ch = wid; ch < nchk; ch += 4) {
+        const int px = ch * 64 + lane;
+        const int i = (int)(((float)px + 0.5f) * inv_dc), j = px - i * dc;
+        const bool pass = px < npx && (tp < 1 || fast_pretest(&s_img[(3 + i) * FC_LD + mis + 3 + j], FC_LD, tp));
         const uint64_t m = __ballot(pass);
-        if (lane == 0) {
-            if (two) {
-                s_mask[rb] = m & 0xffffffffull;
-                if (rb + 1 < dr) s_mask[rb + 1] = m >> 32;
-            } else {
-                s_mask[rb] = m;
-            }
-        }
+        if (lane == 0) s_mask[ch] = m;
     }
     __syncthreads();
     ORBGPU_PROF_MARK(1);
-    if (wid == 0) mask_scan64(s_mask, dr, s_off, lane);
+    if (wid == 0) mask_scan64(s_mask, nchk, s_off, lane);
     __syncthreads();
     const int nl = s_off[64];
-    for (int rb = wid * rstep; rb < dr; rb += 4 * rstep) {
-        const int i = rb + sub;
-        if (i < dr && col_ok) {
-            const uint64_t m = s_mask[i];
-            if ((m >> col) & 1ull) s_list[s_off[i] + __popcll(m & ((1ull << col) - 1ull))] = (uint16_t)(((3 + i) << 8) | c);
+    for (int ch = wid; ch < nchk; ch += 4) {
+        const uint64_t m = s_mask[ch];
+        if ((m >> lane) & 1ull) {
+            const int px = ch * 64 + lane;
+            const int i = (int)(((float)px + 0.5f) * inv_dc), j = px - i * dc;
+            s_list[s_off[ch] + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(((3 + i) << 8) | (3 + j));
         }
     }
     __syncthreads();
