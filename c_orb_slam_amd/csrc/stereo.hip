@@ -203,10 +203,12 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
 
 // median filter (Frame.cc:624-639): sort the kept SADs, thDist = 1.5f*1.4f*median,
 // invalidate SAD >= thDist (the reference walks the sorted tail from the end).
-__global__ void __launch_bounds__(1024) k_stereo_filter(const StereoDev* __restrict__ probs) {
+// 4 waves and LDS sized at launch (next power of two of the batch's largest NL): the workgroup
+// fits in the slot of one retiring extraction workgroup (1,024 threads + 16 KB waited ~3x longer)
+__global__ void __launch_bounds__(256) k_stereo_filter(const StereoDev* __restrict__ probs) {
     ORBGPU_LATENCY_WAVE();
     const StereoDev& S = probs[blockIdx.x];
-    __shared__ int v[kStereoMaxKeys];
+    extern __shared__ int v[];
     __shared__ int cnt, kept;
     const int tid = threadIdx.x;
     if (tid == 0) cnt = 0;
@@ -261,7 +263,9 @@ int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoPa
     hipLaunchKernelGGL(k_stereo_rows, dim3(nprob), dim3(1024), 0, s, d_probs, P);
     if (maxNL > 0)
         hipLaunchKernelGGL(k_stereo_match, dim3((maxNL + 3) / 4, nprob), dim3(256), 0, s, d_probs, P);
-    hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(1024), 0, s, d_probs);
+    int m = 1;
+    while (m < std::max(maxNL, 1)) m <<= 1;
+    hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(256), (size_t)m * sizeof(int), s, d_probs);
     ORB_HIP_CHECK(hipGetLastError());
     return 0;
 }
