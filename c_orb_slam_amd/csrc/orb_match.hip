@@ -38,57 +38,89 @@ __device__ __forceinline__ float gemm_row(const float* T, int r, float X0, float
 }
 
 // ---------------------------------------------------------------- grid build
-// LDS is sized at launch for the batch's largest frame (grid_lds_bytes), so the workgroup fits
-// in the slot a retiring extraction workgroup frees while the two lanes share the chip.
-__host__ __device__ inline int pow2_at_least(int n) {
-    int p = 1;
-    while (p < n) p <<= 1;
-    return p;
-}
-inline size_t grid_lds_bytes(int maxN) { return (size_t)pow2_at_least(std::max(maxN, 1)) * 4; }
+
+// Frame::AssignFeaturesToGrid (Frame.cc:230-245) as a counting sort: gridIdx lists every cell's
+// keypoints in index order, cells in x-major order (cell = px * 48 + py), gridStart[c] its
+// offset; keypoints outside the grid follow as 4095.  Per-cell counts and cursors are packed
+// 16-bit pairs in LDS (a cell holds at most N <= 4096 keypoints), the scatter is by LDS atomics,
+// and a thread per cell restores index order inside its (few-entry) segment.
+inline size_t grid_lds_bytes(int maxN) { return (((size_t)std::max(maxN, 1) * 2 + 15) & ~(size_t)15); }
 inline size_t select_lds_bytes(int maxN) { return ((size_t)std::max(maxN, 1) * 10 + 15) & ~(size_t)15; }
 
 __global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs) {
     ORBGPU_LATENCY_WAVE();
-    extern __shared__ uint32_t s_key[];   // pow2_at_least(max N) entries
+    constexpr int kPer = kGridCells / 256;   // 12 cells per thread in the scan
+    static_assert(kGridCells % 512 == 0, "packed pairs per thread");
+    __shared__ uint32_t s_cnt[kGridCells / 2];
+    __shared__ int s_wsum[4];
+    extern __shared__ int16_t s_cell[];   // max N entries: cell of keypoint i or -1
     SearchDev& P = probs[blockIdx.x];
     const FrameDev& F = P.cur;
-    const int N = F.N;
-    int Pn = 1;
-    while (Pn < N) Pn <<= 1;
-    for (int i = threadIdx.x; i < Pn; i += 256) {
-        uint32_t key = 0xffffffffu;
-        if (i < N) {
-            const orb_kp_dev kp = F.keysUn[i];
-            const int px = (int)roundf((kp.x - F.minX) * F.gridWInv);
-            const int py = (int)roundf((kp.y - F.minY) * F.gridHInv);
-            if (!(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows))
-                key = ((uint32_t)(px * kGridRows + py) << 12) | (uint32_t)i;
+    const int N = F.N, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int w = tid; w < kGridCells / 2; w += 256) s_cnt[w] = 0u;
+    __syncthreads();
+    for (int i = tid; i < N; i += 256) {
+        const orb_kp_dev kp = F.keysUn[i];
+        const int px = (int)roundf((kp.x - F.minX) * F.gridWInv);
+        const int py = (int)roundf((kp.y - F.minY) * F.gridHInv);
+        int cell = -1;
+        if (!(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows)) {
+            cell = px * kGridRows + py;
+            atomicAdd(&s_cnt[cell >> 1], 1u << (16 * (cell & 1)));
         }
-        s_key[i] = key;
+        s_cell[i] = (int16_t)cell;
     }
     __syncthreads();
-    for (int k = 2; k <= Pn; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < Pn; i += 256) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const uint32_t a = s_key[i], b = s_key[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) { s_key[i] = b; s_key[ixj] = a; }
-                }
+    // exclusive scan of the counts: thread t owns cells [kPer t, kPer t + kPer)
+    int cnt[kPer], tot = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k += 2) {
+        const uint32_t w = s_cnt[(kPer * tid + k) >> 1];
+        cnt[k] = (int)(w & 0xffffu);
+        cnt[k + 1] = (int)(w >> 16);
+        tot += cnt[k] + cnt[k + 1];
+    }
+    int incl = tot;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_wsum[wid] = incl;
+    __syncthreads();
+    int run = incl - tot;
+    for (int w = 0; w < wid; w++) run += s_wsum[w];
+    const int total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+#pragma unroll
+    for (int k = 0; k < kPer; k += 2) {
+        const int c = kPer * tid + k;
+        P.gridStart[c] = run;
+        P.gridStart[c + 1] = run + cnt[k];
+        s_cnt[c >> 1] = (uint32_t)run | ((uint32_t)(run + cnt[k]) << 16);   // cursors
+        run += cnt[k] + cnt[k + 1];
+    }
+    if (tid == 255) P.gridStart[kGridCells] = total;
+    __syncthreads();
+    for (int i = tid; i < N; i += 256) {
+        const int cell = s_cell[i];
+        if (cell >= 0) {
+            const int sh = 16 * (cell & 1);
+            const int pos = (int)((atomicAdd(&s_cnt[cell >> 1], 1u << sh) >> sh) & 0xffffu);
+            P.gridIdx[pos] = i;
+        }
+    }
+    for (int i = total + tid; i < N; i += 256) P.gridIdx[i] = 4095;
+    __syncthreads();
+    for (int c = tid; c < kGridCells; c += 256) {   // index order inside each cell
+        const int b0 = P.gridStart[c], b1 = P.gridStart[c + 1];
+        for (int x = b0 + 1; x < b1; x++) {
+            const int v = P.gridIdx[x];
+            int y = x - 1;
+            while (y >= b0 && P.gridIdx[y] > v) {
+                P.gridIdx[y + 1] = P.gridIdx[y];
+                y--;
             }
-            __syncthreads();
+            P.gridIdx[y + 1] = v;
         }
-    for (int i = threadIdx.x; i < N; i += 256) P.gridIdx[i] = (int)(s_key[i] & 0xfff);
-    for (int c = threadIdx.x; c <= kGridCells; c += 256) {
-        const uint32_t target = (uint32_t)c << 12;
-        int lo = 0, hi = N;  // first position with key >= target
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (s_key[mid] < target) lo = mid + 1; else hi = mid;
-        }
-        P.gridStart[c] = lo;
     }
 }
 
