@@ -42,7 +42,9 @@ W, H, NFEAT = 1241, 376, 1200
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (one rank each); default: WORLD_SIZE or 1")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: ranks meet over gloo and rank 0 prints n_gpus")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64, help="stereo frames per step")
@@ -59,8 +61,58 @@ def lift_depth(rng, n):
     return rng.uniform(5.0, 50.0, size=n).astype(np.float32)
 
 
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes (one per GPU) before
+    this process touches the GPU, relay rank 0's JSON line, exit with the worst exit code.
+    Under torch.distributed.run WORLD_SIZE is already set and this is not used."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].stdout.read()
+    codes = [p.wait() for p in procs]
+    sys.stdout.write(out.decode())
+    sys.stdout.flush()
+    return next((c for c in codes if c != 0), 0)
+
+
+def dry_run(args):
+    """The rank plumbing of main() on gloo (CPU): every rank joins, rank 0 prints what the real run
+    would report as n_gpus / parallelism (tests/test_bench_launcher.py)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    seen = world
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks_joined": seen, "parallelism": f"replicas{world}"}), flush=True)
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(env_world or 1)
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (launch one rank per GPU)")
+    if args.dry_run:
+        return dry_run(args)
     # stdout carries exactly one JSON line: libraries that print banners at init (RCCL prints
     # its version block when a communicator is created) write to fd 1, so point fd 1 at
     # stderr for the run and keep the real stdout for the result.
