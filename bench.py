@@ -52,7 +52,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--reserve-cus", type=int, default=0,
                     help="extractor streams leave out one CU in N for the tracking lane (0: off)")
-    ap.add_argument("--gba-kf", type=int, default=512, help="keyframes of the sharded global-BA problem")
+    ap.add_argument("--gba-kf", type=int, default=2000,
+                    help="keyframes of the sharded global-BA problem (SURVEY config 5: 2k, 8k, 16k)")
     ap.add_argument("--gba-reps", type=int, default=3)
     return ap.parse_args()
 

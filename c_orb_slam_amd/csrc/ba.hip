@@ -446,14 +446,13 @@ __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double*
 __global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __restrict__ Emat,
                                                 const double* __restrict__ Hpl, const double* __restrict__ cb,
                                                 const double* Hpp, const double* bp, double lam_host, int use_dev,
-                                                const double* scal, double* S, double* bs, int own) {
+                                                const double* scal, SysAddr S, double* bs, int own) {
     __shared__ double cs[36][kChunks];
     const int blk = blockIdx.x;
     const int i1 = s.blkI[blk], i2 = s.blkJ[blk];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int s0 = s.blkStart[blk], n = s.blkStart[blk + 1] - s0;
     const int m = (n + 63) >> 6;
-    const int nn = 6 * s.nP;
     const bool diag = i1 == i2;
     const int nent = diag ? 27 : 36;
     for (int c = w; c < m; c += nw) {
@@ -516,7 +515,7 @@ __global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __r
         h = Hpp[21 * i1 + q];
         if (c == r) h += lambda;
     }
-    S[(size_t)(6 * i1 + r) * nn + 6 * i2 + c] = h - v;
+    *S.at(6 * i1 + r, 6 * i2 + c) = h - v;
 }
 
 // Dense LDL^T of the upper triangle + solve, one workgroup (256 threads).
@@ -629,6 +628,7 @@ __device__ long long g_ldlt_probe[256];
     } while (0)
 #endif
 constexpr int kLdltMax = 128;
+constexpr int kDenseMaxN = 144;   // >= every n the dense single-workgroup solvers take (n^2 doubles in LDS)
 constexpr int kLdltWaves = 16;
 constexpr int kLdltRows = kLdltMax / kLdltWaves;
 __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restrict__ Sg, const double* bs, double* x,
@@ -1707,6 +1707,12 @@ int BaEngine::init() {
     return 0;
 }
 
+bool BaEngine::dense_solver(int n) const {
+    const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
+    const size_t ldsBytes = sizeof(double) * ((size_t)n + (size_t)n * n);
+    return n <= kDenseMaxN && ((n <= kLdltMax && regShm <= ldsMax_) || ldsBytes <= ldsMax_);
+}
+
 // Carve every device buffer of the problem out of one grow-only arena.
 int BaEngine::carve(bool commit, size_t* total) {
     const size_t ne = (size_t)std::max(ne_, 1), nkf = (size_t)std::max(nkf_, 1), npt = (size_t)std::max(npt_, 1);
@@ -1735,7 +1741,10 @@ int BaEngine::carve(bool commit, size_t* total) {
     dBl_ = (double*)take(sizeof(double) * 3 * npt);
     dB_ = (double*)take(sizeof(double) * (6 * nkf + 3 * npt));
     dX2_ = (double*)take(sizeof(double) * (6 * nkf + 3 * npt));
-    dS_ = (double*)take(sizeof(double) * 36 * nkf * nkf);
+    // dense S only for the single-workgroup solvers (n = 6 nP <= kDenseMaxN); larger systems
+    // live in the block-sparse tiles of sp_ (ldlt.hip)
+    const size_t nd = std::min(6 * nkf, (size_t)kDenseMaxN);
+    dS_ = (double*)take(sizeof(double) * nd * nd);
     dBs_ = (double*)take(sizeof(double) * 6 * nkf);
     dDinv_ = (double*)take(sizeof(double) * 9 * npt);
     dDb_ = (double*)take(sizeof(double) * 3 * npt);
@@ -1749,7 +1758,6 @@ int BaEngine::carve(bool commit, size_t* total) {
     tmpA1_ = (double*)take(sizeof(double) * tmpN);
     tmpB0_ = (double*)take(sizeof(double) * tmpN);
     tmpB1_ = (double*)take(sizeof(double) * tmpN);
-    dLdltWs_ = take(ldlt_tiled_workspace((int)(6 * nkf)));
     *total = off;
     return 0;
 }
@@ -1966,8 +1974,9 @@ int BaEngine::build_structure(int level) {
     st_.leList = d + off[8]; st_.lpStart = d + off[9]; st_.lpList = d + off[10]; st_.blkI = d + off[11];
     st_.blkJ = d + off[12]; st_.blkStart = d + off[13]; st_.pairA = d + off[14]; st_.pairB = d + off[15];
     nTiles_ = 0;
-    if (comm_ && nP > 0) {
-        // union (over the shards) of the 64x64 tiles the Schur blocks touch; S travels as those tiles
+    tiled_ = nP > 0 && !dense_solver(6 * nP);
+    if ((comm_ || tiled_) && nP > 0) {
+        // the 64x64 tiles the Schur blocks touch (union over the shards)
         const int n = 6 * nP, nt = (n + 63) / 64;
         std::vector<double> tm((size_t)nt * nt, 0.0);
         for (int b = 0; b < nBlk; b++) {
@@ -1976,31 +1985,40 @@ int BaEngine::build_structure(int level) {
                 for (int J = (6 * i2) / 64; J <= (6 * i2 + 5) / 64; J++)
                     if (I <= J) tm[(size_t)I * nt + J] = 1.0;
         }
-        if (tm.size() > scratchN_) return -3;
-        ORB_HIP_CHECK(hipMemcpyAsync(dScratch_, tm.data(), sizeof(double) * tm.size(), hipMemcpyHostToDevice, stream_));
-        if (int e = comm_->allreduce(dScratch_, tm.size(), RedOp::Max, stream_)) return e;
-        ORB_HIP_CHECK(hipMemcpyAsync(tm.data(), dScratch_, sizeof(double) * tm.size(), hipMemcpyDeviceToHost, stream_));
-        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
-        std::vector<int2> tl;
-        for (int I = 0; I < nt; I++)
-            for (int J = I; J < nt; J++)
-                if (tm[(size_t)I * nt + J] != 0.0) tl.push_back(make_int2(I, J));
-        nTiles_ = (int)tl.size();
-        const size_t need = sizeof(int2) * tl.size() + 256 + sizeof(double) * ((size_t)nTiles_ * 4096 + n);
-        if (need > packCap_) {
-            if (dPack_) (void)hipFree(dPack_);
-            dPack_ = nullptr;
-            packCap_ = 0;
-            ORB_HIP_CHECK(hipMalloc(&dPack_, need));
-            packCap_ = need;
+        if (comm_) {
+            if (tm.size() > scratchN_) return -3;
+            ORB_HIP_CHECK(hipMemcpyAsync(dScratch_, tm.data(), sizeof(double) * tm.size(), hipMemcpyHostToDevice, stream_));
+            if (int e = comm_->allreduce(dScratch_, tm.size(), RedOp::Max, stream_)) return e;
+            ORB_HIP_CHECK(hipMemcpyAsync(tm.data(), dScratch_, sizeof(double) * tm.size(), hipMemcpyDeviceToHost, stream_));
+            ORB_HIP_CHECK(hipStreamSynchronize(stream_));
         }
-        dTiles_ = (int2*)dPack_;
-        dPackBuf_ = (double*)((char*)dPack_ + ((sizeof(int2) * tl.size() + 255) & ~(size_t)255));
-        ORB_HIP_CHECK(hipMemcpyAsync(dTiles_, tl.data(), sizeof(int2) * tl.size(), hipMemcpyHostToDevice, stream_));
-        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        if (tiled_) {
+            // block-sparse system: symbolic factorisation; S travels as the Schur-pattern prefix
+            std::vector<uint8_t> mask(tm.size());
+            for (size_t q = 0; q < tm.size(); q++) mask[q] = tm[q] != 0.0;
+            if (int e = sp_.build(n, mask, stream_)) return e;
+        } else {
+            std::vector<int2> tl;
+            for (int I = 0; I < nt; I++)
+                for (int J = I; J < nt; J++)
+                    if (tm[(size_t)I * nt + J] != 0.0) tl.push_back(make_int2(I, J));
+            nTiles_ = (int)tl.size();
+            const size_t need = sizeof(int2) * tl.size() + 256 + sizeof(double) * ((size_t)nTiles_ * 4096 + n);
+            if (need > packCap_) {
+                if (dPack_) (void)hipFree(dPack_);
+                dPack_ = nullptr;
+                packCap_ = 0;
+                ORB_HIP_CHECK(hipMalloc(&dPack_, need));
+                packCap_ = need;
+            }
+            dTiles_ = (int2*)dPack_;
+            dPackBuf_ = (double*)((char*)dPack_ + ((sizeof(int2) * tl.size() + 255) & ~(size_t)255));
+            ORB_HIP_CHECK(hipMemcpyAsync(dTiles_, tl.data(), sizeof(int2) * tl.size(), hipMemcpyHostToDevice, stream_));
+            ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        }
     }
     ORB_HIP_CHECK(hipMemsetAsync(dX2_, 0, sizeof(double) * (6 * (size_t)nP + 3 * (size_t)nL + 1), stream_));
-    ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * 36 * (size_t)nP * nP + 8, stream_));
+    if (!tiled_) ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * 36 * (size_t)nP * nP + 8, stream_));
     // the pageable hStruct_ copy must finish before the host vector is reused
     ORB_HIP_CHECK(hipStreamSynchronize(stream_));
     return 0;
@@ -2054,19 +2072,27 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
     const bool use_reg = n <= kLdltMax && regShm <= ldsMax_;
     // n <= 128: register-resident single-workgroup LDL^T; S fits LDS: single-workgroup in LDS;
-    // larger: tiled multi-workgroup LDL^T in HBM (ldlt.hip)
-    const bool use_tiled = !use_reg && !in_lds;
-    // the in-place (HBM) LDL^T overwrites S (fill-in, L in the lower triangle), and a shard's
-    // S holds the previous trial's all-reduced blocks outside its own pattern: clear S
-    const bool clearS = use_tiled || comm_ != nullptr;
+    // larger: block-sparse tiled LDL^T in HBM (ldlt.hip, structure from build_structure)
+    if (tiled_ != (n > 0 && !use_reg && !in_lds)) return -1;
+    const SysAddr sa = tiled_ ? sp_.addr() : SysAddr{dS_, n, nullptr, nullptr, 0};
     do {
         // setLambda + BlockSolver::solve
         if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
                                    lambda_, use_dev, dScal_, dEmat_, dCb_);
-        if (clearS && n) ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * (size_t)n * n, s));
+        // the in-place LDL^T overwrites S (fill-in, L), and a shard's S holds the previous
+        // trial's all-reduced blocks outside its own pattern: clear S
+        if (tiled_) {
+            if (int e = sp_.zero(s)) return e;
+        } else if (comm_ && n) {
+            ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * (size_t)n * n, s));
+        }
         if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(1024), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
-                                       lambda_, use_dev, dScal_, dS_, dBs_, own ? 1 : 0);
-        if (comm_ && nTiles_) {   // all-reduce the union-pattern tiles of S and b_s (packed)
+                                       lambda_, use_dev, dScal_, sa, dBs_, own ? 1 : 0);
+        if (comm_ && tiled_) {   // all-reduce the Schur-pattern tiles of S and b_s
+            ORB_HIP_CHECK(hipGetLastError());
+            const RedBuf rb[2] = {{sp_.tiles(), (size_t)sp_.nA() * 4096}, {dBs_, (size_t)n}};
+            if (int e = comm_->allreduce(rb, 2, RedOp::Sum, s)) return e;
+        } else if (comm_ && nTiles_) {   // all-reduce the union-pattern tiles of S and b_s (packed)
             hipLaunchKernelGGL(k_tile_pack, dim3(nTiles_), dim3(256), 0, s, n, dS_, dTiles_, dPackBuf_);
             double* pb = dPackBuf_ + (size_t)nTiles_ * 4096;
             ORB_HIP_CHECK(hipMemcpyAsync(pb, dBs_, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
@@ -2075,12 +2101,13 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
             hipLaunchKernelGGL(k_tile_unpack, dim3(nTiles_), dim3(256), 0, s, n, dS_, dTiles_, dPackBuf_);
             ORB_HIP_CHECK(hipMemcpyAsync(dBs_, pb, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
         }
-        if (use_reg)
+        if (tiled_) {
+            if (int e = sp_.solve(dBs_, dX2_, dScal_, s)) return e;
+        } else if (use_reg) {
             hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_);
-        else if (in_lds)
+        } else {
             hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds);
-        else if (int e = ldlt_tiled_solve(n, dS_, dBs_, dX2_, dScal_, dLdltWs_, s))
-            return e;
+        }
         // push + update
         if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_,
                                         dXbak_, dX2_, dHplA_, dHll_, dBl_, lambda_, use_dev, dScal_);
@@ -2266,6 +2293,14 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
 // ---------------------------------------------------------------- unit entry points
 namespace orbgpu {
 int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) {
+    if (variant == 2) {   // block-sparse tiled solver; only the upper triangle of S is read
+        std::vector<double> U((size_t)n * n, 0.0);
+        for (int i = 0; i < n; i++)
+            for (int j = i; j < n; j++) U[(size_t)i * n + j] = S[(size_t)i * n + j];
+        int ok = 0;
+        if (int e = ldlt_sparse_dense(n, U.data(), b, x, &ok, nullptr)) return e < 0 ? e : -1;
+        return ok;
+    }
     double *dS = nullptr, *dB = nullptr, *dX = nullptr, *dScal = nullptr;
     const size_t nn = (size_t)std::max(n, 1);
     ORB_HIP_CHECK(hipMalloc(&dS, sizeof(double) * nn * nn));
@@ -2275,19 +2310,10 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     ORB_HIP_CHECK(hipMemcpy(dS, S, sizeof(double) * n * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemcpy(dB, b, sizeof(double) * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemset(dX, 0, sizeof(double) * nn));
-    void* ws = nullptr;
     if (variant == 0) {
         const size_t shm = sizeof(double) * ((size_t)n * n + 14 * kLdltMax);
         if (n > kLdltMax) return -3;
         hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal);
-    } else if (variant == 2) {  // tiled: strict lower triangle must start at zero
-        std::vector<double> U((size_t)n * n, 0.0);
-        for (int i = 0; i < n; i++)
-            for (int j = i; j < n; j++) U[(size_t)i * n + j] = S[(size_t)i * n + j];
-        ORB_HIP_CHECK(hipMemcpy(dS, U.data(), sizeof(double) * U.size(), hipMemcpyHostToDevice));
-        ORB_HIP_CHECK(hipMalloc(&ws, ldlt_tiled_workspace(n)));
-        if (int e = ldlt_tiled_solve(n, dS, dB, dX, dScal, ws, 0)) return e;
-        ORB_HIP_CHECK(hipDeviceSynchronize());
     } else {
         hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), sizeof(double) * n + 16, 0, n, dS, dB, dX, dScal, 0);
     }
@@ -2296,30 +2322,18 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     ORB_HIP_CHECK(hipMemcpy(sc, dScal, sizeof(sc), hipMemcpyDeviceToHost));
     ORB_HIP_CHECK(hipMemcpy(x, dX, sizeof(double) * n, hipMemcpyDeviceToHost));
     (void)hipFree(dS); (void)hipFree(dB); (void)hipFree(dX); (void)hipFree(dScal);
-    if (ws) (void)hipFree(ws);
     return sc[3] != 0.0 ? 1 : 0;
 }
 
-// tiled factorisation only: A (n x n, upper = S) -> d on the diagonal, L in the strict lower triangle
+// tiled factorisation only: A (n x n, upper = S) -> d on the diagonal, L in the strict lower
+// triangle, the eliminated rows above
 int debug_ldlt_factor(int n, const double* S, double* out) {
     if (n <= 0) return 0;
-    double *dS = nullptr, *dB = nullptr, *dX = nullptr, *dScal = nullptr;
-    void* ws = nullptr;
-    std::vector<double> U((size_t)n * n, 0.0);
+    std::vector<double> U((size_t)n * n, 0.0), b(n, 0.0), x(n, 0.0);
     for (int i = 0; i < n; i++)
         for (int j = i; j < n; j++) U[(size_t)i * n + j] = S[(size_t)i * n + j];
-    ORB_HIP_CHECK(hipMalloc(&dS, sizeof(double) * U.size()));
-    ORB_HIP_CHECK(hipMalloc(&dB, sizeof(double) * n));
-    ORB_HIP_CHECK(hipMalloc(&dX, sizeof(double) * n));
-    ORB_HIP_CHECK(hipMalloc(&dScal, sizeof(double) * 16));
-    ORB_HIP_CHECK(hipMalloc(&ws, ldlt_tiled_workspace(n)));
-    ORB_HIP_CHECK(hipMemcpy(dS, U.data(), sizeof(double) * U.size(), hipMemcpyHostToDevice));
-    ORB_HIP_CHECK(hipMemset(dB, 0, sizeof(double) * n));
-    if (int e = ldlt_tiled_solve(n, dS, dB, dX, dScal, ws, 0)) return e;
-    ORB_HIP_CHECK(hipDeviceSynchronize());
-    ORB_HIP_CHECK(hipMemcpy(out, dS, sizeof(double) * U.size(), hipMemcpyDeviceToHost));
-    (void)hipFree(dS); (void)hipFree(dB); (void)hipFree(dX); (void)hipFree(dScal); (void)hipFree(ws);
-    return 0;
+    int ok = 0;
+    return ldlt_sparse_dense(n, U.data(), b.data(), x.data(), &ok, out);
 }
 
 __global__ void k_unit_wave_tree(const double* v, double* out) {
@@ -2330,10 +2344,10 @@ __global__ void k_unit_wave_tree(const double* v, double* out) {
 // instrumented builds only: read and clear this unit's section timers
 int debug_prof(unsigned long long* out32) {
 #ifdef ORBGPU_PROF
-    ORB_HIP_CHECK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_orbgpu_prof), sizeof(unsigned long long) * 32));
+    ORB_HIP_CHECK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_orbgpu_prof), sizeof(unsigned long long) * 16));
     unsigned long long z[32] = {};
     ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_orbgpu_prof), z, sizeof(z)));
-    return 0;
+    return ldlt_debug_prof(out32 + 16);   // ldlt.hip's timers (slots 16-23)
 #else
     (void)out32;
     return -1;

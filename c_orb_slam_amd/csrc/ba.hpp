@@ -9,6 +9,7 @@
 
 #include "../../include/orbslam_gpu.h"
 #include "comm.hpp"
+#include "ldlt.hpp"
 
 namespace orbgpu {
 
@@ -82,6 +83,8 @@ private:
     bool stopped(const volatile bool* stop) const { return comm_ ? stopRed_ : (stop && *stop); }
     int reduce_stop(const volatile bool* stop);
     bool sharded() const { return comm_ && comm_->size() > 1; }
+    // the single-workgroup dense solvers (register-resident or LDS-resident S) take n
+    bool dense_solver(int n) const;
 
     hipStream_t stream_ = nullptr;
     // problem (device)
@@ -105,7 +108,8 @@ private:
     double *dEmat_ = nullptr, *dCb_ = nullptr, *dScal_ = nullptr, *dScratch_ = nullptr, *dHplA_ = nullptr;
     double *tmpA0_ = nullptr, *tmpA1_ = nullptr, *tmpB0_ = nullptr, *tmpB1_ = nullptr;
     unsigned* dCounter_ = nullptr;
-    void* dLdltWs_ = nullptr;
+    SparseLdlt sp_;                // block-sparse pose system (n > the dense solvers' reach)
+    bool tiled_ = false;
     void* arena_ = nullptr;
     size_t arenaCap_ = 0;
     double* hScal_ = nullptr;      // pinned

@@ -41,7 +41,7 @@ int validate(const ba_problem* P, const ba_result* R) {
         if (pt < 0 || pt >= P->n_pt || kf < 0 || kf >= P->n_kf) return ORB_E_INVALID;
         if (!pairs.insert((int64_t)pt * P->n_kf + kf).second) return ORB_E_INVALID;
     }
-    if (6LL * P->n_kf > 6LL * 4096) return ORB_E_CAPACITY;
+    if (P->n_kf > 32768) return ORB_E_CAPACITY;   // block-sparse pose system: tile map (n_kf / 10.7)^2 ints
     return ORB_OK;
 }
 

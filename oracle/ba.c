@@ -423,6 +423,66 @@ int ora_ldlt_solve(double* S, int n, const double* b, double* x)
     return 1;
 }
 
+/* The same solve on envelope (profile) storage of the upper triangle, for large pose systems
+ * (a 16k-keyframe map has n = 96k: 74 GB dense).  Column c holds rows f[c]..c; f is the
+ * nondecreasing hull of the first structurally nonzero row of each column, so the LDL^T fill
+ * stays inside and row k reaches exactly the columns (k, last[k]].  Per element the operation
+ * sequence is ora_ldlt_solve's: the entries it skips are the exact zeros outside the envelope,
+ * which the dense version subtracts as 0 * S[k][j] (equal up to the sign of a zero). */
+typedef struct { int n; int* f; int* last; size_t* cs; double* v; } env_mat;
+#define ENV(E, r, c) ((E)->v[(E)->cs[c] + (size_t)((r) - (E)->f[c])])
+
+/* f: first row per column (f[c] <= c), made monotone here; allocates the zeroed storage */
+static int env_init(env_mat* E, int n, int* f)
+{
+    E->n = n;
+    E->f = f;
+    for (int c = n - 2; c >= 0; c--) if (f[c + 1] < f[c]) f[c] = f[c + 1];
+    E->cs = (size_t*)malloc(sizeof(size_t) * (n + 1));
+    E->last = (int*)malloc(sizeof(int) * (n + 1));
+    size_t t = 0;
+    for (int c = 0; c < n; c++) { E->cs[c] = t; t += (size_t)(c - f[c] + 1); }
+    E->cs[n] = t;
+    E->v = (double*)calloc(t + 1, sizeof(double));
+    int j = 0;
+    for (int k = 0; k < n; k++) {
+        if (j < k) j = k;
+        while (j + 1 < n && f[j + 1] <= k) j++;
+        E->last[k] = j;
+    }
+    return E->v != NULL;
+}
+
+static void env_free(env_mat* E) { free(E->cs); free(E->last); free(E->v); }
+
+static int ora_env_ldlt_solve(env_mat* E, const double* b, double* x)
+{
+    const int n = E->n;
+    double* l = (double*)malloc(sizeof(double) * (n + 1));
+    for (int k = 0; k < n; k++) {
+        const double d = ENV(E, k, k);
+        if (d == 0.0) { free(l); return 0; }
+        const int hi = E->last[k];
+        for (int i = k + 1; i <= hi; i++) l[i] = ENV(E, k, i) / d;
+        for (int i = k + 1; i <= hi; i++) {
+            if (l[i] == 0.0) continue;
+            for (int j = i; j <= hi; j++) ENV(E, i, j) -= l[i] * ENV(E, k, j);
+        }
+        for (int i = k + 1; i <= hi; i++) ENV(E, k, i) = l[i];   /* row k now holds L^T */
+    }
+    double* y = (double*)malloc(sizeof(double) * (n + 1));
+    memcpy(y, b, sizeof(double) * n);
+    for (int k = 0; k < n; k++)          /* L y = b (column sweep) */
+        for (int i = k + 1; i <= E->last[k]; i++) y[i] -= ENV(E, k, i) * y[k];
+    for (int k = 0; k < n; k++) y[k] = y[k] / ENV(E, k, k);
+    for (int k = n - 1; k >= 0; k--)     /* L^T x = z (column sweep) */
+        for (int i = E->f[k]; i < k; i++) y[i] -= ENV(E, i, k) * y[k];
+    memcpy(x, y, sizeof(double) * n);
+    free(y);
+    free(l);
+    return 1;
+}
+
 /* ---- the optimizer -------------------------------------------------------- */
 typedef struct {
     int nkf, npt, ne;
@@ -622,7 +682,6 @@ static int schur_solve(ba_ctx* c, double lambda)
     /* S (upper) and b_schur: terms in landmark order.  Per landmark its pose edges sorted by
      * pose (g2o's per-landmark block list); Schur block (i1 <= i2) -> its (a1, a2) pairs in
      * landmark order, so the cost is sum_l k_l^2 like the reference's BlockSolver::solve. */
-    double* S = (double*)calloc((size_t)n * n + 1, sizeof(double));
     double* bs = (double*)malloc(sizeof(double) * (n + 1));
     int* lpStart = (int*)calloc(nL + 2, sizeof(int));
     int* lpList = (int*)malloc(sizeof(int) * (c->nE + 1));
@@ -668,6 +727,18 @@ static int schur_solve(ba_ctx* c, double lambda)
                 pA[q] = lpList[u];
                 pB[q] = lpList[w];
             }
+    /* the envelope of S: per column the first row any Schur block (or the diagonal) reaches */
+    int* fcol = (int*)malloc(sizeof(int) * (n + 1));
+    for (int c = 0; c < n; c++) fcol[c] = 6 * (c / 6);
+    for (int l = 0; l < nL; l++)
+        for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
+            for (int w = u; w < lpStart[l + 1]; w++) {
+                const int i1 = POSE_OF(lpList[u]), i2 = POSE_OF(lpList[w]);
+                for (int cc = 0; cc < 6; cc++)
+                    if (6 * i1 < fcol[6 * i2 + cc]) fcol[6 * i2 + cc] = 6 * i1;
+            }
+    env_mat Env;
+    env_init(&Env, n, fcol);
     int maxM = 1;
     for (int q = 0; q < nBlk; q++) if (bStart[q + 1] - bStart[q] > maxM) maxM = bStart[q + 1] - bStart[q];
     double* v = (double*)malloc(sizeof(double) * (maxM + nL + 1));
@@ -688,7 +759,7 @@ static int schur_solve(ba_ctx* c, double lambda)
                         h = c->Hpp[21 * i1 + DIAG21[r] + (cc - r)];
                         if (cc == r) h += lambda;
                     }
-                    S[(size_t)(6 * i1 + r) * n + 6 * i2 + cc] = h - ora_csum(v, m);
+                    ENV(&Env, 6 * i1 + r, 6 * i2 + cc) = h - ora_csum(v, m);
                 }
         }
     /* b_schur: per pose, its landmarks' terms in landmark order */
@@ -711,7 +782,7 @@ static int schur_solve(ba_ctx* c, double lambda)
         free(psStart); free(psList); free(pf);
     }
     double* xp = (double*)malloc(sizeof(double) * (n + 1));
-    int ok = n == 0 ? 1 : ora_ldlt_solve(S, n, bs, xp);
+    int ok = n == 0 ? 1 : ora_env_ldlt_solve(&Env, bs, xp);
     if (ok) {
         memcpy(c->x, xp, sizeof(double) * n);
         /* xl = Dinv (bl - sum_i B_i^T xp_i); rightMultiply over the landmark's blocks in pose order */
@@ -734,7 +805,8 @@ static int schur_solve(ba_ctx* c, double lambda)
     }
 #undef POSE_OF
     free(lpStart); free(lpList); free(blkOf); free(bStart); free(pA); free(pB); free(fill);
-    free(xp); free(v); free(S); free(bs); free(E); free(cb); free(Dinv); free(db);
+    env_free(&Env); free(fcol);
+    free(xp); free(v); free(bs); free(E); free(cb); free(Dinv); free(db);
     return ok;
 }
 
