@@ -310,6 +310,9 @@ int   ora_pose_optimization(const ora_pose_problem* P, float* Tcw_out, uint8_t* 
 int   ora_ldlt_pivot_solve(double* H, int n, const double* b, double* x);
 double ora_csum(double* v, int n);
 int   ora_ldlt_solve(double* S, int n, const double* b, double* x);
+enum { ORA_BA_CANONICAL = 0, ORA_BA_G2O = 1 };
+void  ora_ba_set_order(int mode);   /* accumulation order of the BA / pose oracle (ba.c) */
+int   ora_ba_get_order(void);
 int   ora_local_ba(const ora_ba_problem* P, const volatile int* stop, ora_ba_result* R, ora_ba_trace* trace);
 /* Optimizer::BundleAdjustment (Optimizer.cc:49-237): all keyframes vertices (fixed iff id 0),
  * one optimize(nIterations), Huber sqrt(5.99)/sqrt(7.815) iff bRobust, no gating. */

@@ -414,6 +414,24 @@ class _BAResult(C.Structure):
                 ("iterations", C.c_int * 2), ("n_erased", C.c_int), ("aborted", C.c_int)]
 
 
+class ba_order:
+    """Context manager: run the BA / PoseOptimization oracle in the given accumulation order,
+    "g2o" (the reference's sequential += order) or "canonical" (the GPU's tree order)."""
+
+    def __init__(self, mode):
+        self.mode = {"canonical": 0, "g2o": 1}[mode]
+
+    def __enter__(self):
+        L = lib()
+        L.ora_ba_get_order.restype = C.c_int
+        self.prev = L.ora_ba_get_order()
+        L.ora_ba_set_order(self.mode)
+        return self
+
+    def __exit__(self, *a):
+        lib().ora_ba_set_order(self.prev)
+
+
 class _BATrace(C.Structure):
     _fields_ = [("n_solves", C.c_int), ("n_trials", C.c_int), ("solve_ini_chi2", C.c_double * 256),
                 ("solve_chi2", C.c_double * 256), ("trial_chi2", C.c_double * 256),
