@@ -36,6 +36,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md (spec)
 ROOFLINE_REPS = 5
 TRAFFIC_FILE = "traffic_r01.json"   # PMC FETCH_SIZE/WRITE_SIZE per launch (tools/pmc_traffic.py)
 VALU_FILE = "valu_r01.json"   # PMC SQ_INSTS_VALU per launch (tools/pmc_valu.py)
+MATCH_PMC_FILE = "match_pmc_r02.json"   # matcher kernels: HBM bytes and VALU instructions per launch (tools/pmc_match.py)
 VALU_PEAK_GINST = 1228.8   # 256 CUs x 2 wave64 VALU issues per cycle x 2.4 GHz (MI355X_MICROARCH.md)
 W, H, NFEAT = 1241, 376, 1200
 
@@ -55,6 +56,8 @@ def parse():
     ap.add_argument("--gba-kf", type=int, default=2000,
                     help="keyframes of the sharded global-BA problem (SURVEY config 5: 2k, 8k, 16k)")
     ap.add_argument("--gba-reps", type=int, default=3)
+    ap.add_argument("--passes-only", action="store_true",
+                    help="only the isolated roofline passes (extraction + matcher kernels), for rocprofv3 --pmc runs")
     return ap.parse_args()
 
 
@@ -254,17 +257,17 @@ def main():
                                            np.int32)
             self.nR = np.ascontiguousarray(fR.result(), np.int32)
 
-        def track(self):
-            """ComputeStereoMatches, UpdateLastFrame, SearchByProjection(Cur, Last, 7), PoseOptimization."""
-            t1 = time.perf_counter()
+        def stereo(self):
             nL, nR = self.nL, self.nR
             check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, self.exL._h, self.exR._h, B, ptr(nL), self.s_kL,
                                                           self.s_dL, ptr(nR), self.s_kR, self.s_dR, float(mbf),
                                                           float(mb), self.s_uR, self.s_dep, ptr(self.nst)),
                   "ComputeStereoMatches batch")
-            t2 = time.perf_counter()
+
+        def search(self):
             # UpdateLastFrame (Frame::UnprojectStereo) and the current frames' empty mvpMapPoints, on
             # the matcher's stream ahead of the search
+            nL = self.nL
             self.n_unp[:] = nL
             self.n_cur[:] = nL[1:]
             self.n_last[:] = nL[:-1]
@@ -278,6 +281,14 @@ def main():
                                                                   self.a_last_kps, self.a_last_mp, self.a_last_out,
                                                                   self.mps, 7.0, 0, ptr(self.nm)),
                   "SearchByProjection batch")
+
+        def track(self):
+            """ComputeStereoMatches, UpdateLastFrame, SearchByProjection(Cur, Last, 7), PoseOptimization."""
+            t1 = time.perf_counter()
+            nL, nR = self.nL, self.nR
+            self.stereo()
+            t2 = time.perf_counter()
+            self.search()
             t3 = time.perf_counter()
             # Optimizer::PoseOptimization(&mCurrentFrame) (Tracking.cc:887) on the matched map points
             check(L.Optimizer_PoseOptimization_frames_device(P, self.pframes, self.a_Tout, self.a_poutl,
@@ -292,6 +303,94 @@ def main():
             kernel_ms.append(tr["fast_cells"])
             pose_inl.append(int(self.ninl.sum()))
             return int(nL.sum() + nR.sum()), int(self.nm.sum()), int(self.nst.sum())
+
+    def matcher_pass(lane, reps):
+        """Isolated matcher launches with device timing and work counters:
+        algorithmic bytes per SURVEY §8d = 32 B streamed candidate descriptor + 4 B index per
+        scored pair + 16 B per query (query descriptor held in registers)."""
+        check(L.ORBmatcher_enable_timing(m._h, 1), "ORBmatcher_enable_timing")
+        ms = np.zeros(8, np.float32)
+        cnt = np.zeros(8, np.int64)
+        acc = {k: [] for k in ("k_build_grid", "k_candidates", "k_select", "k_stereo_rows", "k_stereo_match",
+                               "k_stereo_filter", "k_csr_hamming")}
+        work = {k: [] for k in ("search_pairs", "search_queries", "stereo_pairs", "stereo_queries", "csr_pairs",
+                                "csr_queries")}
+
+        def grab(kernels, counters):
+            check(L.ORBmatcher_last_timings(m._h, ms.ctypes.data, cnt.ctypes.data), "ORBmatcher_last_timings")
+            for k, i in kernels:
+                acc[k].append(float(ms[i]))
+            for k, i in counters:
+                work[k].append(int(cnt[i]))
+
+        # dense tiles: frame b's left descriptors against frame b+1's (16 pairs of ~1200 x 1200)
+        B2 = min(16, B - 1)
+        nL = lane.nL
+        qd = torch.cat([lane.d_desc[b, :nL[b]] for b in range(B2)]).contiguous()
+        td = torch.cat([lane.d_desc[b + 1, :nL[b + 1]] for b in range(B2)]).contiguous()
+        tbase = np.concatenate([[0], np.cumsum(nL[1:B2 + 1])])[:B2]
+        cand = torch.cat([(int(tbase[b]) + torch.arange(int(nL[b + 1]), dtype=torch.int32, device=dev)).repeat(int(nL[b]))
+                          for b in range(B2)]).contiguous()
+        per_q = torch.cat([torch.full((int(nL[b]),), int(nL[b + 1]), dtype=torch.int32, device=dev) for b in range(B2)])
+        off = torch.zeros(len(per_q) + 1, dtype=torch.int32, device=dev)
+        off[1:] = torch.cumsum(per_q, 0)
+        nq = len(per_q)
+        dist = torch.empty(len(cand), dtype=torch.int32, device=dev)
+        bi, bd, sd = (torch.empty(nq, dtype=torch.int32, device=dev) for _ in range(3))
+        torch.cuda.synchronize()
+        for _ in range(reps):
+            lane.stereo()
+            grab((("k_stereo_rows", 3), ("k_stereo_match", 4), ("k_stereo_filter", 5)),
+                 (("stereo_pairs", 2), ("stereo_queries", 3)))
+            lane.search()
+            grab((("k_build_grid", 0), ("k_candidates", 1), ("k_select", 2)),
+                 (("search_pairs", 0), ("search_queries", 1)))
+            check(L.ORBmatcher_SearchCandidates(m._h, C.c_void_p(qd.data_ptr()), nq, C.c_void_p(td.data_ptr()),
+                                                len(td), C.c_void_p(off.data_ptr()), C.c_void_p(cand.data_ptr()),
+                                                C.c_void_p(dist.data_ptr()), C.c_void_p(bi.data_ptr()),
+                                                C.c_void_p(bd.data_ptr()), C.c_void_p(sd.data_ptr())), "SearchCandidates")
+            grab((("k_csr_hamming", 6),), (("csr_pairs", 4), ("csr_queries", 5)))
+        check(L.ORBmatcher_enable_timing(m._h, 0), "ORBmatcher_enable_timing")
+        pmc = {}
+        pf = ROOT / "profiles" / MATCH_PMC_FILE
+        if pf.exists():
+            try:
+                pmc = json.loads(pf.read_text())
+            except Exception:
+                pmc = {}
+        out = {}
+        for k, pk, qk in (("k_candidates", "search_pairs", "search_queries"), ("k_stereo_match", "stereo_pairs",
+                                                                               "stereo_queries"),
+                          ("k_csr_hamming", "csr_pairs", "csr_queries")):
+            t = float(np.mean(acc[k]))
+            pairs, qs = float(np.mean(work[pk])), float(np.mean(work[qk]))
+            alg = pairs * 36 + qs * 16
+            gbs = alg / (t * 1e-3) / 1e9
+            e = {"avg_launch_ms": round(t, 4), "pairs_per_launch": int(pairs), "queries_per_launch": int(qs),
+                 "alg_bytes_per_launch": int(alg), "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(gbs / HBM_PEAK_GBS, 5), "pairs_per_s": round(pairs / (t * 1e-3), 1)}
+            if k in pmc:
+                e["traffic"] = pmc[k].get("hbm_bytes_per_launch")
+                if e["traffic"]:   # what HBM actually moved (descriptor re-reads are L2/MALL hits)
+                    e["hbm_achieved"] = round(e["traffic"] / (t * 1e-3) / 1e9, 2)
+                    e["hbm_frac"] = round(e["hbm_achieved"] / HBM_PEAK_GBS, 5)
+                vi = pmc[k].get("valu_insts_per_launch")
+                if vi:
+                    vr = vi / (t * 1e-3) / 1e9
+                    e["valu"] = {"insts_per_launch": int(vi), "achieved": round(vr, 1), "peak": VALU_PEAK_GINST,
+                                 "unit": "G wave-instr/s", "frac": round(vr / VALU_PEAK_GINST, 4)}
+                e["pmc_source"] = f"profiles/{MATCH_PMC_FILE}"
+            out[k] = e
+        out["k_csr_hamming"]["workload"] = f"dense tiles: {B2} frame pairs, every left descriptor of frame b against " \
+                                           f"every left descriptor of frame b+1 (SURVEY config 2 (ii))"
+        for k in ("k_build_grid", "k_select", "k_stereo_rows", "k_stereo_filter"):
+            out[k] = {"avg_launch_ms": round(float(np.mean(acc[k])), 4), "bound": "latency (one workgroup per frame)"}
+        out["definition"] = ("alg bytes = 36 B per scored (query, candidate) pair (32 B candidate descriptor + 4 B "
+                             "index) + 16 B per query, SURVEY §8d; duration = HIP events on the matcher stream, "
+                             f"mean of {reps} isolated launches; hbm_achieved = PMC HBM bytes per launch / duration "
+                             "(the candidate descriptors of a frame are re-read from L2/MALL, so alg bytes exceed "
+                             "HBM traffic: the dense tile's 36 B/pair run at L2 rate)")
+        return out
 
     stage_acc = {}
     phase_acc = {}
@@ -328,6 +427,8 @@ def main():
             state["ready"].track()
             state["ready"] = None
 
+    if args.passes_only:   # one extracted, tracked batch; then only the isolated passes below
+        args.warmup, args.steps = 1, 0
     for _ in range(args.warmup):
         step()
     drain()
@@ -409,6 +510,14 @@ def main():
             "avg_launch_ms_in_pipeline": round(float(np.mean(kernel_ms)), 4),
             "secondary_bound": "VALU (16-px circle test; DESIGN.md §3)", "valu": valu}
 
+    # matcher roofline (north star: "achieved HBM GB/s for the matcher ... against the chip's
+    # peak"): the ready lane's ComputeStereoMatches and SearchByProjection batches and a dense
+    # 1200x1200 descriptor tile per frame pair (SURVEY config 2 (ii)) through the CSR engine,
+    # each ROOFLINE_REPS times with nothing else in flight, HIP events on the matcher stream
+    mroof = matcher_pass(lanes[0], ROOFLINE_REPS)
+    if args.passes_only:
+        return
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(lefts, rights, Rs, args.cpu_seconds)
@@ -438,7 +547,8 @@ def main():
             "keypoints_per_image": round(tot_kp / (2 * frames_total), 1),
             "pose_inliers_per_frame": round(float(np.sum(pose_inl)) / max(len(pose_inl) * P, 1), 1),
             "stage_ms_per_step": stage_ms,
-            "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}, "roofline": roof, "cpu_baseline": cpu, "local_ba": ba,
+            "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}, "roofline": roof,
+            "matcher_roofline": mroof, "cpu_baseline": cpu, "local_ba": ba,
             "global_ba": gba,
         }
         json_out.write(json.dumps(out) + "\n")
@@ -527,37 +637,114 @@ def bench_global_ba(args, world, rank, dist, dev):
             "dtype": "f64 (f32 I/O)"}
 
 
-def gba_cpu_baseline(n_kf):
-    """Oracle BundleAdjustment (C restatement of the g2o path, 1 thread) on the same problem, one call."""
+_ORACLE_TIMING = {}
+
+
+def timing_oracle():
+    """The oracle as SURVEY §8d times it: a separate build with the reference's own flags
+    (CMakeLists.txt:10-11: -O3 -march=native, FP contraction allowed), compiled on this host at
+    run time (-march=native must see the CPU that runs it); the -ffp-contract=off -O2 build stays
+    the parity oracle.  Loads it into tests/oracle_lib and returns the flags used."""
+    if _ORACLE_TIMING:
+        return _ORACLE_TIMING["flags"]
+    import subprocess
+    import tempfile
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    src = ROOT / "oracle"
+    out = Path(tempfile.gettempdir()) / f"liborb_oracle_timing_{os.getpid()}.so"
+    flags = ["-O3", "-march=native", "-std=gnu11", "-fPIC"]
+    srcs = [str(src / f) for f in ("ocv_semantics.c", "orb_extract.c", "orb_match.c", "rng.c", "linalg.c", "pnp.c",
+                                   "sim3.c", "ba.c", "stereo.c", "matchers2.c", "matchers3.c", "dbow2.c")]
+    try:
+        subprocess.run(["gcc"] + flags + ["-shared", "-o", str(out)] + srcs + ["-lm"], check=True,
+                       capture_output=True, timeout=300)
+        oracle_lib.use_library(out)
+        _ORACLE_TIMING["flags"] = " ".join(flags)
+    except Exception as e:  # noqa: BLE001 -- fall back to the parity build, say so
+        _ORACLE_TIMING["flags"] = f"-O2 -ffp-contract=off (timing build failed: {type(e).__name__})"
+    return _ORACLE_TIMING["flags"]
+
+
+def cpu_share():
+    """Host cores this process may use: the affinity set, capped by a cgroup CPU quota (a GPU
+    box shares its host; nproc shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def _streams(P, fn):
+    """Run fn(i) on P threads at once (the oracle's C calls release the GIL); wall of the slowest."""
+    from concurrent.futures import ThreadPoolExecutor
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(P) as ex:
+        res = list(ex.map(fn, range(P)))
+    return res, time.perf_counter() - t0
+
+
+def gba_cpu_baseline(n_kf, n_its=10):
+    """Oracle BundleAdjustment(nIterations=10, bRobust=false) on the same config-5 problem: one
+    full call per stream, P independent streams (all-core) and the single stream alongside."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
     from ba_cases import global_ba_problem
+    flags = timing_oracle()
     pr = global_ba_problem(0, n_kf=n_kf, pts_per_kf=150)
     t0 = time.perf_counter()
-    o = oracle_lib.oracle_global_ba(pr, 2, False)   # bounded sample: the first 2 LM solves of the same call
-    dt = time.perf_counter() - t0
-    return {"value": round(o["iterations"][0] / dt, 3), "unit": "iter/s", "cores": 1, "kind": "port",
-            "sample": f"BundleAdjustment(nIterations=2) on the same config-5 problem ({n_kf} KFs), "
-                      f"oracle/ba.c -O2 (sparse Schur, envelope LDL^T), 1 thread"}
+    o = oracle_lib.oracle_global_ba(pr, n_its, False)
+    dt1 = time.perf_counter() - t0
+    P, aff, quota = cpu_share()
+    # one full call per stream; memory per stream ~ the problem's, bounded
+    P = max(1, min(P, 8))
+    res, wall = _streams(P, lambda i: oracle_lib.oracle_global_ba(pr, n_its, False)["iterations"][0])
+    return {"value": round(sum(res) / wall, 3), "unit": "iter/s", "cores": P, "kind": "port",
+            "sample": f"{P} independent oracle BundleAdjustment(nIterations={n_its}) calls on the same config-5 "
+                      f"problem ({n_kf} KFs) on {P} threads ({_cpu_model()}; affinity {aff}, cgroup quota {quota}), "
+                      f"oracle/ba.c {flags} (sparse Schur, envelope LDL^T); {sum(res)} LM solves in {wall:.1f} s",
+            "single_thread": {"value": round(o["iterations"][0] / dt1, 3), "unit": "iter/s", "cores": 1,
+                              "sample": f"one full call, {o['iterations'][0]} LM solves in {dt1:.1f} s"}}
 
 
 def ba_cpu_baseline(budget_s):
-    """Oracle LocalBundleAdjustment (C restatement of the g2o path, 1 thread) on the same problem."""
+    """Oracle LocalBundleAdjustment on the same config-4 problem: P independent streams of whole
+    calls (all-core) and one stream alongside."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
     from ba_cases import ba_problem
+    flags = timing_oracle()
     pr = ba_problem(0)
-    t0 = time.perf_counter()
-    its = calls = 0
-    while True:
-        o = oracle_lib.oracle_local_ba(pr)
-        its += sum(o["iterations"])
-        calls += 1
-        if time.perf_counter() - t0 > budget_s and calls >= 2:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(its / dt, 2), "unit": "iter/s", "cores": 1, "kind": "port",
-            "sample": f"{calls} LocalBundleAdjustment calls on config 4 ({its} LM solves), oracle/ba.c -O2, 1 thread"}
+
+    def stream(i, budget):
+        t0 = time.perf_counter()
+        its = calls = 0
+        while True:
+            o = oracle_lib.oracle_local_ba(pr)
+            its += sum(o["iterations"])
+            calls += 1
+            if time.perf_counter() - t0 > budget and calls >= 2:
+                return its, calls, time.perf_counter() - t0
+
+    its1, calls1, dt1 = stream(0, budget_s / 2)
+    P, aff, quota = cpu_share()
+    res, wall = _streams(P, lambda i: stream(i, budget_s / 2))
+    its = sum(r[0] for r in res)
+    calls = sum(r[1] for r in res)
+    return {"value": round(its / max(r[2] for r in res), 2), "unit": "iter/s", "cores": P, "kind": "port",
+            "sample": f"{P} independent streams of LocalBundleAdjustment calls on config 4 on {P} threads "
+                      f"({_cpu_model()}; affinity {aff}, cgroup quota {quota}): {calls} calls, {its} LM solves; "
+                      f"oracle/ba.c {flags}",
+            "single_thread": {"value": round(its1 / dt1, 2), "unit": "iter/s", "cores": 1,
+                              "sample": f"{calls1} calls ({its1} LM solves) on 1 thread"}}
 
 
 class _CpuStream:
@@ -639,26 +826,23 @@ def _cpu_model():
 def cpu_baseline(lefts, rights, Rs, budget_s):
     """The oracle timed on the host cores on a bounded sample of the same workload:
     (i) one reference-structured stream on 1 thread; (ii) P independent streams on P threads
-    (P = this box's CPU share, at most 16) -> whole-host frames/s, the figure `value` reports."""
-    from concurrent.futures import ThreadPoolExecutor
+    (P = the cores this process may use: affinity capped by the cgroup quota) -> whole-host
+    frames/s, the figure `value` reports.  Timing build of the oracle (-O3 -march=native)."""
+    flags = timing_oracle()
     one = _CpuStream(lefts, rights, Rs)
     one.run(0, budget_s / 2, 4)
     fps1 = one.done / sum(one.t.values())
-    try:
-        share = len(os.sched_getaffinity(0))
-    except AttributeError:
-        share = os.cpu_count() or 1
-    P = max(1, min(16, share))
+    P, aff, quota = cpu_share()
     streams = [_CpuStream(lefts, rights, Rs) for _ in range(P)]
-    with ThreadPoolExecutor(P) as ex:
-        walls = list(ex.map(lambda a: a[1].run(a[0] * 7, budget_s / 2, 2), enumerate(streams)))
+    walls, _ = _streams(P, lambda i: streams[i].run(i * 7, budget_s / 2, 2))
     framesP = sum(s.done for s in streams)
     fpsP = framesP / max(walls)
     t = one.t
     return {"value": round(fpsP, 3), "unit": "frames/s", "cores": P, "kind": "port",
-            "sample": f"{P} independent reference-structured streams on {P} threads ({_cpu_model()}): oracle "
-                      f"ORBextractor x2 + ComputeStereoMatches + SearchByProjection(Cur,Last,7) + PoseOptimization "
-                      f"per stereo frame, -O2 C restatement; {framesP} frames in {max(walls):.1f} s",
+            "sample": f"{P} independent reference-structured streams on {P} threads ({_cpu_model()}; affinity {aff}, "
+                      f"cgroup quota {quota}): oracle ORBextractor x2 + ComputeStereoMatches + "
+                      f"SearchByProjection(Cur,Last,7) + PoseOptimization per stereo frame, C restatement built "
+                      f"{flags}; {framesP} frames in {max(walls):.1f} s",
             "single_thread": {"value": round(fps1, 3), "unit": "frames/s", "cores": 1,
                               "sample": f"{one.done} frames on 1 thread: extract {t['extract'] / one.done * 1e3:.1f} "
                                         f"ms/frame, stereo {t['stereo'] / one.done * 1e3:.2f} ms, match "

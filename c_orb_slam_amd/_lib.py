@@ -158,6 +158,9 @@ def lib():
     L.ORBvocabulary_score.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp, vp]
     L.orbgpu_unit_ldlt_solve.argtypes = [i32, vp, vp, vp, i32, P(i32)]
     L.orbgpu_unit_csum.argtypes = [vp, i32, vp]
+    L.orbgpu_unit_pnp_layout.argtypes = [i32, vp, vp, vp, vp]
+    L.ORBmatcher_enable_timing.argtypes = [vp, i32]
+    L.ORBmatcher_last_timings.argtypes = [vp, vp, vp]
     L.orbgpu_unit_ldlt_factor.argtypes = [i32, vp, vp]
     L.orbgpu_unit_wave_tree.argtypes = [vp, vp]
     L.orbgpu_debug_prof.argtypes = [vp]

@@ -96,6 +96,16 @@ int ORBmatcher_set_device_pointers(ORBmatcher_h h, int on) {
 
 void* ORBmatcher_stream(ORBmatcher_h h) { return h ? (void*)h->m->stream() : nullptr; }
 
+int ORBmatcher_enable_timing(ORBmatcher_h h, int on) {
+    if (!h) return ORB_E_INVALID;
+    return h->m->set_timing(on != 0) ? ORB_E_HIP : ORB_OK;
+}
+
+int ORBmatcher_last_timings(ORBmatcher_h h, float* ms8, long long* counts8) {
+    if (!h || !ms8 || !counts8) return ORB_E_INVALID;
+    return h->m->timings(ms8, counts8) ? ORB_E_HIP : ORB_OK;
+}
+
 // ORBmatcher.cc:1647-1663 (SWAR popcount == popcount)
 int ORBmatcher_DescriptorDistance(const uint8_t* a, const uint8_t* b) {
     if (!a || !b) return ORB_E_INVALID;

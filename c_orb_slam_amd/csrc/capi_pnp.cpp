@@ -113,4 +113,9 @@ int PnPsolver_iterate(PnPsolver_h h, int nIterations, orb_rng* rng, int* bNoMore
     return PnPsolver_iterate_batch(1, &h, nIterations, &rng, bNoMore, &inliers, nInliers, Tcw, has_pose);
 }
 
+int orbgpu_unit_pnp_layout(int n, const int* N, const int* K, const int* minSet, long long* out4) {
+    if (n < 0 || (n > 0 && (!N || !K || !minSet)) || !out4) return ORB_E_INVALID;
+    return orbgpu::pnp_layout_check(n, N, K, minSet, out4) ? ORB_E_CAPACITY : ORB_OK;
+}
+
 }  // extern "C"

@@ -117,7 +117,7 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
     if (hipMemcpyAsync(d_probs, probs.data(), sizeof(orbgpu::StereoDev) * npairs, hipMemcpyHostToDevice, s) !=
         hipSuccess)
         return ORB_E_HIP;
-    if (orbgpu::stereo_launch(d_probs, npairs, maxNL, P, s)) return ORB_E_HIP;
+    if (orbgpu::stereo_launch(d_probs, npairs, maxNL, P, s, m)) return ORB_E_HIP;
     if (hipMemcpyAsync(nmatches, d_kept, 4 * (size_t)npairs, hipMemcpyDeviceToHost, s) != hipSuccess)
         return ORB_E_HIP;
     if (!dev)

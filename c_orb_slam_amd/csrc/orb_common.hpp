@@ -126,6 +126,12 @@ __device__ __forceinline__ int wave_sum(int v) {
 // Issue priority of a latency-critical wave over co-resident bulk waves on its SIMD.
 #define ORBGPU_LATENCY_WAVE() __builtin_amdgcn_s_setprio(3)
 
+// sum over the 64 lanes of a wave (every lane active), result in every lane
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 }  // namespace orbgpu
 
 // Section timers for instrumented builds (make prof -> -DORBGPU_PROF): clock64() deltas of

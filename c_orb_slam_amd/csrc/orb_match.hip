@@ -292,15 +292,17 @@ __device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked block
 
 // Parallel phase: one thread per query.
 template <bool LAST>
-__global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict__ probs, float th, int bMono) {
+__global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict__ probs, float th, int bMono,
+                                                    unsigned long long* counters) {
     ORBGPU_LATENCY_WAVE();
     const SearchDev P = probs[blockIdx.y];
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= P.nq) return;
+    if (!counters && q >= P.nq) return;
     int2 top[kTopK];
     int cnt = -1;
     auto never = [](int) { return false; };
-    if (LAST) {
+    if (q >= P.nq) {   // measurement only: the wave stays whole for its counter sums
+    } else if (LAST) {
         bool bF, bB;
         fwd_bwd(P, bMono != 0, bF, bB);
         const LastQuery lq = last_query(P, q, th, bF, bB);
@@ -309,9 +311,20 @@ __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict_
         const LocalQuery lq = local_query(P, q, th);
         if (lq.valid) cnt = scan_local(P, lq, never, top, kTopK);
     }
-    P.qinfo[q] = make_int4(cnt, 0, 0, 0);
-    const int kk = cnt < kTopK ? cnt : kTopK;
-    for (int k = 0; k < kk; k++) P.topk[(size_t)q * kTopK + k] = top[k];
+    if (q < P.nq) {
+        P.qinfo[q] = make_int4(cnt, 0, 0, 0);
+        const int kk = cnt < kTopK ? cnt : kTopK;
+        for (int k = 0; k < kk; k++) P.topk[(size_t)q * kTopK + k] = top[k];
+    }
+    if (counters) {   // measurement: scored pairs and windowed queries
+        const unsigned long long pr = wave_sum_u64(cnt > 0 ? (unsigned long long)cnt : 0ull);
+        const unsigned long long nqv = wave_sum_u64(cnt >= 0 ? 1ull : 0ull);
+        if ((threadIdx.x & 63) == 0) {
+            const int sl = (blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 6)) & (kCountSlots - 1);
+            atomicAdd(&counters[0 * kCountSlots + sl], pr);
+            atomicAdd(&counters[1 * kCountSlots + sl], nqv);
+        }
+    }
 }
 
 // Greedy replay as a fixed-point iteration (one 256-thread workgroup per problem).
@@ -487,7 +500,8 @@ __global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ pr
 __global__ void __launch_bounds__(256) k_csr_hamming(const uint8_t* __restrict__ q, int nq, const uint8_t* __restrict__ t,
                                                      const int* __restrict__ off, const int* __restrict__ cand,
                                                      int* __restrict__ dist, int* __restrict__ best_idx,
-                                                     int* __restrict__ best_dist, int* __restrict__ second_dist) {
+                                                     int* __restrict__ best_dist, int* __restrict__ second_dist,
+                                                     unsigned long long* counters) {
     const int lane = threadIdx.x & 63;
     const int qi = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (qi >= nq) return;
@@ -511,6 +525,11 @@ __global__ void __launch_bounds__(256) k_csr_hamming(const uint8_t* __restrict__
         k2 = n2;
     }
     if (lane == 0) {
+        if (counters) {
+            const int sl = blockIdx.x & (kCountSlots - 1);
+            atomicAdd(&counters[4 * kCountSlots + sl], (unsigned long long)(e - b));
+            atomicAdd(&counters[5 * kCountSlots + sl], 1ull);
+        }
         best_idx[qi] = k1 == ~0ull ? -1 : cand[b + (int)(k1 & 0xffffffffu)];
         best_dist[qi] = k1 == ~0ull ? 256 : (int)(k1 >> 32);
         second_dist[qi] = k2 == ~0ull ? 256 : (int)(k2 >> 32);
@@ -597,6 +616,9 @@ int Matcher::area_candidates(const SearchDev& frame, const AreaQuery* d_q, int n
 
 // --------------------------------------------------------------------- host
 Matcher::~Matcher() {
+    for (int i = 0; i < 16; i++)
+        if (ev_[i]) (void)hipEventDestroy(ev_[i]);
+    if (d_count_) (void)hipFree(d_count_);
     if (d_cand_) (void)hipFree(d_cand_);
     if (d_scratch_) (void)hipFree(d_scratch_);
     if (d_probs_) (void)hipFree(d_probs_);
@@ -665,18 +687,30 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     }
     ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, probs.data(), pb, hipMemcpyHostToDevice, stream_));
     SearchDev* dp = (SearchDev*)d_probs_;
+    if (timing_) {
+        if (int e = zero_counters(0, 2)) return e;
+        mark(0);
+    }
     hipLaunchKernelGGL(k_build_grid, dim3(np), dim3(256), grid_lds_bytes(maxN), stream_, dp);
+    mark(1);
     if (maxq > 0) {
         if (lastMode) {
-            hipLaunchKernelGGL(k_candidates<true>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, (int)bMono);
+            hipLaunchKernelGGL(k_candidates<true>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, (int)bMono,
+                               counters());
+            mark(2);
             hipLaunchKernelGGL(k_select<true>, dim3(np), dim3(256), select_lds_bytes(maxN), stream_, dp, th, (int)bMono,
                                nnratio_, (int)checkOri_, maxN);
         } else {
-            hipLaunchKernelGGL(k_candidates<false>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0);
+            hipLaunchKernelGGL(k_candidates<false>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0,
+                               counters());
+            mark(2);
             hipLaunchKernelGGL(k_select<false>, dim3(np), dim3(256), select_lds_bytes(maxN), stream_, dp, th, 0,
                                nnratio_, 0, maxN);
         }
+    } else {
+        mark(2);
     }
+    mark(3);
     ORB_HIP_CHECK(hipGetLastError());
     return 0;
 }
@@ -688,9 +722,58 @@ int Matcher::candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, cons
                         int* best_idx, int* best_dist, int* second_dist) {
     (void)nt;
     if (nq <= 0) return 0;
+    if (timing_) {
+        if (int e = zero_counters(4, 2)) return e;
+        mark(12);
+    }
     hipLaunchKernelGGL(k_csr_hamming, dim3((nq + 3) / 4), dim3(256), 0, stream_, q, nq, t, off, cand, dist, best_idx,
-                       best_dist, second_dist);
+                       best_dist, second_dist, counters());
+    mark(13);
     ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int Matcher::set_timing(bool on) {
+    if (on && !d_count_) {
+        for (int i = 0; i < 16; i++) ORB_HIP_CHECK(hipEventCreate(&ev_[i]));
+        ORB_HIP_CHECK(hipMalloc(&d_count_, sizeof(unsigned long long) * 8 * kCountSlots));
+        ORB_HIP_CHECK(hipMemset(d_count_, 0, sizeof(unsigned long long) * 8 * kCountSlots));
+    }
+    timing_ = on;
+    return 0;
+}
+
+void Matcher::mark(int i) {
+    if (!timing_) return;
+    (void)hipEventRecord(ev_[i], stream_);
+    evSet_[i] = true;
+}
+
+int Matcher::zero_counters(int first, int n) {
+    ORB_HIP_CHECK(hipMemsetAsync(d_count_ + (size_t)first * kCountSlots, 0, sizeof(unsigned long long) * n * kCountSlots,
+                                 stream_));
+    return 0;
+}
+
+// events: search 0..3 (grid | candidates | select), stereo 4..7 (rows | match | filter), CSR 12..13
+int Matcher::timings(float* ms8, long long* cnt8) {
+    for (int i = 0; i < 8; i++) {
+        ms8[i] = -1.0f;
+        cnt8[i] = -1;
+    }
+    if (!d_count_) return 0;
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    const int pairs[7][2] = {{0, 1}, {1, 2}, {2, 3}, {4, 5}, {5, 6}, {6, 7}, {12, 13}};
+    for (int k = 0; k < 7; k++) {
+        const int a = pairs[k][0], b = pairs[k][1];
+        if (evSet_[a] && evSet_[b]) (void)hipEventElapsedTime(&ms8[k], ev_[a], ev_[b]);
+    }
+    std::vector<unsigned long long> c(8 * kCountSlots);
+    ORB_HIP_CHECK(hipMemcpy(c.data(), d_count_, sizeof(unsigned long long) * c.size(), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 8; i++) {
+        cnt8[i] = 0;
+        for (int k = 0; k < kCountSlots; k++) cnt8[i] += (long long)c[(size_t)i * kCountSlots + k];
+    }
     return 0;
 }
 

@@ -65,6 +65,8 @@ struct AreaQuery {
     int qd;
 };
 
+constexpr int kCountSlots = 64;   // measurement counters: kCountSlots addresses per counter
+
 class Matcher {
 public:
     Matcher(float nnratio, bool checkOri) : nnratio_(nnratio), checkOri_(checkOri) {}
@@ -89,6 +91,19 @@ public:
     int arena_reserve(size_t bytes);
     void* arena_alloc(size_t bytes);
 
+    // Measurement (bench roofline): with timing on, the search / stereo / CSR launches record
+    // HIP events on stream() around each kernel and count their work units on the device.
+    //   ms[0..7]:  k_build_grid, k_candidates, k_select, k_stereo_rows, k_stereo_match,
+    //              k_stereo_filter, k_csr_hamming, (spare)
+    //   cnt[0..7]: search (query, candidate) pairs scored, search queries with a window,
+    //              stereo (left, right) pairs scored, stereo left keypoints, CSR pairs, CSR queries
+    int set_timing(bool on);
+    bool timing() const { return timing_; }
+    int timings(float* ms8, long long* cnt8);
+    void mark(int i);   // record event i on stream() (timing on)
+    unsigned long long* counters() const { return timing_ ? d_count_ : nullptr; }
+    int zero_counters(int first, int n);
+
 private:
     int run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastMode);
     float nnratio_;
@@ -103,6 +118,10 @@ private:
     size_t arena_cap_ = 0, arena_used_ = 0;
     void* d_cand_ = nullptr;
     size_t cand_cap_ = 0;
+    bool timing_ = false;
+    hipEvent_t ev_[16] = {};
+    bool evSet_[16] = {};
+    unsigned long long* d_count_ = nullptr;
 };
 
 int debug_prof_match(unsigned long long* out32);   // section timers of k_select (prof builds)

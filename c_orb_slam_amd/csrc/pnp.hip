@@ -240,6 +240,63 @@ int PnPBatch::ensure(size_t dev_bytes, size_t host_bytes, size_t probs) {
 }
 
 // PnPsolver::iterate for `n` solvers; solver k draws from rngs[k] (may alias).
+// Byte layout of one iterate() call's device work area and pinned staging.  The accounting
+// (how much to allocate) and the carve (where each buffer goes) both come from here, so they
+// cannot drift apart: an earlier version summed unaligned sizes for the Refine scratch while
+// the carve aligned each sub-buffer, and the last solvers' Refine buffers ran past the work
+// area (the PnP fault of 9f527cb; tests/test_pnp_layout.py pins the invariant).
+struct PnPLayout {
+    static size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
+    static int words(int N) { return (N + 31) >> 5; }
+    // hypothesis region of a solver with K hypotheses: idx | masks | counts | (R, t)
+    static size_t hyp_bytes(int K, int minSet) { return al((size_t)K * minSet * 4); }
+    static size_t mask_bytes(int K, int N) { return al((size_t)K * words(N) * 4); }
+    static size_t cnt_bytes(int K) { return al((size_t)K * 4); }
+    static size_t rt_bytes(int K) { return al((size_t)K * 12 * 8); }
+    // pinned staging of a solver's results: counts | masks | (R, t)
+    static size_t host_mask_off(int K) { return cnt_bytes(K); }
+    static size_t host_rt_off(int K, int N) { return cnt_bytes(K) + mask_bytes(K, N); }
+    static size_t host_slot(int K, int N) { return host_rt_off(K, N) + al((size_t)K * 96); }
+    // Refine slot of a solver: inlier idx list | mask | (R, t) | inlier count
+    static size_t ref_mask_off(int N) { return al((size_t)N * 4); }
+    static size_t ref_rt_off(int N) { return ref_mask_off(N) + al((size_t)words(N) * 4); }
+    static size_t ref_out_off(int N) { return ref_rt_off(N) + 96; }
+    static size_t ref_slot(int N) { return al(ref_out_off(N) + 4); }
+};
+
+int pnp_layout_check(int n, const int* N, const int* K, const int* minSet, long long* out4) {
+    // accounting as iterate() does it
+    size_t dev = 0, host = 0;
+    for (int k = 0; k < n; k++) {
+        dev += PnPLayout::hyp_bytes(K[k], minSet[k]) + PnPLayout::mask_bytes(K[k], N[k]) + PnPLayout::cnt_bytes(K[k]) +
+               PnPLayout::rt_bytes(K[k]);
+        host = std::max(host, PnPLayout::host_slot(K[k], N[k]));
+    }
+    const size_t ref_base = dev;
+    for (int k = 0; k < n; k++) dev += PnPLayout::ref_slot(N[k]);
+    const size_t dev_cap = dev + 256, host_cap = (host + 256) * n + 1024;
+    // every byte the carve touches: hypothesis regions, all solvers needing Refine at once
+    size_t dend = 0, o = 0, hend = 0, ho = 0;
+    for (int k = 0; k < n; k++) {
+        o += PnPLayout::hyp_bytes(K[k], minSet[k]) + PnPLayout::mask_bytes(K[k], N[k]) + PnPLayout::cnt_bytes(K[k]);
+        dend = std::max(dend, o + (size_t)K[k] * 96);
+        o += PnPLayout::rt_bytes(K[k]);
+        hend = std::max(hend, ho + PnPLayout::host_rt_off(K[k], N[k]) + (size_t)K[k] * 96);
+        ho += PnPLayout::host_slot(K[k], N[k]);
+    }
+    size_t ro = ref_base;
+    for (int k = 0; k < n; k++) {
+        dend = std::max(dend, ro + PnPLayout::ref_out_off(N[k]) + 4);
+        dend = std::max(dend, ro + (size_t)N[k] * 4);
+        ro += PnPLayout::ref_slot(N[k]);
+    }
+    out4[0] = (long long)dev_cap;
+    out4[1] = (long long)dend;
+    out4[2] = (long long)host_cap;
+    out4[3] = (long long)hend;
+    return dend <= dev_cap && hend <= host_cap ? 0 : 1;
+}
+
 int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnPResult* res) {
     hipStream_t s = stream_;
     struct Job {
@@ -251,7 +308,7 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
     };
     std::vector<Job> jobs(n);
     size_t dev = 0, host = 0;
-    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    using LY = PnPLayout;
     for (int k = 0; k < n; k++) {
         PnPSolver& P = *S[k];
         PnPResult& r = res[k];
@@ -268,17 +325,16 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
         if (J.K <= 0) J.K = 0;
         J.active = J.K > 0;
         J.snap = *rngs[k];
-        const int words = (P.N_ + 31) >> 5;
-        J.hyp_off = dev; dev += al((size_t)J.K * P.minSet_ * 4);
-        J.mask_off = dev; dev += al((size_t)J.K * words * 4);
-        J.cnt_off = dev; dev += al((size_t)J.K * 4);
-        J.rt_off = dev; dev += al((size_t)J.K * 12 * 8);
-        host = std::max(host, al((size_t)J.K * 4) + al((size_t)J.K * words * 4) + al((size_t)J.K * 96));
+        J.hyp_off = dev; dev += LY::hyp_bytes(J.K, P.minSet_);
+        J.mask_off = dev; dev += LY::mask_bytes(J.K, P.N_);
+        J.cnt_off = dev; dev += LY::cnt_bytes(J.K);
+        J.rt_off = dev; dev += LY::rt_bytes(J.K);
+        host = std::max(host, LY::host_slot(J.K, P.N_));
         if (int e = P.upload(s)) return e;
     }
     // refine scratch (per solver): idx list N + mask + rt + count
     size_t ref_base = dev;
-    for (int k = 0; k < n; k++) dev += al((size_t)S[k]->N_ * 4) + al((size_t)((S[k]->N_ + 31) / 32) * 4) + 96 + 256;
+    for (int k = 0; k < n; k++) dev += LY::ref_slot(S[k]->N_);
     if (int e = ensure(dev + 256, (host + 256) * n + 1024, (size_t)n)) return e;
     char* D = (char*)d_work_;
     char* Hh = (char*)h_work_;
@@ -354,11 +410,11 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
         const int words = (P.N_ + 31) >> 5;
         hoff[k] = ho;
         ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho, D + J.cnt_off, (size_t)J.K * 4, hipMemcpyDeviceToHost, s));
-        ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho + al((size_t)J.K * 4), D + J.mask_off, (size_t)J.K * words * 4,
+        ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho + LY::host_mask_off(J.K), D + J.mask_off, (size_t)J.K * words * 4,
                                      hipMemcpyDeviceToHost, s));
-        ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho + al((size_t)J.K * 4) + al((size_t)J.K * words * 4), D + J.rt_off,
-                                     (size_t)J.K * 96, hipMemcpyDeviceToHost, s));
-        ho += al((size_t)J.K * 4) + al((size_t)J.K * words * 4) + al((size_t)J.K * 96);
+        ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho + LY::host_rt_off(J.K, P.N_), D + J.rt_off, (size_t)J.K * 96,
+                                     hipMemcpyDeviceToHost, s));
+        ho += LY::host_slot(J.K, P.N_);
     }
     ORB_HIP_CHECK(hipStreamSynchronize(s));
     // 3. sequential replay; Refine requests batched across solvers
@@ -373,8 +429,8 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
             PnPSolver& P = *S[k];
             const int words = (P.N_ + 31) >> 5;
             const int* cnt = (const int*)(Hh + hoff[k]);
-            const uint32_t* masks = (const uint32_t*)(Hh + hoff[k] + al((size_t)J.K * 4));
-            const double* rts = (const double*)(Hh + hoff[k] + al((size_t)J.K * 4) + al((size_t)J.K * words * 4));
+            const uint32_t* masks = (const uint32_t*)(Hh + hoff[k] + LY::host_mask_off(J.K));
+            const double* rts = (const double*)(Hh + hoff[k] + LY::host_rt_off(J.K, P.N_));
             bool wait = false;
             while (J.next < J.K) {
                 const int h = J.next;
@@ -450,16 +506,15 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
             for (int i = 0; i < P.N_; i++)
                 if (P.bestInliers_[i]) idx.push_back(i);
             roff[q] = ro;
-            const int words = (P.N_ + 31) >> 5;
             ORB_HIP_CHECK(hipMemcpyAsync(D + ro, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, s));
             PnPProbDev r = pd[need[q]];
             r.ref_idx = (const int*)(D + ro);
             r.ref_n = (int)idx.size();
-            r.ref_mask = (uint32_t*)(D + ro + al((size_t)P.N_ * 4));
-            r.ref_rt = (double*)(D + ro + al((size_t)P.N_ * 4) + al((size_t)words * 4));
-            r.ref_out = (int*)(D + ro + al((size_t)P.N_ * 4) + al((size_t)words * 4) + 96);
+            r.ref_mask = (uint32_t*)(D + ro + LY::ref_mask_off(P.N_));
+            r.ref_rt = (double*)(D + ro + LY::ref_rt_off(P.N_));
+            r.ref_out = (int*)(D + ro + LY::ref_out_off(P.N_));
             rq[q] = r;
-            ro += al((size_t)P.N_ * 4) + al((size_t)words * 4) + 96 + 256;
+            ro += LY::ref_slot(P.N_);
         }
         ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, rq.data(), sizeof(PnPProbDev) * rq.size(), hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_pnp_refine, dim3((unsigned)(need.size() + 63) / 64), dim3(64), 0, s,

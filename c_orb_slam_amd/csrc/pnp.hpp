@@ -89,4 +89,8 @@ private:
     size_t work_cap_ = 0, hwork_cap_ = 0, probs_cap_ = 0;
 };
 
+// Layout invariant of PnPBatch::iterate's work area (unit entry): out4 = {device bytes
+// allocated, device end touched, host bytes allocated, host end touched}; 0 if both fit.
+int pnp_layout_check(int n, const int* N, const int* K, const int* minSet, long long* out4);
+
 }  // namespace orbgpu

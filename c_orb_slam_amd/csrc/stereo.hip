@@ -15,6 +15,7 @@
 //   k_stereo_filter  one workgroup per pair: bitonic sort of the kept SADs in LDS, median,
 //                    thDist = 1.5f*1.4f*median, invalidation of SAD >= thDist.
 #include "stereo.hpp"
+#include "orb_match.hpp"
 
 #include <algorithm>
 #include <climits>
@@ -92,7 +93,8 @@ __global__ void __launch_bounds__(1024) k_stereo_rows(const StereoDev* __restric
     }
 }
 
-__global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restrict__ probs, StereoParams P) {
+__global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restrict__ probs, StereoParams P,
+                                                      unsigned long long* counters) {
     ORBGPU_LATENCY_WAVE();
     const StereoDev& S = probs[blockIdx.y];
     const int lane = threadIdx.x & 63;
@@ -113,6 +115,7 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
 #pragma unroll
         for (int k = 0; k < 8; k++) q[k] = dl[k];
         unsigned best = 0xffffffffu;
+        int scored = 0;
         const int c1 = S.rowStart[row + 1];
         for (int c = S.rowStart[row] + lane; c < c1; c += 64) {
             const int iR = S.rowIdx[c];
@@ -125,8 +128,17 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
 #pragma unroll
             for (int k = 0; k < 8; k++) dist += __popc(q[k] ^ dr[k]);
             if (dist < 100) best = min(best, ((unsigned)dist << 16) | (unsigned)iR);
+            scored++;
         }
         best = wave_min_u(best);
+        if (counters) {   // measurement: scored (left, right) pairs and searched left keypoints
+            const int tot = wave_sum_i(scored);
+            if (lane == 0) {   // spread over kCountSlots addresses: one per wave would serialise
+                const int sl = (blockIdx.x + blockIdx.y * 7) & (kCountSlots - 1);
+                atomicAdd(&counters[2 * kCountSlots + sl], (unsigned long long)tot);
+                atomicAdd(&counters[3 * kCountSlots + sl], 1ull);
+            }
+        }
         const int bestDist = best == 0xffffffffu ? 100 : (int)(best >> 16);
         const int bestIdxR = (int)(best & 0xffffu);
         if (bestDist < 75) {   // thOrbDist = (TH_HIGH + TH_LOW) / 2
@@ -258,14 +270,23 @@ __global__ void __launch_bounds__(256) k_stereo_filter(const StereoDev* __restri
     if (tid == 0) *S.kept = kept;
 }
 
-int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoParams& P, hipStream_t s) {
+int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoParams& P, hipStream_t s, Matcher* tm) {
     if (nprob <= 0) return 0;
+    const bool timed = tm && tm->timing();
+    if (timed) {
+        if (int e = tm->zero_counters(2, 2)) return e;
+        tm->mark(4);
+    }
     hipLaunchKernelGGL(k_stereo_rows, dim3(nprob), dim3(1024), 0, s, d_probs, P);
+    if (timed) tm->mark(5);
     if (maxNL > 0)
-        hipLaunchKernelGGL(k_stereo_match, dim3((maxNL + 3) / 4, nprob), dim3(256), 0, s, d_probs, P);
+        hipLaunchKernelGGL(k_stereo_match, dim3((maxNL + 3) / 4, nprob), dim3(256), 0, s, d_probs, P,
+                           timed ? tm->counters() : nullptr);
+    if (timed) tm->mark(6);
     int m = 1;
     while (m < std::max(maxNL, 1)) m <<= 1;
     hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(256), (size_t)m * sizeof(int), s, d_probs);
+    if (timed) tm->mark(7);
     ORB_HIP_CHECK(hipGetLastError());
     return 0;
 }

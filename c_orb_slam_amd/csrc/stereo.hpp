@@ -42,7 +42,10 @@ struct StereoDev {
     int* rowIdx;            // scratch (NR * band rows)
 };
 
-int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoParams& P, hipStream_t s);
+class Matcher;
+// tm (optional): the matcher whose timing events / counters record the launches (its stream is s)
+int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoParams& P, hipStream_t s,
+                  Matcher* tm = nullptr);
 
 // Frame::UnprojectStereo over a batch of frames (Frame.cc:666-680)
 struct UnprojDev {

@@ -113,6 +113,19 @@ int ORBmatcher_destroy(ORBmatcher_h h);
 int ORBmatcher_set_device_pointers(ORBmatcher_h h, int on);
 void* ORBmatcher_stream(ORBmatcher_h h);
 
+/* Measurement (no reference counterpart; bench roofline): with timing on, every search,
+ * stereo and CSR call on this matcher records HIP events around its kernels on
+ * ORBmatcher_stream() and counts its work on the device.  ORBmatcher_last_timings waits for
+ * the stream and returns the last call's kernel times (ms, -1 = not run):
+ *   ms8[0..6]: k_build_grid, k_candidates, k_select, k_stereo_rows, k_stereo_match,
+ *              k_stereo_filter, k_csr_hamming;
+ * and work counts:
+ *   counts8[0..5]: SearchByProjection (query, candidate) pairs scored, queries with a window,
+ *                  ComputeStereoMatches (left, right) pairs scored, left keypoints searched,
+ *                  SearchCandidates pairs, SearchCandidates queries. */
+int ORBmatcher_enable_timing(ORBmatcher_h h, int on);
+int ORBmatcher_last_timings(ORBmatcher_h h, float* ms8, long long* counts8);
+
 /* static int ORBmatcher::DescriptorDistance(a, b)   ORBmatcher.cc:1647-1663 (host) */
 int ORBmatcher_DescriptorDistance(const uint8_t* a, const uint8_t* b);
 
@@ -638,6 +651,10 @@ int orbgpu_unit_ldlt_solve(int n, const double* S, const double* b, double* x, i
 int orbgpu_unit_csum(const double* v, int n, double* out);
 /* tiled LDL^T factorisation only (n x n row-major, upper triangle read): out = d on the
  * diagonal, L in the strict lower triangle, eliminated rows in the strict upper. */
+/* PnPsolver batch work-area layout invariant (host only, no device): for n solvers with
+ * N[k] correspondences, K[k] hypotheses and minSet[k], out4 = {device bytes allocated, device
+ * end touched, host bytes allocated, host end touched}; ORB_OK iff everything touched fits. */
+int orbgpu_unit_pnp_layout(int n, const int* N, const int* K, const int* minSet, long long* out4);
 int orbgpu_unit_ldlt_factor(int n, const double* S, double* out);
 /* one wave's canonical 64-tree of v64[0..64) (cross-lane permlane/DPP path) */
 int orbgpu_unit_wave_tree(const double* v64, double* out);

@@ -25,6 +25,13 @@ def build():
 _lib = None
 
 
+def use_library(path):
+    """Load another build of the same oracle sources (bench.py's -O3 -march=native timing build)."""
+    global _lib, LIB_PATH
+    LIB_PATH = Path(path)
+    _lib = None
+
+
 def lib():
     global _lib
     if _lib is None:
