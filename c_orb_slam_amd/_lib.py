@@ -57,6 +57,11 @@ class orb_mappoints(C.Structure):
     _fields_ = [("n", C.c_int), ("pos", C.c_void_p), ("desc", C.c_void_p), ("observations", C.c_void_p)]
 
 
+class orb_localmap(C.Structure):
+    _fields_ = [("n", C.c_int), ("pos", C.c_void_p), ("desc", C.c_void_p), ("observations", C.c_void_p),
+                ("max_dist", C.c_void_p), ("min_dist", C.c_void_p), ("normal", C.c_void_p), ("skip", C.c_void_p)]
+
+
 def header_functions(path=HEADER):
     """Names of every function the public header declares."""
     txt = re.sub(r"/\*.*?\*/", "", Path(path).read_text(), flags=re.S)
@@ -159,6 +164,8 @@ def lib():
     L.orbgpu_unit_ldlt_solve.argtypes = [i32, vp, vp, vp, i32, P(i32)]
     L.orbgpu_unit_csum.argtypes = [vp, i32, vp]
     L.orbgpu_unit_pnp_layout.argtypes = [i32, vp, vp, vp, vp]
+    L.ORBmatcher_SearchLocalPoints_batch.argtypes = [vp, i32, vp, vp, vp, f32, f32, vp, vp]
+    L.Frame_isInFrustum_batch.argtypes = [vp, i32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp]
     L.ORBmatcher_enable_timing.argtypes = [vp, i32]
     L.ORBmatcher_last_timings.argtypes = [vp, vp, vp]
     L.orbgpu_unit_ldlt_factor.argtypes = [i32, vp, vp]

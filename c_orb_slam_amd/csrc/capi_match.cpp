@@ -278,6 +278,109 @@ int ORBmatcher_SearchByProjection_MapPoints(ORBmatcher_h h, const orb_frame* F, 
     return ORB_OK;
 }
 
+int Frame_isInFrustum_batch(ORBmatcher_h h, int count, const orb_frame* F, const orb_localmap* maps,
+                            float viewingCosLimit, float logScaleFactor, uint8_t* const* in_view,
+                            float* const* proj_x, float* const* proj_xr, float* const* proj_y, int32_t* const* level,
+                            float* const* view_cos, int* nvisible) {
+    if (!h || count < 0 || (count > 0 && (!F || !maps || !in_view || !proj_x || !proj_xr || !proj_y || !level ||
+                                          !view_cos || !nvisible)))
+        return ORB_E_INVALID;
+    if (count == 0) return ORB_OK;
+    Matcher* m = h->m;
+    if (!m->device_pointers()) return ORB_E_INVALID;
+    hipStream_t s = m->stream();
+    size_t need = al((size_t)count * 4) + al(sizeof(orbgpu::FrustumDev) * count) + 4096;
+    for (int p = 0; p < count; p++) {
+        const orb_localmap& M = maps[p];
+        if (!frame_ok(&F[p]) || !F[p].Tcw || M.n < 0) return ORB_E_INVALID;
+        if (M.n > 0 && (!M.pos || !M.max_dist || !M.min_dist || !M.normal || !M.skip || !in_view[p] || !proj_x[p] ||
+                        !proj_xr[p] || !proj_y[p] || !level[p] || !view_cos[p]))
+            return ORB_E_INVALID;
+        need += al((size_t)M.n * 4);
+    }
+    if (m->arena_reserve(need)) return ORB_E_HIP;
+    int err = 0;
+    int* d_nv = (int*)m->arena_alloc((size_t)count * 4);
+    if (!d_nv || hipMemsetAsync(d_nv, 0, (size_t)count * 4, s) != hipSuccess) return ORB_E_HIP;
+    std::vector<SearchDev> probs(count);
+    std::vector<orbgpu::FrustumDev> fr(count);
+    for (int p = 0; p < count; p++) {
+        SearchDev& P = probs[p];
+        memset(&P, 0, sizeof(P));
+        P.cur = frame_dev(m, &F[p], true, s, &err);
+        P.nq = maps[p].n;
+        P.mpPos = maps[p].pos;
+        orbgpu::FrustumDev& f = fr[p];
+        f.maxDist = maps[p].max_dist;
+        f.minDist = maps[p].min_dist;
+        f.normal = maps[p].normal;
+        f.skip = maps[p].skip;
+        f.inView = in_view[p];
+        f.projX = proj_x[p];
+        f.projXR = proj_xr[p];
+        f.projY = proj_y[p];
+        f.level = level[p];
+        f.viewCos = view_cos[p];
+        f.mpIndex = (int*)m->arena_alloc((size_t)std::max(maps[p].n, 1) * 4);
+        f.nvisible = d_nv + p;
+        if (!f.mpIndex) return ORB_E_HIP;
+    }
+    if (err) return err;
+    if (m->frustum(probs, fr, viewingCosLimit, logScaleFactor)) return ORB_E_HIP;
+    if (hipMemcpyAsync(nvisible, d_nv, (size_t)count * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return ORB_E_HIP;
+    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+}
+
+int ORBmatcher_SearchLocalPoints_batch(ORBmatcher_h h, int count, const orb_frame* F, int32_t* const* cur_mp,
+                                       const orb_localmap* maps, float logScaleFactor, float th, int* nmatches,
+                                       int* nvisible) {
+    if (!h || count < 0 || (count > 0 && (!F || !cur_mp || !maps || !nmatches || !nvisible))) return ORB_E_INVALID;
+    if (count == 0) return ORB_OK;
+    Matcher* m = h->m;
+    if (!m->device_pointers()) return ORB_E_INVALID;   // device-resident tracking path only
+    hipStream_t s = m->stream();
+    size_t need = al((size_t)count * 8) + al(sizeof(orbgpu::FrustumDev) * count) + 4096;
+    for (int p = 0; p < count; p++) {
+        const orb_localmap& M = maps[p];
+        if (!frame_ok(&F[p]) || !F[p].Tcw || M.n < 0 || !cur_mp[p]) return ORB_E_INVALID;
+        if (M.n > 0 && (!M.pos || !M.desc || !M.observations || !M.max_dist || !M.min_dist || !M.normal || !M.skip))
+            return ORB_E_INVALID;
+        need += 7 * al((size_t)M.n * 4) + 256;
+    }
+    if (m->arena_reserve(need)) return ORB_E_HIP;
+    int err = 0;
+    int* d_cnt = (int*)m->arena_alloc((size_t)count * 8);
+    if (!d_cnt) return ORB_E_HIP;
+    if (hipMemsetAsync(d_cnt, 0, (size_t)count * 8, s) != hipSuccess) return ORB_E_HIP;
+    std::vector<SearchDev> probs(count);
+    std::vector<orbgpu::FrustumDev> fr(count);
+    for (int p = 0; p < count; p++) {
+        SearchDev& P = probs[p];
+        memset(&P, 0, sizeof(P));
+        P.cur = frame_dev(m, &F[p], true, s, &err);
+        P.nq = maps[p].n;
+        P.mpPos = maps[p].pos;
+        P.mpDesc = maps[p].desc;
+        P.mpObs = maps[p].observations;
+        P.curMP = cur_mp[p];
+        P.nmatches = d_cnt + p;
+        orbgpu::FrustumDev& f = fr[p];
+        memset(&f, 0, sizeof(f));
+        f.maxDist = maps[p].max_dist;
+        f.minDist = maps[p].min_dist;
+        f.normal = maps[p].normal;
+        f.skip = maps[p].skip;
+        f.nvisible = d_cnt + count + p;
+    }
+    if (err) return err;
+    const int rc = m->search_local_points(probs, fr, 0.5f, logScaleFactor, th);
+    if (rc) return rc == -1 ? ORB_E_INVALID : ORB_E_HIP;
+    if (hipMemcpyAsync(nmatches, d_cnt, (size_t)count * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(nvisible, d_cnt + count, (size_t)count * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return ORB_E_HIP;
+    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+}
+
 int ORBmatcher_SearchCandidates(ORBmatcher_h h, const uint8_t* qdesc, int nq, const uint8_t* tdesc, int nt,
                                 const int32_t* off, const int32_t* cand, int32_t* dist, int32_t* best_idx,
                                 int32_t* best_dist, int32_t* second_dist) {

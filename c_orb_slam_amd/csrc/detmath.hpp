@@ -92,5 +92,64 @@ __device__ __forceinline__ double exp_d(double x) {
     return ldexp(y, k);
 }
 
+
+// fdlibm __ieee754_log as an IEEE operation sequence (oracle/matchers2.c ora_det_log), for
+// positive finite x: MapPoint::PredictScale's log(ratio) (MapPoint.cc:402-417) is glibc logf
+// on a float; (float)log_d(x) equals it on every float the tracking path feeds it
+// (tests/test_oracle_kat.py::test_det_log_predict_scale_exhaustive).
+__device__ __forceinline__ double log_d(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+                 Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                 Lg7 = 1.479819860511658591e-01;
+    if (!(x > 0.0)) return x == 0.0 ? -HUGE_VAL : (x - x) / 0.0;
+    if (x > 1.79769313486231570815e+308) return x;
+    unsigned long long bits = (unsigned long long)__double_as_longlong(x);
+    int hx = (int)(bits >> 32);
+    const unsigned lx = (unsigned)bits;
+    int k = 0;
+    if (hx < 0x00100000) {   // subnormal: scale by 2^54
+        x *= 1.80143985094819840000e+16;
+        k -= 54;
+        bits = (unsigned long long)__double_as_longlong(x);
+        hx = (int)(bits >> 32);
+    }
+    (void)lx;
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    const int i0 = (hx + 0x95f64) & 0x100000;
+    bits = ((unsigned long long)(unsigned)(hx | (i0 ^ 0x3ff00000)) << 32) | (bits & 0xffffffffull);
+    x = __longlong_as_double((long long)bits);
+    k += (i0 >> 20);
+    const double f = x - 1.0;
+    const double dk = (double)k;
+    if ((0x000fffff & (2 + hx)) < 3) {   // |f| < 2^-20
+        if (f == 0.0) return k == 0 ? 0.0 : dk * ln2_hi + dk * ln2_lo;
+        const double R = f * f * (0.5 - 0.33333333333333333 * f);
+        return k == 0 ? f - R : dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    int i = hx - 0x6147a;
+    const double w = z * z;
+    const int j = 0x6b851 - hx;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    const double R = t2 + t1;
+    if (i > 0) {
+        const double hfsq = 0.5 * f * f;
+        return k == 0 ? f - (hfsq - s * (hfsq + R)) : dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    return k == 0 ? f - s * (f - R) : dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+// MapPoint::PredictScale(currentDist, Frame*) (MapPoint.cc:402-417)
+__device__ __forceinline__ int predict_scale(float maxDistance, float currentDist, float logScaleFactor, int nlevels) {
+    const float ratio = maxDistance / currentDist;
+    int n = (int)ceilf((float)log_d((double)ratio) / logScaleFactor);
+    return n < 0 ? 0 : (n >= nlevels ? nlevels - 1 : n);
+}
+
 }  // namespace detmath
 }  // namespace orbgpu

@@ -18,6 +18,8 @@
 
 #include <cstring>
 
+#include "detmath.hpp"
+
 namespace orbgpu {
 
 constexpr int TH_HIGH = 100;  // ORBmatcher.cc:37
@@ -325,6 +327,66 @@ __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict_
             atomicAdd(&counters[1 * kCountSlots + sl], nqv);
         }
     }
+}
+
+// Frame::isInFrustum(pMP, viewingCosLimit) (Frame.cc:269-325), one thread per local map point.
+// Float evaluation as the reference writes it: Pc = Rcw P + tcw and mOw = -Rcw^T tcw as one
+// cv::gemm each (f64 accumulation, one rounding), invz = 1.0f / PcZ,
+// dist = cv::norm(PO) and PO.dot(Pn) accumulated in double, PredictScale through
+// detmath::predict_scale (glibc logf's levels on every input, tests/test_oracle_kat.py).
+__global__ void __launch_bounds__(256) k_frustum(const SearchDev* __restrict__ probs, const FrustumDev* __restrict__ frs,
+                                                 float viewingCosLimit, float logScaleFactor) {
+    ORBGPU_LATENCY_WAVE();
+    const SearchDev& P = probs[blockIdx.y];
+    const FrustumDev& Fq = frs[blockIdx.y];
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool on = j < P.nq;
+    int vis = 0;
+    if (on) {
+        Fq.mpIndex[j] = j;
+        const FrameDev& F = P.cur;
+        if (!Fq.skip[j]) {
+            const float* T = F.Tcw;
+            const float* X = P.mpPos + 3 * (size_t)j;
+            const float PcX = gemm_row(T, 0, X[0], X[1], X[2]);
+            const float PcY = gemm_row(T, 1, X[0], X[1], X[2]);
+            const float PcZ = gemm_row(T, 2, X[0], X[1], X[2]);
+            if (!(PcZ < 0.0f)) {
+                const float invz = 1.0f / PcZ;
+                const float u = F.fx * PcX * invz + F.cx;
+                const float v = F.fy * PcY * invz + F.cy;
+                if (!(u < F.minX || u > F.maxX) && !(v < F.minY || v > F.maxY)) {
+                    const float maxDistance = 1.2f * Fq.maxDist[j];   // GetMaxDistanceInvariance
+                    const float minDistance = 0.8f * Fq.minDist[j];   // GetMinDistanceInvariance
+                    float Ow[3];
+                    for (int i = 0; i < 3; i++) {
+                        const double s = (double)T[0 * 4 + i] * T[3] + (double)T[1 * 4 + i] * T[7] +
+                                         (double)T[2 * 4 + i] * T[11];
+                        Ow[i] = (float)(s * -1.0);
+                    }
+                    const float PO[3] = {X[0] - Ow[0], X[1] - Ow[1], X[2] - Ow[2]};
+                    const double s2 = ((double)PO[0] * PO[0] + (double)PO[1] * PO[1]) + (double)PO[2] * PO[2];
+                    const float dist = (float)sqrt(s2);
+                    if (!(dist < minDistance || dist > maxDistance)) {
+                        const float* Pn = Fq.normal + 3 * (size_t)j;
+                        const double dot = ((double)PO[0] * Pn[0] + (double)PO[1] * Pn[1]) + (double)PO[2] * Pn[2];
+                        const float viewCos = (float)(dot / (double)dist);
+                        if (!(viewCos < viewingCosLimit)) {
+                            vis = 1;
+                            Fq.projX[j] = u;
+                            Fq.projXR[j] = u - F.bf * invz;
+                            Fq.projY[j] = v;
+                            Fq.level[j] = detmath::predict_scale(Fq.maxDist[j], dist, logScaleFactor, F.nlevels);
+                            Fq.viewCos[j] = viewCos;
+                        }
+                    }
+                }
+            }
+        }
+        Fq.inView[j] = (uint8_t)vis;
+    }
+    const unsigned long long nv = wave_sum_u64((unsigned long long)vis);
+    if ((threadIdx.x & 63) == 0 && nv) atomicAdd(Fq.nvisible, (int)nv);
 }
 
 // Greedy replay as a fixed-point iteration (one 256-thread workgroup per problem).
@@ -687,6 +749,12 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     }
     ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, probs.data(), pb, hipMemcpyHostToDevice, stream_));
     SearchDev* dp = (SearchDev*)d_probs_;
+    if (frustum_ && maxq > 0) {   // SearchLocalPoints: Frame::isInFrustum fills the query arrays first
+        mark(8);
+        hipLaunchKernelGGL(k_frustum, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, (const SearchDev*)dp,
+                           frustum_, frustumCos_, frustumLsf_);
+        mark(9);
+    }
     if (timing_) {
         if (int e = zero_counters(0, 2)) return e;
         mark(0);
@@ -716,6 +784,67 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
 }
 
 int Matcher::search_last(std::vector<SearchDev>& probs, float th, bool bMono) { return run(probs, th, bMono, true); }
+
+int Matcher::frustum(std::vector<SearchDev>& probs, const std::vector<FrustumDev>& fr, float viewingCosLimit,
+                     float logScaleFactor) {
+    const int np = (int)probs.size();
+    int maxq = 0;
+    for (auto& p : probs) maxq = std::max(maxq, p.nq);
+    if (np == 0 || maxq == 0) return 0;
+    const size_t pb = sizeof(SearchDev) * np;
+    if (pb > probs_cap_) {
+        if (d_probs_) (void)hipFree(d_probs_);
+        probs_cap_ = pb * 2;
+        ORB_HIP_CHECK(hipMalloc(&d_probs_, probs_cap_));
+    }
+    FrustumDev* dfr = (FrustumDev*)arena_alloc(sizeof(FrustumDev) * np);
+    if (!dfr) return -2;
+    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, probs.data(), pb, hipMemcpyHostToDevice, stream_));
+    ORB_HIP_CHECK(hipMemcpyAsync(dfr, fr.data(), sizeof(FrustumDev) * np, hipMemcpyHostToDevice, stream_));
+    mark(8);
+    hipLaunchKernelGGL(k_frustum, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, (const SearchDev*)d_probs_, dfr,
+                       viewingCosLimit, logScaleFactor);
+    mark(9);
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int Matcher::search_local_points(std::vector<SearchDev>& probs, std::vector<FrustumDev>& fr, float viewingCosLimit,
+                                 float logScaleFactor, float th) {
+    const int np = (int)probs.size();
+    if (np == 0) return 0;
+    int maxq = 0;
+    for (auto& p : probs) maxq = std::max(maxq, p.nq);
+    if (maxq > 0) {
+        // per-problem isInFrustum outputs (inView 1 B, projX/XR/Y/viewCos 4 B, level/mpIndex 4 B)
+        size_t need = sizeof(FrustumDev) * np + 256;
+        for (auto& p : probs) need += 7 * ((((size_t)p.nq * 4) + 255) & ~(size_t)255);
+        char* base = (char*)arena_alloc(need);
+        if (!base) return -2;
+        char* o = base + ((sizeof(FrustumDev) * np + 255) & ~(size_t)255);
+        for (int k = 0; k < np; k++) {
+            const size_t b = (((size_t)probs[k].nq * 4) + 255) & ~(size_t)255;
+            FrustumDev& f = fr[k];
+            f.inView = (uint8_t*)o; o += b;
+            f.projX = (float*)o; o += b;
+            f.projXR = (float*)o; o += b;
+            f.projY = (float*)o; o += b;
+            f.level = (int*)o; o += b;
+            f.viewCos = (float*)o; o += b;
+            f.mpIndex = (int*)o; o += b;
+            SearchDev& P = probs[k];
+            P.inView = f.inView; P.projX = f.projX; P.projXR = f.projXR; P.projY = f.projY;
+            P.level = f.level; P.viewCos = f.viewCos; P.mpIndex = f.mpIndex;
+        }
+        ORB_HIP_CHECK(hipMemcpyAsync(base, fr.data(), sizeof(FrustumDev) * np, hipMemcpyHostToDevice, stream_));
+        frustum_ = (const FrustumDev*)base;   // launched by run() once the problems are on the device
+        frustumCos_ = viewingCosLimit;
+        frustumLsf_ = logScaleFactor;
+    }
+    const int rc = run(probs, th, false, false);
+    frustum_ = nullptr;
+    return rc;
+}
 int Matcher::search_local(std::vector<SearchDev>& probs, float th) { return run(probs, th, false, false); }
 
 int Matcher::candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, const int* off, const int* cand, int* dist,
@@ -755,7 +884,8 @@ int Matcher::zero_counters(int first, int n) {
     return 0;
 }
 
-// events: search 0..3 (grid | candidates | select), stereo 4..7 (rows | match | filter), CSR 12..13
+// events: search 0..3 (grid | candidates | select), stereo 4..7 (rows | match | filter), CSR 12..13,
+// isInFrustum 8..9
 int Matcher::timings(float* ms8, long long* cnt8) {
     for (int i = 0; i < 8; i++) {
         ms8[i] = -1.0f;
@@ -763,8 +893,8 @@ int Matcher::timings(float* ms8, long long* cnt8) {
     }
     if (!d_count_) return 0;
     ORB_HIP_CHECK(hipStreamSynchronize(stream_));
-    const int pairs[7][2] = {{0, 1}, {1, 2}, {2, 3}, {4, 5}, {5, 6}, {6, 7}, {12, 13}};
-    for (int k = 0; k < 7; k++) {
+    const int pairs[8][2] = {{0, 1}, {1, 2}, {2, 3}, {4, 5}, {5, 6}, {6, 7}, {12, 13}, {8, 9}};
+    for (int k = 0; k < 8; k++) {
         const int a = pairs[k][0], b = pairs[k][1];
         if (evSet_[a] && evSet_[b]) (void)hipEventElapsedTime(&ms8[k], ev_[a], ev_[b]);
     }

@@ -58,6 +58,23 @@ struct SearchDev {
     int2* hist;       // nq (bin, idx)
 };
 
+// Frame::isInFrustum inputs / outputs of one SearchLocalPoints problem (Tracking.cc:1143-1193):
+// the local map points are the problem's map point table (SearchDev mpPos / mpDesc / mpObs)
+struct FrustumDev {
+    const float* maxDist;   // MapPoint::mfMaxDistance
+    const float* minDist;   // mfMinDistance
+    const float* normal;    // GetNormal() (3 per point)
+    const uint8_t* skip;    // mnLastFrameSeen == CurrentFrame.mnId or isBad()
+    uint8_t* inView;        // outputs: mbTrackInView, mTrackProjX / XR / Y, mnTrackScaleLevel,
+    float* projX;           //          mTrackViewCos
+    float* projXR;
+    float* projY;
+    int* level;
+    float* viewCos;
+    int* mpIndex;
+    int* nvisible;          // IncreaseVisible() count (nToMatch)
+};
+
 // one GetFeaturesInArea query of the area-candidate engine; qd = query descriptor row (-1 = none)
 struct AreaQuery {
     float x, y, r;
@@ -77,6 +94,13 @@ public:
     // Runs `n` SearchByProjection(Cur, Last) problems in one set of launches.
     int search_last(std::vector<SearchDev>& probs, float th, bool bMono);
     int search_local(std::vector<SearchDev>& probs, float th);
+    // Tracking::SearchLocalPoints: isInFrustum(pMP, viewingCosLimit) on the device for every
+    // local map point of each problem, then SearchByProjection(F, vpLocalMapPoints, th)
+    int search_local_points(std::vector<SearchDev>& probs, std::vector<FrustumDev>& fr, float viewingCosLimit,
+                            float logScaleFactor, float th);
+    // Frame::isInFrustum only (outputs in fr's device arrays; arena-allocated problem copy)
+    int frustum(std::vector<SearchDev>& probs, const std::vector<FrustumDev>& fr, float viewingCosLimit,
+                float logScaleFactor);
     int candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, const int* off, const int* cand, int* dist,
                    int* best_idx, int* best_dist, int* second_dist);
     hipStream_t stream() const { return stream_; }
@@ -94,7 +118,7 @@ public:
     // Measurement (bench roofline): with timing on, the search / stereo / CSR launches record
     // HIP events on stream() around each kernel and count their work units on the device.
     //   ms[0..7]:  k_build_grid, k_candidates, k_select, k_stereo_rows, k_stereo_match,
-    //              k_stereo_filter, k_csr_hamming, (spare)
+    //              k_stereo_filter, k_csr_hamming, k_frustum
     //   cnt[0..7]: search (query, candidate) pairs scored, search queries with a window,
     //              stereo (left, right) pairs scored, stereo left keypoints, CSR pairs, CSR queries
     int set_timing(bool on);
@@ -119,6 +143,8 @@ private:
     void* d_cand_ = nullptr;
     size_t cand_cap_ = 0;
     bool timing_ = false;
+    const FrustumDev* frustum_ = nullptr;   // pending k_frustum of search_local_points
+    float frustumCos_ = 0.5f, frustumLsf_ = 0.f;
     hipEvent_t ev_[16] = {};
     bool evSet_[16] = {};
     unsigned long long* d_count_ = nullptr;

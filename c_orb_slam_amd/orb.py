@@ -313,6 +313,100 @@ class ORBmatcher:
               "ORBmatcher_ComputeStereoMatches_batch")
         return [u[:len(k)] for u, k in zip(uR, kL)], [d[:len(k)] for d, k in zip(dep, kL)], n
 
+    def _local_batch(self, frames, maps, dev, want_desc=True):
+        """Device copies (torch) of host Frames and local maps (dicts of numpy arrays: pos, desc,
+        obs, max_dist, min_dist, normal, skip) and their C structs."""
+        import torch
+        from ._lib import orb_frame, orb_localmap
+        keep, fs, ms = [], [], []
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        for F, M in zip(frames, maps):
+            n = len(M["pos"])
+            d = dict(k=t(F.keysUn.view(np.int32).reshape(F.N, 7) if F.N else np.zeros((1, 7), np.int32)),
+                     desc=t(F.desc if F.N else np.zeros((1, 32), np.uint8)), scale=t(F.scale),
+                     Tcw=t(F.Tcw.reshape(16)),
+                     uR=None if F.uRight is None else t(F.uRight if F.N else np.zeros(1, np.float32)),
+                     pos=t(np.asarray(M["pos"], np.float32).reshape(-1, 3) if n else np.zeros((1, 3), np.float32)),
+                     mdesc=t(np.asarray(M.get("desc", np.zeros((n, 32))), np.uint8).reshape(-1, 32) if n
+                             else np.zeros((1, 32), np.uint8)),
+                     obs=t(np.asarray(M.get("obs", np.ones(n)), np.int32) if n else np.zeros(1, np.int32)),
+                     mx=t(np.asarray(M["max_dist"], np.float32) if n else np.zeros(1, np.float32)),
+                     mn=t(np.asarray(M["min_dist"], np.float32) if n else np.zeros(1, np.float32)),
+                     nrm=t(np.asarray(M["normal"], np.float32).reshape(-1, 3) if n else np.zeros((1, 3), np.float32)),
+                     skip=t(np.asarray(M["skip"], np.uint8) if n else np.zeros(1, np.uint8)))
+            keep.append(d)
+            f = orb_frame()
+            f.N = F.N
+            f.keysUn, f.desc = d["k"].data_ptr(), d["desc"].data_ptr()
+            f.uRight = None if d["uR"] is None else d["uR"].data_ptr()
+            f.minX, f.maxX, f.minY, f.maxY = F.minX, F.maxX, F.minY, F.maxY
+            f.gridWInv, f.gridHInv = F.gridWInv, F.gridHInv
+            f.scaleFactors, f.nlevels = d["scale"].data_ptr(), len(F.scale)
+            f.fx, f.fy, f.cx, f.cy, f.bf, f.b = F.fx, F.fy, F.cx, F.cy, F.bf, F.b
+            f.Tcw = d["Tcw"].data_ptr()
+            fs.append(f)
+            ms.append(orb_localmap(n, d["pos"].data_ptr(), d["mdesc"].data_ptr(), d["obs"].data_ptr(),
+                                   d["mx"].data_ptr(), d["mn"].data_ptr(), d["nrm"].data_ptr(), d["skip"].data_ptr()))
+        cnt = max(len(fs), 1)
+        return keep, (orb_frame * cnt)(*fs), (orb_localmap * cnt)(*ms)
+
+    def isInFrustum(self, frames, maps, logScaleFactor, viewingCosLimit=0.5):
+        """Frame::isInFrustum (Frame.cc:269-325) of every local map point of maps[f] in frames[f]
+        (host Frames / dicts) on the device -> per frame dict(in_view, proj_x, proj_xr, proj_y, level,
+        view_cos, nvisible) as numpy."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        keep, fa, ma = self._local_batch(frames, maps, dev)
+        outs = []
+        for M in maps:
+            n = max(len(M["pos"]), 1)
+            outs.append(dict(in_view=torch.full((n,), 7, dtype=torch.uint8, device=dev),
+                             proj_x=torch.zeros(n, device=dev), proj_xr=torch.zeros(n, device=dev),
+                             proj_y=torch.zeros(n, device=dev), level=torch.zeros(n, dtype=torch.int32, device=dev),
+                             view_cos=torch.zeros(n, device=dev)))
+        arr = lambda k: (C.c_void_p * max(len(outs), 1))(*[o[k].data_ptr() for o in outs])
+        nv = np.zeros(max(len(frames), 1), np.int32)
+        check(self._L.ORBmatcher_set_device_pointers(self._h, 1))
+        try:
+            check(self._L.Frame_isInFrustum_batch(self._h, len(frames), fa, ma, float(viewingCosLimit),
+                                                  float(logScaleFactor), arr("in_view"), arr("proj_x"),
+                                                  arr("proj_xr"), arr("proj_y"), arr("level"), arr("view_cos"),
+                                                  ptr(nv)), "Frame_isInFrustum_batch")
+        finally:
+            check(self._L.ORBmatcher_set_device_pointers(self._h, 0))
+        res = []
+        for o, M, k in zip(outs, maps, nv):
+            n = len(M["pos"])
+            r = {key: v.cpu().numpy()[:n] for key, v in o.items()}
+            r["nvisible"] = int(k)
+            res.append(r)
+        del keep
+        return res
+
+    def SearchLocalPoints(self, frames, cur_mps, maps, logScaleFactor, th=1.0):
+        """Tracking::SearchLocalPoints (Tracking.cc:1143-1193): isInFrustum(pMP, 0.5) + SearchByProjection(F,
+        mvpLocalMapPoints, th) per frame on the device (ORBmatcher_SearchLocalPoints_batch); cur_mps[f] (int32
+        numpy, F.N) updated in place.  -> (nmatches, nvisible) arrays."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        keep, fa, ma = self._local_batch(frames, maps, dev)
+        cm = [torch.from_numpy(np.ascontiguousarray(c, np.int32) if len(c) else np.full(1, -1, np.int32)).to(dev)
+              for c in cur_mps]
+        arr = (C.c_void_p * max(len(cm), 1))(*[c.data_ptr() for c in cm])
+        nm = np.zeros(max(len(frames), 1), np.int32)
+        nv = np.zeros(max(len(frames), 1), np.int32)
+        check(self._L.ORBmatcher_set_device_pointers(self._h, 1))
+        try:
+            check(self._L.ORBmatcher_SearchLocalPoints_batch(self._h, len(frames), fa, arr, ma, float(logScaleFactor),
+                                                             float(th), ptr(nm), ptr(nv)),
+                  "ORBmatcher_SearchLocalPoints_batch")
+        finally:
+            check(self._L.ORBmatcher_set_device_pointers(self._h, 0))
+        for c, d in zip(cur_mps, cm):
+            c[:] = d.cpu().numpy()[:len(c)]
+        del keep
+        return nm[:len(frames)], nv[:len(frames)]
+
     def UnprojectStereo_device(self, frames):
         """Frame::UnprojectStereo (Frame.cc:666-680) for every keypoint of device-resident frames,
         enqueued on this matcher's stream (ORBmatcher_stream): frames[f] is a dict of torch device

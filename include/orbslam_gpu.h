@@ -187,6 +187,43 @@ int ORBmatcher_SearchByProjection_MapPoints(ORBmatcher_h h, const orb_frame* F, 
                                             const float* view_cos, const int32_t* mp_index,
                                             const orb_mappoints* mps, float th, int* nmatches);
 
+/* Tracking::mvpLocalMapPoints with the MapPoint fields isInFrustum and SearchByProjection read. */
+typedef struct orb_localmap {
+    int n;
+    const float* pos;            /* GetWorldPos (n x 3) */
+    const uint8_t* desc;         /* GetDescriptor (n x 32) */
+    const int* observations;     /* Observations() (n) */
+    const float* max_dist;       /* mfMaxDistance (n) */
+    const float* min_dist;       /* mfMinDistance (n) */
+    const float* normal;         /* GetNormal() (n x 3) */
+    const uint8_t* skip;         /* mnLastFrameSeen == CurrentFrame.mnId, or isBad() (n) */
+} orb_localmap;
+
+/* bool Frame::isInFrustum(MapPoint* pMP, float viewingCosLimit)      Frame.cc:269-325
+ * For every point of maps[p] not skipped: the visibility test against frame F[p] (Tcw, bounds,
+ * intrinsics, mbf, nlevels) and the MapPoint tracking fields it fills: in_view (mbTrackInView),
+ * proj_x / proj_xr / proj_y (mTrackProjX / XR / Y), level (mnTrackScaleLevel, PredictScale),
+ * view_cos (mTrackViewCos); outputs of points not in view are left untouched except in_view = 0.
+ * nvisible[p] = points in view.  Device pointers only; desc / observations of maps unused. */
+int Frame_isInFrustum_batch(ORBmatcher_h h, int count, const orb_frame* F, const orb_localmap* maps,
+                            float viewingCosLimit, float logScaleFactor, uint8_t* const* in_view,
+                            float* const* proj_x, float* const* proj_xr, float* const* proj_y,
+                            int32_t* const* level, float* const* view_cos, int* nvisible);
+
+/* void Tracking::SearchLocalPoints()                          Tracking.cc:1143-1193
+ * For every local map point not skipped: Frame::isInFrustum(pMP, 0.5) (Frame.cc:269-325,
+ * MapPoint::PredictScale MapPoint.cc:402-417), then SearchByProjection(F, mvpLocalMapPoints,
+ * th) with the matcher's nnratio (ORBmatcher(0.8) in the reference; ORBmatcher.cc:45-129).
+ * cur_mp[p] (in/out, F[p].N): mCurrentFrame.mvpMapPoints as rows of maps[p] (-1 = NULL);
+ * the caller clears the outliers of the first PoseOptimization and marks the matched and
+ * discarded points in `skip` first (Tracking.cc:893-913, 1146-1161).  logScaleFactor =
+ * Frame::mfLogScaleFactor.  nmatches[p] = SearchByProjection's return value, nvisible[p] =
+ * nToMatch (points IncreaseVisible() counts).  Device pointers only (ORBmatcher_set_device_
+ * pointers(h, 1)); one launch set for all `count` frames. */
+int ORBmatcher_SearchLocalPoints_batch(ORBmatcher_h h, int count, const orb_frame* F, int32_t* const* cur_mp,
+                                       const orb_localmap* maps, float logScaleFactor, float th,
+                                       int* nmatches, int* nvisible);
+
 /* void Frame::ComputeStereoMatches()                            Frame.cc:466-640
  * Rectified stereo matching of the left keypoints of image `index` (0 only for the single
  * form; image p of the batch form) of the last ORBextractor_extract[_batch] call of `left`

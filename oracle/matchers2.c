@@ -79,6 +79,72 @@ static void camera_center(const float* T, float* O)
     }
 }
 
+/* fdlibm __ieee754_log as an IEEE operation sequence (the GPU's detmath::log_d, same order):
+ * the device's stand-in for glibc logf in PredictScale; ora_predict_scale_mismatches checks
+ * the two agree on every float of a range. */
+double ora_det_log(double x)
+{
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+                 Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                 Lg7 = 1.479819860511658591e-01;
+    if (!(x > 0.0)) return x == 0.0 ? -HUGE_VAL : (x - x) / 0.0;
+    if (x > 1.79769313486231570815e+308) return x;
+    unsigned long long bits;
+    memcpy(&bits, &x, 8);
+    int hx = (int)(bits >> 32);
+    int k = 0;
+    if (hx < 0x00100000) {
+        x *= 1.80143985094819840000e+16;
+        k -= 54;
+        memcpy(&bits, &x, 8);
+        hx = (int)(bits >> 32);
+    }
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    const int i0 = (hx + 0x95f64) & 0x100000;
+    bits = ((unsigned long long)(unsigned)(hx | (i0 ^ 0x3ff00000)) << 32) | (bits & 0xffffffffull);
+    memcpy(&x, &bits, 8);
+    k += (i0 >> 20);
+    const double f = x - 1.0;
+    const double dk = (double)k;
+    if ((0x000fffff & (2 + hx)) < 3) {
+        if (f == 0.0) return k == 0 ? 0.0 : dk * ln2_hi + dk * ln2_lo;
+        const double R = f * f * (0.5 - 0.33333333333333333 * f);
+        return k == 0 ? f - R : dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    int i = hx - 0x6147a;
+    const double w = z * z;
+    const int j = 0x6b851 - hx;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    const double R = t2 + t1;
+    if (i > 0) {
+        const double hfsq = 0.5 * f * f;
+        return k == 0 ? f - (hfsq - s * (hfsq + R)) : dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    return k == 0 ? f - s * (f - R) : dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+/* Every float r in [lo, hi]: ceilf(logf(r) / lsf) (glibc, the reference's PredictScale) vs
+ * ceilf((float)ora_det_log(r) / lsf); returns the number of r where the levels differ. */
+long long ora_predict_scale_mismatches(float lo, float hi, float lsf, long long* n_checked, long long* n_logf_diff)
+{
+    long long bad = 0, n = 0, d = 0;
+    for (float r = lo; r <= hi; r = nextafterf(r, INFINITY)) {
+        const float a = logf(r), b = (float)ora_det_log((double)r);
+        if (a != b) d++;
+        if (ceilf(a / lsf) != ceilf(b / lsf)) bad++;
+        n++;
+    }
+    *n_checked = n;
+    *n_logf_diff = d;
+    return bad;
+}
+
 /* MapPoint::PredictScale (MapPoint.cc:402-417) */
 static int predict_scale(float maxDistance, float currentDist, float logScaleFactor, int nlevels)
 {
@@ -87,6 +153,51 @@ static int predict_scale(float maxDistance, float currentDist, float logScaleFac
     if (nScale < 0) nScale = 0;
     else if (nScale >= nlevels) nScale = nlevels - 1;
     return nScale;
+}
+
+/* Frame::isInFrustum(pMP, viewingCosLimit) (Frame.cc:269-325) for n map points, with
+ * MapPoint::GetMax/MinDistanceInvariance (1.2f / 0.8f, MapPoint.cc:373-383) and PredictScale
+ * (glibc logf, as the reference).  Pc and mOw as one cv::gemm each (f64 accumulation, one
+ * rounding), cv::norm and Mat::dot accumulated in double.  Returns the points in view. */
+int ora_is_in_frustum(const float* Tcw, float fx, float fy, float cx, float cy, float mbf, float minX, float maxX,
+                      float minY, float maxY, int nlevels, float logScaleFactor, int n, const float* pos,
+                      const float* maxDist, const float* minDist, const float* normal, const uint8_t* skip,
+                      float viewingCosLimit, uint8_t* inView, float* projX, float* projXR, float* projY, int* level,
+                      float* viewCos)
+{
+    float Ow[3];
+    camera_center(Tcw, Ow);
+    int nv = 0;
+    for (int j = 0; j < n; j++) {
+        inView[j] = 0;
+        if (skip[j]) continue;
+        const float* P = pos + 3 * (size_t)j;
+        const float PcX = gemm_row3(Tcw, 0, P), PcY = gemm_row3(Tcw, 1, P), PcZ = gemm_row3(Tcw, 2, P);
+        if (PcZ < 0.0f) continue;
+        const float invz = 1.0f / PcZ;
+        const float u = fx * PcX * invz + cx;
+        const float v = fy * PcY * invz + cy;
+        if (u < minX || u > maxX) continue;
+        if (v < minY || v > maxY) continue;
+        const float maxDistance = 1.2f * maxDist[j];
+        const float minDistance = 0.8f * minDist[j];
+        const float PO[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};
+        const double s2 = ((double)PO[0] * PO[0] + (double)PO[1] * PO[1]) + (double)PO[2] * PO[2];
+        const float dist = (float)sqrt(s2);
+        if (dist < minDistance || dist > maxDistance) continue;
+        const float* Pn = normal + 3 * (size_t)j;
+        const double dot = ((double)PO[0] * Pn[0] + (double)PO[1] * Pn[1]) + (double)PO[2] * Pn[2];
+        const float vc = (float)(dot / (double)dist);
+        if (vc < viewingCosLimit) continue;
+        inView[j] = 1;
+        projX[j] = u;
+        projXR[j] = u - mbf * invz;
+        projY[j] = v;
+        level[j] = predict_scale(maxDist[j], dist, logScaleFactor, nlevels);
+        viewCos[j] = vc;
+        nv++;
+    }
+    return nv;
 }
 
 int ora_search_by_projection_kf(const ora_frame* F, const float* Tcw, const float* K, int* curMP, int n, const int* kfMP,

@@ -342,6 +342,13 @@ int   ora_optimize_sim3(const ora_sim3opt_problem* P, double* S12, uint8_t* eras
 /* g2o::Sim3(Converter::toMatrix3d(R), toVector3d(t), s) */
 void  ora_sim3_from_Rts(const float* R, const float* t, float s, double* S12);
 double ora_det_exp(double x);
+double ora_det_log(double x);
+int ora_is_in_frustum(const float* Tcw, float fx, float fy, float cx, float cy, float mbf, float minX, float maxX,
+                      float minY, float maxY, int nlevels, float logScaleFactor, int n, const float* pos,
+                      const float* maxDist, const float* minDist, const float* normal, const uint8_t* skip,
+                      float viewingCosLimit, uint8_t* inView, float* projX, float* projXR, float* projY, int* level,
+                      float* viewCos);
+long long ora_predict_scale_mismatches(float lo, float hi, float lsf, long long* n_checked, long long* n_logf_diff);
 
 #ifdef __cplusplus
 }

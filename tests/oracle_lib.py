@@ -312,6 +312,40 @@ def oracle_search_local(F, cur_mp, mp_obs, in_view, proj_x, proj_xr, proj_y, lev
     return L.ora_search_by_projection_local(C.byref(of.s), ptr(cur_mp), ptr(obs), C.byref(m), th, nnratio)
 
 
+def oracle_is_in_frustum(F, M, logScaleFactor, viewingCosLimit=0.5):
+    """Frame::isInFrustum (Frame.cc:269-325) of every point of local map M (dict) in Frame F."""
+    n = len(M["pos"])
+    pos = np.ascontiguousarray(M["pos"], np.float32).reshape(-1, 3)
+    mx, mn = np.ascontiguousarray(M["max_dist"], np.float32), np.ascontiguousarray(M["min_dist"], np.float32)
+    nrm = np.ascontiguousarray(M["normal"], np.float32).reshape(-1, 3)
+    skip = np.ascontiguousarray(M["skip"], np.uint8)
+    r = dict(in_view=np.zeros(n, np.uint8), proj_x=np.zeros(n, np.float32), proj_xr=np.zeros(n, np.float32),
+             proj_y=np.zeros(n, np.float32), level=np.zeros(n, np.int32), view_cos=np.zeros(n, np.float32))
+    L = lib()
+    f32 = C.c_float
+    L.ora_is_in_frustum.argtypes = [C.c_void_p] + [f32] * 9 + [C.c_int, f32, C.c_int] + [C.c_void_p] * 5 + [f32] + \
+        [C.c_void_p] * 6
+    T = np.ascontiguousarray(F.Tcw, np.float32).reshape(16)
+    nv = L.ora_is_in_frustum(ptr(T), F.fx, F.fy, F.cx, F.cy, F.bf, F.minX, F.maxX, F.minY, F.maxY, len(F.scale),
+                             logScaleFactor, n, ptr(pos), ptr(mx), ptr(mn), ptr(nrm), ptr(skip), viewingCosLimit,
+                             ptr(r["in_view"]), ptr(r["proj_x"]), ptr(r["proj_xr"]), ptr(r["proj_y"]), ptr(r["level"]),
+                             ptr(r["view_cos"]))
+    r["nvisible"] = nv
+    return r
+
+
+def oracle_search_local_points(F, cur_mp, M, logScaleFactor, th=1.0, nnratio=0.8):
+    """Tracking::SearchLocalPoints (Tracking.cc:1143-1193) on the oracle; cur_mp updated in place."""
+    fr = oracle_is_in_frustum(F, M, logScaleFactor)
+    n = len(M["pos"])
+    nm = 0
+    if fr["nvisible"] > 0:
+        nm = oracle_search_local(F, cur_mp, M["obs"], fr["in_view"], fr["proj_x"], fr["proj_xr"], fr["proj_y"],
+                                 fr["level"], fr["view_cos"], np.asarray(M["desc"], np.uint8).reshape(-1, 32),
+                                 np.arange(n, dtype=np.int32), th, nnratio)
+    return nm, fr["nvisible"]
+
+
 # ---------------------------------------------------------------- PnP oracle
 class OraclePnP:
     """PnPsolver(F, vpMapPointMatches) restated on CPU (reference src/PnPsolver.cc)."""

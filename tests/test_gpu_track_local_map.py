@@ -1,0 +1,128 @@
+"""TrackLocalMap's device path (Tracking.cc:930-974) vs the CPU oracle:
+
+* Frame::isInFrustum(pMP, 0.5) (Frame.cc:269-325) with MapPoint::PredictScale
+  (MapPoint.cc:402-417) for every local map point -- in-view flags and the tracking fields
+  (mTrackProjX / XR / Y, mnTrackScaleLevel, mTrackViewCos) bit-exact, every rejection branch
+  exercised (behind the camera, outside the image, outside the scale-invariance distance,
+  viewing angle, skipped points);
+* Tracking::SearchLocalPoints (Tracking.cc:1143-1193): isInFrustum + SearchByProjection(F,
+  mvpLocalMapPoints, th) with ORBmatcher(0.8) -- match indices and counts bit-exact, batched
+  over frames in one launch set."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from c_orb_slam_amd import synthetic
+from c_orb_slam_amd.orb import Frame
+
+pytestmark = pytest.mark.gpu
+
+W, H = 1241, 376
+
+
+@pytest.fixture(scope="module")
+def seq(gpu):
+    frames, Hs, Rs = synthetic.sequence(33, 4, return_rotations=True)
+    ex = gpu.ORBextractor(1200, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=4)
+    res = ex.extract_batch(frames)
+    return Rs, res, ex.GetScaleFactors()
+
+
+def local_map(rng, kps, desc, scale, Twc=np.eye(4, dtype=np.float32), extra=300):
+    """Map points lifted from a keyframe's keypoints (world = that frame's camera, then Twc), with
+    the MapPoint fields UpdateNormalAndDepth sets (MapPoint.cc:349-371), plus points that fail
+    each isInFrustum test."""
+    fx, fy, cx, cy = synthetic.intrinsics(W, H)
+    n = len(kps)
+    d = rng.uniform(4.0, 60.0, n)
+    Xc = np.stack([(kps["x"] - cx) / fx * d, (kps["y"] - cy) / fy * d, d], 1)
+    oct_ = kps["octave"].astype(int)
+    # extras: behind the camera, far outside the image, scale-invariance misses, oblique normals
+    e = rng.integers(0, 4, extra)
+    Xe = rng.normal(0, 1, (extra, 3)) * [10, 5, 20]
+    Xe[e == 0, 2] = -np.abs(Xe[e == 0, 2]) - 1
+    Xe[e == 1, :2] *= 50
+    Xe[e >= 2, 2] = np.abs(Xe[e >= 2, 2]) + 5
+    X = np.vstack([Xc, Xe])
+    oct_all = np.concatenate([oct_, rng.integers(0, 8, extra)])
+    dist = np.linalg.norm(X, axis=1)
+    mx = dist * scale[oct_all]
+    mx[n:][e[:] == 2] *= rng.choice([0.3, 3.0], int((e == 2).sum()))      # outside [0.8 min, 1.2 max]
+    mn = mx / scale[7]
+    nrm = X / dist[:, None]
+    tilt = np.where(np.concatenate([rng.random(n) < 0.05, e == 3]), 1.5, 0.1)
+    nrm = nrm + rng.normal(0, 1, nrm.shape) * tilt[:, None]
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    R, t = Twc[:3, :3].astype(np.float64), Twc[:3, 3].astype(np.float64)
+    Xw = X @ R.T + t
+    nw = nrm @ R.T
+    m = len(Xw)
+    dsc = np.vstack([desc, rng.integers(0, 256, (extra, 32), dtype=np.uint8)])
+    return dict(pos=Xw.astype(np.float32), desc=dsc, obs=rng.integers(0, 5, m).astype(np.int32),
+                max_dist=mx.astype(np.float32), min_dist=mn.astype(np.float32), normal=nw.astype(np.float32),
+                skip=(rng.random(m) < 0.08).astype(np.uint8))
+
+
+def cur_frame(rng, k1, d1, scale, Rs, stereo=True):
+    fx, fy, cx, cy = synthetic.intrinsics(W, H)
+    bf = synthetic.KITTI_BF
+    uR = None
+    if stereo:
+        dd = rng.uniform(5, 50, len(k1)).astype(np.float32)
+        uR = np.where(rng.random(len(k1)) < 0.6, k1["x"] - np.float32(bf) / dd, -1).astype(np.float32)
+    T = synthetic.pose_from_rotation(Rs)
+    return Frame(k1, d1, scale, T, fx, fy, cx, cy, bf if stereo else 0.0, W, H, uRight=uR)
+
+
+def test_is_in_frustum_matches_oracle(gpu, seq):
+    Rs, res, scale = seq
+    lsf = np.float32(np.log(np.float32(1.2)))
+    rng = np.random.default_rng(1)
+    frames, maps = [], []
+    for f in range(3):
+        (k0, d0), (k1, d1) = res[f], res[f + 1]
+        maps.append(local_map(rng, k0, d0, scale))
+        frames.append(cur_frame(rng, k1, d1, scale, Rs[f]))
+    maps.append(dict(pos=np.zeros((0, 3), np.float32), desc=np.zeros((0, 32), np.uint8), obs=np.zeros(0, np.int32),
+                     max_dist=np.zeros(0, np.float32), min_dist=np.zeros(0, np.float32),
+                     normal=np.zeros((0, 3), np.float32), skip=np.zeros(0, np.uint8)))   # empty local map
+    frames.append(frames[0])
+    m = gpu.ORBmatcher(0.8, False)
+    g = m.isInFrustum(frames, maps, lsf)
+    for F, M, gr in zip(frames, maps, g):
+        o = oracle_lib.oracle_is_in_frustum(F, M, lsf)
+        assert gr["nvisible"] == o["nvisible"]
+        assert np.array_equal(gr["in_view"], o["in_view"])
+        v = o["in_view"].astype(bool)
+        for k in ("proj_x", "proj_xr", "proj_y", "level", "view_cos"):
+            assert np.array_equal(gr[k][v], o[k][v]), k
+    # every rejection branch and the acceptance path were taken
+    o = oracle_lib.oracle_is_in_frustum(frames[0], maps[0], lsf)
+    assert 0 < o["nvisible"] < len(maps[0]["pos"]) - maps[0]["skip"].sum()
+    assert len(np.unique(o["level"][o["in_view"].astype(bool)])) >= 4
+
+
+@pytest.mark.parametrize("th", [1.0, 3.0, 5.0])
+def test_search_local_points_matches_oracle(gpu, seq, th):
+    Rs, res, scale = seq
+    lsf = np.float32(np.log(np.float32(1.2)))
+    rng = np.random.default_rng(int(th * 10))
+    frames, maps, cms = [], [], []
+    for f in range(3):
+        (k0, d0), (k1, d1) = res[f], res[f + 1]
+        M = local_map(rng, k0, d0, scale)
+        F = cur_frame(rng, k1, d1, scale, Rs[f], stereo=f != 1)
+        cm = np.where(rng.random(F.N) < 0.15, rng.integers(0, len(M["pos"]), F.N), -1).astype(np.int32)
+        M["skip"][cm[cm >= 0]] = 1            # points already in the frame (mnLastFrameSeen)
+        frames.append(F)
+        maps.append(M)
+        cms.append(cm)
+    m = gpu.ORBmatcher(0.8, False)
+    g = [c.copy() for c in cms]
+    nm, nv = m.SearchLocalPoints(frames, g, maps, lsf, th)
+    for F, M, c0, gc, n1, n2 in zip(frames, maps, cms, g, nm, nv):
+        oc = c0.copy()
+        no, nvo = oracle_lib.oracle_search_local_points(F, oc, M, lsf, th, 0.8)
+        assert n2 == nvo and n1 == no
+        assert np.array_equal(gc, oc), np.nonzero(gc != oc)[0][:10]
+        assert no > 50

@@ -408,3 +408,20 @@ def test_oracle_optimize_sim3_early_return():
     S0 = oracle_lib.oracle_sim3_from_Rts(pr["R0"], pr["t0"], pr["s0"])
     n, S, er, _ = oracle_lib.oracle_optimize_sim3(pr, S0)
     assert pr["valid"].sum() < 10 and n == 0 and np.array_equal(S, S0)
+
+
+def test_det_log_predict_scale_exhaustive():
+    """MapPoint::PredictScale (MapPoint.cc:402-417) takes glibc logf of ratio = mfMaxDistance /
+    dist; on the device it is (float) of a restated fdlibm log in double (detmath::log_d, the
+    same operation sequence as ora_det_log).  Over every float ratio isInFrustum can produce
+    (dist within [0.8 minDistance, 1.2 maxDistance]: ratio in [1/1.2, 1.2^7 / 0.8]) and well
+    beyond, the predicted levels agree exactly."""
+    L = oracle_lib.lib()
+    L.ora_predict_scale_mismatches.restype = C.c_longlong
+    L.ora_predict_scale_mismatches.argtypes = [C.c_float, C.c_float, C.c_float, C.POINTER(C.c_longlong),
+                                               C.POINTER(C.c_longlong)]
+    lsf = np.float32(np.log(np.float32(1.2)))
+    n, d = C.c_longlong(), C.c_longlong()
+    bad = L.ora_predict_scale_mismatches(0.25, 16.0, float(lsf), C.byref(n), C.byref(d))
+    assert n.value > 40_000_000
+    assert bad == 0, (bad, d.value, n.value)
