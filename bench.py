@@ -39,6 +39,7 @@ VALU_FILE = "valu_r01.json"   # PMC SQ_INSTS_VALU per launch (tools/pmc_valu.py)
 MATCH_PMC_FILE = "match_pmc_r02.json"   # matcher kernels: HBM bytes and VALU instructions per launch (tools/pmc_match.py)
 VALU_PEAK_GINST = 1228.8   # 256 CUs x 2 wave64 VALU issues per cycle x 2.4 GHz (MI355X_MICROARCH.md)
 W, H, NFEAT = 1241, 376, 1200
+K_LOCAL = 5   # local map = the map points of the last K_LOCAL frames (UpdateLocalMap's local keyframes)
 
 
 def parse():
@@ -162,7 +163,8 @@ def main():
     gH = np.float32(np.float32(48) / np.float32(H))
     P = B - 1
     arr = lambda xs: (C.c_void_p * len(xs))(*xs)
-    from c_orb_slam_amd._lib import orb_unproject, pose_frame
+    from c_orb_slam_amd._lib import orb_unproject, pose_frame, orb_localmap
+    lsf = np.float32(np.log(np.float32(1.2)))   # Frame::mfLogScaleFactor
     from concurrent.futures import ThreadPoolExecutor
     # HIP's current device is per thread: every worker binds it first
     pool = ThreadPoolExecutor(2, initializer=lambda: torch.cuda.set_device(dev))
@@ -173,8 +175,19 @@ def main():
         w = C.sizeof(cls) // 4
         return np.ctypeslib.as_array((C.c_int32 * (count * w)).from_address(C.addressof(arr))).reshape(count, w)[:, 0]
 
+    # absolute poses in the batch's world (frame 0's camera): frame b+1 is frame b rotated by Rs[b]
+    Tabs = [np.eye(4, dtype=np.float32)]
+    for R in Rs:
+        Tabs.append(synthetic.pose_from_rotation(np.asarray(R, np.float64) @ Tabs[-1][:3, :3].astype(np.float64)))
+    d_Tcw = torch.from_numpy(np.stack([T.reshape(16) for T in Tabs])).to(dev)                 # mTcw (motion model)
+    d_Twc = torch.from_numpy(np.stack([np.linalg.inv(T).astype(np.float32).reshape(16) for T in Tabs])).to(dev)
+    d_obs = torch.ones(B * cap, dtype=torch.int32, device=dev)
+
     class Lane:
-        """One batch in flight: its own extractor pair (pyramids, keypoints) and tracking buffers."""
+        """One batch in flight: its own extractor pair (pyramids, keypoints) and tracking buffers.
+        Map: every frame b's stereo keypoints become map points (UnprojectStereo with its absolute
+        Twc), block b of a (B x cap) table; the local map of pair p (current frame p+1) is the blocks
+        of frames max(0, p-K+1)..p, contiguous in the table (UpdateLocalMap's local keyframes)."""
 
         def __init__(self):
             self.exL = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=B)
@@ -185,21 +198,45 @@ def main():
             self.d_descR = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
             self.d_uR = torch.empty((B, cap), dtype=torch.float32, device=dev)      # mvuRight
             self.d_depth = torch.empty((B, cap), dtype=torch.float32, device=dev)   # mvDepth
-            self.d_mp_pos = torch.empty((B, cap, 3), dtype=torch.float32, device=dev)
-            self.d_last_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
+            self.d_mp_pos = torch.zeros((B, cap, 3), dtype=torch.float32, device=dev)
+            self.d_slot = torch.empty((B, cap), dtype=torch.int32, device=dev)      # UnprojectStereo slots
+            self.d_last_mp = torch.empty((P, cap), dtype=torch.int32, device=dev)   # LastFrame.mvpMapPoints
             self.d_cur_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
+            self.d_maxd = torch.zeros((B, cap), dtype=torch.float32, device=dev)    # MapPoint::mfMaxDistance
+            self.d_mind = torch.zeros((B, cap), dtype=torch.float32, device=dev)
+            self.d_nrm = torch.zeros((B, cap, 3), dtype=torch.float32, device=dev)
+            self.d_skip = torch.ones((P, K_LOCAL * cap + 1), dtype=torch.uint8, device=dev)
             self.scale = torch.from_numpy(self.exL.GetScaleFactors()).to(dev)
             self.d_Tout = torch.empty((P, 16), dtype=torch.float32, device=dev)
+            self.d_Tout2 = torch.empty((P, 16), dtype=torch.float32, device=dev)
             self.d_poutl = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
+            self.d_poutl2 = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
             self.isig_tab = torch.from_numpy(self.exL.GetInverseScaleSigmaSquares()).to(dev)
+            self.bs = [max(0, p - K_LOCAL + 1) for p in range(P)]                   # first local block of pair p
+            self.loc_off = torch.tensor([(p - self.bs[p]) * cap for p in range(P)], dtype=torch.int32, device=dev)
             # ctypes views of the batch, built once (device pointers do not move; only counts change)
-            self.curs = (orb_frame * P)(*[self.frame_struct(b, poses[b - 1].data_ptr()) for b in range(1, B)])
-            self.lasts = (orb_frame * P)(*[self.frame_struct(b, eye.data_ptr()) for b in range(0, B - 1)])
+            self.curs = (orb_frame * P)(*[self.frame_struct(b, d_Tcw[b].data_ptr()) for b in range(1, B)])
+            # TrackLocalMap sees mCurrentFrame.mTcw as set by the first PoseOptimization
+            self.curs_local = (orb_frame * P)(*[self.frame_struct(b, self.d_Tout[b - 1].data_ptr())
+                                                for b in range(1, B)])
+            # gather rows: local-map row j of pair p <- table row bs[p]*cap + j (sentinel: no row)
+            gi = np.full((P, K_LOCAL * cap + 1), B * cap, np.int64)
+            for p_ in range(P):
+                q_ = max(0, p_ - K_LOCAL + 1)
+                gi[p_, :(p_ - q_ + 1) * cap] = np.arange(q_ * cap, (p_ + 1) * cap)
+            self.skip_rows = torch.from_numpy(gi).to(dev)
+            self.lasts = (orb_frame * P)(*[self.frame_struct(b, d_Tcw[b].data_ptr()) for b in range(0, B - 1)])
             self.mps = (orb_mappoints * P)()
+            self.lmaps = (orb_localmap * P)()
             for p in range(P):
-                self.mps[p].pos = self.d_mp_pos[p].data_ptr()
-                self.mps[p].desc = self.d_desc[p].data_ptr()
+                q = self.bs[p]
+                self.mps[p].n = (p - q + 1) * cap
+                self.mps[p].pos = self.d_mp_pos[q].data_ptr()
+                self.mps[p].desc = self.d_desc[q].data_ptr()
                 self.mps[p].observations = d_obs.data_ptr()
+                self.lmaps[p] = orb_localmap((p - q + 1) * cap, self.d_mp_pos[q].data_ptr(), self.d_desc[q].data_ptr(),
+                                             d_obs.data_ptr(), self.d_maxd[q].data_ptr(), self.d_mind[q].data_ptr(),
+                                             self.d_nrm[q].data_ptr(), self.d_skip[p].data_ptr())
             self.a_cur_mp = arr([self.d_cur_mp[b].data_ptr() for b in range(1, B)])
             self.a_last_kps = arr([self.d_kps[b].data_ptr() for b in range(P)])
             self.a_last_mp = arr([self.d_last_mp[b].data_ptr() for b in range(P)])
@@ -210,28 +247,42 @@ def main():
             self.s_dR = arr([self.d_descR[b].data_ptr() for b in range(B)])
             self.s_uR = arr([self.d_uR[b].data_ptr() for b in range(B)])
             self.s_dep = arr([self.d_depth[b].data_ptr() for b in range(B)])
-            # UpdateLastFrame: Frame::UnprojectStereo of frame b's stereo keypoints (Twc = I: the last
-            # frame is the reference) -> the map point table of pair b and LastFrame.mvpMapPoints
+            # UpdateLastFrame / CreateNewKeyFrame: Frame::UnprojectStereo of frame b's stereo keypoints
+            # with its absolute Twc -> block b of the map point table
             self.unp = (orb_unproject * B)(*[
-                orb_unproject(0, self.d_kps[b].data_ptr(), self.d_depth[b].data_ptr(), eye.data_ptr(), float(fx),
+                orb_unproject(0, self.d_kps[b].data_ptr(), self.d_depth[b].data_ptr(), d_Twc[b].data_ptr(), float(fx),
                               float(fy), float(cx), float(cy), self.d_mp_pos[b].data_ptr(),
-                              self.d_last_mp[b].data_ptr()) for b in range(B)])
-            # PoseOptimization(&mCurrentFrame): the frame's own arrays, map points by index
+                              self.d_slot[b].data_ptr()) for b in range(B)])
+            # PoseOptimization(&mCurrentFrame): the frame's own arrays, map points by local-map index;
+            # TrackWithMotionModel's call from the motion-model pose, TrackLocalMap's from its result
             self.pframes = (pose_frame * P)(*[
-                pose_frame(0, poses[p].data_ptr(), self.d_cur_mp[p + 1].data_ptr(), self.d_mp_pos[p].data_ptr(),
-                           self.d_kps[p + 1].data_ptr(), self.d_uR[p + 1].data_ptr(), self.isig_tab.data_ptr(), 8,
-                           float(fx), float(fy), float(cx), float(cy), float(mbf)) for p in range(P)])
+                pose_frame(0, d_Tcw[p + 1].data_ptr(), self.d_cur_mp[p + 1].data_ptr(),
+                           self.d_mp_pos[self.bs[p]].data_ptr(), self.d_kps[p + 1].data_ptr(),
+                           self.d_uR[p + 1].data_ptr(), self.isig_tab.data_ptr(), 8, float(fx), float(fy), float(cx),
+                           float(cy), float(mbf)) for p in range(P)])
+            self.pframes2 = (pose_frame * P)(*[
+                pose_frame(0, self.d_Tout[p].data_ptr(), self.d_cur_mp[p + 1].data_ptr(),
+                           self.d_mp_pos[self.bs[p]].data_ptr(), self.d_kps[p + 1].data_ptr(),
+                           self.d_uR[p + 1].data_ptr(), self.isig_tab.data_ptr(), 8, float(fx), float(fy), float(cx),
+                           float(cy), float(mbf)) for p in range(P)])
             self.a_Tout = arr([self.d_Tout[p].data_ptr() for p in range(P)])
             self.a_poutl = arr([self.d_poutl[p].data_ptr() for p in range(P)])
+            self.a_Tout2 = arr([self.d_Tout2[p].data_ptr() for p in range(P)])
+            self.a_poutl2 = arr([self.d_poutl2[p].data_ptr() for p in range(P)])
             self.n_unp = n_field(self.unp, orb_unproject, B)
             self.n_cur = n_field(self.curs, orb_frame, P)
             self.n_last = n_field(self.lasts, orb_frame, P)
-            self.n_mps = n_field(self.mps, orb_mappoints, P)
             self.n_pose = n_field(self.pframes, pose_frame, P)
+            self.n_pose2 = n_field(self.pframes2, pose_frame, P)
+            self.n_curl = n_field(self.curs_local, orb_frame, P)
             self.ninl = np.zeros(P, np.int32)
+            self.ninl2 = np.zeros(P, np.int32)
             self.nm = np.zeros(P, np.int32)
+            self.nml = np.zeros(P, np.int32)
+            self.nvis = np.zeros(P, np.int32)
             self.nst = np.zeros(B, np.int32)
             self.nL = self.nR = None
+            self.kidx = torch.arange(cap, dtype=torch.int32, device=dev)
 
         def frame_struct(self, b, Tptr):
             f = orb_frame()
@@ -265,16 +316,28 @@ def main():
                   "ComputeStereoMatches batch")
 
         def search(self):
-            # UpdateLastFrame (Frame::UnprojectStereo) and the current frames' empty mvpMapPoints, on
-            # the matcher's stream ahead of the search
+            # UpdateLastFrame (Frame::UnprojectStereo) of every frame of the batch, the map points'
+            # normal and scale-invariance distances (MapPoint::UpdateNormalAndDepth, MapPoint.cc:
+            # 331-371: one observation, the creating frame), LastFrame.mvpMapPoints as local-map
+            # rows and the current frames' empty mvpMapPoints, on the matcher's stream
             nL = self.nL
             self.n_unp[:] = nL
             self.n_cur[:] = nL[1:]
             self.n_last[:] = nL[:-1]
-            self.n_mps[:] = nL[:-1]
             self.n_pose[:] = nL[1:]
+            self.n_pose2[:] = nL[1:]
+            with torch.cuda.stream(match_stream):
+                self.d_slot.fill_(-1)
             check(L.Frame_UnprojectStereo_batch_device(m._h, B, self.unp), "UnprojectStereo batch")
             with torch.cuda.stream(match_stream):
+                Ow = d_Twc.view(B, 4, 4)[:, :3, 3]
+                PO = self.d_mp_pos - Ow[:, None, :]
+                dist = torch.linalg.vector_norm(PO, dim=2)
+                self.d_nrm.copy_(PO / dist.clamp_min(1e-6)[..., None])
+                self.d_maxd.copy_(dist * self.scale[self.d_kps[:, :, 5].clamp(0, 7).long()])
+                self.d_mind.copy_(self.d_maxd / self.scale[7])
+                lm = self.d_slot[:P]
+                self.d_last_mp.copy_(torch.where(lm >= 0, lm + self.loc_off[:, None], lm))
                 self.d_cur_mp.fill_(-1)
             # TrackWithMotionModel: SearchByProjection(CurrentFrame, LastFrame, th=7, stereo) (Tracking.cc:869-885)
             check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, P, self.curs, self.a_cur_mp, self.lasts,
@@ -282,8 +345,30 @@ def main():
                                                                   self.mps, 7.0, 0, ptr(self.nm)),
                   "SearchByProjection batch")
 
+        def local_map(self):
+            """TrackLocalMap (Tracking.cc:930-974) after TrackWithMotionModel's PoseOptimization:
+            discard its outliers (Tracking.cc:893-913), skip the points already in the frame
+            (SearchLocalPoints 1146-1161) and the table rows without a map point, isInFrustum +
+            SearchByProjection(F, mvpLocalMapPoints, th=1) (stereo, ORBmatcher(0.8)), then the
+            second PoseOptimization."""
+            with torch.cuda.stream(match_stream):
+                cm = self.d_cur_mp[1:]
+                # local-map rows without a map point (no stereo depth / past the frame's N)
+                slot = torch.cat([self.d_slot.reshape(-1), self.d_slot.new_full((1,), -1)])
+                self.d_skip.copy_((slot[self.skip_rows] < 0).to(torch.uint8))
+                sk = torch.where(cm >= 0, cm, torch.full_like(cm, K_LOCAL * cap)).long()
+                self.d_skip.scatter_(1, sk, 1)
+                cm.copy_(torch.where(self.d_poutl.bool(), torch.full_like(cm, -1), cm))
+            self.n_curl[:] = self.nL[1:]
+            check(L.ORBmatcher_SearchLocalPoints_batch(m._h, P, self.curs_local, self.a_cur_mp, self.lmaps,
+                                                       float(lsf), 1.0, ptr(self.nml), ptr(self.nvis)),
+                  "SearchLocalPoints batch")
+            check(L.Optimizer_PoseOptimization_frames_device(P, self.pframes2, self.a_Tout2, self.a_poutl2,
+                                                             ptr(self.ninl2)), "PoseOptimization (local map)")
+
         def track(self):
-            """ComputeStereoMatches, UpdateLastFrame, SearchByProjection(Cur, Last, 7), PoseOptimization."""
+            """ComputeStereoMatches, UpdateLastFrame, SearchByProjection(Cur, Last, 7), PoseOptimization,
+            TrackLocalMap (SearchLocalPoints, PoseOptimization)."""
             t1 = time.perf_counter()
             nL, nR = self.nL, self.nR
             self.stereo()
@@ -294,15 +379,129 @@ def main():
             check(L.Optimizer_PoseOptimization_frames_device(P, self.pframes, self.a_Tout, self.a_poutl,
                                                              ptr(self.ninl)), "PoseOptimization batch")
             t4 = time.perf_counter()
-            for k, v in (("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3)):
+            self.local_map()
+            t5 = time.perf_counter()
+            for k, v in (("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3), ("local_map", t5 - t4)):
                 phase_acc[k] = phase_acc.get(k, 0.0) + v * 1e3
             tl, tr = self.exL.last_timings(), self.exR.last_timings()
             for k in tl:
                 stage_acc[k] = stage_acc.get(k, 0.0) + tl[k] + tr[k]
             kernel_ms.append(tl["fast_cells"])
             kernel_ms.append(tr["fast_cells"])
-            pose_inl.append(int(self.ninl.sum()))
-            return int(nL.sum() + nR.sum()), int(self.nm.sum()), int(self.nst.sum())
+            pose_inl.append(int(self.ninl2.sum()))
+            local_acc.append((int(self.nml.sum()), int(self.nvis.sum())))
+            return int(nL.sum() + nR.sum()), int(self.nm.sum() + self.nml.sum()), int(self.nst.sum())
+
+    def latency_leg(nf):
+        """Per-frame tracking latency, the reference's own figure (wall time of one TrackStereo,
+        stereo_kitti.cc:80-97): batch 1, frames in sequence, each frame's motion model from the
+        previous frames' optimised poses (Tracking.cc:869, mVelocity), the local map from the last
+        K_LOCAL frames' map points; every call synchronous as Tracking makes them."""
+        nf = min(nf, B)
+        eL1 = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=1)
+        eR1 = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=1)
+        k = torch.empty((nf, cap, 7), dtype=torch.int32, device=dev)
+        d = torch.empty((nf, cap, 32), dtype=torch.uint8, device=dev)
+        kR = torch.empty((cap, 7), dtype=torch.int32, device=dev)
+        dR = torch.empty((cap, 32), dtype=torch.uint8, device=dev)
+        uR = torch.empty((nf, cap), dtype=torch.float32, device=dev)
+        dep = torch.empty((nf, cap), dtype=torch.float32, device=dev)
+        pos = torch.zeros((nf, cap, 3), dtype=torch.float32, device=dev)
+        slot = torch.full((nf, cap), -1, dtype=torch.int32, device=dev)
+        maxd = torch.zeros((nf, cap), dtype=torch.float32, device=dev)
+        mind = torch.zeros((nf, cap), dtype=torch.float32, device=dev)
+        nrm = torch.zeros((nf, cap, 3), dtype=torch.float32, device=dev)
+        skip = torch.ones(K_LOCAL * cap + 1, dtype=torch.uint8, device=dev)
+        cur_mp = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        last_mp = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        Tpred = torch.zeros(16, dtype=torch.float32, device=dev)
+        Tlast = torch.zeros(16, dtype=torch.float32, device=dev)
+        Twc_l = torch.zeros(16, dtype=torch.float32, device=dev)
+        T1, T2 = (torch.zeros(16, dtype=torch.float32, device=dev) for _ in range(2))
+        o1, o2 = (torch.zeros(cap, dtype=torch.uint8, device=dev) for _ in range(2))
+        isig = lanes[0].isig_tab
+        scale = lanes[0].scale
+        one = np.zeros(1, np.int32)
+        Tcw = [np.eye(4, dtype=np.float32)]
+        walls = []
+        nmatch = []
+        for t in range(nf):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fR = pool.submit(eR1.extract_device, d_R[t].data_ptr(), 1, W, H, W, W * H, kR.data_ptr(), dR.data_ptr(), cap)
+            nL = eL1.extract_device(d_L[t].data_ptr(), 1, W, H, W, W * H, k[t].data_ptr(), d[t].data_ptr(), cap)
+            nR = fR.result()
+            nl, nr = np.array([nL[0]], np.int32), np.array([nR[0]], np.int32)
+            check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, eL1._h, eR1._h, 1, ptr(nl), arr([k[t].data_ptr()]),
+                                                          arr([d[t].data_ptr()]), ptr(nr), arr([kR.data_ptr()]),
+                                                          arr([dR.data_ptr()]), float(mbf), float(mb),
+                                                          arr([uR[t].data_ptr()]), arr([dep[t].data_ptr()]), ptr(one)),
+                  "ComputeStereoMatches")
+            if t > 0:
+                V = Tcw[t - 1] @ np.linalg.inv(Tcw[t - 2]) if t >= 2 else np.eye(4, dtype=np.float32)
+                Tp = (V @ Tcw[t - 1]).astype(np.float32)
+                Tpred.copy_(torch.from_numpy(Tp.reshape(16)))
+                Tlast.copy_(torch.from_numpy(Tcw[t - 1].reshape(16)))
+                Twc_l.copy_(torch.from_numpy(np.linalg.inv(Tcw[t - 1]).astype(np.float32).reshape(16)))
+                nlast = int(last_n[0])
+                u = orb_unproject(nlast, k[t - 1].data_ptr(), dep[t - 1].data_ptr(), Twc_l.data_ptr(), float(fx),
+                                  float(fy), float(cx), float(cy), pos[t - 1].data_ptr(), slot[t - 1].data_ptr())
+                check(L.Frame_UnprojectStereo_batch_device(m._h, 1, C.byref(u)), "UnprojectStereo")
+                q = max(0, t - K_LOCAL)
+                nloc = (t - q) * cap
+                with torch.cuda.stream(match_stream):
+                    PO = pos[t - 1] - Twc_l.view(4, 4)[:3, 3]
+                    dist = torch.linalg.vector_norm(PO, dim=1)
+                    nrm[t - 1].copy_(PO / dist.clamp_min(1e-6)[:, None])
+                    maxd[t - 1].copy_(dist * scale[k[t - 1, :, 5].clamp(0, 7).long()])
+                    mind[t - 1].copy_(maxd[t - 1] / scale[7])
+                    last_mp.copy_(torch.where(slot[t - 1] >= 0, slot[t - 1] + (t - 1 - q) * cap, slot[t - 1]))
+                    cur_mp.fill_(-1)
+                fc = lanes[0].frame_struct(0, Tpred.data_ptr())
+                fc.keysUn, fc.desc, fc.uRight, fc.N = k[t].data_ptr(), d[t].data_ptr(), uR[t].data_ptr(), int(nL[0])
+                fl = lanes[0].frame_struct(0, Tlast.data_ptr())
+                fl.keysUn, fl.desc, fl.uRight, fl.N = k[t - 1].data_ptr(), d[t - 1].data_ptr(), uR[t - 1].data_ptr(), nlast
+                mp = orb_mappoints(nloc, pos[q].data_ptr(), d[q].data_ptr(), d_obs.data_ptr())
+                nm1 = np.zeros(1, np.int32)
+                check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, 1, C.byref(fc), arr([cur_mp.data_ptr()]),
+                                                                      C.byref(fl), arr([k[t - 1].data_ptr()]),
+                                                                      arr([last_mp.data_ptr()]),
+                                                                      arr([d_outlier.data_ptr()]), C.byref(mp), 7.0, 0,
+                                                                      ptr(nm1)), "SearchByProjection(Last)")
+                pf = pose_frame(int(nL[0]), Tpred.data_ptr(), cur_mp.data_ptr(), pos[q].data_ptr(), k[t].data_ptr(),
+                                uR[t].data_ptr(), isig.data_ptr(), 8, float(fx), float(fy), float(cx), float(cy),
+                                float(mbf))
+                ni = np.zeros(1, np.int32)
+                check(L.Optimizer_PoseOptimization_frames_device(1, C.byref(pf), arr([T1.data_ptr()]),
+                                                                 arr([o1.data_ptr()]), ptr(ni)), "PoseOptimization")
+                with torch.cuda.stream(match_stream):
+                    sl = torch.cat([slot[q:t].reshape(-1), slot.new_full((K_LOCAL * cap + 1 - nloc,), -1)])
+                    skip.copy_((sl < 0).to(torch.uint8))
+                    skip.scatter_(0, torch.where(cur_mp >= 0, cur_mp, torch.full_like(cur_mp, K_LOCAL * cap)).long(),
+                                  torch.ones(cap, dtype=torch.uint8, device=dev))
+                    cur_mp.copy_(torch.where(o1.bool(), torch.full_like(cur_mp, -1), cur_mp))
+                fc.Tcw = T1.data_ptr()
+                lmap = orb_localmap(nloc, pos[q].data_ptr(), d[q].data_ptr(), d_obs.data_ptr(), maxd[q].data_ptr(),
+                                    mind[q].data_ptr(), nrm[q].data_ptr(), skip.data_ptr())
+                nm2, nv2 = np.zeros(1, np.int32), np.zeros(1, np.int32)
+                check(L.ORBmatcher_SearchLocalPoints_batch(m._h, 1, C.byref(fc), arr([cur_mp.data_ptr()]),
+                                                           C.byref(lmap), float(lsf), 1.0, ptr(nm2), ptr(nv2)),
+                      "SearchLocalPoints")
+                pf.Tcw = T1.data_ptr()
+                check(L.Optimizer_PoseOptimization_frames_device(1, C.byref(pf), arr([T2.data_ptr()]),
+                                                                 arr([o2.data_ptr()]), ptr(ni)), "PoseOptimization 2")
+                Tcw.append(T2.cpu().numpy().reshape(4, 4).copy())
+                nmatch.append(int(nm1[0] + nm2[0]))
+            last_n = nL
+            walls.append((time.perf_counter() - t0) * 1e3)
+        w = np.array(walls[2:])   # the first two frames have no motion model / local map yet
+        err = [float(np.abs(Tcw[t][:3, :3] - Tabs[t][:3, :3]).max()) for t in range(1, len(Tcw))]
+        return {"metric": "tracking latency per stereo frame (batch 1, sequential)", "mean_ms": round(float(w.mean()), 3),
+                "p50_ms": round(float(np.percentile(w, 50)), 3), "p90_ms": round(float(np.percentile(w, 90)), 3),
+                "frames": int(len(w)), "matches_per_frame": round(float(np.mean(nmatch)), 1),
+                "max_rotation_error": round(max(err), 6),
+                "note": "Frame(imLeft, imRight) + TrackWithMotionModel + TrackLocalMap per frame, synchronous C-ABI "
+                        "calls; pose t from pose t-1 and t-2 (constant-velocity model)"}
 
     def matcher_pass(lane, reps):
         """Isolated matcher launches with device timing and work counters:
@@ -394,6 +593,7 @@ def main():
 
     stage_acc = {}
     phase_acc = {}
+    local_acc = []
     pose_inl = []
     kernel_ms = []   # k_fast_cells duration per step (HIP events on the extractor streams)
     lanes = [Lane(), Lane()]
@@ -437,6 +637,7 @@ def main():
     phase_acc.clear()
     kernel_ms.clear()
     pose_inl.clear()
+    local_acc.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -517,6 +718,7 @@ def main():
     mroof = matcher_pass(lanes[0], ROOFLINE_REPS)
     if args.passes_only:
         return
+    latency = latency_leg(24)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -540,15 +742,20 @@ def main():
             "data": "synthetic (seeded KITTI-shaped textured stereo frames: camera-rotation motion, "
                     "ground-plane disparity field 4..40 px)",
             "config": {"workload": "kitti00_stereo: ORB extract L+R, ComputeStereoMatches, "
-                                   "SearchByProjection(Cur,Last,th=7), PoseOptimization", "width": W, "height": H,
+                                   "TrackWithMotionModel (UpdateLastFrame, SearchByProjection(Cur,Last,th=7), "
+                                   "PoseOptimization), TrackLocalMap (isInFrustum + SearchByProjection(F, local map "
+                                   f"of the last {K_LOCAL} frames' map points, th=1) + PoseOptimization)",
+                       "width": W, "height": H,
                        "nfeatures": NFEAT, "nlevels": 8, "scale_factor": 1.2, "fast_th": [20, 7],
                        "stereo_frames_per_step": B, "parallelism": f"replicas{world}", "extractor_cu_reserve": args.reserve_cus},
             "matches_per_s": round(tot_match / dt, 1), "stereo_matches_per_s": round(tot_stereo / dt, 1),
             "keypoints_per_image": round(tot_kp / (2 * frames_total), 1),
             "pose_inliers_per_frame": round(float(np.sum(pose_inl)) / max(len(pose_inl) * P, 1), 1),
+            "local_map_matches_per_frame": round(float(sum(a for a, _ in local_acc)) / max(len(local_acc) * P, 1), 1),
+            "local_map_visible_per_frame": round(float(sum(b for _, b in local_acc)) / max(len(local_acc) * P, 1), 1),
             "stage_ms_per_step": stage_ms,
             "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}, "roofline": roof,
-            "matcher_roofline": mroof, "cpu_baseline": cpu, "local_ba": ba,
+            "matcher_roofline": mroof, "latency": latency, "cpu_baseline": cpu, "local_ba": ba,
             "global_ba": gba,
         }
         json_out.write(json.dumps(out) + "\n")
@@ -749,8 +956,11 @@ def ba_cpu_baseline(budget_s):
 
 class _CpuStream:
     """One reference-structured CPU tracking stream on the oracle (line-faithful C restatement):
-    per stereo frame extract L and R, ComputeStereoMatches, SearchByProjection(Cur, Last, 7),
-    PoseOptimization.  The oracle's C calls release the GIL, so streams run on separate cores."""
+    per stereo frame extract L and R, ComputeStereoMatches, TrackWithMotionModel (UnprojectStereo,
+    SearchByProjection(Cur, Last, 7), PoseOptimization) and TrackLocalMap (isInFrustum +
+    SearchByProjection(F, local map, 1) + PoseOptimization) over the map points of the last
+    K_LOCAL frames -- the GPU step's work.  The oracle's C calls release the GIL, so streams run
+    on separate cores."""
 
     def __init__(self, lefts, rights, Rs):
         sys.path.insert(0, str(ROOT / "tests"))
@@ -765,10 +975,26 @@ class _CpuStream:
         self.fx, self.fy, self.cx, self.cy = synthetic.intrinsics(W, H)
         self.mbf = np.float32(synthetic.KITTI_BF)
         self.mb = np.float32(self.mbf / np.float32(self.fx))
+        self.lsf = np.float32(np.log(np.float32(1.2)))
         self.synthetic = synthetic
-        self.prev = None
-        self.t = {"extract": 0.0, "stereo": 0.0, "match": 0.0, "pose": 0.0}
+        Tabs = [np.eye(4, dtype=np.float32)]
+        for R in Rs:
+            Tabs.append(synthetic.pose_from_rotation(np.asarray(R, np.float64) @ Tabs[-1][:3, :3].astype(np.float64)))
+        self.Tabs = Tabs
+        self.hist = []   # the last K_LOCAL frames: (keys, desc, depth, map point block)
+        self.t = {"extract": 0.0, "stereo": 0.0, "match": 0.0, "pose": 0.0, "local_map": 0.0}
         self.done = 0
+
+    def _block(self, k, d, dep, i):
+        """UnprojectStereo of frame i with its absolute Twc + UpdateNormalAndDepth."""
+        Twc = np.linalg.inv(self.Tabs[i]).astype(np.float32)
+        X, slot = self.ol.oracle_unproject_stereo(k, dep, Twc, self.fx, self.fy, self.cx, self.cy)
+        X = np.nan_to_num(X)
+        PO = X - Twc[:3, 3]
+        dist = np.maximum(np.linalg.norm(PO, axis=1), 1e-6).astype(np.float32)
+        mx = (dist * self.scale[np.clip(k["octave"], 0, 7)]).astype(np.float32)
+        return dict(pos=X, desc=d, slot=slot, normal=(PO / dist[:, None]).astype(np.float32), max_dist=mx,
+                    min_dist=(mx / self.scale[7]).astype(np.float32))
 
     def frame(self, i):
         from c_orb_slam_amd.orb import Frame, MapPoints
@@ -781,26 +1007,45 @@ class _CpuStream:
         tc = time.perf_counter()
         self.t["extract"] += tb - ta
         self.t["stereo"] += tc - tb
-        if self.prev is not None and i != 0:
-            pk, pd, pdep = self.prev
-            last = Frame(pk, pd, self.scale, np.eye(4, dtype=np.float32), fx, fy, cx, cy, mbf, W, H)
-            cur = Frame(kL, dL, self.scale, self.synthetic.pose_from_rotation(self.Rs[i - 1]), fx, fy, cx, cy, mbf,
-                        W, H, uRight=uR)
-            X, lm = ol.oracle_unproject_stereo(pk, pdep, np.eye(4, dtype=np.float32), fx, fy, cx, cy)
-            X = np.nan_to_num(X)
-            mps = MapPoints(X, pd, np.ones(len(pk), np.int32))
+        if i == 0:
+            self.hist = []
+        if self.hist:
+            pk, pd, pdep = self.hist[-1][:3]
+            self.hist[-1] = self.hist[-1][:3] + (self._block(pk, pd, pdep, i - 1),)   # UpdateLastFrame
+            blocks = [h[3] for h in self.hist]
+            off = np.cumsum([0] + [len(b["pos"]) for b in blocks])
+            M = {k: np.concatenate([b[k] for b in blocks]) for k in ("pos", "desc", "normal", "max_dist", "min_dist")}
+            M["obs"] = np.ones(len(M["pos"]), np.int32)
+            nolm = np.concatenate([b["slot"] < 0 for b in blocks])
+            last = Frame(pk, pd, self.scale, self.Tabs[i - 1], fx, fy, cx, cy, mbf, W, H)
+            cur = Frame(kL, dL, self.scale, self.Tabs[i], fx, fy, cx, cy, mbf, W, H, uRight=uR)
+            lm = np.where(blocks[-1]["slot"] >= 0, blocks[-1]["slot"] + off[-2], -1).astype(np.int32)
+            mps = MapPoints(M["pos"], M["desc"], M["obs"])
             cm = np.full(cur.N, -1, np.int32)
             td = time.perf_counter()
             ol.oracle_search_last(cur, cm, last, pk, lm, np.zeros(len(pk), np.uint8), mps, 7.0, False, 0.9, True)
             te = time.perf_counter()
             self.t["match"] += te - td
-            has = (cm >= 0).astype(np.uint8)
-            pr = dict(Tcw=cur.Tcw, has_mp=has, Xw=X[np.maximum(cm, 0)],
-                      obs=np.stack([kL["x"], kL["y"], uR], 1).astype(np.float32),
-                      inv_sigma2=self.isig[kL["octave"]].astype(np.float32), cam=(fx, fy, cx, cy, mbf))
-            ol.oracle_pose_optimization(pr)
-            self.t["pose"] += time.perf_counter() - te
-        self.prev = (kL, dL, dep)
+            obs = np.stack([kL["x"], kL["y"], uR], 1).astype(np.float32)
+            isg = self.isig[kL["octave"]].astype(np.float32)
+            pr = dict(Tcw=cur.Tcw, has_mp=(cm >= 0).astype(np.uint8), Xw=M["pos"][np.maximum(cm, 0)], obs=obs,
+                      inv_sigma2=isg, cam=(fx, fy, cx, cy, mbf))
+            o1 = ol.oracle_pose_optimization(pr)
+            tf = time.perf_counter()
+            self.t["pose"] += tf - te
+            # TrackLocalMap: discard outliers, skip points in the frame, SearchLocalPoints, PoseOptimization
+            skip = nolm.copy()
+            skip[cm[cm >= 0]] = True
+            cm[o1["outlier"].astype(bool)] = -1
+            M["skip"] = skip.astype(np.uint8)
+            cur.Tcw = np.ascontiguousarray(o1["Tcw"], np.float32)
+            ol.oracle_search_local_points(cur, cm, M, self.lsf, 1.0, 0.8)
+            pr2 = dict(Tcw=cur.Tcw, has_mp=(cm >= 0).astype(np.uint8), Xw=M["pos"][np.maximum(cm, 0)], obs=obs,
+                       inv_sigma2=isg, cam=(fx, fy, cx, cy, mbf))
+            ol.oracle_pose_optimization(pr2)
+            self.t["local_map"] += time.perf_counter() - tf
+        self.hist.append((kL, dL, dep))
+        self.hist = self.hist[-K_LOCAL:]
         self.done += 1
 
     def run(self, start, budget_s, min_frames):
@@ -841,13 +1086,15 @@ def cpu_baseline(lefts, rights, Rs, budget_s):
     return {"value": round(fpsP, 3), "unit": "frames/s", "cores": P, "kind": "port",
             "sample": f"{P} independent reference-structured streams on {P} threads ({_cpu_model()}; affinity {aff}, "
                       f"cgroup quota {quota}): oracle ORBextractor x2 + ComputeStereoMatches + "
-                      f"SearchByProjection(Cur,Last,7) + PoseOptimization per stereo frame, C restatement built "
+                      f"SearchByProjection(Cur,Last,7) + PoseOptimization + TrackLocalMap (isInFrustum + "
+                      f"SearchByProjection(F, local map, 1) + PoseOptimization) per stereo frame, C restatement built "
                       f"{flags}; {framesP} frames in {max(walls):.1f} s",
             "single_thread": {"value": round(fps1, 3), "unit": "frames/s", "cores": 1,
                               "sample": f"{one.done} frames on 1 thread: extract {t['extract'] / one.done * 1e3:.1f} "
                                         f"ms/frame, stereo {t['stereo'] / one.done * 1e3:.2f} ms, match "
                                         f"{t['match'] / max(one.done - 1, 1) * 1e3:.2f} ms, pose "
-                                        f"{t['pose'] / max(one.done - 1, 1) * 1e3:.2f} ms"}}
+                                        f"{t['pose'] / max(one.done - 1, 1) * 1e3:.2f} ms, local map "
+                                        f"{t['local_map'] / max(one.done - 1, 1) * 1e3:.2f} ms"}}
 
 
 if __name__ == "__main__":
