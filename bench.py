@@ -163,7 +163,7 @@ def main():
     gH = np.float32(np.float32(48) / np.float32(H))
     P = B - 1
     arr = lambda xs: (C.c_void_p * len(xs))(*xs)
-    from c_orb_slam_amd._lib import orb_unproject, pose_frame, orb_localmap
+    from c_orb_slam_amd._lib import orb_unproject, pose_frame, orb_localmap, orb_newpoints, orb_localprep
     lsf = np.float32(np.log(np.float32(1.2)))   # Frame::mfLogScaleFactor
     from concurrent.futures import ThreadPoolExecutor
     # HIP's current device is per thread: every worker binds it first
@@ -200,12 +200,11 @@ def main():
             self.d_depth = torch.empty((B, cap), dtype=torch.float32, device=dev)   # mvDepth
             self.d_mp_pos = torch.zeros((B, cap, 3), dtype=torch.float32, device=dev)
             self.d_slot = torch.empty((B, cap), dtype=torch.int32, device=dev)      # UnprojectStereo slots
-            self.d_last_mp = torch.empty((P, cap), dtype=torch.int32, device=dev)   # LastFrame.mvpMapPoints
             self.d_cur_mp = torch.empty((B, cap), dtype=torch.int32, device=dev)
             self.d_maxd = torch.zeros((B, cap), dtype=torch.float32, device=dev)    # MapPoint::mfMaxDistance
             self.d_mind = torch.zeros((B, cap), dtype=torch.float32, device=dev)
             self.d_nrm = torch.zeros((B, cap, 3), dtype=torch.float32, device=dev)
-            self.d_skip = torch.ones((P, K_LOCAL * cap + 1), dtype=torch.uint8, device=dev)
+            self.d_skip = torch.ones((P, K_LOCAL * cap), dtype=torch.uint8, device=dev)
             self.scale = torch.from_numpy(self.exL.GetScaleFactors()).to(dev)
             self.d_Tout = torch.empty((P, 16), dtype=torch.float32, device=dev)
             self.d_Tout2 = torch.empty((P, 16), dtype=torch.float32, device=dev)
@@ -213,18 +212,12 @@ def main():
             self.d_poutl2 = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
             self.isig_tab = torch.from_numpy(self.exL.GetInverseScaleSigmaSquares()).to(dev)
             self.bs = [max(0, p - K_LOCAL + 1) for p in range(P)]                   # first local block of pair p
-            self.loc_off = torch.tensor([(p - self.bs[p]) * cap for p in range(P)], dtype=torch.int32, device=dev)
             # ctypes views of the batch, built once (device pointers do not move; only counts change)
             self.curs = (orb_frame * P)(*[self.frame_struct(b, d_Tcw[b].data_ptr()) for b in range(1, B)])
             # TrackLocalMap sees mCurrentFrame.mTcw as set by the first PoseOptimization
             self.curs_local = (orb_frame * P)(*[self.frame_struct(b, self.d_Tout[b - 1].data_ptr())
                                                 for b in range(1, B)])
-            # gather rows: local-map row j of pair p <- table row bs[p]*cap + j (sentinel: no row)
-            gi = np.full((P, K_LOCAL * cap + 1), B * cap, np.int64)
-            for p_ in range(P):
-                q_ = max(0, p_ - K_LOCAL + 1)
-                gi[p_, :(p_ - q_ + 1) * cap] = np.arange(q_ * cap, (p_ + 1) * cap)
-            self.skip_rows = torch.from_numpy(gi).to(dev)
+
             self.lasts = (orb_frame * P)(*[self.frame_struct(b, d_Tcw[b].data_ptr()) for b in range(0, B - 1)])
             self.mps = (orb_mappoints * P)()
             self.lmaps = (orb_localmap * P)()
@@ -239,7 +232,7 @@ def main():
                                              self.d_nrm[q].data_ptr(), self.d_skip[p].data_ptr())
             self.a_cur_mp = arr([self.d_cur_mp[b].data_ptr() for b in range(1, B)])
             self.a_last_kps = arr([self.d_kps[b].data_ptr() for b in range(P)])
-            self.a_last_mp = arr([self.d_last_mp[b].data_ptr() for b in range(P)])
+            self.a_last_mp = arr([self.d_slot[b].data_ptr() for b in range(P)])   # LastFrame.mvpMapPoints
             self.a_last_out = arr([d_outlier.data_ptr()] * P)
             self.s_kL = arr([self.d_kps[b].data_ptr() for b in range(B)])
             self.s_dL = arr([self.d_desc[b].data_ptr() for b in range(B)])
@@ -247,12 +240,19 @@ def main():
             self.s_dR = arr([self.d_descR[b].data_ptr() for b in range(B)])
             self.s_uR = arr([self.d_uR[b].data_ptr() for b in range(B)])
             self.s_dep = arr([self.d_depth[b].data_ptr() for b in range(B)])
-            # UpdateLastFrame / CreateNewKeyFrame: Frame::UnprojectStereo of frame b's stereo keypoints
-            # with its absolute Twc -> block b of the map point table
-            self.unp = (orb_unproject * B)(*[
-                orb_unproject(0, self.d_kps[b].data_ptr(), self.d_depth[b].data_ptr(), d_Twc[b].data_ptr(), float(fx),
-                              float(fy), float(cx), float(cy), self.d_mp_pos[b].data_ptr(),
-                              self.d_slot[b].data_ptr()) for b in range(B)])
+            # UpdateLastFrame / CreateNewKeyFrame: new MapPoints from frame b's stereo keypoints
+            # (UnprojectStereo with its absolute Twc + UpdateNormalAndDepth) -> block b of the
+            # table; row ids relative to the local map of pair b, whose last frame b is
+            self.newp = (orb_newpoints * B)(*[
+                orb_newpoints(0, self.d_kps[b].data_ptr(), self.d_depth[b].data_ptr(), d_Twc[b].data_ptr(),
+                              float(fx), float(fy), float(cx), float(cy), self.scale.data_ptr(), 8,
+                              (b - max(0, b - K_LOCAL + 1)) * cap, self.d_mp_pos[b].data_ptr(),
+                              self.d_slot[b].data_ptr(), self.d_nrm[b].data_ptr(), self.d_maxd[b].data_ptr(),
+                              self.d_mind[b].data_ptr()) for b in range(B)])
+            self.prep = (orb_localprep * P)(*[
+                orb_localprep(0, self.d_cur_mp[p + 1].data_ptr(), self.d_poutl[p].data_ptr(),
+                              (p - self.bs[p] + 1) * cap, self.d_slot[self.bs[p]].data_ptr(),
+                              self.d_skip[p].data_ptr()) for p in range(P)])
             # PoseOptimization(&mCurrentFrame): the frame's own arrays, map points by local-map index;
             # TrackWithMotionModel's call from the motion-model pose, TrackLocalMap's from its result
             self.pframes = (pose_frame * P)(*[
@@ -269,7 +269,8 @@ def main():
             self.a_poutl = arr([self.d_poutl[p].data_ptr() for p in range(P)])
             self.a_Tout2 = arr([self.d_Tout2[p].data_ptr() for p in range(P)])
             self.a_poutl2 = arr([self.d_poutl2[p].data_ptr() for p in range(P)])
-            self.n_unp = n_field(self.unp, orb_unproject, B)
+            self.n_unp = n_field(self.newp, orb_newpoints, B)
+            self.n_prep = n_field(self.prep, orb_localprep, P)
             self.n_cur = n_field(self.curs, orb_frame, P)
             self.n_last = n_field(self.lasts, orb_frame, P)
             self.n_pose = n_field(self.pframes, pose_frame, P)
@@ -328,17 +329,8 @@ def main():
             self.n_pose2[:] = nL[1:]
             with torch.cuda.stream(match_stream):
                 self.d_slot.fill_(-1)
-            check(L.Frame_UnprojectStereo_batch_device(m._h, B, self.unp), "UnprojectStereo batch")
-            with torch.cuda.stream(match_stream):
-                Ow = d_Twc.view(B, 4, 4)[:, :3, 3]
-                PO = self.d_mp_pos - Ow[:, None, :]
-                dist = torch.linalg.vector_norm(PO, dim=2)
-                self.d_nrm.copy_(PO / dist.clamp_min(1e-6)[..., None])
-                self.d_maxd.copy_(dist * self.scale[self.d_kps[:, :, 5].clamp(0, 7).long()])
-                self.d_mind.copy_(self.d_maxd / self.scale[7])
-                lm = self.d_slot[:P]
-                self.d_last_mp.copy_(torch.where(lm >= 0, lm + self.loc_off[:, None], lm))
                 self.d_cur_mp.fill_(-1)
+            check(L.MapPoint_CreateStereo_batch_device(m._h, B, self.newp), "MapPoint_CreateStereo batch")
             # TrackWithMotionModel: SearchByProjection(CurrentFrame, LastFrame, th=7, stereo) (Tracking.cc:869-885)
             check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, P, self.curs, self.a_cur_mp, self.lasts,
                                                                   self.a_last_kps, self.a_last_mp, self.a_last_out,
@@ -351,14 +343,8 @@ def main():
             (SearchLocalPoints 1146-1161) and the table rows without a map point, isInFrustum +
             SearchByProjection(F, mvpLocalMapPoints, th=1) (stereo, ORBmatcher(0.8)), then the
             second PoseOptimization."""
-            with torch.cuda.stream(match_stream):
-                cm = self.d_cur_mp[1:]
-                # local-map rows without a map point (no stereo depth / past the frame's N)
-                slot = torch.cat([self.d_slot.reshape(-1), self.d_slot.new_full((1,), -1)])
-                self.d_skip.copy_((slot[self.skip_rows] < 0).to(torch.uint8))
-                sk = torch.where(cm >= 0, cm, torch.full_like(cm, K_LOCAL * cap)).long()
-                self.d_skip.scatter_(1, sk, 1)
-                cm.copy_(torch.where(self.d_poutl.bool(), torch.full_like(cm, -1), cm))
+            self.n_prep[:] = self.nL[1:]
+            check(L.Tracking_PrepareLocalSearch_batch_device(m._h, P, self.prep), "PrepareLocalSearch batch")
             self.n_curl[:] = self.nL[1:]
             check(L.ORBmatcher_SearchLocalPoints_batch(m._h, P, self.curs_local, self.a_cur_mp, self.lmaps,
                                                        float(lsf), 1.0, ptr(self.nml), ptr(self.nvis)),
@@ -411,9 +397,8 @@ def main():
         maxd = torch.zeros((nf, cap), dtype=torch.float32, device=dev)
         mind = torch.zeros((nf, cap), dtype=torch.float32, device=dev)
         nrm = torch.zeros((nf, cap, 3), dtype=torch.float32, device=dev)
-        skip = torch.ones(K_LOCAL * cap + 1, dtype=torch.uint8, device=dev)
+        skip = torch.ones(K_LOCAL * cap, dtype=torch.uint8, device=dev)
         cur_mp = torch.full((cap,), -1, dtype=torch.int32, device=dev)
-        last_mp = torch.full((cap,), -1, dtype=torch.int32, device=dev)
         Tpred = torch.zeros(16, dtype=torch.float32, device=dev)
         Tlast = torch.zeros(16, dtype=torch.float32, device=dev)
         Twc_l = torch.zeros(16, dtype=torch.float32, device=dev)
@@ -440,23 +425,19 @@ def main():
             if t > 0:
                 V = Tcw[t - 1] @ np.linalg.inv(Tcw[t - 2]) if t >= 2 else np.eye(4, dtype=np.float32)
                 Tp = (V @ Tcw[t - 1]).astype(np.float32)
-                Tpred.copy_(torch.from_numpy(Tp.reshape(16)))
-                Tlast.copy_(torch.from_numpy(Tcw[t - 1].reshape(16)))
-                Twc_l.copy_(torch.from_numpy(np.linalg.inv(Tcw[t - 1]).astype(np.float32).reshape(16)))
                 nlast = int(last_n[0])
-                u = orb_unproject(nlast, k[t - 1].data_ptr(), dep[t - 1].data_ptr(), Twc_l.data_ptr(), float(fx),
-                                  float(fy), float(cx), float(cy), pos[t - 1].data_ptr(), slot[t - 1].data_ptr())
-                check(L.Frame_UnprojectStereo_batch_device(m._h, 1, C.byref(u)), "UnprojectStereo")
                 q = max(0, t - K_LOCAL)
                 nloc = (t - q) * cap
-                with torch.cuda.stream(match_stream):
-                    PO = pos[t - 1] - Twc_l.view(4, 4)[:3, 3]
-                    dist = torch.linalg.vector_norm(PO, dim=1)
-                    nrm[t - 1].copy_(PO / dist.clamp_min(1e-6)[:, None])
-                    maxd[t - 1].copy_(dist * scale[k[t - 1, :, 5].clamp(0, 7).long()])
-                    mind[t - 1].copy_(maxd[t - 1] / scale[7])
-                    last_mp.copy_(torch.where(slot[t - 1] >= 0, slot[t - 1] + (t - 1 - q) * cap, slot[t - 1]))
+                with torch.cuda.stream(match_stream):   # ordered before the matcher's launches
+                    Tpred.copy_(torch.from_numpy(Tp.reshape(16)))
+                    Tlast.copy_(torch.from_numpy(Tcw[t - 1].reshape(16)))
+                    Twc_l.copy_(torch.from_numpy(np.linalg.inv(Tcw[t - 1]).astype(np.float32).reshape(16)))
                     cur_mp.fill_(-1)
+                u = orb_newpoints(nlast, k[t - 1].data_ptr(), dep[t - 1].data_ptr(), Twc_l.data_ptr(), float(fx),
+                                  float(fy), float(cx), float(cy), scale.data_ptr(), 8, (t - 1 - q) * cap,
+                                  pos[t - 1].data_ptr(), slot[t - 1].data_ptr(), nrm[t - 1].data_ptr(),
+                                  maxd[t - 1].data_ptr(), mind[t - 1].data_ptr())
+                check(L.MapPoint_CreateStereo_batch_device(m._h, 1, C.byref(u)), "MapPoint_CreateStereo")
                 fc = lanes[0].frame_struct(0, Tpred.data_ptr())
                 fc.keysUn, fc.desc, fc.uRight, fc.N = k[t].data_ptr(), d[t].data_ptr(), uR[t].data_ptr(), int(nL[0])
                 fl = lanes[0].frame_struct(0, Tlast.data_ptr())
@@ -465,7 +446,7 @@ def main():
                 nm1 = np.zeros(1, np.int32)
                 check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, 1, C.byref(fc), arr([cur_mp.data_ptr()]),
                                                                       C.byref(fl), arr([k[t - 1].data_ptr()]),
-                                                                      arr([last_mp.data_ptr()]),
+                                                                      arr([slot[t - 1].data_ptr()]),
                                                                       arr([d_outlier.data_ptr()]), C.byref(mp), 7.0, 0,
                                                                       ptr(nm1)), "SearchByProjection(Last)")
                 pf = pose_frame(int(nL[0]), Tpred.data_ptr(), cur_mp.data_ptr(), pos[q].data_ptr(), k[t].data_ptr(),
@@ -474,12 +455,9 @@ def main():
                 ni = np.zeros(1, np.int32)
                 check(L.Optimizer_PoseOptimization_frames_device(1, C.byref(pf), arr([T1.data_ptr()]),
                                                                  arr([o1.data_ptr()]), ptr(ni)), "PoseOptimization")
-                with torch.cuda.stream(match_stream):
-                    sl = torch.cat([slot[q:t].reshape(-1), slot.new_full((K_LOCAL * cap + 1 - nloc,), -1)])
-                    skip.copy_((sl < 0).to(torch.uint8))
-                    skip.scatter_(0, torch.where(cur_mp >= 0, cur_mp, torch.full_like(cur_mp, K_LOCAL * cap)).long(),
-                                  torch.ones(cap, dtype=torch.uint8, device=dev))
-                    cur_mp.copy_(torch.where(o1.bool(), torch.full_like(cur_mp, -1), cur_mp))
+                prep = orb_localprep(int(nL[0]), cur_mp.data_ptr(), o1.data_ptr(), nloc, slot[q].data_ptr(),
+                                     skip.data_ptr())
+                check(L.Tracking_PrepareLocalSearch_batch_device(m._h, 1, C.byref(prep)), "PrepareLocalSearch")
                 fc.Tcw = T1.data_ptr()
                 lmap = orb_localmap(nloc, pos[q].data_ptr(), d[q].data_ptr(), d_obs.data_ptr(), maxd[q].data_ptr(),
                                     mind[q].data_ptr(), nrm[q].data_ptr(), skip.data_ptr())

@@ -57,6 +57,18 @@ class orb_mappoints(C.Structure):
     _fields_ = [("n", C.c_int), ("pos", C.c_void_p), ("desc", C.c_void_p), ("observations", C.c_void_p)]
 
 
+class orb_newpoints(C.Structure):
+    _fields_ = [("N", C.c_int), ("keysUn", C.c_void_p), ("depth", C.c_void_p), ("Twc", C.c_void_p),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("scaleFactors", C.c_void_p), ("nlevels", C.c_int), ("row_base", C.c_int32), ("x3D", C.c_void_p),
+                ("row", C.c_void_p), ("normal", C.c_void_p), ("max_dist", C.c_void_p), ("min_dist", C.c_void_p)]
+
+
+class orb_localprep(C.Structure):
+    _fields_ = [("N", C.c_int), ("cur_mp", C.c_void_p), ("outlier", C.c_void_p), ("n", C.c_int),
+                ("row", C.c_void_p), ("skip", C.c_void_p)]
+
+
 class orb_localmap(C.Structure):
     _fields_ = [("n", C.c_int), ("pos", C.c_void_p), ("desc", C.c_void_p), ("observations", C.c_void_p),
                 ("max_dist", C.c_void_p), ("min_dist", C.c_void_p), ("normal", C.c_void_p), ("skip", C.c_void_p)]
@@ -164,6 +176,8 @@ def lib():
     L.orbgpu_unit_ldlt_solve.argtypes = [i32, vp, vp, vp, i32, P(i32)]
     L.orbgpu_unit_csum.argtypes = [vp, i32, vp]
     L.orbgpu_unit_pnp_layout.argtypes = [i32, vp, vp, vp, vp]
+    L.MapPoint_CreateStereo_batch_device.argtypes = [vp, i32, vp]
+    L.Tracking_PrepareLocalSearch_batch_device.argtypes = [vp, i32, vp]
     L.ORBmatcher_SearchLocalPoints_batch.argtypes = [vp, i32, vp, vp, vp, f32, f32, vp, vp]
     L.Frame_isInFrustum_batch.argtypes = [vp, i32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp]
     L.ORBmatcher_enable_timing.argtypes = [vp, i32]

@@ -164,4 +164,55 @@ int Frame_UnprojectStereo_batch_device(ORBmatcher_h h, int count, const orb_unpr
     return orbgpu::unproject_batch(P.data(), count, h->m->stream()) ? ORB_E_HIP : ORB_OK;
 }
 
+int MapPoint_CreateStereo_batch_device(ORBmatcher_h h, int count, const orb_newpoints* Q) {
+    if (!h || count < 0 || (count > 0 && !Q)) return ORB_E_INVALID;
+    if (count == 0) return ORB_OK;
+    std::vector<orbgpu::UnprojDev> P((size_t)count);
+    for (int f = 0; f < count; f++) {
+        const orb_newpoints& q = Q[f];
+        if (q.N < 0 || (q.N > 0 && (!q.keysUn || !q.depth || !q.Twc || !q.x3D || !q.row || !q.normal ||
+                                    !q.max_dist || !q.min_dist || !q.scaleFactors || q.nlevels <= 0)))
+            return ORB_E_INVALID;
+        orbgpu::UnprojDev& d = P[f];
+        std::memset(&d, 0, sizeof(d));
+        d.N = q.N;
+        d.keys = (const orbgpu::orb_kp_dev*)q.keysUn;
+        d.depth = q.depth;
+        d.Twc = q.Twc;
+        d.fx = q.fx; d.fy = q.fy; d.cx = q.cx; d.cy = q.cy;
+        d.invfx = 1.0f / q.fx;
+        d.invfy = 1.0f / q.fy;
+        d.x3D = q.x3D;
+        d.mp = q.row;
+        d.mp_base = q.row_base;
+        d.normal = q.normal;
+        d.maxDist = q.max_dist;
+        d.minDist = q.min_dist;
+        d.scale = q.scaleFactors;
+        d.nlevels = q.nlevels;
+    }
+    return orbgpu::unproject_batch(P.data(), count, h->m->stream()) ? ORB_E_HIP : ORB_OK;
+}
+
+int Tracking_PrepareLocalSearch_batch_device(ORBmatcher_h h, int count, const orb_localprep* Q) {
+    if (!h || count < 0 || (count > 0 && !Q)) return ORB_E_INVALID;
+    if (count == 0) return ORB_OK;
+    orbgpu::Matcher* m = h->m;
+    std::vector<orbgpu::LocalPrepDev> P((size_t)count);
+    for (int f = 0; f < count; f++) {
+        const orb_localprep& q = Q[f];
+        if (q.N < 0 || q.n < 0 || (q.N > 0 && (!q.cur_mp || !q.outlier)) || (q.n > 0 && (!q.row || !q.skip)))
+            return ORB_E_INVALID;
+        P[f] = orbgpu::LocalPrepDev{q.N, q.cur_mp, q.outlier, q.n, q.row, q.skip};
+    }
+    if (m->arena_reserve(sizeof(orbgpu::LocalPrepDev) * count + 256)) return ORB_E_HIP;
+    void* d = m->arena_alloc(sizeof(orbgpu::LocalPrepDev) * count);
+    hipStream_t s = m->stream();
+    if (!d || hipMemcpyAsync(d, P.data(), sizeof(orbgpu::LocalPrepDev) * count, hipMemcpyHostToDevice, s) != hipSuccess)
+        return ORB_E_HIP;
+    if (orbgpu::local_prep_batch((const orbgpu::LocalPrepDev*)d, count, s)) return ORB_E_HIP;
+    // the staging copy is pageable: finish before the host vector goes away
+    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+}
+
 }  // extern "C"

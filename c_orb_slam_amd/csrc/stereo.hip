@@ -306,17 +306,60 @@ __global__ void __launch_bounds__(256) k_unproject(UnprojBatch B) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.N) return;
     const float z = P.depth[i];
-    if (P.mp) P.mp[i] = z > 0 ? i : -1;
+    if (P.mp) P.mp[i] = z > 0 ? P.mp_base + i : -1;
     if (!(z > 0)) return;
     const orb_kp_dev kp = P.keys[i];
     const float x = (kp.x - P.cx) * z * P.invfx;
     const float y = (kp.y - P.cy) * z * P.invfy;
     const float* T = P.Twc;
+    float X[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) {
         const double acc = (double)T[r * 4 + 0] * x + (double)T[r * 4 + 1] * y + (double)T[r * 4 + 2] * z;
-        P.x3D[3 * i + r] = (float)(acc + (double)T[r * 4 + 3]);
+        X[r] = (float)(acc + (double)T[r * 4 + 3]);
+        P.x3D[3 * i + r] = X[r];
     }
+    if (P.normal) {
+        // MapPoint::UpdateNormalAndDepth with the creating frame as the only observation
+        // (MapPoint.cc:331-371): cv::norm accumulated in double, normali / norm as a float
+        // scale of the float vector, mfMaxDistance = dist * mvScaleFactors[octave]
+        const float PO[3] = {X[0] - T[3], X[1] - T[7], X[2] - T[11]};
+        const double s2 = ((double)PO[0] * PO[0] + (double)PO[1] * PO[1]) + (double)PO[2] * PO[2];
+        const double nd = sqrt(s2);
+        const float inv = (float)(1.0 / nd);
+#pragma unroll
+        for (int r = 0; r < 3; r++) P.normal[3 * i + r] = PO[r] * inv;
+        const float dist = (float)nd;
+        const int lv = min(max(kp.octave, 0), P.nlevels - 1);
+        const float mx = dist * P.scale[lv];
+        P.maxDist[i] = mx;
+        P.minDist[i] = mx / P.scale[P.nlevels - 1];
+    }
+}
+
+// Tracking.cc:893-913 (TrackWithMotionModel discards the outliers of its PoseOptimization and
+// marks their points seen) + 1146-1161 (SearchLocalPoints skips the points already in the
+// frame): skip[j] = no map point in local-map row j, or row j in mvpMapPoints; then the outlier
+// rows of mvpMapPoints are cleared.  One workgroup per frame (the two phases are ordered).
+__global__ void __launch_bounds__(1024) k_local_prep(const LocalPrepDev* __restrict__ probs) {
+    ORBGPU_LATENCY_WAVE();
+    const LocalPrepDev& P = probs[blockIdx.x];
+    for (int j = threadIdx.x; j < P.n; j += blockDim.x) P.skip[j] = P.row[j] < 0 ? 1 : 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < P.N; i += blockDim.x) {
+        const int m = P.curMP[i];
+        if (m >= 0) {
+            if (m < P.n) P.skip[m] = 1;
+            if (P.outlier[i]) P.curMP[i] = -1;
+        }
+    }
+}
+
+int local_prep_batch(const LocalPrepDev* d_probs, int count, hipStream_t s) {
+    if (count <= 0) return 0;
+    hipLaunchKernelGGL(k_local_prep, dim3(count), dim3(1024), 0, s, d_probs);
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 int unproject_batch(const UnprojDev* probs, int count, hipStream_t s) {

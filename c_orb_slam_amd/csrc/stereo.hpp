@@ -56,7 +56,25 @@ struct UnprojDev {
     float fx, fy, cx, cy, invfx, invfy;
     float* x3D;
     int* mp;
+    // new map points (MapPoint_CreateStereo): row ids from mp_base, UpdateNormalAndDepth outputs
+    int mp_base;
+    float* normal;      // null: UnprojectStereo only
+    float* maxDist;
+    float* minDist;
+    const float* scale;
+    int nlevels;
 };
+
+// Tracking's bookkeeping between TrackWithMotionModel's PoseOptimization and SearchLocalPoints
+struct LocalPrepDev {
+    int N;
+    int* curMP;
+    const uint8_t* outlier;
+    int n;
+    const int* row;
+    uint8_t* skip;
+};
+int local_prep_batch(const LocalPrepDev* d_probs, int count, hipStream_t s);
 constexpr int kUnprojPerLaunch = 56;   // frames per launch, passed by value (kernel-argument space)
 // enqueue on `s` (no staging buffer: the frames are kernel arguments)
 int unproject_batch(const UnprojDev* probs, int count, hipStream_t s);

@@ -263,6 +263,45 @@ typedef struct orb_unproject {
 } orb_unproject;
 int Frame_UnprojectStereo_batch_device(ORBmatcher_h h, int count, const orb_unproject* U);
 
+/* New MapPoints from a stereo frame (Tracking::StereoInitialization / CreateNewKeyFrame /
+ * UpdateLastFrame, Tracking.cc:520-560, 1025-1080, 837-860): for every keypoint with depth > 0,
+ * x3D = UnprojectStereo(i) as above and MapPoint::UpdateNormalAndDepth (MapPoint.cc:331-371)
+ * with the frame as the only observation: normal = (x3D - mOw) / |x3D - mOw|, mfMaxDistance =
+ * |x3D - mOw| * mvScaleFactors[octave], mfMinDistance = mfMaxDistance / mvScaleFactors[nlevels-1].
+ * row[i] = row_base + i (the point's row in the caller's map table) for depth > 0, else -1.
+ * Device pointers; enqueued on ORBmatcher_stream. */
+typedef struct orb_newpoints {
+    int N;
+    const orb_kp* keysUn;        /* mvKeysUn (N) */
+    const float* depth;          /* mvDepth (N) */
+    const float* Twc;            /* 16 floats: [mRwc | mOw] */
+    float fx, fy, cx, cy;
+    const float* scaleFactors;   /* mvScaleFactors (nlevels) */
+    int nlevels;
+    int32_t row_base;
+    float* x3D;                  /* out: N x 3 */
+    int32_t* row;                /* out: N */
+    float* normal;               /* out: N x 3 (GetNormal) */
+    float* max_dist;             /* out: N (mfMaxDistance) */
+    float* min_dist;             /* out: N (mfMinDistance) */
+} orb_newpoints;
+int MapPoint_CreateStereo_batch_device(ORBmatcher_h h, int count, const orb_newpoints* P);
+
+/* Tracking's bookkeeping between TrackWithMotionModel and SearchLocalPoints: the outliers of
+ * the first PoseOptimization are dropped from mvpMapPoints and their points marked seen
+ * (Tracking.cc:893-913), the frame's points are skipped by SearchLocalPoints (1146-1161).
+ * skip[j] (out, n) = (row[j] < 0: no map point / isBad) or j in cur_mp; then cur_mp[i] = -1
+ * where outlier[i].  One launch for all frames; device pointers; synchronous. */
+typedef struct orb_localprep {
+    int N;
+    int32_t* cur_mp;             /* in/out (N): mvpMapPoints as local-map rows */
+    const uint8_t* outlier;      /* mvbOutlier (N) after PoseOptimization */
+    int n;                       /* local-map rows */
+    const int32_t* row;          /* n: < 0 = no map point */
+    uint8_t* skip;               /* out: n */
+} orb_localprep;
+int Tracking_PrepareLocalSearch_batch_device(ORBmatcher_h h, int count, const orb_localprep* P);
+
 /* ======================================================================
  * ORBVocabulary (reference include/ORBVocabulary.h: DBoW2::TemplatedVocabulary<
  * FORB::TDescriptor, FORB>, Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h)

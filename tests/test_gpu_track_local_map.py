@@ -126,3 +126,63 @@ def test_search_local_points_matches_oracle(gpu, seq, th):
         assert n2 == nvo and n1 == no
         assert np.array_equal(gc, oc), np.nonzero(gc != oc)[0][:10]
         assert no > 50
+
+
+def test_create_stereo_points_and_local_prep(gpu):
+    """MapPoint_CreateStereo_batch_device (UnprojectStereo + UpdateNormalAndDepth for one
+    observation) against the oracle's UnprojectStereo and the float / double convention written
+    out in numpy; Tracking_PrepareLocalSearch_batch_device against its definition."""
+    import ctypes as C
+    import torch
+    from c_orb_slam_amd._lib import lib, orb_newpoints, orb_localprep
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(3)
+    fx, fy, cx, cy = synthetic.intrinsics(W, H)
+    n = 1800
+    k = np.zeros(n, oracle_lib.KP_DTYPE)
+    k["x"] = rng.uniform(0, W, n)
+    k["y"] = rng.uniform(0, H, n)
+    k["octave"] = rng.integers(0, 8, n)
+    dep = rng.uniform(-5, 60, n).astype(np.float32)
+    a = rng.normal(0, 0.2, 3)
+    Rm = np.linalg.qr(np.eye(3) + np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]]))[0]
+    Twc = np.eye(4, dtype=np.float32)
+    Twc[:3, :3] = Rm
+    Twc[:3, 3] = rng.normal(0, 3, 3)
+    scale = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    dk, dd, dT, ds = t(k.view(np.int32).reshape(n, 7)), t(dep), t(Twc.reshape(16)), t(scale)
+    X = torch.zeros((n, 3), device=dev)
+    row = torch.full((n,), -7, dtype=torch.int32, device=dev)
+    nrm = torch.zeros((n, 3), device=dev)
+    mx, mn = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    m = gpu.ORBmatcher(0.8, False)
+    q = orb_newpoints(n, dk.data_ptr(), dd.data_ptr(), dT.data_ptr(), float(fx), float(fy), float(cx), float(cy),
+                      ds.data_ptr(), 8, 100, X.data_ptr(), row.data_ptr(), nrm.data_ptr(), mx.data_ptr(), mn.data_ptr())
+    assert lib().MapPoint_CreateStereo_batch_device(m._h, 1, C.byref(q)) == 0
+    torch.cuda.synchronize()
+    x3, slot = oracle_lib.oracle_unproject_stereo(k, dep, Twc, fx, fy, cx, cy)
+    ok = dep > 0
+    assert np.array_equal(row.cpu().numpy(), np.where(ok, 100 + np.arange(n), -1))
+    assert np.array_equal(X.cpu().numpy()[ok], x3[ok])
+    PO = (x3[ok] - Twc[:3, 3]).astype(np.float32)
+    nd = np.sqrt((PO[:, 0].astype(np.float64) * PO[:, 0] + PO[:, 1].astype(np.float64) * PO[:, 1]) +
+                 PO[:, 2].astype(np.float64) * PO[:, 2])
+    inv = (1.0 / nd).astype(np.float32)
+    assert np.array_equal(nrm.cpu().numpy()[ok], PO * inv[:, None])
+    mxo = nd.astype(np.float32) * scale[k["octave"][ok]]
+    assert np.array_equal(mx.cpu().numpy()[ok], mxo)
+    assert np.array_equal(mn.cpu().numpy()[ok], (mxo / scale[7]).astype(np.float32))
+    # PrepareLocalSearch: skip = no map point | in the frame; outliers dropped
+    nr, N = 5000, 1200
+    rows = np.where(rng.random(nr) < 0.2, -1, np.arange(nr)).astype(np.int32)
+    cm = np.where(rng.random(N) < 0.5, rng.integers(0, nr, N), -1).astype(np.int32)
+    outl = (rng.random(N) < 0.1).astype(np.uint8)
+    dcm, dout, drow = t(cm), t(outl), t(rows)
+    dskip = torch.full((nr,), 9, dtype=torch.uint8, device=dev)
+    pq = orb_localprep(N, dcm.data_ptr(), dout.data_ptr(), nr, drow.data_ptr(), dskip.data_ptr())
+    assert lib().Tracking_PrepareLocalSearch_batch_device(m._h, 1, C.byref(pq)) == 0
+    sk = (rows < 0).astype(np.uint8)
+    sk[cm[cm >= 0]] = 1
+    assert np.array_equal(dskip.cpu().numpy(), sk)
+    assert np.array_equal(dcm.cpu().numpy(), np.where((cm >= 0) & (outl == 1), -1, cm))
