@@ -23,6 +23,7 @@
 namespace orbgpu {
 
 constexpr int TH_HIGH = 100;  // ORBmatcher.cc:37
+constexpr int kSelectLocalThreads = 1024;
 constexpr int HISTO_LENGTH = 30;
 
 __device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
@@ -402,8 +403,8 @@ __global__ void __launch_bounds__(256) k_frustum(const SearchDev* __restrict__ p
 // query against the kTopK list, with a full rescan only when every kept candidate is
 // taken.  Overwrites (a later query re-taking a keypoint whose earlier taker has no
 // observations) keep the latest taker, as the reference's sequential assignment does.
-template <bool LAST>
-__global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ probs, float th, int bMono,
+template <bool LAST, int NT>
+__global__ void __launch_bounds__(NT) k_select(const SearchDev* __restrict__ probs, float th, int bMono,
                                                 float nnratio, int checkOri, int Nmax) {
     ORBGPU_LATENCY_WAVE();
     // dynamic LDS, max N of the batch entries each (select_lds_bytes)
@@ -419,7 +420,7 @@ __global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ pr
     const SearchDev P = probs[blockIdx.x];
     const int tid = threadIdx.x;
     const int N = P.cur.N, nq = P.nq;
-    for (int i = tid; i < N; i += 256) {
+    for (int i = tid; i < N; i += NT) {
         const int m = P.curMP[i];
         s_occ0[i] = (m >= 0 && P.mpObs[m] > 0) ? 1 : 0;
         s_owner[i] = INT_MAX;
@@ -431,7 +432,7 @@ __global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ pr
     bool bF = false, bB = false;
     if (LAST) fwd_bwd(P, bMono != 0, bF, bB);
     // per query: qinfo.x = candidate count (k_candidates), .y = current choice (-1 none), .z = obs flag
-    for (int q = tid; q < nq; q += 256) {
+    for (int q = tid; q < nq; q += NT) {
         const int c = P.qinfo[q].x;
         const int mp = LAST ? P.lastMP[q] : P.mpIndex[q];
         P.qinfo[q].z = (c > 0 && mp >= 0 && P.mpObs[mp] > 0) ? 1 : 0;
@@ -476,19 +477,19 @@ __global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ pr
         }
         return bestIdx;
     };
-    for (int q = tid; q < nq; q += 256) P.qinfo[q].y = decide(q);   // round 0: nothing claimed yet
+    for (int q = tid; q < nq; q += NT) P.qinfo[q].y = decide(q);   // round 0: nothing claimed yet
     for (int round = 0; round <= nq; round++) {
         __syncthreads();
-        for (int i = tid; i < N; i += 256) s_owner[i] = INT_MAX;
+        for (int i = tid; i < N; i += NT) s_owner[i] = INT_MAX;
         if (tid == 0) s_changed = 0;
         __syncthreads();
-        for (int q = tid; q < nq; q += 256) {
+        for (int q = tid; q < nq; q += NT) {
             const int4 qi = P.qinfo[q];
             if (qi.y >= 0 && qi.z) atomicMin(&s_owner[qi.y], q);
         }
         __syncthreads();
         bool ch = false;
-        for (int q = tid; q < nq; q += 256) {
+        for (int q = tid; q < nq; q += NT) {
             const int c = decide(q);
             if (c != P.qinfo[q].y) { P.qinfo[q].y = c; ch = true; }
         }
@@ -499,7 +500,7 @@ __global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ pr
     ORBGPU_PROF_MARK(1);
     // the fixed point: takes, latest taker per keypoint, match count
     int nm = 0;
-    for (int q = tid; q < nq; q += 256) {
+    for (int q = tid; q < nq; q += NT) {
         const int c = P.qinfo[q].y;
         if (c >= 0) { atomicMax(&s_lastq[c], q); nm++; }
     }
@@ -507,7 +508,7 @@ __global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ pr
     __syncthreads();
     if (LAST && checkOri) {
         // rotation-consistency histogram over the matches (ORBmatcher.cc:1422-1467)
-        for (int q = tid; q < nq; q += 256) {
+        for (int q = tid; q < nq; q += NT) {
             const int bi = P.qinfo[q].y;
             if (bi < 0) continue;
             float rot = P.last.keysUn[q].angle - P.cur.keysUn[bi].angle;
@@ -536,7 +537,7 @@ __global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ pr
         __syncthreads();
         const int ind1 = s_ind[0], ind2 = s_ind[1], ind3 = s_ind[2];
         int removed = 0;
-        for (int q = tid; q < nq; q += 256) {
+        for (int q = tid; q < nq; q += NT) {
             if (P.qinfo[q].y < 0) continue;
             const int2 h = P.hist[q];
             if (h.x != ind1 && h.x != ind2 && h.x != ind3) {
@@ -548,7 +549,7 @@ __global__ void __launch_bounds__(256) k_select(const SearchDev* __restrict__ pr
     }
     __syncthreads();
     ORBGPU_PROF_MARK(2);
-    for (int i = tid; i < N; i += 256) {
+    for (int i = tid; i < N; i += NT) {
         const int lq = s_lastq[i];
         if (s_rm[i]) P.curMP[i] = -1;
         else if (lq >= 0) P.curMP[i] = LAST ? P.lastMP[lq] : P.mpIndex[lq];
@@ -766,13 +767,16 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
             hipLaunchKernelGGL(k_candidates<true>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, (int)bMono,
                                counters());
             mark(2);
-            hipLaunchKernelGGL(k_select<true>, dim3(np), dim3(256), select_lds_bytes(maxN), stream_, dp, th, (int)bMono,
+            hipLaunchKernelGGL((k_select<true, 256>), dim3(np), dim3(256), select_lds_bytes(maxN), stream_, dp, th, (int)bMono,
                                nnratio_, (int)checkOri_, maxN);
         } else {
             hipLaunchKernelGGL(k_candidates<false>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0,
                                counters());
             mark(2);
-            hipLaunchKernelGGL(k_select<false>, dim3(np), dim3(256), select_lds_bytes(maxN), stream_, dp, th, 0,
+            // SearchLocalPoints-sized query sets (thousands of local map points, long occupancy
+            // chains between duplicated points): 16 waves per round of the fixed point
+            hipLaunchKernelGGL((k_select<false, kSelectLocalThreads>), dim3(np), dim3(kSelectLocalThreads),
+                               select_lds_bytes(maxN), stream_, dp, th, 0,
                                nnratio_, 0, maxN);
         }
     } else {
