@@ -1129,10 +1129,14 @@ __device__ __forceinline__ void pose_pass(F f, int nA, const int* aE, const Pose
             else
 #pragma unroll
                 for (int q = 0; q < K; q++) v[q] = 0.0;
+            if (nA == 1) {   // ora_csum keeps a single term untouched
+                if (lane == 0)
 #pragma unroll
-            for (int q = 0; q < K; q++) {
-                const double t = nA == 1 ? v[q] : wave_tree(v[q]);
-                if (lane == 0) cs[q][w] = t;
+                    for (int q = 0; q < K; q++) cs[q][0] = v[q];
+            } else {
+                const double t = packed_trees<K>(v);
+                const int q = bitrev6(lane);
+                if (q < K) cs[q][w] = t;
             }
         }
         __syncthreads();
@@ -1153,10 +1157,10 @@ __device__ __forceinline__ void pose_pass(F f, int nA, const int* aE, const Pose
         else
 #pragma unroll
             for (int q = 0; q < K; q++) v[q] = 0.0;
-#pragma unroll
-        for (int q = 0; q < K; q++) {
-            const double t = nA == 1 ? v[q] : wave_tree(v[q]);   // ora_csum keeps a single term untouched
-            if (lane == 0) cs[q][c] = t;
+        {   // nA > 64 here: every chunk is a full canonical tree
+            const double t = packed_trees<K>(v);
+            const int q = bitrev6(lane);
+            if (q < K) cs[q][c] = t;
         }
         c = cn;
         a = an;
@@ -1174,13 +1178,13 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     PoseProbDev& P = probs[blockIdx.x];
     const int ne = P.ne;
     const PoseEdgeDev* E = Eall + P.e0;
-    double* err = errAll + 3 * (size_t)P.e0;
+    (void)errAll;   // errors are recomputed at classification instead of kept per pass
     uint8_t* outl = outlAll + P.e0;
     __shared__ uint8_t level[kPoseMaxEdges], robust[kPoseMaxEdges];
     __shared__ int aE[kPoseMaxEdges];
     __shared__ double cs[28][kPoseMaxEdges / 64];
     __shared__ double red[32];
-    __shared__ Se3 T, Tbak;
+    __shared__ Se3 T, Tbak, Terr;
     __shared__ double xs[6], Hs[21], bs[6];
     __shared__ double lambda, ni, currentChi, iniChi;
     __shared__ int nA, nBadLM, qmax, again, term, nBad, okS, wsum[16];
@@ -1209,7 +1213,6 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     auto err_term = [&](const PoseEdgeD& e, int i, double* v) {
         double e3[3];
         pose_err(e, T, P, e3);
-        for (int j = 0; j < 3; j++) err[3 * i + j] = e3[j];
         v[0] = pose_rho0(e, pose_chi2(e, e3), robust[i]);
     };
     for (int it = 0; it < 4; it++) {
@@ -1249,7 +1252,6 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                 pose_pass<28>([&](const PoseEdgeD& e, int i, double* v) {
                     double e3[3];
                     pose_err(e, T, P, e3);
-                    for (int j = 0; j < 3; j++) err[3 * i + j] = e3[j];
                     const double c = pose_chi2(e, e3);
                     const bool rb = robust[i];
                     v[0] = pose_rho0(e, c, rb);
@@ -1340,10 +1342,14 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                         if (ok2)
                             for (int j = 0; j < 6; j++) xs[j] = xn[j];
                         okS = ok2 ? 1 : 0;
+                        ORBGPU_PROF_MARK(5);
                         Se3 d, r;
                         se3_exp(xs, d);
+                        ORBGPU_PROF_MARK(6);
                         se3_mul(d, T, r);
+                        ORBGPU_PROF_MARK(7);
                         T = r;
+                        Terr = r;   // the pose of the last computeActiveErrors
                     }
                     __syncthreads();
                     ORBGPU_PROF_MARK(2);
@@ -1395,11 +1401,10 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
         int mybad = 0;
         for (int i = tid; i < ne; i += blockDim.x) {
             const PoseEdgeD e = pose_edge_load(E, i, dM, dS);
-            double e3[3] = {err[3 * i], err[3 * i + 1], err[3 * i + 2]};
-            if (outl[i]) {
-                pose_err(e, T, P, e3);
-                for (int j = 0; j < 3; j++) err[3 * i + j] = e3[j];
-            }
+            // active edges keep the error of the last pass (recomputed: the same operations on
+            // the same pose), outliers get computeError() at the final estimate
+            double e3[3];
+            pose_err(e, outl[i] ? T : Terr, P, e3);
             const float chi2 = (float)pose_chi2(e, e3);
             if (chi2 > (e.stereo ? chi2Stereo : chi2Mono)) {
                 outl[i] = 1;

@@ -130,6 +130,54 @@ __device__ __forceinline__ double wave_tree(double v) {
     return v;
 }
 
+// K canonical 64-trees at once (K <= 64), packed: after the level with offset `off` each value
+// only needs `off` lanes, so two registers merge into one (the second value's pair sums are
+// formed in the upper lanes as a[i + off] + a[i], the same IEEE sum as a[i] + a[i + off]).
+// Value q ends in lane bitrev6(q); about 2.3x fewer cross-lane moves and 3x fewer adds than K
+// separate wave_tree()s.
+template <int OFF, bool HIGH>
+__device__ __forceinline__ unsigned xl_pair_move(unsigned v) {
+    if constexpr (OFF == 32) return __builtin_amdgcn_permlane32_swap(v, v, false, false)[HIGH ? 0 : 1];
+    else if constexpr (OFF == 16) return __builtin_amdgcn_permlane16_swap(v, v, false, false)[HIGH ? 0 : 1];
+    else return __builtin_amdgcn_update_dpp(0u, v, (HIGH ? 0x110 : 0x100) + OFF, 0xf, 0xf, false);
+}
+template <int OFF, bool HIGH>
+__device__ __forceinline__ double xl_pair_sum(double v) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = xl_pair_move<OFF, HIGH>((unsigned)(u & 0xffffffffu));
+    const unsigned hi = xl_pair_move<OFF, HIGH>((unsigned)(u >> 32));
+    return v + __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+template <int R, int OFF>
+__device__ __forceinline__ void packed_level(double* a, int lane) {
+#pragma unroll
+    for (int j = 0; j < (R + 1) / 2; j++) {
+        const double lo = xl_pair_sum<OFF, false>(a[2 * j]);
+        if (2 * j + 1 < R) {
+            const double hi = xl_pair_sum<OFF, true>(a[2 * j + 1]);
+            a[j] = (lane & OFF) ? hi : lo;
+        } else {
+            a[j] = lo;
+        }
+    }
+}
+__device__ __forceinline__ int bitrev6(int x) { return (int)(__builtin_bitreverse32((unsigned)x) >> 26); }
+// v[0..K) per lane (clobbered); returns this lane's finished tree, value index bitrev6(lane)
+template <int K>
+__device__ __forceinline__ double packed_trees(double* v) {
+    static_assert(K >= 1 && K <= 64, "packed_trees: 1..64 values");
+    const int lane = threadIdx.x & 63;
+    constexpr int R1 = K, R2 = (R1 + 1) / 2, R3 = (R2 + 1) / 2, R4 = (R3 + 1) / 2, R5 = (R4 + 1) / 2,
+                  R6 = (R5 + 1) / 2;
+    packed_level<R1, 32>(v, lane);
+    packed_level<R2, 16>(v, lane);
+    packed_level<R3, 8>(v, lane);
+    packed_level<R4, 4>(v, lane);
+    packed_level<R5, 2>(v, lane);
+    packed_level<R6, 1>(v, lane);
+    return v[0];
+}
+
 // Canonical sum (oracle ora_csum) of f(0..n) by one wave; sc: this wave's LDS scratch
 // (>= ceil(n/64) doubles).  Result broadcast to all lanes.
 template <class F>

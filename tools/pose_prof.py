@@ -15,7 +15,7 @@ out = (C.c_ulonglong * 32)()
 lib().orbgpu_debug_prof(out)
 PoseOptimizationBatch(frames)
 lib().orbgpu_debug_prof(out)
-names = ["iter_top", "fused28", "solve_thread0", "trial_pass", "decide"]
+names = ["iter_top", "fused28", "solve_tail_sync", "trial_pass", "decide", "to_ldlt_done", "se3_exp", "se3_mul"]
 v = [out[i] for i in range(len(names))]
 tot = sum(v)
 print("cycles (frame 0, one call):", dict(zip(names, v)), "total", tot)
