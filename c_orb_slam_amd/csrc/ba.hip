@@ -1109,6 +1109,27 @@ __device__ __forceinline__ double pose_rho0(const PoseEdgeD& e, double c, bool r
 constexpr int kPoseMaxEdges = 8192;
 constexpr int kPoseThreads = 512;   // 256 VGPRs per lane for the fused 28-term pass
 constexpr int kPosePer = kPoseMaxEdges / kPoseThreads;
+constexpr int kPoseLdsEdges = 2048;   // active edges staged in LDS per round (64 KiB)
+
+// Canonical totals (ora_csum level 2) of the m chunk trees cs[q][0..m) of K sums, by wave 0:
+// lane c holds chunk c and the K trees run packed (the same pairing as local_csum_inplace).
+template <int K>
+__device__ __forceinline__ void pose_chunk_totals(double (*cs)[kPoseMaxEdges / 64], int m, double* res) {
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    if (m <= 1) {
+        if (lane < K) res[lane] = m == 1 ? cs[lane][0] : 0.0;
+    } else if (m <= 64) {
+        double v[K];
+#pragma unroll
+        for (int q = 0; q < K; q++) v[q] = lane < m ? cs[q][lane] : 0.0;
+        const double t = packed_trees<K>(v);
+        const int q = bitrev6(lane);
+        if (q < K) res[q] = t;
+    } else if (lane < K) {
+        res[lane] = local_csum_inplace(cs[lane], m);
+    }
+}
 
 // Block-wide canonical sums (ora_csum) of K per-active-edge values: wave w owns chunks
 // c = w, w + nw, ... of 64 active edges; the edge of chunk c + nw is loaded while chunk c is
@@ -1117,7 +1138,7 @@ constexpr int kPosePer = kPoseMaxEdges / kPoseThreads;
 template <int K, class F>
 __device__ __forceinline__ void pose_pass(F f, int nA, const int* aE, const PoseEdgeDev* E, double dM, double dS,
                                           double (*cs)[kPoseMaxEdges / 64], double* res, const PoseEdgeD& mine,
-                                          int mineIdx) {
+                                          int mineIdx, const PoseEdgeDev* Ls) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int m = (nA + 63) >> 6;
     if (m <= nw) {
@@ -1140,18 +1161,22 @@ __device__ __forceinline__ void pose_pass(F f, int nA, const int* aE, const Pose
             }
         }
         __syncthreads();
-        if ((int)threadIdx.x < K) res[threadIdx.x] = nA > 0 ? local_csum_inplace(cs[threadIdx.x], m) : 0.0;
+        pose_chunk_totals<K>(cs, nA > 0 ? m : 0, res);
         __syncthreads();
         return;
     }
+    // the first kPoseLdsEdges active edges come from the round's LDS copy, the rest from HBM
+    auto load = [&](int a, int i) {
+        return a < kPoseLdsEdges ? pose_edge_load(Ls, a, dM, dS) : pose_edge_load(E, i, dM, dS);
+    };
     int c = w;
     int a = c * 64 + lane;
     int i = a < nA ? aE[a] : 0;
-    PoseEdgeD e = pose_edge_load(E, i, dM, dS);
+    PoseEdgeD e = load(a, i);
     while (c < m) {
         const int cn = c + nw, an = cn * 64 + lane;
         const int in = (cn < m && an < nA) ? aE[an] : 0;
-        const PoseEdgeD en = pose_edge_load(E, in, dM, dS);   // prefetch the next chunk's edge
+        const PoseEdgeD en = load(an, in);   // prefetch the next chunk's edge
         double v[K];
         if (a < nA) f(e, i, v);
         else
@@ -1168,8 +1193,167 @@ __device__ __forceinline__ void pose_pass(F f, int nA, const int* aE, const Pose
         e = en;
     }
     __syncthreads();
-    if ((int)threadIdx.x < K) res[threadIdx.x] = nA > 0 ? local_csum_inplace(cs[threadIdx.x], m) : 0.0;
+    pose_chunk_totals<K>(cs, nA > 0 ? m : 0, res);
     __syncthreads();
+}
+
+
+// ---- wave-level dense solve of the pose system ---------------------------------------
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)(u & 0xffffffffu), l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+// N independent IEEE divisions num[j] / den[j] as ONE lane-parallel division (lane j), results
+// broadcast to every lane.  The whole wave must be active and hold the same operands.
+template <int N>
+__device__ __forceinline__ void lane_div(const double* num, const double* den, double* out) {
+    const int lane = threadIdx.x & 63;
+    double a = num[0], b = den[0];
+#pragma unroll
+    for (int j = 1; j < N; j++) {
+        // opaque operands: a select chain over an array indexed by the lane otherwise becomes
+        // a scratch-memory lookup
+        double nj = num[j], dj = den[j];
+        asm volatile("" : "+v"(nj), "+v"(dj));
+        a = lane == j ? nj : a;
+        b = lane == j ? dj : b;
+    }
+    const double q = a / b;
+#pragma unroll
+    for (int j = 0; j < N; j++) out[j] = lane_bcast(q, j);
+}
+
+// LinearSolverDense (Eigen LDLT with diagonal pivoting) of (H + lambda I) x = b, H the packed
+// upper triangle Hs[21], run redundantly by a whole wave: the same IEEE operations as
+// ldlt_pivot6.  Left-looking LDLT never touches a diagonal entry before its own step, so the
+// pivot sequence is a function of |diag(H) + lambda| alone: it is fixed first, the
+// factorisation then runs unpivoted on P A P^T with static register indices, and the row
+// divisions of a step (and the 6 of the solve) are one lane-parallel division each.
+__device__ __forceinline__ bool pose_solve_w(const double* Hs, const double* bs, double lambda, double* x) {
+    // With distinct |pivots| the sequence is the descending order of |diag| (ties or NaN take
+    // the reference routine: its tie-break follows the swap history).  Ranks instead of swaps
+    // keep every index static (no scratch).
+    double dv[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) dv[i] = fabs(Hs[DIAG21[i]] + lambda);
+    bool distinct = true;
+    int rank[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        int r = 0;
+        distinct = distinct && dv[j] == dv[j];
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+            if (i != j) {
+                r += dv[i] > dv[j] ? 1 : 0;
+                distinct = distinct && dv[i] != dv[j];
+            }
+        rank[j] = r;
+    }
+    int ord[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+        int o = 0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) o = rank[j] == r ? j : o;
+        ord[r] = o;
+    }
+    double A[36];   // lower triangle of P (H + lambda I) P^T
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int c = 0; c <= r; c++) {
+            const int a = min(ord[r], ord[c]), b = max(ord[r], ord[c]);
+            double h = Hs[a * 6 - (a * (a - 1)) / 2 + (b - a)];
+            if (r == c) h += lambda;
+            A[r * 6 + c] = h;
+        }
+    if (!distinct || !(fabs(A[0]) > 0.0)) {   // ties / NaN, or the reference's zero-pivot stop
+        double Hd[36], bb[6];
+#pragma unroll
+        for (int r = 0, q = 0; r < 6; r++)
+#pragma unroll
+            for (int cc = r; cc < 6; cc++, q++) {
+                double h = Hs[q];
+                if (cc == r) h += lambda;
+                Hd[r * 6 + cc] = h;
+                Hd[cc * 6 + r] = h;
+            }
+#pragma unroll
+        for (int j = 0; j < 6; j++) bb[j] = bs[j];
+        return ldlt_pivot6(Hd, bb, x);
+    }
+    int sign = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        if (k > 0) {
+            double tmp[6];
+#pragma unroll
+            for (int j = 0; j < k; j++) tmp[j] = A[j * 6 + j] * A[k * 6 + j];
+            double s = 0;
+#pragma unroll
+            for (int j = 0; j < k; j++) s += A[k * 6 + j] * tmp[j];
+            A[k * 6 + k] -= s;
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) {
+                double t = 0;
+#pragma unroll
+                for (int j = 0; j < k; j++) t += A[i * 6 + j] * tmp[j];
+                A[i * 6 + k] -= t;
+            }
+        }
+        const double akk = A[k * 6 + k];
+        if (k < 5 && fabs(akk) > 0.0) {
+            double num[5], den[5], q[5];
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                num[j] = k + 1 + j < 6 ? A[(k + 1 + j) * 6 + k] : 1.0;
+                den[j] = akk;
+            }
+            lane_div<5>(num, den, q);
+#pragma unroll
+            for (int i = k + 1; i < 6; i++) A[i * 6 + k] = q[i - k - 1];
+        }
+        if (sign == 1) {
+            if (akk < 0) sign = 3;
+        } else if (sign == 2) {
+            if (akk > 0) sign = 3;
+        } else if (sign == 0) {
+            if (akk > 0) sign = 1;
+            else if (akk < 0) sign = 2;
+        }
+    }
+    if (!(sign == 1 || sign == 0)) return false;
+    double y[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) y[i] = bs[ord[i]];
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j < i; j++) y[i] -= A[i * 6 + j] * y[j];
+    {
+        double den[6], q[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) den[i] = A[i * 6 + i];
+        lane_div<6>(y, den, q);
+#pragma unroll
+        for (int i = 0; i < 6; i++) y[i] = fabs(A[i * 6 + i]) > DBL_MIN ? q[i] : 0.0;
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; i--)
+#pragma unroll
+        for (int j = 5; j > i; j--) y[i] -= A[j * 6 + i] * y[j];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        double v = 0.0;
+#pragma unroll
+        for (int p = 0; p < 6; p++)
+            if (ord[p] == j) v = y[p];
+        x[j] = v;
+    }
+    return true;
 }
 
 __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, const PoseEdgeDev* __restrict__ Eall,
@@ -1182,6 +1366,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     uint8_t* outl = outlAll + P.e0;
     __shared__ uint8_t level[kPoseMaxEdges], robust[kPoseMaxEdges];
     __shared__ int aE[kPoseMaxEdges];
+    __shared__ PoseEdgeDev Ls[kPoseLdsEdges];
     __shared__ double cs[28][kPoseMaxEdges / 64];
     __shared__ double red[32];
     __shared__ Se3 T, Tbak, Terr;
@@ -1243,10 +1428,16 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
         const int na = nA;
         const int myIdx = tid < na ? aE[tid] : 0;
         const PoseEdgeD myE = pose_edge_load(E, myIdx, dM, dS);
+        if (na > kPoseThreads) {   // chunked passes: stage the round's active edges in LDS
+            const int nst = min(na, kPoseLdsEdges);
+            for (int a = tid; a < nst; a += blockDim.x) Ls[a] = E[aE[a]];
+            __syncthreads();
+        }
         if (na > 0) {   // optimize(10); without active edges the vertex is not optimised at all
             ORBGPU_PROF_START;
             for (int k = 0; k < 10; k++) {
                 ORBGPU_PROF_MARK(0);
+                ORBGPU_PROF_COUNT(8);
                 // computeActiveErrors + activeRobustChi2 (entry 0) and buildSystem (entries 1..27:
                 // J^T W J upper triangle, -J^T W e), one pass, canonical sums per entry
                 pose_pass<28>([&](const PoseEdgeD& e, int i, double* v) {
@@ -1277,34 +1468,35 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                     J[15] = J[3];
                     J[16] = 0;
                     J[17] = J[5] - (P.bf * invz_2);
-                    const int D = e.stereo ? 3 : 2;
+                    // monocular edges: a zero third Jacobian row (and err[2] = 0) makes every
+                    // third term +-0, an exact identity on the two-term partial sums (which
+                    // start from +0 + t0 and so are never -0): the sums run branch-free
+#pragma unroll
+                    for (int j = 12; j < 18; j++) J[j] = e.stereo ? J[j] : 0.0;
                     double r1 = 1.;
                     if (rb && !(c <= e.dsqr)) r1 = e.delta / sqrt(c);
                     const double wgt = rb ? r1 * e.info : e.info;
-                    double omr[3] = {0, 0, 0};
+                    double omr[3];
 #pragma unroll
-                    for (int kk = 0; kk < 3; kk++)
-                        if (kk < D) {
-                            omr[kk] = -(e.info * e3[kk]);
-                            if (rb) omr[kk] *= r1;
-                        }
+                    for (int kk = 0; kk < 3; kk++) {
+                        omr[kk] = -(e.info * e3[kk]);
+                        if (rb) omr[kk] *= r1;
+                    }
 #pragma unroll
                     for (int r = 0; r < 6; r++) {
                         double sb = 0;
 #pragma unroll
-                        for (int kk = 0; kk < 3; kk++)
-                            if (kk < D) sb += J[kk * 6 + r] * omr[kk];
+                        for (int kk = 0; kk < 3; kk++) sb += J[kk * 6 + r] * omr[kk];
                         v[22 + r] = sb;
 #pragma unroll
                         for (int cc = r; cc < 6; cc++) {
                             double hh = 0;
 #pragma unroll
-                            for (int kk = 0; kk < 3; kk++)
-                                if (kk < D) hh += (J[kk * 6 + r] * wgt) * J[kk * 6 + cc];
+                            for (int kk = 0; kk < 3; kk++) hh += (J[kk * 6 + r] * wgt) * J[kk * 6 + cc];
                             v[1 + r * 6 - (r * (r - 1)) / 2 + (cc - r)] = hh;
                         }
                     }
-                }, na, aE, E, dM, dS, cs, red, myE, myIdx);
+                }, na, aE, E, dM, dS, cs, red, myE, myIdx, Ls);
                 ORBGPU_PROF_MARK(1);
                 if (tid < 28) {
                     if (tid == 0) currentChi = iniChi = red[0];
@@ -1324,36 +1516,32 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                 }
                 __syncthreads();
                 do {
-                    if (tid == 0) {
-                        Tbak = T;
-                        double Hd[36], xn[6], bb[6];
+                    ORBGPU_PROF_MARK(10);
+                    if (tid < 64) {   // wave 0: lane-parallel divisions in the solve
+                        double xn[6];
+                        const bool ok2 = pose_solve_w(Hs, bs, lambda, xn);
+                        double xl[6];
 #pragma unroll
-                        for (int r = 0, q = 0; r < 6; r++)
-#pragma unroll
-                            for (int cc = r; cc < 6; cc++, q++) {
-                                double h = Hs[q];
-                                if (cc == r) h += lambda;
-                                Hd[r * 6 + cc] = h;
-                                Hd[cc * 6 + r] = h;
-                            }
-#pragma unroll
-                        for (int j = 0; j < 6; j++) bb[j] = bs[j];
-                        const bool ok2 = ldlt_pivot6(Hd, bb, xn);
-                        if (ok2)
-                            for (int j = 0; j < 6; j++) xs[j] = xn[j];
-                        okS = ok2 ? 1 : 0;
+                        for (int j = 0; j < 6; j++) xl[j] = ok2 ? xn[j] : xs[j];
                         ORBGPU_PROF_MARK(5);
+                        ORBGPU_PROF_COUNT(9);
                         Se3 d, r;
-                        se3_exp(xs, d);
+                        se3_exp(xl, d);
                         ORBGPU_PROF_MARK(6);
                         se3_mul(d, T, r);
                         ORBGPU_PROF_MARK(7);
-                        T = r;
-                        Terr = r;   // the pose of the last computeActiveErrors
+                        if (tid == 0) {
+                            Tbak = T;
+#pragma unroll
+                            for (int j = 0; j < 6; j++) xs[j] = xl[j];
+                            okS = ok2 ? 1 : 0;
+                            T = r;
+                            Terr = r;   // the pose of the last computeActiveErrors
+                        }
                     }
                     __syncthreads();
                     ORBGPU_PROF_MARK(2);
-                    pose_pass<1>(err_term, na, aE, E, dM, dS, cs, red, myE, myIdx);
+                    pose_pass<1>(err_term, na, aE, E, dM, dS, cs, red, myE, myIdx, Ls);
                     ORBGPU_PROF_MARK(3);
                     if (tid == 0) {
                         double tempChi = red[0];

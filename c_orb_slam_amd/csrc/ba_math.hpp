@@ -131,34 +131,58 @@ __device__ __forceinline__ double wave_tree(double v) {
 }
 
 // K canonical 64-trees at once (K <= 64), packed: after the level with offset `off` each value
-// only needs `off` lanes, so two registers merge into one (the second value's pair sums are
-// formed in the upper lanes as a[i + off] + a[i], the same IEEE sum as a[i] + a[i + off]).
-// Value q ends in lane bitrev6(q); about 2.3x fewer cross-lane moves and 3x fewer adds than K
-// separate wave_tree()s.
-template <int OFF, bool HIGH>
-__device__ __forceinline__ unsigned xl_pair_move(unsigned v) {
-    if constexpr (OFF == 32) return __builtin_amdgcn_permlane32_swap(v, v, false, false)[HIGH ? 0 : 1];
-    else if constexpr (OFF == 16) return __builtin_amdgcn_permlane16_swap(v, v, false, false)[HIGH ? 0 : 1];
-    else return __builtin_amdgcn_update_dpp(0u, v, (HIGH ? 0x110 : 0x100) + OFF, 0xf, 0xf, false);
+// only needs `off` lanes, so the pair (x, y) of registers merges into one: x's pair sums in
+// the lanes with bit `off` clear, y's (formed as y[i] + y[i - off] or y[i] + y[i + off], the
+// same IEEE sums as the tree's) in the lanes with it set.  Offsets 32 and 16 are one
+// v_permlane{32,16}_swap per dword of the PAIR (the swap exchanges exactly the halves the two
+// trees need); offsets 8, 2, 1 a lane-select plus one DPP xor-move; 4 two bank-masked DPP
+// moves.  Value q ends in lane bitrev6(q).
+template <int OFF>
+__device__ __forceinline__ unsigned dpp_xor_move(unsigned v) {
+    static_assert(OFF == 8 || OFF == 2 || OFF == 1, "xor offsets with a single DPP control");
+    // row_ror:8 (= xor 8 inside a row of 16), quad_perm [2,3,0,1], quad_perm [1,0,3,2]
+    return __builtin_amdgcn_update_dpp(0u, v, OFF == 8 ? 0x128 : (OFF == 2 ? 0x4e : 0xb1), 0xf, 0xf, false);
 }
-template <int OFF, bool HIGH>
-__device__ __forceinline__ double xl_pair_sum(double v) {
-    const unsigned long long u = __double_as_longlong(v);
-    const unsigned lo = xl_pair_move<OFF, HIGH>((unsigned)(u & 0xffffffffu));
-    const unsigned hi = xl_pair_move<OFF, HIGH>((unsigned)(u >> 32));
-    return v + __longlong_as_double(((unsigned long long)hi << 32) | lo);
+__device__ __forceinline__ double dbl_of(unsigned lo, unsigned hi) {
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ unsigned dlo(double v) { return (unsigned)(__double_as_longlong(v) & 0xffffffffu); }
+__device__ __forceinline__ unsigned dhi(double v) { return (unsigned)(__double_as_longlong(v) >> 32); }
+
+template <int OFF>
+__device__ __forceinline__ double packed_pair(double x, double y, int lane) {
+    if constexpr (OFF == 32 || OFF == 16) {
+        const auto l = OFF == 32 ? __builtin_amdgcn_permlane32_swap(dlo(x), dlo(y), false, false)
+                                 : __builtin_amdgcn_permlane16_swap(dlo(x), dlo(y), false, false);
+        const auto h = OFF == 32 ? __builtin_amdgcn_permlane32_swap(dhi(x), dhi(y), false, false)
+                                 : __builtin_amdgcn_permlane16_swap(dhi(x), dhi(y), false, false);
+        return dbl_of(l[0], h[0]) + dbl_of(l[1], h[1]);
+    } else if constexpr (OFF == 4) {
+        const bool up = (lane & 4) != 0;
+        const double p = up ? y : x;
+        // banks (4-lane groups) 0,2 take x from 4 lanes up, banks 1,3 take y from 4 lanes down
+        unsigned ql = __builtin_amdgcn_update_dpp(dlo(y), dlo(x), 0x104, 0xf, 0x5, false);
+        unsigned qh = __builtin_amdgcn_update_dpp(dhi(y), dhi(x), 0x104, 0xf, 0x5, false);
+        ql = __builtin_amdgcn_update_dpp(ql, dlo(y), 0x114, 0xf, 0xa, false);
+        qh = __builtin_amdgcn_update_dpp(qh, dhi(y), 0x114, 0xf, 0xa, false);
+        return p + dbl_of(ql, qh);
+    } else {
+        const bool up = (lane & OFF) != 0;
+        const double p = up ? y : x, sx = up ? x : y;
+        return p + dbl_of(dpp_xor_move<OFF>(dlo(sx)), dpp_xor_move<OFF>(dhi(sx)));
+    }
+}
+// an unpaired register: plain tree step (valid in the lanes with bit `off` clear)
+template <int OFF>
+__device__ __forceinline__ double packed_single(double x) {
+    return x + dbl_of(xl_down(dlo(x), OFF), xl_down(dhi(x), OFF));
 }
 template <int R, int OFF>
 __device__ __forceinline__ void packed_level(double* a, int lane) {
 #pragma unroll
     for (int j = 0; j < (R + 1) / 2; j++) {
-        const double lo = xl_pair_sum<OFF, false>(a[2 * j]);
-        if (2 * j + 1 < R) {
-            const double hi = xl_pair_sum<OFF, true>(a[2 * j + 1]);
-            a[j] = (lane & OFF) ? hi : lo;
-        } else {
-            a[j] = lo;
-        }
+        if (2 * j + 1 < R) a[j] = packed_pair<OFF>(a[2 * j], a[2 * j + 1], lane);
+        else a[j] = packed_single<OFF>(a[2 * j]);
     }
 }
 __device__ __forceinline__ int bitrev6(int x) { return (int)(__builtin_bitreverse32((unsigned)x) >> 26); }

@@ -147,7 +147,12 @@ static __device__ unsigned long long g_orbgpu_prof[32];   // one copy per transl
             _orbgpu_pt = _t;                                                                  \
         }                                                                                     \
     } while (0)
+#define ORBGPU_PROF_COUNT(i)                                                                  \
+    do {                                                                                      \
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_orbgpu_prof[i], 1ull);          \
+    } while (0)
 #else
 #define ORBGPU_PROF_START
 #define ORBGPU_PROF_MARK(i)
+#define ORBGPU_PROF_COUNT(i)
 #endif

@@ -20,3 +20,4 @@ v = [out[i] for i in range(len(names))]
 tot = sum(v)
 print("cycles (frame 0, one call):", dict(zip(names, v)), "total", tot)
 print({n: round(x / tot, 3) for n, x in zip(names, v)})
+print("fused passes", out[8], "trials", out[9], "pre-solve (syncs, lambda)", out[10])
