@@ -710,6 +710,9 @@ def main():
     gba = bench_global_ba(args, world, rank, dist if world > 1 else None, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         gba["cpu_baseline"] = gba_cpu_baseline(args.gba_kf)
+    # RANSAC hypothesis scoring (SURVEY config 3): every rank runs it (replicas), rank 0 reports
+    ransac = bench_ransac(cpu=rank == 0 and world == 1 and not args.no_cpu_baseline,
+                          cpu_budget_s=args.cpu_seconds / 3)
 
     if rank == 0:
         stage_ms = {k: round(v / args.steps, 4) for k, v in stage_acc.items()}
@@ -734,7 +737,7 @@ def main():
             "stage_ms_per_step": stage_ms,
             "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}, "roofline": roof,
             "matcher_roofline": mroof, "latency": latency, "cpu_baseline": cpu, "local_ba": ba,
-            "global_ba": gba,
+            "global_ba": gba, "ransac": ransac,
         }
         json_out.write(json.dumps(out) + "\n")
         json_out.flush()
@@ -820,6 +823,151 @@ def bench_global_ba(args, world, rank, dist, dev):
                        "points": len(pr["pt_id"]), "edges": ne, "edges_per_rank": len(shard["edge_pt"]),
                        "lm": "optimize(10), bRobust=false", "parallelism": f"keyframe-block shards x{world} (RCCL)"},
             "dtype": "f64 (f32 I/O)"}
+
+
+RANSAC_PROBLEMS, RANSAC_HYP = 100, 300
+PNP_BYTES_PER_PAIR = 24   # p3d 12 B + p2d 8 B + maxErr 4 B read per (hypothesis, correspondence)
+SIM3_BYTES_PER_PAIR = 48  # X1, X2 24 B + p1, p2 16 B + two maxErr 8 B
+
+
+def bench_ransac(reps=5, cpu=True, cpu_budget_s=8.0):
+    """SURVEY config 3: batched RANSAC hypothesis scoring.  EPnP (PnPsolver::iterate,
+    PnPsolver.cc:165-339) over 100 relocalization-shaped problems x 300 hypotheses per call for
+    N in {50, 150, 500}, and Sim3Solver::iterate (Sim3Solver.cc:180-224) over 100 loop
+    candidates x 300 hypotheses.  minInliers = N, so no hypothesis reaches the acceptance test:
+    every draw is solved and scored on both sides, the reference loop's full 300 iterations
+    (no early exit).  One call = one PnPsolver_iterate_batch; device time = the two hypothesis
+    launches (solve, CheckInliers) by HIP events on the batch stream."""
+    import ctypes as C
+    sys.path.insert(0, str(ROOT / "tests"))
+    from c_orb_slam_amd._lib import check, lib
+    from c_orb_slam_amd.ransac import PnPsolver, Rng, Sim3Solver, iterate_batch, sim3_iterate_batch
+    from pnp_cases import pnp_problem
+    from sim3_cases import sim3_problem
+    L = lib()
+    check(L.PnPsolver_enable_timing(1), "PnPsolver_enable_timing")
+    check(L.Sim3Solver_enable_timing(1), "Sim3Solver_enable_timing")
+    ms2 = (C.c_float * 2)()
+    cnt2 = (C.c_longlong * 2)()
+
+    def run(make, batch_fn, timings_fn, bytes_per_pair, reset=None):
+        solvers = make()
+        rngs = [Rng(1 + k) for k in range(len(solvers))]
+        batch_fn(solvers, RANSAC_HYP, rngs)   # warm-up: allocations, upload
+        walls, solve, chk = [], [], []
+        for _ in range(reps):
+            if reset:
+                reset(solvers)
+            t0 = time.perf_counter()
+            batch_fn(solvers, RANSAC_HYP, rngs)
+            walls.append(time.perf_counter() - t0)
+            check(timings_fn(ms2, cnt2), "last_timings")
+            solve.append(ms2[0])
+            chk.append(ms2[1])
+        hyp, pairs = int(cnt2[0]), int(cnt2[1])
+        dev_ms = float(np.mean(solve)) + float(np.mean(chk))
+        c_ms = float(np.mean(chk))
+        ach = pairs * (bytes_per_pair + 1 / 8) / (c_ms * 1e-3) / 1e9
+        return {"hypotheses_per_call": hyp, "pairs_per_call": pairs,
+                "device_hyp_per_s": round(hyp / (dev_ms * 1e-3), 1),
+                "wall_hyp_per_s": round(hyp / float(np.mean(walls)), 1),
+                "ms_solve": round(float(np.mean(solve)), 4), "ms_check": round(c_ms, 4),
+                "ms_call_wall": round(float(np.mean(walls)) * 1e3, 3),
+                "check_roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": round(ach / HBM_PEAK_GBS, 5),
+                                   "alg_bytes_per_pair": bytes_per_pair + 1 / 8,
+                                   "note": "algorithmic bytes (every hypothesis reads every correspondence, writes "
+                                           "1 bit); the kernel stages a solver's correspondences in LDS once per "
+                                           "16 hypotheses, so its HBM traffic is ~1/16 of this"}}
+
+    out = {"workload": f"SURVEY config 3: {RANSAC_PROBLEMS} problems x {RANSAC_HYP} hypotheses per call, "
+                       "minInliers = N (no early exit)", "pnp": {}, "sim3": {}}
+    pnp_sets = {}
+    for N in (50, 150, 500):
+        prs = [pnp_problem(1000 + s, N) for s in range(RANSAC_PROBLEMS)]
+        pnp_sets[N] = prs
+
+        def make(prs=prs, N=N):
+            ss = []
+            for pr in prs:
+                s = PnPsolver(pr["p3d"], pr["p2d"], pr["sigma2"], pr["kp_idx"], pr["n_matches"], *pr["K"])
+                s.SetRansacParameters(0.99, N, RANSAC_HYP, 4, 0.4, 5.991)
+                ss.append(s)
+            return ss
+        out["pnp"][str(N)] = run(make, iterate_batch, L.PnPsolver_last_timings, PNP_BYTES_PER_PAIR)
+    # Sim3Solver's loop runs while BOTH mnIterations < mRansacMaxIts and the call's budget hold
+    # (Sim3Solver.cc:197), so mRansacMaxIts must reach 300: minInliers = 0.24 N gives
+    # ceil(log(0.01) / log(1 - 0.24^3)) = 331 -> 300; 90% outliers keep every hypothesis below it
+    N3 = 150
+    min3 = int(0.24 * N3)
+    s3 = [sim3_problem(2000 + s, N3, outlier_frac=0.9) for s in range(RANSAC_PROBLEMS)]
+
+    def make3():
+        ss = []
+        for pr in s3:
+            s = Sim3Solver(pr["X1"], pr["X2"], pr["s1"], pr["s2"], pr["idx1"], pr["N1"], pr["K1"], pr["K2"], pr["fix"])
+            s.SetRansacParameters(0.99, min3, RANSAC_HYP)
+            ss.append(s)
+        return ss
+
+    def reset3(ss):   # SetRansacParameters restarts mnIterations
+        for s in ss:
+            s.SetRansacParameters(0.99, min3, RANSAC_HYP)
+    out["sim3"][str(N3)] = run(make3, sim3_iterate_batch, L.Sim3Solver_last_timings, SIM3_BYTES_PER_PAIR, reset3)
+    out["sim3"][str(N3)]["min_inliers"] = min3
+    check(L.PnPsolver_enable_timing(0), "PnPsolver_enable_timing")
+    check(L.Sim3Solver_enable_timing(0), "Sim3Solver_enable_timing")
+    if cpu:
+        out["cpu_baseline"] = ransac_cpu_baseline(pnp_sets, s3, N3, min3, cpu_budget_s)
+        for kind in ("pnp", "sim3"):
+            for N, r in out[kind].items():
+                c = out["cpu_baseline"][kind].get(N)
+                if c:
+                    r["speedup_vs_cpu_all_core"] = round(r["wall_hyp_per_s"] / c["hyp_per_s"], 1)
+    return out
+
+
+def ransac_cpu_baseline(pnp_sets, s3, N3, min3, budget_s):
+    """Oracle PnPsolver / Sim3Solver iterate(300) with the same parameters on the same problems
+    (full 300 hypotheses each): P independent threads, each taking whole problems, bounded to
+    ~budget_s per configuration."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    flags = timing_oracle()
+    P, aff, quota = cpu_share()
+    out = {"pnp": {}, "cores": P, "kind": "port"}
+
+    def timed(fn, n_items):
+        # one item on one thread sizes the sample, then P threads take items round-robin
+        t0 = time.perf_counter()
+        fn(0)
+        one = time.perf_counter() - t0
+        n = int(min(20 * n_items, max(P, budget_s / max(one, 1e-6) * P / 3)))
+        res, wall = _streams(P, lambda i: [fn(j) for j in range(i, n, P)])
+        return n, wall, one
+
+    for N, prs in pnp_sets.items():
+        def fn(j, prs=prs, N=N):
+            pr = prs[j % len(prs)]
+            o = oracle_lib.OraclePnP(pr["p3d"], pr["p2d"], pr["sigma2"], pr["kp_idx"], pr["n_matches"], *pr["K"])
+            o.set_ransac(0.99, N, RANSAC_HYP, 4, 0.4, 5.991)
+            o.iterate(RANSAC_HYP, oracle_lib.new_rng(1 + j))
+        n, wall, one = timed(fn, len(prs))
+        out["pnp"][str(N)] = {"hyp_per_s": round(n * RANSAC_HYP / wall, 1), "problems": n, "seconds": round(wall, 2),
+                              "single_thread_hyp_per_s": round(RANSAC_HYP / one, 1)}
+
+    def fn3(j):
+        pr = s3[j % len(s3)]
+        o = oracle_lib.OracleSim3(pr["X1"], pr["X2"], pr["s1"], pr["s2"], pr["idx1"], pr["N1"], pr["K1"], pr["K2"],
+                                  pr["fix"])
+        o.set_ransac(0.99, min3, RANSAC_HYP)
+        o.iterate(RANSAC_HYP, oracle_lib.new_rng(1 + j))
+    n, wall, one = timed(fn3, len(s3))
+    out["sim3"] = {str(N3): {"hyp_per_s": round(n * RANSAC_HYP / wall, 1), "problems": n, "seconds": round(wall, 2),
+                             "single_thread_hyp_per_s": round(RANSAC_HYP / one, 1)}}
+    out["sample"] = (f"oracle/pnp.c + sim3.c {flags}, {P} threads ({_cpu_model()}; affinity {aff}, cgroup quota "
+                     f"{quota}); each problem a fresh solver, iterate({RANSAC_HYP}) = {RANSAC_HYP} hypotheses")
+    return out
 
 
 _ORACLE_TIMING = {}

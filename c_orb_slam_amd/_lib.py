@@ -146,6 +146,8 @@ def lib():
     L.PnPsolver_iterate.argtypes = [vp, i32, vp, P(i32), vp, P(i32), vp, P(i32)]
     L.PnPsolver_iterate_batch.argtypes = [i32, vp, i32, vp, vp, vp, vp, vp, vp]
     L.PnPsolver_get_state.argtypes = [vp, P(i32), P(i32), P(i32)]
+    L.PnPsolver_enable_timing.argtypes = [i32]
+    L.PnPsolver_last_timings.argtypes = [vp, vp]
     L.Optimizer_LocalBundleAdjustment.argtypes = [vp, vp, vp]
     L.Optimizer_BundleAdjustment.argtypes = [vp, i32, i32, vp, vp]
     L.Optimizer_LocalBundleAdjustment_sharded.argtypes = [vp, vp, vp, vp]
@@ -194,6 +196,8 @@ def lib():
     L.Sim3Solver_iterate_batch.argtypes = [i32, vp, i32, vp, vp, vp, vp, vp, vp]
     L.Sim3Solver_get_estimate.argtypes = [vp, vp, vp, vp]
     L.Sim3Solver_get_state.argtypes = [vp, P(i32), P(i32), P(i32)]
+    L.Sim3Solver_enable_timing.argtypes = [i32]
+    L.Sim3Solver_last_timings.argtypes = [vp, vp]
     _lib = L
     return L
 

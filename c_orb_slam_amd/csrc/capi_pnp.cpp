@@ -113,6 +113,22 @@ int PnPsolver_iterate(PnPsolver_h h, int nIterations, orb_rng* rng, int* bNoMore
     return PnPsolver_iterate_batch(1, &h, nIterations, &rng, bNoMore, &inliers, nInliers, Tcw, has_pose);
 }
 
+int PnPsolver_enable_timing(int on) {
+    int rc = 0;
+    orbgpu::PnPBatch* e = engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    e->enable_timing(on != 0);
+    return ORB_OK;
+}
+
+int PnPsolver_last_timings(float* ms2, long long* counts2) {
+    if (!ms2 || !counts2) return ORB_E_INVALID;
+    int rc = 0;
+    orbgpu::PnPBatch* e = engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    return e->last_timings(ms2, counts2) ? ORB_E_INVALID : ORB_OK;
+}
+
 int orbgpu_unit_pnp_layout(int n, const int* N, const int* K, const int* minSet, long long* out4) {
     if (n < 0 || (n > 0 && (!N || !K || !minSet)) || !out4) return ORB_E_INVALID;
     return orbgpu::pnp_layout_check(n, N, K, minSet, out4) ? ORB_E_CAPACITY : ORB_OK;

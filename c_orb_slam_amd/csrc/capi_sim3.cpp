@@ -109,4 +109,20 @@ int Sim3Solver_iterate(Sim3Solver_h h, int nIterations, orb_rng* rng, int* bNoMo
     return Sim3Solver_iterate_batch(1, &h, nIterations, &rng, bNoMore, &inliers, nInliers, T12, has_pose);
 }
 
+int Sim3Solver_enable_timing(int on) {
+    int rc = 0;
+    orbgpu::Sim3Batch* e = engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    e->enable_timing(on != 0);
+    return ORB_OK;
+}
+
+int Sim3Solver_last_timings(float* ms2, long long* counts2) {
+    if (!ms2 || !counts2) return ORB_E_INVALID;
+    int rc = 0;
+    orbgpu::Sim3Batch* e = engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    return e->last_timings(ms2, counts2) ? ORB_E_INVALID : ORB_OK;
+}
+
 }  // extern "C"

@@ -75,6 +75,8 @@ __device__ __forceinline__ void store_rt(double* out, const double R[3][3], cons
     }
 }
 
+// Hypothesis solve (PnPsolver.cc:196-210): a thread per hypothesis runs EPnP on its minimal set
+// in FP64 and stores (R, t); counts[h] = -1 flags an invalid draw (never expected).
 __global__ void __launch_bounds__(64) k_pnp_hypotheses(const PnPProbDev* __restrict__ probs) {
     const PnPProbDev P = probs[blockIdx.y];
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
@@ -90,9 +92,71 @@ __global__ void __launch_bounds__(64) k_pnp_hypotheses(const PnPProbDev* __restr
     epnp::Solver<IdxPts> S(pts, P.minSet, P.fu, P.fv, P.uc, P.vc);
     double R[3][3], t[3];
     S.compute_pose(R, t);
-    const int words = (P.N + 31) >> 5;
-    P.counts[h] = check_inliers(P, R, t, P.masks + (size_t)h * words);
     store_rt(P.rt + (size_t)h * 12, R, t);
+    P.counts[h] = 0;
+}
+
+// CheckInliers (308-339) of every hypothesis, lane-parallel over correspondences: a workgroup
+// per (solver, kPnPCheckHyp hypotheses), the solver's 24-B correspondences staged once in LDS
+// (when they fit) and reused by every hypothesis of the block; each wave scores a hypothesis
+// 64 points at a time, the inlier bits of a 64-point chunk are one ballot (two mask words) and
+// the count a popcount.  Per point the same float/double expression sequence as the reference.
+constexpr int kPnPCheckThreads = 256;
+constexpr int kPnPCheckHyp = 16;
+constexpr int kPnPStageMax = 2048;   // 48 KiB of LDS
+__global__ void __launch_bounds__(kPnPCheckThreads) k_pnp_check(const PnPProbDev* __restrict__ probs) {
+    const PnPProbDev& P = probs[blockIdx.y];
+    const int N = P.N, nhyp = P.nhyp;
+    const int h0 = blockIdx.x * kPnPCheckHyp;
+    if (h0 >= nhyp) return;
+    __shared__ float sX[kPnPStageMax * 3], sU[kPnPStageMax * 2], sE[kPnPStageMax];
+    const bool staged = N <= kPnPStageMax;
+    if (staged) {
+        for (int i = threadIdx.x; i < 3 * N; i += blockDim.x) sX[i] = P.p3d[i];
+        for (int i = threadIdx.x; i < 2 * N; i += blockDim.x) sU[i] = P.p2d[i];
+        for (int i = threadIdx.x; i < N; i += blockDim.x) sE[i] = P.maxErr[i];
+    }
+    __syncthreads();
+    const float* X3 = staged ? sX : P.p3d;
+    const float* U2 = staged ? sU : P.p2d;
+    const float* ME = staged ? sE : P.maxErr;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const int words = (N + 31) >> 5;
+    const double uc = P.uc, vc = P.vc, fu = P.fu, fv = P.fv;
+    for (int h = h0 + w; h < min(h0 + kPnPCheckHyp, nhyp); h += nw) {
+        if (P.counts[h] < 0) continue;   // invalid draw
+        const double* rt = P.rt + (size_t)h * 12;
+        double R[9], t[3];
+#pragma unroll
+        for (int j = 0; j < 9; j++) R[j] = rt[j];
+#pragma unroll
+        for (int j = 0; j < 3; j++) t[j] = rt[9 + j];
+        uint32_t* mask = P.masks + (size_t)h * words;
+        int n = 0;
+        for (int c = 0; c * 64 < N; c++) {
+            const int i = c * 64 + lane;
+            bool in = false;
+            if (i < N) {
+                const float X = X3[3 * i], Y = X3[3 * i + 1], Z = X3[3 * i + 2];
+                const float Xc = (float)(R[0] * X + R[1] * Y + R[2] * Z + t[0]);
+                const float Yc = (float)(R[3] * X + R[4] * Y + R[5] * Z + t[1]);
+                const float invZc = (float)(1 / (R[6] * X + R[7] * Y + R[8] * Z + t[2]));
+                const double ue = uc + fu * Xc * invZc;
+                const double ve = vc + fv * Yc * invZc;
+                const float distX = (float)(U2[2 * i] - ue);
+                const float distY = (float)(U2[2 * i + 1] - ve);
+                const float error2 = distX * distX + distY * distY;
+                in = error2 < ME[i];
+            }
+            const unsigned long long b = __ballot(in);
+            n += __popcll(b);
+            if (lane == 0) {
+                mask[2 * c] = (uint32_t)b;
+                if (2 * c + 1 < words) mask[2 * c + 1] = (uint32_t)(b >> 32);
+            }
+        }
+        if (lane == 0) P.counts[h] = n;
+    }
 }
 
 // Refine (260-305): EPnP on the best-so-far inliers, then CheckInliers.
@@ -207,6 +271,8 @@ static void rt_to_tcw(const double* rt, float* T) {
 }
 
 PnPBatch::~PnPBatch() {
+    for (auto& e : ev_)
+        if (e) (void)hipEventDestroy(e);
     if (d_work_) (void)hipFree(d_work_);
     if (d_probs_) (void)hipFree(d_probs_);
     if (h_work_) (void)hipHostFree(h_work_);
@@ -217,6 +283,19 @@ int PnPBatch::init() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    for (auto& e : ev_) ORB_HIP_CHECK(hipEventCreate(&e));
+    return 0;
+}
+
+// ms of the last timed iterate()'s hypothesis launches: {solve, check}; plus the hypotheses
+// and (hypothesis, point) pairs they covered
+int PnPBatch::last_timings(float* ms2, long long* hyp_pts2) {
+    if (!timed_) return -1;
+    ORB_HIP_CHECK(hipEventSynchronize(ev_[2]));
+    ORB_HIP_CHECK(hipEventElapsedTime(&ms2[0], ev_[0], ev_[1]));
+    ORB_HIP_CHECK(hipEventElapsedTime(&ms2[1], ev_[1], ev_[2]));
+    hyp_pts2[0] = last_hyp_;
+    hyp_pts2[1] = last_pts_;
     return 0;
 }
 
@@ -245,18 +324,17 @@ int PnPBatch::ensure(size_t dev_bytes, size_t host_bytes, size_t probs) {
 // cannot drift apart: an earlier version summed unaligned sizes for the Refine scratch while
 // the carve aligned each sub-buffer, and the last solvers' Refine buffers ran past the work
 // area (the PnP fault of 9f527cb; tests/test_pnp_layout.py pins the invariant).
+//   device: [draws of every solver | (masks, counts, (R, t)) of every solver | Refine slots]
+//   pinned host: a byte-for-byte mirror of the first two regions, so the draws go up in one
+//   copy and the results come back in one copy for any number of solvers.
 struct PnPLayout {
     static size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
     static int words(int N) { return (N + 31) >> 5; }
-    // hypothesis region of a solver with K hypotheses: idx | masks | counts | (R, t)
     static size_t hyp_bytes(int K, int minSet) { return al((size_t)K * minSet * 4); }
     static size_t mask_bytes(int K, int N) { return al((size_t)K * words(N) * 4); }
     static size_t cnt_bytes(int K) { return al((size_t)K * 4); }
     static size_t rt_bytes(int K) { return al((size_t)K * 12 * 8); }
-    // pinned staging of a solver's results: counts | masks | (R, t)
-    static size_t host_mask_off(int K) { return cnt_bytes(K); }
-    static size_t host_rt_off(int K, int N) { return cnt_bytes(K) + mask_bytes(K, N); }
-    static size_t host_slot(int K, int N) { return host_rt_off(K, N) + al((size_t)K * 96); }
+    static size_t res_bytes(int K, int N) { return mask_bytes(K, N) + cnt_bytes(K) + rt_bytes(K); }
     // Refine slot of a solver: inlier idx list | mask | (R, t) | inlier count
     static size_t ref_mask_off(int N) { return al((size_t)N * 4); }
     static size_t ref_rt_off(int N) { return ref_mask_off(N) + al((size_t)words(N) * 4); }
@@ -266,25 +344,28 @@ struct PnPLayout {
 
 int pnp_layout_check(int n, const int* N, const int* K, const int* minSet, long long* out4) {
     // accounting as iterate() does it
-    size_t dev = 0, host = 0;
-    for (int k = 0; k < n; k++) {
-        dev += PnPLayout::hyp_bytes(K[k], minSet[k]) + PnPLayout::mask_bytes(K[k], N[k]) + PnPLayout::cnt_bytes(K[k]) +
-               PnPLayout::rt_bytes(K[k]);
-        host = std::max(host, PnPLayout::host_slot(K[k], N[k]));
-    }
-    const size_t ref_base = dev;
+    size_t dev = 0;
+    for (int k = 0; k < n; k++) dev += PnPLayout::hyp_bytes(K[k], minSet[k]) + PnPLayout::res_bytes(K[k], N[k]);
+    const size_t mirror = dev;
     for (int k = 0; k < n; k++) dev += PnPLayout::ref_slot(N[k]);
-    const size_t dev_cap = dev + 256, host_cap = (host + 256) * n + 1024;
-    // every byte the carve touches: hypothesis regions, all solvers needing Refine at once
-    size_t dend = 0, o = 0, hend = 0, ho = 0;
+    const size_t dev_cap = dev + 256, host_cap = mirror + 256;
+    // every byte the carve touches: the draw region, the result region (kernels write masks,
+    // counts and K * 96 B of poses), every solver's Refine slot at once; the host mirror
+    size_t dend = 0, o = 0;
     for (int k = 0; k < n; k++) {
-        o += PnPLayout::hyp_bytes(K[k], minSet[k]) + PnPLayout::mask_bytes(K[k], N[k]) + PnPLayout::cnt_bytes(K[k]);
+        dend = std::max(dend, o + (size_t)K[k] * minSet[k] * 4);
+        o += PnPLayout::hyp_bytes(K[k], minSet[k]);
+    }
+    for (int k = 0; k < n; k++) {
+        dend = std::max(dend, o + (size_t)K[k] * PnPLayout::words(N[k]) * 4);
+        o += PnPLayout::mask_bytes(K[k], N[k]);
+        dend = std::max(dend, o + (size_t)K[k] * 4);
+        o += PnPLayout::cnt_bytes(K[k]);
         dend = std::max(dend, o + (size_t)K[k] * 96);
         o += PnPLayout::rt_bytes(K[k]);
-        hend = std::max(hend, ho + PnPLayout::host_rt_off(K[k], N[k]) + (size_t)K[k] * 96);
-        ho += PnPLayout::host_slot(K[k], N[k]);
     }
-    size_t ro = ref_base;
+    const size_t hend = o;
+    size_t ro = o;
     for (int k = 0; k < n; k++) {
         dend = std::max(dend, ro + PnPLayout::ref_out_off(N[k]) + 4);
         dend = std::max(dend, ro + (size_t)N[k] * 4);
@@ -307,7 +388,7 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
         int next = 0;         // next hypothesis to replay
     };
     std::vector<Job> jobs(n);
-    size_t dev = 0, host = 0;
+    size_t dev = 0;
     using LY = PnPLayout;
     for (int k = 0; k < n; k++) {
         PnPSolver& P = *S[k];
@@ -326,20 +407,24 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
         J.active = J.K > 0;
         J.snap = *rngs[k];
         J.hyp_off = dev; dev += LY::hyp_bytes(J.K, P.minSet_);
-        J.mask_off = dev; dev += LY::mask_bytes(J.K, P.N_);
-        J.cnt_off = dev; dev += LY::cnt_bytes(J.K);
-        J.rt_off = dev; dev += LY::rt_bytes(J.K);
-        host = std::max(host, LY::host_slot(J.K, P.N_));
         if (int e = P.upload(s)) return e;
     }
+    const size_t res_base = dev;
+    for (int k = 0; k < n; k++) {
+        Job& J = jobs[k];
+        const int N = S[k]->N_;
+        J.mask_off = dev; dev += LY::mask_bytes(J.K, N);
+        J.cnt_off = dev; dev += LY::cnt_bytes(J.K);
+        J.rt_off = dev; dev += LY::rt_bytes(J.K);
+    }
     // refine scratch (per solver): idx list N + mask + rt + count
-    size_t ref_base = dev;
+    const size_t ref_base = dev;
     for (int k = 0; k < n; k++) dev += LY::ref_slot(S[k]->N_);
-    if (int e = ensure(dev + 256, (host + 256) * n + 1024, (size_t)n)) return e;
+    if (int e = ensure(dev + 256, ref_base + 256, (size_t)n)) return e;
     char* D = (char*)d_work_;
     char* Hh = (char*)h_work_;
-    // 1. generate all hypotheses (draws as the reference would make them)
-    std::vector<int> hyp;
+    // 1. generate all hypotheses (draws as the reference would make them), straight into the
+    //    pinned mirror of the draw region
     std::vector<PnPProbDev> pd(n);
     int maxK = 0;
     for (int k = 0; k < n; k++) {
@@ -348,19 +433,23 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
         std::memset(&pd[k], 0, sizeof(PnPProbDev));
         if (!J.active) continue;
         orb_rng g = J.snap;
-        hyp.assign((size_t)J.K * P.minSet_, 0);
-        std::vector<int> avail(P.N_);
+        int* hyp = (int*)(Hh + J.hyp_off);
+        // vAvailableIndices = mvAllIndices per iteration (PnPsolver.cc:196-203): the draw writes
+        // minSet slots, undone after each hypothesis instead of re-filling all N
+        std::vector<int> avail(P.N_), pos(P.minSet_), old(P.minSet_);
+        for (int i = 0; i < P.N_; i++) avail[i] = i;
         for (int h = 0; h < J.K; h++) {
-            for (int i = 0; i < P.N_; i++) avail[i] = i;
             int navail = P.N_;
             for (int i = 0; i < P.minSet_; ++i) {
                 const int randi = random_int(&g, 0, navail - 1);
                 hyp[(size_t)h * P.minSet_ + i] = avail[randi];
+                pos[i] = randi;
+                old[i] = avail[randi];
                 avail[randi] = avail[navail - 1];
                 navail--;
             }
+            for (int i = P.minSet_ - 1; i >= 0; --i) avail[pos[i]] = old[i];
         }
-        ORB_HIP_CHECK(hipMemcpyAsync(D + J.hyp_off, hyp.data(), hyp.size() * 4, hipMemcpyHostToDevice, s));
         const float* dp = (const float*)P.d_pts_;
         PnPProbDev& q = pd[k];
         q.p3d = dp;
@@ -396,26 +485,25 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
             if (!ok) return -1;
         }
     }
+    if (res_base > 0) ORB_HIP_CHECK(hipMemcpyAsync(D, Hh, res_base, hipMemcpyHostToDevice, s));
     ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(PnPProbDev) * n, hipMemcpyHostToDevice, s));
-    if (maxK > 0)
+    if (maxK > 0) {
+        if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[0], s));
         hipLaunchKernelGGL(k_pnp_hypotheses, dim3((maxK + 63) / 64, n), dim3(64), 0, s, (const PnPProbDev*)d_probs_);
-    ORB_HIP_CHECK(hipGetLastError());
-    // 2. results back (counts, masks, poses) in one pinned region per solver
-    std::vector<size_t> hoff(n, 0);
-    size_t ho = 0;
-    for (int k = 0; k < n; k++) {
-        Job& J = jobs[k];
-        if (!J.active) continue;
-        PnPSolver& P = *S[k];
-        const int words = (P.N_ + 31) >> 5;
-        hoff[k] = ho;
-        ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho, D + J.cnt_off, (size_t)J.K * 4, hipMemcpyDeviceToHost, s));
-        ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho + LY::host_mask_off(J.K), D + J.mask_off, (size_t)J.K * words * 4,
-                                     hipMemcpyDeviceToHost, s));
-        ORB_HIP_CHECK(hipMemcpyAsync(Hh + ho + LY::host_rt_off(J.K, P.N_), D + J.rt_off, (size_t)J.K * 96,
-                                     hipMemcpyDeviceToHost, s));
-        ho += LY::host_slot(J.K, P.N_);
+        if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
+        hipLaunchKernelGGL(k_pnp_check, dim3((maxK + kPnPCheckHyp - 1) / kPnPCheckHyp, n), dim3(kPnPCheckThreads), 0, s,
+                           (const PnPProbDev*)d_probs_);
+        if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
+        last_hyp_ = 0;
+        for (int k = 0; k < n; k++) last_hyp_ += jobs[k].active ? jobs[k].K : 0;
+        last_pts_ = 0;
+        for (int k = 0; k < n; k++) last_pts_ += jobs[k].active ? (long long)jobs[k].K * S[k]->N_ : 0;
+        timed_ = timing_;
     }
+    ORB_HIP_CHECK(hipGetLastError());
+    // 2. results back (counts, masks, poses of every solver) in one copy
+    if (ref_base > res_base)
+        ORB_HIP_CHECK(hipMemcpyAsync(Hh + res_base, D + res_base, ref_base - res_base, hipMemcpyDeviceToHost, s));
     ORB_HIP_CHECK(hipStreamSynchronize(s));
     // 3. sequential replay; Refine requests batched across solvers
     std::vector<char> done(n, 0);
@@ -428,9 +516,9 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
             Job& J = jobs[k];
             PnPSolver& P = *S[k];
             const int words = (P.N_ + 31) >> 5;
-            const int* cnt = (const int*)(Hh + hoff[k]);
-            const uint32_t* masks = (const uint32_t*)(Hh + hoff[k] + LY::host_mask_off(J.K));
-            const double* rts = (const double*)(Hh + hoff[k] + LY::host_rt_off(J.K, P.N_));
+            const int* cnt = (const int*)(Hh + J.cnt_off);
+            const uint32_t* masks = (const uint32_t*)(Hh + J.mask_off);
+            const double* rts = (const double*)(Hh + J.rt_off);
             bool wait = false;
             while (J.next < J.K) {
                 const int h = J.next;

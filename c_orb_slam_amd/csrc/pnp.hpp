@@ -79,8 +79,13 @@ public:
     int init();
     int iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnPResult* res);
     hipStream_t stream() const { return stream_; }
+    void enable_timing(bool on) { timing_ = on; }
+    int last_timings(float* ms2, long long* hyp_pts2);
 
 private:
+    bool timing_ = false, timed_ = false;
+    hipEvent_t ev_[3] = {};
+    long long last_hyp_ = 0, last_pts_ = 0;
     int ensure(size_t dev_bytes, size_t host_bytes, size_t probs);
     hipStream_t stream_ = nullptr;
     void* d_work_ = nullptr;

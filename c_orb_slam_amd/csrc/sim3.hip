@@ -104,6 +104,23 @@ __device__ __forceinline__ void jacobi_eigen4(float* A, float* W, float* V) {
     }
 }
 
+// mT21i = [sR^-1 | -sR^-1 t] (Sim3Solver.cc:323-335); shared by the solve and the check kernel
+__device__ __forceinline__ void sim3_T21(const float* R, const float* t, float s, float* T21) {
+    float sRinv[9];
+    const double is = 1.0 / s;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            sRinv[3 * i + j] = (float)(is * (double)R[3 * j + i]);
+            T21[4 * i + j] = sRinv[3 * i + j];
+        }
+    for (int i = 0; i < 3; i++) {
+        const double v = (double)sRinv[3 * i] * t[0] + (double)sRinv[3 * i + 1] * t[1] + (double)sRinv[3 * i + 2] * t[2];
+        T21[4 * i + 3] = (float)(-v);
+    }
+    T21[12] = T21[13] = T21[14] = 0.f;
+    T21[15] = 1.f;
+}
+
 // ComputeSim3 (226-337); P1/P2 [row][col], column i = point i.  est: R9 t3 s T12[16] T21[16]
 __device__ __forceinline__ void compute_sim3(const float P1[3][3], const float P2[3][3], int bFixScale, float* R,
                                              float* t, float* s_out, float* T12, float* T21) {
@@ -180,20 +197,11 @@ __device__ __forceinline__ void compute_sim3(const float P1[3][3], const float P
     }
     for (int i = 0; i < 16; i++) T12[i] = T21[i] = 0.f;
     T12[15] = T21[15] = 1.f;
-    float sRinv[9];
-    const double is = 1.0 / s;
     for (int i = 0; i < 3; i++) {
-        for (int j = 0; j < 3; j++) {
-            T12[4 * i + j] = (float)(s * (double)R[3 * i + j]);
-            sRinv[3 * i + j] = (float)(is * (double)R[3 * j + i]);
-            T21[4 * i + j] = sRinv[3 * i + j];
-        }
+        for (int j = 0; j < 3; j++) T12[4 * i + j] = (float)(s * (double)R[3 * i + j]);
         T12[4 * i + 3] = t[i];
     }
-    for (int i = 0; i < 3; i++) {
-        const double v = (double)sRinv[3 * i] * t[0] + (double)sRinv[3 * i + 1] * t[1] + (double)sRinv[3 * i + 2] * t[2];
-        T21[4 * i + 3] = (float)(-v);
-    }
+    sim3_T21(R, t, s, T21);
 }
 
 __device__ __forceinline__ void project(const float* X, const float* T, const float* K, float* uv) {
@@ -220,35 +228,83 @@ __global__ void __launch_bounds__(64) k_sim3_hypotheses(const Sim3ProbDev* __res
     }
     float R[9], t[3], s, T12[16], T21[16];
     compute_sim3(P1, P2, P.bFixScale, R, t, &s, T12, T21);
-    // CheckInliers (340-364)
-    const int words = (P.N + 31) >> 5;
-    uint32_t* mask = P.masks + (size_t)h * words;
-    int n = 0;
-    for (int w = 0; w < words; w++) {
-        uint32_t bits = 0;
-        for (int b = 0; b < 32; b++) {
-            const int i = w * 32 + b;
-            if (i >= P.N) break;
-            float p2im1[2], p1im2[2];
-            project(P.X2 + 3 * i, T12, P.K1, p2im1);
-            project(P.X1 + 3 * i, T21, P.K2, p1im2);
-            const float d1x = P.p1[2 * i] - p2im1[0], d1y = P.p1[2 * i + 1] - p2im1[1];
-            const float d2x = p1im2[0] - P.p2[2 * i], d2y = p1im2[1] - P.p2[2 * i + 1];
-            const float err1 = (float)((double)d1x * d1x + (double)d1y * d1y);
-            const float err2 = (float)((double)d2x * d2x + (double)d2y * d2y);
-            if (err1 < P.maxErr1[i] && err2 < P.maxErr2[i]) {
-                bits |= 1u << b;
-                n++;
-            }
-        }
-        mask[w] = bits;
-    }
-    P.counts[h] = n;
     float* e = P.est + (size_t)h * 32;
     for (int i = 0; i < 9; i++) e[i] = R[i];
     for (int i = 0; i < 3; i++) e[9 + i] = t[i];
     e[12] = s;
     for (int i = 0; i < 16; i++) e[16 + i] = T12[i];
+}
+
+// CheckInliers (340-364) lane-parallel over the matched pairs: a workgroup per (solver,
+// kSim3CheckHyp hypotheses), the solver's 48-B pairs staged once in LDS when they fit, a wave
+// per hypothesis, one ballot per 64 pairs.  T21 is re-derived from the stored (R, t, s) by the
+// same sim3_T21 the solve used.
+constexpr int kSim3CheckThreads = 256;
+constexpr int kSim3CheckHyp = 16;
+constexpr int kSim3StageMax = 1024;   // 48 KiB of LDS
+__global__ void __launch_bounds__(kSim3CheckThreads) k_sim3_check(const Sim3ProbDev* __restrict__ probs) {
+    const Sim3ProbDev& P = probs[blockIdx.y];
+    const int N = P.N, nhyp = P.nhyp;
+    const int h0 = blockIdx.x * kSim3CheckHyp;
+    if (h0 >= nhyp) return;
+    __shared__ float sX1[kSim3StageMax * 3], sX2[kSim3StageMax * 3], sp1[kSim3StageMax * 2],
+        sp2[kSim3StageMax * 2], sE1[kSim3StageMax], sE2[kSim3StageMax];
+    const bool staged = N <= kSim3StageMax;
+    if (staged) {
+        for (int i = threadIdx.x; i < 3 * N; i += blockDim.x) {
+            sX1[i] = P.X1[i];
+            sX2[i] = P.X2[i];
+        }
+        for (int i = threadIdx.x; i < 2 * N; i += blockDim.x) {
+            sp1[i] = P.p1[i];
+            sp2[i] = P.p2[i];
+        }
+        for (int i = threadIdx.x; i < N; i += blockDim.x) {
+            sE1[i] = P.maxErr1[i];
+            sE2[i] = P.maxErr2[i];
+        }
+    }
+    __syncthreads();
+    const float* X1 = staged ? sX1 : P.X1;
+    const float* X2 = staged ? sX2 : P.X2;
+    const float* p1 = staged ? sp1 : P.p1;
+    const float* p2 = staged ? sp2 : P.p2;
+    const float* E1 = staged ? sE1 : P.maxErr1;
+    const float* E2 = staged ? sE2 : P.maxErr2;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const int words = (N + 31) >> 5;
+    for (int h = h0 + w; h < min(h0 + kSim3CheckHyp, nhyp); h += nw) {
+        const float* e = P.est + (size_t)h * 32;
+        float R[9], t[3], T12[16], T21[16];
+        for (int i = 0; i < 9; i++) R[i] = e[i];
+        for (int i = 0; i < 3; i++) t[i] = e[9 + i];
+        const float s = e[12];
+        for (int i = 0; i < 16; i++) T12[i] = e[16 + i];
+        sim3_T21(R, t, s, T21);
+        uint32_t* mask = P.masks + (size_t)h * words;
+        int n = 0;
+        for (int c = 0; c * 64 < N; c++) {
+            const int i = c * 64 + lane;
+            bool in = false;
+            if (i < N) {
+                float p2im1[2], p1im2[2];
+                project(X2 + 3 * i, T12, P.K1, p2im1);
+                project(X1 + 3 * i, T21, P.K2, p1im2);
+                const float d1x = p1[2 * i] - p2im1[0], d1y = p1[2 * i + 1] - p2im1[1];
+                const float d2x = p1im2[0] - p2[2 * i], d2y = p1im2[1] - p2[2 * i + 1];
+                const float err1 = (float)((double)d1x * d1x + (double)d1y * d1y);
+                const float err2 = (float)((double)d2x * d2x + (double)d2y * d2y);
+                in = err1 < E1[i] && err2 < E2[i];
+            }
+            const unsigned long long b = __ballot(in);
+            n += __popcll(b);
+            if (lane == 0) {
+                mask[2 * c] = (uint32_t)b;
+                if (2 * c + 1 < words) mask[2 * c + 1] = (uint32_t)(b >> 32);
+            }
+        }
+        if (lane == 0) P.counts[h] = n;
+    }
 }
 
 // ----------------------------------------------------------------------- host
@@ -324,6 +380,8 @@ int Sim3Solver::upload(hipStream_t s) {
 }
 
 Sim3Batch::~Sim3Batch() {
+    for (auto& e : ev_)
+        if (e) (void)hipEventDestroy(e);
     if (d_work_) (void)hipFree(d_work_);
     if (d_probs_) (void)hipFree(d_probs_);
     if (h_work_) (void)hipHostFree(h_work_);
@@ -334,6 +392,17 @@ int Sim3Batch::init() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    for (auto& e : ev_) ORB_HIP_CHECK(hipEventCreate(&e));
+    return 0;
+}
+
+int Sim3Batch::last_timings(float* ms2, long long* hyp_pts2) {
+    if (!timed_) return -1;
+    ORB_HIP_CHECK(hipEventSynchronize(ev_[2]));
+    ORB_HIP_CHECK(hipEventElapsedTime(&ms2[0], ev_[0], ev_[1]));
+    ORB_HIP_CHECK(hipEventElapsedTime(&ms2[1], ev_[1], ev_[2]));
+    hyp_pts2[0] = last_hyp_;
+    hyp_pts2[1] = last_pts_;
     return 0;
 }
 
@@ -341,9 +410,12 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
     hipStream_t s = stream_;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     std::vector<int> K(n, 0);
-    std::vector<size_t> hyp_off(n), cnt_off(n), mask_off(n), est_off(n), hoff(n);
+    std::vector<size_t> hyp_off(n), cnt_off(n), mask_off(n), est_off(n);
     std::vector<orb_rng> snap(n);
-    size_t dev = 0, host = 0;
+    // work area: [every solver's hypothesis draws | every solver's counts, masks, estimates];
+    // the pinned host buffer mirrors it byte for byte, so the draws go up in ONE copy and the
+    // results come back in ONE copy whatever the number of solvers
+    size_t dev = 0;
     for (int k = 0; k < n; k++) {
         Sim3Solver& P = *S[k];
         Sim3Result& r = res[k];
@@ -358,15 +430,17 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
         // `while (mnIterations < max && nCurrent < nIterations)`
         K[k] = std::max(0, std::min(P.maxIts_ - P.nIterations_, nIterations));
         snap[k] = *rngs[k];
-        const int words = (P.N_ + 31) >> 5;
         hyp_off[k] = dev; dev += al((size_t)K[k] * 12);
+        if (int e = P.upload(s)) return e;
+    }
+    const size_t res_base = dev;
+    for (int k = 0; k < n; k++) {
+        const int words = (S[k]->N_ + 31) >> 5;
         cnt_off[k] = dev; dev += al((size_t)K[k] * 4);
         mask_off[k] = dev; dev += al((size_t)K[k] * words * 4);
         est_off[k] = dev; dev += al((size_t)K[k] * 128);
-        hoff[k] = host;
-        host += al((size_t)K[k] * 4) + al((size_t)K[k] * words * 4) + al((size_t)K[k] * 128);
-        if (int e = P.upload(s)) return e;
     }
+    const size_t host = dev;
     if (dev + 256 > work_cap_) {
         if (d_work_) (void)hipFree(d_work_);
         ORB_HIP_CHECK(hipMalloc(&d_work_, dev + 256));
@@ -385,27 +459,29 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
     char* D = (char*)d_work_;
     char* Hh = (char*)h_work_;
     std::vector<Sim3ProbDev> pd(n);
-    std::vector<std::vector<int>> hyps(n);
     int maxK = 0;
     for (int k = 0; k < n; k++) {
         std::memset(&pd[k], 0, sizeof(Sim3ProbDev));
         if (K[k] <= 0) continue;
         Sim3Solver& P = *S[k];
         orb_rng g = snap[k];
-        std::vector<int>& hyp = hyps[k];
-        hyp.assign((size_t)K[k] * 3, 0);
+        int* hyp = (int*)(Hh + hyp_off[k]);
+        // vAvailableIndices = mvAllIndices per iteration: the draw writes 3 slots, undone after
+        // each hypothesis instead of re-filling all N (same draws, O(1) per hypothesis)
         std::vector<int> avail(P.N_);
+        for (int i = 0; i < P.N_; i++) avail[i] = i;
         for (int h = 0; h < K[k]; h++) {
-            for (int i = 0; i < P.N_; i++) avail[i] = i;
-            int navail = P.N_;
+            int navail = P.N_, pos[3], old[3];
             for (int i = 0; i < 3; ++i) {
                 const int randi = random_int3(&g, 0, navail - 1);
                 hyp[3 * h + i] = avail[randi];
+                pos[i] = randi;
+                old[i] = avail[randi];
                 avail[randi] = avail[navail - 1];
                 navail--;
             }
+            for (int i = 2; i >= 0; --i) avail[pos[i]] = old[i];
         }
-        ORB_HIP_CHECK(hipMemcpyAsync(D + hyp_off[k], hyp.data(), hyp.size() * 4, hipMemcpyHostToDevice, s));
         const float* d = (const float*)P.d_pts_;
         Sim3ProbDev& q = pd[k];
         q.X1 = d; q.X2 = d + 3 * P.N_; q.p1 = d + 6 * P.N_; q.p2 = d + 8 * P.N_;
@@ -421,20 +497,26 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
         q.est = (float*)(D + est_off[k]);
         maxK = std::max(maxK, K[k]);
     }
+    if (res_base > 0)
+        ORB_HIP_CHECK(hipMemcpyAsync(D, Hh, res_base, hipMemcpyHostToDevice, s));
     ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(Sim3ProbDev) * n, hipMemcpyHostToDevice, s));
-    if (maxK > 0)
+    if (maxK > 0) {
+        if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[0], s));
         hipLaunchKernelGGL(k_sim3_hypotheses, dim3((maxK + 63) / 64, n), dim3(64), 0, s, (const Sim3ProbDev*)d_probs_);
-    ORB_HIP_CHECK(hipGetLastError());
-    for (int k = 0; k < n; k++) {
-        if (K[k] <= 0) continue;
-        const int words = (S[k]->N_ + 31) >> 5;
-        char* h = Hh + hoff[k];
-        ORB_HIP_CHECK(hipMemcpyAsync(h, D + cnt_off[k], (size_t)K[k] * 4, hipMemcpyDeviceToHost, s));
-        ORB_HIP_CHECK(hipMemcpyAsync(h + al((size_t)K[k] * 4), D + mask_off[k], (size_t)K[k] * words * 4,
-                                     hipMemcpyDeviceToHost, s));
-        ORB_HIP_CHECK(hipMemcpyAsync(h + al((size_t)K[k] * 4) + al((size_t)K[k] * words * 4), D + est_off[k],
-                                     (size_t)K[k] * 128, hipMemcpyDeviceToHost, s));
+        if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
+        hipLaunchKernelGGL(k_sim3_check, dim3((maxK + kSim3CheckHyp - 1) / kSim3CheckHyp, n), dim3(kSim3CheckThreads),
+                           0, s, (const Sim3ProbDev*)d_probs_);
+        if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
+        last_hyp_ = last_pts_ = 0;
+        for (int k = 0; k < n; k++) {
+            last_hyp_ += K[k] > 0 ? K[k] : 0;
+            last_pts_ += K[k] > 0 ? (long long)K[k] * S[k]->N_ : 0;
+        }
+        timed_ = timing_;
     }
+    ORB_HIP_CHECK(hipGetLastError());
+    if (dev > res_base)
+        ORB_HIP_CHECK(hipMemcpyAsync(Hh + res_base, D + res_base, dev - res_base, hipMemcpyDeviceToHost, s));
     ORB_HIP_CHECK(hipStreamSynchronize(s));
     // sequential replay (Sim3Solver.cc:158-206)
     for (int k = 0; k < n; k++) {
@@ -442,16 +524,16 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
         Sim3Result& r = res[k];
         if (P.N_ < P.minInliers_) continue;
         const int words = (P.N_ + 31) >> 5;
-        const char* h = Hh + hoff[k];
-        const int* cnt = (const int*)h;
-        const uint32_t* masks = (const uint32_t*)(h + al((size_t)K[k] * 4));
-        const float* est = (const float*)(h + al((size_t)K[k] * 4) + al((size_t)K[k] * words * 4));
+        const int* cnt = (const int*)(Hh + cnt_off[k]);
+        const uint32_t* masks = (const uint32_t*)(Hh + mask_off[k]);
+        const float* est = (const float*)(Hh + est_off[k]);
         int consumed = K[k];
+        int best = -1;   // last hypothesis that became the best: its mask is expanded once, below
         for (int hh = 0; hh < K[k]; hh++) {
             P.nIterations_++;
             const int c = cnt[hh];
             if (c >= P.nBestInliers_) {
-                for (int i = 0; i < P.N_; i++) P.bestInliers_[i] = (masks[(size_t)hh * words + (i >> 5)] >> (i & 31)) & 1;
+                best = hh;
                 P.nBestInliers_ = c;
                 const float* e = est + (size_t)hh * 32;
                 std::memcpy(P.bestR_, e, 36);
@@ -459,6 +541,9 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
                 P.bestS_ = e[12];
                 std::memcpy(P.bestT12_, e + 16, 64);
                 if (c > P.minInliers_) {
+                    for (int i = 0; i < P.N_; i++)
+                        P.bestInliers_[i] = (masks[(size_t)hh * words + (i >> 5)] >> (i & 31)) & 1;
+                    best = -1;
                     r.has_pose = 1;
                     r.nInliers = c;
                     for (int i = 0; i < P.N_; i++)
@@ -469,6 +554,8 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
                 }
             }
         }
+        if (best >= 0)
+            for (int i = 0; i < P.N_; i++) P.bestInliers_[i] = (masks[(size_t)best * words + (i >> 5)] >> (i & 31)) & 1;
         *rngs[k] = snap[k];
         for (int d = 0; d < consumed * 3; d++) (void)rng_rand(rngs[k]);
         if (!r.has_pose && P.nIterations_ >= P.maxIts_) r.bNoMore = 1;

@@ -58,8 +58,13 @@ public:
     ~Sim3Batch();
     int init();
     int iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, Sim3Result* res);
+    void enable_timing(bool on) { timing_ = on; }
+    int last_timings(float* ms2, long long* hyp_pts2);
 
 private:
+    bool timing_ = false, timed_ = false;
+    hipEvent_t ev_[3] = {};
+    long long last_hyp_ = 0, last_pts_ = 0;
     hipStream_t stream_ = nullptr;
     void *d_work_ = nullptr, *d_probs_ = nullptr, *h_work_ = nullptr;
     size_t work_cap_ = 0, probs_cap_ = 0, hwork_cap_ = 0;

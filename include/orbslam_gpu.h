@@ -512,6 +512,11 @@ int PnPsolver_iterate_batch(int count, PnPsolver_h* hs, int nIterations, orb_rng
                             int* has_pose);
 /* RANSAC bookkeeping (mnIterations, mRansacMaxIts, mRansacMinInliers) */
 int PnPsolver_get_state(PnPsolver_h h, int* iterations, int* max_its, int* min_inliers);
+/* Measurement (no reference counterpart): HIP-event timing of the calling thread's
+ * hypothesis launches.  last_timings: ms2 = {EPnP solve, CheckInliers} of the last timed
+ * iterate call, counts2 = {hypotheses, (hypothesis, correspondence) pairs}. */
+int PnPsolver_enable_timing(int on);
+int PnPsolver_last_timings(float* ms2, long long* counts2);
 
 /* ======================================================================
  * Sim3Solver  (reference include/Sim3Solver.h:39-137, src/Sim3Solver.cc)
@@ -545,6 +550,9 @@ int Sim3Solver_iterate_batch(int count, Sim3Solver_h* hs, int nIterations, orb_r
 int Sim3Solver_get_estimate(Sim3Solver_h h, float* R, float* t, float* s);
 /* (mnIterations, mRansacMaxIts, mRansacMinInliers) */
 int Sim3Solver_get_state(Sim3Solver_h h, int* iterations, int* max_its, int* min_inliers);
+/* Measurement, as PnPsolver_enable_timing / PnPsolver_last_timings: {ComputeSim3, CheckInliers}. */
+int Sim3Solver_enable_timing(int on);
+int Sim3Solver_last_timings(float* ms2, long long* counts2);
 
 /* ======================================================================
  * Local bundle adjustment  (reference Optimizer::LocalBundleAdjustment,
