@@ -1109,7 +1109,6 @@ __device__ __forceinline__ double pose_rho0(const PoseEdgeD& e, double c, bool r
 constexpr int kPoseMaxEdges = 8192;
 constexpr int kPoseThreads = 512;   // 256 VGPRs per lane for the fused 28-term pass
 constexpr int kPosePer = kPoseMaxEdges / kPoseThreads;
-constexpr int kPoseLdsEdges = 2048;   // active edges staged in LDS per round (64 KiB)
 
 // Canonical totals (ora_csum level 2) of the m chunk trees cs[q][0..m) of K sums, by wave 0:
 // lane c holds chunk c and the K trees run packed (the same pairing as local_csum_inplace).
@@ -1136,9 +1135,9 @@ __device__ __forceinline__ void pose_chunk_totals(double (*cs)[kPoseMaxEdges / 6
 // computed.  f(e, i, out[K]) evaluates active edge i (edge e loaded).  Chunk trees go to
 // cs[q][c]; thread q < K finishes entry q.
 template <int K, class F>
-__device__ __forceinline__ void pose_pass(F f, int nA, const int* aE, const PoseEdgeDev* E, double dM, double dS,
+__device__ __forceinline__ void pose_pass(F f, int nA, const uint16_t* aE, const PoseEdgeDev* E, double dM, double dS,
                                           double (*cs)[kPoseMaxEdges / 64], double* res, const PoseEdgeD& mine,
-                                          int mineIdx, const PoseEdgeDev* Ls) {
+                                          int mineIdx) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int m = (nA + 63) >> 6;
     if (m <= nw) {
@@ -1165,18 +1164,14 @@ __device__ __forceinline__ void pose_pass(F f, int nA, const int* aE, const Pose
         __syncthreads();
         return;
     }
-    // the first kPoseLdsEdges active edges come from the round's LDS copy, the rest from HBM
-    auto load = [&](int a, int i) {
-        return a < kPoseLdsEdges ? pose_edge_load(Ls, a, dM, dS) : pose_edge_load(E, i, dM, dS);
-    };
     int c = w;
     int a = c * 64 + lane;
     int i = a < nA ? aE[a] : 0;
-    PoseEdgeD e = load(a, i);
+    PoseEdgeD e = pose_edge_load(E, i, dM, dS);
     while (c < m) {
         const int cn = c + nw, an = cn * 64 + lane;
         const int in = (cn < m && an < nA) ? aE[an] : 0;
-        const PoseEdgeD en = load(an, in);   // prefetch the next chunk's edge
+        const PoseEdgeD en = pose_edge_load(E, in, dM, dS);   // prefetch the next chunk's edge
         double v[K];
         if (a < nA) f(e, i, v);
         else
@@ -1364,9 +1359,10 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     const PoseEdgeDev* E = Eall + P.e0;
     (void)errAll;   // errors are recomputed at classification instead of kept per pass
     uint8_t* outl = outlAll + P.e0;
-    __shared__ uint8_t level[kPoseMaxEdges], robust[kPoseMaxEdges];
-    __shared__ int aE[kPoseMaxEdges];
-    __shared__ PoseEdgeDev Ls[kPoseLdsEdges];
+    // LDS kept near 53 KiB so three workgroups fit a CU next to the extraction kernels: edge
+    // flags (bit 0: level 1 = inactive, bit 1: robust kernel set), active-edge list as u16
+    __shared__ uint8_t fl[kPoseMaxEdges];
+    __shared__ uint16_t aE[kPoseMaxEdges];
     __shared__ double cs[28][kPoseMaxEdges / 64];
     __shared__ double red[32];
     __shared__ Se3 T, Tbak, Terr;
@@ -1388,8 +1384,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
         return;
     }
     for (int i = tid; i < ne; i += blockDim.x) {
-        level[i] = 0;
-        robust[i] = 1;
+        fl[i] = 2;
         outl[i] = 0;
     }
     __syncthreads();
@@ -1398,7 +1393,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     auto err_term = [&](const PoseEdgeD& e, int i, double* v) {
         double e3[3];
         pose_err(e, T, P, e3);
-        v[0] = pose_rho0(e, pose_chi2(e, e3), robust[i]);
+        v[0] = pose_rho0(e, pose_chi2(e, e3), (fl[i] & 2) != 0);
     };
     for (int it = 0; it < 4; it++) {
         if (tid == 0) {
@@ -1409,7 +1404,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
         {
             const int base = tid * kPosePer;
             int c = 0;
-            for (int j = 0; j < kPosePer; j++) c += (base + j < ne && level[base + j] == 0) ? 1 : 0;
+            for (int j = 0; j < kPosePer; j++) c += (base + j < ne && (fl[base + j] & 1) == 0) ? 1 : 0;
             int incl = c;   // inclusive scan within the wave
             for (int o = 1; o < 64; o <<= 1) {
                 const int t = __shfl_up(incl, o, 64);
@@ -1421,18 +1416,13 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
             for (int w = 0; w < (tid >> 6); w++) off += wsum[w];
             int pos = off + incl - c;
             for (int j = 0; j < kPosePer; j++)
-                if (base + j < ne && level[base + j] == 0) aE[pos++] = base + j;
+                if (base + j < ne && (fl[base + j] & 1) == 0) aE[pos++] = (uint16_t)(base + j);
             if (tid == blockDim.x - 1) nA = off + incl;
             __syncthreads();
         }
         const int na = nA;
         const int myIdx = tid < na ? aE[tid] : 0;
         const PoseEdgeD myE = pose_edge_load(E, myIdx, dM, dS);
-        if (na > kPoseThreads) {   // chunked passes: stage the round's active edges in LDS
-            const int nst = min(na, kPoseLdsEdges);
-            for (int a = tid; a < nst; a += blockDim.x) Ls[a] = E[aE[a]];
-            __syncthreads();
-        }
         if (na > 0) {   // optimize(10); without active edges the vertex is not optimised at all
             ORBGPU_PROF_START;
             for (int k = 0; k < 10; k++) {
@@ -1444,7 +1434,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                     double e3[3];
                     pose_err(e, T, P, e3);
                     const double c = pose_chi2(e, e3);
-                    const bool rb = robust[i];
+                    const bool rb = (fl[i] & 2) != 0;
                     v[0] = pose_rho0(e, c, rb);
                     double p[3];
                     se3_map(T, e.X, p);
@@ -1496,7 +1486,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                             v[1 + r * 6 - (r * (r - 1)) / 2 + (cc - r)] = hh;
                         }
                     }
-                }, na, aE, E, dM, dS, cs, red, myE, myIdx, Ls);
+                }, na, aE, E, dM, dS, cs, red, myE, myIdx);
                 ORBGPU_PROF_MARK(1);
                 if (tid < 28) {
                     if (tid == 0) currentChi = iniChi = red[0];
@@ -1541,7 +1531,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                     }
                     __syncthreads();
                     ORBGPU_PROF_MARK(2);
-                    pose_pass<1>(err_term, na, aE, E, dM, dS, cs, red, myE, myIdx, Ls);
+                    pose_pass<1>(err_term, na, aE, E, dM, dS, cs, red, myE, myIdx);
                     ORBGPU_PROF_MARK(3);
                     if (tid == 0) {
                         double tempChi = red[0];
@@ -1594,15 +1584,17 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
             double e3[3];
             pose_err(e, outl[i] ? T : Terr, P, e3);
             const float chi2 = (float)pose_chi2(e, e3);
+            uint8_t f = fl[i];
             if (chi2 > (e.stereo ? chi2Stereo : chi2Mono)) {
                 outl[i] = 1;
-                level[i] = 1;
+                f |= 1;
                 mybad++;
             } else {
                 outl[i] = 0;
-                level[i] = 0;
+                f &= 2;
             }
-            if (it == 2) robust[i] = 0;
+            if (it == 2) f &= 1;   // setRobustKernel(0)
+            fl[i] = f;
         }
         if (mybad) atomicAdd(&nBad, mybad);
         __syncthreads();
