@@ -349,25 +349,33 @@ def main():
             check(L.ORBmatcher_SearchLocalPoints_batch(m._h, P, self.curs_local, self.a_cur_mp, self.lmaps,
                                                        float(lsf), 1.0, ptr(self.nml), ptr(self.nvis)),
                   "SearchLocalPoints batch")
-            check(L.Optimizer_PoseOptimization_frames_device(P, self.pframes2, self.a_Tout2, self.a_poutl2,
-                                                             ptr(self.ninl2)), "PoseOptimization (local map)")
+            check(L.Optimizer_PoseOptimization_frames_device_deferred(m._h, P, self.pframes2, self.a_Tout2,
+                                                                      self.a_poutl2, ptr(self.ninl2)),
+                  "PoseOptimization (local map)")
 
         def track(self):
             """ComputeStereoMatches, UpdateLastFrame, SearchByProjection(Cur, Last, 7), PoseOptimization,
-            TrackLocalMap (SearchLocalPoints, PoseOptimization)."""
+            TrackLocalMap (SearchLocalPoints, PoseOptimization): one deferred chain on the matcher's
+            stream (ORBmatcher_set_deferred), every call queued behind the previous one without a
+            host round trip, the per-frame counts written by ORBmatcher_finish."""
             t1 = time.perf_counter()
             nL, nR = self.nL, self.nR
+            check(L.ORBmatcher_set_deferred(m._h, 1), "ORBmatcher_set_deferred")
             self.stereo()
             t2 = time.perf_counter()
             self.search()
             t3 = time.perf_counter()
             # Optimizer::PoseOptimization(&mCurrentFrame) (Tracking.cc:887) on the matched map points
-            check(L.Optimizer_PoseOptimization_frames_device(P, self.pframes, self.a_Tout, self.a_poutl,
-                                                             ptr(self.ninl)), "PoseOptimization batch")
+            check(L.Optimizer_PoseOptimization_frames_device_deferred(m._h, P, self.pframes, self.a_Tout,
+                                                                      self.a_poutl, ptr(self.ninl)),
+                  "PoseOptimization batch")
             t4 = time.perf_counter()
             self.local_map()
             t5 = time.perf_counter()
-            for k, v in (("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3), ("local_map", t5 - t4)):
+            check(L.ORBmatcher_set_deferred(m._h, 0), "ORBmatcher_set_deferred")   # finish: counts land
+            t6 = time.perf_counter()
+            for k, v in (("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3), ("local_map", t5 - t4),
+                         ("finish", t6 - t5)):
                 phase_acc[k] = phase_acc.get(k, 0.0) + v * 1e3
             tl, tr = self.exL.last_timings(), self.exR.last_timings()
             for k in tl:

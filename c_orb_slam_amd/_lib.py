@@ -107,6 +107,9 @@ def lib():
     L.ORBextractor_stream.argtypes = [vp]
     L.ORBextractor_last_timings.argtypes = [vp, vp]
     L.ORBmatcher_create.argtypes = [f32, i32, P(vp)]
+    L.ORBmatcher_set_deferred.argtypes = [vp, i32]
+    L.ORBmatcher_finish.argtypes = [vp]
+    L.Optimizer_PoseOptimization_frames_device_deferred.argtypes = [vp, i32, vp, vp, vp, vp]
     L.ORBmatcher_destroy.argtypes = [vp]
     L.ORBmatcher_set_device_pointers.argtypes = [vp, i32]
     L.ORBmatcher_stream.restype = vp

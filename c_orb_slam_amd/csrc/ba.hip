@@ -1049,6 +1049,7 @@ struct PoseProbDev {
     const float* uR;           // mvuRight
     const float* isig_tab;     // mvInvLevelSigma2
     int nlev;
+    int* ninl;                 // optional device out: inliers (ne - nBad), 0 below 3 edges, -1 over capacity
 };
 
 // one edge in double (the g2o edge's _measurement / information / Huber delta)
@@ -1371,11 +1372,15 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     __shared__ int nA, nBadLM, qmax, again, term, nBad, okS, wsum[16];
     const int tid = threadIdx.x;
     const double dM = (double)(float)sqrt(5.991), dS = (double)(float)sqrt(7.815);
-    if (ne < 0) return;   // device mode: capacity exceeded (reported by the host)
+    if (ne < 0) {   // device mode: capacity exceeded (reported by the host)
+        if (tid == 0 && P.ninl) *P.ninl = -1;
+        return;
+    }
     if (ne < 3) {
         if (tid == 0) {
             P.T = P.T0;
             P.nbad = -1;
+            if (P.ninl) *P.ninl = 0;
         }
         if (P.Tcw_out) {
             if (tid < 16) P.Tcw_out[tid] = P.Tcw[tid];
@@ -1603,6 +1608,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     if (tid == 0) {
         P.T = T;
         P.nbad = nBad;
+        if (P.ninl) *P.ninl = ne - nBad;
     }
     if (P.Tcw_out) {   // pFrame->SetPose(Converter::toCvMat(SE3quat_recov)); mvbOutlier
         if (tid == 0) {
@@ -1719,7 +1725,7 @@ int PoseEngine::run_device(int count, const pose_problem* P, float* const* Tcw_o
 }
 
 int PoseEngine::run_frames_device(int count, const pose_frame* F, float* const* Tcw_out, uint8_t* const* outlier,
-                                  int* ninliers) {
+                                  int* ninliers, hipStream_t s, DeferredChain* chain) {
     std::vector<int> Ns(count);
     for (int f = 0; f < count; f++) Ns[f] = F[f].N;
     return launch_device(count, Ns.data(), [&](int f, PoseProbDev& pp) {
@@ -1728,17 +1734,23 @@ int PoseEngine::run_frames_device(int count, const pose_frame* F, float* const* 
         pp.Tcw = Q.Tcw;
         pp.mpidx = Q.mp; pp.mp_pos = Q.mp_pos; pp.keys = (const float*)Q.keysUn; pp.uR = Q.uRight;
         pp.isig_tab = Q.invLevelSigma2; pp.nlev = Q.nlevels;
-    }, Tcw_out, outlier, ninliers);
+    }, Tcw_out, outlier, ninliers, s, chain);
 }
 
+// Device-mode launch.  Default: own stream, results synchronised before return.  With a
+// DeferredChain: enqueued on `s` behind the caller's previous work, the problem table staged
+// through the chain's pinned blocks and the inlier counts landing in `ninliers` at
+// chain.finish() (-1 for a frame over kPoseMaxEdges).
 int PoseEngine::launch_device(int count, const int* Ns, const std::function<void(int, PoseProbDev&)>& fill,
-                              float* const* Tcw_out, uint8_t* const* outlier, int* ninliers) {
+                              float* const* Tcw_out, uint8_t* const* outlier, int* ninliers, hipStream_t s,
+                              DeferredChain* chain) {
+    hipStream_t st = s ? s : stream_;
     size_t nmax = 0;
     for (int f = 0; f < count; f++) nmax += (size_t)std::min(Ns[f], kPoseMaxEdges + 1);
     const auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t bProb = al(sizeof(PoseProbDev) * count), bEdge = al(sizeof(PoseEdgeDev) * std::max<size_t>(nmax, 1));
-    const size_t bErr = al(sizeof(double) * 3 * std::max<size_t>(nmax, 1)), bOut = al(std::max<size_t>(nmax, 1));
-    const size_t need = bProb + bEdge + bErr + bOut;
+    const size_t bOut = al(std::max<size_t>(nmax, 1)), bNin = al(sizeof(int) * count);
+    const size_t need = bProb + bEdge + bOut + bNin;
     if (need > cap_) {
         if (dArena_) (void)hipFree(dArena_);
         if (hArena_) (void)hipHostFree(hArena_);
@@ -1748,9 +1760,14 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
         ORB_HIP_CHECK(hipHostMalloc(&hArena_, need));
         cap_ = need;
     }
-    char* h = (char*)hArena_;
     char* d = (char*)dArena_;
-    PoseProbDev* hp = (PoseProbDev*)h;
+    int* dNin = (int*)(d + bProb + bEdge + bOut);
+    std::vector<PoseProbDev> tmp;
+    PoseProbDev* hp = (PoseProbDev*)hArena_;
+    if (chain) {   // hArena_ may still be the source of an earlier queued copy: stage instead
+        tmp.resize(count);
+        hp = tmp.data();
+    }
     size_t e0 = 0;
     for (int f = 0; f < count; f++) {
         PoseProbDev& pp = hp[f];
@@ -1761,16 +1778,25 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
         fill(f, pp);
         pp.Tcw_out = Tcw_out[f];
         pp.outlier = outlier[f];
+        pp.ninl = dNin + f;
     }
     PoseProbDev* dp = (PoseProbDev*)d;
     PoseEdgeDev* dE = (PoseEdgeDev*)(d + bProb);
-    ORB_HIP_CHECK(hipMemcpyAsync(d, h, bProb, hipMemcpyHostToDevice, stream_));
-    hipLaunchKernelGGL(k_pose_pack, dim3(count), dim3(kPackThreads), 0, stream_, dp, dE);
-    hipLaunchKernelGGL(k_pose_opt, dim3(count), dim3(kPoseThreads), 0, stream_, dp, (const PoseEdgeDev*)dE,
-                       (double*)(d + bProb + bEdge), (uint8_t*)(d + bProb + bEdge + bErr));
+    const void* src = chain ? chain->stage(hp, sizeof(PoseProbDev) * count) : (const void*)hp;
+    if (!src) return -2;
+    ORB_HIP_CHECK(hipMemcpyAsync(d, src, sizeof(PoseProbDev) * count, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_pose_pack, dim3(count), dim3(kPackThreads), 0, st, dp, dE);
+    hipLaunchKernelGGL(k_pose_opt, dim3(count), dim3(kPoseThreads), 0, st, dp, (const PoseEdgeDev*)dE, nullptr,
+                       (uint8_t*)(d + bProb + bEdge));
     ORB_HIP_CHECK(hipGetLastError());
-    ORB_HIP_CHECK(hipMemcpyAsync(h, d, bProb, hipMemcpyDeviceToHost, stream_));
-    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (chain) {
+        void* land = chain->land(ninliers, sizeof(int) * count);
+        if (!land) return -2;
+        ORB_HIP_CHECK(hipMemcpyAsync(land, dNin, sizeof(int) * count, hipMemcpyDeviceToHost, st));
+        return 0;
+    }
+    ORB_HIP_CHECK(hipMemcpyAsync(hp, d, bProb, hipMemcpyDeviceToHost, st));
+    ORB_HIP_CHECK(hipStreamSynchronize(st));
     int rc = 0;
     for (int f = 0; f < count; f++) {
         const PoseProbDev& pp = hp[f];

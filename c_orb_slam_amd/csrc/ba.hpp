@@ -10,6 +10,7 @@
 #include "../../include/orbslam_gpu.h"
 #include "comm.hpp"
 #include "ldlt.hpp"
+#include "orb_common.hpp"
 
 namespace orbgpu {
 
@@ -144,13 +145,15 @@ public:
     // P's arrays, Tcw_out[f] (16 floats) and outlier[f] are device pointers
     int run_device(int count, const pose_problem* P, float* const* Tcw_out, uint8_t* const* outlier, int* ninliers);
     // pose_frame form: the edges are gathered from the frame's own arrays on the device
+    // s / chain: enqueue on the caller's stream inside its DeferredChain (results at finish())
     int run_frames_device(int count, const pose_frame* F, float* const* Tcw_out, uint8_t* const* outlier,
-                          int* ninliers);
+                          int* ninliers, hipStream_t s = nullptr, DeferredChain* chain = nullptr);
     hipStream_t stream() const { return stream_; }
 
 private:
     int launch_device(int count, const int* Ns, const std::function<void(int, PoseProbDev&)>& fill,
-                      float* const* Tcw_out, uint8_t* const* outlier, int* ninliers);
+                      float* const* Tcw_out, uint8_t* const* outlier, int* ninliers, hipStream_t s = nullptr,
+                      DeferredChain* chain = nullptr);
     hipStream_t stream_ = nullptr;
     void* dArena_ = nullptr;
     void* hArena_ = nullptr;   // pinned staging: problems + edges in, outliers back

@@ -7,6 +7,8 @@
 #include <vector>
 
 #include "ba.hpp"
+#include "capi_handles.hpp"
+#include "orb_match.hpp"
 #include "sim3opt.hpp"
 #include "orb_extract.hpp"
 #include "orb_match.hpp"
@@ -158,6 +160,26 @@ int Optimizer_PoseOptimization_frames_device(int count, const pose_frame* F, flo
     const int r = e->run_frames_device(count, F, Tcw_out, outlier, ninliers);
     if (r == -3) return ORB_E_CAPACITY;
     return r ? ORB_E_HIP : ORB_OK;
+}
+
+int Optimizer_PoseOptimization_frames_device_deferred(ORBmatcher_h chain, int count, const pose_frame* F,
+                                                      float* const* Tcw_out, uint8_t* const* outlier,
+                                                      int* ninliers) {
+    if (!chain || !chain->m->chain().on()) return ORB_E_INVALID;
+    if (count < 0 || (count > 0 && (!F || !Tcw_out || !outlier || !ninliers))) return ORB_E_INVALID;
+    for (int f = 0; f < count; f++) {
+        const pose_frame& Q = F[f];
+        if (Q.N < 0 || !Q.Tcw || !Tcw_out[f]) return ORB_E_INVALID;
+        if (Q.N > 0 && (!outlier[f] || !Q.mp || !Q.mp_pos || !Q.keysUn || !Q.uRight || !Q.invLevelSigma2 ||
+                        Q.nlevels <= 0))
+            return ORB_E_INVALID;
+    }
+    if (count == 0) return ORB_OK;
+    int rc = 0;
+    orbgpu::PoseEngine* e = pose_engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    orbgpu::Matcher* m = chain->m;
+    return e->run_frames_device(count, F, Tcw_out, outlier, ninliers, m->stream(), &m->chain()) ? ORB_E_HIP : ORB_OK;
 }
 
 int Optimizer_OptimizeSim3_batch(int count, const sim3opt_problem* P, double* S12, uint8_t* const* erased,

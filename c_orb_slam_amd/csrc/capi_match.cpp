@@ -101,6 +101,18 @@ int ORBmatcher_enable_timing(ORBmatcher_h h, int on) {
     return h->m->set_timing(on != 0) ? ORB_E_HIP : ORB_OK;
 }
 
+int ORBmatcher_set_deferred(ORBmatcher_h h, int on) {
+    if (!h || !h->m->device_pointers()) return ORB_E_INVALID;   // device-resident batches only
+    if (!on && h->m->chain().on() && h->m->chain().finish(h->m->stream())) return ORB_E_HIP;
+    h->m->chain().set(on != 0);
+    return ORB_OK;
+}
+
+int ORBmatcher_finish(ORBmatcher_h h) {
+    if (!h) return ORB_E_INVALID;
+    return h->m->chain().finish(h->m->stream()) ? ORB_E_HIP : ORB_OK;
+}
+
 int ORBmatcher_last_timings(ORBmatcher_h h, float* ms8, long long* counts8) {
     if (!h || !ms8 || !counts8) return ORB_E_INVALID;
     return h->m->timings(ms8, counts8) ? ORB_E_HIP : ORB_OK;
@@ -197,8 +209,12 @@ int ORBmatcher_SearchByProjection_LastFrame_batch(ORBmatcher_h h, int npairs, co
     }
     int rc = m->search_last(probs, th, bMono != 0);
     if (rc) return rc == -1 ? ORB_E_INVALID : ORB_E_HIP;
+    if (dev) {   // device mode may be deferred (ORBmatcher_set_deferred)
+        if (m->d2h_counts(nmatches, d_nm, (size_t)npairs * 4)) return ORB_E_HIP;
+        return m->end_call() ? ORB_E_HIP : ORB_OK;
+    }
     if (hipMemcpyAsync(nmatches, d_nm, (size_t)npairs * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return ORB_E_HIP;
-    if (!dev) {
+    {
         for (int p = 0; p < npairs; p++)
             if (cur[p].N > 0 &&
                 hipMemcpyAsync(cur_mp[p], probs[p].curMP, (size_t)cur[p].N * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
@@ -375,10 +391,10 @@ int ORBmatcher_SearchLocalPoints_batch(ORBmatcher_h h, int count, const orb_fram
     if (err) return err;
     const int rc = m->search_local_points(probs, fr, 0.5f, logScaleFactor, th);
     if (rc) return rc == -1 ? ORB_E_INVALID : ORB_E_HIP;
-    if (hipMemcpyAsync(nmatches, d_cnt, (size_t)count * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(nvisible, d_cnt + count, (size_t)count * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+    if (m->d2h_counts(nmatches, d_cnt, (size_t)count * 4) || m->d2h_counts(nvisible, d_cnt + count, (size_t)count * 4))
         return ORB_E_HIP;
-    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+    (void)s;
+    return m->end_call() ? ORB_E_HIP : ORB_OK;
 }
 
 int ORBmatcher_SearchCandidates(ORBmatcher_h h, const uint8_t* qdesc, int nq, const uint8_t* tdesc, int nt,

@@ -114,10 +114,14 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
     if (err || !d_kept) return ORB_E_HIP;
     auto* d_probs = (orbgpu::StereoDev*)m->arena_alloc(sizeof(orbgpu::StereoDev) * npairs);
     if (!d_probs) return ORB_E_HIP;
-    if (hipMemcpyAsync(d_probs, probs.data(), sizeof(orbgpu::StereoDev) * npairs, hipMemcpyHostToDevice, s) !=
-        hipSuccess)
+    if (hipMemcpyAsync(d_probs, m->h2d_src(probs.data(), sizeof(orbgpu::StereoDev) * npairs),
+                       sizeof(orbgpu::StereoDev) * npairs, hipMemcpyHostToDevice, s) != hipSuccess)
         return ORB_E_HIP;
     if (orbgpu::stereo_launch(d_probs, npairs, maxNL, P, s, m)) return ORB_E_HIP;
+    if (dev) {   // device mode may be deferred (ORBmatcher_set_deferred)
+        if (m->d2h_counts(nmatches, d_kept, 4 * (size_t)npairs)) return ORB_E_HIP;
+        return m->end_call() ? ORB_E_HIP : ORB_OK;
+    }
     if (hipMemcpyAsync(nmatches, d_kept, 4 * (size_t)npairs, hipMemcpyDeviceToHost, s) != hipSuccess)
         return ORB_E_HIP;
     if (!dev)
@@ -208,11 +212,12 @@ int Tracking_PrepareLocalSearch_batch_device(ORBmatcher_h h, int count, const or
     if (m->arena_reserve(sizeof(orbgpu::LocalPrepDev) * count + 256)) return ORB_E_HIP;
     void* d = m->arena_alloc(sizeof(orbgpu::LocalPrepDev) * count);
     hipStream_t s = m->stream();
-    if (!d || hipMemcpyAsync(d, P.data(), sizeof(orbgpu::LocalPrepDev) * count, hipMemcpyHostToDevice, s) != hipSuccess)
+    if (!d || hipMemcpyAsync(d, m->h2d_src(P.data(), sizeof(orbgpu::LocalPrepDev) * count),
+                             sizeof(orbgpu::LocalPrepDev) * count, hipMemcpyHostToDevice, s) != hipSuccess)
         return ORB_E_HIP;
     if (orbgpu::local_prep_batch((const orbgpu::LocalPrepDev*)d, count, s)) return ORB_E_HIP;
-    // the staging copy is pageable: finish before the host vector goes away
-    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+    // outside deferred mode the staging copy is pageable: finish before the host vector goes
+    return m->end_call() ? ORB_E_HIP : ORB_OK;
 }
 
 }  // extern "C"

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
+#include <vector>
 
 #define ORB_HIP_CHECK(expr)                                                            \
     do {                                                                               \
@@ -20,6 +22,63 @@
     } while (0)
 
 namespace orbgpu {
+
+// Deferred completion of a chain of batch calls on one stream (bench tracking lane): the host
+// sources of a call's H2D copies and the destinations of its count D2H copies live in pinned
+// blocks that stay untouched until finish(), so a call can return without synchronising and
+// the next call's kernels queue right behind it.  finish() waits for the stream, copies the
+// counts to the callers' arrays and recycles the blocks (same order every chain: no growth).
+class DeferredChain {
+public:
+    ~DeferredChain() {
+        for (auto& b : blocks_) (void)hipHostFree(b.p);
+    }
+    bool on() const { return on_; }
+    void set(bool v) { on_ = v; }
+    // pinned copy of host bytes, valid until finish()
+    void* stage(const void* src, size_t bytes) {
+        void* p = take(bytes);
+        if (p && bytes) std::memcpy(p, src, bytes);
+        return p;
+    }
+    // pinned landing block for a D2H copy whose bytes go to `user` at finish()
+    void* land(void* user, size_t bytes) {
+        void* p = take(bytes);
+        if (p) outs_.push_back(Out{p, user, bytes});
+        return p;
+    }
+    int finish(hipStream_t s) {
+        ORB_HIP_CHECK(hipStreamSynchronize(s));
+        for (auto& o : outs_) std::memcpy(o.user, o.pin, o.bytes);
+        outs_.clear();
+        used_ = 0;
+        return 0;
+    }
+
+private:
+    struct Block {
+        void* p;
+        size_t cap;
+    };
+    struct Out {
+        void* pin;
+        void* user;
+        size_t bytes;
+    };
+    void* take(size_t bytes) {
+        bytes = (bytes + 255) & ~(size_t)255;
+        if (used_ < blocks_.size() && blocks_[used_].cap >= bytes) return blocks_[used_++].p;
+        void* p = nullptr;
+        const size_t cap = bytes < 65536 ? 65536 : bytes;
+        if (hipHostMalloc(&p, cap) != hipSuccess) return nullptr;
+        blocks_.insert(blocks_.begin() + (long)used_, Block{p, cap});
+        return blocks_[used_++].p;
+    }
+    bool on_ = false;
+    std::vector<Block> blocks_;
+    size_t used_ = 0;
+    std::vector<Out> outs_;
+};
 
 constexpr int kEdge = 19;          // EDGE_THRESHOLD, ORBextractor.cc:67
 constexpr int kPatch = 31;         // PATCH_SIZE, ORBextractor.cc:65

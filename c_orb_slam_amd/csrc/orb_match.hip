@@ -748,7 +748,7 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
         probs_cap_ = pb * 2;
         ORB_HIP_CHECK(hipMalloc(&d_probs_, probs_cap_));
     }
-    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, probs.data(), pb, hipMemcpyHostToDevice, stream_));
+    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, h2d_src(probs.data(), pb), pb, hipMemcpyHostToDevice, stream_));
     SearchDev* dp = (SearchDev*)d_probs_;
     if (frustum_ && maxq > 0) {   // SearchLocalPoints: Frame::isInFrustum fills the query arrays first
         mark(8);
@@ -840,7 +840,8 @@ int Matcher::search_local_points(std::vector<SearchDev>& probs, std::vector<Frus
             P.inView = f.inView; P.projX = f.projX; P.projXR = f.projXR; P.projY = f.projY;
             P.level = f.level; P.viewCos = f.viewCos; P.mpIndex = f.mpIndex;
         }
-        ORB_HIP_CHECK(hipMemcpyAsync(base, fr.data(), sizeof(FrustumDev) * np, hipMemcpyHostToDevice, stream_));
+        ORB_HIP_CHECK(hipMemcpyAsync(base, h2d_src(fr.data(), sizeof(FrustumDev) * np), sizeof(FrustumDev) * np,
+                                     hipMemcpyHostToDevice, stream_));
         frustum_ = (const FrustumDev*)base;   // launched by run() once the problems are on the device
         frustumCos_ = viewingCosLimit;
         frustumLsf_ = logScaleFactor;

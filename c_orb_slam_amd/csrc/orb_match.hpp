@@ -104,6 +104,23 @@ public:
     int candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, const int* off, const int* cand, int* dist,
                    int* best_idx, int* best_dist, int* second_dist);
     hipStream_t stream() const { return stream_; }
+    // deferred mode (ORBmatcher_set_deferred): batch device calls return without a stream sync
+    DeferredChain& chain() { return chain_; }
+    // H2D source: the caller's host bytes, or a pinned copy of them in deferred mode
+    const void* h2d_src(const void* host, size_t bytes) { return chain_.on() ? chain_.stage(host, bytes) : host; }
+    // D2H of device counts into `user`; in deferred mode via a pinned block copied at finish()
+    int d2h_counts(void* user, const void* dev, size_t bytes) {
+        void* dst = chain_.on() ? chain_.land(user, bytes) : user;
+        if (!dst) return -2;
+        ORB_HIP_CHECK(hipMemcpyAsync(dst, dev, bytes, hipMemcpyDeviceToHost, stream_));
+        return 0;
+    }
+    // end of a call: sync unless deferred
+    int end_call() {
+        if (chain_.on()) return 0;
+        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        return 0;
+    }
     float nnratio() const { return nnratio_; }
     bool check_ori() const { return checkOri_; }
 
@@ -134,6 +151,7 @@ private:
     bool checkOri_;
     bool device_ptrs_ = false;
     hipStream_t stream_ = nullptr;
+    DeferredChain chain_;
     void* d_scratch_ = nullptr;
     size_t scratch_cap_ = 0;
     void* d_probs_ = nullptr;

@@ -209,11 +209,13 @@ def PoseOptimizationBatchDevice(frames, Tcw_out, outliers):
     return n[:F]
 
 
-def PoseOptimizationFramesDevice(frames, Tcw_out, outliers):
+def PoseOptimizationFramesDevice(frames, Tcw_out, outliers, chain=None, n_out=None):
     """Optimizer::PoseOptimization(Frame*) on device-resident frames as the reference reads them
     (Optimizer.cc:255-347): frames[f] holds torch device tensors Tcw (16 f32), mp (N i32 indices
     into mp_pos, -1 = NULL), mp_pos (M x 3 f32), keysUn (N x 7 words, cv::KeyPoint layout),
-    uRight (N f32), invLevelSigma2 (nlevels f32) and cam (5 floats, host).  -> nInliers[F]."""
+    uRight (N f32), invLevelSigma2 (nlevels f32) and cam (5 floats, host).  -> nInliers[F].
+    chain: an ORBmatcher in deferred mode (ORBmatcher_set_deferred): the call is queued on its
+    stream and n_out (int32 numpy, F) is written by ORBmatcher_finish."""
     from ._lib import pose_frame
     F = len(frames)
     ps = []
@@ -228,6 +230,10 @@ def PoseOptimizationFramesDevice(frames, Tcw_out, outliers):
     probs = (pose_frame * max(F, 1))(*ps)
     tptr = (C.c_void_p * max(F, 1))(*[t.data_ptr() for t in Tcw_out])
     optr = (C.c_void_p * max(F, 1))(*[o.data_ptr() for o in outliers])
+    if chain is not None:
+        check(lib().Optimizer_PoseOptimization_frames_device_deferred(chain._h, F, probs, tptr, optr, ptr(n_out)),
+              "Optimizer_PoseOptimization_frames_device_deferred")
+        return n_out
     n = np.zeros(max(F, 1), np.int32)
     check(lib().Optimizer_PoseOptimization_frames_device(F, probs, tptr, optr, ptr(n)),
           "Optimizer_PoseOptimization_frames_device")

@@ -383,7 +383,7 @@ class ORBmatcher:
         del keep
         return res
 
-    def SearchLocalPoints(self, frames, cur_mps, maps, logScaleFactor, th=1.0):
+    def SearchLocalPoints(self, frames, cur_mps, maps, logScaleFactor, th=1.0, deferred=False):
         """Tracking::SearchLocalPoints (Tracking.cc:1143-1193): isInFrustum(pMP, 0.5) + SearchByProjection(F,
         mvpLocalMapPoints, th) per frame on the device (ORBmatcher_SearchLocalPoints_batch); cur_mps[f] (int32
         numpy, F.N) updated in place.  -> (nmatches, nvisible) arrays."""
@@ -397,10 +397,14 @@ class ORBmatcher:
         nv = np.zeros(max(len(frames), 1), np.int32)
         check(self._L.ORBmatcher_set_device_pointers(self._h, 1))
         try:
+            if deferred:   # queued on the stream; the counts land at finish (set_deferred(0))
+                check(self._L.ORBmatcher_set_deferred(self._h, 1))
             check(self._L.ORBmatcher_SearchLocalPoints_batch(self._h, len(frames), fa, arr, ma, float(logScaleFactor),
                                                              float(th), ptr(nm), ptr(nv)),
                   "ORBmatcher_SearchLocalPoints_batch")
         finally:
+            if deferred:
+                check(self._L.ORBmatcher_set_deferred(self._h, 0))
             check(self._L.ORBmatcher_set_device_pointers(self._h, 0))
         for c, d in zip(cur_mps, cm):
             c[:] = d.cpu().numpy()[:len(c)]

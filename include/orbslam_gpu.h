@@ -125,6 +125,17 @@ void* ORBmatcher_stream(ORBmatcher_h h);
  *                  SearchCandidates pairs, SearchCandidates queries. */
 int ORBmatcher_enable_timing(ORBmatcher_h h, int on);
 int ORBmatcher_last_timings(ORBmatcher_h h, float* ms8, long long* counts8);
+/* Deferred completion (no reference counterpart; the reference's calls are synchronous).
+ * With deferred on (device-pointer matchers only), the device-resident batch calls
+ * ORBmatcher_ComputeStereoMatches_batch, MapPoint_CreateStereo_batch_device,
+ * ORBmatcher_SearchByProjection_LastFrame_batch, Tracking_PrepareLocalSearch_batch_device,
+ * ORBmatcher_SearchLocalPoints_batch and Optimizer_PoseOptimization_frames_device_deferred
+ * return as soon as their work is queued on ORBmatcher_stream(h); their per-problem counts
+ * (nmatches, nvisible, ninliers) are written when ORBmatcher_finish(h) returns.  A chain of
+ * TrackWithMotionModel + TrackLocalMap calls then runs without a host round trip between
+ * the calls.  Turning deferred off finishes a pending chain. */
+int ORBmatcher_set_deferred(ORBmatcher_h h, int on);
+int ORBmatcher_finish(ORBmatcher_h h);
 
 /* static int ORBmatcher::DescriptorDistance(a, b)   ORBmatcher.cc:1647-1663 (host) */
 int ORBmatcher_DescriptorDistance(const uint8_t* a, const uint8_t* b);
@@ -692,6 +703,12 @@ typedef struct pose_frame {
 /* Same outputs and capacity rule as Optimizer_PoseOptimization_batch_device. */
 int Optimizer_PoseOptimization_frames_device(int count, const pose_frame* F, float* const* Tcw_out,
                                              uint8_t* const* outlier, int* ninliers);
+/* The same, queued on the deferred chain of matcher `chain` (ORBmatcher_set_deferred): behind
+ * the chain's earlier calls on ORBmatcher_stream(chain); ninliers[f] is written at
+ * ORBmatcher_finish(chain), -1 for a frame over the edge capacity. */
+int Optimizer_PoseOptimization_frames_device_deferred(ORBmatcher_h chain, int count, const pose_frame* F,
+                                                      float* const* Tcw_out, uint8_t* const* outlier,
+                                                      int* ninliers);
 
 /* ----------------------------------------------------------------------
  * Keyframe-block sharded BA across GPUs: one process (or

@@ -109,3 +109,48 @@ def test_pose_frames_form_equals_packed_and_oracle(gpu, seed):
         o = oracle_lib.oracle_pose_optimization(fr)
         assert int(n_f[f]) == int(o["inliers"])
         assert np.array_equal(Tf[f].cpu().numpy().reshape(4, 4), o["Tcw"])
+
+
+def test_deferred_chain_equals_synchronous(gpu):
+    """ORBmatcher_set_deferred: two PoseOptimization batches queued on the matcher's stream
+    without a host sync in between give the synchronous call's poses, outliers and counts, and
+    the counts land only at ORBmatcher_finish."""
+    import torch
+    from c_orb_slam_amd._lib import check, lib
+    from c_orb_slam_amd.optimizer import PoseOptimizationFramesDevice
+    dev = torch.device("cuda", 0)
+    frames = [pose_problem(700 + s, N=300 + 400 * s) for s in range(3)]
+    framed = []
+    for fr in frames:
+        N = len(fr["has_mp"])
+        octv, tab = _octaves(fr["inv_sigma2"])
+        k = np.zeros(N, oracle_lib.KP_DTYPE)
+        k["x"], k["y"], k["octave"] = fr["obs"][:, 0], fr["obs"][:, 1], octv
+        mp = np.where(fr["has_mp"] > 0, np.arange(N), -1).astype(np.int32)
+        framed.append(dict(Tcw=torch.from_numpy(np.ascontiguousarray(fr["Tcw"], np.float32).reshape(16)).to(dev),
+                           mp=torch.from_numpy(mp).to(dev), mp_pos=torch.from_numpy(fr["Xw"]).to(dev),
+                           keysUn=torch.from_numpy(k.view(np.int32).reshape(N, 7).copy()).to(dev),
+                           uRight=torch.from_numpy(np.ascontiguousarray(fr["obs"][:, 2])).to(dev),
+                           invLevelSigma2=torch.from_numpy(tab).to(dev), cam=fr["cam"]))
+    mk = lambda fill: [torch.full((len(f["has_mp"]),), fill, dtype=torch.uint8, device=dev) for f in frames]
+    T0 = [torch.zeros(16, dtype=torch.float32, device=dev) for _ in frames]
+    o0 = mk(9)
+    n0 = PoseOptimizationFramesDevice(framed, T0, o0)
+    m = gpu.ORBmatcher(0.8, False)
+    L = lib()
+    check(L.ORBmatcher_set_device_pointers(m._h, 1))
+    T1 = [torch.zeros(16, dtype=torch.float32, device=dev) for _ in frames]
+    T2 = [torch.zeros(16, dtype=torch.float32, device=dev) for _ in frames]
+    o1, o2 = mk(9), mk(9)   # entries of keypoints without a map point keep the caller's value
+    n1, n2 = np.full(3, -9, np.int32), np.full(3, -9, np.int32)
+    check(L.ORBmatcher_set_deferred(m._h, 1))
+    PoseOptimizationFramesDevice(framed, T1, o1, chain=m, n_out=n1)
+    PoseOptimizationFramesDevice(framed, T2, o2, chain=m, n_out=n2)
+    assert (n1 == -9).all() and (n2 == -9).all()      # nothing lands before finish
+    check(L.ORBmatcher_finish(m._h))
+    check(L.ORBmatcher_set_deferred(m._h, 0))
+    for n, T, o in ((n1, T1, o1), (n2, T2, o2)):
+        assert np.array_equal(n, n0)
+        for f in range(3):
+            assert np.array_equal(T[f].cpu().numpy(), T0[f].cpu().numpy())
+            assert np.array_equal(o[f].cpu().numpy(), o0[f].cpu().numpy())

@@ -120,6 +120,10 @@ def test_search_local_points_matches_oracle(gpu, seq, th):
     m = gpu.ORBmatcher(0.8, False)
     g = [c.copy() for c in cms]
     nm, nv = m.SearchLocalPoints(frames, g, maps, lsf, th)
+    gd = [c.copy() for c in cms]   # the deferred chain form gives the same matches and counts
+    nmd, nvd = m.SearchLocalPoints(frames, gd, maps, lsf, th, deferred=True)
+    assert np.array_equal(nm, nmd) and np.array_equal(nv, nvd)
+    assert all(np.array_equal(a, b) for a, b in zip(g, gd))
     for F, M, c0, gc, n1, n2 in zip(frames, maps, cms, g, nm, nv):
         oc = c0.copy()
         no, nvo = oracle_lib.oracle_search_local_points(F, oc, M, lsf, th, 0.8)
