@@ -12,6 +12,11 @@ trace, bench = sys.argv[1], json.loads(open(sys.argv[2]).read().strip().splitlin
 roof = bench["roofline"]
 k, reps = roof["kernel"], roof.get("launches", 5)
 rows = sorted((r for r in csv.DictReader(open(trace)) if k in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
+# the roofline pass runs full batches; later legs (the batch-1 latency leg) launch the same kernel
+# on one image: keep the full-batch launches only
+gsz = lambda r: int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+gmax = max(gsz(r) for r in rows)
+rows = [r for r in rows if gsz(r) == gmax]
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
 iso = d[-reps:]
 pipe = d[:-reps]
