@@ -1366,7 +1366,11 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
     __shared__ uint16_t aE[kPoseMaxEdges];
     __shared__ double cs[28][kPoseMaxEdges / 64];
     __shared__ double red[32];
-    __shared__ Se3 T, Tbak, Terr;
+    // speculative solves for 1..kPoseSpec consecutive rejections of a trial (waves 1..kPoseSpec)
+    constexpr int kPoseSpec = 3;
+    __shared__ Se3 T, Tbak, Terr, Tbase, Tspec[kPoseSpec];
+    __shared__ double xspec[kPoseSpec][6];
+    __shared__ int specOk[kPoseSpec], specNext, specReady;
     __shared__ double xs[6], Hs[21], bs[6];
     __shared__ double lambda, ni, currentChi, iniChi;
     __shared__ int nA, nBadLM, qmax, again, term, nBad, okS, wsum[16];
@@ -1508,11 +1512,28 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                         nBadLM = 0;
                     }
                     qmax = 0;
+                    Tbase = T;   // the estimate every trial of this iteration starts from
+                    specReady = 0;
+                    specNext = kPoseSpec;
                 }
                 __syncthreads();
                 do {
                     ORBGPU_PROF_MARK(10);
-                    if (tid < 64) {   // wave 0: lane-parallel divisions in the solve
+                    if (specReady) {
+                        // the previous trial was rejected (lambda *= ni, estimate restored) and a
+                        // speculating wave already solved that system: the identical operations,
+                        // done while the earlier trial's solve ran
+                        if (tid == 0) {
+                            const int L = specNext;
+                            Tbak = T;
+#pragma unroll
+                            for (int j = 0; j < 6; j++) xs[j] = xspec[L][j];
+                            okS = 1;
+                            T = Tspec[L];
+                            Terr = Tspec[L];
+                            specNext = L + 1;
+                        }
+                    } else if (tid < 64) {   // wave 0: lane-parallel divisions in the solve
                         double xn[6];
                         const bool ok2 = pose_solve_w(Hs, bs, lambda, xn);
                         double xl[6];
@@ -1523,7 +1544,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                         Se3 d, r;
                         se3_exp(xl, d);
                         ORBGPU_PROF_MARK(6);
-                        se3_mul(d, T, r);
+                        se3_mul(d, Tbase, r);
                         ORBGPU_PROF_MARK(7);
                         if (tid == 0) {
                             Tbak = T;
@@ -1533,6 +1554,30 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                             T = r;
                             Terr = r;   // the pose of the last computeActiveErrors
                         }
+                    } else if (tid < 64 * (kPoseSpec + 1)) {
+                        // waves 1..kPoseSpec, concurrently: the solves L+1 consecutive rejections
+                        // of this trial would need (lambda *= ni; ni *= 2 repeated, the same H, b
+                        // and starting estimate)
+                        const int L = (tid >> 6) - 1;
+                        double ls = lambda, ns = ni;
+                        for (int j = 0; j <= L; j++) {
+                            ls *= ns;
+                            ns *= 2;
+                        }
+                        double xn[6];
+                        const bool ok = pose_solve_w(Hs, bs, ls, xn);
+                        if (ok) {
+                            Se3 d, r;
+                            se3_exp(xn, d);
+                            se3_mul(d, Tbase, r);
+                            if ((tid & 63) == 0) {
+                                Tspec[L] = r;
+#pragma unroll
+                                for (int j = 0; j < 6; j++) xspec[L][j] = xn[j];
+                            }
+                        }
+                        if ((tid & 63) == 0) specOk[L] = ok ? 1 : 0;
+                        if (tid == 64) specNext = 0;
                     }
                     __syncthreads();
                     ORBGPU_PROF_MARK(2);
@@ -1562,6 +1607,7 @@ __global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, c
                         }
                         qmax++;
                         again = (rho < 0 && qmax < 10) ? 1 : 0;
+                        specReady = again && specNext < kPoseSpec && specOk[specNext] ? 1 : 0;
                         if (!again) {
                             if (qmax == 10 || rho == 0) {
                                 term = 1;
