@@ -859,7 +859,10 @@ def bench_global_ba(args, world, rank, dist, dev):
             "dtype": "f64 (f32 I/O)"}
 
 
-LOCAL_BA_STREAMS = 16   # concurrent LocalBundleAdjustment streams of the local-BA throughput figure
+# concurrent LocalBundleAdjustment streams of the local-BA throughput figure (ORBGPU_LBA_STREAMS
+# overrides: rocprofv3 7.0's kernel-trace callbacks have crashed twice inside a memcpy under 16
+# host threads launching at once, never without the profiler; profile runs use 1)
+LOCAL_BA_STREAMS = int(os.environ.get("ORBGPU_LBA_STREAMS", "16"))
 RANSAC_PROBLEMS, RANSAC_HYP = 100, 300
 PNP_BYTES_PER_PAIR = 24   # p3d 12 B + p2d 8 B + maxErr 4 B read per (hypothesis, correspondence)
 SIM3_BYTES_PER_PAIR = 48  # X1, X2 24 B + p1, p2 16 B + two maxErr 8 B

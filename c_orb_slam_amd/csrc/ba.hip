@@ -1948,7 +1948,37 @@ BaEngine::~BaEngine() {
     if (arena_) (void)hipFree(arena_);
     if (dStruct_) (void)hipFree(dStruct_);
     if (hScal_) (void)hipHostFree(hScal_);
+    if (hStage_) (void)hipHostFree(hStage_);
     if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+int BaEngine::stage_reserve(size_t bytes) {
+    if (bytes <= hStageCap_) return 0;
+    if (hStage_) (void)hipHostFree(hStage_);
+    hStage_ = nullptr;
+    hStageCap_ = 0;
+    ORB_HIP_CHECK(hipHostMalloc(&hStage_, bytes));
+    hStageCap_ = bytes;
+    return 0;
+}
+
+// H2D / D2H copies of host bytes through the engine's pinned staging block, complete on return
+int BaEngine::h2d_sync(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return 0;
+    if (int e = stage_reserve(bytes)) return e;
+    std::memcpy(hStage_, src, bytes);
+    ORB_HIP_CHECK(hipMemcpyAsync(dst, hStage_, bytes, hipMemcpyHostToDevice, stream_));
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    return 0;
+}
+
+int BaEngine::d2h_sync(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return 0;
+    if (int e = stage_reserve(bytes)) return e;
+    ORB_HIP_CHECK(hipMemcpyAsync(hStage_, src, bytes, hipMemcpyDeviceToHost, stream_));
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    std::memcpy(dst, hStage_, bytes);
+    return 0;
 }
 
 int BaEngine::init() {
@@ -2067,10 +2097,10 @@ int BaEngine::upload_problem(const ba_problem* P) {
     }
     level_.assign(ne_, 0);
     hipStream_t s = stream_;
-    if (nkf_) ORB_HIP_CHECK(hipMemcpyAsync(dT_, T.data(), sizeof(Se3) * nkf_, hipMemcpyHostToDevice, s));
-    if (npt_) ORB_HIP_CHECK(hipMemcpyAsync(dX_, X.data(), sizeof(double) * X.size(), hipMemcpyHostToDevice, s));
+    if (nkf_ && h2d_sync(dT_, T.data(), sizeof(Se3) * nkf_)) return -2;
+    if (npt_ && h2d_sync(dX_, X.data(), sizeof(double) * X.size())) return -2;
     if (ne_) {
-        ORB_HIP_CHECK(hipMemcpyAsync(dE_, E.data(), sizeof(EdgeDev) * ne_, hipMemcpyHostToDevice, s));
+        if (h2d_sync(dE_, E.data(), sizeof(EdgeDev) * ne_)) return -2;
         ORB_HIP_CHECK(hipMemsetAsync(dLevel_, 0, ne_, s));
         ORB_HIP_CHECK(hipMemsetAsync(dRobust_, (mode_.global && !mode_.robust) ? 0 : 1, ne_, s));
         ORB_HIP_CHECK(hipMemsetAsync(dErr_, 0, sizeof(double) * 3 * ne_, s));
@@ -2100,9 +2130,9 @@ int BaEngine::build_structure(int level) {
         for (int k = 0; k < nkf_; k++) red[k] = kfAct[k];
         red[nkf_] = (double)aE.size();
         red[nkf_ + 1] = (double)nLloc;
-        ORB_HIP_CHECK(hipMemcpyAsync(dScratch_, red.data(), sizeof(double) * red.size(), hipMemcpyHostToDevice, stream_));
+        if (h2d_sync(dScratch_, red.data(), sizeof(double) * red.size())) return -2;
         if (int e = comm_->allreduce(dScratch_, red.size(), RedOp::Sum, stream_)) return e;
-        ORB_HIP_CHECK(hipMemcpyAsync(red.data(), dScratch_, sizeof(double) * red.size(), hipMemcpyDeviceToHost, stream_));
+        if (d2h_sync(red.data(), dScratch_, sizeof(double) * red.size())) return -2;
         ORB_HIP_CHECK(hipStreamSynchronize(stream_));
         for (int k = 0; k < nkf_; k++) kfAct[k] = red[k] > 0 ? 1 : 0;
         nEglob_ = (int)red[nkf_];
@@ -2223,7 +2253,7 @@ int BaEngine::build_structure(int level) {
         ORB_HIP_CHECK(hipMalloc(&dStruct_, tot * 4 * 2));
         dStructCap_ = tot * 4 * 2;
     }
-    ORB_HIP_CHECK(hipMemcpyAsync(dStruct_, hStruct_.data(), tot * 4, hipMemcpyHostToDevice, stream_));
+    if (h2d_sync(dStruct_, hStruct_.data(), tot * 4)) return -2;
     const int32_t* d = dStruct_;
     st_.nE = nE; st_.nP = nP; st_.nL = nL; st_.nBlk = nBlk;
     st_.aE = d + off[0]; st_.ePose = d + off[1]; st_.eLand = d + off[2]; st_.poseKf = d + off[3];
@@ -2244,9 +2274,9 @@ int BaEngine::build_structure(int level) {
         }
         if (comm_) {
             if (tm.size() > scratchN_) return -3;
-            ORB_HIP_CHECK(hipMemcpyAsync(dScratch_, tm.data(), sizeof(double) * tm.size(), hipMemcpyHostToDevice, stream_));
+            if (h2d_sync(dScratch_, tm.data(), sizeof(double) * tm.size())) return -2;
             if (int e = comm_->allreduce(dScratch_, tm.size(), RedOp::Max, stream_)) return e;
-            ORB_HIP_CHECK(hipMemcpyAsync(tm.data(), dScratch_, sizeof(double) * tm.size(), hipMemcpyDeviceToHost, stream_));
+            if (d2h_sync(tm.data(), dScratch_, sizeof(double) * tm.size())) return -2;
             ORB_HIP_CHECK(hipStreamSynchronize(stream_));
         }
         if (tiled_) {
@@ -2270,7 +2300,7 @@ int BaEngine::build_structure(int level) {
             }
             dTiles_ = (int2*)dPack_;
             dPackBuf_ = (double*)((char*)dPack_ + ((sizeof(int2) * tl.size() + 255) & ~(size_t)255));
-            ORB_HIP_CHECK(hipMemcpyAsync(dTiles_, tl.data(), sizeof(int2) * tl.size(), hipMemcpyHostToDevice, stream_));
+            if (h2d_sync(dTiles_, tl.data(), sizeof(int2) * tl.size())) return -2;
             ORB_HIP_CHECK(hipStreamSynchronize(stream_));
         }
     }
@@ -2469,9 +2499,7 @@ int BaEngine::gate_edges(int final_check, uint8_t* erase) {
     hipLaunchKernelGGL(k_gate, dim3(nblk(ne_, 256)), dim3(256), 0, stream_, ne_, dE_, dT_, dX_, dErr_, dFlag, dLevel_,
                        dRobust_, final_check ? 0 : 1);
     ORB_HIP_CHECK(hipGetLastError());
-    ORB_HIP_CHECK(hipMemcpyAsync(erase, dFlag, ne_, hipMemcpyDeviceToHost, stream_));
-    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
-    return 0;
+    return d2h_sync(erase, dFlag, ne_);
 }
 
 int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, Comm* comm, const BaMode* mode) {
@@ -2529,9 +2557,8 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
     }
     std::vector<Se3> T(nkf_);
     std::vector<double> X(3 * (size_t)npt_);
-    if (nkf_) ORB_HIP_CHECK(hipMemcpyAsync(T.data(), dT_, sizeof(Se3) * nkf_, hipMemcpyDeviceToHost, stream_));
-    if (npt_) ORB_HIP_CHECK(hipMemcpyAsync(X.data(), dX_, sizeof(double) * X.size(), hipMemcpyDeviceToHost, stream_));
-    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (nkf_ && d2h_sync(T.data(), dT_, sizeof(Se3) * nkf_)) return -2;
+    if (npt_ && d2h_sync(X.data(), dX_, sizeof(double) * X.size())) return -2;
     for (int k = 0; k < nkf_; k++)
         if (kfLocal_[k]) host_se3_to_Tcw(T[k], R->kf_Tcw + 16 * k);
     // BundleAdjustment writes back only the points that got a vertex (vbNotIncludedMP, Optimizer.cc:217-219);

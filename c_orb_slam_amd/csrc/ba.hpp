@@ -114,6 +114,13 @@ private:
     void* arena_ = nullptr;
     size_t arenaCap_ = 0;
     double* hScal_ = nullptr;      // pinned
+    // pinned staging of the setup uploads (problem arrays, structure): several engines set up
+    // concurrently from different host threads, so no pageable hipMemcpy staging path is used
+    void* hStage_ = nullptr;
+    size_t hStageCap_ = 0;
+    int h2d_sync(void* dst, const void* src, size_t bytes);
+    int d2h_sync(void* dst, const void* src, size_t bytes);
+    int stage_reserve(size_t bytes);
     size_t scratchN_ = 0;
     size_t ldsMax_ = 0;
     // sharding

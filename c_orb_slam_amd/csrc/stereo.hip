@@ -340,8 +340,9 @@ __global__ void __launch_bounds__(256) k_unproject(UnprojBatch B) {
 // Tracking.cc:893-913 (TrackWithMotionModel discards the outliers of its PoseOptimization and
 // marks their points seen) + 1146-1161 (SearchLocalPoints skips the points already in the
 // frame): skip[j] = no map point in local-map row j, or row j in mvpMapPoints; then the outlier
-// rows of mvpMapPoints are cleared.  One workgroup per frame (the two phases are ordered).
-__global__ void __launch_bounds__(1024) k_local_prep(const LocalPrepDev* __restrict__ probs) {
+// rows of mvpMapPoints are cleared.  One workgroup per frame (the two phases are ordered); 4
+// waves, so it finds a slot beside the extraction lane's workgroups.
+__global__ void __launch_bounds__(256) k_local_prep(const LocalPrepDev* __restrict__ probs) {
     ORBGPU_LATENCY_WAVE();
     const LocalPrepDev& P = probs[blockIdx.x];
     for (int j = threadIdx.x; j < P.n; j += blockDim.x) P.skip[j] = P.row[j] < 0 ? 1 : 0;
@@ -357,7 +358,7 @@ __global__ void __launch_bounds__(1024) k_local_prep(const LocalPrepDev* __restr
 
 int local_prep_batch(const LocalPrepDev* d_probs, int count, hipStream_t s) {
     if (count <= 0) return 0;
-    hipLaunchKernelGGL(k_local_prep, dim3(count), dim3(1024), 0, s, d_probs);
+    hipLaunchKernelGGL(k_local_prep, dim3(count), dim3(256), 0, s, d_probs);
     ORB_HIP_CHECK(hipGetLastError());
     return 0;
 }
