@@ -1108,7 +1108,7 @@ __device__ __forceinline__ double pose_rho0(const PoseEdgeD& e, double c, bool r
 
 
 constexpr int kPoseMaxEdges = 8192;
-constexpr int kPoseThreads = 512;   // 256 VGPRs per lane for the fused 28-term pass
+constexpr int kPoseThreads = 256;   // one wave per SIMD: the workgroup fits beside the extraction grids
 constexpr int kPosePer = kPoseMaxEdges / kPoseThreads;
 
 // Canonical totals (ora_csum level 2) of the m chunk trees cs[q][0..m) of K sums, by wave 0:
