@@ -1028,11 +1028,9 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     }
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
-    // 2. blur (independent of keypoints; overlaps nothing yet, kept on the stream)
-    hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
-                       (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_, (int)tiles_.size());
-    ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
-    // 3. FAST per cell
+    // 2. FAST per cell (the blur, which only the descriptors read, runs after the octree: the
+    //    VALU-heavy FAST grid then overlaps the tracking lane's matching, and the HBM-bound
+    //    blur its FP64 PoseOptimization)
     const int ncells = (int)cells_.size();
     if (work_B_ != B && build_work(B)) return -2;
     hipLaunchKernelGGL(k_fast_cells, dim3(work_n_), dim3(256), 0, s, (const uint8_t*)d_pyr_, img_bytes_,
@@ -1040,14 +1038,14 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
                        (int*)d_counts_, ncells, (const int*)d_work_);
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[3], s));
-    // 4. compaction
+    // 3. compaction
     ORB_HIP_CHECK(hipMemsetAsync(d_gtotal_, 0, 4, s));
     hipLaunchKernelGGL(k_compact, dim3(B), dim3(1024), 0, s, (const uint32_t*)d_slots_, slots_per_image_,
                        (const int*)d_counts_, (const CellDesc*)d_cells_, ncells, (const int*)d_lcb_, nlevels_,
                        (uint32_t*)d_packed_, (int*)d_hdr_, d_gtotal_, packed_cap_);
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[4], s));
-    // 5. DistributeOctTree per (image, level) + per-image selected lists, on the device
+    // 4. DistributeOctTree per (image, level) + per-image selected lists, on the device
     int* d_err = (int*)d_nout_ + B;
     ORB_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
     if (int e = octree_launch((const uint32_t*)d_packed_, (const int*)d_hdr_, B, nlevels_,
@@ -1056,6 +1054,10 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
                               d_err, s))
         return e;
     ORB_HIP_CHECK(hipEventRecord(ev_[5], s));
+    // 5. blur: GaussianBlur of every level (ORBextractor.cc:1085-1086)
+    hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
+                       (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_, (int)tiles_.size());
+    ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
     // 6. orientation + descriptors
     orb_kp_dev* okps = (orb_kp_dev*)kps;
     uint8_t* odesc = desc;
@@ -1125,12 +1127,13 @@ int debug_prof_extract(unsigned long long* out32) {
 
 int Extractor::timings(float* ms6) {
     float t[6] = {0};
+    // launch order: pyramid [0,1] fast [1,3] compact [3,4] octree [4,5] blur [5,2] orient [2,6]
     (void)hipEventElapsedTime(&t[0], ev_[0], ev_[1]);
-    (void)hipEventElapsedTime(&t[1], ev_[1], ev_[2]);
-    (void)hipEventElapsedTime(&t[2], ev_[2], ev_[3]);
+    (void)hipEventElapsedTime(&t[1], ev_[5], ev_[2]);
+    (void)hipEventElapsedTime(&t[2], ev_[1], ev_[3]);
     (void)hipEventElapsedTime(&t[3], ev_[3], ev_[4]);
     (void)hipEventElapsedTime(&t[4], ev_[4], ev_[5]);
-    (void)hipEventElapsedTime(&t[5], ev_[5], ev_[6]);
+    (void)hipEventElapsedTime(&t[5], ev_[2], ev_[6]);
     for (int i = 0; i < 6; i++) ms6[i] = t[i];
     return 0;
 }
