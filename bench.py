@@ -282,6 +282,8 @@ def main():
             self.nml = np.zeros(P, np.int32)
             self.nvis = np.zeros(P, np.int32)
             self.nst = np.zeros(B, np.int32)
+            self.epoch = 0        # the deferred-chain epoch of this lane's last tracking chain
+            self.kp_count = 0
             self.nL = self.nR = None
             self.kidx = torch.arange(cap, dtype=torch.int32, device=dev)
 
@@ -301,7 +303,11 @@ def main():
 
         def extract(self):
             # Frame(imLeft, imRight): two ORBextractor calls (Frame.cc:78-81) on two host threads and
-            # two HIP streams, like the reference's two extractor threads per stereo frame
+            # two HIP streams, like the reference's two extractor threads per stereo frame.  The
+            # lane's buffers may still be read by the tracking chain of its previous batch: wait
+            # for that chain's device work first (not for its counts)
+            if self.epoch:
+                check(L.ORBmatcher_chain_wait(m._h, self.epoch), "ORBmatcher_chain_wait")
             fR = pool.submit(self.exR.extract_device, d_R.data_ptr(), B, W, H, W, W * H, self.d_kpsR.data_ptr(),
                              self.d_descR.data_ptr(), cap)
             self.nL = np.ascontiguousarray(self.exL.extract_device(d_L.data_ptr(), B, W, H, W, W * H,
@@ -353,13 +359,15 @@ def main():
                                                                       self.a_poutl2, ptr(self.ninl2)),
                   "PoseOptimization (local map)")
 
-        def track(self):
+        def enqueue(self):
             """ComputeStereoMatches, UpdateLastFrame, SearchByProjection(Cur, Last, 7), PoseOptimization,
             TrackLocalMap (SearchLocalPoints, PoseOptimization): one deferred chain on the matcher's
-            stream (ORBmatcher_set_deferred), every call queued behind the previous one without a
-            host round trip, the per-frame counts written by ORBmatcher_finish."""
+            stream (ORBmatcher_set_deferred), every call queued behind the previous one -- and the
+            whole chain behind the previous batch's -- without a host round trip; the chain is
+            closed into an epoch whose counts collect() writes."""
             t1 = time.perf_counter()
             nL, nR = self.nL, self.nR
+            self.kp_count = int(nL.sum() + nR.sum())
             check(L.ORBmatcher_set_deferred(m._h, 1), "ORBmatcher_set_deferred")
             self.stereo()
             t2 = time.perf_counter()
@@ -372,11 +380,17 @@ def main():
             t4 = time.perf_counter()
             self.local_map()
             t5 = time.perf_counter()
-            check(L.ORBmatcher_set_deferred(m._h, 0), "ORBmatcher_set_deferred")   # finish: counts land
-            t6 = time.perf_counter()
-            for k, v in (("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3), ("local_map", t5 - t4),
-                         ("finish", t6 - t5)):
+            eid = C.c_longlong(0)
+            check(L.ORBmatcher_chain_close(m._h, C.byref(eid)), "ORBmatcher_chain_close")
+            self.epoch = eid.value
+            for k, v in (("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3), ("local_map", t5 - t4)):
                 phase_acc[k] = phase_acc.get(k, 0.0) + v * 1e3
+
+        def collect(self):
+            """Finish this lane's chain (counts land) and book its statistics."""
+            t5 = time.perf_counter()
+            check(L.ORBmatcher_chain_finish(m._h, self.epoch), "ORBmatcher_chain_finish")
+            phase_acc["finish"] = phase_acc.get("finish", 0.0) + (time.perf_counter() - t5) * 1e3
             tl, tr = self.exL.last_timings(), self.exR.last_timings()
             for k in tl:
                 stage_acc[k] = stage_acc.get(k, 0.0) + tl[k] + tr[k]
@@ -384,7 +398,7 @@ def main():
             kernel_ms.append(tr["fast_cells"])
             pose_inl.append(int(self.ninl2.sum()))
             local_acc.append((int(self.nml.sum()), int(self.nvis.sum())))
-            return int(nL.sum() + nR.sum()), int(self.nm.sum() + self.nml.sum()), int(self.nst.sum())
+            return self.kp_count, int(self.nm.sum() + self.nml.sum()), int(self.nst.sum())
 
     def latency_leg(nf):
         """Per-frame tracking latency, the reference's own figure (wall time of one TrackStereo,
@@ -591,17 +605,22 @@ def main():
             for ex in (ln.exL, ln.exR):
                 check(L.ORBextractor_reserve_cus(ex._h, args.reserve_cus), "ORBextractor_reserve_cus")
     ex_pool = ThreadPoolExecutor(1, initializer=lambda: torch.cuda.set_device(dev))
-    state = {"k": 0, "ready": None}
+    state = {"k": 0, "ready": None, "pending": None}
 
     def step():
         """Software pipeline over two lanes: the extraction of batch k (worker threads, extractor
-        streams) runs while batch k-1 is tracked on this thread (matcher / pose / torch streams)."""
+        streams) runs while batch k-1's tracking chain is queued on the matcher stream right
+        behind batch k-2's; batch k-2's counts are collected while k-1's chain runs.  -> the
+        collected batch's counts (None before the pipeline is full)."""
         lane = lanes[state["k"] % 2]
         te = time.perf_counter()
         fut = ex_pool.submit(lane.extract)
-        res = (0, 0, 0)
+        res = None
         if state["ready"] is not None:
-            res = state["ready"].track()
+            state["ready"].enqueue()
+            if state["pending"] is not None:
+                res = state["pending"].collect()
+            state["pending"] = state["ready"]
         fut.result()
         phase_acc["step_wall"] = phase_acc.get("step_wall", 0.0) + (time.perf_counter() - te) * 1e3
         state["ready"] = lane
@@ -609,9 +628,19 @@ def main():
         return res
 
     def drain():
+        """Track the extracted batch, collect every chain in order, leave the matcher synchronous."""
+        out = []
         if state["ready"] is not None:
-            state["ready"].track()
+            state["ready"].enqueue()
+            if state["pending"] is not None:
+                out.append(state["pending"].collect())
+            state["pending"] = state["ready"]
             state["ready"] = None
+        if state["pending"] is not None:
+            out.append(state["pending"].collect())
+            state["pending"] = None
+        check(L.ORBmatcher_set_deferred(m._h, 0), "ORBmatcher_set_deferred")
+        return out
 
     if args.passes_only:   # one extracted, tracked batch; then only the isolated passes below
         args.warmup, args.steps = 1, 0
@@ -628,12 +657,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tot_kp = tot_match = tot_stereo = 0
+    got = []
     for _ in range(args.steps):
-        a, b, c = step()
-        tot_kp += a
-        tot_match += b
-        tot_stereo += c
+        r = step()
+        if r is not None:
+            got.append(r)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -642,7 +670,12 @@ def main():
         buf = (C.c_ulonglong * 32)()
         L.orbgpu_debug_prof_match(buf)
         print("k_select sections (cycles, problem 0, summed over the timed steps):", list(buf)[:8], file=sys.stderr)
-    drain()   # the batch extracted by the last timed step (outside the timed region)
+    # the last timed chain's counts (its device work finished inside the timed region), then the
+    # batch extracted by the last timed step, tracked outside it
+    got += drain()[:1] if args.steps else []
+    tot_kp = sum(r[0] for r in got)
+    tot_match = sum(r[1] for r in got)
+    tot_stereo = sum(r[2] for r in got)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

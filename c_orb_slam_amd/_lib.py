@@ -109,6 +109,9 @@ def lib():
     L.ORBmatcher_create.argtypes = [f32, i32, P(vp)]
     L.ORBmatcher_set_deferred.argtypes = [vp, i32]
     L.ORBmatcher_finish.argtypes = [vp]
+    L.ORBmatcher_chain_close.argtypes = [vp, P(C.c_longlong)]
+    L.ORBmatcher_chain_wait.argtypes = [vp, C.c_longlong]
+    L.ORBmatcher_chain_finish.argtypes = [vp, C.c_longlong]
     L.Optimizer_PoseOptimization_frames_device_deferred.argtypes = [vp, i32, vp, vp, vp, vp]
     L.ORBmatcher_destroy.argtypes = [vp]
     L.ORBmatcher_set_device_pointers.argtypes = [vp, i32]

@@ -113,6 +113,21 @@ int ORBmatcher_finish(ORBmatcher_h h) {
     return h->m->chain().finish(h->m->stream()) ? ORB_E_HIP : ORB_OK;
 }
 
+int ORBmatcher_chain_close(ORBmatcher_h h, long long* epoch) {
+    if (!h || !epoch || !h->m->chain().on()) return ORB_E_INVALID;
+    return h->m->chain().close(h->m->stream(), epoch) ? ORB_E_HIP : ORB_OK;
+}
+
+int ORBmatcher_chain_wait(ORBmatcher_h h, long long epoch) {
+    if (!h) return ORB_E_INVALID;
+    return h->m->chain().wait(epoch) ? ORB_E_HIP : ORB_OK;
+}
+
+int ORBmatcher_chain_finish(ORBmatcher_h h, long long epoch) {
+    if (!h) return ORB_E_INVALID;
+    return h->m->chain().finish_upto(epoch) ? ORB_E_HIP : ORB_OK;
+}
+
 int ORBmatcher_last_timings(ORBmatcher_h h, float* ms8, long long* counts8) {
     if (!h || !ms8 || !counts8) return ORB_E_INVALID;
     return h->m->timings(ms8, counts8) ? ORB_E_HIP : ORB_OK;

@@ -9,6 +9,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <vector>
 
 #define ORB_HIP_CHECK(expr)                                                            \
@@ -25,59 +27,123 @@ namespace orbgpu {
 
 // Deferred completion of a chain of batch calls on one stream (bench tracking lane): the host
 // sources of a call's H2D copies and the destinations of its count D2H copies live in pinned
-// blocks that stay untouched until finish(), so a call can return without synchronising and
-// the next call's kernels queue right behind it.  finish() waits for the stream, copies the
-// counts to the callers' arrays and recycles the blocks (same order every chain: no growth).
+// blocks that stay untouched until the chain is finished, so a call can return without
+// synchronising and the next call's kernels queue right behind it.  A chain is closed into an
+// epoch (an event on the stream); epochs finish in order -- wait for the event, copy the counts
+// to the callers' arrays, release the blocks -- so the next chain can be queued while an older
+// one still runs.  wait() (event only) may be called from another host thread.
 class DeferredChain {
 public:
     ~DeferredChain() {
         for (auto& b : blocks_) (void)hipHostFree(b.p);
+        for (auto& e : events_)
+            if (e) (void)hipEventDestroy(e);
     }
     bool on() const { return on_; }
     void set(bool v) { on_ = v; }
-    // pinned copy of host bytes, valid until finish()
+    // pinned copy of host bytes, valid until the current chain finishes
     void* stage(const void* src, size_t bytes) {
         void* p = take(bytes);
         if (p && bytes) std::memcpy(p, src, bytes);
         return p;
     }
-    // pinned landing block for a D2H copy whose bytes go to `user` at finish()
+    // pinned landing block for a D2H copy whose bytes go to `user` when the chain finishes
     void* land(void* user, size_t bytes) {
         void* p = take(bytes);
-        if (p) outs_.push_back(Out{p, user, bytes});
+        if (p) cur_outs_.push_back(Out{p, user, bytes});
         return p;
     }
-    int finish(hipStream_t s) {
-        ORB_HIP_CHECK(hipStreamSynchronize(s));
-        for (auto& o : outs_) std::memcpy(o.user, o.pin, o.bytes);
-        outs_.clear();
-        used_ = 0;
+    // close the current chain: record its end on `s`; *id = its epoch
+    int close(hipStream_t s, long long* id) {
+        std::lock_guard<std::mutex> g(mu_);
+        const long long e = next_id_++;
+        hipEvent_t& ev = events_[e % kEvents];
+        if (!ev) ORB_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        ORB_HIP_CHECK(hipEventRecord(ev, s));
+        closed_.push_back(Epoch{e, std::move(cur_blocks_), std::move(cur_outs_)});
+        cur_blocks_.clear();
+        cur_outs_.clear();
+        if (id) *id = e;
         return 0;
+    }
+    // host wait for epoch `id` to complete on the device (no landing); any thread
+    int wait(long long id) {
+        hipEvent_t ev = nullptr;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (id <= done_id_ || id >= next_id_) return 0;
+            ev = events_[id % kEvents];   // re-recorded only kEvents epochs later: never earlier
+        }
+        ORB_HIP_CHECK(hipEventSynchronize(ev));
+        return 0;
+    }
+    // finish every closed epoch up to `id`, in order
+    int finish_upto(long long id) {
+        for (;;) {
+            Epoch ep;
+            hipEvent_t ev;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (closed_.empty() || closed_.front().id > id) return 0;
+                ep = std::move(closed_.front());
+                closed_.pop_front();
+                ev = events_[ep.id % kEvents];
+            }
+            ORB_HIP_CHECK(hipEventSynchronize(ev));
+            for (auto& o : ep.outs) std::memcpy(o.user, o.pin, o.bytes);
+            std::lock_guard<std::mutex> g(mu_);
+            for (int k : ep.blocks) blocks_[k].busy = false;
+            done_id_ = ep.id;
+        }
+    }
+    // close the current chain and finish everything
+    int finish(hipStream_t s) {
+        long long id = 0;
+        if (int e = close(s, &id)) return e;
+        return finish_upto(id);
     }
 
 private:
+    static constexpr int kEvents = 16;
     struct Block {
         void* p;
         size_t cap;
+        bool busy;
     };
     struct Out {
         void* pin;
         void* user;
         size_t bytes;
     };
+    struct Epoch {
+        long long id;
+        std::vector<int> blocks;
+        std::vector<Out> outs;
+    };
     void* take(size_t bytes) {
         bytes = (bytes + 255) & ~(size_t)255;
-        if (used_ < blocks_.size() && blocks_[used_].cap >= bytes) return blocks_[used_++].p;
+        std::lock_guard<std::mutex> g(mu_);
+        for (size_t k = 0; k < blocks_.size(); k++)
+            if (!blocks_[k].busy && blocks_[k].cap >= bytes) {
+                blocks_[k].busy = true;
+                cur_blocks_.push_back((int)k);
+                return blocks_[k].p;
+            }
         void* p = nullptr;
         const size_t cap = bytes < 65536 ? 65536 : bytes;
         if (hipHostMalloc(&p, cap) != hipSuccess) return nullptr;
-        blocks_.insert(blocks_.begin() + (long)used_, Block{p, cap});
-        return blocks_[used_++].p;
+        blocks_.push_back(Block{p, cap, true});
+        cur_blocks_.push_back((int)blocks_.size() - 1);
+        return p;
     }
     bool on_ = false;
+    std::mutex mu_;
     std::vector<Block> blocks_;
-    size_t used_ = 0;
-    std::vector<Out> outs_;
+    std::vector<int> cur_blocks_;
+    std::vector<Out> cur_outs_;
+    std::deque<Epoch> closed_;
+    hipEvent_t events_[kEvents] = {};
+    long long next_id_ = 1, done_id_ = 0;
 };
 
 constexpr int kEdge = 19;          // EDGE_THRESHOLD, ORBextractor.cc:67

@@ -136,6 +136,14 @@ int ORBmatcher_last_timings(ORBmatcher_h h, float* ms8, long long* counts8);
  * the calls.  Turning deferred off finishes a pending chain. */
 int ORBmatcher_set_deferred(ORBmatcher_h h, int on);
 int ORBmatcher_finish(ORBmatcher_h h);
+/* Overlapping chains: close the calls queued so far into an epoch (returns at once), queue the
+ * next step's calls, and finish the older epoch later.  chain_wait blocks until an epoch's
+ * device work is done (no counts written; callable from another host thread, e.g. before
+ * reusing that epoch's input buffers); chain_finish(e) waits for every epoch <= e and writes
+ * their counts. */
+int ORBmatcher_chain_close(ORBmatcher_h h, long long* epoch);
+int ORBmatcher_chain_wait(ORBmatcher_h h, long long epoch);
+int ORBmatcher_chain_finish(ORBmatcher_h h, long long epoch);
 
 /* static int ORBmatcher::DescriptorDistance(a, b)   ORBmatcher.cc:1647-1663 (host) */
 int ORBmatcher_DescriptorDistance(const uint8_t* a, const uint8_t* b);
