@@ -148,7 +148,32 @@ def test_deferred_chain_equals_synchronous(gpu):
     PoseOptimizationFramesDevice(framed, T2, o2, chain=m, n_out=n2)
     assert (n1 == -9).all() and (n2 == -9).all()      # nothing lands before finish
     check(L.ORBmatcher_finish(m._h))
+    # overlapping chains: close one epoch, queue the next behind it, wait for the first from
+    # another host thread (device work only), then finish them in order
+    import ctypes as C
+    import threading
+    T3 = [torch.zeros(16, dtype=torch.float32, device=dev) for _ in frames]
+    T4 = [torch.zeros(16, dtype=torch.float32, device=dev) for _ in frames]
+    o3, o4 = mk(9), mk(9)
+    n3, n4 = np.full(3, -9, np.int32), np.full(3, -9, np.int32)
+    e3, e4 = C.c_longlong(0), C.c_longlong(0)
+    PoseOptimizationFramesDevice(framed, T3, o3, chain=m, n_out=n3)
+    check(L.ORBmatcher_chain_close(m._h, C.byref(e3)))
+    PoseOptimizationFramesDevice(framed, T4, o4, chain=m, n_out=n4)
+    check(L.ORBmatcher_chain_close(m._h, C.byref(e4)))
+    assert e4.value == e3.value + 1
+    th = threading.Thread(target=lambda: check(L.ORBmatcher_chain_wait(m._h, e3.value)))
+    th.start()
+    th.join()
+    assert (n3 == -9).all()                           # waiting writes nothing
+    check(L.ORBmatcher_chain_finish(m._h, e3.value))
+    assert np.array_equal(n3, n0) and (n4 == -9).all()
+    check(L.ORBmatcher_chain_finish(m._h, e4.value))
+    assert np.array_equal(n4, n0)
     check(L.ORBmatcher_set_deferred(m._h, 0))
+    for f in range(3):
+        assert np.array_equal(T3[f].cpu().numpy(), T0[f].cpu().numpy())
+        assert np.array_equal(T4[f].cpu().numpy(), T0[f].cpu().numpy())
     for n, T, o in ((n1, T1, o1), (n2, T2, o2)):
         assert np.array_equal(n, n0)
         for f in range(3):
