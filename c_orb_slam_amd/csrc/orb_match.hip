@@ -299,7 +299,16 @@ __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict_
                                                     unsigned long long* counters) {
     ORBGPU_LATENCY_WAVE();
     const SearchDev P = probs[blockIdx.y];
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!LAST && P.visList) {   // SearchLocalPoints: thread t takes the t-th in-view query
+        const int nv = *P.visCount;
+        if (q >= nv) {
+            if (!counters) return;
+            q = P.nq;   // measurement only
+        } else {
+            q = P.visList[q];
+        }
+    }
     if (!counters && q >= P.nq) return;
     int2 top[kTopK];
     int cnt = -1;
@@ -385,9 +394,17 @@ __global__ void __launch_bounds__(256) k_frustum(const SearchDev* __restrict__ p
             }
         }
         Fq.inView[j] = (uint8_t)vis;
+        if (!vis && P.qinfo) P.qinfo[j] = make_int4(-1, 0, 0, 0);   // no window: k_candidates skips it
     }
-    const unsigned long long nv = wave_sum_u64((unsigned long long)vis);
-    if ((threadIdx.x & 63) == 0 && nv) atomicAdd(Fq.nvisible, (int)nv);
+    const unsigned long long vm = __ballot(vis != 0);
+    const int nv = (int)__popcll(vm);
+    if (P.visList && nv) {   // compact the in-view queries, one atomic per wave
+        int base = 0;
+        if ((threadIdx.x & 63) == 0) base = atomicAdd(P.visCount, nv);
+        base = __shfl(base, 0, 64);
+        if (vis) P.visList[base + (int)__popcll(vm & ((1ull << (threadIdx.x & 63)) - 1ull))] = j;
+    }
+    if ((threadIdx.x & 63) == 0 && nv) atomicAdd(Fq.nvisible, nv);
 }
 
 // Greedy replay as a fixed-point iteration (one 256-thread workgroup per problem).
@@ -720,20 +737,29 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     if (np == 0) return 0;
     size_t need = 0;
     int maxq = 0, maxN = 1;
+    const bool vis = frustum_ != nullptr;   // SearchLocalPoints: in-view query lists
     for (auto& p : probs) {
         if (p.cur.N > kMaxFrameKeys || p.cur.N < 0 || p.nq < 0) return -1;
         maxN = std::max(maxN, p.cur.N);
         need += ((size_t)(kGridCells + 1 + p.cur.N) * 4 + 255) & ~(size_t)255;
         need += ((size_t)p.nq * (kTopK * 8 + 16 + 8) + 255) & ~(size_t)255;
+        if (vis) need += ((size_t)p.nq * 4 + 255) & ~(size_t)255;
         maxq = std::max(maxq, p.nq);
     }
+    if (vis) need += ((size_t)np * 4 + 255) & ~(size_t)255;
     if (need > scratch_cap_) {
         if (d_scratch_) (void)hipFree(d_scratch_);
         scratch_cap_ = need * 2;
         ORB_HIP_CHECK(hipMalloc(&d_scratch_, scratch_cap_));
     }
     char* s = (char*)d_scratch_;
-    for (auto& p : probs) {
+    int* visCounts = nullptr;
+    if (vis) {
+        visCounts = (int*)s;
+        s += ((size_t)np * 4 + 255) & ~(size_t)255;
+    }
+    for (size_t k = 0; k < probs.size(); k++) {
+        SearchDev& p = probs[k];
         p.gridStart = (int*)s;
         p.gridIdx = p.gridStart + kGridCells + 1;
         s += ((size_t)(kGridCells + 1 + p.cur.N) * 4 + 255) & ~(size_t)255;
@@ -741,7 +767,15 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
         p.qinfo = (int4*)(p.topk + (size_t)p.nq * kTopK);
         p.hist = (int2*)(p.qinfo + p.nq);
         s += ((size_t)p.nq * (kTopK * 8 + 16 + 8) + 255) & ~(size_t)255;
+        p.visList = nullptr;
+        p.visCount = nullptr;
+        if (vis) {
+            p.visList = (int*)s;
+            p.visCount = visCounts + k;
+            s += ((size_t)p.nq * 4 + 255) & ~(size_t)255;
+        }
     }
+    if (vis) ORB_HIP_CHECK(hipMemsetAsync(visCounts, 0, (size_t)np * 4, stream_));
     const size_t pb = sizeof(SearchDev) * np;
     if (pb > probs_cap_) {
         if (d_probs_) (void)hipFree(d_probs_);

@@ -56,6 +56,10 @@ struct SearchDev {
     int2* topk;       // nq * kTopK  (x = dist, y = candidate index)
     int4* qinfo;      // nq: x = ncand (-1 skip), y = bits(u), z = bits(v), w = bits(radius/r)
     int2* hist;       // nq (bin, idx)
+    // SearchLocalPoints: k_frustum lists the in-view queries (any order) so that k_candidates'
+    // waves are dense in queries with a window; null otherwise
+    int* visList;     // nq
+    int* visCount;    // 1
 };
 
 // Frame::isInFrustum inputs / outputs of one SearchLocalPoints problem (Tracking.cc:1143-1193):
