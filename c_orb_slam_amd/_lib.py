@@ -106,6 +106,7 @@ def lib():
     L.ORBextractor_stream.restype = vp
     L.ORBextractor_stream.argtypes = [vp]
     L.ORBextractor_last_timings.argtypes = [vp, vp]
+    L.ORBextractor_last_corner_count.argtypes = [vp, vp]
     L.ORBmatcher_create.argtypes = [f32, i32, P(vp)]
     L.ORBmatcher_set_deferred.argtypes = [vp, i32]
     L.ORBmatcher_finish.argtypes = [vp]
@@ -173,6 +174,9 @@ def lib():
     L.Optimizer_OptimizeSim3_batch.argtypes = [i32, vp, vp, vp, vp]
     L.Optimizer_PoseOptimization_frames_device.argtypes = [i32, vp, vp, vp, vp]
     L.Frame_UnprojectStereo_batch_device.argtypes = [vp, i32, vp]
+    L.Frame_UndistortKeyPoints.argtypes = [vp, vp]
+    L.Frame_UndistortKeyPoints_batch.argtypes = [vp, i32, vp]
+    L.Frame_ComputeImageBounds.argtypes = [vp, i32, i32, vp, vp, i32, vp]
     L.ORBvocabulary_create.argtypes = [P(vp)]
     L.ORBvocabulary_destroy.argtypes = [vp]
     L.ORBvocabulary_loadFromTextFile.argtypes = [vp, C.c_char_p]
@@ -231,6 +235,11 @@ class orb_unproject(C.Structure):
     _fields_ = [("N", C.c_int), ("keysUn", C.c_void_p), ("depth", C.c_void_p), ("Twc", C.c_void_p),
                 ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
                 ("x3D", C.c_void_p), ("mp", C.c_void_p)]
+
+
+class orb_undistort(C.Structure):
+    _fields_ = [("N", C.c_int), ("keys", C.c_void_p), ("keysUn", C.c_void_p), ("K", C.c_float * 9),
+                ("dist", C.c_float * 8), ("ndist", C.c_int)]
 
 
 class orb_bow(C.Structure):

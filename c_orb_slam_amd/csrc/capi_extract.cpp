@@ -109,4 +109,9 @@ int ORBextractor_last_timings(ORBextractor_h h, float* ms6) {
     return h->ex->timings(ms6);
 }
 
+int ORBextractor_last_corner_count(ORBextractor_h h, long long* total) {
+    if (!h || !total) return ORB_E_INVALID;
+    return h->ex->corner_total(total) ? ORB_E_INVALID : ORB_OK;
+}
+
 }  // extern "C"

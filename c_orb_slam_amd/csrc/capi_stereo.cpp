@@ -168,6 +168,106 @@ int Frame_UnprojectStereo_batch_device(ORBmatcher_h h, int count, const orb_unpr
     return orbgpu::unproject_batch(P.data(), count, h->m->stream()) ? ORB_E_HIP : ORB_OK;
 }
 
+static int fill_undist(const orb_undistort& q, orbgpu::UndistDev& d) {
+    if (q.N < 0 || q.N > (1 << 24) || (q.N > 0 && (!q.keys || !q.keysUn))) return ORB_E_INVALID;
+    if (q.ndist != 4 && q.ndist != 5 && q.ndist != 8) return ORB_E_INVALID;   // cv::undistortPoints sizes ORB-SLAM2 reads
+    std::memset(&d, 0, sizeof(d));
+    d.N = q.N;
+    d.keys = (const orbgpu::orb_kp_dev*)q.keys;
+    d.keysUn = (orbgpu::orb_kp_dev*)q.keysUn;
+    d.has_dist = q.dist[0] != 0.0f;   // Frame.cc:406: mDistCoef.at<float>(0)==0.0 -> mvKeysUn = mvKeys
+    for (int i = 0; i < 9; i++) d.A[i] = (double)q.K[i];
+    for (int i = 0; i < 8; i++) d.k[i] = i < q.ndist ? (double)q.dist[i] : 0.0;
+    return ORB_OK;
+}
+
+int Frame_UndistortKeyPoints_batch(ORBmatcher_h h, int count, const orb_undistort* U) {
+    if (!h || count < 0 || (count > 0 && !U)) return ORB_E_INVALID;
+    if (count == 0) return ORB_OK;
+    std::vector<orbgpu::UndistDev> P((size_t)count);
+    for (int f = 0; f < count; f++)
+        if (int e = fill_undist(U[f], P[f])) return e;
+    hipStream_t s = h->m->stream();
+    if (h->m->device_pointers()) return orbgpu::undistort_batch(P.data(), count, s) ? ORB_E_HIP : ORB_OK;
+    // host arrays: one device block holding every frame's keys and results, copied per call
+    size_t tot = 0;
+    for (int f = 0; f < count; f++) tot += (size_t)P[f].N;
+    if (tot == 0) return ORB_OK;
+    void* d = nullptr;
+    if (hipMalloc(&d, 2 * tot * sizeof(orb_kp)) != hipSuccess) return ORB_E_HIP;
+    orbgpu::orb_kp_dev* dk = (orbgpu::orb_kp_dev*)d;
+    int rc = ORB_OK;
+    size_t o = 0;
+    for (int f = 0; f < count && rc == ORB_OK; f++) {
+        if (P[f].N && hipMemcpyAsync(dk + o, U[f].keys, P[f].N * sizeof(orb_kp), hipMemcpyHostToDevice, s) != hipSuccess)
+            rc = ORB_E_HIP;
+        P[f].keys = dk + o;
+        P[f].keysUn = dk + tot + o;
+        o += (size_t)P[f].N;
+    }
+    if (rc == ORB_OK && orbgpu::undistort_batch(P.data(), count, s)) rc = ORB_E_HIP;
+    o = 0;
+    for (int f = 0; f < count && rc == ORB_OK; f++) {
+        if (P[f].N && hipMemcpyAsync(U[f].keysUn, dk + tot + o, P[f].N * sizeof(orb_kp), hipMemcpyDeviceToHost, s) !=
+                          hipSuccess)
+            rc = ORB_E_HIP;
+        o += (size_t)P[f].N;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_E_HIP;
+    (void)hipFree(d);
+    return rc;
+}
+
+int Frame_UndistortKeyPoints(ORBmatcher_h h, const orb_undistort* U) {
+    if (!h || !U) return ORB_E_INVALID;
+    if (h->m->device_pointers()) {   // the single form is synchronous in either pointer space
+        const int e = Frame_UndistortKeyPoints_batch(h, 1, U);
+        if (e) return e;
+        return hipStreamSynchronize(h->m->stream()) == hipSuccess ? ORB_OK : ORB_E_HIP;
+    }
+    return Frame_UndistortKeyPoints_batch(h, 1, U);
+}
+
+int Frame_ComputeImageBounds(ORBmatcher_h h, int cols, int rows, const float* K, const float* dist, int ndist,
+                             float* bounds) {
+    if (!h || !K || !dist || !bounds || cols <= 0 || rows <= 0) return ORB_E_INVALID;
+    if (ndist != 4 && ndist != 5 && ndist != 8) return ORB_E_INVALID;
+    if (dist[0] != 0.0f) {   // Frame.cc:438-455: the four image corners through cv::undistortPoints
+        orb_kp c[4];
+        std::memset(c, 0, sizeof(c));
+        c[1].x = (float)cols;
+        c[2].y = (float)rows;
+        c[3].x = (float)cols; c[3].y = (float)rows;
+        orb_kp u[4];
+        orb_undistort q;
+        std::memset(&q, 0, sizeof(q));
+        q.N = 4;
+        q.keys = c;
+        q.keysUn = u;
+        std::memcpy(q.K, K, sizeof(q.K));
+        for (int i = 0; i < ndist; i++) q.dist[i] = dist[i];
+        q.ndist = ndist;
+        const bool dev = h->m->device_pointers();
+        h->m->set_device_pointers(false);   // the corners are host values
+        const int e = Frame_UndistortKeyPoints_batch(h, 1, &q);
+        h->m->set_device_pointers(dev);
+        if (e) return e;
+        bounds[0] = std::min(u[0].x, u[2].x);   // mnMinX = min(mat(0,0), mat(2,0))
+        bounds[1] = std::max(u[1].x, u[3].x);
+        bounds[2] = std::min(u[0].y, u[1].y);
+        bounds[3] = std::max(u[2].y, u[3].y);
+    } else {
+        bounds[0] = 0.0f;
+        bounds[1] = (float)cols;
+        bounds[2] = 0.0f;
+        bounds[3] = (float)rows;
+    }
+    // Frame.cc:155-156 (FRAME_GRID_COLS / ROWS = 64 / 48)
+    bounds[4] = static_cast<float>(64) / static_cast<float>(bounds[1] - bounds[0]);
+    bounds[5] = static_cast<float>(48) / static_cast<float>(bounds[3] - bounds[2]);
+    return ORB_OK;
+}
+
 int MapPoint_CreateStereo_batch_device(ORBmatcher_h h, int count, const orb_newpoints* Q) {
     if (!h || count < 0 || (count > 0 && !Q)) return ORB_E_INVALID;
     if (count == 0) return ORB_OK;

@@ -1102,6 +1102,15 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     return 0;
 }
 
+int Extractor::corner_total(long long* total) {
+    if (last_B_ <= 0 || !d_gtotal_) return -1;
+    int v = 0;   // k_compact's atomic total over the batch (d_gtotal_), read after the call
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    ORB_HIP_CHECK(hipMemcpy(&v, d_gtotal_, 4, hipMemcpyDeviceToHost));
+    *total = v;
+    return 0;
+}
+
 int Extractor::get_blurred(int index, int level, uint8_t* dst, int dst_step, int* w, int* h) {
     if (level < 0 || level >= nlevels_ || index < 0 || index >= last_B_ || !d_blur_) return -1;
     const LevelHost& L = levels_[level];

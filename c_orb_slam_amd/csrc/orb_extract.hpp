@@ -61,6 +61,7 @@ public:
     int get_level(int index, int level, uint8_t* dst, int dst_step, int* w, int* h);
     int get_blurred(int index, int level, uint8_t* dst, int dst_step, int* w, int* h);
     int timings(float* ms6);
+    int corner_total(long long* total);   // FAST corners written by the last extract()
     hipStream_t stream() const { return stream_; }
     // recreate the stream with a CU mask leaving out one CU in every `one_in_n` (0: all CUs)
     int reserve_cus(int one_in_n);

@@ -44,22 +44,32 @@ __device__ __forceinline__ float gemm_row(const float* T, int r, float X0, float
 
 // Frame::AssignFeaturesToGrid (Frame.cc:230-245) as a counting sort: gridIdx lists every cell's
 // keypoints in index order, cells in x-major order (cell = px * 48 + py), gridStart[c] its
-// offset; keypoints outside the grid follow as 4095.  Per-cell counts and cursors are packed
-// 16-bit pairs in LDS (a cell holds at most N <= 4096 keypoints), the scatter is by LDS atomics,
-// and a thread per cell restores index order inside its (few-entry) segment.
-inline size_t grid_lds_bytes(int maxN) { return (((size_t)std::max(maxN, 1) * 2 + 15) & ~(size_t)15); }
+// offset; keypoints outside the grid follow as 4095.  Everything stays in LDS until the final
+// scattered store: per-cell counts, starts and cursors are packed 16-bit pairs (a cell holds at
+// most N <= 4096 keypoints), the keypoints are scattered into their cell segments by LDS
+// atomics (arbitrary order inside a segment), and each keypoint's final slot is its segment
+// start plus the number of smaller indices in its segment (a stable order with no serial sort:
+// O(sum of squared cell sizes / 256) LDS reads, a few per keypoint for ordinary frames, and still
+// spread over the whole workgroup when every keypoint lands in one cell).
+inline size_t grid_lds_bytes(int maxN) { return (((size_t)std::max(maxN, 1) * 4 + 4 + 15) & ~(size_t)15); }
 inline size_t select_lds_bytes(int maxN) { return ((size_t)std::max(maxN, 1) * 10 + 15) & ~(size_t)15; }
+
+__device__ __forceinline__ int packed16(const uint32_t* a, int c) { return (int)((a[c >> 1] >> (16 * (c & 1))) & 0xffffu); }
 
 __global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs) {
     ORBGPU_LATENCY_WAVE();
     constexpr int kPer = kGridCells / 256;   // 12 cells per thread in the scan
     static_assert(kGridCells % 512 == 0, "packed pairs per thread");
-    __shared__ uint32_t s_cnt[kGridCells / 2];
+    __shared__ uint32_t s_cnt[kGridCells / 2];   // counts, then cursors
+    __shared__ uint32_t s_beg[kGridCells / 2];   // segment starts
     __shared__ int s_wsum[4];
-    extern __shared__ int16_t s_cell[];   // max N entries: cell of keypoint i or -1
+    extern __shared__ int s_dyn32[];
+    int16_t* s_dyn = reinterpret_cast<int16_t*>(s_dyn32);
     SearchDev& P = probs[blockIdx.x];
     const FrameDev& F = P.cur;
     const int N = F.N, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    int16_t* s_cell = s_dyn;                       // N: cell of keypoint i or -1
+    int16_t* s_idx = s_dyn + ((N + 1) & ~1);       // total: keypoints in cell order (unordered inside)
     for (int w = tid; w < kGridCells / 2; w += 256) s_cnt[w] = 0u;
     __syncthreads();
     for (int i = tid; i < N; i += 256) {
@@ -98,7 +108,9 @@ __global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs) {
         const int c = kPer * tid + k;
         P.gridStart[c] = run;
         P.gridStart[c + 1] = run + cnt[k];
-        s_cnt[c >> 1] = (uint32_t)run | ((uint32_t)(run + cnt[k]) << 16);   // cursors
+        const uint32_t pr = (uint32_t)run | ((uint32_t)(run + cnt[k]) << 16);
+        s_cnt[c >> 1] = pr;   // cursors
+        s_beg[c >> 1] = pr;   // starts
         run += cnt[k] + cnt[k + 1];
     }
     if (tid == 255) P.gridStart[kGridCells] = total;
@@ -108,22 +120,18 @@ __global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs) {
         if (cell >= 0) {
             const int sh = 16 * (cell & 1);
             const int pos = (int)((atomicAdd(&s_cnt[cell >> 1], 1u << sh) >> sh) & 0xffffu);
-            P.gridIdx[pos] = i;
+            s_idx[pos] = (int16_t)i;
         }
     }
     for (int i = total + tid; i < N; i += 256) P.gridIdx[i] = 4095;
     __syncthreads();
-    for (int c = tid; c < kGridCells; c += 256) {   // index order inside each cell
-        const int b0 = P.gridStart[c], b1 = P.gridStart[c + 1];
-        for (int x = b0 + 1; x < b1; x++) {
-            const int v = P.gridIdx[x];
-            int y = x - 1;
-            while (y >= b0 && P.gridIdx[y] > v) {
-                P.gridIdx[y + 1] = P.gridIdx[y];
-                y--;
-            }
-            P.gridIdx[y + 1] = v;
-        }
+    // stable slot of every placed keypoint: its segment start + the smaller indices in the segment
+    for (int p = tid; p < total; p += 256) {
+        const int i = s_idx[p], c = s_cell[i];
+        const int b0 = packed16(s_beg, c), b1 = c + 1 < kGridCells ? packed16(s_beg, c + 1) : total;
+        int r = 0;
+        for (int q = b0; q < b1; q++) r += (int)s_idx[q] < i;
+        P.gridIdx[b0 + r] = i;
     }
 }
 

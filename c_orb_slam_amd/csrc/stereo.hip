@@ -356,6 +356,64 @@ __global__ void __launch_bounds__(256) k_local_prep(const LocalPrepDev* __restri
     }
 }
 
+// ---------------------------------------------------------------- UndistortKeyPoints
+// cvUndistortPoints (OpenCV 3.2 imgproc/undistort.cpp) for one CV_32FC2 point, as
+// Frame::UndistortKeyPoints calls it (Frame.cc:418-419): normalise with 1/fx, 1/fy in double,
+// 5 fixed-point iterations of the inverse radial/tangential model, then the new camera matrix
+// (RR = K * I: the literal 3x3 product below, exact for K's zeros and ones).  The operation
+// order is the reference's (the tilt and thin-prism terms are 0 and exact, see the oracle);
+// the build's -ffp-contract=off keeps every product and sum rounded separately.
+__device__ __forceinline__ void undistort_pt(float sx, float sy, const double* A, const double* k, int iters,
+                                             float* ox, float* oy) {
+    const double fx = A[0], fy = A[4], ifx = 1. / fx, ify = 1. / fy, cx = A[2], cy = A[5];
+    double x = sx, y = sy, x0, y0;
+    x0 = x = (x - cx) * ifx;
+    y0 = y = (y - cy) * ify;
+    for (int j = 0; j < iters; j++) {
+        const double r2 = x * x + y * y;
+        const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+        const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x);
+        const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    const double xx = A[0] * x + A[1] * y + A[2];
+    const double yy = A[3] * x + A[4] * y + A[5];
+    const double ww = 1. / (A[6] * x + A[7] * y + A[8]);
+    *ox = (float)(xx * ww);
+    *oy = (float)(yy * ww);
+}
+
+struct UndistBatch {
+    UndistDev p[kUndistPerLaunch];
+};
+
+__global__ void __launch_bounds__(256) k_undistort(UndistBatch B) {
+    ORBGPU_LATENCY_WAVE();
+    const UndistDev& P = B.p[blockIdx.y];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.N) return;
+    orb_kp_dev kp = P.keys[i];
+    if (P.has_dist) undistort_pt(kp.x, kp.y, P.A, P.k, 5, &kp.x, &kp.y);
+    P.keysUn[i] = kp;
+}
+
+int undistort_batch(const UndistDev* probs, int count, hipStream_t s) {
+    for (int f0 = 0; f0 < count; f0 += kUndistPerLaunch) {
+        const int n = std::min(kUndistPerLaunch, count - f0);
+        UndistBatch B;
+        std::memset(&B, 0, sizeof(B));
+        int maxN = 0;
+        for (int f = 0; f < n; f++) {
+            B.p[f] = probs[f0 + f];
+            maxN = std::max(maxN, B.p[f].N);
+        }
+        if (maxN > 0) hipLaunchKernelGGL(k_undistort, dim3((maxN + 255) / 256, n), dim3(256), 0, s, B);
+    }
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 int local_prep_batch(const LocalPrepDev* d_probs, int count, hipStream_t s) {
     if (count <= 0) return 0;
     hipLaunchKernelGGL(k_local_prep, dim3(count), dim3(256), 0, s, d_probs);

@@ -79,4 +79,17 @@ constexpr int kUnprojPerLaunch = 56;   // frames per launch, passed by value (ke
 // enqueue on `s` (no staging buffer: the frames are kernel arguments)
 int unproject_batch(const UnprojDev* probs, int count, hipStream_t s);
 
+// Frame::UndistortKeyPoints over a batch of frames (Frame.cc:404-430): cv::undistortPoints
+// (OpenCV 3.2 cvUndistortPoints, R = I, P = K) on every keypoint; the rest of the KeyPoint is
+// copied.  has_dist = 0 (mDistCoef.at<float>(0) == 0) copies mvKeys.
+struct UndistDev {
+    int N, has_dist;
+    const orb_kp_dev* keys;
+    orb_kp_dev* keysUn;
+    double A[9];   // mK as double (cvConvert)
+    double k[8];   // k1 k2 p1 p2 k3 k4 k5 k6 as double, zero-filled
+};
+constexpr int kUndistPerLaunch = 24;   // frames per launch, passed by value
+int undistort_batch(const UndistDev* probs, int count, hipStream_t s);
+
 }  // namespace orbgpu

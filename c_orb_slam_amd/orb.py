@@ -134,6 +134,12 @@ class ORBextractor:
         check(self._L.ORBextractor_last_timings(self._h, ptr(t)))
         return dict(zip(["pyramid", "blur", "fast_cells", "compact", "octree", "orient_desc"], t.tolist()))
 
+    def last_corner_count(self):
+        """FAST corners the last call kept (all its images), before DistributeOctTree."""
+        n = np.zeros(1, np.int64)
+        check(self._L.ORBextractor_last_corner_count(self._h, ptr(n)))
+        return int(n[0])
+
 
 class Frame:
     """The Frame fields the matcher reads (Frame.h).  Arrays are host numpy."""
@@ -426,6 +432,51 @@ class ORBmatcher:
                                     mp.data_ptr() if mp is not None else None))
         arr = (orb_unproject * max(len(us), 1))(*us)
         check(self._L.Frame_UnprojectStereo_batch_device(self._h, len(us), arr), "Frame_UnprojectStereo_batch_device")
+
+    @staticmethod
+    def _undistort_struct(N, keys_ptr, out_ptr, K, dist):
+        from ._lib import orb_undistort
+        K = np.ascontiguousarray(K, np.float32).reshape(-1)
+        dist = np.ascontiguousarray(dist, np.float32).reshape(-1)
+        if K.size != 9 or dist.size not in (4, 5, 8):
+            raise ValueError("K must be 3x3 and mDistCoef 4, 5 or 8 coefficients")
+        u = orb_undistort()
+        u.N, u.keys, u.keysUn, u.ndist = int(N), keys_ptr, out_ptr, int(dist.size)
+        u.K[:] = K.tolist()
+        u.dist[:dist.size] = dist.tolist()
+        return u
+
+    def UndistortKeyPoints(self, keys, K, dist):
+        """Frame::UndistortKeyPoints (Frame.cc:404-430): mvKeys (KP_DTYPE) -> mvKeysUn, through
+        cv::undistortPoints(pts, pts, mK, mDistCoef, Mat(), mK) on the GPU."""
+        keys = np.ascontiguousarray(keys, KP_DTYPE)
+        out = np.zeros(max(len(keys), 1), KP_DTYPE)
+        u = self._undistort_struct(len(keys), keys.ctypes.data if len(keys) else None, out.ctypes.data, K, dist)
+        check(self._L.Frame_UndistortKeyPoints(self._h, C.byref(u)), "Frame_UndistortKeyPoints")
+        return out[:len(keys)]
+
+    def UndistortKeyPoints_device(self, frames):
+        """The batch form over device-resident frames, enqueued on this matcher's stream: frames[f]
+        = dict(keys, keysUn (torch device tensors, N x 7 words), K (3x3), dist)."""
+        from ._lib import orb_undistort
+        us = [self._undistort_struct(f["keys"].shape[0], f["keys"].data_ptr(), f["keysUn"].data_ptr(), f["K"], f["dist"])
+              for f in frames]
+        arr = (orb_undistort * max(len(us), 1))(*us)
+        check(self._L.ORBmatcher_set_device_pointers(self._h, 1))
+        try:
+            check(self._L.Frame_UndistortKeyPoints_batch(self._h, len(us), arr), "Frame_UndistortKeyPoints_batch")
+        finally:
+            check(self._L.ORBmatcher_set_device_pointers(self._h, 0))
+
+    def ComputeImageBounds(self, cols, rows, K, dist):
+        """Frame::ComputeImageBounds (Frame.cc:436-464) + the grid factors (Frame.cc:155-156) ->
+        (mnMinX, mnMaxX, mnMinY, mnMaxY, mfGridElementWidthInv, mfGridElementHeightInv)."""
+        K = np.ascontiguousarray(K, np.float32).reshape(-1)
+        dist = np.ascontiguousarray(dist, np.float32).reshape(-1)
+        b = np.zeros(6, np.float32)
+        check(self._L.Frame_ComputeImageBounds(self._h, int(cols), int(rows), ptr(K), ptr(dist), int(dist.size), ptr(b)),
+              "Frame_ComputeImageBounds")
+        return tuple(np.float32(v) for v in b)
 
     def SearchByProjection_KeyFrame(self, F: Frame, cur_mp, kf_mp, skip, kf_angle, mps: MapPoints, max_dist,
                                     min_dist, logScaleFactor, th, ORBdist):

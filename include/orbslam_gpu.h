@@ -92,6 +92,10 @@ void* ORBextractor_stream(ORBextractor_h h);
 /* Per-stage device time of the last call (ms), from HIP events:
  * [0]=pyramid [1]=blur [2]=FAST cells [3]=compaction [4]=octree(host) [5]=orientation+rBRIEF */
 int ORBextractor_last_timings(ORBextractor_h h, float* ms6);
+/* FAST corners kept by the last call, summed over its images (after the per-cell NMS and cell
+ * caps of ORBextractor.cc:776-829, before DistributeOctTree): the k_fast_cells output that the
+ * bench's algorithmic-bytes figure counts. */
+int ORBextractor_last_corner_count(ORBextractor_h h, long long* total);
 /* Scheduling (no reference counterpart): keep one CU in every `one_in_n` of each XCD out of
  * this extractor's launches (its stream is recreated with a CU mask), so the tracking lane's
  * one-workgroup-per-frame kernels (matcher greedy replay, PoseOptimization) find free wave
@@ -281,6 +285,31 @@ typedef struct orb_unproject {
     int32_t* mp;                 /* out (may be NULL): i if depth > 0, else -1 */
 } orb_unproject;
 int Frame_UnprojectStereo_batch_device(ORBmatcher_h h, int count, const orb_unproject* U);
+
+/* void Frame::UndistortKeyPoints()                               Frame.cc:404-430
+ * mvKeysUn from mvKeys: when mDistCoef.at<float>(0) == 0 a copy; otherwise every keypoint's pt
+ * through cv::undistortPoints(pts, pts, mK, mDistCoef, Mat(), mK) (OpenCV 3.2
+ * cvUndistortPoints: double arithmetic, 5 fixed-point iterations; "parity unpinned" at that
+ * OpenCV call site) and the rest of each KeyPoint copied.  K: mK row-major;
+ * dist: mDistCoef (k1 k2 p1 p2 [k3] [k4 k5 k6]), ndist = 4, 5 or 8.  Pointer space per
+ * ORBmatcher_set_device_pointers: device arrays are enqueued on ORBmatcher_stream (batch form)
+ * and host arrays are copied and waited for. */
+typedef struct orb_undistort {
+    int N;
+    const orb_kp* keys;          /* mvKeys (N) */
+    orb_kp* keysUn;              /* out: mvKeysUn (N); may not alias keys */
+    float K[9];                  /* mK */
+    float dist[8];               /* mDistCoef, ndist used */
+    int ndist;
+} orb_undistort;
+int Frame_UndistortKeyPoints(ORBmatcher_h h, const orb_undistort* U);
+int Frame_UndistortKeyPoints_batch(ORBmatcher_h h, int count, const orb_undistort* U);
+/* void Frame::ComputeImageBounds(const cv::Mat&)                    Frame.cc:436-464
+ * plus the grid factors the Frame constructors derive from it (Frame.cc:155-156):
+ * bounds[0..5] = mnMinX, mnMaxX, mnMinY, mnMaxY, mfGridElementWidthInv, mfGridElementHeightInv.
+ * With distortion the four image corners go through the UndistortKeyPoints kernel. */
+int Frame_ComputeImageBounds(ORBmatcher_h h, int cols, int rows, const float* K, const float* dist, int ndist,
+                             float* bounds);
 
 /* New MapPoints from a stereo frame (Tracking::StereoInitialization / CreateNewKeyFrame /
  * UpdateLastFrame, Tracking.cc:520-560, 1025-1080, 837-860): for every keypoint with depth > 0,

@@ -14,6 +14,7 @@
  *   resize LINEAR 8U -> imgproc/imgwarp.cpp fixed point (11 bit) ORBextractor.cc:1120
  *   GaussianBlur 8U  -> imgproc/smooth.cpp + filter.cpp 8-bit fixed-point separable
  *                       filter, scalar (non-SSE) column cast      ORBextractor.cc:1086
+ *   undistortPoints  -> imgproc/undistort.cpp cvUndistortPoints  Frame.cc:404-464
  */
 #include "orb_oracle.h"
 #include <math.h>
@@ -353,4 +354,47 @@ long ora_check_sincos_vs_libm(float lo, float hi, long stride)
         if (uhi - u < (uint32_t)stride) break;
     }
     return bad;
+}
+
+/* cv::undistortPoints(src, dst, K, D, noArray(), K) for CV_32FC2 points (OpenCV 3.2
+ * imgproc/undistort.cpp, cvUndistortPoints), as Frame::UndistortKeyPoints and
+ * Frame::ComputeImageBounds call it (Frame.cc:418-419, 445-447).  The camera matrix and the
+ * coefficients are converted to double (cvConvert); with coefficients the distortion is
+ * compensated by 5 fixed-point iterations (iters = 5); R is the identity and the new camera
+ * matrix P = K enters as RR = P * I (cvMatMul, exact: every product by 0 or 1 is exact and
+ * every added term +-0).  The tilt (k[12], k[13]) and thin-prism (k[8..11]) terms of the
+ * 12/14-coefficient models are 0 for the 4/5/8-coefficient vectors ORB-SLAM2 passes; with an
+ * identity tilt matrix the untilt step is exact, and their +0 terms are exact, so they are
+ * not restated.  k: 8 doubles (k1 k2 p1 p2 k3 k4 k5 k6), zero-filled beyond the given count. */
+void ora_undistort_points(const float* src, int n, const float K[9], const double k[8], int has_dist, float* dst)
+{
+    double A[3][3], RR[3][3];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) A[r][c] = (double)K[r * 3 + c];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) RR[r][c] = A[r][c];
+    const int iters = has_dist ? 5 : 1;
+    const double fx = A[0][0], fy = A[1][1];
+    const double ifx = 1. / fx, ify = 1. / fy;
+    const double cx = A[0][2], cy = A[1][2];
+    for (int i = 0; i < n; i++) {
+        double x = src[2 * i], y = src[2 * i + 1], x0, y0;
+        x0 = x = (x - cx) * ifx;
+        y0 = y = (y - cy) * ify;
+        for (int j = 0; j < iters; j++) {
+            double r2 = x * x + y * y;
+            double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+            double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x);
+            double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y;
+            x = (x0 - deltaX) * icdist;
+            y = (y0 - deltaY) * icdist;
+        }
+        double xx = RR[0][0] * x + RR[0][1] * y + RR[0][2];
+        double yy = RR[1][0] * x + RR[1][1] * y + RR[1][2];
+        double ww = 1. / (RR[2][0] * x + RR[2][1] * y + RR[2][2]);
+        x = xx * ww;
+        y = yy * ww;
+        dst[2 * i] = (float)x;
+        dst[2 * i + 1] = (float)y;
+    }
 }

@@ -232,6 +232,15 @@ double ora_voc_score_l1(const uint32_t* w1, const double* v1, int n1, const uint
 void  ora_unproject_stereo(const ora_kp* kps, const float* depth, int N, const float* Twc, float fx, float fy,
                            float cx, float cy, float* x3D, int* mp);
 
+/* ---- cv::undistortPoints (ocv_semantics.c), OpenCV 3.2 cvUndistortPoints with R = I, P = K;
+ * Frame::UndistortKeyPoints / ComputeImageBounds (stereo.c), Frame.cc:404-464 ------------
+ * src/dst: n (x, y) float pairs; k: 8 double coefficients; has_dist = 0 runs one iteration
+ * with k = 0 (no distortion).  bounds: minX, maxX, minY, maxY, grid width/height inverses. */
+void  ora_undistort_points(const float* src, int n, const float K[9], const double k[8], int has_dist, float* dst);
+void  ora_undistort_keypoints(const ora_kp* keys, int N, const float K[9], const float* dist, int ndist,
+                              ora_kp* keysUn);
+void  ora_compute_image_bounds(int cols, int rows, const float K[9], const float* dist, int ndist, float bounds[6]);
+
 /* ---- Frame::ComputeStereoMatches (stereo.c), reference Frame.cc:466-640 ----------
  * kL/dL: left mvKeys + descriptors (NL), kR/dR: right (NR); exL/exR: the extractors that
  * produced them (their last pyramids); rows0 = level-0 rows.  Writes mvuRight / mvDepth

@@ -175,3 +175,55 @@ void ora_unproject_stereo(const ora_kp* kps, const float* depth, int N, const fl
         }
     }
 }
+
+/* mDistCoef (4, 5 or 8 floats) -> the double k[8] cvUndistortPoints works with (cvConvert). */
+static void dist_to_k(const float* dist, int ndist, double k[8])
+{
+    for (int i = 0; i < 8; i++) k[i] = i < ndist ? (double)dist[i] : 0.0;
+}
+
+/* Frame::UndistortKeyPoints, Frame.cc:404-430: mvKeysUn = mvKeys when mDistCoef.at<float>(0)
+ * is 0 (the other coefficients are not looked at); otherwise every keypoint's pt goes through
+ * cv::undistortPoints(mat, mat, mK, mDistCoef, Mat(), mK) and the rest of the KeyPoint is
+ * copied. */
+void ora_undistort_keypoints(const ora_kp* keys, int N, const float K[9], const float* dist, int ndist,
+                             ora_kp* keysUn)
+{
+    for (int i = 0; i < N; i++) keysUn[i] = keys[i];
+    if (dist[0] == 0.0f) return;
+    double k[8];
+    dist_to_k(dist, ndist, k);
+    for (int i = 0; i < N; i++) {
+        const float src[2] = {keys[i].x, keys[i].y};
+        float dst[2];
+        ora_undistort_points(src, 1, K, k, 1, dst);
+        keysUn[i].x = dst[0];
+        keysUn[i].y = dst[1];
+    }
+}
+
+/* Frame::ComputeImageBounds, Frame.cc:432-464, and the grid factors of the Frame constructors
+ * (mfGridElementWidthInv = FRAME_GRID_COLS / (mnMaxX - mnMinX), Frame.cc:97-98): bounds[0..5] =
+ * mnMinX, mnMaxX, mnMinY, mnMaxY, mfGridElementWidthInv, mfGridElementHeightInv. */
+void ora_compute_image_bounds(int cols, int rows, const float K[9], const float* dist, int ndist, float bounds[6])
+{
+    if (dist[0] != 0.0f) {
+        const float c[8] = {0.0f, 0.0f, (float)cols, 0.0f, 0.0f, (float)rows, (float)cols, (float)rows};
+        float u[8];
+        double k[8];
+        dist_to_k(dist, ndist, k);
+        ora_undistort_points(c, 4, K, k, 1, u);
+        /* std::min(a, b) = b < a ? b : a; std::max(a, b) = a < b ? b : a */
+        bounds[0] = u[4] < u[0] ? u[4] : u[0];
+        bounds[1] = u[2] < u[6] ? u[6] : u[2];
+        bounds[2] = u[3] < u[1] ? u[3] : u[1];
+        bounds[3] = u[5] < u[7] ? u[7] : u[5];
+    } else {
+        bounds[0] = 0.0f;
+        bounds[1] = (float)cols;
+        bounds[2] = 0.0f;
+        bounds[3] = (float)rows;
+    }
+    bounds[4] = (float)64 / (float)(bounds[1] - bounds[0]);
+    bounds[5] = (float)48 / (float)(bounds[3] - bounds[2]);
+}

@@ -161,6 +161,41 @@ def oracle_unproject_stereo(kps, depth, Twc, fx, fy, cx, cy):
     return x3D[:n], mp[:n]
 
 
+def oracle_undistort_keypoints(keys, K, dist):
+    """Frame::UndistortKeyPoints (Frame.cc:404-430) restated (oracle/stereo.c, ocv_semantics.c)."""
+    L = lib()
+    L.ora_undistort_keypoints.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    keys = np.ascontiguousarray(keys, KP_DTYPE)
+    K = np.ascontiguousarray(K, np.float32).reshape(-1)
+    dist = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    out = np.zeros(max(len(keys), 1), KP_DTYPE)
+    L.ora_undistort_keypoints(ptr(keys), len(keys), ptr(K), ptr(dist), int(dist.size), ptr(out))
+    return out[:len(keys)]
+
+
+def oracle_undistort_points(pts, K, k8, has_dist=True):
+    """cv::undistortPoints(pts, pts, K, D, Mat(), K) restated (OpenCV 3.2 cvUndistortPoints)."""
+    L = lib()
+    L.ora_undistort_points.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+    K = np.ascontiguousarray(K, np.float32).reshape(-1)
+    k = np.zeros(8, np.float64)
+    k[:len(k8)] = k8
+    out = np.zeros_like(pts)
+    L.ora_undistort_points(ptr(pts), len(pts), ptr(K), ptr(k), int(bool(has_dist)), ptr(out))
+    return out
+
+
+def oracle_compute_image_bounds(cols, rows, K, dist):
+    L = lib()
+    L.ora_compute_image_bounds.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    K = np.ascontiguousarray(K, np.float32).reshape(-1)
+    dist = np.ascontiguousarray(dist, np.float32).reshape(-1)
+    b = np.zeros(6, np.float32)
+    L.ora_compute_image_bounds(int(cols), int(rows), ptr(K), ptr(dist), int(dist.size), ptr(b))
+    return tuple(np.float32(v) for v in b)
+
+
 class OracleVocabulary:
     """TemplatedVocabulary (Thirdparty/DBoW2) restated on CPU: loadFromTextFile, transform, score."""
 

@@ -141,3 +141,28 @@ def test_batched_pairs_equal_single(gpu, kitti_frames):
     assert rc == 0
     for p in range(2):
         assert nm[p] == singles[p][0] and np.array_equal(outs[p], singles[p][1])
+
+
+@pytest.mark.parametrize("frac", [0.6, 1.0])
+def test_search_by_projection_clustered_cell(gpu, kitti_frames, frac):
+    """Many keypoints in one grid cell (AssignFeaturesToGrid, Frame.cc:230-245): the device grid
+    keeps index order inside a crowded cell, so GetFeaturesInArea enumerates (and breaks
+    distance ties) as the reference does."""
+    frames, Hs, Rs, res, scale = kitti_frames
+    K4 = synthetic.intrinsics(1241, 376)
+    rng = np.random.default_rng(int(frac * 10) + 5)
+    (k0, d0), (k1, d1) = res[0], res[1]
+    k1 = k1.copy()
+    sel = rng.random(len(k1)) < frac
+    k1["x"][sel] = rng.uniform(620.0, 629.0, sel.sum()).astype(np.float32)   # grid cell (32, 24)
+    k1["y"][sel] = rng.uniform(187.8, 191.0, sel.sum()).astype(np.float32)
+    d1 = d1.copy()
+    d1[sel] = d0[rng.integers(0, len(d0), sel.sum())]   # equal descriptors: many distance ties
+    cur, last, mps, last_mp, last_out = frame_pair(k0, d0, k1, d1, Rs[0], K4, 1241, 376, scale, rng)
+    m = gpu.ORBmatcher(0.9, True)
+    for th in (15.0, 100.0):
+        g = np.full(cur.N, -1, np.int32)
+        o = g.copy()
+        ng = m.SearchByProjection_LastFrame(cur, g, last, k0, last_mp, last_out, mps, th, True)
+        no = oracle_lib.oracle_search_last(cur, o, last, k0, last_mp, last_out, mps, th, True, 0.9, True)
+        assert ng == no and np.array_equal(g, o), (th, ng, no)

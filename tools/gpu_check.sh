@@ -32,7 +32,7 @@ echo "[gpu_check] bench" && date
 timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
 echo "[gpu_check] rocprofv3" && date
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o bench -- python3 "$R/bench.py" --no-cpu-baseline \
+ORBGPU_LBA_STREAMS=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o bench -- python3 "$R/bench.py" --no-cpu-baseline \
   > "$OUT/prof_bench.log" 2>&1 || { tail -30 "$OUT/prof_bench.log"; exit 1; }
 python3 tools/prof_csv.py "$(find "$OUT/prof" -name '*kernel_stats.csv' | head -1)" 60 > "$OUT/kernel_stats.txt"
 python3 tools/roofline_check.py "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)" "$OUT/bench.json" | tee "$OUT/roofline_check.json"
