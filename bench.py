@@ -672,7 +672,7 @@ def main():
     if os.environ.get("ORBGPU_PROF_DUMP"):   # instrumented build (make prof): k_select section timers
         buf = (C.c_ulonglong * 32)()
         L.orbgpu_debug_prof_match(buf)
-        print("k_select sections (cycles, problem 0, summed over the timed steps):", list(buf)[:8], file=sys.stderr)
+        print("k_select sections (cycles, problem 0, summed over the timed steps):", list(buf)[:16], file=sys.stderr)
     # the last timed chain's counts (its device work finished inside the timed region), then the
     # batch extracted by the last timed step, tracked outside it
     got += drain()[:1] if args.steps else []

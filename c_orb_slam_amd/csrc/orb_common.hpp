@@ -262,11 +262,14 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // Section timers for instrumented builds (make prof -> -DORBGPU_PROF): clock64() deltas of
 // workgroup 0 / thread 0 accumulated into g_orbgpu_prof[slot]; compiled out otherwise.
 #ifdef ORBGPU_PROF
+#ifndef ORBGPU_PROF_BLOCK
+#define ORBGPU_PROF_BLOCK 0   // the workgroup whose sections are timed
+#endif
 static __device__ unsigned long long g_orbgpu_prof[32];   // one copy per translation unit
 #define ORBGPU_PROF_START unsigned long long _orbgpu_pt = clock64()
 #define ORBGPU_PROF_MARK(i)                                                                   \
     do {                                                                                      \
-        if (blockIdx.x == 0 && threadIdx.x == 0) {                                            \
+        if (blockIdx.x == ORBGPU_PROF_BLOCK && threadIdx.x == 0) {                            \
             const unsigned long long _t = clock64();                                          \
             atomicAdd(&g_orbgpu_prof[i], _t - _orbgpu_pt);                                    \
             _orbgpu_pt = _t;                                                                  \
@@ -274,7 +277,7 @@ static __device__ unsigned long long g_orbgpu_prof[32];   // one copy per transl
     } while (0)
 #define ORBGPU_PROF_COUNT(i)                                                                  \
     do {                                                                                      \
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_orbgpu_prof[i], 1ull);          \
+        if (blockIdx.x == ORBGPU_PROF_BLOCK && threadIdx.x == 0) atomicAdd(&g_orbgpu_prof[i], 1ull); \
     } while (0)
 #else
 #define ORBGPU_PROF_START

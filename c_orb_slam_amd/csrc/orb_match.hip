@@ -7,13 +7,14 @@
 //                 parallel): projection, Frame::GetFeaturesInArea window over
 //                 the device grid, static filters, popcount distances, and the
 //                 kTopK smallest (dist, enumeration order) candidates;
-//   k_select      (one workgroup per problem): the sequential greedy replay,
+//   k_select_r    (one workgroup per problem): the sequential greedy replay,
 //                 solved as a parallel fixed-point iteration over the queries
 //                 (occupancy owners in LDS), with a full rescan only when every
 //                 kept candidate is already taken, then the rotation-consistency
 //                 histogram (ORBmatcher.cc:1447-1467).
 // k_build_grid rebuilds Frame::mGrid (AssignFeaturesToGrid, Frame.cc:230-245)
 // as a CSR in cell order (ix-major) with keypoint order kept inside a cell.
+#define ORBGPU_PROF_BLOCK 20   // prof builds: k_select_r sections of a mid-batch frame (full local map)
 #include "orb_match.hpp"
 
 #include <cstring>
@@ -52,11 +53,16 @@ __device__ __forceinline__ float gemm_row(const float* T, int r, float X0, float
 // O(sum of squared cell sizes / 256) LDS reads, a few per keypoint for ordinary frames, and still
 // spread over the whole workgroup when every keypoint lands in one cell).
 inline size_t grid_lds_bytes(int maxN) { return (((size_t)std::max(maxN, 1) * 4 + 4 + 15) & ~(size_t)15); }
-inline size_t select_lds_bytes(int maxN) { return ((size_t)std::max(maxN, 1) * 10 + 15) & ~(size_t)15; }
+inline size_t select_lds_bytes(int maxN) { return ((size_t)std::max(maxN, 1) * 11 + 15) & ~(size_t)15; }
 
 __device__ __forceinline__ int packed16(const uint32_t* a, int c) { return (int)((a[c >> 1] >> (16 * (c & 1))) & 0xffffu); }
 
-__global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs) {
+// dropOccupied (the greedy searches of run()): keypoints whose slot already holds a map point
+// with Observations() > 0 when the call starts are left out of the cells.  The reference skips
+// them as candidates (ORBmatcher.cc:87-89, 1403-1405), and a slot occupied at the start stays
+// occupied (the loops only fill empty or observation-less slots), so no query of the call can
+// take them; the remaining candidates keep their enumeration order.
+__global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs, int dropOccupied) {
     ORBGPU_LATENCY_WAVE();
     constexpr int kPer = kGridCells / 256;   // 12 cells per thread in the scan
     static_assert(kGridCells % 512 == 0, "packed pairs per thread");
@@ -77,7 +83,12 @@ __global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs) {
         const int px = (int)roundf((kp.x - F.minX) * F.gridWInv);
         const int py = (int)roundf((kp.y - F.minY) * F.gridHInv);
         int cell = -1;
-        if (!(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows)) {
+        bool occ = false;
+        if (dropOccupied) {
+            const int m = P.curMP[i];
+            occ = m >= 0 && P.mpObs[m] > 0;
+        }
+        if (!(px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) && !occ) {
             cell = px * kGridRows + py;
             atomicAdd(&s_cnt[cell >> 1], 1u << (16 * (cell & 1)));
         }
@@ -415,7 +426,7 @@ __global__ void __launch_bounds__(256) k_frustum(const SearchDev* __restrict__ p
     if ((threadIdx.x & 63) == 0 && nv) atomicAdd(Fq.nvisible, nv);
 }
 
-// Greedy replay as a fixed-point iteration (one 256-thread workgroup per problem).
+// Greedy replay as a fixed-point iteration (one workgroup per problem).
 // The reference loop is sequential: query q may not take a keypoint that an earlier
 // query q' < q already took with Observations() > 0 (ORBmatcher.cc:87-89, 1403-1405).
 // Its outcome is the unique solution of
@@ -423,125 +434,226 @@ __global__ void __launch_bounds__(256) k_frustum(const SearchDev* __restrict__ p
 // and since choice(q) depends only on earlier queries, Jacobi iteration over all queries
 // in parallel reaches it: after round r every query whose dependency chain is shorter
 // than r is final, and a round that changes nothing is the fixed point.  Conflicts are
-// rare (a few per frame), so it converges in 2-4 rounds; each round is one owner[]
+// rare, so it converges in a few rounds (about 4 for SearchLocalPoints, 12 for the
+// last-frame search of the bench); each round is one owner[]
 // rebuild (atomicMin of the claiming query per keypoint, in LDS) plus one decide() per
 // query against the kTopK list, with a full rescan only when every kept candidate is
 // taken.  Overwrites (a later query re-taking a keypoint whose earlier taker has no
 // observations) keep the latest taker, as the reference's sequential assignment does.
-template <bool LAST, int NT>
-__global__ void __launch_bounds__(NT) k_select(const SearchDev* __restrict__ probs, float th, int bMono,
-                                                float nnratio, int checkOri, int Nmax) {
+constexpr int kSelQLast = 8, kSelQLocal = 4;   // register slots per thread of k_select_r
+static_assert(512 * kSelQLast >= kMaxFrameKeys, "LAST mode: every query of a frame in a register slot");
+
+// decide(q) from global memory only (the whole top-K list, then the rescan with occupancy): the
+// rare path of k_select_r, kept out of line so that its unrolled slots stay small
+template <bool LAST>
+__device__ __noinline__ int select_slow(const SearchDev* __restrict__ Pp, int q, int c, const uint8_t* s_occ0,
+                                        const int* s_owner, const uint8_t* s_oct, float th, int bF, int bB,
+                                        float nnratio) {
+    const SearchDev& P = *Pp;
+    auto occupied = [&](int idx) { return s_occ0[idx] != 0 || s_owner[idx] < q; };
+    const int kk = c < kTopK ? c : kTopK;
+    const int2* top = P.topk + (size_t)q * kTopK;
+    constexpr int need = LAST ? 1 : 2;
+    int bestDist = 256, bestIdx = -1, bestDist2 = 256, idx2 = -1, nfree = 0;
+    for (int k = 0; k < kk && nfree < need; k++) {
+        const int2 e = top[k];
+        if (occupied(e.y)) continue;
+        if (nfree == 0) { bestDist = e.x; bestIdx = e.y; }
+        else { bestDist2 = e.x; idx2 = e.y; }
+        nfree++;
+    }
+    if (nfree < need && c > kTopK) {
+        int2 top2[2];
+        bestDist = bestDist2 = 256;
+        bestIdx = idx2 = -1;
+        if (LAST) {
+            const LastQuery lq = last_query(P, q, th, bF != 0, bB != 0);
+            if (scan_last(P, lq, occupied, top2, 1) > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
+        } else {
+            const LocalQuery lq = local_query(P, q, th);
+            const int c2 = scan_local(P, lq, occupied, top2, 2);
+            if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
+            if (c2 > 1) { bestDist2 = top2[1].x; idx2 = top2[1].y; }
+        }
+    }
+    if (bestDist > TH_HIGH) return -1;
+    if (!LAST) {
+        const int bestLevel = s_oct[bestIdx];
+        const int bestLevel2 = idx2 >= 0 ? (int)s_oct[idx2] : -1;
+        if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) return -1;
+    }
+    return bestIdx;
+}
+
+// k_select_r: the fixed point above with the query state in registers.  The queries (all of
+// them, or SearchLocalPoints' in-view list) are dealt to the threads, Q per thread (slot s of
+// thread t = list entry t + s * NT); each slot holds its query's candidate count, observation
+// flag, current choice and first 4 kept candidates (dist << 16 | index), loaded once, so a
+// round touches only LDS (owners, initial occupancy, octaves).  A query whose first 4
+// candidates are all taken, and list entries beyond NT * Q, go through select_slow (global
+// memory).  A query's choice depends on the query order only through `owner < q`, so dealing
+// the queries to threads in any order is the same iteration.
+template <bool LAST, int NT, int Q>
+__global__ void __launch_bounds__(NT) k_select_r(const SearchDev* __restrict__ probs, float th, int bMono,
+                                                  float nnratio, int checkOri, int Nmax) {
     ORBGPU_LATENCY_WAVE();
-    // dynamic LDS, max N of the batch entries each (select_lds_bytes)
     extern __shared__ int s_dyn[];
     int* s_owner = s_dyn;                                           // earliest claiming query with Observations() > 0
     int* s_lastq = s_dyn + Nmax;                                    // latest claiming query (any)
     uint8_t* s_occ0 = reinterpret_cast<uint8_t*>(s_dyn + 2 * Nmax); // occupancy before this call
     uint8_t* s_rm = s_occ0 + Nmax;                                  // slot cleared by the rotation check
+    uint8_t* s_oct = s_rm + Nmax;                                   // keypoint octave
     __shared__ int s_hsz[HISTO_LENGTH];
     __shared__ int s_ind[3];
     __shared__ int s_changed, s_nm, s_rmcnt;
     ORBGPU_PROF_START;
-    const SearchDev P = probs[blockIdx.x];
+    const SearchDev* Pp = probs + blockIdx.x;
+    const SearchDev& P = *Pp;
     const int tid = threadIdx.x;
     const int N = P.cur.N, nq = P.nq;
+    const int* list = (!LAST && P.visList) ? P.visList : nullptr;
+    const int nact = list ? *P.visCount : nq;
     for (int i = tid; i < N; i += NT) {
         const int m = P.curMP[i];
         s_occ0[i] = (m >= 0 && P.mpObs[m] > 0) ? 1 : 0;
         s_owner[i] = INT_MAX;
         s_lastq[i] = -1;
         s_rm[i] = 0;
+        if (!LAST) s_oct[i] = (uint8_t)P.cur.keysUn[i].octave;
     }
     if (tid < HISTO_LENGTH) s_hsz[tid] = 0;
     if (tid == 0) { s_nm = 0; s_rmcnt = 0; }
     bool bF = false, bB = false;
     if (LAST) fwd_bwd(P, bMono != 0, bF, bB);
-    // per query: qinfo.x = candidate count (k_candidates), .y = current choice (-1 none), .z = obs flag
-    for (int q = tid; q < nq; q += NT) {
-        const int c = P.qinfo[q].x;
+    uint32_t tk[Q][4];
+    int qs[Q], cnt[Q], ch[Q];
+    uint32_t obsm = 0;
+    auto obs_of = [&](int q) {
         const int mp = LAST ? P.lastMP[q] : P.mpIndex[q];
-        P.qinfo[q].z = (c > 0 && mp >= 0 && P.mpObs[mp] > 0) ? 1 : 0;
-    }
-    __syncthreads();
-    ORBGPU_PROF_MARK(0);
-    // decide(q): the reference's choice for query q given the occupancy by earlier queries
-    auto decide = [&](int q) -> int {
-        const int cnt = P.qinfo[q].x;
-        if (cnt <= 0) return -1;
-        auto occupied = [&](int idx) { return s_occ0[idx] != 0 || s_owner[idx] < q; };
-        const int kk = cnt < kTopK ? cnt : kTopK;
-        const int2* top = P.topk + (size_t)q * kTopK;
-        int bestDist = 256, bestIdx = -1, bestDist2 = 256, idx2 = -1, nfree = 0;
-        for (int k = 0; k < kk && nfree < (LAST ? 1 : 2); k++) {
-            const int2 e = top[k];
-            if (occupied(e.y)) continue;
-            if (nfree == 0) { bestDist = e.x; bestIdx = e.y; }
-            else { bestDist2 = e.x; idx2 = e.y; }
-            nfree++;
-        }
-        if (nfree < (LAST ? 1 : 2) && cnt > kTopK) {
-            // every kept candidate that could decide is taken: rescan with occupancy (rare)
-            int2 top2[2];
-            bestDist = bestDist2 = 256;
-            bestIdx = idx2 = -1;
-            if (LAST) {
-                const LastQuery lq = last_query(P, q, th, bF, bB);
-                if (scan_last(P, lq, occupied, top2, 1) > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
-            } else {
-                const LocalQuery lq = local_query(P, q, th);
-                const int c2 = scan_local(P, lq, occupied, top2, 2);
-                if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
-                if (c2 > 1) { bestDist2 = top2[1].x; idx2 = top2[1].y; }
+        return mp >= 0 && P.mpObs[mp] > 0;
+    };
+#pragma unroll
+    for (int s = 0; s < Q; s++) {
+        const int k = tid + s * NT;
+        qs[s] = k < nact ? (list ? list[k] : k) : -1;
+        cnt[s] = -1;
+        ch[s] = -1;
+#pragma unroll
+        for (int j = 0; j < 4; j++) tk[s][j] = 0u;
+        if (qs[s] >= 0) {
+            const int q = qs[s];
+            const int c = P.qinfo[q].x;
+            cnt[s] = c;
+            if (c > 0) {
+                if (obs_of(q)) obsm |= 1u << s;
+                const int4* t4 = reinterpret_cast<const int4*>(P.topk + (size_t)q * kTopK);
+                const int4 a = t4[0], b = t4[1];   // entries >= min(c, kTopK) are never read
+                tk[s][0] = ((uint32_t)a.x << 16) | (uint32_t)a.y;
+                tk[s][1] = ((uint32_t)a.z << 16) | (uint32_t)a.w;
+                tk[s][2] = ((uint32_t)b.x << 16) | (uint32_t)b.y;
+                tk[s][3] = ((uint32_t)b.z << 16) | (uint32_t)b.w;
             }
         }
+    }
+    __syncthreads();
+    ORBGPU_PROF_MARK(LAST ? 0 : 8);
+    constexpr int need = LAST ? 1 : 2;
+    auto decide = [&](int s) -> int {   // decide(q) for slot s
+        const int q = qs[s];
+        const int c = cnt[s];
+        if (c <= 0) return -1;
+        const int kk = c < kTopK ? c : kTopK;
+        int bestDist = 256, bestIdx = -1, bestDist2 = 256, idx2 = -1, nfree = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (j < kk && nfree < need) {
+                const int idx = (int)(tk[s][j] & 0xffffu), d = (int)(tk[s][j] >> 16);
+                if (!(s_occ0[idx] != 0 || s_owner[idx] < q)) {
+                    if (nfree == 0) { bestDist = d; bestIdx = idx; }
+                    else { bestDist2 = d; idx2 = idx; }
+                    nfree++;
+                }
+            }
+        }
+        if (nfree < need && kk > 4)   // the first 4 kept candidates are taken: the rest of the list
+            return select_slow<LAST>(Pp, q, c, s_occ0, s_owner, s_oct, th, bF, bB, nnratio);
         if (bestDist > TH_HIGH) return -1;
         if (!LAST) {
-            const int bestLevel = P.cur.keysUn[bestIdx].octave;
-            const int bestLevel2 = idx2 >= 0 ? P.cur.keysUn[idx2].octave : -1;
+            const int bestLevel = s_oct[bestIdx];
+            const int bestLevel2 = idx2 >= 0 ? (int)s_oct[idx2] : -1;
             if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) return -1;
         }
         return bestIdx;
     };
-    for (int q = tid; q < nq; q += NT) P.qinfo[q].y = decide(q);   // round 0: nothing claimed yet
+    // list entries beyond the register slots: choice in qinfo.y, obs flag in qinfo.z
+    auto decide_g = [&](int q) -> int {
+        const int c = P.qinfo[q].x;
+        return c > 0 ? select_slow<LAST>(Pp, q, c, s_occ0, s_owner, s_oct, th, bF, bB, nnratio) : -1;
+    };
+    for (int k = NT * Q + tid; k < nact; k += NT) {
+        const int q = list ? list[k] : k;
+        P.qinfo[q].z = (P.qinfo[q].x > 0 && obs_of(q)) ? 1 : 0;
+        P.qinfo[q].y = decide_g(q);
+    }
+#pragma unroll
+    for (int s = 0; s < Q; s++) ch[s] = decide(s);   // round 0: nothing claimed yet
     for (int round = 0; round <= nq; round++) {
         __syncthreads();
         for (int i = tid; i < N; i += NT) s_owner[i] = INT_MAX;
         if (tid == 0) s_changed = 0;
         __syncthreads();
-        for (int q = tid; q < nq; q += NT) {
+#pragma unroll
+        for (int s = 0; s < Q; s++)
+            if (ch[s] >= 0 && ((obsm >> s) & 1u)) atomicMin(&s_owner[ch[s]], qs[s]);
+        for (int k = NT * Q + tid; k < nact; k += NT) {
+            const int q = list ? list[k] : k;
             const int4 qi = P.qinfo[q];
             if (qi.y >= 0 && qi.z) atomicMin(&s_owner[qi.y], q);
         }
         __syncthreads();
-        bool ch = false;
-        for (int q = tid; q < nq; q += NT) {
-            const int c = decide(q);
-            if (c != P.qinfo[q].y) { P.qinfo[q].y = c; ch = true; }
+        bool chg = false;
+#pragma unroll
+        for (int s = 0; s < Q; s++) {
+            const int c = decide(s);
+            if (c != ch[s]) { ch[s] = c; chg = true; }
         }
-        if (ch) s_changed = 1;
+        for (int k = NT * Q + tid; k < nact; k += NT) {
+            const int q = list ? list[k] : k;
+            const int c = decide_g(q);
+            if (c != P.qinfo[q].y) { P.qinfo[q].y = c; chg = true; }
+        }
+        if (chg) s_changed = 1;
         __syncthreads();
+        ORBGPU_PROF_COUNT(LAST ? 6 : 14);
         if (!s_changed) break;
     }
-    ORBGPU_PROF_MARK(1);
-    // the fixed point: takes, latest taker per keypoint, match count
+    ORBGPU_PROF_MARK(LAST ? 1 : 9);
     int nm = 0;
-    for (int q = tid; q < nq; q += NT) {
+#pragma unroll
+    for (int s = 0; s < Q; s++)
+        if (ch[s] >= 0) { atomicMax(&s_lastq[ch[s]], qs[s]); nm++; }
+    for (int k = NT * Q + tid; k < nact; k += NT) {
+        const int q = list ? list[k] : k;
         const int c = P.qinfo[q].y;
         if (c >= 0) { atomicMax(&s_lastq[c], q); nm++; }
     }
     atomicAdd(&s_nm, nm);
     __syncthreads();
     if (LAST && checkOri) {
-        // rotation-consistency histogram over the matches (ORBmatcher.cc:1422-1467)
-        for (int q = tid; q < nq; q += NT) {
-            const int bi = P.qinfo[q].y;
+        // rotation-consistency histogram over the matches (ORBmatcher.cc:1422-1467); LAST mode
+        // has no list beyond the slots (nq <= kMaxFrameKeys <= NT * Q, checked by the host)
+        int bins[Q];
+#pragma unroll
+        for (int s = 0; s < Q; s++) {
+            bins[s] = -1;
+            const int bi = ch[s];
             if (bi < 0) continue;
-            float rot = P.last.keysUn[q].angle - P.cur.keysUn[bi].angle;
+            float rot = P.last.keysUn[qs[s]].angle - P.cur.keysUn[bi].angle;
             if (rot < 0.0f) rot += 360.0f;
             int bin = (int)roundf(rot * (1.0f / HISTO_LENGTH));
             if (bin == HISTO_LENGTH) bin = 0;
             atomicAdd(&s_hsz[bin], 1);
-            P.hist[q] = make_int2(bin, bi);
+            bins[s] = bin;
         }
         __syncthreads();
         if (tid == 0) {
@@ -562,25 +674,26 @@ __global__ void __launch_bounds__(NT) k_select(const SearchDev* __restrict__ pro
         __syncthreads();
         const int ind1 = s_ind[0], ind2 = s_ind[1], ind3 = s_ind[2];
         int removed = 0;
-        for (int q = tid; q < nq; q += NT) {
-            if (P.qinfo[q].y < 0) continue;
-            const int2 h = P.hist[q];
-            if (h.x != ind1 && h.x != ind2 && h.x != ind3) {
-                s_rm[h.y] = 1;
+#pragma unroll
+        for (int s = 0; s < Q; s++) {
+            if (ch[s] < 0) continue;
+            const int b = bins[s];
+            if (b != ind1 && b != ind2 && b != ind3) {
+                s_rm[ch[s]] = 1;
                 removed++;
             }
         }
         atomicAdd(&s_rmcnt, removed);
     }
     __syncthreads();
-    ORBGPU_PROF_MARK(2);
+    ORBGPU_PROF_MARK(LAST ? 2 : 10);
     for (int i = tid; i < N; i += NT) {
         const int lq = s_lastq[i];
         if (s_rm[i]) P.curMP[i] = -1;
         else if (lq >= 0) P.curMP[i] = LAST ? P.lastMP[lq] : P.mpIndex[lq];
     }
     if (tid == 0) *P.nmatches = s_nm - s_rmcnt;
-    ORBGPU_PROF_MARK(3);
+    ORBGPU_PROF_MARK(LAST ? 3 : 11);
 }
 
 // CSR candidate mode: one wave per query, lanes over candidates; (dist<<20 | k)
@@ -678,7 +791,7 @@ int Matcher::area_candidates(const SearchDev& frame, const AreaQuery* d_q, int n
     s += (((size_t)nq + 1) * 4 + 255) & ~(size_t)255;
     SearchDev* dp = (SearchDev*)s;
     ORB_HIP_CHECK(hipMemcpyAsync(dp, &P, sizeof(SearchDev), hipMemcpyHostToDevice, stream_));
-    hipLaunchKernelGGL(k_build_grid, dim3(1), dim3(256), grid_lds_bytes(frame.cur.N), stream_, dp);
+    hipLaunchKernelGGL(k_build_grid, dim3(1), dim3(256), grid_lds_bytes(frame.cur.N), stream_, dp, 0);
     if (nq == 0) return hipStreamSynchronize(stream_) == hipSuccess ? 0 : -2;
     hipLaunchKernelGGL(k_area_count, dim3((nq + 255) / 256), dim3(256), 0, stream_, dp, d_q, nq, d_cnt);
     ORB_HIP_CHECK(hipGetLastError());
@@ -802,24 +915,24 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
         if (int e = zero_counters(0, 2)) return e;
         mark(0);
     }
-    hipLaunchKernelGGL(k_build_grid, dim3(np), dim3(256), grid_lds_bytes(maxN), stream_, dp);
+    hipLaunchKernelGGL(k_build_grid, dim3(np), dim3(256), grid_lds_bytes(maxN), stream_, dp, 1);
     mark(1);
     if (maxq > 0) {
         if (lastMode) {
             hipLaunchKernelGGL(k_candidates<true>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, (int)bMono,
                                counters());
             mark(2);
-            hipLaunchKernelGGL((k_select<true, 256>), dim3(np), dim3(256), select_lds_bytes(maxN), stream_, dp, th, (int)bMono,
-                               nnratio_, (int)checkOri_, maxN);
+            // nq = the last frame's N <= kMaxFrameKeys = 512 * kSelQLast: every query in a slot
+            hipLaunchKernelGGL((k_select_r<true, 512, kSelQLast>), dim3(np), dim3(512), select_lds_bytes(maxN), stream_, dp,
+                               th, (int)bMono, nnratio_, (int)checkOri_, maxN);
         } else {
             hipLaunchKernelGGL(k_candidates<false>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0,
                                counters());
             mark(2);
             // SearchLocalPoints-sized query sets (thousands of local map points, long occupancy
             // chains between duplicated points): 16 waves per round of the fixed point
-            hipLaunchKernelGGL((k_select<false, kSelectLocalThreads>), dim3(np), dim3(kSelectLocalThreads),
-                               select_lds_bytes(maxN), stream_, dp, th, 0,
-                               nnratio_, 0, maxN);
+            hipLaunchKernelGGL((k_select_r<false, kSelectLocalThreads, kSelQLocal>), dim3(np), dim3(kSelectLocalThreads),
+                               select_lds_bytes(maxN), stream_, dp, th, 0, nnratio_, 0, maxN);
         }
     } else {
         mark(2);
