@@ -279,59 +279,73 @@ __device__ __forceinline__ void mask_scan64(const uint64_t* masks, int n, int* o
     if (lane == 63) off[64] = incl;
 }
 
-// One workgroup (4 waves) per (cell, image); every pixel loop is division-free.
-//   stage    ROI rows as aligned dwords into LDS (3 rows per wave instruction)
-//   pretest  FAST-9 necessary condition at min(iniTh, minTh) per detection pixel, two rows per
-//            wave instruction when the cell is <= 32 columns wide; per-row survivor masks
-//   list     survivors in raster order (row-count scan), ~10 % of the pixels
+__device__ __forceinline__ int sel4(int k, int a0, int a1, int a2, int a3) {
+    return k == 0 ? a0 : k == 1 ? a1 : k == 2 ? a2 : a3;
+}
+
+// One workgroup (4 waves) per (cell group, image): up to 2 x 2 cells whose ROIs tile one union
+// ROI (CellGroup), so the staging, the syncs and the scans are shared by up to four cells.
+// Every pixel loop is division-free.
+//   stage    union ROI rows as aligned dwords into LDS (3 rows per wave instruction)
+//   pretest  FAST-9 necessary condition at min(iniTh, minTh) per detection pixel: lanes over
+//            the union's detection columns (<= 64), one ballot per detection row
+//   list     survivors, ~10 % of the pixels, cell by cell (TL, TR, BL, BR) and raster order
+//            inside a cell (row-count scans): cell k's are list entries [lb_k, lb_k+1)
 //   score    OpenCV cornerScore<16> for the list only (pixels failing the pretest score < th)
-//   NMS      list entries: keep = S >= th && S > every 8-neighbour's (S >= th ? S : 0);
-//            kept entries compacted in list (= raster) order by a chunk-count scan.
+//   NMS      per entry and for BOTH thresholds: keep = S >= th && S > every 8-neighbour's
+//            (S >= th ? S : 0) <=> S >= th && S > every 8-neighbour's S (one local-maximum test
+//            for both thresholds), a neighbour outside the entry's own cell counting 0 (the
+//            reference runs FAST on each cell's ROI alone, ORBextractor.cc:794-829)
+//   output   per cell: its iniTh keeps if it has any, else its minTh keeps (the retry of
+//            ORBextractor.cc:810-815), compacted in list order into the cell's slots
 __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ pyr, size_t img_bytes,
-                                                    const CellDesc* __restrict__ cells, int iniTh, int minTh,
+                                                    const CellGroup* __restrict__ groups, int iniTh, int minTh,
                                                     uint32_t* __restrict__ slots, size_t slots_per_image,
                                                     int* __restrict__ counts, int ncells,
                                                     const int* __restrict__ work) {
     __shared__ uint32_t s_img32[FC_MAXR * FC_LD / 4];
     __shared__ uint32_t s_sc32[FC_MAXR * FC_LD / 4];
     __shared__ uint16_t s_list[64 * 64];
-    __shared__ uint64_t s_mask[64];
-    __shared__ int s_off[65];
+    __shared__ uint64_t s_mask[64], s_khi[64];
+    __shared__ int s_off[65], s_offR[64];
+    __shared__ int s_lb[5];
     uint8_t* s_img = reinterpret_cast<uint8_t*>(s_img32);
     uint8_t* s_sc = reinterpret_cast<uint8_t*>(s_sc32);
-    // work order (Extractor::build_work): workgroup g runs on XCD g % 8; whole cell rows of an
-    // image go to one XCD (rows dealt round-robin), so horizontally adjacent cells -- which
+    uint64_t* s_klo = reinterpret_cast<uint64_t*>(s_img32);   // the ROI is dead after scoring
+    // work order (Extractor::build_work): workgroup g runs on XCD g % 8; whole group rows of an
+    // image go to one XCD (rows dealt round-robin), so horizontally adjacent groups -- which
     // share ROI halo columns and 128-B lines -- hit that XCD's L2 instead of being fetched
     // once per XCD, while every XCD still gets the same mix of levels
     ORBGPU_PROF_START;
     const int wk = work[blockIdx.x];
     if (wk < 0) return;   // padding of a shorter XCD list
-    const int cell = wk & 0xffff, b = wk >> 16;
-    const CellDesc cd = cells[cell];
-    const int rows = cd.r1 - cd.r0, cols = cd.c1 - cd.c0;
+    const int gi = wk & 0xffff, b = wk >> 16;
+    const CellGroup& g = groups[gi];
+    const int rows = g.rows, cols = g.cols, rs = g.rsplit, cs = g.csplit;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    int* cnt_out = counts + (size_t)b * ncells + cell;
-    if (rows < 7 || cols < 7) {
-        if (tid == 0) *cnt_out = 0;
+    const int dr = max(rows - 6, 0), dc = max(cols - 6, 0);
+    int* cnt_out = counts + (size_t)b * ncells;
+    if (dr == 0 || dc == 0) {
+        if (tid < 4 && g.cell[tid] >= 0) cnt_out[g.cell[tid]] = 0;
         return;
     }
     // ROI rows staged as aligned dwords: pixel (r, c) sits at LDS byte r*FC_LD + mis + c
-    const uint8_t* P = pyr + (size_t)b * img_bytes + cd.lvl_off + (size_t)(kEdge + cd.r0) * cd.pitch + kEdge + cd.c0;
+    const uint8_t* P = pyr + (size_t)b * img_bytes + g.lvl_off + (size_t)(kEdge + g.r0) * g.pitch + kEdge + g.c0;
     const int mis = (int)((uintptr_t)P & 3);
     const uint32_t* P32 = reinterpret_cast<const uint32_t*>(P - mis);
     constexpr int ldw = FC_LD / 4;
-    const int wpr = (cols + mis + 3) >> 2, pw = cd.pitch >> 2;
+    const int wpr = (cols + mis + 3) >> 2, pw = g.pitch >> 2;
     {
         // 3 rows x 19 dwords per wave instruction; rows wid*3 + rr + 12k (k < 6 covers FC_MAXR):
         // every load of the thread is issued before the first LDS store (one wait, not six)
         const int rr = lane / ldw, w = lane - rr * ldw;
         const bool ok = rr < 3 && w < wpr;
-        const uint32_t* g = P32 + (size_t)(wid * 3 + rr) * pw + w;
+        const uint32_t* gp = P32 + (size_t)(wid * 3 + rr) * pw + w;
         uint32_t v[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) {
             const int r = wid * 3 + rr + 12 * k;
-            v[k] = (ok && r < rows) ? g[(size_t)12 * k * pw] : 0u;
+            v[k] = (ok && r < rows) ? gp[(size_t)12 * k * pw] : 0u;
         }
 #pragma unroll
         for (int k = 0; k < 6; k++) {
@@ -342,31 +356,46 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     for (int i = tid; i < rows * ldw; i += 256) s_sc32[i] = 0u;
     __syncthreads();
     ORBGPU_PROF_MARK(0);
-    const int dr = rows - 6, dc = cols - 6;
     const int tp = min(iniTh, minTh);
-    // detection pixels flattened in raster order, 64 per wave instruction (all lanes busy for
-    // any cell width): pixel p = i * dc + j of chunk p >> 6; i = floor((p + 0.5) / dc) is exact
-    // in float for p < 4096, dc <= 64 (the fraction stays >= 1/128 from an integer)
-    const int npx = dr * dc, nchk = (npx + 63) >> 6;
-    const float inv_dc = 1.0f / (float)dc;
-    for (int ch = wid; ch < nchk; ch += 4) {
-        const int px = ch * 64 + lane;
-        const int i = (int)(((float)px + 0.5f) * inv_dc), j = px - i * dc;
-        const bool pass = px < npx && (tp < 1 || fast_pretest(&s_img[(3 + i) * FC_LD + mis + 3 + j], FC_LD, tp));
+    // detection columns on the lanes (dc <= 64: the union ROI is <= FC_MAXR wide), detection rows
+    // over the waves; row i's survivor mask is one ballot, its left-cell bits the low cs bits
+    const uint64_t Lm = cs >= 64 ? ~0ull : ((1ull << cs) - 1ull);
+    for (int i = wid; i < dr; i += 4) {
+        const bool pass = lane < dc && (tp < 1 || fast_pretest(&s_img[(3 + i) * FC_LD + mis + 3 + lane], FC_LD, tp));
         const uint64_t m = __ballot(pass);
-        if (lane == 0) s_mask[ch] = m;
+        if (lane == 0) s_mask[i] = m;
     }
     __syncthreads();
     ORBGPU_PROF_MARK(1);
-    if (wid == 0) mask_scan64(s_mask, nchk, s_off, lane);
+    // wave 0, lane = detection row: the list holds the TL cell's survivors in raster order, then
+    // TR's, BL's, BR's; row i's left (right) run starts at s_off[i] (s_offR[i])
+    if (wid == 0) {
+        const uint64_t m = lane < dr ? s_mask[lane] : 0ull;
+        const int cl = (int)__popcll(m & Lm), cr = (int)__popcll(m & ~Lm);
+        int il = cl, ir = cr;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int yl = __shfl_up(il, o, 64), yr = __shfl_up(ir, o, 64);
+            if (lane >= o) { il += yl; ir += yr; }
+        }
+        const int topL = rs > 0 ? __shfl(il, rs - 1, 64) : 0, topR = rs > 0 ? __shfl(ir, rs - 1, 64) : 0;
+        const int allL = __shfl(il, 63, 64), allR = __shfl(ir, 63, 64);
+        const int el = il - cl, er = ir - cr;
+        const bool bot = lane >= rs;
+        s_off[lane] = bot ? topR + el : el;
+        s_offR[lane] = bot ? allL + er : topL + er;
+        if (lane == 0) {
+            s_lb[0] = 0; s_lb[1] = topL; s_lb[2] = topL + topR; s_lb[3] = allL + topR; s_lb[4] = allL + allR;
+        }
+    }
     __syncthreads();
-    const int nl = s_off[64];
-    for (int ch = wid; ch < nchk; ch += 4) {
-        const uint64_t m = s_mask[ch];
+    const int nl = s_lb[4];
+    for (int i = wid; i < dr; i += 4) {
+        const uint64_t m = s_mask[i];
         if ((m >> lane) & 1ull) {
-            const int px = ch * 64 + lane;
-            const int i = (int)(((float)px + 0.5f) * inv_dc), j = px - i * dc;
-            s_list[s_off[ch] + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(((3 + i) << 8) | (3 + j));
+            const uint64_t below = m & ((1ull << lane) - 1ull);
+            const int pos = lane < cs ? s_off[i] + (int)__popcll(below) : s_offR[i] + (int)__popcll(below & ~Lm);
+            s_list[pos] = (uint16_t)(((3 + i) << 8) | (3 + lane));
         }
     }
     __syncthreads();
@@ -377,56 +406,82 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     }
     __syncthreads();
     ORBGPU_PROF_MARK(2);
-    uint32_t* out = slots + (size_t)b * slots_per_image + cd.slot_off;
     const int nch = (nl + 63) >> 6;
-    int th = iniTh;
-    for (int pass = 0; pass < 2; pass++) {
-        for (int ch = wid; ch < nch; ch += 4) {
-            const int k = ch * 64 + lane;
-            bool keep = false;
-            if (k < nl) {
-                const int rc = s_list[k], r = rc >> 8, cc = rc & 0xff;
-                const int s = s_sc[r * FC_LD + cc];
-                if (s >= th) {
-                    keep = true;
-#pragma unroll
-                    for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                        for (int dx = -1; dx <= 1; dx++) {
-                            if (!dx && !dy) continue;
-                            int n = s_sc[(r + dy) * FC_LD + cc + dx];
-                            n = n >= th ? n : 0;
-                            keep = keep && (s > n);
-                        }
-                }
-            }
-            const uint64_t m = __ballot(keep);
-            if (lane == 0) s_mask[ch] = m;
+    for (int ch = wid; ch < nch; ch += 4) {
+        const int k = ch * 64 + lane;
+        bool khi = false, klo = false;
+        if (k < nl) {
+            const int rc = s_list[k], r = rc >> 8, cc = rc & 0xff;
+            const int s = s_sc[r * FC_LD + cc];
+            const bool bot = r >= 3 + rs, rgt = cc >= 3 + cs;
+            // the entry's own cell: detection rows [rlo, rhi), columns [clo, chi)
+            const int rlo = bot ? 3 + rs : 3, rhi = bot ? 3 + dr : 3 + rs;
+            const int clo = rgt ? 3 + cs : 3, chi = rgt ? 3 + dc : 3 + cs;
+            const bool up = r - 1 >= rlo, dn = r + 1 < rhi, lf = cc - 1 >= clo, rt = cc + 1 < chi;
+            const uint8_t* q = &s_sc[r * FC_LD + cc];
+            const int n0 = (up && lf) ? q[-FC_LD - 1] : 0, n1 = up ? q[-FC_LD] : 0, n2 = (up && rt) ? q[-FC_LD + 1] : 0;
+            const int n3 = lf ? q[-1] : 0, n4 = rt ? q[1] : 0;
+            const int n5 = (dn && lf) ? q[FC_LD - 1] : 0, n6 = dn ? q[FC_LD] : 0, n7 = (dn && rt) ? q[FC_LD + 1] : 0;
+            // for s >= th a neighbour below th (stored as 0 in the reference's score row) is below
+            // s as well, so S > (n >= th ? n : 0) for every n <=> S > max n: one comparison
+            // serves both thresholds
+            const bool lmax = s > max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
+            khi = lmax && s >= iniTh;
+            klo = lmax && s >= minTh;
         }
-        __syncthreads();
-        if (wid == 0) mask_scan64(s_mask, nch, s_off, lane);
-        __syncthreads();
-        const int total = s_off[64];
-        if (total > 0 || pass == 1) {
-            for (int ch = wid; ch < nch; ch += 4) {
-                const uint64_t m = s_mask[ch];
-                if ((m >> lane) & 1ull) {
-                    const int pos = s_off[ch] + __popcll(m & ((1ull << lane) - 1ull));
-                    if (pos < cd.cap) {
-                        const int rc = s_list[ch * 64 + lane], r = rc >> 8, cc = rc & 0xff;
-                        const uint32_t sv = s_sc[r * FC_LD + cc];
-                        const uint32_t xr = (uint32_t)(cc + cd.offx), yr = (uint32_t)(r + cd.offy);
-                        out[pos] = (sv << 24) | (yr << 12) | xr;
-                    }
-                }
-            }
-            if (tid == 0) *cnt_out = min(total, cd.cap);
-            ORBGPU_PROF_MARK(3);
-            break;
-        }
-        th = minTh;
-        __syncthreads();   // s_mask / s_off are rewritten by the second pass
+        const uint64_t mh = __ballot(khi), ml = __ballot(klo);
+        if (lane == 0) { s_khi[ch] = mh; s_klo[ch] = ml; }
     }
+    __syncthreads();
+    // wave 0, lane = list chunk: cell k keeps its iniTh corners if it has any; the chosen keeps
+    // (fin) are scanned over the chunks.  The list is cell-major, so the keeps before cell k's
+    // first entry are the keeps of cells < k.
+    if (wid == 0) {
+        const uint64_t h = lane < nch ? s_khi[lane] : 0ull, lo = lane < nch ? s_klo[lane] : 0ull;
+        uint64_t fin = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int a = s_lb[k] - lane * 64, e = s_lb[k + 1] - lane * 64;   // chunk-relative range
+            const uint64_t ma = a <= 0 ? ~0ull : a >= 64 ? 0ull : ~((1ull << a) - 1ull);
+            const uint64_t me = e <= 0 ? 0ull : e >= 64 ? ~0ull : ((1ull << e) - 1ull);
+            const uint64_t mk = ma & me;
+            const bool hi = __ballot((h & mk) != 0ull) != 0ull;
+            fin |= mk & (hi ? h : lo);
+        }
+        if (lane < 64) s_mask[lane] = fin;
+        const int cnt = (int)__popcll(fin);
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        s_off[lane] = incl - cnt;
+        if (lane == 63) s_off[64] = incl;
+    }
+    __syncthreads();
+    // keeps before list position p
+    auto before = [&](int p) {
+        const int c = p >> 6, o = p & 63;
+        return s_off[c] + (o ? (int)__popcll(s_mask[c] & ((1ull << o) - 1ull)) : 0);
+    };
+    if (tid < 4 && g.cell[tid] >= 0) cnt_out[g.cell[tid]] = min(before(s_lb[tid + 1]) - before(s_lb[tid]), g.cap[tid]);
+    uint32_t* out = slots + (size_t)b * slots_per_image;
+    for (int ch = wid; ch < nch; ch += 4) {
+        const uint64_t m = s_mask[ch];
+        if ((m >> lane) & 1ull) {
+            const int rc = s_list[ch * 64 + lane], r = rc >> 8, cc = rc & 0xff;
+            const int k = (r >= 3 + rs) * 2 + (cc >= 3 + cs);
+            const int pos = s_off[ch] + __popcll(m & ((1ull << lane) - 1ull)) - before(sel4(k, s_lb[0], s_lb[1], s_lb[2], s_lb[3]));
+            if (pos < sel4(k, g.cap[0], g.cap[1], g.cap[2], g.cap[3])) {
+                const uint32_t sv = s_sc[r * FC_LD + cc];
+                const uint32_t xr = (uint32_t)(cc + sel4(k, g.xadd[0], g.xadd[1], g.xadd[2], g.xadd[3]));
+                const uint32_t yr = (uint32_t)(r + sel4(k, g.yadd[0], g.yadd[1], g.yadd[2], g.yadd[3]));
+                out[sel4(k, g.slot_off[0], g.slot_off[1], g.slot_off[2], g.slot_off[3]) + pos] = (sv << 24) | (yr << 12) | xr;
+            }
+        }
+    }
+    ORBGPU_PROF_MARK(3);
 }
 
 // Per image: concatenate the cell outputs of every level in cell order
@@ -623,13 +678,13 @@ Extractor::~Extractor() { release(); }
 
 void Extractor::release() {
     auto F = [](void* p) { if (p) (void)hipFree(p); };
-    F(d_in_); F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_work_);
+    F(d_in_); F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_work_); F(d_groups_);
     F(d_lcb_); F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_);
     F(d_kps_); F(d_desc_); F(d_jobsel_); F(d_jobcnt_); F(d_octlv_); F(d_gscr_); F(d_nout_); F(d_ptiles_);
     d_ptiles_ = nullptr;
     d_jobsel_ = d_jobcnt_ = d_octlv_ = d_gscr_ = d_nout_ = nullptr;
     d_in_ = d_pyr_ = d_blur_ = nullptr;
-    d_slots_ = nullptr; d_counts_ = nullptr; d_cells_ = nullptr; d_tiles_ = nullptr; d_work_ = nullptr;
+    d_slots_ = nullptr; d_counts_ = nullptr; d_cells_ = nullptr; d_tiles_ = nullptr; d_work_ = nullptr; d_groups_ = nullptr;
     work_B_ = -1;
     d_lcb_ = nullptr; d_packed_ = nullptr; d_hdr_ = nullptr; d_gtotal_ = nullptr; d_sel_ = nullptr;
     d_levels_ = nullptr; d_tabs_ = nullptr; d_kps_ = nullptr; d_desc_ = nullptr;
@@ -667,17 +722,18 @@ int Extractor::init_device(int maxW, int maxH, int maxBatch) {
     return 0;
 }
 
-// k_fast_cells work order for a batch of B images: the cell rows (cells sharing level and ROI
+// k_fast_cells work order for a batch of B images: the group rows (groups sharing level and ROI
 // top row, in cell order) of every image are dealt round-robin to the 8 XCDs; entry
-// g = slot * 8 + xcd of the table is the slot-th (b << 16 | cell) of that XCD's list, -1 past
+// g = slot * 8 + xcd of the table is the slot-th (b << 16 | group) of that XCD's list, -1 past
 // its end.
 int Extractor::build_work(int B) {
     constexpr int kXcds = 8;
-    const int ncells = (int)cells_.size();
+    const int ngroups = (int)groups_.size();
     std::vector<int> unit;
-    for (int c = 0; c < ncells; c++)
-        if (c == 0 || cells_[c].level != cells_[c - 1].level || cells_[c].r0 != cells_[c - 1].r0) unit.push_back(c);
-    unit.push_back(ncells);
+    for (int c = 0; c < ngroups; c++)
+        if (c == 0 || groups_[c].lvl_off != groups_[c - 1].lvl_off || groups_[c].r0 != groups_[c - 1].r0)
+            unit.push_back(c);
+    unit.push_back(ngroups);
     std::vector<std::vector<int>> lists(kXcds);
     long u = 0;
     for (int b = 0; b < B; b++)
@@ -806,6 +862,61 @@ int Extractor::setup_geometry(int W, int H) {
     level_cell_begin_[nlevels_] = (int)cells_.size();
     slots_per_image_ = (slot + 63) & ~(size_t)63;
     if (cells_.size() > 4096) return -1;
+    // cell groups: a level's cells form a grid (the skips above depend on i or on j only); two
+    // neighbouring rows (columns) share a workgroup when the second one's ROI starts wCell
+    // (hCell) after the first one's and ends at most FC_MAXR after it, and holds detection pixels
+    groups_.clear();
+    for (int l = 0; l < nlevels_; l++) {
+        const int cb = level_cell_begin_[l], ce = level_cell_begin_[l + 1];
+        if (cb == ce) continue;
+        std::vector<int> rowb;   // first cell of every cell row
+        for (int c = cb; c < ce; c++)
+            if (c == cb || cells_[c].r0 != cells_[c - 1].r0) rowb.push_back(c);
+        const int ncol = (int)(rowb.size() > 1 ? rowb[1] - rowb[0] : ce - cb);
+        if ((ce - cb) != ncol * (int)rowb.size()) return -1;
+        auto spans = [](int a0, int a1, int b0, int b1) {   // ROIs [a0,a1), [b0,b1) tile a union
+            return a1 == b0 + 6 && b1 - b0 >= 7 && b1 - a0 <= FC_MAXR;
+        };
+        std::vector<std::pair<int, int>> rsel, csel;   // (first, count) row / column pairs
+        for (int i = 0; i < (int)rowb.size();) {
+            const CellDesc &a = cells_[rowb[i]];
+            const bool two = i + 1 < (int)rowb.size() && spans(a.r0, a.r1, cells_[rowb[i + 1]].r0, cells_[rowb[i + 1]].r1);
+            rsel.push_back({i, two ? 2 : 1});
+            i += two ? 2 : 1;
+        }
+        for (int j = 0; j < ncol;) {
+            const CellDesc &a = cells_[cb + j];
+            const bool two = j + 1 < ncol && spans(a.c0, a.c1, cells_[cb + j + 1].c0, cells_[cb + j + 1].c1);
+            csel.push_back({j, two ? 2 : 1});
+            j += two ? 2 : 1;
+        }
+        for (auto& rp : rsel)
+            for (auto& cp : csel) {
+                CellGroup g{};
+                const CellDesc& tl = cells_[rowb[rp.first] + cp.first];
+                const CellDesc& br = cells_[rowb[rp.first + rp.second - 1] + cp.first + cp.second - 1];
+                g.r0 = tl.r0; g.c0 = tl.c0;
+                g.rows = br.r1 - tl.r0; g.cols = br.c1 - tl.c0;
+                g.rsplit = rp.second == 2 ? tl.r1 - tl.r0 - 6 : std::max(g.rows - 6, 0);
+                g.csplit = cp.second == 2 ? tl.c1 - tl.c0 - 6 : std::max(g.cols - 6, 0);
+                g.pitch = tl.pitch;
+                g.lvl_off = tl.lvl_off;
+                for (int k = 0; k < 4; k++) {
+                    const int di = k >> 1, dj = k & 1;
+                    g.cell[k] = -1;
+                    if (di >= rp.second || dj >= cp.second) continue;
+                    const int c = rowb[rp.first + di] + cp.first + dj;
+                    const CellDesc& cd = cells_[c];
+                    g.cell[k] = c;
+                    g.cap[k] = cd.cap;
+                    g.slot_off[k] = cd.slot_off;
+                    g.xadd[k] = cd.offx - (cd.c0 - g.c0);
+                    g.yadd[k] = cd.offy - (cd.r0 - g.r0);
+                }
+                groups_.push_back(g);
+            }
+    }
+    if (groups_.size() > 65535) return -1;
     // blur tiles
     tiles_.clear();
     for (int l = 0; l < nlevels_; l++) {
@@ -920,7 +1031,7 @@ int Extractor::setup_geometry(int W, int H) {
     ptile_begin_[nlevels_] = (int)ptiles_.size();
     // (re)allocate device buffers for maxB_
     auto F = [](void*& p) { if (p) (void)hipFree(p); p = nullptr; };
-    F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_lcb_); F(d_work_);
+    F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_lcb_); F(d_work_); F(d_groups_);
     work_B_ = -1;
     F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_); F(d_ptiles_);
     const int B = maxB_;
@@ -934,6 +1045,8 @@ int Extractor::setup_geometry(int W, int H) {
     ORB_HIP_CHECK(hipMalloc(&d_counts_, cells_.size() * 4 * B));
     ORB_HIP_CHECK(hipMalloc(&d_cells_, cells_.size() * sizeof(CellDesc)));
     ORB_HIP_CHECK(hipMemcpy(d_cells_, cells_.data(), cells_.size() * sizeof(CellDesc), hipMemcpyHostToDevice));
+    ORB_HIP_CHECK(hipMalloc(&d_groups_, groups_.size() * sizeof(CellGroup)));
+    ORB_HIP_CHECK(hipMemcpy(d_groups_, groups_.data(), groups_.size() * sizeof(CellGroup), hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMalloc(&d_tiles_, tiles_.size() * sizeof(BlurTile)));
     ORB_HIP_CHECK(hipMemcpy(d_tiles_, tiles_.data(), tiles_.size() * sizeof(BlurTile), hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMalloc(&d_lcb_, level_cell_begin_.size() * 4));
@@ -1034,7 +1147,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     const int ncells = (int)cells_.size();
     if (work_B_ != B && build_work(B)) return -2;
     hipLaunchKernelGGL(k_fast_cells, dim3(work_n_), dim3(256), 0, s, (const uint8_t*)d_pyr_, img_bytes_,
-                       (const CellDesc*)d_cells_, iniTh_, minTh_, (uint32_t*)d_slots_, slots_per_image_,
+                       (const CellGroup*)d_groups_, iniTh_, minTh_, (uint32_t*)d_slots_, slots_per_image_,
                        (int*)d_counts_, ncells, (const int*)d_work_);
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[3], s));

@@ -28,6 +28,18 @@ struct CellDesc {          // one FAST cell ROI, ORBextractor.cc:794-829
     long long lvl_off;     // byte offset of the padded level in an image slab
 };
 
+// Up to 2 x 2 neighbouring cells of one level (one k_fast_cells workgroup): their ROIs overlap by
+// the 6-px FAST frame, so they tile one union ROI whose detection pixels are the cells' own,
+// concatenated.  Cell k: bit 0 = right column, bit 1 = bottom row; cell[k] < 0 if absent.
+struct CellGroup {
+    int r0, c0, rows, cols;     // union ROI (level interior coords)
+    int rsplit, csplit;         // detection rows of the top cells / columns of the left cells
+    int pitch, pad;
+    long long lvl_off;
+    int cell[4], cap[4], slot_off[4];
+    int xadd[4], yadd[4];       // union-ROI (col, row) + (xadd, yadd) = the cell's (offx, offy) + ROI (col, row)
+};
+
 struct BlurTile {
     long long off, boff;
     int pitch, bpitch, w, h, tx, ty;
@@ -97,6 +109,7 @@ private:
     int geomW_ = -1, geomH_ = -1;
     std::vector<LevelHost> levels_;
     std::vector<CellDesc> cells_;
+    std::vector<CellGroup> groups_;
     std::vector<int> level_cell_begin_;
     std::vector<BlurTile> tiles_;
     std::vector<PyrTile> ptiles_;
@@ -114,6 +127,7 @@ private:
     void *d_sel_ = nullptr, *d_levels_ = nullptr, *d_tabs_ = nullptr, *d_kps_ = nullptr, *d_desc_ = nullptr;
     int* d_gtotal_ = nullptr;
     void* d_work_ = nullptr;   // k_fast_cells work order (build_work), for work_B_ images
+    void* d_groups_ = nullptr;
     int work_B_ = -1, work_n_ = 0;
     bool d_gtotal_alias_ = false;
     size_t in_cap_ = 0, out_cap_ = 0;
