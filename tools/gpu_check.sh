@@ -27,7 +27,7 @@ W="workload: tools/extract_timing.py 64 = the bench roofline pass (left batch, s
 python3 tools/pmc_traffic.py "$(find "$OUT/FETCH_SIZE" -name '*counter_collection.csv' | head -1)" \
   "$(find "$OUT/WRITE_SIZE" -name '*counter_collection.csv' | head -1)" "$OUT/traffic.json" "$W" || exit 1
 python3 tools/pmc_valu.py "$(find "$OUT/SQ_INSTS_VALU" -name '*counter_collection.csv' | head -1)" "$OUT/valu.json" "$W" || exit 1
-cp "$OUT/traffic.json" profiles/traffic_r01.json && cp "$OUT/valu.json" profiles/valu_r01.json
+cp "$OUT/traffic.json" profiles/traffic_r02.json && cp "$OUT/valu.json" profiles/valu_r02.json
 echo "[gpu_check] bench" && date
 timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
