@@ -35,6 +35,21 @@ __device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
+// the query's descriptor held in registers across its candidates
+struct Desc32 {
+    uint4 a0, a1;
+    __device__ __forceinline__ explicit Desc32(const uint8_t* a) {
+        a0 = reinterpret_cast<const uint4*>(a)[0];
+        a1 = reinterpret_cast<const uint4*>(a)[1];
+    }
+    __device__ __forceinline__ int dist(const uint8_t* b) const {
+        const uint4* pb = reinterpret_cast<const uint4*>(b);
+        const uint4 b0 = pb[0], b1 = pb[1];
+        return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+               __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+    }
+};
+
 // Rcw*X + tcw as one cv::gemm (GEMMSingleMul<float,double>): f64 accumulate, one rounding.
 __device__ __forceinline__ float gemm_row(const float* T, int r, float X0, float X1, float X2) {
     double s = (double)T[r * 4 + 0] * X0 + (double)T[r * 4 + 1] * X1 + (double)T[r * 4 + 2] * X2;
@@ -183,17 +198,28 @@ __device__ __forceinline__ void for_features_in_area(const SearchDev& P, const Q
         }
 }
 
-// Sorted insertion by (dist, order): later equal distances go after earlier ones.
-__device__ __forceinline__ void topk_insert(int2* top, int& n, int K, int dist, int idx) {
-    if (n == K && dist >= top[K - 1].x) return;
-    int p = n < K ? n : K - 1;
-    while (p > 0 && top[p - 1].x > dist) {
-        top[p] = top[p - 1];
-        p--;
+// The K best (dist, idx) of a query's candidates, sorted by dist, equal distances in visit
+// order (later after earlier), held in registers: an unrolled compare-and-shift network with
+// static slot indices (a dynamically indexed private array lives in scratch memory).  Empty
+// slots hold dist INT_MAX, so a full list's cut-off test `dist >= t[K-1].x` covers both cases.
+template <int K>
+struct TopK {
+    int2 t[K];
+    __device__ __forceinline__ TopK() {
+#pragma unroll
+        for (int p = 0; p < K; p++) t[p] = make_int2(INT_MAX, -1);
     }
-    top[p] = make_int2(dist, idx);
-    if (n < K) n++;
-}
+    __device__ __forceinline__ void insert(int dist, int idx) {
+        if (dist >= t[K - 1].x) return;
+#pragma unroll
+        for (int p = K - 1; p > 0; p--) {
+            const bool sh = t[p - 1].x > dist;   // slot p takes its predecessor
+            const bool at = !sh && t[p].x > dist;   // the insertion point
+            t[p] = sh ? t[p - 1] : at ? make_int2(dist, idx) : t[p];
+        }
+        if (t[0].x > dist) t[0] = make_int2(dist, idx);
+    }
+};
 
 struct LastQuery {
     bool valid;
@@ -249,10 +275,10 @@ __device__ __forceinline__ void fwd_bwd(const SearchDev& P, bool bMono, bool& bF
 }
 
 // Enumerate a LastFrame query's passing candidates; `blocked(i2)` models occupancy.
-template <class Blocked>
-__device__ int scan_last(const SearchDev& P, const LastQuery& q, Blocked blocked, int2* top, int K) {
-    int n = 0, cnt = 0;
-    const uint8_t* dMP = P.mpDesc + 32 * (size_t)q.mp;
+template <class Blocked, class Top>
+__device__ int scan_last(const SearchDev& P, const LastQuery& q, Blocked blocked, Top& top) {
+    int cnt = 0;
+    const Desc32 dMP(P.mpDesc + 32 * (size_t)q.mp);
     for_features_in_area(P, q.w, [&](int i2) {
         if (blocked(i2)) return;
         if (P.cur.uRight && P.cur.uRight[i2] > 0) {
@@ -260,8 +286,7 @@ __device__ int scan_last(const SearchDev& P, const LastQuery& q, Blocked blocked
             const float er = fabsf(ur - P.cur.uRight[i2]);
             if (er > q.radius) return;
         }
-        const int dist = hamming32(dMP, P.cur.desc + 32 * (size_t)i2);
-        topk_insert(top, n, K, dist, i2);
+        top.insert(dMP.dist(P.cur.desc + 32 * (size_t)i2), i2);
         cnt++;
     });
     return cnt;
@@ -295,18 +320,17 @@ __device__ __forceinline__ LocalQuery local_query(const SearchDev& P, int j, flo
     return q;
 }
 
-template <class Blocked>
-__device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked blocked, int2* top, int K) {
-    int n = 0, cnt = 0;
-    const uint8_t* d0 = P.mpDesc + 32 * (size_t)q.mp;
+template <class Blocked, class Top>
+__device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked blocked, Top& top) {
+    int cnt = 0;
+    const Desc32 d0(P.mpDesc + 32 * (size_t)q.mp);
     for_features_in_area(P, q.w, [&](int idx) {
         if (blocked(idx)) return;
         if (P.cur.uRight && P.cur.uRight[idx] > 0) {
             const float er = fabsf(q.projXR - P.cur.uRight[idx]);
             if (er > q.r * P.cur.scale[q.level]) return;
         }
-        const int dist = hamming32(d0, P.cur.desc + 32 * (size_t)idx);
-        topk_insert(top, n, K, dist, idx);
+        top.insert(d0.dist(P.cur.desc + 32 * (size_t)idx), idx);
         cnt++;
     });
     return cnt;
@@ -329,7 +353,7 @@ __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict_
         }
     }
     if (!counters && q >= P.nq) return;
-    int2 top[kTopK];
+    TopK<kTopK> top;
     int cnt = -1;
     auto never = [](int) { return false; };
     if (q >= P.nq) {   // measurement only: the wave stays whole for its counter sums
@@ -337,15 +361,17 @@ __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict_
         bool bF, bB;
         fwd_bwd(P, bMono != 0, bF, bB);
         const LastQuery lq = last_query(P, q, th, bF, bB);
-        if (lq.valid) cnt = scan_last(P, lq, never, top, kTopK);
+        if (lq.valid) cnt = scan_last(P, lq, never, top);
     } else {
         const LocalQuery lq = local_query(P, q, th);
-        if (lq.valid) cnt = scan_local(P, lq, never, top, kTopK);
+        if (lq.valid) cnt = scan_local(P, lq, never, top);
     }
     if (q < P.nq) {
         P.qinfo[q] = make_int4(cnt, 0, 0, 0);
         const int kk = cnt < kTopK ? cnt : kTopK;
-        for (int k = 0; k < kk; k++) P.topk[(size_t)q * kTopK + k] = top[k];
+#pragma unroll
+        for (int k = 0; k < kTopK; k++)
+            if (k < kk) P.topk[(size_t)q * kTopK + k] = top.t[k];
     }
     if (counters) {   // measurement: scored pairs and windowed queries
         const unsigned long long pr = wave_sum_u64(cnt > 0 ? (unsigned long long)cnt : 0ull);
@@ -463,17 +489,18 @@ __device__ __noinline__ int select_slow(const SearchDev* __restrict__ Pp, int q,
         nfree++;
     }
     if (nfree < need && c > kTopK) {
-        int2 top2[2];
         bestDist = bestDist2 = 256;
         bestIdx = idx2 = -1;
         if (LAST) {
+            TopK<1> top2;
             const LastQuery lq = last_query(P, q, th, bF != 0, bB != 0);
-            if (scan_last(P, lq, occupied, top2, 1) > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
+            if (scan_last(P, lq, occupied, top2) > 0) { bestDist = top2.t[0].x; bestIdx = top2.t[0].y; }
         } else {
+            TopK<2> top2;
             const LocalQuery lq = local_query(P, q, th);
-            const int c2 = scan_local(P, lq, occupied, top2, 2);
-            if (c2 > 0) { bestDist = top2[0].x; bestIdx = top2[0].y; }
-            if (c2 > 1) { bestDist2 = top2[1].x; idx2 = top2[1].y; }
+            const int c2 = scan_local(P, lq, occupied, top2);
+            if (c2 > 0) { bestDist = top2.t[0].x; bestIdx = top2.t[0].y; }
+            if (c2 > 1) { bestDist2 = top2.t[1].x; idx2 = top2.t[1].y; }
         }
     }
     if (bestDist > TH_HIGH) return -1;
