@@ -213,11 +213,15 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
         const double tmp[6] = {fx, 0, ((-x) / z) * fx, 0, fy, ((-y) / z) * fy};
         const double s = -1. / z;
         double st[6];
+#pragma unroll
         for (int k = 0; k < 6; k++) st[k] = s * tmp[k];
+#pragma unroll
         for (int r = 0; r < 2; r++)
+#pragma unroll
             for (int c = 0; c < 3; c++) A[r * 3 + c] = (st[r * 3] * R[c] + st[r * 3 + 1] * R[3 + c]) + st[r * 3 + 2] * R[6 + c];
     } else {
         const double bf = e.bf;
+#pragma unroll
         for (int c = 0; c < 3; c++) {
             A[0 * 3 + c] = ((-fx) * R[0 * 3 + c]) / z + ((fx * x) * R[2 * 3 + c]) / z_2;
             A[1 * 3 + c] = ((-fy) * R[1 * 3 + c]) / z + ((fy * y) * R[2 * 3 + c]) / z_2;
@@ -245,45 +249,60 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
         B[16] = 0;
         B[17] = B[5] - bf / z_2;
     } else {
+#pragma unroll
         for (int k = 12; k < 18; k++) B[k] = 0;
     }
-    // constructQuadraticForm (base_binary_edge.hpp:55-120)
+    // constructQuadraticForm (base_binary_edge.hpp:55-120); every loop unrolled with static
+    // indices (k < D as a predicate, the same k-ascending sums), so A, B, omr stay in registers
     const double w = robust ? rho1 * e.info : e.info;
     double omr[3] = {0, 0, 0};
-    for (int k = 0; k < D; k++) {
-        omr[k] = -(e.info * err[k]);
-        if (robust) omr[k] *= rho1;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        if (k < D) {
+            omr[k] = -(e.info * err[k]);
+            if (robust) omr[k] *= rho1;
+        }
     }
     const int nE = a.s.nE;
     double* t = a.terms;
+#pragma unroll
     for (int r = 0; r < 3; r++) {
         double s = 0;
-        for (int k = 0; k < D; k++) s += A[k * 3 + r] * omr[k];
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            if (k < D) s += A[k * 3 + r] * omr[k];
         t[(T_BL + r) * nE + i] = s;
+#pragma unroll
         for (int c = 0; c < 3; c++) {
             double h = 0;
-            for (int k = 0; k < D; k++) h += (A[k * 3 + r] * w) * A[k * 3 + c];
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                if (k < D) h += (A[k * 3 + r] * w) * A[k * 3 + c];
             t[(T_HLL + r * 3 + c) * nE + i] = h;
         }
     }
     if (a.s.ePose[i] < 0) return;
-    int q = 0;
+#pragma unroll
     for (int r = 0; r < 6; r++) {
         double s = 0;
-        for (int k = 0; k < D; k++) s += B[k * 6 + r] * omr[k];
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            if (k < D) s += B[k * 6 + r] * omr[k];
         t[(T_BP + r) * nE + i] = s;
+#pragma unroll
         for (int c = r; c < 6; c++) {
             double h = 0;
-            for (int k = 0; k < D; k++) h += (B[k * 6 + r] * w) * B[k * 6 + c];
-            t[(T_HPP + q) * nE + i] = h;
-            q++;
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                if (k < D) h += (B[k * 6 + r] * w) * B[k * 6 + c];
+            t[(T_HPP + (r * (13 - r)) / 2 + (c - r)) * nE + i] = h;
         }
+#pragma unroll
         for (int c = 0; c < 3; c++) {
             double h = 0;
-            if (robust)
-                for (int k = 0; k < D; k++) h += (B[k * 6 + r] * w) * A[k * 3 + c];
-            else
-                for (int k = 0; k < D; k++) h += B[k * 6 + r] * (A[k * 3 + c] * e.info);
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                if (k < D) h += robust ? (B[k * 6 + r] * w) * A[k * 3 + c] : B[k * 6 + r] * (A[k * 3 + c] * e.info);
             a.Hpl[18 * (size_t)i + r * 3 + c] = h;
         }
     }
