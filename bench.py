@@ -47,8 +47,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=None, help="GPUs (one rank each); default: WORLD_SIZE or 1")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: ranks meet over gloo and rank 0 prints n_gpus")
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="stereo frames per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -8,7 +8,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$R" || exit 1
 timeout -k 10 400 python -u -m pytest tests/test_gpu_match.py tests/test_gpu_search.py tests/test_gpu_track_local_map.py \
-  tests/test_gpu_frame_ops.py -x -q --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
+  tests/test_gpu_frame_ops.py tests/test_gpu_stereo.py -x -q --timeout 120 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
 timeout -k 10 400 python bench.py --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
 python3 - "$OUT/bench.json" <<'PY'
