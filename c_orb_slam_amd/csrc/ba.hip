@@ -1127,8 +1127,17 @@ __device__ __forceinline__ double pose_rho0(const PoseEdgeD& e, double c, bool r
 
 
 constexpr int kPoseMaxEdges = 8192;
-constexpr int kPoseThreads = 256;   // one wave per SIMD: the workgroup fits beside the extraction grids
-constexpr int kPosePer = kPoseMaxEdges / kPoseThreads;
+// one wave per SIMD: the workgroup fits beside the extraction grids (batches); a batch of at
+// most pose_wide_max() frames (the per-frame tracking latency) takes two waves per SIMD instead,
+// half the chunks per wave in every edge pass (the same canonical sums: bit-identical)
+constexpr int kPoseThreads = 256, kPoseThreadsWide = 512;
+static int pose_wide_max() {   // ORBGPU_POSE_WIDE_MAX overrides the batch limit of the wide kernel
+    static const int v = [] {
+        const char* e = getenv("ORBGPU_POSE_WIDE_MAX");
+        return e ? atoi(e) : 8;
+    }();
+    return v;
+}
 
 // Canonical totals (ora_csum level 2) of the m chunk trees cs[q][0..m) of K sums, by wave 0:
 // lane c holds chunk c and the K trees run packed (the same pairing as local_csum_inplace).
@@ -1371,9 +1380,11 @@ __device__ __forceinline__ bool pose_solve_w(const double* Hs, const double* bs,
     return true;
 }
 
-__global__ void __launch_bounds__(kPoseThreads) k_pose_opt(PoseProbDev* probs, const PoseEdgeDev* __restrict__ Eall,
-                                                   double* errAll, uint8_t* outlAll) {
+template <int NT>
+__global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseEdgeDev* __restrict__ Eall,
+                                                 double* errAll, uint8_t* outlAll) {
     ORBGPU_LATENCY_WAVE();
+    constexpr int kPosePer = kPoseMaxEdges / NT;
     PoseProbDev& P = probs[blockIdx.x];
     const int ne = P.ne;
     const PoseEdgeDev* E = Eall + P.e0;
@@ -1851,8 +1862,12 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
     if (!src) return -2;
     ORB_HIP_CHECK(hipMemcpyAsync(d, src, sizeof(PoseProbDev) * count, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_pose_pack, dim3(count), dim3(kPackThreads), 0, st, dp, dE);
-    hipLaunchKernelGGL(k_pose_opt, dim3(count), dim3(kPoseThreads), 0, st, dp, (const PoseEdgeDev*)dE, nullptr,
-                       (uint8_t*)(d + bProb + bEdge));
+    if (count <= pose_wide_max())
+        hipLaunchKernelGGL(k_pose_opt<kPoseThreadsWide>, dim3(count), dim3(kPoseThreadsWide), 0, st, dp, (const PoseEdgeDev*)dE, nullptr,
+                           (uint8_t*)(d + bProb + bEdge));
+    else
+        hipLaunchKernelGGL(k_pose_opt<kPoseThreads>, dim3(count), dim3(kPoseThreads), 0, st, dp, (const PoseEdgeDev*)dE, nullptr,
+                           (uint8_t*)(d + bProb + bEdge));
     ORB_HIP_CHECK(hipGetLastError());
     if (chain) {
         void* land = chain->land(ninliers, sizeof(int) * count);
@@ -1936,8 +1951,14 @@ int PoseEngine::run(int count, const pose_problem* P, float* Tcw_out, uint8_t* c
     PoseProbDev* dp = (PoseProbDev*)d;
     ORB_HIP_CHECK(hipMemcpyAsync(d, h, bProb + sizeof(PoseEdgeDev) * ne, hipMemcpyHostToDevice, stream_));
     if (count > 0)
-        hipLaunchKernelGGL(k_pose_opt, dim3(count), dim3(kPoseThreads), 0, stream_, dp, (const PoseEdgeDev*)(d + bProb),
-                           (double*)(d + bProb + bEdge), (uint8_t*)(d + bProb + bEdge + bErr));
+    {
+        if (count <= pose_wide_max())
+            hipLaunchKernelGGL(k_pose_opt<kPoseThreadsWide>, dim3(count), dim3(kPoseThreadsWide), 0, stream_, dp, (const PoseEdgeDev*)(d + bProb),
+                               (double*)(d + bProb + bEdge), (uint8_t*)(d + bProb + bEdge + bErr));
+        else
+            hipLaunchKernelGGL(k_pose_opt<kPoseThreads>, dim3(count), dim3(kPoseThreads), 0, stream_, dp, (const PoseEdgeDev*)(d + bProb),
+                               (double*)(d + bProb + bEdge), (uint8_t*)(d + bProb + bEdge + bErr));
+    }
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipMemcpyAsync(h, d, bProb, hipMemcpyDeviceToHost, stream_));
     if (ne) ORB_HIP_CHECK(hipMemcpyAsync(hOut, d + bProb + bEdge + bErr, ne, hipMemcpyDeviceToHost, stream_));
