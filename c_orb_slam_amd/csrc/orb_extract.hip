@@ -266,6 +266,29 @@ __device__ __forceinline__ bool fast_pretest(const uint8_t* p, int ld, int t) {
            (bd && ba);
 }
 
+// The same test for two rows at once in packed 16-bit lanes (row A low half, row B high half):
+// x darker than v by more than t <=> (v - (t+1)) - x >= 0, brighter <=> x - (v + (t+1)) >= 0,
+// so the sign bits of the packed differences are the negated comparisons, and
+// fail = !dark && !bright = ((na & nc) | (nb & nd)) & ((ba & bc) | (bb & bd)) on those bits.
+// Bit 15 / bit 31 of the result set: row A / row B fails.
+typedef short short2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ short2v pk16(int lo, int hi) {
+    short2v r;
+    r.x = (short)lo;
+    r.y = (short)hi;
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_bits(short2v v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t fast_pretest2_fail(const uint8_t* pa, const uint8_t* pb, int ld, short2v T1) {
+    const short2v v = pk16(pa[0], pb[0]);
+    const short2v a = pk16(pa[3 * ld], pb[3 * ld]), b = pk16(pa[3], pb[3]);
+    const short2v c = pk16(pa[-3 * ld], pb[-3 * ld]), d = pk16(pa[-3], pb[-3]);
+    const short2v vm = v - T1, vp = v + T1;
+    const uint32_t na = pk_bits(vm - a), nb = pk_bits(vm - b), nc = pk_bits(vm - c), nd = pk_bits(vm - d);
+    const uint32_t ba = pk_bits(a - vp), bb = pk_bits(b - vp), bc = pk_bits(c - vp), bd = pk_bits(d - vp);
+    return ((na & nc) | (nb & nd)) & ((ba & bc) | (bb & bd));
+}
+
 // Exclusive scan by wave 0 of the popcounts of masks[0..n) (n <= 64) into off[0..n], off[64] = total.
 __device__ __forceinline__ void mask_scan64(const uint64_t* masks, int n, int* off, int lane) {
     const int cnt = lane < n ? (int)__popcll(masks[lane]) : 0;
@@ -360,10 +383,30 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     // detection columns on the lanes (dc <= 64: the union ROI is <= FC_MAXR wide), detection rows
     // over the waves; row i's survivor mask is one ballot, its left-cell bits the low cs bits
     const uint64_t Lm = cs >= 64 ? ~0ull : ((1ull << cs) - 1ull);
-    for (int i = wid; i < dr; i += 4) {
-        const bool pass = lane < dc && (tp < 1 || fast_pretest(&s_img[(3 + i) * FC_LD + mis + 3 + lane], FC_LD, tp));
-        const uint64_t m = __ballot(pass);
-        if (lane == 0) s_mask[i] = m;
+    if (tp < 1) {
+        for (int i = wid; i < dr; i += 4) {
+            const uint64_t m = __ballot(lane < dc);
+            if (lane == 0) s_mask[i] = m;
+        }
+    } else {
+        // rows i and i + 4 of the wave in one packed pass (row i + 4 clamped into the ROI when
+        // it is past the last detection row; its mask is then not stored)
+        const short2v T1 = pk16(tp + 1, tp + 1);
+        for (int i = wid; i < dr; i += 8) {
+            const int i1 = min(i + 4, dr - 1);
+            bool p0 = false, p1 = false;
+            if (lane < dc) {
+                const uint32_t f = fast_pretest2_fail(&s_img[(3 + i) * FC_LD + mis + 3 + lane],
+                                                      &s_img[(3 + i1) * FC_LD + mis + 3 + lane], FC_LD, T1);
+                p0 = !(f & 0x8000u);
+                p1 = !(f & 0x80000000u);
+            }
+            const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
+            if (lane == 0) {
+                s_mask[i] = m0;
+                if (i + 4 < dr) s_mask[i + 4] = m1;
+            }
+        }
     }
     __syncthreads();
     ORBGPU_PROF_MARK(1);
