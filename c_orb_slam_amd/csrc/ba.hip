@@ -145,9 +145,11 @@ struct LinArgs {
 };
 
 // computeActiveErrors + activeRobustChi2 terms (+ linearizeOplus + constructQuadraticForm)
-// canonical total of chunk sums c[0..m) with 256 threads (LDS level buffer), into *out
+// canonical total of chunk sums c[0..m) with 256 threads (LDS level buffer), into *out;
+// m <= 64 * kCsumLv chunks, i.e. up to 16.7 M edges (config 5 at 16 k keyframes: ~11 M)
+constexpr int kCsumLv = 4096;
 __device__ __forceinline__ void block_finish_csum(const double* c, int m, int nterms, const double* single, double* out) {
-    __shared__ double lv[1024];
+    __shared__ double lv[kCsumLv];
     if (nterms <= 1) {
         if (threadIdx.x == 0) *out = nterms == 1 ? *single : 0.0;
         return;
@@ -2271,7 +2273,7 @@ int BaEngine::build_structure(int level) {
         if (peStart[i + 1] - peStart[i] > 64 * kChunks) return -3;
     for (int l = 0; l < nL; l++)
         if (leStart[l + 1] - leStart[l] > 64 * 64) return -3;
-    if (nE > 1024 * 64 * 64 || 6LL * nP + 3LL * nL > (long long)scratchN_) return -3;
+    if (nE > kCsumLv * 64 * 64 || 6LL * nP + 3LL * nL > (long long)scratchN_) return -3;
     for (int b = 0; b < nBlk; b++)
         if (blkStart[b + 1] - blkStart[b] > 64 * kChunks) return -3;
     // pack and upload
