@@ -145,11 +145,12 @@ struct LinArgs {
 };
 
 // computeActiveErrors + activeRobustChi2 terms (+ linearizeOplus + constructQuadraticForm)
-// canonical total of chunk sums c[0..m) with 256 threads (LDS level buffer), into *out;
-// m <= 64 * kCsumLv chunks, i.e. up to 16.7 M edges (config 5 at 16 k keyframes: ~11 M)
+// canonical total of chunk sums c[0..m) with 256 threads, into *out: the level-2 trees go to an
+// LDS buffer (m <= 64 * 1024 chunks, 4.2 M edges) or, for larger problems (config 5 at 8-16 k
+// keyframes), to the chunk buffer's tail c[m..m + m/64] (carve sizes it); m <= 64 * kCsumLv
 constexpr int kCsumLv = 4096;
-__device__ __forceinline__ void block_finish_csum(const double* c, int m, int nterms, const double* single, double* out) {
-    __shared__ double lv[kCsumLv];
+__device__ __forceinline__ void block_finish_csum(double* c, int m, int nterms, const double* single, double* out) {
+    __shared__ double lv[1024];
     if (nterms <= 1) {
         if (threadIdx.x == 0) *out = nterms == 1 ? *single : 0.0;
         return;
@@ -159,10 +160,12 @@ __device__ __forceinline__ void block_finish_csum(const double* c, int m, int nt
         return;
     }
     int m2 = (m + 63) >> 6;
+    double* L = m2 <= 1024 ? lv : c + m;
     for (int t = threadIdx.x; t < m2; t += blockDim.x)
-        lv[t] = tree64_local([&](int k) { return c[t * 64 + k]; }, min(64, m - t * 64));
+        L[t] = tree64_local([&](int k) { return c[t * 64 + k]; }, min(64, m - t * 64));
+    __threadfence();
     __syncthreads();
-    if (threadIdx.x == 0) *out = local_csum_inplace(lv, m2);
+    if (threadIdx.x == 0) *out = local_csum_inplace(L, m2);
 }
 
 __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
@@ -2046,7 +2049,7 @@ bool BaEngine::dense_solver(int n) const {
 int BaEngine::carve(bool commit, size_t* total) {
     const size_t ne = (size_t)std::max(ne_, 1), nkf = (size_t)std::max(nkf_, 1), npt = (size_t)std::max(npt_, 1);
     scratchN_ = 6 * nkf + 3 * npt + ne + 64;
-    const size_t tmpN = scratchN_ / 64 + 64;
+    const size_t tmpN = scratchN_ / 64 + scratchN_ / 4096 + 128;   // chunk trees + their level-2 tail
     size_t off = 0;
     char* base = (char*)arena_;
     auto take = [&](size_t bytes) -> void* {
