@@ -1,5 +1,5 @@
 # Top-level build: the HIP product library and the CPU parity oracle.
-all: lib oracle
+all: lib oracle abi
 
 lib:
 	$(MAKE) -C c_orb_slam_amd/csrc -j8
@@ -7,8 +7,16 @@ lib:
 oracle:
 	$(MAKE) -C oracle
 
+# a plain C11 caller of include/orbslam_gpu.h linked against the product library
+# (tests/test_library.py builds its own copy on CPU; the GPU test runs this one)
+abi: build/abi_caller
+build/abi_caller: tests/c_abi/abi_caller.c include/orbslam_gpu.h lib
+	mkdir -p build
+	gcc -std=c11 -pedantic -Wall -Wextra -Werror -O2 -Iinclude tests/c_abi/abi_caller.c \
+	    -Lc_orb_slam_amd -lorbslam_gpu -Wl,-rpath,'$$ORIGIN/../c_orb_slam_amd' -o $@
+
 clean:
 	$(MAKE) -C c_orb_slam_amd/csrc clean
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib oracle clean
+.PHONY: all lib oracle abi clean

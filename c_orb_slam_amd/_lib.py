@@ -190,12 +190,13 @@ def lib():
     L.orbgpu_unit_pnp_layout.argtypes = [i32, vp, vp, vp, vp]
     L.MapPoint_CreateStereo_batch_device.argtypes = [vp, i32, vp]
     L.Tracking_PrepareLocalSearch_batch_device.argtypes = [vp, i32, vp]
-    L.ORBmatcher_SearchLocalPoints_batch.argtypes = [vp, i32, vp, vp, vp, f32, f32, vp, vp]
+    L.ORBmatcher_SearchLocalPoints_batch.argtypes = [vp, i32, vp, vp, vp, f32, f32, f32, vp, vp]
     L.Frame_isInFrustum_batch.argtypes = [vp, i32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp]
     L.ORBmatcher_enable_timing.argtypes = [vp, i32]
     L.ORBmatcher_last_timings.argtypes = [vp, vp, vp]
     L.orbgpu_unit_ldlt_factor.argtypes = [i32, vp, vp]
     L.orbgpu_unit_wave_tree.argtypes = [vp, vp]
+    L.orbgpu_unit_set_csum_lds_max.argtypes = [i32]
     L.orbgpu_debug_prof.argtypes = [vp]
     L.orbgpu_debug_prof_match.argtypes = [vp]
     L.orbgpu_debug_prof_extract.argtypes = [vp]

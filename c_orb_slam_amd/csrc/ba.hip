@@ -149,6 +149,9 @@ struct LinArgs {
 // LDS buffer (m <= 64 * 1024 chunks, 4.2 M edges) or, for larger problems (config 5 at 8-16 k
 // keyframes), to the chunk buffer's tail c[m..m + m/64] (carve sizes it); m <= 64 * kCsumLv
 constexpr int kCsumLv = 4096;
+// level-2 trees up to this many go to LDS (1024 = the LDS buffer); tests lower it through
+// orbgpu_unit_set_csum_lds_max to drive the chunk-buffer tail path at small sizes
+__device__ int g_csum_lds_max = 1024;
 __device__ __forceinline__ void block_finish_csum(double* c, int m, int nterms, const double* single, double* out) {
     __shared__ double lv[1024];
     if (nterms <= 1) {
@@ -160,7 +163,7 @@ __device__ __forceinline__ void block_finish_csum(double* c, int m, int nterms, 
         return;
     }
     int m2 = (m + 63) >> 6;
-    double* L = m2 <= 1024 ? lv : c + m;
+    double* L = m2 <= min(g_csum_lds_max, 1024) ? lv : c + m;
     for (int t = threadIdx.x; t < m2; t += blockDim.x)
         L[t] = tree64_local([&](int k) { return c[t * 64 + k]; }, min(64, m - t * 64));
     __threadfence();
@@ -1833,6 +1836,7 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
     const size_t bOut = al(std::max<size_t>(nmax, 1)), bNin = al(sizeof(int) * count);
     const size_t need = bProb + bEdge + bOut + bNin;
     if (need > cap_) {
+        if (lastUseSet_) ORB_HIP_CHECK(hipEventSynchronize(lastUse_));   // queued kernels may still read it
         if (dArena_) (void)hipFree(dArena_);
         if (hArena_) (void)hipHostFree(hArena_);
         dArena_ = hArena_ = nullptr;
@@ -1865,6 +1869,9 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
     PoseEdgeDev* dE = (PoseEdgeDev*)(d + bProb);
     const void* src = chain ? chain->stage(hp, sizeof(PoseProbDev) * count) : (const void*)hp;
     if (!src) return -2;
+    // the arena's previous user may be queued on another stream (a deferred chain of another
+    // matcher, or this engine's own stream): overwrite the problem table only after it is done
+    if (lastUseSet_) ORB_HIP_CHECK(hipStreamWaitEvent(st, lastUse_, 0));
     ORB_HIP_CHECK(hipMemcpyAsync(d, src, sizeof(PoseProbDev) * count, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_pose_pack, dim3(count), dim3(kPackThreads), 0, st, dp, dE);
     if (count <= pose_wide_max())
@@ -1878,9 +1885,13 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
         void* land = chain->land(ninliers, sizeof(int) * count);
         if (!land) return -2;
         ORB_HIP_CHECK(hipMemcpyAsync(land, dNin, sizeof(int) * count, hipMemcpyDeviceToHost, st));
+        ORB_HIP_CHECK(hipEventRecord(lastUse_, st));
+        lastUseSet_ = true;
         return 0;
     }
     ORB_HIP_CHECK(hipMemcpyAsync(hp, d, bProb, hipMemcpyDeviceToHost, st));
+    ORB_HIP_CHECK(hipEventRecord(lastUse_, st));
+    lastUseSet_ = true;
     ORB_HIP_CHECK(hipStreamSynchronize(st));
     int rc = 0;
     for (int f = 0; f < count; f++) {
@@ -1892,6 +1903,8 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
 }
 
 PoseEngine::~PoseEngine() {
+    if (lastUseSet_) (void)hipEventSynchronize(lastUse_);
+    if (lastUse_) (void)hipEventDestroy(lastUse_);
     if (dArena_) (void)hipFree(dArena_);
     if (hArena_) (void)hipHostFree(hArena_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -1901,6 +1914,7 @@ int PoseEngine::init() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    ORB_HIP_CHECK(hipEventCreateWithFlags(&lastUse_, hipEventDisableTiming));
     return 0;
 }
 
@@ -1919,6 +1933,7 @@ int PoseEngine::run(int count, const pose_problem* P, float* Tcw_out, uint8_t* c
     const size_t bProb = al(sizeof(PoseProbDev) * count), bEdge = al(sizeof(PoseEdgeDev) * std::max<size_t>(ne, 1));
     const size_t bErr = al(sizeof(double) * 3 * std::max<size_t>(ne, 1)), bOut = al(std::max<size_t>(ne, 1));
     const size_t need = bProb + bEdge + bErr + bOut;
+    if (lastUseSet_) ORB_HIP_CHECK(hipEventSynchronize(lastUse_));   // hArena_ / dArena_ free again
     if (need > cap_) {
         if (dArena_) (void)hipFree(dArena_);
         if (hArena_) (void)hipHostFree(hArena_);
@@ -1967,6 +1982,8 @@ int PoseEngine::run(int count, const pose_problem* P, float* Tcw_out, uint8_t* c
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipMemcpyAsync(h, d, bProb, hipMemcpyDeviceToHost, stream_));
     if (ne) ORB_HIP_CHECK(hipMemcpyAsync(hOut, d + bProb + bEdge + bErr, ne, hipMemcpyDeviceToHost, stream_));
+    ORB_HIP_CHECK(hipEventRecord(lastUse_, stream_));
+    lastUseSet_ = true;
     ORB_HIP_CHECK(hipStreamSynchronize(stream_));
     for (int f = 0; f < count; f++) {
         const pose_problem& Q = P[f];
@@ -2681,6 +2698,12 @@ int debug_prof(unsigned long long* out32) {
     (void)out32;
     return -1;
 #endif
+}
+
+int debug_set_csum_lds_max(int v) {
+    ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_csum_lds_max), &v, sizeof(int)));
+    ORB_HIP_CHECK(hipDeviceSynchronize());
+    return 0;
 }
 
 int debug_wave_tree(const double* v64, double* out) {

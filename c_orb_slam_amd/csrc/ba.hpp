@@ -165,12 +165,17 @@ private:
     void* dArena_ = nullptr;
     void* hArena_ = nullptr;   // pinned staging: problems + edges in, outliers back
     size_t cap_ = 0;
+    // recorded after the last work that reads dArena_ (on whichever stream it was queued):
+    // the next user waits on it before overwriting the arena
+    hipEvent_t lastUse_ = nullptr;
+    bool lastUseSet_ = false;
 };
 
 int debug_ldlt(int n, const double* S, const double* b, double* x, int variant);
 int debug_csum(const double* v, int n, double* out);
 int debug_ldlt_factor(int n, const double* S, double* out);
 int debug_wave_tree(const double* v64, double* out);
+int debug_set_csum_lds_max(int v);
 int debug_prof(unsigned long long* out32);
 
 }  // namespace orbgpu

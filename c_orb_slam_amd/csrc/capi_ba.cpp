@@ -337,6 +337,11 @@ int orbgpu_debug_prof_match(unsigned long long* out32) {
     return out32 ? orbgpu::debug_prof_match(out32) : ORB_E_INVALID;
 }
 
+int orbgpu_unit_set_csum_lds_max(int m2_max) {
+    if (m2_max < 0 || m2_max > 1024) return ORB_E_INVALID;
+    return orbgpu::debug_set_csum_lds_max(m2_max) ? ORB_E_HIP : ORB_OK;
+}
+
 int orbgpu_unit_wave_tree(const double* v64, double* out) {
     if (!v64 || !out) return ORB_E_INVALID;
     int rc = 0;

@@ -363,8 +363,8 @@ int Frame_isInFrustum_batch(ORBmatcher_h h, int count, const orb_frame* F, const
 }
 
 int ORBmatcher_SearchLocalPoints_batch(ORBmatcher_h h, int count, const orb_frame* F, int32_t* const* cur_mp,
-                                       const orb_localmap* maps, float logScaleFactor, float th, int* nmatches,
-                                       int* nvisible) {
+                                       const orb_localmap* maps, float logScaleFactor, float th, float nnratio,
+                                       int* nmatches, int* nvisible) {
     if (!h || count < 0 || (count > 0 && (!F || !cur_mp || !maps || !nmatches || !nvisible))) return ORB_E_INVALID;
     if (count == 0) return ORB_OK;
     Matcher* m = h->m;
@@ -404,7 +404,7 @@ int ORBmatcher_SearchLocalPoints_batch(ORBmatcher_h h, int count, const orb_fram
         f.nvisible = d_cnt + count + p;
     }
     if (err) return err;
-    const int rc = m->search_local_points(probs, fr, 0.5f, logScaleFactor, th);
+    const int rc = m->search_local_points(probs, fr, 0.5f, logScaleFactor, th, nnratio > 0.f ? nnratio : m->nnratio());
     if (rc) return rc == -1 ? ORB_E_INVALID : ORB_E_HIP;
     if (m->d2h_counts(nmatches, d_cnt, (size_t)count * 4) || m->d2h_counts(nvisible, d_cnt + count, (size_t)count * 4))
         return ORB_E_HIP;

@@ -176,83 +176,75 @@ __device__ __forceinline__ double dist2(const double* p1, const double* p2) {
     return (p1[0] - p2[0]) * (p1[0] - p2[0]) + (p1[1] - p2[1]) * (p1[1] - p2[1]) + (p1[2] - p2[2]) * (p1[2] - p2[2]);
 }
 
-// Householder QR solve (PnPsolver.cc:860-950, incl. its row-scan quirk); false if singular.
-__device__ __forceinline__ bool qr_solve(double* A, int nr, int nc, double* b, double* X) {
-    double A1[4], A2[4];
-    double* pA = A;
-    double* ppAkk = pA;
-    for (int k = 0; k < nc; k++) {
-        double* ppAik = ppAkk;
-        double eta = fabs(*ppAik);
-        for (int i = k + 1; i < nr; i++) {
-            const double elt = fabs(*ppAik);
-            if (eta < elt) eta = elt;
-            ppAik += nc;
+// Gauss-Newton step of EPnP's beta refinement (PnPsolver.cc:840-858 calls
+// qr_solve, 860-950): least squares on the 6x4 Jacobian J by Householder
+// reflections, held in registers (fully unrolled, static indices).
+//
+// Numerics that parity pins (the column scale and every sum keep the
+// reference's order; the algorithm itself is the textbook one):
+//  - column k is scaled by 1/m_k, m_k = max |J(r,k)| taken over rows
+//    k .. 4 only: the reference's max-scan starts at the diagonal and stops
+//    one row short of the last one;
+//  - v = scaled column with v_k += s, s = sign(v_k)·||v||; the reflector's
+//    norm term is s·v_k and the R diagonal is -m_k·s;
+//  - reflections are applied to the later columns, then to the right-hand
+//    side, column by column; back substitution runs bottom-up.
+// Returns false (x untouched) when a column is exactly zero.
+__device__ __forceinline__ bool householder_ls_6x4(double (&J)[6][4], double (&rhs)[6], double (&x)[4]) {
+    double vnorm[4], rdiag[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double m = fabs(J[k][k]);
+#pragma unroll
+        for (int r = k; r < 5; ++r) m = (m < fabs(J[r][k])) ? fabs(J[r][k]) : m;
+        if (m == 0) return false;
+        const double inv_m = 1. / m;
+        double ss = 0.0;
+#pragma unroll
+        for (int r = k; r < 6; ++r) {
+            J[r][k] *= inv_m;
+            ss += J[r][k] * J[r][k];
         }
-        if (eta == 0) return false;
-        double* pp = ppAkk;
-        double sum = 0.0, inv_eta = 1. / eta;
-        for (int i = k; i < nr; i++) {
-            *pp *= inv_eta;
-            sum += *pp * *pp;
-            pp += nc;
+        const double s = (J[k][k] < 0) ? -sqrt(ss) : sqrt(ss);
+        J[k][k] += s;
+        vnorm[k] = s * J[k][k];
+        rdiag[k] = -m * s;
+#pragma unroll
+        for (int c = k + 1; c < 4; ++c) {
+            double proj = 0;
+#pragma unroll
+            for (int r = k; r < 6; ++r) proj += J[r][k] * J[r][c];
+            const double f = proj / vnorm[k];
+#pragma unroll
+            for (int r = k; r < 6; ++r) J[r][c] -= f * J[r][k];
         }
-        double sigma = sqrt(sum);
-        if (*ppAkk < 0) sigma = -sigma;
-        *ppAkk += sigma;
-        A1[k] = sigma * *ppAkk;
-        A2[k] = -eta * sigma;
-        for (int j = k + 1; j < nc; j++) {
-            double* p2 = ppAkk;
-            double s2 = 0;
-            for (int i = k; i < nr; i++) {
-                s2 += *p2 * p2[j - k];
-                p2 += nc;
-            }
-            const double tau = s2 / A1[k];
-            p2 = ppAkk;
-            for (int i = k; i < nr; i++) {
-                p2[j - k] -= tau * *p2;
-                p2 += nc;
-            }
-        }
-        ppAkk += nc + 1;
     }
-    double* ppAjj = pA;
-    for (int j = 0; j < nc; j++) {
-        double* ppAij = ppAjj;
-        double tau = 0;
-        for (int i = j; i < nr; i++) {
-            tau += *ppAij * b[i];
-            ppAij += nc;
-        }
-        tau /= A1[j];
-        ppAij = ppAjj;
-        for (int i = j; i < nr; i++) {
-            b[i] -= tau * *ppAij;
-            ppAij += nc;
-        }
-        ppAjj += nc + 1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double proj = 0;
+#pragma unroll
+        for (int r = k; r < 6; ++r) proj += J[r][k] * rhs[r];
+        proj /= vnorm[k];
+#pragma unroll
+        for (int r = k; r < 6; ++r) rhs[r] -= proj * J[r][k];
     }
-    X[nc - 1] = b[nc - 1] / A2[nc - 1];
-    for (int i = nc - 2; i >= 0; i--) {
-        double* ppAij = pA + i * nc + (i + 1);
-        double sum = 0;
-        for (int j = i + 1; j < nc; j++) {
-            sum += *ppAij * X[j];
-            ppAij++;
-        }
-        X[i] = (b[i] - sum) / A2[i];
+    x[3] = rhs[3] / rdiag[3];
+#pragma unroll
+    for (int i = 2; i >= 0; --i) {
+        double acc = 0;
+#pragma unroll
+        for (int c = i + 1; c < 4; ++c) acc += J[i][c] * x[c];
+        x[i] = (rhs[i] - acc) / rdiag[i];
     }
     return true;
 }
 
 __device__ __forceinline__ void gauss_newton(const double* L, const double* rho, double betas[4]) {
-    double A[24], b[6], x[4] = {0, 0, 0, 0};
+    double A[6][4], b[6], x[4] = {0, 0, 0, 0};
     for (int k = 0; k < 5; k++) {
         for (int i = 0; i < 6; i++) {
             const double* rowL = L + i * 10;
-            double* rowA = A + i * 4;
+            double* rowA = A[i];
             rowA[0] = 2 * rowL[0] * betas[0] + rowL[1] * betas[1] + rowL[3] * betas[2] + rowL[6] * betas[3];
             rowA[1] = rowL[1] * betas[0] + 2 * rowL[2] * betas[1] + rowL[4] * betas[2] + rowL[7] * betas[3];
             rowA[2] = rowL[3] * betas[0] + rowL[4] * betas[1] + 2 * rowL[5] * betas[2] + rowL[8] * betas[3];
@@ -262,7 +254,7 @@ __device__ __forceinline__ void gauss_newton(const double* L, const double* rho,
                              rowL[6] * betas[0] * betas[3] + rowL[7] * betas[1] * betas[3] + rowL[8] * betas[2] * betas[3] +
                              rowL[9] * betas[3] * betas[3]);
         }
-        qr_solve(A, 6, 4, b, x);  // singular: x keeps its previous value
+        householder_ls_6x4(A, b, x);  // singular: x keeps its previous value
         for (int i = 0; i < 4; i++) betas[i] += x[i];
     }
 }

@@ -32,12 +32,15 @@ namespace orbgpu {
 // epoch (an event on the stream); epochs finish in order -- wait for the event, copy the counts
 // to the callers' arrays, release the blocks -- so the next chain can be queued while an older
 // one still runs.  wait() (event only) may be called from another host thread.
+//
+// Each epoch owns its event until it is finished and no waiter holds it: an event is never
+// re-recorded while a host thread may be synchronising on it, however many epochs are open.
 class DeferredChain {
 public:
     ~DeferredChain() {
         for (auto& b : blocks_) (void)hipHostFree(b.p);
         for (auto& e : events_)
-            if (e) (void)hipEventDestroy(e);
+            if (e.ev) (void)hipEventDestroy(e.ev);
     }
     bool on() const { return on_; }
     void set(bool v) { on_ = v; }
@@ -56,11 +59,16 @@ public:
     // close the current chain: record its end on `s`; *id = its epoch
     int close(hipStream_t s, long long* id) {
         std::lock_guard<std::mutex> g(mu_);
+        size_t k = 0;
+        while (k < events_.size() && (events_[k].live || events_[k].waiters > 0)) k++;
+        if (k == events_.size()) {
+            events_.push_back(Ev{});
+            ORB_HIP_CHECK(hipEventCreateWithFlags(&events_[k].ev, hipEventDisableTiming));
+        }
+        ORB_HIP_CHECK(hipEventRecord(events_[k].ev, s));
+        events_[k].live = true;
         const long long e = next_id_++;
-        hipEvent_t& ev = events_[e % kEvents];
-        if (!ev) ORB_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        ORB_HIP_CHECK(hipEventRecord(ev, s));
-        closed_.push_back(Epoch{e, std::move(cur_blocks_), std::move(cur_outs_)});
+        closed_.push_back(Epoch{e, (int)k, std::move(cur_blocks_), std::move(cur_outs_)});
         cur_blocks_.clear();
         cur_outs_.clear();
         if (id) *id = e;
@@ -68,31 +76,48 @@ public:
     }
     // host wait for epoch `id` to complete on the device (no landing); any thread
     int wait(long long id) {
+        int k = -1;
         hipEvent_t ev = nullptr;
         {
             std::lock_guard<std::mutex> g(mu_);
-            if (id <= done_id_ || id >= next_id_) return 0;
-            ev = events_[id % kEvents];   // re-recorded only kEvents epochs later: never earlier
+            for (const Epoch& ep : closed_)
+                if (ep.id == id) k = ep.ev;
+            if (k < 0) return 0;   // finished already (or never closed)
+            events_[k].waiters++;
+            ev = events_[k].ev;
         }
-        ORB_HIP_CHECK(hipEventSynchronize(ev));
-        return 0;
+        const hipError_t rc = hipEventSynchronize(ev);
+        std::lock_guard<std::mutex> g(mu_);
+        events_[k].waiters--;
+        return rc == hipSuccess ? 0 : -2;
     }
-    // finish every closed epoch up to `id`, in order
+    // finish every closed epoch up to `id`, in order.  An epoch stays in closed_ until its
+    // event has completed, so wait() from another thread never returns early.
     int finish_upto(long long id) {
+        std::lock_guard<std::mutex> fg(finish_mu_);
         for (;;) {
-            Epoch ep;
+            int k;
             hipEvent_t ev;
             {
                 std::lock_guard<std::mutex> g(mu_);
                 if (closed_.empty() || closed_.front().id > id) return 0;
+                k = closed_.front().ev;
+                events_[k].waiters++;
+                ev = events_[k].ev;
+            }
+            const hipError_t rc = hipEventSynchronize(ev);
+            Epoch ep;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                events_[k].waiters--;
+                if (rc != hipSuccess) return -2;
                 ep = std::move(closed_.front());
                 closed_.pop_front();
-                ev = events_[ep.id % kEvents];
+                events_[k].live = false;
             }
-            ORB_HIP_CHECK(hipEventSynchronize(ev));
             for (auto& o : ep.outs) std::memcpy(o.user, o.pin, o.bytes);
             std::lock_guard<std::mutex> g(mu_);
-            for (int k : ep.blocks) blocks_[k].busy = false;
+            for (int b : ep.blocks) blocks_[b].busy = false;
             done_id_ = ep.id;
         }
     }
@@ -104,7 +129,6 @@ public:
     }
 
 private:
-    static constexpr int kEvents = 16;
     struct Block {
         void* p;
         size_t cap;
@@ -117,8 +141,14 @@ private:
     };
     struct Epoch {
         long long id;
+        int ev;   // index into events_
         std::vector<int> blocks;
         std::vector<Out> outs;
+    };
+    struct Ev {
+        hipEvent_t ev = nullptr;
+        bool live = false;   // recorded for an epoch not finished yet
+        int waiters = 0;     // host threads inside hipEventSynchronize on it
     };
     void* take(size_t bytes) {
         bytes = (bytes + 255) & ~(size_t)255;
@@ -138,11 +168,12 @@ private:
     }
     bool on_ = false;
     std::mutex mu_;
+    std::mutex finish_mu_;   // one finisher at a time (epochs finish in order)
     std::vector<Block> blocks_;
     std::vector<int> cur_blocks_;
     std::vector<Out> cur_outs_;
     std::deque<Epoch> closed_;
-    hipEvent_t events_[kEvents] = {};
+    std::vector<Ev> events_;
     long long next_id_ = 1, done_id_ = 0;
 };
 

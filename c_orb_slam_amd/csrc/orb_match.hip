@@ -880,7 +880,7 @@ void* Matcher::arena_alloc(size_t bytes) {
     return p;
 }
 
-int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastMode) {
+int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastMode, float nnratio) {
     const int np = (int)probs.size();
     if (np == 0) return 0;
     size_t need = 0;
@@ -951,7 +951,7 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
             mark(2);
             // nq = the last frame's N <= kMaxFrameKeys = 512 * kSelQLast: every query in a slot
             hipLaunchKernelGGL((k_select_r<true, 512, kSelQLast>), dim3(np), dim3(512), select_lds_bytes(maxN), stream_, dp,
-                               th, (int)bMono, nnratio_, (int)checkOri_, maxN);
+                               th, (int)bMono, nnratio, (int)checkOri_, maxN);
         } else {
             hipLaunchKernelGGL(k_candidates<false>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0,
                                counters());
@@ -959,7 +959,7 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
             // SearchLocalPoints-sized query sets (thousands of local map points, long occupancy
             // chains between duplicated points): 16 waves per round of the fixed point
             hipLaunchKernelGGL((k_select_r<false, kSelectLocalThreads, kSelQLocal>), dim3(np), dim3(kSelectLocalThreads),
-                               select_lds_bytes(maxN), stream_, dp, th, 0, nnratio_, 0, maxN);
+                               select_lds_bytes(maxN), stream_, dp, th, 0, nnratio, 0, maxN);
         }
     } else {
         mark(2);
@@ -969,7 +969,9 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     return 0;
 }
 
-int Matcher::search_last(std::vector<SearchDev>& probs, float th, bool bMono) { return run(probs, th, bMono, true); }
+int Matcher::search_last(std::vector<SearchDev>& probs, float th, bool bMono) {
+    return run(probs, th, bMono, true, nnratio_);
+}
 
 int Matcher::frustum(std::vector<SearchDev>& probs, const std::vector<FrustumDev>& fr, float viewingCosLimit,
                      float logScaleFactor) {
@@ -996,7 +998,7 @@ int Matcher::frustum(std::vector<SearchDev>& probs, const std::vector<FrustumDev
 }
 
 int Matcher::search_local_points(std::vector<SearchDev>& probs, std::vector<FrustumDev>& fr, float viewingCosLimit,
-                                 float logScaleFactor, float th) {
+                                 float logScaleFactor, float th, float nnratio) {
     const int np = (int)probs.size();
     if (np == 0) return 0;
     int maxq = 0;
@@ -1028,11 +1030,11 @@ int Matcher::search_local_points(std::vector<SearchDev>& probs, std::vector<Frus
         frustumCos_ = viewingCosLimit;
         frustumLsf_ = logScaleFactor;
     }
-    const int rc = run(probs, th, false, false);
+    const int rc = run(probs, th, false, false, nnratio);
     frustum_ = nullptr;
     return rc;
 }
-int Matcher::search_local(std::vector<SearchDev>& probs, float th) { return run(probs, th, false, false); }
+int Matcher::search_local(std::vector<SearchDev>& probs, float th) { return run(probs, th, false, false, nnratio_); }
 
 int Matcher::candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, const int* off, const int* cand, int* dist,
                         int* best_idx, int* best_dist, int* second_dist) {

@@ -99,9 +99,10 @@ public:
     int search_last(std::vector<SearchDev>& probs, float th, bool bMono);
     int search_local(std::vector<SearchDev>& probs, float th);
     // Tracking::SearchLocalPoints: isInFrustum(pMP, viewingCosLimit) on the device for every
-    // local map point of each problem, then SearchByProjection(F, vpLocalMapPoints, th)
+    // local map point of each problem, then SearchByProjection(F, vpLocalMapPoints, th) with
+    // ratio `nnratio` (the reference's SearchLocalPoints builds its own ORBmatcher(0.8))
     int search_local_points(std::vector<SearchDev>& probs, std::vector<FrustumDev>& fr, float viewingCosLimit,
-                            float logScaleFactor, float th);
+                            float logScaleFactor, float th, float nnratio);
     // Frame::isInFrustum only (outputs in fr's device arrays; arena-allocated problem copy)
     int frustum(std::vector<SearchDev>& probs, const std::vector<FrustumDev>& fr, float viewingCosLimit,
                 float logScaleFactor);
@@ -150,7 +151,7 @@ public:
     int zero_counters(int first, int n);
 
 private:
-    int run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastMode);
+    int run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastMode, float nnratio);
     float nnratio_;
     bool checkOri_;
     bool device_ptrs_ = false;

@@ -78,6 +78,17 @@ class ORBextractor:
               "ORBextractor_extract_batch(device)")
         return n
 
+    def extract_host_to_device(self, image, d_kps_ptr, d_desc_ptr, cap):
+        """operator() on a host (pageable) image, keypoints and descriptors left in HBM for the
+        device-resident tracking calls: the H2D copy of the image is part of the call.  -> count."""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        H, W = img.shape
+        n = np.zeros(1, np.int32)
+        check(self._L.ORBextractor_extract_batch(self._h, ptr(img), 1, W, H, img.strides[0], img.strides[0] * H, 0,
+                                                 C.c_void_p(d_kps_ptr), C.c_void_p(d_desc_ptr), cap, 1, ptr(n)),
+              "ORBextractor_extract_batch(host image)")
+        return n
+
     def image_pyramid_level(self, level, index=0):
         """mvImagePyramid[level] WITH its 19-px border (ORBextractor.h:85)."""
         w, h = C.c_int(), C.c_int()
@@ -389,10 +400,11 @@ class ORBmatcher:
         del keep
         return res
 
-    def SearchLocalPoints(self, frames, cur_mps, maps, logScaleFactor, th=1.0, deferred=False):
+    def SearchLocalPoints(self, frames, cur_mps, maps, logScaleFactor, th=1.0, deferred=False, nnratio=0.0):
         """Tracking::SearchLocalPoints (Tracking.cc:1143-1193): isInFrustum(pMP, 0.5) + SearchByProjection(F,
         mvpLocalMapPoints, th) per frame on the device (ORBmatcher_SearchLocalPoints_batch); cur_mps[f] (int32
-        numpy, F.N) updated in place.  -> (nmatches, nvisible) arrays."""
+        numpy, F.N) updated in place.  nnratio > 0 overrides this matcher's ratio for the call (the reference
+        uses ORBmatcher(0.8), Tracking.cc:1184).  -> (nmatches, nvisible) arrays."""
         import torch
         dev = torch.device("cuda", torch.cuda.current_device())
         keep, fa, ma = self._local_batch(frames, maps, dev)
@@ -406,7 +418,7 @@ class ORBmatcher:
             if deferred:   # queued on the stream; the counts land at finish (set_deferred(0))
                 check(self._L.ORBmatcher_set_deferred(self._h, 1))
             check(self._L.ORBmatcher_SearchLocalPoints_batch(self._h, len(frames), fa, arr, ma, float(logScaleFactor),
-                                                             float(th), ptr(nm), ptr(nv)),
+                                                             float(th), float(nnratio), ptr(nm), ptr(nv)),
                   "ORBmatcher_SearchLocalPoints_batch")
         finally:
             if deferred:

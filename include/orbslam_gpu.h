@@ -236,7 +236,9 @@ int Frame_isInFrustum_batch(ORBmatcher_h h, int count, const orb_frame* F, const
 /* void Tracking::SearchLocalPoints()                          Tracking.cc:1143-1193
  * For every local map point not skipped: Frame::isInFrustum(pMP, 0.5) (Frame.cc:269-325,
  * MapPoint::PredictScale MapPoint.cc:402-417), then SearchByProjection(F, mvpLocalMapPoints,
- * th) with the matcher's nnratio (ORBmatcher(0.8) in the reference; ORBmatcher.cc:45-129).
+ * th) with ratio `nnratio` (the reference constructs ORBmatcher matcher(0.8) for this search,
+ * Tracking.cc:1184; ORBmatcher.cc:45-129): pass 0.8 to follow it on any matcher, or <= 0 to
+ * use the matcher's own nnratio (so one deferred chain serves every search of a step).
  * cur_mp[p] (in/out, F[p].N): mCurrentFrame.mvpMapPoints as rows of maps[p] (-1 = NULL);
  * the caller clears the outliers of the first PoseOptimization and marks the matched and
  * discarded points in `skip` first (Tracking.cc:893-913, 1146-1161).  logScaleFactor =
@@ -245,7 +247,7 @@ int Frame_isInFrustum_batch(ORBmatcher_h h, int count, const orb_frame* F, const
  * pointers(h, 1)); one launch set for all `count` frames. */
 int ORBmatcher_SearchLocalPoints_batch(ORBmatcher_h h, int count, const orb_frame* F, int32_t* const* cur_mp,
                                        const orb_localmap* maps, float logScaleFactor, float th,
-                                       int* nmatches, int* nvisible);
+                                       float nnratio, int* nmatches, int* nvisible);
 
 /* void Frame::ComputeStereoMatches()                            Frame.cc:466-640
  * Rectified stereo matching of the left keypoints of image `index` (0 only for the single
@@ -796,6 +798,10 @@ int orbgpu_unit_pnp_layout(int n, const int* N, const int* K, const int* minSet,
 int orbgpu_unit_ldlt_factor(int n, const double* S, double* out);
 /* one wave's canonical 64-tree of v64[0..64) (cross-lane permlane/DPP path) */
 int orbgpu_unit_wave_tree(const double* v64, double* out);
+/* Test knob: the BA chi2 canonical sum keeps at most m2_max level-2 trees in LDS (default and
+ * maximum 1024, i.e. 4.2 M edges) and writes larger sets to its chunk buffer's tail; 0 sends
+ * every problem down the tail path.  Process-wide, device-side. */
+int orbgpu_unit_set_csum_lds_max(int m2_max);
 /* Instrumented builds only (make prof): read and clear the BA/pose section timers (32 x u64
  * clock64 deltas of workgroup 0); ORB_E_INVALID in normal builds. */
 int orbgpu_debug_prof(unsigned long long* out32);

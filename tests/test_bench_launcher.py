@@ -32,3 +32,14 @@ def test_default_is_one_rank():
 def test_world_size_mismatch_refused():
     r = _run(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_failed_rank_stops_the_job():
+    """A rank > 0 that dies before the rendezvous leaves rank 0 blocked in init_process_group: the
+    launcher must notice, stop rank 0 and return the failing rank's code."""
+    import time
+    t0 = time.monotonic()
+    r = _run(["--gpus", "2", "--dry-run"], {"BENCH_DRY_FAIL_RANK": "1"})
+    assert r.returncode == 3, (r.returncode, r.stderr)
+    assert "rank 1 exited with 3" in r.stderr
+    assert time.monotonic() - t0 < 120

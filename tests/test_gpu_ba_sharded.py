@@ -40,6 +40,27 @@ def test_global_ba_matches_oracle(gpu, n_kf, robust):
     assert not g["edge_erase"].any()
 
 
+@pytest.mark.parametrize("lds_max", [0, 3])
+def test_global_ba_chi2_tail_path_matches_oracle(gpu, lds_max):
+    """The chi2 canonical sum keeps <= 1024 level-2 trees in LDS and sends larger problems
+    (config 5 above 4.2 M edges: 8k-16k keyframes) to the chunk buffer's tail.  Lowering the
+    LDS threshold drives the tail path at a size the oracle finishes in seconds: the LM trace
+    and the results must stay bit-identical to the oracle."""
+    from c_orb_slam_amd._lib import lib
+    from c_orb_slam_amd.optimizer import BundleAdjustment
+    pr = global_ba_problem(11, n_kf=160, pts_per_kf=60)     # ~40 k edges: 10 level-2 trees
+    assert len(pr["edge_pt"]) > 4 * 64 * 64
+    assert lib().orbgpu_unit_set_csum_lds_max(lds_max) == 0
+    try:
+        g = BundleAdjustment(pr, 10, False, trace=True)
+    finally:
+        assert lib().orbgpu_unit_set_csum_lds_max(1024) == 0
+    o = oracle_lib.oracle_global_ba(pr, 10, False)
+    assert g["iterations"] == o["iterations"]
+    np.testing.assert_allclose(g["trial_chi2"], o["trial_chi2"], rtol=1e-12)
+    _exact(g, o)
+
+
 def test_global_ba_points_without_edges_untouched(gpu):
     from c_orb_slam_amd.optimizer import BundleAdjustment
     pr = global_ba_problem(3, n_kf=10, pts_per_kf=40)

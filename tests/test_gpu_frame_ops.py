@@ -179,3 +179,64 @@ def test_deferred_chain_equals_synchronous(gpu):
         for f in range(3):
             assert np.array_equal(T[f].cpu().numpy(), T0[f].cpu().numpy())
             assert np.array_equal(o[f].cpu().numpy(), o0[f].cpu().numpy())
+
+
+def test_deferred_and_synchronous_pose_interleaved(gpu):
+    """The pose engine's device arena is shared by every PoseOptimization call of a host thread.
+    A deferred batch still queued on one matcher's stream, then a synchronous batch (larger, so
+    the arena grows), then a deferred batch on a second matcher: each must give its own
+    standalone result (the arena's next user waits for the queued kernels that read it)."""
+    import torch
+    from c_orb_slam_amd._lib import check, lib
+    from c_orb_slam_amd.optimizer import PoseOptimizationFramesDevice
+    dev = torch.device("cuda", 0)
+
+    def framed_of(seeds, base_n):
+        out = []
+        for i, s in enumerate(seeds):
+            fr = pose_problem(s, N=base_n + 350 * i)
+            N = len(fr["has_mp"])
+            octv, tab = _octaves(fr["inv_sigma2"])
+            k = np.zeros(N, oracle_lib.KP_DTYPE)
+            k["x"], k["y"], k["octave"] = fr["obs"][:, 0], fr["obs"][:, 1], octv
+            mp = np.where(fr["has_mp"] > 0, np.arange(N), -1).astype(np.int32)
+            out.append(dict(Tcw=torch.from_numpy(np.ascontiguousarray(fr["Tcw"], np.float32).reshape(16)).to(dev),
+                            mp=torch.from_numpy(mp).to(dev), mp_pos=torch.from_numpy(fr["Xw"]).to(dev),
+                            keysUn=torch.from_numpy(k.view(np.int32).reshape(N, 7).copy()).to(dev),
+                            uRight=torch.from_numpy(np.ascontiguousarray(fr["obs"][:, 2])).to(dev),
+                            invLevelSigma2=torch.from_numpy(tab).to(dev), cam=fr["cam"]))
+        return out
+
+    A = framed_of([910, 911], 300)
+    B = framed_of([920, 921, 922, 923, 924, 925], 900)     # more edges than A: the arena grows
+    Cf = framed_of([930, 931, 932], 500)
+    outs = lambda fs: ([torch.zeros(16, dtype=torch.float32, device=dev) for _ in fs],
+                       [torch.full((f["mp"].numel(),), 9, dtype=torch.uint8, device=dev) for f in fs])
+    ref = {}
+    for name, fs in (("A", A), ("B", B), ("C", Cf)):
+        T, o = outs(fs)
+        n = PoseOptimizationFramesDevice(fs, T, o)
+        ref[name] = (n, [t.cpu().numpy() for t in T], [x.cpu().numpy() for x in o])
+    L = lib()
+    m1, m2 = gpu.ORBmatcher(0.8, False), gpu.ORBmatcher(0.8, False)
+    for m in (m1, m2):
+        check(L.ORBmatcher_set_device_pointers(m._h, 1))
+        check(L.ORBmatcher_set_deferred(m._h, 1))
+    TA, oA = outs(A)
+    nA = np.full(len(A), -9, np.int32)
+    PoseOptimizationFramesDevice(A, TA, oA, chain=m1, n_out=nA)        # queued, not finished
+    TB, oB = outs(B)
+    nB = PoseOptimizationFramesDevice(B, TB, oB)                        # synchronous, own stream
+    TC, oC = outs(Cf)
+    nC = np.full(len(Cf), -9, np.int32)
+    PoseOptimizationFramesDevice(Cf, TC, oC, chain=m2, n_out=nC)       # another matcher's stream
+    check(L.ORBmatcher_finish(m2._h))
+    check(L.ORBmatcher_finish(m1._h))
+    for m in (m1, m2):
+        check(L.ORBmatcher_set_deferred(m._h, 0))
+    for name, n, T, o in (("A", nA, TA, oA), ("B", nB, TB, oB), ("C", nC, TC, oC)):
+        rn, rT, ro = ref[name]
+        assert np.array_equal(np.asarray(n), np.asarray(rn)), name
+        for f in range(len(T)):
+            assert np.array_equal(T[f].cpu().numpy(), rT[f]), (name, f)
+            assert np.array_equal(o[f].cpu().numpy(), ro[f]), (name, f)

@@ -132,6 +132,32 @@ def test_search_local_points_matches_oracle(gpu, seq, th):
         assert no > 50
 
 
+def test_search_local_points_ratio_override(gpu, seq):
+    """The reference's SearchLocalPoints builds ORBmatcher(0.8) (Tracking.cc:1184) while TrackWithMotionModel's
+    matcher is ORBmatcher(0.9, true) (Tracking.cc:869): a 0.9-constructed matcher given nnratio=0.8 for the call must
+    give the oracle's 0.8 result (so one deferred chain serves both searches), and 0.9 where it differs."""
+    Rs, res, scale = seq
+    lsf = np.float32(np.log(np.float32(1.2)))
+    rng = np.random.default_rng(77)
+    frames, maps, cms = [], [], []
+    for f in range(3):
+        (k0, d0), (k1, d1) = res[f], res[f + 1]
+        M = local_map(rng, k0, d0, scale)
+        frames.append(cur_frame(rng, k1, d1, scale, Rs[f], stereo=True))
+        maps.append(M)
+        cms.append(np.full(frames[-1].N, -1, np.int32))
+    m = gpu.ORBmatcher(0.9, True)
+    for ratio, deferred in ((0.8, False), (0.8, True), (0.0, False)):
+        g = [c.copy() for c in cms]
+        nm, nv = m.SearchLocalPoints(frames, g, maps, lsf, 1.0, deferred=deferred, nnratio=ratio)
+        want = ratio if ratio > 0 else 0.9
+        for F, M, c0, gc, n1, n2 in zip(frames, maps, cms, g, nm, nv):
+            oc = c0.copy()
+            no, nvo = oracle_lib.oracle_search_local_points(F, oc, M, lsf, 1.0, want)
+            assert (n1, n2) == (no, nvo), (ratio, n1, no)
+            assert np.array_equal(gc, oc)
+
+
 def test_create_stereo_points_and_local_prep(gpu):
     """MapPoint_CreateStereo_batch_device (UnprojectStereo + UpdateNormalAndDepth for one
     observation) against the oracle's UnprojectStereo and the float / double convention written

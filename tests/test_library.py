@@ -116,3 +116,63 @@ def test_optimize_sim3_validates_without_device():
     P.th2 = 10.0
     if not orb.device_available():
         assert L.Optimizer_OptimizeSim3(C.byref(P), ptr(S), ptr(er), C.byref(n)) == ORB_E_NODEVICE
+
+
+def _abi_image():
+    """tests/c_abi/abi_caller.c's seeded 640x480 image, restated (uint32 LCG, 8-bit blocks + noise)."""
+    W, H = 640, 480
+    img = np.zeros((H, W), np.uint8)
+    s = 12345
+    for y in range(H):
+        for x in range(W):
+            s = (s * 1664525 + 1013904223) & 0xFFFFFFFF
+            img[y, x] = ((x // 40) * 37 + (y // 30) * 91) % 200 + ((s >> 24) & 31)
+    return img
+
+
+def test_c11_caller_compiles_links_and_runs(tmp_path):
+    """A plain C11 translation unit includes include/orbslam_gpu.h with -std=c11 -pedantic -Werror,
+    links against liborbslam_gpu.so and calls it: the host-only entry points answer, and without
+    a device the create() calls report ORB_E_NODEVICE."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    exe = tmp_path / "abi_caller"
+    r = subprocess.run([cc, "-std=c11", "-pedantic", "-Wall", "-Wextra", "-Werror", "-O1", f"-I{root / 'include'}",
+                        str(root / "tests" / "c_abi" / "abi_caller.c"), f"-L{root / 'c_orb_slam_amd'}", "-lorbslam_gpu",
+                        f"-Wl,-rpath,{root / 'c_orb_slam_amd'}", "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "abi_caller ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_c11_caller_extracts_like_the_python_binding(tmp_path):
+    """The prebuilt C11 caller (make abi -> build/abi_caller) runs ORBextractor_extract from host
+    buffers to host buffers on the GPU; its keypoints and descriptors equal the ctypes binding's
+    and the oracle's, byte for byte."""
+    import subprocess
+    from pathlib import Path
+    import oracle_lib
+    root = Path(__file__).resolve().parents[1]
+    exe = root / "build" / "abi_caller"
+    assert exe.exists(), "build/abi_caller missing: run `make abi` before the GPU tests"
+    out = tmp_path / "kps.bin"
+    r = subprocess.run([str(exe), str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    raw = out.read_bytes()
+    n = int(np.frombuffer(raw[:4], np.int32)[0])
+    ck = np.frombuffer(raw[4:4 + 28 * n], dtype=np.uint8)
+    cd = np.frombuffer(raw[4 + 28 * n:4 + 60 * n], dtype=np.uint8).reshape(n, 32)
+    img = _abi_image()
+    kps, desc = orb.ORBextractor(1000, 1.2, 8, 20, 7, max_width=640, max_height=480)(img)
+    assert len(kps) == n
+    assert np.array_equal(kps.view(np.uint8).reshape(-1), ck)
+    assert np.array_equal(desc, cd)
+    okps, odesc = oracle_lib.OracleExtractor(1000, 1.2, 8, 20, 7)(img)
+    assert np.array_equal(okps.view(np.uint8).reshape(-1), ck) and np.array_equal(odesc, cd)
