@@ -118,7 +118,7 @@ def _rot_y(a):
 
 
 def global_ba_problem(seed=0, n_kf=64, pts_per_kf=150, obs_range=(3, 10), stereo_frac=0.5, cam=KITTI,
-                      pose_noise=(0.02, 0.2), point_noise=0.1):
+                      pose_noise=(0.02, 0.2), point_noise=0.1, laps=0, loop_frac=0.05, loop_obs=(1, 3)):
     """Merged-map global-BA-shaped problem (KITTI intrinsics).
 
     Keyframes ~1 m apart along a gently turning drive; each keyframe creates `pts_per_kf`
@@ -126,14 +126,28 @@ def global_ba_problem(seed=0, n_kf=64, pts_per_kf=150, obs_range=(3, 10), stereo
     its creator (visibility-checked, >= 2 observations).  No gross outliers: LoopClosing
     runs BundleAdjustment with bRobust=false (LoopClosing.cc:650).  Keyframe mnId = index
     (id 0 fixed); edges in map-point order, each point's observations in shuffled order.
-    Vectorised numpy (10^5-10^6 edges in seconds)."""
+    Vectorised numpy (10^5-10^6 edges in seconds).
+
+    laps >= 2: the drive is a circuit driven `laps` times (n_kf / laps keyframes per lap, each
+    lap 0.5 m further out), the shape of a map whose loops LoopClosing has closed before
+    GlobalBundleAdjustemnt runs (LoopClosing.cc:231-360, 650): a `loop_frac` share of the
+    points is also observed by U{loop_obs} keyframes at the same place on every other lap (the
+    observations SearchAndFuse adds), so keyframes far apart in mnId share points and the
+    pose system gains long-range covisibility, not just a band."""
     rng = np.random.default_rng(seed)
     fx, fy, cx, cy, bf = cam
     W, H = KITTI_WH
-    yaw = np.cumsum(rng.normal(0, 0.02, n_kf))
+    if laps >= 2:
+        n_lap = n_kf // laps
+        idx = np.arange(n_kf)
+        yaw = 2 * np.pi * (idx % n_lap) / n_lap + rng.normal(0, 0.002, n_kf)
+        R = n_lap / (2 * np.pi) + 0.5 * (idx // n_lap)
+        twc = np.stack([R - R * np.cos(yaw), rng.normal(0, 0.05, n_kf), R * np.sin(yaw)], 1)
+    else:
+        yaw = np.cumsum(rng.normal(0, 0.02, n_kf))
+        step = np.stack([np.sin(yaw), np.zeros(n_kf), np.cos(yaw)], 1)
+        twc = np.cumsum(step, 0) - step[0]
     Rwc = np.stack([_rot_y(a) for a in yaw])
-    step = np.stack([np.sin(yaw), np.zeros(n_kf), np.cos(yaw)], 1)
-    twc = np.cumsum(step, 0) - step[0]
     Rcw = np.transpose(Rwc, (0, 2, 1))
     tcw = -np.einsum("kij,kj->ki", Rcw, twc)
     # candidate points in each creator keyframe's frame
@@ -158,7 +172,26 @@ def global_ba_problem(seed=0, n_kf=64, pts_per_kf=150, obs_range=(3, 10), stereo
         ok &= (zz > 1.0) & (uu >= 10) & (uu < W - 10) & (vv >= 10) & (vv < H - 10)
         pe.append(np.flatnonzero(ok))
         ke.append(kf[ok])
+    if laps >= 2:   # loop closures: the same place on the other laps
+        lp = np.flatnonzero(rng.random(n) < loop_frac)
+        kl = rng.integers(loop_obs[0], loop_obs[1] + 1, len(lp))
+        base = creator[lp] % n_lap
+        for m in range(laps):
+            for j in range(loop_obs[1]):
+                kf = base + m * n_lap + j
+                ok = (j < kl) & (kf < n_kf) & (kf // n_lap != creator[lp] // n_lap) & (kf != creator[lp])
+                kfc = np.minimum(kf, n_kf - 1)
+                Xcj = np.einsum("nij,nj->ni", Rcw[kfc], Xw[lp]) + tcw[kfc]
+                zz = Xcj[:, 2]
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    uu, vv = fx * Xcj[:, 0] / zz + cx, fy * Xcj[:, 1] / zz + cy
+                ok &= (zz > 1.0) & (uu >= 10) & (uu < W - 10) & (vv >= 10) & (vv < H - 10)
+                pe.append(lp[ok])
+                ke.append(kf[ok])
     pe, ke = np.concatenate(pe), np.concatenate(ke)
+    # one observation per (point, keyframe) (a KeyFrame holds a MapPoint once)
+    _, first = np.unique(pe.astype(np.int64) * n_kf + ke, return_index=True)
+    pe, ke = pe[np.sort(first)], ke[np.sort(first)]
     cnt = np.bincount(pe, minlength=n)
     keep = cnt >= 2
     newid = np.cumsum(keep) - 1
