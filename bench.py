@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--gba-kf", type=int, default=2000,
                     help="keyframes of the sharded global-BA problem (SURVEY config 5: 2k, 8k, 16k)")
     ap.add_argument("--gba-reps", type=int, default=3)
+    ap.add_argument("--gba-laps", type=int, default=-1,
+                    help="loop-closed map: the keyframes drive this many laps of one circuit (-1: one lap per "
+                         "500 keyframes; 0: an open drive, a pure band)")
     ap.add_argument("--launch-timeout", type=float, default=3000.0,
                     help="bound on the whole job when bench.py spawns its own ranks (seconds)")
     ap.add_argument("--passes-only", action="store_true",
@@ -843,13 +846,13 @@ def main():
     # global BA (SURVEY config 5): ONE problem keyframe-block sharded over the ranks, RCCL exchange
     gba = bench_global_ba(args, world, rank, dist if world > 1 else None, dev)
     if inline_cpu:
-        gba["cpu_baseline"] = gba_cpu_baseline(args.gba_kf)
+        gba["cpu_baseline"] = gba_cpu_baseline(args.gba_kf, gba_laps(args))
     # RANSAC hypothesis scoring (SURVEY config 3): every rank runs it (replicas), rank 0 reports
     ransac = bench_ransac(cpu=inline_cpu, cpu_budget_s=args.cpu_seconds / 3)
     if want_cpu and world > 1:
         cpu = cpu_baseline(lefts, rights, Rs, args.cpu_seconds)
         ba["cpu_baseline"] = ba_cpu_baseline(args.cpu_seconds / 4)
-        gba["cpu_baseline"] = gba_cpu_baseline(args.gba_kf)
+        gba["cpu_baseline"] = gba_cpu_baseline(args.gba_kf, gba_laps(args))
         ransac_cpu_into(ransac, args.cpu_seconds / 3)
     if world > 1:
         dist.barrier()
@@ -952,6 +955,10 @@ def bench_local_ba(args, world, rank, dist, dev):
             "dtype": "f64 (f32 I/O)"}
 
 
+def gba_laps(args):
+    return args.gba_kf // 500 if args.gba_laps < 0 else args.gba_laps
+
+
 def bench_global_ba(args, world, rank, dist, dev):
     """Optimizer::BundleAdjustment (nIterations=10, bRobust=false, LoopClosing.cc:650) on one
     merged-map-shaped problem (SURVEY config 5, KITTI intrinsics), keyframe-block sharded over
@@ -961,7 +968,7 @@ def bench_global_ba(args, world, rank, dist, dev):
     sys.path.insert(0, str(ROOT / "tests"))
     from ba_cases import global_ba_problem
     from c_orb_slam_amd.optimizer import BundleAdjustmentSharded, Comm, partition_points, shard_problem
-    pr = global_ba_problem(0, n_kf=args.gba_kf, pts_per_kf=150)
+    pr = global_ba_problem(0, n_kf=args.gba_kf, pts_per_kf=150, laps=gba_laps(args))
     shard = shard_problem(pr, partition_points(pr, world), rank)
     uid = [Comm.unique_id() if rank == 0 else None]
     if dist is not None:
@@ -986,7 +993,9 @@ def bench_global_ba(args, world, rank, dist, dev):
     return {"metric": "global-BA iter/s", "value": round(its / dt, 2), "unit": "iter/s",
             "ms_per_call": round(dt / args.gba_reps * 1e3, 3), "edges_per_s": round(its * ne / dt, 1),
             "scaling": "strong", "calls": args.gba_reps,
-            "config": {"workload": "kitti_merged_map_global_ba (SURVEY config 5)", "keyframes": args.gba_kf,
+            "config": {"workload": "kitti_merged_map_global_ba (SURVEY config 5): loop-closed map, "
+                                   f"{gba_laps(args)} laps of one circuit, 5% of the points covisible across laps",
+                       "keyframes": args.gba_kf, "laps": gba_laps(args),
                        "points": len(pr["pt_id"]), "edges": ne, "edges_per_rank": len(shard["edge_pt"]),
                        "lm": "optimize(10), bRobust=false", "parallelism": f"keyframe-block shards x{world} (RCCL)"},
             "dtype": "f64 (f32 I/O)"}
@@ -1166,7 +1175,8 @@ def timing_oracle():
     out = Path(tempfile.gettempdir()) / f"liborb_oracle_timing_{os.getpid()}.so"
     flags = ["-O3", "-march=native", "-std=gnu11", "-fPIC"]
     srcs = [str(src / f) for f in ("ocv_semantics.c", "orb_extract.c", "orb_match.c", "rng.c", "linalg.c", "pnp.c",
-                                   "sim3.c", "ba.c", "stereo.c", "matchers2.c", "matchers3.c", "dbow2.c")]
+                                   "sim3.c", "ba.c", "stereo.c", "matchers2.c", "matchers3.c", "dbow2.c",
+                                   "ordering.c")]
     try:
         subprocess.run(["gcc"] + flags + ["-shared", "-o", str(out)] + srcs + ["-lm"], check=True,
                        capture_output=True, timeout=300)
@@ -1203,14 +1213,16 @@ def _streams(P, fn):
     return res, time.perf_counter() - t0
 
 
-def gba_cpu_baseline(n_kf, n_its=10):
-    """Oracle BundleAdjustment(nIterations=10, bRobust=false) on the same config-5 problem: one
-    full call per stream, P independent streams (all-core) and the single stream alongside."""
+def gba_cpu_baseline(n_kf, laps, n_its=3):
+    """Oracle BundleAdjustment(nIterations=n_its, bRobust=false) on the same config-5 problem: one
+    call per stream, P independent streams (all-core) and the single stream alongside.  Rate =
+    LM iterations (solve() calls) per second; n_its = 3 bounds the sample (the GPU leg's 10-
+    iteration calls include the same per-call structure build)."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
     from ba_cases import global_ba_problem
     flags = timing_oracle()
-    pr = global_ba_problem(0, n_kf=n_kf, pts_per_kf=150)
+    pr = global_ba_problem(0, n_kf=n_kf, pts_per_kf=150, laps=laps)
     t0 = time.perf_counter()
     o = oracle_lib.oracle_global_ba(pr, n_its, False)
     dt1 = time.perf_counter() - t0
@@ -1220,8 +1232,8 @@ def gba_cpu_baseline(n_kf, n_its=10):
     res, wall = _streams(P, lambda i: oracle_lib.oracle_global_ba(pr, n_its, False)["iterations"][0])
     return {"value": round(sum(res) / wall, 3), "unit": "iter/s", "cores": P, "kind": "port",
             "sample": f"{P} independent oracle BundleAdjustment(nIterations={n_its}) calls on the same config-5 "
-                      f"problem ({n_kf} KFs) on {P} threads ({_cpu_model()}; affinity {aff}, cgroup quota {quota}), "
-                      f"oracle/ba.c {flags} (sparse Schur, envelope LDL^T); {sum(res)} LM solves in {wall:.1f} s",
+                      f"problem ({n_kf} KFs, {laps} laps) on {P} threads ({_cpu_model()}; affinity {aff}, cgroup quota {quota}), "
+                      f"oracle/ba.c {flags} (sparse Schur, nested-dissection block-sparse LDL^T); {sum(res)} LM solves in {wall:.1f} s",
             "single_thread": {"value": round(o["iterations"][0] / dt1, 3), "unit": "iter/s", "cores": 1,
                               "sample": f"one full call, {o['iterations'][0]} LM solves in {dt1:.1f} s"}}
 

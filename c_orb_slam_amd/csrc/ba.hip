@@ -655,6 +655,7 @@ __device__ long long g_ldlt_probe[256];
     } while (0)
 #endif
 constexpr int kLdltMax = 128;
+constexpr int kTiledMinPoses = 24;   // 6 x 24 = 144 rows: the first n the LDS-resident dense solver cannot hold
 constexpr int kDenseMaxN = 144;   // >= every n the dense single-workgroup solvers take (n^2 doubles in LDS)
 constexpr int kLdltWaves = 16;
 constexpr int kLdltRows = kLdltMax / kLdltWaves;
@@ -2323,9 +2324,40 @@ int BaEngine::build_structure(int level) {
     st_.leList = d + off[8]; st_.lpStart = d + off[9]; st_.lpList = d + off[10]; st_.blkI = d + off[11];
     st_.blkJ = d + off[12]; st_.blkStart = d + off[13]; st_.pairA = d + off[14]; st_.pairB = d + off[15];
     nTiles_ = 0;
-    tiled_ = nP > 0 && !dense_solver(6 * nP);
-    if ((comm_ || tiled_) && nP > 0) {
-        // the 64x64 tiles the Schur blocks touch (union over the shards)
+    // at least kTiledMinPoses free poses: the block-sparse nested-dissection solver (the oracle
+    // switches at the same count); below, the dense single-workgroup solvers in natural order
+    tiled_ = nP >= kTiledMinPoses;
+    if (!tiled_ && nP > 0 && !dense_solver(6 * nP)) return -3;
+    if (tiled_ && nP > 0) {
+        // block-sparse system: the pose graph (poses sharing a point; union over the shards,
+        // so every rank orders and factors the same structure) -> nested-dissection order,
+        // symbolic factorisation; S travels as the Schur-pattern prefix of the tiles
+        std::vector<int64_t> mine;
+        for (int b = 0; b < nBlk; b++)
+            if (blkI[b] != blkJ[b]) mine.push_back((int64_t)blkI[b] * nP + blkJ[b]);
+        std::vector<int64_t> all;
+        if (comm_) {
+            if (int e = gather_blocks(mine, &all)) return e;
+        } else {
+            all = std::move(mine);
+        }
+        std::sort(all.begin(), all.end());
+        all.erase(std::unique(all.begin(), all.end()), all.end());
+        std::vector<int> deg(nP + 1, 0), as(nP + 1, 0), adj(2 * all.size());
+        for (int64_t q : all) {
+            deg[q / nP]++;
+            deg[q % nP]++;
+        }
+        for (int i = 0; i < nP; i++) as[i + 1] = as[i] + deg[i];
+        std::vector<int> fillp(as.begin(), as.end() - 1);
+        for (int64_t q : all) {   // (i1, i2) ascending: every list comes out sorted
+            adj[fillp[q / nP]++] = (int)(q % nP);
+        }
+        for (int64_t q : all) adj[fillp[q % nP]++] = (int)(q / nP);
+        for (int i = 0; i < nP; i++) std::sort(adj.begin() + as[i], adj.begin() + as[i + 1]);
+        if (int e = sp_.build(6 * nP, 6, as, adj, true, stream_)) return e;
+    } else if (comm_ && nP > 0) {
+        // dense system: the 64x64 tiles the Schur blocks touch (union over the shards)
         const int n = 6 * nP, nt = (n + 63) / 64;
         std::vector<double> tm((size_t)nt * nt, 0.0);
         for (int b = 0; b < nBlk; b++) {
@@ -2334,42 +2366,68 @@ int BaEngine::build_structure(int level) {
                 for (int J = (6 * i2) / 64; J <= (6 * i2 + 5) / 64; J++)
                     if (I <= J) tm[(size_t)I * nt + J] = 1.0;
         }
-        if (comm_) {
-            if (tm.size() > scratchN_) return -3;
-            if (h2d_sync(dScratch_, tm.data(), sizeof(double) * tm.size())) return -2;
-            if (int e = comm_->allreduce(dScratch_, tm.size(), RedOp::Max, stream_)) return e;
-            if (d2h_sync(tm.data(), dScratch_, sizeof(double) * tm.size())) return -2;
-            ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        if (tm.size() > scratchN_) return -3;
+        if (h2d_sync(dScratch_, tm.data(), sizeof(double) * tm.size())) return -2;
+        if (int e = comm_->allreduce(dScratch_, tm.size(), RedOp::Max, stream_)) return e;
+        if (d2h_sync(tm.data(), dScratch_, sizeof(double) * tm.size())) return -2;
+        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        std::vector<int2> tl;
+        for (int I = 0; I < nt; I++)
+            for (int J = I; J < nt; J++)
+                if (tm[(size_t)I * nt + J] != 0.0) tl.push_back(make_int2(I, J));
+        nTiles_ = (int)tl.size();
+        const size_t need = sizeof(int2) * tl.size() + 256 + sizeof(double) * ((size_t)nTiles_ * 4096 + n);
+        if (need > packCap_) {
+            if (dPack_) (void)hipFree(dPack_);
+            dPack_ = nullptr;
+            packCap_ = 0;
+            ORB_HIP_CHECK(hipMalloc(&dPack_, need));
+            packCap_ = need;
         }
-        if (tiled_) {
-            // block-sparse system: symbolic factorisation; S travels as the Schur-pattern prefix
-            std::vector<uint8_t> mask(tm.size());
-            for (size_t q = 0; q < tm.size(); q++) mask[q] = tm[q] != 0.0;
-            if (int e = sp_.build(n, mask, stream_)) return e;
-        } else {
-            std::vector<int2> tl;
-            for (int I = 0; I < nt; I++)
-                for (int J = I; J < nt; J++)
-                    if (tm[(size_t)I * nt + J] != 0.0) tl.push_back(make_int2(I, J));
-            nTiles_ = (int)tl.size();
-            const size_t need = sizeof(int2) * tl.size() + 256 + sizeof(double) * ((size_t)nTiles_ * 4096 + n);
-            if (need > packCap_) {
-                if (dPack_) (void)hipFree(dPack_);
-                dPack_ = nullptr;
-                packCap_ = 0;
-                ORB_HIP_CHECK(hipMalloc(&dPack_, need));
-                packCap_ = need;
-            }
-            dTiles_ = (int2*)dPack_;
-            dPackBuf_ = (double*)((char*)dPack_ + ((sizeof(int2) * tl.size() + 255) & ~(size_t)255));
-            if (h2d_sync(dTiles_, tl.data(), sizeof(int2) * tl.size())) return -2;
-            ORB_HIP_CHECK(hipStreamSynchronize(stream_));
-        }
+        dTiles_ = (int2*)dPack_;
+        dPackBuf_ = (double*)((char*)dPack_ + ((sizeof(int2) * tl.size() + 255) & ~(size_t)255));
+        if (h2d_sync(dTiles_, tl.data(), sizeof(int2) * tl.size())) return -2;
+        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
     }
     ORB_HIP_CHECK(hipMemsetAsync(dX2_, 0, sizeof(double) * (6 * (size_t)nP + 3 * (size_t)nL + 1), stream_));
     if (!tiled_) ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * 36 * (size_t)nP * nP + 8, stream_));
     // the pageable hStruct_ copy must finish before the host vector is reused
     ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    return 0;
+}
+
+// All-gather of the ranks' off-diagonal Schur blocks (i1 * nP + i2) through the sum
+// all-reduce: every rank learns the per-rank counts, writes its own entries into its segment
+// of a zeroed buffer, and the sum hands every rank the concatenation in rank order.  Once per
+// structure; the values are integers below 2^53, exact in doubles.
+int BaEngine::gather_blocks(const std::vector<int64_t>& mine, std::vector<int64_t>* all) {
+    const int R = comm_->size(), me = comm_->rank();
+    std::vector<double> h(R, 0.0);
+    h[me] = (double)mine.size();
+    double* d = nullptr;
+    ORB_HIP_CHECK(hipMalloc(&d, sizeof(double) * std::max<size_t>(R, 1)));
+    int rc = 0;
+    std::vector<size_t> off(R + 1, 0);
+    if (!rc && h2d_sync(d, h.data(), sizeof(double) * R)) rc = -2;
+    if (!rc) rc = comm_->allreduce(d, (size_t)R, RedOp::Sum, stream_);
+    if (!rc && d2h_sync(h.data(), d, sizeof(double) * R)) rc = -2;
+    if (!rc && hipStreamSynchronize(stream_) != hipSuccess) rc = -2;
+    (void)hipFree(d);
+    if (rc) return rc;
+    for (int r = 0; r < R; r++) off[r + 1] = off[r] + (size_t)h[r];
+    const size_t tot = off[R];
+    all->assign(tot, 0);
+    if (tot == 0) return 0;
+    std::vector<double> buf(tot, 0.0);
+    for (size_t q = 0; q < mine.size(); q++) buf[off[me] + q] = (double)mine[q];
+    ORB_HIP_CHECK(hipMalloc(&d, sizeof(double) * tot));
+    if (h2d_sync(d, buf.data(), sizeof(double) * tot)) rc = -2;
+    if (!rc) rc = comm_->allreduce(d, tot, RedOp::Sum, stream_);
+    if (!rc && d2h_sync(buf.data(), d, sizeof(double) * tot)) rc = -2;
+    if (!rc && hipStreamSynchronize(stream_) != hipSuccess) rc = -2;
+    (void)hipFree(d);
+    if (rc) return rc;
+    for (size_t q = 0; q < tot; q++) (*all)[q] = (int64_t)buf[q];
     return 0;
 }
 
@@ -2422,8 +2480,8 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const bool use_reg = n <= kLdltMax && regShm <= ldsMax_;
     // n <= 128: register-resident single-workgroup LDL^T; S fits LDS: single-workgroup in LDS;
     // larger: block-sparse tiled LDL^T in HBM (ldlt.hip, structure from build_structure)
-    if (tiled_ != (n > 0 && !use_reg && !in_lds)) return -1;
-    const SysAddr sa = tiled_ ? sp_.addr() : SysAddr{dS_, n, nullptr, nullptr, 0};
+    if (!tiled_ && n > 0 && !use_reg && !in_lds) return -1;
+    const SysAddr sa = tiled_ ? sp_.addr() : SysAddr{dS_, n, nullptr, nullptr, 0, nullptr};
     do {
         // setLambda + BlockSolver::solve
         if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
@@ -2639,12 +2697,12 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
 // ---------------------------------------------------------------- unit entry points
 namespace orbgpu {
 int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) {
-    if (variant == 2) {   // block-sparse tiled solver; only the upper triangle of S is read
+    if (variant == 2 || variant == 3) {   // block-sparse tiled solver (3: nested dissection); upper triangle read
         std::vector<double> U((size_t)n * n, 0.0);
         for (int i = 0; i < n; i++)
             for (int j = i; j < n; j++) U[(size_t)i * n + j] = S[(size_t)i * n + j];
         int ok = 0;
-        if (int e = ldlt_sparse_dense(n, U.data(), b, x, &ok, nullptr)) return e < 0 ? e : -1;
+        if (int e = ldlt_sparse_dense(n, U.data(), b, x, &ok, nullptr, variant == 3)) return e < 0 ? e : -1;
         return ok;
     }
     double *dS = nullptr, *dB = nullptr, *dX = nullptr, *dScal = nullptr;
@@ -2679,7 +2737,7 @@ int debug_ldlt_factor(int n, const double* S, double* out) {
     for (int i = 0; i < n; i++)
         for (int j = i; j < n; j++) U[(size_t)i * n + j] = S[(size_t)i * n + j];
     int ok = 0;
-    return ldlt_sparse_dense(n, U.data(), b.data(), x.data(), &ok, out);
+    return ldlt_sparse_dense(n, U.data(), b.data(), x.data(), &ok, out, false);
 }
 
 __global__ void k_unit_wave_tree(const double* v, double* out) {

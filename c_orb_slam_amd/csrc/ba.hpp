@@ -77,6 +77,7 @@ public:
 private:
     int upload_problem(const ba_problem* P);
     int build_structure(int level);
+    int gather_blocks(const std::vector<int64_t>& mine, std::vector<int64_t>* all);
     int optimize(int iterations, const volatile bool* stop, int* its);
     int lm_solve(int iteration, const volatile bool* stop, bool* terminate);
     int gate_edges(int final_check, uint8_t* erase);

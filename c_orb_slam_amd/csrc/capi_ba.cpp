@@ -8,6 +8,7 @@
 
 #include "ba.hpp"
 #include "capi_handles.hpp"
+#include "ordering.hpp"
 #include "orb_match.hpp"
 #include "sim3opt.hpp"
 #include "orb_extract.hpp"
@@ -335,6 +336,22 @@ int orbgpu_debug_prof_extract(unsigned long long* out32) {
 }
 int orbgpu_debug_prof_match(unsigned long long* out32) {
     return out32 ? orbgpu::debug_prof_match(out32) : ORB_E_INVALID;
+}
+
+int orbgpu_unit_nd_order(int n, const int32_t* adjStart, const int32_t* adj, int leaf, int32_t* perm,
+                         int32_t* n_nodes, int32_t* height) {
+    if (n < 0 || leaf < 1 || (n > 0 && (!adjStart || !adj || !perm))) return ORB_E_INVALID;
+    std::vector<int> as(adjStart, adjStart + n + 1), ad(adj, adj + (n > 0 ? adjStart[n] : 0));
+    orbgpu::NdTree t;
+    orbgpu::nd_order(n, as, ad, leaf, &t);
+    for (int i = 0; i < n; i++) perm[i] = t.perm[i];
+    if (n_nodes) *n_nodes = (int32_t)t.start.size();
+    if (height) {
+        int h = 0;
+        for (int v : t.height) h = std::max(h, v);
+        *height = h;
+    }
+    return ORB_OK;
 }
 
 int orbgpu_unit_set_csum_lds_max(int m2_max) {

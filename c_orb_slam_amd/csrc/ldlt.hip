@@ -1,35 +1,34 @@
 // ldlt.hip -- block-sparse LDL^T solve of the reduced pose system S x = b_s for large bundle
-// adjustments (reference: g2o LinearSolverEigen = Eigen SimplicialLDLT on the sparse Schur
-// complement, Thirdparty/g2o/g2o/solvers/linear_solver_eigen.h:60-124; restated in oracle/ba.c
-// ora_ldlt_solve).
+// adjustments (reference: g2o LinearSolverEigen = Eigen SimplicialLDLT + AMD on the sparse Schur
+// complement, Thirdparty/g2o/g2o/solvers/linear_solver_eigen.h:60-124; restated in oracle/ba.c).
 //
-// Storage: S is kept as 64 x 64 tiles of its upper triangle, only the tiles the Schur pattern
-// (keyframes that share map points) and the factorisation's fill-in touch.  The symbolic
-// factorisation runs once per structure on the host, at tile granularity, in natural pose
-// order: row p of U gains the union of its elimination-tree children's rows.  A keyframe
-// sequence whose points are seen by nearby keyframes gives a band of 2-3 tiles per row, so a
-// 16k-keyframe map (n = 96k) holds ~4.5k tiles (150 MB) instead of a 74 GB dense matrix.
-//   U  [slot] row-major tile (I, J), I <= J: S on entry; after the factorisation the
-//      eliminated rows (U), and on diagonal tiles d on the diagonal and L strictly below;
-//   LT [slot] of tile (p, J), p < J: LT[k][j] = L[J0 + j][p0 + k] (pivot-major, coalesced
-//      for the trailing update and the forward solve).
-// Per-element operation sequence is the oracle's: pivot k ascending, d_k = A[k][k],
-// l_i = A[k][i] / d_k, A[i][j] -= l_i * A[k][j], no FMA contraction (the oracle skips l_i == 0,
-// which only differs in the sign of a zero);
-// forward y_i -= L[i][k] y_k (k ascending), y_k /= d_k, backward y_i -= L[k][i] y_k (k
-// descending).  Tiles whose L is exactly zero are skipped in the trailing update and the
-// solves, which is the oracle's l == 0 skip (exact up to the sign of zero).
+// Order.  The poses are permuted by a nested dissection of the pose graph (ordering.hpp): the
+// separator tree bounds the fill on loop-closed maps and is the task tree of the factorisation.
+// Each tree node's rows are packed into whole 64 x 64 tiles of a "tile space" (a node never
+// shares a tile with another node; its last tile is partial: th[t] rows, zero beyond), so the
+// tile elimination tree follows the separator tree: the tiles of sibling subtrees never meet.
 //
-// Two launches per solve: one 512-thread workgroup walks the panels (64 pivots each):
-//   diag   wave 0, lane j = column j of the diagonal tile in registers, l_i broadcast
-//          through LDS;
-//   chunks the U tiles (p, J > p) of the panel row, one wave each: left-looking per column
-//          with the diagonal L in LDS; writes U, LT and the tile's L-nonzero flag;
-//   trail  the tile pairs (I <= J) of the panel's nonzero L tiles, two 256-thread groups
-//          (4x4 register micro-tiles over LDS-staged LT (p, I) and U (p, J));
-// then one wave runs the forward and backward solves block by block.  The band is a chain of
-// dependent panels: there is no panel parallelism to spread over more workgroups in natural
-// order, and one workgroup removes the 3 launches (and the grid drain) per panel.
+// Storage: only the tiles of S's pattern and their fill (symbolic factorisation at tile level,
+// once per structure):
+//   U  [slot] row-major tile (I, J), I <= J in tile space: S on entry; after the factorisation
+//      the eliminated rows (U), and on diagonal tiles d on the diagonal and L strictly below;
+//   LT [slot] of tile (p, J), p < J: LT[k][j] = L[J0 + j][p0 + k] (pivot-major, coalesced).
+// Per-element operation sequence (the oracle's): element (i, j) receives the updates
+// a_ij -= l_ik u_kj of every pivot k < i in ascending k, d_k = a_kk, l_ik = a_ki / d_k, no FMA
+// contraction; whole tiles whose L is zero are skipped (the oracle skips l == 0: equal up to the
+// sign of a zero).  The forward solve y_i -= L[i][k] y_k runs k ascending, y_k /= d_k, the
+// backward solve y_i -= L[k][i] y_k k descending -- the same sequences whatever the schedule.
+//
+// Schedule: the tree's levels (height 0 = leaves) run bottom-up, two launches per level:
+//   update  one workgroup per target tile (I, J) of the level's nodes that a DESCENDANT tile
+//           row K touches: A(I, J) -= sum_K L(I, K) U(K, J), K ascending (left-looking: reads
+//           finished descendant tiles only, writes a tile owned by this node: no races);
+//   factor  one 512-thread workgroup per node walks its own panels right-looking (diagonal
+//           tile, U/LT row tiles, trailing updates of its own rows only), then solves its rows
+//           of L y = b;
+// then the backward solve runs the levels top-down (one wave per node).  Nodes of one level
+// share no tile, so their workgroups run concurrently; the descendants' updates of an
+// ancestor tile arrive in ascending K, i.e. in pivot order, as in the sequential sweep.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -39,6 +38,7 @@
 
 #include "ldlt.hpp"
 #include "orb_common.hpp"
+#include "ordering.hpp"
 
 namespace orbgpu {
 
@@ -47,22 +47,31 @@ constexpr int LP = LT + 1;       // LDS row pitch (doubles) of the diagonal L
 constexpr int kSpThreads = 512;  // 8 waves
 constexpr int kMaxRow = 2048;    // tiles per panel row
 constexpr size_t kSpLds = sizeof(double) * (2 * 2 * LT * LT + LT) + sizeof(int) * (kMaxRow + 16);
+constexpr int kNdLeaf = 32;      // nested-dissection leaf size (poses)
 
 struct SpDev {
     int n, nt;
     const int* slotOf;
     double* U;
     double* LT;
-    const int* rowStart;
+    const int* th;        // rows of tile t (tile space)
+    const int* rowMap;    // tile-space row -> system row (-1: padding)
+    const int* rowStart;  // panel p: tiles (p, J > p)
     const int* rowJ;
     const int* rowSlot;
-    const int* colStart;
+    const int* colStart;  // tile row I: tiles (K < I, I), K ascending
     const int* colK;
     const int* colSlot;
-    const int* pairStart;
-    const int4* pairs;   // (index of I in the panel row, index of J, target slot, 0)
+    const int* pairStart; // panel p: trailing pairs inside p's node
+    const int4* pairs;    // (index of I in the panel row, index of J, target slot, 0)
+    const int* nodeT;     // node k: tiles [nodeT[2k], nodeT[2k + 1])
+    const int* levNodes;  // node ids by level
+    const int4* tgts;     // update targets by level: (slot(I, J), I, J, first K pair)
+    const int4* kps;      // (slot(K, I), slot(K, J), K, 0), per target in ascending K
     uint8_t* lnz;
-    double* y;
+    double* y;            // tile space
+    double* xs;           // tile space
+    int* fail;
 };
 
 // Tile access through a buffer descriptor (wave-uniform tile base in SGPRs, 32-bit per-lane
@@ -92,8 +101,63 @@ __device__ __forceinline__ double rdlane(double v, int l) {
     return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
-__global__ void __launch_bounds__(kSpThreads) k_ldlt_sparse(SpDev S, const double* __restrict__ b,
-                                                             double* __restrict__ x, double* scal) {
+// A(I, J) -= L(I, K) U(K, J) over a target's descendant tile rows K (ascending): 256 threads,
+// 4 x 4 register micro-tiles, the two operand tiles staged in LDS per K.
+__global__ void __launch_bounds__(256) k_ldlt_update(SpDev S, int t0) {
+    __shared__ double Lg[LT * LT];   // [k][i] = L[I0 + i][K0 + k]
+    __shared__ double Ug[LT * LT];   // [k][j] = U[K0 + k][J0 + j]
+    if (*(volatile int*)S.fail) return;
+    const int4 tg = S.tgts[t0 + blockIdx.x];
+    const int kp0 = tg.w, kp1 = S.tgts[t0 + blockIdx.x + 1].w;
+    const int I = tg.y, J = tg.z;
+    const int ih = S.th[I], jw = S.th[J];
+    const int gt = threadIdx.x, ty = gt >> 4, tx = gt & 15;
+    double* T = S.U + (size_t)tg.x * (LT * LT);
+    double acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const int i = ty + 16 * a, j = tx + 16 * bb;
+            acc[a][bb] = (i < ih && j < jw) ? T[i * LT + j] : 0.0;
+        }
+    for (int q = kp0; q < kp1; q++) {
+        const int4 kp = S.kps[q];
+        if (!S.lnz[kp.x] || !S.lnz[kp.y]) continue;   // block-uniform
+        const double2* srcL = (const double2*)(S.LT + (size_t)kp.x * (LT * LT));
+        const double2* srcU = (const double2*)(S.U + (size_t)kp.y * (LT * LT));
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < (LT * LT / 2) / 256; u++) {
+            ((double2*)Lg)[gt + 256 * u] = srcL[gt + 256 * u];
+            ((double2*)Ug)[gt + 256 * u] = srcU[gt + 256 * u];
+        }
+        __syncthreads();
+        const int kw = S.th[kp.z];
+        for (int k = 0; k < kw; k++) {
+            double l[4], u[4];
+#pragma unroll
+            for (int a = 0; a < 4; a++) l[a] = Lg[k * LT + ty + 16 * a];
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) u[bb] = Ug[k * LT + tx + 16 * bb];
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int bb = 0; bb < 4; bb++) acc[a][bb] -= l[a] * u[bb];
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const int i = ty + 16 * a, j = tx + 16 * bb;
+            if (i < ih && j < jw && (I != J || i <= j)) T[i * LT + j] = acc[a][bb];
+        }
+}
+
+// One workgroup per node of a level: the node's panels right-looking (trailing updates inside
+// the node), then its rows of L y = b (wave 0).
+__global__ void __launch_bounds__(kSpThreads) k_ldlt_factor(SpDev S, int n0, const double* __restrict__ b) {
     // static LDS: addresses fold into the ds_read offsets (a dynamic base is a relocation the
     // compiler hoists into one SGPR per address)
     __shared__ double sm[kSpLds / sizeof(double)];
@@ -102,21 +166,23 @@ __global__ void __launch_bounds__(kSpThreads) k_ldlt_sparse(SpDev S, const doubl
     int* flagS = (int*)(dsh + LT);         // L-nonzero flag per chunk of the panel row
     int* failS = flagS + kMaxRow;
     const int tid0 = threadIdx.x, lane0 = tid0 & 63, w = tid0 >> 6;
-    const int n = S.n, nt = S.nt;
-    if (tid0 == 0) *failS = 0;
+    const int node = S.levNodes[n0 + blockIdx.x];
+    const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    if (tid0 == 0) *failS = *(volatile int*)S.fail;
     __syncthreads();
+    if (*failS) return;
     ORBGPU_PROF_START;
-    for (int p = 0; p < nt; p++) {
+    for (int p = T0; p < T1; p++) {
         // opaque per panel: keeps LICM from hoisting every lane mask and lane address of the
         // unrolled loops out of the panel loop (it spilled them)
         int lane = lane0, tid = tid0;
         asm volatile("" : "+v"(lane), "+v"(tid));
-        const int p0 = p * LT, pw = min(LT, n - p0);
+        const int pw = S.th[p];
         const int rs = S.rowStart[p], m = S.rowStart[p + 1] - rs;
         // ---- diagonal tile (wave 0)
         if (w == 0) {
-            // tiles are zero outside the system (rows / columns >= n) and below the diagonal
-            const __amdgpu_buffer_rsrc_t Ud = tile_rsrc(S.U + (size_t)S.slotOf[(size_t)p * nt + p] * (LT * LT));
+            // tiles are zero outside the system (padding rows / columns) and below the diagonal
+            const __amdgpu_buffer_rsrc_t Ud = tile_rsrc(S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT));
             const int vo = lane * 8;
             double col[LT];
 #pragma unroll
@@ -140,13 +206,16 @@ __global__ void __launch_bounds__(kSpThreads) k_ldlt_sparse(SpDev S, const doubl
                     }
                 }
             }
-            // pivots past the system's end: L = 0, d = 1, so the chunk pass needs no predicates
+            // padding pivots: L = 0, d = 1, so the chunk pass needs no predicates
             for (int k = pw; k < LT; k++) {
                 Ls[k * LP + lane] = 0.0;
                 if (lane == 0) dsh[k] = 1.0;
             }
             if (bad) {
-                if (lane == 0) *failS = 1;
+                if (lane == 0) {
+                    *failS = 1;
+                    *S.fail = 1;
+                }
             } else {
 #pragma unroll
                 for (int r = 0; r < LT; r++)
@@ -155,7 +224,7 @@ __global__ void __launch_bounds__(kSpThreads) k_ldlt_sparse(SpDev S, const doubl
         }
         __syncthreads();
         ORBGPU_PROF_MARK(16);
-        if (*failS) break;
+        if (*failS) return;
         // ---- U tiles (p, J > p) of the panel row: one wave per tile, lane = column
         const int wu = __builtin_amdgcn_readfirstlane(w);
         for (int t = wu; t < m; t += kSpThreads / 64) {
@@ -191,7 +260,7 @@ __global__ void __launch_bounds__(kSpThreads) k_ldlt_sparse(SpDev S, const doubl
         }
         __syncthreads();
         ORBGPU_PROF_MARK(17);
-        // ---- trailing update: A(I, J) -= L(I, p) U(p, J) over the panel's tile pairs
+        // ---- trailing update inside the node: A(I, J) -= L(I, p) U(p, J)
         const int ps = S.pairStart[p], np = S.pairStart[p + 1] - ps;
         const int g = tid >> 8, gt = tid & 255, ty = gt >> 4, tx = gt & 15;
         double* Lg = sm + g * (2 * LT * LT);   // [k][i] = L[I0 + i][p0 + k]
@@ -218,7 +287,7 @@ __global__ void __launch_bounds__(kSpThreads) k_ldlt_sparse(SpDev S, const doubl
             __syncthreads();
             if (act) {
                 const int I = S.rowJ[rs + pr.x], J = S.rowJ[rs + pr.y];
-                const int ih = min(LT, n - I * LT), jw = min(LT, n - J * LT);
+                const int ih = S.th[I], jw = S.th[J];
                 double* T = S.U + (size_t)pr.z * (LT * LT);
                 double acc[4][4];
 #pragma unroll
@@ -251,37 +320,31 @@ __global__ void __launch_bounds__(kSpThreads) k_ldlt_sparse(SpDev S, const doubl
         }
         ORBGPU_PROF_MARK(18);
     }
-    if (tid0 == 0) scal[3] = *failS ? 0.0 : 1.0;
-}
-
-// Forward / backward solves after a successful factorisation: one wave, block by block
-// (lane = row of the block); the chain of dependent blocks is the band's.
-__global__ void __launch_bounds__(64) k_ldlt_sparse_solve(SpDev S, const double* __restrict__ b,
-                                                           double* __restrict__ x, const double* scal) {
-    if (scal[3] == 0.0) return;
-    const int lane = threadIdx.x;
-    const int n = S.n, nt = S.nt;
-    // ---- L y = b, block by block; lane = row
+    // ---- L y = b on the node's rows (wave 0; lane = row): descendants' y are final
+    if (w != 0) return;
+    const int lane = lane0;
     double Lr[LT];
-    for (int I = 0; I < nt; I++) {
-        const int I0 = I * LT, ih = min(LT, n - I0);
+    for (int I = T0; I < T1; I++) {
+        const int I0 = I * LT, ih = S.th[I];
         const bool on = lane < ih;
-        double acc = on ? b[I0 + lane] : 0.0;
+        double acc = on ? b[S.rowMap[I0 + lane]] : 0.0;
         for (int e = S.colStart[I]; e < S.colStart[I + 1]; e++) {
             const int sl = S.colSlot[e];
             if (!S.lnz[sl]) continue;
-            const int K0 = S.colK[e] * LT;   // K < I: a full tile
+            const int K = S.colK[e], K0 = K * LT, kh = S.th[K];
             const double yk = S.y[K0 + lane];
             const double* Lo = S.LT + (size_t)sl * (LT * LT);   // [k][i] = L[I0 + i][K0 + k]
 #pragma unroll
             for (int k = 0; k < LT; k++) Lr[k] = Lo[k * LT + lane];
 #pragma unroll
             for (int k = 0; k < LT; k++) {
-                const double v = acc - Lr[k] * rdlane(yk, k);
-                acc = on ? v : acc;
+                if (k < kh) {
+                    const double v = acc - Lr[k] * rdlane(yk, k);
+                    acc = on ? v : acc;
+                }
             }
         }
-        const double* Ud = S.U + (size_t)S.slotOf[(size_t)I * nt + I] * (LT * LT);
+        const double* Ud = S.U + (size_t)S.slotOf[(size_t)I * S.nt + I] * (LT * LT);
 #pragma unroll
         for (int k = 0; k < LT; k++) Lr[k] = (on && k < lane) ? Ud[lane * LT + k] : 0.0;
 #pragma unroll
@@ -292,19 +355,31 @@ __global__ void __launch_bounds__(64) k_ldlt_sparse_solve(SpDev S, const double*
                 acc = (on && lane > k) ? v : acc;
             }
         }
-        if (on) S.y[I0 + lane] = acc;
+        S.y[I0 + lane] = on ? acc : 0.0;
     }
-    // ---- y /= d, then L^T x = y with k descending
-    for (int I = nt - 1; I >= 0; I--) {
-        const int I0 = I * LT, ih = min(LT, n - I0);
+}
+
+// y /= d, then L^T x = y with k descending: one wave per node of a level (levels top-down);
+// the rows of a node's ancestors are final.  The first launch also publishes the outcome.
+__global__ void __launch_bounds__(64) k_ldlt_backward(SpDev S, int n0, double* __restrict__ x, double* scal,
+                                                      int first) {
+    const int lane = threadIdx.x;
+    const int failed = *(volatile int*)S.fail;
+    if (first && blockIdx.x == 0 && lane == 0) scal[3] = failed ? 0.0 : 1.0;
+    if (failed) return;
+    const int node = S.levNodes[n0 + blockIdx.x];
+    const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    double Lr[LT];
+    for (int I = T1 - 1; I >= T0; I--) {
+        const int I0 = I * LT, ih = S.th[I];
         const bool on = lane < ih;
-        const double* Ud = S.U + (size_t)S.slotOf[(size_t)I * nt + I] * (LT * LT);
+        const double* Ud = S.U + (size_t)S.slotOf[(size_t)I * S.nt + I] * (LT * LT);
         double acc = on ? S.y[I0 + lane] / Ud[lane * LT + lane] : 0.0;
         for (int e = S.rowStart[I + 1] - 1; e >= S.rowStart[I]; e--) {
             const int sl = S.rowSlot[e];
             if (!S.lnz[sl]) continue;
-            const int K0 = S.rowJ[e] * LT, kh = min(LT, n - K0);
-            const double xk = lane < kh ? x[K0 + lane] : 0.0;
+            const int K0 = S.rowJ[e] * LT, kh = S.th[S.rowJ[e]];
+            const double xk = lane < kh ? S.xs[K0 + lane] : 0.0;
             const double* Lo = S.LT + (size_t)sl * (LT * LT);   // [i][k] = L[K0 + k][I0 + i]
 #pragma unroll
             for (int k = 0; k < LT; k++) Lr[k] = on ? Lo[lane * LT + k] : 0.0;
@@ -326,7 +401,8 @@ __global__ void __launch_bounds__(64) k_ldlt_sparse_solve(SpDev S, const double*
                 acc = (on && lane < k) ? v : acc;
             }
         }
-        if (on) x[I0 + lane] = acc;
+        S.xs[I0 + lane] = on ? acc : 0.0;
+        if (on) x[S.rowMap[I0 + lane]] = acc;
     }
 }
 
@@ -347,16 +423,65 @@ SparseLdlt::~SparseLdlt() {
     if (mem_) (void)hipFree(mem_);
 }
 
-int SparseLdlt::build(int n, const std::vector<uint8_t>& mask, hipStream_t s) {
+int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std::vector<int>& adj, bool nd,
+                      hipStream_t s) {
     n_ = n;
-    nt_ = (n + LT - 1) / LT;
-    const int nt = nt_;
-    if (n <= 0) {
-        nslot_ = nA_ = 0;
-        return 0;
+    nt_ = 0;
+    nslot_ = nA_ = 0;
+    nLev_ = 0;
+    if (n <= 0) return 0;
+    const int ng = (n + g - 1) / g;
+    if ((int)adjStart.size() != ng + 1) return -1;
+    auto gsz = [&](int q) { return std::min(g, n - q * g); };
+    // ---- order and tile space
+    NdTree tree;
+    if (nd) {
+        nd_order(ng, adjStart, adj, kNdLeaf, &tree);
+    } else {   // natural order, one node
+        tree.perm.resize(ng);
+        for (int q = 0; q < ng; q++) tree.perm[q] = q;
+        tree.start = {0};
+        tree.end = {ng};
+        tree.parent = {-1};
+        tree.height = {0};
     }
-    if ((size_t)nt * nt != mask.size()) return -1;
-    // symbolic factorisation at tile granularity (natural order): struct(p) joins its parent's
+    const int nnode = (int)tree.start.size();
+    hProw_.assign(ng, 0);
+    std::vector<int> nodeT(2 * nnode), th;
+    int nt = 0;
+    for (int k = 0; k < nnode; k++) {
+        int rows = 0;
+        for (int pos = tree.start[k]; pos < tree.end[k]; pos++) {
+            hProw_[tree.perm[pos]] = nt * LT + rows;
+            rows += gsz(tree.perm[pos]);
+        }
+        const int tiles = (rows + LT - 1) / LT;
+        nodeT[2 * k] = nt;
+        nodeT[2 * k + 1] = nt + tiles;
+        for (int t = 0; t < tiles; t++) th.push_back(std::min(LT, rows - t * LT));
+        nt += tiles;
+    }
+    nt_ = nt;
+    std::vector<int> tileNode(nt);
+    for (int k = 0; k < nnode; k++)
+        for (int t = nodeT[2 * k]; t < nodeT[2 * k + 1]; t++) tileNode[t] = k;
+    std::vector<int> rowMap((size_t)nt * LT, -1);
+    for (int q = 0; q < ng; q++)
+        for (int r = 0; r < gsz(q); r++) rowMap[(size_t)hProw_[q] + r] = q * g + r;
+    // ---- tile pattern of S: every (group, group) block of the graph and the diagonal groups
+    std::vector<uint8_t> mask((size_t)nt * nt, 0);
+    auto mark_blocks = [&](int q1, int q2) {
+        const int a0 = hProw_[q1] / LT, a1 = (hProw_[q1] + gsz(q1) - 1) / LT;
+        const int b0 = hProw_[q2] / LT, b1 = (hProw_[q2] + gsz(q2) - 1) / LT;
+        for (int I = a0; I <= a1; I++)
+            for (int J = b0; J <= b1; J++) mask[(size_t)std::min(I, J) * nt + std::max(I, J)] = 1;
+    };
+    for (int q = 0; q < ng; q++) {
+        mark_blocks(q, q);
+        for (int e = adjStart[q]; e < adjStart[q + 1]; e++)
+            if (adj[e] > q) mark_blocks(q, adj[e]);
+    }
+    // ---- symbolic factorisation at tile level: struct(p) joins its parent's
     std::vector<std::vector<int>> rows(nt);
     for (int I = 0; I < nt; I++) {
         rows[I].push_back(I);
@@ -384,7 +509,8 @@ int SparseLdlt::build(int n, const std::vector<uint8_t>& mask, hipStream_t s) {
         for (int J : rows[I])
             if (hSlotOf_[(size_t)I * nt + J] < 0) hSlotOf_[(size_t)I * nt + J] = ns++;
     nslot_ = ns;
-    // panel rows (J > p), block columns (K < I), trailing pairs
+    auto slot = [&](int I, int J) { return hSlotOf_[(size_t)I * nt + J]; };
+    // ---- panel rows (J > p), block columns (K < I), trailing pairs inside the node
     std::vector<int> rowStart(nt + 1, 0), rowJ, rowSlot, colStart(nt + 1, 0), colK, colSlot, pairStart(nt + 1, 0);
     std::vector<int4> pairs;
     std::vector<std::vector<int>> cols(nt);
@@ -392,18 +518,21 @@ int SparseLdlt::build(int n, const std::vector<uint8_t>& mask, hipStream_t s) {
         rowStart[p] = (int)rowJ.size();
         pairStart[p] = (int)pairs.size();
         const std::vector<int>& r = rows[p];
+        const int tEnd = nodeT[2 * tileNode[p] + 1];
         for (size_t q = 1; q < r.size(); q++) {
             rowJ.push_back(r[q]);
-            rowSlot.push_back(hSlotOf_[(size_t)p * nt + r[q]]);
+            rowSlot.push_back(slot(p, r[q]));
             cols[r[q]].push_back(p);
         }
         const int m = (int)r.size() - 1;
-        for (int a = 0; a < m; a++)
+        for (int a = 0; a < m; a++) {
+            if (r[1 + a] >= tEnd) break;   // rows sorted: the rest belong to ancestors
             for (int bb = a; bb < m; bb++) {
-                const int t = hSlotOf_[(size_t)r[1 + a] * nt + r[1 + bb]];
+                const int t = slot(r[1 + a], r[1 + bb]);
                 if (t < 0) return -1;   // the fill closure guarantees the target tile
                 pairs.push_back(make_int4(a, bb, t, 0));
             }
+        }
     }
     rowStart[nt] = (int)rowJ.size();
     pairStart[nt] = (int)pairs.size();
@@ -411,11 +540,55 @@ int SparseLdlt::build(int n, const std::vector<uint8_t>& mask, hipStream_t s) {
         colStart[I] = (int)colK.size();
         for (int K : cols[I]) {   // ascending K
             colK.push_back(K);
-            colSlot.push_back(hSlotOf_[(size_t)K * nt + I]);
+            colSlot.push_back(slot(K, I));
         }
     }
     colStart[nt] = (int)colK.size();
-    // device storage (grow-only)
+    // ---- levels: nodes by height; the update targets of each level's nodes
+    int H = 0;
+    for (int k = 0; k < nnode; k++) H = std::max(H, tree.height[k]);
+    nLev_ = H + 1;
+    hLevNodeStart_.assign(nLev_ + 1, 0);
+    hLevTgtStart_.assign(nLev_ + 1, 0);
+    std::vector<int> levNodes;
+    std::vector<int4> tgts, kps;
+    for (int h = 0; h < nLev_; h++) {
+        hLevNodeStart_[h] = (int)levNodes.size();
+        hLevTgtStart_[h] = (int)tgts.size();
+        for (int k = 0; k < nnode; k++) {
+            if (tree.height[k] != h) continue;
+            levNodes.push_back(k);
+            const int t0 = nodeT[2 * k], t1 = nodeT[2 * k + 1];
+            for (int I = t0; I < t1; I++)
+                for (int J : rows[I]) {
+                    const int first = (int)kps.size();
+                    for (int K : cols[I]) {
+                        if (K >= t0) break;   // the node's own panels: right-looking in k_ldlt_factor
+                        const int sj = slot(K, J);
+                        if (sj >= 0) kps.push_back(make_int4(slot(K, I), sj, K, 0));
+                    }
+                    if ((int)kps.size() > first) tgts.push_back(make_int4(slot(I, J), I, J, first));
+                }
+        }
+    }
+    hLevNodeStart_[nLev_] = (int)levNodes.size();
+    hLevTgtStart_[nLev_] = (int)tgts.size();
+    tgts.push_back(make_int4(0, 0, 0, (int)kps.size()));   // sentinel: the last target's K range end
+    // every tile a kernel addresses exists (host check before any launch)
+    for (int I = 0; I < nt; I++)
+        if (slot(I, I) < 0) return -1;
+    for (int v : rowSlot)
+        if (v < 0) return -1;
+    for (int v : colSlot)
+        if (v < 0) return -1;
+    for (size_t q = 0; q + 1 < tgts.size(); q++)
+        if (tgts[q].x < 0 || tgts[q].w > tgts[q + 1].w) return -1;
+    for (const int4& q : kps)
+        if (q.x < 0 || q.y < 0 || q.z < 0 || q.z >= nt) return -1;
+    for (int q : levNodes)
+        if (q < 0 || q >= nnode) return -1;
+    nUpd_ = (long long)kps.size();
+    // ---- device storage (grow-only)
     const size_t tileB = sizeof(double) * LT * LT;
     size_t off = 0;
     auto take = [&](size_t b) {
@@ -427,10 +600,42 @@ int SparseLdlt::build(int n, const std::vector<uint8_t>& mask, hipStream_t s) {
     const size_t oU = take(tileB * nslot_);
     const size_t oLT = take(tileB * nslot_);
     const size_t oY = take(sizeof(double) * (size_t)nt * LT);
+    const size_t oXs = take(sizeof(double) * (size_t)nt * LT);
     const size_t oLnz = take(nslot_);
-    const size_t nInts = rowStart.size() + rowJ.size() + rowSlot.size() + colStart.size() + colK.size() + colSlot.size() +
-                         pairStart.size() + 4 * pairs.size() + 64;
-    const size_t oLists = take(sizeof(int) * nInts);
+    const size_t oFail = take(sizeof(int) * 4);
+    const size_t oProw = take(sizeof(int) * (size_t)ng);
+    std::vector<int> L;
+    auto put = [&](const std::vector<int>& v) {
+        const size_t o = L.size();
+        L.insert(L.end(), v.begin(), v.end());
+        return o;
+    };
+    auto put4 = [&](const std::vector<int4>& v) {
+        while (L.size() % 4) L.push_back(0);
+        const size_t o = L.size();
+        for (const int4& q : v) {
+            L.push_back(q.x);
+            L.push_back(q.y);
+            L.push_back(q.z);
+            L.push_back(q.w);
+        }
+        return o;
+    };
+    offTh_ = put(th);
+    offRowMap_ = put(rowMap);
+    offRowStart_ = put(rowStart);
+    offRowJ_ = put(rowJ);
+    offRowSlot_ = put(rowSlot);
+    offColStart_ = put(colStart);
+    offColK_ = put(colK);
+    offColSlot_ = put(colSlot);
+    offPairStart_ = put(pairStart);
+    offNodeT_ = put(nodeT);
+    offLevNodes_ = put(levNodes);
+    offPairs_ = put4(pairs);
+    offTgts_ = put4(tgts);
+    offKps_ = put4(kps);
+    const size_t oLists = take(sizeof(int) * (L.size() + 64));
     if (off > cap_) {
         if (mem_) (void)hipFree(mem_);
         mem_ = nullptr;
@@ -443,31 +648,13 @@ int SparseLdlt::build(int n, const std::vector<uint8_t>& mask, hipStream_t s) {
     U_ = (double*)(base + oU);
     LT_ = (double*)(base + oLT);
     y_ = (double*)(base + oY);
+    xs_ = (double*)(base + oXs);
     lnz_ = (uint8_t*)(base + oLnz);
+    fail_ = (int*)(base + oFail);
+    prow_ = (int*)(base + oProw);
     lists_ = (int*)(base + oLists);
-    std::vector<int> L;
-    L.reserve(nInts);
-    auto put = [&](const std::vector<int>& v) {
-        const size_t o = L.size();
-        L.insert(L.end(), v.begin(), v.end());
-        return o;
-    };
-    offRowStart_ = put(rowStart);
-    offRowJ_ = put(rowJ);
-    offRowSlot_ = put(rowSlot);
-    offColStart_ = put(colStart);
-    offColK_ = put(colK);
-    offColSlot_ = put(colSlot);
-    offPairStart_ = put(pairStart);
-    while (L.size() % 4) L.push_back(0);
-    offPairs_ = L.size();
-    for (const int4& q : pairs) {
-        L.push_back(q.x);
-        L.push_back(q.y);
-        L.push_back(q.z);
-        L.push_back(q.w);
-    }
     ORB_HIP_CHECK(hipMemcpyAsync(slotOf_, hSlotOf_.data(), sizeof(int) * hSlotOf_.size(), hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(prow_, hProw_.data(), sizeof(int) * hProw_.size(), hipMemcpyHostToDevice, s));
     ORB_HIP_CHECK(hipMemcpyAsync(lists_, L.data(), sizeof(int) * L.size(), hipMemcpyHostToDevice, s));
     ORB_HIP_CHECK(hipStreamSynchronize(s));   // pageable sources
     return 0;
@@ -486,6 +673,8 @@ int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
     d.slotOf = slotOf_;
     d.U = U_;
     d.LT = LT_;
+    d.th = lists_ + offTh_;
+    d.rowMap = lists_ + offRowMap_;
     d.rowStart = lists_ + offRowStart_;
     d.rowJ = lists_ + offRowJ_;
     d.rowSlot = lists_ + offRowSlot_;
@@ -494,35 +683,75 @@ int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
     d.colSlot = lists_ + offColSlot_;
     d.pairStart = lists_ + offPairStart_;
     d.pairs = (const int4*)(lists_ + offPairs_);
+    d.nodeT = lists_ + offNodeT_;
+    d.levNodes = lists_ + offLevNodes_;
+    d.tgts = (const int4*)(lists_ + offTgts_);
+    d.kps = (const int4*)(lists_ + offKps_);
     d.lnz = lnz_;
     d.y = y_;
-    hipLaunchKernelGGL(k_ldlt_sparse, dim3(1), dim3(kSpThreads), 0, s, d, b, x, scal);
-    hipLaunchKernelGGL(k_ldlt_sparse_solve, dim3(1), dim3(64), 0, s, d, b, x, scal);
+    d.xs = xs_;
+    d.fail = fail_;
+    ORB_HIP_CHECK(hipMemsetAsync(fail_, 0, sizeof(int), s));
+    for (int h = 0; h < nLev_; h++) {
+        const int nt = hLevTgtStart_[h + 1] - hLevTgtStart_[h];
+        if (nt > 0) hipLaunchKernelGGL(k_ldlt_update, dim3(nt), dim3(256), 0, s, d, hLevTgtStart_[h]);
+        const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
+        hipLaunchKernelGGL(k_ldlt_factor, dim3(nn), dim3(kSpThreads), 0, s, d, hLevNodeStart_[h], b);
+    }
+    for (int h = nLev_ - 1; h >= 0; h--) {
+        const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
+        hipLaunchKernelGGL(k_ldlt_backward, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], x, scal,
+                           h == nLev_ - 1 ? 1 : 0);
+    }
     ORB_HIP_CHECK(hipGetLastError());
     return 0;
 }
 
-int ldlt_sparse_dense(int n, const double* S, const double* b, double* x, int* ok, double* factor_out) {
+int ldlt_sparse_dense(int n, const double* S, const double* b, double* x, int* ok, double* factor_out, bool nd) {
     *ok = 0;
     if (n <= 0) {
         *ok = 1;
         return 0;
     }
-    const int nt = (n + LT - 1) / LT;
-    std::vector<uint8_t> mask((size_t)nt * nt, 0);
-    for (int i = 0; i < n; i++)
-        for (int j = i; j < n; j++)
-            if (S[(size_t)i * n + j] != 0.0) mask[(size_t)(i / LT) * nt + j / LT] = 1;
+    // groups of 6 rows (poses; the last one may be short), adjacent when their block is nonzero
+    const int g = 6, ng = (n + g - 1) / g;
+    std::vector<std::vector<int>> nb(ng);
+    for (int q1 = 0; q1 < ng; q1++)
+        for (int q2 = q1 + 1; q2 < ng; q2++) {
+            bool nz = false;
+            for (int i = q1 * g; i < std::min(n, q1 * g + g) && !nz; i++)
+                for (int j = q2 * g; j < std::min(n, q2 * g + g); j++)
+                    if (S[(size_t)i * n + j] != 0.0) {
+                        nz = true;
+                        break;
+                    }
+            if (nz) {
+                nb[q1].push_back(q2);
+                nb[q2].push_back(q1);
+            }
+        }
+    std::vector<int> as(ng + 1, 0), adj;
+    for (int q = 0; q < ng; q++) {
+        std::sort(nb[q].begin(), nb[q].end());
+        as[q] = (int)adj.size();
+        adj.insert(adj.end(), nb[q].begin(), nb[q].end());
+    }
+    as[ng] = (int)adj.size();
     hipStream_t s = nullptr;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     SparseLdlt L;
-    if (int e = L.build(n, mask, s)) return e;
+    if (int e = L.build(n, g, as, adj, nd, s)) return e;
+    const int nt = L.nt();
     const std::vector<int>& so = L.host_slot_of();
+    const std::vector<int>& prow = L.host_prow();
+    auto trow = [&](int i) { return prow[i / g] + i % g; };   // tile-space row of system row i
     std::vector<double> T((size_t)L.nslot() * LT * LT, 0.0);
     for (int i = 0; i < n; i++)
         for (int j = i; j < n; j++) {
-            const int sl = so[(size_t)(i / LT) * nt + j / LT];
-            if (sl >= 0) T[(size_t)sl * LT * LT + (i % LT) * LT + j % LT] = S[(size_t)i * n + j];
+            int a = trow(i), c = trow(j);
+            if (a > c) std::swap(a, c);
+            const int sl = so[(size_t)(a / LT) * nt + c / LT];
+            if (sl >= 0) T[(size_t)sl * LT * LT + (a % LT) * LT + c % LT] = S[(size_t)i * n + j];
         }
     double *dB = nullptr, *dX = nullptr, *dScal = nullptr;
     ORB_HIP_CHECK(hipMalloc(&dB, sizeof(double) * n));
@@ -538,7 +767,7 @@ int ldlt_sparse_dense(int n, const double* S, const double* b, double* x, int* o
     ORB_HIP_CHECK(hipMemcpy(sc, dScal, sizeof(sc), hipMemcpyDeviceToHost));
     ORB_HIP_CHECK(hipMemcpy(x, dX, sizeof(double) * n, hipMemcpyDeviceToHost));
     *ok = sc[3] != 0.0 ? 1 : 0;
-    if (factor_out) {   // the dense layout of the factor: U above, d on the diagonal, L below
+    if (factor_out && !nd) {   // natural order: tile space is the system; U above, d on the diagonal, L below
         std::vector<double> Lt(T.size());
         ORB_HIP_CHECK(hipMemcpy(T.data(), L.tiles(), sizeof(double) * T.size(), hipMemcpyDeviceToHost));
         ORB_HIP_CHECK(hipMemcpy(Lt.data(), L.lt_tiles(), sizeof(double) * Lt.size(), hipMemcpyDeviceToHost));

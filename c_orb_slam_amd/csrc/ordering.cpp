@@ -1,0 +1,137 @@
+// ordering.cpp -- nested-dissection order of the pose graph (specification in ordering.hpp).
+#include "ordering.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace orbgpu {
+
+namespace {
+
+struct Nd {
+    const std::vector<int>& as;
+    const std::vector<int>& adj;
+    int leaf;
+    NdTree* t;
+    std::vector<int> inS;    // stamp: node is in the current set
+    std::vector<int> mark;   // stamp: visited by the current BFS
+    int stamp = 0;
+
+    // BFS level sets from r over the nodes with inS == sid
+    void levels(int r, int sid, std::vector<std::vector<int>>& L) {
+        L.clear();
+        const int st = ++stamp;
+        mark[r] = st;
+        L.push_back({r});
+        for (;;) {
+            std::vector<int> nxt;
+            for (int v : L.back())
+                for (int e = as[v]; e < as[v + 1]; e++) {
+                    const int w = adj[e];
+                    if (inS[w] == sid && mark[w] != st) {
+                        mark[w] = st;
+                        nxt.push_back(w);
+                    }
+                }
+            if (nxt.empty()) break;
+            std::sort(nxt.begin(), nxt.end());
+            L.push_back(std::move(nxt));
+        }
+    }
+
+    int new_node(int s, int e, int h) {
+        t->start.push_back(s);
+        t->end.push_back(e);
+        t->parent.push_back(-1);
+        t->height.push_back(h);
+        return (int)t->start.size() - 1;
+    }
+
+    // appends the roots of S's subtrees to `roots`
+    void order(std::vector<int> S, std::vector<int>& roots) {
+        const int sid = ++stamp;
+        for (int v : S) inS[v] = sid;
+        // connected components, in order of their smallest node
+        {
+            std::vector<std::vector<int>> comps;
+            const int st = ++stamp;
+            for (int s0 : S) {
+                if (mark[s0] == st) continue;
+                std::vector<int> comp{s0}, q{s0};
+                mark[s0] = st;
+                for (size_t h = 0; h < q.size(); h++) {
+                    const int v = q[h];
+                    for (int e = as[v]; e < as[v + 1]; e++) {
+                        const int w = adj[e];
+                        if (inS[w] == sid && mark[w] != st) {
+                            mark[w] = st;
+                            q.push_back(w);
+                            comp.push_back(w);
+                        }
+                    }
+                }
+                std::sort(comp.begin(), comp.end());
+                comps.push_back(std::move(comp));
+            }
+            if (comps.size() > 1) {
+                for (auto& c : comps) order(std::move(c), roots);
+                return;
+            }
+        }
+        const int n = (int)S.size();
+        auto make_leaf = [&]() {
+            const int s = (int)t->perm.size();
+            t->perm.insert(t->perm.end(), S.begin(), S.end());
+            roots.push_back(new_node(s, (int)t->perm.size(), 0));
+        };
+        if (n <= leaf) return make_leaf();
+        std::vector<std::vector<int>> L;
+        levels(S[0], sid, L);
+        const int u = L.back()[0];
+        levels(u, sid, L);
+        const int h = (int)L.size() - 1;
+        if (h < 2) return make_leaf();
+        int best = -1;
+        long long bk[4] = {0, 0, 0, 0};
+        int A = 0;
+        for (int m = 1; m < h; m++) {
+            A += (int)L[m - 1].size();
+            const int Lm = (int)L[m].size(), B = n - A - Lm;
+            const bool ok = 5LL * std::min(A, B) >= n;
+            const long long key[4] = {ok ? 0 : 1, ok ? Lm : std::abs(A - B), std::abs(A - B), m};
+            if (best < 0 || std::lexicographical_compare(key, key + 4, bk, bk + 4)) {
+                best = m;
+                std::copy(key, key + 4, bk);
+            }
+        }
+        std::vector<int> Aset, Bset;
+        for (int i = 0; i < best; i++) Aset.insert(Aset.end(), L[i].begin(), L[i].end());
+        for (int i = best + 1; i <= h; i++) Bset.insert(Bset.end(), L[i].begin(), L[i].end());
+        std::sort(Aset.begin(), Aset.end());
+        std::sort(Bset.begin(), Bset.end());
+        std::vector<int> sep = std::move(L[best]);
+        std::vector<int> kids;
+        order(std::move(Aset), kids);
+        order(std::move(Bset), kids);
+        int hmax = 0;
+        for (int c : kids) hmax = std::max(hmax, t->height[c]);
+        const int s = (int)t->perm.size();
+        t->perm.insert(t->perm.end(), sep.begin(), sep.end());
+        const int id = new_node(s, (int)t->perm.size(), hmax + 1);
+        for (int c : kids) t->parent[c] = id;
+        roots.push_back(id);
+    }
+};
+
+}  // namespace
+
+void nd_order(int n, const std::vector<int>& adjStart, const std::vector<int>& adj, int leaf, NdTree* out) {
+    *out = NdTree{};
+    if (n <= 0) return;
+    Nd nd{adjStart, adj, leaf, out, std::vector<int>(n, 0), std::vector<int>(n, 0)};
+    std::vector<int> all(n), roots;
+    for (int i = 0; i < n; i++) all[i] = i;
+    nd.order(std::move(all), roots);
+}
+
+}  // namespace orbgpu

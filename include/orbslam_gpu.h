@@ -802,6 +802,12 @@ int orbgpu_unit_wave_tree(const double* v64, double* out);
  * maximum 1024, i.e. 4.2 M edges) and writes larger sets to its chunk buffer's tail; 0 sends
  * every problem down the tail path.  Process-wide, device-side. */
 int orbgpu_unit_set_csum_lds_max(int m2_max);
+/* The elimination order of the block-sparse pose system (host only, no device): nested
+ * dissection of a graph (adjStart[n + 1] / adj: symmetric, sorted lists) with leaves of at
+ * most `leaf` nodes; perm[k] = node eliminated k-th; the separator tree's node count and
+ * height (0 = a single leaf). */
+int orbgpu_unit_nd_order(int n, const int32_t* adjStart, const int32_t* adj, int leaf, int32_t* perm,
+                         int32_t* n_nodes, int32_t* height);
 /* Instrumented builds only (make prof): read and clear the BA/pose section timers (32 x u64
  * clock64 deltas of workgroup 0); ORB_E_INVALID in normal builds. */
 int orbgpu_debug_prof(unsigned long long* out32);

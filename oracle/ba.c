@@ -26,9 +26,11 @@
  *     (bit-identical tests); ora_ba_set_order(ORA_BA_G2O) switches the oracle to the
  *     reference's own sequential order (g2o block_solver.hpp:353-560,
  *     sparse_optimizer.cpp:61-114), which the GPU is held to at 1e-5;
- *   - the pose system is factorised by a dense right-looking LDL^T on the
- *     upper triangle in natural pose order (SimplicialLDLT+AMD in the
- *     reference); failure = an exactly zero pivot, like Eigen's LDLT;
+ *   - the pose system is factorised by a right-looking LDL^T on the upper
+ *     triangle (SimplicialLDLT+AMD in the reference): in natural pose order
+ *     below ORA_TILED_MIN_POSES free poses, above in the nested-dissection
+ *     order of the pose graph (ordering.c); failure = an exactly zero pivot,
+ *     like Eigen's LDLT;
  *   - sin/cos in SE3Quat::exp use ora_det_sincos (sim3.c); pow(theta,3) in
  *     exp and pow(2*rho-1,3) in the LM step are (a*a)*a;
  *   - small fixed-size products sum their terms left to right.
@@ -761,18 +763,43 @@ static int schur_solve(ba_ctx* c, double lambda)
                 pA[q] = lpList[u];
                 pB[q] = lpList[w];
             }
-    /* the envelope of S: per column the first row any Schur block (or the diagonal) reaches */
-    int* fcol = (int*)malloc(sizeof(int) * (n + 1));
-    for (int c = 0; c < n; c++) fcol[c] = 6 * (c / 6);
-    for (int l = 0; l < nL; l++)
-        for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
-            for (int w = u; w < lpStart[l + 1]; w++) {
-                const int i1 = POSE_OF(lpList[u]), i2 = POSE_OF(lpList[w]);
-                for (int cc = 0; cc < 6; cc++)
-                    if (6 * i1 < fcol[6 * i2 + cc]) fcol[6 * i2 + cc] = 6 * i1;
-            }
+    /* Storage of S.  nP < ORA_TILED_MIN_POSES: natural order in an envelope (the GPU's dense
+     * single-workgroup solvers); otherwise the nested-dissection order of the pose graph and
+     * the block-sparse factor (ordering.c; the GPU's tiled solver) */
+    const int use_nd = nP >= ORA_TILED_MIN_POSES;
+    int* fcol = NULL;
     env_mat Env;
-    env_init(&Env, n, fcol);
+    memset(&Env, 0, sizeof(Env));
+    ora_sp* SP = NULL;
+    if (use_nd) {
+        int* as = (int*)calloc(nP + 1, sizeof(int));
+        for (int i1 = 0; i1 < nP; i1++)
+            for (int i2 = i1 + 1; i2 < nP; i2++)
+                if (blkOf[(size_t)i1 * nP + i2] >= 0) { as[i1 + 1]++; as[i2 + 1]++; }
+        for (int i = 0; i < nP; i++) as[i + 1] += as[i];
+        int* adj = (int*)malloc(sizeof(int) * (as[nP] + 1));
+        int* f = (int*)malloc(sizeof(int) * (nP + 1));
+        memcpy(f, as, sizeof(int) * nP);
+        for (int i1 = 0; i1 < nP; i1++)   /* lists sorted: i1 ascending, then i2 ascending */
+            for (int i2 = 0; i2 < nP; i2++)
+                if (i1 != i2 && blkOf[(size_t)(i1 < i2 ? i1 : i2) * nP + (i1 < i2 ? i2 : i1)] >= 0) adj[f[i1]++] = i2;
+        int* perm = (int*)malloc(sizeof(int) * (nP + 1));
+        ora_nd_order(nP, as, adj, ORA_ND_LEAF, perm);
+        SP = ora_sp_create(n, 6, as, adj, perm);
+        free(perm); free(f); free(adj); free(as);
+    } else {
+        /* the envelope of S: per column the first row any Schur block (or the diagonal) reaches */
+        fcol = (int*)malloc(sizeof(int) * (n + 1));
+        for (int c = 0; c < n; c++) fcol[c] = 6 * (c / 6);
+        for (int l = 0; l < nL; l++)
+            for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
+                for (int w = u; w < lpStart[l + 1]; w++) {
+                    const int i1 = POSE_OF(lpList[u]), i2 = POSE_OF(lpList[w]);
+                    for (int cc = 0; cc < 6; cc++)
+                        if (6 * i1 < fcol[6 * i2 + cc]) fcol[6 * i2 + cc] = 6 * i1;
+                }
+        env_init(&Env, n, fcol);
+    }
     int maxM = 1;
     for (int q = 0; q < nBlk; q++) if (bStart[q + 1] - bStart[q] > maxM) maxM = bStart[q + 1] - bStart[q];
     double* v = (double*)malloc(sizeof(double) * (maxM + nL + 1));
@@ -793,7 +820,9 @@ static int schur_solve(ba_ctx* c, double lambda)
                         h = c->Hpp[21 * i1 + DIAG21[r] + (cc - r)];
                         if (cc == r) h += lambda;
                     }
-                    ENV(&Env, 6 * i1 + r, 6 * i2 + cc) = ba_sub_terms(h, v, m);
+                    const double val = ba_sub_terms(h, v, m);
+                    if (use_nd) *ora_sp_at(SP, 6 * i1 + r, 6 * i2 + cc) = val;
+                    else ENV(&Env, 6 * i1 + r, 6 * i2 + cc) = val;
                 }
         }
     /* b_schur: per pose, its landmarks' terms in landmark order */
@@ -816,7 +845,7 @@ static int schur_solve(ba_ctx* c, double lambda)
         free(psStart); free(psList); free(pf);
     }
     double* xp = (double*)malloc(sizeof(double) * (n + 1));
-    int ok = n == 0 ? 1 : ora_env_ldlt_solve(&Env, bs, xp);
+    int ok = n == 0 ? 1 : (use_nd ? ora_sp_solve(SP, bs, xp) : ora_env_ldlt_solve(&Env, bs, xp));
     if (ok) {
         memcpy(c->x, xp, sizeof(double) * n);
         /* xl = Dinv (bl - sum_i B_i^T xp_i); rightMultiply over the landmark's blocks in pose order */
@@ -839,7 +868,8 @@ static int schur_solve(ba_ctx* c, double lambda)
     }
 #undef POSE_OF
     free(lpStart); free(lpList); free(blkOf); free(bStart); free(pA); free(pB); free(fill);
-    env_free(&Env); free(fcol);
+    if (use_nd) ora_sp_free(SP);
+    else { env_free(&Env); free(fcol); }
     free(xp); free(v); free(bs); free(E); free(cb); free(Dinv); free(db);
     return ok;
 }

@@ -319,6 +319,17 @@ int   ora_pose_optimization(const ora_pose_problem* P, float* Tcw_out, uint8_t* 
 int   ora_ldlt_pivot_solve(double* H, int n, const double* b, double* x);
 double ora_csum(double* v, int n);
 int   ora_ldlt_solve(double* S, int n, const double* b, double* x);
+/* ordering.c: nested-dissection order of a graph (adjacency lists sorted, symmetric) and the
+ * block-sparse LDL^T of a grouped system in a given group order (perm: position -> group) */
+#define ORA_TILED_MIN_POSES 24   /* the GPU's dense solvers take fewer free poses */
+#define ORA_ND_LEAF 32
+void  ora_nd_order(int n, const int* adjStart, const int* adj, int leaf, int* perm);
+typedef struct ora_sp ora_sp;
+ora_sp* ora_sp_create(int n, int g, const int* adjStart, const int* adj, const int* perm);
+double* ora_sp_at(ora_sp* s, int r, int c);
+int   ora_sp_solve(ora_sp* s, const double* b, double* x);
+void  ora_sp_free(ora_sp* s);
+int   ora_ldlt_solve_nd(const double* S, int n, const double* b, double* x);
 enum { ORA_BA_CANONICAL = 0, ORA_BA_G2O = 1 };
 void  ora_ba_set_order(int mode);   /* accumulation order of the BA / pose oracle (ba.c) */
 int   ora_ba_get_order(void);

@@ -149,3 +149,44 @@ def test_global_ba_config5_2000kf_matches_oracle(gpu):
     _close(s, o)
     for r in per[1:]:
         assert np.array_equal(r["kf_Tcw"], per[0]["kf_Tcw"])
+
+
+def test_global_ba_config5_2000kf_loops_matches_oracle(gpu):
+    """Config 5 shaped as a loop-closed merged map: 2,000 keyframes driven as 4 laps of one
+    circuit, 5 % of the points also seen at the same place on the other laps (the covisibility
+    LoopClosing's SearchAndFuse leaves behind before GlobalBundleAdjustemnt, LoopClosing.cc:
+    231-360, 650), so keyframes ~500 ids apart share points.  The pose system goes through the
+    nested-dissection, level-scheduled tiled LDL^T; the oracle factors in the same order
+    (oracle/ordering.c): bit-identical LM trace and results."""
+    from c_orb_slam_amd.optimizer import BundleAdjustment
+    pr = global_ba_problem(5, n_kf=2000, pts_per_kf=150, laps=4)
+    assert len(pr["edge_pt"]) > 1_000_000
+    assert (np.abs(pr["edge_kf"][1:] - pr["edge_kf"][:-1])[pr["edge_pt"][1:] == pr["edge_pt"][:-1]] > 400).sum() > 5000
+    o = oracle_lib.oracle_global_ba(pr, 10, False)
+    g = BundleAdjustment(pr, 10, False, trace=True)
+    assert g["iterations"] == o["iterations"]
+    np.testing.assert_allclose(g["trial_chi2"], o["trial_chi2"], rtol=1e-12)
+    _exact(g, o)
+
+
+def test_global_ba_config5_2000kf_loops_g2o_order_sharded(gpu):
+    """The same loop-closed 2,000-keyframe map against the oracle in the REFERENCE's accumulation
+    order (g2o's sequential sums, ORA_BA_G2O): 1e-5 relative with identical iteration and LM
+    trial counts, unsharded and keyframe-block sharded over 8 in-process ranks (the RCCL
+    protocol on one device; every rank derives the same order from the gathered union of the
+    shards' Schur blocks)."""
+    from c_orb_slam_amd.optimizer import BundleAdjustment, run_sharded_local
+    pr = global_ba_problem(5, n_kf=2000, pts_per_kf=150, laps=4)
+    with oracle_lib.ba_order("g2o"):
+        o = oracle_lib.oracle_global_ba(pr, 10, False)
+    g = BundleAdjustment(pr, 10, False, trace=True)
+    assert g["iterations"] == o["iterations"]
+    assert len(g["trial_chi2"]) == len(o["trial_chi2"])
+    np.testing.assert_allclose(g["solve_chi2"], o["solve_chi2"], rtol=1e-7)
+    _close(g, o)
+    s, per = run_sharded_local(pr, 8, "global", 10, False, trace=True)
+    assert s["iterations"] == o["iterations"]
+    np.testing.assert_allclose(s["solve_chi2"], o["solve_chi2"], rtol=1e-7)
+    _close(s, o)
+    for r in per[1:]:
+        assert np.array_equal(r["kf_Tcw"], per[0]["kf_Tcw"])

@@ -105,6 +105,57 @@ def test_ldlt_tiled_matches_oracle(gpu, n, kind):
     np.testing.assert_allclose(S @ x, b, rtol=1e-8, atol=1e-8)
 
 
+def _ora_ldlt_nd(S, b):
+    L = oracle_lib.lib()
+    L.ora_ldlt_solve_nd.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    x = np.zeros(len(b))
+    ok = L.ora_ldlt_solve_nd(ptr(np.ascontiguousarray(S, np.float64)), len(b), ptr(np.array(b, np.float64)), ptr(x))
+    return ok, x
+
+
+@pytest.mark.parametrize("nb,kind", [(30, "banded"), (200, "banded"), (333, "banded"), (200, "loops"),
+                                     (400, "laps"), (150, "random")])
+def test_ldlt_nested_dissection_matches_oracle(gpu, nb, kind):
+    """The level-scheduled tiled LDL^T in nested-dissection order (variant 3: the order the BA
+    uses for >= 24 poses) against the oracle's block-sparse restatement in the same order:
+    bit-identical x, and S x = b."""
+    from c_orb_slam_amd._lib import lib
+    rng = np.random.default_rng(100 + nb)
+    if kind == "laps":   # a 4-lap circuit: the same place on every lap covisible
+        n_lap = nb // 4
+        loops = [(i, i + n_lap * m) for i in range(0, n_lap, 2) for m in (1, 2, 3) if i + n_lap * m < nb]
+        S = _banded_spd(rng, nb, 6, loops=loops)
+    elif kind == "random":
+        pairs = rng.integers(0, nb, (3 * nb, 2))
+        S = _banded_spd(rng, nb, 1, loops=[(min(a, b), max(a, b)) for a, b in pairs if a != b])
+    else:
+        S = _banded_spd(rng, nb, 8, loops=[(1, nb - 2), (3, nb // 2), (nb // 4, 3 * nb // 4)] if kind == "loops" else ())
+    n = 6 * nb
+    S_in = S.copy()
+    S_in[np.tril_indices(n, -1)] = np.nan   # only the upper triangle is read
+    b = rng.normal(size=n)
+    x = np.zeros(n)
+    ok = C.c_int()
+    assert lib().orbgpu_unit_ldlt_solve(n, ptr(np.ascontiguousarray(S_in)), ptr(b), ptr(x), 3, C.byref(ok)) == 0
+    oko, xo = _ora_ldlt_nd(np.triu(S), b)
+    assert ok.value == oko == 1
+    assert np.array_equal(x, xo), np.abs(x - xo).max()
+    np.testing.assert_allclose(S @ x, b, rtol=1e-8, atol=1e-8)
+
+
+def test_ldlt_nested_dissection_zero_pivot_fails(gpu):
+    from c_orb_slam_amd._lib import lib
+    rng = np.random.default_rng(5)
+    S = _banded_spd(rng, 120, 4, loops=[(2, 110)])
+    S[6 * 70 + 2, :] = 0.0
+    S[:, 6 * 70 + 2] = 0.0   # an exactly zero pivot in the middle of the order
+    x = np.full(720, 7.0)
+    ok = C.c_int(5)
+    assert lib().orbgpu_unit_ldlt_solve(720, ptr(np.ascontiguousarray(S)), ptr(np.ones(720)), ptr(x), 3, C.byref(ok)) == 0
+    assert ok.value == 0
+    assert (x == 7.0).all()
+
+
 def test_ldlt_tiled_zero_pivot_fails(gpu):
     from c_orb_slam_amd._lib import lib
     n = 300
