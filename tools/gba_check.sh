@@ -17,7 +17,7 @@ rc=$?
 grep -E "PASSED|FAILED|ERROR" "$OUT/pytest.log" | tail -60
 tail -3 "$OUT/pytest.log"
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o gba -- python3 tools/gba_timing.py 2000:0 2000:4 > "$OUT/gba_timing.txt" 2>&1 || { tail -20 "$OUT/gba_timing.txt"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -f csv -o gba -- python3 tools/gba_timing.py 2000:0 2000:4 > "$OUT/gba_timing.txt" 2>&1 || { tail -20 "$OUT/gba_timing.txt"; exit 1; }
 grep "nkf" "$OUT/gba_timing.txt"
 f=$(find "$OUT/prof" -name '*kernel_stats.csv' | head -1)
 [ -n "$f" ] && cp "$f" "$OUT/kernel_stats.csv" && head -25 "$f"
