@@ -60,6 +60,10 @@ def parse():
     ap.add_argument("--gba-laps", type=int, default=-1,
                     help="loop-closed map: the keyframes drive this many laps of one circuit (-1: one lap per "
                          "500 keyframes; 0: an open drive, a pure band)")
+    ap.add_argument("--nfeatures", type=int, default=NFEAT,
+                    help="ORBextractor nFeatures of the stereo pipeline (1200: the metric's; 2000: KITTI00-02.yaml)")
+    ap.add_argument("--pipeline-only", action="store_true",
+                    help="only the timed stereo pipeline (+ its CPU baseline): one compact JSON line")
     ap.add_argument("--launch-timeout", type=float, default=3000.0,
                     help="bound on the whole job when bench.py spawns its own ranks (seconds)")
     ap.add_argument("--passes-only", action="store_true",
@@ -147,7 +151,9 @@ def dry_run(args):
 
 
 def main():
+    global NFEAT
     args = parse()
+    NFEAT = args.nfeatures
     env_world = os.environ.get("WORLD_SIZE")
     if args.gpus is None:
         args.gpus = int(env_world or 1)
@@ -775,6 +781,20 @@ def main():
     # TrackWithMotionModel + TrackLocalMap
     frames_total = P * args.steps * world
     fps = frames_total / dt
+    if args.pipeline_only:   # the yaml feature count's line: pipeline + its CPU baseline
+        if rank == 0:
+            cpu = None if args.no_cpu_baseline else cpu_baseline(lefts, rights, Rs, args.cpu_seconds)
+            line = {"nfeatures": NFEAT, "value": round(fps, 2), "unit": "frames/s", "steps": args.steps,
+                    "ms_per_step": round(dt / args.steps * 1e3, 3), "tracked_frames_per_step": P,
+                    "matches_per_s": round(tot_match / dt, 1),
+                    "keypoints_per_image": round(tot_kp / (2 * B * args.steps * world), 1), "cpu_baseline": cpu}
+            if cpu:
+                line["speedup_vs_cpu_all_core"] = round(fps / cpu["value"], 1)
+            json_out.write(json.dumps(line) + "\n")
+            json_out.flush()
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     # roofline of the dominant extraction kernel (k_fast_cells), measured in its own pass after
     # the timed region: inside the pipeline the kernel shares the GPU with the other extractor
@@ -858,6 +878,21 @@ def main():
         dist.barrier()
 
     ransac.pop("_cpu_args", None)
+    nf2000 = None
+    if rank == 0 and world == 1 and NFEAT != 2000:
+        # the same pipeline at the yaml's nFeatures 2000 (KITTI00-02.yaml:38) in a
+        # fresh process (its own extractors and arenas), with its own CPU baseline
+        import subprocess
+        cmd = [sys.executable, str(Path(__file__).resolve()), "--nfeatures", "2000", "--pipeline-only",
+               "--steps", str(max(10, args.steps // 3)), "--warmup", "3", "--cpu-seconds", str(args.cpu_seconds / 2)]
+        if args.no_cpu_baseline:
+            cmd.append("--no-cpu-baseline")
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+            nf2000 = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+                {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-400:]}
+        except Exception as e:  # noqa: BLE001 -- reported in the line, the headline stands
+            nf2000 = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:
         stage_ms = {k: round(v / args.steps, 4) for k, v in stage_acc.items()}
         out = {
@@ -881,7 +916,7 @@ def main():
             "stage_ms_per_step": stage_ms,
             "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}, "roofline": roof,
             "matcher_roofline": mroof, "latency": latency, "cpu_baseline": cpu, "local_ba": ba,
-            "global_ba": gba, "ransac": ransac,
+            "global_ba": gba, "ransac": ransac, "nfeatures_2000": nf2000,
         }
         json_out.write(json.dumps(out) + "\n")
         json_out.flush()
@@ -942,7 +977,8 @@ def bench_local_ba(args, world, rank, dist, dev):
         dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:])
         dt_s, its_s = float(t[0].item()), int(t[1].item())
-    return {"metric": "local-BA iter/s", "value": round(its_s / dt_s, 1), "unit": "iter/s",
+    sharded = bench_local_ba_sharded(args, world, rank, dist, dev, pr)
+    return {"metric": "local-BA iter/s", "value": round(its_s / dt_s, 1), "unit": "iter/s", "sharded": sharded,
             "streams": S, "single_stream": {"value": round(its / dt, 1), "unit": "iter/s",
                                             "ms_per_call": round(dt / reps * 1e3, 3),
                                             "note": "one problem at a time (the LocalMapping thread's latency)"},
@@ -953,6 +989,42 @@ def bench_local_ba(args, world, rank, dist, dev):
                        "stereo_edges": int((pr["edge_obs"][:, 2] >= 0).sum()),
                        "lm": "optimize(5) + gating + optimize(10)", "parallelism": f"replicas{world}"},
             "dtype": "f64 (f32 I/O)"}
+
+
+def bench_local_ba_sharded(args, world, rank, dist, dev, pr):
+    """Optimizer_LocalBundleAdjustment_sharded on config 4 (north_star: "Local-BA
+    residual/Jacobian evaluation shards by keyframe block across the GPUs ... with an RCCL
+    all-reduce of the normal-equation update"): ONE problem, its map points partitioned by the
+    block of their reference keyframe over the N ranks, an RCCL exchange per LM trial (strong
+    scaling; at N = 1 the exchange steps are identities).  iter = one LM solve()."""
+    import torch
+    from c_orb_slam_amd.optimizer import Comm, LocalBundleAdjustmentSharded, partition_points, shard_problem
+    shard = shard_problem(pr, partition_points(pr, world), rank)
+    uid = [Comm.unique_id() if rank == 0 else None]
+    if dist is not None:
+        dist.broadcast_object_list(uid, src=0)
+    comm = Comm.rccl(world, rank, uid[0])
+    for _ in range(2):
+        LocalBundleAdjustmentSharded(shard, comm)       # warm-up (allocations, structure)
+    reps = max(5, args.steps)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    its = 0
+    for _ in range(reps):
+        its += sum(LocalBundleAdjustmentSharded(shard, comm)["iterations"])
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    comm.close()
+    return {"metric": "local-BA iter/s, keyframe-block sharded", "value": round(its / dt, 1), "unit": "iter/s",
+            "ms_per_call": round(dt / reps * 1e3, 3), "calls": reps, "scaling": "strong",
+            "edges_per_rank": len(shard["edge_pt"]),
+            "parallelism": f"keyframe-block shards x{world} (RCCL all-reduce of the Schur system per LM trial)",
+            "note": "one problem split over the ranks; the replicas figure (`value`) runs one problem per stream"}
 
 
 def gba_laps(args):
