@@ -1403,16 +1403,16 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
     // flags (bit 0: level 1 = inactive, bit 1: robust kernel set), active-edge list as u16
     __shared__ uint8_t fl[kPoseMaxEdges];
     __shared__ uint16_t aE[kPoseMaxEdges];
-    __shared__ double cs[28][kPoseMaxEdges / 64];
+    __shared__ double cs[31][kPoseMaxEdges / 64];
     __shared__ double red[32];
     // speculative solves for 1..kPoseSpec consecutive rejections of a trial (waves 1..kPoseSpec)
     constexpr int kPoseSpec = 3;
-    __shared__ Se3 T, Tbak, Terr, Tbase, Tspec[kPoseSpec];
-    __shared__ double xspec[kPoseSpec][6];
-    __shared__ int specOk[kPoseSpec], specNext, specReady;
-    __shared__ double xs[6], Hs[21], bs[6];
+    __shared__ Se3 T, Terr, Tbase, Tc[kPoseSpec + 1];   // Tc: the candidates of a round of trials
+    __shared__ double xc[kPoseSpec + 1][6];
+    __shared__ int okc[kPoseSpec + 1];
+    __shared__ double xs[6], Hs[21], bs[6], sysN[28];
     __shared__ double lambda, ni, currentChi, iniChi;
-    __shared__ int nA, nBadLM, qmax, again, term, nBad, okS, wsum[16];
+    __shared__ int nA, nBadLM, qmax, again, term, nBad, haveSys, wsum[16];
     const int tid = threadIdx.x;
     const double dM = (double)(float)sqrt(5.991), dS = (double)(float)sqrt(7.815);
     if (ne < 0) {   // device mode: capacity exceeded (reported by the host)
@@ -1437,12 +1437,6 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
     }
     __syncthreads();
     const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
-    // computeActiveErrors + activeRobustChi2 term of edge i
-    auto err_term = [&](const PoseEdgeD& e, int i, double* v) {
-        double e3[3];
-        pose_err(e, T, P, e3);
-        v[0] = pose_rho0(e, pose_chi2(e, e3), (fl[i] & 2) != 0);
-    };
     for (int it = 0; it < 4; it++) {
         if (tid == 0) {
             T = P.T0;   // vSE3->setEstimate(Converter::toSE3Quat(pFrame->mTcw)) every round
@@ -1473,74 +1467,86 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
         const PoseEdgeD myE = pose_edge_load(E, myIdx, dM, dS);
         if (na > 0) {   // optimize(10); without active edges the vertex is not optimised at all
             ORBGPU_PROF_START;
+            // J, robust weight and the 28 entries (robust chi2, J^T W J upper triangle, -J^T W e)
+            // of active edge i at pose X, into v[0..28)
+            auto sys_terms = [&](const PoseEdgeD& e, int i, const Se3& X, double* v) {
+                double e3[3];
+                pose_err(e, X, P, e3);
+                const double c = pose_chi2(e, e3);
+                const bool rb = (fl[i] & 2) != 0;
+                v[0] = pose_rho0(e, c, rb);
+                double p[3];
+                se3_map(X, e.X, p);
+                const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
+                double J[18];
+                J[0] = ((x * y) * invz_2) * P.fx;
+                J[1] = (-(1 + ((x * x) * invz_2))) * P.fx;
+                J[2] = (y * invz) * P.fx;
+                J[3] = (-invz) * P.fx;
+                J[4] = 0;
+                J[5] = (x * invz_2) * P.fx;
+                J[6] = (1 + ((y * y) * invz_2)) * P.fy;
+                J[7] = (((-x) * y) * invz_2) * P.fy;
+                J[8] = ((-x) * invz) * P.fy;
+                J[9] = 0;
+                J[10] = (-invz) * P.fy;
+                J[11] = (y * invz_2) * P.fy;
+                J[12] = J[0] - ((P.bf * y) * invz_2);
+                J[13] = J[1] + ((P.bf * x) * invz_2);
+                J[14] = J[2];
+                J[15] = J[3];
+                J[16] = 0;
+                J[17] = J[5] - (P.bf * invz_2);
+                // monocular edges: a zero third Jacobian row (and err[2] = 0) makes every
+                // third term +-0, an exact identity on the two-term partial sums (which
+                // start from +0 + t0 and so are never -0): the sums run branch-free
+#pragma unroll
+                for (int j = 12; j < 18; j++) J[j] = e.stereo ? J[j] : 0.0;
+                double r1 = 1.;
+                if (rb && !(c <= e.dsqr)) r1 = e.delta / sqrt(c);
+                const double wgt = rb ? r1 * e.info : e.info;
+                double omr[3];
+#pragma unroll
+                for (int kk = 0; kk < 3; kk++) {
+                    omr[kk] = -(e.info * e3[kk]);
+                    if (rb) omr[kk] *= r1;
+                }
+#pragma unroll
+                for (int r = 0; r < 6; r++) {
+                    double sb = 0;
+#pragma unroll
+                    for (int kk = 0; kk < 3; kk++) sb += J[kk * 6 + r] * omr[kk];
+                    v[22 + r] = sb;
+#pragma unroll
+                    for (int cc = r; cc < 6; cc++) {
+                        double hh = 0;
+#pragma unroll
+                        for (int kk = 0; kk < 3; kk++) hh += (J[kk * 6 + r] * wgt) * J[kk * 6 + cc];
+                        v[1 + r * 6 - (r * (r - 1)) / 2 + (cc - r)] = hh;
+                    }
+                }
+            };
+            if (tid == 0) haveSys = 0;
+            __syncthreads();
             for (int k = 0; k < 10; k++) {
                 ORBGPU_PROF_MARK(0);
-                ORBGPU_PROF_COUNT(8);
-                // computeActiveErrors + activeRobustChi2 (entry 0) and buildSystem (entries 1..27:
-                // J^T W J upper triangle, -J^T W e), one pass, canonical sums per entry
-                pose_pass<28>([&](const PoseEdgeD& e, int i, double* v) {
-                    double e3[3];
-                    pose_err(e, T, P, e3);
-                    const double c = pose_chi2(e, e3);
-                    const bool rb = (fl[i] & 2) != 0;
-                    v[0] = pose_rho0(e, c, rb);
-                    double p[3];
-                    se3_map(T, e.X, p);
-                    const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
-                    double J[18];
-                    J[0] = ((x * y) * invz_2) * P.fx;
-                    J[1] = (-(1 + ((x * x) * invz_2))) * P.fx;
-                    J[2] = (y * invz) * P.fx;
-                    J[3] = (-invz) * P.fx;
-                    J[4] = 0;
-                    J[5] = (x * invz_2) * P.fx;
-                    J[6] = (1 + ((y * y) * invz_2)) * P.fy;
-                    J[7] = (((-x) * y) * invz_2) * P.fy;
-                    J[8] = ((-x) * invz) * P.fy;
-                    J[9] = 0;
-                    J[10] = (-invz) * P.fy;
-                    J[11] = (y * invz_2) * P.fy;
-                    J[12] = J[0] - ((P.bf * y) * invz_2);
-                    J[13] = J[1] + ((P.bf * x) * invz_2);
-                    J[14] = J[2];
-                    J[15] = J[3];
-                    J[16] = 0;
-                    J[17] = J[5] - (P.bf * invz_2);
-                    // monocular edges: a zero third Jacobian row (and err[2] = 0) makes every
-                    // third term +-0, an exact identity on the two-term partial sums (which
-                    // start from +0 + t0 and so are never -0): the sums run branch-free
-#pragma unroll
-                    for (int j = 12; j < 18; j++) J[j] = e.stereo ? J[j] : 0.0;
-                    double r1 = 1.;
-                    if (rb && !(c <= e.dsqr)) r1 = e.delta / sqrt(c);
-                    const double wgt = rb ? r1 * e.info : e.info;
-                    double omr[3];
-#pragma unroll
-                    for (int kk = 0; kk < 3; kk++) {
-                        omr[kk] = -(e.info * e3[kk]);
-                        if (rb) omr[kk] *= r1;
+                if (!haveSys) {
+                    ORBGPU_PROF_COUNT(8);
+                    // computeActiveErrors + activeRobustChi2 (entry 0) and buildSystem (entries
+                    // 1..27), one pass, canonical sums per entry
+                    pose_pass<28>([&](const PoseEdgeD& e, int i, double* v) { sys_terms(e, i, T, v); }, na, aE, E, dM,
+                                  dS, cs, red, myE, myIdx);
+                    if (tid < 28) {
+                        if (tid == 0) currentChi = iniChi = red[0];
+                        else if (tid < 22) Hs[tid - 1] = red[tid];
+                        else bs[tid - 22] = red[tid];
                     }
-#pragma unroll
-                    for (int r = 0; r < 6; r++) {
-                        double sb = 0;
-#pragma unroll
-                        for (int kk = 0; kk < 3; kk++) sb += J[kk * 6 + r] * omr[kk];
-                        v[22 + r] = sb;
-#pragma unroll
-                        for (int cc = r; cc < 6; cc++) {
-                            double hh = 0;
-#pragma unroll
-                            for (int kk = 0; kk < 3; kk++) hh += (J[kk * 6 + r] * wgt) * J[kk * 6 + cc];
-                            v[1 + r * 6 - (r * (r - 1)) / 2 + (cc - r)] = hh;
-                        }
-                    }
-                }, na, aE, E, dM, dS, cs, red, myE, myIdx);
-                ORBGPU_PROF_MARK(1);
-                if (tid < 28) {
-                    if (tid == 0) currentChi = iniChi = red[0];
-                    else if (tid < 22) Hs[tid - 1] = red[tid];
-                    else bs[tid - 22] = red[tid];
+                } else if (tid < 28) {   // the system at this estimate came with its accepted trial
+                    if (tid == 0) currentChi = iniChi = sysN[0];
+                    else if (tid < 22) Hs[tid - 1] = sysN[tid];
+                    else bs[tid - 22] = sysN[tid];
                 }
+                ORBGPU_PROF_MARK(1);
                 __syncthreads();
                 if (tid == 0) {
                     if (k == 0) {   // computeLambdaInit over the pose diagonal
@@ -1551,28 +1557,19 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
                         nBadLM = 0;
                     }
                     qmax = 0;
+                    haveSys = 0;
                     Tbase = T;   // the estimate every trial of this iteration starts from
-                    specReady = 0;
-                    specNext = kPoseSpec;
                 }
                 __syncthreads();
+                // Trials, up to four per round: candidate 0 solves at the current lambda (wave 0)
+                // while waves 1..kPoseSpec solve the systems of 1..kPoseSpec consecutive
+                // rejections (lambda *= ni; ni *= 2, the same H, b and starting estimate); ONE
+                // pass then evaluates every candidate's robust chi2 -- and the next iteration's
+                // system at candidate 0, which is the estimate whenever the first trial is
+                // accepted -- and the trials are replayed in the reference's order from it.
                 do {
                     ORBGPU_PROF_MARK(10);
-                    if (specReady) {
-                        // the previous trial was rejected (lambda *= ni, estimate restored) and a
-                        // speculating wave already solved that system: the identical operations,
-                        // done while the earlier trial's solve ran
-                        if (tid == 0) {
-                            const int L = specNext;
-                            Tbak = T;
-#pragma unroll
-                            for (int j = 0; j < 6; j++) xs[j] = xspec[L][j];
-                            okS = 1;
-                            T = Tspec[L];
-                            Terr = Tspec[L];
-                            specNext = L + 1;
-                        }
-                    } else if (tid < 64) {   // wave 0: lane-parallel divisions in the solve
+                    if (tid < 64) {
                         double xn[6];
                         const bool ok2 = pose_solve_w(Hs, bs, lambda, xn);
                         double xl[6];
@@ -1582,21 +1579,14 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
                         ORBGPU_PROF_COUNT(9);
                         Se3 d, r;
                         se3_exp(xl, d);
-                        ORBGPU_PROF_MARK(6);
                         se3_mul(d, Tbase, r);
-                        ORBGPU_PROF_MARK(7);
                         if (tid == 0) {
-                            Tbak = T;
 #pragma unroll
-                            for (int j = 0; j < 6; j++) xs[j] = xl[j];
-                            okS = ok2 ? 1 : 0;
-                            T = r;
-                            Terr = r;   // the pose of the last computeActiveErrors
+                            for (int j = 0; j < 6; j++) xc[0][j] = xl[j];
+                            okc[0] = ok2 ? 1 : 0;
+                            Tc[0] = r;
                         }
                     } else if (tid < 64 * (kPoseSpec + 1)) {
-                        // waves 1..kPoseSpec, concurrently: the solves L+1 consecutive rejections
-                        // of this trial would need (lambda *= ni; ni *= 2 repeated, the same H, b
-                        // and starting estimate)
                         const int L = (tid >> 6) - 1;
                         double ls = lambda, ns = ni;
                         for (int j = 0; j <= L; j++) {
@@ -1605,61 +1595,79 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
                         }
                         double xn[6];
                         const bool ok = pose_solve_w(Hs, bs, ls, xn);
+                        Se3 r = Tbase;
                         if (ok) {
-                            Se3 d, r;
+                            Se3 d;
                             se3_exp(xn, d);
                             se3_mul(d, Tbase, r);
-                            if ((tid & 63) == 0) {
-                                Tspec[L] = r;
-#pragma unroll
-                                for (int j = 0; j < 6; j++) xspec[L][j] = xn[j];
-                            }
                         }
-                        if ((tid & 63) == 0) specOk[L] = ok ? 1 : 0;
-                        if (tid == 64) specNext = 0;
+                        if ((tid & 63) == 0) {
+                            Tc[L + 1] = r;
+#pragma unroll
+                            for (int j = 0; j < 6; j++) xc[L + 1][j] = xn[j];
+                            okc[L + 1] = ok ? 1 : 0;
+                        }
                     }
                     __syncthreads();
                     ORBGPU_PROF_MARK(2);
-                    pose_pass<1>(err_term, na, aE, E, dM, dS, cs, red, myE, myIdx);
+                    pose_pass<28 + kPoseSpec>([&](const PoseEdgeD& e, int i, double* v) {
+                        sys_terms(e, i, Tc[0], v);
+#pragma unroll
+                        for (int L = 1; L <= kPoseSpec; L++) {
+                            double e3[3];
+                            pose_err(e, Tc[L], P, e3);
+                            v[27 + L] = pose_rho0(e, pose_chi2(e, e3), (fl[i] & 2) != 0);
+                        }
+                    }, na, aE, E, dM, dS, cs, red, myE, myIdx);
                     ORBGPU_PROF_MARK(3);
                     if (tid == 0) {
-                        double tempChi = red[0];
-                        if (!okS) tempChi = DBL_MAX;
-                        double rho = currentChi - tempChi;
-                        double sv[6];
-                        for (int j = 0; j < 6; j++) sv[j] = xs[j] * (lambda * xs[j] + bs[j]);
-                        double scale = tree64_local([&](int j) { return sv[j]; }, 6);
-                        scale += 1e-3;
-                        rho /= scale;
-                        if (rho > 0 && isfinite(tempChi)) {
-                            const double a3 = 2 * rho - 1;
-                            double alpha = 1. - (a3 * a3) * a3;
-                            alpha = fmin(alpha, 2. / 3.);
-                            const double scaleFactor = fmax(1. / 3., alpha);
-                            lambda *= scaleFactor;
-                            ni = 2;
-                            currentChi = tempChi;
-                        } else {
-                            lambda *= ni;
-                            ni *= 2;
-                            T = Tbak;
-                        }
-                        qmax++;
-                        again = (rho < 0 && qmax < 10) ? 1 : 0;
-                        specReady = again && specNext < kPoseSpec && specOk[specNext] ? 1 : 0;
-                        if (!again) {
-                            if (qmax == 10 || rho == 0) {
-                                term = 1;
+                        again = 1;
+                        for (int j = 0; j <= kPoseSpec && again; j++) {
+                            if (j > 0 && !okc[j]) break;   // a failed speculative solve: a new round redoes it
+                            double tempChi = j == 0 ? red[0] : red[27 + j];
+                            if (j == 0 && !okc[0]) tempChi = DBL_MAX;
+#pragma unroll
+                            for (int q = 0; q < 6; q++) xs[q] = xc[j][q];
+                            double rho = currentChi - tempChi;
+                            double sv[6];
+                            for (int q = 0; q < 6; q++) sv[q] = xs[q] * (lambda * xs[q] + bs[q]);
+                            double scale = tree64_local([&](int q) { return sv[q]; }, 6);
+                            scale += 1e-3;
+                            rho /= scale;
+                            Terr = Tc[j];   // the pose of the last computeActiveErrors
+                            if (rho > 0 && isfinite(tempChi)) {
+                                const double a3 = 2 * rho - 1;
+                                double alpha = 1. - (a3 * a3) * a3;
+                                alpha = fmin(alpha, 2. / 3.);
+                                const double scaleFactor = fmax(1. / 3., alpha);
+                                lambda *= scaleFactor;
+                                ni = 2;
+                                currentChi = tempChi;
+                                T = Tc[j];
+                                if (j == 0) haveSys = 1;   // red[0..28) is the system at the new estimate
                             } else {
-                                if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
-                                else nBadLM = 0;
-                                term = nBadLM >= 3 ? 1 : 0;
+                                lambda *= ni;
+                                ni *= 2;
+                                T = Tbase;
+                            }
+                            qmax++;
+                            again = (rho < 0 && qmax < 10) ? 1 : 0;
+                            if (!again) {
+                                if (qmax == 10 || rho == 0) {
+                                    term = 1;
+                                } else {
+                                    if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
+                                    else nBadLM = 0;
+                                    term = nBadLM >= 3 ? 1 : 0;
+                                }
                             }
                         }
                     }
                     __syncthreads();
+                    if (haveSys && tid < 28) sysN[tid] = red[tid];
                     ORBGPU_PROF_MARK(4);
                 } while (again);
+                __syncthreads();
                 if (term) break;
             }
         }
@@ -1847,7 +1855,9 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
         cap_ = need;
     }
     char* d = (char*)dArena_;
-    int* dNin = (int*)(d + bProb + bEdge + bOut);
+    // inlier counts: the arena, or in a chain its count blocks (copied when the chain closes)
+    int* dNin = chain ? (int*)chain->dev_counts(sizeof(int) * count) : (int*)(d + bProb + bEdge + bOut);
+    if (!dNin) return -2;
     std::vector<PoseProbDev> tmp;
     PoseProbDev* hp = (PoseProbDev*)hArena_;
     if (chain) {   // hArena_ may still be the source of an earlier queued copy: stage instead
@@ -1883,9 +1893,7 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
                            (uint8_t*)(d + bProb + bEdge));
     ORB_HIP_CHECK(hipGetLastError());
     if (chain) {
-        void* land = chain->land(ninliers, sizeof(int) * count);
-        if (!land) return -2;
-        ORB_HIP_CHECK(hipMemcpyAsync(land, dNin, sizeof(int) * count, hipMemcpyDeviceToHost, st));
+        chain->land_dev(ninliers, dNin, sizeof(int) * count);
         ORB_HIP_CHECK(hipEventRecord(lastUse_, st));
         lastUseSet_ = true;
         return 0;

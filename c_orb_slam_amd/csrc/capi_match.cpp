@@ -217,7 +217,7 @@ int ORBmatcher_SearchByProjection_LastFrame_batch(ORBmatcher_h h, int npairs, co
     if (err) return err;
     // nmatches: small device array
     {
-        void* d = m->arena_alloc((size_t)npairs * 4 + 4);
+        void* d = dev ? m->count_buf((size_t)npairs * 4 + 4) : m->arena_alloc((size_t)npairs * 4 + 4);
         if (!d) return ORB_E_HIP;
         d_nm = (int*)d;
         for (int p = 0; p < npairs; p++) probs[p].nmatches = d_nm + p;
@@ -380,7 +380,7 @@ int ORBmatcher_SearchLocalPoints_batch(ORBmatcher_h h, int count, const orb_fram
     }
     if (m->arena_reserve(need)) return ORB_E_HIP;
     int err = 0;
-    int* d_cnt = (int*)m->arena_alloc((size_t)count * 8);
+    int* d_cnt = (int*)m->count_buf((size_t)count * 8);
     if (!d_cnt) return ORB_E_HIP;
     if (hipMemsetAsync(d_cnt, 0, (size_t)count * 8, s) != hipSuccess) return ORB_E_HIP;
     std::vector<SearchDev> probs(count);

@@ -83,7 +83,7 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
     if (m->arena_reserve(need + 4096)) return ORB_E_HIP;
     int err = 0;
     std::vector<orbgpu::StereoDev> probs(npairs);
-    int* d_kept = (int*)m->arena_alloc(4 * (size_t)npairs);
+    int* d_kept = (int*)(dev ? m->count_buf(4 * (size_t)npairs) : m->arena_alloc(4 * (size_t)npairs));
     for (int p = 0; p < npairs; p++) {
         orbgpu::StereoDev& S = probs[p];
         S.NL = NL[p];

@@ -39,6 +39,7 @@ class DeferredChain {
 public:
     ~DeferredChain() {
         for (auto& b : blocks_) (void)hipHostFree(b.p);
+        for (auto& b : devs_) (void)hipFree(b.p);
         for (auto& e : events_)
             if (e.ev) (void)hipEventDestroy(e.ev);
     }
@@ -56,8 +57,61 @@ public:
         if (p) cur_outs_.push_back(Out{p, user, bytes});
         return p;
     }
+    // Device memory for a call's counts (kernels write them), valid until the chain finishes:
+    // land_dev() defers the copy to close(), where ONE D2H per device block carries every
+    // count of the epoch -- no copy sits between the chain's kernels.
+    void* dev_counts(size_t bytes) {
+        bytes = (bytes + 255) & ~(size_t)255;
+        std::lock_guard<std::mutex> g(mu_);
+        if (cur_dev_ < 0 || devs_[cur_dev_].used + bytes > devs_[cur_dev_].cap) {
+            int k = -1;
+            for (size_t q = 0; q < devs_.size(); q++)
+                if (!devs_[q].busy && devs_[q].cap >= bytes) {
+                    k = (int)q;
+                    break;
+                }
+            if (k < 0) {
+                void* p = nullptr;
+                const size_t cap = bytes < 65536 ? 65536 : bytes;
+                if (hipMalloc(&p, cap) != hipSuccess) return nullptr;
+                devs_.push_back(DevBlock{p, cap, 0, false});
+                k = (int)devs_.size() - 1;
+            }
+            devs_[k].busy = true;
+            devs_[k].used = 0;
+            cur_devs_.push_back(k);
+            cur_dev_ = k;
+        }
+        DevBlock& b = devs_[cur_dev_];
+        void* p = (char*)b.p + b.used;
+        b.used += bytes;
+        return p;
+    }
+    void land_dev(void* user, const void* dev, size_t bytes) {
+        std::lock_guard<std::mutex> g(mu_);
+        cur_dev_outs_.push_back(DevOut{user, dev, bytes});
+    }
     // close the current chain: record its end on `s`; *id = its epoch
     int close(hipStream_t s, long long* id) {
+        // the epoch's device count blocks: one D2H each into a pinned block, mapped to the users
+        std::vector<int> devs;
+        std::vector<DevOut> douts;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            devs.swap(cur_devs_);
+            douts.swap(cur_dev_outs_);
+            cur_dev_ = -1;
+        }
+        for (int k : devs) {
+            const DevBlock b = devs_[k];
+            if (!b.used) continue;
+            char* pin = (char*)take(b.used);
+            if (!pin) return -2;
+            ORB_HIP_CHECK(hipMemcpyAsync(pin, b.p, b.used, hipMemcpyDeviceToHost, s));
+            for (const DevOut& o : douts)
+                if ((const char*)o.dev >= (const char*)b.p && (const char*)o.dev < (const char*)b.p + b.cap)
+                    cur_outs_.push_back(Out{pin + ((const char*)o.dev - (const char*)b.p), o.user, o.bytes});
+        }
         std::lock_guard<std::mutex> g(mu_);
         size_t k = 0;
         while (k < events_.size() && (events_[k].live || events_[k].waiters > 0)) k++;
@@ -68,7 +122,7 @@ public:
         ORB_HIP_CHECK(hipEventRecord(events_[k].ev, s));
         events_[k].live = true;
         const long long e = next_id_++;
-        closed_.push_back(Epoch{e, (int)k, std::move(cur_blocks_), std::move(cur_outs_)});
+        closed_.push_back(Epoch{e, (int)k, std::move(cur_blocks_), std::move(cur_outs_), std::move(devs)});
         cur_blocks_.clear();
         cur_outs_.clear();
         if (id) *id = e;
@@ -118,6 +172,7 @@ public:
             for (auto& o : ep.outs) std::memcpy(o.user, o.pin, o.bytes);
             std::lock_guard<std::mutex> g(mu_);
             for (int b : ep.blocks) blocks_[b].busy = false;
+            for (int b : ep.devs) devs_[b].busy = false;
             done_id_ = ep.id;
         }
     }
@@ -144,6 +199,17 @@ private:
         int ev;   // index into events_
         std::vector<int> blocks;
         std::vector<Out> outs;
+        std::vector<int> devs;   // device count blocks
+    };
+    struct DevBlock {
+        void* p;
+        size_t cap, used;
+        bool busy;
+    };
+    struct DevOut {
+        void* user;
+        const void* dev;
+        size_t bytes;
     };
     struct Ev {
         hipEvent_t ev = nullptr;
@@ -174,6 +240,10 @@ private:
     std::vector<Out> cur_outs_;
     std::deque<Epoch> closed_;
     std::vector<Ev> events_;
+    std::vector<DevBlock> devs_;
+    std::vector<int> cur_devs_;
+    std::vector<DevOut> cur_dev_outs_;
+    int cur_dev_ = -1;
     long long next_id_ = 1, done_id_ = 0;
 };
 

@@ -113,11 +113,17 @@ public:
     DeferredChain& chain() { return chain_; }
     // H2D source: the caller's host bytes, or a pinned copy of them in deferred mode
     const void* h2d_src(const void* host, size_t bytes) { return chain_.on() ? chain_.stage(host, bytes) : host; }
-    // D2H of device counts into `user`; in deferred mode via a pinned block copied at finish()
+    // Device memory for a call's counts: the arena, or in deferred mode the chain's count
+    // blocks (they outlive the call: the copy happens when the chain closes)
+    void* count_buf(size_t bytes) { return chain_.on() ? chain_.dev_counts(bytes) : arena_alloc(bytes); }
+    // D2H of device counts (from count_buf) into `user`: now, or in deferred mode at the
+    // chain's close (one copy for the epoch, landing at finish())
     int d2h_counts(void* user, const void* dev, size_t bytes) {
-        void* dst = chain_.on() ? chain_.land(user, bytes) : user;
-        if (!dst) return -2;
-        ORB_HIP_CHECK(hipMemcpyAsync(dst, dev, bytes, hipMemcpyDeviceToHost, stream_));
+        if (chain_.on()) {
+            chain_.land_dev(user, dev, bytes);
+            return 0;
+        }
+        ORB_HIP_CHECK(hipMemcpyAsync(user, dev, bytes, hipMemcpyDeviceToHost, stream_));
         return 0;
     }
     // end of a call: sync unless deferred
