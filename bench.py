@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md (spec)
 ROOFLINE_REPS = 5
 TRAFFIC_FILE = "traffic_r02.json"   # PMC FETCH_SIZE/WRITE_SIZE per launch (tools/pmc_traffic.py)
 VALU_FILE = "valu_r02.json"   # PMC SQ_INSTS_VALU per launch (tools/pmc_valu.py)
-MATCH_PMC_FILE = "match_pmc_r02.json"   # matcher kernels: HBM bytes and VALU instructions per launch (tools/pmc_match.py)
+MATCH_PMC_FILE = "match_pmc_r03.json"   # matcher kernels: HBM bytes and VALU instructions per launch (tools/pmc_match.py)
 VALU_PEAK_GINST = 1228.8   # 256 CUs x 2 wave64 VALU issues per cycle x 2.4 GHz (MI355X_MICROARCH.md)
 W, H, NFEAT = 1241, 376, 1200
 K_LOCAL = 5   # local map = the map points of the last K_LOCAL frames (UpdateLocalMap's local keyframes)
@@ -639,9 +639,31 @@ def main():
                  (("search_pairs", 0), ("search_queries", 1)))
             check(L.ORBmatcher_SearchCandidates(m._h, C.c_void_p(qd.data_ptr()), nq, C.c_void_p(td.data_ptr()),
                                                 len(td), C.c_void_p(off.data_ptr()), C.c_void_p(cand.data_ptr()),
-                                                C.c_void_p(dist.data_ptr()), C.c_void_p(bi.data_ptr()),
+                                                None, C.c_void_p(bi.data_ptr()),
                                                 C.c_void_p(bd.data_ptr()), C.c_void_p(sd.data_ptr())), "SearchCandidates")
             grab((("k_csr_hamming", 6),), (("csr_pairs", 4), ("csr_queries", 5)))
+        # the same 16 tiles through the brute-force kernel (LDS-resident train blocks, no
+        # candidate lists): SURVEY config 2 (ii) as the north star states it
+        bi_l = [torch.empty(int(nL[b]), dtype=torch.int32, device=dev) for b in range(B2)]
+        bd_l = [torch.empty(int(nL[b]), dtype=torch.int32, device=dev) for b in range(B2)]
+        sd_l = [torch.empty(int(nL[b]), dtype=torch.int32, device=dev) for b in range(B2)]
+        qp = arr([lane.d_desc[b].data_ptr() for b in range(B2)])
+        tp = arr([lane.d_desc[b + 1].data_ptr() for b in range(B2)])
+        nq_d = np.ascontiguousarray(nL[:B2], np.int32)
+        nt_d = np.ascontiguousarray(nL[1:B2 + 1], np.int32)
+        dense_ms, dense_pairs = [], []
+        dms, dpairs = C.c_float(), C.c_longlong()
+        for _ in range(reps):
+            check(L.ORBmatcher_SearchDense_batch(m._h, B2, qp, ptr(nq_d), tp, ptr(nt_d),
+                                                 arr([x.data_ptr() for x in bi_l]), arr([x.data_ptr() for x in bd_l]),
+                                                 arr([x.data_ptr() for x in sd_l])), "SearchDense_batch")
+            check(L.ORBmatcher_last_dense_timing(m._h, C.byref(dms), C.byref(dpairs)), "last_dense_timing")
+            dense_ms.append(dms.value)
+            dense_pairs.append(dpairs.value)
+        # the dense kernel's answer equals the CSR engine's on the same tiles (bit-exact)
+        csr_bd = bd.cpu().numpy()
+        dense_ok = bool(np.array_equal(np.concatenate([x.cpu().numpy() for x in bd_l]), csr_bd) and
+                        np.array_equal(np.concatenate([x.cpu().numpy() for x in sd_l]), sd.cpu().numpy()))
         check(L.ORBmatcher_enable_timing(m._h, 0), "ORBmatcher_enable_timing")
         pmc = {}
         pf = ROOT / "profiles" / MATCH_PMC_FILE
@@ -675,6 +697,31 @@ def main():
             out[k] = e
         out["k_csr_hamming"]["workload"] = f"dense tiles: {B2} frame pairs, every left descriptor of frame b against " \
                                            f"every left descriptor of frame b+1 (SURVEY config 2 (ii))"
+        t = float(np.mean(dense_ms))
+        pairs = float(np.mean(dense_pairs))
+        qs = float(nq_d.sum())
+        alg = pairs * 32 + qs * 16          # streamed train descriptor per pair + 16 B out per query
+        ed = {"avg_launch_ms": round(t, 4), "pairs_per_launch": int(pairs), "queries_per_launch": int(qs),
+              "alg_bytes_per_launch": int(alg), "pairs_per_s": round(pairs / (t * 1e-3), 1),
+              "achieved": round(alg / (t * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "equals_csr_result": dense_ok,
+              "workload": f"the same {B2} dense tiles as k_csr_hamming, brute force over LDS-resident 256-row train "
+                          "blocks (k_dense_hamming + k_dense_merge; time = both kernels)",
+              "note": "alg bytes count 32 B per pair as if every pair streamed its train descriptor; the kernel "
+                      "reads each train block once per 256 queries (LDS broadcast), so it is VALU-bound: see valu"}
+        if "k_dense_hamming" in pmc:
+            e2 = pmc["k_dense_hamming"]
+            if e2.get("hbm_bytes_per_launch"):
+                ed["traffic"] = e2["hbm_bytes_per_launch"]
+                ed["hbm_achieved"] = round(ed["traffic"] / (t * 1e-3) / 1e9, 2)
+                ed["hbm_frac"] = round(ed["hbm_achieved"] / HBM_PEAK_GBS, 5)
+            vi = e2.get("valu_insts_per_launch")
+            if vi:
+                vr = vi / (t * 1e-3) / 1e9
+                ed["valu"] = {"insts_per_launch": int(vi), "achieved": round(vr, 1), "peak": VALU_PEAK_GINST,
+                              "unit": "G wave-instr/s", "frac": round(vr / VALU_PEAK_GINST, 4)}
+            ed["pmc_source"] = f"profiles/{MATCH_PMC_FILE}"
+        out["k_dense_hamming"] = ed
         for k in ("k_build_grid", "k_select", "k_stereo_rows", "k_stereo_filter"):
             out[k] = {"avg_launch_ms": round(float(np.mean(acc[k])), 4), "bound": "latency (one workgroup per frame)"}
         out["definition"] = ("alg bytes = 36 B per scored (query, candidate) pair (32 B candidate descriptor + 4 B "

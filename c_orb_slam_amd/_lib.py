@@ -84,13 +84,38 @@ def header_functions(path=HEADER):
 _lib = None
 
 
+class _MissingSymbol:
+    """A symbol an older tools build (ORBGPU_LIB) does not export: binding it is a no-op, calling it fails."""
+
+    def __init__(self, name):
+        self.__dict__["name"] = name
+
+    def __setattr__(self, k, v):
+        pass
+
+    def __call__(self, *a):
+        raise AttributeError(f"{LIB_PATH} does not export {self.name}")
+
+
+class _ToolsCDLL(C.CDLL):
+    def __getattr__(self, name):
+        try:
+            return super().__getattr__(name)
+        except AttributeError:
+            if name.startswith("__"):
+                raise
+            return _MissingSymbol(name)
+
+
 def lib():
     global _lib
     if _lib is not None:
         return _lib
     if not LIB_PATH.exists():
         raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
-    L = C.CDLL(str(LIB_PATH))
+    # the product library must export every binding below; a tools build given by ORBGPU_LIB (an
+    # instrumented or older build for A/B timing) may lack newer entry points
+    L = (_ToolsCDLL if os.environ.get("ORBGPU_LIB") else C.CDLL)(str(LIB_PATH))
     vp, i32, f32, sz = C.c_void_p, C.c_int, C.c_float, C.c_size_t
     P = C.POINTER
     L.orbgpu_version.restype = C.c_char_p
@@ -190,6 +215,8 @@ def lib():
     L.orbgpu_unit_pnp_layout.argtypes = [i32, vp, vp, vp, vp]
     L.MapPoint_CreateStereo_batch_device.argtypes = [vp, i32, vp]
     L.Tracking_PrepareLocalSearch_batch_device.argtypes = [vp, i32, vp]
+    L.ORBmatcher_SearchDense_batch.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp]
+    L.ORBmatcher_last_dense_timing.argtypes = [vp, vp, vp]
     L.ORBmatcher_SearchLocalPoints_batch.argtypes = [vp, i32, vp, vp, vp, f32, f32, f32, vp, vp]
     L.Frame_isInFrustum_batch.argtypes = [vp, i32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp]
     L.ORBmatcher_enable_timing.argtypes = [vp, i32]

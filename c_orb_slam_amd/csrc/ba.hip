@@ -1403,7 +1403,7 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
     // flags (bit 0: level 1 = inactive, bit 1: robust kernel set), active-edge list as u16
     __shared__ uint8_t fl[kPoseMaxEdges];
     __shared__ uint16_t aE[kPoseMaxEdges];
-    __shared__ double cs[31][kPoseMaxEdges / 64];
+    __shared__ double cs[28][kPoseMaxEdges / 64];
     __shared__ double red[32];
     // speculative solves for 1..kPoseSpec consecutive rejections of a trial (waves 1..kPoseSpec)
     constexpr int kPoseSpec = 3;
@@ -1412,7 +1412,7 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
     __shared__ int okc[kPoseSpec + 1];
     __shared__ double xs[6], Hs[21], bs[6], sysN[28];
     __shared__ double lambda, ni, currentChi, iniChi;
-    __shared__ int nA, nBadLM, qmax, again, term, nBad, haveSys, wsum[16];
+    __shared__ int nA, nBadLM, qmax, again, term, nBad, haveSys, specPass, wsum[16];
     const int tid = threadIdx.x;
     const double dM = (double)(float)sqrt(5.991), dS = (double)(float)sqrt(7.815);
     if (ne < 0) {   // device mode: capacity exceeded (reported by the host)
@@ -1563,10 +1563,11 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
                 __syncthreads();
                 // Trials, up to four per round: candidate 0 solves at the current lambda (wave 0)
                 // while waves 1..kPoseSpec solve the systems of 1..kPoseSpec consecutive
-                // rejections (lambda *= ni; ni *= 2, the same H, b and starting estimate); ONE
-                // pass then evaluates every candidate's robust chi2 -- and the next iteration's
-                // system at candidate 0, which is the estimate whenever the first trial is
-                // accepted -- and the trials are replayed in the reference's order from it.
+                // rejections (lambda *= ni; ni *= 2, the same H, b and starting estimate).  The
+                // pass of the first trial computes the whole system at candidate 0 (its robust
+                // chi2 is entry 0), so an accepted first trial hands the next iteration its
+                // system; a rejected one is followed by ONE pass for the speculative candidates,
+                // whose trials are then replayed in the reference's order.
                 do {
                     ORBGPU_PROF_MARK(10);
                     if (tid < 64) {
@@ -1610,61 +1611,72 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
                     }
                     __syncthreads();
                     ORBGPU_PROF_MARK(2);
-                    pose_pass<28 + kPoseSpec>([&](const PoseEdgeD& e, int i, double* v) {
-                        sys_terms(e, i, Tc[0], v);
-#pragma unroll
-                        for (int L = 1; L <= kPoseSpec; L++) {
-                            double e3[3];
-                            pose_err(e, Tc[L], P, e3);
-                            v[27 + L] = pose_rho0(e, pose_chi2(e, e3), (fl[i] & 2) != 0);
-                        }
-                    }, na, aE, E, dM, dS, cs, red, myE, myIdx);
+                    // the trial at candidate 0: its robust chi2 and, with it, the system at that
+                    // estimate (the next iteration's whenever the trial is accepted)
+                    pose_pass<28>([&](const PoseEdgeD& e, int i, double* v) { sys_terms(e, i, Tc[0], v); }, na, aE, E, dM,
+                                  dS, cs, red, myE, myIdx);
                     ORBGPU_PROF_MARK(3);
-                    if (tid == 0) {
-                        again = 1;
-                        for (int j = 0; j <= kPoseSpec && again; j++) {
-                            if (j > 0 && !okc[j]) break;   // a failed speculative solve: a new round redoes it
-                            double tempChi = j == 0 ? red[0] : red[27 + j];
-                            if (j == 0 && !okc[0]) tempChi = DBL_MAX;
+                    // one trial of the reference's loop (optimization_algorithm_levenberg.cpp:100-149)
+                    // at candidate j with robust chi2 tempChi; tid 0 only
+                    auto trial = [&](int j, double tempChi) {
+                        if (!okc[j]) tempChi = DBL_MAX;
 #pragma unroll
-                            for (int q = 0; q < 6; q++) xs[q] = xc[j][q];
-                            double rho = currentChi - tempChi;
-                            double sv[6];
-                            for (int q = 0; q < 6; q++) sv[q] = xs[q] * (lambda * xs[q] + bs[q]);
-                            double scale = tree64_local([&](int q) { return sv[q]; }, 6);
-                            scale += 1e-3;
-                            rho /= scale;
-                            Terr = Tc[j];   // the pose of the last computeActiveErrors
-                            if (rho > 0 && isfinite(tempChi)) {
-                                const double a3 = 2 * rho - 1;
-                                double alpha = 1. - (a3 * a3) * a3;
-                                alpha = fmin(alpha, 2. / 3.);
-                                const double scaleFactor = fmax(1. / 3., alpha);
-                                lambda *= scaleFactor;
-                                ni = 2;
-                                currentChi = tempChi;
-                                T = Tc[j];
-                                if (j == 0) haveSys = 1;   // red[0..28) is the system at the new estimate
+                        for (int q = 0; q < 6; q++) xs[q] = xc[j][q];
+                        double rho = currentChi - tempChi;
+                        double sv[6];
+                        for (int q = 0; q < 6; q++) sv[q] = xs[q] * (lambda * xs[q] + bs[q]);
+                        double scale = tree64_local([&](int q) { return sv[q]; }, 6);
+                        scale += 1e-3;
+                        rho /= scale;
+                        Terr = Tc[j];   // the pose of the last computeActiveErrors
+                        if (rho > 0 && isfinite(tempChi)) {
+                            const double a3 = 2 * rho - 1;
+                            double alpha = 1. - (a3 * a3) * a3;
+                            alpha = fmin(alpha, 2. / 3.);
+                            const double scaleFactor = fmax(1. / 3., alpha);
+                            lambda *= scaleFactor;
+                            ni = 2;
+                            currentChi = tempChi;
+                            T = Tc[j];
+                            if (j == 0) haveSys = 1;   // red[0..28) is the system at the new estimate
+                        } else {
+                            lambda *= ni;
+                            ni *= 2;
+                            T = Tbase;
+                        }
+                        qmax++;
+                        again = (rho < 0 && qmax < 10) ? 1 : 0;
+                        if (!again) {
+                            if (qmax == 10 || rho == 0) {
+                                term = 1;
                             } else {
-                                lambda *= ni;
-                                ni *= 2;
-                                T = Tbase;
-                            }
-                            qmax++;
-                            again = (rho < 0 && qmax < 10) ? 1 : 0;
-                            if (!again) {
-                                if (qmax == 10 || rho == 0) {
-                                    term = 1;
-                                } else {
-                                    if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
-                                    else nBadLM = 0;
-                                    term = nBadLM >= 3 ? 1 : 0;
-                                }
+                                if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
+                                else nBadLM = 0;
+                                term = nBadLM >= 3 ? 1 : 0;
                             }
                         }
+                    };
+                    if (tid == 0) {
+                        trial(0, red[0]);
+                        specPass = again && okc[1] ? 1 : 0;
                     }
                     __syncthreads();
                     if (haveSys && tid < 28) sysN[tid] = red[tid];
+                    if (specPass) {
+                        // candidate 0 rejected: the speculative candidates' robust chi2 in one pass,
+                        // then their trials in order while they are rejected
+                        pose_pass<kPoseSpec>([&](const PoseEdgeD& e, int i, double* v) {
+#pragma unroll
+                            for (int L = 1; L <= kPoseSpec; L++) {
+                                double e3[3];
+                                pose_err(e, Tc[L], P, e3);
+                                v[L - 1] = pose_rho0(e, pose_chi2(e, e3), (fl[i] & 2) != 0);
+                            }
+                        }, na, aE, E, dM, dS, cs, red, myE, myIdx);
+                        if (tid == 0)
+                            for (int j = 1; j <= kPoseSpec && again && okc[j]; j++) trial(j, red[j - 1]);
+                        __syncthreads();
+                    }
                     ORBGPU_PROF_MARK(4);
                 } while (again);
                 __syncthreads();

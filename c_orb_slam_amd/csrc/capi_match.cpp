@@ -412,6 +412,67 @@ int ORBmatcher_SearchLocalPoints_batch(ORBmatcher_h h, int count, const orb_fram
     return m->end_call() ? ORB_E_HIP : ORB_OK;
 }
 
+int ORBmatcher_SearchDense_batch(ORBmatcher_h h, int count, const uint8_t* const* qdesc, const int* nq,
+                                 const uint8_t* const* tdesc, const int* nt, int32_t* const* best_idx,
+                                 int32_t* const* best_dist, int32_t* const* second_dist) {
+    if (!h || count < 0 || (count > 0 && (!qdesc || !nq || !tdesc || !nt || !best_idx || !best_dist || !second_dist)))
+        return ORB_E_INVALID;
+    for (int p = 0; p < count; p++) {
+        if (nq[p] < 0 || nt[p] < 0) return ORB_E_INVALID;
+        if (nq[p] > 0 && (!qdesc[p] || !best_idx[p] || !best_dist[p] || !second_dist[p])) return ORB_E_INVALID;
+        if (nt[p] > 0 && !tdesc[p]) return ORB_E_INVALID;
+    }
+    if (count == 0) return ORB_OK;
+    Matcher* m = h->m;
+    const bool dev = m->device_pointers();
+    hipStream_t s = m->stream();
+    std::vector<orbgpu::DenseDev> probs;
+    if (!dev) {
+        size_t need = 4096;
+        for (int p = 0; p < count; p++) need += al((size_t)nq[p] * 32) + al((size_t)nt[p] * 32) + 3 * al((size_t)nq[p] * 4);
+        if (m->arena_reserve(need)) return ORB_E_HIP;
+    }
+    int err = 0;
+    for (int p = 0; p < count; p++) {
+        if (nq[p] == 0) continue;
+        orbgpu::DenseDev d;
+        d.nq = nq[p];
+        d.nt = nt[p];
+        if (dev) {
+            d.q = qdesc[p];
+            d.t = tdesc[p];
+            d.best_idx = best_idx[p];
+            d.best_dist = best_dist[p];
+            d.second_dist = second_dist[p];
+        } else {
+            d.q = up(m, qdesc[p], (size_t)nq[p] * 32, s, &err);
+            d.t = nt[p] ? up(m, tdesc[p], (size_t)nt[p] * 32, s, &err) : nullptr;
+            d.best_idx = (int*)m->arena_alloc((size_t)nq[p] * 4);
+            d.best_dist = (int*)m->arena_alloc((size_t)nq[p] * 4);
+            d.second_dist = (int*)m->arena_alloc((size_t)nq[p] * 4);
+            if (!d.best_idx || !d.best_dist || !d.second_dist) err = ORB_E_HIP;
+        }
+        probs.push_back(d);
+    }
+    if (err) return err;
+    if (m->dense(probs)) return ORB_E_HIP;
+    if (dev) return m->end_call() ? ORB_E_HIP : ORB_OK;
+    for (int p = 0, k = 0; p < count; p++) {
+        if (nq[p] == 0) continue;
+        const orbgpu::DenseDev& d = probs[k++];
+        if (hipMemcpyAsync(best_idx[p], d.best_idx, (size_t)nq[p] * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(best_dist[p], d.best_dist, (size_t)nq[p] * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(second_dist[p], d.second_dist, (size_t)nq[p] * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return ORB_E_HIP;
+    }
+    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+}
+
+int ORBmatcher_last_dense_timing(ORBmatcher_h h, float* ms, long long* pairs) {
+    if (!h || !ms || !pairs) return ORB_E_INVALID;
+    return h->m->dense_timing(ms, pairs) ? ORB_E_HIP : ORB_OK;
+}
+
 int ORBmatcher_SearchCandidates(ORBmatcher_h h, const uint8_t* qdesc, int nq, const uint8_t* tdesc, int nt,
                                 const int32_t* off, const int32_t* cand, int32_t* dist, int32_t* best_idx,
                                 int32_t* best_dist, int32_t* second_dist) {

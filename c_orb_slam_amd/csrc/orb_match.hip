@@ -167,10 +167,45 @@ struct QueryWin {
     int minLevel, maxLevel;
 };
 
+// Where a search reads the current frame's grid, keypoints and descriptors: HBM (GView), or
+// the LDS copy a k_candidates workgroup stages once for its queries (LView).
+struct GView {
+    const SearchDev& P;
+    __device__ __forceinline__ int start(int c) const { return P.gridStart[c]; }
+    __device__ __forceinline__ int idx(int j) const { return P.gridIdx[j]; }
+    __device__ __forceinline__ void kp(int i, float& x, float& y, int& oct) const {
+        const orb_kp_dev k = P.cur.keysUn[i];
+        x = k.x;
+        y = k.y;
+        oct = k.octave;
+    }
+    __device__ __forceinline__ int dist(const Desc32& d, int i) const { return d.dist(P.cur.desc + 32 * (size_t)i); }
+};
+struct LView {
+    const uint16_t* gs;   // gridStart (kGridCells + 1)
+    const uint16_t* gi;   // gridIdx (N)
+    const float2* xy;     // keysUn x, y (N)
+    const uint8_t* oct;   // keysUn octave (N)
+    const uint4* desc;    // descriptors (2 per keypoint)
+    __device__ __forceinline__ int start(int c) const { return gs[c]; }
+    __device__ __forceinline__ int idx(int j) const { return gi[j]; }
+    __device__ __forceinline__ void kp(int i, float& x, float& y, int& o) const {
+        const float2 v = xy[i];
+        x = v.x;
+        y = v.y;
+        o = oct[i];
+    }
+    __device__ __forceinline__ int dist(const Desc32& d, int i) const {
+        const uint4 b0 = desc[2 * i], b1 = desc[2 * i + 1];
+        return __popc(d.a0.x ^ b0.x) + __popc(d.a0.y ^ b0.y) + __popc(d.a0.z ^ b0.z) + __popc(d.a0.w ^ b0.w) +
+               __popc(d.a1.x ^ b1.x) + __popc(d.a1.y ^ b1.y) + __popc(d.a1.z ^ b1.z) + __popc(d.a1.w ^ b1.w);
+    }
+};
+
 // Frame::GetFeaturesInArea (Frame.cc:327-380) over the CSR grid, calling
 // visit(idx) in the reference's enumeration order.
-template <class Visit>
-__device__ __forceinline__ void for_features_in_area(const SearchDev& P, const QueryWin& w, Visit visit) {
+template <class View, class Visit>
+__device__ __forceinline__ void for_features_in_area(const SearchDev& P, const View& V, const QueryWin& w, Visit visit) {
     const FrameDev& F = P.cur;
     const int nMinCellX = max(0, (int)floorf((w.x - F.minX - w.r) * F.gridWInv));
     if (nMinCellX >= kGridCols) return;
@@ -184,18 +219,24 @@ __device__ __forceinline__ void for_features_in_area(const SearchDev& P, const Q
     for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
         for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
             const int c = ix * kGridRows + iy;
-            const int e = P.gridStart[c + 1];
-            for (int j = P.gridStart[c]; j < e; j++) {
-                const int idx = P.gridIdx[j];
-                const orb_kp_dev kp = F.keysUn[idx];
+            const int e = V.start(c + 1);
+            for (int j = V.start(c); j < e; j++) {
+                const int idx = V.idx(j);
+                float kx, ky;
+                int ko;
+                V.kp(idx, kx, ky, ko);
                 if (bCheckLevels) {
-                    if (kp.octave < w.minLevel) continue;
-                    if (w.maxLevel >= 0 && kp.octave > w.maxLevel) continue;
+                    if (ko < w.minLevel) continue;
+                    if (w.maxLevel >= 0 && ko > w.maxLevel) continue;
                 }
-                const float distx = kp.x - w.x, disty = kp.y - w.y;
+                const float distx = kx - w.x, disty = ky - w.y;
                 if (fabsf(distx) < w.r && fabsf(disty) < w.r) visit(idx);
             }
         }
+}
+template <class Visit>
+__device__ __forceinline__ void for_features_in_area(const SearchDev& P, const QueryWin& w, Visit visit) {
+    for_features_in_area(P, GView{P}, w, visit);
 }
 
 // The K best (dist, idx) of a query's candidates, sorted by dist, equal distances in visit
@@ -275,21 +316,25 @@ __device__ __forceinline__ void fwd_bwd(const SearchDev& P, bool bMono, bool& bF
 }
 
 // Enumerate a LastFrame query's passing candidates; `blocked(i2)` models occupancy.
-template <class Blocked, class Top>
-__device__ int scan_last(const SearchDev& P, const LastQuery& q, Blocked blocked, Top& top) {
+template <class Blocked, class Top, class View = GView>
+__device__ int scan_last(const SearchDev& P, const LastQuery& q, Blocked blocked, Top& top, const View& V) {
     int cnt = 0;
     const Desc32 dMP(P.mpDesc + 32 * (size_t)q.mp);
-    for_features_in_area(P, q.w, [&](int i2) {
+    for_features_in_area(P, V, q.w, [&](int i2) {
         if (blocked(i2)) return;
         if (P.cur.uRight && P.cur.uRight[i2] > 0) {
             const float ur = q.u - P.cur.bf * q.invzc;
             const float er = fabsf(ur - P.cur.uRight[i2]);
             if (er > q.radius) return;
         }
-        top.insert(dMP.dist(P.cur.desc + 32 * (size_t)i2), i2);
+        top.insert(V.dist(dMP, i2), i2);
         cnt++;
     });
     return cnt;
+}
+template <class Blocked, class Top>
+__device__ int scan_last(const SearchDev& P, const LastQuery& q, Blocked blocked, Top& top) {
+    return scan_last(P, q, blocked, top, GView{P});
 }
 
 struct LocalQuery {
@@ -320,32 +365,65 @@ __device__ __forceinline__ LocalQuery local_query(const SearchDev& P, int j, flo
     return q;
 }
 
-template <class Blocked, class Top>
-__device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked blocked, Top& top) {
+template <class Blocked, class Top, class View = GView>
+__device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked blocked, Top& top, const View& V) {
     int cnt = 0;
     const Desc32 d0(P.mpDesc + 32 * (size_t)q.mp);
-    for_features_in_area(P, q.w, [&](int idx) {
+    for_features_in_area(P, V, q.w, [&](int idx) {
         if (blocked(idx)) return;
         if (P.cur.uRight && P.cur.uRight[idx] > 0) {
             const float er = fabsf(q.projXR - P.cur.uRight[idx]);
             if (er > q.r * P.cur.scale[q.level]) return;
         }
-        top.insert(d0.dist(P.cur.desc + 32 * (size_t)idx), idx);
+        top.insert(V.dist(d0, idx), idx);
         cnt++;
     });
     return cnt;
 }
+template <class Blocked, class Top>
+__device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked blocked, Top& top) {
+    return scan_local(P, q, blocked, top, GView{P});
+}
 
-// Parallel phase: one thread per query.
-template <bool LAST>
+// Parallel phase: one thread per query.  STAGE: the workgroup first copies the current
+// frame's grid, keypoint positions / octaves and descriptors into LDS (every problem has
+// N <= kStageMaxN), so the window walks -- cell start -> keypoint index -> keypoint ->
+// descriptor, a chain of dependent loads per candidate -- read LDS instead of L2/HBM.
+constexpr int kStageMaxN = 1536;
+constexpr size_t kStageLds = sizeof(uint16_t) * (kGridCells + 2) + sizeof(uint16_t) * kStageMaxN +
+                             sizeof(float2) * kStageMaxN + kStageMaxN + 32 * (size_t)kStageMaxN + 64;
+template <bool LAST, bool STAGE>
 __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict__ probs, float th, int bMono,
                                                     unsigned long long* counters) {
     ORBGPU_LATENCY_WAVE();
     const SearchDev P = probs[blockIdx.y];
     int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (!LAST && P.visList) {   // SearchLocalPoints: thread t takes the t-th in-view query
-        const int nv = *P.visCount;
-        if (q >= nv) {
+    int nvis = P.nq;
+    if (!LAST && P.visList) nvis = *P.visCount;   // SearchLocalPoints: thread t takes the t-th in-view query
+    if (STAGE && !counters && (int)(blockIdx.x * blockDim.x) >= nvis) return;   // no query in this block
+    LView V{};
+    if constexpr (STAGE) {
+        extern __shared__ __align__(16) unsigned char s_stage[];
+        uint4* s_desc = reinterpret_cast<uint4*>(s_stage);                              // 32 N
+        float2* s_xy = reinterpret_cast<float2*>(s_stage + 32 * (size_t)kStageMaxN);   // 8 N
+        uint16_t* s_gs = reinterpret_cast<uint16_t*>(s_xy + kStageMaxN);               // cells + 1
+        uint16_t* s_gi = s_gs + kGridCells + 2;                                         // N
+        uint8_t* s_oct = reinterpret_cast<uint8_t*>(s_gi + kStageMaxN);                // N
+        const int N = P.cur.N, tid = threadIdx.x;
+        const uint4* gd = reinterpret_cast<const uint4*>(P.cur.desc);
+        for (int k = tid; k < 2 * N; k += 256) s_desc[k] = gd[k];
+        for (int k = tid; k < N; k += 256) {
+            const orb_kp_dev kp = P.cur.keysUn[k];
+            s_xy[k] = make_float2(kp.x, kp.y);
+            s_oct[k] = (uint8_t)kp.octave;
+            s_gi[k] = (uint16_t)P.gridIdx[k];
+        }
+        for (int c = tid; c <= kGridCells; c += 256) s_gs[c] = (uint16_t)P.gridStart[c];
+        __syncthreads();
+        V = LView{s_gs, s_gi, s_xy, s_oct, s_desc};
+    }
+    if (!LAST && P.visList) {
+        if (q >= nvis) {
             if (!counters) return;
             q = P.nq;   // measurement only
         } else {
@@ -361,10 +439,10 @@ __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict_
         bool bF, bB;
         fwd_bwd(P, bMono != 0, bF, bB);
         const LastQuery lq = last_query(P, q, th, bF, bB);
-        if (lq.valid) cnt = scan_last(P, lq, never, top);
+        if (lq.valid) cnt = STAGE ? scan_last(P, lq, never, top, V) : scan_last(P, lq, never, top);
     } else {
         const LocalQuery lq = local_query(P, q, th);
-        if (lq.valid) cnt = scan_local(P, lq, never, top);
+        if (lq.valid) cnt = STAGE ? scan_local(P, lq, never, top, V) : scan_local(P, lq, never, top);
     }
     if (q < P.nq) {
         P.qinfo[q] = make_int4(cnt, 0, 0, 0);
@@ -738,7 +816,7 @@ __global__ void __launch_bounds__(256) k_csr_hamming(const uint8_t* __restrict__
     unsigned long long k1 = ~0ull, k2 = ~0ull;
     for (int k = b + lane; k < e; k += 64) {
         const int d = hamming32(qd, t + 32 * (size_t)cand[k]);
-        dist[k] = d;
+        if (dist) dist[k] = d;   // best / second need no per-pair store
         const unsigned long long key = ((unsigned long long)d << 32) | (unsigned)(k - b);
         if (key < k1) { k2 = k1; k1 = key; }
         else if (key < k2) k2 = key;
@@ -762,6 +840,94 @@ __global__ void __launch_bounds__(256) k_csr_hamming(const uint8_t* __restrict__
         best_dist[qi] = k1 == ~0ull ? 256 : (int)(k1 >> 32);
         second_dist[qi] = k2 == ~0ull ? 256 : (int)(k2 >> 32);
     }
+}
+
+// ------------------------------------------------------- dense (brute-force) matching
+// Every query of a problem against every train descriptor of it, best / second distance with the
+// reference loops' rule (distance strictly below the best: earliest index wins ties; ORBmatcher.cc
+// e.g. 1411-1423, 1647-1663).  A workgroup takes 256 queries (one per thread, descriptor in
+// registers) x one block of kDenseBlock train descriptors staged in LDS: every wave reads the
+// same train descriptor (an LDS broadcast) per step, so a pair costs 8 XOR + 8 popcount-adds and
+// no memory traffic.  The blocks' (best, second) keys (distance << 32 | index) merge exactly:
+// the minimum key is the sequential loop's best, the second-smallest key's distance its second.
+constexpr int kDenseBlock = 256;
+constexpr int kDenseQ = 256;
+
+struct DenseJob {
+    int prob, q0, t0, part;   // problem, first query, first train row, partial slot
+};
+
+__global__ void __launch_bounds__(kDenseQ) k_dense_hamming(const DenseDev* __restrict__ probs,
+                                                           const DenseJob* __restrict__ jobs,
+                                                           unsigned long long* __restrict__ part,
+                                                           unsigned long long* counters) {
+    __shared__ uint4 tl[kDenseBlock * 2];
+    const DenseJob J = jobs[blockIdx.x];
+    const DenseDev P = probs[J.prob];
+    const int tid = threadIdx.x;
+    const int nt = min(kDenseBlock, P.nt - J.t0);
+    const uint4* src = reinterpret_cast<const uint4*>(P.t + 32 * (size_t)J.t0);
+    for (int k = tid; k < 2 * nt; k += kDenseQ) tl[k] = src[k];
+    const int qi = J.q0 + tid;
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    if (qi < P.nq) {
+        a0 = reinterpret_cast<const uint4*>(P.q + 32 * (size_t)qi)[0];
+        a1 = reinterpret_cast<const uint4*>(P.q + 32 * (size_t)qi)[1];
+    }
+    __syncthreads();
+    unsigned b1 = 0xffffffffu, b2 = 0xffffffffu, bi = 0;
+    for (int j = 0; j < nt; j++) {
+        const uint4 t0 = tl[2 * j], t1 = tl[2 * j + 1];   // wave-uniform address: broadcast
+        const unsigned d = __popc(a0.x ^ t0.x) + __popc(a0.y ^ t0.y) + __popc(a0.z ^ t0.z) + __popc(a0.w ^ t0.w) +
+                           __popc(a1.x ^ t1.x) + __popc(a1.y ^ t1.y) + __popc(a1.z ^ t1.z) + __popc(a1.w ^ t1.w);
+        if (d < b1) {
+            b2 = b1;
+            b1 = d;
+            bi = (unsigned)j;
+        } else if (d < b2) {
+            b2 = d;
+        }
+    }
+    if (qi < P.nq) {
+        unsigned long long* o = part + 2 * ((size_t)J.part * kDenseQ + tid);
+        o[0] = b1 == 0xffffffffu ? ~0ull : ((unsigned long long)b1 << 32) | (unsigned)(J.t0 + (int)bi);
+        // the block's second-smallest key: its distance is b2; any index past the best keeps
+        // the merge's ordering of equal distances irrelevant to second_dist
+        o[1] = b2 == 0xffffffffu ? ~0ull : ((unsigned long long)b2 << 32) | 0xffffffffu;
+    }
+    if (counters && tid == 0) {
+        const int sl = blockIdx.x & (kCountSlots - 1);
+        atomicAdd(&counters[6 * kCountSlots + sl], (unsigned long long)nt * (unsigned long long)min(kDenseQ, P.nq - J.q0));
+    }
+}
+
+// Merge the train blocks' partial keys of every query (one thread per query).
+__global__ void __launch_bounds__(256) k_dense_merge(const DenseDev* __restrict__ probs, const int* __restrict__ qjob,
+                                                     const DenseJob* __restrict__ jobs, int nblk_per_q,
+                                                     const unsigned long long* __restrict__ part, int nq_blocks,
+                                                     int njobs) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;   // (query block, thread)
+    const int qb = g / kDenseQ, tq = g % kDenseQ;
+    if (qb >= nq_blocks) return;
+    const DenseJob J0 = jobs[qjob[qb]];
+    const DenseDev P = probs[J0.prob];
+    const int qi = J0.q0 + tq;
+    if (qi >= P.nq) return;
+    unsigned long long k1 = ~0ull, k2 = ~0ull;
+    for (int b = 0; b < nblk_per_q && qjob[qb] + b < njobs; b++) {
+        const DenseJob J = jobs[qjob[qb] + b];
+        if (J.prob != J0.prob || J.q0 != J0.q0) break;
+        const unsigned long long* o = part + 2 * ((size_t)J.part * kDenseQ + tq);
+        const unsigned long long o1 = o[0], o2 = o[1];
+        const unsigned long long n1 = o1 < k1 ? o1 : k1, hi = o1 < k1 ? k1 : o1;
+        unsigned long long n2 = o2 < k2 ? o2 : k2;
+        n2 = hi < n2 ? hi : n2;
+        k1 = n1;
+        k2 = n2;
+    }
+    P.best_idx[qi] = k1 == ~0ull ? -1 : (int)(k1 & 0xffffffffu);
+    P.best_dist[qi] = k1 == ~0ull ? 256 : (int)(k1 >> 32);
+    P.second_dist[qi] = k2 == ~0ull ? 256 : (int)(k2 >> 32);
 }
 
 // ------------------------------------------------------- area-candidate engine
@@ -848,6 +1014,7 @@ Matcher::~Matcher() {
         if (ev_[i]) (void)hipEventDestroy(ev_[i]);
     if (d_count_) (void)hipFree(d_count_);
     if (d_cand_) (void)hipFree(d_cand_);
+    if (d_dense_) (void)hipFree(d_dense_);
     if (d_scratch_) (void)hipFree(d_scratch_);
     if (d_probs_) (void)hipFree(d_probs_);
     if (d_arena_) (void)hipFree(d_arena_);
@@ -946,15 +1113,23 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     mark(1);
     if (maxq > 0) {
         if (lastMode) {
-            hipLaunchKernelGGL(k_candidates<true>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, (int)bMono,
-                               counters());
+            if (maxN <= kStageMaxN)
+                hipLaunchKernelGGL((k_candidates<true, true>), dim3((maxq + 255) / 256, np), dim3(256), kStageLds, stream_, dp,
+                                   th, (int)bMono, counters());
+            else
+                hipLaunchKernelGGL((k_candidates<true, false>), dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th,
+                                   (int)bMono, counters());
             mark(2);
             // nq = the last frame's N <= kMaxFrameKeys = 512 * kSelQLast: every query in a slot
             hipLaunchKernelGGL((k_select_r<true, 512, kSelQLast>), dim3(np), dim3(512), select_lds_bytes(maxN), stream_, dp,
                                th, (int)bMono, nnratio, (int)checkOri_, maxN);
         } else {
-            hipLaunchKernelGGL(k_candidates<false>, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0,
-                               counters());
+            if (maxN <= kStageMaxN)
+                hipLaunchKernelGGL((k_candidates<false, true>), dim3((maxq + 255) / 256, np), dim3(256), kStageLds, stream_,
+                                   dp, th, 0, counters());
+            else
+                hipLaunchKernelGGL((k_candidates<false, false>), dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0,
+                                   counters());
             mark(2);
             // SearchLocalPoints-sized query sets (thousands of local map points, long occupancy
             // chains between duplicated points): 16 waves per round of the fixed point
@@ -1048,6 +1223,74 @@ int Matcher::candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, cons
                        best_dist, second_dist, counters());
     mark(13);
     ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int Matcher::dense(const std::vector<DenseDev>& probs) {
+    const int np = (int)probs.size();
+    if (np == 0) return 0;
+    std::vector<DenseJob> jobs;
+    std::vector<int> qjob;   // first job of each query block (its train blocks follow it)
+    int maxBlk = 0;
+    for (int p = 0; p < np; p++) {
+        // a problem without train rows still runs one (empty) block: its queries get (-1, 256, 256)
+        const int nb = std::max(1, (probs[p].nt + kDenseBlock - 1) / kDenseBlock);
+        maxBlk = std::max(maxBlk, nb);
+        for (int q0 = 0; q0 < probs[p].nq; q0 += kDenseQ) {
+            qjob.push_back((int)jobs.size());
+            for (int b = 0; b < nb; b++) jobs.push_back(DenseJob{p, q0, b * kDenseBlock, (int)jobs.size()});
+        }
+    }
+    const size_t bP = (sizeof(DenseDev) * np + 255) & ~(size_t)255, bJ = (sizeof(DenseJob) * jobs.size() + 255) & ~(size_t)255;
+    const size_t bQ = (sizeof(int) * qjob.size() + 255) & ~(size_t)255;
+    const size_t bPart = sizeof(unsigned long long) * 2 * kDenseQ * std::max<size_t>(jobs.size(), 1);
+    const size_t need = bP + bJ + bQ + bPart;
+    if (need > dense_cap_) {
+        if (d_dense_) (void)hipFree(d_dense_);
+        d_dense_ = nullptr;
+        dense_cap_ = 0;
+        ORB_HIP_CHECK(hipMalloc(&d_dense_, need * 2));
+        dense_cap_ = need * 2;
+    }
+    char* b = (char*)d_dense_;
+    DenseDev* dP = (DenseDev*)b;
+    DenseJob* dJ = (DenseJob*)(b + bP);
+    int* dQ = (int*)(b + bP + bJ);
+    unsigned long long* dPart = (unsigned long long*)(b + bP + bJ + bQ);
+    // one staging copy: problems | jobs | query-block index
+    std::vector<char> h(bP + bJ + bQ, 0);
+    std::memcpy(h.data(), probs.data(), sizeof(DenseDev) * np);
+    if (!jobs.empty()) std::memcpy(h.data() + bP, jobs.data(), sizeof(DenseJob) * jobs.size());
+    if (!qjob.empty()) std::memcpy(h.data() + bP + bJ, qjob.data(), sizeof(int) * qjob.size());
+    ORB_HIP_CHECK(hipMemcpyAsync(b, h2d_src(h.data(), h.size()), h.size(), hipMemcpyHostToDevice, stream_));
+    if (timing_) {
+        if (int e = zero_counters(6, 1)) return e;
+        mark(14);
+    }
+    if (!jobs.empty())
+        hipLaunchKernelGGL(k_dense_hamming, dim3((unsigned)jobs.size()), dim3(kDenseQ), 0, stream_, (const DenseDev*)dP,
+                           (const DenseJob*)dJ, dPart, counters());
+    if (!qjob.empty())
+        hipLaunchKernelGGL(k_dense_merge, dim3((unsigned)((qjob.size() * kDenseQ + 255) / 256)), dim3(256), 0, stream_,
+                           (const DenseDev*)dP, (const int*)dQ, (const DenseJob*)dJ, maxBlk, dPart, (int)qjob.size(),
+                           (int)jobs.size());
+    mark(15);
+    ORB_HIP_CHECK(hipGetLastError());
+    if (!chain_.on()) ORB_HIP_CHECK(hipStreamSynchronize(stream_));   // the pageable staging vector
+    return 0;
+}
+
+int Matcher::dense_timing(float* ms, long long* pairs) {
+    *ms = -1.0f;
+    *pairs = -1;
+    if (!d_count_) return 0;
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (evSet_[14] && evSet_[15]) (void)hipEventElapsedTime(ms, ev_[14], ev_[15]);
+    std::vector<unsigned long long> c(kCountSlots);
+    ORB_HIP_CHECK(hipMemcpy(c.data(), d_count_ + 6 * kCountSlots, sizeof(unsigned long long) * kCountSlots,
+                            hipMemcpyDeviceToHost));
+    *pairs = 0;
+    for (unsigned long long v : c) *pairs += (long long)v;
     return 0;
 }
 

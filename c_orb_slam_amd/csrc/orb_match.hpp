@@ -79,6 +79,17 @@ struct FrustumDev {
     int* nvisible;          // IncreaseVisible() count (nToMatch)
 };
 
+// One brute-force matching problem (ORBmatcher_SearchDense_batch): device descriptor arrays,
+// per-query outputs
+struct DenseDev {
+    const uint8_t* q;
+    const uint8_t* t;
+    int nq, nt;
+    int* best_idx;
+    int* best_dist;
+    int* second_dist;
+};
+
 // one GetFeaturesInArea query of the area-candidate engine; qd = query descriptor row (-1 = none)
 struct AreaQuery {
     float x, y, r;
@@ -108,6 +119,9 @@ public:
                 float logScaleFactor);
     int candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, const int* off, const int* cand, int* dist,
                    int* best_idx, int* best_dist, int* second_dist);
+    // brute force: every query of each problem against every train row (LDS-resident blocks)
+    int dense(const std::vector<DenseDev>& probs);
+    int dense_timing(float* ms, long long* pairs);
     hipStream_t stream() const { return stream_; }
     // deferred mode (ORBmatcher_set_deferred): batch device calls return without a stream sync
     DeferredChain& chain() { return chain_; }
@@ -171,6 +185,8 @@ private:
     size_t arena_cap_ = 0, arena_used_ = 0;
     void* d_cand_ = nullptr;
     size_t cand_cap_ = 0;
+    void* d_dense_ = nullptr;
+    size_t dense_cap_ = 0;
     bool timing_ = false;
     const FrustumDev* frustum_ = nullptr;   // pending k_frustum of search_local_points
     float frustumCos_ = 0.5f, frustumLsf_ = 0.f;

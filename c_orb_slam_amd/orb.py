@@ -265,6 +265,23 @@ class ORBmatcher:
         b = np.ascontiguousarray(b, np.uint8)
         return lib().ORBmatcher_DescriptorDistance(ptr(a), ptr(b))
 
+    def SearchDense(self, queries, trains):
+        """Brute-force matching (ORBmatcher_SearchDense_batch): problem p matches every descriptor
+        of queries[p] (n x 32 u8) against every row of trains[p]; host arrays.  -> list of
+        (best_idx, best_dist, second_dist) int32 arrays (ORBmatcher.cc loop rule: strict '<')."""
+        n = len(queries)
+        qs = [np.ascontiguousarray(q, np.uint8).reshape(-1, 32) for q in queries]
+        ts = [np.ascontiguousarray(t, np.uint8).reshape(-1, 32) for t in trains]
+        outs = [tuple(np.zeros(len(q), np.int32) for _ in range(3)) for q in qs]
+        arr = lambda xs: (C.c_void_p * max(n, 1))(*[x.ctypes.data if x.size else None for x in xs])
+        nq = np.array([len(q) for q in qs] or [0], np.int32)
+        nt = np.array([len(t) for t in ts] or [0], np.int32)
+        check(self._L.ORBmatcher_set_device_pointers(self._h, 0))
+        check(self._L.ORBmatcher_SearchDense_batch(self._h, n, arr(qs), ptr(nq), arr(ts), ptr(nt),
+                                                   arr([o[0] for o in outs]), arr([o[1] for o in outs]),
+                                                   arr([o[2] for o in outs])), "ORBmatcher_SearchDense_batch")
+        return outs
+
     def SearchByProjection_LastFrame(self, cur: Frame, cur_mp, last: Frame, last_keys, last_mp, last_outlier,
                                      mps: MapPoints, th, bMono):
         """SearchByProjection(CurrentFrame, LastFrame, th, bMono) (ORBmatcher.cc:1328).

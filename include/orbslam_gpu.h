@@ -509,8 +509,21 @@ int ORBmatcher_SearchBySim3(ORBmatcher_h h, const orb_frame* KF1, const int32_t*
 
 /* Hamming distances for CSR candidate lists (the inner loop of every Search*):
  * query q (descriptor qdesc[q]) against train rows cand[off[q] .. off[q+1]).
- * Writes dist[k] for every candidate k and best/second per query
- * (strict '<', earliest candidate wins ties, like the reference loops). */
+ * Writes dist[k] for every candidate k (dist may be NULL: best/second only) and best/second
+ * per query (strict '<', earliest candidate wins ties, like the reference loops). */
+/* Brute-force matching (SURVEY config 2 (ii): the dense descriptor tile; north star "Hamming
+ * brute-force ... over LDS-resident descriptor blocks"): for `count` problems, every query
+ * descriptor qdesc[p] (nq[p] x 32) against every train row tdesc[p] (nt[p] x 32); per query the
+ * best train index (-1 if none), its distance and the second-best distance (256 if none), by
+ * the reference loops' rule (ORBmatcher.cc: DescriptorDistance 1647-1663; best on a strictly
+ * smaller distance, so the earliest index wins ties; an equal distance becomes the second).
+ * Pointer space per ORBmatcher_set_device_pointers (device mode: enqueued, deferred-chain aware). */
+int ORBmatcher_SearchDense_batch(ORBmatcher_h h, int count, const uint8_t* const* qdesc, const int* nq,
+                                 const uint8_t* const* tdesc, const int* nt, int32_t* const* best_idx,
+                                 int32_t* const* best_dist, int32_t* const* second_dist);
+/* Measurement: the last SearchDense_batch's kernel time (ms, HIP events on ORBmatcher_stream,
+ * timing on) and its (query, train) pair count. */
+int ORBmatcher_last_dense_timing(ORBmatcher_h h, float* ms, long long* pairs);
 int ORBmatcher_SearchCandidates(ORBmatcher_h h, const uint8_t* qdesc, int nq,
                                 const uint8_t* tdesc, int nt, const int32_t* off,
                                 const int32_t* cand, int32_t* dist, int32_t* best_idx,

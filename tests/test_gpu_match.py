@@ -166,3 +166,44 @@ def test_search_by_projection_clustered_cell(gpu, kitti_frames, frac):
         ng = m.SearchByProjection_LastFrame(cur, g, last, k0, last_mp, last_out, mps, th, True)
         no = oracle_lib.oracle_search_last(cur, o, last, k0, last_mp, last_out, mps, th, True, 0.9, True)
         assert ng == no and np.array_equal(g, o), (th, ng, no)
+
+
+def _dense_ref(q, t):
+    """The reference loop over train rows in order (ORBmatcher.cc:1647-1663 distance; best on a
+    strictly smaller distance, an equal one becomes the second), vectorised with numpy."""
+    if len(t) == 0:
+        return np.full(len(q), -1), np.full(len(q), 256), np.full(len(q), 256)
+    d = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(2)
+    bi = d.argmin(1)                                  # first index of the minimum
+    bd = d.min(1)
+    sd = np.partition(d, 1, axis=1)[:, 1] if d.shape[1] > 1 else np.full(len(q), 256)
+    return bi, bd, sd
+
+
+def test_search_dense_matches_reference_loop(gpu):
+    """Brute-force matching with LDS-resident train blocks: every query's best index, best and
+    second distance equal the sequential loop's, across block edges (train counts around the
+    256-row block), duplicate descriptors (ties), an empty train set and a one-row train set."""
+    import oracle_lib
+    rng = np.random.default_rng(41)
+    shapes = [(1200, 1200), (257, 256), (300, 257), (513, 511), (64, 1), (40, 0), (1, 700)]
+    qs, ts = [], []
+    for nq, nt in shapes:
+        q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+        t = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+        if nt > 10:
+            t[nt // 2] = t[3]                        # duplicate rows: equal distances, earliest wins
+            q[: min(nq, 5)] = t[3]                   # exact matches (distance 0) at a duplicated row
+        qs.append(q)
+        ts.append(t)
+    m = gpu.ORBmatcher(0.9, True)
+    out = m.SearchDense(qs, ts)
+    for q, t, (bi, bd, sd) in zip(qs, ts, out):
+        rbi, rbd, rsd = _dense_ref(q, t)
+        assert np.array_equal(bi, rbi) and np.array_equal(bd, rbd) and np.array_equal(sd, rsd)
+    q, t = qs[1], ts[1]   # the distance itself is the oracle's DescriptorDistance
+    for k in range(0, len(q), 37):
+        L = oracle_lib.lib()
+        assert out[1][1][k] == min(L.ora_descriptor_distance(oracle_lib.ptr(np.ascontiguousarray(q[k])),
+                                                             oracle_lib.ptr(np.ascontiguousarray(t[j])))
+                                   for j in range(len(t)))

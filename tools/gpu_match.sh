@@ -17,7 +17,7 @@ python3 tools/pmc_match.py "$(find "$OUT/FETCH_SIZE" -name '*counter_collection.
   "$(find "$OUT/WRITE_SIZE" -name '*counter_collection.csv' | head -1)" \
   "$(find "$OUT/SQ_INSTS_VALU" -name '*counter_collection.csv' | head -1)" "$OUT/match_pmc.json" \
   "workload: bench.py --passes-only (B=64 KITTI stereo batch: 5 isolated ComputeStereoMatches + SearchByProjection(Cur,Last,7) + 16 dense 1200x1200 tiles)" > /dev/null || exit 1
-cp "$OUT/match_pmc.json" profiles/match_pmc_r02.json
+cp "$OUT/match_pmc.json" profiles/match_pmc_r03.json
 rm -rf "$OUT/FETCH_SIZE" "$OUT/WRITE_SIZE" "$OUT/SQ_INSTS_VALU"
 timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"

@@ -15,9 +15,9 @@ out = (C.c_ulonglong * 32)()
 lib().orbgpu_debug_prof(out)
 PoseOptimizationBatch(frames)
 lib().orbgpu_debug_prof(out)
-names = ["iter_top", "fused28", "solve_tail_sync", "trial_pass", "decide", "to_ldlt_done", "se3_exp", "se3_mul"]
+names = ["iter_top", "fused28", "solve_tail_sync", "cand_pass", "decide", "to_solve_done", "unused6", "unused7"]
 v = [out[i] for i in range(len(names))]
 tot = sum(v)
 print("cycles (frame 0, one call):", dict(zip(names, v)), "total", tot)
 print({n: round(x / tot, 3) for n, x in zip(names, v)})
-print("fused passes", out[8], "trials", out[9], "pre-solve (syncs, lambda)", out[10])
+print("28-sum passes", out[8], "rounds (solve + candidate pass)", out[9], "round start", out[10])

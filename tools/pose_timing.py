@@ -9,7 +9,8 @@ import numpy as np  # noqa: E402
 from c_orb_slam_amd import PoseOptimizationBatch  # noqa: E402
 from pose_cases import pose_problem  # noqa: E402
 
-for F in (1, 64, 256):
+Fs = [int(a) for a in sys.argv[1:]] or [1, 64, 256]
+for F in Fs:
     frames = [pose_problem(s, N=2000) for s in range(F)]
     PoseOptimizationBatch(frames)
     t = time.perf_counter()
