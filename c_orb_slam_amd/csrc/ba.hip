@@ -27,6 +27,7 @@
 #include <numeric>
 
 #include "ba_math.hpp"
+#include "ba_struct.hpp"
 #include "detmath.hpp"
 #include "ldlt.hpp"
 #include "orb_common.hpp"
@@ -124,6 +125,14 @@ __device__ __forceinline__ double wave_trees(const double* v, double* buf) {
 
 constexpr int DIAG21[6] = {0, 6, 11, 15, 18, 20};
 
+// Device-resident LM (BaEngine::optimize_device): every kernel of a step takes a gate word that
+// k_lm_trial_end set for it; a step the decision made unnecessary runs as empty launches.
+// nullptr: always run (the host-driven path).
+#define BA_GATE(run)                  \
+    do {                              \
+        if ((run) && !*(run)) return; \
+    } while (0)
+
 // term layout (SoA, stride nE): Hpp 0..20 | bp 21..26 | Hll 27..35 | bl 36..38
 constexpr int T_HPP = 0, T_BP = 21, T_HLL = 27, T_BL = 36, T_N = 39;
 
@@ -142,6 +151,7 @@ struct LinArgs {
     double* chunks;   // per-wave chunk trees of rc (ceil(nE/64))
     unsigned* counter;
     double* out;      // canonical sum of rc
+    const int* run;   // gate (device LM) or nullptr
 };
 
 // computeActiveErrors + activeRobustChi2 terms (+ linearizeOplus + constructQuadraticForm)
@@ -172,6 +182,7 @@ __device__ __forceinline__ void block_finish_csum(double* c, int m, int nterms, 
 }
 
 __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
+    BA_GATE(a.run);
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < a.s.nE;
     double r0 = 0.0, rho1 = 1.0;
@@ -341,10 +352,9 @@ constexpr int kChunks = 128;  // per-list LDS chunk sums: lists up to 8192 terms
 // per free pose: Hpp (upper 21) and b_p as canonical sums over its active edges (edge order).
 // Each lane loads the 27 terms of one edge; one wave tree per entry and chunk; chunk sums
 // reduced per entry by one thread.
-__global__ void __launch_bounds__(1024) k_pose_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
-                                                      double* bp) {
+__device__ __forceinline__ void pose_reduce_block(const BaStructDev& s, const double* __restrict__ terms, double* Hpp,
+                                                  double* bp, int i) {
     __shared__ double cs[27][kChunks];
-    const int i = blockIdx.x;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int s0 = s.peStart[i], n = s.peStart[i + 1] - s0;
     const int m = (n + 63) >> 6;
@@ -374,10 +384,17 @@ __global__ void __launch_bounds__(1024) k_pose_reduce(BaStructDev s, const doubl
     }
 }
 
+__global__ void __launch_bounds__(1024) k_pose_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
+                                                      double* bp, const int* run) {
+    BA_GATE(run);
+    pose_reduce_block(s, terms, Hpp, bp, blockIdx.x);
+}
+
 // per (landmark, entry): Hll (full 3x3) and b_l over the landmark's active edges (edge order)
 __global__ void __launch_bounds__(256) k_land_reduce(BaStructDev s, const double* __restrict__ terms, double* Hll,
-                                                     double* bl) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+                                                     double* bl, const int* run);
+__device__ __forceinline__ void land_reduce_thread(const BaStructDev& s, const double* __restrict__ terms, double* Hll,
+                                                   double* bl, int g) {
     if (g >= 12 * s.nL) return;
     const int l = g / 12, q = g % 12;
     const int s0 = s.leStart[l], n = s.leStart[l + 1] - s0;
@@ -399,9 +416,25 @@ __global__ void __launch_bounds__(256) k_land_reduce(BaStructDev s, const double
     else bl[3 * l + (q - 9)] = v;
 }
 
+__global__ void __launch_bounds__(256) k_land_reduce(BaStructDev s, const double* __restrict__ terms, double* Hll,
+                                                     double* bl, const int* run) {
+    BA_GATE(run);
+    land_reduce_thread(s, terms, Hll, bl, blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// both reductions of buildSystem in one launch: blocks [0, nP) reduce a pose each, the rest
+// a (landmark, entry) per thread
+__global__ void __launch_bounds__(1024) k_sys_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
+                                                     double* bp, double* Hll, double* bl, const int* run) {
+    BA_GATE(run);
+    if ((int)blockIdx.x < s.nP) pose_reduce_block(s, terms, Hpp, bp, blockIdx.x);
+    else land_reduce_thread(s, terms, Hll, bl, (blockIdx.x - s.nP) * blockDim.x + threadIdx.x);
+}
+
 // computeLambdaInit: tau * max |diag| over poses and landmarks (order-free max)
 __global__ void __launch_bounds__(1024) k_lambda_init(int nP, int nL, const double* Hpp, const double* Hll,
-                                                      double* scal) {
+                                                      double* scal, const int* run) {
+    BA_GATE(run);
     __shared__ double red[1024];
     double m = 0.;
     for (int j = threadIdx.x; j < 6 * nP + 3 * nL; j += blockDim.x) {
@@ -450,7 +483,8 @@ __device__ __forceinline__ void land_dinv(const double* Hll, int l, double lambd
 // per active edge with a free pose: BDinv = Hpl Dinv and B (Dinv b_l)  (block_solver.hpp:376-404)
 __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double* Hll, const double* bl,
                                                     const double* __restrict__ Hpl, double lam_host, int use_dev,
-                                                    const double* scal, double* Emat, double* cb) {
+                                                    const double* scal, double* Emat, double* cb, const int* run) {
+    BA_GATE(run);
     const int a = blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= s.nE || s.ePose[a] < 0) return;
     const int l = s.eLand[a];
@@ -473,7 +507,9 @@ __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double*
 __global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __restrict__ Emat,
                                                 const double* __restrict__ Hpl, const double* __restrict__ cb,
                                                 const double* Hpp, const double* bp, double lam_host, int use_dev,
-                                                const double* scal, SysAddr S, double* bs, int own) {
+                                                const double* scal, SysAddr S, double* bs, int own,
+                                                const int* run) {
+    BA_GATE(run);
     __shared__ double cs[36][kChunks];
     const int blk = blockIdx.x;
     const int i1 = s.blkI[blk], i2 = s.blkJ[blk];
@@ -549,7 +585,9 @@ __global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __r
 // Same per-element operation sequence as oracle ora_ldlt_solve, blocked by 6-column panels:
 // wave 0 factorises the panel rows and writes L (lower triangle), then every wave
 // applies the panel's rank-1 updates, in k order, to its trailing rows.
-__global__ void __launch_bounds__(256) k_ldlt(int n, double* Sg, const double* bs, double* x, double* scal, int in_lds) {
+__global__ void __launch_bounds__(256) k_ldlt(int n, double* Sg, const double* bs, double* x, double* scal, int in_lds,
+                                              const int* run) {
+    BA_GATE(run);
     extern __shared__ double lds[];
     double* y = lds;            // n
     double* A = in_lds ? lds + n : Sg;
@@ -637,7 +675,7 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
-// Register-resident LDL^T + solve for n <= 128 (<= 21 free keyframes), 1024 threads.
+// Register-resident LDL^T + solve for n < 128 (<= 21 free keyframes), 1024 threads.
 // Thread (wave w < 16, lane) owns rows i = 16 r + w (r < 8) of columns j = lane, lane + 64.
 // Per 6-column panel: owners publish the panel rows to LDS (U), wave 0 factorises them
 // in registers and writes L (Lall[k][i] = L[i][k], Lpan[i][k - p0]) and d_k, then every
@@ -660,7 +698,8 @@ constexpr int kDenseMaxN = 144;   // >= every n the dense single-workgroup solve
 constexpr int kLdltWaves = 16;
 constexpr int kLdltRows = kLdltMax / kLdltWaves;
 __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restrict__ Sg, const double* bs, double* x,
-                                                   double* scal) {
+                                                   double* scal, const int* run) {
+    BA_GATE(run);
     extern __shared__ double lds[];
     double* Lall = lds;                    // n x n, Lall[k * n + i] = L[i][k]
     double* U = Lall + (size_t)n * n;      // 6 x kLdltMax panel rows
@@ -669,16 +708,18 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
     double* y = dvec + kLdltMax;           // n
     __shared__ int ok;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    // [S | b] (n <= 126 < kLdltMax): column n carries the right-hand side, so the row updates run
+    // the forward substitution L y = b with the oracle's sequence (y_i -= l_ik y_k, k ascending)
+    // and y_k is final when row k becomes a pivot row
     double R[2][kLdltRows];
 #pragma unroll
     for (int c = 0; c < 2; c++)
 #pragma unroll
         for (int r = 0; r < kLdltRows; r++) {
             const int i = kLdltWaves * r + w, j = lane + 64 * c;
-            R[c][r] = (i < n && j < n && i <= j) ? Sg[(size_t)i * n + j] : 0.0;
+            R[c][r] = (i < n && j < n && i <= j) ? Sg[(size_t)i * n + j] : (i < n && j == n) ? bs[i] : 0.0;
         }
     LDLT_PROBE(0);
-    for (int q = tid; q < n; q += blockDim.x) y[q] = bs[q];
     if (tid == 0) ok = 1;
     __syncthreads();
     LDLT_PROBE(1);
@@ -703,35 +744,46 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
                 u1[t] = t < pw ? U[t * kLdltMax + lane + 64] : 0.0;
             }
             bool bad = false;
+            // the pivot of column t + 1 is formed on its own lane from that lane's own l (the value
+            // every lane receives by broadcast), so the dependent chain per column is one broadcast,
+            // one division and one multiply-subtract; a zero pivot only raises the flag
+            double d = readlane_d(p0 < 64 ? u0[0] : u1[0], p0 & 63);
 #pragma unroll
             for (int t = 0; t < 6; t++) {
-                if (t >= pw || bad) break;
-                const int k = p0 + t;
-                const double d = readlane_d(k < 64 ? u0[t] : u1[t], k & 63);
-                if (d == 0.0) {
-                    bad = true;
-                    break;
-                }
-                const bool a0 = lane > k && lane < n, a1 = lane + 64 > k && lane + 64 < n;
-                const double l0 = a0 ? u0[t] / d : 0.0;
-                const double l1 = a1 ? u1[t] / d : 0.0;
+                if (t < pw) {
+                    const int k = p0 + t;
+                    bad |= d == 0.0;
+                    const bool a0 = lane > k && lane < n, a1 = lane + 64 > k && lane + 64 < n;
+                    const double l0 = a0 ? u0[t] / d : 0.0;
+                    const double l1 = a1 ? u1[t] / d : 0.0;
+                    double dn = 0.0;
+                    if (t + 1 < pw) {
+                        const int k1 = k + 1;
+                        const double pv = k1 < 64 ? u0[t + 1] - l0 * u0[t] : u1[t + 1] - l1 * u1[t];
+                        dn = readlane_d(pv, k1 & 63);
+                    }
 #pragma unroll
-                for (int t2 = t + 1; t2 < 6; t2++) {
-                    if (t2 >= pw) break;
-                    const int i = p0 + t2;
-                    const double li = readlane_d(i < 64 ? l0 : l1, i & 63);
-                    if (lane >= i) u0[t2] -= li * u0[t];
-                    if (lane + 64 >= i) u1[t2] -= li * u1[t];
+                    for (int t2 = t + 1; t2 < 6; t2++) {
+                        if (t2 < pw) {
+                            const int i = p0 + t2;
+                            const double li = readlane_d(i < 64 ? l0 : l1, i & 63);
+                            if (lane >= i) u0[t2] -= li * u0[t];
+                            if (lane + 64 >= i) u1[t2] -= li * u1[t];
+                        }
+                    }
+                    if (a0) {
+                        Lall[(size_t)k * n + lane] = l0;
+                        Lpan[lane * 6 + t] = l0;
+                    }
+                    if (a1) {
+                        Lall[(size_t)k * n + lane + 64] = l1;
+                        Lpan[(lane + 64) * 6 + t] = l1;
+                    }
+                    if (lane == 0) dvec[k] = d;
+                    if (lane == n) y[k] = u0[t];
+                    if (lane + 64 == n) y[k] = u1[t];
+                    d = dn;
                 }
-                if (a0) {
-                    Lall[(size_t)k * n + lane] = l0;
-                    Lpan[lane * 6 + t] = l0;
-                }
-                if (a1) {
-                    Lall[(size_t)k * n + lane + 64] = l1;
-                    Lpan[(lane + 64) * 6 + t] = l1;
-                }
-                if (lane == 0) dvec[k] = d;
             }
             if (bad && lane == 0) ok = 0;
 #pragma unroll
@@ -750,6 +802,8 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
             u0[t] = t < pw ? U[t * kLdltMax + lane] : 0.0;
             u1[t] = t < pw ? U[t * kLdltMax + lane + 64] : 0.0;
         }
+        // rows i >= 64 own no column below 64 on or right of the diagonal; column registers
+        // 64.. exist only for n >= 64 (the right-hand side sits at column n)
 #pragma unroll
         for (int r = 0; r < kLdltRows; r++) {
             const int i = kLdltWaves * r + w;
@@ -757,15 +811,20 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
                 double L[6];
 #pragma unroll
                 for (int t = 0; t < 6; t++) L[t] = t < pw ? Lpan[i * 6 + t] : 0.0;
-                double v0 = R[0][r], v1 = R[1][r];
+                if (i < 64) {
+                    double v0 = R[0][r];
 #pragma unroll
-                for (int t = 0; t < 6; t++) {
-                    if (t >= pw) break;
-                    v0 -= L[t] * u0[t];
-                    v1 -= L[t] * u1[t];
+                    for (int t = 0; t < 6; t++)
+                        if (t < pw) v0 -= L[t] * u0[t];
+                    if (lane >= i) R[0][r] = v0;
                 }
-                if (lane >= i) R[0][r] = v0;
-                if (lane + 64 >= i) R[1][r] = v1;
+                if (n >= 64) {
+                    double v1 = R[1][r];
+#pragma unroll
+                    for (int t = 0; t < 6; t++)
+                        if (t < pw) v1 -= L[t] * u1[t];
+                    if (lane + 64 >= i) R[1][r] = v1;
+                }
             }
         }
         __syncthreads();
@@ -777,44 +836,6 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
         return;
     }
     if (w != 0) return;
-    // L y = b: per row, subtractions in k order.  Operands of 8 steps are loaded ahead of
-    // the dependent chain (loads do not depend on acc).
-    for (int r0 = 0; r0 < n; r0 += 64) {
-        const int i = r0 + lane;
-        const bool on = i < n;
-        const int ic = on ? i : 0;
-        double acc = on ? y[i] : 0.0;
-        int k = 0;
-        for (; k + 8 <= r0; k += 8) {
-            double L8[8], Y8[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                L8[u] = Lall[(size_t)(k + u) * n + ic];
-                Y8[u] = y[k + u];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) acc -= L8[u] * Y8[u];
-        }
-        for (; k < r0; k++) acc -= Lall[(size_t)k * n + ic] * y[k];
-        const int kend = min(r0 + 64, n);
-        k = r0;
-        for (; k + 8 <= kend; k += 8) {
-            double L8[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) L8[u] = Lall[(size_t)(k + u) * n + ic];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const double yk = readlane_d(acc, k + u - r0);
-                if (i > k + u) acc -= L8[u] * yk;
-            }
-        }
-        for (; k < kend; k++) {
-            const double yk = readlane_d(acc, k - r0);
-            if (i > k) acc -= Lall[(size_t)k * n + ic] * yk;
-        }
-        if (on) y[i] = acc;
-        __builtin_amdgcn_wave_barrier();
-    }
     LDLT_PROBE(3);
     for (int k = lane; k < n; k += 64) y[k] = y[k] / dvec[k];
     __builtin_amdgcn_wave_barrier();
@@ -863,7 +884,9 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
 // push + back-substitution (block_solver.hpp:457-484) + SparseOptimizer::update (oplus)
 __global__ void __launch_bounds__(256) k_update(BaStructDev s, Se3* T, Se3* Tbak, double* X, double* Xbak,
                                                 double* x, const double* __restrict__ Hpl, const double* Hll,
-                                                const double* bl, double lam_host, int use_dev, const double* scal) {
+                                                const double* bl, double lam_host, int use_dev, const double* scal,
+                                                const int* run) {
+    BA_GATE(run);
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     const int nP = s.nP;
     if (g < nP) {
@@ -905,7 +928,9 @@ __global__ void __launch_bounds__(256) k_update(BaStructDev s, Se3* T, Se3* Tbak
     }
 }
 
-__global__ void __launch_bounds__(256) k_pop(BaStructDev s, Se3* T, const Se3* Tbak, double* X, const double* Xbak) {
+__global__ void __launch_bounds__(256) k_pop(BaStructDev s, Se3* T, const Se3* Tbak, double* X, const double* Xbak,
+                                             const int* run) {
+    BA_GATE(run);
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g < s.nP) {
         const int kf = s.poseKf[g];
@@ -922,7 +947,8 @@ __global__ void __launch_bounds__(256) k_pop(BaStructDev s, Se3* T, const Se3* T
 // wave trees of 64 consecutive terms (coalesced), chunk sums reduced by one thread.
 __global__ void __launch_bounds__(1024) k_scale(int nP, int nL, const double* x, const double* bp, const double* bl,
                                                 double lam_host, int use_dev, const double* scal, double* out,
-                                                int poses) {
+                                                int poses, const int* run) {
+    BA_GATE(run);
     __shared__ double lv[2048];
     const int n = 6 * nP + 3 * nL;
     const double lambda = lam_of(lam_host, use_dev, scal);
@@ -949,7 +975,8 @@ __global__ void __launch_bounds__(1024) k_scale(int nP, int nL, const double* x,
 // computeScale terms for large problems (6 nP + 3 nL > 2048 * 64): written out, then k_csum
 __global__ void __launch_bounds__(256) k_scale_terms(int nP, int nL, const double* x, const double* bp,
                                                      const double* bl, double lam_host, int use_dev,
-                                                     const double* scal, double* v, int poses) {
+                                                     const double* scal, double* v, int poses, const int* run) {
+    BA_GATE(run);
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= 6 * nP + 3 * nL) return;
     const double lambda = lam_of(lam_host, use_dev, scal);
@@ -970,7 +997,8 @@ struct CsumList {
     double* tmp1;
     double* out;
 };
-__global__ void __launch_bounds__(1024) k_csum(CsumList L0, CsumList L1) {
+__global__ void __launch_bounds__(1024) k_csum(CsumList L0, CsumList L1, const int* run) {
+    BA_GATE(run);
     const CsumList L = blockIdx.x == 0 ? L0 : L1;
     if (L.n <= 1) {
         if (threadIdx.x == 0) *L.out = L.n == 1 ? L.v[0] : 0.0;
@@ -993,6 +1021,148 @@ __global__ void __launch_bounds__(1024) k_csum(CsumList L0, CsumList L1) {
         m = m2;
     }
     if (threadIdx.x == 0) *L.out = dst[0];
+}
+
+// ---------------------------------------------------------------- device-resident LM control
+// OptimizationAlgorithmLevenberg::solve's trial loop and SparseOptimizer::optimize's iteration
+// loop (optimization_algorithm_levenberg.cpp:59-164, sparse_optimizer.cpp:354-418) decided on the
+// device, so a run's kernels queue back to back with no host round trip per trial.  The host
+// queues whole steps (system kernels gated by ctl[1], trial kernels by ctl[0]) one step ahead of
+// the decisions it has seen; k_lm_trial_end sets the gates of the next step.
+// Host-pinned coherent words (LmHost): [0] stop flag mirror (host writes), [1] done, [2] steps
+// decided, [3] iterations (device writes).
+__global__ void __launch_bounds__(64) k_lm_begin(LmDev* L, int iterations) {
+    if (threadIdx.x != 0) return;
+    L->ctl[0] = 1;
+    L->ctl[1] = 1;
+    L->ctl[2] = 1;   // computeLambdaInit on the first iteration
+    L->it = 0;
+    L->iterations = iterations;
+    L->qmax = 0;
+    L->nBad = 0;
+    L->haveChi = 0;
+    L->done = 0;
+    L->nTrial = 0;
+    L->nSolve = 0;
+    L->ni = 2;
+    L->currentChi = 0;
+    L->iniChi = 0;
+}
+
+// one thread: the host code of BaEngine::lm_solve after its readback, verbatim in order;
+// returns whether the trial is undone (pop)
+__device__ int lm_decide(LmDev* L, double* scal, volatile int* host) {
+    if (!L->haveChi) {
+        L->currentChi = L->iniChi = scal[0];
+        L->haveChi = 1;
+    }
+    const bool ok2 = scal[3] != 0.0;
+    double tempChi = scal[1];
+    if (!ok2) tempChi = DBL_MAX;
+    double rho = L->currentChi - tempChi;
+    double scale = scal[2];
+    scale += 1e-3;
+    rho /= scale;
+    double lambda = scal[5];
+    int pop = 0;
+    if (rho > 0 && isfinite(tempChi)) {
+        const double a3 = 2 * rho - 1;
+        double alpha = 1. - (a3 * a3) * a3;
+        alpha = fmin(alpha, 2. / 3.);
+        const double scaleFactor = fmax(1. / 3., alpha);
+        lambda *= scaleFactor;
+        L->ni = 2;
+        L->currentChi = tempChi;
+    } else {
+        lambda *= L->ni;
+        L->ni *= 2;
+        pop = 1;
+    }
+    scal[5] = lambda;
+    L->qmax++;
+    if (L->nTrial < kLmTrials) {
+        L->trialChi[L->nTrial] = tempChi;
+        L->trialLam[L->nTrial] = lambda;
+    }
+    L->nTrial++;
+    const bool stop = host[0] != 0;
+    L->ctl[2] = 0;
+    if (rho < 0 && L->qmax < 10 && !stop) {   // another trial on the same system
+        L->ctl[1] = 0;
+    } else {                                  // lm_solve returns
+        if (L->nSolve < kLmSolves) {
+            L->solveIni[L->nSolve] = L->iniChi;
+            L->solveChi[L->nSolve] = L->currentChi;
+        }
+        L->nSolve++;
+        bool term = false;
+        if (L->qmax == 10 || rho == 0) {
+            term = true;
+        } else {
+            if ((L->iniChi - L->currentChi) * 1e3 < L->iniChi) L->nBad++;
+            else L->nBad = 0;
+            if (L->nBad >= 3) term = true;
+        }
+        L->it++;
+        if (term || L->it >= L->iterations || stop) {
+            L->done = 1;
+            L->ctl[0] = 0;
+            L->ctl[1] = 0;
+        } else {
+            L->ctl[1] = 1;
+            L->haveChi = 0;
+            L->qmax = 0;
+        }
+    }
+    host[3] = L->it;
+    host[2] = host[2] + 1;
+    host[1] = L->done;   // read by the host after this step's event: kernel completion publishes it
+    return pop;
+}
+
+// End of a trial: computeScale (k_scale's canonical sum, problems with 6 nP + 3 nL <= 2048 * 64;
+// larger ones ran k_scale_terms + k_csum into scal[2] and pass scale = 0), the LM decision, and
+// the pop of a rejected trial, in one workgroup.
+__global__ void __launch_bounds__(1024) k_lm_trial_end(LmDev* L, double* scal, volatile int* host, BaStructDev s,
+                                                       Se3* T, const Se3* Tbak, double* X, const double* Xbak,
+                                                       const double* x, const double* bp, const double* bl, int scale) {
+    __shared__ double lv[2048];
+    __shared__ int pop;
+    if (!L->ctl[0]) return;   // a step queued after the run ended
+    const int nP = s.nP, nL = s.nL;
+    if (scale) {
+        const int n = 6 * nP + 3 * nL;
+        const double lambda = scal[5];
+        auto term = [&](int j) {
+            const double b = j < 6 * nP ? bp[j] : bl[j - 6 * nP];
+            return x[j] * (lambda * x[j] + b);
+        };
+        if (n <= 1) {
+            if (threadIdx.x == 0) scal[2] = n == 1 ? term(0) : 0.0;
+        } else {
+            const int m = (n + 63) >> 6;
+            const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            for (int c = w; c < m; c += 16) {
+                const int j = c * 64 + lane;
+                const double t = wave_tree(j < n ? term(j) : 0.0);
+                if (lane == 0) lv[c] = t;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) scal[2] = local_csum_inplace(lv, m);
+        }
+    }
+    if (threadIdx.x == 0) pop = lm_decide(L, scal, host);
+    __syncthreads();
+    if (!pop) return;
+    for (int g = threadIdx.x; g < nP + nL; g += blockDim.x) {   // k_pop
+        if (g < nP) {
+            const int kf = s.poseKf[g];
+            T[kf] = Tbak[kf];
+        } else {
+            const int pt = s.landPt[g - nP];
+            for (int k = 0; k < 3; k++) X[3 * pt + k] = Xbak[3 * pt + k];
+        }
+    }
 }
 
 // outlier gating / final check over all edges (Optimizer.cc:674-706, 714-746):
@@ -2031,6 +2201,9 @@ BaEngine::~BaEngine() {
     if (arena_) (void)hipFree(arena_);
     if (dStruct_) (void)hipFree(dStruct_);
     if (hScal_) (void)hipHostFree(hScal_);
+    if (hLm_) (void)hipHostFree(hLm_);
+    for (auto ev : lmEv_)
+        if (ev) (void)hipEventDestroy(ev);
     if (hStage_) (void)hipHostFree(hStage_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -2069,6 +2242,8 @@ int BaEngine::init() {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     ORB_HIP_CHECK(hipHostMalloc((void**)&hScal_, 64 * sizeof(double)));
+    ORB_HIP_CHECK(hipHostMalloc((void**)&hLm_, 16 * sizeof(int), hipHostMallocCoherent));
+    for (auto& ev : lmEv_) ORB_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     int dev = 0;
     ORB_HIP_CHECK(hipGetDevice(&dev));
     hipDeviceProp_t prop;
@@ -2080,7 +2255,7 @@ int BaEngine::init() {
 bool BaEngine::dense_solver(int n) const {
     const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
     const size_t ldsBytes = sizeof(double) * ((size_t)n + (size_t)n * n);
-    return n <= kDenseMaxN && ((n <= kLdltMax && regShm <= ldsMax_) || ldsBytes <= ldsMax_);
+    return n <= kDenseMaxN && ((n < kLdltMax && regShm <= ldsMax_) || ldsBytes <= ldsMax_);
 }
 
 // Carve every device buffer of the problem out of one grow-only arena.
@@ -2123,6 +2298,7 @@ int BaEngine::carve(bool commit, size_t* total) {
     dHplA_ = (double*)take(sizeof(double) * 18 * ne);
     dScal_ = (double*)take(sizeof(double) * 16);
     dCounter_ = (unsigned*)take(sizeof(unsigned) * 16);
+    dLm_ = (LmDev*)take(sizeof(LmDev));
     dScratch_ = (double*)take(sizeof(double) * scratchN_);
     tmpA0_ = (double*)take(sizeof(double) * tmpN);
     tmpA1_ = (double*)take(sizeof(double) * tmpN);
@@ -2180,30 +2356,31 @@ int BaEngine::upload_problem(const ba_problem* P) {
     }
     level_.assign(ne_, 0);
     hipStream_t s = stream_;
-    if (nkf_ && h2d_sync(dT_, T.data(), sizeof(Se3) * nkf_)) return -2;
-    if (npt_ && h2d_sync(dX_, X.data(), sizeof(double) * X.size())) return -2;
+    // poses, points and edges through one pinned staging block, one wait
+    const size_t bT = sizeof(Se3) * nkf_, bX = sizeof(double) * X.size(), bE = sizeof(EdgeDev) * ne_;
+    if (int e = stage_reserve(bT + bX + bE + 64)) return e;
+    char* st = (char*)hStage_;
+    std::memcpy(st, T.data(), bT);
+    std::memcpy(st + bT, X.data(), bX);
+    std::memcpy(st + bT + bX, E.data(), bE);
+    if (bT) ORB_HIP_CHECK(hipMemcpyAsync(dT_, st, bT, hipMemcpyHostToDevice, s));
+    if (bX) ORB_HIP_CHECK(hipMemcpyAsync(dX_, st + bT, bX, hipMemcpyHostToDevice, s));
+    if (bE) ORB_HIP_CHECK(hipMemcpyAsync(dE_, st + bT + bX, bE, hipMemcpyHostToDevice, s));
     if (ne_) {
-        if (h2d_sync(dE_, E.data(), sizeof(EdgeDev) * ne_)) return -2;
         ORB_HIP_CHECK(hipMemsetAsync(dLevel_, 0, ne_, s));
         ORB_HIP_CHECK(hipMemsetAsync(dRobust_, (mode_.global && !mode_.robust) ? 0 : 1, ne_, s));
         ORB_HIP_CHECK(hipMemsetAsync(dErr_, 0, sizeof(double) * 3 * ne_, s));
     }
     ORB_HIP_CHECK(hipMemsetAsync(dCounter_, 0, sizeof(unsigned) * 16, s));
-    ORB_HIP_CHECK(hipStreamSynchronize(s));  // host vectors above are pageable temporaries
+    ORB_HIP_CHECK(hipStreamSynchronize(s));  // the staging block is reused by the next upload
     return 0;
 }
 
 // initializeOptimization(level) + buildIndexMapping + BlockSolver::buildStructure
 int BaEngine::build_structure(int level) {
-    std::vector<int32_t> aE;
-    aE.reserve(ne_);
-    std::vector<uint8_t> kfAct(nkf_, 0), ptAct(npt_, 0);
-    for (int i = 0; i < ne_; i++)
-        if (level_[i] == level) {
-            aE.push_back(i);
-            kfAct[eKf_[i]] = 1;
-            ptAct[ePt_[i]] = 1;
-        }
+    BaHostStruct& H = hs_;
+    std::vector<uint8_t> kfAct, ptAct;
+    ba_active_set(level, nkf_, npt_, ne_, eKf_.data(), ePt_.data(), level_.data(), &H.aE, &kfAct, &ptAct);
     if (comm_) {
         // shards agree on the pose set: a keyframe is active if any shard has an active edge
         // on it (its pose index must be the same everywhere); also the global edge/landmark counts
@@ -2211,7 +2388,7 @@ int BaEngine::build_structure(int level) {
         for (int p = 0; p < npt_; p++) nLloc += ptAct[p];
         std::vector<double> red(nkf_ + 2);
         for (int k = 0; k < nkf_; k++) red[k] = kfAct[k];
-        red[nkf_] = (double)aE.size();
+        red[nkf_] = (double)H.aE.size();
         red[nkf_ + 1] = (double)nLloc;
         if (h2d_sync(dScratch_, red.data(), sizeof(double) * red.size())) return -2;
         if (int e = comm_->allreduce(dScratch_, red.size(), RedOp::Sum, stream_)) return e;
@@ -2221,95 +2398,19 @@ int BaEngine::build_structure(int level) {
         nEglob_ = (int)red[nkf_];
         nLglob_ = (int)red[nkf_ + 1];
     }
-    std::vector<int32_t> poseKf, landPt;
-    for (int k = 0; k < nkf_; k++)
-        if (kfAct[k] && !kfFixed_[k]) poseKf.push_back(k);
-    std::sort(poseKf.begin(), poseKf.end(), [&](int a, int b) { return kfId_[a] < kfId_[b]; });
-    for (int p = 0; p < npt_; p++)
-        if (ptAct[p]) landPt.push_back(p);
-    std::sort(landPt.begin(), landPt.end(), [&](int a, int b) { return ptId_[a] < ptId_[b]; });
-    const int nE = (int)aE.size(), nP = (int)poseKf.size(), nL = (int)landPt.size();
+    if (ba_build_lists(nkf_, npt_, eKf_.data(), ePt_.data(), kfFixed_.data(), kfId_.data(), ptId_.data(), kfAct, ptAct,
+                       &H))
+        return -1;
+    const int nE = (int)H.aE.size(), nP = (int)H.poseKf.size(), nL = (int)H.landPt.size();
     if (!comm_) {
         nEglob_ = nE;
         nLglob_ = nL;
     }
-    std::vector<int32_t> poseIdx(nkf_, -1), landIdx(npt_, -1);
-    for (int i = 0; i < nP; i++) poseIdx[poseKf[i]] = i;
-    for (int i = 0; i < nL; i++) landIdx[landPt[i]] = i;
-    std::vector<int32_t> ePose(nE), eLand(nE);
-    std::vector<int32_t> peStart(nP + 1, 0), leStart(nL + 1, 0), lpStart(nL + 1, 0);
-    for (int a = 0; a < nE; a++) {
-        ePose[a] = poseIdx[eKf_[aE[a]]];
-        eLand[a] = landIdx[ePt_[aE[a]]];
-        if (ePose[a] >= 0) {
-            peStart[ePose[a] + 1]++;
-            lpStart[eLand[a] + 1]++;
-        }
-        leStart[eLand[a] + 1]++;
-    }
-    for (int i = 0; i < nP; i++) peStart[i + 1] += peStart[i];
-    for (int i = 0; i < nL; i++) {
-        leStart[i + 1] += leStart[i];
-        lpStart[i + 1] += lpStart[i];
-    }
-    std::vector<int32_t> peList(std::max(peStart[nP], 1)), leList(std::max(leStart[nL], 1)), lpList(std::max(lpStart[nL], 1));
-    {
-        std::vector<int32_t> fp(peStart.begin(), peStart.end() - 1), fl(leStart.begin(), leStart.end() - 1),
-            fq(lpStart.begin(), lpStart.end() - 1);
-        for (int a = 0; a < nE; a++) {
-            if (ePose[a] >= 0) {
-                peList[fp[ePose[a]]++] = a;
-                lpList[fq[eLand[a]]++] = a;
-            }
-            leList[fl[eLand[a]]++] = a;
-        }
-    }
-    // landmark blocks in pose order; enforce one edge per (pose, landmark)
-    for (int l = 0; l < nL; l++) {
-        std::sort(lpList.begin() + lpStart[l], lpList.begin() + lpStart[l + 1],
-                  [&](int a, int b) { return ePose[a] < ePose[b]; });
-        for (int j = lpStart[l] + 1; j < lpStart[l + 1]; j++)
-            if (ePose[lpList[j]] == ePose[lpList[j - 1]]) return -1;
-    }
-    // Schur pattern: blocks (i1 <= i2), diagonal always; terms in landmark order
-    std::vector<int64_t> cnt;
-    std::vector<int32_t> blkOf((size_t)nP * nP, -1), blkI, blkJ;
-    for (int i = 0; i < nP; i++) {
-        blkOf[(size_t)i * nP + i] = (int)blkI.size();
-        blkI.push_back(i);
-        blkJ.push_back(i);
-    }
-    std::vector<int32_t> bcount(nP, 0);
-    for (int l = 0; l < nL; l++)
-        for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
-            for (int v = u; v < lpStart[l + 1]; v++) {
-                const int i1 = ePose[lpList[u]], i2 = ePose[lpList[v]];
-                int32_t& b = blkOf[(size_t)i1 * nP + i2];
-                if (b < 0) {
-                    b = (int)blkI.size();
-                    blkI.push_back(i1);
-                    blkJ.push_back(i2);
-                }
-            }
+    const std::vector<int32_t>&aE = H.aE, &ePose = H.ePose, &eLand = H.eLand, &poseKf = H.poseKf, &landPt = H.landPt,
+          &peStart = H.peStart, &peList = H.peList, &leStart = H.leStart, &leList = H.leList, &lpStart = H.lpStart,
+          &lpList = H.lpList, &blkI = H.blkI, &blkJ = H.blkJ, &blkStart = H.blkStart, &pairA = H.pairA,
+          &pairB = H.pairB;
     const int nBlk = (int)blkI.size();
-    std::vector<int32_t> blkStart(nBlk + 1, 0);
-    for (int l = 0; l < nL; l++)
-        for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
-            for (int v = u; v < lpStart[l + 1]; v++)
-                blkStart[blkOf[(size_t)ePose[lpList[u]] * nP + ePose[lpList[v]]] + 1]++;
-    for (int b = 0; b < nBlk; b++) blkStart[b + 1] += blkStart[b];
-    const int nPair = blkStart[nBlk];
-    std::vector<int32_t> pairA(std::max(nPair, 1)), pairB(std::max(nPair, 1));
-    {
-        std::vector<int32_t> fb(blkStart.begin(), blkStart.end() - 1);
-        for (int l = 0; l < nL; l++)
-            for (int u = lpStart[l]; u < lpStart[l + 1]; u++)
-                for (int v = u; v < lpStart[l + 1]; v++) {
-                    const int b = blkOf[(size_t)ePose[lpList[u]] * nP + ePose[lpList[v]]];
-                    pairA[fb[b]] = lpList[u];
-                    pairB[fb[b]++] = lpList[v];
-                }
-    }
     for (int i = 0; i < nP; i++)
         if (peStart[i + 1] - peStart[i] > 64 * kChunks) return -3;
     for (int l = 0; l < nL; l++)
@@ -2336,7 +2437,11 @@ int BaEngine::build_structure(int level) {
         ORB_HIP_CHECK(hipMalloc(&dStruct_, tot * 4 * 2));
         dStructCap_ = tot * 4 * 2;
     }
-    if (h2d_sync(dStruct_, hStruct_.data(), tot * 4)) return -2;
+    if (int e = stage_reserve(tot * 4)) return e;   // copied below, waited for at the end
+    std::memcpy(hStage_, hStruct_.data(), tot * 4);
+    ORB_HIP_CHECK(hipMemcpyAsync(dStruct_, hStage_, tot * 4, hipMemcpyHostToDevice, stream_));
+    // the sharded and block-sparse set-ups below stage more uploads through the same block
+    if (comm_ || nP >= kTiledMinPoses) ORB_HIP_CHECK(hipStreamSynchronize(stream_));
     const int32_t* d = dStruct_;
     st_.nE = nE; st_.nP = nP; st_.nL = nL; st_.nBlk = nBlk;
     st_.aE = d + off[0]; st_.ePose = d + off[1]; st_.eLand = d + off[2]; st_.poseKf = d + off[3];
@@ -2411,7 +2516,7 @@ int BaEngine::build_structure(int level) {
     }
     ORB_HIP_CHECK(hipMemsetAsync(dX2_, 0, sizeof(double) * (6 * (size_t)nP + 3 * (size_t)nL + 1), stream_));
     if (!tiled_) ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * 36 * (size_t)nP * nP + 8, stream_));
-    // the pageable hStruct_ copy must finish before the host vector is reused
+    // the staged structure copy must finish before the staging block is reused
     ORB_HIP_CHECK(hipStreamSynchronize(stream_));
     return 0;
 }
@@ -2466,11 +2571,11 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const BaStructDev& S = st_;
     const int nE = S.nE, nP = S.nP, nL = S.nL;
     const bool own = !comm_ || comm_->rank() == 0;
-    LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1, tmpA0_, dCounter_, dScal_ + 0};
+    LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1, tmpA0_, dCounter_, dScal_ + 0, nullptr};
     if (comm_ && !nE) ORB_HIP_CHECK(hipMemsetAsync(dScal_, 0, 2 * sizeof(double), s));
     if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
-    if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(1024), 0, s, S, dTerms_, dHpp_, dBp_);
-    if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(12 * nL, 256)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_);
+    if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(1024), 0, s, S, dTerms_, dHpp_, dBp_, nullptr);
+    if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(12 * nL, 256)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_, nullptr);
     if (comm_) {
         const RedBuf rb[3] = {{dHpp_, 21 * (size_t)nP}, {dBp_, 6 * (size_t)nP}, {dScal_, 1}};
         ORB_HIP_CHECK(hipGetLastError());
@@ -2478,7 +2583,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     }
     int use_dev = 0;
     if (iteration == 0) {
-        hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, nP, nL, dHpp_, dHll_, dScal_);
+        hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, nP, nL, dHpp_, dHll_, dScal_, nullptr);
         if (comm_) {
             ORB_HIP_CHECK(hipGetLastError());
             if (int e = comm_->allreduce(dScal_ + 4, 2, RedOp::Max, s)) return e;
@@ -2497,7 +2602,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const int in_lds = ldsBytes <= ldsMax_ ? 1 : 0;
     const size_t shm = in_lds ? ldsBytes : sizeof(double) * (size_t)n;
     const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
-    const bool use_reg = n <= kLdltMax && regShm <= ldsMax_;
+    const bool use_reg = n < kLdltMax && regShm <= ldsMax_;   // b rides in column n
     // n <= 128: register-resident single-workgroup LDL^T; S fits LDS: single-workgroup in LDS;
     // larger: block-sparse tiled LDL^T in HBM (ldlt.hip, structure from build_structure)
     if (!tiled_ && n > 0 && !use_reg && !in_lds) return -1;
@@ -2505,7 +2610,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     do {
         // setLambda + BlockSolver::solve
         if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
-                                   lambda_, use_dev, dScal_, dEmat_, dCb_);
+                                   lambda_, use_dev, dScal_, dEmat_, dCb_, nullptr);
         // the in-place LDL^T overwrites S (fill-in, L), and a shard's S holds the previous
         // trial's all-reduced blocks outside its own pattern: clear S
         if (tiled_) {
@@ -2514,7 +2619,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
             ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * (size_t)n * n, s));
         }
         if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(1024), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
-                                       lambda_, use_dev, dScal_, sa, dBs_, own ? 1 : 0);
+                                       lambda_, use_dev, dScal_, sa, dBs_, own ? 1 : 0, nullptr);
         if (comm_ && tiled_) {   // all-reduce the Schur-pattern tiles of S and b_s
             ORB_HIP_CHECK(hipGetLastError());
             const RedBuf rb[2] = {{sp_.tiles(), (size_t)sp_.nA() * 4096}, {dBs_, (size_t)n}};
@@ -2531,26 +2636,26 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         if (tiled_) {
             if (int e = sp_.solve(dBs_, dX2_, dScal_, s)) return e;
         } else if (use_reg) {
-            hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_);
+            hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else {
-            hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds);
+            hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, nullptr);
         }
         // push + update
         if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_,
-                                        dXbak_, dX2_, dHplA_, dHll_, dBl_, lambda_, use_dev, dScal_);
+                                        dXbak_, dX2_, dHplA_, dHll_, dBl_, lambda_, use_dev, dScal_, nullptr);
         // computeActiveErrors + activeRobustChi2 ; computeScale
         la.linearize = 0;
         la.out = dScal_ + 1;
         if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
         if (6 * nP + 3 * nL <= 2048 * 64) {
             hipLaunchKernelGGL(k_scale, dim3(1), dim3(1024), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_, use_dev, dScal_,
-                               dScal_ + 2, own ? 1 : 0);
+                               dScal_ + 2, own ? 1 : 0, nullptr);
         } else {
             const int nv = 6 * nP + 3 * nL;
             hipLaunchKernelGGL(k_scale_terms, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_,
-                               use_dev, dScal_, dScratch_, own ? 1 : 0);
+                               use_dev, dScal_, dScratch_, own ? 1 : 0, nullptr);
             CsumList L0{dScratch_, nv, tmpA0_, tmpA1_, dScal_ + 2};
-            hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, L0, L0);
+            hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, L0, L0, nullptr);
         }
         ORB_HIP_CHECK(hipGetLastError());
         if (comm_) {
@@ -2589,7 +2694,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
             lambda_ *= ni_;
             ni_ *= 2;
             if (nP + nL) hipLaunchKernelGGL(k_pop, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_,
-                                            dXbak_);
+                                            dXbak_, nullptr);
         }
         qmax++;
         trace_.trial_chi2.push_back(tempChi);
@@ -2610,6 +2715,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
 
 // SparseOptimizer::optimize (sparse_optimizer.cpp:354-418)
 int BaEngine::optimize(int iterations, const volatile bool* stop, int* its) {
+    if (device_lm(iterations)) return optimize_device(iterations, stop, its);
     *its = 0;
     bool ok = true;
     for (int i = 0; i < iterations && !stopped(stop) && ok; i++) {
@@ -2617,6 +2723,99 @@ int BaEngine::optimize(int iterations, const volatile bool* stop, int* its) {
         if (int e = lm_solve(i, stop, &term)) return e;
         ok = !term;
         (*its)++;
+    }
+    return 0;
+}
+
+// The device-resident LM (k_lm_trial_end) runs unsharded problems on the single-workgroup dense
+// solvers: one queue of kernels per optimize() call, no host round trip per trial.  ORBGPU_LM_HOST=1
+// keeps the host-driven loop (lm_solve) for A/B runs.
+static bool lm_host_forced() {
+    static const bool v = [] {
+        const char* e = std::getenv("ORBGPU_LM_HOST");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+bool BaEngine::device_lm(int iterations) const {
+    return !comm_ && !tiled_ && iterations > 0 && (size_t)iterations * 10 <= (size_t)kLmTrials &&
+           !lm_host_forced() && dense_solver(6 * st_.nP);
+}
+
+// the kernels of one LM step: [system: linearize, reduce, lambda init] [trial ... decide, pop]
+void BaEngine::enqueue_lm_step(bool first) {
+    hipStream_t s = stream_;
+    const BaStructDev& S = st_;
+    const int nE = S.nE, nP = S.nP, nL = S.nL;
+    const int* ctl = dLm_->ctl;
+    LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1, tmpA0_, dCounter_, dScal_ + 0, ctl + 1};
+    if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+    if (nP + nL) hipLaunchKernelGGL(k_sys_reduce, dim3(nP + nblk(12 * nL, 1024)), dim3(1024), 0, s, S, dTerms_, dHpp_,
+                                    dBp_, dHll_, dBl_, ctl + 1);
+    if (first) hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, nP, nL, dHpp_, dHll_, dScal_, ctl + 2);
+    const int n = 6 * nP;
+    const size_t ldsBytes = sizeof(double) * ((size_t)n + (size_t)n * n);
+    const int in_lds = ldsBytes <= ldsMax_ ? 1 : 0;
+    const size_t shm = in_lds ? ldsBytes : sizeof(double) * (size_t)n;
+    const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
+    const bool use_reg = n < kLdltMax && regShm <= ldsMax_;   // b rides in column n
+    const SysAddr sa{dS_, n, nullptr, nullptr, 0, nullptr};
+    if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_, 0.0, 1,
+                               dScal_, dEmat_, dCb_, ctl);
+    if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(1024), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_, 0.0,
+                                   1, dScal_, sa, dBs_, 1, ctl);
+    if (use_reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, ctl);
+    if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_, dXbak_,
+                                    dX2_, dHplA_, dHll_, dBl_, 0.0, 1, dScal_, ctl);
+    la.linearize = 0;
+    la.out = dScal_ + 1;
+    la.run = ctl;
+    if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+    const bool small = 6 * nP + 3 * nL <= 2048 * 64;
+    if (!small) {
+        const int nv = 6 * nP + 3 * nL;
+        hipLaunchKernelGGL(k_scale_terms, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dX2_, dBp_, dBl_, 0.0, 1,
+                           dScal_, dScratch_, 1, ctl);
+        CsumList L0{dScratch_, nv, tmpA0_, tmpA1_, dScal_ + 2};
+        hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, L0, L0, ctl);
+    }
+    hipLaunchKernelGGL(k_lm_trial_end, dim3(1), dim3(1024), 0, s, dLm_, dScal_, (volatile int*)hLm_, S, dT_, dTbak_,
+                       dX_, dXbak_, dX2_, dBp_, dBl_, small ? 1 : 0);
+}
+
+int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* its) {
+    *its = 0;
+    if (stopped(stop)) return 0;
+    hLm_[0] = stopped(stop) ? 1 : 0;
+    hLm_[1] = 0;
+    hLm_[2] = 0;
+    hLm_[3] = 0;
+    hipLaunchKernelGGL(k_lm_begin, dim3(1), dim3(64), 0, stream_, dLm_, iterations);
+    // at most 10 trials per iteration; the host stays one step ahead of the decisions
+    const int maxSteps = 10 * iterations;
+    for (int j = 0; j < maxSteps; j++) {
+        enqueue_lm_step(j == 0);
+        ORB_HIP_CHECK(hipGetLastError());
+        ORB_HIP_CHECK(hipEventRecord(lmEv_[j & 1], stream_));
+        if (j >= 1) {
+            ORB_HIP_CHECK(hipEventSynchronize(lmEv_[(j - 1) & 1]));
+            if (((volatile int*)hLm_)[1]) break;
+        }
+        hLm_[0] = stopped(stop) ? 1 : 0;
+    }
+    LmDev h;
+    if (int e = d2h_sync(&h, dLm_, sizeof(LmDev))) return e;   // also drains the queue
+    if (!h.done) return -7;    // the step bound is the trial bound: unreachable
+    *its = h.it;
+    for (int t = 0; t < std::min(h.nTrial, kLmTrials); t++) {
+        trace_.trial_chi2.push_back(h.trialChi[t]);
+        trace_.trial_lambda.push_back(h.trialLam[t]);
+    }
+    for (int t = 0; t < std::min(h.nSolve, kLmSolves); t++) {
+        trace_.solve_ini_chi2.push_back(h.solveIni[t]);
+        trace_.solve_chi2.push_back(h.solveChi[t]);
     }
     return 0;
 }
@@ -2697,8 +2896,16 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
     }
     std::vector<Se3> T(nkf_);
     std::vector<double> X(3 * (size_t)npt_);
-    if (nkf_ && d2h_sync(T.data(), dT_, sizeof(Se3) * nkf_)) return -2;
-    if (npt_ && d2h_sync(X.data(), dX_, sizeof(double) * X.size())) return -2;
+    {   // poses and points back through the staging block, one wait
+        const size_t bT = sizeof(Se3) * nkf_, bX = sizeof(double) * X.size();
+        if (int e = stage_reserve(bT + bX + 64)) return e;
+        char* st = (char*)hStage_;
+        if (bT) ORB_HIP_CHECK(hipMemcpyAsync(st, dT_, bT, hipMemcpyDeviceToHost, stream_));
+        if (bX) ORB_HIP_CHECK(hipMemcpyAsync(st + bT, dX_, bX, hipMemcpyDeviceToHost, stream_));
+        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        std::memcpy(T.data(), st, bT);
+        std::memcpy(X.data(), st + bT, bX);
+    }
     for (int k = 0; k < nkf_; k++)
         if (kfLocal_[k]) host_se3_to_Tcw(T[k], R->kf_Tcw + 16 * k);
     // BundleAdjustment writes back only the points that got a vertex (vbNotIncludedMP, Optimizer.cc:217-219);
@@ -2725,6 +2932,7 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
         if (int e = ldlt_sparse_dense(n, U.data(), b, x, &ok, nullptr, variant == 3)) return e < 0 ? e : -1;
         return ok;
     }
+    if (variant == 0 && n >= kLdltMax) return -3;   // [S | b] needs a column register for b
     double *dS = nullptr, *dB = nullptr, *dX = nullptr, *dScal = nullptr;
     const size_t nn = (size_t)std::max(n, 1);
     ORB_HIP_CHECK(hipMalloc(&dS, sizeof(double) * nn * nn));
@@ -2736,10 +2944,9 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     ORB_HIP_CHECK(hipMemset(dX, 0, sizeof(double) * nn));
     if (variant == 0) {
         const size_t shm = sizeof(double) * ((size_t)n * n + 14 * kLdltMax);
-        if (n > kLdltMax) return -3;
-        hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal);
+        hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal, nullptr);
     } else {
-        hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), sizeof(double) * n + 16, 0, n, dS, dB, dX, dScal, 0);
+        hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), sizeof(double) * n + 16, 0, n, dS, dB, dX, dScal, 0, nullptr);
     }
     ORB_HIP_CHECK(hipGetLastError());
     double sc[16];
@@ -2803,7 +3010,7 @@ int debug_csum(const double* v, int n, double* out) {
     ORB_HIP_CHECK(hipMemcpy(dV, v, sizeof(double) * n, hipMemcpyHostToDevice));
     double* o = dT + 2 * (nn / 64 + 64);
     CsumList L{dV, n, dT, dT + nn / 64 + 64, o};
-    hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, 0, L, L);
+    hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, 0, L, L, nullptr);
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipMemcpy(out, o, sizeof(double), hipMemcpyDeviceToHost));
     (void)hipFree(dV); (void)hipFree(dT);

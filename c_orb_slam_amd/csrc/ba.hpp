@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../../include/orbslam_gpu.h"
+#include "ba_struct.hpp"
 #include "comm.hpp"
 #include "ldlt.hpp"
 #include "orb_common.hpp"
@@ -62,6 +63,17 @@ struct BaMode {
     bool robust = true;    // global: bRobust
 };
 
+// device-resident LM state (ba.hip k_lm_begin / k_lm_decide): gates of the next step's kernels
+// (ctl: 0 trial, 1 system, 2 lambda init), the Levenberg state and the per-trial trace
+constexpr int kLmTrials = 128;   // 10 trials x <= 12 iterations per optimize() call
+constexpr int kLmSolves = 16;
+struct LmDev {
+    int ctl[4];
+    int it, iterations, qmax, nBad, haveChi, done, nTrial, nSolve;
+    double ni, currentChi, iniChi;
+    double trialChi[kLmTrials], trialLam[kLmTrials], solveIni[kLmSolves], solveChi[kLmSolves];
+};
+
 class BaEngine {
 public:
     ~BaEngine();
@@ -80,6 +92,9 @@ private:
     int gather_blocks(const std::vector<int64_t>& mine, std::vector<int64_t>* all);
     int optimize(int iterations, const volatile bool* stop, int* its);
     int lm_solve(int iteration, const volatile bool* stop, bool* terminate);
+    bool device_lm(int iterations) const;
+    int optimize_device(int iterations, const volatile bool* stop, int* its);
+    void enqueue_lm_step(bool first);
     int gate_edges(int final_check, uint8_t* erase);
     int carve(bool commit, size_t* total);
     bool stopped(const volatile bool* stop) const { return comm_ ? stopRed_ : (stop && *stop); }
@@ -102,6 +117,7 @@ private:
     // structure
     BaStructDev st_{};
     std::vector<int32_t> hStruct_;
+    BaHostStruct hs_;              // host lists of the current structure (reused across calls)
     int32_t* dStruct_ = nullptr;
     size_t dStructCap_ = 0;
     // system / workspace
@@ -115,6 +131,9 @@ private:
     void* arena_ = nullptr;
     size_t arenaCap_ = 0;
     double* hScal_ = nullptr;      // pinned
+    LmDev* dLm_ = nullptr;         // device LM state (arena)
+    int* hLm_ = nullptr;           // pinned coherent: stop mirror, done, steps, iterations
+    hipEvent_t lmEv_[2] = {nullptr, nullptr};
     // pinned staging of the setup uploads (problem arrays, structure): several engines set up
     // concurrently from different host threads, so no pageable hipMemcpy staging path is used
     void* hStage_ = nullptr;

@@ -1,0 +1,174 @@
+// ba_struct.cpp -- host index maps and lists of one BA optimisation level (ba_struct.hpp).
+// Every list comes out in the order the reference's structures imply:
+//   vertices ascending by mnId (g2o's _ivMap is sorted by vertex id, sparse_optimizer.cpp:
+//   buildIndexMapping; poses below landmarks by the Optimizer's id scheme, Optimizer.cc:
+//   561-627), per-vertex edge lists in edge insertion order, and each landmark's pose terms
+//   in pose order (BlockSolver::buildStructure walks the landmark's edges per pose,
+//   block_solver.hpp:139-168).  Counting sorts throughout: O(edges + vertices) per call.
+#include "ba_struct.hpp"
+
+#include <algorithm>
+#include <numeric>
+
+namespace orbgpu {
+
+void ba_active_set(int level, int nkf, int npt, int ne, const int32_t* eKf, const int32_t* ePt, const uint8_t* edgeLevel,
+                   std::vector<int32_t>* aE, std::vector<uint8_t>* kfAct, std::vector<uint8_t>* ptAct) {
+    aE->clear();
+    aE->reserve(ne);
+    kfAct->assign(nkf, 0);
+    ptAct->assign(npt, 0);
+    for (int i = 0; i < ne; i++)
+        if (edgeLevel[i] == level) {
+            aE->push_back(i);
+            (*kfAct)[eKf[i]] = 1;
+            (*ptAct)[ePt[i]] = 1;
+        }
+}
+
+// indices i with flag[i] set, ascending by id[i] (ids are distinct)
+static void by_id(int n, const uint8_t* flag, const int32_t* id, std::vector<int32_t>* out) {
+    out->clear();
+    for (int i = 0; i < n; i++)
+        if (flag[i]) out->push_back(i);
+    auto less = [&](int a, int b) { return id[a] < id[b]; };
+    if (!std::is_sorted(out->begin(), out->end(), less)) std::sort(out->begin(), out->end(), less);
+}
+
+int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, const uint8_t* kfFixed,
+                   const int32_t* kfId, const int32_t* ptId, const std::vector<uint8_t>& kfAct,
+                   const std::vector<uint8_t>& ptAct, BaHostStruct* S) {
+    std::vector<uint8_t> freeKf(nkf);
+    for (int k = 0; k < nkf; k++) freeKf[k] = kfAct[k] && !kfFixed[k];
+    by_id(nkf, freeKf.data(), kfId, &S->poseKf);
+    by_id(npt, ptAct.data(), ptId, &S->landPt);
+    const std::vector<int32_t>& aE = S->aE;
+    const int nE = (int)aE.size(), nP = (int)S->poseKf.size(), nL = (int)S->landPt.size();
+    std::vector<int32_t> poseIdx(nkf, -1), landIdx(npt, -1);
+    for (int i = 0; i < nP; i++) poseIdx[S->poseKf[i]] = i;
+    for (int i = 0; i < nL; i++) landIdx[S->landPt[i]] = i;
+    // raw pointers below: stores through S's vectors would otherwise alias every load
+    S->ePose.resize(nE);
+    S->eLand.resize(nE);
+    S->peStart.assign(nP + 1, 0);
+    S->leStart.assign(nL + 1, 0);
+    S->lpStart.assign(nL + 1, 0);
+    {
+        int32_t* __restrict__ eP = S->ePose.data();
+        int32_t* __restrict__ eL = S->eLand.data();
+        int32_t* __restrict__ ps = S->peStart.data();
+        int32_t* __restrict__ ls = S->leStart.data();
+        int32_t* __restrict__ qs = S->lpStart.data();
+        const int32_t* __restrict__ pi = poseIdx.data();
+        const int32_t* __restrict__ li = landIdx.data();
+        const int32_t* __restrict__ ae = aE.data();
+        for (int a = 0; a < nE; a++) {
+            const int e = ae[a], p = pi[eKf[e]], l = li[ePt[e]];
+            eP[a] = p;
+            eL[a] = l;
+            const int32_t f = p >= 0;   // branch-free: fixed-pose edges count 0 (into ps[0] += 0)
+            ls[l + 1]++;
+            ps[p + 1] += f;
+            qs[l + 1] += f;
+        }
+        for (int i = 0; i < nP; i++) ps[i + 1] += ps[i];
+        for (int i = 0; i < nL; i++) {
+            ls[i + 1] += ls[i];
+            qs[i + 1] += qs[i];
+        }
+    }
+    const int nPe = S->peStart[nP], nLe = S->leStart[nL], nLp = S->lpStart[nL];
+    S->peList.resize(std::max(nPe, 1));
+    S->leList.resize(std::max(nLe, 1));
+    S->lpList.resize(std::max(nLp, 1));
+    std::vector<int32_t> lpPose(std::max(nLp, 1));
+    {
+        const int32_t* __restrict__ eP = S->ePose.data();
+        const int32_t* __restrict__ eL = S->eLand.data();
+        const int32_t* __restrict__ ps = S->peStart.data();
+        int32_t* __restrict__ pl = S->peList.data();
+        int32_t* __restrict__ ll = S->leList.data();
+        int32_t* __restrict__ ql = S->lpList.data();
+        int32_t* __restrict__ qp = lpPose.data();
+        std::vector<int32_t> fp(S->peStart.begin(), S->peStart.end() - 1), fl(S->leStart.begin(), S->leStart.end() - 1),
+            fq(S->lpStart.begin(), S->lpStart.end() - 1);
+        int32_t* __restrict__ fpp = fp.data();
+        int32_t* __restrict__ flp = fl.data();
+        int32_t* __restrict__ fqp = fq.data();
+        for (int a = 0; a < nE; a++) {
+            if (eP[a] >= 0) pl[fpp[eP[a]]++] = a;
+            ll[flp[eL[a]]++] = a;
+        }
+        // landmark buckets filled pose by pose: each comes out in ascending pose order
+        for (int p = 0; p < nP; p++)
+            for (int j = ps[p]; j < ps[p + 1]; j++) {
+                const int a = pl[j], q = fqp[eL[a]]++;
+                ql[q] = a;
+                qp[q] = p;
+            }
+    }
+    const int32_t* __restrict__ qs = S->lpStart.data();
+    const int32_t* __restrict__ ql = S->lpList.data();
+    const int32_t* __restrict__ qp = lpPose.data();
+    for (int l = 0; l < nL; l++)   // one edge per (pose, landmark)
+        for (int j = qs[l] + 1; j < qs[l + 1]; j++)
+            if (qp[j] == qp[j - 1]) return -1;
+    // Schur pattern: diagonal blocks first, then blocks in order of first use (landmark order,
+    // pose pairs u <= v); one pass numbers and counts, one pass fills
+    std::vector<int32_t> blkOf((size_t)nP * nP, -1), bi, bj, cnt;
+    for (int i = 0; i < nP; i++) {
+        blkOf[(size_t)i * nP + i] = i;
+        bi.push_back(i);
+        bj.push_back(i);
+        cnt.push_back(0);
+    }
+    {
+        int32_t* __restrict__ bo = blkOf.data();
+        for (int l = 0; l < nL; l++) {
+            const int b0 = qs[l], b1 = qs[l + 1];
+            for (int u = b0; u < b1; u++) {
+                int32_t* __restrict__ row = bo + (size_t)qp[u] * nP;
+                for (int v = u; v < b1; v++) {
+                    int b = row[qp[v]];
+                    if (b < 0) {
+                        b = row[qp[v]] = (int)bi.size();
+                        bi.push_back(qp[u]);
+                        bj.push_back(qp[v]);
+                        cnt.push_back(0);
+                    }
+                    cnt[b]++;
+                }
+            }
+        }
+    }
+    const int nBlk = (int)bi.size();
+    S->blkI.swap(bi);
+    S->blkJ.swap(bj);
+    S->blkStart.assign(nBlk + 1, 0);
+    for (int b = 0; b < nBlk; b++) S->blkStart[b + 1] = S->blkStart[b] + cnt[b];
+    const int nPair = S->blkStart[nBlk];
+    S->pairA.resize(std::max(nPair, 1));
+    S->pairB.resize(std::max(nPair, 1));
+    {
+        std::vector<int32_t> fb(S->blkStart.begin(), S->blkStart.end() - 1);
+        int32_t* __restrict__ fbp = fb.data();
+        int32_t* __restrict__ pa = S->pairA.data();
+        int32_t* __restrict__ pb = S->pairB.data();
+        const int32_t* __restrict__ bo = blkOf.data();
+        for (int l = 0; l < nL; l++) {
+            const int b0 = qs[l], b1 = qs[l + 1];
+            for (int u = b0; u < b1; u++) {
+                const int32_t* __restrict__ row = bo + (size_t)qp[u] * nP;
+                const int au = ql[u];
+                for (int v = u; v < b1; v++) {
+                    const int q = fbp[row[qp[v]]]++;
+                    pa[q] = au;
+                    pb[q] = ql[v];
+                }
+            }
+        }
+    }
+    return 0;
+}
+
+}  // namespace orbgpu

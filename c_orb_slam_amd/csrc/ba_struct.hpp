@@ -1,0 +1,33 @@
+// ba_struct.hpp -- host side of initializeOptimization(level) + buildIndexMapping +
+// BlockSolver::buildStructure (g2o sparse_optimizer.cpp:198-287, block_solver.hpp:73-216):
+// the active edge set of one optimisation level, vertex index maps and every list the BA
+// kernels walk (ba.hip).  Pure C++, no device calls: BaEngine::build_structure packs the
+// result and uploads it once per structure.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace orbgpu {
+
+struct BaHostStruct {
+    // aE: active edge -> edge; ePose / eLand: active edge -> pose index (-1 fixed) / landmark
+    // poseKf / landPt: index -> keyframe / point (ascending mnId)
+    // peStart/peList: pose -> active edges (edge order); leStart/leList: landmark -> active
+    // edges (edge order); lpStart/lpList: landmark -> active edges with a free pose (pose order)
+    // blkI/blkJ: Schur blocks (diagonal first, then first use in landmark order);
+    // blkStart/pairA/pairB: per block, the landmark terms (landmark order)
+    std::vector<int32_t> aE, ePose, eLand, poseKf, landPt, peStart, peList, leStart, leList, lpStart, lpList, blkI,
+        blkJ, blkStart, pairA, pairB;
+};
+
+// Active edges of `level` and the vertices they touch.
+void ba_active_set(int level, int nkf, int npt, int ne, const int32_t* eKf, const int32_t* ePt, const uint8_t* edgeLevel,
+                   std::vector<int32_t>* aE, std::vector<uint8_t>* kfAct, std::vector<uint8_t>* ptAct);
+
+// The index maps and lists of an active set.  kfAct may be the union over shards.  Returns 0,
+// or -1 when a landmark has two edges to one pose (g2o would build a duplicate Hpl block).
+int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, const uint8_t* kfFixed,
+                   const int32_t* kfId, const int32_t* ptId, const std::vector<uint8_t>& kfAct,
+                   const std::vector<uint8_t>& ptAct, BaHostStruct* S);
+
+}  // namespace orbgpu

@@ -3,7 +3,6 @@
 #include <algorithm>
 #include <cstring>
 #include <new>
-#include <unordered_set>
 #include <vector>
 
 #include "ba.hpp"
@@ -32,18 +31,29 @@ int validate(const ba_problem* P, const ba_result* R) {
     if (P->n_pt && (!P->pt_id || !P->pt_pos || !R->pt_pos)) return ORB_E_INVALID;
     if (P->n_edge && (!P->edge_pt || !P->edge_kf || !P->edge_obs || !P->edge_inv_sigma2 || !R->edge_erase))
         return ORB_E_INVALID;
-    std::unordered_set<int32_t> ids;
-    for (int k = 0; k < P->n_kf; k++)
-        if (!ids.insert(P->kf_id[k]).second) return ORB_E_INVALID;
-    ids.clear();
-    for (int p = 0; p < P->n_pt; p++)
-        if (!ids.insert(P->pt_id[p]).second) return ORB_E_INVALID;
-    std::unordered_set<int64_t> pairs;
+    // distinct ids (sorted copies) and one edge per (map point, keyframe): the edges bucketed by
+    // point, a keyframe stamp per bucket -- O(edges), no hashing (validation runs on every call)
+    auto distinct = [](const int32_t* v, int n) {
+        std::vector<int32_t> c(v, v + n);
+        std::sort(c.begin(), c.end());
+        return std::adjacent_find(c.begin(), c.end()) == c.end();
+    };
+    if (!distinct(P->kf_id, P->n_kf) || !distinct(P->pt_id, P->n_pt)) return ORB_E_INVALID;
+    std::vector<int32_t> start((size_t)P->n_pt + 1, 0);
     for (int i = 0; i < P->n_edge; i++) {
         const int32_t pt = P->edge_pt[i], kf = P->edge_kf[i];
         if (pt < 0 || pt >= P->n_pt || kf < 0 || kf >= P->n_kf) return ORB_E_INVALID;
-        if (!pairs.insert((int64_t)pt * P->n_kf + kf).second) return ORB_E_INVALID;
+        start[pt + 1]++;
     }
+    for (int p = 0; p < P->n_pt; p++) start[p + 1] += start[p];
+    std::vector<int32_t> kfs(std::max(P->n_edge, 1)), fill(start.begin(), start.end() - 1);
+    for (int i = 0; i < P->n_edge; i++) kfs[fill[P->edge_pt[i]]++] = P->edge_kf[i];
+    std::vector<int32_t> stamp(std::max(P->n_kf, 1), -1);
+    for (int p = 0; p < P->n_pt; p++)
+        for (int j = start[p]; j < start[p + 1]; j++) {
+            if (stamp[kfs[j]] == p) return ORB_E_INVALID;
+            stamp[kfs[j]] = p;
+        }
     if (P->n_kf > 32768) return ORB_E_CAPACITY;   // block-sparse pose system: tile map (n_kf / 10.7)^2 ints
     return ORB_OK;
 }

@@ -385,22 +385,25 @@ __device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked block
     return scan_local(P, q, blocked, top, GView{P});
 }
 
-// Parallel phase: one thread per query.  STAGE: the workgroup first copies the current
-// frame's grid, keypoint positions / octaves and descriptors into LDS (every problem has
-// N <= kStageMaxN), so the window walks -- cell start -> keypoint index -> keypoint ->
-// descriptor, a chain of dependent loads per candidate -- read LDS instead of L2/HBM.
+// Parallel phase: one thread per query.  STAGE: one 1024-thread workgroup per problem first
+// copies the current frame's grid, keypoint positions / octaves and descriptors into LDS (every
+// problem has N <= kStageMaxN), then walks all of the problem's queries, so the window walks --
+// cell start -> keypoint index -> keypoint -> descriptor, a chain of dependent loads per
+// candidate -- read LDS, and the frame is read from HBM once per problem.
 constexpr int kStageMaxN = 1536;
+constexpr int kStageThreads = 1024;
 constexpr size_t kStageLds = sizeof(uint16_t) * (kGridCells + 2) + sizeof(uint16_t) * kStageMaxN +
                              sizeof(float2) * kStageMaxN + kStageMaxN + 32 * (size_t)kStageMaxN + 64;
-template <bool LAST, bool STAGE>
-__global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict__ probs, float th, int bMono,
-                                                    unsigned long long* counters) {
+template <bool LAST, bool STAGE, int NT>
+__global__ void __launch_bounds__(NT) k_candidates(const SearchDev* __restrict__ probs, float th, int bMono,
+                                                   unsigned long long* counters) {
     ORBGPU_LATENCY_WAVE();
     const SearchDev P = probs[blockIdx.y];
-    int q = blockIdx.x * blockDim.x + threadIdx.x;
     int nvis = P.nq;
-    if (!LAST && P.visList) nvis = *P.visCount;   // SearchLocalPoints: thread t takes the t-th in-view query
-    if (STAGE && !counters && (int)(blockIdx.x * blockDim.x) >= nvis) return;   // no query in this block
+    if (!LAST && P.visList) nvis = *P.visCount;   // SearchLocalPoints: the t-th in-view query
+    if (STAGE && !counters && nvis == 0) return;
+    const int tBegin = STAGE ? (int)threadIdx.x : (int)(blockIdx.x * NT + threadIdx.x);
+    const int tStride = STAGE ? NT : (int)(gridDim.x * NT);
     LView V{};
     if constexpr (STAGE) {
         extern __shared__ __align__(16) unsigned char s_stage[];
@@ -411,49 +414,44 @@ __global__ void __launch_bounds__(256) k_candidates(const SearchDev* __restrict_
         uint8_t* s_oct = reinterpret_cast<uint8_t*>(s_gi + kStageMaxN);                // N
         const int N = P.cur.N, tid = threadIdx.x;
         const uint4* gd = reinterpret_cast<const uint4*>(P.cur.desc);
-        for (int k = tid; k < 2 * N; k += 256) s_desc[k] = gd[k];
-        for (int k = tid; k < N; k += 256) {
+        for (int k = tid; k < 2 * N; k += NT) s_desc[k] = gd[k];
+        for (int k = tid; k < N; k += NT) {
             const orb_kp_dev kp = P.cur.keysUn[k];
             s_xy[k] = make_float2(kp.x, kp.y);
             s_oct[k] = (uint8_t)kp.octave;
             s_gi[k] = (uint16_t)P.gridIdx[k];
         }
-        for (int c = tid; c <= kGridCells; c += 256) s_gs[c] = (uint16_t)P.gridStart[c];
+        for (int c = tid; c <= kGridCells; c += NT) s_gs[c] = (uint16_t)P.gridStart[c];
         __syncthreads();
         V = LView{s_gs, s_gi, s_xy, s_oct, s_desc};
     }
-    if (!LAST && P.visList) {
-        if (q >= nvis) {
-            if (!counters) return;
-            q = P.nq;   // measurement only
-        } else {
-            q = P.visList[q];
-        }
-    }
-    if (!counters && q >= P.nq) return;
-    TopK<kTopK> top;
-    int cnt = -1;
+    bool bF = false, bB = false;
+    if (LAST) fwd_bwd(P, bMono != 0, bF, bB);
+    unsigned long long pr = 0, nqv = 0;
     auto never = [](int) { return false; };
-    if (q >= P.nq) {   // measurement only: the wave stays whole for its counter sums
-    } else if (LAST) {
-        bool bF, bB;
-        fwd_bwd(P, bMono != 0, bF, bB);
-        const LastQuery lq = last_query(P, q, th, bF, bB);
-        if (lq.valid) cnt = STAGE ? scan_last(P, lq, never, top, V) : scan_last(P, lq, never, top);
-    } else {
-        const LocalQuery lq = local_query(P, q, th);
-        if (lq.valid) cnt = STAGE ? scan_local(P, lq, never, top, V) : scan_local(P, lq, never, top);
-    }
-    if (q < P.nq) {
+    for (int t = tBegin; t < nvis; t += tStride) {
+        const int q = (!LAST && P.visList) ? P.visList[t] : t;
+        if (q >= P.nq) continue;
+        TopK<kTopK> top;
+        int cnt = -1;
+        if (LAST) {
+            const LastQuery lq = last_query(P, q, th, bF, bB);
+            if (lq.valid) cnt = STAGE ? scan_last(P, lq, never, top, V) : scan_last(P, lq, never, top);
+        } else {
+            const LocalQuery lq = local_query(P, q, th);
+            if (lq.valid) cnt = STAGE ? scan_local(P, lq, never, top, V) : scan_local(P, lq, never, top);
+        }
         P.qinfo[q] = make_int4(cnt, 0, 0, 0);
         const int kk = cnt < kTopK ? cnt : kTopK;
 #pragma unroll
         for (int k = 0; k < kTopK; k++)
             if (k < kk) P.topk[(size_t)q * kTopK + k] = top.t[k];
+        if (cnt > 0) pr += (unsigned long long)cnt;
+        if (cnt >= 0) nqv++;
     }
     if (counters) {   // measurement: scored pairs and windowed queries
-        const unsigned long long pr = wave_sum_u64(cnt > 0 ? (unsigned long long)cnt : 0ull);
-        const unsigned long long nqv = wave_sum_u64(cnt >= 0 ? 1ull : 0ull);
+        pr = wave_sum_u64(pr);
+        nqv = wave_sum_u64(nqv);
         if ((threadIdx.x & 63) == 0) {
             const int sl = (blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 6)) & (kCountSlots - 1);
             atomicAdd(&counters[0 * kCountSlots + sl], pr);
@@ -1114,22 +1112,22 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     if (maxq > 0) {
         if (lastMode) {
             if (maxN <= kStageMaxN)
-                hipLaunchKernelGGL((k_candidates<true, true>), dim3((maxq + 255) / 256, np), dim3(256), kStageLds, stream_, dp,
-                                   th, (int)bMono, counters());
+                hipLaunchKernelGGL((k_candidates<true, true, kStageThreads>), dim3(1, np), dim3(kStageThreads), kStageLds,
+                                   stream_, dp, th, (int)bMono, counters());
             else
-                hipLaunchKernelGGL((k_candidates<true, false>), dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th,
-                                   (int)bMono, counters());
+                hipLaunchKernelGGL((k_candidates<true, false, 256>), dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp,
+                                   th, (int)bMono, counters());
             mark(2);
             // nq = the last frame's N <= kMaxFrameKeys = 512 * kSelQLast: every query in a slot
             hipLaunchKernelGGL((k_select_r<true, 512, kSelQLast>), dim3(np), dim3(512), select_lds_bytes(maxN), stream_, dp,
                                th, (int)bMono, nnratio, (int)checkOri_, maxN);
         } else {
             if (maxN <= kStageMaxN)
-                hipLaunchKernelGGL((k_candidates<false, true>), dim3((maxq + 255) / 256, np), dim3(256), kStageLds, stream_,
-                                   dp, th, 0, counters());
+                hipLaunchKernelGGL((k_candidates<false, true, kStageThreads>), dim3(1, np), dim3(kStageThreads), kStageLds,
+                                   stream_, dp, th, 0, counters());
             else
-                hipLaunchKernelGGL((k_candidates<false, false>), dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp, th, 0,
-                                   counters());
+                hipLaunchKernelGGL((k_candidates<false, false, 256>), dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp,
+                                   th, 0, counters());
             mark(2);
             // SearchLocalPoints-sized query sets (thousands of local map points, long occupancy
             // chains between duplicated points): 16 waves per round of the fixed point

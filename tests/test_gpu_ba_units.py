@@ -49,7 +49,7 @@ def _spd(rng, n):
 
 
 @pytest.mark.parametrize("variant", [0, 1])
-@pytest.mark.parametrize("n", [1, 6, 12, 60, 64, 66, 84, 126, 128])
+@pytest.mark.parametrize("n", [1, 6, 12, 60, 63, 64, 66, 84, 90, 126, 127, 128])
 def test_ldlt_matches_oracle(gpu, n, variant):
     from c_orb_slam_amd._lib import lib
     rng = np.random.default_rng(100 + n)
@@ -60,7 +60,11 @@ def test_ldlt_matches_oracle(gpu, n, variant):
     b = rng.normal(size=n)
     x = np.zeros(n)
     ok = C.c_int()
-    assert lib().orbgpu_unit_ldlt_solve(n, ptr(np.ascontiguousarray(S_in)), ptr(b), ptr(x), variant, C.byref(ok)) == 0
+    rc = lib().orbgpu_unit_ldlt_solve(n, ptr(np.ascontiguousarray(S_in)), ptr(b), ptr(x), variant, C.byref(ok))
+    if variant == 0 and n >= 128:   # the register solver keeps b in column n: n <= 127 (the product's n <= 126)
+        assert rc != 0
+        return
+    assert rc == 0
     oko, xo = _ora_ldlt(S_in, b)
     assert ok.value == oko == 1
     assert np.array_equal(x, xo), np.abs(x - xo).max()

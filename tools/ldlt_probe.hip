@@ -1,12 +1,14 @@
-// ldlt_probe.hip -- phase timing (shader cycles) of k_ldlt_reg on an n=84 SPD system.
+// ldlt_probe.hip -- phase timing (shader cycles) of k_ldlt_reg on an n x n SPD system (default 90).
+// build: compile this file, csrc/ldlt.hip (hipcc -c) and csrc/ordering.cpp (g++ -c), link with hipcc -> build/ldlt_probe
 #define ORB_LDLT_PROBE 1
 #include "../c_orb_slam_amd/csrc/ba.hip"
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #include <random>
 
-int main() {
-    const int n = 84;
+int main(int argc, char** argv) {
+    const int n = argc > 1 ? atoi(argv[1]) : 90;
     std::mt19937 g(1);
     std::normal_distribution<double> N(0, 1);
     std::vector<double> A(n * n), S(n * n, 0), b(n);
@@ -24,18 +26,18 @@ int main() {
     hipMemcpy(dB, b.data(), 8 * n, hipMemcpyHostToDevice);
     const size_t shm = sizeof(double) * ((size_t)n * n + 14 * orbgpu::kLdltMax);
     for (int rep = 0; rep < 3; rep++) {
-        hipLaunchKernelGGL(orbgpu::k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal);
+        hipLaunchKernelGGL(orbgpu::k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal, nullptr);
         hipDeviceSynchronize();
     }
     long long p[256];
     hipMemcpyFromSymbol(p, HIP_SYMBOL(orbgpu::g_ldlt_probe), sizeof(p));
     printf("load %lld | panels %lld | fwd %lld | bwd %lld  (cycles)\n", p[1] - p[0], p[2] - p[1], p[3] - p[2], p[4] - p[3]);
     long long pub = 0, ph1 = 0, tr = 0;
-    for (int k = 0; k < 14; k++) {
+    for (int k = 0; k < n / 6; k++) {
         pub += p[11 + 4 * k] - p[10 + 4 * k];
         ph1 += p[12 + 4 * k] - p[11 + 4 * k];
         tr += p[13 + 4 * k] - p[12 + 4 * k];
     }
-    printf("publish %lld | phase1 %lld | trailing %lld  (cycles, 14 panels)\n", pub, ph1, tr);
+    printf("publish %lld | phase1 %lld | trailing %lld  (cycles, n/6 panels)\n", pub, ph1, tr);
     return 0;
 }
