@@ -629,6 +629,7 @@ def main():
         nq = len(per_q)
         dist = torch.empty(len(cand), dtype=torch.int32, device=dev)
         bi, bd, sd = (torch.empty(nq, dtype=torch.int32, device=dev) for _ in range(3))
+        pose_ms, pose_edges, pms = [], [], C.c_float()
         torch.cuda.synchronize()
         for _ in range(reps):
             lane.stereo()
@@ -637,6 +638,13 @@ def main():
             lane.search()
             grab((("k_build_grid", 0), ("k_candidates", 1), ("k_select", 2)),
                  (("search_pairs", 0), ("search_queries", 1)))
+            # PoseOptimization of the same batch (TrackWithMotionModel's call), k_pose_opt timed alone
+            check(L.Optimizer_pose_timing(1, None), "Optimizer_pose_timing")
+            check(L.Optimizer_PoseOptimization_frames_device(P, lane.pframes, lane.a_Tout, lane.a_poutl,
+                                                             ptr(lane.ninl)), "PoseOptimization (isolated)")
+            check(L.Optimizer_pose_timing(0, C.byref(pms)), "Optimizer_pose_timing")
+            pose_ms.append(pms.value)
+            pose_edges.append((int(lane.n_pose.sum()), int(lane.ninl.sum())))
             check(L.ORBmatcher_SearchCandidates(m._h, C.c_void_p(qd.data_ptr()), nq, C.c_void_p(td.data_ptr()),
                                                 len(td), C.c_void_p(off.data_ptr()), C.c_void_p(cand.data_ptr()),
                                                 None, C.c_void_p(bi.data_ptr()),
@@ -722,6 +730,25 @@ def main():
                               "unit": "G wave-instr/s", "frac": round(vr / VALU_PEAK_GINST, 4)}
             ed["pmc_source"] = f"profiles/{MATCH_PMC_FILE}"
         out["k_dense_hamming"] = ed
+        # k_pose_opt (the tracking lane's critical path): one workgroup per frame runs the whole LM
+        # loop; bound by the VALU issue of the CUs it occupies
+        t = float(np.mean(pose_ms))
+        ep = {"avg_launch_ms": round(t, 4), "frames_per_launch": P,
+              "keypoints_per_launch": int(np.mean([a for a, _ in pose_edges])),
+              "inliers_per_launch": int(np.mean([b for _, b in pose_edges])),
+              "bound": "valu", "workload": "TrackWithMotionModel's PoseOptimization of the batch (one 256-thread "
+                                           "workgroup per frame: 4 rounds of optimize(10))"}
+        pk = next((k for k in pmc if k.startswith("k_pose_opt")), None)
+        if pk and pmc[pk].get("valu_insts_per_launch"):
+            vi = pmc[pk]["valu_insts_per_launch"]
+            vr = vi / (t * 1e-3) / 1e9
+            ep.update({"insts_per_launch": int(vi), "achieved": round(vr, 1), "peak": VALU_PEAK_GINST,
+                       "unit": "G wave-instr/s", "frac": round(vr / VALU_PEAK_GINST, 4),
+                       "frac_of_occupied_cus": round(vr / (VALU_PEAK_GINST * P / 256), 4),
+                       "pmc_source": f"profiles/{MATCH_PMC_FILE}"})
+            if pmc[pk].get("hbm_bytes_per_launch"):
+                ep["traffic"] = pmc[pk]["hbm_bytes_per_launch"]
+        out["k_pose_opt"] = ep
         for k in ("k_build_grid", "k_select", "k_stereo_rows", "k_stereo_filter"):
             out[k] = {"avg_launch_ms": round(float(np.mean(acc[k])), 4), "bound": "latency (one workgroup per frame)"}
         out["definition"] = ("alg bytes = 36 B per scored (query, candidate) pair (32 B candidate descriptor + 4 B "

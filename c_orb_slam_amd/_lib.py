@@ -198,6 +198,7 @@ def lib():
     L.Optimizer_OptimizeSim3.argtypes = [vp, vp, vp, P(i32)]
     L.Optimizer_OptimizeSim3_batch.argtypes = [i32, vp, vp, vp, vp]
     L.Optimizer_PoseOptimization_frames_device.argtypes = [i32, vp, vp, vp, vp]
+    L.Optimizer_pose_timing.argtypes = [i32, vp]
     L.Frame_UnprojectStereo_batch_device.argtypes = [vp, i32, vp]
     L.Frame_UndistortKeyPoints.argtypes = [vp, vp]
     L.Frame_UndistortKeyPoints_batch.argtypes = [vp, i32, vp]

@@ -736,62 +736,67 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
         }
         __syncthreads();
         LDLT_PROBE(11 + 4 * (p0 / 6));
-        if (w == 0) {
-            double u0[6], u1[6];
+        if (tid < kLdltMax) {
+            // panel factorisation, one thread per column j (waves 0-1): every thread first
+            // factorises the panel's 6x6 diagonal block from LDS (the same operations as the
+            // block's own columns perform below, so d and the block's L agree bit for bit), then
+            // its own column: l_jk = u_kj / d_k and u_tj -= L[t][k] u_kj, k ascending -- no
+            // cross-lane traffic inside the panel
+            const int j = tid;
+            double Bk[6][6], Lb[6][6], dd[6];
+#pragma unroll
+            for (int t = 0; t < 6; t++)
+#pragma unroll
+                for (int c = 0; c < 6; c++) {
+                    Bk[t][c] = (t < pw && c < pw && c >= t) ? U[t * kLdltMax + p0 + c] : 0.0;
+                    Lb[t][c] = 0.0;
+                }
+            bool bad = false;
 #pragma unroll
             for (int t = 0; t < 6; t++) {
-                u0[t] = t < pw ? U[t * kLdltMax + lane] : 0.0;
-                u1[t] = t < pw ? U[t * kLdltMax + lane + 64] : 0.0;
+                dd[t] = Bk[t][t];
+                if (t < pw) {
+                    bad |= dd[t] == 0.0;
+#pragma unroll
+                    for (int t2 = t + 1; t2 < 6; t2++)
+                        if (t2 < pw) Lb[t2][t] = Bk[t][t2] / dd[t];
+#pragma unroll
+                    for (int t2 = t + 1; t2 < 6; t2++)
+#pragma unroll
+                        for (int c = t2; c < 6; c++)
+                            if (c < pw) Bk[t2][c] -= Lb[t2][t] * Bk[t][c];
+                }
             }
-            bool bad = false;
-            // the pivot of column t + 1 is formed on its own lane from that lane's own l (the value
-            // every lane receives by broadcast), so the dependent chain per column is one broadcast,
-            // one division and one multiply-subtract; a zero pivot only raises the flag
-            double d = readlane_d(p0 < 64 ? u0[0] : u1[0], p0 & 63);
+            LDLT_PROBE(200 + (p0 / 6 < 15 ? p0 / 6 : 15));
+            double u[6];
+#pragma unroll
+            for (int t = 0; t < 6; t++) u[t] = t < pw ? U[t * kLdltMax + j] : 0.0;
 #pragma unroll
             for (int t = 0; t < 6; t++) {
                 if (t < pw) {
                     const int k = p0 + t;
-                    bad |= d == 0.0;
-                    const bool a0 = lane > k && lane < n, a1 = lane + 64 > k && lane + 64 < n;
-                    const double l0 = a0 ? u0[t] / d : 0.0;
-                    const double l1 = a1 ? u1[t] / d : 0.0;
-                    double dn = 0.0;
-                    if (t + 1 < pw) {
-                        const int k1 = k + 1;
-                        const double pv = k1 < 64 ? u0[t + 1] - l0 * u0[t] : u1[t + 1] - l1 * u1[t];
-                        dn = readlane_d(pv, k1 & 63);
-                    }
+                    const bool act = j > k && j < n;
+                    const double l = act ? u[t] / dd[t] : 0.0;
 #pragma unroll
-                    for (int t2 = t + 1; t2 < 6; t2++) {
-                        if (t2 < pw) {
-                            const int i = p0 + t2;
-                            const double li = readlane_d(i < 64 ? l0 : l1, i & 63);
-                            if (lane >= i) u0[t2] -= li * u0[t];
-                            if (lane + 64 >= i) u1[t2] -= li * u1[t];
-                        }
+                    for (int t2 = t + 1; t2 < 6; t2++)
+                        if (t2 < pw && j >= p0 + t2) u[t2] -= Lb[t2][t] * u[t];
+                    if (act) {
+                        Lall[(size_t)k * n + j] = l;
+                        Lpan[j * 6 + t] = l;
                     }
-                    if (a0) {
-                        Lall[(size_t)k * n + lane] = l0;
-                        Lpan[lane * 6 + t] = l0;
-                    }
-                    if (a1) {
-                        Lall[(size_t)k * n + lane + 64] = l1;
-                        Lpan[(lane + 64) * 6 + t] = l1;
-                    }
-                    if (lane == 0) dvec[k] = d;
-                    if (lane == n) y[k] = u0[t];
-                    if (lane + 64 == n) y[k] = u1[t];
-                    d = dn;
+                    if (j == n) y[k] = u[t];   // row k's right-hand side is final: forward-substituted y_k
                 }
             }
-            if (bad && lane == 0) ok = 0;
+            LDLT_PROBE(220 + (p0 / 6 < 15 ? p0 / 6 : 15));
 #pragma unroll
             for (int t = 0; t < 6; t++)
-                if (t < pw) {
-                    U[t * kLdltMax + lane] = u0[t];
-                    U[t * kLdltMax + lane + 64] = u1[t];
-                }
+                if (t < pw) U[t * kLdltMax + j] = u[t];
+            if (j == 0) {
+#pragma unroll
+                for (int t = 0; t < 6; t++)
+                    if (t < pw) dvec[p0 + t] = dd[t];
+                if (bad) ok = 0;
+            }
         }
         __syncthreads();
         LDLT_PROBE(12 + 4 * (p0 / 6));
@@ -1306,14 +1311,15 @@ __device__ __forceinline__ double pose_rho0(const PoseEdgeD& e, double c, bool r
 
 
 constexpr int kPoseMaxEdges = 8192;
-// one wave per SIMD: the workgroup fits beside the extraction grids (batches); a batch of at
-// most pose_wide_max() frames (the per-frame tracking latency) takes two waves per SIMD instead,
-// half the chunks per wave in every edge pass (the same canonical sums: bit-identical)
+// two waves per SIMD (512 threads): half the chunks per wave in every edge pass (the same
+// canonical sums: bit-identical).  Measured in the pipeline beside the extraction grids too:
+// 28.8 k vs 28.1 k frames/s for the one-wave-per-SIMD instance (256 threads) at B = 64, so
+// every batch takes it; ORBGPU_POSE_WIDE_MAX = F keeps it for batches of at most F frames only
 constexpr int kPoseThreads = 256, kPoseThreadsWide = 512;
-static int pose_wide_max() {   // ORBGPU_POSE_WIDE_MAX overrides the batch limit of the wide kernel
+static int pose_wide_max() {
     static const int v = [] {
         const char* e = getenv("ORBGPU_POSE_WIDE_MAX");
-        return e ? atoi(e) : 8;
+        return e ? atoi(e) : (1 << 30);
     }();
     return v;
 }
@@ -2067,6 +2073,7 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
     if (lastUseSet_) ORB_HIP_CHECK(hipStreamWaitEvent(st, lastUse_, 0));
     ORB_HIP_CHECK(hipMemcpyAsync(d, src, sizeof(PoseProbDev) * count, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_pose_pack, dim3(count), dim3(kPackThreads), 0, st, dp, dE);
+    if (timing_) ORB_HIP_CHECK(hipEventRecord(tA_, st));
     if (count <= pose_wide_max())
         hipLaunchKernelGGL(k_pose_opt<kPoseThreadsWide>, dim3(count), dim3(kPoseThreadsWide), 0, st, dp, (const PoseEdgeDev*)dE, nullptr,
                            (uint8_t*)(d + bProb + bEdge));
@@ -2074,6 +2081,10 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
         hipLaunchKernelGGL(k_pose_opt<kPoseThreads>, dim3(count), dim3(kPoseThreads), 0, st, dp, (const PoseEdgeDev*)dE, nullptr,
                            (uint8_t*)(d + bProb + bEdge));
     ORB_HIP_CHECK(hipGetLastError());
+    if (timing_) {
+        ORB_HIP_CHECK(hipEventRecord(tB_, st));
+        timed_ = true;
+    }
     if (chain) {
         chain->land_dev(ninliers, dNin, sizeof(int) * count);
         ORB_HIP_CHECK(hipEventRecord(lastUse_, st));
@@ -2093,9 +2104,18 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
     return rc;
 }
 
+int PoseEngine::last_timing(float* ms) {
+    if (!timed_) return -1;
+    ORB_HIP_CHECK(hipEventSynchronize(tB_));
+    ORB_HIP_CHECK(hipEventElapsedTime(ms, tA_, tB_));
+    return 0;
+}
+
 PoseEngine::~PoseEngine() {
     if (lastUseSet_) (void)hipEventSynchronize(lastUse_);
     if (lastUse_) (void)hipEventDestroy(lastUse_);
+    if (tA_) (void)hipEventDestroy(tA_);
+    if (tB_) (void)hipEventDestroy(tB_);
     if (dArena_) (void)hipFree(dArena_);
     if (hArena_) (void)hipHostFree(hArena_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -2106,6 +2126,8 @@ int PoseEngine::init() {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     ORB_HIP_CHECK(hipEventCreateWithFlags(&lastUse_, hipEventDisableTiming));
+    ORB_HIP_CHECK(hipEventCreate(&tA_));
+    ORB_HIP_CHECK(hipEventCreate(&tB_));
     return 0;
 }
 

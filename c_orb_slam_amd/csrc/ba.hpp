@@ -176,6 +176,9 @@ public:
     int run_frames_device(int count, const pose_frame* F, float* const* Tcw_out, uint8_t* const* outlier,
                           int* ninliers, hipStream_t s = nullptr, DeferredChain* chain = nullptr);
     hipStream_t stream() const { return stream_; }
+    // k_pose_opt duration of the last launch (HIP events on its stream) while timing is on
+    void set_timing(bool on) { timing_ = on; }
+    int last_timing(float* ms);
 
 private:
     int launch_device(int count, const int* Ns, const std::function<void(int, PoseProbDev&)>& fill,
@@ -189,6 +192,8 @@ private:
     // the next user waits on it before overwriting the arena
     hipEvent_t lastUse_ = nullptr;
     bool lastUseSet_ = false;
+    bool timing_ = false, timed_ = false;
+    hipEvent_t tA_ = nullptr, tB_ = nullptr;
 };
 
 int debug_ldlt(int n, const double* S, const double* b, double* x, int variant);

@@ -154,6 +154,19 @@ int Optimizer_PoseOptimization_batch_device(int count, const pose_problem* P, fl
     return r ? ORB_E_HIP : ORB_OK;
 }
 
+int Optimizer_pose_timing(int enable, float* last_ms) {
+    int rc = 0;
+    orbgpu::PoseEngine* e = pose_engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    if (enable >= 0) e->set_timing(enable != 0);
+    if (last_ms) {
+        const int r = e->last_timing(last_ms);
+        if (r == -1) return ORB_E_INVALID;   // nothing timed yet
+        if (r) return ORB_E_HIP;
+    }
+    return ORB_OK;
+}
+
 int Optimizer_PoseOptimization_frames_device(int count, const pose_frame* F, float* const* Tcw_out,
                                              uint8_t* const* outlier, int* ninliers) {
     if (count < 0 || (count > 0 && (!F || !Tcw_out || !outlier || !ninliers))) return ORB_E_INVALID;

@@ -752,6 +752,11 @@ typedef struct pose_frame {
     int nlevels;
     float fx, fy, cx, cy, bf;
 } pose_frame;
+/* Measurement: enable >= 0 switches k_pose_opt timing (HIP events around the launch on the calling
+ * thread's pose engine) on or off; last_ms (optional) receives the duration of the last timed
+ * launch (waits for it).  ORB_E_INVALID when nothing was timed yet.  No reference counterpart. */
+int Optimizer_pose_timing(int enable, float* last_ms);
+
 /* Same outputs and capacity rule as Optimizer_PoseOptimization_batch_device. */
 int Optimizer_PoseOptimization_frames_device(int count, const pose_frame* F, float* const* Tcw_out,
                                              uint8_t* const* outlier, int* ninliers);

@@ -190,3 +190,4 @@ def test_wave_tree_matches_canonical_tree(gpu):
         out = C.c_double()
         assert lib().orbgpu_unit_wave_tree(ptr(np.ascontiguousarray(v)), C.byref(out)) == 0
         assert out.value == _ora_csum(v), trial
+

@@ -39,5 +39,11 @@ int main(int argc, char** argv) {
         tr += p[13 + 4 * k] - p[12 + 4 * k];
     }
     printf("publish %lld | phase1 %lld | trailing %lld  (cycles, n/6 panels)\n", pub, ph1, tr);
+    long long blk = 0, col = 0;
+    for (int k = 0; k < n / 6 && k < 15; k++) {
+        blk += p[200 + k] - p[11 + 4 * k];
+        col += p[220 + k] - p[200 + k];
+    }
+    printf("phase1 split (first 15 panels): diagonal block %lld | own column %lld (cycles)\n", blk, col);
     return 0;
 }

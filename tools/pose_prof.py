@@ -9,7 +9,10 @@ from c_orb_slam_amd import PoseOptimizationBatch  # noqa: E402
 from c_orb_slam_amd._lib import lib  # noqa: E402
 from pose_cases import pose_problem  # noqa: E402
 
-frames = [pose_problem(s, N=1500) for s in range(64)]
+# argv: keypoints per frame, fraction with a map point (the bench's batch: ~1200 and ~0.45)
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 1500
+mp = float(sys.argv[2]) if len(sys.argv) > 2 else 0.7
+frames = [pose_problem(s, N=N, mp_frac=mp) for s in range(64)]
 PoseOptimizationBatch(frames)
 out = (C.c_ulonglong * 32)()
 lib().orbgpu_debug_prof(out)
