@@ -190,3 +190,20 @@ def test_global_ba_config5_2000kf_loops_g2o_order_sharded(gpu):
     _close(s, o)
     for r in per[1:]:
         assert np.array_equal(r["kf_Tcw"], per[0]["kf_Tcw"])
+
+
+@pytest.mark.timeout(600)
+def test_global_ba_config5_8000kf_loops_matches_oracle(gpu):
+    """Config 5 at its middle stated size: 8,000 keyframes as 4 laps of one circuit (~1.12 M
+    points, ~6 M edges, n = 47,994 pose rows through the nested-dissection tiled LDL^T),
+    BundleAdjustment with one LM iteration (the factorisation and every accumulation at full
+    size; the single-thread oracle needs ~50 s per iteration here): bit-identical LM trace,
+    poses and points."""
+    from c_orb_slam_amd.optimizer import BundleAdjustment
+    pr = global_ba_problem(6, n_kf=8000, pts_per_kf=150, laps=4)
+    assert len(pr["edge_pt"]) > 5_000_000
+    o = oracle_lib.oracle_global_ba(pr, 1, False)
+    g = BundleAdjustment(pr, 1, False, trace=True)
+    assert g["iterations"] == o["iterations"]
+    np.testing.assert_allclose(g["trial_chi2"], o["trial_chi2"], rtol=1e-12)
+    _exact(g, o)
