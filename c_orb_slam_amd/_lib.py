@@ -199,6 +199,7 @@ def lib():
     L.Optimizer_OptimizeSim3_batch.argtypes = [i32, vp, vp, vp, vp]
     L.Optimizer_PoseOptimization_frames_device.argtypes = [i32, vp, vp, vp, vp]
     L.Optimizer_pose_timing.argtypes = [i32, vp]
+    L.orbgpu_unit_ba_struct.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, C.c_longlong]
     L.Frame_UnprojectStereo_batch_device.argtypes = [vp, i32, vp]
     L.Frame_UndistortKeyPoints.argtypes = [vp, vp]
     L.Frame_UndistortKeyPoints_batch.argtypes = [vp, i32, vp]

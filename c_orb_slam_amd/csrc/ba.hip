@@ -2219,6 +2219,7 @@ int PoseEngine::run(int count, const pose_problem* P, float* Tcw_out, uint8_t* c
 }
 
 BaEngine::~BaEngine() {
+    if (stream_) (void)hipStreamSynchronize(stream_);
     if (dPack_) (void)hipFree(dPack_);
     if (arena_) (void)hipFree(arena_);
     if (dStruct_) (void)hipFree(dStruct_);
@@ -2231,6 +2232,10 @@ BaEngine::~BaEngine() {
 }
 
 int BaEngine::stage_reserve(size_t bytes) {
+    if (uploadPending_) {   // the problem upload may still read the staging block
+        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        uploadPending_ = false;
+    }
     if (bytes <= hStageCap_) return 0;
     if (hStage_) (void)hipHostFree(hStage_);
     hStage_ = nullptr;
@@ -2394,7 +2399,9 @@ int BaEngine::upload_problem(const ba_problem* P) {
         ORB_HIP_CHECK(hipMemsetAsync(dErr_, 0, sizeof(double) * 3 * ne_, s));
     }
     ORB_HIP_CHECK(hipMemsetAsync(dCounter_, 0, sizeof(unsigned) * 16, s));
-    ORB_HIP_CHECK(hipStreamSynchronize(s));  // the staging block is reused by the next upload
+    // no wait here: the host builds the structure while the copies run; the next user of the
+    // staging block (stage_reserve) waits for them
+    uploadPending_ = true;
     return 0;
 }
 

@@ -138,6 +138,7 @@ private:
     // concurrently from different host threads, so no pageable hipMemcpy staging path is used
     void* hStage_ = nullptr;
     size_t hStageCap_ = 0;
+    bool uploadPending_ = false;   // upload_problem's copies may still read hStage_
     int h2d_sync(void* dst, const void* src, size_t bytes);
     int d2h_sync(void* dst, const void* src, size_t bytes);
     int stage_reserve(size_t bytes);

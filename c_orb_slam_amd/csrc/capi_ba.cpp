@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "ba.hpp"
+#include "ba_struct.hpp"
 #include "capi_handles.hpp"
 #include "ordering.hpp"
 #include "orb_match.hpp"
@@ -380,6 +381,32 @@ int orbgpu_unit_nd_order(int n, const int32_t* adjStart, const int32_t* adj, int
 int orbgpu_unit_set_csum_lds_max(int m2_max) {
     if (m2_max < 0 || m2_max > 1024) return ORB_E_INVALID;
     return orbgpu::debug_set_csum_lds_max(m2_max) ? ORB_E_HIP : ORB_OK;
+}
+
+int orbgpu_unit_ba_struct(int nkf, int npt, int ne, const int32_t* edge_kf, const int32_t* edge_pt,
+                          const uint8_t* edge_level, const uint8_t* kf_fixed, const int32_t* kf_id,
+                          const int32_t* pt_id, int level, int32_t* out, long long cap) {
+    if (nkf < 0 || npt < 0 || ne < 0 || !out || cap < 5) return ORB_E_INVALID;
+    if ((ne && (!edge_kf || !edge_pt || !edge_level)) || (nkf && (!kf_fixed || !kf_id)) || (npt && !pt_id))
+        return ORB_E_INVALID;
+    for (int i = 0; i < ne; i++)
+        if (edge_kf[i] < 0 || edge_kf[i] >= nkf || edge_pt[i] < 0 || edge_pt[i] >= npt) return ORB_E_INVALID;
+    orbgpu::BaHostStruct S;
+    std::vector<uint8_t> kfAct, ptAct;
+    orbgpu::ba_active_set(level, nkf, npt, ne, edge_kf, edge_pt, edge_level, &S.aE, &kfAct, &ptAct);
+    if (orbgpu::ba_build_lists(nkf, npt, edge_kf, edge_pt, kf_fixed, kf_id, pt_id, kfAct, ptAct, &S)) return ORB_E_INVALID;
+    const int nE = (int)S.aE.size(), nP = (int)S.poseKf.size(), nL = (int)S.landPt.size();
+    const int nBlk = (int)S.blkI.size(), nPair = S.blkStart[nBlk];
+    // [nE nP nL nBlk nPair | poseKf | landPt | ePose | eLand | lpStart | lpList | blkI | blkJ | blkStart | pairA | pairB]
+    const long long need = 5LL + nP + nL + 2LL * nE + (nL + 1) + S.lpStart[nL] + 2LL * nBlk + (nBlk + 1) + 2LL * nPair;
+    if (need > cap) return ORB_E_CAPACITY;
+    int32_t* o = out;
+    *o++ = nE; *o++ = nP; *o++ = nL; *o++ = nBlk; *o++ = nPair;
+    auto put = [&](const std::vector<int32_t>& v, size_t n) { o = std::copy(v.begin(), v.begin() + n, o); };
+    put(S.poseKf, nP); put(S.landPt, nL); put(S.ePose, nE); put(S.eLand, nE); put(S.lpStart, nL + 1);
+    put(S.lpList, S.lpStart[nL]); put(S.blkI, nBlk); put(S.blkJ, nBlk); put(S.blkStart, nBlk + 1);
+    put(S.pairA, nPair); put(S.pairB, nPair);
+    return ORB_OK;
 }
 
 int orbgpu_unit_wave_tree(const double* v64, double* out) {

@@ -385,11 +385,11 @@ __device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked block
     return scan_local(P, q, blocked, top, GView{P});
 }
 
-// Parallel phase: one thread per query.  STAGE: one 1024-thread workgroup per problem first
-// copies the current frame's grid, keypoint positions / octaves and descriptors into LDS (every
-// problem has N <= kStageMaxN), then walks all of the problem's queries, so the window walks --
-// cell start -> keypoint index -> keypoint -> descriptor, a chain of dependent loads per
-// candidate -- read LDS, and the frame is read from HBM once per problem.
+// Parallel phase: one thread per query.  STAGE: each 1024-thread workgroup first copies the
+// current frame's grid, keypoint positions / octaves and descriptors into LDS (every problem has
+// N <= kStageMaxN), then walks its 1024 queries, so the window walks -- cell start -> keypoint
+// index -> keypoint -> descriptor, a chain of dependent loads per candidate -- read LDS, and the
+// frame is read from HBM once per 1024 queries.
 constexpr int kStageMaxN = 1536;
 constexpr int kStageThreads = 1024;
 constexpr size_t kStageLds = sizeof(uint16_t) * (kGridCells + 2) + sizeof(uint16_t) * kStageMaxN +
@@ -401,9 +401,11 @@ __global__ void __launch_bounds__(NT) k_candidates(const SearchDev* __restrict__
     const SearchDev P = probs[blockIdx.y];
     int nvis = P.nq;
     if (!LAST && P.visList) nvis = *P.visCount;   // SearchLocalPoints: the t-th in-view query
-    if (STAGE && !counters && nvis == 0) return;
-    const int tBegin = STAGE ? (int)threadIdx.x : (int)(blockIdx.x * NT + threadIdx.x);
-    const int tStride = STAGE ? NT : (int)(gridDim.x * NT);
+    // a workgroup with no query of its own stages nothing (SearchLocalPoints' in-view count is
+    // known on the device only: the grid covers every local map point)
+    if (!counters && (int)(blockIdx.x * NT) >= nvis) return;
+    const int tBegin = (int)(blockIdx.x * NT + threadIdx.x);
+    const int tStride = (int)(gridDim.x * NT);
     LView V{};
     if constexpr (STAGE) {
         extern __shared__ __align__(16) unsigned char s_stage[];
@@ -1112,7 +1114,8 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     if (maxq > 0) {
         if (lastMode) {
             if (maxN <= kStageMaxN)
-                hipLaunchKernelGGL((k_candidates<true, true, kStageThreads>), dim3(1, np), dim3(kStageThreads), kStageLds,
+                hipLaunchKernelGGL((k_candidates<true, true, kStageThreads>), dim3((maxq + kStageThreads - 1) / kStageThreads, np),
+                                   dim3(kStageThreads), kStageLds,
                                    stream_, dp, th, (int)bMono, counters());
             else
                 hipLaunchKernelGGL((k_candidates<true, false, 256>), dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp,
@@ -1123,7 +1126,8 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
                                th, (int)bMono, nnratio, (int)checkOri_, maxN);
         } else {
             if (maxN <= kStageMaxN)
-                hipLaunchKernelGGL((k_candidates<false, true, kStageThreads>), dim3(1, np), dim3(kStageThreads), kStageLds,
+                hipLaunchKernelGGL((k_candidates<false, true, kStageThreads>), dim3((maxq + kStageThreads - 1) / kStageThreads, np),
+                                   dim3(kStageThreads), kStageLds,
                                    stream_, dp, th, 0, counters());
             else
                 hipLaunchKernelGGL((k_candidates<false, false, 256>), dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp,

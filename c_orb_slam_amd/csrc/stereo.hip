@@ -6,10 +6,10 @@
 // the left octave, a parabola through the best three SADs, depth = bf / disparity, and the
 // 2.1 x median SAD outlier filter.  No occupancy: every left keypoint is independent.
 //
-//   k_stereo_match   one wave per left keypoint (4 per workgroup), all pairs of the batch in
-//                    one launch (grid.y = pair): lanes sweep the right keypoints in index
-//                    order with popcount distances, a wave min over (dist, iR) picks the
-//                    reference's first strict minimum; the 11 SADs are integer wave sums
+//   k_stereo_match   one 16-lane group per left keypoint (16 per workgroup), all pairs of the
+//                    batch in one launch (grid.y = pair): lanes sweep the right keypoints in
+//                    index order with popcount distances, a group min over (dist, iR) picks the
+//                    reference's first strict minimum; the 11 SADs are integer group sums
 //                    (cv::norm of centred integer windows is exact), the parabola and the
 //                    disparity follow the reference's float expression order.
 //   k_stereo_filter  one workgroup per pair: bitonic sort of the kept SADs in LDS, median,
@@ -23,18 +23,6 @@
 
 namespace orbgpu {
 
-
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ unsigned wave_min_u(unsigned v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o, 64));
-    return v;
-}
 
 // vRowIndices (Frame.cc:476-493) as a CSR per pair: right keypoint iR is listed on every row
 // yi in [floor(y - r), ceil(y + r)], r = 2 * mvScaleFactors[octave].  The order inside a row
@@ -93,13 +81,29 @@ __global__ void __launch_bounds__(1024) k_stereo_rows(const StereoDev* __restric
     }
 }
 
+// sums / minima over the 16 lanes of a group (lanes 16g .. 16g+15 of the wave)
+__device__ __forceinline__ int group_sum_i(int v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 16);
+    return v;
+}
+
+__device__ __forceinline__ unsigned group_min_u(unsigned v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o, 16));
+    return v;
+}
+
+// One 16-lane group per left keypoint (16 keypoints per 256-thread workgroup, 4 per wave): the
+// row candidates 16 at a time, the 121 window pixels 8 per lane, the SADs as group sums.  All
+// reductions are integer minima / sums, so the result does not depend on the lane mapping.
 __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restrict__ probs, StereoParams P,
                                                       unsigned long long* counters) {
     ORBGPU_LATENCY_WAVE();
     const StereoDev& S = probs[blockIdx.y];
-    const int lane = threadIdx.x & 63;
-    const int iL = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (iL >= S.NL) return;
+    const int sub = threadIdx.x & 15;
+    const int iL = blockIdx.x * 16 + (threadIdx.x >> 4);
+    if (iL >= S.NL) return;   // the whole group
     const orb_kp_dev kpL = S.kL[iL];
     float uR_out = -1.0f, depth_out = -1.0f;
     int sad_out = -1;
@@ -117,7 +121,7 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
         unsigned best = 0xffffffffu;
         int scored = 0;
         const int c1 = S.rowStart[row + 1];
-        for (int c = S.rowStart[row] + lane; c < c1; c += 64) {
+        for (int c = S.rowStart[row] + sub; c < c1; c += 16) {
             const int iR = S.rowIdx[c];
             const orb_kp_dev kpR = S.kR[iR];
             if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
@@ -130,11 +134,11 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
             if (dist < 100) best = min(best, ((unsigned)dist << 16) | (unsigned)iR);
             scored++;
         }
-        best = wave_min_u(best);
+        best = group_min_u(best);
         if (counters) {   // measurement: scored (left, right) pairs and searched left keypoints
-            const int tot = wave_sum_i(scored);
-            if (lane == 0) {   // spread over kCountSlots addresses: one per wave would serialise
-                const int sl = (blockIdx.x + blockIdx.y * 7) & (kCountSlots - 1);
+            const int tot = group_sum_i(scored);
+            if (sub == 0) {   // spread over kCountSlots addresses: one per group would serialise
+                const int sl = (blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 4)) & (kCountSlots - 1);
                 atomicAdd(&counters[2 * kCountSlots + sl], (unsigned long long)tot);
                 atomicAdd(&counters[3 * kCountSlots + sl], 1ull);
             }
@@ -155,27 +159,27 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
                 const uint8_t* IR = S.pyrR + lv.off + (size_t)kEdge * lv.pitch + kEdge;
                 const int yL = (int)scaledvL, xL = (int)scaleduL, xR0 = (int)scaleduR0;
                 const int cL = IL[(ptrdiff_t)yL * lv.pitch + xL];
-                // lane owns window pixels p = lane and lane + 64 (p < 121)
-                int a[2], dyv[2], dxv[2];
+                // lane owns window pixels p = sub + 16 t (p < 121)
+                int a[8], offv[8];
 #pragma unroll
-                for (int t = 0; t < 2; t++) {
-                    const int p = lane + 64 * t;
-                    dyv[t] = p / 11 - 5;
-                    dxv[t] = p % 11 - 5;
-                    a[t] = p < 121 ? IL[(ptrdiff_t)(yL + dyv[t]) * lv.pitch + xL + dxv[t]] - cL : 0;
+                for (int t = 0; t < 8; t++) {
+                    const int p = sub + 16 * t;
+                    const int dy = p / 11 - 5, dx = p % 11 - 5;
+                    offv[t] = (yL + dy) * lv.pitch + dx;
+                    a[t] = p < 121 ? IL[(ptrdiff_t)offv[t] + xL] - cL : 0;
                 }
                 int vD[11];
 #pragma unroll
                 for (int inc = 0; inc < 11; inc++) {
                     const int xR = xR0 + inc - L;
                     const int cR = IR[(ptrdiff_t)yL * lv.pitch + xR];
-                    int s = 0;
+                    int sacc = 0;
 #pragma unroll
-                    for (int t = 0; t < 2; t++) {
-                        const int p = lane + 64 * t;
-                        if (p < 121) s += abs(a[t] - (IR[(ptrdiff_t)(yL + dyv[t]) * lv.pitch + xR + dxv[t]] - cR));
+                    for (int t = 0; t < 8; t++) {
+                        const int p = sub + 16 * t;
+                        if (p < 121) sacc += abs(a[t] - (IR[(ptrdiff_t)offv[t] + xR] - cR));
                     }
-                    vD[inc] = wave_sum_i(s);
+                    vD[inc] = group_sum_i(sacc);
                 }
                 int bestD = INT_MAX, bestinc = 0;
 #pragma unroll
@@ -206,7 +210,7 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
             }
         }
     }
-    if (lane == 0) {
+    if (sub == 0) {
         S.uRight[iL] = uR_out;
         S.depth[iL] = depth_out;
         S.sad[iL] = sad_out;
@@ -280,7 +284,7 @@ int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoPa
     hipLaunchKernelGGL(k_stereo_rows, dim3(nprob), dim3(1024), 0, s, d_probs, P);
     if (timed) tm->mark(5);
     if (maxNL > 0)
-        hipLaunchKernelGGL(k_stereo_match, dim3((maxNL + 3) / 4, nprob), dim3(256), 0, s, d_probs, P,
+        hipLaunchKernelGGL(k_stereo_match, dim3((maxNL + 15) / 16, nprob), dim3(256), 0, s, d_probs, P,
                            timed ? tm->counters() : nullptr);
     if (timed) tm->mark(6);
     int m = 1;

@@ -814,6 +814,15 @@ int orbgpu_unit_csum(const double* v, int n, double* out);
  * end touched, host bytes allocated, host end touched}; ORB_OK iff everything touched fits. */
 int orbgpu_unit_pnp_layout(int n, const int* N, const int* K, const int* minSet, long long* out4);
 int orbgpu_unit_ldlt_factor(int n, const double* S, double* out);
+/* Host only (no device): the BA structure of one optimisation level (csrc/ba_struct.cpp,
+ * initializeOptimization + buildIndexMapping + BlockSolver::buildStructure) packed into out:
+ * [nE nP nL nBlk nPair | poseKf[nP] | landPt[nL] | ePose[nE] | eLand[nE] | lpStart[nL+1] |
+ *  lpList | blkI[nBlk] | blkJ[nBlk] | blkStart[nBlk+1] | pairA[nPair] | pairB[nPair]];
+ * ORB_E_CAPACITY when cap (int32 entries) is too small, ORB_E_INVALID on a duplicate
+ * (pose, landmark) edge. */
+int orbgpu_unit_ba_struct(int nkf, int npt, int ne, const int32_t* edge_kf, const int32_t* edge_pt,
+                          const uint8_t* edge_level, const uint8_t* kf_fixed, const int32_t* kf_id,
+                          const int32_t* pt_id, int level, int32_t* out, long long cap);
 /* one wave's canonical 64-tree of v64[0..64) (cross-lane permlane/DPP path) */
 int orbgpu_unit_wave_tree(const double* v64, double* out);
 /* Test knob: the BA chi2 canonical sum keeps at most m2_max level-2 trees in LDS (default and
