@@ -5,7 +5,7 @@
 // scalar semantics (one-sided Jacobi SVD, SVBkSb), in the exact operation
 // order of the CPU oracle so GPU and oracle agree bit for bit:
 //   cvMulTransposed  -> M^T M accumulated row by row (no M is materialised)
-//   cvSVD / cvSolve(CV_SVD) / cvInvert(CV_SVD) -> jacobi_svd + backsubstitution
+//   cvSVD / cvSolve(CV_SVD) / cvInvert(CV_SVD) -> jacobi_t + backsubstitution
 // Correspondences are read through an accessor (point k -> world xyz, pixel uv),
 // so the 4-point hypotheses and the n-point Refine share one code path.
 #pragma once
@@ -17,29 +17,36 @@ namespace epnp {
 constexpr double kDblEps = 2.220446049250313e-16;
 constexpr double kDblMin = 2.2250738585072014e-308;
 
-// JacobiSVDImpl_<double> (OpenCV 3.2 lapack.cpp): At n x m (stride astep).
-__device__ __forceinline__ void jacobi_svd(double* At, int astep, double* W_out, double* Vt, int vstep, int m, int n, int n1) {
+// JacobiSVDImpl_<double> (OpenCV 3.2 lapack.cpp) for the static shapes of compute_pose (the
+// 12 x 12 M^T M, the 6 x n cvSolve systems, the 3 x 3 decompositions; n1 = N): every index is
+// static, so At, V and W live in registers instead of per-lane scratch memory.  WANTV false:
+// the caller asked for no V (cvSVD without a V output), whose rotations are then skipped --
+// V is written, never read, by the sweeps.  The descending sort swaps rows through selects
+// over the static candidates.
+template <int M, int N, bool WANTV>
+__device__ __forceinline__ void jacobi_t(double (&At)[N][M], double (&Wo)[N], double (&Vt)[N][N]) {
     const double eps = kDblEps * 10;
-    double W[12];
-    const int max_iter = m > 30 ? m : 30;
-    for (int i = 0; i < n; i++) {
+    double W[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
         double sd = 0;
-        for (int k = 0; k < m; k++) {
-            const double t = At[i * astep + k];
-            sd += t * t;
-        }
+#pragma unroll
+        for (int k = 0; k < M; k++) sd += At[i][k] * At[i][k];
         W[i] = sd;
-        for (int k = 0; k < n; k++) Vt[i * vstep + k] = 0;
-        Vt[i * vstep + i] = 1;
+        if (WANTV)
+#pragma unroll
+            for (int k = 0; k < N; k++) Vt[i][k] = k == i ? 1.0 : 0.0;
     }
+    const int max_iter = M > 30 ? M : 30;
     for (int iter = 0; iter < max_iter; iter++) {
         bool changed = false;
-        for (int i = 0; i < n - 1; i++)
-            for (int j = i + 1; j < n; j++) {
-                double* Ai = At + i * astep;
-                double* Aj = At + j * astep;
+#pragma unroll
+        for (int i = 0; i < N - 1; i++)
+#pragma unroll
+            for (int j = i + 1; j < N; j++) {
                 double a = W[i], p = 0, b = W[j];
-                for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
+#pragma unroll
+                for (int k = 0; k < M; k++) p += At[i][k] * At[j][k];
                 if (fabs(p) <= eps * sqrt(a * b)) continue;
                 p *= 2;
                 const double beta = a - b, gamma = sqrt(p * p + beta * beta);
@@ -53,121 +60,165 @@ __device__ __forceinline__ void jacobi_svd(double* At, int astep, double* W_out,
                     s = p / (gamma * c * 2);
                 }
                 a = b = 0;
-                for (int k = 0; k < m; k++) {
-                    const double t0 = c * Ai[k] + s * Aj[k];
-                    const double t1 = -s * Ai[k] + c * Aj[k];
-                    Ai[k] = t0;
-                    Aj[k] = t1;
+#pragma unroll
+                for (int k = 0; k < M; k++) {
+                    const double t0 = c * At[i][k] + s * At[j][k];
+                    const double t1 = -s * At[i][k] + c * At[j][k];
+                    At[i][k] = t0;
+                    At[j][k] = t1;
                     a += t0 * t0;
                     b += t1 * t1;
                 }
                 W[i] = a;
                 W[j] = b;
                 changed = true;
-                double* Vi = Vt + i * vstep;
-                double* Vj = Vt + j * vstep;
-                for (int k = 0; k < n; k++) {
-                    const double t0 = c * Vi[k] + s * Vj[k];
-                    const double t1 = -s * Vi[k] + c * Vj[k];
-                    Vi[k] = t0;
-                    Vj[k] = t1;
-                }
+                if (WANTV)
+#pragma unroll
+                    for (int k = 0; k < N; k++) {
+                        const double t0 = c * Vt[i][k] + s * Vt[j][k];
+                        const double t1 = -s * Vt[i][k] + c * Vt[j][k];
+                        Vt[i][k] = t0;
+                        Vt[j][k] = t1;
+                    }
             }
         if (!changed) break;
     }
-    for (int i = 0; i < n; i++) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
         double sd = 0;
-        for (int k = 0; k < m; k++) {
-            const double t = At[i * astep + k];
-            sd += t * t;
-        }
+#pragma unroll
+        for (int k = 0; k < M; k++) sd += At[i][k] * At[i][k];
         W[i] = sqrt(sd);
     }
-    for (int i = 0; i < n - 1; i++) {
+#pragma unroll
+    for (int i = 0; i < N - 1; i++) {
         int j = i;
-        for (int k = i + 1; k < n; k++)
-            if (W[j] < W[k]) j = k;
-        if (i != j) {
-            const double tw = W[i]; W[i] = W[j]; W[j] = tw;
-            for (int k = 0; k < m; k++) { const double t = At[i * astep + k]; At[i * astep + k] = At[j * astep + k]; At[j * astep + k] = t; }
-            for (int k = 0; k < n; k++) { const double t = Vt[i * vstep + k]; Vt[i * vstep + k] = Vt[j * vstep + k]; Vt[j * vstep + k] = t; }
+        double wj = W[i];
+#pragma unroll
+        for (int k = i + 1; k < N; k++)
+            if (wj < W[k]) {
+                j = k;
+                wj = W[k];
+            }
+#pragma unroll
+        for (int r = i + 1; r < N; r++) {
+            const bool sw = j == r;
+            const double tw = W[i];
+            W[i] = sw ? W[r] : W[i];
+            W[r] = sw ? tw : W[r];
+#pragma unroll
+            for (int k = 0; k < M; k++) {
+                const double t = At[i][k];
+                At[i][k] = sw ? At[r][k] : At[i][k];
+                At[r][k] = sw ? t : At[r][k];
+            }
+            if (WANTV)
+#pragma unroll
+                for (int k = 0; k < N; k++) {
+                    const double t = Vt[i][k];
+                    Vt[i][k] = sw ? Vt[r][k] : Vt[i][k];
+                    Vt[r][k] = sw ? t : Vt[r][k];
+                }
         }
     }
-    for (int i = 0; i < n; i++) W_out[i] = W[i];
+#pragma unroll
+    for (int i = 0; i < N; i++) Wo[i] = W[i];
     uint64_t rng = 0x12345678;
-    for (int i = 0; i < n1; i++) {
-        double sd = i < n ? W[i] : 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        double sd = W[i];
         for (int ii = 0; ii < 100 && sd <= kDblMin; ii++) {
-            const double val0 = 1. / m;
-            for (int k = 0; k < m; k++) {
+            const double val0 = 1. / M;
+#pragma unroll
+            for (int k = 0; k < M; k++) {
                 rng = (uint64_t)(unsigned)rng * 4164903690U + (unsigned)(rng >> 32);
-                At[i * astep + k] = ((unsigned)rng & 256) != 0 ? val0 : -val0;
+                At[i][k] = ((unsigned)rng & 256) != 0 ? val0 : -val0;
             }
             for (int it2 = 0; it2 < 2; it2++)
+#pragma unroll
                 for (int j = 0; j < i; j++) {
                     sd = 0;
-                    for (int k = 0; k < m; k++) sd += At[i * astep + k] * At[j * astep + k];
+#pragma unroll
+                    for (int k = 0; k < M; k++) sd += At[i][k] * At[j][k];
                     double asum = 0;
-                    for (int k = 0; k < m; k++) {
-                        const double t = At[i * astep + k] - sd * At[j * astep + k];
-                        At[i * astep + k] = t;
+#pragma unroll
+                    for (int k = 0; k < M; k++) {
+                        const double t = At[i][k] - sd * At[j][k];
+                        At[i][k] = t;
                         asum += fabs(t);
                     }
                     asum = asum > eps * 100 ? 1 / asum : 0;
-                    for (int k = 0; k < m; k++) At[i * astep + k] *= asum;
+#pragma unroll
+                    for (int k = 0; k < M; k++) At[i][k] *= asum;
                 }
             sd = 0;
-            for (int k = 0; k < m; k++) {
-                const double t = At[i * astep + k];
-                sd += t * t;
-            }
+#pragma unroll
+            for (int k = 0; k < M; k++) sd += At[i][k] * At[i][k];
             sd = sqrt(sd);
         }
         const double scale = 1 / sd;
-        for (int k = 0; k < m; k++) At[i * astep + k] *= scale;
+#pragma unroll
+        for (int k = 0; k < M; k++) At[i][k] *= scale;
     }
 }
 
-// SVD::compute(A m x n, m >= n): w, Ut (n x m), Vt (n x n).  A is consumed as At scratch.
-__device__ __forceinline__ void svd(const double* A, int m, int n, double* w, double* Ut, double* Vt) {
-    for (int i = 0; i < n; i++)
-        for (int k = 0; k < m; k++) Ut[i * m + k] = A[k * n + i];
-    jacobi_svd(Ut, m, w, Vt, n, m, n, n);
+// svd() for a static M x N (row-major A): Ut = A^T decomposed in registers
+template <int M, int N, bool WANTV>
+__device__ __forceinline__ void svd_t(const double* A, double (&w)[N], double (&Ut)[N][M], double (&Vt)[N][N]) {
+#pragma unroll
+    for (int i = 0; i < N; i++)
+#pragma unroll
+        for (int k = 0; k < M; k++) Ut[i][k] = A[k * N + i];
+    jacobi_t<M, N, WANTV>(Ut, w, Vt);
 }
 
-__device__ __forceinline__ void svd_solve(const double* A, int m, int n, const double* b, double* x) {
-    double w[6], Ut[36], Vt[36];
-    svd(A, m, n, w, Ut, Vt);
-    const int nm = m < n ? m : n;
+// cvSolve(A, b, x, CV_SVD) for a static M x N A (the find_betas_approx_* systems)
+template <int M, int N>
+__device__ __forceinline__ void svd_solve_t(const double* A, const double* b, double* x) {
+    double w[N], Ut[N][M], Vt[N][N];
+    svd_t<M, N, true>(A, w, Ut, Vt);
+    constexpr int nm = M < N ? M : N;
     double threshold = 0;
-    for (int j = 0; j < n; j++) x[j] = 0;
+#pragma unroll
+    for (int j = 0; j < N; j++) x[j] = 0;
+#pragma unroll
     for (int i = 0; i < nm; i++) threshold += w[i];
     threshold *= kDblEps * 2;
+#pragma unroll
     for (int i = 0; i < nm; i++) {
         double wi = w[i];
         if (fabs(wi) <= threshold) continue;
         wi = 1 / wi;
         double s = 0;
-        for (int j = 0; j < m; j++) s += Ut[i * m + j] * b[j];
+#pragma unroll
+        for (int j = 0; j < M; j++) s += Ut[i][j] * b[j];
         s *= wi;
-        for (int j = 0; j < n; j++) x[j] = x[j] + s * Vt[i * n + j];
+#pragma unroll
+        for (int j = 0; j < N; j++) x[j] = x[j] + s * Vt[i][j];
     }
 }
 
+
 __device__ __forceinline__ void svd_invert3(const double* A, double* X) {
-    double w[3], Ut[9], Vt[9], buf[3];
-    svd(A, 3, 3, w, Ut, Vt);
+    double w[3], Ut[3][3], Vt[3][3], buf[3];
+    svd_t<3, 3, true>(A, w, Ut, Vt);
     double threshold = 0;
+#pragma unroll
     for (int i = 0; i < 9; i++) X[i] = 0;
+#pragma unroll
     for (int i = 0; i < 3; i++) threshold += w[i];
     threshold *= kDblEps * 2;
+#pragma unroll
     for (int i = 0; i < 3; i++) {
         double wi = w[i];
         if (fabs(wi) <= threshold) continue;
         wi = 1 / wi;
-        for (int j = 0; j < 3; j++) buf[j] = Ut[i * 3 + j] * wi;
+#pragma unroll
+        for (int j = 0; j < 3; j++) buf[j] = Ut[i][j] * wi;
+#pragma unroll
         for (int r = 0; r < 3; r++)
-            for (int c = 0; c < 3; c++) X[r * 3 + c] += Vt[i * 3 + r] * buf[c];
+#pragma unroll
+            for (int c = 0; c < 3; c++) X[r * 3 + c] += Vt[i][r] * buf[c];
     }
 }
 
@@ -291,7 +342,7 @@ struct Solver {
             for (int j = 0; j < 3; j++) cws[0][j] += p[j];
         }
         for (int j = 0; j < 3; j++) cws[0][j] /= n;
-        double pw0tpw0[9], dc[3], uct[9], vt[9];
+        double pw0tpw0[9], dc[3], uct[3][3], vt_unused[3][3];
         for (int a = 0; a < 3; a++)
             for (int b = a; b < 3; b++) {
                 double s = 0;
@@ -303,10 +354,10 @@ struct Solver {
                 pw0tpw0[a * 3 + b] = s;
                 pw0tpw0[b * 3 + a] = s;
             }
-        svd(pw0tpw0, 3, 3, dc, uct, vt);
+        svd_t<3, 3, false>(pw0tpw0, dc, uct, vt_unused);
         for (int i = 1; i < 4; i++) {
             const double k = sqrt(dc[i - 1] / n);
-            for (int j = 0; j < 3; j++) cws[i][j] = cws[0][j] + k * uct[3 * (i - 1) + j];
+            for (int j = 0; j < 3; j++) cws[i][j] = cws[0][j] + k * uct[i - 1][j];
         }
     }
 
@@ -317,14 +368,19 @@ struct Solver {
         svd_invert3(cc, ci);
     }
 
-    // cvMulTransposed(M, MtM, 1): rows of M in order 2i, 2i+1, accumulated in place.
-    __device__ __forceinline__ void mtm(double* out) const {
-        for (int i = 0; i < 144; i++) out[i] = 0;
+    // cvMulTransposed(M, MtM, 1): rows of M in order 2i, 2i+1, accumulated in place.  The 78
+    // upper-triangle sums stay in registers across the points (static indices) and are written
+    // once.
+    __device__ __forceinline__ void mtm(double (&out)[12][12]) const {
+        double acc[78];
+#pragma unroll
+        for (int q = 0; q < 78; q++) acc[q] = 0;
         for (int i = 0; i < n; i++) {
             double a[4], u, v;
             alphas(i, a);
             P.uv(i, u, v);
             double r1[12], r2[12];
+#pragma unroll
             for (int k = 0; k < 4; k++) {
                 r1[3 * k] = a[k] * fu;
                 r1[3 * k + 1] = 0.0;
@@ -333,13 +389,22 @@ struct Solver {
                 r2[3 * k + 1] = a[k] * fv;
                 r2[3 * k + 2] = a[k] * (vc - v);
             }
-            for (int r = 0; r < 12; r++)
-                for (int c = r; c < 12; c++) out[r * 12 + c] += r1[r] * r1[c];
-            for (int r = 0; r < 12; r++)
-                for (int c = r; c < 12; c++) out[r * 12 + c] += r2[r] * r2[c];
+#pragma unroll
+            for (int r = 0, q = 0; r < 12; r++)
+#pragma unroll
+                for (int c = r; c < 12; c++, q++) acc[q] += r1[r] * r1[c];
+#pragma unroll
+            for (int r = 0, q = 0; r < 12; r++)
+#pragma unroll
+                for (int c = r; c < 12; c++, q++) acc[q] += r2[r] * r2[c];
         }
-        for (int r = 0; r < 12; r++)
-            for (int c = 0; c < r; c++) out[r * 12 + c] = out[c * 12 + r];
+#pragma unroll
+        for (int r = 0, q = 0; r < 12; r++)
+#pragma unroll
+            for (int c = r; c < 12; c++, q++) {
+                out[r][c] = acc[q];
+                out[c][r] = acc[q];
+            }
     }
 
     __device__ __forceinline__ double reprojection_error(const double R[3][3], const double t[3]) const {
@@ -373,7 +438,7 @@ struct Solver {
             pc0[j] /= n;
             pw0[j] /= n;
         }
-        double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, d[3], ut[9], vt[9];
+        double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, d[3], ut[3][3], vt[3][3];
         for (int i = 0; i < n; i++) {
             double pcv[3], pw[3];
             pc(i, pcv);
@@ -384,12 +449,12 @@ struct Solver {
                 abt[3 * j + 2] += (pcv[j] - pc0[j]) * (pw[2] - pw0[2]);
             }
         }
-        svd(abt, 3, 3, d, ut, vt);
+        svd_t<3, 3, true>(abt, d, ut, vt);
         double U[9], V[9];
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
-                U[3 * i + j] = ut[3 * j + i];
-                V[3 * i + j] = vt[3 * j + i];
+                U[3 * i + j] = ut[j][i];
+                V[3 * i + j] = vt[j][i];
             }
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) R[i][j] = dot3(U + 3 * i, V + 3 * j);
@@ -405,10 +470,11 @@ struct Solver {
         t[2] = pc0[2] - dot3(R[2], pw0);
     }
 
-    __device__ __forceinline__ double compute_R_and_t(const double* ut, const double* betas, double R[3][3], double t[3]) {
+    // u4: rows 8..11 of Ut (the four smallest singular vectors of MtM), u4 + 12 (3 - i) = row 11 - i
+    __device__ __forceinline__ double compute_R_and_t(const double* u4, const double* betas, double R[3][3], double t[3]) {
         for (int i = 0; i < 4; i++) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
         for (int i = 0; i < 4; i++) {
-            const double* v = ut + 12 * (11 - i);
+            const double* v = u4 + 12 * (3 - i);
             for (int j = 0; j < 4; j++)
                 for (int k = 0; k < 3; k++) ccs[j][k] += betas[i] * v[3 * j + k];
         }
@@ -426,12 +492,20 @@ struct Solver {
     __device__ __forceinline__ double compute_pose(double R[3][3], double t[3]) {
         choose_control_points();
         barycentric();
-        double m[144], d[12], ut[144], vt[144];
-        mtm(m);
-        svd(m, 12, 12, d, ut, vt);
+        // cvSVD(MtM, D, Ut, 0, CV_SVD_MODIFY_A | CV_SVD_U_T) (PnPsolver.cc:492-493): MtM is
+        // symmetric, so its transpose is itself and the Jacobi sweeps run on it in place; V is
+        // not requested
+        // (the whole decomposition in registers; only the 4 rows compute_pose reads are kept)
+        double At[12][12], d[12], v_unused[12][12], u4[48];
+        mtm(At);
+        jacobi_t<12, 12, false>(At, d, v_unused);
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int k = 0; k < 12; k++) u4[12 * r + k] = At[8 + r][k];
         double L[60], rho[6];
         {
-            const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+            const double* v[4] = {u4 + 36, u4 + 24, u4 + 12, u4};
             double dv[4][6][3];
             for (int i = 0; i < 4; i++) {
                 int a = 0, b = 1;
@@ -469,7 +543,7 @@ struct Solver {
             for (int i = 0; i < 6; i++) {
                 l[4 * i] = L[10 * i]; l[4 * i + 1] = L[10 * i + 1]; l[4 * i + 2] = L[10 * i + 3]; l[4 * i + 3] = L[10 * i + 6];
             }
-            svd_solve(l, 6, 4, rho, b4);
+            svd_solve_t<6, 4>(l, rho, b4);
             double* be = Betas[1];
             if (b4[0] < 0) {
                 be[0] = sqrt(-b4[0]); be[1] = -b4[1] / be[0]; be[2] = -b4[2] / be[0]; be[3] = -b4[3] / be[0];
@@ -478,11 +552,11 @@ struct Solver {
             }
         }
         gauss_newton(L, rho, Betas[1]);
-        rep[1] = compute_R_and_t(ut, Betas[1], Rs[1], ts[1]);
+        rep[1] = compute_R_and_t(u4, Betas[1], Rs[1], ts[1]);
         {  // find_betas_approx_2
             double l[18], b3[3];
             for (int i = 0; i < 6; i++) { l[3 * i] = L[10 * i]; l[3 * i + 1] = L[10 * i + 1]; l[3 * i + 2] = L[10 * i + 2]; }
-            svd_solve(l, 6, 3, rho, b3);
+            svd_solve_t<6, 3>(l, rho, b3);
             double* be = Betas[2];
             if (b3[0] < 0) {
                 be[0] = sqrt(-b3[0]);
@@ -496,12 +570,12 @@ struct Solver {
             be[3] = 0.0;
         }
         gauss_newton(L, rho, Betas[2]);
-        rep[2] = compute_R_and_t(ut, Betas[2], Rs[2], ts[2]);
+        rep[2] = compute_R_and_t(u4, Betas[2], Rs[2], ts[2]);
         {  // find_betas_approx_3
             double l[30], b5[5];
             for (int i = 0; i < 6; i++)
                 for (int j = 0; j < 5; j++) l[5 * i + j] = L[10 * i + j];
-            svd_solve(l, 6, 5, rho, b5);
+            svd_solve_t<6, 5>(l, rho, b5);
             double* be = Betas[3];
             if (b5[0] < 0) {
                 be[0] = sqrt(-b5[0]);
@@ -515,7 +589,7 @@ struct Solver {
             be[3] = 0.0;
         }
         gauss_newton(L, rho, Betas[3]);
-        rep[3] = compute_R_and_t(ut, Betas[3], Rs[3], ts[3]);
+        rep[3] = compute_R_and_t(u4, Betas[3], Rs[3], ts[3]);
         int N = 1;
         if (rep[2] < rep[1]) N = 2;
         if (rep[3] < rep[N]) N = 3;
