@@ -23,9 +23,10 @@
 //   update  one workgroup per target tile (I, J) of the level's nodes that a DESCENDANT tile
 //           row K touches: A(I, J) -= sum_K L(I, K) U(K, J), K ascending (left-looking: reads
 //           finished descendant tiles only, writes a tile owned by this node: no races);
-//   factor  one 512-thread workgroup per node walks its own panels right-looking (diagonal
-//           tile, U/LT row tiles, trailing updates of its own rows only), then solves its rows
-//           of L y = b;
+//   factor  the level's nodes walk their own panels right-looking in lock step: per panel step
+//           three launches over every node of the level (diagonal tiles, the panel rows' U/LT
+//           tiles, the trailing updates of the nodes' own rows), a workgroup per tile; then
+//           one wave per node solves its rows of L y = b;
 // then the backward solve runs the levels top-down (one wave per node).  Nodes of one level
 // share no tile, so their workgroups run concurrently; the descendants' updates of an
 // ancestor tile arrive in ascending K, i.e. in pivot order, as in the sequential sweep.
@@ -44,9 +45,7 @@ namespace orbgpu {
 
 constexpr int LT = kTile;        // tile edge
 constexpr int LP = LT + 1;       // LDS row pitch (doubles) of the diagonal L
-constexpr int kSpThreads = 512;  // 8 waves
 constexpr int kMaxRow = 2048;    // tiles per panel row
-constexpr size_t kSpLds = sizeof(double) * (2 * 2 * LT * LT + LT) + sizeof(int) * (kMaxRow + 16);
 constexpr int kNdLeaf = 32;      // nested-dissection leaf size (poses)
 
 struct SpDev {
@@ -68,6 +67,9 @@ struct SpDev {
     const int* levNodes;  // node ids by level
     const int4* tgts;     // update targets by level: (slot(I, J), I, J, first K pair)
     const int4* kps;      // (slot(K, I), slot(K, J), K, 0), per target in ascending K
+    const int* stepP;     // panel steps: the panels of (level, step), see k_ldlt_pdiag
+    const int2* rowJobs;  // (panel, index in its row) of each U tile of a step
+    const int2* pairJobs; // (panel, pair index) of each trailing target of a step
     uint8_t* lnz;
     double* y;            // tile space
     double* xs;           // tile space
@@ -155,174 +157,155 @@ __global__ void __launch_bounds__(256) k_ldlt_update(SpDev S, int t0) {
         }
 }
 
-// One workgroup per node of a level: the node's panels right-looking (trailing updates inside
-// the node), then its rows of L y = b (wave 0).
-__global__ void __launch_bounds__(kSpThreads) k_ldlt_factor(SpDev S, int n0, const double* __restrict__ b) {
-    // static LDS: addresses fold into the ds_read offsets (a dynamic base is a relocation the
-    // compiler hoists into one SGPR per address)
-    __shared__ double sm[kSpLds / sizeof(double)];
-    double* Ls = sm;                       // [k][i] = L[i][k] of the diagonal tile (aliases the staging)
-    double* dsh = sm + 2 * 2 * LT * LT;    // d_k of the panel
-    int* flagS = (int*)(dsh + LT);         // L-nonzero flag per chunk of the panel row
-    int* failS = flagS + kMaxRow;
-    const int tid0 = threadIdx.x, lane0 = tid0 & 63, w = tid0 >> 6;
-    const int node = S.levNodes[n0 + blockIdx.x];
-    const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
-    if (tid0 == 0) *failS = *(volatile int*)S.fail;
-    __syncthreads();
-    if (*failS) return;
-    ORBGPU_PROF_START;
-    for (int p = T0; p < T1; p++) {
-        // opaque per panel: keeps LICM from hoisting every lane mask and lane address of the
-        // unrolled loops out of the panel loop (it spilled them)
-        int lane = lane0, tid = tid0;
-        asm volatile("" : "+v"(lane), "+v"(tid));
-        const int pw = S.th[p];
-        const int rs = S.rowStart[p], m = S.rowStart[p + 1] - rs;
-        // ---- diagonal tile (wave 0)
-        if (w == 0) {
-            // tiles are zero outside the system (padding rows / columns) and below the diagonal
-            const __amdgpu_buffer_rsrc_t Ud = tile_rsrc(S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT));
-            const int vo = lane * 8;
-            double col[LT];
+// A level's nodes factor their own panels right-looking, panel step by panel step: step s
+// takes panel T0 + s of every node of the level that has one, in three launches (diagonal
+// tile, the panel row's U / L^T tiles, the trailing updates inside the nodes), so every tile
+// of a step is its own workgroup.  Then k_ldlt_pfwd solves the level's rows of L y = b.
+
+// Diagonal tile of each panel of the step: one wave per panel, lane = column.  On exit the tile
+// holds U (d on the diagonal) in its upper triangle and L strictly below.
+__global__ void __launch_bounds__(64) k_ldlt_pdiag(SpDev S, int j0) {
+    __shared__ double Ls[LT * LP];
+    __shared__ double dsh[LT];
+    if (*(volatile int*)S.fail) return;
+    const int p = S.stepP[j0 + blockIdx.x];
+    const int lane = threadIdx.x;
+    const int pw = S.th[p];
+    const __amdgpu_buffer_rsrc_t Ud = tile_rsrc(S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT));
+    const int vo = lane * 8;
+    double col[LT];
 #pragma unroll
-            for (int r = 0; r < LT; r++) col[r] = tld(Ud, vo, r * LT * 8);
-            bool bad = false;
+    for (int r = 0; r < LT; r++) col[r] = tld(Ud, vo, r * LT * 8);
+    bool bad = false;
 #pragma unroll
-            for (int k = 0; k < LT; k++) {
-                if (k < pw && !bad) {
-                    if (lane == k) dsh[k] = col[k];
-                    __builtin_amdgcn_wave_barrier();
-                    const double d = dsh[k];
-                    if (d == 0.0) {
-                        bad = true;
-                    } else {
-                        Ls[k * LP + lane] = lane > k ? col[k] / d : 0.0;
-                        __builtin_amdgcn_wave_barrier();
-                        const double ck = col[k];
-#pragma unroll
-                        for (int i = k + 1; i < LT; i++) col[i] -= Ls[k * LP + i] * ck;
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                }
-            }
-            // padding pivots: L = 0, d = 1, so the chunk pass needs no predicates
-            for (int k = pw; k < LT; k++) {
-                Ls[k * LP + lane] = 0.0;
-                if (lane == 0) dsh[k] = 1.0;
-            }
-            if (bad) {
-                if (lane == 0) {
-                    *failS = 1;
-                    *S.fail = 1;
-                }
+    for (int k = 0; k < LT; k++) {
+        if (k < pw && !bad) {
+            if (lane == k) dsh[k] = col[k];
+            __builtin_amdgcn_wave_barrier();
+            const double d = dsh[k];
+            if (d == 0.0) {
+                bad = true;
             } else {
+                Ls[k * LP + lane] = lane > k ? col[k] / d : 0.0;
+                __builtin_amdgcn_wave_barrier();
+                const double ck = col[k];
 #pragma unroll
-                for (int r = 0; r < LT; r++)
-                    if (r < pw && lane < pw) tst(Ud, lane >= r ? col[r] : Ls[lane * LP + r], vo, r * LT * 8);
-            }
-        }
-        __syncthreads();
-        ORBGPU_PROF_MARK(16);
-        if (*failS) return;
-        // ---- U tiles (p, J > p) of the panel row: one wave per tile, lane = column
-        const int wu = __builtin_amdgcn_readfirstlane(w);
-        for (int t = wu; t < m; t += kSpThreads / 64) {
-            const int sl = S.rowSlot[rs + t];
-            const __amdgpu_buffer_rsrc_t Ut = tile_rsrc(S.U + (size_t)sl * (LT * LT));
-            const __amdgpu_buffer_rsrc_t Lo = tile_rsrc(S.LT + (size_t)sl * (LT * LT));
-            const int vo = lane * 8;
-            double c[LT];
-#pragma unroll
-            for (int r = 0; r < LT; r++) c[r] = tld(Ut, vo, r * LT * 8);   // zero outside the system
-            // per element the updates arrive in k order (the oracle's); the scheduling barrier
-            // keeps the compiler from hoisting every pivot's 63 broadcast reads at once
-#pragma unroll
-            for (int k = 0; k < LT - 1; k++) {
-                const double ck = c[k];
-#pragma unroll
-                for (int i = k + 1; i < LT; i++) c[i] -= Ls[k * LP + i] * ck;   // L[i][k], wave-uniform address
+                for (int i = k + 1; i < LT; i++) col[i] -= Ls[k * LP + i] * ck;
                 __builtin_amdgcn_sched_barrier(0);
             }
-            bool nz = false;
-#pragma unroll
-            for (int r = 0; r < LT; r++) {
-                tst(Ut, c[r], vo, r * LT * 8);
-                nz |= c[r] != 0.0;
-                tst(Lo, c[r] / dsh[r], vo, r * LT * 8);
-            }
-            // flag = some eliminated U[k][j] != 0, a superset of "some l != 0": skipping on it is exact
-            const bool any = __any(nz);
-            if (lane == 0) {
-                flagS[t] = any ? 1 : 0;
-                S.lnz[sl] = any ? 1 : 0;
-            }
         }
-        __syncthreads();
-        ORBGPU_PROF_MARK(17);
-        // ---- trailing update inside the node: A(I, J) -= L(I, p) U(p, J)
-        const int ps = S.pairStart[p], np = S.pairStart[p + 1] - ps;
-        const int g = tid >> 8, gt = tid & 255, ty = gt >> 4, tx = gt & 15;
-        double* Lg = sm + g * (2 * LT * LT);   // [k][i] = L[I0 + i][p0 + k]
-        double* Ug = Lg + LT * LT;             // [k][j] = U[p0 + k][J0 + j]
-        for (int q0 = 0; q0 < np; q0 += 2) {
-            const int q = q0 + g;
-            int4 pr = make_int4(0, 0, 0, 0);
-            bool act = false;
-            if (q < np) {
-                pr = S.pairs[ps + q];
-                act = flagS[pr.x] && flagS[pr.y];
-            }
-            if (act) {
-                const double2* srcL = (const double2*)(S.LT + (size_t)S.rowSlot[rs + pr.x] * (LT * LT));
-                const double2* srcU = (const double2*)(S.U + (size_t)S.rowSlot[rs + pr.y] * (LT * LT));
-                double2* dL = (double2*)Lg;
-                double2* dU = (double2*)Ug;
-#pragma unroll
-                for (int u = 0; u < (LT * LT / 2) / 256; u++) {
-                    dL[gt + 256 * u] = srcL[gt + 256 * u];
-                    dU[gt + 256 * u] = srcU[gt + 256 * u];
-                }
-            }
-            __syncthreads();
-            if (act) {
-                const int I = S.rowJ[rs + pr.x], J = S.rowJ[rs + pr.y];
-                const int ih = S.th[I], jw = S.th[J];
-                double* T = S.U + (size_t)pr.z * (LT * LT);
-                double acc[4][4];
-#pragma unroll
-                for (int a = 0; a < 4; a++)
-#pragma unroll
-                    for (int bb = 0; bb < 4; bb++) {
-                        const int i = ty + 16 * a, j = tx + 16 * bb;
-                        acc[a][bb] = (i < ih && j < jw) ? T[i * LT + j] : 0.0;
-                    }
-                for (int k = 0; k < pw; k++) {
-                    double l[4], u[4];
-#pragma unroll
-                    for (int a = 0; a < 4; a++) l[a] = Lg[k * LT + ty + 16 * a];
-#pragma unroll
-                    for (int bb = 0; bb < 4; bb++) u[bb] = Ug[k * LT + tx + 16 * bb];
-#pragma unroll
-                    for (int a = 0; a < 4; a++)
-#pragma unroll
-                        for (int bb = 0; bb < 4; bb++) acc[a][bb] -= l[a] * u[bb];
-                }
-#pragma unroll
-                for (int a = 0; a < 4; a++)
-#pragma unroll
-                    for (int bb = 0; bb < 4; bb++) {
-                        const int i = ty + 16 * a, j = tx + 16 * bb;
-                        if (i < ih && j < jw && (I != J || i <= j)) T[i * LT + j] = acc[a][bb];
-                    }
-            }
-            __syncthreads();
-        }
-        ORBGPU_PROF_MARK(18);
     }
-    // ---- L y = b on the node's rows (wave 0; lane = row): descendants' y are final
-    if (w != 0) return;
-    const int lane = lane0;
+    if (bad) {
+        if (lane == 0) *S.fail = 1;
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < LT; r++)
+        if (r < pw && lane < pw) tst(Ud, lane >= r ? col[r] : Ls[lane * LP + r], vo, r * LT * 8);
+}
+
+// U tiles (p, J > p) of each panel row of the step: one wave per tile, lane = column; the
+// panel's L and d come from its factored diagonal tile (padding pivots: L = 0, d = 1).
+__global__ void __launch_bounds__(64) k_ldlt_prow(SpDev S, int j0) {
+    __shared__ double Ls[LT * LP];   // [k][i] = L[i][k]
+    __shared__ double dsh[LT];
+    if (*(volatile int*)S.fail) return;
+    const int2 job = S.rowJobs[j0 + blockIdx.x];   // (panel, index in its row)
+    const int p = job.x, lane = threadIdx.x;
+    const int pw = S.th[p];
+    const double* D = S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT);
+#pragma unroll 4
+    for (int k = 0; k < LT; k++) Ls[k * LP + lane] = (k < pw && lane > k) ? D[lane * LT + k] : 0.0;
+    dsh[lane] = lane < pw ? D[lane * LT + lane] : 1.0;
+    __syncthreads();
+    const int e = S.rowStart[p] + job.y;
+    const int sl = S.rowSlot[e];
+    const __amdgpu_buffer_rsrc_t Ut = tile_rsrc(S.U + (size_t)sl * (LT * LT));
+    const __amdgpu_buffer_rsrc_t Lo = tile_rsrc(S.LT + (size_t)sl * (LT * LT));
+    const int vo = lane * 8;
+    double c[LT];
+#pragma unroll
+    for (int r = 0; r < LT; r++) c[r] = tld(Ut, vo, r * LT * 8);   // zero outside the system
+    // per element the updates arrive in k order (the oracle's); the scheduling barrier keeps the
+    // compiler from hoisting every pivot's 63 broadcast reads at once
+#pragma unroll
+    for (int k = 0; k < LT - 1; k++) {
+        const double ck = c[k];
+#pragma unroll
+        for (int i = k + 1; i < LT; i++) c[i] -= Ls[k * LP + i] * ck;   // L[i][k], wave-uniform address
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    bool nz = false;
+#pragma unroll
+    for (int r = 0; r < LT; r++) {
+        tst(Ut, c[r], vo, r * LT * 8);
+        nz |= c[r] != 0.0;
+        tst(Lo, c[r] / dsh[r], vo, r * LT * 8);
+    }
+    // flag = some eliminated U[k][j] != 0, a superset of "some l != 0": skipping on it is exact
+    const bool any = __any(nz);
+    if (lane == 0) S.lnz[sl] = any ? 1 : 0;
+}
+
+// Trailing updates inside the nodes: A(I, J) -= L(I, p) U(p, J), one 256-thread workgroup per
+// target of the step (4 x 4 register micro-tiles, both operand tiles staged in LDS).
+__global__ void __launch_bounds__(256) k_ldlt_ptrail(SpDev S, int j0) {
+    __shared__ double Lg[LT * LT];   // [k][i] = L[I0 + i][p0 + k]
+    __shared__ double Ug[LT * LT];   // [k][j] = U[p0 + k][J0 + j]
+    if (*(volatile int*)S.fail) return;
+    const int2 job = S.pairJobs[j0 + blockIdx.x];   // (panel, pair index)
+    const int p = job.x;
+    const int rs = S.rowStart[p];
+    const int4 pr = S.pairs[S.pairStart[p] + job.y];
+    const int slI = S.rowSlot[rs + pr.x], slJ = S.rowSlot[rs + pr.y];
+    if (!S.lnz[slI] || !S.lnz[slJ]) return;   // block-uniform
+    const int gt = threadIdx.x, ty = gt >> 4, tx = gt & 15;
+    const double2* srcL = (const double2*)(S.LT + (size_t)slI * (LT * LT));
+    const double2* srcU = (const double2*)(S.U + (size_t)slJ * (LT * LT));
+#pragma unroll
+    for (int u = 0; u < (LT * LT / 2) / 256; u++) {
+        ((double2*)Lg)[gt + 256 * u] = srcL[gt + 256 * u];
+        ((double2*)Ug)[gt + 256 * u] = srcU[gt + 256 * u];
+    }
+    __syncthreads();
+    const int I = S.rowJ[rs + pr.x], J = S.rowJ[rs + pr.y];
+    const int ih = S.th[I], jw = S.th[J], pw = S.th[p];
+    double* T = S.U + (size_t)pr.z * (LT * LT);
+    double acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const int i = ty + 16 * a, j = tx + 16 * bb;
+            acc[a][bb] = (i < ih && j < jw) ? T[i * LT + j] : 0.0;
+        }
+    for (int k = 0; k < pw; k++) {
+        double l[4], u[4];
+#pragma unroll
+        for (int a = 0; a < 4; a++) l[a] = Lg[k * LT + ty + 16 * a];
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) u[bb] = Ug[k * LT + tx + 16 * bb];
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) acc[a][bb] -= l[a] * u[bb];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const int i = ty + 16 * a, j = tx + 16 * bb;
+            if (i < ih && j < jw && (I != J || i <= j)) T[i * LT + j] = acc[a][bb];
+        }
+}
+
+// L y = b on the rows of each node of a level (one wave per node; lane = row): the descendants'
+// y are final.
+__global__ void __launch_bounds__(64) k_ldlt_pfwd(SpDev S, int n0, const double* __restrict__ b) {
+    if (*(volatile int*)S.fail) return;
+    const int node = S.levNodes[n0 + blockIdx.x];
+    const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    const int lane = threadIdx.x;
     double Lr[LT];
     for (int I = T0; I < T1; I++) {
         const int I0 = I * LT, ih = S.th[I];
@@ -573,6 +556,32 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     }
     hLevNodeStart_[nLev_] = (int)levNodes.size();
     hLevTgtStart_[nLev_] = (int)tgts.size();
+    // panel steps of each level: step s = panel T0 + s of every node of the level that has one;
+    // per step the panels, the U tiles of their rows and the trailing targets inside the nodes
+    std::vector<int> stepP;
+    std::vector<int2> rowJobs, pairJobs;
+    hSteps_.clear();
+    hLevStepStart_.assign(nLev_ + 1, 0);
+    for (int h = 0; h < nLev_; h++) {
+        hLevStepStart_[h] = (int)hSteps_.size();
+        int maxT = 0;
+        for (int q = hLevNodeStart_[h]; q < hLevNodeStart_[h + 1]; q++)
+            maxT = std::max(maxT, nodeT[2 * levNodes[q] + 1] - nodeT[2 * levNodes[q]]);
+        for (int st = 0; st < maxT; st++) {
+            const int4 rec = make_int4((int)stepP.size(), (int)rowJobs.size(), (int)pairJobs.size(), 0);
+            for (int q = hLevNodeStart_[h]; q < hLevNodeStart_[h + 1]; q++) {
+                const int k = levNodes[q];
+                const int pnl = nodeT[2 * k] + st;
+                if (pnl >= nodeT[2 * k + 1]) continue;
+                stepP.push_back(pnl);
+                for (int e = 0; e < rowStart[pnl + 1] - rowStart[pnl]; e++) rowJobs.push_back(make_int2(pnl, e));
+                for (int e = 0; e < pairStart[pnl + 1] - pairStart[pnl]; e++) pairJobs.push_back(make_int2(pnl, e));
+            }
+            hSteps_.push_back(rec);
+        }
+    }
+    hLevStepStart_[nLev_] = (int)hSteps_.size();
+    hSteps_.push_back(make_int4((int)stepP.size(), (int)rowJobs.size(), (int)pairJobs.size(), 0));   // sentinel
     tgts.push_back(make_int4(0, 0, 0, (int)kps.size()));   // sentinel: the last target's K range end
     // every tile a kernel addresses exists (host check before any launch)
     for (int I = 0; I < nt; I++)
@@ -635,6 +644,18 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     offPairs_ = put4(pairs);
     offTgts_ = put4(tgts);
     offKps_ = put4(kps);
+    offStepP_ = put(stepP);
+    auto put2 = [&](const std::vector<int2>& v) {
+        while (L.size() % 2) L.push_back(0);
+        const size_t o = L.size();
+        for (const int2& q : v) {
+            L.push_back(q.x);
+            L.push_back(q.y);
+        }
+        return o;
+    };
+    offRowJobs_ = put2(rowJobs);
+    offPairJobs_ = put2(pairJobs);
     const size_t oLists = take(sizeof(int) * (L.size() + 64));
     if (off > cap_) {
         if (mem_) (void)hipFree(mem_);
@@ -687,6 +708,9 @@ int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
     d.levNodes = lists_ + offLevNodes_;
     d.tgts = (const int4*)(lists_ + offTgts_);
     d.kps = (const int4*)(lists_ + offKps_);
+    d.stepP = lists_ + offStepP_;
+    d.rowJobs = (const int2*)(lists_ + offRowJobs_);
+    d.pairJobs = (const int2*)(lists_ + offPairJobs_);
     d.lnz = lnz_;
     d.y = y_;
     d.xs = xs_;
@@ -695,8 +719,14 @@ int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
     for (int h = 0; h < nLev_; h++) {
         const int nt = hLevTgtStart_[h + 1] - hLevTgtStart_[h];
         if (nt > 0) hipLaunchKernelGGL(k_ldlt_update, dim3(nt), dim3(256), 0, s, d, hLevTgtStart_[h]);
+        for (int st = hLevStepStart_[h]; st < hLevStepStart_[h + 1]; st++) {
+            const int4 a = hSteps_[st], z = hSteps_[st + 1];
+            if (z.x > a.x) hipLaunchKernelGGL(k_ldlt_pdiag, dim3(z.x - a.x), dim3(64), 0, s, d, a.x);
+            if (z.y > a.y) hipLaunchKernelGGL(k_ldlt_prow, dim3(z.y - a.y), dim3(64), 0, s, d, a.y);
+            if (z.z > a.z) hipLaunchKernelGGL(k_ldlt_ptrail, dim3(z.z - a.z), dim3(256), 0, s, d, a.z);
+        }
         const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
-        hipLaunchKernelGGL(k_ldlt_factor, dim3(nn), dim3(kSpThreads), 0, s, d, hLevNodeStart_[h], b);
+        hipLaunchKernelGGL(k_ldlt_pfwd, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], b);
     }
     for (int h = nLev_ - 1; h >= 0; h--) {
         const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
