@@ -34,8 +34,8 @@ sys.path.insert(0, str(ROOT))
 METRIC = "tracking FPS + ORB matches/sec, KITTI-00 stereo; local-BA iter/sec"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md (spec)
 ROOFLINE_REPS = 5
-TRAFFIC_FILE = "traffic_r02.json"   # PMC FETCH_SIZE/WRITE_SIZE per launch (tools/pmc_traffic.py)
-VALU_FILE = "valu_r02.json"   # PMC SQ_INSTS_VALU per launch (tools/pmc_valu.py)
+TRAFFIC_FILE = "traffic_r03.json"   # PMC FETCH_SIZE/WRITE_SIZE per launch (tools/pmc_traffic.py)
+VALU_FILE = "valu_r03.json"   # PMC SQ_INSTS_VALU per launch (tools/pmc_valu.py)
 MATCH_PMC_FILE = "match_pmc_r03.json"   # matcher kernels: HBM bytes and VALU instructions per launch (tools/pmc_match.py)
 VALU_PEAK_GINST = 1228.8   # 256 CUs x 2 wave64 VALU issues per cycle x 2.4 GHz (MI355X_MICROARCH.md)
 W, H, NFEAT = 1241, 376, 1200

@@ -29,7 +29,7 @@ python3 tools/pmc_traffic.py "$(find "$OUT/FETCH_SIZE" -name '*counter_collectio
 python3 tools/pmc_valu.py "$(find "$OUT/SQ_INSTS_VALU" -name '*counter_collection.csv' | head -1)" "$OUT/valu.json" "$W" || exit 1
 # the box-side copy feeds this run's bench line; copy gpurun_out/<tag>/{traffic,valu}.json into
 # profiles/ afterwards so the committed files (read by the round-end bench) match the kernel
-cp "$OUT/traffic.json" profiles/traffic_r02.json && cp "$OUT/valu.json" profiles/valu_r02.json
+cp "$OUT/traffic.json" profiles/traffic_r03.json && cp "$OUT/valu.json" profiles/valu_r03.json
 echo "[gpu_check] bench" && date
 timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Matcher roofline evidence: three --pmc passes (FETCH_SIZE, WRITE_SIZE, SQ_INSTS_VALU) over the
-# bench's isolated passes, the per-kernel json (profiles/match_pmc_r02.json), then the bench line
+# bench's isolated passes, the per-kernel json (profiles/match_pmc_r03.json), then the bench line
 # and a kernel-stats profile of the same run.  usage: bash tools/gpu_match.sh <tag>
 set -o pipefail
 TAG=${1:-m}
