@@ -1354,44 +1354,31 @@ __device__ __forceinline__ void pose_pass(F f, int nA, const uint16_t* aE, const
                                           int mineIdx) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int m = (nA + 63) >> 6;
-    if (m <= nw) {
-        // one chunk per wave: active edge tid is this thread's for the whole round, kept in
-        // registers (loaded once per round) instead of re-read from HBM/L2 every pass
-        if (w < m) {
-            double v[K];
-            if ((int)threadIdx.x < nA) f(mine, mineIdx, v);
-            else
-#pragma unroll
-                for (int q = 0; q < K; q++) v[q] = 0.0;
-            if (nA == 1) {   // ora_csum keeps a single term untouched
-                if (lane == 0)
-#pragma unroll
-                    for (int q = 0; q < K; q++) cs[q][0] = v[q];
-            } else {
-                const double t = packed_trees<K>(v);
-                const int q = bitrev6(lane);
-                if (q < K) cs[q][w] = t;
-            }
-        }
-        __syncthreads();
-        pose_chunk_totals<K>(cs, nA > 0 ? m : 0, res);
-        __syncthreads();
-        return;
-    }
+    // chunk c = w is active edge tid: this thread's for the whole round, kept in registers
+    // (loaded once per round); later chunks are loaded one ahead.  One code path for every
+    // chunk count keeps a single inlined copy of f per call site (instruction-cache footprint)
     int c = w;
-    int a = c * 64 + lane;
-    int i = a < nA ? aE[a] : 0;
-    PoseEdgeD e = pose_edge_load(E, i, dM, dS);
+    int a = threadIdx.x;
+    int i = mineIdx;
+    PoseEdgeD e = mine;
     while (c < m) {
         const int cn = c + nw, an = cn * 64 + lane;
-        const int in = (cn < m && an < nA) ? aE[an] : 0;
-        const PoseEdgeD en = pose_edge_load(E, in, dM, dS);   // prefetch the next chunk's edge
+        int in = 0;
+        PoseEdgeD en = e;
+        if (cn < m) {   // prefetch the next chunk's edge
+            in = an < nA ? aE[an] : 0;
+            en = pose_edge_load(E, in, dM, dS);
+        }
         double v[K];
         if (a < nA) f(e, i, v);
         else
 #pragma unroll
             for (int q = 0; q < K; q++) v[q] = 0.0;
-        {   // nA > 64 here: every chunk is a full canonical tree
+        if (nA == 1) {   // ora_csum keeps a single term untouched
+            if (lane == 0)
+#pragma unroll
+                for (int q = 0; q < K; q++) cs[q][0] = v[q];
+        } else {
             const double t = packed_trees<K>(v);
             const int q = bitrev6(lane);
             if (q < K) cs[q][c] = t;
@@ -1702,95 +1689,79 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
                     }
                 }
             };
+            // One LM iteration is a system pass at T (skipped when the accepted trial of the
+            // previous iteration already evaluated it) followed by trials; a trial is the solves
+            // (waves 0..kPoseSpec) and ONE pass at candidate 0.  Both passes run through the same
+            // call site (sysPhase picks the pose), and the four solves through one: a single
+            // inlined copy of the 28-sum edge body keeps the LM loop's code within the
+            // instruction cache the workgroup shares with its neighbours.
             if (tid == 0) haveSys = 0;
             __syncthreads();
-            for (int k = 0; k < 10; k++) {
-                ORBGPU_PROF_MARK(0);
-                if (!haveSys) {
-                    ORBGPU_PROF_COUNT(8);
-                    // computeActiveErrors + activeRobustChi2 (entry 0) and buildSystem (entries
-                    // 1..27), one pass, canonical sums per entry
-                    pose_pass<28>([&](const PoseEdgeD& e, int i, double* v) { sys_terms(e, i, T, v); }, na, aE, E, dM,
-                                  dS, cs, red, myE, myIdx);
-                    if (tid < 28) {
-                        if (tid == 0) currentChi = iniChi = red[0];
-                        else if (tid < 22) Hs[tid - 1] = red[tid];
-                        else bs[tid - 22] = red[tid];
-                    }
-                } else if (tid < 28) {   // the system at this estimate came with its accepted trial
-                    if (tid == 0) currentChi = iniChi = sysN[0];
-                    else if (tid < 22) Hs[tid - 1] = sysN[tid];
-                    else bs[tid - 22] = sysN[tid];
-                }
-                ORBGPU_PROF_MARK(1);
-                __syncthreads();
-                if (tid == 0) {
-                    if (k == 0) {   // computeLambdaInit over the pose diagonal
-                        double mx = 0.;
-                        for (int j = 0; j < 6; j++) mx = fmax(fabs(Hs[DIAG21[j]]), mx);
-                        lambda = 1e-5 * mx;
-                        ni = 2;
-                        nBadLM = 0;
-                    }
-                    qmax = 0;
-                    haveSys = 0;
-                    Tbase = T;   // the estimate every trial of this iteration starts from
-                }
-                __syncthreads();
-                // Trials, up to four per round: candidate 0 solves at the current lambda (wave 0)
-                // while waves 1..kPoseSpec solve the systems of 1..kPoseSpec consecutive
-                // rejections (lambda *= ni; ni *= 2, the same H, b and starting estimate).  The
-                // pass of the first trial computes the whole system at candidate 0 (its robust
-                // chi2 is entry 0), so an accepted first trial hands the next iteration its
-                // system; a rejected one is followed by ONE pass for the speculative candidates,
-                // whose trials are then replayed in the reference's order.
-                do {
+            int kit = 0;            // LM iteration (uniform: every thread steps it alike)
+            bool sysPhase = true;   // the next pass evaluates the system at T
+            for (;;) {
+                if (!sysPhase) {
                     ORBGPU_PROF_MARK(10);
-                    if (tid < 64) {
-                        double xn[6];
-                        const bool ok2 = pose_solve_w(Hs, bs, lambda, xn);
-                        double xl[6];
-#pragma unroll
-                        for (int j = 0; j < 6; j++) xl[j] = ok2 ? xn[j] : xs[j];
-                        ORBGPU_PROF_MARK(5);
-                        ORBGPU_PROF_COUNT(9);
-                        Se3 d, r;
-                        se3_exp(xl, d);
-                        se3_mul(d, Tbase, r);
-                        if (tid == 0) {
-#pragma unroll
-                            for (int j = 0; j < 6; j++) xc[0][j] = xl[j];
-                            okc[0] = ok2 ? 1 : 0;
-                            Tc[0] = r;
-                        }
-                    } else if (tid < 64 * (kPoseSpec + 1)) {
-                        const int L = (tid >> 6) - 1;
+                    // Trials, up to four per round: candidate 0 solves at the current lambda
+                    // (wave 0) while waves 1..kPoseSpec solve the systems of 1..kPoseSpec
+                    // consecutive rejections (lambda *= ni; ni *= 2, the same H, b and starting
+                    // estimate).  The pass of the first trial computes the whole system at
+                    // candidate 0 (its robust chi2 is entry 0), so an accepted first trial hands
+                    // the next iteration its system; a rejected one is followed by ONE pass for
+                    // the speculative candidates, whose trials are then replayed in the
+                    // reference's order.
+                    if (tid < 64 * (kPoseSpec + 1)) {
+                        const int L = tid >> 6;   // 0: the current trial, L: L rejections ahead
                         double ls = lambda, ns = ni;
-                        for (int j = 0; j <= L; j++) {
+                        for (int j = 0; j < L; j++) {
                             ls *= ns;
                             ns *= 2;
                         }
                         double xn[6];
                         const bool ok = pose_solve_w(Hs, bs, ls, xn);
+                        ORBGPU_PROF_MARK(5);
+                        ORBGPU_PROF_COUNT(9);
+                        // candidate 0 steps from xs when the solve fails (its trial is then
+                        // rejected: tempChi = DBL_MAX); a failed speculative solve stays at Tbase
+                        double xl[6];
+#pragma unroll
+                        for (int j = 0; j < 6; j++) xl[j] = (ok || L > 0) ? xn[j] : xs[j];
                         Se3 r = Tbase;
-                        if (ok) {
+                        if (ok || L == 0) {
                             Se3 d;
-                            se3_exp(xn, d);
+                            se3_exp(xl, d);
                             se3_mul(d, Tbase, r);
                         }
                         if ((tid & 63) == 0) {
-                            Tc[L + 1] = r;
+                            Tc[L] = r;
 #pragma unroll
-                            for (int j = 0; j < 6; j++) xc[L + 1][j] = xn[j];
-                            okc[L + 1] = ok ? 1 : 0;
+                            for (int j = 0; j < 6; j++) xc[L][j] = xl[j];
+                            okc[L] = ok ? 1 : 0;
                         }
                     }
                     __syncthreads();
                     ORBGPU_PROF_MARK(2);
-                    // the trial at candidate 0: its robust chi2 and, with it, the system at that
-                    // estimate (the next iteration's whenever the trial is accepted)
-                    pose_pass<28>([&](const PoseEdgeD& e, int i, double* v) { sys_terms(e, i, Tc[0], v); }, na, aE, E, dM,
+                } else {
+                    ORBGPU_PROF_MARK(0);
+                    ORBGPU_PROF_COUNT(8);
+                }
+                // sysPhase: computeActiveErrors + activeRobustChi2 (entry 0) and buildSystem
+                // (entries 1..27) at T; a trial: its robust chi2 at candidate 0 and, with it, the
+                // system at that estimate (the next iteration's whenever the trial is accepted).
+                // Canonical sums per entry.
+                {
+                    const Se3& X = sysPhase ? T : Tc[0];
+                    pose_pass<28>([&](const PoseEdgeD& e, int i, double* v) { sys_terms(e, i, X, v); }, na, aE, E, dM,
                                   dS, cs, red, myE, myIdx);
+                }
+                if (sysPhase) {
+                    ORBGPU_PROF_MARK(1);
+                    if (tid < 28) {
+                        if (tid == 0) currentChi = iniChi = red[0];
+                        else if (tid < 22) Hs[tid - 1] = red[tid];
+                        else bs[tid - 22] = red[tid];
+                    }
+                } else {
                     ORBGPU_PROF_MARK(3);
                     // one trial of the reference's loop (optimization_algorithm_levenberg.cpp:100-149)
                     // at candidate j with robust chi2 tempChi; tid 0 only
@@ -1854,9 +1825,35 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
                         __syncthreads();
                     }
                     ORBGPU_PROF_MARK(4);
-                } while (again);
+                    if (again) continue;   // the next trial of this iteration
+                    __syncthreads();
+                    if (term || ++kit == 10) break;
+                    if (!haveSys) {   // the next iteration starts with a system pass at T
+                        sysPhase = true;
+                        continue;
+                    }
+                    if (tid < 28) {   // the system at this estimate came with its accepted trial
+                        if (tid == 0) currentChi = iniChi = sysN[0];
+                        else if (tid < 22) Hs[tid - 1] = sysN[tid];
+                        else bs[tid - 22] = sysN[tid];
+                    }
+                }
+                // iteration start (Hs, bs, currentChi = iniChi are the system at T)
                 __syncthreads();
-                if (term) break;
+                if (tid == 0) {
+                    if (kit == 0) {   // computeLambdaInit over the pose diagonal
+                        double mx = 0.;
+                        for (int j = 0; j < 6; j++) mx = fmax(fabs(Hs[DIAG21[j]]), mx);
+                        lambda = 1e-5 * mx;
+                        ni = 2;
+                        nBadLM = 0;
+                    }
+                    qmax = 0;
+                    haveSys = 0;
+                    Tbase = T;   // the estimate every trial of this iteration starts from
+                }
+                sysPhase = false;
+                __syncthreads();
             }
         }
         // classification (Optimizer.cc:376-426): outliers get their error recomputed

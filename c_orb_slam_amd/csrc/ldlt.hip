@@ -389,6 +389,166 @@ __global__ void __launch_bounds__(64) k_ldlt_backward(SpDev S, int n0, double* _
     }
 }
 
+// The sweeps with a workgroup per node and a wave per tile row of the node (tile I = T0 + w + W r),
+// the rows' accumulators in LDS.  Per row the subtractions keep the sequence of k_ldlt_pfwd /
+// k_ldlt_backward (forward: k ascending; backward: k descending): first every contribution from
+// outside the node (descendant tiles forward, ancestor tiles backward; their y / x are final),
+// all rows in parallel; then the node's own tiles one at a time -- the owner finishes tile K
+// with its diagonal tile, and after a barrier every row still waiting applies tile K's block.
+// Rows of off lanes (lane >= th) compute values nobody reads, so the chains carry no selects.
+constexpr int kSweepWaves = 8;
+constexpr int kSweepMaxTiles = 240;   // node tiles whose accumulators fit the LDS (120 KB)
+
+__device__ __forceinline__ double sweep_chain_fwd(double acc, const double* Lo, int lane, double yk, int kh) {
+    double Lr[LT];
+#pragma unroll
+    for (int k = 0; k < LT; k++) Lr[k] = Lo[k * LT + lane];   // L[I0 + lane][K0 + k]
+#pragma unroll
+    for (int k = 0; k < LT; k++)
+        if (k < kh) acc = acc - Lr[k] * rdlane(yk, k);
+    return acc;
+}
+__device__ __forceinline__ double sweep_chain_bwd(double acc, const double* Lo, int lane, double xk, int kh) {
+    double Lr[LT];
+#pragma unroll
+    for (int k = 0; k < LT; k++) Lr[k] = Lo[lane * LT + k];   // L[K0 + k][I0 + lane]
+#pragma unroll
+    for (int k = LT - 1; k >= 0; k--)
+        if (k < kh) acc = acc - Lr[k] * rdlane(xk, k);
+    return acc;
+}
+
+__global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_fwdn(SpDev S, int n0, const double* __restrict__ b) {
+    extern __shared__ double accs[];   // [tile - T0][lane]
+    __shared__ int cur[kSweepMaxTiles];   // the tile's first col-list entry inside the node
+    if (*(volatile int*)S.fail) return;
+    const int node = S.levNodes[n0 + blockIdx.x];
+    const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    const int W = blockDim.x >> 6, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int I = T0 + w; I < T1; I += W) {
+        const int I0 = I * LT;
+        double acc = lane < S.th[I] ? b[S.rowMap[I0 + lane]] : 0.0;
+        int e = S.colStart[I];
+        for (; e < S.colStart[I + 1]; e++) {
+            const int K = S.colK[e];
+            if (K >= T0) break;   // ascending K: the descendants come first
+            const int sl = S.colSlot[e];
+            if (!S.lnz[sl]) continue;
+            acc = sweep_chain_fwd(acc, S.LT + (size_t)sl * (LT * LT), lane, S.y[K * LT + lane], S.th[K]);
+        }
+        accs[(I - T0) * LT + lane] = acc;
+        if (lane == 0) cur[I - T0] = e;
+    }
+    __syncthreads();
+    for (int s = 0; s < T1 - T0; s++) {
+        const int K = T0 + s, K0 = K * LT, kh = S.th[K];
+        if (s % W == w) {   // the owner: diagonal tile, y_K final
+            const bool on = lane < kh;
+            double acc = accs[s * LT + lane];
+            const double* Ud = S.U + (size_t)S.slotOf[(size_t)K * S.nt + K] * (LT * LT);
+            double Lr[LT];
+#pragma unroll
+            for (int k = 0; k < LT; k++) Lr[k] = (on && k < lane) ? Ud[lane * LT + k] : 0.0;
+#pragma unroll
+            for (int k = 0; k < LT; k++) {
+                if (k < kh) {
+                    const double v = acc - Lr[k] * rdlane(acc, k);
+                    acc = lane > k ? v : acc;
+                }
+            }
+            acc = on ? acc : 0.0;
+            S.y[K0 + lane] = acc;
+            accs[s * LT + lane] = acc;
+        }
+        __syncthreads();
+        const double yk = accs[s * LT + lane];
+        for (int I = T0 + w; I < T1; I += W) {
+            if (I <= K) continue;
+            const int e = cur[I - T0];
+            if (e >= S.colStart[I + 1] || S.colK[e] != K) continue;   // no block (K, I)
+            if (lane == 0) cur[I - T0] = e + 1;
+            const int sl = S.colSlot[e];
+            if (!S.lnz[sl]) continue;
+            accs[(I - T0) * LT + lane] =
+                sweep_chain_fwd(accs[(I - T0) * LT + lane], S.LT + (size_t)sl * (LT * LT), lane, yk, kh);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_bwdn(SpDev S, int n0, double* __restrict__ x, double* scal,
+                                                                int first) {
+    extern __shared__ double accs[];
+    __shared__ int cur[kSweepMaxTiles];   // the tile's last row-list entry inside the node
+    const int lane = threadIdx.x & 63;
+    const int failed = *(volatile int*)S.fail;
+    if (first && blockIdx.x == 0 && threadIdx.x == 0) scal[3] = failed ? 0.0 : 1.0;
+    if (failed) return;
+    const int node = S.levNodes[n0 + blockIdx.x];
+    const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    const int W = blockDim.x >> 6, w = threadIdx.x >> 6;
+    for (int I = T0 + w; I < T1; I += W) {
+        const int I0 = I * LT;
+        const double* Ud = S.U + (size_t)S.slotOf[(size_t)I * S.nt + I] * (LT * LT);
+        double acc = lane < S.th[I] ? S.y[I0 + lane] / Ud[lane * LT + lane] : 0.0;
+        int e = S.rowStart[I + 1] - 1;
+        for (; e >= S.rowStart[I]; e--) {
+            const int J = S.rowJ[e];
+            if (J < T1) break;   // descending J: the ancestors come first
+            const int sl = S.rowSlot[e];
+            if (!S.lnz[sl]) continue;
+            acc = sweep_chain_bwd(acc, S.LT + (size_t)sl * (LT * LT), lane, lane < S.th[J] ? S.xs[J * LT + lane] : 0.0,
+                                  S.th[J]);
+        }
+        accs[(I - T0) * LT + lane] = acc;
+        if (lane == 0) cur[I - T0] = e;
+    }
+    __syncthreads();
+    for (int s = T1 - T0 - 1; s >= 0; s--) {
+        const int K = T0 + s, K0 = K * LT, kh = S.th[K];
+        if (s % W == w) {   // the owner: diagonal tile, x_K final
+            const bool on = lane < kh;
+            double acc = accs[s * LT + lane];
+            const double* Ud = S.U + (size_t)S.slotOf[(size_t)K * S.nt + K] * (LT * LT);
+            double Lr[LT];
+#pragma unroll
+            for (int k = 0; k < LT; k++) Lr[k] = (on && k < kh) ? Ud[k * LT + lane] : 0.0;   // L[K0 + k][K0 + lane]
+#pragma unroll
+            for (int k = LT - 1; k >= 0; k--) {
+                if (k < kh) {
+                    const double v = acc - Lr[k] * rdlane(acc, k);
+                    acc = lane < k ? v : acc;
+                }
+            }
+            acc = on ? acc : 0.0;
+            S.xs[K0 + lane] = acc;
+            if (on) x[S.rowMap[K0 + lane]] = acc;
+            accs[s * LT + lane] = acc;
+        }
+        __syncthreads();
+        const double xk = accs[s * LT + lane];
+        for (int I = T0 + w; I < K; I += W) {
+            const int e = cur[I - T0];
+            if (e < S.rowStart[I] || S.rowJ[e] != K) continue;   // no block (I, K)
+            if (lane == 0) cur[I - T0] = e - 1;
+            const int sl = S.rowSlot[e];
+            if (!S.lnz[sl]) continue;
+            accs[(I - T0) * LT + lane] =
+                sweep_chain_bwd(accs[(I - T0) * LT + lane], S.LT + (size_t)sl * (LT * LT), lane, xk, kh);
+        }
+        __syncthreads();
+    }
+}
+
+// ORBGPU_LDLT_SWEEP=1 keeps the one-wave-per-node sweeps (A/B)
+static bool sweep_nodes() {
+    static const bool v = [] {
+        const char* e = getenv("ORBGPU_LDLT_SWEEP");
+        return !(e && atoi(e) == 1);
+    }();
+    return v;
+}
+
 int ldlt_debug_prof(unsigned long long* out8) {
 #ifdef ORBGPU_PROF
     ORB_HIP_CHECK(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_orbgpu_prof), sizeof(unsigned long long) * 8, 16 * 8));
@@ -556,6 +716,10 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     }
     hLevNodeStart_[nLev_] = (int)levNodes.size();
     hLevTgtStart_[nLev_] = (int)tgts.size();
+    hLevMaxT_.assign(nLev_, 0);
+    for (int h = 0; h < nLev_; h++)
+        for (int q = hLevNodeStart_[h]; q < hLevNodeStart_[h + 1]; q++)
+            hLevMaxT_[h] = std::max(hLevMaxT_[h], nodeT[2 * levNodes[q] + 1] - nodeT[2 * levNodes[q]]);
     // panel steps of each level: step s = panel T0 + s of every node of the level that has one;
     // per step the panels, the U tiles of their rows and the trailing targets inside the nodes
     std::vector<int> stepP;
@@ -726,12 +890,22 @@ int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
             if (z.z > a.z) hipLaunchKernelGGL(k_ldlt_ptrail, dim3(z.z - a.z), dim3(256), 0, s, d, a.z);
         }
         const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
-        hipLaunchKernelGGL(k_ldlt_pfwd, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], b);
+        const int mt = hLevMaxT_[h];
+        if (sweep_nodes() && mt > 1 && mt <= kSweepMaxTiles)
+            hipLaunchKernelGGL(k_ldlt_fwdn, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)), sizeof(double) * LT * mt, s, d,
+                               hLevNodeStart_[h], b);
+        else
+            hipLaunchKernelGGL(k_ldlt_pfwd, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], b);
     }
     for (int h = nLev_ - 1; h >= 0; h--) {
         const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
-        hipLaunchKernelGGL(k_ldlt_backward, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], x, scal,
-                           h == nLev_ - 1 ? 1 : 0);
+        const int mt = hLevMaxT_[h];
+        if (sweep_nodes() && mt > 1 && mt <= kSweepMaxTiles)
+            hipLaunchKernelGGL(k_ldlt_bwdn, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)), sizeof(double) * LT * mt, s, d,
+                               hLevNodeStart_[h], x, scal, h == nLev_ - 1 ? 1 : 0);
+        else
+            hipLaunchKernelGGL(k_ldlt_backward, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], x, scal,
+                               h == nLev_ - 1 ? 1 : 0);
     }
     ORB_HIP_CHECK(hipGetLastError());
     return 0;

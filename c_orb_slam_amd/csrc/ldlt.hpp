@@ -75,6 +75,7 @@ private:
            offColK_ = 0, offColSlot_ = 0, offPairStart_ = 0, offNodeT_ = 0, offLevNodes_ = 0, offPairs_ = 0,
            offTgts_ = 0, offKps_ = 0, offStepP_ = 0, offRowJobs_ = 0, offPairJobs_ = 0;
     std::vector<int> hSlotOf_, hProw_, hLevNodeStart_, hLevTgtStart_, hLevStepStart_;
+    std::vector<int> hLevMaxT_;   // per level: the most tiles of one of its nodes (sweep launch shape)
     std::vector<int4> hSteps_;   // per panel step: first (panel, row job, pair job); + sentinel
 };
 
