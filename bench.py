@@ -37,6 +37,7 @@ ROOFLINE_REPS = 5
 TRAFFIC_FILE = "traffic_r03.json"   # PMC FETCH_SIZE/WRITE_SIZE per launch (tools/pmc_traffic.py)
 VALU_FILE = "valu_r03.json"   # PMC SQ_INSTS_VALU per launch (tools/pmc_valu.py)
 MATCH_PMC_FILE = "match_pmc_r03.json"   # matcher kernels: HBM bytes and VALU instructions per launch (tools/pmc_match.py)
+STEREO_WINDOW_BYTES = 11 * 11 + 11 * 21   # per SAD-evaluated keypoint: left window + right search band
 VALU_PEAK_GINST = 1228.8   # 256 CUs x 2 wave64 VALU issues per cycle x 2.4 GHz (MI355X_MICROARCH.md)
 W, H, NFEAT = 1241, 376, 1200
 K_LOCAL = 5   # local map = the map points of the last K_LOCAL frames (UpdateLocalMap's local keyframes)
@@ -606,7 +607,7 @@ def main():
         acc = {k: [] for k in ("k_build_grid", "k_candidates", "k_select", "k_stereo_rows", "k_stereo_match",
                                "k_stereo_filter", "k_csr_hamming")}
         work = {k: [] for k in ("search_pairs", "search_queries", "stereo_pairs", "stereo_queries", "csr_pairs",
-                                "csr_queries")}
+                                "csr_queries", "stereo_sad")}
 
         def grab(kernels, counters):
             check(L.ORBmatcher_last_timings(m._h, ms.ctypes.data, cnt.ctypes.data), "ORBmatcher_last_timings")
@@ -634,7 +635,7 @@ def main():
         for _ in range(reps):
             lane.stereo()
             grab((("k_stereo_rows", 3), ("k_stereo_match", 4), ("k_stereo_filter", 5)),
-                 (("stereo_pairs", 2), ("stereo_queries", 3)))
+                 (("stereo_pairs", 2), ("stereo_queries", 3), ("stereo_sad", 7)))
             lane.search()
             grab((("k_build_grid", 0), ("k_candidates", 1), ("k_select", 2)),
                  (("search_pairs", 0), ("search_queries", 1)))
@@ -687,6 +688,8 @@ def main():
             t = float(np.mean(acc[k]))
             pairs, qs = float(np.mean(work[pk])), float(np.mean(work[qk]))
             alg = pairs * 36 + qs * 16
+            sad = float(np.mean(work["stereo_sad"])) if k == "k_stereo_match" else 0.0
+            alg += sad * STEREO_WINDOW_BYTES   # the SAD windows ComputeStereoMatches reads (Frame.cc:560-588)
             gbs = alg / (t * 1e-3) / 1e9
             e = {"avg_launch_ms": round(t, 4), "pairs_per_launch": int(pairs), "queries_per_launch": int(qs),
                  "alg_bytes_per_launch": int(alg), "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -702,6 +705,11 @@ def main():
                     e["valu"] = {"insts_per_launch": int(vi), "achieved": round(vr, 1), "peak": VALU_PEAK_GINST,
                                  "unit": "G wave-instr/s", "frac": round(vr / VALU_PEAK_GINST, 4)}
                 e["pmc_source"] = f"profiles/{MATCH_PMC_FILE}"
+            if k == "k_stereo_match":
+                e["sad_keypoints_per_launch"] = int(sad)
+                e["alg_bytes_note"] = (f"36 B per scored pair + 16 B per query + {STEREO_WINDOW_BYTES} B per keypoint "
+                                       "whose SAD windows are read (11x11 left window + the 11x21 right band it "
+                                       "slides over)")
             out[k] = e
         out["k_csr_hamming"]["workload"] = f"dense tiles: {B2} frame pairs, every left descriptor of frame b against " \
                                            f"every left descriptor of frame b+1 (SURVEY config 2 (ii))"

@@ -1326,21 +1326,26 @@ static int pose_wide_max() {
 
 // Canonical totals (ora_csum level 2) of the m chunk trees cs[q][0..m) of K sums, by wave 0:
 // lane c holds chunk c and the K trees run packed (the same pairing as local_csum_inplace).
+// K = 28 is split over waves 0-3, 7 trees each (every value's packed tree is the canonical one
+// whatever the packing width, so the split changes no bit; wave 0 alone was a serial segment of
+// every LM trial).
 template <int K>
 __device__ __forceinline__ void pose_chunk_totals(double (*cs)[kPoseMaxEdges / 64], int m, double* res) {
-    if (threadIdx.x >= 64) return;
-    const int lane = threadIdx.x;
+    constexpr int KW = K == 28 ? 7 : K;
+    const int w = threadIdx.x >> 6;
+    if (w >= K / KW) return;
+    const int lane = threadIdx.x & 63, q0 = w * KW;
     if (m <= 1) {
-        if (lane < K) res[lane] = m == 1 ? cs[lane][0] : 0.0;
+        if (lane < KW) res[q0 + lane] = m == 1 ? cs[q0 + lane][0] : 0.0;
     } else if (m <= 64) {
-        double v[K];
+        double v[KW];
 #pragma unroll
-        for (int q = 0; q < K; q++) v[q] = lane < m ? cs[q][lane] : 0.0;
-        const double t = packed_trees<K>(v);
+        for (int q = 0; q < KW; q++) v[q] = lane < m ? cs[q0 + q][lane] : 0.0;
+        const double t = packed_trees<KW>(v);
         const int q = bitrev6(lane);
-        if (q < K) res[q] = t;
-    } else if (lane < K) {
-        res[lane] = local_csum_inplace(cs[lane], m);
+        if (q < KW) res[q0 + q] = t;
+    } else if (lane < KW) {
+        res[q0 + lane] = local_csum_inplace(cs[q0 + lane], m);
     }
 }
 
@@ -1552,6 +1557,134 @@ __device__ __forceinline__ bool pose_solve_w(const double* Hs, const double* bs,
     return true;
 }
 
+// The same solve with lane r holding row r of P (H + lambda I) P^T (lanes >= 6 shadow row 5):
+// every IEEE operation of pose_solve_w, each row's in the lane that owns it, so a step's row
+// updates and divisions are one lane-parallel instruction each and only the pivot and the
+// finished y_j travel between lanes; the backward sweep reads the columns of L through scr
+// (36 doubles of this wave's LDS).  x is returned in every lane.
+__device__ __forceinline__ bool pose_solve_l(const double* Hs, const double* bs, double lambda, double* x,
+                                             double* scr) {
+    double dv[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) dv[i] = fabs(Hs[DIAG21[i]] + lambda);
+    bool distinct = true;
+    int rank[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        int r = 0;
+        distinct = distinct && dv[j] == dv[j];
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+            if (i != j) {
+                r += dv[i] > dv[j] ? 1 : 0;
+                distinct = distinct && dv[i] != dv[j];
+            }
+        rank[j] = r;
+    }
+    int ord[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+        int o = 0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) o = rank[j] == r ? j : o;
+        ord[r] = o;
+    }
+    const double a00 = Hs[DIAG21[ord[0]]] + lambda;
+    if (!distinct || !(fabs(a00) > 0.0)) {   // ties / NaN, or the reference's zero-pivot stop
+        double Hd[36], bb[6];
+#pragma unroll
+        for (int r = 0, q = 0; r < 6; r++)
+#pragma unroll
+            for (int cc = r; cc < 6; cc++, q++) {
+                double h = Hs[q];
+                if (cc == r) h += lambda;
+                Hd[r * 6 + cc] = h;
+                Hd[cc * 6 + r] = h;
+            }
+#pragma unroll
+        for (int j = 0; j < 6; j++) bb[j] = bs[j];
+        return ldlt_pivot6(Hd, bb, x);
+    }
+    const int lane = threadIdx.x & 63, row = lane < 6 ? lane : 5;
+    int orow = ord[0];
+#pragma unroll
+    for (int p = 1; p < 6; p++) orow = row == p ? ord[p] : orow;
+    double a[6];   // row `row` of P (H + lambda I) P^T, lower part used
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+        const int i0 = min(orow, ord[c]), i1 = max(orow, ord[c]);
+        double h = Hs[i0 * 6 - (i0 * (i0 - 1)) / 2 + (i1 - i0)];
+        if (row == c) h += lambda;
+        a[c] = h;
+    }
+    // branch-free: the reference's sign state machine ends in 1 / 2 / 3 / 0 exactly when some /
+    // only positive, only negative, both, no nonzero pivots were seen, so two flags replace it
+    double d[6];
+    bool anyNeg = false;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        if (k > 0) {
+            double tmp[6];
+#pragma unroll
+            for (int j = 0; j < k; j++) tmp[j] = d[j] * lane_bcast(a[j], k);   // A[j][j] * A[k][j]
+            double u = 0;
+#pragma unroll
+            for (int j = 0; j < k; j++) u += a[j] * tmp[j];
+            const double ak = a[k] - u;
+            a[k] = row >= k ? ak : a[k];
+        }
+        const double akk = lane_bcast(a[k], k);
+        d[k] = akk;
+        if (k < 5) {
+            const double q = a[k] / akk;
+            a[k] = (fabs(akk) > 0.0 && row > k) ? q : a[k];
+        }
+        anyNeg = anyNeg || akk < 0;
+    }
+    if (anyNeg) return false;
+    double y = bs[orow];
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const double yj = lane_bcast(y, j);
+        const double v = y - a[j] * yj;
+        y = row > j ? v : y;
+    }
+    double arr = a[0];
+#pragma unroll
+    for (int c = 1; c < 6; c++) arr = row == c ? a[c] : arr;   // own diagonal
+    {
+        const double q = y / arr;
+        y = fabs(arr) > DBL_MIN ? q : 0.0;
+    }
+    // columns of L: lane r needs A[j][r], j > r
+    if (lane < 6)
+#pragma unroll
+        for (int c = 0; c < 6; c++) scr[lane * 6 + c] = a[c];
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    double col[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) col[j] = scr[j * 6 + row];
+#pragma unroll
+    for (int j = 5; j >= 1; j--) {
+        const double xj = lane_bcast(y, j);
+        const double v = y - col[j] * xj;
+        y = row < j ? v : y;
+    }
+    double yb[6];
+#pragma unroll
+    for (int p = 0; p < 6; p++) yb[p] = lane_bcast(y, p);
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        double v = 0.0;
+#pragma unroll
+        for (int p = 0; p < 6; p++)
+            if (ord[p] == j) v = yb[p];
+        x[j] = v;
+    }
+    return true;
+}
+
 template <int NT>
 __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseEdgeDev* __restrict__ Eall,
                                                  double* errAll, uint8_t* outlAll) {
@@ -1573,6 +1706,7 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
     __shared__ Se3 T, Terr, Tbase, Tc[kPoseSpec + 1];   // Tc: the candidates of a round of trials
     __shared__ double xc[kPoseSpec + 1][6];
     __shared__ int okc[kPoseSpec + 1];
+    __shared__ double scrSolve[kPoseSpec + 1][36];   // pose_solve_l's column exchange, one per solving wave
     __shared__ double xs[6], Hs[21], bs[6], sysN[28];
     __shared__ double lambda, ni, currentChi, iniChi;
     __shared__ int nA, nBadLM, qmax, again, term, nBad, haveSys, specPass, wsum[16];
@@ -1718,7 +1852,11 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
                             ns *= 2;
                         }
                         double xn[6];
+#ifndef ORBGPU_POSE_SOLVE_W
+                        const bool ok = pose_solve_l(Hs, bs, ls, xn, scrSolve[L]);
+#else
                         const bool ok = pose_solve_w(Hs, bs, ls, xn);
+#endif
                         ORBGPU_PROF_MARK(5);
                         ORBGPU_PROF_COUNT(9);
                         // candidate 0 steps from xs when the solve fails (its trial is then

@@ -12,8 +12,8 @@
 //                    reference's first strict minimum; the 11 SADs are integer group sums
 //                    (cv::norm of centred integer windows is exact), the parabola and the
 //                    disparity follow the reference's float expression order.
-//   k_stereo_filter  one workgroup per pair: bitonic sort of the kept SADs in LDS, median,
-//                    thDist = 1.5f*1.4f*median, invalidation of SAD >= thDist.
+//   k_stereo_filter  one workgroup per pair: the median of the kept SADs by a two-level LDS
+//                    histogram select, thDist = 1.5f*1.4f*median, invalidation of SAD >= thDist.
 #include "stereo.hpp"
 #include "orb_match.hpp"
 
@@ -155,6 +155,9 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
             const StereoLevel lv = P.lv[levelL];
             const float iniu = scaleduR0 + L - w, endu = scaleduR0 + L + w + 1;
             if (!(iniu < 0 || endu >= lv.w)) {
+                if (counters && sub == 0)   // measurement: keypoints whose SAD windows are read
+                    atomicAdd(&counters[7 * kCountSlots + ((blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 4)) &
+                                                           (kCountSlots - 1))], 1ull);
                 const uint8_t* IL = S.pyrL + lv.off + (size_t)kEdge * lv.pitch + kEdge;
                 const uint8_t* IR = S.pyrR + lv.off + (size_t)kEdge * lv.pitch + kEdge;
                 const int yL = (int)scaledvL, xL = (int)scaleduL, xR0 = (int)scaleduR0;
@@ -217,48 +220,77 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
     }
 }
 
-// median filter (Frame.cc:624-639): sort the kept SADs, thDist = 1.5f*1.4f*median,
-// invalidate SAD >= thDist (the reference walks the sorted tail from the end).
-// 4 waves and LDS sized at launch (next power of two of the batch's largest NL): the workgroup
-// fits in the slot of one retiring extraction workgroup (1,024 threads + 16 KB waited ~3x longer)
+// median filter (Frame.cc:624-639): the reference sorts the kept SADs, takes the middle one,
+// thDist = 1.5f*1.4f*median, and invalidates SAD >= thDist walking the sorted tail from the end.
+// 4 waves and 1 KB of LDS: the workgroup fits in the slot of one retiring extraction workgroup
+// (1,024 threads + 16 KB waited ~3x longer)
+// The median is vDistIdx[n/2] of the sorted SADs, i.e. the (n/2)-th smallest kept SAD: a radix
+// select over two LDS histograms (SAD >> 7, then SAD & 127 inside the bucket that holds rank
+// n/2) instead of sorting.  A SAD is a sum of 121 absolute byte differences: < 2^15.
+__device__ __forceinline__ void stereo_select_bucket(const int* hist, int nb, int rank, int* out_bin, int* out_rank) {
+    // one wave: lane l holds bins 4l..4l+3 (nb <= 256); the bin where the running count passes rank
+    const int lane = threadIdx.x;
+    int c[4], loc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        c[k] = 4 * lane + k < nb ? hist[4 * lane + k] : 0;
+        loc += c[k];
+    }
+    int incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    int run = incl - loc;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (run <= rank && rank < run + c[k]) {
+            *out_bin = 4 * lane + k;
+            *out_rank = rank - run;
+        }
+        run += c[k];
+    }
+}
+
 __global__ void __launch_bounds__(256) k_stereo_filter(const StereoDev* __restrict__ probs) {
     ORBGPU_LATENCY_WAVE();
     const StereoDev& S = probs[blockIdx.x];
-    extern __shared__ int v[];
-    __shared__ int cnt, kept;
+    __shared__ int hist[256];
+    __shared__ int cnt, kept, bin, rnk;
     const int tid = threadIdx.x;
+    hist[tid] = 0;
     if (tid == 0) cnt = 0;
     __syncthreads();
+    int mine = 0;
     for (int i = tid; i < S.NL; i += blockDim.x) {
         const int d = S.sad[i];
-        if (d >= 0) v[atomicAdd(&cnt, 1)] = d;
+        if (d >= 0) {
+            atomicAdd(&hist[d >> 7], 1);
+            mine++;
+        }
     }
+    if (mine) atomicAdd(&cnt, mine);
     __syncthreads();
     const int n = cnt;
     if (n == 0) {   // empty vDistIdx is UB in the reference; nothing to filter
         if (tid == 0) *S.kept = 0;
         return;
     }
-    int m = 1;
-    while (m < n) m <<= 1;
-    for (int i = n + tid; i < m; i += blockDim.x) v[i] = INT_MAX;
+    if (tid < 64) stereo_select_bucket(hist, 256, n / 2, &bin, &rnk);
     __syncthreads();
-    for (int k = 2; k <= m; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < m; i += blockDim.x) {
-                const int ix = i ^ j;
-                if (ix > i) {
-                    const bool up = (i & k) == 0;
-                    const int a = v[i], b = v[ix];
-                    if ((a > b) == up) {
-                        v[i] = b;
-                        v[ix] = a;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    const float median = (float)v[n / 2];
+    const int hb = bin, r2 = rnk;
+    __syncthreads();
+    hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < S.NL; i += blockDim.x) {
+        const int d = S.sad[i];
+        if (d >= 0 && (d >> 7) == hb) atomicAdd(&hist[d & 127], 1);
+    }
+    __syncthreads();
+    if (tid < 64) stereo_select_bucket(hist, 128, r2, &bin, &rnk);
+    __syncthreads();
+    const float median = (float)(hb * 128 + bin);
     const float thDist = 1.5f * 1.4f * median;
     if (tid == 0) kept = n;
     __syncthreads();
@@ -279,6 +311,7 @@ int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoPa
     const bool timed = tm && tm->timing();
     if (timed) {
         if (int e = tm->zero_counters(2, 2)) return e;
+        if (int e = tm->zero_counters(7, 1)) return e;
         tm->mark(4);
     }
     hipLaunchKernelGGL(k_stereo_rows, dim3(nprob), dim3(1024), 0, s, d_probs, P);
@@ -287,9 +320,7 @@ int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoPa
         hipLaunchKernelGGL(k_stereo_match, dim3((maxNL + 15) / 16, nprob), dim3(256), 0, s, d_probs, P,
                            timed ? tm->counters() : nullptr);
     if (timed) tm->mark(6);
-    int m = 1;
-    while (m < std::max(maxNL, 1)) m <<= 1;
-    hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(256), (size_t)m * sizeof(int), s, d_probs);
+    hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(256), 0, s, d_probs);
     if (timed) tm->mark(7);
     ORB_HIP_CHECK(hipGetLastError());
     return 0;

@@ -126,7 +126,8 @@ void* ORBmatcher_stream(ORBmatcher_h h);
  * and work counts:
  *   counts8[0..5]: SearchByProjection (query, candidate) pairs scored, queries with a window,
  *                  ComputeStereoMatches (left, right) pairs scored, left keypoints searched,
- *                  SearchCandidates pairs, SearchCandidates queries. */
+ *                  SearchCandidates pairs, SearchCandidates queries;
+ *   counts8[7]: ComputeStereoMatches left keypoints whose 11x11 SAD windows were read. */
 int ORBmatcher_enable_timing(ORBmatcher_h h, int on);
 int ORBmatcher_last_timings(ORBmatcher_h h, float* ms8, long long* counts8);
 /* Deferred completion (no reference counterpart; the reference's calls are synchronous).
