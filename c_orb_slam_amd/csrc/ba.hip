@@ -17,6 +17,8 @@
 // so results are bit-identical to the CPU restatement.
 #include "ba.hpp"
 
+#include <type_traits>
+
 #include <functional>
 
 #include <algorithm>
@@ -70,13 +72,14 @@ __device__ __forceinline__ void se3_exp(const double* upd, Se3& out) {
 __device__ __forceinline__ void edge_error(const EdgeDev& e, const Se3& T, const double* X, double* err) {
     double p[3];
     se3_map(T, X, p);
+    const SharedDiv dz(p[2]);
     if (!e.stereo) {
-        const double px = p[0] / p[2], py = p[1] / p[2];
+        const double px = dz.div(p[0]), py = dz.div(p[1]);
         err[0] = e.obs[0] - (px * e.fx + e.cx);
         err[1] = e.obs[1] - (py * e.fy + e.cy);
         err[2] = 0;
     } else {
-        const float invz = (float)(1.0 / p[2]);
+        const float invz = (float)dz.div(1.0);
         const float bf = (float)e.bf;
         const double u = (p[0] * (double)invz) * e.fx + e.cx;
         const double v = (p[1] * (double)invz) * e.fy + e.cy;
@@ -226,11 +229,14 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
     se3_map(T, X, p);
     quat_to_R(T.q, R);
     const double x = p[0], y = p[1], z = p[2], z_2 = z * z;
+    // every x / z and x / z_2 through one reciprocal each (SharedDiv: the same correctly rounded
+    // quotients as the division)
+    const SharedDiv dz(z), dz2(z_2);
     const double fx = e.fx, fy = e.fy;
     const int D = e.stereo ? 3 : 2;
     if (!e.stereo) {
-        const double tmp[6] = {fx, 0, ((-x) / z) * fx, 0, fy, ((-y) / z) * fy};
-        const double s = -1. / z;
+        const double tmp[6] = {fx, 0, dz.div(-x) * fx, 0, fy, dz.div(-y) * fy};
+        const double s = dz.div(-1.);
         double st[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) st[k] = s * tmp[k];
@@ -242,31 +248,32 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
         const double bf = e.bf;
 #pragma unroll
         for (int c = 0; c < 3; c++) {
-            A[0 * 3 + c] = ((-fx) * R[0 * 3 + c]) / z + ((fx * x) * R[2 * 3 + c]) / z_2;
-            A[1 * 3 + c] = ((-fy) * R[1 * 3 + c]) / z + ((fy * y) * R[2 * 3 + c]) / z_2;
-            A[2 * 3 + c] = A[0 * 3 + c] - (bf * R[2 * 3 + c]) / z_2;
+            A[0 * 3 + c] = dz.div((-fx) * R[0 * 3 + c]) + dz2.div((fx * x) * R[2 * 3 + c]);
+            A[1 * 3 + c] = dz.div((-fy) * R[1 * 3 + c]) + dz2.div((fy * y) * R[2 * 3 + c]);
+            A[2 * 3 + c] = A[0 * 3 + c] - dz2.div(bf * R[2 * 3 + c]);
         }
     }
-    B[0] = ((x * y) / z_2) * fx;
-    B[1] = (-(1 + ((x * x) / z_2))) * fx;
-    B[2] = (y / z) * fx;
-    B[3] = (-1. / z) * fx;
+    const double m1z = dz.div(-1.);
+    B[0] = dz2.div(x * y) * fx;
+    B[1] = (-(1 + dz2.div(x * x))) * fx;
+    B[2] = dz.div(y) * fx;
+    B[3] = m1z * fx;
     B[4] = 0;
-    B[5] = (x / z_2) * fx;
-    B[6] = (1 + ((y * y) / z_2)) * fy;
-    B[7] = (((-x) * y) / z_2) * fy;
-    B[8] = ((-x) / z) * fy;
+    B[5] = dz2.div(x) * fx;
+    B[6] = (1 + dz2.div(y * y)) * fy;
+    B[7] = dz2.div((-x) * y) * fy;
+    B[8] = dz.div(-x) * fy;
     B[9] = 0;
-    B[10] = (-1. / z) * fy;
-    B[11] = (y / z_2) * fy;
+    B[10] = m1z * fy;
+    B[11] = dz2.div(y) * fy;
     if (e.stereo) {
         const double bf = e.bf;
-        B[12] = B[0] - (bf * y) / z_2;
-        B[13] = B[1] + (bf * x) / z_2;
+        B[12] = B[0] - dz2.div(bf * y);
+        B[13] = B[1] + dz2.div(bf * x);
         B[14] = B[2];
         B[15] = B[3];
         B[16] = 0;
-        B[17] = B[5] - bf / z_2;
+        B[17] = B[5] - dz2.div(bf);
     } else {
 #pragma unroll
         for (int k = 12; k < 18; k++) B[k] = 0;
@@ -350,7 +357,7 @@ __device__ __forceinline__ double wave_lds_csum(double* arr, int m) {
 constexpr int kChunks = 128;  // per-list LDS chunk sums: lists up to 8192 terms
 
 // per free pose: Hpp (upper 21) and b_p as canonical sums over its active edges (edge order).
-// Each lane loads the 27 terms of one edge; one wave tree per entry and chunk; chunk sums
+// Each lane loads the 27 terms of one edge; the 27 chunk trees run packed; chunk sums
 // reduced per entry by one thread.
 __device__ __forceinline__ void pose_reduce_block(const BaStructDev& s, const double* __restrict__ terms, double* Hpp,
                                                   double* bp, int i) {
@@ -369,10 +376,14 @@ __device__ __forceinline__ void pose_reduce_block(const BaStructDev& s, const do
             const int col = q < 21 ? T_HPP + q : T_BP + (q - 21);
             v[q] = valid ? terms[(size_t)col * nE + a] : 0.0;
         }
+        if (n == 1) {   // ora_csum keeps a single term untouched
+            if (lane == 0)
 #pragma unroll
-        for (int q = 0; q < 27; q++) {
-            const double t = n == 1 ? v[q] : wave_tree(v[q]);  // ora_csum keeps a single term untouched
-            if (lane == 0) cs[q][c] = t;
+                for (int q = 0; q < 27; q++) cs[q][c] = v[q];
+        } else {   // the 27 canonical chunk trees, packed
+            const double t = packed_trees<27>(v);
+            const int q = bitrev6(lane);
+            if (q < 27) cs[q][c] = t;
         }
     }
     __syncthreads();
@@ -503,12 +514,16 @@ __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double*
 
 // Schur complement block (i1, i2): S = [Hpp + lambda I] - csum_l BDinv_l,i1 B_l,i2^T
 // (upper triangle of the diagonal blocks), and b_s = b_p - csum_l B db.
-// Each lane loads the two 6x3 blocks of one landmark term once and feeds all entries.
-__global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __restrict__ Emat,
-                                                const double* __restrict__ Hpl, const double* __restrict__ cb,
-                                                const double* Hpp, const double* bp, double lam_host, int use_dev,
-                                                const double* scal, SysAddr S, double* bs, int own,
-                                                const int* run) {
+// Each lane loads the two 6x3 blocks of one landmark term once and feeds all entries; a chunk's
+// 27 / 36 canonical 64-trees run packed (packed_trees: every value's tree is the canonical one).
+// NT = 256 for systems of many blocks (global BA: most blocks hold one or two chunks), 512 for
+// the few long blocks of a local BA.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __restrict__ Emat,
+                                              const double* __restrict__ Hpl, const double* __restrict__ cb,
+                                              const double* Hpp, const double* bp, double lam_host, int use_dev,
+                                              const double* scal, SysAddr S, double* bs, int own,
+                                              const int* run) {
     BA_GATE(run);
     __shared__ double cs[36][kChunks];
     const int blk = blockIdx.x;
@@ -528,31 +543,37 @@ __global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __r
             E[q] = valid ? Emat[18 * (size_t)a1 + q] : 0.0;
             B[q] = valid ? Hpl[18 * (size_t)a2 + q] : 0.0;
         }
+        auto put = [&](double* v, auto kk) {
+            constexpr int K = decltype(kk)::value;
+            if (n == 1) {   // ora_csum keeps a single term untouched
+                if (lane == 0)
+#pragma unroll
+                    for (int q = 0; q < K; q++) cs[q][c] = v[q];
+            } else {
+                const double t = packed_trees<K>(v);
+                const int q = bitrev6(lane);
+                if (q < K) cs[q][c] = t;
+            }
+        };
         if (diag) {
+            double v[27];
             int q = 0;
 #pragma unroll
             for (int r = 0; r < 6; r++)
 #pragma unroll
-                for (int cc = r; cc < 6; cc++, q++) {
-                    const double v = valid ? (E[r * 3] * B[cc * 3] + E[r * 3 + 1] * B[cc * 3 + 1]) + E[r * 3 + 2] * B[cc * 3 + 2] : 0.0;
-                    const double t = n == 1 ? v : wave_tree(v);
-                    if (lane == 0) cs[q][c] = t;
-                }
+                for (int cc = r; cc < 6; cc++, q++)
+                    v[q] = valid ? (E[r * 3] * B[cc * 3] + E[r * 3 + 1] * B[cc * 3 + 1]) + E[r * 3 + 2] * B[cc * 3 + 2] : 0.0;
 #pragma unroll
-            for (int r = 0; r < 6; r++) {
-                const double v = valid ? cb[6 * (size_t)a1 + r] : 0.0;
-                const double t = n == 1 ? v : wave_tree(v);
-                if (lane == 0) cs[21 + r][c] = t;
-            }
+            for (int r = 0; r < 6; r++) v[21 + r] = valid ? cb[6 * (size_t)a1 + r] : 0.0;
+            put(v, std::integral_constant<int, 27>{});
         } else {
+            double v[36];
 #pragma unroll
             for (int r = 0; r < 6; r++)
 #pragma unroll
-                for (int cc = 0; cc < 6; cc++) {
-                    const double v = valid ? (E[r * 3] * B[cc * 3] + E[r * 3 + 1] * B[cc * 3 + 1]) + E[r * 3 + 2] * B[cc * 3 + 2] : 0.0;
-                    const double t = n == 1 ? v : wave_tree(v);
-                    if (lane == 0) cs[r * 6 + cc][c] = t;
-                }
+                for (int cc = 0; cc < 6; cc++)
+                    v[r * 6 + cc] = valid ? (E[r * 3] * B[cc * 3] + E[r * 3 + 1] * B[cc * 3 + 1]) + E[r * 3 + 2] * B[cc * 3 + 2] : 0.0;
+            put(v, std::integral_constant<int, 36>{});
         }
     }
     __syncthreads();
@@ -579,6 +600,12 @@ __global__ void __launch_bounds__(1024) k_schur(BaStructDev s, const double* __r
         if (c == r) h += lambda;
     }
     *S.at(6 * i1 + r, 6 * i2 + c) = h - v;
+}
+
+template <class... A>
+static void schur_launch(int nBlk, hipStream_t st, A... args) {
+    if (nBlk >= 256) hipLaunchKernelGGL(k_schur<256>, dim3(nBlk), dim3(256), 0, st, args...);
+    else hipLaunchKernelGGL(k_schur<512>, dim3(nBlk), dim3(512), 0, st, args...);
 }
 
 // Dense LDL^T of the upper triangle + solve, one workgroup (256 threads).
@@ -977,20 +1004,23 @@ __global__ void __launch_bounds__(1024) k_scale(int nP, int nL, const double* x,
     if (threadIdx.x == 0) *out = local_csum_inplace(lv, m);
 }
 
-// computeScale terms for large problems (6 nP + 3 nL > 2048 * 64): written out, then k_csum
-__global__ void __launch_bounds__(256) k_scale_terms(int nP, int nL, const double* x, const double* bp,
-                                                     const double* bl, double lam_host, int use_dev,
-                                                     const double* scal, double* v, int poses, const int* run) {
+// computeScale terms for large problems (6 nP + 3 nL > 2048 * 64) fused with the first
+// canonical level: wave c writes the 64-tree of
+// v[64c .. 64c + 64) (zero past the end) to chunks[c]; k_csum then sums the chunk trees, which
+// continues ora_csum at its second level
+__global__ void __launch_bounds__(256) k_scale_chunks(int nP, int nL, const double* x, const double* bp,
+                                                      const double* bl, double lam_host, int use_dev,
+                                                      const double* scal, double* chunks, int poses, const int* run) {
     BA_GATE(run);
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= 6 * nP + 3 * nL) return;
-    const double lambda = lam_of(lam_host, use_dev, scal);
-    if (j < 6 * nP && !poses) {
-        v[j] = 0.0;
-        return;
+    double v = 0.0;
+    if (j < 6 * nP + 3 * nL && (j >= 6 * nP || poses)) {
+        const double lambda = lam_of(lam_host, use_dev, scal);
+        const double b = j < 6 * nP ? bp[j] : bl[j - 6 * nP];
+        v = x[j] * (lambda * x[j] + b);
     }
-    const double b = j < 6 * nP ? bp[j] : bl[j - 6 * nP];
-    v[j] = x[j] * (lambda * x[j] + b);
+    const double t = wave_tree(v);
+    if ((threadIdx.x & 63) == 0) chunks[j >> 6] = t;
 }
 
 // canonical sum of one list per workgroup (blockIdx.x selects the list), 1024 threads,
@@ -1126,7 +1156,7 @@ __device__ int lm_decide(LmDev* L, double* scal, volatile int* host) {
 }
 
 // End of a trial: computeScale (k_scale's canonical sum, problems with 6 nP + 3 nL <= 2048 * 64;
-// larger ones ran k_scale_terms + k_csum into scal[2] and pass scale = 0), the LM decision, and
+// larger ones ran k_scale_chunks + k_csum into scal[2] and pass scale = 0), the LM decision, and
 // the pop of a rejected trial, in one workgroup.
 __global__ void __launch_bounds__(1024) k_lm_trial_end(LmDev* L, double* scal, volatile int* host, BaStructDev s,
                                                        Se3* T, const Se3* Tbak, double* X, const double* Xbak,
@@ -1278,22 +1308,28 @@ __device__ __forceinline__ PoseEdgeD pose_edge_load(const PoseEdgeDev* E, int i,
     return e;
 }
 
-__device__ __forceinline__ void pose_err(const PoseEdgeD& e, const Se3& T, const PoseProbDev& P, double* err) {
-    double p[3];
-    se3_map(T, e.X, p);
+// the error at camera point p (dz: the shared divisions by p[2])
+__device__ __forceinline__ void pose_err_p(const PoseEdgeD& e, const double* p, const SharedDiv& dz,
+                                           const PoseProbDev& P, double* err) {
     if (!e.stereo) {
-        const double px = p[0] / p[2], py = p[1] / p[2];
+        const double px = dz.div(p[0]), py = dz.div(p[1]);
         err[0] = e.obs[0] - (px * P.fx + P.cx);
         err[1] = e.obs[1] - (py * P.fy + P.cy);
         err[2] = 0;
     } else {
-        const float invz = (float)(1.0 / p[2]);
+        const float invz = (float)dz.div(1.0);
         const double u = (p[0] * (double)invz) * P.fx + P.cx;
         const double v = (p[1] * (double)invz) * P.fy + P.cy;
         err[0] = e.obs[0] - u;
         err[1] = e.obs[1] - v;
         err[2] = e.obs[2] - (u - P.bf * (double)invz);
     }
+}
+
+__device__ __forceinline__ void pose_err(const PoseEdgeD& e, const Se3& T, const PoseProbDev& P, double* err) {
+    double p[3];
+    se3_map(T, e.X, p);
+    pose_err_p(e, p, SharedDiv(p[2]), P, err);
 }
 
 __device__ __forceinline__ double pose_chi2(const PoseEdgeD& e, const double* err) {
@@ -1353,10 +1389,12 @@ __device__ __forceinline__ void pose_chunk_totals(double (*cs)[kPoseMaxEdges / 6
 // c = w, w + nw, ... of 64 active edges; the edge of chunk c + nw is loaded while chunk c is
 // computed.  f(e, i, out[K]) evaluates active edge i (edge e loaded).  Chunk trees go to
 // cs[q][c]; thread q < K finishes entry q.
-template <int K, class F>
-__device__ __forceinline__ void pose_pass(F f, int nA, const uint16_t* aE, const PoseEdgeDev* E, double dM, double dS,
-                                          double (*cs)[kPoseMaxEdges / 64], double* res, const PoseEdgeD& mine,
-                                          int mineIdx) {
+template <int K, class F, class Post>
+// post: run by thread 0 right after its own totals (res[0] among them) and before the closing
+// barrier, i.e. beside the other waves' totals
+__device__ __forceinline__ void pose_pass_post(F f, int nA, const uint16_t* aE, const PoseEdgeDev* E, double dM,
+                                               double dS, double (*cs)[kPoseMaxEdges / 64], double* res,
+                                               const PoseEdgeD& mine, int mineIdx, Post post) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int m = (nA + 63) >> 6;
     // chunk c = w is active edge tid: this thread's for the whole round, kept in registers
@@ -1395,7 +1433,14 @@ __device__ __forceinline__ void pose_pass(F f, int nA, const uint16_t* aE, const
     }
     __syncthreads();
     pose_chunk_totals<K>(cs, nA > 0 ? m : 0, res);
+    if (threadIdx.x == 0) post();
     __syncthreads();
+}
+template <int K, class F>
+__device__ __forceinline__ void pose_pass(F f, int nA, const uint16_t* aE, const PoseEdgeDev* E, double dM, double dS,
+                                          double (*cs)[kPoseMaxEdges / 64], double* res, const PoseEdgeD& mine,
+                                          int mineIdx) {
+    pose_pass_post<K>(f, nA, aE, E, dM, dS, cs, res, mine, mineIdx, [] {});
 }
 
 
@@ -1767,14 +1812,15 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
             // J, robust weight and the 28 entries (robust chi2, J^T W J upper triangle, -J^T W e)
             // of active edge i at pose X, into v[0..28)
             auto sys_terms = [&](const PoseEdgeD& e, int i, const Se3& X, double* v) {
+                double p[3];
+                se3_map(X, e.X, p);
+                const SharedDiv dz(p[2]);
                 double e3[3];
-                pose_err(e, X, P, e3);
+                pose_err_p(e, p, dz, P, e3);
                 const double c = pose_chi2(e, e3);
                 const bool rb = (fl[i] & 2) != 0;
                 v[0] = pose_rho0(e, c, rb);
-                double p[3];
-                se3_map(X, e.X, p);
-                const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
+                const double x = p[0], y = p[1], invz = dz.div(1.0), invz_2 = invz * invz;
                 double J[18];
                 J[0] = ((x * y) * invz_2) * P.fx;
                 J[1] = (-(1 + ((x * x) * invz_2))) * P.fx;
@@ -1883,14 +1929,60 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
                     ORBGPU_PROF_MARK(0);
                     ORBGPU_PROF_COUNT(8);
                 }
+                // one trial of the reference's loop (optimization_algorithm_levenberg.cpp:100-149)
+                // at candidate j with robust chi2 tempChi; tid 0 only
+                auto trial = [&](int j, double tempChi) {
+                    if (!okc[j]) tempChi = DBL_MAX;
+#pragma unroll
+                    for (int q = 0; q < 6; q++) xs[q] = xc[j][q];
+                    double rho = currentChi - tempChi;
+                    double sv[6];
+                    for (int q = 0; q < 6; q++) sv[q] = xs[q] * (lambda * xs[q] + bs[q]);
+                    double scale = tree64_local([&](int q) { return sv[q]; }, 6);
+                    scale += 1e-3;
+                    rho /= scale;
+                    Terr = Tc[j];   // the pose of the last computeActiveErrors
+                    if (rho > 0 && isfinite(tempChi)) {
+                        const double a3 = 2 * rho - 1;
+                        double alpha = 1. - (a3 * a3) * a3;
+                        alpha = fmin(alpha, 2. / 3.);
+                        const double scaleFactor = fmax(1. / 3., alpha);
+                        lambda *= scaleFactor;
+                        ni = 2;
+                        currentChi = tempChi;
+                        T = Tc[j];
+                        if (j == 0) haveSys = 1;   // red[0..28) is the system at the new estimate
+                    } else {
+                        lambda *= ni;
+                        ni *= 2;
+                        T = Tbase;
+                    }
+                    qmax++;
+                    again = (rho < 0 && qmax < 10) ? 1 : 0;
+                    if (!again) {
+                        if (qmax == 10 || rho == 0) {
+                            term = 1;
+                        } else {
+                            if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
+                            else nBadLM = 0;
+                            term = nBadLM >= 3 ? 1 : 0;
+                        }
+                    }
+                };
                 // sysPhase: computeActiveErrors + activeRobustChi2 (entry 0) and buildSystem
                 // (entries 1..27) at T; a trial: its robust chi2 at candidate 0 and, with it, the
                 // system at that estimate (the next iteration's whenever the trial is accepted).
                 // Canonical sums per entry.
-                {
+                {   // a trial's decision runs on thread 0 as soon as its chi2 total (red[0]) is in,
+                    // beside the other waves' totals (the pass reads no state the decision writes)
                     const Se3& X = sysPhase ? T : Tc[0];
-                    pose_pass<28>([&](const PoseEdgeD& e, int i, double* v) { sys_terms(e, i, X, v); }, na, aE, E, dM,
-                                  dS, cs, red, myE, myIdx);
+                    pose_pass_post<28>([&](const PoseEdgeD& e, int i, double* v) { sys_terms(e, i, X, v); }, na, aE, E,
+                                       dM, dS, cs, red, myE, myIdx, [&] {
+                                           if (!sysPhase) {
+                                               trial(0, red[0]);
+                                               specPass = again && okc[1] ? 1 : 0;
+                                           }
+                                       });
                 }
                 if (sysPhase) {
                     ORBGPU_PROF_MARK(1);
@@ -1901,51 +1993,6 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
                     }
                 } else {
                     ORBGPU_PROF_MARK(3);
-                    // one trial of the reference's loop (optimization_algorithm_levenberg.cpp:100-149)
-                    // at candidate j with robust chi2 tempChi; tid 0 only
-                    auto trial = [&](int j, double tempChi) {
-                        if (!okc[j]) tempChi = DBL_MAX;
-#pragma unroll
-                        for (int q = 0; q < 6; q++) xs[q] = xc[j][q];
-                        double rho = currentChi - tempChi;
-                        double sv[6];
-                        for (int q = 0; q < 6; q++) sv[q] = xs[q] * (lambda * xs[q] + bs[q]);
-                        double scale = tree64_local([&](int q) { return sv[q]; }, 6);
-                        scale += 1e-3;
-                        rho /= scale;
-                        Terr = Tc[j];   // the pose of the last computeActiveErrors
-                        if (rho > 0 && isfinite(tempChi)) {
-                            const double a3 = 2 * rho - 1;
-                            double alpha = 1. - (a3 * a3) * a3;
-                            alpha = fmin(alpha, 2. / 3.);
-                            const double scaleFactor = fmax(1. / 3., alpha);
-                            lambda *= scaleFactor;
-                            ni = 2;
-                            currentChi = tempChi;
-                            T = Tc[j];
-                            if (j == 0) haveSys = 1;   // red[0..28) is the system at the new estimate
-                        } else {
-                            lambda *= ni;
-                            ni *= 2;
-                            T = Tbase;
-                        }
-                        qmax++;
-                        again = (rho < 0 && qmax < 10) ? 1 : 0;
-                        if (!again) {
-                            if (qmax == 10 || rho == 0) {
-                                term = 1;
-                            } else {
-                                if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
-                                else nBadLM = 0;
-                                term = nBadLM >= 3 ? 1 : 0;
-                            }
-                        }
-                    };
-                    if (tid == 0) {
-                        trial(0, red[0]);
-                        specPass = again && okc[1] ? 1 : 0;
-                    }
-                    __syncthreads();
                     if (haveSys && tid < 28) sysN[tid] = red[tid];
                     if (specPass) {
                         // candidate 0 rejected: the speculative candidates' robust chi2 in one pass,
@@ -2782,7 +2829,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         } else if (comm_ && n) {
             ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * (size_t)n * n, s));
         }
-        if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(1024), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
+        if (S.nBlk) schur_launch(S.nBlk, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
                                        lambda_, use_dev, dScal_, sa, dBs_, own ? 1 : 0, nullptr);
         if (comm_ && tiled_) {   // all-reduce the Schur-pattern tiles of S and b_s
             ORB_HIP_CHECK(hipGetLastError());
@@ -2816,9 +2863,9 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
                                dScal_ + 2, own ? 1 : 0, nullptr);
         } else {
             const int nv = 6 * nP + 3 * nL;
-            hipLaunchKernelGGL(k_scale_terms, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_,
-                               use_dev, dScal_, dScratch_, own ? 1 : 0, nullptr);
-            CsumList L0{dScratch_, nv, tmpA0_, tmpA1_, dScal_ + 2};
+            hipLaunchKernelGGL(k_scale_chunks, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_,
+                               use_dev, dScal_, tmpA0_, own ? 1 : 0, nullptr);
+            CsumList L0{tmpA0_, (nv + 63) / 64, tmpA1_, tmpA0_, dScal_ + 2};
             hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, L0, L0, nullptr);
         }
         ORB_HIP_CHECK(hipGetLastError());
@@ -2927,7 +2974,7 @@ void BaEngine::enqueue_lm_step(bool first) {
     const SysAddr sa{dS_, n, nullptr, nullptr, 0, nullptr};
     if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_, 0.0, 1,
                                dScal_, dEmat_, dCb_, ctl);
-    if (S.nBlk) hipLaunchKernelGGL(k_schur, dim3(S.nBlk), dim3(1024), 0, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_, 0.0,
+    if (S.nBlk) schur_launch(S.nBlk, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_, 0.0,
                                    1, dScal_, sa, dBs_, 1, ctl);
     if (use_reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, ctl);
@@ -2940,9 +2987,9 @@ void BaEngine::enqueue_lm_step(bool first) {
     const bool small = 6 * nP + 3 * nL <= 2048 * 64;
     if (!small) {
         const int nv = 6 * nP + 3 * nL;
-        hipLaunchKernelGGL(k_scale_terms, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dX2_, dBp_, dBl_, 0.0, 1,
-                           dScal_, dScratch_, 1, ctl);
-        CsumList L0{dScratch_, nv, tmpA0_, tmpA1_, dScal_ + 2};
+        hipLaunchKernelGGL(k_scale_chunks, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dX2_, dBp_, dBl_, 0.0, 1,
+                           dScal_, tmpA0_, 1, ctl);
+        CsumList L0{tmpA0_, (nv + 63) / 64, tmpA1_, tmpA0_, dScal_ + 2};
         hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, L0, L0, ctl);
     }
     hipLaunchKernelGGL(k_lm_trial_end, dim3(1), dim3(1024), 0, s, dLm_, dScal_, (volatile int*)hLm_, S, dT_, dTbak_,
@@ -3134,6 +3181,28 @@ int debug_ldlt_factor(int n, const double* S, double* out) {
 __global__ void k_unit_wave_tree(const double* v, double* out) {
     const double t = wave_tree(v[threadIdx.x]);
     if (threadIdx.x == 0) *out = t;
+}
+
+// SharedDiv against the plain division on n operand pairs: out[2i] = shared, out[2i + 1] = a / b
+__global__ void __launch_bounds__(256) k_unit_shared_div(const double* a, const double* b, int n, double* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const SharedDiv d(b[i]);
+    out[2 * i] = d.div(a[i]);
+    out[2 * i + 1] = a[i] / b[i];
+}
+
+int debug_shared_div(const double* a, const double* b, int n, double* out) {
+    if (n <= 0) return 0;
+    double* d = nullptr;
+    ORB_HIP_CHECK(hipMalloc(&d, sizeof(double) * 4 * (size_t)n));
+    ORB_HIP_CHECK(hipMemcpy(d, a, sizeof(double) * n, hipMemcpyHostToDevice));
+    ORB_HIP_CHECK(hipMemcpy(d + n, b, sizeof(double) * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_unit_shared_div, dim3((n + 255) / 256), dim3(256), 0, 0, d, d + n, n, d + 2 * n);
+    ORB_HIP_CHECK(hipGetLastError());
+    ORB_HIP_CHECK(hipMemcpy(out, d + 2 * n, sizeof(double) * 2 * (size_t)n, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return 0;
 }
 
 // instrumented builds only: read and clear this unit's section timers

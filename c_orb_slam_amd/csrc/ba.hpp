@@ -201,6 +201,7 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant);
 int debug_csum(const double* v, int n, double* out);
 int debug_ldlt_factor(int n, const double* S, double* out);
 int debug_wave_tree(const double* v64, double* out);
+int debug_shared_div(const double* a, const double* b, int n, double* out);
 int debug_set_csum_lds_max(int v);
 int debug_prof(unsigned long long* out32);
 

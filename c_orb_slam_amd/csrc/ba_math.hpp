@@ -14,11 +14,50 @@ namespace orbgpu {
 // ---------------------------------------------------------------- math (host + device)
 #define HD __host__ __device__ __forceinline__
 
+// ---------------------------------------------------------------- shared-denominator division
+// Correctly rounded a / b for several numerators of one denominator.  gfx950 divides as
+//   b' = v_div_scale(b, b, a); r = v_rcp(b'); a' = v_div_scale(a, b, a) (VCC);
+//   e = fma(-b', r, 1); r = fma(r, e, r); e = fma(-b', r, 1); r = fma(r, e, r);
+//   q = a' r; rem = fma(-b', q, a'); q = v_div_fmas(rem, r, q) (VCC); v_div_fixup(q, b, a).
+// v_div_scale returns its operand unchanged and clears VCC unless an exponent is near the
+// range limits (the quotient or 1/b near over/underflow, an exponent gap >= 768), so inside
+// 2^-300 < |a|, |b| < 2^300 the sequence is exactly: r from b alone, then per numerator
+// q = a r, rem = fma(-b, q, a), fma(rem, r, q), v_div_fixup.  The reciprocal is computed once;
+// numerators outside the range (zeros included) take the plain division.
+struct SharedDiv {
+    double b, r;
+    bool ok;
+    __device__ __forceinline__ explicit SharedDiv(double den) : b(den) {
+        const double ab = fabs(den);
+        ok = ab > 0x1p-300 && ab < 0x1p300;
+        double x = __builtin_amdgcn_rcp(den);
+        double e = fma(-den, x, 1.0);
+        x = fma(x, e, x);
+        e = fma(-den, x, 1.0);
+        r = fma(x, e, x);
+    }
+    __device__ __forceinline__ double div(double a) const {
+        const double aa = fabs(a);
+        if (ok && aa > 0x1p-300 && aa < 0x1p300) {
+            const double q = a * r;
+            const double rem = fma(-b, q, a);
+            return __builtin_amdgcn_div_fixup(fma(rem, r, q), b, a);
+        }
+        return a / b;
+    }
+};
+
+
 HD void quat_normalize(double* q) {
     const double z = ((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3];
     if (z > 0) {
         const double n = sqrt(z);
+#ifdef __HIP_DEVICE_COMPILE__
+        const SharedDiv d(n);   // the same quotients, one reciprocal
+        for (int i = 0; i < 4; i++) q[i] = d.div(q[i]);
+#else
         for (int i = 0; i < 4; i++) q[i] = q[i] / n;
+#endif
     }
 }
 

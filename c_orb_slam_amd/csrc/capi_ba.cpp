@@ -417,6 +417,14 @@ int orbgpu_unit_wave_tree(const double* v64, double* out) {
     return orbgpu::debug_wave_tree(v64, out) ? ORB_E_HIP : ORB_OK;
 }
 
+int orbgpu_unit_shared_div(const double* a, const double* b, int n, double* out) {
+    if (!a || !b || !out || n < 0) return ORB_E_INVALID;
+    int rc = 0;
+    engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    return orbgpu::debug_shared_div(a, b, n, out) ? ORB_E_HIP : ORB_OK;
+}
+
 int orbgpu_unit_csum(const double* v, int n, double* out) {
     if (n < 0 || (n > 0 && !v) || !out) return ORB_E_INVALID;
     int rc = 0;

@@ -166,7 +166,6 @@ __global__ void __launch_bounds__(256) k_ldlt_update(SpDev S, int t0) {
 // holds U (d on the diagonal) in its upper triangle and L strictly below.
 __global__ void __launch_bounds__(64) k_ldlt_pdiag(SpDev S, int j0) {
     __shared__ double Ls[LT * LP];
-    __shared__ double dsh[LT];
     if (*(volatile int*)S.fail) return;
     const int p = S.stepP[j0 + blockIdx.x];
     const int lane = threadIdx.x;
@@ -180,9 +179,7 @@ __global__ void __launch_bounds__(64) k_ldlt_pdiag(SpDev S, int j0) {
 #pragma unroll
     for (int k = 0; k < LT; k++) {
         if (k < pw && !bad) {
-            if (lane == k) dsh[k] = col[k];
-            __builtin_amdgcn_wave_barrier();
-            const double d = dsh[k];
+            const double d = rdlane(col[k], k);   // the pivot, from lane k's register (no LDS round trip)
             if (d == 0.0) {
                 bad = true;
             } else {

@@ -826,6 +826,9 @@ int orbgpu_unit_ba_struct(int nkf, int npt, int ne, const int32_t* edge_kf, cons
                           const int32_t* pt_id, int level, int32_t* out, long long cap);
 /* one wave's canonical 64-tree of v64[0..64) (cross-lane permlane/DPP path) */
 int orbgpu_unit_wave_tree(const double* v64, double* out);
+/* The BA kernels' shared-denominator division (SharedDiv, ba_math.hpp) against the plain FP64
+ * division on n pairs: out[2i] = SharedDiv(b[i]).div(a[i]), out[2i + 1] = a[i] / b[i]. */
+int orbgpu_unit_shared_div(const double* a, const double* b, int n, double* out);
 /* Test knob: the BA chi2 canonical sum keeps at most m2_max level-2 trees in LDS (default and
  * maximum 1024, i.e. 4.2 M edges) and writes larger sets to its chunk buffer's tail; 0 sends
  * every problem down the tail path.  Process-wide, device-side. */
