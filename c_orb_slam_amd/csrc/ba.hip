@@ -779,14 +779,20 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
                     Lb[t][c] = 0.0;
                 }
             bool bad = false;
+            // each pivot divides up to 5 block entries and then this thread's column entry: one
+            // reciprocal per pivot (SharedDiv, the division's own quotients) instead of VCC-serialised
+            // divisions
+            SharedDiv sd[6] = {SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0),
+                               SharedDiv(1.0)};
 #pragma unroll
             for (int t = 0; t < 6; t++) {
                 dd[t] = Bk[t][t];
                 if (t < pw) {
                     bad |= dd[t] == 0.0;
+                    sd[t] = SharedDiv(dd[t]);
 #pragma unroll
                     for (int t2 = t + 1; t2 < 6; t2++)
-                        if (t2 < pw) Lb[t2][t] = Bk[t][t2] / dd[t];
+                        if (t2 < pw) Lb[t2][t] = sd[t].div(Bk[t][t2]);
 #pragma unroll
                     for (int t2 = t + 1; t2 < 6; t2++)
 #pragma unroll
@@ -803,7 +809,7 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
                 if (t < pw) {
                     const int k = p0 + t;
                     const bool act = j > k && j < n;
-                    const double l = act ? u[t] / dd[t] : 0.0;
+                    const double l = act ? sd[t].div(u[t]) : 0.0;
 #pragma unroll
                     for (int t2 = t + 1; t2 < 6; t2++)
                         if (t2 < pw && j >= p0 + t2) u[t2] -= Lb[t2][t] * u[t];
