@@ -27,6 +27,7 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <thread>
 
 #include "ba_math.hpp"
 #include "ba_struct.hpp"
@@ -2523,6 +2524,26 @@ int BaEngine::carve(bool commit, size_t* total) {
     return 0;
 }
 
+// Host loops over large problems (a global BA's 1.5 M edges) on up to 16 threads, in contiguous
+// ranges; small problems (a local BA) stay on the calling thread
+template <class F>
+static void host_parallel(int n, F f) {
+    const int hw = (int)std::thread::hardware_concurrency();
+    const int T = n >= (1 << 18) ? std::max(1, std::min(16, hw)) : 1;
+    if (T <= 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int chunk = (n + T - 1) / T;
+    for (int t = 1; t < T; t++) {
+        const int a = t * chunk, b = std::min(n, a + chunk);
+        if (a < b) th.emplace_back([&f, a, b] { f(a, b); });
+    }
+    f(0, std::min(n, chunk));
+    for (auto& x : th) x.join();
+}
+
 int BaEngine::upload_problem(const ba_problem* P) {
     nkf_ = P->n_kf;
     npt_ = P->n_pt;
@@ -2549,35 +2570,36 @@ int BaEngine::upload_problem(const ba_problem* P) {
     if (mode_.global) kfLocal_.assign(nkf_, 1);
     ptHasEdge_.assign(npt_, 0);
     for (int i = 0; i < ne_; i++) ptHasEdge_[P->edge_pt[i]] = 1;
-    std::vector<Se3> T(nkf_);
-    for (int k = 0; k < nkf_; k++) host_se3_from_Tcw(P->kf_Tcw + 16 * k, T[k]);
-    std::vector<double> X(3 * (size_t)npt_);
-    for (size_t q = 0; q < X.size(); q++) X[q] = (double)P->pt_pos[q];
-    // Huber deltas: LocalBundleAdjustment sqrt(5.991) (Optimizer.cc:585), BundleAdjustment sqrt(5.99) (:87)
-    const float thMono = (float)std::sqrt(mode_.global ? 5.99 : 5.991), thStereo = (float)std::sqrt(7.815);
-    std::vector<EdgeDev> E(ne_);
-    for (int i = 0; i < ne_; i++) {
-        EdgeDev& e = E[i];
-        std::memset(&e, 0, sizeof(e));
-        e.pt = P->edge_pt[i];
-        e.kf = P->edge_kf[i];
-        e.stereo = !(P->edge_obs[3 * i + 2] < 0);
-        for (int j = 0; j < 3; j++) e.obs[j] = (double)P->edge_obs[3 * i + j];
-        e.info = (double)P->edge_inv_sigma2[i];
-        const float* cam = P->kf_cam + 5 * e.kf;
-        e.fx = cam[0]; e.fy = cam[1]; e.cx = cam[2]; e.cy = cam[3]; e.bf = cam[4];
-        e.delta = (double)(e.stereo ? thStereo : thMono);
-        e.dsqr = e.delta * e.delta;
-    }
-    level_.assign(ne_, 0);
-    hipStream_t s = stream_;
-    // poses, points and edges through one pinned staging block, one wait
-    const size_t bT = sizeof(Se3) * nkf_, bX = sizeof(double) * X.size(), bE = sizeof(EdgeDev) * ne_;
+    // poses, points and edges written straight into the pinned staging block (no intermediate
+    // host copy), uploaded with one wait
+    const size_t bT = sizeof(Se3) * nkf_, bX = sizeof(double) * 3 * (size_t)npt_, bE = sizeof(EdgeDev) * ne_;
     if (int e = stage_reserve(bT + bX + bE + 64)) return e;
     char* st = (char*)hStage_;
-    std::memcpy(st, T.data(), bT);
-    std::memcpy(st + bT, X.data(), bX);
-    std::memcpy(st + bT + bX, E.data(), bE);
+    Se3* Ts = reinterpret_cast<Se3*>(st);
+    double* Xs = reinterpret_cast<double*>(st + bT);
+    EdgeDev* Es = reinterpret_cast<EdgeDev*>(st + bT + bX);
+    for (int k = 0; k < nkf_; k++) host_se3_from_Tcw(P->kf_Tcw + 16 * k, Ts[k]);
+    for (size_t q = 0; q < 3 * (size_t)npt_; q++) Xs[q] = (double)P->pt_pos[q];
+    // Huber deltas: LocalBundleAdjustment sqrt(5.991) (Optimizer.cc:585), BundleAdjustment sqrt(5.99) (:87)
+    const float thMono = (float)std::sqrt(mode_.global ? 5.99 : 5.991), thStereo = (float)std::sqrt(7.815);
+    host_parallel(ne_, [&](int a, int b) {
+        for (int i = a; i < b; i++) {
+            EdgeDev e;
+            std::memset(&e, 0, sizeof(e));
+            e.pt = P->edge_pt[i];
+            e.kf = P->edge_kf[i];
+            e.stereo = !(P->edge_obs[3 * i + 2] < 0);
+            for (int j = 0; j < 3; j++) e.obs[j] = (double)P->edge_obs[3 * i + j];
+            e.info = (double)P->edge_inv_sigma2[i];
+            const float* cam = P->kf_cam + 5 * e.kf;
+            e.fx = cam[0]; e.fy = cam[1]; e.cx = cam[2]; e.cy = cam[3]; e.bf = cam[4];
+            e.delta = (double)(e.stereo ? thStereo : thMono);
+            e.dsqr = e.delta * e.delta;
+            Es[i] = e;
+        }
+    });
+    level_.assign(ne_, 0);
+    hipStream_t s = stream_;
     if (bT) ORB_HIP_CHECK(hipMemcpyAsync(dT_, st, bT, hipMemcpyHostToDevice, s));
     if (bX) ORB_HIP_CHECK(hipMemcpyAsync(dX_, st + bT, bX, hipMemcpyHostToDevice, s));
     if (bE) ORB_HIP_CHECK(hipMemcpyAsync(dE_, st + bT + bX, bE, hipMemcpyHostToDevice, s));
@@ -2641,21 +2663,23 @@ int BaEngine::build_structure(int level) {
                                                       &blkJ,    &blkStart, &pairA, &pairB};
     size_t tot = 0;
     for (auto* p : parts) tot += (p->size() + 63) & ~(size_t)63;
-    hStruct_.assign(tot, 0);
-    std::vector<size_t> off;
-    size_t o = 0;
-    for (auto* p : parts) {
-        off.push_back(o);
-        std::copy(p->begin(), p->end(), hStruct_.begin() + o);
-        o += (p->size() + 63) & ~(size_t)63;
-    }
     if (tot * 4 > dStructCap_) {
         if (dStruct_) (void)hipFree(dStruct_);
         ORB_HIP_CHECK(hipMalloc(&dStruct_, tot * 4 * 2));
         dStructCap_ = tot * 4 * 2;
     }
     if (int e = stage_reserve(tot * 4)) return e;   // copied below, waited for at the end
-    std::memcpy(hStage_, hStruct_.data(), tot * 4);
+    // the lists packed straight into the pinned staging block (64-entry aligned sections)
+    int32_t* hs = reinterpret_cast<int32_t*>(hStage_);
+    std::vector<size_t> off;
+    size_t o = 0;
+    for (auto* p : parts) {
+        off.push_back(o);
+        const size_t len = p->size(), padded = (len + 63) & ~(size_t)63;
+        if (len) std::memcpy(hs + o, p->data(), sizeof(int32_t) * len);
+        std::memset(hs + o + len, 0, sizeof(int32_t) * (padded - len));
+        o += padded;
+    }
     ORB_HIP_CHECK(hipMemcpyAsync(dStruct_, hStage_, tot * 4, hipMemcpyHostToDevice, stream_));
     // the sharded and block-sparse set-ups below stage more uploads through the same block
     if (comm_ || nP >= kTiledMinPoses) ORB_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -3076,6 +3100,7 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
         return 0;
     }
     if (int e = upload_problem(P)) return e;
+    const auto t_up = clk::now();
     if (comm_) {  // every shard takes the same early-return decision
         if (int e = reduce_stop(stop)) return e;
     }
@@ -3087,6 +3112,7 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
         R->aborted = 1;
         return 0;
     }
+    const auto t_opt0 = clk::now();
     if (mode_.global) {
         // Optimizer::BundleAdjustment: initializeOptimization(); optimize(nIterations) (Optimizer.cc:190-191)
         if (st_.nP + nLglob_ > 0)
@@ -3111,6 +3137,7 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
         if (int e = gate_edges(1, R->edge_erase)) return e;
         for (int i = 0; i < ne_; i++) R->n_erased += R->edge_erase[i];
     }
+    const auto t_opt1 = clk::now();
     std::vector<Se3> T(nkf_);
     std::vector<double> X(3 * (size_t)npt_);
     {   // poses and points back through the staging block, one wait
@@ -3132,6 +3159,15 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
             for (int k = 0; k < 3; k++) R->pt_pos[3 * p + k] = (float)X[3 * p + k];
     last_ms[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     last_ms[1] = t_struct;
+    static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;   // host-phase breakdown (tools/)
+    if (say) {
+        auto ms = [](clk::time_point a, clk::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        fprintf(stderr, "[ba] call %.1f ms: upload %.1f, structure %.1f, optimize %.1f (incl. the second pass's "
+                        "structure), readback %.1f\n", last_ms[0], ms(t0, t_up), t_struct, ms(t_opt0, t_opt1),
+                ms(t_opt1, clk::now()));
+    }
     comm_ = nullptr;
     return 0;
 }

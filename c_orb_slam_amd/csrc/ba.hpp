@@ -116,7 +116,6 @@ private:
     std::vector<uint8_t> kfFixed_, kfLocal_, level_, ptHasEdge_;
     // structure
     BaStructDev st_{};
-    std::vector<int32_t> hStruct_;
     BaHostStruct hs_;              // host lists of the current structure (reused across calls)
     int32_t* dStruct_ = nullptr;
     size_t dStructCap_ = 0;
