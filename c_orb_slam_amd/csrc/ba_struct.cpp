@@ -8,7 +8,9 @@
 #include "ba_struct.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <numeric>
+#include <thread>
 
 namespace orbgpu {
 
@@ -149,23 +151,61 @@ int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, con
     const int nPair = S->blkStart[nBlk];
     S->pairA.resize(std::max(nPair, 1));
     S->pairB.resize(std::max(nPair, 1));
+    // fill: each block's terms in landmark order.  Large systems (a global BA) split the landmarks
+    // into T contiguous ranges: per-range block counts, per-block prefix over the ranges (range t
+    // starts after ranges < t), then every range fills its own slots -- the same order.
     {
-        std::vector<int32_t> fb(S->blkStart.begin(), S->blkStart.end() - 1);
-        int32_t* __restrict__ fbp = fb.data();
         int32_t* __restrict__ pa = S->pairA.data();
         int32_t* __restrict__ pb = S->pairB.data();
         const int32_t* __restrict__ bo = blkOf.data();
-        for (int l = 0; l < nL; l++) {
-            const int b0 = qs[l], b1 = qs[l + 1];
-            for (int u = b0; u < b1; u++) {
-                const int32_t* __restrict__ row = bo + (size_t)qp[u] * nP;
-                const int au = ql[u];
-                for (int v = u; v < b1; v++) {
-                    const int q = fbp[row[qp[v]]]++;
-                    pa[q] = au;
-                    pb[q] = ql[v];
+        const char* env = getenv("ORBGPU_STRUCT_THREADS");
+        const int hw = (int)std::thread::hardware_concurrency();
+        int T = env ? atoi(env) : (nPair >= (1 << 18) ? std::min(16, std::max(1, hw)) : 1);
+        T = std::max(1, std::min(T, std::max(1, nL)));
+        auto walk = [&](int l0, int l1, int32_t* cur, bool fill) {
+            for (int l = l0; l < l1; l++) {
+                const int b0 = qs[l], b1 = qs[l + 1];
+                for (int u = b0; u < b1; u++) {
+                    const int32_t* __restrict__ row = bo + (size_t)qp[u] * nP;
+                    const int au = ql[u];
+                    for (int v = u; v < b1; v++) {
+                        const int b = row[qp[v]];
+                        if (fill) {
+                            const int q = cur[b]++;
+                            pa[q] = au;
+                            pb[q] = ql[v];
+                        } else {
+                            cur[b]++;
+                        }
+                    }
                 }
             }
+        };
+        if (T == 1) {
+            std::vector<int32_t> fb(S->blkStart.begin(), S->blkStart.end() - 1);
+            walk(0, nL, fb.data(), true);
+        } else {
+            const int chunk = (nL + T - 1) / T;
+            std::vector<std::vector<int32_t>> cur(T, std::vector<int32_t>(nBlk, 0));
+            auto par = [&](auto f) {
+                std::vector<std::thread> th;
+                for (int t = 1; t < T; t++) th.emplace_back([&f, t] { f(t); });
+                f(0);
+                for (auto& x : th) x.join();
+            };
+            par([&](int t) { walk(std::min(nL, t * chunk), std::min(nL, (t + 1) * chunk), cur[t].data(), false); });
+            par([&](int t) {   // blocks [t * bc, (t + 1) * bc): counts -> starting slots per range
+                const int bc = (nBlk + T - 1) / T;
+                for (int b = std::min(nBlk, t * bc); b < std::min(nBlk, (t + 1) * bc); b++) {
+                    int base = S->blkStart[b];
+                    for (int r = 0; r < T; r++) {
+                        const int c = cur[r][b];
+                        cur[r][b] = base;
+                        base += c;
+                    }
+                }
+            });
+            par([&](int t) { walk(std::min(nL, t * chunk), std::min(nL, (t + 1) * chunk), cur[t].data(), true); });
         }
     }
     return 0;
