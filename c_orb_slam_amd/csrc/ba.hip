@@ -180,10 +180,15 @@ __device__ __forceinline__ void block_finish_csum(double* c, int m, int nterms, 
     double* L = m2 <= min(g_csum_lds_max, 1024) ? lv : c + m;
     for (int t = threadIdx.x; t < m2; t += blockDim.x)
         L[t] = tree64_local([&](int k) { return c[t * 64 + k]; }, min(64, m - t * 64));
-    __threadfence();
+    __threadfence_block();   // L may be the chunk buffer's tail: read by thread 0 of this block
     __syncthreads();
     if (threadIdx.x == 0) *out = local_csum_inplace(L, m2);
 }
+
+// The chi2 total of k_linearize's chunk trees, one workgroup.  A launch of its own: the kernel
+// boundary orders the chunk stores for this reader, where the former last-block-finishes
+// pattern needed a device-scope fence in every wave (an L2 writeback + invalidate on gfx950).
+__global__ void __launch_bounds__(256) k_chi2_finish(LinArgs a);
 
 __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
     BA_GATE(a.run);
@@ -208,20 +213,11 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
         if (robust) huber(e, chi, &r0, &rho1);
         a.rc[i] = r0;
     }
-    // activeRobustChi2: chunk tree per wave (64 consecutive active edges), last block finishes
+    // activeRobustChi2: chunk tree per wave (64 consecutive active edges); k_chi2_finish sums
+    // the chunks in its own launch
     {
         const double t = wave_tree(r0);
         if ((threadIdx.x & 63) == 0) a.chunks[i >> 6] = t;
-        __threadfence();
-        __syncthreads();
-        __shared__ bool last;
-        if (threadIdx.x == 0) last = atomicAdd(a.counter, 1u) == gridDim.x - 1;
-        __syncthreads();
-        if (last) {
-            __threadfence();
-            block_finish_csum(a.chunks, (a.s.nE + 63) >> 6, a.s.nE, a.rc, a.out);
-            if (threadIdx.x == 0) *a.counter = 0;
-        }
     }
     if (!valid || !a.linearize) return;
     {
@@ -334,6 +330,11 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
         }
     }
     }
+}
+
+__global__ void __launch_bounds__(256) k_chi2_finish(LinArgs a) {
+    BA_GATE(a.run);
+    block_finish_csum(a.chunks, (a.s.nE + 63) >> 6, a.s.nE, a.rc, a.out);
 }
 
 // Reduce chunk sums arr[0..m) (already level-1 trees) to the canonical total, one wave.
@@ -2814,7 +2815,10 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const bool own = !comm_ || comm_->rank() == 0;
     LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1, tmpA0_, dCounter_, dScal_ + 0, nullptr};
     if (comm_ && !nE) ORB_HIP_CHECK(hipMemsetAsync(dScal_, 0, 2 * sizeof(double), s));
-    if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+    if (nE) {
+        hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+        hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+    }
     if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(1024), 0, s, S, dTerms_, dHpp_, dBp_, nullptr);
     if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(12 * nL, 256)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_, nullptr);
     if (comm_) {
@@ -2887,7 +2891,10 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         // computeActiveErrors + activeRobustChi2 ; computeScale
         la.linearize = 0;
         la.out = dScal_ + 1;
-        if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+        if (nE) {
+            hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+            hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+        }
         if (6 * nP + 3 * nL <= 2048 * 64) {
             hipLaunchKernelGGL(k_scale, dim3(1), dim3(1024), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_, use_dev, dScal_,
                                dScal_ + 2, own ? 1 : 0, nullptr);
@@ -2991,7 +2998,10 @@ void BaEngine::enqueue_lm_step(bool first) {
     const int nE = S.nE, nP = S.nP, nL = S.nL;
     const int* ctl = dLm_->ctl;
     LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1, tmpA0_, dCounter_, dScal_ + 0, ctl + 1};
-    if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+    if (nE) {
+        hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+        hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+    }
     if (nP + nL) hipLaunchKernelGGL(k_sys_reduce, dim3(nP + nblk(12 * nL, 1024)), dim3(1024), 0, s, S, dTerms_, dHpp_,
                                     dBp_, dHll_, dBl_, ctl + 1);
     if (first) hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, nP, nL, dHpp_, dHll_, dScal_, ctl + 2);
@@ -3013,7 +3023,10 @@ void BaEngine::enqueue_lm_step(bool first) {
     la.linearize = 0;
     la.out = dScal_ + 1;
     la.run = ctl;
-    if (nE) hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+    if (nE) {
+        hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+        hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+    }
     const bool small = 6 * nP + 3 * nL <= 2048 * 64;
     if (!small) {
         const int nv = 6 * nP + 3 * nL;
