@@ -2618,6 +2618,15 @@ int BaEngine::upload_problem(const ba_problem* P) {
 
 // initializeOptimization(level) + buildIndexMapping + BlockSolver::buildStructure
 int BaEngine::build_structure(int level) {
+    using sclk = std::chrono::steady_clock;
+    static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;
+    auto ts0 = sclk::now();
+    auto lap = [&](const char* what) {   // ORBGPU_BA_TIMES: the structure build's phases
+        if (!say) return;
+        const auto t = sclk::now();
+        fprintf(stderr, "[ba]   structure %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - ts0).count());
+        ts0 = t;
+    };
     BaHostStruct& H = hs_;
     std::vector<uint8_t> kfAct, ptAct;
     ba_active_set(level, nkf_, npt_, ne_, eKf_.data(), ePt_.data(), level_.data(), &H.aE, &kfAct, &ptAct);
@@ -2638,9 +2647,11 @@ int BaEngine::build_structure(int level) {
         nEglob_ = (int)red[nkf_];
         nLglob_ = (int)red[nkf_ + 1];
     }
+    lap("active set");
     if (ba_build_lists(nkf_, npt_, eKf_.data(), ePt_.data(), kfFixed_.data(), kfId_.data(), ptId_.data(), kfAct, ptAct,
                        &H))
         return -1;
+    lap("lists");
     const int nE = (int)H.aE.size(), nP = (int)H.poseKf.size(), nL = (int)H.landPt.size();
     if (!comm_) {
         nEglob_ = nE;
@@ -2722,7 +2733,9 @@ int BaEngine::build_structure(int level) {
         }
         for (int64_t q : all) adj[fillp[q % nP]++] = (int)(q / nP);
         for (int i = 0; i < nP; i++) std::sort(adj.begin() + as[i], adj.begin() + as[i + 1]);
+        lap("pack + pose graph");
         if (int e = sp_.build(6 * nP, 6, as, adj, true, stream_)) return e;
+        lap("nested dissection + symbolic factorisation");
     } else if (comm_ && nP > 0) {
         // dense system: the 64x64 tiles the Schur blocks touch (union over the shards)
         const int n = 6 * nP, nt = (n + 63) / 64;
