@@ -2528,9 +2528,9 @@ int BaEngine::carve(bool commit, size_t* total) {
 // Host loops over large problems (a global BA's 1.5 M edges) on up to 16 threads, in contiguous
 // ranges; small problems (a local BA) stay on the calling thread
 template <class F>
-static void host_parallel(int n, F f) {
+static void host_parallel(int n, F f, int minN = 1 << 18) {
     const int hw = (int)std::thread::hardware_concurrency();
-    const int T = n >= (1 << 18) ? std::max(1, std::min(16, hw)) : 1;
+    const int T = n >= minN ? std::max(1, std::min(16, hw)) : 1;
     if (T <= 1) {
         f(0, n);
         return;
@@ -2681,17 +2681,27 @@ int BaEngine::build_structure(int level) {
         dStructCap_ = tot * 4 * 2;
     }
     if (int e = stage_reserve(tot * 4)) return e;   // copied below, waited for at the end
-    // the lists packed straight into the pinned staging block (64-entry aligned sections)
+    // the lists packed straight into the pinned staging block (64-entry aligned sections), the
+    // copy split over host threads in 64-entry groups on large systems
     int32_t* hs = reinterpret_cast<int32_t*>(hStage_);
     std::vector<size_t> off;
     size_t o = 0;
     for (auto* p : parts) {
         off.push_back(o);
-        const size_t len = p->size(), padded = (len + 63) & ~(size_t)63;
-        if (len) std::memcpy(hs + o, p->data(), sizeof(int32_t) * len);
-        std::memset(hs + o + len, 0, sizeof(int32_t) * (padded - len));
-        o += padded;
+        o += (p->size() + 63) & ~(size_t)63;
     }
+    host_parallel((int)(tot / 64), [&](int g0, int g1) {
+        const size_t a = (size_t)g0 * 64, b = (size_t)g1 * 64;
+        for (size_t k = 0; k < parts.size(); k++) {
+            const size_t s0 = off[k], len = parts[k]->size(), e0 = s0 + ((len + 63) & ~(size_t)63);
+            const size_t x0 = std::max(a, s0), x1 = std::min(b, e0);
+            if (x0 >= x1) continue;
+            const size_t d1 = std::min(x1, s0 + len);   // list entries [x0, d1), zero padding [d1, x1)
+            if (x0 < d1) std::memcpy(hs + x0, parts[k]->data() + (x0 - s0), sizeof(int32_t) * (d1 - x0));
+            const size_t z0 = std::max(x0, s0 + len);
+            if (z0 < x1) std::memset(hs + z0, 0, sizeof(int32_t) * (x1 - z0));
+        }
+    }, 1 << 14);
     ORB_HIP_CHECK(hipMemcpyAsync(dStruct_, hStage_, tot * 4, hipMemcpyHostToDevice, stream_));
     // the sharded and block-sparse set-ups below stage more uploads through the same block
     if (comm_ || nP >= kTiledMinPoses) ORB_HIP_CHECK(hipStreamSynchronize(stream_));

@@ -8,6 +8,8 @@
 #include "ba_struct.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <numeric>
 #include <thread>
@@ -40,6 +42,15 @@ static void by_id(int n, const uint8_t* flag, const int32_t* id, std::vector<int
 int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, const uint8_t* kfFixed,
                    const int32_t* kfId, const int32_t* ptId, const std::vector<uint8_t>& kfAct,
                    const std::vector<uint8_t>& ptAct, BaHostStruct* S) {
+    static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;   // the phases below (tools/)
+    using sclk = std::chrono::steady_clock;
+    auto ts0 = sclk::now();
+    auto lap = [&](const char* what) {
+        if (!say) return;
+        const auto t = sclk::now();
+        fprintf(stderr, "[ba]     lists: %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - ts0).count());
+        ts0 = t;
+    };
     std::vector<uint8_t> freeKf(nkf);
     for (int k = 0; k < nkf; k++) freeKf[k] = kfAct[k] && !kfFixed[k];
     by_id(nkf, freeKf.data(), kfId, &S->poseKf);
@@ -79,6 +90,7 @@ int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, con
             qs[i + 1] += qs[i];
         }
     }
+    lap("index maps + counts");
     const int nPe = S->peStart[nP], nLe = S->leStart[nL], nLp = S->lpStart[nL];
     S->peList.resize(std::max(nPe, 1));
     S->leList.resize(std::max(nLe, 1));
@@ -109,12 +121,14 @@ int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, con
                 qp[q] = p;
             }
     }
+    lap("edge lists");
     const int32_t* __restrict__ qs = S->lpStart.data();
     const int32_t* __restrict__ ql = S->lpList.data();
     const int32_t* __restrict__ qp = lpPose.data();
     for (int l = 0; l < nL; l++)   // one edge per (pose, landmark)
         for (int j = qs[l] + 1; j < qs[l + 1]; j++)
             if (qp[j] == qp[j - 1]) return -1;
+    lap("duplicate check");
     // Schur pattern: diagonal blocks first, then blocks in order of first use (landmark order,
     // pose pairs u <= v); one pass numbers and counts, one pass fills
     std::vector<int32_t> blkOf((size_t)nP * nP, -1), bi, bj, cnt;
@@ -143,6 +157,7 @@ int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, con
             }
         }
     }
+    lap("block numbering + counts");
     const int nBlk = (int)bi.size();
     S->blkI.swap(bi);
     S->blkJ.swap(bj);
@@ -208,6 +223,7 @@ int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, con
             par([&](int t) { walk(std::min(nL, t * chunk), std::min(nL, (t + 1) * chunk), cur[t].data(), true); });
         }
     }
+    lap("pair fill");
     return 0;
 }
 
