@@ -443,6 +443,8 @@ def main():
             tl, tr = self.tl, self.tr
             for k in tl:
                 stage_acc[k] = stage_acc.get(k, 0.0) + tl[k] + tr[k]
+                stage_lr["left"][k] = stage_lr["left"].get(k, 0.0) + tl[k]
+                stage_lr["right"][k] = stage_lr["right"].get(k, 0.0) + tr[k]
             kernel_ms.append(tl["fast_cells"])
             kernel_ms.append(tr["fast_cells"])
             pose_inl.append(int(self.ninl2.sum()))
@@ -767,6 +769,7 @@ def main():
         return out
 
     stage_acc = {}
+    stage_lr = {"left": {}, "right": {}}   # the same per extractor stream (left / right images)
     phase_acc = {}
     local_acc = []
     pose_inl = []
@@ -824,6 +827,8 @@ def main():
     drain()
     step()   # prime the pipeline: one batch extracted, awaiting tracking
     stage_acc.clear()
+    for d in stage_lr.values():
+        d.clear()
     phase_acc.clear()
     kernel_ms.clear()
     pose_inl.clear()
@@ -869,7 +874,10 @@ def main():
             line = {"nfeatures": NFEAT, "value": round(fps, 2), "unit": "frames/s", "steps": args.steps,
                     "ms_per_step": round(dt / args.steps * 1e3, 3), "tracked_frames_per_step": P,
                     "matches_per_s": round(tot_match / dt, 1),
-                    "keypoints_per_image": round(tot_kp / (2 * B * args.steps * world), 1), "cpu_baseline": cpu}
+                    "keypoints_per_image": round(tot_kp / (2 * B * args.steps * world), 1), "cpu_baseline": cpu,
+                    "stage_ms_per_step_by_image": {side: {k: round(v / args.steps, 4) for k, v in d.items()}
+                                                   for side, d in stage_lr.items()},
+                    "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}}
             if cpu:
                 line["speedup_vs_cpu_all_core"] = round(fps / cpu["value"], 1)
             json_out.write(json.dumps(line) + "\n")
@@ -996,6 +1004,8 @@ def main():
             "local_map_matches_per_frame": round(float(sum(a for a, _ in local_acc)) / max(len(local_acc) * P, 1), 1),
             "local_map_visible_per_frame": round(float(sum(b for _, b in local_acc)) / max(len(local_acc) * P, 1), 1),
             "stage_ms_per_step": stage_ms,
+            "stage_ms_per_step_by_image": {side: {k: round(v / args.steps, 4) for k, v in d.items()}
+                                           for side, d in stage_lr.items()},
             "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}, "roofline": roof,
             "matcher_roofline": mroof, "latency": latency, "cpu_baseline": cpu, "local_ba": ba,
             "global_ba": gba, "ransac": ransac, "nfeatures_2000": nf2000,
