@@ -1377,11 +1377,11 @@ def _streams(P, fn):
     return res, time.perf_counter() - t0
 
 
-def gba_cpu_baseline(n_kf, laps, n_its=3):
+def gba_cpu_baseline(n_kf, laps, n_its=10):
     """Oracle BundleAdjustment(nIterations=n_its, bRobust=false) on the same config-5 problem: one
     call per stream, P independent streams (all-core) and the single stream alongside.  Rate =
-    LM iterations (solve() calls) per second; n_its = 3 bounds the sample (the GPU leg's 10-
-    iteration calls include the same per-call structure build)."""
+    LM iterations (solve() calls) per second including the per-call set-up, with the GPU leg's
+    nIterations (10, LoopClosing.cc:650) so both spread their set-up over the same iterations."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
     from ba_cases import global_ba_problem

@@ -16,6 +16,7 @@
 // Every accumulation uses the canonical 64-wide tree order (oracle/ba.c ora_csum),
 // so results are bit-identical to the CPU restatement.
 #include "ba.hpp"
+#include <atomic>
 
 #include <type_traits>
 
@@ -1170,8 +1171,12 @@ __global__ void __launch_bounds__(1024) k_lm_trial_end(LmDev* L, double* scal, v
                                                        Se3* T, const Se3* Tbak, double* X, const double* Xbak,
                                                        const double* x, const double* bp, const double* bl, int scale) {
     __shared__ double lv[2048];
-    __shared__ int pop;
-    if (!L->ctl[0]) return;   // a step queued after the run ended
+    __shared__ int pop, live;
+    // one read of the run flag for the whole workgroup: lm_decide below may clear ctl[0] (the
+    // run ends with this trial) and a wave reading it after that would skip the pop
+    if (threadIdx.x == 0) live = L->ctl[0];
+    __syncthreads();
+    if (!live) return;   // a step queued after the run ended
     const int nP = s.nP, nL = s.nL;
     if (scale) {
         const int n = 6 * nP + 3 * nL;
@@ -2823,6 +2828,17 @@ int BaEngine::gather_blocks(const std::vector<int64_t>& mine, std::vector<int64_
 
 static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 
+// computeScale in one workgroup (k_scale / k_lm_trial_end) up to this many terms, above it
+// k_scale_chunks + k_csum; orbgpu_unit_set_scale_small_max lowers it so tests drive the chunked
+// path (and the device LM's scale == 0 branch) at oracle-sized problems
+static std::atomic<int> g_scale_small_max{2048 * 64};
+static bool scale_small(int nP, int nL) { return 6 * nP + 3 * nL <= g_scale_small_max.load(); }
+int debug_set_scale_small_max(int v) {
+    if (v < 0 || v > 2048 * 64) return 1;
+    g_scale_small_max.store(v);
+    return 0;
+}
+
 // OptimizationAlgorithmLevenberg::solve (optimization_algorithm_levenberg.cpp:59-164)
 // Sharded (comm_ set): the pose rows of H and the Schur complement are sums over the shards'
 // points, so each shard reduces its own edges and the exchange steps are
@@ -2918,7 +2934,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
             hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
             hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
         }
-        if (6 * nP + 3 * nL <= 2048 * 64) {
+        if (scale_small(nP, nL)) {
             hipLaunchKernelGGL(k_scale, dim3(1), dim3(1024), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_, use_dev, dScal_,
                                dScal_ + 2, own ? 1 : 0, nullptr);
         } else {
@@ -3050,7 +3066,7 @@ void BaEngine::enqueue_lm_step(bool first) {
         hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
         hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
     }
-    const bool small = 6 * nP + 3 * nL <= 2048 * 64;
+    const bool small = scale_small(nP, nL);
     if (!small) {
         const int nv = 6 * nP + 3 * nL;
         hipLaunchKernelGGL(k_scale_chunks, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dX2_, dBp_, dBl_, 0.0, 1,

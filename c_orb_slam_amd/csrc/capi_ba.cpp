@@ -365,6 +365,16 @@ int orbgpu_debug_prof_match(unsigned long long* out32) {
 int orbgpu_unit_nd_order(int n, const int32_t* adjStart, const int32_t* adj, int leaf, int32_t* perm,
                          int32_t* n_nodes, int32_t* height) {
     if (n < 0 || leaf < 1 || (n > 0 && (!adjStart || !adj || !perm))) return ORB_E_INVALID;
+    // the lists must be a well-formed CSR graph: offsets from 0, non-decreasing, every neighbour
+    // in [0, n) and no self loop (nd_order indexes its marks with them unchecked)
+    if (n > 0) {
+        if (adjStart[0] != 0) return ORB_E_INVALID;
+        for (int i = 0; i < n; i++) {
+            if (adjStart[i + 1] < adjStart[i]) return ORB_E_INVALID;
+            for (int e = adjStart[i]; e < adjStart[i + 1]; e++)
+                if (adj[e] < 0 || adj[e] >= n || adj[e] == i) return ORB_E_INVALID;
+        }
+    }
     std::vector<int> as(adjStart, adjStart + n + 1), ad(adj, adj + (n > 0 ? adjStart[n] : 0));
     orbgpu::NdTree t;
     orbgpu::nd_order(n, as, ad, leaf, &t);
@@ -381,6 +391,10 @@ int orbgpu_unit_nd_order(int n, const int32_t* adjStart, const int32_t* adj, int
 int orbgpu_unit_set_csum_lds_max(int m2_max) {
     if (m2_max < 0 || m2_max > 1024) return ORB_E_INVALID;
     return orbgpu::debug_set_csum_lds_max(m2_max) ? ORB_E_HIP : ORB_OK;
+}
+
+int orbgpu_unit_set_scale_small_max(int terms) {
+    return orbgpu::debug_set_scale_small_max(terms) ? ORB_E_INVALID : ORB_OK;
 }
 
 int orbgpu_unit_ba_struct(int nkf, int npt, int ne, const int32_t* edge_kf, const int32_t* edge_pt,

@@ -12,7 +12,8 @@ int orbgpu_device_available(void) {
     return n > 0 ? 1 : 0;
 }
 
-const char* orbgpu_version(void) { return "c_orb_slam_amd 0.1 (gfx950)"; }
+const char* orbgpu_version(void) { return "c_orb_slam_amd 0.2 (gfx950)"; }
+int orbgpu_abi_version(void) { return ORBGPU_ABI_VERSION; }
 
 int ORBextractor_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST,
                         int max_width, int max_height, int max_batch, ORBextractor_h* out) {

@@ -91,35 +91,56 @@ public:
         std::lock_guard<std::mutex> g(mu_);
         cur_dev_outs_.push_back(DevOut{user, dev, bytes});
     }
-    // close the current chain: record its end on `s`; *id = its epoch
+    // close the current chain: record its end on `s`; *id = its epoch.  On a failure the
+    // chain's blocks are released once the stream has drained (nothing queued still reads or
+    // writes them) and the error is also reported by the next finish, so counts are never
+    // dropped silently.
     int close(hipStream_t s, long long* id) {
         // the epoch's device count blocks: one D2H each into a pinned block, mapped to the users
         std::vector<int> devs;
         std::vector<DevOut> douts;
+        std::vector<DevBlock> snap;   // devs_ may grow (dev_counts) once mu_ is released
         {
             std::lock_guard<std::mutex> g(mu_);
             devs.swap(cur_devs_);
             douts.swap(cur_dev_outs_);
             cur_dev_ = -1;
+            for (int k : devs) snap.push_back(devs_[k]);
         }
-        for (int k : devs) {
-            const DevBlock b = devs_[k];
+        bool ok = true;
+        std::vector<Out> mapped;
+        for (const DevBlock& b : snap) {
             if (!b.used) continue;
             char* pin = (char*)take(b.used);
-            if (!pin) return -2;
-            ORB_HIP_CHECK(hipMemcpyAsync(pin, b.p, b.used, hipMemcpyDeviceToHost, s));
+            if (!pin || hipMemcpyAsync(pin, b.p, b.used, hipMemcpyDeviceToHost, s) != hipSuccess) {
+                ok = false;
+                break;
+            }
             for (const DevOut& o : douts)
                 if ((const char*)o.dev >= (const char*)b.p && (const char*)o.dev < (const char*)b.p + b.cap)
-                    cur_outs_.push_back(Out{pin + ((const char*)o.dev - (const char*)b.p), o.user, o.bytes});
+                    mapped.push_back(Out{pin + ((const char*)o.dev - (const char*)b.p), o.user, o.bytes});
         }
         std::lock_guard<std::mutex> g(mu_);
         size_t k = 0;
-        while (k < events_.size() && (events_[k].live || events_[k].waiters > 0)) k++;
-        if (k == events_.size()) {
-            events_.push_back(Ev{});
-            ORB_HIP_CHECK(hipEventCreateWithFlags(&events_[k].ev, hipEventDisableTiming));
+        if (ok) {
+            while (k < events_.size() && (events_[k].live || events_[k].waiters > 0)) k++;
+            if (k == events_.size()) {
+                events_.push_back(Ev{});
+                ok = hipEventCreateWithFlags(&events_[k].ev, hipEventDisableTiming) == hipSuccess;
+            }
+            ok = ok && hipEventRecord(events_[k].ev, s) == hipSuccess;
         }
-        ORB_HIP_CHECK(hipEventRecord(events_[k].ev, s));
+        if (!ok) {
+            fprintf(stderr, "[orbslam_gpu] deferred chain: closing the epoch failed; its counts are lost\n");
+            (void)hipStreamSynchronize(s);
+            for (int d : devs) devs_[d].busy = false;
+            for (int b : cur_blocks_) blocks_[b].busy = false;
+            cur_blocks_.clear();
+            cur_outs_.clear();
+            failed_ = true;
+            return -2;
+        }
+        for (auto& o : mapped) cur_outs_.push_back(o);
         events_[k].live = true;
         const long long e = next_id_++;
         closed_.push_back(Epoch{e, (int)k, std::move(cur_blocks_), std::move(cur_outs_), std::move(devs)});
@@ -154,6 +175,10 @@ public:
             hipEvent_t ev;
             {
                 std::lock_guard<std::mutex> g(mu_);
+                if (failed_) {   // an earlier close() lost its epoch
+                    failed_ = false;
+                    return -2;
+                }
                 if (closed_.empty() || closed_.front().id > id) return 0;
                 k = closed_.front().ev;
                 events_[k].waiters++;
@@ -245,6 +270,7 @@ private:
     std::vector<DevOut> cur_dev_outs_;
     int cur_dev_ = -1;
     long long next_id_ = 1, done_id_ = 0;
+    bool failed_ = false;
 };
 
 constexpr int kEdge = 19;          // EDGE_THRESHOLD, ORBextractor.cc:67

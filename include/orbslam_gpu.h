@@ -43,6 +43,13 @@ typedef struct orb_kp {
 /* Library info: 1 if a HIP device is usable, else 0 (never aborts). */
 int orbgpu_device_available(void);
 const char* orbgpu_version(void);
+/* ABI revision of this header.  A caller compiled against revision R checks
+ * orbgpu_abi_version() == R at start-up: an entry point whose signature changed bumps it.
+ *   1: round 1-3 ABI
+ *   2: ORBmatcher_SearchLocalPoints_batch takes the ORBmatcher(nnratio) float before the
+ *      outputs (a revision-1 binary would pass its pointers with nnratio undefined) */
+#define ORBGPU_ABI_VERSION 2
+int orbgpu_abi_version(void);
 
 /* ======================================================================
  * ORBextractor  (reference include/ORBextractor.h:51-113, src/ORBextractor.cc)
@@ -833,6 +840,10 @@ int orbgpu_unit_shared_div(const double* a, const double* b, int n, double* out)
  * maximum 1024, i.e. 4.2 M edges) and writes larger sets to its chunk buffer's tail; 0 sends
  * every problem down the tail path.  Process-wide, device-side. */
 int orbgpu_unit_set_csum_lds_max(int m2_max);
+/* Test knob: computeScale runs in the LM trial's single workgroup for 6 nP + 3 nL <= terms
+ * (default and maximum 2048 * 64) and as a chunked two-kernel sum above it; 0 sends every
+ * problem down the chunked path.  Process-wide, host-side. */
+int orbgpu_unit_set_scale_small_max(int terms);
 /* The elimination order of the block-sparse pose system (host only, no device): nested
  * dissection of a graph (adjStart[n + 1] / adj: symmetric, sorted lists) with leaves of at
  * most `leaf` nodes; perm[k] = node eliminated k-th; the separator tree's node count and

@@ -35,6 +35,8 @@ static void make_image(uint8_t* img) {
 
 int main(int argc, char** argv) {
     uint8_t a[32], b[32];
+    /* the library implements the ABI revision this caller was compiled against */
+    if (orbgpu_abi_version() != ORBGPU_ABI_VERSION) return fail("ABI revision mismatch", orbgpu_abi_version());
     for (int i = 0; i < 32; i++) {
         a[i] = (uint8_t)(i * 37 + 1);
         b[i] = (uint8_t)(i * 11 + 5);

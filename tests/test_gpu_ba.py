@@ -82,3 +82,22 @@ def test_ba_improves_estimate(gpu):
     T1 = g["kf_Tcw"].reshape(-1, 4, 4)[:, :3, 3]
     Tt = pr["Tcw_true"][:, :3, 3]
     assert np.abs(T1 - Tt).mean() < np.abs(T0 - Tt).mean()
+
+
+@pytest.mark.parametrize("seed,kw", [(0, {}), (5, dict(n_local=12, n_fixed=6, n_pt=800, outlier_frac=0.3))])
+def test_ba_chunked_scale_path_device_lm_matches_oracle(gpu, seed, kw):
+    """computeScale above 2048 * 64 terms runs as k_scale_chunks + k_csum and k_lm_trial_end
+    gets scale == 0: its LM decision then has no barrier of its own before it may end the run,
+    and a rejected final trial must still be undone by every wave.  The knob sends
+    a config-4-sized problem down that path; the device LM must stay bit-identical to the
+    oracle and to the host-driven loop."""
+    from c_orb_slam_amd._lib import lib
+    pr = ba_problem(seed, **kw)
+    assert lib().orbgpu_unit_set_scale_small_max(0) == 0
+    try:
+        g, o = _run_both(pr)
+    finally:
+        assert lib().orbgpu_unit_set_scale_small_max(2048 * 64) == 0
+    _check(g, o)
+    assert np.array_equal(g["kf_Tcw"], o["kf_Tcw"].reshape(g["kf_Tcw"].shape))
+    assert np.array_equal(g["pt_pos"], o["pt_pos"].reshape(g["pt_pos"].shape))

@@ -178,3 +178,32 @@ def test_loop_closed_map_fill_is_bounded():
     nat, nd = fill(np.arange(n)), fill(pos)
     assert nd < nat / 3, (nd, nat)
     assert h >= 3
+
+
+def test_nd_order_rejects_malformed_graphs():
+    """orbgpu_unit_nd_order validates its CSR input: offsets from 0 and
+    non-decreasing, neighbours in [0, n), no self loops -> ORB_E_INVALID, nothing read out of
+    range."""
+    ORB_E_INVALID = -1
+    n = 6
+    as_, adj = _csr(n, [(i, i + 1) for i in range(n - 1)])
+    perm = np.zeros(n, np.int32)
+    nn, h = C.c_int32(), C.c_int32()
+
+    def call(a, d):
+        return lib().orbgpu_unit_nd_order(n, ptr(a), ptr(d), 4, ptr(perm), C.byref(nn), C.byref(h))
+
+    assert call(as_, adj) == 0
+    bad = as_.copy()
+    bad[0] = 1
+    assert call(bad, adj) == ORB_E_INVALID                 # offsets not from 0
+    bad = as_.copy()
+    bad[3] = bad[2] - 1
+    assert call(bad, adj) == ORB_E_INVALID                 # decreasing offsets
+    for v in (-1, n, 10**6):
+        d = adj.copy()
+        d[2] = v
+        assert call(as_, d) == ORB_E_INVALID               # neighbour out of range
+    d = adj.copy()
+    d[as_[2]] = 2
+    assert call(as_, d) == ORB_E_INVALID                   # self loop

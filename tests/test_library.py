@@ -2,6 +2,8 @@
 validates arguments before touching the device, and reports ORB_E_NODEVICE
 (never a silent CPU fallback) when no GPU is visible."""
 import ctypes as C
+import re
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -20,6 +22,10 @@ def test_all_header_symbols_exported():
 
 def test_version_and_device_probe():
     assert b"gfx950" in lib().orbgpu_version()
+    # the header's ABI revision (ORBmatcher_SearchLocalPoints_batch's signature changed: 2)
+    hdr = (Path(__file__).resolve().parents[1] / "include" / "orbslam_gpu.h").read_text()
+    rev = int(re.search(r"#define ORBGPU_ABI_VERSION (\d+)", hdr).group(1))
+    assert lib().orbgpu_abi_version() == rev == 2
     assert orb.device_available() in (True, False)
 
 
