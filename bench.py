@@ -63,6 +63,9 @@ def parse():
                          "500 keyframes; 0: an open drive, a pure band)")
     ap.add_argument("--nfeatures", type=int, default=NFEAT,
                     help="ORBextractor nFeatures of the stereo pipeline (1200: the metric's; 2000: KITTI00-02.yaml)")
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="batches in flight (buffer sets): extraction of batch k waits for the tracking chain "
+                         "of batch k - lanes, which last used its buffers")
     ap.add_argument("--pipeline-only", action="store_true",
                     help="only the timed stereo pipeline (+ its CPU baseline): one compact JSON line")
     ap.add_argument("--launch-timeout", type=float, default=3000.0,
@@ -824,7 +827,7 @@ def main():
     local_acc = []
     pose_inl = []
     kernel_ms = []   # k_fast_cells duration per step (HIP events on the extractor streams)
-    lanes = [Lane(), Lane()]
+    lanes = [Lane() for _ in range(args.lanes)]
     exL = lanes[0].exL
     if args.reserve_cus:
         # the tracking lane's one-workgroup-per-frame kernels (k_select, k_pose_opt) need free
@@ -840,7 +843,7 @@ def main():
         streams) runs while batch k-1's tracking chain is queued on the matcher stream right
         behind batch k-2's; batch k-2's counts are collected while k-1's chain runs.  -> the
         collected batch's counts (None before the pipeline is full)."""
-        lane = lanes[state["k"] % 2]
+        lane = lanes[state["k"] % len(lanes)]
         te = time.perf_counter()
         fut = ex_pool.submit(lane.extract)
         res = None

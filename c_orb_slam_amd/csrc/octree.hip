@@ -67,6 +67,39 @@ __device__ __forceinline__ int oct_scan(int n, Flag flag, Put put, int* wsum) {
     return total;
 }
 
+// Block-wide exclusive scan of val(i) over i < n; put(i, prefix) for every i.  Returns the
+// total.  Every thread of the block calls it (two barriers).
+template <class Val, class Put>
+__device__ __forceinline__ int oct_scan_val(int n, Val val, Put put, int* wsum) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int per = (n + OCT_T - 1) / OCT_T;
+    const int a = min(n, t * per), e = min(n, a + per);
+    int local = 0;
+    for (int i = a; i < e; i++) local += val(i);
+    int incl = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int off = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < OCT_T / 64; w++) {
+        const int s = wsum[w];
+        if (w < wid) off += s;
+        total += s;
+    }
+    int ex = off + incl - local;
+    for (int i = a; i < e; i++) {
+        put(i, ex);
+        ex += val(i);
+    }
+    __syncthreads();
+    return total;
+}
+
 __device__ __forceinline__ void oct_child_rect(const OctShared& S, int p, int q, int& a0, int& b0, int& a1, int& b1) {
     const int X0 = S.x0[p], Y0 = S.y0[p], X1 = S.x1[p], Y1 = S.y1[p];
     const int halfX = (int)ceilf((float)(X1 - X0) / 2), halfY = (int)ceilf((float)(Y1 - Y0) / 2);
@@ -287,71 +320,100 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
                 }
                 S.vs2[r] = (uint16_t)id;
             }
+            for (int i = tid; i < 4 * mm; i += OCT_T) S.ia[i] = 0;
             if (tid == 0) S.newm = 0;
-            if (tid < 12) S.ia[tid] = 0;
             __syncthreads();
-            for (int j = mm - 1; j >= 0; j--) {
-                const int p = S.vs2[j];
-                const int kb = S.kbeg[p], kc = S.cnt[p];
-                for (int i = tid; i < kc; i += OCT_T) {
-                    const int k = arena[kb + i];
-                    const int q = oct_quadrant(S, p, src[k]);
-                    tmp[kb + i] = (uint16_t)k;
-                    knode[kb + i] = (uint16_t)q;
-                    atomicAdd(&S.ia[q], 1);
+            // The round's divides (largest first, ORBextractor.cc:700-736) are sequential only in
+            // their bookkeeping (push_front order, node ids, the size >= N stop): the keys of
+            // every node of the round are partitioned into its quadrants at once.  A node the
+            // stop leaves undivided keeps its key SET (its slice is only reordered, and every
+            // later use of a slice is order-free: best key = max response, then min index).
+            // er[j] = first flattened key position of vs2[j]
+            const int tot = oct_scan_val(
+                mm, [&](int j) { return (int)S.cnt[S.vs2[j]]; }, [&](int j, int ex) { S.er[j] = (uint16_t)ex; },
+                S.wsum);
+            auto owner = [&](int t) {   // largest j with er[j] <= t
+                int lo = 0, hi = mm - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if ((int)S.er[mid] <= t) lo = mid;
+                    else hi = mid - 1;
                 }
-                __syncthreads();
-                if (tid == 0) {
-                    int start = kb;
+                return lo;
+            };
+            for (int t = tid; t < tot; t += OCT_T) {
+                const int j = owner(t), p = S.vs2[j], pos = S.kbeg[p] + (t - S.er[j]);
+                const int k = arena[pos];
+                const int q = oct_quadrant(S, p, src[k]);
+                tmp[pos] = (uint16_t)k;
+                knode[pos] = (uint16_t)q;
+                atomicAdd(&S.ia[4 * j + q], 1);
+            }
+            __syncthreads();
+            // quadrant starts inside each node's slice (children n1..n4 take consecutive
+            // sub-slices); ia becomes the scatter cursors
+            for (int j = tid; j < mm; j += OCT_T) {
+                int start = S.kbeg[S.vs2[j]];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    S.vpos[4 * j + q] = (uint16_t)start;
+                    start += S.ia[4 * j + q];
+                    S.ia[4 * j + q] = 0;
+                }
+            }
+            __syncthreads();
+            for (int t = tid; t < tot; t += OCT_T) {
+                const int j = owner(t), p = S.vs2[j], pos = S.kbeg[p] + (t - S.er[j]);
+                const int q = knode[pos];
+                arena[S.vpos[4 * j + q] + atomicAdd(&S.ia[4 * j + q], 1)] = tmp[pos];
+            }
+            __syncthreads();
+            // the reference's sequential loop over the round's nodes: children pushed to the
+            // front (n1..n4), the parent erased, stop as soon as the list reaches N
+            if (tid == 0) {
+                for (int j = mm - 1; j >= 0; j--) {
+                    const int p = S.vs2[j];
                     for (int q = 0; q < 4; q++) {
-                        const int c = S.ia[q];
-                        S.ia[4 + q] = start;
-                        S.ia[8 + q] = 0;
+                        const int c = S.ia[4 * j + q];
                         if (c > 0) {
                             const int id = S.nfree++;
                             if (S.nfree > 2 * kOctNMax || id == cur) S.flag = 1;
-                            if (!S.flag) {
-                                int a0, b0, a1, b1;
-                                oct_child_rect(S, p, q, a0, b0, a1, b1);
-                                S.x0[id] = (int16_t)a0;
-                                S.y0[id] = (int16_t)b0;
-                                S.x1[id] = (int16_t)a1;
-                                S.y1[id] = (int16_t)b1;
-                                S.cnt[id] = (uint16_t)c;
-                                S.seq[id] = (uint16_t)(S.seqctr++);
-                                S.kbeg[id] = (uint16_t)start;
-                                // lNodes.push_front
-                                S.prv[id] = -1;
-                                S.nxt[id] = (int16_t)S.head;
-                                if (S.head >= 0) S.prv[S.head] = (int16_t)id;
-                                S.head = id;
-                                S.size++;
-                                if (c > 1) S.vs[S.newm++] = (uint16_t)id;
-                            }
+                            if (S.flag) break;
+                            int a0, b0, a1, b1;
+                            oct_child_rect(S, p, q, a0, b0, a1, b1);
+                            S.x0[id] = (int16_t)a0;
+                            S.y0[id] = (int16_t)b0;
+                            S.x1[id] = (int16_t)a1;
+                            S.y1[id] = (int16_t)b1;
+                            S.cnt[id] = (uint16_t)c;
+                            S.seq[id] = (uint16_t)(S.seqctr++);
+                            S.kbeg[id] = S.vpos[4 * j + q];
+                            // lNodes.push_front
+                            S.prv[id] = -1;
+                            S.nxt[id] = (int16_t)S.head;
+                            if (S.head >= 0) S.prv[S.head] = (int16_t)id;
+                            S.head = id;
+                            S.size++;
+                            if (c > 1) S.vs[S.newm++] = (uint16_t)id;
                         }
-                        start += c;
                     }
+                    if (S.flag) break;
                     // lNodes.erase(parent)
                     const int pp = S.prv[p], pn = S.nxt[p];
-                    if (pp >= 0) S.nxt[pp] = (int16_t)pn; else S.head = pn;
+                    if (pp >= 0) S.nxt[pp] = (int16_t)pn;
+                    else S.head = pn;
                     if (pn >= 0) S.prv[pn] = (int16_t)pp;
                     S.size--;
-                    S.ia[0] = S.ia[1] = S.ia[2] = S.ia[3] = 0;
+                    if (S.size >= N) break;
                 }
-                __syncthreads();
-                if (S.flag) {
-                    if (tid == 0) {
-                        jobcnt[job] = 0;
-                        atomicOr(err, 8);
-                    }
-                    return;
+            }
+            __syncthreads();
+            if (S.flag) {
+                if (tid == 0) {
+                    jobcnt[job] = 0;
+                    atomicOr(err, 8);
                 }
-                for (int i = tid; i < kc; i += OCT_T) {
-                    const int q = knode[kb + i];
-                    arena[S.ia[4 + q] + atomicAdd(&S.ia[8 + q], 1)] = tmp[kb + i];
-                }
-                __syncthreads();
-                if (S.size >= N) break;
+                return;
             }
             if (S.size >= N || S.size == prevSize) break;
             if (tid == 0) S.m = S.newm;
