@@ -1,16 +1,16 @@
-// pnp.hip -- gfx950 EPnP RANSAC: the device side of PnPsolver::iterate
-// (reference src/PnPsolver.cc:165-339).
+// pnp.hip -- gfx950 EPnP RANSAC: PnPsolver::iterate (reference src/PnPsolver.cc:165-339) on the
+// device, host only at the call's two ends.
 //
-// The reference loop draws a minimal set with the process rand(), solves
-// EPnP, scores every correspondence, and returns as soon as Refine() on the
-// best-so-far inliers succeeds.  The draws do not depend on the results, so a
-// call's hypotheses are generated up front from a snapshot of the caller's
-// glibc-rand state and scored in ONE launch for every solver of the batch
-// (k_pnp_hypotheses: a thread per hypothesis, EPnP in FP64 + CheckInliers over
-// all N correspondences, inlier bitmask out).  The host then replays the
-// sequential accept/Refine logic; each Refine it reaches is one more launch
-// (k_pnp_refine), and the RNG is re-advanced by exactly the draws the
-// reference would have consumed.
+// The reference loop draws a minimal set with the process rand(), solves EPnP, scores every
+// correspondence and returns as soon as Refine() on the best-so-far inliers succeeds.  The draws
+// do not depend on the results, so a call's hypotheses are generated up front from the caller's
+// stream (k_pnp_draws: the glibc recurrence a wave at a time, ransac_dev.hpp), solved
+// (k_pnp_hypotheses: a thread per hypothesis, EPnP in FP64) and scored (k_pnp_check: CheckInliers
+// lane-parallel) for every solver of the batch at once.  k_pnp_replay then walks each solver's
+// hypotheses in the reference's order -- best on `>`, Refine() of the best set (cached while the
+// set stands), early return, the `||` loop's exhaustion branch -- and writes one record per solver
+// with the stream advanced by exactly the draws consumed.  One H2D (the problem table), one D2H
+// (the records).
 #include "pnp.hpp"
 
 #include <algorithm>
@@ -20,6 +20,7 @@
 #include <cstring>
 
 #include "epnp.hpp"
+#include "ransac_dev.hpp"
 
 namespace orbgpu {
 
@@ -78,7 +79,7 @@ __device__ __forceinline__ void store_rt(double* out, const double R[3][3], cons
 // Hypothesis solve (PnPsolver.cc:196-210): a thread per hypothesis runs EPnP on its minimal set
 // in FP64 and stores (R, t); counts[h] = -1 flags an invalid draw (never expected).
 __global__ void __launch_bounds__(64) k_pnp_hypotheses(const PnPProbDev* __restrict__ probs) {
-    const PnPProbDev P = probs[blockIdx.y];
+    const PnPProbDev& P = probs[blockIdx.y];
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= P.nhyp) return;
     for (int k = 0; k < P.minSet; k++) {
@@ -159,17 +160,141 @@ __global__ void __launch_bounds__(kPnPCheckThreads) k_pnp_check(const PnPProbDev
     }
 }
 
-// Refine (260-305): EPnP on the best-so-far inliers, then CheckInliers.
-__global__ void __launch_bounds__(64) k_pnp_refine(const PnPProbDev* __restrict__ probs, int nprob) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= nprob) return;
-    const PnPProbDev P = probs[p];
-    IdxPts pts{P.p3d, P.p2d, P.ref_idx};
-    epnp::Solver<IdxPts> S(pts, P.ref_n, P.fu, P.fv, P.uc, P.vc);
-    double R[3][3], t[3];
-    S.compute_pose(R, t);
-    P.ref_out[0] = check_inliers(P, R, t, P.ref_mask);
-    store_rt(P.ref_rt, R, t);
+// The call's minimal sets from the caller's stream, a wave per solver (PnPsolver.cc:189-201).
+__global__ void __launch_bounds__(64) k_pnp_draws(const PnPProbDev* __restrict__ probs) {
+    __shared__ uint32_t win[32];
+    const PnPProbDev& P = probs[blockIdx.x];
+    if (P.nhyp <= 0) return;
+    draw_sets(P.rng, P.nhyp, P.minSet, P.N, P.raw, P.hyp_idx, win);
+}
+
+// CheckInliers of pose (R, t) over all N correspondences by one wave: mask words + count.
+__device__ __forceinline__ int check_inliers_wave(const PnPProbDev& P, const double* R, const double* t, uint32_t* mask) {
+    const int lane = threadIdx.x & 63, N = P.N, words = (N + 31) >> 5;
+    int n = 0;
+    for (int c = 0; c * 64 < N; c++) {
+        const int i = c * 64 + lane;
+        bool in = false;
+        if (i < N) {
+            const float X = P.p3d[3 * i], Y = P.p3d[3 * i + 1], Z = P.p3d[3 * i + 2];
+            const float Xc = (float)(R[0] * X + R[1] * Y + R[2] * Z + t[0]);
+            const float Yc = (float)(R[3] * X + R[4] * Y + R[5] * Z + t[1]);
+            const float invZc = (float)(1 / (R[6] * X + R[7] * Y + R[8] * Z + t[2]));
+            const double ue = P.uc + P.fu * Xc * invZc;
+            const double ve = P.vc + P.fv * Yc * invZc;
+            const float distX = (float)(P.p2d[2 * i] - ue);
+            const float distY = (float)(P.p2d[2 * i + 1] - ve);
+            const float error2 = distX * distX + distY * distY;
+            in = error2 < P.maxErr[i];
+        }
+        const unsigned long long b = __ballot(in);
+        n += __popcll(b);
+        if (lane == 0) {
+            mask[2 * c] = (uint32_t)b;
+            if (2 * c + 1 < words) mask[2 * c + 1] = (uint32_t)(b >> 32);
+        }
+    }
+    return n;
+}
+
+__device__ __forceinline__ void rt_to_tcw_d(const double* rt, float* T) {
+    // cv::Mat(3,3,CV_64F,mRi).convertTo(CV_32F) into eye(4) (PnPsolver.cc:217-224)
+    for (int i = 0; i < 16; i++) T[i] = 0.f;
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) T[4 * i + j] = (float)rt[3 * i + j];
+        T[4 * i + 3] = (float)rt[9 + i];
+    }
+    T[15] = 1.f;
+}
+
+// PnPsolver::iterate's loop (165-258) over the scored hypotheses, a wave per solver.  The
+// control flow is wave-uniform (every lane reads the same counts and state); lane 0 runs the
+// serial EPnP of Refine() (260-305) on the best set, the wave its CheckInliers.
+__global__ void __launch_bounds__(64) k_pnp_replay(const PnPProbDev* __restrict__ probs) {
+    const PnPProbDev& P = probs[blockIdx.x];
+    const int lane = threadIdx.x & 63, N = P.N, words = (N + 31) >> 5;
+    PnPStateDev* st = P.state;
+    int nIt = P.nIt0;
+    int nBest = st->nBest, refValid = st->refValid, refNin = st->refNin;
+    int consumed = P.nhyp, success = 0;
+    for (int h = 0; h < P.nhyp; h++) {
+        nIt++;
+        const int c = P.counts[h];
+        if (c < P.minInliers) continue;
+        if (c > nBest) {   // mvbBestInliers = mvbInliersi; mnBestInliers; mBestTcw
+            const uint32_t* m = P.masks + (size_t)h * words;
+            for (int w = lane; w < words; w += 64) P.bestMask[w] = m[w];
+            if (lane == 0) rt_to_tcw_d(P.rt + (size_t)h * 12, st->bestTcw);
+            nBest = c;
+            refValid = 0;
+        }
+        if (!refValid) {   // Refine(): EPnP on the best inliers in index order, then CheckInliers
+            __syncthreads();
+            int n = 0;
+            for (int base = 0; base < N; base += 64) {
+                const int i = base + lane;
+                const bool in = i < N && ((P.bestMask[i >> 5] >> (i & 31)) & 1);
+                const unsigned long long b = __ballot(in);
+                if (in) P.refIdx[n + __popcll(b & ((1ull << lane) - 1))] = i;
+                n += __popcll(b);
+            }
+            __syncthreads();
+            if (lane == 0) {
+                IdxPts pts{P.p3d, P.p2d, P.refIdx};
+                epnp::Solver<IdxPts> S(pts, n, P.fu, P.fv, P.uc, P.vc);
+                double R[3][3], t[3];
+                S.compute_pose(R, t);
+                store_rt(st->refRt, R, t);
+            }
+            __syncthreads();
+            double R[9], t[3];
+            for (int j = 0; j < 9; j++) R[j] = st->refRt[j];
+            for (int j = 0; j < 3; j++) t[j] = st->refRt[9 + j];
+            refNin = check_inliers_wave(P, R, t, P.refMask);
+            refValid = 1;
+        }
+        if (refNin > P.minInliers) {   // Refine() succeeded: return the refined pose (228-235)
+            success = 1;
+            consumed = h + 1;
+            break;
+        }
+    }
+    __syncthreads();
+    PnPOutDev* o = P.out;
+    const uint32_t* src = nullptr;
+    if (lane == 0) {
+        o->has_pose = 0;
+        o->bNoMore = 0;
+        o->nInliers = 0;
+        o->consumed = consumed;
+        o->nIterations = nIt;
+        for (int i = 0; i < 16; i++) o->Tcw[i] = 0.f;
+    }
+    if (success) {
+        src = P.refMask;
+        if (lane == 0) {
+            o->has_pose = 1;
+            o->nInliers = refNin;
+            rt_to_tcw_d(st->refRt, o->Tcw);
+        }
+    } else if (nIt >= P.maxIts) {   // 241-257: the loop ran out
+        if (lane == 0) o->bNoMore = 1;
+        if (nBest >= P.minInliers) {
+            src = P.bestMask;
+            if (lane == 0) {
+                o->has_pose = 1;
+                o->nInliers = nBest;
+                for (int i = 0; i < 16; i++) o->Tcw[i] = st->bestTcw[i];
+            }
+        }
+    }
+    for (int w = lane; w < words; w += 64) P.outMask[w] = src ? src[w] : 0u;
+    rng_after(P.rng, P.raw, consumed * P.minSet, &o->rng);
+    if (lane == 0) {
+        st->nBest = nBest;
+        st->refValid = refValid;
+        st->refNin = refNin;
+    }
 }
 
 // ------------------------------------------------------------------- host
@@ -216,7 +341,6 @@ PnPSolver::PnPSolver(int N, const float* p3d, const float* p2d, const float* sig
     sigma2_.assign(sigma2, sigma2 + N);
     kpIdx_.assign(kpIdx, kpIdx + N);
     maxErr_.assign(N, 0.f);
-    bestInliers_.assign(N, 0);
     set_ransac(0.99, 8, 300, 4, 0.4f, 5.991f);  // PnPsolver.h:67 defaults (ctor calls SetRansacParameters())
 }
 
@@ -242,32 +366,34 @@ void PnPSolver::set_ransac(double probability, int minInliers, int maxIterations
     maxIts_ = std::max(1, std::min(nIterations, maxIts_));
     for (int i = 0; i < N_; i++) maxErr_[i] = sigma2_[i] * th2;
     dev_dirty_ = true;
+    ref_stale_ = true;
 }
+
+static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
+static int mask_words(int N) { return (N + 31) >> 5; }
+
+// device block: p3d | p2d | maxErr | PnPStateDev | best mask | Refine mask | Refine index list
+size_t PnPSolver::state_off() const { return al256((size_t)N_ * 24 + 64); }
 
 int PnPSolver::upload(hipStream_t s) {
     if (!dev_dirty_) return 0;
-    const size_t bytes = (size_t)N_ * (3 + 2 + 1) * 4 + 64;
-    if (bytes > d_pts_cap_) {
+    const size_t so = state_off(), W = (size_t)mask_words(N_) * 4;
+    const size_t bytes = so + al256(sizeof(PnPStateDev)) + 2 * al256(W) + al256((size_t)N_ * 4 + 4);
+    if (bytes > d_pts_cap_) {   // first upload: a fresh state (no best set, no Refine cached)
         if (d_pts_) (void)hipFree(d_pts_);
         ORB_HIP_CHECK(hipMalloc(&d_pts_, bytes));
         d_pts_cap_ = bytes;
+        ORB_HIP_CHECK(hipMemsetAsync((char*)d_pts_ + so, 0, bytes - so, s));
+    } else if (ref_stale_) {   // PnPStateDev::refValid = 0 (mvMaxError changed)
+        ORB_HIP_CHECK(hipMemsetAsync((char*)d_pts_ + so + offsetof(PnPStateDev, refValid), 0, 4, s));
     }
+    ref_stale_ = false;
     float* d = (float*)d_pts_;
     ORB_HIP_CHECK(hipMemcpyAsync(d, p3d_.data(), (size_t)N_ * 12, hipMemcpyHostToDevice, s));
     ORB_HIP_CHECK(hipMemcpyAsync(d + 3 * N_, p2d_.data(), (size_t)N_ * 8, hipMemcpyHostToDevice, s));
     ORB_HIP_CHECK(hipMemcpyAsync(d + 5 * N_, maxErr_.data(), (size_t)N_ * 4, hipMemcpyHostToDevice, s));
     dev_dirty_ = false;
     return 0;
-}
-
-static void rt_to_tcw(const double* rt, float* T) {
-    // cv::Mat(3,3,CV_64F,mRi).convertTo(CV_32F) into eye(4) (PnPsolver.cc:217-224)
-    for (int i = 0; i < 16; i++) T[i] = 0.f;
-    for (int i = 0; i < 3; i++) {
-        for (int j = 0; j < 3; j++) T[4 * i + j] = (float)rt[3 * i + j];
-        T[4 * i + 3] = (float)rt[9 + i];
-    }
-    T[15] = 1.f;
 }
 
 PnPBatch::~PnPBatch() {
@@ -318,58 +444,56 @@ int PnPBatch::ensure(size_t dev_bytes, size_t host_bytes, size_t probs) {
     return 0;
 }
 
-// PnPsolver::iterate for `n` solvers; solver k draws from rngs[k] (may alias).
 // Byte layout of one iterate() call's device work area and pinned staging.  The accounting
 // (how much to allocate) and the carve (where each buffer goes) both come from here, so they
-// cannot drift apart: an earlier version summed unaligned sizes for the Refine scratch while
-// the carve aligned each sub-buffer, and the last solvers' Refine buffers ran past the work
-// area (the PnP fault of 9f527cb; tests/test_pnp_layout.py pins the invariant).
-//   device: [draws of every solver | (masks, counts, (R, t)) of every solver | Refine slots]
-//   pinned host: a byte-for-byte mirror of the first two regions, so the draws go up in one
-//   copy and the results come back in one copy for any number of solvers.
+// cannot drift apart (the PnP fault of 9f527cb: an earlier accounting summed unaligned sizes
+// while the carve aligned every sub-buffer; tests/test_pnp_layout.py pins the invariant).
+//   device: [per solver: draws | stream words | counts | masks | (R, t)] [per solver: record]
+//   pinned host: a byte-for-byte mirror of the record region (ONE copy back per call)
 struct PnPLayout {
-    static size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
-    static int words(int N) { return (N + 31) >> 5; }
+    static size_t al(size_t v) { return al256(v); }
+    static int words(int N) { return mask_words(N); }
     static size_t hyp_bytes(int K, int minSet) { return al((size_t)K * minSet * 4); }
-    static size_t mask_bytes(int K, int N) { return al((size_t)K * words(N) * 4); }
+    static size_t raw_bytes(int K, int minSet) { return al((size_t)K * minSet * 4); }
     static size_t cnt_bytes(int K) { return al((size_t)K * 4); }
+    static size_t mask_bytes(int K, int N) { return al((size_t)K * words(N) * 4); }
     static size_t rt_bytes(int K) { return al((size_t)K * 12 * 8); }
-    static size_t res_bytes(int K, int N) { return mask_bytes(K, N) + cnt_bytes(K) + rt_bytes(K); }
-    // Refine slot of a solver: inlier idx list | mask | (R, t) | inlier count
-    static size_t ref_mask_off(int N) { return al((size_t)N * 4); }
-    static size_t ref_rt_off(int N) { return ref_mask_off(N) + al((size_t)words(N) * 4); }
-    static size_t ref_out_off(int N) { return ref_rt_off(N) + 96; }
-    static size_t ref_slot(int N) { return al(ref_out_off(N) + 4); }
+    static size_t scratch_bytes(int K, int N, int minSet) {
+        return hyp_bytes(K, minSet) + raw_bytes(K, minSet) + cnt_bytes(K) + mask_bytes(K, N) + rt_bytes(K);
+    }
+    static size_t out_bytes(int N) { return al(sizeof(PnPOutDev) + (size_t)words(N) * 4); }
 };
 
 int pnp_layout_check(int n, const int* N, const int* K, const int* minSet, long long* out4) {
+    using LY = PnPLayout;
     // accounting as iterate() does it
-    size_t dev = 0;
-    for (int k = 0; k < n; k++) dev += PnPLayout::hyp_bytes(K[k], minSet[k]) + PnPLayout::res_bytes(K[k], N[k]);
-    const size_t mirror = dev;
-    for (int k = 0; k < n; k++) dev += PnPLayout::ref_slot(N[k]);
-    const size_t dev_cap = dev + 256, host_cap = mirror + 256;
-    // every byte the carve touches: the draw region, the result region (kernels write masks,
-    // counts and K * 96 B of poses), every solver's Refine slot at once; the host mirror
+    size_t dev = 0, host = 0;
+    for (int k = 0; k < n; k++) dev += LY::scratch_bytes(K[k], N[k], minSet[k]);
+    const size_t out_base = dev;
+    for (int k = 0; k < n; k++) host += LY::out_bytes(N[k]);
+    dev += host;
+    const size_t dev_cap = dev + 256, host_cap = host + 256;
+    // every byte the kernels touch, carved as iterate() carves it
     size_t dend = 0, o = 0;
     for (int k = 0; k < n; k++) {
-        dend = std::max(dend, o + (size_t)K[k] * minSet[k] * 4);
-        o += PnPLayout::hyp_bytes(K[k], minSet[k]);
+        const size_t W = (size_t)LY::words(N[k]) * 4;
+        dend = std::max(dend, o + (size_t)K[k] * minSet[k] * 4);   // hyp_idx
+        o += LY::hyp_bytes(K[k], minSet[k]);
+        dend = std::max(dend, o + (size_t)K[k] * minSet[k] * 4);   // raw
+        o += LY::raw_bytes(K[k], minSet[k]);
+        dend = std::max(dend, o + (size_t)K[k] * 4);               // counts
+        o += LY::cnt_bytes(K[k]);
+        dend = std::max(dend, o + (size_t)K[k] * W);               // masks
+        o += LY::mask_bytes(K[k], N[k]);
+        dend = std::max(dend, o + (size_t)K[k] * 96);              // (R, t)
+        o += LY::rt_bytes(K[k]);
     }
+    size_t hend = 0, ho = 0;
     for (int k = 0; k < n; k++) {
-        dend = std::max(dend, o + (size_t)K[k] * PnPLayout::words(N[k]) * 4);
-        o += PnPLayout::mask_bytes(K[k], N[k]);
-        dend = std::max(dend, o + (size_t)K[k] * 4);
-        o += PnPLayout::cnt_bytes(K[k]);
-        dend = std::max(dend, o + (size_t)K[k] * 96);
-        o += PnPLayout::rt_bytes(K[k]);
-    }
-    const size_t hend = o;
-    size_t ro = o;
-    for (int k = 0; k < n; k++) {
-        dend = std::max(dend, ro + PnPLayout::ref_out_off(N[k]) + 4);
-        dend = std::max(dend, ro + (size_t)N[k] * 4);
-        ro += PnPLayout::ref_slot(N[k]);
+        const size_t end = ho + sizeof(PnPOutDev) + (size_t)LY::words(N[k]) * 4;
+        dend = std::max(dend, out_base + end);
+        hend = std::max(hend, end);
+        ho += LY::out_bytes(N[k]);
     }
     out4[0] = (long long)dev_cap;
     out4[1] = (long long)dend;
@@ -378,18 +502,13 @@ int pnp_layout_check(int n, const int* N, const int* K, const int* minSet, long 
     return dend <= dev_cap && hend <= host_cap ? 0 : 1;
 }
 
+// PnPsolver::iterate for `n` solvers; solver k draws from rngs[k] (distinct streams: the C
+// entry runs solvers that share a stream one after another)
 int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnPResult* res) {
     hipStream_t s = stream_;
-    struct Job {
-        int K = 0;            // hypotheses generated for this call
-        orb_rng snap;         // RNG state before the call
-        size_t hyp_off = 0, mask_off = 0, cnt_off = 0, rt_off = 0;
-        bool active = false;
-        int next = 0;         // next hypothesis to replay
-    };
-    std::vector<Job> jobs(n);
-    size_t dev = 0;
     using LY = PnPLayout;
+    std::vector<int> K(n, 0), act(n, 0);
+    size_t dev = 0, host = 0;
     for (int k = 0; k < n; k++) {
         PnPSolver& P = *S[k];
         PnPResult& r = res[k];
@@ -401,223 +520,96 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
             r.bNoMore = 1;
             continue;
         }
-        Job& J = jobs[k];
-        J.K = std::max(P.maxIts_ - P.nIterations_, nIterations);  // `while (it < max || cur < nIt)`
-        if (J.K <= 0) J.K = 0;
-        J.active = J.K > 0;
-        J.snap = *rngs[k];
-        J.hyp_off = dev; dev += LY::hyp_bytes(J.K, P.minSet_);
+        act[k] = 1;
+        K[k] = std::max(std::max(P.maxIts_ - P.nIterations_, nIterations), 0);   // `while (it < max || cur < nIt)`
+        if ((size_t)P.N_ >= (size_t)kRngMaxRange) return -1;
+        dev += LY::scratch_bytes(K[k], P.N_, P.minSet_);
+        host += LY::out_bytes(P.N_);
         if (int e = P.upload(s)) return e;
     }
-    const size_t res_base = dev;
-    for (int k = 0; k < n; k++) {
-        Job& J = jobs[k];
-        const int N = S[k]->N_;
-        J.mask_off = dev; dev += LY::mask_bytes(J.K, N);
-        J.cnt_off = dev; dev += LY::cnt_bytes(J.K);
-        J.rt_off = dev; dev += LY::rt_bytes(J.K);
-    }
-    // refine scratch (per solver): idx list N + mask + rt + count
-    const size_t ref_base = dev;
-    for (int k = 0; k < n; k++) dev += LY::ref_slot(S[k]->N_);
-    if (int e = ensure(dev + 256, ref_base + 256, (size_t)n)) return e;
+    const size_t out_base = dev;
+    dev += host;
+    if (int e = ensure(dev + 256, host + 256, (size_t)n)) return e;
     char* D = (char*)d_work_;
     char* Hh = (char*)h_work_;
-    // 1. generate all hypotheses (draws as the reference would make them), straight into the
-    //    pinned mirror of the draw region
     std::vector<PnPProbDev> pd(n);
-    int maxK = 0;
+    std::vector<size_t> out_off(n, 0);
+    size_t o = 0, ho = 0;
+    int maxK = 0, nact = 0;
+    long long hyp = 0, pts = 0;
     for (int k = 0; k < n; k++) {
-        Job& J = jobs[k];
+        PnPProbDev& q = pd[nact];
+        if (!act[k]) continue;
         PnPSolver& P = *S[k];
-        std::memset(&pd[k], 0, sizeof(PnPProbDev));
-        if (!J.active) continue;
-        orb_rng g = J.snap;
-        int* hyp = (int*)(Hh + J.hyp_off);
-        // vAvailableIndices = mvAllIndices per iteration (PnPsolver.cc:196-203): the draw writes
-        // minSet slots, undone after each hypothesis instead of re-filling all N
-        std::vector<int> avail(P.N_), pos(P.minSet_), old(P.minSet_);
-        for (int i = 0; i < P.N_; i++) avail[i] = i;
-        for (int h = 0; h < J.K; h++) {
-            int navail = P.N_;
-            for (int i = 0; i < P.minSet_; ++i) {
-                const int randi = random_int(&g, 0, navail - 1);
-                hyp[(size_t)h * P.minSet_ + i] = avail[randi];
-                pos[i] = randi;
-                old[i] = avail[randi];
-                avail[randi] = avail[navail - 1];
-                navail--;
-            }
-            for (int i = P.minSet_ - 1; i >= 0; --i) avail[pos[i]] = old[i];
-        }
-        const float* dp = (const float*)P.d_pts_;
-        PnPProbDev& q = pd[k];
+        std::memset(&q, 0, sizeof(PnPProbDev));
+        const size_t W = (size_t)mask_words(P.N_) * 4;
+        char* blk = (char*)P.d_pts_;
+        const float* dp = (const float*)blk;
         q.p3d = dp;
         q.p2d = dp + 3 * P.N_;
         q.maxErr = dp + 5 * P.N_;
         q.N = P.N_;
         q.fu = P.fu_; q.fv = P.fv_; q.uc = P.uc_; q.vc = P.vc_;
-        q.hyp_idx = (const int*)(D + J.hyp_off);
-        q.nhyp = J.K;
+        q.nhyp = K[k];
         q.minSet = P.minSet_;
-        q.counts = (int*)(D + J.cnt_off);
-        q.masks = (uint32_t*)(D + J.mask_off);
-        q.rt = (double*)(D + J.rt_off);
-        maxK = std::max(maxK, J.K);
+        q.hyp_idx = (int*)(D + o); o += LY::hyp_bytes(K[k], P.minSet_);
+        q.raw = (uint32_t*)(D + o); o += LY::raw_bytes(K[k], P.minSet_);
+        q.counts = (int*)(D + o); o += LY::cnt_bytes(K[k]);
+        q.masks = (uint32_t*)(D + o); o += LY::mask_bytes(K[k], P.N_);
+        q.rt = (double*)(D + o); o += LY::rt_bytes(K[k]);
+        q.minInliers = P.minInliers_;
+        q.maxIts = P.maxIts_;
+        q.nIt0 = P.nIterations_;
+        q.rng = *rngs[k];
+        const size_t so = P.state_off();
+        q.state = (PnPStateDev*)(blk + so);
+        q.bestMask = (uint32_t*)(blk + so + al256(sizeof(PnPStateDev)));
+        q.refMask = (uint32_t*)((char*)q.bestMask + al256(W));
+        q.refIdx = (int*)((char*)q.refMask + al256(W));
+        out_off[k] = ho;
+        q.out = (PnPOutDev*)(D + out_base + ho);
+        q.outMask = (uint32_t*)(D + out_base + ho + sizeof(PnPOutDev));
+        ho += LY::out_bytes(P.N_);
+        maxK = std::max(maxK, K[k]);
+        hyp += K[k];
+        pts += (long long)K[k] * P.N_;
+        nact++;
     }
-    if (getenv("ORBGPU_CHECK_PTRS")) {
-        auto in = [](const void* p, size_t bytes) {
-            void* base = nullptr;
-            size_t size = 0;
-            if (hipMemGetAddressRange((hipDeviceptr_t*)&base, &size, (hipDeviceptr_t)p) != hipSuccess) return false;
-            return (const char*)p >= (const char*)base && (const char*)p + bytes <= (const char*)base + size;
-        };
-        for (int k = 0; k < n; k++) {
-            const PnPProbDev& q = pd[k];
-            if (!jobs[k].active) continue;
-            const int words = (q.N + 31) >> 5;
-            const bool ok = in(q.p3d, q.N * 12) && in(q.p2d, q.N * 8) && in(q.maxErr, q.N * 4) &&
-                            in(q.hyp_idx, (size_t)q.nhyp * q.minSet * 4) && in(q.counts, (size_t)q.nhyp * 4) &&
-                            in(q.masks, (size_t)q.nhyp * words * 4) && in(q.rt, (size_t)q.nhyp * 96) &&
-                            in(d_probs_, sizeof(PnPProbDev) * n);
-            fprintf(stderr, "[pnp] k=%d N=%d nhyp=%d minSet=%d ptrs %s p3d=%p hyp=%p work=%p cap=%zu\n", k, q.N, q.nhyp,
-                    q.minSet, ok ? "ok" : "BAD", (const void*)q.p3d, (const void*)q.hyp_idx, d_work_, work_cap_);
-            if (!ok) return -1;
-        }
-    }
-    if (res_base > 0) ORB_HIP_CHECK(hipMemcpyAsync(D, Hh, res_base, hipMemcpyHostToDevice, s));
-    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(PnPProbDev) * n, hipMemcpyHostToDevice, s));
+    if (nact == 0) return 0;
+    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(PnPProbDev) * nact, hipMemcpyHostToDevice, s));
+    const PnPProbDev* dprobs = (const PnPProbDev*)d_probs_;
+    hipLaunchKernelGGL(k_pnp_draws, dim3(nact), dim3(64), 0, s, dprobs);
     if (maxK > 0) {
         if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[0], s));
-        hipLaunchKernelGGL(k_pnp_hypotheses, dim3((maxK + 63) / 64, n), dim3(64), 0, s, (const PnPProbDev*)d_probs_);
+        hipLaunchKernelGGL(k_pnp_hypotheses, dim3((maxK + 63) / 64, nact), dim3(64), 0, s, dprobs);
         if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
-        hipLaunchKernelGGL(k_pnp_check, dim3((maxK + kPnPCheckHyp - 1) / kPnPCheckHyp, n), dim3(kPnPCheckThreads), 0, s,
-                           (const PnPProbDev*)d_probs_);
+        hipLaunchKernelGGL(k_pnp_check, dim3((maxK + kPnPCheckHyp - 1) / kPnPCheckHyp, nact), dim3(kPnPCheckThreads), 0,
+                           s, dprobs);
         if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
-        last_hyp_ = 0;
-        for (int k = 0; k < n; k++) last_hyp_ += jobs[k].active ? jobs[k].K : 0;
-        last_pts_ = 0;
-        for (int k = 0; k < n; k++) last_pts_ += jobs[k].active ? (long long)jobs[k].K * S[k]->N_ : 0;
+        last_hyp_ = hyp;
+        last_pts_ = pts;
         timed_ = timing_;
     }
+    hipLaunchKernelGGL(k_pnp_replay, dim3(nact), dim3(64), 0, s, dprobs);
     ORB_HIP_CHECK(hipGetLastError());
-    // 2. results back (counts, masks, poses of every solver) in one copy
-    if (ref_base > res_base)
-        ORB_HIP_CHECK(hipMemcpyAsync(Hh + res_base, D + res_base, ref_base - res_base, hipMemcpyDeviceToHost, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(Hh, D + out_base, host, hipMemcpyDeviceToHost, s));
     ORB_HIP_CHECK(hipStreamSynchronize(s));
-    // 3. sequential replay; Refine requests batched across solvers
-    std::vector<char> done(n, 0);
-    std::vector<int> ref_n(n, 0);
-    for (int k = 0; k < n; k++) done[k] = !jobs[k].active;
-    for (;;) {
-        std::vector<int> need;  // solvers waiting for a Refine
-        for (int k = 0; k < n; k++) {
-            if (done[k]) continue;
-            Job& J = jobs[k];
-            PnPSolver& P = *S[k];
-            const int words = (P.N_ + 31) >> 5;
-            const int* cnt = (const int*)(Hh + J.cnt_off);
-            const uint32_t* masks = (const uint32_t*)(Hh + J.mask_off);
-            const double* rts = (const double*)(Hh + J.rt_off);
-            bool wait = false;
-            while (J.next < J.K) {
-                const int h = J.next;
-                if (P.refine_pending_ < 0) {  // iteration h not yet counted
-                    P.nIterations_++;
-                    const int c = cnt[h];
-                    if (c >= P.minInliers_) {
-                        if (c > P.nBestInliers_) {
-                            for (int i = 0; i < P.N_; i++)
-                                P.bestInliers_[i] = (masks[(size_t)h * words + (i >> 5)] >> (i & 31)) & 1;
-                            P.nBestInliers_ = c;
-                            rt_to_tcw(rts + (size_t)h * 12, P.bestTcw_);
-                            P.refine_valid_ = false;
-                        }
-                        P.refine_pending_ = h;
-                        if (!P.refine_valid_) {  // Refine(best) not computed for this best set yet
-                            wait = true;
-                            break;
-                        }
-                    } else {
-                        J.next++;
-                        continue;
-                    }
-                }
-                // Refine result for the current best set is available
-                P.refine_pending_ = -1;
-                if (P.refNin_ > P.minInliers_) {
-                    PnPResult& r = res[k];
-                    r.has_pose = 1;
-                    r.nInliers = P.refNin_;
-                    std::fill(r.inliers, r.inliers + P.nMatches_, 0);
-                    for (int i = 0; i < P.N_; i++)
-                        if (P.refMask_[i >> 5] >> (i & 31) & 1) r.inliers[P.kpIdx_[i]] = 1;
-                    rt_to_tcw(P.refRt_, r.Tcw);
-                    // consumed draws: hypotheses 0..h
-                    *rngs[k] = J.snap;
-                    for (int d = 0; d < (h + 1) * P.minSet_; d++) (void)rng_rand(rngs[k]);
-                    done[k] = 1;
-                    break;
-                }
-                J.next++;
-            }
-            if (done[k]) continue;
-            if (wait) {
-                need.push_back(k);
-                continue;
-            }
-            // loop exhausted (PnPsolver.cc:241-257)
-            *rngs[k] = J.snap;
-            for (int d = 0; d < J.K * P.minSet_; d++) (void)rng_rand(rngs[k]);
-            PnPResult& r = res[k];
-            if (P.nIterations_ >= P.maxIts_) {
-                r.bNoMore = 1;
-                if (P.nBestInliers_ >= P.minInliers_) {
-                    r.has_pose = 1;
-                    r.nInliers = P.nBestInliers_;
-                    std::fill(r.inliers, r.inliers + P.nMatches_, 0);
-                    for (int i = 0; i < P.N_; i++)
-                        if (P.bestInliers_[i]) r.inliers[P.kpIdx_[i]] = 1;
-                    std::memcpy(r.Tcw, P.bestTcw_, sizeof(float) * 16);
-                }
-            }
-            done[k] = 1;
-        }
-        if (need.empty()) break;
-        // Refine launch for every waiting solver
-        std::vector<PnPProbDev> rq(need.size());
-        size_t ro = ref_base;
-        std::vector<size_t> roff(need.size());
-        for (size_t q = 0; q < need.size(); q++) {
-            PnPSolver& P = *S[need[q]];
-            std::vector<int> idx;
+    for (int k = 0; k < n; k++) {
+        if (!act[k]) continue;
+        PnPSolver& P = *S[k];
+        PnPResult& r = res[k];
+        const PnPOutDev* od = (const PnPOutDev*)(Hh + out_off[k]);
+        const uint32_t* m = (const uint32_t*)(Hh + out_off[k] + sizeof(PnPOutDev));
+        P.nIterations_ = od->nIterations;
+        *rngs[k] = od->rng;
+        r.has_pose = od->has_pose;
+        r.bNoMore = od->bNoMore;
+        r.nInliers = od->nInliers;
+        if (r.has_pose) {
+            std::memcpy(r.Tcw, od->Tcw, sizeof(float) * 16);
             for (int i = 0; i < P.N_; i++)
-                if (P.bestInliers_[i]) idx.push_back(i);
-            roff[q] = ro;
-            ORB_HIP_CHECK(hipMemcpyAsync(D + ro, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, s));
-            PnPProbDev r = pd[need[q]];
-            r.ref_idx = (const int*)(D + ro);
-            r.ref_n = (int)idx.size();
-            r.ref_mask = (uint32_t*)(D + ro + LY::ref_mask_off(P.N_));
-            r.ref_rt = (double*)(D + ro + LY::ref_rt_off(P.N_));
-            r.ref_out = (int*)(D + ro + LY::ref_out_off(P.N_));
-            rq[q] = r;
-            ro += LY::ref_slot(P.N_);
+                if ((m[i >> 5] >> (i & 31)) & 1) r.inliers[P.kpIdx_[i]] = 1;
         }
-        ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, rq.data(), sizeof(PnPProbDev) * rq.size(), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_pnp_refine, dim3((unsigned)(need.size() + 63) / 64), dim3(64), 0, s,
-                           (const PnPProbDev*)d_probs_, (int)need.size());
-        ORB_HIP_CHECK(hipGetLastError());
-        for (size_t q = 0; q < need.size(); q++) {
-            PnPSolver& P = *S[need[q]];
-            const int words = (P.N_ + 31) >> 5;
-            P.refMask_.resize(words);
-            ORB_HIP_CHECK(hipMemcpyAsync(P.refMask_.data(), rq[q].ref_mask, (size_t)words * 4, hipMemcpyDeviceToHost, s));
-            ORB_HIP_CHECK(hipMemcpyAsync(P.refRt_, rq[q].ref_rt, 96, hipMemcpyDeviceToHost, s));
-            ORB_HIP_CHECK(hipMemcpyAsync(&P.refNin_, rq[q].ref_out, 4, hipMemcpyDeviceToHost, s));
-        }
-        ORB_HIP_CHECK(hipStreamSynchronize(s));
-        for (int k : need) S[k]->refine_valid_ = true;
     }
     return 0;
 }

@@ -11,6 +11,22 @@ namespace orbgpu {
 void rng_seed(orb_rng* g, unsigned seed);
 int rng_rand(orb_rng* g);
 
+// per solver, persistent across iterate() calls, in the solver's device block: the best-so-far
+// hypothesis (mnBestInliers, mBestTcw; its inlier mask follows) and the Refine() of that set
+// (PnPsolver.cc:260-305, cached: it depends only on the best set and mvMaxError)
+struct PnPStateDev {
+    int nBest, refValid, refNin, pad;
+    float bestTcw[16];
+    double refRt[12];
+};
+// per solver per call: iterate()'s outputs (the inlier mask, N bits, follows)
+struct PnPOutDev {
+    int has_pose, bNoMore, nInliers, nIterations, consumed, pad[3];
+    float Tcw[16];
+    orb_rng rng;   // the stream after the draws the reference loop consumed
+    int pad2[3];
+};
+
 struct PnPProbDev {
     const float* p3d;
     const float* p2d;
@@ -18,17 +34,21 @@ struct PnPProbDev {
     int N;
     double fu, fv, uc, vc;
     // hypotheses
-    const int* hyp_idx;
+    int* hyp_idx;
+    uint32_t* raw;   // the stream words behind the draws
     int nhyp, minSet;
     int* counts;
     uint32_t* masks;
     double* rt;
-    // refine
-    const int* ref_idx;
-    int ref_n;
-    uint32_t* ref_mask;
-    double* ref_rt;
-    int* ref_out;
+    // replay (PnPsolver::iterate's loop on the device)
+    int minInliers, maxIts, nIt0, pad;
+    orb_rng rng;     // the caller's stream at the call
+    PnPStateDev* state;
+    uint32_t* bestMask;
+    uint32_t* refMask;
+    int* refIdx;
+    PnPOutDev* out;
+    uint32_t* outMask;
 };
 
 struct PnPResult {
@@ -57,20 +77,15 @@ public:
     double prob_ = 0.99;
     int minInliers_ = 8, maxIts_ = 300, minSet_ = 4;
     float epsilon_ = 0.4f;
-    // RANSAC state persisting across iterate() calls
-    int nIterations_ = 0, nBestInliers_ = 0;
-    std::vector<uint8_t> bestInliers_;
-    float bestTcw_[16] = {};
-    // cached Refine() of the current best set
-    bool refine_valid_ = false;
-    int refine_pending_ = -1;
-    int refNin_ = 0;
-    std::vector<uint32_t> refMask_;
-    double refRt_[12] = {};
-    // device copy of the correspondences
+    // RANSAC state persisting across iterate() calls: the iteration counter here (it sizes a
+    // call's hypotheses), the best set and its Refine() in the device block (PnPStateDev)
+    int nIterations_ = 0;
+    // device block: correspondences | PnPStateDev | best mask | Refine mask | Refine index list
     void* d_pts_ = nullptr;
     size_t d_pts_cap_ = 0;
     bool dev_dirty_ = true;
+    bool ref_stale_ = false;   // set_ransac changed mvMaxError: the cached Refine() is void
+    size_t state_off() const;
 };
 
 class PnPBatch {

@@ -9,6 +9,7 @@
 // replays the `>=` best update and the `> minInliers` early return and
 // advances the RNG by exactly 3 draws per consumed iteration.
 #include "sim3.hpp"
+#include "ransac_dev.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -215,7 +216,7 @@ __device__ __forceinline__ void project(const float* X, const float* T, const fl
 }
 
 __global__ void __launch_bounds__(64) k_sim3_hypotheses(const Sim3ProbDev* __restrict__ probs) {
-    const Sim3ProbDev P = probs[blockIdx.y];
+    const Sim3ProbDev& P = probs[blockIdx.y];
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= P.nhyp) return;
     float P1[3][3], P2[3][3];
@@ -307,11 +308,62 @@ __global__ void __launch_bounds__(kSim3CheckThreads) k_sim3_check(const Sim3Prob
     }
 }
 
-// ----------------------------------------------------------------------- host
-static int random_int3(orb_rng* g, int min, int max) {
-    const int d = max - min + 1;
-    return int(((double)rng_rand(g) / ((double)2147483647 + 1.0)) * d) + min;
+// The call's minimal sets from the caller's stream, a wave per solver (Sim3Solver.cc:166-178).
+__global__ void __launch_bounds__(64) k_sim3_draws(const Sim3ProbDev* __restrict__ probs) {
+    __shared__ uint32_t win[32];
+    const Sim3ProbDev& P = probs[blockIdx.x];
+    if (P.nhyp <= 0) return;
+    draw_sets(P.rng, P.nhyp, 3, P.N, P.raw, P.hyp_idx, win);
 }
+
+// Sim3Solver::iterate's loop (158-206) over the scored hypotheses, a wave per solver: best on
+// `>=`, return the CURRENT hypothesis as soon as it has more than mRansacMinInliers inliers.
+// (mvbBestInliers is written by the reference and never read: not kept.)
+__global__ void __launch_bounds__(64) k_sim3_replay(const Sim3ProbDev* __restrict__ probs) {
+    const Sim3ProbDev& P = probs[blockIdx.x];
+    const int lane = threadIdx.x & 63, words = (P.N + 31) >> 5;
+    Sim3StateDev* st = P.state;
+    int nIt = P.nIt0, nBest = st->nBest, best = -1, consumed = P.nhyp, success = 0;
+    for (int h = 0; h < P.nhyp; h++) {
+        nIt++;
+        const int c = P.counts[h];
+        if (c >= nBest) {
+            best = h;
+            nBest = c;
+            if (c > P.minInliers) {
+                success = 1;
+                consumed = h + 1;
+                break;
+            }
+        }
+    }
+    Sim3OutDev* o = P.out;
+    if (lane == 0) {
+        if (best >= 0) {
+            const float* e = P.est + (size_t)best * 32;
+            for (int i = 0; i < 9; i++) st->bestR[i] = e[i];
+            for (int i = 0; i < 3; i++) st->bestT[i] = e[9 + i];
+            st->bestS = e[12];
+            for (int i = 0; i < 16; i++) st->bestT12[i] = e[16 + i];
+        }
+        st->nBest = nBest;
+        o->has_pose = success;
+        o->nInliers = success ? nBest : 0;
+        o->bNoMore = !success && nIt >= P.maxIts;
+        o->nIterations = nIt;
+        o->consumed = consumed;
+        o->nBest = nBest;
+        for (int i = 0; i < 16; i++) o->T12[i] = success ? st->bestT12[i] : 0.f;
+        for (int i = 0; i < 9; i++) o->bestR[i] = st->bestR[i];
+        for (int i = 0; i < 3; i++) o->bestT[i] = st->bestT[i];
+        o->bestS = st->bestS;
+    }
+    const uint32_t* m = P.masks + (size_t)(success ? best : 0) * words;
+    for (int w = lane; w < words; w += 64) P.outMask[w] = success ? m[w] : 0u;
+    rng_after(P.rng, P.raw, consumed * 3, &o->rng);
+}
+
+// ----------------------------------------------------------------------- host
 
 Sim3Solver::Sim3Solver(int N, const float* X1c, const float* X2c, const float* s1, const float* s2, const int* idx1,
                        int N1, const float* K1, const float* K2, bool bFixScale)
@@ -339,7 +391,6 @@ Sim3Solver::Sim3Solver(int N, const float* X1c, const float* X2c, const float* s
             out[1] = K[1] * y + K[3];
         }
     }
-    bestInliers_.assign(N, 0);
     set_ransac(0.99, 6, 300);  // Sim3Solver.h:45 defaults, called by the ctor
 }
 
@@ -360,13 +411,19 @@ void Sim3Solver::set_ransac(double probability, int minInliers, int maxIteration
     nIterations_ = 0;
 }
 
+static size_t al256s(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// device block: X1 | X2 | p1 | p2 | maxErr1 | maxErr2 | Sim3StateDev
+size_t Sim3Solver::state_off() const { return al256s((size_t)N_ * 12 * 4 + 64); }
+
 int Sim3Solver::upload(hipStream_t s) {
     if (!dirty_) return 0;
-    const size_t bytes = (size_t)N_ * 12 * 4 + 64;
-    if (bytes > d_cap_) {
+    const size_t so = state_off(), bytes = so + al256s(sizeof(Sim3StateDev));
+    if (bytes > d_cap_) {   // first upload: a fresh state (no best estimate yet)
         if (d_pts_) (void)hipFree(d_pts_);
         ORB_HIP_CHECK(hipMalloc(&d_pts_, bytes));
         d_cap_ = bytes;
+        ORB_HIP_CHECK(hipMemsetAsync((char*)d_pts_ + so, 0, bytes - so, s));
     }
     float* d = (float*)d_pts_;
     ORB_HIP_CHECK(hipMemcpyAsync(d, X1_.data(), (size_t)N_ * 12, hipMemcpyHostToDevice, s));
@@ -406,16 +463,19 @@ int Sim3Batch::last_timings(float* ms2, long long* hyp_pts2) {
     return 0;
 }
 
+// Sim3Solver::iterate for `n` solvers (distinct streams).  Device work area: [per solver: draws |
+// stream words | counts | masks | estimates] [per solver: record]; the pinned host buffer
+// mirrors the record region (ONE copy back per call).
 int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, Sim3Result* res) {
     hipStream_t s = stream_;
-    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    std::vector<int> K(n, 0);
-    std::vector<size_t> hyp_off(n), cnt_off(n), mask_off(n), est_off(n);
-    std::vector<orb_rng> snap(n);
-    // work area: [every solver's hypothesis draws | every solver's counts, masks, estimates];
-    // the pinned host buffer mirrors it byte for byte, so the draws go up in ONE copy and the
-    // results come back in ONE copy whatever the number of solvers
-    size_t dev = 0;
+    auto al = al256s;
+    auto words_of = [](int N) { return (N + 31) >> 5; };
+    auto out_bytes = [&](int N) { return al(sizeof(Sim3OutDev) + (size_t)words_of(N) * 4); };
+    auto scratch = [&](int K, int N) {
+        return 2 * al((size_t)K * 12) + al((size_t)K * 4) + al((size_t)K * words_of(N) * 4) + al((size_t)K * 128);
+    };
+    std::vector<int> K(n, 0), act(n, 0);
+    size_t dev = 0, host = 0;
     for (int k = 0; k < n; k++) {
         Sim3Solver& P = *S[k];
         Sim3Result& r = res[k];
@@ -427,20 +487,16 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
             r.bNoMore = 1;
             continue;
         }
+        if ((size_t)P.N_ >= (size_t)kRngMaxRange) return -1;
+        act[k] = 1;
         // `while (mnIterations < max && nCurrent < nIterations)`
         K[k] = std::max(0, std::min(P.maxIts_ - P.nIterations_, nIterations));
-        snap[k] = *rngs[k];
-        hyp_off[k] = dev; dev += al((size_t)K[k] * 12);
+        dev += scratch(K[k], P.N_);
+        host += out_bytes(P.N_);
         if (int e = P.upload(s)) return e;
     }
-    const size_t res_base = dev;
-    for (int k = 0; k < n; k++) {
-        const int words = (S[k]->N_ + 31) >> 5;
-        cnt_off[k] = dev; dev += al((size_t)K[k] * 4);
-        mask_off[k] = dev; dev += al((size_t)K[k] * words * 4);
-        est_off[k] = dev; dev += al((size_t)K[k] * 128);
-    }
-    const size_t host = dev;
+    const size_t out_base = dev;
+    dev += host;
     if (dev + 256 > work_cap_) {
         if (d_work_) (void)hipFree(d_work_);
         ORB_HIP_CHECK(hipMalloc(&d_work_, dev + 256));
@@ -459,106 +515,80 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
     char* D = (char*)d_work_;
     char* Hh = (char*)h_work_;
     std::vector<Sim3ProbDev> pd(n);
-    int maxK = 0;
+    std::vector<size_t> out_off(n, 0);
+    size_t o = 0, ho = 0;
+    int maxK = 0, nact = 0;
+    long long hyp = 0, pts = 0;
     for (int k = 0; k < n; k++) {
-        std::memset(&pd[k], 0, sizeof(Sim3ProbDev));
-        if (K[k] <= 0) continue;
+        if (!act[k]) continue;
         Sim3Solver& P = *S[k];
-        orb_rng g = snap[k];
-        int* hyp = (int*)(Hh + hyp_off[k]);
-        // vAvailableIndices = mvAllIndices per iteration: the draw writes 3 slots, undone after
-        // each hypothesis instead of re-filling all N (same draws, O(1) per hypothesis)
-        std::vector<int> avail(P.N_);
-        for (int i = 0; i < P.N_; i++) avail[i] = i;
-        for (int h = 0; h < K[k]; h++) {
-            int navail = P.N_, pos[3], old[3];
-            for (int i = 0; i < 3; ++i) {
-                const int randi = random_int3(&g, 0, navail - 1);
-                hyp[3 * h + i] = avail[randi];
-                pos[i] = randi;
-                old[i] = avail[randi];
-                avail[randi] = avail[navail - 1];
-                navail--;
-            }
-            for (int i = 2; i >= 0; --i) avail[pos[i]] = old[i];
-        }
+        Sim3ProbDev& q = pd[nact++];
+        std::memset(&q, 0, sizeof(Sim3ProbDev));
         const float* d = (const float*)P.d_pts_;
-        Sim3ProbDev& q = pd[k];
         q.X1 = d; q.X2 = d + 3 * P.N_; q.p1 = d + 6 * P.N_; q.p2 = d + 8 * P.N_;
         q.maxErr1 = d + 10 * P.N_; q.maxErr2 = d + 11 * P.N_;
         q.N = P.N_;
         q.bFixScale = P.bFixScale_ ? 1 : 0;
         std::memcpy(q.K1, P.K1_, 16);
         std::memcpy(q.K2, P.K2_, 16);
-        q.hyp_idx = (const int*)(D + hyp_off[k]);
         q.nhyp = K[k];
-        q.counts = (int*)(D + cnt_off[k]);
-        q.masks = (uint32_t*)(D + mask_off[k]);
-        q.est = (float*)(D + est_off[k]);
+        q.hyp_idx = (int*)(D + o); o += al((size_t)K[k] * 12);
+        q.raw = (uint32_t*)(D + o); o += al((size_t)K[k] * 12);
+        q.counts = (int*)(D + o); o += al((size_t)K[k] * 4);
+        q.masks = (uint32_t*)(D + o); o += al((size_t)K[k] * words_of(P.N_) * 4);
+        q.est = (float*)(D + o); o += al((size_t)K[k] * 128);
+        q.minInliers = P.minInliers_;
+        q.maxIts = P.maxIts_;
+        q.nIt0 = P.nIterations_;
+        q.rng = *rngs[k];
+        q.state = (Sim3StateDev*)((char*)P.d_pts_ + P.state_off());
+        out_off[k] = ho;
+        q.out = (Sim3OutDev*)(D + out_base + ho);
+        q.outMask = (uint32_t*)(D + out_base + ho + sizeof(Sim3OutDev));
+        ho += out_bytes(P.N_);
         maxK = std::max(maxK, K[k]);
+        hyp += K[k];
+        pts += (long long)K[k] * P.N_;
     }
-    if (res_base > 0)
-        ORB_HIP_CHECK(hipMemcpyAsync(D, Hh, res_base, hipMemcpyHostToDevice, s));
-    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(Sim3ProbDev) * n, hipMemcpyHostToDevice, s));
+    if (nact == 0) return 0;
+    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(Sim3ProbDev) * nact, hipMemcpyHostToDevice, s));
+    const Sim3ProbDev* dprobs = (const Sim3ProbDev*)d_probs_;
+    hipLaunchKernelGGL(k_sim3_draws, dim3(nact), dim3(64), 0, s, dprobs);
     if (maxK > 0) {
         if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[0], s));
-        hipLaunchKernelGGL(k_sim3_hypotheses, dim3((maxK + 63) / 64, n), dim3(64), 0, s, (const Sim3ProbDev*)d_probs_);
+        hipLaunchKernelGGL(k_sim3_hypotheses, dim3((maxK + 63) / 64, nact), dim3(64), 0, s, dprobs);
         if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
-        hipLaunchKernelGGL(k_sim3_check, dim3((maxK + kSim3CheckHyp - 1) / kSim3CheckHyp, n), dim3(kSim3CheckThreads),
-                           0, s, (const Sim3ProbDev*)d_probs_);
+        hipLaunchKernelGGL(k_sim3_check, dim3((maxK + kSim3CheckHyp - 1) / kSim3CheckHyp, nact), dim3(kSim3CheckThreads),
+                           0, s, dprobs);
         if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
-        last_hyp_ = last_pts_ = 0;
-        for (int k = 0; k < n; k++) {
-            last_hyp_ += K[k] > 0 ? K[k] : 0;
-            last_pts_ += K[k] > 0 ? (long long)K[k] * S[k]->N_ : 0;
-        }
+        last_hyp_ = hyp;
+        last_pts_ = pts;
         timed_ = timing_;
     }
+    hipLaunchKernelGGL(k_sim3_replay, dim3(nact), dim3(64), 0, s, dprobs);
     ORB_HIP_CHECK(hipGetLastError());
-    if (dev > res_base)
-        ORB_HIP_CHECK(hipMemcpyAsync(Hh + res_base, D + res_base, dev - res_base, hipMemcpyDeviceToHost, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(Hh, D + out_base, host, hipMemcpyDeviceToHost, s));
     ORB_HIP_CHECK(hipStreamSynchronize(s));
-    // sequential replay (Sim3Solver.cc:158-206)
     for (int k = 0; k < n; k++) {
+        if (!act[k]) continue;
         Sim3Solver& P = *S[k];
         Sim3Result& r = res[k];
-        if (P.N_ < P.minInliers_) continue;
-        const int words = (P.N_ + 31) >> 5;
-        const int* cnt = (const int*)(Hh + cnt_off[k]);
-        const uint32_t* masks = (const uint32_t*)(Hh + mask_off[k]);
-        const float* est = (const float*)(Hh + est_off[k]);
-        int consumed = K[k];
-        int best = -1;   // last hypothesis that became the best: its mask is expanded once, below
-        for (int hh = 0; hh < K[k]; hh++) {
-            P.nIterations_++;
-            const int c = cnt[hh];
-            if (c >= P.nBestInliers_) {
-                best = hh;
-                P.nBestInliers_ = c;
-                const float* e = est + (size_t)hh * 32;
-                std::memcpy(P.bestR_, e, 36);
-                std::memcpy(P.bestT_, e + 9, 12);
-                P.bestS_ = e[12];
-                std::memcpy(P.bestT12_, e + 16, 64);
-                if (c > P.minInliers_) {
-                    for (int i = 0; i < P.N_; i++)
-                        P.bestInliers_[i] = (masks[(size_t)hh * words + (i >> 5)] >> (i & 31)) & 1;
-                    best = -1;
-                    r.has_pose = 1;
-                    r.nInliers = c;
-                    for (int i = 0; i < P.N_; i++)
-                        if (P.bestInliers_[i]) r.inliers[P.idx1_[i]] = 1;
-                    std::memcpy(r.T12, P.bestT12_, 64);
-                    consumed = hh + 1;
-                    break;
-                }
-            }
+        const Sim3OutDev* od = (const Sim3OutDev*)(Hh + out_off[k]);
+        const uint32_t* m = (const uint32_t*)(Hh + out_off[k] + sizeof(Sim3OutDev));
+        P.nIterations_ = od->nIterations;
+        P.nBestInliers_ = od->nBest;
+        std::memcpy(P.bestR_, od->bestR, 36);
+        std::memcpy(P.bestT_, od->bestT, 12);
+        P.bestS_ = od->bestS;
+        *rngs[k] = od->rng;
+        r.has_pose = od->has_pose;
+        r.bNoMore = od->bNoMore;
+        r.nInliers = od->nInliers;
+        if (r.has_pose) {
+            std::memcpy(r.T12, od->T12, 64);
+            for (int i = 0; i < P.N_; i++)
+                if ((m[i >> 5] >> (i & 31)) & 1) r.inliers[P.idx1_[i]] = 1;
         }
-        if (best >= 0)
-            for (int i = 0; i < P.N_; i++) P.bestInliers_[i] = (masks[(size_t)best * words + (i >> 5)] >> (i & 31)) & 1;
-        *rngs[k] = snap[k];
-        for (int d = 0; d < consumed * 3; d++) (void)rng_rand(rngs[k]);
-        if (!r.has_pose && P.nIterations_ >= P.maxIts_) r.bNoMore = 1;
     }
     return 0;
 }

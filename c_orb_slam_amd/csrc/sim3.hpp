@@ -8,6 +8,21 @@
 
 namespace orbgpu {
 
+// per solver, persistent across iterate() calls, in the solver's device block: the best-so-far
+// estimate (mnBestInliers, mBestRotation / mBestTranslation / mBestScale / mBestT12)
+struct Sim3StateDev {
+    int nBest, pad[3];
+    float bestR[9], bestT[3], bestS, bestT12[16], pad2[3];
+};
+// per solver per call: iterate()'s outputs (the inlier mask, N bits, follows)
+struct Sim3OutDev {
+    int has_pose, bNoMore, nInliers, nIterations, consumed, nBest, pad[2];
+    float T12[16];
+    float bestR[9], bestT[3], bestS, pad2[3];
+    orb_rng rng;   // the stream after the draws the reference loop consumed
+    int pad3[3];
+};
+
 struct Sim3ProbDev {
     const float* X1;   // N x 3 camera-frame points of KF1 (mvX3Dc1)
     const float* X2;   // N x 3 (mvX3Dc2)
@@ -17,11 +32,18 @@ struct Sim3ProbDev {
     const float* maxErr2;
     int N, bFixScale;
     float K1[4], K2[4];
-    const int* hyp_idx;  // nhyp x 3
+    int* hyp_idx;  // nhyp x 3
+    uint32_t* raw;     // the stream words behind the draws
     int nhyp;
     int* counts;
     uint32_t* masks;
     float* est;          // nhyp x 32: R9 t3 s T12[16]
+    // replay (Sim3Solver::iterate's loop on the device)
+    int minInliers, maxIts, nIt0, pad;
+    orb_rng rng;
+    Sim3StateDev* state;
+    Sim3OutDev* out;
+    uint32_t* outMask;
 };
 
 class Sim3Solver {
@@ -39,9 +61,9 @@ public:
     float K1_[4], K2_[4];
     double prob_ = 0.99;
     int minInliers_ = 6, maxIts_ = 300;
-    int nIterations_ = 0, nBestInliers_ = 0;
-    std::vector<uint8_t> bestInliers_;
-    float bestR_[9] = {}, bestT_[3] = {}, bestS_ = 0, bestT12_[16] = {};
+    int nIterations_ = 0, nBestInliers_ = 0;   // mirrors of the device state after each call
+    float bestR_[9] = {}, bestT_[3] = {}, bestS_ = 0;
+    size_t state_off() const;
     void* d_pts_ = nullptr;
     size_t d_cap_ = 0;
     bool dirty_ = true;
