@@ -705,6 +705,123 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
+// z = D^-1 y, then L^T x = z (per row, subtractions in descending k order; L[k][i] =
+// Lall[i * n + k]) by one wave; y is overwritten.  The oracle's ora_ldlt_solve sequence.
+__device__ __forceinline__ void ldlt_backward_wave(int n, const double* Lall, const double* dvec, double* y, double* x,
+                                                   double* scal) {
+    const int lane = threadIdx.x & 63;
+    for (int k = lane; k < n; k += 64) y[k] = y[k] / dvec[k];
+    __builtin_amdgcn_wave_barrier();
+    for (int r1 = n; r1 > 0; r1 -= 64) {
+        const int r0 = max(r1 - 64, 0);
+        const int i = r0 + lane;
+        const bool on = i < r1;
+        const int ic = on ? i : r0;
+        double acc = on ? y[i] : 0.0;
+        int k = n - 1;
+        for (; k - 8 >= r1 - 1; k -= 8) {
+            double L8[8], Y8[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                L8[u] = Lall[(size_t)ic * n + (k - u)];
+                Y8[u] = y[k - u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc -= L8[u] * Y8[u];
+        }
+        for (; k >= r1; k--) acc -= Lall[(size_t)ic * n + k] * y[k];
+        k = r1 - 1;
+        for (; k - 8 >= r0 - 1; k -= 8) {
+            double L8[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) L8[u] = Lall[(size_t)ic * n + (k - u)];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const double yk = readlane_d(acc, k - u - r0);
+                if (i < k - u) acc -= L8[u] * yk;
+            }
+        }
+        for (; k >= r0; k--) {
+            const double yk = readlane_d(acc, k - r0);
+            if (i < k) acc -= Lall[(size_t)ic * n + k] * yk;
+        }
+        if (on) y[i] = acc;
+        __builtin_amdgcn_wave_barrier();
+    }
+    for (int k = lane; k < n; k += 64) x[k] = y[k];
+    if (lane == 0) scal[3] = 1.0;
+}
+
+// Row-owner LDL^T + forward substitution for n <= kLdltRowMax (16 free keyframes: a local BA),
+// two waves.  Thread i holds row i of [S | b] (its upper part, j >= i) in registers.  At pivot
+// k, row k -- final after its k updates -- sits in LDS (published by its owner at the end of
+// pivot k - 1, double-buffered); every row i > k forms l_ik = u_ki / d_k and subtracts
+// l_ik * u_kj from each of its entries, k ascending per element: the oracle's ora_ldlt_solve
+// sequence (the right-hand side, column n, runs the forward substitution y_i -= l_ik y_k).
+// Row k + 1 then publishes itself: one barrier per pivot, no panel round trips.
+constexpr int kLdltRowMax = 96;
+__global__ void __launch_bounds__(128) k_ldlt_row(int n, const double* __restrict__ Sg, const double* bs, double* x,
+                                                  double* scal, const int* run) {
+    BA_GATE(run);
+    __shared__ double Ur[2][kLdltRowMax + 1];   // published row k: entries j < n, b_k at [kLdltRowMax]
+    __shared__ double Lall[kLdltRowMax * kLdltRowMax];   // L[i][k] at Lall[k * n + i]
+    __shared__ double dvec[kLdltRowMax], y[kLdltRowMax];
+    const int i = threadIdx.x;
+    const bool mine = i < n;
+    double a[kLdltRowMax];
+#pragma unroll
+    for (int j = 0; j < kLdltRowMax; j++) a[j] = (mine && j < n && j >= i) ? Sg[(size_t)i * n + j] : 0.0;
+    double bi = mine ? bs[i] : 0.0;
+    if (i == 0) {
+#pragma unroll
+        for (int j = 0; j < kLdltRowMax; j++)
+            if (j < n) Ur[0][j] = a[j];
+        Ur[0][kLdltRowMax] = bi;
+    }
+    __syncthreads();
+    bool ok = true;
+    for (int k = 0; k < n; k++) {
+        const double* U = Ur[k & 1];
+        const double d = U[k];
+        if (d == 0.0) {   // uniform: every thread reads the same pivot
+            ok = false;
+            break;
+        }
+        if (i == 0) {
+            dvec[k] = d;
+            y[k] = U[kLdltRowMax];   // b_k after its k updates: forward-substituted y_k
+        }
+        if (i > k && mine) {
+            const double l = U[i] / d;
+            Lall[(size_t)k * n + i] = l;
+#pragma unroll
+            for (int c = 0; c < kLdltRowMax / 8; c++) {
+                if (8 * c + 7 < i) continue;
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const int j = 8 * c + q;
+                    if (j >= i && j < n) a[j] -= l * U[j];
+                }
+            }
+            bi -= l * U[kLdltRowMax];
+            if (i == k + 1) {   // row k + 1 is final: publish it for the next pivot
+                double* V = Ur[(k + 1) & 1];
+#pragma unroll
+                for (int j = 0; j < kLdltRowMax; j++)
+                    if (j >= i && j < n) V[j] = a[j];
+                V[kLdltRowMax] = bi;
+            }
+        }
+        __syncthreads();
+    }
+    if (!ok) {
+        if (i == 0) scal[3] = 0.0;
+        return;
+    }
+    if (i >= 64) return;
+    ldlt_backward_wave(n, Lall, dvec, y, x, scal);
+}
+
 // Register-resident LDL^T + solve for n < 128 (<= 21 free keyframes), 1024 threads.
 // Thread (wave w < 16, lane) owns rows i = 16 r + w (r < 8) of columns j = lane, lane + 64.
 // Per 6-column panel: owners publish the panel rows to LDS (U), wave 0 factorises them
@@ -878,47 +995,7 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
     }
     if (w != 0) return;
     LDLT_PROBE(3);
-    for (int k = lane; k < n; k += 64) y[k] = y[k] / dvec[k];
-    __builtin_amdgcn_wave_barrier();
-    // L^T x = z: per row, subtractions in descending k order (L[k][i] = Lall[i * n + k])
-    for (int r1 = n; r1 > 0; r1 -= 64) {
-        const int r0 = max(r1 - 64, 0);
-        const int i = r0 + lane;
-        const bool on = i < r1;
-        const int ic = on ? i : r0;
-        double acc = on ? y[i] : 0.0;
-        int k = n - 1;
-        for (; k - 8 >= r1 - 1; k -= 8) {
-            double L8[8], Y8[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                L8[u] = Lall[(size_t)ic * n + (k - u)];
-                Y8[u] = y[k - u];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) acc -= L8[u] * Y8[u];
-        }
-        for (; k >= r1; k--) acc -= Lall[(size_t)ic * n + k] * y[k];
-        k = r1 - 1;
-        for (; k - 8 >= r0 - 1; k -= 8) {
-            double L8[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) L8[u] = Lall[(size_t)ic * n + (k - u)];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const double yk = readlane_d(acc, k - u - r0);
-                if (i < k - u) acc -= L8[u] * yk;
-            }
-        }
-        for (; k >= r0; k--) {
-            const double yk = readlane_d(acc, k - r0);
-            if (i < k) acc -= Lall[(size_t)ic * n + k] * yk;
-        }
-        if (on) y[i] = acc;
-        __builtin_amdgcn_wave_barrier();
-    }
-    for (int k = lane; k < n; k += 64) x[k] = y[k];
-    if (lane == 0) scal[3] = 1.0;
+    ldlt_backward_wave(n, Lall, dvec, y, x, scal);
     LDLT_PROBE(4);
 }
 
@@ -2832,6 +2909,15 @@ static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 // k_scale_chunks + k_csum; orbgpu_unit_set_scale_small_max lowers it so tests drive the chunked
 // path (and the device LM's scale == 0 branch) at oracle-sized problems
 static std::atomic<int> g_scale_small_max{2048 * 64};
+// the row-owner dense LDL^T (k_ldlt_row) up to kLdltRowMax rows; ORBGPU_LDLT_ROW=0 keeps the
+// panel kernel (k_ldlt_reg) for A/B runs.  Both perform the oracle's operation sequence.
+static bool ldlt_row_ok(int n) {
+    static const bool off = [] {
+        const char* e = std::getenv("ORBGPU_LDLT_ROW");
+        return e && e[0] == '0';
+    }();
+    return n <= kLdltRowMax && !off;
+}
 static bool scale_small(int nP, int nL) { return 6 * nP + 3 * nL <= g_scale_small_max.load(); }
 int debug_set_scale_small_max(int v) {
     if (v < 0 || v > 2048 * 64) return 1;
@@ -2886,6 +2972,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const int in_lds = ldsBytes <= ldsMax_ ? 1 : 0;
     const size_t shm = in_lds ? ldsBytes : sizeof(double) * (size_t)n;
     const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
+    const bool use_row = ldlt_row_ok(n);
     const bool use_reg = n < kLdltMax && regShm <= ldsMax_;   // b rides in column n
     // n <= 128: register-resident single-workgroup LDL^T; S fits LDS: single-workgroup in LDS;
     // larger: block-sparse tiled LDL^T in HBM (ldlt.hip, structure from build_structure)
@@ -2919,6 +3006,8 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         }
         if (tiled_) {
             if (int e = sp_.solve(dBs_, dX2_, dScal_, s)) return e;
+        } else if (use_row) {
+            hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else if (use_reg) {
             hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else {
@@ -3055,7 +3144,8 @@ void BaEngine::enqueue_lm_step(bool first) {
                                dScal_, dEmat_, dCb_, ctl);
     if (S.nBlk) schur_launch(S.nBlk, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_, 0.0,
                                    1, dScal_, sa, dBs_, 1, ctl);
-    if (use_reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    if (ldlt_row_ok(n)) hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else if (use_reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, ctl);
     if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_, dXbak_,
                                     dX2_, dHplA_, dHll_, dBl_, 0.0, 1, dScal_, ctl);
@@ -3247,7 +3337,10 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     ORB_HIP_CHECK(hipMemcpy(dS, S, sizeof(double) * n * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemcpy(dB, b, sizeof(double) * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemset(dX, 0, sizeof(double) * nn));
-    if (variant == 0) {
+    if (variant == 4) {
+        if (n > kLdltRowMax) return -3;
+        hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, 0, n, dS, dB, dX, dScal, nullptr);
+    } else if (variant == 0) {
         const size_t shm = sizeof(double) * ((size_t)n * n + 14 * kLdltMax);
         hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal, nullptr);
     } else {
