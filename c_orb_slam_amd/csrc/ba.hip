@@ -2598,6 +2598,9 @@ int BaEngine::carve(bool commit, size_t* total) {
     dScal_ = (double*)take(sizeof(double) * 16);
     dCounter_ = (unsigned*)take(sizeof(unsigned) * 16);
     dLm_ = (LmDev*)take(sizeof(LmDev));
+    dKfFixed_ = (uint8_t*)take(nkf);
+    dKfId_ = (int32_t*)take(sizeof(int32_t) * nkf);
+    dPtId_ = (int32_t*)take(sizeof(int32_t) * npt);
     dScratch_ = (double*)take(sizeof(double) * scratchN_);
     tmpA0_ = (double*)take(sizeof(double) * tmpN);
     tmpA1_ = (double*)take(sizeof(double) * tmpN);
@@ -2656,11 +2659,17 @@ int BaEngine::upload_problem(const ba_problem* P) {
     // poses, points and edges written straight into the pinned staging block (no intermediate
     // host copy), uploaded with one wait
     const size_t bT = sizeof(Se3) * nkf_, bX = sizeof(double) * 3 * (size_t)npt_, bE = sizeof(EdgeDev) * ne_;
-    if (int e = stage_reserve(bT + bX + bE + 64)) return e;
+    // + the static vertex data the device structure builder reads (fixed flags, mnIds)
+    const size_t bF = ((size_t)nkf_ + 7) & ~(size_t)7, bK = sizeof(int32_t) * nkf_, bP = sizeof(int32_t) * npt_;
+    if (int e = stage_reserve(bT + bX + bE + bF + bK + bP + 64)) return e;
     char* st = (char*)hStage_;
     Se3* Ts = reinterpret_cast<Se3*>(st);
     double* Xs = reinterpret_cast<double*>(st + bT);
     EdgeDev* Es = reinterpret_cast<EdgeDev*>(st + bT + bX);
+    char* sv = st + bT + bX + bE;
+    std::memcpy(sv, kfFixed_.data(), nkf_);
+    std::memcpy(sv + bF, P->kf_id, bK);
+    std::memcpy(sv + bF + bK, P->pt_id, bP);
     for (int k = 0; k < nkf_; k++) host_se3_from_Tcw(P->kf_Tcw + 16 * k, Ts[k]);
     for (size_t q = 0; q < 3 * (size_t)npt_; q++) Xs[q] = (double)P->pt_pos[q];
     // Huber deltas: LocalBundleAdjustment sqrt(5.991) (Optimizer.cc:585), BundleAdjustment sqrt(5.99) (:87)
@@ -2686,6 +2695,9 @@ int BaEngine::upload_problem(const ba_problem* P) {
     if (bT) ORB_HIP_CHECK(hipMemcpyAsync(dT_, st, bT, hipMemcpyHostToDevice, s));
     if (bX) ORB_HIP_CHECK(hipMemcpyAsync(dX_, st + bT, bX, hipMemcpyHostToDevice, s));
     if (bE) ORB_HIP_CHECK(hipMemcpyAsync(dE_, st + bT + bX, bE, hipMemcpyHostToDevice, s));
+    if (nkf_) ORB_HIP_CHECK(hipMemcpyAsync(dKfFixed_, sv, nkf_, hipMemcpyHostToDevice, s));
+    if (bK) ORB_HIP_CHECK(hipMemcpyAsync(dKfId_, sv + bF, bK, hipMemcpyHostToDevice, s));
+    if (bP) ORB_HIP_CHECK(hipMemcpyAsync(dPtId_, sv + bF + bK, bP, hipMemcpyHostToDevice, s));
     if (ne_) {
         ORB_HIP_CHECK(hipMemsetAsync(dLevel_, 0, ne_, s));
         ORB_HIP_CHECK(hipMemsetAsync(dRobust_, (mode_.global && !mode_.robust) ? 0 : 1, ne_, s));
@@ -2696,6 +2708,16 @@ int BaEngine::upload_problem(const ba_problem* P) {
     // staging block (stage_reserve) waits for them
     uploadPending_ = true;
     return 0;
+}
+
+// ORBGPU_STRUCT_HOST=1: the host restatement (ba_struct.cpp) builds the lists instead of the
+// device (A/B runs; both produce the same lists, tests/test_gpu_ba_struct.py)
+static bool struct_host() {
+    static const bool v = [] {
+        const char* e = std::getenv("ORBGPU_STRUCT_HOST");
+        return e && e[0] == '1';
+    }();
+    return v;
 }
 
 // initializeOptimization(level) + buildIndexMapping + BlockSolver::buildStructure
@@ -2709,90 +2731,126 @@ int BaEngine::build_structure(int level) {
         fprintf(stderr, "[ba]   structure %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - ts0).count());
         ts0 = t;
     };
-    BaHostStruct& H = hs_;
-    std::vector<uint8_t> kfAct, ptAct;
-    ba_active_set(level, nkf_, npt_, ne_, eKf_.data(), ePt_.data(), level_.data(), &H.aE, &kfAct, &ptAct);
-    if (comm_) {
-        // shards agree on the pose set: a keyframe is active if any shard has an active edge
-        // on it (its pose index must be the same everywhere); also the global edge/landmark counts
-        int nLloc = 0;
-        for (int p = 0; p < npt_; p++) nLloc += ptAct[p];
-        std::vector<double> red(nkf_ + 2);
-        for (int k = 0; k < nkf_; k++) red[k] = kfAct[k];
-        red[nkf_] = (double)H.aE.size();
-        red[nkf_ + 1] = (double)nLloc;
-        if (h2d_sync(dScratch_, red.data(), sizeof(double) * red.size())) return -2;
-        if (int e = comm_->allreduce(dScratch_, red.size(), RedOp::Sum, stream_)) return e;
-        if (d2h_sync(red.data(), dScratch_, sizeof(double) * red.size())) return -2;
-        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
-        for (int k = 0; k < nkf_; k++) kfAct[k] = red[k] > 0 ? 1 : 0;
-        nEglob_ = (int)red[nkf_];
-        nLglob_ = (int)red[nkf_ + 1];
-    }
-    lap("active set");
-    if (ba_build_lists(nkf_, npt_, eKf_.data(), ePt_.data(), kfFixed_.data(), kfId_.data(), ptId_.data(), kfAct, ptAct,
-                       &H))
-        return -1;
-    lap("lists");
-    const int nE = (int)H.aE.size(), nP = (int)H.poseKf.size(), nL = (int)H.landPt.size();
-    if (!comm_) {
-        nEglob_ = nE;
-        nLglob_ = nL;
-    }
-    const std::vector<int32_t>&aE = H.aE, &ePose = H.ePose, &eLand = H.eLand, &poseKf = H.poseKf, &landPt = H.landPt,
-          &peStart = H.peStart, &peList = H.peList, &leStart = H.leStart, &leList = H.leList, &lpStart = H.lpStart,
-          &lpList = H.lpList, &blkI = H.blkI, &blkJ = H.blkJ, &blkStart = H.blkStart, &pairA = H.pairA,
-          &pairB = H.pairB;
-    const int nBlk = (int)blkI.size();
-    for (int i = 0; i < nP; i++)
-        if (peStart[i + 1] - peStart[i] > 64 * kChunks) return -3;
-    for (int l = 0; l < nL; l++)
-        if (leStart[l + 1] - leStart[l] > 64 * 64) return -3;
-    if (nE > kCsumLv * 64 * 64 || 6LL * nP + 3LL * nL > (long long)scratchN_) return -3;
-    for (int b = 0; b < nBlk; b++)
-        if (blkStart[b + 1] - blkStart[b] > 64 * kChunks) return -3;
-    // pack and upload
-    std::vector<const std::vector<int32_t>*> parts = {&aE,      &ePose,   &eLand,  &poseKf, &landPt, &peStart,
-                                                      &peList,  &leStart, &leList, &lpStart, &lpList, &blkI,
-                                                      &blkJ,    &blkStart, &pairA, &pairB};
-    size_t tot = 0;
-    for (auto* p : parts) tot += (p->size() + 63) & ~(size_t)63;
-    if (tot * 4 > dStructCap_) {
-        if (dStruct_) (void)hipFree(dStruct_);
-        ORB_HIP_CHECK(hipMalloc(&dStruct_, tot * 4 * 2));
-        dStructCap_ = tot * 4 * 2;
-    }
-    if (int e = stage_reserve(tot * 4)) return e;   // copied below, waited for at the end
-    // the lists packed straight into the pinned staging block (64-entry aligned sections), the
-    // copy split over host threads in 64-entry groups on large systems
-    int32_t* hs = reinterpret_cast<int32_t*>(hStage_);
-    std::vector<size_t> off;
-    size_t o = 0;
-    for (auto* p : parts) {
-        off.push_back(o);
-        o += (p->size() + 63) & ~(size_t)63;
-    }
-    host_parallel((int)(tot / 64), [&](int g0, int g1) {
-        const size_t a = (size_t)g0 * 64, b = (size_t)g1 * 64;
-        for (size_t k = 0; k < parts.size(); k++) {
-            const size_t s0 = off[k], len = parts[k]->size(), e0 = s0 + ((len + 63) & ~(size_t)63);
-            const size_t x0 = std::max(a, s0), x1 = std::min(b, e0);
-            if (x0 >= x1) continue;
-            const size_t d1 = std::min(x1, s0 + len);   // list entries [x0, d1), zero padding [d1, x1)
-            if (x0 < d1) std::memcpy(hs + x0, parts[k]->data() + (x0 - s0), sizeof(int32_t) * (d1 - x0));
-            const size_t z0 = std::max(x0, s0 + len);
-            if (z0 < x1) std::memset(hs + z0, 0, sizeof(int32_t) * (x1 - z0));
+    int nE = 0, nP = 0, nL = 0, nBlk = 0;
+    std::vector<int64_t> offKeys;    // off-diagonal Schur blocks i1 * nP + i2, ascending (tiled path)
+    std::vector<int32_t> blkIJ;      // blkI ++ blkJ (dense sharded path)
+    if (!struct_host()) {
+        // the lists built on the device from the edges already in HBM (ba_struct_gpu.hip)
+        GpuStructInfo info{};
+        const int r = gs_.build(level, nkf_, npt_, ne_, dE_, dLevel_, dKfFixed_, dKfId_, dPtId_, comm_, stream_, &st_,
+                                &info, comm_ ? &blkIJ : nullptr);
+        if (r == -1) return -1;
+        if (r) return r;
+        lap("lists (device)");
+        nE = info.nE;
+        nP = info.nP;
+        nL = info.nL;
+        nBlk = info.nBlk;
+        nEglob_ = info.nEglob;
+        nLglob_ = info.nLglob;
+        if (info.maxPe > 64 * kChunks || info.maxLe > 64 * 64 || info.maxBlk > 64 * kChunks) return -3;
+        if (nE > kCsumLv * 64 * 64 || 6LL * nP + 3LL * nL > (long long)scratchN_) return -3;
+        if (nP >= kTiledMinPoses && !comm_) {
+            if (int e = gs_.offkeys(&offKeys, stream_)) return e;
+        } else if (nP >= kTiledMinPoses) {
+            for (int b = 0; b < nBlk; b++)
+                if (blkIJ[b] != blkIJ[nBlk + b]) offKeys.push_back((int64_t)blkIJ[b] * nP + blkIJ[nBlk + b]);
         }
-    }, 1 << 14);
-    ORB_HIP_CHECK(hipMemcpyAsync(dStruct_, hStage_, tot * 4, hipMemcpyHostToDevice, stream_));
-    // the sharded and block-sparse set-ups below stage more uploads through the same block
-    if (comm_ || nP >= kTiledMinPoses) ORB_HIP_CHECK(hipStreamSynchronize(stream_));
-    const int32_t* d = dStruct_;
-    st_.nE = nE; st_.nP = nP; st_.nL = nL; st_.nBlk = nBlk;
-    st_.aE = d + off[0]; st_.ePose = d + off[1]; st_.eLand = d + off[2]; st_.poseKf = d + off[3];
-    st_.landPt = d + off[4]; st_.peStart = d + off[5]; st_.peList = d + off[6]; st_.leStart = d + off[7];
-    st_.leList = d + off[8]; st_.lpStart = d + off[9]; st_.lpList = d + off[10]; st_.blkI = d + off[11];
-    st_.blkJ = d + off[12]; st_.blkStart = d + off[13]; st_.pairA = d + off[14]; st_.pairB = d + off[15];
+    } else {
+        BaHostStruct& H = hs_;
+        std::vector<uint8_t> kfAct, ptAct;
+        ba_active_set(level, nkf_, npt_, ne_, eKf_.data(), ePt_.data(), level_.data(), &H.aE, &kfAct, &ptAct);
+        if (comm_) {
+            // shards agree on the pose set: a keyframe is active if any shard has an active edge
+            // on it (its pose index must be the same everywhere); also the global edge/landmark counts
+            int nLloc = 0;
+            for (int p = 0; p < npt_; p++) nLloc += ptAct[p];
+            std::vector<double> red(nkf_ + 2);
+            for (int k = 0; k < nkf_; k++) red[k] = kfAct[k];
+            red[nkf_] = (double)H.aE.size();
+            red[nkf_ + 1] = (double)nLloc;
+            if (h2d_sync(dScratch_, red.data(), sizeof(double) * red.size())) return -2;
+            if (int e = comm_->allreduce(dScratch_, red.size(), RedOp::Sum, stream_)) return e;
+            if (d2h_sync(red.data(), dScratch_, sizeof(double) * red.size())) return -2;
+            ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+            for (int k = 0; k < nkf_; k++) kfAct[k] = red[k] > 0 ? 1 : 0;
+            nEglob_ = (int)red[nkf_];
+            nLglob_ = (int)red[nkf_ + 1];
+        }
+        lap("active set");
+        if (ba_build_lists(nkf_, npt_, eKf_.data(), ePt_.data(), kfFixed_.data(), kfId_.data(), ptId_.data(), kfAct, ptAct,
+                           &H))
+            return -1;
+        lap("lists");
+        nE = (int)H.aE.size();
+        nP = (int)H.poseKf.size();
+        nL = (int)H.landPt.size();
+        if (!comm_) {
+            nEglob_ = nE;
+            nLglob_ = nL;
+        }
+        const std::vector<int32_t>&aE = H.aE, &ePose = H.ePose, &eLand = H.eLand, &poseKf = H.poseKf, &landPt = H.landPt,
+              &peStart = H.peStart, &peList = H.peList, &leStart = H.leStart, &leList = H.leList, &lpStart = H.lpStart,
+              &lpList = H.lpList, &blkI = H.blkI, &blkJ = H.blkJ, &blkStart = H.blkStart, &pairA = H.pairA,
+              &pairB = H.pairB;
+        nBlk = (int)blkI.size();
+        for (int i = 0; i < nP; i++)
+            if (peStart[i + 1] - peStart[i] > 64 * kChunks) return -3;
+        for (int l = 0; l < nL; l++)
+            if (leStart[l + 1] - leStart[l] > 64 * 64) return -3;
+        if (nE > kCsumLv * 64 * 64 || 6LL * nP + 3LL * nL > (long long)scratchN_) return -3;
+        for (int b = 0; b < nBlk; b++)
+            if (blkStart[b + 1] - blkStart[b] > 64 * kChunks) return -3;
+        // pack and upload
+        std::vector<const std::vector<int32_t>*> parts = {&aE,      &ePose,   &eLand,  &poseKf, &landPt, &peStart,
+                                                          &peList,  &leStart, &leList, &lpStart, &lpList, &blkI,
+                                                          &blkJ,    &blkStart, &pairA, &pairB};
+        size_t tot = 0;
+        for (auto* p : parts) tot += (p->size() + 63) & ~(size_t)63;
+        if (tot * 4 > dStructCap_) {
+            if (dStruct_) (void)hipFree(dStruct_);
+            ORB_HIP_CHECK(hipMalloc(&dStruct_, tot * 4 * 2));
+            dStructCap_ = tot * 4 * 2;
+        }
+        if (int e = stage_reserve(tot * 4)) return e;   // copied below, waited for at the end
+        // the lists packed straight into the pinned staging block (64-entry aligned sections), the
+        // copy split over host threads in 64-entry groups on large systems
+        int32_t* hs = reinterpret_cast<int32_t*>(hStage_);
+        std::vector<size_t> off;
+        size_t o = 0;
+        for (auto* p : parts) {
+            off.push_back(o);
+            o += (p->size() + 63) & ~(size_t)63;
+        }
+        host_parallel((int)(tot / 64), [&](int g0, int g1) {
+            const size_t a = (size_t)g0 * 64, b = (size_t)g1 * 64;
+            for (size_t k = 0; k < parts.size(); k++) {
+                const size_t s0 = off[k], len = parts[k]->size(), e0 = s0 + ((len + 63) & ~(size_t)63);
+                const size_t x0 = std::max(a, s0), x1 = std::min(b, e0);
+                if (x0 >= x1) continue;
+                const size_t d1 = std::min(x1, s0 + len);   // list entries [x0, d1), zero padding [d1, x1)
+                if (x0 < d1) std::memcpy(hs + x0, parts[k]->data() + (x0 - s0), sizeof(int32_t) * (d1 - x0));
+                const size_t z0 = std::max(x0, s0 + len);
+                if (z0 < x1) std::memset(hs + z0, 0, sizeof(int32_t) * (x1 - z0));
+            }
+        }, 1 << 14);
+        ORB_HIP_CHECK(hipMemcpyAsync(dStruct_, hStage_, tot * 4, hipMemcpyHostToDevice, stream_));
+        // the sharded and block-sparse set-ups below stage more uploads through the same block
+        if (comm_ || nP >= kTiledMinPoses) ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        const int32_t* d = dStruct_;
+        st_.nE = nE; st_.nP = nP; st_.nL = nL; st_.nBlk = nBlk;
+        st_.aE = d + off[0]; st_.ePose = d + off[1]; st_.eLand = d + off[2]; st_.poseKf = d + off[3];
+        st_.landPt = d + off[4]; st_.peStart = d + off[5]; st_.peList = d + off[6]; st_.leStart = d + off[7];
+        st_.leList = d + off[8]; st_.lpStart = d + off[9]; st_.lpList = d + off[10]; st_.blkI = d + off[11];
+        st_.blkJ = d + off[12]; st_.blkStart = d + off[13]; st_.pairA = d + off[14]; st_.pairB = d + off[15];
+        if (nP >= kTiledMinPoses)
+            for (int b = 0; b < nBlk; b++)
+                if (blkI[b] != blkJ[b]) offKeys.push_back((int64_t)blkI[b] * nP + blkJ[b]);
+        if (comm_) {
+            blkIJ.assign(blkI.begin(), blkI.end());
+            blkIJ.insert(blkIJ.end(), blkJ.begin(), blkJ.end());
+        }
+    }
     nTiles_ = 0;
     // at least kTiledMinPoses free poses: the block-sparse nested-dissection solver (the oracle
     // switches at the same count); below, the dense single-workgroup solvers in natural order
@@ -2802,9 +2860,7 @@ int BaEngine::build_structure(int level) {
         // block-sparse system: the pose graph (poses sharing a point; union over the shards,
         // so every rank orders and factors the same structure) -> nested-dissection order,
         // symbolic factorisation; S travels as the Schur-pattern prefix of the tiles
-        std::vector<int64_t> mine;
-        for (int b = 0; b < nBlk; b++)
-            if (blkI[b] != blkJ[b]) mine.push_back((int64_t)blkI[b] * nP + blkJ[b]);
+        std::vector<int64_t> mine = std::move(offKeys);
         std::vector<int64_t> all;
         if (comm_) {
             if (int e = gather_blocks(mine, &all)) return e;
@@ -2833,7 +2889,7 @@ int BaEngine::build_structure(int level) {
         const int n = 6 * nP, nt = (n + 63) / 64;
         std::vector<double> tm((size_t)nt * nt, 0.0);
         for (int b = 0; b < nBlk; b++) {
-            const int i1 = blkI[b], i2 = blkJ[b];
+            const int i1 = blkIJ[b], i2 = blkIJ[nBlk + b];
             for (int I = (6 * i1) / 64; I <= (6 * i1 + 5) / 64; I++)
                 for (int J = (6 * i2) / 64; J <= (6 * i2 + 5) / 64; J++)
                     if (I <= J) tm[(size_t)I * nt + J] = 1.0;

@@ -9,6 +9,8 @@
 
 #include "../../include/orbslam_gpu.h"
 #include "ba_struct.hpp"
+#include "ba_struct_gpu.hpp"
+#include "ba_types.hpp"
 #include "comm.hpp"
 #include "ldlt.hpp"
 #include "orb_common.hpp"
@@ -19,36 +21,6 @@ struct Se3 {  // g2o::SE3Quat: q = (x, y, z, w) like Eigen coeffs(), t
     double q[4];
     double t[3];
     double pad;
-};
-
-struct EdgeDev {  // one g2o edge (vertex 0 = point, vertex 1 = keyframe pose)
-    double obs[3];
-    double info;            // invSigma2 (float -> double)
-    double fx, fy, cx, cy, bf;
-    double delta, dsqr;     // RobustKernelHuber: delta = (double)(float)sqrt(th)
-    int32_t pt, kf;
-    int32_t stereo, pad;
-};
-
-// per-phase active structure (initializeOptimization + buildIndexMapping + buildStructure)
-struct BaStructDev {
-    int nE, nP, nL, nBlk;
-    const int32_t* aE;        // active edge -> edge
-    const int32_t* ePose;     // active edge -> pose index or -1 (fixed keyframe)
-    const int32_t* eLand;     // active edge -> landmark index
-    const int32_t* poseKf;    // pose index -> keyframe
-    const int32_t* landPt;    // landmark index -> point
-    const int32_t* peStart;   // pose -> active edges (edge order)
-    const int32_t* peList;
-    const int32_t* leStart;   // landmark -> active edges (edge order)
-    const int32_t* leList;
-    const int32_t* lpStart;   // landmark -> active edges with a free pose (pose order)
-    const int32_t* lpList;
-    const int32_t* blkI;      // Schur blocks (i1 <= i2), diagonal blocks always present
-    const int32_t* blkJ;
-    const int32_t* blkStart;  // block -> pair terms (landmark order)
-    const int32_t* pairA;     // active edge of the landmark to pose i1
-    const int32_t* pairB;     // active edge of the landmark to pose i2
 };
 
 struct BaTrace {
@@ -116,7 +88,10 @@ private:
     std::vector<uint8_t> kfFixed_, kfLocal_, level_, ptHasEdge_;
     // structure
     BaStructDev st_{};
-    BaHostStruct hs_;              // host lists of the current structure (reused across calls)
+    BaHostStruct hs_;              // host lists of the current structure (ORBGPU_STRUCT_HOST=1 path)
+    GpuStructBuilder gs_;          // the lists built on the device (default)
+    uint8_t* dKfFixed_ = nullptr;  // device copies of the static vertex data the builder reads
+    int32_t *dKfId_ = nullptr, *dPtId_ = nullptr;
     int32_t* dStruct_ = nullptr;
     size_t dStructCap_ = 0;
     // system / workspace

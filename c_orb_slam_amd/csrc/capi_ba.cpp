@@ -7,6 +7,7 @@
 
 #include "ba.hpp"
 #include "ba_struct.hpp"
+#include "ba_struct_gpu.hpp"
 #include "capi_handles.hpp"
 #include "ordering.hpp"
 #include "orb_match.hpp"
@@ -420,6 +421,30 @@ int orbgpu_unit_ba_struct(int nkf, int npt, int ne, const int32_t* edge_kf, cons
     put(S.poseKf, nP); put(S.landPt, nL); put(S.ePose, nE); put(S.eLand, nE); put(S.lpStart, nL + 1);
     put(S.lpList, S.lpStart[nL]); put(S.blkI, nBlk); put(S.blkJ, nBlk); put(S.blkStart, nBlk + 1);
     put(S.pairA, nPair); put(S.pairB, nPair);
+    return ORB_OK;
+}
+
+int orbgpu_unit_ba_struct_all(int nkf, int npt, int ne, const int32_t* edge_kf, const int32_t* edge_pt,
+                              const uint8_t* edge_level, const uint8_t* kf_fixed, const int32_t* kf_id,
+                              const int32_t* pt_id, int level, int gpu, int32_t* out, long long cap, long long* n_out) {
+    if (nkf < 0 || npt < 0 || ne < 0 || !out || !n_out) return ORB_E_INVALID;
+    if ((ne && (!edge_kf || !edge_pt || !edge_level)) || (nkf && (!kf_fixed || !kf_id)) || (npt && !pt_id))
+        return ORB_E_INVALID;
+    for (int i = 0; i < ne; i++)
+        if (edge_kf[i] < 0 || edge_kf[i] >= nkf || edge_pt[i] < 0 || edge_pt[i] >= npt) return ORB_E_INVALID;
+    if (gpu) {
+        int rc = 0;
+        engine(&rc);
+        if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    }
+    std::vector<int32_t> v;
+    const int r = orbgpu::debug_struct_all(nkf, npt, ne, edge_kf, edge_pt, edge_level, kf_fixed, kf_id, pt_id, level,
+                                           gpu, &v);
+    if (r == -1) return ORB_E_INVALID;
+    if (r) return ORB_E_HIP;
+    *n_out = (long long)v.size();
+    if ((long long)v.size() > cap) return ORB_E_CAPACITY;
+    std::copy(v.begin(), v.end(), out);
     return ORB_OK;
 }
 

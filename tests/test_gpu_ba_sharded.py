@@ -207,3 +207,54 @@ def test_global_ba_config5_8000kf_loops_matches_oracle(gpu):
     assert g["iterations"] == o["iterations"]
     np.testing.assert_allclose(g["trial_chi2"], o["trial_chi2"], rtol=1e-12)
     _exact(g, o)
+
+
+def _golden_large(name):
+    import hashlib
+    import json
+    from pathlib import Path
+    p = Path(__file__).resolve().parent / "golden" / "gba_large.json"
+    data = json.loads(p.read_text()) if p.exists() else {}
+    if name not in data:
+        pytest.skip(f"{name} not in tests/golden/gba_large.json (tests/golden/make_gba_large.py)")
+    g = data[name]
+    c = g["case"]
+    pr = global_ba_problem(c["seed"], n_kf=c["n_kf"], pts_per_kf=c["pts_per_kf"], laps=c["laps"])
+    h = hashlib.sha256()
+    for k in ("kf_id", "kf_Tcw", "kf_local", "kf_cam", "pt_id", "pt_pos", "edge_pt", "edge_kf", "edge_obs",
+              "edge_inv_sigma2"):
+        h.update(np.ascontiguousarray(pr[k]).tobytes())
+    assert h.hexdigest() == g["input_sha256"], "the generated problem differs from the fixture's"
+    return pr, g
+
+
+def _check_golden(res, g):
+    import hashlib
+    assert list(res["iterations"]) == g["iterations"]
+    assert len(res["trial_chi2"]) == len(g["trial_chi2"])
+    np.testing.assert_allclose(res["trial_chi2"], g["trial_chi2"], rtol=1e-12)
+    np.testing.assert_allclose(res["trial_lambda"], g["trial_lambda"], rtol=1e-12)
+    assert hashlib.sha256(np.ascontiguousarray(res["kf_Tcw"], np.float32).tobytes()).hexdigest() == g["kf_Tcw_sha256"]
+    assert hashlib.sha256(np.ascontiguousarray(res["pt_pos"], np.float32).tobytes()).hexdigest() == g["pt_pos_sha256"]
+
+
+@pytest.mark.timeout(900)
+def test_global_ba_config5_8000kf_ten_iterations_golden(gpu):
+    """Config 5 at 8,000 keyframes with the reference's own call, BundleAdjustment(..., 10, ...)
+    (LoopClosing.cc:650): the oracle's 10-iteration run (minutes single-threaded) is a committed
+    fixture (tests/golden/make_gba_large.py: LM trace + SHA-256 of the float32 poses and points);
+    the GPU must reproduce the trace and both digests bit for bit."""
+    from c_orb_slam_amd.optimizer import BundleAdjustment
+    pr, g = _golden_large("kf8000_its10")
+    res = BundleAdjustment(pr, 10, False, trace=True)
+    _check_golden(res, g)
+
+
+@pytest.mark.timeout(900)
+def test_global_ba_config5_16000kf_golden(gpu):
+    """Config 5 at its largest stated size, 16,000 keyframes (~2.2 M points, ~12 M edges), one LM
+    iteration against the oracle's committed fixture: trace and result digests bit for bit."""
+    from c_orb_slam_amd.optimizer import BundleAdjustment
+    pr, g = _golden_large("kf16000_its1")
+    res = BundleAdjustment(pr, 1, False, trace=True)
+    _check_golden(res, g)
