@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--lanes", type=int, default=2,
                     help="batches in flight (buffer sets): extraction of batch k waits for the tracking chain "
                          "of batch k - lanes, which last used its buffers")
+    ap.add_argument("--stereo-batch", type=int, default=0,
+                    help="1: Frame(imLeft, imRight)'s two extractions as ONE batch call of 2B images on one "
+                         "extractor stream (ComputeStereoMatches_batch_at pairs image b with image B + b)")
     ap.add_argument("--pipeline-only", action="store_true",
                     help="only the timed stereo pipeline (+ its CPU baseline): one compact JSON line")
     ap.add_argument("--launch-timeout", type=float, default=3000.0,
@@ -241,8 +244,8 @@ def main():
     m = orb.ORBmatcher(0.9, True)
     L = lib()
     check(L.ORBmatcher_set_device_pointers(m._h, 1))
-    d_L = torch.from_numpy(lefts).to(dev)
-    d_R = torch.from_numpy(rights).to(dev)
+    d_LR = torch.from_numpy(np.concatenate([lefts, rights])).to(dev)   # [lefts | rights], one allocation
+    d_L, d_R = d_LR[:B], d_LR[B:]
     d_obs = torch.ones(cap, dtype=torch.int32, device=dev)
     d_outlier = torch.zeros(cap, dtype=torch.uint8, device=dev)
     eye = torch.eye(4, dtype=torch.float32, device=dev)
@@ -278,12 +281,20 @@ def main():
         of frames max(0, p-K+1)..p, contiguous in the table (UpdateLocalMap's local keyframes)."""
 
         def __init__(self):
-            self.exL = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=B)
-            self.exR = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=B)
-            self.d_kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)   # mvKeys (== mvKeysUn, KITTI k1=0)
-            self.d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
-            self.d_kpsR = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
-            self.d_descR = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+            if args.stereo_batch:   # one extractor, one stream: [lefts | rights] as one batch of 2B images
+                self.exL = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=2 * B)
+                self.exR = self.exL
+                self.d_kps_all = torch.empty((2 * B, cap, 7), dtype=torch.int32, device=dev)
+                self.d_desc_all = torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev)
+                self.d_kps, self.d_kpsR = self.d_kps_all[:B], self.d_kps_all[B:]
+                self.d_desc, self.d_descR = self.d_desc_all[:B], self.d_desc_all[B:]
+            else:
+                self.exL = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=B)
+                self.exR = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=B)
+                self.d_kps = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)   # mvKeys (== mvKeysUn, KITTI k1=0)
+                self.d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+                self.d_kpsR = torch.empty((B, cap, 7), dtype=torch.int32, device=dev)
+                self.d_descR = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
             self.d_uR = torch.empty((B, cap), dtype=torch.float32, device=dev)      # mvuRight
             self.d_depth = torch.empty((B, cap), dtype=torch.float32, device=dev)   # mvDepth
             self.d_mp_pos = torch.zeros((B, cap, 3), dtype=torch.float32, device=dev)
@@ -396,6 +407,14 @@ def main():
             # for that chain's device work first (not for its counts)
             if self.epoch:
                 check(L.ORBmatcher_chain_wait(m._h, self.epoch), "ORBmatcher_chain_wait")
+            if args.stereo_batch:
+                n = np.ascontiguousarray(self.exL.extract_device(d_LR.data_ptr(), 2 * B, W, H, W, W * H,
+                                                                 self.d_kps_all.data_ptr(), self.d_desc_all.data_ptr(),
+                                                                 cap), np.int32)
+                self.nL, self.nR = np.ascontiguousarray(n[:B]), np.ascontiguousarray(n[B:])
+                self.tl = self.exL.last_timings()
+                self.tr = {k: 0.0 for k in self.tl}
+                return
             fR = pool.submit(self.exR.extract_device, d_R.data_ptr(), B, W, H, W, W * H, self.d_kpsR.data_ptr(),
                              self.d_descR.data_ptr(), cap)
             self.nL = np.ascontiguousarray(self.exL.extract_device(d_L.data_ptr(), B, W, H, W, W * H,
@@ -408,9 +427,10 @@ def main():
 
         def stereo(self):
             nL, nR = self.nL, self.nR
-            check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, self.exL._h, self.exR._h, B, ptr(nL), self.s_kL,
-                                                          self.s_dL, ptr(nR), self.s_kR, self.s_dR, float(mbf),
-                                                          float(mb), self.s_uR, self.s_dep, ptr(self.nst)),
+            check(L.ORBmatcher_ComputeStereoMatches_batch_at(m._h, self.exL._h, 0, self.exR._h,
+                                                             B if args.stereo_batch else 0, B, ptr(nL), self.s_kL,
+                                                             self.s_dL, ptr(nR), self.s_kR, self.s_dR, float(mbf),
+                                                             float(mb), self.s_uR, self.s_dep, ptr(self.nst)),
                   "ComputeStereoMatches batch")
 
         def search(self):

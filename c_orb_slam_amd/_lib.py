@@ -153,6 +153,8 @@ def lib():
                                                   P(i32)]
     L.ORBmatcher_ComputeStereoMatches_batch.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, f32, vp, vp,
                                                         vp]
+    L.ORBmatcher_ComputeStereoMatches_batch_at.argtypes = [vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp, vp, f32, f32,
+                                                           vp, vp, vp]
     L.ORBmatcher_SearchByProjection_KeyFrame.argtypes = [vp, P(orb_frame), vp, i32, vp, vp, vp, P(orb_mappoints), vp,
                                                          vp, f32, f32, i32, P(i32)]
     L.ORBmatcher_SearchForInitialization.argtypes = [vp, P(orb_frame), P(orb_frame), vp, vp, i32, P(i32)]

@@ -30,14 +30,24 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
                                           const int* NR, const orb_kp* const* keysR,
                                           const uint8_t* const* descR, float mbf, float mb,
                                           float* const* uRight, float* const* depth, int* nmatches) {
-    if (!h || !left || !right || npairs < 0 || !NL || !keysL || !descL || !NR || !keysR || !descR || !uRight ||
-        !depth || !nmatches)
+    return ORBmatcher_ComputeStereoMatches_batch_at(h, left, 0, right, 0, npairs, NL, keysL, descL, NR, keysR, descR,
+                                                    mbf, mb, uRight, depth, nmatches);
+}
+
+int ORBmatcher_ComputeStereoMatches_batch_at(ORBmatcher_h h, ORBextractor_h left, int first_left,
+                                             ORBextractor_h right, int first_right, int npairs, const int* NL,
+                                             const orb_kp* const* keysL, const uint8_t* const* descL, const int* NR,
+                                             const orb_kp* const* keysR, const uint8_t* const* descR, float mbf,
+                                             float mb, float* const* uRight, float* const* depth, int* nmatches) {
+    if (!h || !left || !right || npairs < 0 || first_left < 0 || first_right < 0 || !NL || !keysL || !descL || !NR ||
+        !keysR || !descR || !uRight || !depth || !nmatches)
         return ORB_E_INVALID;
     if (npairs == 0) return ORB_OK;
     const orbgpu::Extractor* EL = left->ex;
     const orbgpu::Extractor* ER = right->ex;
-    if (!EL->pyramid_base() || !ER->pyramid_base() || npairs > EL->last_batch() || npairs > ER->last_batch())
-        return ORB_E_INVALID;   // image p of the last extract() of both extractors
+    if (!EL->pyramid_base() || !ER->pyramid_base() || first_left + npairs > EL->last_batch() ||
+        first_right + npairs > ER->last_batch())
+        return ORB_E_INVALID;   // images first + p of the last extract() of the extractors
     const auto& LL = EL->levels();
     const auto& LR = ER->levels();
     if (LL.size() != LR.size() || (int)LL.size() > orbgpu::kStereoMaxLevels) return ORB_E_INVALID;
@@ -54,7 +64,8 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
     const bool dev = m->device_pointers();
     hipStream_t s = m->stream();
     // the pyramids are produced on the extractors' streams
-    if (hipStreamSynchronize(EL->stream()) != hipSuccess || hipStreamSynchronize(ER->stream()) != hipSuccess)
+    if (hipStreamSynchronize(EL->stream()) != hipSuccess ||
+        (ER != EL && hipStreamSynchronize(ER->stream()) != hipSuccess))
         return ORB_E_HIP;
     orbgpu::StereoParams P;
     std::memset(&P, 0, sizeof(P));
@@ -88,8 +99,8 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
         orbgpu::StereoDev& S = probs[p];
         S.NL = NL[p];
         S.NR = NR[p];
-        S.pyrL = EL->pyramid_base() + (size_t)p * EL->pyramid_image_bytes();
-        S.pyrR = ER->pyramid_base() + (size_t)p * ER->pyramid_image_bytes();
+        S.pyrL = EL->pyramid_base() + (size_t)(first_left + p) * EL->pyramid_image_bytes();
+        S.pyrR = ER->pyramid_base() + (size_t)(first_right + p) * ER->pyramid_image_bytes();
         S.sad = (int*)m->arena_alloc(4 * (size_t)NL[p] + 4);
         S.rowStart = (int*)m->arena_alloc(4 * ((size_t)P.rows0 + 1));
         S.rowIdx = (int*)m->arena_alloc(4 * (size_t)NR[p] * band + 4);

@@ -276,6 +276,17 @@ int ORBmatcher_ComputeStereoMatches_batch(ORBmatcher_h h, ORBextractor_h left, O
                                           const orb_kp* const* keysR, const uint8_t* const* descR,
                                           float mbf, float mb, float* const* uRight,
                                           float* const* depth, int* nmatches);
+/* The same with pair p = (image first_left + p of `left`'s last batch, image first_right + p of
+ * `right`'s): both images of every pair may come from ONE extractor's batch call over
+ * [lefts..., rights...] (left == right, first_right = npairs), i.e. Frame(imLeft, imRight)'s two
+ * extractions (Frame.cc:78-81) as one batch launch set. */
+int ORBmatcher_ComputeStereoMatches_batch_at(ORBmatcher_h h, ORBextractor_h left, int first_left,
+                                             ORBextractor_h right, int first_right, int npairs,
+                                             const int* NL, const orb_kp* const* keysL,
+                                             const uint8_t* const* descL, const int* NR,
+                                             const orb_kp* const* keysR, const uint8_t* const* descR,
+                                             float mbf, float mb, float* const* uRight,
+                                             float* const* depth, int* nmatches);
 
 /* cv::Mat Frame::UnprojectStereo(const int& i)                   Frame.cc:666-680
  * x3D = mRwc * ((u-cx)*z*invfx, (v-cy)*z*invfy, z) + mOw for every keypoint with
