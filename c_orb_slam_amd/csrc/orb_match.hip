@@ -17,6 +17,8 @@
 #define ORBGPU_PROF_BLOCK 20   // prof builds: k_select_r sections of a mid-batch frame (full local map)
 #include "orb_match.hpp"
 
+#include <cstdlib>
+
 #include <cstring>
 
 #include "detmath.hpp"
@@ -392,6 +394,15 @@ __device__ int scan_local(const SearchDev& P, const LocalQuery& q, Blocked block
 // frame is read from HBM once per 1024 queries.
 constexpr int kStageMaxN = 1536;
 constexpr int kStageThreads = 1024;
+// ORBGPU_CAND_NT=256: the staged candidate search in 256-thread workgroups (each stages the
+// frame itself; 4x the workgroups over more CUs) instead of 1024 (A/B runs)
+static int stage_threads() {
+    static const int v = [] {
+        const char* e = std::getenv("ORBGPU_CAND_NT");
+        return e && std::atoi(e) == 256 ? 256 : kStageThreads;
+    }();
+    return v;
+}
 constexpr size_t kStageLds = sizeof(uint16_t) * (kGridCells + 2) + sizeof(uint16_t) * kStageMaxN +
                              sizeof(float2) * kStageMaxN + kStageMaxN + 32 * (size_t)kStageMaxN + 64;
 template <bool LAST, bool STAGE, int NT>
@@ -1024,7 +1035,16 @@ Matcher::~Matcher() {
 int Matcher::init_device() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
-    ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    // ORBGPU_MATCH_STREAM_PRIO=1: the tracking lane's stream at the device's highest priority
+    // (A/B runs of the pipelined bench; the reference has no counterpart)
+    const char* pe = std::getenv("ORBGPU_MATCH_STREAM_PRIO");
+    if (pe && pe[0] == '1') {
+        int lo = 0, hi = 0;
+        ORB_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        ORB_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
+    } else {
+        ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    }
     return 0;
 }
 
@@ -1113,7 +1133,10 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     mark(1);
     if (maxq > 0) {
         if (lastMode) {
-            if (maxN <= kStageMaxN)
+            if (maxN <= kStageMaxN && stage_threads() == 256)
+                hipLaunchKernelGGL((k_candidates<true, true, 256>), dim3((maxq + 255) / 256, np), dim3(256), kStageLds,
+                                   stream_, dp, th, (int)bMono, counters());
+            else if (maxN <= kStageMaxN)
                 hipLaunchKernelGGL((k_candidates<true, true, kStageThreads>), dim3((maxq + kStageThreads - 1) / kStageThreads, np),
                                    dim3(kStageThreads), kStageLds,
                                    stream_, dp, th, (int)bMono, counters());
@@ -1125,7 +1148,10 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
             hipLaunchKernelGGL((k_select_r<true, 512, kSelQLast>), dim3(np), dim3(512), select_lds_bytes(maxN), stream_, dp,
                                th, (int)bMono, nnratio, (int)checkOri_, maxN);
         } else {
-            if (maxN <= kStageMaxN)
+            if (maxN <= kStageMaxN && stage_threads() == 256)
+                hipLaunchKernelGGL((k_candidates<false, true, 256>), dim3((maxq + 255) / 256, np), dim3(256), kStageLds,
+                                   stream_, dp, th, 0, counters());
+            else if (maxN <= kStageMaxN)
                 hipLaunchKernelGGL((k_candidates<false, true, kStageThreads>), dim3((maxq + kStageThreads - 1) / kStageThreads, np),
                                    dim3(kStageThreads), kStageLds,
                                    stream_, dp, th, 0, counters());

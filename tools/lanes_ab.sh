@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of the bench pipeline: --pipeline-only lines for each variant (extra bench args, quoted),
+# A/B of the bench pipeline: --pipeline-only lines for each variant ("[ENV=val ...;]bench args"),
 # two runs each, interleaved.  usage: bash tools/lanes_ab.sh <tag> "<args A>" "<args B>" ...
 set -o pipefail
 TAG=${1:-lanes}
@@ -15,7 +15,10 @@ for rep in 1 2; do
   i=0
   for v in "$@"; do
     i=$((i+1))
-    timeout -k 10 300 python bench.py --pipeline-only --no-cpu-baseline --steps 80 $v > "$OUT/pipe_v${i}_$rep.json" 2> "$OUT/pipe_v${i}_$rep.err" \
+    # a variant is "[ENV=val ...;]bench args"
+    envs=""; args="$v"
+    case "$v" in *";"*) envs="${v%%;*}"; args="${v#*;}";; esac
+    timeout -k 10 300 env $envs python bench.py --pipeline-only --no-cpu-baseline --steps 80 $args > "$OUT/pipe_v${i}_$rep.json" 2> "$OUT/pipe_v${i}_$rep.err" \
       || { tail -20 "$OUT/pipe_v${i}_$rep.err"; exit 1; }
     python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(repr(sys.argv[2]), d['value'], d['ms_per_step'], d['phase_ms_per_step'], {k: {s: round(x, 3) for s, x in v.items()} for k, v in d['stage_ms_per_step_by_image'].items()})" "$OUT/pipe_v${i}_$rep.json" "$v"
   done

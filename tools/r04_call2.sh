@@ -21,4 +21,4 @@ for v in "1 0" "0 0" "1 1"; do
   ORBGPU_LDLT_ROW=$1 ORBGPU_STRUCT_HOST=$2 timeout -k 10 200 python tools/ba_timing.py 30 > "$OUT/ba_timing_row$1_host$2.txt" 2>&1 || { tail -20 "$OUT/ba_timing_row$1_host$2.txt"; exit 1; }
   echo "ldlt_row=$1 struct_host=$2"; tail -4 "$OUT/ba_timing_row$1_host$2.txt"
 done
-SKIP_TESTS=1 bash tools/lanes_ab.sh $TAG/lanes "--lanes 2" "--lanes 3" "--lanes 2 --reserve-cus 4" "--lanes 3 --reserve-cus 4"
+SKIP_TESTS=1 bash tools/lanes_ab.sh $TAG/lanes "--lanes 2" "--lanes 3" "--lanes 2 --reserve-cus 4"

@@ -1,0 +1,21 @@
+#!/bin/bash
+# round-4 call 3: global BA (device structure, config-5 8k x 10 / 16k golden fixtures), the stereo
+# API change, global-BA timing device vs host structure, pipeline A/B with --stereo-batch.
+set -o pipefail
+TAG=${1:-r04e}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$R" || exit 1
+export TMPDIR=/tmp
+timeout -k 10 240 python -u -m pytest tests/test_gpu_stereo.py tests/test_gpu_track_local_map.py tests/test_gpu_match.py -x -q --timeout 200 --timeout-method thread > "$OUT/pytest_match.txt" 2>&1 \
+  || { tail -40 "$OUT/pytest_match.txt"; exit 1; }
+tail -1 "$OUT/pytest_match.txt"
+for h in 0 1; do
+  ORBGPU_STRUCT_HOST=$h ORBGPU_BA_TIMES=1 timeout -k 10 200 python tools/gba_timing.py 2000:4 > "$OUT/gba_timing_host$h.txt" 2>&1 || { tail -20 "$OUT/gba_timing_host$h.txt"; exit 1; }
+  echo "struct_host=$h"; grep "nkf\|\[ba\] call" "$OUT/gba_timing_host$h.txt" | tail -3
+done
+SKIP_TESTS=1 bash tools/lanes_ab.sh $TAG/lanes "--lanes 2" "--lanes 2 --stereo-batch 1" "--lanes 3 --stereo-batch 1" "ORBGPU_MATCH_STREAM_PRIO=1;--lanes 2 --stereo-batch 1" "ORBGPU_CAND_NT=256;--lanes 2 --stereo-batch 1" || exit 1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_ba_sharded.py -x -v --timeout 900 --timeout-method thread > "$OUT/pytest_sharded.txt" 2>&1 \
+  || { tail -40 "$OUT/pytest_sharded.txt"; exit 1; }
+tail -3 "$OUT/pytest_sharded.txt"
