@@ -16,6 +16,7 @@ for h in 0 1; do
   echo "struct_host=$h"; grep "nkf\|\[ba\] call" "$OUT/gba_timing_host$h.txt" | tail -3
 done
 SKIP_TESTS=1 bash tools/lanes_ab.sh $TAG/lanes "--lanes 2" "--lanes 2 --stereo-batch 1" "--lanes 3 --stereo-batch 1" "ORBGPU_MATCH_STREAM_PRIO=1;--lanes 2 --stereo-batch 1" "ORBGPU_CAND_NT=256;--lanes 2 --stereo-batch 1" || exit 1
+bash tools/ldlt_levels.sh $TAG/levels 2000:4 > /dev/null 2>&1 && tail -3 "$OUT/levels/levels.txt"
 timeout -k 10 900 python -u -m pytest tests/test_gpu_ba_sharded.py -x -v --timeout 900 --timeout-method thread > "$OUT/pytest_sharded.txt" 2>&1 \
   || { tail -40 "$OUT/pytest_sharded.txt"; exit 1; }
 tail -3 "$OUT/pytest_sharded.txt"
