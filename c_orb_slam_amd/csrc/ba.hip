@@ -3277,7 +3277,7 @@ int BaEngine::gate_edges(int final_check, uint8_t* erase) {
     hipLaunchKernelGGL(k_gate, dim3(nblk(ne_, 256)), dim3(256), 0, stream_, ne_, dE_, dT_, dX_, dErr_, dFlag, dLevel_,
                        dRobust_, final_check ? 0 : 1);
     ORB_HIP_CHECK(hipGetLastError());
-    return d2h_sync(erase, dFlag, ne_);
+    return erase ? d2h_sync(erase, dFlag, ne_) : 0;
 }
 
 int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, Comm* comm, const BaMode* mode) {
@@ -3322,10 +3322,14 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
             if (int e = reduce_stop(stop)) return e;
         }
         if (!stopped(stop)) {
-            std::vector<uint8_t> flag(ne_);
-            if (int e = gate_edges(0, flag.data())) return e;
-            for (int i = 0; i < ne_; i++)
-                if (flag[i]) level_[i] = 1;
+            if (struct_host()) {   // the host builder reads the levels from the host mirror
+                std::vector<uint8_t> flag(ne_);
+                if (int e = gate_edges(0, flag.data())) return e;
+                for (int i = 0; i < ne_; i++)
+                    if (flag[i]) level_[i] = 1;
+            } else {               // k_gate moved the outliers to level 1 in dLevel_ itself
+                if (int e = gate_edges(0, nullptr)) return e;
+            }
             ts = clk::now();
             if (int e = build_structure(0)) return e;
             t_struct += std::chrono::duration<double, std::milli>(clk::now() - ts).count();
