@@ -211,8 +211,13 @@ __global__ void __launch_bounds__(64) k_ldlt_prow(SpDev S, int j0) {
     const int p = job.x, lane = threadIdx.x;
     const int pw = S.th[p];
     const double* D = S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT);
+    // L[i][k] = D[i][k] (i > k) into Ls[k][i]: row r of D read by the wave in one coalesced load
+    // (lane = column k) per row, instead of a 512-B-strided column gather per k
 #pragma unroll 4
-    for (int k = 0; k < LT; k++) Ls[k * LP + lane] = (k < pw && lane > k) ? D[lane * LT + k] : 0.0;
+    for (int r = 0; r < LT; r++) {
+        const double v = D[r * LT + lane];
+        Ls[lane * LP + r] = (lane < pw && r > lane) ? v : 0.0;
+    }
     dsh[lane] = lane < pw ? D[lane * LT + lane] : 1.0;
     __syncthreads();
     const int e = S.rowStart[p] + job.y;
