@@ -1262,7 +1262,7 @@ def bench_ransac(reps=5, cpu=True, cpu_budget_s=8.0):
     import ctypes as C
     sys.path.insert(0, str(ROOT / "tests"))
     from c_orb_slam_amd._lib import check, lib
-    from c_orb_slam_amd.ransac import PnPsolver, Rng, Sim3Solver, iterate_batch, sim3_iterate_batch
+    from c_orb_slam_amd.ransac import BatchCall, PnPsolver, Rng, Sim3Solver, iterate_batch, sim3_iterate_batch
     from pnp_cases import pnp_problem
     from sim3_cases import sim3_problem
     L = lib()
@@ -1271,17 +1271,23 @@ def bench_ransac(reps=5, cpu=True, cpu_budget_s=8.0):
     ms2 = (C.c_float * 2)()
     cnt2 = (C.c_longlong * 2)()
 
-    def run(make, batch_fn, timings_fn, bytes_per_pair, reset=None):
+    def run(kind, make, batch_fn, timings_fn, bytes_per_pair, reset=None):
         solvers = make()
         rngs = [Rng(1 + k) for k in range(len(solvers))]
         batch_fn(solvers, RANSAC_HYP, rngs)   # warm-up: allocations, upload
-        walls, solve, chk = [], [], []
-        for _ in range(reps):
+        call = BatchCall(kind, solvers, RANSAC_HYP, rngs)
+        walls, pywalls, solve, chk = [], [], [], []
+        for rep in range(2 * reps):
             if reset:
                 reset(solvers)
+            # even reps: the C-ABI call alone (the drop-in boundary: argument arrays kept by the
+            # caller, results in its buffers); odd reps: the Python wrapper around it
             t0 = time.perf_counter()
-            batch_fn(solvers, RANSAC_HYP, rngs)
-            walls.append(time.perf_counter() - t0)
+            if rep % 2 == 0:
+                call()
+            else:
+                batch_fn(solvers, RANSAC_HYP, rngs)
+            (walls if rep % 2 == 0 else pywalls).append(time.perf_counter() - t0)
             check(timings_fn(ms2, cnt2), "last_timings")
             solve.append(ms2[0])
             chk.append(ms2[1])
@@ -1289,11 +1295,14 @@ def bench_ransac(reps=5, cpu=True, cpu_budget_s=8.0):
         dev_ms = float(np.mean(solve)) + float(np.mean(chk))
         c_ms = float(np.mean(chk))
         ach = pairs * (bytes_per_pair + 1 / 8) / (c_ms * 1e-3) / 1e9
+        wall = float(np.median(walls))
         return {"hypotheses_per_call": hyp, "pairs_per_call": pairs,
                 "device_hyp_per_s": round(hyp / (dev_ms * 1e-3), 1),
-                "wall_hyp_per_s": round(hyp / float(np.mean(walls)), 1),
+                "wall_hyp_per_s": round(hyp / wall, 1),
+                "wall_over_device": round(dev_ms * 1e-3 / wall, 3),
                 "ms_solve": round(float(np.mean(solve)), 4), "ms_check": round(c_ms, 4),
-                "ms_call_wall": round(float(np.mean(walls)) * 1e3, 3),
+                "ms_call_wall": round(wall * 1e3, 3),
+                "ms_call_wall_python": round(float(np.median(pywalls)) * 1e3, 3),
                 "check_roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": round(ach / HBM_PEAK_GBS, 5),
                                    "alg_bytes_per_pair": bytes_per_pair + 1 / 8,
@@ -1315,7 +1324,7 @@ def bench_ransac(reps=5, cpu=True, cpu_budget_s=8.0):
                 s.SetRansacParameters(0.99, N, RANSAC_HYP, 4, 0.4, 5.991)
                 ss.append(s)
             return ss
-        out["pnp"][str(N)] = run(make, iterate_batch, L.PnPsolver_last_timings, PNP_BYTES_PER_PAIR)
+        out["pnp"][str(N)] = run("pnp", make, iterate_batch, L.PnPsolver_last_timings, PNP_BYTES_PER_PAIR)
     # Sim3Solver's loop runs while BOTH mnIterations < mRansacMaxIts and the call's budget hold
     # (Sim3Solver.cc:197), so mRansacMaxIts must reach 300: minInliers = 0.24 N gives
     # ceil(log(0.01) / log(1 - 0.24^3)) = 331 -> 300; 90% outliers keep every hypothesis below it
@@ -1334,7 +1343,7 @@ def bench_ransac(reps=5, cpu=True, cpu_budget_s=8.0):
     def reset3(ss):   # SetRansacParameters restarts mnIterations
         for s in ss:
             s.SetRansacParameters(0.99, min3, RANSAC_HYP)
-    out["sim3"][str(N3)] = run(make3, sim3_iterate_batch, L.Sim3Solver_last_timings, SIM3_BYTES_PER_PAIR, reset3)
+    out["sim3"][str(N3)] = run("sim3", make3, sim3_iterate_batch, L.Sim3Solver_last_timings, SIM3_BYTES_PER_PAIR, reset3)
     out["sim3"][str(N3)]["min_inliers"] = min3
     check(L.PnPsolver_enable_timing(0), "PnPsolver_enable_timing")
     check(L.Sim3Solver_enable_timing(0), "Sim3Solver_enable_timing")

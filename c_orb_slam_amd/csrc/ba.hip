@@ -2710,14 +2710,24 @@ int BaEngine::upload_problem(const ba_problem* P) {
     return 0;
 }
 
-// ORBGPU_STRUCT_HOST=1: the host restatement (ba_struct.cpp) builds the lists instead of the
-// device (A/B runs; both produce the same lists, tests/test_gpu_ba_struct.py)
-static bool struct_host() {
-    static const bool v = [] {
+// Who builds the structure lists: the device for large problems (a global BA's millions of
+// edges), the host restatement (ba_struct.cpp) below kStructGpuMinEdges, where the device
+// builder's ~20 small launches cost more than the host's counting sorts (local BA, config 4:
+// 1.00 vs 0.66 ms per call, gpurun_out r04d ba_timing).  ORBGPU_STRUCT_HOST=1 / 0 forces the
+// host / device builder (A/B runs; both produce the same lists, tests/test_gpu_ba_struct.py).
+constexpr int kStructGpuMinEdges = 100000;
+static std::atomic<int> g_struct_gpu_min{kStructGpuMinEdges};   // orbgpu_unit_set_struct_gpu_min_edges
+static bool struct_host(int ne) {
+    static const int v = [] {
         const char* e = std::getenv("ORBGPU_STRUCT_HOST");
-        return e && e[0] == '1';
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
-    return v;
+    return v < 0 ? ne < g_struct_gpu_min.load() : v == 1;
+}
+int debug_set_struct_gpu_min_edges(int v) {
+    if (v < 0) return -1;
+    g_struct_gpu_min.store(v);
+    return 0;
 }
 
 // initializeOptimization(level) + buildIndexMapping + BlockSolver::buildStructure
@@ -2734,7 +2744,7 @@ int BaEngine::build_structure(int level) {
     int nE = 0, nP = 0, nL = 0, nBlk = 0;
     std::vector<int64_t> offKeys;    // off-diagonal Schur blocks i1 * nP + i2, ascending (tiled path)
     std::vector<int32_t> blkIJ;      // blkI ++ blkJ (dense sharded path)
-    if (!struct_host()) {
+    if (!struct_host(ne_)) {
         // the lists built on the device from the edges already in HBM (ba_struct_gpu.hip)
         GpuStructInfo info{};
         const int r = gs_.build(level, nkf_, npt_, ne_, dE_, dLevel_, dKfFixed_, dKfId_, dPtId_, comm_, stream_, &st_,
@@ -2965,14 +2975,15 @@ static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 // k_scale_chunks + k_csum; orbgpu_unit_set_scale_small_max lowers it so tests drive the chunked
 // path (and the device LM's scale == 0 branch) at oracle-sized problems
 static std::atomic<int> g_scale_small_max{2048 * 64};
-// the row-owner dense LDL^T (k_ldlt_row) up to kLdltRowMax rows; ORBGPU_LDLT_ROW=0 keeps the
-// panel kernel (k_ldlt_reg) for A/B runs.  Both perform the oracle's operation sequence.
+// the row-owner dense LDL^T (k_ldlt_row) up to kLdltRowMax rows with ORBGPU_LDLT_ROW=1; the
+// panel kernel (k_ldlt_reg) by default -- measured 2.1x faster per local-BA call (4.34 vs
+// 9.07 ms, gpurun_out r04d ba_timing).  Both perform the oracle's operation sequence.
 static bool ldlt_row_ok(int n) {
-    static const bool off = [] {
+    static const bool on = [] {
         const char* e = std::getenv("ORBGPU_LDLT_ROW");
-        return e && e[0] == '0';
+        return e && e[0] == '1';
     }();
-    return n <= kLdltRowMax && !off;
+    return n <= kLdltRowMax && on;
 }
 static bool scale_small(int nP, int nL) { return 6 * nP + 3 * nL <= g_scale_small_max.load(); }
 int debug_set_scale_small_max(int v) {
@@ -3322,7 +3333,7 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
             if (int e = reduce_stop(stop)) return e;
         }
         if (!stopped(stop)) {
-            if (struct_host()) {   // the host builder reads the levels from the host mirror
+            if (struct_host(ne_)) {   // the host builder reads the levels from the host mirror
                 std::vector<uint8_t> flag(ne_);
                 if (int e = gate_edges(0, flag.data())) return e;
                 for (int i = 0; i < ne_; i++)

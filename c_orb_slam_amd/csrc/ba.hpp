@@ -178,6 +178,7 @@ int debug_wave_tree(const double* v64, double* out);
 int debug_shared_div(const double* a, const double* b, int n, double* out);
 int debug_set_csum_lds_max(int v);
 int debug_set_scale_small_max(int v);
+int debug_set_struct_gpu_min_edges(int v);
 int debug_prof(unsigned long long* out32);
 
 }  // namespace orbgpu

@@ -397,6 +397,9 @@ int orbgpu_unit_set_csum_lds_max(int m2_max) {
 int orbgpu_unit_set_scale_small_max(int terms) {
     return orbgpu::debug_set_scale_small_max(terms) ? ORB_E_INVALID : ORB_OK;
 }
+int orbgpu_unit_set_struct_gpu_min_edges(int edges) {
+    return orbgpu::debug_set_struct_gpu_min_edges(edges) ? ORB_E_INVALID : ORB_OK;
+}
 
 int orbgpu_unit_ba_struct(int nkf, int npt, int ne, const int32_t* edge_kf, const int32_t* edge_pt,
                           const uint8_t* edge_level, const uint8_t* kf_fixed, const int32_t* kf_id,

@@ -529,10 +529,13 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
     }
     const size_t out_base = dev;
     dev += host;
-    if (int e = ensure(dev + 256, host + 256, (size_t)n)) return e;
+    // the problem table is staged in the pinned block too (after the records): a pageable
+    // source would make its copy a synchronous staging round trip
+    const size_t probs_h = al256(host);
+    if (int e = ensure(dev + 256, probs_h + sizeof(PnPProbDev) * n + 256, (size_t)n)) return e;
     char* D = (char*)d_work_;
     char* Hh = (char*)h_work_;
-    std::vector<PnPProbDev> pd(n);
+    PnPProbDev* pd = (PnPProbDev*)(Hh + probs_h);
     std::vector<size_t> out_off(n, 0);
     size_t o = 0, ho = 0;
     int maxK = 0, nact = 0;
@@ -576,7 +579,7 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
         nact++;
     }
     if (nact == 0) return 0;
-    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(PnPProbDev) * nact, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd, sizeof(PnPProbDev) * nact, hipMemcpyHostToDevice, s));
     const PnPProbDev* dprobs = (const PnPProbDev*)d_probs_;
     hipLaunchKernelGGL(k_pnp_draws, dim3(nact), dim3(64), 0, s, dprobs);
     if (maxK > 0) {

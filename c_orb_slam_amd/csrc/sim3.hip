@@ -502,10 +502,13 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
         ORB_HIP_CHECK(hipMalloc(&d_work_, dev + 256));
         work_cap_ = dev + 256;
     }
-    if (host + 256 > hwork_cap_) {
+    // the problem table is staged in the pinned block too (after the records): a pageable
+    // source would make its copy a synchronous staging round trip
+    const size_t probs_h = al(host), hbytes = probs_h + sizeof(Sim3ProbDev) * n + 256;
+    if (hbytes > hwork_cap_) {
         if (h_work_) (void)hipHostFree(h_work_);
-        ORB_HIP_CHECK(hipHostMalloc(&h_work_, host + 256));
-        hwork_cap_ = host + 256;
+        ORB_HIP_CHECK(hipHostMalloc(&h_work_, hbytes));
+        hwork_cap_ = hbytes;
     }
     if (sizeof(Sim3ProbDev) * n > probs_cap_) {
         if (d_probs_) (void)hipFree(d_probs_);
@@ -514,7 +517,7 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
     }
     char* D = (char*)d_work_;
     char* Hh = (char*)h_work_;
-    std::vector<Sim3ProbDev> pd(n);
+    Sim3ProbDev* pd = (Sim3ProbDev*)(Hh + probs_h);
     std::vector<size_t> out_off(n, 0);
     size_t o = 0, ho = 0;
     int maxK = 0, nact = 0;
@@ -551,7 +554,7 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
         pts += (long long)K[k] * P.N_;
     }
     if (nact == 0) return 0;
-    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd.data(), sizeof(Sim3ProbDev) * nact, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd, sizeof(Sim3ProbDev) * nact, hipMemcpyHostToDevice, s));
     const Sim3ProbDev* dprobs = (const Sim3ProbDev*)d_probs_;
     hipLaunchKernelGGL(k_sim3_draws, dim3(nact), dim3(64), 0, s, dprobs);
     if (maxK > 0) {

@@ -156,3 +156,28 @@ def sim3_iterate_batch(solvers, nIterations, rngs):
           "Sim3Solver_iterate_batch")
     return [((T[k].reshape(4, 4) if has[k] else None), bool(nm[k]), bufs[k][:solvers[k].n_matches].astype(bool),
              int(nin[k])) for k in range(n)]
+
+
+class BatchCall:
+    """A batch entry (PnPsolver_iterate_batch / Sim3Solver_iterate_batch) with its argument
+    arrays built once, as a C++ caller keeps them between calls: call() is the C call alone and
+    leaves its results in has / no_more / n_inliers / T / inliers[k]."""
+
+    def __init__(self, kind, solvers, nIterations, rngs):
+        L = lib()
+        self._fn = L.PnPsolver_iterate_batch if kind == "pnp" else L.Sim3Solver_iterate_batch
+        self.n = n = len(solvers)
+        self.nIterations = nIterations
+        self._hs = (C.c_void_p * n)(*[s._h.value for s in solvers])
+        self._rp = (C.c_void_p * n)(*[C.cast(C.byref(r.s), C.c_void_p).value for r in rngs])
+        self.inliers = [np.zeros(max(s.n_matches, 1), np.uint8) for s in solvers]
+        self._ip = (C.c_void_p * n)(*[b.ctypes.data for b in self.inliers])
+        self.no_more, self.n_inliers, self.has = (np.zeros(n, np.int32) for _ in range(3))
+        self.T = np.zeros((n, 16), np.float32)
+        self._args = (n, self._hs, nIterations, self._rp, ptr(self.no_more), self._ip, ptr(self.n_inliers),
+                      ptr(self.T), ptr(self.has))
+        self._solvers = solvers   # the handles stay alive with the call
+        self._rngs = rngs
+
+    def __call__(self):
+        check(self._fn(*self._args), "iterate_batch")

@@ -864,6 +864,10 @@ int orbgpu_unit_set_csum_lds_max(int m2_max);
  * (default and maximum 2048 * 64) and as a chunked two-kernel sum above it; 0 sends every
  * problem down the chunked path.  Process-wide, host-side. */
 int orbgpu_unit_set_scale_small_max(int terms);
+/* Test knob: BA runs with at least `edges` edges build their structure lists on the device
+ * (ba_struct_gpu.hip), smaller ones on the host (default 100000; 0 sends every run to the
+ * device builder).  ORBGPU_STRUCT_HOST=1 / 0 in the environment overrides it.  Process-wide. */
+int orbgpu_unit_set_struct_gpu_min_edges(int edges);
 /* The elimination order of the block-sparse pose system (host only, no device): nested
  * dissection of a graph (adjStart[n + 1] / adj: symmetric, sorted lists) with leaves of at
  * most `leaf` nodes; perm[k] = node eliminated k-th; the separator tree's node count and

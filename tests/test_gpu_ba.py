@@ -101,3 +101,20 @@ def test_ba_chunked_scale_path_device_lm_matches_oracle(gpu, seed, kw):
     _check(g, o)
     assert np.array_equal(g["kf_Tcw"], o["kf_Tcw"].reshape(g["kf_Tcw"].shape))
     assert np.array_equal(g["pt_pos"], o["pt_pos"].reshape(g["pt_pos"].shape))
+
+
+@pytest.mark.parametrize("seed,kw", [(0, {}), (5, dict(n_local=12, n_fixed=6, n_pt=800, outlier_frac=0.3))])
+def test_ba_device_structure_matches_oracle(gpu, seed, kw):
+    """Local BA below the device builder's edge threshold builds its lists on the host; the knob
+    sends it through the device builder (ba_struct_gpu.hip) and k_gate's level moves in HBM
+    (no flag readback before optimize(10)): bit-identical to the oracle either way."""
+    from c_orb_slam_amd._lib import lib
+    pr = ba_problem(seed, **kw)
+    assert lib().orbgpu_unit_set_struct_gpu_min_edges(0) == 0
+    try:
+        g, o = _run_both(pr)
+    finally:
+        assert lib().orbgpu_unit_set_struct_gpu_min_edges(100000) == 0
+    _check(g, o)
+    assert np.array_equal(g["kf_Tcw"], o["kf_Tcw"].reshape(g["kf_Tcw"].shape))
+    assert np.array_equal(g["pt_pos"], o["pt_pos"].reshape(g["pt_pos"].shape))
