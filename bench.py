@@ -66,9 +66,11 @@ def parse():
     ap.add_argument("--lanes", type=int, default=2,
                     help="batches in flight (buffer sets): extraction of batch k waits for the tracking chain "
                          "of batch k - lanes, which last used its buffers")
-    ap.add_argument("--stereo-batch", type=int, default=0,
-                    help="1: Frame(imLeft, imRight)'s two extractions as ONE batch call of 2B images on one "
-                         "extractor stream (ComputeStereoMatches_batch_at pairs image b with image B + b)")
+    ap.add_argument("--stereo-batch", type=int, default=1,
+                    help="1 (default): Frame(imLeft, imRight)'s two extractions as ONE batch call of 2B images on "
+                         "one extractor stream (ComputeStereoMatches_batch_at pairs image b with image B + b; "
+                         "31.4-32.1k vs 30.2-30.4k frames/s with 0, profiles/r04b_lanes_ab.txt); 0: two "
+                         "extractors on two host threads and two streams")
     ap.add_argument("--pipeline-only", action="store_true",
                     help="only the timed stereo pipeline (+ its CPU baseline): one compact JSON line")
     ap.add_argument("--launch-timeout", type=float, default=3000.0,
@@ -819,7 +821,7 @@ def main():
         ep = {"avg_launch_ms": round(t, 4), "frames_per_launch": P,
               "keypoints_per_launch": int(np.mean([a for a, _ in pose_edges])),
               "inliers_per_launch": int(np.mean([b for _, b in pose_edges])),
-              "bound": "valu", "workload": "TrackWithMotionModel's PoseOptimization of the batch (one 256-thread "
+              "bound": "valu", "workload": "TrackWithMotionModel's PoseOptimization of the batch (one 512-thread "
                                            "workgroup per frame: 4 rounds of optimize(10))"}
         pk = next((k for k in pmc if k.startswith("k_pose_opt")), None)
         if pk and pmc[pk].get("valu_insts_per_launch"):
@@ -893,6 +895,11 @@ def main():
         check(L.ORBmatcher_set_deferred(m._h, 0), "ORBmatcher_set_deferred")
         return out
 
+    def stage_by_stream():
+        """Extraction stage ms per step by extractor stream (--stereo-batch: one stream, both images)."""
+        per = {side: {k: round(v / args.steps, 4) for k, v in d.items()} for side, d in stage_lr.items()}
+        return {"left+right (one 2B-image stream)": per["left"]} if args.stereo_batch else per
+
     if args.passes_only:   # one extracted, tracked batch; then only the isolated passes below
         args.warmup, args.steps = 1, 0
     for _ in range(args.warmup):
@@ -948,8 +955,7 @@ def main():
                     "ms_per_step": round(dt / args.steps * 1e3, 3), "tracked_frames_per_step": P,
                     "matches_per_s": round(tot_match / dt, 1),
                     "keypoints_per_image": round(tot_kp / (2 * B * args.steps * world), 1), "cpu_baseline": cpu,
-                    "stage_ms_per_step_by_image": {side: {k: round(v / args.steps, 4) for k, v in d.items()}
-                                                   for side, d in stage_lr.items()},
+                    "stage_ms_per_step_by_image": stage_by_stream(),
                     "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}}
             if cpu:
                 line["speedup_vs_cpu_all_core"] = round(fps / cpu["value"], 1)
@@ -1081,8 +1087,7 @@ def main():
             "local_map_matches_per_frame": round(float(sum(a for a, _ in local_acc)) / max(len(local_acc) * P, 1), 1),
             "local_map_visible_per_frame": round(float(sum(b for _, b in local_acc)) / max(len(local_acc) * P, 1), 1),
             "stage_ms_per_step": stage_ms,
-            "stage_ms_per_step_by_image": {side: {k: round(v / args.steps, 4) for k, v in d.items()}
-                                           for side, d in stage_lr.items()},
+            "stage_ms_per_step_by_image": stage_by_stream(),
             "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}, "roofline": roof,
             "matcher_roofline": mroof, "latency": latency, "cpu_baseline": cpu, "local_ba": ba,
             "global_ba": gba, "ransac": ransac, "nfeatures_2000": nf2000,

@@ -822,6 +822,99 @@ __global__ void __launch_bounds__(128) k_ldlt_row(int n, const double* __restric
     ldlt_backward_wave(n, Lall, dvec, y, x, scal);
 }
 
+// Column-owner LDL^T + solve for n <= kLdltColMax (16 free keyframes: a local BA), 4 waves.
+// Lane c owns columns c and c + 64 of [S | b] (b in column n); wave w owns rows i = 4 r + w,
+// so a thread holds A[i][c] for its wave's rows in registers.  Pivot k: the pivot row (final
+// after k updates) sits in LDS, published by its owner at the end of pivot k - 1 (double-
+// buffered); every thread forms l_ck = u_kc / d_k for its columns (two lane-parallel quotients,
+// one reciprocal), the wave reads back the l of its own rows, and subtracts l_ik u_kj from its
+// rows, k ascending per element: the oracle's ora_ldlt_solve sequence (column n runs the
+// forward substitution y_i -= l_ik y_k).  The owner of row k + 1 updates that row first and
+// publishes it, one barrier per pivot.  The pivot loop is rolled: its body (24 rows x 2
+// columns) stays in the instruction cache, unlike a fully unrolled 90-pivot chain.
+constexpr int kLdltColMax = 96;
+constexpr int kLdltColRows = kLdltColMax / 4;
+__global__ void __launch_bounds__(256) k_ldlt_col(int n, const double* __restrict__ Sg, const double* bs, double* x,
+                                                  double* scal, const int* run) {
+    BA_GATE(run);
+    __shared__ double Ur[2][128];                        // published row k: columns 0..n (b at n)
+    __shared__ double Lall[kLdltColMax * kLdltColMax];   // L[i][k] at Lall[k * n + i]
+    __shared__ double lw[4][kLdltColRows + 8];           // l_ik of wave w's rows (r = i / 4)
+    __shared__ double dvec[kLdltColMax], y[kLdltColMax];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int c0 = lane, c1 = lane + 64;
+    double A0[kLdltColRows], A1[kLdltColRows];
+#pragma unroll
+    for (int r = 0; r < kLdltColRows; r++) {
+        const int i = 4 * r + w;
+        const bool row = i < n;
+        A0[r] = (row && c0 < n && c0 >= i) ? Sg[(size_t)i * n + c0] : (row && c0 == n) ? bs[i] : 0.0;
+        A1[r] = (row && c1 < n && c1 >= i) ? Sg[(size_t)i * n + c1] : (row && c1 == n) ? bs[i] : 0.0;
+    }
+    if (w == 0) {
+        Ur[0][c0] = A0[0];
+        Ur[0][c1] = A1[0];
+    }
+    __syncthreads();
+    bool ok = true;
+    for (int k = 0; k < n; k++) {
+        const double* U = Ur[k & 1];
+        double* V = Ur[(k + 1) & 1];
+        const double d = U[k];
+        if (d == 0.0) {   // uniform: every thread reads the same pivot
+            ok = false;
+            break;
+        }
+        const double u0 = U[c0], u1 = U[c1];
+        const int own = (k + 1) & 3;   // the wave of row k + 1
+        const SharedDiv sd(d);
+        if (w == own) {
+            // row k + 1 first: its l from the broadcast u_{k,k+1} (the same quotient lane k + 1 forms)
+            const int r1 = (k + 1) >> 2;
+            const double l1 = sd.div(U[k + 1 < n ? k + 1 : k]);
+#pragma unroll
+            for (int r = 0; r < kLdltColRows; r++)
+                if (r == r1 && k + 1 < n) {
+                    A0[r] -= l1 * u0;
+                    A1[r] -= l1 * u1;
+                    V[c0] = A0[r];
+                    V[c1] = A1[r];
+                }
+        }
+        const double l0 = sd.div(u0), l1v = sd.div(u1);
+        if (w == 0) {
+            if (c0 > k && c0 < n) Lall[k * n + c0] = l0;
+            if (c1 > k && c1 < n) Lall[k * n + c1] = l1v;
+            if (lane == 0) {
+                dvec[k] = d;
+                y[k] = U[n];   // b_k after its k updates: the forward-substituted y_k
+            }
+        }
+        if ((lane & 3) == w) {   // the l of this wave's rows, c = 4 r + w
+            lw[w][lane >> 2] = l0;
+            lw[w][16 + (lane >> 2)] = l1v;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's own LDS writes are visible
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < kLdltColRows; r++) {
+            const int i = 4 * r + w;
+            if (i > k + 1 && i < n) {   // row k + 1 was done above
+                const double li = lw[w][r];
+                A0[r] -= li * u0;
+                A1[r] -= li * u1;
+            }
+        }
+        __syncthreads();
+    }
+    if (!ok) {
+        if (tid == 0) scal[3] = 0.0;
+        return;
+    }
+    if (w != 0) return;
+    ldlt_backward_wave(n, Lall, dvec, y, x, scal);
+}
+
 // Register-resident LDL^T + solve for n < 128 (<= 21 free keyframes), 1024 threads.
 // Thread (wave w < 16, lane) owns rows i = 16 r + w (r < 8) of columns j = lane, lane + 64.
 // Per 6-column panel: owners publish the panel rows to LDS (U), wave 0 factorises them
@@ -2975,15 +3068,24 @@ static inline int nblk(int n, int b) { return (n + b - 1) / b; }
 // k_scale_chunks + k_csum; orbgpu_unit_set_scale_small_max lowers it so tests drive the chunked
 // path (and the device LM's scale == 0 branch) at oracle-sized problems
 static std::atomic<int> g_scale_small_max{2048 * 64};
-// the row-owner dense LDL^T (k_ldlt_row) up to kLdltRowMax rows with ORBGPU_LDLT_ROW=1; the
-// panel kernel (k_ldlt_reg) by default -- measured 2.1x faster per local-BA call (4.34 vs
-// 9.07 ms, gpurun_out r04d ba_timing).  Both perform the oracle's operation sequence.
-static bool ldlt_row_ok(int n) {
-    static const bool on = [] {
-        const char* e = std::getenv("ORBGPU_LDLT_ROW");
-        return e && e[0] == '1';
+// The dense single-workgroup LDL^T of a pose system of n rows: the 1,024-thread panel kernel
+// (k_ldlt_reg) by default; ORBGPU_LDLT_DENSE=col / row picks the column-owner kernel (k_ldlt_col,
+// n <= 96) or the row-owner kernel (k_ldlt_row) for A/B runs.  Measured per local-BA call
+// (config 4, tools/ba_timing.py): panel 3.91-4.00 ms, column-owner 5.05 ms (136 us per solve
+// against 77), row-owner 8.63 ms (profiles/r04b_*, r04l_*).  All perform the oracle's operation
+// sequence.
+enum class DenseLdlt { Col, Reg, Row, Lds };
+static DenseLdlt dense_ldlt_kind(int n, bool use_reg) {
+    static const int pick = [] {
+        const char* e = std::getenv("ORBGPU_LDLT_DENSE");
+        if (!e) return 1;
+        if (!strcmp(e, "col")) return 0;
+        if (!strcmp(e, "row")) return 2;
+        return 1;
     }();
-    return n <= kLdltRowMax && on;
+    if (pick == 2 && n <= kLdltRowMax) return DenseLdlt::Row;
+    if (pick == 0 && n <= kLdltColMax) return DenseLdlt::Col;
+    return use_reg ? DenseLdlt::Reg : DenseLdlt::Lds;
 }
 static bool scale_small(int nP, int nL) { return 6 * nP + 3 * nL <= g_scale_small_max.load(); }
 int debug_set_scale_small_max(int v) {
@@ -3039,8 +3141,8 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const int in_lds = ldsBytes <= ldsMax_ ? 1 : 0;
     const size_t shm = in_lds ? ldsBytes : sizeof(double) * (size_t)n;
     const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
-    const bool use_row = ldlt_row_ok(n);
     const bool use_reg = n < kLdltMax && regShm <= ldsMax_;   // b rides in column n
+    const DenseLdlt kind = dense_ldlt_kind(n, use_reg);
     // n <= 128: register-resident single-workgroup LDL^T; S fits LDS: single-workgroup in LDS;
     // larger: block-sparse tiled LDL^T in HBM (ldlt.hip, structure from build_structure)
     if (!tiled_ && n > 0 && !use_reg && !in_lds) return -1;
@@ -3073,9 +3175,11 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         }
         if (tiled_) {
             if (int e = sp_.solve(dBs_, dX2_, dScal_, s)) return e;
-        } else if (use_row) {
+        } else if (kind == DenseLdlt::Col) {
+            hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
+        } else if (kind == DenseLdlt::Row) {
             hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
-        } else if (use_reg) {
+        } else if (kind == DenseLdlt::Reg) {
             hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else {
             hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, nullptr);
@@ -3211,8 +3315,10 @@ void BaEngine::enqueue_lm_step(bool first) {
                                dScal_, dEmat_, dCb_, ctl);
     if (S.nBlk) schur_launch(S.nBlk, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_, 0.0,
                                    1, dScal_, sa, dBs_, 1, ctl);
-    if (ldlt_row_ok(n)) hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
-    else if (use_reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    const DenseLdlt kind = dense_ldlt_kind(n, use_reg);
+    if (kind == DenseLdlt::Col) hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else if (kind == DenseLdlt::Row) hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else if (kind == DenseLdlt::Reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, ctl);
     if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_, dXbak_,
                                     dX2_, dHplA_, dHll_, dBl_, 0.0, 1, dScal_, ctl);
@@ -3408,7 +3514,10 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     ORB_HIP_CHECK(hipMemcpy(dS, S, sizeof(double) * n * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemcpy(dB, b, sizeof(double) * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemset(dX, 0, sizeof(double) * nn));
-    if (variant == 4) {
+    if (variant == 5) {
+        if (n > kLdltColMax) return -3;
+        hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, 0, n, dS, dB, dX, dScal, nullptr);
+    } else if (variant == 4) {
         if (n > kLdltRowMax) return -3;
         hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, 0, n, dS, dB, dX, dScal, nullptr);
     } else if (variant == 0) {

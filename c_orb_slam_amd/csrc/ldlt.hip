@@ -249,6 +249,124 @@ __global__ void __launch_bounds__(64) k_ldlt_prow(SpDev S, int j0) {
     if (lane == 0) S.lnz[sl] = any ? 1 : 0;
 }
 
+// The same two kernels with a rolled pivot loop.  Fully unrolled, k_ldlt_pdiag / k_ldlt_prow are
+// 69 / 59 KB of straight-line code that every launch runs once, so the wave waits on instruction
+// fetch; here a loop over 8-pivot chunks runs one 8-pivot body (~9 KB): register t of the chunk
+// is pivot 8c + t, the live column shifts down by 8 registers after each chunk, and groups of 8
+// registers past the live rows are skipped.  Per element the updates still arrive in ascending
+// pivot order (the same operations as the unrolled kernels and the oracle); padding pivots
+// (k >= pw), whose L is zero, are not applied (the oracle has no such rows).
+constexpr int kChunk = 8;
+
+__global__ void __launch_bounds__(64) k_ldlt_pdiag_r(SpDev S, int j0) {
+    __shared__ double Ls[LT * LP];
+    if (*(volatile int*)S.fail) return;
+    const int p = S.stepP[j0 + blockIdx.x];
+    const int lane = threadIdx.x;
+    const int pw = S.th[p];
+    const __amdgpu_buffer_rsrc_t Ud = tile_rsrc(S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT));
+    const int vo = lane * 8;
+    double col[LT];   // col[r] = tile row kb + r of column `lane` (kb: the chunk's first pivot)
+#pragma unroll
+    for (int r = 0; r < LT; r++) col[r] = tld(Ud, vo, r * LT * 8);
+    bool bad = false;
+    for (int c = 0; c < LT / kChunk; c++) {
+        const int kb = kChunk * c;
+        if (kb >= pw || bad) break;
+#pragma unroll
+        for (int t = 0; t < kChunk; t++) {
+            const int k = kb + t;
+            if (k < pw && !bad) {
+                const double d = rdlane(col[t], k);
+                if (d == 0.0) {
+                    bad = true;
+                } else {
+                    Ls[k * LP + lane] = lane > k ? col[t] / d : 0.0;
+                    __builtin_amdgcn_wave_barrier();
+                    // row k is final: U (lane >= k) and the L of the earlier pivots (lane < k)
+                    if (lane < pw) tst(Ud, lane >= k ? col[t] : Ls[lane * LP + k], vo, k * LT * 8);
+                    const double ck = col[t];
+#pragma unroll
+                    for (int q = 0; q < LT / kChunk; q++) {
+                        if (q < LT / kChunk - c) {   // registers 8q..8q+7 hold live rows
+#pragma unroll
+                            for (int r = kChunk * q; r < kChunk * q + kChunk; r++)
+                                if (r > t) col[r] -= Ls[k * LP + kb + r] * ck;
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < LT - kChunk; r++) col[r] = col[r + kChunk];
+    }
+    if (bad && lane == 0) *S.fail = 1;
+}
+
+__global__ void __launch_bounds__(64) k_ldlt_prow_r(SpDev S, int j0) {
+    __shared__ double Ls[LT * LP];   // [k][i] = L[i][k]
+    __shared__ double dsh[LT];
+    if (*(volatile int*)S.fail) return;
+    const int2 job = S.rowJobs[j0 + blockIdx.x];   // (panel, index in its row)
+    const int p = job.x, lane = threadIdx.x;
+    const int pw = S.th[p];
+    const double* D = S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT);
+    for (int r = 0; r < LT; r++) {
+        const double v = D[r * LT + lane];
+        Ls[lane * LP + r] = (lane < pw && r > lane) ? v : 0.0;
+    }
+    dsh[lane] = lane < pw ? D[lane * LT + lane] : 1.0;
+    __syncthreads();
+    const int e = S.rowStart[p] + job.y;
+    const int sl = S.rowSlot[e];
+    const __amdgpu_buffer_rsrc_t Ut = tile_rsrc(S.U + (size_t)sl * (LT * LT));
+    const __amdgpu_buffer_rsrc_t Lo = tile_rsrc(S.LT + (size_t)sl * (LT * LT));
+    const int vo = lane * 8;
+    double c[LT];   // c[r] = tile row kb + r of column `lane`
+#pragma unroll
+    for (int r = 0; r < LT; r++) c[r] = tld(Ut, vo, r * LT * 8);   // zero outside the system
+    bool nz = false;
+    for (int ch = 0; ch < LT / kChunk; ch++) {
+        const int kb = kChunk * ch;
+        if (kb >= pw) break;
+#pragma unroll
+        for (int t = 0; t < kChunk; t++) {
+            const int k = kb + t;
+            if (k < pw) {
+                const double ck = c[t];   // row k final: all its updates (pivots < k) are in
+                tst(Ut, ck, vo, k * LT * 8);
+                tst(Lo, ck / dsh[k], vo, k * LT * 8);
+                nz |= ck != 0.0;
+#pragma unroll
+                for (int q = 0; q < LT / kChunk; q++) {
+                    if (q < LT / kChunk - ch) {
+#pragma unroll
+                        for (int r = kChunk * q; r < kChunk * q + kChunk; r++)
+                            if (r > t) c[r] -= Ls[k * LP + kb + r] * ck;   // L[kb + r][k], wave-uniform address
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < LT - kChunk; r++) c[r] = c[r + kChunk];
+    }
+    for (int r = pw; r < LT; r++) tst(Lo, 0.0, vo, r * LT * 8);   // padding rows of L^T: zero
+    // flag = some eliminated U[k][j] != 0, a superset of "some l != 0": skipping on it is exact
+    const bool any = __any(nz);
+    if (lane == 0) S.lnz[sl] = any ? 1 : 0;
+}
+
+// ORBGPU_LDLT_ROLL=0 keeps the fully unrolled panel kernels (A/B)
+static bool rolled_panels() {
+    static const bool v = [] {
+        const char* e = getenv("ORBGPU_LDLT_ROLL");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // Trailing updates inside the nodes: A(I, J) -= L(I, p) U(p, J), one 256-thread workgroup per
 // target of the step (4 x 4 register micro-tiles, both operand tiles staged in LDS).
 __global__ void __launch_bounds__(256) k_ldlt_ptrail(SpDev S, int j0) {
@@ -887,8 +1005,10 @@ int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
         if (nt > 0) hipLaunchKernelGGL(k_ldlt_update, dim3(nt), dim3(256), 0, s, d, hLevTgtStart_[h]);
         for (int st = hLevStepStart_[h]; st < hLevStepStart_[h + 1]; st++) {
             const int4 a = hSteps_[st], z = hSteps_[st + 1];
-            if (z.x > a.x) hipLaunchKernelGGL(k_ldlt_pdiag, dim3(z.x - a.x), dim3(64), 0, s, d, a.x);
-            if (z.y > a.y) hipLaunchKernelGGL(k_ldlt_prow, dim3(z.y - a.y), dim3(64), 0, s, d, a.y);
+            if (z.x > a.x) hipLaunchKernelGGL(rolled_panels() ? k_ldlt_pdiag_r : k_ldlt_pdiag, dim3(z.x - a.x), dim3(64),
+                                              0, s, d, a.x);
+            if (z.y > a.y) hipLaunchKernelGGL(rolled_panels() ? k_ldlt_prow_r : k_ldlt_prow, dim3(z.y - a.y), dim3(64), 0,
+                                              s, d, a.y);
             if (z.z > a.z) hipLaunchKernelGGL(k_ldlt_ptrail, dim3(z.z - a.z), dim3(256), 0, s, d, a.z);
         }
         const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];

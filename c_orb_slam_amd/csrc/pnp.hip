@@ -214,18 +214,29 @@ __global__ void __launch_bounds__(64) k_pnp_replay(const PnPProbDev* __restrict_
     const PnPProbDev& P = probs[blockIdx.x];
     const int lane = threadIdx.x & 63, N = P.N, words = (N + 31) >> 5;
     PnPStateDev* st = P.state;
-    int nIt = P.nIt0;
     int nBest = st->nBest, refValid = st->refValid, refNin = st->refNin;
     int consumed = P.nhyp, success = 0;
-    for (int h = 0; h < P.nhyp; h++) {
-        nIt++;
-        const int c = P.counts[h];
-        if (c < P.minInliers) continue;
-        if (c > nBest) {   // mvbBestInliers = mvbInliersi; mnBestInliers; mBestTcw
-            const uint32_t* m = P.masks + (size_t)h * words;
+    // The reference's loop only acts at an "event": a hypothesis with at least minInliers inliers
+    // that beats the best (c > nBest) or meets an invalid Refine.  Between events the state is
+    // constant, so 64 counts at a time are tested lane-parallel and the first event of the chunk
+    // (ballot) is replayed; the walk resumes right after it.  Iterations = hypotheses consumed.
+    int h0 = 0;
+    while (h0 < P.nhyp && !success) {
+        const int h = h0 + lane;
+        const int c = h < P.nhyp ? P.counts[h] : -1;
+        const bool ev = h < P.nhyp && c >= P.minInliers && (c > nBest || !refValid);
+        const unsigned long long evb = __ballot(ev);
+        if (!evb) {
+            h0 += 64;
+            continue;
+        }
+        const int e = __ffsll((long long)evb) - 1;
+        const int he = h0 + e, ce = __shfl(c, e, 64);
+        if (ce > nBest) {   // mvbBestInliers = mvbInliersi; mnBestInliers; mBestTcw
+            const uint32_t* m = P.masks + (size_t)he * words;
             for (int w = lane; w < words; w += 64) P.bestMask[w] = m[w];
-            if (lane == 0) rt_to_tcw_d(P.rt + (size_t)h * 12, st->bestTcw);
-            nBest = c;
+            if (lane == 0) rt_to_tcw_d(P.rt + (size_t)he * 12, st->bestTcw);
+            nBest = ce;
             refValid = 0;
         }
         if (!refValid) {   // Refine(): EPnP on the best inliers in index order, then CheckInliers
@@ -255,10 +266,11 @@ __global__ void __launch_bounds__(64) k_pnp_replay(const PnPProbDev* __restrict_
         }
         if (refNin > P.minInliers) {   // Refine() succeeded: return the refined pose (228-235)
             success = 1;
-            consumed = h + 1;
-            break;
+            consumed = he + 1;
         }
+        h0 = he + 1;
     }
+    const int nIt = P.nIt0 + consumed;
     __syncthreads();
     PnPOutDev* o = P.out;
     const uint32_t* src = nullptr;

@@ -323,20 +323,36 @@ __global__ void __launch_bounds__(64) k_sim3_replay(const Sim3ProbDev* __restric
     const Sim3ProbDev& P = probs[blockIdx.x];
     const int lane = threadIdx.x & 63, words = (P.N + 31) >> 5;
     Sim3StateDev* st = P.state;
-    int nIt = P.nIt0, nBest = st->nBest, best = -1, consumed = P.nhyp, success = 0;
-    for (int h = 0; h < P.nhyp; h++) {
-        nIt++;
-        const int c = P.counts[h];
-        if (c >= nBest) {
-            best = h;
-            nBest = c;
-            if (c > P.minInliers) {
-                success = 1;
-                consumed = h + 1;
-                break;
-            }
+    int nBest = st->nBest, best = -1, consumed = P.nhyp, success = 0;
+    // 64 hypotheses per step: the best before hypothesis h is the running maximum of the counts
+    // (nBest takes c whenever c >= nBest), i.e. an exclusive prefix max over the chunk carried
+    // across chunks; the walk stops at the first update with more than minInliers (ballot), else
+    // the chunk's last update is the best so far.
+    for (int base = 0; base < P.nhyp && !success; base += 64) {
+        const int h = base + lane;
+        const int c = h < P.nhyp ? P.counts[h] : INT_MIN;
+        int inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(inc, o, 64);
+            if (lane >= o) inc = max(inc, t);
+        }
+        int exc = __shfl_up(inc, 1, 64);
+        if (lane == 0) exc = INT_MIN;
+        const bool upd = h < P.nhyp && c >= max(nBest, exc);
+        const unsigned long long ex = __ballot(upd && c > P.minInliers), up = __ballot(upd);
+        if (ex) {
+            const int e = __ffsll((long long)ex) - 1;
+            best = base + e;
+            nBest = __shfl(c, e, 64);
+            success = 1;
+            consumed = best + 1;
+        } else {
+            if (up) best = base + 63 - __clzll((long long)up);
+            nBest = max(nBest, __shfl(inc, 63, 64));
         }
     }
+    const int nIt = P.nIt0 + consumed;
     Sim3OutDev* o = P.out;
     if (lane == 0) {
         if (best >= 0) {

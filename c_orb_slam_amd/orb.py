@@ -328,8 +328,11 @@ class ORBmatcher:
                                                       ptr(dep), C.byref(n)), "ORBmatcher_ComputeStereoMatches")
         return uR[:len(kL)], dep[:len(kL)], n.value
 
-    def ComputeStereoMatches_batch(self, left, right, keysL, descL, keysR, descR, mbf, mb):
-        """Batched form over the images 0..P-1 of the last extract_batch of both extractors."""
+    def ComputeStereoMatches_batch(self, left, right, keysL, descL, keysR, descR, mbf, mb, first_left=0,
+                                   first_right=0):
+        """Batched form over the images 0..P-1 of the last extract_batch of both extractors; pair p
+        takes image first_left + p of `left` and first_right + p of `right` (one extractor's batch
+        over [lefts..., rights...]: left is right, first_right = P)."""
         P = len(keysL)
         kL = [np.ascontiguousarray(k, KP_DTYPE) for k in keysL]
         kR = [np.ascontiguousarray(k, KP_DTYPE) for k in keysR]
@@ -341,10 +344,11 @@ class ORBmatcher:
         NL = np.array([len(k) for k in kL], np.int32)
         NR = np.array([len(k) for k in kR], np.int32)
         n = np.zeros(P, np.int32)
-        check(self._L.ORBmatcher_ComputeStereoMatches_batch(self._h, left._h, right._h, P, ptr(NL), arr(kL), arr(dL),
-                                                            ptr(NR), arr(kR), arr(dR), float(mbf), float(mb),
-                                                            arr(uR), arr(dep), ptr(n)),
-              "ORBmatcher_ComputeStereoMatches_batch")
+        check(self._L.ORBmatcher_ComputeStereoMatches_batch_at(self._h, left._h, int(first_left), right._h,
+                                                               int(first_right), P, ptr(NL), arr(kL), arr(dL),
+                                                               ptr(NR), arr(kR), arr(dR), float(mbf), float(mb),
+                                                               arr(uR), arr(dep), ptr(n)),
+              "ORBmatcher_ComputeStereoMatches_batch_at")
         return [u[:len(k)] for u, k in zip(uR, kL)], [d[:len(k)] for d, k in zip(dep, kL)], n
 
     def _local_batch(self, frames, maps, dev, want_desc=True):

@@ -80,3 +80,29 @@ def test_stereo_batch_matches_single(gpu):
         assert n == ns[b]
         assert np.array_equal(uR.view(np.uint32), uRs[b].view(np.uint32))
         assert np.array_equal(dep.view(np.uint32), deps[b].view(np.uint32))
+
+
+def test_stereo_one_extractor_batch(gpu):
+    """Frame(imLeft, imRight)'s two extractions as ONE batch call over [lefts..., rights...] on one
+    extractor (the bench's --stereo-batch pipeline): ComputeStereoMatches_batch_at pairs image b
+    with image P + b, and every pair is bit-identical to the two-extractor batch."""
+    P = 3
+    Ls, Rs = synthetic.stereo_batch(11, P, 1241, 376)
+    one = gpu.ORBextractor(1200, 1.2, 8, 20, 7, max_width=1241, max_height=376, max_batch=2 * P)
+    kd = one.extract_batch(np.concatenate([Ls, Rs]))
+    exL = gpu.ORBextractor(1200, 1.2, 8, 20, 7, max_width=1241, max_height=376, max_batch=P)
+    exR = gpu.ORBextractor(1200, 1.2, 8, 20, 7, max_width=1241, max_height=376, max_batch=P)
+    kdL = exL.extract_batch(Ls)
+    kdR = exR.extract_batch(Rs)
+    for b in range(P):   # the extractions themselves are per-image bit-exact
+        assert np.array_equal(kd[b][0].view(np.uint8), kdL[b][0].view(np.uint8))
+        assert np.array_equal(kd[P + b][1], kdR[b][1])
+    m = gpu.ORBmatcher(0.6, True)
+    mb = np.float32(np.float32(KITTI_BF) / np.float32(KITTI_FX))
+    args = lambda kl, kr: ([k for k, _ in kl], [d for _, d in kl], [k for k, _ in kr], [d for _, d in kr], KITTI_BF, mb)
+    u1, d1, n1 = m.ComputeStereoMatches_batch(one, one, *args(kd[:P], kd[P:]), first_left=0, first_right=P)
+    u2, d2, n2 = m.ComputeStereoMatches_batch(exL, exR, *args(kdL, kdR))
+    assert np.array_equal(n1, n2) and n1.min() > 50
+    for b in range(P):
+        assert np.array_equal(u1[b].view(np.uint32), u2[b].view(np.uint32))
+        assert np.array_equal(d1[b].view(np.uint32), d2[b].view(np.uint32))
