@@ -1213,9 +1213,12 @@ def bench_global_ba(args, world, rank, dist, dev):
     import torch
     sys.path.insert(0, str(ROOT / "tests"))
     from ba_cases import global_ba_problem
-    from c_orb_slam_amd.optimizer import BundleAdjustmentSharded, Comm, partition_points, shard_problem
+    from c_orb_slam_amd.optimizer import BundleAdjustmentSharded, Comm, last_sharding, partition_points_nd, shard_problem
     pr = global_ba_problem(0, n_kf=args.gba_kf, pts_per_kf=150, laps=gba_laps(args))
-    shard = shard_problem(pr, partition_points(pr, world), rank)
+    # separator-tree partition: at N > 1 each rank factors its own subtrees of the pose system
+    # and only the separators' tiles and rows travel (Optimizer_partition_points_nd)
+    pt_rank, kf_owner = partition_points_nd(pr, world, with_kf_owner=True)
+    shard = shard_problem(pr, pt_rank, rank)
     uid = [Comm.unique_id() if rank == 0 else None]
     if dist is not None:
         dist.broadcast_object_list(uid, src=0)
@@ -1234,9 +1237,16 @@ def bench_global_ba(args, world, rank, dist, dev):
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    used, sh_tiles, sh_rows, pattern = last_sharding()
     comm.close()
     ne = len(pr["edge_pt"])
-    return {"metric": "global-BA iter/s", "value": round(its / dt, 2), "unit": "iter/s",
+    poses = int((kf_owner >= -1).sum())
+    sharding = {"factorisation": "sharded (own subtrees + replicated separators)" if used else "replicated",
+                "separator_poses": int((kf_owner == -1).sum()), "free_poses": poses,
+                "rank_poses": [int((kf_owner == q).sum()) for q in range(world)],
+                "exchange_doubles_per_trial": (sh_tiles * 4096 + sh_rows + 6 * poses) if used else (pattern * 4096 + 6 * poses),
+                "schur_pattern_tiles": pattern, "separator_tiles": sh_tiles}
+    return {"metric": "global-BA iter/s", "value": round(its / dt, 2), "unit": "iter/s", "sharding": sharding,
             "ms_per_call": round(dt / args.gba_reps * 1e3, 3), "edges_per_s": round(its * ne / dt, 1),
             "scaling": "strong", "calls": args.gba_reps,
             "config": {"workload": "kitti_merged_map_global_ba (SURVEY config 5): loop-closed map, "

@@ -187,6 +187,8 @@ def lib():
     L.Optimizer_LocalBundleAdjustment_sharded.argtypes = [vp, vp, vp, vp]
     L.Optimizer_BundleAdjustment_sharded.argtypes = [vp, vp, i32, i32, vp, vp]
     L.Optimizer_partition_points.argtypes = [vp, i32, vp]
+    L.Optimizer_partition_points_nd.argtypes = [vp, i32, vp, vp]
+    L.Optimizer_last_sharding.argtypes = [vp]
     L.orbgpu_comm_unique_id.argtypes = [vp]
     L.orbgpu_comm_init_rccl.argtypes = [i32, i32, vp, P(vp)]
     L.orbgpu_comm_init_local.argtypes = [i32, vp]

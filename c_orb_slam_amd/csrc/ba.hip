@@ -526,7 +526,7 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
                                               const double* __restrict__ Hpl, const double* __restrict__ cb,
                                               const double* Hpp, const double* bp, double lam_host, int use_dev,
                                               const double* scal, SysAddr S, double* bs, int own,
-                                              const int* run) {
+                                              const uint8_t* poseAdd, const int* run) {
     BA_GATE(run);
     __shared__ double cs[36][kChunks];
     const int blk = blockIdx.x;
@@ -584,6 +584,7 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
     const int q = threadIdx.x;
     const double v = local_csum_inplace(cs[q], m);
     const double lambda = lam_of(lam_host, use_dev, scal);
+    if (poseAdd) own = poseAdd[i1];   // sharded factorisation: the pose's owner adds its terms
     if (diag && q >= 21) {  // a shard that does not own the pose terms contributes -sum only
         bs[6 * i1 + (q - 21)] = (own ? bp[6 * i1 + (q - 21)] : 0.0) - v;
         return;
@@ -839,7 +840,7 @@ __global__ void __launch_bounds__(256) k_ldlt_col(int n, const double* __restric
     BA_GATE(run);
     __shared__ double Ur[2][128];                        // published row k: columns 0..n (b at n)
     __shared__ double Lall[kLdltColMax * kLdltColMax];   // L[i][k] at Lall[k * n + i]
-    __shared__ double lw[4][kLdltColRows + 8];           // l_ik of wave w's rows (r = i / 4)
+    __shared__ __attribute__((aligned(16))) double lw[4][kLdltColRows + 8];   // l_ik of wave w's rows (r = i / 4)
     __shared__ double dvec[kLdltColMax], y[kLdltColMax];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int c0 = lane, c1 = lane + 64;
@@ -867,11 +868,10 @@ __global__ void __launch_bounds__(256) k_ldlt_col(int n, const double* __restric
         }
         const double u0 = U[c0], u1 = U[c1];
         const int own = (k + 1) & 3;   // the wave of row k + 1
-        const SharedDiv sd(d);
         if (w == own) {
             // row k + 1 first: its l from the broadcast u_{k,k+1} (the same quotient lane k + 1 forms)
             const int r1 = (k + 1) >> 2;
-            const double l1 = sd.div(U[k + 1 < n ? k + 1 : k]);
+            const double l1 = U[k + 1 < n ? k + 1 : k] / d;
 #pragma unroll
             for (int r = 0; r < kLdltColRows; r++)
                 if (r == r1 && k + 1 < n) {
@@ -881,7 +881,9 @@ __global__ void __launch_bounds__(256) k_ldlt_col(int n, const double* __restric
                     V[c1] = A1[r];
                 }
         }
-        const double l0 = sd.div(u0), l1v = sd.div(u1);
+        // plain divisions: two cost 160 cycles, one reciprocal shared by two 324
+        // (tools/micro/ldlt_col.hip)
+        const double l0 = u0 / d, l1v = u1 / d;
         if (w == 0) {
             if (c0 > k && c0 < n) Lall[k * n + c0] = l0;
             if (c1 > k && c1 < n) Lall[k * n + c1] = l1v;
@@ -896,13 +898,115 @@ __global__ void __launch_bounds__(256) k_ldlt_col(int n, const double* __restric
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's own LDS writes are visible
         __builtin_amdgcn_wave_barrier();
+        // rows i = 4 r + w > k + 1 (row k + 1 was done above), four at a time: a group with a live
+        // row loads its four l together and updates branch-free (a branch per row serialised the
+        // LDS latency of every row: 2.1 k cycles per pivot, tools/micro/ldlt_col.hip)
+        const int rlive = (k + 5 - w) >> 2;   // first r with 4 r + w >= k + 2
 #pragma unroll
-        for (int r = 0; r < kLdltColRows; r++) {
-            const int i = 4 * r + w;
-            if (i > k + 1 && i < n) {   // row k + 1 was done above
-                const double li = lw[w][r];
-                A0[r] -= li * u0;
-                A1[r] -= li * u1;
+        for (int g = 0; g < kLdltColRows / 4; g++) {
+            if (4 * g + 3 >= rlive && 16 * g + w < n) {
+                const double2 la = *reinterpret_cast<const double2*>(&lw[w][4 * g]);
+                const double2 lb = *reinterpret_cast<const double2*>(&lw[w][4 * g + 2]);
+                const double lv[4] = {la.x, la.y, lb.x, lb.y};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int r = 4 * g + q, i = 4 * r + w;
+                    const bool live = i > k + 1 && i < n;
+                    const double v0 = A0[r] - lv[q] * u0, v1 = A1[r] - lv[q] * u1;
+                    A0[r] = live ? v0 : A0[r];
+                    A1[r] = live ? v1 : A1[r];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!ok) {
+        if (tid == 0) scal[3] = 0.0;
+        return;
+    }
+    if (w != 0) return;
+    ldlt_backward_wave(n, Lall, dvec, y, x, scal);
+}
+
+// Row-lane LDL^T + solve for n <= kLdltColMax, 4 waves: lane i owns rows i and i + 64 of
+// [S | b] (b in column n), wave w the columns j = 4 r + w (r <= 24).  Pivot k: the published row
+// k (final after k updates) sits in LDS, permuted so a wave's columns are contiguous; every lane
+// forms its rows' l_ik = u_ki / d_k itself (no l broadcast), reads u_kj of its wave's live
+// columns as broadcasts and subtracts l_ik u_kj, k ascending per element: the oracle's
+// ora_ldlt_solve sequence (column n runs the forward substitution).  Then lane k + 1 publishes
+// its row; one barrier per pivot.  Rows at or above the pivot and lower-triangle entries carry
+// values nobody reads, so the updates need no per-row predicate.
+constexpr int kLdltTCols = kLdltColMax / 4 + 1;   // 25 columns per wave: j <= 96 covers b at n <= 96
+__global__ void __launch_bounds__(256) k_ldlt_t(int n, const double* __restrict__ Sg, const double* bs, double* x,
+                                                double* scal, const int* run) {
+    BA_GATE(run);
+    __shared__ __attribute__((aligned(16))) double Up[2][4][kLdltTCols + 3];   // row k: Up[.][j & 3][j >> 2]
+    __shared__ double Lall[kLdltColMax * kLdltColMax];   // S staging, then L[i][k] at Lall[k * n + i]
+    __shared__ double dvec[kLdltColMax], y[kLdltColMax];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int i0 = lane, i1 = lane + 64;
+    // S through LDS: coalesced global reads, then each lane its rows
+    for (int q = tid; q < n * n; q += 256) Lall[q] = Sg[q];
+    __syncthreads();
+    double A0[kLdltTCols], A1[kLdltTCols];
+#pragma unroll
+    for (int r = 0; r < kLdltTCols; r++) {
+        const int j = 4 * r + w;
+        A0[r] = (i0 < n && j < n && j >= i0) ? Lall[i0 * n + j] : (i0 < n && j == n) ? bs[i0] : 0.0;
+        A1[r] = (i1 < n && j < n && j >= i1) ? Lall[i1 * n + j] : (i1 < n && j == n) ? bs[i1] : 0.0;
+    }
+    if (lane == 0) {   // row 0
+#pragma unroll
+        for (int r = 0; r < kLdltTCols; r++) Up[0][w][r] = A0[r];
+    }
+    __syncthreads();   // the staging area is free for L from here
+    bool ok = true;
+    for (int k = 0; k < n; k++) {
+        const double(*U)[kLdltTCols + 3] = Up[k & 1];
+        const double d = U[k & 3][k >> 2];
+        if (d == 0.0) {   // uniform
+            ok = false;
+            break;
+        }
+        // this lane's rows: l = u_ki / d_k (rows <= k compute values nobody reads)
+        const double l0 = k < 63 ? U[i0 & 3][i0 >> 2] / d : 0.0;
+        const double l1 = n > 64 ? U[i1 & 3][i1 >> 2] / d : 0.0;
+        if (w == 0) {
+            if (i0 > k && i0 < n) Lall[k * n + i0] = l0;
+            if (i1 > k && i1 < n) Lall[k * n + i1] = l1;
+            if (lane == 0) {
+                dvec[k] = d;
+                y[k] = U[n & 3][n >> 2];   // b_k after its k updates: the forward-substituted y_k
+            }
+        }
+        // live columns j > k of this wave, four at a time (a uniform skip of dead groups)
+        const int rlive = (k + 4 - w) >> 2;   // first r with 4 r + w >= k + 1
+#pragma unroll
+        for (int g = 0; g < (kLdltTCols + 3) / 4; g++) {
+            if (4 * g + 3 >= rlive && 16 * g + w <= n) {
+                const double2 ua = *reinterpret_cast<const double2*>(&U[w][4 * g]);
+                const double2 ub = *reinterpret_cast<const double2*>(&U[w][4 * g + 2]);
+                const double uv[4] = {ua.x, ua.y, ub.x, ub.y};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int r = 4 * g + q;
+                    if (r < kLdltTCols) {
+                        if (k < 63) A0[r] -= l0 * uv[q];
+                        if (n > 64) A1[r] -= l1 * uv[q];
+                    }
+                }
+            }
+        }
+        // row k + 1 is final: its lane publishes this wave's columns
+        const int kp = k + 1;
+        if (kp < n && (kp < 64 ? lane == kp : lane == kp - 64)) {
+            double* V = Up[kp & 1][w];
+            if (kp < 64) {   // two loops: a select of the arrays would move them to scratch
+#pragma unroll
+                for (int r = 0; r < kLdltTCols; r++) V[r] = A0[r];
+            } else {
+#pragma unroll
+                for (int r = 0; r < kLdltTCols; r++) V[r] = A1[r];
             }
         }
         __syncthreads();
@@ -933,7 +1037,7 @@ __device__ long long g_ldlt_probe[256];
     } while (0)
 #endif
 constexpr int kLdltMax = 128;
-constexpr int kTiledMinPoses = 24;   // 6 x 24 = 144 rows: the first n the LDS-resident dense solver cannot hold
+constexpr int kTiledMinPoses = kBaTiledMinPoses;   // 6 x 24 = 144 rows: the first n the LDS-resident dense solver cannot hold
 constexpr int kDenseMaxN = 144;   // >= every n the dense single-workgroup solvers take (n^2 doubles in LDS)
 constexpr int kLdltWaves = 16;
 constexpr int kLdltRows = kLdltMax / kLdltWaves;
@@ -2808,6 +2912,15 @@ int BaEngine::upload_problem(const ba_problem* P) {
 // builder's ~20 small launches cost more than the host's counting sorts (local BA, config 4:
 // 1.00 vs 0.66 ms per call, gpurun_out r04d ba_timing).  ORBGPU_STRUCT_HOST=1 / 0 forces the
 // host / device builder (A/B runs; both produce the same lists, tests/test_gpu_ba_struct.py).
+// ORBGPU_BA_DIST=0 keeps the replicated factorisation on every rank (A/B runs)
+static bool dist_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("ORBGPU_BA_DIST");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 constexpr int kStructGpuMinEdges = 100000;
 static std::atomic<int> g_struct_gpu_min{kStructGpuMinEdges};   // orbgpu_unit_set_struct_gpu_min_edges
 static bool struct_host(int ne) {
@@ -2835,6 +2948,7 @@ int BaEngine::build_structure(int level) {
         ts0 = t;
     };
     int nE = 0, nP = 0, nL = 0, nBlk = 0;
+    distOk_ = false;
     std::vector<int64_t> offKeys;    // off-diagonal Schur blocks i1 * nP + i2, ascending (tiled path)
     std::vector<int32_t> blkIJ;      // blkI ++ blkJ (dense sharded path)
     if (!struct_host(ne_)) {
@@ -2987,6 +3101,23 @@ int BaEngine::build_structure(int level) {
         lap("pack + pose graph");
         if (int e = sp_.build(6 * nP, 6, as, adj, true, stream_)) return e;
         lap("nested dissection + symbolic factorisation");
+        distOk_ = false;
+        if (comm_ && comm_->size() > 1 && dist_enabled() && sp_.plan(comm_->size(), comm_->rank(), stream_) == 0) {
+            // the sharded factorisation needs every rank's points inside its own subtrees and the
+            // separators (Optimizer_partition_points_nd); one misaligned rank keeps the replicated
+            // solve on all of them
+            int* dFlag = reinterpret_cast<int*>(dCounter_ + 8);
+            if (int e = sp_.align_flag(st_.ePose, nE, dFlag, stream_)) return e;
+            int f = 0;
+            if (d2h_sync(&f, dFlag, sizeof(int))) return -2;
+            hScal_[34] = f ? 1.0 : 0.0;
+            if (h2d_sync(dScratch_, hScal_ + 34, sizeof(double))) return -2;
+            if (int e = comm_->allreduce(dScratch_, 1, RedOp::Max, stream_)) return e;
+            if (d2h_sync(hScal_ + 34, dScratch_, sizeof(double))) return -2;
+            ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+            distOk_ = hScal_[34] == 0.0;
+            lap("sharded factorisation plan");
+        }
     } else if (comm_ && nP > 0) {
         // dense system: the 64x64 tiles the Schur blocks touch (union over the shards)
         const int n = 6 * nP, nt = (n + 63) / 64;
@@ -3074,16 +3205,18 @@ static std::atomic<int> g_scale_small_max{2048 * 64};
 // (config 4, tools/ba_timing.py): panel 3.91-4.00 ms, column-owner 5.05 ms (136 us per solve
 // against 77), row-owner 8.63 ms (profiles/r04b_*, r04l_*).  All perform the oracle's operation
 // sequence.
-enum class DenseLdlt { Col, Reg, Row, Lds };
+enum class DenseLdlt { Col, Reg, Row, Lds, T };
 static DenseLdlt dense_ldlt_kind(int n, bool use_reg) {
     static const int pick = [] {
         const char* e = std::getenv("ORBGPU_LDLT_DENSE");
         if (!e) return 1;
         if (!strcmp(e, "col")) return 0;
         if (!strcmp(e, "row")) return 2;
+        if (!strcmp(e, "t")) return 3;
         return 1;
     }();
     if (pick == 2 && n <= kLdltRowMax) return DenseLdlt::Row;
+    if (pick == 3 && n <= kLdltColMax) return DenseLdlt::T;
     if (pick == 0 && n <= kLdltColMax) return DenseLdlt::Col;
     return use_reg ? DenseLdlt::Reg : DenseLdlt::Lds;
 }
@@ -3159,8 +3292,12 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
             ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * (size_t)n * n, s));
         }
         if (S.nBlk) schur_launch(S.nBlk, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
-                                       lambda_, use_dev, dScal_, sa, dBs_, own ? 1 : 0, nullptr);
-        if (comm_ && tiled_) {   // all-reduce the Schur-pattern tiles of S and b_s
+                                       lambda_, use_dev, dScal_, sa, dBs_, own ? 1 : 0,
+                                       distOk_ ? sp_.pose_add() : (const uint8_t*)nullptr, (const int*)nullptr);
+        if (comm_ && tiled_ && distOk_) {
+            // sharded factorisation: each rank's partial S and b_s go straight into it (solve_dist
+            // exchanges the separator tiles and rows only)
+        } else if (comm_ && tiled_) {   // all-reduce the Schur-pattern tiles of S and b_s
             ORB_HIP_CHECK(hipGetLastError());
             const RedBuf rb[2] = {{sp_.tiles(), (size_t)sp_.nA() * 4096}, {dBs_, (size_t)n}};
             if (int e = comm_->allreduce(rb, 2, RedOp::Sum, s)) return e;
@@ -3173,10 +3310,14 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
             hipLaunchKernelGGL(k_tile_unpack, dim3(nTiles_), dim3(256), 0, s, n, dS_, dTiles_, dPackBuf_);
             ORB_HIP_CHECK(hipMemcpyAsync(dBs_, pb, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
         }
-        if (tiled_) {
+        if (tiled_ && distOk_) {
+            if (int e = sp_.solve_dist(dBs_, dX2_, dScal_, s, comm_)) return e;
+        } else if (tiled_) {
             if (int e = sp_.solve(dBs_, dX2_, dScal_, s)) return e;
         } else if (kind == DenseLdlt::Col) {
             hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
+        } else if (kind == DenseLdlt::T) {
+            hipLaunchKernelGGL(k_ldlt_t, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else if (kind == DenseLdlt::Row) {
             hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else if (kind == DenseLdlt::Reg) {
@@ -3314,9 +3455,10 @@ void BaEngine::enqueue_lm_step(bool first) {
     if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_, 0.0, 1,
                                dScal_, dEmat_, dCb_, ctl);
     if (S.nBlk) schur_launch(S.nBlk, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_, 0.0,
-                                   1, dScal_, sa, dBs_, 1, ctl);
+                                   1, dScal_, sa, dBs_, 1, (const uint8_t*)nullptr, ctl);
     const DenseLdlt kind = dense_ldlt_kind(n, use_reg);
     if (kind == DenseLdlt::Col) hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else if (kind == DenseLdlt::T) hipLaunchKernelGGL(k_ldlt_t, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else if (kind == DenseLdlt::Row) hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else if (kind == DenseLdlt::Reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, ctl);
@@ -3476,6 +3618,10 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
     for (int p = 0; p < npt_; p++)
         if (!mode_.global || ptHasEdge_[p])
             for (int k = 0; k < 3; k++) R->pt_pos[3 * p + k] = (float)X[3 * p + k];
+    last_dist[0] = distOk_ ? 1 : 0;
+    last_dist[1] = distOk_ ? sp_.dist_shared_tiles() : 0;
+    last_dist[2] = distOk_ ? sp_.dist_shared_rows() : 0;
+    last_dist[3] = tiled_ ? sp_.nA() : 0;
     last_ms[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     last_ms[1] = t_struct;
     static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;   // host-phase breakdown (tools/)
@@ -3514,9 +3660,10 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     ORB_HIP_CHECK(hipMemcpy(dS, S, sizeof(double) * n * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemcpy(dB, b, sizeof(double) * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemset(dX, 0, sizeof(double) * nn));
-    if (variant == 5) {
+    if (variant == 5 || variant == 6) {
         if (n > kLdltColMax) return -3;
-        hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, 0, n, dS, dB, dX, dScal, nullptr);
+        if (variant == 5) hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, 0, n, dS, dB, dX, dScal, nullptr);
+        else hipLaunchKernelGGL(k_ldlt_t, dim3(1), dim3(256), 0, 0, n, dS, dB, dX, dScal, nullptr);
     } else if (variant == 4) {
         if (n > kLdltRowMax) return -3;
         hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, 0, n, dS, dB, dX, dScal, nullptr);

@@ -17,6 +17,9 @@
 
 namespace orbgpu {
 
+// from this many free poses the reduced system is factored block-sparse (ldlt.hip)
+constexpr int kBaTiledMinPoses = 24;
+
 struct Se3 {  // g2o::SE3Quat: q = (x, y, z, w) like Eigen coeffs(), t
     double q[4];
     double t[3];
@@ -57,6 +60,8 @@ public:
             const BaMode* mode = nullptr);
     const BaTrace& trace() const { return trace_; }
     double last_ms[4] = {0, 0, 0, 0};  // total, structure (host), solves (device+control), io
+    // last run: sharded factorisation used, separator tiles and rows exchanged, Schur-pattern tiles
+    int last_dist[4] = {0, 0, 0, 0};
 
 private:
     int upload_problem(const ba_problem* P);
@@ -102,6 +107,7 @@ private:
     unsigned* dCounter_ = nullptr;
     SparseLdlt sp_;                // block-sparse pose system (n > the dense solvers' reach)
     bool tiled_ = false;
+    bool distOk_ = false;   // sharded factorisation planned and the ranks' points aligned to it
     void* arena_ = nullptr;
     size_t arenaCap_ = 0;
     double* hScal_ = nullptr;      // pinned

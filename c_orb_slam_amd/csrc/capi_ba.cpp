@@ -274,6 +274,77 @@ int Optimizer_partition_points(const ba_problem* P, int nranks, int32_t* pt_rank
     return ORB_OK;
 }
 
+int Optimizer_partition_points_nd(const ba_problem* P, int nranks, int32_t* pt_rank, int32_t* kf_owner) {
+    if (!P || nranks < 1 || P->n_kf < 0 || P->n_pt < 0 || P->n_edge < 0) return ORB_E_INVALID;
+    if (P->n_pt && !pt_rank) return ORB_E_INVALID;
+    if (P->n_edge && (!P->edge_pt || !P->edge_kf)) return ORB_E_INVALID;
+    if (P->n_kf && !P->kf_id) return ORB_E_INVALID;
+    if (P->n_pt && !P->pt_id) return ORB_E_INVALID;
+    const int nkf = P->n_kf, npt = P->n_pt, ne = P->n_edge;
+    for (int i = 0; i < ne; i++)
+        if (P->edge_pt[i] < 0 || P->edge_pt[i] >= npt || P->edge_kf[i] < 0 || P->edge_kf[i] >= nkf)
+            return ORB_E_INVALID;
+    // BundleAdjustment's structure at level 0 (every keyframe a vertex, fixed iff mnId == 0):
+    // the pose numbering and Schur blocks every rank's engine derives from the union of shards
+    std::vector<int32_t> eKf(P->edge_kf, P->edge_kf + ne), ePt(P->edge_pt, P->edge_pt + ne);
+    std::vector<int32_t> kfId(P->kf_id, P->kf_id + nkf), ptId(P->pt_id, P->pt_id + npt);
+    std::vector<uint8_t> kfFixed(nkf), level(ne, 0), kfAct, ptAct;
+    for (int k = 0; k < nkf; k++) kfFixed[k] = P->kf_id[k] == 0 ? 1 : 0;
+    orbgpu::BaHostStruct H;
+    orbgpu::ba_active_set(0, nkf, npt, ne, eKf.data(), ePt.data(), level.data(), &H.aE, &kfAct, &ptAct);
+    if (orbgpu::ba_build_lists(nkf, npt, eKf.data(), ePt.data(), kfFixed.data(), kfId.data(), ptId.data(), kfAct, ptAct,
+                               &H))
+        return ORB_E_INVALID;
+    const int nP = (int)H.poseKf.size();
+    if (kf_owner)
+        for (int k = 0; k < nkf; k++) kf_owner[k] = -2;   // not a free pose of the structure
+    if (nranks == 1 || nP < orbgpu::kBaTiledMinPoses) {   // no block-sparse factorisation to shard
+        return Optimizer_partition_points(P, nranks, pt_rank);
+    }
+    // the pose graph of the Schur blocks, as BaEngine::build_structure forms it
+    std::vector<int64_t> keys;
+    for (size_t b = 0; b < H.blkI.size(); b++)
+        if (H.blkI[b] != H.blkJ[b]) keys.push_back((int64_t)H.blkI[b] * nP + H.blkJ[b]);
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    std::vector<int> deg(nP + 1, 0), as(nP + 1, 0), adj(2 * keys.size());
+    for (int64_t q : keys) {
+        deg[q / nP]++;
+        deg[q % nP]++;
+    }
+    for (int i = 0; i < nP; i++) as[i + 1] = as[i] + deg[i];
+    std::vector<int> fillp(as.begin(), as.end() - 1);
+    for (int64_t q : keys) adj[fillp[q / nP]++] = (int)(q % nP);
+    for (int64_t q : keys) adj[fillp[q % nP]++] = (int)(q / nP);
+    for (int i = 0; i < nP; i++) std::sort(adj.begin() + as[i], adj.begin() + as[i + 1]);
+    orbgpu::NdTree tree;
+    orbgpu::nd_order(nP, as, adj, orbgpu::kNdLeafPoses, &tree);
+    std::vector<int> owner;
+    orbgpu::nd_assign(tree, nranks, &owner);
+    std::vector<int> poseOwner(nP, -1);
+    for (size_t k = 0; k < tree.start.size(); k++)
+        for (int q = tree.start[k]; q < tree.end[k]; q++) poseOwner[tree.perm[q]] = owner[k];
+    if (kf_owner)
+        for (int q = 0; q < nP; q++) kf_owner[H.poseKf[q]] = poseOwner[q];
+    // a point goes to the rank of the first subtree pose it observes (all of its poses are in
+    // that subtree or the separators above it); a point of separator poses only, round robin
+    std::vector<int32_t> landOf(npt, -1);
+    for (size_t l = 0; l < H.landPt.size(); l++) landOf[H.landPt[l]] = (int32_t)l;
+    int rr = 0;
+    for (int p = 0; p < npt; p++) {
+        int r = -1;
+        const int l = landOf[p];
+        if (l >= 0)
+            for (int q = H.lpStart[l]; q < H.lpStart[l + 1] && r < 0; q++) {
+                const int pose = H.ePose[H.lpList[q]];
+                if (pose >= 0) r = poseOwner[pose];
+            }
+        if (r < 0) r = rr++ % nranks;
+        pt_rank[p] = r;
+    }
+    return ORB_OK;
+}
+
 int orbgpu_comm_unique_id(uint8_t* id) {
     if (!id) return ORB_E_INVALID;
     return orbgpu::rccl_unique_id(id);
@@ -323,6 +394,15 @@ int Optimizer_last_trace(double* solve_ini_chi2, double* solve_chi2, int solve_c
         if (trial_chi2) trial_chi2[i] = t.trial_chi2[i];
         if (trial_lambda) trial_lambda[i] = t.trial_lambda[i];
     }
+    return ORB_OK;
+}
+
+int Optimizer_last_sharding(int* info4) {
+    if (!info4) return ORB_E_INVALID;
+    int rc = 0;
+    orbgpu::BaEngine* e = engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    for (int i = 0; i < 4; i++) info4[i] = e->last_dist[i];
     return ORB_OK;
 }
 

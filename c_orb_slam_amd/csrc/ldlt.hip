@@ -40,13 +40,14 @@
 #include "ldlt.hpp"
 #include "orb_common.hpp"
 #include "ordering.hpp"
+#include "comm.hpp"
 
 namespace orbgpu {
 
 constexpr int LT = kTile;        // tile edge
 constexpr int LP = LT + 1;       // LDS row pitch (doubles) of the diagonal L
 constexpr int kMaxRow = 2048;    // tiles per panel row
-constexpr int kNdLeaf = 32;      // nested-dissection leaf size (poses)
+constexpr int kNdLeaf = kNdLeafPoses;   // nested-dissection leaf size (poses)
 
 struct SpDev {
     int n, nt;
@@ -74,7 +75,17 @@ struct SpDev {
     double* y;            // tile space
     double* xs;           // tile space
     int* fail;
+    // sharded schedule (SparseLdlt::solve_dist); the plain solve leaves tcls null
+    const uint8_t* tcls;  // tile class: 0 another rank's subtree, 1 shared separator, 2 this rank's subtree
+    int want;             // launches touch the targets / panels / nodes of this class only (-1: all)
+    int kmode;            // 0: every pivot tile K; 1 / 2: only K of that class (updates, forward sweep)
+    double* dst;          // k_ldlt_update delta mode: the target tiles live in the exchange buffer
+    const int* packIdx;   // slot -> tile index in dst (delta mode)
 };
+
+// the sharded schedule's filters (block-uniform)
+__device__ __forceinline__ bool skip_tile(const SpDev& S, int t) { return S.want >= 0 && S.tcls[t] != S.want; }
+__device__ __forceinline__ bool skip_k(const SpDev& S, int K) { return S.kmode && S.tcls[K] != S.kmode; }
 
 // Tile access through a buffer descriptor (wave-uniform tile base in SGPRs, 32-bit per-lane
 // offset, constant row offsets folded into the instruction): the unrolled 64-row loops then
@@ -112,9 +123,10 @@ __global__ void __launch_bounds__(256) k_ldlt_update(SpDev S, int t0) {
     const int4 tg = S.tgts[t0 + blockIdx.x];
     const int kp0 = tg.w, kp1 = S.tgts[t0 + blockIdx.x + 1].w;
     const int I = tg.y, J = tg.z;
+    if (skip_tile(S, I)) return;
     const int ih = S.th[I], jw = S.th[J];
     const int gt = threadIdx.x, ty = gt >> 4, tx = gt & 15;
-    double* T = S.U + (size_t)tg.x * (LT * LT);
+    double* T = S.dst ? S.dst + (size_t)S.packIdx[tg.x] * (LT * LT) : S.U + (size_t)tg.x * (LT * LT);
     double acc[4][4];
 #pragma unroll
     for (int a = 0; a < 4; a++)
@@ -125,7 +137,7 @@ __global__ void __launch_bounds__(256) k_ldlt_update(SpDev S, int t0) {
         }
     for (int q = kp0; q < kp1; q++) {
         const int4 kp = S.kps[q];
-        if (!S.lnz[kp.x] || !S.lnz[kp.y]) continue;   // block-uniform
+        if (!S.lnz[kp.x] || !S.lnz[kp.y] || skip_k(S, kp.z)) continue;   // block-uniform
         const double2* srcL = (const double2*)(S.LT + (size_t)kp.x * (LT * LT));
         const double2* srcU = (const double2*)(S.U + (size_t)kp.y * (LT * LT));
         __syncthreads();
@@ -168,6 +180,7 @@ __global__ void __launch_bounds__(64) k_ldlt_pdiag(SpDev S, int j0) {
     __shared__ double Ls[LT * LP];
     if (*(volatile int*)S.fail) return;
     const int p = S.stepP[j0 + blockIdx.x];
+    if (skip_tile(S, p)) return;
     const int lane = threadIdx.x;
     const int pw = S.th[p];
     const __amdgpu_buffer_rsrc_t Ud = tile_rsrc(S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT));
@@ -209,6 +222,7 @@ __global__ void __launch_bounds__(64) k_ldlt_prow(SpDev S, int j0) {
     if (*(volatile int*)S.fail) return;
     const int2 job = S.rowJobs[j0 + blockIdx.x];   // (panel, index in its row)
     const int p = job.x, lane = threadIdx.x;
+    if (skip_tile(S, p)) return;
     const int pw = S.th[p];
     const double* D = S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT);
     // L[i][k] = D[i][k] (i > k) into Ls[k][i]: row r of D read by the wave in one coalesced load
@@ -262,6 +276,7 @@ __global__ void __launch_bounds__(64) k_ldlt_pdiag_r(SpDev S, int j0) {
     __shared__ double Ls[LT * LP];
     if (*(volatile int*)S.fail) return;
     const int p = S.stepP[j0 + blockIdx.x];
+    if (skip_tile(S, p)) return;
     const int lane = threadIdx.x;
     const int pw = S.th[p];
     const __amdgpu_buffer_rsrc_t Ud = tile_rsrc(S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT));
@@ -310,6 +325,7 @@ __global__ void __launch_bounds__(64) k_ldlt_prow_r(SpDev S, int j0) {
     if (*(volatile int*)S.fail) return;
     const int2 job = S.rowJobs[j0 + blockIdx.x];   // (panel, index in its row)
     const int p = job.x, lane = threadIdx.x;
+    if (skip_tile(S, p)) return;
     const int pw = S.th[p];
     const double* D = S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT);
     for (int r = 0; r < LT; r++) {
@@ -358,6 +374,196 @@ __global__ void __launch_bounds__(64) k_ldlt_prow_r(SpDev S, int j0) {
     if (lane == 0) S.lnz[sl] = any ? 1 : 0;
 }
 
+// U tiles of the panel rows with four waves per tile: wave w takes columns 16w..16w+15, a
+// quad of lanes per column, lane s of the quad rows 4q + s (q < 16).  Pivot k's row value
+// reaches the quad by one DPP broadcast from lane k mod 4, every lane applies it to its own
+// rows below k with the L it reads from LDS (four distinct addresses per instruction), so a
+// wave issues a quarter of the one-wave kernel's FP64 work and the four waves run on the
+// CU's four SIMDs without any barrier.  The lane's rows shift down by one register after every
+// four pivots (pivot 4m + t is register 0 of quad lane t).  Same per-element sequence.
+__device__ __forceinline__ double quad_bcast(double v, int t) {
+    const unsigned long long u = __double_as_longlong(v);
+    int lo = (int)(u & 0xffffffffu), hi = (int)(u >> 32);
+    const int ctl = t | (t << 2) | (t << 4) | (t << 6);   // quad_perm(t, t, t, t)
+    switch (t) {   // the DPP control is an immediate
+    case 0:
+        lo = __builtin_amdgcn_mov_dpp(lo, 0x00, 0xf, 0xf, false);
+        hi = __builtin_amdgcn_mov_dpp(hi, 0x00, 0xf, 0xf, false);
+        break;
+    case 1:
+        lo = __builtin_amdgcn_mov_dpp(lo, 0x55, 0xf, 0xf, false);
+        hi = __builtin_amdgcn_mov_dpp(hi, 0x55, 0xf, 0xf, false);
+        break;
+    case 2:
+        lo = __builtin_amdgcn_mov_dpp(lo, 0xaa, 0xf, 0xf, false);
+        hi = __builtin_amdgcn_mov_dpp(hi, 0xaa, 0xf, 0xf, false);
+        break;
+    default:
+        lo = __builtin_amdgcn_mov_dpp(lo, 0xff, 0xf, 0xf, false);
+        hi = __builtin_amdgcn_mov_dpp(hi, 0xff, 0xf, 0xf, false);
+        break;
+    }
+    (void)ctl;
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+__global__ void __launch_bounds__(256) k_ldlt_prow4(SpDev S, int j0) {
+    __shared__ double Ls[LT * LP + 4 * LT];   // [k][i] = L[i][k]; the pad keeps dead-row reads in bounds
+    __shared__ double dsh[LT];
+    __shared__ int anyNz;
+    if (*(volatile int*)S.fail) return;
+    const int2 job = S.rowJobs[j0 + blockIdx.x];   // (panel, index in its row)
+    const int p = job.x, tid = threadIdx.x;
+    if (skip_tile(S, p)) return;
+    const int pw = S.th[p];
+    const double* D = S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT);
+    {   // L of the panel from its factored diagonal tile: 16 coalesced row loads in flight per thread
+        const int col = tid & 63, r0 = tid >> 6;
+        double v[LT / 4];
+#pragma unroll
+        for (int u = 0; u < LT / 4; u++) v[u] = D[(r0 + 4 * u) * LT + col];
+#pragma unroll
+        for (int u = 0; u < LT / 4; u++) {
+            const int r = r0 + 4 * u;
+            Ls[col * LP + r] = (col < pw && r > col) ? v[u] : 0.0;
+        }
+        if (tid < LT) dsh[tid] = tid < pw ? D[tid * LT + tid] : 1.0;
+        if (tid == 0) anyNz = 0;
+    }
+    __syncthreads();
+    const int e = S.rowStart[p] + job.y;
+    const int sl = S.rowSlot[e];
+    const __amdgpu_buffer_rsrc_t Ut = tile_rsrc(S.U + (size_t)sl * (LT * LT));
+    const __amdgpu_buffer_rsrc_t Lo = tile_rsrc(S.LT + (size_t)sl * (LT * LT));
+    const int w = tid >> 6, lane = tid & 63, s = lane & 3, j = 16 * w + (lane >> 2);
+    const int vo = j * 8;
+    double c[LT / 4];   // c[q] = tile row 4 (m + q) + s of column j (m: the pivot group)
+#pragma unroll
+    for (int q = 0; q < LT / 4; q++) c[q] = tld(Ut, vo, (4 * q + s) * LT * 8);
+    bool nz = false;
+    for (int m = 0; m < LT / 4; m++) {
+        if (4 * m >= pw) break;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int k = 4 * m + t;
+            if (k < pw) {
+                const double ck = quad_bcast(c[0], t);   // row k of column j: final
+                if (s == t) {
+                    tst(Ut, ck, vo, k * LT * 8);
+                    tst(Lo, ck / dsh[k], vo, k * LT * 8);
+                    nz |= ck != 0.0;
+                }
+                const double* Lk = Ls + k * LP + 4 * m + s;   // Lk[4 q] = L[4 (m + q) + s][k]
+                {
+                    const double v = c[0] - Lk[0] * ck;
+                    c[0] = s > t ? v : c[0];
+                }
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    if (4 * g <= LT / 4 - 1 - m) {   // registers 4g..4g+3 hold some live row
+#pragma unroll
+                        for (int q = 4 * g; q < 4 * g + 4; q++)
+                            if (q > 0) c[q] -= Lk[4 * q] * ck;
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < LT / 4 - 1; q++) c[q] = c[q + 1];
+        c[LT / 4 - 1] = 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < LT / 4; q++) {   // padding rows of L^T: zero
+        const int r = 4 * q + s;
+        if (r >= pw) tst(Lo, 0.0, vo, r * LT * 8);
+    }
+    // flag = some eliminated U[k][j] != 0, a superset of "some l != 0": skipping on it is exact
+    if (__any(nz) && lane == 0) atomicOr(&anyNz, 1);
+    __syncthreads();
+    if (tid == 0) S.lnz[sl] = anyNz ? 1 : 0;
+}
+
+// The diagonal tile with the same four-wave quad layout.  Pivot k: the quad of column k
+// publishes d_k; after a barrier every column's quad forms its l = u_kj / d_k (the column index
+// as a row index), stores row k of the tile (U right of the diagonal, the earlier pivots' L left
+// of it) and publishes l; after a second barrier every lane applies pivot k to its rows below k.
+// Per element the oracle's sequence; lower-triangle registers carry values nobody reads.
+__global__ void __launch_bounds__(256) k_ldlt_pdiag4(SpDev S, int j0) {
+    __shared__ double Ls[LT * LP + 4 * LT];   // [k][i] = L[i][k]; the pad keeps dead-row reads in bounds
+    __shared__ double dk[2];
+    if (*(volatile int*)S.fail) return;
+    const int p = S.stepP[j0 + blockIdx.x];
+    if (skip_tile(S, p)) return;
+    const int tid = threadIdx.x;
+    const int pw = S.th[p];
+    const __amdgpu_buffer_rsrc_t Ud = tile_rsrc(S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT));
+    const int w = tid >> 6, lane = tid & 63, s = lane & 3, j = 16 * w + (lane >> 2);
+    const int vo = j * 8;
+    double c[LT / 4];   // c[q] = tile row 4 (m + q) + s of column j
+#pragma unroll
+    for (int q = 0; q < LT / 4; q++) c[q] = tld(Ud, vo, (4 * q + s) * LT * 8);
+    bool bad = false;
+    for (int m = 0; m < LT / 4 && !bad; m++) {
+        if (4 * m >= pw) break;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int k = 4 * m + t;
+            if (k < pw && !bad) {
+                const double ck = quad_bcast(c[0], t);   // row k of column j: final
+                if (j == k && s == t) dk[k & 1] = ck;
+                __syncthreads();
+                const double d = dk[k & 1];
+                if (d == 0.0) {   // uniform
+                    bad = true;
+                } else {
+                    if (s == t) {
+                        if (j < pw) tst(Ud, j >= k ? ck : Ls[j * LP + k], vo, k * LT * 8);
+                        Ls[k * LP + j] = j > k ? ck / d : 0.0;   // L[j][k]
+                    }
+                    __syncthreads();
+                    const double* Lk = Ls + k * LP + 4 * m + s;   // Lk[4 q] = L[4 (m + q) + s][k]
+                    {
+                        const double v = c[0] - Lk[0] * ck;
+                        c[0] = s > t ? v : c[0];
+                    }
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        if (4 * g <= LT / 4 - 1 - m) {
+#pragma unroll
+                            for (int q = 4 * g; q < 4 * g + 4; q++)
+                                if (q > 0) c[q] -= Lk[4 * q] * ck;
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < LT / 4 - 1; q++) c[q] = c[q + 1];
+        c[LT / 4 - 1] = 0.0;
+    }
+    if (bad && tid == 0) *S.fail = 1;
+}
+
+// ORBGPU_LDLT_PROW=1 keeps the one-wave panel-row kernel (A/B)
+static bool prow_quads() {
+    static const bool v = [] {
+        const char* e = getenv("ORBGPU_LDLT_PROW");
+        return !(e && e[0] == '1');
+    }();
+    return v;
+}
+
+// ORBGPU_LDLT_PDIAG4=1 takes the four-wave diagonal kernel
+static bool pdiag_quads() {
+    static const bool v = [] {
+        const char* e = getenv("ORBGPU_LDLT_PDIAG4");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 // ORBGPU_LDLT_ROLL=0 keeps the fully unrolled panel kernels (A/B)
 static bool rolled_panels() {
     static const bool v = [] {
@@ -375,6 +581,7 @@ __global__ void __launch_bounds__(256) k_ldlt_ptrail(SpDev S, int j0) {
     if (*(volatile int*)S.fail) return;
     const int2 job = S.pairJobs[j0 + blockIdx.x];   // (panel, pair index)
     const int p = job.x;
+    if (skip_tile(S, p)) return;
     const int rs = S.rowStart[p];
     const int4 pr = S.pairs[S.pairStart[p] + job.y];
     const int slI = S.rowSlot[rs + pr.x], slJ = S.rowSlot[rs + pr.y];
@@ -425,6 +632,7 @@ __global__ void __launch_bounds__(64) k_ldlt_pfwd(SpDev S, int n0, const double*
     if (*(volatile int*)S.fail) return;
     const int node = S.levNodes[n0 + blockIdx.x];
     const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    if (T1 > T0 && skip_tile(S, T0)) return;
     const int lane = threadIdx.x;
     double Lr[LT];
     for (int I = T0; I < T1; I++) {
@@ -433,7 +641,7 @@ __global__ void __launch_bounds__(64) k_ldlt_pfwd(SpDev S, int n0, const double*
         double acc = on ? b[S.rowMap[I0 + lane]] : 0.0;
         for (int e = S.colStart[I]; e < S.colStart[I + 1]; e++) {
             const int sl = S.colSlot[e];
-            if (!S.lnz[sl]) continue;
+            if (!S.lnz[sl] || skip_k(S, S.colK[e])) continue;
             const int K = S.colK[e], K0 = K * LT, kh = S.th[K];
             const double yk = S.y[K0 + lane];
             const double* Lo = S.LT + (size_t)sl * (LT * LT);   // [k][i] = L[I0 + i][K0 + k]
@@ -472,6 +680,7 @@ __global__ void __launch_bounds__(64) k_ldlt_backward(SpDev S, int n0, double* _
     if (failed) return;
     const int node = S.levNodes[n0 + blockIdx.x];
     const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    if (T1 > T0 && skip_tile(S, T0)) return;
     double Lr[LT];
     for (int I = T1 - 1; I >= T0; I--) {
         const int I0 = I * LT, ih = S.th[I];
@@ -544,6 +753,7 @@ __global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_fwdn(SpDev S, int n0,
     if (*(volatile int*)S.fail) return;
     const int node = S.levNodes[n0 + blockIdx.x];
     const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    if (T1 > T0 && skip_tile(S, T0)) return;
     const int W = blockDim.x >> 6, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int I = T0 + w; I < T1; I += W) {
         const int I0 = I * LT;
@@ -553,7 +763,7 @@ __global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_fwdn(SpDev S, int n0,
             const int K = S.colK[e];
             if (K >= T0) break;   // ascending K: the descendants come first
             const int sl = S.colSlot[e];
-            if (!S.lnz[sl]) continue;
+            if (!S.lnz[sl] || skip_k(S, K)) continue;
             acc = sweep_chain_fwd(acc, S.LT + (size_t)sl * (LT * LT), lane, S.y[K * LT + lane], S.th[K]);
         }
         accs[(I - T0) * LT + lane] = acc;
@@ -606,6 +816,7 @@ __global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_bwdn(SpDev S, int n0,
     if (failed) return;
     const int node = S.levNodes[n0 + blockIdx.x];
     const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    if (T1 > T0 && skip_tile(S, T0)) return;
     const int W = blockDim.x >> 6, w = threadIdx.x >> 6;
     for (int I = T0 + w; I < T1; I += W) {
         const int I0 = I * LT;
@@ -684,6 +895,7 @@ static inline size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 SparseLdlt::~SparseLdlt() {
     if (mem_) (void)hipFree(mem_);
+    if (distMem_) (void)hipFree(distMem_);
 }
 
 int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std::vector<int>& adj, bool nd,
@@ -709,6 +921,8 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
         tree.height = {0};
     }
     const int nnode = (int)tree.start.size();
+    nd_ = nd;
+    dist_ = false;
     hProw_.assign(ng, 0);
     std::vector<int> nodeT(2 * nnode), th;
     int nt = 0;
@@ -725,6 +939,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
         nt += tiles;
     }
     nt_ = nt;
+    hNodeT_ = nodeT;
     std::vector<int> tileNode(nt);
     for (int k = 0; k < nnode; k++)
         for (int t = nodeT[2 * k]; t < nodeT[2 * k + 1]; t++) tileNode[t] = k;
@@ -836,6 +1051,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     }
     hLevNodeStart_[nLev_] = (int)levNodes.size();
     hLevTgtStart_[nLev_] = (int)tgts.size();
+    tree_ = tree;
     hLevMaxT_.assign(nLev_, 0);
     for (int h = 0; h < nLev_; h++)
         for (int q = hLevNodeStart_[h]; q < hLevNodeStart_[h + 1]; q++)
@@ -970,8 +1186,7 @@ int SparseLdlt::zero(hipStream_t s) {
     return 0;
 }
 
-int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
-    if (n_ <= 0) return 0;
+SpDev SparseLdlt::dev() const {
     SpDev d;
     d.n = n_;
     d.nt = nt_;
@@ -999,36 +1214,243 @@ int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
     d.y = y_;
     d.xs = xs_;
     d.fail = fail_;
+    d.tcls = nullptr;
+    d.want = -1;
+    d.kmode = 0;
+    d.dst = nullptr;
+    d.packIdx = nullptr;
+    return d;
+}
+
+void SparseLdlt::enqueue_factor_level(const SpDev& d, int h, const double* b, hipStream_t s) {
+    const int nt = hLevTgtStart_[h + 1] - hLevTgtStart_[h];
+    if (nt > 0) hipLaunchKernelGGL(k_ldlt_update, dim3(nt), dim3(256), 0, s, d, hLevTgtStart_[h]);
+    for (int st = hLevStepStart_[h]; st < hLevStepStart_[h + 1]; st++) {
+        const int4 a = hSteps_[st], z = hSteps_[st + 1];
+        if (z.x > a.x) {
+            // the four-wave diagonal kernel measured no faster than the rolled one-wave kernel
+            // (38 vs 36-38 us per launch, profiles/r04l3_gba_ldlt_levels.txt): opt-in
+            if (pdiag_quads())
+                hipLaunchKernelGGL(k_ldlt_pdiag4, dim3(z.x - a.x), dim3(256), 0, s, d, a.x);
+            else
+                hipLaunchKernelGGL(rolled_panels() ? k_ldlt_pdiag_r : k_ldlt_pdiag, dim3(z.x - a.x), dim3(64), 0, s, d,
+                                   a.x);
+        }
+        if (z.y > a.y) {
+            if (prow_quads())
+                hipLaunchKernelGGL(k_ldlt_prow4, dim3(z.y - a.y), dim3(256), 0, s, d, a.y);
+            else
+                hipLaunchKernelGGL(rolled_panels() ? k_ldlt_prow_r : k_ldlt_prow, dim3(z.y - a.y), dim3(64), 0, s, d,
+                                   a.y);
+        }
+        if (z.z > a.z) hipLaunchKernelGGL(k_ldlt_ptrail, dim3(z.z - a.z), dim3(256), 0, s, d, a.z);
+    }
+    const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
+    const int mt = hLevMaxT_[h];
+    if (sweep_nodes() && mt > 1 && mt <= kSweepMaxTiles)
+        hipLaunchKernelGGL(k_ldlt_fwdn, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)), sizeof(double) * LT * mt, s, d,
+                           hLevNodeStart_[h], b);
+    else
+        hipLaunchKernelGGL(k_ldlt_pfwd, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], b);
+}
+
+void SparseLdlt::enqueue_backward_level(const SpDev& d, int h, double* x, double* scal, int first, hipStream_t s) {
+    const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
+    const int mt = hLevMaxT_[h];
+    if (sweep_nodes() && mt > 1 && mt <= kSweepMaxTiles)
+        hipLaunchKernelGGL(k_ldlt_bwdn, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)), sizeof(double) * LT * mt, s, d,
+                           hLevNodeStart_[h], x, scal, first);
+    else
+        hipLaunchKernelGGL(k_ldlt_backward, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], x, scal, first);
+}
+
+int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
+    if (n_ <= 0) return 0;
+    const SpDev d = dev();
     ORB_HIP_CHECK(hipMemsetAsync(fail_, 0, sizeof(int), s));
+    for (int h = 0; h < nLev_; h++) enqueue_factor_level(d, h, b, s);
+    for (int h = nLev_ - 1; h >= 0; h--) enqueue_backward_level(d, h, x, scal, h == nLev_ - 1 ? 1 : 0, s);
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// ---- sharded factorisation (plan / solve_dist) -----------------------------------------------
+
+// shared tiles into / out of the exchange buffer (a workgroup per tile)
+__global__ void __launch_bounds__(256) k_slot_pack(const double* __restrict__ U, const int* slots, double* buf) {
+    const double2* src = (const double2*)(U + (size_t)slots[blockIdx.x] * (LT * LT));
+    double2* dst = (double2*)(buf + (size_t)blockIdx.x * (LT * LT));
+    for (int q = threadIdx.x; q < LT * LT / 2; q += 256) dst[q] = src[q];
+}
+__global__ void __launch_bounds__(256) k_slot_unpack(double* __restrict__ U, const int* slots, const double* buf) {
+    const double2* src = (const double2*)(buf + (size_t)blockIdx.x * (LT * LT));
+    double2* dst = (double2*)(U + (size_t)slots[blockIdx.x] * (LT * LT));
+    for (int q = threadIdx.x; q < LT * LT / 2; q += 256) dst[q] = src[q];
+}
+
+// The separator rows' forward-sweep input from this rank: b_I minus the contributions of this
+// rank's subtree tiles K (their y final), a wave per separator tile row I.
+__global__ void __launch_bounds__(64) k_ldlt_fwd_part(SpDev S, const double* __restrict__ b, const int* shT,
+                                                      double* dst) {
+    const int I = shT[blockIdx.x], I0 = I * LT, lane = threadIdx.x;
+    double acc = lane < S.th[I] ? b[S.rowMap[I0 + lane]] : 0.0;
+    if (!*(volatile int*)S.fail) {
+        for (int e = S.colStart[I]; e < S.colStart[I + 1]; e++) {
+            const int K = S.colK[e], sl = S.colSlot[e];
+            if (S.tcls[K] != 2 || !S.lnz[sl]) continue;
+            acc = sweep_chain_fwd(acc, S.LT + (size_t)sl * (LT * LT), lane, S.y[K * LT + lane], S.th[K]);
+        }
+    }
+    dst[(size_t)blockIdx.x * LT + lane] = acc;
+}
+// reduced separator rows back into b (system order)
+__global__ void __launch_bounds__(64) k_b_unpack(SpDev S, const int* shT, const double* src, double* b) {
+    const int I = shT[blockIdx.x], lane = threadIdx.x;
+    if (lane < S.th[I]) b[S.rowMap[I * LT + lane]] = src[(size_t)blockIdx.x * LT + lane];
+}
+// the separator rows of x are counted once in the final all-reduce (rank 0's)
+__global__ void __launch_bounds__(64) k_x_zero_rows(SpDev S, const int* shT, double* x) {
+    const int I = shT[blockIdx.x], lane = threadIdx.x;
+    if (lane < S.th[I]) x[S.rowMap[I * LT + lane]] = 0.0;
+}
+__global__ void k_fail_pub(const int* fail, double* slot) { *slot = *(volatile const int*)fail ? 1.0 : 0.0; }
+__global__ void k_scal_pub(const double* slot, double* scal) { scal[3] = *slot == 0.0 ? 1.0 : 0.0; }
+__global__ void __launch_bounds__(256) k_align(const int* __restrict__ ePose, int nE, const int* __restrict__ prow,
+                                               const uint8_t* __restrict__ tcls, int* flag) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nE) return;
+    const int p = ePose[e];
+    if (p >= 0 && tcls[prow[p] / LT] == 0) atomicOr(flag, 1);
+}
+
+int SparseLdlt::plan(int R, int rank, hipStream_t s) {
+    dist_ = false;
+    rank_ = rank;
+    if (R <= 1 || n_ <= 0 || !nd_) return -1;
+    std::vector<int> owner;
+    nd_assign(tree_, R, &owner);
+    const int nnode = (int)tree_.start.size();
+    std::vector<uint8_t> tcls(nt_, 0);
+    levOwn_.assign(nLev_, 0);
+    levSh_.assign(nLev_, 0);
+    for (int k = 0; k < nnode; k++) {
+        const uint8_t c = owner[k] < 0 ? 1 : owner[k] == rank ? 2 : 0;
+        for (int t = hNodeT_[2 * k]; t < hNodeT_[2 * k + 1]; t++) tcls[t] = c;
+        if (c == 2) levOwn_[tree_.height[k]] = 1;
+        if (c == 1) levSh_[tree_.height[k]] = 1;
+    }
+    std::vector<int> shSlots, shT, packIdx(nslot_, -1);
+    for (int I = 0; I < nt_; I++) {
+        if (tcls[I] != 1) continue;
+        shT.push_back(I);
+        for (int J = I; J < nt_; J++) {   // an ancestor of a separator is a separator
+            const int sl = hSlotOf_[(size_t)I * nt_ + J];
+            if (sl < 0) continue;
+            packIdx[sl] = (int)shSlots.size();
+            shSlots.push_back(sl);
+        }
+    }
+    const int ng = (int)hProw_.size();
+    std::vector<uint8_t> poseAdd(ng, 0);
+    for (int q = 0; q < ng; q++) {
+        const uint8_t c = tcls[hProw_[q] / LT];
+        poseAdd[q] = (c == 2 || (c == 1 && rank == 0)) ? 1 : 0;
+    }
+    nShSlots_ = (int)shSlots.size();
+    nShT_ = (int)shT.size();
+    size_t off = 0;
+    auto take = [&](size_t b) {
+        const size_t o = off;
+        off += al256(b);
+        return o;
+    };
+    const size_t oT = take(nt_), oP = take(sizeof(int) * nslot_), oS = take(sizeof(int) * (nShSlots_ + 1)),
+                 oH = take(sizeof(int) * (nShT_ + 1)), oA = take(ng),
+                 oX = take(sizeof(double) * ((size_t)nShSlots_ * LT * LT + (size_t)nShT_ * LT + 8));
+    if (off > distCap_) {
+        if (distMem_) (void)hipFree(distMem_);
+        distMem_ = nullptr;
+        distCap_ = 0;
+        ORB_HIP_CHECK(hipMalloc(&distMem_, off));
+        distCap_ = off;
+    }
+    char* base = (char*)distMem_;
+    dTcls_ = (uint8_t*)(base + oT);
+    dPackIdx_ = (int*)(base + oP);
+    dShSlots_ = (int*)(base + oS);
+    dShT_ = (int*)(base + oH);
+    dPoseAdd_ = (uint8_t*)(base + oA);
+    dXbuf_ = (double*)(base + oX);
+    ORB_HIP_CHECK(hipMemcpyAsync(dTcls_, tcls.data(), nt_, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(dPackIdx_, packIdx.data(), sizeof(int) * nslot_, hipMemcpyHostToDevice, s));
+    if (nShSlots_)
+        ORB_HIP_CHECK(hipMemcpyAsync(dShSlots_, shSlots.data(), sizeof(int) * nShSlots_, hipMemcpyHostToDevice, s));
+    if (nShT_) ORB_HIP_CHECK(hipMemcpyAsync(dShT_, shT.data(), sizeof(int) * nShT_, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipMemcpyAsync(dPoseAdd_, poseAdd.data(), ng, hipMemcpyHostToDevice, s));
+    ORB_HIP_CHECK(hipStreamSynchronize(s));   // pageable sources
+    dist_ = true;
+    return 0;
+}
+
+int SparseLdlt::align_flag(const int* ePose, int nE, int* flag, hipStream_t s) {
+    ORB_HIP_CHECK(hipMemsetAsync(flag, 0, sizeof(int), s));
+    if (dist_ && nE > 0)
+        hipLaunchKernelGGL(k_align, dim3((nE + 255) / 256), dim3(256), 0, s, ePose, nE, prow_, dTcls_, flag);
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int SparseLdlt::solve_dist(double* b, double* x, double* scal, hipStream_t s, Comm* comm) {
+    if (!dist_) return -1;
+    if (n_ <= 0) return 0;
+    SpDev d = dev();
+    d.tcls = dTcls_;
+    ORB_HIP_CHECK(hipMemsetAsync(fail_, 0, sizeof(int), s));
+    ORB_HIP_CHECK(hipMemsetAsync(x, 0, sizeof(double) * n_, s));
+    const size_t nxb = (size_t)nShSlots_ * LT * LT, nyb = (size_t)nShT_ * LT;
+    double* xb = dXbuf_;
+    // this rank's subtrees, bottom-up (their nodes only: the kernels skip the other classes)
+    SpDev da = d;
+    da.want = 2;
+    for (int h = 0; h < nLev_; h++)
+        if (levOwn_[h]) enqueue_factor_level(da, h, b, s);
+    // the separators' inputs from this rank: S minus its subtrees' updates (ascending K), b minus
+    // their forward contributions
+    if (nShSlots_) hipLaunchKernelGGL(k_slot_pack, dim3(nShSlots_), dim3(256), 0, s, U_, dShSlots_, xb);
+    SpDev db = d;
+    db.want = 1;
+    db.kmode = 2;
+    db.dst = xb;
+    db.packIdx = dPackIdx_;
     for (int h = 0; h < nLev_; h++) {
         const int nt = hLevTgtStart_[h + 1] - hLevTgtStart_[h];
-        if (nt > 0) hipLaunchKernelGGL(k_ldlt_update, dim3(nt), dim3(256), 0, s, d, hLevTgtStart_[h]);
-        for (int st = hLevStepStart_[h]; st < hLevStepStart_[h + 1]; st++) {
-            const int4 a = hSteps_[st], z = hSteps_[st + 1];
-            if (z.x > a.x) hipLaunchKernelGGL(rolled_panels() ? k_ldlt_pdiag_r : k_ldlt_pdiag, dim3(z.x - a.x), dim3(64),
-                                              0, s, d, a.x);
-            if (z.y > a.y) hipLaunchKernelGGL(rolled_panels() ? k_ldlt_prow_r : k_ldlt_prow, dim3(z.y - a.y), dim3(64), 0,
-                                              s, d, a.y);
-            if (z.z > a.z) hipLaunchKernelGGL(k_ldlt_ptrail, dim3(z.z - a.z), dim3(256), 0, s, d, a.z);
-        }
-        const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
-        const int mt = hLevMaxT_[h];
-        if (sweep_nodes() && mt > 1 && mt <= kSweepMaxTiles)
-            hipLaunchKernelGGL(k_ldlt_fwdn, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)), sizeof(double) * LT * mt, s, d,
-                               hLevNodeStart_[h], b);
-        else
-            hipLaunchKernelGGL(k_ldlt_pfwd, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], b);
+        if (levSh_[h] && nt > 0) hipLaunchKernelGGL(k_ldlt_update, dim3(nt), dim3(256), 0, s, db, hLevTgtStart_[h]);
     }
-    for (int h = nLev_ - 1; h >= 0; h--) {
-        const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
-        const int mt = hLevMaxT_[h];
-        if (sweep_nodes() && mt > 1 && mt <= kSweepMaxTiles)
-            hipLaunchKernelGGL(k_ldlt_bwdn, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)), sizeof(double) * LT * mt, s, d,
-                               hLevNodeStart_[h], x, scal, h == nLev_ - 1 ? 1 : 0);
-        else
-            hipLaunchKernelGGL(k_ldlt_backward, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], x, scal,
-                               h == nLev_ - 1 ? 1 : 0);
-    }
+    if (nShT_) hipLaunchKernelGGL(k_ldlt_fwd_part, dim3(nShT_), dim3(64), 0, s, d, b, dShT_, xb + nxb);
+    ORB_HIP_CHECK(hipGetLastError());
+    if (int e = comm->allreduce(xb, nxb + nyb, RedOp::Sum, s)) return e;
+    // the separators, redundantly on every rank (only separator K's updates remain)
+    if (nShSlots_) hipLaunchKernelGGL(k_slot_unpack, dim3(nShSlots_), dim3(256), 0, s, U_, dShSlots_, xb);
+    if (nShT_) hipLaunchKernelGGL(k_b_unpack, dim3(nShT_), dim3(64), 0, s, d, dShT_, xb + nxb, b);
+    SpDev dc = d;
+    dc.want = 1;
+    dc.kmode = 1;
+    for (int h = 0; h < nLev_; h++)
+        if (levSh_[h]) enqueue_factor_level(dc, h, b, s);
+    // backward: the separators top-down, then this rank's subtrees top-down
+    SpDev dd = d;
+    dd.want = 1;
+    for (int h = nLev_ - 1; h >= 0; h--)
+        if (levSh_[h]) enqueue_backward_level(dd, h, x, scal, 0, s);
+    for (int h = nLev_ - 1; h >= 0; h--)
+        if (levOwn_[h]) enqueue_backward_level(da, h, x, scal, 0, s);
+    if (rank_ != 0 && nShT_) hipLaunchKernelGGL(k_x_zero_rows, dim3(nShT_), dim3(64), 0, s, d, dShT_, x);
+    double* fslot = xb + nxb + nyb;
+    hipLaunchKernelGGL(k_fail_pub, dim3(1), dim3(1), 0, s, fail_, fslot);
+    ORB_HIP_CHECK(hipGetLastError());
+    const RedBuf rb[2] = {{x, (size_t)n_}, {fslot, 1}};
+    if (int e = comm->allreduce(rb, 2, RedOp::Sum, s)) return e;
+    hipLaunchKernelGGL(k_scal_pub, dim3(1), dim3(1), 0, s, fslot, scal);
     ORB_HIP_CHECK(hipGetLastError());
     return 0;
 }

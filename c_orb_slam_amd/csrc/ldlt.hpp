@@ -6,9 +6,13 @@
 #include <cstdint>
 #include <vector>
 
+#include "ordering.hpp"
+
 namespace orbgpu {
 
 constexpr int kTile = 64;
+struct SpDev;
+class Comm;
 
 // Where k_schur writes S(r, c) (r <= c, system order): a dense row-major (nn x nn) matrix, or
 // the tiles of the block-sparse system.  There the poses are permuted (nested dissection):
@@ -48,6 +52,22 @@ public:
     // 1 on success (x written), 0 on an exactly zero pivot (x untouched).
     int solve(const double* b, double* x, double* scal, hipStream_t s);
     int zero(hipStream_t s);   // clear every tile (before S is assembled)
+    // Sharded factorisation (R ranks, this one `rank`): whole subtrees of the separator tree per
+    // rank (nd_assign), the separators above them factored by every rank.  plan() derives the
+    // tile classes, the exchange lists and the per-pose owner flags; -1 if the order has no
+    // tree (natural order) or R < 2.  After it, solve_dist() replaces solve(): each rank factors
+    // its subtrees, all-reduces {S - its subtrees' updates, b - their forward contributions} over
+    // the separator tiles and rows, factors the separators redundantly, back-substitutes its
+    // subtrees and all-reduces x.  S here is the rank's OWN partial Schur complement (no prior
+    // all-reduce): it must touch only this rank's subtrees and the separators (align_flag()).
+    int plan(int R, int rank, hipStream_t s);
+    bool dist() const { return dist_; }
+    int solve_dist(double* b, double* x, double* scal, hipStream_t s, Comm* comm);
+    // 1 in *flag if an active edge of this rank has its pose in another rank's subtree
+    int align_flag(const int* ePose, int nE, int* flag, hipStream_t s);
+    const uint8_t* pose_add() const { return dPoseAdd_; }   // k_schur: this rank adds Hpp + lambda, b_p
+    int dist_shared_tiles() const { return nShSlots_; }
+    int dist_shared_rows() const { return nShT_ * kTile; }
     SysAddr addr() const { return SysAddr{nullptr, n_, slotOf_, U_, nt_, prow_}; }
     double* tiles() const { return U_; }
     double* lt_tiles() const { return LT_; }
@@ -61,7 +81,20 @@ public:
     const std::vector<int>& host_prow() const { return hProw_; }
 
 private:
+    SpDev dev() const;
+    void enqueue_factor_level(const SpDev& d, int h, const double* b, hipStream_t s);
+    void enqueue_backward_level(const SpDev& d, int h, double* x, double* scal, int first, hipStream_t s);
     int n_ = 0, nt_ = 0, nslot_ = 0, nA_ = 0, nLev_ = 0;
+    bool nd_ = false, dist_ = false;
+    int rank_ = 0, nShSlots_ = 0, nShT_ = 0;
+    NdTree tree_;
+    std::vector<int> hNodeT_;
+    std::vector<uint8_t> levOwn_, levSh_;
+    void* distMem_ = nullptr;
+    size_t distCap_ = 0;
+    uint8_t *dTcls_ = nullptr, *dPoseAdd_ = nullptr;
+    int *dPackIdx_ = nullptr, *dShSlots_ = nullptr, *dShT_ = nullptr;
+    double* dXbuf_ = nullptr;
     long long nUpd_ = 0;
     void* mem_ = nullptr;
     size_t cap_ = 0;

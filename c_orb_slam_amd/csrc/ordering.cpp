@@ -134,4 +134,69 @@ void nd_order(int n, const std::vector<int>& adjStart, const std::vector<int>& a
     nd.order(std::move(all), roots);
 }
 
+void nd_assign(const NdTree& t, int R, std::vector<int>* owner) {
+    const int nn = (int)t.start.size();
+    owner->assign(nn, R <= 1 ? 0 : -1);
+    if (R <= 1 || nn == 0) return;
+    // subtree pose counts (children precede their parent in postorder)
+    std::vector<long long> cost(nn, 0);
+    std::vector<std::vector<int>> kids(nn);
+    for (int k = 0; k < nn; k++) {
+        cost[k] += t.end[k] - t.start[k];
+        if (t.parent[k] >= 0) {
+            cost[t.parent[k]] += cost[k];
+            kids[t.parent[k]].push_back(k);
+        }
+    }
+    // longest-processing-time assignment of a frontier; its makespan in poses
+    auto lpt = [&](std::vector<int> f, std::vector<int>* rootOwner) {
+        std::sort(f.begin(), f.end(), [&](int a, int b) { return cost[a] != cost[b] ? cost[a] > cost[b] : a < b; });
+        std::vector<long long> load(R, 0);
+        for (int k : f) {
+            int r = 0;
+            for (int q = 1; q < R; q++)
+                if (load[q] < load[r]) r = q;
+            if (rootOwner) (*rootOwner)[k] = r;
+            load[r] += cost[k];
+        }
+        return *std::max_element(load.begin(), load.end());
+    };
+    // split the largest splittable subtree again and again (its root joins the separators every
+    // rank factors), up to 4R subtrees; keep the frontier of the step with the least (separator
+    // poses + the most poses one rank gets) -- one split can raise that sum while the next ones
+    // lower it, so every prefix of the split sequence is scored
+    std::vector<int> front;
+    for (int k = 0; k < nn; k++)
+        if (t.parent[k] < 0) front.push_back(k);
+    long long shared = 0, bestT = lpt(front, nullptr);
+    std::vector<int> bestFront = front;
+    while ((int)front.size() < 4 * R) {
+        int pick = -1;
+        for (int q = 0; q < (int)front.size(); q++) {
+            const int k = front[q];
+            if (kids[k].empty()) continue;
+            if (pick < 0 || cost[k] > cost[front[pick]] || (cost[k] == cost[front[pick]] && k < front[pick])) pick = q;
+        }
+        if (pick < 0) break;
+        const int k = front[pick];
+        front.erase(front.begin() + pick);
+        front.insert(front.end(), kids[k].begin(), kids[k].end());
+        shared += t.end[k] - t.start[k];
+        const long long T = shared + lpt(front, nullptr);
+        if (T < bestT) {
+            bestT = T;
+            bestFront = front;
+        }
+    }
+    front = bestFront;
+    std::vector<int> rootOwner(nn, -1);
+    lpt(front, &rootOwner);
+    // a subtree's nodes take its root's rank: parents follow their children in postorder, so
+    // descending indices visit a parent first
+    for (int k = nn - 1; k >= 0; k--) {
+        if (rootOwner[k] >= 0) (*owner)[k] = rootOwner[k];
+        else if (t.parent[k] >= 0 && (*owner)[t.parent[k]] >= 0) (*owner)[k] = (*owner)[t.parent[k]];
+    }
+}
+
 }  // namespace orbgpu

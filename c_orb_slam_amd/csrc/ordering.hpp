@@ -25,6 +25,8 @@
 
 namespace orbgpu {
 
+constexpr int kNdLeafPoses = 32;   // leaf size of the pose systems' nested dissection (ldlt.hip, partitioner)
+
 struct NdTree {
     std::vector<int> perm;      // perm[k] = node (pose) at elimination position k
     // tree nodes in postorder: positions [start, end) of perm, parent (-1 = root), height
@@ -34,5 +36,14 @@ struct NdTree {
 
 // adjStart (n + 1) / adj: symmetric adjacency, each list sorted ascending, no self loops.
 void nd_order(int n, const std::vector<int>& adjStart, const std::vector<int>& adj, int leaf, NdTree* out);
+
+// Ranks of a sharded factorisation over the separator tree: owner[k] = the rank that factors
+// node k alone (a whole subtree per rank), -1 = a separator above the ranks' subtrees, factored
+// by every rank.  The largest splittable subtree (in poses) is split again and again -- its
+// root joins the separators -- up to 4R subtrees, and the step with the least (separator poses +
+// the most poses one rank gets) is kept; the subtrees go to ranks by longest-processing-time
+// first.  A pure function of the tree: every rank and the point partitioner derive the same
+// assignment.
+void nd_assign(const NdTree& t, int R, std::vector<int>* owner);
 
 }  // namespace orbgpu

@@ -249,6 +249,27 @@ def partition_points(problem, nranks):
     return out[:k.npt]
 
 
+def partition_points_nd(problem, nranks, with_kf_owner=False):
+    """pt_rank[p] for the sharded factorisation of a global BA: whole subtrees of the pose
+    graph's nested dissection per rank, a point with the rank of the first subtree pose it
+    observes (Optimizer_partition_points_nd, host only).  with_kf_owner: also the rank of each
+    keyframe's subtree (-1 separator, -2 no free pose)."""
+    k = _Packed(_args(problem))
+    out = np.zeros(max(k.npt, 1), np.int32)
+    kfo = np.zeros(max(len(problem["kf_id"]), 1), np.int32)
+    check(lib().Optimizer_partition_points_nd(C.byref(k.P), int(nranks), ptr(out), ptr(kfo)),
+          "Optimizer_partition_points_nd")
+    return (out[:k.npt], kfo[:len(problem["kf_id"])]) if with_kf_owner else out[:k.npt]
+
+
+def last_sharding():
+    """The calling thread's last BA run: (sharded factorisation used, separator tiles exchanged
+    per trial, separator rows, Schur-pattern tiles the replicated path would all-reduce)."""
+    v = np.zeros(4, np.int32)
+    check(lib().Optimizer_last_sharding(ptr(v)), "Optimizer_last_sharding")
+    return tuple(int(x) for x in v)
+
+
 def shard_problem(problem, pt_rank, rank):
     """Rank `rank`'s shard: every keyframe, its own points and all of their edges, in the original
     (reference creation) order.  Adds pt_index / edge_index: positions in the full problem."""
@@ -341,11 +362,14 @@ def BundleAdjustmentSharded(shard, comm, nIterations=10, bRobust=False, stop=Non
     return k.result(trace)
 
 
-def run_sharded_local(problem, nranks, mode="local", nIterations=10, bRobust=False, trace=False, pt_rank=None):
+def run_sharded_local(problem, nranks, mode="local", nIterations=10, bRobust=False, trace=False, pt_rank=None,
+                      partition="block"):
     """Run the sharded protocol with `nranks` in-process ranks (threads) on the current device;
-    returns (merged result, per-rank results).  mode: "local" or "global"."""
+    returns (merged result, per-rank results).  mode: "local" or "global"; partition: "block"
+    (keyframe blocks) or "nd" (separator-tree subtrees: the sharded factorisation).  Each rank's
+    result carries `sharding` (last_sharding())."""
     if pt_rank is None:
-        pt_rank = partition_points(problem, nranks)
+        pt_rank = partition_points_nd(problem, nranks) if partition == "nd" else partition_points(problem, nranks)
     shards = [shard_problem(problem, pt_rank, r) for r in range(nranks)]
     comms = Comm.local_group(nranks)
     results = [None] * nranks
@@ -357,6 +381,7 @@ def run_sharded_local(problem, nranks, mode="local", nIterations=10, bRobust=Fal
                 results[r] = LocalBundleAdjustmentSharded(shards[r], comms[r], trace=trace)
             else:
                 results[r] = BundleAdjustmentSharded(shards[r], comms[r], nIterations, bRobust, trace=trace)
+            results[r]["sharding"] = last_sharding()
         except Exception as e:  # noqa: BLE001 -- re-raised below
             errors[r] = e
 

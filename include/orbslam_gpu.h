@@ -791,7 +791,9 @@ int Optimizer_PoseOptimization_frames_device_deferred(ORBmatcher_h chain, int co
  * thread) per rank, map points partitioned by the block of their reference
  * keyframe, poses replicated.  Per LM trial the ranks all-reduce the partial
  * Schur complement {S, b_s} and the scalars {chi2, scale, stop}; every rank
- * solves the identical reduced system.  Pass each rank the SAME keyframes and
+ * solves the identical reduced system -- or, with the separator-tree partition
+ * (Optimizer_partition_points_nd) of a block-sparse system, each rank factors
+ * its own subtrees and only the separators' tiles and rows are exchanged.  Pass each rank the SAME keyframes and
  * its own points + all of their edges (edge order preserved); the results are
  * the rank's points / edges and the (identical) poses.
  * ---------------------------------------------------------------------- */
@@ -809,6 +811,20 @@ int orbgpu_comm_destroy(orbgpu_comm_h h);
  * of a point = keyframe of its first edge; keyframes in mnId order are cut into
  * nranks contiguous blocks of ~equal edge weight.  Host only (no device needed). */
 int Optimizer_partition_points(const ba_problem* P, int nranks, int32_t* pt_rank);
+/* Separator-tree partition for the sharded factorisation of a global BA (BundleAdjustment):
+ * the nested dissection of the pose graph the engine derives (ordering.hpp), whole subtrees
+ * to ranks (nd_assign), each point to the rank of the first subtree pose it observes (a point
+ * of separator poses only: round robin).  With it every rank's Schur terms stay inside its own
+ * subtrees and the separators, so the ranks factor their subtrees alone and exchange only the
+ * separator tiles and rows (Optimizer_BundleAdjustment_sharded checks this and otherwise keeps
+ * the replicated factorisation).  Fewer than 24 free poses or one rank: the keyframe-block
+ * partition.  kf_owner (optional, n_kf entries): the rank whose subtree holds keyframe k's
+ * pose, -1 for a separator pose, -2 for a keyframe that is no free pose.  Host only. */
+int Optimizer_partition_points_nd(const ba_problem* P, int nranks, int32_t* pt_rank, int32_t* kf_owner);
+/* The calling thread's last BA run: [sharded factorisation used (0/1), separator tiles and
+ * separator rows exchanged per LM trial, Schur-pattern tiles (what the replicated path
+ * all-reduces)]. */
+int Optimizer_last_sharding(int* info4);
 int Optimizer_LocalBundleAdjustment_sharded(const ba_problem* shard, orbgpu_comm_h comm,
                                             const volatile bool* stop, ba_result* R);
 int Optimizer_BundleAdjustment_sharded(const ba_problem* shard, orbgpu_comm_h comm, int nIterations,
@@ -824,7 +840,7 @@ int Optimizer_last_timings(double* ms2);
 /* Unit entry points of the BA building blocks (parity tests): the dense LDL^T
  * solve of the reduced pose system (variant 0 = register-resident panel kernel,
  * n <= 127; 1 = generic kernel; 2 / 3 = block-sparse tiled, natural / nested-dissection order;
- * 4 = row-owner kernel, n <= 96; 5 = column-owner kernel, n <= 96) and
+ * 4 = row-owner kernel, n <= 96; 5 / 6 = column-owner / row-lane kernel, n <= 96) and
  * the canonical FP64 sum. */
 int orbgpu_unit_ldlt_solve(int n, const double* S, const double* b, double* x, int variant, int* ok);
 int orbgpu_unit_csum(const double* v, int n, double* out);

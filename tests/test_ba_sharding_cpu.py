@@ -45,6 +45,39 @@ def test_partition_contiguous_blocks_and_balance(nranks):
         assert w.min() > 0.5 * w.mean() and w.max() < 1.5 * w.mean(), w
 
 
+@pytest.mark.parametrize("nranks,laps,n_kf", [(2, 0, 400), (4, 4, 400), (8, 4, 400), (8, 4, 2000)])
+def test_partition_nd_subtrees(nranks, laps, n_kf):
+    """Optimizer_partition_points_nd (host only): every point one rank, deterministic, and a
+    keyframe observed by points of two ranks must be a separator pose, so few keyframes are:
+    each rank's Schur terms stay inside its own subtrees and the separators."""
+    from c_orb_slam_amd.optimizer import partition_points_nd
+    pr = global_ba_problem(3, n_kf=n_kf, pts_per_kf=40, laps=laps)
+    r, kfo = partition_points_nd(pr, nranks, with_kf_owner=True)
+    assert r.shape == (len(pr["pt_id"]),) and r.min() >= 0 and r.max() < nranks
+    assert np.array_equal(r, partition_points_nd(pr, nranks))
+    assert (kfo[pr["kf_id"] == 0] == -2).all()          # the fixed keyframe is no pose
+    assert set(np.unique(kfo[pr["kf_id"] != 0])) <= set(range(-1, nranks))
+    # the invariant the sharded factorisation relies on: a point observes only poses of its
+    # rank's subtrees or separators
+    own = kfo[pr["edge_kf"]]
+    assert ((own == -1) | (own == -2) | (own == r[pr["edge_pt"]])).all()
+    sizes = [(kfo == q).sum() for q in range(nranks)]
+    if n_kf >= 2000:   # config-5 size: every rank a subtree, separators a small share
+        assert min(sizes) > 0 and max(sizes) < 2 * np.mean(sizes), sizes
+        assert (kfo == -1).sum() < 0.2 * n_kf
+    else:              # a small loop-closed map may leave ranks without a subtree (separators only)
+        assert sum(sizes) > 0
+
+
+def test_partition_nd_small_or_single_rank_is_block():
+    """Below the block-sparse size (24 free poses) or at one rank: the keyframe-block partition."""
+    from c_orb_slam_amd.optimizer import partition_points, partition_points_nd
+    pr = global_ba_problem(1, n_kf=20, pts_per_kf=30)
+    assert np.array_equal(partition_points_nd(pr, 3), partition_points(pr, 3))
+    pr = global_ba_problem(1, n_kf=60, pts_per_kf=30)
+    assert (partition_points_nd(pr, 1) == 0).all()
+
+
 def test_partition_validates():
     from c_orb_slam_amd._lib import ba_problem as BP
     L = _lib()

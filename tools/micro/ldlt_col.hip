@@ -45,7 +45,7 @@ __global__ void __launch_bounds__(256) k_col(int n, const double* __restrict__ S
                                              unsigned long long* rt) {
     __shared__ double Ur[2][128];
     __shared__ double Lall[kMax * kMax];
-    __shared__ double lw[4][kRows + 8];
+    __shared__ __attribute__((aligned(16))) double lw[4][kRows + 8];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int c0 = lane, c1 = lane + 64;
     unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -71,11 +71,10 @@ __global__ void __launch_bounds__(256) k_col(int n, const double* __restrict__ S
         const double d = U[k];
         const double u0 = U[c0], u1 = U[c1];
         const int own = (k + 1) & 3;
-        const SharedDiv sd(d);
         STAMP(0);
         if (w == own) {
             const int r1 = (k + 1) >> 2;
-            const double l1 = sd.div(U[k + 1 < n ? k + 1 : k]);
+            const double l1 = U[k + 1 < n ? k + 1 : k] / d;
 #pragma unroll
             for (int r = 0; r < kRows; r++)
                 if (r == r1 && k + 1 < n) {
@@ -86,7 +85,7 @@ __global__ void __launch_bounds__(256) k_col(int n, const double* __restrict__ S
                 }
         }
         STAMP(1);
-        const double l0 = sd.div(u0), l1v = sd.div(u1);
+        const double l0 = u0 / d, l1v = u1 / d;
         STAMP(2);
         if (w == 0) {
             if (c0 > k && c0 < n) Lall[k * n + c0] = l0;
@@ -99,13 +98,21 @@ __global__ void __launch_bounds__(256) k_col(int n, const double* __restrict__ S
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
         STAMP(3);
+        const int rlive = (k + 5 - w) >> 2;
 #pragma unroll
-        for (int r = 0; r < kRows; r++) {
-            const int i = 4 * r + w;
-            if (i > k + 1 && i < n) {
-                const double li = lw[w][r];
-                A0[r] -= li * u0;
-                A1[r] -= li * u1;
+        for (int g = 0; g < kRows / 4; g++) {
+            if (4 * g + 3 >= rlive && 16 * g + w < n) {
+                const double2 la = *reinterpret_cast<const double2*>(&lw[w][4 * g]);
+                const double2 lb = *reinterpret_cast<const double2*>(&lw[w][4 * g + 2]);
+                const double lv[4] = {la.x, la.y, lb.x, lb.y};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int r = 4 * g + q, i = 4 * r + w;
+                    const bool live = i > k + 1 && i < n;
+                    const double v0 = A0[r] - lv[q] * u0, v1 = A1[r] - lv[q] * u1;
+                    A0[r] = live ? v0 : A0[r];
+                    A1[r] = live ? v1 : A1[r];
+                }
             }
         }
         STAMP(4);
@@ -198,7 +205,7 @@ int main() {
     hipMemcpyFromSymbol(t, HIP_SYMBOL(g_t), sizeof(t));
     printf("k_col n=%d: event %.1f us; loop %llu cycles over %llu realtime ticks (%.0f MHz)\n", n, ms * 1e3, t[0][6],
            t[0][7], t[0][6] / (t[0][7] / 100.0));
-    const char* ph[6] = {"U reads + rcp", "own row + publish", "2 divisions", "l round trip", "row updates", "barrier"};
+    const char* ph[6] = {"U reads", "own row + publish", "2 divisions", "l round trip", "row updates", "barrier"};
     for (int w = 0; w < 4; w++) {
         printf("wave %d per pivot:", w);
         for (int i = 0; i < 6; i++) printf(" %s %.0f |", ph[i], t[w][i] / (double)n);
