@@ -1019,6 +1019,119 @@ __global__ void __launch_bounds__(256) k_ldlt_t(int n, const double* __restrict_
     ldlt_backward_wave(n, Lall, dvec, y, x, scal);
 }
 
+// 2-D block-cyclic LDL^T + solve for n <= kLdltColMax, 4 waves: thread (a, b) holds A[i][j] for
+// i = 16 r + a, j = 16 c + b of [S | b] (b in column n); a wave holds four row classes, so a
+// register row or column past the live part of the matrix is skipped by the whole wave.  Per
+// panel of 8 pivots: the owners publish the panel rows, wave 0 factors them right-looking
+// (lane = column: l_jk = u_kj / d_k lane-parallel, the later panel rows updated with the l read
+// back by readlane), writing the final U rows and the L columns to LDS, then every thread
+// applies the panel's pivots, ascending, to its live entries.  Per element the oracle's
+// ora_ldlt_solve sequence; two barriers per panel.
+constexpr int k2dPW = 8, k2dR = 6, k2dC = 7;   // panel width; rows 16 r + a (r < 6), columns 16 c + b (c < 7)
+__global__ void __launch_bounds__(256) k_ldlt_2d(int n, const double* __restrict__ Sg, const double* bs, double* x,
+                                                 double* scal, const int* run) {
+    BA_GATE(run);
+    __shared__ double Lall[kLdltColMax * kLdltColMax];   // S staging, then L[i][k] at Lall[k * n + i]
+    __shared__ double UP[k2dPW][128];                    // the panel's final U rows, columns 0..n
+    __shared__ double Pn[k2dPW][128];                    // the panel rows as published
+    __shared__ double dvec[kLdltColMax], y[kLdltColMax];
+    __shared__ int ok;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int a = 4 * w + (lane & 3), b = lane >> 2;
+    for (int q = tid; q < n * n; q += 256) Lall[q] = Sg[q];
+    if (tid == 0) ok = 1;
+    __syncthreads();
+    double A[k2dR][k2dC];
+#pragma unroll
+    for (int r = 0; r < k2dR; r++)
+#pragma unroll
+        for (int c = 0; c < k2dC; c++) {
+            const int i = 16 * r + a, j = 16 * c + b;
+            A[r][c] = (i < n && j < n && j >= i) ? Lall[i * n + j] : (i < n && j == n) ? bs[i] : 0.0;
+        }
+    for (int p0 = 0; p0 < n; p0 += k2dPW) {
+        const int p1 = min(p0 + k2dPW, n);
+        // the panel rows' current values (final: every earlier panel is applied)
+#pragma unroll
+        for (int r = 0; r < k2dR; r++) {
+            const int i = 16 * r + a;
+            if (i >= p0 && i < p1)
+#pragma unroll
+                for (int c = 0; c < k2dC; c++) Pn[i - p0][16 * c + b] = A[r][c];
+        }
+        __syncthreads();   // also: every thread is done with the previous panel's UP
+        if (w == 0) {
+            double u0[k2dPW], u1[k2dPW];
+#pragma unroll
+            for (int t = 0; t < k2dPW; t++) {
+                u0[t] = p0 + t < n ? Pn[t][lane] : 0.0;
+                u1[t] = p0 + t < n ? Pn[t][lane + 64] : 0.0;
+            }
+            bool good = true;
+#pragma unroll
+            for (int t = 0; t < k2dPW; t++) {
+                const int k = p0 + t;
+                if (k < n && good) {
+                    UP[t][lane] = u0[t];   // row k is final
+                    UP[t][lane + 64] = u1[t];
+                    const double d = k < 64 ? readlane_d(u0[t], k) : readlane_d(u1[t], k - 64);
+                    if (d == 0.0) {   // uniform
+                        good = false;
+                        if (lane == 0) ok = 0;
+                    } else {
+                        const double l0 = u0[t] / d, l1 = u1[t] / d;   // l_jk, j = lane / lane + 64
+                        if (lane > k && lane < n) Lall[k * n + lane] = l0;
+                        if (lane + 64 > k && lane + 64 < n) Lall[k * n + lane + 64] = l1;
+                        const double yk = n < 64 ? readlane_d(u0[t], n) : readlane_d(u1[t], n - 64);
+                        if (lane == 0) {
+                            dvec[k] = d;
+                            y[k] = yk;   // b_k after its k updates: the forward-substituted y_k
+                        }
+#pragma unroll
+                        for (int t2 = t + 1; t2 < k2dPW; t2++) {
+                            const int i = p0 + t2;
+                            if (i < n) {
+                                const double li = i < 64 ? readlane_d(l0, i) : readlane_d(l1, i - 64);
+                                u0[t2] -= li * u0[t];
+                                u1[t2] -= li * u1[t];
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (!ok) break;
+        // rows >= p1: the panel's pivots, ascending, on the live register rows / columns
+        const int pw = p1 - p0;
+#pragma unroll
+        for (int r = 0; r < k2dR; r++) {
+            if (16 * r + 4 * w + 3 < p1) continue;   // the wave's four rows of register row r are done
+            const int i = 16 * r + a;
+            double lv[k2dPW];
+#pragma unroll
+            for (int t = 0; t < k2dPW; t++) lv[t] = t < pw ? Lall[(p0 + t) * n + i] : 0.0;
+#pragma unroll
+            for (int c = 0; c < k2dC; c++) {
+                if (16 * c + 15 < p1) continue;      // every column of register column c is done
+                const int j = 16 * c + b;
+                double v = A[r][c];
+#pragma unroll
+                for (int t = 0; t < k2dPW; t++)
+                    if (t < pw) v -= lv[t] * UP[t][j];
+                A[r][c] = v;
+            }
+        }
+    }
+    if (!ok) {
+        if (tid == 0) scal[3] = 0.0;
+        return;
+    }
+    __syncthreads();
+    if (w != 0) return;
+    ldlt_backward_wave(n, Lall, dvec, y, x, scal);
+}
+
 // Register-resident LDL^T + solve for n < 128 (<= 21 free keyframes), 1024 threads.
 // Thread (wave w < 16, lane) owns rows i = 16 r + w (r < 8) of columns j = lane, lane + 64.
 // Per 6-column panel: owners publish the panel rows to LDS (U), wave 0 factorises them
@@ -3205,7 +3318,7 @@ static std::atomic<int> g_scale_small_max{2048 * 64};
 // (config 4, tools/ba_timing.py): panel 3.91-4.00 ms, column-owner 5.05 ms (136 us per solve
 // against 77), row-owner 8.63 ms (profiles/r04b_*, r04l_*).  All perform the oracle's operation
 // sequence.
-enum class DenseLdlt { Col, Reg, Row, Lds, T };
+enum class DenseLdlt { Col, Reg, Row, Lds, T, D2 };
 static DenseLdlt dense_ldlt_kind(int n, bool use_reg) {
     static const int pick = [] {
         const char* e = std::getenv("ORBGPU_LDLT_DENSE");
@@ -3213,8 +3326,10 @@ static DenseLdlt dense_ldlt_kind(int n, bool use_reg) {
         if (!strcmp(e, "col")) return 0;
         if (!strcmp(e, "row")) return 2;
         if (!strcmp(e, "t")) return 3;
+        if (!strcmp(e, "2d")) return 4;
         return 1;
     }();
+    if (pick == 4 && n <= kLdltColMax) return DenseLdlt::D2;
     if (pick == 2 && n <= kLdltRowMax) return DenseLdlt::Row;
     if (pick == 3 && n <= kLdltColMax) return DenseLdlt::T;
     if (pick == 0 && n <= kLdltColMax) return DenseLdlt::Col;
@@ -3318,6 +3433,8 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
             hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else if (kind == DenseLdlt::T) {
             hipLaunchKernelGGL(k_ldlt_t, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
+        } else if (kind == DenseLdlt::D2) {
+            hipLaunchKernelGGL(k_ldlt_2d, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else if (kind == DenseLdlt::Row) {
             hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else if (kind == DenseLdlt::Reg) {
@@ -3459,6 +3576,7 @@ void BaEngine::enqueue_lm_step(bool first) {
     const DenseLdlt kind = dense_ldlt_kind(n, use_reg);
     if (kind == DenseLdlt::Col) hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else if (kind == DenseLdlt::T) hipLaunchKernelGGL(k_ldlt_t, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else if (kind == DenseLdlt::D2) hipLaunchKernelGGL(k_ldlt_2d, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else if (kind == DenseLdlt::Row) hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else if (kind == DenseLdlt::Reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, ctl);
@@ -3660,10 +3778,11 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
     ORB_HIP_CHECK(hipMemcpy(dS, S, sizeof(double) * n * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemcpy(dB, b, sizeof(double) * n, hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMemset(dX, 0, sizeof(double) * nn));
-    if (variant == 5 || variant == 6) {
+    if (variant == 5 || variant == 6 || variant == 7) {
         if (n > kLdltColMax) return -3;
         if (variant == 5) hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, 0, n, dS, dB, dX, dScal, nullptr);
-        else hipLaunchKernelGGL(k_ldlt_t, dim3(1), dim3(256), 0, 0, n, dS, dB, dX, dScal, nullptr);
+        else if (variant == 6) hipLaunchKernelGGL(k_ldlt_t, dim3(1), dim3(256), 0, 0, n, dS, dB, dX, dScal, nullptr);
+        else hipLaunchKernelGGL(k_ldlt_2d, dim3(1), dim3(256), 0, 0, n, dS, dB, dX, dScal, nullptr);
     } else if (variant == 4) {
         if (n > kLdltRowMax) return -3;
         hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, 0, n, dS, dB, dX, dScal, nullptr);

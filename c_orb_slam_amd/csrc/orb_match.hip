@@ -406,17 +406,23 @@ static int stage_threads() {
 constexpr size_t kStageLds = sizeof(uint16_t) * (kGridCells + 2) + sizeof(uint16_t) * kStageMaxN +
                              sizeof(float2) * kStageMaxN + kStageMaxN + 32 * (size_t)kStageMaxN + 64;
 template <bool LAST, bool STAGE, int NT>
-__global__ void __launch_bounds__(NT) k_candidates(const SearchDev* __restrict__ probs, float th, int bMono,
-                                                   unsigned long long* counters) {
+__global__ void __launch_bounds__(NT) k_candidates(const SearchDev* __restrict__ probs, int np, int gx, float th,
+                                                   int bMono, unsigned long long* counters) {
     ORBGPU_LATENCY_WAVE();
-    const SearchDev P = probs[blockIdx.y];
+    // XCD-aware order: workgroups L and L + 8 share an XCD (blocks are dealt round-robin over the
+    // 8 XCDs), so workgroup L takes problem (L % 8) + 8 (L / 8 / gx), block (L / 8) % gx: every
+    // block of a problem runs on one XCD and the frame it stages is fetched into one L2
+    const int xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
+    const int by = xcd + 8 * (slot / gx), bx = slot % gx;
+    if (by >= np) return;
+    const SearchDev P = probs[by];
     int nvis = P.nq;
     if (!LAST && P.visList) nvis = *P.visCount;   // SearchLocalPoints: the t-th in-view query
     // a workgroup with no query of its own stages nothing (SearchLocalPoints' in-view count is
     // known on the device only: the grid covers every local map point)
-    if (!counters && (int)(blockIdx.x * NT) >= nvis) return;
-    const int tBegin = (int)(blockIdx.x * NT + threadIdx.x);
-    const int tStride = (int)(gridDim.x * NT);
+    if (!counters && bx * NT >= nvis) return;
+    const int tBegin = bx * NT + (int)threadIdx.x;
+    const int tStride = gx * NT;
     LView V{};
     if constexpr (STAGE) {
         extern __shared__ __align__(16) unsigned char s_stage[];
@@ -466,7 +472,7 @@ __global__ void __launch_bounds__(NT) k_candidates(const SearchDev* __restrict__
         pr = wave_sum_u64(pr);
         nqv = wave_sum_u64(nqv);
         if ((threadIdx.x & 63) == 0) {
-            const int sl = (blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 6)) & (kCountSlots - 1);
+            const int sl = (bx + by * 7 + (threadIdx.x >> 6)) & (kCountSlots - 1);
             atomicAdd(&counters[0 * kCountSlots + sl], pr);
             atomicAdd(&counters[1 * kCountSlots + sl], nqv);
         }
@@ -1067,6 +1073,10 @@ void* Matcher::arena_alloc(size_t bytes) {
     return p;
 }
 
+// k_candidates' XCD-aware 1-D grid: gx blocks per problem, problems dealt to the 8 XCDs
+static inline int cand_gx(int maxq, int nt) { return (maxq + nt - 1) / nt; }
+static inline dim3 cand_grid(int maxq, int nt, int np) { return dim3(8 * cand_gx(maxq, nt) * ((np + 7) / 8)); }
+
 int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastMode, float nnratio) {
     const int np = (int)probs.size();
     if (np == 0) return 0;
@@ -1134,30 +1144,30 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     if (maxq > 0) {
         if (lastMode) {
             if (maxN <= kStageMaxN && stage_threads() == 256)
-                hipLaunchKernelGGL((k_candidates<true, true, 256>), dim3((maxq + 255) / 256, np), dim3(256), kStageLds,
-                                   stream_, dp, th, (int)bMono, counters());
+                hipLaunchKernelGGL((k_candidates<true, true, 256>), cand_grid(maxq, 256, np), dim3(256), kStageLds,
+                                   stream_, dp, np, cand_gx(maxq, 256), th, (int)bMono, counters());
             else if (maxN <= kStageMaxN)
-                hipLaunchKernelGGL((k_candidates<true, true, kStageThreads>), dim3((maxq + kStageThreads - 1) / kStageThreads, np),
+                hipLaunchKernelGGL((k_candidates<true, true, kStageThreads>), cand_grid(maxq, kStageThreads, np),
                                    dim3(kStageThreads), kStageLds,
-                                   stream_, dp, th, (int)bMono, counters());
+                                   stream_, dp, np, cand_gx(maxq, kStageThreads), th, (int)bMono, counters());
             else
-                hipLaunchKernelGGL((k_candidates<true, false, 256>), dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp,
-                                   th, (int)bMono, counters());
+                hipLaunchKernelGGL((k_candidates<true, false, 256>), cand_grid(maxq, 256, np), dim3(256), 0, stream_, dp,
+                                   np, cand_gx(maxq, 256), th, (int)bMono, counters());
             mark(2);
             // nq = the last frame's N <= kMaxFrameKeys = 512 * kSelQLast: every query in a slot
             hipLaunchKernelGGL((k_select_r<true, 512, kSelQLast>), dim3(np), dim3(512), select_lds_bytes(maxN), stream_, dp,
                                th, (int)bMono, nnratio, (int)checkOri_, maxN);
         } else {
             if (maxN <= kStageMaxN && stage_threads() == 256)
-                hipLaunchKernelGGL((k_candidates<false, true, 256>), dim3((maxq + 255) / 256, np), dim3(256), kStageLds,
-                                   stream_, dp, th, 0, counters());
+                hipLaunchKernelGGL((k_candidates<false, true, 256>), cand_grid(maxq, 256, np), dim3(256), kStageLds,
+                                   stream_, dp, np, cand_gx(maxq, 256), th, 0, counters());
             else if (maxN <= kStageMaxN)
-                hipLaunchKernelGGL((k_candidates<false, true, kStageThreads>), dim3((maxq + kStageThreads - 1) / kStageThreads, np),
+                hipLaunchKernelGGL((k_candidates<false, true, kStageThreads>), cand_grid(maxq, kStageThreads, np),
                                    dim3(kStageThreads), kStageLds,
-                                   stream_, dp, th, 0, counters());
+                                   stream_, dp, np, cand_gx(maxq, kStageThreads), th, 0, counters());
             else
-                hipLaunchKernelGGL((k_candidates<false, false, 256>), dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, dp,
-                                   th, 0, counters());
+                hipLaunchKernelGGL((k_candidates<false, false, 256>), cand_grid(maxq, 256, np), dim3(256), 0, stream_, dp,
+                                   np, cand_gx(maxq, 256), th, 0, counters());
             mark(2);
             // SearchLocalPoints-sized query sets (thousands of local map points, long occupancy
             // chains between duplicated points): 16 waves per round of the fixed point

@@ -4,8 +4,9 @@
 // The reference loop draws a minimal set with the process rand(), solves EPnP, scores every
 // correspondence and returns as soon as Refine() on the best-so-far inliers succeeds.  The draws
 // do not depend on the results, so a call's hypotheses are generated up front from the caller's
-// stream (k_pnp_draws: the glibc recurrence a wave at a time, ransac_dev.hpp), solved
-// (k_pnp_hypotheses: a thread per hypothesis, EPnP in FP64) and scored (k_pnp_check: CheckInliers
+// stream (inside k_pnp_hypotheses: each workgroup regenerates the glibc recurrence up to its own
+// draws, ransac_dev.hpp draw_range), solved (k_pnp_hypotheses: a thread per hypothesis, EPnP in
+// FP64) and scored (k_pnp_check: CheckInliers
 // lane-parallel) for every solver of the batch at once.  k_pnp_replay then walks each solver's
 // hypotheses in the reference's order -- best on `>`, Refine() of the best set (cached while the
 // set stands), early return, the `||` loop's exhaustion branch -- and writes one record per solver
@@ -79,7 +80,12 @@ __device__ __forceinline__ void store_rt(double* out, const double R[3][3], cons
 // Hypothesis solve (PnPsolver.cc:196-210): a thread per hypothesis runs EPnP on its minimal set
 // in FP64 and stores (R, t); counts[h] = -1 flags an invalid draw (never expected).
 __global__ void __launch_bounds__(64) k_pnp_hypotheses(const PnPProbDev* __restrict__ probs) {
+    __shared__ uint32_t win[32];
     const PnPProbDev& P = probs[blockIdx.y];
+    const int h0 = blockIdx.x * 64;
+    if (h0 >= P.nhyp) return;   // workgroup-uniform
+    // this workgroup's minimal sets from the caller's stream (PnPsolver.cc:189-201)
+    draw_range(P.rng, P.minSet, P.N, P.raw, P.hyp_idx, win, h0, min(P.nhyp, h0 + 64));
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= P.nhyp) return;
     for (int k = 0; k < P.minSet; k++) {
@@ -161,12 +167,6 @@ __global__ void __launch_bounds__(kPnPCheckThreads) k_pnp_check(const PnPProbDev
 }
 
 // The call's minimal sets from the caller's stream, a wave per solver (PnPsolver.cc:189-201).
-__global__ void __launch_bounds__(64) k_pnp_draws(const PnPProbDev* __restrict__ probs) {
-    __shared__ uint32_t win[32];
-    const PnPProbDev& P = probs[blockIdx.x];
-    if (P.nhyp <= 0) return;
-    draw_sets(P.rng, P.nhyp, P.minSet, P.N, P.raw, P.hyp_idx, win);
-}
 
 // CheckInliers of pose (R, t) over all N correspondences by one wave: mask words + count.
 __device__ __forceinline__ int check_inliers_wave(const PnPProbDev& P, const double* R, const double* t, uint32_t* mask) {
@@ -593,7 +593,6 @@ int PnPBatch::iterate(int n, PnPSolver** S, int nIterations, orb_rng** rngs, PnP
     if (nact == 0) return 0;
     ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd, sizeof(PnPProbDev) * nact, hipMemcpyHostToDevice, s));
     const PnPProbDev* dprobs = (const PnPProbDev*)d_probs_;
-    hipLaunchKernelGGL(k_pnp_draws, dim3(nact), dim3(64), 0, s, dprobs);
     if (maxK > 0) {
         if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[0], s));
         hipLaunchKernelGGL(k_pnp_hypotheses, dim3((maxK + 63) / 64, nact), dim3(64), 0, s, dprobs);

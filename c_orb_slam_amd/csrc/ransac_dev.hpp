@@ -19,8 +19,9 @@ namespace orbgpu {
 constexpr int kRngMaxRange = 1 << 22;   // RandomInt ranges the integer form reproduces exactly
 
 // raw[0..D) = the next D table words of stream g (x[n..n+D)); every lane of a 64-thread
-// workgroup calls it; win: 32 u32 of LDS.
-__device__ __forceinline__ void rng_generate(const orb_rng& g, int D, uint32_t* raw, uint32_t* win) {
+// workgroup calls it; win: 32 u32 of LDS.  Only the words from `from` on are stored (a
+// workgroup that draws hypotheses [h0, h1) regenerates the stream up to its own words).
+__device__ __forceinline__ void rng_generate(const orb_rng& g, int D, uint32_t* raw, uint32_t* win, int from = 0) {
     const int lane = threadIdx.x & 63;
     if (lane < 31) {
         int s = g.f + lane;
@@ -37,7 +38,7 @@ __device__ __forceinline__ void rng_generate(const orb_rng& g, int D, uint32_t* 
         __syncthreads();
         if (lane < 31) {
             win[lane] = v;
-            if (base + lane < D) raw[base + lane] = v;
+            if (base + lane < D && base + lane >= from) raw[base + lane] = v;
         }
         __syncthreads();
     }
@@ -127,6 +128,37 @@ __device__ __forceinline__ void draw_sets(const orb_rng& g, int K, int ms, int N
             draw_set_n(rw, N, ms, s);
             for (int i = 0; i < ms; i++) o[i] = s[i];
         }
+    }
+}
+
+// The minimal sets of hypotheses [h0, h1) of the call (h1 - h0 <= 64), inside the kernel that
+// solves them: the stream up to word h1 * ms is regenerated by this workgroup (a few dozen
+// 31-word steps), its own words stored, then lane h - h0 draws set h.  Every workgroup of a
+// solver does this for its own range, so no separate draw launch precedes the solves; the
+// replay reads the stored words back for the stream position.  64-thread workgroup (one wave:
+// the raw words a lane stored are read by other lanes after the barrier).
+__device__ __forceinline__ void draw_range(const orb_rng& g, int ms, int N, uint32_t* raw, int* idx, uint32_t* win,
+                                           int h0, int h1) {
+    rng_generate(g, h1 * ms, raw, win, h0 * ms);
+    __syncthreads();
+    const int h = h0 + (int)(threadIdx.x & 63);
+    if (h >= h1) return;
+    const uint32_t* rw = raw + (size_t)h * ms;
+    int* o = idx + (size_t)h * ms;
+    if (ms == 4) {
+        int s[4];
+        draw_set<4>(rw, N, s);
+#pragma unroll
+        for (int i = 0; i < 4; i++) o[i] = s[i];
+    } else if (ms == 3) {
+        int s[3];
+        draw_set<3>(rw, N, s);
+#pragma unroll
+        for (int i = 0; i < 3; i++) o[i] = s[i];
+    } else {
+        int s[64];
+        draw_set_n(rw, N, ms, s);
+        for (int i = 0; i < ms; i++) o[i] = s[i];
     }
 }
 

@@ -216,7 +216,12 @@ __device__ __forceinline__ void project(const float* X, const float* T, const fl
 }
 
 __global__ void __launch_bounds__(64) k_sim3_hypotheses(const Sim3ProbDev* __restrict__ probs) {
+    __shared__ uint32_t win[32];
     const Sim3ProbDev& P = probs[blockIdx.y];
+    const int h0 = blockIdx.x * 64;
+    if (h0 >= P.nhyp) return;   // workgroup-uniform
+    // this workgroup's minimal sets from the caller's stream (Sim3Solver.cc:166-178)
+    draw_range(P.rng, 3, P.N, P.raw, P.hyp_idx, win, h0, min(P.nhyp, h0 + 64));
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= P.nhyp) return;
     float P1[3][3], P2[3][3];
@@ -308,13 +313,6 @@ __global__ void __launch_bounds__(kSim3CheckThreads) k_sim3_check(const Sim3Prob
     }
 }
 
-// The call's minimal sets from the caller's stream, a wave per solver (Sim3Solver.cc:166-178).
-__global__ void __launch_bounds__(64) k_sim3_draws(const Sim3ProbDev* __restrict__ probs) {
-    __shared__ uint32_t win[32];
-    const Sim3ProbDev& P = probs[blockIdx.x];
-    if (P.nhyp <= 0) return;
-    draw_sets(P.rng, P.nhyp, 3, P.N, P.raw, P.hyp_idx, win);
-}
 
 // Sim3Solver::iterate's loop (158-206) over the scored hypotheses, a wave per solver: best on
 // `>=`, return the CURRENT hypothesis as soon as it has more than mRansacMinInliers inliers.
@@ -572,7 +570,6 @@ int Sim3Batch::iterate(int n, Sim3Solver** S, int nIterations, orb_rng** rngs, S
     if (nact == 0) return 0;
     ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, pd, sizeof(Sim3ProbDev) * nact, hipMemcpyHostToDevice, s));
     const Sim3ProbDev* dprobs = (const Sim3ProbDev*)d_probs_;
-    hipLaunchKernelGGL(k_sim3_draws, dim3(nact), dim3(64), 0, s, dprobs);
     if (maxK > 0) {
         if (timing_) ORB_HIP_CHECK(hipEventRecord(ev_[0], s));
         hipLaunchKernelGGL(k_sim3_hypotheses, dim3((maxK + 63) / 64, nact), dim3(64), 0, s, dprobs);

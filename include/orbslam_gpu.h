@@ -840,7 +840,8 @@ int Optimizer_last_timings(double* ms2);
 /* Unit entry points of the BA building blocks (parity tests): the dense LDL^T
  * solve of the reduced pose system (variant 0 = register-resident panel kernel,
  * n <= 127; 1 = generic kernel; 2 / 3 = block-sparse tiled, natural / nested-dissection order;
- * 4 = row-owner kernel, n <= 96; 5 / 6 = column-owner / row-lane kernel, n <= 96) and
+ * 4 = row-owner kernel, n <= 96; 5 / 6 / 7 = column-owner / row-lane / 2-D block-cyclic kernel,
+ * n <= 96) and
  * the canonical FP64 sum. */
 int orbgpu_unit_ldlt_solve(int n, const double* S, const double* b, double* x, int variant, int* ok);
 int orbgpu_unit_csum(const double* v, int n, double* out);

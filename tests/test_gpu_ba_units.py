@@ -48,7 +48,7 @@ def _spd(rng, n):
     return S
 
 
-@pytest.mark.parametrize("variant", [0, 1, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 4, 5, 6, 7])
 @pytest.mark.parametrize("n", [1, 2, 5, 6, 12, 60, 63, 64, 65, 66, 84, 90, 95, 96, 97, 126, 127, 128])
 def test_ldlt_matches_oracle(gpu, n, variant):
     from c_orb_slam_amd._lib import lib
@@ -64,7 +64,7 @@ def test_ldlt_matches_oracle(gpu, n, variant):
     if variant == 0 and n >= 128:   # the register solver keeps b in column n: n <= 127 (the product's n <= 126)
         assert rc != 0
         return
-    if variant in (4, 5, 6) and n > 96:   # the row- / column-owner / row-lane solvers: n <= 96
+    if variant in (4, 5, 6, 7) and n > 96:   # the row- / column-owner / row-lane / 2-D solvers: n <= 96
         assert rc != 0
         return
     assert rc == 0
@@ -180,7 +180,7 @@ def test_ldlt_zero_pivot_fails(gpu):
     S[7, 7] = 0.0
     x = np.zeros(12)
     ok = C.c_int(5)
-    for variant in (0, 1, 4, 5, 6):
+    for variant in (0, 1, 4, 5, 6, 7):
         assert lib().orbgpu_unit_ldlt_solve(12, ptr(S), ptr(np.ones(12)), ptr(x), variant, C.byref(ok)) == 0
         assert ok.value == 0
 

@@ -9,7 +9,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$R" || exit 1
 export TMPDIR=/tmp
-[ -x tools/micro/ldlt_col ] && { timeout -k 10 60 ./tools/micro/ldlt_col | tee "$OUT/micro_ldlt_col.txt" || exit 1; }
+# (phase microbenchmark: tools/micro/ldlt_col.hip)
 timeout -k 10 600 python -u -m pytest tests/test_gpu_ba_units.py tests/test_gpu_ba.py tests/test_gpu_ba_g2o_order.py tests/test_gpu_ba_struct.py tests/test_gpu_pnp.py tests/test_gpu_sim3.py tests/test_gpu_stereo.py -x -q --timeout 200 --timeout-method thread > "$OUT/pytest_ba.txt" 2>&1 \
   || { tail -40 "$OUT/pytest_ba.txt"; exit 1; }
 tail -1 "$OUT/pytest_ba.txt"
@@ -18,7 +18,7 @@ python3 -c "
 import json,sys; d=json.load(open(sys.argv[1]))
 for kd in ('pnp','sim3'):
     for k,v in d[kd].items(): print(kd, k, v['device_hyp_per_s'], v['wall_hyp_per_s'], v['wall_over_device'], v['ms_call_wall'])" "$OUT/ransac.json"
-for v in reg col t; do
+for v in reg 2d; do
   ORBGPU_LDLT_DENSE=$v timeout -k 10 200 python tools/ba_timing.py 30 > "$OUT/ba_timing_$v.txt" 2>&1 || { tail -20 "$OUT/ba_timing_$v.txt"; exit 1; }
   echo "dense=$v"; tail -2 "$OUT/ba_timing_$v.txt"
 done
