@@ -1013,6 +1013,10 @@ def main():
     # peak"): the ready lane's ComputeStereoMatches and SearchByProjection batches and a dense
     # 1200x1200 descriptor tile per frame pair (SURVEY config 2 (ii)) through the CSR engine,
     # each ROOFLINE_REPS times with nothing else in flight, HIP events on the matcher stream
+    if args.stereo_batch:
+        # the roofline pass above left the shared [lefts | rights] extractor's last batch at the B
+        # left images: extract the lane's stereo batch again for the matcher passes
+        lanes[0].extract()
     mroof = matcher_pass(lanes[0], ROOFLINE_REPS)
     roof = pose_roofline(mroof["k_pose_opt"], roof_fast)
     if args.passes_only:
