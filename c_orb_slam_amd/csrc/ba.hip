@@ -1760,6 +1760,21 @@ static int pose_wide_max() {
     return v;
 }
 
+// Opt-in (ORBGPU_POSE_LDS_KB=n): reserve n KiB of LDS per pose workgroup in the chained batch
+// launch, so that the extraction grids' LDS-staged kernels cannot share the CUs the pose
+// workgroups run on (dynamic bytes added on top of the kernel's static LDS)
+static size_t pose_lds_pad(const void* fn) {
+    static const int kb = [] {
+        const char* e = getenv("ORBGPU_POSE_LDS_KB");
+        return e ? atoi(e) : 0;
+    }();
+    if (kb <= 0) return 0;
+    hipFuncAttributes a;
+    if (hipFuncGetAttributes(&a, fn) != hipSuccess) return 0;
+    const size_t want = (size_t)std::min(kb, 160) * 1024;
+    return want > a.sharedSizeBytes ? want - a.sharedSizeBytes : 0;
+}
+
 // Canonical totals (ora_csum level 2) of the m chunk trees cs[q][0..m) of K sums, by wave 0:
 // lane c holds chunk c and the K trees run packed (the same pairing as local_csum_inplace).
 // K = 28 is split over waves 0-3, 7 trees each (every value's packed tree is the canonical one
@@ -2657,10 +2672,12 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
     hipLaunchKernelGGL(k_pose_pack, dim3(count), dim3(kPackThreads), 0, st, dp, dE);
     if (timing_) ORB_HIP_CHECK(hipEventRecord(tA_, st));
     if (count <= pose_wide_max())
-        hipLaunchKernelGGL(k_pose_opt<kPoseThreadsWide>, dim3(count), dim3(kPoseThreadsWide), 0, st, dp, (const PoseEdgeDev*)dE, nullptr,
-                           (uint8_t*)(d + bProb + bEdge));
+        hipLaunchKernelGGL(k_pose_opt<kPoseThreadsWide>, dim3(count), dim3(kPoseThreadsWide),
+                           pose_lds_pad((const void*)k_pose_opt<kPoseThreadsWide>), st, dp, (const PoseEdgeDev*)dE,
+                           nullptr, (uint8_t*)(d + bProb + bEdge));
     else
-        hipLaunchKernelGGL(k_pose_opt<kPoseThreads>, dim3(count), dim3(kPoseThreads), 0, st, dp, (const PoseEdgeDev*)dE, nullptr,
+        hipLaunchKernelGGL(k_pose_opt<kPoseThreads>, dim3(count), dim3(kPoseThreads),
+                           pose_lds_pad((const void*)k_pose_opt<kPoseThreads>), st, dp, (const PoseEdgeDev*)dE, nullptr,
                            (uint8_t*)(d + bProb + bEdge));
     ORB_HIP_CHECK(hipGetLastError());
     if (timing_) {

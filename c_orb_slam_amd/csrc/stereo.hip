@@ -98,11 +98,17 @@ __device__ __forceinline__ unsigned group_min_u(unsigned v) {
 // row candidates 16 at a time, the 121 window pixels 8 per lane, the SADs as group sums.  All
 // reductions are integer minima / sums, so the result does not depend on the lane mapping.
 __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restrict__ probs, StereoParams P,
-                                                      unsigned long long* counters) {
+                                                      unsigned long long* counters, int np, int gx) {
     ORBGPU_LATENCY_WAVE();
-    const StereoDev& S = probs[blockIdx.y];
+    // XCD-aware order (workgroups L and L + 8 share an XCD): every workgroup of a pair runs on one
+    // XCD, so the pair's right keypoints and descriptors, which all its left keypoints scan, and
+    // its pyramid rows are fetched into one L2
+    const int xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
+    const int by = xcd + 8 * (slot / gx), bx = slot % gx;
+    if (by >= np) return;
+    const StereoDev& S = probs[by];
     const int sub = threadIdx.x & 15;
-    const int iL = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int iL = bx * 16 + (threadIdx.x >> 4);
     if (iL >= S.NL) return;   // the whole group
     const orb_kp_dev kpL = S.kL[iL];
     float uR_out = -1.0f, depth_out = -1.0f;
@@ -138,7 +144,7 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
         if (counters) {   // measurement: scored (left, right) pairs and searched left keypoints
             const int tot = group_sum_i(scored);
             if (sub == 0) {   // spread over kCountSlots addresses: one per group would serialise
-                const int sl = (blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 4)) & (kCountSlots - 1);
+                const int sl = (bx + by * 7 + (threadIdx.x >> 4)) & (kCountSlots - 1);
                 atomicAdd(&counters[2 * kCountSlots + sl], (unsigned long long)tot);
                 atomicAdd(&counters[3 * kCountSlots + sl], 1ull);
             }
@@ -156,8 +162,8 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
             const float iniu = scaleduR0 + L - w, endu = scaleduR0 + L + w + 1;
             if (!(iniu < 0 || endu >= lv.w)) {
                 if (counters && sub == 0)   // measurement: keypoints whose SAD windows are read
-                    atomicAdd(&counters[7 * kCountSlots + ((blockIdx.x + blockIdx.y * 7 + (threadIdx.x >> 4)) &
-                                                           (kCountSlots - 1))], 1ull);
+                    atomicAdd(&counters[7 * kCountSlots + ((bx + by * 7 + (threadIdx.x >> 4)) & (kCountSlots - 1))],
+                              1ull);
                 const uint8_t* IL = S.pyrL + lv.off + (size_t)kEdge * lv.pitch + kEdge;
                 const uint8_t* IR = S.pyrR + lv.off + (size_t)kEdge * lv.pitch + kEdge;
                 const int yL = (int)scaledvL, xL = (int)scaleduL, xR0 = (int)scaleduR0;
@@ -317,8 +323,8 @@ int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoPa
     hipLaunchKernelGGL(k_stereo_rows, dim3(nprob), dim3(1024), 0, s, d_probs, P);
     if (timed) tm->mark(5);
     if (maxNL > 0)
-        hipLaunchKernelGGL(k_stereo_match, dim3((maxNL + 15) / 16, nprob), dim3(256), 0, s, d_probs, P,
-                           timed ? tm->counters() : nullptr);
+        hipLaunchKernelGGL(k_stereo_match, dim3(8 * ((maxNL + 15) / 16) * ((nprob + 7) / 8)), dim3(256), 0, s, d_probs, P,
+                           timed ? tm->counters() : nullptr, nprob, (maxNL + 15) / 16);
     if (timed) tm->mark(6);
     hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(256), 0, s, d_probs);
     if (timed) tm->mark(7);
