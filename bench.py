@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--lanes", type=int, default=2,
                     help="batches in flight (buffer sets): extraction of batch k waits for the tracking chain "
                          "of batch k - lanes, which last used its buffers")
+    ap.add_argument("--lane-matchers", type=int, default=1,
+                    help="1 (default): every lane after the first tracks on its own ORBmatcher (own stream, "
+                         "arena and deferred chain), so the tracking chains of consecutive batches overlap on "
+                         "the device instead of queueing on one stream (32.3-32.5k vs 29.6-29.7k frames/s with "
+                         "0, profiles/r04n_lanes_ab.txt); 0: one matcher for every lane")
     ap.add_argument("--stereo-batch", type=int, default=1,
                     help="1 (default): Frame(imLeft, imRight)'s two extractions as ONE batch call of 2B images on "
                          "one extractor stream (ComputeStereoMatches_batch_at pairs image b with image B + b; "
@@ -282,7 +287,15 @@ def main():
         Twc), block b of a (B x cap) table; the local map of pair p (current frame p+1) is the blocks
         of frames max(0, p-K+1)..p, contiguous in the table (UpdateLocalMap's local keyframes)."""
 
-        def __init__(self):
+        def __init__(self, first):
+            # the lane's matcher: the shared one, or (--lane-matchers) its own for every lane but the
+            # first, whose chains then run beside the other lanes' on their own streams
+            if first or not args.lane_matchers:
+                self.m, self.ms = m, match_stream
+            else:
+                self.m = orb.ORBmatcher(0.9, True)
+                check(L.ORBmatcher_set_device_pointers(self.m._h, 1))
+                self.ms = torch.cuda.ExternalStream(L.ORBmatcher_stream(self.m._h), device=dev)
             if args.stereo_batch:   # one extractor, one stream: [lefts | rights] as one batch of 2B images
                 self.exL = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=2 * B)
                 self.exR = self.exL
@@ -408,7 +421,7 @@ def main():
             # lane's buffers may still be read by the tracking chain of its previous batch: wait
             # for that chain's device work first (not for its counts)
             if self.epoch:
-                check(L.ORBmatcher_chain_wait(m._h, self.epoch), "ORBmatcher_chain_wait")
+                check(L.ORBmatcher_chain_wait(self.m._h, self.epoch), "ORBmatcher_chain_wait")
             if args.stereo_batch:
                 n = np.ascontiguousarray(self.exL.extract_device(d_LR.data_ptr(), 2 * B, W, H, W, W * H,
                                                                  self.d_kps_all.data_ptr(), self.d_desc_all.data_ptr(),
@@ -429,7 +442,7 @@ def main():
 
         def stereo(self):
             nL, nR = self.nL, self.nR
-            check(L.ORBmatcher_ComputeStereoMatches_batch_at(m._h, self.exL._h, 0, self.exR._h,
+            check(L.ORBmatcher_ComputeStereoMatches_batch_at(self.m._h, self.exL._h, 0, self.exR._h,
                                                              B if args.stereo_batch else 0, B, ptr(nL), self.s_kL,
                                                              self.s_dL, ptr(nR), self.s_kR, self.s_dR, float(mbf),
                                                              float(mb), self.s_uR, self.s_dep, ptr(self.nst)),
@@ -446,12 +459,12 @@ def main():
             self.n_last[:] = nL[:-1]
             self.n_pose[:] = nL[1:]
             self.n_pose2[:] = nL[1:]
-            with torch.cuda.stream(match_stream):
+            with torch.cuda.stream(self.ms):
                 self.d_slot.fill_(-1)
                 self.d_cur_mp.fill_(-1)
-            check(L.MapPoint_CreateStereo_batch_device(m._h, B, self.newp), "MapPoint_CreateStereo batch")
+            check(L.MapPoint_CreateStereo_batch_device(self.m._h, B, self.newp), "MapPoint_CreateStereo batch")
             # TrackWithMotionModel: SearchByProjection(CurrentFrame, LastFrame, th=7, stereo) (Tracking.cc:869-885)
-            check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, P, self.curs, self.a_cur_mp, self.lasts,
+            check(L.ORBmatcher_SearchByProjection_LastFrame_batch(self.m._h, P, self.curs, self.a_cur_mp, self.lasts,
                                                                   self.a_last_kps, self.a_last_mp, self.a_last_out,
                                                                   self.mps, 7.0, 0, ptr(self.nm)),
                   "SearchByProjection batch")
@@ -463,12 +476,12 @@ def main():
             SearchByProjection(F, mvpLocalMapPoints, th=1) (stereo, ORBmatcher(0.8)), then the
             second PoseOptimization."""
             self.n_prep[:] = self.nL[1:]
-            check(L.Tracking_PrepareLocalSearch_batch_device(m._h, P, self.prep), "PrepareLocalSearch batch")
+            check(L.Tracking_PrepareLocalSearch_batch_device(self.m._h, P, self.prep), "PrepareLocalSearch batch")
             self.n_curl[:] = self.nL[1:]
-            check(L.ORBmatcher_SearchLocalPoints_batch(m._h, P, self.curs_local, self.a_cur_mp, self.lmaps,
+            check(L.ORBmatcher_SearchLocalPoints_batch(self.m._h, P, self.curs_local, self.a_cur_mp, self.lmaps,
                                                        float(lsf), 1.0, 0.8, ptr(self.nml), ptr(self.nvis)),
                   "SearchLocalPoints batch")
-            check(L.Optimizer_PoseOptimization_frames_device_deferred(m._h, P, self.pframes2, self.a_Tout2,
+            check(L.Optimizer_PoseOptimization_frames_device_deferred(self.m._h, P, self.pframes2, self.a_Tout2,
                                                                       self.a_poutl2, ptr(self.ninl2)),
                   "PoseOptimization (local map)")
 
@@ -481,20 +494,20 @@ def main():
             t1 = time.perf_counter()
             nL, nR = self.nL, self.nR
             self.kp_count = int(nL.sum() + nR.sum())
-            check(L.ORBmatcher_set_deferred(m._h, 1), "ORBmatcher_set_deferred")
+            check(L.ORBmatcher_set_deferred(self.m._h, 1), "ORBmatcher_set_deferred")
             self.stereo()
             t2 = time.perf_counter()
             self.search()
             t3 = time.perf_counter()
             # Optimizer::PoseOptimization(&mCurrentFrame) (Tracking.cc:887) on the matched map points
-            check(L.Optimizer_PoseOptimization_frames_device_deferred(m._h, P, self.pframes, self.a_Tout,
+            check(L.Optimizer_PoseOptimization_frames_device_deferred(self.m._h, P, self.pframes, self.a_Tout,
                                                                       self.a_poutl, ptr(self.ninl)),
                   "PoseOptimization batch")
             t4 = time.perf_counter()
             self.local_map()
             t5 = time.perf_counter()
             eid = C.c_longlong(0)
-            check(L.ORBmatcher_chain_close(m._h, C.byref(eid)), "ORBmatcher_chain_close")
+            check(L.ORBmatcher_chain_close(self.m._h, C.byref(eid)), "ORBmatcher_chain_close")
             self.epoch = eid.value
             for k, v in (("stereo", t2 - t1), ("lift+search", t3 - t2), ("pose", t4 - t3), ("local_map", t5 - t4)):
                 phase_acc[k] = phase_acc.get(k, 0.0) + v * 1e3
@@ -502,7 +515,7 @@ def main():
         def collect(self):
             """Finish this lane's chain (counts land) and book its statistics."""
             t5 = time.perf_counter()
-            check(L.ORBmatcher_chain_finish(m._h, self.epoch), "ORBmatcher_chain_finish")
+            check(L.ORBmatcher_chain_finish(self.m._h, self.epoch), "ORBmatcher_chain_finish")
             phase_acc["finish"] = phase_acc.get("finish", 0.0) + (time.perf_counter() - t5) * 1e3
             tl, tr = self.tl, self.tr
             for k in tl:
@@ -849,7 +862,7 @@ def main():
     local_acc = []
     pose_inl = []
     kernel_ms = []   # k_fast_cells duration per step (HIP events on the extractor streams)
-    lanes = [Lane() for _ in range(args.lanes)]
+    lanes = [Lane(i == 0) for i in range(args.lanes)]
     exL = lanes[0].exL
     if args.reserve_cus:
         # the tracking lane's one-workgroup-per-frame kernels (k_select, k_pose_opt) need free
@@ -892,7 +905,8 @@ def main():
         if state["pending"] is not None:
             out.append(state["pending"].collect())
             state["pending"] = None
-        check(L.ORBmatcher_set_deferred(m._h, 0), "ORBmatcher_set_deferred")
+        for ln in lanes:
+            check(L.ORBmatcher_set_deferred(ln.m._h, 0), "ORBmatcher_set_deferred")
         return out
 
     def stage_by_stream():

@@ -19,9 +19,11 @@
 // oracle) breaks them by node creation order -- DESIGN.md Appendix, quirk Q1.
 #include "octree.hpp"
 
+#include <cstdlib>
+
 namespace orbgpu {
 
-constexpr int OCT_T = 256;
+constexpr int OCT_TMAX = 1024;   // largest workgroup instance (k_octree<256|512|1024>)
 
 struct OctShared {
     int16_t x0[2 * kOctNMax], y0[2 * kOctNMax], x1[2 * kOctNMax], y1[2 * kOctNMax];
@@ -31,17 +33,18 @@ struct OctShared {
     uint16_t vpos[4 * kOctNMax];   // virtual child -> push index -> list position
     uint16_t er[kOctNMax], eidx[kOctNMax];
     uint16_t vs[kOctNMax], vs2[kOctNMax];
+    uint32_t sk[kOctNMax];         // phase-2 sort keys (size << 16 | creation order)
     uint16_t knode[kOctKMax], arena[kOctKMax], tmp[kOctKMax];
-    int wsum[OCT_T / 64];
+    int wsum[OCT_TMAX / 64];
     int head, size, nfree, m, newm, seqctr, flag;
 };
 
 // Block-wide exclusive scan of flag(i) over i < n; put(i, rank) for flagged i.  Returns the
 // total.  Every thread of the block calls it (two barriers).
-template <class Flag, class Put>
+template <int T, class Flag, class Put>
 __device__ __forceinline__ int oct_scan(int n, Flag flag, Put put, int* wsum) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const int per = (n + OCT_T - 1) / OCT_T;
+    const int per = (n + T - 1) / T;
     const int a = min(n, t * per), e = min(n, a + per);
     int local = 0;
     for (int i = a; i < e; i++) local += flag(i) ? 1 : 0;
@@ -55,7 +58,7 @@ __device__ __forceinline__ int oct_scan(int n, Flag flag, Put put, int* wsum) {
     __syncthreads();
     int off = 0, total = 0;
 #pragma unroll
-    for (int w = 0; w < OCT_T / 64; w++) {
+    for (int w = 0; w < T / 64; w++) {
         const int s = wsum[w];
         if (w < wid) off += s;
         total += s;
@@ -69,10 +72,10 @@ __device__ __forceinline__ int oct_scan(int n, Flag flag, Put put, int* wsum) {
 
 // Block-wide exclusive scan of val(i) over i < n; put(i, prefix) for every i.  Returns the
 // total.  Every thread of the block calls it (two barriers).
-template <class Val, class Put>
+template <int T, class Val, class Put>
 __device__ __forceinline__ int oct_scan_val(int n, Val val, Put put, int* wsum) {
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const int per = (n + OCT_T - 1) / OCT_T;
+    const int per = (n + T - 1) / T;
     const int a = min(n, t * per), e = min(n, a + per);
     int local = 0;
     for (int i = a; i < e; i++) local += val(i);
@@ -86,7 +89,7 @@ __device__ __forceinline__ int oct_scan_val(int n, Val val, Put put, int* wsum) 
     __syncthreads();
     int off = 0, total = 0;
 #pragma unroll
-    for (int w = 0; w < OCT_T / 64; w++) {
+    for (int w = 0; w < T / 64; w++) {
         const int s = wsum[w];
         if (w < wid) off += s;
         total += s;
@@ -120,11 +123,13 @@ __device__ __forceinline__ int oct_quadrant(const OctShared& S, int p, uint32_t 
 
 __device__ __forceinline__ int oct_best_key(uint32_t pk, int k) { return (int)((pk >> 24) << 16) | (0xffff - k); }
 
-__global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ packed, const int* __restrict__ hdr,
+template <int T>
+__global__ void __launch_bounds__(T) k_octree(const uint32_t* __restrict__ packed, const int* __restrict__ hdr,
                                                  int nlevels, const OctLevelDev* __restrict__ lv,
                                                  uint32_t* __restrict__ jobsel, int* __restrict__ jobcnt, int jcap,
                                                  uint16_t* __restrict__ gscratch, size_t gstride, int* __restrict__ err) {
     __shared__ OctShared S;
+    ORBGPU_PROF_START;
     const int job = blockIdx.x, b = job / nlevels, l = job - b * nlevels;
     const int tid = threadIdx.x;
     const int* H = hdr + (size_t)b * (nlevels + 2);
@@ -163,9 +168,9 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
         return;
     }
     const float hX = (float)W / (float)nIni;
-    for (int i = tid; i < nIni; i += OCT_T) S.ia[i] = 0;
+    for (int i = tid; i < nIni; i += T) S.ia[i] = 0;
     __syncthreads();
-    for (int k = tid; k < n; k += OCT_T) {
+    for (int k = tid; k < n; k += T) {
         const uint32_t pk = src[k];
         int ib = (int)((float)(pk & 0xfff) / hX);
         ib = min(ib, nIni - 1);
@@ -175,7 +180,7 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
     __syncthreads();
     // list = non-empty initial nodes in order (buffer 0), node id == position
     int cur = 0;
-    int Sz = oct_scan(
+    int Sz = oct_scan<T>(
         nIni, [&](int i) { return S.ia[i] > 0; },
         [&](int i, int r) {
             S.x0[r] = (int16_t)(int)(hX * (float)i);
@@ -187,24 +192,26 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
             S.er[i] = (uint16_t)r;
         },
         S.wsum);
-    for (int k = tid; k < n; k += OCT_T) knode[k] = S.er[knode[k]];
+    for (int k = tid; k < n; k += T) knode[k] = S.er[knode[k]];
     int seqbase = nIni;
     int phase2 = 0, m = 0;
     __syncthreads();
+    ORBGPU_PROF_MARK(0);   // initial nodes
     // ---- phase 1 (ORBextractor.cc:594-673)
     for (;;) {
         const int prevSize = Sz;
-        const int nE = oct_scan(
+        const int nE = oct_scan<T>(
             Sz, [&](int i) { return S.cnt[cur + i] > 1; },
             [&](int i, int r) {
                 S.er[i] = (uint16_t)r;
                 S.eidx[r] = (uint16_t)i;
             },
             S.wsum);
+        ORBGPU_PROF_COUNT(9);
         if (nE == 0) break;   // every node holds one key: size == prevSize
-        for (int v = tid; v < 4 * nE; v += OCT_T) S.ia[v] = 0;
+        for (int v = tid; v < 4 * nE; v += T) S.ia[v] = 0;
         __syncthreads();
-        for (int k = tid; k < n; k += OCT_T) {
+        for (int k = tid; k < n; k += T) {
             const int p = knode[k];
             if (S.cnt[cur + p] > 1) {
                 const int v = 4 * S.er[p] + oct_quadrant(S, cur + p, src[k]);
@@ -216,11 +223,11 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
         }
         __syncthreads();
         // push order of the non-empty children: parents in list order, n1..n4
-        const int nC = oct_scan(
+        const int nC = oct_scan<T>(
             4 * nE, [&](int v) { return S.ia[v] > 0; }, [&](int v, int r) { S.vpos[v] = (uint16_t)r; }, S.wsum);
         const int nb = kOctNMax - cur;
         // 1-key nodes keep their relative order behind the children
-        const int nNM = oct_scan(
+        const int nNM = oct_scan<T>(
             Sz, [&](int i) { return S.cnt[cur + i] == 1; }, [&](int i, int r) { S.er[i] = (uint16_t)(nC + r); },
             S.wsum);
         if (nC + nNM > kOctNMax) {
@@ -230,7 +237,7 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
             }
             return;
         }
-        for (int v = tid; v < 4 * nE; v += OCT_T) {
+        for (int v = tid; v < 4 * nE; v += T) {
             const int c = S.ia[v];
             if (c > 0) {
                 const int t = S.vpos[v], pos = nC - 1 - t, parent = cur + S.eidx[v >> 2];
@@ -245,7 +252,7 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
                 S.vpos[v] = (uint16_t)pos;
             }
         }
-        for (int i = tid; i < Sz; i += OCT_T)
+        for (int i = tid; i < Sz; i += T)
             if (S.cnt[cur + i] == 1) {
                 const int pos = S.er[i];
                 S.x0[nb + pos] = S.x0[cur + i];
@@ -257,10 +264,10 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
             }
         __syncthreads();
         // vSizeAndPointerToNode: children with > 1 key, push order
-        const int nToExpand = oct_scan(
+        const int nToExpand = oct_scan<T>(
             4 * nE, [&](int v) { return S.ia[v] > 1; }, [&](int v, int r) { S.vs[r] = (uint16_t)S.vpos[v]; },
             S.wsum);
-        for (int k = tid; k < n; k += OCT_T) {
+        for (int k = tid; k < n; k += T) {
             const int v = tmp[k];
             knode[k] = v != 0xffff ? S.vpos[v] : S.er[knode[k]];
         }
@@ -275,21 +282,21 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
             break;
         }
     }
+    ORBGPU_PROF_MARK(1);   // phase 1
     if (phase2) {
         // ---- phase 2 (ORBextractor.cc:673-738): arena slices, linked list, largest first
         const int nb = kOctNMax - cur;
-        // kbeg = exclusive scan of cnt in list order
+        // kbeg = exclusive scan of cnt in list order; the list linked in position order
         {
-            // small serial scan by thread 0 (Sz <= kOctNMax)
+            oct_scan_val<T>(
+                Sz, [&](int i) { return (int)S.cnt[cur + i]; }, [&](int i, int ex) { S.kbeg[cur + i] = (uint16_t)ex; },
+                S.wsum);
+            for (int i = tid; i < Sz; i += T) {
+                S.ia[i] = 0;
+                S.prv[cur + i] = (int16_t)(i > 0 ? cur + i - 1 : -1);
+                S.nxt[cur + i] = (int16_t)(i + 1 < Sz ? cur + i + 1 : -1);
+            }
             if (tid == 0) {
-                int acc = 0;
-                for (int i = 0; i < Sz; i++) {
-                    S.kbeg[cur + i] = (uint16_t)acc;
-                    acc += S.cnt[cur + i];
-                    S.ia[i] = 0;
-                    S.prv[cur + i] = (int16_t)(i > 0 ? cur + i - 1 : -1);
-                    S.nxt[cur + i] = (int16_t)(i + 1 < Sz ? cur + i + 1 : -1);
-                }
                 S.head = Sz > 0 ? cur : -1;
                 S.size = Sz;
                 S.nfree = nb;
@@ -297,39 +304,42 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
                 S.m = m;
                 S.flag = 0;
             }
-            for (int i = tid; i < m; i += OCT_T) S.vs[i] = (uint16_t)(cur + S.vs[i]);
+            for (int i = tid; i < m; i += T) S.vs[i] = (uint16_t)(cur + S.vs[i]);
             __syncthreads();
-            for (int k = tid; k < n; k += OCT_T) {
+            for (int k = tid; k < n; k += T) {
                 const int p = knode[k];
                 arena[S.kbeg[cur + p] + atomicAdd(&S.ia[p], 1)] = (uint16_t)k;
             }
             __syncthreads();
         }
+        ORBGPU_PROF_MARK(2);   // phase-2 set-up
         for (;;) {
+            ORBGPU_PROF_COUNT(8);
             const int prevSize = S.size;
             const int mm = S.m;
             // sort ascending by (size, creation order): rank sort, keys unique
-            for (int i = tid; i < mm; i += OCT_T) {
+            for (int i = tid; i < mm; i += T) {
                 const int id = S.vs[i];
-                const uint32_t ki = ((uint32_t)S.cnt[id] << 16) | S.seq[id];
-                int r = 0;
-                for (int j = 0; j < mm; j++) {
-                    const int jd = S.vs[j];
-                    const uint32_t kj = ((uint32_t)S.cnt[jd] << 16) | S.seq[jd];
-                    r += kj < ki ? 1 : 0;
-                }
-                S.vs2[r] = (uint16_t)id;
+                S.sk[i] = ((uint32_t)S.cnt[id] << 16) | S.seq[id];
             }
-            for (int i = tid; i < 4 * mm; i += OCT_T) S.ia[i] = 0;
+            __syncthreads();
+            for (int i = tid; i < mm; i += T) {
+                const uint32_t ki = S.sk[i];
+                int r = 0;
+                for (int j = 0; j < mm; j++) r += S.sk[j] < ki ? 1 : 0;
+                S.vs2[r] = S.vs[i];
+            }
+            for (int i = tid; i < 4 * mm; i += T) S.ia[i] = 0;
             if (tid == 0) S.newm = 0;
             __syncthreads();
+            ORBGPU_PROF_MARK(3);   // rank sort
             // The round's divides (largest first, ORBextractor.cc:700-736) are sequential only in
             // their bookkeeping (push_front order, node ids, the size >= N stop): the keys of
             // every node of the round are partitioned into its quadrants at once.  A node the
             // stop leaves undivided keeps its key SET (its slice is only reordered, and every
             // later use of a slice is order-free: best key = max response, then min index).
             // er[j] = first flattened key position of vs2[j]
-            const int tot = oct_scan_val(
+            const int tot = oct_scan_val<T>(
                 mm, [&](int j) { return (int)S.cnt[S.vs2[j]]; }, [&](int j, int ex) { S.er[j] = (uint16_t)ex; },
                 S.wsum);
             auto owner = [&](int t) {   // largest j with er[j] <= t
@@ -341,18 +351,19 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
                 }
                 return lo;
             };
-            for (int t = tid; t < tot; t += OCT_T) {
+            // (flattened position t: its key in tmp[t], its (node, quadrant) in knode[t])
+            for (int t = tid; t < tot; t += T) {
                 const int j = owner(t), p = S.vs2[j], pos = S.kbeg[p] + (t - S.er[j]);
                 const int k = arena[pos];
                 const int q = oct_quadrant(S, p, src[k]);
-                tmp[pos] = (uint16_t)k;
-                knode[pos] = (uint16_t)q;
+                tmp[t] = (uint16_t)k;
+                knode[t] = (uint16_t)(4 * j + q);
                 atomicAdd(&S.ia[4 * j + q], 1);
             }
             __syncthreads();
             // quadrant starts inside each node's slice (children n1..n4 take consecutive
             // sub-slices); ia becomes the scatter cursors
-            for (int j = tid; j < mm; j += OCT_T) {
+            for (int j = tid; j < mm; j += T) {
                 int start = S.kbeg[S.vs2[j]];
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
@@ -362,23 +373,30 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
                 }
             }
             __syncthreads();
-            for (int t = tid; t < tot; t += OCT_T) {
-                const int j = owner(t), p = S.vs2[j], pos = S.kbeg[p] + (t - S.er[j]);
-                const int q = knode[pos];
-                arena[S.vpos[4 * j + q] + atomicAdd(&S.ia[4 * j + q], 1)] = tmp[pos];
+            for (int t = tid; t < tot; t += T) {
+                const int v = knode[t];
+                arena[S.vpos[v] + atomicAdd(&S.ia[v], 1)] = tmp[t];
             }
             __syncthreads();
+            ORBGPU_PROF_MARK(4);   // key partition
             // the reference's sequential loop over the round's nodes: children pushed to the
             // front (n1..n4), the parent erased, stop as soon as the list reaches N
+            // (list scalars in registers; an erased node is marked prv = -2)
             if (tid == 0) {
+                int head = S.head, size = S.size, nfree = S.nfree, seqctr = S.seqctr, newm = 0, flag = 0;
                 for (int j = mm - 1; j >= 0; j--) {
                     const int p = S.vs2[j];
+                    int c4[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) c4[q] = S.ia[4 * j + q];
                     for (int q = 0; q < 4; q++) {
-                        const int c = S.ia[4 * j + q];
+                        const int c = c4[q];
                         if (c > 0) {
-                            const int id = S.nfree++;
-                            if (S.nfree > 2 * kOctNMax || id == cur) S.flag = 1;
-                            if (S.flag) break;
+                            const int id = nfree++;
+                            if (nfree > 2 * kOctNMax || id == cur) {
+                                flag = 1;
+                                break;
+                            }
                             int a0, b0, a1, b1;
                             oct_child_rect(S, p, q, a0, b0, a1, b1);
                             S.x0[id] = (int16_t)a0;
@@ -386,28 +404,36 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
                             S.x1[id] = (int16_t)a1;
                             S.y1[id] = (int16_t)b1;
                             S.cnt[id] = (uint16_t)c;
-                            S.seq[id] = (uint16_t)(S.seqctr++);
+                            S.seq[id] = (uint16_t)(seqctr++);
                             S.kbeg[id] = S.vpos[4 * j + q];
                             // lNodes.push_front
                             S.prv[id] = -1;
-                            S.nxt[id] = (int16_t)S.head;
-                            if (S.head >= 0) S.prv[S.head] = (int16_t)id;
-                            S.head = id;
-                            S.size++;
-                            if (c > 1) S.vs[S.newm++] = (uint16_t)id;
+                            S.nxt[id] = (int16_t)head;
+                            if (head >= 0) S.prv[head] = (int16_t)id;
+                            head = id;
+                            size++;
+                            if (c > 1) S.vs[newm++] = (uint16_t)id;
                         }
                     }
-                    if (S.flag) break;
+                    if (flag) break;
                     // lNodes.erase(parent)
                     const int pp = S.prv[p], pn = S.nxt[p];
                     if (pp >= 0) S.nxt[pp] = (int16_t)pn;
-                    else S.head = pn;
+                    else head = pn;
                     if (pn >= 0) S.prv[pn] = (int16_t)pp;
-                    S.size--;
-                    if (S.size >= N) break;
+                    S.prv[p] = -2;
+                    size--;
+                    if (size >= N) break;
                 }
+                S.head = head;
+                S.size = size;
+                S.nfree = nfree;
+                S.seqctr = seqctr;
+                S.newm = newm;
+                S.flag = flag;
             }
             __syncthreads();
+            ORBGPU_PROF_MARK(5);   // serial list update
             if (S.flag) {
                 if (tid == 0) {
                     jobcnt[job] = 0;
@@ -419,14 +445,17 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
             if (tid == 0) S.m = S.newm;
             __syncthreads();
         }
-        // final list order, then the best key of each node over its slice
-        if (tid == 0) {
-            int i = 0;
-            for (int id = S.head; id >= 0 && i < 2 * kOctNMax; id = S.nxt[id]) S.vpos[i++] = (uint16_t)id;
-            S.size = i;
-        }
-        __syncthreads();
-        const int sz = S.size;
+        // final list order: every divide pushed its children to the front, so the list is the
+        // live phase-2 nodes newest first (ids nfree-1 down to nb), then the live nodes phase 1
+        // left (ids cur.. in list position order)
+        const int n2 = S.nfree - nb;
+        const int sz = oct_scan<T>(
+            n2 + Sz,
+            [&](int u) {
+                const int id = u < n2 ? nb + n2 - 1 - u : cur + (u - n2);
+                return S.prv[id] != -2;
+            },
+            [&](int u, int r) { S.vpos[r] = (uint16_t)(u < n2 ? nb + n2 - 1 - u : cur + (u - n2)); }, S.wsum);
         if (sz > jcap) {
             if (tid == 0) {
                 jobcnt[job] = 0;
@@ -434,21 +463,27 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
             }
             return;
         }
-        for (int i = tid; i < sz; i += OCT_T) {
+        // the best key of each node over its slice (max response, then min index): the live
+        // slices partition the arena, so each position names its node (tmp) and the keys
+        // meet in one atomic max per node
+        for (int i = tid; i < sz; i += T) {
             const int id = S.vpos[i];
             const int kb = S.kbeg[id], kc = S.cnt[id];
-            int best = -1, bk = 0;
-            for (int t = 0; t < kc; t++) {
-                const int k = arena[kb + t];
-                const int v = oct_best_key(src[k], k);
-                if (v > best) {
-                    best = v;
-                    bk = k;
-                }
-            }
-            jobsel[(size_t)job * jcap + i] = src[bk];
+            for (int t = 0; t < kc; t++) tmp[kb + t] = (uint16_t)i;
+            S.ia[i] = -1;
+        }
+        __syncthreads();
+        for (int pos = tid; pos < n; pos += T) {
+            const int k = arena[pos];
+            atomicMax(&S.ia[tmp[pos]], oct_best_key(src[k], k));
+        }
+        __syncthreads();
+        for (int i = tid; i < sz; i += T) {
+            const int k = 0xffff - (S.ia[i] & 0xffff);
+            jobsel[(size_t)job * jcap + i] = src[k];
         }
         if (tid == 0) jobcnt[job] = sz;
+        ORBGPU_PROF_MARK(6);   // final walk + best keys
         return;
     }
     // ---- phase 1 finished: list = positions 0..Sz-1 of buffer `cur`
@@ -459,15 +494,16 @@ __global__ void __launch_bounds__(OCT_T) k_octree(const uint32_t* __restrict__ p
         }
         return;
     }
-    for (int i = tid; i < Sz; i += OCT_T) S.ia[i] = -1;
+    for (int i = tid; i < Sz; i += T) S.ia[i] = -1;
     __syncthreads();
-    for (int k = tid; k < n; k += OCT_T) atomicMax(&S.ia[knode[k]], oct_best_key(src[k], k));
+    for (int k = tid; k < n; k += T) atomicMax(&S.ia[knode[k]], oct_best_key(src[k], k));
     __syncthreads();
-    for (int i = tid; i < Sz; i += OCT_T) {
+    for (int i = tid; i < Sz; i += T) {
         const int k = 0xffff - (S.ia[i] & 0xffff);
         jobsel[(size_t)job * jcap + i] = src[k];
     }
     if (tid == 0) jobcnt[job] = Sz;
+    ORBGPU_PROF_MARK(7);   // phase-1 best keys
 }
 
 // Per image: level-major concatenation of the job lists -> (packed, b<<20 | l<<16 | k) at
@@ -497,11 +533,37 @@ __global__ void __launch_bounds__(64) k_sel_build(const uint32_t* __restrict__ j
     }
 }
 
+int octree_prof_read(unsigned long long* out16) {
+#ifdef ORBGPU_PROF
+    unsigned long long v[32];
+    ORB_HIP_CHECK(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_orbgpu_prof), sizeof(v)));
+    for (int i = 0; i < 16; i++) out16[i] = v[i];
+    unsigned long long z[32] = {};
+    ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_orbgpu_prof), z, sizeof(z)));
+    return 0;
+#else
+    (void)out16;
+    return -1;
+#endif
+}
+
 int octree_launch(const uint32_t* packed, const int* hdr, int B, int nlevels, const OctLevelDev* lv, uint32_t* jobsel,
                   int* jobcnt, int jcap, uint16_t* gscratch, size_t gstride, int cap, int2* sel, int selcap, int* nout,
                   int* err, hipStream_t s) {
-    hipLaunchKernelGGL(k_octree, dim3(B * nlevels), dim3(OCT_T), 0, s, packed, hdr, nlevels, lv, jobsel, jobcnt, jcap,
-                       gscratch, gstride, err);
+    static const int nt = [] {
+        const char* e = getenv("ORBGPU_OCT_T");
+        const int v = e ? atoi(e) : 256;
+        return v == 512 || v == 1024 ? v : 256;
+    }();
+    if (nt == 1024)
+        hipLaunchKernelGGL(k_octree<1024>, dim3(B * nlevels), dim3(1024), 0, s, packed, hdr, nlevels, lv, jobsel, jobcnt,
+                           jcap, gscratch, gstride, err);
+    else if (nt == 512)
+        hipLaunchKernelGGL(k_octree<512>, dim3(B * nlevels), dim3(512), 0, s, packed, hdr, nlevels, lv, jobsel, jobcnt,
+                           jcap, gscratch, gstride, err);
+    else
+        hipLaunchKernelGGL(k_octree<256>, dim3(B * nlevels), dim3(256), 0, s, packed, hdr, nlevels, lv, jobsel, jobcnt,
+                           jcap, gscratch, gstride, err);
     hipLaunchKernelGGL(k_sel_build, dim3(B), dim3(64), 0, s, (const uint32_t*)jobsel, (const int*)jobcnt, nlevels,
                        jcap, cap, sel, selcap, nout, err);
     ORB_HIP_CHECK(hipGetLastError());

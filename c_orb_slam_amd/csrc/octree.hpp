@@ -18,6 +18,9 @@ struct OctLevelDev {   // DistributeOctTree(vToDistributeKeys, minX, maxX, minY,
 // k_octree over B * nlevels jobs, then k_sel_build: sel[b * selcap + k] = (packed, b<<20|l<<16|k),
 // nout[b].  err bits: 1 capacity (cap / selcap), 2 > 65535 keys, 4 bad geometry, 8 node pool,
 // 16 job capacity.
+// instrumented builds (make prof): k_octree section cycles of job 0 into out16, then reset
+int octree_prof_read(unsigned long long* out16);
+
 int octree_launch(const uint32_t* packed, const int* hdr, int B, int nlevels, const OctLevelDev* lv, uint32_t* jobsel,
                   int* jobcnt, int jcap, uint16_t* gscratch, size_t gstride, int cap, int2* sel, int selcap, int* nout,
                   int* err, hipStream_t s);

@@ -737,6 +737,10 @@ void Extractor::release() {
     for (auto& e : ev_) e = nullptr;
     if (stream_) (void)hipStreamDestroy(stream_);
     stream_ = nullptr;
+    if (evBlur_) (void)hipEventDestroy(evBlur_);
+    evBlur_ = nullptr;
+    if (side_) (void)hipStreamDestroy(side_);
+    side_ = nullptr;
 }
 
 int Extractor::init_device(int maxW, int maxH, int maxBatch) {
@@ -744,6 +748,10 @@ int Extractor::init_device(int maxW, int maxH, int maxBatch) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -4;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     for (auto& e : ev_) ORB_HIP_CHECK(hipEventCreate(&e));
+    if (const char* e = getenv("ORBGPU_BLUR_SIDE"); e && atoi(e) > 0) {
+        ORB_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+        ORB_HIP_CHECK(hipEventCreateWithFlags(&evBlur_, hipEventDisableTiming));
+    }
     static bool consts_done = false;  // per process; guarded by first-use in create
     if (!consts_done) {
         ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kPattern, sizeof(kPattern)));
@@ -1184,6 +1192,12 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     }
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
+    if (side_) {
+        ORB_HIP_CHECK(hipStreamWaitEvent(side_, ev_[1], 0));
+        hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, side_, (const uint8_t*)d_pyr_,
+                           (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_, (int)tiles_.size());
+        ORB_HIP_CHECK(hipEventRecord(evBlur_, side_));
+    }
     // 2. FAST per cell (the blur, which only the descriptors read, runs after the octree: the
     //    VALU-heavy FAST grid then overlaps the tracking lane's matching, and the HBM-bound
     //    blur its FP64 PoseOptimization)
@@ -1210,9 +1224,13 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
                               d_err, s))
         return e;
     ORB_HIP_CHECK(hipEventRecord(ev_[5], s));
-    // 5. blur: GaussianBlur of every level (ORBextractor.cc:1085-1086)
-    hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
-                       (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_, (int)tiles_.size());
+    // 5. blur: GaussianBlur of every level (ORBextractor.cc:1085-1086); on the side stream it
+    //    was launched after the pyramid
+    if (side_)
+        ORB_HIP_CHECK(hipStreamWaitEvent(s, evBlur_, 0));
+    else
+        hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
+                           (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_, (int)tiles_.size());
     ORB_HIP_CHECK(hipEventRecord(ev_[2], s));
     // 6. orientation + descriptors
     orb_kp_dev* okps = (orb_kp_dev*)kps;
@@ -1280,10 +1298,10 @@ int Extractor::get_blurred(int index, int level, uint8_t* dst, int dst_step, int
 
 int debug_prof_extract(unsigned long long* out32) {
 #ifdef ORBGPU_PROF
-    ORB_HIP_CHECK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_orbgpu_prof), sizeof(unsigned long long) * 32));
+    ORB_HIP_CHECK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_orbgpu_prof), sizeof(unsigned long long) * 16));
     unsigned long long z[32] = {};
     ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_orbgpu_prof), z, sizeof(z)));
-    return 0;
+    return octree_prof_read(out32 + 16);   // slots 16-31: k_octree's sections (octree.hip)
 #else
     (void)out32;
     return -1;

@@ -121,6 +121,10 @@ private:
 
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[7] = {};
+    // opt-in (ORBGPU_BLUR_SIDE=1): the blur runs on its own stream from the pyramid's end,
+    // beside FAST / compaction / octree, and the descriptors wait for it
+    hipStream_t side_ = nullptr;
+    hipEvent_t evBlur_ = nullptr;
     void *d_in_ = nullptr, *d_pyr_ = nullptr, *d_blur_ = nullptr, *d_slots_ = nullptr, *d_counts_ = nullptr;
     void *d_ptiles_ = nullptr;
     void *d_cells_ = nullptr, *d_tiles_ = nullptr, *d_lcb_ = nullptr, *d_packed_ = nullptr, *d_hdr_ = nullptr;

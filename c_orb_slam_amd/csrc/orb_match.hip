@@ -396,6 +396,16 @@ constexpr int kStageMaxN = 1536;
 constexpr int kStageThreads = 1024;
 // ORBGPU_CAND_NT=256: the staged candidate search in 256-thread workgroups (each stages the
 // frame itself; 4x the workgroups over more CUs) instead of 1024 (A/B runs)
+// ORBGPU_SELECT_LOCAL_NT=512: SearchLocalPoints' selection in 512-thread workgroups (8 query
+// slots per thread, the same 4,096 per problem) instead of 1,024 (A/B runs): a workgroup then
+// needs 8 free wave slots on a CU, not 16, beside the extraction grids
+static int select_local_threads() {
+    static const int v = [] {
+        const char* e = std::getenv("ORBGPU_SELECT_LOCAL_NT");
+        return e && std::atoi(e) == 512 ? 512 : kSelectLocalThreads;
+    }();
+    return v;
+}
 static int stage_threads() {
     static const int v = [] {
         const char* e = std::getenv("ORBGPU_CAND_NT");
@@ -1171,8 +1181,12 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
             mark(2);
             // SearchLocalPoints-sized query sets (thousands of local map points, long occupancy
             // chains between duplicated points): 16 waves per round of the fixed point
-            hipLaunchKernelGGL((k_select_r<false, kSelectLocalThreads, kSelQLocal>), dim3(np), dim3(kSelectLocalThreads),
-                               select_lds_bytes(maxN), stream_, dp, th, 0, nnratio, 0, maxN);
+            if (select_local_threads() == 512)
+                hipLaunchKernelGGL((k_select_r<false, 512, 2 * kSelQLocal>), dim3(np), dim3(512), select_lds_bytes(maxN),
+                                   stream_, dp, th, 0, nnratio, 0, maxN);
+            else
+                hipLaunchKernelGGL((k_select_r<false, kSelectLocalThreads, kSelQLocal>), dim3(np),
+                                   dim3(kSelectLocalThreads), select_lds_bytes(maxN), stream_, dp, th, 0, nnratio, 0, maxN);
         }
     } else {
         mark(2);

@@ -35,3 +35,7 @@ if __import__("os").environ.get("ORBGPU_PROF_DUMP"):
     buf = (C.c_ulonglong * 32)()
     lib().orbgpu_debug_prof_extract(buf)
     print("k_fast_cells sections (cycles, cell 0 of image 0, 13 calls):", list(buf)[:6], flush=True)
+    names = ["init", "phase1", "p2_setup", "p2_sort", "p2_partition", "p2_serial", "p2_final", "p1_best"]
+    print("k_octree sections (cycles per call, job 0 = image 0 level 0):",
+          {n: round(buf[16 + i] / 13) for i, n in enumerate(names)},
+          "phase-2 rounds", round(buf[24] / 13, 1), "phase-1 rounds", round(buf[25] / 13, 1), flush=True)
