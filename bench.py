@@ -80,6 +80,15 @@ def parse():
                     help="only the timed stereo pipeline (+ its CPU baseline): one compact JSON line")
     ap.add_argument("--launch-timeout", type=float, default=3000.0,
                     help="bound on the whole job when bench.py spawns its own ranks (seconds)")
+    ap.add_argument("--enqueue-first", type=int, default=1,
+                    help="1 (default): a step enqueues the ready batch's tracking chain before it starts the "
+                         "next extraction, so the chain's and the extraction's host launches do not interleave "
+                         "(32.9-33.1k vs 32.1-32.4k frames/s with 0, profiles/r04s_enqueue_first_ab.txt)")
+    ap.add_argument("--latency-stereo-batch", type=int, default=1,
+                    help="batch-1 latency leg, device path: 1 (default) one extractor call over the frame's two "
+                         "images; 0: two extractors on two host threads")
+    ap.add_argument("--latency-only", action="store_true",
+                    help="only the batch-1 tracking latency legs (device and host path): one JSON line (A/B runs)")
     ap.add_argument("--passes-only", action="store_true",
                     help="only the isolated roofline passes (extraction + matcher kernels), for rocprofv3 --pmc runs")
     return ap.parse_args()
@@ -287,15 +296,11 @@ def main():
         Twc), block b of a (B x cap) table; the local map of pair p (current frame p+1) is the blocks
         of frames max(0, p-K+1)..p, contiguous in the table (UpdateLocalMap's local keyframes)."""
 
-        def __init__(self, first):
+        def __init__(self, mt):
             # the lane's matcher: the shared one, or (--lane-matchers) its own for every lane but the
             # first, whose chains then run beside the other lanes' on their own streams
-            if first or not args.lane_matchers:
-                self.m, self.ms = m, match_stream
-            else:
-                self.m = orb.ORBmatcher(0.9, True)
-                check(L.ORBmatcher_set_device_pointers(self.m._h, 1))
-                self.ms = torch.cuda.ExternalStream(L.ORBmatcher_stream(self.m._h), device=dev)
+            self.m = mt
+            self.ms = match_stream if mt is m else torch.cuda.ExternalStream(L.ORBmatcher_stream(mt._h), device=dev)
             if args.stereo_batch:   # one extractor, one stream: [lefts | rights] as one batch of 2B images
                 self.exL = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=2 * B)
                 self.exR = self.exL
@@ -552,8 +557,12 @@ def main():
             d2h_bytes = []
         eL1 = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=1)
         eR1 = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=1)
-        k = torch.empty((nf, cap, 7), dtype=torch.int32, device=dev)
-        d = torch.empty((nf, cap, 32), dtype=torch.uint8, device=dev)
+        # device path: Frame(imLeft, imRight)'s two extractions as one call over the frame's two
+        # HBM-resident images (left t, right t = left t + B images), the right image's results
+        # landing in the next frame's slot of k / d (overwritten by that frame's left image)
+        eLR = None if host_io or not args.latency_stereo_batch else orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=2)
+        k = torch.empty((nf + 1, cap, 7), dtype=torch.int32, device=dev)
+        d = torch.empty((nf + 1, cap, 32), dtype=torch.uint8, device=dev)
         kR = torch.empty((cap, 7), dtype=torch.int32, device=dev)
         dR = torch.empty((cap, 32), dtype=torch.uint8, device=dev)
         uR = torch.empty((nf, cap), dtype=torch.float32, device=dev)
@@ -582,17 +591,28 @@ def main():
             if host_io:   # Frame(imLeft, imRight) on pageable host images (Frame.cc:78-81)
                 fR = pool.submit(eR1.extract_host_to_device, rights[t], kR.data_ptr(), dR.data_ptr(), cap)
                 nL = eL1.extract_host_to_device(lefts[t], k[t].data_ptr(), d[t].data_ptr(), cap)
-            else:
+            elif eLR is None:
                 fR = pool.submit(eR1.extract_device, d_R[t].data_ptr(), 1, W, H, W, W * H, kR.data_ptr(), dR.data_ptr(),
                                  cap)
                 nL = eL1.extract_device(d_L[t].data_ptr(), 1, W, H, W, W * H, k[t].data_ptr(), d[t].data_ptr(), cap)
-            nR = fR.result()
-            nl, nr = np.array([nL[0]], np.int32), np.array([nR[0]], np.int32)
-            check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, eL1._h, eR1._h, 1, ptr(nl), arr([k[t].data_ptr()]),
-                                                          arr([d[t].data_ptr()]), ptr(nr), arr([kR.data_ptr()]),
-                                                          arr([dR.data_ptr()]), float(mbf), float(mb),
-                                                          arr([uR[t].data_ptr()]), arr([dep[t].data_ptr()]), ptr(one)),
-                  "ComputeStereoMatches")
+            if host_io or eLR is None:
+                nR = fR.result()
+                nl, nr = np.array([nL[0]], np.int32), np.array([nR[0]], np.int32)
+                check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, eL1._h, eR1._h, 1, ptr(nl), arr([k[t].data_ptr()]),
+                                                              arr([d[t].data_ptr()]), ptr(nr), arr([kR.data_ptr()]),
+                                                              arr([dR.data_ptr()]), float(mbf), float(mb),
+                                                              arr([uR[t].data_ptr()]), arr([dep[t].data_ptr()]),
+                                                              ptr(one)), "ComputeStereoMatches")
+            else:
+                nLR = eLR.extract_device(d_L[t].data_ptr(), 2, W, H, W, B * W * H, k[t].data_ptr(), d[t].data_ptr(), cap)
+                nL = nLR[:1]
+                nl, nr = np.array([nLR[0]], np.int32), np.array([nLR[1]], np.int32)
+                check(L.ORBmatcher_ComputeStereoMatches_batch_at(m._h, eLR._h, 0, eLR._h, 1, 1, ptr(nl),
+                                                                 arr([k[t].data_ptr()]), arr([d[t].data_ptr()]), ptr(nr),
+                                                                 arr([k[t + 1].data_ptr()]), arr([d[t + 1].data_ptr()]),
+                                                                 float(mbf), float(mb), arr([uR[t].data_ptr()]),
+                                                                 arr([dep[t].data_ptr()]), ptr(one)),
+                      "ComputeStereoMatches")
             if t > 0:
                 V = Tcw[t - 1] @ np.linalg.inv(Tcw[t - 2]) if t >= 2 else np.eye(4, dtype=np.float32)
                 Tp = (V @ Tcw[t - 1]).astype(np.float32)
@@ -862,7 +882,16 @@ def main():
     local_acc = []
     pose_inl = []
     kernel_ms = []   # k_fast_cells duration per step (HIP events on the extractor streams)
-    lanes = [Lane(i == 0) for i in range(args.lanes)]
+    # every lane's matcher before any extractor: HIP deals new streams to its hardware queues in
+    # creation order, so the matchers' streams come out on queues of their own
+    lane_m = [m]
+    for _ in range(1, args.lanes):
+        if args.lane_matchers:
+            lane_m.append(orb.ORBmatcher(0.9, True))
+            check(L.ORBmatcher_set_device_pointers(lane_m[-1]._h, 1))
+        else:
+            lane_m.append(m)
+    lanes = [Lane(mt) for mt in lane_m]
     exL = lanes[0].exL
     if args.reserve_cus:
         # the tracking lane's one-workgroup-per-frame kernels (k_select, k_pose_opt) need free
@@ -880,10 +909,17 @@ def main():
         collected batch's counts (None before the pipeline is full)."""
         lane = lanes[state["k"] % len(lanes)]
         te = time.perf_counter()
-        fut = ex_pool.submit(lane.extract)
+        if args.enqueue_first and state["ready"] is not None:
+            # the tracking chain's launches first, then the extraction's: the two threads' launch
+            # streams do not interleave on the host
+            state["ready"].enqueue()
+            fut = ex_pool.submit(lane.extract)
+        else:
+            fut = ex_pool.submit(lane.extract)
+            if state["ready"] is not None:
+                state["ready"].enqueue()
         res = None
         if state["ready"] is not None:
-            state["ready"].enqueue()
             if state["pending"] is not None:
                 res = state["pending"].collect()
             state["pending"] = state["ready"]
@@ -914,7 +950,7 @@ def main():
         per = {side: {k: round(v / args.steps, 4) for k, v in d.items()} for side, d in stage_lr.items()}
         return {"left+right (one 2B-image stream)": per["left"]} if args.stereo_batch else per
 
-    if args.passes_only:   # one extracted, tracked batch; then only the isolated passes below
+    if args.passes_only or args.latency_only:   # one extracted, tracked batch; then the legs below
         args.warmup, args.steps = 1, 0
     for _ in range(args.warmup):
         step()
@@ -962,6 +998,12 @@ def main():
     # TrackWithMotionModel + TrackLocalMap
     frames_total = P * args.steps * world
     fps = frames_total / dt
+    if args.latency_only:
+        if rank == 0:
+            lat = latency_leg(24)
+            lat["host_path"] = latency_leg(24, host_io=True)
+            print(json.dumps({"latency": lat}), file=json_out, flush=True)
+        return
     if args.pipeline_only:   # the yaml feature count's line: pipeline + its CPU baseline
         if rank == 0:
             cpu = None if args.no_cpu_baseline else cpu_baseline(lefts, rights, Rs, args.cpu_seconds)

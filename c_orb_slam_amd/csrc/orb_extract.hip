@@ -42,6 +42,10 @@ static const int8_t kPattern[256 * 4] = {
 // own L2 instead of being fetched again by a different XCD.
 __device__ __forceinline__ int xcd_tile(int bid, int nb) { return (bid & 7) * (nb >> 3) + (bid >> 3); }
 static inline unsigned grid8(int n) { return (unsigned)((n + 7) & ~7); }
+// opt-in ORBGPU_FAST_SPLIT=1: FAST of levels 0-2 (70 % of the pixels) on a side stream, beside the
+// build of levels 3-7 (1.505 -> 1.483 ms per 128-image call alone, no gain in the pipeline:
+// profiles/r04t_fast_split_ab.txt)
+constexpr int kFastSplitLevel = 3;
 
 // copyMakeBorder(image, temp, 19,19,19,19, BORDER_REFLECT_101), 16 bytes/thread.
 // Interior chunks: the (arbitrarily aligned) source row is read as aligned dwords and
@@ -739,6 +743,9 @@ void Extractor::release() {
     stream_ = nullptr;
     if (evBlur_) (void)hipEventDestroy(evBlur_);
     evBlur_ = nullptr;
+    if (evPyrA_) (void)hipEventDestroy(evPyrA_);
+    if (evFastA_) (void)hipEventDestroy(evFastA_);
+    evPyrA_ = evFastA_ = nullptr;
     if (side_) (void)hipStreamDestroy(side_);
     side_ = nullptr;
 }
@@ -748,9 +755,15 @@ int Extractor::init_device(int maxW, int maxH, int maxBatch) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -4;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     for (auto& e : ev_) ORB_HIP_CHECK(hipEventCreate(&e));
-    if (const char* e = getenv("ORBGPU_BLUR_SIDE"); e && atoi(e) > 0) {
-        ORB_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-        ORB_HIP_CHECK(hipEventCreateWithFlags(&evBlur_, hipEventDisableTiming));
+    const char* eb = getenv("ORBGPU_BLUR_SIDE");
+    const char* ef = getenv("ORBGPU_FAST_SPLIT");
+    const bool blurSide = eb && atoi(eb) > 0;
+    fastSplit_ = ef && atoi(ef) == 1 && !blurSide;
+    if (blurSide || fastSplit_) ORB_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    if (blurSide) ORB_HIP_CHECK(hipEventCreateWithFlags(&evBlur_, hipEventDisableTiming));
+    if (fastSplit_) {
+        ORB_HIP_CHECK(hipEventCreateWithFlags(&evPyrA_, hipEventDisableTiming));
+        ORB_HIP_CHECK(hipEventCreateWithFlags(&evFastA_, hipEventDisableTiming));
     }
     static bool consts_done = false;  // per process; guarded by first-use in create
     if (!consts_done) {
@@ -776,7 +789,8 @@ int Extractor::init_device(int maxW, int maxH, int maxBatch) {
 // k_fast_cells work order for a batch of B images: the group rows (groups sharing level and ROI
 // top row, in cell order) of every image are dealt round-robin to the 8 XCDs; entry
 // g = slot * 8 + xcd of the table is the slot-th (b << 16 | group) of that XCD's list, -1 past
-// its end.
+// its end.  Two such tables back to back: the levels below kFastSplitLevel, then the rest
+// (each a multiple of 8 entries, so the concatenation is one table as well).
 int Extractor::build_work(int B) {
     constexpr int kXcds = 8;
     const int ngroups = (int)groups_.size();
@@ -785,16 +799,26 @@ int Extractor::build_work(int B) {
         if (c == 0 || groups_[c].lvl_off != groups_[c - 1].lvl_off || groups_[c].r0 != groups_[c - 1].r0)
             unit.push_back(c);
     unit.push_back(ngroups);
-    std::vector<std::vector<int>> lists(kXcds);
-    long u = 0;
-    for (int b = 0; b < B; b++)
-        for (size_t k = 0; k + 1 < unit.size(); k++, u++)
-            for (int c = unit[k]; c < unit[k + 1]; c++) lists[u % kXcds].push_back((b << 16) | c);
-    size_t len = 0;
-    for (auto& l : lists) len = std::max(len, l.size());
-    std::vector<int> work(len * kXcds, -1);
-    for (int x = 0; x < kXcds; x++)
-        for (size_t sl = 0; sl < lists[x].size(); sl++) work[sl * kXcds + x] = lists[x][sl];
+    const long long splitOff =
+        nlevels_ > kFastSplitLevel ? (long long)levels_[kFastSplitLevel].off : std::numeric_limits<long long>::max();
+    std::vector<int> work;
+    for (int part = 0; part < 2; part++) {
+        std::vector<std::vector<int>> lists(kXcds);
+        long u = 0;
+        for (int b = 0; b < B; b++)
+            for (size_t k = 0; k + 1 < unit.size(); k++) {
+                if ((groups_[unit[k]].lvl_off < splitOff) != (part == 0)) continue;
+                for (int c = unit[k]; c < unit[k + 1]; c++) lists[u % kXcds].push_back((b << 16) | c);
+                u++;
+            }
+        size_t len = 0;
+        for (auto& l : lists) len = std::max(len, l.size());
+        const size_t base = work.size();
+        work.resize(base + len * kXcds, -1);
+        for (int x = 0; x < kXcds; x++)
+            for (size_t sl = 0; sl < lists[x].size(); sl++) work[base + sl * kXcds + x] = lists[x][sl];
+        work_part_[part] = (int)(len * kXcds);
+    }
     if (d_work_) (void)hipFree(d_work_);
     d_work_ = nullptr;
     ORB_HIP_CHECK(hipMalloc(&d_work_, std::max<size_t>(work.size(), 1) * 4));
@@ -1172,13 +1196,25 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
         src = (const uint8_t*)d_in_;
     }
     ORB_HIP_CHECK(hipEventRecord(ev_[0], s));
-    // 1. pyramid
+    const int ncells = (int)cells_.size();
+    if (work_B_ != B && build_work(B)) return -2;
+    const bool split = fastSplit_ && work_part_[0] > 0 && work_part_[1] > 0;
+    // 1. pyramid; with the split, FAST of the levels below kFastSplitLevel starts on side_ as soon
+    //    as they are built (their cells read nothing else), beside the small levels' chain
     {
         const LevelHost& L0 = levels_[0];
         const int n = (L0.pitch / 16) * L0.ph;
         hipLaunchKernelGGL(k_pyr_level0, dim3((n + 255) / 256, B), dim3(256), 0, s, src, img_stride, step, W, H,
                            (uint8_t*)d_pyr_, img_bytes_, L0.pitch, L0.ph);
         for (int l = 1; l < nlevels_; l++) {
+            if (split && l == kFastSplitLevel) {
+                ORB_HIP_CHECK(hipEventRecord(evPyrA_, s));
+                ORB_HIP_CHECK(hipStreamWaitEvent(side_, evPyrA_, 0));
+                hipLaunchKernelGGL(k_fast_cells, dim3(work_part_[0]), dim3(256), 0, side_, (const uint8_t*)d_pyr_,
+                                   img_bytes_, (const CellGroup*)d_groups_, iniTh_, minTh_, (uint32_t*)d_slots_,
+                                   slots_per_image_, (int*)d_counts_, ncells, (const int*)d_work_);
+                ORB_HIP_CHECK(hipEventRecord(evFastA_, side_));
+            }
             const LevelHost& L = levels_[l];
             const LevelHost& P = levels_[l - 1];
             const uint8_t* T = (const uint8_t*)d_tabs_;
@@ -1192,7 +1228,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     }
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
-    if (side_) {
+    if (evBlur_) {
         ORB_HIP_CHECK(hipStreamWaitEvent(side_, ev_[1], 0));
         hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, side_, (const uint8_t*)d_pyr_,
                            (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_, (int)tiles_.size());
@@ -1201,11 +1237,16 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     // 2. FAST per cell (the blur, which only the descriptors read, runs after the octree: the
     //    VALU-heavy FAST grid then overlaps the tracking lane's matching, and the HBM-bound
     //    blur its FP64 PoseOptimization)
-    const int ncells = (int)cells_.size();
-    if (work_B_ != B && build_work(B)) return -2;
-    hipLaunchKernelGGL(k_fast_cells, dim3(work_n_), dim3(256), 0, s, (const uint8_t*)d_pyr_, img_bytes_,
-                       (const CellGroup*)d_groups_, iniTh_, minTh_, (uint32_t*)d_slots_, slots_per_image_,
-                       (int*)d_counts_, ncells, (const int*)d_work_);
+    if (split) {
+        hipLaunchKernelGGL(k_fast_cells, dim3(work_part_[1]), dim3(256), 0, s, (const uint8_t*)d_pyr_, img_bytes_,
+                           (const CellGroup*)d_groups_, iniTh_, minTh_, (uint32_t*)d_slots_, slots_per_image_,
+                           (int*)d_counts_, ncells, (const int*)d_work_ + work_part_[0]);
+        ORB_HIP_CHECK(hipStreamWaitEvent(s, evFastA_, 0));
+    } else {
+        hipLaunchKernelGGL(k_fast_cells, dim3(work_n_), dim3(256), 0, s, (const uint8_t*)d_pyr_, img_bytes_,
+                           (const CellGroup*)d_groups_, iniTh_, minTh_, (uint32_t*)d_slots_, slots_per_image_,
+                           (int*)d_counts_, ncells, (const int*)d_work_);
+    }
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[3], s));
     // 3. compaction
@@ -1226,7 +1267,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     ORB_HIP_CHECK(hipEventRecord(ev_[5], s));
     // 5. blur: GaussianBlur of every level (ORBextractor.cc:1085-1086); on the side stream it
     //    was launched after the pyramid
-    if (side_)
+    if (evBlur_)
         ORB_HIP_CHECK(hipStreamWaitEvent(s, evBlur_, 0));
     else
         hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,

@@ -125,6 +125,10 @@ private:
     // beside FAST / compaction / octree, and the descriptors wait for it
     hipStream_t side_ = nullptr;
     hipEvent_t evBlur_ = nullptr;
+    // FAST of the large levels on side_ while the stream builds the small ones (opt-in,
+    // ORBGPU_FAST_SPLIT=1)
+    bool fastSplit_ = false;
+    hipEvent_t evPyrA_ = nullptr, evFastA_ = nullptr;
     void *d_in_ = nullptr, *d_pyr_ = nullptr, *d_blur_ = nullptr, *d_slots_ = nullptr, *d_counts_ = nullptr;
     void *d_ptiles_ = nullptr;
     void *d_cells_ = nullptr, *d_tiles_ = nullptr, *d_lcb_ = nullptr, *d_packed_ = nullptr, *d_hdr_ = nullptr;
@@ -133,6 +137,7 @@ private:
     void* d_work_ = nullptr;   // k_fast_cells work order (build_work), for work_B_ images
     void* d_groups_ = nullptr;
     int work_B_ = -1, work_n_ = 0;
+    int work_part_[2] = {0, 0};   // table entries of the levels < kFastSplitLevel, then of the rest
     bool d_gtotal_alias_ = false;
     size_t in_cap_ = 0, out_cap_ = 0;
     // device octree (octree.hip): per-job selections, per-image selected lists
