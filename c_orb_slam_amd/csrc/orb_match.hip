@@ -406,6 +406,15 @@ static int select_local_threads() {
     }();
     return v;
 }
+// ORBGPU_CAND_LOCAL_STAGE=0: SearchLocalPoints' candidate search without the LDS-staged frame
+// (no LDS, so its workgroups are not held back by the extraction grids' LDS use; A/B runs)
+static bool cand_local_stage() {
+    static const bool v = [] {
+        const char* e = std::getenv("ORBGPU_CAND_LOCAL_STAGE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
 static int stage_threads() {
     static const int v = [] {
         const char* e = std::getenv("ORBGPU_CAND_NT");
@@ -1168,10 +1177,10 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
             hipLaunchKernelGGL((k_select_r<true, 512, kSelQLast>), dim3(np), dim3(512), select_lds_bytes(maxN), stream_, dp,
                                th, (int)bMono, nnratio, (int)checkOri_, maxN);
         } else {
-            if (maxN <= kStageMaxN && stage_threads() == 256)
+            if (maxN <= kStageMaxN && cand_local_stage() && stage_threads() == 256)
                 hipLaunchKernelGGL((k_candidates<false, true, 256>), cand_grid(maxq, 256, np), dim3(256), kStageLds,
                                    stream_, dp, np, cand_gx(maxq, 256), th, 0, counters());
-            else if (maxN <= kStageMaxN)
+            else if (maxN <= kStageMaxN && cand_local_stage())
                 hipLaunchKernelGGL((k_candidates<false, true, kStageThreads>), cand_grid(maxq, kStageThreads, np),
                                    dim3(kStageThreads), kStageLds,
                                    stream_, dp, np, cand_gx(maxq, kStageThreads), th, 0, counters());
