@@ -893,15 +893,16 @@ struct DenseJob {
     int prob, q0, t0, part;   // problem, first query, first train row, partial slot
 };
 
+template <int TB>
 __global__ void __launch_bounds__(kDenseQ) k_dense_hamming(const DenseDev* __restrict__ probs,
                                                            const DenseJob* __restrict__ jobs,
                                                            unsigned long long* __restrict__ part,
                                                            unsigned long long* counters) {
-    __shared__ uint4 tl[kDenseBlock * 2];
+    __shared__ uint4 tl[TB * 2];
     const DenseJob J = jobs[blockIdx.x];
     const DenseDev P = probs[J.prob];
     const int tid = threadIdx.x;
-    const int nt = min(kDenseBlock, P.nt - J.t0);
+    const int nt = min(TB, P.nt - J.t0);
     const uint4* src = reinterpret_cast<const uint4*>(P.t + 32 * (size_t)J.t0);
     for (int k = tid; k < 2 * nt; k += kDenseQ) tl[k] = src[k];
     const int qi = J.q0 + tid;
@@ -911,25 +912,37 @@ __global__ void __launch_bounds__(kDenseQ) k_dense_hamming(const DenseDev* __res
         a1 = reinterpret_cast<const uint4*>(P.q + 32 * (size_t)qi)[1];
     }
     __syncthreads();
-    unsigned b1 = 0xffffffffu, b2 = 0xffffffffu, bi = 0;
-    for (int j = 0; j < nt; j++) {
-        const uint4 t0 = tl[2 * j], t1 = tl[2 * j + 1];   // wave-uniform address: broadcast
-        const unsigned d = __popc(a0.x ^ t0.x) + __popc(a0.y ^ t0.y) + __popc(a0.z ^ t0.z) + __popc(a0.w ^ t0.w) +
-                           __popc(a1.x ^ t1.x) + __popc(a1.y ^ t1.y) + __popc(a1.z ^ t1.z) + __popc(a1.w ^ t1.w);
-        if (d < b1) {
-            b2 = b1;
-            b1 = d;
-            bi = (unsigned)j;
-        } else if (d < b2) {
-            b2 = d;
-        }
+    // keys d << 16 | j (d <= 256, j < kDenseBlock): in j order, the reference's strict
+    // `dist < bestDist` / `dist < bestDist2` updates are b1 = min(b1, key) and
+    // b2 = min(b2, max(b1, key)) on the keys (b1 <= b2; an equal distance later in j is a larger key,
+    // so it never displaces the best and does become the second).  Four train rows per step:
+    // their LDS broadcasts are issued together and the four popcount chains are independent.
+    unsigned b1 = 0xffffffffu, b2 = 0xffffffffu;
+    auto dist = [&](const uint4& t0, const uint4& t1) {
+        return __popc(a0.x ^ t0.x) + __popc(a0.y ^ t0.y) + __popc(a0.z ^ t0.z) + __popc(a0.w ^ t0.w) +
+               __popc(a1.x ^ t1.x) + __popc(a1.y ^ t1.y) + __popc(a1.z ^ t1.z) + __popc(a1.w ^ t1.w);
+    };
+    auto take = [&](unsigned key) {
+        b2 = min(b2, max(b1, key));   // (b1 <= b2): the median of b1, b2, key
+        b1 = min(b1, key);
+    };
+    int j = 0;
+    for (; j + 4 <= nt; j += 4) {
+        const uint4 t0 = tl[2 * j], t1 = tl[2 * j + 1], t2 = tl[2 * j + 2], t3 = tl[2 * j + 3];
+        const uint4 t4 = tl[2 * j + 4], t5 = tl[2 * j + 5], t6 = tl[2 * j + 6], t7 = tl[2 * j + 7];
+        const unsigned d0 = dist(t0, t1), d1 = dist(t2, t3), d2 = dist(t4, t5), d3 = dist(t6, t7);
+        take((d0 << 16) | (unsigned)j);
+        take((d1 << 16) | (unsigned)(j + 1));
+        take((d2 << 16) | (unsigned)(j + 2));
+        take((d3 << 16) | (unsigned)(j + 3));
     }
+    for (; j < nt; j++) take((dist(tl[2 * j], tl[2 * j + 1]) << 16) | (unsigned)j);
     if (qi < P.nq) {
         unsigned long long* o = part + 2 * ((size_t)J.part * kDenseQ + tid);
-        o[0] = b1 == 0xffffffffu ? ~0ull : ((unsigned long long)b1 << 32) | (unsigned)(J.t0 + (int)bi);
+        o[0] = b1 == 0xffffffffu ? ~0ull : ((unsigned long long)(b1 >> 16) << 32) | (unsigned)(J.t0 + (int)(b1 & 0xffffu));
         // the block's second-smallest key: its distance is b2; any index past the best keeps
         // the merge's ordering of equal distances irrelevant to second_dist
-        o[1] = b2 == 0xffffffffu ? ~0ull : ((unsigned long long)b2 << 32) | 0xffffffffu;
+        o[1] = b2 == 0xffffffffu ? ~0ull : ((unsigned long long)(b2 >> 16) << 32) | 0xffffffffu;
     }
     if (counters && tid == 0) {
         const int sl = blockIdx.x & (kCountSlots - 1);
@@ -1287,19 +1300,31 @@ int Matcher::candidates(const uint8_t* q, int nq, const uint8_t* t, int nt, cons
     return 0;
 }
 
+// train rows per k_dense_hamming workgroup: 256, or 128 / 64 (ORBGPU_DENSE_TB) for more
+// workgroups (and waves per SIMD) over the same tiles, at more partial keys for the merge
+static int dense_block() {
+    static const int v = [] {
+        const char* e = std::getenv("ORBGPU_DENSE_TB");
+        const int b = e ? std::atoi(e) : kDenseBlock;
+        return b == 64 || b == 128 ? b : kDenseBlock;
+    }();
+    return v;
+}
+
 int Matcher::dense(const std::vector<DenseDev>& probs) {
     const int np = (int)probs.size();
     if (np == 0) return 0;
+    const int TB = dense_block();
     std::vector<DenseJob> jobs;
     std::vector<int> qjob;   // first job of each query block (its train blocks follow it)
     int maxBlk = 0;
     for (int p = 0; p < np; p++) {
         // a problem without train rows still runs one (empty) block: its queries get (-1, 256, 256)
-        const int nb = std::max(1, (probs[p].nt + kDenseBlock - 1) / kDenseBlock);
+        const int nb = std::max(1, (probs[p].nt + TB - 1) / TB);
         maxBlk = std::max(maxBlk, nb);
         for (int q0 = 0; q0 < probs[p].nq; q0 += kDenseQ) {
             qjob.push_back((int)jobs.size());
-            for (int b = 0; b < nb; b++) jobs.push_back(DenseJob{p, q0, b * kDenseBlock, (int)jobs.size()});
+            for (int b = 0; b < nb; b++) jobs.push_back(DenseJob{p, q0, b * TB, (int)jobs.size()});
         }
     }
     const size_t bP = (sizeof(DenseDev) * np + 255) & ~(size_t)255, bJ = (sizeof(DenseJob) * jobs.size() + 255) & ~(size_t)255;
@@ -1328,9 +1353,17 @@ int Matcher::dense(const std::vector<DenseDev>& probs) {
         if (int e = zero_counters(6, 1)) return e;
         mark(14);
     }
-    if (!jobs.empty())
-        hipLaunchKernelGGL(k_dense_hamming, dim3((unsigned)jobs.size()), dim3(kDenseQ), 0, stream_, (const DenseDev*)dP,
-                           (const DenseJob*)dJ, dPart, counters());
+    if (!jobs.empty()) {
+        if (TB == 64)
+            hipLaunchKernelGGL(k_dense_hamming<64>, dim3((unsigned)jobs.size()), dim3(kDenseQ), 0, stream_,
+                               (const DenseDev*)dP, (const DenseJob*)dJ, dPart, counters());
+        else if (TB == 128)
+            hipLaunchKernelGGL(k_dense_hamming<128>, dim3((unsigned)jobs.size()), dim3(kDenseQ), 0, stream_,
+                               (const DenseDev*)dP, (const DenseJob*)dJ, dPart, counters());
+        else
+            hipLaunchKernelGGL(k_dense_hamming<kDenseBlock>, dim3((unsigned)jobs.size()), dim3(kDenseQ), 0, stream_,
+                               (const DenseDev*)dP, (const DenseJob*)dJ, dPart, counters());
+    }
     if (!qjob.empty())
         hipLaunchKernelGGL(k_dense_merge, dim3((unsigned)((qjob.size() * kDenseQ + 255) / 256)), dim3(256), 0, stream_,
                            (const DenseDev*)dP, (const int*)dQ, (const DenseJob*)dJ, maxBlk, dPart, (int)qjob.size(),
