@@ -753,7 +753,15 @@ void Extractor::release() {
 int Extractor::init_device(int maxW, int maxH, int maxBatch) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -4;
-    ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    // ORBGPU_EXTRACT_STREAM_PRIO=1: the extraction stream at the device's highest priority (A/B
+    // runs of the pipelined bench)
+    if (const char* pe = getenv("ORBGPU_EXTRACT_STREAM_PRIO"); pe && pe[0] == '1') {
+        int lo = 0, hi = 0;
+        ORB_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        ORB_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
+    } else {
+        ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    }
     for (auto& e : ev_) ORB_HIP_CHECK(hipEventCreate(&e));
     const char* eb = getenv("ORBGPU_BLUR_SIDE");
     const char* ef = getenv("ORBGPU_FAST_SPLIT");
