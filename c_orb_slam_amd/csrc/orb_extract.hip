@@ -52,8 +52,15 @@ constexpr int kFastSplitLevel = 3;
 // realigned with v_alignbyte; the two border chunks of a row reflect byte by byte.
 __global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ src, size_t src_stride, int step,
                                                     int W, int H, uint8_t* __restrict__ pyr, size_t img_bytes,
-                                                    int pitch, int ph) {
+                                                    int pitch, int ph, int* __restrict__ zero0,
+                                                    int* __restrict__ zero1) {
     const int b = blockIdx.y;
+    // the call's two counters (k_compact's corner total, the octree's error bits), cleared by
+    // the first kernel of the stream instead of two fill launches before their users
+    if (blockIdx.x == 0 && b == 0 && threadIdx.x == 0) {
+        *zero0 = 0;
+        *zero1 = 0;
+    }
     const int chunks = pitch >> 4;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= chunks * ph) return;
@@ -1213,7 +1220,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
         const LevelHost& L0 = levels_[0];
         const int n = (L0.pitch / 16) * L0.ph;
         hipLaunchKernelGGL(k_pyr_level0, dim3((n + 255) / 256, B), dim3(256), 0, s, src, img_stride, step, W, H,
-                           (uint8_t*)d_pyr_, img_bytes_, L0.pitch, L0.ph);
+                           (uint8_t*)d_pyr_, img_bytes_, L0.pitch, L0.ph, d_gtotal_, (int*)d_nout_ + B);
         for (int l = 1; l < nlevels_; l++) {
             if (split && l == kFastSplitLevel) {
                 ORB_HIP_CHECK(hipEventRecord(evPyrA_, s));
@@ -1258,7 +1265,6 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[3], s));
     // 3. compaction
-    ORB_HIP_CHECK(hipMemsetAsync(d_gtotal_, 0, 4, s));
     hipLaunchKernelGGL(k_compact, dim3(B), dim3(1024), 0, s, (const uint32_t*)d_slots_, slots_per_image_,
                        (const int*)d_counts_, (const CellDesc*)d_cells_, ncells, (const int*)d_lcb_, nlevels_,
                        (uint32_t*)d_packed_, (int*)d_hdr_, d_gtotal_, packed_cap_);
@@ -1266,7 +1272,6 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     ORB_HIP_CHECK(hipEventRecord(ev_[4], s));
     // 4. DistributeOctTree per (image, level) + per-image selected lists, on the device
     int* d_err = (int*)d_nout_ + B;
-    ORB_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
     if (int e = octree_launch((const uint32_t*)d_packed_, (const int*)d_hdr_, B, nlevels_,
                               (const OctLevelDev*)d_octlv_, (uint32_t*)d_jobsel_, (int*)d_jobcnt_, jcap_,
                               (uint16_t*)d_gscr_, (size_t)packed_cap_, cap, (int2*)d_sel_, selcap_, (int*)d_nout_,
