@@ -504,11 +504,16 @@ __global__ void __launch_bounds__(NT) k_candidates(const SearchDev* __restrict__
 // dist = cv::norm(PO) and PO.dot(Pn) accumulated in double, PredictScale through
 // detmath::predict_scale (glibc logf's levels on every input, tests/test_oracle_kat.py).
 __global__ void __launch_bounds__(256) k_frustum(const SearchDev* __restrict__ probs, const FrustumDev* __restrict__ frs,
-                                                 float viewingCosLimit, float logScaleFactor) {
+                                                 float viewingCosLimit, float logScaleFactor, int np, int gx) {
     ORBGPU_LATENCY_WAVE();
-    const SearchDev& P = probs[blockIdx.y];
-    const FrustumDev& Fq = frs[blockIdx.y];
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    // XCD-aware order (as k_candidates): problem p's blocks run on XCD p % 8, where its
+    // candidate search and selection then read the query arrays this kernel writes
+    const int xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
+    const int by = xcd + 8 * (slot / gx), bx = slot % gx;
+    if (by >= np) return;
+    const SearchDev& P = probs[by];
+    const FrustumDev& Fq = frs[by];
+    const int j = bx * blockDim.x + threadIdx.x;
     const bool on = j < P.nq;
     int vis = 0;
     if (on) {
@@ -1163,8 +1168,8 @@ int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastM
     SearchDev* dp = (SearchDev*)d_probs_;
     if (frustum_ && maxq > 0) {   // SearchLocalPoints: Frame::isInFrustum fills the query arrays first
         mark(8);
-        hipLaunchKernelGGL(k_frustum, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, (const SearchDev*)dp,
-                           frustum_, frustumCos_, frustumLsf_);
+        hipLaunchKernelGGL(k_frustum, cand_grid(maxq, 256, np), dim3(256), 0, stream_, (const SearchDev*)dp,
+                           frustum_, frustumCos_, frustumLsf_, np, cand_gx(maxq, 256));
         mark(9);
     }
     if (timing_) {
@@ -1239,8 +1244,8 @@ int Matcher::frustum(std::vector<SearchDev>& probs, const std::vector<FrustumDev
     ORB_HIP_CHECK(hipMemcpyAsync(d_probs_, probs.data(), pb, hipMemcpyHostToDevice, stream_));
     ORB_HIP_CHECK(hipMemcpyAsync(dfr, fr.data(), sizeof(FrustumDev) * np, hipMemcpyHostToDevice, stream_));
     mark(8);
-    hipLaunchKernelGGL(k_frustum, dim3((maxq + 255) / 256, np), dim3(256), 0, stream_, (const SearchDev*)d_probs_, dfr,
-                       viewingCosLimit, logScaleFactor);
+    hipLaunchKernelGGL(k_frustum, cand_grid(maxq, 256, np), dim3(256), 0, stream_, (const SearchDev*)d_probs_, dfr,
+                       viewingCosLimit, logScaleFactor, np, cand_gx(maxq, 256));
     mark(9);
     ORB_HIP_CHECK(hipGetLastError());
     return 0;
