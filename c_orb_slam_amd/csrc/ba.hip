@@ -3053,12 +3053,16 @@ static bool dist_enabled() {
 
 constexpr int kStructGpuMinEdges = 100000;
 static std::atomic<int> g_struct_gpu_min{kStructGpuMinEdges};   // orbgpu_unit_set_struct_gpu_min_edges
-static bool struct_host(int ne) {
+// The two builders issue different collectives (the device one all-reduces nkf and then 2
+// counts, the host one nkf + 2 at once), so a sharded run must pick the same builder on every
+// rank: the choice may not depend on the rank's own edge count, and sharded runs always build
+// on the device.  ORBGPU_STRUCT_HOST is process-wide, hence rank-independent.
+static bool struct_host(int ne, bool sharded) {
     static const int v = [] {
         const char* e = std::getenv("ORBGPU_STRUCT_HOST");
         return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
-    return v < 0 ? ne < g_struct_gpu_min.load() : v == 1;
+    return v < 0 ? (!sharded && ne < g_struct_gpu_min.load()) : v == 1;
 }
 int debug_set_struct_gpu_min_edges(int v) {
     if (v < 0) return -1;
@@ -3081,7 +3085,7 @@ int BaEngine::build_structure(int level) {
     distOk_ = false;
     std::vector<int64_t> offKeys;    // off-diagonal Schur blocks i1 * nP + i2, ascending (tiled path)
     std::vector<int32_t> blkIJ;      // blkI ++ blkJ (dense sharded path)
-    if (!struct_host(ne_)) {
+    if (!struct_host(ne_, comm_ && comm_->size() > 1)) {
         // the lists built on the device from the edges already in HBM (ba_struct_gpu.hip)
         GpuStructInfo info{};
         const int r = gs_.build(level, nkf_, npt_, ne_, dE_, dLevel_, dKfFixed_, dKfId_, dPtId_, comm_, stream_, &st_,
@@ -3716,7 +3720,7 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
             if (int e = reduce_stop(stop)) return e;
         }
         if (!stopped(stop)) {
-            if (struct_host(ne_)) {   // the host builder reads the levels from the host mirror
+            if (struct_host(ne_, comm_ && comm_->size() > 1)) {   // the host builder reads the levels from the host mirror
                 std::vector<uint8_t> flag(ne_);
                 if (int e = gate_edges(0, flag.data())) return e;
                 for (int i = 0; i < ne_; i++)

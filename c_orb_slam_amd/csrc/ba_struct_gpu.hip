@@ -131,7 +131,10 @@ __global__ void k_gs_scalars(const int* peStart, const int* leStart, const int* 
     sc[C_NPE] = peStart[nP];
     sc[C_NLE] = leStart[nL];
     sc[C_NLP] = lpStart[nL];
-    sc[C_NPAIR] = (int)tStart[nL];
+    // the Schur-term count must fit the int the buffers are sized from: flag it
+    // and report capacity instead of writing past them at 64-bit tStart offsets
+    if (tStart[nL] > 0x7fffffffLL) atomicOr(sc + C_ERR, 2);
+    sc[C_NPAIR] = tStart[nL] > 0x7fffffffLL ? 0 : (int)tStart[nL];
 }
 
 // every Schur term (u <= v over the landmark's lpList), numbered in the host walk's order
@@ -381,7 +384,7 @@ int GpuStructBuilder::build(int level, int nkf, int npt, int ne, const EdgeDev* 
     const long long nPairL = hSc_[C_NPAIR];
     if (hSc_[C_ERR]) {
         info->err = hSc_[C_ERR];
-        return -1;
+        return (hSc_[C_ERR] & 2) ? -3 : -1;   // 2: more Schur terms than an int counts (capacity)
     }
     const int nPair = (int)nPairL;
     // 4. buildStructure's Schur pattern

@@ -236,7 +236,14 @@ int Optimizer_PoseOptimization(const pose_problem* P, float* Tcw_out, uint8_t* o
     return Optimizer_PoseOptimization_batch(1, P, Tcw_out, o, ninliers);
 }
 
+static int block_partition(const ba_problem* P, int nranks, int32_t* pt_rank, std::vector<int32_t>* kfRankOut);
+
 int Optimizer_partition_points(const ba_problem* P, int nranks, int32_t* pt_rank) {
+    return block_partition(P, nranks, pt_rank, nullptr);
+}
+
+// the keyframe-block partition; kfRankOut (optional) receives every keyframe's block
+static int block_partition(const ba_problem* P, int nranks, int32_t* pt_rank, std::vector<int32_t>* kfRankOut) {
     if (!P || nranks < 1 || P->n_kf < 0 || P->n_pt < 0 || P->n_edge < 0) return ORB_E_INVALID;
     if (P->n_pt && !pt_rank) return ORB_E_INVALID;
     if (P->n_edge && (!P->edge_pt || !P->edge_kf)) return ORB_E_INVALID;
@@ -271,6 +278,7 @@ int Optimizer_partition_points(const ba_problem* P, int nranks, int32_t* pt_rank
         acc += w[k];
     }
     for (int p = 0; p < P->n_pt; p++) pt_rank[p] = ref[p] >= 0 ? kfRank[ref[p]] : 0;
+    if (kfRankOut) *kfRankOut = std::move(kfRank);
     return ORB_OK;
 }
 
@@ -298,8 +306,12 @@ int Optimizer_partition_points_nd(const ba_problem* P, int nranks, int32_t* pt_r
     const int nP = (int)H.poseKf.size();
     if (kf_owner)
         for (int k = 0; k < nkf; k++) kf_owner[k] = -2;   // not a free pose of the structure
-    if (nranks == 1 || nP < orbgpu::kBaTiledMinPoses) {   // no block-sparse factorisation to shard
-        return Optimizer_partition_points(P, nranks, pt_rank);
+    if (nranks == 1 || nP < orbgpu::kBaTiledMinPoses) {   // no block-sparse factorisation to shard:
+        std::vector<int32_t> kfRank;                       // the keyframe-block partition, and a
+        if (int e = block_partition(P, nranks, pt_rank, &kfRank)) return e;   // free pose's owner
+        if (kf_owner)                                      // is its keyframe's block
+            for (int32_t k : H.poseKf) kf_owner[k] = kfRank[k];
+        return ORB_OK;
     }
     // the pose graph of the Schur blocks, as BaEngine::build_structure forms it
     std::vector<int64_t> keys;

@@ -79,8 +79,10 @@ int PnPsolver_iterate_batch(int count, PnPsolver_h* hs, int nIterations, orb_rng
     int rc = 0;
     orbgpu::PnPBatch* e = engine(&rc);
     if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
-    // the same stream object shared by several solvers must be consumed in solver order:
-    // run those groups sequentially, independent streams together
+    // the same stream object shared by several solvers must be consumed in solver order, and a
+    // handle listed twice carries its state (best set, cached Refine, counter) from one entry to
+    // the next: run those batches sequentially (one replay workgroup per entry would race on the
+    // handle's device state), independent entries together
     std::vector<orbgpu::PnPSolver*> S(count);
     std::vector<orbgpu::PnPResult> R(count);
     for (int k = 0; k < count; k++) {
@@ -91,7 +93,7 @@ int PnPsolver_iterate_batch(int count, PnPsolver_h* hs, int nIterations, orb_rng
     bool shared = false;
     for (int k = 1; k < count && !shared; k++)
         for (int j = 0; j < k; j++)
-            if (rngs[j] == rngs[k]) { shared = true; break; }
+            if (rngs[j] == rngs[k] || hs[j] == hs[k]) { shared = true; break; }
     int r = 0;
     if (!shared) {
         r = e->iterate(count, S.data(), nIterations, rngs, R.data());

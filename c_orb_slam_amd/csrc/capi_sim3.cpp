@@ -86,10 +86,13 @@ int Sim3Solver_iterate_batch(int count, Sim3Solver_h* hs, int nIterations, orb_r
         S[k] = hs[k]->s;
         R[k].inliers = inliers[k];
     }
-    bool shared = false;  // a stream shared by several solvers is consumed in solver order
+    // a stream shared by several solvers is consumed in solver order, and a handle listed twice
+    // carries its state (best set, counter) from one entry to the next: both run sequentially
+    // (one replay workgroup per entry would otherwise race on the handle's device state)
+    bool shared = false;
     for (int k = 1; k < count && !shared; k++)
         for (int j = 0; j < k; j++)
-            if (rngs[j] == rngs[k]) { shared = true; break; }
+            if (rngs[j] == rngs[k] || hs[j] == hs[k]) { shared = true; break; }
     int r = 0;
     if (!shared) r = e->iterate(count, S.data(), nIterations, rngs, R.data());
     else

@@ -819,7 +819,8 @@ int Optimizer_partition_points(const ba_problem* P, int nranks, int32_t* pt_rank
  * separator tiles and rows (Optimizer_BundleAdjustment_sharded checks this and otherwise keeps
  * the replicated factorisation).  Fewer than 24 free poses or one rank: the keyframe-block
  * partition.  kf_owner (optional, n_kf entries): the rank whose subtree holds keyframe k's
- * pose, -1 for a separator pose, -2 for a keyframe that is no free pose.  Host only. */
+ * pose, -1 for a separator pose, -2 for a keyframe that is no free pose; with the
+ * keyframe-block fallback, a free pose's owner is its keyframe's block.  Host only. */
 int Optimizer_partition_points_nd(const ba_problem* P, int nranks, int32_t* pt_rank, int32_t* kf_owner);
 /* The calling thread's last BA run: [sharded factorisation used (0/1), separator tiles and
  * separator rows exchanged per LM trial, Schur-pattern tiles (what the replicated path

@@ -140,6 +140,15 @@ void  ora_rng_seed(ora_rng* g, unsigned int seed);
 int   ora_rng_rand(ora_rng* g);
 int   ora_rng_random_int(ora_rng* g, int min, int max);  /* DUtils::Random::RandomInt */
 
+/* RANSAC event log (test instrumentation): the events of the last iterate() call as
+ * (hypothesis index within the call, kind) pairs; returns the number of events */
+#define ORA_EV_CAP 512
+static inline void ora_ev_push(int (*ev)[2], int* n, int h, int kind)
+{
+    if (*n < ORA_EV_CAP) { ev[*n][0] = h; ev[*n][1] = kind; }
+    (*n)++;
+}
+
 /* ---- OpenCV C-API linear algebra restated (linalg.c) --------------------- */
 void  ora_svd(const double* A, int m, int n, double* w, double* Ut, double* Vt);
 void  ora_svd_solve(const double* A, int m, int n, const double* b, double* x);
@@ -160,6 +169,7 @@ int   ora_pnp_iterate(ora_pnp* P, int nIterations, ora_rng* rng, int* bNoMore, u
 int   ora_pnp_iterations(const ora_pnp* P);
 int   ora_pnp_max_its(const ora_pnp* P);
 int   ora_pnp_min_inliers(const ora_pnp* P);
+int   ora_pnp_events(const ora_pnp* P, int* out, int cap);   /* kinds: 1 best, 2 Refine failed, 3 Refine ok */
 
 
 /* ---- Sim3Solver (sim3.c), reference src/Sim3Solver.cc --------------------- */
@@ -175,6 +185,7 @@ int   ora_sim3_iterate(ora_sim3* S, int nIterations, ora_rng* rng, int* bNoMore,
                        float* T12);
 void  ora_sim3_estimate(const ora_sim3* S, float* R, float* t, float* s);
 int   ora_sim3_iterations(const ora_sim3* S);
+int   ora_sim3_events(const ora_sim3* S, int* out, int cap);  /* kinds: 1 best update, 3 returned */
 
 
 /* ---- remaining ORBmatcher searches (matchers2.c) ------------------------------

@@ -447,6 +447,11 @@ struct ora_pnp {
     int nRefined;
     uint8_t* refinedInliers;
     float refinedTcw[16];
+    /* test instrumentation (no reference counterpart): the events of the last iterate() call,
+     * (hypothesis index within the call, kind) with kind 1 = best update, 2 = Refine failed,
+     * 3 = Refine succeeded; the first ORA_EV_CAP are kept, ev_n counts them all */
+    int ev_n;
+    int ev[ORA_EV_CAP][2];
 };
 
 /* PnPsolver ctor (67-110) on already-packed correspondences + SetRansacParameters defaults */
@@ -578,6 +583,7 @@ int ora_pnp_iterate(ora_pnp* P, int nIterations, ora_rng* rng, int* bNoMore, uin
 {
     *bNoMore = 0;
     *nInliers = 0;
+    P->ev_n = 0;
     memset(inliers_out, 0, P->nMatches);
     if (P->N < P->minInliers) {
         *bNoMore = 1;
@@ -604,8 +610,11 @@ int ora_pnp_iterate(ora_pnp* P, int nIterations, ora_rng* rng, int* bNoMore, uin
                 memcpy(P->bestInliers, P->inliersi, P->N);
                 P->nBestInliers = P->nInliersi;
                 pose_to_tcw(P->Ri, P->ti, P->bestTcw);
+                ora_ev_push(P->ev, &P->ev_n, nCurrentIterations - 1, 1);
             }
-            if (refine(P)) {
+            const int ok = refine(P);
+            ora_ev_push(P->ev, &P->ev_n, nCurrentIterations - 1, ok ? 3 : 2);
+            if (ok) {
                 *nInliers = P->nRefined;
                 for (int i = 0; i < P->N; i++)
                     if (P->refinedInliers[i]) inliers_out[P->kpIdx[i]] = 1;
@@ -630,3 +639,10 @@ int ora_pnp_iterate(ora_pnp* P, int nIterations, ora_rng* rng, int* bNoMore, uin
 }
 
 int ora_pnp_iterations(const ora_pnp* P) { return P->nIterations; }
+
+int ora_pnp_events(const ora_pnp* P, int* out, int cap)
+{
+    const int n = P->ev_n < ORA_EV_CAP ? P->ev_n : ORA_EV_CAP;
+    for (int i = 0; i < n && i < cap; i++) { out[2 * i] = P->ev[i][0]; out[2 * i + 1] = P->ev[i][1]; }
+    return P->ev_n;
+}

@@ -284,6 +284,8 @@ struct ora_sim3 {
     int nIterations, nBestInliers;
     uint8_t *inl, *bestInl;
     sim3_est best;
+    int ev_n;              /* test instrumentation: events of the last iterate() call */
+    int ev[ORA_EV_CAP][2];
 };
 
 /* Sim3Solver ctor (37-112) on packed, already-filtered pairs: X1/X2 camera-frame points
@@ -376,6 +378,7 @@ int ora_sim3_iterate(ora_sim3* S, int nIterations, ora_rng* rng, int* bNoMore, u
     *bNoMore = 0;
     memset(inliers, 0, S->N1);
     *nInliers = 0;
+    S->ev_n = 0;
     if (S->N < S->minInliers) {
         *bNoMore = 1;
         return 0;
@@ -405,6 +408,7 @@ int ora_sim3_iterate(ora_sim3* S, int nIterations, ora_rng* rng, int* bNoMore, u
             memcpy(S->bestInl, S->inl, S->N);
             S->nBestInliers = ni;
             S->best = E;
+            ora_ev_push(S->ev, &S->ev_n, nCurrent - 1, ni > S->minInliers ? 3 : 1);
             if (ni > S->minInliers) {
                 *nInliers = ni;
                 for (int i = 0; i < S->N; i++)
@@ -428,3 +432,10 @@ void ora_sim3_estimate(const ora_sim3* S, float* R, float* t, float* s)
 }
 
 int ora_sim3_iterations(const ora_sim3* S) { return S->nIterations; }
+
+int ora_sim3_events(const ora_sim3* S, int* out, int cap)
+{
+    const int n = S->ev_n < ORA_EV_CAP ? S->ev_n : ORA_EV_CAP;
+    for (int i = 0; i < n && i < cap; i++) { out[2 * i] = S->ev[i][0]; out[2 * i + 1] = S->ev[i][1]; }
+    return S->ev_n;
+}

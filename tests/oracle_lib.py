@@ -382,6 +382,14 @@ def oracle_search_local_points(F, cur_mp, M, logScaleFactor, th=1.0, nnratio=0.8
 
 
 # ---------------------------------------------------------------- PnP oracle
+def _events(fn, h):
+    fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    buf = np.zeros(2 * 512, np.int32)
+    n = fn(h, ptr(buf), 512)
+    assert n <= 512, "event log overflow"
+    return [(int(buf[2 * i]), int(buf[2 * i + 1])) for i in range(n)]
+
+
 class OraclePnP:
     """PnPsolver(F, vpMapPointMatches) restated on CPU (reference src/PnPsolver.cc)."""
 
@@ -423,6 +431,11 @@ class OraclePnP:
     @property
     def iterations(self):
         return self.L.ora_pnp_iterations(self.h)
+
+    def events(self):
+        """The last iterate() call's events: [(hypothesis index in the call, kind)], kind 1 = best
+        update, 2 = Refine failed, 3 = Refine succeeded (oracle instrumentation)."""
+        return _events(self.L.ora_pnp_events, self.h)
 
 
 class OracleSim3:
@@ -470,6 +483,11 @@ class OracleSim3:
     @property
     def iterations(self):
         return self.L.ora_sim3_iterations(self.h)
+
+    def events(self):
+        """The last iterate() call's events: [(hypothesis index in the call, kind)], kind 1 = best
+        update, 3 = best update returned (oracle instrumentation)."""
+        return _events(self.L.ora_sim3_events, self.h)
 
 
 def new_rng(seed=1):

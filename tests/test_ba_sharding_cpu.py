@@ -74,6 +74,16 @@ def test_partition_nd_small_or_single_rank_is_block():
     from c_orb_slam_amd.optimizer import partition_points, partition_points_nd
     pr = global_ba_problem(1, n_kf=20, pts_per_kf=30)
     assert np.array_equal(partition_points_nd(pr, 3), partition_points(pr, 3))
+    # the fallback still names an owner for every free pose: its keyframe's block,
+    # the block of the points whose first observation it is
+    r, kfo = partition_points_nd(pr, 3, with_kf_owner=True)
+    assert (kfo[pr["kf_id"] == 0] == -2).all() and (kfo[pr["kf_id"] != 0] >= 0).all()
+    first = {}
+    for e, (p, k) in enumerate(zip(pr["edge_pt"], pr["edge_kf"])):
+        first.setdefault(int(p), int(k))
+    for p, k in first.items():
+        if pr["kf_id"][k] != 0:
+            assert r[p] == kfo[k]
     pr = global_ba_problem(1, n_kf=60, pts_per_kf=30)
     assert (partition_points_nd(pr, 1) == 0).all()
 

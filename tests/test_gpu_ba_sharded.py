@@ -128,6 +128,31 @@ def test_sharded_rank_without_points(gpu):
     _close(s, o)
 
 
+def test_sharded_struct_builder_threshold_between_ranks(gpu):
+    """The structure builder (host lists below the edge threshold, device lists above it) must be
+    the same on every rank, since the two issue different collectives: with the threshold set
+    between two ranks' edge counts the sharded run still matches the oracle."""
+    from c_orb_slam_amd._lib import lib
+    from c_orb_slam_amd.optimizer import run_sharded_local
+    pr = global_ba_problem(6, n_kf=24, pts_per_kf=60)
+    npt = len(pr["pt_id"])
+    pt_rank = np.zeros(npt, np.int32)
+    pt_rank[(npt * 3) // 4:] = 1                      # rank 0: 3/4 of the points, rank 1: 1/4
+    ept = np.asarray(pr["edge_pt"])
+    e0, e1 = int((pt_rank[ept] == 0).sum()), int((pt_rank[ept] == 1).sum())
+    assert e0 > e1 + 2
+    assert lib().orbgpu_unit_set_struct_gpu_min_edges((e0 + e1) // 2) == 0
+    try:
+        s, per = run_sharded_local(pr, 2, "global", 10, False, pt_rank=pt_rank, trace=True)
+    finally:
+        assert lib().orbgpu_unit_set_struct_gpu_min_edges(100000) == 0
+    o = oracle_lib.oracle_global_ba(pr, 10, False)
+    assert s["iterations"] == o["iterations"]
+    np.testing.assert_allclose(s["solve_chi2"], o["solve_chi2"], rtol=1e-9)
+    _close(s, o)
+    assert np.array_equal(per[1]["kf_Tcw"], per[0]["kf_Tcw"])
+
+
 def test_global_ba_config5_2000kf_matches_oracle(gpu):
     """SURVEY.md §8d config 5 at its smallest stated size: a merged-map-shaped problem of 2,000
     keyframes (150 new points each, seen by U{3..10} consecutive keyframes: ~281k points, ~1.4M
