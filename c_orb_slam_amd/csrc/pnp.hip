@@ -217,14 +217,18 @@ __global__ void __launch_bounds__(64) k_pnp_replay(const PnPProbDev* __restrict_
     int nBest = st->nBest, refValid = st->refValid, refNin = st->refNin;
     int consumed = P.nhyp, success = 0;
     // The reference's loop only acts at an "event": a hypothesis with at least minInliers inliers
-    // that beats the best (c > nBest) or meets an invalid Refine.  Between events the state is
-    // constant, so 64 counts at a time are tested lane-parallel and the first event of the chunk
-    // (ballot) is replayed; the walk resumes right after it.  Iterations = hypotheses consumed.
+    // that beats the best (c > nBest), meets an invalid Refine, or meets a cached Refine that
+    // succeeds -- Refine() runs for every hypothesis with >= minInliers, so when the best set of
+    // a previous call refined successfully (that call returned it), the first such hypothesis of
+    // this call returns it again (PnPsolver.cc:203-235).  Between events the state is constant,
+    // so 64 counts at a time are tested lane-parallel and the first event of the chunk (ballot)
+    // is replayed; the walk resumes right after it.  Iterations = hypotheses consumed.
     int h0 = 0;
     while (h0 < P.nhyp && !success) {
         const int h = h0 + lane;
         const int c = h < P.nhyp ? P.counts[h] : -1;
-        const bool ev = h < P.nhyp && c >= P.minInliers && (c > nBest || !refValid);
+        const bool refOk = refValid && refNin > P.minInliers;
+        const bool ev = h < P.nhyp && c >= P.minInliers && (c > nBest || !refValid || refOk);
         const unsigned long long evb = __ballot(ev);
         if (!evb) {
             h0 += 64;
