@@ -684,6 +684,7 @@ def main():
         out = {"metric": "tracking latency per stereo frame (batch 1, sequential)", "mean_ms": round(float(w.mean()), 3),
                "p50_ms": round(float(np.percentile(w, 50)), 3), "p90_ms": round(float(np.percentile(w, 90)), 3),
                "frames": int(len(w)), "matches_per_frame": round(float(np.mean(nmatch)), 1),
+               "frame_ms": [round(float(v), 3) for v in walls],
                "max_rotation_error": round(max(err), 6),
                "note": "Frame(imLeft, imRight) + TrackWithMotionModel + TrackLocalMap per frame, synchronous C-ABI "
                        "calls; pose t from pose t-1 and t-2 (constant-velocity model)"}

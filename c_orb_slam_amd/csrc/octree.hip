@@ -1,7 +1,8 @@
 // octree.hip -- gfx950 ORBextractor::DistributeOctTree (reference src/ORBextractor.cc:481-763).
 //
 // One workgroup per (image, level) job, all jobs of a batch in one launch, straight after
-// k_compact: no host round trip between FAST and the descriptor kernel.
+// k_fast_cells (each job compacts its own level's cell outputs first): no host round trip
+// between FAST and the descriptor kernel.
 //
 // The std::list algorithm is restated over two observations:
 //  * keys inside a node are always a subsequence of the input order, and the only
@@ -24,6 +25,7 @@
 namespace orbgpu {
 
 constexpr int OCT_TMAX = 1024;   // largest workgroup instance (k_octree<256|512|1024>)
+constexpr int kOctCellsMax = 2048;   // FAST cells of one level (a job's compaction)
 
 struct OctShared {
     int16_t x0[2 * kOctNMax], y0[2 * kOctNMax], x1[2 * kOctNMax], y1[2 * kOctNMax];
@@ -34,6 +36,7 @@ struct OctShared {
     uint16_t er[kOctNMax], eidx[kOctNMax];
     uint16_t vs[kOctNMax], vs2[kOctNMax];
     uint32_t sk[kOctNMax];         // phase-2 sort keys (size << 16 | creation order)
+    int cdelta[kOctCellsMax];      // compaction: slot index - list index of every cell's first candidate
     uint16_t knode[kOctKMax], arena[kOctKMax], tmp[kOctKMax];
     int wsum[OCT_TMAX / 64];
     int head, size, nfree, m, newm, seqctr, flag;
@@ -124,28 +127,69 @@ __device__ __forceinline__ int oct_quadrant(const OctShared& S, int p, uint32_t 
 __device__ __forceinline__ int oct_best_key(uint32_t pk, int k) { return (int)((pk >> 24) << 16) | (0xffff - k); }
 
 template <int T>
-__global__ void __launch_bounds__(T) k_octree(const uint32_t* __restrict__ packed, const int* __restrict__ hdr,
-                                                 int nlevels, const OctLevelDev* __restrict__ lv,
+__global__ void __launch_bounds__(T) k_octree(OctInput in, int nlevels, const OctLevelDev* __restrict__ lv,
                                                  uint32_t* __restrict__ jobsel, int* __restrict__ jobcnt, int jcap,
                                                  uint16_t* __restrict__ gscratch, size_t gstride, int* __restrict__ err) {
     __shared__ OctShared S;
     ORBGPU_PROF_START;
     const int job = blockIdx.x, b = job / nlevels, l = job - b * nlevels;
     const int tid = threadIdx.x;
-    const int* H = hdr + (size_t)b * (nlevels + 2);
-    const int base = H[nlevels + 1];
-    int loff = 0;
-    for (int k = 0; k < l; k++) loff += H[1 + k];
-    const int n = H[1 + l];
-    if (base < 0 || n <= 0 || n > 0xffff) {
+    // ---- the level's FAST candidates in cell order (ORBextractor.cc:776-829's push order):
+    //      cell offsets by a block scan of the counts (S.ia), then a thread per candidate finds
+    //      its cell (binary search over the offsets) and copies it from the cell's slot run to the
+    //      level's own range of `packed` (read back below by this workgroup only); the copies of
+    //      a thread are independent, so their loads are in flight together
+    const int cb = in.lcb[l], nc = in.lcb[l + 1] - cb;
+    const int* cnt = in.counts + (size_t)b * in.ncells + cb;
+    if (nc + 1 > 4 * kOctNMax || nc > kOctCellsMax) {
         if (tid == 0) {
             jobcnt[job] = 0;
-            if (base < 0) atomicOr(err, 1);   // k_compact: packed capacity
-            else if (n > 0xffff) atomicOr(err, 2);
+            atomicOr(err, 2);
         }
         return;
     }
-    const uint32_t* src = packed + base + loff;
+    const int n = oct_scan_val<T>(
+        nc, [&](int i) { return cnt[i]; },
+        [&](int i, int o) {
+            S.ia[i] = o;
+            S.cdelta[i] = in.cell_slot[cb + i] - in.cell_slot[cb] - o;
+        },
+        S.wsum);
+    const size_t base = (size_t)b * in.slots_per_image + (size_t)in.cell_slot[cb];
+    if (n <= 0 || n > 0xffff) {
+        if (tid == 0) {
+            jobcnt[job] = 0;
+            if (n > 0xffff) atomicOr(err, 2);
+        }
+        return;
+    }
+    {
+        const uint32_t* sl = in.slots + base;   // cell c's run starts at sl[ia[c] + cdelta[c]]
+        uint32_t* dst = in.packed + base;
+        constexpr int U = 4;
+        for (int k0 = tid; k0 < n; k0 += U * T) {
+            uint32_t v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int k = k0 + u * T;
+                if (k < n) {
+                    int lo = 0, hi = nc - 1;   // the last cell whose offset is <= k (it holds k)
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (S.ia[mid] <= k) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    v[u] = sl[k + S.cdelta[lo]];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (k0 + u * T < n) dst[k0 + u * T] = v[u];
+        }
+        if (tid == 0) atomicAdd(in.g_total, n);
+    }
+    __syncthreads();
+    const uint32_t* src = in.packed + base;
     const OctLevelDev L = lv[l];
     const int N = L.N;
     // keys: node / arena / scratch indices in LDS, or in the global scratch for big jobs
@@ -153,7 +197,7 @@ __global__ void __launch_bounds__(T) k_octree(const uint32_t* __restrict__ packe
     uint16_t* arena = S.arena;
     uint16_t* tmp = S.tmp;
     if (n > kOctKMax) {
-        knode = gscratch + (size_t)base + loff;
+        knode = gscratch + base;
         arena = knode + gstride;
         tmp = arena + gstride;
     }
@@ -547,22 +591,22 @@ int octree_prof_read(unsigned long long* out16) {
 #endif
 }
 
-int octree_launch(const uint32_t* packed, const int* hdr, int B, int nlevels, const OctLevelDev* lv, uint32_t* jobsel,
-                  int* jobcnt, int jcap, uint16_t* gscratch, size_t gstride, int cap, int2* sel, int selcap, int* nout,
-                  int* err, hipStream_t s) {
+int octree_launch(const OctInput& in, int B, int nlevels, const OctLevelDev* lv, uint32_t* jobsel, int* jobcnt, int jcap,
+                  uint16_t* gscratch, size_t gstride, int cap, int2* sel, int selcap, int* nout, int* err,
+                  hipStream_t s) {
     static const int nt = [] {
         const char* e = getenv("ORBGPU_OCT_T");
         const int v = e ? atoi(e) : 256;
         return v == 512 || v == 1024 ? v : 256;
     }();
     if (nt == 1024)
-        hipLaunchKernelGGL(k_octree<1024>, dim3(B * nlevels), dim3(1024), 0, s, packed, hdr, nlevels, lv, jobsel, jobcnt,
+        hipLaunchKernelGGL(k_octree<1024>, dim3(B * nlevels), dim3(1024), 0, s, in, nlevels, lv, jobsel, jobcnt,
                            jcap, gscratch, gstride, err);
     else if (nt == 512)
-        hipLaunchKernelGGL(k_octree<512>, dim3(B * nlevels), dim3(512), 0, s, packed, hdr, nlevels, lv, jobsel, jobcnt,
+        hipLaunchKernelGGL(k_octree<512>, dim3(B * nlevels), dim3(512), 0, s, in, nlevels, lv, jobsel, jobcnt,
                            jcap, gscratch, gstride, err);
     else
-        hipLaunchKernelGGL(k_octree<256>, dim3(B * nlevels), dim3(256), 0, s, packed, hdr, nlevels, lv, jobsel, jobcnt,
+        hipLaunchKernelGGL(k_octree<256>, dim3(B * nlevels), dim3(256), 0, s, in, nlevels, lv, jobsel, jobcnt,
                            jcap, gscratch, gstride, err);
     hipLaunchKernelGGL(k_sel_build, dim3(B), dim3(64), 0, s, (const uint32_t*)jobsel, (const int*)jobcnt, nlevels,
                        jcap, cap, sel, selcap, nout, err);

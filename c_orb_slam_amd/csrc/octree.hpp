@@ -21,8 +21,23 @@ struct OctLevelDev {   // DistributeOctTree(vToDistributeKeys, minX, maxX, minY,
 // instrumented builds (make prof): k_octree section cycles of job 0 into out16, then reset
 int octree_prof_read(unsigned long long* out16);
 
-int octree_launch(const uint32_t* packed, const int* hdr, int B, int nlevels, const OctLevelDev* lv, uint32_t* jobsel,
-                  int* jobcnt, int jcap, uint16_t* gscratch, size_t gstride, int cap, int2* sel, int selcap, int* nout,
-                  int* err, hipStream_t s);
+// The FAST output a job reads (k_fast_cells): cell c of image b holds counts[b * ncells + c]
+// candidates at slots[b * slots_per_image + cell_slot[c]]; level l's cells are [lcb[l], lcb[l+1]).
+// Each job compacts its level's cells, in cell order (the reference's vToDistributeKeys order),
+// into packed at the level's own slot range (disjoint per job), and adds its count to g_total.
+struct OctInput {
+    const uint32_t* slots;
+    size_t slots_per_image;
+    const int* counts;
+    const int* cell_slot;
+    const int* lcb;
+    int ncells;
+    uint32_t* packed;
+    int* g_total;
+};
+
+int octree_launch(const OctInput& in, int B, int nlevels, const OctLevelDev* lv, uint32_t* jobsel, int* jobcnt, int jcap,
+                  uint16_t* gscratch, size_t gstride, int cap, int2* sel, int selcap, int* nout, int* err,
+                  hipStream_t s);
 
 }  // namespace orbgpu

@@ -378,6 +378,24 @@ __device__ __forceinline__ int wave_sum(int v) {
 // Issue priority of a latency-critical wave over co-resident bulk waves on its SIMD.
 #define ORBGPU_LATENCY_WAVE() __builtin_amdgcn_s_setprio(3)
 
+// (problem, block) of a 1-D grid of gx blocks per problem.  With >= 8 problems the order is
+// XCD-aware: workgroups L and L + 8 share an XCD (blocks are dealt round-robin over the 8 XCDs),
+// so workgroup L takes problem (L % 8) + 8 (L / 8 / gx), block (L / 8) % gx, and every block of a
+// problem runs on one XCD (its staged inputs are fetched into one L2).  Fewer problems would
+// leave XCDs idle, so their blocks are spread over all of them.  Grid size: xcd_grid().
+__device__ __forceinline__ bool xcd_problem_block(int np, int gx, int& by, int& bx) {
+    if (np >= 8) {
+        const int xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
+        by = xcd + 8 * (slot / gx);
+        bx = slot % gx;
+    } else {
+        by = (int)blockIdx.x / gx;
+        bx = (int)blockIdx.x - by * gx;
+    }
+    return by < np;
+}
+inline dim3 xcd_grid(int gx, int np) { return dim3(np >= 8 ? 8 * gx * ((np + 7) / 8) : gx * np); }
+
 // sum over the 64 lanes of a wave (every lane active), result in every lane
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -7,8 +7,8 @@
 //   k_blur7        GaussianBlur 7x7 sigma 2 (8-bit fixed point)    ORBextractor.cc:1085-1086
 //   k_fast_cells   per-cell FAST(th=20) / FAST(th=7) + NMS, LDS-staged ROI,
 //                  raster-order compaction                        ORBextractor.cc:776-829
-//   k_compact      per-image, per-level candidate lists (cell order)
-//   host           DistributeOctTree (order-defining)             ORBextractor.cc:539-763
+//   k_octree       per (image, level): the level's candidates in cell order, then
+//                  DistributeOctTree (order-defining)             ORBextractor.cc:539-763
 //   k_orient_desc  IC_Angle + rotated BRIEF, one wave per keypoint ORBextractor.cc:77-147
 //
 // HBM layout: per image, the padded levels (pitch = align16(w+38)) are
@@ -29,6 +29,7 @@ namespace orbgpu {
 __constant__ int8_t c_pattern[256 * 4];     // rBRIEF pairs (x0,y0,x1,y1)
 __constant__ int8_t c_disc[2 * 1024];       // IC_Angle disc offsets (u, v)
 __constant__ int c_ndisc;
+__constant__ int c_umax[16];                // IC_Angle: half width d(|v|) of disc row v (d(0) = 15)
 __constant__ int c_gauss[7];
 
 static const int8_t kPattern[256 * 4] = {
@@ -55,7 +56,7 @@ __global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ 
                                                     int pitch, int ph, int* __restrict__ zero0,
                                                     int* __restrict__ zero1) {
     const int b = blockIdx.y;
-    // the call's two counters (k_compact's corner total, the octree's error bits), cleared by
+    // the call's two counters (k_octree's corner total, the octree's error bits), cleared by
     // the first kernel of the stream instead of two fill launches before their users
     if (blockIdx.x == 0 && b == 0 && threadIdx.x == 0) {
         *zero0 = 0;
@@ -158,17 +159,151 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, s
     }
 }
 
+// The small pyramid levels [la, nlevels) in ONE launch (the tail of the chain of resizes,
+// ORBextractor.cc:1107-1132, where a launch per level costs more than its pixels): workgroup
+// (k, b) owns row strip k of every chained level of image b.  The strips of level l are the
+// images of level l+1's strips under the row map (boundary A_l(k) = yrows_{l+1}[A_{l+1}(k)].x),
+// so the rows a strip computes at level l are its own rows plus the few rows (the cone) that its
+// level-(l+1) rows read beyond them, recomputed instead of exchanged.  Everything a workgroup
+// reads is staged first, with all its loads in flight together: the source rows of level la-1
+// (interior, from the padded level in HBM) and every chained level's row taps.  Per level: the
+// strip's rows into an LDS buffer (ping-pong between two; the first level reads the staged
+// source), then every padded row that reflects (REFLECT_101) to one of its own rows is written
+// out, 16 bytes a thread.  A thread keeps the column taps of its 4 output columns in registers
+// and walks rows.  Same fixed-point arithmetic per pixel as k_pyr_resize: identical levels.
+__global__ void __launch_bounds__(256) k_pyr_chain(uint8_t* __restrict__ pyr, size_t img_bytes, long long src_off,
+                                                   int src_pitch, int src_w, const ChainLevel* __restrict__ lv, int nl,
+                                                   const int4* __restrict__ strips, const uint16_t* __restrict__ rows,
+                                                   const uint8_t* __restrict__ tabs, int src_lds, int src_rp) {
+    extern __shared__ uint32_t s_chain[];
+    uint8_t* sb = reinterpret_cast<uint8_t*>(s_chain);
+    const int k = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    uint8_t* base = pyr + (size_t)b * img_bytes;
+    const int4 sr = strips[k * (nl + 1) + nl];   // source rows [x, y) of level la-1; row-tap slots at z
+    {
+        // source rows: padded columns [16, 16 + src_rp) as dwords (interior column c at byte c + 3)
+        const uint32_t* S32 = reinterpret_cast<const uint32_t*>(base + src_off + (size_t)(kEdge + sr.x) * src_pitch + 16);
+        const int wpr = src_rp >> 2, nsr = sr.y - sr.x, spw = src_pitch >> 2;
+        uint32_t* d = s_chain + (src_lds >> 2);
+        for (int t = tid; t < nsr * wpr; t += 256) {
+            const int r = t / wpr, q = t - r * wpr;
+            d[t] = S32[(size_t)r * spw + q];
+        }
+        // row taps of every chained level's compute rows: (y0 | y1 << 16, beta pair)
+        int2* rt = reinterpret_cast<int2*>(sb + sr.z);
+        int slot = 0;
+        for (int i = 0; i < nl; i++) {
+            const int4 st = strips[k * (nl + 1) + i];
+            const int2* yr = reinterpret_cast<const int2*>(tabs + lv[i].yr);
+            const int* yb = reinterpret_cast<const int*>(tabs + lv[i].yb);
+            for (int t = tid; t < st.y - st.x; t += 256) {
+                const int2 yy = yr[st.x + t];
+                rt[slot + t] = make_int2(yy.x | (yy.y << 16), yb[st.x + t]);
+            }
+            slot += st.y - st.x;
+        }
+    }
+    __syncthreads();
+    const uint8_t* prev = sb + src_lds + 3;   // interior column 0 of the staged source
+    int prev_lo = sr.x, prev_rp = src_rp, prev_n = sr.y - sr.x;
+    const int2* rt = reinterpret_cast<const int2*>(sb + sr.z);
+    for (int i = 0; i < nl; i++) {
+        const ChainLevel L = lv[i];
+        const int4 st = strips[k * (nl + 1) + i];   // compute rows [x, y), padded-row list [z, z + w)
+        const int nrows = st.y - st.x, ngr = (L.w + 3) >> 2, nph = L.nph;
+        uint8_t* cur = sb + L.lds;
+        if (tid < nph * ngr) {
+            const int ph = tid / ngr, g = tid - ph * ngr;
+            const int* xofs = reinterpret_cast<const int*>(tabs + L.xofs);
+            const short2* xal = reinterpret_cast<const short2*>(tabs + L.xal);
+            int sx[4], s1[4];
+            short2 al[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int dx = min(4 * g + j, L.w - 1);
+                sx[j] = xofs[dx];
+                al[j] = xal[dx];
+                s1[j] = sx[j] + (al[j].y != 0);
+            }
+            for (int r = ph; r < nrows; r += nph) {
+                const int2 e = rt[r];
+                const int y0 = e.x & 0xffff, y1 = e.x >> 16;
+                const short2 be = __builtin_bit_cast(short2, e.y);
+                // rows of the previous level's buffer (inside its cone by construction)
+                const uint8_t* R0 = prev + min(max(y0 - prev_lo, 0), prev_n - 1) * prev_rp;
+                const uint8_t* R1 = prev + min(max(y1 - prev_lo, 0), prev_n - 1) * prev_rp;
+                uint32_t v = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (4 * g + j < L.w) {
+                        const short2 a = al[j];
+                        const int D0 = R0[sx[j]] * a.x + R0[s1[j]] * a.y;
+                        const int D1 = R1[sx[j]] * a.x + R1[s1[j]] * a.y;
+                        const int o = (((be.x * (D0 >> 4)) >> 16) + ((be.y * (D1 >> 4)) >> 16) + 2) >> 2;
+                        v |= (uint32_t)(uint8_t)o << (8 * j);
+                    }
+                }
+                *reinterpret_cast<uint32_t*>(cur + r * L.rp + 4 * g) = v;
+            }
+        }
+        rt += nrows;
+        __syncthreads();
+        // the padded rows of this strip: row py is interior row refl101(py - 19, h)
+        const int nch = L.pitch >> 4;
+        for (int t = tid; t < st.w * nch; t += 256) {
+            const int ri = t / nch, ch = t - ri * nch;
+            const int py = rows[st.z + ri];
+            const int y = refl101(py - kEdge, L.h);
+            const uint8_t* row = cur + min(max(y - st.x, 0), nrows - 1) * L.rp;
+            const int x0 = ch * 16 - kEdge;   // = 1 (mod 4)
+            uint4 o;
+            if (x0 >= 1 && x0 + 16 <= L.w) {
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(row + x0 - 1);
+                const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+                o.x = __builtin_amdgcn_alignbyte(w1, w0, 1);
+                o.y = __builtin_amdgcn_alignbyte(w2, w1, 1);
+                o.z = __builtin_amdgcn_alignbyte(w3, w2, 1);
+                o.w = __builtin_amdgcn_alignbyte(w4, w3, 1);
+            } else {
+                uint32_t q[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int j = 0; j < 16; j++) q[j >> 2] |= (uint32_t)row[refl101(x0 + j, L.w)] << (8 * (j & 3));
+                o = make_uint4(q[0], q[1], q[2], q[3]);
+            }
+            *reinterpret_cast<uint4*>(base + L.off + (size_t)py * L.pitch + 16 * ch) = o;
+        }
+        prev = cur;
+        prev_lo = st.x;
+        prev_rp = L.rp;
+        prev_n = nrows;
+    }
+    (void)src_w;
+}
+
 // GaussianBlur(7x7, sigma 2, REFLECT_101) on CV_8U: int taps (round(k*256)),
 // int row pass, int column pass, (v + 2^15) >> 16, saturate.  The padded
 // level's 19-px REFLECT_101 border supplies the filter border.  Tile 128x32,
-// dword LDS staging (the padded row is dword-aligned at interior x0-3), four
-// outputs per thread per pass, dword stores into the unpadded blurred level.
+// dword LDS staging (the padded row is dword-aligned at interior x0-3), dword
+// stores into the unpadded blurred level.  Every sum is an exact integer sum, so
+// the order of the terms is free (the result is the reference's bit for bit):
+//   row pass     two v_dot4_u32_u8 per output pixel on the byte window (v_alignbyte
+//                realigns it), for two staged rows at once; a row sum is <= 255 * 256,
+//                so the sums of rows r, r+1 at one column pack into one dword (u16 pair)
+//   column pass  four v_dot2_u32_u16 per output pixel on those row pairs: output row
+//                2p reads pairs (2p, 2p+1) .. (2p+6, 2p+7) with taps (t0,t1) .. (t6,0),
+//                output row 2p+1 the same pairs with taps (0,t0), (t1,t2) .. (t5,t6)
 constexpr int BT_W = 128, BT_H = 32, BT_LW = BT_W + 8;  // staged cols: interior [x0-3, x0+133)
+typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dot2u(uint32_t pair, uint32_t taps, uint32_t acc) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2v, pair), __builtin_bit_cast(ushort2v, taps), acc, false);
+}
 __global__ void __launch_bounds__(256) k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                size_t img_bytes, size_t blur_bytes,
                                                const BlurTile* __restrict__ tiles, int ntiles) {
-    __shared__ uint32_t s_src[(BT_H + 6) * (BT_LW / 4)];
-    __shared__ int4 s_row[(BT_H + 6) * (BT_W / 4)];
+    constexpr int WPR = BT_LW / 4;          // words per staged row
+    constexpr int SR = BT_H + 6;            // staged rows (38: 19 row pairs)
+    __shared__ uint32_t s_src[SR * WPR];
+    __shared__ uint4 s_pair[(SR / 2) * (BT_W / 4)];   // [pair][4-px group]: 4 packed (r, r+1) sums
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
     if (tile >= ntiles) return;
     const BlurTile tl = tiles[tile];
@@ -176,54 +311,62 @@ __global__ void __launch_bounds__(256) k_blur7(const uint8_t* __restrict__ pyr, 
     const uint8_t* P = pyr + (size_t)b * img_bytes + tl.off;           // padded level base
     uint8_t* O = blur + (size_t)b * blur_bytes + tl.boff;               // unpadded blurred level
     const int x0 = tl.tx * BT_W, y0 = tl.ty * BT_H;
-    constexpr int WPR = BT_LW / 4;  // words per staged row
-    for (int i = threadIdx.x; i < (BT_H + 6) * WPR; i += 256) {
+    for (int i = threadIdx.x; i < SR * WPR; i += 256) {
         const int r = i / WPR, wq = i - r * WPR;
         const int yy = min(y0 + r - 3, tl.h + 2) + kEdge;                 // padded row
         const int c = min(kEdge - 3 + x0 + 4 * wq, tl.pitch - 4);           // padded col (dword aligned)
         s_src[i] = *reinterpret_cast<const uint32_t*>(P + (size_t)yy * tl.pitch + c);
     }
+    const uint32_t TLO = (uint32_t)c_gauss[0] | ((uint32_t)c_gauss[1] << 8) | ((uint32_t)c_gauss[2] << 16) |
+                         ((uint32_t)c_gauss[3] << 24);
+    const uint32_t THI = (uint32_t)c_gauss[4] | ((uint32_t)c_gauss[5] << 8) | ((uint32_t)c_gauss[6] << 16);
     __syncthreads();
-    // NB: read aligned dwords and split them; byte-indexed LDS reads get merged by
-    // hipcc into ds_read_u16 at odd offsets, which gfx950 serves misaligned.
-    for (int i = threadIdx.x; i < (BT_H + 6) * (BT_W / 4); i += 256) {
-        const int r = i / (BT_W / 4), q = i - r * (BT_W / 4);
-        const uint32_t w0 = s_src[r * WPR + q], w1 = s_src[r * WPR + q + 1], w2 = s_src[r * WPR + q + 2];
-        int v[10];
+    for (int i = threadIdx.x; i < (SR / 2) * (BT_W / 4); i += 256) {
+        const int pr = i / (BT_W / 4), q = i - pr * (BT_W / 4);
+        uint32_t o[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            v[k] = (w0 >> (8 * k)) & 0xff;
-            v[4 + k] = (w1 >> (8 * k)) & 0xff;
+        for (int h = 0; h < 2; h++) {
+            const uint32_t* w = s_src + (2 * pr + h) * WPR + q;
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t lo = j ? __builtin_amdgcn_alignbyte(w1, w0, j) : w0;
+                const uint32_t hi = j ? __builtin_amdgcn_alignbyte(w2, w1, j) : w1;
+                const uint32_t r = __builtin_amdgcn_udot4(lo, TLO, __builtin_amdgcn_udot4(hi, THI, 0u, false), false);
+                o[j] = h ? (o[j] | (r << 16)) : r;
+            }
         }
-        v[8] = w2 & 0xff;
-        v[9] = (w2 >> 8) & 0xff;
-        int4 o;
-        o.x = c_gauss[0] * v[0] + c_gauss[1] * v[1] + c_gauss[2] * v[2] + c_gauss[3] * v[3] + c_gauss[4] * v[4] + c_gauss[5] * v[5] + c_gauss[6] * v[6];
-        o.y = c_gauss[0] * v[1] + c_gauss[1] * v[2] + c_gauss[2] * v[3] + c_gauss[3] * v[4] + c_gauss[4] * v[5] + c_gauss[5] * v[6] + c_gauss[6] * v[7];
-        o.z = c_gauss[0] * v[2] + c_gauss[1] * v[3] + c_gauss[2] * v[4] + c_gauss[3] * v[5] + c_gauss[4] * v[6] + c_gauss[5] * v[7] + c_gauss[6] * v[8];
-        o.w = c_gauss[0] * v[3] + c_gauss[1] * v[4] + c_gauss[2] * v[5] + c_gauss[3] * v[6] + c_gauss[4] * v[7] + c_gauss[5] * v[8] + c_gauss[6] * v[9];
-        s_row[i] = o;
+        s_pair[i] = make_uint4(o[0], o[1], o[2], o[3]);
     }
+    // column taps as u16 pairs
+    const uint32_t C01 = (uint32_t)c_gauss[0] | ((uint32_t)c_gauss[1] << 16);
+    const uint32_t C23 = (uint32_t)c_gauss[2] | ((uint32_t)c_gauss[3] << 16);
+    const uint32_t C45 = (uint32_t)c_gauss[4] | ((uint32_t)c_gauss[5] << 16);
+    const uint32_t C6_ = (uint32_t)c_gauss[6];
+    const uint32_t C_0 = (uint32_t)c_gauss[0] << 16;
+    const uint32_t C12 = (uint32_t)c_gauss[1] | ((uint32_t)c_gauss[2] << 16);
+    const uint32_t C34 = (uint32_t)c_gauss[3] | ((uint32_t)c_gauss[4] << 16);
+    const uint32_t C56 = (uint32_t)c_gauss[5] | ((uint32_t)c_gauss[6] << 16);
     __syncthreads();
-    for (int i = threadIdx.x; i < BT_H * (BT_W / 4); i += 256) {
-        const int r = i / (BT_W / 4), q = i - r * (BT_W / 4);
-        const int y = y0 + r, x = x0 + 4 * q;
+    for (int i = threadIdx.x; i < (BT_H / 2) * (BT_W / 4); i += 256) {
+        const int p = i / (BT_W / 4), q = i - p * (BT_W / 4);
+        const int y = y0 + 2 * p, x = x0 + 4 * q;
         if (y >= tl.h || x >= tl.w) continue;
-        int4 acc = make_int4(0, 0, 0, 0);
+        const uint4 a = s_pair[(p + 0) * (BT_W / 4) + q], bq = s_pair[(p + 1) * (BT_W / 4) + q];
+        const uint4 c = s_pair[(p + 2) * (BT_W / 4) + q], d = s_pair[(p + 3) * (BT_W / 4) + q];
+        const uint32_t A[4] = {a.x, a.y, a.z, a.w}, B[4] = {bq.x, bq.y, bq.z, bq.w};
+        const uint32_t Cc[4] = {c.x, c.y, c.z, c.w}, D[4] = {d.x, d.y, d.z, d.w};
+        uint32_t ev = 0, od = 0;
 #pragma unroll
-        for (int k = 0; k < 7; k++) {
-            const int4 t = s_row[(r + k) * (BT_W / 4) + q];
-            acc.x += c_gauss[k] * t.x; acc.y += c_gauss[k] * t.y;
-            acc.z += c_gauss[k] * t.z; acc.w += c_gauss[k] * t.w;
+        for (int j = 0; j < 4; j++) {
+            const uint32_t se = dot2u(D[j], C6_, dot2u(Cc[j], C45, dot2u(B[j], C23, dot2u(A[j], C01, 0u))));
+            const uint32_t so = dot2u(D[j], C56, dot2u(Cc[j], C34, dot2u(B[j], C12, dot2u(A[j], C_0, 0u))));
+            // every term is >= 0, so saturate_cast<uchar> is an unsigned min
+            ev |= min((se + (1u << 15)) >> 16, 255u) << (8 * j);
+            od |= min((so + (1u << 15)) >> 16, 255u) << (8 * j);
         }
-        // every term is >= 0, so saturate_cast<uchar> is an unsigned min.  (The signed
-        // min(max(.,0),255) form is lowered by hipcc to v_ashr_pk_u8_i32 pairs whose
-        // destination high half is not cleared before the following v_or3_b32.)
-        const uint32_t px = min((uint32_t)(acc.x + (1 << 15)) >> 16, 255u) |
-                            (min((uint32_t)(acc.y + (1 << 15)) >> 16, 255u) << 8) |
-                            (min((uint32_t)(acc.z + (1 << 15)) >> 16, 255u) << 16) |
-                            (min((uint32_t)(acc.w + (1 << 15)) >> 16, 255u) << 24);
-        *reinterpret_cast<uint32_t*>(O + (size_t)y * tl.bpitch + x) = px;
+        *reinterpret_cast<uint32_t*>(O + (size_t)y * tl.bpitch + x) = ev;
+        if (y + 1 < tl.h) *reinterpret_cast<uint32_t*>(O + (size_t)(y + 1) * tl.bpitch + x) = od;
     }
 }
 
@@ -538,85 +681,29 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     ORBGPU_PROF_MARK(3);
 }
 
-// Per image: concatenate the cell outputs of every level in cell order
-// (= the reference's vToDistributeKeys order) into one packed list.
-// Header per image: [total][cnt_l0..cnt_lL-1][base] in hdr.
-__global__ void __launch_bounds__(1024) k_compact(const uint32_t* __restrict__ slots, size_t slots_per_image,
-                                                  const int* __restrict__ counts, const CellDesc* __restrict__ cells,
-                                                  int ncells, const int* __restrict__ level_cell_begin, int nlevels,
-                                                  uint32_t* __restrict__ packed, int* __restrict__ hdr,
-                                                  int* __restrict__ g_total, int packed_cap) {
-    __shared__ int s_off[4096 + 1];
-    __shared__ int s_base;
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int* cnt = counts + (size_t)b * ncells;
-    // exclusive scan of counts over cells (ncells <= 4096): 4 per thread + wave scans
-    __shared__ int s_wsum[16];
-    int v[4], loc = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int i = tid * 4 + k;
-        v[k] = i < ncells ? cnt[i] : 0;
-        loc += v[k];
-    }
-    const int lane0 = tid & 63, w0 = tid >> 6;
-    int incl = loc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o, 64);
-        if (lane0 >= o) incl += y;
-    }
-    if (lane0 == 63) s_wsum[w0] = incl;
-    __syncthreads();
-    int wpre = 0;
-    for (int w = 0; w < w0; w++) wpre += s_wsum[w];
-    int run = wpre + incl - loc;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int i = tid * 4 + k;
-        if (i < ncells) s_off[i] = run;
-        run += v[k];
-    }
-    if (tid == 1023) s_off[ncells] = run;  // total (tid 1023 holds the block total)
-    __syncthreads();
-    if (tid == 0) {
-        const int total = s_off[ncells];
-        int base = atomicAdd(g_total, total);
-        if (base + total > packed_cap) base = -1;
-        s_base = base;
-        int* H = hdr + (size_t)b * (nlevels + 2);
-        H[0] = total;
-        for (int l = 0; l < nlevels; l++) H[1 + l] = s_off[level_cell_begin[l + 1]] - s_off[level_cell_begin[l]];
-        H[nlevels + 1] = base;
-    }
-    __syncthreads();
-    const int base = s_base;
-    if (base < 0) return;
-    const uint32_t* S = slots + (size_t)b * slots_per_image;
-    // one wave per cell
-    const int lane = tid & 63, wid = tid >> 6;
-    for (int c = wid; c < ncells; c += 16) {
-        const int n = s_off[c + 1] - s_off[c];
-        const uint32_t* src = S + cells[c].slot_off;
-        uint32_t* dst = packed + base + s_off[c];
-        for (int k = lane; k < n; k += 64) dst[k] = src[k];
-    }
-}
-
-// IC_Angle (unblurred level) + rotated BRIEF (blurred level), one wave per
-// keypoint.  Moments are exact integer sums (order-free); the 256 tests of
-// lane l are pairs l, l+64, l+128, l+192, so the four wave ballots ARE the
-// 32 descriptor bytes (byte i bit k = pair 8i+k, little endian).
+// IC_Angle (unblurred level) + rotated BRIEF (blurred level), one wave per keypoint.
+//   IC_Angle   lane = (disc row v, half): the row's 16 pixels u in [-15, 0] (half 0) or [1, 16]
+//              (half 1) are one unaligned 16-byte load (5 dwords, v_alignbyte), masked to
+//              |u| <= umax[|v|]; sum I and sum i*I (i = byte index) are v_sad_u8 / v_dot4_u32_u8,
+//              so m_10 = sum u*I and m_01 = sum v*I are two wave sums.  Exact integer moments:
+//              the same as the reference's loops (ORBextractor.cc:77-103) in any order.
+//   BRIEF      the 37 x 37 blurred patch around the keypoint (every rotated test lies within 18
+//              px) is staged in LDS with row-coalesced dword loads, then the 512 tests of the 256
+//              pairs are LDS byte reads: lane l evaluates pairs l, l+64, l+128, l+192, so the
+//              four wave ballots ARE the 32 descriptor bytes (byte i bit k = pair 8i+k).
+//              Keypoints are >= 19 px inside their level (FAST's 3-px frame inside the 16-px
+//              cell border), so the patch never leaves the blurred level.
+constexpr int kBriefR = 18, kBriefRows = 2 * kBriefR + 1, kBriefLd = 40;   // patch rows, LDS row bytes
 __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                      size_t img_bytes, size_t blur_bytes, const int2* __restrict__ sel, int selcap,
                                                      const int* __restrict__ nout, const LevelDev* __restrict__ lv,
                                                      orb_kp_dev* __restrict__ kps, uint8_t* __restrict__ desc,
                                                      int cap_per_image, int gx, int B) {
+    __shared__ uint32_t s_patch[4][kBriefRows * kBriefLd / 4];
     // batches of >= 8 images: workgroup g runs on XCD g % 8, and image b's keypoint groups all
     // go to XCD b % 8 (images in turn), so the level and blurred-level lines their patches
     // share stay in that XCD's L2; smaller batches spread every image over all XCDs
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int img, grp;
     if (B >= 8) {
         const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -627,8 +714,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         grp = blockIdx.x - img * gx;
     }
     if (img >= B) return;
-    const int k = grp * 4 + (threadIdx.x >> 6);
-    if (k >= nout[img] || k >= cap_per_image) return;
+    const int k = grp * 4 + wv;
+    if (k >= nout[img] || k >= cap_per_image) return;   // wave-uniform: no barrier below
     const int2 s = sel[(size_t)img * selcap + k];
     const uint32_t pk = (uint32_t)s.x;
     const int meta = s.y;
@@ -636,13 +723,52 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     const int x = (int)(pk & 0xfff) + (kEdge - 3), y = (int)((pk >> 12) & 0xfff) + (kEdge - 3);
     const int score = (int)(pk >> 24);
     const LevelDev L = lv[l];
-    const uint8_t* cimg = pyr + (size_t)b * img_bytes + L.off + (size_t)(kEdge + y) * L.pitch + kEdge + x;
-    int m01 = 0, m10 = 0;
-    for (int i = lane; i < c_ndisc; i += 64) {
-        const int u = c_disc[2 * i], v = c_disc[2 * i + 1];
-        const int val = cimg[v * L.pitch + u];
-        m10 += u * val;
-        m01 += v * val;
+    // stage the blurred patch (rows y-18 .. y+18, dword columns from (x-18) & ~3) first: its
+    // loads are in flight during the moments
+    const int c0 = (x - kBriefR) & ~3, mis = (x - kBriefR) - c0;
+    const uint8_t* cbase = blur + (size_t)b * blur_bytes + L.boff + (size_t)(y - kBriefR) * L.bpitch + c0;
+    uint32_t* sp = s_patch[wv];
+    constexpr int kPatchWords = kBriefRows * (kBriefLd / 4);
+    uint32_t pv[(kPatchWords + 63) / 64];
+#pragma unroll
+    for (int t = 0; t < (kPatchWords + 63) / 64; t++) {
+        const int i = lane + 64 * t;
+        const int r = i / (kBriefLd / 4), q = i - r * (kBriefLd / 4);
+        pv[t] = (i < kPatchWords && c0 + 4 * q < L.bpitch)
+                    ? *reinterpret_cast<const uint32_t*>(cbase + (size_t)r * L.bpitch + 4 * q) : 0u;
+    }
+    // IC_Angle moments
+    int m10 = 0, m01 = 0;
+    if (lane < 2 * kPatch) {
+        const int v = (lane >> 1) - kHalfPatch, h = lane & 1;
+        const int d = c_umax[v < 0 ? -v : v];
+        const uint8_t* row = pyr + (size_t)b * img_bytes + L.off + (size_t)(kEdge + y + v) * L.pitch + kEdge + x
+                             - kHalfPatch + 16 * h;   // pixel u = -15 + 16 h + i at byte i
+        const uintptr_t a = (uintptr_t)row;
+        const uint32_t* a32 = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint32_t w0 = a32[0], w1 = a32[1], w2 = a32[2], w3 = a32[3], w4 = sh ? a32[4] : 0u;
+        uint32_t px[4] = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                          __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+        // valid bytes: half 0 i >= 15 - d (u >= -d), half 1 i <= d - 1 (u <= d)
+        const int lo = h ? 0 : kHalfPatch - d, hi = h ? d : 16;   // [lo, hi)
+        uint32_t S = 0, T = 0;
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const int a0 = min(max(lo - 4 * m, 0), 4), a1 = min(max(hi - 4 * m, 0), 4);   // bytes [a0, a1)
+            const uint32_t mk = a1 <= a0 ? 0u : ((a1 == 4 ? 0xffffffffu : ((1u << (8 * a1)) - 1u)) & ~((1u << (8 * a0)) - 1u));
+            const uint32_t w = px[m] & mk;
+            const uint32_t W = (uint32_t)(4 * m) * 0x01010101u + 0x03020100u;   // byte weights 4m .. 4m+3
+            S = __builtin_amdgcn_sad_u8(w, 0u, S);
+            T = __builtin_amdgcn_udot4(w, W, T, false);
+        }
+        m10 = (int)T + (h ? (int)S : -kHalfPatch * (int)S);
+        m01 = v * (int)S;
+    }
+#pragma unroll
+    for (int t = 0; t < (kPatchWords + 63) / 64; t++) {
+        const int i = lane + 64 * t;
+        if (i < kPatchWords) sp[i] = pv[t];
     }
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
@@ -651,15 +777,15 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     float sa, ca;
     glibc_sincosf(angle * factorPI, &sa, &ca);
     const float a = ca, bb = sa;
-    const uint8_t* cb = blur + (size_t)b * blur_bytes + L.boff + (size_t)y * L.bpitch + x;
+    const uint8_t* cb = reinterpret_cast<const uint8_t*>(sp) + kBriefR * kBriefLd + mis + kBriefR;
     uint64_t words[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int p = lane + 64 * q;
         const float x0 = (float)c_pattern[4 * p], y0 = (float)c_pattern[4 * p + 1];
         const float x1 = (float)c_pattern[4 * p + 2], y1 = (float)c_pattern[4 * p + 3];
-        const int t0 = cb[cv_round(x0 * bb + y0 * a) * L.bpitch + cv_round(x0 * a - y0 * bb)];
-        const int t1 = cb[cv_round(x1 * bb + y1 * a) * L.bpitch + cv_round(x1 * a - y1 * bb)];
+        const int t0 = cb[cv_round(x0 * bb + y0 * a) * kBriefLd + cv_round(x0 * a - y0 * bb)];
+        const int t1 = cb[cv_round(x1 * bb + y1 * a) * kBriefLd + cv_round(x1 * a - y1 * bb)];
         words[q] = __ballot(t0 < t1);
     }
     const size_t o = (size_t)b * cap_per_image + idx;
@@ -735,7 +861,10 @@ void Extractor::release() {
     F(d_in_); F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_work_); F(d_groups_);
     F(d_lcb_); F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_);
     F(d_kps_); F(d_desc_); F(d_jobsel_); F(d_jobcnt_); F(d_octlv_); F(d_gscr_); F(d_nout_); F(d_ptiles_);
+    F(d_chain_); F(d_cellslot_);
     d_ptiles_ = nullptr;
+    d_chain_ = nullptr;
+    d_cellslot_ = nullptr;
     d_jobsel_ = d_jobcnt_ = d_octlv_ = d_gscr_ = d_nout_ = nullptr;
     d_in_ = d_pyr_ = d_blur_ = nullptr;
     d_slots_ = nullptr; d_counts_ = nullptr; d_cells_ = nullptr; d_tiles_ = nullptr; d_work_ = nullptr; d_groups_ = nullptr;
@@ -797,6 +926,9 @@ int Extractor::init_device(int maxW, int maxH, int maxBatch) {
     const int nd = (int)disc.size() / 2;
     ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_disc), disc.data(), disc.size()));
     ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_ndisc), &nd, sizeof(int)));
+    int um[16];
+    for (int v = 0; v <= kHalfPatch; v++) um[v] = v == 0 ? kHalfPatch : umax_[v];
+    ORB_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), um, sizeof(um)));
     maxW_ = maxW; maxH_ = maxH; maxB_ = maxBatch;
     return 0;
 }
@@ -880,6 +1012,142 @@ void Extractor::gaussian_taps(int taps[7]) {
         cf[i] = (float)(cf[i] * sum);
         taps[i] = (int)std::lrint(cf[i] * 256.0f);
     }
+}
+
+// Plan of k_pyr_chain (levels la .. nlevels-1; yr[l] = level l's row map, 2 ints per row):
+// K row strips per image, the fewest (at least kChainMinStrips) whose LDS -- the staged source
+// rows of level la-1, two level buffers, the row taps -- fits kChainLdsMax.  Own rows: level
+// nlevels-1 split evenly, level l's strip boundaries the images of level l+1's under the row
+// map.  Compute rows: own rows plus every row the level above's compute rows read.  Padded rows:
+// each goes to the strip owning the interior row it reflects to.  Every range is checked here,
+// so the kernel's indexing stays inside its buffers.  Opt-in: ORBGPU_PYR_CHAIN=1.
+int Extractor::plan_chain(const std::vector<std::vector<int>>& yr) {
+    chain_ = false;
+    chainTab_.clear();
+    static const bool off = [] {   // opt-in (ORBGPU_PYR_CHAIN=1): slower than the per-level
+        const char* e = getenv("ORBGPU_PYR_CHAIN");   // launches so far
+        return !(e && e[0] == '1');
+    }();
+    // the first chained level (ORBGPU_PYR_CHAIN_FROM, default 3): levels 1 .. la-1 keep their
+    // own k_pyr_resize launches (large levels, bandwidth-bound tiles)
+    static const int from = [] {
+        const char* e = getenv("ORBGPU_PYR_CHAIN_FROM");
+        return e ? std::max(1, atoi(e)) : 3;
+    }();
+    const int la = from, lb = nlevels_ - 1, nl = lb - la + 1;
+    if (off || la > lb) return 0;
+    for (int l = la; l <= lb; l++)
+        if (((levels_[l].w + 3) >> 2) > 256) return 0;   // one 4-column group per thread
+    const int hTop = levels_[lb].h;
+    std::vector<int> rp(nlevels_);
+    for (int l = 0; l < nlevels_; l++) rp[l] = (levels_[l].w + 3) & ~3;
+    const int srcRp = (levels_[la - 1].w + 6 + 3) & ~3;   // padded columns [16, 16 + srcRp) staged
+    constexpr int kChainMinStrips = 8;
+    for (int K = std::min(kChainMinStrips, hTop); K <= std::min(hTop, 256); K++) {
+        // own boundaries A[l][0..K]
+        std::vector<std::vector<int>> A(nlevels_, std::vector<int>(K + 1));
+        for (int k = 0; k <= K; k++) A[lb][k] = (int)(((long long)k * hTop) / K);
+        for (int l = lb - 1; l >= 0; l--) {
+            A[l][0] = 0;
+            A[l][K] = levels_[l].h;
+            for (int k = 1; k < K; k++) A[l][k] = yr[l + 1][2 * A[l + 1][k]];
+        }
+        bool ok = true;
+        for (int l = la; l <= lb && ok; l++)
+            for (int k = 0; k < K; k++)
+                if (A[l][k] >= A[l][k + 1]) ok = false;   // every strip owns rows on every level
+        if (!ok) break;
+        // compute ranges; source rows of level la-1
+        std::vector<std::vector<std::pair<int, int>>> C(K, std::vector<std::pair<int, int>>(nlevels_));
+        std::vector<std::pair<int, int>> Src(K);
+        size_t buf[2] = {0, 0}, srcBytes = 0, rtRows = 0;
+        for (int k = 0; k < K; k++) {
+            C[k][lb] = {A[lb][k], A[lb][k + 1]};
+            for (int l = lb - 1; l >= la; l--) {
+                const auto& u = C[k][l + 1];
+                const int lo = std::min(yr[l + 1][2 * u.first], A[l][k]);
+                const int hi = std::max(yr[l + 1][2 * (u.second - 1) + 1] + 1, A[l][k + 1]);
+                C[k][l] = {lo, hi};
+            }
+            size_t rows = 0;
+            for (int l = la; l <= lb; l++) {
+                const auto& c = C[k][l];
+                if (c.first < 0 || c.second > levels_[l].h || c.first >= c.second) return -1;
+                if (c.first > 0xffff || c.second > 0xffff) return -1;   // row taps packed in 16 bits
+                const auto p = l > la ? C[k][l - 1] : std::make_pair(0, 0);
+                int smin = 1 << 30, smax = -1;
+                for (int dy = c.first; dy < c.second; dy++) {
+                    smin = std::min(smin, yr[l][2 * dy]);
+                    smax = std::max(smax, yr[l][2 * dy + 1]);
+                    // the rows level l reads from level l-1 lie in that level's buffer
+                    if (l > la && (yr[l][2 * dy] < p.first || yr[l][2 * dy + 1] >= p.second)) return -1;
+                }
+                if (l == la) Src[k] = {smin, smax + 1};
+                const size_t bytes = (size_t)(c.second - c.first) * rp[l] + 16;
+                buf[(l - la) & 1] = std::max(buf[(l - la) & 1], bytes);
+                rows += (size_t)(c.second - c.first);
+            }
+            srcBytes = std::max(srcBytes, (size_t)(Src[k].second - Src[k].first) * srcRp + 16);
+            rtRows = std::max(rtRows, rows);
+        }
+        const size_t o1 = (srcBytes + 15) & ~(size_t)15, o2 = o1 + ((buf[0] + 15) & ~(size_t)15),
+                     o3 = o2 + ((buf[1] + 15) & ~(size_t)15);
+        const size_t lds = o3 + rtRows * 8;
+        if (lds > (size_t)kChainLdsMax) continue;
+        // tables: levels | strips (nl + 1 entries per strip) | padded-row lists
+        std::vector<ChainLevel> cl(nl);
+        std::vector<int32_t> strips((size_t)4 * K * (nl + 1));
+        std::vector<uint16_t> rowl;
+        for (int l = la; l <= lb; l++) {
+            ChainLevel& c = cl[l - la];
+            const LevelHost& L = levels_[l];
+            if (L.ph > 65535) return -1;
+            c.off = (long long)L.off;
+            c.w = L.w; c.h = L.h; c.pitch = L.pitch; c.rp = rp[l];
+            c.lds = ((l - la) & 1) ? (int)o2 : (int)o1;
+            c.xofs = (int)tab_off_[l][0]; c.xal = (int)tab_off_[l][1];
+            c.yr = (int)tab_off_[l][2]; c.yb = (int)tab_off_[l][3];
+            c.nph = std::max(1, 256 / ((L.w + 3) >> 2));
+            std::vector<std::vector<uint16_t>> own(K);
+            for (int py = 0; py < L.ph; py++) {
+                int y = py - kEdge;
+                if (L.h == 1) y = 0;
+                while (y < 0 || y >= L.h) y = y < 0 ? -y : 2 * L.h - y - 2;
+                const int k = (int)(std::upper_bound(A[l].begin(), A[l].end(), y) - A[l].begin()) - 1;
+                own[k].push_back((uint16_t)py);
+            }
+            for (int k = 0; k < K; k++) {
+                int32_t* e = &strips[((size_t)k * (nl + 1) + (l - la)) * 4];
+                e[0] = C[k][l].first;
+                e[1] = C[k][l].second;
+                e[2] = (int32_t)rowl.size();
+                e[3] = (int32_t)own[k].size();
+                rowl.insert(rowl.end(), own[k].begin(), own[k].end());
+            }
+        }
+        for (int k = 0; k < K; k++) {
+            int32_t* e = &strips[((size_t)k * (nl + 1) + nl) * 4];
+            e[0] = Src[k].first;
+            e[1] = Src[k].second;
+            e[2] = (int32_t)o3;
+            e[3] = 0;
+            if (Src[k].first < 0 || Src[k].second > levels_[la - 1].h) return -1;
+        }
+        chainK_ = K;
+        chainFrom_ = la;
+        chainLds_ = (int)lds;
+        chainSrcLds_ = 0;
+        chainSrcRp_ = srcRp;
+        chainStripOff_ = (sizeof(ChainLevel) * nl + 15) & ~(size_t)15;
+        chainRowOff_ = chainStripOff_ + strips.size() * 4;
+        chainTab_.assign(chainRowOff_ + rowl.size() * 2, 0);
+        std::memcpy(chainTab_.data(), cl.data(), sizeof(ChainLevel) * nl);
+        std::memcpy(chainTab_.data() + chainStripOff_, strips.data(), strips.size() * 4);
+        std::memcpy(chainTab_.data() + chainRowOff_, rowl.data(), rowl.size() * 2);
+        chain_ = true;
+        return 0;
+    }
+    return 0;   // no plan fits: a launch per level
 }
 
 // Geometry of the pyramid / cells / resize tables for an image size.
@@ -1028,6 +1296,9 @@ int Extractor::setup_geometry(int W, int H) {
         return o;
     };
     tab_off_.assign(nlevels_, {0, 0, 0, 0});
+    std::vector<std::vector<int>> yrAll(nlevels_);   // every level's row map, for plan_chain
+    xofsAll_.assign(nlevels_, {});
+    xalAll_.assign(nlevels_, {});
     ptiles_.clear();
     ptile_begin_.assign(nlevels_ + 1, 0);
     plds_.assign(nlevels_, 0);
@@ -1113,18 +1384,29 @@ int Extractor::setup_geometry(int W, int H) {
                 }
             plds_[l] = (int)lds;
         }
+        yrAll[l] = yr;
+        xofsAll_[l] = xofs;
+        xalAll_[l] = xal;
         tab_off_[l][0] = push(xofs.data(), xofs.size() * 4);
         tab_off_[l][1] = push(xal.data(), xal.size() * 2);
         tab_off_[l][2] = push(yr.data(), yr.size() * 4);
         tab_off_[l][3] = push(yb.data(), yb.size() * 2);
     }
     ptile_begin_[nlevels_] = (int)ptiles_.size();
+    if (plan_chain(yrAll)) return -1;
     // (re)allocate device buffers for maxB_
     auto F = [](void*& p) { if (p) (void)hipFree(p); p = nullptr; };
     F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_lcb_); F(d_work_); F(d_groups_);
+    F(d_cellslot_);
     work_B_ = -1;
     F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_); F(d_ptiles_);
     const int B = maxB_;
+    if (d_chain_) (void)hipFree(d_chain_);
+    d_chain_ = nullptr;
+    if (chain_) {
+        ORB_HIP_CHECK(hipMalloc(&d_chain_, chainTab_.size()));
+        ORB_HIP_CHECK(hipMemcpy(d_chain_, chainTab_.data(), chainTab_.size(), hipMemcpyHostToDevice));
+    }
     ORB_HIP_CHECK(hipMalloc(&d_ptiles_, std::max<size_t>(ptiles_.size(), 1) * sizeof(PyrTile)));
     if (!ptiles_.empty())
         ORB_HIP_CHECK(hipMemcpy(d_ptiles_, ptiles_.data(), ptiles_.size() * sizeof(PyrTile), hipMemcpyHostToDevice));
@@ -1139,9 +1421,16 @@ int Extractor::setup_geometry(int W, int H) {
     ORB_HIP_CHECK(hipMemcpy(d_groups_, groups_.data(), groups_.size() * sizeof(CellGroup), hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMalloc(&d_tiles_, tiles_.size() * sizeof(BlurTile)));
     ORB_HIP_CHECK(hipMemcpy(d_tiles_, tiles_.data(), tiles_.size() * sizeof(BlurTile), hipMemcpyHostToDevice));
+    {
+        std::vector<int> cs(cells_.size());
+        for (size_t c = 0; c < cells_.size(); c++) cs[c] = cells_[c].slot_off;
+        ORB_HIP_CHECK(hipMalloc(&d_cellslot_, std::max<size_t>(cs.size(), 1) * 4));
+        ORB_HIP_CHECK(hipMemcpy(d_cellslot_, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
+    }
     ORB_HIP_CHECK(hipMalloc(&d_lcb_, level_cell_begin_.size() * 4));
     ORB_HIP_CHECK(hipMemcpy(d_lcb_, level_cell_begin_.data(), level_cell_begin_.size() * 4, hipMemcpyHostToDevice));
-    packed_cap_ = (int)std::min<size_t>(slots_per_image_ * B, (size_t)1 << 30);
+    if (slots_per_image_ * B > ((size_t)1 << 30)) return -1;   // k_octree's per-level ranges of packed
+    packed_cap_ = (int)(slots_per_image_ * B);
     ORB_HIP_CHECK(hipMalloc(&d_packed_, (size_t)packed_cap_ * 4));
     ORB_HIP_CHECK(hipMalloc(&d_hdr_, (size_t)B * (nlevels_ + 2) * 4 + 64));
     d_gtotal_ = (int*)((char*)d_hdr_ + (size_t)B * (nlevels_ + 2) * 4);
@@ -1221,7 +1510,8 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
         const int n = (L0.pitch / 16) * L0.ph;
         hipLaunchKernelGGL(k_pyr_level0, dim3((n + 255) / 256, B), dim3(256), 0, s, src, img_stride, step, W, H,
                            (uint8_t*)d_pyr_, img_bytes_, L0.pitch, L0.ph, d_gtotal_, (int*)d_nout_ + B);
-        for (int l = 1; l < nlevels_; l++) {
+        const int lend = chain_ && !split ? chainFrom_ : nlevels_;   // levels [1, lend) one launch each
+        for (int l = 1; l < lend; l++) {
             if (split && l == kFastSplitLevel) {
                 ORB_HIP_CHECK(hipEventRecord(evPyrA_, s));
                 ORB_HIP_CHECK(hipStreamWaitEvent(side_, evPyrA_, 0));
@@ -1239,6 +1529,14 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
                                (const int*)(T + tab_off_[l][0]), (const short2*)(T + tab_off_[l][1]),
                                (const int2*)(T + tab_off_[l][2]), (const short2*)(T + tab_off_[l][3]),
                                (const PyrTile*)d_ptiles_ + ptile_begin_[l], nt);
+        }
+        if (lend < nlevels_) {
+            const uint8_t* T = (const uint8_t*)d_chain_;
+            const LevelHost& P = levels_[lend - 1];
+            hipLaunchKernelGGL(k_pyr_chain, dim3(chainK_, B), dim3(256), chainLds_, s, (uint8_t*)d_pyr_, img_bytes_,
+                               (long long)P.off, P.pitch, P.w, (const ChainLevel*)T, nlevels_ - lend,
+                               (const int4*)(T + chainStripOff_), (const uint16_t*)(T + chainRowOff_),
+                               (const uint8_t*)d_tabs_, chainSrcLds_, chainSrcRp_);
         }
     }
     ORB_HIP_CHECK(hipGetLastError());
@@ -1264,18 +1562,15 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     }
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[3], s));
-    // 3. compaction
-    hipLaunchKernelGGL(k_compact, dim3(B), dim3(1024), 0, s, (const uint32_t*)d_slots_, slots_per_image_,
-                       (const int*)d_counts_, (const CellDesc*)d_cells_, ncells, (const int*)d_lcb_, nlevels_,
-                       (uint32_t*)d_packed_, (int*)d_hdr_, d_gtotal_, packed_cap_);
-    ORB_HIP_CHECK(hipGetLastError());
+    // 3-4. per (image, level): compaction of the level's cell outputs, DistributeOctTree, then the
+    //      per-image selected lists, on the device (k_octree compacts its own level)
     ORB_HIP_CHECK(hipEventRecord(ev_[4], s));
-    // 4. DistributeOctTree per (image, level) + per-image selected lists, on the device
     int* d_err = (int*)d_nout_ + B;
-    if (int e = octree_launch((const uint32_t*)d_packed_, (const int*)d_hdr_, B, nlevels_,
-                              (const OctLevelDev*)d_octlv_, (uint32_t*)d_jobsel_, (int*)d_jobcnt_, jcap_,
-                              (uint16_t*)d_gscr_, (size_t)packed_cap_, cap, (int2*)d_sel_, selcap_, (int*)d_nout_,
-                              d_err, s))
+    OctInput oin{(const uint32_t*)d_slots_, slots_per_image_, (const int*)d_counts_, (const int*)d_cellslot_,
+                 (const int*)d_lcb_, ncells, (uint32_t*)d_packed_, d_gtotal_};
+    if (int e = octree_launch(oin, B, nlevels_, (const OctLevelDev*)d_octlv_, (uint32_t*)d_jobsel_, (int*)d_jobcnt_,
+                              jcap_, (uint16_t*)d_gscr_, (size_t)packed_cap_, cap, (int2*)d_sel_, selcap_,
+                              (int*)d_nout_, d_err, s))
         return e;
     ORB_HIP_CHECK(hipEventRecord(ev_[5], s));
     // 5. blur: GaussianBlur of every level (ORBextractor.cc:1085-1086); on the side stream it
@@ -1332,7 +1627,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
 
 int Extractor::corner_total(long long* total) {
     if (last_B_ <= 0 || !d_gtotal_) return -1;
-    int v = 0;   // k_compact's atomic total over the batch (d_gtotal_), read after the call
+    int v = 0;   // k_octree's atomic total over the batch (d_gtotal_), read after the call
     ORB_HIP_CHECK(hipStreamSynchronize(stream_));
     ORB_HIP_CHECK(hipMemcpy(&v, d_gtotal_, 4, hipMemcpyDeviceToHost));
     *total = v;

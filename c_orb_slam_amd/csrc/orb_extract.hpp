@@ -52,6 +52,15 @@ struct PyrTile {
     int py0, px0, nrow, sr0, nsr, sc0, nsw, pad;
 };
 
+// k_pyr_chain: the levels [1, nlevels) of the pyramid in one launch, one workgroup per
+// (row strip, image).  Per chained level: its padded geometry, the LDS buffer its computed rows
+// live in (ping-pong between two buffers) and its resize tables (byte offsets into d_tabs_).
+struct ChainLevel {
+    long long off;
+    int w, h, pitch, rp, lds, xofs, xal, yr, yb, nph;   // nph: threads per column group (row phases)
+};
+constexpr int kChainLdsMax = 64 * 1024;
+
 struct LevelDev {
     long long off, boff;
     int pitch, bpitch;
@@ -114,6 +123,17 @@ private:
     std::vector<BlurTile> tiles_;
     std::vector<PyrTile> ptiles_;
     std::vector<int> ptile_begin_, plds_;
+    // the chained pyramid (plan_chain): strips per image, dynamic LDS, device tables
+    // [ChainLevel x (nlevels-1) | int4 strip ranges x K x (nlevels-1) | u16 padded rows]
+    int plan_chain(const std::vector<std::vector<int>>& yr);
+    bool chain_ = false;
+    int chainK_ = 0, chainLds_ = 0, chainFrom_ = 0, chainSrcLds_ = 0, chainSrcRp_ = 0;
+    std::vector<std::vector<int>> xofsAll_;     // every level's column map and taps (plan_chain)
+    std::vector<std::vector<short>> xalAll_;
+    size_t chainStripOff_ = 0, chainRowOff_ = 0;
+    std::vector<uint8_t> chainTab_;
+    void* d_chain_ = nullptr;
+    void* d_cellslot_ = nullptr;   // slot offset of every cell (k_octree's compaction)
     std::vector<std::array<size_t, 4>> tab_off_;
     size_t img_bytes_ = 0, blur_bytes_ = 0, slots_per_image_ = 0;
     int packed_cap_ = 0, sel_cap_ = 0;

@@ -428,12 +428,10 @@ template <bool LAST, bool STAGE, int NT>
 __global__ void __launch_bounds__(NT) k_candidates(const SearchDev* __restrict__ probs, int np, int gx, float th,
                                                    int bMono, unsigned long long* counters) {
     ORBGPU_LATENCY_WAVE();
-    // XCD-aware order: workgroups L and L + 8 share an XCD (blocks are dealt round-robin over the
-    // 8 XCDs), so workgroup L takes problem (L % 8) + 8 (L / 8 / gx), block (L / 8) % gx: every
-    // block of a problem runs on one XCD and the frame it stages is fetched into one L2
-    const int xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
-    const int by = xcd + 8 * (slot / gx), bx = slot % gx;
-    if (by >= np) return;
+    // XCD-aware order (xcd_problem_block): every block of a problem runs on one XCD and the
+    // frame it stages is fetched into one L2
+    int by, bx;
+    if (!xcd_problem_block(np, gx, by, bx)) return;
     const SearchDev P = probs[by];
     int nvis = P.nq;
     if (!LAST && P.visList) nvis = *P.visCount;   // SearchLocalPoints: the t-th in-view query
@@ -508,9 +506,8 @@ __global__ void __launch_bounds__(256) k_frustum(const SearchDev* __restrict__ p
     ORBGPU_LATENCY_WAVE();
     // XCD-aware order (as k_candidates): problem p's blocks run on XCD p % 8, where its
     // candidate search and selection then read the query arrays this kernel writes
-    const int xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
-    const int by = xcd + 8 * (slot / gx), bx = slot % gx;
-    if (by >= np) return;
+    int by, bx;
+    if (!xcd_problem_block(np, gx, by, bx)) return;
     const SearchDev& P = probs[by];
     const FrustumDev& Fq = frs[by];
     const int j = bx * blockDim.x + threadIdx.x;
@@ -1112,7 +1109,7 @@ void* Matcher::arena_alloc(size_t bytes) {
 
 // k_candidates' XCD-aware 1-D grid: gx blocks per problem, problems dealt to the 8 XCDs
 static inline int cand_gx(int maxq, int nt) { return (maxq + nt - 1) / nt; }
-static inline dim3 cand_grid(int maxq, int nt, int np) { return dim3(8 * cand_gx(maxq, nt) * ((np + 7) / 8)); }
+static inline dim3 cand_grid(int maxq, int nt, int np) { return xcd_grid(cand_gx(maxq, nt), np); }
 
 int Matcher::run(std::vector<SearchDev>& probs, float th, bool bMono, bool lastMode, float nnratio) {
     const int np = (int)probs.size();

@@ -100,12 +100,11 @@ __device__ __forceinline__ unsigned group_min_u(unsigned v) {
 __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restrict__ probs, StereoParams P,
                                                       unsigned long long* counters, int np, int gx) {
     ORBGPU_LATENCY_WAVE();
-    // XCD-aware order (workgroups L and L + 8 share an XCD): every workgroup of a pair runs on one
-    // XCD, so the pair's right keypoints and descriptors, which all its left keypoints scan, and
-    // its pyramid rows are fetched into one L2
-    const int xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
-    const int by = xcd + 8 * (slot / gx), bx = slot % gx;
-    if (by >= np) return;
+    // XCD-aware order (xcd_problem_block): every workgroup of a pair runs on one XCD, so the
+    // pair's right keypoints and descriptors, which all its left keypoints scan, and its pyramid
+    // rows are fetched into one L2
+    int by, bx;
+    if (!xcd_problem_block(np, gx, by, bx)) return;
     const StereoDev& S = probs[by];
     const int sub = threadIdx.x & 15;
     const int iL = bx * 16 + (threadIdx.x >> 4);
@@ -323,7 +322,7 @@ int stereo_launch(const StereoDev* d_probs, int nprob, int maxNL, const StereoPa
     hipLaunchKernelGGL(k_stereo_rows, dim3(nprob), dim3(1024), 0, s, d_probs, P);
     if (timed) tm->mark(5);
     if (maxNL > 0)
-        hipLaunchKernelGGL(k_stereo_match, dim3(8 * ((maxNL + 15) / 16) * ((nprob + 7) / 8)), dim3(256), 0, s, d_probs, P,
+        hipLaunchKernelGGL(k_stereo_match, xcd_grid((maxNL + 15) / 16, nprob), dim3(256), 0, s, d_probs, P,
                            timed ? tm->counters() : nullptr, nprob, (maxNL + 15) / 16);
     if (timed) tm->mark(6);
     hipLaunchKernelGGL(k_stereo_filter, dim3(nprob), dim3(256), 0, s, d_probs);
