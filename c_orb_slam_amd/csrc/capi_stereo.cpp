@@ -86,7 +86,7 @@ int ORBmatcher_ComputeStereoMatches_batch_at(ORBmatcher_h h, ORBextractor_h left
     size_t need = al(sizeof(orbgpu::StereoDev) * npairs) + al(4 * (size_t)npairs);
     int maxNL = 0;
     for (int p = 0; p < npairs; p++) {
-        need += al(4 * (size_t)NL[p]) + al(4 * ((size_t)P.rows0 + 1)) + al(4 * (size_t)NR[p] * band + 4);
+        need += al(4 * (size_t)NL[p]) + al(4 * ((size_t)P.rows0 + 1)) + al(8 * (size_t)NR[p] * band + 8);
         if (!dev) need += al(28 * (size_t)NL[p]) + al(32 * (size_t)NL[p]) + al(28 * (size_t)NR[p]) +
                           al(32 * (size_t)NR[p]) + 2 * al(4 * (size_t)NL[p]);
         maxNL = std::max(maxNL, NL[p]);
@@ -103,7 +103,7 @@ int ORBmatcher_ComputeStereoMatches_batch_at(ORBmatcher_h h, ORBextractor_h left
         S.pyrR = ER->pyramid_base() + (size_t)(first_right + p) * ER->pyramid_image_bytes();
         S.sad = (int*)m->arena_alloc(4 * (size_t)NL[p] + 4);
         S.rowStart = (int*)m->arena_alloc(4 * ((size_t)P.rows0 + 1));
-        S.rowIdx = (int*)m->arena_alloc(4 * (size_t)NR[p] * band + 4);
+        S.rowIdx = (int2*)m->arena_alloc(8 * (size_t)NR[p] * band + 8);
         if (!S.sad || !S.rowStart || !S.rowIdx) return ORB_E_HIP;
         S.kept = d_kept + p;
         if (dev) {

@@ -132,7 +132,10 @@ __global__ void __launch_bounds__(T) k_octree(OctInput in, int nlevels, const Oc
                                                  uint16_t* __restrict__ gscratch, size_t gstride, int* __restrict__ err) {
     __shared__ OctShared S;
     ORBGPU_PROF_START;
-    const int job = blockIdx.x, b = job / nlevels, l = job - b * nlevels;
+    // level-major dispatch order: the long jobs (level 0: the most candidates and features) of
+    // every image start first and the short ones fill in behind them
+    const int B = (int)gridDim.x / nlevels;
+    const int l = (int)blockIdx.x / B, b = (int)blockIdx.x - l * B, job = b * nlevels + l;
     const int tid = threadIdx.x;
     // ---- the level's FAST candidates in cell order (ORBextractor.cc:776-829's push order):
     //      cell offsets by a block scan of the counts (S.ia), then a thread per candidate finds

@@ -96,6 +96,12 @@ __global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ 
 // tile reads (host-computed, PyrTile) is staged into LDS as aligned dwords, then every
 // thread forms 4 adjacent columns of every 4th row (coefficients of its columns held in
 // registers) and stores dwords, a wave covering 256 contiguous bytes of a row.
+// tile heights: 16 rows for small batches (more workgroups per image), 32 for large ones
+// (fewer, longer workgroups: every staging load in flight at once)
+constexpr int kPyrTileH[2] = {16, 32};
+template <int TH>
+constexpr int stage_regs() { return (((TH * 5 + 3) / 4 + 3) * ((PT_W * 5 / 4 + 12) / 4) + 255) / 256; }
+template <int TH>
 __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, size_t img_bytes, size_t src_off,
                                                     int src_pitch, size_t dst_off, int dst_pitch, int dst_ph, int w,
                                                     int h, const int* __restrict__ xofs,
@@ -111,8 +117,23 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, s
     uint8_t* base = pyr + (size_t)b * img_bytes;
     const uint32_t* S32 = reinterpret_cast<const uint32_t*>(base + src_off + (size_t)(kEdge + tl.sr0) * src_pitch + tl.sc0);
     const int spw = src_pitch >> 2;
-    for (int r = wid; r < tl.nsr; r += 4)
-        for (int c = lane; c < tl.nsw; c += 64) s_src[r * tl.nsw + c] = S32[(size_t)r * spw + c];
+    {
+        // the source rectangle as dwords: every load of a thread in flight before its first LDS
+        // store (stage_regs<TH>() per round; one round covers a TH x PT_W tile at scale <= 1.25)
+        const int nw = tl.nsr * tl.nsw;
+        for (int t0 = threadIdx.x; t0 < nw; t0 += 256 * stage_regs<TH>()) {
+            uint32_t v[stage_regs<TH>()];
+#pragma unroll
+            for (int u = 0; u < stage_regs<TH>(); u++) {
+                const int t = t0 + 256 * u;
+                const int r = t / tl.nsw, c = t - r * tl.nsw;
+                v[u] = t < nw ? S32[(size_t)r * spw + c] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < stage_regs<TH>(); u++)
+                if (t0 + 256 * u < nw) s_src[t0 + 256 * u] = v[u];
+        }
+    }
     const int px = tl.px0 + 4 * lane;
     const bool col_ok = px < dst_pitch;
     int lx[4];
@@ -123,11 +144,11 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, s
         lx[k] = col_ok ? xofs[x] + kEdge - tl.sc0 : 0;
         al[k] = col_ok ? xalpha[x] : make_short2(0, 0);
     }
-    // this thread's rows (j = wid, wid+4, ... < nrow <= PT_H): row taps fetched before the barrier
-    int2 rr[PT_H / 4];
-    short2 bb[PT_H / 4];
+    // this thread's rows (j = wid, wid+4, ... < nrow <= TH): row taps fetched before the barrier
+    int2 rr[TH / 4];
+    short2 bb[TH / 4];
 #pragma unroll
-    for (int i = 0; i < PT_H / 4; i++) {
+    for (int i = 0; i < TH / 4; i++) {
         const int j = wid + 4 * i;
         const int y = refl101(tl.py0 + min(j, tl.nrow - 1) - kEdge, h);
         rr[i] = yrows[y];
@@ -138,7 +159,7 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, s
     const uint8_t* sb = reinterpret_cast<const uint8_t*>(s_src);
     const int rowb = tl.nsw * 4;
 #pragma unroll
-    for (int i = 0; i < PT_H / 4; i++) {
+    for (int i = 0; i < TH / 4; i++) {
         const int j = wid + 4 * i;
         if (j >= tl.nrow) break;
         const int py = tl.py0 + j;
@@ -311,11 +332,21 @@ __global__ void __launch_bounds__(256) k_blur7(const uint8_t* __restrict__ pyr, 
     const uint8_t* P = pyr + (size_t)b * img_bytes + tl.off;           // padded level base
     uint8_t* O = blur + (size_t)b * blur_bytes + tl.boff;               // unpadded blurred level
     const int x0 = tl.tx * BT_W, y0 = tl.ty * BT_H;
-    for (int i = threadIdx.x; i < SR * WPR; i += 256) {
-        const int r = i / WPR, wq = i - r * WPR;
-        const int yy = min(y0 + r - 3, tl.h + 2) + kEdge;                 // padded row
-        const int c = min(kEdge - 3 + x0 + 4 * wq, tl.pitch - 4);           // padded col (dword aligned)
-        s_src[i] = *reinterpret_cast<const uint32_t*>(P + (size_t)yy * tl.pitch + c);
+    {
+        // every staging load of a thread in flight before its first LDS store
+        constexpr int NU = (SR * WPR + 255) / 256;
+        uint32_t v[NU];
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int i = threadIdx.x + 256 * u;
+            const int r = i / WPR, wq = i - r * WPR;
+            const int yy = min(y0 + r - 3, tl.h + 2) + kEdge;                 // padded row
+            const int c = min(kEdge - 3 + x0 + 4 * wq, tl.pitch - 4);           // padded col (dword aligned)
+            v[u] = i < SR * WPR ? *reinterpret_cast<const uint32_t*>(P + (size_t)yy * tl.pitch + c) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < NU; u++)
+            if (threadIdx.x + 256 * u < SR * WPR) s_src[threadIdx.x + 256 * u] = v[u];
     }
     const uint32_t TLO = (uint32_t)c_gauss[0] | ((uint32_t)c_gauss[1] << 8) | ((uint32_t)c_gauss[2] << 16) |
                          ((uint32_t)c_gauss[3] << 24);
@@ -506,28 +537,34 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
         if (tid < 4 && g.cell[tid] >= 0) cnt_out[g.cell[tid]] = 0;
         return;
     }
-    // ROI rows staged as aligned dwords: pixel (r, c) sits at LDS byte r*FC_LD + mis + c
-    const uint8_t* P = pyr + (size_t)b * img_bytes + g.lvl_off + (size_t)(kEdge + g.r0) * g.pitch + kEdge + g.c0;
-    const int mis = (int)((uintptr_t)P & 3);
-    const uint32_t* P32 = reinterpret_cast<const uint32_t*>(P - mis);
+    // ROI rows staged as realigned dwords: pixel (r, c) sits at LDS byte r*FC_LD + 1 + c, so the
+    // detection columns 3 + j start on a dword (j = 0) and a lane's 4 columns are one LDS dword.
+    // LDS dword w of a row holds the global bytes Q + 4w .. Q + 4w + 3 (Q = pixel (r, -1)), one
+    // v_alignbyte of two aligned global dwords
+    const uint8_t* Q = pyr + (size_t)b * img_bytes + g.lvl_off + (size_t)(kEdge + g.r0) * g.pitch + kEdge + g.c0 - 1;
+    const int qmis = (int)((uintptr_t)Q & 3);
+    const uint32_t* Q32 = reinterpret_cast<const uint32_t*>(Q - qmis);
     constexpr int ldw = FC_LD / 4;
-    const int wpr = (cols + mis + 3) >> 2, pw = g.pitch >> 2;
+    constexpr int mis = 1;
+    const int wpr = (cols + 4) >> 2, pw = g.pitch >> 2;
     {
         // 3 rows x 19 dwords per wave instruction; rows wid*3 + rr + 12k (k < 6 covers FC_MAXR):
         // every load of the thread is issued before the first LDS store (one wait, not six)
         const int rr = lane / ldw, w = lane - rr * ldw;
         const bool ok = rr < 3 && w < wpr;
-        const uint32_t* gp = P32 + (size_t)(wid * 3 + rr) * pw + w;
-        uint32_t v[6];
+        const uint32_t* gp = Q32 + (size_t)(wid * 3 + rr) * pw + w;
+        uint32_t v[6], v1[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) {
             const int r = wid * 3 + rr + 12 * k;
-            v[k] = (ok && r < rows) ? gp[(size_t)12 * k * pw] : 0u;
+            const bool on = ok && r < rows;
+            v[k] = on ? gp[(size_t)12 * k * pw] : 0u;
+            v1[k] = on ? gp[(size_t)12 * k * pw + 1] : 0u;
         }
 #pragma unroll
         for (int k = 0; k < 6; k++) {
             const int r = wid * 3 + rr + 12 * k;
-            if (ok && r < rows) s_img32[r * ldw + w] = v[k];
+            if (ok && r < rows) s_img32[r * ldw + w] = __builtin_amdgcn_alignbyte(v1[k], v[k], qmis);
         }
     }
     for (int i = tid; i < rows * ldw; i += 256) s_sc32[i] = 0u;
@@ -543,23 +580,44 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
             if (lane == 0) s_mask[i] = m;
         }
     } else {
-        // rows i and i + 4 of the wave in one packed pass (row i + 4 clamped into the ROI when
-        // it is past the last detection row; its mask is then not stored)
+        // 4 detection columns per lane, 16 lanes per row, 4 rows per wave pass (16 per pass): a
+        // lane's pixels are one LDS dword (v), its compass points the dwords 3 rows up / down and
+        // the neighbouring dwords realigned by 3 bytes (v_alignbyte); two packed 16-bit tests
+        // cover the 4 pixels, and the row's 64-bit survivor mask is assembled from the lanes'
+        // nibbles by three DPP ORs within each group of 8 lanes
         const short2v T1 = pk16(tp + 1, tp + 1);
-        for (int i = wid; i < dr; i += 8) {
-            const int i1 = min(i + 4, dr - 1);
-            bool p0 = false, p1 = false;
-            if (lane < dc) {
-                const uint32_t f = fast_pretest2_fail(&s_img[(3 + i) * FC_LD + mis + 3 + lane],
-                                                      &s_img[(3 + i1) * FC_LD + mis + 3 + lane], FC_LD, T1);
-                p0 = !(f & 0x8000u);
-                p1 = !(f & 0x80000000u);
+        const int rho = lane >> 4, L = lane & 15;
+        uint32_t* m32 = reinterpret_cast<uint32_t*>(s_mask);
+        const int cv = dc - 4 * L;
+        const uint32_t colmask = cv >= 4 ? 0xfu : (cv > 0 ? (1u << cv) - 1u : 0u);
+        for (int i0 = 4 * wid; i0 < dr; i0 += 16) {
+            const int i = i0 + rho;
+            const int ic = min(i, dr - 1);   // rows past the last detection row: computed, not stored
+            const uint32_t* rw = s_img32 + (3 + ic) * ldw + L;
+            const uint32_t pv = rw[0], vv = rw[1], nv = rw[2];
+            const uint32_t av = rw[3 * ldw + 1], cvv = rw[-3 * ldw + 1];
+            const uint32_t bv = __builtin_amdgcn_alignbyte(nv, vv, 3), dv = __builtin_amdgcn_alignbyte(vv, pv, 1);
+            uint32_t fl[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t sel = h ? 0x0c030c02u : 0x0c010c00u;
+                const short2v v = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, vv, sel));
+                const short2v a = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, av, sel));
+                const short2v bq = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, bv, sel));
+                const short2v c = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, cvv, sel));
+                const short2v d = __builtin_bit_cast(short2v, __builtin_amdgcn_perm(0u, dv, sel));
+                const short2v vm = v - T1, vp = v + T1;
+                const uint32_t na = pk_bits(vm - a), nb = pk_bits(vm - bq), nc = pk_bits(vm - c), nd = pk_bits(vm - d);
+                const uint32_t ba = pk_bits(a - vp), bb = pk_bits(bq - vp), bc = pk_bits(c - vp), bd = pk_bits(d - vp);
+                fl[h] = ((na & nc) | (nb & nd)) & ((ba & bc) | (bb & bd));
             }
-            const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
-            if (lane == 0) {
-                s_mask[i] = m0;
-                if (i + 4 < dr) s_mask[i + 4] = m1;
-            }
+            const uint32_t nib = (((~fl[0] >> 15) & 1u) | ((~fl[0] >> 30) & 2u) | ((~fl[1] >> 13) & 4u) |
+                                  ((~fl[1] >> 28) & 8u)) & colmask;
+            int x = (int)(nib << (4 * (L & 7)));
+            x |= __builtin_amdgcn_mov_dpp(x, 0xB1, 0xf, 0xf, true);    // quad_perm xor 1
+            x |= __builtin_amdgcn_mov_dpp(x, 0x4E, 0xf, 0xf, true);    // quad_perm xor 2
+            x |= __builtin_amdgcn_mov_dpp(x, 0x141, 0xf, 0xf, true);   // row_half_mirror (8 lanes)
+            if ((L & 7) == 0 && i < dr) m32[2 * i + (L >> 3)] = (uint32_t)x;
         }
     }
     __syncthreads();
@@ -1300,8 +1358,9 @@ int Extractor::setup_geometry(int W, int H) {
     xofsAll_.assign(nlevels_, {});
     xalAll_.assign(nlevels_, {});
     ptiles_.clear();
-    ptile_begin_.assign(nlevels_ + 1, 0);
-    plds_.assign(nlevels_, 0);
+    ptile_begin_.assign(2 * (nlevels_ + 1), 0);   // variant v, level l: ptile_n_ tiles from here
+    ptile_n_.assign(2 * nlevels_, 0);
+    plds_.assign(2 * nlevels_, 0);
     for (int l = 1; l < nlevels_; l++) {
         const int sw = levels_[l - 1].w, sh = levels_[l - 1].h, dw = levels_[l].w, dh = levels_[l].h;
         const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
@@ -1342,8 +1401,9 @@ int Extractor::setup_geometry(int W, int H) {
                 while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - p - 2;
                 return p;
             };
-            ptile_begin_[l] = (int)ptiles_.size();
-            // tile height: PT_H rows unless the source rectangle would exceed the LDS budget
+          for (int v = 0; v < 2; v++) {
+            ptile_begin_[v * (nlevels_ + 1) + l] = (int)ptiles_.size();
+            // tile height: kPyrTileH[v] rows unless the source rectangle would exceed the LDS budget
             // (scale factors well above the reference's 1.2)
             auto make = [&](int py0, int px0, int nrow, PyrTile& t) {
                 int r0 = 1 << 30, r1 = -1, c0 = 1 << 30, c1 = -1;
@@ -1363,7 +1423,7 @@ int Extractor::setup_geometry(int W, int H) {
                 t.nsw = (c1 + kEdge - t.sc0) / 4 + 1;
                 return (size_t)t.nsr * t.nsw * 4 <= (size_t)kPyrLdsMax;
             };
-            int nrow = PT_H;
+            int nrow = kPyrTileH[v];
             for (bool ok = false; !ok;) {
                 ok = true;
                 for (int py0 = 0; py0 < D.ph && ok; py0 += nrow)
@@ -1382,7 +1442,9 @@ int Extractor::setup_geometry(int W, int H) {
                     lds = std::max(lds, (size_t)t.nsr * t.nsw * 4);
                     ptiles_.push_back(t);
                 }
-            plds_[l] = (int)lds;
+            plds_[v * nlevels_ + l] = (int)lds;
+            ptile_n_[v * nlevels_ + l] = (int)ptiles_.size() - ptile_begin_[v * (nlevels_ + 1) + l];
+          }
         }
         yrAll[l] = yr;
         xofsAll_[l] = xofs;
@@ -1392,7 +1454,6 @@ int Extractor::setup_geometry(int W, int H) {
         tab_off_[l][2] = push(yr.data(), yr.size() * 4);
         tab_off_[l][3] = push(yb.data(), yb.size() * 2);
     }
-    ptile_begin_[nlevels_] = (int)ptiles_.size();
     if (plan_chain(yrAll)) return -1;
     // (re)allocate device buffers for maxB_
     auto F = [](void*& p) { if (p) (void)hipFree(p); p = nullptr; };
@@ -1523,12 +1584,14 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
             const LevelHost& L = levels_[l];
             const LevelHost& P = levels_[l - 1];
             const uint8_t* T = (const uint8_t*)d_tabs_;
-            const int nt = ptile_begin_[l + 1] - ptile_begin_[l];
-            hipLaunchKernelGGL(k_pyr_resize, dim3(grid8(nt), B), dim3(256), plds_[l], s, (uint8_t*)d_pyr_, img_bytes_,
+            const int v = B >= 8 ? 1 : 0, pb = v * (nlevels_ + 1) + l;
+            const int nt = ptile_n_[v * nlevels_ + l];
+            auto kern = v ? k_pyr_resize<kPyrTileH[1]> : k_pyr_resize<kPyrTileH[0]>;
+            hipLaunchKernelGGL(kern, dim3(grid8(nt), B), dim3(256), plds_[v * nlevels_ + l], s, (uint8_t*)d_pyr_, img_bytes_,
                                P.off, P.pitch, L.off, L.pitch, L.ph, L.w, L.h,
                                (const int*)(T + tab_off_[l][0]), (const short2*)(T + tab_off_[l][1]),
                                (const int2*)(T + tab_off_[l][2]), (const short2*)(T + tab_off_[l][3]),
-                               (const PyrTile*)d_ptiles_ + ptile_begin_[l], nt);
+                               (const PyrTile*)d_ptiles_ + ptile_begin_[pb], nt);
         }
         if (lend < nlevels_) {
             const uint8_t* T = (const uint8_t*)d_chain_;
@@ -1541,6 +1604,15 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     }
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipEventRecord(ev_[1], s));
+    // ORBGPU_BLUR_EARLY=1: the blur right after the pyramid on the extractor's own stream (A/B
+    // of the pipelined bench: which tracking kernels the FAST grid then overlaps)
+    static const bool blurEarly = [] {
+        const char* e = getenv("ORBGPU_BLUR_EARLY");
+        return e && e[0] == '1';
+    }();
+    if (blurEarly && !evBlur_)
+        hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
+                           (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_, (int)tiles_.size());
     if (evBlur_) {
         ORB_HIP_CHECK(hipStreamWaitEvent(side_, ev_[1], 0));
         hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, side_, (const uint8_t*)d_pyr_,
@@ -1577,7 +1649,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     //    was launched after the pyramid
     if (evBlur_)
         ORB_HIP_CHECK(hipStreamWaitEvent(s, evBlur_, 0));
-    else
+    else if (!blurEarly)
         hipLaunchKernelGGL(k_blur7, dim3(grid8((int)tiles_.size()), B), dim3(256), 0, s, (const uint8_t*)d_pyr_,
                            (uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const BlurTile*)d_tiles_, (int)tiles_.size());
     ORB_HIP_CHECK(hipEventRecord(ev_[2], s));

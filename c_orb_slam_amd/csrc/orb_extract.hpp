@@ -47,7 +47,7 @@ struct BlurTile {
 
 // One destination tile of k_pyr_resize: padded-destination origin and the source
 // rectangle it reads (interior rows [sr0, sr0+nsr), padded dword columns [sc0, sc0+4*nsw)).
-constexpr int PT_W = 256, PT_H = 16, kPyrLdsMax = 48 * 1024;
+constexpr int PT_W = 256, kPyrLdsMax = 48 * 1024;
 struct PyrTile {
     int py0, px0, nrow, sr0, nsr, sc0, nsw, pad;
 };
@@ -122,7 +122,7 @@ private:
     std::vector<int> level_cell_begin_;
     std::vector<BlurTile> tiles_;
     std::vector<PyrTile> ptiles_;
-    std::vector<int> ptile_begin_, plds_;
+    std::vector<int> ptile_begin_, ptile_n_, plds_;   // per tile-height variant and level
     // the chained pyramid (plan_chain): strips per image, dynamic LDS, device tables
     // [ChainLevel x (nlevels-1) | int4 strip ranges x K x (nlevels-1) | u16 padded rows]
     int plan_chain(const std::vector<std::vector<int>>& yr);

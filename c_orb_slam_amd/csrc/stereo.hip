@@ -26,7 +26,9 @@ namespace orbgpu {
 
 // vRowIndices (Frame.cc:476-493) as a CSR per pair: right keypoint iR is listed on every row
 // yi in [floor(y - r), ceil(y + r)], r = 2 * mvScaleFactors[octave].  The order inside a row
-// does not matter: the match kernel takes the minimum of (dist, iR).
+// does not matter: the match kernel takes the minimum of (dist, iR).  An entry carries what the
+// scan filters on (uR, octave) beside iR, so the match kernel reads a row's entries as one
+// contiguous run instead of gathering every candidate's 28-byte keypoint.
 __global__ void __launch_bounds__(1024) k_stereo_rows(const StereoDev* __restrict__ probs, StereoParams P) {
     ORBGPU_LATENCY_WAVE();
     const StereoDev& S = probs[blockIdx.x];
@@ -77,7 +79,8 @@ __global__ void __launch_bounds__(1024) k_stereo_rows(const StereoDev* __restric
         const orb_kp_dev kp = S.kR[iR];
         const float r = 2.0f * P.scale[kp.octave];
         const int maxr = min((int)ceilf(kp.y + r), rows - 1), minr = max((int)floorf(kp.y - r), 0);
-        for (int y = minr; y <= maxr; y++) S.rowIdx[atomicAdd(&s_cnt[y], 1)] = iR;
+        const int2 ent = make_int2(__float_as_int(kp.x), iR | (kp.octave << 24));
+        for (int y = minr; y <= maxr; y++) S.rowIdx[atomicAdd(&s_cnt[y], 1)] = ent;
     }
 }
 
@@ -127,10 +130,10 @@ __global__ void __launch_bounds__(256) k_stereo_match(const StereoDev* __restric
         int scored = 0;
         const int c1 = S.rowStart[row + 1];
         for (int c = S.rowStart[row] + sub; c < c1; c += 16) {
-            const int iR = S.rowIdx[c];
-            const orb_kp_dev kpR = S.kR[iR];
-            if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
-            const float uR = kpR.x;
+            const int2 ent = S.rowIdx[c];
+            const int iR = ent.y & 0xffffff, octR = ent.y >> 24;
+            if (octR < levelL - 1 || octR > levelL + 1) continue;
+            const float uR = __int_as_float(ent.x);
             if (!(uR >= minU && uR <= maxU)) continue;
             const uint32_t* dr = (const uint32_t*)(S.dR + 32 * (size_t)iR);
             int dist = 0;

@@ -39,7 +39,7 @@ struct StereoDev {
     int* sad;               // scratch (NL): best SAD or -1
     int* kept;              // out: stereo matches after the median filter
     int* rowStart;          // scratch (rows0 + 1): vRowIndices as CSR (Frame.cc:476-493)
-    int* rowIdx;            // scratch (NR * band rows)
+    int2* rowIdx;           // scratch (NR * band rows): (uR bits, iR | octave << 24) per entry
 };
 
 class Matcher;

@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""One config-5 sharded global BA run for tools/gba_rank_model.py: R in-process ranks with the
+separator-tree partition, a warm-up call then one measured call (each call on fresh rank
+threads); prints the exchange volume per trial and the LM trial count of the measured call.
+usage: gba_rank_run.py <R> [nkf:laps]"""
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+from ba_cases import global_ba_problem  # noqa: E402
+
+
+def main():
+    from c_orb_slam_amd.optimizer import partition_points_nd, run_sharded_local
+    R = int(sys.argv[1])
+    spec = sys.argv[2] if len(sys.argv) > 2 else "2000:4"
+    nkf, _, lp = spec.partition(":")
+    pr = global_ba_problem(0, n_kf=int(nkf), pts_per_kf=150, laps=int(lp or 0))
+    part = "nd" if R > 1 else "block"
+    run_sharded_local(pr, R, "global", 10, False, partition=part)   # warm-up
+    s, per = run_sharded_local(pr, R, "global", 10, False, partition=part, trace=True)
+    used, tiles, rows, pattern = per[0]["sharding"]
+    _, kfo = partition_points_nd(pr, R, with_kf_owner=True)
+    poses = int((kfo >= -1).sum())
+    xd = (tiles * 4096 + rows + 6 * poses) if used else (pattern * 4096 + 6 * poses)
+    print(f"R {R} iterations {s['iterations'][0]} trials {len(s['trial_chi2'])} exchange_doubles_per_trial {xd} "
+          f"sharded_factorisation {used} separator_tiles {tiles} pattern_tiles {pattern}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
