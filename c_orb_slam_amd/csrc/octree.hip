@@ -25,7 +25,7 @@
 namespace orbgpu {
 
 constexpr int OCT_TMAX = 1024;   // largest workgroup instance (k_octree<256|512|1024>)
-constexpr int kOctCellsMax = 2048;   // FAST cells of one level (a job's compaction)
+constexpr int kOctCellsMax = kOctKMax / 2;   // FAST cells of one level (a job's compaction; in S.tmp)
 
 struct OctShared {
     int16_t x0[2 * kOctNMax], y0[2 * kOctNMax], x1[2 * kOctNMax], y1[2 * kOctNMax];
@@ -36,8 +36,8 @@ struct OctShared {
     uint16_t er[kOctNMax], eidx[kOctNMax];
     uint16_t vs[kOctNMax], vs2[kOctNMax];
     uint32_t sk[kOctNMax];         // phase-2 sort keys (size << 16 | creation order)
-    int cdelta[kOctCellsMax];      // compaction: slot index - list index of every cell's first candidate
-    uint16_t knode[kOctKMax], arena[kOctKMax], tmp[kOctKMax];
+    uint16_t knode[kOctKMax], arena[kOctKMax];
+    alignas(16) uint16_t tmp[kOctKMax];   // also the compaction's int cell deltas
     int wsum[OCT_TMAX / 64];
     int head, size, nfree, m, newm, seqctr, flag;
 };
@@ -132,6 +132,22 @@ __global__ void __launch_bounds__(T) k_octree(OctInput in, int nlevels, const Oc
                                                  uint16_t* __restrict__ gscratch, size_t gstride, int* __restrict__ err) {
     __shared__ OctShared S;
     ORBGPU_PROF_START;
+#ifdef ORBGPU_PROF
+    // every job's duration (instrumented builds): slot 10 = max (cycles << 4 | level), slot 11 =
+    // the sum, slot 12 = the job count, written on every return path by the destructor
+    struct JobTimer {
+        unsigned long long t0;
+        int lvl;
+        __device__ ~JobTimer() {
+            if (threadIdx.x == 0) {
+                const unsigned long long c = clock64() - t0;
+                atomicMax(&g_orbgpu_prof[10], (c << 4) | (unsigned long long)lvl);
+                atomicAdd(&g_orbgpu_prof[11], c);
+                atomicAdd(&g_orbgpu_prof[12], 1ull);
+            }
+        }
+    } jt{(unsigned long long)clock64(), (int)blockIdx.x / ((int)gridDim.x / nlevels)};
+#endif
     // level-major dispatch order: the long jobs (level 0: the most candidates and features) of
     // every image start first and the short ones fill in behind them
     const int B = (int)gridDim.x / nlevels;
@@ -151,11 +167,13 @@ __global__ void __launch_bounds__(T) k_octree(OctInput in, int nlevels, const Oc
         }
         return;
     }
+    // the cell deltas live in S.tmp (free until phase 1; kOctCellsMax ints)
+    int* cdelta = reinterpret_cast<int*>(S.tmp);
     const int n = oct_scan_val<T>(
         nc, [&](int i) { return cnt[i]; },
         [&](int i, int o) {
             S.ia[i] = o;
-            S.cdelta[i] = in.cell_slot[cb + i] - in.cell_slot[cb] - o;
+            cdelta[i] = in.cell_slot[cb + i] - in.cell_slot[cb] - o;
         },
         S.wsum);
     const size_t base = (size_t)b * in.slots_per_image + (size_t)in.cell_slot[cb];
@@ -182,7 +200,7 @@ __global__ void __launch_bounds__(T) k_octree(OctInput in, int nlevels, const Oc
                         if (S.ia[mid] <= k) lo = mid;
                         else hi = mid - 1;
                     }
-                    v[u] = sl[k + S.cdelta[lo]];
+                    v[u] = sl[k + cdelta[lo]];
                 }
             }
 #pragma unroll
@@ -599,8 +617,8 @@ int octree_launch(const OctInput& in, int B, int nlevels, const OctLevelDev* lv,
                   hipStream_t s) {
     static const int nt = [] {
         const char* e = getenv("ORBGPU_OCT_T");
-        const int v = e ? atoi(e) : 256;
-        return v == 512 || v == 1024 ? v : 256;
+        const int v = e ? atoi(e) : 512;   // 512: 0.139 -> 0.137 ms (128 images), 0.101 -> 0.093 (2)
+        return v == 256 || v == 1024 ? v : 512;
     }();
     if (nt == 1024)
         hipLaunchKernelGGL(k_octree<1024>, dim3(B * nlevels), dim3(1024), 0, s, in, nlevels, lv, jobsel, jobcnt,

@@ -210,9 +210,11 @@ __global__ void __launch_bounds__(256) k_pyr_chain(uint8_t* __restrict__ pyr, si
             const int r = t / wpr, q = t - r * wpr;
             d[t] = S32[(size_t)r * spw + q];
         }
-        // row taps of every chained level's compute rows: (y0 | y1 << 16, beta pair)
+        // row taps of every chained level's compute rows: (y0 | y1 << 16, beta pair), and the
+        // padded rows every level writes out
         int2* rt = reinterpret_cast<int2*>(sb + sr.z);
-        int slot = 0;
+        uint16_t* rl = reinterpret_cast<uint16_t*>(sb + sr.w);
+        int slot = 0, rslot = 0;
         for (int i = 0; i < nl; i++) {
             const int4 st = strips[k * (nl + 1) + i];
             const int2* yr = reinterpret_cast<const int2*>(tabs + lv[i].yr);
@@ -221,13 +223,16 @@ __global__ void __launch_bounds__(256) k_pyr_chain(uint8_t* __restrict__ pyr, si
                 const int2 yy = yr[st.x + t];
                 rt[slot + t] = make_int2(yy.x | (yy.y << 16), yb[st.x + t]);
             }
+            for (int t = tid; t < st.w; t += 256) rl[rslot + t] = rows[st.z + t];
             slot += st.y - st.x;
+            rslot += st.w;
         }
     }
     __syncthreads();
     const uint8_t* prev = sb + src_lds + 3;   // interior column 0 of the staged source
     int prev_lo = sr.x, prev_rp = src_rp, prev_n = sr.y - sr.x;
     const int2* rt = reinterpret_cast<const int2*>(sb + sr.z);
+    const uint16_t* rl = reinterpret_cast<const uint16_t*>(sb + sr.w);
     for (int i = 0; i < nl; i++) {
         const ChainLevel L = lv[i];
         const int4 st = strips[k * (nl + 1) + i];   // compute rows [x, y), padded-row list [z, z + w)
@@ -246,7 +251,8 @@ __global__ void __launch_bounds__(256) k_pyr_chain(uint8_t* __restrict__ pyr, si
                 al[j] = xal[dx];
                 s1[j] = sx[j] + (al[j].y != 0);
             }
-            for (int r = ph; r < nrows; r += nph) {
+            // one output dword (4 columns) of row r
+            auto row_out = [&](int r) {
                 const int2 e = rt[r];
                 const int y0 = e.x & 0xffff, y1 = e.x >> 16;
                 const short2 be = __builtin_bit_cast(short2, e.y);
@@ -264,7 +270,14 @@ __global__ void __launch_bounds__(256) k_pyr_chain(uint8_t* __restrict__ pyr, si
                         v |= (uint32_t)(uint8_t)o << (8 * j);
                     }
                 }
-                *reinterpret_cast<uint32_t*>(cur + r * L.rp + 4 * g) = v;
+                return v;
+            };
+            // two rows per step: their LDS reads are independent and in flight together
+            for (int r = ph; r < nrows; r += 2 * nph) {
+                const int r2 = r + nph < nrows ? r + nph : r;
+                const uint32_t va = row_out(r), vb = row_out(r2);
+                *reinterpret_cast<uint32_t*>(cur + r * L.rp + 4 * g) = va;
+                *reinterpret_cast<uint32_t*>(cur + r2 * L.rp + 4 * g) = vb;
             }
         }
         rt += nrows;
@@ -273,7 +286,7 @@ __global__ void __launch_bounds__(256) k_pyr_chain(uint8_t* __restrict__ pyr, si
         const int nch = L.pitch >> 4;
         for (int t = tid; t < st.w * nch; t += 256) {
             const int ri = t / nch, ch = t - ri * nch;
-            const int py = rows[st.z + ri];
+            const int py = rl[ri];
             const int y = refl101(py - kEdge, L.h);
             const uint8_t* row = cur + min(max(y - st.x, 0), nrows - 1) * L.rp;
             const int x0 = ch * 16 - kEdge;   // = 1 (mod 4)
@@ -293,6 +306,7 @@ __global__ void __launch_bounds__(256) k_pyr_chain(uint8_t* __restrict__ pyr, si
             }
             *reinterpret_cast<uint4*>(base + L.off + (size_t)py * L.pitch + 16 * ch) = o;
         }
+        rl += st.w;
         prev = cur;
         prev_lo = st.x;
         prev_rp = L.rp;
@@ -754,14 +768,16 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
 constexpr int kBriefR = 18, kBriefRows = 2 * kBriefR + 1, kBriefLd = 40;   // patch rows, LDS row bytes
 __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                      size_t img_bytes, size_t blur_bytes, const int2* __restrict__ sel, int selcap,
-                                                     const int* __restrict__ nout, const LevelDev* __restrict__ lv,
+                                                     const int* __restrict__ nout, const LevelArgs lva,
                                                      orb_kp_dev* __restrict__ kps, uint8_t* __restrict__ desc,
                                                      int cap_per_image, int gx, int B) {
     __shared__ uint32_t s_patch[4][kBriefRows * kBriefLd / 4];
     // batches of >= 8 images: workgroup g runs on XCD g % 8, and image b's keypoint groups all
     // go to XCD b % 8 (images in turn), so the level and blurred-level lines their patches
     // share stay in that XCD's L2; smaller batches spread every image over all XCDs
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // the wave's keypoint, its record and its level are wave-uniform: scalar loads (the level
+    // table is a kernel argument), so one dependent memory round trip precedes the pixel loads
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int img, grp;
     if (B >= 8) {
         const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -775,12 +791,12 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     const int k = grp * 4 + wv;
     if (k >= nout[img] || k >= cap_per_image) return;   // wave-uniform: no barrier below
     const int2 s = sel[(size_t)img * selcap + k];
-    const uint32_t pk = (uint32_t)s.x;
-    const int meta = s.y;
+    const uint32_t pk = (uint32_t)__builtin_amdgcn_readfirstlane(s.x);
+    const int meta = __builtin_amdgcn_readfirstlane(s.y);
     const int b = meta >> 20, l = (meta >> 16) & 15, idx = meta & 0xffff;
     const int x = (int)(pk & 0xfff) + (kEdge - 3), y = (int)((pk >> 12) & 0xfff) + (kEdge - 3);
     const int score = (int)(pk >> 24);
-    const LevelDev L = lv[l];
+    const LevelDev L = lva.lv[l];
     // stage the blurred patch (rows y-18 .. y+18, dword columns from (x-18) & ~3) first: its
     // loads are in flight during the moments
     const int c0 = (x - kBriefR) & ~3, mis = (x - kBriefR) - c0;
@@ -1150,7 +1166,22 @@ int Extractor::plan_chain(const std::vector<std::vector<int>>& yr) {
         }
         const size_t o1 = (srcBytes + 15) & ~(size_t)15, o2 = o1 + ((buf[0] + 15) & ~(size_t)15),
                      o3 = o2 + ((buf[1] + 15) & ~(size_t)15);
-        const size_t lds = o3 + rtRows * 8;
+        // padded rows written per strip (own rows + the border rows reflecting to them)
+        size_t rlRows = 0;
+        for (int k = 0; k < K; k++) {
+            size_t n = 0;
+            for (int l = la; l <= lb; l++) {
+                for (int py = 0; py < levels_[l].ph; py++) {
+                    int y = py - kEdge;
+                    if (levels_[l].h == 1) y = 0;
+                    while (y < 0 || y >= levels_[l].h) y = y < 0 ? -y : 2 * levels_[l].h - y - 2;
+                    if (y >= A[l][k] && y < A[l][k + 1]) n++;
+                }
+            }
+            rlRows = std::max(rlRows, n);
+        }
+        const size_t o4 = o3 + ((rtRows * 8 + 15) & ~(size_t)15);
+        const size_t lds = o4 + rlRows * 2;
         if (lds > (size_t)kChainLdsMax) continue;
         // tables: levels | strips (nl + 1 entries per strip) | padded-row lists
         std::vector<ChainLevel> cl(nl);
@@ -1188,7 +1219,7 @@ int Extractor::plan_chain(const std::vector<std::vector<int>>& yr) {
             e[0] = Src[k].first;
             e[1] = Src[k].second;
             e[2] = (int32_t)o3;
-            e[3] = 0;
+            e[3] = (int32_t)o4;
             if (Src[k].first < 0 || Src[k].second > levels_[la - 1].h) return -1;
         }
         chainK_ = K;
@@ -1507,6 +1538,8 @@ int Extractor::setup_geometry(int W, int H) {
         ld[l].bpitch = levels_[l].bpitch;
         ld[l].kp_size = (float)(int)(kPatch * scale_[l]);
     }
+    if (nlevels_ > kMaxLevels) return -1;
+    for (int l = 0; l < nlevels_; l++) levelArgs_.lv[l] = ld[l];
     ORB_HIP_CHECK(hipMalloc(&d_levels_, ld.size() * sizeof(LevelDev)));
     ORB_HIP_CHECK(hipMemcpy(d_levels_, ld.data(), ld.size() * sizeof(LevelDev), hipMemcpyHostToDevice));
     ORB_HIP_CHECK(hipMalloc(&d_tabs_, std::max<size_t>(tabs.size(), 16)));
@@ -1673,7 +1706,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
         const int nwg = B >= 8 ? gx * 8 * ((B + 7) / 8) : gx * B;
         hipLaunchKernelGGL(k_orient_desc, dim3(nwg), dim3(256), 0, s, (const uint8_t*)d_pyr_,
                            (const uint8_t*)d_blur_, img_bytes_, blur_bytes_, (const int2*)d_sel_, selcap_,
-                           (const int*)d_nout_, (const LevelDev*)d_levels_, okps, odesc, cap, gx, B);
+                           (const int*)d_nout_, levelArgs_, okps, odesc, cap, gx, B);
     }
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipMemcpyAsync(h_nout_, d_nout_, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, s));

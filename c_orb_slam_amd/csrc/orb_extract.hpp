@@ -66,6 +66,11 @@ struct LevelDev {
     int pitch, bpitch;
     float scale, kp_size;
 };
+// every level's LevelDev by value, as a kernel argument (read with scalar loads)
+constexpr int kMaxLevels = 16;
+struct LevelArgs {
+    LevelDev lv[kMaxLevels];
+};
 
 struct LevelHost {
     int w, h, pw, ph, pitch, bpitch;
@@ -117,6 +122,7 @@ private:
     int maxW_ = 0, maxH_ = 0, maxB_ = 0;
     int geomW_ = -1, geomH_ = -1;
     std::vector<LevelHost> levels_;
+    LevelArgs levelArgs_{};
     std::vector<CellDesc> cells_;
     std::vector<CellGroup> groups_;
     std::vector<int> level_cell_begin_;

@@ -39,3 +39,5 @@ if __import__("os").environ.get("ORBGPU_PROF_DUMP"):
     print("k_octree sections (cycles per call, job 0 = image 0 level 0):",
           {n: round(buf[16 + i] / 13) for i, n in enumerate(names)},
           "phase-2 rounds", round(buf[24] / 13, 1), "phase-1 rounds", round(buf[25] / 13, 1), flush=True)
+    print("k_octree jobs: slowest", buf[26] >> 4, "cycles (level", buf[26] & 15, "), mean",
+          round(buf[27] / max(buf[28], 1)), "cycles over", buf[28], "jobs", flush=True)
