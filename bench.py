@@ -34,9 +34,9 @@ sys.path.insert(0, str(ROOT))
 METRIC = "tracking FPS + ORB matches/sec, KITTI-00 stereo; local-BA iter/sec"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md (spec)
 ROOFLINE_REPS = 5
-TRAFFIC_FILE = "traffic_r04.json"   # PMC FETCH_SIZE/WRITE_SIZE per launch (tools/pmc_traffic.py)
-VALU_FILE = "valu_r04.json"   # PMC SQ_INSTS_VALU per launch (tools/pmc_valu.py)
-MATCH_PMC_FILE = "match_pmc_r04.json"   # matcher kernels: HBM bytes and VALU instructions per launch (tools/pmc_match.py)
+TRAFFIC_FILE = "traffic_r05.json"   # PMC FETCH_SIZE/WRITE_SIZE per launch (tools/pmc_traffic.py)
+VALU_FILE = "valu_r05.json"   # PMC SQ_INSTS_VALU per launch (tools/pmc_valu.py)
+MATCH_PMC_FILE = "match_pmc_r05.json"   # matcher kernels: HBM bytes and VALU instructions per launch (tools/pmc_match.py)
 STEREO_WINDOW_BYTES = 11 * 11 + 11 * 21   # per SAD-evaluated keypoint: left window + right search band
 VALU_PEAK_GINST = 1228.8   # 256 CUs x 2 wave64 VALU issues per cycle x 2.4 GHz (MI355X_MICROARCH.md)
 W, H, NFEAT = 1241, 376, 1200
