@@ -358,6 +358,7 @@ __device__ __forceinline__ double wave_lds_csum(double* arr, int m) {
 
 
 constexpr int kChunks = 128;  // per-list LDS chunk sums: lists up to 8192 terms
+constexpr int kSysThreads = 512;   // 256 VGPRs per lane: the 27 packed chunk trees stay unspilled
 
 // per free pose: Hpp (upper 21) and b_p as canonical sums over its active edges (edge order).
 // Each lane loads the 27 terms of one edge; the 27 chunk trees run packed; chunk sums
@@ -398,7 +399,7 @@ __device__ __forceinline__ void pose_reduce_block(const BaStructDev& s, const do
     }
 }
 
-__global__ void __launch_bounds__(1024) k_pose_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
+__global__ void __launch_bounds__(kSysThreads) k_pose_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
                                                       double* bp, const int* run) {
     BA_GATE(run);
     pose_reduce_block(s, terms, Hpp, bp, blockIdx.x);
@@ -421,10 +422,25 @@ __device__ __forceinline__ void land_reduce_thread(const BaStructDev& s, const d
     } else if (n <= 64) {
         v = tree64_local([&](int k) { return cp[li[k]]; }, n);
     } else {  // long tracks (<= 4096 edges, validated): chunk trees, then one more level
+        // tree64_local over the m chunk trees without an array (scratch): its pairing tree is walked
+        // depth-first, leaf t = chunk bitrev6(t), with a binary-counter stack of partial sums
         const int m = (n + 63) >> 6;
-        double c[64];
-        for (int t = 0; t < m; t++) c[t] = tree64_local([&](int k) { return cp[li[t * 64 + k]]; }, min(64, n - t * 64));
-        v = tree64_local([&](int k) { return c[k]; }, m);
+        double st[6];
+        v = 0.0;
+        for (int t = 0; t < 64; t++) {
+            const int c = bitrev6(t);
+            double u = c < m ? tree64_local([&](int k) { return cp[li[c * 64 + k]]; }, min(64, n - c * 64)) : 0.0;
+#pragma unroll
+            for (int lvl = 0; lvl < 6; lvl++) {
+                if ((t >> lvl) & 1) {
+                    u = st[lvl] + u;
+                } else {
+                    st[lvl] = u;
+                    break;
+                }
+            }
+            v = u;
+        }
     }
     if (q < 9) Hll[9 * l + q] = v;
     else bl[3 * l + (q - 9)] = v;
@@ -438,7 +454,7 @@ __global__ void __launch_bounds__(256) k_land_reduce(BaStructDev s, const double
 
 // both reductions of buildSystem in one launch: blocks [0, nP) reduce a pose each, the rest
 // a (landmark, entry) per thread
-__global__ void __launch_bounds__(1024) k_sys_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
+__global__ void __launch_bounds__(kSysThreads) k_sys_reduce(BaStructDev s, const double* __restrict__ terms, double* Hpp,
                                                      double* bp, double* Hll, double* bl, const int* run) {
     BA_GATE(run);
     if ((int)blockIdx.x < s.nP) pose_reduce_block(s, terms, Hpp, bp, blockIdx.x);
@@ -1132,12 +1148,13 @@ __global__ void __launch_bounds__(256) k_ldlt_2d(int n, const double* __restrict
     ldlt_backward_wave(n, Lall, dvec, y, x, scal);
 }
 
-// Register-resident LDL^T + solve for n < 128 (<= 21 free keyframes), 1024 threads.
-// Thread (wave w < 16, lane) owns rows i = 16 r + w (r < 8) of columns j = lane, lane + 64.
-// Per 6-column panel: owners publish the panel rows to LDS (U), wave 0 factorises them
-// in registers and writes L (Lall[k][i] = L[i][k], Lpan[i][k - p0]) and d_k, then every
-// thread applies the panel's updates to its rows in k order.  Per-element operation
-// sequence identical to oracle ora_ldlt_solve.
+// Register-resident LDL^T + solve for n < 128 (<= 21 free keyframes), 512 threads.
+// Thread (wave w < 8, lane) owns rows i = 8 r + w (r < 16) of columns j = lane, lane + 64.
+// Per 6-column panel: waves 0-1 factorise the panel (one thread per column j: the panel's 6x6
+// diagonal block, then column j) from its rows in LDS and write L (Lall[k][i] = L[i][k],
+// Lpan[i][k - p0]) and d_k; then every thread applies the panel's updates to its rows in k order
+// and the owners of the next panel's rows publish them to the other panel buffer.  Two barriers
+// per panel.  Per-element operation sequence identical to oracle ora_ldlt_solve.
 #ifdef ORB_LDLT_PROBE
 __device__ long long g_ldlt_probe[256];
 #define LDLT_PROBE(slot) \
@@ -1152,19 +1169,204 @@ __device__ long long g_ldlt_probe[256];
 constexpr int kLdltMax = 128;
 constexpr int kTiledMinPoses = kBaTiledMinPoses;   // 6 x 24 = 144 rows: the first n the LDS-resident dense solver cannot hold
 constexpr int kDenseMaxN = 144;   // >= every n the dense single-workgroup solvers take (n^2 doubles in LDS)
-constexpr int kLdltWaves = 16;
+constexpr int kLdltWaves = 8;     // 512 threads: 256 VGPRs per lane, the panel registers stay unspilled
+constexpr int kLdltThreads = 64 * kLdltWaves;
 constexpr int kLdltRows = kLdltMax / kLdltWaves;
-__global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restrict__ Sg, const double* bs, double* x,
-                                                   double* scal, const int* run) {
+// LDS of k_ldlt_reg: Lall (n x n), two 6 x kLdltMax panel buffers, Lpan (kLdltMax x 6), d, y
+static inline size_t ldlt_reg_shm(int n) { return sizeof(double) * ((size_t)n * n + 20 * kLdltMax); }
+
+// SharedDiv::div without its branch: the quotient of an in-range numerator, or a * r for a zero
+// one (a / b = a signed zero); any other numerator (or an out-of-range divisor) sets `bad` and the
+// caller redoes the work with SharedDiv::div.
+__device__ __forceinline__ double div_fast(const SharedDiv& d, double a, bool& bad) {
+    const double q = a * d.r;
+    const double rem = fma(-d.b, q, a);
+    const double res = __builtin_amdgcn_div_fixup(fma(rem, d.r, q), d.b, a);
+    const double aa = fabs(a);
+    const bool inr = aa > 0x1p-300 && aa < 0x1p300;
+    bad = bad || !(inr || aa == 0.0);
+    return inr ? res : q;
+}
+
+// the panel factorisation of k_ldlt_reg for one column thread j, any panel width pw <= 6, with
+// SharedDiv::div (the fallback of ldlt_panel6)
+__device__ __forceinline__ void ldlt_panel_generic(int n, int p0, int pw, int j, double* U, double* Lall,
+                                                   double* Lpan, double* dvec, double* y, int* ok) {
+    double Bk[6][6], Lb[6][6], dd[6];
+#pragma unroll
+    for (int t = 0; t < 6; t++)
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+            Bk[t][c] = (t < pw && c < pw && c >= t) ? U[t * kLdltMax + p0 + c] : 0.0;
+            Lb[t][c] = 0.0;
+        }
+    bool bad = false;
+    SharedDiv sd[6] = {SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0),
+                       SharedDiv(1.0)};
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        dd[t] = Bk[t][t];
+        if (t < pw) {
+            bad |= dd[t] == 0.0;
+            sd[t] = SharedDiv(dd[t]);
+#pragma unroll
+            for (int t2 = t + 1; t2 < 6; t2++)
+                if (t2 < pw) Lb[t2][t] = sd[t].div(Bk[t][t2]);
+#pragma unroll
+            for (int t2 = t + 1; t2 < 6; t2++)
+#pragma unroll
+                for (int c = t2; c < 6; c++)
+                    if (c < pw) Bk[t2][c] -= Lb[t2][t] * Bk[t][c];
+        }
+    }
+    double u[6];
+#pragma unroll
+    for (int t = 0; t < 6; t++) u[t] = t < pw ? U[t * kLdltMax + j] : 0.0;
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        if (t < pw) {
+            const int k = p0 + t;
+            const bool act = j > k && j < n;
+            const double l = act ? sd[t].div(u[t]) : 0.0;
+#pragma unroll
+            for (int t2 = t + 1; t2 < 6; t2++)
+                if (t2 < pw && j >= p0 + t2) u[t2] -= Lb[t2][t] * u[t];
+            if (act) {
+                Lall[(size_t)k * n + j] = l;
+                Lpan[j * 6 + t] = l;
+            }
+            if (j == n) y[k] = u[t];   // row k's right-hand side is final: forward-substituted y_k
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 6; t++)
+        if (t < pw) U[t * kLdltMax + j] = u[t];
+    if (j == 0) {
+#pragma unroll
+        for (int t = 0; t < 6; t++)
+            if (t < pw) dvec[p0 + t] = dd[t];
+        if (bad) *ok = 0;
+    }
+}
+
+// A full panel (pw = 6) in one basic block: every thread first factorises the 6x6 diagonal block
+// from LDS itself (the same operations as the block's own columns perform, so d and the block's L
+// agree bit for bit), then its own column: l_jk = u_kj / d_k and u_tj -= L[t][k] u_kj, k
+// ascending.  Results stay in registers until the wave knows that every division was a fast one;
+// a wave with a zero pivot or an out-of-range operand redoes the panel with ldlt_panel_generic.
+__device__ __forceinline__ void ldlt_panel6(int n, int p0, int j, double* U, double* Lall, double* Lpan,
+                                            double* dvec, double* y, int* ok) {
+    double B[6][6], Lb[6][6], dd[6];
+#pragma unroll
+    for (int t = 0; t < 6; t++)
+#pragma unroll
+        for (int c = t; c < 6; c++) B[t][c] = U[t * kLdltMax + p0 + c];
+    double u[6];
+#pragma unroll
+    for (int t = 0; t < 6; t++) u[t] = U[t * kLdltMax + j];
+    bool bad = false;
+    SharedDiv sd[6] = {SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0),
+                       SharedDiv(1.0)};
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        dd[t] = B[t][t];
+        sd[t] = SharedDiv(dd[t]);
+        bad = bad || !sd[t].ok;
+#pragma unroll
+        for (int t2 = t + 1; t2 < 6; t2++) Lb[t2][t] = div_fast(sd[t], B[t][t2], bad);
+#pragma unroll
+        for (int t2 = t + 1; t2 < 6; t2++)
+#pragma unroll
+            for (int c = t2; c < 6; c++) B[t2][c] -= Lb[t2][t] * B[t][c];
+    }
+    double l[6];
+    bool badc = false;
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        const bool act = j > p0 + t && j < n;
+        bool bt = false;
+        const double q = div_fast(sd[t], u[t], bt);
+        badc = badc || (act && bt);
+        l[t] = act ? q : 0.0;
+#pragma unroll
+        for (int t2 = t + 1; t2 < 6; t2++) {
+            const double v = u[t2] - Lb[t2][t] * u[t];
+            u[t2] = j >= p0 + t2 ? v : u[t2];
+        }
+    }
+    if (__ballot(bad || badc)) {
+        ldlt_panel_generic(n, p0, 6, j, U, Lall, Lpan, dvec, y, ok);
+        return;
+    }
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        const int k = p0 + t;
+        if (j > k && j < n) {
+            Lall[(size_t)k * n + j] = l[t];
+            Lpan[j * 6 + t] = l[t];
+        }
+        U[t * kLdltMax + j] = u[t];
+    }
+    if (j == n)
+#pragma unroll
+        for (int t = 0; t < 6; t++) y[p0 + t] = u[t];   // forward-substituted y_k
+    if (j == 0)
+#pragma unroll
+        for (int t = 0; t < 6; t++) dvec[p0 + t] = dd[t];
+}
+
+// k_ldlt_reg's trailing update by one thread: its rows i = 8 r + w >= p1 (w wave-uniform, so the
+// row tests are scalar branches) subtract the panel's six rank-one updates in k order.  Rows
+// [p1, q1) -- the next panel's, final now -- go to Un.  Rows i >= 64 own no column below 64 on or
+// right of the diagonal; column registers 64.. matter only for n >= 64 (the right-hand side sits
+// at column n).
+__device__ __forceinline__ void ldlt_trail(double (&R)[2][kLdltRows], const double* U, double* Un, const double* Lpan,
+                                           int n, int p1, int q1, int w, int lane) {
+    double u0[6], u1[6];
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        u0[t] = U[t * kLdltMax + lane];
+        u1[t] = U[t * kLdltMax + lane + 64];
+    }
+#pragma unroll
+    for (int r = 0; r < kLdltRows; r++) {
+        const int i = kLdltWaves * r + w;
+        if (i >= p1 && i < n) {
+            double L[6];
+#pragma unroll
+            for (int t = 0; t < 6; t++) L[t] = Lpan[i * 6 + t];
+            if (i < 64) {
+                double v0 = R[0][r];
+#pragma unroll
+                for (int t = 0; t < 6; t++) v0 -= L[t] * u0[t];
+                R[0][r] = lane >= i ? v0 : R[0][r];
+            }
+            if (n >= 64) {
+                double v1 = R[1][r];
+#pragma unroll
+                for (int t = 0; t < 6; t++) v1 -= L[t] * u1[t];
+                R[1][r] = lane + 64 >= i ? v1 : R[1][r];
+            }
+            if (i < q1) {   // the next panel's row: final, published
+                Un[(i - p1) * kLdltMax + lane] = R[0][r];
+                Un[(i - p1) * kLdltMax + lane + 64] = R[1][r];
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kLdltThreads) k_ldlt_reg(int n, const double* __restrict__ Sg, const double* bs,
+                                                           double* x, double* scal, const int* run) {
     BA_GATE(run);
     extern __shared__ double lds[];
-    double* Lall = lds;                    // n x n, Lall[k * n + i] = L[i][k]
-    double* U = Lall + (size_t)n * n;      // 6 x kLdltMax panel rows
-    double* Lpan = U + 6 * kLdltMax;       // kLdltMax x 6
-    double* dvec = Lpan + 6 * kLdltMax;    // n
-    double* y = dvec + kLdltMax;           // n
+    double* Lall = lds;                               // n x n, Lall[k * n + i] = L[i][k]
+    double* Ub = Lall + (size_t)n * n;                // 2 x (6 x kLdltMax) panel rows
+    double* Lpan = Ub + 12 * kLdltMax;                // kLdltMax x 6
+    double* dvec = Lpan + 6 * kLdltMax;               // n
+    double* y = dvec + kLdltMax;                      // n
     __shared__ int ok;
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: row branches stay scalar
     // [S | b] (n <= 126 < kLdltMax): column n carries the right-hand side, so the row updates run
     // the forward substitution L y = b with the oracle's sequence (y_i -= l_ik y_k, k ascending)
     // and y_k is final when row k becomes a pivot row
@@ -1177,126 +1379,46 @@ __global__ void __launch_bounds__(1024) k_ldlt_reg(int n, const double* __restri
             R[c][r] = (i < n && j < n && i <= j) ? Sg[(size_t)i * n + j] : (i < n && j == n) ? bs[i] : 0.0;
         }
     LDLT_PROBE(0);
+#pragma unroll
+    for (int r = 0; r < kLdltRows; r++) {   // panel 0's rows
+        const int i = kLdltWaves * r + w;
+        if (i < 6 && i < n) {
+            Ub[i * kLdltMax + lane] = R[0][r];
+            Ub[i * kLdltMax + lane + 64] = R[1][r];
+        }
+    }
     if (tid == 0) ok = 1;
     __syncthreads();
     LDLT_PROBE(1);
+    int buf = 0;
     for (int p0 = 0; p0 < n; p0 += 6) {
-        const int p1 = min(p0 + 6, n), pw = p1 - p0;
-        LDLT_PROBE(10 + 4 * (p0 / 6));
-#pragma unroll
-        for (int r = 0; r < kLdltRows; r++) {
-            const int i = kLdltWaves * r + w;
-            if (i >= p0 && i < p1) {
-                U[(i - p0) * kLdltMax + lane] = R[0][r];
-                U[(i - p0) * kLdltMax + lane + 64] = R[1][r];
-            }
-        }
-        __syncthreads();
+        const int p1 = min(p0 + 6, n), pw = p1 - p0, q1 = min(p1 + 6, n);
+        double* U = Ub + buf * 6 * kLdltMax;
+        double* Un = Ub + (buf ^ 1) * 6 * kLdltMax;
         LDLT_PROBE(11 + 4 * (p0 / 6));
-        if (tid < kLdltMax) {
-            // panel factorisation, one thread per column j (waves 0-1): every thread first
-            // factorises the panel's 6x6 diagonal block from LDS (the same operations as the
-            // block's own columns perform below, so d and the block's L agree bit for bit), then
-            // its own column: l_jk = u_kj / d_k and u_tj -= L[t][k] u_kj, k ascending -- no
-            // cross-lane traffic inside the panel
-            const int j = tid;
-            double Bk[6][6], Lb[6][6], dd[6];
-#pragma unroll
-            for (int t = 0; t < 6; t++)
-#pragma unroll
-                for (int c = 0; c < 6; c++) {
-                    Bk[t][c] = (t < pw && c < pw && c >= t) ? U[t * kLdltMax + p0 + c] : 0.0;
-                    Lb[t][c] = 0.0;
-                }
-            bool bad = false;
-            // each pivot divides up to 5 block entries and then this thread's column entry: one
-            // reciprocal per pivot (SharedDiv, the division's own quotients) instead of VCC-serialised
-            // divisions
-            SharedDiv sd[6] = {SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0), SharedDiv(1.0),
-                               SharedDiv(1.0)};
-#pragma unroll
-            for (int t = 0; t < 6; t++) {
-                dd[t] = Bk[t][t];
-                if (t < pw) {
-                    bad |= dd[t] == 0.0;
-                    sd[t] = SharedDiv(dd[t]);
-#pragma unroll
-                    for (int t2 = t + 1; t2 < 6; t2++)
-                        if (t2 < pw) Lb[t2][t] = sd[t].div(Bk[t][t2]);
-#pragma unroll
-                    for (int t2 = t + 1; t2 < 6; t2++)
-#pragma unroll
-                        for (int c = t2; c < 6; c++)
-                            if (c < pw) Bk[t2][c] -= Lb[t2][t] * Bk[t][c];
-                }
-            }
-            LDLT_PROBE(200 + (p0 / 6 < 15 ? p0 / 6 : 15));
-            double u[6];
-#pragma unroll
-            for (int t = 0; t < 6; t++) u[t] = t < pw ? U[t * kLdltMax + j] : 0.0;
-#pragma unroll
-            for (int t = 0; t < 6; t++) {
-                if (t < pw) {
-                    const int k = p0 + t;
-                    const bool act = j > k && j < n;
-                    const double l = act ? sd[t].div(u[t]) : 0.0;
-#pragma unroll
-                    for (int t2 = t + 1; t2 < 6; t2++)
-                        if (t2 < pw && j >= p0 + t2) u[t2] -= Lb[t2][t] * u[t];
-                    if (act) {
-                        Lall[(size_t)k * n + j] = l;
-                        Lpan[j * 6 + t] = l;
-                    }
-                    if (j == n) y[k] = u[t];   // row k's right-hand side is final: forward-substituted y_k
-                }
-            }
-            LDLT_PROBE(220 + (p0 / 6 < 15 ? p0 / 6 : 15));
-#pragma unroll
-            for (int t = 0; t < 6; t++)
-                if (t < pw) U[t * kLdltMax + j] = u[t];
-            if (j == 0) {
-#pragma unroll
-                for (int t = 0; t < 6; t++)
-                    if (t < pw) dvec[p0 + t] = dd[t];
-                if (bad) ok = 0;
-            }
+        if (w < kLdltMax / 64) {
+            if (pw == 6) ldlt_panel6(n, p0, tid, U, Lall, Lpan, dvec, y, &ok);
+            else ldlt_panel_generic(n, p0, pw, tid, U, Lall, Lpan, dvec, y, &ok);
         }
         __syncthreads();
         LDLT_PROBE(12 + 4 * (p0 / 6));
         if (!ok) break;
-        double u0[6], u1[6];
-#pragma unroll
-        for (int t = 0; t < 6; t++) {
-            u0[t] = t < pw ? U[t * kLdltMax + lane] : 0.0;
-            u1[t] = t < pw ? U[t * kLdltMax + lane + 64] : 0.0;
-        }
-        // rows i >= 64 own no column below 64 on or right of the diagonal; column registers
-        // 64.. exist only for n >= 64 (the right-hand side sits at column n)
-#pragma unroll
-        for (int r = 0; r < kLdltRows; r++) {
-            const int i = kLdltWaves * r + w;
-            if (i >= p1 && i < n) {
-                double L[6];
-#pragma unroll
-                for (int t = 0; t < 6; t++) L[t] = t < pw ? Lpan[i * 6 + t] : 0.0;
-                if (i < 64) {
-                    double v0 = R[0][r];
-#pragma unroll
-                    for (int t = 0; t < 6; t++)
-                        if (t < pw) v0 -= L[t] * u0[t];
-                    if (lane >= i) R[0][r] = v0;
-                }
-                if (n >= 64) {
-                    double v1 = R[1][r];
-#pragma unroll
-                    for (int t = 0; t < 6; t++)
-                        if (t < pw) v1 -= L[t] * u1[t];
-                    if (lane + 64 >= i) R[1][r] = v1;
-                }
-            }
-        }
+        // the panel's updates, k ascending per element, and the next panel's rows published
+#ifdef ORB_LDLT_PROBE
+        const long long tw0 = clock64();
+#endif
+        // (a partial panel, pw < 6, is the last one: p1 = n, no row is live and nothing is read).
+        // The wave index is re-made opaque per panel: hoisted out of the panel loop, the sixteen
+        // rows' offsets and tests spilled SGPRs into VGPR lanes (a v_readlane each per row)
+        int wv = w;
+        asm volatile("" : "+s"(wv));
+        ldlt_trail(R, U, Un, Lpan, n, p1, q1, wv, lane);
+#ifdef ORB_LDLT_PROBE
+        if (lane == 0 && p0 / 6 < 16) g_ldlt_probe[96 + 8 * (p0 / 6) + w] = clock64() - tw0;   // per-wave trailing time
+#endif
         __syncthreads();
         LDLT_PROBE(13 + 4 * (p0 / 6));
+        buf ^= 1;
     }
     LDLT_PROBE(2);
     if (!ok) {
@@ -1475,26 +1597,54 @@ __global__ void __launch_bounds__(64) k_lm_begin(LmDev* L, int iterations) {
     L->done = 0;
     L->nTrial = 0;
     L->nSolve = 0;
+    L->steps = 0;
     L->ni = 2;
     L->currentChi = 0;
     L->iniChi = 0;
 }
 
 // one thread: the host code of BaEngine::lm_solve after its readback, verbatim in order;
-// returns whether the trial is undone (pop)
-__device__ int lm_decide(LmDev* L, double* scal, volatile int* host) {
-    if (!L->haveChi) {
-        L->currentChi = L->iniChi = scal[0];
-        L->haveChi = 1;
+// returns whether the trial is undone (pop).  The LM state's scalars, the trial's scalars and the
+// host's stop flag are read up front (independent loads in flight together) and written back at
+// the end: through the global pointers every access would wait for the one before it.
+struct LmHead {
+    int ctl[4];
+    int it, iterations, qmax, nBad, haveChi, done, nTrial, nSolve, steps;
+    double ni, currentChi, iniChi;
+};
+__device__ int lm_decide(LmDev* Lg, double* scal, volatile int* host, const double* chi) {
+    const bool stop = host[0] != 0;
+    LmHead L;
+    L.ctl[0] = Lg->ctl[0];
+    L.ctl[1] = Lg->ctl[1];
+    L.ctl[2] = Lg->ctl[2];
+    L.ctl[3] = Lg->ctl[3];
+    L.it = Lg->it;
+    L.iterations = Lg->iterations;
+    L.qmax = Lg->qmax;
+    L.nBad = Lg->nBad;
+    L.haveChi = Lg->haveChi;
+    L.done = Lg->done;
+    L.nTrial = Lg->nTrial;
+    L.nSolve = Lg->nSolve;
+    L.steps = Lg->steps;
+    L.ni = Lg->ni;
+    L.currentChi = Lg->currentChi;
+    L.iniChi = Lg->iniChi;
+    const double s0 = chi ? chi[0] : scal[0], s1 = chi ? chi[1] : scal[1];   // chi: the fused totals (LDS)
+    const double s2 = scal[2], s3 = scal[3], s5 = scal[5];
+    if (!L.haveChi) {
+        L.currentChi = L.iniChi = s0;
+        L.haveChi = 1;
     }
-    const bool ok2 = scal[3] != 0.0;
-    double tempChi = scal[1];
+    const bool ok2 = s3 != 0.0;
+    double tempChi = s1;
     if (!ok2) tempChi = DBL_MAX;
-    double rho = L->currentChi - tempChi;
-    double scale = scal[2];
+    double rho = L.currentChi - tempChi;
+    double scale = s2;
     scale += 1e-3;
     rho /= scale;
-    double lambda = scal[5];
+    double lambda = s5;
     int pop = 0;
     if (rho > 0 && isfinite(tempChi)) {
         const double a3 = 2 * rho - 1;
@@ -1502,62 +1652,86 @@ __device__ int lm_decide(LmDev* L, double* scal, volatile int* host) {
         alpha = fmin(alpha, 2. / 3.);
         const double scaleFactor = fmax(1. / 3., alpha);
         lambda *= scaleFactor;
-        L->ni = 2;
-        L->currentChi = tempChi;
+        L.ni = 2;
+        L.currentChi = tempChi;
     } else {
-        lambda *= L->ni;
-        L->ni *= 2;
+        lambda *= L.ni;
+        L.ni *= 2;
         pop = 1;
     }
     scal[5] = lambda;
-    L->qmax++;
-    if (L->nTrial < kLmTrials) {
-        L->trialChi[L->nTrial] = tempChi;
-        L->trialLam[L->nTrial] = lambda;
+    L.qmax++;
+    if (L.nTrial < kLmTrials) {
+        Lg->trialChi[L.nTrial] = tempChi;
+        Lg->trialLam[L.nTrial] = lambda;
     }
-    L->nTrial++;
-    const bool stop = host[0] != 0;
-    L->ctl[2] = 0;
-    if (rho < 0 && L->qmax < 10 && !stop) {   // another trial on the same system
-        L->ctl[1] = 0;
+    L.nTrial++;
+    L.ctl[2] = 0;
+    if (rho < 0 && L.qmax < 10 && !stop) {   // another trial on the same system
+        L.ctl[1] = 0;
     } else {                                  // lm_solve returns
-        if (L->nSolve < kLmSolves) {
-            L->solveIni[L->nSolve] = L->iniChi;
-            L->solveChi[L->nSolve] = L->currentChi;
+        if (L.nSolve < kLmSolves) {
+            Lg->solveIni[L.nSolve] = L.iniChi;
+            Lg->solveChi[L.nSolve] = L.currentChi;
         }
-        L->nSolve++;
+        L.nSolve++;
         bool term = false;
-        if (L->qmax == 10 || rho == 0) {
+        if (L.qmax == 10 || rho == 0) {
             term = true;
         } else {
-            if ((L->iniChi - L->currentChi) * 1e3 < L->iniChi) L->nBad++;
-            else L->nBad = 0;
-            if (L->nBad >= 3) term = true;
+            if ((L.iniChi - L.currentChi) * 1e3 < L.iniChi) L.nBad++;
+            else L.nBad = 0;
+            if (L.nBad >= 3) term = true;
         }
-        L->it++;
-        if (term || L->it >= L->iterations || stop) {
-            L->done = 1;
-            L->ctl[0] = 0;
-            L->ctl[1] = 0;
+        L.it++;
+        if (term || L.it >= L.iterations || stop) {
+            L.done = 1;
+            L.ctl[0] = 0;
+            L.ctl[1] = 0;
         } else {
-            L->ctl[1] = 1;
-            L->haveChi = 0;
-            L->qmax = 0;
+            L.ctl[1] = 1;
+            L.haveChi = 0;
+            L.qmax = 0;
         }
     }
-    host[3] = L->it;
-    host[2] = host[2] + 1;
-    host[1] = L->done;   // read by the host after this step's event: kernel completion publishes it
+    L.steps++;
+    Lg->ctl[0] = L.ctl[0];
+    Lg->ctl[1] = L.ctl[1];
+    Lg->ctl[2] = L.ctl[2];
+    Lg->it = L.it;
+    Lg->qmax = L.qmax;
+    Lg->nBad = L.nBad;
+    Lg->haveChi = L.haveChi;
+    Lg->done = L.done;
+    Lg->nTrial = L.nTrial;
+    Lg->nSolve = L.nSolve;
+    Lg->steps = L.steps;
+    Lg->ni = L.ni;
+    Lg->currentChi = L.currentChi;
+    Lg->iniChi = L.iniChi;
+    host[3] = L.it;
+    host[2] = L.steps;
+    host[1] = L.done;   // read by the host after this step's event: kernel completion publishes it
     return pop;
 }
 
-// End of a trial: computeScale (k_scale's canonical sum, problems with 6 nP + 3 nL <= 2048 * 64;
-// larger ones ran k_scale_chunks + k_csum into scal[2] and pass scale = 0), the LM decision, and
-// the pop of a rejected trial, in one workgroup.
+// End of a trial: the chi2 totals of the step's two linearisations (ChiFuse: k_linearize's chunk
+// trees, summed here instead of by two k_chi2_finish launches), computeScale (k_scale's canonical
+// sum, problems with 6 nP + 3 nL <= 2048 * 64; larger ones ran k_scale_chunks + k_csum into
+// scal[2] and pass scale = 0), the LM decision, and the pop of a rejected trial, in one workgroup.
+constexpr int kChiFuseMax = 1024;   // chunk trees per linearisation (nE <= 65536) summed in LDS
+struct ChiFuse {
+    const double* chunksSys;     // the system linearisation's chunk trees (chi2 -> scal[0]), or null
+    const double* chunksTrial;   // the trial's (-> scal[1])
+    int nE;
+};
 __global__ void __launch_bounds__(1024) k_lm_trial_end(LmDev* L, double* scal, volatile int* host, BaStructDev s,
                                                        Se3* T, const Se3* Tbak, double* X, const double* Xbak,
-                                                       const double* x, const double* bp, const double* bl, int scale) {
+                                                       const double* x, const double* bp, const double* bl, int scale,
+                                                       ChiFuse cf) {
     __shared__ double lv[2048];
+    __shared__ double cA[kChiFuseMax], cB[kChiFuseMax];
+    __shared__ double chi[2];
     __shared__ int pop, live;
     // one read of the run flag for the whole workgroup: lm_decide below may clear ctl[0] (the
     // run ends with this trial) and a wave reading it after that would skip the pop
@@ -1565,28 +1739,44 @@ __global__ void __launch_bounds__(1024) k_lm_trial_end(LmDev* L, double* scal, v
     __syncthreads();
     if (!live) return;   // a step queued after the run ended
     const int nP = s.nP, nL = s.nL;
-    if (scale) {
-        const int n = 6 * nP + 3 * nL;
-        const double lambda = scal[5];
-        auto term = [&](int j) {
-            const double b = j < 6 * nP ? bp[j] : bl[j - 6 * nP];
-            return x[j] * (lambda * x[j] + b);
-        };
-        if (n <= 1) {
-            if (threadIdx.x == 0) scal[2] = n == 1 ? term(0) : 0.0;
-        } else {
-            const int m = (n + 63) >> 6;
-            const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-            for (int c = w; c < m; c += 16) {
-                const int j = c * 64 + lane;
-                const double t = wave_tree(j < n ? term(j) : 0.0);
-                if (lane == 0) lv[c] = t;
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) scal[2] = local_csum_inplace(lv, m);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const bool fuse = cf.chunksSys != nullptr;
+    const int mc = (cf.nE + 63) >> 6;   // fuse: 2 <= nE, mc <= kChiFuseMax (host)
+    if (fuse)
+        for (int c = threadIdx.x; c < mc; c += blockDim.x) {
+            cA[c] = cf.chunksSys[c];
+            cB[c] = cf.chunksTrial[c];
+        }
+    const int n = 6 * nP + 3 * nL;
+    const int m = (n + 63) >> 6;
+    const double lambda = scal[5];
+    auto term = [&](int j) {
+        const double b = j < 6 * nP ? bp[j] : bl[j - 6 * nP];
+        return x[j] * (lambda * x[j] + b);
+    };
+    if (scale && n > 1)
+        for (int c = w; c < m; c += 16) {
+            const int j = c * 64 + lane;
+            const double t = wave_tree(j < n ? term(j) : 0.0);
+            if (lane == 0) lv[c] = t;
+        }
+    __syncthreads();
+    // block_finish_csum's totals: wave_tree pairs as tree64_local, so wave_lds_csum is
+    // local_csum_inplace's canonical sum
+    if (scale && w == 0) {
+        const double t = n > 1 ? wave_lds_csum(lv, m) : n == 1 ? term(0) : 0.0;
+        if (lane == 0) scal[2] = t;
+    }
+    if (fuse && (w == 1 || w == 2)) {
+        double* c = w == 1 ? cA : cB;
+        const double t = mc == 1 ? c[0] : wave_lds_csum(c, mc);
+        if (lane == 0) {
+            chi[w - 1] = t;
+            scal[w - 1] = t;
         }
     }
-    if (threadIdx.x == 0) pop = lm_decide(L, scal, host);
+    __syncthreads();
+    if (threadIdx.x == 0) pop = lm_decide(L, scal, host, fuse ? chi : nullptr);
     __syncthreads();
     if (!pop) return;
     for (int g = threadIdx.x; g < nP + nL; g += blockDim.x) {   // k_pop
@@ -2879,7 +3069,7 @@ int BaEngine::init() {
 }
 
 bool BaEngine::dense_solver(int n) const {
-    const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
+    const size_t regShm = ldlt_reg_shm(n);
     const size_t ldsBytes = sizeof(double) * ((size_t)n + (size_t)n * n);
     return n <= kDenseMaxN && ((n < kLdltMax && regShm <= ldsMax_) || ldsBytes <= ldsMax_);
 }
@@ -3382,7 +3572,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
         hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
     }
-    if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(1024), 0, s, S, dTerms_, dHpp_, dBp_, nullptr);
+    if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(kSysThreads), 0, s, S, dTerms_, dHpp_, dBp_, nullptr);
     if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(12 * nL, 256)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_, nullptr);
     if (comm_) {
         const RedBuf rb[3] = {{dHpp_, 21 * (size_t)nP}, {dBp_, 6 * (size_t)nP}, {dScal_, 1}};
@@ -3409,7 +3599,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     const size_t ldsBytes = sizeof(double) * ((size_t)n + (size_t)n * n);
     const int in_lds = ldsBytes <= ldsMax_ ? 1 : 0;
     const size_t shm = in_lds ? ldsBytes : sizeof(double) * (size_t)n;
-    const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
+    const size_t regShm = ldlt_reg_shm(n);
     const bool use_reg = n < kLdltMax && regShm <= ldsMax_;   // b rides in column n
     const DenseLdlt kind = dense_ldlt_kind(n, use_reg);
     // n <= 128: register-resident single-workgroup LDL^T; S fits LDS: single-workgroup in LDS;
@@ -3459,7 +3649,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         } else if (kind == DenseLdlt::Row) {
             hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else if (kind == DenseLdlt::Reg) {
-            hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
+            hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(kLdltThreads), regShm, s, n, dS_, dBs_, dX2_, dScal_, nullptr);
         } else {
             hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, nullptr);
         }
@@ -3579,18 +3769,22 @@ void BaEngine::enqueue_lm_step(bool first) {
     const int nE = S.nE, nP = S.nP, nL = S.nL;
     const int* ctl = dLm_->ctl;
     LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1, tmpA0_, dCounter_, dScal_ + 0, ctl + 1};
+    // two or more edges: the chi2 totals are summed by k_lm_trial_end from chunk buffers of their own
+    // (a single edge's total is its r0, which the trial's linearisation overwrites)
+    const bool fuse = nE >= 2 && (nE + 63) / 64 <= kChiFuseMax;
+    if (fuse) la.chunks = tmpB0_;
     if (nE) {
         hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
-        hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+        if (!fuse) hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
     }
-    if (nP + nL) hipLaunchKernelGGL(k_sys_reduce, dim3(nP + nblk(12 * nL, 1024)), dim3(1024), 0, s, S, dTerms_, dHpp_,
+    if (nP + nL) hipLaunchKernelGGL(k_sys_reduce, dim3(nP + nblk(12 * nL, kSysThreads)), dim3(kSysThreads), 0, s, S, dTerms_, dHpp_,
                                     dBp_, dHll_, dBl_, ctl + 1);
     if (first) hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, nP, nL, dHpp_, dHll_, dScal_, ctl + 2);
     const int n = 6 * nP;
     const size_t ldsBytes = sizeof(double) * ((size_t)n + (size_t)n * n);
     const int in_lds = ldsBytes <= ldsMax_ ? 1 : 0;
     const size_t shm = in_lds ? ldsBytes : sizeof(double) * (size_t)n;
-    const size_t regShm = sizeof(double) * ((size_t)n * n + 12 * kLdltMax + 2 * kLdltMax);
+    const size_t regShm = ldlt_reg_shm(n);
     const bool use_reg = n < kLdltMax && regShm <= ldsMax_;   // b rides in column n
     const SysAddr sa{dS_, n, nullptr, nullptr, 0, nullptr};
     if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_, 0.0, 1,
@@ -3602,16 +3796,17 @@ void BaEngine::enqueue_lm_step(bool first) {
     else if (kind == DenseLdlt::T) hipLaunchKernelGGL(k_ldlt_t, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else if (kind == DenseLdlt::D2) hipLaunchKernelGGL(k_ldlt_2d, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else if (kind == DenseLdlt::Row) hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
-    else if (kind == DenseLdlt::Reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else if (kind == DenseLdlt::Reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(kLdltThreads), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, ctl);
     if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_, dXbak_,
                                     dX2_, dHplA_, dHll_, dBl_, 0.0, 1, dScal_, ctl);
     la.linearize = 0;
     la.out = dScal_ + 1;
     la.run = ctl;
+    if (fuse) la.chunks = tmpB1_;
     if (nE) {
         hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
-        hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+        if (!fuse) hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
     }
     const bool small = scale_small(nP, nL);
     if (!small) {
@@ -3622,7 +3817,8 @@ void BaEngine::enqueue_lm_step(bool first) {
         hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, L0, L0, ctl);
     }
     hipLaunchKernelGGL(k_lm_trial_end, dim3(1), dim3(1024), 0, s, dLm_, dScal_, (volatile int*)hLm_, S, dT_, dTbak_,
-                       dX_, dXbak_, dX2_, dBp_, dBl_, small ? 1 : 0);
+                       dX_, dXbak_, dX2_, dBp_, dBl_, small ? 1 : 0,
+                       fuse ? ChiFuse{tmpB0_, tmpB1_, nE} : ChiFuse{nullptr, nullptr, 0});
 }
 
 int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* its) {
@@ -3811,8 +4007,8 @@ int debug_ldlt(int n, const double* S, const double* b, double* x, int variant) 
         if (n > kLdltRowMax) return -3;
         hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, 0, n, dS, dB, dX, dScal, nullptr);
     } else if (variant == 0) {
-        const size_t shm = sizeof(double) * ((size_t)n * n + 14 * kLdltMax);
-        hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal, nullptr);
+        const size_t shm = ldlt_reg_shm(n);
+        hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(kLdltThreads), shm, 0, n, dS, dB, dX, dScal, nullptr);
     } else {
         hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), sizeof(double) * n + 16, 0, n, dS, dB, dX, dScal, 0, nullptr);
     }

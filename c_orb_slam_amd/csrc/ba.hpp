@@ -44,7 +44,7 @@ constexpr int kLmTrials = 128;   // 10 trials x <= 12 iterations per optimize() 
 constexpr int kLmSolves = 16;
 struct LmDev {
     int ctl[4];
-    int it, iterations, qmax, nBad, haveChi, done, nTrial, nSolve;
+    int it, iterations, qmax, nBad, haveChi, done, nTrial, nSolve, steps;
     double ni, currentChi, iniChi;
     double trialChi[kLmTrials], trialLam[kLmTrials], solveIni[kLmSolves], solveChi[kLmSolves];
 };

@@ -24,26 +24,24 @@ int main(int argc, char** argv) {
     hipMalloc(&dS, 8 * n * n); hipMalloc(&dB, 8 * n); hipMalloc(&dX, 8 * n); hipMalloc(&dScal, 128);
     hipMemcpy(dS, S.data(), 8 * n * n, hipMemcpyHostToDevice);
     hipMemcpy(dB, b.data(), 8 * n, hipMemcpyHostToDevice);
-    const size_t shm = sizeof(double) * ((size_t)n * n + 14 * orbgpu::kLdltMax);
+    const size_t shm = orbgpu::ldlt_reg_shm(n);
     for (int rep = 0; rep < 3; rep++) {
-        hipLaunchKernelGGL(orbgpu::k_ldlt_reg, dim3(1), dim3(1024), shm, 0, n, dS, dB, dX, dScal, nullptr);
+        hipLaunchKernelGGL(orbgpu::k_ldlt_reg, dim3(1), dim3(orbgpu::kLdltThreads), shm, 0, n, dS, dB, dX, dScal, nullptr);
         hipDeviceSynchronize();
     }
     long long p[256];
     hipMemcpyFromSymbol(p, HIP_SYMBOL(orbgpu::g_ldlt_probe), sizeof(p));
     printf("load %lld | panels %lld | fwd %lld | bwd %lld  (cycles)\n", p[1] - p[0], p[2] - p[1], p[3] - p[2], p[4] - p[3]);
-    long long pub = 0, ph1 = 0, tr = 0;
-    for (int k = 0; k < n / 6; k++) {
-        pub += p[11 + 4 * k] - p[10 + 4 * k];
+    long long ph1 = 0, tr = 0;
+    for (int k = 0; k < (n + 5) / 6; k++) {
         ph1 += p[12 + 4 * k] - p[11 + 4 * k];
         tr += p[13 + 4 * k] - p[12 + 4 * k];
     }
-    printf("publish %lld | phase1 %lld | trailing %lld  (cycles, n/6 panels)\n", pub, ph1, tr);
-    long long blk = 0, col = 0;
-    for (int k = 0; k < n / 6 && k < 15; k++) {
-        blk += p[200 + k] - p[11 + 4 * k];
-        col += p[220 + k] - p[200 + k];
+    printf("panel factorisation %lld | trailing update + next panel rows %lld  (cycles, %d panels)\n", ph1, tr, (n + 5) / 6);
+    for (int k = 0; k < (n + 5) / 6 && k < 16; k++) {
+        printf("panel %2d wave trailing cycles:", k);
+        for (int w = 0; w < 8; w++) printf(" %6lld", p[96 + 8 * k + w]);
+        printf("\n");
     }
-    printf("phase1 split (first 15 panels): diagonal block %lld | own column %lld (cycles)\n", blk, col);
     return 0;
 }
