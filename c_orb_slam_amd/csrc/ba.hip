@@ -1148,13 +1148,7 @@ __global__ void __launch_bounds__(256) k_ldlt_2d(int n, const double* __restrict
     ldlt_backward_wave(n, Lall, dvec, y, x, scal);
 }
 
-// Register-resident LDL^T + solve for n < 128 (<= 21 free keyframes), 512 threads.
-// Thread (wave w < 8, lane) owns rows i = 8 r + w (r < 16) of columns j = lane, lane + 64.
-// Per 6-column panel: waves 0-1 factorise the panel (one thread per column j: the panel's 6x6
-// diagonal block, then column j) from its rows in LDS and write L (Lall[k][i] = L[i][k],
-// Lpan[i][k - p0]) and d_k; then every thread applies the panel's updates to its rows in k order
-// and the owners of the next panel's rows publish them to the other panel buffer.  Two barriers
-// per panel.  Per-element operation sequence identical to oracle ora_ldlt_solve.
+// The dense LDL^T of the local BA's reduced system (k_ldlt_reg, below).
 #ifdef ORB_LDLT_PROBE
 __device__ long long g_ldlt_probe[256];
 #define LDLT_PROBE(slot) \
@@ -1171,9 +1165,9 @@ constexpr int kTiledMinPoses = kBaTiledMinPoses;   // 6 x 24 = 144 rows: the fir
 constexpr int kDenseMaxN = 144;   // >= every n the dense single-workgroup solvers take (n^2 doubles in LDS)
 constexpr int kLdltWaves = 8;     // 512 threads: 256 VGPRs per lane, the panel registers stay unspilled
 constexpr int kLdltThreads = 64 * kLdltWaves;
-constexpr int kLdltRows = kLdltMax / kLdltWaves;
-// LDS of k_ldlt_reg: Lall (n x n), two 6 x kLdltMax panel buffers, Lpan (kLdltMax x 6), d, y
-static inline size_t ldlt_reg_shm(int n) { return sizeof(double) * ((size_t)n * n + 20 * kLdltMax); }
+// LDS of k_ldlt_reg: Lall (n x n), three 6 x kLdltMax panel row buffers, two kLdltMax x 6 panel L
+// buffers, d, y
+static inline size_t ldlt_reg_shm(int n) { return sizeof(double) * ((size_t)n * n + 1 + 32 * kLdltMax); }
 
 // SharedDiv::div without its branch: the quotient of an in-range numerator, or a * r for a zero
 // one (a / b = a signed zero); any other numerator (or an out-of-range divisor) sets `bad` and the
@@ -1315,26 +1309,30 @@ __device__ __forceinline__ void ldlt_panel6(int n, int p0, int j, double* U, dou
         for (int t = 0; t < 6; t++) dvec[p0 + t] = dd[t];
 }
 
-// k_ldlt_reg's trailing update by one thread: its rows i = 8 r + w >= p1 (w wave-uniform, so the
-// row tests are scalar branches) subtract the panel's six rank-one updates in k order.  Rows
-// [p1, q1) -- the next panel's, final now -- go to Un.  Rows i >= 64 own no column below 64 on or
-// right of the diagonal; column registers 64.. matter only for n >= 64 (the right-hand side sits
-// at column n).
-__device__ __forceinline__ void ldlt_trail(double (&R)[2][kLdltRows], const double* U, double* Un, const double* Lpan,
-                                           int n, int p1, int q1, int w, int lane) {
+// Row waves of k_ldlt_reg (waves 2..7, kRowWaves of them): wave 2 + t owns rows i = 6 r + t
+// (slot r < kRowSlots) of columns j = lane, lane + 64, so a 6-row panel p is slot p of every row
+// wave.  In phase p a row wave applies panel p - 1's six rank-one updates (its L from Lp, its
+// rows u from Up) in k order to its rows i >= 6 (p + 1) -- panel p's own rows were handed to the
+// factor waves one phase earlier -- and publishes slot p + 1 (panel p + 1's row, now updated by
+// every panel up to p - 1) to Un.  Rows i >= 64 own no column below 64 on or right of the
+// diagonal; column registers 64.. matter only for n >= 64 (the right-hand side sits at column n).
+constexpr int kRowWaves = 6;
+constexpr int kRowSlots = (kLdltMax + kRowWaves - 1) / kRowWaves;
+__device__ __forceinline__ void ldlt_rows(double (&R)[2][kRowSlots], const double* Up, const double* Lp, double* Un,
+                                          int n, int p1, int t6, int lane) {
     double u0[6], u1[6];
 #pragma unroll
     for (int t = 0; t < 6; t++) {
-        u0[t] = U[t * kLdltMax + lane];
-        u1[t] = U[t * kLdltMax + lane + 64];
+        u0[t] = Up[t * kLdltMax + lane];
+        u1[t] = Up[t * kLdltMax + lane + 64];
     }
 #pragma unroll
-    for (int r = 0; r < kLdltRows; r++) {
-        const int i = kLdltWaves * r + w;
+    for (int r = 0; r < kRowSlots; r++) {
+        const int i = kRowWaves * r + t6;
         if (i >= p1 && i < n) {
             double L[6];
 #pragma unroll
-            for (int t = 0; t < 6; t++) L[t] = Lpan[i * 6 + t];
+            for (int t = 0; t < 6; t++) L[t] = Lp[i * 6 + t];
             if (i < 64) {
                 double v0 = R[0][r];
 #pragma unroll
@@ -1347,7 +1345,7 @@ __device__ __forceinline__ void ldlt_trail(double (&R)[2][kLdltRows], const doub
                 for (int t = 0; t < 6; t++) v1 -= L[t] * u1[t];
                 R[1][r] = lane + 64 >= i ? v1 : R[1][r];
             }
-            if (i < q1) {   // the next panel's row: final, published
+            if (i < p1 + 6) {   // panel p + 1's row
                 Un[(i - p1) * kLdltMax + lane] = R[0][r];
                 Un[(i - p1) * kLdltMax + lane + 64] = R[1][r];
             }
@@ -1355,70 +1353,113 @@ __device__ __forceinline__ void ldlt_trail(double (&R)[2][kLdltRows], const doub
     }
 }
 
+// Register-resident LDL^T + solve for n < 128 (<= 21 free keyframes), 512 threads, with a
+// one-panel lookahead: waves 0-1 factorise 6-column panels (one thread per column j), waves 2-7
+// hold the rows.  Phase p: the factor waves take panel p's rows (published by the row waves in
+// phase p - 1, updated by every panel up to p - 2), apply panel p - 1's updates to them
+// themselves, and factorise panel p (ldlt_panel6); meanwhile the row waves apply panel p - 1 to
+// the rows below panel p and publish panel p + 1's rows -- the trailing update runs under the
+// factorisation.  One barrier per phase (the factor waves also meet once between their update
+// and the factorisation: a panel's diagonal block spans both waves' columns).  Panel rows rotate
+// through three buffers, panel L through two.  Per-element operation sequence identical to
+// oracle ora_ldlt_solve (every element receives the pivots' updates in ascending k).
 __global__ void __launch_bounds__(kLdltThreads) k_ldlt_reg(int n, const double* __restrict__ Sg, const double* bs,
                                                            double* x, double* scal, const int* run) {
     BA_GATE(run);
     extern __shared__ double lds[];
     double* Lall = lds;                               // n x n, Lall[k * n + i] = L[i][k]
-    double* Ub = Lall + (size_t)n * n;                // 2 x (6 x kLdltMax) panel rows
-    double* Lpan = Ub + 12 * kLdltMax;                // kLdltMax x 6
-    double* dvec = Lpan + 6 * kLdltMax;               // n
+    double* Ub = Lall + (((size_t)n * n + 1) & ~(size_t)1);   // 3 x (6 x kLdltMax) panel rows (16-B aligned)
+    double* Lb = Ub + 18 * kLdltMax;                  // 2 x (kLdltMax x 6) panel L
+    double* dvec = Lb + 12 * kLdltMax;                // n
     double* y = dvec + kLdltMax;                      // n
-    __shared__ int ok;
+    __shared__ int ok, meet;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: row branches stay scalar
+    const bool factor = w < kLdltMax / 64;
+    const int t6 = w - kLdltMax / 64;
     // [S | b] (n <= 126 < kLdltMax): column n carries the right-hand side, so the row updates run
     // the forward substitution L y = b with the oracle's sequence (y_i -= l_ik y_k, k ascending)
     // and y_k is final when row k becomes a pivot row
-    double R[2][kLdltRows];
+    double R[2][kRowSlots];
+    if (!factor) {
 #pragma unroll
-    for (int c = 0; c < 2; c++)
+        for (int c = 0; c < 2; c++)
 #pragma unroll
-        for (int r = 0; r < kLdltRows; r++) {
-            const int i = kLdltWaves * r + w, j = lane + 64 * c;
-            R[c][r] = (i < n && j < n && i <= j) ? Sg[(size_t)i * n + j] : (i < n && j == n) ? bs[i] : 0.0;
-        }
-    LDLT_PROBE(0);
-#pragma unroll
-    for (int r = 0; r < kLdltRows; r++) {   // panel 0's rows
-        const int i = kLdltWaves * r + w;
-        if (i < 6 && i < n) {
-            Ub[i * kLdltMax + lane] = R[0][r];
-            Ub[i * kLdltMax + lane + 64] = R[1][r];
+            for (int r = 0; r < kRowSlots; r++) {
+                const int i = kRowWaves * r + t6, j = lane + 64 * c;
+                R[c][r] = (i < n && j < n && i <= j) ? Sg[(size_t)i * n + j] : (i < n && j == n) ? bs[i] : 0.0;
+            }
+        if (t6 < n) {   // panel 0's rows (slot 0)
+            Ub[t6 * kLdltMax + lane] = R[0][0];
+            Ub[t6 * kLdltMax + lane + 64] = R[1][0];
         }
     }
-    if (tid == 0) ok = 1;
+    LDLT_PROBE(0);
+    if (tid == 0) {
+        ok = 1;
+        meet = 0;
+    }
     __syncthreads();
     LDLT_PROBE(1);
-    int buf = 0;
+    int cur = 0;   // panel p's row buffer: p mod 3
     for (int p0 = 0; p0 < n; p0 += 6) {
-        const int p1 = min(p0 + 6, n), pw = p1 - p0, q1 = min(p1 + 6, n);
-        double* U = Ub + buf * 6 * kLdltMax;
-        double* Un = Ub + (buf ^ 1) * 6 * kLdltMax;
+        const int p1 = min(p0 + 6, n), pw = p1 - p0;
+        const int prv = cur == 0 ? 2 : cur - 1, nxt = cur == 2 ? 0 : cur + 1;
+        double* U = Ub + cur * 6 * kLdltMax;
+        double* Lpan = Lb + ((p0 / 6) & 1) * 6 * kLdltMax;
+        const double* Up = Ub + prv * 6 * kLdltMax;
+        const double* Lp = Lb + (((p0 / 6) & 1) ^ 1) * 6 * kLdltMax;
         LDLT_PROBE(11 + 4 * (p0 / 6));
-        if (w < kLdltMax / 64) {
+        if (factor) {
+            if (p0 > 0) {
+                // panel p - 1's updates on panel p's rows, column j = tid, k ascending
+                const int j = tid;
+                double up[6];
+#pragma unroll
+                for (int k = 0; k < 6; k++) up[k] = Up[k * kLdltMax + j];
+                // (rows t >= pw of a partial last panel are updated too: nobody reads them, and their
+                // L reads stay inside the LDS block)
+                double v[6];
+#pragma unroll
+                for (int t = 0; t < 6; t++) v[t] = U[t * kLdltMax + j];
+#pragma unroll
+                for (int t = 0; t < 6; t++)
+#pragma unroll
+                    for (int k = 0; k < 6; k++) v[t] -= Lp[(p0 + t) * 6 + k] * up[k];
+#pragma unroll
+                for (int t = 0; t < 6; t++) U[t * kLdltMax + j] = v[t];
+                // both factor waves' columns are in: the diagonal block reads either's
+                if (lane == 0) __hip_atomic_fetch_add(&meet, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int want = 2 * (p0 / 6);
+                while (__hip_atomic_load(&meet, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            LDLT_PROBE(100 + (p0 / 6 < 20 ? p0 / 6 : 20));
             if (pw == 6) ldlt_panel6(n, p0, tid, U, Lall, Lpan, dvec, y, &ok);
             else ldlt_panel_generic(n, p0, pw, tid, U, Lall, Lpan, dvec, y, &ok);
+        } else {
+            // panel p - 1's updates on the rows below panel p, panel p + 1's rows published.  The
+            // slot index is re-made opaque per panel: hoisted out of the panel loop, the rows'
+            // offsets and tests spill SGPRs into VGPR lanes (a v_readlane each per row)
+            int tv = t6;
+            asm volatile("" : "+s"(tv));
+            if (p0 > 0) {
+                ldlt_rows(R, Up, Lp, Ub + nxt * 6 * kLdltMax, n, p1, tv, lane);
+            } else if (6 + t6 < n) {   // phase 0: panel 1's rows (slot 1) as they are
+                Ub[nxt * 6 * kLdltMax + t6 * kLdltMax + lane] = R[0][1];
+                Ub[nxt * 6 * kLdltMax + t6 * kLdltMax + lane + 64] = R[1][1];
+            }
+#ifdef ORB_LDLT_PROBE
+            if (lane == 0 && p0 / 6 < 16) g_ldlt_probe[124 + 6 * (p0 / 6) + t6] = clock64();   // row waves done
+#endif
         }
+#ifdef ORB_LDLT_PROBE
+        if (factor && tid == 0) g_ldlt_probe[220 + (p0 / 6 < 20 ? p0 / 6 : 20)] = clock64();   // factor done
+#endif
         __syncthreads();
         LDLT_PROBE(12 + 4 * (p0 / 6));
         if (!ok) break;
-        // the panel's updates, k ascending per element, and the next panel's rows published
-#ifdef ORB_LDLT_PROBE
-        const long long tw0 = clock64();
-#endif
-        // (a partial panel, pw < 6, is the last one: p1 = n, no row is live and nothing is read).
-        // The wave index is re-made opaque per panel: hoisted out of the panel loop, the sixteen
-        // rows' offsets and tests spilled SGPRs into VGPR lanes (a v_readlane each per row)
-        int wv = w;
-        asm volatile("" : "+s"(wv));
-        ldlt_trail(R, U, Un, Lpan, n, p1, q1, wv, lane);
-#ifdef ORB_LDLT_PROBE
-        if (lane == 0 && p0 / 6 < 16) g_ldlt_probe[96 + 8 * (p0 / 6) + w] = clock64() - tw0;   // per-wave trailing time
-#endif
-        __syncthreads();
-        LDLT_PROBE(13 + 4 * (p0 / 6));
-        buf ^= 1;
+        cur = nxt;
     }
     LDLT_PROBE(2);
     if (!ok) {

@@ -32,16 +32,18 @@ int main(int argc, char** argv) {
     long long p[256];
     hipMemcpyFromSymbol(p, HIP_SYMBOL(orbgpu::g_ldlt_probe), sizeof(p));
     printf("load %lld | panels %lld | fwd %lld | bwd %lld  (cycles)\n", p[1] - p[0], p[2] - p[1], p[3] - p[2], p[4] - p[3]);
-    long long ph1 = 0, tr = 0;
+    long long ph = 0;
+    printf("phase cycles:");
     for (int k = 0; k < (n + 5) / 6; k++) {
-        ph1 += p[12 + 4 * k] - p[11 + 4 * k];
-        tr += p[13 + 4 * k] - p[12 + 4 * k];
+        ph += p[12 + 4 * k] - p[11 + 4 * k];
+        printf(" %lld", p[12 + 4 * k] - p[11 + 4 * k]);
     }
-    printf("panel factorisation %lld | trailing update + next panel rows %lld  (cycles, %d panels)\n", ph1, tr, (n + 5) / 6);
-    for (int k = 0; k < (n + 5) / 6 && k < 16; k++) {
-        printf("panel %2d wave trailing cycles:", k);
-        for (int w = 0; w < 8; w++) printf(" %6lld", p[96 + 8 * k + w]);
-        printf("\n");
+    printf("\nphases (factor panel p | rows: panel p - 1's updates) %lld cycles, %d panels\n", ph, (n + 5) / 6);
+    for (int k = 1; k < (n + 5) / 6 && k < 16; k++) {
+        printf("phase %2d: rows updated %5lld factor %5lld | row waves done at", k, p[100 + k] - p[11 + 4 * k],
+               p[220 + k] - p[100 + k]);
+        for (int t = 0; t < 6; t++) printf(" %5lld", p[124 + 6 * k + t] - p[11 + 4 * k]);
+        printf(" | barrier at %5lld\n", p[12 + 4 * k] - p[11 + 4 * k]);
     }
     return 0;
 }
