@@ -305,21 +305,22 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
             t[(T_HLL + r * 3 + c) * nE + i] = h;
         }
     }
-    if (a.s.ePose[i] < 0) return;
+    const int pp = a.s.pePos[i];   // the pose terms and Hpl at the edge's pose-list position
+    if (pp < 0) return;
 #pragma unroll
     for (int r = 0; r < 6; r++) {
         double s = 0;
 #pragma unroll
         for (int k = 0; k < 3; k++)
             if (k < D) s += B[k * 6 + r] * omr[k];
-        t[(T_BP + r) * nE + i] = s;
+        t[(T_BP + r) * nE + pp] = s;
 #pragma unroll
         for (int c = r; c < 6; c++) {
             double h = 0;
 #pragma unroll
             for (int k = 0; k < 3; k++)
                 if (k < D) h += (B[k * 6 + r] * w) * B[k * 6 + c];
-            t[(T_HPP + (r * (13 - r)) / 2 + (c - r)) * nE + i] = h;
+            t[(T_HPP + (r * (13 - r)) / 2 + (c - r)) * nE + pp] = h;
         }
 #pragma unroll
         for (int c = 0; c < 3; c++) {
@@ -327,7 +328,7 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
 #pragma unroll
             for (int k = 0; k < 3; k++)
                 if (k < D) h += robust ? (B[k * 6 + r] * w) * A[k * 3 + c] : B[k * 6 + r] * (A[k * 3 + c] * e.info);
-            a.Hpl[18 * (size_t)i + r * 3 + c] = h;
+            a.Hpl[18 * (size_t)pp + r * 3 + c] = h;
         }
     }
     }
@@ -373,7 +374,7 @@ __device__ __forceinline__ void pose_reduce_block(const BaStructDev& s, const do
     for (int c = w; c < m; c += nw) {
         const int j = c * 64 + lane;
         const bool valid = j < n;
-        const int a = valid ? s.peList[s0 + j] : 0;
+        const int a = valid ? s0 + j : 0;   // the pose's edges' terms sit at their list positions
         double v[27];
 #pragma unroll
         for (int q = 0; q < 27; q++) {
@@ -515,9 +516,9 @@ __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double*
                                                     const double* __restrict__ Hpl, double lam_host, int use_dev,
                                                     const double* scal, double* Emat, double* cb, const int* run) {
     BA_GATE(run);
-    const int a = blockIdx.x * blockDim.x + threadIdx.x;
-    if (a >= s.nE || s.ePose[a] < 0) return;
-    const int l = s.eLand[a];
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;   // pose-list position
+    if (a >= s.nPe) return;
+    const int l = s.eLand[s.peList[a]];
     const double lambda = lam_of(lam_host, use_dev, scal);
     double Di[9], d[3];
     land_dinv(Hll, l, lambda, Di);
@@ -544,6 +545,7 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
                                               const double* scal, SysAddr S, double* bs, int own,
                                               const uint8_t* poseAdd, const int* run) {
     BA_GATE(run);
+    ORBGPU_PROF_START;
     __shared__ double cs[36][kChunks];
     const int blk = blockIdx.x;
     const int i1 = s.blkI[blk], i2 = s.blkJ[blk];
@@ -595,10 +597,14 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
             put(v, std::integral_constant<int, 36>{});
         }
     }
+    ORBGPU_PROF_MARK(11);   // (instrumented builds: block 0's wave 0 -- chunk terms and trees)
     __syncthreads();
+    ORBGPU_PROF_MARK(12);
+    ORBGPU_PROF_COUNT(15);
     if ((int)threadIdx.x >= nent) return;
     const int q = threadIdx.x;
     const double v = local_csum_inplace(cs[q], m);
+    ORBGPU_PROF_MARK(13);
     const double lambda = lam_of(lam_host, use_dev, scal);
     if (poseAdd) own = poseAdd[i1];   // sharded factorisation: the pose's owner adds its terms
     if (diag && q >= 21) {  // a shard that does not own the pose terms contributes -sum only
@@ -1498,14 +1504,40 @@ __global__ void __launch_bounds__(256) k_update(BaStructDev s, Se3* T, Se3* Tbak
     double* xl = x + 6 * nP + 3 * l;
     if (scal[3] != 0.0) {  // solver succeeded: xl = Dinv (b_l - sum_i B_i^T xp_i), blocks in pose order
         double cl[3] = {bl[3 * l], bl[3 * l + 1], bl[3 * l + 2]};
-        for (int j = s.lpStart[l]; j < s.lpStart[l + 1]; j++) {
-            const int a = s.lpList[j];
-            const double* B = Hpl + 18 * (size_t)a;
-            const double* cp = x + 6 * s.ePose[a];
-            for (int k = 0; k < 3; k++) {
-                double acc = 0;
-                for (int r = 0; r < 6; r++) acc += B[r * 3 + k] * (-cp[r]);
-                cl[k] += acc;
+        // the landmark's pose edges four at a time: their list entries, then their positions and
+        // poses, then their Hpl blocks and pose steps are loaded before any is used, so the chain
+        // of dependent loads is paid once per four edges; the sums keep the list order
+        const int j1 = s.lpStart[l + 1];
+        for (int j0 = s.lpStart[l]; j0 < j1; j0 += 4) {
+            int a[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) a[u] = j0 + u < j1 ? s.lpList[j0 + u] : -1;
+            int pp[4], pe[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                pp[u] = a[u] >= 0 ? s.pePos[a[u]] : 0;
+                pe[u] = a[u] >= 0 ? s.ePose[a[u]] : 0;
+            }
+            double Bv[4][18], cv[4][6];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const double* B = Hpl + 18 * (size_t)pp[u];
+                const double* cp = x + 6 * pe[u];
+#pragma unroll
+                for (int q = 0; q < 18; q++) Bv[u][q] = a[u] >= 0 ? B[q] : 0.0;
+#pragma unroll
+                for (int r = 0; r < 6; r++) cv[u][r] = a[u] >= 0 ? cp[r] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (a[u] < 0) break;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    double acc = 0;
+#pragma unroll
+                    for (int r = 0; r < 6; r++) acc += Bv[u][r * 3 + k] * (-cv[u][r]);
+                    cl[k] += acc;
+                }
             }
         }
         double Di[9];
@@ -3158,6 +3190,7 @@ int BaEngine::carve(bool commit, size_t* total) {
     dLm_ = (LmDev*)take(sizeof(LmDev));
     dKfFixed_ = (uint8_t*)take(nkf);
     dKfId_ = (int32_t*)take(sizeof(int32_t) * nkf);
+    dPePos_ = (int32_t*)take(sizeof(int32_t) * ne);
     dPtId_ = (int32_t*)take(sizeof(int32_t) * npt);
     dScratch_ = (double*)take(sizeof(double) * scratchN_);
     tmpA0_ = (double*)take(sizeof(double) * tmpN);
@@ -3301,6 +3334,19 @@ int debug_set_struct_gpu_min_edges(int v) {
     return 0;
 }
 
+// pose-list positions of a device-built structure: pePos[peList[j]] = j (pePos preset to -1), then
+// the Schur pair lists rewritten from edges to positions
+__global__ void __launch_bounds__(256) k_pe_pos(const int32_t* peList, int nPe, int32_t* pePos) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < nPe) pePos[peList[j]] = j;
+}
+__global__ void __launch_bounds__(256) k_pair_pos(int32_t* pairA, int32_t* pairB, int nPair, const int32_t* pePos) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nPair) return;
+    pairA[t] = pePos[pairA[t]];
+    pairB[t] = pePos[pairB[t]];
+}
+
 // initializeOptimization(level) + buildIndexMapping + BlockSolver::buildStructure
 int BaEngine::build_structure(int level) {
     using sclk = std::chrono::steady_clock;
@@ -3309,7 +3355,7 @@ int BaEngine::build_structure(int level) {
     auto lap = [&](const char* what) {   // ORBGPU_BA_TIMES: the structure build's phases
         if (!say) return;
         const auto t = sclk::now();
-        fprintf(stderr, "[ba]   structure %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - ts0).count());
+        fprintf(stderr, "[ba]   structure %s %.0f us\n", what, std::chrono::duration<double, std::micro>(t - ts0).count());
         ts0 = t;
     };
     int nE = 0, nP = 0, nL = 0, nBlk = 0;
@@ -3330,6 +3376,17 @@ int BaEngine::build_structure(int level) {
         nBlk = info.nBlk;
         nEglob_ = info.nEglob;
         nLglob_ = info.nLglob;
+        if (nE) {
+            ORB_HIP_CHECK(hipMemsetAsync(dPePos_, 0xff, sizeof(int32_t) * nE, stream_));
+            if (info.nPe)
+                hipLaunchKernelGGL(k_pe_pos, dim3((info.nPe + 255) / 256), dim3(256), 0, stream_, st_.peList, info.nPe, dPePos_);
+            if (info.nPair)
+                hipLaunchKernelGGL(k_pair_pos, dim3((info.nPair + 255) / 256), dim3(256), 0, stream_,
+                                   const_cast<int32_t*>(st_.pairA), const_cast<int32_t*>(st_.pairB), info.nPair, dPePos_);
+            ORB_HIP_CHECK(hipGetLastError());
+        }
+        st_.pePos = dPePos_;
+        st_.nPe = info.nPe;
         if (info.maxPe > 64 * kChunks || info.maxLe > 64 * 64 || info.maxBlk > 64 * kChunks) return -3;
         if (nE > kCsumLv * 64 * 64 || 6LL * nP + 3LL * nL > (long long)scratchN_) return -3;
         if (nP >= kTiledMinPoses && !comm_) {
@@ -3367,6 +3424,16 @@ int BaEngine::build_structure(int level) {
         nE = (int)H.aE.size();
         nP = (int)H.poseKf.size();
         nL = (int)H.landPt.size();
+        {   // pose-list positions; the Schur pairs rewritten from edges to positions
+            const int nPe = H.peStart[nP];
+            hPePos_.assign(std::max(nE, 1), -1);
+            for (int j = 0; j < nPe; j++) hPePos_[H.peList[j]] = j;
+            const int nPair = H.blkStart[H.blkI.size()];
+            for (int t = 0; t < nPair; t++) {
+                H.pairA[t] = hPePos_[H.pairA[t]];
+                H.pairB[t] = hPePos_[H.pairB[t]];
+            }
+        }
         if (!comm_) {
             nEglob_ = nE;
             nLglob_ = nL;
@@ -3386,7 +3453,7 @@ int BaEngine::build_structure(int level) {
         // pack and upload
         std::vector<const std::vector<int32_t>*> parts = {&aE,      &ePose,   &eLand,  &poseKf, &landPt, &peStart,
                                                           &peList,  &leStart, &leList, &lpStart, &lpList, &blkI,
-                                                          &blkJ,    &blkStart, &pairA, &pairB};
+                                                          &blkJ,    &blkStart, &pairA, &pairB, &hPePos_};
         size_t tot = 0;
         for (auto* p : parts) tot += (p->size() + 63) & ~(size_t)63;
         if (tot * 4 > dStructCap_) {
@@ -3425,6 +3492,7 @@ int BaEngine::build_structure(int level) {
         st_.landPt = d + off[4]; st_.peStart = d + off[5]; st_.peList = d + off[6]; st_.leStart = d + off[7];
         st_.leList = d + off[8]; st_.lpStart = d + off[9]; st_.lpList = d + off[10]; st_.blkI = d + off[11];
         st_.blkJ = d + off[12]; st_.blkStart = d + off[13]; st_.pairA = d + off[14]; st_.pairB = d + off[15];
+        st_.pePos = d + off[16]; st_.nPe = peStart[nP];
         if (nP >= kTiledMinPoses)
             for (int b = 0; b < nBlk; b++)
                 if (blkI[b] != blkJ[b]) offKeys.push_back((int64_t)blkI[b] * nP + blkJ[b]);
@@ -4008,8 +4076,8 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
         auto ms = [](clk::time_point a, clk::time_point b) {
             return std::chrono::duration<double, std::milli>(b - a).count();
         };
-        fprintf(stderr, "[ba] call %.1f ms: upload %.1f, structure %.1f, optimize %.1f (incl. the second pass's "
-                        "structure), readback %.1f\n", last_ms[0], ms(t0, t_up), t_struct, ms(t_opt0, t_opt1),
+        fprintf(stderr, "[ba] call %.3f ms: upload %.3f, structure %.3f, optimize %.3f (incl. the second pass's "
+                        "structure), readback %.3f\n", last_ms[0], ms(t0, t_up), t_struct, ms(t_opt0, t_opt1),
                 ms(t_opt1, clk::now()));
     }
     comm_ = nullptr;

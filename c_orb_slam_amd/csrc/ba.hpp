@@ -103,6 +103,8 @@ private:
     double *dTerms_ = nullptr, *dRc_ = nullptr, *dHpp_ = nullptr, *dBp_ = nullptr, *dHll_ = nullptr, *dBl_ = nullptr;
     double *dB_ = nullptr, *dX2_ = nullptr, *dS_ = nullptr, *dBs_ = nullptr, *dDinv_ = nullptr, *dDb_ = nullptr;
     double *dEmat_ = nullptr, *dCb_ = nullptr, *dScal_ = nullptr, *dScratch_ = nullptr, *dHplA_ = nullptr;
+    int32_t* dPePos_ = nullptr;   // device-built structures: active edge -> pose-list position
+    std::vector<int32_t> hPePos_;   // host-built structures: the same, packed with the lists
     double *tmpA0_ = nullptr, *tmpA1_ = nullptr, *tmpB0_ = nullptr, *tmpB1_ = nullptr;
     unsigned* dCounter_ = nullptr;
     SparseLdlt sp_;                // block-sparse pose system (n > the dense solvers' reach)

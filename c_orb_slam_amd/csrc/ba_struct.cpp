@@ -48,7 +48,7 @@ int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, con
     auto lap = [&](const char* what) {
         if (!say) return;
         const auto t = sclk::now();
-        fprintf(stderr, "[ba]     lists: %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - ts0).count());
+        fprintf(stderr, "[ba]     lists: %s %.1f us\n", what, std::chrono::duration<double, std::micro>(t - ts0).count());
         ts0 = t;
     };
     std::vector<uint8_t> freeKf(nkf);

@@ -31,8 +31,13 @@ struct BaStructDev {
     const int32_t* blkI;      // Schur blocks (i1 <= i2), diagonal blocks always present
     const int32_t* blkJ;
     const int32_t* blkStart;  // block -> pair terms (landmark order)
-    const int32_t* pairA;     // active edge of the landmark to pose i1
-    const int32_t* pairB;     // active edge of the landmark to pose i2
+    const int32_t* pairA;     // active edge of the landmark to pose i1 (BaEngine: its pose-list position)
+    const int32_t* pairB;     // active edge of the landmark to pose i2 (BaEngine: its pose-list position)
+    // BaEngine only: active edge -> its position in peList (-1: fixed pose), and nPe = peStart[nP].
+    // A free-pose edge's pose terms, Hpl, Emat and c_b live at that position, so every per-pose
+    // walk (the pose reduction, a Schur block's terms in landmark order) reads consecutive records.
+    const int32_t* pePos;
+    int nPe;
 };
 
 }  // namespace orbgpu

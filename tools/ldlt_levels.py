@@ -9,8 +9,11 @@ import sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 ld = [r for r in rows if "k_ldlt_" in r["Kernel_Name"] and "k_ldlt_reg" not in r["Kernel_Name"]]
 # a solve starts at the first update/factor after a backward run
-starts = [i for i in range(len(ld)) if "backward" not in ld[i]["Kernel_Name"] and
-          (i == 0 or "backward" in ld[i - 1]["Kernel_Name"])]
+def bwd(r):
+    return "backward" in r["Kernel_Name"] or "bwdn" in r["Kernel_Name"]
+
+
+starts = [i for i in range(len(ld)) if not bwd(ld[i]) and (i == 0 or bwd(ld[i - 1]))]
 seg = ld[starts[-1]:]
 t0 = int(seg[0]["Start_Timestamp"])
 tot = {}
