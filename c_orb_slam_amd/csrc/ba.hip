@@ -536,17 +536,22 @@ __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double*
 // (upper triangle of the diagonal blocks), and b_s = b_p - csum_l B db.
 // Each lane loads the two 6x3 blocks of one landmark term once and feeds all entries; a chunk's
 // 27 / 36 canonical 64-trees run packed (packed_trees: every value's tree is the canonical one).
-// NT = 256 for systems of many blocks (global BA: most blocks hold one or two chunks), 512 for
-// the few long blocks of a local BA.
+// NT = 64 for systems of many blocks (global BA: most blocks hold one or two chunks): one wave
+// per block walks its chunks, the chunk sums in dynamic LDS sized by the longest block (ldc
+// chunks), so a CU keeps four times the blocks in flight of a four-wave workgroup; 512 for the
+// few long blocks of a local BA (chunk sums in static LDS, ldc = kChunks).
 template <int NT>
 __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __restrict__ Emat,
                                               const double* __restrict__ Hpl, const double* __restrict__ cb,
                                               const double* Hpp, const double* bp, double lam_host, int use_dev,
                                               const double* scal, SysAddr S, double* bs, int own,
-                                              const uint8_t* poseAdd, const int* run) {
+                                              const uint8_t* poseAdd, const int* run, int ldcDyn) {
     BA_GATE(run);
     ORBGPU_PROF_START;
-    __shared__ double cs[36][kChunks];
+    __shared__ double csS[NT == 64 ? 1 : 36 * kChunks];
+    extern __shared__ double lds[];
+    double* cs = NT == 64 ? lds : csS;   // cs[q * ldc + c]: entry q's chunk c
+    const int ldc = NT == 64 ? ldcDyn : kChunks;
     const int blk = blockIdx.x;
     const int i1 = s.blkI[blk], i2 = s.blkJ[blk];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
@@ -554,10 +559,22 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
     const int m = (n + 63) >> 6;
     const bool diag = i1 == i2;
     const int nent = diag ? 27 : 36;
+    // the next chunk's pair entries are loaded one iteration ahead: a chunk's record loads then
+    // wait on one memory round trip, not two
+    int a1n = 0, a2n = 0;
+    if (w < m && w * 64 + lane < n) {
+        a1n = s.pairA[s0 + w * 64 + lane];
+        a2n = s.pairB[s0 + w * 64 + lane];
+    }
     for (int c = w; c < m; c += nw) {
         const int j = c * 64 + lane;
         const bool valid = j < n;
-        const int a1 = valid ? s.pairA[s0 + j] : 0, a2 = valid ? s.pairB[s0 + j] : 0;
+        const int a1 = valid ? a1n : 0, a2 = valid ? a2n : 0;
+        {
+            const int jn = j + 64 * nw;
+            a1n = jn < n ? s.pairA[s0 + jn] : 0;
+            a2n = jn < n ? s.pairB[s0 + jn] : 0;
+        }
         double E[18], B[18];
 #pragma unroll
         for (int q = 0; q < 18; q++) {
@@ -569,11 +586,11 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
             if (n == 1) {   // ora_csum keeps a single term untouched
                 if (lane == 0)
 #pragma unroll
-                    for (int q = 0; q < K; q++) cs[q][c] = v[q];
+                    for (int q = 0; q < K; q++) cs[q * ldc + c] = v[q];
             } else {
                 const double t = packed_trees<K>(v);
                 const int q = bitrev6(lane);
-                if (q < K) cs[q][c] = t;
+                if (q < K) cs[q * ldc + c] = t;
             }
         };
         if (diag) {
@@ -603,7 +620,7 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
     ORBGPU_PROF_COUNT(15);
     if ((int)threadIdx.x >= nent) return;
     const int q = threadIdx.x;
-    const double v = local_csum_inplace(cs[q], m);
+    const double v = local_csum_inplace(cs + q * ldc, m);
     ORBGPU_PROF_MARK(13);
     const double lambda = lam_of(lam_host, use_dev, scal);
     if (poseAdd) own = poseAdd[i1];   // sharded factorisation: the pose's owner adds its terms
@@ -628,10 +645,14 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
     *S.at(6 * i1 + r, 6 * i2 + c) = h - v;
 }
 
+// ldc: chunks of the longest block (the one-wave kernel's LDS rows)
 template <class... A>
-static void schur_launch(int nBlk, hipStream_t st, A... args) {
-    if (nBlk >= 256) hipLaunchKernelGGL(k_schur<256>, dim3(nBlk), dim3(256), 0, st, args...);
-    else hipLaunchKernelGGL(k_schur<512>, dim3(nBlk), dim3(512), 0, st, args...);
+static void schur_launch(int nBlk, int ldc, hipStream_t st, A... args) {
+    if (nBlk >= 256)
+        hipLaunchKernelGGL(k_schur<64>, dim3(nBlk), dim3(64), sizeof(double) * 36 * (size_t)std::max(ldc, 1), st, args...,
+                           std::max(ldc, 1));
+    else
+        hipLaunchKernelGGL(k_schur<512>, dim3(nBlk), dim3(512), 0, st, args..., kChunks);
 }
 
 // Dense LDL^T of the upper triangle + solve, one workgroup (256 threads).
@@ -3388,6 +3409,7 @@ int BaEngine::build_structure(int level) {
         st_.pePos = dPePos_;
         st_.nPe = info.nPe;
         if (info.maxPe > 64 * kChunks || info.maxLe > 64 * 64 || info.maxBlk > 64 * kChunks) return -3;
+        blkChunks_ = (info.maxBlk + 63) / 64;
         if (nE > kCsumLv * 64 * 64 || 6LL * nP + 3LL * nL > (long long)scratchN_) return -3;
         if (nP >= kTiledMinPoses && !comm_) {
             if (int e = gs_.offkeys(&offKeys, stream_)) return e;
@@ -3448,8 +3470,10 @@ int BaEngine::build_structure(int level) {
         for (int l = 0; l < nL; l++)
             if (leStart[l + 1] - leStart[l] > 64 * 64) return -3;
         if (nE > kCsumLv * 64 * 64 || 6LL * nP + 3LL * nL > (long long)scratchN_) return -3;
-        for (int b = 0; b < nBlk; b++)
-            if (blkStart[b + 1] - blkStart[b] > 64 * kChunks) return -3;
+        int maxBlk = 0;
+        for (int b = 0; b < nBlk; b++) maxBlk = std::max(maxBlk, blkStart[b + 1] - blkStart[b]);
+        if (maxBlk > 64 * kChunks) return -3;
+        blkChunks_ = (maxBlk + 63) / 64;
         // pack and upload
         std::vector<const std::vector<int32_t>*> parts = {&aE,      &ePose,   &eLand,  &poseKf, &landPt, &peStart,
                                                           &peList,  &leStart, &leList, &lpStart, &lpList, &blkI,
@@ -3726,7 +3750,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         } else if (comm_ && n) {
             ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * (size_t)n * n, s));
         }
-        if (S.nBlk) schur_launch(S.nBlk, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
+        if (S.nBlk) schur_launch(S.nBlk, blkChunks_, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_,
                                        lambda_, use_dev, dScal_, sa, dBs_, own ? 1 : 0,
                                        distOk_ ? sp_.pose_add() : (const uint8_t*)nullptr, (const int*)nullptr);
         if (comm_ && tiled_ && distOk_) {
@@ -3898,7 +3922,7 @@ void BaEngine::enqueue_lm_step(bool first) {
     const SysAddr sa{dS_, n, nullptr, nullptr, 0, nullptr};
     if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_, 0.0, 1,
                                dScal_, dEmat_, dCb_, ctl);
-    if (S.nBlk) schur_launch(S.nBlk, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_, 0.0,
+    if (S.nBlk) schur_launch(S.nBlk, blkChunks_, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_, 0.0,
                                    1, dScal_, sa, dBs_, 1, (const uint8_t*)nullptr, ctl);
     const DenseLdlt kind = dense_ldlt_kind(n, use_reg);
     if (kind == DenseLdlt::Col) hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);

@@ -105,6 +105,7 @@ private:
     double *dEmat_ = nullptr, *dCb_ = nullptr, *dScal_ = nullptr, *dScratch_ = nullptr, *dHplA_ = nullptr;
     int32_t* dPePos_ = nullptr;   // device-built structures: active edge -> pose-list position
     std::vector<int32_t> hPePos_;   // host-built structures: the same, packed with the lists
+    int blkChunks_ = 1;   // chunks (64 terms) of the structure's longest Schur block
     double *tmpA0_ = nullptr, *tmpA1_ = nullptr, *tmpB0_ = nullptr, *tmpB1_ = nullptr;
     unsigned* dCounter_ = nullptr;
     SparseLdlt sp_;                // block-sparse pose system (n > the dense solvers' reach)

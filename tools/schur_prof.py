@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Section timers of k_schur's block 0 (the first diagonal block) over local-BA calls, from an
-instrumented build: ORBGPU_LIB=build/liborbslam_gpu_prof.so python tools/schur_prof.py [calls]."""
+"""Section timers of k_schur's block 0 (the first diagonal block) over local-BA calls (or global-BA
+calls: second argument "gba"), from an instrumented build:
+ORBGPU_LIB=build/liborbslam_gpu_prof.so python tools/schur_prof.py [calls] [gba]."""
 import ctypes as C
 import sys
 from pathlib import Path
@@ -17,15 +18,22 @@ KEYS = ("kf_id", "kf_Tcw", "kf_local", "kf_cam", "pt_id", "pt_pos", "edge_pt", "
 
 
 def main():
-    from c_orb_slam_amd.optimizer import LocalBundleAdjustment
+    from c_orb_slam_amd.optimizer import LocalBundleAdjustment, BundleAdjustment
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    pr = ba_problem(0)
-    args = [pr[k] for k in KEYS]
-    LocalBundleAdjustment(*args)
+    gba = len(sys.argv) > 2 and sys.argv[2] == "gba"   # config 5 (2000 keyframes, 4 laps) instead
+    if gba:
+        from ba_cases import global_ba_problem
+        pr = global_ba_problem(0, n_kf=2000, pts_per_kf=150, laps=4)
+        run = lambda: BundleAdjustment(pr, 10, False)  # noqa: E731
+    else:
+        pr = ba_problem(0)
+        args = [pr[k] for k in KEYS]
+        run = lambda: LocalBundleAdjustment(*args)  # noqa: E731
+    run()
     out = (C.c_ulonglong * 32)()
     lib().orbgpu_debug_prof(out)
     for _ in range(reps):
-        LocalBundleAdjustment(*args)
+        run()
     lib().orbgpu_debug_prof(out)
     n = max(out[15], 1)
     print(f"k_schur block 0 over {out[15]} launches, cycles per launch: terms+trees (wave 0) {out[11] / n:.0f} | "
