@@ -18,6 +18,7 @@
 #include "ba.hpp"
 #include <atomic>
 
+#include <tuple>
 #include <type_traits>
 
 #include <functional>
@@ -536,9 +537,10 @@ __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double*
 // (upper triangle of the diagonal blocks), and b_s = b_p - csum_l B db.
 // Each lane loads the two 6x3 blocks of one landmark term once and feeds all entries; a chunk's
 // 27 / 36 canonical 64-trees run packed (packed_trees: every value's tree is the canonical one).
-// NT = 64 for systems of many blocks (global BA: most blocks hold one or two chunks): one wave
-// per block walks its chunks, the chunk sums in dynamic LDS sized by the longest block (ldc
-// chunks), so a CU keeps four times the blocks in flight of a four-wave workgroup; 512 for the
+// NT = 256 for systems of many blocks (global BA): a workgroup takes one diagonal block with its
+// four waves (the blocks of the poses' own edges, the longest), or four off-diagonal blocks, one
+// wave each (most hold one or two chunks: a wave per block keeps four times the blocks in
+// flight); the chunk sums in dynamic LDS sized by the longest block (ldc chunks).  512 for the
 // few long blocks of a local BA (chunk sums in static LDS, ldc = kChunks).
 template <int NT>
 __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __restrict__ Emat,
@@ -548,13 +550,19 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
                                               const uint8_t* poseAdd, const int* run, int ldcDyn) {
     BA_GATE(run);
     ORBGPU_PROF_START;
-    __shared__ double csS[NT == 64 ? 1 : 36 * kChunks];
+    constexpr bool kMixed = NT == 256;
+    __shared__ double csS[kMixed ? 1 : 36 * kChunks];
     extern __shared__ double lds[];
-    double* cs = NT == 64 ? lds : csS;   // cs[q * ldc + c]: entry q's chunk c
-    const int ldc = NT == 64 ? ldcDyn : kChunks;
-    const int blk = blockIdx.x;
+    const int ldc = kMixed ? ldcDyn : kChunks;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the block's waves: all of the workgroup (group) or this wave alone
+    const bool group = !kMixed || (int)blockIdx.x < s.nP;
+    const int blk = group ? (int)blockIdx.x : s.nP + ((int)blockIdx.x - s.nP) * 4 + wave;
+    if (blk >= s.nBlk) return;   // (wave-uniform: only a per-wave block can be past the end)
+    const int w = group ? wave : 0, nw = group ? (int)(blockDim.x >> 6) : 1;
+    const int tq = group ? (int)threadIdx.x : lane;   // the thread's index inside the block's waves
+    double* cs = !kMixed ? csS : (group ? lds : lds + (size_t)wave * 36 * ldc);   // cs[q * ldc + c]
     const int i1 = s.blkI[blk], i2 = s.blkJ[blk];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int s0 = s.blkStart[blk], n = s.blkStart[blk + 1] - s0;
     const int m = (n + 63) >> 6;
     const bool diag = i1 == i2;
@@ -615,11 +623,16 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
         }
     }
     ORBGPU_PROF_MARK(11);   // (instrumented builds: block 0's wave 0 -- chunk terms and trees)
-    __syncthreads();
+    if (group) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+    }
     ORBGPU_PROF_MARK(12);
     ORBGPU_PROF_COUNT(15);
-    if ((int)threadIdx.x >= nent) return;
-    const int q = threadIdx.x;
+    if (tq >= nent) return;
+    const int q = tq;
     const double v = local_csum_inplace(cs + q * ldc, m);
     ORBGPU_PROF_MARK(13);
     const double lambda = lam_of(lam_host, use_dev, scal);
@@ -648,9 +661,11 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
 // ldc: chunks of the longest block (the one-wave kernel's LDS rows)
 template <class... A>
 static void schur_launch(int nBlk, int ldc, hipStream_t st, A... args) {
-    if (nBlk >= 256)
-        hipLaunchKernelGGL(k_schur<64>, dim3(nBlk), dim3(64), sizeof(double) * 36 * (size_t)std::max(ldc, 1), st, args...,
-                           std::max(ldc, 1));
+    if (nBlk >= 256) {
+        const int nP = std::get<0>(std::make_tuple(args...)).nP;   // the leading diagonal blocks
+        hipLaunchKernelGGL(k_schur<256>, dim3(nP + (nBlk - nP + 3) / 4), dim3(256),
+                           sizeof(double) * 4 * 36 * (size_t)std::max(ldc, 1), st, args..., std::max(ldc, 1));
+    }
     else
         hipLaunchKernelGGL(k_schur<512>, dim3(nBlk), dim3(512), 0, st, args..., kChunks);
 }
@@ -3508,6 +3523,7 @@ int BaEngine::build_structure(int level) {
             }
         }, 1 << 14);
         ORB_HIP_CHECK(hipMemcpyAsync(dStruct_, hStage_, tot * 4, hipMemcpyHostToDevice, stream_));
+        lap("pack + upload");
         // the sharded and block-sparse set-ups below stage more uploads through the same block
         if (comm_ || nP >= kTiledMinPoses) ORB_HIP_CHECK(hipStreamSynchronize(stream_));
         const int32_t* d = dStruct_;
@@ -3612,6 +3628,7 @@ int BaEngine::build_structure(int level) {
     if (!tiled_) ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * 36 * (size_t)nP * nP + 8, stream_));
     // the staged structure copy must finish before the staging block is reused
     ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    lap("wait for the uploads");
     return 0;
 }
 
