@@ -3126,6 +3126,7 @@ BaEngine::~BaEngine() {
     for (auto ev : lmEv_)
         if (ev) (void)hipEventDestroy(ev);
     if (hStage_) (void)hipHostFree(hStage_);
+    if (hStage2_) (void)hipHostFree(hStage2_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -3140,6 +3141,20 @@ int BaEngine::stage_reserve(size_t bytes) {
     hStageCap_ = 0;
     ORB_HIP_CHECK(hipHostMalloc(&hStage_, bytes));
     hStageCap_ = bytes;
+    return 0;
+}
+
+int BaEngine::stage2_reserve(size_t bytes) {
+    if (stage2Pending_) {   // the previous structure's copy may still read the block
+        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        stage2Pending_ = false;
+    }
+    if (bytes <= hStage2Cap_) return 0;
+    if (hStage2_) (void)hipHostFree(hStage2_);
+    hStage2_ = nullptr;
+    hStage2Cap_ = 0;
+    ORB_HIP_CHECK(hipHostMalloc(&hStage2_, bytes));
+    hStage2Cap_ = bytes;
     return 0;
 }
 
@@ -3500,10 +3515,10 @@ int BaEngine::build_structure(int level) {
             ORB_HIP_CHECK(hipMalloc(&dStruct_, tot * 4 * 2));
             dStructCap_ = tot * 4 * 2;
         }
-        if (int e = stage_reserve(tot * 4)) return e;   // copied below, waited for at the end
+        if (int e = stage2_reserve(tot * 4)) return e;   // copied below, not waited for
         // the lists packed straight into the pinned staging block (64-entry aligned sections), the
         // copy split over host threads in 64-entry groups on large systems
-        int32_t* hs = reinterpret_cast<int32_t*>(hStage_);
+        int32_t* hs = reinterpret_cast<int32_t*>(hStage2_);
         std::vector<size_t> off;
         size_t o = 0;
         for (auto* p : parts) {
@@ -3522,7 +3537,8 @@ int BaEngine::build_structure(int level) {
                 if (z0 < x1) std::memset(hs + z0, 0, sizeof(int32_t) * (x1 - z0));
             }
         }, 1 << 14);
-        ORB_HIP_CHECK(hipMemcpyAsync(dStruct_, hStage_, tot * 4, hipMemcpyHostToDevice, stream_));
+        ORB_HIP_CHECK(hipMemcpyAsync(dStruct_, hStage2_, tot * 4, hipMemcpyHostToDevice, stream_));
+        stage2Pending_ = true;
         lap("pack + upload");
         // the sharded and block-sparse set-ups below stage more uploads through the same block
         if (comm_ || nP >= kTiledMinPoses) ORB_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -3626,9 +3642,9 @@ int BaEngine::build_structure(int level) {
     }
     ORB_HIP_CHECK(hipMemsetAsync(dX2_, 0, sizeof(double) * (6 * (size_t)nP + 3 * (size_t)nL + 1), stream_));
     if (!tiled_) ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * 36 * (size_t)nP * nP + 8, stream_));
-    // the staged structure copy must finish before the staging block is reused
-    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
-    lap("wait for the uploads");
+    // (the structure's copy reads its own staging block, whose next user waits for it; kernels
+    // queued after this are stream-ordered behind every copy and memset above)
+    lap("queued");
     return 0;
 }
 

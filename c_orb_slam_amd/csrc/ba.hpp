@@ -122,6 +122,12 @@ private:
     void* hStage_ = nullptr;
     size_t hStageCap_ = 0;
     bool uploadPending_ = false;   // upload_problem's copies may still read hStage_
+    // the structure lists' own staging block: packed while the problem upload still reads hStage_,
+    // its copy not waited for (the next structure's pack waits if it is still pending)
+    void* hStage2_ = nullptr;
+    size_t hStage2Cap_ = 0;
+    bool stage2Pending_ = false;
+    int stage2_reserve(size_t bytes);
     int h2d_sync(void* dst, const void* src, size_t bytes);
     int d2h_sync(void* dst, const void* src, size_t bytes);
     int stage_reserve(size_t bytes);

@@ -30,13 +30,46 @@ void ba_active_set(int level, int nkf, int npt, int ne, const int32_t* eKf, cons
         }
 }
 
-// indices i with flag[i] set, ascending by id[i] (ids are distinct)
+// indices i with flag[i] set, ascending by id[i] (ids are distinct): an LSD radix sort of 64-bit
+// keys (the id, sign-flipped so unsigned order is signed order, above the index), three 11-bit
+// passes over the id -- a landmark set of thousands sorts in O(n) instead of a comparison sort's
+// n log n indirect compares
 static void by_id(int n, const uint8_t* flag, const int32_t* id, std::vector<int32_t>* out) {
     out->clear();
+    thread_local std::vector<uint64_t> keys, tmp;
+    keys.clear();
+    bool sorted = true;
+    int32_t last = 0;
     for (int i = 0; i < n; i++)
-        if (flag[i]) out->push_back(i);
-    auto less = [&](int a, int b) { return id[a] < id[b]; };
-    if (!std::is_sorted(out->begin(), out->end(), less)) std::sort(out->begin(), out->end(), less);
+        if (flag[i]) {
+            if (!keys.empty() && id[i] <= last) sorted = false;
+            last = id[i];
+            keys.push_back(((uint64_t)((uint32_t)id[i] ^ 0x80000000u) << 32) | (uint32_t)i);
+        }
+    const size_t m = keys.size();
+    if (!sorted) {
+        if (m < 64) {
+            std::sort(keys.begin(), keys.end());
+        } else {
+            tmp.resize(m);
+            uint32_t cnt[2048];
+            for (int pass = 0; pass < 3; pass++) {
+                const int sh = 32 + 11 * pass;
+                std::fill(cnt, cnt + 2048, 0u);
+                for (size_t k = 0; k < m; k++) cnt[(keys[k] >> sh) & 2047]++;
+                uint32_t acc = 0;
+                for (int b = 0; b < 2048; b++) {
+                    const uint32_t c = cnt[b];
+                    cnt[b] = acc;
+                    acc += c;
+                }
+                for (size_t k = 0; k < m; k++) tmp[cnt[(keys[k] >> sh) & 2047]++] = keys[k];
+                keys.swap(tmp);
+            }
+        }
+    }
+    out->resize(m);
+    for (size_t k = 0; k < m; k++) (*out)[k] = (int32_t)(keys[k] & 0xffffffffu);
 }
 
 int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, const uint8_t* kfFixed,
