@@ -158,6 +158,18 @@ struct LinArgs {
     unsigned* counter;
     double* out;      // canonical sum of rc
     const int* run;   // gate (device LM) or nullptr
+    // the device LM's trial pass with the update fused in (fuse = 1): blocks [0, edgeBlocks) take
+    // the edges at the trial's poses and points, computed from x on the fly with k_update's
+    // operations; the blocks after them write the trial's poses / points to Tn / Xn (committed
+    // by k_lm_trial_end on acceptance) and the landmarks' steps into x
+    int fuse = 0;
+    int edgeBlocks = 0;
+    double* x = nullptr;
+    const double* Hll = nullptr;
+    const double* bl = nullptr;
+    const double* scal = nullptr;
+    Se3* Tn = nullptr;
+    double* Xn = nullptr;
 };
 
 // computeActiveErrors + activeRobustChi2 terms (+ linearizeOplus + constructQuadraticForm)
@@ -190,10 +202,110 @@ __device__ __forceinline__ void block_finish_csum(double* c, int m, int nterms, 
 // The chi2 total of k_linearize's chunk trees, one workgroup.  A launch of its own: the kernel
 // boundary orders the chunk stores for this reader, where the former last-block-finishes
 // pattern needed a device-scope fence in every wave (an L2 writeback + invalidate on gfx950).
+// Eigen 3x3 inverse (compute_inverse_size3)
+__device__ __forceinline__ void inv3(const double* m, double* r) {
+#define M(i, j) m[(i) * 3 + (j)]
+#define COF(i, j) (M(((i) + 1) % 3, ((j) + 1) % 3) * M(((i) + 2) % 3, ((j) + 2) % 3) - \
+                   M(((i) + 1) % 3, ((j) + 2) % 3) * M(((i) + 2) % 3, ((j) + 1) % 3))
+    const double c0 = COF(0, 0), c1 = COF(1, 0), c2 = COF(2, 0);
+    const double det = (c0 * M(0, 0) + c1 * M(1, 0)) + c2 * M(2, 0);
+    const double invdet = 1.0 / det;
+    r[0] = c0 * invdet; r[1] = c1 * invdet; r[2] = c2 * invdet;
+    r[3] = COF(0, 1) * invdet; r[4] = COF(1, 1) * invdet; r[5] = COF(2, 1) * invdet;
+    r[6] = COF(0, 2) * invdet; r[7] = COF(1, 2) * invdet; r[8] = COF(2, 2) * invdet;
+#undef COF
+#undef M
+}
+
+// Dinv = (Hll + lambda I)^-1 of landmark l (setLambda + D->inverse(), block_solver.hpp:383-389)
+__device__ __forceinline__ void land_dinv(const double* Hll, int l, double lambda, double* Di) {
+    double D[9];
+    for (int q = 0; q < 9; q++) D[q] = Hll[9 * l + q];
+    for (int j = 0; j < 3; j++) D[4 * j] += lambda;
+    inv3(D, Di);
+}
+
+// k_update's operations, shared with the fused trial pass (k_linearize, fuse = 1) so the two give
+// the same values: the pose step T <- exp(x_p) T, and the landmark step xl = Dinv (b_l - sum_i
+// B_i^T xp_i) over the landmark's pose edges in pose order (x's own entries when the solve failed)
+__device__ __forceinline__ Se3 pose_step(const Se3& t0, const double* xp) {
+    double upd[6];
+    for (int k = 0; k < 6; k++) upd[k] = xp[k];
+    Se3 d, r;
+    se3_exp(upd, d);
+    se3_mul(d, t0, r);
+    return r;
+}
+__device__ __forceinline__ void land_step(const BaStructDev& s, int l, const double* __restrict__ Hpl, const double* Hll,
+                                          const double* bl, const double* x, double lambda, bool solved, double* xl) {
+    if (!solved) {
+        for (int k = 0; k < 3; k++) xl[k] = x[6 * s.nP + 3 * l + k];
+        return;
+    }
+    double cl[3] = {bl[3 * l], bl[3 * l + 1], bl[3 * l + 2]};
+    // the landmark's pose edges four at a time: their list entries, then their positions and
+    // poses, then their Hpl blocks and pose steps are loaded before any is used, so the chain of
+    // dependent loads is paid once per four edges; the sums keep the list order
+    const int j1 = s.lpStart[l + 1];
+    for (int j0 = s.lpStart[l]; j0 < j1; j0 += 4) {
+        int a[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) a[u] = j0 + u < j1 ? s.lpList[j0 + u] : -1;
+        int pp[4], pe[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            pp[u] = a[u] >= 0 ? s.pePos[a[u]] : 0;
+            pe[u] = a[u] >= 0 ? s.ePose[a[u]] : 0;
+        }
+        double Bv[4][18], cv[4][6];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const double* B = Hpl + 18 * (size_t)pp[u];
+            const double* cp = x + 6 * pe[u];
+#pragma unroll
+            for (int q = 0; q < 18; q++) Bv[u][q] = a[u] >= 0 ? B[q] : 0.0;
+#pragma unroll
+            for (int r = 0; r < 6; r++) cv[u][r] = a[u] >= 0 ? cp[r] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (a[u] < 0) break;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                double acc = 0;
+#pragma unroll
+                for (int r = 0; r < 6; r++) acc += Bv[u][r * 3 + k] * (-cv[u][r]);
+                cl[k] += acc;
+            }
+        }
+    }
+    double Di[9];
+    land_dinv(Hll, l, lambda, Di);
+    for (int r = 0; r < 3; r++) xl[r] = (Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1]) + Di[r * 3 + 2] * cl[2];
+}
+
 __global__ void __launch_bounds__(256) k_chi2_finish(LinArgs a);
 
-__global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
+template <bool FUSE>
+__global__ void __launch_bounds__(256) k_linearize_t(LinArgs a) {
     BA_GATE(a.run);
+    if (FUSE && (int)blockIdx.x >= a.edgeBlocks) {   // owners: the trial's poses and points
+        const int g = ((int)blockIdx.x - a.edgeBlocks) * (int)blockDim.x + (int)threadIdx.x;
+        const int nP = a.s.nP;
+        if (g < nP) {
+            a.Tn[g] = pose_step(a.T[a.s.poseKf[g]], a.x + 6 * g);
+        } else if (g - nP < a.s.nL) {
+            const int l = g - nP, pt = a.s.landPt[l];
+            const bool solved = a.scal[3] != 0.0;
+            double xl[3];
+            land_step(a.s, l, a.Hpl, a.Hll, a.bl, a.x, a.scal[5], solved, xl);
+            for (int k = 0; k < 3; k++) {
+                if (solved) a.x[6 * nP + 3 * l + k] = xl[k];
+                a.Xn[3 * l + k] = a.X[3 * pt + k] + xl[k];
+            }
+        }
+        return;
+    }
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = i < a.s.nE;
     double r0 = 0.0, rho1 = 1.0;
@@ -205,8 +317,16 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
     if (valid) {
         const int ei = a.s.aE[i];
         e = a.E[ei];
-        T = a.T[e.kf];
-        X[0] = a.X[3 * e.pt]; X[1] = a.X[3 * e.pt + 1]; X[2] = a.X[3 * e.pt + 2];
+        if (FUSE) {   // the trial's pose and point of this edge (what the owners write)
+            const int g = a.s.ePose[i];
+            T = g >= 0 ? pose_step(a.T[e.kf], a.x + 6 * g) : a.T[e.kf];
+            double xl[3];
+            land_step(a.s, a.s.eLand[i], a.Hpl, a.Hll, a.bl, a.x, a.scal[5], a.scal[3] != 0.0, xl);
+            for (int k = 0; k < 3; k++) X[k] = a.X[3 * e.pt + k] + xl[k];
+        } else {
+            T = a.T[e.kf];
+            X[0] = a.X[3 * e.pt]; X[1] = a.X[3 * e.pt + 1]; X[2] = a.X[3 * e.pt + 2];
+        }
         edge_error(e, T, X, err);
         for (int k = 0; k < 3; k++) a.err[3 * ei + k] = err[k];
         const double chi = edge_chi2(e, err);
@@ -334,6 +454,11 @@ __global__ void __launch_bounds__(256) k_linearize(LinArgs a) {
     }
     }
 }
+
+// the plain pass (system linearisation, host-driven trials) and the device LM's trial pass with
+// the update fused in: two instances, so the plain pass keeps its registers (88 VGPRs, not 256)
+static constexpr auto k_linearize = k_linearize_t<false>;
+static constexpr auto k_linearize_upd = k_linearize_t<true>;
 
 __global__ void __launch_bounds__(256) k_chi2_finish(LinArgs a) {
     BA_GATE(a.run);
@@ -487,29 +612,6 @@ __global__ void __launch_bounds__(1024) k_lambda_init(int nP, int nL, const doub
 
 __device__ __forceinline__ double lam_of(double lam_host, int use_dev, const double* scal) {
     return use_dev ? scal[5] : lam_host;
-}
-
-// Eigen 3x3 inverse (compute_inverse_size3)
-__device__ __forceinline__ void inv3(const double* m, double* r) {
-#define M(i, j) m[(i) * 3 + (j)]
-#define COF(i, j) (M(((i) + 1) % 3, ((j) + 1) % 3) * M(((i) + 2) % 3, ((j) + 2) % 3) - \
-                   M(((i) + 1) % 3, ((j) + 2) % 3) * M(((i) + 2) % 3, ((j) + 1) % 3))
-    const double c0 = COF(0, 0), c1 = COF(1, 0), c2 = COF(2, 0);
-    const double det = (c0 * M(0, 0) + c1 * M(1, 0)) + c2 * M(2, 0);
-    const double invdet = 1.0 / det;
-    r[0] = c0 * invdet; r[1] = c1 * invdet; r[2] = c2 * invdet;
-    r[3] = COF(0, 1) * invdet; r[4] = COF(1, 1) * invdet; r[5] = COF(2, 1) * invdet;
-    r[6] = COF(0, 2) * invdet; r[7] = COF(1, 2) * invdet; r[8] = COF(2, 2) * invdet;
-#undef COF
-#undef M
-}
-
-// Dinv = (Hll + lambda I)^-1 of landmark l (setLambda + D->inverse(), block_solver.hpp:383-389)
-__device__ __forceinline__ void land_dinv(const double* Hll, int l, double lambda, double* Di) {
-    double D[9];
-    for (int q = 0; q < 9; q++) D[q] = Hll[9 * l + q];
-    for (int j = 0; j < 3; j++) D[4 * j] += lambda;
-    inv3(D, Di);
 }
 
 // per active edge with a free pose: BDinv = Hpl Dinv and B (Dinv b_l)  (block_solver.hpp:376-404)
@@ -1526,61 +1628,17 @@ __global__ void __launch_bounds__(256) k_update(BaStructDev s, Se3* T, Se3* Tbak
         const int kf = s.poseKf[g];
         const Se3 t0 = T[kf];
         Tbak[kf] = t0;
-        double upd[6];
-        for (int k = 0; k < 6; k++) upd[k] = x[6 * g + k];
-        Se3 d, r;
-        se3_exp(upd, d);
-        se3_mul(d, t0, r);
-        T[kf] = r;
+        T[kf] = pose_step(t0, x + 6 * g);
         return;
     }
     const int l = g - nP;
     if (l >= s.nL) return;
     const int pt = s.landPt[l];
-    double* xl = x + 6 * nP + 3 * l;
-    if (scal[3] != 0.0) {  // solver succeeded: xl = Dinv (b_l - sum_i B_i^T xp_i), blocks in pose order
-        double cl[3] = {bl[3 * l], bl[3 * l + 1], bl[3 * l + 2]};
-        // the landmark's pose edges four at a time: their list entries, then their positions and
-        // poses, then their Hpl blocks and pose steps are loaded before any is used, so the chain
-        // of dependent loads is paid once per four edges; the sums keep the list order
-        const int j1 = s.lpStart[l + 1];
-        for (int j0 = s.lpStart[l]; j0 < j1; j0 += 4) {
-            int a[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) a[u] = j0 + u < j1 ? s.lpList[j0 + u] : -1;
-            int pp[4], pe[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                pp[u] = a[u] >= 0 ? s.pePos[a[u]] : 0;
-                pe[u] = a[u] >= 0 ? s.ePose[a[u]] : 0;
-            }
-            double Bv[4][18], cv[4][6];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const double* B = Hpl + 18 * (size_t)pp[u];
-                const double* cp = x + 6 * pe[u];
-#pragma unroll
-                for (int q = 0; q < 18; q++) Bv[u][q] = a[u] >= 0 ? B[q] : 0.0;
-#pragma unroll
-                for (int r = 0; r < 6; r++) cv[u][r] = a[u] >= 0 ? cp[r] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (a[u] < 0) break;
-#pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    double acc = 0;
-#pragma unroll
-                    for (int r = 0; r < 6; r++) acc += Bv[u][r * 3 + k] * (-cv[u][r]);
-                    cl[k] += acc;
-                }
-            }
-        }
-        double Di[9];
-        land_dinv(Hll, l, lam_of(lam_host, use_dev, scal), Di);
-        for (int r = 0; r < 3; r++) xl[r] = (Di[r * 3] * cl[0] + Di[r * 3 + 1] * cl[1]) + Di[r * 3 + 2] * cl[2];
-    }
+    const bool solved = scal[3] != 0.0;
+    double xl[3];
+    land_step(s, l, Hpl, Hll, bl, x, lam_of(lam_host, use_dev, scal), solved, xl);
     for (int k = 0; k < 3; k++) {
+        if (solved) x[6 * nP + 3 * l + k] = xl[k];
         const double v = X[3 * pt + k];
         Xbak[3 * pt + k] = v;
         X[3 * pt + k] = v + xl[k];
@@ -1837,7 +1895,7 @@ struct ChiFuse {
 __global__ void __launch_bounds__(1024) k_lm_trial_end(LmDev* L, double* scal, volatile int* host, BaStructDev s,
                                                        Se3* T, const Se3* Tbak, double* X, const double* Xbak,
                                                        const double* x, const double* bp, const double* bl, int scale,
-                                                       ChiFuse cf) {
+                                                       ChiFuse cf, const Se3* Tn, const double* Xn) {
     __shared__ double lv[2048];
     __shared__ double cA[kChiFuseMax], cB[kChiFuseMax];
     __shared__ double chi[2];
@@ -1887,6 +1945,18 @@ __global__ void __launch_bounds__(1024) k_lm_trial_end(LmDev* L, double* scal, v
     __syncthreads();
     if (threadIdx.x == 0) pop = lm_decide(L, scal, host, fuse ? chi : nullptr);
     __syncthreads();
+    if (Tn) {   // the update was fused into the trial pass: an accepted trial commits its poses / points
+        if (pop) return;
+        for (int g = threadIdx.x; g < nP + nL; g += blockDim.x) {
+            if (g < nP) {
+                T[s.poseKf[g]] = Tn[g];
+            } else {
+                const int l = g - nP, pt = s.landPt[l];
+                for (int k = 0; k < 3; k++) X[3 * pt + k] = Xn[3 * l + k];
+            }
+        }
+        return;
+    }
     if (!pop) return;
     for (int g = threadIdx.x; g < nP + nL; g += blockDim.x) {   // k_pop
         if (g < nP) {
@@ -3242,6 +3312,8 @@ int BaEngine::carve(bool commit, size_t* total) {
     dKfFixed_ = (uint8_t*)take(nkf);
     dKfId_ = (int32_t*)take(sizeof(int32_t) * nkf);
     dPePos_ = (int32_t*)take(sizeof(int32_t) * ne);
+    dTn_ = (Se3*)take(sizeof(Se3) * nkf);
+    dXn_ = (double*)take(sizeof(double) * 3 * npt);
     dPtId_ = (int32_t*)take(sizeof(int32_t) * npt);
     dScratch_ = (double*)take(sizeof(double) * scratchN_);
     tmpA0_ = (double*)take(sizeof(double) * tmpN);
@@ -3964,15 +4036,29 @@ void BaEngine::enqueue_lm_step(bool first) {
     else if (kind == DenseLdlt::Row) hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else if (kind == DenseLdlt::Reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(kLdltThreads), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
     else hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, ctl);
-    if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_, dXbak_,
-                                    dX2_, dHplA_, dHll_, dBl_, 0.0, 1, dScal_, ctl);
     la.linearize = 0;
     la.out = dScal_ + 1;
     la.run = ctl;
-    if (fuse) la.chunks = tmpB1_;
-    if (nE) {
-        hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
-        if (!fuse) hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+    if (fuse) {
+        // the update inside the trial pass: edges at the trial's poses and points, the owners'
+        // values to dTn_ / dXn_ (committed by k_lm_trial_end when the trial is accepted)
+        la.chunks = tmpB1_;
+        la.fuse = 1;
+        la.edgeBlocks = nblk(nE, 256);
+        la.x = dX2_;
+        la.Hll = dHll_;
+        la.bl = dBl_;
+        la.scal = dScal_;
+        la.Tn = dTn_;
+        la.Xn = dXn_;
+        hipLaunchKernelGGL(k_linearize_upd, dim3(la.edgeBlocks + nblk(nP + nL, 256)), dim3(256), 0, s, la);
+    } else {
+        if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_, dXbak_,
+                                        dX2_, dHplA_, dHll_, dBl_, 0.0, 1, dScal_, ctl);
+        if (nE) {
+            hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+            hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+        }
     }
     const bool small = scale_small(nP, nL);
     if (!small) {
@@ -3984,7 +4070,8 @@ void BaEngine::enqueue_lm_step(bool first) {
     }
     hipLaunchKernelGGL(k_lm_trial_end, dim3(1), dim3(1024), 0, s, dLm_, dScal_, (volatile int*)hLm_, S, dT_, dTbak_,
                        dX_, dXbak_, dX2_, dBp_, dBl_, small ? 1 : 0,
-                       fuse ? ChiFuse{tmpB0_, tmpB1_, nE} : ChiFuse{nullptr, nullptr, 0});
+                       fuse ? ChiFuse{tmpB0_, tmpB1_, nE} : ChiFuse{nullptr, nullptr, 0}, fuse ? dTn_ : nullptr,
+                       fuse ? dXn_ : nullptr);
 }
 
 int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* its) {
@@ -4047,7 +4134,9 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     trace_ = BaTrace{};
-    comm_ = comm;
+    // a one-rank group is the unsharded call: every exchange would be the identity, so none is
+    // made (no collective, no host round trip per structure and stop decision)
+    comm_ = comm && comm->size() > 1 ? comm : nullptr;
     mode_ = mode ? *mode : BaMode{};
     stopRed_ = false;
     std::memcpy(R->kf_Tcw, P->kf_Tcw, sizeof(float) * 16 * P->n_kf);

@@ -104,6 +104,8 @@ private:
     double *dB_ = nullptr, *dX2_ = nullptr, *dS_ = nullptr, *dBs_ = nullptr, *dDinv_ = nullptr, *dDb_ = nullptr;
     double *dEmat_ = nullptr, *dCb_ = nullptr, *dScal_ = nullptr, *dScratch_ = nullptr, *dHplA_ = nullptr;
     int32_t* dPePos_ = nullptr;   // device-built structures: active edge -> pose-list position
+    Se3* dTn_ = nullptr;          // the device LM's trial poses / points (fused update), committed on acceptance
+    double* dXn_ = nullptr;
     std::vector<int32_t> hPePos_;   // host-built structures: the same, packed with the lists
     int blkChunks_ = 1;   // chunks (64 terms) of the structure's longest Schur block
     double *tmpA0_ = nullptr, *tmpA1_ = nullptr, *tmpB0_ = nullptr, *tmpB1_ = nullptr;
