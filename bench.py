@@ -574,9 +574,11 @@ def main():
         nrm = torch.zeros((nf, cap, 3), dtype=torch.float32, device=dev)
         skip = torch.ones(K_LOCAL * cap, dtype=torch.uint8, device=dev)
         cur_mp = torch.full((cap,), -1, dtype=torch.int32, device=dev)
-        Tpred = torch.zeros(16, dtype=torch.float32, device=dev)
-        Tlast = torch.zeros(16, dtype=torch.float32, device=dev)
-        Twc_l = torch.zeros(16, dtype=torch.float32, device=dev)
+        # the frame's three 4x4 poses (motion-model prediction, last Tcw, last Twc) travel in ONE
+        # pinned H2D copy, as a C++ caller would pass them, not three pageable copies
+        Tdev = torch.zeros(48, dtype=torch.float32, device=dev)
+        Thost = torch.zeros(48, dtype=torch.float32).pin_memory()
+        Tpred, Tlast, Twc_l = Tdev[0:16], Tdev[16:32], Tdev[32:48]
         T1, T2 = (torch.zeros(16, dtype=torch.float32, device=dev) for _ in range(2))
         o1, o2 = (torch.zeros(cap, dtype=torch.uint8, device=dev) for _ in range(2))
         isig = lanes[0].isig_tab
@@ -625,10 +627,12 @@ def main():
                 nlast = int(last_n[0])
                 q = max(0, t - K_LOCAL)
                 nloc = (t - q) * cap
+                hv = Thost.numpy()
+                hv[0:16] = Tp.reshape(16)
+                hv[16:32] = Tcw[t - 1].reshape(16)
+                hv[32:48] = np.linalg.inv(Tcw[t - 1]).astype(np.float32).reshape(16)
                 with torch.cuda.stream(match_stream):   # ordered before the matcher's launches
-                    Tpred.copy_(torch.from_numpy(Tp.reshape(16)))
-                    Tlast.copy_(torch.from_numpy(Tcw[t - 1].reshape(16)))
-                    Twc_l.copy_(torch.from_numpy(np.linalg.inv(Tcw[t - 1]).astype(np.float32).reshape(16)))
+                    Tdev.copy_(Thost, non_blocking=True)
                     cur_mp.fill_(-1)
                 u = orb_newpoints(nlast, k[t - 1].data_ptr(), dep[t - 1].data_ptr(), Twc_l.data_ptr(), float(fx),
                                   float(fy), float(cx), float(cy), scale.data_ptr(), 8, (t - 1 - q) * cap,
