@@ -632,7 +632,11 @@ def main():
                 hv[16:32] = Tcw[t - 1].reshape(16)
                 hv[32:48] = np.linalg.inv(Tcw[t - 1]).astype(np.float32).reshape(16)
                 with torch.cuda.stream(match_stream):   # ordered before the matcher's launches
-                    Tdev.copy_(Thost, non_blocking=True)
+                    if os.environ.get("BENCH_LAT_POSE_PAGEABLE") == "1":   # (A/B: the three pageable copies)
+                        for q3 in range(3):
+                            Tdev[16 * q3:16 * q3 + 16].copy_(torch.from_numpy(hv[16 * q3:16 * q3 + 16].copy()))
+                    else:
+                        Tdev.copy_(Thost, non_blocking=True)
                     cur_mp.fill_(-1)
                 u = orb_newpoints(nlast, k[t - 1].data_ptr(), dep[t - 1].data_ptr(), Twc_l.data_ptr(), float(fx),
                                   float(fy), float(cx), float(cy), scale.data_ptr(), 8, (t - 1 - q) * cap,

@@ -277,6 +277,19 @@ __device__ __forceinline__ double wave_csum(F f, int n, double* sc) {
 // for off = 32..1 -- the same pairing as wave_tree, evaluated in one thread.
 template <class G>
 __device__ __forceinline__ double tree64_local(G get, int cnt) {
+    if (cnt <= 8) {
+        // the same tree for at most 8 values: levels off = 32, 16, 8 only add +0 (x + 0 + 0 + 0 ==
+        // x + 0, the sign of a zero included), so the leaves are w[i] = get(i) + 0 (i < cnt) or
+        // +0, then offsets 4, 2, 1 -- 8 reads instead of 64 predicated ones
+        double w[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) w[i] = i < cnt ? get(i) + 0.0 : 0.0;
+#pragma unroll
+        for (int off = 4; off >= 1; off >>= 1)
+#pragma unroll
+            for (int i = 0; i < off; i++) w[i] = w[i] + w[i + off];
+        return w[0];
+    }
     double a[32];
 #pragma unroll
     for (int i = 0; i < 32; i++) a[i] = (i < cnt ? get(i) : 0.0) + (i + 32 < cnt ? get(i + 32) : 0.0);

@@ -35,9 +35,24 @@ int validate(const ba_problem* P, const ba_result* R) {
         return ORB_E_INVALID;
     // distinct ids (sorted copies) and one edge per (map point, keyframe): the edges bucketed by
     // point, a keyframe stamp per bucket -- O(edges), no hashing (validation runs on every call)
+    // (ids sorted by an LSD radix sort of the sign-flipped keys, three 11-bit passes: O(n))
     auto distinct = [](const int32_t* v, int n) {
-        std::vector<int32_t> c(v, v + n);
-        std::sort(c.begin(), c.end());
+        if (n < 2) return true;
+        std::vector<uint32_t> c(n), t(n);
+        for (int i = 0; i < n; i++) c[i] = (uint32_t)v[i] ^ 0x80000000u;
+        uint32_t cnt[2048];
+        for (int sh = 0; sh < 32; sh += 11) {
+            std::fill(cnt, cnt + 2048, 0u);
+            for (int i = 0; i < n; i++) cnt[(c[i] >> sh) & 2047]++;
+            uint32_t acc = 0;
+            for (int b = 0; b < 2048; b++) {
+                const uint32_t k = cnt[b];
+                cnt[b] = acc;
+                acc += k;
+            }
+            for (int i = 0; i < n; i++) t[cnt[(c[i] >> sh) & 2047]++] = c[i];
+            c.swap(t);
+        }
         return std::adjacent_find(c.begin(), c.end()) == c.end();
     };
     if (!distinct(P->kf_id, P->n_kf) || !distinct(P->pt_id, P->n_pt)) return ORB_E_INVALID;
