@@ -1499,14 +1499,13 @@ __device__ __forceinline__ void ldlt_rows(double (&R)[2][kRowSlots], const doubl
 
 // Register-resident LDL^T + solve for n < 128 (<= 21 free keyframes), 512 threads, with a
 // one-panel lookahead: waves 0-1 factorise 6-column panels (one thread per column j), waves 2-7
-// hold the rows.  Phase p: the factor waves take panel p's rows (published by the row waves in
-// phase p - 1, updated by every panel up to p - 2), apply panel p - 1's updates to them
-// themselves, and factorise panel p (ldlt_panel6); meanwhile the row waves apply panel p - 1 to
-// the rows below panel p and publish panel p + 1's rows -- the trailing update runs under the
-// factorisation.  One barrier per phase (the factor waves also meet once between their update
-// and the factorisation: a panel's diagonal block spans both waves' columns).  Panel rows rotate
-// through three buffers, panel L through two.  Per-element operation sequence identical to
-// oracle ora_ldlt_solve (every element receives the pivots' updates in ascending k).
+// hold the rows.  Phase p: the factor waves factorise panel p from its rows in LDS (every earlier
+// panel's updates applied) and signal; the row waves apply panel p - 1 to their rows below panel
+// p (the trailing update runs under the factorisation), publish panel p + 1's rows to LDS and,
+// once panel p is factored, apply panel p to those rows there (one row per wave, no register
+// indexing).  One barrier per phase; panel rows rotate through three buffers, panel L through
+// two.  Per-element operation sequence identical to oracle ora_ldlt_solve (every element receives
+// the pivots' updates in ascending k).
 __global__ void __launch_bounds__(kLdltThreads) k_ldlt_reg(int n, const double* __restrict__ Sg, const double* bs,
                                                            double* x, double* scal, const int* run) {
     BA_GATE(run);
@@ -1516,7 +1515,7 @@ __global__ void __launch_bounds__(kLdltThreads) k_ldlt_reg(int n, const double* 
     double* Lb = Ub + 18 * kLdltMax;                  // 2 x (kLdltMax x 6) panel L
     double* dvec = Lb + 12 * kLdltMax;                // n
     double* y = dvec + kLdltMax;                      // n
-    __shared__ int ok, meet;
+    __shared__ int ok, done;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: row branches stay scalar
     const bool factor = w < kLdltMax / 64;
@@ -1541,46 +1540,26 @@ __global__ void __launch_bounds__(kLdltThreads) k_ldlt_reg(int n, const double* 
     LDLT_PROBE(0);
     if (tid == 0) {
         ok = 1;
-        meet = 0;
+        done = 0;
     }
     __syncthreads();
     LDLT_PROBE(1);
     int cur = 0;   // panel p's row buffer: p mod 3
     for (int p0 = 0; p0 < n; p0 += 6) {
-        const int p1 = min(p0 + 6, n), pw = p1 - p0;
+        const int p1 = min(p0 + 6, n), pw = p1 - p0, pi = p0 / 6;
         const int prv = cur == 0 ? 2 : cur - 1, nxt = cur == 2 ? 0 : cur + 1;
         double* U = Ub + cur * 6 * kLdltMax;
-        double* Lpan = Lb + ((p0 / 6) & 1) * 6 * kLdltMax;
-        const double* Up = Ub + prv * 6 * kLdltMax;
-        const double* Lp = Lb + (((p0 / 6) & 1) ^ 1) * 6 * kLdltMax;
-        LDLT_PROBE(11 + 4 * (p0 / 6));
+        double* Un = Ub + nxt * 6 * kLdltMax;
+        double* Lpan = Lb + (pi & 1) * 6 * kLdltMax;
+        LDLT_PROBE(11 + 4 * (pi < 20 ? pi : 20));
         if (factor) {
-            if (p0 > 0) {
-                // panel p - 1's updates on panel p's rows, column j = tid, k ascending
-                const int j = tid;
-                double up[6];
-#pragma unroll
-                for (int k = 0; k < 6; k++) up[k] = Up[k * kLdltMax + j];
-                // (rows t >= pw of a partial last panel are updated too: nobody reads them, and their
-                // L reads stay inside the LDS block)
-                double v[6];
-#pragma unroll
-                for (int t = 0; t < 6; t++) v[t] = U[t * kLdltMax + j];
-#pragma unroll
-                for (int t = 0; t < 6; t++)
-#pragma unroll
-                    for (int k = 0; k < 6; k++) v[t] -= Lp[(p0 + t) * 6 + k] * up[k];
-#pragma unroll
-                for (int t = 0; t < 6; t++) U[t * kLdltMax + j] = v[t];
-                // both factor waves' columns are in: the diagonal block reads either's
-                if (lane == 0) __hip_atomic_fetch_add(&meet, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const int want = 2 * (p0 / 6);
-                while (__hip_atomic_load(&meet, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-                    __builtin_amdgcn_s_sleep(1);
-            }
-            LDLT_PROBE(100 + (p0 / 6 < 20 ? p0 / 6 : 20));
             if (pw == 6) ldlt_panel6(n, p0, tid, U, Lall, Lpan, dvec, y, &ok);
             else ldlt_panel_generic(n, p0, pw, tid, U, Lall, Lpan, dvec, y, &ok);
+            // (also after a zero pivot: the row waves wait for this count)
+            if (lane == 0) __hip_atomic_fetch_add(&done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef ORB_LDLT_PROBE
+            if (tid == 0 && pi < 20) g_ldlt_probe[220 + pi] = clock64();   // factor done
+#endif
         } else {
             // panel p - 1's updates on the rows below panel p, panel p + 1's rows published.  The
             // slot index is re-made opaque per panel: hoisted out of the panel loop, the rows'
@@ -1588,20 +1567,38 @@ __global__ void __launch_bounds__(kLdltThreads) k_ldlt_reg(int n, const double* 
             int tv = t6;
             asm volatile("" : "+s"(tv));
             if (p0 > 0) {
-                ldlt_rows(R, Up, Lp, Ub + nxt * 6 * kLdltMax, n, p1, tv, lane);
+                ldlt_rows(R, Ub + prv * 6 * kLdltMax, Lb + ((pi & 1) ^ 1) * 6 * kLdltMax, Un, n, p1, tv, lane);
             } else if (6 + t6 < n) {   // phase 0: panel 1's rows (slot 1) as they are
-                Ub[nxt * 6 * kLdltMax + t6 * kLdltMax + lane] = R[0][1];
-                Ub[nxt * 6 * kLdltMax + t6 * kLdltMax + lane + 64] = R[1][1];
+                Un[t6 * kLdltMax + lane] = R[0][1];
+                Un[t6 * kLdltMax + lane + 64] = R[1][1];
             }
 #ifdef ORB_LDLT_PROBE
-            if (lane == 0 && p0 / 6 < 16) g_ldlt_probe[124 + 6 * (p0 / 6) + t6] = clock64();   // row waves done
+            if (lane == 0 && pi < 16) g_ldlt_probe[124 + 6 * pi + t6] = clock64();   // bulk done
 #endif
+            const int i = p1 + tv;   // this wave's row of panel p + 1 (panel p is full when it exists)
+            if (i < n) {
+                while (__hip_atomic_load(&done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 2 * (pi + 1))
+                    __builtin_amdgcn_s_sleep(1);
+                double L[6], u0[6], u1[6];
+#pragma unroll
+                for (int t = 0; t < 6; t++) {
+                    L[t] = Lpan[i * 6 + t];
+                    u0[t] = U[t * kLdltMax + lane];
+                    u1[t] = U[t * kLdltMax + lane + 64];
+                }
+                double v0 = Un[tv * kLdltMax + lane], v1 = Un[tv * kLdltMax + lane + 64];
+                const double o0 = v0, o1 = v1;
+#pragma unroll
+                for (int t = 0; t < 6; t++) {
+                    v0 -= L[t] * u0[t];
+                    v1 -= L[t] * u1[t];
+                }
+                Un[tv * kLdltMax + lane] = lane >= i ? v0 : o0;
+                Un[tv * kLdltMax + lane + 64] = lane + 64 >= i ? v1 : o1;
+            }
         }
-#ifdef ORB_LDLT_PROBE
-        if (factor && tid == 0) g_ldlt_probe[220 + (p0 / 6 < 20 ? p0 / 6 : 20)] = clock64();   // factor done
-#endif
         __syncthreads();
-        LDLT_PROBE(12 + 4 * (p0 / 6));
+        LDLT_PROBE(12 + 4 * (pi < 20 ? pi : 20));
         if (!ok) break;
         cur = nxt;
     }

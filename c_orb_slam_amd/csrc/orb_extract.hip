@@ -947,6 +947,9 @@ void Extractor::release() {
     d_levels_ = nullptr; d_tabs_ = nullptr; d_kps_ = nullptr; d_desc_ = nullptr;
     if (h_nout_) (void)hipHostFree(h_nout_);
     h_nout_ = nullptr;
+    if (h_in_) (void)hipHostFree(h_in_);
+    h_in_ = nullptr;
+    h_in_cap_ = 0;
     for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
     for (auto& e : ev_) e = nullptr;
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -1590,7 +1593,17 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
             ORB_HIP_CHECK(hipMalloc(&d_in_, need));
             in_cap_ = need;
         }
-        ORB_HIP_CHECK(hipMemcpyAsync(d_in_, imgs, need, hipMemcpyHostToDevice, s));
+        // the previous call's copy out of h_in_ is done once ev_[0] (recorded right after it) is
+        if (h_in_) ORB_HIP_CHECK(hipEventSynchronize(ev_[0]));
+        if (need > h_in_cap_) {
+            if (h_in_) (void)hipHostFree(h_in_);
+            h_in_ = nullptr;
+            h_in_cap_ = 0;
+            ORB_HIP_CHECK(hipHostMalloc(&h_in_, need));
+            h_in_cap_ = need;
+        }
+        std::memcpy(h_in_, imgs, need);
+        ORB_HIP_CHECK(hipMemcpyAsync(d_in_, h_in_, need, hipMemcpyHostToDevice, s));
         src = (const uint8_t*)d_in_;
     }
     ORB_HIP_CHECK(hipEventRecord(ev_[0], s));

@@ -166,6 +166,10 @@ private:
     int work_part_[2] = {0, 0};   // table entries of the levels < kFastSplitLevel, then of the rest
     bool d_gtotal_alias_ = false;
     size_t in_cap_ = 0, out_cap_ = 0;
+    // host images go through this pinned block (a host memcpy, then an async DMA copy): the HIP
+    // runtime's own path for pageable sources stalled an occasional call by several ms
+    void* h_in_ = nullptr;
+    size_t h_in_cap_ = 0;
     // device octree (octree.hip): per-job selections, per-image selected lists
     void *d_jobsel_ = nullptr, *d_jobcnt_ = nullptr, *d_octlv_ = nullptr, *d_gscr_ = nullptr, *d_nout_ = nullptr;
     int jcap_ = 0, selcap_ = 0;

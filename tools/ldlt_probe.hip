@@ -40,8 +40,7 @@ int main(int argc, char** argv) {
     }
     printf("\nphases (factor panel p | rows: panel p - 1's updates) %lld cycles, %d panels\n", ph, (n + 5) / 6);
     for (int k = 1; k < (n + 5) / 6 && k < 16; k++) {
-        printf("phase %2d: rows updated %5lld factor %5lld | row waves done at", k, p[100 + k] - p[11 + 4 * k],
-               p[220 + k] - p[100 + k]);
+        printf("phase %2d: factor done at %5lld | row waves' trailing update done at", k, p[220 + k] - p[11 + 4 * k]);
         for (int t = 0; t < 6; t++) printf(" %5lld", p[124 + 6 * k + t] - p[11 + 4 * k]);
         printf(" | barrier at %5lld\n", p[12 + 4 * k] - p[11 + 4 * k]);
     }
