@@ -561,6 +561,12 @@ def main():
         # HBM-resident images (left t, right t = left t + B images), the right image's results
         # landing in the next frame's slot of k / d (overwritten by that frame's left image)
         eLR = None if host_io or not args.latency_stereo_batch else orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=2)
+        # host path: Frame(imLeft, imRight)'s two host images in one extractor call (one staging block,
+        # one H2D copy, one stream); BENCH_LAT_HOST_THREADS=1 keeps the reference's shape of two
+        # extractor calls on two threads (A/B: concurrent blocking waits on two streams there show
+        # sporadic ~7 ms wake-ups, profiles/r05vlat_slowest_frames.txt)
+        host_pair = host_io and os.environ.get("BENCH_LAT_HOST_THREADS") != "1"
+        eLRh = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, max_width=W, max_height=H, max_batch=2) if host_pair else None
         k = torch.empty((nf + 1, cap, 7), dtype=torch.int32, device=dev)
         d = torch.empty((nf + 1, cap, 32), dtype=torch.uint8, device=dev)
         kR = torch.empty((cap, 7), dtype=torch.int32, device=dev)
@@ -587,6 +593,7 @@ def main():
         Tcw = [np.eye(4, dtype=np.float32)]
         walls = []
         nmatch = []
+        marks = []   # per frame: (phase, ms since the frame's start) -- where a slow frame spent its time
         # the drop-in caller is C++ (System::TrackStereo): no interpreter garbage collection runs
         # between its frames, so none runs inside this leg's timed frames either
         import gc
@@ -596,15 +603,41 @@ def main():
         for t in range(nf):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            if host_io:   # Frame(imLeft, imRight) on pageable host images (Frame.cc:78-81)
-                fR = pool.submit(eR1.extract_host_to_device, rights[t], kR.data_ptr(), dR.data_ptr(), cap)
+            mk = []
+            marks.append(mk)
+
+            def mark(name):
+                mk.append((name, (time.perf_counter() - t0) * 1e3))
+
+            if host_pair:   # Frame(imLeft, imRight) on pageable host images (Frame.cc:78-81), one call
+                nLR = eLRh.extract_host_images_to_device([lefts[t], rights[t]], k[t].data_ptr(), d[t].data_ptr(), cap)
+                mark("extract_both")
+                nL, nR = nLR[:1], nLR[1:]
+                nl, nr = np.array([nLR[0]], np.int32), np.array([nLR[1]], np.int32)
+                check(L.ORBmatcher_ComputeStereoMatches_batch_at(m._h, eLRh._h, 0, eLRh._h, 1, 1, ptr(nl),
+                                                                 arr([k[t].data_ptr()]), arr([d[t].data_ptr()]), ptr(nr),
+                                                                 arr([k[t + 1].data_ptr()]), arr([d[t + 1].data_ptr()]),
+                                                                 float(mbf), float(mb), arr([uR[t].data_ptr()]),
+                                                                 arr([dep[t].data_ptr()]), ptr(one)),
+                      "ComputeStereoMatches")
+            elif host_io:   # the same as two extractor calls on two threads
+                def right_host(img):
+                    r = eR1.extract_host_to_device(img, kR.data_ptr(), dR.data_ptr(), cap)
+                    mark("extract_right")
+                    return r
+
+                fR = pool.submit(right_host, rights[t])
                 nL = eL1.extract_host_to_device(lefts[t], k[t].data_ptr(), d[t].data_ptr(), cap)
+                mark("extract_left")
             elif eLR is None:
                 fR = pool.submit(eR1.extract_device, d_R[t].data_ptr(), 1, W, H, W, W * H, kR.data_ptr(), dR.data_ptr(),
                                  cap)
                 nL = eL1.extract_device(d_L[t].data_ptr(), 1, W, H, W, W * H, k[t].data_ptr(), d[t].data_ptr(), cap)
-            if host_io or eLR is None:
+            if host_pair:
+                pass
+            elif host_io or eLR is None:
                 nR = fR.result()
+                mark("extract_both")
                 nl, nr = np.array([nL[0]], np.int32), np.array([nR[0]], np.int32)
                 check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, eL1._h, eR1._h, 1, ptr(nl), arr([k[t].data_ptr()]),
                                                               arr([d[t].data_ptr()]), ptr(nr), arr([kR.data_ptr()]),
@@ -621,6 +654,7 @@ def main():
                                                                  float(mbf), float(mb), arr([uR[t].data_ptr()]),
                                                                  arr([dep[t].data_ptr()]), ptr(one)),
                       "ComputeStereoMatches")
+            mark("stereo")
             if t > 0:
                 V = Tcw[t - 1] @ np.linalg.inv(Tcw[t - 2]) if t >= 2 else np.eye(4, dtype=np.float32)
                 Tp = (V @ Tcw[t - 1]).astype(np.float32)
@@ -660,6 +694,7 @@ def main():
                 ni = np.zeros(1, np.int32)
                 check(L.Optimizer_PoseOptimization_frames_device(1, C.byref(pf), arr([T1.data_ptr()]),
                                                                  arr([o1.data_ptr()]), ptr(ni)), "PoseOptimization")
+                mark("motion_model")
                 prep = orb_localprep(int(nL[0]), cur_mp.data_ptr(), o1.data_ptr(), nloc, slot[q].data_ptr(),
                                      skip.data_ptr())
                 check(L.Tracking_PrepareLocalSearch_batch_device(m._h, 1, C.byref(prep)), "PrepareLocalSearch")
@@ -670,16 +705,18 @@ def main():
                 check(L.ORBmatcher_SearchLocalPoints_batch(m._h, 1, C.byref(fc), arr([cur_mp.data_ptr()]),
                                                            C.byref(lmap), float(lsf), 1.0, 0.8, ptr(nm2), ptr(nv2)),
                       "SearchLocalPoints")
+                mark("local_search")
                 pf.Tcw = T1.data_ptr()
                 check(L.Optimizer_PoseOptimization_frames_device(1, C.byref(pf), arr([T2.data_ptr()]),
                                                                  arr([o2.data_ptr()]), ptr(ni)), "PoseOptimization 2")
+                mark("local_pose")
                 if host_io:   # the Frame's members back on the host (one stream sync)
                     n0, n1 = int(nL[0]), int(nR[0])
                     with torch.cuda.stream(match_stream):
                         hk[:n0].copy_(k[t, :n0], non_blocking=True)
                         hd[:n0].copy_(d[t, :n0], non_blocking=True)
-                        hkR[:n1].copy_(kR[:n1], non_blocking=True)
-                        hdR[:n1].copy_(dR[:n1], non_blocking=True)
+                        hkR[:n1].copy_((k[t + 1] if host_pair else kR)[:n1], non_blocking=True)
+                        hdR[:n1].copy_((d[t + 1] if host_pair else dR)[:n1], non_blocking=True)
                         huR[:n0].copy_(uR[t, :n0], non_blocking=True)
                         hdep[:n0].copy_(dep[t, :n0], non_blocking=True)
                         hT.copy_(T2, non_blocking=True)
@@ -692,6 +729,7 @@ def main():
                     Tcw.append(T2.cpu().numpy().reshape(4, 4).copy())
                 nmatch.append(int(nm1[0] + nm2[0]))
             last_n = nL
+            mark("end")
             walls.append((time.perf_counter() - t0) * 1e3)
         if gc_was:
             gc.enable()
@@ -704,9 +742,19 @@ def main():
                "max_rotation_error": round(max(err), 6),
                "note": "Frame(imLeft, imRight) + TrackWithMotionModel + TrackLocalMap per frame, synchronous C-ABI "
                        "calls; pose t from pose t-1 and t-2 (constant-velocity model)"}
+        # the slowest timed frame's phase marks beside the median frame's (ms since the frame's start)
+        tw = int(np.argmax(walls[2:])) + 2
+        med = {}
+        for mk in marks[2:]:
+            for name, v in mk:
+                med.setdefault(name, []).append(v)
+        out["slowest_frame"] = {"frame": tw, "marks_ms": {nm: round(v, 3) for nm, v in marks[tw]},
+                                "median_marks_ms": {nm: round(float(np.median(v)), 3) for nm, v in med.items()}}
         if host_io:
-            out["io"] = ("host: both 1241x376 images read from pageable host memory inside the extractor calls "
-                         f"(2 x {W * H} B H2D), the Frame's results copied back before the clock stops "
+            out["io"] = ("host: both 1241x376 images read from pageable host memory inside the extractor call "
+                         + ("(ORBextractor_extract_images: one call for the pair, staged in one pinned block, "
+                            if host_pair else "(two extractor calls on two threads, ")
+                         + f"2 x {W * H} B H2D), the Frame's results copied back before the clock stops "
                          f"(~{int(np.mean(d2h_bytes))} B D2H: keypoints + descriptors L/R, mvuRight, mvDepth, "
                          "mTcw, mvpMapPoints, mvbOutlier) -- System::TrackStereo semantics (System.cc:116)")
         else:

@@ -123,6 +123,7 @@ def lib():
     L.ORBextractor_destroy.argtypes = [vp]
     L.ORBextractor_extract.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, P(i32)]
     L.ORBextractor_extract_batch.argtypes = [vp, vp, i32, i32, i32, i32, sz, i32, vp, vp, i32, i32, vp]
+    L.ORBextractor_extract_images.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, i32, i32, vp]
     L.ORBextractor_get_level.argtypes = [vp, i32, i32, vp, i32, P(i32), P(i32)]
     L.ORBextractor_get_blurred_level.argtypes = [vp, i32, i32, vp, i32, P(i32), P(i32)]
     L.ORBextractor_get_levels.argtypes = [vp, P(i32), P(f32)]

@@ -652,6 +652,9 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
                                               const uint8_t* poseAdd, const int* run, int ldcDyn) {
     BA_GATE(run);
     ORBGPU_PROF_START;
+#ifdef ORBGPU_PROF
+    const unsigned long long tBlk0 = clock64();   // (instrumented builds: per-wave block durations)
+#endif
     constexpr bool kMixed = NT == 256;
     __shared__ double csS[kMixed ? 1 : 36 * kChunks];
     extern __shared__ double lds[];
@@ -725,6 +728,15 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
         }
     }
     ORBGPU_PROF_MARK(11);   // (instrumented builds: block 0's wave 0 -- chunk terms and trees)
+#ifdef ORBGPU_PROF
+    if (kMixed && lane == 0) {   // the many-block launch: log2 histogram of the waves' chunk phases
+        const unsigned long long dt = clock64() - tBlk0;
+        int bkt = 63 - __builtin_clzll(dt | 1ull) - 10;
+        bkt = bkt < 0 ? 0 : (bkt > 9 ? 9 : bkt);
+        atomicAdd(&g_orbgpu_prof[bkt], 1ull);
+        atomicAdd(&g_orbgpu_prof[group ? 10 : 14], dt);
+    }
+#endif
     if (group) {
         __syncthreads();
     } else {
@@ -1769,16 +1781,15 @@ __global__ void __launch_bounds__(64) k_lm_begin(LmDev* L, int iterations) {
 
 // one thread: the host code of BaEngine::lm_solve after its readback, verbatim in order;
 // returns whether the trial is undone (pop).  The LM state's scalars, the trial's scalars and the
-// host's stop flag are read up front (independent loads in flight together) and written back at
-// the end: through the global pointers every access would wait for the one before it.
+// host's stop flag are read by the caller at the start of k_lm_trial_end (independent loads in
+// flight together, behind the workgroup's sums) and written back at the end: through the global
+// pointers every access would wait for the one before it.
 struct LmHead {
     int ctl[4];
     int it, iterations, qmax, nBad, haveChi, done, nTrial, nSolve, steps;
     double ni, currentChi, iniChi;
 };
-__device__ int lm_decide(LmDev* Lg, double* scal, volatile int* host, const double* chi) {
-    const bool stop = host[0] != 0;
-    LmHead L;
+__device__ __forceinline__ void lm_load(const LmDev* Lg, LmHead& L) {
     L.ctl[0] = Lg->ctl[0];
     L.ctl[1] = Lg->ctl[1];
     L.ctl[2] = Lg->ctl[2];
@@ -1795,8 +1806,11 @@ __device__ int lm_decide(LmDev* Lg, double* scal, volatile int* host, const doub
     L.ni = Lg->ni;
     L.currentChi = Lg->currentChi;
     L.iniChi = Lg->iniChi;
-    const double s0 = chi ? chi[0] : scal[0], s1 = chi ? chi[1] : scal[1];   // chi: the fused totals (LDS)
-    const double s2 = scal[2], s3 = scal[3], s5 = scal[5];
+}
+// L: the state as lm_load read it; stop: the host's flag; s0..s5: the trial's scalars (chi2 of the
+// system and the trial, scale, the trial's solve status, -, lambda)
+__device__ int lm_decide(LmDev* Lg, LmHead L, double* scal, volatile int* host, bool stop, double s0, double s1,
+                         double s2, double s3, double s5) {
     if (!L.haveChi) {
         L.currentChi = L.iniChi = s0;
         L.haveChi = 1;
@@ -1884,30 +1898,45 @@ __device__ int lm_decide(LmDev* Lg, double* scal, volatile int* host, const doub
 // sum, problems with 6 nP + 3 nL <= 2048 * 64; larger ones ran k_scale_chunks + k_csum into
 // scal[2] and pass scale = 0), the LM decision, and the pop of a rejected trial, in one workgroup.
 constexpr int kChiFuseMax = 1024;   // chunk trees per linearisation (nE <= 65536) summed in LDS
+constexpr int kTeThreads = 1024;
+constexpr int kTePre = 4;      // committed landmarks per thread loaded ahead
+constexpr int kScalePre = 8;   // scale chunks per wave loaded ahead of their trees
 struct ChiFuse {
     const double* chunksSys;     // the system linearisation's chunk trees (chi2 -> scal[0]), or null
     const double* chunksTrial;   // the trial's (-> scal[1])
     int nE;
 };
-__global__ void __launch_bounds__(1024) k_lm_trial_end(LmDev* L, double* scal, volatile int* host, BaStructDev s,
+__global__ void __launch_bounds__(kTeThreads) k_lm_trial_end(LmDev* L, double* scal, volatile int* host, BaStructDev s,
                                                        Se3* T, const Se3* Tbak, double* X, const double* Xbak,
                                                        const double* x, const double* bp, const double* bl, int scale,
                                                        ChiFuse cf, const Se3* Tn, const double* Xn) {
     __shared__ double lv[2048];
     __shared__ double cA[kChiFuseMax], cB[kChiFuseMax];
-    __shared__ double chi[2];
+    __shared__ double tot[3];   // the fused chi2 totals (system, trial) and the scale sum
     __shared__ int pop, live;
-    // one read of the run flag for the whole workgroup: lm_decide below may clear ctl[0] (the
-    // run ends with this trial) and a wave reading it after that would skip the pop
-    if (threadIdx.x == 0) live = L->ctl[0];
-    __syncthreads();
-    if (!live) return;   // a step queued after the run ended
     const int nP = s.nP, nL = s.nL;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // Everything this kernel reads is loaded before its first barrier, in flight together: the LM
+    // state, the host's stop flag and the trial's scalars (thread 0), the chunk trees, the scale
+    // terms and the values an accepted trial commits.  Nothing is written before that barrier, which
+    // publishes the run flag: a step queued after the run ended stops there (its loads read
+    // allocated buffers).  One read of the flag for the whole workgroup: lm_decide may clear
+    // ctl[0] and a wave reading it after that would skip the pop.
+    LmHead H;
+    bool stop = false;
+    double g0 = 0, g1 = 0, g2 = 0, g3 = 0;
+    if (threadIdx.x == 0) {
+        lm_load(L, H);
+        stop = host[0] != 0;
+        g0 = scal[0];
+        g1 = scal[1];
+        g2 = scal[2];
+        g3 = scal[3];
+    }
     const bool fuse = cf.chunksSys != nullptr;
     const int mc = (cf.nE + 63) >> 6;   // fuse: 2 <= nE, mc <= kChiFuseMax (host)
     if (fuse)
-        for (int c = threadIdx.x; c < mc; c += blockDim.x) {
+        for (int c = threadIdx.x; c < mc; c += kTeThreads) {
             cA[c] = cf.chunksSys[c];
             cB[c] = cf.chunksTrial[c];
         }
@@ -1915,47 +1944,90 @@ __global__ void __launch_bounds__(1024) k_lm_trial_end(LmDev* L, double* scal, v
     const int m = (n + 63) >> 6;
     const double lambda = scal[5];
     auto term = [&](int j) {
-        const double b = j < 6 * nP ? bp[j] : bl[j - 6 * nP];
-        return x[j] * (lambda * x[j] + b);
+        const double* b = j < 6 * nP ? bp + j : bl + (j - 6 * nP);
+        return x[j] * (lambda * x[j] + *b);
     };
+    // the scale terms of kScalePre chunks per wave loaded before their trees
     if (scale && n > 1)
-        for (int c = w; c < m; c += 16) {
-            const int j = c * 64 + lane;
-            const double t = wave_tree(j < n ? term(j) : 0.0);
-            if (lane == 0) lv[c] = t;
+        for (int c0 = w; c0 < m; c0 += 16 * kScalePre) {
+            double tv[kScalePre];
+#pragma unroll
+            for (int k = 0; k < kScalePre; k++) {
+                const int j = (c0 + 16 * k) * 64 + lane;
+                tv[k] = j < n ? term(j) : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < kScalePre; k++) {
+                const double t = wave_tree(tv[k]);
+                if (lane == 0 && c0 + 16 * k < m) lv[c0 + 16 * k] = t;
+            }
         }
+    // an accepted trial's commit (Tn set): the first kTePre landmarks and the pose of each thread
+    double xc[kTePre][3], tc[8];
+    int pc[kTePre];
+    int kc = -1;
+    if (Tn) {
+#pragma unroll
+        for (int k = 0; k < kTePre; k++) {
+            const int l = threadIdx.x + k * kTeThreads;
+            pc[k] = -1;
+            if (l < nL) {
+                pc[k] = s.landPt[l];
+                for (int d = 0; d < 3; d++) xc[k][d] = Xn[3 * l + d];
+            }
+        }
+        if ((int)threadIdx.x < nP) {
+            kc = s.poseKf[threadIdx.x];
+            const double* src = (const double*)(Tn + threadIdx.x);
+#pragma unroll
+            for (int d = 0; d < 8; d++) tc[d] = src[d];
+        }
+    }
+    if (threadIdx.x == 0) live = H.ctl[0];
     __syncthreads();
+    if (!live) return;   // a step queued after the run ended
     // block_finish_csum's totals: wave_tree pairs as tree64_local, so wave_lds_csum is
     // local_csum_inplace's canonical sum
     if (scale && w == 0) {
         const double t = n > 1 ? wave_lds_csum(lv, m) : n == 1 ? term(0) : 0.0;
-        if (lane == 0) scal[2] = t;
+        if (lane == 0) {
+            tot[2] = t;
+            scal[2] = t;
+        }
     }
     if (fuse && (w == 1 || w == 2)) {
         double* c = w == 1 ? cA : cB;
         const double t = mc == 1 ? c[0] : wave_lds_csum(c, mc);
         if (lane == 0) {
-            chi[w - 1] = t;
+            tot[w - 1] = t;
             scal[w - 1] = t;
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) pop = lm_decide(L, scal, host, fuse ? chi : nullptr);
+    if (threadIdx.x == 0)
+        pop = lm_decide(L, H, scal, host, stop, fuse ? tot[0] : g0, fuse ? tot[1] : g1, scale ? tot[2] : g2, g3,
+                        lambda);
     __syncthreads();
     if (Tn) {   // the update was fused into the trial pass: an accepted trial commits its poses / points
         if (pop) return;
-        for (int g = threadIdx.x; g < nP + nL; g += blockDim.x) {
-            if (g < nP) {
-                T[s.poseKf[g]] = Tn[g];
-            } else {
-                const int l = g - nP, pt = s.landPt[l];
-                for (int k = 0; k < 3; k++) X[3 * pt + k] = Xn[3 * l + k];
-            }
+        if (kc >= 0) {
+            double* dst = (double*)(T + kc);
+#pragma unroll
+            for (int d = 0; d < 8; d++) dst[d] = tc[d];
+        }
+        for (int g = threadIdx.x + kTeThreads; g < nP; g += kTeThreads) T[s.poseKf[g]] = Tn[g];
+#pragma unroll
+        for (int k = 0; k < kTePre; k++)
+            if (pc[k] >= 0)
+                for (int d = 0; d < 3; d++) X[3 * pc[k] + d] = xc[k][d];
+        for (int l = threadIdx.x + kTePre * kTeThreads; l < nL; l += kTeThreads) {
+            const int pt = s.landPt[l];
+            for (int d = 0; d < 3; d++) X[3 * pt + d] = Xn[3 * l + d];
         }
         return;
     }
     if (!pop) return;
-    for (int g = threadIdx.x; g < nP + nL; g += blockDim.x) {   // k_pop
+    for (int g = threadIdx.x; g < nP + nL; g += kTeThreads) {   // k_pop
         if (g < nP) {
             const int kf = s.poseKf[g];
             T[kf] = Tbak[kf];
@@ -4065,7 +4137,7 @@ void BaEngine::enqueue_lm_step(bool first) {
         CsumList L0{tmpA0_, (nv + 63) / 64, tmpA1_, tmpA0_, dScal_ + 2};
         hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, L0, L0, ctl);
     }
-    hipLaunchKernelGGL(k_lm_trial_end, dim3(1), dim3(1024), 0, s, dLm_, dScal_, (volatile int*)hLm_, S, dT_, dTbak_,
+    hipLaunchKernelGGL(k_lm_trial_end, dim3(1), dim3(kTeThreads), 0, s, dLm_, dScal_, (volatile int*)hLm_, S, dT_, dTbak_,
                        dX_, dXbak_, dX2_, dBp_, dBl_, small ? 1 : 0,
                        fuse ? ChiFuse{tmpB0_, tmpB1_, nE} : ChiFuse{nullptr, nullptr, 0}, fuse ? dTn_ : nullptr,
                        fuse ? dXn_ : nullptr);
@@ -4079,15 +4151,33 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
     hLm_[2] = 0;
     hLm_[3] = 0;
     hipLaunchKernelGGL(k_lm_begin, dim3(1), dim3(64), 0, stream_, dLm_, iterations);
-    // at most 10 trials per iteration; the host stays one step ahead of the decisions
+    // at most 10 trials per iteration; the host stays one step ahead of the decisions.  It learns
+    // of them from the words k_lm_trial_end writes to host memory ([2] steps decided, [1] done), not
+    // from an event per step: an event record is a marker packet, about 5 us of idle queue after
+    // every trial (profiles/r05vlba_*).  ORBGPU_LM_EVENTS=1 keeps the events (A/B).
     const int maxSteps = 10 * iterations;
+    static const bool useEvents = [] {
+        const char* e = getenv("ORBGPU_LM_EVENTS");
+        return e && e[0] == '1';
+    }();
+    volatile int* hw = (volatile int*)hLm_;
     for (int j = 0; j < maxSteps; j++) {
         enqueue_lm_step(j == 0);
         ORB_HIP_CHECK(hipGetLastError());
-        ORB_HIP_CHECK(hipEventRecord(lmEv_[j & 1], stream_));
-        if (j >= 1) {
-            ORB_HIP_CHECK(hipEventSynchronize(lmEv_[(j - 1) & 1]));
-            if (((volatile int*)hLm_)[1]) break;
+        if (useEvents) {
+            ORB_HIP_CHECK(hipEventRecord(lmEv_[j & 1], stream_));
+            if (j >= 1) {
+                ORB_HIP_CHECK(hipEventSynchronize(lmEv_[(j - 1) & 1]));
+                if (hw[1]) break;
+            }
+        } else if (j >= 1) {
+            // step j - 1 decided (steps >= j) or the run over; a drained stream ends the wait too
+            // (its writes are all visible then, and the final readback below checks the state)
+            for (unsigned spin = 1; hw[2] < j && !hw[1]; spin++) {
+                if ((spin & 255) == 0 && hipStreamQuery(stream_) == hipSuccess) break;
+                __builtin_ia32_pause();
+            }
+            if (hw[1]) break;
         }
         hLm_[0] = stopped(stop) ? 1 : 0;
     }

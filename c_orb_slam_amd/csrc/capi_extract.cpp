@@ -63,6 +63,21 @@ int ORBextractor_extract_batch(ORBextractor_h h, const uint8_t* imgs, int batch,
     return ORB_OK;
 }
 
+int ORBextractor_extract_images(ORBextractor_h h, const uint8_t* const* imgs, int batch, int width, int height,
+                                int step, orb_kp* kps, uint8_t* desc, int cap_per_image, int outputs_on_device,
+                                int* n_out) {
+    if (!h || !imgs || !kps || !desc || !n_out || batch <= 0 || step < width || cap_per_image < 0 || height <= 0)
+        return ORB_E_INVALID;
+    for (int b = 0; b < batch; b++)
+        if (!imgs[b]) return ORB_E_INVALID;
+    int rc = h->ex->extract(nullptr, batch, width, height, step, (size_t)step * height, false, kps, desc,
+                            cap_per_image, outputs_on_device != 0, n_out, imgs);
+    if (rc == -3) return ORB_E_CAPACITY;
+    if (rc == -2) return ORB_E_HIP;
+    if (rc) return ORB_E_INVALID;
+    return ORB_OK;
+}
+
 int ORBextractor_get_level(ORBextractor_h h, int index, int level, uint8_t* dst, int dst_step, int* w, int* h_) {
     if (!h || !w || !h_) return ORB_E_INVALID;
     int rc = h->ex->get_level(index, level, dst, dst_step, w, h_);

@@ -1580,7 +1580,7 @@ int Extractor::setup_geometry(int W, int H) {
 
 int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_t img_stride,
                        bool imgs_on_device, orb_kp* kps, uint8_t* desc, int cap, bool out_on_device,
-                       int* n_out) {
+                       int* n_out, const uint8_t* const* list) {
     if (B <= 0 || B > maxB_ || W <= 0 || H <= 0) return -1;
     if (W > maxW_ || H > maxH_) return -1;
     if (int e = setup_geometry(W, H)) return e;
@@ -1602,7 +1602,12 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
             ORB_HIP_CHECK(hipHostMalloc(&h_in_, need));
             h_in_cap_ = need;
         }
-        std::memcpy(h_in_, imgs, need);
+        if (list) {   // separate host images (Frame's two cv::Mat): one staging block, one H2D copy
+            const size_t one = (size_t)step * (H - 1) + W;
+            for (int b = 0; b < B; b++) std::memcpy((uint8_t*)h_in_ + img_stride * b, list[b], one);
+        } else {
+            std::memcpy(h_in_, imgs, need);
+        }
         ORB_HIP_CHECK(hipMemcpyAsync(d_in_, h_in_, need, hipMemcpyHostToDevice, s));
         src = (const uint8_t*)d_in_;
     }

@@ -82,8 +82,10 @@ public:
     Extractor(int nfeatures, float scaleFactor, int nlevels, int iniTh, int minTh);
     ~Extractor();
     int init_device(int maxW, int maxH, int maxBatch);
+    // list != nullptr: B host images at list[b] (row stride step), staged as one block (imgs unused)
     int extract(const uint8_t* imgs, int B, int W, int H, int step, size_t img_stride, bool imgs_on_device,
-                orb_kp* kps, uint8_t* desc, int cap, bool out_on_device, int* n_out);
+                orb_kp* kps, uint8_t* desc, int cap, bool out_on_device, int* n_out,
+                const uint8_t* const* list = nullptr);
     int get_level(int index, int level, uint8_t* dst, int dst_step, int* w, int* h);
     int get_blurred(int index, int level, uint8_t* dst, int dst_step, int* w, int* h);
     int timings(float* ms6);

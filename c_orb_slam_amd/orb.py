@@ -89,6 +89,21 @@ class ORBextractor:
               "ORBextractor_extract_batch(host image)")
         return n
 
+    def extract_host_images_to_device(self, images, d_kps_ptr, d_desc_ptr, cap):
+        """Frame(imLeft, imRight)'s extractions (Frame.cc:78-81) in one call: the host images of
+        equal size staged as one block, one H2D copy, keypoints / descriptors of image b left in HBM
+        at d_kps_ptr + b*cap entries.  -> counts."""
+        imgs = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+        H, W = imgs[0].shape
+        if any(im.shape != (H, W) for im in imgs):
+            raise ValueError("images of different sizes")
+        lst = (C.c_void_p * len(imgs))(*[im.ctypes.data for im in imgs])
+        n = np.zeros(len(imgs), np.int32)
+        check(self._L.ORBextractor_extract_images(self._h, lst, len(imgs), W, H, imgs[0].strides[0],
+                                                  C.c_void_p(d_kps_ptr), C.c_void_p(d_desc_ptr), cap, 1, ptr(n)),
+              "ORBextractor_extract_images")
+        return n
+
     def image_pyramid_level(self, level, index=0):
         """mvImagePyramid[level] WITH its 19-px border (ORBextractor.h:85)."""
         w, h = C.c_int(), C.c_int()

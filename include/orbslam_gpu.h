@@ -80,6 +80,14 @@ int ORBextractor_extract_batch(ORBextractor_h h, const uint8_t* imgs, int batch,
                                orb_kp* kps, uint8_t* desc, int cap_per_image,
                                int outputs_on_device, int* n_out);
 
+/* Host images at separate addresses: Frame(imLeft, imRight)'s two cv::Mat (Frame.cc:78-81 runs
+ * the left and right extractors on two threads; here both are one call on one stream).  Image b
+ * at imgs[b] (host, row stride `step`); the images are staged in one pinned block and copied to
+ * HBM with one H2D copy.  Outputs as ORBextractor_extract_batch (image b at kps + b*cap). */
+int ORBextractor_extract_images(ORBextractor_h h, const uint8_t* const* imgs, int batch, int width,
+                                int height, int step, orb_kp* kps, uint8_t* desc, int cap_per_image,
+                                int outputs_on_device, int* n_out);
+
 /* mvImagePyramid[level] (ORBextractor.h:85) of image `index` of the last call,
  * copied to host WITH its 19-px REFLECT_101 border (Frame.cc:573-580 reads it).
  * dst must hold (w+38)*(h+38) bytes at stride dst_step; *w,*h = unpadded dims. */

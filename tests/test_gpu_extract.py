@@ -112,6 +112,39 @@ def test_extract_non_contiguous_stride(gpu):
     assert np.array_equal(desc[:n.value], od)
 
 
+def test_extract_images_separate_host_buffers(gpu):
+    """ORBextractor_extract_images: Frame(imLeft, imRight)'s two host images at unrelated addresses
+    (one with a padded row stride) in one call; each image's keypoints / descriptors equal the
+    oracle's, over two calls (the pinned staging block reused); a null image is rejected."""
+    import ctypes as C
+    from c_orb_slam_amd._lib import KP_DTYPE, lib, ptr
+    frames, _ = synthetic.sequence(21, 4, 1241, 376)
+    ex = gpu.ORBextractor(1200, 1.2, 8, 20, 7, max_width=1241, max_height=376, max_batch=2)
+    orc = oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7)
+    cap = 4096
+    for call in range(2):
+        a = np.ascontiguousarray(frames[2 * call])
+        big = np.zeros((376, 1300), np.uint8)   # the second image inside a wider buffer: row stride 1300
+        big[:, :1241] = frames[2 * call + 1]
+        # both images share the row stride of the call: copy the first into a 1300-wide buffer too
+        abig = np.zeros((376, 1300), np.uint8)
+        abig[:, :1241] = a
+        lst = (C.c_void_p * 2)(abig.ctypes.data, big.ctypes.data)
+        kps = np.zeros(2 * cap, KP_DTYPE)
+        desc = np.zeros((2 * cap, 32), np.uint8)
+        n = np.zeros(2, np.int32)
+        assert lib().ORBextractor_extract_images(ex._h, lst, 2, 1241, 376, 1300, ptr(kps), ptr(desc), cap, 0,
+                                                 ptr(n)) == 0
+        for b in range(2):
+            ok, od = orc(frames[2 * call + b])
+            got = kps[b * cap:b * cap + n[b]]
+            assert n[b] == len(ok) and np.array_equal(got.view(np.uint8), ok.view(np.uint8)), f"call {call} image {b}"
+            assert np.array_equal(desc[b * cap:b * cap + n[b]], od), f"call {call} image {b}"
+    bad = (C.c_void_p * 2)(abig.ctypes.data, None)
+    assert lib().ORBextractor_extract_images(ex._h, bad, 2, 1241, 376, 1300, ptr(kps), ptr(desc), cap, 0,
+                                             ptr(n)) != 0
+
+
 def _sparse_image(seed, w=1241, h=376, nrect=12):
     rng = np.random.default_rng(seed)
     img = np.full((h, w), 90, np.uint8)

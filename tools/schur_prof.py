@@ -35,6 +35,9 @@ def main():
     for _ in range(reps):
         run()
     lib().orbgpu_debug_prof(out)
+    if gba:   # the many-block launch: per-wave chunk-phase durations (log2 buckets from 1 k cycles)
+        print("waves by chunk-phase cycles:", {f">={1 << (10 + b)}": out[b] for b in range(10)})
+        print(f"chunk-phase cycles summed: diagonal-block waves {out[10]:.3g}, off-diagonal waves {out[14]:.3g}")
     n = max(out[15], 1)
     print(f"k_schur block 0 over {out[15]} launches, cycles per launch: terms+trees (wave 0) {out[11] / n:.0f} | "
           f"barrier wait {out[12] / n:.0f} | final sums {out[13] / n:.0f}")
