@@ -1759,7 +1759,7 @@ __global__ void __launch_bounds__(1024) k_csum(CsumList L0, CsumList L1, const i
 // queues whole steps (system kernels gated by ctl[1], trial kernels by ctl[0]) one step ahead of
 // the decisions it has seen; k_lm_trial_end sets the gates of the next step.
 // Host-pinned coherent words (LmHost): [0] stop flag mirror (host writes), [1] done, [2] steps
-// decided, [3] iterations (device writes).
+// decided, [3] iterations, [4..5] (done, steps) as one 8-byte word the host polls (device writes).
 __global__ void __launch_bounds__(64) k_lm_begin(LmDev* L, int iterations) {
     if (threadIdx.x != 0) return;
     L->ctl[0] = 1;
@@ -1889,7 +1889,9 @@ __device__ int lm_decide(LmDev* Lg, LmHead L, double* scal, volatile int* host, 
     Lg->iniChi = L.iniChi;
     host[3] = L.it;
     host[2] = L.steps;
-    host[1] = L.done;   // read by the host after this step's event: kernel completion publishes it
+    host[1] = L.done;
+    // the pair (done, steps) as one aligned 8-byte store: the host's poll sees both or neither
+    *(volatile unsigned long long*)(host + 4) = ((unsigned long long)(unsigned)L.steps << 32) | (unsigned)L.done;
     return pop;
 }
 
@@ -3357,7 +3359,10 @@ int BaEngine::carve(bool commit, size_t* total) {
     dLevel_ = (uint8_t*)take(ne);
     dRobust_ = (uint8_t*)take(ne);
     dErr_ = (double*)take(sizeof(double) * 3 * ne);
-    dTerms_ = (double*)take(sizeof(double) * T_N * ne);
+    // also the landing place of the compact edge upload (upload_problem), expanded before any use
+    const size_t compactE = 4 * ((4 * ne + 7) / 8 * 8 / 4) * 2 + (12 * ne + 7) / 8 * 8 + (4 * ne + 7) / 8 * 8 +
+                            (20 * nkf + 7) / 8 * 8;
+    dTerms_ = (double*)take(std::max(sizeof(double) * T_N * ne, compactE));
     dRc_ = (double*)take(sizeof(double) * ne);
     dHpp_ = (double*)take(sizeof(double) * 21 * nkf);
     dBp_ = (double*)take(sizeof(double) * 6 * nkf);
@@ -3391,6 +3396,37 @@ int BaEngine::carve(bool commit, size_t* total) {
     tmpB1_ = (double*)take(sizeof(double) * tmpN);
     *total = off;
     return 0;
+}
+
+// The edges as the caller holds them (ba_problem: 24 B per edge, 20 B per keyframe camera) are
+// uploaded as they are and expanded into EdgeDev records (104 B) here: a quarter of the H2D
+// bytes and no host pass writing 104 B per edge into the pinned block.  Same conversions as a
+// host expansion would make (float -> double, the Huber deltas as (double)(float)sqrt(th)).
+__global__ void __launch_bounds__(256) k_expand_edges(int ne, const int32_t* __restrict__ ePt,
+                                                      const int32_t* __restrict__ eKf, const float* __restrict__ obs,
+                                                      const float* __restrict__ isig, const float* __restrict__ cam,
+                                                      float thMono, float thStereo, EdgeDev* __restrict__ E) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ne) return;
+    EdgeDev e;
+    e.pt = ePt[i];
+    e.kf = eKf[i];
+    const float o0 = obs[3 * i], o1 = obs[3 * i + 1], o2 = obs[3 * i + 2];
+    e.stereo = !(o2 < 0);
+    e.pad = 0;
+    e.obs[0] = (double)o0;
+    e.obs[1] = (double)o1;
+    e.obs[2] = (double)o2;
+    e.info = (double)isig[i];
+    const float* c = cam + 5 * e.kf;
+    e.fx = c[0];
+    e.fy = c[1];
+    e.cx = c[2];
+    e.cy = c[3];
+    e.bf = c[4];
+    e.delta = (double)(e.stereo ? thStereo : thMono);
+    e.dsqr = e.delta * e.delta;
+    E[i] = e;
 }
 
 // Host loops over large problems (a global BA's 1.5 M edges) on up to 16 threads, in contiguous
@@ -3441,14 +3477,19 @@ int BaEngine::upload_problem(const ba_problem* P) {
     for (int i = 0; i < ne_; i++) ptHasEdge_[P->edge_pt[i]] = 1;
     // poses, points and edges written straight into the pinned staging block (no intermediate
     // host copy), uploaded with one wait
-    const size_t bT = sizeof(Se3) * nkf_, bX = sizeof(double) * 3 * (size_t)npt_, bE = sizeof(EdgeDev) * ne_;
+    // edges compact (pt, kf, obs[3], invSigma2) + the keyframe cameras, 8-byte aligned parts
+    auto al8 = [](size_t b) { return (b + 7) & ~(size_t)7; };
+    const size_t bT = sizeof(Se3) * nkf_, bX = sizeof(double) * 3 * (size_t)npt_;
+    const size_t bEi = al8(sizeof(int32_t) * ne_), bEo = al8(sizeof(float) * 3 * ne_), bEs = al8(sizeof(float) * ne_),
+                 bCam = al8(sizeof(float) * 5 * nkf_);
+    const size_t bE = 2 * bEi + bEo + bEs + bCam;
     // + the static vertex data the device structure builder reads (fixed flags, mnIds)
     const size_t bF = ((size_t)nkf_ + 7) & ~(size_t)7, bK = sizeof(int32_t) * nkf_, bP = sizeof(int32_t) * npt_;
     if (int e = stage_reserve(bT + bX + bE + bF + bK + bP + 64)) return e;
     char* st = (char*)hStage_;
     Se3* Ts = reinterpret_cast<Se3*>(st);
     double* Xs = reinterpret_cast<double*>(st + bT);
-    EdgeDev* Es = reinterpret_cast<EdgeDev*>(st + bT + bX);
+    char* Es = st + bT + bX;
     char* sv = st + bT + bX + bE;
     std::memcpy(sv, kfFixed_.data(), nkf_);
     std::memcpy(sv + bF, P->kf_id, bK);
@@ -3458,26 +3499,23 @@ int BaEngine::upload_problem(const ba_problem* P) {
     // Huber deltas: LocalBundleAdjustment sqrt(5.991) (Optimizer.cc:585), BundleAdjustment sqrt(5.99) (:87)
     const float thMono = (float)std::sqrt(mode_.global ? 5.99 : 5.991), thStereo = (float)std::sqrt(7.815);
     host_parallel(ne_, [&](int a, int b) {
-        for (int i = a; i < b; i++) {
-            EdgeDev e;
-            std::memset(&e, 0, sizeof(e));
-            e.pt = P->edge_pt[i];
-            e.kf = P->edge_kf[i];
-            e.stereo = !(P->edge_obs[3 * i + 2] < 0);
-            for (int j = 0; j < 3; j++) e.obs[j] = (double)P->edge_obs[3 * i + j];
-            e.info = (double)P->edge_inv_sigma2[i];
-            const float* cam = P->kf_cam + 5 * e.kf;
-            e.fx = cam[0]; e.fy = cam[1]; e.cx = cam[2]; e.cy = cam[3]; e.bf = cam[4];
-            e.delta = (double)(e.stereo ? thStereo : thMono);
-            e.dsqr = e.delta * e.delta;
-            Es[i] = e;
-        }
+        std::memcpy(Es + sizeof(int32_t) * a, P->edge_pt + a, sizeof(int32_t) * (b - a));
+        std::memcpy(Es + bEi + sizeof(int32_t) * a, P->edge_kf + a, sizeof(int32_t) * (b - a));
+        std::memcpy(Es + 2 * bEi + sizeof(float) * 3 * (size_t)a, P->edge_obs + 3 * (size_t)a, sizeof(float) * 3 * (b - a));
+        std::memcpy(Es + 2 * bEi + bEo + sizeof(float) * a, P->edge_inv_sigma2 + a, sizeof(float) * (b - a));
     });
+    std::memcpy(Es + 2 * bEi + bEo + bEs, P->kf_cam, sizeof(float) * 5 * nkf_);
     level_.assign(ne_, 0);
     hipStream_t s = stream_;
     if (bT) ORB_HIP_CHECK(hipMemcpyAsync(dT_, st, bT, hipMemcpyHostToDevice, s));
     if (bX) ORB_HIP_CHECK(hipMemcpyAsync(dX_, st + bT, bX, hipMemcpyHostToDevice, s));
-    if (bE) ORB_HIP_CHECK(hipMemcpyAsync(dE_, st + bT + bX, bE, hipMemcpyHostToDevice, s));
+    if (ne_) {   // compact edges into dTerms_ (free until the first linearisation), expanded into dE_
+        char* cE = (char*)dTerms_;
+        ORB_HIP_CHECK(hipMemcpyAsync(cE, Es, bE, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_expand_edges, dim3((ne_ + 255) / 256), dim3(256), 0, s, ne_, (const int32_t*)cE,
+                           (const int32_t*)(cE + bEi), (const float*)(cE + 2 * bEi), (const float*)(cE + 2 * bEi + bEo),
+                           (const float*)(cE + 2 * bEi + bEo + bEs), thMono, thStereo, dE_);
+    }
     if (nkf_) ORB_HIP_CHECK(hipMemcpyAsync(dKfFixed_, sv, nkf_, hipMemcpyHostToDevice, s));
     if (bK) ORB_HIP_CHECK(hipMemcpyAsync(dKfId_, sv + bF, bK, hipMemcpyHostToDevice, s));
     if (bP) ORB_HIP_CHECK(hipMemcpyAsync(dPtId_, sv + bF + bK, bP, hipMemcpyHostToDevice, s));
@@ -4150,6 +4188,8 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
     hLm_[1] = 0;
     hLm_[2] = 0;
     hLm_[3] = 0;
+    hLm_[4] = 0;
+    hLm_[5] = 0;
     hipLaunchKernelGGL(k_lm_begin, dim3(1), dim3(64), 0, stream_, dLm_, iterations);
     // at most 10 trials per iteration; the host stays one step ahead of the decisions.  It learns
     // of them from the words k_lm_trial_end writes to host memory ([2] steps decided, [1] done), not
@@ -4161,9 +4201,16 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
         return e && e[0] == '1';
     }();
     volatile int* hw = (volatile int*)hLm_;
+    static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;   // host enqueue / wait split (tools/)
+    using sclk = std::chrono::steady_clock;
+    double tEnq = 0, tWait = 0;
+    int nSteps = 0;
     for (int j = 0; j < maxSteps; j++) {
+        const auto q0 = sclk::now();
         enqueue_lm_step(j == 0);
         ORB_HIP_CHECK(hipGetLastError());
+        const auto q1 = sclk::now();
+        nSteps++;
         if (useEvents) {
             ORB_HIP_CHECK(hipEventRecord(lmEv_[j & 1], stream_));
             if (j >= 1) {
@@ -4171,16 +4218,33 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
                 if (hw[1]) break;
             }
         } else if (j >= 1) {
-            // step j - 1 decided (steps >= j) or the run over; a drained stream ends the wait too
-            // (its writes are all visible then, and the final readback below checks the state)
-            for (unsigned spin = 1; hw[2] < j && !hw[1]; spin++) {
-                if ((spin & 255) == 0 && hipStreamQuery(stream_) == hipSuccess) break;
+            // step j - 1 decided (steps >= j) or the run over.  No HIP call inside the wait: a
+            // stream query or event sync makes the runtime fence the next launch (a ~5 us idle
+            // gap on the queue after every trial).  Only a wait past 50 ms asks whether the stream
+            // drained (its writes are all visible then; the final readback checks the state).
+            const auto w0 = sclk::now();
+            volatile unsigned long long* hw64 = (volatile unsigned long long*)(hLm_ + 4);   // (done, steps)
+            for (unsigned spin = 1;; spin++) {
+                const unsigned long long v = *hw64;
+                if ((int)(v >> 32) >= j || (v & 0xffffffffu)) break;
+                if ((spin & 4095) == 0 && sclk::now() - w0 > std::chrono::milliseconds(50) &&
+                    hipStreamQuery(stream_) == hipSuccess)
+                    break;
                 __builtin_ia32_pause();
             }
-            if (hw[1]) break;
+            if ((*hw64 & 0xffffffffu) || hw[1]) {
+                tEnq += std::chrono::duration<double, std::micro>(q1 - q0).count();
+                tWait += std::chrono::duration<double, std::micro>(sclk::now() - q1).count();
+                break;
+            }
         }
+        tEnq += std::chrono::duration<double, std::micro>(q1 - q0).count();
+        tWait += std::chrono::duration<double, std::micro>(sclk::now() - q1).count();
         hLm_[0] = stopped(stop) ? 1 : 0;
     }
+    if (say)
+        fprintf(stderr, "[ba]   LM steps queued %d: host enqueue %.1f us/step, wait %.1f us/step\n", nSteps,
+                tEnq / nSteps, tWait / nSteps);
     LmDev h;
     if (int e = d2h_sync(&h, dLm_, sizeof(LmDev))) return e;   // also drains the queue
     if (!h.done) return -7;    // the step bound is the trial bound: unreachable

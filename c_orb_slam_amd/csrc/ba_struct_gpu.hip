@@ -42,6 +42,13 @@ enum Sc { C_NE, C_NP, C_NL, C_NPAIR, C_NLP, C_NPE, C_NLE, C_ERR, C_MAXPE, C_MAXL
 constexpr int kT = 256;
 inline unsigned nb(long long n) { return (unsigned)std::max<long long>(1, (n + kT - 1) / kT); }
 
+// Counters and maxima over many threads into one word: one atomic per wave (a wave-wide max / sum
+// first), not one per thread -- thousands of same-address atomics serialise at the L2.
+__device__ __forceinline__ int wave_max_i(int v) {
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
 __global__ void k_gs_active(int ne, const EdgeDev* __restrict__ E, const uint8_t* __restrict__ lv, int level,
                             int* flag, int* kfAct, int* ptAct) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -68,11 +75,13 @@ __global__ void k_gs_d_to_act(int n, const double* d, int* a) {
 __global__ void k_gs_vkeys(int n, const int* act, const uint8_t* fixed, const int32_t* id, unsigned long long* key,
                            int* idx, int* sc, int slot) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const bool a = act[k] && !(fixed && fixed[k]);
-    key[k] = (a ? 0ull : (1ull << 32)) | (unsigned long long)((uint32_t)id[k] ^ 0x80000000u);
-    idx[k] = k;
-    if (a) atomicAdd(sc + slot, 1);
+    const bool a = k < n && act[k] && !(fixed && fixed[k]);
+    if (k < n) {
+        key[k] = (a ? 0ull : (1ull << 32)) | (unsigned long long)((uint32_t)id[k] ^ 0x80000000u);
+        idx[k] = k;
+    }
+    const int c = __popcll(__ballot(a));
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(sc + slot, c);
 }
 
 __global__ void k_gs_index(int n, const int* __restrict__ sc, int slot, const int* __restrict__ sorted, int* map) {
@@ -115,8 +124,12 @@ __global__ void k_gs_counts(int npt, int nkf, const int* __restrict__ sc_in, con
         const long long m = i < nL ? lpCnt[i] : 0;
         tc[i] = m * (m + 1) / 2;
     }
-    if (i < nL) atomicMax(sc + C_MAXLE, leCnt[i]);
-    if (i < nP && i < nkf) atomicMax(sc + C_MAXPE, peCnt[i]);
+    const int le = wave_max_i(i < nL ? leCnt[i] : 0);
+    const int pe = wave_max_i(i < nP && i < nkf ? peCnt[i] : 0);
+    if ((threadIdx.x & 63) == 0) {
+        if (le) atomicMax(sc + C_MAXLE, le);
+        if (pe) atomicMax(sc + C_MAXPE, pe);
+    }
 }
 
 // one (pose, landmark) pair per edge: adjacent equal (landmark, pose) keys are an error
@@ -186,7 +199,8 @@ __global__ void k_gs_blocks(int nPair, int nkf, int nP, const unsigned long long
     const int pu = (int)(k[i] / (unsigned long long)nkf), pv = (int)(k[i] % (unsigned long long)nkf);
     const int b = pu == pv ? pu : nP + rank[st[s0]];
     bOf[i] = b;
-    atomicAdd(&bCnt[b], 1);
+    // a block's terms are one segment of the sorted keys: its last term stores the count
+    if (i + 1 == nPair || k[i + 1] != k[i]) bCnt[b] = i - s0 + 1;
     if (i == s0) {
         blkI[b] = pu;
         blkJ[b] = pv;
@@ -205,7 +219,8 @@ __global__ void k_gs_fill(int nPair, const int* __restrict__ st, const int* __re
 
 __global__ void k_gs_blkmax(int nBlk, const int* __restrict__ bCnt, int* sc) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nBlk) atomicMax(sc + C_MAXBLK, bCnt[b]);
+    const int m = wave_max_i(b < nBlk ? bCnt[b] : 0);
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(sc + C_MAXBLK, m);
 }
 
 __global__ void k_gs_offkey(int nOffMax, const int* __restrict__ sc, const unsigned long long* __restrict__ k, int nkf,

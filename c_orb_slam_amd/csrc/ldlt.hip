@@ -33,7 +33,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -908,6 +911,15 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     const int ng = (n + g - 1) / g;
     if ((int)adjStart.size() != ng + 1) return -1;
     auto gsz = [&](int q) { return std::min(g, n - q * g); };
+    static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;   // the build's phases (tools/)
+    auto ts0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!say) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[ba]     ldlt build: %s %.0f us\n", what,
+                std::chrono::duration<double, std::micro>(t - ts0).count());
+        ts0 = t;
+    };
     // ---- order and tile space
     NdTree tree;
     if (nd) {
@@ -920,6 +932,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
         tree.parent = {-1};
         tree.height = {0};
     }
+    lap("nested dissection");
     const int nnode = (int)tree.start.size();
     nd_ = nd;
     dist_ = false;
@@ -976,6 +989,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
         }
         if ((int)r.size() - 1 > kMaxRow) return -3;
     }
+    lap("tile pattern + symbolic");
     // slots: the Schur pattern first (the exchanged prefix), then the fill-in
     hSlotOf_.assign((size_t)nt * nt, -1);
     int ns = 0;
@@ -1097,6 +1111,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     for (int q : levNodes)
         if (q < 0 || q >= nnode) return -1;
     nUpd_ = (long long)kps.size();
+    lap("slots + schedule");
     // ---- device storage (grow-only)
     const size_t tileB = sizeof(double) * LT * LT;
     size_t off = 0;
@@ -1178,6 +1193,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     ORB_HIP_CHECK(hipMemcpyAsync(prow_, hProw_.data(), sizeof(int) * hProw_.size(), hipMemcpyHostToDevice, s));
     ORB_HIP_CHECK(hipMemcpyAsync(lists_, L.data(), sizeof(int) * L.size(), hipMemcpyHostToDevice, s));
     ORB_HIP_CHECK(hipStreamSynchronize(s));   // pageable sources
+    lap("lists + upload");
     return 0;
 }
 
