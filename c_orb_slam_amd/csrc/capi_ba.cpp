@@ -38,6 +38,9 @@ int validate(const ba_problem* P, const ba_result* R) {
     // (ids sorted by an LSD radix sort of the sign-flipped keys, three 11-bit passes: O(n))
     auto distinct = [](const int32_t* v, int n) {
         if (n < 2) return true;
+        int i0 = 1;   // ids in ascending order (the usual mnId order): distinct by one scan
+        while (i0 < n && v[i0 - 1] < v[i0]) i0++;
+        if (i0 == n) return true;
         std::vector<uint32_t> c(n), t(n);
         for (int i = 0; i < n; i++) c[i] = (uint32_t)v[i] ^ 0x80000000u;
         uint32_t cnt[2048];
@@ -56,6 +59,28 @@ int validate(const ba_problem* P, const ba_result* R) {
         return std::adjacent_find(c.begin(), c.end()) == c.end();
     };
     if (!distinct(P->kf_id, P->n_kf) || !distinct(P->pt_id, P->n_pt)) return ORB_E_INVALID;
+    if (P->n_kf > 32768) return ORB_E_CAPACITY;   // block-sparse pose system: tile map (n_kf / 10.7)^2 ints
+    {   // the Optimizer adds each map point's edges together (Optimizer.cc:99-160, 536-627): then one
+        // pass with a keyframe stamp per run of equal points checks the pairs; a point met in two
+        // runs falls through to the bucketing below
+        std::vector<uint8_t> seen(std::max(P->n_pt, 1), 0);
+        std::vector<int32_t> stamp(std::max(P->n_kf, 1), -1);
+        int32_t cur = -1, run = -1;
+        int i = 0;
+        for (; i < P->n_edge; i++) {
+            const int32_t pt = P->edge_pt[i], kf = P->edge_kf[i];
+            if (pt < 0 || pt >= P->n_pt || kf < 0 || kf >= P->n_kf) return ORB_E_INVALID;
+            if (pt != cur) {
+                if (seen[pt]) break;
+                seen[pt] = 1;
+                cur = pt;
+                run++;
+            }
+            if (stamp[kf] == run) return ORB_E_INVALID;
+            stamp[kf] = run;
+        }
+        if (i == P->n_edge) return ORB_OK;
+    }
     std::vector<int32_t> start((size_t)P->n_pt + 1, 0);
     for (int i = 0; i < P->n_edge; i++) {
         const int32_t pt = P->edge_pt[i], kf = P->edge_kf[i];
@@ -71,7 +96,6 @@ int validate(const ba_problem* P, const ba_result* R) {
             if (stamp[kfs[j]] == p) return ORB_E_INVALID;
             stamp[kfs[j]] = p;
         }
-    if (P->n_kf > 32768) return ORB_E_CAPACITY;   // block-sparse pose system: tile map (n_kf / 10.7)^2 ints
     return ORB_OK;
 }
 
