@@ -535,9 +535,7 @@ __global__ void __launch_bounds__(kSysThreads) k_pose_reduce(BaStructDev s, cons
 // per (landmark, entry): Hll (full 3x3) and b_l over the landmark's active edges (edge order)
 __global__ void __launch_bounds__(256) k_land_reduce(BaStructDev s, const double* __restrict__ terms, double* Hll,
                                                      double* bl, const int* run);
-__device__ __forceinline__ void land_reduce_thread(const BaStructDev& s, const double* __restrict__ terms, double* Hll,
-                                                   double* bl, int g) {
-    if (g >= 12 * s.nL) return;
+__device__ __forceinline__ double land_reduce_value(const BaStructDev& s, const double* __restrict__ terms, int g) {
     const int l = g / 12, q = g % 12;
     const int s0 = s.leStart[l], n = s.leStart[l + 1] - s0;
     const int col = q < 9 ? T_HLL + q : T_BL + (q - 9);
@@ -569,6 +567,13 @@ __device__ __forceinline__ void land_reduce_thread(const BaStructDev& s, const d
             v = u;
         }
     }
+    return v;
+}
+__device__ __forceinline__ void land_reduce_thread(const BaStructDev& s, const double* __restrict__ terms, double* Hll,
+                                                   double* bl, int g) {
+    if (g >= 12 * s.nL) return;
+    const int l = g / 12, q = g % 12;
+    const double v = land_reduce_value(s, terms, g);
     if (q < 9) Hll[9 * l + q] = v;
     else bl[3 * l + (q - 9)] = v;
 }
@@ -614,7 +619,22 @@ __device__ __forceinline__ double lam_of(double lam_host, int use_dev, const dou
     return use_dev ? scal[5] : lam_host;
 }
 
-// per active edge with a free pose: BDinv = Hpl Dinv and B (Dinv b_l)  (block_solver.hpp:376-404)
+// per active edge with a free pose: BDinv = Hpl Dinv and B (Dinv b_l)  (block_solver.hpp:376-404);
+// H9 / b3: the landmark's Hll and b_l, a: the edge's pose-list position
+__device__ __forceinline__ void prep_entry(const double* H9, const double* b3, double lambda,
+                                           const double* __restrict__ Hpl, int a, double* Emat, double* cb) {
+    double Di[9], d[3];
+    land_dinv(H9, 0, lambda, Di);
+    const double b[3] = {b3[0], b3[1], b3[2]};
+    for (int r = 0; r < 3; r++) d[r] = (Di[r * 3] * b[0] + Di[r * 3 + 1] * b[1]) + Di[r * 3 + 2] * b[2];
+    const double* Bi = Hpl + 18 * (size_t)a;
+    for (int r = 0; r < 6; r++) {
+        const double b0 = Bi[r * 3], b1 = Bi[r * 3 + 1], b2 = Bi[r * 3 + 2];
+        for (int k = 0; k < 3; k++) Emat[18 * (size_t)a + r * 3 + k] = (b0 * Di[k] + b1 * Di[3 + k]) + b2 * Di[6 + k];
+        cb[6 * (size_t)a + r] = (b0 * d[0] + b1 * d[1]) + b2 * d[2];
+    }
+}
+
 __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double* Hll, const double* bl,
                                                     const double* __restrict__ Hpl, double lam_host, int use_dev,
                                                     const double* scal, double* Emat, double* cb, const int* run) {
@@ -622,16 +642,51 @@ __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double*
     const int a = blockIdx.x * blockDim.x + threadIdx.x;   // pose-list position
     if (a >= s.nPe) return;
     const int l = s.eLand[s.peList[a]];
-    const double lambda = lam_of(lam_host, use_dev, scal);
-    double Di[9], d[3];
-    land_dinv(Hll, l, lambda, Di);
-    const double b[3] = {bl[3 * l], bl[3 * l + 1], bl[3 * l + 2]};
-    for (int r = 0; r < 3; r++) d[r] = (Di[r * 3] * b[0] + Di[r * 3 + 1] * b[1]) + Di[r * 3 + 2] * b[2];
-    const double* Bi = Hpl + 18 * (size_t)a;
-    for (int r = 0; r < 6; r++) {
-        const double b0 = Bi[r * 3], b1 = Bi[r * 3 + 1], b2 = Bi[r * 3 + 2];
-        for (int k = 0; k < 3; k++) Emat[18 * (size_t)a + r * 3 + k] = (b0 * Di[k] + b1 * Di[3 + k]) + b2 * Di[6 + k];
-        cb[6 * (size_t)a + r] = (b0 * d[0] + b1 * d[1]) + b2 * d[2];
+    prep_entry(Hll + 9 * l, bl + 3 * l, lam_of(lam_host, use_dev, scal), Hpl, a, Emat, cb);
+}
+
+// The device LM's steps after the first (lambda already on the device): buildSystem's reductions
+// and k_point_prep in one launch.  Blocks [0, nP) reduce a pose each (system gate ctl[1]); each
+// later block reduces kLandBlk whole landmarks (12 threads per landmark, ctl[1]) and then, under
+// the trial gate ctl[0], preps the pose-list entries of those landmarks (their lpList edges) from
+// the values it just reduced -- or, on a rejected trial's step (system gated off), from Hll / b_l
+// as the last system left them.  Same values as k_sys_reduce + k_point_prep.
+constexpr int kLandBlk = kSysThreads / 12;
+__global__ void __launch_bounds__(kSysThreads) k_sys_reduce_prep(BaStructDev s, const double* __restrict__ terms,
+                                                                 double* Hpp, double* bp, double* Hll, double* bl,
+                                                                 const double* __restrict__ Hpl, const double* scal,
+                                                                 double* Emat, double* cb, const int* ctl) {
+    __shared__ double sH[kLandBlk * 9], sB[kLandBlk * 3];
+    const bool sys = ctl[1] != 0, trial = ctl[0] != 0;
+    if (!sys && !trial) return;
+    if ((int)blockIdx.x < s.nP) {
+        if (sys) pose_reduce_block(s, terms, Hpp, bp, blockIdx.x);
+        return;
+    }
+    const int l0 = ((int)blockIdx.x - s.nP) * kLandBlk, l1 = min(s.nL, l0 + kLandBlk);
+    const int t = threadIdx.x;
+    if (sys && t < 12 * kLandBlk) {
+        const int g = 12 * l0 + t;
+        if (g < 12 * l1) {
+            const int l = g / 12, q = g % 12;
+            const double v = land_reduce_value(s, terms, g);
+            if (q < 9) {
+                Hll[9 * l + q] = v;
+                sH[9 * (l - l0) + q] = v;
+            } else {
+                bl[3 * l + (q - 9)] = v;
+                sB[3 * (l - l0) + (q - 9)] = v;
+            }
+        }
+    }
+    if (!trial) return;
+    __syncthreads();
+    const double lambda = scal[5];
+    for (int j = s.lpStart[l0] + t; j < s.lpStart[l1]; j += blockDim.x) {
+        const int e = s.lpList[j], l = s.eLand[e];
+        const double* H9 = sys ? sH + 9 * (l - l0) : Hll + 9 * l;
+        const double* b3 = sys ? sB + 3 * (l - l0) : bl + 3 * l;
+        prep_entry(H9, b3, lambda, Hpl, s.pePos[e], Emat, cb);
     }
 }
 
@@ -3340,6 +3395,25 @@ bool BaEngine::dense_solver(int n) const {
 }
 
 // Carve every device buffer of the problem out of one grow-only arena.
+struct UploadLayout {   // byte offsets in the staging span (all 8-byte aligned)
+    size_t oT, oX, oPt, oKf, oObs, oIs, oCam, oFx, oKid, oPid, total;
+};
+static UploadLayout upload_layout(size_t ne, size_t nkf, size_t npt) {
+    auto al8 = [](size_t b) { return (b + 7) & ~(size_t)7; };
+    UploadLayout L;
+    L.oT = 0;
+    L.oX = L.oT + sizeof(Se3) * nkf;
+    L.oPt = L.oX + sizeof(double) * 3 * npt;
+    L.oKf = L.oPt + al8(sizeof(int32_t) * ne);
+    L.oObs = L.oKf + al8(sizeof(int32_t) * ne);
+    L.oIs = L.oObs + al8(sizeof(float) * 3 * ne);
+    L.oCam = L.oIs + al8(sizeof(float) * ne);
+    L.oFx = L.oCam + al8(sizeof(float) * 5 * nkf);
+    L.oKid = L.oFx + al8(nkf);
+    L.oPid = L.oKid + al8(sizeof(int32_t) * nkf);
+    L.total = L.oPid + al8(sizeof(int32_t) * npt);
+    return L;
+}
 int BaEngine::carve(bool commit, size_t* total) {
     const size_t ne = (size_t)std::max(ne_, 1), nkf = (size_t)std::max(nkf_, 1), npt = (size_t)std::max(npt_, 1);
     scratchN_ = 6 * nkf + 3 * npt + ne + 64;
@@ -3359,10 +3433,8 @@ int BaEngine::carve(bool commit, size_t* total) {
     dLevel_ = (uint8_t*)take(ne);
     dRobust_ = (uint8_t*)take(ne);
     dErr_ = (double*)take(sizeof(double) * 3 * ne);
-    // also the landing place of the compact edge upload (upload_problem), expanded before any use
-    const size_t compactE = 4 * ((4 * ne + 7) / 8 * 8 / 4) * 2 + (12 * ne + 7) / 8 * 8 + (4 * ne + 7) / 8 * 8 +
-                            (20 * nkf + 7) / 8 * 8;
-    dTerms_ = (double*)take(std::max(sizeof(double) * T_N * ne, compactE));
+    // also the landing place of the problem's upload (upload_problem), unpacked before any use
+    dTerms_ = (double*)take(std::max(sizeof(double) * T_N * ne, upload_layout(ne, nkf, npt).total));
     dRc_ = (double*)take(sizeof(double) * ne);
     dHpp_ = (double*)take(sizeof(double) * 21 * nkf);
     dBp_ = (double*)take(sizeof(double) * 6 * nkf);
@@ -3398,35 +3470,68 @@ int BaEngine::carve(bool commit, size_t* total) {
     return 0;
 }
 
-// The edges as the caller holds them (ba_problem: 24 B per edge, 20 B per keyframe camera) are
-// uploaded as they are and expanded into EdgeDev records (104 B) here: a quarter of the H2D
-// bytes and no host pass writing 104 B per edge into the pinned block.  Same conversions as a
-// host expansion would make (float -> double, the Huber deltas as (double)(float)sqrt(th)).
-__global__ void __launch_bounds__(256) k_expand_edges(int ne, const int32_t* __restrict__ ePt,
-                                                      const int32_t* __restrict__ eKf, const float* __restrict__ obs,
-                                                      const float* __restrict__ isig, const float* __restrict__ cam,
-                                                      float thMono, float thStereo, EdgeDev* __restrict__ E) {
+// The problem as the caller holds it goes up in ONE H2D copy of the pinned staging block (poses
+// as Se3, points as doubles, the edges compact: 24 B per edge and 20 B per keyframe camera, the
+// vertex flags and ids) and one kernel unpacks it: the EdgeDev records (104 B) expanded here, a
+// quarter of the H2D bytes of host-expanded records, and the per-edge state initialised in the same
+// pass -- one copy and one launch instead of six copies and four fills on the queue.  Same
+// conversions as a host expansion (float -> double, the Huber deltas as (double)(float)sqrt(th)).
+__global__ void __launch_bounds__(256) k_zero2(double* a, size_t na, double* b, size_t nb) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < na) a[i] = 0.0;
+    if (i < nb) b[i] = 0.0;
+}
+
+struct UploadArgs {
+    const char* src;
+    UploadLayout L;
+    int ne, nkf, npt;
+    float thMono, thStereo;
+    int robust;
+    Se3* T;
+    double* X;
+    EdgeDev* E;
+    uint8_t *kfFixed, *level, *robustFlag;
+    int32_t *kfId, *ptId;
+    double* err;
+    unsigned* counter;
+};
+__global__ void __launch_bounds__(256) k_unpack_upload(UploadArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ne) return;
-    EdgeDev e;
-    e.pt = ePt[i];
-    e.kf = eKf[i];
-    const float o0 = obs[3 * i], o1 = obs[3 * i + 1], o2 = obs[3 * i + 2];
-    e.stereo = !(o2 < 0);
-    e.pad = 0;
-    e.obs[0] = (double)o0;
-    e.obs[1] = (double)o1;
-    e.obs[2] = (double)o2;
-    e.info = (double)isig[i];
-    const float* c = cam + 5 * e.kf;
-    e.fx = c[0];
-    e.fy = c[1];
-    e.cx = c[2];
-    e.cy = c[3];
-    e.bf = c[4];
-    e.delta = (double)(e.stereo ? thStereo : thMono);
-    e.dsqr = e.delta * e.delta;
-    E[i] = e;
+    const UploadLayout& L = a.L;
+    if (i < a.ne) {
+        const float* obs = (const float*)(a.src + L.oObs);
+        EdgeDev e;
+        e.pt = ((const int32_t*)(a.src + L.oPt))[i];
+        e.kf = ((const int32_t*)(a.src + L.oKf))[i];
+        const float o0 = obs[3 * i], o1 = obs[3 * i + 1], o2 = obs[3 * i + 2];
+        e.stereo = !(o2 < 0);
+        e.pad = 0;
+        e.obs[0] = (double)o0;
+        e.obs[1] = (double)o1;
+        e.obs[2] = (double)o2;
+        e.info = (double)((const float*)(a.src + L.oIs))[i];
+        const float* c = (const float*)(a.src + L.oCam) + 5 * e.kf;
+        e.fx = c[0];
+        e.fy = c[1];
+        e.cx = c[2];
+        e.cy = c[3];
+        e.bf = c[4];
+        e.delta = (double)(e.stereo ? a.thStereo : a.thMono);
+        e.dsqr = e.delta * e.delta;
+        a.E[i] = e;
+        a.level[i] = 0;
+        a.robustFlag[i] = (uint8_t)a.robust;
+        for (int k = 0; k < 3; k++) a.err[3 * i + k] = 0.0;
+    }
+    if (i < 8 * a.nkf) ((double*)a.T)[i] = ((const double*)(a.src + L.oT))[i];
+    if (i < 3 * a.npt) a.X[i] = ((const double*)(a.src + L.oX))[i];
+    if (i < a.nkf) {
+        a.kfFixed[i] = ((const uint8_t*)(a.src + L.oFx))[i];
+        a.kfId[i] = ((const int32_t*)(a.src + L.oKid))[i];
+    }
+    if (i < a.npt) a.ptId[i] = ((const int32_t*)(a.src + L.oPid))[i];
+    if (i < 16) a.counter[i] = 0;
 }
 
 // Host loops over large problems (a global BA's 1.5 M edges) on up to 16 threads, in contiguous
@@ -3475,56 +3580,51 @@ int BaEngine::upload_problem(const ba_problem* P) {
     if (mode_.global) kfLocal_.assign(nkf_, 1);
     ptHasEdge_.assign(npt_, 0);
     for (int i = 0; i < ne_; i++) ptHasEdge_[P->edge_pt[i]] = 1;
-    // poses, points and edges written straight into the pinned staging block (no intermediate
-    // host copy), uploaded with one wait
-    // edges compact (pt, kf, obs[3], invSigma2) + the keyframe cameras, 8-byte aligned parts
-    auto al8 = [](size_t b) { return (b + 7) & ~(size_t)7; };
-    const size_t bT = sizeof(Se3) * nkf_, bX = sizeof(double) * 3 * (size_t)npt_;
-    const size_t bEi = al8(sizeof(int32_t) * ne_), bEo = al8(sizeof(float) * 3 * ne_), bEs = al8(sizeof(float) * ne_),
-                 bCam = al8(sizeof(float) * 5 * nkf_);
-    const size_t bE = 2 * bEi + bEo + bEs + bCam;
-    // + the static vertex data the device structure builder reads (fixed flags, mnIds)
-    const size_t bF = ((size_t)nkf_ + 7) & ~(size_t)7, bK = sizeof(int32_t) * nkf_, bP = sizeof(int32_t) * npt_;
-    if (int e = stage_reserve(bT + bX + bE + bF + bK + bP + 64)) return e;
+    // poses, points, compact edges and vertex data written straight into the pinned staging block
+    // (no intermediate host copy): one H2D copy, unpacked by k_unpack_upload
+    const UploadLayout UL = upload_layout(ne_, nkf_, npt_);
+    if (int e = stage_reserve(UL.total + 64)) return e;
     char* st = (char*)hStage_;
-    Se3* Ts = reinterpret_cast<Se3*>(st);
-    double* Xs = reinterpret_cast<double*>(st + bT);
-    char* Es = st + bT + bX;
-    char* sv = st + bT + bX + bE;
-    std::memcpy(sv, kfFixed_.data(), nkf_);
-    std::memcpy(sv + bF, P->kf_id, bK);
-    std::memcpy(sv + bF + bK, P->pt_id, bP);
+    Se3* Ts = reinterpret_cast<Se3*>(st + UL.oT);
+    double* Xs = reinterpret_cast<double*>(st + UL.oX);
+    std::memcpy(st + UL.oFx, kfFixed_.data(), nkf_);
+    std::memcpy(st + UL.oKid, P->kf_id, sizeof(int32_t) * nkf_);
+    std::memcpy(st + UL.oPid, P->pt_id, sizeof(int32_t) * npt_);
+    std::memcpy(st + UL.oCam, P->kf_cam, sizeof(float) * 5 * nkf_);
     for (int k = 0; k < nkf_; k++) host_se3_from_Tcw(P->kf_Tcw + 16 * k, Ts[k]);
     for (size_t q = 0; q < 3 * (size_t)npt_; q++) Xs[q] = (double)P->pt_pos[q];
-    // Huber deltas: LocalBundleAdjustment sqrt(5.991) (Optimizer.cc:585), BundleAdjustment sqrt(5.99) (:87)
-    const float thMono = (float)std::sqrt(mode_.global ? 5.99 : 5.991), thStereo = (float)std::sqrt(7.815);
     host_parallel(ne_, [&](int a, int b) {
-        std::memcpy(Es + sizeof(int32_t) * a, P->edge_pt + a, sizeof(int32_t) * (b - a));
-        std::memcpy(Es + bEi + sizeof(int32_t) * a, P->edge_kf + a, sizeof(int32_t) * (b - a));
-        std::memcpy(Es + 2 * bEi + sizeof(float) * 3 * (size_t)a, P->edge_obs + 3 * (size_t)a, sizeof(float) * 3 * (b - a));
-        std::memcpy(Es + 2 * bEi + bEo + sizeof(float) * a, P->edge_inv_sigma2 + a, sizeof(float) * (b - a));
+        std::memcpy(st + UL.oPt + sizeof(int32_t) * a, P->edge_pt + a, sizeof(int32_t) * (b - a));
+        std::memcpy(st + UL.oKf + sizeof(int32_t) * a, P->edge_kf + a, sizeof(int32_t) * (b - a));
+        std::memcpy(st + UL.oObs + sizeof(float) * 3 * (size_t)a, P->edge_obs + 3 * (size_t)a, sizeof(float) * 3 * (b - a));
+        std::memcpy(st + UL.oIs + sizeof(float) * a, P->edge_inv_sigma2 + a, sizeof(float) * (b - a));
     });
-    std::memcpy(Es + 2 * bEi + bEo + bEs, P->kf_cam, sizeof(float) * 5 * nkf_);
     level_.assign(ne_, 0);
     hipStream_t s = stream_;
-    if (bT) ORB_HIP_CHECK(hipMemcpyAsync(dT_, st, bT, hipMemcpyHostToDevice, s));
-    if (bX) ORB_HIP_CHECK(hipMemcpyAsync(dX_, st + bT, bX, hipMemcpyHostToDevice, s));
-    if (ne_) {   // compact edges into dTerms_ (free until the first linearisation), expanded into dE_
-        char* cE = (char*)dTerms_;
-        ORB_HIP_CHECK(hipMemcpyAsync(cE, Es, bE, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_expand_edges, dim3((ne_ + 255) / 256), dim3(256), 0, s, ne_, (const int32_t*)cE,
-                           (const int32_t*)(cE + bEi), (const float*)(cE + 2 * bEi), (const float*)(cE + 2 * bEi + bEo),
-                           (const float*)(cE + 2 * bEi + bEo + bEs), thMono, thStereo, dE_);
-    }
-    if (nkf_) ORB_HIP_CHECK(hipMemcpyAsync(dKfFixed_, sv, nkf_, hipMemcpyHostToDevice, s));
-    if (bK) ORB_HIP_CHECK(hipMemcpyAsync(dKfId_, sv + bF, bK, hipMemcpyHostToDevice, s));
-    if (bP) ORB_HIP_CHECK(hipMemcpyAsync(dPtId_, sv + bF + bK, bP, hipMemcpyHostToDevice, s));
-    if (ne_) {
-        ORB_HIP_CHECK(hipMemsetAsync(dLevel_, 0, ne_, s));
-        ORB_HIP_CHECK(hipMemsetAsync(dRobust_, (mode_.global && !mode_.robust) ? 0 : 1, ne_, s));
-        ORB_HIP_CHECK(hipMemsetAsync(dErr_, 0, sizeof(double) * 3 * ne_, s));
-    }
-    ORB_HIP_CHECK(hipMemsetAsync(dCounter_, 0, sizeof(unsigned) * 16, s));
+    char* dst = (char*)dTerms_;   // free until the first linearisation
+    ORB_HIP_CHECK(hipMemcpyAsync(dst, st, UL.total, hipMemcpyHostToDevice, s));
+    UploadArgs ua;
+    ua.src = dst;
+    ua.L = UL;
+    ua.ne = ne_;
+    ua.nkf = nkf_;
+    ua.npt = npt_;
+    // Huber deltas: LocalBundleAdjustment sqrt(5.991) (Optimizer.cc:585), BundleAdjustment sqrt(5.99) (:87)
+    ua.thMono = (float)std::sqrt(mode_.global ? 5.99 : 5.991);
+    ua.thStereo = (float)std::sqrt(7.815);
+    ua.robust = (mode_.global && !mode_.robust) ? 0 : 1;
+    ua.T = dT_;
+    ua.X = dX_;
+    ua.E = dE_;
+    ua.kfFixed = dKfFixed_;
+    ua.level = dLevel_;
+    ua.robustFlag = dRobust_;
+    ua.kfId = dKfId_;
+    ua.ptId = dPtId_;
+    ua.err = dErr_;
+    ua.counter = dCounter_;
+    const long long nthr = std::max<long long>({(long long)ne_, 8LL * nkf_, 3LL * npt_, 16LL});
+    hipLaunchKernelGGL(k_unpack_upload, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, ua);
     // no wait here: the host builds the structure while the copies run; the next user of the
     // staging block (stage_reserve) waits for them
     uploadPending_ = true;
@@ -3819,8 +3919,11 @@ int BaEngine::build_structure(int level) {
         if (h2d_sync(dTiles_, tl.data(), sizeof(int2) * tl.size())) return -2;
         ORB_HIP_CHECK(hipStreamSynchronize(stream_));
     }
-    ORB_HIP_CHECK(hipMemsetAsync(dX2_, 0, sizeof(double) * (6 * (size_t)nP + 3 * (size_t)nL + 1), stream_));
-    if (!tiled_) ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * 36 * (size_t)nP * nP + 8, stream_));
+    {   // the step vector and (dense solvers) S zeroed in one launch
+        const size_t nx = 6 * (size_t)nP + 3 * (size_t)nL + 1, ns = tiled_ ? 0 : 36 * (size_t)nP * nP + 1;
+        const size_t nz = std::max(nx, ns);
+        hipLaunchKernelGGL(k_zero2, dim3((unsigned)((nz + 255) / 256)), dim3(256), 0, stream_, dX2_, nx, dS_, ns);
+    }
     // (the structure's copy reads its own staging block, whose next user waits for it; kernels
     // queued after this are stream-ordered behind every copy and memset above)
     lap("queued");
@@ -4099,6 +4202,15 @@ static bool lm_host_forced() {
     return v;
 }
 
+// ORBGPU_FUSED_PREP=0 keeps k_sys_reduce + k_point_prep on every step (A/B)
+static bool fused_prep() {
+    static const bool v = [] {
+        const char* e = std::getenv("ORBGPU_FUSED_PREP");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // A one-rank group has no exchange (every all-reduce is the identity), so its sharded call is the
 // unsharded call and takes the same device LM.  With more ranks the trial's all-reduces sit
 // between the device steps: the host loop keeps them in order.
@@ -4122,8 +4234,17 @@ void BaEngine::enqueue_lm_step(bool first) {
         hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
         if (!fuse) hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
     }
-    if (nP + nL) hipLaunchKernelGGL(k_sys_reduce, dim3(nP + nblk(12 * nL, kSysThreads)), dim3(kSysThreads), 0, s, S, dTerms_, dHpp_,
-                                    dBp_, dHll_, dBl_, ctl + 1);
+    // the first step computes lambda from the reduced system (k_lambda_init) before the point prep;
+    // later steps find lambda on the device and prep inside the reduction's launch
+    const bool fusedPrep = !first && fused_prep();
+    if (nP + nL) {
+        if (fusedPrep)
+            hipLaunchKernelGGL(k_sys_reduce_prep, dim3(nP + nblk(nL, kLandBlk)), dim3(kSysThreads), 0, s, S, dTerms_,
+                               dHpp_, dBp_, dHll_, dBl_, dHplA_, dScal_, dEmat_, dCb_, ctl);
+        else
+            hipLaunchKernelGGL(k_sys_reduce, dim3(nP + nblk(12 * nL, kSysThreads)), dim3(kSysThreads), 0, s, S, dTerms_,
+                               dHpp_, dBp_, dHll_, dBl_, ctl + 1);
+    }
     if (first) hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, nP, nL, dHpp_, dHll_, dScal_, ctl + 2);
     const int n = 6 * nP;
     const size_t ldsBytes = sizeof(double) * ((size_t)n + (size_t)n * n);
@@ -4132,8 +4253,9 @@ void BaEngine::enqueue_lm_step(bool first) {
     const size_t regShm = ldlt_reg_shm(n);
     const bool use_reg = n < kLdltMax && regShm <= ldsMax_;   // b rides in column n
     const SysAddr sa{dS_, n, nullptr, nullptr, 0, nullptr};
-    if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_, 0.0, 1,
-                               dScal_, dEmat_, dCb_, ctl);
+    if (nE && !(fusedPrep && nP + nL))
+        hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_, 0.0, 1, dScal_,
+                           dEmat_, dCb_, ctl);
     if (S.nBlk) schur_launch(S.nBlk, blkChunks_, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_, 0.0,
                                    1, dScal_, sa, dBs_, 1, (const uint8_t*)nullptr, ctl);
     const DenseLdlt kind = dense_ldlt_kind(n, use_reg);
