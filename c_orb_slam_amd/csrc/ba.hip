@@ -3328,8 +3328,8 @@ BaEngine::~BaEngine() {
 
 int BaEngine::stage_reserve(size_t bytes) {
     if (uploadPending_) {   // the problem upload may still read the staging block
-        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
         uploadPending_ = false;
+        if (int e = poll_stream()) return e;
     }
     if (bytes <= hStageCap_) return 0;
     if (hStage_) (void)hipHostFree(hStage_);
@@ -3364,6 +3364,37 @@ int BaEngine::h2d_sync(void* dst, const void* src, size_t bytes) {
     return 0;
 }
 
+// Stream drain by polling: a one-thread kernel queued behind the stream's work writes a sequence
+// number to pinned coherent memory and the host spins on it.  A blocking stream sync sleeps and
+// wakes tens of microseconds after the copy it waits for (the gaps before k_gate and after each
+// optimize() in profiles/r05d2lba_lba_timeline.txt); past 50 ms the spin hands over to it.
+__global__ void k_signal(volatile int* w, int v) {
+    if (threadIdx.x == 0) *w = v;
+}
+int BaEngine::poll_stream() {
+    volatile int* w = (volatile int*)hLm_ + 8;
+    const int v = ++signalSeq_;
+    hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, stream_, w, v);
+    ORB_HIP_CHECK(hipGetLastError());
+    const auto w0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 1; *w != v; spin++) {
+        if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - w0 > std::chrono::milliseconds(50)) {
+            ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+            break;
+        }
+        __builtin_ia32_pause();
+    }
+    return 0;
+}
+int BaEngine::d2h_poll(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return 0;
+    if (int e = stage_reserve(bytes)) return e;
+    ORB_HIP_CHECK(hipMemcpyAsync(hStage_, src, bytes, hipMemcpyDeviceToHost, stream_));
+    if (int e = poll_stream()) return e;
+    std::memcpy(dst, hStage_, bytes);
+    return 0;
+}
+
 int BaEngine::d2h_sync(void* dst, const void* src, size_t bytes) {
     if (!bytes) return 0;
     if (int e = stage_reserve(bytes)) return e;
@@ -3379,6 +3410,7 @@ int BaEngine::init() {
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     ORB_HIP_CHECK(hipHostMalloc((void**)&hScal_, 64 * sizeof(double)));
     ORB_HIP_CHECK(hipHostMalloc((void**)&hLm_, 16 * sizeof(int), hipHostMallocCoherent));
+    std::memset((void*)hLm_, 0, 16 * sizeof(int));   // [8]: poll_stream's sequence word
     for (auto& ev : lmEv_) ORB_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     int dev = 0;
     ORB_HIP_CHECK(hipGetDevice(&dev));
@@ -4368,7 +4400,7 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
         fprintf(stderr, "[ba]   LM steps queued %d: host enqueue %.1f us/step, wait %.1f us/step\n", nSteps,
                 tEnq / nSteps, tWait / nSteps);
     LmDev h;
-    if (int e = d2h_sync(&h, dLm_, sizeof(LmDev))) return e;   // also drains the queue
+    if (int e = d2h_poll(&h, dLm_, sizeof(LmDev))) return e;   // also drains the queue
     if (!h.done) return -7;    // the step bound is the trial bound: unreachable
     *its = h.it;
     for (int t = 0; t < std::min(h.nTrial, kLmTrials); t++) {
@@ -4400,7 +4432,7 @@ int BaEngine::gate_edges(int final_check, uint8_t* erase) {
     hipLaunchKernelGGL(k_gate, dim3(nblk(ne_, 256)), dim3(256), 0, stream_, ne_, dE_, dT_, dX_, dErr_, dFlag, dLevel_,
                        dRobust_, final_check ? 0 : 1);
     ORB_HIP_CHECK(hipGetLastError());
-    return erase ? d2h_sync(erase, dFlag, ne_) : 0;
+    return erase ? d2h_poll(erase, dFlag, ne_) : 0;
 }
 
 int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, Comm* comm, const BaMode* mode) {
@@ -4473,7 +4505,7 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
         char* st = (char*)hStage_;
         if (bT) ORB_HIP_CHECK(hipMemcpyAsync(st, dT_, bT, hipMemcpyDeviceToHost, stream_));
         if (bX) ORB_HIP_CHECK(hipMemcpyAsync(st + bT, dX_, bX, hipMemcpyDeviceToHost, stream_));
-        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        if (int e = poll_stream()) return e;
         std::memcpy(T.data(), st, bT);
         std::memcpy(X.data(), st + bT, bX);
     }

@@ -132,6 +132,9 @@ private:
     int stage2_reserve(size_t bytes);
     int h2d_sync(void* dst, const void* src, size_t bytes);
     int d2h_sync(void* dst, const void* src, size_t bytes);
+    int d2h_poll(void* dst, const void* src, size_t bytes);   // d2h_sync without the blocking wait
+    int poll_stream();                                         // drain the stream by polling hLm_[8]
+    int signalSeq_ = 0;
     int stage_reserve(size_t bytes);
     size_t scratchN_ = 0;
     size_t ldsMax_ = 0;
