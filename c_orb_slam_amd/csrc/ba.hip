@@ -3188,7 +3188,7 @@ int PoseEngine::launch_device(int count, const int* Ns, const std::function<void
     ORB_HIP_CHECK(hipMemcpyAsync(hp, d, bProb, hipMemcpyDeviceToHost, st));
     ORB_HIP_CHECK(hipEventRecord(lastUse_, st));
     lastUseSet_ = true;
-    ORB_HIP_CHECK(hipStreamSynchronize(st));
+    ORB_HIP_CHECK(stream_wait(st));
     int rc = 0;
     for (int f = 0; f < count; f++) {
         const PoseProbDev& pp = hp[f];

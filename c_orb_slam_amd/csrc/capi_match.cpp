@@ -235,7 +235,7 @@ int ORBmatcher_SearchByProjection_LastFrame_batch(ORBmatcher_h h, int npairs, co
                 hipMemcpyAsync(cur_mp[p], probs[p].curMP, (size_t)cur[p].N * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
                 return ORB_E_HIP;
     }
-    if (hipStreamSynchronize(s) != hipSuccess) return ORB_E_HIP;
+    if (orbgpu::stream_wait(s) != hipSuccess) return ORB_E_HIP;
     return ORB_OK;
 }
 
@@ -305,7 +305,7 @@ int ORBmatcher_SearchByProjection_MapPoints(ORBmatcher_h h, const orb_frame* F, 
     if (hipMemcpyAsync(nmatches, d_nm, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return ORB_E_HIP;
     if (!dev && F->N > 0 && hipMemcpyAsync(cur_mp, P.curMP, (size_t)F->N * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
         return ORB_E_HIP;
-    if (hipStreamSynchronize(s) != hipSuccess) return ORB_E_HIP;
+    if (orbgpu::stream_wait(s) != hipSuccess) return ORB_E_HIP;
     return ORB_OK;
 }
 
@@ -359,7 +359,7 @@ int Frame_isInFrustum_batch(ORBmatcher_h h, int count, const orb_frame* F, const
     if (err) return err;
     if (m->frustum(probs, fr, viewingCosLimit, logScaleFactor)) return ORB_E_HIP;
     if (hipMemcpyAsync(nvisible, d_nv, (size_t)count * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return ORB_E_HIP;
-    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+    return orbgpu::stream_wait(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
 }
 
 int ORBmatcher_SearchLocalPoints_batch(ORBmatcher_h h, int count, const orb_frame* F, int32_t* const* cur_mp,
@@ -465,7 +465,7 @@ int ORBmatcher_SearchDense_batch(ORBmatcher_h h, int count, const uint8_t* const
             hipMemcpyAsync(second_dist[p], d.second_dist, (size_t)nq[p] * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
             return ORB_E_HIP;
     }
-    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+    return orbgpu::stream_wait(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
 }
 
 int ORBmatcher_last_dense_timing(ORBmatcher_h h, float* ms, long long* pairs) {
@@ -485,7 +485,7 @@ int ORBmatcher_SearchCandidates(ORBmatcher_h h, const uint8_t* qdesc, int nq, co
     if (dev) {
         int rc = m->candidates(qdesc, nq, tdesc, nt, off, cand, dist, best_idx, best_dist, second_dist);
         if (rc) return ORB_E_HIP;
-        return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+        return orbgpu::stream_wait(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
     }
     const int ncand = off[nq];
     if (off[0] != 0 || ncand < 0) return ORB_E_INVALID;
@@ -513,7 +513,7 @@ int ORBmatcher_SearchCandidates(ORBmatcher_h h, const uint8_t* qdesc, int nq, co
         hipMemcpyAsync(best_dist, dbd, (size_t)nq * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(second_dist, dsd, (size_t)nq * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
         return ORB_E_HIP;
-    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+    return orbgpu::stream_wait(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
 }
 
 }  // extern "C"

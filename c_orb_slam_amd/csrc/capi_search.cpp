@@ -187,7 +187,7 @@ int node_lists(Matcher* m, const orb_featvec* fv1, const uint8_t* ok1, const uin
     if (err || !dd || !dbi || !dbd || !dsd) return ORB_E_HIP;
     if (m->candidates(dq, nq, dt, n2, doff, dc, dd, dbi, dbd, dsd)) return ORB_E_HIP;
     if (hipMemcpyAsync(L.dist.data(), dd, (size_t)nc * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return ORB_E_HIP;
-    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+    return orbgpu::stream_wait(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
 }
 
 

@@ -64,8 +64,8 @@ int ORBmatcher_ComputeStereoMatches_batch_at(ORBmatcher_h h, ORBextractor_h left
     const bool dev = m->device_pointers();
     hipStream_t s = m->stream();
     // the pyramids are produced on the extractors' streams
-    if (hipStreamSynchronize(EL->stream()) != hipSuccess ||
-        (ER != EL && hipStreamSynchronize(ER->stream()) != hipSuccess))
+    if (orbgpu::stream_wait(EL->stream()) != hipSuccess ||
+        (ER != EL && orbgpu::stream_wait(ER->stream()) != hipSuccess))
         return ORB_E_HIP;
     orbgpu::StereoParams P;
     std::memset(&P, 0, sizeof(P));
@@ -142,7 +142,7 @@ int ORBmatcher_ComputeStereoMatches_batch_at(ORBmatcher_h h, ORBextractor_h left
                           hipMemcpyAsync(depth[p], probs[p].depth, 4 * (size_t)NL[p], hipMemcpyDeviceToHost, s) !=
                               hipSuccess))
                 return ORB_E_HIP;
-    return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
+    return orbgpu::stream_wait(s) == hipSuccess ? ORB_OK : ORB_E_HIP;
 }
 
 int ORBmatcher_ComputeStereoMatches(ORBmatcher_h h, ORBextractor_h left, ORBextractor_h right, int index, int NL,
@@ -224,7 +224,7 @@ int Frame_UndistortKeyPoints_batch(ORBmatcher_h h, int count, const orb_undistor
             rc = ORB_E_HIP;
         o += (size_t)P[f].N;
     }
-    if (hipStreamSynchronize(s) != hipSuccess) rc = ORB_E_HIP;
+    if (orbgpu::stream_wait(s) != hipSuccess) rc = ORB_E_HIP;
     (void)hipFree(d);
     return rc;
 }
@@ -234,7 +234,7 @@ int Frame_UndistortKeyPoints(ORBmatcher_h h, const orb_undistort* U) {
     if (h->m->device_pointers()) {   // the single form is synchronous in either pointer space
         const int e = Frame_UndistortKeyPoints_batch(h, 1, U);
         if (e) return e;
-        return hipStreamSynchronize(h->m->stream()) == hipSuccess ? ORB_OK : ORB_E_HIP;
+        return orbgpu::stream_wait(h->m->stream()) == hipSuccess ? ORB_OK : ORB_E_HIP;
     }
     return Frame_UndistortKeyPoints_batch(h, 1, U);
 }

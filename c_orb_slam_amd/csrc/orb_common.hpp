@@ -25,6 +25,13 @@
 
 namespace orbgpu {
 
+// Wait for everything queued on stream s by polling: a one-thread kernel queued behind the work
+// writes a sequence number to the calling thread's pinned coherent word and the host spins on it.
+// hipStreamSynchronize sleeps and wakes some 20-30 us after the work it waits for (BA readbacks,
+// profiles/r05d2lba vs r05e2lba timelines), once per synchronous call of a tracking frame.  Past
+// 50 ms of spinning, or without a pinned word, it is hipStreamSynchronize.  (orb_match.hip)
+hipError_t stream_wait(hipStream_t s);
+
 // Deferred completion of a chain of batch calls on one stream (bench tracking lane): the host
 // sources of a call's H2D copies and the destinations of its count D2H copies live in pinned
 // blocks that stay untouched until the chain is finished, so a call can return without

@@ -1729,7 +1729,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipMemcpyAsync(h_nout_, d_nout_, (size_t)(B + 1) * 4, hipMemcpyDeviceToHost, s));
     ORB_HIP_CHECK(hipEventRecord(ev_[6], s));
-    ORB_HIP_CHECK(hipStreamSynchronize(s));
+    ORB_HIP_CHECK(stream_wait(s));
     const int err = h_nout_[B];
     for (int b = 0; b < B; b++) n_out[b] = h_nout_[b];
     if (err & 1) return -3;   // keypoints beyond `cap` (or the selection capacity)
@@ -1742,7 +1742,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
             ORB_HIP_CHECK(hipMemcpyAsync(desc + (size_t)b * cap * 32, odesc + (size_t)b * cap * 32, (size_t)n_out[b] * 32,
                                          hipMemcpyDeviceToHost, s));
         }
-        ORB_HIP_CHECK(hipStreamSynchronize(s));
+        ORB_HIP_CHECK(stream_wait(s));
     }
     last_B_ = B;
     return 0;

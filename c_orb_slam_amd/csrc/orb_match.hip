@@ -17,6 +17,7 @@
 #define ORBGPU_PROF_BLOCK 20   // prof builds: k_select_r sections of a mid-batch frame (full local map)
 #include "orb_match.hpp"
 
+#include <chrono>
 #include <cstdlib>
 
 #include <cstring>
@@ -79,6 +80,40 @@ __device__ __forceinline__ int packed16(const uint32_t* a, int c) { return (int)
 // them as candidates (ORBmatcher.cc:87-89, 1403-1405), and a slot occupied at the start stays
 // occupied (the loops only fill empty or observation-less slots), so no query of the call can
 // take them; the remaining candidates keep their enumeration order.
+__global__ void k_stream_signal(volatile int* w, int v) {
+    if (threadIdx.x == 0) *w = v;
+}
+
+hipError_t stream_wait(hipStream_t s) {
+    thread_local volatile int* word = nullptr;
+    thread_local int seq = 0;
+    thread_local bool tried = false;
+    static const bool blocking = [] {   // ORBGPU_SYNC_BLOCKING=1: plain hipStreamSynchronize (A/B)
+        const char* e = std::getenv("ORBGPU_SYNC_BLOCKING");
+        return e && e[0] == '1';
+    }();
+    if (blocking) return hipStreamSynchronize(s);
+    if (!word && !tried) {
+        tried = true;
+        void* p = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocCoherent) == hipSuccess) {
+            std::memset(p, 0, 64);
+            word = (volatile int*)p;
+        }
+    }
+    if (!word) return hipStreamSynchronize(s);
+    const int v = ++seq;
+    hipLaunchKernelGGL(k_stream_signal, dim3(1), dim3(64), 0, s, word, v);
+    if (hipError_t e = hipGetLastError()) return e;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 1; *word != v; spin++) {
+        if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
+            return hipStreamSynchronize(s);
+        __builtin_ia32_pause();
+    }
+    return hipSuccess;
+}
+
 __global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs, int dropOccupied) {
     ORBGPU_LATENCY_WAVE();
     constexpr int kPer = kGridCells / 256;   // 12 cells per thread in the scan
@@ -1036,11 +1071,11 @@ int Matcher::area_candidates(const SearchDev& frame, const AreaQuery* d_q, int n
     SearchDev* dp = (SearchDev*)s;
     ORB_HIP_CHECK(hipMemcpyAsync(dp, &P, sizeof(SearchDev), hipMemcpyHostToDevice, stream_));
     hipLaunchKernelGGL(k_build_grid, dim3(1), dim3(256), grid_lds_bytes(frame.cur.N), stream_, dp, 0);
-    if (nq == 0) return hipStreamSynchronize(stream_) == hipSuccess ? 0 : -2;
+    if (nq == 0) return stream_wait(stream_) == hipSuccess ? 0 : -2;
     hipLaunchKernelGGL(k_area_count, dim3((nq + 255) / 256), dim3(256), 0, stream_, dp, d_q, nq, d_cnt);
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipMemcpyAsync(off.data() + 1, d_cnt, sizeof(int) * nq, hipMemcpyDeviceToHost, stream_));
-    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    ORB_HIP_CHECK(stream_wait(stream_));
     for (int i = 0; i < nq; i++) off[i + 1] += off[i];
     const int total = off[nq];
     cand.resize((size_t)std::max(total, 1));
@@ -1055,7 +1090,7 @@ int Matcher::area_candidates(const SearchDev& frame, const AreaQuery* d_q, int n
                        (int2*)d_cand_);
     ORB_HIP_CHECK(hipGetLastError());
     ORB_HIP_CHECK(hipMemcpyAsync(cand.data(), d_cand_, sizeof(int2) * (size_t)total, hipMemcpyDeviceToHost, stream_));
-    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    ORB_HIP_CHECK(stream_wait(stream_));
     return 0;
 }
 
@@ -1372,7 +1407,7 @@ int Matcher::dense(const std::vector<DenseDev>& probs) {
                            (int)jobs.size());
     mark(15);
     ORB_HIP_CHECK(hipGetLastError());
-    if (!chain_.on()) ORB_HIP_CHECK(hipStreamSynchronize(stream_));   // the pageable staging vector
+    if (!chain_.on()) ORB_HIP_CHECK(stream_wait(stream_));   // the pageable staging vector
     return 0;
 }
 
@@ -1380,7 +1415,7 @@ int Matcher::dense_timing(float* ms, long long* pairs) {
     *ms = -1.0f;
     *pairs = -1;
     if (!d_count_) return 0;
-    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    ORB_HIP_CHECK(stream_wait(stream_));
     if (evSet_[14] && evSet_[15]) (void)hipEventElapsedTime(ms, ev_[14], ev_[15]);
     std::vector<unsigned long long> c(kCountSlots);
     ORB_HIP_CHECK(hipMemcpy(c.data(), d_count_ + 6 * kCountSlots, sizeof(unsigned long long) * kCountSlots,
@@ -1420,7 +1455,7 @@ int Matcher::timings(float* ms8, long long* cnt8) {
         cnt8[i] = -1;
     }
     if (!d_count_) return 0;
-    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    ORB_HIP_CHECK(stream_wait(stream_));
     const int pairs[8][2] = {{0, 1}, {1, 2}, {2, 3}, {4, 5}, {5, 6}, {6, 7}, {12, 13}, {8, 9}};
     for (int k = 0; k < 8; k++) {
         const int a = pairs[k][0], b = pairs[k][1];
