@@ -600,6 +600,7 @@ def main():
         kp = [k[t].data_ptr() for t in range(nf + 1)]
         dp = [d[t].data_ptr() for t in range(nf + 1)]
         dL_ptr = [d_L[t].data_ptr() for t in range(nf)]
+        hT2 = torch.zeros(16, dtype=torch.float32).pin_memory()
         pre = [None] * nf
         for t in range(nf):
             q = max(0, t - K_LOCAL)
@@ -624,7 +625,10 @@ def main():
                                      uR[t].data_ptr(), isig.data_ptr(), 8, float(fx), float(fy), float(cx), float(cy),
                                      float(mbf))
                 g["pose1"] = (arr([T1.data_ptr()]), arr([o1.data_ptr()]))
-                g["pose2"] = (arr([T2.data_ptr()]), arr([o2.data_ptr()]))
+                # device path: the frame's final pose written by the pose kernel straight into pinned
+                # host memory (device-visible), where Tracking keeps mTcw; the host path copies
+                # it back with the Frame's other members
+                g["pose2"] = (arr([T2.data_ptr() if host_io else hT2.data_ptr()]), arr([o2.data_ptr()]))
                 g["prep"] = orb_localprep(0, cur_mp.data_ptr(), o1.data_ptr(), nloc, slot[q].data_ptr(), skip.data_ptr())
                 g["lmap"] = orb_localmap(nloc, pos[q].data_ptr(), dp[q], d_obs.data_ptr(), maxd[q].data_ptr(),
                                          mind[q].data_ptr(), nrm[q].data_ptr(), skip.data_ptr())
@@ -633,7 +637,6 @@ def main():
         T1p, Tpp = T1.data_ptr(), Tpred.data_ptr()
         nl, nr = np.zeros(1, np.int32), np.zeros(1, np.int32)
         nm1, ni, nm2, nv2 = (np.zeros(1, np.int32) for _ in range(4))
-        hT2 = torch.empty(16, dtype=torch.float32).pin_memory()
         # the drop-in caller is C++ (System::TrackStereo): no interpreter garbage collection runs
         # between its frames, so none runs inside this leg's timed frames either
         import gc
@@ -747,7 +750,7 @@ def main():
                     d2h_bytes.append(n0 * (28 + 32 + 4 + 4 + 4 + 1) + n1 * 60 + 64)
                     Tcw.append(hT.numpy().reshape(4, 4).copy())
                 else:
-                    Tcw.append(T2.cpu().numpy().reshape(4, 4).copy())
+                    Tcw.append(hT2.numpy().reshape(4, 4).copy())
                 nmatch.append(int(nm1[0] + nm2[0]))
             last_n = nL
             mark("end")
