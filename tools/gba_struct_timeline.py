@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Timeline of the structure phase of the last BundleAdjustment call in a rocprofv3 trace of
-tools/gba_timing.py: from the call's compact-edge copy / first k_gs_ kernel to its first
+tools/gba_timing.py: from the call's upload copy and unpack kernel to its first
 k_linearize, with the idle gap before each entry (host work between launches shows as gaps).
 usage: gba_struct_timeline.py kernel_trace.csv [memory_copy_trace.csv]"""
 import csv
@@ -14,9 +14,9 @@ if len(sys.argv) > 2:
     for r in csv.DictReader(open(sys.argv[2])):
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy " + r.get("Direction", "")[:24]))
 ev.sort()
-exp = [i for i, e in enumerate(ev) if e[2].startswith("k_expand_edges")]
+exp = [i for i, e in enumerate(ev) if e[2].startswith(("k_unpack_upload", "k_expand_edges"))]
 if not exp:
-    sys.exit("no k_expand_edges in the trace")
+    sys.exit("no upload kernel in the trace")
 a = exp[-1]
 while a > 0 and ev[a - 1][2].startswith("copy"):   # the call's uploads
     a -= 1
