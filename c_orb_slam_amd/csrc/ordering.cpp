@@ -3,10 +3,14 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <thread>
 
 namespace orbgpu {
 
 namespace {
+
+constexpr int kParDepth = 2;    // the top two dissection levels split over host threads
+constexpr int kParMin = 256;     // ... when both sides have this many poses
 
 struct Nd {
     const std::vector<int>& as;
@@ -48,11 +52,21 @@ struct Nd {
     }
 
     // appends the roots of S's subtrees to `roots`
-    void order(std::vector<int> S, std::vector<int>& roots) {
+    void order(std::vector<int> S, std::vector<int>& roots, int depth = 0) {
         const int sid = ++stamp;
         for (int v : S) inS[v] = sid;
+        const int n = (int)S.size();
+        // the level sets from S[0] reach all of S exactly when S is connected: the usual case,
+        // and then the component search below (the same traversal) is skipped
+        std::vector<std::vector<int>> L;
+        if (n > leaf) {
+            levels(S[0], sid, L);
+            size_t reach = 0;
+            for (const auto& lv : L) reach += lv.size();
+            if ((int)reach != n) L.clear();
+        }
         // connected components, in order of their smallest node
-        {
+        if (L.empty()) {
             std::vector<std::vector<int>> comps;
             const int st = ++stamp;
             for (int s0 : S) {
@@ -74,19 +88,17 @@ struct Nd {
                 comps.push_back(std::move(comp));
             }
             if (comps.size() > 1) {
-                for (auto& c : comps) order(std::move(c), roots);
+                for (auto& c : comps) order(std::move(c), roots, depth);
                 return;
             }
         }
-        const int n = (int)S.size();
         auto make_leaf = [&]() {
             const int s = (int)t->perm.size();
             t->perm.insert(t->perm.end(), S.begin(), S.end());
             roots.push_back(new_node(s, (int)t->perm.size(), 0));
         };
         if (n <= leaf) return make_leaf();
-        std::vector<std::vector<int>> L;
-        levels(S[0], sid, L);
+        if (L.empty()) levels(S[0], sid, L);
         const int u = L.back()[0];
         levels(u, sid, L);
         const int h = (int)L.size() - 1;
@@ -111,8 +123,28 @@ struct Nd {
         std::sort(Bset.begin(), Bset.end());
         std::vector<int> sep = std::move(L[best]);
         std::vector<int> kids;
-        order(std::move(Aset), kids);
-        order(std::move(Bset), kids);
+        if (depth < kParDepth && (int)Aset.size() >= kParMin && (int)Bset.size() >= kParMin) {
+            // the two sides are independent: B on a thread of its own into a tree fragment (own
+            // stamps), spliced after A's nodes -- the same tree as the sequential recursion
+            NdTree tb;
+            std::vector<int> kidsB;
+            Nd nb{as, adj, leaf, &tb, std::vector<int>(inS.size(), 0), std::vector<int>(mark.size(), 0)};
+            std::thread th([&] { nb.order(std::move(Bset), kidsB, depth + 1); });
+            order(std::move(Aset), kids, depth + 1);
+            th.join();
+            const int basePerm = (int)t->perm.size(), baseNode = (int)t->start.size();
+            t->perm.insert(t->perm.end(), tb.perm.begin(), tb.perm.end());
+            for (size_t k = 0; k < tb.start.size(); k++) {
+                t->start.push_back(tb.start[k] + basePerm);
+                t->end.push_back(tb.end[k] + basePerm);
+                t->parent.push_back(tb.parent[k] >= 0 ? tb.parent[k] + baseNode : -1);
+                t->height.push_back(tb.height[k]);
+            }
+            for (int c : kidsB) kids.push_back(c + baseNode);
+        } else {
+            order(std::move(Aset), kids, depth + 1);
+            order(std::move(Bset), kids, depth + 1);
+        }
         int hmax = 0;
         for (int c : kids) hmax = std::max(hmax, t->height[c]);
         const int s = (int)t->perm.size();
