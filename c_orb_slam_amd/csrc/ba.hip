@@ -4161,7 +4161,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
             if (int e = comm_->allreduce(rb, 2, RedOp::Sum, s)) return e;
         }
         ORB_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
-        ORB_HIP_CHECK(hipStreamSynchronize(s));
+        if (int e = poll_stream()) return e;   // (s is stream_)
         if (comm_) stopRed_ = hScal_[6] != 0.0;
         if (!haveChi) {
             currentChi = iniChi = hScal_[0];

@@ -394,7 +394,7 @@ int GpuStructBuilder::build(int level, int nkf, int npt, int ne, const EdgeDev* 
     }
     GS_CHECK(hipGetLastError());
     GS_CHECK(hipMemcpyAsync(hSc_, sc, sizeof(int) * C_N, hipMemcpyDeviceToHost, s));
-    GS_CHECK(hipStreamSynchronize(s));
+    GS_CHECK(stream_wait(s));
     const int nE = hSc_[C_NE], nP = hSc_[C_NP], nL = hSc_[C_NL];
     const long long nPairL = hSc_[C_NPAIR];
     if (hSc_[C_ERR]) {
@@ -458,7 +458,7 @@ int GpuStructBuilder::build(int level, int nkf, int npt, int ne, const EdgeDev* 
     }
     GS_CHECK(hipGetLastError());
     GS_CHECK(hipMemcpyAsync(hSc_ + C_MAXBLK, sc + C_MAXBLK, sizeof(int) * 2, hipMemcpyDeviceToHost, s));
-    GS_CHECK(hipStreamSynchronize(s));
+    GS_CHECK(stream_wait(s));
     nOff = nPair > 0 ? hSc_[C_NOFF] : 0;
     const int nBlk = nP + nOff;
     info->nE = nE;
@@ -505,7 +505,7 @@ int GpuStructBuilder::build(int level, int nkf, int npt, int ne, const EdgeDev* 
         if (nBlk) {
             GS_CHECK(hipMemcpyAsync(blkIJ->data(), blkI, sizeof(int) * nBlk, hipMemcpyDeviceToHost, s));
             GS_CHECK(hipMemcpyAsync(blkIJ->data() + nBlk, blkJ, sizeof(int) * nBlk, hipMemcpyDeviceToHost, s));
-            GS_CHECK(hipStreamSynchronize(s));
+            GS_CHECK(stream_wait(s));
         }
     }
     return 0;
@@ -536,7 +536,7 @@ int GpuStructBuilder::offkeys(std::vector<int64_t>* out, hipStream_t s) {
     hipLaunchKernelGGL(k_gs_offkey, dim3(nb(nOff_)), dim3(kT), 0, s, nOff_, sc, ok, nkf, nP, okl);
     GS_CHECK(hipGetLastError());
     GS_CHECK(hipMemcpyAsync(out->data(), okl, sizeof(long long) * nOff_, hipMemcpyDeviceToHost, s));
-    GS_CHECK(hipStreamSynchronize(s));
+    GS_CHECK(stream_wait(s));
     return 0;
 }
 

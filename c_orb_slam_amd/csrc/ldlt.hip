@@ -1192,7 +1192,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     ORB_HIP_CHECK(hipMemcpyAsync(slotOf_, hSlotOf_.data(), sizeof(int) * hSlotOf_.size(), hipMemcpyHostToDevice, s));
     ORB_HIP_CHECK(hipMemcpyAsync(prow_, hProw_.data(), sizeof(int) * hProw_.size(), hipMemcpyHostToDevice, s));
     ORB_HIP_CHECK(hipMemcpyAsync(lists_, L.data(), sizeof(int) * L.size(), hipMemcpyHostToDevice, s));
-    ORB_HIP_CHECK(hipStreamSynchronize(s));   // pageable sources
+    ORB_HIP_CHECK(stream_wait(s));   // pageable sources
     lap("lists + upload");
     return 0;
 }
