@@ -533,6 +533,14 @@ def main():
             local_acc.append((int(self.nml.sum()), int(self.nvis.sum())))
             return self.kp_count, int(self.nm.sum() + self.nml.sum()), int(self.nst.sum())
 
+    def rigid_inv(T):
+        """Twc from Tcw as the reference forms it (Frame::UpdatePoseMatrices: R^T, -R^T t)."""
+        Ti = np.eye(4, dtype=np.float32)
+        R = T[:3, :3]
+        Ti[:3, :3] = R.T
+        Ti[:3, 3] = -(R.T @ T[:3, 3])
+        return Ti
+
     def latency_leg(nf, host_io=False):
         """Per-frame tracking latency, the reference's own figure (wall time of one TrackStereo,
         stereo_kitti.cc:80-97): batch 1, frames in sequence, each frame's motion model from the
@@ -579,11 +587,14 @@ def main():
         mind = torch.zeros((nf, cap), dtype=torch.float32, device=dev)
         nrm = torch.zeros((nf, cap, 3), dtype=torch.float32, device=dev)
         skip = torch.ones(K_LOCAL * cap, dtype=torch.uint8, device=dev)
-        cur_mp = torch.full((cap,), -1, dtype=torch.int32, device=dev)
         # the frame's three 4x4 poses (motion-model prediction, last Tcw, last Twc) travel in ONE
         # pinned H2D copy, as a C++ caller would pass them, not three pageable copies
-        Tdev = torch.zeros(48, dtype=torch.float32, device=dev)
-        Thost = torch.zeros(48, dtype=torch.float32).pin_memory()
+        # ... and the current frame's map-point slots (mvpMapPoints, all NULL = -1 at the start of
+        # the frame) ride in the same copy: one H2D per frame sets the poses and clears the slots
+        Tbuf = torch.zeros(48 + cap, dtype=torch.int32, device=dev)
+        Thbuf = torch.zeros(48 + cap, dtype=torch.int32).pin_memory()
+        Thbuf[48:] = -1
+        Tdev, Thost, cur_mp = Tbuf[:48].view(torch.float32), Thbuf[:48].view(torch.float32), Tbuf[48:]
         Tpred, Tlast, Twc_l = Tdev[0:16], Tdev[16:32], Tdev[32:48]
         T1, T2 = (torch.zeros(16, dtype=torch.float32, device=dev) for _ in range(2))
         o1, o2 = (torch.zeros(cap, dtype=torch.uint8, device=dev) for _ in range(2))
@@ -695,21 +706,16 @@ def main():
                                                                  ptr(one)), "ComputeStereoMatches")
             mark("stereo")
             if t > 0:
-                V = Tcw[t - 1] @ np.linalg.inv(Tcw[t - 2]) if t >= 2 else np.eye(4, dtype=np.float32)
+                V = Tcw[t - 1] @ rigid_inv(Tcw[t - 2]) if t >= 2 else np.eye(4, dtype=np.float32)
                 Tp = (V @ Tcw[t - 1]).astype(np.float32)
                 nlast = int(last_n[0])
                 g = pre[t]
                 hv = Thost.numpy()
                 hv[0:16] = Tp.reshape(16)
                 hv[16:32] = Tcw[t - 1].reshape(16)
-                hv[32:48] = np.linalg.inv(Tcw[t - 1]).astype(np.float32).reshape(16)
+                hv[32:48] = rigid_inv(Tcw[t - 1]).reshape(16)
                 with torch.cuda.stream(match_stream):   # ordered before the matcher's launches
-                    if os.environ.get("BENCH_LAT_POSE_PAGEABLE") == "1":   # (A/B: the three pageable copies)
-                        for q3 in range(3):
-                            Tdev[16 * q3:16 * q3 + 16].copy_(torch.from_numpy(hv[16 * q3:16 * q3 + 16].copy()))
-                    else:
-                        Tdev.copy_(Thost, non_blocking=True)
-                    cur_mp.fill_(-1)
+                    Tbuf.copy_(Thbuf, non_blocking=True)
                 u = g["u"]
                 u.N = nlast
                 check(L.MapPoint_CreateStereo_batch_device(m._h, 1, C.byref(u)), "MapPoint_CreateStereo")

@@ -3603,8 +3603,10 @@ int BaEngine::upload_problem(const ba_problem* P) {
 
     kfId_.assign(P->kf_id, P->kf_id + nkf_);
     ptId_.assign(P->pt_id, P->pt_id + npt_);
-    ePt_.assign(P->edge_pt, P->edge_pt + ne_);
-    eKf_.assign(P->edge_kf, P->edge_kf + ne_);
+    // the caller's edge arrays, read in place by the host structure builder during this call
+    // (a global BA's 1.5 M edges are not copied)
+    ePt_ = P->edge_pt;
+    eKf_ = P->edge_kf;
     kfLocal_.assign(P->kf_local, P->kf_local + nkf_);
     kfFixed_.resize(nkf_);
     for (int k = 0; k < nkf_; k++)  // BundleAdjustment: every keyframe is a vertex, fixed iff mnId == 0 (Optimizer.cc:79)
@@ -3761,7 +3763,7 @@ int BaEngine::build_structure(int level) {
     } else {
         BaHostStruct& H = hs_;
         std::vector<uint8_t> kfAct, ptAct;
-        ba_active_set(level, nkf_, npt_, ne_, eKf_.data(), ePt_.data(), level_.data(), &H.aE, &kfAct, &ptAct);
+        ba_active_set(level, nkf_, npt_, ne_, eKf_, ePt_, level_.data(), &H.aE, &kfAct, &ptAct);
         if (comm_) {
             // shards agree on the pose set: a keyframe is active if any shard has an active edge
             // on it (its pose index must be the same everywhere); also the global edge/landmark counts
@@ -3780,7 +3782,7 @@ int BaEngine::build_structure(int level) {
             nLglob_ = (int)red[nkf_ + 1];
         }
         lap("active set");
-        if (ba_build_lists(nkf_, npt_, eKf_.data(), ePt_.data(), kfFixed_.data(), kfId_.data(), ptId_.data(), kfAct, ptAct,
+        if (ba_build_lists(nkf_, npt_, eKf_, ePt_, kfFixed_.data(), kfId_.data(), ptId_.data(), kfAct, ptAct,
                            &H))
             return -1;
         lap("lists");

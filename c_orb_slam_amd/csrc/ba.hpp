@@ -89,7 +89,9 @@ private:
     uint8_t *dLevel_ = nullptr, *dRobust_ = nullptr;
     double* dErr_ = nullptr;       // ne x 3, last computed _error
     // host mirror of the static problem
-    std::vector<int32_t> kfId_, ptId_, ePt_, eKf_;
+    std::vector<int32_t> kfId_, ptId_;
+    const int32_t* ePt_ = nullptr;   // the current call's edge arrays (ba_problem, caller-owned)
+    const int32_t* eKf_ = nullptr;
     std::vector<uint8_t> kfFixed_, kfLocal_, level_, ptHasEdge_;
     // structure
     BaStructDev st_{};
