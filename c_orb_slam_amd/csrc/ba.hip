@@ -3761,9 +3761,38 @@ int BaEngine::build_structure(int level) {
                 if (blkIJ[b] != blkIJ[nBlk + b]) offKeys.push_back((int64_t)blkIJ[b] * nP + blkIJ[nBlk + b]);
         }
     } else {
+        // the second pass after the outlier gating: the first pass's lists filtered (its edges are
+        // a superset) instead of built again; ORBGPU_STRUCT_CHECK=1 also builds them afresh and
+        // compares every list
+        const bool refine = refineNext_ && !comm_ && hsValid_;
+        refineNext_ = false;
+        if (refine) {
+            if (ba_refine_lists(hs_, level_.data(), level, &hs2_)) return -1;
+            static const bool check = getenv("ORBGPU_STRUCT_CHECK") != nullptr;
+            if (check) {
+                BaHostStruct F;
+                std::vector<uint8_t> ka, pa;
+                ba_active_set(level, nkf_, npt_, ne_, eKf_, ePt_, level_.data(), &F.aE, &ka, &pa);
+                if (ba_build_lists(nkf_, npt_, eKf_, ePt_, kfFixed_.data(), kfId_.data(), ptId_.data(), ka, pa, &F))
+                    return -1;
+                const std::vector<int32_t>* x[] = {&F.aE, &F.ePose, &F.eLand, &F.poseKf, &F.landPt, &F.peStart,
+                                                   &F.peList, &F.leStart, &F.leList, &F.lpStart, &F.lpList, &F.blkI,
+                                                   &F.blkJ, &F.blkStart, &F.pairA, &F.pairB};
+                const std::vector<int32_t>* y[] = {&hs2_.aE, &hs2_.ePose, &hs2_.eLand, &hs2_.poseKf, &hs2_.landPt,
+                                                   &hs2_.peStart, &hs2_.peList, &hs2_.leStart, &hs2_.leList,
+                                                   &hs2_.lpStart, &hs2_.lpList, &hs2_.blkI, &hs2_.blkJ,
+                                                   &hs2_.blkStart, &hs2_.pairA, &hs2_.pairB};
+                for (int k = 0; k < 16; k++)
+                    if (*x[k] != *y[k]) {
+                        fprintf(stderr, "[ba] refined structure list %d differs from a fresh build\n", k);
+                        return -2;
+                    }
+            }
+            std::swap(hs_, hs2_);
+        }
         BaHostStruct& H = hs_;
         std::vector<uint8_t> kfAct, ptAct;
-        ba_active_set(level, nkf_, npt_, ne_, eKf_, ePt_, level_.data(), &H.aE, &kfAct, &ptAct);
+        if (!refine) ba_active_set(level, nkf_, npt_, ne_, eKf_, ePt_, level_.data(), &H.aE, &kfAct, &ptAct);
         if (comm_) {
             // shards agree on the pose set: a keyframe is active if any shard has an active edge
             // on it (its pose index must be the same everywhere); also the global edge/landmark counts
@@ -3782,10 +3811,11 @@ int BaEngine::build_structure(int level) {
             nLglob_ = (int)red[nkf_ + 1];
         }
         lap("active set");
-        if (ba_build_lists(nkf_, npt_, eKf_, ePt_, kfFixed_.data(), kfId_.data(), ptId_.data(), kfAct, ptAct,
-                           &H))
+        if (!refine &&
+            ba_build_lists(nkf_, npt_, eKf_, ePt_, kfFixed_.data(), kfId_.data(), ptId_.data(), kfAct, ptAct, &H))
             return -1;
-        lap("lists");
+        hsValid_ = true;
+        lap(refine ? "lists (refined)" : "lists");
         nE = (int)H.aE.size();
         nP = (int)H.poseKf.size();
         nL = (int)H.landPt.size();
@@ -4236,6 +4266,15 @@ static bool lm_host_forced() {
     return v;
 }
 
+// ORBGPU_STRUCT_REFINE=0 builds the second local-BA pass's lists afresh (A/B)
+static bool refine_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("ORBGPU_STRUCT_REFINE");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // ORBGPU_FUSED_PREP=0 keeps k_sys_reduce + k_point_prep on every step (A/B)
 static bool fused_prep() {
     static const bool v = [] {
@@ -4446,6 +4485,8 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
     comm_ = comm && comm->size() > 1 ? comm : nullptr;
     mode_ = mode ? *mode : BaMode{};
     stopRed_ = false;
+    hsValid_ = false;     // hs_ holds this call's lists only after its first host build
+    refineNext_ = false;
     std::memcpy(R->kf_Tcw, P->kf_Tcw, sizeof(float) * 16 * P->n_kf);
     std::memcpy(R->pt_pos, P->pt_pos, sizeof(float) * 3 * P->n_pt);
     if (P->n_edge) std::memset(R->edge_erase, 0, P->n_edge);
@@ -4490,6 +4531,7 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
                 if (int e = gate_edges(0, nullptr)) return e;
             }
             ts = clk::now();
+            refineNext_ = refine_enabled();
             if (int e = build_structure(0)) return e;
             t_struct += std::chrono::duration<double, std::milli>(clk::now() - ts).count();
             if (nEglob_ > 0 && st_.nP + nLglob_ > 0)

@@ -136,6 +136,8 @@ private:
     int d2h_sync(void* dst, const void* src, size_t bytes);
     int d2h_poll(void* dst, const void* src, size_t bytes);   // d2h_sync without the blocking wait
     int poll_stream();                                         // drain the stream by polling hLm_[8]
+    BaHostStruct hs2_;            // the refined lists of a second pass (swapped into hs_)
+    bool hsValid_ = false, refineNext_ = false;
     int signalSeq_ = 0;
     int stage_reserve(size_t bytes);
     size_t scratchN_ = 0;

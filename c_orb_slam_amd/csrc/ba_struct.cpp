@@ -72,10 +72,12 @@ static void by_id(int n, const uint8_t* flag, const int32_t* id, std::vector<int
     for (size_t k = 0; k < m; k++) (*out)[k] = (int32_t)(keys[k] & 0xffffffffu);
 }
 
-int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, const uint8_t* kfFixed,
-                   const int32_t* kfId, const int32_t* ptId, const std::vector<uint8_t>& kfAct,
-                   const std::vector<uint8_t>& ptAct, BaHostStruct* S) {
-    static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;   // the phases below (tools/)
+// The Schur pattern of a structure whose lpStart / lpList (landmark -> free-pose edges, pose
+// order) and their poses qp are built: blocks numbered (diagonal first, then first use in the
+// (landmark, u <= v) walk), each block's terms in landmark order.
+int ba_build_blocks(int nP, int nL, const int32_t* __restrict__ qs, const int32_t* __restrict__ ql,
+                    const int32_t* __restrict__ qp, BaHostStruct* S) {
+    static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;
     using sclk = std::chrono::steady_clock;
     auto ts0 = sclk::now();
     auto lap = [&](const char* what) {
@@ -84,84 +86,6 @@ int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, con
         fprintf(stderr, "[ba]     lists: %s %.1f us\n", what, std::chrono::duration<double, std::micro>(t - ts0).count());
         ts0 = t;
     };
-    std::vector<uint8_t> freeKf(nkf);
-    for (int k = 0; k < nkf; k++) freeKf[k] = kfAct[k] && !kfFixed[k];
-    by_id(nkf, freeKf.data(), kfId, &S->poseKf);
-    by_id(npt, ptAct.data(), ptId, &S->landPt);
-    const std::vector<int32_t>& aE = S->aE;
-    const int nE = (int)aE.size(), nP = (int)S->poseKf.size(), nL = (int)S->landPt.size();
-    std::vector<int32_t> poseIdx(nkf, -1), landIdx(npt, -1);
-    for (int i = 0; i < nP; i++) poseIdx[S->poseKf[i]] = i;
-    for (int i = 0; i < nL; i++) landIdx[S->landPt[i]] = i;
-    // raw pointers below: stores through S's vectors would otherwise alias every load
-    S->ePose.resize(nE);
-    S->eLand.resize(nE);
-    S->peStart.assign(nP + 1, 0);
-    S->leStart.assign(nL + 1, 0);
-    S->lpStart.assign(nL + 1, 0);
-    {
-        int32_t* __restrict__ eP = S->ePose.data();
-        int32_t* __restrict__ eL = S->eLand.data();
-        int32_t* __restrict__ ps = S->peStart.data();
-        int32_t* __restrict__ ls = S->leStart.data();
-        int32_t* __restrict__ qs = S->lpStart.data();
-        const int32_t* __restrict__ pi = poseIdx.data();
-        const int32_t* __restrict__ li = landIdx.data();
-        const int32_t* __restrict__ ae = aE.data();
-        for (int a = 0; a < nE; a++) {
-            const int e = ae[a], p = pi[eKf[e]], l = li[ePt[e]];
-            eP[a] = p;
-            eL[a] = l;
-            const int32_t f = p >= 0;   // branch-free: fixed-pose edges count 0 (into ps[0] += 0)
-            ls[l + 1]++;
-            ps[p + 1] += f;
-            qs[l + 1] += f;
-        }
-        for (int i = 0; i < nP; i++) ps[i + 1] += ps[i];
-        for (int i = 0; i < nL; i++) {
-            ls[i + 1] += ls[i];
-            qs[i + 1] += qs[i];
-        }
-    }
-    lap("index maps + counts");
-    const int nPe = S->peStart[nP], nLe = S->leStart[nL], nLp = S->lpStart[nL];
-    S->peList.resize(std::max(nPe, 1));
-    S->leList.resize(std::max(nLe, 1));
-    S->lpList.resize(std::max(nLp, 1));
-    std::vector<int32_t> lpPose(std::max(nLp, 1));
-    {
-        const int32_t* __restrict__ eP = S->ePose.data();
-        const int32_t* __restrict__ eL = S->eLand.data();
-        const int32_t* __restrict__ ps = S->peStart.data();
-        int32_t* __restrict__ pl = S->peList.data();
-        int32_t* __restrict__ ll = S->leList.data();
-        int32_t* __restrict__ ql = S->lpList.data();
-        int32_t* __restrict__ qp = lpPose.data();
-        std::vector<int32_t> fp(S->peStart.begin(), S->peStart.end() - 1), fl(S->leStart.begin(), S->leStart.end() - 1),
-            fq(S->lpStart.begin(), S->lpStart.end() - 1);
-        int32_t* __restrict__ fpp = fp.data();
-        int32_t* __restrict__ flp = fl.data();
-        int32_t* __restrict__ fqp = fq.data();
-        for (int a = 0; a < nE; a++) {
-            if (eP[a] >= 0) pl[fpp[eP[a]]++] = a;
-            ll[flp[eL[a]]++] = a;
-        }
-        // landmark buckets filled pose by pose: each comes out in ascending pose order
-        for (int p = 0; p < nP; p++)
-            for (int j = ps[p]; j < ps[p + 1]; j++) {
-                const int a = pl[j], q = fqp[eL[a]]++;
-                ql[q] = a;
-                qp[q] = p;
-            }
-    }
-    lap("edge lists");
-    const int32_t* __restrict__ qs = S->lpStart.data();
-    const int32_t* __restrict__ ql = S->lpList.data();
-    const int32_t* __restrict__ qp = lpPose.data();
-    for (int l = 0; l < nL; l++)   // one edge per (pose, landmark)
-        for (int j = qs[l] + 1; j < qs[l + 1]; j++)
-            if (qp[j] == qp[j - 1]) return -1;
-    lap("duplicate check");
     // Schur pattern: diagonal blocks first, then blocks in order of first use (landmark order,
     // pose pairs u <= v); one pass numbers and counts, one pass fills
     std::vector<int32_t> blkOf((size_t)nP * nP, -1), bi, bj, cnt;
@@ -258,6 +182,169 @@ int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, con
     }
     lap("pair fill");
     return 0;
+}
+
+int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, const uint8_t* kfFixed,
+                   const int32_t* kfId, const int32_t* ptId, const std::vector<uint8_t>& kfAct,
+                   const std::vector<uint8_t>& ptAct, BaHostStruct* S) {
+    static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;   // the phases below (tools/)
+    using sclk = std::chrono::steady_clock;
+    auto ts0 = sclk::now();
+    auto lap = [&](const char* what) {
+        if (!say) return;
+        const auto t = sclk::now();
+        fprintf(stderr, "[ba]     lists: %s %.1f us\n", what, std::chrono::duration<double, std::micro>(t - ts0).count());
+        ts0 = t;
+    };
+    std::vector<uint8_t> freeKf(nkf);
+    for (int k = 0; k < nkf; k++) freeKf[k] = kfAct[k] && !kfFixed[k];
+    by_id(nkf, freeKf.data(), kfId, &S->poseKf);
+    by_id(npt, ptAct.data(), ptId, &S->landPt);
+    const std::vector<int32_t>& aE = S->aE;
+    const int nE = (int)aE.size(), nP = (int)S->poseKf.size(), nL = (int)S->landPt.size();
+    std::vector<int32_t> poseIdx(nkf, -1), landIdx(npt, -1);
+    for (int i = 0; i < nP; i++) poseIdx[S->poseKf[i]] = i;
+    for (int i = 0; i < nL; i++) landIdx[S->landPt[i]] = i;
+    // raw pointers below: stores through S's vectors would otherwise alias every load
+    S->ePose.resize(nE);
+    S->eLand.resize(nE);
+    S->peStart.assign(nP + 1, 0);
+    S->leStart.assign(nL + 1, 0);
+    S->lpStart.assign(nL + 1, 0);
+    {
+        int32_t* __restrict__ eP = S->ePose.data();
+        int32_t* __restrict__ eL = S->eLand.data();
+        int32_t* __restrict__ ps = S->peStart.data();
+        int32_t* __restrict__ ls = S->leStart.data();
+        int32_t* __restrict__ qs = S->lpStart.data();
+        const int32_t* __restrict__ pi = poseIdx.data();
+        const int32_t* __restrict__ li = landIdx.data();
+        const int32_t* __restrict__ ae = aE.data();
+        for (int a = 0; a < nE; a++) {
+            const int e = ae[a], p = pi[eKf[e]], l = li[ePt[e]];
+            eP[a] = p;
+            eL[a] = l;
+            const int32_t f = p >= 0;   // branch-free: fixed-pose edges count 0 (into ps[0] += 0)
+            ls[l + 1]++;
+            ps[p + 1] += f;
+            qs[l + 1] += f;
+        }
+        for (int i = 0; i < nP; i++) ps[i + 1] += ps[i];
+        for (int i = 0; i < nL; i++) {
+            ls[i + 1] += ls[i];
+            qs[i + 1] += qs[i];
+        }
+    }
+    lap("index maps + counts");
+    const int nPe = S->peStart[nP], nLe = S->leStart[nL], nLp = S->lpStart[nL];
+    S->peList.resize(std::max(nPe, 1));
+    S->leList.resize(std::max(nLe, 1));
+    S->lpList.resize(std::max(nLp, 1));
+    std::vector<int32_t> lpPose(std::max(nLp, 1));
+    {
+        const int32_t* __restrict__ eP = S->ePose.data();
+        const int32_t* __restrict__ eL = S->eLand.data();
+        const int32_t* __restrict__ ps = S->peStart.data();
+        int32_t* __restrict__ pl = S->peList.data();
+        int32_t* __restrict__ ll = S->leList.data();
+        int32_t* __restrict__ ql = S->lpList.data();
+        int32_t* __restrict__ qp = lpPose.data();
+        std::vector<int32_t> fp(S->peStart.begin(), S->peStart.end() - 1), fl(S->leStart.begin(), S->leStart.end() - 1),
+            fq(S->lpStart.begin(), S->lpStart.end() - 1);
+        int32_t* __restrict__ fpp = fp.data();
+        int32_t* __restrict__ flp = fl.data();
+        int32_t* __restrict__ fqp = fq.data();
+        for (int a = 0; a < nE; a++) {
+            if (eP[a] >= 0) pl[fpp[eP[a]]++] = a;
+            ll[flp[eL[a]]++] = a;
+        }
+        // landmark buckets filled pose by pose: each comes out in ascending pose order
+        for (int p = 0; p < nP; p++)
+            for (int j = ps[p]; j < ps[p + 1]; j++) {
+                const int a = pl[j], q = fqp[eL[a]]++;
+                ql[q] = a;
+                qp[q] = p;
+            }
+    }
+    lap("edge lists");
+    const int32_t* __restrict__ qs = S->lpStart.data();
+    const int32_t* __restrict__ ql = S->lpList.data();
+    const int32_t* __restrict__ qp = lpPose.data();
+    for (int l = 0; l < nL; l++)   // one edge per (pose, landmark)
+        for (int j = qs[l] + 1; j < qs[l + 1]; j++)
+            if (qp[j] == qp[j - 1]) return -1;
+    lap("duplicate check");
+    return ba_build_blocks(nP, nL, qs, ql, qp, S);
+}
+
+
+// The lists of a level whose active edges are a subset of an earlier structure's (A: the same
+// problem, its edges of another level set or gated since): every list of A filtered to the edges
+// now at `level`, in A's order -- edge order, id order and pose order all survive a filter -- and
+// a vertex kept while one of its edges is.  The Schur pattern is numbered again (a block's first
+// use can move).  Equal to ba_active_set + ba_build_lists on the same level (no duplicate check:
+// A's edges had none).
+int ba_refine_lists(const BaHostStruct& A, const uint8_t* edgeLevel, int level, BaHostStruct* S) {
+    const int nE1 = (int)A.aE.size(), nP1 = (int)A.poseKf.size(), nL1 = (int)A.landPt.size();
+    std::vector<int32_t> a2(std::max(nE1, 1), -1);
+    S->aE.clear();
+    for (int a = 0; a < nE1; a++)
+        if (edgeLevel[A.aE[a]] == level) {
+            a2[a] = (int)S->aE.size();
+            S->aE.push_back(A.aE[a]);
+        }
+    const int nE = (int)S->aE.size();
+    // vertices: kept while an edge of theirs is (a free pose's edges are its peList segment)
+    std::vector<int32_t> pMap(std::max(nP1, 1), -1), lMap(std::max(nL1, 1), -1);
+    S->poseKf.clear();
+    for (int i = 0; i < nP1; i++)
+        for (int j = A.peStart[i]; j < A.peStart[i + 1]; j++)
+            if (a2[A.peList[j]] >= 0) {
+                pMap[i] = (int)S->poseKf.size();
+                S->poseKf.push_back(A.poseKf[i]);
+                break;
+            }
+    S->landPt.clear();
+    for (int l = 0; l < nL1; l++)
+        for (int j = A.leStart[l]; j < A.leStart[l + 1]; j++)
+            if (a2[A.leList[j]] >= 0) {
+                lMap[l] = (int)S->landPt.size();
+                S->landPt.push_back(A.landPt[l]);
+                break;
+            }
+    const int nP = (int)S->poseKf.size(), nL = (int)S->landPt.size();
+    S->ePose.resize(nE);
+    S->eLand.resize(nE);
+    for (int a = 0; a < nE1; a++)
+        if (a2[a] >= 0) {
+            S->ePose[a2[a]] = A.ePose[a] >= 0 ? pMap[A.ePose[a]] : -1;
+            S->eLand[a2[a]] = lMap[A.eLand[a]];
+        }
+    // a filter of each vertex's segment, the vertices in their (kept) order
+    auto filter = [&](const std::vector<int32_t>& st, const std::vector<int32_t>& li, int n1,
+                      const std::vector<int32_t>& vmap, std::vector<int32_t>* st2, std::vector<int32_t>* li2,
+                      std::vector<int32_t>* pose2) {
+        st2->assign(1, 0);
+        li2->clear();
+        if (pose2) pose2->clear();
+        for (int v = 0; v < n1; v++) {
+            if (vmap[v] < 0) continue;
+            for (int j = st[v]; j < st[v + 1]; j++) {
+                const int a = a2[li[j]];
+                if (a < 0) continue;
+                li2->push_back(a);
+                if (pose2) pose2->push_back(S->ePose[a]);
+            }
+            st2->push_back((int)li2->size());
+        }
+        if (li2->empty()) li2->push_back(0);   // the sizes ba_build_lists leaves (>= 1)
+    };
+    filter(A.peStart, A.peList, nP1, pMap, &S->peStart, &S->peList, nullptr);
+    filter(A.leStart, A.leList, nL1, lMap, &S->leStart, &S->leList, nullptr);
+    std::vector<int32_t> lpPose;
+    filter(A.lpStart, A.lpList, nL1, lMap, &S->lpStart, &S->lpList, &lpPose);
+    if (lpPose.empty()) lpPose.push_back(0);
+    return ba_build_blocks(nP, nL, S->lpStart.data(), S->lpList.data(), lpPose.data(), S);
 }
 
 }  // namespace orbgpu

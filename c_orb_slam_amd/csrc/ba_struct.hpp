@@ -30,4 +30,12 @@ int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, con
                    const int32_t* kfId, const int32_t* ptId, const std::vector<uint8_t>& kfAct,
                    const std::vector<uint8_t>& ptAct, BaHostStruct* S);
 
+// The Schur pattern from built lp lists (ba_build_lists' last phases).
+int ba_build_blocks(int nP, int nL, const int32_t* qs, const int32_t* ql, const int32_t* qp, BaHostStruct* S);
+
+// The lists of `level` from an earlier structure A of the same problem whose active edges are a
+// superset (the second LocalBundleAdjustment pass after the outlier gating): A's lists filtered,
+// the Schur pattern renumbered.  Same lists as ba_active_set + ba_build_lists.
+int ba_refine_lists(const BaHostStruct& A, const uint8_t* edgeLevel, int level, BaHostStruct* S);
+
 }  // namespace orbgpu
