@@ -595,6 +595,16 @@ def main():
         Thbuf = torch.zeros(48 + cap, dtype=torch.int32).pin_memory()
         Thbuf[48:] = -1
         Tdev, Thost, cur_mp = Tbuf[:48].view(torch.float32), Thbuf[:48].view(torch.float32), Tbuf[48:]
+        # the copy as a C++ caller issues it: hipMemcpyAsync on the matcher's stream (no framework
+        # dispatch per frame); the framework copy if the runtime library cannot be bound
+        try:
+            hip_rt = C.CDLL("libamdhip64.so")
+            hip_rt.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+            hip_rt.hipMemcpyAsync.restype = C.c_int
+        except OSError:
+            hip_rt = None
+        tb_args = (C.c_void_p(Tbuf.data_ptr()), C.c_void_p(Thbuf.data_ptr()), C.c_size_t(4 * (48 + cap)), 1,
+                   C.c_void_p(match_stream.cuda_stream))
         Tpred, Tlast, Twc_l = Tdev[0:16], Tdev[16:32], Tdev[32:48]
         T1, T2 = (torch.zeros(16, dtype=torch.float32, device=dev) for _ in range(2))
         o1, o2 = (torch.zeros(cap, dtype=torch.uint8, device=dev) for _ in range(2))
@@ -714,8 +724,12 @@ def main():
                 hv[0:16] = Tp.reshape(16)
                 hv[16:32] = Tcw[t - 1].reshape(16)
                 hv[32:48] = rigid_inv(Tcw[t - 1]).reshape(16)
-                with torch.cuda.stream(match_stream):   # ordered before the matcher's launches
-                    Tbuf.copy_(Thbuf, non_blocking=True)
+                if hip_rt is not None:   # ordered before the matcher's launches (its stream)
+                    if hip_rt.hipMemcpyAsync(*tb_args) != 0:
+                        raise RuntimeError("hipMemcpyAsync")
+                else:
+                    with torch.cuda.stream(match_stream):
+                        Tbuf.copy_(Thbuf, non_blocking=True)
                 u = g["u"]
                 u.N = nlast
                 check(L.MapPoint_CreateStereo_batch_device(m._h, 1, C.byref(u)), "MapPoint_CreateStereo")
