@@ -193,6 +193,7 @@ def lib():
     L.orbgpu_comm_unique_id.argtypes = [vp]
     L.orbgpu_comm_init_rccl.argtypes = [i32, i32, vp, P(vp)]
     L.orbgpu_comm_init_local.argtypes = [i32, vp]
+    L.orbgpu_comm_init_shm.argtypes = [C.c_char_p, i32, i32, C.c_size_t, P(vp)]
     L.orbgpu_comm_rank.argtypes = [vp, P(i32), P(i32)]
     L.orbgpu_comm_destroy.argtypes = [vp]
     L.Optimizer_last_trace.argtypes = [vp, vp, i32, P(i32), vp, vp, i32, P(i32)]

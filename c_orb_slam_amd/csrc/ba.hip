@@ -2680,6 +2680,9 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
         if (P.Tcw_out) {
             if (tid < 16) P.Tcw_out[tid] = P.Tcw[tid];
             for (int i = tid; i < ne; i += blockDim.x) P.outlier[E[i].meta & 0x7fffffff] = 0;
+            // Tcw_out may be pinned host memory read by a host that polls a later kernel's signal
+            // word: write the pose back at system scope before this workgroup ends
+            if (tid < 16) __threadfence_system();
         }
         return;
     }
@@ -2994,6 +2997,7 @@ __global__ void __launch_bounds__(NT) k_pose_opt(PoseProbDev* probs, const PoseE
             }
             o[12] = o[13] = o[14] = 0.f;
             o[15] = 1.f;
+            __threadfence_system();   // see the ne < 3 exit above: host-visible before the workgroup ends
         }
         for (int i = tid; i < ne; i += blockDim.x) P.outlier[E[i].meta & 0x7fffffff] = outl[i];
     }
@@ -3342,8 +3346,8 @@ int BaEngine::stage_reserve(size_t bytes) {
 
 int BaEngine::stage2_reserve(size_t bytes) {
     if (stage2Pending_) {   // the previous structure's copy may still read the block
-        ORB_HIP_CHECK(hipStreamSynchronize(stream_));
         stage2Pending_ = false;
+        if (int e = poll_stream()) return e;
     }
     if (bytes <= hStage2Cap_) return 0;
     if (hStage2_) (void)hipHostFree(hStage2_);
@@ -3383,6 +3387,11 @@ int BaEngine::poll_stream() {
             break;
         }
         __builtin_ia32_pause();
+    }
+    const hipError_t q = hipStreamQuery(stream_);   // a sticky error of the drained work
+    if (q != hipSuccess && q != hipErrorNotReady) {
+        fprintf(stderr, "[orbgpu] HIP error %s after the stream drain\n", hipGetErrorString(q));
+        return -2;
     }
     return 0;
 }
@@ -3792,6 +3801,7 @@ int BaEngine::build_structure(int level) {
         }
         BaHostStruct& H = hs_;
         std::vector<uint8_t> kfAct, ptAct;
+        if (!eKf_ || !ePt_) return -1;   // only inside run(): the caller's edge arrays
         if (!refine) ba_active_set(level, nkf_, npt_, ne_, eKf_, ePt_, level_.data(), &H.aE, &kfAct, &ptAct);
         if (comm_) {
             // shards agree on the pose set: a keyframe is active if any shard has an active edge
@@ -3884,7 +3894,9 @@ int BaEngine::build_structure(int level) {
         stage2Pending_ = true;
         lap("pack + upload");
         // the sharded and block-sparse set-ups below stage more uploads through the same block
-        if (comm_ || nP >= kTiledMinPoses) ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+        if (comm_ || nP >= kTiledMinPoses) {
+            if (int e = poll_stream()) return e;
+        }
         const int32_t* d = dStruct_;
         st_.nE = nE; st_.nP = nP; st_.nL = nL; st_.nBlk = nBlk;
         st_.aE = d + off[0]; st_.ePose = d + off[1]; st_.eLand = d + off[2]; st_.poseKf = d + off[3];
@@ -4481,6 +4493,12 @@ int BaEngine::gate_edges(int final_check, uint8_t* erase) {
 int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, Comm* comm, const BaMode* mode) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
+    // the caller's edge arrays (upload_problem) are valid during this call only: forget them on
+    // every exit
+    struct EdgeRefs {
+        BaEngine* e;
+        ~EdgeRefs() { e->ePt_ = e->eKf_ = nullptr; }
+    } edgeRefs{this};
     trace_ = BaTrace{};
     // a one-rank group is the unsharded call: every exchange would be the identity, so none is
     // made (no collective, no host round trip per structure and stop decision)

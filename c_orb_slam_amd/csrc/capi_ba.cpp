@@ -416,6 +416,14 @@ int orbgpu_comm_init_local(int nranks, orbgpu_comm_h* out) {
     return ORB_OK;
 }
 
+int orbgpu_comm_init_shm(const char* name, int nranks, int rank, size_t max_doubles, orbgpu_comm_h* out) {
+    if (!out) return ORB_E_INVALID;
+    int rc = 0;
+    orbgpu::Comm* c = orbgpu::shm_comm_create(name, nranks, rank, max_doubles, &rc);
+    *out = reinterpret_cast<orbgpu_comm_h>(c);
+    return rc;
+}
+
 int orbgpu_comm_rank(orbgpu_comm_h h, int* rank, int* size) {
     if (!h) return ORB_E_INVALID;
     if (rank) *rank = as_comm(h)->rank();

@@ -2,9 +2,19 @@
 #include "comm.hpp"
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include <rccl/rccl.h>
 
@@ -195,6 +205,190 @@ private:
     size_t resCap_ = 0;
 };
 }  // namespace
+
+// ---------------------------------------------------------------- processes on one host (shared memory)
+namespace {
+constexpr long long kShmMagic = 0x4f52424753484d31LL;   // "ORBGSHM1"
+constexpr int kShmMaxRanks = 64;
+struct ShmHeader {
+    std::atomic<long long> magic;
+    std::atomic<int> attached;
+    std::atomic<int> arrived;
+    std::atomic<long long> gen;
+    int nranks;
+    long long cap;                       // doubles per rank slot
+    long long len[kShmMaxRanks];         // this exchange's length per rank (-1: the rank failed)
+};
+static_assert(std::atomic<long long>::is_always_lock_free && std::atomic<int>::is_always_lock_free,
+              "cross-process atomics must be lock-free");
+constexpr size_t kShmHdr = 4096;
+
+double shm_timeout_s() {
+    const char* e = std::getenv("ORBGPU_SHM_TIMEOUT");
+    return e ? std::atof(e) : 300.0;
+}
+
+class ShmComm final : public Comm {
+public:
+    ShmComm(void* base, size_t bytes, int nranks, int rank) : base_(base), bytes_(bytes) {
+        size_ = nranks;
+        rank_ = rank;
+        H_ = (ShmHeader*)base;
+    }
+    ~ShmComm() override {
+        if (res_) (void)hipHostFree(res_);
+        if (base_) munmap(base_, bytes_);
+    }
+    double* slot(int r) const { return (double*)((char*)base_ + kShmHdr) + (size_t)r * H_->cap; }
+    // every rank of the group arrives; false on timeout (a rank died or never came)
+    bool barrier() {
+        const long long g = H_->gen.load(std::memory_order_acquire);
+        if (H_->arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == size_) {
+            H_->arrived.store(0, std::memory_order_relaxed);
+            H_->gen.fetch_add(1, std::memory_order_acq_rel);
+            return true;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        const double lim = shm_timeout_s();
+        for (unsigned spin = 0; H_->gen.load(std::memory_order_acquire) == g; spin++) {
+            if (spin < 2048) {
+                __builtin_ia32_pause();
+            } else {
+                if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > lim) return false;
+                if (spin < 8192)
+                    sched_yield();
+                else
+                    std::this_thread::sleep_for(std::chrono::microseconds(50));
+            }
+        }
+        return true;
+    }
+    int allreduce(const RedBuf* bufs, int nbufs, RedOp op, hipStream_t s) override {
+        if (size_ == 1) return ORB_OK;
+        size_t tot = 0;
+        for (int i = 0; i < nbufs; i++) tot += bufs[i].n;
+        int rc = tot > (size_t)H_->cap ? ORB_E_CAPACITY : ORB_OK;
+        if (rc == ORB_OK && tot > resCap_) {
+            if (res_) (void)hipHostFree(res_);
+            res_ = nullptr;
+            resCap_ = 0;
+            if (hipHostMalloc((void**)&res_, sizeof(double) * tot) != hipSuccess)
+                rc = ORB_E_HIP;
+            else
+                resCap_ = tot;
+        }
+        size_t off = 0;   // partial -> pinned -> this rank's slot
+        for (int i = 0; i < nbufs && rc == ORB_OK; i++) {
+            if (bufs[i].n && hipMemcpyAsync(res_ + off, bufs[i].dev, sizeof(double) * bufs[i].n, hipMemcpyDeviceToHost,
+                                            s) != hipSuccess)
+                rc = ORB_E_HIP;
+            off += bufs[i].n;
+        }
+        if (rc == ORB_OK && hipStreamSynchronize(s) != hipSuccess) rc = ORB_E_HIP;
+        if (rc == ORB_OK) std::memcpy(slot(rank_), res_, sizeof(double) * tot);
+        H_->len[rank_] = rc == ORB_OK ? (long long)tot : -1;
+        if (!barrier()) return ORB_E_HIP;   // every rank's partial is in its slot
+        for (int r = 0; r < size_; r++)
+            if (H_->len[r] != (long long)tot) rc = rc == ORB_OK ? ORB_E_HIP : rc;   // a failed rank, or shapes differ
+        if (rc == ORB_OK) {   // rank order, once per element: the same bits on every rank (LocalComm's order)
+            std::memcpy(res_, slot(0), sizeof(double) * tot);
+            for (int r = 1; r < size_; r++) {
+                const double* p = slot(r);
+                if (op == RedOp::Sum)
+                    for (size_t j = 0; j < tot; j++) res_[j] = res_[j] + p[j];
+                else
+                    for (size_t j = 0; j < tot; j++) res_[j] = std::max(res_[j], p[j]);
+            }
+        }
+        if (!barrier()) return ORB_E_HIP;   // nobody reads the slots any more
+        if (rc != ORB_OK) return rc;
+        off = 0;
+        for (int i = 0; i < nbufs; i++) {
+            if (bufs[i].n && hipMemcpyAsync(bufs[i].dev, res_ + off, sizeof(double) * bufs[i].n,
+                                            hipMemcpyHostToDevice, s) != hipSuccess)
+                return ORB_E_HIP;
+            off += bufs[i].n;
+        }
+        return hipStreamSynchronize(s) == hipSuccess ? ORB_OK : ORB_E_HIP;   // res_ is reused next call
+    }
+
+private:
+    void* base_;
+    size_t bytes_;
+    ShmHeader* H_ = nullptr;
+    double* res_ = nullptr;
+    size_t resCap_ = 0;
+};
+}  // namespace
+
+Comm* shm_comm_create(const char* name, int nranks, int rank, size_t max_doubles, int* rc) {
+    *rc = ORB_E_INVALID;
+    if (!name || name[0] != '/' || nranks < 1 || nranks > kShmMaxRanks || rank < 0 || rank >= nranks || !max_doubles)
+        return nullptr;
+    const size_t bytes = kShmHdr + sizeof(double) * max_doubles * (size_t)nranks;
+    const double lim = shm_timeout_s();
+    const auto t0 = std::chrono::steady_clock::now();
+    auto waited = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+    int fd = -1;
+    if (rank == 0) {   // creates a fresh segment (a stale one of the same name is replaced)
+        shm_unlink(name);
+        fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) {
+            if (fd >= 0) close(fd);
+            *rc = ORB_E_HIP;
+            return nullptr;
+        }
+    } else {   // waits for rank 0's segment
+        while ((fd = shm_open(name, O_RDWR, 0600)) < 0) {
+            if (waited() > lim) {
+                *rc = ORB_E_HIP;
+                return nullptr;
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        }
+        struct stat st;
+        while (fstat(fd, &st) == 0 && (size_t)st.st_size < bytes) {
+            if (waited() > lim) break;
+            std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        }
+    }
+    void* base = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (base == MAP_FAILED) {
+        *rc = ORB_E_HIP;
+        return nullptr;
+    }
+    ShmHeader* H = (ShmHeader*)base;
+    if (rank == 0) {
+        H->nranks = nranks;
+        H->cap = (long long)max_doubles;
+        H->magic.store(kShmMagic, std::memory_order_release);
+    } else {
+        while (H->magic.load(std::memory_order_acquire) != kShmMagic) {
+            if (waited() > lim) {
+                munmap(base, bytes);
+                *rc = ORB_E_HIP;
+                return nullptr;
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        if (H->nranks != nranks || H->cap != (long long)max_doubles) {   // the ranks disagree on the group
+            munmap(base, bytes);
+            *rc = ORB_E_INVALID;
+            return nullptr;
+        }
+    }
+    H->attached.fetch_add(1, std::memory_order_acq_rel);
+    ShmComm* c = new ShmComm(base, bytes, nranks, rank);
+    if (!c->barrier()) {   // every rank attached
+        delete c;
+        *rc = ORB_E_HIP;
+        return nullptr;
+    }
+    if (rank == 0) shm_unlink(name);   // the mappings stay; no name is left behind in /dev/shm
+    *rc = ORB_OK;
+    return c;
+}
 
 std::vector<Comm*> local_comm_group(int nranks) {
     auto g = std::make_shared<LocalGroup>(nranks);

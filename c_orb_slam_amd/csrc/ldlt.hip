@@ -629,6 +629,149 @@ __global__ void __launch_bounds__(256) k_ldlt_ptrail(SpDev S, int j0) {
         }
 }
 
+// Quadrant forms of k_ldlt_update / k_ldlt_ptrail.  A 64 x 64 tile update is 524 k FP64
+// operations per pivot tile K: one CU (four SIMDs, 16 FP64 lanes each) needs >= 8 k cycles per K
+// whatever its thread count, and a top-level target gathers tens of descendant K in sequence.
+// Four workgroups per target tile, each owning a 32 x 32 quadrant (qi, qj), put four CUs on it:
+// 256 threads, 2 x 2 register micro-tiles (rows 2ty, 2ty+1, columns 2tx, 2tx+1, each pair one
+// 16-B LDS read), per K the quadrant's 32 rows of L(I, K) and 32 columns of U(K, J) staged in LDS
+// (2 x 16 KB) while the next K's operands are already in flight to registers.  Per element the
+// sequence is unchanged (K ascending, k ascending, a -= l * u with one rounding per product and
+// per subtraction): the split is spatial only, so the factor is bit-identical.
+constexpr int LQ = LT / 2;   // quadrant edge
+
+typedef double d2v __attribute__((ext_vector_type(2)));   // native vector: stays in registers (HIP's
+                                                         // double2 wrapper was demoted to scratch here)
+struct QuadOps {   // one K's operands of a quadrant, 4 x 16 B per thread and operand
+    d2v l[4], u[4];
+};
+__device__ __forceinline__ void quad_load(QuadOps& o, const double* Lsrc, const double* Usrc, int qi, int qj, int gt) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int e = gt + 256 * u, k = e >> 4, c2 = e & 15;
+        o.l[u] = *(const d2v*)(Lsrc + k * LT + LQ * qi + 2 * c2);
+        o.u[u] = *(const d2v*)(Usrc + k * LT + LQ * qj + 2 * c2);
+    }
+}
+__device__ __forceinline__ void quad_stage(const QuadOps& o, d2v* Lg, d2v* Ug, int gt) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        Lg[gt + 256 * u] = o.l[u];   // [k][pair of quadrant rows]
+        Ug[gt + 256 * u] = o.u[u];   // [k][pair of quadrant columns]
+    }
+}
+__device__ __forceinline__ void quad_apply(double (&acc)[2][2], const d2v* Lg, const d2v* Ug, int kw, int ty,
+                                           int tx) {
+    for (int k = 0; k < kw; k++) {
+        const d2v l = Lg[k * (LQ / 2) + ty];
+        const d2v u = Ug[k * (LQ / 2) + tx];
+        acc[0][0] -= l.x * u.x;
+        acc[0][1] -= l.x * u.y;
+        acc[1][0] -= l.y * u.x;
+        acc[1][1] -= l.y * u.y;
+    }
+}
+__device__ __forceinline__ void quad_init(double (&acc)[2][2], const double* T, int qi, int qj, int ty, int tx, int ih,
+                                          int jw) {
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+            const int i = LQ * qi + 2 * ty + a, j = LQ * qj + 2 * tx + b;
+            acc[a][b] = (i < ih && j < jw) ? T[i * LT + j] : 0.0;
+        }
+}
+__device__ __forceinline__ void quad_store(const double (&acc)[2][2], double* T, int qi, int qj, int ty, int tx, int ih,
+                                           int jw, bool diag) {
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+            const int i = LQ * qi + 2 * ty + a, j = LQ * qj + 2 * tx + b;
+            if (i < ih && j < jw && (!diag || i <= j)) T[i * LT + j] = acc[a][b];
+        }
+}
+
+// the first K pair at or after q that contributes (block-uniform: every thread reads the same words)
+__device__ __forceinline__ int upd_next(const SpDev& S, int q, int kp1) {
+    for (; q < kp1; q++) {
+        const int4 kp = S.kps[q];
+        if (S.lnz[kp.x] && S.lnz[kp.y] && !skip_k(S, kp.z)) break;
+    }
+    return q;
+}
+
+__global__ void __launch_bounds__(256) k_ldlt_update_q(SpDev S, int t0) {
+    __shared__ d2v Lg[LT * LQ / 2];
+    __shared__ d2v Ug[LT * LQ / 2];
+    if (*(volatile int*)S.fail) return;
+    const int ti = t0 + (blockIdx.x >> 2), qd = blockIdx.x & 3, qi = qd >> 1, qj = qd & 1;
+    const int4 tg = S.tgts[ti];
+    const int kp0 = tg.w, kp1 = S.tgts[ti + 1].w;
+    const int I = tg.y, J = tg.z;
+    if (skip_tile(S, I)) return;
+    const int ih = S.th[I], jw = S.th[J];
+    if ((I == J && qi > qj) || LQ * qi >= ih || LQ * qj >= jw) return;   // a quadrant nobody stores
+    const int gt = threadIdx.x, ty = gt >> 4, tx = gt & 15;
+    double* T = S.dst ? S.dst + (size_t)S.packIdx[tg.x] * (LT * LT) : S.U + (size_t)tg.x * (LT * LT);
+    double acc[2][2];
+    quad_init(acc, T, qi, qj, ty, tx, ih, jw);
+    // (the operand loads are unconditional -- past the last K they re-read its tiles -- so the
+    // register buffer is not demoted to scratch; a target always has a K pair, k_ldlt build)
+    QuadOps ops;
+    int q = upd_next(S, kp0, kp1);
+    int4 kp = S.kps[q < kp1 ? q : kp0];
+    quad_load(ops, S.LT + (size_t)kp.x * (LT * LT), S.U + (size_t)kp.y * (LT * LT), qi, qj, gt);
+    while (q < kp1) {
+        const int kw = S.th[kp.z];
+        __syncthreads();   // the previous K's LDS reads are done
+        quad_stage(ops, Lg, Ug, gt);
+        __syncthreads();
+        q = upd_next(S, q + 1, kp1);
+        if (q < kp1) kp = S.kps[q];
+        // the next K's operands travel while this one is applied
+        quad_load(ops, S.LT + (size_t)kp.x * (LT * LT), S.U + (size_t)kp.y * (LT * LT), qi, qj, gt);
+        quad_apply(acc, Lg, Ug, kw, ty, tx);
+    }
+    quad_store(acc, T, qi, qj, ty, tx, ih, jw, I == J);
+}
+
+__global__ void __launch_bounds__(256) k_ldlt_ptrail_q(SpDev S, int j0) {
+    __shared__ d2v Lg[LT * LQ / 2];
+    __shared__ d2v Ug[LT * LQ / 2];
+    if (*(volatile int*)S.fail) return;
+    const int2 job = S.pairJobs[j0 + (blockIdx.x >> 2)];   // (panel, pair index)
+    const int qd = blockIdx.x & 3, qi = qd >> 1, qj = qd & 1;
+    const int p = job.x;
+    if (skip_tile(S, p)) return;
+    const int rs = S.rowStart[p];
+    const int4 pr = S.pairs[S.pairStart[p] + job.y];
+    const int slI = S.rowSlot[rs + pr.x], slJ = S.rowSlot[rs + pr.y];
+    if (!S.lnz[slI] || !S.lnz[slJ]) return;   // block-uniform
+    const int I = S.rowJ[rs + pr.x], J = S.rowJ[rs + pr.y];
+    const int ih = S.th[I], jw = S.th[J], pw = S.th[p];
+    if ((I == J && qi > qj) || LQ * qi >= ih || LQ * qj >= jw) return;
+    const int gt = threadIdx.x, ty = gt >> 4, tx = gt & 15;
+    QuadOps ops;
+    quad_load(ops, S.LT + (size_t)slI * (LT * LT), S.U + (size_t)slJ * (LT * LT), qi, qj, gt);
+    double* T = S.U + (size_t)pr.z * (LT * LT);
+    double acc[2][2];
+    quad_init(acc, T, qi, qj, ty, tx, ih, jw);
+    quad_stage(ops, Lg, Ug, gt);
+    __syncthreads();
+    quad_apply(acc, Lg, Ug, pw, ty, tx);
+    quad_store(acc, T, qi, qj, ty, tx, ih, jw, I == J);
+}
+
+// ORBGPU_LDLT_QUAD=0 keeps the one-workgroup-per-tile update and trailing kernels (A/B)
+static bool quad_updates() {
+    static const bool v = [] {
+        const char* e = getenv("ORBGPU_LDLT_QUAD");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // L y = b on the rows of each node of a level (one wave per node; lane = row): the descendants'
 // y are final.
 __global__ void __launch_bounds__(64) k_ldlt_pfwd(SpDev S, int n0, const double* __restrict__ b) {
@@ -748,6 +891,252 @@ __device__ __forceinline__ double sweep_chain_bwd(double acc, const double* Lo, 
     for (int k = LT - 1; k >= 0; k--)
         if (k < kh) acc = acc - Lr[k] * rdlane(xk, k);
     return acc;
+}
+
+// The same chains with the pivot values read as wave-uniform LDS operands (vsh[k], one broadcast
+// read each) instead of a cross-lane readlane per step: the products no longer wait on a
+// broadcast, and the chain is one dependent subtraction per step.
+__device__ __forceinline__ double sweep_chain_fwd_u(double acc, const double* Lo, int lane, const double* vsh, int kh) {
+    double Lr[LT];
+#pragma unroll
+    for (int k = 0; k < LT; k++) Lr[k] = Lo[k * LT + lane];   // L[I0 + lane][K0 + k]
+#pragma unroll
+    for (int k = 0; k < LT; k++)
+        if (k < kh) acc = acc - Lr[k] * vsh[k];
+    return acc;
+}
+__device__ __forceinline__ double sweep_chain_bwd_u(double acc, const double* Lo, int lane, const double* vsh, int kh) {
+    double Lr[LT];
+#pragma unroll
+    for (int k = 0; k < LT; k++) Lr[k] = Lo[lane * LT + k];   // L[K0 + k][I0 + lane]
+#pragma unroll
+    for (int k = LT - 1; k >= 0; k--)
+        if (k < kh) acc = acc - Lr[k] * vsh[k];
+    return acc;
+}
+
+// A tile row's contributions from outside its node, software-pipelined over the row's pivot tiles:
+// 16-row chunks of each L tile double-buffered in registers (the next chunk, and at a tile's last
+// chunk the next tile's first, in flight while one is applied), the tile's y / x staged in the
+// wave's LDS slot `vsh` and read wave-uniform.  Forward: descendant tiles K < T0, K ascending, k
+// ascending; backward: ancestor tiles J >= T1, J descending, k descending.  Per row the
+// subtraction sequence of k_ldlt_pfwd / k_ldlt_backward.  *eStop: the first list entry inside the
+// node (forward) / the last one inside it (backward).
+constexpr int SCH = 16;   // pivot rows per register chunk
+__device__ __forceinline__ void fwd_chunk_load(double (&r)[SCH], const double* Lo, int c, int lane) {
+#pragma unroll
+    for (int t = 0; t < SCH; t++) r[t] = Lo[(SCH * c + t) * LT + lane];
+}
+__device__ __forceinline__ double fwd_chunk_apply(double acc, const double (&r)[SCH], const double* vsh, int c, int kh) {
+#pragma unroll
+    for (int t = 0; t < SCH; t++)
+        if (SCH * c + t < kh) acc = acc - r[t] * vsh[SCH * c + t];
+    return acc;
+}
+__device__ double fwd_outside(const SpDev& S, int I, int T0, double acc, int lane, double* vsh, int* eStop) {
+    const int e1 = S.colStart[I + 1];
+    int eS = S.colStart[I];
+    while (eS < e1 && S.colK[eS] < T0) eS++;   // ascending K: the descendants come first
+    *eStop = eS;
+    auto nextv = [&](int e) {
+        while (e < eS && (!S.lnz[S.colSlot[e]] || skip_k(S, S.colK[e]))) e++;
+        return e;
+    };
+    int e = nextv(S.colStart[I]);
+    double A[SCH], Bq[SCH];
+    double yv = 0.0;
+    if (e < eS) {
+        fwd_chunk_load(A, S.LT + (size_t)S.colSlot[e] * (LT * LT), 0, lane);
+        yv = S.y[S.colK[e] * LT + lane];
+    }
+    while (e < eS) {
+        const int kh = S.th[S.colK[e]];
+        const double* Lo = S.LT + (size_t)S.colSlot[e] * (LT * LT);
+        vsh[lane] = yv;
+        __builtin_amdgcn_wave_barrier();
+        const int en = nextv(e + 1);
+        fwd_chunk_load(Bq, Lo, 1, lane);
+        acc = fwd_chunk_apply(acc, A, vsh, 0, kh);
+        fwd_chunk_load(A, Lo, 2, lane);
+        acc = fwd_chunk_apply(acc, Bq, vsh, 1, kh);
+        fwd_chunk_load(Bq, Lo, 3, lane);
+        acc = fwd_chunk_apply(acc, A, vsh, 2, kh);
+        if (en < eS) {   // the next tile's first chunk and y travel during this tile's last chunk
+            fwd_chunk_load(A, S.LT + (size_t)S.colSlot[en] * (LT * LT), 0, lane);
+            yv = S.y[S.colK[en] * LT + lane];
+        }
+        acc = fwd_chunk_apply(acc, Bq, vsh, 3, kh);
+        __builtin_amdgcn_wave_barrier();
+        e = en;
+    }
+    return acc;
+}
+__device__ __forceinline__ void bwd_chunk_load(double (&r)[SCH], const double* Lo, int c, int lane) {
+#pragma unroll
+    for (int t = 0; t < SCH; t += 2) {   // L[K0 + k][I0 + lane] for k = 16c + t, 16c + t + 1: one 16-B load
+        const double2 v = *(const double2*)(Lo + lane * LT + SCH * c + t);
+        r[t] = v.x;
+        r[t + 1] = v.y;
+    }
+}
+__device__ __forceinline__ double bwd_chunk_apply(double acc, const double (&r)[SCH], const double* vsh, int c, int kh) {
+#pragma unroll
+    for (int t = SCH - 1; t >= 0; t--)
+        if (SCH * c + t < kh) acc = acc - r[t] * vsh[SCH * c + t];
+    return acc;
+}
+__device__ double bwd_outside(const SpDev& S, int I, int T1, double acc, int lane, double* vsh, int* eStop) {
+    const int e0 = S.rowStart[I];
+    int eS = S.rowStart[I + 1] - 1;
+    while (eS >= e0 && S.rowJ[eS] >= T1) eS--;   // descending J: the ancestors come first
+    *eStop = eS;
+    auto nextv = [&](int e) {
+        while (e > eS && !S.lnz[S.rowSlot[e]]) e--;
+        return e;
+    };
+    int e = nextv(S.rowStart[I + 1] - 1);
+    double A[SCH], Bq[SCH];
+    double xv = 0.0;
+    if (e > eS) {
+        bwd_chunk_load(A, S.LT + (size_t)S.rowSlot[e] * (LT * LT), 3, lane);
+        const int J = S.rowJ[e];
+        xv = lane < S.th[J] ? S.xs[J * LT + lane] : 0.0;
+    }
+    while (e > eS) {
+        const int kh = S.th[S.rowJ[e]];
+        const double* Lo = S.LT + (size_t)S.rowSlot[e] * (LT * LT);
+        vsh[lane] = xv;
+        __builtin_amdgcn_wave_barrier();
+        const int en = nextv(e - 1);
+        bwd_chunk_load(Bq, Lo, 2, lane);
+        acc = bwd_chunk_apply(acc, A, vsh, 3, kh);
+        bwd_chunk_load(A, Lo, 1, lane);
+        acc = bwd_chunk_apply(acc, Bq, vsh, 2, kh);
+        bwd_chunk_load(Bq, Lo, 0, lane);
+        acc = bwd_chunk_apply(acc, A, vsh, 1, kh);
+        if (en > eS) {
+            bwd_chunk_load(A, S.LT + (size_t)S.rowSlot[en] * (LT * LT), 3, lane);
+            const int J = S.rowJ[en];
+            xv = lane < S.th[J] ? S.xs[J * LT + lane] : 0.0;
+        }
+        acc = bwd_chunk_apply(acc, Bq, vsh, 0, kh);
+        __builtin_amdgcn_wave_barrier();
+        e = en;
+    }
+    return acc;
+}
+
+// The node sweeps with the pipelined outside phase and wave-uniform LDS operands (ORBGPU_LDLT_SWEEP=2
+// keeps k_ldlt_fwdn / k_ldlt_bwdn for A/B).  Same per-row sequences.
+__global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_fwdn_u(SpDev S, int n0, const double* __restrict__ b) {
+    extern __shared__ double accs[];   // [tile - T0][lane]
+    __shared__ int cur[kSweepMaxTiles];
+    __shared__ double vsh[kSweepWaves][LT];
+    if (*(volatile int*)S.fail) return;
+    const int node = S.levNodes[n0 + blockIdx.x];
+    const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    if (T1 > T0 && skip_tile(S, T0)) return;
+    const int W = blockDim.x >> 6, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int I = T0 + w; I < T1; I += W) {
+        const int I0 = I * LT;
+        double acc = lane < S.th[I] ? b[S.rowMap[I0 + lane]] : 0.0;
+        int e;
+        acc = fwd_outside(S, I, T0, acc, lane, vsh[w], &e);
+        accs[(I - T0) * LT + lane] = acc;
+        if (lane == 0) cur[I - T0] = e;
+    }
+    __syncthreads();
+    for (int s = 0; s < T1 - T0; s++) {
+        const int K = T0 + s, K0 = K * LT, kh = S.th[K];
+        if (s % W == w) {   // the owner: diagonal tile, y_K final
+            const bool on = lane < kh;
+            double acc = accs[s * LT + lane];
+            const double* Ud = S.U + (size_t)S.slotOf[(size_t)K * S.nt + K] * (LT * LT);
+            double Lr[LT];
+#pragma unroll
+            for (int k = 0; k < LT; k++) Lr[k] = (on && k < lane) ? Ud[lane * LT + k] : 0.0;
+#pragma unroll
+            for (int k = 0; k < LT; k++) {
+                if (k < kh) {
+                    const double v = acc - Lr[k] * rdlane(acc, k);
+                    acc = lane > k ? v : acc;
+                }
+            }
+            acc = on ? acc : 0.0;
+            S.y[K0 + lane] = acc;
+            accs[s * LT + lane] = acc;
+        }
+        __syncthreads();
+        for (int I = T0 + w; I < T1; I += W) {
+            if (I <= K) continue;
+            const int e = cur[I - T0];
+            if (e >= S.colStart[I + 1] || S.colK[e] != K) continue;   // no block (K, I)
+            if (lane == 0) cur[I - T0] = e + 1;
+            const int sl = S.colSlot[e];
+            if (!S.lnz[sl]) continue;
+            accs[(I - T0) * LT + lane] =
+                sweep_chain_fwd_u(accs[(I - T0) * LT + lane], S.LT + (size_t)sl * (LT * LT), lane, accs + s * LT, kh);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_bwdn_u(SpDev S, int n0, double* __restrict__ x, double* scal,
+                                                                  int first) {
+    extern __shared__ double accs[];
+    __shared__ int cur[kSweepMaxTiles];
+    __shared__ double vsh[kSweepWaves][LT];
+    const int lane = threadIdx.x & 63;
+    const int failed = *(volatile int*)S.fail;
+    if (first && blockIdx.x == 0 && threadIdx.x == 0) scal[3] = failed ? 0.0 : 1.0;
+    if (failed) return;
+    const int node = S.levNodes[n0 + blockIdx.x];
+    const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    if (T1 > T0 && skip_tile(S, T0)) return;
+    const int W = blockDim.x >> 6, w = threadIdx.x >> 6;
+    for (int I = T0 + w; I < T1; I += W) {
+        const int I0 = I * LT;
+        const double* Ud = S.U + (size_t)S.slotOf[(size_t)I * S.nt + I] * (LT * LT);
+        double acc = lane < S.th[I] ? S.y[I0 + lane] / Ud[lane * LT + lane] : 0.0;
+        int e;
+        acc = bwd_outside(S, I, T1, acc, lane, vsh[w], &e);
+        accs[(I - T0) * LT + lane] = acc;
+        if (lane == 0) cur[I - T0] = e;
+    }
+    __syncthreads();
+    for (int s = T1 - T0 - 1; s >= 0; s--) {
+        const int K = T0 + s, K0 = K * LT, kh = S.th[K];
+        if (s % W == w) {   // the owner: diagonal tile, x_K final
+            const bool on = lane < kh;
+            double acc = accs[s * LT + lane];
+            const double* Ud = S.U + (size_t)S.slotOf[(size_t)K * S.nt + K] * (LT * LT);
+            double Lr[LT];
+#pragma unroll
+            for (int k = 0; k < LT; k++) Lr[k] = (on && k < kh) ? Ud[k * LT + lane] : 0.0;   // L[K0 + k][K0 + lane]
+#pragma unroll
+            for (int k = LT - 1; k >= 0; k--) {
+                if (k < kh) {
+                    const double v = acc - Lr[k] * rdlane(acc, k);
+                    acc = lane < k ? v : acc;
+                }
+            }
+            acc = on ? acc : 0.0;
+            S.xs[K0 + lane] = acc;
+            if (on) x[S.rowMap[K0 + lane]] = acc;
+            accs[s * LT + lane] = acc;
+        }
+        __syncthreads();
+        for (int I = T0 + w; I < K; I += W) {
+            const int e = cur[I - T0];
+            if (e < S.rowStart[I] || S.rowJ[e] != K) continue;   // no block (I, K)
+            if (lane == 0) cur[I - T0] = e - 1;
+            const int sl = S.rowSlot[e];
+            if (!S.lnz[sl]) continue;
+            accs[(I - T0) * LT + lane] =
+                sweep_chain_bwd_u(accs[(I - T0) * LT + lane], S.LT + (size_t)sl * (LT * LT), lane, accs + s * LT, kh);
+        }
+        __syncthreads();
+    }
 }
 
 __global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_fwdn(SpDev S, int n0, const double* __restrict__ b) {
@@ -874,14 +1263,16 @@ __global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_bwdn(SpDev S, int n0,
     }
 }
 
-// ORBGPU_LDLT_SWEEP=1 keeps the one-wave-per-node sweeps (A/B)
-static bool sweep_nodes() {
-    static const bool v = [] {
+// ORBGPU_LDLT_SWEEP=1 keeps the one-wave-per-node sweeps, =2 the node sweeps with cross-lane
+// broadcasts (A/B); default: the pipelined node sweeps (k_ldlt_fwdn_u / k_ldlt_bwdn_u)
+static int sweep_mode() {
+    static const int v = [] {
         const char* e = getenv("ORBGPU_LDLT_SWEEP");
-        return !(e && atoi(e) == 1);
+        return e ? atoi(e) : 0;
     }();
     return v;
 }
+static bool sweep_nodes() { return sweep_mode() != 1; }
 
 int ldlt_debug_prof(unsigned long long* out8) {
 #ifdef ORBGPU_PROF
@@ -1240,7 +1631,12 @@ SpDev SparseLdlt::dev() const {
 
 void SparseLdlt::enqueue_factor_level(const SpDev& d, int h, const double* b, hipStream_t s) {
     const int nt = hLevTgtStart_[h + 1] - hLevTgtStart_[h];
-    if (nt > 0) hipLaunchKernelGGL(k_ldlt_update, dim3(nt), dim3(256), 0, s, d, hLevTgtStart_[h]);
+    if (nt > 0) {
+        if (quad_updates())
+            hipLaunchKernelGGL(k_ldlt_update_q, dim3(4 * nt), dim3(256), 0, s, d, hLevTgtStart_[h]);
+        else
+            hipLaunchKernelGGL(k_ldlt_update, dim3(nt), dim3(256), 0, s, d, hLevTgtStart_[h]);
+    }
     for (int st = hLevStepStart_[h]; st < hLevStepStart_[h + 1]; st++) {
         const int4 a = hSteps_[st], z = hSteps_[st + 1];
         if (z.x > a.x) {
@@ -1259,13 +1655,18 @@ void SparseLdlt::enqueue_factor_level(const SpDev& d, int h, const double* b, hi
                 hipLaunchKernelGGL(rolled_panels() ? k_ldlt_prow_r : k_ldlt_prow, dim3(z.y - a.y), dim3(64), 0, s, d,
                                    a.y);
         }
-        if (z.z > a.z) hipLaunchKernelGGL(k_ldlt_ptrail, dim3(z.z - a.z), dim3(256), 0, s, d, a.z);
+        if (z.z > a.z) {
+            if (quad_updates())
+                hipLaunchKernelGGL(k_ldlt_ptrail_q, dim3(4 * (z.z - a.z)), dim3(256), 0, s, d, a.z);
+            else
+                hipLaunchKernelGGL(k_ldlt_ptrail, dim3(z.z - a.z), dim3(256), 0, s, d, a.z);
+        }
     }
     const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
     const int mt = hLevMaxT_[h];
     if (sweep_nodes() && mt > 1 && mt <= kSweepMaxTiles)
-        hipLaunchKernelGGL(k_ldlt_fwdn, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)), sizeof(double) * LT * mt, s, d,
-                           hLevNodeStart_[h], b);
+        hipLaunchKernelGGL(sweep_mode() == 2 ? k_ldlt_fwdn : k_ldlt_fwdn_u, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)),
+                           sizeof(double) * LT * mt, s, d, hLevNodeStart_[h], b);
     else
         hipLaunchKernelGGL(k_ldlt_pfwd, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], b);
 }
@@ -1274,8 +1675,8 @@ void SparseLdlt::enqueue_backward_level(const SpDev& d, int h, double* x, double
     const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
     const int mt = hLevMaxT_[h];
     if (sweep_nodes() && mt > 1 && mt <= kSweepMaxTiles)
-        hipLaunchKernelGGL(k_ldlt_bwdn, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)), sizeof(double) * LT * mt, s, d,
-                           hLevNodeStart_[h], x, scal, first);
+        hipLaunchKernelGGL(sweep_mode() == 2 ? k_ldlt_bwdn : k_ldlt_bwdn_u, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)),
+                           sizeof(double) * LT * mt, s, d, hLevNodeStart_[h], x, scal, first);
     else
         hipLaunchKernelGGL(k_ldlt_backward, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], x, scal, first);
 }
@@ -1440,7 +1841,12 @@ int SparseLdlt::solve_dist(double* b, double* x, double* scal, hipStream_t s, Co
     db.packIdx = dPackIdx_;
     for (int h = 0; h < nLev_; h++) {
         const int nt = hLevTgtStart_[h + 1] - hLevTgtStart_[h];
-        if (levSh_[h] && nt > 0) hipLaunchKernelGGL(k_ldlt_update, dim3(nt), dim3(256), 0, s, db, hLevTgtStart_[h]);
+        if (levSh_[h] && nt > 0) {
+            if (quad_updates())
+                hipLaunchKernelGGL(k_ldlt_update_q, dim3(4 * nt), dim3(256), 0, s, db, hLevTgtStart_[h]);
+            else
+                hipLaunchKernelGGL(k_ldlt_update, dim3(nt), dim3(256), 0, s, db, hLevTgtStart_[h]);
+        }
     }
     if (nShT_) hipLaunchKernelGGL(k_ldlt_fwd_part, dim3(nShT_), dim3(64), 0, s, d, b, dShT_, xb + nxb);
     ORB_HIP_CHECK(hipGetLastError());

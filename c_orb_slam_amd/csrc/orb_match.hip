@@ -84,34 +84,48 @@ __global__ void k_stream_signal(volatile int* w, int v) {
     if (threadIdx.x == 0) *w = v;
 }
 
+// The calling thread's pinned signal word, freed when the thread ends (thread pools that create and
+// drop threads do not leak pinned pages).
+struct SignalWord {
+    volatile int* word = nullptr;
+    int seq = 0;
+    bool tried = false;
+    ~SignalWord() {
+        if (word) (void)hipHostFree((void*)word);
+    }
+};
+
+// Drains stream s by spinning on a word a one-thread kernel writes behind the queued work: the
+// calling thread spins one CPU core for up to 50 ms per call (then falls back to a blocking
+// hipStreamSynchronize).  A blocking sync woke 20-40 us late.  Once the word is seen,
+// hipStreamQuery reports an asynchronous failure of the drained work, as hipStreamSynchronize would.
 hipError_t stream_wait(hipStream_t s) {
-    thread_local volatile int* word = nullptr;
-    thread_local int seq = 0;
-    thread_local bool tried = false;
+    thread_local SignalWord sw;
     static const bool blocking = [] {   // ORBGPU_SYNC_BLOCKING=1: plain hipStreamSynchronize (A/B)
         const char* e = std::getenv("ORBGPU_SYNC_BLOCKING");
         return e && e[0] == '1';
     }();
     if (blocking) return hipStreamSynchronize(s);
-    if (!word && !tried) {
-        tried = true;
+    if (!sw.word && !sw.tried) {
+        sw.tried = true;
         void* p = nullptr;
         if (hipHostMalloc(&p, 64, hipHostMallocCoherent) == hipSuccess) {
             std::memset(p, 0, 64);
-            word = (volatile int*)p;
+            sw.word = (volatile int*)p;
         }
     }
-    if (!word) return hipStreamSynchronize(s);
-    const int v = ++seq;
-    hipLaunchKernelGGL(k_stream_signal, dim3(1), dim3(64), 0, s, word, v);
+    if (!sw.word) return hipStreamSynchronize(s);
+    const int v = ++sw.seq;
+    hipLaunchKernelGGL(k_stream_signal, dim3(1), dim3(64), 0, s, sw.word, v);
     if (hipError_t e = hipGetLastError()) return e;
     const auto t0 = std::chrono::steady_clock::now();
-    for (unsigned spin = 1; *word != v; spin++) {
+    for (unsigned spin = 1; *sw.word != v; spin++) {
         if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
             return hipStreamSynchronize(s);
         __builtin_ia32_pause();
     }
-    return hipSuccess;
+    const hipError_t q = hipStreamQuery(s);   // the signal kernel has run: only a sticky error remains
+    return q == hipErrorNotReady ? hipSuccess : q;
 }
 
 __global__ void __launch_bounds__(256) k_build_grid(SearchDev* probs, int dropOccupied) {

@@ -333,6 +333,15 @@ class Comm:
         check(lib().orbgpu_comm_init_local(int(nranks), hs), "orbgpu_comm_init_local")
         return [cls(C.c_void_p(h)) for h in hs]
 
+    @classmethod
+    def shm(cls, name, nranks, rank, max_doubles):
+        """One process per rank on one host (orbgpu_comm_init_shm): every rank passes the same fresh
+        name ("/..."), nranks and max_doubles (the largest exchange in doubles)."""
+        h = C.c_void_p()
+        check(lib().orbgpu_comm_init_shm(name.encode(), int(nranks), int(rank), int(max_doubles), C.byref(h)),
+              "orbgpu_comm_init_shm")
+        return cls(h)
+
     @property
     def rank_size(self):
         r, s = C.c_int(), C.c_int()

@@ -813,6 +813,13 @@ int orbgpu_comm_unique_id(uint8_t* id128);
 int orbgpu_comm_init_rccl(int nranks, int rank, const uint8_t* id128, orbgpu_comm_h* out);
 /* `nranks` in-process ranks (one host thread each, one device): out[0..nranks). */
 int orbgpu_comm_init_local(int nranks, orbgpu_comm_h* out);
+/* One process per rank on one host (e.g. several ranks sharing one GPU, where RCCL cannot place
+ * them): every rank calls this with the same fresh POSIX shm name ("/..."), nranks and
+ * max_doubles (the largest exchange, in doubles); rank 0 creates the segment, the others attach
+ * (bounded wait, ORBGPU_SHM_TIMEOUT s, default 300), and the name is unlinked once all attached.
+ * Partials go through host memory and are summed in rank order on every rank (the in-process
+ * group's order).  ORB_E_CAPACITY if an exchange exceeds max_doubles. */
+int orbgpu_comm_init_shm(const char* name, int nranks, int rank, size_t max_doubles, orbgpu_comm_h* out);
 int orbgpu_comm_rank(orbgpu_comm_h h, int* rank, int* size);
 int orbgpu_comm_destroy(orbgpu_comm_h h);
 /* Keyframe-block partition: pt_rank[p] = rank owning point p.  Reference keyframe

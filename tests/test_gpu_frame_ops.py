@@ -5,6 +5,9 @@
 * Optimizer::PoseOptimization(Frame*) in the frame form (map points as indices into a table,
   keypoints, mvuRight, the mvInvLevelSigma2 table; Optimizer.cc:255-347) -- identical to the
   packed device form and to the oracle (Tcw bits, outlier flags, nInliers)."""
+import sys
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -240,3 +243,45 @@ def test_deferred_and_synchronous_pose_interleaved(gpu):
         for f in range(len(T)):
             assert np.array_equal(T[f].cpu().numpy(), rT[f]), (name, f)
             assert np.array_equal(o[f].cpu().numpy(), ro[f]), (name, f)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_pose_output_in_pinned_host_memory_visible_on_return(gpu, seed):
+    """Optimizer_PoseOptimization_frames_device with Tcw_out in pinned host memory (torch's default,
+    non-coherent pinned pages, and coherent ones): the pose the host reads the moment the call
+    returns (the library's polled stream drain) equals the same call's device-buffer output read
+    after a blocking device synchronisation, and the oracle's pose (bench.py's latency leg reads
+    its final pose this way)."""
+    import torch
+    from c_orb_slam_amd.optimizer import PoseOptimizationFramesDevice
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from bench import _coherent_host_f32
+    dev = torch.device("cuda", 0)
+    frames = [pose_problem(900 + 10 * seed + s, N=350 + 300 * s) for s in range(4)]
+    framed = []
+    for fr in frames:
+        N = len(fr["has_mp"])
+        octv, tab = _octaves(fr["inv_sigma2"])
+        k = np.zeros(N, oracle_lib.KP_DTYPE)
+        k["x"], k["y"], k["octave"] = fr["obs"][:, 0], fr["obs"][:, 1], octv
+        mp = np.where(fr["has_mp"] > 0, np.arange(N), -1).astype(np.int32)
+        framed.append(dict(Tcw=torch.from_numpy(np.ascontiguousarray(fr["Tcw"], np.float32).reshape(16)).to(dev),
+                           mp=torch.from_numpy(mp).to(dev), mp_pos=torch.from_numpy(fr["Xw"]).to(dev),
+                           keysUn=torch.from_numpy(k.view(np.int32).reshape(N, 7).copy()).to(dev),
+                           uRight=torch.from_numpy(np.ascontiguousarray(fr["obs"][:, 2])).to(dev),
+                           invLevelSigma2=torch.from_numpy(tab).to(dev), cam=fr["cam"]))
+    outl = lambda: [torch.zeros(len(f["has_mp"]), dtype=torch.uint8, device=dev) for f in frames]
+    Td = [torch.zeros(16, dtype=torch.float32, device=dev) for _ in frames]
+    PoseOptimizationFramesDevice(framed, Td, outl())
+    torch.cuda.synchronize()
+    ref = [t.cpu().numpy().copy() for t in Td]
+    for alloc in ("pinned", "coherent"):
+        for rep in range(3):
+            Th = [(torch.full((16,), -7.0, dtype=torch.float32).pin_memory() if alloc == "pinned"
+                   else _coherent_host_f32(16).fill_(-7.0)) for _ in frames]
+            PoseOptimizationFramesDevice(framed, Th, outl())
+            got = [t.numpy().copy() for t in Th]   # no synchronisation after the call
+            for f, fr in enumerate(frames):
+                assert np.array_equal(got[f], ref[f]), (alloc, rep, f)
+                o = oracle_lib.oracle_pose_optimization(fr)
+                assert np.array_equal(got[f].reshape(4, 4), o["Tcw"])
