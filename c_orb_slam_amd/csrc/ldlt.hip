@@ -84,6 +84,7 @@ struct SpDev {
     int kmode;            // 0: every pivot tile K; 1 / 2: only K of that class (updates, forward sweep)
     double* dst;          // k_ldlt_update delta mode: the target tiles live in the exchange buffer
     const int* packIdx;   // slot -> tile index in dst (delta mode)
+    int yfused;           // the forward sweep rides along the factorisation (y as an extra column)
 };
 
 // the sharded schedule's filters (block-uniform)
@@ -225,7 +226,7 @@ __global__ void __launch_bounds__(64) k_ldlt_prow(SpDev S, int j0) {
     if (*(volatile int*)S.fail) return;
     const int2 job = S.rowJobs[j0 + blockIdx.x];   // (panel, index in its row)
     const int p = job.x, lane = threadIdx.x;
-    if (skip_tile(S, p)) return;
+    if (job.y < 0 || skip_tile(S, p)) return;   // (y jobs: the four-wave kernel's only)
     const int pw = S.th[p];
     const double* D = S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT);
     // L[i][k] = D[i][k] (i > k) into Ls[k][i]: row r of D read by the wave in one coalesced load
@@ -328,7 +329,7 @@ __global__ void __launch_bounds__(64) k_ldlt_prow_r(SpDev S, int j0) {
     if (*(volatile int*)S.fail) return;
     const int2 job = S.rowJobs[j0 + blockIdx.x];   // (panel, index in its row)
     const int p = job.x, lane = threadIdx.x;
-    if (skip_tile(S, p)) return;
+    if (job.y < 0 || skip_tile(S, p)) return;   // (y jobs: the four-wave kernel's only)
     const int pw = S.th[p];
     const double* D = S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT);
     for (int r = 0; r < LT; r++) {
@@ -415,9 +416,11 @@ __global__ void __launch_bounds__(256) k_ldlt_prow4(SpDev S, int j0) {
     __shared__ double dsh[LT];
     __shared__ int anyNz;
     if (*(volatile int*)S.fail) return;
-    const int2 job = S.rowJobs[j0 + blockIdx.x];   // (panel, index in its row)
+    const int2 job = S.rowJobs[j0 + blockIdx.x];   // (panel, index in its row; -1: the panel's y)
     const int p = job.x, tid = threadIdx.x;
     if (skip_tile(S, p)) return;
+    const bool yj = job.y < 0;   // fused forward sweep: y_p as one more column of the panel row
+    if (yj && !S.yfused) return;
     const int pw = S.th[p];
     const double* D = S.U + (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT);
     {   // L of the panel from its factored diagonal tile: 16 coalesced row loads in flight per thread
@@ -434,15 +437,21 @@ __global__ void __launch_bounds__(256) k_ldlt_prow4(SpDev S, int j0) {
         if (tid == 0) anyNz = 0;
     }
     __syncthreads();
-    const int e = S.rowStart[p] + job.y;
-    const int sl = S.rowSlot[e];
+    const int e = S.rowStart[p] + (yj ? 0 : job.y);
+    const int sl = S.rowSlot[e];   // (a y job keeps a valid slot: its descriptors are never used to store)
     const __amdgpu_buffer_rsrc_t Ut = tile_rsrc(S.U + (size_t)sl * (LT * LT));
     const __amdgpu_buffer_rsrc_t Lo = tile_rsrc(S.LT + (size_t)sl * (LT * LT));
     const int w = tid >> 6, lane = tid & 63, s = lane & 3, j = 16 * w + (lane >> 2);
     const int vo = j * 8;
+    double* yp = S.y + p * LT;
     double c[LT / 4];   // c[q] = tile row 4 (m + q) + s of column j (m: the pivot group)
+    if (yj) {
 #pragma unroll
-    for (int q = 0; q < LT / 4; q++) c[q] = tld(Ut, vo, (4 * q + s) * LT * 8);
+        for (int q = 0; q < LT / 4; q++) c[q] = j == 0 ? yp[4 * q + s] : 0.0;
+    } else {
+#pragma unroll
+        for (int q = 0; q < LT / 4; q++) c[q] = tld(Ut, vo, (4 * q + s) * LT * 8);
+    }
     bool nz = false;
     for (int m = 0; m < LT / 4; m++) {
         if (4 * m >= pw) break;
@@ -452,9 +461,13 @@ __global__ void __launch_bounds__(256) k_ldlt_prow4(SpDev S, int j0) {
             if (k < pw) {
                 const double ck = quad_bcast(c[0], t);   // row k of column j: final
                 if (s == t) {
-                    tst(Ut, ck, vo, k * LT * 8);
-                    tst(Lo, ck / dsh[k], vo, k * LT * 8);
-                    nz |= ck != 0.0;
+                    if (yj) {
+                        if (j == 0) yp[k] = ck;
+                    } else {
+                        tst(Ut, ck, vo, k * LT * 8);
+                        tst(Lo, ck / dsh[k], vo, k * LT * 8);
+                        nz |= ck != 0.0;
+                    }
                 }
                 const double* Lk = Ls + k * LP + 4 * m + s;   // Lk[4 q] = L[4 (m + q) + s][k]
                 {
@@ -476,6 +489,7 @@ __global__ void __launch_bounds__(256) k_ldlt_prow4(SpDev S, int j0) {
         for (int q = 0; q < LT / 4 - 1; q++) c[q] = c[q + 1];
         c[LT / 4 - 1] = 0.0;
     }
+    if (yj) return;   // uniform: the y job stores nothing else
 #pragma unroll
     for (int q = 0; q < LT / 4; q++) {   // padding rows of L^T: zero
         const int r = 4 * q + s;
@@ -584,7 +598,7 @@ __global__ void __launch_bounds__(256) k_ldlt_ptrail(SpDev S, int j0) {
     if (*(volatile int*)S.fail) return;
     const int2 job = S.pairJobs[j0 + blockIdx.x];   // (panel, pair index)
     const int p = job.x;
-    if (skip_tile(S, p)) return;
+    if (job.y < 0 || skip_tile(S, p)) return;   // (y jobs: the quadrant kernel's only)
     const int rs = S.rowStart[p];
     const int4 pr = S.pairs[S.pairStart[p] + job.y];
     const int slI = S.rowSlot[rs + pr.x], slJ = S.rowSlot[rs + pr.y];
@@ -701,15 +715,58 @@ __device__ __forceinline__ int upd_next(const SpDev& S, int q, int kp1) {
     return q;
 }
 
+// The forward substitution fused into the factorisation (SpDev::yfused): y_I -= L(I, K) y_K over
+// the descendant pivot tiles of row I, K ascending, k ascending -- the oracle's forward sweep
+// sequence for those terms -- run by the quadrant (1, 0) workgroup of the diagonal target (I, I),
+// which nobody else needs (its K list is every descendant K with L(I, K) != 0).  All four waves
+// stage each L(I, K) tile and y_K in LDS (the next ones in flight), wave 0 runs the 64 row chains.
+__device__ void upd_y(const SpDev& S, int I, int kp0, int kp1, d2v* sh, double* ysh) {
+    const int gt = threadIdx.x, lane = gt & 63, w = gt >> 6;
+    d2v lr[8];
+    double yr = 0.0;
+    auto load = [&](int q) {
+        const int4 kp = S.kps[q];
+        const double* Lo = S.LT + (size_t)kp.x * (LT * LT);
+#pragma unroll
+        for (int u = 0; u < 8; u++) lr[u] = *(const d2v*)(Lo + 2 * (gt + 256 * u));   // [k][i] row-major pairs
+        if (gt < LT) yr = S.y[kp.z * LT + gt];
+    };
+    double acc = S.y[I * LT + lane];
+    int q = upd_next(S, kp0, kp1);
+    int4 kp = S.kps[q < kp1 ? q : kp0];
+    load(q < kp1 ? q : kp0);
+    while (q < kp1) {
+        const int kw = S.th[kp.z];
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 8; u++) sh[gt + 256 * u] = lr[u];
+        if (gt < LT) ysh[gt] = yr;
+        __syncthreads();
+        q = upd_next(S, q + 1, kp1);
+        if (q < kp1) kp = S.kps[q];
+        load(q < kp1 ? q : kp0);
+        if (w == 0) {
+            const double* Lf = (const double*)sh;   // Lf[k * 64 + i] = L[I0 + i][K0 + k]
+            for (int k = 0; k < kw; k++) acc = acc - Lf[k * LT + lane] * ysh[k];
+        }
+    }
+    if (w == 0) S.y[I * LT + lane] = acc;
+}
+
 __global__ void __launch_bounds__(256) k_ldlt_update_q(SpDev S, int t0) {
-    __shared__ d2v Lg[LT * LQ / 2];
-    __shared__ d2v Ug[LT * LQ / 2];
+    __shared__ d2v Lg[LT * LQ];   // [0, LT * LQ / 2): L quadrant; then U quadrant (the y path: one L tile)
+    __shared__ double ysh[LT];
+    d2v* Ug = Lg + LT * LQ / 2;
     if (*(volatile int*)S.fail) return;
     const int ti = t0 + (blockIdx.x >> 2), qd = blockIdx.x & 3, qi = qd >> 1, qj = qd & 1;
     const int4 tg = S.tgts[ti];
     const int kp0 = tg.w, kp1 = S.tgts[ti + 1].w;
     const int I = tg.y, J = tg.z;
     if (skip_tile(S, I)) return;
+    if (I == J && qi > qj) {   // the quadrant nobody stores: the fused forward sweep's descendant terms
+        if (S.yfused) upd_y(S, I, kp0, kp1, Lg, ysh);
+        return;
+    }
     const int ih = S.th[I], jw = S.th[J];
     if ((I == J && qi > qj) || LQ * qi >= ih || LQ * qj >= jw) return;   // a quadrant nobody stores
     const int gt = threadIdx.x, ty = gt >> 4, tx = gt & 15;
@@ -745,6 +802,20 @@ __global__ void __launch_bounds__(256) k_ldlt_ptrail_q(SpDev S, int j0) {
     const int p = job.x;
     if (skip_tile(S, p)) return;
     const int rs = S.rowStart[p];
+    if (job.y < 0) {   // fused forward sweep: y_I -= L(I, p) y_p, I = the panel row's entry -1 - job.y
+        if (!S.yfused || qd != 0 || threadIdx.x >= LT) return;
+        const int e = rs - 1 - job.y, sl = S.rowSlot[e], I = S.rowJ[e], lane = threadIdx.x;
+        if (!S.lnz[sl]) return;
+        double* ysh = (double*)Lg;
+        ysh[lane] = S.y[p * LT + lane];
+        __builtin_amdgcn_wave_barrier();
+        const double* Lo = S.LT + (size_t)sl * (LT * LT);   // [k][i] = L[I0 + i][p0 + k]
+        const int pw = S.th[p];
+        double acc = S.y[I * LT + lane];
+        for (int k = 0; k < pw; k++) acc = acc - Lo[k * LT + lane] * ysh[k];
+        S.y[I * LT + lane] = acc;
+        return;
+    }
     const int4 pr = S.pairs[S.pairStart[p] + job.y];
     const int slI = S.rowSlot[rs + pr.x], slJ = S.rowSlot[rs + pr.y];
     if (!S.lnz[slI] || !S.lnz[slJ]) return;   // block-uniform
@@ -814,6 +885,12 @@ __global__ void __launch_bounds__(64) k_ldlt_pfwd(SpDev S, int n0, const double*
         }
         S.y[I0 + lane] = on ? acc : 0.0;
     }
+}
+
+// The fused forward sweep's start: y = b in tile space (padding rows 0), a wave per tile.
+__global__ void __launch_bounds__(64) k_ldlt_yinit(SpDev S, const double* __restrict__ b) {
+    const int I = blockIdx.x, lane = threadIdx.x;
+    S.y[I * LT + lane] = lane < S.th[I] ? b[S.rowMap[I * LT + lane]] : 0.0;
 }
 
 // y /= d, then L^T x = y with k descending: one wave per node of a level (levels top-down);
@@ -1480,7 +1557,11 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
                 if (pnl >= nodeT[2 * k + 1]) continue;
                 stepP.push_back(pnl);
                 for (int e = 0; e < rowStart[pnl + 1] - rowStart[pnl]; e++) rowJobs.push_back(make_int2(pnl, e));
+                rowJobs.push_back(make_int2(pnl, -1));   // the fused forward sweep's y_p (skipped unless yfused)
                 for (int e = 0; e < pairStart[pnl + 1] - pairStart[pnl]; e++) pairJobs.push_back(make_int2(pnl, e));
+                // ... and its y_I -= L(I, p) y_p for the panel row's entries inside the node
+                for (int e = 0; e < rowStart[pnl + 1] - rowStart[pnl]; e++)
+                    if (rowJ[rowStart[pnl] + e] < nodeT[2 * k + 1]) pairJobs.push_back(make_int2(pnl, -1 - e));
             }
             hSteps_.push_back(rec);
         }
@@ -1626,6 +1707,7 @@ SpDev SparseLdlt::dev() const {
     d.kmode = 0;
     d.dst = nullptr;
     d.packIdx = nullptr;
+    d.yfused = 0;
     return d;
 }
 
@@ -1662,6 +1744,7 @@ void SparseLdlt::enqueue_factor_level(const SpDev& d, int h, const double* b, hi
                 hipLaunchKernelGGL(k_ldlt_ptrail, dim3(z.z - a.z), dim3(256), 0, s, d, a.z);
         }
     }
+    if (d.yfused) return;   // the forward sweep rode along
     const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h];
     const int mt = hLevMaxT_[h];
     if (sweep_nodes() && mt > 1 && mt <= kSweepMaxTiles)
@@ -1681,10 +1764,22 @@ void SparseLdlt::enqueue_backward_level(const SpDev& d, int h, double* x, double
         hipLaunchKernelGGL(k_ldlt_backward, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], x, scal, first);
 }
 
+// ORBGPU_LDLT_FWD=0 keeps the forward sweep as its own per-level launches (A/B)
+static bool fused_forward() {
+    static const bool v = [] {
+        const char* e = getenv("ORBGPU_LDLT_FWD");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
     if (n_ <= 0) return 0;
-    const SpDev d = dev();
+    SpDev d = dev();
+    // the fused forward sweep needs the y-aware kernels (quadrant updates, four-wave panel rows)
+    d.yfused = (fused_forward() && quad_updates() && prow_quads()) ? 1 : 0;
     ORB_HIP_CHECK(hipMemsetAsync(fail_, 0, sizeof(int), s));
+    if (d.yfused) hipLaunchKernelGGL(k_ldlt_yinit, dim3(nt_), dim3(64), 0, s, d, b);
     for (int h = 0; h < nLev_; h++) enqueue_factor_level(d, h, b, s);
     for (int h = nLev_ - 1; h >= 0; h--) enqueue_backward_level(d, h, x, scal, h == nLev_ - 1 ? 1 : 0, s);
     ORB_HIP_CHECK(hipGetLastError());
