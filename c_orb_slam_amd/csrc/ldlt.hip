@@ -74,6 +74,7 @@ struct SpDev {
     const int* stepP;     // panel steps: the panels of (level, step), see k_ldlt_pdiag
     const int2* rowJobs;  // (panel, index in its row) of each U tile of a step
     const int2* pairJobs; // (panel, pair index) of each trailing target of a step
+    const int4* panelJobs; // (panel, first role, roles, 0): k_ldlt_panel's workgroups of a step
     uint8_t* lnz;
     double* y;            // tile space
     double* xs;           // tile space
@@ -85,7 +86,9 @@ struct SpDev {
     double* dst;          // k_ldlt_update delta mode: the target tiles live in the exchange buffer
     const int* packIdx;   // slot -> tile index in dst (delta mode)
     int yfused;           // the forward sweep rides along the factorisation (y as an extra column)
+    int pfused;           // k_ldlt_panel: factored diagonal tiles land in their L^T slot, copied by k_ldlt_ptrail_q
 };
+constexpr int kDiagCopyJob = -2147483647 - 1;   // pairJobs marker: copy the panel's factored diagonal tile
 
 // the sharded schedule's filters (block-uniform)
 __device__ __forceinline__ bool skip_tile(const SpDev& S, int t) { return S.want >= 0 && S.tcls[t] != S.want; }
@@ -590,6 +593,130 @@ static bool rolled_panels() {
     return v;
 }
 
+// A panel step's diagonal factorisation and its panel row's eliminations in ONE launch
+// (k_ldlt_pdiag_r + k_ldlt_prow4 fused): a 512-thread workgroup per group of up to 7 row tiles
+// of a panel.  Wave 0 holds the diagonal tile (lane = column) and, per pivot k, publishes d_k and
+// the column of L in LDS; after one barrier every wave applies pivot k to its own tile (wave
+// 1 + r: row tile r of the group, lane = column; the fused forward sweep's y_p rides as one more
+// role with its column in lane 0), so a row tile's elimination runs in lock step with the
+// diagonal instead of after it, and the diagonal tile is not reloaded.  Every group of a panel
+// factors the diagonal redundantly (the same operations); the first one stores it -- into the
+// tile's unused L^T slot, since the other groups of the launch read the unfactored tile from U;
+// the next launch (k_ldlt_ptrail_q's copy jobs) moves it into place.  Per element
+// the sequence of k_ldlt_pdiag_r / k_ldlt_prow4: pivots ascending, l = u / d, a -= l * u, L^T =
+// u / d_k; padding pivots (k >= pw) not applied.
+// row tiles (or y) per workgroup beside the diagonal wave: R + 1 waves share the CU's FP64 issue,
+// so R = 3 (one wave per SIMD) by default; ORBGPU_LDLT_PANEL_ROLES = 1 / 3 / 7 (A/B)
+static int panel_roles() {
+    static const int v = [] {
+        const char* e = getenv("ORBGPU_LDLT_PANEL_ROLES");
+        const int r = e ? atoi(e) : 3;
+        return (r == 1 || r == 7) ? r : 3;
+    }();
+    return v;
+}
+
+template <int R>
+__global__ void __launch_bounds__(64 * (1 + R)) k_ldlt_panel(SpDev S, int j0) {
+    __shared__ double Ls[LT * LP];   // [k][i] = L[i][k] of the diagonal tile
+    __shared__ double dsh[LT];
+    __shared__ int sbad;
+    if (*(volatile int*)S.fail) return;
+    const int4 job = S.panelJobs[j0 + blockIdx.x];   // (panel, first role, roles, 0)
+    const int p = job.x;
+    if (skip_tile(S, p)) return;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int pw = S.th[p];
+    const int rs = S.rowStart[p], nrow = S.rowStart[p + 1] - rs;
+    const int role = w == 0 ? -1 : job.y + w - 1;   // -1 diagonal; [0, nrow) a row tile; nrow: y_p
+    const bool active = w == 0 || (w - 1 < job.z && (role < nrow || S.yfused));
+    const bool yrole = role == nrow;
+    const bool storeDiag = job.y == 0;
+    const int vo = lane * 8;
+    const int sl = (role >= 0 && role < nrow) ? S.rowSlot[rs + role] : S.slotOf[(size_t)p * S.nt + p];
+    const __amdgpu_buffer_rsrc_t Ut = tile_rsrc(S.U + (size_t)sl * (LT * LT));
+    const __amdgpu_buffer_rsrc_t Lo = tile_rsrc(S.LT + (size_t)sl * (LT * LT));
+    double* yp = S.y + p * LT;
+    if (threadIdx.x == 0) sbad = 0;
+    double col[LT];   // col[r] = tile row kb + r of column `lane` (kb: the chunk's first pivot)
+    if (yrole) {
+#pragma unroll
+        for (int r = 0; r < LT; r++) col[r] = lane == 0 ? yp[r] : 0.0;
+    } else if (active) {
+#pragma unroll
+        for (int r = 0; r < LT; r++) col[r] = tld(Ut, vo, r * LT * 8);   // zero outside the system
+    } else {
+#pragma unroll
+        for (int r = 0; r < LT; r++) col[r] = 0.0;
+    }
+    __syncthreads();
+    bool nz = false, bad = false;
+    for (int c = 0; c < LT / kChunk && !bad; c++) {
+        const int kb = kChunk * c;
+        if (kb >= pw) break;
+#pragma unroll
+        for (int t = 0; t < kChunk; t++) {
+            const int k = kb + t;
+            if (k < pw && !bad) {
+                if (w == 0) {   // pivot k: d_k and the column of L
+                    const double d = rdlane(col[t], k);
+                    if (d == 0.0) {
+                        if (lane == 0) sbad = 1;
+                    } else {
+                        Ls[k * LP + lane] = lane > k ? col[t] / d : 0.0;
+                        if (lane == 0) dsh[k] = d;
+                    }
+                }
+                __syncthreads();
+                if (sbad) {
+                    bad = true;
+                } else {
+                    const double ck = col[t];   // row k: final (pivots < k applied)
+                    if (w == 0) {
+                        if (storeDiag && lane < pw) tst(Lo, lane >= k ? ck : Ls[lane * LP + k], vo, k * LT * 8);
+                    } else if (yrole) {
+                        if (lane == 0) yp[k] = ck;
+                    } else if (active) {
+                        tst(Ut, ck, vo, k * LT * 8);
+                        tst(Lo, ck / dsh[k], vo, k * LT * 8);
+                        nz |= ck != 0.0;
+                    }
+#pragma unroll
+                    for (int q = 0; q < LT / kChunk; q++) {
+                        if (q < LT / kChunk - c) {   // registers 8q..8q+7 hold live rows
+#pragma unroll
+                            for (int r = kChunk * q; r < kChunk * q + kChunk; r++)
+                                if (r > t) col[r] -= Ls[k * LP + kb + r] * col[t];
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < LT - kChunk; r++) col[r] = col[r + kChunk];
+    }
+    if (bad) {
+        if (threadIdx.x == 0) *S.fail = 1;
+        return;
+    }
+    if (w > 0 && active && !yrole) {
+        for (int r = pw; r < LT; r++) tst(Lo, 0.0, vo, r * LT * 8);   // padding rows of L^T: zero
+        // flag = some eliminated U[k][j] != 0, a superset of "some l != 0": skipping on it is exact
+        const bool any = __any(nz);
+        if (lane == 0) S.lnz[sl] = any ? 1 : 0;
+    }
+}
+
+// ORBGPU_LDLT_PANEL=0 keeps the separate diagonal and panel-row launches (A/B)
+static bool fused_panels() {
+    static const bool v = [] {
+        const char* e = getenv("ORBGPU_LDLT_PANEL");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // Trailing updates inside the nodes: A(I, J) -= L(I, p) U(p, J), one 256-thread workgroup per
 // target of the step (4 x 4 register micro-tiles, both operand tiles staged in LDS).
 __global__ void __launch_bounds__(256) k_ldlt_ptrail(SpDev S, int j0) {
@@ -802,6 +929,14 @@ __global__ void __launch_bounds__(256) k_ldlt_ptrail_q(SpDev S, int j0) {
     const int p = job.x;
     if (skip_tile(S, p)) return;
     const int rs = S.rowStart[p];
+    if (job.y == kDiagCopyJob) {   // k_ldlt_panel's factored diagonal tile: L^T shadow -> U, a quarter each
+        if (!S.pfused) return;
+        const size_t sd = (size_t)S.slotOf[(size_t)p * S.nt + p] * (LT * LT);
+        const d2v* src = (const d2v*)(S.LT + sd) + qd * (LT * LT / 8);
+        d2v* dst = (d2v*)(S.U + sd) + qd * (LT * LT / 8);
+        for (int u = threadIdx.x; u < LT * LT / 8; u += 256) dst[u] = src[u];
+        return;
+    }
     if (job.y < 0) {   // fused forward sweep: y_I -= L(I, p) y_p, I = the panel row's entry -1 - job.y
         if (!S.yfused || qd != 0 || threadIdx.x >= LT) return;
         const int e = rs - 1 - job.y, sl = S.rowSlot[e], I = S.rowJ[e], lane = threadIdx.x;
@@ -1340,6 +1475,130 @@ __global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_bwdn(SpDev S, int n0,
     }
 }
 
+// Backward sweep by levels with the ancestors' terms PUSHED (the default): per element the
+// sequence of k_ldlt_backward (x_i = y_i / d_i, then L[j][i] x_j for j descending), split as
+//   k_ldlt_binit   acc = y / d for every tile row;
+//   per level H, top-down:
+//     k_ldlt_bin     the level's nodes finish their rows from acc: their own tiles, descending
+//                    (the node sweep of k_ldlt_bwdn without its outside phase);
+//     k_ldlt_bpush   every tile row below whose ancestor node at level H holds tiles J of its row
+//                    list applies them now: acc_I -= L(J, I)^T x_J, J descending, k descending.
+// A row's ancestors sit on levels above its own and carry larger tile indices the higher they
+// are, so the pushes arrive in descending J: the same sequence.  The pushes of a level are one
+// launch over all rows below (a workgroup per (row, ancestor node)), instead of each row walking
+// every ancestor tile inside its own level's launch (one wave streaming tens of 32 KB tiles).
+__global__ void __launch_bounds__(64) k_ldlt_binit(SpDev S, double* __restrict__ acc) {
+    if (*(volatile int*)S.fail) return;
+    const int I = blockIdx.x, lane = threadIdx.x;
+    const double* Ud = S.U + (size_t)S.slotOf[(size_t)I * S.nt + I] * (LT * LT);
+    acc[I * LT + lane] = lane < S.th[I] ? S.y[I * LT + lane] / Ud[lane * LT + lane] : 0.0;
+}
+
+// (row I, entries [lo, hi] of its row list inside one ancestor node): L^T tiles staged in LDS (row
+// pitch LP) by all four waves, the next tile's loads in flight; wave 0 runs the 64 row chains.
+__global__ void __launch_bounds__(256) k_ldlt_bpush(SpDev S, const int4* __restrict__ tg, double* __restrict__ acc) {
+    __shared__ double Lr[LT * LP];   // [i][k'] = L[J0 + k'][I0 + i]
+    __shared__ double xsh[LT];
+    if (*(volatile int*)S.fail) return;
+    const int4 t = tg[blockIdx.x];   // (I, hi, lo, 0)
+    const int I = t.x, hi = t.y, lo = t.z;
+    const int gt = threadIdx.x, lane = gt & 63, w = gt >> 6;
+    auto nextv = [&](int e) {
+        while (e >= lo && !S.lnz[S.rowSlot[e]]) e--;
+        return e;
+    };
+    d2v lr[8];
+    double xr = 0.0;
+    auto load = [&](int e) {
+        const double* Lo = S.LT + (size_t)S.rowSlot[e] * (LT * LT);
+#pragma unroll
+        for (int u = 0; u < 8; u++) lr[u] = *(const d2v*)(Lo + 2 * (gt + 256 * u));
+        const int J = S.rowJ[e];
+        if (gt < LT) xr = gt < S.th[J] ? S.xs[J * LT + gt] : 0.0;
+    };
+    double a = acc[I * LT + lane];
+    int e = nextv(hi);
+    load(e >= lo ? e : hi);
+    while (e >= lo) {
+        const int kh = S.th[S.rowJ[e]];
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 8; u++) {   // element pair (i, k'), (i, k' + 1): i = q >> 5, k' = 2 (q & 31)
+            const int q = gt + 256 * u, i = q >> 5, k2 = 2 * (q & 31);
+            Lr[i * LP + k2] = lr[u].x;
+            Lr[i * LP + k2 + 1] = lr[u].y;
+        }
+        if (gt < LT) xsh[gt] = xr;
+        __syncthreads();
+        const int en = nextv(e - 1);
+        load(en >= lo ? en : e);   // the next tile travels while this one is applied
+        if (w == 0) {
+            const double* row = Lr + lane * LP;
+            for (int k = LT - 1; k >= 0; k--)
+                if (k < kh) a = a - row[k] * xsh[k];
+        }
+        e = en;
+    }
+    if (w == 0) acc[I * LT + lane] = a;
+}
+
+// The level's nodes: their rows start from acc (every ancestor term applied), then the node's own
+// tiles one at a time, descending, as in k_ldlt_bwdn.
+__global__ void __launch_bounds__(64 * kSweepWaves) k_ldlt_bin(SpDev S, int n0, const double* __restrict__ acc0,
+                                                              double* __restrict__ x, double* scal, int first) {
+    extern __shared__ double accs[];
+    __shared__ int cur[kSweepMaxTiles];
+    const int lane = threadIdx.x & 63;
+    const int failed = *(volatile int*)S.fail;
+    if (first && blockIdx.x == 0 && threadIdx.x == 0) scal[3] = failed ? 0.0 : 1.0;
+    if (failed) return;
+    const int node = S.levNodes[n0 + blockIdx.x];
+    const int T0 = S.nodeT[2 * node], T1 = S.nodeT[2 * node + 1];
+    if (T1 > T0 && skip_tile(S, T0)) return;
+    const int W = blockDim.x >> 6, w = threadIdx.x >> 6;
+    for (int I = T0 + w; I < T1; I += W) {
+        int e = S.rowStart[I + 1] - 1;
+        while (e >= S.rowStart[I] && S.rowJ[e] >= T1) e--;   // the ancestors' entries: pushed already
+        accs[(I - T0) * LT + lane] = acc0[I * LT + lane];
+        if (lane == 0) cur[I - T0] = e;
+    }
+    __syncthreads();
+    for (int s = T1 - T0 - 1; s >= 0; s--) {
+        const int K = T0 + s, K0 = K * LT, kh = S.th[K];
+        if (s % W == w) {   // the owner: diagonal tile, x_K final
+            const bool on = lane < kh;
+            double a = accs[s * LT + lane];
+            const double* Ud = S.U + (size_t)S.slotOf[(size_t)K * S.nt + K] * (LT * LT);
+            double Lk[LT];
+#pragma unroll
+            for (int k = 0; k < LT; k++) Lk[k] = (on && k < kh) ? Ud[k * LT + lane] : 0.0;   // L[K0 + k][K0 + lane]
+#pragma unroll
+            for (int k = LT - 1; k >= 0; k--) {
+                if (k < kh) {
+                    const double v = a - Lk[k] * rdlane(a, k);
+                    a = lane < k ? v : a;
+                }
+            }
+            a = on ? a : 0.0;
+            S.xs[K0 + lane] = a;
+            if (on) x[S.rowMap[K0 + lane]] = a;
+            accs[s * LT + lane] = a;
+        }
+        __syncthreads();
+        const double xk = accs[s * LT + lane];
+        for (int I = T0 + w; I < K; I += W) {
+            const int e = cur[I - T0];
+            if (e < S.rowStart[I] || S.rowJ[e] != K) continue;   // no block (I, K)
+            if (lane == 0) cur[I - T0] = e - 1;
+            const int sl = S.rowSlot[e];
+            if (!S.lnz[sl]) continue;
+            accs[(I - T0) * LT + lane] =
+                sweep_chain_bwd(accs[(I - T0) * LT + lane], S.LT + (size_t)sl * (LT * LT), lane, xk, kh);
+        }
+        __syncthreads();
+    }
+}
+
 // ORBGPU_LDLT_SWEEP=1 keeps the one-wave-per-node sweeps, =2 the node sweeps with cross-lane
 // broadcasts (A/B); default: the pipelined node sweeps (k_ldlt_fwdn_u / k_ldlt_bwdn_u)
 static int sweep_mode() {
@@ -1542,6 +1801,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     // per step the panels, the U tiles of their rows and the trailing targets inside the nodes
     std::vector<int> stepP;
     std::vector<int2> rowJobs, pairJobs;
+    std::vector<int4> panelJobs;   // k_ldlt_panel: per panel, groups of panel_roles() roles (row tiles, then y)
     hSteps_.clear();
     hLevStepStart_.assign(nLev_ + 1, 0);
     for (int h = 0; h < nLev_; h++) {
@@ -1550,7 +1810,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
         for (int q = hLevNodeStart_[h]; q < hLevNodeStart_[h + 1]; q++)
             maxT = std::max(maxT, nodeT[2 * levNodes[q] + 1] - nodeT[2 * levNodes[q]]);
         for (int st = 0; st < maxT; st++) {
-            const int4 rec = make_int4((int)stepP.size(), (int)rowJobs.size(), (int)pairJobs.size(), 0);
+            const int4 rec = make_int4((int)stepP.size(), (int)rowJobs.size(), (int)pairJobs.size(), (int)panelJobs.size());
             for (int q = hLevNodeStart_[h]; q < hLevNodeStart_[h + 1]; q++) {
                 const int k = levNodes[q];
                 const int pnl = nodeT[2 * k] + st;
@@ -1558,16 +1818,41 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
                 stepP.push_back(pnl);
                 for (int e = 0; e < rowStart[pnl + 1] - rowStart[pnl]; e++) rowJobs.push_back(make_int2(pnl, e));
                 rowJobs.push_back(make_int2(pnl, -1));   // the fused forward sweep's y_p (skipped unless yfused)
+                const int roles = rowStart[pnl + 1] - rowStart[pnl] + 1, pr = panel_roles();   // row tiles + y_p
+                for (int r0 = 0; r0 < roles; r0 += pr) panelJobs.push_back(make_int4(pnl, r0, std::min(pr, roles - r0), 0));
                 for (int e = 0; e < pairStart[pnl + 1] - pairStart[pnl]; e++) pairJobs.push_back(make_int2(pnl, e));
                 // ... and its y_I -= L(I, p) y_p for the panel row's entries inside the node
                 for (int e = 0; e < rowStart[pnl + 1] - rowStart[pnl]; e++)
                     if (rowJ[rowStart[pnl] + e] < nodeT[2 * k + 1]) pairJobs.push_back(make_int2(pnl, -1 - e));
+                pairJobs.push_back(make_int2(pnl, kDiagCopyJob));   // (k_ldlt_panel runs only)
             }
             hSteps_.push_back(rec);
         }
     }
     hLevStepStart_[nLev_] = (int)hSteps_.size();
-    hSteps_.push_back(make_int4((int)stepP.size(), (int)rowJobs.size(), (int)pairJobs.size(), 0));   // sentinel
+    // backward pushes: per tile row, its row list's entries grouped by ancestor node (descending J),
+    // each group a target of the launch after that node's level finishes (k_ldlt_bpush)
+    std::vector<std::vector<int4>> pushByLev(nLev_);
+    for (int I = 0; I < nt; I++) {
+        const int own = tileNode[I];
+        int e = rowStart[I + 1] - 1;
+        while (e >= rowStart[I]) {
+            const int X = tileNode[rowJ[e]];
+            if (X == own) break;   // the node's own tiles (ascending list: the ancestors are above)
+            int lo = e;
+            while (lo - 1 >= rowStart[I] && tileNode[rowJ[lo - 1]] == X) lo--;
+            pushByLev[tree.height[X]].push_back(make_int4(I, e, lo, 0));
+            e = lo - 1;
+        }
+    }
+    std::vector<int4> pushT;
+    hLevPushStart_.assign(nLev_ + 1, 0);
+    for (int h = 0; h < nLev_; h++) {
+        hLevPushStart_[h] = (int)pushT.size();
+        pushT.insert(pushT.end(), pushByLev[h].begin(), pushByLev[h].end());
+    }
+    hLevPushStart_[nLev_] = (int)pushT.size();
+    hSteps_.push_back(make_int4((int)stepP.size(), (int)rowJobs.size(), (int)pairJobs.size(), (int)panelJobs.size()));   // sentinel
     tgts.push_back(make_int4(0, 0, 0, (int)kps.size()));   // sentinel: the last target's K range end
     // every tile a kernel addresses exists (host check before any launch)
     for (int I = 0; I < nt; I++)
@@ -1597,6 +1882,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     const size_t oLT = take(tileB * nslot_);
     const size_t oY = take(sizeof(double) * (size_t)nt * LT);
     const size_t oXs = take(sizeof(double) * (size_t)nt * LT);
+    const size_t oAcc = take(sizeof(double) * (size_t)nt * LT);
     const size_t oLnz = take(nslot_);
     const size_t oFail = take(sizeof(int) * 4);
     const size_t oProw = take(sizeof(int) * (size_t)ng);
@@ -1643,6 +1929,8 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     };
     offRowJobs_ = put2(rowJobs);
     offPairJobs_ = put2(pairJobs);
+    offPanelJobs_ = put4(panelJobs);
+    offPush_ = put4(pushT);
     const size_t oLists = take(sizeof(int) * (L.size() + 64));
     if (off > cap_) {
         if (mem_) (void)hipFree(mem_);
@@ -1657,6 +1945,7 @@ int SparseLdlt::build(int n, int g, const std::vector<int>& adjStart, const std:
     LT_ = (double*)(base + oLT);
     y_ = (double*)(base + oY);
     xs_ = (double*)(base + oXs);
+    acc_ = (double*)(base + oAcc);
     lnz_ = (uint8_t*)(base + oLnz);
     fail_ = (int*)(base + oFail);
     prow_ = (int*)(base + oProw);
@@ -1698,6 +1987,7 @@ SpDev SparseLdlt::dev() const {
     d.stepP = lists_ + offStepP_;
     d.rowJobs = (const int2*)(lists_ + offRowJobs_);
     d.pairJobs = (const int2*)(lists_ + offPairJobs_);
+    d.panelJobs = (const int4*)(lists_ + offPanelJobs_);
     d.lnz = lnz_;
     d.y = y_;
     d.xs = xs_;
@@ -1708,6 +1998,8 @@ SpDev SparseLdlt::dev() const {
     d.dst = nullptr;
     d.packIdx = nullptr;
     d.yfused = 0;
+    // the fused panel launch needs the quadrant trailing kernel (its copy jobs) and the y-aware rows
+    d.pfused = (fused_panels() && quad_updates() && prow_quads()) ? 1 : 0;
     return d;
 }
 
@@ -1721,6 +2013,17 @@ void SparseLdlt::enqueue_factor_level(const SpDev& d, int h, const double* b, hi
     }
     for (int st = hLevStepStart_[h]; st < hLevStepStart_[h + 1]; st++) {
         const int4 a = hSteps_[st], z = hSteps_[st + 1];
+        if (d.pfused) {   // diagonal + panel row in one launch
+            if (z.w > a.w) {
+                const int pr = panel_roles();
+                if (pr == 1)
+                    hipLaunchKernelGGL(k_ldlt_panel<1>, dim3(z.w - a.w), dim3(128), 0, s, d, a.w);
+                else if (pr == 7)
+                    hipLaunchKernelGGL(k_ldlt_panel<7>, dim3(z.w - a.w), dim3(512), 0, s, d, a.w);
+                else
+                    hipLaunchKernelGGL(k_ldlt_panel<3>, dim3(z.w - a.w), dim3(256), 0, s, d, a.w);
+            }
+        } else {
         if (z.x > a.x) {
             // the four-wave diagonal kernel measured no faster than the rolled one-wave kernel
             // (38 vs 36-38 us per launch, profiles/r04l3_gba_ldlt_levels.txt): opt-in
@@ -1736,6 +2039,7 @@ void SparseLdlt::enqueue_factor_level(const SpDev& d, int h, const double* b, hi
             else
                 hipLaunchKernelGGL(rolled_panels() ? k_ldlt_prow_r : k_ldlt_prow, dim3(z.y - a.y), dim3(64), 0, s, d,
                                    a.y);
+        }
         }
         if (z.z > a.z) {
             if (quad_updates())
@@ -1764,6 +2068,15 @@ void SparseLdlt::enqueue_backward_level(const SpDev& d, int h, double* x, double
         hipLaunchKernelGGL(k_ldlt_backward, dim3(nn), dim3(64), 0, s, d, hLevNodeStart_[h], x, scal, first);
 }
 
+// ORBGPU_LDLT_BPUSH=0 keeps the per-level backward launches that walk every ancestor tile (A/B)
+static bool pushed_backward() {
+    static const bool v = [] {
+        const char* e = getenv("ORBGPU_LDLT_BPUSH");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // ORBGPU_LDLT_FWD=0 keeps the forward sweep as its own per-level launches (A/B)
 static bool fused_forward() {
     static const bool v = [] {
@@ -1781,7 +2094,21 @@ int SparseLdlt::solve(const double* b, double* x, double* scal, hipStream_t s) {
     ORB_HIP_CHECK(hipMemsetAsync(fail_, 0, sizeof(int), s));
     if (d.yfused) hipLaunchKernelGGL(k_ldlt_yinit, dim3(nt_), dim3(64), 0, s, d, b);
     for (int h = 0; h < nLev_; h++) enqueue_factor_level(d, h, b, s);
-    for (int h = nLev_ - 1; h >= 0; h--) enqueue_backward_level(d, h, x, scal, h == nLev_ - 1 ? 1 : 0, s);
+    int maxT = 0;
+    for (int h = 0; h < nLev_; h++) maxT = std::max(maxT, hLevMaxT_[h]);
+    if (pushed_backward() && maxT <= kSweepMaxTiles) {
+        const int4* pt = (const int4*)(lists_ + offPush_);
+        hipLaunchKernelGGL(k_ldlt_binit, dim3(nt_), dim3(64), 0, s, d, acc_);
+        for (int h = nLev_ - 1; h >= 0; h--) {
+            const int nn = hLevNodeStart_[h + 1] - hLevNodeStart_[h], mt = std::max(1, hLevMaxT_[h]);
+            hipLaunchKernelGGL(k_ldlt_bin, dim3(nn), dim3(64 * std::min(mt, kSweepWaves)), sizeof(double) * LT * mt, s,
+                               d, hLevNodeStart_[h], (const double*)acc_, x, scal, h == nLev_ - 1 ? 1 : 0);
+            const int np = hLevPushStart_[h + 1] - hLevPushStart_[h];
+            if (np > 0) hipLaunchKernelGGL(k_ldlt_bpush, dim3(np), dim3(256), 0, s, d, pt + hLevPushStart_[h], acc_);
+        }
+    } else {
+        for (int h = nLev_ - 1; h >= 0; h--) enqueue_backward_level(d, h, x, scal, h == nLev_ - 1 ? 1 : 0, s);
+    }
     ORB_HIP_CHECK(hipGetLastError());
     return 0;
 }

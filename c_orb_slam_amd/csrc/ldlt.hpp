@@ -101,15 +101,15 @@ private:
     int* slotOf_ = nullptr;
     int* prow_ = nullptr;
     int* fail_ = nullptr;
-    double *U_ = nullptr, *LT_ = nullptr, *y_ = nullptr, *xs_ = nullptr;
+    double *U_ = nullptr, *LT_ = nullptr, *y_ = nullptr, *xs_ = nullptr, *acc_ = nullptr;
     int* lists_ = nullptr;
     uint8_t* lnz_ = nullptr;
     size_t offTh_ = 0, offRowMap_ = 0, offRowStart_ = 0, offRowJ_ = 0, offRowSlot_ = 0, offColStart_ = 0,
            offColK_ = 0, offColSlot_ = 0, offPairStart_ = 0, offNodeT_ = 0, offLevNodes_ = 0, offPairs_ = 0,
-           offTgts_ = 0, offKps_ = 0, offStepP_ = 0, offRowJobs_ = 0, offPairJobs_ = 0;
-    std::vector<int> hSlotOf_, hProw_, hLevNodeStart_, hLevTgtStart_, hLevStepStart_;
+           offTgts_ = 0, offKps_ = 0, offStepP_ = 0, offRowJobs_ = 0, offPairJobs_ = 0, offPanelJobs_ = 0, offPush_ = 0;
+    std::vector<int> hSlotOf_, hProw_, hLevNodeStart_, hLevTgtStart_, hLevStepStart_, hLevPushStart_;
     std::vector<int> hLevMaxT_;   // per level: the most tiles of one of its nodes (sweep launch shape)
-    std::vector<int4> hSteps_;   // per panel step: first (panel, row job, pair job); + sentinel
+    std::vector<int4> hSteps_;   // per panel step: first (panel, row job, pair job, panel job); + sentinel
 };
 
 // Unit entry: dense host S (upper read) -> pattern of its nonzero 6 x 6 blocks -> sparse solve

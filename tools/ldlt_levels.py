@@ -10,7 +10,8 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Time
 ld = [r for r in rows if "k_ldlt_" in r["Kernel_Name"] and "k_ldlt_reg" not in r["Kernel_Name"]]
 # a solve starts at the first update/factor after a backward run
 def bwd(r):
-    return "backward" in r["Kernel_Name"] or "bwdn" in r["Kernel_Name"]
+    n = r["Kernel_Name"]
+    return "backward" in n or "bwdn" in n or "k_ldlt_bin" in n or "bpush" in n
 
 
 starts = [i for i in range(len(ld)) if not bwd(ld[i]) and (i == 0 or bwd(ld[i - 1]))]
