@@ -743,11 +743,21 @@ __global__ void __launch_bounds__(NT) k_schur(BaStructDev s, const double* __res
             a1n = jn < n ? s.pairA[s0 + jn] : 0;
             a2n = jn < n ? s.pairB[s0 + jn] : 0;
         }
+        // the two 144-B records as nine 16-B loads each (records are 16-B aligned in the arena):
+        // half the gather instructions of element-wise 8-B loads
         double E[18], B[18];
+        {
+            typedef double d2 __attribute__((ext_vector_type(2)));
+            const d2* Er = (const d2*)(Emat + 18 * (size_t)a1);
+            const d2* Br = (const d2*)(Hpl + 18 * (size_t)a2);
 #pragma unroll
-        for (int q = 0; q < 18; q++) {
-            E[q] = valid ? Emat[18 * (size_t)a1 + q] : 0.0;
-            B[q] = valid ? Hpl[18 * (size_t)a2 + q] : 0.0;
+            for (int q = 0; q < 9; q++) {
+                const d2 e = Er[q], b = Br[q];   // (a1 = a2 = 0 on invalid lanes: in bounds)
+                E[2 * q] = valid ? e.x : 0.0;
+                E[2 * q + 1] = valid ? e.y : 0.0;
+                B[2 * q] = valid ? b.x : 0.0;
+                B[2 * q + 1] = valid ? b.y : 0.0;
+            }
         }
         auto put = [&](double* v, auto kk) {
             constexpr int K = decltype(kk)::value;

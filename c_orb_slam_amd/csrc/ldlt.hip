@@ -906,16 +906,29 @@ __global__ void __launch_bounds__(256) k_ldlt_update_q(SpDev S, int t0) {
     int q = upd_next(S, kp0, kp1);
     int4 kp = S.kps[q < kp1 ? q : kp0];
     quad_load(ops, S.LT + (size_t)kp.x * (LT * LT), S.U + (size_t)kp.y * (LT * LT), qi, qj, gt);
+    int4 kc = S.kps[q + 1 < kp1 ? q + 1 : kp0];   // the next candidate's pair, one iteration ahead
     while (q < kp1) {
         const int kw = S.th[kp.z];
         __syncthreads();   // the previous K's LDS reads are done
         quad_stage(ops, Lg, Ug, gt);
         __syncthreads();
-        q = upd_next(S, q + 1, kp1);
-        if (q < kp1) kp = S.kps[q];
-        // the next K's operands travel while this one is applied
-        quad_load(ops, S.LT + (size_t)kp.x * (LT * LT), S.U + (size_t)kp.y * (LT * LT), qi, qj, gt);
+        // the next K is usually the next pair: its operands are requested right away, with its
+        // flags in flight beside them (no dependent flag round trip before the loads); a pair the
+        // flags rule out (an exactly zero L tile) is replaced after this K's compute
+        int qn = q + 1;
+        int4 kn = qn < kp1 ? kc : kp;
+        quad_load(ops, S.LT + (size_t)kn.x * (LT * LT), S.U + (size_t)kn.y * (LT * LT), qi, qj, gt);
+        const bool ok = qn < kp1 && S.lnz[kn.x] && S.lnz[kn.y] && !skip_k(S, kn.z);
+        kc = S.kps[qn + 1 < kp1 ? qn + 1 : kp0];
         quad_apply(acc, Lg, Ug, kw, ty, tx);
+        if (qn < kp1 && !ok) {   // (block-uniform)
+            qn = upd_next(S, qn + 1, kp1);
+            kn = qn < kp1 ? S.kps[qn] : kp;
+            quad_load(ops, S.LT + (size_t)kn.x * (LT * LT), S.U + (size_t)kn.y * (LT * LT), qi, qj, gt);
+            kc = S.kps[qn + 1 < kp1 ? qn + 1 : kp0];
+        }
+        q = qn;
+        kp = kn;
     }
     quad_store(acc, T, qi, qj, ty, tx, ih, jw, I == J);
 }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Multi-GPU cost model of config 5 (round 5): kernel traces of 1, 2, 4, 8 in-process ranks
+# Multi-GPU cost model of config 5 (rounds 5-6): kernel traces of 1, 2, 4, 8 in-process ranks
 # (separator-tree partition) of one BundleAdjustment(10) call, then tools/gba_rank_model.py.
 # usage: bash tools/r05_gba_model.sh <tag> [nkf:laps]
 set -o pipefail
