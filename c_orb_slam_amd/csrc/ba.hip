@@ -217,6 +217,8 @@ __device__ __forceinline__ void inv3(const double* m, double* r) {
 #undef M
 }
 
+typedef double bd2 __attribute__((ext_vector_type(2)));   // 16-B loads / stores of aligned FP64 records
+
 // Dinv = (Hll + lambda I)^-1 of landmark l (setLambda + D->inverse(), block_solver.hpp:383-389)
 __device__ __forceinline__ void land_dinv(const double* Hll, int l, double lambda, double* Di) {
     double D[9];
@@ -260,12 +262,20 @@ __device__ __forceinline__ void land_step(const BaStructDev& s, int l, const dou
         double Bv[4][18], cv[4][6];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const double* B = Hpl + 18 * (size_t)pp[u];
-            const double* cp = x + 6 * pe[u];
+            const bd2* B = (const bd2*)(Hpl + 18 * (size_t)pp[u]);   // 16-B aligned 144-B records
+            const bd2* cp = (const bd2*)(x + 6 * pe[u]);
 #pragma unroll
-            for (int q = 0; q < 18; q++) Bv[u][q] = a[u] >= 0 ? B[q] : 0.0;
+            for (int q = 0; q < 9; q++) {
+                const bd2 v = B[q];
+                Bv[u][2 * q] = a[u] >= 0 ? v.x : 0.0;
+                Bv[u][2 * q + 1] = a[u] >= 0 ? v.y : 0.0;
+            }
 #pragma unroll
-            for (int r = 0; r < 6; r++) cv[u][r] = a[u] >= 0 ? cp[r] : 0.0;
+            for (int r = 0; r < 3; r++) {
+                const bd2 v = cp[r];
+                cv[u][2 * r] = a[u] >= 0 ? v.x : 0.0;
+                cv[u][2 * r + 1] = a[u] >= 0 ? v.y : 0.0;
+            }
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -428,6 +438,7 @@ __global__ void __launch_bounds__(256) k_linearize_t(LinArgs a) {
     }
     const int pp = a.s.pePos[i];   // the pose terms and Hpl at the edge's pose-list position
     if (pp < 0) return;
+    double hpl[18];
 #pragma unroll
     for (int r = 0; r < 6; r++) {
         double s = 0;
@@ -449,9 +460,12 @@ __global__ void __launch_bounds__(256) k_linearize_t(LinArgs a) {
 #pragma unroll
             for (int k = 0; k < 3; k++)
                 if (k < D) h += robust ? (B[k * 6 + r] * w) * A[k * 3 + c] : B[k * 6 + r] * (A[k * 3 + c] * e.info);
-            a.Hpl[18 * (size_t)pp + r * 3 + c] = h;
+            hpl[r * 3 + c] = h;
         }
     }
+    bd2* hd = (bd2*)(a.Hpl + 18 * (size_t)pp);   // the 144-B record as nine 16-B stores
+#pragma unroll
+    for (int q = 0; q < 9; q++) hd[q] = bd2{hpl[2 * q], hpl[2 * q + 1]};
     }
 }
 
@@ -627,12 +641,30 @@ __device__ __forceinline__ void prep_entry(const double* H9, const double* b3, d
     land_dinv(H9, 0, lambda, Di);
     const double b[3] = {b3[0], b3[1], b3[2]};
     for (int r = 0; r < 3; r++) d[r] = (Di[r * 3] * b[0] + Di[r * 3 + 1] * b[1]) + Di[r * 3 + 2] * b[2];
-    const double* Bi = Hpl + 18 * (size_t)a;
+    // the 144-B Hpl record in, the 144-B E record and 48-B c_b record out as 16-B accesses
+    double Bi[18], Eo[18], co[6];
+    {
+        const bd2* src = (const bd2*)(Hpl + 18 * (size_t)a);
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+            const bd2 v = src[q];
+            Bi[2 * q] = v.x;
+            Bi[2 * q + 1] = v.y;
+        }
+    }
+#pragma unroll
     for (int r = 0; r < 6; r++) {
         const double b0 = Bi[r * 3], b1 = Bi[r * 3 + 1], b2 = Bi[r * 3 + 2];
-        for (int k = 0; k < 3; k++) Emat[18 * (size_t)a + r * 3 + k] = (b0 * Di[k] + b1 * Di[3 + k]) + b2 * Di[6 + k];
-        cb[6 * (size_t)a + r] = (b0 * d[0] + b1 * d[1]) + b2 * d[2];
+#pragma unroll
+        for (int k = 0; k < 3; k++) Eo[r * 3 + k] = (b0 * Di[k] + b1 * Di[3 + k]) + b2 * Di[6 + k];
+        co[r] = (b0 * d[0] + b1 * d[1]) + b2 * d[2];
     }
+    bd2* Ed = (bd2*)(Emat + 18 * (size_t)a);
+    bd2* cd = (bd2*)(cb + 6 * (size_t)a);
+#pragma unroll
+    for (int q = 0; q < 9; q++) Ed[q] = bd2{Eo[2 * q], Eo[2 * q + 1]};
+#pragma unroll
+    for (int q = 0; q < 3; q++) cd[q] = bd2{co[2 * q], co[2 * q + 1]};
 }
 
 __global__ void __launch_bounds__(256) k_point_prep(BaStructDev s, const double* Hll, const double* bl,
