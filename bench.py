@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--lanes", type=int, default=2,
                     help="batches in flight (buffer sets): extraction of batch k waits for the tracking chain "
                          "of batch k - lanes, which last used its buffers")
+    ap.add_argument("--depth", type=int, default=1,
+                    help="extractions in flight: 1 = batch k's extraction is submitted after batch k-1's chain "
+                         "is enqueued and waited for within the step; 2 = batch k's extraction is queued at the "
+                         "start of step k, before the host waits for batch k-1's (no idle extraction lane while "
+                         "the host enqueues a chain; needs --lanes >= 3)")
     ap.add_argument("--lane-matchers", type=int, default=1,
                     help="1 (default): every lane after the first tracks on its own ORBmatcher (own stream, "
                          "arena and deferred chain), so the tracking chains of consecutive batches overlap on "
@@ -1036,10 +1041,35 @@ def main():
         for ln in lanes:
             for ex in (ln.exL, ln.exR):
                 check(L.ORBextractor_reserve_cus(ex._h, args.reserve_cus), "ORBextractor_reserve_cus")
-    ex_pool = ThreadPoolExecutor(1, initializer=lambda: torch.cuda.set_device(dev))
-    state = {"k": 0, "ready": None, "pending": None}
+    if args.depth > 1 and len(lanes) < 3:
+        sys.exit("bench.py: --depth 2 needs --lanes >= 3 (a lane's buffers are reused by batch k + lanes)")
+    ex_pool = ThreadPoolExecutor(2 if args.depth > 1 else 1, initializer=lambda: torch.cuda.set_device(dev))
+    state = {"k": 0, "ready": None, "pending": None, "inflight": None}
+
+    def step_deep():
+        """Two extractions in flight: batch k's extraction is queued first (a worker thread; its
+        kernels wait only for the GPU), then the host waits for batch k-1's extraction, enqueues its
+        tracking chain and collects batch k-2's counts.  The extraction lane never idles while the
+        host enqueues a chain.  -> the collected batch's counts (None before the pipeline is full)."""
+        lane = lanes[state["k"] % len(lanes)]
+        te = time.perf_counter()
+        fut = ex_pool.submit(lane.extract)
+        res = None
+        if state["inflight"] is not None:
+            pl, pf = state["inflight"]
+            pf.result()
+            pl.enqueue()
+            if state["pending"] is not None:
+                res = state["pending"].collect()
+            state["pending"] = pl
+        state["inflight"] = (lane, fut)
+        phase_acc["step_wall"] = phase_acc.get("step_wall", 0.0) + (time.perf_counter() - te) * 1e3
+        state["k"] += 1
+        return res
 
     def step():
+        if args.depth > 1:
+            return step_deep()
         """Software pipeline over two lanes: the extraction of batch k (worker threads, extractor
         streams) runs while batch k-1's tracking chain is queued on the matcher stream right
         behind batch k-2's; batch k-2's counts are collected while k-1's chain runs.  -> the
@@ -1157,6 +1187,11 @@ def main():
     def drain():
         """Track the extracted batch, collect every chain in order, leave the matcher synchronous."""
         out = []
+        if state["inflight"] is not None:   # (--depth 2) the batch being extracted
+            pl, pf = state["inflight"]
+            pf.result()
+            state["inflight"] = None
+            state["ready"] = pl
         if state["ready"] is not None:
             state["ready"].enqueue()
             if state["pending"] is not None:
