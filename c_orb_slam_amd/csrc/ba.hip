@@ -3762,8 +3762,23 @@ __global__ void __launch_bounds__(256) k_pair_pos(int32_t* pairA, int32_t* pairB
     pairB[t] = pePos[pairB[t]];
 }
 
+// ORBGPU_ND_ASYNC=0 builds the block-sparse structure before the first LM launch (A/B)
+static bool nd_async() {
+    static const bool v = [] {
+        const char* e = getenv("ORBGPU_ND_ASYNC");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
+int BaEngine::join_sp_build() {
+    if (!spBuild_.valid()) return 0;
+    return spBuild_.get();
+}
+
 // initializeOptimization(level) + buildIndexMapping + BlockSolver::buildStructure
 int BaEngine::build_structure(int level) {
+    if (int e = join_sp_build()) return e;   // (a previous structure's helper, if any)
     using sclk = std::chrono::steady_clock;
     static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;
     auto ts0 = sclk::now();
@@ -3985,8 +4000,22 @@ int BaEngine::build_structure(int level) {
         for (int64_t q : all) adj[fillp[q % nP]++] = (int)(q / nP);
         for (int i = 0; i < nP; i++) std::sort(adj.begin() + as[i], adj.begin() + as[i + 1]);
         lap("pack + pose graph");
-        if (int e = sp_.build(6 * nP, 6, as, adj, true, stream_)) return e;
-        lap("nested dissection + symbolic factorisation");
+        if (!comm_ && nd_async()) {
+            // the nested dissection and symbolic factorisation (host, ~1.6 ms at 2,000 keyframes)
+            // run on a helper thread while this thread queues the first LM iteration's
+            // linearisation and reductions, which do not touch the block structure; lm_solve joins
+            // before the Schur assembly (join_sp_build)
+            int dev = 0;
+            ORB_HIP_CHECK(hipGetDevice(&dev));
+            spBuild_ = std::async(std::launch::async, [this, nP, dev, as = std::move(as), adj = std::move(adj)]() {
+                if (hipSetDevice(dev) != hipSuccess) return -2;   // the current device is per thread
+                return sp_.build(6 * nP, 6, as, adj, true, stream_);
+            });
+            lap("nested dissection + symbolic factorisation started");
+        } else {
+            if (int e = sp_.build(6 * nP, 6, as, adj, true, stream_)) return e;
+            lap("nested dissection + symbolic factorisation");
+        }
         distOk_ = false;
         if (comm_ && comm_->size() > 1 && dist_enabled() && sp_.plan(comm_->size(), comm_->rank(), stream_) == 0) {
             // the sharded factorisation needs every rank's points inside its own subtrees and the
@@ -4171,6 +4200,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     // n <= 128: register-resident single-workgroup LDL^T; S fits LDS: single-workgroup in LDS;
     // larger: block-sparse tiled LDL^T in HBM (ldlt.hip, structure from build_structure)
     if (!tiled_ && n > 0 && !use_reg && !in_lds) return -1;
+    if (int e = join_sp_build()) return e;   // the block structure, built beside the first linearisation
     const SysAddr sa = tiled_ ? sp_.addr() : SysAddr{dS_, n, nullptr, nullptr, 0, nullptr};
     do {
         // setLambda + BlockSolver::solve
@@ -4539,7 +4569,10 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
     // every exit
     struct EdgeRefs {
         BaEngine* e;
-        ~EdgeRefs() { e->ePt_ = e->eKf_ = nullptr; }
+        ~EdgeRefs() {
+            e->ePt_ = e->eKf_ = nullptr;
+            (void)e->join_sp_build();   // no helper thread outlives the call
+        }
     } edgeRefs{this};
     trace_ = BaTrace{};
     // a one-rank group is the unsharded call: every exchange would be the identity, so none is

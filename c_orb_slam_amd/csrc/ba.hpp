@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <future>
 #include <vector>
 
 #include "../../include/orbslam_gpu.h"
@@ -113,6 +114,9 @@ private:
     double *tmpA0_ = nullptr, *tmpA1_ = nullptr, *tmpB0_ = nullptr, *tmpB1_ = nullptr;
     unsigned* dCounter_ = nullptr;
     SparseLdlt sp_;                // block-sparse pose system (n > the dense solvers' reach)
+    std::future<int> spBuild_;     // sp_.build on a helper thread (unsharded global BA): joined by
+                                   // join_sp_build() before the first use of sp_ (lm_solve's Schur)
+    int join_sp_build();
     bool tiled_ = false;
     bool distOk_ = false;   // sharded factorisation planned and the ranks' points aligned to it
     void* arena_ = nullptr;

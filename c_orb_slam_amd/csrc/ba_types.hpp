@@ -5,7 +5,7 @@
 
 namespace orbgpu {
 
-struct EdgeDev {  // one g2o edge (vertex 0 = point, vertex 1 = keyframe pose)
+struct alignas(16) EdgeDev {  // one g2o edge (vertex 0 = point, vertex 1 = keyframe pose); 16-B aligned: 16-B loads
     double obs[3];
     double info;            // invSigma2 (float -> double)
     double fx, fy, cx, cy, bf;
