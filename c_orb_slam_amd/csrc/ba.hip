@@ -592,10 +592,17 @@ __device__ __forceinline__ void land_reduce_thread(const BaStructDev& s, const d
     else bl[3 * l + (q - 9)] = v;
 }
 
+// Threads entry-major: thread g takes entry q = g / nL of landmark l = g mod nL, so neighbouring
+// threads read one SoA column at neighbouring landmarks' edges (a landmark's active edges are
+// consecutive in edge order: coalesced), not twelve columns of one landmark (twelve lines per
+// wave load).  The same values as land_reduce_thread's landmark-major order.
 __global__ void __launch_bounds__(256) k_land_reduce(BaStructDev s, const double* __restrict__ terms, double* Hll,
                                                      double* bl, const int* run) {
     BA_GATE(run);
-    land_reduce_thread(s, terms, Hll, bl, blockIdx.x * blockDim.x + threadIdx.x);
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= 12 * s.nL) return;
+    const int q = g / s.nL, l = g - q * s.nL;
+    land_reduce_thread(s, terms, Hll, bl, 12 * l + q);
 }
 
 // both reductions of buildSystem in one launch: blocks [0, nP) reduce a pose each, the rest
