@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--lanes", type=int, default=2,
                     help="batches in flight (buffer sets): extraction of batch k waits for the tracking chain "
                          "of batch k - lanes, which last used its buffers")
+    ap.add_argument("--sequence", type=int, default=0,
+                    help="1: sequence-shaped pipeline -- the B frame pairs of a step are B sequences in lock step "
+                         "(sequence s tracks image s+t at step t): each pair's LastFrame pose and motion-model "
+                         "prediction come from the previous steps' ESTIMATES (Tracking.cc:867-928), not the "
+                         "generator's poses, so step t's tracking waits for step t-1's")
     ap.add_argument("--depth", type=int, default=1,
                     help="extractions in flight: 1 = batch k's extraction is submitted after batch k-1's chain "
                          "is enqueued and waited for within the step; 2 = batch k's extraction is queued at the "
@@ -353,13 +358,22 @@ def main():
             self.d_poutl2 = torch.zeros((P, cap), dtype=torch.uint8, device=dev)
             self.isig_tab = torch.from_numpy(self.exL.GetInverseScaleSigmaSquares()).to(dev)
             self.bs = [max(0, p - K_LOCAL + 1) for p in range(P)]                   # first local block of pair p
+            # the poses the chain reads: the generator's (batch mode) or, with --sequence, the lane's
+            # own arrays rewritten at the start of every chain from the previous steps' estimates
+            if args.sequence:
+                self.sPred = d_Tcw.clone()   # [b]: motion-model prediction for current frame b
+                self.sLast = d_Tcw.clone()   # [b]: LastFrame.mTcw of frame b
+                self.sTwc = d_Twc.clone()    # [b]: its inverse (UnprojectStereo of frame b)
+                Tpred_, Tlast_, Twc_ = self.sPred, self.sLast, self.sTwc
+            else:
+                Tpred_, Tlast_, Twc_ = d_Tcw, d_Tcw, d_Twc
             # ctypes views of the batch, built once (device pointers do not move; only counts change)
-            self.curs = (orb_frame * P)(*[self.frame_struct(b, d_Tcw[b].data_ptr()) for b in range(1, B)])
+            self.curs = (orb_frame * P)(*[self.frame_struct(b, Tpred_[b].data_ptr()) for b in range(1, B)])
             # TrackLocalMap sees mCurrentFrame.mTcw as set by the first PoseOptimization
             self.curs_local = (orb_frame * P)(*[self.frame_struct(b, self.d_Tout[b - 1].data_ptr())
                                                 for b in range(1, B)])
 
-            self.lasts = (orb_frame * P)(*[self.frame_struct(b, d_Tcw[b].data_ptr()) for b in range(0, B - 1)])
+            self.lasts = (orb_frame * P)(*[self.frame_struct(b, Tlast_[b].data_ptr()) for b in range(0, B - 1)])
             self.mps = (orb_mappoints * P)()
             self.lmaps = (orb_localmap * P)()
             for p in range(P):
@@ -385,7 +399,7 @@ def main():
             # (UnprojectStereo with its absolute Twc + UpdateNormalAndDepth) -> block b of the
             # table; row ids relative to the local map of pair b, whose last frame b is
             self.newp = (orb_newpoints * B)(*[
-                orb_newpoints(0, self.d_kps[b].data_ptr(), self.d_depth[b].data_ptr(), d_Twc[b].data_ptr(),
+                orb_newpoints(0, self.d_kps[b].data_ptr(), self.d_depth[b].data_ptr(), Twc_[b].data_ptr(),
                               float(fx), float(fy), float(cx), float(cy), self.scale.data_ptr(), 8,
                               (b - max(0, b - K_LOCAL + 1)) * cap, self.d_mp_pos[b].data_ptr(),
                               self.d_slot[b].data_ptr(), self.d_nrm[b].data_ptr(), self.d_maxd[b].data_ptr(),
@@ -397,7 +411,7 @@ def main():
             # PoseOptimization(&mCurrentFrame): the frame's own arrays, map points by local-map index;
             # TrackWithMotionModel's call from the motion-model pose, TrackLocalMap's from its result
             self.pframes = (pose_frame * P)(*[
-                pose_frame(0, d_Tcw[p + 1].data_ptr(), self.d_cur_mp[p + 1].data_ptr(),
+                pose_frame(0, Tpred_[p + 1].data_ptr(), self.d_cur_mp[p + 1].data_ptr(),
                            self.d_mp_pos[self.bs[p]].data_ptr(), self.d_kps[p + 1].data_ptr(),
                            self.d_uR[p + 1].data_ptr(), self.isig_tab.data_ptr(), 8, float(fx), float(fy), float(cx),
                            float(cy), float(mbf)) for p in range(P)])
@@ -526,6 +540,8 @@ def main():
             nL, nR = self.nL, self.nR
             self.kp_count = int(nL.sum() + nR.sum())
             check(L.ORBmatcher_set_deferred(self.m._h, 1), "ORBmatcher_set_deferred")
+            if args.sequence:
+                seq_predict(self)
             self.stereo()
             t2 = time.perf_counter()
             self.search()
@@ -536,6 +552,8 @@ def main():
                   "PoseOptimization batch")
             t4 = time.perf_counter()
             self.local_map()
+            if args.sequence:
+                seq_record(self)
             t5 = time.perf_counter()
             eid = C.c_longlong(0)
             check(L.ORBmatcher_chain_close(self.m._h, C.byref(eid)), "ORBmatcher_chain_close")
@@ -567,7 +585,7 @@ def main():
         Ti[:3, 3] = -(R.T @ T[:3, 3])
         return Ti
 
-    def latency_leg(nf, host_io=False):
+    def latency_leg(nf, host_io=False, mm=None, barrier=None):
         """Per-frame tracking latency, the reference's own figure (wall time of one TrackStereo,
         stereo_kitti.cc:80-97): batch 1, frames in sequence, each frame's motion model from the
         previous frames' optimised poses (Tracking.cc:869, mVelocity), the local map from the last
@@ -578,6 +596,12 @@ def main():
         images, mvuRight, mvDepth, mTcw, mvpMapPoints (local-map rows) and mvbOutlier -- before the
         clock stops.  Otherwise the images are HBM-resident and the results stay on the device."""
         nf = min(nf, B)
+        # mm: this leg's own ORBmatcher (sequence_leg runs several legs on their own threads);
+        # barrier: a threading.Barrier the legs pass together right before their timed frames
+        own_gc = mm is None
+        if mm is None:
+            mm = m
+        mstream = match_stream if mm is m else torch.cuda.ExternalStream(L.ORBmatcher_stream(mm._h), device=dev)
         if host_io:
             hk = torch.empty((cap, 7), dtype=torch.int32).pin_memory()
             hd = torch.empty((cap, 32), dtype=torch.uint8).pin_memory()
@@ -630,7 +654,7 @@ def main():
         except OSError:
             hip_rt = None
         tb_args = (C.c_void_p(Tbuf.data_ptr()), C.c_void_p(Thbuf.data_ptr()), C.c_size_t(4 * (48 + cap)), 1,
-                   C.c_void_p(match_stream.cuda_stream))
+                   C.c_void_p(mstream.cuda_stream))
         Tpred, Tlast, Twc_l = Tdev[0:16], Tdev[16:32], Tdev[32:48]
         T1, T2 = (torch.zeros(16, dtype=torch.float32, device=dev) for _ in range(2))
         o1, o2 = (torch.zeros(cap, dtype=torch.uint8, device=dev) for _ in range(2))
@@ -689,9 +713,13 @@ def main():
         # the drop-in caller is C++ (System::TrackStereo): no interpreter garbage collection runs
         # between its frames, so none runs inside this leg's timed frames either
         import gc
-        gc_was = gc.isenabled()
-        gc.collect()
-        gc.disable()
+        gc_was = gc.isenabled() and own_gc
+        if own_gc:
+            gc.collect()
+            gc.disable()
+        if barrier is not None:
+            barrier.wait()
+        t_begin = time.perf_counter()
         try:  # a failing check() must not leave the collector off for the rest of the bench
             for t in range(nf):
                 torch.cuda.synchronize()
@@ -708,7 +736,7 @@ def main():
                     nL, nR = nLR[:1], nLR[1:]
                     nl[0], nr[0] = nLR[0], nLR[1]
                     a0, a1, a2, a3, a4, a5 = pre[t]["stereo_lr"]
-                    check(L.ORBmatcher_ComputeStereoMatches_batch_at(m._h, eLRh._h, 0, eLRh._h, 1, 1, ptr(nl), a0, a1,
+                    check(L.ORBmatcher_ComputeStereoMatches_batch_at(mm._h, eLRh._h, 0, eLRh._h, 1, 1, ptr(nl), a0, a1,
                                                                      ptr(nr), a2, a3, float(mbf), float(mb), a4, a5,
                                                                      ptr(one)), "ComputeStereoMatches")
                 elif host_io:   # the same as two extractor calls on two threads
@@ -730,7 +758,7 @@ def main():
                     nR = fR.result()
                     mark("extract_both")
                     nl, nr = np.array([nL[0]], np.int32), np.array([nR[0]], np.int32)
-                    check(L.ORBmatcher_ComputeStereoMatches_batch(m._h, eL1._h, eR1._h, 1, ptr(nl), arr([k[t].data_ptr()]),
+                    check(L.ORBmatcher_ComputeStereoMatches_batch(mm._h, eL1._h, eR1._h, 1, ptr(nl), arr([k[t].data_ptr()]),
                                                                   arr([d[t].data_ptr()]), ptr(nr), arr([kR.data_ptr()]),
                                                                   arr([dR.data_ptr()]), float(mbf), float(mb),
                                                                   arr([uR[t].data_ptr()]), arr([dep[t].data_ptr()]),
@@ -740,7 +768,7 @@ def main():
                     nL = nLR[:1]
                     nl[0], nr[0] = nLR[0], nLR[1]
                     a0, a1, a2, a3, a4, a5 = pre[t]["stereo_lr"]
-                    check(L.ORBmatcher_ComputeStereoMatches_batch_at(m._h, eLR._h, 0, eLR._h, 1, 1, ptr(nl), a0, a1,
+                    check(L.ORBmatcher_ComputeStereoMatches_batch_at(mm._h, eLR._h, 0, eLR._h, 1, 1, ptr(nl), a0, a1,
                                                                      ptr(nr), a2, a3, float(mbf), float(mb), a4, a5,
                                                                      ptr(one)), "ComputeStereoMatches")
                 mark("stereo")
@@ -757,16 +785,16 @@ def main():
                         if hip_rt.hipMemcpyAsync(*tb_args) != 0:
                             raise RuntimeError("hipMemcpyAsync")
                     else:
-                        with torch.cuda.stream(match_stream):
+                        with torch.cuda.stream(mstream):
                             Tbuf.copy_(Thbuf, non_blocking=True)
                     u = g["u"]
                     u.N = nlast
-                    check(L.MapPoint_CreateStereo_batch_device(m._h, 1, C.byref(u)), "MapPoint_CreateStereo")
+                    check(L.MapPoint_CreateStereo_batch_device(mm._h, 1, C.byref(u)), "MapPoint_CreateStereo")
                     fc, fl, mp, pf = g["fc"], g["fl"], g["mp"], g["pf"]
                     fc.N, fl.N, pf.N = int(nL[0]), nlast, int(nL[0])
                     fc.Tcw, pf.Tcw = Tpp, Tpp
                     a0, a1, a2, a3 = g["last"]
-                    check(L.ORBmatcher_SearchByProjection_LastFrame_batch(m._h, 1, C.byref(fc), a0, C.byref(fl), a1, a2, a3,
+                    check(L.ORBmatcher_SearchByProjection_LastFrame_batch(mm._h, 1, C.byref(fc), a0, C.byref(fl), a1, a2, a3,
                                                                           C.byref(mp), 7.0, 0, ptr(nm1)),
                           "SearchByProjection(Last)")
                     b0, b1 = g["pose1"]
@@ -774,9 +802,9 @@ def main():
                     mark("motion_model")
                     prep = g["prep"]
                     prep.N = int(nL[0])
-                    check(L.Tracking_PrepareLocalSearch_batch_device(m._h, 1, C.byref(prep)), "PrepareLocalSearch")
+                    check(L.Tracking_PrepareLocalSearch_batch_device(mm._h, 1, C.byref(prep)), "PrepareLocalSearch")
                     fc.Tcw = T1p
-                    check(L.ORBmatcher_SearchLocalPoints_batch(m._h, 1, C.byref(fc), g["cur"], C.byref(g["lmap"]), float(lsf),
+                    check(L.ORBmatcher_SearchLocalPoints_batch(mm._h, 1, C.byref(fc), g["cur"], C.byref(g["lmap"]), float(lsf),
                                                                1.0, 0.8, ptr(nm2), ptr(nv2)), "SearchLocalPoints")
                     mark("local_search")
                     pf.Tcw = T1p
@@ -785,7 +813,7 @@ def main():
                     mark("local_pose")
                     if host_io:   # the Frame's members back on the host (one stream sync)
                         n0, n1 = int(nL[0]), int(nR[0])
-                        with torch.cuda.stream(match_stream):
+                        with torch.cuda.stream(mstream):
                             hk[:n0].copy_(k[t, :n0], non_blocking=True)
                             hd[:n0].copy_(d[t, :n0], non_blocking=True)
                             hkR[:n1].copy_((k[t + 1] if host_pair else kR)[:n1], non_blocking=True)
@@ -795,7 +823,7 @@ def main():
                             hT.copy_(T2, non_blocking=True)
                             hmp[:n0].copy_(cur_mp[:n0], non_blocking=True)
                             hout[:n0].copy_(o2[:n0], non_blocking=True)
-                        match_stream.synchronize()
+                        mstream.synchronize()
                         d2h_bytes.append(n0 * (28 + 32 + 4 + 4 + 4 + 1) + n1 * 60 + 64)
                         Tcw.append(hT.numpy().reshape(4, 4).copy())
                     else:
@@ -807,9 +835,11 @@ def main():
         finally:
             if gc_was:
                 gc.enable()
+        t_end = time.perf_counter()
         w = np.array(walls[2:])   # the first two frames have no motion model / local map yet
         err = [float(np.abs(Tcw[t][:3, :3] - Tabs[t][:3, :3]).max()) for t in range(1, len(Tcw))]
         out = {"metric": "tracking latency per stereo frame (batch 1, sequential)", "mean_ms": round(float(w.mean()), 3),
+               "_span_s": (t_begin, t_end),
                "p50_ms": round(float(np.percentile(w, 50)), 3), "p90_ms": round(float(np.percentile(w, 90)), 3),
                "frames": int(len(w)), "matches_per_frame": round(float(np.mean(nmatch)), 1),
                "frame_ms": [round(float(v), 3) for v in walls],
@@ -837,6 +867,57 @@ def main():
         else:
             out["io"] = "device: images HBM-resident, results left in HBM"
         return out
+
+    def sequence_leg(S, nf):
+        """Sequence-shaped throughput: S independent stereo sequences tracked concurrently, each
+        frame by frame in order exactly as the latency leg tracks one (the motion model from the
+        sequence's own previous estimated poses, Tracking.cc:867-928; the local map from its last
+        K_LOCAL frames; every call synchronous, Frame + TrackWithMotionModel + TrackLocalMap), each
+        sequence on its own host thread with its own matcher, extractor and buffers (a serving
+        process with S camera streams, or S SLAM sessions).  -> frames/s over all sequences."""
+        import threading
+        import gc
+        mts = []
+        for _ in range(S):
+            mt = orb.ORBmatcher(0.9, True)
+            check(L.ORBmatcher_set_device_pointers(mt._h, 1))
+            mts.append(mt)
+        bar = threading.Barrier(S)
+        outs, errs = [None] * S, [None] * S
+
+        def work(i):
+            try:
+                torch.cuda.set_device(dev)
+                outs[i] = latency_leg(nf, mm=mts[i], barrier=bar)
+            except Exception as e:  # noqa: BLE001 -- re-raised below
+                errs[i] = e
+                bar.abort()
+
+        gc_was = gc.isenabled()
+        gc.collect()
+        gc.disable()
+        try:
+            ts = [threading.Thread(target=work, args=(i,)) for i in range(S)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+        finally:
+            if gc_was:
+                gc.enable()
+        for e in errs:
+            if e is not None:
+                raise e
+        t0 = min(o["_span_s"][0] for o in outs)
+        t1 = max(o["_span_s"][1] for o in outs)
+        frames = S * min(nf, B)
+        p50 = [o["p50_ms"] for o in outs]
+        return {"metric": "tracked stereo frames/s, S concurrent sequences (frames in order, batch 1 each)",
+                "value": round(frames / (t1 - t0), 1), "unit": "frames/s", "sequences": S,
+                "frames_per_sequence": min(nf, B), "wall_s": round(t1 - t0, 4),
+                "p50_ms_per_frame_range": [round(min(p50), 3), round(max(p50), 3)],
+                "max_rotation_error": round(max(o["max_rotation_error"] for o in outs), 6),
+                "io": "device: images HBM-resident, results left in HBM (each sequence as latency.p50_ms)"}
 
     def matcher_pass(lane, reps):
         """Isolated matcher launches with device timing and work counters:
@@ -1033,6 +1114,48 @@ def main():
             check(L.ORBmatcher_set_device_pointers(lane_m[-1]._h, 1))
         else:
             lane_m.append(m)
+    # --sequence: a ring of three (B, 4, 4) estimate sets (est[t % 3][b] = the estimate of image b
+    # made at step t; image 0 has no pair and keeps the generator's pose as the anchor) and the
+    # event after the last chain's estimates
+    seq = {"est": [d_Tcw.view(B, 4, 4).clone() for _ in range(3)], "t": 0, "ev": None}
+
+    def rigid_inv_t(T):
+        """Batched Twc from Tcw (Frame::UpdatePoseMatrices: R^T, -R^T t)."""
+        Ti = torch.zeros_like(T)
+        Rt = T[:, :3, :3].transpose(1, 2)
+        Ti[:, :3, :3] = Rt
+        Ti[:, :3, 3] = -(Rt @ T[:, :3, 3:4])[:, :, 0]
+        Ti[:, 3, 3] = 1.0
+        return Ti
+
+    def seq_predict(lane):
+        """Per sequence (pair p: LastFrame = image p, CurrentFrame = image p + 1): LastFrame.mTcw is
+        image p's estimate from the previous step, mVelocity = T_{c-1} T_{c-2}^-1 from the previous
+        two steps' estimates, the prediction mVelocity T_{c-1} (Tracking.cc:867-928, 1281-1291), all
+        on the lane's matcher stream after the previous step's estimates landed."""
+        t = seq["t"]
+        e1, e2 = seq["est"][(t - 1) % 3], seq["est"][(t - 2) % 3]
+        with torch.cuda.stream(lane.ms):
+            if seq["ev"] is not None:
+                lane.ms.wait_event(seq["ev"])
+            lane.sLast.copy_(e1.reshape(B, 16))
+            lane.sTwc.copy_(rigid_inv_t(e1).reshape(B, 16))
+            Tm1 = e1[:-1]                                            # T_{c-1}, c = 1 .. B-1
+            V = torch.eye(4, dtype=torch.float32, device=dev).repeat(B - 1, 1, 1)
+            V[1:] = Tm1[1:] @ rigid_inv_t(e2[:-2])                    # c >= 2: T_{c-1} T_{c-2}^-1
+            lane.sPred[1:].copy_((V @ Tm1).reshape(B - 1, 16))
+
+    def seq_record(lane):
+        """This step's estimates (TrackLocalMap's PoseOptimization) into the ring, then the event the
+        next step's chain waits on."""
+        t = seq["t"]
+        with torch.cuda.stream(lane.ms):
+            seq["est"][t % 3][1:].copy_(lane.d_Tout2.view(P, 4, 4))
+            ev = torch.cuda.Event()
+            ev.record(lane.ms)
+        seq["ev"] = ev
+        seq["t"] = t + 1
+
     lanes = [Lane(mt) for mt in lane_m]
     exL = lanes[0].exL
     if args.reserve_cus:
@@ -1265,12 +1388,16 @@ def main():
         if rank == 0:
             lat = latency_leg(24)
             lat["host_path"] = latency_leg(24, host_io=True)
+            lat["sequences"] = {str(S): sequence_leg(S, 24) for S in (4, 16)}
+            for v in (lat, lat["host_path"]):
+                v.pop("_span_s", None)
             print(json.dumps({"latency": lat}), file=json_out, flush=True)
         return
     if args.pipeline_only:   # the yaml feature count's line: pipeline + its CPU baseline
         if rank == 0:
             cpu = None if args.no_cpu_baseline else cpu_baseline(lefts, rights, Rs, args.cpu_seconds)
             line = {"nfeatures": NFEAT, "value": round(fps, 2), "unit": "frames/s", "steps": args.steps,
+                    "sequence": bool(args.sequence),
                     "ms_per_step": round(dt / args.steps * 1e3, 3), "tracked_frames_per_step": P,
                     "matches_per_s": round(tot_match / dt, 1),
                     "keypoints_per_image": round(tot_kp / (2 * B * args.steps * world), 1), "cpu_baseline": cpu,
@@ -1278,6 +1405,13 @@ def main():
                     "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}}
             if cpu:
                 line["speedup_vs_cpu_all_core"] = round(fps / cpu["value"], 1)
+            if args.sequence:   # the estimates stay on the true trajectory (rotation, max abs entry)
+                torch.cuda.synchronize()
+                est = seq["est"][(seq["t"] - 1) % 3][1:, :3, :3]
+                line["max_rotation_error"] = round(float((est - d_Tcw.view(B, 4, 4)[1:, :3, :3]).abs().max()), 6)
+                line["note"] = ("B sequences in lock step: every pair's LastFrame pose and motion-model prediction "
+                                "from the previous steps' estimates (device-side, no host round trip), so each step's "
+                                "tracking chain waits for the previous step's")
             json_out.write(json.dumps(line) + "\n")
             json_out.flush()
         if world > 1:
@@ -1342,6 +1476,9 @@ def main():
         return
     latency = latency_leg(24)
     latency["host_path"] = latency_leg(24, host_io=True)
+    latency["sequences"] = {str(S): sequence_leg(S, 24) for S in (4, 16)}
+    for v in [latency] + [latency["host_path"]]:
+        v.pop("_span_s", None)
 
     # CPU baselines (the reference CPU path timed "in the same run"): rank 0 only.  At
     # N = 1 each runs right after its GPU leg; at N > 1 rank 0 runs them all after every GPU leg,
@@ -1371,7 +1508,7 @@ def main():
         dist.barrier()
 
     ransac.pop("_cpu_args", None)
-    nf2000 = None
+    nf2000 = seqline = None
     if rank == 0 and world == 1 and NFEAT != 2000:
         # the same pipeline at the yaml's nFeatures 2000 (KITTI00-02.yaml:38) in a
         # fresh process (its own extractors and arenas), with its own CPU baseline
@@ -1386,6 +1523,16 @@ def main():
                 {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-400:]}
         except Exception as e:  # noqa: BLE001 -- reported in the line, the headline stands
             nf2000 = {"error": f"{type(e).__name__}: {e}"}
+        # the sequence-shaped pipeline (--sequence 1): the same step with each pair's poses from the
+        # previous steps' estimates, in a fresh process
+        cmd = [sys.executable, str(Path(__file__).resolve()), "--sequence", "1", "--pipeline-only", "--no-cpu-baseline",
+               "--steps", str(max(10, args.steps // 2)), "--warmup", "3"]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+            seqline = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+                {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-400:]}
+        except Exception as e:  # noqa: BLE001 -- reported in the line, the headline stands
+            seqline = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:
         stage_ms = {k: round(v / args.steps, 4) for k, v in stage_acc.items()}
         out = {
@@ -1413,7 +1560,7 @@ def main():
             "stage_ms_per_step_by_image": stage_by_stream(),
             "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}, "roofline": roof,
             "matcher_roofline": mroof, "latency": latency, "cpu_baseline": cpu, "local_ba": ba,
-            "global_ba": gba, "ransac": ransac, "nfeatures_2000": nf2000,
+            "global_ba": gba, "ransac": ransac, "nfeatures_2000": nf2000, "sequence_pipeline": seqline,
         }
         if host_io is not None:
             host_io["frac_of_value"] = round(host_io["value"] / fps, 3)
