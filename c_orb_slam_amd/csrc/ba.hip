@@ -34,6 +34,7 @@
 #include "ba_math.hpp"
 #include "ba_struct.hpp"
 #include "detmath.hpp"
+#include "host_par.hpp"
 #include "ldlt.hpp"
 #include "orb_common.hpp"
 
@@ -3624,26 +3625,6 @@ __global__ void __launch_bounds__(256) k_unpack_upload(UploadArgs a) {
     if (i < 16) a.counter[i] = 0;
 }
 
-// Host loops over large problems (a global BA's 1.5 M edges) on up to 16 threads, in contiguous
-// ranges; small problems (a local BA) stay on the calling thread
-template <class F>
-static void host_parallel(int n, F f, int minN = 1 << 18) {
-    const int hw = (int)std::thread::hardware_concurrency();
-    const int T = n >= minN ? std::max(1, std::min(16, hw)) : 1;
-    if (T <= 1) {
-        f(0, n);
-        return;
-    }
-    std::vector<std::thread> th;
-    const int chunk = (n + T - 1) / T;
-    for (int t = 1; t < T; t++) {
-        const int a = t * chunk, b = std::min(n, a + chunk);
-        if (a < b) th.emplace_back([&f, a, b] { f(a, b); });
-    }
-    f(0, std::min(n, chunk));
-    for (auto& x : th) x.join();
-}
-
 int BaEngine::upload_problem(const ba_problem* P) {
     nkf_ = P->n_kf;
     npt_ = P->n_pt;
@@ -3671,7 +3652,6 @@ int BaEngine::upload_problem(const ba_problem* P) {
         kfFixed_[k] = ((!mode_.global && !P->kf_local[k]) || P->kf_id[k] == 0) ? 1 : 0;
     if (mode_.global) kfLocal_.assign(nkf_, 1);
     ptHasEdge_.assign(npt_, 0);
-    for (int i = 0; i < ne_; i++) ptHasEdge_[P->edge_pt[i]] = 1;
     // poses, points, compact edges and vertex data written straight into the pinned staging block
     // (no intermediate host copy): one H2D copy, unpacked by k_unpack_upload
     const UploadLayout UL = upload_layout(ne_, nkf_, npt_);
@@ -3684,8 +3664,13 @@ int BaEngine::upload_problem(const ba_problem* P) {
     std::memcpy(st + UL.oPid, P->pt_id, sizeof(int32_t) * npt_);
     std::memcpy(st + UL.oCam, P->kf_cam, sizeof(float) * 5 * nkf_);
     for (int k = 0; k < nkf_; k++) host_se3_from_Tcw(P->kf_Tcw + 16 * k, Ts[k]);
-    for (size_t q = 0; q < 3 * (size_t)npt_; q++) Xs[q] = (double)P->pt_pos[q];
+    host_parallel(npt_, [&](int a, int b) {
+        for (size_t q = 3 * (size_t)a; q < 3 * (size_t)b; q++) Xs[q] = (double)P->pt_pos[q];
+    });
+    uint8_t* hasEdge = ptHasEdge_.data();
     host_parallel(ne_, [&](int a, int b) {
+        // (ranges share points: the flag bytes are stored atomically, all with the same value)
+        for (int i = a; i < b; i++) __atomic_store_n(&hasEdge[P->edge_pt[i]], (uint8_t)1, __ATOMIC_RELAXED);
         std::memcpy(st + UL.oPt + sizeof(int32_t) * a, P->edge_pt + a, sizeof(int32_t) * (b - a));
         std::memcpy(st + UL.oKf + sizeof(int32_t) * a, P->edge_kf + a, sizeof(int32_t) * (b - a));
         std::memcpy(st + UL.oObs + sizeof(float) * 3 * (size_t)a, P->edge_obs + 3 * (size_t)a, sizeof(float) * 3 * (b - a));
@@ -3784,6 +3769,29 @@ int BaEngine::join_sp_build() {
 }
 
 // initializeOptimization(level) + buildIndexMapping + BlockSolver::buildStructure
+// The pose graph of the Schur pattern's off-diagonal blocks (keys i1 * nP + i2, i1 < i2; any order,
+// duplicates allowed) as sorted adjacency lists: as[i] .. as[i + 1] of adj
+static void pose_graph_csr(int nP, std::vector<int64_t>& all, std::vector<int>* asOut, std::vector<int>* adjOut) {
+    std::sort(all.begin(), all.end());
+    all.erase(std::unique(all.begin(), all.end()), all.end());
+    std::vector<int> deg(nP + 1, 0);
+    std::vector<int>& as = *asOut;
+    std::vector<int>& adj = *adjOut;
+    as.assign(nP + 1, 0);
+    adj.assign(2 * all.size(), 0);
+    for (int64_t q : all) {
+        deg[q / nP]++;
+        deg[q % nP]++;
+    }
+    for (int i = 0; i < nP; i++) as[i + 1] = as[i] + deg[i];
+    std::vector<int> fillp(as.begin(), as.end() - 1);
+    for (int64_t q : all) {   // (i1, i2) ascending: every list comes out sorted
+        adj[fillp[q / nP]++] = (int)(q % nP);
+    }
+    for (int64_t q : all) adj[fillp[q % nP]++] = (int)(q / nP);
+    for (int i = 0; i < nP; i++) std::sort(adj.begin() + as[i], adj.begin() + as[i + 1]);
+}
+
 int BaEngine::build_structure(int level) {
     if (int e = join_sp_build()) return e;   // (a previous structure's helper, if any)
     using sclk = std::chrono::steady_clock;
@@ -3986,40 +3994,30 @@ int BaEngine::build_structure(int level) {
         // so every rank orders and factors the same structure) -> nested-dissection order,
         // symbolic factorisation; S travels as the Schur-pattern prefix of the tiles
         std::vector<int64_t> mine = std::move(offKeys);
-        std::vector<int64_t> all;
-        if (comm_) {
-            if (int e = gather_blocks(mine, &all)) return e;
-        } else {
-            all = std::move(mine);
-        }
-        std::sort(all.begin(), all.end());
-        all.erase(std::unique(all.begin(), all.end()), all.end());
-        std::vector<int> deg(nP + 1, 0), as(nP + 1, 0), adj(2 * all.size());
-        for (int64_t q : all) {
-            deg[q / nP]++;
-            deg[q % nP]++;
-        }
-        for (int i = 0; i < nP; i++) as[i + 1] = as[i] + deg[i];
-        std::vector<int> fillp(as.begin(), as.end() - 1);
-        for (int64_t q : all) {   // (i1, i2) ascending: every list comes out sorted
-            adj[fillp[q / nP]++] = (int)(q % nP);
-        }
-        for (int64_t q : all) adj[fillp[q % nP]++] = (int)(q / nP);
-        for (int i = 0; i < nP; i++) std::sort(adj.begin() + as[i], adj.begin() + as[i + 1]);
-        lap("pack + pose graph");
         if (!comm_ && nd_async()) {
-            // the nested dissection and symbolic factorisation (host, ~1.6 ms at 2,000 keyframes)
-            // run on a helper thread while this thread queues the first LM iteration's
+            // the pose graph, nested dissection and symbolic factorisation (host, ~2.5 ms at 2,000
+            // keyframes) run on a helper thread while this thread queues the first LM iteration's
             // linearisation and reductions, which do not touch the block structure; lm_solve joins
             // before the Schur assembly (join_sp_build)
             int dev = 0;
             ORB_HIP_CHECK(hipGetDevice(&dev));
-            spBuild_ = std::async(std::launch::async, [this, nP, dev, as = std::move(as), adj = std::move(adj)]() {
+            spBuild_ = std::async(std::launch::async, [this, nP, dev, keys = std::move(mine)]() mutable {
                 if (hipSetDevice(dev) != hipSuccess) return -2;   // the current device is per thread
+                std::vector<int> as, adj;
+                pose_graph_csr(nP, keys, &as, &adj);
                 return sp_.build(6 * nP, 6, as, adj, true, stream_);
             });
-            lap("nested dissection + symbolic factorisation started");
+            lap("pose graph + nested dissection + symbolic factorisation started");
         } else {
+            std::vector<int64_t> all;
+            if (comm_) {
+                if (int e = gather_blocks(mine, &all)) return e;
+            } else {
+                all = std::move(mine);
+            }
+            std::vector<int> as, adj;
+            pose_graph_csr(nP, all, &as, &adj);
+            lap("pose graph");
             if (int e = sp_.build(6 * nP, 6, as, adj, true, stream_)) return e;
             lap("nested dissection + symbolic factorisation");
         }

@@ -1,6 +1,7 @@
 // capi_ba.cpp -- extern "C" Optimizer_LocalBundleAdjustment (include/orbslam_gpu.h).
 // Replaces ORB_SLAM2::Optimizer::LocalBundleAdjustment (reference src/Optimizer.cc:453-778).
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -9,6 +10,7 @@
 #include "ba_struct.hpp"
 #include "ba_struct_gpu.hpp"
 #include "capi_handles.hpp"
+#include "host_par.hpp"
 #include "ordering.hpp"
 #include "orb_match.hpp"
 #include "sim3opt.hpp"
@@ -25,6 +27,48 @@ orbgpu::BaEngine* engine(int* rc) {
     }
     *rc = erc;
     return e;
+}
+
+// Edges grouped by map point: 0 valid, 1 invalid (an index out of range, or a repeated keyframe
+// inside a point's run), 2 some point starts two runs (the caller buckets).  Large problems run
+// on up to 16 threads over ranges of whole runs (a range starts at the first run that starts in
+// it); a run start claims its point with an atomic exchange, so a point met twice is seen by
+// whichever range comes second.
+int grouped_pairs(const ba_problem* P) {
+    const int ne = P->n_edge;
+    const int32_t* ep = P->edge_pt;
+    const int32_t* ek = P->edge_kf;
+    const uint32_t npt = (uint32_t)P->n_pt, nkf = (uint32_t)P->n_kf;
+    std::vector<uint8_t> seen(std::max(P->n_pt, 1), 0);
+    std::atomic<int> bad{0}, rep{0};
+    const auto run_start = [&](int i) {   // first run start at or after i
+        while (i > 0 && i < ne && ep[i] == ep[i - 1]) i++;
+        return i;
+    };
+    orbgpu::host_parallel(ne, [&](int a, int b) {
+        const int i0 = run_start(a), i1 = run_start(b);
+        if (i0 >= i1) return;
+        std::vector<int32_t> stamp(std::max(P->n_kf, 1), -1);
+        int32_t cur = -1, run = -1;
+        bool dup = false, again = false;
+        for (int i = i0; i < i1; i++) {
+            const int32_t pt = ep[i], kf = ek[i];
+            if ((uint32_t)pt >= npt || (uint32_t)kf >= nkf) {
+                dup = true;
+                break;
+            }
+            if (pt != cur) {
+                again |= __atomic_exchange_n(&seen[pt], (uint8_t)1, __ATOMIC_RELAXED) != 0;
+                cur = pt;
+                run++;
+            }
+            dup |= stamp[kf] == run;
+            stamp[kf] = run;
+        }
+        if (dup) bad.store(1, std::memory_order_relaxed);
+        if (again) rep.store(1, std::memory_order_relaxed);
+    });
+    return bad.load() ? 1 : rep.load() ? 2 : 0;
 }
 
 int validate(const ba_problem* P, const ba_result* R) {
@@ -63,23 +107,9 @@ int validate(const ba_problem* P, const ba_result* R) {
     {   // the Optimizer adds each map point's edges together (Optimizer.cc:99-160, 536-627): then one
         // pass with a keyframe stamp per run of equal points checks the pairs; a point met in two
         // runs falls through to the bucketing below
-        std::vector<uint8_t> seen(std::max(P->n_pt, 1), 0);
-        std::vector<int32_t> stamp(std::max(P->n_kf, 1), -1);
-        int32_t cur = -1, run = -1;
-        int i = 0;
-        for (; i < P->n_edge; i++) {
-            const int32_t pt = P->edge_pt[i], kf = P->edge_kf[i];
-            if (pt < 0 || pt >= P->n_pt || kf < 0 || kf >= P->n_kf) return ORB_E_INVALID;
-            if (pt != cur) {
-                if (seen[pt]) break;
-                seen[pt] = 1;
-                cur = pt;
-                run++;
-            }
-            if (stamp[kf] == run) return ORB_E_INVALID;
-            stamp[kf] = run;
-        }
-        if (i == P->n_edge) return ORB_OK;
+        const int g = grouped_pairs(P);
+        if (g == 1) return ORB_E_INVALID;
+        if (g == 0) return ORB_OK;
     }
     std::vector<int32_t> start((size_t)P->n_pt + 1, 0);
     for (int i = 0; i < P->n_edge; i++) {
