@@ -51,23 +51,10 @@ constexpr int kFastSplitLevel = 3;
 // copyMakeBorder(image, temp, 19,19,19,19, BORDER_REFLECT_101), 16 bytes/thread.
 // Interior chunks: the (arbitrarily aligned) source row is read as aligned dwords and
 // realigned with v_alignbyte; the two border chunks of a row reflect byte by byte.
-__global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ src, size_t src_stride, int step,
-                                                    int W, int H, uint8_t* __restrict__ pyr, size_t img_bytes,
-                                                    int pitch, int ph, int* __restrict__ zero0,
-                                                    int* __restrict__ zero1) {
-    const int b = blockIdx.y;
-    // the call's two counters (k_octree's corner total, the octree's error bits), cleared by
-    // the first kernel of the stream instead of two fill launches before their users
-    if (blockIdx.x == 0 && b == 0 && threadIdx.x == 0) {
-        *zero0 = 0;
-        *zero1 = 0;
-    }
-    const int chunks = pitch >> 4;
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= chunks * ph) return;
-    const int py = t / chunks, px0 = (t - py * chunks) * 16;
+// The 16 bytes of padded row py at padded column px0 of one image (src: its first row)
+__device__ __forceinline__ uint4 pyr_l0_chunk(const uint8_t* __restrict__ src, int step, int W, int H, int py, int px0) {
     const int sy = refl101(py - kEdge, H);
-    const uint8_t* srow = src + (size_t)b * src_stride + (size_t)sy * step;
+    const uint8_t* srow = src + (size_t)sy * step;
     const int x0 = px0 - kEdge;
     uint4 o;
     if (x0 >= 0 && x0 + 15 < W) {
@@ -86,6 +73,25 @@ __global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ 
         for (int k = 0; k < 16; k++) v[k >> 2] |= (uint32_t)srow[refl101(x0 + k, W)] << (8 * (k & 3));
         o = make_uint4(v[0], v[1], v[2], v[3]);
     }
+    return o;
+}
+
+__global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ src, size_t src_stride, int step,
+                                                    int W, int H, uint8_t* __restrict__ pyr, size_t img_bytes,
+                                                    int pitch, int ph, int* __restrict__ zero0,
+                                                    int* __restrict__ zero1) {
+    const int b = blockIdx.y;
+    // the call's two counters (k_octree's corner total, the octree's error bits), cleared by
+    // the first kernel of the stream instead of two fill launches before their users
+    if (blockIdx.x == 0 && b == 0 && threadIdx.x == 0) {
+        *zero0 = 0;
+        *zero1 = 0;
+    }
+    const int chunks = pitch >> 4;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= chunks * ph) return;
+    const int py = t / chunks, px0 = (t - py * chunks) * 16;
+    const uint4 o = pyr_l0_chunk(src + (size_t)b * src_stride, step, W, H, py, px0);
     *reinterpret_cast<uint4*>(pyr + (size_t)b * img_bytes + (size_t)py * pitch + px0) = o;
 }
 
@@ -101,20 +107,23 @@ __global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ 
 constexpr int kPyrTileH[2] = {16, 32};
 template <int TH>
 constexpr int stage_regs() { return (((TH * 5 + 3) / 4 + 3) * ((PT_W * 5 / 4 + 12) / 4) + 255) / 256; }
-template <int TH>
-__global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, size_t img_bytes, size_t src_off,
-                                                    int src_pitch, size_t dst_off, int dst_pitch, int dst_ph, int w,
-                                                    int h, const int* __restrict__ xofs,
-                                                    const short2* __restrict__ xalpha, const int2* __restrict__ yrows,
-                                                    const short2* __restrict__ ybeta,
-                                                    const PyrTile* __restrict__ tiles, int ntiles) {
-    extern __shared__ uint32_t s_src[];   // tl.nsr rows x tl.nsw dwords
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
-    if (tile >= ntiles) return;
-    const PyrTile tl = tiles[tile];
-    const int b = blockIdx.y;
+// One tile of a level: the source rectangle staged (dword loads, all in flight), then 4 columns x
+// every 4th row per thread.  WT: the output dwords stored write-through (sc1: handed to other
+// workgroups of the same launch, k_pyr_flow); the stores are then drained by the caller.
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(uint8_t* p, size_t bytes) {
+    const unsigned long long a = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    void* q = (void*)(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)bytes, 0x00020000);
+}
+template <int TH, bool WT>
+__device__ __forceinline__ void pyr_tile(uint8_t* __restrict__ base, size_t img_bytes, size_t src_off, int src_pitch,
+                                         size_t dst_off, int dst_pitch, int w, int h, const int* __restrict__ xofs,
+                                         const short2* __restrict__ xalpha, const int2* __restrict__ yrows,
+                                         const short2* __restrict__ ybeta, const PyrTile& tl, uint32_t* s_src) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint8_t* base = pyr + (size_t)b * img_bytes;
     const uint32_t* S32 = reinterpret_cast<const uint32_t*>(base + src_off + (size_t)(kEdge + tl.sr0) * src_pitch + tl.sc0);
     const int spw = src_pitch >> 2;
     {
@@ -158,6 +167,8 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, s
     if (!col_ok) return;
     const uint8_t* sb = reinterpret_cast<const uint8_t*>(s_src);
     const int rowb = tl.nsw * 4;
+    __amdgpu_buffer_rsrc_t rs;
+    if (WT) rs = slab_rsrc(base, img_bytes);
 #pragma unroll
     for (int i = 0; i < TH / 4; i++) {
         const int j = wid + 4 * i;
@@ -176,8 +187,104 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, s
             const int o = (((bb_.x * (D0 >> 4)) >> 16) + ((bb_.y * (D1 >> 4)) >> 16) + 2) >> 2;
             v |= (uint32_t)(uint8_t)o << (8 * k);
         }
-        *reinterpret_cast<uint32_t*>(base + dst_off + (size_t)py * dst_pitch + px) = v;
+        if (WT)
+            __builtin_amdgcn_raw_buffer_store_b32(v, rs, (int)(dst_off + (size_t)py * dst_pitch + px), 0, 16);
+        else
+            *reinterpret_cast<uint32_t*>(base + dst_off + (size_t)py * dst_pitch + px) = v;
     }
+}
+
+template <int TH>
+__global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, size_t img_bytes, size_t src_off,
+                                                    int src_pitch, size_t dst_off, int dst_pitch, int dst_ph, int w,
+                                                    int h, const int* __restrict__ xofs,
+                                                    const short2* __restrict__ xalpha, const int2* __restrict__ yrows,
+                                                    const short2* __restrict__ ybeta,
+                                                    const PyrTile* __restrict__ tiles, int ntiles) {
+    extern __shared__ uint32_t s_src[];   // tl.nsr rows x tl.nsw dwords
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    if (tile >= ntiles) return;
+    const PyrTile tl = tiles[tile];
+    (void)dst_ph;
+    pyr_tile<TH, false>(pyr + (size_t)blockIdx.y * img_bytes, img_bytes, src_off, src_pitch, dst_off, dst_pitch, w, h,
+                        xofs, xalpha, yrows, ybeta, tl, s_src);
+}
+
+// The whole pyramid (the level-0 copy and every resize, ORBextractor.cc:1107-1132) as ONE launch
+// of dependent tasks instead of a launch per level: tasks are numbered level by level (image-major
+// inside a level), so every task a task waits for has a lower number and was dispatched before it
+// (in-order dispatch per XCD: no wait can block its own producers).  Level 0: a band of th padded
+// rows of one image; level l >= 1: one k_pyr_resize tile.  A level-l tile first waits for the
+// bands of level l-1 that hold its source rows: one band counter per (image, level, band) counts
+// its finished tasks (ncol per band; epoch * ncol once this call's are all in).  Hand-off
+// (cdna_hip_programming.md §6 Guideline 16, R1): the rows are stored write-through (sc1), every
+// wave drains its stores, the workgroup meets at a barrier, one lane adds to the band counter
+// (agent scope); the consumer polls relaxed from one lane, then ONE agent-scope acquire (this
+// CU's L1) before its plain staging loads.  Row pitches are multiples of 128 B and levels start
+// on 256-B boundaries, so no cache line holds bytes of two rows: a line is never fetched before
+// its row is complete.  Same per-pixel arithmetic (pyr_l0_chunk, pyr_tile): identical levels.
+typedef __attribute__((address_space(1))) int g_i32;
+__device__ __forceinline__ void flow_publish(int* cnt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its sc1 stores done
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add((g_i32*)cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one lane: spin (bounded) until *cnt >= need; false on timeout
+__device__ __forceinline__ bool flow_wait(int* cnt, int need) {
+    for (int spins = 0; __hip_atomic_load((g_i32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need; spins++) {
+        if (spins > (1 << 22)) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
+template <int TH>
+__global__ void __launch_bounds__(256) k_pyr_flow(const uint8_t* __restrict__ src, size_t src_stride, int step, int W,
+                                                  int H, uint8_t* __restrict__ pyr, size_t img_bytes, const FlowArgs A,
+                                                  const PyrTile* __restrict__ tiles, const uint8_t* __restrict__ tabs,
+                                                  int* __restrict__ cnt, int epoch, int* __restrict__ zero0,
+                                                  int* __restrict__ err) {
+    extern __shared__ uint32_t s_src[];
+    const int t = blockIdx.x;
+    int l = 0;
+    while (l + 1 < A.nl && t >= A.L[l + 1].task0) l++;
+    const FlowLevel& D = A.L[l];
+    const int rel = t - D.task0, b = rel / D.ntiles, k = rel - b * D.ntiles;
+    uint8_t* base = pyr + (size_t)b * img_bytes;
+    int* cb = cnt + (size_t)b * A.nbands;
+    if (l == 0) {
+        // the call's counters, as k_pyr_level0 clears them (task 0 is dispatched first)
+        if (t == 0 && threadIdx.x == 0) {
+            *zero0 = 0;
+            *err = 0;
+        }
+        const __amdgpu_buffer_rsrc_t rs = slab_rsrc(base, img_bytes);
+        const int py0 = k * D.th, nr = min(D.th, D.ph - py0), chunks = D.pitch >> 4;
+        const uint8_t* sb = src + (size_t)b * src_stride;
+        for (int q = threadIdx.x; q < nr * chunks; q += 256) {
+            const int r = q / chunks, py = py0 + r, px0 = (q - r * chunks) * 16;
+            const uint4 o = pyr_l0_chunk(sb, step, W, H, py, px0);
+            const u32x4v v = {o.x, o.y, o.z, o.w};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(D.off + (size_t)py * D.pitch + px0), 0, 16);
+        }
+        flow_publish(cb + D.band0 + k);
+        return;
+    }
+    const PyrTile tl = tiles[D.tile0 + k];
+    const FlowLevel& S = A.L[l - 1];
+    if (threadIdx.x == 0) {
+        const int r0 = kEdge + tl.sr0, r1 = kEdge + tl.sr0 + tl.nsr - 1;
+        bool ok = true;
+        for (int kb = r0 / S.th; kb <= r1 / S.th && ok; kb++) ok = flow_wait(cb + S.band0 + kb, epoch * S.ncol);
+        if (!ok) atomicOr(err, 4);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    pyr_tile<TH, true>(base, img_bytes, S.off, S.pitch, D.off, D.pitch, D.w, D.h,
+                       reinterpret_cast<const int*>(tabs + D.xofs), reinterpret_cast<const short2*>(tabs + D.xal),
+                       reinterpret_cast<const int2*>(tabs + D.yr), reinterpret_cast<const short2*>(tabs + D.yb), tl,
+                       s_src);
+    flow_publish(cb + D.band0 + tl.py0 / D.th);
 }
 
 // The small pyramid levels [la, nlevels) in ONE launch (the tail of the chain of resizes,
@@ -935,7 +1042,8 @@ void Extractor::release() {
     F(d_in_); F(d_pyr_); F(d_blur_); F(d_slots_); F(d_counts_); F(d_cells_); F(d_tiles_); F(d_work_); F(d_groups_);
     F(d_lcb_); F(d_packed_); F(d_hdr_); F(d_sel_); F(d_levels_); F(d_tabs_);
     F(d_kps_); F(d_desc_); F(d_jobsel_); F(d_jobcnt_); F(d_octlv_); F(d_gscr_); F(d_nout_); F(d_ptiles_);
-    F(d_chain_); F(d_cellslot_);
+    F(d_chain_); F(d_cellslot_); F(d_flowcnt_);
+    d_flowcnt_ = nullptr;
     d_ptiles_ = nullptr;
     d_chain_ = nullptr;
     d_cellslot_ = nullptr;
@@ -980,6 +1088,12 @@ int Extractor::init_device(int maxW, int maxH, int maxBatch) {
     const char* ef = getenv("ORBGPU_FAST_SPLIT");
     const bool blurSide = eb && atoi(eb) > 0;
     fastSplit_ = ef && atoi(ef) == 1 && !blurSide;
+    // opt-in (ORBGPU_PYR_FLOW=1): the whole pyramid as one launch of dependent tasks; slower than
+    // the launch per level alone (0.264 vs 0.239 ms at 128 images) and far slower in the pipeline
+    // (37.4 k vs 43.7 k frames/s: its waiting workgroups hold CU slots the tracking lane needs),
+    // profiles/r06fp_pyr_flow_ab.txt
+    const char* ew = getenv("ORBGPU_PYR_FLOW");
+    flow_ = ew && ew[0] == '1';
     if (blurSide || fastSplit_) ORB_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
     if (blurSide) ORB_HIP_CHECK(hipEventCreateWithFlags(&evBlur_, hipEventDisableTiming));
     if (fastSplit_) {
@@ -1243,6 +1357,39 @@ int Extractor::plan_chain(const std::vector<std::vector<int>>& yr) {
 }
 
 // Geometry of the pyramid / cells / resize tables for an image size.
+// k_pyr_flow's per-level task table for a batch of B images (tile-height variant v)
+FlowArgs Extractor::flow_args(int v, int B) const {
+    FlowArgs A{};
+    A.nl = nlevels_;
+    int task = 0, band = 0;
+    for (int l = 0; l < nlevels_; l++) {
+        const LevelHost& L = levels_[l];
+        FlowLevel& F = A.L[l];
+        F.off = (long long)L.off;
+        F.pitch = L.pitch;
+        F.ph = L.ph;
+        F.w = L.w;
+        F.h = L.h;
+        F.th = ptile_th_[v * nlevels_ + l];
+        const int nb = (L.ph + F.th - 1) / F.th;
+        F.ncol = l == 0 ? 1 : (L.pitch + PT_W - 1) / PT_W;
+        F.ntiles = l == 0 ? nb : ptile_n_[v * nlevels_ + l];
+        F.tile0 = l == 0 ? 0 : ptile_begin_[v * (nlevels_ + 1) + l];
+        F.band0 = band;
+        F.task0 = task;
+        if (l > 0) {
+            F.xofs = (int)tab_off_[l][0];
+            F.xal = (int)tab_off_[l][1];
+            F.yr = (int)tab_off_[l][2];
+            F.yb = (int)tab_off_[l][3];
+        }
+        band += nb;
+        task += B * F.ntiles;
+    }
+    A.nbands = band;
+    return A;
+}
+
 int Extractor::setup_geometry(int W, int H) {
     if (W == geomW_ && H == geomH_) return 0;
     if (W > 4000 || H > 4000) return -1;
@@ -1255,7 +1402,8 @@ int Extractor::setup_geometry(int W, int H) {
         if (L.w < 1 || L.h < 1) return -1;
         L.pw = L.w + 2 * kEdge;
         L.ph = L.h + 2 * kEdge;
-        L.pitch = align_up(L.pw, 16);
+        // k_pyr_flow: 128-B rows, so a cache line never holds bytes of two rows (its row hand-off)
+        L.pitch = align_up(L.pw, flow_ ? 128 : 16);
         L.off = off;
         off += (size_t)L.pitch * L.ph;
         off = (off + 255) & ~(size_t)255;
@@ -1395,6 +1543,7 @@ int Extractor::setup_geometry(int W, int H) {
     ptile_begin_.assign(2 * (nlevels_ + 1), 0);   // variant v, level l: ptile_n_ tiles from here
     ptile_n_.assign(2 * nlevels_, 0);
     plds_.assign(2 * nlevels_, 0);
+    ptile_th_.assign(2 * nlevels_, 0);
     for (int l = 1; l < nlevels_; l++) {
         const int sw = levels_[l - 1].w, sh = levels_[l - 1].h, dw = levels_[l].w, dh = levels_[l].h;
         const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
@@ -1477,6 +1626,7 @@ int Extractor::setup_geometry(int W, int H) {
                     ptiles_.push_back(t);
                 }
             plds_[v * nlevels_ + l] = (int)lds;
+            ptile_th_[v * nlevels_ + l] = nrow;
             ptile_n_[v * nlevels_ + l] = (int)ptiles_.size() - ptile_begin_[v * (nlevels_ + 1) + l];
           }
         }
@@ -1505,6 +1655,20 @@ int Extractor::setup_geometry(int W, int H) {
     ORB_HIP_CHECK(hipMalloc(&d_ptiles_, std::max<size_t>(ptiles_.size(), 1) * sizeof(PyrTile)));
     if (!ptiles_.empty())
         ORB_HIP_CHECK(hipMemcpy(d_ptiles_, ptiles_.data(), ptiles_.size() * sizeof(PyrTile), hipMemcpyHostToDevice));
+    // k_pyr_flow: band counters (level 0 in bands of the variant's tile height)
+    if (d_flowcnt_) (void)hipFree(d_flowcnt_);
+    d_flowcnt_ = nullptr;
+    for (int v = 0; v < 2; v++) {
+        ptile_th_[v * nlevels_] = kPyrTileH[v];
+        int nb = 0, lds = 0;
+        for (int l = 0; l < nlevels_; l++) {
+            nb += (levels_[l].ph + ptile_th_[v * nlevels_ + l] - 1) / ptile_th_[v * nlevels_ + l];
+            lds = std::max(lds, plds_[v * nlevels_ + l]);
+        }
+        flowBands_[v] = nb;
+        flowLds_[v] = lds;
+    }
+    ORB_HIP_CHECK(hipMalloc(&d_flowcnt_, (size_t)std::max(flowBands_[0], flowBands_[1]) * B * 4));
     ORB_HIP_CHECK(hipMalloc(&d_pyr_, img_bytes_ * B));
     ORB_HIP_CHECK(hipMalloc(&d_blur_, blur_bytes_ * B));
     ORB_HIP_CHECK(hipMemset(d_blur_, 0, blur_bytes_ * B));
@@ -1620,9 +1784,23 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
     {
         const LevelHost& L0 = levels_[0];
         const int n = (L0.pitch / 16) * L0.ph;
-        hipLaunchKernelGGL(k_pyr_level0, dim3((n + 255) / 256, B), dim3(256), 0, s, src, img_stride, step, W, H,
-                           (uint8_t*)d_pyr_, img_bytes_, L0.pitch, L0.ph, d_gtotal_, (int*)d_nout_ + B);
-        const int lend = chain_ && !split ? chainFrom_ : nlevels_;   // levels [1, lend) one launch each
+        const bool flow = flow_ && !split && !chain_;
+        if (flow) {
+            // every level in one launch (k_pyr_flow); its band counters zeroed first
+            const int v = B >= 8 ? 1 : 0;
+            ORB_HIP_CHECK(hipMemsetAsync(d_flowcnt_, 0, (size_t)flowBands_[v] * B * 4, s));
+            const FlowArgs A = flow_args(v, B);
+            int tasks = 0;
+            for (int l = 0; l < nlevels_; l++) tasks += B * A.L[l].ntiles;
+            auto kern = v ? k_pyr_flow<kPyrTileH[1]> : k_pyr_flow<kPyrTileH[0]>;
+            hipLaunchKernelGGL(kern, dim3(tasks), dim3(256), flowLds_[v], s, src, img_stride, step, W, H,
+                               (uint8_t*)d_pyr_, img_bytes_, A, (const PyrTile*)d_ptiles_, (const uint8_t*)d_tabs_,
+                               d_flowcnt_, 1, d_gtotal_, (int*)d_nout_ + B);
+        } else {
+            hipLaunchKernelGGL(k_pyr_level0, dim3((n + 255) / 256, B), dim3(256), 0, s, src, img_stride, step, W, H,
+                               (uint8_t*)d_pyr_, img_bytes_, L0.pitch, L0.ph, d_gtotal_, (int*)d_nout_ + B);
+        }
+        const int lend = flow ? 1 : chain_ && !split ? chainFrom_ : nlevels_;   // levels [1, lend) one launch each
         for (int l = 1; l < lend; l++) {
             if (split && l == kFastSplitLevel) {
                 ORB_HIP_CHECK(hipEventRecord(evPyrA_, s));
@@ -1644,7 +1822,7 @@ int Extractor::extract(const uint8_t* imgs, int B, int W, int H, int step, size_
                                (const int2*)(T + tab_off_[l][2]), (const short2*)(T + tab_off_[l][3]),
                                (const PyrTile*)d_ptiles_ + ptile_begin_[pb], nt);
         }
-        if (lend < nlevels_) {
+        if (!flow && lend < nlevels_) {
             const uint8_t* T = (const uint8_t*)d_chain_;
             const LevelHost& P = levels_[lend - 1];
             hipLaunchKernelGGL(k_pyr_chain, dim3(chainK_, B), dim3(256), chainLds_, s, (uint8_t*)d_pyr_, img_bytes_,

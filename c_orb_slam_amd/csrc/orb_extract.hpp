@@ -61,6 +61,21 @@ struct ChainLevel {
 };
 constexpr int kChainLdsMax = 64 * 1024;
 
+// k_pyr_flow: the pyramid as one launch of dependent tasks; per level its padded geometry, its
+// tasks and band counters, and (levels >= 1) its resize tables as byte offsets into d_tabs_
+struct FlowLevel {
+    long long off;          // padded level in the image slab
+    int pitch, ph, w, h;
+    int task0, ntiles;      // first task of the level (image 0); tasks per image
+    int tile0;              // levels >= 1: the level's first PyrTile
+    int band0, th, ncol;    // band counters: first slot, padded rows per band, tasks per band
+    int xofs, xal, yr, yb;
+};
+struct FlowArgs {
+    FlowLevel L[16];
+    int nl, nbands;         // levels; band counters per image
+};
+
 struct LevelDev {
     long long off, boff;
     int pitch, bpitch;
@@ -131,6 +146,13 @@ private:
     std::vector<BlurTile> tiles_;
     std::vector<PyrTile> ptiles_;
     std::vector<int> ptile_begin_, ptile_n_, plds_;   // per tile-height variant and level
+    std::vector<int> ptile_th_;                       // rows per tile (band), per variant and level
+    // k_pyr_flow (opt-in, ORBGPU_PYR_FLOW=1; default: a launch per level): band counters for
+    // maxB_ images (zeroed before every launch) and the flow's dynamic LDS, per variant
+    bool flow_ = false;
+    int* d_flowcnt_ = nullptr;
+    int flowBands_[2] = {0, 0}, flowLds_[2] = {0, 0};
+    FlowArgs flow_args(int v, int B) const;
     // the chained pyramid (plan_chain): strips per image, dynamic LDS, device tables
     // [ChainLevel x (nlevels-1) | int4 strip ranges x K x (nlevels-1) | u16 padded rows]
     int plan_chain(const std::vector<std::vector<int>>& yr);

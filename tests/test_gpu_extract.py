@@ -167,3 +167,26 @@ def test_extract_octree_regimes(gpu, kind, nf):
     assert len(gk) == len(ok) and np.array_equal(gk.view(np.uint8), ok.view(np.uint8)), _diag(gk, gd, ok, od)
     if len(ok):
         assert np.array_equal(gd, od)
+
+
+@pytest.mark.parametrize("B", [3, 12])
+def test_pyramid_flow_alternating_batches(gpu, B):
+    """k_pyr_flow hands pyramid rows between workgroups of one launch: alternate two different
+    batches (and a smaller one) through one extractor, so a row read before its producer finished
+    would show the previous call's bytes; every padded level of every image byte-exact.  B = 3 and
+    12 take the two tile-height variants (16 / 32 rows)."""
+    frames, _ = synthetic.sequence(21, 2 * B, 1241, 376)
+    sets = [frames[:B], frames[B:], frames[:B][::-1], frames[B:][: max(1, B // 2)]]
+    ex = gpu.ORBextractor(1200, 1.2, 8, 20, 7, max_width=1241, max_height=376, max_batch=B)
+    orc = oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7)
+    want = {}
+    for imgs in sets:
+        ex.extract_batch(np.ascontiguousarray(imgs))
+        for b, img in enumerate(imgs):
+            key = img.tobytes()[:4096] + bytes([b % 256])
+            if key not in want:
+                orc(img)
+                want[key] = [orc.level(l).copy() for l in range(8)]
+            for l in range(8):
+                gl = ex.image_pyramid_level(l, b)
+                assert np.array_equal(gl, want[key][l]), f"image {b} level {l} differs at {np.argwhere(gl != want[key][l])[:5]}"
