@@ -593,17 +593,14 @@ __device__ __forceinline__ void land_reduce_thread(const BaStructDev& s, const d
     else bl[3 * l + (q - 9)] = v;
 }
 
-// Threads entry-major: thread g takes entry q = g / nL of landmark l = g mod nL, so neighbouring
-// threads read one SoA column at neighbouring landmarks' edges (a landmark's active edges are
-// consecutive in edge order: coalesced), not twelve columns of one landmark (twelve lines per
-// wave load).  The same values as land_reduce_thread's landmark-major order.
+// Threads landmark-major (thread g: entry g mod 12 of landmark g / 12).  Measured against the
+// entry-major mapping (one SoA column over neighbouring landmarks per wave load): 178 vs 232 us
+// per config-5 launch (gpurun_out r06o2 / r06t), the twelve columns of a landmark's few edges
+// share their lines in L2.
 __global__ void __launch_bounds__(256) k_land_reduce(BaStructDev s, const double* __restrict__ terms, double* Hll,
                                                      double* bl, const int* run) {
     BA_GATE(run);
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= 12 * s.nL) return;
-    const int q = g / s.nL, l = g - q * s.nL;
-    land_reduce_thread(s, terms, Hll, bl, 12 * l + q);
+    land_reduce_thread(s, terms, Hll, bl, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // both reductions of buildSystem in one launch: blocks [0, nP) reduce a pose each, the rest
@@ -3772,7 +3769,7 @@ int BaEngine::join_sp_build() {
 // The pose graph of the Schur pattern's off-diagonal blocks (keys i1 * nP + i2, i1 < i2; any order,
 // duplicates allowed) as sorted adjacency lists: as[i] .. as[i + 1] of adj
 static void pose_graph_csr(int nP, std::vector<int64_t>& all, std::vector<int>* asOut, std::vector<int>* adjOut) {
-    std::sort(all.begin(), all.end());
+    if (!std::is_sorted(all.begin(), all.end())) std::sort(all.begin(), all.end());   // (the device list is)
     all.erase(std::unique(all.begin(), all.end()), all.end());
     std::vector<int> deg(nP + 1, 0);
     std::vector<int>& as = *asOut;
@@ -3784,12 +3781,18 @@ static void pose_graph_csr(int nP, std::vector<int64_t>& all, std::vector<int>* 
         deg[q % nP]++;
     }
     for (int i = 0; i < nP; i++) as[i + 1] = as[i] + deg[i];
+    // keys (i1, i2) ascending, i1 < i2: row i gets its smaller neighbours (from the keys (i1, i),
+    // i1 ascending) before its larger ones (keys (i, i2), i2 ascending), so every list comes out
+    // sorted without a per-row sort
     std::vector<int> fillp(as.begin(), as.end() - 1);
-    for (int64_t q : all) {   // (i1, i2) ascending: every list comes out sorted
-        adj[fillp[q / nP]++] = (int)(q % nP);
+    bool upper = true;
+    for (int64_t q : all) {
+        adj[fillp[q % nP]++] = (int)(q / nP);
+        upper = upper && q / nP < q % nP;
     }
-    for (int64_t q : all) adj[fillp[q % nP]++] = (int)(q / nP);
-    for (int i = 0; i < nP; i++) std::sort(adj.begin() + as[i], adj.begin() + as[i + 1]);
+    for (int64_t q : all) adj[fillp[q / nP]++] = (int)(q % nP);
+    if (!upper)   // (keys below the diagonal: not the order above)
+        for (int i = 0; i < nP; i++) std::sort(adj.begin() + as[i], adj.begin() + as[i + 1]);
 }
 
 int BaEngine::build_structure(int level) {
@@ -4205,12 +4208,17 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
     // n <= 128: register-resident single-workgroup LDL^T; S fits LDS: single-workgroup in LDS;
     // larger: block-sparse tiled LDL^T in HBM (ldlt.hip, structure from build_structure)
     if (!tiled_ && n > 0 && !use_reg && !in_lds) return -1;
-    if (int e = join_sp_build()) return e;   // the block structure, built beside the first linearisation
-    const SysAddr sa = tiled_ ? sp_.addr() : SysAddr{dS_, n, nullptr, nullptr, 0, nullptr};
+    SysAddr sa{dS_, n, nullptr, nullptr, 0, nullptr};
+    bool joined = false;
     do {
         // setLambda + BlockSolver::solve
         if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_,
                                    lambda_, use_dev, dScal_, dEmat_, dCb_, nullptr);
+        if (!joined) {   // the block structure, built beside the first linearisation and point prep
+            if (int e = join_sp_build()) return e;
+            if (tiled_) sa = sp_.addr();
+            joined = true;
+        }
         // the in-place LDL^T overwrites S (fill-in, L), and a shard's S holds the previous
         // trial's all-reduced blocks outside its own pattern: clear S
         if (tiled_) {
