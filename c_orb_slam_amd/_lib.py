@@ -129,6 +129,7 @@ def lib():
     L.ORBextractor_get_levels.argtypes = [vp, P(i32), P(f32)]
     L.ORBextractor_get_scale_tables.argtypes = [vp, vp, vp, vp, vp, vp]
     L.ORBextractor_reserve_cus.argtypes = [vp, i32]
+    L.ORBextractor_share_stream.argtypes = [vp, vp]
     L.ORBextractor_stream.restype = vp
     L.ORBextractor_stream.argtypes = [vp]
     L.ORBextractor_last_timings.argtypes = [vp, vp]
@@ -190,6 +191,7 @@ def lib():
     L.Optimizer_partition_points.argtypes = [vp, i32, vp]
     L.Optimizer_partition_points_nd.argtypes = [vp, i32, vp, vp]
     L.Optimizer_last_sharding.argtypes = [vp]
+    L.Optimizer_last_lm_path.argtypes = [vp]
     L.orbgpu_comm_unique_id.argtypes = [vp]
     L.orbgpu_comm_init_rccl.argtypes = [i32, i32, vp, P(vp)]
     L.orbgpu_comm_init_local.argtypes = [i32, vp]

@@ -1862,6 +1862,8 @@ __global__ void __launch_bounds__(1024) k_csum(CsumList L0, CsumList L1, const i
 // the decisions it has seen; k_lm_trial_end sets the gates of the next step.
 // Host-pinned coherent words (LmHost): [0] stop flag mirror (host writes), [1] done, [2] steps
 // decided, [3] iterations, [4..5] (done, steps) as one 8-byte word the host polls (device writes).
+// host words [kLmHostDone + s]: done after step s (s < kLmHostSteps >= the step bound 10 x iterations)
+constexpr int kLmHostDone = 16, kLmHostSteps = kLmTrials + 8;
 __global__ void __launch_bounds__(64) k_lm_begin(LmDev* L, int iterations) {
     if (threadIdx.x != 0) return;
     L->ctl[0] = 1;
@@ -1992,6 +1994,13 @@ __device__ int lm_decide(LmDev* Lg, LmHead L, double* scal, volatile int* host, 
     host[3] = L.it;
     host[2] = L.steps;
     host[1] = L.done;
+    // done after step `steps` - 1, per step: what every rank of a sharded run decides its next
+    // enqueue on (the latest (done, steps) pair may already include a later step), written ahead
+    // of the pair the host polls
+    if (L.steps <= kLmHostSteps) {
+        host[kLmHostDone + L.steps - 1] = L.done;
+        __threadfence_system();
+    }
     // the pair (done, steps) as one aligned 8-byte store: the host's poll sees both or neither
     *(volatile unsigned long long*)(host + 4) = ((unsigned long long)(unsigned)L.steps << 32) | (unsigned)L.done;
     return pop;
@@ -2013,7 +2022,8 @@ struct ChiFuse {
 __global__ void __launch_bounds__(kTeThreads) k_lm_trial_end(LmDev* L, double* scal, volatile int* host, BaStructDev s,
                                                        Se3* T, const Se3* Tbak, double* X, const double* Xbak,
                                                        const double* x, const double* bp, const double* bl, int scale,
-                                                       ChiFuse cf, const Se3* Tn, const double* Xn) {
+                                                       ChiFuse cf, const Se3* Tn, const double* Xn,
+                                                       const double* stopDev) {
     __shared__ double lv[2048];
     __shared__ double cA[kChiFuseMax], cB[kChiFuseMax];
     __shared__ double tot[3];   // the fused chi2 totals (system, trial) and the scale sum
@@ -2031,7 +2041,8 @@ __global__ void __launch_bounds__(kTeThreads) k_lm_trial_end(LmDev* L, double* s
     double g0 = 0, g1 = 0, g2 = 0, g3 = 0;
     if (threadIdx.x == 0) {
         lm_load(L, H);
-        stop = host[0] != 0;
+        // a sharded run's stop flag is the ranks' all-reduced one (every rank decides alike)
+        stop = stopDev ? stopDev[0] != 0.0 : host[0] != 0;
         g0 = scal[0];
         g1 = scal[1];
         g2 = scal[2];
@@ -3368,6 +3379,7 @@ BaEngine::~BaEngine() {
     if (dPack_) (void)hipFree(dPack_);
     if (arena_) (void)hipFree(arena_);
     if (dStruct_) (void)hipFree(dStruct_);
+    if (dLmStage_) (void)hipFree(dLmStage_);
     if (hScal_) (void)hipHostFree(hScal_);
     if (hLm_) (void)hipHostFree(hLm_);
     for (auto ev : lmEv_)
@@ -3465,8 +3477,8 @@ int BaEngine::init() {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     ORB_HIP_CHECK(hipHostMalloc((void**)&hScal_, 64 * sizeof(double)));
-    ORB_HIP_CHECK(hipHostMalloc((void**)&hLm_, 16 * sizeof(int), hipHostMallocCoherent));
-    std::memset((void*)hLm_, 0, 16 * sizeof(int));   // [8]: poll_stream's sequence word
+    ORB_HIP_CHECK(hipHostMalloc((void**)&hLm_, (kLmHostDone + kLmHostSteps) * sizeof(int), hipHostMallocCoherent));
+    std::memset((void*)hLm_, 0, (kLmHostDone + kLmHostSteps) * sizeof(int));   // [8]: poll_stream's sequence word
     for (auto& ev : lmEv_) ORB_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     int dev = 0;
     ORB_HIP_CHECK(hipGetDevice(&dev));
@@ -4271,6 +4283,8 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
         if (nE) {
             hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
             hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+        } else if (comm_ && qmax > 0) {   // a rank without edges: its trial chi2 is 0 (the last trial's
+            ORB_HIP_CHECK(hipMemsetAsync(dScal_ + 1, 0, sizeof(double), s));   // all-reduced total otherwise)
         }
         if (scale_small(nP, nL)) {
             hipLaunchKernelGGL(k_scale, dim3(1), dim3(1024), 0, s, nP, nL, dX2_, dBp_, dBl_, lambda_, use_dev, dScal_,
@@ -4322,6 +4336,7 @@ int BaEngine::lm_solve(int iteration, const volatile bool* stop, bool* terminate
                                             dXbak_, nullptr);
         }
         qmax++;
+        last_lm[1]++;
         trace_.trial_chi2.push_back(tempChi);
         trace_.trial_lambda.push_back(lambda_);
     } while (rho < 0 && qmax < 10 && !stopped(stop));
@@ -4386,9 +4401,13 @@ static bool fused_prep() {
 // A one-rank group has no exchange (every all-reduce is the identity), so its sharded call is the
 // unsharded call and takes the same device LM.  With more ranks the trial's all-reduces sit
 // between the device steps: the host loop keeps them in order.
+// Sharded runs too (enqueue_lm_step_comm): the exchanges are stream-ordered calls between the
+// step's kernels, so no rank reads a trial's result back.  The block-sparse (tiled) solver keeps
+// the host loop: its ~100 launches per solve take no gate, so a step queued after the run ended
+// would factor once more.
 bool BaEngine::device_lm(int iterations) const {
-    return (!comm_ || comm_->size() == 1) && !tiled_ && iterations > 0 && (size_t)iterations * 10 <= (size_t)kLmTrials &&
-           !lm_host_forced() && dense_solver(6 * st_.nP);
+    return !tiled_ && iterations > 0 && (size_t)iterations * 10 <= (size_t)kLmTrials && !lm_host_forced() &&
+           dense_solver(6 * st_.nP);
 }
 
 // the kernels of one LM step: [system: linearize, reduce, lambda init] [trial ... decide, pop]
@@ -4472,7 +4491,132 @@ void BaEngine::enqueue_lm_step(bool first) {
     hipLaunchKernelGGL(k_lm_trial_end, dim3(1), dim3(kTeThreads), 0, s, dLm_, dScal_, (volatile int*)hLm_, S, dT_, dTbak_,
                        dX_, dXbak_, dX2_, dBp_, dBl_, small ? 1 : 0,
                        fuse ? ChiFuse{tmpB0_, tmpB1_, nE} : ChiFuse{nullptr, nullptr, 0}, fuse ? dTn_ : nullptr,
-                       fuse ? dXn_ : nullptr);
+                       fuse ? dXn_ : nullptr, (const double*)nullptr);
+}
+
+// the system's all-reduce staging of enqueue_lm_step_comm: dir 0 [Hpp | b_p | chi2] -> stage, dir 1
+// back (gated by the system flag: on a trial of the same system the exchange still runs, on
+// whatever the staging holds, and nothing is copied back)
+__global__ void __launch_bounds__(256) k_lm_stage(int nP, double* Hpp, double* bp, double* scal, double* stage, int dir,
+                                                  const int* run) {
+    BA_GATE(run);
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, n1 = 21 * nP, n2 = 27 * nP;
+    if (i > n2) return;
+    double* p = i < n1 ? Hpp + i : i < n2 ? bp + (i - n1) : scal;
+    if (dir == 0) stage[i] = *p;
+    else *p = stage[i];
+}
+// the host's stop flag (the word the host mirrors) as a double for the ranks' all-reduce
+__global__ void k_lm_stop_in(const volatile int* host, double* dst) {
+    if (threadIdx.x == 0) *dst = host[0] != 0 ? 1.0 : 0.0;
+}
+// a rank without edges: zero chi2 partial (gated like the linearisation it replaces)
+__global__ void k_lm_zero_chi(double* scal, const int* run) {
+    BA_GATE(run);
+    if (threadIdx.x == 0) scal[0] = 0.0;
+}
+
+// One LM step of a rank of a sharded run (dense reduced system): lm_solve's kernels for one
+// trial -- the system part (linearisation, reductions and their all-reduce) gated by ctl[1], the
+// trial part by ctl[0] -- with the exchanges in the same places and the decision made on the
+// device by k_lm_trial_end from the all-reduced scalars (chi2s, scale, stop).  The all-reduces
+// cannot be gated: every rank enqueues the same steps (optimize_device), a gated step exchanges
+// scratch that nothing reads afterwards.  Same kernels, arguments and exchanges as lm_solve: the
+// same bits.
+int BaEngine::enqueue_lm_step_comm(bool first) {
+    hipStream_t s = stream_;
+    const BaStructDev& S = st_;
+    const int nE = S.nE, nP = S.nP, nL = S.nL;
+    const int* ctl = dLm_->ctl;
+    const bool own = comm_->rank() == 0;
+    LinArgs la{S, dE_, dT_, dX_, dRobust_, dErr_, dRc_, dTerms_, dHplA_, 1, tmpA0_, dCounter_, dScal_ + 0, ctl + 1};
+    // system (a new iteration): chi2, Hpp, b_p, then their all-reduce through the staging
+    if (!nE) hipLaunchKernelGGL(k_lm_zero_chi, dim3(1), dim3(64), 0, s, dScal_, ctl + 1);
+    if (nE) {
+        hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+        hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+    }
+    if (nP) hipLaunchKernelGGL(k_pose_reduce, dim3(nP), dim3(kSysThreads), 0, s, S, dTerms_, dHpp_, dBp_, ctl + 1);
+    if (nL) hipLaunchKernelGGL(k_land_reduce, dim3(nblk(12 * nL, 256)), dim3(256), 0, s, S, dTerms_, dHll_, dBl_, ctl + 1);
+    const size_t ns = 27 * (size_t)nP + 1;
+    if (ns > lmStageCap_) {
+        if (dLmStage_) (void)hipFree(dLmStage_);
+        dLmStage_ = nullptr;
+        lmStageCap_ = 0;
+        ORB_HIP_CHECK(hipMalloc(&dLmStage_, sizeof(double) * ns));
+        ORB_HIP_CHECK(hipMemsetAsync(dLmStage_, 0, sizeof(double) * ns, s));
+        lmStageCap_ = ns;
+    }
+    hipLaunchKernelGGL(k_lm_stage, dim3(nblk((int)ns, 256)), dim3(256), 0, s, nP, dHpp_, dBp_, dScal_, dLmStage_, 0, ctl + 1);
+    ORB_HIP_CHECK(hipGetLastError());
+    if (int e = comm_->allreduce(dLmStage_, ns, RedOp::Sum, s)) return e;
+    hipLaunchKernelGGL(k_lm_stage, dim3(nblk((int)ns, 256)), dim3(256), 0, s, nP, dHpp_, dBp_, dScal_, dLmStage_, 1, ctl + 1);
+    if (first) {   // computeLambdaInit, the maximum over the ranks (the first step is always live)
+        hipLaunchKernelGGL(k_lambda_init, dim3(1), dim3(1024), 0, s, nP, nL, dHpp_, dHll_, dScal_, ctl + 2);
+        ORB_HIP_CHECK(hipGetLastError());
+        if (int e = comm_->allreduce(dScal_ + 4, 2, RedOp::Max, s)) return e;
+    }
+    // trial
+    const int n = 6 * nP;
+    const size_t ldsBytes = sizeof(double) * ((size_t)n + (size_t)n * n);
+    const int in_lds = ldsBytes <= ldsMax_ ? 1 : 0;
+    const size_t shm = in_lds ? ldsBytes : sizeof(double) * (size_t)n;
+    const size_t regShm = ldlt_reg_shm(n);
+    const bool use_reg = n < kLdltMax && regShm <= ldsMax_;
+    const DenseLdlt kind = dense_ldlt_kind(n, use_reg);
+    const SysAddr sa{dS_, n, nullptr, nullptr, 0, nullptr};
+    if (nE) hipLaunchKernelGGL(k_point_prep, dim3(nblk(nE, 256)), dim3(256), 0, s, S, dHll_, dBl_, dHplA_, 0.0, 1, dScal_,
+                               dEmat_, dCb_, ctl);
+    if (n) ORB_HIP_CHECK(hipMemsetAsync(dS_, 0, sizeof(double) * (size_t)n * n, s));
+    if (S.nBlk) schur_launch(S.nBlk, blkChunks_, s, S, dEmat_, dHplA_, dCb_, dHpp_, dBp_, 0.0, 1, dScal_, sa, dBs_,
+                             own ? 1 : 0, (const uint8_t*)nullptr, ctl);
+    if (nTiles_) {   // the union-pattern tiles of S and b_s, packed
+        hipLaunchKernelGGL(k_tile_pack, dim3(nTiles_), dim3(256), 0, s, n, dS_, dTiles_, dPackBuf_);
+        double* pb = dPackBuf_ + (size_t)nTiles_ * 4096;
+        ORB_HIP_CHECK(hipMemcpyAsync(pb, dBs_, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+        ORB_HIP_CHECK(hipGetLastError());
+        if (int e = comm_->allreduce(dPackBuf_, (size_t)nTiles_ * 4096 + n, RedOp::Sum, s)) return e;
+        hipLaunchKernelGGL(k_tile_unpack, dim3(nTiles_), dim3(256), 0, s, n, dS_, dTiles_, dPackBuf_);
+        ORB_HIP_CHECK(hipMemcpyAsync(dBs_, pb, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    }
+    if (kind == DenseLdlt::Col) hipLaunchKernelGGL(k_ldlt_col, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else if (kind == DenseLdlt::T) hipLaunchKernelGGL(k_ldlt_t, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else if (kind == DenseLdlt::D2) hipLaunchKernelGGL(k_ldlt_2d, dim3(1), dim3(256), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else if (kind == DenseLdlt::Row) hipLaunchKernelGGL(k_ldlt_row, dim3(1), dim3(128), 0, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else if (kind == DenseLdlt::Reg) hipLaunchKernelGGL(k_ldlt_reg, dim3(1), dim3(kLdltThreads), regShm, s, n, dS_, dBs_, dX2_, dScal_, ctl);
+    else hipLaunchKernelGGL(k_ldlt, dim3(1), dim3(256), shm + 16, s, n, dS_, dBs_, dX2_, dScal_, in_lds, ctl);
+    if (nP + nL) hipLaunchKernelGGL(k_update, dim3(nblk(nP + nL, 256)), dim3(256), 0, s, S, dT_, dTbak_, dX_, dXbak_, dX2_,
+                                    dHplA_, dHll_, dBl_, 0.0, 1, dScal_, ctl);
+    la.linearize = 0;
+    la.out = dScal_ + 1;
+    la.run = ctl;
+    if (nE) {
+        hipLaunchKernelGGL(k_linearize, dim3(nblk(nE, 256)), dim3(256), 0, s, la);
+        hipLaunchKernelGGL(k_chi2_finish, dim3(1), dim3(256), 0, s, la);
+    } else {   // (lm_solve's memset of chi2 for a rank without edges, here per trial)
+        ORB_HIP_CHECK(hipMemsetAsync(dScal_ + 1, 0, sizeof(double), s));
+    }
+    if (scale_small(nP, nL)) {
+        hipLaunchKernelGGL(k_scale, dim3(1), dim3(1024), 0, s, nP, nL, dX2_, dBp_, dBl_, 0.0, 1, dScal_, dScal_ + 2,
+                           own ? 1 : 0, ctl);
+    } else {
+        const int nv = 6 * nP + 3 * nL;
+        hipLaunchKernelGGL(k_scale_chunks, dim3(nblk(nv, 256)), dim3(256), 0, s, nP, nL, dX2_, dBp_, dBl_, 0.0, 1,
+                           dScal_, tmpA0_, own ? 1 : 0, ctl);
+        CsumList L0{tmpA0_, (nv + 63) / 64, tmpA1_, tmpA0_, dScal_ + 2};
+        hipLaunchKernelGGL(k_csum, dim3(1), dim3(1024), 0, s, L0, L0, ctl);
+    }
+    hipLaunchKernelGGL(k_lm_stop_in, dim3(1), dim3(64), 0, s, (const volatile int*)hLm_, dScal_ + 6);
+    ORB_HIP_CHECK(hipGetLastError());
+    {
+        const RedBuf rb[2] = {{dScal_ + 1, 2}, {dScal_ + 6, 1}};
+        if (int e = comm_->allreduce(rb, 2, RedOp::Sum, s)) return e;
+    }
+    hipLaunchKernelGGL(k_lm_trial_end, dim3(1), dim3(kTeThreads), 0, s, dLm_, dScal_, (volatile int*)hLm_, S, dT_, dTbak_,
+                       dX_, dXbak_, dX2_, dBp_, dBl_, 0, ChiFuse{nullptr, nullptr, 0}, (const Se3*)nullptr,
+                       (const double*)nullptr, (const double*)(dScal_ + 6));
+    ORB_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* its) {
@@ -4501,15 +4645,20 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
     int nSteps = 0;
     for (int j = 0; j < maxSteps; j++) {
         const auto q0 = sclk::now();
-        enqueue_lm_step(j == 0);
+        if (comm_) {
+            if (int e = enqueue_lm_step_comm(j == 0)) return e;
+        } else {
+            enqueue_lm_step(j == 0);
+        }
         ORB_HIP_CHECK(hipGetLastError());
         const auto q1 = sclk::now();
         nSteps++;
+        last_lm[0]++;
         if (useEvents) {
             ORB_HIP_CHECK(hipEventRecord(lmEv_[j & 1], stream_));
             if (j >= 1) {
                 ORB_HIP_CHECK(hipEventSynchronize(lmEv_[(j - 1) & 1]));
-                if (hw[1]) break;
+                if (hw[kLmHostDone + j - 1]) break;
             }
         } else if (j >= 1) {
             // step j - 1 decided (steps >= j) or the run over.  No HIP call inside the wait: a
@@ -4526,7 +4675,10 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
                     break;
                 __builtin_ia32_pause();
             }
-            if ((*hw64 & 0xffffffffu) || hw[1]) {
+            // done after step j - 1 (not the latest pair: it may already hold step j's decision,
+            // which other ranks of a sharded run have not seen when they decide whether to queue
+            // step j + 1: every rank queues the same steps)
+            if (hw[kLmHostDone + j - 1]) {
                 tEnq += std::chrono::duration<double, std::micro>(q1 - q0).count();
                 tWait += std::chrono::duration<double, std::micro>(sclk::now() - q1).count();
                 break;
@@ -4592,6 +4744,8 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
     // made (no collective, no host round trip per structure and stop decision)
     comm_ = comm && comm->size() > 1 ? comm : nullptr;
     mode_ = mode ? *mode : BaMode{};
+    last_lm[0] = last_lm[1] = last_lm[3] = 0;
+    last_lm[2] = comm_ ? 1 : 0;
     stopRed_ = false;
     hsValid_ = false;     // hs_ holds this call's lists only after its first host build
     refineNext_ = false;

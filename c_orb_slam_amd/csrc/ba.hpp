@@ -63,6 +63,9 @@ public:
     double last_ms[4] = {0, 0, 0, 0};  // total, structure (host), solves (device+control), io
     // last run: sharded factorisation used, separator tiles and rows exchanged, Schur-pattern tiles
     int last_dist[4] = {0, 0, 0, 0};
+    // the last run's LM control: [0] steps the device-resident LM queued, [1] trials the host loop
+    // (lm_solve) decided after a readback, [2] 1 if sharded (Optimizer_last_lm_path)
+    int last_lm[4] = {0, 0, 0, 0};
 
 private:
     int upload_problem(const ba_problem* P);
@@ -73,6 +76,10 @@ private:
     bool device_lm(int iterations) const;
     int optimize_device(int iterations, const volatile bool* stop, int* its);
     void enqueue_lm_step(bool first);
+    // the same step for a rank of a sharded run: lm_solve's kernels and exchanges, gated
+    int enqueue_lm_step_comm(bool first);
+    double* dLmStage_ = nullptr;   // the system's all-reduce staging (Hpp, b_p, chi2) of enqueue_lm_step_comm
+    size_t lmStageCap_ = 0;
     int gate_edges(int final_check, uint8_t* erase);
     int carve(bool commit, size_t* total);
     bool stopped(const volatile bool* stop) const { return comm_ ? stopRed_ : (stop && *stop); }

@@ -495,6 +495,15 @@ int Optimizer_last_sharding(int* info4) {
     return ORB_OK;
 }
 
+int Optimizer_last_lm_path(int* info4) {
+    if (!info4) return ORB_E_INVALID;
+    int rc = 0;
+    orbgpu::BaEngine* e = engine(&rc);
+    if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    for (int i = 0; i < 4; i++) info4[i] = e->last_lm[i];
+    return ORB_OK;
+}
+
 int Optimizer_last_timings(double* ms2) {
     if (!ms2) return ORB_E_INVALID;
     int rc = 0;

@@ -117,6 +117,12 @@ void* ORBextractor_stream(ORBextractor_h h) { return h ? (void*)h->ex->stream() 
 int ORBextractor_reserve_cus(ORBextractor_h h, int one_in_n) {
     if (!h || one_in_n < 0 || one_in_n == 1) return ORB_E_INVALID;
     const int r = h->ex->reserve_cus(one_in_n);
+    return r == -4 ? ORB_E_NODEVICE : r == -1 ? ORB_E_INVALID : (r ? ORB_E_HIP : ORB_OK);
+}
+
+int ORBextractor_share_stream(ORBextractor_h h, ORBextractor_h with) {
+    if (!h || !with) return ORB_E_INVALID;
+    const int r = h->ex->share_stream(with->ex);
     return r == -4 ? ORB_E_NODEVICE : (r ? ORB_E_HIP : ORB_OK);
 }
 

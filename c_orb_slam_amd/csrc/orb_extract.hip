@@ -1060,7 +1060,7 @@ void Extractor::release() {
     h_in_cap_ = 0;
     for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
     for (auto& e : ev_) e = nullptr;
-    if (stream_) (void)hipStreamDestroy(stream_);
+    if (stream_ && ownStream_) (void)hipStreamDestroy(stream_);
     stream_ = nullptr;
     if (evBlur_) (void)hipEventDestroy(evBlur_);
     evBlur_ = nullptr;
@@ -1166,8 +1166,19 @@ int Extractor::build_work(int B) {
     return 0;
 }
 
+int Extractor::share_stream(Extractor* with) {
+    if (!stream_ || !with || !with->stream_) return -4;
+    if (with == this) return 0;
+    ORB_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (ownStream_) (void)hipStreamDestroy(stream_);
+    stream_ = with->stream_;
+    ownStream_ = false;
+    return 0;
+}
+
 int Extractor::reserve_cus(int one_in_n) {
     if (!stream_) return -4;
+    if (!ownStream_) return -1;   // a shared stream belongs to the other extractor
     int dev = 0, ncu = 0;
     ORB_HIP_CHECK(hipGetDevice(&dev));
     ORB_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));

@@ -108,6 +108,8 @@ public:
     hipStream_t stream() const { return stream_; }
     // recreate the stream with a CU mask leaving out one CU in every `one_in_n` (0: all CUs)
     int reserve_cus(int one_in_n);
+    // launch on `with`'s stream (not owned; `with` must outlive this extractor)
+    int share_stream(Extractor* with);
     int build_work(int B);
     // Device pyramid of the last extract() (mvImagePyramid with its 19-px border): image b's
     // padded level l starts at pyramid_base() + b * pyramid_image_bytes() + levels()[l].off.
@@ -170,6 +172,7 @@ private:
     int last_B_ = 0;
 
     hipStream_t stream_ = nullptr;
+    bool ownStream_ = true;
     hipEvent_t ev_[7] = {};
     // opt-in (ORBGPU_BLUR_SIDE=1): the blur runs on its own stream from the pyramid's end,
     // beside FAST / compaction / octree, and the descriptors wait for it

@@ -262,6 +262,14 @@ def partition_points_nd(problem, nranks, with_kf_owner=False):
     return (out[:k.npt], kfo[:len(problem["kf_id"])]) if with_kf_owner else out[:k.npt]
 
 
+def last_lm_path():
+    """The calling thread's last BA run: steps of the device-resident LM, trials the host loop decided
+    after a readback, and whether it was sharded (Optimizer_last_lm_path)."""
+    v = np.zeros(4, np.int32)
+    check(lib().Optimizer_last_lm_path(ptr(v)), "Optimizer_last_lm_path")
+    return dict(device_steps=int(v[0]), host_trials=int(v[1]), sharded=bool(v[2]))
+
+
 def last_sharding():
     """The calling thread's last BA run: (sharded factorisation used, separator tiles exchanged
     per trial, separator rows, Schur-pattern tiles the replicated path would all-reduce)."""
@@ -391,6 +399,7 @@ def run_sharded_local(problem, nranks, mode="local", nIterations=10, bRobust=Fal
             else:
                 results[r] = BundleAdjustmentSharded(shards[r], comms[r], nIterations, bRobust, trace=trace)
             results[r]["sharding"] = last_sharding()
+            results[r]["lm_path"] = last_lm_path()
         except Exception as e:  # noqa: BLE001 -- re-raised below
             errors[r] = e
 

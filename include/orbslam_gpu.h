@@ -117,6 +117,11 @@ int ORBextractor_last_corner_count(ORBextractor_h h, long long* total);
  * slots while a batch is being extracted.  one_in_n = 0 restores the full device.  Call
  * between extractions; ORBextractor_stream() changes. */
 int ORBextractor_reserve_cus(ORBextractor_h h, int one_in_n);
+/* Scheduling (no reference counterpart): h launches on `with`'s stream from now on, so the
+ * extractions of two extractors queue back to back on the device in call order (a pipeline
+ * that enqueues batch k+1 while batch k runs leaves no gap between them).  `with` keeps owning
+ * the stream and must outlive h; ORBextractor_reserve_cus(h, ...) is refused afterwards. */
+int ORBextractor_share_stream(ORBextractor_h h, ORBextractor_h with);
 
 /* ======================================================================
  * ORBmatcher  (reference include/ORBmatcher.h:41-103, src/ORBmatcher.cc)
@@ -841,6 +846,11 @@ int Optimizer_partition_points_nd(const ba_problem* P, int nranks, int32_t* pt_r
  * separator rows exchanged per LM trial, Schur-pattern tiles (what the replicated path
  * all-reduces)]. */
 int Optimizer_last_sharding(int* info4);
+/* The calling thread's last BA run's LM control: info4[0] = steps the device-resident LM queued
+ * (k_lm_trial_end decides each trial on the device; a sharded run exchanges between the step's
+ * kernels), info4[1] = trials the host loop decided after reading a trial's result back,
+ * info4[2] = 1 if the run was sharded over more than one rank, info4[3] = 0. */
+int Optimizer_last_lm_path(int* info4);
 int Optimizer_LocalBundleAdjustment_sharded(const ba_problem* shard, orbgpu_comm_h comm,
                                             const volatile bool* stop, ba_result* R);
 int Optimizer_BundleAdjustment_sharded(const ba_problem* shard, orbgpu_comm_h comm, int nIterations,

@@ -103,6 +103,33 @@ def test_sharded_local_ba_matches_oracle(gpu, nranks):
         np.testing.assert_array_equal(r["trial_lambda"], per[0]["trial_lambda"])
 
 
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_sharded_local_ba_device_lm(gpu, nranks):
+    """A sharded LocalBundleAdjustment runs the device-resident LM on every rank: each step's
+    exchanges (system, Schur tiles, the trial's chi2 / scale / stop) are queued between its
+    kernels and k_lm_trial_end decides every trial on the device, so no rank reads a trial's
+    result back (host_trials == 0); every rank queues the same steps.  Results against the oracle
+    as for the host loop (Optimizer.cc:453-778, optimization_algorithm_levenberg.cpp:102-149)."""
+    from c_orb_slam_amd.optimizer import run_sharded_local
+    pr = ba_problem(0)
+    s, per = run_sharded_local(pr, nranks, "local", trace=True)
+    o = oracle_lib.oracle_local_ba(pr)
+    assert s["iterations"] == o["iterations"]
+    assert np.array_equal(s["edge_erase"], o["edge_erase"])
+    np.testing.assert_allclose(s["solve_chi2"], o["solve_chi2"], rtol=1e-9)
+    _close(s, o)
+    paths = [r["lm_path"] for r in per]
+    for p in paths:
+        assert p["sharded"] and p["host_trials"] == 0 and p["device_steps"] > 0, paths
+    assert len({p["device_steps"] for p in paths}) == 1, paths
+    # at least one step per trial the oracle ran, and at most one queued after the run ended per
+    # optimize() call (two calls: the passes before and after the outlier gating)
+    assert len(o["trial_chi2"]) <= paths[0]["device_steps"] <= len(o["trial_chi2"]) + 2
+    for r in per[1:]:
+        assert np.array_equal(r["kf_Tcw"], per[0]["kf_Tcw"])
+        np.testing.assert_array_equal(r["trial_lambda"], per[0]["trial_lambda"])
+
+
 @pytest.mark.parametrize("nranks,n_kf", [(2, 24), (4, 40), (8, 64)])
 def test_sharded_global_ba_matches_oracle(gpu, nranks, n_kf):
     from c_orb_slam_amd.optimizer import run_sharded_local
