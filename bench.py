@@ -76,6 +76,11 @@ def parse():
                          "is enqueued and waited for within the step; 2 = batch k's extraction is queued at the "
                          "start of step k, before the host waits for batch k-1's (no idle extraction lane while "
                          "the host enqueues a chain; needs --lanes >= 3)")
+    ap.add_argument("--shared-ex-stream", type=int, default=0,
+                    help="1: every lane's extractor launches on the first lane's stream "
+                         "(ORBextractor_share_stream), so with --depth 2 batch k+1's extraction is queued behind "
+                         "batch k's on the device and starts with no gap; allows --depth 2 with 2 lanes (a lane's "
+                         "extraction waits for its previous chain: ORBmatcher_chain_wait)")
     ap.add_argument("--lane-matchers", type=int, default=1,
                     help="1 (default): every lane after the first tracks on its own ORBmatcher (own stream, "
                          "arena and deferred chain), so the tracking chains of consecutive batches overlap on "
@@ -1164,8 +1169,14 @@ def main():
         for ln in lanes:
             for ex in (ln.exL, ln.exR):
                 check(L.ORBextractor_reserve_cus(ex._h, args.reserve_cus), "ORBextractor_reserve_cus")
-    if args.depth > 1 and len(lanes) < 3:
-        sys.exit("bench.py: --depth 2 needs --lanes >= 3 (a lane's buffers are reused by batch k + lanes)")
+    if args.shared_ex_stream:
+        if not args.stereo_batch:
+            sys.exit("bench.py: --shared-ex-stream needs --stereo-batch 1 (one extractor per lane)")
+        for ln in lanes[1:]:
+            check(L.ORBextractor_share_stream(ln.exL._h, lanes[0].exL._h), "ORBextractor_share_stream")
+    if args.depth > 1 and len(lanes) < 3 and not args.shared_ex_stream:
+        sys.exit("bench.py: --depth 2 needs --lanes >= 3 (a lane's buffers are reused by batch k + lanes) "
+                 "or --shared-ex-stream 1")
     ex_pool = ThreadPoolExecutor(2 if args.depth > 1 else 1, initializer=lambda: torch.cuda.set_device(dev))
     state = {"k": 0, "ready": None, "pending": None, "inflight": None}
 
