@@ -91,8 +91,7 @@ __global__ void k_gs_index(int n, const int* __restrict__ sc, int slot, const in
 
 __global__ void k_gs_edges(int ne, const int* __restrict__ sc, const int* __restrict__ aE, const EdgeDev* __restrict__ E,
                            const int* __restrict__ poseIdx, const int* __restrict__ landIdx, int nkf, int* ePose,
-                           int* eLand, uint32_t* kPe, uint32_t* kLe, unsigned long long* kLp, int* vA, int* peCnt,
-                           int* leCnt, int* lpCnt) {
+                           int* eLand, uint32_t* kPe, uint32_t* kLe, unsigned long long* kLp, int* vA) {
     const int a = blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= ne) return;
     vA[a] = a;
@@ -103,15 +102,45 @@ __global__ void k_gs_edges(int ne, const int* __restrict__ sc, const int* __rest
         kPe[a] = p >= 0 ? (uint32_t)p : 0xffffffffu;
         kLe[a] = (uint32_t)l;
         kLp[a] = p >= 0 ? (unsigned long long)l * (unsigned long long)nkf + (unsigned long long)p : ~0ull;
-        atomicAdd(&leCnt[l], 1);
-        if (p >= 0) {
-            atomicAdd(&peCnt[p], 1);
-            atomicAdd(&lpCnt[l], 1);
-        }
     } else {
         kPe[a] = 0xffffffffu;
         kLe[a] = 0xffffffffu;
         kLp[a] = ~0ull;
+    }
+}
+
+// first position of a key >= v in a sorted key array (the lists' segment starts)
+template <class K>
+__device__ __forceinline__ int lower_bound_k(const K* __restrict__ k, int n, K v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (k[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+// The per-pose / per-landmark segment starts and counts of the three sorted edge lists: the start
+// of pose p is the number of sorted keys below p (invalid keys sort last), so the starts equal the
+// exclusive sums of the per-vertex counts -- without a same-address atomic per edge (1.5 M of them
+// onto 2,000 pose counters serialised at the L2: 0.3 ms per config-5 build).
+__global__ void k_gs_starts(int ne, int nkf, int npt, const uint32_t* __restrict__ kPe2, const uint32_t* __restrict__ kLe2,
+                            const unsigned long long* __restrict__ kLp2, int* peStart, int* peCnt, int* leStart,
+                            int* leCnt, int* lpStart, int* lpCnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= nkf) {
+        const int a = lower_bound_k(kPe2, ne, (uint32_t)i);
+        peStart[i] = a;
+        peCnt[i] = i < nkf ? lower_bound_k(kPe2, ne, (uint32_t)(i + 1)) - a : 0;
+    }
+    if (i <= npt) {
+        const int a = lower_bound_k(kLe2, ne, (uint32_t)i);
+        leStart[i] = a;
+        leCnt[i] = i < npt ? lower_bound_k(kLe2, ne, (uint32_t)(i + 1)) - a : 0;
+        const unsigned long long nk = (unsigned long long)nkf;
+        const int b = lower_bound_k(kLp2, ne, (unsigned long long)i * nk);
+        lpStart[i] = b;
+        lpCnt[i] = i < npt ? lower_bound_k(kLp2, ne, (unsigned long long)(i + 1) * nk) - b : 0;
     }
 }
 
@@ -151,24 +180,35 @@ __global__ void k_gs_scalars(const int* peStart, const int* leStart, const int* 
 }
 
 // every Schur term (u <= v over the landmark's lpList), numbered in the host walk's order
+// One thread per Schur term t (coalesced stores): its landmark l is the last with tStart[l] <= t,
+// then (u, v) the (t - tStart[l])-th pair u <= v of the landmark's lpList in the host's walk order
 __global__ void k_gs_terms(int npt, int nkf, const int* __restrict__ sc, const int* __restrict__ lpStart,
                            const int* __restrict__ lpList, const unsigned long long* __restrict__ kLp,
                            const long long* __restrict__ tStart, unsigned long long* bkey, int* tidx, int* tA, int* tB) {
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= npt || l >= sc[C_NL]) return;
-    const int b0 = lpStart[l], m = lpStart[l + 1] - b0;
-    long long t = tStart[l];
-    for (int u = 0; u < m; u++) {
-        const unsigned long long pu = kLp[b0 + u] % (unsigned long long)nkf;
-        const int au = lpList[b0 + u];
-        for (int v = u; v < m; v++, t++) {
-            const unsigned long long pv = kLp[b0 + v] % (unsigned long long)nkf;
-            bkey[t] = pu * (unsigned long long)nkf + pv;
-            tidx[t] = (int)t;
-            tA[t] = au;
-            tB[t] = lpList[b0 + v];
-        }
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int nL = min(npt, sc[C_NL]);
+    if (t >= tStart[nL]) return;
+    int lo = 0, hi = nL;   // the last l in [0, nL) with tStart[l] <= t
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tStart[mid] <= t) lo = mid;
+        else hi = mid;
     }
+    const int l = lo;
+    const int b0 = lpStart[l], m = lpStart[l + 1] - b0;
+    long long r = t - tStart[l];
+    int u = 0;
+    while (r >= m - u) {
+        r -= m - u;
+        u++;
+    }
+    const int v = u + (int)r;
+    const unsigned long long pu = kLp[b0 + u] % (unsigned long long)nkf;
+    const unsigned long long pv = kLp[b0 + v] % (unsigned long long)nkf;
+    bkey[t] = pu * (unsigned long long)nkf + pv;
+    tidx[t] = (int)t;
+    tA[t] = lpList[b0 + u];
+    tB[t] = lpList[b0 + v];
 }
 
 __global__ void k_gs_heads(int nPair, int nkf, const unsigned long long* __restrict__ k, const int* __restrict__ st,
@@ -355,12 +395,9 @@ int GpuStructBuilder::build(int level, int nkf, int npt, int ne, const EdgeDev* 
     GS_PTR(int, lpStart, S_LPSTART, npt + 1);
     GS_PTR(long long, tc, S_TC, npt + 1);
     GS_PTR(long long, tStart, S_TSTART, npt + 1);
-    GS_CHECK(hipMemsetAsync(peCnt, 0, sizeof(int) * (nkf + 1), s));
-    GS_CHECK(hipMemsetAsync(leCnt, 0, sizeof(int) * (npt + 1), s));
-    GS_CHECK(hipMemsetAsync(lpCnt, 0, sizeof(int) * (npt + 1), s));
     if (ne) {
         hipLaunchKernelGGL(k_gs_edges, dim3(nb(ne)), dim3(kT), 0, s, ne, sc, aE, dE, poseIdx, landIdx, nkf, ePose, eLand,
-                           kPe, kLe, kLp, vA, peCnt, leCnt, lpCnt);
+                           kPe, kLe, kLp, vA);
         if (int e = cub([&](void* t, size_t& b) {
                 return hipcub::DeviceRadixSort::SortPairs(t, b, kPe, kPe2, vA, peList, ne, 0, 32, s);
             }))
@@ -375,12 +412,13 @@ int GpuStructBuilder::build(int level, int nkf, int npt, int ne, const EdgeDev* 
             return e;
         hipLaunchKernelGGL(k_gs_dup, dim3(nb(ne)), dim3(kT), 0, s, ne, sc, kLp2, sc);
     }
-    if (int e = cub([&](void* t, size_t& b) { return hipcub::DeviceScan::ExclusiveSum(t, b, peCnt, peStart, nkf + 1, s); }))
-        return e;
-    if (int e = cub([&](void* t, size_t& b) { return hipcub::DeviceScan::ExclusiveSum(t, b, leCnt, leStart, npt + 1, s); }))
-        return e;
-    if (int e = cub([&](void* t, size_t& b) { return hipcub::DeviceScan::ExclusiveSum(t, b, lpCnt, lpStart, npt + 1, s); }))
-        return e;
+    {   // segment starts and counts of the sorted lists (no edges: every start 0)
+        const uint32_t* kPe2s = ne ? kPe2 : kPe;   // (unsorted, unused at ne = 0)
+        const uint32_t* kLe2s = ne ? kLe2 : kLe;
+        const unsigned long long* kLp2s = ne ? kLp2 : kLp;
+        hipLaunchKernelGGL(k_gs_starts, dim3(nb((long long)std::max(nkf, npt) + 1)), dim3(kT), 0, s, ne, nkf, npt, kPe2s,
+                           kLe2s, kLp2s, peStart, peCnt, leStart, leCnt, lpStart, lpCnt);
+    }
     hipLaunchKernelGGL(k_gs_counts, dim3(nb((long long)std::max(nkf, npt) + 1)), dim3(kT), 0, s, npt, nkf, sc, peCnt,
                        leCnt, lpCnt, tc, sc);
     if (int e = cub([&](void* t, size_t& b) { return hipcub::DeviceScan::ExclusiveSum(t, b, tc, tStart, npt + 1, s); }))
@@ -427,7 +465,7 @@ int GpuStructBuilder::build(int level, int nkf, int npt, int ne, const EdgeDev* 
     if (nP) hipLaunchKernelGGL(k_gs_diag, dim3(nb(nP)), dim3(kT), 0, s, nP, blkI, blkJ);
     int nOff = 0;
     if (nPair > 0) {
-        hipLaunchKernelGGL(k_gs_terms, dim3(nb(npt)), dim3(kT), 0, s, npt, nkf, sc, lpStart, lpList, kLp2, tStart, bkey,
+        hipLaunchKernelGGL(k_gs_terms, dim3(nb(nPair)), dim3(kT), 0, s, npt, nkf, sc, lpStart, lpList, kLp2, tStart, bkey,
                            tidx, tA, tB);
         int endbit = 1;
         while (endbit < 64 && ((unsigned long long)nkf * (unsigned long long)nkf >> endbit) != 0) endbit++;
