@@ -169,12 +169,15 @@ def test_extract_octree_regimes(gpu, kind, nf):
         assert np.array_equal(gd, od)
 
 
+@pytest.mark.parametrize("flow", [0, 1])
 @pytest.mark.parametrize("B", [3, 12])
-def test_pyramid_flow_alternating_batches(gpu, B):
-    """k_pyr_flow hands pyramid rows between workgroups of one launch: alternate two different
-    batches (and a smaller one) through one extractor, so a row read before its producer finished
-    would show the previous call's bytes; every padded level of every image byte-exact.  B = 3 and
-    12 take the two tile-height variants (16 / 32 rows)."""
+def test_pyramid_flow_alternating_batches(gpu, B, flow, monkeypatch):
+    """Alternate two different batches (and a smaller one) through one extractor: every padded
+    level of every image byte-exact.  flow = 1 builds the pyramid with k_pyr_flow (opt-in
+    ORBGPU_PYR_FLOW=1, read when the extractor is created), which hands pyramid rows between
+    workgroups of one launch, so a row read before its producer finished would show the previous
+    call's bytes.  B = 3 and 12 take the two tile-height variants (16 / 32 rows)."""
+    monkeypatch.setenv("ORBGPU_PYR_FLOW", str(flow))
     frames, _ = synthetic.sequence(21, 2 * B, 1241, 376)
     sets = [frames[:B], frames[B:], frames[:B][::-1], frames[B:][: max(1, B // 2)]]
     ex = gpu.ORBextractor(1200, 1.2, 8, 20, 7, max_width=1241, max_height=376, max_batch=B)
