@@ -81,6 +81,10 @@ def parse():
                          "(ORBextractor_share_stream), so with --depth 2 batch k+1's extraction is queued behind "
                          "batch k's on the device and starts with no gap; allows --depth 2 with 2 lanes (a lane's "
                          "extraction waits for its previous chain: ORBmatcher_chain_wait)")
+    ap.add_argument("--h2d-streams", type=int, default=1,
+                    help="host-IO leg: the step's H2D copy split over this many copy streams; 1 (default): "
+                         "2 and 4 pieces were slower, 0.86 / 0.54-0.60 of value against 0.93-0.97 "
+                         "(profiles/r06h2d_host_io_streams_ab.txt)")
     ap.add_argument("--lane-matchers", type=int, default=1,
                     help="1 (default): every lane after the first tracks on its own ORBmatcher (own stream, "
                          "arena and deferred chain), so the tracking chains of consecutive batches overlap on "
@@ -1242,6 +1246,11 @@ def main():
         stage = [torch.empty_like(src).pin_memory() for _ in lanes]
         dimg = [torch.empty_like(d_LR) for _ in lanes]
         cs = torch.cuda.Stream(dev)
+        # the copy in max(1, --h2d-streams) pieces on as many streams (DMA engines side by side); cs
+        # starts and joins them, so its events bracket the whole step's upload
+        nsplit = max(1, args.h2d_streams)
+        cs_more = [torch.cuda.Stream(dev) for _ in range(nsplit - 1)]
+        ev_piece = [torch.cuda.Event() for _ in range(nsplit - 1)]
         ev_done = [torch.cuda.Event() for _ in lanes]
         ev_t = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in lanes]
         up_pool = ThreadPoolExecutor(1, initializer=lambda: torch.cuda.set_device(dev))
@@ -1252,9 +1261,20 @@ def main():
             t = time.perf_counter()
             stage[j].copy_(src)                 # pageable -> pinned (host memcpy)
             stats["memcpy_s"] += time.perf_counter() - t
+            n = dimg[j].numel()
+            cuts = [n * q // nsplit for q in range(nsplit + 1)]
+            dflat, sflat = dimg[j].view(-1), stage[j].view(-1)
             with torch.cuda.stream(cs):
                 ev_t[j][0].record(cs)
-                dimg[j].copy_(stage[j], non_blocking=True)
+            for q, sq in enumerate(cs_more):
+                sq.wait_event(ev_t[j][0])
+                with torch.cuda.stream(sq):
+                    dflat[cuts[q + 1]:cuts[q + 2]].copy_(sflat[cuts[q + 1]:cuts[q + 2]], non_blocking=True)
+                    ev_piece[q].record(sq)
+            with torch.cuda.stream(cs):
+                dflat[cuts[0]:cuts[1]].copy_(sflat[cuts[0]:cuts[1]], non_blocking=True)
+                for e in ev_piece:
+                    cs.wait_event(e)
                 ev_t[j][1].record(cs)
                 ev_done[j].record(cs)
             stats["n"] += 1
@@ -1314,9 +1334,10 @@ def main():
                 "h2d_bytes_per_step": int(nbytes),
                 "h2d_GBps_achieved": round(nbytes / (float(np.mean(dma_ms)) * 1e-3) / 1e9, 2),
                 "host_memcpy_GBps": round(nbytes * stats["n"] / max(stats["memcpy_s"], 1e-9) / 1e9, 2),
+                "h2d_streams": nsplit,
                 "io": "host: each step's 2B images from one pageable host array -> pinned staging (host memcpy) "
-                      "-> H2D DMA on a copy stream, one step ahead of the extraction that waits on it; "
-                      "h2d_GBps_achieved = bytes / the DMA's HIP-event time"}
+                      "-> H2D DMA in h2d_streams pieces on as many copy streams, one step ahead of the "
+                      "extraction that waits on it; h2d_GBps_achieved = bytes / the DMA's HIP-event time"}
 
     def drain():
         """Track the extracted batch, collect every chain in order, leave the matcher synchronous."""
@@ -1413,7 +1434,8 @@ def main():
                     "matches_per_s": round(tot_match / dt, 1),
                     "keypoints_per_image": round(tot_kp / (2 * B * args.steps * world), 1), "cpu_baseline": cpu,
                     "stage_ms_per_step_by_image": stage_by_stream(),
-                    "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()}}
+                    "phase_ms_per_step": {k: round(v / args.steps, 4) for k, v in phase_acc.items()},
+                    "value_host_io": host_io}
             if cpu:
                 line["speedup_vs_cpu_all_core"] = round(fps / cpu["value"], 1)
             if args.sequence:   # the estimates stay on the true trajectory (rotation, max abs entry)
