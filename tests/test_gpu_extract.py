@@ -193,3 +193,26 @@ def test_pyramid_flow_alternating_batches(gpu, B, flow, monkeypatch):
             for l in range(8):
                 gl = ex.image_pyramid_level(l, b)
                 assert np.array_equal(gl, want[key][l]), f"image {b} level {l} differs at {np.argwhere(gl != want[key][l])[:5]}"
+
+
+def test_extractors_sharing_a_stream(gpu):
+    """ORBextractor_share_stream: two extractors launching on one stream (the second one's calls
+    queue behind the first one's) keep their own buffers: each batch bit-exact against the oracle,
+    and CU reservation is refused on the borrowed stream."""
+    from c_orb_slam_amd._lib import lib
+    frames, _ = synthetic.sequence(13, 4, 1241, 376)
+    a = gpu.ORBextractor(1200, 1.2, 8, 20, 7, max_width=1241, max_height=376, max_batch=2)
+    b = gpu.ORBextractor(1200, 1.2, 8, 20, 7, max_width=1241, max_height=376, max_batch=2)
+    assert lib().ORBextractor_share_stream(b._h, a._h) == 0
+    assert lib().ORBextractor_stream(b._h) == lib().ORBextractor_stream(a._h)
+    assert lib().ORBextractor_reserve_cus(b._h, 8) != 0
+    orc = oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7)
+    for rep in range(2):
+        ra = a.extract_batch(frames[:2])
+        rb = b.extract_batch(frames[2:])
+        for imgs, res in ((frames[:2], ra), (frames[2:], rb)):
+            for img, (k, d) in zip(imgs, res):
+                ok, od = orc(img)
+                assert np.array_equal(k.view(np.uint8), ok.view(np.uint8)), rep
+                assert np.array_equal(d, od), rep
+    del rb, b   # the borrower goes first (the stream's owner must outlive it)
