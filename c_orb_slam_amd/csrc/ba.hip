@@ -1862,8 +1862,6 @@ __global__ void __launch_bounds__(1024) k_csum(CsumList L0, CsumList L1, const i
 // the decisions it has seen; k_lm_trial_end sets the gates of the next step.
 // Host-pinned coherent words (LmHost): [0] stop flag mirror (host writes), [1] done, [2] steps
 // decided, [3] iterations, [4..5] (done, steps) as one 8-byte word the host polls (device writes).
-// host words [kLmHostDone + s]: done after step s (s < kLmHostSteps >= the step bound 10 x iterations)
-constexpr int kLmHostDone = 16, kLmHostSteps = kLmTrials + 8;
 __global__ void __launch_bounds__(64) k_lm_begin(LmDev* L, int iterations) {
     if (threadIdx.x != 0) return;
     L->ctl[0] = 1;
@@ -1994,13 +1992,6 @@ __device__ int lm_decide(LmDev* Lg, LmHead L, double* scal, volatile int* host, 
     host[3] = L.it;
     host[2] = L.steps;
     host[1] = L.done;
-    // done after step `steps` - 1, per step: what every rank of a sharded run decides its next
-    // enqueue on (the latest (done, steps) pair may already include a later step), written ahead
-    // of the pair the host polls
-    if (L.steps <= kLmHostSteps) {
-        host[kLmHostDone + L.steps - 1] = L.done;
-        __threadfence_system();
-    }
     // the pair (done, steps) as one aligned 8-byte store: the host's poll sees both or neither
     *(volatile unsigned long long*)(host + 4) = ((unsigned long long)(unsigned)L.steps << 32) | (unsigned)L.done;
     return pop;
@@ -3477,8 +3468,8 @@ int BaEngine::init() {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -4;
     ORB_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     ORB_HIP_CHECK(hipHostMalloc((void**)&hScal_, 64 * sizeof(double)));
-    ORB_HIP_CHECK(hipHostMalloc((void**)&hLm_, (kLmHostDone + kLmHostSteps) * sizeof(int), hipHostMallocCoherent));
-    std::memset((void*)hLm_, 0, (kLmHostDone + kLmHostSteps) * sizeof(int));   // [8]: poll_stream's sequence word
+    ORB_HIP_CHECK(hipHostMalloc((void**)&hLm_, 16 * sizeof(int), hipHostMallocCoherent));
+    std::memset((void*)hLm_, 0, 16 * sizeof(int));   // [8]: poll_stream's sequence word
     for (auto& ev : lmEv_) ORB_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     int dev = 0;
     ORB_HIP_CHECK(hipGetDevice(&dev));
@@ -4638,7 +4629,18 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
         const char* e = getenv("ORBGPU_LM_EVENTS");
         return e && e[0] == '1';
     }();
-    volatile int* hw = (volatile int*)hLm_;
+    // Whether the run ended with step s's decision, read once step s is decided.  Not simply the
+    // latest (done, steps) pair: it may already hold step s + 1's decision, which another rank of
+    // a sharded run may not have seen when it decides whether to queue step s + 2 -- and every
+    // rank must queue the same steps.  The pair is one 8-byte store: steps == s + 1 means its done
+    // bit is step s's; steps > s + 1 means step s + 1 was decided, so it was live and step s did
+    // not end the run; steps <= s (the stream drained without deciding step s) ends the loop.
+    volatile unsigned long long* hw64 = (volatile unsigned long long*)(hLm_ + 4);   // (done, steps)
+    auto done_after = [&](int st) {
+        const unsigned long long v = *hw64;
+        const int steps = (int)(v >> 32);
+        return steps == st + 1 ? (v & 0xffffffffu) != 0 : steps <= st;
+    };
     static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;   // host enqueue / wait split (tools/)
     using sclk = std::chrono::steady_clock;
     double tEnq = 0, tWait = 0;
@@ -4658,7 +4660,7 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
             ORB_HIP_CHECK(hipEventRecord(lmEv_[j & 1], stream_));
             if (j >= 1) {
                 ORB_HIP_CHECK(hipEventSynchronize(lmEv_[(j - 1) & 1]));
-                if (hw[kLmHostDone + j - 1]) break;
+                if (done_after(j - 1)) break;
             }
         } else if (j >= 1) {
             // step j - 1 decided (steps >= j) or the run over.  No HIP call inside the wait: a
@@ -4666,7 +4668,6 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
             // gap on the queue after every trial).  Only a wait past 50 ms asks whether the stream
             // drained (its writes are all visible then; the final readback checks the state).
             const auto w0 = sclk::now();
-            volatile unsigned long long* hw64 = (volatile unsigned long long*)(hLm_ + 4);   // (done, steps)
             for (unsigned spin = 1;; spin++) {
                 const unsigned long long v = *hw64;
                 if ((int)(v >> 32) >= j || (v & 0xffffffffu)) break;
@@ -4675,10 +4676,7 @@ int BaEngine::optimize_device(int iterations, const volatile bool* stop, int* it
                     break;
                 __builtin_ia32_pause();
             }
-            // done after step j - 1 (not the latest pair: it may already hold step j's decision,
-            // which other ranks of a sharded run have not seen when they decide whether to queue
-            // step j + 1: every rank queues the same steps)
-            if (hw[kLmHostDone + j - 1]) {
+            if (done_after(j - 1)) {
                 tEnq += std::chrono::duration<double, std::micro>(q1 - q0).count();
                 tWait += std::chrono::duration<double, std::micro>(sclk::now() - q1).count();
                 break;
