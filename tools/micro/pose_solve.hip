@@ -62,6 +62,66 @@ __global__ void __launch_bounds__(64) k_solve_micro_l(const double* Hin, const d
         for (int j = 0; j < 6; j++) out[j] = x[j];
     }
 }
+// pose_solve_l's prelude only (pivot ranks, order, the lane's permuted row): its share of a solve
+__device__ __forceinline__ double solve_prelude(const double* Hs, const double* bs, double lambda) {
+    double dv[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) dv[i] = fabs(Hs[DIAG21[i]] + lambda);
+    bool distinct = true;
+    int rank[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        int r = 0;
+        distinct = distinct && dv[j] == dv[j];
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+            if (i != j) {
+                r += dv[i] > dv[j] ? 1 : 0;
+                distinct = distinct && dv[i] != dv[j];
+            }
+        rank[j] = r;
+    }
+    int ord[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+        int o = 0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) o = rank[j] == r ? j : o;
+        ord[r] = o;
+    }
+    const int lane = threadIdx.x & 63, row = lane < 6 ? lane : 5;
+    int orow = ord[0];
+#pragma unroll
+    for (int p = 1; p < 6; p++) orow = row == p ? ord[p] : orow;
+    double a[6];
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+        const int i0 = min(orow, ord[c]), i1 = max(orow, ord[c]);
+        double h = Hs[i0 * 6 - (i0 * (i0 - 1)) / 2 + (i1 - i0)];
+        if (row == c) h += lambda;
+        a[c] = h;
+    }
+    return distinct ? a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + bs[orow] : 0.0;
+}
+__global__ void __launch_bounds__(64) k_prelude_micro(const double* Hin, const double* bin, double lambda, double* out,
+                                                      unsigned long long* cyc, int R) {
+    __shared__ double Hs[21], bs[6];
+    if (threadIdx.x < 21) Hs[threadIdx.x] = Hin[threadIdx.x];
+    if (threadIdx.x < 6) bs[threadIdx.x] = bin[threadIdx.x];
+    __syncthreads();
+    double lam = lambda, acc = 0;
+    unsigned long long t0 = clock64();
+    for (int r = 0; r < R; r++) {
+        const double v = solve_prelude(Hs, bs, lam);
+        acc += v;
+        lam = lam * 1.0000001 + v * 1e-300;
+    }
+    unsigned long long t1 = clock64();
+    if (threadIdx.x == 0) {
+        cyc[3] = (t1 - t0) / R;
+        out[0] = acc;
+    }
+}
 // both solves on n systems (one wave each): x and ok of pose_solve_w, then of pose_solve_l
 __global__ void __launch_bounds__(64) k_solve_cmp(const double* H, const double* b, const double* lam, double* xo, int* oko) {
     __shared__ double Hs[21], bs[6], scr[36];
@@ -157,5 +217,11 @@ int main() {
         bad += !same;
     }
     printf("pose_solve_l vs pose_solve_w: %d systems (%d solved), %d differ\n", n, nok, bad);
+    for (int rep = 0; rep < 2; rep++) {
+        hipLaunchKernelGGL(k_prelude_micro, dim3(1), dim3(64), 0, 0, dH, db, 1e-3, dout, dc, 64);
+        (void)hipDeviceSynchronize();
+    }
+    (void)hipMemcpy(c, dc, sizeof(c), hipMemcpyDeviceToHost);
+    printf("cycles per call: pose_solve_l prelude %llu\n", c[3]);
     return bad != 0;
 }
