@@ -1173,12 +1173,13 @@ int Extractor::share_stream(Extractor* with) {
     if (ownStream_) (void)hipStreamDestroy(stream_);
     stream_ = with->stream_;
     ownStream_ = false;
+    with->lent_++;   // its stream may no longer be recreated (reserve_cus)
     return 0;
 }
 
 int Extractor::reserve_cus(int one_in_n) {
     if (!stream_) return -4;
-    if (!ownStream_) return -1;   // a shared stream belongs to the other extractor
+    if (!ownStream_ || lent_) return -1;   // a shared stream: another extractor launches on it
     int dev = 0, ncu = 0;
     ORB_HIP_CHECK(hipGetDevice(&dev));
     ORB_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));

@@ -173,6 +173,7 @@ private:
 
     hipStream_t stream_ = nullptr;
     bool ownStream_ = true;
+    int lent_ = 0;   // extractors that launch on this one's stream (share_stream)
     hipEvent_t ev_[7] = {};
     // opt-in (ORBGPU_BLUR_SIDE=1): the blur runs on its own stream from the pyramid's end,
     // beside FAST / compaction / octree, and the descriptors wait for it

@@ -120,7 +120,7 @@ int ORBextractor_reserve_cus(ORBextractor_h h, int one_in_n);
 /* Scheduling (no reference counterpart): h launches on `with`'s stream from now on, so the
  * extractions of two extractors queue back to back on the device in call order (a pipeline
  * that enqueues batch k+1 while batch k runs leaves no gap between them).  `with` keeps owning
- * the stream and must outlive h; ORBextractor_reserve_cus(h, ...) is refused afterwards. */
+ * the stream and must outlive h; ORBextractor_reserve_cus is refused on both afterwards. */
 int ORBextractor_share_stream(ORBextractor_h h, ORBextractor_h with);
 
 /* ======================================================================

@@ -198,7 +198,7 @@ def test_pyramid_flow_alternating_batches(gpu, B, flow, monkeypatch):
 def test_extractors_sharing_a_stream(gpu):
     """ORBextractor_share_stream: two extractors launching on one stream (the second one's calls
     queue behind the first one's) keep their own buffers: each batch bit-exact against the oracle,
-    and CU reservation is refused on the borrowed stream."""
+    and CU reservation (which recreates a stream) is refused on both."""
     from c_orb_slam_amd._lib import lib
     frames, _ = synthetic.sequence(13, 4, 1241, 376)
     a = gpu.ORBextractor(1200, 1.2, 8, 20, 7, max_width=1241, max_height=376, max_batch=2)
@@ -206,6 +206,7 @@ def test_extractors_sharing_a_stream(gpu):
     assert lib().ORBextractor_share_stream(b._h, a._h) == 0
     assert lib().ORBextractor_stream(b._h) == lib().ORBextractor_stream(a._h)
     assert lib().ORBextractor_reserve_cus(b._h, 8) != 0
+    assert lib().ORBextractor_reserve_cus(a._h, 8) != 0   # (it would recreate the stream b launches on)
     orc = oracle_lib.OracleExtractor(1200, 1.2, 8, 20, 7)
     for rep in range(2):
         ra = a.extract_batch(frames[:2])
