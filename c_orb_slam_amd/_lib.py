@@ -237,6 +237,7 @@ def lib():
     L.orbgpu_unit_set_csum_lds_max.argtypes = [i32]
     L.orbgpu_unit_set_scale_small_max.argtypes = [i32]
     L.orbgpu_unit_set_struct_gpu_min_edges.argtypes = [i32]
+    L.orbgpu_unit_set_posegraph_check.argtypes = [i32]
     L.orbgpu_unit_ba_struct_all.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, i32, vp, C.c_longlong, vp]
     L.orbgpu_unit_nd_order.argtypes = [i32, vp, vp, i32, vp, vp, vp]
     L.orbgpu_debug_prof.argtypes = [vp]

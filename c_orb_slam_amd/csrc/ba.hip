@@ -3652,6 +3652,7 @@ int BaEngine::upload_problem(const ba_problem* P) {
         kfFixed_[k] = ((!mode_.global && !P->kf_local[k]) || P->kf_id[k] == 0) ? 1 : 0;
     if (mode_.global) kfLocal_.assign(nkf_, 1);
     ptHasEdge_.assign(npt_, 0);
+    kfHasEdge_.assign(nkf_, 0);
     // poses, points, compact edges and vertex data written straight into the pinned staging block
     // (no intermediate host copy): one H2D copy, unpacked by k_unpack_upload
     const UploadLayout UL = upload_layout(ne_, nkf_, npt_);
@@ -3668,9 +3669,17 @@ int BaEngine::upload_problem(const ba_problem* P) {
         for (size_t q = 3 * (size_t)a; q < 3 * (size_t)b; q++) Xs[q] = (double)P->pt_pos[q];
     });
     uint8_t* hasEdge = ptHasEdge_.data();
+    uint8_t* kfEdge = kfHasEdge_.data();
     host_parallel(ne_, [&](int a, int b) {
-        // (ranges share points: the flag bytes are stored atomically, all with the same value)
-        for (int i = a; i < b; i++) __atomic_store_n(&hasEdge[P->edge_pt[i]], (uint8_t)1, __ATOMIC_RELAXED);
+        // (ranges share points and keyframes: the flag bytes are stored atomically, all with the
+        // same value)
+        for (int i = a; i < b; i++) {
+            __atomic_store_n(&hasEdge[P->edge_pt[i]], (uint8_t)1, __ATOMIC_RELAXED);
+            // (a few thousand keyframe flags shared by every thread: stored only while unset, so
+            // the lines stay shared instead of bouncing between the cores)
+            uint8_t* f = &kfEdge[P->edge_kf[i]];
+            if (!__atomic_load_n(f, __ATOMIC_RELAXED)) __atomic_store_n(f, (uint8_t)1, __ATOMIC_RELAXED);
+        }
         std::memcpy(st + UL.oPt + sizeof(int32_t) * a, P->edge_pt + a, sizeof(int32_t) * (b - a));
         std::memcpy(st + UL.oKf + sizeof(int32_t) * a, P->edge_kf + a, sizeof(int32_t) * (b - a));
         std::memcpy(st + UL.oObs + sizeof(float) * 3 * (size_t)a, P->edge_obs + 3 * (size_t)a, sizeof(float) * 3 * (b - a));
@@ -3798,8 +3807,130 @@ static void pose_graph_csr(int nP, std::vector<int64_t>& all, std::vector<int>* 
         for (int i = 0; i < nP; i++) std::sort(adj.begin() + as[i], adj.begin() + as[i + 1]);
 }
 
+// ORBGPU_EARLY_GRAPH=0 derives the pose graph from the device lists only (A/B)
+static bool early_graph_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("ORBGPU_EARLY_GRAPH");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+static std::atomic<int> g_posegraph_check{0};   // orbgpu_unit_set_posegraph_check
+int debug_set_posegraph_check(int on) {
+    g_posegraph_check.store(on ? 1 : 0);
+    return 0;
+}
+constexpr int kEarlyGraphMaxPoses = 4096;   // a bit matrix of nP^2 bits per host thread
+
+// The pose graph of an unsharded global BA's first structure, from the caller's edges on the host
+// (buildIndexMapping's free poses with an edge, ascending id; two poses adjacent when they share
+// a map point: every pair of a point's free-pose edges), so that the nested dissection and the
+// symbolic factorisation run on a helper thread WHILE the device builds the lists, instead of
+// after them.  The same off-diagonal block set as the device's Schur pattern (k_gs_terms): the
+// keys come out ascending from a bit matrix.  Level 0 of a global BA: every edge is active.
+// Needs the points' edges in runs (validated, edgesGrouped).  build_structure adopts it when the
+// device's pose count agrees and otherwise joins and discards it.
+int BaEngine::start_early_pose_graph() {
+    spEarlyNP_ = -1;
+    std::vector<int> order;
+    order.reserve(nkf_);
+    for (int k = 0; k < nkf_; k++)
+        if (!kfFixed_[k] && kfHasEdge_[k]) order.push_back(k);
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return kfId_[a] < kfId_[b]; });
+    const int nP = (int)order.size();
+    if (nP < kTiledMinPoses || nP > kEarlyGraphMaxPoses) return 0;
+    std::vector<int32_t> poseOf(nkf_, -1);
+    for (int i = 0; i < nP; i++) poseOf[order[i]] = i;
+    int dev = 0;
+    ORB_HIP_CHECK(hipGetDevice(&dev));
+    spEarlyNP_ = nP;
+    spEarlyKeys_.clear();
+    const bool keep = g_posegraph_check.load() != 0;
+    const int32_t* ep = ePt_;
+    const int32_t* ek = eKf_;
+    const int ne = ne_;
+    spEarly_ = std::async(std::launch::async, [this, dev, nP, ne, ep, ek, keep, poseOf = std::move(poseOf)]() {
+        if (hipSetDevice(dev) != hipSuccess) return -2;   // the current device is per thread
+        const size_t nw = ((size_t)nP * nP + 63) / 64;
+        const int hw = (int)std::thread::hardware_concurrency();
+        const int T = ne >= (1 << 18) ? std::max(1, std::min(16, hw)) : 1;
+        std::vector<std::vector<uint64_t>> bits(T);
+        auto run_start = [&](int i) {   // first run start at or after i
+            while (i > 0 && i < ne && ep[i] == ep[i - 1]) i++;
+            return i;
+        };
+        auto mark = [&](int t) {   // ranges of whole runs, one bit matrix per thread
+            std::vector<uint64_t>& B = bits[t];
+            B.assign(nw, 0);
+            const int chunk = (ne + T - 1) / T;
+            const int i0 = run_start(std::min(ne, t * chunk)), i1 = run_start(std::min(ne, (t + 1) * chunk));
+            int ps[64];
+            for (int i = i0; i < i1;) {
+                int j = i, m = 0;
+                std::vector<int> big;
+                for (; j < i1 && ep[j] == ep[i]; j++) {
+                    const int p = poseOf[ek[j]];
+                    if (p < 0) continue;
+                    if (m < 64) ps[m++] = p;
+                    else big.push_back(p);
+                }
+                if (!big.empty()) {   // (a point with more than 64 free-pose edges)
+                    big.insert(big.begin(), ps, ps + m);
+                    for (size_t u = 0; u < big.size(); u++)
+                        for (size_t v = u + 1; v < big.size(); v++) {
+                            const size_t a = std::min(big[u], big[v]), b = std::max(big[u], big[v]);
+                            const size_t q = a * nP + b;
+                            B[q >> 6] |= 1ull << (q & 63);
+                        }
+                } else {
+                    for (int u = 0; u < m; u++)
+                        for (int v = u + 1; v < m; v++) {
+                            const size_t a = std::min(ps[u], ps[v]), b = std::max(ps[u], ps[v]);
+                            const size_t q = a * nP + b;
+                            B[q >> 6] |= 1ull << (q & 63);
+                        }
+                }
+                i = j;
+            }
+        };
+        {
+            std::vector<std::thread> th;
+            for (int t = 1; t < T; t++) th.emplace_back(mark, t);
+            mark(0);
+            for (auto& x : th) x.join();
+        }
+        if (T > 1) {   // OR-merge into thread 0's matrix, word ranges split over the threads
+            const size_t wc = (nw + T - 1) / T;
+            auto merge = [&](int t) {
+                const size_t w0 = std::min(nw, t * wc), w1 = std::min(nw, (t + 1) * wc);
+                for (int r = 1; r < T; r++)
+                    for (size_t w = w0; w < w1; w++) bits[0][w] |= bits[r][w];
+            };
+            std::vector<std::thread> th;
+            for (int t = 1; t < T; t++) th.emplace_back(merge, t);
+            merge(0);
+            for (auto& x : th) x.join();
+        }
+        std::vector<int64_t> keys;   // ascending: the bit index is the key i1 * nP + i2
+        for (size_t w = 0; w < nw; w++)
+            for (uint64_t v = bits[0][w]; v; v &= v - 1) keys.push_back((int64_t)(w * 64 + __builtin_ctzll(v)));
+        if (keep) spEarlyKeys_ = keys;
+        std::vector<int> as, adj;
+        pose_graph_csr(nP, keys, &as, &adj);
+        return sp_.build(6 * nP, 6, as, adj, true, stream_);
+    });
+    return 0;
+}
+
 int BaEngine::build_structure(int level) {
     if (int e = join_sp_build()) return e;   // (a previous structure's helper, if any)
+    if (spEarly_.valid()) (void)spEarly_.get();
+    spEarlyNP_ = -1;
+    // the unsharded global BA's first structure: pose graph, nested dissection and symbolic
+    // factorisation from the host edges, beside the device lists below
+    if (!comm_ && mode_.global && level == 0 && edgesGrouped && ePt_ && eKf_ && nd_async() && early_graph_enabled() &&
+        !struct_host(ne_, false))
+        if (int e = start_early_pose_graph()) return e;
     using sclk = std::chrono::steady_clock;
     static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;
     auto ts0 = sclk::now();
@@ -3841,7 +3972,29 @@ int BaEngine::build_structure(int level) {
         if (info.maxPe > 64 * kChunks || info.maxLe > 64 * 64 || info.maxBlk > 64 * kChunks) return -3;
         blkChunks_ = (info.maxBlk + 63) / 64;
         if (nE > kCsumLv * 64 * 64 || 6LL * nP + 3LL * nL > (long long)scratchN_) return -3;
-        if (nP >= kTiledMinPoses && !comm_) {
+        if (spEarly_.valid() && (nP != spEarlyNP_ || g_posegraph_check.load())) {
+            // the device's pose set differs (not expected: then the lists' graph is used), or the
+            // early keys are checked against the device's
+            const int e = spEarly_.get();
+            const int np = spEarlyNP_;
+            spEarlyNP_ = -1;
+            if (e) return e;
+            if (np == nP) {
+                if (int e2 = gs_.offkeys(&offKeys, stream_)) return e2;
+                if (offKeys != spEarlyKeys_) {
+                    fprintf(stderr, "[ba] early pose graph differs from the device's (%zu vs %zu keys)\n",
+                            spEarlyKeys_.size(), offKeys.size());
+                    return -2;
+                }
+                spEarlyNP_ = np;   // checked: sp_ holds the structure already
+                spBuild_ = std::async(std::launch::deferred, [] { return 0; });
+            }
+        }
+        if (spEarly_.valid()) {   // adopted: joined before the first Schur assembly (join_sp_build)
+            spBuild_ = std::move(spEarly_);
+        } else if (spEarlyNP_ == nP) {
+            // checked against the device's keys above: sp_ holds the structure
+        } else if (nP >= kTiledMinPoses && !comm_) {
             if (int e = gs_.offkeys(&offKeys, stream_)) return e;
         } else if (nP >= kTiledMinPoses) {
             for (int b = 0; b < nBlk; b++)
@@ -4000,7 +4153,9 @@ int BaEngine::build_structure(int level) {
         // so every rank orders and factors the same structure) -> nested-dissection order,
         // symbolic factorisation; S travels as the Schur-pattern prefix of the tiles
         std::vector<int64_t> mine = std::move(offKeys);
-        if (!comm_ && nd_async()) {
+        if (spEarlyNP_ == nP) {
+            lap("pose graph + nested dissection + symbolic factorisation started early");
+        } else if (!comm_ && nd_async()) {
             // the pose graph, nested dissection and symbolic factorisation (host, ~2.5 ms at 2,000
             // keyframes) run on a helper thread while this thread queues the first LM iteration's
             // linearisation and reductions, which do not touch the block structure; lm_solve joins
@@ -4733,8 +4888,9 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
     struct EdgeRefs {
         BaEngine* e;
         ~EdgeRefs() {
+            (void)e->join_sp_build();   // no helper thread outlives the call (both read the
+            if (e->spEarly_.valid()) (void)e->spEarly_.get();   // caller's edge arrays)
             e->ePt_ = e->eKf_ = nullptr;
-            (void)e->join_sp_build();   // no helper thread outlives the call
         }
     } edgeRefs{this};
     trace_ = BaTrace{};

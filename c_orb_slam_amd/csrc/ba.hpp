@@ -66,6 +66,10 @@ public:
     // the last run's LM control: [0] steps the device-resident LM queued, [1] trials the host loop
     // (lm_solve) decided after a readback, [2] 1 if sharded (Optimizer_last_lm_path)
     int last_lm[4] = {0, 0, 0, 0};
+    // set by the C ABI before run(): every map point's edges form one run (validated), so the
+    // unsharded global BA may derive the pose graph from the caller's edges on the host while
+    // the device builds the lists (early_pose_graph)
+    bool edgesGrouped = false;
 
 private:
     int upload_problem(const ba_problem* P);
@@ -100,7 +104,7 @@ private:
     std::vector<int32_t> kfId_, ptId_;
     const int32_t* ePt_ = nullptr;   // the current call's edge arrays (ba_problem, caller-owned)
     const int32_t* eKf_ = nullptr;
-    std::vector<uint8_t> kfFixed_, kfLocal_, level_, ptHasEdge_;
+    std::vector<uint8_t> kfFixed_, kfLocal_, level_, ptHasEdge_, kfHasEdge_;
     // structure
     BaStructDev st_{};
     BaHostStruct hs_;              // host lists of the current structure (ORBGPU_STRUCT_HOST=1 path)
@@ -121,6 +125,12 @@ private:
     double *tmpA0_ = nullptr, *tmpA1_ = nullptr, *tmpB0_ = nullptr, *tmpB1_ = nullptr;
     unsigned* dCounter_ = nullptr;
     SparseLdlt sp_;                // block-sparse pose system (n > the dense solvers' reach)
+    // the early pose graph (host, from the caller's edges) + nested dissection + symbolic
+    // factorisation, started before the device lists: its pose count, and its keys when checked
+    std::future<int> spEarly_;
+    int spEarlyNP_ = -1;
+    std::vector<int64_t> spEarlyKeys_;
+    int start_early_pose_graph();
     std::future<int> spBuild_;     // sp_.build on a helper thread (unsharded global BA): joined by
                                    // join_sp_build() before the first use of sp_ (lm_solve's Schur)
     int join_sp_build();
@@ -214,6 +224,7 @@ int debug_shared_div(const double* a, const double* b, int n, double* out);
 int debug_set_csum_lds_max(int v);
 int debug_set_scale_small_max(int v);
 int debug_set_struct_gpu_min_edges(int v);
+int debug_set_posegraph_check(int on);
 int debug_prof(unsigned long long* out32);
 
 }  // namespace orbgpu

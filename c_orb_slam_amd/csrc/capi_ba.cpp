@@ -71,7 +71,10 @@ int grouped_pairs(const ba_problem* P) {
     return bad.load() ? 1 : rep.load() ? 2 : 0;
 }
 
-int validate(const ba_problem* P, const ba_result* R) {
+// grouped (optional): set when every map point's edges are one run (the Optimizer's order; the
+// engine can then walk a point's edges without bucketing them)
+int validate(const ba_problem* P, const ba_result* R, bool* grouped = nullptr) {
+    if (grouped) *grouped = false;
     if (!P || !R || P->n_kf < 0 || P->n_pt < 0 || P->n_edge < 0) return ORB_E_INVALID;
     if (P->n_kf && (!P->kf_id || !P->kf_Tcw || !P->kf_local || !P->kf_cam || !R->kf_Tcw)) return ORB_E_INVALID;
     if (P->n_pt && (!P->pt_id || !P->pt_pos || !R->pt_pos)) return ORB_E_INVALID;
@@ -109,7 +112,10 @@ int validate(const ba_problem* P, const ba_result* R) {
         // runs falls through to the bucketing below
         const int g = grouped_pairs(P);
         if (g == 1) return ORB_E_INVALID;
-        if (g == 0) return ORB_OK;
+        if (g == 0) {
+            if (grouped) *grouped = true;
+            return ORB_OK;
+        }
     }
     std::vector<int32_t> start((size_t)P->n_pt + 1, 0);
     for (int i = 0; i < P->n_edge; i++) {
@@ -131,10 +137,12 @@ int validate(const ba_problem* P, const ba_result* R) {
 
 int run_ba(const ba_problem* P, const volatile bool* stop, ba_result* R, orbgpu::Comm* comm,
            const orbgpu::BaMode* mode) {
-    if (int v = validate(P, R)) return v;
+    bool grouped = false;
+    if (int v = validate(P, R, &grouped)) return v;
     int rc = 0;
     orbgpu::BaEngine* e = engine(&rc);
     if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
+    e->edgesGrouped = grouped;
     const int r = e->run(P, stop, R, comm, mode);
     if (r == -1) return ORB_E_INVALID;
     if (r == -3) return ORB_E_CAPACITY;
@@ -575,6 +583,10 @@ int orbgpu_unit_set_csum_lds_max(int m2_max) {
 int orbgpu_unit_set_scale_small_max(int terms) {
     return orbgpu::debug_set_scale_small_max(terms) ? ORB_E_INVALID : ORB_OK;
 }
+int orbgpu_unit_set_posegraph_check(int on) {
+    return orbgpu::debug_set_posegraph_check(on);
+}
+
 int orbgpu_unit_set_struct_gpu_min_edges(int edges) {
     return orbgpu::debug_set_struct_gpu_min_edges(edges) ? ORB_E_INVALID : ORB_OK;
 }

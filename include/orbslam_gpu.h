@@ -912,6 +912,10 @@ int orbgpu_unit_set_scale_small_max(int terms);
  * (ba_struct_gpu.hip), smaller ones on the host (default 100000; 0 sends every run to the
  * device builder).  ORBGPU_STRUCT_HOST=1 / 0 in the environment overrides it.  Process-wide. */
 int orbgpu_unit_set_struct_gpu_min_edges(int edges);
+/* Test knob: an unsharded global BA derives its first pose graph from the caller's edges on the
+ * host, beside the device's structure lists; on = 1 also fetches the device's off-diagonal Schur
+ * blocks and fails the call (ORB_E_HIP) if the two graphs differ.  Process-wide. */
+int orbgpu_unit_set_posegraph_check(int on);
 /* The elimination order of the block-sparse pose system (host only, no device): nested
  * dissection of a graph (adjStart[n + 1] / adj: symmetric, sorted lists) with leaves of at
  * most `leaf` nodes; perm[k] = node eliminated k-th; the separator tree's node count and

@@ -61,6 +61,27 @@ def test_global_ba_chi2_tail_path_matches_oracle(gpu, lds_max):
     _exact(g, o)
 
 
+@pytest.mark.parametrize("n_kf,laps", [(120, 2), (400, 4)])
+def test_global_ba_early_pose_graph_matches_device(gpu, n_kf, laps):
+    """An unsharded global BA derives its first pose graph from the caller's edges on the host
+    (beside the device's structure lists): with the check on, the call fails unless the early
+    graph equals the device's off-diagonal Schur blocks; the result against the oracle."""
+    from c_orb_slam_amd._lib import lib
+    from c_orb_slam_amd.optimizer import BundleAdjustment
+    pr = global_ba_problem(n_kf + laps, n_kf=n_kf, pts_per_kf=60, laps=laps)
+    assert lib().orbgpu_unit_set_struct_gpu_min_edges(0) == 0   # the device lists at any size
+    assert lib().orbgpu_unit_set_posegraph_check(1) == 0
+    try:
+        g = BundleAdjustment(pr, 10, False, trace=True)
+    finally:
+        assert lib().orbgpu_unit_set_posegraph_check(0) == 0
+        assert lib().orbgpu_unit_set_struct_gpu_min_edges(100000) == 0
+    o = oracle_lib.oracle_global_ba(pr, 10, False)
+    assert g["iterations"] == o["iterations"]
+    np.testing.assert_allclose(g["trial_chi2"], o["trial_chi2"], rtol=1e-12)
+    _exact(g, o)
+
+
 def test_global_ba_points_without_edges_untouched(gpu):
     from c_orb_slam_amd.optimizer import BundleAdjustment
     pr = global_ba_problem(3, n_kf=10, pts_per_kf=40)
