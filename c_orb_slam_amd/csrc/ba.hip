@@ -4053,7 +4053,8 @@ int BaEngine::build_structure(int level) {
         }
         lap("active set");
         if (!refine &&
-            ba_build_lists(nkf_, npt_, eKf_, ePt_, kfFixed_.data(), kfId_.data(), ptId_.data(), kfAct, ptAct, &H))
+            ba_build_lists(nkf_, npt_, eKf_, ePt_, kfFixed_.data(), kfId_.data(), ptId_.data(), kfAct, ptAct, &H,
+                           !edgesValidated))
             return -1;
         hsValid_ = true;
         lap(refine ? "lists (refined)" : "lists");

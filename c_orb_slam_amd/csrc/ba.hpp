@@ -70,6 +70,9 @@ public:
     // unsharded global BA may derive the pose graph from the caller's edges on the host while
     // the device builds the lists (early_pose_graph)
     bool edgesGrouped = false;
+    // set by the C ABI before run(): one edge per (map point, keyframe) was checked there, so the
+    // host structure builder skips its own duplicate check
+    bool edgesValidated = false;
 
 private:
     int upload_problem(const ba_problem* P);

@@ -186,7 +186,7 @@ int ba_build_blocks(int nP, int nL, const int32_t* __restrict__ qs, const int32_
 
 int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, const uint8_t* kfFixed,
                    const int32_t* kfId, const int32_t* ptId, const std::vector<uint8_t>& kfAct,
-                   const std::vector<uint8_t>& ptAct, BaHostStruct* S) {
+                   const std::vector<uint8_t>& ptAct, BaHostStruct* S, bool checkDup) {
     static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;   // the phases below (tools/)
     using sclk = std::chrono::steady_clock;
     auto ts0 = sclk::now();
@@ -270,10 +270,12 @@ int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, con
     const int32_t* __restrict__ qs = S->lpStart.data();
     const int32_t* __restrict__ ql = S->lpList.data();
     const int32_t* __restrict__ qp = lpPose.data();
-    for (int l = 0; l < nL; l++)   // one edge per (pose, landmark)
-        for (int j = qs[l] + 1; j < qs[l + 1]; j++)
-            if (qp[j] == qp[j - 1]) return -1;
-    lap("duplicate check");
+    if (checkDup) {   // one edge per (pose, landmark); (the C ABI validated its callers' edges)
+        for (int l = 0; l < nL; l++)
+            for (int j = qs[l] + 1; j < qs[l + 1]; j++)
+                if (qp[j] == qp[j - 1]) return -1;
+        lap("duplicate check");
+    }
     return ba_build_blocks(nP, nL, qs, ql, qp, S);
 }
 

@@ -28,7 +28,7 @@ void ba_active_set(int level, int nkf, int npt, int ne, const int32_t* eKf, cons
 // or -1 when a landmark has two edges to one pose (g2o would build a duplicate Hpl block).
 int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, const uint8_t* kfFixed,
                    const int32_t* kfId, const int32_t* ptId, const std::vector<uint8_t>& kfAct,
-                   const std::vector<uint8_t>& ptAct, BaHostStruct* S);
+                   const std::vector<uint8_t>& ptAct, BaHostStruct* S, bool checkDup = true);
 
 // The Schur pattern from built lp lists (ba_build_lists' last phases).
 int ba_build_blocks(int nP, int nL, const int32_t* qs, const int32_t* ql, const int32_t* qp, BaHostStruct* S);

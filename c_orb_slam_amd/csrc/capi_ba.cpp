@@ -143,6 +143,7 @@ int run_ba(const ba_problem* P, const volatile bool* stop, ba_result* R, orbgpu:
     orbgpu::BaEngine* e = engine(&rc);
     if (rc) return rc == -4 ? ORB_E_NODEVICE : ORB_E_HIP;
     e->edgesGrouped = grouped;
+    e->edgesValidated = true;
     const int r = e->run(P, stop, R, comm, mode);
     if (r == -1) return ORB_E_INVALID;
     if (r == -3) return ORB_E_CAPACITY;
