@@ -60,7 +60,11 @@ def main():
         per, first = rank_times(path)
         # every call runs its ranks on fresh host threads: the last call's ranks are the R
         # threads that started last (earlier threads: warm-up calls)
-        last = sorted(first, key=lambda t: first[t])[-R:]
+        # (helper threads -- the structure's nested dissection, the early pose graph -- launch a
+        # few copies and fills of their own: only threads with a rank's share of the work count)
+        big = max(sum(v.values()) for v in per.values())
+        cand = [t for t in first if sum(per[t].values()) >= 0.05 * big]
+        last = sorted(cand, key=lambda t: first[t])[-R:]
         ranks = sorted(((t, per[t]) for t in last), key=lambda kv: -sum(kv[1].values()))
         tot = [sum(v.values()) / calls for _, v in ranks]
         fac = [v["factorisation"] / calls for _, v in ranks]
