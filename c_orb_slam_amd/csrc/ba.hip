@@ -3487,7 +3487,7 @@ bool BaEngine::dense_solver(int n) const {
 
 // Carve every device buffer of the problem out of one grow-only arena.
 struct UploadLayout {   // byte offsets in the staging span (all 8-byte aligned)
-    size_t oT, oX, oPt, oKf, oObs, oIs, oCam, oFx, oKid, oPid, total;
+    size_t oT, oX, oPt, oKf, oObs, oIs, oCam, oFx, oKid, oPid, oOrd, total;
 };
 static UploadLayout upload_layout(size_t ne, size_t nkf, size_t npt) {
     auto al8 = [](size_t b) { return (b + 7) & ~(size_t)7; };
@@ -3502,7 +3502,8 @@ static UploadLayout upload_layout(size_t ne, size_t nkf, size_t npt) {
     L.oFx = L.oCam + al8(sizeof(float) * 5 * nkf);
     L.oKid = L.oFx + al8(nkf);
     L.oPid = L.oKid + al8(sizeof(int32_t) * nkf);
-    L.total = L.oPid + al8(sizeof(int32_t) * npt);
+    L.oOrd = L.oPid + al8(sizeof(int32_t) * npt);
+    L.total = L.oOrd + al8(sizeof(int32_t) * npt);
     return L;
 }
 int BaEngine::carve(bool commit, size_t* total) {
@@ -3552,6 +3553,8 @@ int BaEngine::carve(bool commit, size_t* total) {
     dTn_ = (Se3*)take(sizeof(Se3) * nkf);
     dXn_ = (double*)take(sizeof(double) * 3 * npt);
     dPtId_ = (int32_t*)take(sizeof(int32_t) * npt);
+    dKp_ = (int32_t*)take(sizeof(int32_t) * ne);
+    dPtOrd_ = (int32_t*)take(sizeof(int32_t) * npt);
     dScratch_ = (double*)take(sizeof(double) * scratchN_);
     tmpA0_ = (double*)take(sizeof(double) * tmpN);
     tmpA1_ = (double*)take(sizeof(double) * tmpN);
@@ -3584,6 +3587,7 @@ struct UploadArgs {
     EdgeDev* E;
     uint8_t *kfFixed, *level, *robustFlag;
     int32_t *kfId, *ptId;
+    int32_t *kp, *ptOrd;   // the one-workgroup structure builder's inputs (null: not built)
     double* err;
     unsigned* counter;
 };
@@ -3611,6 +3615,7 @@ __global__ void __launch_bounds__(256) k_unpack_upload(UploadArgs a) {
         e.delta = (double)(e.stereo ? a.thStereo : a.thMono);
         e.dsqr = e.delta * e.delta;
         a.E[i] = e;
+        if (a.kp) a.kp[i] = (e.kf << 13) | e.pt;
         a.level[i] = 0;
         a.robustFlag[i] = (uint8_t)a.robust;
         for (int k = 0; k < 3; k++) a.err[3 * i + k] = 0.0;
@@ -3622,6 +3627,7 @@ __global__ void __launch_bounds__(256) k_unpack_upload(UploadArgs a) {
         a.kfId[i] = ((const int32_t*)(a.src + L.oKid))[i];
     }
     if (i < a.npt) a.ptId[i] = ((const int32_t*)(a.src + L.oPid))[i];
+    if (a.ptOrd && i < a.npt) a.ptOrd[i] = ((const int32_t*)(a.src + L.oOrd))[i];
     if (i < 16) a.counter[i] = 0;
 }
 
@@ -3686,6 +3692,13 @@ int BaEngine::upload_problem(const ba_problem* P) {
         std::memcpy(st + UL.oIs + sizeof(float) * a, P->edge_inv_sigma2 + a, sizeof(float) * (b - a));
     });
     level_.assign(ne_, 0);
+    // the one-workgroup structure builder reads compact edge keys and the points' id order
+    smallUp_ = small_struct();
+    if (smallUp_) {
+        std::vector<int32_t> ord;
+        ba_order_by_id(npt_, P->pt_id, &ord);
+        std::memcpy(st + UL.oOrd, ord.data(), sizeof(int32_t) * npt_);
+    }
     hipStream_t s = stream_;
     char* dst = (char*)dTerms_;   // free until the first linearisation
     ORB_HIP_CHECK(hipMemcpyAsync(dst, st, UL.total, hipMemcpyHostToDevice, s));
@@ -3707,6 +3720,8 @@ int BaEngine::upload_problem(const ba_problem* P) {
     ua.robustFlag = dRobust_;
     ua.kfId = dKfId_;
     ua.ptId = dPtId_;
+    ua.kp = smallUp_ ? dKp_ : nullptr;
+    ua.ptOrd = smallUp_ ? dPtOrd_ : nullptr;
     ua.err = dErr_;
     ua.counter = dCounter_;
     const long long nthr = std::max<long long>({(long long)ne_, 8LL * nkf_, 3LL * npt_, 16LL});
@@ -3743,6 +3758,27 @@ static bool struct_host(int ne, bool sharded) {
         return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
     return v < 0 ? (!sharded && ne < g_struct_gpu_min.load()) : v == 1;
+}
+// Local-BA sizes build their lists in one workgroup on the device (GpuStructBuilder::build_small:
+// one launch and one polled count readback per level against ~0.2 ms of host counting sorts per
+// level, tools/r06_lba_ab.sh).  ORBGPU_STRUCT_SMALL=0 keeps the previous choice (A/B runs);
+// ORBGPU_STRUCT_HOST=1 still forces the host builder.
+static bool small_struct_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("ORBGPU_STRUCT_SMALL");
+        const char* h = std::getenv("ORBGPU_STRUCT_HOST");
+        return !(e && e[0] == '0') && !(h && h[0] == '1');
+    }();
+    return v;
+}
+bool BaEngine::small_struct() const {
+    if (comm_ || !small_struct_enabled()) return false;
+    int nFree = 0;
+    for (int k = 0; k < nkf_; k++) nFree += kfFixed_[k] ? 0 : 1;
+    return GpuStructBuilder::small_fits(nkf_, npt_, ne_, nFree);
+}
+bool BaEngine::host_lists() const {
+    return !small_struct() && struct_host(ne_, comm_ && comm_->size() > 1);
 }
 int debug_set_struct_gpu_min_edges(int v) {
     if (v < 0) return -1;
@@ -3929,7 +3965,7 @@ int BaEngine::build_structure(int level) {
     // the unsharded global BA's first structure: pose graph, nested dissection and symbolic
     // factorisation from the host edges, beside the device lists below
     if (!comm_ && mode_.global && level == 0 && edgesGrouped && ePt_ && eKf_ && nd_async() && early_graph_enabled() &&
-        !struct_host(ne_, false))
+        !host_lists())
         if (int e = start_early_pose_graph()) return e;
     using sclk = std::chrono::steady_clock;
     static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;
@@ -3944,21 +3980,27 @@ int BaEngine::build_structure(int level) {
     distOk_ = false;
     std::vector<int64_t> offKeys;    // off-diagonal Schur blocks i1 * nP + i2, ascending (tiled path)
     std::vector<int32_t> blkIJ;      // blkI ++ blkJ (dense sharded path)
-    if (!struct_host(ne_, comm_ && comm_->size() > 1)) {
-        // the lists built on the device from the edges already in HBM (ba_struct_gpu.hip)
+    if (!host_lists()) {
+        // the lists built on the device from the edges already in HBM (ba_struct_gpu.hip): in one
+        // workgroup at local-BA sizes (with the pose-list positions), else by the multi-launch builder
         GpuStructInfo info{};
-        const int r = gs_.build(level, nkf_, npt_, ne_, dE_, dLevel_, dKfFixed_, dKfId_, dPtId_, comm_, stream_, &st_,
-                                &info, comm_ ? &blkIJ : nullptr);
+        int r = 1;
+        if (smallUp_ && small_struct())
+            r = gs_.build_small(level, nkf_, npt_, ne_, dKp_, dPtOrd_, dLevel_, dKfFixed_, dKfId_, dPePos_, stream_, &st_,
+                                &info);
+        if (r == 1)
+            r = gs_.build(level, nkf_, npt_, ne_, dE_, dLevel_, dKfFixed_, dKfId_, dPtId_, comm_, stream_, &st_, &info,
+                          comm_ ? &blkIJ : nullptr);
         if (r == -1) return -1;
         if (r) return r;
-        lap("lists (device)");
+        lap(info.posDone ? "lists (device, one workgroup)" : "lists (device)");
         nE = info.nE;
         nP = info.nP;
         nL = info.nL;
         nBlk = info.nBlk;
         nEglob_ = info.nEglob;
         nLglob_ = info.nLglob;
-        if (nE) {
+        if (nE && !info.posDone) {
             ORB_HIP_CHECK(hipMemsetAsync(dPePos_, 0xff, sizeof(int32_t) * nE, stream_));
             if (info.nPe)
                 hipLaunchKernelGGL(k_pe_pos, dim3((info.nPe + 255) / 256), dim3(256), 0, stream_, st_.peList, info.nPe, dPePos_);
@@ -4939,7 +4981,7 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
             if (int e = reduce_stop(stop)) return e;
         }
         if (!stopped(stop)) {
-            if (struct_host(ne_, comm_ && comm_->size() > 1)) {   // the host builder reads the levels from the host mirror
+            if (host_lists()) {   // the host builder reads the levels from the host mirror
                 std::vector<uint8_t> flag(ne_);
                 if (int e = gate_edges(0, flag.data())) return e;
                 for (int i = 0; i < ne_; i++)

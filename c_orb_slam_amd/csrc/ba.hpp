@@ -85,6 +85,12 @@ private:
     void enqueue_lm_step(bool first);
     // the same step for a rank of a sharded run: lm_solve's kernels and exchanges, gated
     int enqueue_lm_step_comm(bool first);
+    // the structure builder of this call: the one-workgroup device builder (local-BA sizes,
+    // unsharded), else the host lists below the device builder's edge threshold
+    bool small_struct() const;
+    bool host_lists() const;
+    bool smallUp_ = false;                          // this call's upload wrote dKp_ / dPtOrd_
+    int32_t *dKp_ = nullptr, *dPtOrd_ = nullptr;    // (keyframe << 13) | point per edge; points by id
     double* dLmStage_ = nullptr;   // the system's all-reduce staging (Hpp, b_p, chi2) of enqueue_lm_step_comm
     size_t lmStageCap_ = 0;
     int gate_edges(int final_check, uint8_t* erase);

@@ -72,6 +72,11 @@ static void by_id(int n, const uint8_t* flag, const int32_t* id, std::vector<int
     for (size_t k = 0; k < m; k++) (*out)[k] = (int32_t)(keys[k] & 0xffffffffu);
 }
 
+void ba_order_by_id(int n, const int32_t* id, std::vector<int32_t>* out) {
+    std::vector<uint8_t> all((size_t)std::max(n, 1), 1);
+    by_id(n, all.data(), id, out);
+}
+
 // The Schur pattern of a structure whose lpStart / lpList (landmark -> free-pose edges, pose
 // order) and their poses qp are built: blocks numbered (diagonal first, then first use in the
 // (landmark, u <= v) walk), each block's terms in landmark order.

@@ -26,6 +26,10 @@ void ba_active_set(int level, int nkf, int npt, int ne, const int32_t* eKf, cons
 
 // The index maps and lists of an active set.  kfAct may be the union over shards.  Returns 0,
 // or -1 when a landmark has two edges to one pose (g2o would build a duplicate Hpl block).
+// every index 0..n-1 ascending by (id[i], i): the vertex order of buildIndexMapping before the
+// active-set filter (the one-workgroup device builder's input)
+void ba_order_by_id(int n, const int32_t* id, std::vector<int32_t>* out);
+
 int ba_build_lists(int nkf, int npt, const int32_t* eKf, const int32_t* ePt, const uint8_t* kfFixed,
                    const int32_t* kfId, const int32_t* ptId, const std::vector<uint8_t>& kfAct,
                    const std::vector<uint8_t>& ptAct, BaHostStruct* S, bool checkDup = true);

@@ -18,6 +18,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 
 #include "ba_struct.hpp"
@@ -282,12 +284,566 @@ __global__ void k_gs_glob_out(const double* d, int* sc) {
 struct Max {
     __device__ __forceinline__ int operator()(int a, int b) const { return a > b ? a : b; }
 };
+
+// ---------------------------------------------------------------- one workgroup, small problems
+// A local BA (SURVEY config 4: 30 keyframes, 3,000 points, 15 k edges) is too small for the
+// multi-launch builder above: its ~40 launches and two readbacks cost more than the host's
+// counting sorts.  k_gs_small builds the same sixteen lists in ONE 1024-thread workgroup.  Global
+// memory is read once at the start (each thread a contiguous chunk of edges, its loads independent)
+// and written as results; every intermediate list lives in LDS (16-bit positions), because a
+// chain of dependent global loads per thread costs ~0.5-1 us a link in a single workgroup (the
+// first version, which kept the lists in global memory, took 330-380 us per level).  The counts
+// reach the host through pinned memory (one poll, no copy).  Every list is the host's
+// (ba_struct.cpp) by construction:
+//   aE            per-thread chunks compacted with one workgroup scan: edge order
+//   poseKf        the free active keyframes ranked by (mnId, index) -- at most kSmMaxP of them
+//   landPt        the active points compacted in the host's (mnId, index) order of all points
+//   le/lp counts  one packed counter per landmark (edges low, free-pose edges high), one scan
+//   leList        LDS cursors, then each landmark's (short) segment sorted by edge position
+//   lpList        a landmark's free-pose edges placed by the rank of their pose in the landmark's
+//                 pose bitmask: pose order without a sort; a pose seen twice = duplicate edge
+//   peList        per wave a contiguous range of active edges, split by pose with ballots
+//                 (stable: edge order inside a pose), bases scanned pose-major over the waves
+//   Schur blocks  a landmark's terms are the pose pairs (i <= j) of its bitmask; an off-diagonal
+//                 block's first use is its first landmark, then (i, j) -- the host walk's order
+//                 (landmark, u, v) because a landmark's lp entries are in pose order; each block's
+//                 terms placed in landmark order by the same wave-range ballot split
+// Anything outside the limits (more free poses, a longer landmark segment) is reported as
+// "fallback" and the multi-launch builder runs instead.  Inputs: the compact per-edge keys
+// (keyframe << 13 | point) and the points' (mnId, index) order, both written at upload.
+constexpr int kSmT = 1024, kSmW = kSmT / 64;
+constexpr int kSmMaxPt = 8192, kSmMaxKf = 1024, kSmMaxE = 16384;
+constexpr int kSmPer = kSmMaxE / kSmT;                       // edges per thread
+constexpr int kSmPtPer = kSmMaxPt / kSmT;                    // points per thread
+constexpr int kSmSteps = kSmMaxPt / kSmW / 64;               // 64-landmark steps per wave
+constexpr int kSmMaxP = 23;                                  // free poses (the dense solvers' range)
+constexpr int kSmTri = (kSmMaxP + 1) * (kSmMaxP + 2) / 2;    // pose pairs i <= j: j (j + 1) / 2 + i
+constexpr int kSmMaxLe = 256;
+// the LDS pool, by phase (bytes)
+constexpr int kOffA = 0;                              // ePose8[e]                 | Schur: per-wave pair counters (A+B)
+constexpr int kOffB = kOffA + kSmMaxE;                // leStart16[l]
+constexpr int kOffC = kOffB + 2 * (kSmMaxPt + 32);    // free keyframes (poses) -> lpList16[q]
+constexpr int kOffD = kOffC + 2 * kSmMaxE;            // packed counts int[l] -> leList16[j] -> pePos16[a] -> Schur ballots
+constexpr int kOffE = kOffD + 4 * (kSmMaxPt + 16);    // point flags (P1-P2) -> lpStart16[l]
+constexpr int kOffF = kOffE + 2 * (kSmMaxPt + 32);    // landIdx16[p] -> le cursors int[l] -> mask32[l]
+constexpr int kPool = kOffF + 4 * (kSmMaxPt + 16);
+static_assert(4 * kSmW * kSmTri <= kOffC, "the pair counters overlap A+B only");
+static_assert(8 * kSmW * (kSmMaxPt / kSmW / 64) * 23 <= kOffE - kOffD, "the Schur step ballots fit D");
+static_assert(4 * kSmMaxKf <= 2 * kSmMaxE, "the free keyframes fit C");
+enum SmSc { SM_NE, SM_NP, SM_NL, SM_NBLK, SM_NPAIR, SM_NPE, SM_NLP, SM_MAXPE, SM_MAXLE, SM_MAXBLK, SM_ERR, SM_FALLBACK,
+            SM_SEQ, SM_N };
+
+struct SmallArgs {
+    int level, nkf, npt, ne, seq;
+    const int32_t* kp;        // per edge (keyframe << 13) | point (k_unpack_upload)
+    const int32_t* ptOrd;     // the points by (mnId, index) (host, once per call)
+    const uint8_t* lv;
+    const uint8_t* kfFixed;
+    const int32_t* kfId;
+    int *aE, *ePose, *eLand, *poseKf, *landPt, *peStart, *peList, *leStart, *leList, *lpStart, *lpList, *blkI, *blkJ,
+        *blkStart, *pairA, *pairB;
+    int* pePos;           // null: pairs hold active-edge positions; else pePos and pairs as pose-list positions
+    int* sc;              // device copy of the counts
+    volatile int* hSc;    // pinned coherent: the counts, then the sequence word
+    volatile long long* ts;   // ORBGPU_BA_TIMES: phase timestamps (wall clock, 100 MHz) or null
+};
+
+__device__ __forceinline__ unsigned long long lanes_below() {
+    return (1ull << (threadIdx.x & 63)) - 1ull;
+}
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+// exclusive prefix of v over the workgroup, *tot the sum (ws: 32 ints of LDS)
+__device__ __forceinline__ int block_excl(int v, int* ws, int* tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int inc = wave_incl_scan(v);
+    if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        const int t = lane < kSmW ? ws[lane] : 0;
+        const int it = wave_incl_scan(t);
+        if (lane < kSmW) ws[kSmW + lane] = it;
+    }
+    __syncthreads();
+    const int base = w ? ws[kSmW + w - 1] : 0;
+    *tot = ws[2 * kSmW - 1];
+    __syncthreads();
+    return base + inc - v;
+}
+__device__ __forceinline__ int block_max(int v, int* ws) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    if (lane == 0) ws[w] = v;
+    __syncthreads();
+    int m = 0;
+    for (int k = 0; k < kSmW; k++) m = max(m, ws[k]);
+    __syncthreads();
+    return m;
+}
+// in-place exclusive scan of a[0, n) in LDS (contiguous chunks per thread); returns the total
+__device__ int block_scan_inplace(int* a, int n, int* ws) {
+    const int per = (n + kSmT - 1) / kSmT;
+    const int c0 = min(n, (int)threadIdx.x * per), c1 = min(n, c0 + per);
+    int s = 0;
+    for (int i = c0; i < c1; i++) s += a[i];
+    int tot;
+    int base = block_excl(s, ws, &tot);
+    for (int i = c0; i < c1; i++) {
+        const int v = a[i];
+        a[i] = base;
+        base += v;
+    }
+    __syncthreads();
+    return tot;
+}
+// the lanes whose `key` equals this lane's (valid lanes only; keys below 2^bits)
+__device__ __forceinline__ unsigned long long same_key(int key, bool valid, int bits) {
+    unsigned long long m = __ballot(valid);
+    for (int b = 0; b < bits; b++) {
+        const bool on = (key >> b) & 1;
+        const unsigned long long t = __ballot(valid && on);
+        m &= on ? t : ~t;
+    }
+    return m;
+}
+
+__global__ void __launch_bounds__(kSmT) k_gs_small(SmallArgs A) {
+    __shared__ __attribute__((aligned(16))) unsigned char pool[kPool];
+    __shared__ uint8_t sKfAct[kSmMaxKf];
+    __shared__ int8_t sPoseIdx[kSmMaxKf];
+    __shared__ int sPe[kSmW * kSmMaxP];
+    __shared__ int sFirst[kSmTri], sTot[kSmTri], sBlk[kSmTri], sBcnt[kSmTri + 1];
+    __shared__ int sFreeId[kSmMaxP + 1];
+    __shared__ int sWs[2 * kSmW];
+    int8_t* const ePose8 = reinterpret_cast<int8_t*>(pool + kOffA);
+    uint16_t* const leStart16 = reinterpret_cast<uint16_t*>(pool + kOffB);
+    int* const sFree = reinterpret_cast<int*>(pool + kOffC);
+    uint16_t* const lpList16 = reinterpret_cast<uint16_t*>(pool + kOffC);
+    int* const cnt = reinterpret_cast<int*>(pool + kOffD);
+    uint16_t* const leList16 = reinterpret_cast<uint16_t*>(pool + kOffD);
+    uint16_t* const pePos16 = reinterpret_cast<uint16_t*>(pool + kOffD);
+    uint8_t* const ptAct = pool + kOffE;
+    uint16_t* const lpStart16 = reinterpret_cast<uint16_t*>(pool + kOffE);
+    uint16_t* const landIdx16 = reinterpret_cast<uint16_t*>(pool + kOffF);
+    int* const cur = reinterpret_cast<int*>(pool + kOffF);
+    uint32_t* const mask = reinterpret_cast<uint32_t*>(pool + kOffF);
+    int* const sBc = reinterpret_cast<int*>(pool);   // per wave, per pose pair: term count, then next slot
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ne = A.ne, nkf = A.nkf, npt = A.npt;
+#define SM_TS(k) \
+    if (A.ts && tid == 0) A.ts[k] = (long long)wall_clock64()
+    SM_TS(0);
+    int nE = 0, nP = 0, nL = 0, nBlk = 0, nPair = 0, nPe = 0, nLp = 0, maxPe = 0, maxLe = 0, maxBlk = 0, err = 0,
+        fallback = 0;
+
+    for (int i = tid; i < npt; i += kSmT) ptAct[i] = 0;
+    for (int i = tid; i < nkf; i += kSmT) {
+        sKfAct[i] = 0;
+        sPoseIdx[i] = -1;
+    }
+    for (int i = tid; i <= npt; i += kSmT) cnt[i] = 0;
+    // 1. initializeOptimization(level): this thread's chunk of kSmPer edges [c0, c1) as four
+    // 16-byte key loads and one 16-byte level load (the compact per-edge keys, not the records)
+    const int c0 = min(ne, tid * kSmPer), c1 = min(ne, c0 + kSmPer);
+    int kp[kSmPer];        // active: (keyframe << 13) | point; later (landmark << 5) | (pose + 1)
+    uint32_t act = 0;
+    if (c1 - c0 == kSmPer) {
+        const int4* k4 = reinterpret_cast<const int4*>(A.kp + c0);
+        const uint4 l4 = *reinterpret_cast<const uint4*>(A.lv + c0);
+        const uint32_t lw[4] = {l4.x, l4.y, l4.z, l4.w};
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const int4 q = k4[v];
+            kp[4 * v] = q.x;
+            kp[4 * v + 1] = q.y;
+            kp[4 * v + 2] = q.z;
+            kp[4 * v + 3] = q.w;
+        }
+#pragma unroll
+        for (int k = 0; k < kSmPer; k++) act |= ((lw[k >> 2] >> (8 * (k & 3))) & 0xffu) == (uint32_t)A.level ? 1u << k : 0u;
+    } else if (c0 < c1) {
+#pragma unroll
+        for (int k = 0; k < kSmPer; k++) {
+            const int i = min(c0 + k, c1 - 1);
+            kp[k] = A.kp[i];
+            act |= (c0 + k < c1 && A.lv[i] == A.level) ? 1u << k : 0u;
+        }
+    }
+    __syncthreads();   // (the flags are cleared)
+#pragma unroll
+    for (int k = 0; k < kSmPer; k++)
+        if ((act >> k) & 1u) {
+            ptAct[kp[k] & 8191] = 1;
+            sKfAct[kp[k] >> 13] = 1;
+        }
+    int aBase;   // this thread's first active-edge position
+    {
+        int tot;
+        aBase = block_excl(__popc(act), sWs, &tot);
+        nE = tot;
+        int q = aBase;
+#pragma unroll
+        for (int k = 0; k < kSmPer; k++)
+            if ((act >> k) & 1u) A.aE[q++] = c0 + k;
+    }
+    SM_TS(1);
+    // 2. buildIndexMapping: the free active keyframes by (mnId, index)
+    for (int b = 0; b < nkf; b += kSmT) {
+        const int k = b + tid;
+        const bool f = k < nkf && sKfAct[k] && !A.kfFixed[k];
+        int tot;
+        const int pos = block_excl(f ? 1 : 0, sWs, &tot);
+        if (f) sFree[nP + pos] = k;
+        nP += tot;
+    }
+    __syncthreads();
+    if (nP > kSmMaxP) {
+        fallback = 1;
+        goto done;
+    }
+    if (tid < nP) sFreeId[tid] = A.kfId[sFree[tid]];
+    __syncthreads();
+    if (tid < nP) {
+        const int k = sFree[tid];
+        const int32_t id = sFreeId[tid];
+        int r = 0;
+        for (int q = 0; q < nP; q++) {
+            const int32_t id2 = sFreeId[q];
+            r += (id2 < id || (id2 == id && sFree[q] < k)) ? 1 : 0;
+        }
+        A.poseKf[r] = k;
+        sPoseIdx[k] = (int8_t)r;
+    }
+    SM_TS(2);
+    {   // the active points in (mnId, index) order: the host's order of all points, compacted
+        const int r0 = min(npt, tid * kSmPtPer), r1 = min(npt, r0 + kSmPtPer);
+        int pp[kSmPtPer];
+        uint32_t pa = 0;
+#pragma unroll
+        for (int k = 0; k < kSmPtPer; k++) {
+            const int r = r0 + k;
+            pp[k] = r < r1 ? A.ptOrd[r] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kSmPtPer; k++) pa |= (r0 + k < r1 && ptAct[pp[k]]) ? 1u << k : 0u;
+        int tot;
+        int q = block_excl(__popc(pa), sWs, &tot);
+        nL = tot;
+#pragma unroll
+        for (int k = 0; k < kSmPtPer; k++)
+            if ((pa >> k) & 1u) {
+                A.landPt[q] = pp[k];
+                landIdx16[pp[k]] = (uint16_t)q;
+                q++;
+            }
+    }
+    __syncthreads();
+    SM_TS(3);
+    SM_TS(4);
+    // 3. per active edge: its pose / landmark index; per landmark one packed counter
+    {
+        int q = aBase;
+#pragma unroll
+        for (int k = 0; k < kSmPer; k++)
+            if ((act >> k) & 1u) {
+                const int p = sPoseIdx[kp[k] >> 13], l = landIdx16[kp[k] & 8191];
+                ePose8[q] = (int8_t)p;
+                A.ePose[q] = p;
+                A.eLand[q] = l;
+                atomicAdd(&cnt[l], p >= 0 ? 0x10001 : 1);
+                kp[k] = (l << 5) | (p + 1);
+                q++;
+            }
+    }
+    __syncthreads();
+    {
+        int m = 0;
+        for (int i = tid; i < nL; i += kSmT) m = max(m, cnt[i] & 0xffff);
+        maxLe = block_max(m, sWs);
+        if (maxLe > kSmMaxLe) {
+            fallback = 1;
+            goto done;
+        }
+        // both scans at once: the low halves sum to nE < 2^16, so nothing carries into the high ones
+        const int tot = block_scan_inplace(cnt, nL + 1, sWs);
+        nLp = tot >> 16;
+        for (int i = tid; i <= nL; i += kSmT) {
+            const int v = cnt[i], le = v & 0xffff, lp = v >> 16;
+            leStart16[i] = (uint16_t)le;
+            lpStart16[i] = (uint16_t)lp;
+            cur[i] = le;
+            A.leStart[i] = le;
+            A.lpStart[i] = lp;
+        }
+    }
+    __syncthreads();
+    SM_TS(5);
+    {   // each landmark's edges through the cursors (then sorted per landmark below)
+        int q = aBase;
+#pragma unroll
+        for (int k = 0; k < kSmPer; k++)
+            if ((act >> k) & 1u) leList16[atomicAdd(&cur[kp[k] >> 5], 1)] = (uint16_t)q++;
+    }
+    __syncthreads();
+    {
+        int dup = 0;
+        for (int l = tid; l < nL; l += kSmT) {
+            const int s0 = leStart16[l], s1 = leStart16[l + 1];
+            for (int j = s0 + 1; j < s1; j++) {
+                const uint16_t v = leList16[j];
+                int k = j - 1;
+                while (k >= s0 && leList16[k] > v) {
+                    leList16[k + 1] = leList16[k];
+                    k--;
+                }
+                leList16[k + 1] = v;
+            }
+            // the free-pose edges in pose order: an edge's slot is its pose's rank in the bitmask
+            uint32_t M = 0;
+            for (int j = s0; j < s1; j++) {
+                const int a = leList16[j], p = ePose8[a];
+                A.leList[j] = a;
+                if (p < 0) continue;
+                dup |= (M >> p) & 1u;
+                M |= 1u << p;
+            }
+            const int q0 = lpStart16[l];
+            for (int j = s0; j < s1; j++) {
+                const int a = leList16[j], p = ePose8[a];
+                if (p >= 0) {
+                    const int q = q0 + __popc(M & ((1u << p) - 1u));
+                    lpList16[q] = (uint16_t)a;
+                    A.lpList[q] = a;
+                }
+            }
+            mask[l] = M;
+        }
+        if (__syncthreads_or(dup)) {
+            err = 1;
+            goto done;
+        }
+    }
+    SM_TS(6);
+    {   // 4. the pose lists: per wave a contiguous range of active edges, split by pose
+        const int pw = (nE + kSmW - 1) / kSmW, e0 = min(nE, wv * pw), e1 = min(nE, e0 + pw);
+        volatile int* const pe = sPe + wv * kSmMaxP;
+        for (int i = lane; i < kSmMaxP; i += 64) pe[i] = 0;
+        for (int b = e0; b < e1; b += 64) {
+            const int a = b + lane;
+            const int p = a < e1 ? ePose8[a] : -1;
+            const unsigned long long m = same_key(p, p >= 0, 5);
+            if (p >= 0 && (m & lanes_below()) == 0) pe[p] += __popcll(m);
+        }
+        __syncthreads();
+        if (wv == 0) {   // per pose: its total, its start, the waves' bases in wave order
+            int t = 0;
+            if (lane < nP)
+                for (int w = 0; w < kSmW; w++) t += sPe[w * kSmMaxP + lane];
+            const int inc = wave_incl_scan(t);
+            if (lane < nP) {
+                int run = inc - t;
+                A.peStart[lane] = run;
+                for (int w = 0; w < kSmW; w++) {
+                    const int c = sPe[w * kSmMaxP + lane];
+                    sPe[w * kSmMaxP + lane] = run;
+                    run += c;
+                }
+            }
+            int mx = t;
+            for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+            const int tot = __shfl(inc, 63);
+            if (lane == 0) {
+                sWs[0] = mx;
+                sWs[1] = tot;
+                A.peStart[nP] = tot;
+            }
+        }
+        __syncthreads();
+        maxPe = sWs[0];
+        nPe = sWs[1];
+        for (int b = e0; b < e1; b += 64) {
+            const int a = b + lane;
+            const int p = a < e1 ? ePose8[a] : -1;
+            const unsigned long long m = same_key(p, p >= 0, 5);
+            if (p >= 0) {
+                const int pos = pe[p] + __popcll(m & lanes_below());
+                A.peList[pos] = a;
+                pePos16[a] = (uint16_t)pos;
+                if (A.pePos) A.pePos[a] = pos;
+                if ((m & lanes_below()) == 0) pe[p] += __popcll(m);
+            } else if (a < e1) {
+                pePos16[a] = 0xffff;
+                if (A.pePos) A.pePos[a] = -1;
+            }
+        }
+        __syncthreads();
+    }
+    SM_TS(7);
+    if (A.pePos) {   // the pairs are written as pose-list positions: map the lp entries once
+        for (int q = tid; q < nLp; q += kSmT) lpList16[q] = pePos16[lpList16[q]];
+        __syncthreads();
+    }
+    {   // 5. buildStructure's Schur pattern over the pose pairs s = j (j + 1) / 2 + i, i <= j.
+        // Each wave owns a contiguous range of landmarks in up to kSmSteps steps of 64 (lane =
+        // landmark, its pose bitmask in a register).  Per step and pose one ballot ("which lanes
+        // see pose p") goes to LDS; a pair's count, first use and every term's slot follow from
+        // ANDs and popcounts of two of them.  Each lane places only its own landmark's terms.
+        const int nTri = nP * (nP + 1) / 2;
+        unsigned long long* const Bt = reinterpret_cast<unsigned long long*>(pool + kOffD) + wv * kSmSteps * kSmMaxP;
+        for (int s = tid; s < kSmTri; s += kSmT) sFirst[s] = 0x7fffffff;
+        for (int s = tid; s <= kSmTri; s += kSmT) sBcnt[s] = 0;
+        const int pl = (nL + kSmW - 1) / kSmW, l0 = min(nL, wv * pl), l1 = min(nL, l0 + pl);
+        const int nst = (l1 - l0 + 63) / 64;
+        uint32_t Ms[kSmSteps];
+        int Q0[kSmSteps];
+#pragma unroll
+        for (int st = 0; st < kSmSteps; st++) {
+            const int l = l0 + st * 64 + lane;
+            const bool ok = st < nst && l < l1;
+            Ms[st] = ok ? mask[l] : 0u;
+            Q0[st] = ok ? lpStart16[l] : 0;
+            if (st < nst)
+                for (int p = 0; p < nP; p++) {
+                    const unsigned long long m = __ballot((Ms[st] >> p) & 1u);
+                    if (lane == 0) Bt[st * kSmMaxP + p] = m;
+                }
+        }
+        __syncthreads();   // (the first-use keys are reset; the ballots are published)
+        // per pair (lane-strided): the wave's term count and its first landmark
+        for (int s = lane; s < nTri; s += 64) {
+            int j = 0;
+            while ((j + 1) * (j + 2) / 2 <= s) j++;
+            const int i = s - j * (j + 1) / 2;
+            int c = 0, first = 0x7fffffff;
+            for (int st = 0; st < nst; st++) {
+                const unsigned long long x = Bt[st * kSmMaxP + i] & Bt[st * kSmMaxP + j];
+                if (x && first == 0x7fffffff) first = l0 + st * 64 + (int)__builtin_ctzll(x);
+                c += __popcll(x);
+            }
+            sBc[wv * kSmTri + s] = c;
+            if (i != j && c) atomicMin(&sFirst[s], first);
+        }
+        __syncthreads();
+        // per pair: its term count; a used off-diagonal pair's first use as one ordered key
+        // (first landmark, i, j) -- sFirst < kSmMaxPt, so the key fits an int
+        int nOffMine = 0;
+        for (int s = tid; s < nTri; s += kSmT) {
+            int j = 0;
+            while ((j + 1) * (j + 2) / 2 <= s) j++;
+            const int i = s - j * (j + 1) / 2;
+            int t = 0;
+            for (int w = 0; w < kSmW; w++) t += sBc[w * kSmTri + s];
+            sTot[s] = t;
+            const bool off = i != j && t > 0;
+            sFirst[s] = off ? sFirst[s] * 1024 + i * 32 + j : 0x7fffffff;
+            nOffMine += off ? 1 : 0;
+        }
+        {
+            int tot;
+            (void)block_excl(nOffMine, sWs, &tot);   // (its barriers publish sTot / sFirst)
+            nBlk = nP + tot;
+        }
+        // block numbers: diagonal blocks 0..nP-1, then the used off-diagonal ones by first use
+        for (int s = tid; s < nTri; s += kSmT) {
+            int j = 0;
+            while ((j + 1) * (j + 2) / 2 <= s) j++;
+            const int i = s - j * (j + 1) / 2;
+            const int key = sFirst[s];
+            int num = -1;
+            if (i == j) {
+                num = i;
+            } else if (key != 0x7fffffff) {
+                int r = 0;
+                for (int s2 = 0; s2 < nTri; s2++) r += sFirst[s2] < key ? 1 : 0;
+                num = nP + r;
+            }
+            sBlk[s] = num;
+            if (num >= 0) {
+                sBcnt[num] = sTot[s];
+                A.blkI[num] = i;
+                A.blkJ[num] = j;
+            }
+        }
+        __syncthreads();
+        int mb = 0;
+        for (int b = tid; b < nBlk; b += kSmT) mb = max(mb, sBcnt[b]);
+        maxBlk = block_max(mb, sWs);
+        nPair = block_scan_inplace(sBcnt, nBlk + 1, sWs);
+        for (int b = tid; b <= nBlk; b += kSmT) A.blkStart[b] = sBcnt[b];
+        for (int s = tid; s < nTri; s += kSmT)
+            if (sBlk[s] >= 0) {
+                int run = sBcnt[sBlk[s]];
+                for (int w = 0; w < kSmW; w++) {
+                    const int c = sBc[w * kSmTri + s];
+                    sBc[w * kSmTri + s] = run;
+                    run += c;
+                }
+            }
+        __syncthreads();
+        // the terms: a term's slot is its wave's base for the pair, plus the wave's earlier steps'
+        // terms of the pair, plus the lanes below it in its step with the pair -- landmark order
+#pragma unroll
+        for (int st = 0; st < kSmSteps; st++) {
+            if (st >= nst) break;
+            const uint32_t M = Ms[st];
+            const int q0 = Q0[st];
+            const unsigned long long* const Bs = Bt + st * kSmMaxP;
+            for (uint32_t mu = M; mu; mu &= mu - 1) {
+                const int i = __builtin_ctz(mu);
+                const int ai = lpList16[q0 + __popc(M & ((1u << i) - 1u))];
+                const unsigned long long bi = Bs[i];
+                for (uint32_t mv = mu; mv; mv &= mv - 1) {
+                    const int j = __builtin_ctz(mv);
+                    const int s = j * (j + 1) / 2 + i;
+                    int pos = sBc[wv * kSmTri + s] + __popcll(bi & Bs[j] & lanes_below());
+                    for (int st2 = 0; st2 < st; st2++) pos += __popcll(Bt[st2 * kSmMaxP + i] & Bt[st2 * kSmMaxP + j]);
+                    A.pairA[pos] = ai;
+                    A.pairB[pos] = lpList16[q0 + __popc(M & ((1u << j) - 1u))];
+                }
+            }
+        }
+    }
+done:
+    __syncthreads();
+    SM_TS(8);
+    if (tid == 0) {
+        int v[SM_N];
+        v[SM_NE] = nE;
+        v[SM_NP] = nP;
+        v[SM_NL] = nL;
+        v[SM_NBLK] = nBlk;
+        v[SM_NPAIR] = nPair;
+        v[SM_NPE] = nPe;
+        v[SM_NLP] = nLp;
+        v[SM_MAXPE] = maxPe;
+        v[SM_MAXLE] = maxLe;
+        v[SM_MAXBLK] = maxBlk;
+        v[SM_ERR] = err;
+        v[SM_FALLBACK] = fallback;
+        v[SM_SEQ] = A.seq;
+        for (int k = 0; k < SM_SEQ; k++) {
+            A.sc[k] = v[k];
+            A.hSc[k] = v[k];
+        }
+        __threadfence_system();
+        A.hSc[SM_SEQ] = A.seq;
+    }
+#undef SM_TS
+}
 }  // namespace
 
 GpuStructBuilder::~GpuStructBuilder() {
     for (auto& p : p_)
         if (p) (void)hipFree(p);
     if (hSc_) (void)hipHostFree(hSc_);
+    if (hSig_) (void)hipHostFree((void*)hSig_);
 }
 
 void* GpuStructBuilder::buf(int slot, size_t bytes) {
@@ -513,6 +1069,7 @@ int GpuStructBuilder::build(int level, int nkf, int npt, int ne, const EdgeDev* 
     info->maxBlk = hSc_[C_MAXBLK];
     info->nEglob = comm ? hSc_[C_NEG] : nE;
     info->nLglob = comm ? hSc_[C_NLG] : nL;
+    info->posDone = 0;
     st->nE = nE;
     st->nP = nP;
     st->nL = nL;
@@ -549,7 +1106,135 @@ int GpuStructBuilder::build(int level, int nkf, int npt, int ne, const EdgeDev* 
     return 0;
 }
 
+bool small_inputs_fit(int nkf, int npt, int ne) {
+    return nkf <= kSmMaxKf && npt <= kSmMaxPt && ne <= kSmMaxE;
+}
+bool GpuStructBuilder::small_fits(int nkf, int npt, int ne, int nFreeKf) {
+    return small_inputs_fit(nkf, npt, ne) && nFreeKf <= kSmMaxP;
+}
+
+int GpuStructBuilder::build_small(int level, int nkf, int npt, int ne, const int32_t* dKp, const int32_t* dPtOrd,
+                                  const uint8_t* dLevel, const uint8_t* dKfFixed, const int32_t* dKfId, int32_t* pePos,
+                                  hipStream_t s, BaStructDev* st, GpuStructInfo* info) {
+    if (!small_inputs_fit(nkf, npt, ne)) return 1;
+    if (!hSig_) {
+        if (hipHostMalloc((void**)&hSig_, sizeof(int) * 64, hipHostMallocCoherent) != hipSuccess) return -2;
+        std::memset((void*)hSig_, 0, sizeof(int) * 64);
+    }
+    const int nE0 = std::max(ne, 1);
+    SmallArgs A{};
+    A.level = level;
+    A.nkf = nkf;
+    A.npt = npt;
+    A.ne = ne;
+    A.seq = ++sigSeq_;
+    A.kp = dKp;
+    A.ptOrd = dPtOrd;
+    A.lv = dLevel;
+    A.kfFixed = dKfFixed;
+    A.kfId = dKfId;
+    // the slots of the multi-launch builder (download() and the engine read the same pointers);
+    // the Schur terms are at most kSmMaxP + 1 choose 2 per landmark, i.e. 12 per free-pose edge
+    GS_PTR(int, sc, S_SC, 64);
+    GS_PTR(int, aE, S_AE, nE0);
+    GS_PTR(int, ePose, S_EPOSE, nE0);
+    GS_PTR(int, eLand, S_ELAND, nE0);
+    GS_PTR(int, poseKf, S_POSEKF, nkf + 1);
+    GS_PTR(int, landPt, S_LANDPT, npt + 1);
+    GS_PTR(int, peStart, S_PESTART, nkf + 1);
+    GS_PTR(int, peList, S_PELIST, nE0);
+    GS_PTR(int, leStart, S_LESTART, npt + 1);
+    GS_PTR(int, leList, S_LELIST, nE0);
+    GS_PTR(int, lpStart, S_LPSTART, npt + 1);
+    GS_PTR(int, lpList, S_LPLIST, nE0);
+    GS_PTR(int, blkI, S_BLKI, kSmTri + 1);
+    GS_PTR(int, blkJ, S_BLKJ, kSmTri + 1);
+    GS_PTR(int, bStart, S_BSTART, kSmTri + 1);
+    GS_PTR(int, pA, S_PA, (size_t)(kSmMaxP + 1) / 2 * nE0 + 1);
+    GS_PTR(int, pB, S_PB, (size_t)(kSmMaxP + 1) / 2 * nE0 + 1);
+    A.aE = aE; A.ePose = ePose; A.eLand = eLand; A.poseKf = poseKf; A.landPt = landPt; A.peStart = peStart;
+    A.peList = peList; A.leStart = leStart; A.leList = leList; A.lpStart = lpStart; A.lpList = lpList; A.blkI = blkI;
+    A.blkJ = blkJ; A.blkStart = bStart; A.pairA = pA; A.pairB = pB; A.pePos = pePos; A.sc = sc;
+    A.hSc = hSig_;
+    static const bool say = getenv("ORBGPU_BA_TIMES") != nullptr;
+    A.ts = say ? reinterpret_cast<volatile long long*>(hSig_ + 32) : nullptr;
+    hipLaunchKernelGGL(k_gs_small, dim3(1), dim3(kSmT), 0, s, A);
+    GS_CHECK(hipGetLastError());
+    // the counts arrive in pinned memory behind the lists: spin on the sequence word (a stream
+    // sync wakes tens of us late); past 50 ms, a stream sync
+    volatile int* w = hSig_ + SM_SEQ;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 1; *w != A.seq; spin++) {
+        if ((spin & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+            GS_CHECK(hipStreamSynchronize(s));
+            if (*w != A.seq) return -2;
+            break;
+        }
+        __builtin_ia32_pause();
+    }
+    const hipError_t q = hipStreamQuery(s);   // a sticky error of the drained work
+    if (q != hipSuccess && q != hipErrorNotReady) return -2;
+    int v[SM_N];
+    for (int k = 0; k < SM_SEQ; k++) v[k] = hSig_[k];
+    if (say) {
+        const volatile long long* t = reinterpret_cast<const volatile long long*>(hSig_ + 32);
+        fprintf(stderr, "[ba]     one-workgroup lists (us): edges %.1f  poses %.1f  points %.1f  -- %.1f  "
+                "counts %.1f  landmark lists %.1f  pose lists %.1f  Schur %.1f  (total %.1f)\n",
+                (t[1] - t[0]) * 0.01, (t[2] - t[1]) * 0.01, (t[3] - t[2]) * 0.01, (t[4] - t[3]) * 0.01,
+                (t[5] - t[4]) * 0.01, (t[6] - t[5]) * 0.01, (t[7] - t[6]) * 0.01, (t[8] - t[7]) * 0.01,
+                (t[8] - t[0]) * 0.01);
+    }
+    if (v[SM_FALLBACK]) return 1;
+    if (v[SM_ERR]) {
+        info->err = v[SM_ERR];
+        return -1;
+    }
+    const int nE = v[SM_NE], nP = v[SM_NP], nL = v[SM_NL], nBlk = v[SM_NBLK], nPair = v[SM_NPAIR];
+    info->nE = nE;
+    info->nP = nP;
+    info->nL = nL;
+    info->nBlk = nBlk;
+    info->nPair = nPair;
+    info->nLp = v[SM_NLP];
+    info->nPe = v[SM_NPE];
+    info->nLe = nE;
+    info->err = 0;
+    info->maxPe = v[SM_MAXPE];
+    info->maxLe = v[SM_MAXLE];
+    info->maxBlk = v[SM_MAXBLK];
+    info->nEglob = nE;
+    info->nLglob = nL;
+    info->posDone = pePos ? 1 : 0;
+    st->nE = nE;
+    st->nP = nP;
+    st->nL = nL;
+    st->nBlk = nBlk;
+    st->aE = aE;
+    st->ePose = ePose;
+    st->eLand = eLand;
+    st->poseKf = poseKf;
+    st->landPt = landPt;
+    st->peStart = peStart;
+    st->peList = peList;
+    st->leStart = leStart;
+    st->leList = leList;
+    st->lpStart = lpStart;
+    st->lpList = lpList;
+    st->blkI = blkI;
+    st->blkJ = blkJ;
+    st->blkStart = bStart;
+    st->pairA = pA;
+    st->pairB = pB;
+    last_ = *st;
+    nkf_ = nkf;
+    nP_ = nP;
+    nPair_ = nPair;
+    nOff_ = -1;   // no sorted block keys behind this build (offkeys() refuses)
+    return 0;
+}
+
 int GpuStructBuilder::offkeys(std::vector<int64_t>* out, hipStream_t s) {
+    if (nOff_ < 0) return -2;   // the one-workgroup build keeps no block keys (dense systems only)
     out->assign(nOff_, 0);
     if (!nOff_) return 0;
     // the sorted block keys at the off-diagonal segment heads, compacted (ascending (i1, i2))
@@ -606,7 +1291,7 @@ int GpuStructBuilder::download(const GpuStructInfo& I, std::vector<int32_t>* out
 // ---------------------------------------------------------------- unit entry (parity tests)
 namespace orbgpu {
 // Both builders on one level of a problem given as plain arrays; out = [nE nP nL nBlk nPair nPe nLe
-// nLp | the 16 lists in download() order].  gpu = 0: the host restatement (ba_struct.cpp).
+// nLp | the 16 lists in download() order].  gpu = 0: the host restatement (ba_struct.cpp), 1 build(), 2 build_small().
 int debug_struct_all(int nkf, int npt, int ne, const int32_t* eKf, const int32_t* ePt, const uint8_t* lv,
                      const uint8_t* kfFixed, const int32_t* kfId, const int32_t* ptId, int level, int gpu,
                      std::vector<int32_t>* out) {
@@ -654,7 +1339,24 @@ int debug_struct_all(int nkf, int npt, int ne, const int32_t* eKf, const int32_t
         GpuStructBuilder b;
         BaStructDev st{};
         GpuStructInfo info{};
-        rc = b.build(level, nkf, npt, ne, dE, dLv, dFx, dKid, dPid, nullptr, s, &st, &info);
+        rc = 1;   // gpu = 2: the one-workgroup builder (the multi-launch one outside its limits)
+        if (gpu == 2 && small_inputs_fit(nkf, npt, ne)) {
+            // its inputs as the engine's upload makes them: the compact edge keys, the point order
+            std::vector<int32_t> kp(std::max(ne, 1)), ord;
+            for (int i = 0; i < ne; i++) kp[i] = (eKf[i] << 13) | ePt[i];
+            ba_order_by_id(npt, ptId, &ord);
+            ord.resize(std::max(npt, 1));
+            int32_t *dKp = nullptr, *dOrd = nullptr;
+            if (hipMalloc(&dKp, 4 * kp.size()) != hipSuccess || hipMalloc(&dOrd, 4 * ord.size()) != hipSuccess ||
+                hipMemcpy(dKp, kp.data(), 4 * kp.size(), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dOrd, ord.data(), 4 * ord.size(), hipMemcpyHostToDevice) != hipSuccess)
+                rc = -2;
+            else
+                rc = b.build_small(level, nkf, npt, ne, dKp, dOrd, dLv, dFx, dKid, nullptr, s, &st, &info);
+            (void)hipFree(dKp);
+            (void)hipFree(dOrd);
+        }
+        if (rc == 1) rc = b.build(level, nkf, npt, ne, dE, dLv, dFx, dKid, dPid, nullptr, s, &st, &info);
         std::vector<int32_t> lists;
         if (!rc) rc = b.download(info, &lists, s);
         if (!rc) {

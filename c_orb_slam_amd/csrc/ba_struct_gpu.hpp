@@ -19,6 +19,7 @@ struct GpuStructInfo {
     int err;                    // bit 0: a landmark with two edges to one pose
     int maxPe, maxLe, maxBlk;   // longest per-pose / per-landmark / per-block list
     int nEglob, nLglob;         // over the shards (comm); == nE, nL otherwise
+    int posDone;                // build_small with pePos: pePos written, pairs are pose-list positions
 };
 
 class GpuStructBuilder {
@@ -31,6 +32,18 @@ public:
     int build(int level, int nkf, int npt, int ne, const EdgeDev* dE, const uint8_t* dLevel, const uint8_t* dKfFixed,
               const int32_t* dKfId, const int32_t* dPtId, Comm* comm, hipStream_t s, BaStructDev* st,
               GpuStructInfo* info, std::vector<int32_t>* blkIJ = nullptr);
+    // The same lists from ONE workgroup (local-BA sizes: <= 1,024 keyframes, <= 8,192 points,
+    // <= 16,384 edges, <= 23 free active poses, <= 256 edges per landmark), the counts polled from
+    // pinned memory.  pePos (optional, >= ne entries): the pose-list position of every active edge
+    // (-1 on fixed keyframes) written too, and pairA / pairB as pose-list positions.  Returns 0,
+    // 1 (outside the limits: nothing usable, run build()), -1 (duplicate edge) or -2 (HIP).
+    // Unsharded only.
+    // Inputs: dKp[e] = (keyframe << 13) | point per edge, dPtOrd = every point by (mnId, index)
+    // (ba_order_by_id).
+    int build_small(int level, int nkf, int npt, int ne, const int32_t* dKp, const int32_t* dPtOrd,
+                    const uint8_t* dLevel, const uint8_t* dKfFixed, const int32_t* dKfId, int32_t* pePos, hipStream_t s,
+                    BaStructDev* st, GpuStructInfo* info);
+    static bool small_fits(int nkf, int npt, int ne, int nFreeKf);
     // after build(): the off-diagonal Schur blocks as i1 * nP + i2, ascending (the pose graph)
     int offkeys(std::vector<int64_t>* out, hipStream_t s);
     // the lists of the last build, back on the host, in one buffer:
@@ -44,12 +57,18 @@ private:
     void* p_[kSlots] = {};
     size_t cap_[kSlots] = {};
     int* hSc_ = nullptr;   // pinned scalar mirror
+    volatile int* hSig_ = nullptr;   // pinned coherent: build_small's counts and sequence word
+    int sigSeq_ = 0;
     BaStructDev last_{};
     int nkf_ = 0, nP_ = 0, nPair_ = 0, nOff_ = 0;
 };
 
+// build_small's size limits without the pose count (<= 1,024 keyframes, <= 8,192 points, <= 16,384 edges)
+bool small_inputs_fit(int nkf, int npt, int ne);
+
 // both builders on one level (unit entry orbgpu_unit_ba_struct_all): [nE nP nL nBlk nPair nPe nLe nLp |
-// the 16 lists]; gpu = 0: the host restatement.  0, -1 (duplicate edge) or -2 (HIP).
+// the 16 lists]; gpu = 0: the host restatement, 1: build(), 2: build_small() (build() outside
+// its limits).  0, -1 (duplicate edge) or -2 (HIP).
 int debug_struct_all(int nkf, int npt, int ne, const int32_t* eKf, const int32_t* ePt, const uint8_t* lv,
                      const uint8_t* kfFixed, const int32_t* kfId, const int32_t* ptId, int level, int gpu,
                      std::vector<int32_t>* out);

@@ -887,8 +887,9 @@ int orbgpu_unit_ldlt_factor(int n, const double* S, double* out);
 int orbgpu_unit_ba_struct(int nkf, int npt, int ne, const int32_t* edge_kf, const int32_t* edge_pt,
                           const uint8_t* edge_level, const uint8_t* kf_fixed, const int32_t* kf_id,
                           const int32_t* pt_id, int level, int32_t* out, long long cap);
-/* The same structure from both builders: gpu = 1 the device builder the BA runs by default
- * (ba_struct_gpu.hip), gpu = 0 the host restatement.  out = [nE nP nL nBlk nPair nPe nLe nLp |
+/* The same structure from the builders: gpu = 1 the multi-launch device builder (ba_struct_gpu.hip),
+ * gpu = 2 the one-workgroup device builder local-BA sizes run (the multi-launch one outside its
+ * limits), gpu = 0 the host restatement.  out = [nE nP nL nBlk nPair nPe nLe nLp |
  * aE | ePose | eLand | poseKf | landPt | peStart | peList | leStart | leList | lpStart | lpList |
  * blkI | blkJ | blkStart | pairA | pairB]; *n_out = its length (ORB_E_CAPACITY beyond cap). */
 int orbgpu_unit_ba_struct_all(int nkf, int npt, int ne, const int32_t* edge_kf, const int32_t* edge_pt,

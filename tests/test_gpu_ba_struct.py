@@ -23,7 +23,7 @@ def _both(pr, fixed, level_mask=None, level=0):
     kid = np.ascontiguousarray(pr["kf_id"], np.int32)
     pid = np.ascontiguousarray(pr["pt_id"], np.int32)
     outs = []
-    for gpu in (0, 1):
+    for gpu in (0, 1, 2):   # host, multi-launch device builder, one-workgroup device builder
         cap = 64 * ne + 8 * (nkf + npt) + 1024
         while True:
             out = np.zeros(cap, np.int32)
@@ -36,7 +36,8 @@ def _both(pr, fixed, level_mask=None, level=0):
             assert rc == 0, (gpu, rc)
             outs.append(out[:n.value].copy())
             break
-    return outs
+    assert np.array_equal(outs[1], outs[2])
+    return outs[:2]
 
 
 def _local_fixed(pr):
@@ -94,9 +95,38 @@ def test_device_structure_rejects_duplicate_edges(gpu):
     pid = np.ascontiguousarray(pr["pt_id"], np.int32)
     out = np.zeros(64 * ne + 4096, np.int32)
     n = C.c_longlong()
-    for gpu_ in (0, 1):
+    for gpu_ in (0, 1, 2):
         if fx[ek[0]]:
             pytest.skip("the duplicated edge hangs off a fixed keyframe")
         rc = lib().orbgpu_unit_ba_struct_all(len(kid), len(pid), ne, ptr(ek), ptr(ep), ptr(lv), ptr(fx), ptr(kid),
                                              ptr(pid), 0, gpu_, ptr(out), len(out), C.byref(n))
         assert rc == -1, (gpu_, rc)
+
+
+@pytest.mark.parametrize("case", ["no_active_edges", "max_free_poses", "over_free_poses", "long_landmark",
+                                  "descending_ids"])
+def test_small_structure_edge_cases(gpu, case):
+    """The one-workgroup builder (build_small, gpu = 2) at its limits: no active edge at the level,
+    23 free poses (its maximum) and 24 (the multi-launch builder takes over), a landmark seen by
+    every keyframe, point ids in descending order (the LDS bitonic sort) -- every list equal to
+    the host's (_both compares all three builders)."""
+    if case == "no_active_edges":
+        pr = ba_problem(3, n_local=6, n_fixed=3, n_pt=200)
+        h, g = _both(pr, _local_fixed(pr), np.zeros(len(pr["edge_pt"]), np.uint8), 1)
+        assert h[:8].tolist()[:4] == [0, 0, 0, 0]
+        return
+    if case in ("max_free_poses", "over_free_poses"):
+        nl = 24 if case == "max_free_poses" else 25   # kf_id 0 is fixed too: 23 / 24 free poses
+        pr = ba_problem(11, n_local=nl, n_fixed=4, n_pt=900, obs_range=(2, 12))
+    elif case == "long_landmark":
+        pr = dict(ba_problem(12, n_local=14, n_fixed=8, n_pt=400))
+        nkf = len(pr["kf_id"])
+        seen = set(zip(pr["edge_kf"].tolist(), pr["edge_pt"].tolist()))
+        add = [k for k in range(nkf) if (k, 0) not in seen]
+        pr["edge_kf"] = np.concatenate([pr["edge_kf"], np.array(add, np.int32)])
+        pr["edge_pt"] = np.concatenate([pr["edge_pt"], np.zeros(len(add), np.int32)])
+    else:
+        pr = dict(ba_problem(13, n_local=10, n_fixed=5, n_pt=700))
+        pr["pt_id"] = (np.arange(len(pr["pt_id"]))[::-1] * 5 + 17).astype(np.int32)
+    h, g = _both(pr, _local_fixed(pr))
+    assert np.array_equal(h, g)
