@@ -3487,7 +3487,7 @@ bool BaEngine::dense_solver(int n) const {
 
 // Carve every device buffer of the problem out of one grow-only arena.
 struct UploadLayout {   // byte offsets in the staging span (all 8-byte aligned)
-    size_t oT, oX, oPt, oKf, oObs, oIs, oCam, oFx, oKid, oPid, oOrd, total;
+    size_t oT, oX, oPt, oKf, oObs, oIs, oCam, oFx, oKid, oPid, total;
 };
 static UploadLayout upload_layout(size_t ne, size_t nkf, size_t npt) {
     auto al8 = [](size_t b) { return (b + 7) & ~(size_t)7; };
@@ -3502,9 +3502,24 @@ static UploadLayout upload_layout(size_t ne, size_t nkf, size_t npt) {
     L.oFx = L.oCam + al8(sizeof(float) * 5 * nkf);
     L.oKid = L.oFx + al8(nkf);
     L.oPid = L.oKid + al8(sizeof(int32_t) * nkf);
-    L.oOrd = L.oPid + al8(sizeof(int32_t) * npt);
-    L.total = L.oOrd + al8(sizeof(int32_t) * npt);
+    L.total = L.oPid + al8(sizeof(int32_t) * npt);
     return L;
+}
+// The one-workgroup structure builder's inputs, staged and copied as one block ahead of the rest
+// of the problem: per edge (keyframe << 13) | point, the points by (mnId, index), the keyframe ids
+// and fixed flags.
+struct SmallInLayout {
+    size_t oKp, oOrd, oKid, oFx, total;
+};
+static SmallInLayout small_in_layout(size_t ne, size_t nkf, size_t npt) {
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    SmallInLayout S;
+    S.oKp = 0;
+    S.oOrd = S.oKp + al(sizeof(int32_t) * ne);
+    S.oKid = S.oOrd + al(sizeof(int32_t) * npt);
+    S.oFx = S.oKid + al(sizeof(int32_t) * nkf);
+    S.total = S.oFx + al(nkf);
+    return S;
 }
 int BaEngine::carve(bool commit, size_t* total) {
     const size_t ne = (size_t)std::max(ne_, 1), nkf = (size_t)std::max(nkf_, 1), npt = (size_t)std::max(npt_, 1);
@@ -3553,8 +3568,15 @@ int BaEngine::carve(bool commit, size_t* total) {
     dTn_ = (Se3*)take(sizeof(Se3) * nkf);
     dXn_ = (double*)take(sizeof(double) * 3 * npt);
     dPtId_ = (int32_t*)take(sizeof(int32_t) * npt);
-    dKp_ = (int32_t*)take(sizeof(int32_t) * ne);
-    dPtOrd_ = (int32_t*)take(sizeof(int32_t) * npt);
+    {   // the one-workgroup structure builder's inputs, one block (small_in_layout)
+        const SmallInLayout S = small_in_layout(ne, nkf, npt);
+        char* b = (char*)take(S.total);
+        dKp_ = (int32_t*)(b + S.oKp);
+        dPtOrd_ = (int32_t*)(b + S.oOrd);
+        dSmKid_ = (int32_t*)(b + S.oKid);
+        dSmFx_ = (uint8_t*)(b + S.oFx);
+        dSmallIn_ = b;
+    }
     dScratch_ = (double*)take(sizeof(double) * scratchN_);
     tmpA0_ = (double*)take(sizeof(double) * tmpN);
     tmpA1_ = (double*)take(sizeof(double) * tmpN);
@@ -3587,7 +3609,6 @@ struct UploadArgs {
     EdgeDev* E;
     uint8_t *kfFixed, *level, *robustFlag;
     int32_t *kfId, *ptId;
-    int32_t *kp, *ptOrd;   // the one-workgroup structure builder's inputs (null: not built)
     double* err;
     unsigned* counter;
 };
@@ -3615,7 +3636,6 @@ __global__ void __launch_bounds__(256) k_unpack_upload(UploadArgs a) {
         e.delta = (double)(e.stereo ? a.thStereo : a.thMono);
         e.dsqr = e.delta * e.delta;
         a.E[i] = e;
-        if (a.kp) a.kp[i] = (e.kf << 13) | e.pt;
         a.level[i] = 0;
         a.robustFlag[i] = (uint8_t)a.robust;
         for (int k = 0; k < 3; k++) a.err[3 * i + k] = 0.0;
@@ -3627,7 +3647,6 @@ __global__ void __launch_bounds__(256) k_unpack_upload(UploadArgs a) {
         a.kfId[i] = ((const int32_t*)(a.src + L.oKid))[i];
     }
     if (i < a.npt) a.ptId[i] = ((const int32_t*)(a.src + L.oPid))[i];
-    if (a.ptOrd && i < a.npt) a.ptOrd[i] = ((const int32_t*)(a.src + L.oOrd))[i];
     if (i < 16) a.counter[i] = 0;
 }
 
@@ -3662,8 +3681,15 @@ int BaEngine::upload_problem(const ba_problem* P) {
     // poses, points, compact edges and vertex data written straight into the pinned staging block
     // (no intermediate host copy): one H2D copy, unpacked by k_unpack_upload
     const UploadLayout UL = upload_layout(ne_, nkf_, npt_);
-    if (int e = stage_reserve(UL.total + 64)) return e;
+    // the one-workgroup structure builder reads compact edge keys and the points' id order: staged
+    // behind the problem and copied first (build_structure queues the problem's copy behind the
+    // level-0 structure kernel)
+    smallUp_ = small_struct();
+    const SmallInLayout SL = small_in_layout(ne_, nkf_, npt_);
+    const size_t oSm = (UL.total + 255) & ~(size_t)255;
+    if (int e = stage_reserve((smallUp_ ? oSm + SL.total : UL.total) + 64)) return e;
     char* st = (char*)hStage_;
+    int32_t* kpS = smallUp_ ? reinterpret_cast<int32_t*>(st + oSm + SL.oKp) : nullptr;
     Se3* Ts = reinterpret_cast<Se3*>(st + UL.oT);
     double* Xs = reinterpret_cast<double*>(st + UL.oX);
     std::memcpy(st + UL.oFx, kfFixed_.data(), nkf_);
@@ -3686,22 +3712,24 @@ int BaEngine::upload_problem(const ba_problem* P) {
             uint8_t* f = &kfEdge[P->edge_kf[i]];
             if (!__atomic_load_n(f, __ATOMIC_RELAXED)) __atomic_store_n(f, (uint8_t)1, __ATOMIC_RELAXED);
         }
+        if (kpS)
+            for (int i = a; i < b; i++) kpS[i] = (P->edge_kf[i] << 13) | P->edge_pt[i];
         std::memcpy(st + UL.oPt + sizeof(int32_t) * a, P->edge_pt + a, sizeof(int32_t) * (b - a));
         std::memcpy(st + UL.oKf + sizeof(int32_t) * a, P->edge_kf + a, sizeof(int32_t) * (b - a));
         std::memcpy(st + UL.oObs + sizeof(float) * 3 * (size_t)a, P->edge_obs + 3 * (size_t)a, sizeof(float) * 3 * (b - a));
         std::memcpy(st + UL.oIs + sizeof(float) * a, P->edge_inv_sigma2 + a, sizeof(float) * (b - a));
     });
     level_.assign(ne_, 0);
-    // the one-workgroup structure builder reads compact edge keys and the points' id order
-    smallUp_ = small_struct();
+    hipStream_t s = stream_;
     if (smallUp_) {
         std::vector<int32_t> ord;
         ba_order_by_id(npt_, P->pt_id, &ord);
-        std::memcpy(st + UL.oOrd, ord.data(), sizeof(int32_t) * npt_);
+        std::memcpy(st + oSm + SL.oOrd, ord.data(), sizeof(int32_t) * npt_);
+        std::memcpy(st + oSm + SL.oKid, P->kf_id, sizeof(int32_t) * nkf_);
+        std::memcpy(st + oSm + SL.oFx, kfFixed_.data(), nkf_);
+        ORB_HIP_CHECK(hipMemcpyAsync(dSmallIn_, st + oSm, SL.total, hipMemcpyHostToDevice, s));
     }
-    hipStream_t s = stream_;
     char* dst = (char*)dTerms_;   // free until the first linearisation
-    ORB_HIP_CHECK(hipMemcpyAsync(dst, st, UL.total, hipMemcpyHostToDevice, s));
     UploadArgs ua;
     ua.src = dst;
     ua.L = UL;
@@ -3720,14 +3748,28 @@ int BaEngine::upload_problem(const ba_problem* P) {
     ua.robustFlag = dRobust_;
     ua.kfId = dKfId_;
     ua.ptId = dPtId_;
-    ua.kp = smallUp_ ? dKp_ : nullptr;
-    ua.ptOrd = smallUp_ ? dPtOrd_ : nullptr;
     ua.err = dErr_;
     ua.counter = dCounter_;
-    const long long nthr = std::max<long long>({(long long)ne_, 8LL * nkf_, 3LL * npt_, 16LL});
-    hipLaunchKernelGGL(k_unpack_upload, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, ua);
+    static_assert(std::is_trivially_copyable<UploadArgs>::value, "deferred upload");
+    deferArgs_.resize(sizeof(UploadArgs));
+    std::memcpy(deferArgs_.data(), &ua, sizeof(UploadArgs));
+    deferBytes_ = UL.total;
+    deferredUpload_ = true;
     // no wait here: the host builds the structure while the copies run; the next user of the
-    // staging block (stage_reserve) waits for them
+    // staging block (stage_reserve) waits for them.  With the one-workgroup builder the problem's
+    // copy and unpack are queued behind the level-0 structure kernel (build_structure)
+    if (!smallUp_) return issue_upload();
+    return 0;
+}
+int BaEngine::issue_upload() {
+    if (!deferredUpload_) return 0;
+    deferredUpload_ = false;
+    UploadArgs ua;
+    std::memcpy(&ua, deferArgs_.data(), sizeof(UploadArgs));
+    ORB_HIP_CHECK(hipMemcpyAsync((void*)ua.src, hStage_, deferBytes_, hipMemcpyHostToDevice, stream_));
+    const long long nthr = std::max<long long>({(long long)ne_, 8LL * nkf_, 3LL * npt_, 16LL});
+    hipLaunchKernelGGL(k_unpack_upload, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, stream_, ua);
+    ORB_HIP_CHECK(hipGetLastError());
     uploadPending_ = true;
     return 0;
 }
@@ -3985,9 +4027,14 @@ int BaEngine::build_structure(int level) {
         // workgroup at local-BA sizes (with the pose-list positions), else by the multi-launch builder
         GpuStructInfo info{};
         int r = 1;
-        if (smallUp_ && small_struct())
-            r = gs_.build_small(level, nkf_, npt_, ne_, dKp_, dPtOrd_, dLevel_, dKfFixed_, dKfId_, dPePos_, stream_, &st_,
-                                &info);
+        if (smallUp_ && small_struct()) {
+            // the first build of the call reads no levels (every edge at level 0) and queues the
+            // problem's copy and unpack behind its kernel
+            const bool first = deferredUpload_;
+            r = gs_.build_small(level, nkf_, npt_, ne_, dKp_, dPtOrd_, first ? nullptr : dLevel_, dSmFx_, dSmKid_, dPePos_,
+                                stream_, &st_, &info, [this] { return issue_upload(); });
+        }
+        if (int e = issue_upload()) return e;   // (not issued yet: the multi-launch builder reads the records)
         if (r == 1)
             r = gs_.build(level, nkf_, npt_, ne_, dE_, dLevel_, dKfFixed_, dKfId_, dPtId_, comm_, stream_, &st_, &info,
                           comm_ ? &blkIJ : nullptr);
@@ -4964,6 +5011,7 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
     double t_struct = 0;
     auto ts = clk::now();
     if (int e = build_structure(0)) return e;
+    if (int e = issue_upload()) return e;   // (already queued by every build path)
     t_struct += std::chrono::duration<double, std::milli>(clk::now() - ts).count();
     if (comm_ && (stopRed_ || nEglob_ == 0)) {  // Optimizer.cc:655-657 (and no edges at all)
         R->aborted = 1;

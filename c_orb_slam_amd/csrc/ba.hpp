@@ -89,8 +89,17 @@ private:
     // unsharded), else the host lists below the device builder's edge threshold
     bool small_struct() const;
     bool host_lists() const;
-    bool smallUp_ = false;                          // this call's upload wrote dKp_ / dPtOrd_
+    bool smallUp_ = false;                          // this call's upload staged the builder's inputs
     int32_t *dKp_ = nullptr, *dPtOrd_ = nullptr;    // (keyframe << 13) | point per edge; points by id
+    int32_t* dSmKid_ = nullptr;                     // keyframe ids and fixed flags (same block)
+    uint8_t* dSmFx_ = nullptr;
+    char* dSmallIn_ = nullptr;
+    // the problem's H2D copy + unpack, prepared by upload_problem and queued by issue_upload
+    // (right away, or behind the level-0 one-workgroup structure kernel)
+    bool deferredUpload_ = false;
+    std::vector<char> deferArgs_;
+    size_t deferBytes_ = 0;
+    int issue_upload();
     double* dLmStage_ = nullptr;   // the system's all-reduce staging (Hpp, b_p, chi2) of enqueue_lm_step_comm
     size_t lmStageCap_ = 0;
     int gate_edges(int final_check, uint8_t* erase);

@@ -302,8 +302,9 @@ struct Max {
 //   leList        LDS cursors, then each landmark's (short) segment sorted by edge position
 //   lpList        a landmark's free-pose edges placed by the rank of their pose in the landmark's
 //                 pose bitmask: pose order without a sort; a pose seen twice = duplicate edge
-//   peList        per wave a contiguous range of active edges, split by pose with ballots
-//                 (stable: edge order inside a pose), bases scanned pose-major over the waves
+//   peList        per wave a contiguous range of active edges (counted per pose in the edge
+//                 pass), split by pose with ballots (stable: edge order inside a pose), bases
+//                 scanned pose-major over the waves
 //   Schur blocks  a landmark's terms are the pose pairs (i <= j) of its bitmask; an off-diagonal
 //                 block's first use is its first landmark, then (i, j) -- the host walk's order
 //                 (landmark, u, v) because a landmark's lp entries are in pose order; each block's
@@ -337,7 +338,7 @@ struct SmallArgs {
     int level, nkf, npt, ne, seq;
     const int32_t* kp;        // per edge (keyframe << 13) | point (k_unpack_upload)
     const int32_t* ptOrd;     // the points by (mnId, index) (host, once per call)
-    const uint8_t* lv;
+    const uint8_t* lv;        // null: every edge at `level` (the first build of a call)
     const uint8_t* kfFixed;
     const int32_t* kfId;
     int *aE, *ePose, *eLand, *poseKf, *landPt, *peStart, *peList, *leStart, *leList, *lpStart, *lpList, *blkI, *blkJ,
@@ -441,7 +442,7 @@ __global__ void __launch_bounds__(kSmT) k_gs_small(SmallArgs A) {
     if (A.ts && tid == 0) A.ts[k] = (long long)wall_clock64()
     SM_TS(0);
     int nE = 0, nP = 0, nL = 0, nBlk = 0, nPair = 0, nPe = 0, nLp = 0, maxPe = 0, maxLe = 0, maxBlk = 0, err = 0,
-        fallback = 0;
+        fallback = 0, pw = 1;
 
     for (int i = tid; i < npt; i += kSmT) ptAct[i] = 0;
     for (int i = tid; i < nkf; i += kSmT) {
@@ -449,6 +450,7 @@ __global__ void __launch_bounds__(kSmT) k_gs_small(SmallArgs A) {
         sPoseIdx[i] = -1;
     }
     for (int i = tid; i <= npt; i += kSmT) cnt[i] = 0;
+    for (int i = tid; i < kSmW * kSmMaxP; i += kSmT) sPe[i] = 0;
     // 1. initializeOptimization(level): this thread's chunk of kSmPer edges [c0, c1) as four
     // 16-byte key loads and one 16-byte level load (the compact per-edge keys, not the records)
     const int c0 = min(ne, tid * kSmPer), c1 = min(ne, c0 + kSmPer);
@@ -456,7 +458,7 @@ __global__ void __launch_bounds__(kSmT) k_gs_small(SmallArgs A) {
     uint32_t act = 0;
     if (c1 - c0 == kSmPer) {
         const int4* k4 = reinterpret_cast<const int4*>(A.kp + c0);
-        const uint4 l4 = *reinterpret_cast<const uint4*>(A.lv + c0);
+        const uint4 l4 = A.lv ? *reinterpret_cast<const uint4*>(A.lv + c0) : make_uint4(0, 0, 0, 0);
         const uint32_t lw[4] = {l4.x, l4.y, l4.z, l4.w};
 #pragma unroll
         for (int v = 0; v < 4; v++) {
@@ -473,7 +475,7 @@ __global__ void __launch_bounds__(kSmT) k_gs_small(SmallArgs A) {
         for (int k = 0; k < kSmPer; k++) {
             const int i = min(c0 + k, c1 - 1);
             kp[k] = A.kp[i];
-            act |= (c0 + k < c1 && A.lv[i] == A.level) ? 1u << k : 0u;
+            act |= (c0 + k < c1 && (A.lv ? A.lv[i] : 0) == A.level) ? 1u << k : 0u;
         }
     }
     __syncthreads();   // (the flags are cleared)
@@ -548,6 +550,7 @@ __global__ void __launch_bounds__(kSmT) k_gs_small(SmallArgs A) {
     SM_TS(3);
     SM_TS(4);
     // 3. per active edge: its pose / landmark index; per landmark one packed counter
+    pw = max(1, (nE + kSmW - 1) / kSmW);   // the pose lists' per-wave ranges of active edges
     {
         int q = aBase;
 #pragma unroll
@@ -558,6 +561,7 @@ __global__ void __launch_bounds__(kSmT) k_gs_small(SmallArgs A) {
                 A.ePose[q] = p;
                 A.eLand[q] = l;
                 atomicAdd(&cnt[l], p >= 0 ? 0x10001 : 1);
+                if (p >= 0) atomicAdd(&sPe[(q / pw) * kSmMaxP + p], 1);   // (order-free counts)
                 kp[k] = (l << 5) | (p + 1);
                 q++;
             }
@@ -632,16 +636,9 @@ __global__ void __launch_bounds__(kSmT) k_gs_small(SmallArgs A) {
     }
     SM_TS(6);
     {   // 4. the pose lists: per wave a contiguous range of active edges, split by pose
-        const int pw = (nE + kSmW - 1) / kSmW, e0 = min(nE, wv * pw), e1 = min(nE, e0 + pw);
+        // (the per-wave, per-pose counts came from the edge pass)
+        const int e0 = min(nE, wv * pw), e1 = min(nE, e0 + pw);
         volatile int* const pe = sPe + wv * kSmMaxP;
-        for (int i = lane; i < kSmMaxP; i += 64) pe[i] = 0;
-        for (int b = e0; b < e1; b += 64) {
-            const int a = b + lane;
-            const int p = a < e1 ? ePose8[a] : -1;
-            const unsigned long long m = same_key(p, p >= 0, 5);
-            if (p >= 0 && (m & lanes_below()) == 0) pe[p] += __popcll(m);
-        }
-        __syncthreads();
         if (wv == 0) {   // per pose: its total, its start, the waves' bases in wave order
             int t = 0;
             if (lane < nP)
@@ -1115,7 +1112,8 @@ bool GpuStructBuilder::small_fits(int nkf, int npt, int ne, int nFreeKf) {
 
 int GpuStructBuilder::build_small(int level, int nkf, int npt, int ne, const int32_t* dKp, const int32_t* dPtOrd,
                                   const uint8_t* dLevel, const uint8_t* dKfFixed, const int32_t* dKfId, int32_t* pePos,
-                                  hipStream_t s, BaStructDev* st, GpuStructInfo* info) {
+                                  hipStream_t s, BaStructDev* st, GpuStructInfo* info,
+                                  const std::function<int()>& afterLaunch) {
     if (!small_inputs_fit(nkf, npt, ne)) return 1;
     if (!hSig_) {
         if (hipHostMalloc((void**)&hSig_, sizeof(int) * 64, hipHostMallocCoherent) != hipSuccess) return -2;
@@ -1160,6 +1158,8 @@ int GpuStructBuilder::build_small(int level, int nkf, int npt, int ne, const int
     A.ts = say ? reinterpret_cast<volatile long long*>(hSig_ + 32) : nullptr;
     hipLaunchKernelGGL(k_gs_small, dim3(1), dim3(kSmT), 0, s, A);
     GS_CHECK(hipGetLastError());
+    if (afterLaunch)   // work the caller queues behind the kernel while the host waits for its counts
+        if (int e = afterLaunch()) return e;
     // the counts arrive in pinned memory behind the lists: spin on the sequence word (a stream
     // sync wakes tens of us late); past 50 ms, a stream sync
     volatile int* w = hSig_ + SM_SEQ;

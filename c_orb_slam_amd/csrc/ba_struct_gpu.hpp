@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "ba_types.hpp"
@@ -39,10 +40,11 @@ public:
     // 1 (outside the limits: nothing usable, run build()), -1 (duplicate edge) or -2 (HIP).
     // Unsharded only.
     // Inputs: dKp[e] = (keyframe << 13) | point per edge, dPtOrd = every point by (mnId, index)
-    // (ba_order_by_id).
+    // (ba_order_by_id); dLevel null = every edge at `level`.  afterLaunch (optional) runs right
+    // after the kernel is queued, before the wait for its counts.
     int build_small(int level, int nkf, int npt, int ne, const int32_t* dKp, const int32_t* dPtOrd,
                     const uint8_t* dLevel, const uint8_t* dKfFixed, const int32_t* dKfId, int32_t* pePos, hipStream_t s,
-                    BaStructDev* st, GpuStructInfo* info);
+                    BaStructDev* st, GpuStructInfo* info, const std::function<int()>& afterLaunch = nullptr);
     static bool small_fits(int nkf, int npt, int ne, int nFreeKf);
     // after build(): the off-diagonal Schur blocks as i1 * nP + i2, ascending (the pose graph)
     int offkeys(std::vector<int64_t>* out, hipStream_t s);
