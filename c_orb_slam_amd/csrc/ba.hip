@@ -3508,6 +3508,7 @@ static UploadLayout upload_layout(size_t ne, size_t nkf, size_t npt) {
 // The one-workgroup structure builder's inputs, staged and copied as one block ahead of the rest
 // of the problem: per edge (keyframe << 13) | point, the points by (mnId, index), the keyframe ids
 // and fixed flags.
+static std::atomic<int> g_ba_runs{0};   // BaEngine::run calls in flight in this process
 struct SmallInLayout {
     size_t oKp, oOrd, oKid, oFx, total;
 };
@@ -3684,7 +3685,10 @@ int BaEngine::upload_problem(const ba_problem* P) {
     // the one-workgroup structure builder reads compact edge keys and the points' id order: staged
     // behind the problem and copied first (build_structure queues the problem's copy behind the
     // level-0 structure kernel)
-    smallUp_ = small_struct();
+    // (only while no other BA call runs in this process: with concurrent calls the host lists of
+    // one overlap the others' GPU work -- 16 streams: 25.0-26.2 k vs 26.9-27.8 k iter/s with the
+    // one-workgroup kernels, profiles/r06st_lba_streams_ab.txt)
+    smallUp_ = small_struct() && g_ba_runs.load(std::memory_order_relaxed) <= 1;
     const SmallInLayout SL = small_in_layout(ne_, nkf_, npt_);
     const size_t oSm = (UL.total + 255) & ~(size_t)255;
     if (int e = stage_reserve((smallUp_ ? oSm + SL.total : UL.total) + 64)) return e;
@@ -3819,8 +3823,8 @@ bool BaEngine::small_struct() const {
     for (int k = 0; k < nkf_; k++) nFree += kfFixed_[k] ? 0 : 1;
     return GpuStructBuilder::small_fits(nkf_, npt_, ne_, nFree);
 }
-bool BaEngine::host_lists() const {
-    return !small_struct() && struct_host(ne_, comm_ && comm_->size() > 1);
+bool BaEngine::host_lists() const {   // (smallUp_: this call's choice, made at upload)
+    return !smallUp_ && struct_host(ne_, comm_ && comm_->size() > 1);
 }
 int debug_set_struct_gpu_min_edges(int v) {
     if (v < 0) return -1;
@@ -4027,7 +4031,7 @@ int BaEngine::build_structure(int level) {
         // workgroup at local-BA sizes (with the pose-list positions), else by the multi-launch builder
         GpuStructInfo info{};
         int r = 1;
-        if (smallUp_ && small_struct()) {
+        if (smallUp_) {
             // the first build of the call reads no levels (every edge at level 0) and queues the
             // problem's copy and unpack behind its kernel
             const bool first = deferredUpload_;
@@ -4983,6 +4987,11 @@ int BaEngine::run(const ba_problem* P, const volatile bool* stop, ba_result* R, 
             e->ePt_ = e->eKf_ = nullptr;
         }
     } edgeRefs{this};
+    struct RunCount {
+        RunCount() { g_ba_runs.fetch_add(1, std::memory_order_relaxed); }
+        ~RunCount() { g_ba_runs.fetch_sub(1, std::memory_order_relaxed); }
+    } runCount;
+    smallUp_ = false;
     trace_ = BaTrace{};
     // a one-rank group is the unsharded call: every exchange would be the identity, so none is
     // made (no collective, no host round trip per structure and stop decision)
